@@ -1,0 +1,152 @@
+"""ctypes bindings for the CPU parity checkers (TEST INFRASTRUCTURE ONLY).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this
+module.  It wraps two libraries built by oracle/Makefile:
+
+* ``liboracle.so`` -- this repo's plain-C restatement (``tdec_oracle.c``)
+* ``_ref/libsrsref.so`` -- the reference decoder compiled from /root/reference
+  (present wherever it was built; it travels to the GPU box as a build artefact)
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ORACLE_SO = os.path.join(HERE, "liboracle.so")
+REF_SO = os.path.join(HERE, "_ref", "libsrsref.so")
+
+CB_SIZES = (
+    [40 + 8 * i for i in range(60)]
+    + [528 + 16 * i for i in range(32)]
+    + [1056 + 32 * i for i in range(32)]
+    + [2112 + 64 * i for i in range(64)]
+)
+assert len(CB_SIZES) == 188 and CB_SIZES[-1] == 6144
+
+_i16p = ctypes.POINTER(ctypes.c_int16)
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_u16p = ctypes.POINTER(ctypes.c_uint16)
+
+
+def _ptr(a, t):
+    return a.ctypes.data_as(t)
+
+
+def nof_subblocks(K):
+    """AUTO 16-bit dispatch of turbodecoder.c:381-393 (AVX2 build)."""
+    if K % 16 == 0 and K > 800:
+        return 16
+    if K % 8 == 0 and K > 400:
+        return 8
+    return 0
+
+
+def in_len(K, layout_sb):
+    return 3 * (K + 32) + 12 if (layout_sb and nof_subblocks(K)) else 3 * K + 12
+
+
+class _Lib:
+    def __init__(self, path, prefix, lazy=False):
+        if not os.path.exists(path):
+            raise FileNotFoundError(path)
+        mode = os.RTLD_LAZY if lazy else ctypes.DEFAULT_MODE
+        self.lib = ctypes.CDLL(path, mode=mode)
+        self.run = getattr(self.lib, prefix + "tdec_run")
+        self.run.argtypes = [ctypes.c_uint32, _i16p, ctypes.c_int, ctypes.c_uint32, _u8p, _i16p]
+        self.run.restype = ctypes.c_int
+
+    def tdec_run(self, K, llr, layout_sb=False, nof_iterations=8, trace=False):
+        llr = np.ascontiguousarray(llr, dtype=np.int16)
+        assert llr.size >= in_len(K, layout_sb)
+        out = np.zeros(K // 8, dtype=np.uint8)
+        tr = np.zeros((nof_iterations, K), dtype=np.int16) if trace else None
+        rc = self.run(K, _ptr(llr, _i16p), int(bool(layout_sb)), nof_iterations, _ptr(out, _u8p),
+                      _ptr(tr, _i16p) if trace else None)
+        if rc:
+            raise ValueError(f"tdec_run failed K={K} rc={rc}")
+        return (out, tr) if trace else out
+
+
+class Oracle(_Lib):
+    """The repo's C restatement."""
+
+    def __init__(self):
+        super().__init__(ORACLE_SO, "oracle_")
+        L = self.lib
+        L.oracle_tcod_encode.argtypes = [ctypes.c_uint32, _u8p, _u8p]
+        L.oracle_natural_to_sb.argtypes = [ctypes.c_uint32, _i16p, _i16p]
+        L.oracle_qpp.argtypes = [ctypes.c_uint32, _u16p, _u16p]
+        L.oracle_tdec_run_batch.argtypes = [ctypes.c_uint32, _i16p, ctypes.c_uint32, ctypes.c_int,
+                                            ctypes.c_uint32, _u8p, ctypes.c_uint32]
+
+    def encode(self, K, bits):
+        bits = np.ascontiguousarray(bits, dtype=np.uint8)
+        out = np.zeros(3 * K + 12, dtype=np.uint8)
+        if self.lib.oracle_tcod_encode(K, _ptr(bits, _u8p), _ptr(out, _u8p)):
+            raise ValueError(K)
+        return out
+
+    def natural_to_sb(self, K, llr):
+        llr = np.ascontiguousarray(llr, dtype=np.int16)
+        out = np.zeros(in_len(K, True), dtype=np.int16)
+        self.lib.oracle_natural_to_sb(K, _ptr(llr, _i16p), _ptr(out, _i16p))
+        return out
+
+    def qpp(self, K):
+        f = np.zeros(K, dtype=np.uint16)
+        r = np.zeros(K, dtype=np.uint16)
+        self.lib.oracle_qpp(K, _ptr(f, _u16p), _ptr(r, _u16p))
+        return f, r
+
+    def run_batch(self, K, llr2d, layout_sb, nof_iterations):
+        llr2d = np.ascontiguousarray(llr2d, dtype=np.int16)
+        n = llr2d.shape[0]
+        out = np.zeros((n, K // 8), dtype=np.uint8)
+        rc = self.lib.oracle_tdec_run_batch(K, _ptr(llr2d, _i16p), llr2d.shape[1], int(bool(layout_sb)),
+                                            nof_iterations, _ptr(out, _u8p), n)
+        if rc:
+            raise ValueError(rc)
+        return out
+
+
+class Reference(_Lib):
+    """The reference decoder compiled from /root/reference (oracle/_ref)."""
+
+    def __init__(self):
+        super().__init__(REF_SO, "ref_", lazy=True)
+        L = self.lib
+        L.ref_tcod_encode.argtypes = [ctypes.c_uint32, _u8p, _u8p]
+        L.ref_rm_turbo_rx_lut.argtypes = [_i16p, _i16p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
+        L.ref_crc_checksum_byte.argtypes = [ctypes.c_uint32, ctypes.c_int, _u8p, ctypes.c_uint32]
+        L.ref_crc_checksum_byte.restype = ctypes.c_uint32
+
+    def encode(self, K, bits):
+        bits = np.ascontiguousarray(bits, dtype=np.uint8)
+        out = np.zeros(3 * K + 12, dtype=np.uint8)
+        if self.lib.ref_tcod_encode(K, _ptr(bits, _u8p), _ptr(out, _u8p)):
+            raise ValueError(K)
+        return out
+
+
+def ref_available():
+    return os.path.exists(REF_SO)
+
+
+def make_llrs(K, ebno_db, rng, n=1, encoder=None):
+    """Synthetic AWGN code blocks in the reference test's convention.
+
+    turbodecoder_test.c:217-255: BPSK bit1 -> +1, bit0 -> -1, noise variance
+    var = 10^(-(EbNo + 10log10(1/3))/10), LLR = (int16)(100*y) (truncation).
+    Returns (bits[n,K] uint8, llr[n,3K+12] int16).
+    """
+    enc = encoder or Oracle()
+    bits = rng.integers(0, 2, size=(n, K), dtype=np.uint8)
+    esno = ebno_db + 10 * np.log10(1.0 / 3.0)
+    var = 10 ** (-esno / 10)
+    llr = np.zeros((n, 3 * K + 12), dtype=np.int16)
+    for i in range(n):
+        sym = enc.encode(K, bits[i]).astype(np.float32) * 2 - 1
+        y = sym + rng.standard_normal(sym.shape).astype(np.float32) * np.float32(np.sqrt(var))
+        llr[i] = np.trunc(np.float32(100) * y).astype(np.int16)
+    return bits, llr

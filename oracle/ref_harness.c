@@ -1,0 +1,232 @@
+/*
+ * oracle/ref_harness.c -- drives the reference turbo decoder compiled from
+ * /root/reference (TEST INFRASTRUCTURE ONLY; built into oracle/_ref/ by
+ * oracle/Makefile and never linked by the product library).
+ *
+ * Why a harness: src/phy/fec/turbo/turbodecoder.c includes "srsran/srsran.h",
+ * which includes the CMake-generated "srsran/version.h".  That header does not
+ * exist without running the reference's build system, so turbodecoder.c is
+ * unbuildable here (no stand-in headers are written).  Everything it
+ * dispatches to IS compiled from the reference as-is:
+ *   - the window MAP kernels: include/srsran/phy/fec/turbo/turbodecoder_win.h
+ *     instantiated below exactly as turbodecoder.c:50-73 does (SSE16, AVX16);
+ *   - the generic MAP kernel: src/phy/fec/turbo/turbodecoder_gen.c;
+ *   - the half-iteration driver: include/srsran/phy/fec/turbo/turbodecoder_iter.h;
+ *   - QPP tables, vector ops, rate matching, CRC, encoder: their .c files.
+ * Only the AUTO-dispatch glue of turbodecoder.c:129-549 is restated here
+ * (init, new_cb, tdec_iteration_16, decision, run_all), so the reference's
+ * own srsran_tdec_t struct and iteration code run unchanged.
+ *
+ * The logging hook srsran_phy_log_print (phy_logger.c, also behind srsran.h)
+ * stays unresolved; it is only reached on error paths with a registered log
+ * handler, so the library is loaded with RTLD_LAZY by the tests.
+ */
+#include <stdbool.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "srsran/phy/fec/cbsegm.h"
+#include "srsran/phy/fec/crc.h"
+#include "srsran/phy/fec/turbo/rm_turbo.h"
+#include "srsran/phy/fec/turbo/tc_interl.h"
+#include "srsran/phy/fec/turbo/turbocoder.h"
+#include "srsran/phy/fec/turbo/turbodecoder.h"
+#include "srsran/phy/utils/debug.h"
+#include "srsran/phy/utils/vector.h"
+
+#include "srsran/phy/fec/turbo/turbodecoder_gen.h"
+
+#define WINIMP_IS_SSE16
+#include "srsran/phy/fec/turbo/turbodecoder_win.h"
+#undef WINIMP_IS_SSE16
+
+#define WINIMP_IS_AVX16
+#include "srsran/phy/fec/turbo/turbodecoder_win.h"
+#undef WINIMP_IS_AVX16
+
+static srsran_tdec_16bit_impl_t ref_gen_impl = {tdec_gen_init,
+                                                tdec_gen_free,
+                                                tdec_gen_dec,
+                                                tdec_gen_extract_input,
+                                                tdec_gen_decision_byte};
+static srsran_tdec_16bit_impl_t ref_sse16_impl = {tdec_winsse16_init,
+                                                  tdec_winsse16_free,
+                                                  tdec_winsse16_dec,
+                                                  tdec_winsse16_extract_input,
+                                                  tdec_winsse16_decision_byte};
+static srsran_tdec_16bit_impl_t ref_avx16_impl = {tdec_winavx16_init,
+                                                  tdec_winavx16_free,
+                                                  tdec_winavx16_dec,
+                                                  tdec_winavx16_extract_input,
+                                                  tdec_winavx16_decision_byte};
+
+#define LLR_IS_16BIT
+#include "srsran/phy/fec/turbo/turbodecoder_iter.h"
+#undef LLR_IS_16BIT
+
+/* Restated from turbodecoder.c:381-393 (this symbol is also needed by rm_turbo.c). */
+uint32_t srsran_tdec_autoimp_get_subblocks(uint32_t long_cb)
+{
+  if (!(long_cb % 16) && long_cb > 800) {
+    return 16;
+  }
+  if (!(long_cb % 8) && long_cb > 400) {
+    return 8;
+  }
+  return 0;
+}
+
+uint32_t srsran_tdec_autoimp_get_subblocks_8bit(uint32_t long_cb)
+{
+  if (!(long_cb % 32) && long_cb > 2048) {
+    return 32;
+  }
+  if (!(long_cb % 16) && long_cb > 800) {
+    return 16;
+  }
+  if (!(long_cb % 8) && long_cb > 400) {
+    return 8;
+  }
+  return 0;
+}
+
+static srsran_tdec_t tdec;
+static bool          tdec_ready = false;
+
+/* AUTO 16-bit init (turbodecoder.c:151-317, SRSRAN_TDEC_AUTO branch). */
+static int harness_init(void)
+{
+  if (tdec_ready) {
+    return 0;
+  }
+  srsran_tdec_t* h = &tdec;
+  memset(h, 0, sizeof(*h));
+  uint32_t len   = SRSRAN_TCOD_MAX_LEN_CB + SRSRAN_TCOD_TOTALTAIL;
+  h->dec_type    = SRSRAN_TDEC_AUTO;
+  h->max_long_cb = SRSRAN_TCOD_MAX_LEN_CB;
+  h->app1        = srsran_vec_i16_malloc(len);
+  h->app2        = srsran_vec_i16_malloc(len);
+  h->ext1        = srsran_vec_i16_malloc(len);
+  h->ext2        = srsran_vec_i16_malloc(len);
+  h->syst0       = srsran_vec_i16_malloc(len);
+  h->parity0     = srsran_vec_i16_malloc(len);
+  h->parity1     = srsran_vec_i16_malloc(len);
+  h->input_conv  = srsran_vec_i16_malloc(len * 3 + 32 * 3);
+  h->dec16[0]    = &ref_gen_impl;   /* AUTO_16_SSE slot holds the generic decoder */
+  h->dec16[1]    = &ref_sse16_impl; /* AUTO_16_SSEWIN */
+  h->dec16[2]    = &ref_avx16_impl; /* AUTO_16_AVXWIN */
+  for (int td = 0; td < SRSRAN_TDEC_NOF_AUTO_MODES_16; td++) {
+    if ((h->nof_blocks16[td] = h->dec16[td]->tdec_init(&h->dec16_hdlr[td], h->max_long_cb)) < 0) {
+      return -1;
+    }
+  }
+  for (int s = 0; s < 4; s++) {
+    for (int i = 0; i < SRSRAN_NOF_TC_CB_SIZES; i++) {
+      if (srsran_tc_interl_init(&h->interleaver[s][i], srsran_cbsegm_cbsize(i)) < 0) {
+        return -1;
+      }
+      srsran_tc_interl_LTE_gen_interl(&h->interleaver[s][i], srsran_cbsegm_cbsize(i), s ? (8 << (s - 1)) : 1);
+    }
+  }
+  h->current_cbidx = -1;
+  tdec_ready       = true;
+  return 0;
+}
+
+static uint32_t inter_idx(uint32_t nsb) { return nsb == 16 ? 2 : (nsb == 8 ? 1 : 0); }
+
+/* tdec_iteration_16 (turbodecoder.c:486-507), AUTO 16-bit branch only. */
+static void harness_iteration(srsran_tdec_t* h, int16_t* input)
+{
+  uint32_t nsb          = srsran_tdec_autoimp_get_subblocks(h->current_long_cb);
+  h->current_llr_type   = SRSRAN_TDEC_16;
+  h->current_dec        = nsb == 16 ? 2 : (nsb == 8 ? 1 : 0);
+  h->current_inter_idx  = inter_idx((uint32_t)h->nof_blocks16[h->current_dec]);
+  run_tdec_iteration_16bit(h, input);
+}
+
+/* The "latest output" the reference decides on (turbodecoder.c:370-378), in natural order. */
+static void latest_natural(srsran_tdec_t* h, int16_t* dst)
+{
+  uint32_t K   = h->current_long_cb;
+  int16_t* src = !(h->n_iter % 2) ? (int16_t*)h->app1 : (int16_t*)h->ext1;
+  uint32_t nsb = srsran_tdec_autoimp_get_subblocks(K);
+  if (!nsb) {
+    memcpy(dst, src, K * sizeof(int16_t));
+    return;
+  }
+  uint32_t L = K / nsb;
+  for (uint32_t n = 0; n < K; n++) {
+    dst[n] = src[(n % L) * nsb + n / L];
+  }
+}
+
+/*
+ * ref_tdec_run: srsran_tdec_run_all (turbodecoder.c:536-549) on one code block.
+ *  layout_sb = 0: natural 3K+12 input, srsran_tdec_force_not_sb() set (as turbodecoder_test does)
+ *  layout_sb = 1: rm_turbo_rx_lut layout (production path, sch.c)
+ *  trace (optional): nof_iterations*K int16, latest decoder output after every half-iteration.
+ */
+int ref_tdec_run(uint32_t K, const int16_t* input, int layout_sb, uint32_t nof_iterations, uint8_t* out, int16_t* trace)
+{
+  if (harness_init()) {
+    return -1;
+  }
+  srsran_tdec_t* h = &tdec;
+  int cbidx        = srsran_cbsegm_cbindex(K);
+  if (cbidx < 0 || srsran_cbsegm_cbsize(cbidx) != (int)K || nof_iterations < 1) {
+    return -1;
+  }
+  h->force_not_sb = layout_sb ? false : true;
+  /* The SB path writes tail values into the input's padding: work on a copy. */
+  uint32_t in_len = layout_sb ? 3 * (K + 32) + 12 : 3 * K + 12;
+  int16_t* buf    = srsran_vec_i16_malloc(3 * (K + 32) + 12 + 64);
+  memset(buf, 0, (3 * (K + 32) + 12 + 64) * sizeof(int16_t));
+  memcpy(buf, input, in_len * sizeof(int16_t));
+
+  h->n_iter          = 0;
+  h->current_long_cb = K;
+  h->current_cbidx   = cbidx;
+  do {
+    harness_iteration(h, buf);
+    if (trace) {
+      latest_natural(h, &trace[(size_t)(h->n_iter - 1) * K]);
+    }
+  } while (h->n_iter < (int)nof_iterations);
+  h->dec16[h->current_dec]->tdec_decision_byte(!(h->n_iter % 2) ? h->app1 : h->ext1, out, K);
+  free(buf);
+  return 0;
+}
+
+/* Reference turbo encoder (turbocoder.c:77-185). */
+int ref_tcod_encode(uint32_t K, const uint8_t* bits, uint8_t* out)
+{
+  static srsran_tcod_t tcod;
+  static bool          ready = false;
+  if (!ready) {
+    if (srsran_tcod_init(&tcod, SRSRAN_TCOD_MAX_LEN_CB)) {
+      return -1;
+    }
+    ready = true;
+  }
+  return srsran_tcod_encode(&tcod, (uint8_t*)bits, out, K);
+}
+
+/* Reference rate de-matching + HARQ combining into an int16 soft buffer (rm_turbo.c:390-445). */
+int ref_rm_turbo_rx_lut(const int16_t* in, int16_t* softbuf, uint32_t in_len, uint32_t cb_idx, uint32_t rv_idx)
+{
+  srsran_rm_turbo_gentables();
+  return srsran_rm_turbo_rx_lut((int16_t*)in, softbuf, in_len, cb_idx, rv_idx);
+}
+
+/* Reference byte-wise CRC (crc.c:117-128). */
+uint32_t ref_crc_checksum_byte(uint32_t poly, int order, const uint8_t* data, uint32_t nbits)
+{
+  srsran_crc_t crc;
+  memset(&crc, 0, sizeof(crc));
+  if (srsran_crc_init(&crc, poly, order)) {
+    return 0xFFFFFFFF;
+  }
+  return srsran_crc_checksum_byte(&crc, data, nbits);
+}

@@ -1,0 +1,242 @@
+#!/usr/bin/env python3
+"""Benchmark: turbo-decoded info Mbps on MI355X (BASELINE.json metric, turbo part).
+
+A "step" is one pass of the hot path over one batch of synthetic input:
+  workload "all188" (default, BASELINE configs[1]): 1024 code blocks of EACH of the
+      188 LTE sizes, 8 half-iterations, rm_turbo sub-block input layout;
+  workload "k6144" (BASELINE configs[0] shape on the GPU): 1024 x 6144-bit blocks.
+Inputs are AWGN code blocks (turbodecoder_test.c convention) resident in HBM before
+the timed region; every launch decodes the full batch (no early stop, no caching).
+
+Multi-GPU: one process per GPU (torch.distributed.run); every rank decodes its own
+batch (units partition with no data-path collective, "weak" scaling); the only
+collectives are the timing barrier and the max-over-ranks of the elapsed time.
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "turbo-decoded info Mbps + PDSCH subframes/s, 20 MHz 64QAM, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def algo_bytes(K):
+    """Algorithmic HBM bytes per code block: int16 LLRs in + K/8 bytes out."""
+    return (3 * K + 12) * 2 + K // 8
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--workload", choices=["all188", "k6144"], default="all188")
+    p.add_argument("--batch", type=int, default=1024, help="code blocks per size per step")
+    p.add_argument("--iters", type=int, default=8, help="half-iterations (srsran nof_iterations)")
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (0 = skip)")
+    p.add_argument("--pool", type=int, default=8, help="distinct AWGN code blocks per size")
+    return p.parse_args()
+
+
+def make_inputs(ora, Ks, pool, batch, rng, torch, device):
+    """Per size: `pool` AWGN code blocks (Eb/No label 4 dB) in SB layout, tiled to `batch` rows on device."""
+    from oracle import make_llrs
+
+    data = {}
+    for K in Ks:
+        _, llr = make_llrs(K, 4.0, rng, pool, ora)
+        sb = np.stack([ora.natural_to_sb(K, x) for x in llr])
+        reps = (batch + pool - 1) // pool
+        host = np.tile(sb, (reps, 1))[:batch]
+        d_in = torch.from_numpy(np.ascontiguousarray(host)).to(device)
+        d_out = torch.empty((batch, K // 8), dtype=torch.uint8, device=device)
+        data[K] = (d_in, d_out, sb)
+    return data
+
+
+def cpu_baseline(Ks, data, iters, budget_s):
+    """Reference decoder (oracle/_ref, compiled from /root/reference) on one host core.
+
+    Bounded sample: repeated passes over the pool code blocks of the workload's
+    sizes until ~budget_s seconds of CPU work; reports decoded info Mbps."""
+    from oracle import Oracle, Reference, ref_available
+
+    kind = "reference" if ref_available() else "port"
+    dec = Reference() if kind == "reference" else Oracle()
+    bits = 0
+    n_cb = 0
+    t0 = time.perf_counter()
+    passes = 0
+    while True:
+        for K in Ks:
+            sb = data[K][2]
+            for x in sb:
+                dec.tdec_run(K, x, True, iters)
+                bits += K
+                n_cb += 1
+        passes += 1
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {
+        "value": round(bits / dt / 1e6, 3),
+        "unit": "Mbps",
+        "cores": 1,
+        "kind": kind,
+        "sample": f"{passes} pass(es) over {len(data[Ks[0]][2])} AWGN blocks of each of {len(Ks)} size(s), "
+                  f"{n_cb} blocks, {iters} half-its, SB layout, {dt:.1f} s on 1 thread",
+    }
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from oracle import Oracle
+    from srsran_4g_amd import tdec
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group(backend="nccl", init_method="env://")
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if not tdec.gpu_available():
+        raise RuntimeError("bench: HIP device not visible to libsrsran_4g_amd")
+
+    Ks = list(tdec.CB_SIZES) if args.workload == "all188" else [6144]
+    ora = Oracle()
+    rng = np.random.default_rng(0x5EED + rank)
+    data = make_inputs(ora, Ks, args.pool, args.batch, rng, torch, device)
+    stream = torch.cuda.current_stream(device)
+    sp = stream.cuda_stream
+
+    def step(events=None):
+        for K in Ks:
+            d_in, d_out, _ = data[K]
+            if events is not None:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+            tdec.gpu_run_batch(K, d_in.data_ptr(), d_in.shape[1], True, d_out.data_ptr(), args.batch, args.iters, sp)
+            if events is not None:
+                e1.record(stream)
+                events.append((K, e0, e1))
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    # ---- timed region: exactly `steps` steps, barrier + sync on both sides ----
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    bits_per_step = args.batch * sum(Ks)
+    value = world * bits_per_step * args.steps / elapsed / 1e6
+
+    # ---- per-launch kernel durations (HIP events on the launch stream), outside the timed region ----
+    events = []
+    for _ in range(max(1, min(args.steps, 3))):
+        step(events)
+    torch.cuda.synchronize()
+    per_kernel = {}
+    for K, e0, e1 in events:
+        name = tdec.load_library().srsran_tdec_gpu_kernel_name(K).decode()
+        ms = e0.elapsed_time(e1)
+        d = per_kernel.setdefault(name, {"launches": 0, "ms": 0.0, "bytes": 0, "bits": 0})
+        d["launches"] += 1
+        d["ms"] += ms
+        d["bytes"] += args.batch * algo_bytes(K)
+        d["bits"] += args.batch * K
+    dom = max(per_kernel, key=lambda n: per_kernel[n]["ms"])
+    dk = per_kernel[dom]
+    avg_ms = dk["ms"] / dk["launches"]
+    bytes_per_launch = dk["bytes"] / dk["launches"]
+    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
+    traffic = None
+    tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(tf):
+        try:
+            traffic = json.load(open(tf)).get(args.workload, {}).get(dom)
+        except Exception:
+            traffic = None
+
+    result = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "Mbps",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int16",
+        "data": "synthetic: AWGN turbo code blocks (Eb/No label 4 dB, turbodecoder_test.c convention), "
+                f"{args.pool} distinct blocks per size tiled to the batch, HBM-resident",
+        "config": {
+            "workload": ("tdec all 188 LTE CB sizes x %d CBs, %d half-its, rm_turbo SB layout" % (args.batch, args.iters))
+            if args.workload == "all188" else ("tdec K=6144 x %d CBs, %d half-its, rm_turbo SB layout" % (args.batch, args.iters)),
+            "cbs_per_size": args.batch,
+            "cb_sizes": len(Ks),
+            "half_iterations": args.iters,
+            "info_bits_per_step_per_gpu": bits_per_step,
+            "parallelism": f"cb-sharded x{world}",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": dom,
+            "achieved": round(achieved, 2),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5),
+            "traffic": traffic,
+            "avg_launch_ms": round(avg_ms, 4),
+            "algo_bytes_per_launch": int(bytes_per_launch),
+        },
+        "per_kernel_mbps": {n: round(d["bits"] / (d["ms"] * 1e-3) / 1e6, 1) for n, d in per_kernel.items()},
+    }
+    if args.workload == "all188":
+        k = [e for e in events if e[0] == 6144]
+        if k:
+            ms = np.mean([e0.elapsed_time(e1) for _, e0, e1 in k])
+            result["k6144_mbps"] = round(args.batch * 6144 / (ms * 1e-3) / 1e6, 1)
+
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        result["cpu_baseline"] = cpu_baseline(Ks if args.workload == "k6144" else Ks, data, args.iters,
+                                              args.cpu_seconds)
+    elif rank == 0:
+        result["cpu_baseline"] = None
+
+    if world > 1:
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,506 @@
+// srsran_4g_amd/csrc/tdec_api.cpp -- C-ABI host side of the HIP turbo decoder.
+//
+// Implements include/srsran_tdec.h (the srsran_tdec_* surface of
+// lib/include/srsran/phy/fec/turbo/turbodecoder.h) over the kernel in
+// tdec_kernel.hip.  Host semantics follow turbodecoder.c:
+//   init / init_manual / free            turbodecoder.c:129-363
+//   new_cb / iteration / run_all          turbodecoder.c:510-549
+//   AUTO dispatch (sub-blocks per K)      turbodecoder.c:381-408
+// Calls are host-synchronous like the reference; the batch entry points are
+// extensions.  There is no CPU fallback: without a HIP device every decode call
+// fails with SRSRAN_ERROR.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <vector>
+
+#include "../../include/srsran_tdec.h"
+#include "tdec_kernel.h"
+
+using namespace srsran_amd;
+
+namespace {
+
+const uint16_t kCbSizes[SRSRAN_NOF_TC_CB_SIZES] = {
+    40,   48,   56,   64,   72,   80,   88,   96,   104,  112,  120,  128,  136,  144,  152,  160,  168,  176,  184,
+    192,  200,  208,  216,  224,  232,  240,  248,  256,  264,  272,  280,  288,  296,  304,  312,  320,  328,  336,
+    344,  352,  360,  368,  376,  384,  392,  400,  408,  416,  424,  432,  440,  448,  456,  464,  472,  480,  488,
+    496,  504,  512,  528,  544,  560,  576,  592,  608,  624,  640,  656,  672,  688,  704,  720,  736,  752,  768,
+    784,  800,  816,  832,  848,  864,  880,  896,  912,  928,  944,  960,  976,  992,  1008, 1024, 1056, 1088, 1120,
+    1152, 1184, 1216, 1248, 1280, 1312, 1344, 1376, 1408, 1440, 1472, 1504, 1536, 1568, 1600, 1632, 1664, 1696, 1728,
+    1760, 1792, 1824, 1856, 1888, 1920, 1952, 1984, 2016, 2048, 2112, 2176, 2240, 2304, 2368, 2432, 2496, 2560, 2624,
+    2688, 2752, 2816, 2880, 2944, 3008, 3072, 3136, 3200, 3264, 3328, 3392, 3456, 3520, 3584, 3648, 3712, 3776, 3840,
+    3904, 3968, 4032, 4096, 4160, 4224, 4288, 4352, 4416, 4480, 4544, 4608, 4672, 4736, 4800, 4864, 4928, 4992, 5056,
+    5120, 5184, 5248, 5312, 5376, 5440, 5504, 5568, 5632, 5696, 5760, 5824, 5888, 5952, 6016, 6080, 6144};
+
+// QPP coefficients, 36.212 Table 5.1.3-3 (tc_interl_lte.c:39-61).
+const uint16_t kF1[SRSRAN_NOF_TC_CB_SIZES] = {
+    3,   7,   19,  7,   7,   11,  5,   11,  7,   41,  103, 15,  9,   17,  9,   21,  101, 21,  57, 23,  13,
+    27,  11,  27,  85,  29,  33,  15,  17,  33,  103, 19,  19,  37,  19,  21,  21,  115, 193, 21, 133, 81,
+    45,  23,  243, 151, 155, 25,  51,  47,  91,  29,  29,  247, 29,  89,  91,  157, 55,  31,  17, 35,  227,
+    65,  19,  37,  41,  39,  185, 43,  21,  155, 79,  139, 23,  217, 25,  17,  127, 25,  239, 17, 137, 215,
+    29,  15,  147, 29,  59,  65,  55,  31,  17,  171, 67,  35,  19,  39,  19,  199, 21,  211, 21, 43,  149,
+    45,  49,  71,  13,  17,  25,  183, 55,  127, 27,  29,  29,  57,  45,  31,  59,  185, 113, 31, 17,  171,
+    209, 253, 367, 265, 181, 39,  27,  127, 143, 43,  29,  45,  157, 47,  13,  111, 443, 51,  51, 451, 257,
+    57,  313, 271, 179, 331, 363, 375, 127, 31,  33,  43,  33,  477, 35,  233, 357, 337, 37,  71, 71,  37,
+    39,  127, 39,  39,  31,  113, 41,  251, 43,  21,  43,  45,  45,  161, 89,  323, 47,  23,  47, 263};
+const uint16_t kF2[SRSRAN_NOF_TC_CB_SIZES] = {
+    10,  12,  42,  16,  18,  20,  22,  24,  26,  84,  90,  32,  34,  108, 38,  120, 84,  44,  46,  48,  50,
+    52,  36,  56,  58,  60,  62,  32,  198, 68,  210, 36,  74,  76,  78,  120, 82,  84,  86,  44,  90,  46,
+    94,  48,  98,  40,  102, 52,  106, 72,  110, 168, 114, 58,  118, 180, 122, 62,  84,  64,  66,  68,  420,
+    96,  74,  76,  234, 80,  82,  252, 86,  44,  120, 92,  94,  48,  98,  80,  102, 52,  106, 48,  110, 112,
+    114, 58,  118, 60,  122, 124, 84,  64,  66,  204, 140, 72,  74,  76,  78,  240, 82,  252, 86,  88,  60,
+    92,  846, 48,  28,  80,  102, 104, 954, 96,  110, 112, 114, 116, 354, 120, 610, 124, 420, 64,  66,  136,
+    420, 216, 444, 456, 468, 80,  164, 504, 172, 88,  300, 92,  188, 96,  28,  240, 204, 104, 212, 192, 220,
+    336, 228, 232, 236, 120, 244, 248, 168, 64,  130, 264, 134, 408, 138, 280, 142, 480, 146, 444, 120, 152,
+    462, 234, 158, 80,  96,  902, 166, 336, 170, 86,  174, 176, 178, 120, 182, 184, 186, 94,  190, 480};
+
+int cb_index(uint32_t K)
+{
+  for (int i = 0; i < SRSRAN_NOF_TC_CB_SIZES; i++) {
+    if (kCbSizes[i] == K) {
+      return i;
+    }
+  }
+  return -1;
+}
+
+constexpr size_t kMaxLds = 160 * 1024;
+
+// Geometry + device tables of one (K, sub-block count) decoder configuration.
+struct Config {
+  int       nsb;  // 16, 8 or 1 (generic)
+  TdecArgs  proto;
+  uint16_t* d_tfwd = nullptr;
+  uint16_t* d_trev = nullptr;
+};
+
+std::mutex                             g_mu;
+std::map<std::pair<uint32_t, int>, Config*> g_cfg;
+int                                    g_have_gpu = -1;
+
+bool have_gpu()
+{
+  if (g_have_gpu < 0) {
+    int n = 0;
+    g_have_gpu = (hipGetDeviceCount(&n) == hipSuccess && n > 0) ? 1 : 0;
+  }
+  return g_have_gpu == 1;
+}
+
+// Build (once) the configuration for K decoded with nsb sub-blocks (1 = generic).
+Config* get_config(uint32_t K, int nsb)
+{
+  std::lock_guard<std::mutex> lk(g_mu);
+  auto key = std::make_pair(K, nsb);
+  auto it  = g_cfg.find(key);
+  if (it != g_cfg.end()) {
+    return it->second;
+  }
+  const int idx = cb_index(K);
+  if (idx < 0 || !have_gpu()) {
+    return nullptr;
+  }
+  TdecArgs a{};
+  a.K = K;
+  if (nsb > 1) {
+    if (K % nsb || K / nsb < (uint32_t)TDEC_OVERLAP) {
+      return nullptr;
+    }
+    a.L   = K / nsb;
+    a.Ls  = a.L | 1u;  // odd slot stride: quads of different sub-blocks hit different LDS banks
+    a.xyw = nsb * a.Ls;
+    a.M   = (a.L + TDEC_W - 1) / TDEC_W;
+  } else {
+    a.L   = K;
+    a.Ls  = (K + 3) | 1u;
+    a.xyw = a.Ls;
+    a.M   = (K + 3 + TDEC_W - 1) / TDEC_W;
+  }
+  a.magicL = (uint32_t)(((1ull << 32) + a.L - 1) / a.L);
+  if (tdec_lds_bytes(nsb, a.xyw, a.M) > kMaxLds) {
+    return nullptr;
+  }
+  // QPP tables (tc_interl_lte.c:69-107) expressed directly as LDS slots.
+  std::vector<uint16_t> fwd(K), rev(K), tf(K), tr(K);
+  const uint64_t f1 = kF1[idx], f2 = kF2[idx];
+  for (uint64_t i = 0; i < K; i++) {
+    const uint32_t j = (uint32_t)((f1 * i + f2 * i * i) % K);
+    fwd[i]           = (uint16_t)j;
+    rev[j]           = (uint16_t)i;
+  }
+  auto slot = [&](uint32_t n) -> uint16_t {
+    return nsb > 1 ? (uint16_t)((n / a.L) * a.Ls + n % a.L) : (uint16_t)n;
+  };
+  for (uint32_t n = 0; n < K; n++) {
+    tf[n] = slot(fwd[n]);
+    tr[n] = slot(rev[n]);
+  }
+  Config* c = new Config();
+  c->nsb    = nsb;
+  c->proto  = a;
+  if (hipMalloc(&c->d_tfwd, K * sizeof(uint16_t)) != hipSuccess ||
+      hipMalloc(&c->d_trev, K * sizeof(uint16_t)) != hipSuccess ||
+      hipMemcpy(c->d_tfwd, tf.data(), K * sizeof(uint16_t), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(c->d_trev, tr.data(), K * sizeof(uint16_t), hipMemcpyHostToDevice) != hipSuccess) {
+    fprintf(stderr, "[srsran_tdec] device table allocation failed for K=%u\n", K);
+    delete c;
+    return nullptr;
+  }
+  g_cfg[key] = c;
+  return c;
+}
+
+int auto_nsb(uint32_t K)
+{
+  const uint32_t n = srsran_tdec_autoimp_get_subblocks(K);
+  return n ? (int)n : 1;
+}
+
+int nsb_for(const srsran_tdec_t* h, uint32_t K)
+{
+  switch (h->dec_type) {
+    case SRSRAN_TDEC_AUTO:
+      return auto_nsb(K);
+    case SRSRAN_TDEC_GENERIC:
+      return 1;
+    case SRSRAN_TDEC_SSE_WINDOW:
+      return 8;
+    case SRSRAN_TDEC_AVX_WINDOW:
+      return 16;
+    default:
+      return -1;
+  }
+}
+
+// Per-object device context (the reference's app/ext/syst/parity buffers).
+struct Ctx {
+  hipStream_t stream = nullptr;
+  short*      d_in   = nullptr;  // one code block input (max SB layout)
+  uint8_t*    d_out  = nullptr;
+  short*      d_state = nullptr; // saved LDS state between srsran_tdec_iteration calls
+  size_t      state_elems = 0;
+  // batch scratch
+  short*      d_bin  = nullptr;
+  uint8_t*    d_bout = nullptr;
+  size_t      bin_elems = 0, bout_bytes = 0;
+};
+
+const size_t kMaxIn = 3 * (SRSRAN_TCOD_MAX_LEN_CB + 32) + SRSRAN_TCOD_TOTALTAIL;
+
+int enqueue(const Config* c, const short* d_in, uint32_t in_stride, int layout_sb, uint8_t* d_out, uint32_t ncb,
+            int n_start, int n_end, short* d_state, hipStream_t stream)
+{
+  TdecArgs a  = c->proto;
+  a.in        = d_in;
+  a.in_stride = in_stride;
+  a.layout_sb = (c->nsb > 1) ? layout_sb : 0;  // K<=400 is always natural (rm_turbo.c:403-425)
+  a.ncb       = ncb;
+  a.n_start   = n_start;
+  a.n_end     = n_end;
+  a.out       = d_out;
+  a.tfwd      = c->d_tfwd;
+  a.trev      = c->d_trev;
+  a.state     = d_state;
+  hipError_t e = tdec_launch(c->nsb, a, stream);
+  if (e != hipSuccess) {
+    fprintf(stderr, "[srsran_tdec] launch failed: %s\n", hipGetErrorString(e));
+    return SRSRAN_ERROR;
+  }
+  return SRSRAN_SUCCESS;
+}
+
+bool grow(void** p, size_t* have, size_t need)
+{
+  if (*have >= need) {
+    return true;
+  }
+  if (*p) {
+    (void)hipFree(*p);
+    *p = nullptr;
+  }
+  if (hipMalloc(p, need) != hipSuccess) {
+    *have = 0;
+    return false;
+  }
+  *have = need;
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+uint32_t srsran_tdec_autoimp_get_subblocks(uint32_t long_cb)
+{
+  if (!(long_cb % 16) && long_cb > 800) {
+    return 16;
+  }
+  if (!(long_cb % 8) && long_cb > 400) {
+    return 8;
+  }
+  return 0;
+}
+
+uint32_t srsran_tdec_autoimp_get_subblocks_8bit(uint32_t long_cb)
+{
+  if (!(long_cb % 32) && long_cb > 2048) {
+    return 32;
+  }
+  if (!(long_cb % 16) && long_cb > 800) {
+    return 16;
+  }
+  if (!(long_cb % 8) && long_cb > 400) {
+    return 8;
+  }
+  return 0;
+}
+
+int srsran_tdec_gpu_available(void)
+{
+  std::lock_guard<std::mutex> lk(g_mu);
+  return have_gpu() ? 1 : 0;
+}
+
+const char* srsran_tdec_gpu_kernel_name(uint32_t long_cb)
+{
+  switch (auto_nsb(long_cb)) {
+    case 16:
+      return "tdec_kernel<16>";
+    case 8:
+      return "tdec_kernel<8>";
+    default:
+      return "tdec_kernel<1>";
+  }
+}
+
+int srsran_tdec_init(srsran_tdec_t* h, uint32_t max_long_cb)
+{
+  return srsran_tdec_init_manual(h, max_long_cb, SRSRAN_TDEC_AUTO);
+}
+
+int srsran_tdec_init_manual(srsran_tdec_t* h, uint32_t max_long_cb, srsran_tdec_impl_type_t dec_type)
+{
+  if (!h) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  memset(h, 0, sizeof(*h));
+  if (dec_type != SRSRAN_TDEC_AUTO && dec_type != SRSRAN_TDEC_GENERIC && dec_type != SRSRAN_TDEC_SSE_WINDOW &&
+      dec_type != SRSRAN_TDEC_AVX_WINDOW) {
+    fprintf(stderr, "[srsran_tdec] decoder %d not supported\n", (int)dec_type);
+    return SRSRAN_ERROR;
+  }
+  if (max_long_cb > SRSRAN_TCOD_MAX_LEN_CB) {
+    return SRSRAN_ERROR;
+  }
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!have_gpu()) {
+      fprintf(stderr, "[srsran_tdec] no HIP device available\n");
+      return SRSRAN_ERROR;
+    }
+  }
+  Ctx* c = new Ctx();
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipMalloc(&c->d_in, kMaxIn * sizeof(short)) != hipSuccess ||
+      hipMalloc(&c->d_out, SRSRAN_TCOD_MAX_LEN_CB / 8) != hipSuccess) {
+    delete c;
+    return SRSRAN_ERROR;
+  }
+  hipMemset(c->d_in, 0, kMaxIn * sizeof(short));
+  h->gpu           = c;
+  h->max_long_cb   = max_long_cb;
+  h->dec_type      = dec_type;
+  h->current_cbidx = -1;
+  return SRSRAN_SUCCESS;
+}
+
+void srsran_tdec_free(srsran_tdec_t* h)
+{
+  if (!h) {
+    return;
+  }
+  Ctx* c = (Ctx*)h->gpu;
+  if (c) {
+    if (c->stream) {
+      hipStreamSynchronize(c->stream);
+      hipStreamDestroy(c->stream);
+    }
+    hipFree(c->d_in);
+    hipFree(c->d_out);
+    hipFree(c->d_state);
+    hipFree(c->d_bin);
+    hipFree(c->d_bout);
+    delete c;
+  }
+  memset(h, 0, sizeof(*h));
+}
+
+void srsran_tdec_force_not_sb(srsran_tdec_t* h)
+{
+  if (h) {
+    h->force_not_sb = true;
+  }
+}
+
+int srsran_tdec_new_cb(srsran_tdec_t* h, uint32_t long_cb)
+{
+  if (!h || long_cb > h->max_long_cb) {
+    fprintf(stderr, "[srsran_tdec] TDEC was initialized for max_long_cb=%d\n", h ? h->max_long_cb : 0);
+    return SRSRAN_ERROR;
+  }
+  h->n_iter          = 0;
+  h->current_long_cb = long_cb;
+  h->current_cbidx   = cb_index(long_cb);
+  if (h->current_cbidx < 0) {
+    fprintf(stderr, "[srsran_tdec] Invalid CB length %d\n", long_cb);
+    return SRSRAN_ERROR;
+  }
+  return SRSRAN_SUCCESS;
+}
+
+int srsran_tdec_get_nof_iterations(srsran_tdec_t* h) { return h ? h->n_iter : 0; }
+
+static size_t input_len(const srsran_tdec_t* h, const Config* c, uint32_t K)
+{
+  const bool sb = !h->force_not_sb && c->nsb > 1;
+  return sb ? 3 * (K + 32) + 12 : 3 * K + 12;
+}
+
+void srsran_tdec_iteration(srsran_tdec_t* h, int16_t* input, uint8_t* output)
+{
+  if (!h || !h->gpu || h->current_cbidx < 0) {
+    fprintf(stderr, "[srsran_tdec] Error CB index not set (call srsran_tdec_new_cb() first\n");
+    return;
+  }
+  Ctx*           ctx = (Ctx*)h->gpu;
+  const uint32_t K   = h->current_long_cb;
+  Config*        c   = get_config(K, nsb_for(h, K));
+  if (!c) {
+    fprintf(stderr, "[srsran_tdec] unsupported K=%u\n", K);
+    return;
+  }
+  const size_t st = 2 * (size_t)c->proto.xyw;
+  if (!grow((void**)&ctx->d_state, &ctx->state_elems, st * sizeof(short))) {
+    return;
+  }
+  if (h->n_iter == 0) {
+    hipMemcpyAsync(ctx->d_in, input, input_len(h, c, K) * sizeof(short), hipMemcpyHostToDevice, ctx->stream);
+  }
+  if (enqueue(c, ctx->d_in, (uint32_t)kMaxIn, !h->force_not_sb, ctx->d_out, 1, h->n_iter, h->n_iter + 1,
+              ctx->d_state, ctx->stream)) {
+    return;
+  }
+  hipMemcpyAsync(output, ctx->d_out, K / 8, hipMemcpyDeviceToHost, ctx->stream);
+  hipStreamSynchronize(ctx->stream);
+  h->n_iter++;
+}
+
+int srsran_tdec_run_all(srsran_tdec_t* h, int16_t* input, uint8_t* output, uint32_t nof_iterations, uint32_t long_cb)
+{
+  if (srsran_tdec_new_cb(h, long_cb)) {
+    return SRSRAN_ERROR;
+  }
+  int ret = srsran_tdec_run_all_batch(h, input, 0, output, 1, nof_iterations, long_cb);
+  if (ret == SRSRAN_SUCCESS) {
+    h->n_iter = nof_iterations > 0 ? (int)nof_iterations : 1;
+  }
+  return ret;
+}
+
+int srsran_tdec_run_all_batch(srsran_tdec_t* h,
+                              const int16_t* input,
+                              uint32_t       in_stride,
+                              uint8_t*       output,
+                              uint32_t       nof_cb,
+                              uint32_t       nof_iterations,
+                              uint32_t       long_cb)
+{
+  if (!h || !h->gpu || !input || !output) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  if (long_cb > h->max_long_cb || cb_index(long_cb) < 0) {
+    return SRSRAN_ERROR;
+  }
+  if (nof_cb == 0) {
+    return SRSRAN_SUCCESS;
+  }
+  Ctx*    ctx = (Ctx*)h->gpu;
+  Config* c   = get_config(long_cb, nsb_for(h, long_cb));
+  if (!c) {
+    return SRSRAN_ERROR;
+  }
+  const size_t len = input_len(h, c, long_cb);
+  if (in_stride == 0) {
+    in_stride = (uint32_t)len;
+  }
+  if (in_stride < len) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  const size_t in_elems  = (size_t)in_stride * (nof_cb - 1) + len;
+  const size_t out_bytes = (size_t)nof_cb * (long_cb / 8);
+  if (!grow((void**)&ctx->d_bin, &ctx->bin_elems, in_elems * sizeof(short)) ||
+      !grow((void**)&ctx->d_bout, &ctx->bout_bytes, out_bytes)) {
+    return SRSRAN_ERROR;
+  }
+  hipMemcpyAsync(ctx->d_bin, input, in_elems * sizeof(short), hipMemcpyHostToDevice, ctx->stream);
+  const int n_end = nof_iterations > 0 ? (int)nof_iterations : 1;  // do { } while (n_iter < nof_iterations)
+  if (enqueue(c, ctx->d_bin, in_stride, !h->force_not_sb, ctx->d_bout, nof_cb, 0, n_end, nullptr, ctx->stream)) {
+    return SRSRAN_ERROR;
+  }
+  hipMemcpyAsync(output, ctx->d_bout, out_bytes, hipMemcpyDeviceToHost, ctx->stream);
+  if (hipStreamSynchronize(ctx->stream) != hipSuccess) {
+    fprintf(stderr, "[srsran_tdec] decode failed: %s\n", hipGetErrorString(hipGetLastError()));
+    return SRSRAN_ERROR;
+  }
+  return SRSRAN_SUCCESS;
+}
+
+int srsran_tdec_gpu_run_batch(uint32_t       long_cb,
+                              const int16_t* d_input,
+                              uint32_t       in_stride,
+                              int            layout_sb,
+                              uint8_t*       d_output,
+                              uint32_t       nof_cb,
+                              uint32_t       nof_iterations,
+                              void*          stream)
+{
+  if (!d_input || !d_output || cb_index(long_cb) < 0) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  Config* c = get_config(long_cb, auto_nsb(long_cb));
+  if (!c) {
+    return SRSRAN_ERROR;
+  }
+  const uint32_t len = (layout_sb && c->nsb > 1) ? 3 * (long_cb + 32) + 12 : 3 * long_cb + 12;
+  if (in_stride < len) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  const int n_end = nof_iterations > 0 ? (int)nof_iterations : 1;
+  return enqueue(c, d_input, in_stride, layout_sb, d_output, nof_cb, 0, n_end, nullptr, (hipStream_t)stream);
+}
+
+void srsran_tdec_iteration_8bit(srsran_tdec_t* h, int8_t* input, uint8_t* output)
+{
+  (void)h;
+  (void)input;
+  (void)output;
+  fprintf(stderr, "[srsran_tdec] 8-bit decoder not provided\n");
+}
+
+int srsran_tdec_run_all_8bit(srsran_tdec_t* h, int8_t* input, uint8_t* output, uint32_t nof_iterations, uint32_t long_cb)
+{
+  (void)h;
+  (void)input;
+  (void)output;
+  (void)nof_iterations;
+  (void)long_cb;
+  fprintf(stderr, "[srsran_tdec] 8-bit decoder not provided\n");
+  return SRSRAN_ERROR;
+}
+
+}  // extern "C"

@@ -1,0 +1,520 @@
+// srsran_4g_amd/csrc/tdec_kernel.hip -- LTE turbo decoder for CDNA4 (gfx950).
+//
+// Bit-exact with srsRAN_4G's AUTO 16-bit turbo decoder (AVX2 build):
+//   K <= 400           generic max-log-MAP, int16 wrap        (turbodecoder_gen.c:58-236)
+//   408 <= K <= 800    8-sub-block sliding window, saturating (turbodecoder_win.h, SSE16)
+//   K >= 816           16-sub-block sliding window, saturating (turbodecoder_win.h, AVX16)
+// dispatch: turbodecoder.c:381-408; half-iteration driver: turbodecoder_iter.h:72-144.
+//
+// Mapping (one wave64 per workgroup):
+//   * a code block's sub-block s is served by a QUAD of lanes; lane j of the quad
+//     holds trellis states (2j, 2j+1) packed as two int16 in one VGPR.  Each trellis
+//     step is ~6 packed VALU ops per lane: two DPP quad_perm reads fetch the source
+//     states, v_perm_b32 (per-lane selector) arranges them, v_pk_add_i16 (clamp)
+//     adds the branch metrics, v_pk_max_i16 selects.
+//   * NSB=16: one CB per wave (16 quads); NSB=8: two CBs; generic (NSB=1): 16 CBs.
+//   * per CB, LDS holds XY[slot] = (x, y) branch inputs of the current constituent
+//     decoder and AUX[slot] (ext1 / app1 bookkeeping of turbodecoder_iter.h); after a
+//     constituent decode XY.lo is overwritten with its output LLR.  The QPP
+//     interleave between half-iterations is an LDS gather.
+//   * beta is not stored per step: the backward pass keeps a checkpoint every W
+//     steps, the forward pass recomputes W betas into registers before consuming
+//     them.  Integer recursion => the recomputed values are bit-identical.
+//   * everything runs inside one launch for all half-iterations; HBM traffic is the
+//     input LLRs once per half-iteration read + K/8 output bytes.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "tdec_kernel.h"
+
+namespace srsran_amd {
+
+typedef short v2s __attribute__((ext_vector_type(2)));
+
+static constexpr int W        = TDEC_W;        // beta checkpoint / recompute window
+static constexpr int OVERLAP  = TDEC_OVERLAP;  // win_overlap_len (turbodecoder_win.h:54,149)
+static constexpr short NEGINF = -10000;
+
+__device__ __forceinline__ v2s u2v(uint32_t u) { return __builtin_bit_cast(v2s, u); }
+__device__ __forceinline__ uint32_t v2u(v2s v) { return __builtin_bit_cast(uint32_t, v); }
+
+template <bool SAT>
+__device__ __forceinline__ v2s padd(v2s a, v2s b)
+{
+  if constexpr (SAT) {
+    return __builtin_elementwise_add_sat(a, b);
+  } else {
+    return a + b;
+  }
+}
+template <bool SAT>
+__device__ __forceinline__ v2s psub(v2s a, v2s b)
+{
+  if constexpr (SAT) {
+    return __builtin_elementwise_sub_sat(a, b);
+  } else {
+    return a - b;
+  }
+}
+__device__ __forceinline__ v2s pmax(v2s a, v2s b) { return __builtin_elementwise_max(a, b); }
+__device__ __forceinline__ v2s lo2(v2s a) { return __builtin_shufflevector(a, a, 0, 0); }
+__device__ __forceinline__ v2s hi2(v2s a) { return __builtin_shufflevector(a, a, 1, 1); }
+__device__ __forceinline__ v2s swp(v2s a) { return __builtin_shufflevector(a, a, 1, 0); }
+__device__ __forceinline__ v2s perm(v2s hi_src, v2s lo_src, uint32_t sel)
+{
+  return u2v(__builtin_amdgcn_perm(v2u(hi_src), v2u(lo_src), sel));
+}
+#define QP(a, b, c, d) ((a) | ((b) << 2) | ((c) << 4) | ((d) << 6))
+template <int CTRL>
+__device__ __forceinline__ v2s dpp(v2s a)
+{
+  return u2v((uint32_t)__builtin_amdgcn_mov_dpp((int)v2u(a), CTRL, 0xf, 0xf, false));
+}
+
+// Per-lane constants (quad position j = lane & 3).
+struct LaneSel {
+  uint32_t rb;     // beta: (o_j, o_{j+4}) from the two DPP reads
+  uint32_t c0, c1; // alpha: bit-0 / bit-1 source pairs
+  uint32_t gb1, gb2, ga0, ga1;  // branch-metric selectors over {x, y, xy, 0}
+};
+
+__device__ __forceinline__ LaneSel lane_sel(int j)
+{
+  LaneSel s;
+  const int h = j & 1;
+  s.rb        = h ? 0x07060302u : 0x05040100u;
+  s.c0        = j < 2 ? 0x07060100u : 0x05040302u;
+  s.c1        = j < 2 ? 0x05040302u : 0x07060100u;
+  // bytes of {XYS=(xy,xy) : XY=(x,y)}: x=0,1 y=2,3 xy=4,5 zero=0x0c
+  const uint32_t b1[4] = {0x05040c0cu, 0x03020100u, 0x01000302u, 0x0c0c0504u};
+  const uint32_t b2[4] = {0x0c0c0504u, 0x01000302u, 0x03020100u, 0x05040c0cu};
+  s.gb1                = j == 0 ? b1[0] : (j == 1 ? b1[1] : (j == 2 ? b1[2] : b1[3]));
+  s.gb2                = j == 0 ? b2[0] : (j == 1 ? b2[1] : (j == 2 ? b2[2] : b2[3]));
+  s.ga0                = h ? 0x0c0c0302u : 0x03020c0cu;
+  s.ga1                = h ? 0x05040100u : 0x01000504u;
+  return s;
+}
+
+// Backward step (turbodecoder_win.h:641-664 / turbodecoder_gen.c:78-100).
+template <bool SAT>
+__device__ __forceinline__ v2s beta_step(v2s P, v2s xy_in, const LaneSel& ls)
+{
+  const v2s xys = padd<SAT>(xy_in, swp(xy_in));
+  const v2s g1  = perm(xys, xy_in, ls.gb1);
+  const v2s g2  = perm(xys, xy_in, ls.gb2);
+  const v2s t1  = dpp<QP(0, 0, 1, 1)>(P);
+  const v2s t2  = dpp<QP(2, 2, 3, 3)>(P);
+  const v2s r   = perm(t2, t1, ls.rb);
+  return pmax(padd<SAT>(lo2(r), g1), padd<SAT>(hi2(r), g2));
+}
+
+// Forward candidates (turbodecoder_win.h:767-785 / turbodecoder_gen.c:133-149).
+template <bool SAT>
+__device__ __forceinline__ void alpha_cand(v2s P, v2s xy_in, const LaneSel& ls, v2s& c0, v2s& c1)
+{
+  const v2s xys = padd<SAT>(xy_in, swp(xy_in));
+  const v2s ga  = perm(xys, xy_in, ls.ga0);
+  const v2s gb  = perm(xys, xy_in, ls.ga1);
+  const v2s u   = dpp<QP(0, 2, 0, 2)>(P);
+  const v2s v   = dpp<QP(1, 3, 1, 3)>(P);
+  c0            = padd<SAT>(perm(v, u, ls.c0), ga);
+  c1            = padd<SAT>(perm(v, u, ls.c1), gb);
+}
+
+// LLR = max_i(beta_i + c1_i) - max_i(beta_i + c0_i) over the quad (win.h:788-815).
+template <bool SAT>
+__device__ __forceinline__ short llr_out(v2s B, v2s c0, v2s c1)
+{
+  const v2s m0 = padd<SAT>(B, c0);
+  const v2s m1 = padd<SAT>(B, c1);
+  v2s q        = pmax(perm(m1, m0, 0x05040100u), perm(m1, m0, 0x07060302u));  // (max0, max1)
+  q            = pmax(q, dpp<QP(1, 0, 3, 2)>(q));
+  q            = pmax(q, dpp<QP(2, 3, 0, 1)>(q));
+  const v2s d  = psub<SAT>(swp(q), q);  // .x = max1 - max0
+  return d.x;
+}
+
+// normalize(): subtract state 0 from all states (win.h:480-498, gen.c:105-110).
+template <bool SAT>
+__device__ __forceinline__ v2s norm(v2s P)
+{
+  return psub<SAT>(P, lo2(dpp<QP(0, 0, 0, 0)>(P)));
+}
+
+__device__ __forceinline__ v2s init_known(int j) { return j == 0 ? v2s{0, NEGINF} : v2s{NEGINF, NEGINF}; }
+
+// beta_trellis (win.h:500-548): tail steps K+2..K for the last sub-block, int16 wrap.
+__device__ __forceinline__ v2s trellis_pair(const short* xt, const short* yt, int j)
+{
+  short o[8] = {0, NEGINF, NEGINF, NEGINF, NEGINF, NEGINF, NEGINF, NEGINF};
+#pragma unroll
+  for (int t = 2; t >= 0; t--) {
+    const short x = xt[t], y = yt[t], xy = (short)(x + y);
+    short n[8];
+    n[0] = max(o[0], (short)(o[4] + xy));
+    n[1] = max((short)(o[0] + xy), o[4]);
+    n[2] = max((short)(o[1] + x), (short)(o[5] + y));
+    n[3] = max((short)(o[1] + y), (short)(o[5] + x));
+    n[4] = max((short)(o[2] + y), (short)(o[6] + x));
+    n[5] = max((short)(o[2] + x), (short)(o[6] + y));
+    n[6] = max((short)(o[3] + xy), o[7]);
+    n[7] = max(o[3], (short)(o[7] + xy));
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      o[i] = n[i];
+    }
+  }
+  v2s r;
+  r.x = j == 0 ? o[0] : (j == 1 ? o[2] : (j == 2 ? o[4] : o[6]));
+  r.y = j == 0 ? o[1] : (j == 1 ? o[3] : (j == 2 ? o[5] : o[7]));
+  return r;
+}
+
+// Per-NSB compile-time geometry.
+template <int NSB>
+struct Geo {
+  static constexpr bool SAT   = NSB > 1;         // window decoders saturate, generic wraps
+  static constexpr int  G     = 4 * NSB;         // lanes per code block
+  static constexpr int  CPW   = 64 / G;          // code blocks per wave
+  static constexpr int  KMAX  = NSB == 16 ? 6144 : (NSB == 8 ? 800 : 400);
+  static constexpr int  NPL   = (KMAX + G - 1) / G;  // prepare positions per lane
+};
+
+struct Smem {
+  uint32_t* xy;   // [CPW][XYW] (x,y) / output LLR in .lo
+  short*    aux;  // [CPW][XYW]
+  uint32_t* ck;   // [M][64]
+};
+
+// Normalisation predicates.
+template <int NSB>
+__device__ __forceinline__ bool beta_norm_at(int p, int K)
+{
+  if constexpr (NSB > 1) {
+    return (p % 2) == 0 && p != 0;
+  } else {
+    return (p % 4) == 0 && p < K;
+  }
+}
+template <int NSB>
+__device__ __forceinline__ bool alpha_norm_at(int t)
+{
+  if constexpr (NSB > 1) {
+    return (t % 2) == 0 && t != 0;
+  } else {
+    return ((t + 1) % 4) == 0;
+  }
+}
+
+// One constituent MAP decode for this quad's sub-block.  XY[base + k] holds the
+// branch inputs; the output LLR overwrites XY.lo.  Nb = length of the beta
+// recursion (L, or K+3 for the generic decoder), La = alpha length (L or K).
+template <int NSB>
+__device__ void map_decode(const Smem& sm, int base, int lane, int j, int s, int K, int L, int Nb, int La, int M,
+                           const short* xt, const short* yt)
+{
+  constexpr bool SAT = Geo<NSB>::SAT;
+  const LaneSel  ls  = lane_sel(j);
+  const uint32_t* xy = sm.xy + base;
+  short*          xyo = reinterpret_cast<short*>(sm.xy + base);
+
+  // ---------------- backward (beta) pass ----------------
+  v2s P;
+  if constexpr (NSB > 1) {
+    // training over the first OVERLAP steps of the own sub-block (win.h:622-630)
+    P = v2s{NEGINF, NEGINF};
+#pragma unroll
+    for (int k = OVERLAP - 1; k >= 0; k--) {
+      P = beta_step<SAT>(P, u2v(xy[k]), ls);
+      if (beta_norm_at<NSB>(k, K)) {
+        P = norm<SAT>(P);
+      }
+    }
+    // sub-block s starts from s+1's training state, the last from the tail (win.h:577-620)
+    const v2s nxt = u2v((uint32_t)__shfl_down((int)v2u(P), 4, 64));
+    P             = (s == NSB - 1) ? trellis_pair(xt, yt, j) : nxt;
+  } else {
+    P = init_known(j);
+  }
+  sm.ck[(M - 1) * 64 + lane] = v2u(P);  // checkpoint M = beta[Nb]
+  for (int m = M - 1; m >= 0; m--) {    // windows [mW, min(mW+W, Nb)), descending
+    const int p0 = m * W;
+    const int p1 = min(p0 + W, Nb);
+    v2s       xw[W];
+#pragma unroll
+    for (int i = 0; i < W; i++) {
+      if (p0 + i < p1) {
+        xw[i] = u2v(xy[p0 + i]);
+      }
+    }
+#pragma unroll
+    for (int i = W - 1; i >= 0; i--) {
+      if (p0 + i < p1) {
+        P = beta_step<SAT>(P, xw[i], ls);
+        if (i == 0 && m != 0) {
+          sm.ck[(m - 1) * 64 + lane] = v2u(P);  // stored (pre-normalisation) beta[mW]
+        }
+        if (beta_norm_at<NSB>(p0 + i, K)) {
+          P = norm<SAT>(P);
+        }
+      }
+    }
+  }
+
+  // ---------------- forward (alpha) pass ----------------
+  if constexpr (NSB > 1) {
+    P = v2s{NEGINF, NEGINF};
+#pragma unroll
+    for (int k = 0; k < OVERLAP; k++) {
+      v2s c0, c1;
+      alpha_cand<SAT>(P, u2v(xy[L - OVERLAP + k]), ls, c0, c1);
+      P = pmax(c0, c1);
+      if (alpha_norm_at<NSB>(k)) {
+        P = norm<SAT>(P);
+      }
+    }
+    const v2s prv = u2v((uint32_t)__shfl_up((int)v2u(P), 4, 64));
+    P             = (s == 0) ? init_known(j) : prv;
+  } else {
+    P = init_known(j);
+  }
+
+  const int nwin = (La + W - 1) / W;
+  for (int m = 0; m < nwin; m++) {
+    const int t0 = m * W;
+    const int c  = min(t0 + W, Nb);       // checkpoint position
+    const int ta = min(t0 + W, La);       // alpha end (exclusive)
+    v2s       xw[W];
+    v2s       bw[W];
+#pragma unroll
+    for (int i = 0; i < W; i++) {
+      if (t0 + i < c) {
+        xw[i] = u2v(xy[t0 + i]);
+      }
+    }
+    // recompute beta[t0+1 .. c] (bw[i] = beta[t0+1+i])
+    v2s Pb = u2v(sm.ck[m * 64 + lane]);
+    {
+      const int ic = c - t0 - 1;
+#pragma unroll
+      for (int i = W - 1; i >= 0; i--) {
+        if (i == ic) {
+          bw[i] = Pb;
+          if (c < Nb && beta_norm_at<NSB>(c, K)) {
+            Pb = norm<SAT>(Pb);
+          }
+        } else if (i < ic) {
+          const int pos = t0 + 1 + i;
+          Pb            = beta_step<SAT>(Pb, xw[i + 1], ls);
+          bw[i]         = Pb;
+          if (beta_norm_at<NSB>(pos, K)) {
+            Pb = norm<SAT>(Pb);
+          }
+        }
+      }
+    }
+    // alpha + LLR over t0 .. ta-1
+#pragma unroll
+    for (int i = 0; i < W; i++) {
+      if (t0 + i < ta) {
+        v2s c0, c1;
+        alpha_cand<SAT>(P, xw[i], ls, c0, c1);
+        const short o = llr_out<SAT>(bw[i], c0, c1);
+        P             = pmax(c0, c1);
+        if (alpha_norm_at<NSB>(t0 + i)) {
+          P = norm<SAT>(P);
+        }
+        xyo[2 * (t0 + i)] = o;
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ uint32_t pack2(short lo, short hi)
+{
+  return (uint32_t)(uint16_t)lo | ((uint32_t)(uint16_t)hi << 16);
+}
+
+template <int NSB>
+__global__ __launch_bounds__(64) void tdec_kernel(TdecArgs a)
+{
+  using Gm                = Geo<NSB>;
+  constexpr bool SAT      = Gm::SAT;
+  constexpr int  G        = Gm::G;
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+
+  const int lane = threadIdx.x;
+  const int cw   = lane / G;                 // CB within wave
+  const int g    = lane % G;                 // lane within CB group
+  const int s    = g >> 2;                   // sub-block
+  const int j    = g & 3;                    // state-pair index
+  const int K    = a.K;
+  const int L    = a.L;
+  const int Ls   = a.Ls;
+  const int XYW  = a.xyw;
+  const int M    = a.M;
+  const int cb   = blockIdx.x * Gm::CPW + cw;
+  const bool live = cb < (int)a.ncb;
+  const int cbr  = live ? cb : (int)a.ncb - 1;
+
+  Smem sm;
+  sm.xy  = smem;
+  sm.aux = reinterpret_cast<short*>(smem + Gm::CPW * XYW);
+  sm.ck  = smem + Gm::CPW * XYW + (Gm::CPW * XYW + 1) / 2;
+  uint32_t* xyc  = sm.xy + cw * XYW;
+  short*    xylo = reinterpret_cast<short*>(xyc);
+  short*    auxc = sm.aux + cw * XYW;
+
+  const short* in  = a.in + (size_t)cbr * a.in_stride;
+  const int    nsb = NSB > 1 ? NSB : 1;
+  // input stream accessors (natural 3K+12 or rm_turbo SB layout)
+  auto sbi = [&](int n) -> int {  // rm_turbo SB position of natural bit n
+    const int q = (int)__umulhi((uint32_t)n, a.magicL);
+    return (n - q * L) * nsb + q;
+  };
+  auto S  = [&](int n) -> short { return a.layout_sb ? in[sbi(n)] : in[3 * n]; };
+  auto P0 = [&](int n) -> short { return a.layout_sb ? in[(K + 32) + sbi(n)] : in[3 * n + 1]; };
+  auto P1 = [&](int n) -> short { return a.layout_sb ? in[2 * (K + 32) + sbi(n)] : in[3 * n + 2]; };
+  const short* tail = a.layout_sb ? in + 3 * (K + 32) : in + 3 * K;
+  short st[3], p0t[3], x2t[3], p1t[3];
+#pragma unroll
+  for (int t = 0; t < 3; t++) {
+    st[t]  = tail[2 * t];
+    p0t[t] = tail[2 * t + 1];
+    x2t[t] = tail[6 + 2 * t];
+    p1t[t] = tail[6 + 2 * t + 1];
+  }
+  auto slot = [&](int n) -> int {
+    if constexpr (NSB > 1) {
+      const int q = (int)__umulhi((uint32_t)n, a.magicL);
+      return q * Ls + (n - q * L);
+    } else {
+      return n;
+    }
+  };
+  const uint16_t* tfwd = a.tfwd;
+  const uint16_t* trev = a.trev;
+
+  // restore state from a previous launch (srsran_tdec_iteration path)
+  if (a.n_start > 0) {
+    const short* se = a.state + (size_t)cbr * 2 * XYW;
+    for (int i = g; i < XYW; i += G) {
+      xylo[2 * i] = se[i];
+      auxc[i]     = se[XYW + i];
+    }
+    __syncthreads();
+  }
+
+  const int base = cw * XYW + (NSB > 1 ? s * Ls : 0);
+  const int Nb   = NSB > 1 ? L : K + 3;
+  const int La   = NSB > 1 ? L : K;
+
+  for (int h = a.n_start; h < a.n_end; h++) {
+    // -------- prepare branch inputs (turbodecoder_iter.h:104-128) --------
+    if ((h & 1) == 0) {
+      if (h == 0) {
+        for (int n = g; n < K; n += G) {
+          xyc[slot(n)] = pack2(S(n), P0(n));
+        }
+      } else {
+        // app1 = ext2 de-interleaved: gather into the dead XY.hi half of the own slot
+        for (int n = g; n < K; n += G) {
+          xylo[2 * slot(n) + 1] = xylo[2 * trev[n]];
+        }
+        __syncthreads();
+        for (int n = g; n < K; n += G) {
+          const int   sl = slot(n);
+          const short a1 = (short)(xylo[2 * sl + 1] - auxc[sl]);  // app1 -= ext1 (vec_sub, wraps)
+          auxc[sl]       = a1;
+          const short sx = S(n);
+          const short x  = SAT ? __builtin_elementwise_add_sat(sx, a1) : (short)(sx + a1);
+          xyc[sl]        = pack2(x, P0(n));
+        }
+      }
+      if constexpr (NSB == 1) {
+        if (g < 3) {
+          xyc[K + g] = pack2(st[g], p0t[g]);
+        }
+      }
+    } else {
+      for (int n = g; n < K; n += G) {  // ext1 -= app1 (h > 1), keep it in AUX
+        const int sl = slot(n);
+        const short e = xylo[2 * sl];
+        auxc[sl]      = h > 1 ? (short)(e - auxc[sl]) : e;
+      }
+      __syncthreads();
+      for (int n = g; n < K; n += G) {  // app2 = ext1 interleaved
+        xyc[slot(n)] = pack2(auxc[tfwd[n]], P1(n));
+      }
+      if constexpr (NSB == 1) {
+        if (g < 3) {
+          xyc[K + g] = pack2(x2t[g], p1t[g]);
+        }
+      }
+    }
+    __syncthreads();
+
+    // -------- constituent MAP decode --------
+    const bool dec1 = (h & 1) == 0;
+    map_decode<NSB>(sm, base, lane, j, s, K, L, Nb, La, M, dec1 ? st : x2t, dec1 ? p0t : p1t);
+    __syncthreads();
+  }
+
+  // -------- hard decision (turbodecoder.c:370-378) --------
+  const bool last_dec1 = ((a.n_end - 1) & 1) == 0;
+  if (live) {
+    uint8_t* out = a.out + (size_t)cb * (K / 8);
+    for (int b = g; b < K / 8; b += G) {
+      uint32_t byte = 0;
+#pragma unroll
+      for (int t = 0; t < 8; t++) {
+        const int   n = 8 * b + t;
+        const short v = last_dec1 ? xylo[2 * slot(n)] : xylo[2 * trev[n]];
+        byte |= (uint32_t)(v > 0) << (7 - t);
+      }
+      out[b] = (uint8_t)byte;
+    }
+    if (a.state) {
+      short* se = a.state + (size_t)cb * 2 * XYW;
+      for (int i = g; i < XYW; i += G) {
+        se[i]       = xylo[2 * i];
+        se[XYW + i] = auxc[i];
+      }
+    }
+  }
+}
+
+template <int NSB>
+static hipError_t launch(const TdecArgs& a, hipStream_t stream)
+{
+  const int    cpw  = Geo<NSB>::CPW;
+  const int    grid = (a.ncb + cpw - 1) / cpw;
+  const size_t lds  = tdec_lds_bytes(NSB, a.xyw, a.M);
+  hipLaunchKernelGGL(tdec_kernel<NSB>, dim3(grid), dim3(64), lds, stream, a);
+  return hipGetLastError();
+}
+
+hipError_t tdec_launch(int nsb, const TdecArgs& a, hipStream_t stream)
+{
+  if (a.ncb == 0) {
+    return hipSuccess;
+  }
+  switch (nsb) {
+    case 16:
+      return launch<16>(a, stream);
+    case 8:
+      return launch<8>(a, stream);
+    case 1:
+      return launch<1>(a, stream);
+    default:
+      return hipErrorInvalidValue;
+  }
+}
+
+size_t tdec_lds_bytes(int nsb, int xyw, int M)
+{
+  const int cpw = 64 / (4 * nsb);
+  return (size_t)cpw * xyw * 4 + (((size_t)cpw * xyw + 1) / 2) * 4 + (size_t)M * 64 * 4;
+}
+
+}  // namespace srsran_amd

@@ -115,7 +115,7 @@ def test_degenerate_inputs(ora, dec, K):
 def test_ragged_batches(ora, dec, ncb):
     """Batch sizes that leave partially filled waves (16 CBs/wave generic, 2/wave K<=800)."""
     rng = np.random.default_rng(ncb)
-    for K in (40, 520, 1088):
+    for K in (40, 528, 1088):
         llr = _inputs(ora, K, rng, ncb, True) if ncb > 1 else _inputs(ora, K, rng, 2, True)[:1]
         got = dec.run_all_batch(llr, 6, K)
         assert np.array_equal(got, ora.run_batch(K, llr, True, 6))

@@ -206,6 +206,85 @@ __device__ __forceinline__ bool alpha_norm_at(int t)
   }
 }
 
+// Backward window: positions p1-1 .. p0 (p1 - p0 <= W), storing the checkpoint
+// beta[p0] (pre-normalisation) into ck slot m-1 when m != 0.  FULL => p1 = p0 + W
+// and the loop is straight-line code with all LDS reads issued up front.
+template <int NSB, bool FULL>
+__device__ __forceinline__ v2s beta_window(v2s P, const uint32_t* xy, int p0, int p1, int m, int K, uint32_t* ck,
+                                           int lane, const LaneSel& ls)
+{
+  constexpr bool SAT = Geo<NSB>::SAT;
+  v2s            xw[W];
+#pragma unroll
+  for (int i = 0; i < W; i++) {
+    if (FULL || p0 + i < p1) {
+      xw[i] = u2v(xy[p0 + i]);
+    }
+  }
+#pragma unroll
+  for (int i = W - 1; i >= 0; i--) {
+    if (FULL || p0 + i < p1) {
+      P = beta_step<SAT>(P, xw[i], ls);
+      if (i == 0 && m != 0) {
+        ck[(m - 1) * 64 + lane] = v2u(P);  // stored (pre-normalisation) beta[mW]
+      }
+      if (beta_norm_at<NSB>(p0 + i, K)) {
+        P = norm<SAT>(P);
+      }
+    }
+  }
+  return P;
+}
+
+// Forward window m: recompute beta[t0+1 .. c] from checkpoint c into registers,
+// then alpha + LLR for t0 .. ta-1, writing the LLR into XY.lo.
+// FULL => c = ta = t0 + W (no guards).
+template <int NSB, bool FULL>
+__device__ __forceinline__ v2s alpha_window(v2s P, const uint32_t* xy, short* xyo, int t0, int c, int ta, int Nb,
+                                            int K, v2s ckv, const LaneSel& ls)
+{
+  constexpr bool SAT = Geo<NSB>::SAT;
+  v2s            xw[W];
+  v2s            bw[W];
+#pragma unroll
+  for (int i = 0; i < W; i++) {
+    if (FULL || t0 + i < c) {
+      xw[i] = u2v(xy[t0 + i]);
+    }
+  }
+  v2s       Pb = ckv;
+  const int ic = FULL ? W - 1 : c - t0 - 1;
+#pragma unroll
+  for (int i = W - 1; i >= 0; i--) {
+    if (i == ic) {
+      bw[i] = Pb;
+      if (c < Nb && beta_norm_at<NSB>(c, K)) {
+        Pb = norm<SAT>(Pb);
+      }
+    } else if (i < ic) {
+      Pb    = beta_step<SAT>(Pb, xw[i + 1], ls);
+      bw[i] = Pb;
+      if (beta_norm_at<NSB>(t0 + 1 + i, K)) {
+        Pb = norm<SAT>(Pb);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < W; i++) {
+    if (FULL || t0 + i < ta) {
+      v2s c0, c1;
+      alpha_cand<SAT>(P, xw[i], ls, c0, c1);
+      const short o = llr_out<SAT>(bw[i], c0, c1);
+      P             = pmax(c0, c1);
+      if (alpha_norm_at<NSB>(t0 + i)) {
+        P = norm<SAT>(P);
+      }
+      xyo[2 * (t0 + i)] = o;
+    }
+  }
+  return P;
+}
+
 // One constituent MAP decode for this quad's sub-block.  XY[base + k] holds the
 // branch inputs; the output LLR overwrites XY.lo.  Nb = length of the beta
 // recursion (L, or K+3 for the generic decoder), La = alpha length (L or K).
@@ -237,27 +316,14 @@ __device__ void map_decode(const Smem& sm, int base, int lane, int j, int s, int
     P = init_known(j);
   }
   sm.ck[(M - 1) * 64 + lane] = v2u(P);  // checkpoint M = beta[Nb]
-  for (int m = M - 1; m >= 0; m--) {    // windows [mW, min(mW+W, Nb)), descending
-    const int p0 = m * W;
-    const int p1 = min(p0 + W, Nb);
-    v2s       xw[W];
-#pragma unroll
-    for (int i = 0; i < W; i++) {
-      if (p0 + i < p1) {
-        xw[i] = u2v(xy[p0 + i]);
-      }
+  {
+    int m = M - 1;
+    if (Nb - m * W < W) {  // top window is partial
+      P = beta_window<NSB, false>(P, xy, m * W, Nb, m, K, sm.ck, lane, ls);
+      m--;
     }
-#pragma unroll
-    for (int i = W - 1; i >= 0; i--) {
-      if (p0 + i < p1) {
-        P = beta_step<SAT>(P, xw[i], ls);
-        if (i == 0 && m != 0) {
-          sm.ck[(m - 1) * 64 + lane] = v2u(P);  // stored (pre-normalisation) beta[mW]
-        }
-        if (beta_norm_at<NSB>(p0 + i, K)) {
-          P = norm<SAT>(P);
-        }
-      }
+    for (; m >= 0; m--) {
+      P = beta_window<NSB, true>(P, xy, m * W, m * W + W, m, K, sm.ck, lane, ls);
     }
   }
 
@@ -281,51 +347,12 @@ __device__ void map_decode(const Smem& sm, int base, int lane, int j, int s, int
 
   const int nwin = (La + W - 1) / W;
   for (int m = 0; m < nwin; m++) {
-    const int t0 = m * W;
-    const int c  = min(t0 + W, Nb);       // checkpoint position
-    const int ta = min(t0 + W, La);       // alpha end (exclusive)
-    v2s       xw[W];
-    v2s       bw[W];
-#pragma unroll
-    for (int i = 0; i < W; i++) {
-      if (t0 + i < c) {
-        xw[i] = u2v(xy[t0 + i]);
-      }
-    }
-    // recompute beta[t0+1 .. c] (bw[i] = beta[t0+1+i])
-    v2s Pb = u2v(sm.ck[m * 64 + lane]);
-    {
-      const int ic = c - t0 - 1;
-#pragma unroll
-      for (int i = W - 1; i >= 0; i--) {
-        if (i == ic) {
-          bw[i] = Pb;
-          if (c < Nb && beta_norm_at<NSB>(c, K)) {
-            Pb = norm<SAT>(Pb);
-          }
-        } else if (i < ic) {
-          const int pos = t0 + 1 + i;
-          Pb            = beta_step<SAT>(Pb, xw[i + 1], ls);
-          bw[i]         = Pb;
-          if (beta_norm_at<NSB>(pos, K)) {
-            Pb = norm<SAT>(Pb);
-          }
-        }
-      }
-    }
-    // alpha + LLR over t0 .. ta-1
-#pragma unroll
-    for (int i = 0; i < W; i++) {
-      if (t0 + i < ta) {
-        v2s c0, c1;
-        alpha_cand<SAT>(P, xw[i], ls, c0, c1);
-        const short o = llr_out<SAT>(bw[i], c0, c1);
-        P             = pmax(c0, c1);
-        if (alpha_norm_at<NSB>(t0 + i)) {
-          P = norm<SAT>(P);
-        }
-        xyo[2 * (t0 + i)] = o;
-      }
+    const int t0  = m * W;
+    const v2s ckv = u2v(sm.ck[m * 64 + lane]);
+    if (t0 + W <= La) {  // then also t0 + W <= Nb
+      P = alpha_window<NSB, true>(P, xy, xyo, t0, t0 + W, t0 + W, Nb, K, ckv, ls);
+    } else {
+      P = alpha_window<NSB, false>(P, xy, xyo, t0, min(t0 + W, Nb), La, Nb, K, ckv, ls);
     }
   }
 }

@@ -123,7 +123,14 @@ def main():
     stream = torch.cuda.current_stream(device)
     sp = stream.cuda_stream
 
+    groups = (list(Ks), [data[K][0].data_ptr() for K in Ks], [data[K][0].shape[1] for K in Ks],
+              [data[K][1].data_ptr() for K in Ks], [args.batch] * len(Ks))
+
     def step(events=None):
+        if events is None and len(Ks) > 1:
+            # one multi-size call: groups fan out over internal streams, joined back into `stream`
+            tdec.gpu_run_multi(groups[0], groups[1], groups[2], True, groups[3], groups[4], args.iters, sp)
+            return
         for K in Ks:
             d_in, d_out, _ = data[K]
             if events is not None:

@@ -121,6 +121,23 @@ int srsran_tdec_gpu_run_batch(uint32_t       long_cb,
                               uint32_t       nof_iterations,
                               void*          stream);
 
+/*
+ * Device-resident multi-size batch: nof_groups groups, group g = nof_cb[g] code
+ * blocks of size long_cb[g] at d_input[g] (in_stride[g] int16 apart) -> d_output[g].
+ * Groups are decoded concurrently on internal streams that fork from and join
+ * back into `stream` (no host synchronisation).  This is the shape of a DL-SCH
+ * transport block (K+ / K- code blocks, cbsegm.c:62-117) and of many TBs at once.
+ */
+int srsran_tdec_gpu_run_multi(uint32_t              nof_groups,
+                              const uint32_t*       long_cb,
+                              const int16_t* const* d_input,
+                              const uint32_t*       in_stride,
+                              int                   layout_sb,
+                              uint8_t* const*       d_output,
+                              const uint32_t*       nof_cb,
+                              uint32_t              nof_iterations,
+                              void*                 stream);
+
 /* 1 if a HIP device is usable, 0 otherwise (no kernel is launched). */
 int srsran_tdec_gpu_available(void);
 

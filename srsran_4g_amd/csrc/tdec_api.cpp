@@ -13,6 +13,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -482,6 +483,115 @@ int srsran_tdec_gpu_run_batch(uint32_t       long_cb,
   }
   const int n_end = nof_iterations > 0 ? (int)nof_iterations : 1;
   return enqueue(c, d_input, in_stride, layout_sb, d_output, nof_cb, 0, n_end, nullptr, (hipStream_t)stream);
+}
+
+namespace {
+// Internal fork/join stream pool for srsran_tdec_gpu_run_multi (per device).
+constexpr int kPoolStreams = 4;
+struct StreamPool {
+  int         device = -1;
+  hipStream_t s[kPoolStreams];
+  hipEvent_t  done[kPoolStreams];
+  hipEvent_t  fork;
+};
+std::mutex               g_pool_mu;
+std::vector<StreamPool*> g_pools;
+
+StreamPool* get_pool()
+{
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) {
+    return nullptr;
+  }
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  for (auto* p : g_pools) {
+    if (p->device == dev) {
+      return p;
+    }
+  }
+  StreamPool* p = new StreamPool();
+  p->device     = dev;
+  for (int i = 0; i < kPoolStreams; i++) {
+    if (hipStreamCreateWithFlags(&p->s[i], hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&p->done[i], hipEventDisableTiming) != hipSuccess) {
+      return nullptr;
+    }
+  }
+  if (hipEventCreateWithFlags(&p->fork, hipEventDisableTiming) != hipSuccess) {
+    return nullptr;
+  }
+  g_pools.push_back(p);
+  return p;
+}
+
+// Rough serial-latency model used only to order launches (longest first).
+double launch_cost(uint32_t K, uint32_t ncb)
+{
+  const int    nsb   = auto_nsb(K);
+  const double chain = nsb > 1 ? 3.0 * (K / nsb) + 160.0 : 3.0 * (K + 3);
+  const double waves = (double)ncb * 4 * nsb / 64.0;
+  return chain * (1.0 + waves / 1024.0);
+}
+}  // namespace
+
+int srsran_tdec_gpu_run_multi(uint32_t              nof_groups,
+                              const uint32_t*       long_cb,
+                              const int16_t* const* d_input,
+                              const uint32_t*       in_stride,
+                              int                   layout_sb,
+                              uint8_t* const*       d_output,
+                              const uint32_t*       nof_cb,
+                              uint32_t              nof_iterations,
+                              void*                 stream)
+{
+  if (nof_groups == 0) {
+    return SRSRAN_SUCCESS;
+  }
+  if (!long_cb || !d_input || !in_stride || !d_output || !nof_cb) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  std::vector<Config*>  cfg(nof_groups);
+  std::vector<uint32_t> order(nof_groups);
+  for (uint32_t g = 0; g < nof_groups; g++) {
+    if (cb_index(long_cb[g]) < 0 || !d_input[g] || !d_output[g]) {
+      return SRSRAN_ERROR_INVALID_INPUTS;
+    }
+    cfg[g] = get_config(long_cb[g], auto_nsb(long_cb[g]));
+    if (!cfg[g]) {
+      return SRSRAN_ERROR;
+    }
+    const uint32_t len = (layout_sb && cfg[g]->nsb > 1) ? 3 * (long_cb[g] + 32) + 12 : 3 * long_cb[g] + 12;
+    if (in_stride[g] < len) {
+      return SRSRAN_ERROR_INVALID_INPUTS;
+    }
+    order[g] = g;
+  }
+  std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+    return launch_cost(long_cb[a], nof_cb[a]) > launch_cost(long_cb[b], nof_cb[b]);
+  });
+  StreamPool* p = get_pool();
+  if (!p) {
+    return SRSRAN_ERROR;
+  }
+  hipStream_t user = (hipStream_t)stream;
+  if (hipEventRecord(p->fork, user) != hipSuccess) {
+    return SRSRAN_ERROR;
+  }
+  for (int i = 0; i < kPoolStreams; i++) {
+    hipStreamWaitEvent(p->s[i], p->fork, 0);
+  }
+  const int n_end = nof_iterations > 0 ? (int)nof_iterations : 1;
+  int       ret   = SRSRAN_SUCCESS;
+  for (uint32_t i = 0; i < nof_groups && ret == SRSRAN_SUCCESS; i++) {
+    const uint32_t g = order[i];
+    ret = enqueue(cfg[g], d_input[g], in_stride[g], layout_sb, d_output[g], nof_cb[g], 0, n_end, nullptr,
+                  p->s[i % kPoolStreams]);
+  }
+  for (int i = 0; i < kPoolStreams; i++) {
+    hipEventRecord(p->done[i], p->s[i]);
+    hipStreamWaitEvent(user, p->done[i], 0);
+  }
+  return ret;
 }
 
 void srsran_tdec_iteration_8bit(srsran_tdec_t* h, int8_t* input, uint8_t* output)

@@ -82,6 +82,9 @@ def load_library():
         "srsran_tdec_run_all_batch": ([P, _i16p, u32, _u8p, u32, u32, u32], ctypes.c_int),
         "srsran_tdec_gpu_run_batch": ([u32, ctypes.c_void_p, u32, ctypes.c_int, ctypes.c_void_p, u32, u32,
                                        ctypes.c_void_p], ctypes.c_int),
+        "srsran_tdec_gpu_run_multi": ([u32, ctypes.POINTER(u32), ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(u32),
+                                       ctypes.c_int, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(u32), u32,
+                                       ctypes.c_void_p], ctypes.c_int),
         "srsran_tdec_gpu_available": ([], ctypes.c_int),
         "srsran_tdec_gpu_kernel_name": ([u32], ctypes.c_char_p),
     }
@@ -175,3 +178,15 @@ def gpu_run_batch(K, d_in, in_stride, layout_sb, d_out, nof_cb, nof_iterations, 
                                                   nof_iterations, stream)
     if rc != SRSRAN_SUCCESS:
         raise RuntimeError(f"srsran_tdec_gpu_run_batch failed ({rc})")
+
+
+def gpu_run_multi(Ks, d_ins, strides, layout_sb, d_outs, ncbs, nof_iterations, stream=None):
+    """Device-resident multi-size batch (srsran_tdec_gpu_run_multi): one group per code-block size."""
+    n = len(Ks)
+    u32 = ctypes.c_uint32
+    vp = ctypes.c_void_p
+    rc = load_library().srsran_tdec_gpu_run_multi(
+        n, (u32 * n)(*Ks), (vp * n)(*d_ins), (u32 * n)(*strides), int(bool(layout_sb)), (vp * n)(*d_outs),
+        (u32 * n)(*ncbs), nof_iterations, stream)
+    if rc != SRSRAN_SUCCESS:
+        raise RuntimeError(f"srsran_tdec_gpu_run_multi failed ({rc})")

@@ -131,6 +131,26 @@ def test_invalid_sizes(dec):
     assert dec.new_cb(6145) != 0
 
 
+def test_gpu_run_multi_mixed_sizes(ora):
+    """srsran_tdec_gpu_run_multi: several sizes decoded concurrently, joined into one stream."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(77)
+    Ks = [40, 400, 408, 800, 816, 5824, 6144, 1056]
+    ncbs = [17, 5, 3, 64, 9, 13, 2, 33]
+    ins, outs, want = [], [], []
+    for K, n in zip(Ks, ncbs):
+        llr = _inputs(ora, K, rng, n, True)
+        ins.append(torch.from_numpy(llr).cuda())
+        outs.append(torch.zeros((n, K // 8), dtype=torch.uint8, device="cuda"))
+        want.append(ora.run_batch(K, llr, True, 8))
+    stream = torch.cuda.current_stream().cuda_stream
+    tdec.gpu_run_multi(Ks, [t.data_ptr() for t in ins], [t.shape[1] for t in ins], True,
+                       [t.data_ptr() for t in outs], ncbs, 8, stream)
+    torch.cuda.current_stream().synchronize()
+    for K, o, w in zip(Ks, outs, want):
+        assert np.array_equal(o.cpu().numpy(), w), K
+
+
 def test_config1_full_batch(ora):
     """BASELINE config 1/2 shape: K=6144 x 1024 CBs, 8 half-iterations, AWGN, device-resident."""
     torch = pytest.importorskip("torch")

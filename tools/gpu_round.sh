@@ -13,5 +13,5 @@ timeout -k 10 300 python bench.py --workload k6144 --steps 20 --warmup 3 --cpu-s
 cat $OUT/bench_k6144.json
 timeout -k 10 400 python bench.py --steps 5 --warmup 2 --cpu-seconds 10 > $OUT/bench_all188.json 2> $OUT/bench_all188.err || exit 1
 cat $OUT/bench_all188.json
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o k6144 -- python3 bench.py --workload k6144 --steps 20 --warmup 3 --cpu-seconds 0 > $OUT/prof_stdout.log 2>&1 || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o k6144 -- python3 bench.py --workload k6144 --steps 20 --warmup 3 --cpu-seconds 0 > $OUT/prof_stdout.log 2>&1 || exit 1
 find $OUT/prof -name "*stats*" | head; 

@@ -206,12 +206,25 @@ __device__ __forceinline__ bool alpha_norm_at(int t)
   }
 }
 
-// Backward window: positions p1-1 .. p0 (p1 - p0 <= W), storing the checkpoint
-// beta[p0] (pre-normalisation) into ck slot m-1 when m != 0.  FULL => p1 = p0 + W
-// and the loop is straight-line code with all LDS reads issued up front.
+// Schedule of one constituent decode ("crossover"): with Mb = ceil(Nb/W) beta
+// windows and Ma = ceil(La/W) alpha windows and split h,
+//   phase 1: alpha forward over windows [0, h)      || beta backward over [h, Mb)
+//            (alpha checkpoints ckA[m] = state entering window m, slots 0..h-1;
+//             beta checkpoints ckB[m] = stored beta[mW] for m > h, slots m-1)
+//   phase 2: alpha forward over windows [h, Ma)      || beta backward over [0, h)
+//            each side recomputes the other direction's metrics for the window
+//            from a checkpoint and emits the LLRs of its positions.
+// The two directions are independent dependency chains, interleaved in one
+// instruction stream.  Every (position, state) value is computed with the
+// reference's arithmetic, so the output is bit-identical to the sequential
+// beta-then-alpha order of turbodecoder_win.h / turbodecoder_gen.c.
+
+// Backward window over positions p1-1 .. p0 (FULL => p1 = p0 + W).  Stores the
+// stored (pre-normalisation) beta[p0] into slot m-1 when store_ck, and returns it
+// in `stored`.
 template <int NSB, bool FULL>
-__device__ __forceinline__ v2s beta_window(v2s P, const uint32_t* xy, int p0, int p1, int m, int K, uint32_t* ck,
-                                           int lane, const LaneSel& ls)
+__device__ __forceinline__ v2s beta_window(v2s P, const uint32_t* xy, int p0, int p1, int m, bool store_ck, int K,
+                                           uint32_t* ck, int lane, const LaneSel& ls, v2s& stored)
 {
   constexpr bool SAT = Geo<NSB>::SAT;
   v2s            xw[W];
@@ -225,8 +238,11 @@ __device__ __forceinline__ v2s beta_window(v2s P, const uint32_t* xy, int p0, in
   for (int i = W - 1; i >= 0; i--) {
     if (FULL || p0 + i < p1) {
       P = beta_step<SAT>(P, xw[i], ls);
-      if (i == 0 && m != 0) {
-        ck[(m - 1) * 64 + lane] = v2u(P);  // stored (pre-normalisation) beta[mW]
+      if (i == 0) {
+        stored = P;
+        if (store_ck) {
+          ck[(m - 1) * 64 + lane] = v2u(P);
+        }
       }
       if (beta_norm_at<NSB>(p0 + i, K)) {
         P = norm<SAT>(P);
@@ -236,9 +252,69 @@ __device__ __forceinline__ v2s beta_window(v2s P, const uint32_t* xy, int p0, in
   return P;
 }
 
-// Forward window m: recompute beta[t0+1 .. c] from checkpoint c into registers,
-// then alpha + LLR for t0 .. ta-1, writing the LLR into XY.lo.
-// FULL => c = ta = t0 + W (no guards).
+// Phase-1 pair: a full alpha window at ta0 (no LLR; checkpoint = entry state in
+// slot ma) interleaved with a full beta window at pb0 = mb*W.
+template <int NSB>
+__device__ __forceinline__ void phase1_pair(v2s& Pa, v2s& Pb, v2s& Bst, const uint32_t* xy, int ta0, int ma, int mb,
+                                            bool store_ckb, int K, uint32_t* ck, int lane, const LaneSel& ls)
+{
+  constexpr bool SAT = Geo<NSB>::SAT;
+  const int      pb0 = mb * W;
+  v2s            xa[W], xb[W];
+#pragma unroll
+  for (int i = 0; i < W; i++) {
+    xa[i] = u2v(xy[ta0 + i]);
+    xb[i] = u2v(xy[pb0 + i]);
+  }
+  ck[ma * 64 + lane] = v2u(Pa);
+#pragma unroll
+  for (int i = 0; i < W; i++) {
+    v2s c0, c1;
+    alpha_cand<SAT>(Pa, xa[i], ls, c0, c1);
+    Pa = pmax(c0, c1);
+    if (alpha_norm_at<NSB>(ta0 + i)) {
+      Pa = norm<SAT>(Pa);
+    }
+    const int ib = W - 1 - i;
+    Pb           = beta_step<SAT>(Pb, xb[ib], ls);
+    if (ib == 0) {
+      Bst = Pb;
+      if (store_ckb) {
+        ck[(mb - 1) * 64 + lane] = v2u(Pb);
+      }
+    }
+    if (beta_norm_at<NSB>(pb0 + ib, K)) {
+      Pb = norm<SAT>(Pb);
+    }
+  }
+}
+
+// Phase-1 alpha-only window (entry checkpoint in slot ma).
+template <int NSB>
+__device__ __forceinline__ v2s alpha_fw_window(v2s P, const uint32_t* xy, int t0, int ma, uint32_t* ck, int lane,
+                                               const LaneSel& ls)
+{
+  constexpr bool SAT = Geo<NSB>::SAT;
+  v2s            xw[W];
+#pragma unroll
+  for (int i = 0; i < W; i++) {
+    xw[i] = u2v(xy[t0 + i]);
+  }
+  ck[ma * 64 + lane] = v2u(P);
+#pragma unroll
+  for (int i = 0; i < W; i++) {
+    v2s c0, c1;
+    alpha_cand<SAT>(P, xw[i], ls, c0, c1);
+    P = pmax(c0, c1);
+    if (alpha_norm_at<NSB>(t0 + i)) {
+      P = norm<SAT>(P);
+    }
+  }
+  return P;
+}
+
+// Phase-2 alpha side, window at t0: recompute beta[t0+1 .. c] from checkpoint c
+// into registers, then alpha + LLR for t0 .. ta-1 (FULL => c = ta = t0 + W).
 template <int NSB, bool FULL>
 __device__ __forceinline__ v2s alpha_window(v2s P, const uint32_t* xy, short* xyo, int t0, int c, int ta, int Nb,
                                             int K, v2s ckv, const LaneSel& ls)
@@ -285,6 +361,45 @@ __device__ __forceinline__ v2s alpha_window(v2s P, const uint32_t* xy, short* xy
   return P;
 }
 
+// Phase-2 beta side, full window at t0: recompute alpha[t0 .. t0+W-1] from the
+// entry checkpoint, then beta backward with the LLR of every position.  Bst is
+// the stored (pre-normalisation) beta of the position above the window.
+template <int NSB>
+__device__ __forceinline__ v2s beta_llr_window(v2s P, v2s& Bst, const uint32_t* xy, short* xyo, int t0, int K,
+                                               v2s cka, const LaneSel& ls)
+{
+  constexpr bool SAT = Geo<NSB>::SAT;
+  v2s            xw[W];
+  v2s            aw[W];
+#pragma unroll
+  for (int i = 0; i < W; i++) {
+    xw[i] = u2v(xy[t0 + i]);
+  }
+  aw[0] = cka;
+#pragma unroll
+  for (int i = 0; i < W - 1; i++) {
+    v2s c0, c1;
+    alpha_cand<SAT>(aw[i], xw[i], ls, c0, c1);
+    v2s a = pmax(c0, c1);
+    if (alpha_norm_at<NSB>(t0 + i)) {
+      a = norm<SAT>(a);
+    }
+    aw[i + 1] = a;
+  }
+#pragma unroll
+  for (int i = W - 1; i >= 0; i--) {
+    v2s c0, c1;
+    alpha_cand<SAT>(aw[i], xw[i], ls, c0, c1);
+    xyo[2 * (t0 + i)] = llr_out<SAT>(Bst, c0, c1);
+    P                 = beta_step<SAT>(P, xw[i], ls);
+    Bst               = P;
+    if (beta_norm_at<NSB>(t0 + i, K)) {
+      P = norm<SAT>(P);
+    }
+  }
+  return P;
+}
+
 // One constituent MAP decode for this quad's sub-block.  XY[base + k] holds the
 // branch inputs; the output LLR overwrites XY.lo.  Nb = length of the beta
 // recursion (L, or K+3 for the generic decoder), La = alpha length (L or K).
@@ -296,64 +411,86 @@ __device__ void map_decode(const Smem& sm, int base, int lane, int j, int s, int
   const LaneSel  ls  = lane_sel(j);
   const uint32_t* xy = sm.xy + base;
   short*          xyo = reinterpret_cast<short*>(sm.xy + base);
+  uint32_t*       ck  = sm.ck;
 
-  // ---------------- backward (beta) pass ----------------
-  v2s P;
+  // ---- initial states: window-boundary training (win.h:566-630, 705-756) ----
+  v2s Pa, Pb;
   if constexpr (NSB > 1) {
-    // training over the first OVERLAP steps of the own sub-block (win.h:622-630)
-    P = v2s{NEGINF, NEGINF};
-#pragma unroll
-    for (int k = OVERLAP - 1; k >= 0; k--) {
-      P = beta_step<SAT>(P, u2v(xy[k]), ls);
-      if (beta_norm_at<NSB>(k, K)) {
-        P = norm<SAT>(P);
-      }
-    }
-    // sub-block s starts from s+1's training state, the last from the tail (win.h:577-620)
-    const v2s nxt = u2v((uint32_t)__shfl_down((int)v2u(P), 4, 64));
-    P             = (s == NSB - 1) ? trellis_pair(xt, yt, j) : nxt;
-  } else {
-    P = init_known(j);
-  }
-  sm.ck[(M - 1) * 64 + lane] = v2u(P);  // checkpoint M = beta[Nb]
-  {
-    int m = M - 1;
-    if (Nb - m * W < W) {  // top window is partial
-      P = beta_window<NSB, false>(P, xy, m * W, Nb, m, K, sm.ck, lane, ls);
-      m--;
-    }
-    for (; m >= 0; m--) {
-      P = beta_window<NSB, true>(P, xy, m * W, m * W + W, m, K, sm.ck, lane, ls);
-    }
-  }
-
-  // ---------------- forward (alpha) pass ----------------
-  if constexpr (NSB > 1) {
-    P = v2s{NEGINF, NEGINF};
+    Pa = v2s{NEGINF, NEGINF};
+    Pb = v2s{NEGINF, NEGINF};
 #pragma unroll
     for (int k = 0; k < OVERLAP; k++) {
-      v2s c0, c1;
-      alpha_cand<SAT>(P, u2v(xy[L - OVERLAP + k]), ls, c0, c1);
-      P = pmax(c0, c1);
+      const int kb = OVERLAP - 1 - k;  // beta trains over the first 40 steps, backwards
+      Pb           = beta_step<SAT>(Pb, u2v(xy[kb]), ls);
+      if (beta_norm_at<NSB>(kb, K)) {
+        Pb = norm<SAT>(Pb);
+      }
+      v2s c0, c1;  // alpha trains over the last 40 steps, forwards
+      alpha_cand<SAT>(Pa, u2v(xy[L - OVERLAP + k]), ls, c0, c1);
+      Pa = pmax(c0, c1);
       if (alpha_norm_at<NSB>(k)) {
-        P = norm<SAT>(P);
+        Pa = norm<SAT>(Pa);
       }
     }
-    const v2s prv = u2v((uint32_t)__shfl_up((int)v2u(P), 4, 64));
-    P             = (s == 0) ? init_known(j) : prv;
+    // move_right / move_left: sub-block s starts from s+1's beta / s-1's alpha
+    const v2s nxt = u2v((uint32_t)__shfl_down((int)v2u(Pb), 4, 64));
+    const v2s prv = u2v((uint32_t)__shfl_up((int)v2u(Pa), 4, 64));
+    Pb            = (s == NSB - 1) ? trellis_pair(xt, yt, j) : nxt;
+    Pa            = (s == 0) ? init_known(j) : prv;
   } else {
-    P = init_known(j);
+    Pa = init_known(j);
+    Pb = init_known(j);
   }
 
-  const int nwin = (La + W - 1) / W;
-  for (int m = 0; m < nwin; m++) {
-    const int t0  = m * W;
-    const v2s ckv = u2v(sm.ck[m * 64 + lane]);
-    if (t0 + W <= La) {  // then also t0 + W <= Nb
-      P = alpha_window<NSB, true>(P, xy, xyo, t0, t0 + W, t0 + W, Nb, K, ckv, ls);
+  const int Mb = M;
+  const int Ma = (La + W - 1) / W;
+  const int h  = max(1, min((Nb + W) / (2 * W), La / W));
+
+  // ---- phase 1 ----
+  ck[(Mb - 1) * 64 + lane] = v2u(Pb);  // ckB[Mb] = beta[Nb] (slot Mb-1 > h-1 since Mb > h)
+  v2s Bst                  = Pb;       // stored beta of the lowest processed position
+  int mb                   = Mb - 1;
+  int ma                   = 0;
+  if (Nb - mb * W < W) {  // partial top beta window
+    Pb = beta_window<NSB, false>(Pb, xy, mb * W, Nb, mb, mb > h, K, ck, lane, ls, Bst);
+    mb--;
+  }
+  for (; ma < h && mb >= h; ma++, mb--) {
+    phase1_pair<NSB>(Pa, Pb, Bst, xy, ma * W, ma, mb, mb > h, K, ck, lane, ls);
+  }
+  for (; ma < h; ma++) {
+    Pa = alpha_fw_window<NSB>(Pa, xy, ma * W, ma, ck, lane, ls);
+  }
+  for (; mb >= h; mb--) {
+    Pb = beta_window<NSB, true>(Pb, xy, mb * W, mb * W + W, mb, mb > h, K, ck, lane, ls, Bst);
+  }
+
+  // ---- phase 2 ----
+  ma = h;
+  mb = h - 1;
+  for (; ma < Ma && mb >= 0; ma++, mb--) {
+    const int t0 = ma * W;
+    if (t0 + W <= La) {
+      const v2s ckb = u2v(ck[ma * 64 + lane]);
+      const v2s cka = u2v(ck[mb * 64 + lane]);
+      Pa            = alpha_window<NSB, true>(Pa, xy, xyo, t0, t0 + W, t0 + W, Nb, K, ckb, ls);
+      Pb            = beta_llr_window<NSB>(Pb, Bst, xy, xyo, mb * W, K, cka, ls);
     } else {
-      P = alpha_window<NSB, false>(P, xy, xyo, t0, min(t0 + W, Nb), La, Nb, K, ckv, ls);
+      break;
     }
+  }
+  for (; ma < Ma; ma++) {
+    const int t0  = ma * W;
+    const v2s ckb = u2v(ck[ma * 64 + lane]);
+    if (t0 + W <= La) {
+      Pa = alpha_window<NSB, true>(Pa, xy, xyo, t0, t0 + W, t0 + W, Nb, K, ckb, ls);
+    } else {
+      Pa = alpha_window<NSB, false>(Pa, xy, xyo, t0, min(t0 + W, Nb), La, Nb, K, ckb, ls);
+    }
+  }
+  for (; mb >= 0; mb--) {
+    const v2s cka = u2v(ck[mb * 64 + lane]);
+    Pb            = beta_llr_window<NSB>(Pb, Bst, xy, xyo, mb * W, K, cka, ls);
   }
 }
 

@@ -137,9 +137,11 @@ Config* get_config(uint32_t K, int nsb)
   auto slot = [&](uint32_t n) -> uint16_t {
     return nsb > 1 ? (uint16_t)((n / a.L) * a.Ls + n % a.L) : (uint16_t)n;
   };
-  for (uint32_t n = 0; n < K; n++) {
-    tf[n] = slot(fwd[n]);
-    tr[n] = slot(rev[n]);
+  // indexed in the kernel's visiting order q (rm_turbo SB order for window decoders)
+  for (uint32_t q = 0; q < K; q++) {
+    const uint32_t n = nsb > 1 ? (q % nsb) * a.L + q / nsb : q;
+    tf[q]            = slot(fwd[n]);
+    tr[q]            = slot(rev[n]);
   }
   Config* c = new Config();
   c->nsb    = nsb;

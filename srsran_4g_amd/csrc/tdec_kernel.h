@@ -19,8 +19,8 @@ struct TdecArgs {
   int             n_start;   // first half-iteration index to run
   int             n_end;     // one past the last half-iteration index
   uint8_t*        out;       // ncb * K/8 hard-decision bytes (device)
-  const uint16_t* tfwd;      // slot of pi(n)       (device, K entries)
-  const uint16_t* trev;      // slot of pi^-1(n)    (device, K entries)
+  const uint16_t* tfwd;      // slot of pi(n(q))    (device, K entries, q order)
+  const uint16_t* trev;      // slot of pi^-1(n(q)) (device, K entries, q order)
   short*          state;     // optional ncb * 2 * xyw saved LLR/AUX state (device) or nullptr
   uint32_t        L;         // sub-block length (K for the generic decoder)
   uint32_t        Ls;        // LDS slot stride per sub-block

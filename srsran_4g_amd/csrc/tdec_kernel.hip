@@ -6,7 +6,7 @@
 //   K >= 816           16-sub-block sliding window, saturating (turbodecoder_win.h, AVX16)
 // dispatch: turbodecoder.c:381-408; half-iteration driver: turbodecoder_iter.h:72-144.
 //
-// Mapping (one wave64 per workgroup):
+// Mapping (two wave64 per workgroup, wave 0 = alpha side, wave 1 = beta side):
 //   * a code block's sub-block s is served by a QUAD of lanes; lane j of the quad
 //     holds trellis states (2j, 2j+1) packed as two int16 in one VGPR.  Each trellis
 //     step is ~6 packed VALU ops per lane: two DPP quad_perm reads fetch the source
@@ -252,43 +252,6 @@ __device__ __forceinline__ v2s beta_window(v2s P, const uint32_t* xy, int p0, in
   return P;
 }
 
-// Phase-1 pair: a full alpha window at ta0 (no LLR; checkpoint = entry state in
-// slot ma) interleaved with a full beta window at pb0 = mb*W.
-template <int NSB>
-__device__ __forceinline__ void phase1_pair(v2s& Pa, v2s& Pb, v2s& Bst, const uint32_t* xy, int ta0, int ma, int mb,
-                                            bool store_ckb, int K, uint32_t* ck, int lane, const LaneSel& ls)
-{
-  constexpr bool SAT = Geo<NSB>::SAT;
-  const int      pb0 = mb * W;
-  v2s            xa[W], xb[W];
-#pragma unroll
-  for (int i = 0; i < W; i++) {
-    xa[i] = u2v(xy[ta0 + i]);
-    xb[i] = u2v(xy[pb0 + i]);
-  }
-  ck[ma * 64 + lane] = v2u(Pa);
-#pragma unroll
-  for (int i = 0; i < W; i++) {
-    v2s c0, c1;
-    alpha_cand<SAT>(Pa, xa[i], ls, c0, c1);
-    Pa = pmax(c0, c1);
-    if (alpha_norm_at<NSB>(ta0 + i)) {
-      Pa = norm<SAT>(Pa);
-    }
-    const int ib = W - 1 - i;
-    Pb           = beta_step<SAT>(Pb, xb[ib], ls);
-    if (ib == 0) {
-      Bst = Pb;
-      if (store_ckb) {
-        ck[(mb - 1) * 64 + lane] = v2u(Pb);
-      }
-    }
-    if (beta_norm_at<NSB>(pb0 + ib, K)) {
-      Pb = norm<SAT>(Pb);
-    }
-  }
-}
-
 // Phase-1 alpha-only window (entry checkpoint in slot ma).
 template <int NSB>
 __device__ __forceinline__ v2s alpha_fw_window(v2s P, const uint32_t* xy, int t0, int ma, uint32_t* ck, int lane,
@@ -400,97 +363,88 @@ __device__ __forceinline__ v2s beta_llr_window(v2s P, v2s& Bst, const uint32_t* 
   return P;
 }
 
-// One constituent MAP decode for this quad's sub-block.  XY[base + k] holds the
-// branch inputs; the output LLR overwrites XY.lo.  Nb = length of the beta
-// recursion (L, or K+3 for the generic decoder), La = alpha length (L or K).
+// One constituent MAP decode for this quad's sub-block, split over the two waves
+// of the workgroup: wave 0 runs the alpha side, wave 1 the beta side of the
+// crossover schedule; they meet only through the checkpoints, one barrier per
+// phase.  XY[base + k] holds the branch inputs; the output LLR overwrites XY.lo.
+// Nb = length of the beta recursion (L, or K+3 for the generic decoder), La =
+// alpha length (L or K), M = Mb = beta checkpoints.  Both waves reach the same
+// barriers.
 template <int NSB>
-__device__ void map_decode(const Smem& sm, int base, int lane, int j, int s, int K, int L, int Nb, int La, int M,
-                           const short* xt, const short* yt)
+__device__ void map_decode(const Smem& sm, int base, int wave, int lane, int j, int s, int K, int L, int Nb, int La,
+                           int M, const short* xt, const short* yt)
 {
   constexpr bool SAT = Geo<NSB>::SAT;
   const LaneSel  ls  = lane_sel(j);
   const uint32_t* xy = sm.xy + base;
   short*          xyo = reinterpret_cast<short*>(sm.xy + base);
   uint32_t*       ck  = sm.ck;
+  const int       Mb  = M;
+  const int       Ma  = (La + W - 1) / W;
+  const int       h   = max(1, min((Nb + W) / (2 * W), La / W));
 
-  // ---- initial states: window-boundary training (win.h:566-630, 705-756) ----
-  v2s Pa, Pb;
-  if constexpr (NSB > 1) {
-    Pa = v2s{NEGINF, NEGINF};
-    Pb = v2s{NEGINF, NEGINF};
+  if (wave == 0) {
+    // ---------------- alpha side ----------------
+    v2s P = init_known(j);
+    if constexpr (NSB > 1) {
+      // training over the last 40 steps of the own sub-block (win.h:747-756)
+      P = v2s{NEGINF, NEGINF};
 #pragma unroll
-    for (int k = 0; k < OVERLAP; k++) {
-      const int kb = OVERLAP - 1 - k;  // beta trains over the first 40 steps, backwards
-      Pb           = beta_step<SAT>(Pb, u2v(xy[kb]), ls);
-      if (beta_norm_at<NSB>(kb, K)) {
-        Pb = norm<SAT>(Pb);
+      for (int k = 0; k < OVERLAP; k++) {
+        v2s c0, c1;
+        alpha_cand<SAT>(P, u2v(xy[L - OVERLAP + k]), ls, c0, c1);
+        P = pmax(c0, c1);
+        if (alpha_norm_at<NSB>(k)) {
+          P = norm<SAT>(P);
+        }
       }
-      v2s c0, c1;  // alpha trains over the last 40 steps, forwards
-      alpha_cand<SAT>(Pa, u2v(xy[L - OVERLAP + k]), ls, c0, c1);
-      Pa = pmax(c0, c1);
-      if (alpha_norm_at<NSB>(k)) {
-        Pa = norm<SAT>(Pa);
-      }
+      const v2s prv = u2v((uint32_t)__shfl_up((int)v2u(P), 4, 64));  // move_left
+      P             = (s == 0) ? init_known(j) : prv;
     }
-    // move_right / move_left: sub-block s starts from s+1's beta / s-1's alpha
-    const v2s nxt = u2v((uint32_t)__shfl_down((int)v2u(Pb), 4, 64));
-    const v2s prv = u2v((uint32_t)__shfl_up((int)v2u(Pa), 4, 64));
-    Pb            = (s == NSB - 1) ? trellis_pair(xt, yt, j) : nxt;
-    Pa            = (s == 0) ? init_known(j) : prv;
-  } else {
-    Pa = init_known(j);
-    Pb = init_known(j);
-  }
-
-  const int Mb = M;
-  const int Ma = (La + W - 1) / W;
-  const int h  = max(1, min((Nb + W) / (2 * W), La / W));
-
-  // ---- phase 1 ----
-  ck[(Mb - 1) * 64 + lane] = v2u(Pb);  // ckB[Mb] = beta[Nb] (slot Mb-1 > h-1 since Mb > h)
-  v2s Bst                  = Pb;       // stored beta of the lowest processed position
-  int mb                   = Mb - 1;
-  int ma                   = 0;
-  if (Nb - mb * W < W) {  // partial top beta window
-    Pb = beta_window<NSB, false>(Pb, xy, mb * W, Nb, mb, mb > h, K, ck, lane, ls, Bst);
-    mb--;
-  }
-  for (; ma < h && mb >= h; ma++, mb--) {
-    phase1_pair<NSB>(Pa, Pb, Bst, xy, ma * W, ma, mb, mb > h, K, ck, lane, ls);
-  }
-  for (; ma < h; ma++) {
-    Pa = alpha_fw_window<NSB>(Pa, xy, ma * W, ma, ck, lane, ls);
-  }
-  for (; mb >= h; mb--) {
-    Pb = beta_window<NSB, true>(Pb, xy, mb * W, mb * W + W, mb, mb > h, K, ck, lane, ls, Bst);
-  }
-
-  // ---- phase 2 ----
-  ma = h;
-  mb = h - 1;
-  for (; ma < Ma && mb >= 0; ma++, mb--) {
-    const int t0 = ma * W;
-    if (t0 + W <= La) {
+    for (int ma = 0; ma < h; ma++) {  // phase 1: windows [0, h), entry checkpoints in slots 0..h-1
+      P = alpha_fw_window<NSB>(P, xy, ma * W, ma, ck, lane, ls);
+    }
+    __syncthreads();
+    for (int ma = h; ma < Ma; ma++) {  // phase 2: windows [h, Ma) with beta recompute + LLR
+      const int t0  = ma * W;
       const v2s ckb = u2v(ck[ma * 64 + lane]);
+      if (t0 + W <= La) {
+        P = alpha_window<NSB, true>(P, xy, xyo, t0, t0 + W, t0 + W, Nb, K, ckb, ls);
+      } else {
+        P = alpha_window<NSB, false>(P, xy, xyo, t0, min(t0 + W, Nb), La, Nb, K, ckb, ls);
+      }
+    }
+  } else {
+    // ---------------- beta side ----------------
+    v2s P = init_known(j);
+    if constexpr (NSB > 1) {
+      // training over the first 40 steps of the own sub-block (win.h:622-630)
+      P = v2s{NEGINF, NEGINF};
+#pragma unroll
+      for (int k = OVERLAP - 1; k >= 0; k--) {
+        P = beta_step<SAT>(P, u2v(xy[k]), ls);
+        if (beta_norm_at<NSB>(k, K)) {
+          P = norm<SAT>(P);
+        }
+      }
+      const v2s nxt = u2v((uint32_t)__shfl_down((int)v2u(P), 4, 64));  // move_right
+      P             = (s == NSB - 1) ? trellis_pair(xt, yt, j) : nxt;   // last sub-block: tail trellis
+    }
+    ck[(Mb - 1) * 64 + lane] = v2u(P);  // ckB[Mb] = beta[Nb]
+    v2s Bst                  = P;
+    int mb                   = Mb - 1;
+    if (Nb - mb * W < W) {  // partial top window
+      P = beta_window<NSB, false>(P, xy, mb * W, Nb, mb, mb > h, K, ck, lane, ls, Bst);
+      mb--;
+    }
+    for (; mb >= h; mb--) {  // phase 1: windows [h, Mb), checkpoints in slots h..Mb-1
+      P = beta_window<NSB, true>(P, xy, mb * W, mb * W + W, mb, mb > h, K, ck, lane, ls, Bst);
+    }
+    __syncthreads();
+    for (mb = h - 1; mb >= 0; mb--) {  // phase 2: windows [0, h) with alpha recompute + LLR
       const v2s cka = u2v(ck[mb * 64 + lane]);
-      Pa            = alpha_window<NSB, true>(Pa, xy, xyo, t0, t0 + W, t0 + W, Nb, K, ckb, ls);
-      Pb            = beta_llr_window<NSB>(Pb, Bst, xy, xyo, mb * W, K, cka, ls);
-    } else {
-      break;
+      P             = beta_llr_window<NSB>(P, Bst, xy, xyo, mb * W, K, cka, ls);
     }
-  }
-  for (; ma < Ma; ma++) {
-    const int t0  = ma * W;
-    const v2s ckb = u2v(ck[ma * 64 + lane]);
-    if (t0 + W <= La) {
-      Pa = alpha_window<NSB, true>(Pa, xy, xyo, t0, t0 + W, t0 + W, Nb, K, ckb, ls);
-    } else {
-      Pa = alpha_window<NSB, false>(Pa, xy, xyo, t0, min(t0 + W, Nb), La, Nb, K, ckb, ls);
-    }
-  }
-  for (; mb >= 0; mb--) {
-    const v2s cka = u2v(ck[mb * 64 + lane]);
-    Pb            = beta_llr_window<NSB>(Pb, Bst, xy, xyo, mb * W, K, cka, ls);
   }
 }
 
@@ -500,16 +454,21 @@ __device__ __forceinline__ uint32_t pack2(short lo, short hi)
 }
 
 template <int NSB>
-__global__ __launch_bounds__(64) void tdec_kernel(TdecArgs a)
+__global__ __launch_bounds__(128) void tdec_kernel(TdecArgs a)
 {
   using Gm                = Geo<NSB>;
   constexpr bool SAT      = Gm::SAT;
-  constexpr int  G        = Gm::G;
+  constexpr int  G        = Gm::G;        // lanes per code block in one wave
+  constexpr int  G2       = 2 * G;        // threads per code block in the workgroup
+  constexpr int  LOG_NSB  = NSB == 16 ? 4 : (NSB == 8 ? 3 : 0);
+  constexpr int  U        = 4;            // positions per thread per batch in the prepare phase
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
 
-  const int lane = threadIdx.x;
-  const int cw   = lane / G;                 // CB within wave
-  const int g    = lane % G;                 // lane within CB group
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int cw   = lane / G;                 // CB within the workgroup
+  const int g    = lane % G;                 // lane within the CB's quad group
+  const int t2   = wave * G + g;             // thread within the CB (both waves)
   const int s    = g >> 2;                   // sub-block
   const int j    = g & 3;                    // state-pair index
   const int K    = a.K;
@@ -529,17 +488,15 @@ __global__ __launch_bounds__(64) void tdec_kernel(TdecArgs a)
   short*    xylo = reinterpret_cast<short*>(xyc);
   short*    auxc = sm.aux + cw * XYW;
 
-  const short* in  = a.in + (size_t)cbr * a.in_stride;
-  const int    nsb = NSB > 1 ? NSB : 1;
-  // input stream accessors (natural 3K+12 or rm_turbo SB layout)
-  auto sbi = [&](int n) -> int {  // rm_turbo SB position of natural bit n
-    const int q = (int)__umulhi((uint32_t)n, a.magicL);
-    return (n - q * L) * nsb + q;
-  };
-  auto S  = [&](int n) -> short { return a.layout_sb ? in[sbi(n)] : in[3 * n]; };
-  auto P0 = [&](int n) -> short { return a.layout_sb ? in[(K + 32) + sbi(n)] : in[3 * n + 1]; };
-  auto P1 = [&](int n) -> short { return a.layout_sb ? in[2 * (K + 32) + sbi(n)] : in[3 * n + 2]; };
-  const short* tail = a.layout_sb ? in + 3 * (K + 32) : in + 3 * K;
+  const short* in = a.in + (size_t)cbr * a.in_stride;
+  const bool   sb = a.layout_sb;
+  // Positions are visited in "q order": the rm_turbo sub-block order for window
+  // decoders (q = k*NSB + s, coalesced in the SB input), natural order otherwise.
+  auto qslot = [&](int q) -> int { return NSB > 1 ? (q & (NSB - 1)) * Ls + (q >> LOG_NSB) : q; };
+  auto qnat  = [&](int q) -> int { return NSB > 1 ? (q & (NSB - 1)) * L + (q >> LOG_NSB) : q; };
+  // stream c (0 = systematic, 1 = parity0, 2 = parity1) at position q
+  auto inq = [&](int c, int q) -> short { return sb ? in[c * (K + 32) + q] : in[3 * qnat(q) + c]; };
+  const short* tail = sb ? in + 3 * (K + 32) : in + 3 * K;
   short st[3], p0t[3], x2t[3], p1t[3];
 #pragma unroll
   for (int t = 0; t < 3; t++) {
@@ -548,21 +505,13 @@ __global__ __launch_bounds__(64) void tdec_kernel(TdecArgs a)
     x2t[t] = tail[6 + 2 * t];
     p1t[t] = tail[6 + 2 * t + 1];
   }
-  auto slot = [&](int n) -> int {
-    if constexpr (NSB > 1) {
-      const int q = (int)__umulhi((uint32_t)n, a.magicL);
-      return q * Ls + (n - q * L);
-    } else {
-      return n;
-    }
-  };
-  const uint16_t* tfwd = a.tfwd;
-  const uint16_t* trev = a.trev;
+  const uint16_t* tfq = a.tfwd;  // slot of pi(n(q))
+  const uint16_t* trq = a.trev;  // slot of pi^-1(n(q))
 
   // restore state from a previous launch (srsran_tdec_iteration path)
   if (a.n_start > 0) {
     const short* se = a.state + (size_t)cbr * 2 * XYW;
-    for (int i = g; i < XYW; i += G) {
+    for (int i = t2; i < XYW; i += G2) {
       xylo[2 * i] = se[i];
       auxc[i]     = se[XYW + i];
     }
@@ -577,70 +526,139 @@ __global__ __launch_bounds__(64) void tdec_kernel(TdecArgs a)
     // -------- prepare branch inputs (turbodecoder_iter.h:104-128) --------
     if ((h & 1) == 0) {
       if (h == 0) {
-        for (int n = g; n < K; n += G) {
-          xyc[slot(n)] = pack2(S(n), P0(n));
+        for (int q0 = t2; q0 < K; q0 += U * G2) {
+          short sv[U], pv[U];
+#pragma unroll
+          for (int u = 0; u < U; u++) {
+            const int q = q0 + u * G2;
+            if (q < K) {
+              sv[u] = inq(0, q);
+              pv[u] = inq(1, q);
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < U; u++) {
+            const int q = q0 + u * G2;
+            if (q < K) {
+              xyc[qslot(q)] = pack2(sv[u], pv[u]);
+            }
+          }
         }
       } else {
         // app1 = ext2 de-interleaved: gather into the dead XY.hi half of the own slot
-        for (int n = g; n < K; n += G) {
-          xylo[2 * slot(n) + 1] = xylo[2 * trev[n]];
+        for (int q0 = t2; q0 < K; q0 += U * G2) {
+          int tv[U];
+#pragma unroll
+          for (int u = 0; u < U; u++) {
+            const int q = q0 + u * G2;
+            if (q < K) {
+              tv[u] = trq[q];
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < U; u++) {
+            const int q = q0 + u * G2;
+            if (q < K) {
+              xylo[2 * qslot(q) + 1] = xylo[2 * tv[u]];
+            }
+          }
         }
         __syncthreads();
-        for (int n = g; n < K; n += G) {
-          const int   sl = slot(n);
-          const short a1 = (short)(xylo[2 * sl + 1] - auxc[sl]);  // app1 -= ext1 (vec_sub, wraps)
-          auxc[sl]       = a1;
-          const short sx = S(n);
-          const short x  = SAT ? __builtin_elementwise_add_sat(sx, a1) : (short)(sx + a1);
-          xyc[sl]        = pack2(x, P0(n));
+        for (int q0 = t2; q0 < K; q0 += U * G2) {
+          short sv[U], pv[U];
+#pragma unroll
+          for (int u = 0; u < U; u++) {
+            const int q = q0 + u * G2;
+            if (q < K) {
+              sv[u] = inq(0, q);
+              pv[u] = inq(1, q);
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < U; u++) {
+            const int q = q0 + u * G2;
+            if (q < K) {
+              const int   sl = qslot(q);
+              const short a1 = (short)(xylo[2 * sl + 1] - auxc[sl]);  // app1 -= ext1 (vec_sub, wraps)
+              auxc[sl]       = a1;
+              const short x  = SAT ? __builtin_elementwise_add_sat(sv[u], a1) : (short)(sv[u] + a1);
+              xyc[sl]        = pack2(x, pv[u]);
+            }
+          }
         }
       }
       if constexpr (NSB == 1) {
-        if (g < 3) {
-          xyc[K + g] = pack2(st[g], p0t[g]);
+        if (t2 < 3) {
+          xyc[K + t2] = pack2(st[t2], p0t[t2]);
         }
       }
     } else {
-      for (int n = g; n < K; n += G) {  // ext1 -= app1 (h > 1), keep it in AUX
-        const int sl = slot(n);
-        const short e = xylo[2 * sl];
-        auxc[sl]      = h > 1 ? (short)(e - auxc[sl]) : e;
+      for (int q = t2; q < K; q += G2) {  // ext1 -= app1 (h > 1), keep it in AUX
+        const int   sl = qslot(q);
+        const short e  = xylo[2 * sl];
+        auxc[sl]       = h > 1 ? (short)(e - auxc[sl]) : e;
       }
       __syncthreads();
-      for (int n = g; n < K; n += G) {  // app2 = ext1 interleaved
-        xyc[slot(n)] = pack2(auxc[tfwd[n]], P1(n));
+      for (int q0 = t2; q0 < K; q0 += U * G2) {  // app2 = ext1 interleaved
+        int   tv[U];
+        short pv[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          const int q = q0 + u * G2;
+          if (q < K) {
+            tv[u] = tfq[q];
+            pv[u] = inq(2, q);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          const int q = q0 + u * G2;
+          if (q < K) {
+            xyc[qslot(q)] = pack2(auxc[tv[u]], pv[u]);
+          }
+        }
       }
       if constexpr (NSB == 1) {
-        if (g < 3) {
-          xyc[K + g] = pack2(x2t[g], p1t[g]);
+        if (t2 < 3) {
+          xyc[K + t2] = pack2(x2t[t2], p1t[t2]);
         }
       }
     }
     __syncthreads();
 
-    // -------- constituent MAP decode --------
+    // -------- constituent MAP decode (wave 0: alpha side, wave 1: beta side) --------
     const bool dec1 = (h & 1) == 0;
-    map_decode<NSB>(sm, base, lane, j, s, K, L, Nb, La, M, dec1 ? st : x2t, dec1 ? p0t : p1t);
+    map_decode<NSB>(sm, base, wave, lane, j, s, K, L, Nb, La, M, dec1 ? st : x2t, dec1 ? p0t : p1t);
     __syncthreads();
   }
 
-  // -------- hard decision (turbodecoder.c:370-378) --------
+  // -------- hard decision (turbodecoder.c:370-378), natural bit order --------
   const bool last_dec1 = ((a.n_end - 1) & 1) == 0;
   if (live) {
     uint8_t* out = a.out + (size_t)cb * (K / 8);
-    for (int b = g; b < K / 8; b += G) {
+    for (int b = t2; b < K / 8; b += G2) {
       uint32_t byte = 0;
 #pragma unroll
       for (int t = 0; t < 8; t++) {
-        const int   n = 8 * b + t;
-        const short v = last_dec1 ? xylo[2 * slot(n)] : xylo[2 * trev[n]];
+        const int n = 8 * b + t;
+        int       sl, q;
+        if constexpr (NSB > 1) {
+          const int sb_ = (int)__umulhi((uint32_t)n, a.magicL);  // n / L
+          const int k   = n - sb_ * L;
+          sl            = sb_ * Ls + k;
+          q             = k * NSB + sb_;
+        } else {
+          sl = n;
+          q  = n;
+        }
+        const short v = last_dec1 ? xylo[2 * sl] : xylo[2 * trq[q]];
         byte |= (uint32_t)(v > 0) << (7 - t);
       }
       out[b] = (uint8_t)byte;
     }
     if (a.state) {
       short* se = a.state + (size_t)cb * 2 * XYW;
-      for (int i = g; i < XYW; i += G) {
+      for (int i = t2; i < XYW; i += G2) {
         se[i]       = xylo[2 * i];
         se[XYW + i] = auxc[i];
       }
@@ -654,7 +672,7 @@ static hipError_t launch(const TdecArgs& a, hipStream_t stream)
   const int    cpw  = Geo<NSB>::CPW;
   const int    grid = (a.ncb + cpw - 1) / cpw;
   const size_t lds  = tdec_lds_bytes(NSB, a.xyw, a.M);
-  hipLaunchKernelGGL(tdec_kernel<NSB>, dim3(grid), dim3(64), lds, stream, a);
+  hipLaunchKernelGGL(tdec_kernel<NSB>, dim3(grid), dim3(128), lds, stream, a);
   return hipGetLastError();
 }
 

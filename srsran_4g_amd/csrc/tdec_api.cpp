@@ -76,8 +76,10 @@ constexpr size_t kMaxLds = 160 * 1024;
 struct Config {
   int       nsb;  // 16, 8 or 1 (generic)
   TdecArgs  proto;
-  uint16_t* d_tfwd = nullptr;
+  uint16_t* d_tfwd = nullptr;  // visit (SB) order
   uint16_t* d_trev = nullptr;
+  uint16_t* d_tfwd_nat = nullptr;  // natural order
+  uint16_t* d_trev_nat = nullptr;
 };
 
 std::mutex                             g_mu;
@@ -127,7 +129,7 @@ Config* get_config(uint32_t K, int nsb)
     return nullptr;
   }
   // QPP tables (tc_interl_lte.c:69-107) expressed directly as LDS slots.
-  std::vector<uint16_t> fwd(K), rev(K), tf(K), tr(K);
+  std::vector<uint16_t> fwd(K), rev(K), tf(K), tr(K), tfn(K), trn(K);
   const uint64_t f1 = kF1[idx], f2 = kF2[idx];
   for (uint64_t i = 0; i < K; i++) {
     const uint32_t j = (uint32_t)((f1 * i + f2 * i * i) % K);
@@ -142,14 +144,17 @@ Config* get_config(uint32_t K, int nsb)
     const uint32_t n = nsb > 1 ? (q % nsb) * a.L + q / nsb : q;
     tf[q]            = slot(fwd[n]);
     tr[q]            = slot(rev[n]);
+    tfn[q]           = slot(fwd[q]);
+    trn[q]           = slot(rev[q]);
   }
   Config* c = new Config();
   c->nsb    = nsb;
   c->proto  = a;
-  if (hipMalloc(&c->d_tfwd, K * sizeof(uint16_t)) != hipSuccess ||
-      hipMalloc(&c->d_trev, K * sizeof(uint16_t)) != hipSuccess ||
-      hipMemcpy(c->d_tfwd, tf.data(), K * sizeof(uint16_t), hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(c->d_trev, tr.data(), K * sizeof(uint16_t), hipMemcpyHostToDevice) != hipSuccess) {
+  auto up = [&](uint16_t** d, const std::vector<uint16_t>& h) {
+    return hipMalloc(d, K * sizeof(uint16_t)) == hipSuccess &&
+           hipMemcpy(*d, h.data(), K * sizeof(uint16_t), hipMemcpyHostToDevice) == hipSuccess;
+  };
+  if (!up(&c->d_tfwd, tf) || !up(&c->d_trev, tr) || !up(&c->d_tfwd_nat, tfn) || !up(&c->d_trev_nat, trn)) {
     fprintf(stderr, "[srsran_tdec] device table allocation failed for K=%u\n", K);
     delete c;
     return nullptr;
@@ -208,7 +213,11 @@ int enqueue(const Config* c, const short* d_in, uint32_t in_stride, int layout_s
   a.out       = d_out;
   a.tfwd      = c->d_tfwd;
   a.trev      = c->d_trev;
+  a.tfwd_nat  = c->d_tfwd_nat;
+  a.trev_nat  = c->d_trev_nat;
   a.state     = d_state;
+  static const uint32_t dbg = getenv("SRSRAN_TDEC_ABLATE") ? (uint32_t)atoi(getenv("SRSRAN_TDEC_ABLATE")) : 0;
+  a.dbg       = dbg;
   hipError_t e = tdec_launch(c->nsb, a, stream);
   if (e != hipSuccess) {
     fprintf(stderr, "[srsran_tdec] launch failed: %s\n", hipGetErrorString(e));

@@ -21,12 +21,15 @@ struct TdecArgs {
   uint8_t*        out;       // ncb * K/8 hard-decision bytes (device)
   const uint16_t* tfwd;      // slot of pi(n(q))    (device, K entries, q order)
   const uint16_t* trev;      // slot of pi^-1(n(q)) (device, K entries, q order)
+  const uint16_t* tfwd_nat;  // slot of pi(n)       (device, K entries, natural order)
+  const uint16_t* trev_nat;  // slot of pi^-1(n)    (device, K entries, natural order)
   short*          state;     // optional ncb * 2 * xyw saved LLR/AUX state (device) or nullptr
   uint32_t        L;         // sub-block length (K for the generic decoder)
   uint32_t        Ls;        // LDS slot stride per sub-block
   uint32_t        xyw;       // LDS words per code block
   uint32_t        M;         // beta checkpoints per sub-block
   uint32_t        magicL;    // ceil(2^32 / L)
+  uint32_t        dbg;       // profiling ablation only (SRSRAN_TDEC_ABLATE): bit0 skip prepare, bit1 skip MAP
 };
 
 hipError_t tdec_launch(int nsb, const TdecArgs& a, hipStream_t stream);

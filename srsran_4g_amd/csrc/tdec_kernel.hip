@@ -454,7 +454,7 @@ __device__ __forceinline__ uint32_t pack2(short lo, short hi)
 }
 
 template <int NSB>
-__global__ __launch_bounds__(128) void tdec_kernel(TdecArgs a)
+__global__ __launch_bounds__(128, 2) void tdec_kernel(TdecArgs a)
 {
   using Gm                = Geo<NSB>;
   constexpr bool SAT      = Gm::SAT;
@@ -505,8 +505,89 @@ __global__ __launch_bounds__(128) void tdec_kernel(TdecArgs a)
     x2t[t] = tail[6 + 2 * t];
     p1t[t] = tail[6 + 2 * t + 1];
   }
-  const uint16_t* tfq = a.tfwd;  // slot of pi(n(q))
-  const uint16_t* trq = a.trev;  // slot of pi^-1(n(q))
+  // Visit order of the prepare phase: rm_turbo SB order (q) for window decoders
+  // on SB input, natural order otherwise.  The QPP tables come in both orders.
+  const bool      vsb = NSB > 1 && sb;
+  const uint16_t* tfq = vsb ? a.tfwd : a.tfwd_nat;  // slot of pi(n(p))
+  const uint16_t* trq = vsb ? a.trev : a.trev_nat;  // slot of pi^-1(n(p))
+  const int       nch = K / 4;
+  auto pslot = [&](int p) -> int {  // LDS slot of visit position p
+    if constexpr (NSB > 1) {
+      if (vsb) {
+        return qslot(p);
+      }
+      const int sbn = (int)__umulhi((uint32_t)p, a.magicL);  // p / L
+      return sbn * Ls + (p - sbn * L);
+    } else {
+      return p;
+    }
+  };
+  // Visit this thread's positions in chunks of 4 (visit order), BATCH chunks at a
+  // time with all global loads of a batch issued before use:
+  // fn(p, sys, par0, par1, table) -- only the streams the half-iteration needs
+  // are loaded (dec1: sys+par0 [+ pi^-1 table], dec2: par1 + pi table).
+  auto for_chunks = [&](int hh, auto&& fn) {
+    constexpr int BATCH = 6;
+    const bool    d1    = (hh & 1) == 0;
+    const bool    need_t = hh > 0;
+    const uint16_t* tab  = d1 ? trq : tfq;
+    for (int c0 = t2; c0 < nch; c0 += BATCH * G2) {
+      uint2 w0[BATCH], w1[BATCH], w2[BATCH], tv[BATCH];
+#pragma unroll
+      for (int i = 0; i < BATCH; i++) {
+        const int c = c0 + i * G2;
+        if (c < nch) {
+          if (vsb) {
+            const short* b = in + 4 * c;
+            if (d1) {
+              w0[i] = *reinterpret_cast<const uint2*>(b);
+              w1[i] = *reinterpret_cast<const uint2*>(b + (K + 32));
+            } else {
+              w2[i] = *reinterpret_cast<const uint2*>(b + 2 * (K + 32));
+            }
+          } else {
+            const uint2* b = reinterpret_cast<const uint2*>(in + 12 * c);
+            w0[i]          = b[0];
+            w1[i]          = b[1];
+            w2[i]          = b[2];
+          }
+          if (need_t) {
+            tv[i] = *reinterpret_cast<const uint2*>(tab + 4 * c);
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < BATCH; i++) {
+        const int c = c0 + i * G2;
+        if (c < nch) {
+#pragma unroll
+          for (int v = 0; v < 4; v++) {
+            short x0, x1, x2;
+            if (vsb) {
+              const uint32_t d0 = v < 2 ? w0[i].x : w0[i].y;
+              const uint32_t d1w = v < 2 ? w1[i].x : w1[i].y;
+              const uint32_t d2 = v < 2 ? w2[i].x : w2[i].y;
+              x0 = (short)((v & 1) ? (d0 >> 16) : (d0 & 0xffff));
+              x1 = (short)((v & 1) ? (d1w >> 16) : (d1w & 0xffff));
+              x2 = (short)((v & 1) ? (d2 >> 16) : (d2 & 0xffff));
+            } else {  // natural: 12 interleaved values S,P0,P1 x 4
+              const uint32_t e[6] = {w0[i].x, w0[i].y, w1[i].x, w1[i].y, w2[i].x, w2[i].y};
+              auto el = [&](int k) -> short { return (short)((k & 1) ? (e[k >> 1] >> 16) : (e[k >> 1] & 0xffff)); };
+              x0 = el(3 * v);
+              x1 = el(3 * v + 1);
+              x2 = el(3 * v + 2);
+            }
+            int t = 0;
+            if (need_t) {
+              const uint32_t d = v < 2 ? tv[i].x : tv[i].y;
+              t                = (int)((v & 1) ? (d >> 16) : (d & 0xffff));
+            }
+            fn(4 * c + v, x0, x1, x2, t);
+          }
+        }
+      }
+    }
+  };
 
   // restore state from a previous launch (srsran_tdec_iteration path)
   if (a.n_start > 0) {
@@ -524,68 +605,25 @@ __global__ __launch_bounds__(128) void tdec_kernel(TdecArgs a)
 
   for (int h = a.n_start; h < a.n_end; h++) {
     // -------- prepare branch inputs (turbodecoder_iter.h:104-128) --------
-    if ((h & 1) == 0) {
+    // Each thread owns chunks of 4 consecutive positions in visit order (SB order
+    // for window decoders on SB input, natural order otherwise); all its global
+    // loads are issued before any of them is consumed.
+    if (h > a.n_start && (a.dbg & 1)) {
+      // profiling ablation: keep the previous branch inputs
+    } else if ((h & 1) == 0) {
       if (h == 0) {
-        for (int q0 = t2; q0 < K; q0 += U * G2) {
-          short sv[U], pv[U];
-#pragma unroll
-          for (int u = 0; u < U; u++) {
-            const int q = q0 + u * G2;
-            if (q < K) {
-              sv[u] = inq(0, q);
-              pv[u] = inq(1, q);
-            }
-          }
-#pragma unroll
-          for (int u = 0; u < U; u++) {
-            const int q = q0 + u * G2;
-            if (q < K) {
-              xyc[qslot(q)] = pack2(sv[u], pv[u]);
-            }
-          }
-        }
+        for_chunks(h, [&](int p, short sx, short p0, short, int) { xyc[pslot(p)] = pack2(sx, p0); });
       } else {
         // app1 = ext2 de-interleaved: gather into the dead XY.hi half of the own slot
-        for (int q0 = t2; q0 < K; q0 += U * G2) {
-          int tv[U];
-#pragma unroll
-          for (int u = 0; u < U; u++) {
-            const int q = q0 + u * G2;
-            if (q < K) {
-              tv[u] = trq[q];
-            }
-          }
-#pragma unroll
-          for (int u = 0; u < U; u++) {
-            const int q = q0 + u * G2;
-            if (q < K) {
-              xylo[2 * qslot(q) + 1] = xylo[2 * tv[u]];
-            }
-          }
-        }
+        for_chunks(h, [&](int p, short, short, short, int t) { xylo[2 * pslot(p) + 1] = xylo[2 * t]; });
         __syncthreads();
-        for (int q0 = t2; q0 < K; q0 += U * G2) {
-          short sv[U], pv[U];
-#pragma unroll
-          for (int u = 0; u < U; u++) {
-            const int q = q0 + u * G2;
-            if (q < K) {
-              sv[u] = inq(0, q);
-              pv[u] = inq(1, q);
-            }
-          }
-#pragma unroll
-          for (int u = 0; u < U; u++) {
-            const int q = q0 + u * G2;
-            if (q < K) {
-              const int   sl = qslot(q);
-              const short a1 = (short)(xylo[2 * sl + 1] - auxc[sl]);  // app1 -= ext1 (vec_sub, wraps)
-              auxc[sl]       = a1;
-              const short x  = SAT ? __builtin_elementwise_add_sat(sv[u], a1) : (short)(sv[u] + a1);
-              xyc[sl]        = pack2(x, pv[u]);
-            }
-          }
-        }
+        for_chunks(h, [&](int p, short sx, short p0, short, int) {
+          const int   sl = pslot(p);
+          const short a1 = (short)(xylo[2 * sl + 1] - auxc[sl]);  // app1 -= ext1 (vec_sub, wraps)
+          auxc[sl]       = a1;
+          const short x  = SAT ? __builtin_elementwise_add_sat(sx, a1) : (short)(sx + a1);
+          xyc[sl]        = pack2(x, p0);
+        });
       }
       if constexpr (NSB == 1) {
         if (t2 < 3) {
@@ -593,31 +631,14 @@ __global__ __launch_bounds__(128) void tdec_kernel(TdecArgs a)
         }
       }
     } else {
-      for (int q = t2; q < K; q += G2) {  // ext1 -= app1 (h > 1), keep it in AUX
-        const int   sl = qslot(q);
+      for (int p = t2; p < K; p += G2) {  // ext1 -= app1 (h > 1), keep it in AUX
+        const int   sl = pslot(p);
         const short e  = xylo[2 * sl];
         auxc[sl]       = h > 1 ? (short)(e - auxc[sl]) : e;
       }
       __syncthreads();
-      for (int q0 = t2; q0 < K; q0 += U * G2) {  // app2 = ext1 interleaved
-        int   tv[U];
-        short pv[U];
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-          const int q = q0 + u * G2;
-          if (q < K) {
-            tv[u] = tfq[q];
-            pv[u] = inq(2, q);
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-          const int q = q0 + u * G2;
-          if (q < K) {
-            xyc[qslot(q)] = pack2(auxc[tv[u]], pv[u]);
-          }
-        }
-      }
+      // app2 = ext1 interleaved
+      for_chunks(h, [&](int p, short, short, short p1, int t) { xyc[pslot(p)] = pack2(auxc[t], p1); });
       if constexpr (NSB == 1) {
         if (t2 < 3) {
           xyc[K + t2] = pack2(x2t[t2], p1t[t2]);
@@ -628,7 +649,9 @@ __global__ __launch_bounds__(128) void tdec_kernel(TdecArgs a)
 
     // -------- constituent MAP decode (wave 0: alpha side, wave 1: beta side) --------
     const bool dec1 = (h & 1) == 0;
-    map_decode<NSB>(sm, base, wave, lane, j, s, K, L, Nb, La, M, dec1 ? st : x2t, dec1 ? p0t : p1t);
+    if (!(a.dbg & 2)) {
+      map_decode<NSB>(sm, base, wave, lane, j, s, K, L, Nb, La, M, dec1 ? st : x2t, dec1 ? p0t : p1t);
+    }
     __syncthreads();
   }
 
@@ -641,17 +664,14 @@ __global__ __launch_bounds__(128) void tdec_kernel(TdecArgs a)
 #pragma unroll
       for (int t = 0; t < 8; t++) {
         const int n = 8 * b + t;
-        int       sl, q;
+        int       sl;
         if constexpr (NSB > 1) {
           const int sb_ = (int)__umulhi((uint32_t)n, a.magicL);  // n / L
-          const int k   = n - sb_ * L;
-          sl            = sb_ * Ls + k;
-          q             = k * NSB + sb_;
+          sl            = sb_ * Ls + (n - sb_ * L);
         } else {
           sl = n;
-          q  = n;
         }
-        const short v = last_dec1 ? xylo[2 * sl] : xylo[2 * trq[q]];
+        const short v = last_dec1 ? xylo[2 * sl] : xylo[2 * a.trev_nat[n]];
         byte |= (uint32_t)(v > 0) << (7 - t);
       }
       out[b] = (uint8_t)byte;

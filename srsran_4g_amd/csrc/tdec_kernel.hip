@@ -100,12 +100,11 @@ template <bool SAT>
 __device__ __forceinline__ v2s beta_step(v2s P, v2s xy_in, const LaneSel& ls)
 {
   const v2s xys = padd<SAT>(xy_in, swp(xy_in));
-  const v2s g1  = perm(xys, xy_in, ls.gb1);
-  const v2s g2  = perm(xys, xy_in, ls.gb2);
+  const v2s g1  = perm(xys, xy_in, ls.gb1);  // the second metric pair is always swap(g1)
   const v2s t1  = dpp<QP(0, 0, 1, 1)>(P);
   const v2s t2  = dpp<QP(2, 2, 3, 3)>(P);
   const v2s r   = perm(t2, t1, ls.rb);
-  return pmax(padd<SAT>(lo2(r), g1), padd<SAT>(hi2(r), g2));
+  return pmax(padd<SAT>(lo2(r), g1), padd<SAT>(hi2(r), swp(g1)));
 }
 
 // Forward candidates (turbodecoder_win.h:767-785 / turbodecoder_gen.c:133-149).
@@ -333,27 +332,25 @@ __device__ __forceinline__ v2s beta_llr_window(v2s P, v2s& Bst, const uint32_t* 
 {
   constexpr bool SAT = Geo<NSB>::SAT;
   v2s            xw[W];
-  v2s            aw[W];
+  v2s            cw0[W], cw1[W];  // alpha candidates of every position (bit 0 / bit 1)
 #pragma unroll
   for (int i = 0; i < W; i++) {
     xw[i] = u2v(xy[t0 + i]);
   }
-  aw[0] = cka;
+  v2s a = cka;
 #pragma unroll
-  for (int i = 0; i < W - 1; i++) {
-    v2s c0, c1;
-    alpha_cand<SAT>(aw[i], xw[i], ls, c0, c1);
-    v2s a = pmax(c0, c1);
-    if (alpha_norm_at<NSB>(t0 + i)) {
-      a = norm<SAT>(a);
+  for (int i = 0; i < W; i++) {
+    alpha_cand<SAT>(a, xw[i], ls, cw0[i], cw1[i]);
+    if (i < W - 1) {
+      a = pmax(cw0[i], cw1[i]);
+      if (alpha_norm_at<NSB>(t0 + i)) {
+        a = norm<SAT>(a);
+      }
     }
-    aw[i + 1] = a;
   }
 #pragma unroll
   for (int i = W - 1; i >= 0; i--) {
-    v2s c0, c1;
-    alpha_cand<SAT>(aw[i], xw[i], ls, c0, c1);
-    xyo[2 * (t0 + i)] = llr_out<SAT>(Bst, c0, c1);
+    xyo[2 * (t0 + i)] = llr_out<SAT>(Bst, cw0[i], cw1[i]);
     P                 = beta_step<SAT>(P, xw[i], ls);
     Bst               = P;
     if (beta_norm_at<NSB>(t0 + i, K)) {
@@ -527,7 +524,7 @@ __global__ __launch_bounds__(128, 2) void tdec_kernel(TdecArgs a)
   // fn(p, sys, par0, par1, table) -- only the streams the half-iteration needs
   // are loaded (dec1: sys+par0 [+ pi^-1 table], dec2: par1 + pi table).
   auto for_chunks = [&](int hh, auto&& fn) {
-    constexpr int BATCH = 6;
+    constexpr int BATCH = NSB == 8 ? 2 : 4;
     const bool    d1    = (hh & 1) == 0;
     const bool    need_t = hh > 0;
     const uint16_t* tab  = d1 ? trq : tfq;

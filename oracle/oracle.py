@@ -24,6 +24,11 @@ CB_SIZES = (
 )
 assert len(CB_SIZES) == 188 and CB_SIZES[-1] == 6144
 
+SEGM_FIELDS = ("F", "C", "K1", "K2", "K1_idx", "K2_idx", "C1", "C2", "tbs")
+SOFTBUF_LEN = 18600  # SOFTBUFFER_SIZE, softbuffer.h:56
+LTE_CRC24A = 0x1864CFB  # phy_common.h:72
+LTE_CRC24B = 0x1800063  # phy_common.h:73
+
 _i16p = ctypes.POINTER(ctypes.c_int16)
 _u8p = ctypes.POINTER(ctypes.c_uint8)
 _u16p = ctypes.POINTER(ctypes.c_uint16)
@@ -99,6 +104,84 @@ class Oracle(_Lib):
         self.lib.oracle_qpp(K, _ptr(f, _u16p), _ptr(r, _u16p))
         return f, r
 
+    # ---- DL-SCH pieces (sch_oracle.c) ----
+    def _sch_sigs(self):
+        L = self.lib
+        u32 = ctypes.c_uint32
+        L.oracle_crc_checksum_byte.argtypes = [u32, ctypes.c_int, _u8p, u32]
+        L.oracle_crc_checksum_byte.restype = u32
+        L.oracle_crc_bits.argtypes = [u32, ctypes.c_int, _u8p, u32]
+        L.oracle_crc_bits.restype = u32
+        L.oracle_cbsegm.argtypes = [u32, ctypes.POINTER(u32)]
+        L.oracle_rm_rx_table.argtypes = [u32, u32, ctypes.c_int, _u16p]
+        L.oracle_rm_turbo_rx.argtypes = [u32, u32, ctypes.c_int, _i16p, u32, _i16p]
+        L.oracle_rm_turbo_tx.argtypes = [u32, u32, _u8p, u32, _u8p]
+        L.oracle_dlsch_decode_tb.argtypes = [u32, u32, u32, u32, _i16p, u32, _i16p, u32, _u8p, _u8p, u32, _u8p,
+                                             ctypes.POINTER(u32), ctypes.POINTER(ctypes.c_float)]
+        L.oracle_dlsch_encode_tb.argtypes = [u32, u32, u32, u32, _u8p, _u8p]
+
+    def crc_byte(self, poly, order, data, nbits):
+        self._sch_sigs()
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        return self.lib.oracle_crc_checksum_byte(poly, order, _ptr(data, _u8p), nbits)
+
+    def crc_bits(self, poly, order, bits):
+        self._sch_sigs()
+        bits = np.ascontiguousarray(bits, dtype=np.uint8)
+        return self.lib.oracle_crc_bits(poly, order, _ptr(bits, _u8p), bits.size)
+
+    def cbsegm(self, tbs):
+        self._sch_sigs()
+        out = (ctypes.c_uint32 * 9)()
+        rc = self.lib.oracle_cbsegm(tbs, out)
+        return rc, dict(zip(SEGM_FIELDS, list(out)))
+
+    def rm_rx_table(self, K, rv, layout_sb):
+        self._sch_sigs()
+        t = np.zeros(3 * K + 12, dtype=np.uint16)
+        self.lib.oracle_rm_rx_table(K, rv, int(bool(layout_sb)), _ptr(t, _u16p))
+        return t
+
+    def rm_turbo_rx(self, K, rv, layout_sb, e, softbuf):
+        self._sch_sigs()
+        e = np.ascontiguousarray(e, dtype=np.int16)
+        sb = np.ascontiguousarray(softbuf, dtype=np.int16).copy()
+        self.lib.oracle_rm_turbo_rx(K, rv, int(bool(layout_sb)), _ptr(e, _i16p), e.size, _ptr(sb, _i16p))
+        return sb
+
+    def rm_turbo_tx(self, K, rv, coded, E):
+        self._sch_sigs()
+        coded = np.ascontiguousarray(coded, dtype=np.uint8)
+        out = np.zeros(E, dtype=np.uint8)
+        self.lib.oracle_rm_turbo_tx(K, rv, _ptr(coded, _u8p), E, _ptr(out, _u8p))
+        return out
+
+    def dlsch_encode(self, tbs, Qm, rv, nof_e_bits, tb_bytes):
+        self._sch_sigs()
+        tb_bytes = np.ascontiguousarray(tb_bytes, dtype=np.uint8)
+        e = np.zeros(nof_e_bits, dtype=np.uint8)
+        n = self.lib.oracle_dlsch_encode_tb(tbs, Qm, rv, nof_e_bits, _ptr(tb_bytes, _u8p), _ptr(e, _u8p))
+        if n < 0:
+            raise ValueError(f"encode failed tbs={tbs}")
+        return e
+
+    def dlsch_decode(self, tbs, Qm, rv, e_llr, max_iterations, state=None):
+        """decode_tb (sch.c:509-573). state = (softbuf[C,18600], cb_crc[C], cb_data[C,768]) for HARQ."""
+        self._sch_sigs()
+        rc, s = self.cbsegm(tbs)
+        C = max(1, s["C"])
+        if state is None:
+            state = (np.zeros((C, SOFTBUF_LEN), np.int16), np.zeros(C, np.uint8), np.zeros((C, 768), np.uint8))
+        sb, crc, cbd = state
+        e_llr = np.ascontiguousarray(e_llr, dtype=np.int16)
+        data = np.zeros(tbs // 8 + 8, dtype=np.uint8)
+        noi = (ctypes.c_uint32 * C)()
+        avg = ctypes.c_float(0)
+        ret = self.lib.oracle_dlsch_decode_tb(tbs, Qm, rv, e_llr.size, _ptr(e_llr, _i16p), max_iterations,
+                                              _ptr(sb, _i16p), sb.shape[1], _ptr(crc, _u8p), _ptr(cbd, _u8p),
+                                              cbd.shape[1], _ptr(data, _u8p), noi, ctypes.byref(avg))
+        return ret, data[: tbs // 8], list(noi), avg.value, state
+
     def run_batch(self, K, llr2d, layout_sb, nof_iterations):
         llr2d = np.ascontiguousarray(llr2d, dtype=np.int16)
         n = llr2d.shape[0]
@@ -125,6 +208,35 @@ class Reference(_Lib):
         bits = np.ascontiguousarray(bits, dtype=np.uint8)
         out = np.zeros(3 * K + 12, dtype=np.uint8)
         if self.lib.ref_tcod_encode(K, _ptr(bits, _u8p), _ptr(out, _u8p)):
+            raise ValueError(K)
+        return out
+
+    def crc_byte(self, poly, order, data, nbits):
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        return self.lib.ref_crc_checksum_byte(poly, order, _ptr(data, _u8p), nbits)
+
+    def cbsegm(self, tbs):
+        f = self.lib.ref_cbsegm
+        f.argtypes = [ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]
+        out = (ctypes.c_uint32 * 9)()
+        rc = f(tbs, out)
+        return rc, dict(zip(SEGM_FIELDS, list(out)))
+
+    def rm_turbo_rx(self, cb_idx, rv, e, softbuf):
+        """srsran_rm_turbo_rx_lut (SB layout for window decoders, as the reference build)."""
+        e = np.ascontiguousarray(e, dtype=np.int16)
+        sb = np.ascontiguousarray(softbuf, dtype=np.int16).copy()
+        rc = self.lib.ref_rm_turbo_rx_lut(_ptr(e, _i16p), _ptr(sb, _i16p), e.size, cb_idx, rv)
+        if rc:
+            raise ValueError(rc)
+        return sb
+
+    def rm_turbo_tx(self, K, rv, coded, E):
+        f = self.lib.ref_rm_turbo_tx
+        f.argtypes = [_u8p, ctypes.c_uint32, _u8p, ctypes.c_uint32, ctypes.c_uint32]
+        coded = np.ascontiguousarray(coded, dtype=np.uint8)
+        out = np.zeros(E, dtype=np.uint8)
+        if f(_ptr(coded, _u8p), K, _ptr(out, _u8p), E, rv):
             raise ValueError(K)
         return out
 

@@ -230,3 +230,66 @@ uint32_t ref_crc_checksum_byte(uint32_t poly, int order, const uint8_t* data, ui
   }
   return srsran_crc_checksum_byte(&crc, data, nbits);
 }
+
+/*
+ * The reference's INFO()/DEBUG() macros (debug.h:65-82) call the logger of
+ * phy_logger.c unless the verbosity is at least that level, in which case they
+ * print to stdout.  Around reference calls that log on their normal path we raise
+ * the verbosity with the reference's own set_srsran_verbose_level() and silence
+ * stdout, so the unbuildable logger is never reached.
+ */
+#include <fcntl.h>
+#include <stdio.h>
+#include <unistd.h>
+static int quiet_fd = -1;
+static void quiet_begin(void)
+{
+  fflush(stdout);
+  quiet_fd = dup(1);
+  int nul  = open("/dev/null", O_WRONLY);
+  dup2(nul, 1);
+  close(nul);
+  set_srsran_verbose_level(SRSRAN_VERBOSE_DEBUG);
+}
+static void quiet_end(void)
+{
+  fflush(stdout);
+  set_srsran_verbose_level(SRSRAN_VERBOSE_NONE);
+  dup2(quiet_fd, 1);
+  close(quiet_fd);
+}
+
+/* Reference code-block segmentation (cbsegm.c:62-117); out = {F,C,K1,K2,K1_idx,K2_idx,C1,C2,tbs}. */
+int ref_cbsegm(uint32_t tbs, uint32_t* out)
+{
+  srsran_cbsegm_t s;
+  memset(&s, 0, sizeof(s));
+  quiet_begin();
+  int ret = srsran_cbsegm(&s, tbs);
+  quiet_end();
+  out[0]  = s.F;
+  out[1]  = s.C;
+  out[2]  = s.K1;
+  out[3]  = s.K2;
+  out[4]  = s.K1_idx;
+  out[5]  = s.K2_idx;
+  out[6]  = s.C1;
+  out[7]  = s.C2;
+  out[8]  = s.tbs;
+  return ret;
+}
+
+/* Reference rate matching TX (rm_turbo.c srsran_rm_turbo_tx, bitwise). */
+int ref_rm_turbo_tx(const uint8_t* coded, uint32_t K, uint8_t* out, uint32_t E, uint32_t rv)
+{
+  static uint8_t w_buff[3 * (6144 + 4 + 32) + 64];
+  memset(w_buff, 0, sizeof(w_buff));
+  quiet_begin();
+  /* the bitwise TX only (re)builds its circular buffer w_buff on an rv=0 call */
+  int ret = srsran_rm_turbo_tx(w_buff, sizeof(w_buff), (uint8_t*)coded, 3 * K + 12, out, E, 0);
+  if (rv && !ret) {
+    ret = srsran_rm_turbo_tx(w_buff, sizeof(w_buff), (uint8_t*)coded, 3 * K + 12, out, E, rv);
+  }
+  quiet_end();
+  return ret;
+}

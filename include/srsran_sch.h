@@ -1,0 +1,237 @@
+/*
+ * include/srsran_sch.h -- DL-SCH receive boundary of the MI355X decoder.
+ *
+ * Drop-in for the reference's DL-SCH decode surface:
+ *   lib/include/srsran/phy/fec/cbsegm.h:32-81          srsran_cbsegm_t, srsran_cbsegm*
+ *   lib/include/srsran/phy/fec/crc.h:39-87             srsran_crc_t, srsran_crc_*
+ *   lib/include/srsran/phy/fec/turbo/rm_turbo.h:54-87  srsran_rm_turbo_{gentables,free_tables,rx_lut,rx_lut_}
+ *   lib/include/srsran/phy/fec/softbuffer.h:41-95      srsran_softbuffer_rx_t, srsran_softbuffer_rx_*
+ *   lib/include/srsran/phy/phch/ra.h:43-53             srsran_ra_tb_t
+ *   lib/include/srsran/phy/phch/pdsch_cfg.h:37-71      srsran_pdsch_grant_t, srsran_pdsch_cfg_t
+ *   lib/include/srsran/phy/phch/sch.h:52-100           srsran_sch_t, srsran_sch_*, srsran_dlsch_decode{,2}
+ *
+ * Differences a caller must know:
+ *   - srsran_softbuffer_rx_t keeps its field layout, but buffer_f[i] and data[i] point into DEVICE
+ *     memory (HBM).  cb_crc[] / tb_crc stay host-readable mirrors, refreshed by every synchronous call.
+ *   - srsran_sch_t keeps the fields callers touch (max_iterations, avg_iterations, llr_is_8bit,
+ *     decoder); the CPU-only scratch buffers are replaced by an opaque `gpu` pointer.
+ *   - the 8-bit LLR path is not provided (llr_is_8bit must stay false).
+ *   - srsran_dlsch_gpu_decode_batch() is an added, asynchronous entry point over device buffers.
+ */
+#ifndef SRSRAN_AMD_SCH_H
+#define SRSRAN_AMD_SCH_H
+
+#include <stdbool.h>
+#include <stdint.h>
+
+#include "srsran_tdec.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#ifndef SRSRAN_ERROR_OUT_OF_BOUNDS
+#define SRSRAN_ERROR_OUT_OF_BOUNDS -5
+#endif
+
+#define SRSRAN_MAX_PRB 110         /* phy_common.h:106 */
+#define SRSRAN_MAX_CODEWORDS 2     /* phy_common.h:60 */
+#define SRSRAN_MAX_CODEBLOCKS 32   /* phy_common.h:64 */
+#define SRSRAN_LTE_CRC24A 0x1864CFB /* phy_common.h:72 */
+#define SRSRAN_LTE_CRC24B 0x1800063 /* phy_common.h:73 */
+#define SOFTBUFFER_SIZE 18600      /* softbuffer.h:58 */
+
+/* ---------------- code block segmentation (cbsegm.h:32-81, cbsegm.c:62-140) ---------------- */
+typedef struct {
+  uint32_t F;
+  uint32_t C;
+  uint32_t K1;
+  uint32_t K2;
+  uint32_t K1_idx;
+  uint32_t K2_idx;
+  uint32_t C1;
+  uint32_t C2;
+  uint32_t tbs;
+  uint32_t L_tb;
+  uint32_t L_cb;
+  uint32_t Z;
+} srsran_cbsegm_t;
+
+int  srsran_cbsegm(srsran_cbsegm_t* s, uint32_t tbs);  /* cbsegm.c:62-117 */
+int  srsran_cbsegm_cbsize(uint32_t index);              /* cbsegm.c:133-140 */
+bool srsran_cbsegm_cbsize_isvalid(uint32_t size);       /* cbsegm.c:142-151 */
+int  srsran_cbsegm_cbindex(uint32_t long_cb);           /* cbsegm.c:119-131 */
+
+/* ---------------- CRC (crc.h:39-87, crc.c:117-195) -- host utility ---------------- */
+typedef struct {
+  uint64_t table[256];
+  int      polynom;
+  int      order;
+  uint64_t crcinit;
+  uint64_t crcmask;
+  uint64_t crchighbit;
+  uint32_t srsran_crc_out;
+} srsran_crc_t;
+
+int      srsran_crc_init(srsran_crc_t* h, uint32_t srsran_crc_poly, int srsran_crc_order); /* crc.c:69-93 */
+int      srsran_crc_set_init(srsran_crc_t* h, uint64_t init_value);                        /* crc.c:95-103 */
+uint32_t srsran_crc_checksum_byte(srsran_crc_t* h, const uint8_t* data, int len);          /* crc.c:145-163 */
+bool     srsran_crc_match_byte(srsran_crc_t* h, uint8_t* data, int len);                   /* crc.c:179-185 */
+uint32_t srsran_crc_attach_byte(srsran_crc_t* h, uint8_t* data, int len);                  /* crc.c:165-177 */
+
+/* ---------------- turbo rate de-matching RX (rm_turbo.h:54-87, rm_turbo.c:390-483) ----------------
+ * Host pointers, host-synchronous: output[deinter[i % (3K+12)]] += input[i] (int16 wrap), executed by
+ * the HIP de-matching kernel.  enable_input_tdec selects the decoder's sub-block (SB) layout for
+ * K >= 408 exactly like rm_turbo.c:403-418; the output buffer must then hold 3*(K+32)+12 values. */
+void srsran_rm_turbo_gentables(void);
+void srsran_rm_turbo_free_tables(void);
+int  srsran_rm_turbo_rx_lut(int16_t* input, int16_t* output, uint32_t in_len, uint32_t cb_idx, uint32_t rv_idx);
+int  srsran_rm_turbo_rx_lut_(int16_t* input,
+                             int16_t* output,
+                             uint32_t in_len,
+                             uint32_t cb_idx,
+                             uint32_t rv_idx,
+                             bool     enable_input_tdec);
+int  srsran_rm_turbo_rx_lut_8bit(int8_t* input, int8_t* output, uint32_t in_len, uint32_t cb_idx, uint32_t rv_idx);
+
+/* ---------------- HARQ soft buffer (softbuffer.h:41-95, softbuffer.c:36-178) ---------------- */
+typedef struct {
+  uint32_t  max_cb;
+  uint32_t  max_cb_size;
+  int16_t** buffer_f; /* DEVICE pointers, one per code block (max_cb_size int16 each) */
+  uint8_t** data;     /* DEVICE pointers, saved CB payload (max_cb_size/8 bytes each) */
+  bool*     cb_crc;   /* host mirror */
+  bool      tb_crc;   /* host mirror */
+  void*     gpu;      /* added: device arena + device flags */
+} srsran_softbuffer_rx_t;
+
+int  srsran_softbuffer_rx_init(srsran_softbuffer_rx_t* q, uint32_t nof_prb);
+int  srsran_softbuffer_rx_init_guru(srsran_softbuffer_rx_t* q, uint32_t max_cb, uint32_t max_cb_size);
+void srsran_softbuffer_rx_reset(srsran_softbuffer_rx_t* p);
+void srsran_softbuffer_rx_reset_tbs(srsran_softbuffer_rx_t* q, uint32_t tbs);
+void srsran_softbuffer_rx_reset_cb(srsran_softbuffer_rx_t* q, uint32_t nof_cb);
+void srsran_softbuffer_rx_reset_cb_crc(srsran_softbuffer_rx_t* q, uint32_t nof_cb);
+void srsran_softbuffer_rx_free(srsran_softbuffer_rx_t* p);
+/* added: copy the device cb_crc / tb_crc flags into the host mirror (after asynchronous batches) */
+int srsran_softbuffer_rx_sync(srsran_softbuffer_rx_t* q);
+
+/* ---------------- grant / PDSCH configuration (ra.h:43-53, pdsch_cfg.h:37-71) ---------------- */
+typedef enum {
+  SRSRAN_MOD_BPSK = 0,
+  SRSRAN_MOD_QPSK,
+  SRSRAN_MOD_16QAM,
+  SRSRAN_MOD_64QAM,
+  SRSRAN_MOD_256QAM,
+  SRSRAN_MOD_NITEMS
+} srsran_mod_t; /* phy_common.h:285-292 */
+
+typedef enum {
+  SRSRAN_TXSCHEME_PORT0,
+  SRSRAN_TXSCHEME_DIVERSITY,
+  SRSRAN_TXSCHEME_SPATIALMUX,
+  SRSRAN_TXSCHEME_CDD
+} srsran_tx_scheme_t; /* phy_common.h:273-278 */
+
+typedef enum { SRSRAN_MIMO_DECODER_ZF, SRSRAN_MIMO_DECODER_MMSE } srsran_mimo_decoder_t; /* phy_common.h:280 */
+
+uint32_t srsran_mod_bits_x_symbol(srsran_mod_t mod); /* phy_common.c */
+
+typedef struct {
+  srsran_mod_t mod;
+  int          tbs;
+  int          rv;
+  uint32_t     nof_bits;
+  uint32_t     cw_idx;
+  bool         enabled;
+  uint32_t     mcs_idx;
+} srsran_ra_tb_t;
+
+typedef struct {
+  srsran_tx_scheme_t tx_scheme;
+  uint32_t           pmi;
+  bool               prb_idx[2][SRSRAN_MAX_PRB];
+  uint32_t           nof_prb;
+  uint32_t           nof_re;
+  uint32_t           nof_symb_slot[2];
+  srsran_ra_tb_t     tb[SRSRAN_MAX_CODEWORDS];
+  int                last_tbs[SRSRAN_MAX_CODEWORDS];
+  uint32_t           nof_tb;
+  uint32_t           nof_layers;
+} srsran_pdsch_grant_t;
+
+typedef struct {
+  srsran_pdsch_grant_t grant;
+
+  uint16_t              rnti;
+  uint32_t              max_nof_iterations;
+  srsran_mimo_decoder_t decoder_type;
+  float                 p_a;
+  uint32_t              p_b;
+  float                 rs_power;
+  bool                  power_scale;
+  bool                  csi_enable;
+  bool                  use_tbs_index_alt;
+
+  union {
+    void*                   tx[SRSRAN_MAX_CODEWORDS];
+    srsran_softbuffer_rx_t* rx[SRSRAN_MAX_CODEWORDS];
+  } softbuffers;
+
+  bool     meas_evm_en;
+  bool     meas_time_en;
+  uint32_t meas_time_value;
+} srsran_pdsch_cfg_t;
+
+/* ---------------- shared channel decoder (sch.h:52-100, sch.c:140-609) ---------------- */
+typedef struct {
+  uint32_t      max_iterations; /* half-iterations, default 10 (sch.c:36,165) */
+  float         avg_iterations;
+  bool          llr_is_8bit;
+  srsran_tdec_t decoder;
+  void*         gpu; /* added: stream, staging and scratch of the DL-SCH GPU path */
+} srsran_sch_t;
+
+int   srsran_sch_init(srsran_sch_t* q);
+void  srsran_sch_free(srsran_sch_t* q);
+void  srsran_sch_set_max_noi(srsran_sch_t* q, uint32_t max_iterations);
+float srsran_sch_last_noi(srsran_sch_t* q);
+
+/* e_bits: host int16 LLRs (grant.tb[tb_idx].nof_bits); data: host payload buffer, receives every byte
+ * the reference's decode_tb writes (tbs/8 + 3 bytes for one CB, up to tbs/8 + 6 for several). */
+int srsran_dlsch_decode(srsran_sch_t* q, srsran_pdsch_cfg_t* cfg, int16_t* e_bits, uint8_t* data);
+int srsran_dlsch_decode2(srsran_sch_t*       q,
+                         srsran_pdsch_cfg_t* cfg,
+                         int16_t*            e_bits,
+                         uint8_t*            data,
+                         int                 tb_idx,
+                         uint32_t            nof_layers);
+
+/* ---------------- added: batched, asynchronous DL-SCH decode over device buffers ----------------
+ * One entry per transport block; every entry is decoded with exactly the semantics of
+ * decode_tb (sch.c:509-573) against its own soft buffer.  Results land in device memory:
+ *   d_result[i]  = SRSRAN_SUCCESS / SRSRAN_ERROR / SRSRAN_ERROR_INVALID_INPUTS (decode_tb's return)
+ *   d_avg_noi[i] = avg_iterations of that TB (sch.c:489)
+ * Soft buffer flags are updated on the device; call srsran_softbuffer_rx_sync() to read them on
+ * the host.  `stream` is a hipStream_t (NULL = the sch object's own stream).  q->max_iterations
+ * applies to every TB.  Returns SRSRAN_SUCCESS once the work is enqueued. */
+typedef struct {
+  uint32_t                tbs;
+  uint32_t                Qm; /* bits per symbol x layers, as decode_tb receives it */
+  uint32_t                rv;
+  uint32_t                nof_e_bits;
+  const int16_t*          d_e_bits; /* device */
+  uint8_t*                d_data;   /* device, >= tbs/8 + 6 bytes */
+  srsran_softbuffer_rx_t* softbuffer;
+} srsran_dlsch_gpu_tb_t;
+
+int srsran_dlsch_gpu_decode_batch(srsran_sch_t*                q,
+                                  uint32_t                     nof_tb,
+                                  const srsran_dlsch_gpu_tb_t* tbs,
+                                  int32_t*                     d_result,
+                                  float*                       d_avg_noi,
+                                  void*                        stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

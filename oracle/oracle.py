@@ -119,6 +119,7 @@ class Oracle(_Lib):
         L.oracle_dlsch_decode_tb.argtypes = [u32, u32, u32, u32, _i16p, u32, _i16p, u32, _u8p, _u8p, u32, _u8p,
                                              ctypes.POINTER(u32), ctypes.POINTER(ctypes.c_float)]
         L.oracle_dlsch_encode_tb.argtypes = [u32, u32, u32, u32, _u8p, _u8p]
+        L.oracle_dlsch_encode_tb_x.argtypes = [u32, u32, u32, u32, _u8p, _u8p, u32]
 
     def crc_byte(self, poly, order, data, nbits):
         self._sch_sigs()
@@ -156,17 +157,21 @@ class Oracle(_Lib):
         self.lib.oracle_rm_turbo_tx(K, rv, _ptr(coded, _u8p), E, _ptr(out, _u8p))
         return out
 
-    def dlsch_encode(self, tbs, Qm, rv, nof_e_bits, tb_bytes):
+    def dlsch_encode(self, tbs, Qm, rv, nof_e_bits, tb_bytes, tb_crc_xor=0):
         self._sch_sigs()
         tb_bytes = np.ascontiguousarray(tb_bytes, dtype=np.uint8)
         e = np.zeros(nof_e_bits, dtype=np.uint8)
-        n = self.lib.oracle_dlsch_encode_tb(tbs, Qm, rv, nof_e_bits, _ptr(tb_bytes, _u8p), _ptr(e, _u8p))
+        n = self.lib.oracle_dlsch_encode_tb_x(tbs, Qm, rv, nof_e_bits, _ptr(tb_bytes, _u8p), _ptr(e, _u8p),
+                                              tb_crc_xor)
         if n < 0:
             raise ValueError(f"encode failed tbs={tbs}")
         return e
 
     def dlsch_decode(self, tbs, Qm, rv, e_llr, max_iterations, state=None):
-        """decode_tb (sch.c:509-573). state = (softbuf[C,18600], cb_crc[C], cb_data[C,768]) for HARQ."""
+        """decode_tb (sch.c:509-573). state = (softbuf[C,18600], cb_crc[C], cb_data[C,768]) for HARQ.
+
+        Returns (ret, data, noi, avg, state); data is the whole zero-initialised payload
+        buffer (tbs/8 + 8 bytes) so bytes written past tbs/8 (CRC bytes) are compared too."""
         self._sch_sigs()
         rc, s = self.cbsegm(tbs)
         C = max(1, s["C"])
@@ -180,7 +185,7 @@ class Oracle(_Lib):
         ret = self.lib.oracle_dlsch_decode_tb(tbs, Qm, rv, e_llr.size, _ptr(e_llr, _i16p), max_iterations,
                                               _ptr(sb, _i16p), sb.shape[1], _ptr(crc, _u8p), _ptr(cbd, _u8p),
                                               cbd.shape[1], _ptr(data, _u8p), noi, ctypes.byref(avg))
-        return ret, data[: tbs // 8], list(noi), avg.value, state
+        return ret, data, list(noi), avg.value, state
 
     def run_batch(self, K, llr2d, layout_sb, nof_iterations):
         llr2d = np.ascontiguousarray(llr2d, dtype=np.int16)

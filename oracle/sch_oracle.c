@@ -215,6 +215,9 @@ int oracle_dlsch_decode_tb(uint32_t       tbs,
   if (s.F) {
     return -2;
   }
+  if (s.C > 32) { /* SRSRAN_MAX_CODEBLOCKS (sch.c:383-386) */
+    return -1;
+  }
   float avg = 0;
   for (uint32_t cb = 0; cb < s.C; cb++) {
     const uint32_t cb_len = cb < s.C1 ? s.K1 : s.K2;
@@ -301,6 +304,19 @@ int oracle_dlsch_decode_tb(uint32_t       tbs,
 /* ---------------- DL-SCH encode (synthetic TBs; sch.c encode_tb semantics, K- first) ---------------- */
 int oracle_dlsch_encode_tb(uint32_t tbs, uint32_t Qm, uint32_t rv, uint32_t nof_e_bits, const uint8_t* tb_bytes, uint8_t* e_bits)
 {
+  return oracle_dlsch_encode_tb_x(tbs, Qm, rv, nof_e_bits, tb_bytes, e_bits, 0);
+}
+
+/* tb_crc_xor != 0 corrupts the TB CRC24A before CB segmentation: every CB CRC then passes
+ * while the TB CRC fails (exercises sch.c:558-570). */
+int oracle_dlsch_encode_tb_x(uint32_t       tbs,
+                             uint32_t       Qm,
+                             uint32_t       rv,
+                             uint32_t       nof_e_bits,
+                             const uint8_t* tb_bytes,
+                             uint8_t*       e_bits,
+                             uint32_t       tb_crc_xor)
+{
   oracle_cbsegm_t s;
   if (oracle_cbsegm(tbs, &s) || s.F) {
     return -1;
@@ -308,7 +324,7 @@ int oracle_dlsch_encode_tb(uint32_t tbs, uint32_t Qm, uint32_t rv, uint32_t nof_
   /* TB bits + CRC24A */
   uint8_t* tb = malloc(tbs / 8 + 3);
   memcpy(tb, tb_bytes, tbs / 8);
-  uint32_t crc = oracle_crc_checksum_byte(LTE_CRC24A, 24, tb, tbs);
+  uint32_t crc = oracle_crc_checksum_byte(LTE_CRC24A, 24, tb, tbs) ^ tb_crc_xor;
   tb[tbs / 8]     = (uint8_t)(crc >> 16);
   tb[tbs / 8 + 1] = (uint8_t)(crc >> 8);
   tb[tbs / 8 + 2] = (uint8_t)crc;

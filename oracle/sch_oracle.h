@@ -30,4 +30,6 @@ int      oracle_dlsch_decode_tb(uint32_t       tbs,
                                 float*         avg_iterations);
 int      oracle_dlsch_encode_tb(uint32_t tbs, uint32_t Qm, uint32_t rv, uint32_t nof_e_bits, const uint8_t* tb_bytes,
                                 uint8_t* e_bits);
+int      oracle_dlsch_encode_tb_x(uint32_t tbs, uint32_t Qm, uint32_t rv, uint32_t nof_e_bits, const uint8_t* tb_bytes,
+                                  uint8_t* e_bits, uint32_t tb_crc_xor);
 #endif

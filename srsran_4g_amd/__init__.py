@@ -4,3 +4,4 @@ The product is the C-ABI library built from srsran_4g_amd/csrc (HIP for gfx950),
 declared in include/srsran_tdec.h.  ``srsran_4g_amd.tdec`` binds it for Python.
 """
 from . import tdec  # noqa: F401
+from . import sch  # noqa: F401

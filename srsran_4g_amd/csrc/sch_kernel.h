@@ -1,0 +1,50 @@
+// srsran_4g_amd/csrc/sch_kernel.h -- launch interface of the DL-SCH kernels.
+//
+// A DL-SCH batch is a set of transport blocks; each TB owns C consecutive "slots"
+// (one per code block).  Three kernels run in order on one stream:
+//   1. rm_rx_kernel     rate de-matching of every slot into its HARQ soft buffer
+//                       (srsran_rm_turbo_rx_lut, rm_turbo.c:390-483)
+//   2. tdec_kernel<ES>  turbo decode with CRC early stop (decode_tb_cb, sch.c:420-456)
+//   3. tb_kernel        TB assembly, CB bookkeeping, TB CRC (sch.c:458-573)
+#ifndef SRSRAN_AMD_SCH_KERNEL_H
+#define SRSRAN_AMD_SCH_KERNEL_H
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace srsran_amd {
+
+static constexpr int SCH_SLOT_BYTES = 768;  // decision bytes per slot (K <= 6144)
+static constexpr int SCH_MAX_CB     = 32;   // SRSRAN_MAX_CODEBLOCKS (phy_common.h:64)
+
+struct RmSlot {
+  const short*    e;     // the CB's E rate-matched LLRs (device)
+  short*          sb;    // the CB's soft buffer (device)
+  const uint8_t*  skip;  // soft buffer cb_crc flag: set -> not de-matched (sch.c:392)
+  const uint16_t* inv;   // layout position -> circular-buffer index, 0xFFFF for padding
+  uint32_t        E;
+  uint32_t        len;   // positions in the soft buffer layout (3K+12 or 3(K+32)+12)
+  uint32_t        N;     // 3K+12: period of the circular buffer after dummy removal
+  uint32_t        pad;
+};
+
+struct SchTb {
+  uint8_t*       data;      // TB payload (device)
+  const uint8_t* cbout;     // decision bytes per slot (SCH_SLOT_BYTES apart)
+  const uint8_t* noi;       // per slot: half-iterations (0 = skipped)
+  const uint8_t* crc_ok;    // per slot
+  uint8_t*       cb_crc;    // soft buffer flags (device, max_cb)
+  uint8_t*       tb_crc;    // soft buffer TB flag (device)
+  uint8_t*       saved;     // soft buffer saved payloads (device)
+  int32_t*       result;    // decode_tb return value (device)
+  float*         avg;       // avg_iterations (device)
+  uint32_t       saved_stride;
+  uint32_t       slot0;
+  uint32_t       C, C1, K1, K2, tbs;
+  int32_t        status;    // 1: decoded; otherwise the return value of a host-side check
+};
+
+hipError_t rm_rx_launch(const RmSlot* d_slots, uint32_t nslots, uint32_t max_len, hipStream_t stream);
+hipError_t tb_launch(const SchTb* d_tbs, uint32_t ntb, hipStream_t stream);
+
+}  // namespace srsran_amd
+#endif

@@ -243,7 +243,83 @@ bool grow(void** p, size_t* have, size_t need)
   return true;
 }
 
+// x^(8m) mod CRC24A / CRC24B, m = 0..768, for the in-kernel CB CRC (device, built once)
+const uint32_t* g_xpow[2] = {nullptr, nullptr};
+
+bool xpow_tables()
+{
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (g_xpow[0]) {
+    return true;
+  }
+  const int             nm = SRSRAN_TCOD_MAX_LEN_CB / 8 + 1;
+  std::vector<uint32_t> h(nm);
+  uint32_t*             d[2] = {nullptr, nullptr};
+  const uint32_t        poly[2] = {LTE_CRC24A, LTE_CRC24B};
+  for (int i = 0; i < 2; i++) {
+    crc24_xpow_table(poly[i], h.data(), nm);
+    if (hipMalloc(&d[i], nm * sizeof(uint32_t)) != hipSuccess ||
+        hipMemcpy(d[i], h.data(), nm * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) {
+      return false;
+    }
+  }
+  g_xpow[0] = d[0];
+  g_xpow[1] = d[1];
+  return true;
+}
+
 }  // namespace
+
+namespace srsran_amd {
+
+int tdec_cb_index(uint32_t K) { return cb_index(K); }
+
+int tdec_sch_enqueue(uint32_t      K,
+                     const TdecCb* d_cbs,
+                     uint32_t      ncb,
+                     uint8_t*      d_out,
+                     uint32_t      out_stride,
+                     uint8_t*      d_noi,
+                     uint8_t*      d_crc_ok,
+                     int           n_end,
+                     hipStream_t   stream)
+{
+  if (ncb == 0) {
+    return SRSRAN_SUCCESS;
+  }
+  Config* c = get_config(K, auto_nsb(K));
+  if (!c || !xpow_tables()) {
+    return SRSRAN_ERROR;
+  }
+  TdecArgs a   = c->proto;
+  a.in         = nullptr;
+  a.in_stride  = 0;
+  a.layout_sb  = c->nsb > 1 ? 1 : 0;  // soft buffer layout (rm_turbo.c:403-418)
+  a.ncb        = ncb;
+  a.n_start    = 0;
+  a.n_end      = n_end > 0 ? n_end : 1;
+  a.out        = d_out;
+  a.tfwd       = c->d_tfwd;
+  a.trev       = c->d_trev;
+  a.tfwd_nat   = c->d_tfwd_nat;
+  a.trev_nat   = c->d_trev_nat;
+  a.state      = nullptr;
+  a.cbs        = d_cbs;
+  a.out_stride = out_stride;
+  a.noi_out    = d_noi;
+  a.crc_ok     = d_crc_ok;
+  a.xpow_a     = g_xpow[0];
+  a.xpow_b     = g_xpow[1];
+  a.min_iters  = 2;  // SRSRAN_PDSCH_MIN_TDEC_ITERS (sch.c:35)
+  hipError_t e = tdec_launch(c->nsb, a, stream);
+  if (e != hipSuccess) {
+    fprintf(stderr, "[srsran_sch] turbo launch failed: %s\n", hipGetErrorString(e));
+    return SRSRAN_ERROR;
+  }
+  return SRSRAN_SUCCESS;
+}
+
+}  // namespace srsran_amd
 
 extern "C" {
 

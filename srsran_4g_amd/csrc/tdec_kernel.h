@@ -10,6 +10,14 @@ namespace srsran_amd {
 static constexpr int TDEC_W       = 32;  // beta checkpoint window (must match the kernel)
 static constexpr int TDEC_OVERLAP = 40;  // sliding-window training length
 
+// One code block of a DL-SCH decode (launch-index order).
+struct TdecCb {
+  const short*   in;    // soft buffer of the block (rate de-matched LLRs)
+  const uint8_t* skip;  // soft buffer cb_crc flag: set -> block already decoded (sch.c:392)
+  uint32_t       slot;  // index into out / noi_out / crc_ok
+  uint32_t       crc_a; // 1 -> CRC24A over tbs+24 (single-CB TB), 0 -> CRC24B (sch.c:440-446)
+};
+
 struct TdecArgs {
   const short*    in;        // ncb code blocks, in_stride int16 apart (device)
   uint32_t        in_stride;
@@ -30,10 +38,37 @@ struct TdecArgs {
   uint32_t        M;         // beta checkpoints per sub-block
   uint32_t        magicL;    // ceil(2^32 / L)
   uint32_t        dbg;       // profiling ablation only (SRSRAN_TDEC_ABLATE): bit0 skip prepare, bit1 skip MAP
+  // ---- DL-SCH mode (decode_tb_cb, sch.c:391-456): enabled when cbs != nullptr ----
+  const struct TdecCb* cbs;  // per launch index: input pointer, skip flag, output slot, CRC type
+  uint32_t        out_stride; // bytes between output slots
+  uint8_t*        noi_out;   // per slot: half-iterations run (0 = skipped, CRC already OK)
+  uint8_t*        crc_ok;    // per slot: 1 if the block's CRC passed (or it was skipped)
+  const uint32_t* xpow_a;    // x^(8m) mod CRC24A, m = 0..768 (device)
+  const uint32_t* xpow_b;    // x^(8m) mod CRC24B
+  int             min_iters; // early stop needs at least this many half-iterations (sch.c:35)
 };
+
+static constexpr uint32_t LTE_CRC24A = 0x1864CFB;  // phy_common.h:72
+static constexpr uint32_t LTE_CRC24B = 0x1800063;  // phy_common.h:73
 
 hipError_t tdec_launch(int nsb, const TdecArgs& a, hipStream_t stream);
 size_t     tdec_lds_bytes(int nsb, int xyw, int M);
+// x^(8m) mod poly for m = 0..nm-1 (host helper for the CRC combine tables)
+void crc24_xpow_table(uint32_t poly, uint32_t* out, int nm);
+
+// DL-SCH decode of ncb code blocks of size K (tdec_api.cpp): AUTO decoder, soft
+// buffer layout (SB for K >= 408), CRC early stop after >= 2 half-iterations, at
+// most n_end half-iterations; decisions to d_out + slot * out_stride.
+int tdec_sch_enqueue(uint32_t      K,
+                     const TdecCb* d_cbs,
+                     uint32_t      ncb,
+                     uint8_t*      d_out,
+                     uint32_t      out_stride,
+                     uint8_t*      d_noi,
+                     uint8_t*      d_crc_ok,
+                     int           n_end,
+                     hipStream_t   stream);
+int tdec_cb_index(uint32_t K);
 
 }  // namespace srsran_amd
 #endif

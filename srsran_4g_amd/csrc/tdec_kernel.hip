@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "crc24_dev.h"
 #include "tdec_kernel.h"
 
 namespace srsran_amd {
@@ -450,7 +451,7 @@ __device__ __forceinline__ uint32_t pack2(short lo, short hi)
   return (uint32_t)(uint16_t)lo | ((uint32_t)(uint16_t)hi << 16);
 }
 
-template <int NSB>
+template <int NSB, bool ES>
 __global__ __launch_bounds__(128, 2) void tdec_kernel(TdecArgs a)
 {
   using Gm                = Geo<NSB>;
@@ -458,7 +459,6 @@ __global__ __launch_bounds__(128, 2) void tdec_kernel(TdecArgs a)
   constexpr int  G        = Gm::G;        // lanes per code block in one wave
   constexpr int  G2       = 2 * G;        // threads per code block in the workgroup
   constexpr int  LOG_NSB  = NSB == 16 ? 4 : (NSB == 8 ? 3 : 0);
-  constexpr int  U        = 4;            // positions per thread per batch in the prepare phase
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
 
   const int wave = threadIdx.x >> 6;
@@ -473,26 +473,52 @@ __global__ __launch_bounds__(128, 2) void tdec_kernel(TdecArgs a)
   const int Ls   = a.Ls;
   const int XYW  = a.xyw;
   const int M    = a.M;
-  const int cb   = blockIdx.x * Gm::CPW + cw;
+  const int cb   = blockIdx.x * Gm::CPW + cw;  // launch index
   const bool live = cb < (int)a.ncb;
-  const int cbr  = live ? cb : (int)a.ncb - 1;
+  const int cbl  = live ? cb : (int)a.ncb - 1;
+  const TdecCb* cbd = ES ? &a.cbs[cbl] : nullptr;
+  const int cbm  = ES ? (int)cbd->slot : cbl;  // output / state slot
+  const bool crc_a = ES && cbd->crc_a;
+  // DL-SCH mode: blocks whose CRC already passed are not decoded; padding blocks
+  // never hold back the workgroup's early exit.
+  bool done = ES && (!live || *cbd->skip);
+  const int ostr = ES ? (int)a.out_stride : K / 8;
 
   Smem sm;
   sm.xy  = smem;
   sm.aux = reinterpret_cast<short*>(smem + Gm::CPW * XYW);
   sm.ck  = smem + Gm::CPW * XYW + (Gm::CPW * XYW + 1) / 2;
+  uint32_t* red  = sm.ck + M * 64;  // [CPW][2] CRC partials per wave
   uint32_t* xyc  = sm.xy + cw * XYW;
   short*    xylo = reinterpret_cast<short*>(xyc);
   short*    auxc = sm.aux + cw * XYW;
 
-  const short* in = a.in + (size_t)cbr * a.in_stride;
+  // Hard decision byte b (bits 8b..8b+7, MSB first) of the latest decoder output:
+  // ext1 after DEC1 (natural slots), app1 = ext2 de-interleaved after DEC2.
+  auto decide_byte = [&](int b, bool after_dec1) -> uint32_t {
+    uint32_t byte = 0;
+#pragma unroll
+    for (int t = 0; t < 8; t++) {
+      const int n = 8 * b + t;
+      int       sl;
+      if constexpr (NSB > 1) {
+        const int sb_ = (int)__umulhi((uint32_t)n, a.magicL);  // n / L
+        sl            = sb_ * Ls + (n - sb_ * L);
+      } else {
+        sl = n;
+      }
+      const short v = after_dec1 ? xylo[2 * sl] : xylo[2 * a.trev_nat[n]];
+      byte |= (uint32_t)(v > 0) << (7 - t);
+    }
+    return byte;
+  };
+
+  const short* in = ES ? cbd->in : a.in + (size_t)cbl * a.in_stride;
   const bool   sb = a.layout_sb;
   // Positions are visited in "q order": the rm_turbo sub-block order for window
   // decoders (q = k*NSB + s, coalesced in the SB input), natural order otherwise.
   auto qslot = [&](int q) -> int { return NSB > 1 ? (q & (NSB - 1)) * Ls + (q >> LOG_NSB) : q; };
   auto qnat  = [&](int q) -> int { return NSB > 1 ? (q & (NSB - 1)) * L + (q >> LOG_NSB) : q; };
-  // stream c (0 = systematic, 1 = parity0, 2 = parity1) at position q
-  auto inq = [&](int c, int q) -> short { return sb ? in[c * (K + 32) + q] : in[3 * qnat(q) + c]; };
   const short* tail = sb ? in + 3 * (K + 32) : in + 3 * K;
   short st[3], p0t[3], x2t[3], p1t[3];
 #pragma unroll
@@ -588,7 +614,7 @@ __global__ __launch_bounds__(128, 2) void tdec_kernel(TdecArgs a)
 
   // restore state from a previous launch (srsran_tdec_iteration path)
   if (a.n_start > 0) {
-    const short* se = a.state + (size_t)cbr * 2 * XYW;
+    const short* se = a.state + (size_t)cbm * 2 * XYW;
     for (int i = t2; i < XYW; i += G2) {
       xylo[2 * i] = se[i];
       auxc[i]     = se[XYW + i];
@@ -600,7 +626,14 @@ __global__ __launch_bounds__(128, 2) void tdec_kernel(TdecArgs a)
   const int Nb   = NSB > 1 ? L : K + 3;
   const int La   = NSB > 1 ? L : K;
 
-  for (int h = a.n_start; h < a.n_end; h++) {
+  if constexpr (ES) {
+    if (live && done && t2 == 0) {  // skipped block (sch.c:392, 476-480)
+      a.noi_out[cbm] = 0;
+      a.crc_ok[cbm]  = 1;
+    }
+  }
+  const int h_end = (ES && __syncthreads_or(!done) == 0) ? a.n_start : a.n_end;
+  for (int h = a.n_start; h < h_end; h++) {
     // -------- prepare branch inputs (turbodecoder_iter.h:104-128) --------
     // Each thread owns chunks of 4 consecutive positions in visit order (SB order
     // for window decoders on SB input, natural order otherwise); all its global
@@ -650,31 +683,64 @@ __global__ __launch_bounds__(128, 2) void tdec_kernel(TdecArgs a)
       map_decode<NSB>(sm, base, wave, lane, j, s, K, L, Nb, La, M, dec1 ? st : x2t, dec1 ? p0t : p1t);
     }
     __syncthreads();
+
+    // -------- DL-SCH early stop: CRC of the hard decision (sch.c:426-456) --------
+    if constexpr (ES) {
+      if (h + 1 >= a.min_iters) {
+        // this thread's contiguous chunk of decision bytes, CRC'd from zero, then
+        // shifted to its place by x^(8*bytes_after) mod P and XOR-combined
+        const int nbytes = K / 8;
+        const int bpt    = (nbytes + G2 - 1) / G2;
+        const int b0     = t2 * bpt;
+        const uint32_t poly = crc_a ? LTE_CRC24A : LTE_CRC24B;
+        uint32_t       crc  = 0;
+        const int      b1   = min(b0 + bpt, nbytes);
+#pragma unroll 1
+        for (int b = b0; b < b1; b++) {
+          crc = crc24_byte(crc, decide_byte(b, dec1), poly);
+        }
+        uint32_t part = b0 < nbytes ? clmul_mod24(crc, (crc_a ? a.xpow_a : a.xpow_b)[nbytes - b1], poly) : 0;
+#pragma unroll
+        for (int off = 1; off < G; off <<= 1) {
+          part ^= (uint32_t)__shfl_xor((int)part, off, 64);
+        }
+        if (g == 0) {
+          red[cw * 2 + wave] = part;
+        }
+        __syncthreads();
+        const bool ok = (red[cw * 2] ^ red[cw * 2 + 1]) == 0;
+        if (ok && !done && live) {
+          uint8_t* out = a.out + (size_t)cbm * ostr;
+#pragma unroll 1
+          for (int b = b0; b < b1; b++) {
+            out[b] = (uint8_t)decide_byte(b, dec1);
+          }
+          if (t2 == 0) {
+            a.noi_out[cbm] = (uint8_t)(h + 1);
+            a.crc_ok[cbm]  = 1;
+          }
+        }
+        done = done || ok;
+      }
+      if (__syncthreads_or(!done) == 0) {
+        break;  // every code block of this workgroup has passed its CRC
+      }
+    }
   }
 
   // -------- hard decision (turbodecoder.c:370-378), natural bit order --------
   const bool last_dec1 = ((a.n_end - 1) & 1) == 0;
-  if (live) {
-    uint8_t* out = a.out + (size_t)cb * (K / 8);
+  if (live && !done) {
+    uint8_t* out = a.out + (size_t)cbm * ostr;
     for (int b = t2; b < K / 8; b += G2) {
-      uint32_t byte = 0;
-#pragma unroll
-      for (int t = 0; t < 8; t++) {
-        const int n = 8 * b + t;
-        int       sl;
-        if constexpr (NSB > 1) {
-          const int sb_ = (int)__umulhi((uint32_t)n, a.magicL);  // n / L
-          sl            = sb_ * Ls + (n - sb_ * L);
-        } else {
-          sl = n;
-        }
-        const short v = last_dec1 ? xylo[2 * sl] : xylo[2 * a.trev_nat[n]];
-        byte |= (uint32_t)(v > 0) << (7 - t);
-      }
-      out[b] = (uint8_t)byte;
+      out[b] = (uint8_t)decide_byte(b, last_dec1);
+    }
+    if (ES && t2 == 0) {
+      a.noi_out[cbm] = (uint8_t)a.n_end;
+      a.crc_ok[cbm]  = 0;
     }
     if (a.state) {
-      short* se = a.state + (size_t)cb * 2 * XYW;
+      short* se = a.state + (size_t)cbm * 2 * XYW;
       for (int i = t2; i < XYW; i += G2) {
         se[i]       = xylo[2 * i];
         se[XYW + i] = auxc[i];
@@ -689,7 +755,11 @@ static hipError_t launch(const TdecArgs& a, hipStream_t stream)
   const int    cpw  = Geo<NSB>::CPW;
   const int    grid = (a.ncb + cpw - 1) / cpw;
   const size_t lds  = tdec_lds_bytes(NSB, a.xyw, a.M);
-  hipLaunchKernelGGL(tdec_kernel<NSB>, dim3(grid), dim3(128), lds, stream, a);
+  if (a.cbs) {
+    hipLaunchKernelGGL((tdec_kernel<NSB, true>), dim3(grid), dim3(128), lds, stream, a);
+  } else {
+    hipLaunchKernelGGL((tdec_kernel<NSB, false>), dim3(grid), dim3(128), lds, stream, a);
+  }
   return hipGetLastError();
 }
 
@@ -713,7 +783,19 @@ hipError_t tdec_launch(int nsb, const TdecArgs& a, hipStream_t stream)
 size_t tdec_lds_bytes(int nsb, int xyw, int M)
 {
   const int cpw = 64 / (4 * nsb);
-  return (size_t)cpw * xyw * 4 + (((size_t)cpw * xyw + 1) / 2) * 4 + (size_t)M * 64 * 4;
+  return (size_t)cpw * xyw * 4 + (((size_t)cpw * xyw + 1) / 2) * 4 + (size_t)M * 64 * 4 + (size_t)cpw * 2 * 4;
+}
+
+void crc24_xpow_table(uint32_t poly, uint32_t* out, int nm)
+{
+  uint32_t v = 1;  // x^0
+  for (int m = 0; m < nm; m++) {
+    out[m] = v;
+    for (int k = 0; k < 8; k++) {  // v *= x (mod P)
+      v = (v & 0x800000u) ? ((v << 1) ^ poly) : (v << 1);
+      v &= 0xFFFFFFu;
+    }
+  }
 }
 
 }  // namespace srsran_amd

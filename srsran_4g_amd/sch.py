@@ -1,0 +1,287 @@
+"""Python mirror of the DL-SCH C API (include/srsran_sch.h).
+
+Binds cbsegm, CRC, rate de-matching, HARQ soft buffers and the DL-SCH decoder
+(sch.c:371-609) of the in-tree HIP library, the way the reference's pdsch_test.c
+drives srsran_dlsch_decode.  No CPU fallback: every decode runs the HIP kernels.
+"""
+import ctypes
+
+import numpy as np
+
+from .tdec import SRSRAN_TCOD_MAX_LEN_CB, load_library, srsran_tdec_t  # noqa: F401
+
+SRSRAN_MAX_PRB = 110
+SRSRAN_MAX_CODEWORDS = 2
+SRSRAN_MAX_CODEBLOCKS = 32
+SOFTBUFFER_SIZE = 18600
+SRSRAN_LTE_CRC24A = 0x1864CFB
+SRSRAN_LTE_CRC24B = 0x1800063
+
+SRSRAN_MOD_BPSK, SRSRAN_MOD_QPSK, SRSRAN_MOD_16QAM, SRSRAN_MOD_64QAM, SRSRAN_MOD_256QAM = range(5)
+MOD_FROM_QM = {1: SRSRAN_MOD_BPSK, 2: SRSRAN_MOD_QPSK, 4: SRSRAN_MOD_16QAM, 6: SRSRAN_MOD_64QAM, 8: SRSRAN_MOD_256QAM}
+
+u32 = ctypes.c_uint32
+
+
+class srsran_cbsegm_t(ctypes.Structure):
+    _fields_ = [(n, u32) for n in ("F", "C", "K1", "K2", "K1_idx", "K2_idx", "C1", "C2", "tbs", "L_tb", "L_cb", "Z")]
+
+
+class srsran_crc_t(ctypes.Structure):
+    _fields_ = [("table", ctypes.c_uint64 * 256), ("polynom", ctypes.c_int), ("order", ctypes.c_int),
+                ("crcinit", ctypes.c_uint64), ("crcmask", ctypes.c_uint64), ("crchighbit", ctypes.c_uint64),
+                ("srsran_crc_out", u32)]
+
+
+class srsran_softbuffer_rx_t(ctypes.Structure):
+    _fields_ = [("max_cb", u32), ("max_cb_size", u32), ("buffer_f", ctypes.POINTER(ctypes.c_void_p)),
+                ("data", ctypes.POINTER(ctypes.c_void_p)), ("cb_crc", ctypes.POINTER(ctypes.c_bool)),
+                ("tb_crc", ctypes.c_bool), ("gpu", ctypes.c_void_p)]
+
+
+class srsran_ra_tb_t(ctypes.Structure):
+    _fields_ = [("mod", ctypes.c_int), ("tbs", ctypes.c_int), ("rv", ctypes.c_int), ("nof_bits", u32),
+                ("cw_idx", u32), ("enabled", ctypes.c_bool), ("mcs_idx", u32)]
+
+
+class srsran_pdsch_grant_t(ctypes.Structure):
+    _fields_ = [("tx_scheme", ctypes.c_int), ("pmi", u32), ("prb_idx", (ctypes.c_bool * SRSRAN_MAX_PRB) * 2),
+                ("nof_prb", u32), ("nof_re", u32), ("nof_symb_slot", u32 * 2),
+                ("tb", srsran_ra_tb_t * SRSRAN_MAX_CODEWORDS), ("last_tbs", ctypes.c_int * SRSRAN_MAX_CODEWORDS),
+                ("nof_tb", u32), ("nof_layers", u32)]
+
+
+class _softbuffers(ctypes.Union):
+    _fields_ = [("tx", ctypes.c_void_p * SRSRAN_MAX_CODEWORDS),
+                ("rx", ctypes.POINTER(srsran_softbuffer_rx_t) * SRSRAN_MAX_CODEWORDS)]
+
+
+class srsran_pdsch_cfg_t(ctypes.Structure):
+    _fields_ = [("grant", srsran_pdsch_grant_t), ("rnti", ctypes.c_uint16), ("max_nof_iterations", u32),
+                ("decoder_type", ctypes.c_int), ("p_a", ctypes.c_float), ("p_b", u32), ("rs_power", ctypes.c_float),
+                ("power_scale", ctypes.c_bool), ("csi_enable", ctypes.c_bool), ("use_tbs_index_alt", ctypes.c_bool),
+                ("softbuffers", _softbuffers), ("meas_evm_en", ctypes.c_bool), ("meas_time_en", ctypes.c_bool),
+                ("meas_time_value", u32)]
+
+
+class srsran_sch_t(ctypes.Structure):
+    _fields_ = [("max_iterations", u32), ("avg_iterations", ctypes.c_float), ("llr_is_8bit", ctypes.c_bool),
+                ("decoder", srsran_tdec_t), ("gpu", ctypes.c_void_p)]
+
+
+class srsran_dlsch_gpu_tb_t(ctypes.Structure):
+    _fields_ = [("tbs", u32), ("Qm", u32), ("rv", u32), ("nof_e_bits", u32), ("d_e_bits", ctypes.c_void_p),
+                ("d_data", ctypes.c_void_p), ("softbuffer", ctypes.POINTER(srsran_softbuffer_rx_t))]
+
+
+_i16p = ctypes.POINTER(ctypes.c_int16)
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_bound = False
+
+
+def lib():
+    global _bound
+    L = load_library()
+    if _bound:
+        return L
+    SB = ctypes.POINTER(srsran_softbuffer_rx_t)
+    SCH = ctypes.POINTER(srsran_sch_t)
+    CFG = ctypes.POINTER(srsran_pdsch_cfg_t)
+    CRC = ctypes.POINTER(srsran_crc_t)
+    sig = {
+        "srsran_cbsegm": ([ctypes.POINTER(srsran_cbsegm_t), u32], ctypes.c_int),
+        "srsran_cbsegm_cbsize": ([u32], ctypes.c_int),
+        "srsran_cbsegm_cbindex": ([u32], ctypes.c_int),
+        "srsran_cbsegm_cbsize_isvalid": ([u32], ctypes.c_bool),
+        "srsran_crc_init": ([CRC, u32, ctypes.c_int], ctypes.c_int),
+        "srsran_crc_set_init": ([CRC, ctypes.c_uint64], ctypes.c_int),
+        "srsran_crc_checksum_byte": ([CRC, _u8p, ctypes.c_int], u32),
+        "srsran_crc_match_byte": ([CRC, _u8p, ctypes.c_int], ctypes.c_bool),
+        "srsran_crc_attach_byte": ([CRC, _u8p, ctypes.c_int], u32),
+        "srsran_mod_bits_x_symbol": ([ctypes.c_int], u32),
+        "srsran_rm_turbo_gentables": ([], None),
+        "srsran_rm_turbo_free_tables": ([], None),
+        "srsran_rm_turbo_rx_lut": ([_i16p, _i16p, u32, u32, u32], ctypes.c_int),
+        "srsran_rm_turbo_rx_lut_": ([_i16p, _i16p, u32, u32, u32, ctypes.c_bool], ctypes.c_int),
+        "srsran_rm_turbo_rx_lut_8bit": ([ctypes.POINTER(ctypes.c_int8), ctypes.POINTER(ctypes.c_int8), u32, u32, u32],
+                                        ctypes.c_int),
+        "srsran_softbuffer_rx_init": ([SB, u32], ctypes.c_int),
+        "srsran_softbuffer_rx_init_guru": ([SB, u32, u32], ctypes.c_int),
+        "srsran_softbuffer_rx_reset": ([SB], None),
+        "srsran_softbuffer_rx_reset_tbs": ([SB, u32], None),
+        "srsran_softbuffer_rx_reset_cb": ([SB, u32], None),
+        "srsran_softbuffer_rx_reset_cb_crc": ([SB, u32], None),
+        "srsran_softbuffer_rx_free": ([SB], None),
+        "srsran_softbuffer_rx_sync": ([SB], ctypes.c_int),
+        "srsran_sch_init": ([SCH], ctypes.c_int),
+        "srsran_sch_free": ([SCH], None),
+        "srsran_sch_set_max_noi": ([SCH, u32], None),
+        "srsran_sch_last_noi": ([SCH], ctypes.c_float),
+        "srsran_dlsch_decode": ([SCH, CFG, _i16p, _u8p], ctypes.c_int),
+        "srsran_dlsch_decode2": ([SCH, CFG, _i16p, _u8p, ctypes.c_int, u32], ctypes.c_int),
+        "srsran_dlsch_gpu_decode_batch": ([SCH, u32, ctypes.POINTER(srsran_dlsch_gpu_tb_t), ctypes.c_void_p,
+                                           ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _bound = True
+    return L
+
+
+def cbsegm(tbs):
+    s = srsran_cbsegm_t()
+    ret = lib().srsran_cbsegm(ctypes.byref(s), tbs)
+    return ret, s
+
+
+def crc_checksum_byte(poly, data, nbits):
+    c = srsran_crc_t()
+    lib().srsran_crc_init(ctypes.byref(c), poly, 24)
+    d = np.ascontiguousarray(data, dtype=np.uint8)
+    return lib().srsran_crc_checksum_byte(ctypes.byref(c), d.ctypes.data_as(_u8p), nbits)
+
+
+def rm_turbo_rx_lut(e, softbuf, cb_idx, rv, enable_input_tdec=True):
+    """In place on a copy of softbuf; returns (ret, new softbuf)."""
+    e = np.ascontiguousarray(e, dtype=np.int16)
+    out = np.array(softbuf, dtype=np.int16, copy=True)
+    ret = lib().srsran_rm_turbo_rx_lut_(e.ctypes.data_as(_i16p), out.ctypes.data_as(_i16p), len(e), cb_idx, rv,
+                                        enable_input_tdec)
+    return ret, out
+
+
+class SoftbufferRx:
+    """srsran_softbuffer_rx_t owner (device arena)."""
+
+    def __init__(self, nof_prb=None, max_cb=None, max_cb_size=SOFTBUFFER_SIZE):
+        self.s = srsran_softbuffer_rx_t()
+        if nof_prb is not None:
+            ret = lib().srsran_softbuffer_rx_init(ctypes.byref(self.s), nof_prb)
+        else:
+            ret = lib().srsran_softbuffer_rx_init_guru(ctypes.byref(self.s), max_cb, max_cb_size)
+        if ret != 0:
+            raise RuntimeError(f"srsran_softbuffer_rx_init failed ({ret})")
+
+    @property
+    def max_cb(self):
+        return self.s.max_cb
+
+    def cb_crc(self, n=None):
+        n = self.s.max_cb if n is None else n
+        return [bool(self.s.cb_crc[i]) for i in range(n)]
+
+    def set_cb_crc(self, i, v):
+        self.s.cb_crc[i] = bool(v)
+
+    @property
+    def tb_crc(self):
+        return bool(self.s.tb_crc)
+
+    def reset(self):
+        lib().srsran_softbuffer_rx_reset(ctypes.byref(self.s))
+
+    def reset_tbs(self, tbs):
+        lib().srsran_softbuffer_rx_reset_tbs(ctypes.byref(self.s), tbs)
+
+    def reset_cb_crc(self, n):
+        lib().srsran_softbuffer_rx_reset_cb_crc(ctypes.byref(self.s), n)
+
+    def sync(self):
+        return lib().srsran_softbuffer_rx_sync(ctypes.byref(self.s))
+
+    def read_cb(self, i, n):
+        """Copy n int16 of code block i's device soft buffer to the host (test helper)."""
+        import torch  # device copies go through torch's HIP runtime
+        out = torch.empty(n, dtype=torch.int16)
+        _memcpy_d2h(out, self.s.buffer_f[i], n * 2)
+        return out.numpy()
+
+    def read_data(self, i, n):
+        import torch
+        out = torch.empty(n, dtype=torch.uint8)
+        _memcpy_d2h(out, self.s.data[i], n)
+        return out.numpy()
+
+    def free(self):
+        if self.s.gpu:
+            lib().srsran_softbuffer_rx_free(ctypes.byref(self.s))
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+_hip = None
+
+
+def _memcpy_d2h(host_tensor, dptr, nbytes):
+    """hipMemcpy device -> host through the HIP runtime already loaded by torch."""
+    global _hip
+    if _hip is None:
+        _hip = ctypes.CDLL("libamdhip64.so.7")
+        _hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        _hip.hipMemcpy.restype = ctypes.c_int
+    r = _hip.hipMemcpy(ctypes.c_void_p(host_tensor.data_ptr()), ctypes.c_void_p(dptr), nbytes, 2)
+    if r != 0:
+        raise RuntimeError(f"hipMemcpy failed ({r})")
+
+
+class Sch:
+    """srsran_sch_t owner with the reference's DL-SCH decode entry points."""
+
+    def __init__(self):
+        self.q = srsran_sch_t()
+        if lib().srsran_sch_init(ctypes.byref(self.q)) != 0:
+            raise RuntimeError("srsran_sch_init failed (no HIP device?)")
+
+    def set_max_noi(self, n):
+        lib().srsran_sch_set_max_noi(ctypes.byref(self.q), n)
+
+    @property
+    def max_iterations(self):
+        return self.q.max_iterations
+
+    def last_noi(self):
+        return lib().srsran_sch_last_noi(ctypes.byref(self.q))
+
+    def decode(self, softbuffer, tbs, Qm, rv, e_bits, nof_layers=1, nof_tb=1, tb_idx=0):
+        """srsran_dlsch_decode2 -> (ret, data bytes, avg_iterations)."""
+        cfg = srsran_pdsch_cfg_t()
+        cfg.grant.nof_tb = nof_tb
+        tb = cfg.grant.tb[tb_idx]
+        tb.mod = MOD_FROM_QM[Qm]
+        tb.tbs = tbs
+        tb.rv = rv
+        tb.nof_bits = len(e_bits)
+        tb.enabled = True
+        cfg.softbuffers.rx[tb_idx] = ctypes.pointer(softbuffer.s)
+        e = np.ascontiguousarray(e_bits, dtype=np.int16)
+        data = np.zeros(tbs // 8 + 64, np.uint8)
+        ret = lib().srsran_dlsch_decode2(ctypes.byref(self.q), ctypes.byref(cfg), e.ctypes.data_as(_i16p),
+                                         data.ctypes.data_as(_u8p), tb_idx, nof_layers)
+        return ret, data, self.last_noi()
+
+    def decode_batch(self, entries, d_result, d_avg, stream=None):
+        """srsran_dlsch_gpu_decode_batch over device buffers.
+
+        entries: list of (tbs, Qm, rv, nof_e_bits, d_e_bits ptr, d_data ptr, SoftbufferRx)."""
+        arr = (srsran_dlsch_gpu_tb_t * len(entries))()
+        for i, (tbs, Qm, rv, nbits, de, dd, sb) in enumerate(entries):
+            arr[i].tbs, arr[i].Qm, arr[i].rv, arr[i].nof_e_bits = tbs, Qm, rv, nbits
+            arr[i].d_e_bits, arr[i].d_data = de, dd
+            arr[i].softbuffer = ctypes.pointer(sb.s)
+        return lib().srsran_dlsch_gpu_decode_batch(ctypes.byref(self.q), len(entries), arr, d_result, d_avg, stream)
+
+    def free(self):
+        if self.q.gpu:
+            lib().srsran_sch_free(ctypes.byref(self.q))
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass

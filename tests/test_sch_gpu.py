@@ -1,0 +1,236 @@
+"""GPU parity of the DL-SCH receive path (rate de-matching + turbo decode with CRC
+early stop + TB assembly/CRC + HARQ soft buffers) against the oracle.
+
+The oracle's decode_tb (oracle/sch_oracle.c) restates sch.c:371-573 on top of the
+pinned turbo decoder / rm_turbo / CRC restatements.  Everything is compared
+bit-exactly: return code, every payload byte the reference writes (including the
+CRC bytes past tbs/8), avg_iterations, per-CB CRC flags, TB flag, soft-buffer
+contents and the saved payload of good CBs across HARQ retransmissions.
+"""
+import zlib
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import CB_SIZES, SOFTBUF_LEN, Oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ora():
+    return Oracle()
+
+
+@pytest.fixture(scope="module")
+def S():
+    from srsran_4g_amd import sch
+    return sch
+
+
+@pytest.fixture(scope="module")
+def q(S):
+    s = S.Sch()
+    yield s
+    s.free()
+
+
+def llrs(ora, tbs, Qm, rv, G, tb, sigma, rng, tb_crc_xor=0):
+    e = ora.dlsch_encode(tbs, Qm, rv, G, tb, tb_crc_xor).astype(np.float32) * 2 - 1
+    if sigma:
+        e = e + rng.standard_normal(e.shape).astype(np.float32) * sigma
+    return np.trunc(100 * e).astype(np.int16)
+
+
+def check_tb(S, q, ora, sb, tbs, Qm, rv, llr, max_iter, state, label):
+    """One decode on both sides; compares everything; returns the oracle state."""
+    q.set_max_noi(max_iter)
+    ret, data, avg = q.decode(sb, tbs, Qm, rv, llr)
+    oret, odata, onoi, oavg, state = ora.dlsch_decode(tbs, Qm, rv, llr, max_iter, state)
+    assert ret == oret, label
+    n = len(odata)
+    assert np.array_equal(data[:n], odata), label
+    assert not data[n:].any(), label
+    assert avg == pytest.approx(oavg, abs=0), label
+    rc, s = S.cbsegm(tbs)
+    C = s.C
+    flags = state[1][:C]
+    assert sb.cb_crc(C) == [bool(x) for x in flags], label
+    if ret == 0:
+        assert sb.tb_crc, label
+    elif flags.any():  # some CB failed: tb_crc false (sch.c:458-462)
+        assert not sb.tb_crc, label
+    for cb in range(C):
+        K = s.K1 if cb < s.C1 else s.K2
+        L = 3 * (K + 32) + 12 if K >= 408 else 3 * K + 12
+        assert np.array_equal(sb.read_cb(cb, L), state[0][cb][:L]), (label, cb)
+        if state[1][cb] and not ret == 0:
+            rlen = K if C == 1 else K - 24
+            assert np.array_equal(sb.read_data(cb, rlen // 8), state[2][cb][: rlen // 8]), (label, cb)
+    return ret, state
+
+
+def test_rm_rx_all_sizes(S, ora):
+    """srsran_rm_turbo_rx_lut_ vs oracle: 188 K x 4 rv x {E < N, E = N, E > 2N} x both layouts."""
+    rng = np.random.default_rng(11)
+    bad = []
+    for idx, K in enumerate(CB_SIZES):
+        N = 3 * K + 12
+        for rv in range(4):
+            for E in (N // 3, N, 2 * N + 37):
+                e = rng.integers(-30000, 30000, E, dtype=np.int16)
+                sb0 = rng.integers(-30000, 30000, SOFTBUF_LEN, dtype=np.int16)
+                for tdec_layout in (True, False):
+                    ret, got = S.rm_turbo_rx_lut(e, sb0, idx, rv, tdec_layout)
+                    exp = ora.rm_turbo_rx(K, rv, tdec_layout, e, sb0)
+                    if ret != 0 or not np.array_equal(got, exp):
+                        bad.append((K, rv, E, tdec_layout))
+    assert not bad, bad[:10]
+
+
+def test_rm_rx_invalid(S):
+    e = np.zeros(100, np.int16)
+    sb0 = np.zeros(SOFTBUF_LEN, np.int16)
+    assert S.rm_turbo_rx_lut(e, sb0, 188, 0)[0] != 0
+    assert S.rm_turbo_rx_lut(e, sb0, 0, 4)[0] != 0
+
+
+def mixed_k_tbs(ora):
+    """A TBS whose segmentation has C2 > 0 and F == 0 (K+ and K- blocks)."""
+    for tbs in range(6200, 200000, 8):
+        rc, s = ora.cbsegm(tbs)
+        if rc == 0 and s["C2"] > 0 and s["F"] == 0 and s["C"] <= 32:
+            return tbs
+    raise AssertionError("no mixed-K TBS found")
+
+
+@pytest.mark.parametrize("case", ["c1_small", "c1_generic", "c1_window8", "c13_64qam", "c4", "mixed_k"])
+def test_dlsch_noise_free(S, q, ora, case):
+    rng = np.random.default_rng(zlib.crc32(case.encode()))
+    tbs, Qm, G = {"c1_small": (16, 2, 240), "c1_generic": (328, 2, 1200), "c1_window8": (680, 4, 2400),
+                  "c13_64qam": (75376, 6, 86400), "c4": (19080, 4, 28800), "mixed_k": (None, 6, None)}[case]
+    if tbs is None:
+        tbs = mixed_k_tbs(ora)
+        G = ((tbs * 6 // 5) // Qm) * Qm
+    sb = S.SoftbufferRx(nof_prb=100)
+    tb = rng.integers(0, 256, tbs // 8, dtype=np.uint8)
+    llr = llrs(ora, tbs, Qm, 0, G, tb, 0, rng)
+    ret, _ = check_tb(S, q, ora, sb, tbs, Qm, 0, llr, 8, None, case)
+    if case != "mixed_k":  # the reference's decoder/encoder disagree on K+/K- order (sch.c:285 vs 392)
+        assert ret == 0
+
+
+def test_dlsch_awgn_harq_sweep(S, q, ora):
+    """75376-bit TB (C3 grant): early stop, partial CB failure, HARQ combining rv0 -> rv2 -> rv3 -> rv1."""
+    tbs, Qm, G = 75376, 6, 86400
+    mixed = False
+    for seed, sigma in enumerate((0.4, 0.45, 0.47, 0.48, 0.5, 0.55)):
+        rng = np.random.default_rng(100 + seed)
+        tb = rng.integers(0, 256, tbs // 8, dtype=np.uint8)
+        sb = S.SoftbufferRx(nof_prb=100)
+        state = None
+        for rv in (0, 2, 3, 1):
+            llr = llrs(ora, tbs, Qm, rv, G, tb, sigma, rng)
+            ret, state = check_tb(S, q, ora, sb, tbs, Qm, rv, llr, 8, state, (sigma, rv))
+            flags = state[1][:13]
+            mixed |= bool(flags.any() and not flags.all())
+            if ret == 0:
+                break
+    assert mixed, "sweep never produced a partially decoded TB"
+
+
+def test_dlsch_tb_crc_failure_resets_cb_flags(S, q, ora):
+    """All CB CRCs pass but the TB CRC fails (sch.c:558-570)."""
+    rng = np.random.default_rng(5)
+    tbs, Qm, G = 19080, 4, 28800
+    tb = rng.integers(0, 256, tbs // 8, dtype=np.uint8)
+    sb = S.SoftbufferRx(nof_prb=100)
+    llr = llrs(ora, tbs, Qm, 0, G, tb, 0, rng, tb_crc_xor=0x5A5A5)
+    ret, state = check_tb(S, q, ora, sb, tbs, Qm, 0, llr, 8, None, "tbcrc")
+    assert ret == -1
+    assert sb.cb_crc(4) == [False] * 4
+    assert sb.tb_crc  # set before the TB CRC check and left as is (sch.c:458-462)
+
+
+@pytest.mark.parametrize("max_iter", [1, 2, 3, 16, 0])
+def test_dlsch_max_noi(S, q, ora, max_iter):
+    rng = np.random.default_rng(9)
+    tbs, Qm, G = 19080, 4, 28800
+    tb = rng.integers(0, 256, tbs // 8, dtype=np.uint8)
+    sb = S.SoftbufferRx(nof_prb=100)
+    llr = llrs(ora, tbs, Qm, 0, G, tb, 0.45, rng)
+    q.set_max_noi(max_iter)
+    eff = q.max_iterations
+    assert eff == (max_iter or 10)
+    check_tb(S, q, ora, sb, tbs, Qm, 0, llr, eff, None, max_iter)
+
+
+def test_dlsch_input_checks(S, q, ora):
+    sb = S.SoftbufferRx(nof_prb=100)
+    llr = np.zeros(3000, np.int16)
+    assert q.decode(sb, 0, 2, 0, llr)[0] == 0      # tbs == 0: nothing to do (sch.c:531-533)
+    assert q.decode(sb, 20, 2, 0, llr)[0] == -2    # filler bits (sch.c:535-538)
+    small = S.SoftbufferRx(max_cb=2)
+    assert q.decode(small, 75376, 6, 0, np.zeros(86400, np.int16))[0] == -2  # C > max_cb (sch.c:540-546)
+    big = S.SoftbufferRx(max_cb=64)
+    tbs = next(t for t in range(196000, 400000, 8) if ora.cbsegm(t)[1]["C"] > 32 and ora.cbsegm(t)[1]["F"] == 0)
+    assert q.decode(big, tbs, 6, 0, np.zeros(tbs * 6 // 5, np.int16))[0] == -1  # SRSRAN_MAX_CODEBLOCKS
+
+
+def test_softbuffer_reset(S, q, ora):
+    rng = np.random.default_rng(3)
+    tbs, Qm, G = 19080, 4, 28800
+    tb = rng.integers(0, 256, tbs // 8, dtype=np.uint8)
+    sb = S.SoftbufferRx(nof_prb=100)
+    llr = llrs(ora, tbs, Qm, 0, G, tb, 0, rng)
+    ret, state = check_tb(S, q, ora, sb, tbs, Qm, 0, llr, 8, None, "first")
+    assert ret == 0 and sb.cb_crc(4) == [True] * 4 and sb.tb_crc
+    # a second decode of the same TB skips every CB and copies the (never saved) payloads
+    ret, state = check_tb(S, q, ora, sb, tbs, Qm, 0, np.zeros_like(llr), 8, state, "again")
+    assert q.last_noi() == 0.0
+    sb.reset_cb_crc(2)
+    assert sb.cb_crc(4) == [False, False, True, True]
+    sb.reset()
+    assert sb.cb_crc() == [False] * sb.max_cb and not sb.tb_crc
+    assert not sb.read_cb(0, 3 * (4608 + 32) + 12).any()
+
+
+def test_dlsch_batch_matches_oracle(S, q, ora):
+    """srsran_dlsch_gpu_decode_batch: mixed TBs (and invalid entries) in one call."""
+    rng = np.random.default_rng(21)
+    cases = [(75376, 6, 86400, 0.45), (19080, 4, 28800, 0), (16, 2, 240, 0), (680, 4, 2400, 0.3),
+             (20, 2, 300, 0), (0, 2, 300, 0), (75376, 6, 86400, 0.5), (328, 2, 1200, 0.5)]
+    q.set_max_noi(8)
+    entries, exp, keep = [], [], []
+    for tbs, Qm, G, sigma in cases:
+        tb = rng.integers(0, 256, max(tbs, 8) // 8, dtype=np.uint8)
+        if tbs % 8 == 0 and tbs:
+            llr = llrs(ora, tbs, Qm, 0, G, tb, sigma, rng)
+        else:
+            llr = rng.integers(-100, 100, G, dtype=np.int16)
+        d_e = torch.from_numpy(llr).cuda()
+        d_data = torch.zeros(tbs // 8 + 64, dtype=torch.uint8, device="cuda")
+        sb = S.SoftbufferRx(nof_prb=100)
+        keep += [d_e, d_data, sb]
+        entries.append((tbs, Qm, 0, G, d_e.data_ptr(), d_data.data_ptr(), sb))
+        if tbs % 8 or tbs == 0:
+            exp.append(((-2 if tbs else 0), None, 0.0, None))
+        else:
+            oret, odata, onoi, oavg, st = ora.dlsch_decode(tbs, Qm, 0, llr, 8)
+            exp.append((oret, odata, oavg, st))
+    d_res = torch.full((len(cases),), 77, dtype=torch.int32, device="cuda")
+    d_avg = torch.zeros(len(cases), dtype=torch.float32, device="cuda")
+    assert q.decode_batch(entries, d_res.data_ptr(), d_avg.data_ptr()) == 0
+    torch.cuda.synchronize()
+    res, avg = d_res.cpu().numpy(), d_avg.cpu().numpy()
+    for i, (oret, odata, oavg, st) in enumerate(exp):
+        assert res[i] == oret, i
+        if odata is not None:
+            data = keep[3 * i + 1].cpu().numpy()
+            assert np.array_equal(data[: len(odata)], odata), i
+            assert avg[i] == oavg, i
+            sb = keep[3 * i + 2]
+            sb.sync()
+            C = S.cbsegm(cases[i][0])[1].C
+            assert sb.cb_crc(C) == [bool(x) for x in st[1][:C]], i

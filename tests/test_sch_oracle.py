@@ -54,7 +54,7 @@ def test_dlsch_roundtrip_noise_free(ora):
         e = ora.dlsch_encode(tbs, Qm, 0, G, tb)
         llr = np.where(e > 0, 100, -100).astype(np.int16)
         ret, data, noi, avg, _ = ora.dlsch_decode(tbs, Qm, 0, llr, 8)
-        assert ret == 0 and np.array_equal(data, tb), tbs
+        assert ret == 0 and np.array_equal(data[: tbs // 8], tb), tbs
         assert all(n == 2 for n in noi) and avg == 2.0
 
 
@@ -70,7 +70,7 @@ def test_dlsch_harq_combining(ora):
         y = e + rng.standard_normal(e.shape).astype(np.float32) * 0.6
         llr = np.trunc(100 * y).astype(np.int16)
         ret, data, noi, avg, state = ora.dlsch_decode(tbs, Qm, rv, llr, 8, state)
-        outs.append((ret, np.array_equal(data, tb)))
+        outs.append((ret, np.array_equal(data[: tbs // 8], tb)))
     assert outs == [(-1, False), (0, True)]
 
 

@@ -369,7 +369,7 @@ __device__ __forceinline__ v2s beta_llr_window(v2s P, v2s& Bst, const uint32_t* 
 // alpha length (L or K), M = Mb = beta checkpoints.  Both waves reach the same
 // barriers.
 template <int NSB>
-__device__ void map_decode(const Smem& sm, int base, int wave, int lane, int j, int s, int K, int L, int Nb, int La,
+__device__ __forceinline__ void map_decode(const Smem& sm, int base, int wave, int lane, int j, int s, int K, int L, int Nb, int La,
                            int M, const short* xt, const short* yt)
 {
   constexpr bool SAT = Geo<NSB>::SAT;
@@ -476,13 +476,10 @@ __global__ __launch_bounds__(128, 2) void tdec_kernel(TdecArgs a)
   const int cb   = blockIdx.x * Gm::CPW + cw;  // launch index
   const bool live = cb < (int)a.ncb;
   const int cbl  = live ? cb : (int)a.ncb - 1;
-  const TdecCb* cbd = ES ? &a.cbs[cbl] : nullptr;
-  const int cbm  = ES ? (int)cbd->slot : cbl;  // output / state slot
-  const bool crc_a = ES && cbd->crc_a;
   // DL-SCH mode: blocks whose CRC already passed are not decoded; padding blocks
-  // never hold back the workgroup's early exit.
-  bool done = ES && (!live || *cbd->skip);
-  const int ostr = ES ? (int)a.out_stride : K / 8;
+  // never hold back the workgroup's early exit.  The block descriptor a.cbs[cbl] is
+  // re-read where needed instead of being kept live across the decode loop.
+  bool done = ES && (!live || *a.cbs[cbl].skip);
 
   Smem sm;
   sm.xy  = smem;
@@ -513,12 +510,11 @@ __global__ __launch_bounds__(128, 2) void tdec_kernel(TdecArgs a)
     return byte;
   };
 
-  const short* in = ES ? cbd->in : a.in + (size_t)cbl * a.in_stride;
+  const short* in = ES ? a.cbs[cbl].in : a.in + (size_t)cbl * a.in_stride;
   const bool   sb = a.layout_sb;
   // Positions are visited in "q order": the rm_turbo sub-block order for window
   // decoders (q = k*NSB + s, coalesced in the SB input), natural order otherwise.
   auto qslot = [&](int q) -> int { return NSB > 1 ? (q & (NSB - 1)) * Ls + (q >> LOG_NSB) : q; };
-  auto qnat  = [&](int q) -> int { return NSB > 1 ? (q & (NSB - 1)) * L + (q >> LOG_NSB) : q; };
   const short* tail = sb ? in + 3 * (K + 32) : in + 3 * K;
   short st[3], p0t[3], x2t[3], p1t[3];
 #pragma unroll
@@ -614,7 +610,7 @@ __global__ __launch_bounds__(128, 2) void tdec_kernel(TdecArgs a)
 
   // restore state from a previous launch (srsran_tdec_iteration path)
   if (a.n_start > 0) {
-    const short* se = a.state + (size_t)cbm * 2 * XYW;
+    const short* se = a.state + (size_t)cbl * 2 * XYW;
     for (int i = t2; i < XYW; i += G2) {
       xylo[2 * i] = se[i];
       auxc[i]     = se[XYW + i];
@@ -628,8 +624,9 @@ __global__ __launch_bounds__(128, 2) void tdec_kernel(TdecArgs a)
 
   if constexpr (ES) {
     if (live && done && t2 == 0) {  // skipped block (sch.c:392, 476-480)
-      a.noi_out[cbm] = 0;
-      a.crc_ok[cbm]  = 1;
+      const uint32_t slot = a.cbs[cbl].slot;
+      a.noi_out[slot]     = 0;
+      a.crc_ok[slot]      = 1;
     }
   }
   const int h_end = (ES && __syncthreads_or(!done) == 0) ? a.n_start : a.n_end;
@@ -692,6 +689,7 @@ __global__ __launch_bounds__(128, 2) void tdec_kernel(TdecArgs a)
         const int nbytes = K / 8;
         const int bpt    = (nbytes + G2 - 1) / G2;
         const int b0     = t2 * bpt;
+        const bool     crc_a = a.cbs[cbl].crc_a;
         const uint32_t poly = crc_a ? LTE_CRC24A : LTE_CRC24B;
         uint32_t       crc  = 0;
         const int      b1   = min(b0 + bpt, nbytes);
@@ -710,14 +708,15 @@ __global__ __launch_bounds__(128, 2) void tdec_kernel(TdecArgs a)
         __syncthreads();
         const bool ok = (red[cw * 2] ^ red[cw * 2 + 1]) == 0;
         if (ok && !done && live) {
-          uint8_t* out = a.out + (size_t)cbm * ostr;
+          const uint32_t slot = a.cbs[cbl].slot;
+          uint8_t*       out  = a.out + (size_t)slot * a.out_stride;
 #pragma unroll 1
           for (int b = b0; b < b1; b++) {
             out[b] = (uint8_t)decide_byte(b, dec1);
           }
           if (t2 == 0) {
-            a.noi_out[cbm] = (uint8_t)(h + 1);
-            a.crc_ok[cbm]  = 1;
+            a.noi_out[slot] = (uint8_t)(h + 1);
+            a.crc_ok[slot]  = 1;
           }
         }
         done = done || ok;
@@ -731,7 +730,8 @@ __global__ __launch_bounds__(128, 2) void tdec_kernel(TdecArgs a)
   // -------- hard decision (turbodecoder.c:370-378), natural bit order --------
   const bool last_dec1 = ((a.n_end - 1) & 1) == 0;
   if (live && !done) {
-    uint8_t* out = a.out + (size_t)cbm * ostr;
+    const int cbm = ES ? (int)a.cbs[cbl].slot : cbl;  // output / state slot
+    uint8_t*  out = a.out + (size_t)cbm * (ES ? a.out_stride : K / 8);
     for (int b = t2; b < K / 8; b += G2) {
       out[b] = (uint8_t)decide_byte(b, last_dec1);
     }

@@ -222,6 +222,7 @@ typedef struct {
   const int16_t*          d_e_bits; /* device */
   uint8_t*                d_data;   /* device, >= tbs/8 + 6 bytes */
   srsran_softbuffer_rx_t* softbuffer;
+  uint32_t                new_data; /* 1: as if srsran_softbuffer_rx_reset_tbs(softbuffer, tbs) ran first */
 } srsran_dlsch_gpu_tb_t;
 
 int srsran_dlsch_gpu_decode_batch(srsran_sch_t*                q,

@@ -160,6 +160,7 @@ struct SchCtx {
   int32_t*    d_res = nullptr;
   float*      d_avg = nullptr;
   uint8_t*    h_io = nullptr;  // pinned: flags in/out, result, avg
+  uint8_t*    d_zero = nullptr;  // a cleared cb_crc flag for new transmissions
   bool        used = false;
 };
 
@@ -260,7 +261,7 @@ int enqueue_batch(srsran_sch_t* q, uint32_t ntb, const srsran_dlsch_gpu_tb_t* tb
       r.E                 = n_e2;
       r.len               = t.len;
       r.N                 = t.N;
-      r.pad               = 0;
+      r.overwrite         = tbs[i].new_data ? 1 : 0;
       max_len             = std::max(max_len, t.len);
       by_k[K].push_back(slot);
       slot_crc_a[slot] = s.C == 1;  // single-CB TB: CRC24A over tbs + 24 (sch.c:440-446)
@@ -274,7 +275,7 @@ int enqueue_batch(srsran_sch_t* q, uint32_t ntb, const srsran_dlsch_gpu_tb_t* tb
     for (uint32_t slot : kv.second) {
       TdecCb c;
       c.in    = rm[slot].sb;
-      c.skip  = rm[slot].skip;
+      c.skip  = rm[slot].overwrite ? x->d_zero : rm[slot].skip;  // a new transmission decodes every CB
       c.slot  = slot;
       c.crc_a = slot_crc_a[slot];
       cbs.push_back(c);
@@ -287,16 +288,24 @@ int enqueue_batch(srsran_sch_t* q, uint32_t ntb, const srsran_dlsch_gpu_tb_t* tb
     t.result = d_result + i;
     t.avg    = d_avg + i;
     t.status = plan[i].status;
+    const srsran_softbuffer_rx_t* sbh = tbs[i].softbuffer;
+    if (sbh && sbh->gpu) {
+      const SbGpu* sb = (const SbGpu*)sbh->gpu;
+      t.cb_crc        = sb->d_flags;
+      t.tb_crc        = sb->d_flags + sbh->max_cb;
+      t.saved         = sb->d_data;
+      t.saved_stride  = sb->data_stride;
+      t.sbuf          = sb->d_buf;
+      t.sb_stride     = sb->stride;
+      t.max_cb        = sbh->max_cb;
+      t.nof_cb_reset  = std::min((tbs[i].tbs + 24) / (SRSRAN_TCOD_MAX_LEN_CB - 24) + 1, sbh->max_cb);
+      t.new_data      = tbs[i].new_data ? 1 : 0;
+    }
     if (plan[i].status != 1) {
       continue;
     }
-    const SbGpu* sb = (const SbGpu*)tbs[i].softbuffer->gpu;
     t.data          = tbs[i].d_data;
     t.cbout         = nullptr;  // filled below once the scratch is sized
-    t.cb_crc        = sb->d_flags;
-    t.tb_crc        = sb->d_flags + tbs[i].softbuffer->max_cb;
-    t.saved         = sb->d_data;
-    t.saved_stride  = sb->data_stride;
     t.slot0         = plan[i].slot0;
     t.C             = plan[i].s.C;
     t.C1            = plan[i].s.C1;
@@ -588,7 +597,7 @@ int srsran_rm_turbo_rx_lut_(int16_t* input,
   s.E    = in_len;
   s.len  = t.len;
   s.N    = t.N;
-  s.pad  = 0;
+  s.overwrite = 0;
   hipMemcpyAsync(c.d_in, input, (size_t)in_len * sizeof(int16_t), hipMemcpyHostToDevice, c.stream);
   hipMemcpyAsync(c.d_out, output, t.len * sizeof(int16_t), hipMemcpyHostToDevice, c.stream);
   hipMemcpyAsync(c.d_slot, &s, sizeof(s), hipMemcpyHostToDevice, c.stream);
@@ -758,7 +767,8 @@ int srsran_sch_init(srsran_sch_t* q)
       hipEventCreateWithFlags(&x->done, hipEventDisableTiming) != hipSuccess ||
       hipMalloc((void**)&x->d_data, kDataCap) != hipSuccess || hipMalloc((void**)&x->d_res, 16) != hipSuccess ||
       hipMalloc((void**)&x->d_avg, 16) != hipSuccess ||
-      hipHostMalloc((void**)&x->h_io, 256, hipHostMallocDefault) != hipSuccess) {
+      hipHostMalloc((void**)&x->h_io, 256, hipHostMallocDefault) != hipSuccess ||
+      hipMalloc((void**)&x->d_zero, 8) != hipSuccess || hipMemset(x->d_zero, 0, 8) != hipSuccess) {
     srsran_sch_free(q);
     return SRSRAN_ERROR;
   }
@@ -792,6 +802,7 @@ void srsran_sch_free(srsran_sch_t* q)
     hipFree(x->d_res);
     hipFree(x->d_avg);
     hipHostFree(x->h_io);
+    hipFree(x->d_zero);
     delete x;
   }
   srsran_tdec_free(&q->decoder);
@@ -866,6 +877,7 @@ int srsran_dlsch_decode2(srsran_sch_t*       q,
   tb.d_e_bits   = x->d_e;
   tb.d_data     = x->d_data;
   tb.softbuffer = sb;
+  tb.new_data   = 0;
   hipStreamSynchronize(x->stream);  // h_io is reused below
   int ret = enqueue_batch(q, 1, &tb, x->d_res, x->d_avg, x->stream);
   if (ret != SRSRAN_SUCCESS) {

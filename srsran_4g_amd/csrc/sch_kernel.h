@@ -24,7 +24,7 @@ struct RmSlot {
   uint32_t        E;
   uint32_t        len;   // positions in the soft buffer layout (3K+12 or 3(K+32)+12)
   uint32_t        N;     // 3K+12: period of the circular buffer after dummy removal
-  uint32_t        pad;
+  uint32_t        overwrite;  // new transmission: sb = sum (the reset buffer is zero), flag ignored
 };
 
 struct SchTb {
@@ -37,7 +37,12 @@ struct SchTb {
   uint8_t*       saved;     // soft buffer saved payloads (device)
   int32_t*       result;    // decode_tb return value (device)
   float*         avg;       // avg_iterations (device)
+  short*         sbuf;      // soft buffer arena (sb_stride int16 per CB), for new-transmission resets
   uint32_t       saved_stride;
+  uint32_t       sb_stride;
+  uint32_t       max_cb;
+  uint32_t       nof_cb_reset;  // CBs srsran_softbuffer_rx_reset_tbs clears (softbuffer.c:146-150)
+  uint32_t       new_data;
   uint32_t       slot0;
   uint32_t       C, C1, K1, K2, tbs;
   int32_t        status;    // 1: decoded; otherwise the return value of a host-side check

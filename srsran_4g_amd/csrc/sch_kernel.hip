@@ -29,14 +29,17 @@ __global__ __launch_bounds__(RM_THREADS) void rm_rx_kernel(const RmSlot* __restr
 {
   const RmSlot s  = slots[blockIdx.y];
   const uint32_t p = (blockIdx.x * RM_THREADS + threadIdx.x) * RM_PER_THREAD;
-  if (p >= s.len || *s.skip) {
+  if (p >= s.len || (!s.overwrite && *s.skip)) {
     return;
   }
   // len is a multiple of 4 (3K+12 / 3K+108 with 8 | K) and buffers are 8-byte aligned
   const uint2 iv = *reinterpret_cast<const uint2*>(s.inv + p);
   uint2       v  = *reinterpret_cast<const uint2*>(s.sb + p);
   const uint32_t idx[4] = {iv.x & 0xffffu, iv.x >> 16, iv.y & 0xffffu, iv.y >> 16};
-  short          acc[4] = {(short)(v.x & 0xffffu), (short)(v.x >> 16), (short)(v.y & 0xffffu), (short)(v.y >> 16)};
+  if (s.overwrite) {
+    v = make_uint2(0, 0);
+  }
+  short acc[4] = {(short)(v.x & 0xffffu), (short)(v.x >> 16), (short)(v.y & 0xffffu), (short)(v.y >> 16)};
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     if (idx[k] != 0xffffu) {
@@ -52,11 +55,40 @@ __global__ __launch_bounds__(RM_THREADS) void rm_rx_kernel(const RmSlot* __restr
 
 static constexpr int TB_THREADS = 256;
 
+// Zero (as srsran_softbuffer_rx_reset_cb does) CB soft buffers [sb0, n), saved payloads
+// [0, n) except those in *keep, and CB flags [f0, max_cb).
+__device__ void reset_range(const SchTb& t, uint32_t sb0, uint32_t n, uint32_t f0, const uint32_t* keep)
+{
+  const int tid = threadIdx.x;
+  for (uint32_t c = sb0; c < n; c++) {
+    for (uint32_t i = tid; i < t.sb_stride; i += TB_THREADS) {
+      t.sbuf[(size_t)c * t.sb_stride + i] = 0;
+    }
+  }
+  for (uint32_t c = 0; c < n; c++) {
+    if (keep && c < 32 && ((*keep >> c) & 1u)) {
+      continue;
+    }
+    for (uint32_t i = tid; i < t.saved_stride; i += TB_THREADS) {
+      t.saved[(size_t)c * t.saved_stride + i] = 0;
+    }
+  }
+  for (uint32_t c = f0 + tid; c < t.max_cb; c += TB_THREADS) {
+    t.cb_crc[c] = 0;
+  }
+}
+
 __global__ __launch_bounds__(TB_THREADS) void tb_kernel(const SchTb* __restrict__ tbs)
 {
   const SchTb t   = tbs[blockIdx.x];
   const int   tid = threadIdx.x;
   if (t.status != 1) {
+    if (t.new_data && t.cb_crc) {  // the reset still happened (softbuffer.c:146-169)
+      reset_range(t, 0, t.nof_cb_reset, 0, nullptr);
+      if (tid == 0) {
+        *t.tb_crc = 0;
+      }
+    }
     if (tid == 0) {
       *t.result = t.status;
       *t.avg    = 0.0f;
@@ -156,6 +188,16 @@ __global__ __launch_bounds__(TB_THREADS) void tb_kernel(const SchTb* __restrict_
   }
   if (tid < (int)C) {
     t.cb_crc[tid] = (okf[tid] && !tb_fail) ? 1 : 0;
+  }
+  if (t.new_data) {
+    // what reset_tbs cleared and this decode did not rewrite: flags past C, soft
+    // buffers past C, saved payloads that were not saved just now
+    const uint32_t saved_now = all_ok ? 0u : 0xffffffffu;
+    uint32_t       mask      = 0;
+    for (uint32_t c = 0; c < C; c++) {
+      mask |= (okf[c] && saved_now) ? (1u << c) : 0u;
+    }
+    reset_range(t, C, t.nof_cb_reset, C, &mask);
   }
   if (tid == 0) {
     *t.tb_crc = all_ok ? 1 : 0;

@@ -71,7 +71,8 @@ class srsran_sch_t(ctypes.Structure):
 
 class srsran_dlsch_gpu_tb_t(ctypes.Structure):
     _fields_ = [("tbs", u32), ("Qm", u32), ("rv", u32), ("nof_e_bits", u32), ("d_e_bits", ctypes.c_void_p),
-                ("d_data", ctypes.c_void_p), ("softbuffer", ctypes.POINTER(srsran_softbuffer_rx_t))]
+                ("d_data", ctypes.c_void_p), ("softbuffer", ctypes.POINTER(srsran_softbuffer_rx_t)),
+                ("new_data", u32)]
 
 
 _i16p = ctypes.POINTER(ctypes.c_int16)
@@ -268,9 +269,11 @@ class Sch:
     def decode_batch(self, entries, d_result, d_avg, stream=None):
         """srsran_dlsch_gpu_decode_batch over device buffers.
 
-        entries: list of (tbs, Qm, rv, nof_e_bits, d_e_bits ptr, d_data ptr, SoftbufferRx)."""
+        entries: list of (tbs, Qm, rv, nof_e_bits, d_e_bits ptr, d_data ptr, SoftbufferRx[, new_data])."""
         arr = (srsran_dlsch_gpu_tb_t * len(entries))()
-        for i, (tbs, Qm, rv, nbits, de, dd, sb) in enumerate(entries):
+        for i, ent in enumerate(entries):
+            tbs, Qm, rv, nbits, de, dd, sb = ent[:7]
+            arr[i].new_data = int(ent[7]) if len(ent) > 7 else 0
             arr[i].tbs, arr[i].Qm, arr[i].rv, arr[i].nof_e_bits = tbs, Qm, rv, nbits
             arr[i].d_e_bits, arr[i].d_data = de, dd
             arr[i].softbuffer = ctypes.pointer(sb.s)

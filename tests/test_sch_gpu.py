@@ -234,3 +234,53 @@ def test_dlsch_batch_matches_oracle(S, q, ora):
             sb.sync()
             C = S.cbsegm(cases[i][0])[1].C
             assert sb.cb_crc(C) == [bool(x) for x in st[1][:C]], i
+
+
+def batch_one(S, q, sb, tbs, Qm, rv, llr, new_data):
+    d_e = torch.from_numpy(llr).cuda()
+    d_data = torch.zeros(tbs // 8 + 64, dtype=torch.uint8, device="cuda")
+    d_res = torch.full((1,), 77, dtype=torch.int32, device="cuda")
+    d_avg = torch.zeros(1, dtype=torch.float32, device="cuda")
+    assert q.decode_batch([(tbs, Qm, rv, len(llr), d_e.data_ptr(), d_data.data_ptr(), sb, new_data)],
+                          d_res.data_ptr(), d_avg.data_ptr()) == 0
+    torch.cuda.synchronize()
+    sb.sync()
+    return int(d_res.item()), d_data.cpu().numpy(), float(d_avg.item())
+
+
+def test_dlsch_batch_new_data_and_harq(S, q, ora):
+    """new_data == 1 behaves as srsran_softbuffer_rx_reset_tbs() followed by decode_tb."""
+    q.set_max_noi(8)
+    rng = np.random.default_rng(31)
+    sb = S.SoftbufferRx(nof_prb=100)
+    steps = [(75376, 6, 86400, 0.48, 0, True), (75376, 6, 86400, 0.48, 2, False),
+             (19080, 4, 28800, 0.45, 0, True), (19080, 4, 28800, 0.45, 2, False), (680, 4, 2400, 0, 0, True)]
+    state, tb = None, None
+    for tbs, Qm, G, sigma, rv, new in steps:
+        if new:
+            tb = rng.integers(0, 256, tbs // 8, dtype=np.uint8)
+            state = None
+        llr = llrs(ora, tbs, Qm, rv, G, tb, sigma, rng)
+        ret, data, avg = batch_one(S, q, sb, tbs, Qm, rv, llr, new)
+        oret, odata, onoi, oavg, state = ora.dlsch_decode(tbs, Qm, rv, llr, 8, state)
+        label = (tbs, rv)
+        assert ret == oret and avg == oavg, label
+        assert np.array_equal(data[: len(odata)], odata), label
+        s = S.cbsegm(tbs)[1]
+        C = s.C
+        flags = sb.cb_crc()
+        assert flags[:C] == [bool(x) for x in state[1][:C]] and not any(flags[C:]), label
+        nof_cb = min((tbs + 24) // 6120 + 1, sb.max_cb)
+        for cb in range(nof_cb):
+            if cb < C:
+                K = s.K1 if cb < s.C1 else s.K2
+                L = 3 * (K + 32) + 12 if K >= 408 else 3 * K + 12
+                assert np.array_equal(sb.read_cb(cb, L), state[0][cb][:L]), (label, cb)
+                rlen = K if C == 1 else K - 24
+                saved = sb.read_data(cb, rlen // 8)
+                if state[1][cb] and ret != 0:
+                    assert np.array_equal(saved, state[2][cb][: rlen // 8]), (label, cb)
+                elif new:
+                    assert not saved.any(), (label, cb)
+            elif new:
+                assert not sb.read_cb(cb, S.SOFTBUFFER_SIZE).any(), (label, cb)

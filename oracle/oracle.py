@@ -173,19 +173,8 @@ class Oracle(_Lib):
         Returns (ret, data, noi, avg, state); data is the whole zero-initialised payload
         buffer (tbs/8 + 8 bytes) so bytes written past tbs/8 (CRC bytes) are compared too."""
         self._sch_sigs()
-        rc, s = self.cbsegm(tbs)
-        C = max(1, s["C"])
-        if state is None:
-            state = (np.zeros((C, SOFTBUF_LEN), np.int16), np.zeros(C, np.uint8), np.zeros((C, 768), np.uint8))
-        sb, crc, cbd = state
-        e_llr = np.ascontiguousarray(e_llr, dtype=np.int16)
-        data = np.zeros(tbs // 8 + 8, dtype=np.uint8)
-        noi = (ctypes.c_uint32 * C)()
-        avg = ctypes.c_float(0)
-        ret = self.lib.oracle_dlsch_decode_tb(tbs, Qm, rv, e_llr.size, _ptr(e_llr, _i16p), max_iterations,
-                                              _ptr(sb, _i16p), sb.shape[1], _ptr(crc, _u8p), _ptr(cbd, _u8p),
-                                              cbd.shape[1], _ptr(data, _u8p), noi, ctypes.byref(avg))
-        return ret, data, list(noi), avg.value, state
+        return _dlsch_decode(self.lib.oracle_dlsch_decode_tb, self.cbsegm(tbs)[1], tbs, Qm, rv, e_llr,
+                             max_iterations, state)
 
     def run_batch(self, K, llr2d, layout_sb, nof_iterations):
         llr2d = np.ascontiguousarray(llr2d, dtype=np.int16)
@@ -196,6 +185,23 @@ class Oracle(_Lib):
         if rc:
             raise ValueError(rc)
         return out
+
+
+def _dlsch_decode(fn, segm, tbs, Qm, rv, e_llr, max_iterations, state):
+    C = max(1, segm["C"])
+    if state is None:
+        state = (np.zeros((C, SOFTBUF_LEN), np.int16), np.zeros(C, np.uint8), np.zeros((C, 768), np.uint8))
+    sb, crc, cbd = state
+    e_llr = np.ascontiguousarray(e_llr, dtype=np.int16)
+    data = np.zeros(tbs // 8 + 8, dtype=np.uint8)
+    noi = (ctypes.c_uint32 * C)()
+    avg = ctypes.c_float(0)
+    u32 = ctypes.c_uint32
+    fn.argtypes = [u32, u32, u32, u32, _i16p, u32, _i16p, u32, _u8p, _u8p, u32, _u8p, ctypes.POINTER(u32),
+                   ctypes.POINTER(ctypes.c_float)]
+    ret = fn(tbs, Qm, rv, e_llr.size, _ptr(e_llr, _i16p), max_iterations, _ptr(sb, _i16p), sb.shape[1],
+             _ptr(crc, _u8p), _ptr(cbd, _u8p), cbd.shape[1], _ptr(data, _u8p), noi, ctypes.byref(avg))
+    return ret, data, list(noi), avg.value, state
 
 
 class Reference(_Lib):
@@ -226,6 +232,11 @@ class Reference(_Lib):
         out = (ctypes.c_uint32 * 9)()
         rc = f(tbs, out)
         return rc, dict(zip(SEGM_FIELDS, list(out)))
+
+    def dlsch_decode(self, tbs, Qm, rv, e_llr, max_iterations, state=None):
+        """decode_tb glue over the reference's rm_turbo / turbo decoder / CRC (ref_harness.c)."""
+        return _dlsch_decode(self.lib.ref_dlsch_decode_tb, self.cbsegm(tbs)[1], tbs, Qm, rv, e_llr,
+                             max_iterations, state)
 
     def rm_turbo_rx(self, cb_idx, rv, e, softbuf):
         """srsran_rm_turbo_rx_lut (SB layout for window decoders, as the reference build)."""

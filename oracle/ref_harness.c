@@ -26,8 +26,10 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include "srsran/phy/common/phy_common.h"
 #include "srsran/phy/fec/cbsegm.h"
 #include "srsran/phy/fec/crc.h"
+#include "srsran/phy/fec/softbuffer.h"
 #include "srsran/phy/fec/turbo/rm_turbo.h"
 #include "srsran/phy/fec/turbo/tc_interl.h"
 #include "srsran/phy/fec/turbo/turbocoder.h"
@@ -292,4 +294,137 @@ int ref_rm_turbo_tx(const uint8_t* coded, uint32_t K, uint8_t* out, uint32_t E, 
   }
   quiet_end();
   return ret;
+}
+
+/*
+ * ref_dlsch_decode_tb: decode_tb / decode_tb_cb (sch.c:371-573) composed from the
+ * reference's own pieces -- srsran_cbsegm, srsran_rm_turbo_rx_lut, the turbo
+ * half-iteration (turbodecoder_iter.h) with its decision_byte, srsran_crc_checksum_byte.
+ * Only the sch.c loop is restated (sch.c includes the generated srsran/version.h via
+ * srsran/srsran.h and cannot be compiled here).  Same arguments as oracle_dlsch_decode_tb.
+ * Note: the reference turbo decoder writes tail values into the SB soft buffer's padding
+ * (turbodecoder_iter.h extract_input), so only decode outputs are comparable, not padding.
+ */
+int ref_dlsch_decode_tb(uint32_t       tbs,
+                        uint32_t       Qm,
+                        uint32_t       rv,
+                        uint32_t       nof_e_bits,
+                        const int16_t* e_bits,
+                        uint32_t       max_iterations,
+                        int16_t*       softbuf,
+                        uint32_t       softbuf_stride,
+                        uint8_t*       cb_crc,
+                        uint8_t*       cb_data,
+                        uint32_t       cb_data_stride,
+                        uint8_t*       data,
+                        uint32_t*      cb_noi_out,
+                        float*         avg_iterations)
+{
+  static srsran_crc_t crc_tb, crc_cb;
+  static bool         crc_ready = false;
+  if (harness_init()) {
+    return -1;
+  }
+  if (!crc_ready) {
+    srsran_crc_init(&crc_tb, SRSRAN_LTE_CRC24A, 24);
+    srsran_crc_init(&crc_cb, SRSRAN_LTE_CRC24B, 24);
+    crc_ready = true;
+  }
+  srsran_rm_turbo_gentables();
+  srsran_cbsegm_t s;
+  quiet_begin();
+  int rc = srsran_cbsegm(&s, tbs);
+  quiet_end();
+  if (rc) {
+    return -1;
+  }
+  if (s.tbs == 0 || s.C == 0) {
+    return 0;
+  }
+  if (s.F) {
+    return -2;
+  }
+  if (s.C > SRSRAN_MAX_CODEBLOCKS) {
+    return -1;
+  }
+  srsran_tdec_t* h   = &tdec;
+  float          avg = 0;
+  h->force_not_sb    = false;
+  for (uint32_t cb = 0; cb < s.C; cb++) {
+    const uint32_t cb_len     = cb < s.C1 ? s.K1 : s.K2;
+    const uint32_t cb_len_idx = cb < s.C1 ? s.K1_idx : s.K2_idx;
+    const uint32_t rlen       = s.C == 1 ? cb_len : cb_len - 24;
+    if (!cb_crc[cb]) {
+      const uint32_t Gp    = nof_e_bits / Qm;
+      const uint32_t gamma = Gp % s.C;
+      const uint32_t n_e   = Qm * (Gp / s.C);
+      uint32_t       rp    = cb * n_e;
+      uint32_t       n_e2  = n_e;
+      if (cb > s.C - gamma) {
+        n_e2 = n_e + Qm;
+        rp   = (s.C - gamma) * n_e + (cb - (s.C - gamma)) * n_e2;
+      }
+      /* buffer_f[cb] is srsran_vec_i16_malloc'ed (aligned) in the reference: stage it */
+      static int16_t* sb = NULL;
+      if (!sb) {
+        sb = srsran_vec_i16_malloc(SOFTBUFFER_SIZE + 64);
+      }
+      memcpy(sb, &softbuf[(size_t)cb * softbuf_stride], softbuf_stride * sizeof(int16_t));
+      srsran_rm_turbo_rx_lut((int16_t*)&e_bits[rp], sb, n_e2, cb_len_idx, rv);
+      h->n_iter          = 0;
+      h->current_long_cb = cb_len;
+      h->current_cbidx   = (int)cb_len_idx;
+      uint32_t noi = 0;
+      bool     early = false;
+      do {
+        harness_iteration(h, sb);
+        h->dec16[h->current_dec]->tdec_decision_byte(!(h->n_iter % 2) ? h->app1 : h->ext1, &data[cb * rlen / 8],
+                                                     cb_len);
+        avg += 1;
+        noi++;
+        srsran_crc_t*  crc     = s.C > 1 ? &crc_cb : &crc_tb;
+        const uint32_t len_crc = s.C > 1 ? cb_len : s.tbs + 24;
+        if (!srsran_crc_checksum_byte(crc, &data[cb * rlen / 8], len_crc) && noi >= 2) {
+          cb_crc[cb] = 1;
+          early      = true;
+        }
+      } while (noi < max_iterations && !early);
+      memcpy(&softbuf[(size_t)cb * softbuf_stride], sb, softbuf_stride * sizeof(int16_t));
+      if (cb_noi_out) {
+        cb_noi_out[cb] = noi;
+      }
+    } else {
+      memcpy(&data[cb * rlen / 8], &cb_data[(size_t)cb * cb_data_stride], rlen / 8);
+      if (cb_noi_out) {
+        cb_noi_out[cb] = 0;
+      }
+    }
+  }
+  bool tb_ok = true;
+  for (uint32_t i = 0; i < s.C && tb_ok; i++) {
+    tb_ok = cb_crc[i];
+  }
+  if (!tb_ok) {
+    for (uint32_t i = 0; i < s.C; i++) {
+      if (cb_crc[i]) {
+        const uint32_t cb_len = i < s.C1 ? s.K1 : s.K2;
+        const uint32_t rlen   = s.C == 1 ? cb_len : cb_len - 24;
+        memcpy(&cb_data[(size_t)i * cb_data_stride], &data[i * rlen / 8], rlen / 8);
+      }
+    }
+  }
+  if (avg_iterations) {
+    *avg_iterations = avg / (float)s.C;
+  }
+  if (!tb_ok) {
+    return -1;
+  }
+  if (s.C == 1) {
+    return 0;
+  }
+  if (srsran_crc_match_byte(&crc_tb, data, s.tbs)) {
+    return 0;
+  }
+  memset(cb_crc, 0, s.C);
+  return -1;
 }

@@ -118,3 +118,26 @@ def test_rm_tx_matches_reference(ora):
         for rv in range(4):
             for E in (300, 3 * K + 12, 3 * K + 500):
                 assert np.array_equal(ora.rm_turbo_tx(K, rv, coded, E), ref.rm_turbo_tx(K, rv, coded, E))
+
+
+@needs_ref
+def test_dlsch_decode_matches_reference_pieces(ora):
+    """Oracle decode_tb vs the same loop over the reference's rm_turbo / turbo / CRC code:
+    noise-free, early-stop, partial failure and HARQ chains (decode outputs and CB flags)."""
+    ref = Reference()
+    rng = np.random.default_rng(12)
+    for tbs, Qm, G, sigmas in ((75376, 6, 86400, (0.0, 0.45, 0.48)), (19080, 4, 28800, (0.45,)),
+                               (680, 4, 2400, (0.0, 0.6)), (16, 2, 240, (0.3,))):
+        for sigma in sigmas:
+            tb = rng.integers(0, 256, tbs // 8, dtype=np.uint8)
+            so = sr = None
+            for rv in (0, 2, 3):
+                e = ora.dlsch_encode(tbs, Qm, rv, G, tb).astype(np.float32) * 2 - 1
+                e = np.trunc(100 * (e + rng.standard_normal(e.shape).astype(np.float32) * sigma)).astype(np.int16)
+                a = ora.dlsch_decode(tbs, Qm, rv, e, 8, so)
+                b = ref.dlsch_decode(tbs, Qm, rv, e, 8, sr)
+                so, sr = a[4], b[4]
+                assert a[0] == b[0] and np.array_equal(a[1], b[1]) and a[2] == b[2] and a[3] == b[3], (tbs, sigma, rv)
+                assert np.array_equal(so[1], sr[1]) and np.array_equal(so[2], sr[2]), (tbs, sigma, rv)
+                if a[0] == 0:
+                    break

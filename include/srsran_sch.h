@@ -212,7 +212,7 @@ int srsran_dlsch_decode2(srsran_sch_t*       q,
  *   d_result[i]  = SRSRAN_SUCCESS / SRSRAN_ERROR / SRSRAN_ERROR_INVALID_INPUTS (decode_tb's return)
  *   d_avg_noi[i] = avg_iterations of that TB (sch.c:489)
  * Soft buffer flags are updated on the device; call srsran_softbuffer_rx_sync() to read them on
- * the host.  `stream` is a hipStream_t (NULL = the sch object's own stream).  q->max_iterations
+ * the host.  `stream` is a hipStream_t (NULL = the default stream).  q->max_iterations
  * applies to every TB.  Returns SRSRAN_SUCCESS once the work is enqueued. */
 typedef struct {
   uint32_t                tbs;

@@ -22,19 +22,29 @@ __device__ __forceinline__ uint32_t crc24_byte(uint32_t crc, uint32_t byte, uint
   return crc & 0xFFFFFFu;
 }
 
-// a * b mod P over GF(2) for 24-bit a, b (P of degree 24, given with its x^24 bit)
+// a * b mod P over GF(2) for 24-bit a, b (P of degree 24, given with its x^24 bit).
+// Horner over the bits of b, MSB first, reducing every step: 32-bit ops only.
 __device__ __forceinline__ uint32_t clmul_mod24(uint32_t a, uint32_t b, uint32_t poly)
 {
-  uint64_t r = 0;
+  uint32_t r = 0;
 #pragma unroll 1
-  for (int i = 0; i < 24; i++) {
-    r ^= ((b >> i) & 1u) ? ((uint64_t)a << i) : 0ull;
+  for (int i = 23; i >= 0; i--) {
+    r = (r << 1) ^ (((b >> i) & 1u) ? a : 0u);
+    r ^= (r & 0x1000000u) ? poly : 0u;
   }
-#pragma unroll 1
-  for (int i = 46; i >= 24; i--) {
-    r ^= ((r >> i) & 1ull) ? ((uint64_t)poly << (i - 24)) : 0ull;
+  return r;
+}
+
+// same, fully unrolled (for kernels with registers to spare)
+__device__ __forceinline__ uint32_t clmul24(uint32_t a, uint32_t b, uint32_t poly)
+{
+  uint32_t r = 0;
+#pragma unroll
+  for (int i = 23; i >= 0; i--) {
+    r = (r << 1) ^ (((b >> i) & 1u) ? a : 0u);
+    r ^= (r & 0x1000000u) ? poly : 0u;
   }
-  return (uint32_t)r;
+  return r;
 }
 
 }  // namespace srsran_amd

@@ -925,8 +925,7 @@ int srsran_dlsch_gpu_decode_batch(srsran_sch_t*                q,
   if (q->llr_is_8bit) {
     return SRSRAN_ERROR;
   }
-  SchCtx* x = (SchCtx*)q->gpu;
-  return enqueue_batch(q, nof_tb, tbs, d_result, d_avg_noi, stream ? (hipStream_t)stream : x->stream);
+  return enqueue_batch(q, nof_tb, tbs, d_result, d_avg_noi, (hipStream_t)stream);
 }
 
 }  // extern "C"

@@ -284,3 +284,15 @@ def test_dlsch_batch_new_data_and_harq(S, q, ora):
                     assert not saved.any(), (label, cb)
             elif new:
                 assert not sb.read_cb(cb, S.SOFTBUFFER_SIZE).any(), (label, cb)
+
+
+def test_rm_rx_long_e(S, ora):
+    """E > 65535 on one code block (repetition over many circular-buffer periods)."""
+    rng = np.random.default_rng(4)
+    for idx in (0, 100, 187):
+        K = CB_SIZES[idx]
+        E = 70001
+        e = rng.integers(-300, 300, E, dtype=np.int16)
+        sb0 = rng.integers(-30000, 30000, SOFTBUF_LEN, dtype=np.int16)
+        ret, got = S.rm_turbo_rx_lut(e, sb0, idx, 1, True)
+        assert ret == 0 and np.array_equal(got, ora.rm_turbo_rx(K, 1, True, e, sb0)), K

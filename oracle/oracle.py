@@ -73,8 +73,61 @@ class _Lib:
         return (out, tr) if trace else out
 
 
-class Oracle(_Lib):
+def aligned(n, dtype, align=64):
+    """Zeroed array whose data pointer is `align`-byte aligned (the reference's SSE loads need it)."""
+    dt = np.dtype(dtype)
+    buf = np.zeros(n * dt.itemsize + align, np.uint8)
+    off = (-buf.ctypes.data) % align
+    return buf[off:off + n * dt.itemsize].view(dt)
+
+
+class _PhyMixin:
+    """PDSCH LLR stages: soft demapping and descrambling (int16)."""
+
+    def demod_s(self, mod, sym):
+        sym = np.asarray(sym, dtype=np.complex64)
+        x = aligned(sym.size, np.complex64)
+        x[:] = sym
+        bits = (1, 2, 4, 6, 8)[mod]
+        out = aligned(sym.size * bits, np.int16)
+        rc = self._demod_fn()(mod, x.ctypes.data_as(ctypes.c_void_p), _ptr(out, _i16p), sym.size)
+        if rc:
+            raise ValueError(rc)
+        return out.copy()
+
+    def sequence_apply_s(self, llr, seed):
+        x = aligned(len(llr), np.int16)
+        x[:] = llr
+        out = aligned(len(llr), np.int16)
+        f = self._seq_fn()
+        f(_ptr(x, _i16p), _ptr(out, _i16p), len(llr), seed)
+        return out.copy()
+
+
+class Oracle(_Lib, _PhyMixin):
     """The repo's C restatement."""
+
+    def _demod_fn(self):
+        f = self.lib.oracle_demod_soft_s
+        f.argtypes = [ctypes.c_int, ctypes.c_void_p, _i16p, ctypes.c_int]
+        return f
+
+    def _seq_fn(self):
+        f = self.lib.oracle_sequence_apply_s
+        f.argtypes = [_i16p, _i16p, ctypes.c_uint32, ctypes.c_uint32]
+        return f
+
+    def sequence_bits(self, seed, n):
+        c = np.zeros(n, np.uint8)
+        self.lib.oracle_sequence_bits.argtypes = [ctypes.c_uint32, _u8p, ctypes.c_uint32]
+        self.lib.oracle_sequence_bits(seed, _ptr(c, _u8p), n)
+        return c
+
+    def pdsch_seed(self, rnti, q, nslot, cell_id):
+        f = self.lib.oracle_pdsch_seed
+        f.argtypes = [ctypes.c_uint16, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32]
+        f.restype = ctypes.c_uint32
+        return f(rnti, q, nslot, cell_id)
 
     def __init__(self):
         super().__init__(ORACLE_SO, "oracle_")
@@ -204,8 +257,27 @@ def _dlsch_decode(fn, segm, tbs, Qm, rv, e_llr, max_iterations, state):
     return ret, data, list(noi), avg.value, state
 
 
-class Reference(_Lib):
+class Reference(_Lib, _PhyMixin):
     """The reference decoder compiled from /root/reference (oracle/_ref)."""
+
+    def _demod_fn(self):
+        f = self.lib.srsran_demod_soft_demodulate_s
+        f.argtypes = [ctypes.c_int, ctypes.c_void_p, _i16p, ctypes.c_int]
+        return f
+
+    def _seq_fn(self):
+        f = self.lib.srsran_sequence_apply_s
+        f.argtypes = [_i16p, _i16p, ctypes.c_uint32, ctypes.c_uint32]
+        return f
+
+    def sequence_pdsch_apply_s(self, llr, rnti, q, nslot, cell_id):
+        x = aligned(len(llr), np.int16)
+        x[:] = llr
+        out = aligned(len(llr), np.int16)
+        f = self.lib.srsran_sequence_pdsch_apply_s
+        f.argtypes = [_i16p, _i16p, ctypes.c_uint16, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
+        f(_ptr(x, _i16p), _ptr(out, _i16p), rnti, q, nslot, cell_id, len(llr))
+        return out.copy()
 
     def __init__(self):
         super().__init__(REF_SO, "ref_", lazy=True)

@@ -1,0 +1,21 @@
+// srsran_4g_amd/csrc/llr_kernel.h -- PDSCH LLR stages: soft demapping + descrambling.
+#ifndef SRSRAN_AMD_LLR_KERNEL_H
+#define SRSRAN_AMD_LLR_KERNEL_H
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace srsran_amd {
+
+// Upload the Gold-sequence jump tables (once per process; idempotent).
+hipError_t gold_tables_init();
+
+// Soft demap nsym symbols (interleaved re/im float) of modulation `mod` (0 BPSK .. 4 256QAM) into
+// int16 LLRs; when `scramble`, LLR i is negated where the Gold sequence c(bit0 + i) of `seed` is 1.
+hipError_t llr_launch(int mod, const float* d_sym, uint32_t nsym, int scramble, uint32_t seed, uint32_t bit0,
+                      int16_t* d_llr, hipStream_t stream);
+
+// out[i] = c(i) ? -in[i] : in[i] (int16 wrap) for the Gold sequence of `seed`.
+hipError_t seq_apply_launch(const int16_t* d_in, int16_t* d_out, uint32_t len, uint32_t seed, hipStream_t stream);
+
+}  // namespace srsran_amd
+#endif

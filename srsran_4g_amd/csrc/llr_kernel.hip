@@ -1,0 +1,334 @@
+// srsran_4g_amd/csrc/llr_kernel.hip -- PDSCH soft demapping + descrambling for CDNA4.
+//
+// Bit-exact with the reference's x86 build (SSE/AVX2) of
+//   srsran_demod_soft_demodulate_s  modem/demod_soft.c:871-894 (per modulation, see below)
+//   srsran_sequence_apply_s         common/sequence.c:507-561  (Gold sequence, 36.211 7.2)
+// The reference demaps 4-symbol blocks with SSE (round half-even, int16 saturation) and the
+// n % 4 tail with scalar C (truncation); QPSK goes through srsran_vec_convert_fi (16-value
+// AVX2 blocks: truncation + saturation; tail: truncation + wrap).  Both splits are kept
+// here by the symbol's index within the call.
+//
+// Layout: one thread per SPT consecutive symbols.  The Gold LFSRs are jumped straight to the
+// thread's first bit with GF(2) matrices A^(2^k) held in constant memory (every lane reads the
+// same column at the same time), then stepped one bit per LLR.  HBM-bound elementwise work:
+// 8 B in per symbol, 2*Qm B out.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "llr_kernel.h"
+
+namespace srsran_amd {
+
+static constexpr int GOLD_NC   = 1600;  // sequence.c:39
+static constexpr int JUMP_BITS = 22;    // offsets below 2^22 LLRs
+
+struct GoldTables {
+  uint32_t x1[JUMP_BITS][31];  // columns of A1^(2^k)
+  uint32_t x2[JUMP_BITS][31];
+  uint32_t x1_nc;              // x1 after Nc steps from x1 = 1
+  uint32_t x2_nc[31];          // x2 after Nc steps from the unit seed 1 << i
+};
+__constant__ GoldTables kGold;
+
+__host__ __device__ inline uint32_t step_x1(uint32_t s) { return (s >> 1) ^ (((s ^ (s >> 3)) & 1u) << 30); }
+__host__ __device__ inline uint32_t step_x2(uint32_t s)
+{
+  return (s >> 1) ^ (((s ^ (s >> 1) ^ (s >> 2) ^ (s >> 3)) & 1u) << 30);
+}
+__host__ __device__ inline uint32_t apply(const uint32_t* cols, uint32_t v)
+{
+  uint32_t r = 0;
+  for (int i = 0; i < 31; i++) {
+    r ^= ((v >> i) & 1u) ? cols[i] : 0u;
+  }
+  return r;
+}
+
+hipError_t gold_tables_init()
+{
+  static bool       done = false;
+  static hipError_t err  = hipSuccess;
+  if (done) {
+    return err;
+  }
+  GoldTables t;
+  for (int i = 0; i < 31; i++) {
+    t.x1[0][i] = step_x1(1u << i);
+    t.x2[0][i] = step_x2(1u << i);
+  }
+  for (int k = 1; k < JUMP_BITS; k++) {
+    for (int i = 0; i < 31; i++) {
+      t.x1[k][i] = apply(t.x1[k - 1], t.x1[k - 1][i]);
+      t.x2[k][i] = apply(t.x2[k - 1], t.x2[k - 1][i]);
+    }
+  }
+  uint32_t s = 1;
+  for (int n = 0; n < GOLD_NC; n++) {
+    s = step_x1(s);
+  }
+  t.x1_nc = s;
+  for (int i = 0; i < 31; i++) {
+    uint32_t v = 1u << i;
+    for (int n = 0; n < GOLD_NC; n++) {
+      v = step_x2(v);
+    }
+    t.x2_nc[i] = v;
+  }
+  err  = hipMemcpyToSymbol(HIP_SYMBOL(kGold), &t, sizeof(t));
+  done = true;
+  return err;
+}
+
+// LFSR states at bit offset `off` of the sequence for `seed`.
+__device__ __forceinline__ void gold_at(uint32_t seed, uint32_t off, uint32_t& x1, uint32_t& x2)
+{
+  x1 = kGold.x1_nc;
+  x2 = apply(kGold.x2_nc, seed & 0x7FFFFFFFu);
+  for (int k = 0; k < JUMP_BITS; k++) {
+    if ((off >> k) & 1u) {
+      x1 = apply(kGold.x1[k], x1);
+      x2 = apply(kGold.x2[k], x2);
+    }
+  }
+}
+
+// ---- x86 conversion semantics (see oracle/phy_oracle.c) ----
+__device__ __forceinline__ int32_t cvt_rn(float x)
+{
+  return (x >= -2147483648.0f && x < 2147483648.0f) ? (int32_t)__builtin_rintf(x) : INT32_MIN;
+}
+__device__ __forceinline__ int32_t cvt_tz(float x)
+{
+  return (x >= -2147483648.0f && x < 2147483648.0f) ? (int32_t)x : INT32_MIN;
+}
+__device__ __forceinline__ int32_t cvt_tz_d(double x)
+{
+  return (x >= -2147483648.0 && x < 2147483648.0) ? (int32_t)x : INT32_MIN;
+}
+__device__ __forceinline__ int16_t sat16(int32_t v) { return (int16_t)max(-32768, min(32767, v)); }
+__device__ __forceinline__ int16_t wrap16(int32_t v) { return (int16_t)(uint16_t)(uint32_t)v; }
+__device__ __forceinline__ int16_t abs16(int16_t v) { return wrap16(v < 0 ? -(int32_t)v : (int32_t)v); }
+
+template <int MOD>
+struct Qm;
+template <>
+struct Qm<0> {
+  static constexpr int v = 1;
+};
+template <>
+struct Qm<1> {
+  static constexpr int v = 2;
+};
+template <>
+struct Qm<2> {
+  static constexpr int v = 4;
+};
+template <>
+struct Qm<3> {
+  static constexpr int v = 6;
+};
+template <>
+struct Qm<4> {
+  static constexpr int v = 8;
+};
+
+// LLRs of symbol i (of n in the call), reference semantics per modulation.
+template <int MOD>
+__device__ __forceinline__ void demap(float re, float im, uint32_t i, uint32_t n, int16_t* o)
+{
+  if constexpr (MOD == 0) {  // demod_bpsk_lte_s (demod_soft.c:96-101)
+    const float t = -100.0f * (re + im);
+    o[0]          = wrap16(cvt_tz_d((double)t * 0.70710678118654752440));
+  } else if constexpr (MOD == 1) {  // srsran_vec_convert_fi (vector_simd.c:436-472), scale -100*sqrt(2)
+    const float    scale = (float)(-100.0 * 1.41421356237309504880);
+    const uint32_t nblk  = 16 * ((2 * n) / 16);
+    const float    v[2]  = {re, im};
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+      const int32_t t = cvt_tz(v[c] * scale);
+      o[c]            = (2 * i + c < nblk) ? sat16(t) : wrap16(t);
+    }
+  } else if constexpr (MOD == 2) {  // demod_16qam_lte_s_sse (demod_soft.c:250-299)
+    const float v[2] = {re, im};
+    if (i < 4 * (n / 4)) {
+#pragma unroll
+      for (int c = 0; c < 2; c++) {
+        const int16_t s = sat16(cvt_rn(v[c] * -400.0f));
+        o[c]            = s;
+        o[2 + c]        = wrap16(abs16(s) - 252);
+      }
+    } else {
+      const float off = 800.0f / sqrtf(10.0f);
+#pragma unroll
+      for (int c = 0; c < 2; c++) {
+        const int16_t y = wrap16(cvt_tz(400.0f * v[c]));
+        o[c]            = wrap16(-(int32_t)y);
+        o[2 + c]        = wrap16(cvt_tz((float)abs((int32_t)y) - off));
+      }
+    }
+  } else if constexpr (MOD == 3) {  // demod_64qam_lte_s_sse (demod_soft.c:569-644)
+    const float v[2] = {re, im};
+    if (i < 4 * (n / 4)) {
+#pragma unroll
+      for (int c = 0; c < 2; c++) {
+        const int16_t s = sat16(cvt_rn(v[c] * -700.0f));
+        const int16_t a = wrap16(abs16(s) - 432);
+        o[c]            = s;
+        o[2 + c]        = a;
+        o[4 + c]        = wrap16(abs16(a) - 216);
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < 2; c++) {
+        const int16_t y = wrap16(cvt_tz(700.0f * v[c]));
+        const int16_t a = wrap16((int32_t)wrap16(abs((int32_t)y)) - 432);
+        o[c]            = wrap16(-(int32_t)y);
+        o[2 + c]        = a;
+        o[4 + c]        = wrap16((int32_t)wrap16(abs((int32_t)a)) - 216);
+      }
+    }
+  } else {  // demod_256qam_lte_s (demod_soft.c:824-844)
+    const float t1 = 8.0f / sqrtf(170.0f), t2 = 4.0f / sqrtf(170.0f), t3 = 2.0f / sqrtf(170.0f);
+    float       a = -re, b = -im;
+    o[0] = wrap16(cvt_tz(1000.0f * a));
+    o[1] = wrap16(cvt_tz(1000.0f * b));
+    a    = fabsf(a) - t1;
+    b    = fabsf(b) - t1;
+    o[2] = wrap16(cvt_tz(1000.0f * a));
+    o[3] = wrap16(cvt_tz(1000.0f * b));
+    a    = fabsf(a) - t2;
+    b    = fabsf(b) - t2;
+    o[4] = wrap16(cvt_tz(1000.0f * a));
+    o[5] = wrap16(cvt_tz(1000.0f * b));
+    a    = fabsf(a) - t3;
+    b    = fabsf(b) - t3;
+    o[6] = wrap16(cvt_tz(1000.0f * a));
+    o[7] = wrap16(cvt_tz(1000.0f * b));
+  }
+}
+
+static constexpr int LLR_THREADS = 256;
+static constexpr int SPT         = 16;  // symbols per thread
+
+template <int MOD>
+__global__ __launch_bounds__(LLR_THREADS) void llr_kernel(const float2* __restrict__ sym, uint32_t n, int scramble,
+                                                          uint32_t seed, uint32_t bit0, int16_t* __restrict__ llr)
+{
+  constexpr int  Q  = Qm<MOD>::v;
+  const uint32_t s0 = (blockIdx.x * LLR_THREADS + threadIdx.x) * SPT;
+  if (s0 >= n) {
+    return;
+  }
+  const int ns = (int)min((uint32_t)SPT, n - s0);
+  float2    v[SPT];
+#pragma unroll
+  for (int k = 0; k < SPT; k++) {
+    v[k] = k < ns ? sym[s0 + k] : make_float2(0.f, 0.f);
+  }
+  uint32_t x1 = 0, x2 = 0;
+  if (scramble) {
+    gold_at(seed, bit0 + s0 * Q, x1, x2);
+  }
+  int16_t o[SPT * Q];
+#pragma unroll
+  for (int k = 0; k < SPT; k++) {
+    demap<MOD>(v[k].x, v[k].y, s0 + k, n, &o[k * Q]);
+  }
+  if (scramble) {
+#pragma unroll
+    for (int b = 0; b < SPT * Q; b++) {
+      o[b] = ((x1 ^ x2) & 1u) ? wrap16(-(int32_t)o[b]) : o[b];
+      x1   = step_x1(x1);
+      x2   = step_x2(x2);
+    }
+  }
+  int16_t* dst = llr + (size_t)s0 * Q;
+  if (ns == SPT && ((uintptr_t)dst & 15) == 0 && (SPT * Q * 2) % 16 == 0) {
+#pragma unroll
+    for (int w = 0; w < SPT * Q / 8; w++) {
+      uint4 u;
+      u.x = (uint32_t)(uint16_t)o[8 * w + 0] | ((uint32_t)(uint16_t)o[8 * w + 1] << 16);
+      u.y = (uint32_t)(uint16_t)o[8 * w + 2] | ((uint32_t)(uint16_t)o[8 * w + 3] << 16);
+      u.z = (uint32_t)(uint16_t)o[8 * w + 4] | ((uint32_t)(uint16_t)o[8 * w + 5] << 16);
+      u.w = (uint32_t)(uint16_t)o[8 * w + 6] | ((uint32_t)(uint16_t)o[8 * w + 7] << 16);
+      reinterpret_cast<uint4*>(dst)[w] = u;
+    }
+  } else {
+    for (int b = 0; b < ns * Q; b++) {
+      dst[b] = o[b];
+    }
+  }
+}
+
+hipError_t llr_launch(int mod, const float* d_sym, uint32_t nsym, int scramble, uint32_t seed, uint32_t bit0,
+                      int16_t* d_llr, hipStream_t stream)
+{
+  if (nsym == 0) {
+    return hipSuccess;
+  }
+  if (scramble) {
+    hipError_t e = gold_tables_init();
+    if (e != hipSuccess) {
+      return e;
+    }
+  }
+  const dim3    grid((nsym + LLR_THREADS * SPT - 1) / (LLR_THREADS * SPT));
+  const float2* s = reinterpret_cast<const float2*>(d_sym);
+  switch (mod) {
+    case 0:
+      hipLaunchKernelGGL(llr_kernel<0>, grid, dim3(LLR_THREADS), 0, stream, s, nsym, scramble, seed, bit0, d_llr);
+      break;
+    case 1:
+      hipLaunchKernelGGL(llr_kernel<1>, grid, dim3(LLR_THREADS), 0, stream, s, nsym, scramble, seed, bit0, d_llr);
+      break;
+    case 2:
+      hipLaunchKernelGGL(llr_kernel<2>, grid, dim3(LLR_THREADS), 0, stream, s, nsym, scramble, seed, bit0, d_llr);
+      break;
+    case 3:
+      hipLaunchKernelGGL(llr_kernel<3>, grid, dim3(LLR_THREADS), 0, stream, s, nsym, scramble, seed, bit0, d_llr);
+      break;
+    case 4:
+      hipLaunchKernelGGL(llr_kernel<4>, grid, dim3(LLR_THREADS), 0, stream, s, nsym, scramble, seed, bit0, d_llr);
+      break;
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+static constexpr int SEQ_PER_THREAD = 64;
+
+__global__ __launch_bounds__(LLR_THREADS) void seq_apply_kernel(const int16_t* __restrict__ in,
+                                                                int16_t* __restrict__ out, uint32_t len,
+                                                                uint32_t seed)
+{
+  const uint32_t i0 = (blockIdx.x * LLR_THREADS + threadIdx.x) * SEQ_PER_THREAD;
+  if (i0 >= len) {
+    return;
+  }
+  uint32_t x1, x2;
+  gold_at(seed, i0, x1, x2);
+  const uint32_t n = min((uint32_t)SEQ_PER_THREAD, len - i0);
+  for (uint32_t k = 0; k < n; k++) {
+    const int16_t v = in[i0 + k];
+    out[i0 + k]     = ((x1 ^ x2) & 1u) ? wrap16(-(int32_t)v) : v;
+    x1              = step_x1(x1);
+    x2              = step_x2(x2);
+  }
+}
+
+hipError_t seq_apply_launch(const int16_t* d_in, int16_t* d_out, uint32_t len, uint32_t seed, hipStream_t stream)
+{
+  if (len == 0) {
+    return hipSuccess;
+  }
+  hipError_t e = gold_tables_init();
+  if (e != hipSuccess) {
+    return e;
+  }
+  const dim3 grid((len + LLR_THREADS * SEQ_PER_THREAD - 1) / (LLR_THREADS * SEQ_PER_THREAD));
+  hipLaunchKernelGGL(seq_apply_kernel, grid, dim3(LLR_THREADS), 0, stream, d_in, d_out, len, seed);
+  return hipGetLastError();
+}
+
+}  // namespace srsran_amd

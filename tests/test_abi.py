@@ -41,11 +41,18 @@ def test_library_exports_every_declared_symbol():
 def test_header_is_c_and_links():
     src = r'''
 #include "srsran_tdec.h"
+#include "srsran_sch.h"
+#include "srsran_phch.h"
 #include <stdio.h>
 int main(void) {
   srsran_tdec_t q;
+  srsran_sch_t sch;
+  srsran_cbsegm_t s;
   printf("%u\n", srsran_tdec_autoimp_get_subblocks(6144));
+  if (srsran_cbsegm(&s, 75376) || s.C != 13 || s.K1 != 5824) return 1;
   if (0) { srsran_tdec_init(&q, 6144); srsran_tdec_run_all(&q, 0, 0, 8, 6144); srsran_tdec_free(&q); }
+  if (0) { srsran_sch_init(&sch); srsran_dlsch_decode(&sch, 0, 0, 0); srsran_sch_free(&sch); }
+  if (0) { cf_t x[4]; short l[24]; srsran_demod_soft_demodulate_s(SRSRAN_MOD_64QAM, x, l, 4); }
   return 0;
 }
 '''

@@ -95,6 +95,24 @@ class _PhyMixin:
             raise ValueError(rc)
         return out.copy()
 
+    def predecode(self, scheme, y, h, nlayers, codebook, scaling, noise):
+        """srsran_predecoding_type with CSI outputs. y: (nrx, n) complex64, h: (nports, nrx, n).
+        Returns x (nlayers, n) complex64 and csi (nlayers, n) float32."""
+        y = np.asarray(y, np.complex64)
+        h = np.asarray(h, np.complex64)
+        nrx, n = y.shape
+        nports = h.shape[0]
+        ya = aligned(y.size, np.complex64).reshape(y.shape)
+        ya[:] = y
+        ha = aligned(h.size, np.complex64).reshape(h.shape)
+        ha[:] = h
+        xa = aligned(max(nlayers, 2) * n, np.complex64).reshape(max(nlayers, 2), n)
+        ca = aligned(max(nlayers, 2) * n, np.float32).reshape(max(nlayers, 2), n)
+        rc = self._predecode(scheme, ya, ha, xa, ca, nrx, nports, nlayers, codebook, n, scaling, noise)
+        if rc < 0:
+            raise ValueError(rc)
+        return xa[:nlayers].copy(), ca[:nlayers].copy()
+
     def sequence_apply_s(self, llr, seed):
         x = aligned(len(llr), np.int16)
         x[:] = llr
@@ -116,6 +134,20 @@ class Oracle(_Lib, _PhyMixin):
         f = self.lib.oracle_sequence_apply_s
         f.argtypes = [_i16p, _i16p, ctypes.c_uint32, ctypes.c_uint32]
         return f
+
+    def _predecode(self, scheme, ya, ha, xa, ca, nrx, nports, nlayers, codebook, n, scaling, noise):
+        f = self.lib.oracle_predecode
+        f.argtypes = [ctypes.c_int] * 5 + [ctypes.c_void_p] * 4 + [ctypes.c_int, ctypes.c_float, ctypes.c_float]
+        return f(scheme, nrx, nports, nlayers, codebook, ya.ctypes.data, ha.ctypes.data, xa.ctypes.data,
+                 ca.ctypes.data, n, scaling, noise)
+
+    def csi_correction(self, mod, csi, e):
+        e = np.array(e, dtype=np.int16, copy=True)
+        csi = np.ascontiguousarray(csi, dtype=np.float32)
+        f = self.lib.oracle_csi_correction
+        f.argtypes = [ctypes.c_int, ctypes.c_void_p, _i16p, ctypes.c_uint32]
+        f(mod, csi.ctypes.data, _ptr(e, _i16p), e.size)
+        return e
 
     def sequence_bits(self, seed, n):
         c = np.zeros(n, np.uint8)
@@ -269,6 +301,38 @@ class Reference(_Lib, _PhyMixin):
         f = self.lib.srsran_sequence_apply_s
         f.argtypes = [_i16p, _i16p, ctypes.c_uint32, ctypes.c_uint32]
         return f
+
+    def _predecode(self, scheme, ya, ha, xa, ca, nrx, nports, nlayers, codebook, n, scaling, noise):
+        # every buffer separately aligned like srsran_vec_cf_malloc (the SIMD bodies use aligned
+        # loads), with slack: the CDD scalar tail writes index n when n is odd (precoding.c:1105-1118)
+        P = ctypes.c_void_p
+        keep = []
+
+        def buf(src, dtype):
+            b = aligned(n + 8, dtype)
+            if src is not None:
+                b[:n] = src
+            keep.append(b)
+            return b
+
+        ys = (P * 4)(*[buf(ya[r], np.complex64).ctypes.data if r < nrx else None for r in range(4)])
+        hs = ((P * 4) * 4)()
+        for p in range(nports):
+            for r in range(nrx):
+                hs[p][r] = buf(ha[p, r], np.complex64).ctypes.data
+        xb = [buf(None, np.complex64) for _ in range(xa.shape[0])]
+        cb = [buf(None, np.float32) for _ in range(2)]
+        xs = (P * 4)(*[xb[l].ctypes.data if l < len(xb) else None for l in range(4)])
+        cs = (P * 2)(cb[0].ctypes.data, cb[1].ctypes.data)
+        f = self.lib.srsran_predecoding_type
+        f.argtypes = [P, P, P, P] + [ctypes.c_int] * 6 + [ctypes.c_float, ctypes.c_float]
+        rc = f(ctypes.addressof(ys), ctypes.addressof(hs), ctypes.addressof(xs), ctypes.addressof(cs), nrx, nports,
+               nlayers, codebook, n, scheme, scaling, noise)
+        for l in range(xa.shape[0]):
+            xa[l] = xb[l][:n]
+        ca[0] = cb[0][:n]
+        ca[1] = cb[1][:n]
+        return rc
 
     def sequence_pdsch_apply_s(self, llr, rnti, q, nslot, cell_id):
         x = aligned(len(llr), np.int16)

@@ -184,3 +184,210 @@ uint32_t oracle_pdsch_seed(uint16_t rnti, int q, uint32_t nslot, uint32_t cell_i
 {
   return ((uint32_t)rnti << 14) + ((uint32_t)q << 13) + ((nslot / 2) << 9) + cell_id;
 }
+
+/* ======================= MIMO predecoding (precoding.c, mat.c) =======================
+ * The scalar ("gen") formulas of the CSI variants the PDSCH uses (pdsch.c:325 always
+ * allocates q->csi, so srsran_predecoding_type takes the *_csi paths):
+ *   PORT0  srsran_predecoding_single_csi       precoding.c:307-355
+ *   CDD    srsran_predecoding_ccd_2x2_mmse_csi precoding.c:1043-1121 (even/odd CDD precoder)
+ *   SM     srsran_predecoding_multiplex_2x2_mmse_csi precoding.c:1437-1540 (codebooks 0..2)
+ *   2x2    srsran_mat_2x2_mmse_csi_gen         mat.c:63-109
+ * Plain IEEE float, every complex op spelled out, no contraction (built with
+ * -ffp-contract=off).  The reference's SIMD bodies use rcp_ps approximations; those agree
+ * with this restatement to ~1e-3 relative (tests/test_phy_oracle.py). */
+typedef struct {
+  float r, i;
+} cpx;
+static cpx cadd(cpx a, cpx b) { return (cpx){a.r + b.r, a.i + b.i}; }
+static cpx csub(cpx a, cpx b) { return (cpx){a.r - b.r, a.i - b.i}; }
+static cpx cmul(cpx a, cpx b) { return (cpx){a.r * b.r - a.i * b.i, a.r * b.i + a.i * b.r}; }
+static cpx cconj(cpx a) { return (cpx){a.r, -a.i}; }
+static cpx cneg(cpx a) { return (cpx){-a.r, -a.i}; }
+static cpx cscale(cpx a, float s) { return (cpx){a.r * s, a.i * s}; }
+static cpx cmulj(cpx a) { return (cpx){-a.i, a.r}; }
+
+static void mmse_csi_gen(cpx y0, cpx y1, cpx h00, cpx h01, cpx h10, cpx h11, cpx* x0, cpx* x1, float* csi0,
+                         float* csi1, float noise, float norm)
+{
+  const cpx c00 = cconj(h00), c01 = cconj(h01), c10 = cconj(h10), c11 = cconj(h11);
+  cpx       a00 = cadd(cmul(c00, h00), cmul(c10, h10));
+  a00.r += noise;
+  const cpx a01 = cadd(cmul(c00, h01), cmul(c10, h11));
+  const cpx a10 = cadd(cmul(c01, h00), cmul(c11, h10));
+  cpx       a11 = cadd(cmul(c01, h01), cmul(c11, h11));
+  a11.r += noise;
+  const cpx   det = csub(cmul(a00, a11), cmul(a01, a10));
+  const float den = det.r * det.r + det.i * det.i;
+  const cpx   rcp = {det.r / den, -det.i / den};
+  const cpx   nrm = cscale(rcp, norm);
+  const cpx   b00 = cmul(a11, nrm), b01 = cmul(cneg(a01), nrm), b10 = cmul(cneg(a10), nrm), b11 = cmul(a00, nrm);
+  const cpx   w00 = cadd(cmul(b00, c00), cmul(b01, c01));
+  const cpx   w01 = cadd(cmul(b00, c10), cmul(b01, c11));
+  const cpx   w10 = cadd(cmul(b10, c00), cmul(b11, c01));
+  const cpx   w11 = cadd(cmul(b10, c10), cmul(b11, c11));
+  *x0             = cadd(cmul(y0, w00), cmul(y1, w01));
+  *x1             = cadd(cmul(y0, w10), cmul(y1, w11));
+  *csi0           = 1.0f / b00.r;
+  *csi1           = 1.0f / b11.r;
+}
+
+/* y[rx][n], h[port][rx][n] (port-major, then rx), x[layer][n], csi[layer][n]; cf32 interleaved.
+ * scheme: 0 PORT0, 3 CDD, 2 SPATIALMUX (srsran_tx_scheme_t). */
+int oracle_predecode(int          scheme,
+                     int          nrx,
+                     int          nports,
+                     int          nlayers,
+                     int          codebook,
+                     const float* y,
+                     const float* h,
+                     float*       x,
+                     float*       csi,
+                     int          n,
+                     float        scaling,
+                     float        noise)
+{
+  const cpx* Y = (const cpx*)y;
+  const cpx* H = (const cpx*)h;
+  cpx*       X = (cpx*)x;
+#define HH(p, r, k) H[((size_t)(p)*nrx + (r)) * n + (k)]
+  if (scheme == 0) {
+    if (nports != 1 || nlayers != 1) {
+      return -1;
+    }
+    const float norm = 1.0f / scaling;
+    for (int k = 0; k < n; k++) {
+      cpx   r  = {0, 0};
+      float hh = 0;
+      for (int p = 0; p < nrx; p++) {
+        const cpx hv = HH(0, p, k);
+        r            = cadd(r, cmul(Y[(size_t)p * n + k], cconj(hv)));
+        hh += hv.r * hv.r + hv.i * hv.i;
+      }
+      csi[k] = hh + noise;
+      const cpx t = cscale(r, norm);
+      X[k]        = (cpx){t.r / csi[k], t.i / csi[k]};
+    }
+    return 0;
+  }
+  if (nrx != 2 || nports != 2 || nlayers != 2) {
+    return -1;
+  }
+  float norm;
+  if (scheme == 3) {
+    norm = 2.0f / scaling;
+  } else if (scheme == 2) {
+    if (codebook == 0) {
+      norm = (float)1.41421356237309504880 / scaling;
+    } else if (codebook == 1 || codebook == 2) {
+      norm = 2.0f / scaling;
+    } else {
+      return -1;
+    }
+  } else {
+    return -1;
+  }
+  for (int k = 0; k < n; k++) {
+    const cpx a = HH(0, 0, k), b = HH(0, 1, k), c = HH(1, 0, k), d = HH(1, 1, k); /* h[port][rx] */
+    cpx       h00, h01, h10, h11;
+    if (scheme == 3) {
+      if ((k & 1) == 0) {
+        h00 = cadd(a, c);
+        h10 = cadd(b, d);
+        h01 = csub(a, c);
+        h11 = csub(b, d);
+      } else {
+        h00 = csub(a, c);
+        h10 = csub(b, d);
+        h01 = cadd(a, c);
+        h11 = cadd(b, d);
+      }
+    } else if (codebook == 0) {
+      h00 = a;
+      h01 = c;
+      h10 = b;
+      h11 = d;
+    } else if (codebook == 1) {
+      h00 = cadd(a, c);
+      h01 = csub(a, c);
+      h10 = cadd(b, d);
+      h11 = csub(b, d);
+    } else {
+      h00 = cadd(a, cmulj(c));
+      h01 = csub(a, cmulj(c));
+      h10 = cadd(b, cmulj(d));
+      h11 = csub(b, cmulj(d));
+    }
+    mmse_csi_gen(Y[k], Y[(size_t)n + k], h00, h01, h10, h11, &X[k], &X[(size_t)n + k], &csi[k], &csi[(size_t)n + k],
+                 noise, norm);
+  }
+#undef HH
+  return 0;
+}
+
+/* ======================= CSI correction (pdsch.c:523-618), SSE build =======================
+ * e: nof_bits int16 LLRs (after descrambling), csi: nof_bits/qm values of the codeword.
+ * Reproduces the SSE body exactly, including _mm_blend_ps(.., 3) handing the two symbols of a
+ * QPSK/64QAM pair each other's CSI on the middle lanes, _mm_cvtps_pi16 (round-half-even,
+ * saturate) and _mm_mulhi_pi16; the scalar tail truncates (float)e * (csi / csi_max). */
+static int16_t cvt_pi16(float x) { return sat16(cvt_rn(x)); }
+static int16_t mulhi16(int16_t a, int16_t b) { return (int16_t)(((int32_t)a * (int32_t)b) >> 16); }
+
+void oracle_csi_correction(int mod, const float* csi, int16_t* e, uint32_t nof_bits)
+{
+  const uint32_t qm = (uint32_t[]){1, 2, 4, 6, 8}[mod];
+  const uint32_t ns = nof_bits / qm;
+  float          mx = 1.0f;
+  if (ns) {
+    mx = csi[0];
+    for (uint32_t k = 1; k < ns; k++) {
+      mx = csi[k] > mx ? csi[k] : mx;
+    }
+  }
+  const float scale = 32767 / mx;
+  int64_t     i     = 0;
+  uint32_t    s     = 0;
+  switch (mod) {
+    case 1:
+      for (; i < (int64_t)nof_bits - 3; i += 4, s += 2) {
+        const int16_t c0 = cvt_pi16(csi[s] * scale), c1 = cvt_pi16(csi[s + 1] * scale);
+        const int16_t c[4] = {c1, c1, c0, c0};
+        for (int k = 0; k < 4; k++) {
+          e[i + k] = mulhi16(e[i + k], c[k]);
+        }
+      }
+      break;
+    case 2:
+      for (; i < (int64_t)nof_bits - 3; i += 4, s++) {
+        const int16_t c = cvt_pi16(csi[s] * scale);
+        for (int k = 0; k < 4; k++) {
+          e[i + k] = mulhi16(e[i + k], c);
+        }
+      }
+      break;
+    case 3:
+      for (; i < (int64_t)nof_bits - 11; i += 12, s += 2) {
+        const int16_t c1 = cvt_pi16(csi[s] * scale), c3 = cvt_pi16(csi[s + 1] * scale);
+        const int16_t c[12] = {c1, c1, c1, c1, c3, c3, c1, c1, c3, c3, c3, c3};
+        for (int k = 0; k < 12; k++) {
+          e[i + k] = mulhi16(e[i + k], c[k]);
+        }
+      }
+      break;
+    case 4:
+      for (; i < (int64_t)nof_bits - 7; i += 8, s++) {
+        const int16_t c = cvt_pi16(csi[s] * scale);
+        for (int k = 0; k < 8; k++) {
+          e[i + k] = mulhi16(e[i + k], c);
+        }
+      }
+      break;
+    default:
+      break;
+  }
+  for (uint32_t k = (uint32_t)(i / qm); k < ns; k++) {
+    const float c = csi[k] / mx;
+    for (uint32_t b = 0; b < qm; b++) {
+      e[qm * k + b] = wrap16(cvt_tz((float)e[qm * k + b] * c));
+    }
+  }
+}

@@ -80,3 +80,31 @@ def test_sequence_known_properties():
     llr = np.arange(1, 101, dtype=np.int16)
     out = ora.sequence_apply_s(llr, 0x1234)
     assert np.array_equal(np.abs(out), llr) and np.array_equal(out < 0, c[:100] == 1)
+
+
+def channel(rng, nports, nrx, n):
+    h = (rng.standard_normal((nports, nrx, n)) + 1j * rng.standard_normal((nports, nrx, n))) * 0.7
+    y = (rng.standard_normal((nrx, n)) + 1j * rng.standard_normal((nrx, n)))
+    return y.astype(np.complex64), h.astype(np.complex64)
+
+
+PRE_CASES = [(0, 1, 1, 1, 0), (0, 2, 1, 1, 0), (3, 2, 2, 2, 0), (2, 2, 2, 2, 0), (2, 2, 2, 2, 1), (2, 2, 2, 2, 2)]
+
+
+@needs_ref
+@pytest.mark.parametrize("scheme,nrx,nports,nlayers,cb", PRE_CASES)
+def test_predecode_matches_reference(scheme, nrx, nports, nlayers, cb):
+    """Oracle (exact IEEE float, scalar formulas) vs the reference SIMD build, whose
+    rcp_ps / rcp14 approximations limit agreement to ~1e-3 relative."""
+    ora, ref = Oracle(), Reference()
+    rng = np.random.default_rng(scheme * 10 + nrx + cb)
+    for n in (14400, 1202, 40):  # odd n: the reference CDD tail overruns (precoding.c:1105-1118)
+        y, h = channel(rng, nports, nrx, n)
+        for scaling, noise in ((1.0, 0.01), (0.7, 0.3)):
+            xo, co = ora.predecode(scheme, y, h, nlayers, cb, scaling, noise)
+            xr, cr = ref.predecode(scheme, y, h, nlayers, cb, scaling, noise)
+            assert np.all(np.isfinite(xo))
+            err = np.abs(xo - xr) / (np.abs(xo) + 1e-3)
+            assert np.percentile(err, 99.9) < 2e-3 and err.max() < 2e-2, (n, err.max())
+            cerr = np.abs(co - cr) / np.abs(co)
+            assert cerr.max() < 2e-3, (n, cerr.max())

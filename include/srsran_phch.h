@@ -41,16 +41,52 @@ void srsran_sequence_pdsch_apply_s(const int16_t* in,
                                    uint32_t       cell_id,
                                    uint32_t       len);
 
-/* added: fused demap + descramble on device buffers (asynchronous on `stream`, a hipStream_t;
- * NULL = default stream).  d_symbols: nsymbols cf_t; d_llr: nsymbols * Qm int16.
- * scramble = 0 skips the descrambling. */
-int srsran_pdsch_gpu_llr(srsran_mod_t   modulation,
-                         const cf_t*    d_symbols,
-                         uint32_t       nsymbols,
-                         int            scramble,
-                         uint32_t       seed,
-                         int16_t*       d_llr,
-                         void*          stream);
+/* added: fused demap + descramble (+ CSI correction, pdsch.c:523-618) on device buffers,
+ * asynchronous on `stream` (a hipStream_t; NULL = default stream).  d_symbols: nsymbols cf_t;
+ * d_llr: nsymbols * Qm int16.  scramble = 0 skips the descrambling; d_csi (per symbol) with
+ * d_csi_max (one float, e.g. from srsran_predecoding_gpu) enables the CSI correction. */
+int srsran_pdsch_gpu_llr(srsran_mod_t modulation,
+                         const cf_t*  d_symbols,
+                         uint32_t     nsymbols,
+                         int          scramble,
+                         uint32_t     seed,
+                         const float* d_csi,
+                         const float* d_csi_max,
+                         int16_t*     d_llr,
+                         void*        stream);
+
+/* ---- MIMO predecoding (precoding.c:1866-1930 srsran_predecoding_type), MMSE with CSI ----
+ * Host pointers, host-synchronous.  Supported: PORT0 (1 port, 1..4 rx), CDD and SPATIALMUX
+ * (2 ports, 2 rx, 2 layers; codebooks 0..2).  csi may be NULL. */
+int srsran_predecoding_type(cf_t*              y[4],
+                            cf_t*              h[4][4],
+                            cf_t*              x[4],
+                            float*             csi[2],
+                            int                nof_rxant,
+                            int                nof_ports,
+                            int                nof_layers,
+                            int                codebook_idx,
+                            int                nof_symbols,
+                            srsran_tx_scheme_t type,
+                            float              scaling,
+                            float              noise_estimate);
+
+/* added: the same on device buffers; d_csi_max (2 floats, or NULL) receives the per-layer CSI
+ * maximum (the caller zeroes it first). */
+int srsran_predecoding_gpu(const cf_t* const d_y[4],
+                           const cf_t* const d_h[4][4],
+                           cf_t* const       d_x[4],
+                           float* const      d_csi[2],
+                           float*            d_csi_max,
+                           int               nof_rxant,
+                           int               nof_ports,
+                           int               nof_layers,
+                           int               codebook_idx,
+                           int               nof_symbols,
+                           srsran_tx_scheme_t type,
+                           float              scaling,
+                           float              noise_estimate,
+                           void*              stream);
 
 #ifdef __cplusplus
 }

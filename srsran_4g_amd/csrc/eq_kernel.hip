@@ -1,0 +1,172 @@
+// srsran_4g_amd/csrc/eq_kernel.hip -- PDSCH MIMO predecoding (MMSE with CSI) for CDNA4.
+//
+// Formulas of the reference's CSI predecoders (the PDSCH always passes CSI buffers,
+// pdsch.c:325/871):
+//   PORT0  srsran_predecoding_single_csi        precoding.c:307-355
+//   CDD    srsran_predecoding_ccd_2x2_mmse_csi  precoding.c:1043-1121 (precoder alternates per RE)
+//   SM     srsran_predecoding_multiplex_2x2_mmse_csi precoding.c:1437-1540 (codebooks 0..2)
+//   2x2    srsran_mat_2x2_mmse_csi_gen          mat.c:63-109
+// computed in IEEE float with the scalar ("gen") operation order and no FMA contraction, so
+// the result equals oracle/phy_oracle.c bit for bit.  (The reference's SIMD bodies use
+// rcp_ps, ~1e-3 relative; see DESIGN.md.)  One thread per resource element: 2x2 CDD reads
+// 48 B and writes 24 B per RE -- HBM-bound elementwise work.  The per-layer CSI maximum that
+// csi_correction needs (pdsch.c:530) is reduced per wave and folded in with one atomicMax.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "eq_kernel.h"
+
+#pragma clang fp contract(off)
+
+namespace srsran_amd {
+
+struct cpx {
+  float r, i;
+};
+__device__ __forceinline__ cpx cadd(cpx a, cpx b) { return {a.r + b.r, a.i + b.i}; }
+__device__ __forceinline__ cpx csub(cpx a, cpx b) { return {a.r - b.r, a.i - b.i}; }
+__device__ __forceinline__ cpx cmul(cpx a, cpx b) { return {a.r * b.r - a.i * b.i, a.r * b.i + a.i * b.r}; }
+__device__ __forceinline__ cpx cconj(cpx a) { return {a.r, -a.i}; }
+__device__ __forceinline__ cpx cneg(cpx a) { return {-a.r, -a.i}; }
+__device__ __forceinline__ cpx cscale(cpx a, float s) { return {a.r * s, a.i * s}; }
+__device__ __forceinline__ cpx cmulj(cpx a) { return {-a.i, a.r}; }
+__device__ __forceinline__ cpx ld(const float2* p, uint32_t k)
+{
+  const float2 v = p[k];
+  return {v.x, v.y};
+}
+
+__device__ __forceinline__ void mmse_csi(cpx y0, cpx y1, cpx h00, cpx h01, cpx h10, cpx h11, cpx& x0, cpx& x1,
+                                         float& csi0, float& csi1, float noise, float norm)
+{
+  const cpx c00 = cconj(h00), c01 = cconj(h01), c10 = cconj(h10), c11 = cconj(h11);
+  cpx       a00 = cadd(cmul(c00, h00), cmul(c10, h10));
+  a00.r += noise;
+  const cpx a01 = cadd(cmul(c00, h01), cmul(c10, h11));
+  const cpx a10 = cadd(cmul(c01, h00), cmul(c11, h10));
+  cpx       a11 = cadd(cmul(c01, h01), cmul(c11, h11));
+  a11.r += noise;
+  const cpx   det = csub(cmul(a00, a11), cmul(a01, a10));
+  const float den = det.r * det.r + det.i * det.i;
+  const cpx   rcp = {det.r / den, -det.i / den};
+  const cpx   nrm = cscale(rcp, norm);
+  const cpx   b00 = cmul(a11, nrm), b01 = cmul(cneg(a01), nrm), b10 = cmul(cneg(a10), nrm), b11 = cmul(a00, nrm);
+  const cpx   w00 = cadd(cmul(b00, c00), cmul(b01, c01));
+  const cpx   w01 = cadd(cmul(b00, c10), cmul(b01, c11));
+  const cpx   w10 = cadd(cmul(b10, c00), cmul(b11, c01));
+  const cpx   w11 = cadd(cmul(b10, c10), cmul(b11, c11));
+  x0              = cadd(cmul(y0, w00), cmul(y1, w01));
+  x1              = cadd(cmul(y0, w10), cmul(y1, w11));
+  csi0            = 1.0f / b00.r;
+  csi1            = 1.0f / b11.r;
+}
+
+__device__ __forceinline__ void wave_max_atomic(uint32_t* dst, float v, bool valid)
+{
+  uint32_t b = valid ? __float_as_uint(v) : 0u;  // csi >= 0: IEEE bits order like the values
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    b = max(b, (uint32_t)__shfl_xor((int)b, off, 64));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMax(dst, b);
+  }
+}
+
+static constexpr int EQ_THREADS = 256;
+
+template <int SCHEME>
+__global__ __launch_bounds__(EQ_THREADS) void predecode_kernel(PredArgs a)
+{
+  const uint32_t k     = blockIdx.x * EQ_THREADS + threadIdx.x;
+  const bool     valid = k < a.n;
+  const uint32_t kk    = valid ? k : 0;
+  if constexpr (SCHEME == 0) {
+    cpx   r  = {0.f, 0.f};
+    float hh = 0.f;
+    for (int p = 0; p < a.nrx; p++) {
+      const cpx hv = ld(a.h[0][p], kk);
+      r            = cadd(r, cmul(ld(a.y[p], kk), cconj(hv)));
+      hh += hv.r * hv.r + hv.i * hv.i;
+    }
+    const float csi = hh + a.noise;
+    const cpx   t   = cscale(r, a.norm);
+    if (valid) {
+      a.csi[0][k] = csi;
+      a.x[0][k]   = make_float2(t.r / csi, t.i / csi);
+    }
+    if (a.csi_max) {
+      wave_max_atomic(&a.csi_max[0], csi, valid);
+    }
+  } else {
+    const cpx p0 = ld(a.h[0][0], kk), p1 = ld(a.h[0][1], kk), q0 = ld(a.h[1][0], kk), q1 = ld(a.h[1][1], kk);
+    cpx       h00, h01, h10, h11;
+    if constexpr (SCHEME == 3) {  // CDD: the large-delay precoder alternates with the RE index
+      if ((kk & 1) == 0) {
+        h00 = cadd(p0, q0);
+        h10 = cadd(p1, q1);
+        h01 = csub(p0, q0);
+        h11 = csub(p1, q1);
+      } else {
+        h00 = csub(p0, q0);
+        h10 = csub(p1, q1);
+        h01 = cadd(p0, q0);
+        h11 = cadd(p1, q1);
+      }
+    } else {
+      if (a.codebook == 0) {
+        h00 = p0;
+        h01 = q0;
+        h10 = p1;
+        h11 = q1;
+      } else if (a.codebook == 1) {
+        h00 = cadd(p0, q0);
+        h01 = csub(p0, q0);
+        h10 = cadd(p1, q1);
+        h11 = csub(p1, q1);
+      } else {
+        h00 = cadd(p0, cmulj(q0));
+        h01 = csub(p0, cmulj(q0));
+        h10 = cadd(p1, cmulj(q1));
+        h11 = csub(p1, cmulj(q1));
+      }
+    }
+    cpx   x0, x1;
+    float c0, c1;
+    mmse_csi(ld(a.y[0], kk), ld(a.y[1], kk), h00, h01, h10, h11, x0, x1, c0, c1, a.noise, a.norm);
+    if (valid) {
+      a.x[0][k]   = make_float2(x0.r, x0.i);
+      a.x[1][k]   = make_float2(x1.r, x1.i);
+      a.csi[0][k] = c0;
+      a.csi[1][k] = c1;
+    }
+    if (a.csi_max) {
+      wave_max_atomic(&a.csi_max[0], c0, valid);
+      wave_max_atomic(&a.csi_max[1], c1, valid);
+    }
+  }
+}
+
+hipError_t predecode_launch(const PredArgs& a, hipStream_t stream)
+{
+  if (a.n == 0) {
+    return hipSuccess;
+  }
+  const dim3 grid((a.n + EQ_THREADS - 1) / EQ_THREADS);
+  switch (a.scheme) {
+    case 0:
+      hipLaunchKernelGGL(predecode_kernel<0>, grid, dim3(EQ_THREADS), 0, stream, a);
+      break;
+    case 2:
+      hipLaunchKernelGGL(predecode_kernel<2>, grid, dim3(EQ_THREADS), 0, stream, a);
+      break;
+    case 3:
+      hipLaunchKernelGGL(predecode_kernel<3>, grid, dim3(EQ_THREADS), 0, stream, a);
+      break;
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace srsran_amd

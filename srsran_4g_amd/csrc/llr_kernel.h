@@ -10,9 +10,10 @@ namespace srsran_amd {
 hipError_t gold_tables_init();
 
 // Soft demap nsym symbols (interleaved re/im float) of modulation `mod` (0 BPSK .. 4 256QAM) into
-// int16 LLRs; when `scramble`, LLR i is negated where the Gold sequence c(bit0 + i) of `seed` is 1.
+// int16 LLRs; when `scramble`, LLR i is negated where the Gold sequence c(bit0 + i) of `seed` is 1;
+// when d_csi is set, the PDSCH CSI correction follows with the max CSI read from *d_csi_max.
 hipError_t llr_launch(int mod, const float* d_sym, uint32_t nsym, int scramble, uint32_t seed, uint32_t bit0,
-                      int16_t* d_llr, hipStream_t stream);
+                      const float* d_csi, const float* d_csi_max, int16_t* d_llr, hipStream_t stream);
 
 // out[i] = c(i) ? -in[i] : in[i] (int16 wrap) for the Gold sequence of `seed`.
 hipError_t seq_apply_launch(const int16_t* d_in, int16_t* d_out, uint32_t len, uint32_t seed, hipStream_t stream);

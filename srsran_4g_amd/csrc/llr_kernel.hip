@@ -210,9 +210,64 @@ __device__ __forceinline__ void demap(float re, float im, uint32_t i, uint32_t n
 static constexpr int LLR_THREADS = 256;
 static constexpr int SPT         = 16;  // symbols per thread
 
+// csi_correction (pdsch.c:523-618, SSE build) for the LLRs o[0..Q) of symbol s:
+// symbols inside the SSE blocks get mulhi(e, cvtps_pi16(csi * 32767/csi_max)) -- with the
+// reference's _mm_blend_ps(.., 3) swap: in a QPSK/64QAM symbol pair the middle lanes take
+// the other symbol's CSI -- and the tail truncates (float)e * (csi / csi_max).
+__device__ __forceinline__ int16_t cvt_pi16(float x) { return sat16(cvt_rn(x)); }
+__device__ __forceinline__ int16_t mulhi16(int16_t a, int16_t b) { return (int16_t)(((int32_t)a * (int32_t)b) >> 16); }
+
+template <int MOD>
+__device__ __forceinline__ void csi_correct(int16_t* o, uint32_t s, const float* csi, float mx, uint32_t nof_bits)
+{
+  constexpr int Q     = Qm<MOD>::v;
+  const float   scale = 32767.0f / mx;
+  uint32_t      nblk;  // symbols covered by the SSE blocks
+  if constexpr (MOD == 1) {
+    nblk = 2 * (nof_bits / 4);
+  } else if constexpr (MOD == 2) {
+    nblk = nof_bits / 4;
+  } else if constexpr (MOD == 3) {
+    nblk = 2 * (nof_bits / 12);
+  } else if constexpr (MOD == 4) {
+    nblk = nof_bits / 8;
+  } else {
+    nblk = 0;
+  }
+  if (s < nblk) {
+    const int16_t c = cvt_pi16(csi[s] * scale);
+    if constexpr (MOD == 1) {  // pair (s, s^1): lanes 0,1 take the odd symbol's CSI, lanes 2,3 the even's
+      const int16_t co = cvt_pi16(csi[s ^ 1u] * scale);
+#pragma unroll
+      for (int b = 0; b < Q; b++) {
+        o[b] = mulhi16(o[b], co);
+      }
+    } else if constexpr (MOD == 3) {  // even s: LLR 4,5 use s+1; odd s: LLR 0,1 use s-1
+      const int16_t co = cvt_pi16(csi[s ^ 1u] * scale);
+#pragma unroll
+      for (int b = 0; b < Q; b++) {
+        const bool other = (s & 1u) ? (b < 2) : (b >= 4);
+        o[b]             = mulhi16(o[b], other ? co : c);
+      }
+    } else {
+#pragma unroll
+      for (int b = 0; b < Q; b++) {
+        o[b] = mulhi16(o[b], c);
+      }
+    }
+  } else {
+    const float c = csi[s] / mx;
+#pragma unroll
+    for (int b = 0; b < Q; b++) {
+      o[b] = wrap16(cvt_tz((float)o[b] * c));
+    }
+  }
+}
+
 template <int MOD>
 __global__ __launch_bounds__(LLR_THREADS) void llr_kernel(const float2* __restrict__ sym, uint32_t n, int scramble,
-                                                          uint32_t seed, uint32_t bit0, int16_t* __restrict__ llr)
+                                                          uint32_t seed, uint32_t bit0, const float* __restrict__ csi,
+                                                          const float* __restrict__ csi_max, int16_t* __restrict__ llr)
 {
   constexpr int  Q  = Qm<MOD>::v;
   const uint32_t s0 = (blockIdx.x * LLR_THREADS + threadIdx.x) * SPT;
@@ -242,6 +297,15 @@ __global__ __launch_bounds__(LLR_THREADS) void llr_kernel(const float2* __restri
       x2   = step_x2(x2);
     }
   }
+  if (csi) {  // after descrambling, as pdsch.c:735-737 orders it
+    const float mx = *csi_max;
+#pragma unroll
+    for (int k = 0; k < SPT; k++) {
+      if (k < ns) {
+        csi_correct<MOD>(&o[k * Q], s0 + k, csi, mx, n * Q);
+      }
+    }
+  }
   int16_t* dst = llr + (size_t)s0 * Q;
   if (ns == SPT && ((uintptr_t)dst & 15) == 0 && (SPT * Q * 2) % 16 == 0) {
 #pragma unroll
@@ -261,7 +325,7 @@ __global__ __launch_bounds__(LLR_THREADS) void llr_kernel(const float2* __restri
 }
 
 hipError_t llr_launch(int mod, const float* d_sym, uint32_t nsym, int scramble, uint32_t seed, uint32_t bit0,
-                      int16_t* d_llr, hipStream_t stream)
+                      const float* d_csi, const float* d_csi_max, int16_t* d_llr, hipStream_t stream)
 {
   if (nsym == 0) {
     return hipSuccess;
@@ -276,19 +340,24 @@ hipError_t llr_launch(int mod, const float* d_sym, uint32_t nsym, int scramble, 
   const float2* s = reinterpret_cast<const float2*>(d_sym);
   switch (mod) {
     case 0:
-      hipLaunchKernelGGL(llr_kernel<0>, grid, dim3(LLR_THREADS), 0, stream, s, nsym, scramble, seed, bit0, d_llr);
+      hipLaunchKernelGGL(llr_kernel<0>, grid, dim3(LLR_THREADS), 0, stream, s, nsym, scramble, seed, bit0, d_csi,
+                         d_csi_max, d_llr);
       break;
     case 1:
-      hipLaunchKernelGGL(llr_kernel<1>, grid, dim3(LLR_THREADS), 0, stream, s, nsym, scramble, seed, bit0, d_llr);
+      hipLaunchKernelGGL(llr_kernel<1>, grid, dim3(LLR_THREADS), 0, stream, s, nsym, scramble, seed, bit0, d_csi,
+                         d_csi_max, d_llr);
       break;
     case 2:
-      hipLaunchKernelGGL(llr_kernel<2>, grid, dim3(LLR_THREADS), 0, stream, s, nsym, scramble, seed, bit0, d_llr);
+      hipLaunchKernelGGL(llr_kernel<2>, grid, dim3(LLR_THREADS), 0, stream, s, nsym, scramble, seed, bit0, d_csi,
+                         d_csi_max, d_llr);
       break;
     case 3:
-      hipLaunchKernelGGL(llr_kernel<3>, grid, dim3(LLR_THREADS), 0, stream, s, nsym, scramble, seed, bit0, d_llr);
+      hipLaunchKernelGGL(llr_kernel<3>, grid, dim3(LLR_THREADS), 0, stream, s, nsym, scramble, seed, bit0, d_csi,
+                         d_csi_max, d_llr);
       break;
     case 4:
-      hipLaunchKernelGGL(llr_kernel<4>, grid, dim3(LLR_THREADS), 0, stream, s, nsym, scramble, seed, bit0, d_llr);
+      hipLaunchKernelGGL(llr_kernel<4>, grid, dim3(LLR_THREADS), 0, stream, s, nsym, scramble, seed, bit0, d_csi,
+                         d_csi_max, d_llr);
       break;
     default:
       return hipErrorInvalidValue;

@@ -10,6 +10,7 @@
 #include <mutex>
 
 #include "../../include/srsran_phch.h"
+#include "eq_kernel.h"
 #include "llr_kernel.h"
 
 using namespace srsran_amd;
@@ -54,6 +55,39 @@ bool ctx_ready()
   return hipStreamCreateWithFlags(&g_ctx.stream, hipStreamNonBlocking) == hipSuccess;
 }
 
+// srsran_predecoding_type's dispatch (precoding.c:1866-1930) for the MMSE CSI predecoders
+// provided here; fills the scheme-dependent norm.  Returns false for unsupported shapes.
+bool pred_setup(PredArgs& a, int nrx, int nports, int nlayers, int codebook, int type, float scaling)
+{
+  a.nrx      = nrx;
+  a.codebook = codebook;
+  switch (type) {
+    case SRSRAN_TXSCHEME_PORT0:
+      if (nports != 1 || nlayers != 1 || nrx < 1 || nrx > 4) {
+        return false;
+      }
+      a.scheme = 0;
+      a.norm   = 1.0f / scaling;  // precoding.c:319
+      return true;
+    case SRSRAN_TXSCHEME_CDD:
+      if (nports != 2 || nrx != 2 || nlayers != 2) {
+        return false;
+      }
+      a.scheme = 3;
+      a.norm   = 2.0f / scaling;  // precoding.c:1052
+      return true;
+    case SRSRAN_TXSCHEME_SPATIALMUX:
+      if (nports != 2 || nrx != 2 || nlayers != 2 || codebook < 0 || codebook > 2) {
+        return false;
+      }
+      a.scheme = 2;
+      a.norm   = codebook == 0 ? (float)1.41421356237309504880 / scaling : 2.0f / scaling;  // precoding.c:1451-1458
+      return true;
+    default:
+      return false;
+  }
+}
+
 uint32_t pdsch_seed(uint16_t rnti, int q, uint32_t nslot, uint32_t cell_id)
 {
   return ((uint32_t)rnti << 14) + ((uint32_t)q << 13) + ((nslot / 2) << 9) + cell_id;  // sequences.c:62-65
@@ -79,8 +113,8 @@ int srsran_demod_soft_demodulate_s(srsran_mod_t modulation, const cf_t* symbols,
     return -1;
   }
   hipMemcpyAsync(g_ctx.d_a, symbols, (size_t)nsymbols * sizeof(cf_t), hipMemcpyHostToDevice, g_ctx.stream);
-  if (llr_launch((int)modulation, (const float*)g_ctx.d_a, (uint32_t)nsymbols, 0, 0, 0, (int16_t*)g_ctx.d_b,
-                 g_ctx.stream) != hipSuccess) {
+  if (llr_launch((int)modulation, (const float*)g_ctx.d_a, (uint32_t)nsymbols, 0, 0, 0, nullptr, nullptr,
+                 (int16_t*)g_ctx.d_b, g_ctx.stream) != hipSuccess) {
     return -1;
   }
   hipMemcpyAsync(llr, g_ctx.d_b, (size_t)nsymbols * q * sizeof(int16_t), hipMemcpyDeviceToHost, g_ctx.stream);
@@ -117,18 +151,121 @@ void srsran_sequence_pdsch_apply_s(const int16_t* in,
   srsran_sequence_apply_s(in, out, len, pdsch_seed(rnti, q, nslot, cell_id));
 }
 
+int srsran_predecoding_type(cf_t*              y[4],
+                            cf_t*              h[4][4],
+                            cf_t*              x[4],
+                            float*             csi[2],
+                            int                nof_rxant,
+                            int                nof_ports,
+                            int                nof_layers,
+                            int                codebook_idx,
+                            int                nof_symbols,
+                            srsran_tx_scheme_t type,
+                            float              scaling,
+                            float              noise_estimate)
+{
+  PredArgs a{};
+  if (nof_ports > 4 || nof_layers > 4 || nof_symbols < 0 ||
+      !pred_setup(a, nof_rxant, nof_ports, nof_layers, codebook_idx, (int)type, scaling)) {
+    fprintf(stderr, "[srsran_predecoding] unsupported: scheme %d, %d ports, %d rx, %d layers\n", (int)type,
+            nof_ports, nof_rxant, nof_layers);
+    return SRSRAN_ERROR;
+  }
+  if (nof_symbols == 0) {
+    return SRSRAN_SUCCESS;
+  }
+  const size_t n   = (size_t)nof_symbols;
+  const size_t nin = (size_t)nof_rxant * (1 + nof_ports);  // y + h
+  const size_t nout = (size_t)nof_layers;
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!ctx_ready() || !grow(&g_ctx.d_a, &g_ctx.a_cap, nin * n * sizeof(cf_t)) ||
+      !grow(&g_ctx.d_b, &g_ctx.b_cap, nout * n * (sizeof(cf_t) + sizeof(float)))) {
+    return SRSRAN_ERROR;
+  }
+  cf_t*  dy  = (cf_t*)g_ctx.d_a;
+  cf_t*  dh  = dy + (size_t)nof_rxant * n;
+  cf_t*  dx  = (cf_t*)g_ctx.d_b;
+  float* dcs = (float*)(dx + nout * n);
+  for (int r = 0; r < nof_rxant; r++) {
+    hipMemcpyAsync(dy + r * n, y[r], n * sizeof(cf_t), hipMemcpyHostToDevice, g_ctx.stream);
+    a.y[r] = (const float2*)(dy + r * n);
+    for (int p = 0; p < nof_ports; p++) {
+      cf_t* d = dh + ((size_t)p * nof_rxant + r) * n;
+      hipMemcpyAsync(d, h[p][r], n * sizeof(cf_t), hipMemcpyHostToDevice, g_ctx.stream);
+      a.h[p][r] = (const float2*)d;
+    }
+  }
+  for (int l = 0; l < nof_layers; l++) {
+    a.x[l] = (float2*)(dx + l * n);
+  }
+  a.csi[0]  = dcs;
+  a.csi[1]  = dcs + n;
+  a.csi_max = nullptr;
+  a.n       = (uint32_t)n;
+  a.noise   = noise_estimate;
+  if (predecode_launch(a, g_ctx.stream) != hipSuccess) {
+    return SRSRAN_ERROR;
+  }
+  for (int l = 0; l < nof_layers; l++) {
+    hipMemcpyAsync(x[l], dx + l * n, n * sizeof(cf_t), hipMemcpyDeviceToHost, g_ctx.stream);
+    if (csi && l < 2 && csi[l]) {
+      hipMemcpyAsync(csi[l], dcs + l * n, n * sizeof(float), hipMemcpyDeviceToHost, g_ctx.stream);
+    }
+  }
+  return hipStreamSynchronize(g_ctx.stream) == hipSuccess ? SRSRAN_SUCCESS : SRSRAN_ERROR;
+}
+
+int srsran_predecoding_gpu(const cf_t* const  d_y[4],
+                           const cf_t* const  d_h[4][4],
+                           cf_t* const        d_x[4],
+                           float* const       d_csi[2],
+                           float*             d_csi_max,
+                           int                nof_rxant,
+                           int                nof_ports,
+                           int                nof_layers,
+                           int                codebook_idx,
+                           int                nof_symbols,
+                           srsran_tx_scheme_t type,
+                           float              scaling,
+                           float              noise_estimate,
+                           void*              stream)
+{
+  PredArgs a{};
+  if (!d_y || !d_h || !d_x || !d_csi || nof_symbols < 0 ||
+      !pred_setup(a, nof_rxant, nof_ports, nof_layers, codebook_idx, (int)type, scaling)) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  for (int r = 0; r < nof_rxant; r++) {
+    a.y[r] = (const float2*)d_y[r];
+    for (int p = 0; p < nof_ports; p++) {
+      a.h[p][r] = (const float2*)d_h[p][r];
+    }
+  }
+  for (int l = 0; l < nof_layers; l++) {
+    a.x[l] = (float2*)d_x[l];
+  }
+  a.csi[0]  = d_csi[0];
+  a.csi[1]  = d_csi[1];
+  a.csi_max = (uint32_t*)d_csi_max;
+  a.n       = (uint32_t)nof_symbols;
+  a.noise   = noise_estimate;
+  return predecode_launch(a, (hipStream_t)stream) == hipSuccess ? SRSRAN_SUCCESS : SRSRAN_ERROR;
+}
+
 int srsran_pdsch_gpu_llr(srsran_mod_t modulation,
                          const cf_t*  d_symbols,
                          uint32_t     nsymbols,
                          int          scramble,
                          uint32_t     seed,
+                         const float* d_csi,
+                         const float* d_csi_max,
                          int16_t*     d_llr,
                          void*        stream)
 {
-  if (srsran_mod_bits_x_symbol(modulation) == 0 || (nsymbols && (!d_symbols || !d_llr))) {
+  if (srsran_mod_bits_x_symbol(modulation) == 0 || (nsymbols && (!d_symbols || !d_llr)) || (d_csi && !d_csi_max)) {
     return SRSRAN_ERROR_INVALID_INPUTS;
   }
-  return llr_launch((int)modulation, (const float*)d_symbols, nsymbols, scramble, seed, 0, d_llr,
+  return llr_launch((int)modulation, (const float*)d_symbols, nsymbols, scramble, seed, 0, d_csi, d_csi_max, d_llr,
                     (hipStream_t)stream) == hipSuccess
              ? SRSRAN_SUCCESS
              : SRSRAN_ERROR;

@@ -149,6 +149,32 @@ class Oracle(_Lib, _PhyMixin):
         f(mod, csi.ctypes.data, _ptr(e, _i16p), e.size)
         return e
 
+    def crs_pilots(self, cell_id, nof_prb, pp, sf):
+        out = np.zeros(4 * 2 * nof_prb, np.complex64)
+        f = self.lib.oracle_crs_pilots
+        f.argtypes = [ctypes.c_uint32] * 4 + [ctypes.c_void_p]
+        f(cell_id, nof_prb, pp, sf, out.ctypes.data)
+        return out[: (4 if pp == 0 else 2) * 2 * nof_prb]
+
+    def gauss_filter(self, order, std):
+        f = np.zeros(16, np.float32)
+        g = self.lib.oracle_gauss_filter
+        g.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_float]
+        g.restype = ctypes.c_uint32
+        n = g(f.ctypes.data, order, std)
+        return f[:n]
+
+    def chest_dl(self, grids, nof_prb, cell_id, nports, sf_idx, symbol_sz):
+        """CRS channel estimate (srsUE defaults). grids: (nrx, 14*12*nof_prb) -> (ce (nports, nrx, n), stats)."""
+        grids = np.ascontiguousarray(grids, np.complex64)
+        nrx, n = grids.shape
+        ce = np.zeros((nports, nrx, n), np.complex64)
+        out = np.zeros(4, np.float32)
+        f = self.lib.oracle_chest_dl
+        f.argtypes = [ctypes.c_void_p] + [ctypes.c_uint32] * 6 + [ctypes.c_void_p, ctypes.c_void_p]
+        f(grids.ctypes.data, nof_prb, cell_id, nports, nrx, sf_idx, symbol_sz, ce.ctypes.data, out.ctypes.data)
+        return ce, dict(noise=float(out[0]), rsrp=float(out[1]), rssi=float(out[2]), cfo=float(out[3]))
+
     def sequence_bits(self, seed, n):
         c = np.zeros(n, np.uint8)
         self.lib.oracle_sequence_bits.argtypes = [ctypes.c_uint32, _u8p, ctypes.c_uint32]

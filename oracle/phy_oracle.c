@@ -391,3 +391,304 @@ void oracle_csi_correction(int mod, const float* csi, int16_t* e, uint32_t nof_b
     }
   }
 }
+
+/* ======================= DL channel estimation (chest_dl.c, refsignal_dl.c) =======================
+ * srsUE default configuration (srsue/src/phy/phy_common.cc:83-107, main.cc defaults): estimator
+ * AVERAGE, Gauss smoothing filter order 4 / stddev 1.0, noise algorithm REFS, normal subframe,
+ * normal CP, FDD.  Restated (chest_dl.c and refsignal_dl.c include the generated srsran.h):
+ *   CRS             srsran_refsignal_cs_set_cell  refsignal_dl.c:65-119, fidx/nsymbol 249-266
+ *   LS              estimate_port                 chest_dl.c:806-834
+ *   noise (REFS)    estimate_noise_pilots         chest_dl.c:325-400
+ *   time average    average_pilots                chest_dl.c:557-600
+ *   smoothing       srsran_conv_same_cf           convolution.c:182-218 (edge extrapolation)
+ *   Gauss filter    srsran_chest_set_smooth_filter_gauss chest_common.c:70-95
+ *   interpolation   srsran_interp_linear_offset   interp.c:258-285, then copy to all symbols
+ *   CFO             chest_estimate_cfo            chest_dl.c:621-641
+ * grid: [rx][14 * 12 * nof_prb] cf32; ce: [port][rx][14 * 12 * nof_prb]. */
+#define NRE 12
+static const float kPi = 3.14159265358979323846f;
+
+static uint32_t crs_v(uint32_t port, uint32_t l)
+{
+  switch (port) {
+    case 0:
+      return (l % 2) ? 3 : 0;
+    case 1:
+      return (l % 2) ? 0 : 3;
+    case 2:
+      return l == 0 ? 0 : 3;
+    default:
+      return l == 0 ? 3 : 0;
+  }
+}
+static uint32_t crs_fidx(uint32_t cell_id, uint32_t l, uint32_t port) { return (crs_v(port, l) + cell_id % 6) % 6; }
+static uint32_t crs_nsymbol(uint32_t l, uint32_t port) { return port < 2 ? ((l % 2) ? (l / 2 + 1) * 7 - 3 : (l / 2) * 7) : 1 + l * 7; }
+static uint32_t crs_nof_symbols(uint32_t port) { return port < 2 ? 4 : 2; }
+
+/* pilots of port pair pp (ports 2pp, 2pp+1) for subframe sf: [nsym][2 * nof_prb] */
+void oracle_crs_pilots(uint32_t cell_id, uint32_t nof_prb, uint32_t pp, uint32_t sf, float* out)
+{
+  cpx*           P        = (cpx*)out;
+  const uint32_t nsym_slot = crs_nof_symbols(2 * pp) / 2;
+  uint8_t        c[4 * 110];
+  for (uint32_t s = 0; s < 2; s++) {
+    const uint32_t ns = 2 * sf + s;
+    for (uint32_t l = 0; l < nsym_slot; l++) {
+      const uint32_t lp     = crs_nsymbol(l, 2 * pp);
+      const uint32_t c_init = 1024 * (7 * (ns + 1) + lp + 1) * (2 * cell_id + 1) + 2 * cell_id + 1;
+      oracle_sequence_bits(c_init, c, 4 * 110);
+      for (uint32_t i = 0; i < 2 * nof_prb; i++) {
+        const uint32_t mp = i + 110 - nof_prb;
+        P[2 * nof_prb * (s * nsym_slot + l) + i] =
+            (cpx){(1 - 2 * (float)c[2 * mp]) * (float)0.70710678118654752440,
+                  (1 - 2 * (float)c[2 * mp + 1]) * (float)0.70710678118654752440};
+      }
+    }
+  }
+}
+
+static float avg_power(const cpx* x, uint32_t n)
+{
+  float acc = 0;
+  for (uint32_t k = 0; k < n; k++) {
+    acc += x[k].r * x[k].r + x[k].i * x[k].i;
+  }
+  return n ? acc / (float)n : 0.f;
+}
+
+static float noise_pilots(const cpx* pe, uint32_t nsym, uint32_t nref, uint32_t fidx0)
+{
+  cpx tmp[4 * 110];
+  if (nsym < 3) { /* chest_dl.c:345-354 */
+    for (uint32_t k = 0; k < nref - 2; k++) {
+      cpx t  = cadd(cadd(pe[k], pe[k + 1]), pe[k + 2]);
+      t      = cscale(t, 1.0f / 3.0f);
+      tmp[k] = csub(pe[k + 1], t);
+    }
+    return avg_power(tmp, nref - 2);
+  }
+  float    sum   = 0;
+  uint32_t count = 0;
+  for (uint32_t i = 1; i < nsym - 1; i++) {
+    const uint32_t off = ((fidx0 < 3) ^ (i & 1)) ? 0 : 1;
+    const cpx*     cur = pe + i * nref;
+    for (uint32_t k = 0; k < nref; k++) {
+      tmp[k] = cur[k];
+    }
+    for (int nb = 0; nb < 2; nb++) {
+      const cpx* o = pe + (nb == 0 ? i - 1 : i + 1) * nref;
+      for (uint32_t k = 0; k < nref - off; k++) {
+        tmp[off + k] = cadd(o[k], tmp[off + k]);
+      }
+      for (uint32_t k = 0; k < nref + off - 1; k++) {
+        tmp[k] = cadd(o[1 - off + k], tmp[k]);
+      }
+      if (off) {
+        tmp[0] = cadd(tmp[0], csub(cscale(o[0], 2.0f), o[1]));
+      } else {
+        tmp[nref - 1] = cadd(tmp[nref - 1], csub(cscale(o[nref - 2], 2.0f), o[nref - 1]));
+      }
+    }
+    for (uint32_t k = 0; k < nref; k++) {
+      tmp[k] = csub(cur[k], cscale(tmp[k], 1.0f / 5.0f));
+    }
+    sum += avg_power(tmp, nref);
+    count++;
+  }
+  return sum / (float)count;
+}
+
+static void conv_same(const cpx* in, const float* f, cpx* out, uint32_t N, uint32_t M)
+{
+  cpx first[16], last[16];
+  for (uint32_t i = 0; i < M + M / 2; i++) {
+    first[i] = i < M / 2 ? csub(cscale(in[1], (float)(2 + M / 2 - i)), cscale(in[0], (float)(1 + M / 2 - i)))
+                         : in[i - M / 2];
+    last[i] = i >= M - 1 ? csub(cscale(in[N - 1], (float)(2 + i - M / 2)), cscale(in[N - 2], (float)(1 + i - M / 2)))
+                         : in[N - M + i + 1];
+  }
+  uint32_t i = 0;
+  for (; i < M / 2; i++) {
+    cpx acc = {0, 0};
+    for (uint32_t k = 0; k < M; k++) {
+      acc = cadd(acc, cscale(first[i + k], f[k]));
+    }
+    out[i] = acc;
+  }
+  for (; i < N - M / 2; i++) {
+    cpx acc = {0, 0};
+    for (uint32_t k = 0; k < M; k++) {
+      acc = cadd(acc, cscale(in[i - M / 2 + k], f[k]));
+    }
+    out[i] = acc;
+  }
+  for (uint32_t j = 0; i < N; i++, j++) {
+    cpx acc = {0, 0};
+    for (uint32_t k = 0; k < M; k++) {
+      acc = cadd(acc, cscale(last[j + k], f[k]));
+    }
+    out[i] = acc;
+  }
+}
+
+void oracle_conv_same(const float* in, const float* f, float* out, uint32_t N, uint32_t M)
+{
+  conv_same((const cpx*)in, f, (cpx*)out, N, M);
+}
+
+uint32_t oracle_gauss_filter(float* f, uint32_t order, float std_dev)
+{
+  const uint32_t len = order + 1;
+  const int      c   = (int)(len - 1) / 2;
+  float          s   = 0;
+  for (uint32_t i = 0; i < len; i++) {
+    f[i] = expf(-powf((float)((int)i - c), 2) / (2.0f * powf(std_dev, 2)));
+  }
+  for (uint32_t i = 0; i < len; i++) {
+    s += f[i];
+  }
+  for (uint32_t i = 0; i < len; i++) {
+    f[i] *= 1.0f / s;
+  }
+  return len;
+}
+
+static void interp_linear_offset(const cpx* in, cpx* out, uint32_t len, uint32_t M, uint32_t off_st, uint32_t off_end)
+{
+  for (uint32_t j = 0; j < off_st; j++) {
+    const cpx d = csub(in[1], in[0]);
+    const cpx t = cscale(d, (float)(j + 1));
+    out[off_st - j - 1] = csub(in[0], (cpx){t.r / (float)M, t.i / (float)M});
+  }
+  const float rM = (float)1 / M;
+  uint32_t    i  = 0;
+  for (; i < len - 1; i++) {
+    const cpx d = cscale(csub(in[i + 1], in[i]), rM);
+    for (uint32_t j = 0; j < M; j++) {
+      out[i * M + j + off_st] = cadd(in[i], cscale(d, (float)j));
+    }
+  }
+  if (len > 1) {
+    const cpx d = csub(in[len - 1], in[len - 2]);
+    for (uint32_t j = 0; j < off_end; j++) {
+      const cpx t = cscale(d, (float)j);
+      out[i * M + j + off_st] = cadd(in[i], (cpx){t.r / (float)M, t.i / (float)M});
+    }
+  }
+}
+
+/* out[0..5]: noise_estimate, rsrp, rssi, cfo, per (rx,port) noise not returned */
+int oracle_chest_dl(const float* grid, uint32_t nof_prb, uint32_t cell_id, uint32_t nports, uint32_t nrx,
+                    uint32_t sf_idx, uint32_t symbol_sz, float* ce, float* out)
+{
+  const uint32_t nre = NRE * nof_prb, nsf = 14 * nre;
+  const cpx*     G   = (const cpx*)grid;
+  cpx*           CE  = (cpx*)ce;
+  float          filt[8];
+  const uint32_t flen = oracle_gauss_filter(filt, 4, 1.0f);
+  static cpx     pil[2][4 * 2 * 110];
+  oracle_crs_pilots(cell_id, nof_prb, 0, sf_idx, (float*)pil[0]);
+  oracle_crs_pilots(cell_id, nof_prb, 1, sf_idx, (float*)pil[1]);
+  float noise[4][4], rsrp[4][4], rssi[4][4], cfo = 0;
+  for (uint32_t rx = 0; rx < nrx; rx++) {
+    const cpx* in = G + (size_t)rx * nsf;
+    for (uint32_t port = 0; port < nports; port++) {
+      const uint32_t nsym = crs_nof_symbols(port), nref = 2 * nof_prb, np = nsym * nref;
+      cpx            recv[4 * 220], pe[4 * 220], avg[4 * 220], tmp[4 * 220];
+      for (uint32_t l = 0; l < nsym; l++) {
+        const uint32_t sym = crs_nsymbol(l, port);
+        uint32_t       f   = crs_fidx(cell_id, l, port);
+        for (uint32_t i = 0; i < nref; i++, f += 6) {
+          recv[l * nref + i] = in[sym * nre + f];
+        }
+      }
+      for (uint32_t k = 0; k < np; k++) {
+        pe[k] = cmul(recv[k], cconj(pil[port / 2][k]));
+      }
+      rsrp[rx][port] = avg_power(recv, np);
+      float rs       = 0;
+      for (uint32_t l = 0; l < nsym; l++) {
+        const cpx* t = in + crs_nsymbol(l, port) * nre;
+        for (uint32_t k = 0; k < nre; k++) {
+          rs += t[k].r * t[k].r + t[k].i * t[k].i;
+        }
+      }
+      rssi[rx][port] = rs / (float)nsym;
+      if (nsym == 4) { /* chest_estimate_cfo (port-0 geometry), kept from the last port processed */
+        cpx sum = {0, 0};
+        for (uint32_t i = 0; i < 2; i++) {
+          for (uint32_t k = 0; k < np / 4; k++) {
+            sum = cadd(sum, cmul(pe[i * np / 4 + k], cconj(pe[(i + 2) * np / 4 + k])));
+          }
+        }
+        const float n  = (float)symbol_sz;
+        const float ng = (float)(int)ceilf(144.0f * n / 2048.0f); /* SRSRAN_CP_LEN_NORM(1, n) */
+        cfo            = -atan2f(sum.i, sum.r) * n / (7.0f * (n + ng)) / 2 / kPi;
+      }
+      const uint32_t fidx0 = crs_fidx(cell_id, 0, port);
+      noise[rx][port]      = noise_pilots(pe, nsym, nref, fidx0);
+      /* average_pilots: time average into a 3-subcarrier grid, then smoothing */
+      uint32_t nr = nref, ns = nsym;
+      if (nsym > 1) {
+        const cpx* a = fidx0 < 3 ? pe : pe + nref;
+        const cpx* b = fidx0 < 3 ? pe + nref : pe;
+        for (uint32_t k = 0; k < nref; k++) {
+          tmp[2 * k]     = a[k];
+          tmp[2 * k + 1] = b[k];
+        }
+        for (uint32_t l = 2; l < nsym - 1; l += 2) {
+          const cpx* c = fidx0 < 3 ? pe + l * nref : pe + (l + 1) * nref;
+          const cpx* d = fidx0 < 3 ? pe + (l + 1) * nref : pe + l * nref;
+          for (uint32_t k = 0; k < nref; k++) {
+            tmp[2 * k]     = cadd(tmp[2 * k], c[k]);
+            tmp[2 * k + 1] = cadd(tmp[2 * k + 1], d[k]);
+          }
+        }
+        nr *= 2;
+        for (uint32_t k = 0; k < nr; k++) {
+          pe[k] = cscale(tmp[k], 2.0f / (float)nsym);
+        }
+        ns = 1;
+      }
+      (void)ns;
+      conv_same(pe, filt, avg, nr, flen);
+      cpx* row = CE + ((size_t)port * nrx + rx) * nsf;
+      if (nsym > 1) {
+        const uint32_t off = cell_id % 3;
+        interp_linear_offset(avg, row, nr, 3, off, 3 - off);
+      } else {
+        const uint32_t off = crs_fidx(cell_id, 0, port);
+        interp_linear_offset(avg, row, nr, 6, off, 6 - off);
+      }
+      for (uint32_t l = 1; l < 14; l++) {
+        memcpy(row + l * nre, row, nre * sizeof(cpx));
+      }
+    }
+  }
+  float n = 0;
+  for (uint32_t rx = 0; rx < nrx; rx++) {
+    float s = 0;
+    for (uint32_t p = 0; p < nports; p++) {
+      s += noise[rx][p];
+    }
+    n += s / (float)nports;
+  }
+  out[0] = n / (float)nrx;
+  float best = -1e9f;
+  for (uint32_t p = 0; p < nports; p++) {
+    float s = 0;
+    for (uint32_t rx = 0; rx < nrx; rx++) {
+      s += rsrp[rx][p];
+    }
+    s /= (float)nrx;
+    best = s > best ? s : best;
+  }
+  out[1] = best;
+  float r = 0;
+  for (uint32_t rx = 0; rx < nrx; rx++) {
+    r += 4 * rssi[rx][0] / (float)nof_prb / (float)NRE;
+  }
+  out[2] = r / (float)nrx;
+  out[3] = cfo;
+  return 0;
+}

@@ -6,3 +6,4 @@ declared in include/srsran_tdec.h.  ``srsran_4g_amd.tdec`` binds it for Python.
 from . import tdec  # noqa: F401
 from . import sch  # noqa: F401
 from . import phch  # noqa: F401
+from . import ue_dl  # noqa: F401

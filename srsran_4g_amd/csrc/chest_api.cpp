@@ -1,0 +1,423 @@
+// srsran_4g_amd/csrc/chest_api.cpp -- C-ABI host side of the DL channel estimator.
+//
+// include/srsran_ue_dl.h: srsran_chest_dl_{init,free,set_cell,res_init,res_free,estimate,
+// estimate_cfg} (chest_dl.c:68-1027) plus the device entry point.  The CRS of every subframe
+// (refsignal_dl.c:65-119, 36.211 6.10.1.1) is generated once per cell on the host and kept in
+// HBM; estimation itself runs in chest_kernel.hip.  No CPU fallback.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "../../include/srsran_ue_dl.h"
+#include "chest_kernel.h"
+
+using namespace srsran_amd;
+
+namespace {
+
+bool g_standard_rates = true;
+
+// LTE Gold sequence c(n), n = 0..len-1 (36.211 7.2, Nc = 1600)
+void gold(uint32_t c_init, uint8_t* c, uint32_t len)
+{
+  uint32_t x1 = 1, x2 = c_init & 0x7FFFFFFFu;
+  auto     s1 = [](uint32_t s) { return (s >> 1) ^ (((s ^ (s >> 3)) & 1u) << 30); };
+  auto     s2 = [](uint32_t s) { return (s >> 1) ^ (((s ^ (s >> 1) ^ (s >> 2) ^ (s >> 3)) & 1u) << 30); };
+  for (int n = 0; n < 1600; n++) {
+    x1 = s1(x1);
+    x2 = s2(x2);
+  }
+  for (uint32_t n = 0; n < len; n++) {
+    c[n] = (uint8_t)((x1 ^ x2) & 1u);
+    x1   = s1(x1);
+    x2   = s2(x2);
+  }
+}
+
+struct ChestGpu {
+  hipStream_t stream  = nullptr;
+  float2*     pilots  = nullptr;  // [sf][pp][4 * CHEST_MAX_NREF]
+  float2*     grid    = nullptr;  // host-synchronous path scratch
+  float2*     ce      = nullptr;
+  float*      stats   = nullptr;  // [rx][port][8]
+  uint32_t    max_prb = 0;
+  uint32_t    nrx     = 0;
+  float       filter[8];
+  uint32_t    filter_len = 0;
+};
+
+constexpr size_t kPilotsPerSf = 2 * 4 * CHEST_MAX_NREF;  // float2 per subframe (both port pairs)
+
+uint32_t gauss(float* f, uint32_t order, float std_dev)  // chest_common.c:70-95
+{
+  const uint32_t len = order + 1;
+  const int      c   = (int)(len - 1) / 2;
+  for (uint32_t i = 0; i < len; i++) {
+    f[i] = expf(-powf((float)((int)i - c), 2) / (2.0f * powf(std_dev, 2)));
+  }
+  float s = 0;
+  for (uint32_t i = 0; i < len; i++) {
+    s += f[i];
+  }
+  if (!std::isnormal(s)) {
+    return 0;
+  }
+  for (uint32_t i = 0; i < len; i++) {
+    f[i] *= 1.0f / s;
+  }
+  return len;
+}
+
+}  // namespace
+
+extern "C" {
+
+int srsran_symbol_sz_power2(uint32_t nof_prb)
+{
+  if (nof_prb <= 6) {
+    return 128;
+  } else if (nof_prb <= 15) {
+    return 256;
+  } else if (nof_prb <= 25) {
+    return 512;
+  } else if (nof_prb <= 52) {
+    return 1024;
+  } else if (nof_prb <= 79) {
+    return 1536;
+  } else if (nof_prb <= 110) {
+    return 2048;
+  }
+  return -1;
+}
+
+int srsran_symbol_sz(uint32_t nof_prb)
+{
+  if (nof_prb == 0 || nof_prb > 110) {
+    return SRSRAN_ERROR;
+  }
+  if (g_standard_rates) {
+    return srsran_symbol_sz_power2(nof_prb);
+  }
+  return nof_prb <= 6 ? 128 : nof_prb <= 15 ? 256 : nof_prb <= 25 ? 384 : nof_prb <= 52 ? 768 : nof_prb <= 79 ? 1024 : 1536;
+}
+
+void srsran_use_standard_symbol_size(bool enabled) { g_standard_rates = enabled; }
+
+int srsran_chest_dl_init(srsran_chest_dl_t* q, uint32_t max_prb, uint32_t nof_rx_antennas)
+{
+  if (!q || max_prb == 0 || max_prb > 110 || nof_rx_antennas == 0 || nof_rx_antennas > SRSRAN_MAX_PORTS) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  memset(q, 0, sizeof(*q));
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
+    fprintf(stderr, "[srsran_chest_dl] no HIP device available\n");
+    return SRSRAN_ERROR;
+  }
+  ChestGpu* g     = new ChestGpu();
+  g->max_prb      = max_prb;
+  g->nrx          = nof_rx_antennas;
+  const size_t sf = 14 * 12 * (size_t)max_prb;
+  if (hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipMalloc((void**)&g->pilots, 10 * kPilotsPerSf * sizeof(float2)) != hipSuccess ||
+      hipMalloc((void**)&g->grid, nof_rx_antennas * sf * sizeof(float2)) != hipSuccess ||
+      hipMalloc((void**)&g->ce, SRSRAN_MAX_PORTS * nof_rx_antennas * sf * sizeof(float2)) != hipSuccess ||
+      hipMalloc((void**)&g->stats, SRSRAN_MAX_PORTS * SRSRAN_MAX_PORTS * 8 * sizeof(float)) != hipSuccess) {
+    q->gpu = g;
+    srsran_chest_dl_free(q);
+    return SRSRAN_ERROR;
+  }
+  q->gpu             = g;
+  q->nof_rx_antennas = nof_rx_antennas;
+  return SRSRAN_SUCCESS;
+}
+
+void srsran_chest_dl_free(srsran_chest_dl_t* q)
+{
+  if (!q) {
+    return;
+  }
+  ChestGpu* g = (ChestGpu*)q->gpu;
+  if (g) {
+    if (g->stream) {
+      hipStreamSynchronize(g->stream);
+      hipStreamDestroy(g->stream);
+    }
+    hipFree(g->pilots);
+    hipFree(g->grid);
+    hipFree(g->ce);
+    hipFree(g->stats);
+    delete g;
+  }
+  memset(q, 0, sizeof(*q));
+}
+
+int srsran_chest_dl_set_cell(srsran_chest_dl_t* q, srsran_cell_t cell)
+{
+  if (!q || !q->gpu || cell.nof_prb == 0 || cell.nof_prb > ((ChestGpu*)q->gpu)->max_prb || cell.id >= 504 ||
+      (cell.nof_ports != 1 && cell.nof_ports != 2 && cell.nof_ports != 4)) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  if (cell.cp != SRSRAN_CP_NORM) {
+    fprintf(stderr, "[srsran_chest_dl] extended CP not provided\n");
+    return SRSRAN_ERROR;
+  }
+  ChestGpu* g = (ChestGpu*)q->gpu;
+  q->cell     = cell;
+  // refsignal_dl.c:65-119: per slot ns, CRS symbol l' of port pair pp, c_init as 36.211 6.10.1.1
+  std::vector<float2> h(10 * kPilotsPerSf, make_float2(0.f, 0.f));
+  std::vector<uint8_t> c(4 * 110);
+  const float          a = (float)0.70710678118654752440;
+  for (uint32_t ns = 0; ns < 20; ns++) {
+    for (uint32_t pp = 0; pp < 2; pp++) {
+      const uint32_t nsym_slot = pp == 0 ? 2 : 1;
+      for (uint32_t l = 0; l < nsym_slot; l++) {
+        const uint32_t lp     = pp == 0 ? (l ? 4 : 0) : 1;
+        const uint32_t c_init = 1024 * (7 * (ns + 1) + lp + 1) * (2 * cell.id + 1) + 2 * cell.id + 1;
+        gold(c_init, c.data(), 4 * 110);
+        float2* dst = &h[(ns / 2) * kPilotsPerSf + pp * 4 * CHEST_MAX_NREF +
+                         2 * cell.nof_prb * ((ns % 2) * nsym_slot + l)];
+        for (uint32_t i = 0; i < 2 * cell.nof_prb; i++) {
+          const uint32_t mp = i + 110 - cell.nof_prb;
+          dst[i]            = make_float2((1 - 2 * (float)c[2 * mp]) * a, (1 - 2 * (float)c[2 * mp + 1]) * a);
+        }
+      }
+    }
+  }
+  if (hipMemcpy(g->pilots, h.data(), h.size() * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess) {
+    return SRSRAN_ERROR;
+  }
+  g->filter_len = gauss(g->filter, 4, 1.0f);
+  return SRSRAN_SUCCESS;
+}
+
+int srsran_chest_dl_res_init(srsran_chest_dl_res_t* q, uint32_t max_prb)
+{
+  if (!q) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  memset(q, 0, sizeof(*q));
+  q->nof_re = 14 * 12 * max_prb;
+  for (int p = 0; p < SRSRAN_MAX_PORTS; p++) {
+    for (int r = 0; r < SRSRAN_MAX_PORTS; r++) {
+      q->ce[p][r] = (cf_t*)calloc(q->nof_re, sizeof(cf_t));
+      if (!q->ce[p][r]) {
+        return SRSRAN_ERROR;
+      }
+    }
+  }
+  return SRSRAN_SUCCESS;
+}
+
+void srsran_chest_dl_res_free(srsran_chest_dl_res_t* q)
+{
+  if (!q) {
+    return;
+  }
+  for (int p = 0; p < SRSRAN_MAX_PORTS; p++) {
+    for (int r = 0; r < SRSRAN_MAX_PORTS; r++) {
+      free(q->ce[p][r]);
+    }
+  }
+  memset(q, 0, sizeof(*q));
+}
+
+static int chest_enqueue(srsran_chest_dl_t* q, uint32_t tti, const float2* d_grid, float2* d_ce, int full,
+                         hipStream_t s, const srsran_chest_dl_cfg_t* cfg = nullptr)
+{
+  ChestGpu* g = (ChestGpu*)q->gpu;
+  ChestArgs a{};
+  a.grid       = d_grid;
+  a.pilots     = g->pilots + (tti % 10) * kPilotsPerSf;
+  a.ce         = d_ce;
+  a.stats      = g->stats;
+  a.nof_prb    = q->cell.nof_prb;
+  a.cell_id    = q->cell.id;
+  a.nports     = q->cell.nof_ports;
+  a.nrx        = q->nof_rx_antennas;
+  a.ce_stride  = (full ? 14 : 1) * 12 * q->cell.nof_prb;
+  a.full_grid  = full ? 1 : 0;
+  a.filter_len = g->filter_len;
+  memcpy(a.filter, g->filter, sizeof(a.filter));
+  if (cfg) {
+    if (cfg->filter_coef[0] <= 0) {
+      a.filter_auto = 1;
+    } else {
+      a.filter_len = gauss(a.filter, (uint32_t)cfg->filter_coef[0], cfg->filter_coef[1]);
+    }
+  }
+  return chest_launch(a, s) == hipSuccess ? SRSRAN_SUCCESS : SRSRAN_ERROR;
+}
+
+// fill_res (chest_dl.c:962-986) from the per (rx, port) statistics
+static void fill_res(srsran_chest_dl_t* q, const float* st, srsran_chest_dl_res_t* res, bool update_cfo)
+{
+  const uint32_t np = q->cell.nof_ports, nrx = q->nof_rx_antennas;
+  float          n  = 0;
+  for (uint32_t rx = 0; rx < nrx; rx++) {
+    float s = 0;
+    for (uint32_t p = 0; p < np; p++) {
+      const float* v          = st + (rx * np + p) * 8;
+      q->noise_estimate[rx][p] = v[0];
+      q->rsrp[rx][p]           = v[1];
+      q->rssi[rx][p]           = v[2];
+      s += v[0];
+    }
+    n += s / (float)np;
+  }
+  // chest_estimate_cfo: the last (rx, port) pair with 4 CRS symbols wins (chest_dl.c:655)
+  for (int idx = (int)(nrx * np) - 1; update_cfo && idx >= 0; idx--) {
+    const uint32_t p = (uint32_t)idx % np;
+    if (p < 2) {
+      const float* v  = st + idx * 8;
+      const float  sz = (float)srsran_symbol_sz(q->cell.nof_prb);
+      const float  ng = (float)(int)ceilf(144.0f * sz / 2048.0f);
+      q->cfo          = -atan2f(v[4], v[3]) * sz / (7.0f * (sz + ng)) / 2 / (float)M_PI;
+      break;
+    }
+  }
+  if (!res) {
+    return;
+  }
+  res->noise_estimate     = n / (float)nrx;
+  res->noise_estimate_dbm = 10.0f * log10f(res->noise_estimate) + 30.0f;
+  res->cfo                = q->cfo;
+  float rsrp_max          = -1e9f;
+  for (uint32_t p = 0; p < np; p++) {
+    float s = 0;
+    for (uint32_t rx = 0; rx < nrx; rx++) {
+      s += q->rsrp[rx][p];
+    }
+    s /= (float)nrx;
+    res->rsrp_port_dbm[p] = 10.0f * log10f(s) + 30.0f;
+    rsrp_max              = s > rsrp_max ? s : rsrp_max;
+    for (uint32_t rx = 0; rx < nrx; rx++) {
+      res->snr_ant_port_db[rx][p]   = 10.0f * log10f(q->rsrp[rx][p] / q->noise_estimate[rx][p]);
+      res->rsrp_ant_port_dbm[rx][p] = 10.0f * log10f(q->rsrp[rx][p]) + 30.0f;
+      res->rsrq_ant_port_db[rx][p]  = 10.0f * log10f(q->cell.nof_prb * q->rsrp[rx][p] / q->rssi[rx][p]);
+    }
+  }
+  res->rsrp     = rsrp_max;
+  res->rsrp_dbm = 10.0f * log10f(rsrp_max) + 30.0f;
+  float rsrq = 0, rssi = 0;
+  for (uint32_t rx = 0; rx < nrx; rx++) {
+    rsrq += q->cell.nof_prb * q->rsrp[rx][0] / q->rssi[rx][0];
+    rssi += 4 * q->rssi[rx][0] / q->cell.nof_prb / SRSRAN_NRE;
+  }
+  res->rsrq     = rsrq / (float)nrx;
+  res->rsrq_db  = 10.0f * log10f(res->rsrq);
+  res->rssi_dbm = 10.0f * log10f(rssi / (float)nrx) + 30.0f;
+  res->snr_db   = 10.0f * log10f(res->rsrp / res->noise_estimate);
+  res->sync_error = 0.0f;
+}
+
+int srsran_chest_dl_estimate_cfg(srsran_chest_dl_t*     q,
+                                 srsran_dl_sf_cfg_t*    sf,
+                                 srsran_chest_dl_cfg_t* cfg,
+                                 cf_t*                  input[SRSRAN_MAX_PORTS],
+                                 srsran_chest_dl_res_t* res)
+{
+  if (!q || !q->gpu || !sf || !cfg || !input || !res || q->cell.nof_prb == 0) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  if (sf->sf_type != SRSRAN_SF_NORM || cfg->estimator_alg != SRSRAN_ESTIMATOR_ALG_AVERAGE ||
+      cfg->filter_type != SRSRAN_CHEST_FILTER_GAUSS || cfg->noise_alg != SRSRAN_NOISE_ALG_REFS ||
+      cfg->sync_error_enable || cfg->rsrp_neighbour || cfg->filter_coef[0] > 7) {
+    fprintf(stderr, "[srsran_chest_dl] only srsUE's default estimator configuration is provided\n");
+    return SRSRAN_ERROR;
+  }
+  ChestGpu*      g   = (ChestGpu*)q->gpu;
+  const uint32_t nsf = 14 * 12 * q->cell.nof_prb, nrx = q->nof_rx_antennas, np = q->cell.nof_ports;
+  for (uint32_t rx = 0; rx < nrx; rx++) {
+    hipMemcpyAsync(g->grid + rx * nsf, input[rx], nsf * sizeof(cf_t), hipMemcpyHostToDevice, g->stream);
+  }
+  if (chest_enqueue(q, sf->tti, g->grid, g->ce, 1, g->stream, cfg)) {
+    return SRSRAN_ERROR;
+  }
+  for (uint32_t p = 0; p < np; p++) {
+    for (uint32_t rx = 0; rx < nrx; rx++) {
+      hipMemcpyAsync(res->ce[p][rx], g->ce + (p * nrx + rx) * nsf, nsf * sizeof(cf_t), hipMemcpyDeviceToHost,
+                     g->stream);
+    }
+  }
+  float st[SRSRAN_MAX_PORTS * SRSRAN_MAX_PORTS * 8];
+  hipMemcpyAsync(st, g->stats, nrx * np * 8 * sizeof(float), hipMemcpyDeviceToHost, g->stream);
+  if (hipStreamSynchronize(g->stream) != hipSuccess) {
+    return SRSRAN_ERROR;
+  }
+  fill_res(q, st, res, cfg->cfo_estimate_enable && ((1u << (sf->tti % 10)) & cfg->cfo_estimate_sf_mask));
+  return SRSRAN_SUCCESS;
+}
+
+int srsran_chest_dl_estimate(srsran_chest_dl_t* q, srsran_dl_sf_cfg_t* sf, cf_t* input[SRSRAN_MAX_PORTS],
+                             srsran_chest_dl_res_t* res)
+{
+  srsran_chest_dl_cfg_t cfg;
+  memset(&cfg, 0, sizeof(cfg));  // AVERAGE, REFS, GAUSS with automatic coefficients (chest_dl.c:999-1007)
+  return srsran_chest_dl_estimate_cfg(q, sf, &cfg, input, res);
+}
+
+}  // extern "C"
+
+// Device-side fill of the four d_res values (noise_estimate, rsrp, rssi, cfo).
+namespace srsran_amd {
+__global__ void chest_finalize_kernel(const float* st, uint32_t np, uint32_t nrx, uint32_t nof_prb, float sz,
+                                      float* out)
+{
+  float n = 0, best = -1e9f, rssi = 0, cfo = 0;
+  for (uint32_t rx = 0; rx < nrx; rx++) {
+    float s = 0;
+    for (uint32_t p = 0; p < np; p++) {
+      s += st[(rx * np + p) * 8];
+    }
+    n += s / (float)np;
+    rssi += 4 * st[(rx * np) * 8 + 2] / (float)nof_prb / 12.0f;
+  }
+  for (uint32_t p = 0; p < np; p++) {
+    float s = 0;
+    for (uint32_t rx = 0; rx < nrx; rx++) {
+      s += st[(rx * np + p) * 8 + 1];
+    }
+    s /= (float)nrx;
+    best = s > best ? s : best;
+  }
+  for (int idx = (int)(nrx * np) - 1; idx >= 0; idx--) {
+    if ((uint32_t)idx % np < 2) {
+      const float ng = (float)(int)ceilf(144.0f * sz / 2048.0f);
+      cfo            = -atan2f(st[idx * 8 + 4], st[idx * 8 + 3]) * sz / (7.0f * (sz + ng)) / 2 / 3.14159265358979f;
+      break;
+    }
+  }
+  out[0] = n / (float)nrx;
+  out[1] = best;
+  out[2] = rssi / (float)nrx;
+  out[3] = cfo;
+}
+}  // namespace srsran_amd
+
+extern "C" int srsran_chest_dl_gpu_estimate(srsran_chest_dl_t* q,
+                                            uint32_t           tti,
+                                            const cf_t*        d_grid,
+                                            cf_t*              d_ce,
+                                            int                full_grid,
+                                            float*             d_res,
+                                            void*              stream)
+{
+  if (!q || !q->gpu || !d_grid || !d_ce || q->cell.nof_prb == 0) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  if (chest_enqueue(q, tti, (const float2*)d_grid, (float2*)d_ce, full_grid, s)) {
+    return SRSRAN_ERROR;
+  }
+  if (d_res) {
+    ChestGpu* g = (ChestGpu*)q->gpu;
+    hipLaunchKernelGGL(chest_finalize_kernel, dim3(1), dim3(1), 0, s, g->stats, q->cell.nof_ports,
+                       q->nof_rx_antennas, q->cell.nof_prb, (float)srsran_symbol_sz(q->cell.nof_prb), d_res);
+  }
+  return hipGetLastError() == hipSuccess ? SRSRAN_SUCCESS : SRSRAN_ERROR;
+}

@@ -1,0 +1,257 @@
+// srsran_4g_amd/csrc/chest_kernel.hip -- DL CRS channel estimation for CDNA4.
+//
+// srsUE's default estimator (AVERAGE, Gauss smoothing order 4 / sigma 1, REFS noise):
+//   LS at the CRS            estimate_port         chest_dl.c:806-834
+//   noise (REFS)             estimate_noise_pilots chest_dl.c:325-400
+//   time average + smoothing average_pilots        chest_dl.c:557-600, convolution.c:182-218
+//   linear interpolation     srsran_interp_linear_offset interp.c:258-285 (then every symbol)
+//   CFO from pilot phases    chest_estimate_cfo    chest_dl.c:621-641
+// One workgroup per (port, rx antenna): the 4 x 200 pilots, the noise residuals and the
+// 400-point smoothed comb live in LDS; the estimate row (1200 subcarriers at 100 PRB) is
+// written once, or 14 times when the caller wants the full srsran_chest_dl_res_t grid.
+// Float operations follow the reference's order (no contraction) so the result matches
+// oracle/phy_oracle.c up to the order of the power/phase reductions.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "chest_kernel.h"
+
+#pragma clang fp contract(off)
+
+namespace srsran_amd {
+
+static constexpr int CH_THREADS = 256;
+
+struct cx {
+  float r, i;
+};
+__device__ __forceinline__ cx ld2(const float2* p, uint32_t k)
+{
+  const float2 v = p[k];
+  return {v.x, v.y};
+}
+__device__ __forceinline__ cx add(cx a, cx b) { return {a.r + b.r, a.i + b.i}; }
+__device__ __forceinline__ cx sub(cx a, cx b) { return {a.r - b.r, a.i - b.i}; }
+__device__ __forceinline__ cx mul(cx a, cx b) { return {a.r * b.r - a.i * b.i, a.r * b.i + a.i * b.r}; }
+__device__ __forceinline__ cx conj(cx a) { return {a.r, -a.i}; }
+__device__ __forceinline__ cx scl(cx a, float s) { return {a.r * s, a.i * s}; }
+__device__ __forceinline__ cx divs(cx a, float s) { return {a.r / s, a.i / s}; }
+
+__device__ __forceinline__ uint32_t crs_v(uint32_t port, uint32_t l)
+{
+  return port == 0 ? ((l & 1) ? 3u : 0u) : port == 1 ? ((l & 1) ? 0u : 3u) : port == 2 ? (l == 0 ? 0u : 3u) : (l == 0 ? 3u : 0u);
+}
+__device__ __forceinline__ uint32_t crs_nsymbol(uint32_t l, uint32_t port)
+{
+  return port < 2 ? ((l & 1) ? (l / 2 + 1) * 7 - 3 : (l / 2) * 7) : 1 + l * 7;
+}
+
+// block-wide sum of one float (all threads get the result)
+__device__ float block_sum(float v, float* red)
+{
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    v += __shfl_xor(v, off, 64);
+  }
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) {
+    red[threadIdx.x >> 6] = v;
+  }
+  __syncthreads();
+  float s = 0.f;
+  for (int w = 0; w < CH_THREADS / 64; w++) {
+    s += red[w];
+  }
+  return s;
+}
+
+__global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
+{
+  __shared__ cx    pe[4 * CHEST_MAX_NREF];
+  __shared__ cx    comb[2 * CHEST_MAX_NREF];
+  __shared__ cx    avg[2 * CHEST_MAX_NREF];
+  __shared__ float red[CH_THREADS / 64];
+
+  const uint32_t port = blockIdx.x / a.nrx, rx = blockIdx.x % a.nrx;
+  const uint32_t tid  = threadIdx.x;
+  const uint32_t nsym = port < 2 ? 4 : 2, nref = 2 * a.nof_prb, np = nsym * nref, nre = 12 * a.nof_prb;
+  const float2*  in   = a.grid + (size_t)rx * 14 * nre;
+  const float2*  pil  = a.pilots + (size_t)(port / 2) * 4 * CHEST_MAX_NREF;
+  const uint32_t fidx0 = (crs_v(port, 0) + a.cell_id % 6) % 6;
+
+  // ---- LS estimates at the CRS and RSRP / RSSI ----
+  float rsrp = 0.f;
+  for (uint32_t k = tid; k < np; k += CH_THREADS) {
+    const uint32_t l = k / nref, i = k % nref;
+    const uint32_t f = (crs_v(port, l) + a.cell_id % 6) % 6 + 6 * i;
+    const cx       r = ld2(in, crs_nsymbol(l, port) * nre + f);
+    pe[k]            = mul(r, conj(ld2(pil, k)));
+    rsrp += r.r * r.r + r.i * r.i;
+  }
+  float rssi = 0.f;
+  for (uint32_t k = tid; k < nsym * nre; k += CH_THREADS) {
+    const cx r = ld2(in, crs_nsymbol(k / nre, port) * nre + k % nre);
+    rssi += r.r * r.r + r.i * r.i;
+  }
+  rsrp = block_sum(rsrp, red) / (float)np;
+  rssi = block_sum(rssi, red) / (float)nsym;  // pe[] complete after block_sum's barriers
+
+  // ---- CFO phase sum (port-0 geometry, chest_dl.c:630-636) ----
+  float cre = 0.f, cim = 0.f;
+  if (nsym == 4) {
+    for (uint32_t k = tid; k < np / 2; k += CH_THREADS) {
+      const uint32_t ii = k / (np / 4), kk = k % (np / 4);
+      const cx       t  = mul(pe[ii * np / 4 + kk], conj(pe[(ii + 2) * np / 4 + kk]));
+      cre += t.r;
+      cim += t.i;
+    }
+    cre = block_sum(cre, red);
+    cim = block_sum(cim, red);
+  }
+
+  // ---- noise from the pilot residuals (REFS) ----
+  float noise = 0.f;
+  if (nsym >= 3) {
+    for (uint32_t i = 1; i < nsym - 1; i++) {
+      const uint32_t off = ((fidx0 < 3) ^ (i & 1)) ? 0 : 1;
+      const cx*      cur = pe + i * nref;
+      float          p   = 0.f;
+      for (uint32_t k = tid; k < nref; k += CH_THREADS) {
+        cx t = cur[k];
+#pragma unroll
+        for (int nb = 0; nb < 2; nb++) {
+          const cx* o = pe + (nb == 0 ? i - 1 : i + 1) * nref;
+          if (k >= off) {
+            t = add(o[k - off], t);
+          }
+          if (k < nref + off - 1) {
+            t = add(o[1 - off + k], t);
+          }
+          if (off && k == 0) {
+            t = add(t, sub(scl(o[0], 2.0f), o[1]));
+          }
+          if (!off && k == nref - 1) {
+            t = add(t, sub(scl(o[nref - 2], 2.0f), o[nref - 1]));
+          }
+        }
+        t = sub(cur[k], scl(t, 1.0f / 5.0f));
+        p += t.r * t.r + t.i * t.i;
+      }
+      noise += block_sum(p, red) / (float)nref;
+    }
+    noise /= (float)(nsym - 2);
+  } else {
+    float p = 0.f;
+    for (uint32_t k = tid; k + 2 < nref; k += CH_THREADS) {
+      cx t = add(add(pe[k], pe[k + 1]), pe[k + 2]);
+      t    = sub(pe[k + 1], scl(t, 1.0f / 3.0f));
+      p += t.r * t.r + t.i * t.i;
+    }
+    noise = block_sum(p, red) / (float)(nref - 2);
+  }
+
+  // ---- time average into a 3-subcarrier comb, then smoothing (average_pilots) ----
+  uint32_t nr = nref;
+  if (nsym > 1) {
+    for (uint32_t k = tid; k < nref; k += CH_THREADS) {
+      cx e0 = pe[(fidx0 < 3 ? 0 : 1) * nref + k], e1 = pe[(fidx0 < 3 ? 1 : 0) * nref + k];
+      for (uint32_t l = 2; l + 1 < nsym; l += 2) {
+        e0 = add(e0, pe[(fidx0 < 3 ? l : l + 1) * nref + k]);
+        e1 = add(e1, pe[(fidx0 < 3 ? l + 1 : l) * nref + k]);
+      }
+      comb[2 * k]     = scl(e0, 2.0f / (float)nsym);
+      comb[2 * k + 1] = scl(e1, 2.0f / (float)nsym);
+    }
+    nr = 2 * nref;
+  } else {
+    for (uint32_t k = tid; k < nref; k += CH_THREADS) {
+      comb[k] = pe[k];
+    }
+  }
+  __syncthreads();
+  float    filt[8];
+  uint32_t M = a.filter_len;
+  for (int k = 0; k < 8; k++) {
+    filt[k] = a.filter[k];
+  }
+  if (a.filter_auto) {  // srsran_chest_set_smooth_filter_gauss(filter, 4, noise * 200) (chest_common.c:70-95)
+    const float sd = noise * 200.0f;
+    float       sum = 0.f;
+    for (int k = 0; k < 5; k++) {
+      filt[k] = expf(-powf((float)(k - 2), 2) / (2.0f * powf(sd, 2)));
+    }
+    for (int k = 0; k < 5; k++) {
+      sum += filt[k];
+    }
+    if (isnormal(sum)) {
+      for (int k = 0; k < 5; k++) {
+        filt[k] *= 1.0f / sum;
+      }
+      M = 5;
+    } else {
+      M = 0;  // srsran_conv_same_cf with an empty filter yields zeros
+    }
+  }
+  for (uint32_t i = tid; i < nr; i += CH_THREADS) {
+    cx acc = {0.f, 0.f};
+    for (uint32_t k = 0; k < M; k++) {
+      const int j = (int)i - (int)(M / 2) + (int)k;  // index into the extended sequence
+      cx        x;
+      if (j < 0) {  // first[]: (2 + M/2 - m) * in[1] - (1 + M/2 - m) * in[0], m = j + M/2
+        const uint32_t m = (uint32_t)(j + (int)(M / 2));
+        x = sub(scl(comb[1], (float)(2 + M / 2 - m)), scl(comb[0], (float)(1 + M / 2 - m)));
+      } else if (j >= (int)nr) {  // last[]: m = j - (nr - M + 1) counts into last[], i >= M - 1
+        const uint32_t m = (uint32_t)(j - (int)(nr - M + 1));
+        x = sub(scl(comb[nr - 1], (float)(2 + m - M / 2)), scl(comb[nr - 2], (float)(1 + m - M / 2)));
+      } else {
+        x = comb[j];
+      }
+      acc = add(acc, scl(x, filt[k]));
+    }
+    avg[i] = acc;
+  }
+  __syncthreads();
+
+  // ---- linear interpolation to every subcarrier (interp_linear_offset) ----
+  const uint32_t step = nsym > 1 ? 3 : 6;
+  const uint32_t off  = nsym > 1 ? a.cell_id % 3 : fidx0;
+  const float    rM   = (float)1 / step;
+  float2*        ce   = a.ce + (size_t)(port * a.nrx + rx) * a.ce_stride;
+  for (uint32_t j = tid; j < nre; j += CH_THREADS) {
+    cx v;
+    if (j < off) {
+      const uint32_t jj = off - 1 - j;
+      v                 = sub(avg[0], divs(scl(sub(avg[1], avg[0]), (float)(jj + 1)), (float)step));
+    } else if (j < off + step * (nr - 1)) {
+      const uint32_t i = (j - off) / step, r = (j - off) % step;
+      v                = add(avg[i], scl(scl(sub(avg[i + 1], avg[i]), rM), (float)r));
+    } else {
+      const uint32_t r = j - off - step * (nr - 1);
+      v                = add(avg[nr - 1], divs(scl(sub(avg[nr - 1], avg[nr - 2]), (float)r), (float)step));
+    }
+    const float2 o = make_float2(v.r, v.i);
+    if (a.full_grid) {
+      for (uint32_t l = 0; l < 14; l++) {
+        ce[l * nre + j] = o;
+      }
+    } else {
+      ce[j] = o;
+    }
+  }
+  if (tid == 0) {
+    float* s = a.stats + (size_t)(rx * a.nports + port) * 8;
+    s[0]     = noise;
+    s[1]     = rsrp;
+    s[2]     = rssi;
+    s[3]     = cre;
+    s[4]     = cim;
+  }
+}
+
+hipError_t chest_launch(const ChestArgs& a, hipStream_t stream)
+{
+  hipLaunchKernelGGL(chest_kernel, dim3(a.nports * a.nrx), dim3(CH_THREADS), 0, stream, a);
+  return hipGetLastError();
+}
+
+}  // namespace srsran_amd

@@ -1,0 +1,141 @@
+"""Python mirror of the DL front-end C API (include/srsran_ue_dl.h): cell / subframe types,
+CRS channel estimation (and, as they land, OFDM, PDSCH, UE DL).  No CPU fallback."""
+import ctypes
+
+import numpy as np
+
+from .tdec import load_library
+
+u32 = ctypes.c_uint32
+MAX_PORTS = 4
+
+
+class srsran_cell_t(ctypes.Structure):
+    _fields_ = [("nof_prb", u32), ("nof_ports", u32), ("id", u32), ("cp", ctypes.c_int), ("phich_length", ctypes.c_int),
+                ("phich_resources", ctypes.c_int), ("frame_type", ctypes.c_int)]
+
+
+class srsran_tdd_config_t(ctypes.Structure):
+    _fields_ = [("sf_config", u32), ("ss_config", u32), ("configured", ctypes.c_bool)]
+
+
+class srsran_dl_sf_cfg_t(ctypes.Structure):
+    _fields_ = [("tdd_config", srsran_tdd_config_t), ("tti", u32), ("cfi", u32), ("sf_type", ctypes.c_int),
+                ("non_mbsfn_region", u32)]
+
+
+class srsran_chest_dl_cfg_t(ctypes.Structure):
+    _fields_ = [("estimator_alg", ctypes.c_int), ("noise_alg", ctypes.c_int), ("filter_type", ctypes.c_int),
+                ("filter_coef", ctypes.c_float * 2), ("mbsfn_area_id", ctypes.c_uint16), ("rsrp_neighbour", ctypes.c_bool),
+                ("cfo_estimate_enable", ctypes.c_bool), ("cfo_estimate_sf_mask", u32), ("sync_error_enable", ctypes.c_bool)]
+
+
+F44 = (ctypes.c_float * MAX_PORTS) * MAX_PORTS
+
+
+class srsran_chest_dl_res_t(ctypes.Structure):
+    _fields_ = [("ce", (ctypes.c_void_p * MAX_PORTS) * MAX_PORTS), ("nof_re", u32), ("noise_estimate", ctypes.c_float),
+                ("noise_estimate_dbm", ctypes.c_float), ("snr_db", ctypes.c_float), ("snr_ant_port_db", F44),
+                ("rsrp", ctypes.c_float), ("rsrp_dbm", ctypes.c_float), ("rsrp_neigh", ctypes.c_float),
+                ("rsrp_port_dbm", ctypes.c_float * MAX_PORTS), ("rsrp_ant_port_dbm", F44), ("rsrq", ctypes.c_float),
+                ("rsrq_db", ctypes.c_float), ("rsrq_ant_port_db", F44), ("rssi_dbm", ctypes.c_float),
+                ("cfo", ctypes.c_float), ("sync_error", ctypes.c_float)]
+
+
+class srsran_chest_dl_t(ctypes.Structure):
+    _fields_ = [("cell", srsran_cell_t), ("nof_rx_antennas", u32), ("rssi", F44), ("rsrp", F44),
+                ("noise_estimate", F44), ("cfo", ctypes.c_float), ("gpu", ctypes.c_void_p)]
+
+
+_bound = False
+
+
+def lib():
+    global _bound
+    L = load_library()
+    if not _bound:
+        CH = ctypes.POINTER(srsran_chest_dl_t)
+        RES = ctypes.POINTER(srsran_chest_dl_res_t)
+        P = ctypes.c_void_p
+        sig = {
+            "srsran_symbol_sz": ([u32], ctypes.c_int),
+            "srsran_symbol_sz_power2": ([u32], ctypes.c_int),
+            "srsran_chest_dl_init": ([CH, u32, u32], ctypes.c_int),
+            "srsran_chest_dl_free": ([CH], None),
+            "srsran_chest_dl_set_cell": ([CH, srsran_cell_t], ctypes.c_int),
+            "srsran_chest_dl_res_init": ([RES, u32], ctypes.c_int),
+            "srsran_chest_dl_res_free": ([RES], None),
+            "srsran_chest_dl_estimate": ([CH, ctypes.POINTER(srsran_dl_sf_cfg_t), P, RES], ctypes.c_int),
+            "srsran_chest_dl_estimate_cfg": ([CH, ctypes.POINTER(srsran_dl_sf_cfg_t),
+                                              ctypes.POINTER(srsran_chest_dl_cfg_t), P, RES], ctypes.c_int),
+            "srsran_chest_dl_gpu_estimate": ([CH, u32, P, P, ctypes.c_int, P, P], ctypes.c_int),
+        }
+        for name, (args, res) in sig.items():
+            f = getattr(L, name)
+            f.argtypes = args
+            f.restype = res
+        _bound = True
+    return L
+
+
+def cell(nof_prb=100, nof_ports=2, cell_id=1):
+    c = srsran_cell_t()
+    c.nof_prb, c.nof_ports, c.id = nof_prb, nof_ports, cell_id
+    return c
+
+
+def srsue_chest_cfg():
+    """srsUE defaults (srsue/src/phy/phy_common.cc:83-107 + main.cc option defaults)."""
+    c = srsran_chest_dl_cfg_t()
+    c.estimator_alg = 0  # AVERAGE
+    c.noise_alg = 0      # REFS
+    c.filter_type = 0    # GAUSS
+    c.filter_coef[0], c.filter_coef[1] = 4, 1.0
+    c.cfo_estimate_enable = True
+    c.cfo_estimate_sf_mask = 1023
+    return c
+
+
+class ChestDl:
+    def __init__(self, cell_, nof_rx):
+        self.q = srsran_chest_dl_t()
+        if lib().srsran_chest_dl_init(ctypes.byref(self.q), cell_.nof_prb, nof_rx):
+            raise RuntimeError("srsran_chest_dl_init failed (no HIP device?)")
+        if lib().srsran_chest_dl_set_cell(ctypes.byref(self.q), cell_):
+            raise RuntimeError("srsran_chest_dl_set_cell failed")
+        self.res = srsran_chest_dl_res_t()
+        lib().srsran_chest_dl_res_init(ctypes.byref(self.res), cell_.nof_prb)
+        self.cell = cell_
+        self.nrx = nof_rx
+
+    def estimate(self, grids, tti, cfg=None):
+        """grids: (nrx, 14*12*nof_prb) complex64 -> (ce[port][rx] arrays, res)."""
+        grids = [np.ascontiguousarray(g, np.complex64) for g in grids]
+        ptrs = (ctypes.c_void_p * MAX_PORTS)(*[g.ctypes.data for g in grids] + [None] * (MAX_PORTS - len(grids)))
+        sf = srsran_dl_sf_cfg_t()
+        sf.tti = tti
+        if cfg is None:
+            rc = lib().srsran_chest_dl_estimate(ctypes.byref(self.q), ctypes.byref(sf), ctypes.addressof(ptrs),
+                                                ctypes.byref(self.res))
+        else:
+            rc = lib().srsran_chest_dl_estimate_cfg(ctypes.byref(self.q), ctypes.byref(sf), ctypes.byref(cfg),
+                                                    ctypes.addressof(ptrs), ctypes.byref(self.res))
+        if rc:
+            raise RuntimeError(f"srsran_chest_dl_estimate failed ({rc})")
+        n = 14 * 12 * self.cell.nof_prb
+        ce = np.zeros((self.cell.nof_ports, self.nrx, n), np.complex64)
+        for p in range(self.cell.nof_ports):
+            for r in range(self.nrx):
+                ctypes.memmove(ce[p, r].ctypes.data, self.res.ce[p][r], n * 8)
+        return ce, self.res
+
+    def free(self):
+        if self.q.gpu:
+            lib().srsran_chest_dl_res_free(ctypes.byref(self.res))
+            lib().srsran_chest_dl_free(ctypes.byref(self.q))
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass

@@ -108,3 +108,104 @@ def test_predecode_matches_reference(scheme, nrx, nports, nlayers, cb):
             assert np.percentile(err, 99.9) < 2e-3 and err.max() < 2e-2, (n, err.max())
             cerr = np.abs(co - cr) / np.abs(co)
             assert cerr.max() < 2e-3, (n, cerr.max())
+
+
+def crs_positions(nof_prb, cell_id, port):
+    """(symbol, subcarrier) of the CRS of `port` (36.211 6.10.1.2)."""
+    pos = []
+    nsym = 4 if port < 2 else 2
+    for l in range(nsym):
+        sym = ((l // 2 + 1) * 7 - 3 if l % 2 else (l // 2) * 7) if port < 2 else 1 + l * 7
+        v = [[0, 3], [3, 0], [0, 3], [3, 0]][port][l % 2] if port < 2 else (0 if (l == 0) == (port == 2) else 3)
+        f0 = (v + cell_id % 6) % 6
+        pos.append([(sym, f0 + 6 * i) for i in range(2 * nof_prb)])
+    return pos
+
+
+def make_subframe(ora, rng, nof_prb=100, cell_id=1, nports=2, nrx=2, sf_idx=1, snr_db=30.0, flat=False):
+    """Received grids of one subframe: CRS of every port + random QPSK data through a smooth channel."""
+    nre = 12 * nof_prb
+    X = (rng.choice([-1, 1], (nports, 14, nre)) + 1j * rng.choice([-1, 1], (nports, 14, nre))) / np.sqrt(2)
+    for p in range(nports):  # CRS REs of any port are empty on the other ports
+        for q in range(nports):
+            for row in crs_positions(nof_prb, cell_id, q):
+                for s, k in row:
+                    X[p, s, k] = 0
+    for p in range(nports):
+        pil = ora.crs_pilots(cell_id, nof_prb, p // 2, sf_idx).reshape(-1, 2 * nof_prb)
+        for l, row in enumerate(crs_positions(nof_prb, cell_id, p)):
+            for i, (s, k) in enumerate(row):
+                X[p, s, k] = pil[l, i]
+    k = np.arange(nre)
+    H = np.zeros((nports, nrx, nre), np.complex64)
+    for p in range(nports):
+        for r in range(nrx):
+            if flat:
+                H[p, r] = rng.standard_normal() + 1j * rng.standard_normal()
+            else:
+                a = rng.standard_normal(3) + 1j * rng.standard_normal(3)
+                H[p, r] = a[0] + a[1] * np.exp(2j * np.pi * k * 0.8 / nre) + 0.3 * a[2] * np.exp(-2j * np.pi * k * 2.3 / nre)
+    Y = np.einsum("prk,psk->rsk", H, X)
+    sig = 10 ** (-snr_db / 20)
+    Y = Y + sig * (rng.standard_normal(Y.shape) + 1j * rng.standard_normal(Y.shape)) / np.sqrt(2)
+    return Y.reshape(nrx, 14 * nre).astype(np.complex64), H, X
+
+
+def test_crs_pilots_are_qpsk_gold():
+    ora = Oracle()
+    p = ora.crs_pilots(1, 100, 0, 1)
+    assert p.size == 800 and np.allclose(np.abs(p), 1.0, atol=1e-6)
+    c = ora.sequence_bits(1024 * (7 * 3 + 0 + 1) * 3 + 2 + 1, 440)  # slot 2, symbol 0, cell 1
+    mp = np.arange(200) + 10
+    exp = ((1 - 2 * c[2 * mp].astype(np.float32)) + 1j * (1 - 2 * c[2 * mp + 1].astype(np.float32))) / np.sqrt(2)
+    assert np.allclose(p[:200], exp, atol=1e-6)
+
+
+def test_chest_flat_noise_free():
+    """A flat channel is recovered exactly on every RE; the REFS noise estimate is ~0."""
+    ora = Oracle()
+    rng = np.random.default_rng(2)
+    Y, H, _ = make_subframe(ora, rng, flat=True, snr_db=200)
+    ce, st = ora.chest_dl(Y, 100, 1, 2, 1, 2048)
+    for p in range(2):
+        for r in range(2):
+            assert np.allclose(ce[p, r], H[p, r][0], rtol=1e-5, atol=1e-5)
+    assert st["noise"] < 1e-10
+
+
+def test_chest_noise_tracks_snr():
+    ora = Oracle()
+    rng = np.random.default_rng(3)
+    for snr in (10.0, 20.0):
+        Y, H, _ = make_subframe(ora, rng, snr_db=snr)
+        ce, st = ora.chest_dl(Y, 100, 1, 2, 1, 2048)
+        assert 0.5 < st["noise"] / 10 ** (-snr / 10) < 2.0, (snr, st)
+        err = np.abs(ce[:, :, :1200] - H) ** 2
+        assert err.mean() < 10 ** (-snr / 10)
+
+
+@needs_ref
+def test_gauss_filter_and_conv_same_match_reference():
+    import ctypes
+    ora, ref = Oracle(), Reference()
+    g = ref.lib.srsran_chest_set_smooth_filter_gauss
+    g.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_float]
+    g.restype = ctypes.c_uint32
+    for order, std in ((4, 1.0), (4, 0.37), (6, 2.0), (2, 1.0)):
+        fr = np.zeros(64, np.float32)
+        n = g(fr.ctypes.data, order, std)
+        fo = ora.gauss_filter(order, std)
+        assert n == fo.size and np.allclose(fr[:n], fo, rtol=1e-6), (order, std)
+    c = ref.lib.srsran_conv_same_cf
+    c.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32]
+    rng = np.random.default_rng(9)
+    for N in (400, 200, 24):
+        x = (rng.standard_normal(N) + 1j * rng.standard_normal(N)).astype(np.complex64)
+        f = ora.gauss_filter(4, 1.0)
+        yr = np.zeros(N, np.complex64)
+        c(x.ctypes.data, f.ctypes.data, yr.ctypes.data, N, f.size)
+        yo = np.zeros(N, np.complex64)
+        fo = ora.lib.oracle_conv_same
+        fo.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_uint32] * 2
+        fo(x.ctypes.data, f.ctypes.data, yo.ctypes.data, N, f.size)
+        assert np.allclose(yo, yr, rtol=1e-5, atol=1e-6), N  # SIMD dot products sum in a different order

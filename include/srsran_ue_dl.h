@@ -140,6 +140,64 @@ int srsran_chest_dl_gpu_estimate(srsran_chest_dl_t* q,
                                  float*             d_res,
                                  void*              stream);
 
+/* ---------------- OFDM receiver (dft/ofdm.h:49-151, ofdm.c) ----------------
+ * GPU FFT (mixed radix 8/4/3/2: 128..2048 points incl. 1536/768/384), no FFTW.  Provided:
+ * normal CP, normal subframes, rx_window_offset = 0, no frequency shift, no phase compensation
+ * (srsran_ue_dl's configuration, ue_dl.c:88-98) and DC removal (keep_dc = false); normalize is honoured.
+ * in_buffer / out_buffer are host pointers as in the reference. */
+typedef struct {
+  uint32_t    nof_prb;
+  cf_t*       in_buffer;
+  cf_t*       out_buffer;
+  srsran_cp_t cp;
+  srsran_sf_t sf_type;
+  bool        normalize;
+  float       freq_shift_f;
+  float       rx_window_offset;
+  uint32_t    symbol_sz;
+  bool        keep_dc;
+  double      phase_compensation_hz;
+} srsran_ofdm_cfg_t;
+
+typedef struct {
+  srsran_ofdm_cfg_t cfg;
+  uint32_t          max_prb;
+  uint32_t          nof_symbols;
+  uint32_t          nof_re;
+  uint32_t          slot_sz;
+  uint32_t          sf_sz;
+  void*             gpu; /* added: device plan, twiddles and staging */
+} srsran_ofdm_t;
+
+int  srsran_ofdm_rx_init_cfg(srsran_ofdm_t* q, srsran_ofdm_cfg_t* cfg);
+int  srsran_ofdm_rx_set_prb(srsran_ofdm_t* q, srsran_cp_t cp, uint32_t nof_prb);
+void srsran_ofdm_rx_free(srsran_ofdm_t* q);
+void srsran_ofdm_rx_sf(srsran_ofdm_t* q);
+void srsran_ofdm_rx_sf_ng(srsran_ofdm_t* q, cf_t* input, cf_t* output);
+void srsran_ofdm_set_normalize(srsran_ofdm_t* q, bool normalize_enable);
+
+/* added: nof_sf subframes x nof_rx antennas on device buffers (d_in: [sf][rx][sf_sz] samples,
+ * d_out: [sf][rx][14 * nof_re]); `cfo` rotates the samples as srsran_cfo_correct(.., cfo) would
+ * (0 = none).  Asynchronous on `stream`. */
+int srsran_ofdm_rx_gpu(srsran_ofdm_t* q, const cf_t* d_in, cf_t* d_out, uint32_t nof_rx, uint32_t nof_sf, float cfo,
+                       void* stream);
+
+/* ---------------- CFO correction (sync/cfo.h:41-63, cfo.c:96-107) ---------------- */
+typedef struct {
+  float    last_freq;
+  float    tol;
+  uint32_t nsamples;
+  uint32_t max_samples;
+  void*    gpu;
+} srsran_cfo_t;
+
+int  srsran_cfo_init(srsran_cfo_t* h, uint32_t nsamples);
+void srsran_cfo_free(srsran_cfo_t* h);
+int  srsran_cfo_resize(srsran_cfo_t* h, uint32_t samples);
+void srsran_cfo_set_tol(srsran_cfo_t* h, float tol);
+/* output[n] = input[n] * exp(j 2 pi freq n), n = 0..nsamples-1 */
+void srsran_cfo_correct(srsran_cfo_t* h, const cf_t* input, cf_t* output, float freq);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,60 @@
+"""numpy OFDM transmitter / receiver with srsRAN's conventions (TEST INFRASTRUCTURE ONLY).
+
+FFTW is not available here and no reference test pins its outputs, so the OFDM
+stage is checked against numpy's FFT (double precision) and by TX -> RX round trips:
+  - symbol i of slot s occupies [s*slot + cp0 + i*(N + cp), +N) (ofdm.c:169-181, 36.211 6.12)
+  - cp0 = ceil(160 N / 2048), cp = ceil(144 N / 2048) (phy_common.h:125-127)
+  - receiver: forward DFT, unnormalised, grid = [X[N-nre/2 ..], X[1 .. nre/2]] (ofdm.c:497-498)
+  - transmitter: the inverse mapping with an IFFT scaled by 1/N, so rx(tx(grid)) == grid
+  - CFO: z[n] = x[n] exp(j 2 pi f n), n from the subframe start (cfo.c:96-107)
+"""
+import math
+
+import numpy as np
+
+
+def cp_lens(N):
+    return math.ceil(160 * N / 2048), math.ceil(144 * N / 2048)
+
+
+def sf_len(N):
+    cp0, cp = cp_lens(N)
+    return 2 * (7 * N + cp0 + 6 * cp)
+
+
+def symbol_starts(N):
+    cp0, cp = cp_lens(N)
+    slot = 7 * N + cp0 + 6 * cp
+    return [s * slot + cp0 + i * (N + cp) for s in range(2) for i in range(7)]
+
+
+def ofdm_rx(x, N, nre, normalize=False):
+    x = np.asarray(x, np.complex128)
+    out = np.zeros((14, nre), np.complex128)
+    for l, st in enumerate(symbol_starts(N)):
+        X = np.fft.fft(x[st:st + N])
+        out[l, : nre // 2] = X[N - nre // 2:]
+        out[l, nre // 2:] = X[1: nre // 2 + 1]
+    if normalize:
+        out /= math.sqrt(N)
+    return out.reshape(-1)
+
+
+def ofdm_tx(grid, N, nre):
+    grid = np.asarray(grid, np.complex128).reshape(14, nre)
+    cp0, cp = cp_lens(N)
+    x = np.zeros(sf_len(N), np.complex128)
+    for l, st in enumerate(symbol_starts(N)):
+        X = np.zeros(N, np.complex128)
+        X[N - nre // 2:] = grid[l, : nre // 2]
+        X[1: nre // 2 + 1] = grid[l, nre // 2:]
+        t = np.fft.ifft(X)
+        c = cp0 if l % 7 == 0 else cp
+        x[st - c: st] = t[N - c:]
+        x[st: st + N] = t
+    return x
+
+
+def cfo(x, f):
+    n = np.arange(len(x))
+    return np.asarray(x, np.complex128) * np.exp(2j * np.pi * f * n)

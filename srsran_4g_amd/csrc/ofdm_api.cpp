@@ -1,0 +1,303 @@
+// srsran_4g_amd/csrc/ofdm_api.cpp -- C-ABI host side of the OFDM receiver and CFO correction.
+//
+// include/srsran_ue_dl.h: srsran_ofdm_rx_{init_cfg,set_prb,free,sf,sf_ng}, srsran_ofdm_set_normalize
+// (ofdm.c:38-563) and srsran_cfo_{init,free,resize,set_tol,correct} (cfo.c:36-107), plus the
+// batched device entry point.  The transforms run in ofdm_kernel.hip; no FFTW, no CPU fallback.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <vector>
+
+#include "../../include/srsran_ue_dl.h"
+#include "ofdm_kernel.h"
+
+using namespace srsran_amd;
+
+namespace {
+
+std::mutex                    g_tw_mu;
+std::map<uint32_t, float2*>   g_tw;  // per FFT size: exp(-2 pi i m / N)
+
+const float2* twiddles(uint32_t N)
+{
+  std::lock_guard<std::mutex> lk(g_tw_mu);
+  auto                        it = g_tw.find(N);
+  if (it != g_tw.end()) {
+    return it->second;
+  }
+  std::vector<float2> h(N);
+  for (uint32_t m = 0; m < N; m++) {
+    const double ang = -2.0 * M_PI * (double)m / (double)N;
+    h[m]             = make_float2((float)cos(ang), (float)sin(ang));
+  }
+  float2* d = nullptr;
+  if (hipMalloc((void**)&d, N * sizeof(float2)) != hipSuccess ||
+      hipMemcpy(d, h.data(), N * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess) {
+    return nullptr;
+  }
+  g_tw[N] = d;
+  return d;
+}
+
+struct OfdmGpu {
+  hipStream_t stream = nullptr;
+  float2*     d_in   = nullptr;
+  float2*     d_out  = nullptr;
+  size_t      in_cap = 0, out_cap = 0;
+  OfdmArgs    proto{};
+};
+
+uint32_t cp_len(uint32_t c, uint32_t N) { return (uint32_t)ceilf((float)c * (float)N / 2048.0f); }  // SRSRAN_CP_LEN
+
+bool grow(void** p, size_t* cap, size_t need)
+{
+  if (*cap >= need) {
+    return true;
+  }
+  hipFree(*p);
+  *p = nullptr;
+  if (hipMalloc(p, need) != hipSuccess) {
+    *cap = 0;
+    return false;
+  }
+  *cap = need;
+  return true;
+}
+
+int configure(srsran_ofdm_t* q, uint32_t nof_prb, uint32_t symbol_sz)
+{
+  OfdmGpu* g = (OfdmGpu*)q->gpu;
+  if (nof_prb == 0 || nof_prb > q->max_prb) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  const uint32_t N = symbol_sz ? symbol_sz : (uint32_t)srsran_symbol_sz(nof_prb);
+  OfdmArgs       a{};
+  a.nstages = ofdm_plan(N, a.radix);
+  if ((int)N <= 0 || N > OFDM_MAX_N || a.nstages <= 0 || 12 * nof_prb > N) {
+    fprintf(stderr, "[srsran_ofdm] unsupported symbol size %u\n", N);
+    return SRSRAN_ERROR;
+  }
+  a.tw = twiddles(N);
+  if (!a.tw) {
+    return SRSRAN_ERROR;
+  }
+  a.N              = N;
+  a.cp0            = cp_len(160, N);  // SRSRAN_CP_NORM_0_LEN
+  a.cp             = cp_len(144, N);  // SRSRAN_CP_NORM_LEN
+  a.nre            = 12 * nof_prb;
+  a.sf_len         = 2 * (7 * N + a.cp0 + 6 * a.cp);
+  a.nrx            = 1;
+  a.norm           = q->cfg.normalize ? 1.0f / sqrtf((float)N) : 1.0f;
+  g->proto         = a;
+  q->cfg.nof_prb   = nof_prb;
+  q->cfg.symbol_sz = N;
+  q->nof_symbols   = 7;
+  q->nof_re        = a.nre;
+  q->slot_sz       = a.sf_len / 2;
+  q->sf_sz         = a.sf_len;
+  return SRSRAN_SUCCESS;
+}
+
+int run(srsran_ofdm_t* q, const float2* d_in, float2* d_out, uint32_t nrx, uint32_t nsf, float cfo, hipStream_t s)
+{
+  OfdmGpu* g = (OfdmGpu*)q->gpu;
+  OfdmArgs a = g->proto;
+  a.in       = d_in;
+  a.out      = d_out;
+  a.nrx      = nrx;
+  a.cfo      = (double)cfo;
+  return ofdm_rx_launch(a, nsf, s) == hipSuccess ? SRSRAN_SUCCESS : SRSRAN_ERROR;
+}
+
+}  // namespace
+
+extern "C" {
+
+int srsran_ofdm_rx_init_cfg(srsran_ofdm_t* q, srsran_ofdm_cfg_t* cfg)
+{
+  if (!q || !cfg || cfg->nof_prb == 0 || cfg->nof_prb > 110) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  if (cfg->cp != SRSRAN_CP_NORM || cfg->sf_type != SRSRAN_SF_NORM || std::isnormal(cfg->freq_shift_f) ||
+      std::isnormal(cfg->rx_window_offset) || std::isnormal(cfg->phase_compensation_hz) || cfg->keep_dc) {
+    fprintf(stderr, "[srsran_ofdm] only the srsran_ue_dl receiver configuration is provided\n");
+    return SRSRAN_ERROR;
+  }
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
+    fprintf(stderr, "[srsran_ofdm] no HIP device available\n");
+    return SRSRAN_ERROR;
+  }
+  memset(q, 0, sizeof(*q));
+  q->cfg     = *cfg;
+  q->max_prb = cfg->nof_prb;
+  OfdmGpu* g = new OfdmGpu();
+  q->gpu     = g;
+  if (hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking) != hipSuccess) {
+    srsran_ofdm_rx_free(q);
+    return SRSRAN_ERROR;
+  }
+  const int ret = configure(q, cfg->nof_prb, cfg->symbol_sz);
+  if (ret) {
+    srsran_ofdm_rx_free(q);
+  }
+  return ret;
+}
+
+int srsran_ofdm_rx_set_prb(srsran_ofdm_t* q, srsran_cp_t cp, uint32_t nof_prb)
+{
+  if (!q || !q->gpu) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  if (cp != SRSRAN_CP_NORM) {
+    return SRSRAN_ERROR;
+  }
+  return configure(q, nof_prb, 0);
+}
+
+void srsran_ofdm_rx_free(srsran_ofdm_t* q)
+{
+  if (!q) {
+    return;
+  }
+  OfdmGpu* g = (OfdmGpu*)q->gpu;
+  if (g) {
+    if (g->stream) {
+      hipStreamSynchronize(g->stream);
+      hipStreamDestroy(g->stream);
+    }
+    hipFree(g->d_in);
+    hipFree(g->d_out);
+    delete g;
+  }
+  memset(q, 0, sizeof(*q));
+}
+
+void srsran_ofdm_set_normalize(srsran_ofdm_t* q, bool normalize_enable)
+{
+  if (q && q->gpu) {
+    q->cfg.normalize             = normalize_enable;
+    ((OfdmGpu*)q->gpu)->proto.norm = normalize_enable ? 1.0f / sqrtf((float)q->cfg.symbol_sz) : 1.0f;
+  }
+}
+
+void srsran_ofdm_rx_sf_ng(srsran_ofdm_t* q, cf_t* input, cf_t* output)
+{
+  if (!q || !q->gpu || !input || !output) {
+    return;
+  }
+  OfdmGpu*     g  = (OfdmGpu*)q->gpu;
+  const size_t ni = q->sf_sz, no = 14 * (size_t)q->nof_re;
+  if (!grow((void**)&g->d_in, &g->in_cap, ni * sizeof(cf_t)) || !grow((void**)&g->d_out, &g->out_cap, no * sizeof(cf_t))) {
+    return;
+  }
+  hipMemcpyAsync(g->d_in, input, ni * sizeof(cf_t), hipMemcpyHostToDevice, g->stream);
+  if (run(q, g->d_in, g->d_out, 1, 1, 0.0f, g->stream) == SRSRAN_SUCCESS) {
+    hipMemcpyAsync(output, g->d_out, no * sizeof(cf_t), hipMemcpyDeviceToHost, g->stream);
+  }
+  hipStreamSynchronize(g->stream);
+}
+
+void srsran_ofdm_rx_sf(srsran_ofdm_t* q)
+{
+  if (q) {
+    srsran_ofdm_rx_sf_ng(q, q->cfg.in_buffer, q->cfg.out_buffer);
+  }
+}
+
+int srsran_ofdm_rx_gpu(srsran_ofdm_t* q, const cf_t* d_in, cf_t* d_out, uint32_t nof_rx, uint32_t nof_sf, float cfo,
+                       void* stream)
+{
+  if (!q || !q->gpu || !d_in || !d_out || nof_rx == 0) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  if (nof_sf == 0) {
+    return SRSRAN_SUCCESS;
+  }
+  return run(q, (const float2*)d_in, (float2*)d_out, nof_rx, nof_sf, cfo, (hipStream_t)stream);
+}
+
+// ---------------- cfo.c ----------------
+struct CfoGpu {
+  hipStream_t stream = nullptr;
+  float2*     d      = nullptr;
+  size_t      cap    = 0;
+};
+
+int srsran_cfo_init(srsran_cfo_t* h, uint32_t nsamples)
+{
+  if (!h) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  memset(h, 0, sizeof(*h));
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
+    fprintf(stderr, "[srsran_cfo] no HIP device available\n");
+    return SRSRAN_ERROR;
+  }
+  CfoGpu* g = new CfoGpu();
+  h->gpu    = g;
+  if (hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking) != hipSuccess ||
+      !grow((void**)&g->d, &g->cap, 2 * (size_t)(nsamples ? nsamples : 1) * sizeof(float2))) {
+    srsran_cfo_free(h);
+    return SRSRAN_ERROR;
+  }
+  h->nsamples    = nsamples;
+  h->max_samples = nsamples;
+  h->tol         = 0.0f;
+  return SRSRAN_SUCCESS;
+}
+
+void srsran_cfo_free(srsran_cfo_t* h)
+{
+  if (!h) {
+    return;
+  }
+  CfoGpu* g = (CfoGpu*)h->gpu;
+  if (g) {
+    if (g->stream) {
+      hipStreamSynchronize(g->stream);
+      hipStreamDestroy(g->stream);
+    }
+    hipFree(g->d);
+    delete g;
+  }
+  memset(h, 0, sizeof(*h));
+}
+
+int srsran_cfo_resize(srsran_cfo_t* h, uint32_t samples)
+{
+  if (!h || !h->gpu || samples > h->max_samples) {
+    return SRSRAN_ERROR;
+  }
+  h->nsamples = samples;
+  return SRSRAN_SUCCESS;
+}
+
+void srsran_cfo_set_tol(srsran_cfo_t* h, float tol)
+{
+  if (h) {
+    h->tol = tol;
+  }
+}
+
+void srsran_cfo_correct(srsran_cfo_t* h, const cf_t* input, cf_t* output, float freq)
+{
+  if (!h || !h->gpu || !input || !output || h->nsamples == 0) {
+    return;
+  }
+  CfoGpu*      g = (CfoGpu*)h->gpu;
+  const size_t n = h->nsamples;
+  hipMemcpyAsync(g->d, input, n * sizeof(cf_t), hipMemcpyHostToDevice, g->stream);
+  if (cfo_launch(g->d, g->d + n, (uint32_t)n, (double)freq, g->stream) == hipSuccess) {
+    hipMemcpyAsync(output, g->d + n, n * sizeof(cf_t), hipMemcpyDeviceToHost, g->stream);
+  }
+  hipStreamSynchronize(g->stream);
+  h->last_freq = freq;
+}
+
+}  // extern "C"

@@ -1,0 +1,37 @@
+// srsran_4g_amd/csrc/ofdm_kernel.h -- OFDM demodulation (CP removal, CFO, FFT, subcarrier map).
+#ifndef SRSRAN_AMD_OFDM_KERNEL_H
+#define SRSRAN_AMD_OFDM_KERNEL_H
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace srsran_amd {
+
+static constexpr int OFDM_MAX_N      = 2048;
+static constexpr int OFDM_MAX_STAGES = 6;
+
+struct OfdmArgs {
+  const float2* in;        // [sf][rx][sf_len] time-domain samples
+  float2*       out;       // [sf][rx][14][nre] resource grid
+  const float2* tw;        // exp(-2 pi i m / N), m = 0..N-1
+  uint32_t      N;         // FFT size (symbol_sz)
+  uint32_t      cp0, cp;   // first / other cyclic prefix lengths of a slot
+  uint32_t      nre;       // 12 * nof_prb
+  uint32_t      sf_len;    // samples per subframe and antenna
+  uint32_t      nrx;
+  float         norm;      // 1 or 1/sqrt(N) (srsran_ofdm_cfg_t.normalize)
+  double        cfo;       // z[n] = x[n] exp(j 2 pi cfo n), n from the subframe start; 0 = off
+  int           nstages;
+  int           radix[OFDM_MAX_STAGES];
+};
+
+// grid: (14, nrx, nsf) workgroups
+hipError_t ofdm_rx_launch(const OfdmArgs& a, uint32_t nsf, hipStream_t stream);
+
+// factor N into radices 8/4/3/2 (largest first); returns the number of stages or -1
+int ofdm_plan(uint32_t N, int* radix);
+
+// standalone CFO correction z[n] = x[n] exp(j 2 pi f n)
+hipError_t cfo_launch(const float2* in, float2* out, uint32_t n, double f, hipStream_t stream);
+
+}  // namespace srsran_amd
+#endif

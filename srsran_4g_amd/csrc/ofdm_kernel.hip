@@ -1,0 +1,210 @@
+// srsran_4g_amd/csrc/ofdm_kernel.hip -- OFDM receiver for CDNA4.
+//
+// srsran_ofdm_rx_sf (ofdm.c:551-563 -> ofdm_rx_slot 474-520) as srsran_ue_dl configures it
+// (ue_dl.c:88-98: no window offset, no normalisation, DC removed): symbol i of slot s starts
+// at s * slot_sz + cp0 + i * (N + cp) (the guru plan of ofdm.c:169-181), forward DFT
+// (FFTW_FORWARD), then the fftshift that drops the DC bin (ofdm.c:497-498): grid[0..nre/2) =
+// X[N - nre/2 ..), grid[nre/2 ..) = X[1 .. nre/2].  srsran_cfo_correct's rotation
+// (cfo.c:96-107, vector_simd.c:1723-1774) can be folded into the sample load.
+//
+// One workgroup per OFDM symbol: the N samples are rotated on load into LDS, transformed by
+// a mixed-radix (8/4/3/2) Stockham FFT with ping-pong LDS buffers (natural-order output, no
+// bit reversal), and only the nre occupied subcarriers are written back.  Twiddles come from
+// a per-N table computed in double precision on the host.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ofdm_kernel.h"
+
+namespace srsran_amd {
+
+static constexpr int OFDM_THREADS = 256;
+
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 cmul(float2 a, float2 b)
+{
+  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ float2 mul_mi(float2 a) { return make_float2(a.y, -a.x); }  // * (-i)
+
+__device__ __forceinline__ void dft2(float2* v)
+{
+  const float2 a = v[0];
+  v[0]           = cadd(a, v[1]);
+  v[1]           = csub(a, v[1]);
+}
+__device__ __forceinline__ void dft4(float2* v)
+{
+  const float2 a0 = cadd(v[0], v[2]), a1 = csub(v[0], v[2]);
+  const float2 a2 = cadd(v[1], v[3]), a3 = mul_mi(csub(v[1], v[3]));
+  v[0]            = cadd(a0, a2);
+  v[2]            = csub(a0, a2);
+  v[1]            = cadd(a1, a3);
+  v[3]            = csub(a1, a3);
+}
+__device__ __forceinline__ void dft3(float2* v)
+{
+  const float  s   = 0.86602540378443864676f;  // sqrt(3)/2
+  const float2 sum = cadd(v[1], v[2]);
+  const float2 t1  = make_float2(v[0].x - 0.5f * sum.x, v[0].y - 0.5f * sum.y);
+  const float2 d   = csub(v[1], v[2]);
+  const float2 t2  = make_float2(d.y * s, -d.x * s);  // (x1 - x2) * (-i sqrt(3)/2)
+  v[0]             = cadd(v[0], sum);
+  v[1]             = cadd(t1, t2);
+  v[2]             = csub(t1, t2);
+}
+__device__ __forceinline__ void dft8(float2* v)
+{
+  float2 e[4] = {v[0], v[2], v[4], v[6]}, o[4] = {v[1], v[3], v[5], v[7]};
+  dft4(e);
+  dft4(o);
+  const float r = 0.70710678118654752440f;
+  o[1]          = make_float2((o[1].x + o[1].y) * r, (o[1].y - o[1].x) * r);    // * e^{-i pi/4}
+  o[2]          = mul_mi(o[2]);                                                  // * e^{-i pi/2}
+  o[3]          = make_float2((-o[3].x + o[3].y) * r, (-o[3].y - o[3].x) * r);  // * e^{-3i pi/4}
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    v[k]     = cadd(e[k], o[k]);
+    v[k + 4] = csub(e[k], o[k]);
+  }
+}
+
+template <int R>
+__device__ __forceinline__ void stage(const float2* src, float2* dst, const float2* tw, uint32_t N, uint32_t Ns)
+{
+  const uint32_t nb = N / R, tstep = N / (Ns * R);
+  for (uint32_t j = threadIdx.x; j < nb; j += OFDM_THREADS) {
+    const uint32_t k = j % Ns;
+    float2         v[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      v[r] = src[j + r * nb];
+    }
+    if (Ns > 1) {
+#pragma unroll
+      for (int r = 1; r < R; r++) {
+        v[r] = cmul(v[r], tw[(r * k * tstep) % N]);
+      }
+    }
+    if constexpr (R == 8) {
+      dft8(v);
+    } else if constexpr (R == 4) {
+      dft4(v);
+    } else if constexpr (R == 3) {
+      dft3(v);
+    } else {
+      dft2(v);
+    }
+    const uint32_t base = (j / Ns) * Ns * R + k;
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      dst[base + r * Ns] = v[r];
+    }
+  }
+}
+
+__global__ __launch_bounds__(OFDM_THREADS) void ofdm_rx_kernel(OfdmArgs a)
+{
+  __shared__ float2 buf[2][OFDM_MAX_N];
+  const uint32_t    sym = blockIdx.x, rx = blockIdx.y, sf = blockIdx.z;
+  const uint32_t    N = a.N, slot = sym / 7, i = sym % 7;
+  const uint32_t    slot_sz = 7 * N + a.cp0 + 6 * a.cp;
+  const uint32_t    off     = slot * slot_sz + a.cp0 + i * (N + a.cp);
+  const float2*     src     = a.in + ((size_t)sf * a.nrx + rx) * a.sf_len + off;
+  for (uint32_t n = threadIdx.x; n < N; n += OFDM_THREADS) {
+    float2 x = src[n];
+    if (a.cfo != 0.0) {
+      // phase 2 pi f (off + n), reduced in double before the float sincos
+      double ph = a.cfo * (double)(off + n);
+      ph -= rint(ph);
+      float s, c;
+      sincosf((float)(6.283185307179586476925 * ph), &s, &c);
+      x = cmul(x, make_float2(c, s));
+    }
+    buf[0][n] = x;
+  }
+  __syncthreads();
+  uint32_t Ns = 1, cur = 0;
+  for (int st = 0; st < a.nstages; st++) {
+    const int R = a.radix[st];
+    if (R == 8) {
+      stage<8>(buf[cur], buf[cur ^ 1], a.tw, N, Ns);
+    } else if (R == 4) {
+      stage<4>(buf[cur], buf[cur ^ 1], a.tw, N, Ns);
+    } else if (R == 3) {
+      stage<3>(buf[cur], buf[cur ^ 1], a.tw, N, Ns);
+    } else {
+      stage<2>(buf[cur], buf[cur ^ 1], a.tw, N, Ns);
+    }
+    Ns *= (uint32_t)R;
+    cur ^= 1;
+    __syncthreads();
+  }
+  float2*        dst  = a.out + (((size_t)sf * a.nrx + rx) * 14 + sym) * a.nre;
+  const uint32_t half = a.nre / 2;
+  for (uint32_t k = threadIdx.x; k < a.nre; k += OFDM_THREADS) {
+    const uint32_t bin = k < half ? N - half + k : k - half + 1;
+    float2         v   = buf[cur][bin];
+    if (a.norm != 1.0f) {
+      v = make_float2(v.x * a.norm, v.y * a.norm);
+    }
+    dst[k] = v;
+  }
+}
+
+int ofdm_plan(uint32_t N, int* radix)
+{
+  int n = 0;
+  while (N > 1 && n < OFDM_MAX_STAGES) {
+    if (N % 8 == 0 && N != 16) {  // 16 = 4 x 4 keeps every stage at >= radix 4
+      radix[n++] = 8;
+      N /= 8;
+    } else if (N % 4 == 0) {
+      radix[n++] = 4;
+      N /= 4;
+    } else if (N % 3 == 0) {
+      radix[n++] = 3;
+      N /= 3;
+    } else if (N % 2 == 0) {
+      radix[n++] = 2;
+      N /= 2;
+    } else {
+      return -1;
+    }
+  }
+  return N == 1 ? n : -1;
+}
+
+hipError_t ofdm_rx_launch(const OfdmArgs& a, uint32_t nsf, hipStream_t stream)
+{
+  if (a.N > OFDM_MAX_N || a.nstages <= 0 || nsf == 0) {
+    return hipErrorInvalidValue;
+  }
+  hipLaunchKernelGGL(ofdm_rx_kernel, dim3(14, a.nrx, nsf), dim3(OFDM_THREADS), 0, stream, a);
+  return hipGetLastError();
+}
+
+__global__ void cfo_kernel(const float2* __restrict__ in, float2* __restrict__ out, uint32_t n, double f)
+{
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) {
+    return;
+  }
+  double ph = f * (double)k;
+  ph -= rint(ph);
+  float s, c;
+  sincosf((float)(6.283185307179586476925 * ph), &s, &c);
+  out[k] = cmul(in[k], make_float2(c, s));
+}
+
+hipError_t cfo_launch(const float2* in, float2* out, uint32_t n, double f, hipStream_t stream)
+{
+  if (n == 0) {
+    return hipSuccess;
+  }
+  hipLaunchKernelGGL(cfo_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, in, out, n, f);
+  return hipGetLastError();
+}
+
+}  // namespace srsran_amd

@@ -47,6 +47,23 @@ class srsran_chest_dl_t(ctypes.Structure):
                 ("noise_estimate", F44), ("cfo", ctypes.c_float), ("gpu", ctypes.c_void_p)]
 
 
+class srsran_ofdm_cfg_t(ctypes.Structure):
+    _fields_ = [("nof_prb", u32), ("in_buffer", ctypes.c_void_p), ("out_buffer", ctypes.c_void_p), ("cp", ctypes.c_int),
+                ("sf_type", ctypes.c_int), ("normalize", ctypes.c_bool), ("freq_shift_f", ctypes.c_float),
+                ("rx_window_offset", ctypes.c_float), ("symbol_sz", u32), ("keep_dc", ctypes.c_bool),
+                ("phase_compensation_hz", ctypes.c_double)]
+
+
+class srsran_ofdm_t(ctypes.Structure):
+    _fields_ = [("cfg", srsran_ofdm_cfg_t), ("max_prb", u32), ("nof_symbols", u32), ("nof_re", u32), ("slot_sz", u32),
+                ("sf_sz", u32), ("gpu", ctypes.c_void_p)]
+
+
+class srsran_cfo_t(ctypes.Structure):
+    _fields_ = [("last_freq", ctypes.c_float), ("tol", ctypes.c_float), ("nsamples", u32), ("max_samples", u32),
+                ("gpu", ctypes.c_void_p)]
+
+
 _bound = False
 
 
@@ -69,6 +86,16 @@ def lib():
             "srsran_chest_dl_estimate_cfg": ([CH, ctypes.POINTER(srsran_dl_sf_cfg_t),
                                               ctypes.POINTER(srsran_chest_dl_cfg_t), P, RES], ctypes.c_int),
             "srsran_chest_dl_gpu_estimate": ([CH, u32, P, P, ctypes.c_int, P, P], ctypes.c_int),
+            "srsran_ofdm_rx_init_cfg": ([ctypes.POINTER(srsran_ofdm_t), ctypes.POINTER(srsran_ofdm_cfg_t)], ctypes.c_int),
+            "srsran_ofdm_rx_set_prb": ([ctypes.POINTER(srsran_ofdm_t), ctypes.c_int, u32], ctypes.c_int),
+            "srsran_ofdm_rx_free": ([ctypes.POINTER(srsran_ofdm_t)], None),
+            "srsran_ofdm_rx_sf": ([ctypes.POINTER(srsran_ofdm_t)], None),
+            "srsran_ofdm_rx_sf_ng": ([ctypes.POINTER(srsran_ofdm_t), P, P], None),
+            "srsran_ofdm_set_normalize": ([ctypes.POINTER(srsran_ofdm_t), ctypes.c_bool], None),
+            "srsran_ofdm_rx_gpu": ([ctypes.POINTER(srsran_ofdm_t), P, P, u32, u32, ctypes.c_float, P], ctypes.c_int),
+            "srsran_cfo_init": ([ctypes.POINTER(srsran_cfo_t), u32], ctypes.c_int),
+            "srsran_cfo_free": ([ctypes.POINTER(srsran_cfo_t)], None),
+            "srsran_cfo_correct": ([ctypes.POINTER(srsran_cfo_t), P, P, ctypes.c_float], None),
         }
         for name, (args, res) in sig.items():
             f = getattr(L, name)
@@ -94,6 +121,50 @@ def srsue_chest_cfg():
     c.cfo_estimate_enable = True
     c.cfo_estimate_sf_mask = 1023
     return c
+
+
+class OfdmRx:
+    """srsran_ofdm_t receiver (srsran_ue_dl configuration)."""
+
+    def __init__(self, nof_prb, normalize=False):
+        self.cfg = srsran_ofdm_cfg_t()
+        self.cfg.nof_prb = nof_prb
+        self.cfg.normalize = normalize
+        self.q = srsran_ofdm_t()
+        if lib().srsran_ofdm_rx_init_cfg(ctypes.byref(self.q), ctypes.byref(self.cfg)):
+            raise RuntimeError("srsran_ofdm_rx_init_cfg failed")
+
+    @property
+    def symbol_sz(self):
+        return self.q.cfg.symbol_sz
+
+    def rx(self, samples):
+        x = np.ascontiguousarray(samples, np.complex64)
+        assert x.size == self.q.sf_sz
+        out = np.zeros(14 * self.q.nof_re, np.complex64)
+        lib().srsran_ofdm_rx_sf_ng(ctypes.byref(self.q), x.ctypes.data, out.ctypes.data)
+        return out
+
+    def free(self):
+        if self.q.gpu:
+            lib().srsran_ofdm_rx_free(ctypes.byref(self.q))
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def cfo_correct(x, freq):
+    h = srsran_cfo_t()
+    x = np.ascontiguousarray(x, np.complex64)
+    if lib().srsran_cfo_init(ctypes.byref(h), x.size):
+        raise RuntimeError("srsran_cfo_init failed")
+    out = np.zeros_like(x)
+    lib().srsran_cfo_correct(ctypes.byref(h), x.ctypes.data, out.ctypes.data, freq)
+    lib().srsran_cfo_free(ctypes.byref(h))
+    return out
 
 
 class ChestDl:

@@ -1,0 +1,70 @@
+"""GPU OFDM receiver and CFO correction.  The FFT stage has no pinned reference output (FFTW
+is absent and no reference test holds its results): it is checked against numpy's
+double-precision FFT with srsRAN's symbol timing / subcarrier mapping (oracle/ofdm_np.py) and
+by TX -> RX round trips, at float32 tolerance."""
+import numpy as np
+import pytest
+import torch
+
+import ofdm_np
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def U():
+    from srsran_4g_amd import ue_dl
+    return ue_dl
+
+
+@pytest.mark.parametrize("nof_prb", [6, 15, 25, 50, 75, 100])
+def test_ofdm_rx_matches_numpy(U, nof_prb):
+    rng = np.random.default_rng(nof_prb)
+    rx = U.OfdmRx(nof_prb)
+    N, nre = rx.symbol_sz, 12 * nof_prb
+    assert N == U.lib().srsran_symbol_sz(nof_prb)
+    x = (rng.standard_normal(ofdm_np.sf_len(N)) + 1j * rng.standard_normal(ofdm_np.sf_len(N))).astype(np.complex64)
+    got = rx.rx(x)
+    exp = ofdm_np.ofdm_rx(x, N, nre)
+    assert np.abs(got - exp).max() < 2e-5 * np.abs(exp).max() * np.log2(N)
+    # round trip of a QAM grid
+    g = (rng.choice([-3, -1, 1, 3], 14 * nre) + 1j * rng.choice([-3, -1, 1, 3], 14 * nre)).astype(np.complex64)
+    back = rx.rx(ofdm_np.ofdm_tx(g, N, nre).astype(np.complex64))
+    assert np.abs(back - g).max() < 1e-4 * 3
+    rx.free()
+
+
+def test_ofdm_normalize(U):
+    rng = np.random.default_rng(1)
+    rx = U.OfdmRx(100, normalize=True)
+    x = (rng.standard_normal(30720) + 1j * rng.standard_normal(30720)).astype(np.complex64)
+    exp = ofdm_np.ofdm_rx(x, 2048, 1200, normalize=True)
+    assert np.abs(rx.rx(x) - exp).max() < 1e-5 * np.abs(exp).max() * 11
+    rx.free()
+
+
+def test_cfo_correct(U):
+    rng = np.random.default_rng(2)
+    x = (rng.standard_normal(30720) + 1j * rng.standard_normal(30720)).astype(np.complex64)
+    for f in (1e-4, -3.3e-3, 0.01):
+        got = U.cfo_correct(x, f)
+        exp = ofdm_np.cfo(x, f)
+        assert np.abs(got - exp).max() < 2e-5 * np.abs(exp).max()
+
+
+def test_ofdm_gpu_batch_with_cfo(U):
+    """Device batch: 3 subframes x 2 antennas, CFO folded into the sample load."""
+    import ctypes
+    rng = np.random.default_rng(3)
+    rx = U.OfdmRx(100)
+    nsf, nrx, L, nre, f = 3, 2, 30720, 1200, 2.5e-4
+    grids = (rng.choice([-1, 1], (nsf, nrx, 14 * nre)) + 1j * rng.choice([-1, 1], (nsf, nrx, 14 * nre)))
+    x = np.stack([np.stack([ofdm_np.cfo(ofdm_np.ofdm_tx(grids[s, r], 2048, nre), -f) for r in range(nrx)])
+                  for s in range(nsf)]).astype(np.complex64)
+    d_in = torch.from_numpy(x.view(np.float32).reshape(-1)).cuda()
+    d_out = torch.zeros(nsf * nrx * 14 * nre * 2, dtype=torch.float32, device="cuda")
+    assert U.lib().srsran_ofdm_rx_gpu(ctypes.byref(rx.q), d_in.data_ptr(), d_out.data_ptr(), nrx, nsf, f, None) == 0
+    torch.cuda.synchronize()
+    got = d_out.cpu().numpy().view(np.complex64).reshape(nsf, nrx, 14 * nre)
+    assert np.abs(got - grids).max() < 2e-4
+    rx.free()

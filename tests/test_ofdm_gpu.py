@@ -48,7 +48,7 @@ def test_cfo_correct(U):
     x = (rng.standard_normal(30720) + 1j * rng.standard_normal(30720)).astype(np.complex64)
     for f in (1e-4, -3.3e-3, 0.01):
         got = U.cfo_correct(x, f)
-        exp = ofdm_np.cfo(x, f)
+        exp = ofdm_np.cfo(x, float(np.float32(f)))  # the API takes freq as a float (cfo.h:58)
         assert np.abs(got - exp).max() < 2e-5 * np.abs(exp).max()
 
 

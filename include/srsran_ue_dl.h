@@ -182,6 +182,16 @@ void srsran_ofdm_set_normalize(srsran_ofdm_t* q, bool normalize_enable);
 int srsran_ofdm_rx_gpu(srsran_ofdm_t* q, const cf_t* d_in, cf_t* d_out, uint32_t nof_rx, uint32_t nof_sf, float cfo,
                        void* stream);
 
+/* ---------------- PDSCH RE map (added; srsran_pdsch_cp pdsch.c:136-220 as a table) ----------------
+ * Number of PDSCH REs of `grant`; writes up to max_len grid indices (l * 12 * nof_prb + k) in
+ * srsran_pdsch_get order; bit 31 marks REs of CRS-bearing symbols. */
+int srsran_pdsch_re_table(const srsran_cell_t*        cell,
+                          const srsran_pdsch_grant_t* grant,
+                          uint32_t                    lstart,
+                          uint32_t                    sf_idx,
+                          uint32_t*                   idx,
+                          uint32_t                    max_len);
+
 /* ---------------- CFO correction (sync/cfo.h:41-63, cfo.c:96-107) ---------------- */
 typedef struct {
   float    last_freq;

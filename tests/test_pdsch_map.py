@@ -1,0 +1,52 @@
+"""CPU test of the PDSCH RE map (host code in srsran_4g_amd/csrc/pdsch_map.cpp, a restatement
+of srsran_pdsch_cp, pdsch.c:136-220) against an independent rule-based restatement
+(oracle/pdsch_np.py): cells of 6..100 PRB (odd and even), 1/2/4 ports, all subframes, CFI 1..3,
+full and partial PRB allocations."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import pdsch_np
+from srsran_4g_amd import sch as S
+from srsran_4g_amd import ue_dl as U
+
+
+def product_table(nof_prb, nports, cell_id, mask, lstart, sf_idx):
+    cell = U.cell(nof_prb, nports, cell_id)
+    g = S.srsran_pdsch_grant_t()
+    g.nof_symb_slot[0] = g.nof_symb_slot[1] = 7
+    for s in range(2):
+        for n in range(nof_prb):
+            g.prb_idx[s][n] = bool(mask[s][n])
+    f = S.lib().srsran_pdsch_re_table
+    f.argtypes = [ctypes.POINTER(U.srsran_cell_t), ctypes.POINTER(S.srsran_pdsch_grant_t), ctypes.c_uint32,
+                  ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32]
+    f.restype = ctypes.c_int
+    n = f(ctypes.byref(cell), ctypes.byref(g), lstart, sf_idx, None, 0)
+    out = np.zeros(max(n, 1), np.uint32)
+    f(ctypes.byref(cell), ctypes.byref(g), lstart, sf_idx, out.ctypes.data, n)
+    return out[:n]
+
+
+@pytest.mark.parametrize("nof_prb", [6, 15, 25, 50, 75, 100, 27])
+@pytest.mark.parametrize("nports", [1, 2, 4])
+def test_re_table_matches_rules(nof_prb, nports):
+    rng = np.random.default_rng(nof_prb * 10 + nports)
+    for sf_idx in range(10):
+        for lstart in (1, 2, 3):
+            full = [[1] * nof_prb, [1] * nof_prb]
+            part = [list(rng.integers(0, 2, nof_prb))] * 2
+            for mask in (full, part):
+                cell_id = int(rng.integers(0, 504))
+                got = product_table(nof_prb, nports, cell_id, mask, lstart, sf_idx)
+                exp = pdsch_np.re_table(nof_prb, nports, cell_id, mask, lstart, sf_idx)
+                assert len(got) == len(exp), (sf_idx, lstart)
+                assert np.array_equal(got & 0x7FFFFFFF, [e[0] for e in exp])
+                assert np.array_equal((got >> 31).astype(bool), [e[1] for e in exp])
+
+
+def test_c3_grant_size():
+    """100 PRB, 2 ports, CFI 1, subframe 1: 14400 PDSCH REs (SURVEY 8, C3 grant)."""
+    got = product_table(100, 2, 1, [[1] * 100, [1] * 100], 1, 1)
+    assert len(got) == 14400

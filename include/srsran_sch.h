@@ -206,6 +206,15 @@ int srsran_dlsch_decode2(srsran_sch_t*       q,
                          int                 tb_idx,
                          uint32_t            nof_layers);
 
+/* added: srsran_dlsch_decode2 whose LLRs are already in device memory (written before the call
+ * returns control to the host, e.g. by a synchronised stream). */
+int srsran_dlsch_decode2_dev(srsran_sch_t*       q,
+                             srsran_pdsch_cfg_t* cfg,
+                             const int16_t*      d_e_bits,
+                             uint8_t*            data,
+                             int                 tb_idx,
+                             uint32_t            nof_layers);
+
 /* ---------------- added: batched, asynchronous DL-SCH decode over device buffers ----------------
  * One entry per transport block; every entry is decoded with exactly the semantics of
  * decode_tb (sch.c:509-573) against its own soft buffer.  Results land in device memory:

@@ -1,0 +1,81 @@
+"""CPU restatement of srsUE's PDSCH receive chain composed from the oracle's pinned pieces
+(TEST INFRASTRUCTURE ONLY -- the checker for the GPU chain; never imported by the product).
+
+  srsran_ue_dl_decode_fft_estimate  ue_dl.c:349-364 -> ofdm_np.ofdm_rx + Oracle.chest_dl
+  srsran_ue_dl_decode_pdsch         ue_dl.c:700-706 -> pdsch_decode below
+  srsran_pdsch_decode               pdsch.c:788-958:
+      srsran_pdsch_get              pdsch_np.re_table (symbols and estimates)
+      apply_power_allocation        pdsch.c:485-521 (rho_b on CRS symbols, rho_a as scaling)
+      srsran_predecoding_type       Oracle.predecode (MMSE with CSI)
+      codeword decode               pdsch.c:661-744: demod_s, sequence_pdsch_apply_s,
+                                    csi_correction, srsran_dlsch_decode2 (Oracle.dlsch_decode)
+Parity: each piece is pinned to the reference (tests/test_phy_oracle.py, test_sch_oracle.py);
+the OFDM stage is numpy (FFTW unavailable, 'parity unpinned' beyond round trips).
+"""
+import math
+
+import numpy as np
+
+import ofdm_np
+import pdsch_np
+
+SCHEME = {"port0": 0, "sm": 2, "cdd": 3}
+MOD = {1: 0, 2: 1, 4: 2, 6: 3, 8: 4}
+RHO_TABLE = ((1.0, 4.0 / 5, 3.0 / 5, 2.0 / 5), (5.0 / 4, 1.0, 3.0 / 4, 1.0 / 2))  # pdsch.c:44-46
+
+
+def symbol_sz(nof_prb):
+    for p, n in ((6, 128), (15, 256), (25, 512), (52, 1024), (79, 1536), (110, 2048)):
+        if nof_prb <= p:
+            return n
+    raise ValueError(nof_prb)
+
+
+def fft_estimate(ora, samples, nof_prb, cell_id, nports, tti, cfo=0.0, N=None):
+    """-> grids (nrx, 14*12*nof_prb) complex64, ce (nports, nrx, n) complex64, stats"""
+    N = N or symbol_sz(nof_prb)
+    nre = 12 * nof_prb
+    grids = []
+    for x in samples:
+        if cfo:
+            x = ofdm_np.cfo(x, cfo)
+        grids.append(ofdm_np.ofdm_rx(x, N, nre).astype(np.complex64))
+    grids = np.stack(grids)
+    ce, st = ora.chest_dl(grids, nof_prb, cell_id, nports, tti % 10, N)
+    return grids, ce, st
+
+
+def pdsch_decode(ora, grids, ce, noise, nof_prb, cell_id, nports, tti, cfi, rnti, tbs, Qm, rv, scheme="cdd",
+                 pmi=0, max_iterations=8, csi_enable=True, power_scale=False, p_a=0.0, p_b=0, prb_mask=None,
+                 states=None):
+    """srsran_pdsch_decode for nof_tb = len(tbs) codewords (one layer each).
+    Returns per codeword dict(ret, data, avg, llr)."""
+    sf_idx = tti % 10
+    lstart = cfi + (1 if nof_prb < 10 else 0)
+    mask = np.ones((2, nof_prb), bool) if prb_mask is None else prb_mask
+    tab = pdsch_np.re_table(nof_prb, nports, cell_id, mask, lstart, sf_idx)
+    idx = np.array([t[0] for t in tab], np.int64)
+    crs = np.array([t[1] for t in tab], bool)
+    y = grids[:, idx].astype(np.complex64)
+    scaling = 1.0
+    if power_scale:
+        rho_a = np.float32(math.pow(10.0, p_a / 20.0) * (1.0 if nports == 1 else math.sqrt(2)))
+        if rho_a != 0 and np.isfinite(rho_a):
+            scaling = float(rho_a)
+        rho_b = np.sqrt(np.float32(RHO_TABLE[0 if nports == 1 else 1][p_b]), dtype=np.float32)
+        if rho_b != 0 and rho_b != 1:
+            y[:, crs] = y[:, crs] * (np.float32(1) / rho_b)
+    h = ce[:, :, idx]
+    ntb = len(tbs)
+    codebook = pmi if ntb == 1 else pmi + 1
+    x, csi = ora.predecode(SCHEME[scheme], y, h, ntb, codebook, scaling, noise)
+    out = []
+    for q in range(ntb):
+        llr = ora.demod_s(MOD[Qm[q]], x[q])
+        llr = ora.sequence_apply_s(llr, ora.pdsch_seed(rnti, q, 2 * sf_idx, cell_id))
+        if csi_enable:
+            llr = ora.csi_correction(MOD[Qm[q]], csi[q], llr)
+        st = states[q] if states else None
+        ret, data, noi, avg, state = ora.dlsch_decode(tbs[q], Qm[q], rv[q], llr, max_iterations, st)
+        out.append(dict(ret=ret, data=data, avg=avg, llr=llr, state=state, nof_re=idx.size))
+    return out

@@ -44,6 +44,8 @@ struct ChestGpu {
   float2*     grid    = nullptr;  // host-synchronous path scratch
   float2*     ce      = nullptr;
   float*      stats   = nullptr;  // [rx][port][8]
+  float*      bstats  = nullptr;  // batch path: [sf][CHEST_STATS_PER_SF]
+  uint32_t    bstats_cap = 0;
   uint32_t    max_prb = 0;
   uint32_t    nrx     = 0;
   float       filter[8];
@@ -151,6 +153,7 @@ void srsran_chest_dl_free(srsran_chest_dl_t* q)
     hipFree(g->grid);
     hipFree(g->ce);
     hipFree(g->stats);
+    hipFree(g->bstats);
     delete g;
   }
   memset(q, 0, sizeof(*q));
@@ -363,42 +366,6 @@ int srsran_chest_dl_estimate(srsran_chest_dl_t* q, srsran_dl_sf_cfg_t* sf, cf_t*
 
 }  // extern "C"
 
-// Device-side fill of the four d_res values (noise_estimate, rsrp, rssi, cfo).
-namespace srsran_amd {
-__global__ void chest_finalize_kernel(const float* st, uint32_t np, uint32_t nrx, uint32_t nof_prb, float sz,
-                                      float* out)
-{
-  float n = 0, best = -1e9f, rssi = 0, cfo = 0;
-  for (uint32_t rx = 0; rx < nrx; rx++) {
-    float s = 0;
-    for (uint32_t p = 0; p < np; p++) {
-      s += st[(rx * np + p) * 8];
-    }
-    n += s / (float)np;
-    rssi += 4 * st[(rx * np) * 8 + 2] / (float)nof_prb / 12.0f;
-  }
-  for (uint32_t p = 0; p < np; p++) {
-    float s = 0;
-    for (uint32_t rx = 0; rx < nrx; rx++) {
-      s += st[(rx * np + p) * 8 + 1];
-    }
-    s /= (float)nrx;
-    best = s > best ? s : best;
-  }
-  for (int idx = (int)(nrx * np) - 1; idx >= 0; idx--) {
-    if ((uint32_t)idx % np < 2) {
-      const float ng = (float)(int)ceilf(144.0f * sz / 2048.0f);
-      cfo            = -atan2f(st[idx * 8 + 4], st[idx * 8 + 3]) * sz / (7.0f * (sz + ng)) / 2 / 3.14159265358979f;
-      break;
-    }
-  }
-  out[0] = n / (float)nrx;
-  out[1] = best;
-  out[2] = rssi / (float)nrx;
-  out[3] = cfo;
-}
-}  // namespace srsran_amd
-
 extern "C" int srsran_chest_dl_gpu_estimate(srsran_chest_dl_t* q,
                                             uint32_t           tti,
                                             const cf_t*        d_grid,
@@ -416,8 +383,59 @@ extern "C" int srsran_chest_dl_gpu_estimate(srsran_chest_dl_t* q,
   }
   if (d_res) {
     ChestGpu* g = (ChestGpu*)q->gpu;
-    hipLaunchKernelGGL(chest_finalize_kernel, dim3(1), dim3(1), 0, s, g->stats, q->cell.nof_ports,
-                       q->nof_rx_antennas, q->cell.nof_prb, (float)srsran_symbol_sz(q->cell.nof_prb), d_res);
+    chest_finalize_launch(g->stats, q->cell.nof_ports, q->nof_rx_antennas, q->cell.nof_prb,
+                          (float)srsran_symbol_sz(q->cell.nof_prb), d_res, 1, s);
   }
   return hipGetLastError() == hipSuccess ? SRSRAN_SUCCESS : SRSRAN_ERROR;
+}
+
+/* added: nsf subframes in one launch.  d_sf_idx[b] = tti % 10 of subframe b (device);
+ * d_grid + b * grid_sf_stride: nof_rx grids; d_ce + b * ce_sf_stride: [port][rx] rows of 12 * nof_prb
+ * (the AVERAGE estimate); d_res + 4 * b: noise_estimate, rsrp, rssi, cfo. */
+extern "C" int srsran_chest_dl_gpu_estimate_batch(srsran_chest_dl_t* q,
+                                                  const uint32_t*    d_sf_idx,
+                                                  uint32_t           nsf,
+                                                  const cf_t*        d_grid,
+                                                  size_t             grid_sf_stride,
+                                                  cf_t*              d_ce,
+                                                  size_t             ce_sf_stride,
+                                                  float*             d_res,
+                                                  void*              stream)
+{
+  if (!q || !q->gpu || !d_sf_idx || !d_grid || !d_ce || !d_res || q->cell.nof_prb == 0) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  ChestGpu* g = (ChestGpu*)q->gpu;
+  if (nsf > g->bstats_cap) {
+    hipFree(g->bstats);
+    g->bstats     = nullptr;
+    g->bstats_cap = 0;
+    if (hipMalloc((void**)&g->bstats, nsf * CHEST_STATS_PER_SF * sizeof(float)) != hipSuccess) {
+      return SRSRAN_ERROR;
+    }
+    g->bstats_cap = nsf;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  ChestArgs   a{};
+  a.grid           = (const float2*)d_grid;
+  a.pilots         = g->pilots;
+  a.sf_idx         = d_sf_idx;
+  a.grid_sf_stride = grid_sf_stride;
+  a.ce             = (float2*)d_ce;
+  a.ce_sf_stride   = ce_sf_stride;
+  a.stats          = g->bstats;
+  a.nof_prb        = q->cell.nof_prb;
+  a.cell_id        = q->cell.id;
+  a.nports         = q->cell.nof_ports;
+  a.nrx            = q->nof_rx_antennas;
+  a.ce_stride      = 12 * q->cell.nof_prb;
+  a.full_grid      = 0;
+  a.filter_len     = g->filter_len;
+  memcpy(a.filter, g->filter, sizeof(a.filter));
+  if (chest_launch(a, s, nsf) != hipSuccess ||
+      chest_finalize_launch(g->bstats, q->cell.nof_ports, q->nof_rx_antennas, q->cell.nof_prb,
+                            (float)srsran_symbol_sz(q->cell.nof_prb), d_res, nsf, s) != hipSuccess) {
+    return SRSRAN_ERROR;
+  }
+  return SRSRAN_SUCCESS;
 }

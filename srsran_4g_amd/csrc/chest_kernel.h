@@ -23,9 +23,20 @@ struct ChestArgs {
   float         filter[8]; // smoothing filter (srsran_chest_set_smooth_filter_gauss)
   uint32_t      filter_len;
   uint32_t      filter_auto; // Gauss order 4, stddev = 200 * noise of the (port, rx) (chest_dl.c:703-704)
+  // ---- batches of subframes (gridDim.y = nof subframes) ----
+  const uint32_t* sf_idx;     // [b] subframe index (tti % 10): pilots + sf_idx[b] * CHEST_PILOTS_PER_SF; null = as given
+  size_t          grid_sf_stride; // float2 between subframes of `grid`
+  size_t          ce_sf_stride;   // float2 between subframes of `ce`
 };
 
-hipError_t chest_launch(const ChestArgs& a, hipStream_t stream);
+static constexpr size_t CHEST_PILOTS_PER_SF = 2 * 4 * CHEST_MAX_NREF;  // float2 (both port pairs)
+static constexpr size_t CHEST_STATS_PER_SF  = 4 * 4 * 8;               // floats of stats per subframe
+
+hipError_t chest_launch(const ChestArgs& a, hipStream_t stream, uint32_t nsf = 1);
+// device-side reduction of the per-(rx, port) stats of nsf subframes into out[b][4] =
+// {noise_estimate, rsrp, rssi, cfo} (fill_res, chest_dl.c:962-986)
+hipError_t chest_finalize_launch(const float* stats, uint32_t np, uint32_t nrx, uint32_t nof_prb, float symbol_sz,
+                                 float* out, uint32_t nsf, hipStream_t stream);
 
 }  // namespace srsran_amd
 #endif

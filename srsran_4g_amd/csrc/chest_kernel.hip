@@ -72,11 +72,12 @@ __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
   __shared__ cx    avg[2 * CHEST_MAX_NREF];
   __shared__ float red[CH_THREADS / 64];
 
-  const uint32_t port = blockIdx.x / a.nrx, rx = blockIdx.x % a.nrx;
+  const uint32_t port = blockIdx.x / a.nrx, rx = blockIdx.x % a.nrx, b = blockIdx.y;
   const uint32_t tid  = threadIdx.x;
   const uint32_t nsym = port < 2 ? 4 : 2, nref = 2 * a.nof_prb, np = nsym * nref, nre = 12 * a.nof_prb;
-  const float2*  in   = a.grid + (size_t)rx * 14 * nre;
-  const float2*  pil  = a.pilots + (size_t)(port / 2) * 4 * CHEST_MAX_NREF;
+  const float2*  in   = a.grid + b * a.grid_sf_stride + (size_t)rx * 14 * nre;
+  const float2*  pil  = a.pilots + (a.sf_idx ? a.sf_idx[b] * CHEST_PILOTS_PER_SF : 0) +
+                      (size_t)(port / 2) * 4 * CHEST_MAX_NREF;
   const uint32_t fidx0 = (crs_v(port, 0) + a.cell_id % 6) % 6;
 
   // ---- LS estimates at the CRS and RSRP / RSSI ----
@@ -216,7 +217,7 @@ __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
   const uint32_t step = nsym > 1 ? 3 : 6;
   const uint32_t off  = nsym > 1 ? a.cell_id % 3 : fidx0;
   const float    rM   = (float)1 / step;
-  float2*        ce   = a.ce + (size_t)(port * a.nrx + rx) * a.ce_stride;
+  float2*        ce   = a.ce + b * a.ce_sf_stride + (size_t)(port * a.nrx + rx) * a.ce_stride;
   for (uint32_t j = tid; j < nre; j += CH_THREADS) {
     cx v;
     if (j < off) {
@@ -239,7 +240,7 @@ __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
     }
   }
   if (tid == 0) {
-    float* s = a.stats + (size_t)(rx * a.nports + port) * 8;
+    float* s = a.stats + b * CHEST_STATS_PER_SF + (size_t)(rx * a.nports + port) * 8;
     s[0]     = noise;
     s[1]     = rsrp;
     s[2]     = rssi;
@@ -248,9 +249,63 @@ __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
   }
 }
 
-hipError_t chest_launch(const ChestArgs& a, hipStream_t stream)
+hipError_t chest_launch(const ChestArgs& a, hipStream_t stream, uint32_t nsf)
 {
-  hipLaunchKernelGGL(chest_kernel, dim3(a.nports * a.nrx), dim3(CH_THREADS), 0, stream, a);
+  if (nsf == 0) {
+    return hipSuccess;
+  }
+  hipLaunchKernelGGL(chest_kernel, dim3(a.nports * a.nrx, nsf), dim3(CH_THREADS), 0, stream, a);
+  return hipGetLastError();
+}
+
+// one thread per subframe
+__global__ void chest_finalize_kernel(const float* stats, uint32_t np, uint32_t nrx, uint32_t nof_prb, float sz,
+                                      float* out, uint32_t nsf)
+{
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nsf) {
+    return;
+  }
+  const float* st = stats + b * CHEST_STATS_PER_SF;
+  float        n = 0, best = -1e9f, rssi = 0, cfo = 0;
+  for (uint32_t rx = 0; rx < nrx; rx++) {
+    float s = 0;
+    for (uint32_t p = 0; p < np; p++) {
+      s += st[(rx * np + p) * 8];
+    }
+    n += s / (float)np;
+    rssi += 4 * st[(rx * np) * 8 + 2] / (float)nof_prb / 12.0f;
+  }
+  for (uint32_t p = 0; p < np; p++) {
+    float s = 0;
+    for (uint32_t rx = 0; rx < nrx; rx++) {
+      s += st[(rx * np + p) * 8 + 1];
+    }
+    s /= (float)nrx;
+    best = s > best ? s : best;
+  }
+  for (int idx = (int)(nrx * np) - 1; idx >= 0; idx--) {  // chest_estimate_cfo: last (rx, port<2) wins
+    if ((uint32_t)idx % np < 2) {
+      const float ng = (float)(int)ceilf(144.0f * sz / 2048.0f);
+      cfo            = -atan2f(st[idx * 8 + 4], st[idx * 8 + 3]) * sz / (7.0f * (sz + ng)) / 2 / 3.14159265358979f;
+      break;
+    }
+  }
+  float* o = out + 4 * b;
+  o[0]     = n / (float)nrx;
+  o[1]     = best;
+  o[2]     = rssi / (float)nrx;
+  o[3]     = cfo;
+}
+
+hipError_t chest_finalize_launch(const float* stats, uint32_t np, uint32_t nrx, uint32_t nof_prb, float symbol_sz,
+                                 float* out, uint32_t nsf, hipStream_t stream)
+{
+  if (nsf == 0) {
+    return hipSuccess;
+  }
+  hipLaunchKernelGGL(chest_finalize_kernel, dim3((nsf + 63) / 64), dim3(64), 0, stream, stats, np, nrx, nof_prb,
+                     symbol_sz, out, nsf);
   return hipGetLastError();
 }
 

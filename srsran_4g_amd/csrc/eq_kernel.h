@@ -18,9 +18,17 @@ struct PredArgs {
   uint32_t      n;
   float         norm;
   float         noise;
+  // ---- fused PDSCH extraction (srsran_pdsch_get, pdsch.c:838-853); all optional ----
+  const uint32_t* idx;       // RE k reads grid index idx[k] & 0x7fffffff (nullptr: k itself)
+  uint32_t        ce_row;    // > 0: h[p][r] is one AVERAGE row, indexed by (grid index % ce_row)
+  const float*    noise_ptr; // device noise estimate (overrides `noise`)
+  float           rho_b_inv; // y scale on CRS-bearing symbols (bit 31 of idx), 1 = none
 };
 
 hipError_t predecode_launch(const PredArgs& a, hipStream_t stream);
+// nitems descriptors (device array), all with the same scheme; max_n = largest n
+hipError_t predecode_batch_launch(const PredArgs* d_items, uint32_t nitems, int scheme, uint32_t max_n,
+                                  hipStream_t stream);
 
 }  // namespace srsran_amd
 #endif

@@ -76,20 +76,36 @@ __device__ __forceinline__ void wave_max_atomic(uint32_t* dst, float v, bool val
 static constexpr int EQ_THREADS = 256;
 
 template <int SCHEME>
-__global__ __launch_bounds__(EQ_THREADS) void predecode_kernel(PredArgs a)
+__device__ __forceinline__ void predecode_item(const PredArgs& a, uint32_t k)
 {
-  const uint32_t k     = blockIdx.x * EQ_THREADS + threadIdx.x;
   const bool     valid = k < a.n;
   const uint32_t kk    = valid ? k : 0;
+  // grid / estimate positions of RE kk (fused srsran_pdsch_get)
+  uint32_t gy = kk, gh = kk;
+  float    ys = 1.0f;
+  if (a.idx) {
+    const uint32_t e = a.idx[kk];
+    gy               = e & 0x7fffffffu;
+    gh               = a.ce_row ? gy % a.ce_row : gy;
+    ys               = (e >> 31) ? a.rho_b_inv : 1.0f;
+  }
+  const float noise = a.noise_ptr ? *a.noise_ptr : a.noise;
+  auto        Y     = [&](int r) -> cpx {
+    cpx v = ld(a.y[r], gy);
+    if (ys != 1.0f) {
+      v = cscale(v, ys);
+    }
+    return v;
+  };
   if constexpr (SCHEME == 0) {
     cpx   r  = {0.f, 0.f};
     float hh = 0.f;
     for (int p = 0; p < a.nrx; p++) {
-      const cpx hv = ld(a.h[0][p], kk);
-      r            = cadd(r, cmul(ld(a.y[p], kk), cconj(hv)));
+      const cpx hv = ld(a.h[0][p], gh);
+      r            = cadd(r, cmul(Y(p), cconj(hv)));
       hh += hv.r * hv.r + hv.i * hv.i;
     }
-    const float csi = hh + a.noise;
+    const float csi = hh + noise;
     const cpx   t   = cscale(r, a.norm);
     if (valid) {
       a.csi[0][k] = csi;
@@ -99,7 +115,7 @@ __global__ __launch_bounds__(EQ_THREADS) void predecode_kernel(PredArgs a)
       wave_max_atomic(&a.csi_max[0], csi, valid);
     }
   } else {
-    const cpx p0 = ld(a.h[0][0], kk), p1 = ld(a.h[0][1], kk), q0 = ld(a.h[1][0], kk), q1 = ld(a.h[1][1], kk);
+    const cpx p0 = ld(a.h[0][0], gh), p1 = ld(a.h[0][1], gh), q0 = ld(a.h[1][0], gh), q1 = ld(a.h[1][1], gh);
     cpx       h00, h01, h10, h11;
     if constexpr (SCHEME == 3) {  // CDD: the large-delay precoder alternates with the RE index
       if ((kk & 1) == 0) {
@@ -133,7 +149,7 @@ __global__ __launch_bounds__(EQ_THREADS) void predecode_kernel(PredArgs a)
     }
     cpx   x0, x1;
     float c0, c1;
-    mmse_csi(ld(a.y[0], kk), ld(a.y[1], kk), h00, h01, h10, h11, x0, x1, c0, c1, a.noise, a.norm);
+    mmse_csi(Y(0), Y(1), h00, h01, h10, h11, x0, x1, c0, c1, noise, a.norm);
     if (valid) {
       a.x[0][k]   = make_float2(x0.r, x0.i);
       a.x[1][k]   = make_float2(x1.r, x1.i);
@@ -145,6 +161,46 @@ __global__ __launch_bounds__(EQ_THREADS) void predecode_kernel(PredArgs a)
       wave_max_atomic(&a.csi_max[1], c1, valid);
     }
   }
+}
+
+template <int SCHEME>
+__global__ __launch_bounds__(EQ_THREADS) void predecode_kernel(PredArgs a)
+{
+  predecode_item<SCHEME>(a, blockIdx.x * EQ_THREADS + threadIdx.x);
+}
+
+template <int SCHEME>
+__global__ __launch_bounds__(EQ_THREADS) void predecode_batch_kernel(const PredArgs* __restrict__ items)
+{
+  const PredArgs& a = items[blockIdx.y];
+  const uint32_t  k = blockIdx.x * EQ_THREADS + threadIdx.x;
+  if (blockIdx.x * EQ_THREADS >= a.n) {
+    return;  // whole block past this item's end (uniform exit keeps the wave reductions intact)
+  }
+  predecode_item<SCHEME>(a, k);
+}
+
+hipError_t predecode_batch_launch(const PredArgs* d_items, uint32_t nitems, int scheme, uint32_t max_n,
+                                  hipStream_t stream)
+{
+  if (nitems == 0 || max_n == 0) {
+    return hipSuccess;
+  }
+  const dim3 grid((max_n + EQ_THREADS - 1) / EQ_THREADS, nitems);
+  switch (scheme) {
+    case 0:
+      hipLaunchKernelGGL(predecode_batch_kernel<0>, grid, dim3(EQ_THREADS), 0, stream, d_items);
+      break;
+    case 2:
+      hipLaunchKernelGGL(predecode_batch_kernel<2>, grid, dim3(EQ_THREADS), 0, stream, d_items);
+      break;
+    case 3:
+      hipLaunchKernelGGL(predecode_batch_kernel<3>, grid, dim3(EQ_THREADS), 0, stream, d_items);
+      break;
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
 }
 
 hipError_t predecode_launch(const PredArgs& a, hipStream_t stream)

@@ -15,6 +15,21 @@ hipError_t gold_tables_init();
 hipError_t llr_launch(int mod, const float* d_sym, uint32_t nsym, int scramble, uint32_t seed, uint32_t bit0,
                       const float* d_csi, const float* d_csi_max, int16_t* d_llr, hipStream_t stream);
 
+// One demap + descramble + CSI job of a batch (PDSCH codeword of one subframe).
+struct LlrItem {
+  const float*  sym;      // interleaved re/im symbols
+  const float*  csi;      // optional CSI per symbol
+  const float*  csi_max;  // max CSI (device), required with csi
+  int16_t*      llr;
+  uint32_t      n;        // symbols
+  uint32_t      seed;
+  uint32_t      bit0;
+  int           scramble;
+};
+// nitems items of one modulation (device array); max_n = largest n
+hipError_t llr_batch_launch(int mod, const LlrItem* d_items, uint32_t nitems, uint32_t max_n, int any_scramble,
+                            hipStream_t stream);
+
 // out[i] = c(i) ? -in[i] : in[i] (int16 wrap) for the Gold sequence of `seed`.
 hipError_t seq_apply_launch(const int16_t* d_in, int16_t* d_out, uint32_t len, uint32_t seed, hipStream_t stream);
 

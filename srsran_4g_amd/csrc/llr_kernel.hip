@@ -265,12 +265,11 @@ __device__ __forceinline__ void csi_correct(int16_t* o, uint32_t s, const float*
 }
 
 template <int MOD>
-__global__ __launch_bounds__(LLR_THREADS) void llr_kernel(const float2* __restrict__ sym, uint32_t n, int scramble,
-                                                          uint32_t seed, uint32_t bit0, const float* __restrict__ csi,
-                                                          const float* __restrict__ csi_max, int16_t* __restrict__ llr)
+__device__ __forceinline__ void llr_body(const float2* __restrict__ sym, uint32_t n, int scramble, uint32_t seed,
+                                         uint32_t bit0, const float* __restrict__ csi,
+                                         const float* __restrict__ csi_max, int16_t* __restrict__ llr, uint32_t s0)
 {
-  constexpr int  Q  = Qm<MOD>::v;
-  const uint32_t s0 = (blockIdx.x * LLR_THREADS + threadIdx.x) * SPT;
+  constexpr int Q = Qm<MOD>::v;
   if (s0 >= n) {
     return;
   }
@@ -322,6 +321,57 @@ __global__ __launch_bounds__(LLR_THREADS) void llr_kernel(const float2* __restri
       dst[b] = o[b];
     }
   }
+}
+
+template <int MOD>
+__global__ __launch_bounds__(LLR_THREADS) void llr_kernel(const float2* __restrict__ sym, uint32_t n, int scramble,
+                                                          uint32_t seed, uint32_t bit0, const float* __restrict__ csi,
+                                                          const float* __restrict__ csi_max, int16_t* __restrict__ llr)
+{
+  llr_body<MOD>(sym, n, scramble, seed, bit0, csi, csi_max, llr, (blockIdx.x * LLR_THREADS + threadIdx.x) * SPT);
+}
+
+template <int MOD>
+__global__ __launch_bounds__(LLR_THREADS) void llr_batch_kernel(const LlrItem* __restrict__ items)
+{
+  const LlrItem& it = items[blockIdx.y];
+  llr_body<MOD>(reinterpret_cast<const float2*>(it.sym), it.n, it.scramble, it.seed, it.bit0, it.csi, it.csi_max,
+                it.llr, (blockIdx.x * LLR_THREADS + threadIdx.x) * SPT);
+}
+
+hipError_t llr_batch_launch(int mod, const LlrItem* d_items, uint32_t nitems, uint32_t max_n, int any_scramble,
+                            hipStream_t stream)
+{
+  if (nitems == 0 || max_n == 0) {
+    return hipSuccess;
+  }
+  if (any_scramble) {
+    hipError_t e = gold_tables_init();
+    if (e != hipSuccess) {
+      return e;
+    }
+  }
+  const dim3 grid((max_n + LLR_THREADS * SPT - 1) / (LLR_THREADS * SPT), nitems);
+  switch (mod) {
+    case 0:
+      hipLaunchKernelGGL(llr_batch_kernel<0>, grid, dim3(LLR_THREADS), 0, stream, d_items);
+      break;
+    case 1:
+      hipLaunchKernelGGL(llr_batch_kernel<1>, grid, dim3(LLR_THREADS), 0, stream, d_items);
+      break;
+    case 2:
+      hipLaunchKernelGGL(llr_batch_kernel<2>, grid, dim3(LLR_THREADS), 0, stream, d_items);
+      break;
+    case 3:
+      hipLaunchKernelGGL(llr_batch_kernel<3>, grid, dim3(LLR_THREADS), 0, stream, d_items);
+      break;
+    case 4:
+      hipLaunchKernelGGL(llr_batch_kernel<4>, grid, dim3(LLR_THREADS), 0, stream, d_items);
+      break;
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
 }
 
 hipError_t llr_launch(int mod, const float* d_sym, uint32_t nsym, int scramble, uint32_t seed, uint32_t bit0,

@@ -1,0 +1,501 @@
+// srsran_4g_amd/csrc/pdsch_api.cpp -- srsran_pdsch_t on the GPU (include/srsran_ue_dl.h).
+//
+// srsran_pdsch_decode (pdsch.c:788-958) as three device passes per batch of subframes:
+//   1. predecode_batch  srsran_pdsch_get (pdsch.c:246-254) fused as a gather through the RE
+//                       table, apply_power_allocation's rho_b (pdsch.c:485-521) fused as a scale
+//                       of CRS-symbol REs, srsran_predecoding_type MMSE + CSI (precoding.c:1866)
+//   2. llr_batch        srsran_pdsch_codeword_decode's demod_soft_demodulate_s, sequence_pdsch_
+//                       apply_s and csi_correction (pdsch.c:683-737) for every codeword
+//   3. DL-SCH batch     srsran_dlsch_decode2 (sch.c:580-609) of every TB (sch_api.cpp)
+// The host-synchronous srsran_pdsch_decode uploads the caller's grids / estimates, runs 1-2 and
+// decodes each codeword with srsran_dlsch_decode2 semantics on the device LLRs.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "llr_kernel.h"
+#include "pdsch_internal.h"
+
+using namespace srsran_amd;
+
+namespace {
+
+constexpr uint32_t kMaxQm = 8;
+
+struct Table {
+  uint32_t* d   = nullptr;
+  uint32_t  len = 0;
+};
+
+struct PdschGpu {
+  hipStream_t                  stream  = nullptr;  // host-synchronous path
+  hipEvent_t                   staged  = nullptr;  // descriptor upload finished (pinned staging reusable)
+  char*                        h_stage = nullptr;
+  char*                        d_stage = nullptr;
+  size_t                       stage_cap = 0;
+  char*                        d_work    = nullptr;
+  size_t                       work_cap  = 0;
+  float2*                      d_in      = nullptr;  // host-synchronous path: grids + estimates
+  size_t                       in_cap    = 0;
+  std::map<std::string, Table> tables;
+};
+
+bool grow_dev(void** p, size_t* cap, size_t need)
+{
+  if (*cap >= need) {
+    return true;
+  }
+  if (*p) {
+    hipDeviceSynchronize();  // buffers may still be in use by enqueued work
+    hipFree(*p);
+  }
+  *p   = nullptr;
+  *cap = 0;
+  need = std::max(need, (size_t)65536);
+  if (hipMalloc(p, need) != hipSuccess) {
+    return false;
+  }
+  *cap = need;
+  return true;
+}
+
+bool grow_stage(PdschGpu* g, size_t need)
+{
+  if (g->stage_cap >= need) {
+    return true;
+  }
+  hipDeviceSynchronize();
+  hipHostFree(g->h_stage);
+  hipFree(g->d_stage);
+  g->h_stage = nullptr;
+  g->d_stage = nullptr;
+  g->stage_cap = 0;
+  need = std::max(need, (size_t)65536);
+  if (hipHostMalloc((void**)&g->h_stage, need) != hipSuccess || hipMalloc((void**)&g->d_stage, need) != hipSuccess) {
+    return false;
+  }
+  g->stage_cap = need;
+  return true;
+}
+
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// RE table of (grant, CFI, subframe) on the device, built once (pdsch_map.cpp)
+const Table* get_table(srsran_pdsch_t* q, PdschGpu* g, const srsran_pdsch_grant_t& gr, uint32_t lstart,
+                       uint32_t sf_idx)
+{
+  std::string key;
+  key.reserve(2 * q->cell.nof_prb + 16);
+  for (uint32_t s = 0; s < 2; s++) {
+    for (uint32_t n = 0; n < q->cell.nof_prb; n++) {
+      key.push_back(gr.prb_idx[s][n] ? '1' : '0');
+    }
+    key.push_back((char)gr.nof_symb_slot[s]);
+  }
+  key.push_back((char)lstart);
+  key.push_back((char)sf_idx);
+  auto it = g->tables.find(key);
+  if (it != g->tables.end()) {
+    return &it->second;
+  }
+  if (g->tables.size() >= 512) {  // bound the cache (grants change with every scheduling decision)
+    hipDeviceSynchronize();
+    for (auto& kv : g->tables) {
+      hipFree(kv.second.d);
+    }
+    g->tables.clear();
+  }
+  const std::vector<uint32_t> t = pdsch_re_table(q->cell, gr, lstart, sf_idx);
+  Table                       tb;
+  tb.len = (uint32_t)t.size();
+  if (hipMalloc((void**)&tb.d, std::max<size_t>(t.size(), 1) * sizeof(uint32_t)) != hipSuccess ||
+      hipMemcpy(tb.d, t.data(), t.size() * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) {
+    hipFree(tb.d);
+    return nullptr;
+  }
+  return &(g->tables[key] = tb);
+}
+
+// One decoded codeword of the batch
+struct Cw {
+  uint32_t sf, tb, cw, Qm, nbits;
+  int      mod;
+};
+
+// Enqueue predecode + LLR of nsf subframes; fills `cws` and the per-codeword LLR pointers.
+// Scratch layout (d_work): x [nsf][2][max_re] float2 | csi [nsf][2][max_re] f32 | csi_max [nsf][2] |
+// llr [nsf][2][max_re * 8] int16
+int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sfs, hipStream_t s,
+                std::vector<Cw>& cws, std::vector<int16_t*>& llr)
+{
+  PdschGpu*      g   = (PdschGpu*)q->gpu;
+  const uint32_t nrx = q->nof_rx_antennas, np = q->cell.nof_ports, nre = 12 * q->cell.nof_prb;
+  std::vector<const Table*> tabs(nsf);
+  std::vector<PredArgs>     pa(nsf);
+  uint32_t                  max_re = 0;
+  cws.clear();
+  for (uint32_t b = 0; b < nsf; b++) {
+    const srsran_pdsch_gpu_sf_t& f = sfs[b];
+    if (!f.cfg || !f.d_grid || !f.d_ce || f.cfi < 1 || f.cfi > 3) {
+      return SRSRAN_ERROR_INVALID_INPUTS;
+    }
+    const srsran_pdsch_grant_t& gr = f.cfg->grant;
+    if (gr.nof_layers == 0 || gr.nof_layers > SRSRAN_MAX_LAYERS) {
+      return SRSRAN_ERROR_OUT_OF_BOUNDS;
+    }
+    if (gr.nof_layers != gr.nof_tb || gr.nof_tb < 1 || gr.nof_tb > 2) {
+      fprintf(stderr, "[srsran_pdsch] unsupported: %u codewords on %u layers\n", gr.nof_tb, gr.nof_layers);
+      return SRSRAN_ERROR;
+    }
+    const uint32_t lstart = f.cfi + (q->cell.nof_prb < 10 ? 1 : 0);  // SRSRAN_NOF_CTRL_SYMBOLS
+    tabs[b]               = get_table(q, g, gr, lstart, f.tti % 10);
+    if (!tabs[b]) {
+      return SRSRAN_ERROR;
+    }
+    if (tabs[b]->len != gr.nof_re) {
+      fprintf(stderr, "[srsran_pdsch] Error expecting %u symbols but got %u\n", gr.nof_re, tabs[b]->len);
+      return SRSRAN_ERROR;
+    }
+    max_re = std::max(max_re, gr.nof_re);
+    // power allocation (pdsch.c:485-521, 795-801)
+    float scaling = 1.0f, rho_b_inv = 1.0f;
+    if (f.cfg->power_scale) {
+      const float rho_a = (float)(powf(10.0f, f.cfg->p_a / 20.0f) * (np == 1 ? 1.0 : M_SQRT2));
+      if (rho_a != 0.0f && std::isnormal(rho_a)) {
+        scaling = rho_a;
+      }
+      static const float kRatio[2][4] = {{1.0f, 4.0f / 5.0f, 3.0f / 5.0f, 2.0f / 5.0f},
+                                         {5.0f / 4.0f, 1.0f, 3.0f / 4.0f, 1.0f / 2.0f}};
+      if (f.cfg->p_b > 3) {
+        return SRSRAN_ERROR_INVALID_INPUTS;
+      }
+      const float rho_b = sqrtf(kRatio[np == 1 ? 0 : 1][f.cfg->p_b]);
+      if (rho_b != 0.0f && rho_b != 1.0f) {
+        rho_b_inv = 1.0f / rho_b;
+      }
+    }
+    PredArgs&      a        = pa[b];
+    const uint32_t codebook = gr.nof_tb == 1 ? gr.pmi : gr.pmi + 1;
+    if (!pred_setup(a, (int)nrx, (int)np, (int)gr.nof_layers, (int)codebook, (int)gr.tx_scheme, scaling)) {
+      fprintf(stderr, "[srsran_pdsch] unsupported: scheme %d, %u ports, %u rx, %u layers\n", (int)gr.tx_scheme, np,
+              nrx, gr.nof_layers);
+      return SRSRAN_ERROR;
+    }
+    a.n         = gr.nof_re;
+    a.noise     = f.cfg->decoder_type == SRSRAN_MIMO_DECODER_ZF ? 0.0f : f.noise;
+    a.noise_ptr = f.cfg->decoder_type == SRSRAN_MIMO_DECODER_ZF ? nullptr : f.d_noise;
+    a.rho_b_inv = rho_b_inv;
+    a.ce_row    = f.ce_full ? 0 : nre;
+    const size_t ce_len = f.ce_full ? (size_t)14 * nre : nre;
+    for (uint32_t r = 0; r < nrx; r++) {
+      a.y[r] = (const float2*)f.d_grid + (size_t)r * 14 * nre;
+      for (uint32_t p = 0; p < np; p++) {
+        a.h[p][r] = (const float2*)f.d_ce + (size_t)(p * nrx + r) * ce_len;
+      }
+    }
+    for (uint32_t tb = 0; tb < SRSRAN_MAX_CODEWORDS; tb++) {
+      const srsran_ra_tb_t& t = gr.tb[tb];
+      if (!t.enabled) {
+        continue;
+      }
+      const uint32_t Qm = srsran_mod_bits_x_symbol(t.mod);
+      if (Qm == 0 || t.cw_idx >= gr.nof_tb || t.nof_bits != gr.nof_re * Qm) {
+        fprintf(stderr, "[srsran_pdsch] unsupported codeword %u: Qm %u, %u bits for %u REs\n", tb, Qm, t.nof_bits,
+                gr.nof_re);
+        return SRSRAN_ERROR;
+      }
+      cws.push_back(Cw{b, tb, t.cw_idx, Qm, t.nof_bits, (int)t.mod});
+    }
+  }
+  if (max_re == 0) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  // scratch
+  const size_t x_sz = align256((size_t)nsf * 2 * max_re * sizeof(float2));
+  const size_t c_sz = align256((size_t)nsf * 2 * max_re * sizeof(float));
+  const size_t m_sz = align256((size_t)nsf * 2 * sizeof(float));
+  const size_t e_sz = align256((size_t)nsf * 2 * max_re * kMaxQm * sizeof(int16_t));
+  if (!grow_dev((void**)&g->d_work, &g->work_cap, x_sz + c_sz + m_sz + e_sz)) {
+    return SRSRAN_ERROR;
+  }
+  float2*  d_x   = (float2*)g->d_work;
+  float*   d_csi = (float*)(g->d_work + x_sz);
+  float*   d_max = (float*)(g->d_work + x_sz + c_sz);
+  int16_t* d_e   = (int16_t*)(g->d_work + x_sz + c_sz + m_sz);
+  for (uint32_t b = 0; b < nsf; b++) {
+    PredArgs& a = pa[b];
+    a.idx       = tabs[b]->d;
+    for (int l = 0; l < 2; l++) {
+      a.x[l]   = d_x + ((size_t)b * 2 + l) * max_re;
+      a.csi[l] = d_csi + ((size_t)b * 2 + l) * max_re;
+    }
+    a.csi_max = (uint32_t*)(d_max + 2 * b);
+  }
+  // LLR descriptors, grouped by modulation
+  std::vector<LlrItem> li(cws.size());
+  llr.assign(cws.size(), nullptr);
+  for (size_t i = 0; i < cws.size(); i++) {
+    const Cw&                    c = cws[i];
+    const srsran_pdsch_gpu_sf_t& f = sfs[c.sf];
+    LlrItem&                     it = li[i];
+    it.sym      = (const float*)(d_x + ((size_t)c.sf * 2 + c.cw) * max_re);
+    it.csi      = f.cfg->csi_enable ? d_csi + ((size_t)c.sf * 2 + c.cw) * max_re : nullptr;
+    it.csi_max  = f.cfg->csi_enable ? d_max + 2 * c.sf + c.cw : nullptr;
+    it.llr      = d_e + ((size_t)c.sf * 2 + c.tb) * max_re * kMaxQm;
+    it.n        = f.cfg->grant.nof_re;
+    it.seed     = pdsch_seed(f.cfg->rnti, (int)c.cw, 2 * (f.tti % 10), q->cell.id);
+    it.bit0     = 0;
+    it.scramble = 1;
+    llr[i]      = it.llr;
+  }
+  std::vector<uint32_t> order_p(nsf), order_l(cws.size());
+  for (uint32_t i = 0; i < nsf; i++) {
+    order_p[i] = i;
+  }
+  for (uint32_t i = 0; i < cws.size(); i++) {
+    order_l[i] = i;
+  }
+  std::stable_sort(order_p.begin(), order_p.end(), [&](uint32_t x, uint32_t y) { return pa[x].scheme < pa[y].scheme; });
+  std::stable_sort(order_l.begin(), order_l.end(), [&](uint32_t x, uint32_t y) { return cws[x].mod < cws[y].mod; });
+  const size_t pa_bytes = align256(nsf * sizeof(PredArgs));
+  const size_t li_bytes = align256(std::max<size_t>(cws.size(), 1) * sizeof(LlrItem));
+  if (hipEventSynchronize(g->staged) != hipSuccess || !grow_stage(g, pa_bytes + li_bytes)) {
+    return SRSRAN_ERROR;
+  }
+  PredArgs* hp = (PredArgs*)g->h_stage;
+  LlrItem*  hl = (LlrItem*)(g->h_stage + pa_bytes);
+  for (uint32_t i = 0; i < nsf; i++) {
+    hp[i] = pa[order_p[i]];
+  }
+  for (uint32_t i = 0; i < cws.size(); i++) {
+    hl[i] = li[order_l[i]];
+  }
+  hipMemcpyAsync(g->d_stage, g->h_stage, pa_bytes + li_bytes, hipMemcpyHostToDevice, s);
+  hipEventRecord(g->staged, s);
+  hipMemsetAsync(d_max, 0, (size_t)nsf * 2 * sizeof(float), s);
+  const PredArgs* dp = (const PredArgs*)g->d_stage;
+  const LlrItem*  dl = (const LlrItem*)(g->d_stage + pa_bytes);
+  for (uint32_t i = 0; i < nsf;) {  // one launch per predecoder scheme
+    uint32_t j = i, mx = 0;
+    while (j < nsf && hp[j].scheme == hp[i].scheme) {
+      mx = std::max(mx, hp[j].n);
+      j++;
+    }
+    if (predecode_batch_launch(dp + i, j - i, hp[i].scheme, mx, s) != hipSuccess) {
+      return SRSRAN_ERROR;
+    }
+    i = j;
+  }
+  for (uint32_t i = 0; i < cws.size();) {  // one launch per modulation
+    uint32_t j = i, mx = 0;
+    while (j < cws.size() && cws[order_l[j]].mod == cws[order_l[i]].mod) {
+      mx = std::max(mx, hl[j].n);
+      j++;
+    }
+    if (llr_batch_launch(cws[order_l[i]].mod, dl + i, j - i, mx, 1, s) != hipSuccess) {
+      return SRSRAN_ERROR;
+    }
+    i = j;
+  }
+  return SRSRAN_SUCCESS;
+}
+
+}  // namespace
+
+extern "C" {
+
+int srsran_pdsch_init_ue(srsran_pdsch_t* q, uint32_t max_prb, uint32_t nof_rx_antennas)
+{
+  if (!q || max_prb == 0 || max_prb > SRSRAN_MAX_PRB || nof_rx_antennas == 0 || nof_rx_antennas > SRSRAN_MAX_PORTS) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  memset(q, 0, sizeof(*q));
+  q->nof_rx_antennas = nof_rx_antennas;
+  q->max_re          = max_prb * 14 * SRSRAN_NRE;
+  q->is_ue           = true;
+  if (gold_tables_init() != hipSuccess || srsran_sch_init(&q->dl_sch)) {
+    fprintf(stderr, "[srsran_pdsch] no HIP device available\n");
+    return SRSRAN_ERROR;
+  }
+  PdschGpu* g = new PdschGpu();
+  q->gpu      = g;
+  if (hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&g->staged, hipEventDisableTiming) != hipSuccess || !grow_stage(g, 65536)) {
+    srsran_pdsch_free(q);
+    return SRSRAN_ERROR;
+  }
+  return SRSRAN_SUCCESS;
+}
+
+void srsran_pdsch_free(srsran_pdsch_t* q)
+{
+  if (!q) {
+    return;
+  }
+  PdschGpu* g = (PdschGpu*)q->gpu;
+  if (g) {
+    hipDeviceSynchronize();
+    for (auto& kv : g->tables) {
+      hipFree(kv.second.d);
+    }
+    hipFree(g->d_work);
+    hipFree(g->d_in);
+    hipFree(g->d_stage);
+    hipHostFree(g->h_stage);
+    if (g->staged) {
+      hipEventDestroy(g->staged);
+    }
+    if (g->stream) {
+      hipStreamDestroy(g->stream);
+    }
+    delete g;
+  }
+  srsran_sch_free(&q->dl_sch);
+  memset(q, 0, sizeof(*q));
+}
+
+int srsran_pdsch_enable_coworker(srsran_pdsch_t* q) { return q ? SRSRAN_SUCCESS : SRSRAN_ERROR_INVALID_INPUTS; }
+
+int srsran_pdsch_set_cell(srsran_pdsch_t* q, srsran_cell_t cell)
+{
+  if (!q || !q->gpu || cell.nof_prb == 0 || cell.nof_prb > SRSRAN_MAX_PRB || cell.nof_ports == 0 ||
+      cell.nof_ports > 2 || cell.id > 503) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  if (cell.cp != SRSRAN_CP_NORM || cell.frame_type != SRSRAN_FDD) {
+    fprintf(stderr, "[srsran_pdsch] only normal-CP FDD cells are provided\n");
+    return SRSRAN_ERROR;
+  }
+  PdschGpu* g = (PdschGpu*)q->gpu;
+  hipDeviceSynchronize();
+  for (auto& kv : g->tables) {
+    hipFree(kv.second.d);
+  }
+  g->tables.clear();
+  q->cell   = cell;
+  q->max_re = cell.nof_prb * 14 * SRSRAN_NRE;
+  return SRSRAN_SUCCESS;
+}
+
+int srsran_pdsch_decode(srsran_pdsch_t*        q,
+                        srsran_dl_sf_cfg_t*    sf,
+                        srsran_pdsch_cfg_t*    cfg,
+                        srsran_chest_dl_res_t* channel,
+                        cf_t*                  sf_symbols[SRSRAN_MAX_PORTS],
+                        srsran_pdsch_res_t     data[SRSRAN_MAX_CODEWORDS])
+{
+  if (!q || !q->gpu || !sf || !cfg || !channel || !sf_symbols || !data) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  if (q->llr_is_8bit || q->dl_sch.llr_is_8bit) {
+    fprintf(stderr, "[srsran_pdsch] 8-bit LLRs are not provided\n");
+    return SRSRAN_ERROR;
+  }
+  PdschGpu*      g   = (PdschGpu*)q->gpu;
+  const uint32_t nrx = q->nof_rx_antennas, np = q->cell.nof_ports, nsym = 14 * 12 * q->cell.nof_prb;
+  if (cfg->max_nof_iterations) {
+    srsran_sch_set_max_noi(&q->dl_sch, cfg->max_nof_iterations);
+  }
+  if (!grow_dev((void**)&g->d_in, &g->in_cap, (size_t)(nrx + np * nrx) * nsym * sizeof(float2))) {
+    return SRSRAN_ERROR;
+  }
+  for (uint32_t r = 0; r < nrx; r++) {
+    if (!sf_symbols[r]) {
+      return SRSRAN_ERROR_INVALID_INPUTS;
+    }
+    hipMemcpyAsync(g->d_in + (size_t)r * nsym, sf_symbols[r], nsym * sizeof(cf_t), hipMemcpyHostToDevice, g->stream);
+    for (uint32_t p = 0; p < np; p++) {
+      hipMemcpyAsync(g->d_in + (size_t)(nrx + p * nrx + r) * nsym, channel->ce[p][r], nsym * sizeof(cf_t),
+                     hipMemcpyHostToDevice, g->stream);
+    }
+  }
+  srsran_pdsch_gpu_sf_t f;
+  memset(&f, 0, sizeof(f));
+  f.cfg     = cfg;
+  f.tti     = sf->tti;
+  f.cfi     = sf->cfi;
+  f.d_grid  = (const cf_t*)g->d_in;
+  f.d_ce    = (const cf_t*)(g->d_in + (size_t)nrx * nsym);
+  f.ce_full = 1;
+  f.noise   = channel->noise_estimate;
+  std::vector<Cw>       cws;
+  std::vector<int16_t*> llr;
+  int                   ret = enqueue_llr(q, 1, &f, g->stream, cws, llr);
+  if (ret) {
+    hipStreamSynchronize(g->stream);
+    return ret;
+  }
+  if (hipStreamSynchronize(g->stream) != hipSuccess) {
+    return SRSRAN_ERROR;
+  }
+  for (size_t i = 0; i < cws.size(); i++) {
+    const uint32_t tb = cws[i].tb;
+    if (data[tb].crc) {
+      continue;  // already acknowledged (pdsch.c:893)
+    }
+    data[tb].evm = NAN;
+    if (!cfg->softbuffers.rx[tb] || !data[tb].payload) {
+      data[tb].crc = false;
+      continue;
+    }
+    const int r = srsran_dlsch_decode2_dev(&q->dl_sch, cfg, llr[i], data[tb].payload, (int)tb, cfg->grant.nof_layers);
+    data[tb].crc                  = r == SRSRAN_SUCCESS;  // pdsch.c:739-747
+    data[tb].avg_iterations_block = srsran_sch_last_noi(&q->dl_sch);
+  }
+  return SRSRAN_SUCCESS;
+}
+
+int srsran_pdsch_gpu_decode_batch(srsran_pdsch_t*              q,
+                                  uint32_t                     nof_sf,
+                                  const srsran_pdsch_gpu_sf_t* sfs,
+                                  int32_t*                     d_result,
+                                  float*                       d_avg_noi,
+                                  void*                        stream)
+{
+  if (!q || !q->gpu || (nof_sf && (!sfs || !d_result || !d_avg_noi))) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  if (nof_sf == 0) {
+    return 0;
+  }
+  if (q->llr_is_8bit || q->dl_sch.llr_is_8bit) {
+    return SRSRAN_ERROR;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  if (sfs[0].cfg && sfs[0].cfg->max_nof_iterations) {
+    srsran_sch_set_max_noi(&q->dl_sch, sfs[0].cfg->max_nof_iterations);
+  }
+  std::vector<Cw>       cws;
+  std::vector<int16_t*> llr;
+  int                   ret = enqueue_llr(q, nof_sf, sfs, s, cws, llr);
+  if (ret) {
+    return ret;
+  }
+  std::vector<srsran_dlsch_gpu_tb_t> tbs(cws.size());
+  for (size_t i = 0; i < cws.size(); i++) {
+    const srsran_pdsch_gpu_sf_t& f = sfs[cws[i].sf];
+    const srsran_ra_tb_t&        t = f.cfg->grant.tb[cws[i].tb];
+    srsran_dlsch_gpu_tb_t&       e = tbs[i];
+    if (!f.cfg->softbuffers.rx[cws[i].tb] || !f.d_payload[cws[i].tb]) {
+      return SRSRAN_ERROR_INVALID_INPUTS;
+    }
+    e.tbs        = (uint32_t)t.tbs;
+    e.Qm         = cws[i].Qm;  // Nl = 1: one layer per codeword
+    e.rv         = (uint32_t)t.rv;
+    e.nof_e_bits = t.nof_bits;
+    e.d_e_bits   = llr[i];
+    e.d_data     = f.d_payload[cws[i].tb];
+    e.softbuffer = f.cfg->softbuffers.rx[cws[i].tb];
+    e.new_data   = f.new_data[cws[i].tb];
+  }
+  ret = srsran_dlsch_gpu_decode_batch(&q->dl_sch, (uint32_t)tbs.size(), tbs.data(), d_result, d_avg_noi, stream);
+  return ret == SRSRAN_SUCCESS ? (int)tbs.size() : ret;
+}
+
+}  // extern "C"

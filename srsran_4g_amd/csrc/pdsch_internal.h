@@ -1,0 +1,22 @@
+// srsran_4g_amd/csrc/pdsch_internal.h -- host helpers shared by the PHCH / PDSCH / UE DL C-ABI files.
+#ifndef SRSRAN_AMD_PDSCH_INTERNAL_H
+#define SRSRAN_AMD_PDSCH_INTERNAL_H
+#include <stdint.h>
+
+#include <vector>
+
+#include "../../include/srsran_ue_dl.h"
+#include "eq_kernel.h"
+
+namespace srsran_amd {
+
+// predecoder scheme + norm for srsran_predecoding_type's arguments (phch_api.cpp)
+bool pred_setup(PredArgs& a, int nrx, int nports, int nlayers, int codebook, int type, float scaling);
+// sequence_pdsch_seed (sequences.c:62-65)
+uint32_t pdsch_seed(uint16_t rnti, int q, uint32_t nslot, uint32_t cell_id);
+// PDSCH RE gather table (pdsch_map.cpp)
+std::vector<uint32_t> pdsch_re_table(const srsran_cell_t& cell, const srsran_pdsch_grant_t& g, uint32_t lstart,
+                                     uint32_t sf_idx);
+
+}  // namespace srsran_amd
+#endif

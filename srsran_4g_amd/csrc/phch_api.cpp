@@ -12,6 +12,7 @@
 #include "../../include/srsran_phch.h"
 #include "eq_kernel.h"
 #include "llr_kernel.h"
+#include "pdsch_internal.h"
 
 using namespace srsran_amd;
 
@@ -55,6 +56,10 @@ bool ctx_ready()
   return hipStreamCreateWithFlags(&g_ctx.stream, hipStreamNonBlocking) == hipSuccess;
 }
 
+}  // namespace
+
+namespace srsran_amd {
+
 // srsran_predecoding_type's dispatch (precoding.c:1866-1930) for the MMSE CSI predecoders
 // provided here; fills the scheme-dependent norm.  Returns false for unsupported shapes.
 bool pred_setup(PredArgs& a, int nrx, int nports, int nlayers, int codebook, int type, float scaling)
@@ -93,7 +98,7 @@ uint32_t pdsch_seed(uint16_t rnti, int q, uint32_t nslot, uint32_t cell_id)
   return ((uint32_t)rnti << 14) + ((uint32_t)q << 13) + ((nslot / 2) << 9) + cell_id;  // sequences.c:62-65
 }
 
-}  // namespace
+}  // namespace srsran_amd
 
 extern "C" {
 

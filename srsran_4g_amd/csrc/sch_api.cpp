@@ -819,12 +819,14 @@ void srsran_sch_set_max_noi(srsran_sch_t* q, uint32_t max_iterations)
 float srsran_sch_last_noi(srsran_sch_t* q) { return q ? q->avg_iterations : 0.0f; }
 
 // ---------------- sch.c:509-609 (host-synchronous) ----------------
-int srsran_dlsch_decode2(srsran_sch_t*       q,
-                         srsran_pdsch_cfg_t* cfg,
-                         int16_t*            e_bits,
-                         uint8_t*            data,
-                         int                 tb_idx,
-                         uint32_t            nof_layers)
+// decode_tb of one TB, host-synchronous; LLRs from the host (e_bits) or already on the device (d_e_bits)
+static int dlsch_decode_sync(srsran_sch_t*       q,
+                             srsran_pdsch_cfg_t* cfg,
+                             const int16_t*      e_bits,
+                             const int16_t*      d_e_bits,
+                             uint8_t*            data,
+                             int                 tb_idx,
+                             uint32_t            nof_layers)
 {
   if (!q || !q->gpu || !cfg || tb_idx < 0 || tb_idx >= SRSRAN_MAX_CODEWORDS) {
     return SRSRAN_ERROR_INVALID_INPUTS;
@@ -838,7 +840,7 @@ int srsran_dlsch_decode2(srsran_sch_t*       q,
   }
   const uint32_t          Qm = srsran_mod_bits_x_symbol(cfg->grant.tb[tb_idx].mod) * Nl;
   srsran_softbuffer_rx_t* sb = cfg->softbuffers.rx[tb_idx];
-  if (!data || !sb || !e_bits || Qm == 0) {
+  if (!data || !sb || (!e_bits && !d_e_bits) || Qm == 0) {
     return SRSRAN_ERROR_INVALID_INPUTS;
   }
   if (s.tbs == 0 || s.C == 0) {
@@ -853,7 +855,7 @@ int srsran_dlsch_decode2(srsran_sch_t*       q,
   SchCtx*        x   = (SchCtx*)q->gpu;
   const uint32_t nbe = cfg->grant.tb[tb_idx].nof_bits;
   hipStreamSynchronize(x->stream);
-  if (!grow_dev((void**)&x->d_e, &x->e_cap, std::max<size_t>(nbe, 1) * sizeof(int16_t))) {
+  if (!d_e_bits && !grow_dev((void**)&x->d_e, &x->e_cap, std::max<size_t>(nbe, 1) * sizeof(int16_t))) {
     return SRSRAN_ERROR;
   }
   // the host cb_crc mirror is authoritative for the synchronous API
@@ -862,7 +864,9 @@ int srsran_dlsch_decode2(srsran_sch_t*       q,
     x->h_io[i] = sb->cb_crc[i] ? 1 : 0;
   }
   hipMemcpyAsync(g->d_flags, x->h_io, s.C, hipMemcpyHostToDevice, x->stream);
-  hipMemcpyAsync(x->d_e, e_bits, (size_t)nbe * sizeof(int16_t), hipMemcpyHostToDevice, x->stream);
+  if (!d_e_bits) {
+    hipMemcpyAsync(x->d_e, e_bits, (size_t)nbe * sizeof(int16_t), hipMemcpyHostToDevice, x->stream);
+  }
   uint32_t end = 0;  // bytes of `data` the reference writes (sch.c:425-431, 476-480)
   for (uint32_t cb = 0; cb < s.C; cb++) {
     const uint32_t K    = cb < s.C1 ? s.K1 : s.K2;
@@ -874,7 +878,7 @@ int srsran_dlsch_decode2(srsran_sch_t*       q,
   tb.Qm         = Qm;
   tb.rv         = (uint32_t)cfg->grant.tb[tb_idx].rv;
   tb.nof_e_bits = nbe;
-  tb.d_e_bits   = x->d_e;
+  tb.d_e_bits   = d_e_bits ? d_e_bits : x->d_e;
   tb.d_data     = x->d_data;
   tb.softbuffer = sb;
   tb.new_data   = 0;
@@ -902,6 +906,30 @@ int srsran_dlsch_decode2(srsran_sch_t*       q,
   sb->tb_crc        = h_flags[64] != 0;
   q->avg_iterations = *h_avg;
   return *h_res;
+}
+
+int srsran_dlsch_decode2(srsran_sch_t*       q,
+                         srsran_pdsch_cfg_t* cfg,
+                         int16_t*            e_bits,
+                         uint8_t*            data,
+                         int                 tb_idx,
+                         uint32_t            nof_layers)
+{
+  return dlsch_decode_sync(q, cfg, e_bits, nullptr, data, tb_idx, nof_layers);
+}
+
+/* added: srsran_dlsch_decode2 with the LLRs already in device memory (complete before the call) */
+int srsran_dlsch_decode2_dev(srsran_sch_t*       q,
+                             srsran_pdsch_cfg_t* cfg,
+                             const int16_t*      d_e_bits,
+                             uint8_t*            data,
+                             int                 tb_idx,
+                             uint32_t            nof_layers)
+{
+  if (!d_e_bits) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  return dlsch_decode_sync(q, cfg, nullptr, d_e_bits, data, tb_idx, nof_layers);
 }
 
 int srsran_dlsch_decode(srsran_sch_t* q, srsran_pdsch_cfg_t* cfg, int16_t* e_bits, uint8_t* data)

@@ -1,9 +1,10 @@
-"""Python mirror of the DL front-end C API (include/srsran_ue_dl.h): cell / subframe types,
-CRS channel estimation (and, as they land, OFDM, PDSCH, UE DL).  No CPU fallback."""
+"""Python mirror of the DL receive C API (include/srsran_ue_dl.h): cell / subframe types, CRS
+channel estimation, OFDM, PDSCH and UE DL (host-synchronous and batched).  No CPU fallback."""
 import ctypes
 
 import numpy as np
 
+from .sch import srsran_pdsch_cfg_t, srsran_sch_t, srsran_softbuffer_rx_t
 from .tdec import load_library
 
 u32 = ctypes.c_uint32
@@ -64,6 +65,44 @@ class srsran_cfo_t(ctypes.Structure):
                 ("gpu", ctypes.c_void_p)]
 
 
+class srsran_pdsch_t(ctypes.Structure):
+    _fields_ = [("cell", srsran_cell_t), ("nof_rx_antennas", u32), ("max_re", u32), ("is_ue", ctypes.c_bool),
+                ("llr_is_8bit", ctypes.c_bool), ("avg_evm", ctypes.c_float), ("dl_sch", srsran_sch_t),
+                ("coworker_ptr", ctypes.c_void_p), ("gpu", ctypes.c_void_p)]
+
+
+class srsran_pdsch_res_t(ctypes.Structure):
+    _fields_ = [("payload", ctypes.c_void_p), ("crc", ctypes.c_bool), ("avg_iterations_block", ctypes.c_float),
+                ("evm", ctypes.c_float)]
+
+
+class srsran_pdsch_gpu_sf_t(ctypes.Structure):
+    _fields_ = [("cfg", ctypes.POINTER(srsran_pdsch_cfg_t)), ("tti", u32), ("cfi", u32), ("d_grid", ctypes.c_void_p),
+                ("d_ce", ctypes.c_void_p), ("ce_full", u32), ("d_noise", ctypes.c_void_p), ("noise", ctypes.c_float),
+                ("d_payload", ctypes.c_void_p * 2), ("new_data", u32 * 2)]
+
+
+class srsran_dl_cfg_t(ctypes.Structure):
+    _fields_ = [("pdsch", srsran_pdsch_cfg_t), ("tm", ctypes.c_int), ("dci_common_ss", ctypes.c_bool)]
+
+
+class srsran_ue_dl_cfg_t(ctypes.Structure):
+    _fields_ = [("cfg", srsran_dl_cfg_t), ("chest_cfg", srsran_chest_dl_cfg_t), ("last_ri", u32),
+                ("snr_to_cqi_offset", ctypes.c_float)]
+
+
+class srsran_ue_dl_t(ctypes.Structure):
+    _fields_ = [("cell", srsran_cell_t), ("nof_rx_antennas", u32), ("current_mbsfn_area_id", ctypes.c_uint16),
+                ("pdsch", srsran_pdsch_t), ("chest", srsran_chest_dl_t), ("chest_res", srsran_chest_dl_res_t),
+                ("fft", srsran_ofdm_t * MAX_PORTS), ("sf_symbols", ctypes.c_void_p * MAX_PORTS),
+                ("gpu", ctypes.c_void_p)]
+
+
+class srsran_ue_dl_gpu_sf_t(ctypes.Structure):
+    _fields_ = [("tti", u32), ("cfi", u32), ("pdsch_cfg", ctypes.POINTER(srsran_pdsch_cfg_t)),
+                ("d_payload", ctypes.c_void_p * 2), ("new_data", u32 * 2)]
+
+
 _bound = False
 
 
@@ -74,6 +113,8 @@ def lib():
         CH = ctypes.POINTER(srsran_chest_dl_t)
         RES = ctypes.POINTER(srsran_chest_dl_res_t)
         P = ctypes.c_void_p
+        PD = ctypes.POINTER(srsran_pdsch_t)
+        UE = ctypes.POINTER(srsran_ue_dl_t)
         sig = {
             "srsran_symbol_sz": ([u32], ctypes.c_int),
             "srsran_symbol_sz_power2": ([u32], ctypes.c_int),
@@ -96,6 +137,27 @@ def lib():
             "srsran_cfo_init": ([ctypes.POINTER(srsran_cfo_t), u32], ctypes.c_int),
             "srsran_cfo_free": ([ctypes.POINTER(srsran_cfo_t)], None),
             "srsran_cfo_correct": ([ctypes.POINTER(srsran_cfo_t), P, P, ctypes.c_float], None),
+            "srsran_chest_dl_gpu_estimate_batch": ([CH, P, u32, P, ctypes.c_size_t, P, ctypes.c_size_t, P, P],
+                                                   ctypes.c_int),
+            "srsran_pdsch_init_ue": ([PD, u32, u32], ctypes.c_int),
+            "srsran_pdsch_free": ([PD], None),
+            "srsran_pdsch_set_cell": ([PD, srsran_cell_t], ctypes.c_int),
+            "srsran_pdsch_enable_coworker": ([PD], ctypes.c_int),
+            "srsran_pdsch_decode": ([PD, ctypes.POINTER(srsran_dl_sf_cfg_t), ctypes.POINTER(srsran_pdsch_cfg_t), RES,
+                                     P, ctypes.POINTER(srsran_pdsch_res_t)], ctypes.c_int),
+            "srsran_pdsch_gpu_decode_batch": ([PD, u32, ctypes.POINTER(srsran_pdsch_gpu_sf_t), P, P, P], ctypes.c_int),
+            "srsran_ue_dl_init": ([UE, P, u32, u32], ctypes.c_int),
+            "srsran_ue_dl_free": ([UE], None),
+            "srsran_ue_dl_set_cell": ([UE, srsran_cell_t], ctypes.c_int),
+            "srsran_ue_dl_decode_fft_estimate": ([UE, ctypes.POINTER(srsran_dl_sf_cfg_t),
+                                                  ctypes.POINTER(srsran_ue_dl_cfg_t)], ctypes.c_int),
+            "srsran_ue_dl_decode_fft_estimate_noguru": ([UE, ctypes.POINTER(srsran_dl_sf_cfg_t),
+                                                         ctypes.POINTER(srsran_ue_dl_cfg_t), P], ctypes.c_int),
+            "srsran_ue_dl_decode_pdsch": ([UE, ctypes.POINTER(srsran_dl_sf_cfg_t), ctypes.POINTER(srsran_pdsch_cfg_t),
+                                           ctypes.POINTER(srsran_pdsch_res_t)], ctypes.c_int),
+            "srsran_ue_dl_gpu_decode_batch": ([UE, ctypes.POINTER(srsran_ue_dl_cfg_t), u32,
+                                               ctypes.POINTER(srsran_ue_dl_gpu_sf_t), P, ctypes.c_float, P, P, P],
+                                              ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             f = getattr(L, name)
@@ -204,6 +266,154 @@ class ChestDl:
         if self.q.gpu:
             lib().srsran_chest_dl_res_free(ctypes.byref(self.res))
             lib().srsran_chest_dl_free(ctypes.byref(self.q))
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+# ---------------- PDSCH / UE DL ----------------
+SCHEME = {"port0": 0, "diversity": 1, "sm": 2, "cdd": 3}
+MOD_FROM_QM = {1: 0, 2: 1, 4: 2, 6: 3, 8: 4}
+
+
+def pdsch_cfg(nof_prb, nof_re, tbs, Qm, rv=(0, 0), scheme="cdd", pmi=0, rnti=0x1234, max_iterations=8,
+              csi_enable=True, power_scale=False, p_a=0.0, p_b=0, softbuffers=(), zf=False):
+    """srsran_pdsch_cfg_t for a full-bandwidth grant of len(tbs) codewords on as many layers
+    (srsUE defaults: csi_enable, 8 half-iterations, MMSE, no power scaling)."""
+    c = srsran_pdsch_cfg_t()
+    g = c.grant
+    g.tx_scheme = SCHEME[scheme]
+    g.pmi = pmi
+    for s in range(2):
+        for n in range(nof_prb):
+            g.prb_idx[s][n] = True
+    g.nof_prb = nof_prb
+    g.nof_re = nof_re
+    g.nof_symb_slot[0] = g.nof_symb_slot[1] = 7
+    g.nof_tb = g.nof_layers = len(tbs)
+    for i, t in enumerate(tbs):
+        tb = g.tb[i]
+        tb.mod = MOD_FROM_QM[Qm[i]]
+        tb.tbs = t
+        tb.rv = rv[i]
+        tb.nof_bits = nof_re * Qm[i]
+        tb.cw_idx = i
+        tb.enabled = True
+    c.rnti = rnti
+    c.max_nof_iterations = max_iterations
+    c.decoder_type = 0 if zf else 1
+    c.p_a, c.p_b = p_a, p_b
+    c.power_scale, c.csi_enable = power_scale, csi_enable
+    for i, sb in enumerate(softbuffers):
+        c.softbuffers.rx[i] = ctypes.pointer(sb.s)
+    return c
+
+
+class Pdsch:
+    """srsran_pdsch_t (UE side)."""
+
+    def __init__(self, cell_, nof_rx):
+        self.q = srsran_pdsch_t()
+        if lib().srsran_pdsch_init_ue(ctypes.byref(self.q), cell_.nof_prb, nof_rx):
+            raise RuntimeError("srsran_pdsch_init_ue failed (no HIP device?)")
+        if lib().srsran_pdsch_set_cell(ctypes.byref(self.q), cell_):
+            raise RuntimeError("srsran_pdsch_set_cell failed")
+        self.cell = cell_
+        self.nrx = nof_rx
+
+    def decode(self, cfg, tti, cfi, grids, ce, noise, acked=(False, False)):
+        """srsran_pdsch_decode on host grids (nrx, n) and full estimates (nports, nrx, n).
+        Returns (ret, [(crc, payload bytes, avg_iterations_block)])."""
+        grids = [np.ascontiguousarray(g, np.complex64) for g in grids]
+        ce = np.ascontiguousarray(ce, np.complex64)
+        sf = srsran_dl_sf_cfg_t()
+        sf.tti, sf.cfi = tti, cfi
+        res = srsran_chest_dl_res_t()
+        for p in range(ce.shape[0]):
+            for r in range(ce.shape[1]):
+                res.ce[p][r] = ce[p, r].ctypes.data
+        res.noise_estimate = noise
+        ptrs = (ctypes.c_void_p * MAX_PORTS)(*[g.ctypes.data for g in grids] + [None] * (MAX_PORTS - len(grids)))
+        ntb = cfg.grant.nof_tb
+        pls = [np.zeros(cfg.grant.tb[i].tbs // 8 + 64, np.uint8) for i in range(ntb)]
+        data = (srsran_pdsch_res_t * 2)()
+        for i in range(ntb):
+            data[i].payload = pls[i].ctypes.data
+            data[i].crc = bool(acked[i])
+        ret = lib().srsran_pdsch_decode(ctypes.byref(self.q), ctypes.byref(sf), ctypes.byref(cfg), ctypes.byref(res),
+                                        ctypes.addressof(ptrs), data)
+        return ret, [(data[i].crc, pls[i], data[i].avg_iterations_block) for i in range(ntb)]
+
+    def free(self):
+        if self.q.gpu:
+            lib().srsran_pdsch_free(ctypes.byref(self.q))
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class UeDl:
+    """srsran_ue_dl_t: host-synchronous decode_fft_estimate / decode_pdsch and the device batch."""
+
+    def __init__(self, cell_, nof_rx):
+        self.q = srsran_ue_dl_t()
+        if lib().srsran_ue_dl_init(ctypes.byref(self.q), None, cell_.nof_prb, nof_rx):
+            raise RuntimeError("srsran_ue_dl_init failed (no HIP device?)")
+        if lib().srsran_ue_dl_set_cell(ctypes.byref(self.q), cell_):
+            raise RuntimeError("srsran_ue_dl_set_cell failed")
+        self.cell = cell_
+        self.nrx = nof_rx
+        self.cfg = srsran_ue_dl_cfg_t()
+        self.cfg.chest_cfg = srsue_chest_cfg()
+
+    def fft_estimate(self, samples, tti, cfi):
+        x = [np.ascontiguousarray(v, np.complex64) for v in samples]
+        ptrs = (ctypes.c_void_p * MAX_PORTS)(*[v.ctypes.data for v in x] + [None] * (MAX_PORTS - len(x)))
+        sf = srsran_dl_sf_cfg_t()
+        sf.tti, sf.cfi = tti, cfi
+        return lib().srsran_ue_dl_decode_fft_estimate_noguru(ctypes.byref(self.q), ctypes.byref(sf),
+                                                             ctypes.byref(self.cfg), ctypes.addressof(ptrs))
+
+    def grids(self):
+        n = 14 * 12 * self.cell.nof_prb
+        out = np.zeros((self.nrx, n), np.complex64)
+        for r in range(self.nrx):
+            ctypes.memmove(out[r].ctypes.data, self.q.sf_symbols[r], n * 8)
+        return out
+
+    def decode_pdsch(self, cfg, tti, cfi):
+        sf = srsran_dl_sf_cfg_t()
+        sf.tti, sf.cfi = tti, cfi
+        ntb = cfg.grant.nof_tb
+        pls = [np.zeros(cfg.grant.tb[i].tbs // 8 + 64, np.uint8) for i in range(ntb)]
+        data = (srsran_pdsch_res_t * 2)()
+        for i in range(ntb):
+            data[i].payload = pls[i].ctypes.data
+        ret = lib().srsran_ue_dl_decode_pdsch(ctypes.byref(self.q), ctypes.byref(sf), ctypes.byref(cfg), data)
+        return ret, [(data[i].crc, pls[i], data[i].avg_iterations_block) for i in range(ntb)]
+
+    def gpu_decode_batch(self, sfs, d_samples, d_result, d_avg, cfo=0.0, stream=None):
+        """sfs: list of (tti, cfi, srsran_pdsch_cfg_t, [d_payload ptrs], [new_data])."""
+        arr = (srsran_ue_dl_gpu_sf_t * len(sfs))()
+        self._keep = [s[2] for s in sfs]
+        for i, (tti, cfi, cfg, pls, nd) in enumerate(sfs):
+            arr[i].tti, arr[i].cfi = tti, cfi
+            arr[i].pdsch_cfg = ctypes.pointer(cfg)
+            for t, p in enumerate(pls):
+                arr[i].d_payload[t] = p
+                arr[i].new_data[t] = nd[t]
+        return lib().srsran_ue_dl_gpu_decode_batch(ctypes.byref(self.q), ctypes.byref(self.cfg), len(sfs), arr,
+                                                   d_samples, cfo, d_result, d_avg, stream)
+
+    def free(self):
+        if self.q.gpu:
+            lib().srsran_ue_dl_free(ctypes.byref(self.q))
 
     def __del__(self):
         try:

@@ -1,0 +1,248 @@
+"""Synthetic eNB-side transmitter: code blocks, DL-SCH transport blocks and complete PDSCH
+subframes in the time domain (tests and bench inputs; neither product nor oracle).
+
+Written from 3GPP TS 36.211 / 36.212 (libsynth.so: synth/tx.c) plus numpy for modulation,
+precoding, resource mapping and the OFDM transmitter.  The conventions are the ones srsRAN's
+receiver assumes (receive side: SURVEY.md 8a):
+  - turbo/LLR convention of turbodecoder_test.c:217-255 (bit 1 -> +1, LLR = trunc(100 y))
+  - modulation 36.211 7.1 (bit 0 -> positive amplitude), unit average power
+  - CDD for 2 ports: y0 = (x0 + x1)/2, y1 = (-1)^i (x0 - x1)/2 (36.211 6.3.4.3, srsRAN scaling)
+  - spatial multiplexing rank 2: 36.211 Table 6.3.4.2.3-1 (codebook 0..2)
+  - CRS 36.211 6.10.1 (c_init = 2^10 (7 (ns+1) + l + 1)(2 N_ID + 1) + 2 N_ID + 1, m' = m + 110 - N_RB)
+  - PDSCH REs in (symbol, subcarrier) order skipping control symbols, CRS of every port and,
+    in subframes 0 / 5, PBCH / PSS / SSS in the centre 6 PRBs (even N_RB)
+  - OFDM: IFFT / N, symbol l of slot s starts after CP ceil(160N/2048) (l = 0) or ceil(144N/2048)
+"""
+import ctypes
+import math
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+_lib = None
+
+QM = {"bpsk": 1, "qpsk": 2, "16qam": 4, "64qam": 6, "256qam": 8}
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        path = os.path.join(HERE, "libsynth.so")
+        if not os.path.exists(path):
+            subprocess.run(["make", "-s", "-C", HERE], check=True)
+        L = ctypes.CDLL(path)
+        P = ctypes.c_void_p
+        u32 = ctypes.c_uint32
+        L.synth_turbo_encode_natural.argtypes = [u32, P, P]
+        L.synth_turbo_encode.argtypes = [u32, P, P, P, P]
+        L.synth_dlsch_encode.argtypes = [u32, u32, u32, u32, u32, P, u32, P]
+        L.synth_gold.argtypes = [u32, u32, P]
+        L.synth_gold.restype = None
+        L.synth_crc.argtypes = [u32, P, u32]
+        L.synth_crc.restype = u32
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+# ---------------- channel coding ----------------
+def turbo_encode(K, bits):
+    """natural srsRAN decoder-input order [d0_i d1_i d2_i], 3K + 12 bits"""
+    bits = np.ascontiguousarray(bits, np.uint8)
+    out = np.zeros(3 * K + 12, np.uint8)
+    if lib().synth_turbo_encode_natural(K, _p(bits), _p(out)):
+        raise ValueError(f"K={K} is not an LTE code block size")
+    return out
+
+
+def make_llrs(K, ebno_db, rng, n=1):
+    """AWGN code blocks in turbodecoder_test.c's convention (217-255): BPSK bit 1 -> +1,
+    var = 10^(-(EbNo + 10 log10(1/3))/10), LLR = (int16)(100 y).  -> (bits[n,K], llr[n,3K+12])"""
+    bits = rng.integers(0, 2, size=(n, K), dtype=np.uint8)
+    var = 10 ** (-(ebno_db + 10 * np.log10(1.0 / 3.0)) / 10)
+    llr = np.zeros((n, 3 * K + 12), dtype=np.int16)
+    for i in range(n):
+        sym = turbo_encode(K, bits[i]).astype(np.float32) * 2 - 1
+        y = sym + rng.standard_normal(sym.shape).astype(np.float32) * np.float32(np.sqrt(var))
+        llr[i] = np.trunc(np.float32(100) * y).astype(np.int16)
+    return bits, llr
+
+
+def dlsch_encode(tbs, Qm, rv, G, tb_bytes, Nl=1, tb_crc_xor=0):
+    """36.212 5.3.2 for one TB -> G coded bits (uint8)"""
+    tb = np.ascontiguousarray(tb_bytes, np.uint8)
+    assert tb.size >= tbs // 8
+    e = np.zeros(G, np.uint8)
+    n = lib().synth_dlsch_encode(tbs, Qm, Nl, rv, G, _p(tb), tb_crc_xor, _p(e))
+    if n != G:
+        raise ValueError(f"dlsch_encode(tbs={tbs}, G={G}) failed ({n})")
+    return e
+
+
+def gold(c_init, n):
+    c = np.zeros(n, np.uint8)
+    lib().synth_gold(c_init, n, _p(c))
+    return c
+
+
+def crc24a(bits):
+    b = np.ascontiguousarray(bits, np.uint8)
+    return lib().synth_crc(0x1864CFB, _p(b), b.size)
+
+
+# ---------------- modulation / precoding ----------------
+def modulate(bits, Qm):
+    """36.211 7.1: bits -> unit-power symbols (complex64)"""
+    b = 1.0 - 2.0 * np.asarray(bits, np.float64).reshape(-1, Qm)
+    if Qm == 1:
+        s = (b[:, 0] + 1j * b[:, 0]) / math.sqrt(2)
+    elif Qm == 2:
+        s = (b[:, 0] + 1j * b[:, 1]) / math.sqrt(2)
+    elif Qm == 4:
+        s = (b[:, 0] * (2 - b[:, 2]) + 1j * b[:, 1] * (2 - b[:, 3])) / math.sqrt(10)
+    elif Qm == 6:
+        s = (b[:, 0] * (4 - b[:, 2] * (2 - b[:, 4])) + 1j * b[:, 1] * (4 - b[:, 3] * (2 - b[:, 5]))) / math.sqrt(42)
+    elif Qm == 8:
+        s = (b[:, 0] * (8 - b[:, 2] * (4 - b[:, 4] * (2 - b[:, 6])))
+             + 1j * b[:, 1] * (8 - b[:, 3] * (4 - b[:, 5] * (2 - b[:, 7])))) / math.sqrt(170)
+    else:
+        raise ValueError(Qm)
+    return s.astype(np.complex64)
+
+
+def precode(x, scheme, codebook=0):
+    """layers x[L][n] -> ports y[P][n]"""
+    x = [np.asarray(v, np.complex128) for v in x]
+    if scheme == "port0":
+        return [x[0]]
+    n = x[0].size
+    if scheme == "cdd":
+        sgn = np.where(np.arange(n) % 2 == 0, 1.0, -1.0)
+        return [(x[0] + x[1]) / 2, sgn * (x[0] - x[1]) / 2]
+    if scheme == "sm":
+        W = {0: np.array([[1, 0], [0, 1]]) / math.sqrt(2), 1: np.array([[1, 1], [1, -1]]) / 2,
+             2: np.array([[1, 1], [1j, -1j]]) / 2}[codebook]
+        return [W[0, 0] * x[0] + W[0, 1] * x[1], W[1, 0] * x[0] + W[1, 1] * x[1]]
+    raise ValueError(scheme)
+
+
+# ---------------- resource grid ----------------
+def crs_shift(port, l):
+    """v of 36.211 6.10.1.2 for symbol l (0..6) of a slot"""
+    if port == 0:
+        return 0 if l == 0 else 3
+    if port == 1:
+        return 3 if l == 0 else 0
+    raise ValueError(port)
+
+
+def crs_symbols(nports):
+    return [0, 4] if nports <= 2 else [0, 1, 4]
+
+
+def crs_values(cell_id, nof_prb, ns, l):
+    c = gold((1 << 10) * (7 * (ns + 1) + l + 1) * (2 * cell_id + 1) + 2 * cell_id + 1, 4 * 110)
+    m = np.arange(2 * nof_prb) + 110 - nof_prb
+    return ((1 - 2.0 * c[2 * m]) + 1j * (1 - 2.0 * c[2 * m + 1])) / math.sqrt(2)
+
+
+def crs_grid(cell_id, nof_prb, nports, port, sf_idx):
+    """port's CRS in a (14, 12 N_RB) grid (2 ports max)"""
+    g = np.zeros((14, 12 * nof_prb), np.complex128)
+    for s in range(2):
+        for l in crs_symbols(nports):
+            k = 6 * np.arange(2 * nof_prb) + (crs_shift(port, l) + cell_id % 6) % 6
+            g[7 * s + l, k] = crs_values(cell_id, nof_prb, 2 * sf_idx + s, l)
+    return g
+
+
+def pdsch_mask(nof_prb, nports, cell_id, cfi, sf_idx, prb=None):
+    """(14, 12 N_RB) bool: REs that carry PDSCH"""
+    assert nof_prb % 2 == 0 or sf_idx not in (0, 5), "odd N_RB centre PRBs not generated"
+    nre = 12 * nof_prb
+    m = np.zeros((14, nre), bool)
+    prb = np.ones(nof_prb, bool) if prb is None else np.asarray(prb, bool)
+    m[:, np.repeat(prb, 12)] = True
+    m[: cfi + (1 if nof_prb < 10 else 0)] = False
+    k = np.arange(nre)
+    for s in range(2):
+        for l in crs_symbols(nports):
+            if nports == 1:
+                m[7 * s + l, (k % 6) == (crs_shift(0, l) + cell_id % 6) % 6] = False
+            else:
+                m[7 * s + l, (k % 3) == cell_id % 3] = False
+    lo, hi = 12 * (nof_prb // 2 - 3), 12 * (nof_prb // 2 + 3)
+    if sf_idx in (0, 5):
+        m[5:7, lo:hi] = False  # SSS, PSS
+    if sf_idx == 0:
+        m[7:11, lo:hi] = False  # PBCH
+    return m
+
+
+def ofdm_tx(grid, N):
+    grid = np.asarray(grid).reshape(14, -1)
+    nre = grid.shape[1]
+    cp0, cp = math.ceil(160 * N / 2048), math.ceil(144 * N / 2048)
+    out = []
+    for l in range(14):
+        X = np.zeros(N, np.complex128)
+        X[N - nre // 2:] = grid[l, : nre // 2]
+        X[1: nre // 2 + 1] = grid[l, nre // 2:]
+        t = np.fft.ifft(X)
+        c = cp0 if l % 7 == 0 else cp
+        out += [t[N - c:], t]
+    return np.concatenate(out)
+
+
+def symbol_sz(nof_prb):
+    """srsran_symbol_sz with standard rates (power-of-two sizes, 1536 for 15 MHz)"""
+    for p, n in ((6, 128), (15, 256), (25, 512), (52, 1024), (79, 1536), (110, 2048)):
+        if nof_prb <= p:
+            return n
+    raise ValueError(nof_prb)
+
+
+def pdsch_seed(rnti, q, ns, cell_id):
+    return (rnti << 14) + (q << 13) + ((ns // 2) << 9) + cell_id
+
+
+def pdsch_subframe(nof_prb, cell_id, nports, tti, cfi, rnti, tbs, Qm, rv, payloads, scheme="cdd", codebook=1,
+                   nrx=2, snr_db=None, rng=None, N=None, channel=None, cfo=0.0):
+    """One PDSCH subframe through OFDM and a static MIMO channel.
+
+    payloads: one uint8 array (tbs/8 bytes) per codeword.  channel: (nrx, nports) complex matrix
+    (default: [[1, 1], [1, -1]] for 2 ports as phy_dl_test.c:568-583 uses, ones for 1 port).
+    Returns (samples[nrx, sf_len] complex64, nof_re)."""
+    N = N or symbol_sz(nof_prb)
+    sf_idx = tti % 10
+    mask = pdsch_mask(nof_prb, nports, cell_id, cfi, sf_idx)
+    nof_re = int(mask.sum())
+    layers = []
+    for q, pl in enumerate(payloads):
+        G = nof_re * Qm
+        e = dlsch_encode(tbs, Qm, rv, G, pl)
+        c = gold(pdsch_seed(rnti, q, 2 * sf_idx, cell_id), G)
+        layers.append(modulate(e ^ c, Qm))
+    ports = precode(layers, scheme, codebook)
+    if len(ports) != nports:
+        raise ValueError("scheme / port count mismatch")
+    tx = []
+    for p in range(nports):
+        g = crs_grid(cell_id, nof_prb, nports, p, sf_idx)
+        g[mask] = ports[p]
+        tx.append(ofdm_tx(g, N))
+    H = np.asarray(channel if channel is not None else
+                   ([[1, 1], [1, -1]] if nports == 2 else [[1]] * nrx), np.complex128)
+    rx = H @ np.stack(tx)
+    if snr_db is not None:
+        pw = np.mean(np.abs(rx) ** 2)
+        sd = math.sqrt(pw / 10 ** (snr_db / 10) / 2)
+        rx = rx + sd * (rng.standard_normal(rx.shape) + 1j * rng.standard_normal(rx.shape))
+    if cfo:
+        rx = rx * np.exp(2j * np.pi * cfo * np.arange(rx.shape[1]))
+    return rx.astype(np.complex64), nof_re

@@ -1,0 +1,213 @@
+"""GPU srsran_pdsch_decode / srsran_ue_dl_* against the oracle chain (oracle/pdsch_chain.py,
+composed from pieces pinned to the reference) on synthetic eNB subframes (synth/).
+
+Bit-exact tier: the GPU PDSCH stage is fed the oracle's own grids and channel estimates, so
+predecode (IEEE float, no contraction), demap, descramble, CSI correction and DL-SCH decode must
+agree exactly -- decode_tb's return, every payload byte it writes, avg iterations.
+Chain tier: GPU OFDM + channel estimation differ from numpy / the oracle by float rounding
+(FFT and reductions in another order; FFT parity is unpinned), so the full GPU chain
+is checked by decoding (CRC pass, payload == transmitted) and by agreement with the oracle chain.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import Oracle
+import pdsch_chain as PC
+from synth import synth as S
+
+pytestmark = pytest.mark.gpu
+
+TBS = 75376  # C3: MCS 28, 100 PRB (grant_probe)
+
+
+@pytest.fixture(scope="module")
+def ora():
+    return Oracle()
+
+
+@pytest.fixture(scope="module")
+def U():
+    from srsran_4g_amd import ue_dl
+    return ue_dl
+
+
+@pytest.fixture(scope="module")
+def SCH():
+    from srsran_4g_amd import sch
+    return sch
+
+
+def _case(ora, rng, nof_prb=100, cell_id=1, nports=2, tti=1, cfi=1, tbs=(TBS, TBS), Qm=(6, 6), scheme="cdd",
+          pmi=0, snr_db=30.0, **kw):
+    assert len(set(tbs)) == 1 and len(set(Qm)) == 1  # synth sends one TBS / modulation per subframe
+    pls = [rng.integers(0, 256, t // 8, dtype=np.uint8) for t in tbs]
+    cb = pmi + 1 if len(tbs) == 2 else pmi
+    x, nre = S.pdsch_subframe(nof_prb, cell_id, nports, tti, cfi, 0x1234, tbs[0], Qm[0], 0, pls, scheme=scheme,
+                              codebook=cb, snr_db=snr_db, rng=rng, **kw)
+    grids, ce, st = PC.fft_estimate(ora, x, nof_prb, cell_id, nports, tti)
+    return pls, x, nre, grids, ce, st
+
+
+CASES = [
+    dict(),                                                 # C3, subframe 1
+    dict(tti=5),                                            # PSS / SSS subframe
+    dict(tti=10),                                           # subframe 0 (PBCH)
+    dict(snr_db=13.0, fail=True),                           # CB CRC failures / early-stop spread
+    dict(tti=10, cfi=2, fail=True),                         # code rate > 0.98: undecodable, fails alike
+    dict(scheme="sm", pmi=0),                               # TM4 codebook 1
+    dict(scheme="sm", pmi=1, cell_id=7),                    # TM4 codebook 2
+    dict(nports=1, scheme="port0", tbs=(30576,), Qm=(4,), cell_id=3, channel=[[1], [0.5 + 0.5j]]),
+    dict(nof_prb=50, cell_id=11, tbs=(36696, 36696), tti=3, cfi=3),
+    dict(nof_prb=6, cell_id=2, tbs=(1800, 1800), Qm=(4, 4), cfi=2, tti=7),
+]
+
+
+@pytest.mark.parametrize("case", range(len(CASES)))
+@pytest.mark.parametrize("opts", [dict(), dict(csi_enable=False), dict(power_scale=True, p_a=-3.0, p_b=2),
+                                  dict(zf=True)])
+def test_pdsch_decode_bitexact(U, SCH, ora, case, opts):
+    kw = dict(CASES[case])
+    if opts and case not in (0, 3, 7):
+        pytest.skip("options exercised on a subset of grants")
+    rng = np.random.default_rng(100 + case)
+    fail = kw.pop("fail", False)
+    nof_prb = kw.pop("nof_prb", 100)
+    cell_id = kw.pop("cell_id", 1)
+    nports = kw.pop("nports", 2)
+    tti = kw.pop("tti", 1)
+    cfi = kw.pop("cfi", 1)
+    tbs = kw.pop("tbs", (TBS, TBS))
+    Qm = kw.pop("Qm", (6, 6))
+    scheme = kw.pop("scheme", "cdd")
+    pmi = kw.pop("pmi", 0)
+    pls, x, nre, grids, ce, st = _case(ora, rng, nof_prb, cell_id, nports, tti, cfi, tbs, Qm, scheme, pmi, **kw)
+    noise = st["noise"]
+    ref = PC.pdsch_decode(ora, grids, ce, noise, nof_prb, cell_id, nports, tti, cfi, 0x1234, list(tbs), list(Qm),
+                          [0] * len(tbs), scheme=scheme, pmi=pmi, csi_enable=opts.get("csi_enable", True),
+                          power_scale=opts.get("power_scale", False), p_a=opts.get("p_a", 0.0),
+                          p_b=opts.get("p_b", 0)) if not opts.get("zf") else \
+        PC.pdsch_decode(ora, grids, ce, 0.0, nof_prb, cell_id, nports, tti, cfi, 0x1234, list(tbs), list(Qm),
+                        [0] * len(tbs), scheme=scheme, pmi=pmi)
+    sbs = [SCH.SoftbufferRx(nof_prb=nof_prb) for _ in tbs]
+    cfg = U.pdsch_cfg(nof_prb, nre, tbs, Qm, scheme=scheme, pmi=pmi, softbuffers=sbs, **opts)
+    pd = U.Pdsch(U.cell(nof_prb, nports, cell_id), grids.shape[0])
+    ret, out = pd.decode(cfg, tti, cfi, grids, ce, noise)
+    assert ret == 0
+    for q, (crc, payload, avg) in enumerate(out):
+        r = ref[q]
+        assert crc == (r["ret"] == 0), q
+        n = tbs[q] // 8 + 6
+        assert np.array_equal(payload[:n], r["data"][:n]), q
+        assert avg == pytest.approx(r["avg"], abs=1e-6), q
+        if not fail:
+            assert crc and np.array_equal(payload[: tbs[q] // 8], pls[q])
+    pd.free()
+
+
+def test_pdsch_already_acked_is_skipped(U, SCH, ora):
+    rng = np.random.default_rng(5)
+    pls, x, nre, grids, ce, st = _case(ora, rng)
+    sbs = [SCH.SoftbufferRx(nof_prb=100) for _ in range(2)]
+    cfg = U.pdsch_cfg(100, nre, (TBS, TBS), (6, 6), softbuffers=sbs)
+    pd = U.Pdsch(U.cell(100, 2, 1), 2)
+    ret, out = pd.decode(cfg, 1, 1, grids, ce, st["noise"], acked=(True, False))
+    assert ret == 0
+    assert out[0][0] and not out[0][1][:16].any()  # TB0 untouched
+    assert out[1][0] and np.array_equal(out[1][1][: TBS // 8], pls[1])
+    pd.free()
+
+
+def test_pdsch_rejects_wrong_nof_re(U, SCH, ora):
+    rng = np.random.default_rng(6)
+    pls, x, nre, grids, ce, st = _case(ora, rng)
+    sbs = [SCH.SoftbufferRx(nof_prb=100) for _ in range(2)]
+    cfg = U.pdsch_cfg(100, nre + 12, (TBS, TBS), (6, 6), softbuffers=sbs)
+    pd = U.Pdsch(U.cell(100, 2, 1), 2)
+    ret, _ = pd.decode(cfg, 1, 1, grids, ce, st["noise"])
+    assert ret != 0
+    pd.free()
+
+
+def test_ue_dl_host_sync_decodes(U, SCH, ora):
+    """srsran_ue_dl_decode_fft_estimate_noguru + srsran_ue_dl_decode_pdsch on time samples"""
+    rng = np.random.default_rng(7)
+    ue = U.UeDl(U.cell(100, 2, 1), 2)
+    for tti in (1, 5, 10):
+        pls, x, nre, grids, ce, st = _case(ora, rng, tti=tti)
+        assert ue.fft_estimate(x, tti, 1) == 0
+        g = ue.grids()
+        assert np.abs(g - grids).max() < 1e-3 * np.abs(grids).max()
+        sbs = [SCH.SoftbufferRx(nof_prb=100) for _ in range(2)]
+        cfg = U.pdsch_cfg(100, nre, (TBS, TBS), (6, 6), softbuffers=sbs)
+        ret, out = ue.decode_pdsch(cfg, tti, 1)
+        assert ret == 0
+        for q in range(2):
+            assert out[q][0] and np.array_equal(out[q][1][: TBS // 8], pls[q])
+    ue.free()
+
+
+def test_ue_dl_batch_matches_host_sync(U, SCH, ora):
+    """srsran_ue_dl_gpu_decode_batch over 10 subframes (all subframe types, 2 grants) == the
+    host-synchronous UE DL path subframe by subframe, and decodes what was sent."""
+    rng = np.random.default_rng(8)
+    ue = U.UeDl(U.cell(100, 2, 1), 2)
+    nsf = 10
+    samples, cfgs, payloads, entries, sbs = [], [], [], [], []
+    d_pl = torch.zeros((nsf, 2, TBS // 8 + 64), dtype=torch.uint8, device="cuda")
+    for b in range(nsf):
+        tti = 21 + b
+        cfi = 2 if b % 3 == 1 else 1  # CFI 2 on subframes 2, 5, 8
+        pls, x, nre, _, _, _ = _case(ora, rng, tti=tti, cfi=cfi)
+        sb = [SCH.SoftbufferRx(nof_prb=100) for _ in range(2)]
+        cfg = U.pdsch_cfg(100, nre, (TBS, TBS), (6, 6), softbuffers=sb)
+        samples.append(x)
+        cfgs.append(cfg)
+        payloads.append(pls)
+        sbs.append(sb)
+        entries.append((tti, cfi, cfg, [d_pl[b, 0].data_ptr(), d_pl[b, 1].data_ptr()], [1, 1]))
+    d_x = torch.from_numpy(np.stack(samples).view(np.float32)).cuda()
+    d_res = torch.full((2 * nsf,), 7, dtype=torch.int32, device="cuda")
+    d_avg = torch.zeros(2 * nsf, dtype=torch.float32, device="cuda")
+    n = ue.gpu_decode_batch(entries, d_x.data_ptr(), d_res.data_ptr(), d_avg.data_ptr(), 0.0, None)
+    assert n == 2 * nsf
+    torch.cuda.synchronize()
+    res = d_res.cpu().numpy()
+    avg = d_avg.cpu().numpy()
+    pl = d_pl.cpu().numpy()
+    ue2 = U.UeDl(U.cell(100, 2, 1), 2)
+    for b in range(nsf):
+        tti, cfi = entries[b][0], entries[b][1]
+        assert ue2.fft_estimate(samples[b], tti, cfi) == 0
+        sb = [SCH.SoftbufferRx(nof_prb=100) for _ in range(2)]
+        cfg = U.pdsch_cfg(100, cfgs[b].grant.nof_re, (TBS, TBS), (6, 6), softbuffers=sb)
+        ret, out = ue2.decode_pdsch(cfg, tti, cfi)
+        for q in range(2):
+            assert res[2 * b + q] == 0 and out[q][0]
+            assert np.array_equal(pl[b, q, : TBS // 8], payloads[b][q])
+            assert np.array_equal(pl[b, q, : TBS // 8 + 6], out[q][1][: TBS // 8 + 6])
+            assert avg[2 * b + q] == pytest.approx(out[q][2], abs=0.2)
+    ue.free()
+    ue2.free()
+
+
+def test_ue_dl_batch_cfo(U, SCH, ora):
+    """a CFO on the samples, removed by the batch's fused rotation"""
+    rng = np.random.default_rng(9)
+    ue = U.UeDl(U.cell(100, 2, 1), 2)
+    f = 150.0 / 30.72e6
+    pls, x, nre, _, _, _ = _case(ora, rng, tti=2, cfo=f)
+    sb = [SCH.SoftbufferRx(nof_prb=100) for _ in range(2)]
+    cfg = U.pdsch_cfg(100, nre, (TBS, TBS), (6, 6), softbuffers=sb)
+    d_pl = torch.zeros((2, TBS // 8 + 64), dtype=torch.uint8, device="cuda")
+    d_x = torch.from_numpy(x[None].view(np.float32)).cuda()
+    d_res = torch.full((2,), 7, dtype=torch.int32, device="cuda")
+    d_avg = torch.zeros(2, dtype=torch.float32, device="cuda")
+    n = ue.gpu_decode_batch([(2, 1, cfg, [d_pl[0].data_ptr(), d_pl[1].data_ptr()], [1, 1])], d_x.data_ptr(),
+                            d_res.data_ptr(), d_avg.data_ptr(), -f, None)
+    assert n == 2
+    torch.cuda.synchronize()
+    assert (d_res.cpu().numpy() == 0).all()
+    for q in range(2):
+        assert np.array_equal(d_pl[q].cpu().numpy()[: TBS // 8], pls[q])
+    ue.free()

@@ -1,0 +1,97 @@
+"""The synthetic transmitter (synth/) against the oracle (pinned to the reference): turbo
+encoder, DL-SCH encoder, Gold sequence, CRS values, PDSCH RE set, modulation vs demapper."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, ROOT)
+
+from oracle import CB_SIZES, Oracle  # noqa: E402
+import pdsch_np  # noqa: E402
+from synth import synth as S  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def ora():
+    return Oracle()
+
+
+def test_turbo_encoder_all_sizes(ora):
+    rng = np.random.default_rng(1)
+    for K in CB_SIZES:
+        b = rng.integers(0, 2, K, dtype=np.uint8)
+        assert np.array_equal(S.turbo_encode(K, b), ora.encode(K, b)), K
+
+
+@pytest.mark.parametrize("tbs,Qm,rv", [(75376, 6, 0), (75376, 6, 2), (1544, 2, 1), (30576, 4, 3), (6200, 6, 0),
+                                       (97896, 8, 0), (40, 2, 0)])
+def test_dlsch_encoder(ora, tbs, Qm, rv):
+    rng = np.random.default_rng(tbs + rv)
+    tb = rng.integers(0, 256, tbs // 8, dtype=np.uint8)
+    for G in (Qm * ((3 * tbs) // (2 * Qm) + 7), 86400 - 86400 % Qm):
+        assert np.array_equal(S.dlsch_encode(tbs, Qm, rv, G, tb), ora.dlsch_encode(tbs, Qm, rv, G, tb)), (tbs, G)
+
+
+def test_tb_crc_corruption(ora):
+    rng = np.random.default_rng(3)
+    tb = rng.integers(0, 256, 75376 // 8, dtype=np.uint8)
+    a = S.dlsch_encode(75376, 6, 0, 86400, tb, tb_crc_xor=0x5A)
+    b = ora.dlsch_encode(75376, 6, 0, 86400, tb, tb_crc_xor=0x5A)
+    assert np.array_equal(a, b)
+
+
+def test_gold(ora):
+    for seed in (0, 1, 0x1234 << 14, 0x7FFFFFFF):
+        assert np.array_equal(S.gold(seed, 5000), ora.sequence_bits(seed, 5000))
+
+
+@pytest.mark.parametrize("cell_id,nof_prb,sf", [(1, 100, 1), (0, 6, 0), (301, 50, 7), (503, 25, 9)])
+def test_crs_values(ora, cell_id, nof_prb, sf):
+    ref = ora.crs_pilots(cell_id, nof_prb, 0, sf).reshape(4, -1)
+    for li in range(4):
+        v = S.crs_values(cell_id, nof_prb, 2 * sf + li // 2, 0 if li % 2 == 0 else 4)
+        np.testing.assert_allclose(v, ref[li], atol=1e-6)
+
+
+@pytest.mark.parametrize("nof_prb,nports,cell_id,cfi,sf", [(100, 2, 1, 1, 1), (100, 2, 1, 1, 0), (100, 2, 7, 2, 5),
+                                                           (50, 1, 2, 3, 0), (6, 2, 5, 2, 5), (100, 1, 0, 1, 3)])
+def test_pdsch_re_set(nof_prb, nports, cell_id, cfi, sf):
+    m = S.pdsch_mask(nof_prb, nports, cell_id, cfi, sf)
+    lstart = cfi + (1 if nof_prb < 10 else 0)
+    ref = pdsch_np.re_table(nof_prb, nports, cell_id, np.ones((2, nof_prb), bool), lstart, sf)
+    got = np.flatnonzero(m.reshape(-1))
+    assert np.array_equal(got, np.array([t[0] for t in ref], np.int64))
+
+
+@pytest.mark.parametrize("Qm,mod", [(2, 1), (4, 2), (6, 3), (8, 4)])
+def test_modulation_matches_demapper(ora, Qm, mod):
+    """noise-free symbols demap to LLRs whose sign gives back the bits (LLR > 0 <=> bit 1)"""
+    rng = np.random.default_rng(Qm)
+    bits = rng.integers(0, 2, Qm * 400, dtype=np.uint8)
+    sym = S.modulate(bits, Qm)
+    allb = ((np.arange(2 ** Qm)[:, None] >> np.arange(Qm - 1, -1, -1)[None, :]) & 1).astype(np.uint8)
+    np.testing.assert_allclose(np.mean(np.abs(S.modulate(allb.reshape(-1), Qm)) ** 2), 1.0, rtol=1e-6)
+    llr = ora.demod_s(mod, sym)
+    assert np.all(llr != 0)
+    assert np.array_equal((llr > 0).astype(np.uint8), bits)
+
+
+def test_cdd_roundtrip(ora):
+    """CDD precoding then the reference-pinned MMSE predecoder with the exact channel returns x"""
+    rng = np.random.default_rng(5)
+    n = 256
+    x = [S.modulate(rng.integers(0, 2, 6 * n, dtype=np.uint8), 6) for _ in range(2)]
+    y = S.precode(x, "cdd")
+    Hm = np.array([[1, 1], [1, -1]], np.complex64)
+    r = [(Hm[i, 0] * y[0] + Hm[i, 1] * y[1]).astype(np.complex64) for i in range(2)]
+    h = np.zeros((2, 2, n), np.complex64)
+    for p in range(2):
+        for i in range(2):
+            h[p, i] = Hm[i, p]
+    xe, _ = ora.predecode(3, np.stack(r), h, 2, 0, 1.0, 1e-6)
+    np.testing.assert_allclose(xe[0], x[0], atol=1e-3)
+    np.testing.assert_allclose(xe[1], x[1], atol=1e-3)

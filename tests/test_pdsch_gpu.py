@@ -58,7 +58,8 @@ CASES = [
     dict(scheme="sm", pmi=0),                               # TM4 codebook 1
     dict(scheme="sm", pmi=1, cell_id=7),                    # TM4 codebook 2
     dict(nports=1, scheme="port0", tbs=(30576,), Qm=(4,), cell_id=3, channel=[[1], [0.5 + 0.5j]]),
-    dict(nof_prb=50, cell_id=11, tbs=(36696, 36696), tti=3, cfi=3),
+    dict(nof_prb=50, cell_id=11, tbs=(36696, 36696), tti=3, cfi=1),
+    dict(nof_prb=50, cell_id=11, tbs=(25456, 25456), tti=4, cfi=3),
     dict(nof_prb=6, cell_id=2, tbs=(1800, 1800), Qm=(4, 4), cfi=2, tti=7),
 ]
 

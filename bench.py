@@ -4,9 +4,12 @@
 A "step" is one pass of the hot path over one batch of synthetic input:
   workload "all188" (default, BASELINE configs[1]): 1024 code blocks of EACH of the
       188 LTE sizes, 8 half-iterations, rm_turbo sub-block input layout;
-  workload "k6144" (BASELINE configs[0] shape on the GPU): 1024 x 6144-bit blocks.
-Inputs are AWGN code blocks (turbodecoder_test.c convention) resident in HBM before
-the timed region; every launch decodes the full batch (no early stop, no caching).
+  workload "k6144" (BASELINE configs[0] shape on the GPU): 1024 x 6144-bit blocks;
+  workload "dlsch": srsran_dlsch_decode of C3 transport blocks (rate dematch + turbo + CRC);
+  workload "pdsch" (BASELINE configs[2], C3): the whole UE DL chain from time-domain samples --
+      OFDM, CRS channel estimation, MMSE predecoding, demap/descramble/CSI, DL-SCH decode.
+Inputs come from the synthetic eNB transmitter (synth/, not the oracle) and are resident in
+HBM before the timed region; every step decodes the full batch (no caching).
 
 Multi-GPU: one process per GPU (torch.distributed.run); every rank decodes its own
 batch (units partition with no data-path collective, "weak" scaling); the only
@@ -40,7 +43,8 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--workload", choices=["all188", "k6144", "dlsch"], default="all188")
+    p.add_argument("--workload", choices=["all188", "k6144", "dlsch", "pdsch"], default="all188")
+    p.add_argument("--snr", type=float, default=30.0, help="pdsch: AWGN SNR (dB) of the synthetic subframes")
     p.add_argument("--subframes", type=int, default=64, help="dlsch: subframes (2 TBs each) per step")
     p.add_argument("--sigma", type=float, default=0.42, help="dlsch: AWGN std on +-1 symbols before LLR scaling")
     p.add_argument("--batch", type=int, default=1024, help="code blocks per size per step")
@@ -50,14 +54,14 @@ def parse():
     return p.parse_args()
 
 
-def make_inputs(ora, Ks, pool, batch, rng, torch, device):
+def make_inputs(Ks, pool, batch, rng, torch, device):
     """Per size: `pool` AWGN code blocks (Eb/No label 4 dB) in SB layout, tiled to `batch` rows on device."""
-    from oracle import make_llrs
+    from synth import synth as SY
 
     data = {}
     for K in Ks:
-        _, llr = make_llrs(K, 4.0, rng, pool, ora)
-        sb = np.stack([ora.natural_to_sb(K, x) for x in llr])
+        _, llr = SY.make_llrs(K, 4.0, rng, pool)
+        sb = SY.natural_to_sb(K, llr)
         reps = (batch + pool - 1) // pool
         host = np.tile(sb, (reps, 1))[:batch]
         d_in = torch.from_numpy(np.ascontiguousarray(host)).to(device)
@@ -108,16 +112,15 @@ def run_dlsch(args, torch, dist, world, rank, device):
     """DL-SCH decode of C3 subframes: per step `subframes` x 2 TBs (TBS 75376, 13 x K=5824 CBs,
     86400 LLRs each), new transmissions, CRC early stop, at most `iters` half-iterations.
     Value = decoded TB info bits / s (PDSCH Mbps at the DL-SCH stage) and subframes/s."""
-    from oracle import Oracle
+    from synth import synth as SY
     from srsran_4g_amd import sch as S
 
-    ora = Oracle()
     rng = np.random.default_rng(0x5EED + rank)
     ntb = 2 * args.subframes
     pool = []
     for _ in range(args.pool):
         tb = rng.integers(0, 256, C3_TBS // 8, dtype=np.uint8)
-        e = ora.dlsch_encode(C3_TBS, C3_QM, 0, C3_BITS, tb).astype(np.float32) * 2 - 1
+        e = SY.dlsch_encode(C3_TBS, C3_QM, 0, C3_BITS, tb).astype(np.float32) * 2 - 1
         y = e + rng.standard_normal(e.shape).astype(np.float32) * args.sigma
         pool.append(np.trunc(100 * y).astype(np.int16))
     host = np.stack([pool[i % args.pool] for i in range(ntb)])
@@ -206,9 +209,9 @@ def run_dlsch(args, torch, dist, world, rank, device):
         },
     }
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        from oracle import Reference, ref_available
+        from oracle import Oracle, Reference, ref_available
         kind = "reference" if ref_available() else "port"
-        dec = Reference() if kind == "reference" else ora
+        dec = Reference() if kind == "reference" else Oracle()
         n = 0
         t0 = time.perf_counter()
         while time.perf_counter() - t0 < args.cpu_seconds:
@@ -229,12 +232,208 @@ def run_dlsch(args, torch, dist, world, rank, device):
         print(json.dumps(result), flush=True)
 
 
+C3_NRE = {0: 13992, 5: 14256}  # PDSCH REs of the C3 grant per subframe index (others: 14400)
+SF_LEN = 30720                  # 20 MHz, N = 2048 (standard sampling rate)
+
+
+def stage_bytes(nsf, nre_sum, ntb):
+    """Algorithmic HBM bytes per launch of each stage kernel for nsf C3 subframes (2 rx, 2 ports):
+    the inputs each kernel must read once and the outputs it must write once."""
+    nrx, ports, nre_row = 2, 2, 1200
+    K, C = 5824, 13
+    return {
+        "ofdm_rx_kernel": nsf * nrx * (SF_LEN + 14 * nre_row) * 8,
+        "chest_kernel": nsf * ports * nrx * (4 * nre_row * 8 + nre_row * 8),
+        "predecode_batch_kernel": nre_sum * (nrx * 8 + 4 + 2 * 8 + 2 * 4) + nsf * ports * nrx * nre_row * 8,
+        "llr_batch_kernel": nre_sum * 2 * (8 + 4 + 6 * 2),
+        "rm_rx_kernel": ntb * (C3_BITS * 2 + C * (3 * (K + 32) + 12) * 2),
+        "tdec_kernel": ntb * C * ((3 * (K + 32) + 12) * 2 + K // 8),
+        "tb_kernel": ntb * (C * K // 8 + C3_TBS // 8),
+    }
+
+
+def run_pdsch(args, torch, dist, world, rank, device):
+    """UE DL chain on C3 subframes: per step `subframes` subframes of 2 rx x 30720 cf32 samples
+    -> 2 TBs each (TBS 75376, 64QAM, TM3 CDD 2x2, CFI 1), new transmissions, at most `iters`
+    half-iterations with CRC early stop.  Value = decoded PDSCH info Mbps; also subframes/s."""
+    from synth import synth as SY
+    from srsran_4g_amd import prof
+    from srsran_4g_amd import sch as S
+    from srsran_4g_amd import ue_dl as U
+
+    rng = np.random.default_rng(0x5EED + rank)
+    cell_id = 1 + rank  # C4: an independent carrier per GPU
+    rnti = 0x1234
+    pool = []
+    for i in range(10):  # one subframe of each index (tti 1..10 -> sf 1..9, 0)
+        tti = i + 1
+        pls = [rng.integers(0, 256, C3_TBS // 8, dtype=np.uint8) for _ in range(2)]
+        x, nre = SY.pdsch_subframe(100, cell_id, 2, tti, 1, rnti, C3_TBS, C3_QM, 0, pls, snr_db=args.snr, rng=rng)
+        pool.append((tti, x, nre, pls))
+    nsf = args.subframes
+    host = np.stack([pool[b % 10][1] for b in range(nsf)])
+    d_x = torch.from_numpy(np.ascontiguousarray(host).view(np.float32)).to(device)
+    ue = U.UeDl(U.cell(100, 2, cell_id), 2)
+    ue.cfg.cfg.pdsch.max_nof_iterations = args.iters
+    sbs = [[S.SoftbufferRx(nof_prb=100) for _ in range(2)] for _ in range(nsf)]
+    cfgs = [U.pdsch_cfg(100, pool[b % 10][2], (C3_TBS, C3_TBS), (C3_QM, C3_QM), rnti=rnti,
+                        max_iterations=args.iters, softbuffers=sbs[b]) for b in range(nsf)]
+    d_pl = torch.zeros((nsf, 2, C3_TBS // 8 + 64), dtype=torch.uint8, device=device)
+    d_res = torch.zeros(2 * nsf, dtype=torch.int32, device=device)
+    d_avg = torch.zeros(2 * nsf, dtype=torch.float32, device=device)
+    arr = U.UeDl.batch_entries([(pool[b % 10][0], 1, cfgs[b], [d_pl[b, 0].data_ptr(), d_pl[b, 1].data_ptr()], [1, 1])
+                                for b in range(nsf)])
+    stream = torch.cuda.current_stream(device)
+    sp = stream.cuda_stream
+
+    def step():
+        if ue.gpu_decode_batch(arr, d_x.data_ptr(), d_res.data_ptr(), d_avg.data_ptr(), 0.0, sp) != 2 * nsf:
+            raise RuntimeError("srsran_ue_dl_gpu_decode_batch failed")
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    res = d_res.cpu().numpy()
+    avg = d_avg.cpu().numpy()
+    pl = d_pl.cpu().numpy()
+    ok = sum(int(np.array_equal(pl[b, q, : C3_TBS // 8], pool[b % 10][3][q])) for b in range(nsf) for q in range(2))
+    value = world * nsf * 2 * C3_TBS * args.steps / elapsed / 1e6
+
+    # per-stage kernel durations from HIP events on the launch streams (library-side), same batch
+    prof.enable(True)
+    nrep = max(1, min(args.steps, 3))
+    for _ in range(nrep):
+        step()
+    torch.cuda.synchronize()
+    stages = prof.read()
+    prof.enable(False)
+    nre_sum = sum(pool[b % 10][2] for b in range(nsf))
+    sb = stage_bytes(nsf, nre_sum, 2 * nsf)
+    per_stage = {}
+    for name, (ms, n) in stages.items():
+        avg_ms = ms / n
+        launches_per_step = n / nrep
+        byts = sb.get(name, 0) / launches_per_step
+        per_stage[name] = {"ms_per_step": round(ms / nrep, 4), "launches_per_step": launches_per_step,
+                           "avg_launch_ms": round(avg_ms, 4), "GBps": round(byts / (avg_ms * 1e-3) / 1e9, 1)}
+    dom = max(per_stage, key=lambda k: per_stage[k]["ms_per_step"])
+    d = per_stage[dom]
+    bytes_per_launch = sb[dom] / d["launches_per_step"]
+    achieved = bytes_per_launch / (d["avg_launch_ms"] * 1e-3) / 1e9
+    traffic = None
+    tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(tf):
+        try:
+            traffic = json.load(open(tf)).get(args.workload, {}).get(dom)
+        except Exception:
+            traffic = None
+    result = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "Mbps",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32+int16",
+        "data": f"synthetic: eNB-side TX (synth/: DL-SCH encode, scrambling, 64QAM, CDD, CRS, OFDM) through "
+                f"[[1,1],[1,-1]] + AWGN {args.snr} dB; 10 distinct subframes (indices 0-9) tiled, HBM-resident",
+        "config": {
+            "workload": f"pdsch C3: {nsf} subframes x (2 rx x {SF_LEN} cf32 samples -> OFDM 2048 -> CRS chest -> "
+                        f"MMSE CDD 2x2 -> 64QAM LLR -> 2 TBs x {C3_TBS} bits), CFI 1, max {args.iters} half-its",
+            "subframes_per_step_per_gpu": nsf,
+            "subframes_per_s": round(world * nsf * args.steps / elapsed, 1),
+            "tb_ok_fraction": round(ok / (2 * nsf), 4),
+            "avg_half_iterations": round(float(avg.mean()), 3),
+            "cell_id": cell_id,
+            "parallelism": f"carrier-per-gpu x{world}",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": dom,
+            "achieved": round(achieved, 2),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5),
+            "traffic": traffic,
+            "avg_launch_ms": d["avg_launch_ms"],
+            "algo_bytes_per_launch": int(bytes_per_launch),
+        },
+        "stages": per_stage,
+        "chain_bytes_per_sf": 2 * SF_LEN * 8 + 2 * C3_TBS // 8,
+    }
+    if (res != 0).any():
+        result["config"]["tb_fail"] = int((res != 0).sum())
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        result["cpu_baseline"] = pdsch_cpu_baseline(pool, args)
+    elif rank == 0:
+        result["cpu_baseline"] = None
+    ue.free()
+    for pair in sbs:
+        for s_ in pair:
+            s_.free()
+    if world > 1:
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+
+
+def pdsch_cpu_baseline(pool, args):
+    """The reference's compiled PDSCH pieces (oracle/_ref: predecoding, demod_soft, sequence, DL-SCH
+    decode_tb over rm_turbo/turbodecoder/crc) with the oracle's C channel estimator and numpy's FFT
+    (FFTW is not in the image) on one host thread, over the same subframes."""
+    import pdsch_chain as PC
+    from oracle import Oracle, Reference, ref_available
+
+    ora = Oracle()
+    ref = Reference() if ref_available() else None
+
+    class Hybrid:
+        def __getattr__(self, name):
+            if ref is not None and name in ("predecode", "demod_s", "sequence_apply_s", "dlsch_decode"):
+                return getattr(ref, name)
+            return getattr(ora, name)
+
+    h = Hybrid()
+    n = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < args.cpu_seconds:
+        tti, x, nre, _ = pool[n % len(pool)]
+        g, ce, st = PC.fft_estimate(ora, x, 100, 1, 2, tti)
+        PC.pdsch_decode(h, g, ce, st["noise"], 100, 1, 2, tti, 1, 0x1234, [C3_TBS, C3_TBS], [C3_QM, C3_QM], [0, 0],
+                        max_iterations=args.iters)
+        n += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(n * 2 * C3_TBS / dt / 1e6, 3), "unit": "Mbps", "cores": 1,
+            "kind": "reference" if ref is not None else "port",
+            "subframes_per_s": round(n / dt, 2),
+            "sample": f"{n} C3 subframes, {dt:.1f} s on 1 thread: reference-compiled predecoding / demod / "
+                      f"descrambling / DL-SCH; oracle C channel estimator; numpy FFT (FFTW absent)"
+                      if ref is not None else f"{n} C3 subframes, {dt:.1f} s on 1 thread (oracle C port + numpy FFT)"}
+
+
 def main():
     args = parse()
     import torch
     import torch.distributed as dist
 
-    from oracle import Oracle
     from srsran_4g_amd import tdec
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -248,11 +447,12 @@ def main():
         raise RuntimeError("bench: HIP device not visible to libsrsran_4g_amd")
     if args.workload == "dlsch":
         return run_dlsch(args, torch, dist, world, rank, device)
+    if args.workload == "pdsch":
+        return run_pdsch(args, torch, dist, world, rank, device)
 
     Ks = list(tdec.CB_SIZES) if args.workload == "all188" else [6144]
-    ora = Oracle()
     rng = np.random.default_rng(0x5EED + rank)
-    data = make_inputs(ora, Ks, args.pool, args.batch, rng, torch, device)
+    data = make_inputs(Ks, args.pool, args.batch, rng, torch, device)
     stream = torch.cuda.current_stream(device)
     sp = stream.cuda_stream
 

@@ -1,0 +1,26 @@
+/*
+ * include/srsran_amd_prof.h -- added diagnostics: HIP-event timing of the GPU pipeline's kernel
+ * launches per stage (no counterpart in the reference).  Stages: 0 OFDM, 1 channel estimation,
+ * 2 predecoding, 3 demap/descramble/CSI, 4 rate dematching, 5 turbo decoding, 6 TB CRC / output.
+ */
+#ifndef SRSRAN_AMD_PROF_H
+#define SRSRAN_AMD_PROF_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SRSRAN_AMD_NOF_STAGES 7
+
+/* start (non-zero) or stop recording; clears the accumulators */
+void srsran_amd_timing_enable(int enable);
+/* waits for the recorded launches, returns per-stage total ms and launch counts, clears them */
+int srsran_amd_timing_read(float ms[SRSRAN_AMD_NOF_STAGES], uint32_t launches[SRSRAN_AMD_NOF_STAGES]);
+/* the kernel name of a stage (as rocprofv3 reports it, without template arguments) */
+const char* srsran_amd_stage_name(int stage);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

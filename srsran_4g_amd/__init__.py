@@ -7,3 +7,4 @@ from . import tdec  # noqa: F401
 from . import sch  # noqa: F401
 from . import phch  # noqa: F401
 from . import ue_dl  # noqa: F401
+from . import prof  # noqa: F401

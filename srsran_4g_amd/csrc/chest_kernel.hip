@@ -15,6 +15,7 @@
 #include <stdint.h>
 
 #include "chest_kernel.h"
+#include "stage_timing.h"
 
 #pragma clang fp contract(off)
 
@@ -251,6 +252,7 @@ __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
 
 hipError_t chest_launch(const ChestArgs& a, hipStream_t stream, uint32_t nsf)
 {
+  StageScope timing_scope(ST_CHEST, stream);
   if (nsf == 0) {
     return hipSuccess;
   }
@@ -301,6 +303,7 @@ __global__ void chest_finalize_kernel(const float* stats, uint32_t np, uint32_t 
 hipError_t chest_finalize_launch(const float* stats, uint32_t np, uint32_t nrx, uint32_t nof_prb, float symbol_sz,
                                  float* out, uint32_t nsf, hipStream_t stream)
 {
+  StageScope timing_scope(ST_CHEST, stream);
   if (nsf == 0) {
     return hipSuccess;
   }

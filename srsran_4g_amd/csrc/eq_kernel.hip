@@ -15,6 +15,7 @@
 #include <stdint.h>
 
 #include "eq_kernel.h"
+#include "stage_timing.h"
 
 #pragma clang fp contract(off)
 
@@ -183,6 +184,7 @@ __global__ __launch_bounds__(EQ_THREADS) void predecode_batch_kernel(const PredA
 hipError_t predecode_batch_launch(const PredArgs* d_items, uint32_t nitems, int scheme, uint32_t max_n,
                                   hipStream_t stream)
 {
+  StageScope timing_scope(ST_PRED, stream);
   if (nitems == 0 || max_n == 0) {
     return hipSuccess;
   }
@@ -205,6 +207,7 @@ hipError_t predecode_batch_launch(const PredArgs* d_items, uint32_t nitems, int 
 
 hipError_t predecode_launch(const PredArgs& a, hipStream_t stream)
 {
+  StageScope timing_scope(ST_PRED, stream);
   if (a.n == 0) {
     return hipSuccess;
   }

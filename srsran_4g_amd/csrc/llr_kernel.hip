@@ -16,6 +16,7 @@
 #include <stdint.h>
 
 #include "llr_kernel.h"
+#include "stage_timing.h"
 
 namespace srsran_amd {
 
@@ -342,6 +343,7 @@ __global__ __launch_bounds__(LLR_THREADS) void llr_batch_kernel(const LlrItem* _
 hipError_t llr_batch_launch(int mod, const LlrItem* d_items, uint32_t nitems, uint32_t max_n, int any_scramble,
                             hipStream_t stream)
 {
+  StageScope timing_scope(ST_LLR, stream);
   if (nitems == 0 || max_n == 0) {
     return hipSuccess;
   }
@@ -377,6 +379,7 @@ hipError_t llr_batch_launch(int mod, const LlrItem* d_items, uint32_t nitems, ui
 hipError_t llr_launch(int mod, const float* d_sym, uint32_t nsym, int scramble, uint32_t seed, uint32_t bit0,
                       const float* d_csi, const float* d_csi_max, int16_t* d_llr, hipStream_t stream)
 {
+  StageScope timing_scope(ST_LLR, stream);
   if (nsym == 0) {
     return hipSuccess;
   }
@@ -438,6 +441,7 @@ __global__ __launch_bounds__(LLR_THREADS) void seq_apply_kernel(const int16_t* _
 
 hipError_t seq_apply_launch(const int16_t* d_in, int16_t* d_out, uint32_t len, uint32_t seed, hipStream_t stream)
 {
+  StageScope timing_scope(ST_LLR, stream);
   if (len == 0) {
     return hipSuccess;
   }

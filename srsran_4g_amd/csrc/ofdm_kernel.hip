@@ -15,6 +15,7 @@
 #include <stdint.h>
 
 #include "ofdm_kernel.h"
+#include "stage_timing.h"
 
 namespace srsran_amd {
 
@@ -178,6 +179,7 @@ int ofdm_plan(uint32_t N, int* radix)
 
 hipError_t ofdm_rx_launch(const OfdmArgs& a, uint32_t nsf, hipStream_t stream)
 {
+  StageScope timing_scope(ST_OFDM, stream);
   if (a.N > OFDM_MAX_N || a.nstages <= 0 || nsf == 0) {
     return hipErrorInvalidValue;
   }
@@ -200,6 +202,7 @@ __global__ void cfo_kernel(const float2* __restrict__ in, float2* __restrict__ o
 
 hipError_t cfo_launch(const float2* in, float2* out, uint32_t n, double f, hipStream_t stream)
 {
+  StageScope timing_scope(ST_OFDM, stream);
   if (n == 0) {
     return hipSuccess;
   }

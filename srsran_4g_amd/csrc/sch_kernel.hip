@@ -19,6 +19,7 @@
 #include "crc24_dev.h"
 #include "sch_kernel.h"
 #include "tdec_kernel.h"
+#include "stage_timing.h"
 
 namespace srsran_amd {
 
@@ -305,6 +306,7 @@ __global__ __launch_bounds__(TB_THREADS) void tb_kernel(const SchTb* __restrict_
 
 hipError_t rm_rx_launch(const RmSlot* d_slots, uint32_t nslots, uint32_t max_len, hipStream_t stream)
 {
+  StageScope timing_scope(ST_RM, stream);
   const uint32_t per_block = RM_THREADS * RM_PER_THREAD;
   const uint32_t gx        = (max_len + per_block - 1) / per_block;
   for (uint32_t s0 = 0; s0 < nslots; s0 += 65535) {
@@ -316,6 +318,7 @@ hipError_t rm_rx_launch(const RmSlot* d_slots, uint32_t nslots, uint32_t max_len
 
 hipError_t tb_launch(const SchTb* d_tbs, uint32_t ntb, hipStream_t stream)
 {
+  StageScope timing_scope(ST_TB, stream);
   if (ntb == 0) {
     return hipSuccess;
   }

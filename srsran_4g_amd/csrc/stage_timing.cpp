@@ -1,0 +1,119 @@
+// srsran_4g_amd/csrc/stage_timing.cpp -- per-stage kernel timing with HIP events on the launch
+// stream (bench.py reads it to report the dominant kernel's average launch duration live).
+#include "stage_timing.h"
+
+#include <atomic>
+#include <mutex>
+#include <vector>
+
+#include "../../include/srsran_amd_prof.h"
+
+namespace srsran_amd {
+namespace {
+
+std::atomic<bool> g_on{false};
+std::mutex        g_mu;
+struct Rec {
+  int        stage;
+  hipEvent_t e0, e1;
+};
+std::vector<Rec>        g_pending;
+std::vector<hipEvent_t> g_pool;
+double                  g_ms[ST_COUNT];
+uint32_t                g_n[ST_COUNT];
+
+hipEvent_t take()
+{
+  if (!g_pool.empty()) {
+    hipEvent_t e = g_pool.back();
+    g_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  hipEventCreate(&e);
+  return e;
+}
+
+void drain()  // caller holds g_mu
+{
+  for (const Rec& r : g_pending) {
+    float ms = 0.f;
+    if (hipEventSynchronize(r.e1) == hipSuccess && hipEventElapsedTime(&ms, r.e0, r.e1) == hipSuccess) {
+      g_ms[r.stage] += ms;
+      g_n[r.stage]++;
+    }
+    g_pool.push_back(r.e0);
+    g_pool.push_back(r.e1);
+  }
+  g_pending.clear();
+}
+
+}  // namespace
+
+StageScope::StageScope(int stage, hipStream_t stream) : stage_(stage), stream_(stream)
+{
+  if (!g_on.load(std::memory_order_relaxed)) {
+    return;
+  }
+  std::lock_guard<std::mutex> lk(g_mu);
+  e0_ = take();
+  if (e0_) {
+    hipEventRecord(e0_, stream_);
+  }
+}
+
+StageScope::~StageScope()
+{
+  if (!e0_) {
+    return;
+  }
+  std::lock_guard<std::mutex> lk(g_mu);
+  hipEvent_t e1 = take();
+  if (!e1) {
+    g_pool.push_back(e0_);
+    return;
+  }
+  hipEventRecord(e1, stream_);
+  g_pending.push_back(Rec{stage_, e0_, e1});
+  if (g_pending.size() > 4096) {
+    drain();
+  }
+}
+
+}  // namespace srsran_amd
+
+using namespace srsran_amd;
+
+extern "C" void srsran_amd_timing_enable(int enable)
+{
+  std::lock_guard<std::mutex> lk(g_mu);
+  drain();
+  for (int i = 0; i < ST_COUNT; i++) {
+    g_ms[i] = 0;
+    g_n[i]  = 0;
+  }
+  g_on.store(enable != 0);
+}
+
+extern "C" int srsran_amd_timing_read(float ms[SRSRAN_AMD_NOF_STAGES], uint32_t launches[SRSRAN_AMD_NOF_STAGES])
+{
+  if (!ms || !launches) {
+    return -1;
+  }
+  std::lock_guard<std::mutex> lk(g_mu);
+  drain();
+  for (int i = 0; i < ST_COUNT; i++) {
+    ms[i]       = (float)g_ms[i];
+    launches[i] = g_n[i];
+    g_ms[i]     = 0;
+    g_n[i]      = 0;
+  }
+  return 0;
+}
+
+extern "C" const char* srsran_amd_stage_name(int stage)
+{
+  static const char* names[ST_COUNT] = {"ofdm_rx_kernel", "chest_kernel", "predecode_batch_kernel",
+                                        "llr_batch_kernel", "rm_rx_kernel", "tdec_kernel", "tb_kernel"};
+  return stage >= 0 && stage < ST_COUNT ? names[stage] : "";
+}

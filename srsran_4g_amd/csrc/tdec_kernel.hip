@@ -27,6 +27,7 @@
 
 #include "crc24_dev.h"
 #include "tdec_kernel.h"
+#include "stage_timing.h"
 
 namespace srsran_amd {
 
@@ -752,6 +753,7 @@ __global__ __launch_bounds__(128, 2) void tdec_kernel(TdecArgs a)
 template <int NSB>
 static hipError_t launch(const TdecArgs& a, hipStream_t stream)
 {
+  StageScope timing_scope(ST_TDEC, stream);
   const int    cpw  = Geo<NSB>::CPW;
   const int    grid = (a.ncb + cpw - 1) / cpw;
   const size_t lds  = tdec_lds_bytes(NSB, a.xyw, a.M);

@@ -398,17 +398,23 @@ class UeDl:
         ret = lib().srsran_ue_dl_decode_pdsch(ctypes.byref(self.q), ctypes.byref(sf), ctypes.byref(cfg), data)
         return ret, [(data[i].crc, pls[i], data[i].avg_iterations_block) for i in range(ntb)]
 
-    def gpu_decode_batch(self, sfs, d_samples, d_result, d_avg, cfo=0.0, stream=None):
-        """sfs: list of (tti, cfi, srsran_pdsch_cfg_t, [d_payload ptrs], [new_data])."""
+    @staticmethod
+    def batch_entries(sfs):
+        """sfs: list of (tti, cfi, srsran_pdsch_cfg_t, [d_payload ptrs], [new_data]) -> ctypes array
+        (keep the cfg objects alive while the array is used)."""
         arr = (srsran_ue_dl_gpu_sf_t * len(sfs))()
-        self._keep = [s[2] for s in sfs]
         for i, (tti, cfi, cfg, pls, nd) in enumerate(sfs):
             arr[i].tti, arr[i].cfi = tti, cfi
             arr[i].pdsch_cfg = ctypes.pointer(cfg)
             for t, p in enumerate(pls):
                 arr[i].d_payload[t] = p
                 arr[i].new_data[t] = nd[t]
-        return lib().srsran_ue_dl_gpu_decode_batch(ctypes.byref(self.q), ctypes.byref(self.cfg), len(sfs), arr,
+        return arr
+
+    def gpu_decode_batch(self, sfs, d_samples, d_result, d_avg, cfo=0.0, stream=None):
+        """srsran_ue_dl_gpu_decode_batch; sfs: entry list (see batch_entries) or a prebuilt array."""
+        arr = sfs if isinstance(sfs, ctypes.Array) else self.batch_entries(sfs)
+        return lib().srsran_ue_dl_gpu_decode_batch(ctypes.byref(self.q), ctypes.byref(self.cfg), len(arr), arr,
                                                    d_samples, cfo, d_result, d_avg, stream)
 
     def free(self):

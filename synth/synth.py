@@ -73,6 +73,33 @@ def make_llrs(K, ebno_db, rng, n=1):
     return bits, llr
 
 
+def nof_subblocks(K):
+    """sub-blocks of srsRAN's AVX2 window decoder for K (turbodecoder.c:381-393)"""
+    if K % 16 == 0 and K > 800:
+        return 16
+    if K % 8 == 0 and K > 400:
+        return 8
+    return 0
+
+
+def natural_to_sb(K, llr):
+    """natural 3K+12 decoder input -> the sub-block layout 3(K+32)+12 that srsran_rm_turbo_rx_lut
+    writes for window decoders (rm_turbo.c:249-273): d^(j)_n goes to j(K+32) + (n % L) nsb + n / L,
+    L = K / nsb; the 12 tail values follow at 3(K+32)."""
+    llr = np.asarray(llr)
+    nsb = nof_subblocks(K)
+    if nsb == 0:
+        return llr.copy()
+    L = K // nsb
+    n = np.arange(K)
+    pos = (n % L) * nsb + n // L
+    out = np.zeros(llr.shape[:-1] + (3 * (K + 32) + 12,), llr.dtype)
+    for j in range(3):
+        out[..., j * (K + 32) + pos] = llr[..., j: 3 * K: 3]
+    out[..., 3 * (K + 32):] = llr[..., 3 * K:]
+    return out
+
+
 def dlsch_encode(tbs, Qm, rv, G, tb_bytes, Nl=1, tb_crc_xor=0):
     """36.212 5.3.2 for one TB -> G coded bits (uint8)"""
     tb = np.ascontiguousarray(tb_bytes, np.uint8)

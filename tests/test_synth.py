@@ -95,3 +95,20 @@ def test_cdd_roundtrip(ora):
     xe, _ = ora.predecode(3, np.stack(r), h, 2, 0, 1.0, 1e-6)
     np.testing.assert_allclose(xe[0], x[0], atol=1e-3)
     np.testing.assert_allclose(xe[1], x[1], atol=1e-3)
+
+
+def test_natural_to_sb(ora):
+    rng = np.random.default_rng(9)
+    for K in (40, 408, 512, 800, 1024, 6144, 6080, 4008):
+        x = rng.integers(-300, 300, 3 * K + 12).astype(np.int16)
+        assert np.array_equal(S.natural_to_sb(K, x), ora.natural_to_sb(K, x)), K
+    x = rng.integers(-300, 300, (3, 3 * 6144 + 12)).astype(np.int16)
+    assert np.array_equal(S.natural_to_sb(6144, x)[1], ora.natural_to_sb(6144, x[1]))
+
+
+def test_make_llrs_matches_oracle_generator():
+    from oracle import make_llrs
+    for K in (6144, 40):
+        b1, l1 = S.make_llrs(K, 4.0, np.random.default_rng(K), 3)
+        b2, l2 = make_llrs(K, 4.0, np.random.default_rng(K), 3)
+        assert np.array_equal(b1, b2) and np.array_equal(l1, l2)

@@ -62,22 +62,41 @@ __device__ __forceinline__ void mmse_csi(cpx y0, cpx y1, cpx h00, cpx h01, cpx h
   csi1            = 1.0f / b11.r;
 }
 
-__device__ __forceinline__ void wave_max_atomic(uint32_t* dst, float v, bool valid)
+// block-wide max of the per-thread CSI maxima (csi >= 0: IEEE bits order like the values), then
+// one atomicMax per block and layer
+template <int NL>
+__device__ __forceinline__ void block_max_atomic(uint32_t* dst, const uint32_t (&v)[NL], uint32_t* red)
 {
-  uint32_t b = valid ? __float_as_uint(v) : 0u;  // csi >= 0: IEEE bits order like the values
+  uint32_t b[NL];
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    b = max(b, (uint32_t)__shfl_xor((int)b, off, 64));
+  for (int l = 0; l < NL; l++) {
+    b[l] = v[l];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      b[l] = max(b[l], (uint32_t)__shfl_xor((int)b[l], off, 64));
+    }
   }
+  const int w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
-    atomicMax(dst, b);
+#pragma unroll
+    for (int l = 0; l < NL; l++) {
+      red[w * NL + l] = b[l];
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < NL) {
+    uint32_t m = 0;
+    for (int i = 0; i < (int)(blockDim.x >> 6); i++) {
+      m = max(m, red[i * NL + threadIdx.x]);
+    }
+    atomicMax(&dst[threadIdx.x], m);
   }
 }
 
 static constexpr int EQ_THREADS = 256;
 
 template <int SCHEME>
-__device__ __forceinline__ void predecode_item(const PredArgs& a, uint32_t k)
+__device__ __forceinline__ void predecode_item(const PredArgs& a, uint32_t k, uint32_t (&mx)[2])
 {
   const bool     valid = k < a.n;
   const uint32_t kk    = valid ? k : 0;
@@ -112,8 +131,8 @@ __device__ __forceinline__ void predecode_item(const PredArgs& a, uint32_t k)
       a.csi[0][k] = csi;
       a.x[0][k]   = make_float2(t.r / csi, t.i / csi);
     }
-    if (a.csi_max) {
-      wave_max_atomic(&a.csi_max[0], csi, valid);
+    if (valid) {
+      mx[0] = max(mx[0], __float_as_uint(csi));
     }
   } else {
     const cpx p0 = ld(a.h[0][0], gh), p1 = ld(a.h[0][1], gh), q0 = ld(a.h[1][0], gh), q1 = ld(a.h[1][1], gh);
@@ -157,9 +176,30 @@ __device__ __forceinline__ void predecode_item(const PredArgs& a, uint32_t k)
       a.csi[0][k] = c0;
       a.csi[1][k] = c1;
     }
-    if (a.csi_max) {
-      wave_max_atomic(&a.csi_max[0], c0, valid);
-      wave_max_atomic(&a.csi_max[1], c1, valid);
+    if (valid) {
+      mx[0] = max(mx[0], __float_as_uint(c0));
+      mx[1] = max(mx[1], __float_as_uint(c1));
+    }
+  }
+}
+
+static constexpr int EQ_RPT = 4;  // REs per thread (strided by the block size: coalesced)
+
+template <int SCHEME>
+__device__ __forceinline__ void predecode_block(const PredArgs& a, uint32_t k0)
+{
+  __shared__ uint32_t red[2 * EQ_THREADS / 64];
+  uint32_t            mx[2] = {0u, 0u};
+#pragma unroll
+  for (int r = 0; r < EQ_RPT; r++) {
+    predecode_item<SCHEME>(a, k0 + r * EQ_THREADS + threadIdx.x, mx);
+  }
+  if (a.csi_max) {
+    if constexpr (SCHEME == 0) {
+      const uint32_t m1[1] = {mx[0]};
+      block_max_atomic<1>(a.csi_max, m1, red);
+    } else {
+      block_max_atomic<2>(a.csi_max, mx, red);
     }
   }
 }
@@ -167,18 +207,18 @@ __device__ __forceinline__ void predecode_item(const PredArgs& a, uint32_t k)
 template <int SCHEME>
 __global__ __launch_bounds__(EQ_THREADS) void predecode_kernel(PredArgs a)
 {
-  predecode_item<SCHEME>(a, blockIdx.x * EQ_THREADS + threadIdx.x);
+  predecode_block<SCHEME>(a, blockIdx.x * EQ_THREADS * EQ_RPT);
 }
 
 template <int SCHEME>
 __global__ __launch_bounds__(EQ_THREADS) void predecode_batch_kernel(const PredArgs* __restrict__ items)
 {
-  const PredArgs& a = items[blockIdx.y];
-  const uint32_t  k = blockIdx.x * EQ_THREADS + threadIdx.x;
-  if (blockIdx.x * EQ_THREADS >= a.n) {
-    return;  // whole block past this item's end (uniform exit keeps the wave reductions intact)
+  const PredArgs& a  = items[blockIdx.y];
+  const uint32_t  k0 = blockIdx.x * EQ_THREADS * EQ_RPT;
+  if (k0 >= a.n) {
+    return;  // whole block past this item's end (uniform: the block reduction stays intact)
   }
-  predecode_item<SCHEME>(a, k);
+  predecode_block<SCHEME>(a, k0);
 }
 
 hipError_t predecode_batch_launch(const PredArgs* d_items, uint32_t nitems, int scheme, uint32_t max_n,
@@ -188,7 +228,7 @@ hipError_t predecode_batch_launch(const PredArgs* d_items, uint32_t nitems, int 
   if (nitems == 0 || max_n == 0) {
     return hipSuccess;
   }
-  const dim3 grid((max_n + EQ_THREADS - 1) / EQ_THREADS, nitems);
+  const dim3 grid((max_n + EQ_THREADS * EQ_RPT - 1) / (EQ_THREADS * EQ_RPT), nitems);
   switch (scheme) {
     case 0:
       hipLaunchKernelGGL(predecode_batch_kernel<0>, grid, dim3(EQ_THREADS), 0, stream, d_items);
@@ -211,7 +251,7 @@ hipError_t predecode_launch(const PredArgs& a, hipStream_t stream)
   if (a.n == 0) {
     return hipSuccess;
   }
-  const dim3 grid((a.n + EQ_THREADS - 1) / EQ_THREADS);
+  const dim3 grid((a.n + EQ_THREADS * EQ_RPT - 1) / (EQ_THREADS * EQ_RPT));
   switch (a.scheme) {
     case 0:
       hipLaunchKernelGGL(predecode_kernel<0>, grid, dim3(EQ_THREADS), 0, stream, a);

@@ -15,19 +15,21 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 #include "llr_kernel.h"
 #include "stage_timing.h"
 
 namespace srsran_amd {
 
 static constexpr int GOLD_NC   = 1600;  // sequence.c:39
-static constexpr int JUMP_BITS = 22;    // offsets below 2^22 LLRs
+static constexpr int JUMP_BITS = 24;    // offsets below 2^24 bits
+static constexpr int JUMP_LVLS = 3;     // offset = b0 + 256 b1 + 65536 b2
 
 struct GoldTables {
-  uint32_t x1[JUMP_BITS][31];  // columns of A1^(2^k)
-  uint32_t x2[JUMP_BITS][31];
-  uint32_t x1_nc;              // x1 after Nc steps from x1 = 1
-  uint32_t x2_nc[31];          // x2 after Nc steps from the unit seed 1 << i
+  uint32_t        x1_nc;      // x1 after Nc steps from x1 = 1
+  uint32_t        x2_nc[31];  // x2 after Nc steps from the unit seed 1 << i
+  const uint32_t* jump;       // [lvl][b][lfsr][32]: columns of A_lfsr^(b * 256^lvl) (device memory)
 };
 __constant__ GoldTables kGold;
 
@@ -39,6 +41,7 @@ __host__ __device__ inline uint32_t step_x2(uint32_t s)
 __host__ __device__ inline uint32_t apply(const uint32_t* cols, uint32_t v)
 {
   uint32_t r = 0;
+#pragma unroll
   for (int i = 0; i < 31; i++) {
     r ^= ((v >> i) & 1u) ? cols[i] : 0u;
   }
@@ -52,18 +55,35 @@ hipError_t gold_tables_init()
   if (done) {
     return err;
   }
-  GoldTables t;
+  // powers A^(2^k) of both LFSR transition matrices (as columns), k < JUMP_BITS
+  std::vector<uint32_t> pw(2 * JUMP_BITS * 31);
+  auto P = [&](int l, int k) { return &pw[(l * JUMP_BITS + k) * 31]; };
   for (int i = 0; i < 31; i++) {
-    t.x1[0][i] = step_x1(1u << i);
-    t.x2[0][i] = step_x2(1u << i);
+    P(0, 0)[i] = step_x1(1u << i);
+    P(1, 0)[i] = step_x2(1u << i);
   }
   for (int k = 1; k < JUMP_BITS; k++) {
-    for (int i = 0; i < 31; i++) {
-      t.x1[k][i] = apply(t.x1[k - 1], t.x1[k - 1][i]);
-      t.x2[k][i] = apply(t.x2[k - 1], t.x2[k - 1][i]);
+    for (int l = 0; l < 2; l++) {
+      for (int i = 0; i < 31; i++) {
+        P(l, k)[i] = apply(P(l, k - 1), P(l, k - 1)[i]);
+      }
     }
   }
-  uint32_t s = 1;
+  std::vector<uint32_t> jt((size_t)JUMP_LVLS * 256 * 2 * 32, 0u);
+  for (int lvl = 0; lvl < JUMP_LVLS; lvl++) {
+    for (int l = 0; l < 2; l++) {
+      const uint32_t* M = P(l, 8 * lvl);  // A^(256^lvl)
+      for (int b = 0; b < 256; b++) {
+        uint32_t*       dst  = &jt[(((size_t)lvl * 256 + b) * 2 + l) * 32];
+        const uint32_t* prev = b ? &jt[(((size_t)lvl * 256 + b - 1) * 2 + l) * 32] : nullptr;
+        for (int i = 0; i < 31; i++) {
+          dst[i] = b ? apply(M, prev[i]) : (1u << i);
+        }
+      }
+    }
+  }
+  GoldTables t;
+  uint32_t   s = 1;
   for (int n = 0; n < GOLD_NC; n++) {
     s = step_x1(s);
   }
@@ -75,20 +95,49 @@ hipError_t gold_tables_init()
     }
     t.x2_nc[i] = v;
   }
-  err  = hipMemcpyToSymbol(HIP_SYMBOL(kGold), &t, sizeof(t));
+  uint32_t* d_jump = nullptr;
+  err = hipMalloc((void**)&d_jump, jt.size() * sizeof(uint32_t));
+  if (err == hipSuccess) {
+    err = hipMemcpy(d_jump, jt.data(), jt.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+  }
+  t.jump = d_jump;
+  if (err == hipSuccess) {
+    err = hipMemcpyToSymbol(HIP_SYMBOL(kGold), &t, sizeof(t));
+  }
   done = true;
   return err;
 }
 
-// LFSR states at bit offset `off` of the sequence for `seed`.
+// columns (32 dwords, 16-byte aligned) applied to v
+__device__ __forceinline__ uint32_t apply_cols(const uint32_t* __restrict__ cols, uint32_t v)
+{
+  const uint4* c4 = reinterpret_cast<const uint4*>(cols);
+  uint32_t     r  = 0;
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    const uint4 c = c4[q];
+    r ^= ((v >> (4 * q)) & 1u) ? c.x : 0u;
+    r ^= ((v >> (4 * q + 1)) & 1u) ? c.y : 0u;
+    r ^= ((v >> (4 * q + 2)) & 1u) ? c.z : 0u;
+    if (q < 7) {
+      r ^= ((v >> (4 * q + 3)) & 1u) ? c.w : 0u;
+    }
+  }
+  return r;
+}
+
+// LFSR states at bit offset `off` (< 2^24) of the sequence for `seed`: three table jumps.
 __device__ __forceinline__ void gold_at(uint32_t seed, uint32_t off, uint32_t& x1, uint32_t& x2)
 {
   x1 = kGold.x1_nc;
   x2 = apply(kGold.x2_nc, seed & 0x7FFFFFFFu);
-  for (int k = 0; k < JUMP_BITS; k++) {
-    if ((off >> k) & 1u) {
-      x1 = apply(kGold.x1[k], x1);
-      x2 = apply(kGold.x2[k], x2);
+#pragma unroll
+  for (int lvl = 0; lvl < JUMP_LVLS; lvl++) {
+    const uint32_t b = (off >> (8 * lvl)) & 255u;
+    if (b) {
+      const uint32_t* t = kGold.jump + (((size_t)lvl * 256 + b) * 2) * 32;
+      x1                = apply_cols(t, x1);
+      x2                = apply_cols(t + 32, x2);
     }
   }
 }
@@ -347,6 +396,9 @@ hipError_t llr_batch_launch(int mod, const LlrItem* d_items, uint32_t nitems, ui
   if (nitems == 0 || max_n == 0) {
     return hipSuccess;
   }
+  if (any_scramble && (uint64_t)max_n * 8 > (1ull << JUMP_BITS)) {
+    return hipErrorInvalidValue;
+  }
   if (any_scramble) {
     hipError_t e = gold_tables_init();
     if (e != hipSuccess) {
@@ -382,6 +434,9 @@ hipError_t llr_launch(int mod, const float* d_sym, uint32_t nsym, int scramble, 
   StageScope timing_scope(ST_LLR, stream);
   if (nsym == 0) {
     return hipSuccess;
+  }
+  if (scramble && (uint64_t)bit0 + (uint64_t)nsym * 8 > (1ull << JUMP_BITS)) {
+    return hipErrorInvalidValue;  // jump tables cover offsets below 2^24
   }
   if (scramble) {
     hipError_t e = gold_tables_init();
@@ -444,6 +499,9 @@ hipError_t seq_apply_launch(const int16_t* d_in, int16_t* d_out, uint32_t len, u
   StageScope timing_scope(ST_LLR, stream);
   if (len == 0) {
     return hipSuccess;
+  }
+  if (len > (1u << JUMP_BITS)) {
+    return hipErrorInvalidValue;
   }
   hipError_t e = gold_tables_init();
   if (e != hipSuccess) {

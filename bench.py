@@ -33,6 +33,37 @@ METRIC = "turbo-decoded info Mbps + PDSCH subframes/s, 20 MHz 64QAM, 1/2/4/8 GPU
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
+def shard(rank):
+    """Per-rank unit of work (independent carriers / CB batches, no data-path collective):
+    rank r decodes its own carrier (cell id 1 + r) from its own seeded synthetic inputs."""
+    return {"cell_id": 1 + rank, "seed": 0x5EED + rank}
+
+
+def timed_region(step, steps, warmup, world, dist, sync, device):
+    """Warm up, then time exactly `steps` steps bracketed by barrier + device sync on both sides;
+    returns the MAX elapsed seconds over ranks (one all_reduce of a scalar, the only collective)."""
+    import torch
+
+    for _ in range(warmup):
+        step()
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
+
+
 def algo_bytes(K):
     """Algorithmic HBM bytes per code block: int16 LLRs in + K/8 bytes out."""
     return (3 * K + 12) * 2 + K // 8
@@ -115,7 +146,7 @@ def run_dlsch(args, torch, dist, world, rank, device):
     from synth import synth as SY
     from srsran_4g_amd import sch as S
 
-    rng = np.random.default_rng(0x5EED + rank)
+    rng = np.random.default_rng(shard(rank)["seed"])
     ntb = 2 * args.subframes
     pool = []
     for _ in range(args.pool):
@@ -139,23 +170,7 @@ def run_dlsch(args, torch, dist, world, rank, device):
         if q.decode_batch(entries, d_res.data_ptr(), d_avg.data_ptr(), sp) != 0:
             raise RuntimeError("srsran_dlsch_gpu_decode_batch failed")
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = timed_region(step, args.steps, args.warmup, world, dist, torch.cuda.synchronize, device)
     res = d_res.cpu().numpy()
     avg = d_avg.cpu().numpy()
     bits_per_step = ntb * C3_TBS
@@ -261,8 +276,8 @@ def run_pdsch(args, torch, dist, world, rank, device):
     from srsran_4g_amd import sch as S
     from srsran_4g_amd import ue_dl as U
 
-    rng = np.random.default_rng(0x5EED + rank)
-    cell_id = 1 + rank  # C4: an independent carrier per GPU
+    rng = np.random.default_rng(shard(rank)["seed"])
+    cell_id = shard(rank)["cell_id"]  # C4: an independent carrier per GPU
     rnti = 0x1234
     pool = []
     for i in range(10):  # one subframe of each index (tti 1..10 -> sf 1..9, 0)
@@ -290,23 +305,7 @@ def run_pdsch(args, torch, dist, world, rank, device):
         if ue.gpu_decode_batch(arr, d_x.data_ptr(), d_res.data_ptr(), d_avg.data_ptr(), 0.0, sp) != 2 * nsf:
             raise RuntimeError("srsran_ue_dl_gpu_decode_batch failed")
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = timed_region(step, args.steps, args.warmup, world, dist, torch.cuda.synchronize, device)
     res = d_res.cpu().numpy()
     avg = d_avg.cpu().numpy()
     pl = d_pl.cpu().numpy()
@@ -451,7 +450,7 @@ def main():
         return run_pdsch(args, torch, dist, world, rank, device)
 
     Ks = list(tdec.CB_SIZES) if args.workload == "all188" else [6144]
-    rng = np.random.default_rng(0x5EED + rank)
+    rng = np.random.default_rng(shard(rank)["seed"])
     data = make_inputs(Ks, args.pool, args.batch, rng, torch, device)
     stream = torch.cuda.current_stream(device)
     sp = stream.cuda_stream
@@ -475,25 +474,8 @@ def main():
                 e1.record(stream)
                 events.append((K, e0, e1))
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-
-    # ---- timed region: exactly `steps` steps, barrier + sync on both sides ----
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    # ---- timed region: exactly `steps` steps, barrier + sync on both sides, max over ranks ----
+    elapsed = timed_region(step, args.steps, args.warmup, world, dist, torch.cuda.synchronize, device)
 
     bits_per_step = args.batch * sum(Ks)
     value = world * bits_per_step * args.steps / elapsed / 1e6

@@ -211,9 +211,10 @@ int srsran_pdsch_re_table(const srsran_cell_t*        cell,
  * srsran_pdsch_decode runs on the GPU: RE extraction fused into the MMSE predecoder (gather
  * through the srsran_pdsch_re_table order), rho_b scaling of CRS symbols fused there too,
  * demapping + descrambling + CSI correction fused into one LLR kernel, then DL-SCH decode.
- * Provided: PORT0 (1 port), CDD and SPATIALMUX (2 ports x 2 rx, 2 codewords on 2 layers),
- * MMSE (ZF = MMSE with noise 0, as pdsch.c:811 passes it), 16-bit LLRs, normal CP, FDD.
- * Not provided (SRSRAN_ERROR): TX diversity, one codeword on two layers, 8-bit LLRs, EVM.
+ * Provided: PORT0 (1 port), TX diversity (2 ports, 1 codeword; layer demap fused), CDD and
+ * SPATIALMUX (2 ports x 2 rx, 2 codewords on 2 layers), MMSE (ZF = MMSE with noise 0, as
+ * pdsch.c:811 passes it), 16-bit LLRs, normal CP, FDD.
+ * Not provided (SRSRAN_ERROR): 4 ports, one codeword on two SM layers, 8-bit LLRs, EVM.
  * The host-side working buffers of the reference struct (ce, symbols, x, d, e, csi) do not
  * exist; the coworker thread is unnecessary (both codewords decode in one GPU pass). */
 typedef struct {

@@ -111,6 +111,8 @@ class _PhyMixin:
         rc = self._predecode(scheme, ya, ha, xa, ca, nrx, nports, nlayers, codebook, n, scaling, noise)
         if rc < 0:
             raise ValueError(rc)
+        if scheme == 1:  # transmit diversity: n/2 symbols per layer, one CSI row for the codeword
+            return xa[:nlayers, : n // 2].copy(), ca[:1].copy()
         return xa[:nlayers].copy(), ca[:nlayers].copy()
 
     def sequence_apply_s(self, llr, seed):

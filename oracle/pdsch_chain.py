@@ -19,7 +19,7 @@ import numpy as np
 import ofdm_np
 import pdsch_np
 
-SCHEME = {"port0": 0, "sm": 2, "cdd": 3}
+SCHEME = {"port0": 0, "diversity": 1, "sm": 2, "cdd": 3}
 MOD = {1: 0, 2: 1, 4: 2, 6: 3, 8: 4}
 RHO_TABLE = ((1.0, 4.0 / 5, 3.0 / 5, 2.0 / 5), (5.0 / 4, 1.0, 3.0 / 4, 1.0 / 2))  # pdsch.c:44-46
 
@@ -68,7 +68,12 @@ def pdsch_decode(ora, grids, ce, noise, nof_prb, cell_id, nports, tti, cfi, rnti
     h = ce[:, :, idx]
     ntb = len(tbs)
     codebook = pmi if ntb == 1 else pmi + 1
-    x, csi = ora.predecode(SCHEME[scheme], y, h, ntb, codebook, scaling, noise)
+    if scheme == "diversity":  # 1 codeword on 2 layers, srsran_layerdemap_diversity (layermap.c:138-147)
+        xl, csi = ora.predecode(1, y, h, 2, codebook, scaling, noise)
+        x = np.empty((1, 2 * xl.shape[1]), np.complex64)
+        x[0, 0::2], x[0, 1::2] = xl[0], xl[1]
+    else:
+        x, csi = ora.predecode(SCHEME[scheme], y, h, ntb, codebook, scaling, noise)
     out = []
     for q in range(ntb):
         llr = ora.demod_s(MOD[Qm[q]], x[q])
@@ -76,6 +81,7 @@ def pdsch_decode(ora, grids, ce, noise, nof_prb, cell_id, nports, tti, cfi, rnti
         if csi_enable:
             llr = ora.csi_correction(MOD[Qm[q]], csi[q], llr)
         st = states[q] if states else None
-        ret, data, noi, avg, state = ora.dlsch_decode(tbs[q], Qm[q], rv[q], llr, max_iterations, st)
+        nl = 2 if scheme == "diversity" else 1  # srsran_dlsch_decode2: Nl = 2 when layers != TBs (sch.c:587-590)
+        ret, data, noi, avg, state = ora.dlsch_decode(tbs[q], Qm[q] * nl, rv[q], llr, max_iterations, st)
         out.append(dict(ret=ret, data=data, avg=avg, llr=llr, state=state, nof_re=idx.size))
     return out

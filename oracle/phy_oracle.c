@@ -192,6 +192,7 @@ uint32_t oracle_pdsch_seed(uint16_t rnti, int q, uint32_t nslot, uint32_t cell_i
  *   CDD    srsran_predecoding_ccd_2x2_mmse_csi precoding.c:1043-1121 (even/odd CDD precoder)
  *   SM     srsran_predecoding_multiplex_2x2_mmse_csi precoding.c:1437-1540 (codebooks 0..2)
  *   2x2    srsran_mat_2x2_mmse_csi_gen         mat.c:63-109
+ *   TXD    srsran_predecoding_diversity_csi    precoding.c:671-700 (2 ports, SFBC pairs)
  * Plain IEEE float, every complex op spelled out, no contraction (built with
  * -ffp-contract=off).  The reference's SIMD bodies use rcp_ps approximations; those agree
  * with this restatement to ~1e-3 relative (tests/test_phy_oracle.py). */
@@ -232,7 +233,8 @@ static void mmse_csi_gen(cpx y0, cpx y1, cpx h00, cpx h01, cpx h10, cpx h11, cpx
 }
 
 /* y[rx][n], h[port][rx][n] (port-major, then rx), x[layer][n], csi[layer][n]; cf32 interleaved.
- * scheme: 0 PORT0, 3 CDD, 2 SPATIALMUX (srsran_tx_scheme_t). */
+ * scheme: 0 PORT0, 1 DIVERSITY, 3 CDD, 2 SPATIALMUX (srsran_tx_scheme_t).  DIVERSITY writes n/2
+ * symbols per layer and csi[0][0..n) (both REs of a pair get the pair's |h|^2 sum). */
 int oracle_predecode(int          scheme,
                      int          nrx,
                      int          nports,
@@ -266,6 +268,34 @@ int oracle_predecode(int          scheme,
       csi[k] = hh + noise;
       const cpx t = cscale(r, norm);
       X[k]        = (cpx){t.r / csi[k], t.i / csi[k]};
+    }
+    return 0;
+  }
+  if (scheme == 1) {
+    if (nports != 2 || nlayers != 2 || nrx < 1 || nrx > 4) {
+      return -1;
+    }
+    for (int i = 0; i < n / 2; i++) {
+      float hh = 0;
+      cpx   x0 = {0, 0}, x1 = {0, 0};
+      for (int p = 0; p < nrx; p++) {
+        const cpx h00 = HH(0, p, 2 * i), h01 = HH(0, p, 2 * i + 1), h10 = HH(1, p, 2 * i), h11 = HH(1, p, 2 * i + 1);
+        hh += h00.r * h00.r + h00.i * h00.i + h11.r * h11.r + h11.i * h11.i;
+        const cpx r0 = Y[(size_t)p * n + 2 * i], r1 = Y[(size_t)p * n + 2 * i + 1];
+        if (hh == 0) {
+          hh = 1e-4f;
+        }
+        x0 = cadd(x0, cadd(cmul(cconj(h00), r0), cmul(h11, cconj(r1))));
+        x1 = cadd(x1, cadd(cmul(cneg(h10), cconj(r0)), cmul(cconj(h01), r1)));
+      }
+      csi[2 * i]     = hh;
+      csi[2 * i + 1] = hh;
+      hh *= scaling;
+      /* (x / hh) in float, then * M_SQRT2 in double (complex float * double), stored as float */
+      X[i]                = (cpx){(float)((double)(x0.r / hh) * 1.41421356237309504880),
+                                  (float)((double)(x0.i / hh) * 1.41421356237309504880)};
+      X[(size_t)n + i]     = (cpx){(float)((double)(x1.r / hh) * 1.41421356237309504880),
+                                   (float)((double)(x1.i / hh) * 1.41421356237309504880)};
     }
     return 0;
   }

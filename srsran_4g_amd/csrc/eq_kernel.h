@@ -12,7 +12,7 @@ struct PredArgs {
   float2*       x[4];     // [layer] equalised symbols
   float*        csi[2];   // [layer] CSI (srsran_predecoding_*_csi)
   uint32_t*     csi_max;  // optional [layer] running max of csi (float bits, csi >= 0)
-  int           scheme;   // 0 PORT0, 2 SPATIALMUX, 3 CDD
+  int           scheme;   // 0 PORT0, 1 DIVERSITY (n = REs, n/2 pairs), 2 SPATIALMUX, 3 CDD
   int           nrx;
   int           codebook;
   uint32_t      n;
@@ -23,6 +23,7 @@ struct PredArgs {
   uint32_t        ce_row;    // > 0: h[p][r] is one AVERAGE row, indexed by (grid index % ce_row)
   const float*    noise_ptr; // device noise estimate (overrides `noise`)
   float           rho_b_inv; // y scale on CRS-bearing symbols (bit 31 of idx), 1 = none
+  int             interleave; // DIVERSITY: write the codeword (layer-demapped) into x[0]
 };
 
 hipError_t predecode_launch(const PredArgs& a, hipStream_t stream);

@@ -5,6 +5,7 @@
 //   PORT0  srsran_predecoding_single_csi        precoding.c:307-355
 //   CDD    srsran_predecoding_ccd_2x2_mmse_csi  precoding.c:1043-1121 (precoder alternates per RE)
 //   SM     srsran_predecoding_multiplex_2x2_mmse_csi precoding.c:1437-1540 (codebooks 0..2)
+//   TXD    srsran_predecoding_diversity_csi     precoding.c:671-700 (2-port SFBC pairs)
 //   2x2    srsran_mat_2x2_mmse_csi_gen          mat.c:63-109
 // computed in IEEE float with the scalar ("gen") operation order and no FMA contraction, so
 // the result equals oracle/phy_oracle.c bit for bit.  (The reference's SIMD bodies use
@@ -95,9 +96,72 @@ __device__ __forceinline__ void block_max_atomic(uint32_t* dst, const uint32_t (
 
 static constexpr int EQ_THREADS = 256;
 
+// grid position, estimate position and y scale of PDSCH RE k (fused srsran_pdsch_get)
+__device__ __forceinline__ void re_at(const PredArgs& a, uint32_t k, uint32_t& gy, uint32_t& gh, float& ys)
+{
+  gy = k, gh = k, ys = 1.0f;
+  if (a.idx) {
+    const uint32_t e = a.idx[k];
+    gy               = e & 0x7fffffffu;
+    gh               = a.ce_row ? gy % a.ce_row : gy;
+    ys               = (e >> 31) ? a.rho_b_inv : 1.0f;
+  }
+}
+
+// srsran_predecoding_diversity_csi, 2 ports (precoding.c:671-700): thread k decodes the SFBC pair
+// (2k, 2k+1); x / hh in float then * M_SQRT2 in double, as the C expression promotes it.
+__device__ __forceinline__ void diversity_pair(const PredArgs& a, uint32_t k, uint32_t (&mx)[2])
+{
+  const bool     valid = k < a.n / 2;
+  const uint32_t kk    = valid ? k : 0;
+  uint32_t       gy0, gh0, gy1, gh1;
+  float          s0, s1;
+  re_at(a, 2 * kk, gy0, gh0, s0);
+  re_at(a, 2 * kk + 1, gy1, gh1, s1);
+  float hh = 0.f;
+  cpx   x0 = {0.f, 0.f}, x1 = {0.f, 0.f};
+  for (int p = 0; p < a.nrx; p++) {
+    const cpx h00 = ld(a.h[0][p], gh0), h01 = ld(a.h[0][p], gh1), h10 = ld(a.h[1][p], gh0), h11 = ld(a.h[1][p], gh1);
+    hh += h00.r * h00.r + h00.i * h00.i + h11.r * h11.r + h11.i * h11.i;
+    cpx r0 = ld(a.y[p], gy0), r1 = ld(a.y[p], gy1);
+    if (s0 != 1.0f) {
+      r0 = cscale(r0, s0);
+    }
+    if (s1 != 1.0f) {
+      r1 = cscale(r1, s1);
+    }
+    if (hh == 0.f) {
+      hh = 1e-4f;
+    }
+    x0 = cadd(x0, cadd(cmul(cconj(h00), r0), cmul(h11, cconj(r1))));
+    x1 = cadd(x1, cadd(cmul(cneg(h10), cconj(r0)), cmul(cconj(h01), r1)));
+  }
+  const float csi = hh;
+  hh *= a.norm;  // scaling
+  const double sq2 = 1.41421356237309504880;
+  const float2 o0  = make_float2((float)((double)(x0.r / hh) * sq2), (float)((double)(x0.i / hh) * sq2));
+  const float2 o1  = make_float2((float)((double)(x1.r / hh) * sq2), (float)((double)(x1.i / hh) * sq2));
+  if (valid) {
+    if (a.interleave) {  // srsran_layerdemap_diversity fused: codeword order d[2k + l] = x_l[k]
+      a.x[0][2 * k]     = o0;
+      a.x[0][2 * k + 1] = o1;
+    } else {
+      a.x[0][k] = o0;
+      a.x[1][k] = o1;
+    }
+    a.csi[0][2 * k]     = csi;
+    a.csi[0][2 * k + 1] = csi;
+    mx[0]               = max(mx[0], __float_as_uint(csi));
+  }
+}
+
 template <int SCHEME>
 __device__ __forceinline__ void predecode_item(const PredArgs& a, uint32_t k, uint32_t (&mx)[2])
 {
+  if constexpr (SCHEME == 1) {
+    diversity_pair(a, k, mx);
+    return;
+  }
   const bool     valid = k < a.n;
   const uint32_t kk    = valid ? k : 0;
   // grid / estimate positions of RE kk (fused srsran_pdsch_get)
@@ -195,7 +259,7 @@ __device__ __forceinline__ void predecode_block(const PredArgs& a, uint32_t k0)
     predecode_item<SCHEME>(a, k0 + r * EQ_THREADS + threadIdx.x, mx);
   }
   if (a.csi_max) {
-    if constexpr (SCHEME == 0) {
+    if constexpr (SCHEME == 0 || SCHEME == 1) {
       const uint32_t m1[1] = {mx[0]};
       block_max_atomic<1>(a.csi_max, m1, red);
     } else {
@@ -215,7 +279,7 @@ __global__ __launch_bounds__(EQ_THREADS) void predecode_batch_kernel(const PredA
 {
   const PredArgs& a  = items[blockIdx.y];
   const uint32_t  k0 = blockIdx.x * EQ_THREADS * EQ_RPT;
-  if (k0 >= a.n) {
+  if (k0 >= (SCHEME == 1 ? a.n / 2 : a.n)) {
     return;  // whole block past this item's end (uniform: the block reduction stays intact)
   }
   predecode_block<SCHEME>(a, k0);
@@ -228,10 +292,17 @@ hipError_t predecode_batch_launch(const PredArgs* d_items, uint32_t nitems, int 
   if (nitems == 0 || max_n == 0) {
     return hipSuccess;
   }
-  const dim3 grid((max_n + EQ_THREADS * EQ_RPT - 1) / (EQ_THREADS * EQ_RPT), nitems);
+  const uint32_t units = scheme == 1 ? max_n / 2 : max_n;  // diversity: one thread per SFBC pair
+  if (units == 0) {
+    return hipSuccess;
+  }
+  const dim3 grid((units + EQ_THREADS * EQ_RPT - 1) / (EQ_THREADS * EQ_RPT), nitems);
   switch (scheme) {
     case 0:
       hipLaunchKernelGGL(predecode_batch_kernel<0>, grid, dim3(EQ_THREADS), 0, stream, d_items);
+      break;
+    case 1:
+      hipLaunchKernelGGL(predecode_batch_kernel<1>, grid, dim3(EQ_THREADS), 0, stream, d_items);
       break;
     case 2:
       hipLaunchKernelGGL(predecode_batch_kernel<2>, grid, dim3(EQ_THREADS), 0, stream, d_items);
@@ -251,10 +322,17 @@ hipError_t predecode_launch(const PredArgs& a, hipStream_t stream)
   if (a.n == 0) {
     return hipSuccess;
   }
-  const dim3 grid((a.n + EQ_THREADS * EQ_RPT - 1) / (EQ_THREADS * EQ_RPT));
+  const uint32_t units = a.scheme == 1 ? a.n / 2 : a.n;
+  if (units == 0) {
+    return hipSuccess;
+  }
+  const dim3 grid((units + EQ_THREADS * EQ_RPT - 1) / (EQ_THREADS * EQ_RPT));
   switch (a.scheme) {
     case 0:
       hipLaunchKernelGGL(predecode_kernel<0>, grid, dim3(EQ_THREADS), 0, stream, a);
+      break;
+    case 1:
+      hipLaunchKernelGGL(predecode_kernel<1>, grid, dim3(EQ_THREADS), 0, stream, a);
       break;
     case 2:
       hipLaunchKernelGGL(predecode_kernel<2>, grid, dim3(EQ_THREADS), 0, stream, a);

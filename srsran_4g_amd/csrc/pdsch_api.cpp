@@ -149,7 +149,8 @@ int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sf
     if (gr.nof_layers == 0 || gr.nof_layers > SRSRAN_MAX_LAYERS) {
       return SRSRAN_ERROR_OUT_OF_BOUNDS;
     }
-    if (gr.nof_layers != gr.nof_tb || gr.nof_tb < 1 || gr.nof_tb > 2) {
+    const bool txd = gr.tx_scheme == SRSRAN_TXSCHEME_DIVERSITY;
+    if (txd ? (gr.nof_tb != 1 || gr.nof_layers != 2) : (gr.nof_layers != gr.nof_tb || gr.nof_tb < 1 || gr.nof_tb > 2)) {
       fprintf(stderr, "[srsran_pdsch] unsupported: %u codewords on %u layers\n", gr.nof_tb, gr.nof_layers);
       return SRSRAN_ERROR;
     }
@@ -187,7 +188,8 @@ int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sf
               nrx, gr.nof_layers);
       return SRSRAN_ERROR;
     }
-    a.n         = gr.nof_re;
+    a.n          = gr.nof_re;
+    a.interleave = txd ? 1 : 0;  // srsran_layerdemap_diversity fused into the predecoder
     a.noise     = f.cfg->decoder_type == SRSRAN_MIMO_DECODER_ZF ? 0.0f : f.noise;
     a.noise_ptr = f.cfg->decoder_type == SRSRAN_MIMO_DECODER_ZF ? nullptr : f.d_noise;
     a.rho_b_inv = rho_b_inv;
@@ -210,7 +212,7 @@ int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sf
                 gr.nof_re);
         return SRSRAN_ERROR;
       }
-      cws.push_back(Cw{b, tb, t.cw_idx, Qm, t.nof_bits, (int)t.mod});
+      cws.push_back(Cw{b, tb, t.cw_idx, Qm * (gr.nof_layers != gr.nof_tb ? 2u : 1u), t.nof_bits, (int)t.mod});
     }
   }
   if (max_re == 0) {
@@ -486,7 +488,7 @@ int srsran_pdsch_gpu_decode_batch(srsran_pdsch_t*              q,
       return SRSRAN_ERROR_INVALID_INPUTS;
     }
     e.tbs        = (uint32_t)t.tbs;
-    e.Qm         = cws[i].Qm;  // Nl = 1: one layer per codeword
+    e.Qm         = cws[i].Qm;  // Qm * Nl as srsran_dlsch_decode2 passes it (sch.c:587-603)
     e.rv         = (uint32_t)t.rv;
     e.nof_e_bits = t.nof_bits;
     e.d_e_bits   = llr[i];

@@ -74,6 +74,13 @@ bool pred_setup(PredArgs& a, int nrx, int nports, int nlayers, int codebook, int
       a.scheme = 0;
       a.norm   = 1.0f / scaling;  // precoding.c:319
       return true;
+    case SRSRAN_TXSCHEME_DIVERSITY:
+      if (nports != 2 || nlayers != 2 || nrx < 1 || nrx > 4) {
+        return false;
+      }
+      a.scheme = 1;
+      a.norm   = scaling;  // hh *= scaling (precoding.c:695)
+      return true;
     case SRSRAN_TXSCHEME_CDD:
       if (nports != 2 || nrx != 2 || nlayers != 2) {
         return false;
@@ -211,13 +218,18 @@ int srsran_predecoding_type(cf_t*              y[4],
   if (predecode_launch(a, g_ctx.stream) != hipSuccess) {
     return SRSRAN_ERROR;
   }
+  const size_t xn = a.scheme == 1 ? n / 2 : n;  // diversity: n/2 symbols per layer, one CSI row of n
   for (int l = 0; l < nof_layers; l++) {
-    hipMemcpyAsync(x[l], dx + l * n, n * sizeof(cf_t), hipMemcpyDeviceToHost, g_ctx.stream);
-    if (csi && l < 2 && csi[l]) {
+    hipMemcpyAsync(x[l], dx + l * n, xn * sizeof(cf_t), hipMemcpyDeviceToHost, g_ctx.stream);
+    if (csi && l < (a.scheme == 1 ? 1 : 2) && csi[l]) {
       hipMemcpyAsync(csi[l], dcs + l * n, n * sizeof(float), hipMemcpyDeviceToHost, g_ctx.stream);
     }
   }
-  return hipStreamSynchronize(g_ctx.stream) == hipSuccess ? SRSRAN_SUCCESS : SRSRAN_ERROR;
+  if (hipStreamSynchronize(g_ctx.stream) != hipSuccess) {
+    return SRSRAN_ERROR;
+  }
+  // the reference's return values: single_csi -> nof_symbols, diversity_csi -> pairs, 2x2 MMSE -> 0
+  return a.scheme == 0 ? (int)n : a.scheme == 1 ? (int)(n / 2) : SRSRAN_SUCCESS;
 }
 
 int srsran_predecoding_gpu(const cf_t* const  d_y[4],

@@ -87,8 +87,10 @@ def predecode(scheme, y, h, nlayers, codebook, scaling, noise):
     cs = _ptrs([csi[0], csi[1]], 2)
     rc = lib().srsran_predecoding_type(ctypes.addressof(ys), ctypes.addressof(hs), ctypes.addressof(xs),
                                        ctypes.addressof(cs), nrx, nports, nlayers, codebook, n, scheme, scaling, noise)
-    if rc:
+    if rc < 0:
         raise RuntimeError(f"srsran_predecoding_type failed ({rc})")
+    if scheme == 1:  # transmit diversity: n/2 symbols per layer, one CSI row for the codeword
+        return x[:nlayers, : n // 2], csi[:1]
     return x[:nlayers], csi[:nlayers]
 
 

@@ -293,7 +293,8 @@ def pdsch_cfg(nof_prb, nof_re, tbs, Qm, rv=(0, 0), scheme="cdd", pmi=0, rnti=0x1
     g.nof_prb = nof_prb
     g.nof_re = nof_re
     g.nof_symb_slot[0] = g.nof_symb_slot[1] = 7
-    g.nof_tb = g.nof_layers = len(tbs)
+    g.nof_tb = len(tbs)
+    g.nof_layers = 2 if scheme == "diversity" else len(tbs)
     for i, t in enumerate(tbs):
         tb = g.tb[i]
         tb.mod = MOD_FROM_QM[Qm[i]]

@@ -151,6 +151,14 @@ def precode(x, scheme, codebook=0):
     if scheme == "cdd":
         sgn = np.where(np.arange(n) % 2 == 0, 1.0, -1.0)
         return [(x[0] + x[1]) / 2, sgn * (x[0] - x[1]) / 2]
+    if scheme == "diversity":  # 36.211 6.3.3.3 layer mapping + 6.3.4.3 SFBC, 2 ports (x = one codeword)
+        d = x[0]
+        x0, x1 = d[0::2], d[1::2]
+        y0 = np.empty(d.size, np.complex128)
+        y1 = np.empty(d.size, np.complex128)
+        y0[0::2], y0[1::2] = x0 / math.sqrt(2), x1 / math.sqrt(2)
+        y1[0::2], y1[1::2] = -np.conj(x1) / math.sqrt(2), np.conj(x0) / math.sqrt(2)
+        return [y0, y1]
     if scheme == "sm":
         W = {0: np.array([[1, 0], [0, 1]]) / math.sqrt(2), 1: np.array([[1, 1], [1, -1]]) / 2,
              2: np.array([[1, 1], [1j, -1j]]) / 2}[codebook]
@@ -252,7 +260,7 @@ def pdsch_subframe(nof_prb, cell_id, nports, tti, cfi, rnti, tbs, Qm, rv, payloa
     layers = []
     for q, pl in enumerate(payloads):
         G = nof_re * Qm
-        e = dlsch_encode(tbs, Qm, rv, G, pl)
+        e = dlsch_encode(tbs, Qm, rv, G, pl, Nl=2 if scheme == "diversity" else 1)
         c = gold(pdsch_seed(rnti, q, 2 * sf_idx, cell_id), G)
         layers.append(modulate(e ^ c, Qm))
     ports = precode(layers, scheme, codebook)

@@ -39,3 +39,12 @@ def test_oracle_chain_port0_16qam(ora):
     g, ce, st = PC.fft_estimate(ora, x, 100, 3, 1, 4)
     res = PC.pdsch_decode(ora, g, ce, st["noise"], 100, 3, 1, 4, 1, 0x1234, [30576], [4], [0], scheme="port0")
     assert res[0]["ret"] == 0 and np.array_equal(res[0]["data"][: 30576 // 8], pl[0])
+
+
+def test_oracle_chain_tm2_diversity(ora):
+    rng = np.random.default_rng(4)
+    pl = [rng.integers(0, 256, TBS // 8, dtype=np.uint8)]
+    x, nre = S.pdsch_subframe(100, 4, 2, 5, 1, 0x1234, TBS, 6, 0, pl, scheme="diversity", snr_db=30.0, rng=rng)
+    g, ce, st = PC.fft_estimate(ora, x, 100, 4, 2, 5)
+    res = PC.pdsch_decode(ora, g, ce, st["noise"], 100, 4, 2, 5, 1, 0x1234, [TBS], [6], [0], scheme="diversity")
+    assert res[0]["ret"] == 0 and np.array_equal(res[0]["data"][: TBS // 8], pl[0])

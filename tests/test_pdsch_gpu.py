@@ -58,6 +58,8 @@ CASES = [
     dict(scheme="sm", pmi=0),                               # TM4 codebook 1
     dict(scheme="sm", pmi=1, cell_id=7),                    # TM4 codebook 2
     dict(nports=1, scheme="port0", tbs=(30576,), Qm=(4,), cell_id=3, channel=[[1], [0.5 + 0.5j]]),
+    dict(scheme="diversity", tbs=(TBS,), Qm=(6,), tti=5, cell_id=4),       # TM2 SFBC, layer demap fused
+    dict(scheme="diversity", tbs=(TBS,), Qm=(6,), snr_db=12.0, fail=True),  # TM2 with CB failures
     dict(nof_prb=50, cell_id=11, tbs=(36696, 36696), tti=3, cfi=1),
     dict(nof_prb=50, cell_id=11, tbs=(25456, 25456), tti=4, cfi=3),
     dict(nof_prb=6, cell_id=2, tbs=(1800, 1800), Qm=(4, 4), cfi=2, tti=7),
@@ -69,7 +71,7 @@ CASES = [
                                   dict(zf=True)])
 def test_pdsch_decode_bitexact(U, SCH, ora, case, opts):
     kw = dict(CASES[case])
-    if opts and case not in (0, 3, 7):
+    if opts and case not in (0, 3, 7, 8):
         pytest.skip("options exercised on a subset of grants")
     rng = np.random.default_rng(100 + case)
     fail = kw.pop("fail", False)

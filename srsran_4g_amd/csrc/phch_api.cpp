@@ -222,7 +222,8 @@ int srsran_predecoding_type(cf_t*              y[4],
   for (int l = 0; l < nof_layers; l++) {
     hipMemcpyAsync(x[l], dx + l * n, xn * sizeof(cf_t), hipMemcpyDeviceToHost, g_ctx.stream);
     if (csi && l < (a.scheme == 1 ? 1 : 2) && csi[l]) {
-      hipMemcpyAsync(csi[l], dcs + l * n, n * sizeof(float), hipMemcpyDeviceToHost, g_ctx.stream);
+      hipMemcpyAsync(csi[l], dcs + l * n, (a.scheme == 1 ? 2 * xn : n) * sizeof(float), hipMemcpyDeviceToHost,
+                     g_ctx.stream);  // diversity: an unpaired last RE is not written (precoding.c:674)
     }
   }
   if (hipStreamSynchronize(g_ctx.stream) != hipSuccess) {

@@ -8,10 +8,10 @@
 // AVX2 blocks: truncation + saturation; tail: truncation + wrap).  Both splits are kept
 // here by the symbol's index within the call.
 //
-// Layout: one thread per SPT consecutive symbols.  The Gold LFSRs are jumped straight to the
-// thread's first bit with GF(2) matrices A^(2^k) held in constant memory (every lane reads the
-// same column at the same time), then stepped one bit per LLR.  HBM-bound elementwise work:
-// 8 B in per symbol, 2*Qm B out.
+// Layout: one workgroup per LLR_THREADS * SPT symbols.  The Gold LFSRs are jumped to each
+// thread's slice of the block's sequence bits with three byte-indexed GF(2) jump tables, stepped
+// 16 bits at a time and staged in LDS; symbols are then processed with a stride of
+// LLR_THREADS (coalesced).  HBM-bound elementwise work: 8 B (+4 B CSI) in, 2*Qm B out per symbol.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -314,61 +314,99 @@ __device__ __forceinline__ void csi_correct(int16_t* o, uint32_t s, const float*
   }
 }
 
-template <int MOD>
-__device__ __forceinline__ void llr_body(const float2* __restrict__ sym, uint32_t n, int scramble, uint32_t seed,
-                                         uint32_t bit0, const float* __restrict__ csi,
-                                         const float* __restrict__ csi_max, int16_t* __restrict__ llr, uint32_t s0)
+// advance both LFSRs by 16 bits and return c(n..n+15) (bit k = c(n+k)): the recurrences
+// x1(m+31) = x1(m+3) ^ x1(m) and x2(m+31) = x2(m+3) ^ x2(m+2) ^ x2(m+1) ^ x2(m) give 28 new bits
+// per shift-xor, 16 of which are used
+__device__ __forceinline__ uint32_t gold16(uint32_t& x1, uint32_t& x2)
 {
-  constexpr int Q = Qm<MOD>::v;
-  if (s0 >= n) {
-    return;
+  const uint32_t c  = (x1 ^ x2) & 0xFFFFu;
+  const uint32_t n1 = ((x1 >> 3) ^ x1) & 0xFFFFu;
+  const uint32_t n2 = ((x2 >> 3) ^ (x2 >> 2) ^ (x2 >> 1) ^ x2) & 0xFFFFu;
+  x1                = (x1 >> 16) | (n1 << 15);
+  x2                = (x2 >> 16) | (n2 << 15);
+  return c;
+}
+
+// One block = LLR_THREADS * SPT consecutive symbols.  Phase 1: thread t jumps the Gold LFSRs to
+// the block's bit t * SPT * Q and writes its SPT * Q sequence bits to LDS (one table jump per
+// 16 * Q bits).  Phase 2: thread t handles symbols t, t + 256, ... -- coalesced loads and
+// stores -- demapping, descrambling from the LDS bits and CSI correction in registers.
+template <int MOD>
+__device__ __forceinline__ void llr_block(const float2* __restrict__ sym, uint32_t n, int scramble, uint32_t seed,
+                                          uint32_t bit0, const float* __restrict__ csi,
+                                          const float* __restrict__ csi_max, int16_t* __restrict__ llr, uint32_t blk)
+{
+  constexpr int       Q = Qm<MOD>::v;
+  __shared__ uint16_t cbits[LLR_THREADS * 8 + 2];  // SPT * Q / 16 = Q chunks per thread
+  const uint32_t      base = blk * (uint32_t)(LLR_THREADS * SPT);
+  if (base >= n) {
+    return;  // uniform per block
   }
-  const int ns = (int)min((uint32_t)SPT, n - s0);
-  float2    v[SPT];
-#pragma unroll
-  for (int k = 0; k < SPT; k++) {
-    v[k] = k < ns ? sym[s0 + k] : make_float2(0.f, 0.f);
-  }
-  uint32_t x1 = 0, x2 = 0;
+  const uint32_t nb = min((uint32_t)(LLR_THREADS * SPT), n - base);
+  const uint32_t t  = threadIdx.x;
   if (scramble) {
-    gold_at(seed, bit0 + s0 * Q, x1, x2);
-  }
-  int16_t o[SPT * Q];
+    if (t * SPT < nb) {
+      uint32_t x1, x2;
+      gold_at(seed, bit0 + (base + t * SPT) * Q, x1, x2);
 #pragma unroll
-  for (int k = 0; k < SPT; k++) {
-    demap<MOD>(v[k].x, v[k].y, s0 + k, n, &o[k * Q]);
-  }
-  if (scramble) {
-#pragma unroll
-    for (int b = 0; b < SPT * Q; b++) {
-      o[b] = ((x1 ^ x2) & 1u) ? wrap16(-(int32_t)o[b]) : o[b];
-      x1   = step_x1(x1);
-      x2   = step_x2(x2);
-    }
-  }
-  if (csi) {  // after descrambling, as pdsch.c:735-737 orders it
-    const float mx = *csi_max;
-#pragma unroll
-    for (int k = 0; k < SPT; k++) {
-      if (k < ns) {
-        csi_correct<MOD>(&o[k * Q], s0 + k, csi, mx, n * Q);
+      for (int j = 0; j < Q; j++) {
+        cbits[t * Q + j] = (uint16_t)gold16(x1, x2);
       }
     }
+    __syncthreads();
   }
-  int16_t* dst = llr + (size_t)s0 * Q;
-  if (ns == SPT && ((uintptr_t)dst & 15) == 0 && (SPT * Q * 2) % 16 == 0) {
-#pragma unroll
-    for (int w = 0; w < SPT * Q / 8; w++) {
-      uint4 u;
-      u.x = (uint32_t)(uint16_t)o[8 * w + 0] | ((uint32_t)(uint16_t)o[8 * w + 1] << 16);
-      u.y = (uint32_t)(uint16_t)o[8 * w + 2] | ((uint32_t)(uint16_t)o[8 * w + 3] << 16);
-      u.z = (uint32_t)(uint16_t)o[8 * w + 4] | ((uint32_t)(uint16_t)o[8 * w + 5] << 16);
-      u.w = (uint32_t)(uint16_t)o[8 * w + 6] | ((uint32_t)(uint16_t)o[8 * w + 7] << 16);
-      reinterpret_cast<uint4*>(dst)[w] = u;
+  const float mx  = csi ? *csi_max : 1.0f;
+  const bool  a16 = ((uintptr_t)llr & 15) == 0;
+  const bool  a4  = ((uintptr_t)llr & 3) == 0;
+#pragma unroll 4
+  for (int r = 0; r < SPT; r++) {
+    const uint32_t i = t + (uint32_t)r * LLR_THREADS;
+    if (i >= nb) {
+      break;
     }
-  } else {
-    for (int b = 0; b < ns * Q; b++) {
-      dst[b] = o[b];
+    const uint32_t s = base + i;
+    const float2   v = sym[s];
+    int16_t        o[Q];
+    demap<MOD>(v.x, v.y, s, n, o);
+    if (scramble) {
+      const uint32_t b  = i * Q;
+      const uint32_t w0 = cbits[b >> 4];
+      const uint32_t w  = ((b & 15) + Q > 16) ? (w0 | ((uint32_t)cbits[(b >> 4) + 1] << 16)) : w0;
+      const uint32_t cb = w >> (b & 15);
+#pragma unroll
+      for (int k = 0; k < Q; k++) {
+        o[k] = ((cb >> k) & 1u) ? wrap16(-(int32_t)o[k]) : o[k];
+      }
+    }
+    if (csi) {  // after descrambling, as pdsch.c:735-737 orders it
+      csi_correct<MOD>(o, s, csi, mx, n * Q);
+    }
+    int16_t* dst = llr + (size_t)s * Q;
+    if (Q == 1 || !a4) {
+#pragma unroll
+      for (int k = 0; k < Q; k++) {
+        dst[k] = o[k];
+      }
+    } else if constexpr (Q == 2) {
+      *reinterpret_cast<uint32_t*>(dst) = (uint32_t)(uint16_t)o[0] | ((uint32_t)(uint16_t)o[1] << 16);
+    } else if constexpr (Q == 8) {
+      uint4 u;
+      u.x = (uint32_t)(uint16_t)o[0] | ((uint32_t)(uint16_t)o[1] << 16);
+      u.y = (uint32_t)(uint16_t)o[2] | ((uint32_t)(uint16_t)o[3] << 16);
+      u.z = (uint32_t)(uint16_t)o[4] | ((uint32_t)(uint16_t)o[5] << 16);
+      u.w = (uint32_t)(uint16_t)o[6] | ((uint32_t)(uint16_t)o[7] << 16);
+      if (a16) {
+        *reinterpret_cast<uint4*>(dst) = u;
+      } else {
+        uint32_t* d = reinterpret_cast<uint32_t*>(dst);
+        d[0] = u.x, d[1] = u.y, d[2] = u.z, d[3] = u.w;
+      }
+    } else {  // Q = 4, 6: 4-byte aligned words (int16 buffers are 4-byte aligned)
+      uint32_t* d = reinterpret_cast<uint32_t*>(dst);
+#pragma unroll
+      for (int k = 0; k < Q / 2; k++) {
+        d[k] = (uint32_t)(uint16_t)o[2 * k] | ((uint32_t)(uint16_t)o[2 * k + 1] << 16);
+      }
     }
   }
 }
@@ -378,15 +416,15 @@ __global__ __launch_bounds__(LLR_THREADS) void llr_kernel(const float2* __restri
                                                           uint32_t seed, uint32_t bit0, const float* __restrict__ csi,
                                                           const float* __restrict__ csi_max, int16_t* __restrict__ llr)
 {
-  llr_body<MOD>(sym, n, scramble, seed, bit0, csi, csi_max, llr, (blockIdx.x * LLR_THREADS + threadIdx.x) * SPT);
+  llr_block<MOD>(sym, n, scramble, seed, bit0, csi, csi_max, llr, blockIdx.x);
 }
 
 template <int MOD>
 __global__ __launch_bounds__(LLR_THREADS) void llr_batch_kernel(const LlrItem* __restrict__ items)
 {
   const LlrItem& it = items[blockIdx.y];
-  llr_body<MOD>(reinterpret_cast<const float2*>(it.sym), it.n, it.scramble, it.seed, it.bit0, it.csi, it.csi_max,
-                it.llr, (blockIdx.x * LLR_THREADS + threadIdx.x) * SPT);
+  llr_block<MOD>(reinterpret_cast<const float2*>(it.sym), it.n, it.scramble, it.seed, it.bit0, it.csi, it.csi_max,
+                 it.llr, blockIdx.x);
 }
 
 hipError_t llr_batch_launch(int mod, const LlrItem* d_items, uint32_t nitems, uint32_t max_n, int any_scramble,
@@ -486,11 +524,17 @@ __global__ __launch_bounds__(LLR_THREADS) void seq_apply_kernel(const int16_t* _
   uint32_t x1, x2;
   gold_at(seed, i0, x1, x2);
   const uint32_t n = min((uint32_t)SEQ_PER_THREAD, len - i0);
-  for (uint32_t k = 0; k < n; k++) {
-    const int16_t v = in[i0 + k];
-    out[i0 + k]     = ((x1 ^ x2) & 1u) ? wrap16(-(int32_t)v) : v;
-    x1              = step_x1(x1);
-    x2              = step_x2(x2);
+#pragma unroll
+  for (int c = 0; c < SEQ_PER_THREAD / 16; c++) {
+    const uint32_t bits = gold16(x1, x2);
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      const uint32_t i = (uint32_t)(16 * c + k);
+      if (i < n) {
+        const int16_t v = in[i0 + i];
+        out[i0 + i]     = ((bits >> k) & 1u) ? wrap16(-(int32_t)v) : v;
+      }
+    }
   }
 }
 

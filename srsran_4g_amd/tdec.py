@@ -12,7 +12,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libsrsran_4g_amd.so")
+LIB_PATH = os.environ.get("SRSRAN_AMD_LIB") or os.path.join(HERE, "lib", "libsrsran_4g_amd.so")  # env override: developer A/B builds only
 
 SRSRAN_SUCCESS = 0
 SRSRAN_ERROR = -1

@@ -153,6 +153,8 @@ struct SchCtx {
   uint8_t*    d_noi = nullptr;
   uint8_t*    d_crc_ok = nullptr;
   size_t      slot_cap = 0;
+  uint32_t*   d_part   = nullptr;  // TB_MAX_CHUNKS chunk CRCs per TB
+  size_t      tb_cap   = 0;
   // synchronous decode scratch
   int16_t*    d_e = nullptr;
   size_t      e_cap = 0;
@@ -228,7 +230,7 @@ int enqueue_batch(srsran_sch_t* q, uint32_t ntb, const srsran_dlsch_gpu_tb_t* tb
   std::vector<RmSlot>                         rm(nslots);
   std::map<uint32_t, std::vector<uint32_t>>   by_k;
   std::vector<uint8_t>                        slot_crc_a(nslots);
-  uint32_t                                    max_len = 0;
+  uint32_t                                    max_len = 0, max_e = 0;
   for (uint32_t i = 0; i < ntb; i++) {
     if (plan[i].status != 1) {
       continue;
@@ -263,6 +265,7 @@ int enqueue_batch(srsran_sch_t* q, uint32_t ntb, const srsran_dlsch_gpu_tb_t* tb
       r.N                 = t.N;
       r.overwrite         = tbs[i].new_data ? 1 : 0;
       max_len             = std::max(max_len, t.len);
+      max_e               = std::max(max_e, n_e2);
       by_k[K].push_back(slot);
       slot_crc_a[slot] = s.C == 1;  // single-CB TB: CRC24A over tbs + 24 (sch.c:440-446)
     }
@@ -355,11 +358,28 @@ int enqueue_batch(srsran_sch_t* q, uint32_t ntb, const srsran_dlsch_gpu_tb_t* tb
       x->slot_cap = cap;
     }
   }
-  for (auto& t : tbd) {
+  if (ntb > x->tb_cap) {
+    if (x->used) {
+      hipEventSynchronize(x->done);
+    }
+    hipFree(x->d_part);
+    x->d_part = nullptr;
+    const size_t cap = std::max((size_t)ntb * 2, (size_t)64);
+    if (hipMalloc((void**)&x->d_part, cap * TB_MAX_CHUNKS * sizeof(uint32_t)) != hipSuccess) {
+      x->tb_cap = 0;
+      return SRSRAN_ERROR;
+    }
+    x->tb_cap = cap;
+  }
+  uint32_t max_tbs = 0;
+  for (uint32_t i = 0; i < ntb; i++) {
+    SchTb& t = tbd[i];
     if (t.status == 1) {
       t.cbout  = x->d_cbout;
       t.noi    = x->d_noi;
       t.crc_ok = x->d_crc_ok;
+      t.part   = x->d_part + (size_t)i * TB_MAX_CHUNKS;
+      max_tbs  = std::max(max_tbs, t.tbs);
     }
   }
   memcpy(x->h_stage, rm.data(), nslots * sizeof(RmSlot));
@@ -373,7 +393,7 @@ int enqueue_batch(srsran_sch_t* q, uint32_t ntb, const srsran_dlsch_gpu_tb_t* tb
 
   int ret = SRSRAN_SUCCESS;
   if (nslots) {
-    if (rm_rx_launch((const RmSlot*)x->d_stage, nslots, max_len, stream) != hipSuccess) {
+    if (rm_rx_launch((const RmSlot*)x->d_stage, nslots, max_len, max_e, stream) != hipSuccess) {
       ret = SRSRAN_ERROR;
     }
     const int n_end = q->max_iterations > 0 ? (int)q->max_iterations : 1;
@@ -384,7 +404,7 @@ int enqueue_batch(srsran_sch_t* q, uint32_t ntb, const srsran_dlsch_gpu_tb_t* tb
                              SCH_SLOT_BYTES, x->d_noi, x->d_crc_ok, n_end, stream);
     }
   }
-  if (ret == SRSRAN_SUCCESS && tb_launch((const SchTb*)(x->d_stage + off_tb), ntb, stream) != hipSuccess) {
+  if (ret == SRSRAN_SUCCESS && tb_launch((const SchTb*)(x->d_stage + off_tb), ntb, max_tbs, stream) != hipSuccess) {
     ret = SRSRAN_ERROR;
   }
   hipEventRecord(x->done, stream);
@@ -601,7 +621,7 @@ int srsran_rm_turbo_rx_lut_(int16_t* input,
   hipMemcpyAsync(c.d_in, input, (size_t)in_len * sizeof(int16_t), hipMemcpyHostToDevice, c.stream);
   hipMemcpyAsync(c.d_out, output, t.len * sizeof(int16_t), hipMemcpyHostToDevice, c.stream);
   hipMemcpyAsync(c.d_slot, &s, sizeof(s), hipMemcpyHostToDevice, c.stream);
-  if (rm_rx_launch(c.d_slot, 1, t.len, c.stream) != hipSuccess) {
+  if (rm_rx_launch(c.d_slot, 1, t.len, in_len, c.stream) != hipSuccess) {
     return SRSRAN_ERROR;
   }
   hipMemcpyAsync(output, c.d_out, t.len * sizeof(int16_t), hipMemcpyDeviceToHost, c.stream);
@@ -797,6 +817,7 @@ void srsran_sch_free(srsran_sch_t* q)
     hipFree(x->d_cbout);
     hipFree(x->d_noi);
     hipFree(x->d_crc_ok);
+    hipFree(x->d_part);
     hipFree(x->d_e);
     hipFree(x->d_data);
     hipFree(x->d_res);

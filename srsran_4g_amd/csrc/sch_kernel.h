@@ -5,7 +5,8 @@
 //   1. rm_rx_kernel     rate de-matching of every slot into its HARQ soft buffer
 //                       (srsran_rm_turbo_rx_lut, rm_turbo.c:390-483)
 //   2. tdec_kernel<ES>  turbo decode with CRC early stop (decode_tb_cb, sch.c:420-456)
-//   3. tb_kernel        TB assembly, CB bookkeeping, TB CRC (sch.c:458-573)
+//   3. tb_assemble_kernel + tb_finish_kernel
+//                       TB assembly, CB bookkeeping, TB CRC (sch.c:458-573)
 #ifndef SRSRAN_AMD_SCH_KERNEL_H
 #define SRSRAN_AMD_SCH_KERNEL_H
 #include <hip/hip_runtime.h>
@@ -15,6 +16,8 @@ namespace srsran_amd {
 
 static constexpr int SCH_SLOT_BYTES = 768;  // decision bytes per slot (K <= 6144)
 static constexpr int SCH_MAX_CB     = 32;   // SRSRAN_MAX_CODEBLOCKS (phy_common.h:64)
+static constexpr int TB_MAX_CHUNKS  = 32;
+static constexpr int RM_LDS_MAX_E   = 24576;  // E LLRs a CB may have for the LDS de-matcher (48 KB)   // 1 KB CRC chunks per TB (>= 32 * 6144 / 8 / 1024)
 
 struct RmSlot {
   const short*    e;     // the CB's E rate-matched LLRs (device)
@@ -38,6 +41,7 @@ struct SchTb {
   int32_t*       result;    // decode_tb return value (device)
   float*         avg;       // avg_iterations (device)
   short*         sbuf;      // soft buffer arena (sb_stride int16 per CB), for new-transmission resets
+  uint32_t*      part;      // TB_MAX_CHUNKS chunk CRC24A values (device scratch)
   uint32_t       saved_stride;
   uint32_t       sb_stride;
   uint32_t       max_cb;
@@ -48,8 +52,11 @@ struct SchTb {
   int32_t        status;    // 1: decoded; otherwise the return value of a host-side check
 };
 
-hipError_t rm_rx_launch(const RmSlot* d_slots, uint32_t nslots, uint32_t max_len, hipStream_t stream);
-hipError_t tb_launch(const SchTb* d_tbs, uint32_t ntb, hipStream_t stream);
+// max_e: the largest E of the batch (the LDS de-matcher takes E <= RM_LDS_MAX_E)
+hipError_t rm_rx_launch(const RmSlot* d_slots, uint32_t nslots, uint32_t max_len, uint32_t max_e,
+                        hipStream_t stream);
+// max_tbs: the largest TBS of the batch (sizes the assembly grid)
+hipError_t tb_launch(const SchTb* d_tbs, uint32_t ntb, uint32_t max_tbs, hipStream_t stream);
 
 }  // namespace srsran_amd
 #endif

@@ -8,11 +8,11 @@
 // which gives coalesced soft-buffer reads/writes, no atomics and no write conflicts;
 // the E-vector gather hits L2 (E <= ~20 KB per CB).
 //
-// tb_kernel: one workgroup per transport block performs the tail of decode_tb_cb and
-// decode_tb (sch.c:458-573): payload assembly in CB order (later CBs overwrite the
-// 3 CRC bytes earlier ones wrote, skipped CBs come from the soft buffer's saved copy),
-// the CB CRC bookkeeping, saving of good CBs on failure, the TB CRC24A and the
-// reset of the CB flags when the TB CRC fails.
+// tb_assemble_kernel + tb_finish_kernel perform the tail of decode_tb_cb and decode_tb
+// (sch.c:458-573): payload assembly in CB order (later CBs overwrite the 3 CRC bytes earlier
+// ones wrote, skipped CBs come from the soft buffer's saved copy) with the TB CRC24A of each
+// 1 KB chunk, then per TB the CB CRC bookkeeping, saving of good CBs on failure, the TB CRC
+// decision and the reset of the CB flags when it fails.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -74,8 +74,46 @@ __global__ __launch_bounds__(RM_THREADS) void rm_rx_kernel(const RmSlot* __restr
   }
 }
 
-static constexpr int TB_THREADS = 1024;
-static constexpr int TB_WAVES   = TB_THREADS / 64;
+// rm_rx_lds_kernel: one workgroup per code block.  The CB's E LLRs are staged in LDS with
+// coalesced loads, then every soft-buffer position gathers its contributions from LDS
+// (4 positions per thread per pass: 8-byte table and soft-buffer accesses, coalesced).
+static constexpr int RM_LDS_THREADS = 512;
+
+__global__ __launch_bounds__(RM_LDS_THREADS) void rm_rx_lds_kernel(const RmSlot* __restrict__ slots)
+{
+  __shared__ short es[RM_LDS_MAX_E];
+  const RmSlot     s = slots[blockIdx.x];
+  if (!s.overwrite && *s.skip) {
+    return;
+  }
+  const int tid = threadIdx.x;
+  for (uint32_t i = tid; i < s.E; i += RM_LDS_THREADS) {
+    es[i] = s.e[i];
+  }
+  __syncthreads();
+  for (uint32_t p = 4 * (uint32_t)tid; p < s.len; p += 4 * RM_LDS_THREADS) {
+    const uint2 iv = *reinterpret_cast<const uint2*>(s.inv + p);
+    uint2       v  = s.overwrite ? make_uint2(0, 0) : *reinterpret_cast<const uint2*>(s.sb + p);
+    short acc[4] = {(short)(v.x & 0xffffu), (short)(v.x >> 16), (short)(v.y & 0xffffu), (short)(v.y >> 16)};
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t idx = k == 0 ? (iv.x & 0xffffu) : k == 1 ? (iv.x >> 16) : k == 2 ? (iv.y & 0xffffu) : (iv.y >> 16);
+      if (idx != 0xffffu) {
+        for (uint32_t i = idx; i < s.E; i += s.N) {  // one period, plus repetitions when E > N
+          acc[k] = (short)(acc[k] + es[i]);
+        }
+      }
+    }
+    v.x                                  = (uint32_t)(uint16_t)acc[0] | ((uint32_t)(uint16_t)acc[1] << 16);
+    v.y                                  = (uint32_t)(uint16_t)acc[2] | ((uint32_t)(uint16_t)acc[3] << 16);
+    *reinterpret_cast<uint2*>(s.sb + p) = v;
+  }
+}
+
+static constexpr int TB_ASM_THREADS = 256;
+static constexpr int TB_CHUNK       = 4 * TB_ASM_THREADS;  // payload bytes per assembly block
+static constexpr int TB_FIN_THREADS = 256;
+static constexpr int TB_THREADS     = TB_FIN_THREADS;  // reset_range stride
 
 // x^(8 * 2^k) mod CRC24A for k = 0..16, built at compile time.
 constexpr uint32_t ce_clmul_mod24(uint32_t a, uint32_t b, uint32_t poly)
@@ -152,7 +190,118 @@ __device__ void reset_range(const SchTb& t, uint32_t sb0, uint32_t n, uint32_t f
   }
 }
 
-__global__ __launch_bounds__(TB_THREADS) void tb_kernel(const SchTb* __restrict__ tbs)
+// Per-CB geometry of a TB as decode_tb leaves the payload (sch.c:425-431, 476-480): CB c writes
+// len[c] bytes at start[c] = c * rlen / 8 (K/8 decoded bytes, or rlen/8 saved bytes when the CB
+// was skipped); later CBs overwrite the CRC bytes of earlier ones.
+struct TbGeom {
+  uint32_t       start[SCH_MAX_CB], len[SCH_MAX_CB], rlen8[SCH_MAX_CB], okf[SCH_MAX_CB];
+  const uint8_t* src[SCH_MAX_CB];
+  uint32_t       noi_sum, end;
+};
+
+__device__ void tb_geometry(const SchTb& t, TbGeom& g)
+{
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    g.noi_sum = 0;
+    g.end     = 0;
+  }
+  __syncthreads();
+  if (tid < (int)t.C) {
+    const uint32_t K    = tid < (int)t.C1 ? t.K1 : t.K2;
+    const uint32_t rlen = t.C == 1 ? K : K - 24;
+    const uint32_t slot = t.slot0 + tid;
+    const uint32_t n    = t.noi[slot];
+    const bool     skip = n == 0;  // CB CRC was already OK: copy the saved payload (sch.c:476-480)
+    g.start[tid]        = tid * rlen / 8;
+    g.rlen8[tid]        = rlen / 8;
+    g.len[tid]          = skip ? rlen / 8 : K / 8;
+    g.src[tid]          = skip ? t.saved + (size_t)tid * t.saved_stride : t.cbout + (size_t)slot * SCH_SLOT_BYTES;
+    g.okf[tid]          = skip ? 1u : t.crc_ok[slot];
+    atomicAdd(&g.noi_sum, n);
+    atomicMax(&g.end, g.start[tid] + g.len[tid]);
+  }
+  __syncthreads();
+}
+
+// byte p of the payload: from the last CB (in decode order) whose write covered it
+__device__ __forceinline__ uint8_t tb_byte(const SchTb& t, const TbGeom& g, uint32_t p)
+{
+  int c;
+  if (t.C1 == t.C || t.K1 == t.K2) {  // one rlen: owner = min(p / rlen8, C - 1)
+    c = (int)min(p / g.rlen8[0], t.C - 1);
+  } else {
+    c = (int)t.C - 1;
+    while (c > 0 && !(p >= g.start[c] && p < g.start[c] + g.len[c])) {
+      c--;
+    }
+  }
+  return g.src[c][p - g.start[c]];
+}
+
+// tb_assemble_kernel: grid (chunks, TBs).  Chunk c covers payload bytes
+// [nbytes - (c+1) * TB_CHUNK, nbytes - c * TB_CHUNK), nbytes = (tbs + 24) / 8 -- aligned to the END
+// of the CRC'd message so leading out-of-range bytes act as zeros, which do not change a
+// zero-initialised CRC.  Each block writes its bytes of the payload and the CRC24A of its chunk
+// (computed from zero; the finish kernel places it with x^(8 * TB_CHUNK * c)).  Chunk 0 also
+// writes the bytes past nbytes (the last CB's CRC24B, sch.c:425-431).
+__global__ __launch_bounds__(TB_ASM_THREADS) void tb_assemble_kernel(const SchTb* __restrict__ tbs)
+{
+  const SchTb t = tbs[blockIdx.y];
+  if (t.status != 1) {
+    return;
+  }
+  __shared__ TbGeom   g;
+  __shared__ uint32_t wave_crc[TB_ASM_THREADS / 64];
+  tb_geometry(t, g);
+  const int      tid    = threadIdx.x;
+  const int      nbytes = (int)((t.tbs + 24) / 8);
+  const int      c1     = nbytes - (int)blockIdx.x * TB_CHUNK;  // one past the chunk's last byte
+  if (c1 <= 0) {
+    return;
+  }
+  const int p0  = c1 - TB_CHUNK + 4 * tid;
+  uint32_t  crc = 0;
+#pragma unroll
+  for (int u = 0; u < 4; u++) {
+    const int p = p0 + u;
+    uint32_t  v = 0;
+    if (p >= 0 && (uint32_t)p < g.end) {
+      v         = tb_byte(t, g, (uint32_t)p);
+      t.data[p] = (uint8_t)v;
+    }
+    crc = crc24_byte(crc, v, LTE_CRC24A);
+  }
+  if (blockIdx.x == 0) {  // bytes past the CRC'd message
+    for (uint32_t p = (uint32_t)nbytes + tid; p < g.end; p += TB_ASM_THREADS) {
+      t.data[p] = tb_byte(t, g, p);
+    }
+  }
+  // shuffle tree: crc(A|B) = crc(A) * x^(8|B|) + crc(B)
+  uint32_t  M    = xpow8(4);  // x^32 mod P: one thread's span
+  const int lane = tid & 63;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t other = (uint32_t)__shfl_xor((int)crc, off, 64);
+    crc = (lane & off) ? (clmul24(other, M, LTE_CRC24A) ^ crc) : (clmul24(crc, M, LTE_CRC24A) ^ other);
+    M   = clmul24(M, M, LTE_CRC24A);
+  }
+  if (lane == 0) {
+    wave_crc[tid >> 6] = crc;
+  }
+  __syncthreads();
+  if (tid == 0) {  // M = x^(8 * 256): one wave's span
+    uint32_t r = wave_crc[0];
+    for (int w = 1; w < TB_ASM_THREADS / 64; w++) {
+      r = clmul24(r, M, LTE_CRC24A) ^ wave_crc[w];
+    }
+    t.part[blockIdx.x] = r;
+  }
+}
+
+// tb_finish_kernel: one workgroup per TB -- CB bookkeeping, TB CRC24A from the chunk CRCs,
+// saving of good CBs on failure, new-transmission resets (sch.c:458-573).
+__global__ __launch_bounds__(TB_FIN_THREADS) void tb_finish_kernel(const SchTb* __restrict__ tbs)
 {
   const SchTb t   = tbs[blockIdx.x];
   const int   tid = threadIdx.x;
@@ -169,128 +318,43 @@ __global__ __launch_bounds__(TB_THREADS) void tb_kernel(const SchTb* __restrict_
     }
     return;
   }
-  __shared__ uint8_t        pay[SCH_MAX_CB * SCH_SLOT_BYTES];  // the TB payload as decode_tb leaves it
-  __shared__ uint32_t       start[SCH_MAX_CB], len[SCH_MAX_CB], rlen8[SCH_MAX_CB];
-  __shared__ const uint8_t* src[SCH_MAX_CB];
-  __shared__ uint32_t       okf[SCH_MAX_CB];
-  __shared__ uint32_t       noi_sum, end_max, wave_crc[TB_WAVES];
-
-  const uint32_t C = t.C;
-  if (tid == 0) {
-    noi_sum = 0;
-    end_max = 0;
-  }
-  __syncthreads();
-  if (tid < (int)C) {
-    const uint32_t K    = tid < (int)t.C1 ? t.K1 : t.K2;
-    const uint32_t rlen = C == 1 ? K : K - 24;
-    const uint32_t slot = t.slot0 + tid;
-    const uint32_t n    = t.noi[slot];
-    const bool     skip = n == 0;  // CB CRC was already OK: copy the saved payload (sch.c:476-480)
-    start[tid]          = tid * rlen / 8;
-    rlen8[tid]          = rlen / 8;
-    len[tid]            = skip ? rlen / 8 : K / 8;
-    src[tid]            = skip ? t.saved + (size_t)tid * t.saved_stride : t.cbout + (size_t)slot * SCH_SLOT_BYTES;
-    okf[tid]            = skip ? 1u : t.crc_ok[slot];
-    atomicAdd(&noi_sum, n);
-    atomicMax(&end_max, start[tid] + len[tid]);
-  }
-  __syncthreads();
-  bool all_ok = true;
+  __shared__ TbGeom g;
+  __shared__ uint32_t tb_crc;
+  tb_geometry(t, g);
+  const uint32_t C      = t.C;
+  bool           all_ok = true;
   for (uint32_t c = 0; c < C; c++) {
-    all_ok = all_ok && okf[c];
+    all_ok = all_ok && g.okf[c];
   }
-  // payload: byte p comes from the last CB (in decode order) whose write covered it
-  // (sch.c:425-431: each CB writes K/8 bytes at cb*rlen/8, over the previous CB's CRC).
-  // Four independent global loads per thread in flight.
-  const uint32_t end     = end_max;
-  const bool     uniform = t.C1 == C || t.K1 == t.K2;  // one rlen: owner = min(p / rlen8, C-1)
-  const uint32_t r8      = rlen8[0];
-  for (uint32_t p0 = tid; p0 < end; p0 += 4 * TB_THREADS) {
-    uint8_t v[4];
-#pragma unroll
-    for (int u = 0; u < 4; u++) {
-      const uint32_t p = p0 + u * TB_THREADS;
-      v[u]             = 0;
-      if (p < end) {
-        int c;
-        if (uniform) {
-          c = (int)min(p / r8, C - 1);
-        } else {
-          c = (int)C - 1;
-          while (c > 0 && !(p >= start[c] && p < start[c] + len[c])) {
-            c--;
-          }
-        }
-        v[u] = src[c][p - start[c]];
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < 4; u++) {
-      const uint32_t p = p0 + u * TB_THREADS;
-      if (p < end) {
-        pay[p] = v[u];
-      }
-    }
-  }
-  __syncthreads();
-  for (uint32_t p = tid; p < end; p += TB_THREADS) {
-    t.data[p] = pay[p];
-  }
-
   bool     tb_fail = false;
   uint32_t keep    = 0;
   if (!all_ok) {
     // keep the good CBs for the next retransmission (sch.c:465-474)
     for (uint32_t c = 0; c < C; c++) {
-      if (okf[c]) {
+      if (g.okf[c]) {
         keep |= 1u << c;
-        for (uint32_t i = tid; i < rlen8[c]; i += TB_THREADS) {
-          t.saved[(size_t)c * t.saved_stride + i] = pay[start[c] + i];
+        for (uint32_t i = tid; i < g.rlen8[c]; i += TB_FIN_THREADS) {
+          t.saved[(size_t)c * t.saved_stride + i] = t.data[g.start[c] + i];
         }
       }
     }
   } else if (C > 1) {
-    // TB CRC24A over tbs + 24 bits (srsran_crc_match_byte, sch.c:560): 256 equal chunks
-    // aligned to the END of the message (leading zero bytes do not change a zero-init CRC),
-    // then a shuffle tree: crc(A|B) = crc(A) * x^(8|B|) + crc(B).
-    const int      nbytes = (int)((t.tbs + 24) / 8);
-    const int      per    = (nbytes + TB_THREADS - 1) / TB_THREADS;
-    const int      b1     = nbytes - (TB_THREADS - 1 - tid) * per;
-    const int      b0     = b1 - per;
-    uint32_t       crc    = 0;
-    for (int b = max(b0, 0); b < b1; b++) {
-      crc = crc24_byte(crc, b >= 0 ? pay[b] : 0u, LTE_CRC24A);
-    }
-    uint32_t M = xpow8((uint32_t)per);  // multiplier for a span of 2^l chunks, l = level
-    const int lane = tid & 63;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const uint32_t other = (uint32_t)__shfl_xor((int)crc, off, 64);
-      crc = (lane & off) ? (clmul24(other, M, LTE_CRC24A) ^ crc) : (clmul24(crc, M, LTE_CRC24A) ^ other);
-      M   = clmul24(M, M, LTE_CRC24A);
-    }
-    if (lane == 0) {
-      wave_crc[tid >> 6] = crc;
+    // TB CRC24A over tbs + 24 bits (srsran_crc_match_byte, sch.c:560): Horner over the chunks
+    if (tid == 0) {
+      const uint32_t nbytes = (t.tbs + 24) / 8;
+      const uint32_t nch    = (nbytes + TB_CHUNK - 1) / TB_CHUNK;
+      const uint32_t Mc     = xpow8(TB_CHUNK);
+      uint32_t       r      = 0;
+      for (int c = (int)nch - 1; c >= 0; c--) {
+        r = clmul24(r, Mc, LTE_CRC24A) ^ t.part[c];
+      }
+      tb_crc = r;
     }
     __syncthreads();
-    if (tid < 64) {  // M = x^(8 * per * 64): one wave's span; same tree over the wave CRCs
-      crc = lane < TB_WAVES ? wave_crc[lane] : 0u;
-#pragma unroll
-      for (int off = 1; off < TB_WAVES; off <<= 1) {
-        const uint32_t other = (uint32_t)__shfl_xor((int)crc, off, 64);
-        crc = (lane & off) ? (clmul24(other, M, LTE_CRC24A) ^ crc) : (clmul24(crc, M, LTE_CRC24A) ^ other);
-        M   = clmul24(M, M, LTE_CRC24A);
-      }
-      if (lane == 0) {
-        wave_crc[0] = crc;
-      }
-    }
-    __syncthreads();
-    tb_fail = wave_crc[0] != 0;  // srsran_softbuffer_rx_reset_cb_crc (sch.c:567)
+    tb_fail = tb_crc != 0;  // srsran_softbuffer_rx_reset_cb_crc (sch.c:567)
   }
   if (tid < (int)C) {
-    t.cb_crc[tid] = (okf[tid] && !tb_fail) ? 1 : 0;
+    t.cb_crc[tid] = (g.okf[tid] && !tb_fail) ? 1 : 0;
   }
   if (t.new_data) {
     // what reset_tbs cleared and this decode did not rewrite: flags past C, soft
@@ -300,13 +364,23 @@ __global__ __launch_bounds__(TB_THREADS) void tb_kernel(const SchTb* __restrict_
   if (tid == 0) {
     *t.tb_crc = all_ok ? 1 : 0;
     *t.result = (all_ok && !tb_fail) ? 0 : -1;
-    *t.avg    = (float)noi_sum / (float)C;
+    *t.avg    = (float)g.noi_sum / (float)C;
   }
 }
 
-hipError_t rm_rx_launch(const RmSlot* d_slots, uint32_t nslots, uint32_t max_len, hipStream_t stream)
+hipError_t rm_rx_launch(const RmSlot* d_slots, uint32_t nslots, uint32_t max_len, uint32_t max_e, hipStream_t stream)
 {
   StageScope timing_scope(ST_RM, stream);
+  if (nslots == 0) {
+    return hipSuccess;
+  }
+  if (max_e <= (uint32_t)RM_LDS_MAX_E) {
+    for (uint32_t s0 = 0; s0 < nslots; s0 += 65535) {
+      const uint32_t n = nslots - s0 < 65535 ? nslots - s0 : 65535;
+      hipLaunchKernelGGL(rm_rx_lds_kernel, dim3(n), dim3(RM_LDS_THREADS), 0, stream, d_slots + s0);
+    }
+    return hipGetLastError();
+  }
   const uint32_t per_block = RM_THREADS * RM_PER_THREAD;
   const uint32_t gx        = (max_len + per_block - 1) / per_block;
   for (uint32_t s0 = 0; s0 < nslots; s0 += 65535) {
@@ -316,13 +390,20 @@ hipError_t rm_rx_launch(const RmSlot* d_slots, uint32_t nslots, uint32_t max_len
   return hipGetLastError();
 }
 
-hipError_t tb_launch(const SchTb* d_tbs, uint32_t ntb, hipStream_t stream)
+hipError_t tb_launch(const SchTb* d_tbs, uint32_t ntb, uint32_t max_tbs, hipStream_t stream)
 {
   StageScope timing_scope(ST_TB, stream);
   if (ntb == 0) {
     return hipSuccess;
   }
-  hipLaunchKernelGGL(tb_kernel, dim3(ntb), dim3(TB_THREADS), 0, stream, d_tbs);
+  const uint32_t nch = ((max_tbs + 24) / 8 + TB_CHUNK - 1) / TB_CHUNK;
+  if (nch > TB_MAX_CHUNKS) {
+    return hipErrorInvalidValue;
+  }
+  if (nch) {
+    hipLaunchKernelGGL(tb_assemble_kernel, dim3(nch, ntb), dim3(TB_ASM_THREADS), 0, stream, d_tbs);
+  }
+  hipLaunchKernelGGL(tb_finish_kernel, dim3(ntb), dim3(TB_FIN_THREADS), 0, stream, d_tbs);
   return hipGetLastError();
 }
 

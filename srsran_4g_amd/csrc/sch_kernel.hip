@@ -110,8 +110,8 @@ __global__ __launch_bounds__(RM_LDS_THREADS) void rm_rx_lds_kernel(const RmSlot*
   }
 }
 
-static constexpr int TB_ASM_THREADS = 256;
-static constexpr int TB_CHUNK       = 4 * TB_ASM_THREADS;  // payload bytes per assembly block
+static constexpr int TB_ASM_THREADS = 64;                   // one wave per chunk
+static constexpr int TB_CHUNK       = 16 * TB_ASM_THREADS;  // payload bytes per assembly block
 static constexpr int TB_FIN_THREADS = 256;
 static constexpr int TB_THREADS     = TB_FIN_THREADS;  // reset_range stride
 
@@ -158,6 +158,29 @@ __device__ __forceinline__ uint32_t xpow8(uint32_t m)
   return r;
 }
 
+// zero bytes [0, nbytes) of p with 16-byte stores where aligned (block-cooperative)
+__device__ void zero_bytes(uint8_t* p, uint32_t nbytes, int tid, int nthreads)
+{
+  const uint32_t head = (uint32_t)((16 - ((uintptr_t)p & 15)) & 15);
+  if (nbytes <= head + 16) {
+    for (uint32_t i = tid; i < nbytes; i += nthreads) {
+      p[i] = 0;
+    }
+    return;
+  }
+  const uint32_t nvec = (nbytes - head) / 16;
+  for (uint32_t i = tid; i < head; i += nthreads) {
+    p[i] = 0;
+  }
+  uint4* v = reinterpret_cast<uint4*>(p + head);
+  for (uint32_t i = tid; i < nvec; i += nthreads) {
+    v[i] = make_uint4(0, 0, 0, 0);
+  }
+  for (uint32_t i = head + 16 * nvec + tid; i < nbytes; i += nthreads) {
+    p[i] = 0;
+  }
+}
+
 // Zero (as srsran_softbuffer_rx_reset_cb does) CB soft buffers [sb0, n), saved payloads
 // [0, n) except those in `keep`, and CB flags [f0, max_cb).
 __device__ void reset_range(const SchTb& t, uint32_t sb0, uint32_t n, uint32_t f0, uint32_t keep)
@@ -171,18 +194,13 @@ __device__ void reset_range(const SchTb& t, uint32_t sb0, uint32_t n, uint32_t f
     }
   }
   if (keep == 0) {  // one contiguous range
-    const uint32_t nb = n * t.saved_stride;
-    for (uint32_t i = tid; i < nb; i += TB_THREADS) {
-      t.saved[i] = 0;
-    }
+    zero_bytes(t.saved, n * t.saved_stride, tid, TB_THREADS);
   } else {
     for (uint32_t c = 0; c < n; c++) {
       if (c < 32 && ((keep >> c) & 1u)) {
         continue;
       }
-      for (uint32_t i = tid; i < t.saved_stride; i += TB_THREADS) {
-        t.saved[(size_t)c * t.saved_stride + i] = 0;
-      }
+      zero_bytes(t.saved + (size_t)c * t.saved_stride, t.saved_stride, tid, TB_THREADS);
     }
   }
   for (uint32_t c = f0 + tid; c < t.max_cb; c += TB_THREADS) {
@@ -239,12 +257,42 @@ __device__ __forceinline__ uint8_t tb_byte(const SchTb& t, const TbGeom& g, uint
   return g.src[c][p - g.start[c]];
 }
 
-// tb_assemble_kernel: grid (chunks, TBs).  Chunk c covers payload bytes
+// CRC24A byte table and x^(128 k) mod CRC24A (k = 0..63), built at compile time
+struct Crc24Tables {
+  uint32_t byte[256];
+  uint32_t xp16[64];
+};
+constexpr Crc24Tables make_crc24_tables()
+{
+  Crc24Tables t{};
+  for (uint32_t b = 0; b < 256; b++) {
+    uint32_t c = b << 16;
+    for (int k = 0; k < 8; k++) {
+      c = (c & 0x800000u) ? ((c << 1) ^ LTE_CRC24A) : (c << 1);
+    }
+    t.byte[b] = c & 0xFFFFFFu;
+  }
+  uint32_t x128 = 1;
+  for (int k = 0; k < 16; k++) {  // x^128 = (x^8)^16
+    x128 = ce_clmul_mod24(x128, 0x100u, LTE_CRC24A);
+  }
+  uint32_t m = 1;
+  for (int k = 0; k < 64; k++) {
+    t.xp16[k] = m;
+    m         = ce_clmul_mod24(m, x128, LTE_CRC24A);
+  }
+  return t;
+}
+__device__ const Crc24Tables kCrcT = make_crc24_tables();
+
+// tb_assemble_kernel: grid (chunks, TBs), one wave per chunk.  Chunk c covers payload bytes
 // [nbytes - (c+1) * TB_CHUNK, nbytes - c * TB_CHUNK), nbytes = (tbs + 24) / 8 -- aligned to the END
 // of the CRC'd message so leading out-of-range bytes act as zeros, which do not change a
-// zero-initialised CRC.  Each block writes its bytes of the payload and the CRC24A of its chunk
-// (computed from zero; the finish kernel places it with x^(8 * TB_CHUNK * c)).  Chunk 0 also
-// writes the bytes past nbytes (the last CB's CRC24B, sch.c:425-431).
+// zero-initialised CRC.  Lane j gathers 16 consecutive bytes, writes them to the payload and
+// CRCs them (LDS byte table); its CRC moves to the chunk end with one multiply by
+// x^(128 (63 - j)) and the lanes XOR-reduce.  The finish kernel places chunk c with
+// x^(8 * TB_CHUNK * c).  Chunk 0 also writes the bytes past nbytes (the last CB's CRC24B,
+// sch.c:425-431).
 __global__ __launch_bounds__(TB_ASM_THREADS) void tb_assemble_kernel(const SchTb* __restrict__ tbs)
 {
   const SchTb t = tbs[blockIdx.y];
@@ -252,50 +300,53 @@ __global__ __launch_bounds__(TB_ASM_THREADS) void tb_assemble_kernel(const SchTb
     return;
   }
   __shared__ TbGeom   g;
-  __shared__ uint32_t wave_crc[TB_ASM_THREADS / 64];
+  __shared__ uint32_t ctab[256];
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < 256 / TB_ASM_THREADS; k++) {
+    ctab[tid + k * TB_ASM_THREADS] = kCrcT.byte[tid + k * TB_ASM_THREADS];
+  }
   tb_geometry(t, g);
-  const int      tid    = threadIdx.x;
-  const int      nbytes = (int)((t.tbs + 24) / 8);
-  const int      c1     = nbytes - (int)blockIdx.x * TB_CHUNK;  // one past the chunk's last byte
+  const int nbytes = (int)((t.tbs + 24) / 8);
+  const int c1     = nbytes - (int)blockIdx.x * TB_CHUNK;  // one past the chunk's last byte
   if (c1 <= 0) {
     return;
   }
-  const int p0  = c1 - TB_CHUNK + 4 * tid;
-  uint32_t  crc = 0;
-#pragma unroll
-  for (int u = 0; u < 4; u++) {
+  const bool uniform = t.C1 == t.C || t.K1 == t.K2;
+  const int  p0      = c1 - TB_CHUNK + 16 * tid;
+  uint32_t   crc     = 0;
+  int        c       = -1;
+#pragma unroll 4
+  for (int u = 0; u < 16; u++) {
     const int p = p0 + u;
     uint32_t  v = 0;
     if (p >= 0 && (uint32_t)p < g.end) {
-      v         = tb_byte(t, g, (uint32_t)p);
+      if (uniform) {
+        if (c < 0) {
+          c = (int)min((uint32_t)p / g.rlen8[0], t.C - 1);
+        } else if (c + 1 < (int)t.C && (uint32_t)p >= g.start[c + 1]) {
+          c++;
+        }
+        v = g.src[c][p - g.start[c]];
+      } else {
+        v = tb_byte(t, g, (uint32_t)p);
+      }
       t.data[p] = (uint8_t)v;
     }
-    crc = crc24_byte(crc, v, LTE_CRC24A);
+    crc = ((crc << 8) ^ ctab[((crc >> 16) ^ v) & 0xFFu]) & 0xFFFFFFu;
   }
   if (blockIdx.x == 0) {  // bytes past the CRC'd message
     for (uint32_t p = (uint32_t)nbytes + tid; p < g.end; p += TB_ASM_THREADS) {
       t.data[p] = tb_byte(t, g, p);
     }
   }
-  // shuffle tree: crc(A|B) = crc(A) * x^(8|B|) + crc(B)
-  uint32_t  M    = xpow8(4);  // x^32 mod P: one thread's span
-  const int lane = tid & 63;
+  crc = clmul24(crc, kCrcT.xp16[TB_ASM_THREADS - 1 - tid], LTE_CRC24A);
 #pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint32_t other = (uint32_t)__shfl_xor((int)crc, off, 64);
-    crc = (lane & off) ? (clmul24(other, M, LTE_CRC24A) ^ crc) : (clmul24(crc, M, LTE_CRC24A) ^ other);
-    M   = clmul24(M, M, LTE_CRC24A);
+  for (int off = 32; off > 0; off >>= 1) {
+    crc ^= (uint32_t)__shfl_xor((int)crc, off, 64);
   }
-  if (lane == 0) {
-    wave_crc[tid >> 6] = crc;
-  }
-  __syncthreads();
-  if (tid == 0) {  // M = x^(8 * 256): one wave's span
-    uint32_t r = wave_crc[0];
-    for (int w = 1; w < TB_ASM_THREADS / 64; w++) {
-      r = clmul24(r, M, LTE_CRC24A) ^ wave_crc[w];
-    }
-    t.part[blockIdx.x] = r;
+  if (tid == 0) {
+    t.part[blockIdx.x] = crc;
   }
 }
 

@@ -33,6 +33,18 @@ METRIC = "turbo-decoded info Mbps + PDSCH subframes/s, 20 MHz 64QAM, 1/2/4/8 GPU
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
+def pmc_traffic(workload, kernel, units):
+    """HBM bytes per launch of `kernel` from profiles/pmc_traffic.json, scaled to `units` code blocks."""
+    tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        e = json.load(open(tf)).get(workload, {}).get(kernel)
+    except Exception:
+        return None
+    if not e:
+        return None
+    return int(round(e["bytes"] * units / e["units"]))
+
+
 def shard(rank):
     """Per-rank unit of work (independent carriers / CB batches, no data-path collective):
     rank r decodes its own carrier (cell id 1 + r) from its own seeded synthetic inputs."""
@@ -76,7 +88,8 @@ def parse():
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--workload", choices=["all188", "k6144", "dlsch", "pdsch"], default="all188")
     p.add_argument("--snr", type=float, default=30.0, help="pdsch: AWGN SNR (dB) of the synthetic subframes")
-    p.add_argument("--subframes", type=int, default=64, help="dlsch: subframes (2 TBs each) per step")
+    p.add_argument("--subframes", type=int, default=78,
+                   help="dlsch / pdsch: subframes (2 TBs each) per step; 78 x 26 CBs = two full turbo-decoder rounds")
     p.add_argument("--sigma", type=float, default=0.42, help="dlsch: AWGN std on +-1 symbols before LLR scaling")
     p.add_argument("--batch", type=int, default=1024, help="code blocks per size per step")
     p.add_argument("--iters", type=int, default=8, help="half-iterations (srsran nof_iterations)")
@@ -176,18 +189,26 @@ def run_dlsch(args, torch, dist, world, rank, device):
     bits_per_step = ntb * C3_TBS
     value = world * bits_per_step * args.steps / elapsed / 1e6
 
-    # whole-batch launch time on the stream (rm + turbo + TB kernels), outside the timed region
-    e0 = torch.cuda.Event(enable_timing=True)
-    e1 = torch.cuda.Event(enable_timing=True)
-    e0.record(stream)
-    step()
-    e1.record(stream)
+    # per-stage kernel durations (library HIP events on the launch stream), outside the timed region
+    from srsran_4g_amd import prof
+    prof.enable(True)
+    nrep = max(1, min(args.steps, 3))
+    for _ in range(nrep):
+        step()
     torch.cuda.synchronize()
-    batch_ms = e0.elapsed_time(e1)
-    # algorithmic bytes per TB: E LLRs in + soft buffer write (new data) and turbo read per
-    # half-iteration is on-chip after the first read -> count E*2 + C*(3K+12)*2*2 + TBS/8 out
-    algo = C3_BITS * 2 + 13 * (3 * 5824 + 12) * 2 * 2 + C3_TBS // 8
-    achieved = ntb * algo / (batch_ms * 1e-3) / 1e9
+    stages = prof.read()
+    prof.enable(False)
+    sb_ = stage_bytes(0, 0, ntb)
+    per_stage = {}
+    for name, (ms, n) in stages.items():
+        lps = n / nrep
+        per_stage[name] = {"ms_per_step": round(ms / nrep, 4), "launches_per_step": lps,
+                           "avg_launch_ms": round(ms / n, 4),
+                           "GBps": round(sb_.get(name, 0) / lps / (ms / n * 1e-3) / 1e9, 1)}
+    dom = max(per_stage, key=lambda k: per_stage[k]["ms_per_step"])
+    d = per_stage[dom]
+    bytes_per_launch = sb_[dom] / d["launches_per_step"]
+    achieved = bytes_per_launch / (d["avg_launch_ms"] * 1e-3) / 1e9
     result = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -213,15 +234,16 @@ def run_dlsch(args, torch, dist, world, rank, device):
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "rm_rx_kernel + tdec_kernel<16,ES> + tb_kernel (whole batch)",
+            "kernel": dom,
             "achieved": round(achieved, 2),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5),
-            "traffic": None,
-            "avg_launch_ms": round(batch_ms, 4),
-            "algo_bytes_per_launch": int(ntb * algo),
+            "traffic": pmc_traffic(args.workload, dom, ntb * 13) if dom == "tdec_kernel" else None,
+            "avg_launch_ms": d["avg_launch_ms"],
+            "algo_bytes_per_launch": int(bytes_per_launch),
         },
+        "stages": per_stage,
     }
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         from oracle import Oracle, Reference, ref_available
@@ -306,6 +328,13 @@ def run_pdsch(args, torch, dist, world, rank, device):
             raise RuntimeError("srsran_ue_dl_gpu_decode_batch failed")
 
     elapsed = timed_region(step, args.steps, args.warmup, world, dist, torch.cuda.synchronize, device)
+    # host enqueue cost of one step (the API builds descriptors and launches asynchronously)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    host_ms = (time.perf_counter() - t1) / args.steps * 1e3
+    torch.cuda.synchronize()
     res = d_res.cpu().numpy()
     avg = d_avg.cpu().numpy()
     pl = d_pl.cpu().numpy()
@@ -333,13 +362,7 @@ def run_pdsch(args, torch, dist, world, rank, device):
     d = per_stage[dom]
     bytes_per_launch = sb[dom] / d["launches_per_step"]
     achieved = bytes_per_launch / (d["avg_launch_ms"] * 1e-3) / 1e9
-    traffic = None
-    tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(tf):
-        try:
-            traffic = json.load(open(tf)).get(args.workload, {}).get(dom)
-        except Exception:
-            traffic = None
+    traffic = pmc_traffic(args.workload, dom, nsf * 26) if dom == "tdec_kernel" else None
     result = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -376,6 +399,7 @@ def run_pdsch(args, torch, dist, world, rank, device):
             "algo_bytes_per_launch": int(bytes_per_launch),
         },
         "stages": per_stage,
+        "host_enqueue_ms_per_step": round(host_ms, 4),
         "chain_bytes_per_sf": 2 * SF_LEN * 8 + 2 * C3_TBS // 8,
     }
     if (res != 0).any():
@@ -499,13 +523,7 @@ def main():
     avg_ms = dk["ms"] / dk["launches"]
     bytes_per_launch = dk["bytes"] / dk["launches"]
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
-    traffic = None
-    tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(tf):
-        try:
-            traffic = json.load(open(tf)).get(args.workload, {}).get(dom)
-        except Exception:
-            traffic = None
+    traffic = pmc_traffic(args.workload, dom, args.batch)
 
     result = {
         "metric": METRIC,

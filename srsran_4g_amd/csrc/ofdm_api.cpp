@@ -76,7 +76,7 @@ int configure(srsran_ofdm_t* q, uint32_t nof_prb, uint32_t symbol_sz)
   }
   const uint32_t N = symbol_sz ? symbol_sz : (uint32_t)srsran_symbol_sz(nof_prb);
   OfdmArgs       a{};
-  a.nstages = ofdm_plan(N, a.radix);
+  a.nstages = ofdm_plan(N, a.radix, a.ns_magic);
   if ((int)N <= 0 || N > OFDM_MAX_N || a.nstages <= 0 || 12 * nof_prb > N) {
     fprintf(stderr, "[srsran_ofdm] unsupported symbol size %u\n", N);
     return SRSRAN_ERROR;

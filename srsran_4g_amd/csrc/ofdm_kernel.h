@@ -22,6 +22,7 @@ struct OfdmArgs {
   double        cfo;       // z[n] = x[n] exp(j 2 pi cfo n), n from the subframe start; 0 = off
   int           nstages;
   int           radix[OFDM_MAX_STAGES];
+  uint32_t      ns_magic[OFDM_MAX_STAGES];  // ceil(2^32 / Ns) of every stage (j / Ns by __umulhi)
 };
 
 // grid: (14, nrx, nsf) workgroups
@@ -29,6 +30,7 @@ hipError_t ofdm_rx_launch(const OfdmArgs& a, uint32_t nsf, hipStream_t stream);
 
 // factor N into radices 8/4/3/2 (largest first); returns the number of stages or -1
 int ofdm_plan(uint32_t N, int* radix);
+int ofdm_plan(uint32_t N, int* radix, uint32_t* ns_magic);
 
 // standalone CFO correction z[n] = x[n] exp(j 2 pi f n)
 hipError_t cfo_launch(const float2* in, float2* out, uint32_t n, double f, hipStream_t stream);

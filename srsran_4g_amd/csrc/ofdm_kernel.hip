@@ -71,12 +71,17 @@ __device__ __forceinline__ void dft8(float2* v)
   }
 }
 
+// j / Ns for j < 2^16 and Ns <= 2^12 with m = ceil(2^32 / Ns) (exact in that range)
+__device__ __forceinline__ uint32_t divm(uint32_t j, uint32_t m) { return __umulhi(j, m); }
+
 template <int R>
-__device__ __forceinline__ void stage(const float2* src, float2* dst, const float2* tw, uint32_t N, uint32_t Ns)
+__device__ __forceinline__ void stage(const float2* src, float2* dst, const float2* __restrict__ tw, uint32_t N,
+                                      uint32_t Ns, uint32_t mNs)
 {
   const uint32_t nb = N / R, tstep = N / (Ns * R);
   for (uint32_t j = threadIdx.x; j < nb; j += OFDM_THREADS) {
-    const uint32_t k = j % Ns;
+    const uint32_t q = Ns > 1 ? divm(j, mNs) : j;
+    const uint32_t k = j - q * Ns;
     float2         v[R];
 #pragma unroll
     for (int r = 0; r < R; r++) {
@@ -85,7 +90,7 @@ __device__ __forceinline__ void stage(const float2* src, float2* dst, const floa
     if (Ns > 1) {
 #pragma unroll
       for (int r = 1; r < R; r++) {
-        v[r] = cmul(v[r], tw[(r * k * tstep) % N]);
+        v[r] = cmul(v[r], tw[r * k * tstep]);  // r k tstep < R Ns tstep = N
       }
     }
     if constexpr (R == 8) {
@@ -97,7 +102,7 @@ __device__ __forceinline__ void stage(const float2* src, float2* dst, const floa
     } else {
       dft2(v);
     }
-    const uint32_t base = (j / Ns) * Ns * R + k;
+    const uint32_t base = q * Ns * R + k;
 #pragma unroll
     for (int r = 0; r < R; r++) {
       dst[base + r * Ns] = v[r];
@@ -128,15 +133,16 @@ __global__ __launch_bounds__(OFDM_THREADS) void ofdm_rx_kernel(OfdmArgs a)
   __syncthreads();
   uint32_t Ns = 1, cur = 0;
   for (int st = 0; st < a.nstages; st++) {
-    const int R = a.radix[st];
+    const int      R   = a.radix[st];
+    const uint32_t mNs = a.ns_magic[st];
     if (R == 8) {
-      stage<8>(buf[cur], buf[cur ^ 1], a.tw, N, Ns);
+      stage<8>(buf[cur], buf[cur ^ 1], a.tw, N, Ns, mNs);
     } else if (R == 4) {
-      stage<4>(buf[cur], buf[cur ^ 1], a.tw, N, Ns);
+      stage<4>(buf[cur], buf[cur ^ 1], a.tw, N, Ns, mNs);
     } else if (R == 3) {
-      stage<3>(buf[cur], buf[cur ^ 1], a.tw, N, Ns);
+      stage<3>(buf[cur], buf[cur ^ 1], a.tw, N, Ns, mNs);
     } else {
-      stage<2>(buf[cur], buf[cur ^ 1], a.tw, N, Ns);
+      stage<2>(buf[cur], buf[cur ^ 1], a.tw, N, Ns, mNs);
     }
     Ns *= (uint32_t)R;
     cur ^= 1;
@@ -152,6 +158,17 @@ __global__ __launch_bounds__(OFDM_THREADS) void ofdm_rx_kernel(OfdmArgs a)
     }
     dst[k] = v;
   }
+}
+
+int ofdm_plan(uint32_t N, int* radix, uint32_t* ns_magic)
+{
+  const int n = ofdm_plan(N, radix);
+  uint32_t  Ns = 1;
+  for (int st = 0; st < n; st++) {
+    ns_magic[st] = Ns > 1 ? (uint32_t)((((uint64_t)1 << 32) + Ns - 1) / Ns) : 0u;
+    Ns *= (uint32_t)radix[st];
+  }
+  return n;
 }
 
 int ofdm_plan(uint32_t N, int* radix)

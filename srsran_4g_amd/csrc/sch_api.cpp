@@ -238,9 +238,12 @@ int enqueue_batch(srsran_sch_t* q, uint32_t ntb, const srsran_dlsch_gpu_tb_t* tb
     const srsran_cbsegm_t& s  = plan[i].s;
     const SbGpu*           sb = (const SbGpu*)tbs[i].softbuffer->gpu;
     const uint32_t         Qm = tbs[i].Qm;
+    InvTable               tk[2];  // the de-matching tables of K1 and K2 (looked up once per TB)
+    if (!inv_table(s.K1_idx, tbs[i].rv, true, &tk[0]) || (s.C2 && !inv_table(s.K2_idx, tbs[i].rv, true, &tk[1]))) {
+      return SRSRAN_ERROR;
+    }
     for (uint32_t cb = 0; cb < s.C; cb++) {
       const uint32_t K     = cb < s.C1 ? s.K1 : s.K2;
-      const uint32_t K_idx = cb < s.C1 ? s.K1_idx : s.K2_idx;
       // E split over the CBs, including the reference's '>' (sch.c:398-407)
       const uint32_t Gp    = tbs[i].nof_e_bits / Qm;
       const uint32_t gamma = Gp % s.C;
@@ -250,10 +253,7 @@ int enqueue_batch(srsran_sch_t* q, uint32_t ntb, const srsran_dlsch_gpu_tb_t* tb
         n_e2 = n_e + Qm;
         rp   = (s.C - gamma) * n_e + (cb - (s.C - gamma)) * n_e2;
       }
-      InvTable t;
-      if (!inv_table(K_idx, tbs[i].rv, true, &t)) {
-        return SRSRAN_ERROR;
-      }
+      const InvTable& t    = tk[cb < s.C1 ? 0 : 1];
       const uint32_t slot = plan[i].slot0 + cb;
       RmSlot&        r    = rm[slot];
       r.e                 = tbs[i].d_e_bits + rp;

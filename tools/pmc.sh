@@ -1,17 +1,16 @@
 #!/bin/bash
-# PMC counter passes (each in its own rocprofv3 run) for the k6144 bench workload.
-# Usage: tools/pmc.sh TAG [workload]
+# PMC counter passes (each its own rocprofv3 run, --pmc only) for one bench workload.
+# Usage: tools/pmc.sh TAG WORKLOAD [extra bench args]
 set -o pipefail
-TAG=${1:-pmc}; WL=${2:-k6144}
-OUT=gpurun_out/$TAG
+TAG=${1:-pmc}; WL=${2:-k6144}; shift 2
+OUT=$GRAFT_REPO_ROOT/gpurun_out/$TAG
 mkdir -p $OUT
-export TMPDIR=/tmp
-CMD="python3 bench.py --workload $WL --steps 3 --warmup 1 --cpu-seconds 0"
+cd /tmp && export TMPDIR=/tmp
 i=0
-for P in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" \
-         "SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INST_CYCLES_SALU SQ_ACTIVE_INST_LDS" \
-         "FETCH_SIZE" "WRITE_SIZE" "GRBM_GUI_ACTIVE GRBM_COUNT" ; do
+for P in "FETCH_SIZE" "WRITE_SIZE" \
+         "SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU" \
+         "SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE"; do
   i=$((i+1))
-  timeout -k 10 240 rocprofv3 --pmc $P --output-format csv -d $OUT/p$i -o pmc -- $CMD > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/p$i.log; exit 1; }
+  timeout -k 10 300 rocprofv3 --pmc $P --output-format csv -d $OUT/p$i -o pmc -- python3 $GRAFT_REPO_ROOT/bench.py --workload $WL --steps 2 --warmup 1 --cpu-seconds 0 "$@" > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/p$i.log; exit 1; }
 done
 echo done

@@ -1,0 +1,35 @@
+"""Summarise tools/pmc.sh passes: per-kernel average counters per dispatch, and HBM traffic per
+launch corrected as MI355X_MICROARCH.md prescribes (FETCH_SIZE x 2 on gfx950, WRITE_SIZE as is;
+both in KiB).  Usage: python tools/pmc_summary.py gpurun_out/pmc_X WORKLOAD out.json"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def short(name):
+    n = name.split("(")[0].replace("void ", "").replace("srsran_amd::", "")
+    return n
+
+
+def main(d, workload, out):
+    acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in sorted(glob.glob(os.path.join(d, "p*", "*counter_collection.csv"))):
+        for r in csv.DictReader(open(f)):
+            acc[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    kernels = {}
+    for k, cs in acc.items():
+        if "rocclr" in k or "at::native" in k:
+            continue
+        avg = {c: sum(v) / len(v) for c, v in cs.items()}
+        if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
+            avg["hbm_bytes_per_launch"] = (2 * avg["FETCH_SIZE"] + avg["WRITE_SIZE"]) * 1024
+        kernels[k] = {c: round(v, 1) for c, v in avg.items()}
+    json.dump({"workload": workload, "source": d, "kernels": kernels}, open(out, "w"), indent=1)
+    print(json.dumps({k: v.get("hbm_bytes_per_launch") for k, v in kernels.items()}))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:4])

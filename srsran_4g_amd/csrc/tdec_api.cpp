@@ -575,11 +575,21 @@ int srsran_tdec_gpu_run_batch(uint32_t       long_cb,
 namespace {
 // Internal fork/join stream pool for srsran_tdec_gpu_run_multi (per device).
 constexpr int kPoolStreams = 4;
+// Device descriptors of one fused multi-size launch (per decoder class).
+struct MultiDesc {
+  char*      h_stage = nullptr;  // pinned: TdecArgs[n] | first[n]
+  char*      d_stage = nullptr;
+  size_t     cap     = 0;
+  hipEvent_t copied  = nullptr;  // the last upload from h_stage finished
+  bool       used    = false;
+};
+
 struct StreamPool {
   int         device = -1;
   hipStream_t s[kPoolStreams];
   hipEvent_t  done[kPoolStreams];
   hipEvent_t  fork;
+  MultiDesc   md[3];  // decoder classes 16, 8, 1 sub-blocks
 };
 std::mutex               g_pool_mu;
 std::vector<StreamPool*> g_pools;
@@ -606,6 +616,11 @@ StreamPool* get_pool()
   }
   if (hipEventCreateWithFlags(&p->fork, hipEventDisableTiming) != hipSuccess) {
     return nullptr;
+  }
+  for (auto& m : p->md) {
+    if (hipEventCreateWithFlags(&m.copied, hipEventDisableTiming) != hipSuccess) {
+      return nullptr;
+    }
   }
   g_pools.push_back(p);
   return p;
@@ -669,10 +684,81 @@ int srsran_tdec_gpu_run_multi(uint32_t              nof_groups,
   }
   const int n_end = nof_iterations > 0 ? (int)nof_iterations : 1;
   int       ret   = SRSRAN_SUCCESS;
-  for (uint32_t i = 0; i < nof_groups && ret == SRSRAN_SUCCESS; i++) {
-    const uint32_t g = order[i];
-    ret = enqueue(cfg[g], d_input[g], in_stride[g], layout_sb, d_output[g], nof_cb[g], 0, n_end, nullptr,
-                  p->s[i % kPoolStreams]);
+  // One fused launch per decoder class (16 / 8 / generic): the sizes of a class share one grid
+  // (more workgroups in flight than per-size launches, no per-launch tail); classes run on
+  // separate pool streams, longest first.
+  const int cls_nsb[3] = {16, 8, 1};
+  for (int ci = 0; ci < 3 && ret == SRSRAN_SUCCESS; ci++) {
+    std::vector<uint32_t> gs;
+    for (uint32_t i = 0; i < nof_groups; i++) {
+      if (cfg[order[i]]->nsb == cls_nsb[ci] && nof_cb[order[i]] > 0) {
+        gs.push_back(order[i]);
+      }
+    }
+    if (gs.empty()) {
+      continue;
+    }
+    hipStream_t st = p->s[ci];
+    if (gs.size() == 1) {
+      const uint32_t g = gs[0];
+      ret = enqueue(cfg[g], d_input[g], in_stride[g], layout_sb, d_output[g], nof_cb[g], 0, n_end, nullptr, st);
+      continue;
+    }
+    const int      cpw   = tdec_cpw(cls_nsb[ci]);
+    const size_t   n     = gs.size();
+    const size_t   abyte = n * sizeof(TdecArgs);
+    const size_t   need  = abyte + n * sizeof(uint32_t);
+    MultiDesc&     m     = p->md[ci];
+    if (m.used) {
+      hipEventSynchronize(m.copied);
+    }
+    if (need > m.cap) {
+      hipStreamSynchronize(st);
+      hipHostFree(m.h_stage);
+      hipFree(m.d_stage);
+      m.h_stage = m.d_stage = nullptr;
+      m.cap                 = 0;
+      if (hipHostMalloc((void**)&m.h_stage, 2 * need) != hipSuccess || hipMalloc((void**)&m.d_stage, 2 * need) != hipSuccess) {
+        return SRSRAN_ERROR;
+      }
+      m.cap = 2 * need;
+    }
+    TdecArgs* ha    = reinterpret_cast<TdecArgs*>(m.h_stage);
+    uint32_t* hf    = reinterpret_cast<uint32_t*>(m.h_stage + abyte);
+    uint32_t  nblk  = 0;
+    size_t    lds   = 0;
+    static const uint32_t dbg = getenv("SRSRAN_TDEC_ABLATE") ? (uint32_t)atoi(getenv("SRSRAN_TDEC_ABLATE")) : 0;
+    for (size_t k = 0; k < n; k++) {
+      const uint32_t g = gs[k];
+      const Config*  c = cfg[g];
+      TdecArgs       a = c->proto;
+      a.in             = d_input[g];
+      a.in_stride      = in_stride[g];
+      a.layout_sb      = c->nsb > 1 ? layout_sb : 0;
+      a.ncb            = nof_cb[g];
+      a.n_start        = 0;
+      a.n_end          = n_end;
+      a.out            = d_output[g];
+      a.tfwd           = c->d_tfwd;
+      a.trev           = c->d_trev;
+      a.tfwd_nat       = c->d_tfwd_nat;
+      a.trev_nat       = c->d_trev_nat;
+      a.state          = nullptr;
+      a.dbg            = dbg;
+      ha[k]            = a;
+      hf[k]            = nblk;
+      nblk += (nof_cb[g] + cpw - 1) / cpw;
+      lds = std::max(lds, tdec_lds_bytes(c->nsb, a.xyw, a.M));
+    }
+    if (hipMemcpyAsync(m.d_stage, m.h_stage, need, hipMemcpyHostToDevice, st) != hipSuccess) {
+      return SRSRAN_ERROR;
+    }
+    hipEventRecord(m.copied, st);
+    m.used = true;
+    if (tdec_multi_launch(cls_nsb[ci], reinterpret_cast<const TdecArgs*>(m.d_stage),
+                          reinterpret_cast<const uint32_t*>(m.d_stage + abyte), (int)n, nblk, lds, st) != hipSuccess) {
+      ret = SRSRAN_ERROR;
+    }
   }
   for (int i = 0; i < kPoolStreams; i++) {
     hipEventRecord(p->done[i], p->s[i]);

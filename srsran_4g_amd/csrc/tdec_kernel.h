@@ -52,6 +52,11 @@ static constexpr uint32_t LTE_CRC24A = 0x1864CFB;  // phy_common.h:72
 static constexpr uint32_t LTE_CRC24B = 0x1800063;  // phy_common.h:73
 
 hipError_t tdec_launch(int nsb, const TdecArgs& a, hipStream_t stream);
+// ngroups descriptors of one decoder class (device array) in one launch; d_first[g] = first
+// workgroup of group g (ascending); lds = the largest tdec_lds_bytes of the groups
+hipError_t tdec_multi_launch(int nsb, const TdecArgs* d_groups, const uint32_t* d_first, int ngroups,
+                             uint32_t nblocks, size_t lds, hipStream_t stream);
+int        tdec_cpw(int nsb);  // code blocks per workgroup
 size_t     tdec_lds_bytes(int nsb, int xyw, int M);
 // x^(8m) mod poly for m = 0..nm-1 (host helper for the CRC combine tables)
 void crc24_xpow_table(uint32_t poly, uint32_t* out, int nm);

@@ -453,7 +453,7 @@ __device__ __forceinline__ uint32_t pack2(short lo, short hi)
 }
 
 template <int NSB, bool ES>
-__global__ __launch_bounds__(128, 2) void tdec_kernel(TdecArgs a)
+__device__ __forceinline__ void tdec_body(const TdecArgs& a, int bid)
 {
   using Gm                = Geo<NSB>;
   constexpr bool SAT      = Gm::SAT;
@@ -474,7 +474,7 @@ __global__ __launch_bounds__(128, 2) void tdec_kernel(TdecArgs a)
   const int Ls   = a.Ls;
   const int XYW  = a.xyw;
   const int M    = a.M;
-  const int cb   = blockIdx.x * Gm::CPW + cw;  // launch index
+  const int cb   = bid * Gm::CPW + cw;  // launch index
   const bool live = cb < (int)a.ncb;
   const int cbl  = live ? cb : (int)a.ncb - 1;
   // DL-SCH mode: blocks whose CRC already passed are not decoded; padding blocks
@@ -749,6 +749,57 @@ __global__ __launch_bounds__(128, 2) void tdec_kernel(TdecArgs a)
     }
   }
 }
+
+template <int NSB, bool ES>
+__global__ __launch_bounds__(128, 2) void tdec_kernel(TdecArgs a)
+{
+  tdec_body<NSB, ES>(a, blockIdx.x);
+}
+
+// Several code-block sizes of one decoder class in one launch: workgroup b belongs to the group
+// g with first[g] <= b < first[g + 1] (descriptors in device memory, read with scalar loads).
+template <int NSB>
+__global__ __launch_bounds__(128, 2) void tdec_multi_kernel(const TdecArgs* __restrict__ groups,
+                                                            const uint32_t* __restrict__ first, int ngroups)
+{
+  const uint32_t b  = blockIdx.x;
+  int            lo = 0, hi = ngroups - 1;  // last g with first[g] <= b
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (first[mid] <= b) {
+      lo = mid;
+    } else {
+      hi = mid - 1;
+    }
+  }
+  const TdecArgs a = groups[lo];
+  tdec_body<NSB, false>(a, (int)(b - first[lo]));
+}
+
+hipError_t tdec_multi_launch(int nsb, const TdecArgs* d_groups, const uint32_t* d_first, int ngroups,
+                             uint32_t nblocks, size_t lds, hipStream_t stream)
+{
+  StageScope timing_scope(ST_TDEC, stream);
+  if (ngroups == 0 || nblocks == 0) {
+    return hipSuccess;
+  }
+  switch (nsb) {
+    case 16:
+      hipLaunchKernelGGL(tdec_multi_kernel<16>, dim3(nblocks), dim3(128), lds, stream, d_groups, d_first, ngroups);
+      break;
+    case 8:
+      hipLaunchKernelGGL(tdec_multi_kernel<8>, dim3(nblocks), dim3(128), lds, stream, d_groups, d_first, ngroups);
+      break;
+    case 1:
+      hipLaunchKernelGGL(tdec_multi_kernel<1>, dim3(nblocks), dim3(128), lds, stream, d_groups, d_first, ngroups);
+      break;
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+int tdec_cpw(int nsb) { return 64 / (4 * nsb); }
 
 template <int NSB>
 static hipError_t launch(const TdecArgs& a, hipStream_t stream)

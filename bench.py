@@ -7,7 +7,9 @@ A "step" is one pass of the hot path over one batch of synthetic input:
   workload "k6144" (BASELINE configs[0] shape on the GPU): 1024 x 6144-bit blocks;
   workload "dlsch": srsran_dlsch_decode of C3 transport blocks (rate dematch + turbo + CRC);
   workload "pdsch" (BASELINE configs[2], C3): the whole UE DL chain from time-domain samples --
-      OFDM, CRS channel estimation, MMSE predecoding, demap/descramble/CSI, DL-SCH decode.
+      OFDM, CRS channel estimation, MMSE predecoding, demap/descramble/CSI, DL-SCH decode;
+  workload "ldpc" (BASELINE configs[4]): NR LDPC decode (srsran_ldpc_decoder, 8-bit layered
+      min-sum, AVX2 arithmetic) of a batch of BG1 / Z=384 codewords, 10 iterations.
 Inputs come from the synthetic eNB transmitter (synth/, not the oracle) and are resident in
 HBM before the timed region; every step decodes the full batch (no caching).
 
@@ -86,7 +88,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--workload", choices=["all188", "k6144", "dlsch", "pdsch"], default="all188")
+    p.add_argument("--workload", choices=["all188", "k6144", "dlsch", "pdsch", "ldpc"], default="all188")
     p.add_argument("--snr", type=float, default=30.0, help="pdsch: AWGN SNR (dB) of the synthetic subframes")
     p.add_argument("--subframes", type=int, default=78,
                    help="dlsch / pdsch: subframes (2 TBs each) per step; 78 x 26 CBs = two full turbo-decoder rounds")
@@ -95,6 +97,11 @@ def parse():
     p.add_argument("--iters", type=int, default=8, help="half-iterations (srsran nof_iterations)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (0 = skip)")
     p.add_argument("--pool", type=int, default=8, help="distinct AWGN code blocks per size")
+    p.add_argument("--bg", type=int, default=1, choices=[1, 2], help="ldpc: base graph")
+    p.add_argument("--ls", type=int, default=384, help="ldpc: lifting size")
+    p.add_argument("--codewords", type=int, default=4096, help="ldpc: codewords per step")
+    p.add_argument("--ldpc-iters", type=int, default=10, help="ldpc: iterations (srsran max_nof_iter)")
+    p.add_argument("--ldpc-snr", type=float, default=1.5, help="ldpc: BPSK Es/N0 (dB) of the synthetic codewords")
     return p.parse_args()
 
 
@@ -452,6 +459,115 @@ def pdsch_cpu_baseline(pool, args):
                       if ref is not None else f"{n} C3 subframes, {dt:.1f} s on 1 thread (oracle C port + numpy FFT)"}
 
 
+def run_ldpc(args, torch, dist, world, rank, device):
+    """NR LDPC decode (BASELINE configs[4]): per step `codewords` BG/Z codewords (int8 LLRs of
+    noisy BPSK codewords from synth/ldpc_tx.py), `ldpc-iters` iterations, no early stop (the
+    reference test's decode_c), packed message bits out.  Value = decoded info bits / s."""
+    from synth import ldpc_tx
+    from srsran_4g_amd import ldpc as G
+
+    bg = args.bg - 1
+    M, N, K = G.BG_SHAPE[bg]
+    ls = args.ls
+    liftK, n = K * ls, (N - 2) * ls
+    rng = np.random.default_rng(shard(rank)["seed"])
+    pool = []
+    pcm = G.compact_pcm(bg, ls)
+    for _ in range(args.pool):
+        cw = ldpc_tx.encode(bg, ls, rng.integers(0, 2, liftK).astype(np.uint8), pcm)[2 * ls:]
+        pool.append(ldpc_tx.bpsk_awgn_int8(cw, rng, args.ldpc_snr))
+    ncw = args.codewords
+    host = np.stack([pool[i % args.pool] for i in range(ncw)])
+    d_in = torch.from_numpy(host).to(device)
+    d_out = torch.zeros((ncw, liftK // 8), dtype=torch.uint8, device=device)
+    dec = G.LdpcDecoder(bg, ls, G.DEC_C_AVX2, scaling=0.8, max_nof_iter=args.ldpc_iters)
+    stream = torch.cuda.current_stream(device)
+    sp = stream.cuda_stream
+
+    def step():
+        if dec.gpu_decode_batch(d_in.data_ptr(), n, ncw, d_out.data_ptr(), liftK // 8, packed=True, stream=sp) != 0:
+            raise RuntimeError("srsran_ldpc_decoder_gpu_decode_batch failed")
+
+    elapsed = timed_region(step, args.steps, args.warmup, world, dist, torch.cuda.synchronize, device)
+    value = world * ncw * liftK * args.steps / elapsed / 1e6
+    ms = []
+    for _ in range(max(1, min(args.steps, 3))):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        step()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        ms.append(e0.elapsed_time(e1))
+    avg_ms = float(np.mean(ms))
+    bytes_per_launch = ncw * (n + liftK // 8)  # int8 LLRs in + packed message out (SURVEY 8d style)
+    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
+    dom = f"ldpc_kernel<{bg}>"
+    # decode quality on the pool (the reference's ldpc_chain_test reports BER the same way)
+    out = d_out.cpu().numpy()
+    result = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "Mbps",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int8",
+        "data": f"synthetic: BPSK AWGN (Es/N0 {args.ldpc_snr} dB) LDPC codewords from synth/ldpc_tx.py, int8 LLRs, "
+                f"{args.pool} distinct codewords tiled to the batch, HBM-resident",
+        "config": {
+            "workload": f"ldpc BG{args.bg} Z={ls}: {ncw} codewords x {liftK} info bits, {args.ldpc_iters} iterations "
+                        "(no early stop), SRSRAN_LDPC_DECODER_C_AVX2 arithmetic, scaling 0.8, packed output",
+            "codewords_per_step_per_gpu": ncw,
+            "parallelism": f"cw-sharded x{world}",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": dom,
+            "achieved": round(achieved, 2),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5),
+            "traffic": pmc_traffic(args.workload, dom, ncw),
+            "avg_launch_ms": round(avg_ms, 4),
+            "algo_bytes_per_launch": int(bytes_per_launch),
+        },
+        "decoded_pool_bits_set": int(np.unpackbits(out[:1]).sum()),
+    }
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        from ldpc import RefLdpc, ref_available, OracleLdpc, DEC_C_AVX2
+        kind = "reference" if ref_available() else "port"
+        nd = 0
+        t0 = time.perf_counter()
+        pool2d = np.stack(pool)
+        if kind == "reference":
+            ref = RefLdpc()
+            while time.perf_counter() - t0 < args.cpu_seconds:
+                ref.decode_many(DEC_C_AVX2, bg, ls, pool2d, scaling=0.8, max_iter=args.ldpc_iters)
+                nd += len(pool)
+        else:
+            ora = OracleLdpc()
+            while time.perf_counter() - t0 < args.cpu_seconds:
+                ora.decode_c(bg, ls, pool[nd % args.pool], scaling=0.8, max_iter=args.ldpc_iters)
+                nd += 1
+        dt = time.perf_counter() - t0
+        result["cpu_baseline"] = {"value": round(nd * liftK / dt / 1e6, 3), "unit": "Mbps", "cores": 1, "kind": kind,
+                                  "sample": f"{nd} codewords (passes over the {args.pool}-codeword pool) through one "
+                                            f"srsran_ldpc_decoder_t (C_AVX2, {args.ldpc_iters} iterations), "
+                                            f"{dt:.1f} s on 1 thread"}
+    elif rank == 0:
+        result["cpu_baseline"] = None
+    dec.free()
+    if world > 1:
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+
+
 def main():
     args = parse()
     import torch
@@ -472,6 +588,8 @@ def main():
         return run_dlsch(args, torch, dist, world, rank, device)
     if args.workload == "pdsch":
         return run_pdsch(args, torch, dist, world, rank, device)
+    if args.workload == "ldpc":
+        return run_ldpc(args, torch, dist, world, rank, device)
 
     Ks = list(tdec.CB_SIZES) if args.workload == "all188" else [6144]
     rng = np.random.default_rng(shard(rank)["seed"])

@@ -101,6 +101,8 @@ class RefLdpc:
                                       ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
                                       ctypes.c_void_p]
         L.ref_ldpc_encode.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        L.ref_ldpc_decode_many.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_int,
+                                           ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p]
         L.create_compact_pcm.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_uint16]
 
     def pcm(self, bg, ls):
@@ -129,6 +131,16 @@ class RefLdpc:
                                    poly, order, _p(out))
         assert r > -100, "reference decoder init failed"
         return r, out
+
+
+    def decode_many(self, dtype, bg, ls, llrs2d, scaling=0.8, max_iter=10):
+        """Every row through one decoder object (CPU throughput sample); returns the messages."""
+        K, N, n = lift(bg, ls)
+        llrs2d = np.ascontiguousarray(llrs2d, np.int8)
+        out = np.zeros((llrs2d.shape[0], K), np.uint8)
+        assert self.L.ref_ldpc_decode_many(dtype, bg, ls, scaling, max_iter, _p(llrs2d), llrs2d.shape[1],
+                                           llrs2d.shape[0], _p(out)) == 0
+        return out
 
 
 def load_examples(path=EXAMPLES):

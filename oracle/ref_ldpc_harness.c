@@ -65,3 +65,25 @@ int ref_ldpc_encode(int bg, int ls, const uint8_t* msg, uint8_t* cw)
   srsran_ldpc_encoder_free(&q);
   return r;
 }
+
+/* n codewords (llr_stride bytes apart) through one decoder object, as a CPU throughput sample */
+int ref_ldpc_decode_many(int type, int bg, int ls, float scaling_fctr, int max_iter, const int8_t* llrs,
+                         uint32_t llr_stride, int n, uint8_t* messages)
+{
+  srsran_ldpc_decoder_args_t args = {};
+  args.type                       = (srsran_ldpc_decoder_type_t)type;
+  args.bg                         = (srsran_basegraph_t)bg;
+  args.ls                         = (uint16_t)ls;
+  args.scaling_fctr               = scaling_fctr;
+  args.max_nof_iter               = (uint32_t)max_iter;
+  srsran_ldpc_decoder_t q;
+  if (srsran_ldpc_decoder_init(&q, &args) != 0) {
+    return -100;
+  }
+  const uint32_t len = q.liftN - 2 * q.ls;
+  for (int i = 0; i < n; i++) {
+    srsran_ldpc_decoder_decode_c(&q, llrs + (size_t)i * llr_stride, messages + (size_t)i * q.liftK, len);
+  }
+  srsran_ldpc_decoder_free(&q);
+  return 0;
+}

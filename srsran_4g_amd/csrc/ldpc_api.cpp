@@ -1,0 +1,386 @@
+// srsran_4g_amd/csrc/ldpc_api.cpp -- C-ABI host side of the HIP NR LDPC decoder.
+//
+// Implements include/srsran_ldpc.h (the srsran_ldpc_decoder_* surface of
+// lib/include/srsran/phy/fec/ldpc/ldpc_decoder.h and create_compact_pcm of base_graph.h) over
+// ldpc_kernel.hip.  Host semantics follow ldpc_decoder.c:
+//   init (args check, geometry, compact PCM, default 10 iterations)   ldpc_decoder.c:552-648
+//   rate-matched length clamp -> number of layers                     ldpc_decoder.c:48-70
+//   return values (max_nof_iter / iterations until CRC / 0)           ldpc_decoder.c:72-95
+// There is no CPU fallback: without a HIP device init fails with SRSRAN_ERROR.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <vector>
+
+#include "../../include/srsran_ldpc.h"
+#include "ldpc_kernel.h"
+
+#include "ldpc_bg_tables.inc"
+
+using namespace srsran_amd;
+
+namespace {
+
+struct Graph {
+  int                   M, N, K, ne;
+  const unsigned short* rs;
+  const unsigned char*  col;
+  const unsigned short* V;  // this lifting size's set
+};
+
+// 38.212 Table 5.3.2-1: Z = a * 2^j, set index by a
+int ls_index(int ls)
+{
+  static const int A[8] = {2, 3, 5, 7, 9, 11, 13, 15};
+  if (ls < 2 || ls > MAX_LIFTSIZE) {
+    return -1;
+  }
+  for (int i = 0; i < 8; i++) {
+    int z = A[i];
+    while (z < ls) {
+      z *= 2;
+    }
+    if (z == ls) {
+      return i;
+    }
+  }
+  return -1;
+}
+
+bool graph(int bg, int ls, Graph& g)
+{
+  const int set = ls_index(ls);
+  if (set < 0 || (bg != BG1 && bg != BG2)) {
+    return false;
+  }
+  g.M   = bg == BG1 ? BG1M : BG2M;
+  g.N   = bg == BG1 ? BG1Nfull : BG2Nfull;
+  g.K   = g.N - g.M;
+  g.rs  = bg == BG1 ? LDPC_BG1_ROW_START : LDPC_BG2_ROW_START;
+  g.col = bg == BG1 ? LDPC_BG1_COL : LDPC_BG2_COL;
+  g.V   = bg == BG1 ? LDPC_BG1_V[set] : LDPC_BG2_V[set];
+  g.ne  = g.rs[g.M];
+  return true;
+}
+
+struct Ctx {
+  hipStream_t stream    = nullptr;
+  uint16_t*   d_sh      = nullptr;
+  int8_t*     d_in      = nullptr;  // single-codeword staging of the host-synchronous calls
+  uint8_t*    d_out     = nullptr;
+  uint8_t*    d_ret     = nullptr;
+  int         scale_mode = LDPC_SCALE_SIMD;
+  int         sf         = 0;
+  std::map<uint64_t, uint32_t*> xpow;  // (poly, order) -> x^n mod P, n = 0 .. liftK
+};
+
+// x^n mod P for n = 0 .. nmax (P with its x^order bit)
+std::vector<uint32_t> xpow_table(uint32_t poly, int order, int nmax)
+{
+  std::vector<uint32_t> t(nmax + 1);
+  uint32_t              v    = 1;
+  const uint32_t        mask = (1u << order) - 1u;
+  for (int n = 0; n <= nmax; n++) {
+    t[n] = v;
+    v    = (v & (1u << (order - 1))) ? ((v << 1) ^ poly) : (v << 1);
+    v &= mask;
+  }
+  return t;
+}
+
+void free_ctx(Ctx* c)
+{
+  if (!c) {
+    return;
+  }
+  for (auto& kv : c->xpow) {
+    hipFree(kv.second);
+  }
+  hipFree(c->d_sh);
+  hipFree(c->d_in);
+  hipFree(c->d_out);
+  hipFree(c->d_ret);
+  if (c->stream) {
+    hipStreamDestroy(c->stream);
+  }
+  delete c;
+}
+
+void free_dec(void* o)
+{
+  srsran_ldpc_decoder_t* q = static_cast<srsran_ldpc_decoder_t*>(o);
+  free_ctx(static_cast<Ctx*>(q->ptr));
+  free(q->pcm);
+  free(q->var_indices);
+}
+
+const uint32_t* xpow_for(srsran_ldpc_decoder_t* q, const srsran_crc_t* crc)
+{
+  Ctx*           c   = static_cast<Ctx*>(q->ptr);
+  const uint64_t key = ((uint64_t)(uint32_t)crc->polynom << 8) | (uint32_t)crc->order;
+  auto           it  = c->xpow.find(key);
+  if (it != c->xpow.end()) {
+    return it->second;
+  }
+  const auto t = xpow_table((uint32_t)crc->polynom, crc->order, q->liftK);
+  uint32_t*  d = nullptr;
+  if (hipMalloc(&d, t.size() * 4) != hipSuccess ||
+      hipMemcpy(d, t.data(), t.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+    hipFree(d);
+    return nullptr;
+  }
+  c->xpow[key] = d;
+  return d;
+}
+
+// ldpc_decoder.c:48-70: clamp the rate-matched length and derive the processed layers
+int layers_for(const srsran_ldpc_decoder_t* q, uint32_t len)
+{
+  if (len > (uint32_t)q->liftN - 2u * q->ls) {
+    len = q->liftN - 2u * q->ls;
+  }
+  if (len < (uint32_t)(q->bgK + 2) * q->ls) {
+    len = (uint32_t)(q->bgK + 2) * q->ls;
+  }
+  if (len % q->ls) {
+    len = (len / q->ls + 1) * q->ls;
+  }
+  return (int)(len / q->ls) - q->bgK + 2;
+}
+
+int launch(srsran_ldpc_decoder_t* q, const int8_t* d_llrs, uint32_t llr_stride, uint32_t nof_cw, uint32_t len,
+           const srsran_crc_t* crc, uint8_t* d_message, uint32_t message_stride, int packed, uint8_t* d_ret,
+           hipStream_t stream)
+{
+  Ctx* c = static_cast<Ctx*>(q->ptr);
+  if (!c || !d_llrs || !d_message) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  if (crc && (crc->order != 16 && crc->order != 24)) {
+    fprintf(stderr, "[srsran_4g_amd] LDPC: CRC order %d not supported\n", crc->order);
+    return SRSRAN_ERROR;
+  }
+  if (packed && (q->liftK % 8)) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  LdpcArgs a;
+  memset(&a, 0, sizeof(a));
+  a.in         = d_llrs;
+  a.in_stride  = llr_stride;
+  a.out        = d_message;
+  a.out_stride = message_stride;
+  a.out_packed = packed;
+  a.ret        = d_ret;
+  a.ncw        = nof_cw;
+  a.ls         = q->ls;
+  a.cw_per_wg  = ldpc_cw_per_wg(q->ls);
+  a.n_layers   = layers_for(q, len);
+  a.max_iter   = (int)q->max_nof_iter;
+  a.scale_mode = c->scale_mode;
+  a.sf         = c->sf;
+  a.sh         = c->d_sh;
+  if (crc) {
+    a.xpow = xpow_for(q, crc);
+    if (!a.xpow) {
+      return SRSRAN_ERROR;
+    }
+    a.crc_poly  = (uint32_t)crc->polynom;
+    a.crc_order = crc->order;
+  }
+  return ldpc_launch(q->bg == BG1 ? 0 : 1, a, stream) == hipSuccess ? SRSRAN_SUCCESS : SRSRAN_ERROR;
+}
+
+int decode_c_impl(void* o, const int8_t* llrs, uint8_t* message, uint32_t len, srsran_crc_t* crc)
+{
+  srsran_ldpc_decoder_t* q = static_cast<srsran_ldpc_decoder_t*>(o);
+  Ctx*                   c = static_cast<Ctx*>(q->ptr);
+  if (!c || !llrs || !message) {
+    return SRSRAN_ERROR;
+  }
+  const size_t n = (size_t)q->liftN - 2u * q->ls;
+  if (hipMemcpyAsync(c->d_in, llrs, n, hipMemcpyHostToDevice, c->stream) != hipSuccess) {
+    return SRSRAN_ERROR;
+  }
+  if (launch(q, c->d_in, (uint32_t)n, 1, len, crc, c->d_out, q->liftK, 0, c->d_ret, c->stream) != SRSRAN_SUCCESS) {
+    return SRSRAN_ERROR;
+  }
+  uint8_t ret = 0;
+  if (hipMemcpyAsync(message, c->d_out, q->liftK, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+      hipMemcpyAsync(&ret, c->d_ret, 1, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+      hipStreamSynchronize(c->stream) != hipSuccess) {
+    return SRSRAN_ERROR;
+  }
+  return (int)ret;
+}
+
+}  // namespace
+
+extern "C" {
+
+int create_compact_pcm(uint16_t* pcm, int8_t (*positions)[MAX_CNCT], srsran_basegraph_t bg, uint16_t ls)
+{
+  Graph g;
+  if (!pcm || !graph(bg, ls, g)) {
+    fprintf(stderr, "[srsran_4g_amd] Invalid lifting size %d\n", ls);
+    return SRSRAN_ERROR;
+  }
+  for (int i = 0; i < g.M * g.N; i++) {
+    pcm[i] = NO_CNCT;
+  }
+  for (int i = 0; i < g.M; i++) {
+    for (int e = g.rs[i]; e < g.rs[i + 1]; e++) {
+      pcm[i * g.N + g.col[e]] = (uint16_t)(g.V[e] % ls);
+    }
+    if (positions) {
+      for (int k = 0; k < MAX_CNCT; k++) {
+        const int e     = g.rs[i] + k;
+        positions[i][k] = e < g.rs[i + 1] ? (int8_t)g.col[e] : (int8_t)-1;
+      }
+    }
+  }
+  return SRSRAN_SUCCESS;
+}
+
+int srsran_ldpc_decoder_init(srsran_ldpc_decoder_t* q, const srsran_ldpc_decoder_args_t* args)
+{
+  if (!q || !args) {
+    return SRSRAN_ERROR;
+  }
+  memset(q, 0, sizeof(*q));
+  Graph g;
+  if (!graph(args->bg, args->ls, g)) {
+    fprintf(stderr, "[srsran_4g_amd] LDPC: invalid base graph %d / lifting size %d\n", (int)args->bg + 1, args->ls);
+    return SRSRAN_ERROR;
+  }
+  const float s = args->scaling_fctr;
+  if (!(s > 0.0f) || s > 1.0f) {  // ldpc_decoder.c:596-601
+    fprintf(stderr, "[srsran_4g_amd] LDPC: scaling factor must be in (0, 1]\n");
+    return SRSRAN_ERROR;
+  }
+  int scale_mode;
+  switch (args->type) {
+    case SRSRAN_LDPC_DECODER_C:
+      scale_mode = LDPC_SCALE_C;
+      break;
+    case SRSRAN_LDPC_DECODER_C_AVX2:
+    case SRSRAN_LDPC_DECODER_C_AVX512:
+      scale_mode = LDPC_SCALE_SIMD;
+      break;
+    default:
+      fprintf(stderr, "[srsran_4g_amd] LDPC decoder type %d not provided on the GPU (8-bit layered only)\n",
+              (int)args->type);
+      return SRSRAN_ERROR;
+  }
+  q->bg           = args->bg;
+  q->ls           = args->ls;
+  q->bgN          = (uint8_t)g.N;
+  q->bgM          = (uint8_t)g.M;
+  q->bgK          = (uint8_t)g.K;
+  q->liftK        = (uint16_t)(g.K * args->ls);
+  q->liftM        = (uint16_t)(g.M * args->ls);
+  q->liftN        = (uint16_t)(g.N * args->ls);
+  q->max_nof_iter = args->max_nof_iter == 0 ? 10 : args->max_nof_iter;
+  q->scaling_fctr = s;
+  q->pcm          = static_cast<uint16_t*>(malloc(sizeof(uint16_t) * g.M * g.N));
+  q->var_indices  = static_cast<int8_t(*)[MAX_CNCT]>(malloc((size_t)g.M * MAX_CNCT));
+  if (!q->pcm || !q->var_indices || create_compact_pcm(q->pcm, q->var_indices, q->bg, q->ls) != SRSRAN_SUCCESS) {
+    free(q->pcm);
+    free(q->var_indices);
+    memset(q, 0, sizeof(*q));
+    return SRSRAN_ERROR;
+  }
+  Ctx* c        = new Ctx;
+  c->scale_mode = scale_mode;
+  // ldpc_dec_c_avx2.c:148 / ldpc_dec_c.c:149 (float arithmetic as the reference)
+  c->sf = scale_mode == LDPC_SCALE_SIMD ? (int)(uint16_t)((s + 0.00001525879) * 65535) : (int)(s * 100);
+  std::vector<uint16_t> sh(g.ne);
+  for (int e = 0; e < g.ne; e++) {
+    sh[e] = (uint16_t)(g.V[e] % args->ls);
+  }
+  const size_t n = (size_t)q->liftN - 2u * q->ls;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipMalloc(&c->d_sh, sh.size() * 2) != hipSuccess || hipMalloc(&c->d_in, n) != hipSuccess ||
+      hipMalloc(&c->d_out, q->liftK) != hipSuccess || hipMalloc(&c->d_ret, 64) != hipSuccess ||
+      hipMemcpy(c->d_sh, sh.data(), sh.size() * 2, hipMemcpyHostToDevice) != hipSuccess) {
+    fprintf(stderr, "[srsran_4g_amd] LDPC: no HIP device / allocation failed\n");
+    (void)hipGetLastError();
+    free_ctx(c);
+    free(q->pcm);
+    free(q->var_indices);
+    memset(q, 0, sizeof(*q));
+    return SRSRAN_ERROR;
+  }
+  q->ptr      = c;
+  q->free     = free_dec;
+  q->decode_c = decode_c_impl;
+  return SRSRAN_SUCCESS;
+}
+
+void srsran_ldpc_decoder_free(srsran_ldpc_decoder_t* q)
+{
+  if (!q) {
+    return;
+  }
+  if (q->free) {
+    q->free(q);
+  }
+  memset(q, 0, sizeof(*q));
+}
+
+int srsran_ldpc_decoder_decode_f(srsran_ldpc_decoder_t* q, const float* llrs, uint8_t* message, uint32_t len)
+{
+  (void)q, (void)llrs, (void)message, (void)len;
+  fprintf(stderr, "[srsran_4g_amd] LDPC: float decoder not provided on the GPU\n");
+  return SRSRAN_ERROR;
+}
+
+int srsran_ldpc_decoder_decode_s(srsran_ldpc_decoder_t* q, const int16_t* llrs, uint8_t* message, uint32_t len)
+{
+  (void)q, (void)llrs, (void)message, (void)len;
+  fprintf(stderr, "[srsran_4g_amd] LDPC: 16-bit decoder not provided on the GPU\n");
+  return SRSRAN_ERROR;
+}
+
+int srsran_ldpc_decoder_decode_c(srsran_ldpc_decoder_t* q, const int8_t* llrs, uint8_t* message, uint32_t len)
+{
+  if (!q || !q->decode_c) {
+    return SRSRAN_ERROR;
+  }
+  return q->decode_c(q, llrs, message, len, nullptr);
+}
+
+int srsran_ldpc_decoder_decode_crc_c(srsran_ldpc_decoder_t* q,
+                                     const int8_t*          llrs,
+                                     uint8_t*               message,
+                                     uint32_t               len,
+                                     srsran_crc_t*          crc)
+{
+  if (!q || !q->decode_c) {
+    return SRSRAN_ERROR;
+  }
+  return q->decode_c(q, llrs, message, len, crc);
+}
+
+int srsran_ldpc_decoder_gpu_decode_batch(srsran_ldpc_decoder_t* q,
+                                         const int8_t*          d_llrs,
+                                         uint32_t               llr_stride,
+                                         uint32_t               nof_cw,
+                                         uint32_t               cdwd_rm_length,
+                                         const srsran_crc_t*    crc,
+                                         uint8_t*               d_message,
+                                         uint32_t               message_stride,
+                                         int                    packed,
+                                         uint8_t*               d_ret,
+                                         void*                  stream)
+{
+  if (!q || !q->ptr) {
+    return SRSRAN_ERROR;
+  }
+  return launch(q, d_llrs, llr_stride, nof_cw, cdwd_rm_length, crc, d_message, message_stride, packed, d_ret,
+                static_cast<hipStream_t>(stream));
+}
+
+}  // extern "C"

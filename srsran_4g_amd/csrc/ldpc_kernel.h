@@ -1,0 +1,41 @@
+// srsran_4g_amd/csrc/ldpc_kernel.h -- launch interface of the HIP NR LDPC decoder.
+#ifndef SRSRAN_AMD_LDPC_KERNEL_H
+#define SRSRAN_AMD_LDPC_KERNEL_H
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace srsran_amd {
+
+static constexpr int LDPC_MAX_EDGES = 316;  // BG1 (BG2: 197)
+static constexpr int LDPC_WG        = 384;  // threads per workgroup upper bound
+
+enum LdpcScale { LDPC_SCALE_C = 0, LDPC_SCALE_SIMD = 1 };
+
+// One batch of codewords of one (base graph, lifting size), all decoded alike.
+struct LdpcArgs {
+  const int8_t*   in;          // ncw x (liftN - 2 ls) LLRs, in_stride bytes apart (device)
+  uint32_t        in_stride;
+  uint8_t*        out;         // ncw x liftK bytes (0/1) or liftK/8 packed bytes (device)
+  uint32_t        out_stride;
+  int             out_packed;  // 1: MSB-first packed bits (liftK/8 bytes, liftK % 8 == 0)
+  uint8_t*        ret;         // optional per codeword: decode_crc_c's return (iterations; 0 = CRC failed)
+  uint32_t        ncw;
+  int             ls;
+  int             cw_per_wg;   // codewords per workgroup (ls threads each)
+  int             n_layers;    // layers processed (rate-matched length, ldpc_decoder.c:70)
+  int             max_iter;
+  int             scale_mode;  // LdpcScale
+  int             sf;          // scaling factor as the mode's integer (65535ths or 100ths)
+  const uint32_t* xpow;        // x^n mod P, n = 0 .. liftK (device), nullptr: no CRC early stop
+  uint32_t        crc_poly;    // with its x^order bit
+  int             crc_order;   // 16 or 24
+  const uint16_t* sh;          // V mod ls per edge of the base graph, edge order (device)
+};
+
+hipError_t ldpc_launch(int bg, const LdpcArgs& a, hipStream_t stream);
+int        ldpc_cw_per_wg(int ls);
+size_t     ldpc_lds_bytes(int bg, int ls);  // per workgroup
+
+}  // namespace srsran_amd
+#endif

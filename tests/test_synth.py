@@ -112,3 +112,20 @@ def test_make_llrs_matches_oracle_generator():
         b1, l1 = S.make_llrs(K, 4.0, np.random.default_rng(K), 3)
         b2, l2 = make_llrs(K, 4.0, np.random.default_rng(K), 3)
         assert np.array_equal(b1, b2) and np.array_equal(l1, l2)
+
+
+def test_ldpc_tx_matches_oracle_encoder():
+    """synth/ldpc_tx.py (bench / test inputs) encodes like the oracle (pinned on the golden examples)."""
+    from ldpc import LIFT_SIZES, OracleLdpc
+
+    from synth import ldpc_tx
+
+    ora = OracleLdpc()
+    rng = np.random.default_rng(9)
+    for bg in (0, 1):
+        for ls in LIFT_SIZES[::3] + [384]:
+            K = (22 if bg == 0 else 10) * ls
+            msgs = rng.integers(0, 2, (3, K)).astype(np.uint8)
+            got = ldpc_tx.encode(bg, ls, msgs)
+            for m, g in zip(msgs, got):
+                assert np.array_equal(g, ora.encode(bg, ls, m)), (bg, ls)

@@ -68,7 +68,7 @@ bool graph(int bg, int ls, Graph& g)
 
 struct Ctx {
   hipStream_t stream    = nullptr;
-  uint16_t*   d_sh      = nullptr;
+  uint32_t*   d_sh      = nullptr;
   int8_t*     d_in      = nullptr;  // single-codeword staging of the host-synchronous calls
   uint8_t*    d_out     = nullptr;
   uint8_t*    d_ret     = nullptr;
@@ -182,6 +182,7 @@ int launch(srsran_ldpc_decoder_t* q, const int8_t* d_llrs, uint32_t llr_stride, 
   a.scale_mode = c->scale_mode;
   a.sf         = c->sf;
   a.sh         = c->d_sh;
+  a.magic_ls   = (uint32_t)((0x100000000ull + q->ls - 1) / q->ls);
   if (crc) {
     a.xpow = xpow_for(q, crc);
     if (!a.xpow) {
@@ -296,15 +297,15 @@ int srsran_ldpc_decoder_init(srsran_ldpc_decoder_t* q, const srsran_ldpc_decoder
   c->scale_mode = scale_mode;
   // ldpc_dec_c_avx2.c:148 / ldpc_dec_c.c:149 (float arithmetic as the reference)
   c->sf = scale_mode == LDPC_SCALE_SIMD ? (int)(uint16_t)((s + 0.00001525879) * 65535) : (int)(s * 100);
-  std::vector<uint16_t> sh(g.ne);
+  std::vector<uint32_t> sh(g.ne);
   for (int e = 0; e < g.ne; e++) {
-    sh[e] = (uint16_t)(g.V[e] % args->ls);
+    sh[e] = (uint32_t)(g.V[e] % args->ls);
   }
   const size_t n = (size_t)q->liftN - 2u * q->ls;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipMalloc(&c->d_sh, sh.size() * 2) != hipSuccess || hipMalloc(&c->d_in, n) != hipSuccess ||
+      hipMalloc(&c->d_sh, sh.size() * 4) != hipSuccess || hipMalloc(&c->d_in, n) != hipSuccess ||
       hipMalloc(&c->d_out, q->liftK) != hipSuccess || hipMalloc(&c->d_ret, 64) != hipSuccess ||
-      hipMemcpy(c->d_sh, sh.data(), sh.size() * 2, hipMemcpyHostToDevice) != hipSuccess) {
+      hipMemcpy(c->d_sh, sh.data(), sh.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
     fprintf(stderr, "[srsran_4g_amd] LDPC: no HIP device / allocation failed\n");
     (void)hipGetLastError();
     free_ctx(c);

@@ -30,7 +30,8 @@ struct LdpcArgs {
   const uint32_t* xpow;        // x^n mod P, n = 0 .. liftK (device), nullptr: no CRC early stop
   uint32_t        crc_poly;    // with its x^order bit
   int             crc_order;   // 16 or 24
-  const uint16_t* sh;          // V mod ls per edge of the base graph, edge order (device)
+  const uint32_t* sh;          // V mod ls per edge of the base graph, edge order (device)
+  uint32_t        magic_ls;    // ceil(2^32 / ls): i / ls = umulhi(i, magic_ls) for i < 2^16
 };
 
 hipError_t ldpc_launch(int bg, const LdpcArgs& a, hipStream_t stream);

@@ -72,6 +72,7 @@ struct Ctx {
   int8_t*     d_in      = nullptr;  // single-codeword staging of the host-synchronous calls
   uint8_t*    d_out     = nullptr;
   uint8_t*    d_ret     = nullptr;
+  uint8_t*    d_lut     = nullptr;  // scale(m), m = 0..127
   int         scale_mode = LDPC_SCALE_SIMD;
   int         sf         = 0;
   std::map<uint64_t, uint32_t*> xpow;  // (poly, order) -> x^n mod P, n = 0 .. liftK
@@ -103,6 +104,7 @@ void free_ctx(Ctx* c)
   hipFree(c->d_in);
   hipFree(c->d_out);
   hipFree(c->d_ret);
+  hipFree(c->d_lut);
   if (c->stream) {
     hipStreamDestroy(c->stream);
   }
@@ -182,6 +184,7 @@ int launch(srsran_ldpc_decoder_t* q, const int8_t* d_llrs, uint32_t llr_stride, 
   a.scale_mode = c->scale_mode;
   a.sf         = c->sf;
   a.sh         = c->d_sh;
+  a.scale_lut  = c->d_lut;
   a.magic_ls   = (uint32_t)((0x100000000ull + q->ls - 1) / q->ls);
   if (crc) {
     a.xpow = xpow_for(q, crc);
@@ -301,8 +304,13 @@ int srsran_ldpc_decoder_init(srsran_ldpc_decoder_t* q, const srsran_ldpc_decoder
   for (int e = 0; e < g.ne; e++) {
     sh[e] = (uint32_t)(g.V[e] % args->ls);
   }
+  uint8_t lut[128];
+  for (int m = 0; m < 128; m++) {  // ldpc_dec_c.c:282 / _mm256_scalei_epi8 (ldpc_dec_c_avx2.c:520-531)
+    lut[m] = (uint8_t)(scale_mode == LDPC_SCALE_SIMD ? ((uint32_t)m * (uint32_t)c->sf) >> 16 : m * c->sf / 100);
+  }
   const size_t n = (size_t)q->liftN - 2u * q->ls;
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+  if (hipMalloc(&c->d_lut, 128) != hipSuccess || hipMemcpy(c->d_lut, lut, 128, hipMemcpyHostToDevice) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc(&c->d_sh, sh.size() * 4) != hipSuccess || hipMalloc(&c->d_in, n) != hipSuccess ||
       hipMalloc(&c->d_out, q->liftK) != hipSuccess || hipMalloc(&c->d_ret, 64) != hipSuccess ||
       hipMemcpy(c->d_sh, sh.data(), sh.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {

@@ -9,6 +9,7 @@ namespace srsran_amd {
 
 static constexpr int LDPC_MAX_EDGES = 316;  // BG1 (BG2: 197)
 static constexpr int LDPC_WG        = 384;  // threads per workgroup upper bound
+static constexpr int LDPC_LDS_HDR   = LDPC_MAX_EDGES * 4 + 128;  // shift table + scaling table
 
 enum LdpcScale { LDPC_SCALE_C = 0, LDPC_SCALE_SIMD = 1 };
 
@@ -27,6 +28,7 @@ struct LdpcArgs {
   int             max_iter;
   int             scale_mode;  // LdpcScale
   int             sf;          // scaling factor as the mode's integer (65535ths or 100ths)
+  const uint8_t*  scale_lut;   // scale(m), m = 0..127, in the decoder's arithmetic (device)
   const uint32_t* xpow;        // x^n mod P, n = 0 .. liftK (device), nullptr: no CRC early stop
   uint32_t        crc_poly;    // with its x^order bit
   int             crc_order;   // 16 or 24
@@ -36,6 +38,7 @@ struct LdpcArgs {
 
 hipError_t ldpc_launch(int bg, const LdpcArgs& a, hipStream_t stream);
 int        ldpc_cw_per_wg(int ls);
+int        ldpc_threads_per_cw(int ls);
 size_t     ldpc_lds_bytes(int bg, int ls);  // per workgroup
 
 }  // namespace srsran_amd

@@ -73,6 +73,18 @@ constexpr int words_before(int L)
   return w;
 }
 
+static constexpr int PK_ONE_WORD_MAX_DEG = 11;  // signs of both checks + 5-bit indices in one dword
+
+template <int BG>
+constexpr int words_before_pk(int L)
+{
+  int w = 0;
+  for (int l = 0; l < L; ++l) {
+    w += deg_of<BG>(l) > PK_ONE_WORD_MAX_DEG ? 3 : 2;
+  }
+  return w;
+}
+
 struct Lane {
   int8_t*         soft;  // this codeword's soft bits (LDS), column stride CS
   const uint32_t* sh;    // shift of every edge for this lifting size (LDS copy)
@@ -176,6 +188,168 @@ __device__ __forceinline__ void run_iteration(const Lane& ln, uint32_t (&st)[NW]
   (run_layer<BG, CS, Ls, NW>(ln, st), ...);
 }
 
+// ---------------------------------------------------------------------------------------
+// Packed path (even ls >= 18): one thread serves the two check nodes z and z + ls/2 of a layer
+// with packed 16-bit arithmetic (v_pk_*_i16), so each VALU instruction advances two checks.
+// Soft bits stay int8 in LDS; the pair is gathered with ds_read_i8 / ds_read_i8_d16_hi and
+// scattered with ds_write_b8 / ds_write_b8_d16_hi.  Per layer and thread the state is
+//   M  = bytes (s1a, s2a, s1b, s2b): scaled min1 / min2 of checks a (lo half) and b (hi half)
+//   S0 = c2v sign bits of a (bits 0..) | idx_a << 11 | signs of b << 16 | idx_b << 27
+//        (degree <= 11; degree 19 rows keep edges 16.. and the indices in a third word S1).
+// Input LLRs of -128 load as -127: the reference maps both to -127 in every use (v2c infinity,
+// sign of the message), so the two are indistinguishable.
+typedef short          v2s __attribute__((ext_vector_type(2)));
+typedef unsigned short v2u __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ v2s as_s(uint32_t u) { return __builtin_bit_cast(v2s, u); }
+__device__ __forceinline__ v2u as_u(uint32_t u) { return __builtin_bit_cast(v2u, u); }
+__device__ __forceinline__ uint32_t bits(v2s v) { return __builtin_bit_cast(uint32_t, v); }
+__device__ __forceinline__ uint32_t bits(v2u v) { return __builtin_bit_cast(uint32_t, v); }
+__device__ __forceinline__ v2s pmin(v2s a, v2s b) { return __builtin_elementwise_min(a, b); }
+__device__ __forceinline__ v2s pmax(v2s a, v2s b) { return __builtin_elementwise_max(a, b); }
+__device__ __forceinline__ v2s pclamp(v2s a, short lo, short hi) { return pmin(pmax(a, v2s{lo, lo}), v2s{hi, hi}); }
+// The 0/1 flags and the multiply-add selects below are written as VOP3P instructions: in plain
+// C the compiler turns them into per-half compares + v_cndmask + v_perm (three times the work).
+__device__ __forceinline__ uint32_t pk_min1(uint32_t a)  // min(a, 1) per unsigned half
+{
+  uint32_t r;
+  asm("v_pk_min_u16 %0, %1, 1 op_sel_hi:[1,0]" : "=v"(r) : "v"(a));
+  return r;
+}
+__device__ __forceinline__ uint32_t pk_subsat(uint32_t a, uint32_t b)  // max(a - b, 0) per unsigned half
+{
+  uint32_t r;
+  asm("v_pk_sub_u16 %0, %1, %2 clamp" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ v2s pk_mad(v2s a, v2s b, v2s c)  // a * b + c per half (low 16 bits)
+{
+  uint32_t r;
+  asm("v_pk_mad_u16 %0, %1, %2, %3" : "=v"(r) : "v"(bits(a)), "v"(bits(b)), "v"(bits(c)));
+  return as_s(r);
+}
+// 1 where a > b (unsigned halves), else 0
+__device__ __forceinline__ v2s pgt01(uint32_t a, uint32_t b) { return as_s(pk_min1(pk_subsat(a, b))); }
+// 1 where a != b, else 0
+__device__ __forceinline__ v2s pne01(uint32_t a, uint32_t b) { return as_s(pk_min1(a ^ b)); }
+
+struct LanePk {
+  int8_t*         soft;   // this codeword's soft bits (LDS), column stride CS
+  const uint32_t* sh;     // shifts (LDS)
+  const uint8_t*  scale;  // scale(m) for m = 0..127 (LDS)
+  int             z;      // first check of the pair
+  int             ls, h;
+  bool            busy;
+  int             n_layers;
+};
+
+template <int BG, int CS, int L, int NW>
+__device__ __forceinline__ void run_layer_pk(const LanePk& ln, uint32_t (&st)[NW])
+{
+  using T               = Topo<BG>;
+  constexpr int  e0     = T::rs[L];
+  constexpr int  deg    = deg_of<BG>(L);
+  constexpr int  w0     = words_before_pk<BG>(L);
+  constexpr bool two    = deg > PK_ONE_WORD_MAX_DEG;
+  if (L >= ln.n_layers) {
+    return;
+  }
+  __syncthreads();  // soft bits written by the previous layer
+  if (!ln.busy) {
+    return;
+  }
+  int zz = ln.z;
+  asm volatile("" : "+v"(zz));
+  const uint32_t* shp = ln.sh + e0;
+  const uint32_t  ls  = (uint32_t)ln.ls;
+  const uint32_t  h   = (uint32_t)ln.h;
+
+  const uint32_t M   = st[w0];
+  const uint32_t S0  = st[w0 + 1];
+  const uint32_t SI  = two ? st[w0 + 2] : S0;  // word holding the indices
+  const v2s      P1  = as_s(M & 0x00FF00FFu);
+  const v2s      P2  = as_s((M >> 8) & 0x00FF00FFu);
+  const v2s      D1  = P1 - P2;
+  const v2u      IDX = as_u(SI) >> (unsigned short)11;
+  const uint32_t c126 = 0x007E007Eu;
+
+  v2s      v2c[deg];
+  uint32_t pos[deg];
+  v2s      m1 = {127, 127}, m2 = {127, 127}, mi = {0, 0};
+  v2s      px = {0, 0};
+#pragma unroll
+  for (int k = 0; k < deg; ++k) {
+    const int      col = T::col[e0 + k];
+    const uint32_t p   = (uint32_t)zz + shp[k];
+    const uint32_t p1  = min(p, p - ls);         // (z + shift) mod ls
+    const uint32_t q   = p1 + h;
+    const uint32_t p2  = min(q, q - ls);         // (z + ls/2 + shift) mod ls
+    __builtin_assume(p1 < (uint32_t)CS);
+    __builtin_assume(p2 < (uint32_t)CS);
+    pos[k]             = p1 | (p2 << 16);
+    const int8_t* sc   = ln.soft + col * CS;
+    const v2s     x    = {(short)sc[p1], (short)sc[p2]};
+    // previous c2v: +-(k == idx ? min2 : min1)
+    const uint32_t Sw   = (k < 16) ? S0 : SI;
+    const int      kk   = k & 15;
+    const v2s      smk  = as_s(bits(as_u(Sw) << (unsigned short)(15 - kk))) >> (short)15;
+    const v2s      mag  = pk_mad(pne01(bits(IDX), (uint32_t)k * 0x10001u), D1, P2);
+    const v2s      xmc  = (x + smk) - (mag ^ smk);  // x - c
+    const v2s      vn   = pclamp(xmc, -63, 63);
+    const v2s      ax   = pmax(x, -x);
+    const v2s      big  = pgt01(bits(ax), c126);  // |x| == 127
+    const v2s      v    = pk_mad(big, x - vn, vn);
+    v2c[k]              = v;
+    const v2s av        = pmax(v, -v);
+    const v2s lt        = pgt01(bits(m1), bits(av));  // av < m1
+    mi                  = pk_mad(lt, v2s{(short)k, (short)k} - mi, mi);
+    m2                  = pmin(pmax(m1, av), m2);
+    m1                  = pmin(m1, av);
+    px                  = px ^ v;
+  }
+  // scaled magnitudes through the LDS table (both scaling arithmetics)
+  const v2s  S1   = {(short)ln.scale[bits(m1) & 0xFFFFu], (short)ln.scale[bits(m1) >> 16]};
+  const v2s  S2   = {(short)ln.scale[bits(m2) & 0xFFFFu], (short)ln.scale[bits(m2) >> 16]};
+  const v2s  D2   = S1 - S2;
+  const v2s  prod = px >> (short)15;
+  uint32_t   acc0 = 0, acc1 = 0;
+#pragma unroll
+  for (int k = 0; k < deg; ++k) {
+    const int      col = T::col[e0 + k];
+    const v2s      mag = pk_mad(pne01(bits(mi), (uint32_t)k * 0x10001u), D2, S2);
+    const v2s      sgn = (prod ^ v2c[k]) >> (short)15;
+    const v2s      c   = (mag ^ sgn) - sgn;
+    const uint32_t bk  = (1u << (k & 15)) | (1u << (16 + (k & 15)));
+    if (k < 16) {
+      acc0 |= bits(sgn) & bk;
+    } else {
+      acc1 |= bits(sgn) & bk;
+    }
+    const v2s t  = c + v2c[k];
+    const v2s b  = pclamp(t, -63, 63);
+    const v2s a2 = pclamp(t, -64, 64);
+    const v2s r  = pk_mad(a2 - b, v2s{64, 64}, b);  // beyond +-63 -> +-127
+    int8_t*   sc = ln.soft + col * CS;
+    const uint32_t pp = pos[k];
+    sc[pp & 0xFFFFu]  = (int8_t)r.x;
+    sc[pp >> 16]      = (int8_t)r.y;
+  }
+  st[w0] = bits(S1) | (bits(S2) << 8);
+  const uint32_t iw = bits(__builtin_bit_cast(v2u, mi) << (unsigned short)11);
+  if constexpr (two) {
+    st[w0 + 1] = acc0;
+    st[w0 + 2] = acc1 | iw;
+  } else {
+    st[w0 + 1] = acc0 | iw;
+  }
+}
+
+template <int BG, int CS, int NW, int... Ls>
+__device__ __forceinline__ void run_iteration_pk(const LanePk& ln, uint32_t (&st)[NW], std::integer_sequence<int, Ls...>)
+{
+  (run_layer_pk<BG, CS, Ls, NW>(ln, st), ...);
+}
+
 // a * b mod P (P of degree `order`, given with its x^order bit), Horner over b's bits
 __device__ __forceinline__ uint32_t mulmod(uint32_t a, uint32_t b, uint32_t poly, int order)
 {
@@ -203,8 +377,9 @@ __global__ __launch_bounds__(LDPC_WG) void ldpc_kernel(LdpcArgs a)
   const uint32_t cw    = blockIdx.x * (uint32_t)a.cw_per_wg + (uint32_t)cwl;
   const bool     live  = act && cw < a.ncw;
   uint32_t*      shl   = reinterpret_cast<uint32_t*>(smem);  // LDPC_MAX_EDGES shifts
-  int8_t*        soft  = smem + LDPC_MAX_EDGES * 4 + (act ? cwl : 0) * CW;
-  uint32_t*      red   = reinterpret_cast<uint32_t*>(smem + LDPC_MAX_EDGES * 4 + a.cw_per_wg * CW);  // CRC parts
+  int8_t*        soft  = smem + LDPC_LDS_HDR + (act ? cwl : 0) * CW;
+  uint32_t*      red   = reinterpret_cast<uint32_t*>(smem + LDPC_LDS_HDR + a.cw_per_wg * CW);  // CRC parts
+  uint32_t*      anyb  = red + a.cw_per_wg;  // "some codeword still decoding" flag
   for (int e = (int)threadIdx.x; e < Topo<BG>::rs[T::M]; e += (int)blockDim.x) {
     shl[e] = a.sh[e];
   }
@@ -242,7 +417,10 @@ __global__ __launch_bounds__(LDPC_WG) void ldpc_kernel(LdpcArgs a)
       if (z == 0 && act) {
         red[cwl] = 0u;
       }
-      __syncthreads();  // last layer's soft bits; red cleared
+      if (threadIdx.x == 0) {
+        *anyb = 0u;
+      }
+      __syncthreads();  // last layer's soft bits; red / anyb cleared
       if (ln.busy) {
         // bits [z K, z K + K) of the message, natural order i = c ls + p
         const int order = a.crc_order;
@@ -271,7 +449,11 @@ __global__ __launch_bounds__(LDPC_WG) void ldpc_kernel(LdpcArgs a)
         ln.busy = false;
         ret     = it + 1;
       }
-      if (__syncthreads_or(ln.busy) == 0) {
+      if (ln.busy) {
+        *anyb = 1u;  // (no __syncthreads_or: its LDS scratch would shift every soft-bit address)
+      }
+      __syncthreads();
+      if (*anyb == 0u) {
         break;
       }
     }
@@ -309,26 +491,166 @@ __global__ __launch_bounds__(LDPC_WG) void ldpc_kernel(LdpcArgs a)
   }
 }
 
+template <int BG, int CS>
+__global__ __launch_bounds__(LDPC_WG) void ldpc_kernel_pk(LdpcArgs a)
+{
+  using T          = Topo<BG>;
+  constexpr int NW = words_before_pk<BG>(T::M);
+  constexpr int CW = T::N * CS;  // LDS bytes per codeword
+  extern __shared__ __attribute__((aligned(16))) int8_t smem[];
+  const int      ls    = a.ls;
+  const int      h     = ls >> 1;
+  const int      liftK = T::K * ls;
+  const int      cwl   = CS >= 384 ? 0 : (int)threadIdx.x / h;
+  const int      z     = (int)threadIdx.x - cwl * h;
+  const bool     act   = cwl < a.cw_per_wg && z < h;
+  const uint32_t cw    = blockIdx.x * (uint32_t)a.cw_per_wg + (uint32_t)cwl;
+  const bool     live  = act && cw < a.ncw;
+  uint32_t*      shl   = reinterpret_cast<uint32_t*>(smem);                 // LDPC_MAX_EDGES shifts
+  uint8_t*       lut   = reinterpret_cast<uint8_t*>(smem + LDPC_MAX_EDGES * 4);  // 128-entry scaling table
+  int8_t*        soft  = smem + LDPC_LDS_HDR + (act ? cwl : 0) * CW;
+  uint32_t*      red   = reinterpret_cast<uint32_t*>(smem + LDPC_LDS_HDR + a.cw_per_wg * CW);  // CRC parts
+  uint32_t*      anyb  = red + a.cw_per_wg;  // "some codeword still decoding" flag
+  for (int e = (int)threadIdx.x; e < Topo<BG>::rs[T::M]; e += (int)blockDim.x) {
+    shl[e] = a.sh[e];
+  }
+  for (int m = (int)threadIdx.x; m < 128; m += (int)blockDim.x) {
+    lut[m] = a.scale_lut[m];
+  }
+
+  // ---- load (init_ldpc_dec_c), -128 -> -127 (see above) ----
+  if (live) {
+    const int8_t* in = a.in + (size_t)cw * a.in_stride + z;
+    soft[z]          = 0;
+    soft[z + h]      = 0;
+    soft[CS + z]     = 0;
+    soft[CS + z + h] = 0;
+#pragma unroll 4
+    for (int c = 2; c < T::N; ++c) {
+      soft[c * CS + z]     = (int8_t)max((int)in[(c - 2) * ls], -127);
+      soft[c * CS + z + h] = (int8_t)max((int)in[(c - 2) * ls + h], -127);
+    }
+  }
+
+  LanePk ln;
+  ln.soft     = soft;
+  ln.sh       = shl;
+  ln.scale    = lut;
+  ln.z        = z;
+  ln.ls       = ls;
+  ln.h        = h;
+  ln.busy     = live;
+  ln.n_layers = a.n_layers;
+
+  uint32_t st[NW];
+#pragma unroll
+  for (int i = 0; i < NW; ++i) {
+    st[i] = 0u;
+  }
+  int ret = a.xpow ? 0 : a.max_iter;
+  for (int it = 0; it < a.max_iter; ++it) {
+    run_iteration_pk<BG, CS, NW>(ln, st, std::make_integer_sequence<int, T::M>{});
+    if (a.xpow) {
+      if (z == 0 && act) {
+        red[cwl] = 0u;
+      }
+      if (threadIdx.x == 0) {
+        *anyb = 0u;
+      }
+      __syncthreads();  // last layer's soft bits; red / anyb cleared
+      if (ln.busy) {
+        // bits [2 z K, 2 z K + 2 K) of the message, natural order i = c ls + p
+        const int order = a.crc_order;
+        const int b0    = 2 * z * T::K;
+        int       c     = (int)__umulhi((uint32_t)b0, a.magic_ls);  // b0 / ls
+        int       p     = b0 - c * ls;
+        uint32_t  crc   = 0;
+#pragma unroll
+        for (int b = 0; b < 2 * T::K; ++b) {
+          const uint32_t bit = soft[c * CS + p] < 0 ? 1u : 0u;
+          const uint32_t fb  = ((crc >> (order - 1)) & 1u) ^ bit;
+          crc                = ((crc << 1) ^ (fb ? a.crc_poly : 0u)) & ((1u << order) - 1u);
+          ++p;
+          if (p == ls) {
+            p = 0;
+            ++c;
+          }
+        }
+        const uint32_t part = mulmod(crc, a.xpow[liftK - b0 - 2 * T::K], a.crc_poly, order) & ((1u << order) - 1u);
+        if (part) {
+          atomicXor(&red[cwl], part);
+        }
+      }
+      __syncthreads();
+      if (ln.busy && red[cwl] == 0u) {  // srsran_crc_match: stop with this iteration's message
+        ln.busy = false;
+        ret     = it + 1;
+      }
+      if (ln.busy) {
+        *anyb = 1u;  // (no __syncthreads_or: its LDS scratch would shift every soft-bit address)
+      }
+      __syncthreads();
+      if (*anyb == 0u) {
+        break;
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- message: bit i = soft[i] < 0 for i < liftK (extract_ldpc_message_c) ----
+  if (live) {
+    uint8_t* out = a.out + (size_t)cw * a.out_stride;
+    if (a.out_packed) {
+      for (int b = z; b < liftK / 8; b += h) {
+        const int i0   = 8 * b;
+        int       c    = (int)__umulhi((uint32_t)i0, a.magic_ls);
+        int       p    = i0 - c * ls;
+        uint32_t  byte = 0;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          byte |= (uint32_t)(soft[c * CS + p] < 0) << (7 - t);
+          ++p;
+          if (p == ls) {
+            p = 0;
+            ++c;
+          }
+        }
+        out[b] = (uint8_t)byte;
+      }
+    } else {
+      for (int c = 0; c < T::K; ++c) {
+        out[c * ls + z]     = soft[c * CS + z] < 0 ? 1 : 0;
+        out[c * ls + z + h] = soft[c * CS + z + h] < 0 ? 1 : 0;
+      }
+    }
+    if (a.ret && z == 0) {
+      a.ret[cw] = (uint8_t)ret;
+    }
+  }
+}
+
 static int col_stride(int ls)
 {
   return ls > 256 ? 384 : (ls > 128 ? 256 : (ls > 64 ? 128 : (ls > 32 ? 64 : (ls > 16 ? 32 : 16))));
 }
 
 #if LDPC_BG_ONLY == 0
+int ldpc_threads_per_cw(int ls) { return ls > 16 ? ls / 2 : ls; }  // packed path: two checks a thread
+
 int ldpc_cw_per_wg(int ls)
 {
   const int cs = col_stride(ls);
-  if (cs >= 256) {
+  if (cs >= 384) {
     return 1;
   }
   // up to 256 threads, and at most 64 KiB of LDS (BG1 geometry bounds both base graphs)
-  return max(1, min(256 / ls, 65536 / (68 * cs)));
+  return max(1, min(256 / ldpc_threads_per_cw(ls), 65536 / (68 * cs)));
 }
 
 size_t ldpc_lds_bytes(int bg, int ls)
 {
   const int n = (bg == 0 ? 68 : 52) * col_stride(ls);
-  return LDPC_MAX_EDGES * 4 + (size_t)ldpc_cw_per_wg(ls) * (n + 4) + 16;
+  return LDPC_LDS_HDR + (size_t)ldpc_cw_per_wg(ls) * (n + 4) + 16;
 }
 #endif
 
@@ -346,19 +668,19 @@ hipError_t ldpc_launch_bg<0>(const LdpcArgs& a, dim3 grid, dim3 block, size_t ld
   constexpr int BG = LDPC_BG_ONLY;
   switch (col_stride(a.ls)) {
     case 384:
-      hipLaunchKernelGGL((ldpc_kernel<BG, 384>), grid, block, lds, s, a);
+      hipLaunchKernelGGL((ldpc_kernel_pk<BG, 384>), grid, block, lds, s, a);
       break;
     case 256:
-      hipLaunchKernelGGL((ldpc_kernel<BG, 256>), grid, block, lds, s, a);
+      hipLaunchKernelGGL((ldpc_kernel_pk<BG, 256>), grid, block, lds, s, a);
       break;
     case 128:
-      hipLaunchKernelGGL((ldpc_kernel<BG, 128>), grid, block, lds, s, a);
+      hipLaunchKernelGGL((ldpc_kernel_pk<BG, 128>), grid, block, lds, s, a);
       break;
     case 64:
-      hipLaunchKernelGGL((ldpc_kernel<BG, 64>), grid, block, lds, s, a);
+      hipLaunchKernelGGL((ldpc_kernel_pk<BG, 64>), grid, block, lds, s, a);
       break;
     case 32:
-      hipLaunchKernelGGL((ldpc_kernel<BG, 32>), grid, block, lds, s, a);
+      hipLaunchKernelGGL((ldpc_kernel_pk<BG, 32>), grid, block, lds, s, a);
       break;
     default:
       hipLaunchKernelGGL((ldpc_kernel<BG, 16>), grid, block, lds, s, a);
@@ -374,7 +696,7 @@ hipError_t ldpc_launch(int bg, const LdpcArgs& a, hipStream_t stream)
     return hipSuccess;
   }
   const int    cpw     = a.cw_per_wg;
-  const int    threads = ((cpw * a.ls + 63) / 64) * 64;
+  const int    threads = ((cpw * ldpc_threads_per_cw(a.ls) + 63) / 64) * 64;
   const int    grid    = (int)((a.ncw + cpw - 1) / cpw);
   const size_t lds     = ldpc_lds_bytes(bg, a.ls);
   if (threads > LDPC_WG || cpw != ldpc_cw_per_wg(a.ls) || a.ls < 2 || a.ls > 384) {

@@ -233,8 +233,13 @@ __device__ __forceinline__ v2s pgt01(uint32_t a, uint32_t b) { return as_s(pk_mi
 // 1 where a != b, else 0
 __device__ __forceinline__ v2s pne01(uint32_t a, uint32_t b) { return as_s(pk_min1(a ^ b)); }
 
+// LDS pointers built from integer offsets: the dynamic LDS block starts at address 0 (the kernel
+// has no static LDS), and addressing it this way lets every column offset fold into the
+// instruction (a generic `smem` symbol would cost an extra v_add per address).
+typedef __attribute__((address_space(3))) int8_t lds_i8;
+
 struct LanePk {
-  int8_t*         soft;   // this codeword's soft bits (LDS), column stride CS
+  lds_i8*         soft;   // this codeword's soft bits (LDS), column stride CS
   const uint32_t* sh;     // shifts (LDS)
   const uint8_t*  scale;  // scale(m) for m = 0..127 (LDS)
   int             z;      // first check of the pair
@@ -273,10 +278,11 @@ __device__ __forceinline__ void run_layer_pk(const LanePk& ln, uint32_t (&st)[NW
   const v2u      IDX = as_u(SI) >> (unsigned short)11;
   const uint32_t c126 = 0x007E007Eu;
 
-  v2s      v2c[deg];
+  v2s      v2c[deg];  // first the gathered soft bits, then the v2c messages
   uint32_t pos[deg];
   v2s      m1 = {127, 127}, m2 = {127, 127}, mi = {0, 0};
   v2s      px = {0, 0};
+  // gather every edge's pair first: all LDS reads of the layer in flight together
 #pragma unroll
   for (int k = 0; k < deg; ++k) {
     const int      col = T::col[e0 + k];
@@ -287,8 +293,12 @@ __device__ __forceinline__ void run_layer_pk(const LanePk& ln, uint32_t (&st)[NW
     __builtin_assume(p1 < (uint32_t)CS);
     __builtin_assume(p2 < (uint32_t)CS);
     pos[k]             = p1 | (p2 << 16);
-    const int8_t* sc   = ln.soft + col * CS;
-    const v2s     x    = {(short)sc[p1], (short)sc[p2]};
+    const lds_i8* sc   = ln.soft + col * CS;
+    v2c[k]             = v2s{(short)sc[p1], (short)sc[p2]};
+  }
+#pragma unroll
+  for (int k = 0; k < deg; ++k) {
+    const v2s x = v2c[k];
     // previous c2v: +-(k == idx ? min2 : min1)
     const uint32_t Sw   = (k < 16) ? S0 : SI;
     const int      kk   = k & 15;
@@ -329,7 +339,7 @@ __device__ __forceinline__ void run_layer_pk(const LanePk& ln, uint32_t (&st)[NW
     const v2s b  = pclamp(t, -63, 63);
     const v2s a2 = pclamp(t, -64, 64);
     const v2s r  = pk_mad(a2 - b, v2s{64, 64}, b);  // beyond +-63 -> +-127
-    int8_t*   sc = ln.soft + col * CS;
+    lds_i8*   sc = ln.soft + col * CS;
     const uint32_t pp = pos[k];
     sc[pp & 0xFFFFu]  = (int8_t)r.x;
     sc[pp >> 16]      = (int8_t)r.y;
@@ -533,7 +543,7 @@ __global__ __launch_bounds__(LDPC_WG) void ldpc_kernel_pk(LdpcArgs a)
   }
 
   LanePk ln;
-  ln.soft     = soft;
+  ln.soft     = (lds_i8*)(uintptr_t)(uint32_t)(LDPC_LDS_HDR + (act ? cwl : 0) * CW);
   ln.sh       = shl;
   ln.scale    = lut;
   ln.z        = z;

@@ -502,7 +502,8 @@ def run_ldpc(args, torch, dist, world, rank, device):
     avg_ms = float(np.mean(ms))
     bytes_per_launch = ncw * (n + liftK // 8)  # int8 LLRs in + packed message out (SURVEY 8d style)
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
-    dom = f"ldpc_kernel<{bg}>"
+    cs = 384 if ls > 256 else 256 if ls > 128 else 128 if ls > 64 else 64 if ls > 32 else 32 if ls > 16 else 16
+    dom = f"ldpc_kernel_pk<{bg}, {cs}>" if ls > 16 else f"ldpc_kernel<{bg}, {cs}>"  # ldpc_kernel.hip dispatch
     # decode quality on the pool (the reference's ldpc_chain_test reports BER the same way)
     out = d_out.cpu().numpy()
     result = {

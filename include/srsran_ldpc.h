@@ -16,8 +16,9 @@
  *   SRSRAN_LDPC_DECODER_C_AVX2, SRSRAN_LDPC_DECODER_C_AVX512
  *                                                   ldpc_dec_c_avx2*.c / _avx512*.c
  *                                                   (scaling (m * (uint16)((s + 2^-16) 65535)) >> 16)
- * Not provided on the GPU (init returns SRSRAN_ERROR): the float (F) and 16-bit (S) decoders and the
- * flooded schedules (*_FLOOD), none of which srsRAN selects by default (sch_nr.c:290-300).
+ *   SRSRAN_LDPC_DECODER_S                           ldpc_dec_s.c   (16-bit LLRs, 15-bit messages, decode_s)
+ * Not provided on the GPU (init returns SRSRAN_ERROR): the float (F) decoder and the flooded
+ * schedules (*_FLOOD), neither of which srsRAN selects by default (sch_nr.c:290-300).
  *
  * Added: srsran_ldpc_decoder_gpu_decode_batch(), an asynchronous batch entry point over device
  * buffers on the caller's HIP stream.
@@ -133,6 +134,19 @@ int srsran_ldpc_decoder_gpu_decode_batch(srsran_ldpc_decoder_t* q,
                                          int                    packed,
                                          uint8_t*               d_ret,
                                          void*                  stream);
+
+/* Same for a SRSRAN_LDPC_DECODER_S decoder: int16 LLRs, llr_stride in int16 elements. */
+int srsran_ldpc_decoder_gpu_decode_batch_s(srsran_ldpc_decoder_t* q,
+                                           const int16_t*         d_llrs,
+                                           uint32_t               llr_stride,
+                                           uint32_t               nof_cw,
+                                           uint32_t               cdwd_rm_length,
+                                           const srsran_crc_t*    crc,
+                                           uint8_t*               d_message,
+                                           uint32_t               message_stride,
+                                           int                    packed,
+                                           uint8_t*               d_ret,
+                                           void*                  stream);
 
 #ifdef __cplusplus
 }

@@ -73,6 +73,7 @@ struct Ctx {
   uint8_t*    d_out     = nullptr;
   uint8_t*    d_ret     = nullptr;
   uint8_t*    d_lut     = nullptr;  // scale(m), m = 0..127
+  int         bits       = 8;  // LLR / message width: 8 (C, C_AVX2, C_AVX512) or 16 (S)
   int         scale_mode = LDPC_SCALE_SIMD;
   int         sf         = 0;
   std::map<uint64_t, uint32_t*> xpow;  // (poly, order) -> x^n mod P, n = 0 .. liftK
@@ -153,13 +154,18 @@ int layers_for(const srsran_ldpc_decoder_t* q, uint32_t len)
   return (int)(len / q->ls) - q->bgK + 2;
 }
 
-int launch(srsran_ldpc_decoder_t* q, const int8_t* d_llrs, uint32_t llr_stride, uint32_t nof_cw, uint32_t len,
-           const srsran_crc_t* crc, uint8_t* d_message, uint32_t message_stride, int packed, uint8_t* d_ret,
-           hipStream_t stream)
+// llr_stride in bytes; bits = width of the caller's LLRs (must match the decoder type)
+int launch(srsran_ldpc_decoder_t* q, const void* d_llrs, int bits, uint32_t llr_stride, uint32_t nof_cw,
+           uint32_t len, const srsran_crc_t* crc, uint8_t* d_message, uint32_t message_stride, int packed,
+           uint8_t* d_ret, hipStream_t stream)
 {
   Ctx* c = static_cast<Ctx*>(q->ptr);
   if (!c || !d_llrs || !d_message) {
     return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  if (bits != c->bits) {
+    fprintf(stderr, "[srsran_4g_amd] LDPC: %d-bit LLRs given to a %d-bit decoder\n", bits, c->bits);
+    return SRSRAN_ERROR;
   }
   if (crc && (crc->order != 16 && crc->order != 24)) {
     fprintf(stderr, "[srsran_4g_amd] LDPC: CRC order %d not supported\n", crc->order);
@@ -171,6 +177,7 @@ int launch(srsran_ldpc_decoder_t* q, const int8_t* d_llrs, uint32_t llr_stride, 
   LdpcArgs a;
   memset(&a, 0, sizeof(a));
   a.in         = d_llrs;
+  a.llr_bits   = bits;
   a.in_stride  = llr_stride;
   a.out        = d_message;
   a.out_stride = message_stride;
@@ -178,7 +185,7 @@ int launch(srsran_ldpc_decoder_t* q, const int8_t* d_llrs, uint32_t llr_stride, 
   a.ret        = d_ret;
   a.ncw        = nof_cw;
   a.ls         = q->ls;
-  a.cw_per_wg  = ldpc_cw_per_wg(q->ls);
+  a.cw_per_wg  = ldpc_cw_per_wg(q->ls, bits);
   a.n_layers   = layers_for(q, len);
   a.max_iter   = (int)q->max_nof_iter;
   a.scale_mode = c->scale_mode;
@@ -197,18 +204,19 @@ int launch(srsran_ldpc_decoder_t* q, const int8_t* d_llrs, uint32_t llr_stride, 
   return ldpc_launch(q->bg == BG1 ? 0 : 1, a, stream) == hipSuccess ? SRSRAN_SUCCESS : SRSRAN_ERROR;
 }
 
-int decode_c_impl(void* o, const int8_t* llrs, uint8_t* message, uint32_t len, srsran_crc_t* crc)
+int decode_impl(srsran_ldpc_decoder_t* q, const void* llrs, int bits, uint8_t* message, uint32_t len,
+                const srsran_crc_t* crc)
 {
-  srsran_ldpc_decoder_t* q = static_cast<srsran_ldpc_decoder_t*>(o);
-  Ctx*                   c = static_cast<Ctx*>(q->ptr);
+  Ctx* c = static_cast<Ctx*>(q->ptr);
   if (!c || !llrs || !message) {
     return SRSRAN_ERROR;
   }
-  const size_t n = (size_t)q->liftN - 2u * q->ls;
-  if (hipMemcpyAsync(c->d_in, llrs, n, hipMemcpyHostToDevice, c->stream) != hipSuccess) {
+  const size_t n = ((size_t)q->liftN - 2u * q->ls) * (size_t)(bits / 8);
+  if (bits != c->bits || hipMemcpyAsync(c->d_in, llrs, n, hipMemcpyHostToDevice, c->stream) != hipSuccess) {
     return SRSRAN_ERROR;
   }
-  if (launch(q, c->d_in, (uint32_t)n, 1, len, crc, c->d_out, q->liftK, 0, c->d_ret, c->stream) != SRSRAN_SUCCESS) {
+  if (launch(q, c->d_in, bits, (uint32_t)n, 1, len, crc, c->d_out, q->liftK, 0, c->d_ret, c->stream) !=
+      SRSRAN_SUCCESS) {
     return SRSRAN_ERROR;
   }
   uint8_t ret = 0;
@@ -218,6 +226,16 @@ int decode_c_impl(void* o, const int8_t* llrs, uint8_t* message, uint32_t len, s
     return SRSRAN_ERROR;
   }
   return (int)ret;
+}
+
+int decode_c_impl(void* o, const int8_t* llrs, uint8_t* message, uint32_t len, srsran_crc_t* crc)
+{
+  return decode_impl(static_cast<srsran_ldpc_decoder_t*>(o), llrs, 8, message, len, crc);
+}
+
+int decode_s_impl(void* o, const int16_t* llrs, uint8_t* message, uint32_t len, srsran_crc_t* crc)
+{
+  return decode_impl(static_cast<srsran_ldpc_decoder_t*>(o), llrs, 16, message, len, crc);
 }
 
 }  // namespace
@@ -265,7 +283,12 @@ int srsran_ldpc_decoder_init(srsran_ldpc_decoder_t* q, const srsran_ldpc_decoder
     return SRSRAN_ERROR;
   }
   int scale_mode;
+  int bits = 8;
   switch (args->type) {
+    case SRSRAN_LDPC_DECODER_S:  // ldpc_dec_s.c: 16-bit LLRs, 15-bit messages, scaling m*s100/100
+      scale_mode = LDPC_SCALE_C;
+      bits       = 16;
+      break;
     case SRSRAN_LDPC_DECODER_C:
       scale_mode = LDPC_SCALE_C;
       break;
@@ -274,7 +297,7 @@ int srsran_ldpc_decoder_init(srsran_ldpc_decoder_t* q, const srsran_ldpc_decoder
       scale_mode = LDPC_SCALE_SIMD;
       break;
     default:
-      fprintf(stderr, "[srsran_4g_amd] LDPC decoder type %d not provided on the GPU (8-bit layered only)\n",
+      fprintf(stderr, "[srsran_4g_amd] LDPC decoder type %d not provided on the GPU (layered C/AVX2/AVX512/S only)\n",
               (int)args->type);
       return SRSRAN_ERROR;
   }
@@ -298,6 +321,7 @@ int srsran_ldpc_decoder_init(srsran_ldpc_decoder_t* q, const srsran_ldpc_decoder
   }
   Ctx* c        = new Ctx;
   c->scale_mode = scale_mode;
+  c->bits       = bits;
   // ldpc_dec_c_avx2.c:148 / ldpc_dec_c.c:149 (float arithmetic as the reference)
   c->sf = scale_mode == LDPC_SCALE_SIMD ? (int)(uint16_t)((s + 0.00001525879) * 65535) : (int)(s * 100);
   std::vector<uint32_t> sh(g.ne);
@@ -308,7 +332,7 @@ int srsran_ldpc_decoder_init(srsran_ldpc_decoder_t* q, const srsran_ldpc_decoder
   for (int m = 0; m < 128; m++) {  // ldpc_dec_c.c:282 / _mm256_scalei_epi8 (ldpc_dec_c_avx2.c:520-531)
     lut[m] = (uint8_t)(scale_mode == LDPC_SCALE_SIMD ? ((uint32_t)m * (uint32_t)c->sf) >> 16 : m * c->sf / 100);
   }
-  const size_t n = (size_t)q->liftN - 2u * q->ls;
+  const size_t n = ((size_t)q->liftN - 2u * q->ls) * (size_t)(bits / 8);
   if (hipMalloc(&c->d_lut, 128) != hipSuccess || hipMemcpy(c->d_lut, lut, 128, hipMemcpyHostToDevice) != hipSuccess ||
       hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc(&c->d_sh, sh.size() * 4) != hipSuccess || hipMalloc(&c->d_in, n) != hipSuccess ||
@@ -322,9 +346,13 @@ int srsran_ldpc_decoder_init(srsran_ldpc_decoder_t* q, const srsran_ldpc_decoder
     memset(q, 0, sizeof(*q));
     return SRSRAN_ERROR;
   }
-  q->ptr      = c;
-  q->free     = free_dec;
-  q->decode_c = decode_c_impl;
+  q->ptr  = c;
+  q->free = free_dec;
+  if (bits == 16) {
+    q->decode_s = decode_s_impl;
+  } else {
+    q->decode_c = decode_c_impl;
+  }
   return SRSRAN_SUCCESS;
 }
 
@@ -348,9 +376,11 @@ int srsran_ldpc_decoder_decode_f(srsran_ldpc_decoder_t* q, const float* llrs, ui
 
 int srsran_ldpc_decoder_decode_s(srsran_ldpc_decoder_t* q, const int16_t* llrs, uint8_t* message, uint32_t len)
 {
-  (void)q, (void)llrs, (void)message, (void)len;
-  fprintf(stderr, "[srsran_4g_amd] LDPC: 16-bit decoder not provided on the GPU\n");
-  return SRSRAN_ERROR;
+  if (!q || !q->decode_s) {  // the reference calls a NULL decode_s for 8-bit decoder types
+    fprintf(stderr, "[srsran_4g_amd] LDPC: decode_s needs a SRSRAN_LDPC_DECODER_S decoder\n");
+    return SRSRAN_ERROR;
+  }
+  return q->decode_s(q, llrs, message, len, nullptr);
 }
 
 int srsran_ldpc_decoder_decode_c(srsran_ldpc_decoder_t* q, const int8_t* llrs, uint8_t* message, uint32_t len)
@@ -388,8 +418,27 @@ int srsran_ldpc_decoder_gpu_decode_batch(srsran_ldpc_decoder_t* q,
   if (!q || !q->ptr) {
     return SRSRAN_ERROR;
   }
-  return launch(q, d_llrs, llr_stride, nof_cw, cdwd_rm_length, crc, d_message, message_stride, packed, d_ret,
+  return launch(q, d_llrs, 8, llr_stride, nof_cw, cdwd_rm_length, crc, d_message, message_stride, packed, d_ret,
                 static_cast<hipStream_t>(stream));
+}
+
+int srsran_ldpc_decoder_gpu_decode_batch_s(srsran_ldpc_decoder_t* q,
+                                           const int16_t*         d_llrs,
+                                           uint32_t               llr_stride,
+                                           uint32_t               nof_cw,
+                                           uint32_t               cdwd_rm_length,
+                                           const srsran_crc_t*    crc,
+                                           uint8_t*               d_message,
+                                           uint32_t               message_stride,
+                                           int                    packed,
+                                           uint8_t*               d_ret,
+                                           void*                  stream)
+{
+  if (!q || !q->ptr) {
+    return SRSRAN_ERROR;
+  }
+  return launch(q, d_llrs, 16, llr_stride * 2u, nof_cw, cdwd_rm_length, crc, d_message, message_stride, packed,
+                d_ret, static_cast<hipStream_t>(stream));
 }
 
 }  // extern "C"

@@ -15,7 +15,8 @@ enum LdpcScale { LDPC_SCALE_C = 0, LDPC_SCALE_SIMD = 1 };
 
 // One batch of codewords of one (base graph, lifting size), all decoded alike.
 struct LdpcArgs {
-  const int8_t*   in;          // ncw x (liftN - 2 ls) LLRs, in_stride bytes apart (device)
+  const void*     in;          // ncw x (liftN - 2 ls) LLRs (int8, or int16 if llr_bits == 16), in_stride bytes apart
+  int             llr_bits;    // 8 (types C, C_AVX2, C_AVX512) or 16 (type S)
   uint32_t        in_stride;
   uint8_t*        out;         // ncw x liftK bytes (0/1) or liftK/8 packed bytes (device)
   uint32_t        out_stride;
@@ -37,9 +38,9 @@ struct LdpcArgs {
 };
 
 hipError_t ldpc_launch(int bg, const LdpcArgs& a, hipStream_t stream);
-int        ldpc_cw_per_wg(int ls);
-int        ldpc_threads_per_cw(int ls);
-size_t     ldpc_lds_bytes(int bg, int ls);  // per workgroup
+int        ldpc_cw_per_wg(int ls, int bits);
+int        ldpc_threads_per_cw(int ls, int bits);
+size_t     ldpc_lds_bytes(int bg, int ls, int bits);  // per workgroup
 
 }  // namespace srsran_amd
 #endif

@@ -56,21 +56,10 @@ struct Topo<1> {
   static constexpr const unsigned char*  col = LDPC_BG2_COL;
 };
 
-static constexpr int ONE_WORD_MAX_DEG = 13;  // 7 + 7 + 5 + 13 sign bits
-
 template <int BG>
 constexpr int deg_of(int l)
 {
   return Topo<BG>::rs[l + 1] - Topo<BG>::rs[l];
-}
-template <int BG>
-constexpr int words_before(int L)
-{
-  int w = 0;
-  for (int l = 0; l < L; ++l) {
-    w += deg_of<BG>(l) > ONE_WORD_MAX_DEG ? 2 : 1;
-  }
-  return w;
 }
 
 static constexpr int PK_ONE_WORD_MAX_DEG = 11;  // signs of both checks + 5-bit indices in one dword
@@ -85,8 +74,36 @@ constexpr int words_before_pk(int L)
   return w;
 }
 
+// Arithmetic of the one-check-per-thread path: 8-bit (ldpc_dec_c.c / _avx2*.c) or 16-bit
+// (ldpc_dec_s.c: 15-bit messages, soft-bit infinity INT16_MAX) messages and their VGPR state.
+template <typename E>
+struct Ar;
+template <>
+struct Ar<int8_t> {
+  static constexpr int INF_MSG = 63, INF_SOFT = 127;  // infinity7, INT8_MAX (ldpc_dec_c.c:52, 292)
+  // state: s1 | s2 << 7 | idx << 14 | signs << 19 (one dword up to degree 13, else signs apart)
+  static constexpr int words(int deg) { return deg > 13 ? 2 : 1; }
+};
+template <>
+struct Ar<int16_t> {
+  static constexpr int INF_MSG = 16383, INF_SOFT = 32767;  // infinity15, INT16_MAX (ldpc_dec_s.c:52, 318)
+  // state: s1 | s2 << 16, idx | signs << 5
+  static constexpr int words(int) { return 2; }
+};
+
+template <int BG, typename E>
+constexpr int words_before_e(int L)
+{
+  int w = 0;
+  for (int l = 0; l < L; ++l) {
+    w += Ar<E>::words(deg_of<BG>(l));
+  }
+  return w;
+}
+
+template <typename E>
 struct Lane {
-  int8_t*         soft;  // this codeword's soft bits (LDS), column stride CS
+  E*              soft;  // this codeword's soft bits (LDS), column stride CS
   const uint32_t* sh;    // shift of every edge for this lifting size (LDS copy)
   int             z;     // lifted check index
   int             ls;
@@ -96,21 +113,24 @@ struct Lane {
   int             sf;
 };
 
-__device__ __forceinline__ int scale_mag(const Lane& ln, int m)
+template <typename E>
+__device__ __forceinline__ int scale_mag(const Lane<E>& ln, int m)
 {
   // _mm256_scalei_epi8: mulhi_epu16 of the (non-negative) byte by sf; ldpc_dec_c.c: m*sf/100
   return ln.scale_mode == LDPC_SCALE_SIMD ? (int)(((uint32_t)m * (uint32_t)ln.sf) >> 16) : m * ln.sf / 100;
 }
 
 // One layer (row L of the base graph) for this thread's check node.
-template <int BG, int CS, int L, int NW>
-__device__ __forceinline__ void run_layer(const Lane& ln, uint32_t (&st)[NW])
+template <int BG, int CS, typename E, int L, int NW>
+__device__ __forceinline__ void run_layer(const Lane<E>& ln, uint32_t (&st)[NW])
 {
-  using T                = Topo<BG>;
-  constexpr int  e0      = T::rs[L];
-  constexpr int  deg     = deg_of<BG>(L);
-  constexpr int  w0      = words_before<BG>(L);
-  constexpr bool two     = deg > ONE_WORD_MAX_DEG;
+  using T               = Topo<BG>;
+  using A               = Ar<E>;
+  constexpr int  e0     = T::rs[L];
+  constexpr int  deg    = deg_of<BG>(L);
+  constexpr int  w0     = words_before_e<BG, E>(L);
+  constexpr bool is8    = sizeof(E) == 1;
+  constexpr bool two    = A::words(deg) == 2;
   if (L >= ln.n_layers) {
     return;
   }
@@ -125,16 +145,25 @@ __device__ __forceinline__ void run_layer(const Lane& ln, uint32_t (&st)[NW])
   const uint32_t* shp = ln.sh + e0;  // LDS: broadcast reads with immediate offsets
   const int       ls  = ln.ls;
 
-  const uint32_t s0  = st[w0];
-  const uint32_t sg  = two ? st[w0 + 1] : (s0 >> 19);
-  const int      o1  = (int)(s0 & 127u);
-  const int      o2  = (int)((s0 >> 7) & 127u);
-  const int      oix = (int)((s0 >> 14) & 31u);
+  int      o1, o2, oix;
+  uint32_t sg;
+  if constexpr (is8) {
+    const uint32_t s0 = st[w0];
+    sg                = two ? st[w0 + 1] : (s0 >> 19);
+    o1                = (int)(s0 & 127u);
+    o2                = (int)((s0 >> 7) & 127u);
+    oix               = (int)((s0 >> 14) & 31u);
+  } else {
+    o1  = (int)(st[w0] & 0xFFFFu);
+    o2  = (int)(st[w0] >> 16);
+    oix = (int)(st[w0 + 1] & 31u);
+    sg  = st[w0 + 1] >> 5;
+  }
 
   int      v2c[deg];
   uint32_t pos[deg];
-  int      m1 = 127, m2 = 127, mi = 0;  // INT8_MAX start (ldpc_dec_c.c:223-228)
-  int      px = 0;                      // XOR of all v2c: its sign = product of signs
+  int      m1 = A::INF_SOFT, m2 = A::INF_SOFT, mi = 0;  // INT8_MAX / INT16_MAX start (ldpc_dec_c.c:223-228)
+  int      px = 0;                                      // XOR of all v2c: its sign = product of signs
 #pragma unroll
   for (int k = 0; k < deg; ++k) {
     const int      col = T::col[e0 + k];
@@ -146,10 +175,14 @@ __device__ __forceinline__ void run_layer(const Lane& ln, uint32_t (&st)[NW])
     const int mag = k == oix ? o2 : o1;
     const int sgn = -(int)((sg >> k) & 1u);
     const int c   = (mag ^ sgn) - sgn;
-    // inner_var_to_check: |x| >= 127 (infinity) propagates as +-127, else clip(x - c) to +-63
-    const int  vn  = min(max(x - c, -63), 63);
-    const bool big = (uint32_t)(x + 126) > 252u;
-    const int  v   = big ? (x | 1) : vn;
+    // inner_var_to_check: |x| >= INF_SOFT propagates as +-INF_SOFT, else clip(x - c) to +-INF_MSG
+    const int vn = min(max(x - c, -A::INF_MSG), A::INF_MSG);
+    int       v;
+    if constexpr (is8) {
+      v = (uint32_t)(x + 126) > 252u ? (x | 1) : vn;
+    } else {
+      v = (x >= A::INF_SOFT || x <= -A::INF_SOFT) ? min(max(x, -A::INF_SOFT), A::INF_SOFT) : vn;
+    }
     v2c[k]         = v;
     const int  av  = max(v, -v);
     const bool lt  = av < m1;                // strict: the first minimum keeps the index
@@ -169,23 +202,28 @@ __device__ __forceinline__ void run_layer(const Lane& ln, uint32_t (&st)[NW])
     const int sgn = (prod ^ v2c[k]) >> 31;  // sign of c2v_k = prod ^ sign(v2c_k)
     const int c   = (mag ^ sgn) - sgn;
     csg |= (uint32_t)(sgn & 1) << k;
-    const int t = c + v2c[k];  // update_ldpc_soft_bits: beyond +-63 -> +-127
-    const int r = (uint32_t)(t + 63) > 126u ? 127 * ((t >> 31) | 1) : t;
-    ln.soft[col * CS + pos[k]] = (int8_t)r;
+    const int t = c + v2c[k];  // update_ldpc_soft_bits: beyond +-INF_MSG -> +-INF_SOFT
+    const int r = (uint32_t)(t + A::INF_MSG) > (uint32_t)(2 * A::INF_MSG) ? A::INF_SOFT * ((t >> 31) | 1) : t;
+    ln.soft[col * CS + pos[k]] = (E)r;
   }
-  const uint32_t w = (uint32_t)s1 | ((uint32_t)s2 << 7) | ((uint32_t)mi << 14);
-  if constexpr (two) {
-    st[w0]     = w;
-    st[w0 + 1] = csg;
+  if constexpr (is8) {
+    const uint32_t w = (uint32_t)s1 | ((uint32_t)s2 << 7) | ((uint32_t)mi << 14);
+    if constexpr (two) {
+      st[w0]     = w;
+      st[w0 + 1] = csg;
+    } else {
+      st[w0] = w | (csg << 19);
+    }
   } else {
-    st[w0] = w | (csg << 19);
+    st[w0]     = (uint32_t)s1 | ((uint32_t)s2 << 16);
+    st[w0 + 1] = (uint32_t)mi | (csg << 5);
   }
 }
 
-template <int BG, int CS, int NW, int... Ls>
-__device__ __forceinline__ void run_iteration(const Lane& ln, uint32_t (&st)[NW], std::integer_sequence<int, Ls...>)
+template <int BG, int CS, typename E, int NW, int... Ls>
+__device__ __forceinline__ void run_iteration(const Lane<E>& ln, uint32_t (&st)[NW], std::integer_sequence<int, Ls...>)
 {
-  (run_layer<BG, CS, Ls, NW>(ln, st), ...);
+  (run_layer<BG, CS, E, Ls, NW>(ln, st), ...);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -372,22 +410,22 @@ __device__ __forceinline__ uint32_t mulmod(uint32_t a, uint32_t b, uint32_t poly
   return r;
 }
 
-template <int BG, int CS>
+template <int BG, int CS, typename E>
 __global__ __launch_bounds__(LDPC_WG) void ldpc_kernel(LdpcArgs a)
 {
   using T          = Topo<BG>;
-  constexpr int NW = words_before<BG>(T::M);
-  constexpr int CW = T::N * CS;  // LDS bytes per codeword
+  constexpr int NW = words_before_e<BG, E>(T::M);
+  constexpr int CW = T::N * CS * (int)sizeof(E);  // LDS bytes per codeword
   extern __shared__ __attribute__((aligned(16))) int8_t smem[];
   const int      ls    = a.ls;
   const int      liftK = T::K * ls;
-  const int      cwl   = CS >= 256 ? 0 : (int)threadIdx.x / ls;
+  const int      cwl   = CS >= 384 ? 0 : (int)threadIdx.x / ls;
   const int      z     = (int)threadIdx.x - cwl * ls;
   const bool     act   = cwl < a.cw_per_wg && z < ls;
   const uint32_t cw    = blockIdx.x * (uint32_t)a.cw_per_wg + (uint32_t)cwl;
   const bool     live  = act && cw < a.ncw;
   uint32_t*      shl   = reinterpret_cast<uint32_t*>(smem);  // LDPC_MAX_EDGES shifts
-  int8_t*        soft  = smem + LDPC_LDS_HDR + (act ? cwl : 0) * CW;
+  E*             soft  = reinterpret_cast<E*>(smem + LDPC_LDS_HDR + (act ? cwl : 0) * CW);
   uint32_t*      red   = reinterpret_cast<uint32_t*>(smem + LDPC_LDS_HDR + a.cw_per_wg * CW);  // CRC parts
   uint32_t*      anyb  = red + a.cw_per_wg;  // "some codeword still decoding" flag
   for (int e = (int)threadIdx.x; e < Topo<BG>::rs[T::M]; e += (int)blockDim.x) {
@@ -396,7 +434,7 @@ __global__ __launch_bounds__(LDPC_WG) void ldpc_kernel(LdpcArgs a)
 
   // ---- load: columns 0, 1 = 0 (punctured), column c >= 2 from llr[(c-2) ls] (init_ldpc_dec_c) ----
   if (live) {
-    const int8_t* in = a.in + (size_t)cw * a.in_stride + z;
+    const E* in = reinterpret_cast<const E*>(reinterpret_cast<const char*>(a.in) + (size_t)cw * a.in_stride) + z;
     soft[z]          = 0;
     soft[CS + z]     = 0;
 #pragma unroll 4
@@ -405,7 +443,7 @@ __global__ __launch_bounds__(LDPC_WG) void ldpc_kernel(LdpcArgs a)
     }
   }
 
-  Lane ln;
+  Lane<E> ln;
   ln.soft       = soft;
   ln.sh         = shl;
   ln.z          = z;
@@ -422,7 +460,7 @@ __global__ __launch_bounds__(LDPC_WG) void ldpc_kernel(LdpcArgs a)
   }
   int ret = a.xpow ? 0 : a.max_iter;
   for (int it = 0; it < a.max_iter; ++it) {
-    run_iteration<BG, CS, NW>(ln, st, std::make_integer_sequence<int, T::M>{});
+    run_iteration<BG, CS, E, NW>(ln, st, std::make_integer_sequence<int, T::M>{});
     if (a.xpow) {
       if (z == 0 && act) {
         red[cwl] = 0u;
@@ -530,7 +568,7 @@ __global__ __launch_bounds__(LDPC_WG) void ldpc_kernel_pk(LdpcArgs a)
 
   // ---- load (init_ldpc_dec_c), -128 -> -127 (see above) ----
   if (live) {
-    const int8_t* in = a.in + (size_t)cw * a.in_stride + z;
+    const int8_t* in = reinterpret_cast<const int8_t*>(a.in) + (size_t)cw * a.in_stride + z;
     soft[z]          = 0;
     soft[z + h]      = 0;
     soft[CS + z]     = 0;
@@ -639,28 +677,34 @@ __global__ __launch_bounds__(LDPC_WG) void ldpc_kernel_pk(LdpcArgs a)
   }
 }
 
-static int col_stride(int ls)
+// Column stride of the soft bits in LDS: 8-bit messages pick the smallest of 6 strides >= ls, 16-bit
+// messages (SRSRAN_LDPC_DECODER_S, 2 bytes a soft bit) one of 3 (fewer kernel instantiations).
+static int col_stride(int ls, int bits)
 {
+  if (bits == 16) {
+    return ls > 128 ? 384 : (ls > 32 ? 128 : 32);
+  }
   return ls > 256 ? 384 : (ls > 128 ? 256 : (ls > 64 ? 128 : (ls > 32 ? 64 : (ls > 16 ? 32 : 16))));
 }
 
 #if LDPC_BG_ONLY == 0
-int ldpc_threads_per_cw(int ls) { return ls > 16 ? ls / 2 : ls; }  // packed path: two checks a thread
+// the 8-bit packed path serves two check nodes a thread (even ls > 16)
+int ldpc_threads_per_cw(int ls, int bits) { return (bits == 8 && ls > 16) ? ls / 2 : ls; }
 
-int ldpc_cw_per_wg(int ls)
+int ldpc_cw_per_wg(int ls, int bits)
 {
-  const int cs = col_stride(ls);
+  const int cs = col_stride(ls, bits);
   if (cs >= 384) {
     return 1;
   }
   // up to 256 threads, and at most 64 KiB of LDS (BG1 geometry bounds both base graphs)
-  return max(1, min(256 / ldpc_threads_per_cw(ls), 65536 / (68 * cs)));
+  return max(1, min(256 / ldpc_threads_per_cw(ls, bits), 65536 / (68 * cs * (bits / 8))));
 }
 
-size_t ldpc_lds_bytes(int bg, int ls)
+size_t ldpc_lds_bytes(int bg, int ls, int bits)
 {
-  const int n = (bg == 0 ? 68 : 52) * col_stride(ls);
-  return LDPC_LDS_HDR + (size_t)ldpc_cw_per_wg(ls) * (n + 4) + 16;
+  const int n = (bg == 0 ? 68 : 52) * col_stride(ls, bits) * (bits / 8);
+  return LDPC_LDS_HDR + (size_t)ldpc_cw_per_wg(ls, bits) * (n + 4) + 16;
 }
 #endif
 
@@ -676,7 +720,21 @@ hipError_t ldpc_launch_bg<0>(const LdpcArgs& a, dim3 grid, dim3 block, size_t ld
 #endif
 {
   constexpr int BG = LDPC_BG_ONLY;
-  switch (col_stride(a.ls)) {
+  if (a.llr_bits == 16) {
+    switch (col_stride(a.ls, 16)) {
+      case 384:
+        hipLaunchKernelGGL((ldpc_kernel<BG, 384, int16_t>), grid, block, lds, s, a);
+        break;
+      case 128:
+        hipLaunchKernelGGL((ldpc_kernel<BG, 128, int16_t>), grid, block, lds, s, a);
+        break;
+      default:
+        hipLaunchKernelGGL((ldpc_kernel<BG, 32, int16_t>), grid, block, lds, s, a);
+        break;
+    }
+    return hipGetLastError();
+  }
+  switch (col_stride(a.ls, 8)) {
     case 384:
       hipLaunchKernelGGL((ldpc_kernel_pk<BG, 384>), grid, block, lds, s, a);
       break;
@@ -693,7 +751,7 @@ hipError_t ldpc_launch_bg<0>(const LdpcArgs& a, dim3 grid, dim3 block, size_t ld
       hipLaunchKernelGGL((ldpc_kernel_pk<BG, 32>), grid, block, lds, s, a);
       break;
     default:
-      hipLaunchKernelGGL((ldpc_kernel<BG, 16>), grid, block, lds, s, a);
+      hipLaunchKernelGGL((ldpc_kernel<BG, 16, int8_t>), grid, block, lds, s, a);
       break;
   }
   return hipGetLastError();
@@ -705,11 +763,13 @@ hipError_t ldpc_launch(int bg, const LdpcArgs& a, hipStream_t stream)
   if (a.ncw == 0) {
     return hipSuccess;
   }
+  const int    bits    = a.llr_bits == 16 ? 16 : 8;
   const int    cpw     = a.cw_per_wg;
-  const int    threads = ((cpw * ldpc_threads_per_cw(a.ls) + 63) / 64) * 64;
+  const int    threads = ((cpw * ldpc_threads_per_cw(a.ls, bits) + 63) / 64) * 64;
   const int    grid    = (int)((a.ncw + cpw - 1) / cpw);
-  const size_t lds     = ldpc_lds_bytes(bg, a.ls);
-  if (threads > LDPC_WG || cpw != ldpc_cw_per_wg(a.ls) || a.ls < 2 || a.ls > 384) {
+  const size_t lds     = ldpc_lds_bytes(bg, a.ls, bits);
+  if (threads > LDPC_WG || cpw != ldpc_cw_per_wg(a.ls, bits) || a.ls < 2 || a.ls > 384 ||
+      (bits == 16 && a.scale_mode != LDPC_SCALE_C)) {
     return hipErrorInvalidValue;
   }
   return bg == 0 ? ldpc_launch_bg<0>(a, dim3(grid), dim3(threads), lds, stream)

@@ -54,6 +54,7 @@ def _lib():
                                                            ctypes.c_uint32, ctypes.c_uint32,
                                                            ctypes.POINTER(srsran_crc_t), P, ctypes.c_uint32,
                                                            ctypes.c_int, P, P]
+        L.srsran_ldpc_decoder_gpu_decode_batch_s.argtypes = L.srsran_ldpc_decoder_gpu_decode_batch.argtypes
         L.create_compact_pcm.argtypes = [P, P, ctypes.c_int, ctypes.c_uint16]
         L.srsran_crc_init.argtypes = [ctypes.POINTER(srsran_crc_t), ctypes.c_uint32, ctypes.c_int]
         _sig = True
@@ -85,7 +86,7 @@ class LdpcDecoder:
         args = srsran_ldpc_decoder_args_t(dtype, bg, ls, scaling, max_nof_iter)
         if _lib().srsran_ldpc_decoder_init(ctypes.byref(self.q), ctypes.byref(args)) != 0:
             raise RuntimeError("srsran_ldpc_decoder_init failed (no HIP device, or unsupported configuration)")
-        self.bg, self.ls = bg, ls
+        self.bg, self.ls, self.dtype = bg, ls, dtype
         M, N, K = BG_SHAPE[bg]
         self.liftK, self.n_llr = K * ls, (N - 2) * ls
 
@@ -107,11 +108,22 @@ class LdpcDecoder:
                                                         ctypes.byref(c))
         return r, out
 
+    def decode_s(self, llrs, length=None):
+        """Host-synchronous 16-bit decode (SRSRAN_LDPC_DECODER_S): (return value, message bits)."""
+        llrs = np.ascontiguousarray(llrs, np.int16)
+        assert llrs.size == self.n_llr
+        out = np.zeros(self.liftK, np.uint8)
+        r = _lib().srsran_ldpc_decoder_decode_s(ctypes.byref(self.q), llrs.ctypes.data, out.ctypes.data,
+                                                self.n_llr if length is None else length)
+        return r, out
+
     def gpu_decode_batch(self, d_llrs, llr_stride, nof_cw, d_message, message_stride, length=None, crc=None,
                          packed=False, d_ret=None, stream=None):
         """Asynchronous batch over device pointers (ints); returns the C status."""
         c = make_crc(*crc) if crc is not None else None
         self._crc_keep = c
-        return _lib().srsran_ldpc_decoder_gpu_decode_batch(
+        fn = (_lib().srsran_ldpc_decoder_gpu_decode_batch_s if self.dtype == DEC_S
+              else _lib().srsran_ldpc_decoder_gpu_decode_batch)
+        return fn(
             ctypes.byref(self.q), d_llrs, llr_stride, nof_cw, self.n_llr if length is None else length,
             ctypes.byref(c) if c is not None else None, d_message, message_stride, int(packed), d_ret, stream)

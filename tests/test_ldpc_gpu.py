@@ -129,3 +129,38 @@ def test_compact_pcm_matches_oracle(ora):
             p, q = G.compact_pcm(bg, ls)
             p0, q0 = ora.pcm(bg, ls)
             assert np.array_equal(p, p0) and np.array_equal(q, q0)
+
+
+def test_16bit_decoder_vs_oracle(ora):
+    """SRSRAN_LDPC_DECODER_S (ldpc_dec_s.c): int16 LLRs, 15-bit messages, decode_s and the batch."""
+    import torch
+
+    rng = np.random.default_rng(16)
+    for bg in (0, 1):
+        for ls in LIFT_SIZES[::3] + [384]:
+            K, N, n = lift(bg, ls)
+            dec = G.LdpcDecoder(bg, ls, G.DEC_S, scaling=0.75, max_nof_iter=5)
+            full = ora.encode(bg, ls, rng.integers(0, 2, K).astype(np.uint8))[2 * ls:]
+            for snr, amp in ((0.5, 900.0), (2.0, 20000.0)):  # the second saturates (INT16 infinity)
+                llr = noisy_llrs(full, rng, snr_db=snr, amp=amp, dtype=np.int16, clip=32767)
+                llr[rng.integers(0, n, 8)] = -32768
+                L = int(rng.integers((K // ls + 2) * ls - ls // 2, n + 1)) if snr < 1 else n
+                got = dec.decode_s(llr, length=L)
+                want = ora.decode_s(bg, ls, llr, scaling=0.75, max_iter=5, length=L)
+                assert got[0] == want[0] and np.array_equal(got[1], want[1]), (bg, ls, snr)
+            assert dec.decode_c(np.zeros(n, np.int8))[0] == -1  # 8-bit call on a 16-bit decoder
+            dec.free()
+        # batch
+        ls, ncw = 208, 9
+        K, N, n = lift(bg, ls)
+        dec = G.LdpcDecoder(bg, ls, G.DEC_S, scaling=0.8, max_nof_iter=6)
+        llrs = np.stack([noisy_llrs(ora.encode(bg, ls, rng.integers(0, 2, K).astype(np.uint8))[2 * ls:], rng,
+                                    snr_db=1.0, amp=700.0, dtype=np.int16, clip=32767) for _ in range(ncw)])
+        d_in = torch.from_numpy(llrs).cuda()
+        d_out = torch.zeros((ncw, K), dtype=torch.uint8, device="cuda")
+        assert dec.gpu_decode_batch(d_in.data_ptr(), n, ncw, d_out.data_ptr(), K) == 0
+        torch.cuda.synchronize()
+        out = d_out.cpu().numpy()
+        for i in range(ncw):
+            assert np.array_equal(out[i], ora.decode_s(bg, ls, llrs[i], scaling=0.8, max_iter=6)[1]), i
+        dec.free()

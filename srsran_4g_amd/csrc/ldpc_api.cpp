@@ -16,7 +16,7 @@
 #include <vector>
 
 #include "../../include/srsran_ldpc.h"
-#include "ldpc_kernel.h"
+#include "ldpc_internal.h"
 
 #include "ldpc_bg_tables.inc"
 
@@ -239,6 +239,41 @@ int decode_s_impl(void* o, const int16_t* llrs, uint8_t* message, uint32_t len, 
 }
 
 }  // namespace
+
+namespace srsran_amd {
+
+int ldpc_layers_for(const srsran_ldpc_decoder_t* q, uint32_t len) { return layers_for(q, len); }
+
+std::vector<uint32_t> ldpc_xpow_table(uint32_t poly, int order, int nmax) { return xpow_table(poly, order, nmax); }
+
+int ldpc_launch_cws(srsran_ldpc_decoder_t* q, const LdpcCw* d_cws, uint32_t n, const uint32_t* const xpow3[3],
+                    hipStream_t stream)
+{
+  Ctx* c = static_cast<Ctx*>(q ? q->ptr : nullptr);
+  if (!c || c->bits != 8) {
+    return SRSRAN_ERROR;
+  }
+  LdpcArgs a;
+  memset(&a, 0, sizeof(a));
+  a.llr_bits   = 8;
+  a.ncw        = n;
+  a.ls         = q->ls;
+  a.cw_per_wg  = ldpc_cw_per_wg(q->ls, 8);
+  a.n_layers   = q->bgM;
+  a.max_iter   = (int)q->max_nof_iter;
+  a.scale_mode = c->scale_mode;
+  a.sf         = c->sf;
+  a.sh         = c->d_sh;
+  a.scale_lut  = c->d_lut;
+  a.magic_ls   = (uint32_t)((0x100000000ull + q->ls - 1) / q->ls);
+  a.cws        = d_cws;
+  for (int i = 0; i < 3; i++) {
+    a.xpow3[i] = xpow3[i];
+  }
+  return ldpc_launch(q->bg == BG1 ? 0 : 1, a, stream) == hipSuccess ? SRSRAN_SUCCESS : SRSRAN_ERROR;
+}
+
+}  // namespace srsran_amd
 
 extern "C" {
 

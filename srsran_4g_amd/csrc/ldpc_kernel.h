@@ -13,6 +13,18 @@ static constexpr int LDPC_LDS_HDR   = LDPC_MAX_EDGES * 4 + 128;  // shift table 
 
 enum LdpcScale { LDPC_SCALE_C = 0, LDPC_SCALE_SIMD = 1 };
 
+// One code block of an NR SCH transport block (CB mode, sch_nr.c:611-690): per-codeword input,
+// number of layers, CRC type, skip flag and outputs.
+struct LdpcCw {
+  const int8_t* in;        // rate de-matched LLRs (the soft buffer of the code block, device)
+  uint8_t*      data;      // packed message bits (cb_len of them) written when the CRC passes
+  uint8_t*      flag;      // cb_crc: set -> skipped (already decoded); set to 1 when the CRC passes
+  uint8_t*      iters;     // iterations used (ret == 0 ? max_iter : ret), 0 when skipped
+  uint16_t      n_layers;  // from the rate-matched length (ldpc_decoder.c:70)
+  uint16_t      cb_len;    // Kp - L_cb
+  uint32_t      crc;       // 0: CRC24B (C > 1), 1: CRC24A, 2: CRC16 (TB CRC of single-CB TBs)
+};
+
 // One batch of codewords of one (base graph, lifting size), all decoded alike.
 struct LdpcArgs {
   const void*     in;          // ncw x (liftN - 2 ls) LLRs (int8, or int16 if llr_bits == 16), in_stride bytes apart
@@ -34,6 +46,8 @@ struct LdpcArgs {
   uint32_t        crc_poly;    // with its x^order bit
   int             crc_order;   // 16 or 24
   const uint32_t* sh;          // V mod ls per edge of the base graph, edge order (device)
+  const LdpcCw*   cws;         // CB mode (nullptr: plain batch): per codeword descriptors
+  const uint32_t* xpow3[3];    // CB mode: x^n mod P tables for CRC24B, CRC24A, CRC16 (device)
   uint32_t        magic_ls;    // ceil(2^32 / ls): i / ls = umulhi(i, magic_ls) for i < 2^16
 };
 

@@ -108,7 +108,8 @@ struct Lane {
   int             z;     // lifted check index
   int             ls;
   bool            busy;  // decodes this layer (live codeword, CRC not yet matched)
-  int             n_layers;
+  int             n_layers;     // this codeword's layers
+  int             n_layers_wg;  // the workgroup's largest (barrier count)
   int             scale_mode;
   int             sf;
 };
@@ -131,11 +132,11 @@ __device__ __forceinline__ void run_layer(const Lane<E>& ln, uint32_t (&st)[NW])
   constexpr int  w0     = words_before_e<BG, E>(L);
   constexpr bool is8    = sizeof(E) == 1;
   constexpr bool two    = A::words(deg) == 2;
-  if (L >= ln.n_layers) {
+  if (L >= ln.n_layers_wg) {
     return;
   }
   __syncthreads();  // soft bits written by the previous layer
-  if (!ln.busy) {
+  if (!ln.busy || L >= ln.n_layers) {
     return;
   }
   // Opaque per-layer copy: without it LICM hoists every edge's address (316 VGPRs) out of the
@@ -283,7 +284,8 @@ struct LanePk {
   int             z;      // first check of the pair
   int             ls, h;
   bool            busy;
-  int             n_layers;
+  int             n_layers;     // this codeword's layers
+  int             n_layers_wg;  // the workgroup's largest (barrier count)
 };
 
 template <int BG, int CS, int L, int NW>
@@ -294,11 +296,11 @@ __device__ __forceinline__ void run_layer_pk(const LanePk& ln, uint32_t (&st)[NW
   constexpr int  deg    = deg_of<BG>(L);
   constexpr int  w0     = words_before_pk<BG>(L);
   constexpr bool two    = deg > PK_ONE_WORD_MAX_DEG;
-  if (L >= ln.n_layers) {
+  if (L >= ln.n_layers_wg) {
     return;
   }
   __syncthreads();  // soft bits written by the previous layer
-  if (!ln.busy) {
+  if (!ln.busy || L >= ln.n_layers) {
     return;
   }
   int zz = ln.z;
@@ -398,6 +400,94 @@ __device__ __forceinline__ void run_iteration_pk(const LanePk& ln, uint32_t (&st
   (run_layer_pk<BG, CS, Ls, NW>(ln, st), ...);
 }
 
+// Per-thread view of its codeword: plain batch (one configuration for all) or CB mode (LdpcCw).
+struct CwCtx {
+  const void*     in;        // this codeword's LLRs
+  bool            live;      // decodes (exists, not already decoded)
+  int             n_layers;  // this codeword's layers
+  const uint32_t* xpow;      // CRC early stop (nullptr: none)
+  uint32_t        poly;
+  int             order;
+};
+
+__device__ __forceinline__ CwCtx cw_ctx(const LdpcArgs& a, uint32_t cw, bool act, int elem_bytes)
+{
+  CwCtx c;
+  const bool exists = act && cw < a.ncw;
+  if (a.cws) {
+    const LdpcCw& d = a.cws[exists ? cw : 0];
+    c.in            = d.in;
+    c.live          = exists && *d.flag == 0;
+    c.n_layers      = d.n_layers;
+    c.xpow          = a.xpow3[d.crc];
+    c.poly          = d.crc == 0 ? 0x1800063u : (d.crc == 1 ? 0x1864CFBu : 0x11021u);  // phy_common.h:72-74
+    c.order         = d.crc == 2 ? 16 : 24;
+  } else {
+    c.in       = reinterpret_cast<const char*>(a.in) + (size_t)cw * a.in_stride;
+    c.live     = exists;
+    c.n_layers = a.n_layers;
+    c.xpow     = a.xpow;
+    c.poly     = a.crc_poly;
+    c.order    = a.crc_order;
+  }
+  (void)elem_bytes;
+  return c;
+}
+
+// Largest layer count of the workgroup's codewords (CB mode): every thread reaches every barrier
+// of the layers up to it.  `slot` is a dword of dynamic LDS.
+__device__ __forceinline__ int wg_layers(const LdpcArgs& a, const CwCtx& c, uint32_t* slot)
+{
+  if (!a.cws) {
+    return a.n_layers;
+  }
+  if (threadIdx.x == 0) {
+    *slot = 0u;
+  }
+  __syncthreads();
+  if (c.live) {
+    atomicMax(slot, (uint32_t)c.n_layers);
+  }
+  __syncthreads();
+  return (int)*slot;
+}
+
+// CB-mode outputs of one codeword (sch_nr.c:664-690): packed message on CRC success, cb_crc flag,
+// iterations; `bit(i)` = hard decision of message bit i.
+template <typename F>
+__device__ __forceinline__ void cb_finish(const LdpcArgs& a, uint32_t cw, bool exists, const CwCtx& c, int ret,
+                                          int t0, int nthreads, F&& bit)
+{
+  const LdpcCw& d = a.cws[cw];
+  if (!exists) {
+    return;
+  }
+  if (!c.live) {  // already decoded in an earlier transmission: untouched, no iterations
+    if (t0 == 0) {
+      *d.iters = 0;
+    }
+    return;
+  }
+  if (ret > 0) {  // srsran_bit_pack_vector(temp_cb, data[r], cb_len): whole bytes, then MSB-aligned rest
+    const int nb = (d.cb_len + 7) / 8;
+    for (int b = t0; b < nb; b += nthreads) {
+      uint32_t byte = 0;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const int i = 8 * b + t;
+        byte |= (uint32_t)(i < (int)d.cb_len ? bit(i) : 0) << (7 - t);
+      }
+      d.data[b] = (uint8_t)byte;
+    }
+  }
+  if (t0 == 0) {
+    *d.iters = (uint8_t)(ret == 0 ? a.max_iter : ret);
+    if (ret > 0) {
+      *d.flag = 1;
+    }
+  }
+}
+
 // a * b mod P (P of degree `order`, given with its x^order bit), Horner over b's bits
 __device__ __forceinline__ uint32_t mulmod(uint32_t a, uint32_t b, uint32_t poly, int order)
 {
@@ -423,7 +513,9 @@ __global__ __launch_bounds__(LDPC_WG) void ldpc_kernel(LdpcArgs a)
   const int      z     = (int)threadIdx.x - cwl * ls;
   const bool     act   = cwl < a.cw_per_wg && z < ls;
   const uint32_t cw    = blockIdx.x * (uint32_t)a.cw_per_wg + (uint32_t)cwl;
-  const bool     live  = act && cw < a.ncw;
+  const bool     exists = act && cw < a.ncw;
+  const CwCtx    cc    = cw_ctx(a, cw, act, (int)sizeof(E));
+  const bool     live  = cc.live;
   uint32_t*      shl   = reinterpret_cast<uint32_t*>(smem);  // LDPC_MAX_EDGES shifts
   E*             soft  = reinterpret_cast<E*>(smem + LDPC_LDS_HDR + (act ? cwl : 0) * CW);
   uint32_t*      red   = reinterpret_cast<uint32_t*>(smem + LDPC_LDS_HDR + a.cw_per_wg * CW);  // CRC parts
@@ -434,9 +526,9 @@ __global__ __launch_bounds__(LDPC_WG) void ldpc_kernel(LdpcArgs a)
 
   // ---- load: columns 0, 1 = 0 (punctured), column c >= 2 from llr[(c-2) ls] (init_ldpc_dec_c) ----
   if (live) {
-    const E* in = reinterpret_cast<const E*>(reinterpret_cast<const char*>(a.in) + (size_t)cw * a.in_stride) + z;
-    soft[z]          = 0;
-    soft[CS + z]     = 0;
+    const E* in  = reinterpret_cast<const E*>(cc.in) + z;
+    soft[z]      = 0;
+    soft[CS + z] = 0;
 #pragma unroll 4
     for (int c = 2; c < T::N; ++c) {
       soft[c * CS + z] = in[(c - 2) * ls];
@@ -444,24 +536,26 @@ __global__ __launch_bounds__(LDPC_WG) void ldpc_kernel(LdpcArgs a)
   }
 
   Lane<E> ln;
-  ln.soft       = soft;
-  ln.sh         = shl;
-  ln.z          = z;
-  ln.ls         = ls;
-  ln.busy       = live;
-  ln.n_layers   = a.n_layers;
-  ln.scale_mode = a.scale_mode;
-  ln.sf         = a.sf;
+  ln.soft        = soft;
+  ln.sh          = shl;
+  ln.z           = z;
+  ln.ls          = ls;
+  ln.busy        = live;
+  ln.n_layers    = cc.n_layers;
+  ln.n_layers_wg = wg_layers(a, cc, anyb + 1);
+  ln.scale_mode  = a.scale_mode;
+  ln.sf          = a.sf;
 
   uint32_t st[NW];
 #pragma unroll
   for (int i = 0; i < NW; ++i) {
     st[i] = 0u;
   }
-  int ret = a.xpow ? 0 : a.max_iter;
+  const bool use_crc = a.xpow || a.cws;
+  int        ret     = use_crc ? 0 : a.max_iter;
   for (int it = 0; it < a.max_iter; ++it) {
     run_iteration<BG, CS, E, NW>(ln, st, std::make_integer_sequence<int, T::M>{});
-    if (a.xpow) {
+    if (use_crc) {
       if (z == 0 && act) {
         red[cwl] = 0u;
       }
@@ -471,7 +565,7 @@ __global__ __launch_bounds__(LDPC_WG) void ldpc_kernel(LdpcArgs a)
       __syncthreads();  // last layer's soft bits; red / anyb cleared
       if (ln.busy) {
         // bits [z K, z K + K) of the message, natural order i = c ls + p
-        const int order = a.crc_order;
+        const int order = cc.order;
         const int b0    = z * T::K;
         int       c     = (int)__umulhi((uint32_t)b0, a.magic_ls);  // b0 / ls
         int       p     = b0 - c * ls;
@@ -480,14 +574,14 @@ __global__ __launch_bounds__(LDPC_WG) void ldpc_kernel(LdpcArgs a)
         for (int b = 0; b < T::K; ++b) {
           const uint32_t bit = soft[c * CS + p] < 0 ? 1u : 0u;
           const uint32_t fb  = ((crc >> (order - 1)) & 1u) ^ bit;
-          crc                = ((crc << 1) ^ (fb ? a.crc_poly : 0u)) & ((1u << order) - 1u);
+          crc                = ((crc << 1) ^ (fb ? cc.poly : 0u)) & ((1u << order) - 1u);
           ++p;
           if (p == ls) {
             p = 0;
             ++c;
           }
         }
-        const uint32_t part = mulmod(crc, a.xpow[liftK - b0 - T::K], a.crc_poly, order) & ((1u << order) - 1u);
+        const uint32_t part = mulmod(crc, cc.xpow[liftK - b0 - T::K], cc.poly, order) & ((1u << order) - 1u);
         if (part) {
           atomicXor(&red[cwl], part);
         }
@@ -509,22 +603,20 @@ __global__ __launch_bounds__(LDPC_WG) void ldpc_kernel(LdpcArgs a)
   __syncthreads();
 
   // ---- message: bit i = soft[i] < 0 for i < liftK (extract_ldpc_message_c) ----
-  if (live) {
+  auto bit = [&](int i) -> uint32_t {
+    const int c = (int)__umulhi((uint32_t)i, a.magic_ls);
+    return soft[c * CS + (i - c * ls)] < 0 ? 1u : 0u;
+  };
+  if (a.cws) {
+    cb_finish(a, cw, exists, cc, ret, z, ls, bit);
+  } else if (live) {
     uint8_t* out = a.out + (size_t)cw * a.out_stride;
     if (a.out_packed) {
       for (int b = z; b < liftK / 8; b += ls) {
-        const int i0   = 8 * b;
-        int       c    = (int)__umulhi((uint32_t)i0, a.magic_ls);
-        int       p    = i0 - c * ls;
-        uint32_t  byte = 0;
+        uint32_t byte = 0;
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
-          byte |= (uint32_t)(soft[c * CS + p] < 0) << (7 - t);
-          ++p;
-          if (p == ls) {
-            p = 0;
-            ++c;
-          }
+          byte |= bit(8 * b + t) << (7 - t);
         }
         out[b] = (uint8_t)byte;
       }
@@ -546,19 +638,21 @@ __global__ __launch_bounds__(LDPC_WG) void ldpc_kernel_pk(LdpcArgs a)
   constexpr int NW = words_before_pk<BG>(T::M);
   constexpr int CW = T::N * CS;  // LDS bytes per codeword
   extern __shared__ __attribute__((aligned(16))) int8_t smem[];
-  const int      ls    = a.ls;
-  const int      h     = ls >> 1;
-  const int      liftK = T::K * ls;
-  const int      cwl   = CS >= 384 ? 0 : (int)threadIdx.x / h;
-  const int      z     = (int)threadIdx.x - cwl * h;
-  const bool     act   = cwl < a.cw_per_wg && z < h;
-  const uint32_t cw    = blockIdx.x * (uint32_t)a.cw_per_wg + (uint32_t)cwl;
-  const bool     live  = act && cw < a.ncw;
-  uint32_t*      shl   = reinterpret_cast<uint32_t*>(smem);                 // LDPC_MAX_EDGES shifts
-  uint8_t*       lut   = reinterpret_cast<uint8_t*>(smem + LDPC_MAX_EDGES * 4);  // 128-entry scaling table
-  int8_t*        soft  = smem + LDPC_LDS_HDR + (act ? cwl : 0) * CW;
-  uint32_t*      red   = reinterpret_cast<uint32_t*>(smem + LDPC_LDS_HDR + a.cw_per_wg * CW);  // CRC parts
-  uint32_t*      anyb  = red + a.cw_per_wg;  // "some codeword still decoding" flag
+  const int      ls     = a.ls;
+  const int      h      = ls >> 1;
+  const int      liftK  = T::K * ls;
+  const int      cwl    = CS >= 384 ? 0 : (int)threadIdx.x / h;
+  const int      z      = (int)threadIdx.x - cwl * h;
+  const bool     act    = cwl < a.cw_per_wg && z < h;
+  const uint32_t cw     = blockIdx.x * (uint32_t)a.cw_per_wg + (uint32_t)cwl;
+  const bool     exists = act && cw < a.ncw;
+  const CwCtx    cc     = cw_ctx(a, cw, act, 1);
+  const bool     live   = cc.live;
+  uint32_t*      shl    = reinterpret_cast<uint32_t*>(smem);                      // LDPC_MAX_EDGES shifts
+  uint8_t*       lut    = reinterpret_cast<uint8_t*>(smem + LDPC_MAX_EDGES * 4);  // 128-entry scaling table
+  int8_t*        soft   = smem + LDPC_LDS_HDR + (act ? cwl : 0) * CW;
+  uint32_t*      red    = reinterpret_cast<uint32_t*>(smem + LDPC_LDS_HDR + a.cw_per_wg * CW);  // CRC parts
+  uint32_t*      anyb   = red + a.cw_per_wg;  // "some codeword still decoding" flag
   for (int e = (int)threadIdx.x; e < Topo<BG>::rs[T::M]; e += (int)blockDim.x) {
     shl[e] = a.sh[e];
   }
@@ -568,7 +662,7 @@ __global__ __launch_bounds__(LDPC_WG) void ldpc_kernel_pk(LdpcArgs a)
 
   // ---- load (init_ldpc_dec_c), -128 -> -127 (see above) ----
   if (live) {
-    const int8_t* in = reinterpret_cast<const int8_t*>(a.in) + (size_t)cw * a.in_stride + z;
+    const int8_t* in = reinterpret_cast<const int8_t*>(cc.in) + z;
     soft[z]          = 0;
     soft[z + h]      = 0;
     soft[CS + z]     = 0;
@@ -581,24 +675,26 @@ __global__ __launch_bounds__(LDPC_WG) void ldpc_kernel_pk(LdpcArgs a)
   }
 
   LanePk ln;
-  ln.soft     = (lds_i8*)(uintptr_t)(uint32_t)(LDPC_LDS_HDR + (act ? cwl : 0) * CW);
-  ln.sh       = shl;
-  ln.scale    = lut;
-  ln.z        = z;
-  ln.ls       = ls;
-  ln.h        = h;
-  ln.busy     = live;
-  ln.n_layers = a.n_layers;
+  ln.soft        = (lds_i8*)(uintptr_t)(uint32_t)(LDPC_LDS_HDR + (act ? cwl : 0) * CW);
+  ln.sh          = shl;
+  ln.scale       = lut;
+  ln.z           = z;
+  ln.ls          = ls;
+  ln.h           = h;
+  ln.busy        = live;
+  ln.n_layers    = cc.n_layers;
+  ln.n_layers_wg = wg_layers(a, cc, anyb + 1);
 
   uint32_t st[NW];
 #pragma unroll
   for (int i = 0; i < NW; ++i) {
     st[i] = 0u;
   }
-  int ret = a.xpow ? 0 : a.max_iter;
+  const bool use_crc = a.xpow || a.cws;
+  int        ret     = use_crc ? 0 : a.max_iter;
   for (int it = 0; it < a.max_iter; ++it) {
     run_iteration_pk<BG, CS, NW>(ln, st, std::make_integer_sequence<int, T::M>{});
-    if (a.xpow) {
+    if (use_crc) {
       if (z == 0 && act) {
         red[cwl] = 0u;
       }
@@ -608,7 +704,7 @@ __global__ __launch_bounds__(LDPC_WG) void ldpc_kernel_pk(LdpcArgs a)
       __syncthreads();  // last layer's soft bits; red / anyb cleared
       if (ln.busy) {
         // bits [2 z K, 2 z K + 2 K) of the message, natural order i = c ls + p
-        const int order = a.crc_order;
+        const int order = cc.order;
         const int b0    = 2 * z * T::K;
         int       c     = (int)__umulhi((uint32_t)b0, a.magic_ls);  // b0 / ls
         int       p     = b0 - c * ls;
@@ -617,14 +713,14 @@ __global__ __launch_bounds__(LDPC_WG) void ldpc_kernel_pk(LdpcArgs a)
         for (int b = 0; b < 2 * T::K; ++b) {
           const uint32_t bit = soft[c * CS + p] < 0 ? 1u : 0u;
           const uint32_t fb  = ((crc >> (order - 1)) & 1u) ^ bit;
-          crc                = ((crc << 1) ^ (fb ? a.crc_poly : 0u)) & ((1u << order) - 1u);
+          crc                = ((crc << 1) ^ (fb ? cc.poly : 0u)) & ((1u << order) - 1u);
           ++p;
           if (p == ls) {
             p = 0;
             ++c;
           }
         }
-        const uint32_t part = mulmod(crc, a.xpow[liftK - b0 - 2 * T::K], a.crc_poly, order) & ((1u << order) - 1u);
+        const uint32_t part = mulmod(crc, cc.xpow[liftK - b0 - 2 * T::K], cc.poly, order) & ((1u << order) - 1u);
         if (part) {
           atomicXor(&red[cwl], part);
         }
@@ -646,22 +742,20 @@ __global__ __launch_bounds__(LDPC_WG) void ldpc_kernel_pk(LdpcArgs a)
   __syncthreads();
 
   // ---- message: bit i = soft[i] < 0 for i < liftK (extract_ldpc_message_c) ----
-  if (live) {
+  auto bit = [&](int i) -> uint32_t {
+    const int c = (int)__umulhi((uint32_t)i, a.magic_ls);
+    return soft[c * CS + (i - c * ls)] < 0 ? 1u : 0u;
+  };
+  if (a.cws) {
+    cb_finish(a, cw, exists, cc, ret, z, h, bit);
+  } else if (live) {
     uint8_t* out = a.out + (size_t)cw * a.out_stride;
     if (a.out_packed) {
       for (int b = z; b < liftK / 8; b += h) {
-        const int i0   = 8 * b;
-        int       c    = (int)__umulhi((uint32_t)i0, a.magic_ls);
-        int       p    = i0 - c * ls;
-        uint32_t  byte = 0;
+        uint32_t byte = 0;
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
-          byte |= (uint32_t)(soft[c * CS + p] < 0) << (7 - t);
-          ++p;
-          if (p == ls) {
-            p = 0;
-            ++c;
-          }
+          byte |= bit(8 * b + t) << (7 - t);
         }
         out[b] = (uint8_t)byte;
       }
@@ -677,8 +771,6 @@ __global__ __launch_bounds__(LDPC_WG) void ldpc_kernel_pk(LdpcArgs a)
   }
 }
 
-// Column stride of the soft bits in LDS: 8-bit messages pick the smallest of 6 strides >= ls, 16-bit
-// messages (SRSRAN_LDPC_DECODER_S, 2 bytes a soft bit) one of 3 (fewer kernel instantiations).
 static int col_stride(int ls, int bits)
 {
   if (bits == 16) {
@@ -704,7 +796,7 @@ int ldpc_cw_per_wg(int ls, int bits)
 size_t ldpc_lds_bytes(int bg, int ls, int bits)
 {
   const int n = (bg == 0 ? 68 : 52) * col_stride(ls, bits) * (bits / 8);
-  return LDPC_LDS_HDR + (size_t)ldpc_cw_per_wg(ls, bits) * (n + 4) + 16;
+  return LDPC_LDS_HDR + (size_t)ldpc_cw_per_wg(ls, bits) * (n + 4) + 16;  // + CRC parts, flag, layer max
 }
 #endif
 

@@ -1,0 +1,571 @@
+// srsran_4g_amd/csrc/nr_sch_api.cpp -- C-ABI host side of the NR SCH receive path on the GPU.
+//
+// Implements include/srsran_sch_nr.h (the srsran_sch_nr_* / srsran_{dl,ul}sch_nr_decode surface of
+// lib/include/srsran/phy/phch/sch_nr.h) over nr_sch_kernel.hip and the LDPC kernels:
+//   LDPC code block segmentation      cbsegm.c:51-60, 152-277
+//   base graph, LBRM N_ref, TB info   sch_nr.c:33-176, ra_nr.c:449-522 (TBS for n_info > 3824)
+//   E per code block                  sch_nr.c:178-189
+//   init / carrier / free             sch_nr.c:283-405 (receive side)
+//   decode                            sch_nr.c:554-750
+// A decode is three launches on the object's stream: rate de-matching of every code block into
+// its (device) soft buffer, one LDPC launch per (base graph, lifting size) with the per-block CRC
+// early stop, and the TB assembly / TB CRC.  No CPU fallback: without a HIP device init fails.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <vector>
+
+#include "../../include/srsran_sch_nr.h"
+#include "ldpc_internal.h"
+#include "nr_sch_kernel.h"
+
+using namespace srsran_amd;
+
+namespace srsran_amd {
+uint8_t* softbuffer_dflags(srsran_softbuffer_rx_t* q);
+uint8_t* softbuffer_ddata(srsran_softbuffer_rx_t* q);
+uint32_t softbuffer_data_stride(srsran_softbuffer_rx_t* q);
+}  // namespace srsran_amd
+
+namespace {
+
+constexpr uint32_t kCrc24a = 0x1864CFB, kCrc24b = 0x1800063, kCrc16 = 0x11021;  // phy_common.h:72-74
+constexpr uint32_t kMaxCb  = SRSRAN_SCH_NR_MAX_NOF_CB_LDPC;
+
+#define CEIL_DIV(n, d) (((n) + (d)-1) / (d))
+
+int ls_valid(uint32_t z)  // 38.212 Table 5.3.2-1
+{
+  static const uint32_t A[8] = {2, 3, 5, 7, 9, 11, 13, 15};
+  for (uint32_t a : A) {
+    uint32_t v = a;
+    while (v < z) {
+      v *= 2;
+    }
+    if (v == z) {
+      return 1;
+    }
+  }
+  return 0;
+}
+
+int cbsegm_ldpc(srsran_cbsegm_t* s, int bg, uint32_t tbs)  // cbsegm.c:199-267
+{
+  if (!s) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  memset(s, 0, sizeof(*s));
+  if (tbs == 0) {
+    return SRSRAN_SUCCESS;
+  }
+  const uint32_t L    = tbs <= 3824 ? 16 : 24;
+  const uint32_t K_cb = bg == BG1 ? SRSRAN_LDPC_BG1_MAX_LEN_CB : SRSRAN_LDPC_BG2_MAX_LEN_CB;
+  const uint32_t B    = tbs + L;
+  uint32_t       C = 1, Bp = B;
+  if (B > K_cb) {
+    C  = CEIL_DIV(B, K_cb - 24u);
+    Bp = B + 24u * C;
+  }
+  const uint32_t Kp = Bp / C;
+  uint32_t       Kb = 22;
+  if (bg == BG2) {
+    Kb = B > 640 ? 10 : (B > 560 ? 9 : (B > 192 ? 8 : 6));
+  }
+  uint32_t Z = 0;
+  for (uint32_t z = CEIL_DIV(Kp, Kb); z <= MAX_LIFTSIZE; z++) {
+    if (ls_valid(z)) {
+      Z = z;
+      break;
+    }
+  }
+  if (Z == 0) {
+    fprintf(stderr, "[srsran_4g_amd] LDPC segmentation: no lifting size for TBS=%u\n", tbs);
+    return SRSRAN_ERROR;
+  }
+  s->tbs  = tbs;
+  s->L_tb = L;
+  s->L_cb = C > 1 ? 24 : 0;
+  s->C    = C;
+  s->F    = Z * (bg == BG1 ? 22u : 10u) * C;
+  s->C1   = C;
+  s->K1   = Z * (bg == BG1 ? 22u : 10u);
+  for (uint32_t i = 0; i < 8; i++) {  // K1_idx = set index of Z
+    static const uint32_t A[8] = {2, 3, 5, 7, 9, 11, 13, 15};
+    uint32_t              v    = A[i];
+    while (v < Z) {
+      v *= 2;
+    }
+    if (v == Z) {
+      s->K1_idx = i;
+    }
+  }
+  s->Z = Z;
+  return SRSRAN_SUCCESS;
+}
+
+uint32_t n_prb_lbrm(uint32_t nof_prb)  // 38.212 Table 5.4.2.1-1 (sch_nr.c:53-75)
+{
+  if (nof_prb <= 66) {
+    return 32;
+  }
+  if (nof_prb <= 107) {
+    return 107;
+  }
+  if (nof_prb <= 135) {
+    return 135;
+  }
+  if (nof_prb <= 162) {
+    return 162;
+  }
+  if (nof_prb <= 217) {
+    return 217;
+  }
+  return 273;
+}
+
+uint32_t tbs_large(uint32_t N_re, double R, uint32_t Qm, uint32_t layers)  // ra_nr.c:467-484, 502-522
+{
+  const uint32_t n_info = (uint32_t)(N_re * 1.0 * R * Qm * layers);
+  const uint32_t n      = (uint32_t)(floor(log2(n_info - 24.0)) - 5.0);
+  uint32_t       nip    = (1u << n) * (uint32_t)round((double)(n_info - 24.0) / (double)(1u << n));
+  if (nip < 3840) {
+    nip = 3840;
+  }
+  if (R <= 0.25) {
+    const uint32_t C = CEIL_DIV(nip + 24u, 3816u);
+    return 8u * C * CEIL_DIV(nip + 24u, 8u * C) - 24u;
+  }
+  if (nip > 8424) {
+    const uint32_t C = CEIL_DIV(nip + 24u, 8424u);
+    return 8u * C * CEIL_DIV(nip + 24u, 8u * C) - 24u;
+  }
+  return 8u * CEIL_DIV(nip + 24u, 8u) - 24u;
+}
+
+int Nref(uint32_t nof_prb, srsran_mcs_table_t table, uint32_t max_mimo_layers)  // sch_nr.c:94-112
+{
+  const uint32_t N_re = SRSRAN_MAX_NRE_NR * n_prb_lbrm(nof_prb);
+  const uint32_t Qm   = table == srsran_mcs_table_256qam ? 8 : 6;
+  const uint32_t tbs  = tbs_large(N_re, 948.0 / 1024.0, Qm, max_mimo_layers < 4 ? max_mimo_layers : 4);
+  const double   R    = 2.0 / 3.0;
+  srsran_cbsegm_t s;
+  if (cbsegm_ldpc(&s, srsran_sch_nr_select_basegraph(tbs, R), tbs) != SRSRAN_SUCCESS) {
+    return SRSRAN_ERROR;
+  }
+  return (int)ceil((double)tbs / (double)(s.C * R));
+}
+
+// one (base graph, lifting size) LDPC decoder of the object
+struct Ctx {
+  hipStream_t                 stream = nullptr;
+  srsran_sch_nr_args_t        args{};
+  srsran_ldpc_decoder_type_t  dtype  = SRSRAN_LDPC_DECODER_C_AVX2;
+  std::map<uint32_t, srsran_ldpc_decoder_t*> dec;  // key: bg << 16 | Z
+  uint32_t*                   d_xpow[3] = {};      // CRC24B, CRC24A, CRC16: x^n mod P, n <= 8448
+  // scratch (grown on demand)
+  NrRmCb*   d_rm    = nullptr;
+  LdpcCw*   d_cw    = nullptr;
+  NrTb*     d_tb    = nullptr;
+  uint8_t*  d_iters = nullptr;
+  size_t    cap_cb = 0, cap_cw = 0, cap_it = 0, cap_tb = 0;
+  int8_t*   d_e     = nullptr;  // host-synchronous calls: staged LLRs / payload / results
+  uint8_t*  d_pl    = nullptr;
+  uint8_t*  d_res   = nullptr;
+  size_t    cap_e = 0, cap_pl = 0;
+};
+
+srsran_ldpc_decoder_t* decoder(Ctx* c, srsran_basegraph_t bg, uint32_t Z)
+{
+  const uint32_t key = ((uint32_t)bg << 16) | Z;
+  auto           it  = c->dec.find(key);
+  if (it != c->dec.end()) {
+    return it->second;
+  }
+  srsran_ldpc_decoder_args_t a = {};
+  a.type                       = c->dtype;
+  a.bg                         = bg;
+  a.ls                         = (uint16_t)Z;
+  a.scaling_fctr               = std::isnormal(c->args.decoder_scaling_factor) ? c->args.decoder_scaling_factor : 0.8f;
+  a.max_nof_iter               = c->args.max_nof_iter;
+  auto* q                      = new srsran_ldpc_decoder_t;
+  if (srsran_ldpc_decoder_init(q, &a) != SRSRAN_SUCCESS) {
+    delete q;
+    return nullptr;
+  }
+  c->dec[key] = q;
+  return q;
+}
+
+template <typename T>
+bool grow(T*& p, size_t& cap, size_t n)
+{
+  if (n <= cap) {
+    return true;
+  }
+  hipFree(p);
+  p   = nullptr;
+  cap = 0;
+  if (hipMalloc((void**)&p, sizeof(T) * n) != hipSuccess) {
+    return false;
+  }
+  cap = n;
+  return true;
+}
+
+// the ldpc_rm.c init_rm parameters (ldpc_rm.c:99-160)
+void rm_params(const srsran_sch_nr_tb_info_t& t, uint32_t rv, uint32_t* k0, uint32_t* Ncb)
+{
+  static const uint32_t BASEK0[4][2] = {{0, 0}, {17, 13}, {33, 25}, {56, 43}};
+  const uint32_t        N            = t.Z * (t.bg == BG1 ? 66u : 50u);
+  if (N <= t.Nref) {
+    *Ncb = N;
+    *k0  = t.Z * BASEK0[rv & 3][t.bg];
+  } else {
+    *Ncb = t.Nref;
+    *k0  = t.Z * ((BASEK0[rv & 3][t.bg] * t.Nref) / N);
+  }
+}
+
+int decode_batch(srsran_sch_nr_t* q, uint32_t n, const srsran_sch_nr_gpu_tb_t* in, uint8_t* d_crc, float* d_avg,
+                 hipStream_t stream)
+{
+  Ctx* c = static_cast<Ctx*>(q->gpu);
+  std::vector<NrRmCb>                                  rm;
+  std::vector<NrTb>                                    tb;
+  std::map<srsran_ldpc_decoder_t*, std::vector<LdpcCw>> groups;
+  std::vector<std::pair<srsran_ldpc_decoder_t*, size_t>> order;
+  size_t total_cb = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    const srsran_sch_tb_t* t = in[i].tb;
+    if (!t || !in[i].sch_cfg || !in[i].d_e_bits || !in[i].d_payload || !t->softbuffer.rx) {
+      return SRSRAN_ERROR_INVALID_INPUTS;
+    }
+    srsran_sch_nr_tb_info_t info;
+    if (srsran_sch_nr_fill_tb_info(&q->carrier, in[i].sch_cfg, t, &info) != SRSRAN_SUCCESS) {
+      return SRSRAN_ERROR;
+    }
+    srsran_softbuffer_rx_t* sb = t->softbuffer.rx;
+    if (info.C == 0 || info.C > kMaxCb || sb->max_cb < info.Cp ||
+        sb->max_cb_size < info.Z * (info.bg == BG1 ? 66u : 50u)) {  // sch_nr.c:601-604
+      fprintf(stderr, "[srsran_4g_amd] NR SCH: TB of %u code blocks does not fit the soft buffer\n", info.C);
+      return SRSRAN_ERROR;
+    }
+    srsran_ldpc_decoder_t* dec = decoder(c, info.bg, info.Z);
+    if (!dec) {
+      return SRSRAN_ERROR;
+    }
+    uint32_t k0, Ncb;
+    rm_params(info, (uint32_t)t->rv, &k0, &Ncb);
+    const uint32_t qn    = info.Nl * info.Qm;
+    const uint32_t E0    = qn * (info.G / (qn * info.Cp));
+    const uint32_t E1    = qn * CEIL_DIV(info.G, qn * info.Cp);
+    const uint32_t jthr  = info.Cp - (info.G / qn) % info.Cp - 1;
+    const uint32_t end   = info.Kr - 2 * info.Z;
+    uint8_t*       flags = softbuffer_dflags(sb);
+    uint8_t*       ddata = softbuffer_ddata(sb);
+    const uint32_t dstr  = softbuffer_data_stride(sb);
+    NrTb           d     = {};
+    d.flags              = flags;
+    d.data               = ddata;
+    d.payload            = in[i].d_payload;
+    d.crc_out            = d_crc + i;
+    d.avg_out            = d_avg + i;
+    d.data_stride        = dstr;
+    d.C                  = info.C;
+    d.A                  = info.A;
+    d.Kp                 = info.Kp;
+    d.L_cb               = info.L_cb;
+    d.L_tb               = info.L_tb;
+    d.iters              = reinterpret_cast<const uint8_t*>(total_cb);  // patched after allocation
+    tb.push_back(d);
+    auto& g = groups[dec];
+    if (g.empty()) {
+      order.push_back({dec, 0});
+    }
+    for (uint32_t r = 0; r < info.C; r++) {
+      NrRmCb b = {};
+      b.e      = in[i].d_e_bits;
+      b.flags  = flags;
+      b.buf    = reinterpret_cast<int8_t*>(sb->buffer_f[r]);
+      b.r      = r;
+      b.E0     = E0;
+      b.E1     = E1;
+      b.jthr   = jthr;
+      b.Qm     = info.Qm;
+      b.k0     = k0;
+      b.Ncb    = Ncb;
+      b.ini    = end - info.F;
+      b.end    = end;
+      rm.push_back(b);
+      const uint32_t E   = r <= jthr ? E0 : E1;
+      LdpcCw         w   = {};
+      w.in               = b.buf;
+      w.data             = ddata + (size_t)r * dstr;
+      w.flag             = flags + r;
+      w.iters            = reinterpret_cast<uint8_t*>(total_cb + r);  // patched after allocation
+      w.n_layers         = (uint16_t)ldpc_layers_for(dec, k0 + E < Ncb ? k0 + E : Ncb);  // ldpc_rm.c:705
+      w.cb_len           = (uint16_t)(info.Kp - info.L_cb);
+      w.crc              = info.L_cb ? 0u : (info.L_tb == 24 ? 1u : 2u);  // sch_nr.c:656-661
+      g.push_back(w);
+    }
+    total_cb += info.C;
+  }
+  if (!grow(c->d_rm, c->cap_cb, total_cb) || !grow(c->d_cw, c->cap_cw, total_cb) ||
+      !grow(c->d_iters, c->cap_it, total_cb) || !grow(c->d_tb, c->cap_tb, n)) {
+    return SRSRAN_ERROR;
+  }
+  for (auto& d : tb) {
+    d.iters = c->d_iters + reinterpret_cast<size_t>(d.iters);
+  }
+  std::vector<LdpcCw> cws;
+  cws.reserve(total_cb);
+  for (auto& o : order) {
+    o.second = cws.size();
+    for (auto w : groups[o.first]) {
+      w.iters = c->d_iters + reinterpret_cast<size_t>(w.iters);
+      cws.push_back(w);
+    }
+  }
+  if (hipMemcpyAsync(c->d_rm, rm.data(), sizeof(NrRmCb) * rm.size(), hipMemcpyHostToDevice, stream) != hipSuccess ||
+      hipMemcpyAsync(c->d_cw, cws.data(), sizeof(LdpcCw) * cws.size(), hipMemcpyHostToDevice, stream) != hipSuccess ||
+      hipMemcpyAsync(c->d_tb, tb.data(), sizeof(NrTb) * tb.size(), hipMemcpyHostToDevice, stream) != hipSuccess) {
+    return SRSRAN_ERROR;
+  }
+  if (nr_rm_launch(c->d_rm, (uint32_t)rm.size(), stream) != hipSuccess) {
+    return SRSRAN_ERROR;
+  }
+  const uint32_t* xp[3] = {c->d_xpow[0], c->d_xpow[1], c->d_xpow[2]};
+  for (auto& o : order) {
+    if (ldpc_launch_cws(o.first, c->d_cw + o.second, (uint32_t)groups[o.first].size(), xp, stream) !=
+        SRSRAN_SUCCESS) {
+      return SRSRAN_ERROR;
+    }
+  }
+  return nr_tb_launch(c->d_tb, n, stream) == hipSuccess ? SRSRAN_SUCCESS : SRSRAN_ERROR;
+}
+
+int decode_sync(srsran_sch_nr_t* q, const srsran_sch_cfg_t* cfg, const srsran_sch_tb_t* tb, int8_t* e_bits,
+                srsran_sch_tb_res_nr_t* res)
+{
+  if (!q || !q->gpu || !cfg || !tb || !e_bits || !res) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  if (!tb->softbuffer.rx) {
+    fprintf(stderr, "[srsran_4g_amd] NR SCH: missing softbuffer\n");
+    return SRSRAN_ERROR;
+  }
+  if (!res->payload) {
+    fprintf(stderr, "[srsran_4g_amd] NR SCH: missing payload pointer\n");
+    return SRSRAN_ERROR;
+  }
+  Ctx*         c  = static_cast<Ctx*>(q->gpu);
+  const size_t ne = tb->nof_bits, npl = (size_t)(tb->tbs > 0 ? tb->tbs : 0) / 8 + 8;
+  if (!grow(c->d_e, c->cap_e, ne + 64) || !grow(c->d_pl, c->cap_pl, npl)) {
+    return SRSRAN_ERROR;
+  }
+  if (!c->d_res && hipMalloc((void**)&c->d_res, 16) != hipSuccess) {
+    return SRSRAN_ERROR;
+  }
+  if (hipMemcpyAsync(c->d_e, e_bits, ne, hipMemcpyHostToDevice, c->stream) != hipSuccess) {
+    return SRSRAN_ERROR;
+  }
+  srsran_sch_nr_gpu_tb_t one = {cfg, tb, c->d_e, c->d_pl};
+  int                    r   = decode_batch(q, 1, &one, c->d_res, reinterpret_cast<float*>(c->d_res + 4), c->stream);
+  if (r != SRSRAN_SUCCESS) {
+    return r;
+  }
+  uint8_t h[8];
+  if (hipMemcpyAsync(h, c->d_res, 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+      hipStreamSynchronize(c->stream) != hipSuccess) {
+    return SRSRAN_ERROR;
+  }
+  res->crc = h[0] != 0;
+  memcpy(&res->avg_iter, h + 4, 4);
+  if (srsran_softbuffer_rx_sync(tb->softbuffer.rx) != SRSRAN_SUCCESS) {
+    return SRSRAN_ERROR;
+  }
+  // the payload is written once every code block passed, whatever the TB CRC says (sch_nr.c:704-723)
+  srsran_sch_nr_tb_info_t info;
+  if (srsran_sch_nr_fill_tb_info(&q->carrier, cfg, tb, &info) != SRSRAN_SUCCESS) {
+    return SRSRAN_ERROR;
+  }
+  bool all = true;
+  for (uint32_t r = 0; r < info.C; r++) {
+    all = all && tb->softbuffer.rx->cb_crc[r];
+  }
+  if (all && hipMemcpy(res->payload, c->d_pl, (size_t)tb->tbs / 8, hipMemcpyDeviceToHost) != hipSuccess) {
+    return SRSRAN_ERROR;
+  }
+  return SRSRAN_SUCCESS;
+}
+
+}  // namespace
+
+extern "C" {
+
+int srsran_cbsegm_ldpc_bg1(srsran_cbsegm_t* s, uint32_t tbs) { return cbsegm_ldpc(s, BG1, tbs); }
+int srsran_cbsegm_ldpc_bg2(srsran_cbsegm_t* s, uint32_t tbs) { return cbsegm_ldpc(s, BG2, tbs); }
+
+srsran_basegraph_t srsran_sch_nr_select_basegraph(uint32_t tbs, double R)
+{
+  // A <= 292, or A <= 3824 and R <= 0.67, or R <= 0.25: base graph 2 (sch_nr.c:33-45)
+  return ((tbs <= 292) || (tbs <= 3824 && R <= 0.67) || (R <= 0.25)) ? BG2 : BG1;
+}
+
+int srsran_sch_nr_fill_tb_info(const srsran_carrier_nr_t* carrier,
+                               const srsran_sch_cfg_t*    sch_cfg,
+                               const srsran_sch_tb_t*     tb,
+                               srsran_sch_nr_tb_info_t*   cfg)
+{
+  if (!sch_cfg || !tb || !cfg) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  memset(cfg, 0, sizeof(*cfg));
+  const srsran_basegraph_t bg = srsran_sch_nr_select_basegraph((uint32_t)tb->tbs, tb->R);
+  srsran_cbsegm_t          s;
+  if (cbsegm_ldpc(&s, bg, (uint32_t)tb->tbs) != SRSRAN_SUCCESS || s.Z > MAX_LIFTSIZE) {
+    return SRSRAN_ERROR;
+  }
+  cfg->bg   = bg;
+  cfg->Qm   = srsran_mod_bits_x_symbol(tb->mod);
+  cfg->A    = (uint32_t)tb->tbs;
+  cfg->L_tb = s.L_tb;
+  cfg->L_cb = s.L_cb;
+  cfg->B    = s.tbs + s.L_tb;
+  cfg->Bp   = cfg->B + s.L_cb * s.C;
+  cfg->Kp   = s.C ? cfg->Bp / s.C : 0;
+  cfg->Kr   = s.K1;
+  cfg->F    = cfg->Kr - cfg->Kp;
+  cfg->Z    = s.Z;
+  cfg->G    = tb->nof_bits;
+  cfg->Nl   = tb->N_L;
+  if (sch_cfg->limited_buffer_rm) {
+    const int n = Nref(carrier ? carrier->nof_prb : 0, sch_cfg->mcs_table, 4);
+    if (n < SRSRAN_SUCCESS) {
+      return SRSRAN_ERROR;
+    }
+    cfg->Nref = (uint32_t)n;
+  } else {
+    cfg->Nref = SRSRAN_LDPC_MAX_LEN_ENCODED_CB;
+  }
+  if (s.C > SRSRAN_SCH_NR_MAX_NOF_CB_LDPC) {  // the reference overruns mask[] here (sch_nr.c:166-168)
+    fprintf(stderr, "[srsran_4g_amd] NR SCH: %u code blocks exceed %u\n", s.C, (uint32_t)SRSRAN_SCH_NR_MAX_NOF_CB_LDPC);
+    return SRSRAN_ERROR;
+  }
+  for (uint32_t r = 0; r < s.C; r++) {
+    cfg->mask[r] = true;
+  }
+  cfg->C  = s.C;
+  cfg->Cp = s.C;
+  return SRSRAN_SUCCESS;
+}
+
+int srsran_sch_nr_init_rx(srsran_sch_nr_t* q, const srsran_sch_nr_args_t* args)
+{
+  if (!q || !args) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  memset(q, 0, sizeof(*q));
+  if (args->decoder_use_flooded) {
+    fprintf(stderr, "[srsran_4g_amd] NR SCH: flooded LDPC schedule not provided on the GPU\n");
+    return SRSRAN_ERROR;
+  }
+  int dev = 0;
+  if (hipGetDeviceCount(&dev) != hipSuccess || dev == 0) {
+    (void)hipGetLastError();
+    fprintf(stderr, "[srsran_4g_amd] NR SCH: no HIP device available\n");
+    return SRSRAN_ERROR;
+  }
+  Ctx* c   = new Ctx;
+  c->args  = *args;
+  c->dtype = args->disable_simd ? SRSRAN_LDPC_DECODER_C : SRSRAN_LDPC_DECODER_C_AVX2;  // sch_nr.c:290-300
+  const uint32_t polys[3] = {kCrc24b, kCrc24a, kCrc16};
+  const int      ords[3]  = {24, 24, 16};
+  bool           ok       = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess;
+  for (int i = 0; ok && i < 3; i++) {
+    const auto t = ldpc_xpow_table(polys[i], ords[i], SRSRAN_LDPC_MAX_LEN_CB + 8);
+    ok           = hipMalloc((void**)&c->d_xpow[i], t.size() * 4) == hipSuccess &&
+         hipMemcpy(c->d_xpow[i], t.data(), t.size() * 4, hipMemcpyHostToDevice) == hipSuccess;
+  }
+  q->gpu = c;
+  if (!ok) {
+    srsran_sch_nr_free(q);
+    return SRSRAN_ERROR;
+  }
+  return SRSRAN_SUCCESS;
+}
+
+int srsran_sch_nr_set_carrier(srsran_sch_nr_t* q, const srsran_carrier_nr_t* carrier)
+{
+  if (!q || !carrier) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  q->carrier = *carrier;
+  return SRSRAN_SUCCESS;
+}
+
+void srsran_sch_nr_free(srsran_sch_nr_t* q)
+{
+  if (!q) {
+    return;
+  }
+  Ctx* c = static_cast<Ctx*>(q->gpu);
+  if (c) {
+    for (auto& kv : c->dec) {
+      srsran_ldpc_decoder_free(kv.second);
+      delete kv.second;
+    }
+    for (auto* p : c->d_xpow) {
+      hipFree(p);
+    }
+    hipFree(c->d_rm);
+    hipFree(c->d_cw);
+    hipFree(c->d_tb);
+    hipFree(c->d_iters);
+    hipFree(c->d_e);
+    hipFree(c->d_pl);
+    hipFree(c->d_res);
+    if (c->stream) {
+      hipStreamDestroy(c->stream);
+    }
+    delete c;
+  }
+  memset(q, 0, sizeof(*q));
+}
+
+int srsran_dlsch_nr_decode(srsran_sch_nr_t*        q,
+                           const srsran_sch_cfg_t* sch_cfg,
+                           const srsran_sch_tb_t*  tb,
+                           int8_t*                 e_bits,
+                           srsran_sch_tb_res_nr_t* res)
+{
+  return decode_sync(q, sch_cfg, tb, e_bits, res);
+}
+
+int srsran_ulsch_nr_decode(srsran_sch_nr_t*        q,
+                           const srsran_sch_cfg_t* sch_cfg,
+                           const srsran_sch_tb_t*  tb,
+                           int8_t*                 e_bits,
+                           srsran_sch_tb_res_nr_t* res)
+{
+  return decode_sync(q, sch_cfg, tb, e_bits, res);
+}
+
+int srsran_sch_nr_gpu_decode_batch(srsran_sch_nr_t*              q,
+                                   uint32_t                      nof_tb,
+                                   const srsran_sch_nr_gpu_tb_t* tbs,
+                                   uint8_t*                      d_crc,
+                                   float*                        d_avg_iter,
+                                   void*                         stream)
+{
+  if (!q || !q->gpu || (nof_tb && (!tbs || !d_crc || !d_avg_iter))) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  return decode_batch(q, nof_tb, tbs, d_crc, d_avg_iter, static_cast<hipStream_t>(stream));
+}
+
+}  // extern "C"

@@ -1,0 +1,34 @@
+// srsran_4g_amd/csrc/nr_sch_kernel.h -- NR SCH receive kernels: LDPC rate de-matching and TB assembly.
+#ifndef SRSRAN_AMD_NR_SCH_KERNEL_H
+#define SRSRAN_AMD_NR_SCH_KERNEL_H
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace srsran_amd {
+
+// One code block's rate de-matching (srsran_ldpc_rm_rx_c, ldpc_rm.c:675-706) into its soft buffer.
+struct NrRmCb {
+  const int8_t*  e;      // the TB's rate-matched LLRs (device)
+  const uint8_t* flags;  // the TB's cb_crc flags (device): a set flag skips the block and its E
+  int8_t*        buf;    // soft buffer of the block (device, >= Ncb bytes)
+  uint32_t       r;      // block index in the TB
+  uint32_t       E0, E1, jthr;  // E_r = r <= jthr ? E0 : E1 (sch_nr.c:178-189)
+  uint32_t       Qm, k0, Ncb, ini, end;  // bit selection: start, circular length, filler range
+};
+
+// One TB's assembly (sch_nr.c:692-748).
+struct NrTb {
+  const uint8_t* flags;   // cb_crc[C] (device)
+  const uint8_t* data;    // packed code block bits, block r at data + r * data_stride (device)
+  const uint8_t* iters;   // iterations per block (device)
+  uint8_t*       payload; // A / 8 bytes (device)
+  uint8_t*       crc_out; // 1: TB CRC ok
+  float*         avg_out; // average iterations
+  uint32_t       data_stride, C, A, Kp, L_cb, L_tb;
+};
+
+hipError_t nr_rm_launch(const NrRmCb* d_cbs, uint32_t ncb, hipStream_t stream);
+hipError_t nr_tb_launch(const NrTb* d_tbs, uint32_t ntb, hipStream_t stream);
+
+}  // namespace srsran_amd
+#endif

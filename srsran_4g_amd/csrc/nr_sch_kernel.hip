@@ -1,0 +1,182 @@
+// srsran_4g_amd/csrc/nr_sch_kernel.hip -- NR SCH receive kernels for CDNA4 (gfx950).
+//
+// nr_rm_kernel: srsran_ldpc_rm_rx_c (ldpc_rm.c:297-338, 396-410, 675-706) for every code block of
+//   a batch, one workgroup per block.  The reference de-interleaves (tmp[i cols + j] = e[j Qm + i]),
+//   walks the circular buffer from k0 skipping the filler range, and adds each LLR into the soft
+//   buffer position it lands on, clipping to +-63 after every add; filler positions get 127.  Here
+//   every soft-buffer position gathers its own contributions instead: position p is the rank-th
+//   non-filler position after k0, so it receives LLRs i = rank, rank + L, rank + 2L, ... (L = Ncb
+//   minus the fillers inside it), added in that order with the same clipping -- the sequential
+//   result, without atomics.  The block's LLR offset in the TB reproduces sch_nr.c: blocks whose CRC
+//   already passed are skipped and do not advance the read pointer (sch_nr.c:633-636 vs 682).
+// nr_tb_kernel: sch_nr.c:692-748 -- if every block passed, concatenate the blocks' packed bits into
+//   the payload and (C > 1) check the TB CRC over the payload against the CRC bits the last block
+//   carries; chunk CRCs are shifted into place with x^(8 bytes after) mod P and XOR-combined.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "nr_sch_kernel.h"
+
+namespace srsran_amd {
+
+__device__ __forceinline__ uint32_t cb_E(const NrRmCb& d, uint32_t r) { return r <= d.jthr ? d.E0 : d.E1; }
+
+// |[a0, a1) ∩ [b0, b1)|
+__device__ __forceinline__ uint32_t overlap(uint32_t a0, uint32_t a1, uint32_t b0, uint32_t b1)
+{
+  const uint32_t lo = max(a0, b0), hi = min(a1, b1);
+  return hi > lo ? hi - lo : 0u;
+}
+
+__global__ __launch_bounds__(256) void nr_rm_kernel(const NrRmCb* __restrict__ cbs)
+{
+  const NrRmCb d = cbs[blockIdx.x];
+  if (d.flags[d.r]) {
+    return;  // already decoded: the reference skips the block (and its rate de-matching)
+  }
+  uint32_t off = 0;  // LLR read offset of this block in the TB
+  for (uint32_t q = 0; q < d.r; ++q) {
+    off += d.flags[q] ? 0u : cb_E(d, q);
+  }
+  const uint32_t E    = cb_E(d, d.r);
+  const uint32_t cols = E / d.Qm;
+  const int8_t*  e    = d.e + off;
+  const uint32_t Ncb  = d.Ncb;
+  const uint32_t fi = min(d.ini, Ncb), fe = min(d.end, Ncb);  // filler positions inside the circle
+  const uint32_t L  = Ncb - (fe - fi);
+  for (uint32_t p = threadIdx.x; p < Ncb; p += blockDim.x) {
+    if (p >= d.ini && p < d.end) {
+      d.buf[p] = 127;  // filler bit: infinity8 (ldpc_rm.c:327-329)
+      continue;
+    }
+    // circular distance from k0, minus the fillers passed on the way
+    const uint32_t dist = p >= d.k0 ? p - d.k0 : p + Ncb - d.k0;
+    uint32_t       nf;
+    if (d.k0 + dist <= Ncb) {
+      nf = overlap(d.k0, d.k0 + dist, fi, fe);
+    } else {
+      nf = overlap(d.k0, Ncb, fi, fe) + overlap(0, d.k0 + dist - Ncb, fi, fe);
+    }
+    const uint32_t rank = dist - nf;
+    if (rank >= E) {
+      continue;
+    }
+    int v = d.buf[p];
+    for (uint32_t i = rank; i < E; i += L) {
+      const uint32_t j = i / cols;  // de-interleaver row
+      const int      x = e[(i - j * cols) * d.Qm + j];
+      v                = min(max(v + x, -63), 63);
+    }
+    d.buf[p] = (int8_t)v;
+  }
+}
+
+// a * b mod P, P of degree `order` given with its x^order bit
+__device__ __forceinline__ uint32_t mulmod(uint32_t a, uint32_t b, uint32_t poly, int order)
+{
+  uint32_t r = 0;
+#pragma unroll 1
+  for (int i = order - 1; i >= 0; i--) {
+    r = (r << 1) ^ (((b >> i) & 1u) ? a : 0u);
+    r ^= ((r >> order) & 1u) ? poly : 0u;
+  }
+  return r;
+}
+
+// x^(8 n) mod P by square-and-multiply
+__device__ __forceinline__ uint32_t xpow8(uint32_t n, uint32_t poly, int order)
+{
+  uint32_t r = 1u, b = 1u << 8;  // x^8 (order >= 16, so no reduction needed)
+  while (n) {
+    if (n & 1u) {
+      r = mulmod(r, b, poly, order);
+    }
+    b = mulmod(b, b, poly, order);
+    n >>= 1;
+  }
+  return r;
+}
+
+__global__ __launch_bounds__(256) void nr_tb_kernel(const NrTb* __restrict__ tbs)
+{
+  __shared__ uint32_t s_ok, s_iters, s_crc;
+  const NrTb d = tbs[blockIdx.x];
+  if (threadIdx.x == 0) {
+    s_ok    = 0;
+    s_iters = 0;
+    s_crc   = 0;
+  }
+  __syncthreads();
+  for (uint32_t r = threadIdx.x; r < d.C; r += blockDim.x) {
+    atomicAdd(&s_ok, d.flags[r] ? 1u : 0u);
+    atomicAdd(&s_iters, (uint32_t)d.iters[r]);
+  }
+  __syncthreads();
+  const bool all_ok = s_ok == d.C;
+  if (threadIdx.x == 0) {
+    *d.avg_out = d.C ? (float)s_iters / (float)d.C : __builtin_nanf("");
+    if (!all_ok || d.C == 1) {
+      *d.crc_out = all_ok ? 1 : 0;  // C == 1: the block's CRC was the TB CRC (sch_nr.c:729-731)
+    }
+  }
+  if (!all_ok) {
+    return;  // not all blocks decoded: no TB union, crc false (sch_nr.c:694-696)
+  }
+  // concatenation: block r contributes its first cb_bytes bytes (the last one cb_bytes_last)
+  const uint32_t cb_bytes      = (d.Kp - d.L_cb) / 8;
+  const uint32_t cb_bytes_last = (d.Kp - d.L_cb - d.L_tb) / 8;
+  const uint32_t nbytes        = (d.C - 1) * cb_bytes + cb_bytes_last;
+  const bool     tbcrc         = d.C > 1;
+  const uint32_t poly          = d.L_tb == 24 ? 0x1864CFBu : 0x11021u;  // CRC24A / CRC16 (sch_nr.c:596)
+  const int      order         = (int)d.L_tb;
+  const uint32_t chunk         = (nbytes + blockDim.x - 1) / blockDim.x;
+  const uint32_t b0 = threadIdx.x * chunk, b1 = min(b0 + chunk, nbytes);
+  uint32_t       crc = 0;
+  for (uint32_t b = b0; b < b1; ++b) {
+    const uint32_t r    = min(b / cb_bytes, d.C - 1);
+    const uint8_t  v    = d.data[(size_t)r * d.data_stride + (b - r * cb_bytes)];
+    d.payload[b]        = v;
+    if (tbcrc) {  // srsran_crc_checksum_byte: MSB first, zero init
+      crc ^= (uint32_t)v << (order - 8);
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        crc = (crc & (1u << (order - 1))) ? ((crc << 1) ^ poly) : (crc << 1);
+      }
+      crc &= (1u << order) - 1u;
+    }
+  }
+  if (tbcrc && b0 < b1) {
+    const uint32_t part = mulmod(crc, xpow8(nbytes - b1, poly, order), poly, order) & ((1u << order) - 1u);
+    atomicXor(&s_crc, part);
+  }
+  __syncthreads();
+  if (tbcrc && threadIdx.x == 0) {
+    // the TB CRC bits follow the data in the last block (sch_nr.c:711-717)
+    const uint8_t* t   = d.data + (size_t)(d.C - 1) * d.data_stride + cb_bytes_last;
+    uint32_t       chk = 0;
+    for (uint32_t b = 0; b < d.L_tb / 8; ++b) {
+      chk = (chk << 8) | t[b];
+    }
+    *d.crc_out = s_crc == chk ? 1 : 0;
+  }
+}
+
+hipError_t nr_rm_launch(const NrRmCb* d_cbs, uint32_t ncb, hipStream_t stream)
+{
+  if (ncb == 0) {
+    return hipSuccess;
+  }
+  hipLaunchKernelGGL(nr_rm_kernel, dim3(ncb), dim3(256), 0, stream, d_cbs);
+  return hipGetLastError();
+}
+
+hipError_t nr_tb_launch(const NrTb* d_tbs, uint32_t ntb, hipStream_t stream)
+{
+  if (ntb == 0) {
+    return hipSuccess;
+  }
+  hipLaunchKernelGGL(nr_tb_kernel, dim3(ntb), dim3(256), 0, stream, d_tbs);
+  return hipGetLastError();
+}
+
+}  // namespace srsran_amd

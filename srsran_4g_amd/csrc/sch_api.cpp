@@ -141,6 +141,17 @@ struct SbGpu {
   uint32_t stride = 0, data_stride = 0;
 };
 
+}  // namespace
+
+namespace srsran_amd {
+// device views of a soft buffer for other modules of the library (NR SCH)
+uint8_t* softbuffer_dflags(srsran_softbuffer_rx_t* q) { return q && q->gpu ? ((SbGpu*)q->gpu)->d_flags : nullptr; }
+uint8_t* softbuffer_ddata(srsran_softbuffer_rx_t* q) { return q && q->gpu ? ((SbGpu*)q->gpu)->d_data : nullptr; }
+uint32_t softbuffer_data_stride(srsran_softbuffer_rx_t* q) { return q && q->gpu ? ((SbGpu*)q->gpu)->data_stride : 0; }
+}  // namespace srsran_amd
+
+namespace {
+
 // ---------------- sch object device context ----------------
 struct SchCtx {
   hipStream_t stream = nullptr;

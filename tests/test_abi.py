@@ -45,12 +45,21 @@ def test_header_is_c_and_links():
 #include "srsran_sch.h"
 #include "srsran_phch.h"
 #include "srsran_ldpc.h"
+#include "srsran_sch_nr.h"
 #include <stdio.h>
 int main(void) {
   srsran_tdec_t q;
   srsran_sch_t sch;
   srsran_cbsegm_t s;
   printf("%u %zu\n", srsran_tdec_autoimp_get_subblocks(6144), sizeof(srsran_ldpc_decoder_t));
+  printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(srsran_carrier_nr_t), sizeof(srsran_sch_cfg_t), sizeof(srsran_sch_tb_t),
+         sizeof(srsran_sch_tb_res_nr_t), sizeof(srsran_sch_nr_args_t), sizeof(srsran_sch_nr_tb_info_t),
+         sizeof(srsran_sch_nr_gpu_tb_t));
+  if (srsran_cbsegm_ldpc_bg1(&s, 100000) || s.C != 12 || s.Z != 384) return 3;
+  if (srsran_sch_nr_select_basegraph(200, 0.9) != BG2) return 4;
+  if (0) { srsran_sch_nr_t nr; srsran_sch_nr_args_t na = {0}; srsran_sch_nr_init_rx(&nr, &na);
+           srsran_dlsch_nr_decode(&nr, 0, 0, 0, 0); srsran_sch_nr_gpu_decode_batch(&nr, 0, 0, 0, 0, 0);
+           srsran_sch_nr_free(&nr); }
   uint16_t pcm[BG1M * BG1Nfull];
   int8_t   pos[BG1M][MAX_CNCT];
   if (create_compact_pcm(pcm, pos, BG1, 384) || pos[4][2] != 26 || pos[4][3] != -1) return 2;
@@ -72,7 +81,12 @@ int main(void) {
                         "-lsrsran_4g_amd", "-Wl,-rpath," + libdir, "-o", exe], check=True)
         out = subprocess.run([exe], check=True, capture_output=True, text=True).stdout
         from srsran_4g_amd import ldpc
-        assert out.split() == ["16", str(ctypes.sizeof(ldpc.srsran_ldpc_decoder_t))]
+        from srsran_4g_amd import sch_nr as N
+        lines = out.split("\n")
+        assert lines[0].split() == ["16", str(ctypes.sizeof(ldpc.srsran_ldpc_decoder_t))]
+        assert [int(x) for x in lines[1].split()] == [ctypes.sizeof(t) for t in (
+            N.srsran_carrier_nr_t, N.srsran_sch_cfg_t, N.srsran_sch_tb_t, N.srsran_sch_tb_res_nr_t,
+            N.srsran_sch_nr_args_t, N.srsran_sch_nr_tb_info_t, N.srsran_sch_nr_gpu_tb_t)]
 
 
 def ref_subblocks(K):
@@ -127,3 +141,11 @@ def test_ldpc_fails_loudly_without_gpu():
 
     with pytest.raises(RuntimeError):
         ldpc.LdpcDecoder(0, 384)
+
+
+@pytest.mark.skipif(tdec.gpu_available(), reason="a HIP device is present")
+def test_nr_sch_fails_loudly_without_gpu():
+    from srsran_4g_amd import sch_nr
+
+    with pytest.raises(RuntimeError):
+        sch_nr.SchNr()

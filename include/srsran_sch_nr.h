@@ -161,14 +161,17 @@ int                srsran_ulsch_nr_decode(srsran_sch_nr_t*        q,
  * Added batch entry point: every TB's rate de-matching, LDPC decoding (one launch per (BG, Z)) and TB
  * assembly, asynchronous on `stream` (a hipStream_t).  Per TB: the configuration as for
  * srsran_dlsch_nr_decode, d_e_bits (tb.nof_bits int8 LLRs, device), d_payload (tbs / 8 bytes,
- * device, written only when every code block passed).  Per TB outputs (device): d_crc[i] (1 = TB CRC
- * ok), d_avg_iter[i].  Soft-buffer flags stay on the device (srsran_softbuffer_rx_sync()).
+ * device, written only when every code block passed), new_data (1: the TB's code blocks start from an
+ * empty soft buffer -- CRC flags, soft bits and saved payloads cleared as srsran_softbuffer_rx_reset_cb
+ * would, done inside the rate de-matching launch).  Per TB outputs (device): d_crc[i] (1 = TB CRC ok),
+ * d_avg_iter[i].  Soft-buffer flags stay on the device (srsran_softbuffer_rx_sync()).
  */
 typedef struct {
   const srsran_sch_cfg_t* sch_cfg;
   const srsran_sch_tb_t*  tb;
   const int8_t*           d_e_bits;
   uint8_t*                d_payload;
+  uint32_t                new_data;
 } srsran_sch_nr_gpu_tb_t;
 
 int srsran_sch_nr_gpu_decode_batch(srsran_sch_nr_t*              q,

@@ -300,6 +300,9 @@ int decode_batch(srsran_sch_nr_t* q, uint32_t n, const srsran_sch_nr_gpu_tb_t* i
       b.Ncb    = Ncb;
       b.ini    = end - info.F;
       b.end    = end;
+      b.data       = ddata + (size_t)r * dstr;
+      b.data_bytes = (info.Kp - info.L_cb + 7) / 8;
+      b.fresh      = in[i].new_data ? 1u : 0u;
       rm.push_back(b);
       const uint32_t E   = r <= jthr ? E0 : E1;
       LdpcCw         w   = {};
@@ -373,7 +376,7 @@ int decode_sync(srsran_sch_nr_t* q, const srsran_sch_cfg_t* cfg, const srsran_sc
   if (hipMemcpyAsync(c->d_e, e_bits, ne, hipMemcpyHostToDevice, c->stream) != hipSuccess) {
     return SRSRAN_ERROR;
   }
-  srsran_sch_nr_gpu_tb_t one = {cfg, tb, c->d_e, c->d_pl};
+  srsran_sch_nr_gpu_tb_t one = {cfg, tb, c->d_e, c->d_pl, 0};
   int                    r   = decode_batch(q, 1, &one, c->d_res, reinterpret_cast<float*>(c->d_res + 4), c->stream);
   if (r != SRSRAN_SUCCESS) {
     return r;

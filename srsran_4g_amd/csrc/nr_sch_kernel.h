@@ -9,11 +9,14 @@ namespace srsran_amd {
 // One code block's rate de-matching (srsran_ldpc_rm_rx_c, ldpc_rm.c:675-706) into its soft buffer.
 struct NrRmCb {
   const int8_t*  e;      // the TB's rate-matched LLRs (device)
-  const uint8_t* flags;  // the TB's cb_crc flags (device): a set flag skips the block and its E
+  uint8_t*       flags;  // the TB's cb_crc flags (device): a set flag skips the block and its E
   int8_t*        buf;    // soft buffer of the block (device, >= Ncb bytes)
   uint32_t       r;      // block index in the TB
   uint32_t       E0, E1, jthr;  // E_r = r <= jthr ? E0 : E1 (sch_nr.c:178-189)
   uint32_t       Qm, k0, Ncb, ini, end;  // bit selection: start, circular length, filler range
+  uint8_t*       data;        // saved payload of the block (device)
+  uint32_t       data_bytes;  // bytes of it a new transmission clears
+  uint32_t       fresh;       // new data: flags, soft bits [0, Ncb) and payload of the TB's blocks start from zero
 };
 
 // One TB's assembly (sch_nr.c:692-748).

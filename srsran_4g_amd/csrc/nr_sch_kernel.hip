@@ -9,6 +9,9 @@
 //   minus the fillers inside it), added in that order with the same clipping -- the sequential
 //   result, without atomics.  The block's LLR offset in the TB reproduces sch_nr.c: blocks whose CRC
 //   already passed are skipped and do not advance the read pointer (sch_nr.c:633-636 vs 682).
+//   With `fresh` (new data) the TB's blocks behave as after srsran_softbuffer_rx_reset_cb (softbuffer.c:
+//   150-169) restricted to what the TB can observe: no block is skipped, accumulation starts from zero
+//   over the whole circular buffer, and the block's CRC flag and saved payload are cleared.
 // nr_tb_kernel: sch_nr.c:692-748 -- if every block passed, concatenate the blocks' packed bits into
 //   the payload and (C > 1) check the TB CRC over the payload against the CRC bits the last block
 //   carries; chunk CRCs are shifted into place with x^(8 bytes after) mod P and XOR-combined.
@@ -31,12 +34,19 @@ __device__ __forceinline__ uint32_t overlap(uint32_t a0, uint32_t a1, uint32_t b
 __global__ __launch_bounds__(256) void nr_rm_kernel(const NrRmCb* __restrict__ cbs)
 {
   const NrRmCb d = cbs[blockIdx.x];
-  if (d.flags[d.r]) {
+  if (d.fresh) {
+    for (uint32_t b = threadIdx.x; b < d.data_bytes; b += blockDim.x) {
+      d.data[b] = 0;
+    }
+    if (threadIdx.x == 0) {
+      d.flags[d.r] = 0;  // read by no other block of a fresh TB
+    }
+  } else if (d.flags[d.r]) {
     return;  // already decoded: the reference skips the block (and its rate de-matching)
   }
   uint32_t off = 0;  // LLR read offset of this block in the TB
   for (uint32_t q = 0; q < d.r; ++q) {
-    off += d.flags[q] ? 0u : cb_E(d, q);
+    off += (!d.fresh && d.flags[q]) ? 0u : cb_E(d, q);
   }
   const uint32_t E    = cb_E(d, d.r);
   const uint32_t cols = E / d.Qm;
@@ -59,9 +69,12 @@ __global__ __launch_bounds__(256) void nr_rm_kernel(const NrRmCb* __restrict__ c
     }
     const uint32_t rank = dist - nf;
     if (rank >= E) {
+      if (d.fresh) {
+        d.buf[p] = 0;
+      }
       continue;
     }
-    int v = d.buf[p];
+    int v = d.fresh ? 0 : d.buf[p];
     for (uint32_t i = rank; i < E; i += L) {
       const uint32_t j = i / cols;  // de-interleaver row
       const int      x = e[(i - j * cols) * d.Qm + j];

@@ -66,7 +66,7 @@ class srsran_sch_nr_t(ctypes.Structure):
 
 class srsran_sch_nr_gpu_tb_t(ctypes.Structure):
     _fields_ = [("sch_cfg", ctypes.POINTER(srsran_sch_cfg_t)), ("tb", ctypes.POINTER(srsran_sch_tb_t)),
-                ("d_e_bits", ctypes.c_void_p), ("d_payload", ctypes.c_void_p)]
+                ("d_e_bits", ctypes.c_void_p), ("d_payload", ctypes.c_void_p), ("new_data", u32)]
 
 
 _bound = False
@@ -200,13 +200,15 @@ class SchNr:
         return ret, bool(res.crc), float(res.avg_iter), payload[:tbs // 8]
 
     def decode_batch(self, entries, d_crc, d_avg, stream=None):
-        """srsran_sch_nr_gpu_decode_batch. entries: list of (cfg, tb, d_e_bits, d_payload); the caller keeps
-        cfg / tb alive until the call returns (descriptors are read during the call)."""
+        """srsran_sch_nr_gpu_decode_batch. entries: list of (cfg, tb, d_e_bits, d_payload[, new_data]); the
+        caller keeps cfg / tb alive until the call returns (descriptors are read during the call)."""
         arr = (srsran_sch_nr_gpu_tb_t * max(len(entries), 1))()
-        for i, (cfg, tb, de, dp) in enumerate(entries):
+        for i, ent in enumerate(entries):
+            cfg, tb, de, dp = ent[:4]
             arr[i].sch_cfg = ctypes.pointer(cfg)
             arr[i].tb = ctypes.pointer(tb)
             arr[i].d_e_bits, arr[i].d_payload = de, dp
+            arr[i].new_data = int(ent[4]) if len(ent) > 4 else 0
         return lib().srsran_sch_nr_gpu_decode_batch(ctypes.byref(self.q), len(entries), arr, d_crc, d_avg, stream)
 
     def free(self):

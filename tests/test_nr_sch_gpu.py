@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 import torch
 
-from nr_sch import OracleNr, new_state
+from nr_sch import OracleNr, new_state, oracle_nr_tb_info_t
 from srsran_4g_amd import sch_nr as S
 from srsran_4g_amd import tdec
 from synth.nr_tx import NrCodeblocks, rm_params
@@ -36,13 +36,21 @@ def _llrs(rng, e, snr, amp=10.0):
 
 
 def _tbs(n_re, R, Qm, Nl):
-    """Largest multiple of 8 <= N_info whose code blocks are equal-sized (the sizes 38.214 5.1.3.2 yields)."""
+    """Largest multiple of 8 <= N_info whose code blocks are equal, byte-aligned (as 38.214 5.1.3.2 sizes are)."""
     tbs = max(24, 8 * (int(n_re * R * Qm * Nl) // 8))
     while True:
         s = S.cbsegm_ldpc(S.select_basegraph(tbs, R), tbs)
-        if (tbs + s["L_tb"] + s["L_cb"] * s["C"]) % s["C"] == 0:
+        if s["C"] == 1 or (tbs + s["L_tb"]) % (8 * s["C"]) == 0:
             return tbs
         tbs -= 8
+
+
+def _ot(t):
+    """The product's TB info as the oracle's struct (the two are asserted equal field by field)."""
+    o = oracle_nr_tb_info_t()
+    for k, v in t.as_dict().items():
+        setattr(o, k, v)
+    return o
 
 
 def _check_state(sb, st, t, tag):
@@ -83,7 +91,7 @@ def test_decode_harq_matches_oracle(ora, q, case, uplink):
         llr = _llrs(rng, enc.rate_match(rv), base + d)
         ret, crc, avg, got = q.decode(sb, tbs, R, Qm, G, Nl, rv, llr, lbrm=lbrm, mcs256=Qm == 8, uplink=uplink)
         assert ret == 0
-        want = ora.decode(t, rv, llr, st, max_iter=6)
+        want = ora.decode(_ot(t), rv, llr, st, max_iter=6)
         assert crc == bool(want[0]) and avg == pytest.approx(want[1], abs=1e-6), (rv, crc, avg, want[:2])
         if all(st["cb_crc"][:t.C]):
             assert np.array_equal(got, want[2])
@@ -105,8 +113,9 @@ def test_noise_free_single_pass(ora, q):
         sb = S.nr_softbuffer()
         ret, crc, avg, got = q.decode(sb, tbs, R, Qm, G, 1, 0, np.where(e == 1, -20, 20).astype(np.int8),
                                       mcs256=Qm == 8)
+        want = ora.decode(_ot(t), 0, np.where(e == 1, -20, 20).astype(np.int8), new_state(t.C), max_iter=6)
         assert ret == 0 and crc and np.array_equal(got, pl), (tbs, t.C)
-        assert avg == 1.0
+        assert avg == pytest.approx(want[1], abs=1e-6)
         sb.free()
 
 
@@ -140,7 +149,7 @@ def test_batch_matches_sequential_oracle(ora, q):
             keep += [d_e, d_p, cfg, tb]
             entries.append((cfg, tb, d_e.data_ptr(), d_p.data_ptr()))
             o["d_p"] = d_p
-            wants.append(ora.decode(o["t"], rv, llr, o["st"], max_iter=6))
+            wants.append(ora.decode(_ot(o["t"]), rv, llr, o["st"], max_iter=6))
         assert q.decode_batch(entries, d_crc.data_ptr(), d_avg.data_ptr()) == 0
         torch.cuda.synchronize()
         crc, avg = d_crc.cpu().numpy(), d_avg.cpu().numpy()
@@ -182,7 +191,7 @@ def test_tb_crc_mismatch_with_all_cbs_ok(ora, q):
     sb = S.nr_softbuffer()
     st = new_state(t.C)
     ret, crc, avg, got = q.decode(sb, tbs, 0.6, 6, G, 1, 0, llr)
-    want = ora.decode(t, 0, llr, st, max_iter=6)
+    want = ora.decode(_ot(t), 0, llr, st, max_iter=6)
     assert ret == 0 and not crc and not want[0]
     assert np.array_equal(got, want[2])
     _check_state(sb, st, t, "tbcrc")
@@ -206,3 +215,35 @@ def test_input_checks(ora, q):
     ret, *_ = q.decode(short, tbs, 0.6, 6, G, 1, 0, np.zeros(G, np.int8))
     assert ret != 0
     short.free()
+
+
+def test_batch_new_data_reuses_soft_buffers(ora, q):
+    """new_data = 1 on a soft buffer left by an earlier TB (flags set, soft bits accumulated) behaves as a
+    freshly reset buffer: same results and state as the oracle from an empty state."""
+    rng = np.random.default_rng(33)
+    q.carrier.nof_prb = 273
+    S.lib().srsran_sch_nr_set_carrier(S.ctypes.byref(q.q), S.ctypes.byref(q.carrier))
+    n_re, R, Qm, Nl = 12 * 13 * 60, 0.7, 6, 1
+    tbs = _tbs(n_re, R, Qm, Nl)
+    G = n_re * Qm * Nl
+    t = S.tb_info(tbs, R, Qm, G, Nl, nof_prb=273)
+    sb = S.nr_softbuffer()
+    for it, (rv, snr) in enumerate(((0, 20.0), (0, 6.0), (2, 5.0), (0, 4.0))):
+        pl = rng.integers(0, 256, tbs // 8).astype(np.uint8)
+        llr = _llrs(rng, NrCodeblocks(t, pl).rate_match(rv), snr)
+        st = new_state(t.C)
+        want = ora.decode(_ot(t), rv, llr, st, max_iter=6)
+        d_e = torch.from_numpy(llr).cuda()
+        d_p = torch.zeros(tbs // 8 + 8, dtype=torch.uint8, device="cuda")
+        d_crc = torch.full((1,), 77, dtype=torch.uint8, device="cuda")
+        d_avg = torch.zeros(1, dtype=torch.float32, device="cuda")
+        cfg, tb = S.make_cfg(), S.make_tb(tbs, R, Qm, G, Nl, rv, sb)
+        assert q.decode_batch([(cfg, tb, d_e.data_ptr(), d_p.data_ptr(), 1)], d_crc.data_ptr(), d_avg.data_ptr()) == 0
+        torch.cuda.synchronize()
+        assert int(d_crc.cpu()[0]) == want_crc(want) and float(d_avg.cpu()[0]) == pytest.approx(want[1], abs=1e-6)
+        _check_state(sb, st, t, it)
+        if want[0]:  # rv 2 alone carries no systematic bits: both converge to the all-zero codeword,
+            # whose zero-initialised CRCs pass (sch_nr.c behaves the same), hence want[2] rather than pl
+            assert np.array_equal(d_p.cpu().numpy()[:tbs // 8], want[2])
+            assert it == 2 or np.array_equal(want[2], pl)
+    sb.free()

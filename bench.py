@@ -9,7 +9,9 @@ A "step" is one pass of the hot path over one batch of synthetic input:
   workload "pdsch" (BASELINE configs[2], C3): the whole UE DL chain from time-domain samples --
       OFDM, CRS channel estimation, MMSE predecoding, demap/descramble/CSI, DL-SCH decode;
   workload "ldpc" (BASELINE configs[4]): NR LDPC decode (srsran_ldpc_decoder, 8-bit layered
-      min-sum, AVX2 arithmetic) of a batch of BG1 / Z=384 codewords, 10 iterations.
+      min-sum, AVX2 arithmetic) of a batch of BG1 / Z=384 codewords, 10 iterations;
+  workload "nrsch" (configs[4] with its callers): srsran_dlsch_nr_decode of full-carrier NR TBs
+      (273 PRB, 256QAM, R 948/1024: LDPC rate de-matching + LDPC with CRC early stop + TB CRC).
 Inputs come from the synthetic eNB transmitter (synth/, not the oracle) and are resident in
 HBM before the timed region; every step decodes the full batch (no caching).
 
@@ -88,7 +90,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--workload", choices=["all188", "k6144", "dlsch", "pdsch", "ldpc"], default="all188")
+    p.add_argument("--workload", choices=["all188", "k6144", "dlsch", "pdsch", "ldpc", "nrsch"], default="all188")
     p.add_argument("--snr", type=float, default=30.0, help="pdsch: AWGN SNR (dB) of the synthetic subframes")
     p.add_argument("--subframes", type=int, default=78,
                    help="dlsch / pdsch: subframes (2 TBs each) per step; 78 x 26 CBs = two full turbo-decoder rounds")
@@ -102,6 +104,8 @@ def parse():
     p.add_argument("--codewords", type=int, default=4096, help="ldpc: codewords per step")
     p.add_argument("--ldpc-iters", type=int, default=10, help="ldpc: iterations (srsran max_nof_iter)")
     p.add_argument("--ldpc-snr", type=float, default=1.5, help="ldpc: BPSK Es/N0 (dB) of the synthetic codewords")
+    p.add_argument("--nr-tbs", type=int, default=64, help="nrsch: transport blocks per step")
+    p.add_argument("--nr-snr", type=float, default=12.0, help="nrsch: Es/N0 (dB) of the bits as +-1 before int8 LLRs")
     return p.parse_args()
 
 
@@ -569,6 +573,157 @@ def run_ldpc(args, torch, dist, world, rank, device):
         print(json.dumps(result), flush=True)
 
 
+NR_PRB, NR_QM, NR_R = 273, 8, 948.0 / 1024.0  # 100 MHz @ 30 kHz, MCS 27 of the 256QAM table (38.214 5.1.3.1-2)
+NR_NRE = 12 * 12 * NR_PRB                      # 12 PDSCH symbols (2 DMRS symbols of 14), 1 layer
+
+
+def run_nrsch(args, torch, dist, world, rank, device):
+    """NR DL-SCH receive: per step `nr-tbs` new transmissions (rv 0) of one full-carrier TB shape,
+    through srsran_sch_nr_gpu_decode_batch (rate de-matching into the soft buffers, LDPC decode
+    with per-CB CRC early stop, max `ldpc-iters` iterations, TB assembly + CRC).  Value = decoded
+    TB bits / s."""
+    from srsran_4g_amd import prof
+    from srsran_4g_amd import sch_nr as S
+    from synth.nr_tx import NrCodeblocks, aligned_tbs, bpsk_llrs
+
+    tbs = aligned_tbs(NR_NRE, NR_R, NR_QM, 1)
+    G = NR_NRE * NR_QM
+    t = S.tb_info(tbs, NR_R, NR_QM, G, 1, nof_prb=NR_PRB, mcs256=True)
+    rng = np.random.default_rng(shard(rank)["seed"])
+    pool, pays = [], []
+    for _ in range(args.pool):
+        pl = rng.integers(0, 256, tbs // 8).astype(np.uint8)
+        pool.append(bpsk_llrs(rng, NrCodeblocks(t, pl).rate_match(0), args.nr_snr))
+        pays.append(pl)
+    ntb = args.nr_tbs
+    d_e = torch.from_numpy(np.stack([pool[i % args.pool] for i in range(ntb)])).to(device)
+    d_p = torch.zeros((ntb, tbs // 8 + 8), dtype=torch.uint8, device=device)
+    d_crc = torch.zeros(ntb, dtype=torch.uint8, device=device)
+    d_avg = torch.zeros(ntb, dtype=torch.float32, device=device)
+    q = S.SchNr(nof_prb=NR_PRB, scaling=0.8, max_nof_iter=args.ldpc_iters)
+    sbs = [S.SoftbufferRx(max_cb=t.C, max_cb_size=S.MAX_CB_SIZE) for _ in range(ntb)]
+    cfg = S.make_cfg(mcs256=True)
+    tbd = [S.make_tb(tbs, NR_R, NR_QM, G, 1, 0, sb) for sb in sbs]
+    arr = (S.srsran_sch_nr_gpu_tb_t * ntb)()
+    for i in range(ntb):
+        arr[i].sch_cfg = S.ctypes.pointer(cfg)
+        arr[i].tb = S.ctypes.pointer(tbd[i])
+        arr[i].d_e_bits, arr[i].d_payload, arr[i].new_data = d_e[i].data_ptr(), d_p[i].data_ptr(), 1
+    L = S.lib()
+    stream = torch.cuda.current_stream(device)
+    sp = stream.cuda_stream
+
+    def step():
+        if L.srsran_sch_nr_gpu_decode_batch(S.ctypes.byref(q.q), ntb, arr, d_crc.data_ptr(), d_avg.data_ptr(), sp):
+            raise RuntimeError("srsran_sch_nr_gpu_decode_batch failed")
+
+    elapsed = timed_region(step, args.steps, args.warmup, world, dist, torch.cuda.synchronize, device)
+    value = world * ntb * tbs * args.steps / elapsed / 1e6
+    crc = d_crc.cpu().numpy()
+    avg = d_avg.cpu().numpy()
+    out = d_p.cpu().numpy()
+    payload_ok = all(np.array_equal(out[i, :tbs // 8], pays[i % args.pool]) for i in range(ntb) if crc[i])
+
+    prof.enable(True)
+    nrep = max(1, min(args.steps, 3))
+    for _ in range(nrep):
+        step()
+    torch.cuda.synchronize()
+    stages = prof.read()
+    prof.enable(False)
+    ncb = ntb * t.C
+    E = G // t.C
+    Ncb = t.Z * (66 if t.bg == 0 else 50)
+    cb_bytes = (t.Kp - t.L_cb) // 8
+    # algorithmic bytes per launch (SURVEY 8d style): LLRs in, soft buffers / payloads out
+    algo = {"nr_rm_kernel": ncb * (E + Ncb + cb_bytes),       # E LLRs in, whole circular buffer + cleared payload out
+            "ldpc_kernel": ncb * (min(E, Ncb) + cb_bytes),      # soft bits covered by the transmission in, payload out
+            "nr_tb_kernel": ntb * 2 * (tbs // 8)}               # block payloads in, TB payload out
+    per_stage = {}
+    for name, (ms, n) in stages.items():
+        lps = n / nrep
+        per_stage[name] = {"ms_per_step": round(ms / nrep, 4), "launches_per_step": lps,
+                           "avg_launch_ms": round(ms / n, 4),
+                           "GBps": round(algo.get(name, 0) / (ms / n * 1e-3) / 1e9, 1)}
+    dom = max(per_stage, key=lambda k: per_stage[k]["ms_per_step"])
+    d = per_stage[dom]
+    achieved = algo[dom] / (d["avg_launch_ms"] * 1e-3) / 1e9
+    bg_cs = f"ldpc_kernel_pk<{t.bg}, 384>"  # ldpc_kernel.hip dispatch for Z = 384
+    result = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "Mbps",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int8",
+        "data": f"synthetic: NR DL-SCH TBs from synth/nr_tx.py (bits as +-1, AWGN Es/N0 {args.nr_snr} dB, int8 "
+                f"LLRs = clip(round(10 y))), {args.pool} distinct TBs tiled to the batch, HBM-resident",
+        "config": {
+            "workload": f"nrsch: {ntb} TBs x {tbs} bits (273 PRB, 256QAM, R 948/1024, 1 layer, G={G}; BG{t.bg + 1} "
+                        f"Z={t.Z}, C={t.C}), new transmissions (rv 0), CRC early stop, max {args.ldpc_iters} "
+                        "iterations, C_AVX2 arithmetic, scaling 0.8",
+            "tbs_per_step_per_gpu": ntb,
+            "tb_ok_fraction": round(float((crc == 1).mean()), 4),
+            "payload_ok": bool(payload_ok),
+            "avg_iterations": round(float(avg.mean()), 3),
+            "parallelism": f"tb-sharded x{world}",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": bg_cs if dom == "ldpc_kernel" else dom,
+            "achieved": round(achieved, 2),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5),
+            "traffic": pmc_traffic(args.workload, bg_cs if dom == "ldpc_kernel" else dom, ncb),
+            "avg_launch_ms": d["avg_launch_ms"],
+            "algo_bytes_per_launch": int(algo[dom]),
+        },
+        "stages": per_stage,
+    }
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        from nr_sch import OracleNr, RefNr, RefNrRx, new_state, ref_available, oracle_nr_tb_info_t
+        kind = "reference" if ref_available() else "port"
+        n = 0
+        t0 = time.perf_counter()
+        if kind == "reference":
+            ref = RefNr()
+            rx, sb = RefNrRx(ref, NR_PRB, 0.8, args.ldpc_iters), ref.softbuffer()
+            while time.perf_counter() - t0 < args.cpu_seconds:
+                sb.reset()  # new transmission
+                rx.decode(sb, tbs, NR_R, NR_QM, G, 1, 0, pool[n % args.pool], mcs256=True)
+                n += 1
+            dt = time.perf_counter() - t0
+            rx.free()
+            sb.free()
+        else:
+            ora = OracleNr()
+            ot = oracle_nr_tb_info_t()
+            for k, v in t.as_dict().items():
+                setattr(ot, k, v)
+            while time.perf_counter() - t0 < args.cpu_seconds:
+                ora.decode(ot, 0, pool[n % args.pool], new_state(t.C), max_iter=args.ldpc_iters)
+                n += 1
+            dt = time.perf_counter() - t0
+        result["cpu_baseline"] = {"value": round(n * tbs / dt / 1e6, 3), "unit": "Mbps", "cores": 1, "kind": kind,
+                                  "sample": f"{n} TBs of the same pool (soft buffer reset per TB) through one "
+                                            f"srsran_sch_nr_t receiver (srsran_dlsch_nr_decode), {dt:.1f} s on 1 thread"}
+    elif rank == 0:
+        result["cpu_baseline"] = None
+    for sb in sbs:
+        sb.free()
+    q.free()
+    if world > 1:
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+
+
 def main():
     args = parse()
     import torch
@@ -591,6 +746,8 @@ def main():
         return run_pdsch(args, torch, dist, world, rank, device)
     if args.workload == "ldpc":
         return run_ldpc(args, torch, dist, world, rank, device)
+    if args.workload == "nrsch":
+        return run_nrsch(args, torch, dist, world, rank, device)
 
     Ks = list(tdec.CB_SIZES) if args.workload == "all188" else [6144]
     rng = np.random.default_rng(shard(rank)["seed"])

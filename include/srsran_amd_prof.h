@@ -1,7 +1,8 @@
 /*
  * include/srsran_amd_prof.h -- added diagnostics: HIP-event timing of the GPU pipeline's kernel
  * launches per stage (no counterpart in the reference).  Stages: 0 OFDM, 1 channel estimation,
- * 2 predecoding, 3 demap/descramble/CSI, 4 rate dematching, 5 turbo decoding, 6 TB CRC / output.
+ * 2 predecoding, 3 demap/descramble/CSI, 4 rate dematching, 5 turbo decoding, 6 TB CRC / output,
+ * 7 NR LDPC rate de-matching, 8 LDPC decoding, 9 NR TB assembly / CRC.
  */
 #ifndef SRSRAN_AMD_PROF_H
 #define SRSRAN_AMD_PROF_H
@@ -11,7 +12,7 @@
 extern "C" {
 #endif
 
-#define SRSRAN_AMD_NOF_STAGES 7
+#define SRSRAN_AMD_NOF_STAGES 10
 
 /* start (non-zero) or stop recording; clears the accumulators */
 void srsran_amd_timing_enable(int enable);

@@ -104,6 +104,11 @@ class RefNr:
         L.ref_ldpc_rm_rx_c.argtypes = [P, P, u32, u32, ctypes.c_int, u32, u32, u32, u32]
         L.ref_cbsegm_ldpc.argtypes = [ctypes.c_int, u32, ctypes.POINTER(u32 * 6)]
         L.ref_nr_encode.argtypes = [u32, ctypes.c_int, ctypes.c_int, u32, u32, u32, ctypes.c_double, u32, u32, P, P]
+        L.ref_nr_rx_new.argtypes = [u32, ctypes.c_float, u32]
+        L.ref_nr_rx_new.restype = P
+        L.ref_nr_rx_free.argtypes = [P]
+        L.ref_nr_rx_decode.argtypes = [P, P, ctypes.c_int, ctypes.c_int, u32, u32, u32, ctypes.c_double, u32, u32, P, P,
+                                       ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_float)]
         L.ref_ra_nr_tbs.argtypes = [u32, ctypes.c_double, ctypes.c_double, u32, u32]
         L.ref_ra_nr_tbs.restype = u32
 
@@ -161,3 +166,27 @@ class RefNr:
                                  _p(e_bits), _p(payload), ctypes.byref(crc), ctypes.byref(avg))
         assert r == 0, r
         return crc.value, avg.value, payload[:tbs // 8]
+
+
+class RefNrRx:
+    """A persistent reference receiver (srsran_sch_nr_init_rx once) for timing: decode() into a soft buffer."""
+
+    def __init__(self, ref, nof_prb, scaling=0.8, max_iter=10):
+        self.L = ref.L
+        self.h = self.L.ref_nr_rx_new(nof_prb, scaling, max_iter)
+        assert self.h
+
+    def decode(self, sb, tbs, R, Qm, G, Nl, rv, e_bits, lbrm=False, mcs256=False):
+        e_bits = np.ascontiguousarray(e_bits, np.int8)
+        payload = np.zeros(tbs // 8 + 8, np.uint8)
+        crc = ctypes.c_int()
+        avg = ctypes.c_float()
+        r = self.L.ref_nr_rx_decode(self.h, sb.h, int(mcs256), int(lbrm), Qm, Nl, tbs, R, rv, G, _p(e_bits),
+                                    _p(payload), ctypes.byref(crc), ctypes.byref(avg))
+        assert r == 0, r
+        return crc.value, avg.value, payload[:tbs // 8]
+
+    def free(self):
+        if self.h:
+            self.L.ref_nr_rx_free(self.h)
+            self.h = None

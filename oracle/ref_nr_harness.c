@@ -87,7 +87,76 @@ int ref_nr_softbuffer_get(void* h, uint32_t r, int8_t* buf, uint32_t n, uint8_t*
   return sb->cb_crc[r] ? 1 : 0;
 }
 
-/* one srsran_dlsch_nr_decode; out[0] = crc, avg_iter written to *avg */
+/* a persistent receiver (srsran_sch_nr_init_rx once, as a UE / gNB holds it) */
+void* ref_nr_rx_new(uint32_t nof_prb, float scaling, uint32_t max_iter)
+{
+  srsran_sch_nr_t* q = calloc(1, sizeof(srsran_sch_nr_t));
+  if (!q) {
+    return NULL;
+  }
+  srsran_sch_nr_args_t args   = {};
+  args.decoder_scaling_factor = scaling;
+  args.max_nof_iter           = max_iter;
+  srsran_carrier_nr_t carrier = {};
+  carrier.nof_prb             = nof_prb;
+  carrier.max_mimo_layers     = 4;
+  quiet_on();
+  if (srsran_sch_nr_init_rx(q, &args) != 0 || srsran_sch_nr_set_carrier(q, &carrier) != 0) {
+    quiet_off();
+    free(q);
+    return NULL;
+  }
+  quiet_off();
+  return q;
+}
+
+void ref_nr_rx_free(void* h)
+{
+  if (h) {
+    srsran_sch_nr_free((srsran_sch_nr_t*)h);
+    free(h);
+  }
+}
+
+/* one srsran_dlsch_nr_decode on receiver `rx` into soft buffer `h` */
+int ref_nr_rx_decode(void*         rx,
+                     void*         h,
+                     int           mcs_table_256qam,
+                     int           lbrm,
+                     uint32_t      Qm,
+                     uint32_t      N_L,
+                     uint32_t      tbs,
+                     double        R,
+                     uint32_t      rv,
+                     uint32_t      nof_bits,
+                     const int8_t* e_bits,
+                     uint8_t*      payload,
+                     int*          crc,
+                     float*        avg_iter)
+{
+  srsran_sch_cfg_t cfg  = {};
+  cfg.mcs_table         = mcs_table_256qam ? srsran_mcs_table_256qam : srsran_mcs_table_64qam;
+  cfg.limited_buffer_rm = lbrm != 0;
+  srsran_sch_tb_t tb    = {};
+  tb.mod                = qm_to_mod(Qm);
+  tb.N_L                = N_L;
+  tb.tbs                = (int)tbs;
+  tb.R                  = R;
+  tb.rv                 = (int)rv;
+  tb.nof_bits           = nof_bits;
+  tb.enabled            = true;
+  tb.softbuffer.rx      = (srsran_softbuffer_rx_t*)h;
+  srsran_sch_tb_res_nr_t res = {};
+  res.payload                = payload;
+  quiet_on();
+  const int r = srsran_dlsch_nr_decode((srsran_sch_nr_t*)rx, &cfg, &tb, (int8_t*)e_bits, &res);
+  quiet_off();
+  *crc      = res.crc ? 1 : 0;
+  *avg_iter = res.avg_iter;
+  return r;
+}
+
+/* one srsran_dlsch_nr_decode with a receiver of its own */
 int ref_nr_decode(void*         h,
                   uint32_t      nof_prb,
                   int           mcs_table_256qam,
@@ -105,42 +174,13 @@ int ref_nr_decode(void*         h,
                   int*          crc,
                   float*        avg_iter)
 {
-  srsran_sch_nr_t      q    = {};
-  srsran_sch_nr_args_t args = {};
-  args.decoder_scaling_factor = scaling;
-  args.max_nof_iter           = max_iter;
-  quiet_on();
-  if (srsran_sch_nr_init_rx(&q, &args) != 0) {
-    quiet_off();
+  void* rx = ref_nr_rx_new(nof_prb, scaling, max_iter);
+  if (!rx) {
     return -100;
   }
-  srsran_carrier_nr_t carrier = {};
-  carrier.nof_prb             = nof_prb;
-  carrier.max_mimo_layers     = 4;
-  if (srsran_sch_nr_set_carrier(&q, &carrier) != 0) {
-    srsran_sch_nr_free(&q);
-    quiet_off();
-    return -101;
-  }
-  srsran_sch_cfg_t cfg  = {};
-  cfg.mcs_table         = mcs_table_256qam ? srsran_mcs_table_256qam : srsran_mcs_table_64qam;
-  cfg.limited_buffer_rm = lbrm != 0;
-  srsran_sch_tb_t tb    = {};
-  tb.mod                = qm_to_mod(Qm);
-  tb.N_L                = N_L;
-  tb.tbs                = (int)tbs;
-  tb.R                  = R;
-  tb.rv                 = (int)rv;
-  tb.nof_bits           = nof_bits;
-  tb.enabled            = true;
-  tb.softbuffer.rx      = (srsran_softbuffer_rx_t*)h;
-  srsran_sch_tb_res_nr_t res = {};
-  res.payload                = payload;
-  const int r                = srsran_dlsch_nr_decode(&q, &cfg, &tb, (int8_t*)e_bits, &res);
-  quiet_off();
-  *crc                       = res.crc ? 1 : 0;
-  *avg_iter                  = res.avg_iter;
-  srsran_sch_nr_free(&q);
+  const int r =
+      ref_nr_rx_decode(rx, h, mcs_table_256qam, lbrm, Qm, N_L, tbs, R, rv, nof_bits, e_bits, payload, crc, avg_iter);
+  ref_nr_rx_free(rx);
   return r;
 }
 

@@ -9,6 +9,7 @@
 // There is no CPU fallback: without a HIP device init fails with SRSRAN_ERROR.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -247,7 +248,7 @@ int ldpc_layers_for(const srsran_ldpc_decoder_t* q, uint32_t len) { return layer
 std::vector<uint32_t> ldpc_xpow_table(uint32_t poly, int order, int nmax) { return xpow_table(poly, order, nmax); }
 
 int ldpc_launch_cws(srsran_ldpc_decoder_t* q, const LdpcCw* d_cws, uint32_t n, const uint32_t* const xpow3[3],
-                    hipStream_t stream)
+                    uint32_t max_layers, hipStream_t stream)
 {
   Ctx* c = static_cast<Ctx*>(q ? q->ptr : nullptr);
   if (!c || c->bits != 8) {
@@ -259,7 +260,7 @@ int ldpc_launch_cws(srsran_ldpc_decoder_t* q, const LdpcCw* d_cws, uint32_t n, c
   a.ncw        = n;
   a.ls         = q->ls;
   a.cw_per_wg  = ldpc_cw_per_wg(q->ls, 8);
-  a.n_layers   = q->bgM;
+  a.n_layers   = (int)std::min<uint32_t>(max_layers ? max_layers : q->bgM, q->bgM);
   a.max_iter   = (int)q->max_nof_iter;
   a.scale_mode = c->scale_mode;
   a.sf         = c->sf;

@@ -37,7 +37,8 @@ struct LdpcArgs {
   uint32_t        ncw;
   int             ls;
   int             cw_per_wg;   // codewords per workgroup (ls threads each)
-  int             n_layers;    // layers processed (rate-matched length, ldpc_decoder.c:70)
+  int             n_layers;    // layers processed (rate-matched length, ldpc_decoder.c:70); CB mode: the
+                               // codewords' largest (selects the kernel instantiation)
   int             max_iter;
   int             scale_mode;  // LdpcScale
   int             sf;          // scaling factor as the mode's integer (65535ths or 100ths)
@@ -50,6 +51,8 @@ struct LdpcArgs {
   const uint32_t* xpow3[3];    // CB mode: x^n mod P tables for CRC24B, CRC24A, CRC16 (device)
   uint32_t        magic_ls;    // ceil(2^32 / ls): i / ls = umulhi(i, magic_ls) for i < 2^16
 };
+
+constexpr int LDPC_FEW_LAYERS = 8;  // layer bound of the reduced-state instantiations
 
 hipError_t ldpc_launch(int bg, const LdpcArgs& a, hipStream_t stream);
 int        ldpc_cw_per_wg(int ls, int bits);

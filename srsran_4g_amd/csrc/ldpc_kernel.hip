@@ -32,6 +32,7 @@
 #include <utility>
 
 #include "ldpc_kernel.h"
+#include "stage_timing.h"
 
 #ifndef LDPC_BG_ONLY
 #error "build with -DLDPC_BG_ONLY=0 (BG1) or 1 (BG2)"
@@ -529,8 +530,9 @@ __global__ __launch_bounds__(LDPC_WG) void ldpc_kernel(LdpcArgs a)
     const E* in  = reinterpret_cast<const E*>(cc.in) + z;
     soft[z]      = 0;
     soft[CS + z] = 0;
+    const int ncols = min(T::N, T::K + max(cc.n_layers, 4));  // columns the codeword's layers touch
 #pragma unroll 4
-    for (int c = 2; c < T::N; ++c) {
+    for (int c = 2; c < ncols; ++c) {
       soft[c * CS + z] = in[(c - 2) * ls];
     }
   }
@@ -631,11 +633,15 @@ __global__ __launch_bounds__(LDPC_WG) void ldpc_kernel(LdpcArgs a)
   }
 }
 
-template <int BG, int CS>
+// ML: layers the instantiation can process (the compressed check state is sized for them); the
+// ML = 8 instantiations serve high-rate codewords (rv 0 at code rates above ~0.6 for BG1) with a
+// fraction of the VGPRs, hence more resident workgroups
+template <int BG, int CS, int ML>
 __global__ __launch_bounds__(LDPC_WG) void ldpc_kernel_pk(LdpcArgs a)
 {
   using T          = Topo<BG>;
-  constexpr int NW = words_before_pk<BG>(T::M);
+  static_assert(ML <= T::M, "layers");
+  constexpr int NW = words_before_pk<BG>(ML);
   constexpr int CW = T::N * CS;  // LDS bytes per codeword
   extern __shared__ __attribute__((aligned(16))) int8_t smem[];
   const int      ls     = a.ls;
@@ -667,8 +673,11 @@ __global__ __launch_bounds__(LDPC_WG) void ldpc_kernel_pk(LdpcArgs a)
     soft[z + h]      = 0;
     soft[CS + z]     = 0;
     soft[CS + z + h] = 0;
+    // extension column K + 4 + j belongs to layer 4 + j only: columns past the codeword's last layer
+    // are never read (for rv 0 transmissions most of the circular buffer)
+    const int ncols = min(T::N, T::K + max(cc.n_layers, 4));
 #pragma unroll 4
-    for (int c = 2; c < T::N; ++c) {
+    for (int c = 2; c < ncols; ++c) {
       soft[c * CS + z]     = (int8_t)max((int)in[(c - 2) * ls], -127);
       soft[c * CS + z + h] = (int8_t)max((int)in[(c - 2) * ls + h], -127);
     }
@@ -693,7 +702,7 @@ __global__ __launch_bounds__(LDPC_WG) void ldpc_kernel_pk(LdpcArgs a)
   const bool use_crc = a.xpow || a.cws;
   int        ret     = use_crc ? 0 : a.max_iter;
   for (int it = 0; it < a.max_iter; ++it) {
-    run_iteration_pk<BG, CS, NW>(ln, st, std::make_integer_sequence<int, T::M>{});
+    run_iteration_pk<BG, CS, NW>(ln, st, std::make_integer_sequence<int, ML>{});
     if (use_crc) {
       if (z == 0 && act) {
         red[cwl] = 0u;
@@ -826,22 +835,22 @@ hipError_t ldpc_launch_bg<0>(const LdpcArgs& a, dim3 grid, dim3 block, size_t ld
     }
     return hipGetLastError();
   }
+  const bool few = a.n_layers <= LDPC_FEW_LAYERS;  // every codeword of the launch within 8 layers
+#define LDPC_PK(CSV)                                                                                                   \
+  case CSV:                                                                                                            \
+    if (few) {                                                                                                         \
+      hipLaunchKernelGGL((ldpc_kernel_pk<BG, CSV, LDPC_FEW_LAYERS>), grid, block, lds, s, a);                          \
+    } else {                                                                                                           \
+      hipLaunchKernelGGL((ldpc_kernel_pk<BG, CSV, Topo<BG>::M>), grid, block, lds, s, a);                              \
+    }                                                                                                                  \
+    break;
   switch (col_stride(a.ls, 8)) {
-    case 384:
-      hipLaunchKernelGGL((ldpc_kernel_pk<BG, 384>), grid, block, lds, s, a);
-      break;
-    case 256:
-      hipLaunchKernelGGL((ldpc_kernel_pk<BG, 256>), grid, block, lds, s, a);
-      break;
-    case 128:
-      hipLaunchKernelGGL((ldpc_kernel_pk<BG, 128>), grid, block, lds, s, a);
-      break;
-    case 64:
-      hipLaunchKernelGGL((ldpc_kernel_pk<BG, 64>), grid, block, lds, s, a);
-      break;
-    case 32:
-      hipLaunchKernelGGL((ldpc_kernel_pk<BG, 32>), grid, block, lds, s, a);
-      break;
+    LDPC_PK(384)
+    LDPC_PK(256)
+    LDPC_PK(128)
+    LDPC_PK(64)
+    LDPC_PK(32)
+#undef LDPC_PK
     default:
       hipLaunchKernelGGL((ldpc_kernel<BG, 16, int8_t>), grid, block, lds, s, a);
       break;
@@ -864,6 +873,7 @@ hipError_t ldpc_launch(int bg, const LdpcArgs& a, hipStream_t stream)
       (bits == 16 && a.scale_mode != LDPC_SCALE_C)) {
     return hipErrorInvalidValue;
   }
+  StageScope timing_scope(ST_LDPC, stream);
   return bg == 0 ? ldpc_launch_bg<0>(a, dim3(grid), dim3(threads), lds, stream)
                  : ldpc_launch_bg<1>(a, dim3(grid), dim3(threads), lds, stream);
 }

@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <map>
 #include <vector>
 
@@ -170,6 +171,8 @@ struct Ctx {
   NrRmCb*   d_rm    = nullptr;
   LdpcCw*   d_cw    = nullptr;
   NrTb*     d_tb    = nullptr;
+  uint32_t* d_tbscr = nullptr;  // 2 dwords per TB, zero between launches (nr_tb_kernel clears them)
+  size_t    cap_scr = 0;
   uint8_t*  d_iters = nullptr;
   size_t    cap_cb = 0, cap_cw = 0, cap_it = 0, cap_tb = 0;
   int8_t*   d_e     = nullptr;  // host-synchronous calls: staged LLRs / payload / results
@@ -238,6 +241,7 @@ int decode_batch(srsran_sch_nr_t* q, uint32_t n, const srsran_sch_nr_gpu_tb_t* i
   std::vector<NrTb>                                    tb;
   std::map<srsran_ldpc_decoder_t*, std::vector<LdpcCw>> groups;
   std::vector<std::pair<srsran_ldpc_decoder_t*, size_t>> order;
+  std::map<srsran_ldpc_decoder_t*, uint32_t>             max_layers;
   size_t total_cb = 0;
   for (uint32_t i = 0; i < n; i++) {
     const srsran_sch_tb_t* t = in[i].tb;
@@ -314,12 +318,25 @@ int decode_batch(srsran_sch_nr_t* q, uint32_t n, const srsran_sch_nr_gpu_tb_t* i
       w.cb_len           = (uint16_t)(info.Kp - info.L_cb);
       w.crc              = info.L_cb ? 0u : (info.L_tb == 24 ? 1u : 2u);  // sch_nr.c:656-661
       g.push_back(w);
+      max_layers[dec] = std::max<uint32_t>(max_layers[dec], w.n_layers);
     }
     total_cb += info.C;
   }
   if (!grow(c->d_rm, c->cap_cb, total_cb) || !grow(c->d_cw, c->cap_cw, total_cb) ||
       !grow(c->d_iters, c->cap_it, total_cb) || !grow(c->d_tb, c->cap_tb, n)) {
     return SRSRAN_ERROR;
+  }
+  if (n * 2 > c->cap_scr) {
+    if (!grow(c->d_tbscr, c->cap_scr, n * 2) || hipMemset(c->d_tbscr, 0, n * 2 * sizeof(uint32_t)) != hipSuccess) {
+      return SRSRAN_ERROR;
+    }
+  }
+  uint32_t slices = 1;
+  for (size_t i = 0; i < tb.size(); i++) {
+    const NrTb&    d      = tb[i];
+    const uint32_t nbytes = ((d.C - 1) * (d.Kp - d.L_cb) + (d.Kp - d.L_cb - d.L_tb)) / 8 + d.C;  // upper bound
+    slices                = std::max(slices, (nbytes + NR_TB_SLICE - 1) / NR_TB_SLICE);
+    tb[i].scratch         = c->d_tbscr + 2 * i;
   }
   for (auto& d : tb) {
     d.iters = c->d_iters + reinterpret_cast<size_t>(d.iters);
@@ -343,12 +360,13 @@ int decode_batch(srsran_sch_nr_t* q, uint32_t n, const srsran_sch_nr_gpu_tb_t* i
   }
   const uint32_t* xp[3] = {c->d_xpow[0], c->d_xpow[1], c->d_xpow[2]};
   for (auto& o : order) {
-    if (ldpc_launch_cws(o.first, c->d_cw + o.second, (uint32_t)groups[o.first].size(), xp, stream) !=
+    if (ldpc_launch_cws(o.first, c->d_cw + o.second, (uint32_t)groups[o.first].size(), xp, max_layers[o.first],
+                        stream) !=
         SRSRAN_SUCCESS) {
       return SRSRAN_ERROR;
     }
   }
-  return nr_tb_launch(c->d_tb, n, stream) == hipSuccess ? SRSRAN_SUCCESS : SRSRAN_ERROR;
+  return nr_tb_launch(c->d_tb, n, slices, stream) == hipSuccess ? SRSRAN_SUCCESS : SRSRAN_ERROR;
 }
 
 int decode_sync(srsran_sch_nr_t* q, const srsran_sch_cfg_t* cfg, const srsran_sch_tb_t* tb, int8_t* e_bits,
@@ -528,6 +546,7 @@ void srsran_sch_nr_free(srsran_sch_nr_t* q)
     hipFree(c->d_rm);
     hipFree(c->d_cw);
     hipFree(c->d_tb);
+    hipFree(c->d_tbscr);
     hipFree(c->d_iters);
     hipFree(c->d_e);
     hipFree(c->d_pl);

@@ -27,11 +27,18 @@ struct NrTb {
   uint8_t*       payload; // A / 8 bytes (device)
   uint8_t*       crc_out; // 1: TB CRC ok
   float*         avg_out; // average iterations
+  uint32_t*      scratch; // 2 dwords (CRC accumulator, finished slices), zero between launches
   uint32_t       data_stride, C, A, Kp, L_cb, L_tb;
 };
 
+// TB assembly slices: each workgroup copies and CRCs NR_TB_SLICE payload bytes of one TB
+constexpr uint32_t NR_TB_THREADS = 256;
+constexpr uint32_t NR_TB_BYTES   = 16;  // contiguous bytes per thread
+constexpr uint32_t NR_TB_SLICE   = NR_TB_THREADS * NR_TB_BYTES;
+
 hipError_t nr_rm_launch(const NrRmCb* d_cbs, uint32_t ncb, hipStream_t stream);
-hipError_t nr_tb_launch(const NrTb* d_tbs, uint32_t ntb, hipStream_t stream);
+// slices = max over the TBs of ceil(payload bytes / NR_TB_SLICE) (at least 1)
+hipError_t nr_tb_launch(const NrTb* d_tbs, uint32_t ntb, uint32_t slices, hipStream_t stream);
 
 }  // namespace srsran_amd
 #endif

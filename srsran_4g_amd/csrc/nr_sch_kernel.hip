@@ -19,6 +19,7 @@
 #include <stdint.h>
 
 #include "nr_sch_kernel.h"
+#include "stage_timing.h"
 
 namespace srsran_amd {
 
@@ -54,66 +55,95 @@ __global__ __launch_bounds__(256) void nr_rm_kernel(const NrRmCb* __restrict__ c
   const uint32_t Ncb  = d.Ncb;
   const uint32_t fi = min(d.ini, Ncb), fe = min(d.end, Ncb);  // filler positions inside the circle
   const uint32_t L  = Ncb - (fe - fi);
-  for (uint32_t p = threadIdx.x; p < Ncb; p += blockDim.x) {
-    if (p >= d.ini && p < d.end) {
-      d.buf[p] = 127;  // filler bit: infinity8 (ldpc_rm.c:327-329)
-      continue;
+  // de-interleaver: the i-th selected bit is e[(i mod cols) Qm + i / cols]
+  auto src = [&](uint32_t i) {
+    const uint32_t j = i / cols;
+    return (i - j * cols) * d.Qm + j;
+  };
+  // U positions per thread per pass, their loads issued together (the pass is latency-bound)
+  constexpr uint32_t U = 4;
+  for (uint32_t p0 = threadIdx.x; p0 < Ncb; p0 += U * blockDim.x) {
+    uint32_t rank[U];
+    int      x[U], v[U];
+    bool     fil[U], has[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      const uint32_t p  = p0 + u * blockDim.x;
+      const bool     ok = p < Ncb;
+      fil[u]            = ok && p >= d.ini && p < d.end;
+      // circular distance from k0, minus the fillers passed on the way
+      const uint32_t dist = p >= d.k0 ? p - d.k0 : p + Ncb - d.k0;
+      uint32_t       nf;
+      if (d.k0 + dist <= Ncb) {
+        nf = overlap(d.k0, d.k0 + dist, fi, fe);
+      } else {
+        nf = overlap(d.k0, Ncb, fi, fe) + overlap(0, d.k0 + dist - Ncb, fi, fe);
+      }
+      rank[u] = dist - nf;
+      has[u]  = ok && !fil[u] && rank[u] < E;
+      x[u]    = has[u] ? (int)e[src(rank[u])] : 0;
+      v[u]    = has[u] && !d.fresh ? (int)d.buf[p] : 0;
     }
-    // circular distance from k0, minus the fillers passed on the way
-    const uint32_t dist = p >= d.k0 ? p - d.k0 : p + Ncb - d.k0;
-    uint32_t       nf;
-    if (d.k0 + dist <= Ncb) {
-      nf = overlap(d.k0, d.k0 + dist, fi, fe);
-    } else {
-      nf = overlap(d.k0, Ncb, fi, fe) + overlap(0, d.k0 + dist - Ncb, fi, fe);
-    }
-    const uint32_t rank = dist - nf;
-    if (rank >= E) {
-      if (d.fresh) {
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      const uint32_t p = p0 + u * blockDim.x;
+      if (fil[u]) {
+        d.buf[p] = 127;  // filler bit: infinity8 (ldpc_rm.c:327-329)
+      } else if (has[u]) {
+        int acc = min(max(v[u] + x[u], -63), 63);
+        for (uint32_t i = rank[u] + L; i < E; i += L) {  // repetitions (E > L): in order, clipped each time
+          acc = min(max(acc + (int)e[src(i)], -63), 63);
+        }
+        d.buf[p] = (int8_t)acc;
+      } else if (d.fresh && p < Ncb) {
         d.buf[p] = 0;
       }
-      continue;
     }
-    int v = d.fresh ? 0 : d.buf[p];
-    for (uint32_t i = rank; i < E; i += L) {
-      const uint32_t j = i / cols;  // de-interleaver row
-      const int      x = e[(i - j * cols) * d.Qm + j];
-      v                = min(max(v + x, -63), 63);
-    }
-    d.buf[p] = (int8_t)v;
   }
 }
 
-// a * b mod P, P of degree `order` given with its x^order bit
-__device__ __forceinline__ uint32_t mulmod(uint32_t a, uint32_t b, uint32_t poly, int order)
+// a * b mod P, P of degree `order` <= 24 given with its x^order bit, a, b < 2^order (Horner over
+// the 24 low bits of b: leading zero bits leave r = 0)
+__host__ __device__ constexpr uint32_t mulmod(uint32_t a, uint32_t b, uint32_t poly, int order)
 {
   uint32_t r = 0;
-#pragma unroll 1
-  for (int i = order - 1; i >= 0; i--) {
+#pragma unroll
+  for (int i = 23; i >= 0; i--) {
     r = (r << 1) ^ (((b >> i) & 1u) ? a : 0u);
     r ^= ((r >> order) & 1u) ? poly : 0u;
   }
   return r;
 }
 
-// x^(8 n) mod P by square-and-multiply
-__device__ __forceinline__ uint32_t xpow8(uint32_t n, uint32_t poly, int order)
-{
-  uint32_t r = 1u, b = 1u << 8;  // x^8 (order >= 16, so no reduction needed)
-  while (n) {
-    if (n & 1u) {
-      r = mulmod(r, b, poly, order);
+// x^(8 2^k) mod P for the TB CRCs: [0] CRC24A, [1] CRC16 (phy_common.h:72-74)
+struct TbCrcPow {
+  uint32_t v[2][32];
+  constexpr TbCrcPow() : v()
+  {
+    const uint32_t polys[2] = {0x1864CFBu, 0x11021u};
+    const int      ords[2]  = {24, 16};
+    for (int t = 0; t < 2; t++) {
+      uint32_t p = 1u << 8;
+      for (int k = 0; k < 32; k++) {
+        v[t][k] = p;
+        p       = mulmod(p, p, polys[t], ords[t]);
+      }
     }
-    b = mulmod(b, b, poly, order);
-    n >>= 1;
   }
-  return r;
-}
+};
+__constant__ TbCrcPow c_tb_pow = TbCrcPow();
 
-__global__ __launch_bounds__(256) void nr_tb_kernel(const NrTb* __restrict__ tbs)
+// Grid (TB, slice).  Every slice checks the blocks' flags itself; slice s copies payload bytes
+// [s NR_TB_SLICE, (s + 1) NR_TB_SLICE) -- 16 contiguous bytes per thread, gathered from the blocks'
+// saved payloads -- and folds the CRC of each thread's 16 bytes, shifted into place by
+// x^(8 bytes after them) mod P, into the TB's accumulator.  The last slice to finish compares it with
+// the CRC bits the last block carries and clears the scratch for the next launch.
+__global__ __launch_bounds__(NR_TB_THREADS) void nr_tb_kernel(const NrTb* __restrict__ tbs)
 {
-  __shared__ uint32_t s_ok, s_iters, s_crc;
-  const NrTb d = tbs[blockIdx.x];
+  __shared__ uint32_t s_tab[256];
+  __shared__ uint32_t s_ok, s_iters, s_crc, s_last;
+  const NrTb     d     = tbs[blockIdx.x];
+  const uint32_t slice = blockIdx.y;
   if (threadIdx.x == 0) {
     s_ok    = 0;
     s_iters = 0;
@@ -126,7 +156,7 @@ __global__ __launch_bounds__(256) void nr_tb_kernel(const NrTb* __restrict__ tbs
   }
   __syncthreads();
   const bool all_ok = s_ok == d.C;
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0 && slice == 0) {
     *d.avg_out = d.C ? (float)s_iters / (float)d.C : __builtin_nanf("");
     if (!all_ok || d.C == 1) {
       *d.crc_out = all_ok ? 1 : 0;  // C == 1: the block's CRC was the TB CRC (sch_nr.c:729-731)
@@ -139,38 +169,79 @@ __global__ __launch_bounds__(256) void nr_tb_kernel(const NrTb* __restrict__ tbs
   const uint32_t cb_bytes      = (d.Kp - d.L_cb) / 8;
   const uint32_t cb_bytes_last = (d.Kp - d.L_cb - d.L_tb) / 8;
   const uint32_t nbytes        = (d.C - 1) * cb_bytes + cb_bytes_last;
-  const bool     tbcrc         = d.C > 1;
-  const uint32_t poly          = d.L_tb == 24 ? 0x1864CFBu : 0x11021u;  // CRC24A / CRC16 (sch_nr.c:596)
-  const int      order         = (int)d.L_tb;
-  const uint32_t chunk         = (nbytes + blockDim.x - 1) / blockDim.x;
-  const uint32_t b0 = threadIdx.x * chunk, b1 = min(b0 + chunk, nbytes);
-  uint32_t       crc = 0;
-  for (uint32_t b = b0; b < b1; ++b) {
-    const uint32_t r    = min(b / cb_bytes, d.C - 1);
-    const uint8_t  v    = d.data[(size_t)r * d.data_stride + (b - r * cb_bytes)];
-    d.payload[b]        = v;
-    if (tbcrc) {  // srsran_crc_checksum_byte: MSB first, zero init
-      crc ^= (uint32_t)v << (order - 8);
+  const uint32_t nslices       = (nbytes + NR_TB_SLICE - 1) / NR_TB_SLICE;
+  if (slice >= nslices) {
+    return;
+  }
+  const bool     tbcrc = d.C > 1;
+  const uint32_t poly  = d.L_tb == 24 ? 0x1864CFBu : 0x11021u;  // CRC24A / CRC16 (sch_nr.c:596)
+  const int      order = (int)d.L_tb;
+  const uint32_t mask  = (1u << order) - 1u;
+  if (tbcrc) {
+    for (uint32_t v = threadIdx.x; v < 256; v += blockDim.x) {
+      uint32_t c = v << (order - 8);
 #pragma unroll
       for (int k = 0; k < 8; k++) {
-        crc = (crc & (1u << (order - 1))) ? ((crc << 1) ^ poly) : (crc << 1);
+        c = (c & (1u << (order - 1))) ? ((c << 1) ^ poly) : (c << 1);
       }
-      crc &= (1u << order) - 1u;
+      s_tab[v] = c & mask;
     }
   }
-  if (tbcrc && b0 < b1) {
-    const uint32_t part = mulmod(crc, xpow8(nbytes - b1, poly, order), poly, order) & ((1u << order) - 1u);
-    atomicXor(&s_crc, part);
+  const uint32_t b0 = slice * NR_TB_SLICE + threadIdx.x * NR_TB_BYTES;
+  const uint32_t b1 = min(b0 + NR_TB_BYTES, nbytes);
+  uint8_t        v[NR_TB_BYTES];
+  if (b0 < b1) {
+    uint32_t r = min(b0 / cb_bytes, d.C - 1), o = b0 - r * cb_bytes;
+#pragma unroll
+    for (uint32_t k = 0; k < NR_TB_BYTES; ++k) {  // independent loads, issued back to back
+      const bool in = b0 + k < b1;
+      v[k]          = in ? d.data[(size_t)r * d.data_stride + o] : 0;
+      if (++o == cb_bytes && r + 1 < d.C) {
+        o = 0;
+        ++r;
+      }
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < NR_TB_BYTES; ++k) {
+      if (b0 + k < b1) {
+        d.payload[b0 + k] = v[k];
+      }
+    }
+  }
+  if (!tbcrc) {
+    return;
+  }
+  __syncthreads();  // tables
+  if (b0 < b1) {
+    uint32_t crc = 0;  // srsran_crc_checksum_byte: MSB first, zero init
+    for (uint32_t k = 0; k < b1 - b0; ++k) {
+      crc = ((crc << 8) & mask) ^ s_tab[((crc >> (order - 8)) ^ v[k]) & 0xFFu];
+    }
+    for (uint32_t n = nbytes - b1, k = 0; n; n >>= 1, ++k) {  // * x^(8 (nbytes - b1))
+      if (n & 1u) {
+        crc = mulmod(crc, c_tb_pow.v[order == 24 ? 0 : 1][k], poly, order);
+      }
+    }
+    atomicXor(&s_crc, crc & mask);
   }
   __syncthreads();
-  if (tbcrc && threadIdx.x == 0) {
+  if (threadIdx.x == 0) {
+    atomicXor(&d.scratch[0], s_crc);
+    __threadfence();
+    s_last = atomicAdd(&d.scratch[1], 1u) == nslices - 1;
+  }
+  __syncthreads();
+  if (s_last && threadIdx.x == 0) {
+    __threadfence();
+    const uint32_t acc = atomicExch(&d.scratch[0], 0u);
+    d.scratch[1]       = 0;
     // the TB CRC bits follow the data in the last block (sch_nr.c:711-717)
     const uint8_t* t   = d.data + (size_t)(d.C - 1) * d.data_stride + cb_bytes_last;
     uint32_t       chk = 0;
     for (uint32_t b = 0; b < d.L_tb / 8; ++b) {
       chk = (chk << 8) | t[b];
     }
-    *d.crc_out = s_crc == chk ? 1 : 0;
+    *d.crc_out = acc == chk ? 1 : 0;
   }
 }
 
@@ -179,16 +250,18 @@ hipError_t nr_rm_launch(const NrRmCb* d_cbs, uint32_t ncb, hipStream_t stream)
   if (ncb == 0) {
     return hipSuccess;
   }
+  StageScope timing_scope(ST_NR_RM, stream);
   hipLaunchKernelGGL(nr_rm_kernel, dim3(ncb), dim3(256), 0, stream, d_cbs);
   return hipGetLastError();
 }
 
-hipError_t nr_tb_launch(const NrTb* d_tbs, uint32_t ntb, hipStream_t stream)
+hipError_t nr_tb_launch(const NrTb* d_tbs, uint32_t ntb, uint32_t slices, hipStream_t stream)
 {
   if (ntb == 0) {
     return hipSuccess;
   }
-  hipLaunchKernelGGL(nr_tb_kernel, dim3(ntb), dim3(256), 0, stream, d_tbs);
+  StageScope timing_scope(ST_NR_TB, stream);
+  hipLaunchKernelGGL(nr_tb_kernel, dim3(ntb, slices > 0 ? slices : 1), dim3(NR_TB_THREADS), 0, stream, d_tbs);
   return hipGetLastError();
 }
 

@@ -3,7 +3,7 @@ import ctypes
 
 from .tdec import load_library
 
-NOF_STAGES = 7
+NOF_STAGES = 10
 _bound = False
 
 

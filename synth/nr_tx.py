@@ -4,7 +4,7 @@ The 38.212 transmit chain the reference's sch_nr_encode runs (sch_nr.c:410-550):
 CRC16 for TBS <= 3824), segmentation (product's srsran_sch_nr_fill_tb_info), CB CRC24B when C > 1,
 filler bits, LDPC encoding (synth/ldpc_tx.py, first 2Z bits punctured), bit selection from k0 over the
 circular buffer of Ncb bits skipping the fillers, and the row/column bit interleaver (ldpc_rm.c:173-201,
-348-362).  Pinned against the compiled reference encoder in tests/test_synth.py.
+348-362).  Pinned against the compiled reference encoder in tests/test_nr_sch_host.py.
 """
 import numpy as np
 
@@ -106,6 +106,25 @@ class NrCodeblocks:
                 sel = sel.reshape(Qm, E // Qm).T.reshape(-1)
             out.append(sel)
         return np.concatenate(out).astype(np.uint8)
+
+
+def aligned_tbs(n_re, R, Qm, Nl):
+    """Largest multiple of 8 <= N_info whose code blocks are equal, byte-aligned (as 38.214 5.1.3.2 sizes are)."""
+    from srsran_4g_amd import sch_nr as S
+
+    tbs = max(24, 8 * (int(n_re * R * Qm * Nl) // 8))
+    while True:
+        s = S.cbsegm_ldpc(S.select_basegraph(tbs, R), tbs)
+        if s["C"] == 1 or (tbs + s["L_tb"]) % (8 * s["C"]) == 0:
+            return tbs
+        tbs -= 8
+
+
+def bpsk_llrs(rng, e, snr, amp=10.0):
+    """Bits as +-1 with AWGN at `snr` dB, int8 LLRs clip(round(amp y)) (bit 1 -> negative)."""
+    x = 1.0 - 2.0 * np.asarray(e, np.float64)
+    y = x + 10 ** (-snr / 20) * rng.standard_normal(x.shape)
+    return np.clip(np.round(amp * y), -127, 127).astype(np.int8)
 
 
 def encode_tb(t, payload, rv, pcm=None):

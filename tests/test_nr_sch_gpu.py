@@ -10,7 +10,7 @@ import torch
 from nr_sch import OracleNr, new_state, oracle_nr_tb_info_t
 from srsran_4g_amd import sch_nr as S
 from srsran_4g_amd import tdec
-from synth.nr_tx import NrCodeblocks, rm_params
+from synth.nr_tx import NrCodeblocks, aligned_tbs, bpsk_llrs, rm_params
 
 pytestmark = pytest.mark.gpu
 
@@ -29,20 +29,8 @@ def q(ora):
     s.free()
 
 
-def _llrs(rng, e, snr, amp=10.0):
-    x = 1.0 - 2.0 * e
-    y = x + 10 ** (-snr / 20) * rng.standard_normal(x.shape)
-    return np.clip(np.round(amp * y), -127, 127).astype(np.int8)
-
-
-def _tbs(n_re, R, Qm, Nl):
-    """Largest multiple of 8 <= N_info whose code blocks are equal, byte-aligned (as 38.214 5.1.3.2 sizes are)."""
-    tbs = max(24, 8 * (int(n_re * R * Qm * Nl) // 8))
-    while True:
-        s = S.cbsegm_ldpc(S.select_basegraph(tbs, R), tbs)
-        if s["C"] == 1 or (tbs + s["L_tb"]) % (8 * s["C"]) == 0:
-            return tbs
-        tbs -= 8
+_llrs = bpsk_llrs
+_tbs = aligned_tbs
 
 
 def _ot(t):

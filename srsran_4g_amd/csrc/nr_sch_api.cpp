@@ -160,7 +160,14 @@ int Nref(uint32_t nof_prb, srsran_mcs_table_t table, uint32_t max_mimo_layers)  
   return (int)ceil((double)tbs / (double)(s.C * R));
 }
 
-// one (base graph, lifting size) LDPC decoder of the object
+// pinned host staging of one descriptor upload and the event that marks it consumed
+struct Stage {
+  uint8_t*   h    = nullptr;
+  size_t     cap  = 0;
+  hipEvent_t ev   = nullptr;
+  bool       used = false;
+};
+
 struct Ctx {
   hipStream_t                 stream = nullptr;
   srsran_sch_nr_args_t        args{};
@@ -168,13 +175,14 @@ struct Ctx {
   std::map<uint32_t, srsran_ldpc_decoder_t*> dec;  // key: bg << 16 | Z
   uint32_t*                   d_xpow[3] = {};      // CRC24B, CRC24A, CRC16: x^n mod P, n <= 8448
   // scratch (grown on demand)
-  NrRmCb*   d_rm    = nullptr;
-  LdpcCw*   d_cw    = nullptr;
-  NrTb*     d_tb    = nullptr;
+  uint8_t*  d_desc  = nullptr;  // descriptors of the last batch: NrRmCb[] | LdpcCw[] | NrTb[]
+  size_t    cap_desc = 0;
+  Stage     stage[2];
+  int       cur = 0;
   uint32_t* d_tbscr = nullptr;  // 2 dwords per TB, zero between launches (nr_tb_kernel clears them)
   size_t    cap_scr = 0;
   uint8_t*  d_iters = nullptr;
-  size_t    cap_cb = 0, cap_cw = 0, cap_it = 0, cap_tb = 0;
+  size_t    cap_it = 0;
   int8_t*   d_e     = nullptr;  // host-synchronous calls: staged LLRs / payload / results
   uint8_t*  d_pl    = nullptr;
   uint8_t*  d_res   = nullptr;
@@ -322,10 +330,16 @@ int decode_batch(srsran_sch_nr_t* q, uint32_t n, const srsran_sch_nr_gpu_tb_t* i
     }
     total_cb += info.C;
   }
-  if (!grow(c->d_rm, c->cap_cb, total_cb) || !grow(c->d_cw, c->cap_cw, total_cb) ||
-      !grow(c->d_iters, c->cap_it, total_cb) || !grow(c->d_tb, c->cap_tb, n)) {
+  // one descriptor upload: [rate de-matching | LDPC | TB] through pinned, double-buffered staging
+  const size_t sz_rm = (sizeof(NrRmCb) * total_cb + 15) & ~size_t(15);
+  const size_t sz_cw = (sizeof(LdpcCw) * total_cb + 15) & ~size_t(15);
+  const size_t sz_tb = sizeof(NrTb) * n;
+  if (!grow(c->d_desc, c->cap_desc, sz_rm + sz_cw + sz_tb) || !grow(c->d_iters, c->cap_it, total_cb)) {
     return SRSRAN_ERROR;
   }
+  NrRmCb* d_rm = reinterpret_cast<NrRmCb*>(c->d_desc);
+  LdpcCw* d_cw = reinterpret_cast<LdpcCw*>(c->d_desc + sz_rm);
+  NrTb*   d_tb = reinterpret_cast<NrTb*>(c->d_desc + sz_rm + sz_cw);
   if (n * 2 > c->cap_scr) {
     if (!grow(c->d_tbscr, c->cap_scr, n * 2) || hipMemset(c->d_tbscr, 0, n * 2 * sizeof(uint32_t)) != hipSuccess) {
       return SRSRAN_ERROR;
@@ -350,23 +364,44 @@ int decode_batch(srsran_sch_nr_t* q, uint32_t n, const srsran_sch_nr_gpu_tb_t* i
       cws.push_back(w);
     }
   }
-  if (hipMemcpyAsync(c->d_rm, rm.data(), sizeof(NrRmCb) * rm.size(), hipMemcpyHostToDevice, stream) != hipSuccess ||
-      hipMemcpyAsync(c->d_cw, cws.data(), sizeof(LdpcCw) * cws.size(), hipMemcpyHostToDevice, stream) != hipSuccess ||
-      hipMemcpyAsync(c->d_tb, tb.data(), sizeof(NrTb) * tb.size(), hipMemcpyHostToDevice, stream) != hipSuccess) {
+  Stage& st = c->stage[c->cur];
+  c->cur ^= 1;
+  if (st.used && hipEventSynchronize(st.ev) != hipSuccess) {  // its previous upload has been consumed
     return SRSRAN_ERROR;
   }
-  if (nr_rm_launch(c->d_rm, (uint32_t)rm.size(), stream) != hipSuccess) {
+  const size_t total = sz_rm + sz_cw + sz_tb;
+  if (total > st.cap) {
+    hipHostFree(st.h);
+    st.h   = nullptr;
+    st.cap = 0;
+    if (hipHostMalloc((void**)&st.h, total, hipHostMallocDefault) != hipSuccess) {
+      return SRSRAN_ERROR;
+    }
+    st.cap = total;
+  }
+  if (!st.ev && hipEventCreateWithFlags(&st.ev, hipEventDisableTiming) != hipSuccess) {
+    return SRSRAN_ERROR;
+  }
+  memcpy(st.h, rm.data(), sizeof(NrRmCb) * rm.size());
+  memcpy(st.h + sz_rm, cws.data(), sizeof(LdpcCw) * cws.size());
+  memcpy(st.h + sz_rm + sz_cw, tb.data(), sz_tb);
+  if (hipMemcpyAsync(c->d_desc, st.h, total, hipMemcpyHostToDevice, stream) != hipSuccess ||
+      hipEventRecord(st.ev, stream) != hipSuccess) {
+    return SRSRAN_ERROR;
+  }
+  st.used = true;
+  if (nr_rm_launch(d_rm, (uint32_t)rm.size(), stream) != hipSuccess) {
     return SRSRAN_ERROR;
   }
   const uint32_t* xp[3] = {c->d_xpow[0], c->d_xpow[1], c->d_xpow[2]};
   for (auto& o : order) {
-    if (ldpc_launch_cws(o.first, c->d_cw + o.second, (uint32_t)groups[o.first].size(), xp, max_layers[o.first],
+    if (ldpc_launch_cws(o.first, d_cw + o.second, (uint32_t)groups[o.first].size(), xp, max_layers[o.first],
                         stream) !=
         SRSRAN_SUCCESS) {
       return SRSRAN_ERROR;
     }
   }
-  return nr_tb_launch(c->d_tb, n, slices, stream) == hipSuccess ? SRSRAN_SUCCESS : SRSRAN_ERROR;
+  return nr_tb_launch(d_tb, n, slices, stream) == hipSuccess ? SRSRAN_SUCCESS : SRSRAN_ERROR;
 }
 
 int decode_sync(srsran_sch_nr_t* q, const srsran_sch_cfg_t* cfg, const srsran_sch_tb_t* tb, int8_t* e_bits,
@@ -543,9 +578,14 @@ void srsran_sch_nr_free(srsran_sch_nr_t* q)
     for (auto* p : c->d_xpow) {
       hipFree(p);
     }
-    hipFree(c->d_rm);
-    hipFree(c->d_cw);
-    hipFree(c->d_tb);
+    hipFree(c->d_desc);
+    for (auto& st : c->stage) {
+      if (st.ev) {
+        hipEventSynchronize(st.ev);
+        hipEventDestroy(st.ev);
+      }
+      hipHostFree(st.h);
+    }
     hipFree(c->d_tbscr);
     hipFree(c->d_iters);
     hipFree(c->d_e);

@@ -56,49 +56,86 @@ __global__ __launch_bounds__(256) void nr_rm_kernel(const NrRmCb* __restrict__ c
   const uint32_t fi = min(d.ini, Ncb), fe = min(d.end, Ncb);  // filler positions inside the circle
   const uint32_t L  = Ncb - (fe - fi);
   // de-interleaver: the i-th selected bit is e[(i mod cols) Qm + i / cols]
-  auto src = [&](uint32_t i) {
-    const uint32_t j = i / cols;
-    return (i - j * cols) * d.Qm + j;
-  };
-  // U positions per thread per pass, their loads issued together (the pass is latency-bound)
-  constexpr uint32_t U = 4;
-  for (uint32_t p0 = threadIdx.x; p0 < Ncb; p0 += U * blockDim.x) {
-    uint32_t rank[U];
-    int      x[U], v[U];
-    bool     fil[U], has[U];
-#pragma unroll
-    for (uint32_t u = 0; u < U; ++u) {
-      const uint32_t p  = p0 + u * blockDim.x;
-      const bool     ok = p < Ncb;
-      fil[u]            = ok && p >= d.ini && p < d.end;
-      // circular distance from k0, minus the fillers passed on the way
-      const uint32_t dist = p >= d.k0 ? p - d.k0 : p + Ncb - d.k0;
-      uint32_t       nf;
-      if (d.k0 + dist <= Ncb) {
-        nf = overlap(d.k0, d.k0 + dist, fi, fe);
-      } else {
-        nf = overlap(d.k0, Ncb, fi, fe) + overlap(0, d.k0 + dist - Ncb, fi, fe);
-      }
-      rank[u] = dist - nf;
-      has[u]  = ok && !fil[u] && rank[u] < E;
-      x[u]    = has[u] ? (int)e[src(rank[u])] : 0;
-      v[u]    = has[u] && !d.fresh ? (int)d.buf[p] : 0;
+  const uint64_t inv = ((1ull << 40) + cols - 1) / cols;  // i / cols exact for i, cols < 2^20
+  auto           div = [&](uint32_t i) { return (uint32_t)(((uint64_t)i * inv) >> 40); };
+  // rank of a non-filler position: its distance from k0 along the circle, minus the fillers passed
+  auto rank_of = [&](uint32_t p) {
+    const uint32_t dist = p >= d.k0 ? p - d.k0 : p + Ncb - d.k0;
+    uint32_t       nf;
+    if (d.k0 + dist <= Ncb) {
+      nf = overlap(d.k0, d.k0 + dist, fi, fe);
+    } else {
+      nf = overlap(d.k0, Ncb, fi, fe) + overlap(0, d.k0 + dist - Ncb, fi, fe);
     }
-#pragma unroll
-    for (uint32_t u = 0; u < U; ++u) {
-      const uint32_t p = p0 + u * blockDim.x;
-      if (fil[u]) {
-        d.buf[p] = 127;  // filler bit: infinity8 (ldpc_rm.c:327-329)
-      } else if (has[u]) {
-        int acc = min(max(v[u] + x[u], -63), 63);
-        for (uint32_t i = rank[u] + L; i < E; i += L) {  // repetitions (E > L): in order, clipped each time
-          acc = min(max(acc + (int)e[src(i)], -63), 63);
-        }
-        d.buf[p] = (int8_t)acc;
-      } else if (d.fresh && p < Ncb) {
+    return dist - nf;
+  };
+  // one position, any case (region boundaries, the tail, repetitions when E > L)
+  auto one = [&](uint32_t p) {
+    if (p >= d.ini && p < d.end) {
+      d.buf[p] = 127;  // filler bit: infinity8 (ldpc_rm.c:327-329)
+      return;
+    }
+    const uint32_t rank = rank_of(p);
+    if (rank >= E) {
+      if (d.fresh) {
         d.buf[p] = 0;
       }
+      return;
     }
+    int acc = d.fresh ? 0 : (int)d.buf[p];
+    for (uint32_t i = rank; i < E; i += L) {  // in order, clipped after every add
+      const uint32_t j = div(i);
+      acc              = min(max(acc + (int)e[(i - j * cols) * d.Qm + j], -63), 63);
+    }
+    d.buf[p] = (int8_t)acc;
+  };
+  // four positions a thread (one dword), coalesced; inside a region that neither the filler range, k0
+  // nor the end of the circle splits, ranks run consecutively
+  const bool     fast = E <= L && cols >= 4;
+  const uint32_t nq   = Ncb / 4;
+  uint32_t*      buf4 = reinterpret_cast<uint32_t*>(d.buf);  // soft buffers are 8-byte aligned
+  for (uint32_t q = threadIdx.x; q < nq; q += blockDim.x) {
+    const uint32_t p0 = 4 * q, p3 = p0 + 3;
+    const bool     split =
+        (p0 < d.ini && p3 >= d.ini) || (p0 < d.end && p3 >= d.end) || (p0 < d.k0 && p3 >= d.k0) || !fast;
+    if (split) {
+      for (uint32_t k = 0; k < 4; ++k) {
+        one(p0 + k);
+      }
+      continue;
+    }
+    if (p0 >= d.ini && p0 < d.end) {
+      buf4[q] = 0x7F7F7F7Fu;
+      continue;
+    }
+    const uint32_t r0 = rank_of(p0);
+    if (r0 >= E) {
+      if (d.fresh) {
+        buf4[q] = 0u;
+      }
+      continue;
+    }
+    const uint32_t j0  = div(r0);
+    const uint32_t m0  = r0 - j0 * cols;
+    const uint32_t old = d.fresh ? 0u : buf4[q];
+    int            x[4];
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {  // cols >= 4: at most one row change in four
+      const bool     wrap = m0 + k >= cols;
+      const uint32_t m = wrap ? m0 + k - cols : m0 + k, j = wrap ? j0 + 1 : j0;
+      x[k] = r0 + k < E ? (int)e[m * d.Qm + j] : 0;
+    }
+    uint32_t out = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+      const int v = (int8_t)(old >> (8 * k));
+      const int r = r0 + k < E ? min(max(v + x[k], -63), 63) : v;
+      out |= (uint32_t)(uint8_t)r << (8 * k);
+    }
+    buf4[q] = out;
+  }
+  for (uint32_t p = 4 * nq + threadIdx.x; p < Ncb; p += blockDim.x) {
+    one(p);
   }
 }
 
@@ -141,6 +178,7 @@ __constant__ TbCrcPow c_tb_pow = TbCrcPow();
 __global__ __launch_bounds__(NR_TB_THREADS) void nr_tb_kernel(const NrTb* __restrict__ tbs)
 {
   __shared__ uint32_t s_tab[256];
+  __shared__ uint32_t s_pow[32];  // x^(8 2^k) mod P
   __shared__ uint32_t s_ok, s_iters, s_crc, s_last;
   const NrTb     d     = tbs[blockIdx.x];
   const uint32_t slice = blockIdx.y;
@@ -186,6 +224,9 @@ __global__ __launch_bounds__(NR_TB_THREADS) void nr_tb_kernel(const NrTb* __rest
       }
       s_tab[v] = c & mask;
     }
+    if (threadIdx.x < 32) {
+      s_pow[threadIdx.x] = c_tb_pow.v[order == 24 ? 0 : 1][threadIdx.x];
+    }
   }
   const uint32_t b0 = slice * NR_TB_SLICE + threadIdx.x * NR_TB_BYTES;
   const uint32_t b1 = min(b0 + NR_TB_BYTES, nbytes);
@@ -214,12 +255,15 @@ __global__ __launch_bounds__(NR_TB_THREADS) void nr_tb_kernel(const NrTb* __rest
   __syncthreads();  // tables
   if (b0 < b1) {
     uint32_t crc = 0;  // srsran_crc_checksum_byte: MSB first, zero init
-    for (uint32_t k = 0; k < b1 - b0; ++k) {
-      crc = ((crc << 8) & mask) ^ s_tab[((crc >> (order - 8)) ^ v[k]) & 0xFFu];
+#pragma unroll
+    for (uint32_t k = 0; k < NR_TB_BYTES; ++k) {  // fixed trip count: v[] stays in registers
+      if (b0 + k < b1) {
+        crc = ((crc << 8) & mask) ^ s_tab[((crc >> (order - 8)) ^ v[k]) & 0xFFu];
+      }
     }
     for (uint32_t n = nbytes - b1, k = 0; n; n >>= 1, ++k) {  // * x^(8 (nbytes - b1))
       if (n & 1u) {
-        crc = mulmod(crc, c_tb_pow.v[order == 24 ? 0 : 1][k], poly, order);
+        crc = mulmod(crc, s_pow[k], poly, order);
       }
     }
     atomicXor(&s_crc, crc & mask);

@@ -507,7 +507,8 @@ def run_ldpc(args, torch, dist, world, rank, device):
     bytes_per_launch = ncw * (n + liftK // 8)  # int8 LLRs in + packed message out (SURVEY 8d style)
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
     cs = 384 if ls > 256 else 256 if ls > 128 else 128 if ls > 64 else 64 if ls > 32 else 32 if ls > 16 else 16
-    dom = f"ldpc_kernel_pk<{bg}, {cs}>" if ls > 16 else f"ldpc_kernel<{bg}, {cs}>"  # ldpc_kernel.hip dispatch
+    # ldpc_kernel.hip dispatch: full-length codewords use every layer (46 for BG1, 42 for BG2)
+    dom = f"ldpc_kernel_pk<{bg}, {cs}, {46 if bg == 0 else 42}>" if ls > 16 else f"ldpc_kernel<{bg}, {cs}, signed char>"
     # decode quality on the pool (the reference's ldpc_chain_test reports BER the same way)
     out = d_out.cpu().numpy()
     result = {
@@ -648,7 +649,8 @@ def run_nrsch(args, torch, dist, world, rank, device):
     dom = max(per_stage, key=lambda k: per_stage[k]["ms_per_step"])
     d = per_stage[dom]
     achieved = algo[dom] / (d["avg_launch_ms"] * 1e-3) / 1e9
-    bg_cs = f"ldpc_kernel_pk<{t.bg}, 384>"  # ldpc_kernel.hip dispatch for Z = 384
+    # ldpc_kernel.hip dispatch for Z = 384: rv-0 blocks above R ~0.6 need <= 8 layers
+    bg_cs = f"ldpc_kernel_pk<{t.bg}, 384, 8>"
     result = {
         "metric": METRIC,
         "value": round(value, 2),

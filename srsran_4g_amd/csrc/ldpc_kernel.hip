@@ -676,10 +676,35 @@ __global__ __launch_bounds__(LDPC_WG) void ldpc_kernel_pk(LdpcArgs a)
     // extension column K + 4 + j belongs to layer 4 + j only: columns past the codeword's last layer
     // are never read (for rv 0 transmissions most of the circular buffer)
     const int ncols = min(T::N, T::K + max(cc.n_layers, 4));
+    if ((ls & 3) == 0 && (reinterpret_cast<uintptr_t>(cc.in) & 3) == 0) {
+      // dwords, 8 in flight a thread: the load is latency-bound (one round trip instead of ncols)
+      const int       q   = ls >> 2;  // dwords per column
+      const int       tot = (ncols - 2) * q;
+      const uint32_t* in4 = reinterpret_cast<const uint32_t*>(cc.in);
+      for (int f0 = z; f0 < tot; f0 += 8 * h) {
+        uint32_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int f = f0 + k * h;
+          v[k]        = f < tot ? in4[f] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int f = f0 + k * h;
+          if (f < tot) {
+            const int      c  = (int)__umulhi((uint32_t)(4 * f), a.magic_ls);  // 4 f / ls
+            const uint32_t t  = v[k] ^ 0x80808080u;                              // bytes that were -128 -> 0
+            const uint32_t nz = (((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;
+            *reinterpret_cast<uint32_t*>(soft + (c + 2) * CS + (4 * f - c * ls)) = v[k] + ((~nz & 0x80808080u) >> 7);
+          }
+        }
+      }
+    } else {
 #pragma unroll 4
-    for (int c = 2; c < ncols; ++c) {
-      soft[c * CS + z]     = (int8_t)max((int)in[(c - 2) * ls], -127);
-      soft[c * CS + z + h] = (int8_t)max((int)in[(c - 2) * ls + h], -127);
+      for (int c = 2; c < ncols; ++c) {
+        soft[c * CS + z]     = (int8_t)max((int)in[(c - 2) * ls], -127);
+        soft[c * CS + z + h] = (int8_t)max((int)in[(c - 2) * ls + h], -127);
+      }
     }
   }
 

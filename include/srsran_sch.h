@@ -241,6 +241,170 @@ int srsran_dlsch_gpu_decode_batch(srsran_sch_t*                q,
                                   float*                       d_avg_noi,
                                   void*                        stream);
 
+/* ---- UL-SCH receive, data part (sch.c:994-1021, 1122-1193) ----
+ * UCI multiplexed on PUSCH (HARQ-ACK, RI, CQI: uci.c) is not provided: srsran_ulsch_decode returns
+ * SRSRAN_ERROR when cfg->uci_cfg asks for any of it.  Mirrors of pusch_cfg.h:29-87, uci_cfg.h:31-59
+ * and cqi.h:74-143 keep the reference's field names so callers compile unchanged. */
+#define SRSRAN_MAX_CARRIERS 5      /* phy_common.h:56 */
+#define SRSRAN_UCI_MAX_ACK_BITS 10 /* uci_cfg.h:27 */
+#define SRSRAN_UCI_MAX_M 9         /* uci_cfg.h:29 */
+
+typedef struct {
+  bool     pending_tb[SRSRAN_MAX_CODEWORDS];
+  uint32_t nof_acks;
+  uint32_t ncce[SRSRAN_UCI_MAX_M];
+  uint32_t N_bundle;
+  uint32_t tdd_ack_M;
+  uint32_t tdd_ack_m;
+  bool     tdd_is_multiplex;
+  uint32_t tpc_for_pucch;
+  uint32_t grant_cc_idx;
+} srsran_uci_cfg_ack_t;
+
+typedef enum {
+  SRSRAN_CQI_TYPE_WIDEBAND = 0,
+  SRSRAN_CQI_TYPE_SUBBAND_UE,
+  SRSRAN_CQI_TYPE_SUBBAND_UE_DIFF,
+  SRSRAN_CQI_TYPE_SUBBAND_HL
+} srsran_cqi_type_t;
+
+typedef struct {
+  bool              data_enable;
+  bool              pmi_present;
+  bool              four_antenna_ports;
+  bool              rank_is_not_one;
+  bool              subband_label_2_bits;
+  uint32_t          scell_index;
+  uint32_t          L;
+  uint32_t          N;
+  uint32_t          sb_idx;
+  srsran_cqi_type_t type;
+  uint32_t          ri_len;
+} srsran_cqi_cfg_t;
+
+typedef struct {
+  srsran_uci_cfg_ack_t ack[SRSRAN_MAX_CARRIERS];
+  srsran_cqi_cfg_t     cqi;
+  bool                 is_scheduling_request_tti;
+} srsran_uci_cfg_t;
+
+typedef struct {
+  uint8_t  wideband_cqi_cw0;
+  uint32_t subband_diff_cqi_cw0;
+  uint8_t  wideband_cqi_cw1;
+  uint32_t subband_diff_cqi_cw1;
+  uint32_t pmi;
+} srsran_cqi_hl_subband_t;
+typedef struct {
+  uint8_t  wideband_cqi;
+  uint8_t  subband_diff_cqi;
+  uint32_t position_subband;
+} srsran_cqi_ue_diff_subband_t;
+typedef struct {
+  uint8_t wideband_cqi;
+  uint8_t spatial_diff_cqi;
+  uint8_t pmi;
+} srsran_cqi_format2_wideband_t;
+typedef struct {
+  uint8_t subband_cqi;
+  uint8_t subband_label;
+} srsran_cqi_ue_subband_t;
+typedef struct {
+  union {
+    srsran_cqi_format2_wideband_t wideband;
+    srsran_cqi_ue_subband_t       subband_ue;
+    srsran_cqi_ue_diff_subband_t  subband_ue_diff;
+    srsran_cqi_hl_subband_t       subband_hl;
+  };
+  bool data_crc;
+} srsran_cqi_value_t;
+
+typedef struct {
+  uint8_t ack_value[SRSRAN_UCI_MAX_ACK_BITS];
+  bool    valid;
+} srsran_uci_value_ack_t;
+
+typedef struct {
+  bool                   scheduling_request;
+  srsran_cqi_value_t     cqi;
+  srsran_uci_value_ack_t ack;
+  uint8_t                ri;
+} srsran_uci_value_t;
+
+typedef struct {
+  uint32_t I_offset_cqi;
+  uint32_t I_offset_ri;
+  uint32_t I_offset_ack;
+} srsran_uci_offset_cfg_t;
+
+typedef struct {
+  uint32_t       L_prb;
+  uint32_t       n_prb[2];
+  uint32_t       n_prb_tilde[2];
+  uint32_t       freq_hopping;
+  uint32_t       nof_re;
+  uint32_t       nof_symb;
+  srsran_ra_tb_t tb;
+  srsran_ra_tb_t last_tb;
+  uint32_t       n_dmrs;
+  bool           is_rar;
+} srsran_pusch_grant_t;
+
+typedef struct {
+  uint16_t                rnti;
+  srsran_uci_cfg_t        uci_cfg;
+  srsran_uci_offset_cfg_t uci_offset;
+  srsran_pusch_grant_t    grant;
+  uint32_t                max_nof_iterations;
+  uint32_t                last_O_cqi;
+  uint32_t                K_segm;
+  uint32_t                current_tx_nb;
+  bool                    csi_enable;
+  bool                    enable_64qam;
+  union {
+    void*                   tx;
+    srsran_softbuffer_rx_t* rx;
+  } softbuffers;
+  bool     meas_time_en;
+  uint32_t meas_time_value;
+  bool     meas_epre_en;
+  bool     meas_ta_en;
+  bool     use_cedron_alg;
+  bool     meas_evm_en;
+} srsran_pusch_cfg_t;
+
+/* sch.c:1122: de-interleave q_bits (nof_bits LLRs in PUSCH order) into g_bits and decode_tb them.
+ * Returns decode_tb's value (SRSRAN_SUCCESS when the TB CRC matched); sets cfg->K_segm. */
+int srsran_ulsch_decode(srsran_sch_t*       q,
+                        srsran_pusch_cfg_t* cfg,
+                        int16_t*            q_bits,
+                        int16_t*            g_bits,
+                        uint8_t*            c_seq,
+                        uint8_t*            data,
+                        srsran_uci_value_t* uci_data); /* untouched: no UCI */
+
+/* Added batch entry point: per TB the de-interleaver (device scratch d_g_bits) and decode_tb, all
+ * asynchronous on `stream`; d_result / d_avg_noi as srsran_dlsch_gpu_decode_batch. */
+typedef struct {
+  uint32_t                tbs;
+  uint32_t                Qm;
+  uint32_t                rv;
+  uint32_t                nof_e_bits; /* H'_total Qm */
+  uint32_t                nof_symb;   /* N_symb^PUSCH */
+  const int16_t*          d_q_bits;   /* device, PUSCH order */
+  int16_t*                d_g_bits;   /* device scratch, nof_e_bits */
+  uint8_t*                d_data;     /* device, >= tbs/8 + 6 bytes */
+  srsran_softbuffer_rx_t* softbuffer;
+  uint32_t                new_data;
+} srsran_ulsch_gpu_tb_t;
+
+int srsran_ulsch_gpu_decode_batch(srsran_sch_t*                q,
+                                  uint32_t                     nof_tb,
+                                  const srsran_ulsch_gpu_tb_t* tbs,
+                                  int32_t*                     d_result,
+                                  float*                       d_avg_noi,
+                                  void*                        stream);
+
 #ifdef __cplusplus
 }
 #endif

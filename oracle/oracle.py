@@ -280,6 +280,15 @@ class Oracle(_Lib, _PhyMixin):
             raise ValueError(f"encode failed tbs={tbs}")
         return e
 
+    def ulsch_deinterleave(self, q_bits, Qm, nof_symb):
+        """ulsch_deinterleave without RI bits (sch.c:994-1021): q (PUSCH order) -> g."""
+        f = self.lib.oracle_ulsch_deinterleave
+        f.argtypes = [_i16p, _i16p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
+        q = np.ascontiguousarray(q_bits, dtype=np.int16)
+        g = np.zeros_like(q)
+        f(_ptr(q, _i16p), _ptr(g, _i16p), Qm, q.size // Qm, nof_symb)
+        return g
+
     def dlsch_decode(self, tbs, Qm, rv, e_llr, max_iterations, state=None):
         """decode_tb (sch.c:509-573). state = (softbuf[C,18600], cb_crc[C], cb_data[C,768]) for HARQ.
 

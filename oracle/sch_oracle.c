@@ -373,3 +373,19 @@ uint32_t oracle_crc_bits(uint32_t poly, int order, const uint8_t* bits, uint32_t
   }
   return (uint32_t)crc;
 }
+
+/* ulsch_deinterleave (sch.c:994-1021) without RI bits: ulsch_interleave_gen (sch.c:661-682) numbers the
+ * positions j Qm + i rows Qm + k in (row j, column i, bit k) order, srsran_vec_lut_sis (vector.c:147-152)
+ * stores g[number] = q[position].  Positions past rows N_symb Qm are neither read nor written. */
+void oracle_ulsch_deinterleave(const int16_t* q, int16_t* g, uint32_t Qm, uint32_t H_prime_total, uint32_t N_symb)
+{
+  const uint32_t rows = H_prime_total / N_symb;
+  uint32_t       idx  = 0;
+  for (uint32_t j = 0; j < rows; j++) {
+    for (uint32_t i = 0; i < N_symb; i++) {
+      for (uint32_t k = 0; k < Qm; k++) {
+        g[idx++] = q[j * Qm + i * rows * Qm + k];
+      }
+    }
+  }
+}

@@ -175,6 +175,8 @@ struct SchCtx {
   uint8_t*    h_io = nullptr;  // pinned: flags in/out, result, avg
   uint8_t*    d_zero = nullptr;  // a cleared cb_crc flag for new transmissions
   bool        used = false;
+  int16_t*    d_ul = nullptr;    // srsran_ulsch_decode: q then g bits
+  size_t      ul_cap = 0;
 };
 
 constexpr size_t kDataCap = (size_t)SCH_MAX_CB * SCH_SLOT_BYTES;
@@ -835,6 +837,7 @@ void srsran_sch_free(srsran_sch_t* q)
     hipFree(x->d_avg);
     hipHostFree(x->h_io);
     hipFree(x->d_zero);
+    hipFree(x->d_ul);
     delete x;
   }
   srsran_tdec_free(&q->decoder);
@@ -986,6 +989,100 @@ int srsran_dlsch_gpu_decode_batch(srsran_sch_t*                q,
     return SRSRAN_ERROR;
   }
   return enqueue_batch(q, nof_tb, tbs, d_result, d_avg_noi, (hipStream_t)stream);
+}
+
+// ---------------- UL-SCH data part (sch.c:994-1021, 1122-1193), no UCI ----------------
+static bool uci_requested(const srsran_pusch_cfg_t* cfg)
+{
+  uint32_t nof_ack = 0;  // srsran_uci_cfg_total_ack (uci.c:716-723)
+  for (uint32_t i = 0; i < SRSRAN_MAX_CARRIERS; i++) {
+    nof_ack += cfg->uci_cfg.ack[i].nof_acks;
+  }
+  return nof_ack > 0 || cfg->uci_cfg.cqi.ri_len > 0 || cfg->uci_cfg.cqi.data_enable;
+}
+
+int srsran_ulsch_decode(srsran_sch_t*       q,
+                        srsran_pusch_cfg_t* cfg,
+                        int16_t*            q_bits,
+                        int16_t*            g_bits,
+                        uint8_t*            c_seq,
+                        uint8_t*            data,
+                        srsran_uci_value_t* uci_data)
+{
+  (void)c_seq;
+  (void)uci_data;
+  if (!q || !q->gpu || !cfg || !q_bits || !g_bits) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  srsran_cbsegm_t s;
+  if (srsran_cbsegm(&s, (uint32_t)cfg->grant.tb.tbs)) {
+    fprintf(stderr, "[srsran_sch] Error computing segmentation for TBS=%d\n", cfg->grant.tb.tbs);
+    return SRSRAN_ERROR;
+  }
+  const uint32_t nb = cfg->grant.tb.nof_bits, Qm = srsran_mod_bits_x_symbol(cfg->grant.tb.mod);
+  cfg->K_segm       = s.C1 * s.K1 + s.C2 * s.K2;
+  if (uci_requested(cfg)) {
+    fprintf(stderr, "[srsran_sch] UCI on PUSCH (HARQ-ACK / RI / CQI) is not provided\n");
+    return SRSRAN_ERROR;
+  }
+  if (Qm == 0 || cfg->grant.nof_symb == 0 || nb % Qm) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  SchCtx* x = (SchCtx*)q->gpu;
+  if (2 * (size_t)nb > x->ul_cap) {
+    hipFree(x->d_ul);
+    x->d_ul   = nullptr;
+    x->ul_cap = 0;
+    if (hipMalloc((void**)&x->d_ul, 2 * (size_t)nb * sizeof(int16_t)) != hipSuccess) {
+      return SRSRAN_ERROR;
+    }
+    x->ul_cap = 2 * (size_t)nb;
+  }
+  int16_t* d_q = x->d_ul;
+  int16_t* d_g = x->d_ul + nb;
+  // the reference leaves the de-interleaved LLRs in g_bits (positions past rows N_symb Qm untouched)
+  if (hipMemcpyAsync(d_g, g_bits, (size_t)nb * 2, hipMemcpyHostToDevice, x->stream) != hipSuccess ||
+      hipMemcpyAsync(d_q, q_bits, (size_t)nb * 2, hipMemcpyHostToDevice, x->stream) != hipSuccess ||
+      ul_deint_launch(d_q, d_g, Qm, nb / Qm, cfg->grant.nof_symb, x->stream) != hipSuccess ||
+      hipMemcpyAsync(g_bits, d_g, (size_t)nb * 2, hipMemcpyDeviceToHost, x->stream) != hipSuccess ||
+      hipStreamSynchronize(x->stream) != hipSuccess) {
+    return SRSRAN_ERROR;
+  }
+  if (s.tbs == 0) {
+    return SRSRAN_SUCCESS;
+  }
+  srsran_pdsch_cfg_t pc;
+  memset(&pc, 0, sizeof(pc));
+  pc.grant.nof_tb        = 1;
+  pc.grant.tb[0]         = cfg->grant.tb;
+  pc.softbuffers.rx[0]   = cfg->softbuffers.rx;
+  pc.max_nof_iterations  = cfg->max_nof_iterations;
+  return dlsch_decode_sync(q, &pc, nullptr, d_g, data, 0, 1);
+}
+
+int srsran_ulsch_gpu_decode_batch(srsran_sch_t*                q,
+                                  uint32_t                     nof_tb,
+                                  const srsran_ulsch_gpu_tb_t* tbs,
+                                  int32_t*                     d_result,
+                                  float*                       d_avg_noi,
+                                  void*                        stream)
+{
+  if (!q || !q->gpu || (nof_tb && (!tbs || !d_result || !d_avg_noi))) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  std::vector<srsran_dlsch_gpu_tb_t> dl(nof_tb);
+  for (uint32_t i = 0; i < nof_tb; i++) {
+    const srsran_ulsch_gpu_tb_t& t = tbs[i];
+    if (!t.d_q_bits || !t.d_g_bits || t.Qm == 0 || t.nof_symb == 0 || t.nof_e_bits % t.Qm) {
+      return SRSRAN_ERROR_INVALID_INPUTS;
+    }
+    if (ul_deint_launch(t.d_q_bits, t.d_g_bits, t.Qm, t.nof_e_bits / t.Qm, t.nof_symb, (hipStream_t)stream) !=
+        hipSuccess) {
+      return SRSRAN_ERROR;
+    }
+    dl[i] = {t.tbs, t.Qm, t.rv, t.nof_e_bits, t.d_g_bits, t.d_data, t.softbuffer, t.new_data};
+  }
+  return srsran_dlsch_gpu_decode_batch(q, nof_tb, dl.data(), d_result, d_avg_noi, stream);
 }
 
 }  // extern "C"

@@ -58,5 +58,10 @@ hipError_t rm_rx_launch(const RmSlot* d_slots, uint32_t nslots, uint32_t max_len
 // max_tbs: the largest TBS of the batch (sizes the assembly grid)
 hipError_t tb_launch(const SchTb* d_tbs, uint32_t ntb, uint32_t max_tbs, hipStream_t stream);
 
+// UL-SCH channel de-interleaver without RI bits (sch.c:661-682, 994-1021):
+// g[(j N_symb + i) Qm + k] = q[(i rows + j) Qm + k], rows = H' / N_symb
+hipError_t ul_deint_launch(const int16_t* q, int16_t* g, uint32_t Qm, uint32_t H_prime_total, uint32_t N_symb,
+                           hipStream_t stream);
+
 }  // namespace srsran_amd
 #endif

@@ -458,4 +458,34 @@ hipError_t tb_launch(const SchTb* d_tbs, uint32_t ntb, uint32_t max_tbs, hipStre
   return hipGetLastError();
 }
 
+// ulsch_deinterleave (sch.c:994-1021) with no RI bits: ulsch_interleave_gen (sch.c:661-682) numbers
+// the input positions (i rows + j) Qm + k in (row j, column i, bit k) order and srsran_vec_lut_sis
+// (vector.c:147-152) stores g[number] = q[position] -- a transpose of the rows x N_symb matrix of
+// Qm-LLR groups.  One thread per output LLR: the stores are contiguous, the loads stride by rows Qm.
+__global__ __launch_bounds__(256) void ul_deint_kernel(const int16_t* __restrict__ q, int16_t* __restrict__ g,
+                                                       uint32_t rows, uint32_t cols, uint32_t Qm)
+{
+  const uint32_t n = rows * cols * Qm;
+  for (uint32_t o = blockIdx.x * blockDim.x + threadIdx.x; o < n; o += gridDim.x * blockDim.x) {
+    const uint32_t t = o / Qm, k = o - t * Qm;
+    const uint32_t j = t / cols, i = t - j * cols;
+    g[o]             = q[(i * rows + j) * Qm + k];
+  }
+}
+
+hipError_t ul_deint_launch(const int16_t* q, int16_t* g, uint32_t Qm, uint32_t H_prime_total, uint32_t N_symb,
+                           hipStream_t stream)
+{
+  if (N_symb == 0 || Qm == 0) {
+    return hipErrorInvalidValue;
+  }
+  const uint32_t rows = H_prime_total / N_symb, n = rows * N_symb * Qm;
+  if (n == 0) {
+    return hipSuccess;
+  }
+  StageScope timing_scope(ST_RM, stream);
+  hipLaunchKernelGGL(ul_deint_kernel, dim3((n + 255) / 256 < 2048u ? (n + 255) / 256 : 2048u), dim3(256), 0, stream, q, g, rows, N_symb, Qm);
+  return hipGetLastError();
+}
+
 }  // namespace srsran_amd

@@ -75,6 +75,56 @@ class srsran_dlsch_gpu_tb_t(ctypes.Structure):
                 ("new_data", u32)]
 
 
+SRSRAN_MAX_CARRIERS = 5
+SRSRAN_UCI_MAX_M = 9
+
+
+class srsran_uci_cfg_ack_t(ctypes.Structure):
+    _fields_ = [("pending_tb", ctypes.c_bool * SRSRAN_MAX_CODEWORDS), ("nof_acks", u32), ("ncce", u32 * SRSRAN_UCI_MAX_M),
+                ("N_bundle", u32), ("tdd_ack_M", u32), ("tdd_ack_m", u32), ("tdd_is_multiplex", ctypes.c_bool),
+                ("tpc_for_pucch", u32), ("grant_cc_idx", u32)]
+
+
+class srsran_cqi_cfg_t(ctypes.Structure):
+    _fields_ = [("data_enable", ctypes.c_bool), ("pmi_present", ctypes.c_bool), ("four_antenna_ports", ctypes.c_bool),
+                ("rank_is_not_one", ctypes.c_bool), ("subband_label_2_bits", ctypes.c_bool), ("scell_index", u32),
+                ("L", u32), ("N", u32), ("sb_idx", u32), ("type", ctypes.c_int), ("ri_len", u32)]
+
+
+class srsran_uci_cfg_t(ctypes.Structure):
+    _fields_ = [("ack", srsran_uci_cfg_ack_t * SRSRAN_MAX_CARRIERS), ("cqi", srsran_cqi_cfg_t),
+                ("is_scheduling_request_tti", ctypes.c_bool)]
+
+
+class srsran_uci_offset_cfg_t(ctypes.Structure):
+    _fields_ = [("I_offset_cqi", u32), ("I_offset_ri", u32), ("I_offset_ack", u32)]
+
+
+class srsran_pusch_grant_t(ctypes.Structure):
+    _fields_ = [("L_prb", u32), ("n_prb", u32 * 2), ("n_prb_tilde", u32 * 2), ("freq_hopping", u32), ("nof_re", u32),
+                ("nof_symb", u32), ("tb", srsran_ra_tb_t), ("last_tb", srsran_ra_tb_t), ("n_dmrs", u32),
+                ("is_rar", ctypes.c_bool)]
+
+
+class _pusch_softbuffers(ctypes.Union):
+    _fields_ = [("tx", ctypes.c_void_p), ("rx", ctypes.POINTER(srsran_softbuffer_rx_t))]
+
+
+class srsran_pusch_cfg_t(ctypes.Structure):
+    _fields_ = [("rnti", ctypes.c_uint16), ("uci_cfg", srsran_uci_cfg_t), ("uci_offset", srsran_uci_offset_cfg_t),
+                ("grant", srsran_pusch_grant_t), ("max_nof_iterations", u32), ("last_O_cqi", u32), ("K_segm", u32),
+                ("current_tx_nb", u32), ("csi_enable", ctypes.c_bool), ("enable_64qam", ctypes.c_bool),
+                ("softbuffers", _pusch_softbuffers), ("meas_time_en", ctypes.c_bool), ("meas_time_value", u32),
+                ("meas_epre_en", ctypes.c_bool), ("meas_ta_en", ctypes.c_bool), ("use_cedron_alg", ctypes.c_bool),
+                ("meas_evm_en", ctypes.c_bool)]
+
+
+class srsran_ulsch_gpu_tb_t(ctypes.Structure):
+    _fields_ = [("tbs", u32), ("Qm", u32), ("rv", u32), ("nof_e_bits", u32), ("nof_symb", u32),
+                ("d_q_bits", ctypes.c_void_p), ("d_g_bits", ctypes.c_void_p), ("d_data", ctypes.c_void_p),
+                ("softbuffer", ctypes.POINTER(srsran_softbuffer_rx_t)), ("new_data", u32)]
+
+
 _i16p = ctypes.POINTER(ctypes.c_int16)
 _u8p = ctypes.POINTER(ctypes.c_uint8)
 _bound = False
@@ -121,6 +171,10 @@ def lib():
         "srsran_dlsch_decode": ([SCH, CFG, _i16p, _u8p], ctypes.c_int),
         "srsran_dlsch_decode2": ([SCH, CFG, _i16p, _u8p, ctypes.c_int, u32], ctypes.c_int),
         "srsran_dlsch_gpu_decode_batch": ([SCH, u32, ctypes.POINTER(srsran_dlsch_gpu_tb_t), ctypes.c_void_p,
+                                           ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
+        "srsran_ulsch_decode": ([SCH, ctypes.POINTER(srsran_pusch_cfg_t), _i16p, _i16p, _u8p, _u8p, ctypes.c_void_p],
+                                ctypes.c_int),
+        "srsran_ulsch_gpu_decode_batch": ([SCH, u32, ctypes.POINTER(srsran_ulsch_gpu_tb_t), ctypes.c_void_p,
                                            ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
@@ -278,6 +332,38 @@ class Sch:
             arr[i].d_e_bits, arr[i].d_data = de, dd
             arr[i].softbuffer = ctypes.pointer(sb.s)
         return lib().srsran_dlsch_gpu_decode_batch(ctypes.byref(self.q), len(entries), arr, d_result, d_avg, stream)
+
+    def ulsch_decode(self, softbuffer, tbs, Qm, rv, nof_symb, q_bits, uci_cfg=None):
+        """srsran_ulsch_decode (no UCI) -> (ret, data bytes, g_bits, avg_iterations, K_segm)."""
+        cfg = srsran_pusch_cfg_t()
+        tb = cfg.grant.tb
+        tb.mod = MOD_FROM_QM[Qm]
+        tb.tbs = tbs
+        tb.rv = rv
+        tb.nof_bits = len(q_bits)
+        tb.enabled = True
+        cfg.grant.nof_symb = nof_symb
+        cfg.grant.nof_re = len(q_bits) // Qm
+        cfg.softbuffers.rx = ctypes.pointer(softbuffer.s)
+        if uci_cfg is not None:
+            uci_cfg(cfg.uci_cfg)
+        q = np.ascontiguousarray(q_bits, dtype=np.int16)
+        g = np.zeros_like(q)
+        data = np.zeros(tbs // 8 + 64, np.uint8)
+        ret = lib().srsran_ulsch_decode(ctypes.byref(self.q), ctypes.byref(cfg), q.ctypes.data_as(_i16p),
+                                        g.ctypes.data_as(_i16p), None, data.ctypes.data_as(_u8p), None)
+        return ret, data, g, self.last_noi(), cfg.K_segm
+
+    def ulsch_decode_batch(self, entries, d_result, d_avg, stream=None):
+        """srsran_ulsch_gpu_decode_batch. entries: (tbs, Qm, rv, nof_e_bits, nof_symb, d_q, d_g, d_data,
+        SoftbufferRx[, new_data])."""
+        arr = (srsran_ulsch_gpu_tb_t * max(len(entries), 1))()
+        for i, ent in enumerate(entries):
+            (arr[i].tbs, arr[i].Qm, arr[i].rv, arr[i].nof_e_bits, arr[i].nof_symb, arr[i].d_q_bits, arr[i].d_g_bits,
+             arr[i].d_data) = ent[:8]
+            arr[i].softbuffer = ctypes.pointer(ent[8].s)
+            arr[i].new_data = int(ent[9]) if len(ent) > 9 else 0
+        return lib().srsran_ulsch_gpu_decode_batch(ctypes.byref(self.q), len(entries), arr, d_result, d_avg, stream)
 
     def free(self):
         if self.q.gpu:

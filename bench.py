@@ -6,6 +6,8 @@ A "step" is one pass of the hot path over one batch of synthetic input:
       188 LTE sizes, 8 half-iterations, rm_turbo sub-block input layout;
   workload "k6144" (BASELINE configs[0] shape on the GPU): 1024 x 6144-bit blocks;
   workload "dlsch": srsran_dlsch_decode of C3 transport blocks (rate dematch + turbo + CRC);
+  workload "ulsch": the same TBs as PUSCH data through srsran_ulsch_gpu_decode_batch (channel
+      de-interleaver + decode_tb; SURVEY 8f rank 1, data part);
   workload "pdsch" (BASELINE configs[2], C3): the whole UE DL chain from time-domain samples --
       OFDM, CRS channel estimation, MMSE predecoding, demap/descramble/CSI, DL-SCH decode;
   workload "ldpc" (BASELINE configs[4]): NR LDPC decode (srsran_ldpc_decoder, 8-bit layered
@@ -90,7 +92,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--workload", choices=["all188", "k6144", "dlsch", "pdsch", "ldpc", "nrsch"], default="all188")
+    p.add_argument("--workload", choices=["all188", "k6144", "dlsch", "ulsch", "pdsch", "ldpc", "nrsch"], default="all188")
     p.add_argument("--snr", type=float, default=30.0, help="pdsch: AWGN SNR (dB) of the synthetic subframes")
     p.add_argument("--subframes", type=int, default=78,
                    help="dlsch / pdsch: subframes (2 TBs each) per step; 78 x 26 CBs = two full turbo-decoder rounds")
@@ -161,6 +163,7 @@ def cpu_baseline(Ks, data, iters, budget_s):
 
 # C3 grant (srsran_ra_dl_dci_to_grant probe): 100 PRB, TM3 2 CW, MCS28 64QAM, cfi 1
 C3_TBS, C3_QM, C3_BITS = 75376, 6, 86400
+UL_NSYMB = 12  # ulsch workload: N_symb^PUSCH of a normal-CP subframe without SRS
 
 
 def run_dlsch(args, torch, dist, world, rank, device):
@@ -178,20 +181,33 @@ def run_dlsch(args, torch, dist, world, rank, device):
         e = SY.dlsch_encode(C3_TBS, C3_QM, 0, C3_BITS, tb).astype(np.float32) * 2 - 1
         y = e + rng.standard_normal(e.shape).astype(np.float32) * args.sigma
         pool.append(np.trunc(100 * y).astype(np.int16))
-    host = np.stack([pool[i % args.pool] for i in range(ntb)])
+    uplink = args.workload == "ulsch"  # the same grant as a PUSCH: 100 PRB x 12 SC-FDMA symbols x 64QAM
+    if uplink:
+        from synth.ulsch_tx import ulsch_interleave
+        host = np.stack([ulsch_interleave(pool[i % args.pool], C3_QM, UL_NSYMB) for i in range(ntb)])
+    else:
+        host = np.stack([pool[i % args.pool] for i in range(ntb)])
     d_e = torch.from_numpy(host).to(device)
+    d_g = torch.zeros_like(d_e) if uplink else None
     d_data = torch.zeros((ntb, C3_TBS // 8 + 64), dtype=torch.uint8, device=device)
     d_res = torch.zeros(ntb, dtype=torch.int32, device=device)
     d_avg = torch.zeros(ntb, dtype=torch.float32, device=device)
     q = S.Sch()
     q.set_max_noi(args.iters)
     sbs = [S.SoftbufferRx(nof_prb=100) for _ in range(ntb)]
-    entries = [(C3_TBS, C3_QM, 0, C3_BITS, d_e[i].data_ptr(), d_data[i].data_ptr(), sbs[i], 1) for i in range(ntb)]
+    if uplink:
+        entries = [(C3_TBS, C3_QM, 0, C3_BITS, UL_NSYMB, d_e[i].data_ptr(), d_g[i].data_ptr(), d_data[i].data_ptr(),
+                    sbs[i], 1) for i in range(ntb)]
+    else:
+        entries = [(C3_TBS, C3_QM, 0, C3_BITS, d_e[i].data_ptr(), d_data[i].data_ptr(), sbs[i], 1) for i in range(ntb)]
     stream = torch.cuda.current_stream(device)
     sp = stream.cuda_stream
 
     def step():
-        if q.decode_batch(entries, d_res.data_ptr(), d_avg.data_ptr(), sp) != 0:
+        if uplink:
+            if q.ulsch_decode_batch(entries, d_res.data_ptr(), d_avg.data_ptr(), sp) != 0:
+                raise RuntimeError("srsran_ulsch_gpu_decode_batch failed")
+        elif q.decode_batch(entries, d_res.data_ptr(), d_avg.data_ptr(), sp) != 0:
             raise RuntimeError("srsran_dlsch_gpu_decode_batch failed")
 
     elapsed = timed_region(step, args.steps, args.warmup, world, dist, torch.cuda.synchronize, device)
@@ -235,8 +251,10 @@ def run_dlsch(args, torch, dist, world, rank, device):
         "data": f"synthetic: DL-SCH TBs (TBS {C3_TBS}, 64QAM bits as +-1, AWGN sigma {args.sigma}, LLR=trunc(100y)), "
                 f"{args.pool} distinct TBs tiled to the batch, HBM-resident",
         "config": {
-            "workload": f"dlsch C3 grant: {args.subframes} subframes x 2 TBs ({C3_TBS} bits, C=13 K=5824, "
-                        f"E={C3_BITS}), new transmissions, CRC early stop, max {args.iters} half-its",
+            "workload": (f"ulsch: {ntb} PUSCH TBs (100 PRB x {UL_NSYMB} symbols, 64QAM: {C3_TBS} bits, C=13 K=5824, "
+                         f"E={C3_BITS}; channel de-interleaver + decode_tb, no UCI)" if uplink else
+                         f"dlsch C3 grant: {args.subframes} subframes x 2 TBs ({C3_TBS} bits, C=13 K=5824, "
+                         f"E={C3_BITS})") + f", new transmissions, CRC early stop, max {args.iters} half-its",
             "tbs_per_step_per_gpu": ntb,
             "subframes_per_s": round(world * args.subframes * args.steps / elapsed, 1),
             "tb_ok_fraction": round(float((res == 0).mean()), 4),
@@ -268,7 +286,9 @@ def run_dlsch(args, torch, dist, world, rank, device):
         dt = time.perf_counter() - t0
         result["cpu_baseline"] = {"value": round(n * C3_TBS / dt / 1e6, 3), "unit": "Mbps", "cores": 1, "kind": kind,
                                   "sample": f"{n} TBs of the same pool decoded (decode_tb loop over the reference's "
-                                            f"rm_turbo/turbo/CRC code), {dt:.1f} s on 1 thread"}
+                                            f"rm_turbo/turbo/CRC code), {dt:.1f} s on 1 thread"
+                                            + ("; the UL channel de-interleaver (a permutation; sch.c is not "
+                                               "buildable here) is not in the CPU timing" if uplink else "")}
     elif rank == 0:
         result["cpu_baseline"] = None
     for sb in sbs:
@@ -742,7 +762,7 @@ def main():
     device = torch.device("cuda", local)
     if not tdec.gpu_available():
         raise RuntimeError("bench: HIP device not visible to libsrsran_4g_amd")
-    if args.workload == "dlsch":
+    if args.workload in ("dlsch", "ulsch"):
         return run_dlsch(args, torch, dist, world, rank, device)
     if args.workload == "pdsch":
         return run_pdsch(args, torch, dist, world, rank, device)

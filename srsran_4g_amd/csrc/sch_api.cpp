@@ -177,6 +177,8 @@ struct SchCtx {
   bool        used = false;
   int16_t*    d_ul = nullptr;    // srsran_ulsch_decode: q then g bits
   size_t      ul_cap = 0;
+  UlDeint*    d_uldesc = nullptr;  // srsran_ulsch_gpu_decode_batch descriptors
+  size_t      uldesc_cap = 0;
 };
 
 constexpr size_t kDataCap = (size_t)SCH_MAX_CB * SCH_SLOT_BYTES;
@@ -838,6 +840,7 @@ void srsran_sch_free(srsran_sch_t* q)
     hipHostFree(x->h_io);
     hipFree(x->d_zero);
     hipFree(x->d_ul);
+    hipFree(x->d_uldesc);
     delete x;
   }
   srsran_tdec_free(&q->decoder);
@@ -1031,6 +1034,7 @@ int srsran_ulsch_decode(srsran_sch_t*       q,
   SchCtx* x = (SchCtx*)q->gpu;
   if (2 * (size_t)nb > x->ul_cap) {
     hipFree(x->d_ul);
+    hipFree(x->d_uldesc);
     x->d_ul   = nullptr;
     x->ul_cap = 0;
     if (hipMalloc((void**)&x->d_ul, 2 * (size_t)nb * sizeof(int16_t)) != hipSuccess) {
@@ -1071,16 +1075,32 @@ int srsran_ulsch_gpu_decode_batch(srsran_sch_t*                q,
     return SRSRAN_ERROR_INVALID_INPUTS;
   }
   std::vector<srsran_dlsch_gpu_tb_t> dl(nof_tb);
+  std::vector<UlDeint>               desc(nof_tb);
+  uint32_t                           max_n = 0;
   for (uint32_t i = 0; i < nof_tb; i++) {
     const srsran_ulsch_gpu_tb_t& t = tbs[i];
     if (!t.d_q_bits || !t.d_g_bits || t.Qm == 0 || t.nof_symb == 0 || t.nof_e_bits % t.Qm) {
       return SRSRAN_ERROR_INVALID_INPUTS;
     }
-    if (ul_deint_launch(t.d_q_bits, t.d_g_bits, t.Qm, t.nof_e_bits / t.Qm, t.nof_symb, (hipStream_t)stream) !=
-        hipSuccess) {
+    const uint32_t rows = t.nof_e_bits / t.Qm / t.nof_symb;
+    desc[i]             = {t.d_q_bits, t.d_g_bits, rows, t.nof_symb, t.Qm};
+    max_n               = std::max(max_n, rows * t.nof_symb * t.Qm);
+    dl[i]               = {t.tbs, t.Qm, t.rv, t.nof_e_bits, t.d_g_bits, t.d_data, t.softbuffer, t.new_data};
+  }
+  SchCtx* x = (SchCtx*)q->gpu;
+  if (nof_tb > x->uldesc_cap) {
+    hipFree(x->d_uldesc);
+    x->d_uldesc   = nullptr;
+    x->uldesc_cap = 0;
+    if (hipMalloc((void**)&x->d_uldesc, nof_tb * sizeof(UlDeint)) != hipSuccess) {
       return SRSRAN_ERROR;
     }
-    dl[i] = {t.tbs, t.Qm, t.rv, t.nof_e_bits, t.d_g_bits, t.d_data, t.softbuffer, t.new_data};
+    x->uldesc_cap = nof_tb;
+  }
+  if (nof_tb && (hipMemcpyAsync(x->d_uldesc, desc.data(), nof_tb * sizeof(UlDeint), hipMemcpyHostToDevice,
+                                (hipStream_t)stream) != hipSuccess ||
+                 ul_deint_batch_launch(x->d_uldesc, nof_tb, max_n, (hipStream_t)stream) != hipSuccess)) {
+    return SRSRAN_ERROR;
   }
   return srsran_dlsch_gpu_decode_batch(q, nof_tb, dl.data(), d_result, d_avg_noi, stream);
 }

@@ -62,6 +62,13 @@ hipError_t tb_launch(const SchTb* d_tbs, uint32_t ntb, uint32_t max_tbs, hipStre
 // g[(j N_symb + i) Qm + k] = q[(i rows + j) Qm + k], rows = H' / N_symb
 hipError_t ul_deint_launch(const int16_t* q, int16_t* g, uint32_t Qm, uint32_t H_prime_total, uint32_t N_symb,
                            hipStream_t stream);
+struct UlDeint {
+  const int16_t* q;
+  int16_t*       g;
+  uint32_t       rows, cols, Qm;
+};
+// many TBs in one launch (grid.y = TB); d_desc on the device, max_n = the largest rows cols Qm
+hipError_t ul_deint_batch_launch(const UlDeint* d_desc, uint32_t ntb, uint32_t max_n, hipStream_t stream);
 
 }  // namespace srsran_amd
 #endif

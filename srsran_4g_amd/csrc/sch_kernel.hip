@@ -488,4 +488,26 @@ hipError_t ul_deint_launch(const int16_t* q, int16_t* g, uint32_t Qm, uint32_t H
   return hipGetLastError();
 }
 
+__global__ __launch_bounds__(256) void ul_deint_batch_kernel(const UlDeint* __restrict__ desc)
+{
+  const UlDeint d = desc[blockIdx.y];
+  const uint32_t n = d.rows * d.cols * d.Qm;
+  for (uint32_t o = blockIdx.x * blockDim.x + threadIdx.x; o < n; o += gridDim.x * blockDim.x) {
+    const uint32_t t = o / d.Qm, k = o - t * d.Qm;
+    const uint32_t j = t / d.cols, i = t - j * d.cols;
+    d.g[o]           = d.q[(i * d.rows + j) * d.Qm + k];
+  }
+}
+
+hipError_t ul_deint_batch_launch(const UlDeint* d_desc, uint32_t ntb, uint32_t max_n, hipStream_t stream)
+{
+  if (ntb == 0 || max_n == 0) {
+    return hipSuccess;
+  }
+  StageScope     timing_scope(ST_RM, stream);
+  const uint32_t bx = (max_n + 255) / 256 < 512u ? (max_n + 255) / 256 : 512u;
+  hipLaunchKernelGGL(ul_deint_batch_kernel, dim3(bx, ntb), dim3(256), 0, stream, d_desc);
+  return hipGetLastError();
+}
+
 }  // namespace srsran_amd

@@ -89,6 +89,69 @@ __global__ __launch_bounds__(256) void nr_rm_kernel(const NrRmCb* __restrict__ c
     }
     d.buf[p] = (int8_t)acc;
   };
+  if (E <= L) {
+    // Every position receives at most one LLR.  Pass 1 writes what no LLR reaches (fillers, and on
+    // new data zeros); pass 2 gives each thread a de-interleaver column m: its Qm LLRs
+    // e[m Qm .. m Qm + Qm) are contiguous, and rank j cols + m lands on position pos(rank) -- for a
+    // fixed row j the lanes' positions are consecutive, so both the loads and the stores coalesce.
+    uint32_t* b4 = reinterpret_cast<uint32_t*>(d.buf);  // soft buffers are 8-byte aligned
+    for (uint32_t q = threadIdx.x; q < Ncb / 4; q += blockDim.x) {
+      const uint32_t p0 = 4 * q;
+      if (!d.fresh && (p0 + 4 <= fi || p0 >= fe)) {
+        continue;  // no filler in this dword
+      }
+      uint32_t w = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < 4; ++k) {
+        w |= (p0 + k >= fi && p0 + k < fe ? 0x7Fu : 0u) << (8 * k);  // filler bits: infinity8 (ldpc_rm.c:327-329)
+      }
+      if (d.fresh) {
+        b4[q] = w;
+      } else {
+        for (uint32_t k = 0; k < 4; ++k) {
+          if (p0 + k >= fi && p0 + k < fe) {
+            d.buf[p0 + k] = 127;
+          }
+        }
+      }
+    }
+    for (uint32_t p = 4 * (Ncb / 4) + threadIdx.x; p < Ncb; p += blockDim.x) {
+      if (p >= fi && p < fe) {
+        d.buf[p] = 127;
+      } else if (d.fresh) {
+        d.buf[p] = 0;
+      }
+    }
+    __syncthreads();
+    // non-filler positions in circle order from k0: lap 1 runs k0 .. Ncb - 1, lap 2 runs 0 .. k0 - 1
+    const uint32_t a1   = d.k0 < fi ? fi - d.k0 : 0u;  // lap 1 before the fillers
+    const uint32_t s1   = max(d.k0, fe);               // lap 1 after them
+    const uint32_t lap1 = a1 + (Ncb > s1 ? Ncb - s1 : 0u);
+    const uint32_t b2   = min(fi, d.k0);               // lap 2 before the fillers
+    auto           pos  = [&](uint32_t i) -> uint32_t {
+      if (i < lap1) {
+        return i < a1 ? d.k0 + i : s1 + (i - a1);
+      }
+      const uint32_t i2 = i - lap1;
+      return i2 < b2 ? i2 : fe + (i2 - b2);
+    };
+    for (uint32_t m = threadIdx.x; m < cols; m += blockDim.x) {
+      int x[8];
+#pragma unroll
+      for (uint32_t j = 0; j < 8; ++j) {
+        x[j] = j < d.Qm ? (int)e[m * d.Qm + j] : 0;
+      }
+#pragma unroll
+      for (uint32_t j = 0; j < 8; ++j) {
+        if (j < d.Qm) {
+          const uint32_t p = pos(j * cols + m);
+          const int      v = d.fresh ? 0 : (int)d.buf[p];
+          d.buf[p]         = (int8_t)min(max(v + x[j], -63), 63);
+        }
+      }
+    }
+    return;
+  }
   // four positions a thread (one dword), coalesced; inside a region that neither the filler range, k0
   // nor the end of the circle splits, ranks run consecutively
   const bool     fast = E <= L && cols >= 4;

@@ -215,33 +215,44 @@ __host__ __device__ constexpr uint32_t mulmod(uint32_t a, uint32_t b, uint32_t p
   return r;
 }
 
-// x^(8 2^k) mod P for the TB CRCs: [0] CRC24A, [1] CRC16 (phy_common.h:72-74)
-struct TbCrcPow {
-  uint32_t v[2][32];
-  constexpr TbCrcPow() : v()
+// Shift factors of the TB CRCs ([0] CRC24A, [1] CRC16, phy_common.h:72-74): thread[t] = x^(8 16 t)
+// and slice[s] = x^(8 NR_TB_SLICE s) mod P -- the bytes after a thread's chunk inside its slice and
+// after the slice
+struct TbCrcShift {
+  uint32_t thread[2][NR_TB_THREADS];
+  uint32_t slice[2][16];
+  constexpr TbCrcShift() : thread(), slice()
   {
     const uint32_t polys[2] = {0x1864CFBu, 0x11021u};
     const int      ords[2]  = {24, 16};
     for (int t = 0; t < 2; t++) {
-      uint32_t p = 1u << 8;
-      for (int k = 0; k < 32; k++) {
-        v[t][k] = p;
-        p       = mulmod(p, p, polys[t], ords[t]);
+      uint32_t x128 = 1u << 8;  // x^8 -> x^128
+      for (int k = 0; k < 4; k++) {
+        x128 = mulmod(x128, x128, polys[t], ords[t]);
+      }
+      thread[t][0] = 1u;
+      for (uint32_t i = 1; i < NR_TB_THREADS; i++) {
+        thread[t][i] = mulmod(thread[t][i - 1], x128, polys[t], ords[t]);
+      }
+      const uint32_t xs = mulmod(thread[t][NR_TB_THREADS - 1], x128, polys[t], ords[t]);  // x^(8 16 256)
+      slice[t][0]       = 1u;
+      for (int i = 1; i < 16; i++) {
+        slice[t][i] = mulmod(slice[t][i - 1], xs, polys[t], ords[t]);
       }
     }
   }
 };
-__constant__ TbCrcPow c_tb_pow = TbCrcPow();
+static_assert(NR_TB_SLICE == 16 * NR_TB_THREADS, "slice = threads x 16 bytes");
+__constant__ TbCrcShift c_tb_shift = TbCrcShift();
 
-// Grid (TB, slice).  Every slice checks the blocks' flags itself; slice s copies payload bytes
-// [s NR_TB_SLICE, (s + 1) NR_TB_SLICE) -- 16 contiguous bytes per thread, gathered from the blocks'
-// saved payloads -- and folds the CRC of each thread's 16 bytes, shifted into place by
-// x^(8 bytes after them) mod P, into the TB's accumulator.  The last slice to finish compares it with
-// the CRC bits the last block carries and clears the scratch for the next launch.
+// Grid (TB, slice).  Every slice checks the blocks' flags itself.  Counted from the end of the payload,
+// thread t of slice s owns the 16 bytes that end 16 t + NR_TB_SLICE s bytes before it: it copies them
+// from the blocks' saved payloads and folds their CRC, times x^(8 16 t) (a constexpr table), into the
+// slice's sum, which thread 0 multiplies by x^(8 NR_TB_SLICE s) into the TB's accumulator.  The last
+// slice to finish compares it with the CRC bits the last block carries and clears the scratch.
 __global__ __launch_bounds__(NR_TB_THREADS) void nr_tb_kernel(const NrTb* __restrict__ tbs)
 {
   __shared__ uint32_t s_tab[256];
-  __shared__ uint32_t s_pow[32];  // x^(8 2^k) mod P
   __shared__ uint32_t s_ok, s_iters, s_crc, s_last;
   const NrTb     d     = tbs[blockIdx.x];
   const uint32_t slice = blockIdx.y;
@@ -287,27 +298,27 @@ __global__ __launch_bounds__(NR_TB_THREADS) void nr_tb_kernel(const NrTb* __rest
       }
       s_tab[v] = c & mask;
     }
-    if (threadIdx.x < 32) {
-      s_pow[threadIdx.x] = c_tb_pow.v[order == 24 ? 0 : 1][threadIdx.x];
-    }
   }
-  const uint32_t b0 = slice * NR_TB_SLICE + threadIdx.x * NR_TB_BYTES;
-  const uint32_t b1 = min(b0 + NR_TB_BYTES, nbytes);
+  // chunks are counted from the end of the payload: thread t of slice s holds the 16 bytes that end
+  // 16 t + NR_TB_SLICE s bytes before it (the first chunk of the payload may be shorter)
+  const uint32_t back = slice * NR_TB_SLICE + threadIdx.x * NR_TB_BYTES;  // bytes after the chunk
+  const uint32_t b1   = back < nbytes ? nbytes - back : 0u;
+  const uint32_t b0   = b1 > NR_TB_BYTES ? b1 - NR_TB_BYTES : 0u;
   uint8_t        v[NR_TB_BYTES];
   if (b0 < b1) {
     uint32_t r = min(b0 / cb_bytes, d.C - 1), o = b0 - r * cb_bytes;
 #pragma unroll
     for (uint32_t k = 0; k < NR_TB_BYTES; ++k) {  // independent loads, issued back to back
-      const bool in = b0 + k < b1;
+      const bool in = k < b1 - b0;
       v[k]          = in ? d.data[(size_t)r * d.data_stride + o] : 0;
-      if (++o == cb_bytes && r + 1 < d.C) {
+      if (in && ++o == cb_bytes && r + 1 < d.C) {
         o = 0;
         ++r;
       }
     }
 #pragma unroll
     for (uint32_t k = 0; k < NR_TB_BYTES; ++k) {
-      if (b0 + k < b1) {
+      if (k < b1 - b0) {
         d.payload[b0 + k] = v[k];
       }
     }
@@ -320,20 +331,18 @@ __global__ __launch_bounds__(NR_TB_THREADS) void nr_tb_kernel(const NrTb* __rest
     uint32_t crc = 0;  // srsran_crc_checksum_byte: MSB first, zero init
 #pragma unroll
     for (uint32_t k = 0; k < NR_TB_BYTES; ++k) {  // fixed trip count: v[] stays in registers
-      if (b0 + k < b1) {
+      if (k < b1 - b0) {
         crc = ((crc << 8) & mask) ^ s_tab[((crc >> (order - 8)) ^ v[k]) & 0xFFu];
       }
     }
-    for (uint32_t n = nbytes - b1, k = 0; n; n >>= 1, ++k) {  // * x^(8 (nbytes - b1))
-      if (n & 1u) {
-        crc = mulmod(crc, s_pow[k], poly, order);
-      }
-    }
+    // * x^(8 16 t): the bytes after the chunk inside the slice
+    crc = mulmod(crc, c_tb_shift.thread[order == 24 ? 0 : 1][threadIdx.x], poly, order);
     atomicXor(&s_crc, crc & mask);
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    atomicXor(&d.scratch[0], s_crc);
+    // * x^(8 NR_TB_SLICE s): the bytes after the slice
+    atomicXor(&d.scratch[0], mulmod(s_crc, c_tb_shift.slice[order == 24 ? 0 : 1][slice], poly, order) & mask);
     __threadfence();
     s_last = atomicAdd(&d.scratch[1], 1u) == nslices - 1;
   }

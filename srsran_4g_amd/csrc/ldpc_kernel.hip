@@ -490,11 +490,13 @@ __device__ __forceinline__ void cb_finish(const LdpcArgs& a, uint32_t cw, bool e
 }
 
 // a * b mod P (P of degree `order`, given with its x^order bit), Horner over b's bits
+// (b < 2^order <= 2^24: Horner over b's 24 low bits, leading zero bits leave r = 0; unrolled, so
+// the per-iteration CRC check is a straight dependency chain without loop overhead)
 __device__ __forceinline__ uint32_t mulmod(uint32_t a, uint32_t b, uint32_t poly, int order)
 {
   uint32_t r = 0;
-#pragma unroll 1
-  for (int i = order - 1; i >= 0; i--) {
+#pragma unroll
+  for (int i = 23; i >= 0; i--) {
     r = (r << 1) ^ (((b >> i) & 1u) ? a : 0u);
     r ^= ((r >> order) & 1u) ? poly : 0u;
   }

@@ -235,3 +235,35 @@ def test_batch_new_data_reuses_soft_buffers(ora, q):
             assert np.array_equal(d_p.cpu().numpy()[:tbs // 8], want[2])
             assert it == 2 or np.array_equal(want[2], pl)
     sb.free()
+
+
+# (Qm, R x 1024) of 38.214 Table 5.1.3.1-1 (MCS 0, 5, 9, 10, 13, 17, 22, 28)
+MCS_SUBSET = [(2, 120), (2, 379), (2, 679), (4, 340), (4, 490), (6, 438), (6, 616), (6, 948)]
+
+
+@pytest.mark.parametrize("n_prb", [1, 7, 25, 52, 106, 273])
+def test_prb_mcs_rv_sweep_noise_free(ora, q, n_prb):
+    """sch_nr_test.c:176-235: every (PRB count, MCS, rv), LLRs +-10 of the encoded bits, a reset soft
+    buffer per decode; rv 0 must decode.  Here every decode is also compared with the oracle."""
+    q.carrier.nof_prb = 273
+    S.lib().srsran_sch_nr_set_carrier(S.ctypes.byref(q.q), S.ctypes.byref(q.carrier))
+    rng = np.random.default_rng(n_prb)
+    for Qm, r1024 in MCS_SUBSET:
+        R = r1024 / 1024
+        n_re = 12 * 12 * n_prb
+        tbs = _tbs(n_re, R, Qm, 1)
+        G = n_re * Qm
+        t = S.tb_info(tbs, R, Qm, G, 1, nof_prb=273)
+        pl = rng.integers(0, 256, tbs // 8).astype(np.uint8)
+        enc = NrCodeblocks(t, pl)
+        for rv in range(4):
+            llr = np.where(enc.rate_match(rv) == 1, -10, 10).astype(np.int8)
+            sb = S.nr_softbuffer(max_cb=max(t.C, 1))
+            ret, crc, avg, got = q.decode(sb, tbs, R, Qm, G, 1, rv, llr)
+            st = new_state(t.C)
+            want = ora.decode(_ot(t), rv, llr, st, max_iter=6)
+            assert ret == 0 and crc == bool(want[0]) and avg == pytest.approx(want[1], abs=1e-6), (Qm, r1024, rv)
+            _check_state(sb, st, t, (Qm, r1024, rv))
+            if rv == 0:
+                assert crc and np.array_equal(got, pl), (n_prb, Qm, r1024, tbs)
+            sb.free()

@@ -1079,12 +1079,13 @@ int srsran_ulsch_gpu_decode_batch(srsran_sch_t*                q,
   uint32_t                           max_n = 0;
   for (uint32_t i = 0; i < nof_tb; i++) {
     const srsran_ulsch_gpu_tb_t& t = tbs[i];
-    if (!t.d_q_bits || !t.d_g_bits || t.Qm == 0 || t.nof_symb == 0 || t.nof_e_bits % t.Qm) {
+    if (!t.d_q_bits || !t.d_g_bits || t.Qm == 0 || t.Qm > 8 || t.nof_symb == 0 || t.nof_symb > 14 ||
+        t.nof_e_bits % t.Qm) {
       return SRSRAN_ERROR_INVALID_INPUTS;
     }
     const uint32_t rows = t.nof_e_bits / t.Qm / t.nof_symb;
     desc[i]             = {t.d_q_bits, t.d_g_bits, rows, t.nof_symb, t.Qm};
-    max_n               = std::max(max_n, rows * t.nof_symb * t.Qm);
+    max_n               = std::max(max_n, rows);
     dl[i]               = {t.tbs, t.Qm, t.rv, t.nof_e_bits, t.d_g_bits, t.d_data, t.softbuffer, t.new_data};
   }
   SchCtx* x = (SchCtx*)q->gpu;

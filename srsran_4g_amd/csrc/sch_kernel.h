@@ -67,8 +67,8 @@ struct UlDeint {
   int16_t*       g;
   uint32_t       rows, cols, Qm;
 };
-// many TBs in one launch (grid.y = TB); d_desc on the device, max_n = the largest rows cols Qm
-hipError_t ul_deint_batch_launch(const UlDeint* d_desc, uint32_t ntb, uint32_t max_n, hipStream_t stream);
+// many TBs in one launch (grid.y = TB); d_desc on the device; cols <= 14, Qm <= 8
+hipError_t ul_deint_batch_launch(const UlDeint* d_desc, uint32_t ntb, uint32_t max_rows, hipStream_t stream);
 
 }  // namespace srsran_amd
 #endif

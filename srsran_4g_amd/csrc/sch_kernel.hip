@@ -488,25 +488,40 @@ hipError_t ul_deint_launch(const int16_t* q, int16_t* g, uint32_t Qm, uint32_t H
   return hipGetLastError();
 }
 
+// Batched form, tiled through LDS: q holds N_symb rows (columns i of the interleaver) of rows Qm
+// LLRs, g is its transpose.  A workgroup takes 64 interleaver rows j of one TB: it reads, for every
+// i, the contiguous run q[(i rows + j0) Qm ..) and writes the contiguous run g[j0 N_symb Qm ..).
+constexpr uint32_t UL_TILE_J = 64, UL_MAX_SYMB = 14, UL_MAX_QM = 8;
 __global__ __launch_bounds__(256) void ul_deint_batch_kernel(const UlDeint* __restrict__ desc)
 {
-  const UlDeint d = desc[blockIdx.y];
-  const uint32_t n = d.rows * d.cols * d.Qm;
-  for (uint32_t o = blockIdx.x * blockDim.x + threadIdx.x; o < n; o += gridDim.x * blockDim.x) {
-    const uint32_t t = o / d.Qm, k = o - t * d.Qm;
-    const uint32_t j = t / d.cols, i = t - j * d.cols;
-    d.g[o]           = d.q[(i * d.rows + j) * d.Qm + k];
+  __shared__ int16_t tile[UL_MAX_SYMB * UL_TILE_J * UL_MAX_QM];
+  const UlDeint  d  = desc[blockIdx.y];
+  const uint32_t j0 = blockIdx.x * UL_TILE_J;
+  if (j0 >= d.rows) {
+    return;
+  }
+  const uint32_t nj  = min(UL_TILE_J, d.rows - j0);
+  const uint32_t run = nj * d.Qm;  // LLRs of one interleaver column inside the tile
+  for (uint32_t x = threadIdx.x; x < d.cols * run; x += blockDim.x) {
+    const uint32_t i = x / run, r = x - i * run;
+    tile[i * UL_TILE_J * UL_MAX_QM + r] = d.q[(i * d.rows + j0) * d.Qm + r];
+  }
+  __syncthreads();
+  const uint32_t row = d.cols * d.Qm;  // LLRs of one output row j
+  for (uint32_t x = threadIdx.x; x < nj * row; x += blockDim.x) {
+    const uint32_t jj = x / row, r = x - jj * row, i = r / d.Qm, k = r - i * d.Qm;
+    d.g[j0 * row + x] = tile[i * UL_TILE_J * UL_MAX_QM + jj * d.Qm + k];
   }
 }
 
-hipError_t ul_deint_batch_launch(const UlDeint* d_desc, uint32_t ntb, uint32_t max_n, hipStream_t stream)
+hipError_t ul_deint_batch_launch(const UlDeint* d_desc, uint32_t ntb, uint32_t max_rows, hipStream_t stream)
 {
-  if (ntb == 0 || max_n == 0) {
+  if (ntb == 0 || max_rows == 0) {
     return hipSuccess;
   }
-  StageScope     timing_scope(ST_RM, stream);
-  const uint32_t bx = (max_n + 255) / 256 < 512u ? (max_n + 255) / 256 : 512u;
-  hipLaunchKernelGGL(ul_deint_batch_kernel, dim3(bx, ntb), dim3(256), 0, stream, d_desc);
+  StageScope timing_scope(ST_RM, stream);
+  hipLaunchKernelGGL(ul_deint_batch_kernel, dim3((max_rows + UL_TILE_J - 1) / UL_TILE_J, ntb), dim3(256), 0, stream,
+                     d_desc);
   return hipGetLastError();
 }
 

@@ -37,6 +37,19 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 METRIC = "turbo-decoded info Mbps + PDSCH subframes/s, 20 MHz 64QAM, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# VALU ceilings (MI355X_MICROARCH.md: 256 CUs x 4 SIMD-32, a wave64 VALU instruction issues over 2 cycles,
+# 2.4 GHz): wave-instruction issue rate, and packed-int16 lane operations (v_pk_*_i16: 2 per lane)
+VALU_ISSUE_PEAK = 256 * 4 * 0.5 * 2.4e9          # 1.229e12 wave-instructions / s
+VALU_PK16_PEAK = 256 * 4 * 32 * 2 * 2.4e9        # 1.573e14 int16 operations / s
+TDEC_OPS_PER_BIT_HALF_IT = 86                    # max-log-MAP alpha + beta + LLR, turbodecoder_win.h
+
+
+def pmc_entry(workload, kernel):
+    tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        return json.load(open(tf)).get(workload, {}).get(kernel)
+    except Exception:
+        return None
 
 
 def pmc_traffic(workload, kernel, units):
@@ -108,6 +121,10 @@ def parse():
     p.add_argument("--ldpc-snr", type=float, default=1.5, help="ldpc: BPSK Es/N0 (dB) of the synthetic codewords")
     p.add_argument("--nr-tbs", type=int, default=64, help="nrsch: transport blocks per step")
     p.add_argument("--nr-snr", type=float, default=12.0, help="nrsch: Es/N0 (dB) of the bits as +-1 before int8 LLRs")
+    p.add_argument("--pdsch-steps", type=int, default=5,
+                   help="all188: timed steps of the C3 PDSCH chain reported in the same line (0 = skip)")
+    p.add_argument("--pdsch-cpu-seconds", type=float, default=4.0, help="all188: CPU baseline budget of the PDSCH part")
+    p.add_argument("--cpu-worker", type=int, default=None, help=argparse.SUPPRESS)
     return p.parse_args()
 
 
@@ -127,38 +144,114 @@ def make_inputs(Ks, pool, batch, rng, torch, device):
     return data
 
 
-def cpu_baseline(Ks, data, iters, budget_s):
-    """Reference decoder (oracle/_ref, compiled from /root/reference) on one host core.
+def cpu_threads():
+    """Host threads of this job's CPU share: OMP_NUM_THREADS where the pool sets it (16 on the GPU
+    box, whose nproc counts the whole machine), else the affinity mask."""
+    try:
+        n = int(os.environ.get("OMP_NUM_THREADS", "0"))
+    except ValueError:
+        n = 0
+    return max(1, min(n or len(os.sched_getaffinity(0)), 16))
 
-    Bounded sample: repeated passes over the pool code blocks of the workload's
-    sizes until ~budget_s seconds of CPU work; reports decoded info Mbps."""
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _tdec_decoder():
     from oracle import Oracle, Reference, ref_available
-
     kind = "reference" if ref_available() else "port"
-    dec = Reference() if kind == "reference" else Oracle()
-    bits = 0
-    n_cb = 0
+    return kind, (Reference() if kind == "reference" else Oracle())
+
+
+def cpu_worker(args):
+    """--cpu-worker SEED: one host process of the all-cores CPU baseline (no torch, no GPU): decodes
+    its own AWGN pool of every workload size with the reference decoder for --cpu-seconds."""
+    from synth import synth as SY
+    from srsran_4g_amd.tdec import CB_SIZES
+
+    Ks = list(CB_SIZES) if args.workload == "all188" else [6144]
+    rng = np.random.default_rng(args.cpu_worker)
+    pool = {K: SY.natural_to_sb(K, SY.make_llrs(K, 4.0, rng, args.pool)[1]) for K in Ks}
+    _, dec = _tdec_decoder()
+    bits = n_cb = 0
     t0 = time.perf_counter()
-    passes = 0
+    while time.perf_counter() - t0 < args.cpu_seconds:
+        for K in Ks:
+            for x in pool[K]:
+                dec.tdec_run(K, x, True, args.iters)
+                bits += K
+                n_cb += 1
+    print(json.dumps({"bits": bits, "blocks": n_cb, "dt": time.perf_counter() - t0}), flush=True)
+
+
+def cpu_baseline(Ks, data, iters, budget_s, workload):
+    """Reference decoder (oracle/_ref, compiled from /root/reference) on the host cores of this job.
+
+    Bounded samples: (1) one thread in this process, repeated passes over the pool code blocks of
+    the workload's sizes for ~budget_s/2 s; (2) the all-cores aggregate: one child process per core (started
+    as children, no exec of this GPU process), each decoding its own pool for ~budget_s/2 s.
+    `value` is the aggregate; decoded info Mbps."""
+    import subprocess
+
+    kind, dec = _tdec_decoder()
+    bits = n_cb = passes = 0
+    half = budget_s / 2
+    t0 = time.perf_counter()
     while True:
         for K in Ks:
             sb = data[K][2]
-            for x in sb:
+            for i, x in enumerate(sb):
                 dec.tdec_run(K, x, True, iters)
                 bits += K
                 n_cb += 1
         passes += 1
-        if time.perf_counter() - t0 >= budget_s:
+        if time.perf_counter() - t0 >= half:
             break
     dt = time.perf_counter() - t0
-    return {
-        "value": round(bits / dt / 1e6, 3),
+    one = bits / dt / 1e6
+    n = cpu_threads()
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--cpu-worker", str(1000 + i),
+                               "--cpu-seconds", str(half), "--iters", str(iters), "--workload", workload],
+                              stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, env=env, cwd=ROOT) for i in range(n)]
+    agg_bits, agg_dt, ok = 0, 0.0, 0
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=half + 120)
+            r = json.loads(out.decode().strip().splitlines()[-1])
+            agg_bits += r["bits"]
+            agg_dt = max(agg_dt, r["dt"])
+            ok += 1
+        except Exception:
+            p.kill()
+    agg = agg_bits / agg_dt / 1e6 if ok else None
+    res = {
+        "value": round(agg, 3) if agg else round(one, 3),
         "unit": "Mbps",
-        "cores": 1,
+        "cores": ok if agg else 1,
         "kind": kind,
-        "sample": f"{passes} pass(es) over {len(data[Ks[0]][2])} AWGN blocks of each of {len(Ks)} size(s), "
-                  f"{n_cb} blocks, {iters} half-its, SB layout, {dt:.1f} s on 1 thread",
+        "cpu_model": cpu_model(),
+        "nproc": os.cpu_count(),
+        "value_1thread": round(one, 3),
+        "sample": f"all-cores: {ok} processes x {half:.0f} s, each over its own {len(data[Ks[0]][2])} AWGN blocks of "
+                  f"each of {len(Ks)} size(s); 1 thread: {passes} pass(es), {n_cb} blocks, {dt:.1f} s; "
+                  f"{iters} half-its, SB layout",
     }
+    return res
+
+
+def ref_outputs(Ks, data, iters):
+    """The reference decoder's output for every distinct pool block of every size (the timed batch
+    tiles these blocks), for the post-timing check of the GPU batch."""
+    _, dec = _tdec_decoder()
+    return {K: np.stack([dec.tdec_run(K, x, True, iters) for x in data[K][2]]) for K in Ks}
 
 
 # C3 grant (SURVEY 8, srsran_ra_dl_dci_to_grant probe): 100 PRB, TM3 2 CW, MCS28 64QAM, cfi 1
@@ -314,16 +407,20 @@ def stage_bytes(nsf, nre_sum, ntb):
         "chest_kernel": nsf * ports * nrx * (4 * nre_row * 8 + nre_row * 8),
         "predecode_batch_kernel": nre_sum * (nrx * 8 + 4 + 2 * 8 + 2 * 4) + nsf * ports * nrx * nre_row * 8,
         "llr_batch_kernel": nre_sum * 2 * (8 + 4 + 6 * 2),
-        "rm_rx_kernel": ntb * (C3_BITS * 2 + C * (3 * (K + 32) + 12) * 2),
+        "rm_rx_lds_kernel": ntb * (C3_BITS * 2 + C * (3 * (K + 32) + 12) * 2),
         "tdec_kernel": ntb * C * ((3 * (K + 32) + 12) * 2 + K // 8),
-        "tb_kernel": ntb * (C * K // 8 + C3_TBS // 8),
+        "tb_assemble_kernel": ntb * (C * K // 8 + C3_TBS // 8),
     }
 
 
-def run_pdsch(args, torch, dist, world, rank, device):
+def run_pdsch(args, torch, dist, world, rank, device, steps=None, warmup=None, cpu_seconds=None, emit=True):
     """UE DL chain on C3 subframes: per step `subframes` subframes of 2 rx x 30720 cf32 samples
     -> 2 TBs each (TBS 75376, 64QAM, TM3 CDD 2x2, CFI 1), new transmissions, at most `iters`
-    half-iterations with CRC early stop.  Value = decoded PDSCH info Mbps; also subframes/s."""
+    half-iterations with CRC early stop.  Value = decoded PDSCH info Mbps; also subframes/s.
+    emit=False: return the result (the default all188 line embeds it) instead of printing it."""
+    steps = args.steps if steps is None else steps
+    warmup = args.warmup if warmup is None else warmup
+    cpu_seconds = args.cpu_seconds if cpu_seconds is None else cpu_seconds
     from synth import synth as SY
     from srsran_4g_amd import prof
     from srsran_4g_amd import sch as S
@@ -341,6 +438,7 @@ def run_pdsch(args, torch, dist, world, rank, device):
     nsf = args.subframes
     host = np.stack([pool[b % 10][1] for b in range(nsf)])
     d_x = torch.from_numpy(np.ascontiguousarray(host).view(np.float32)).to(device)
+    U.use_standard_symbol_size(True)  # C3 is quoted at N = 2048 (standard rates, as srsUE runs)
     ue = U.UeDl(U.cell(100, 2, cell_id), 2)
     ue.cfg.cfg.pdsch.max_nof_iterations = args.iters
     sbs = [[S.SoftbufferRx(nof_prb=100) for _ in range(2)] for _ in range(nsf)]
@@ -358,23 +456,34 @@ def run_pdsch(args, torch, dist, world, rank, device):
         if ue.gpu_decode_batch(arr, d_x.data_ptr(), d_res.data_ptr(), d_avg.data_ptr(), 0.0, sp) != 2 * nsf:
             raise RuntimeError("srsran_ue_dl_gpu_decode_batch failed")
 
-    elapsed = timed_region(step, args.steps, args.warmup, world, dist, torch.cuda.synchronize, device)
+    elapsed = timed_region(step, steps, warmup, world, dist, torch.cuda.synchronize, device)
+    # PCIe-inclusive rate (never `value`): the time samples start in pinned host memory and are
+    # copied H2D on the launch stream before every step
+    h_x = torch.from_numpy(np.ascontiguousarray(host).view(np.float32)).pin_memory()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(steps):
+        with torch.cuda.stream(stream):
+            d_x.copy_(h_x, non_blocking=True)
+        step()
+    torch.cuda.synchronize()
+    h2d_s = (time.perf_counter() - t1) / steps
     # host enqueue cost of one step (the API builds descriptors and launches asynchronously)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         step()
-    host_ms = (time.perf_counter() - t1) / args.steps * 1e3
+    host_ms = (time.perf_counter() - t1) / steps * 1e3
     torch.cuda.synchronize()
     res = d_res.cpu().numpy()
     avg = d_avg.cpu().numpy()
     pl = d_pl.cpu().numpy()
     ok = sum(int(np.array_equal(pl[b, q, : C3_TBS // 8], pool[b % 10][3][q])) for b in range(nsf) for q in range(2))
-    value = world * nsf * 2 * C3_TBS * args.steps / elapsed / 1e6
+    value = world * nsf * 2 * C3_TBS * steps / elapsed / 1e6
 
     # per-stage kernel durations from HIP events on the launch streams (library-side), same batch
     prof.enable(True)
-    nrep = max(1, min(args.steps, 3))
+    nrep = max(1, min(steps, 3))
     for _ in range(nrep):
         step()
     torch.cuda.synchronize()
@@ -393,15 +502,15 @@ def run_pdsch(args, torch, dist, world, rank, device):
     d = per_stage[dom]
     bytes_per_launch = sb[dom] / d["launches_per_step"]
     achieved = bytes_per_launch / (d["avg_launch_ms"] * 1e-3) / 1e9
-    traffic = pmc_traffic(args.workload, dom, nsf * 26) if dom == "tdec_kernel" else None
+    traffic = pmc_traffic("pdsch", dom, nsf * 26) if dom == "tdec_kernel" else None
     result = {
         "metric": METRIC,
         "value": round(value, 2),
         "unit": "Mbps",
         "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": round(elapsed / steps * 1e3, 3),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -412,7 +521,8 @@ def run_pdsch(args, torch, dist, world, rank, device):
             "workload": f"pdsch C3: {nsf} subframes x (2 rx x {SF_LEN} cf32 samples -> OFDM 2048 -> CRS chest -> "
                         f"MMSE CDD 2x2 -> 64QAM LLR -> 2 TBs x {C3_TBS} bits), CFI 1, max {args.iters} half-its",
             "subframes_per_step_per_gpu": nsf,
-            "subframes_per_s": round(world * nsf * args.steps / elapsed, 1),
+            "subframes_per_s": round(world * nsf * steps / elapsed, 1),
+            "subframes_per_s_h2d_inclusive": round(world * nsf / h2d_s, 1),
             "tb_ok_fraction": round(ok / (2 * nsf), 4),
             "avg_half_iterations": round(float(avg.mean()), 3),
             "cell_id": cell_id,
@@ -435,21 +545,24 @@ def run_pdsch(args, torch, dist, world, rank, device):
     }
     if (res != 0).any():
         result["config"]["tb_fail"] = int((res != 0).sum())
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        result["cpu_baseline"] = pdsch_cpu_baseline(pool, args)
+    if rank == 0 and world == 1 and cpu_seconds > 0:
+        result["cpu_baseline"] = pdsch_cpu_baseline(pool, args, cpu_seconds)
     elif rank == 0:
         result["cpu_baseline"] = None
     ue.free()
     for pair in sbs:
         for s_ in pair:
             s_.free()
+    if not emit:
+        return result
     if world > 1:
         dist.destroy_process_group()
     if rank == 0:
         print(json.dumps(result), flush=True)
+    return result
 
 
-def pdsch_cpu_baseline(pool, args):
+def pdsch_cpu_baseline(pool, args, budget_s):
     """The reference's compiled PDSCH pieces (oracle/_ref: predecoding, demod_soft, sequence, DL-SCH
     decode_tb over rm_turbo/turbodecoder/crc) with the oracle's C channel estimator and numpy's FFT
     (FFTW is not in the image) on one host thread, over the same subframes."""
@@ -468,7 +581,7 @@ def pdsch_cpu_baseline(pool, args):
     h = Hybrid()
     n = 0
     t0 = time.perf_counter()
-    while time.perf_counter() - t0 < args.cpu_seconds:
+    while time.perf_counter() - t0 < budget_s:
         tti, x, nre, _ = pool[n % len(pool)]
         g, ce, st = PC.fft_estimate(ora, x, 100, 1, 2, tti)
         PC.pdsch_decode(h, g, ce, st["noise"], 100, 1, 2, tti, 1, 0x1234, [C3_TBS, C3_TBS], [C3_QM, C3_QM], [0, 0],
@@ -748,6 +861,8 @@ def run_nrsch(args, torch, dist, world, rank, device):
 
 def main():
     args = parse()
+    if args.cpu_worker is not None:
+        return cpu_worker(args)
     import torch
     import torch.distributed as dist
 
@@ -834,14 +949,57 @@ def main():
         dom = "tdec_multi_kernel<16>"
         avg_ms = float(np.mean(ms16))
         bytes_per_launch = sum(args.batch * algo_bytes(Ks[i]) for i in k16)
-        traffic = pmc_traffic(args.workload, dom, args.batch * len(k16))
+        dom_units = args.batch * len(k16)
+        traffic = pmc_traffic(args.workload, dom, dom_units)
     else:
         dom = max(per_kernel, key=lambda n: per_kernel[n]["ms"])
         dk = per_kernel[dom]
         avg_ms = dk["ms"] / dk["launches"]
         bytes_per_launch = dk["bytes"] / dk["launches"]
-        traffic = pmc_traffic(args.workload, dom, args.batch)
+        dom_units = args.batch
+        k16 = [0]
+        traffic = pmc_traffic(args.workload, dom, dom_units)
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
+    # VALU view of the same launch (the binding ceiling of the turbo decoder):
+    #  * valu_issue_frac: VALU wave-instructions per launch (rocprofv3 SQ_INSTS_VALU, committed in
+    #    profiles/pmc_traffic.json, scaled to this batch) / (launch time x issue peak)
+    #  * valu_alg_frac: SURVEY 8d's 86 packed-int16 ops per bit and half-iteration / the pk-int16 peak
+    dom_bits = sum(args.batch * Ks[i] for i in k16) if len(Ks) > 1 else args.batch * Ks[0]
+    ent = pmc_entry(args.workload, dom)
+    valu_insts = ent["valu_insts"] * dom_units / ent["units"] if ent and "valu_insts" in ent else None
+    valu = {
+        "valu_issue_frac": round(valu_insts / (avg_ms * 1e-3) / VALU_ISSUE_PEAK, 4) if valu_insts else None,
+        "valu_insts_per_launch": int(valu_insts) if valu_insts else None,
+        "valu_alg_frac": round(TDEC_OPS_PER_BIT_HALF_IT * dom_bits * args.iters / (avg_ms * 1e-3) / VALU_PK16_PEAK, 4),
+        "valu_issue_peak": VALU_ISSUE_PEAK,
+        "valu_pk16_peak": VALU_PK16_PEAK,
+    }
+
+    # 16 half-iterations (SURVEY 8d "also 16"): the same batch, events on the launch stream
+    ms_16 = []
+    for _ in range(2):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        if len(Ks) > 1:
+            tdec.gpu_run_multi(groups[0], groups[1], groups[2], True, groups[3], groups[4], 16, sp)
+        else:
+            tdec.gpu_run_batch(Ks[0], groups[1][0], groups[2][0], True, groups[3][0], args.batch, 16, sp)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        ms_16.append(e0.elapsed_time(e1))
+    mbps_16 = world * bits_per_step / (min(ms_16) * 1e-3) / 1e6
+
+    # output check: re-run the timed batch and compare every decoded block with the reference
+    # decoder's output for its pool block (oracle/_ref, or the port where /root/reference is absent)
+    step()
+    torch.cuda.synchronize()
+    want = ref_outputs(Ks, data, args.iters)
+    bad = 0
+    for K in Ks:
+        got = data[K][1].cpu().numpy()
+        exp = want[K][np.arange(args.batch) % args.pool]
+        bad += int((got != exp).any(axis=1).sum())
 
     result = {
         "metric": METRIC,
@@ -866,7 +1024,7 @@ def main():
             "info_bits_per_step_per_gpu": bits_per_step,
             "parallelism": f"cb-sharded x{world}",
         },
-        "roofline": {
+        "roofline": dict({
             "bound": "hbm",
             "kernel": dom,
             "achieved": round(achieved, 2),
@@ -876,8 +1034,11 @@ def main():
             "traffic": traffic,
             "avg_launch_ms": round(avg_ms, 4),
             "algo_bytes_per_launch": int(bytes_per_launch),
-        },
+        }, **valu),
         "per_kernel_mbps": {n: round(d["bits"] / (d["ms"] * 1e-3) / 1e6, 1) for n, d in per_kernel.items()},
+        "mbps_16_half_its": round(mbps_16, 1),
+        "output_check": {"blocks": args.batch * len(Ks), "mismatched": bad,
+                         "against": "reference decoder (oracle/_ref) on each pool block"},
     }
     if args.workload == "all188":
         k = [e for e in events if e[0] == 6144]
@@ -886,10 +1047,33 @@ def main():
             result["k6144_mbps"] = round(args.batch * 6144 / (ms * 1e-3) / 1e6, 1)
 
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        result["cpu_baseline"] = cpu_baseline(Ks if args.workload == "k6144" else Ks, data, args.iters,
-                                              args.cpu_seconds)
+        result["cpu_baseline"] = cpu_baseline(Ks, data, args.iters, args.cpu_seconds, args.workload)
     elif rank == 0:
         result["cpu_baseline"] = None
+
+    if args.workload == "all188" and args.pdsch_steps > 0:
+        # the PDSCH half of the metric (BASELINE configs[2], C3): the whole UE DL chain, same line
+        del data
+        torch.cuda.empty_cache()
+        pd = run_pdsch(args, torch, dist, world, rank, device, steps=args.pdsch_steps, warmup=2,
+                       cpu_seconds=args.pdsch_cpu_seconds if args.cpu_seconds > 0 else 0, emit=False)
+        result["pdsch_subframes_per_s"] = pd["config"]["subframes_per_s"]
+        result["pdsch"] = {
+            "workload": pd["config"]["workload"],
+            "subframes_per_s": pd["config"]["subframes_per_s"],
+            "subframes_per_s_h2d_inclusive": pd["config"]["subframes_per_s_h2d_inclusive"],
+            "mbps": pd["value"],
+            "ms_per_step": pd["ms_per_step"],
+            "steps": pd["steps"],
+            "tb_ok_fraction": pd["config"]["tb_ok_fraction"],
+            "avg_half_iterations": pd["config"]["avg_half_iterations"],
+            "roofline": pd["roofline"],
+            "stages": pd["stages"],
+            "chain_bytes_per_sf": pd["chain_bytes_per_sf"],
+            "chain_roofline_frac": round(pd["config"]["subframes_per_s"] * pd["chain_bytes_per_sf"]
+                                         / (world * HBM_PEAK_GBS * 1e9), 5),
+            "cpu_baseline": pd.get("cpu_baseline"),
+        }
 
     if world > 1:
         dist.destroy_process_group()

@@ -60,9 +60,17 @@ typedef struct {
   uint32_t            non_mbsfn_region;
 } srsran_dl_sf_cfg_t;
 
-int srsran_symbol_sz(uint32_t nof_prb);              /* phy_common.c:361-385 (standard rates: powers of 2) */
-int srsran_symbol_sz_power2(uint32_t nof_prb);       /* phy_common.c:340-359 */
-void srsran_use_standard_symbol_size(bool enabled);  /* phy_common.c:322-325 (only `true` is provided) */
+/* FFT size per bandwidth.  As in the reference (phy_common.c:31-35), the default is the
+ * non-standard 3/4 sampling rate (100 PRB -> 1536, 50 -> 768, 25 -> 384); srsUE and the
+ * reference tests switch to power-of-two sizes with srsran_use_standard_symbol_size(true).
+ * Both settings are implemented (mixed-radix FFT, radix 8/4/3/2). */
+int  srsran_symbol_sz(uint32_t nof_prb);              /* phy_common.c:361-385 */
+int  srsran_symbol_sz_power2(uint32_t nof_prb);       /* phy_common.c:340-359 */
+void srsran_use_standard_symbol_size(bool enabled);  /* phy_common.c:322-325 */
+bool srsran_symbol_size_is_standard(void);           /* phy_common.c:327-330 */
+int  srsran_sampling_freq_hz(uint32_t nof_prb);      /* phy_common.c:332-338 */
+int  srsran_nof_prb(uint32_t symbol_sz);             /* phy_common.c:387-419 */
+bool srsran_symbol_sz_isvalid(uint32_t symbol_sz);   /* phy_common.c:421-437 */
 
 /* ---------------- chest_dl.h ---------------- */
 typedef enum { SRSRAN_NOISE_ALG_REFS = 0, SRSRAN_NOISE_ALG_PSS, SRSRAN_NOISE_ALG_EMPTY } srsran_chest_dl_noise_alg_t;

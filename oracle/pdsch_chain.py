@@ -24,8 +24,11 @@ MOD = {1: 0, 2: 1, 4: 2, 6: 3, 8: 4}
 RHO_TABLE = ((1.0, 4.0 / 5, 3.0 / 5, 2.0 / 5), (5.0 / 4, 1.0, 3.0 / 4, 1.0 / 2))  # pdsch.c:44-46
 
 
-def symbol_sz(nof_prb):
-    for p, n in ((6, 128), (15, 256), (25, 512), (52, 1024), (79, 1536), (110, 2048)):
+def symbol_sz(nof_prb, standard=True):
+    """srsran_symbol_sz (phy_common.c:340-385): standard rates = power-of-two sizes (1536 for 15 MHz);
+    otherwise the reference's default 3/4 rates (384 / 768 / 1536 for 25 / 50 / 100 PRB)."""
+    sizes = (512, 1024, 1536, 2048) if standard else (384, 768, 1024, 1536)
+    for p, n in zip((6, 15, 25, 52, 79, 110), (128, 256) + sizes):
         if nof_prb <= p:
             return n
     raise ValueError(nof_prb)

@@ -19,7 +19,9 @@ using namespace srsran_amd;
 
 namespace {
 
-bool g_standard_rates = true;
+// phy_common.c:31-35: non-standard (3/4) sampling rates unless built with FORCE_STANDARD_RATE;
+// srsUE and the reference tests opt in with srsran_use_standard_symbol_size(true).
+bool g_standard_rates = false;
 
 // LTE Gold sequence c(n), n = 0..len-1 (36.211 7.2, Nc = 1600)
 void gold(uint32_t c_init, uint8_t* c, uint32_t len)
@@ -108,6 +110,30 @@ int srsran_symbol_sz(uint32_t nof_prb)
 }
 
 void srsran_use_standard_symbol_size(bool enabled) { g_standard_rates = enabled; }
+
+bool srsran_symbol_size_is_standard(void) { return g_standard_rates; }
+
+int srsran_sampling_freq_hz(uint32_t nof_prb)
+{
+  const int n = srsran_symbol_sz(nof_prb);
+  return n < 0 ? SRSRAN_ERROR : 15000 * n;
+}
+
+int srsran_nof_prb(uint32_t symbol_sz)  // phy_common.c:387-430
+{
+  static const uint32_t kStd[6] = {128, 256, 512, 1024, 1536, 2048};
+  static const uint32_t kNon[6] = {128, 256, 384, 768, 1024, 1536};
+  static const int      kPrb[6] = {6, 15, 25, 50, 75, 100};
+  const uint32_t*       t       = g_standard_rates ? kStd : kNon;
+  for (int i = 0; i < 6; i++) {
+    if (t[i] == symbol_sz) {
+      return kPrb[i];
+    }
+  }
+  return SRSRAN_ERROR;
+}
+
+bool srsran_symbol_sz_isvalid(uint32_t symbol_sz) { return srsran_nof_prb(symbol_sz) > 0; }  // phy_common.c:421-437
 
 int srsran_chest_dl_init(srsran_chest_dl_t* q, uint32_t max_prb, uint32_t nof_rx_antennas)
 {

@@ -15,8 +15,11 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <map>
+#include <mutex>
 #include <vector>
 
+#include "devkey.h"
 #include "llr_kernel.h"
 #include "stage_timing.h"
 
@@ -50,11 +53,15 @@ __host__ __device__ inline uint32_t apply(const uint32_t* cols, uint32_t v)
 
 hipError_t gold_tables_init()
 {
-  static bool       done = false;
-  static hipError_t err  = hipSuccess;
-  if (done) {
-    return err;
+  // built once per device (kGold is the current device's copy of the constant)
+  static std::mutex                mu;
+  static std::map<int, hipError_t> done;
+  std::lock_guard<std::mutex>      lk(mu);
+  const int                        dev = cur_dev();
+  if (done.count(dev)) {
+    return done[dev];
   }
+  hipError_t err = hipSuccess;
   // powers A^(2^k) of both LFSR transition matrices (as columns), k < JUMP_BITS
   std::vector<uint32_t> pw(2 * JUMP_BITS * 31);
   auto P = [&](int l, int k) { return &pw[(l * JUMP_BITS + k) * 31]; };
@@ -104,7 +111,7 @@ hipError_t gold_tables_init()
   if (err == hipSuccess) {
     err = hipMemcpyToSymbol(HIP_SYMBOL(kGold), &t, sizeof(t));
   }
-  done = true;
+  done[dev] = err;
   return err;
 }
 

@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "../../include/srsran_ue_dl.h"
+#include "devkey.h"
 #include "ofdm_kernel.h"
 
 using namespace srsran_amd;
@@ -20,12 +21,13 @@ using namespace srsran_amd;
 namespace {
 
 std::mutex                    g_tw_mu;
-std::map<uint32_t, float2*>   g_tw;  // per FFT size: exp(-2 pi i m / N)
+std::map<std::pair<int, uint32_t>, float2*> g_tw;  // per (device, FFT size): exp(-2 pi i m / N)
 
 const float2* twiddles(uint32_t N)
 {
   std::lock_guard<std::mutex> lk(g_tw_mu);
-  auto                        it = g_tw.find(N);
+  const auto                  key = std::make_pair(cur_dev(), N);
+  auto                        it  = g_tw.find(key);
   if (it != g_tw.end()) {
     return it->second;
   }
@@ -39,7 +41,7 @@ const float2* twiddles(uint32_t N)
       hipMemcpy(d, h.data(), N * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess) {
     return nullptr;
   }
-  g_tw[N] = d;
+  g_tw[key] = d;
   return d;
 }
 

@@ -7,9 +7,11 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <map>
 #include <mutex>
 
 #include "../../include/srsran_phch.h"
+#include "devkey.h"
 #include "eq_kernel.h"
 #include "llr_kernel.h"
 #include "pdsch_internal.h"
@@ -19,13 +21,14 @@ using namespace srsran_amd;
 namespace {
 
 std::mutex g_mu;
-struct Ctx {
+struct Ctx {  // host-synchronous stage APIs: one stream + scratch per device
   hipStream_t stream = nullptr;
   void*       d_a    = nullptr;
   size_t      a_cap  = 0;
   void*       d_b    = nullptr;
   size_t      b_cap  = 0;
-} g_ctx;
+};
+std::map<int, Ctx> g_ctxs;
 
 bool grow(void** p, size_t* cap, size_t need)
 {
@@ -43,7 +46,7 @@ bool grow(void** p, size_t* cap, size_t need)
   return true;
 }
 
-bool ctx_ready()
+bool ctx_ready(Ctx& g_ctx)
 {
   if (g_ctx.stream) {
     return true;
@@ -120,7 +123,8 @@ int srsran_demod_soft_demodulate_s(srsran_mod_t modulation, const cf_t* symbols,
     return 0;
   }
   std::lock_guard<std::mutex> lk(g_mu);
-  if (!ctx_ready() || !grow(&g_ctx.d_a, &g_ctx.a_cap, (size_t)nsymbols * sizeof(cf_t)) ||
+  Ctx&                        g_ctx = g_ctxs[cur_dev()];
+  if (!ctx_ready(g_ctx) || !grow(&g_ctx.d_a, &g_ctx.a_cap, (size_t)nsymbols * sizeof(cf_t)) ||
       !grow(&g_ctx.d_b, &g_ctx.b_cap, (size_t)nsymbols * q * sizeof(int16_t))) {
     return -1;
   }
@@ -139,8 +143,9 @@ void srsran_sequence_apply_s(const int16_t* in, int16_t* out, uint32_t length, u
     return;
   }
   std::lock_guard<std::mutex> lk(g_mu);
+  Ctx&                        g_ctx = g_ctxs[cur_dev()];
   const size_t bytes = (size_t)length * sizeof(int16_t);
-  if (!ctx_ready() || !grow(&g_ctx.d_a, &g_ctx.a_cap, bytes) || !grow(&g_ctx.d_b, &g_ctx.b_cap, bytes)) {
+  if (!ctx_ready(g_ctx) || !grow(&g_ctx.d_a, &g_ctx.a_cap, bytes) || !grow(&g_ctx.d_b, &g_ctx.b_cap, bytes)) {
     return;
   }
   hipMemcpyAsync(g_ctx.d_a, in, bytes, hipMemcpyHostToDevice, g_ctx.stream);
@@ -190,7 +195,8 @@ int srsran_predecoding_type(cf_t*              y[4],
   const size_t nin = (size_t)nof_rxant * (1 + nof_ports);  // y + h
   const size_t nout = (size_t)nof_layers;
   std::lock_guard<std::mutex> lk(g_mu);
-  if (!ctx_ready() || !grow(&g_ctx.d_a, &g_ctx.a_cap, nin * n * sizeof(cf_t)) ||
+  Ctx&                        g_ctx = g_ctxs[cur_dev()];
+  if (!ctx_ready(g_ctx) || !grow(&g_ctx.d_a, &g_ctx.a_cap, nin * n * sizeof(cf_t)) ||
       !grow(&g_ctx.d_b, &g_ctx.b_cap, nout * n * (sizeof(cf_t) + sizeof(float)))) {
     return SRSRAN_ERROR;
   }

@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "../../include/srsran_sch.h"
+#include "devkey.h"
 #include "sch_kernel.h"
 #include "tdec_kernel.h"
 
@@ -72,7 +73,7 @@ struct InvTable {
   uint32_t  len = 0;  // soft buffer positions of the layout
   uint32_t  N   = 0;  // 3K + 12
 };
-std::map<uint32_t, InvTable> g_inv;
+std::map<uint64_t, InvTable> g_inv;  // (device, cb_idx, rv, layout)
 
 uint32_t rx_subblocks(uint32_t K, bool tdec_layout)
 {
@@ -83,7 +84,7 @@ bool inv_table(uint32_t cb_idx, uint32_t rv, bool tdec_layout, InvTable* out)
 {
   const uint32_t              K   = (uint32_t)srsran_cbsegm_cbsize(cb_idx);
   const uint32_t              nsb = rx_subblocks(K, tdec_layout);
-  const uint32_t              key = (cb_idx * 4 + rv) * 2 + (nsb ? 1 : 0);
+  const uint64_t              key = ((uint64_t)cur_dev() << 32) | ((cb_idx * 4 + rv) * 2 + (nsb ? 1 : 0));
   std::lock_guard<std::mutex> lk(g_mu);
   auto                        it = g_inv.find(key);
   if (it != g_inv.end()) {
@@ -583,14 +584,15 @@ void srsran_rm_turbo_free_tables(void) {}
 
 namespace {
 std::mutex g_rm_mu;
-struct RmCtx {
+struct RmCtx {  // one per device: the host-synchronous srsran_rm_turbo_rx_lut_ scratch
   hipStream_t stream = nullptr;
   int16_t*    d_in   = nullptr;
   size_t      in_cap = 0;
   int16_t*    d_out  = nullptr;
   RmSlot*     d_slot = nullptr;
   uint8_t*    d_zero = nullptr;
-} g_rm;
+};
+std::map<int, RmCtx> g_rm;
 }  // namespace
 
 int srsran_rm_turbo_rx_lut_(int16_t* input,
@@ -612,7 +614,7 @@ int srsran_rm_turbo_rx_lut_(int16_t* input,
     return SRSRAN_ERROR;
   }
   std::lock_guard<std::mutex> lk(g_rm_mu);
-  RmCtx&                      c = g_rm;
+  RmCtx&                      c = g_rm[cur_dev()];
   if (!c.stream) {
     if (hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc((void**)&c.d_out, (size_t)SOFTBUFFER_SIZE * sizeof(int16_t)) != hipSuccess ||
@@ -1034,7 +1036,6 @@ int srsran_ulsch_decode(srsran_sch_t*       q,
   SchCtx* x = (SchCtx*)q->gpu;
   if (2 * (size_t)nb > x->ul_cap) {
     hipFree(x->d_ul);
-    hipFree(x->d_uldesc);
     x->d_ul   = nullptr;
     x->ul_cap = 0;
     if (hipMalloc((void**)&x->d_ul, 2 * (size_t)nb * sizeof(int16_t)) != hipSuccess) {

@@ -3,8 +3,11 @@
 #include "stage_timing.h"
 
 #include <atomic>
+#include <map>
 #include <mutex>
 #include <vector>
+
+#include "devkey.h"
 
 #include "../../include/srsran_amd_prof.h"
 
@@ -17,18 +20,20 @@ std::atomic<bool> g_on{false};
 std::mutex        g_mu;
 struct Rec {
   int        stage;
+  int        dev;
   hipEvent_t e0, e1;
 };
-std::vector<Rec>        g_pending;
-std::vector<hipEvent_t> g_pool;
+std::vector<Rec>                       g_pending;
+std::map<int, std::vector<hipEvent_t>> g_pool;  // per device: an event is recorded on its own device's streams
 double                  g_ms[ST_COUNT];
 uint32_t                g_n[ST_COUNT];
 
-hipEvent_t take()
+hipEvent_t take(int dev)
 {
-  if (!g_pool.empty()) {
-    hipEvent_t e = g_pool.back();
-    g_pool.pop_back();
+  std::vector<hipEvent_t>& pool = g_pool[dev];
+  if (!pool.empty()) {
+    hipEvent_t e = pool.back();
+    pool.pop_back();
     return e;
   }
   hipEvent_t e = nullptr;
@@ -44,8 +49,8 @@ void drain()  // caller holds g_mu
       g_ms[r.stage] += ms;
       g_n[r.stage]++;
     }
-    g_pool.push_back(r.e0);
-    g_pool.push_back(r.e1);
+    g_pool[r.dev].push_back(r.e0);
+    g_pool[r.dev].push_back(r.e1);
   }
   g_pending.clear();
 }
@@ -58,7 +63,8 @@ StageScope::StageScope(int stage, hipStream_t stream) : stage_(stage), stream_(s
     return;
   }
   std::lock_guard<std::mutex> lk(g_mu);
-  e0_ = take();
+  dev_ = cur_dev();
+  e0_  = take(dev_);
   if (e0_) {
     hipEventRecord(e0_, stream_);
   }
@@ -70,13 +76,13 @@ StageScope::~StageScope()
     return;
   }
   std::lock_guard<std::mutex> lk(g_mu);
-  hipEvent_t e1 = take();
+  hipEvent_t e1 = take(dev_);
   if (!e1) {
-    g_pool.push_back(e0_);
+    g_pool[dev_].push_back(e0_);
     return;
   }
   hipEventRecord(e1, stream_);
-  g_pending.push_back(Rec{stage_, e0_, e1});
+  g_pending.push_back(Rec{stage_, dev_, e0_, e1});
   if (g_pending.size() > 4096) {
     drain();
   }
@@ -116,7 +122,7 @@ extern "C" int srsran_amd_timing_read(float ms[SRSRAN_AMD_NOF_STAGES], uint32_t 
 extern "C" const char* srsran_amd_stage_name(int stage)
 {
   static const char* names[ST_COUNT] = {"ofdm_rx_kernel", "chest_kernel", "predecode_batch_kernel",
-                                        "llr_batch_kernel", "rm_rx_kernel", "tdec_kernel", "tb_kernel",
+                                        "llr_batch_kernel", "rm_rx_lds_kernel", "tdec_kernel", "tb_assemble_kernel",
                                         "nr_rm_kernel", "ldpc_kernel", "nr_tb_kernel"};
   return stage >= 0 && stage < ST_COUNT ? names[stage] : "";
 }

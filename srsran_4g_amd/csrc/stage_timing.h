@@ -18,6 +18,7 @@ private:
   int         stage_;
   hipStream_t stream_;
   hipEvent_t  e0_ = nullptr;
+  int         dev_ = 0;
 };
 
 }  // namespace srsran_amd

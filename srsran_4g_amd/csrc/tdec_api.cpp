@@ -16,10 +16,12 @@
 #include <algorithm>
 #include <cstring>
 #include <map>
+#include <tuple>
 #include <mutex>
 #include <vector>
 
 #include "../../include/srsran_tdec.h"
+#include "devkey.h"
 #include "tdec_kernel.h"
 
 using namespace srsran_amd;
@@ -83,7 +85,7 @@ struct Config {
 };
 
 std::mutex                             g_mu;
-std::map<std::pair<uint32_t, int>, Config*> g_cfg;
+std::map<std::tuple<int, uint32_t, int>, Config*> g_cfg;  // (device, K, nsb)
 int                                    g_have_gpu = -1;
 
 bool have_gpu()
@@ -99,7 +101,7 @@ bool have_gpu()
 Config* get_config(uint32_t K, int nsb)
 {
   std::lock_guard<std::mutex> lk(g_mu);
-  auto key = std::make_pair(K, nsb);
+  auto key = std::make_tuple(cur_dev(), K, nsb);
   auto it  = g_cfg.find(key);
   if (it != g_cfg.end()) {
     return it->second;
@@ -244,13 +246,19 @@ bool grow(void** p, size_t* have, size_t need)
 }
 
 // x^(8m) mod CRC24A / CRC24B, m = 0..768, for the in-kernel CB CRC (device, built once)
-const uint32_t* g_xpow[2] = {nullptr, nullptr};
+struct XpowTables {
+  const uint32_t* d[2] = {nullptr, nullptr};
+};
+std::map<int, XpowTables> g_xpow;  // per device
 
-bool xpow_tables()
+// the current device's tables (nullptr if they cannot be built)
+const XpowTables* xpow_tables()
 {
   std::lock_guard<std::mutex> lk(g_mu);
-  if (g_xpow[0]) {
-    return true;
+  const int dev = cur_dev();
+  auto      it  = g_xpow.find(dev);
+  if (it != g_xpow.end()) {
+    return &it->second;
   }
   const int             nm = SRSRAN_TCOD_MAX_LEN_CB / 8 + 1;
   std::vector<uint32_t> h(nm);
@@ -260,12 +268,13 @@ bool xpow_tables()
     crc24_xpow_table(poly[i], h.data(), nm);
     if (hipMalloc(&d[i], nm * sizeof(uint32_t)) != hipSuccess ||
         hipMemcpy(d[i], h.data(), nm * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) {
-      return false;
+      return nullptr;
     }
   }
-  g_xpow[0] = d[0];
-  g_xpow[1] = d[1];
-  return true;
+  XpowTables& t = g_xpow[dev];
+  t.d[0]        = d[0];
+  t.d[1]        = d[1];
+  return &t;
 }
 
 }  // namespace
@@ -288,7 +297,8 @@ int tdec_sch_enqueue(uint32_t      K,
     return SRSRAN_SUCCESS;
   }
   Config* c = get_config(K, auto_nsb(K));
-  if (!c || !xpow_tables()) {
+  const XpowTables* xp = xpow_tables();
+  if (!c || !xp) {
     return SRSRAN_ERROR;
   }
   TdecArgs a   = c->proto;
@@ -308,8 +318,8 @@ int tdec_sch_enqueue(uint32_t      K,
   a.out_stride = out_stride;
   a.noi_out    = d_noi;
   a.crc_ok     = d_crc_ok;
-  a.xpow_a     = g_xpow[0];
-  a.xpow_b     = g_xpow[1];
+  a.xpow_a     = xp->d[0];
+  a.xpow_b     = xp->d[1];
   a.min_iters  = 2;  // SRSRAN_PDSCH_MIN_TDEC_ITERS (sch.c:35)
   hipError_t e = tdec_launch(c->nsb, a, stream);
   if (e != hipSuccess) {

@@ -118,6 +118,11 @@ def lib():
         sig = {
             "srsran_symbol_sz": ([u32], ctypes.c_int),
             "srsran_symbol_sz_power2": ([u32], ctypes.c_int),
+            "srsran_use_standard_symbol_size": ([ctypes.c_bool], None),
+            "srsran_symbol_size_is_standard": ([], ctypes.c_bool),
+            "srsran_sampling_freq_hz": ([u32], ctypes.c_int),
+            "srsran_nof_prb": ([u32], ctypes.c_int),
+            "srsran_symbol_sz_isvalid": ([u32], ctypes.c_bool),
             "srsran_chest_dl_init": ([CH, u32, u32], ctypes.c_int),
             "srsran_chest_dl_free": ([CH], None),
             "srsran_chest_dl_set_cell": ([CH, srsran_cell_t], ctypes.c_int),
@@ -165,6 +170,16 @@ def lib():
             f.restype = res
         _bound = True
     return L
+
+
+def use_standard_symbol_size(enabled):
+    """srsran_use_standard_symbol_size: the library defaults to the reference's non-standard rates
+    (100 PRB -> N = 1536); srsUE and the C3 workload (N = 2048) switch standard rates on."""
+    lib().srsran_use_standard_symbol_size(bool(enabled))
+
+
+def symbol_size_is_standard():
+    return bool(lib().srsran_symbol_size_is_standard())
 
 
 def cell(nof_prb=100, nof_ports=2, cell_id=1):

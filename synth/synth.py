@@ -234,9 +234,11 @@ def ofdm_tx(grid, N):
     return np.concatenate(out)
 
 
-def symbol_sz(nof_prb):
-    """srsran_symbol_sz with standard rates (power-of-two sizes, 1536 for 15 MHz)"""
-    for p, n in ((6, 128), (15, 256), (25, 512), (52, 1024), (79, 1536), (110, 2048)):
+def symbol_sz(nof_prb, standard=True):
+    """srsran_symbol_sz (phy_common.c:340-385): standard rates = power-of-two sizes (1536 for 15 MHz);
+    otherwise the reference's default 3/4 rates (384 / 768 / 1536 for 25 / 50 / 100 PRB)."""
+    sizes = (512, 1024, 1536, 2048) if standard else (384, 768, 1024, 1536)
+    for p, n in zip((6, 15, 25, 52, 79, 110), (128, 256) + sizes):
         if nof_prb <= p:
             return n
     raise ValueError(nof_prb)

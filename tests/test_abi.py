@@ -26,7 +26,7 @@ def declared_functions():
         if f.endswith(".h"):
             src = open(os.path.join(INCLUDE, f)).read()
             src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-            for m in re.finditer(r"^\s*[A-Za-z_][\w\s\*]*?\b(srsran_\w+)\s*\(", src, flags=re.M):
+            for m in re.finditer(r"^\s*[A-Za-z_][\w\s\*]*?\b(srsran_\w+|create_compact_pcm)\s*\(", src, flags=re.M):
                 names.add(m.group(1))
     return sorted(names)
 
@@ -149,3 +149,14 @@ def test_nr_sch_fails_loudly_without_gpu():
 
     with pytest.raises(RuntimeError):
         sch_nr.SchNr()
+
+
+def test_library_exports_only_the_c_abi():
+    """libsrsran_4g_amd.so exports the srsran_* C entry points and nothing else (exports.map): no C++
+    helper or kernel symbol can collide with srsRAN's own when the library is linked into it."""
+    import subprocess
+    so = tdec.LIB_PATH
+    out = subprocess.run(["nm", "-D", "--defined-only", so], capture_output=True, text=True, check=True).stdout
+    syms = [ln.split()[-1] for ln in out.splitlines() if ln.strip()]
+    bad = [s for s in syms if not s.startswith("srsran_") and s != "create_compact_pcm"]  # base_graph.h:113
+    assert syms and not bad, bad[:20]

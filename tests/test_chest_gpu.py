@@ -24,6 +24,15 @@ def U():
     return ue_dl
 
 
+@pytest.fixture(scope="module", autouse=True)
+def standard_rates(U):
+    """these cases run at standard rates (N = 2048 at 100 PRB, as srsUE / C3); the reference
+    default (3/4 rates) is restored afterwards and tested on its own"""
+    U.use_standard_symbol_size(True)
+    yield
+    U.use_standard_symbol_size(False)
+
+
 @pytest.mark.parametrize("nof_prb,cell_id,nports,nrx,sf", [(100, 1, 2, 2, 1), (100, 5, 2, 2, 0), (50, 7, 1, 1, 6),
                                                             (25, 301, 2, 1, 9), (6, 2, 4, 2, 3), (100, 0, 1, 2, 5)])
 def test_chest_matches_oracle(U, ora, nof_prb, cell_id, nports, nrx, sf):

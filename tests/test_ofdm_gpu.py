@@ -17,6 +17,15 @@ def U():
     return ue_dl
 
 
+@pytest.fixture(scope="module", autouse=True)
+def standard_rates(U):
+    """these cases run at standard rates (N = 2048 at 100 PRB, as srsUE / C3); the reference
+    default (3/4 rates) is restored afterwards and tested on its own"""
+    U.use_standard_symbol_size(True)
+    yield
+    U.use_standard_symbol_size(False)
+
+
 @pytest.mark.parametrize("nof_prb", [6, 15, 25, 50, 75, 100])
 def test_ofdm_rx_matches_numpy(U, nof_prb):
     rng = np.random.default_rng(nof_prb)
@@ -68,3 +77,23 @@ def test_ofdm_gpu_batch_with_cfo(U):
     got = d_out.cpu().numpy().view(np.complex64).reshape(nsf, nrx, 14 * nre)
     assert np.abs(got - grids).max() < 2e-4
     rx.free()
+
+
+@pytest.mark.parametrize("nof_prb,N", [(25, 384), (50, 768), (75, 1024), (100, 1536)])
+def test_ofdm_rx_reference_default_rates(U, nof_prb, N):
+    """the reference's default 3/4 sampling rates (phy_common.c:31-35, 361-385): non-power-of-two
+    FFT sizes (radix-3 stage) at 25 / 50 / 100 PRB"""
+    U.use_standard_symbol_size(False)
+    try:
+        assert U.lib().srsran_symbol_sz(nof_prb) == N and not U.symbol_size_is_standard()
+        assert U.lib().srsran_nof_prb(N) == nof_prb and U.lib().srsran_sampling_freq_hz(nof_prb) == 15000 * N
+        rng = np.random.default_rng(N)
+        rx = U.OfdmRx(nof_prb)
+        nre = 12 * nof_prb
+        assert rx.symbol_sz == N
+        x = (rng.standard_normal(ofdm_np.sf_len(N)) + 1j * rng.standard_normal(ofdm_np.sf_len(N))).astype(np.complex64)
+        exp = ofdm_np.ofdm_rx(x, N, nre)
+        assert np.abs(rx.rx(x) - exp).max() < 2e-5 * np.abs(exp).max() * np.log2(N)
+        rx.free()
+    finally:
+        U.use_standard_symbol_size(True)

@@ -1,0 +1,769 @@
+// srsran_4g_amd/csrc/tdec16_kernel.hip -- LTE turbo decoder for K >= 816 (16 sub-blocks) on CDNA4.
+//
+// Bit-exact with srsRAN_4G's AVX2 16-bit window decoder (turbodecoder_win.h, WINIMP avx16:
+// saturating int16, 16 sub-blocks, 40-step overlap training, normalisation every 2 steps) driven
+// by the half-iteration loop of turbodecoder_iter.h:72-144, on the rm_turbo sub-block (SB) input
+// layout (rm_turbo.c:260-273).  This is the hot class of the all-188 workload and of every
+// DL-SCH / PDSCH code block of K >= 816; tdec_kernel.hip keeps the 8-sub-block and generic
+// decoders, the natural input layout and the srsran_tdec_iteration state save/restore.
+//
+// Mapping -- a LANE PAIR per sub-block:
+//   * the 8 trellis states of a sub-block live in two lanes, 4 states each as two packed int16
+//     VGPRs.  A step is 9 VALU a lane: 3 v_pk_add_i16 clamp + 2 v_pk_max_i16 on register pairs
+//     whose halves are picked by op_sel (the butterflies need no data movement inside a lane),
+//     one DPP swap between the two lanes and 2 v_perm_b32 with per-lane selectors.  The state
+//     pairing (beta: (0,4)(1,5) | (7,3)(6,2); alpha: (0,1)(2,3) | (6,7)(4,5)) is chosen so both
+//     lanes run the same instruction stream and the alpha candidates line up with the betas for
+//     the LLR (derivation in DESIGN.md section 4.1).  18 lane-instructions per step and sub-block
+//     against 36 for a quad of lanes holding 2 states each (tdec_kernel.hip).
+//   * workgroup = 2 waves x 2 code blocks of the same K: wave 0 runs the alpha side, wave 1 the
+//     beta side of both blocks (32 lanes per block and side), in the crossover schedule of
+//     tdec_kernel.hip (phase 1: alpha over windows [0,h) || beta over [h,M); phase 2: each side
+//     recomputes the other direction from LDS checkpoints, W = 16 steps a window, and emits LLRs).
+//   * LDS per code block is ONE int16 array S over the soft-buffer slots plus the checkpoints and
+//     a decision bitmap (~19 KB at K = 6144, half of tdec_kernel.hip's 40 KB).  S carries the
+//     a-priori / extrinsic bookkeeping of the reference's app1/ext1/ext2 buffers in place:
+//       DEC1 (even half-iteration) at slot a:  x = sat(syst + S[a]),  y = parity0
+//            S[a] <- out1 - S[a]                   (ext1 -= app1, vec_sub: wraps)
+//       DEC2 (odd)  at slot a, b = pi-slot(a): x = S[b],  y = parity1
+//            S[b] <- out2 - S[b]                   (app1 = ext2 de-interleaved; app1 -= ext1)
+//     The hard decision of the half-iteration (ext1 after DEC1, app1 after DEC2:
+//     turbodecoder.c:370-378) is the sign of out, ORed into the bitmap as it is produced.
+//   * systematic / parity LLRs are not staged: every window loads its W positions straight from
+//     the input (L2) one window ahead of use.  Everything runs in one launch for all
+//     half-iterations; the DL-SCH variant (ES) adds the CRC early stop of decode_tb_cb
+//     (sch.c:426-456) on the bitmap.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "crc24_dev.h"
+#include "stage_timing.h"
+#include "tdec_kernel.h"
+
+namespace srsran_amd {
+namespace {
+
+typedef short v2s __attribute__((ext_vector_type(2)));
+
+constexpr int   W    = 16;            // window: steps between checkpoints
+constexpr int   OVL  = TDEC_OVERLAP;  // win_overlap_len (turbodecoder_win.h:54)
+constexpr int   NSB  = 16;            // nof_blocks of the avx16 window decoder
+constexpr short NEG  = -10000;        // -INF (turbodecoder_win.h:56)
+constexpr int   CPWG = 2;             // code blocks per workgroup
+
+__device__ __forceinline__ v2s u2v(uint32_t u) { return __builtin_bit_cast(v2s, u); }
+__device__ __forceinline__ uint32_t v2u(v2s v) { return __builtin_bit_cast(uint32_t, v); }
+__device__ __forceinline__ v2s padd(v2s a, v2s b) { return __builtin_elementwise_add_sat(a, b); }
+__device__ __forceinline__ v2s psub(v2s a, v2s b) { return __builtin_elementwise_sub_sat(a, b); }
+__device__ __forceinline__ v2s pmax(v2s a, v2s b) { return __builtin_elementwise_max(a, b); }
+__device__ __forceinline__ v2s lo2(v2s a) { return __builtin_shufflevector(a, a, 0, 0); }
+__device__ __forceinline__ v2s hi2(v2s a) { return __builtin_shufflevector(a, a, 1, 1); }
+__device__ __forceinline__ v2s swp(v2s a) { return __builtin_shufflevector(a, a, 1, 0); }
+// v_perm_b32: selector bytes 0-3 pick bytes of lo_src, 4-7 bytes of hi_src
+__device__ __forceinline__ v2s perm(v2s hi_src, v2s lo_src, uint32_t sel)
+{
+  return u2v(__builtin_amdgcn_perm(v2u(hi_src), v2u(lo_src), sel));
+}
+#define QP(a, b, c, d) ((a) | ((b) << 2) | ((c) << 4) | ((d) << 6))
+template <int CTRL>
+__device__ __forceinline__ v2s dpp(v2s a)
+{
+  return u2v((uint32_t)__builtin_amdgcn_mov_dpp((int)v2u(a), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ v2s pswap(v2s a) { return dpp<QP(1, 0, 3, 2)>(a); }  // the other lane of the pair
+
+__device__ __forceinline__ uint32_t pack2(short lo, short hi) { return (uint32_t)(uint16_t)lo | ((uint32_t)(uint16_t)hi << 16); }
+
+// Per-lane v_perm selectors (j = lane & 1).
+struct PairSel {
+  uint32_t b0, b1;   // beta: new V0 / V1 from (O0, R)
+  uint32_t as, ak;   // alpha: the half sent to the other lane / the half kept, from (O0, O1)
+};
+__device__ __forceinline__ PairSel pair_sel(int j)
+{
+  PairSel p;
+  p.b0 = j ? 0x03020706u : 0x01000504u;  // a: (O0.lo, R.lo)   b: (O0.hi, R.hi)
+  p.b1 = j ? 0x01000504u : 0x03020706u;  // a: (O0.hi, R.hi)   b: (O0.lo, R.lo)
+  p.as = j ? 0x03020706u : 0x07060302u;  // a: (O0.hi, O1.hi)  b: (O1.hi, O0.hi)
+  p.ak = j ? 0x01000504u : 0x05040100u;  // a: (O0.lo, O1.lo)  b: (O1.lo, O0.lo)
+  return p;
+}
+
+// Trellis state of one sub-block in a lane pair.
+struct St {
+  v2s v0, v1;
+};
+
+// Backward step (turbodecoder_win.h:641-664).  Beta pairing: lane a (b0,b4)(b1,b5), lane b
+// (b7,b3)(b6,b2).  O0 = max(V0, swap(V0 + xy)) gives (n0,n1) | (n6,n7); O1 = max(V1 + x,
+// swap(V1 + y)) gives (n2,n3) | (n4,n5); the lanes trade O1 and re-pair.
+__device__ __forceinline__ St beta_step(St p, v2s xy, const PairSel& ps)
+{
+  const v2s xys = padd(xy, swp(xy));
+  const v2s O0  = pmax(p.v0, swp(padd(p.v0, xys)));
+  const v2s O1  = pmax(padd(p.v1, lo2(xy)), swp(padd(p.v1, hi2(xy))));
+  const v2s R   = pswap(O1);
+  return St{perm(O0, R, ps.b0), perm(O0, R, ps.b1)};
+}
+
+// Forward candidates (turbodecoder_win.h:767-785): c0 = bit-0 (m_b), c1 = bit-1 (new) metrics
+// of the destination states, paired as the betas.  Alpha pairing: lane a (a0,a1)(a2,a3),
+// lane b (a6,a7)(a4,a5).
+struct Cand {
+  v2s c00, c10, c01, c11;  // c0 / c1 of pair 0 and pair 1
+};
+__device__ __forceinline__ Cand alpha_cand(St p, v2s xy)
+{
+  const v2s xys = padd(xy, swp(xy));
+  Cand      c;
+  c.c00 = p.v0;
+  c.c10 = padd(swp(p.v0), xys);
+  c.c01 = padd(swp(p.v1), hi2(xy));
+  c.c11 = padd(p.v1, lo2(xy));
+  return c;
+}
+__device__ __forceinline__ St alpha_next(const Cand& c, const PairSel& ps)
+{
+  const v2s O0 = pmax(c.c00, c.c10);  // a: (s0,s4)  b: (s7,s3)
+  const v2s O1 = pmax(c.c01, c.c11);  // a: (s1,s5)  b: (s6,s2)
+  return St{perm(O1, O0, ps.ak), pswap(perm(O1, O0, ps.as))};
+}
+
+// LLR = max_s(beta + c1) - max_s(beta + c0) over the 8 states (turbodecoder_win.h:788-815).
+__device__ __forceinline__ short llr_out(St b, const Cand& c)
+{
+  const v2s m0 = pmax(padd(b.v0, c.c00), padd(b.v1, c.c01));
+  const v2s m1 = pmax(padd(b.v0, c.c10), padd(b.v1, c.c11));
+  v2s       r  = pmax(perm(m1, m0, 0x05040100u), perm(m1, m0, 0x07060302u));  // (max0, max1) of the lane
+  r            = pmax(r, pswap(r));
+  return psub(swp(r), r).x;
+}
+
+// normalize() (turbodecoder_win.h:480-498): subtract state 0 (lane a, V0.lo in both pairings).
+__device__ __forceinline__ St norm(St p)
+{
+  const v2s z = lo2(dpp<QP(0, 0, 2, 2)>(p.v0));
+  return St{psub(p.v0, z), psub(p.v1, z)};
+}
+__device__ __forceinline__ bool norm_at(int k) { return (k & 1) == 0 && k != 0; }  // normalize_period 2
+
+__device__ __forceinline__ St neg_state() { return St{v2s{NEG, NEG}, v2s{NEG, NEG}}; }
+__device__ __forceinline__ St alpha_known(int j) { return j ? neg_state() : St{v2s{0, NEG}, v2s{NEG, NEG}}; }
+
+// beta_trellis (turbodecoder_win.h:500-548): the tail steps K+2..K of the last sub-block,
+// non-saturating (sadd without use_saturated_add).
+__device__ __forceinline__ St trellis_pair(const short* xt, const short* yt, int j)
+{
+  short o[8] = {0, NEG, NEG, NEG, NEG, NEG, NEG, NEG};
+#pragma unroll
+  for (int t = 2; t >= 0; t--) {
+    const short x = xt[t], y = yt[t], xy = (short)(x + y);
+    short       n[8];
+    n[0] = max(o[0], (short)(o[4] + xy));
+    n[1] = max((short)(o[0] + xy), o[4]);
+    n[2] = max((short)(o[1] + x), (short)(o[5] + y));
+    n[3] = max((short)(o[1] + y), (short)(o[5] + x));
+    n[4] = max((short)(o[2] + y), (short)(o[6] + x));
+    n[5] = max((short)(o[2] + x), (short)(o[6] + y));
+    n[6] = max((short)(o[3] + xy), o[7]);
+    n[7] = max(o[3], (short)(o[7] + xy));
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      o[i] = n[i];
+    }
+  }
+  return j ? St{v2s{o[7], o[3]}, v2s{o[6], o[2]}} : St{v2s{o[0], o[4]}, v2s{o[1], o[5]}};
+}
+
+__device__ __forceinline__ uint32_t ck_word(int m, int l32) { return (uint32_t)(m * 32 + l32) * 2; }
+
+// LDS of one code block (dwords): S [16*Ls int16] | CK [M*32 lanes*8 B] | BITS [K/8 B] | RED [2]
+struct Geo16 {
+  int s_dw, ck_dw, bits_dw, cb_dw;
+};
+__host__ __device__ __forceinline__ Geo16 geo16(int K, int Ls, int M)
+{
+  Geo16 g;
+  g.s_dw    = (NSB * Ls + 1) / 2;
+  g.ck_dw   = M * 64;
+  g.bits_dw = (K / 8 + 3) / 4;
+  g.cb_dw   = g.s_dw + g.ck_dw + g.bits_dw + 2;
+  return g;
+}
+
+// One window of W inputs of this lane's sub-block, as loaded from global memory.
+// (kept as separate 16-bit registers: packing two loads into one VGPR at issue time would make
+// the wave wait for both right there and defeat the prefetch)
+struct Raw {
+  short a[W];  // systematic LLR (DEC1) / slot of pi(position) (DEC2)
+  short b[W];  // parity0 / parity1
+};
+
+// global-memory pointers (address space 1): the window loads must be global_load, not flat
+// (a flat load also counts in lgkmcnt, so every LDS wait would drain the prefetched window)
+typedef const short __attribute__((address_space(1)))*    gshort;
+typedef const uint16_t __attribute__((address_space(1)))* gushort;
+
+// Per-lane context of one half-iteration.
+struct Lane16 {
+  int             wave, l32, s, j, K, L, Ls, M, KP;
+  uint32_t        magicLs;
+  gshort          in;
+  gushort         tf;   // q order, SB input: slot of pi(n(q))
+  short*          S;    // this block's S (LDS)
+  uint32_t*       CK;   // this block's checkpoints (LDS)
+  uint32_t*       BITS; // this block's decision bitmap (LDS)
+  PairSel         ps;
+};
+
+// Inputs of a window [t0, min(t0 + W, kend)) of this lane's sub-block (q = k*16 + s in the SB
+// layout): DEC1 loads systematic + parity0, DEC2 the pi slot + parity1.  FULL: the whole window
+// lies below kend; otherwise positions past kend are clamped to kend - 1 (loaded, never used) so
+// no load is predicated and no read leaves the block's buffer.
+template <bool D2, bool FULL>
+__device__ __forceinline__ void issue(const Lane16& c, Raw& r, int t0, int kend)
+{
+  const gshort par = c.in + (D2 ? 2 * c.KP : c.KP);
+#pragma unroll
+  for (int i = 0; i < W; i++) {
+    const int k = FULL ? t0 + i : min(t0 + i, kend - 1);
+    const int q = k * NSB + c.s;
+#if defined(T16_ABL) && (T16_ABL & 1)  // profiling ablation: no global loads
+    r.a[i] = (short)(q & 1023);
+    r.b[i] = (short)(q & 511);
+    (void)par;
+#else
+    r.a[i] = D2 ? (short)c.tf[q] : c.in[q];
+    r.b[i] = par[q];
+#endif
+  }
+}
+// Stage 2: the S values a window needs (DEC1: the a-priori S[a] of each position; DEC2: ext1 at
+// the pi slot b, whose address came with stage 1).
+template <bool D2, bool FULL>
+__device__ __forceinline__ void issue_lds(const Lane16& c, const Raw& r, int t0, int kend, short* dv)
+{
+#pragma unroll
+  for (int i = 0; i < W; i++) {
+    const int k = FULL ? t0 + i : min(t0 + i, kend - 1);
+#if defined(T16_ABL) && (T16_ABL & 2)  // profiling ablation: no LDS reads of S
+    dv[i] = (short)(k & 255);
+    (void)r;
+#else
+    dv[i] = D2 ? c.S[(uint16_t)r.a[i]] : c.S[c.s * c.Ls + k];
+#endif
+  }
+}
+// Stage 3: branch inputs (x, y) packed, and what the output needs: DEC1 the a-priori value,
+// DEC2 the slot b (x = S[b] is xw.lo).
+template <bool D2>
+__device__ __forceinline__ void combine(const Raw& r, const short* dv, uint32_t* xw, short* aux)
+{
+#pragma unroll
+  for (int i = 0; i < W; i++) {
+    short x;
+    if (D2) {
+      x      = dv[i];
+      aux[i] = r.a[i];
+    } else {
+      x      = __builtin_elementwise_add_sat(r.a[i], dv[i]);
+      aux[i] = dv[i];
+    }
+    xw[i] = pack2(x, r.b[i]);
+  }
+}
+
+// The LLR o of position k: S update (vec_sub, wraps) and the decision bit (ORed every
+// half-iteration, no branch; the bitmap is cleared before each one).
+template <bool D2>
+__device__ __forceinline__ void emit(const Lane16& c, int k, short o, short aux, uint32_t xw)
+{
+  int   slot, n;
+  short sub;
+  if (D2) {
+    slot         = (uint16_t)aux;
+    const int sb = (int)__umulhi((uint32_t)slot, c.magicLs);
+    n            = slot - sb * (c.Ls - c.L);
+    sub          = (short)(xw & 0xffffu);  // x = ext1 at slot b
+  } else {
+    slot = c.s * c.Ls + k;
+    n    = c.s * c.L + k;
+    sub  = aux;                            // app1 used by this DEC1
+  }
+#if defined(T16_ABL) && (T16_ABL & 4)  // profiling ablation: no output stores
+  if (o == 12345) {
+#endif
+  c.S[slot] = (short)(o - sub);
+  atomicOr(&c.BITS[n >> 5], (uint32_t)(o > 0) << (((n >> 3) & 3) * 8 + 7 - (n & 7)));
+#if defined(T16_ABL) && (T16_ABL & 4)
+  }
+#endif
+}
+
+// Phase-2 alpha side, window at t0 (alpha_window of tdec_kernel.hip): beta[t0+1 .. cc] recomputed
+// from the stored beta at cc = min(t0 + W, L) (checkpoint), then alpha + LLR of t0 .. cc-1.
+template <bool D2, bool FULL>
+__device__ __forceinline__ St alpha_llr_window(const Lane16& c, St P, int t0, St Pb, const uint32_t* xw,
+                                               const short* aux)
+{
+  const int L  = c.L;
+  const int cc = FULL ? t0 + W : L;
+  const int ic = cc - t0 - 1;
+  St        bw[W];
+#pragma unroll
+  for (int i = W - 1; i >= 0; i--) {
+    if (FULL ? i == W - 1 : i == ic) {
+      bw[i] = Pb;
+      if (cc < L && norm_at(cc)) Pb = norm(Pb);
+    } else if (FULL || i < ic) {
+      Pb    = beta_step(Pb, u2v(xw[i + 1]), c.ps);
+      bw[i] = Pb;
+      if (norm_at(t0 + 1 + i)) Pb = norm(Pb);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < W; i++) {
+    if (FULL || t0 + i < L) {
+      const Cand  cd = alpha_cand(P, u2v(xw[i]));
+      const short o  = llr_out(bw[i], cd);
+      P              = alpha_next(cd, c.ps);
+      if (norm_at(t0 + i)) P = norm(P);
+      emit<D2>(c, t0 + i, o, aux[i], xw[i]);
+    }
+  }
+  return P;
+}
+
+// Phase-1 beta side, window at t0: backward over t0+W-1 .. t0 (FULL) or L-1 .. t0; Bst = the stored
+// beta at t0, which is the checkpoint of window t0/W - 1 when `store`.
+template <bool FULL>
+__device__ __forceinline__ St beta_window(const Lane16& c, St P, int t0, bool store, St& Bst, const uint32_t* xw)
+{
+#pragma unroll
+  for (int i = W - 1; i >= 0; i--) {
+    if (FULL || t0 + i < c.L) {
+      P = beta_step(P, u2v(xw[i]), c.ps);
+      if (i == 0) {
+        Bst = P;
+        if (store) {
+          *reinterpret_cast<uint2*>(&c.CK[ck_word(t0 / W - 1, c.l32)]) = make_uint2(v2u(P.v0), v2u(P.v1));
+        }
+      }
+      if (norm_at(t0 + i)) P = norm(P);
+    }
+  }
+  return P;
+}
+
+// The window inputs of one side, prefetched along the side's window sequence:
+//   alpha side: training [L-40, L-24), [L-24, L-8), [L-8, L); then windows 0, 1, ..., Ma-1
+//   beta side:  training [32, 40), [16, 32), [0, 16);       then windows Ma-1, ..., 1, 0
+// The global loads of window idx + 1 are issued when window idx starts (a whole window of compute
+// to arrive); DEC1's LDS reads of S (addresses known in advance) go with them.  DEC2's S gathers
+// need the pi slots of the window itself: they are issued when it starts, just before the next
+// window's global loads, which cover their latency.  Reading S ahead of use is safe: within a
+// half-iteration a position's S is written only by the side that emits its LLR, after that side
+// has read it, and no position is read again later.
+template <bool D2>
+struct Pipe16 {
+  Raw   g;      // global loads of the next window (in flight)
+  short dv[W];  // DEC1: its S values (in flight); DEC2: this window's gathers
+  int   nwin, Ma;
+  bool  beta;
+
+  __device__ __forceinline__ int t0_of(int idx, int L) const
+  {
+    if (beta) {
+      return idx < 3 ? 2 * W - W * idx : (Ma - 1 - (idx - 3)) * W;
+    }
+    return idx < 3 ? L - OVL + W * idx : (idx - 3) * W;
+  }
+  __device__ __forceinline__ int kend_of(int idx, int L) const { return beta && idx < 3 ? OVL : L; }
+  __device__ __forceinline__ bool full_of(int idx, int L) const { return t0_of(idx, L) + W <= kend_of(idx, L); }
+
+  __device__ __forceinline__ void load(const Lane16& c, int idx)
+  {
+    if (idx < nwin) {
+      const int t0 = t0_of(idx, c.L), ke = kend_of(idx, c.L);
+      if (full_of(idx, c.L)) {
+        issue<D2, true>(c, g, t0, ke);
+        if (!D2) {
+          issue_lds<D2, true>(c, g, t0, ke, dv);
+        }
+      } else {
+        issue<D2, false>(c, g, t0, ke);
+        if (!D2) {
+          issue_lds<D2, false>(c, g, t0, ke, dv);
+        }
+      }
+    }
+  }
+  __device__ __forceinline__ void start(const Lane16& c) { load(c, 0); }
+  // window idx begins: its (x, y) and output aux; the loads of idx + 1 are issued
+  __device__ __forceinline__ void next(const Lane16& c, int idx, uint32_t* xw, short* aux)
+  {
+    Raw cur = g;
+    if (D2) {
+      const int t0 = t0_of(idx, c.L), ke = kend_of(idx, c.L);
+      issue_lds<D2, true>(c, cur, t0, ke, dv);  // slots come from the table: no clamping needed
+    }
+    short dcur[W];
+#pragma unroll
+    for (int i = 0; i < W; i++) {
+      dcur[i] = dv[i];
+    }
+    load(c, idx + 1);
+    combine<D2>(cur, dcur, xw, aux);
+  }
+};
+
+// One constituent MAP decode of this lane's sub-block; wave 0 = alpha side, wave 1 = beta side.
+template <bool D2>
+__device__ __forceinline__ void map16(const Lane16& cin)
+{
+  // Opaque copy of the per-lane sub-block index: every window address derives from it, so none
+  // can be hoisted out of the half-iteration loop (LICM would keep hundreds of addresses live
+  // across it and spill).
+  Lane16 c = cin;
+  asm volatile("" : "+v"(c.s));
+  const int L     = c.L;
+  const int Mfull = L / W;            // windows entirely below L
+  const int Ma    = (L + W - 1) / W;  // = c.M
+  const int h     = max(1, min((L + W) / (2 * W), L / W));
+  const PairSel& ps = c.ps;
+  Pipe16<D2> pp;
+  pp.nwin = 3 + Ma;
+  pp.Ma   = Ma;
+  pp.beta = c.wave != 0;
+  uint32_t xw[W];
+  short    aux[W];
+  pp.start(c);
+  if (c.wave == 0) {
+    // ================= alpha side =================
+    St P = neg_state();
+    // training over the last 40 steps of the own sub-block (win.h:747-756)
+    pp.next(c, 0, xw, aux);
+#pragma unroll
+    for (int i = 0; i < W; i++) {
+      P = alpha_next(alpha_cand(P, u2v(xw[i])), ps);
+      if (norm_at(i)) P = norm(P);
+    }
+    pp.next(c, 1, xw, aux);
+#pragma unroll
+    for (int i = 0; i < W; i++) {
+      P = alpha_next(alpha_cand(P, u2v(xw[i])), ps);
+      if (norm_at(W + i)) P = norm(P);
+    }
+    pp.next(c, 2, xw, aux);
+#pragma unroll
+    for (int i = 0; i < OVL - 2 * W; i++) {
+      P = alpha_next(alpha_cand(P, u2v(xw[i])), ps);
+      if (norm_at(2 * W + i)) P = norm(P);
+    }
+    {  // move_left: sub-block s starts from the training state of s - 1; s = 0 is known
+      St q;
+      q.v0 = u2v((uint32_t)__shfl_up((int)v2u(P.v0), 2, 64));
+      q.v1 = u2v((uint32_t)__shfl_up((int)v2u(P.v1), 2, 64));
+      P    = c.s == 0 ? alpha_known(c.j) : q;
+    }
+    // phase 1: windows [0, h) (all full), entry checkpoints in slots 0..h-1
+#pragma unroll 1
+    for (int ma = 0; ma < h; ma++) {
+      const int t0 = ma * W;
+      pp.next(c, 3 + ma, xw, aux);
+      *reinterpret_cast<uint2*>(&c.CK[ck_word(ma, c.l32)]) = make_uint2(v2u(P.v0), v2u(P.v1));
+#pragma unroll
+      for (int i = 0; i < W; i++) {
+        P = alpha_next(alpha_cand(P, u2v(xw[i])), ps);
+        if (norm_at(t0 + i)) P = norm(P);
+      }
+    }
+    __syncthreads();
+    // phase 2: windows [h, Ma): beta recomputed from the checkpoint above the window, then
+    // alpha + LLR; the last window may be partial
+#pragma unroll 1
+    for (int ma = h; ma < Ma; ma++) {
+      const int t0 = ma * W;
+      pp.next(c, 3 + ma, xw, aux);
+      const uint2 ckv = *reinterpret_cast<const uint2*>(&c.CK[ck_word(ma, c.l32)]);
+      const St    Pb{u2v(ckv.x), u2v(ckv.y)};
+      if (ma < Mfull) {
+        P = alpha_llr_window<D2, true>(c, P, t0, Pb, xw, aux);
+      } else {
+        P = alpha_llr_window<D2, false>(c, P, t0, Pb, xw, aux);
+      }
+    }
+  } else {
+    // ================= beta side =================
+    St P = neg_state();
+    // training over the first 40 steps of the own sub-block, backwards (win.h:622-630)
+    pp.next(c, 0, xw, aux);
+#pragma unroll
+    for (int i = OVL - 2 * W - 1; i >= 0; i--) {
+      P = beta_step(P, u2v(xw[i]), ps);
+      if (norm_at(2 * W + i)) P = norm(P);
+    }
+    pp.next(c, 1, xw, aux);
+#pragma unroll
+    for (int i = W - 1; i >= 0; i--) {
+      P = beta_step(P, u2v(xw[i]), ps);
+      if (norm_at(W + i)) P = norm(P);
+    }
+    pp.next(c, 2, xw, aux);
+#pragma unroll
+    for (int i = W - 1; i >= 0; i--) {
+      P = beta_step(P, u2v(xw[i]), ps);
+      if (norm_at(i)) P = norm(P);
+    }
+    {  // move_right: sub-block s starts from the training state of s + 1; the last from the tail
+      St q;
+      q.v0 = u2v((uint32_t)__shfl_down((int)v2u(P.v0), 2, 64));
+      q.v1 = u2v((uint32_t)__shfl_down((int)v2u(P.v1), 2, 64));
+      if (c.s == NSB - 1) {  // trellis termination: systematic / parity0 (DEC1), app2 / parity1 (DEC2)
+        const gshort tail = c.in + 3 * c.KP + (D2 ? 6 : 0);
+        short        xt[3], yt[3];
+#pragma unroll
+        for (int t = 0; t < 3; t++) {
+          xt[t] = tail[2 * t];
+          yt[t] = tail[2 * t + 1];
+        }
+        P = trellis_pair(xt, yt, c.j);
+      } else {
+        P = q;
+      }
+    }
+    const int mtop = Ma - 1;
+    *reinterpret_cast<uint2*>(&c.CK[ck_word(mtop, c.l32)]) = make_uint2(v2u(P.v0), v2u(P.v1));  // beta[L]
+    St Bst = P;  // stored (pre-normalisation) beta of the position above the current window
+    // phase 1: windows [h, Ma) from the top (the top one maybe partial); the stored beta at the
+    // start of window mb is the checkpoint of window mb - 1 (slot mb - 1) for mb > h
+#pragma unroll 1
+    for (int mb = mtop; mb >= h; mb--) {
+      const int t0 = mb * W;
+      pp.next(c, 3 + mtop - mb, xw, aux);
+      if (mb < Mfull) {
+        P = beta_window<true>(c, P, t0, mb > h, Bst, xw);
+      } else {
+        P = beta_window<false>(c, P, t0, mb > h, Bst, xw);
+      }
+    }
+    __syncthreads();
+    // phase 2: windows [0, h) from the top: alpha recomputed from the entry checkpoint, then
+    // beta backwards with the LLR of every position (beta_llr_window of tdec_kernel.hip)
+#pragma unroll 1
+    for (int mb = h - 1; mb >= 0; mb--) {
+      const int t0 = mb * W;
+      pp.next(c, 3 + mtop - mb, xw, aux);
+      const uint2 cka = *reinterpret_cast<const uint2*>(&c.CK[ck_word(mb, c.l32)]);
+      St          Pa{u2v(cka.x), u2v(cka.y)};
+      St          aw[W];  // alpha entering each position (candidates rebuilt at LLR time)
+#pragma unroll
+      for (int i = 0; i < W; i++) {
+        aw[i] = Pa;
+        if (i < W - 1) {
+          Pa = alpha_next(alpha_cand(Pa, u2v(xw[i])), ps);
+          if (norm_at(t0 + i)) Pa = norm(Pa);
+        }
+      }
+#pragma unroll
+      for (int i = W - 1; i >= 0; i--) {
+        const short o = llr_out(Bst, alpha_cand(aw[i], u2v(xw[i])));
+        P             = beta_step(P, u2v(xw[i]), ps);
+        Bst           = P;
+        if (norm_at(t0 + i)) P = norm(P);
+        emit<D2>(c, t0 + i, o, aux[i], xw[i]);
+      }
+    }
+  }
+}
+
+}  // namespace
+
+template <bool ES>
+__device__ __forceinline__ void tdec16_body(const TdecArgs& a, int bid)
+{
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int cbw  = lane >> 5;         // block of the workgroup
+  const int l32  = lane & 31;         // lane within the block's side
+  const int t2   = wave * 32 + l32;   // thread within the block (both sides), 0..63
+  const int K    = (int)a.K;
+  const int L    = (int)a.L;
+  const int Ls   = (int)a.Ls;
+  const int M    = (L + W - 1) / W;
+  const Geo16 g  = geo16(K, Ls, M);
+  const int cb   = bid * CPWG + cbw;
+  const bool live = cb < (int)a.ncb;
+  const int cbl  = live ? cb : (int)a.ncb - 1;
+  bool done      = ES && (!live || *a.cbs[cbl].skip);
+
+  uint32_t* base = smem + cbw * g.cb_dw;
+  Lane16    c;
+  c.wave    = wave;
+  c.l32     = l32;
+  c.s       = l32 >> 1;
+  c.j       = l32 & 1;
+  c.K       = K;
+  c.L       = L;
+  c.Ls      = Ls;
+  c.M       = M;
+  c.KP      = K + 32;  // SB stream stride (rm_turbo.c:260-273)
+  c.magicLs = a.magicLs;
+  c.in      = (gshort)(ES ? a.cbs[cbl].in : a.in + (size_t)cbl * a.in_stride);
+  c.tf      = (gushort)a.tfwd;
+  c.S       = reinterpret_cast<short*>(base);
+  c.CK      = base + g.s_dw;
+  c.BITS    = c.CK + g.ck_dw;
+  c.ps      = pair_sel(c.j);
+  uint32_t* RED = c.BITS + g.bits_dw;
+
+  if constexpr (ES) {
+    if (live && done && t2 == 0) {  // skipped block (sch.c:392, 476-480)
+      const uint32_t slot = a.cbs[cbl].slot;
+      a.noi_out[slot]     = 0;
+      a.crc_ok[slot]      = 1;
+    }
+  }
+  // S = 0: no a-priori information before the first half-iteration
+  for (int i = threadIdx.x; i < CPWG * g.s_dw; i += 128) {
+    smem[(i / g.s_dw) * g.cb_dw + i % g.s_dw] = 0u;
+  }
+  const int h_end = (ES && __syncthreads_or(!done) == 0) ? 0 : a.n_end;
+
+#pragma unroll 1
+  for (int hi = 0; hi < h_end; hi++) {
+    const bool crc_now = ES && hi + 1 >= a.min_iters;  // early-stop check (sch.c:433: from the 2nd)
+    for (int i = threadIdx.x; i < CPWG * g.bits_dw; i += 128) {
+      smem[(i / g.bits_dw) * g.cb_dw + g.s_dw + g.ck_dw + i % g.bits_dw] = 0u;
+    }
+    __syncthreads();
+    if (hi & 1) {
+      map16<true>(c);
+    } else {
+      map16<false>(c);
+    }
+    __syncthreads();
+
+    // ---------------- DL-SCH early stop: CRC of the hard decision (sch.c:426-456) ----------------
+    if constexpr (ES) {
+      if (crc_now) {
+        const uint8_t* bytes  = reinterpret_cast<const uint8_t*>(c.BITS);
+        const int      nbytes = K / 8;
+        const int      bpt    = (nbytes + 63) / 64;
+        const int      b0     = t2 * bpt;
+        const int      b1     = min(b0 + bpt, nbytes);
+        const bool     crc_a  = a.cbs[cbl].crc_a;
+        const uint32_t poly   = crc_a ? LTE_CRC24A : LTE_CRC24B;
+        uint32_t       crc    = 0;
+#pragma unroll 1
+        for (int b = b0; b < b1; b++) {
+          crc = crc24_byte(crc, bytes[b], poly);
+        }
+        uint32_t part = b0 < nbytes ? clmul_mod24(crc, (crc_a ? a.xpow_a : a.xpow_b)[nbytes - b1], poly) : 0;
+#pragma unroll
+        for (int off = 1; off < 32; off <<= 1) {
+          part ^= (uint32_t)__shfl_xor((int)part, off, 64);
+        }
+        if (l32 == 0) {
+          RED[wave] = part;
+        }
+        __syncthreads();
+        const bool ok = (RED[0] ^ RED[1]) == 0;
+        if (ok && !done && live) {
+          const uint32_t slot = a.cbs[cbl].slot;
+          uint8_t*       out  = a.out + (size_t)slot * a.out_stride;
+          for (int b = t2; b < nbytes; b += 64) {
+            out[b] = bytes[b];
+          }
+          if (t2 == 0) {
+            a.noi_out[slot] = (uint8_t)(hi + 1);
+            a.crc_ok[slot]  = 1;
+          }
+        }
+        done = done || ok;
+      }
+      if (__syncthreads_or(!done) == 0) {
+        break;  // both blocks of the workgroup passed their CRC
+      }
+    }
+  }
+
+  // ---------------- hard decision of the last half-iteration (turbodecoder.c:370-378) ----------------
+  if (live && !done && h_end > 0) {
+    const int      cbm   = ES ? (int)a.cbs[cbl].slot : cbl;
+    uint8_t*       out   = a.out + (size_t)cbm * (ES ? a.out_stride : K / 8);
+    const uint8_t* bytes = reinterpret_cast<const uint8_t*>(c.BITS);
+    for (int b = t2; b < K / 8; b += 64) {
+      out[b] = bytes[b];
+    }
+    if (ES && t2 == 0) {
+      a.noi_out[cbm] = (uint8_t)a.n_end;
+      a.crc_ok[cbm]  = 0;
+    }
+  }
+}
+
+template <bool ES>
+__global__ __launch_bounds__(128, 2) void tdec16_kernel(TdecArgs a)
+{
+  tdec16_body<ES>(a, blockIdx.x);
+}
+
+// Several sizes of the class in one launch (tdec_multi_kernel of tdec_kernel.hip): workgroup b
+// belongs to the group g with first[g] <= b < first[g + 1].
+__global__ __launch_bounds__(128, 2) void tdec16_multi_kernel(const TdecArgs* __restrict__ groups,
+                                                           const uint32_t* __restrict__ first, int ngroups)
+{
+  const uint32_t b  = blockIdx.x;
+  int            lo = 0, hi = ngroups - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (first[mid] <= b) {
+      lo = mid;
+    } else {
+      hi = mid - 1;
+    }
+  }
+  const TdecArgs a = groups[lo];
+  tdec16_body<false>(a, (int)(b - first[lo]));
+}
+
+bool tdec16_eligible(int nsb, const TdecArgs& a)
+{
+  return nsb == 16 && a.layout_sb && a.n_start == 0 && a.state == nullptr && a.dbg == 0 && a.L >= (uint32_t)OVL;
+}
+
+size_t tdec16_lds_bytes(const TdecArgs& a)
+{
+  const Geo16 g = geo16((int)a.K, (int)a.Ls, (int)((a.L + W - 1) / W));
+  return (size_t)CPWG * g.cb_dw * 4;
+}
+
+int tdec16_cpw() { return CPWG; }
+
+hipError_t tdec16_launch(const TdecArgs& a, hipStream_t stream)
+{
+  StageScope timing_scope(ST_TDEC, stream);
+  const int    grid = (a.ncb + CPWG - 1) / CPWG;
+  const size_t lds  = tdec16_lds_bytes(a);
+  if (a.cbs) {
+    hipLaunchKernelGGL((tdec16_kernel<true>), dim3(grid), dim3(128), lds, stream, a);
+  } else {
+    hipLaunchKernelGGL((tdec16_kernel<false>), dim3(grid), dim3(128), lds, stream, a);
+  }
+  return hipGetLastError();
+}
+
+hipError_t tdec16_multi_launch(const TdecArgs* d_groups, const uint32_t* d_first, int ngroups, uint32_t nblocks,
+                               size_t lds, hipStream_t stream)
+{
+  StageScope timing_scope(ST_TDEC, stream);
+  if (ngroups == 0 || nblocks == 0) {
+    return hipSuccess;
+  }
+  hipLaunchKernelGGL(tdec16_multi_kernel, dim3(nblocks), dim3(128), lds, stream, d_groups, d_first, ngroups);
+  return hipGetLastError();
+}
+
+}  // namespace srsran_amd

@@ -126,7 +126,8 @@ Config* get_config(uint32_t K, int nsb)
     a.xyw = a.Ls;
     a.M   = (K + 3 + TDEC_W - 1) / TDEC_W;
   }
-  a.magicL = (uint32_t)(((1ull << 32) + a.L - 1) / a.L);
+  a.magicL  = (uint32_t)(((1ull << 32) + a.L - 1) / a.L);
+  a.magicLs = (uint32_t)(((1ull << 32) + a.Ls - 1) / a.Ls);
   if (tdec_lds_bytes(nsb, a.xyw, a.M) > kMaxLds) {
     return nullptr;
   }
@@ -714,7 +715,9 @@ int srsran_tdec_gpu_run_multi(uint32_t              nof_groups,
       ret = enqueue(cfg[g], d_input[g], in_stride[g], layout_sb, d_output[g], nof_cb[g], 0, n_end, nullptr, st);
       continue;
     }
-    const int      cpw   = tdec_cpw(cls_nsb[ci]);
+    // the 16-sub-block class on SB input runs the lane-pair decoder (tdec16_kernel.hip)
+    const bool     pair  = cls_nsb[ci] == 16 && layout_sb;
+    const int      cpw   = pair ? tdec16_cpw() : tdec_cpw(cls_nsb[ci]);
     const size_t   n     = gs.size();
     const size_t   abyte = n * sizeof(TdecArgs);
     const size_t   need  = abyte + n * sizeof(uint32_t);
@@ -758,15 +761,17 @@ int srsran_tdec_gpu_run_multi(uint32_t              nof_groups,
       ha[k]            = a;
       hf[k]            = nblk;
       nblk += (nof_cb[g] + cpw - 1) / cpw;
-      lds = std::max(lds, tdec_lds_bytes(c->nsb, a.xyw, a.M));
+      lds = std::max(lds, pair ? tdec16_lds_bytes(a) : tdec_lds_bytes(c->nsb, a.xyw, a.M));
     }
     if (hipMemcpyAsync(m.d_stage, m.h_stage, need, hipMemcpyHostToDevice, st) != hipSuccess) {
       return SRSRAN_ERROR;
     }
     hipEventRecord(m.copied, st);
     m.used = true;
-    if (tdec_multi_launch(cls_nsb[ci], reinterpret_cast<const TdecArgs*>(m.d_stage),
-                          reinterpret_cast<const uint32_t*>(m.d_stage + abyte), (int)n, nblk, lds, st) != hipSuccess) {
+    const TdecArgs* dg = reinterpret_cast<const TdecArgs*>(m.d_stage);
+    const uint32_t* df = reinterpret_cast<const uint32_t*>(m.d_stage + abyte);
+    if ((pair && dbg == 0 ? tdec16_multi_launch(dg, df, (int)n, nblk, lds, st)
+                          : tdec_multi_launch(cls_nsb[ci], dg, df, (int)n, nblk, lds, st)) != hipSuccess) {
       ret = SRSRAN_ERROR;
     }
   }

@@ -37,6 +37,7 @@ struct TdecArgs {
   uint32_t        xyw;       // LDS words per code block
   uint32_t        M;         // beta checkpoints per sub-block
   uint32_t        magicL;    // ceil(2^32 / L)
+  uint32_t        magicLs;   // ceil(2^32 / Ls)
   uint32_t        dbg;       // profiling ablation only (SRSRAN_TDEC_ABLATE): bit0 skip prepare, bit1 skip MAP
   // ---- DL-SCH mode (decode_tb_cb, sch.c:391-456): enabled when cbs != nullptr ----
   const struct TdecCb* cbs;  // per launch index: input pointer, skip flag, output slot, CRC type
@@ -57,6 +58,15 @@ hipError_t tdec_launch(int nsb, const TdecArgs& a, hipStream_t stream);
 hipError_t tdec_multi_launch(int nsb, const TdecArgs* d_groups, const uint32_t* d_first, int ngroups,
                              uint32_t nblocks, size_t lds, hipStream_t stream);
 int        tdec_cpw(int nsb);  // code blocks per workgroup
+
+// tdec16_kernel.hip: the lane-pair decoder of the 16-sub-block class on the SB input layout
+// (every plain / DL-SCH launch of K >= 816 without state save/restore)
+bool       tdec16_eligible(int nsb, const TdecArgs& a);
+hipError_t tdec16_launch(const TdecArgs& a, hipStream_t stream);
+hipError_t tdec16_multi_launch(const TdecArgs* d_groups, const uint32_t* d_first, int ngroups, uint32_t nblocks,
+                               size_t lds, hipStream_t stream);
+size_t     tdec16_lds_bytes(const TdecArgs& a);
+int        tdec16_cpw();
 size_t     tdec_lds_bytes(int nsb, int xyw, int M);
 // x^(8m) mod poly for m = 0..nm-1 (host helper for the CRC combine tables)
 void crc24_xpow_table(uint32_t poly, uint32_t* out, int nm);

@@ -821,6 +821,9 @@ hipError_t tdec_launch(int nsb, const TdecArgs& a, hipStream_t stream)
   if (a.ncb == 0) {
     return hipSuccess;
   }
+  if (tdec16_eligible(nsb, a)) {
+    return tdec16_launch(a, stream);
+  }
   switch (nsb) {
     case 16:
       return launch<16>(a, stream);

@@ -729,9 +729,15 @@ __global__ __launch_bounds__(128, 2) void tdec16_multi_kernel(const TdecArgs* __
   tdec16_body<false>(a, (int)(b - first[lo]));
 }
 
+// Two blocks a workgroup: the lane-pair kernel needs >= 2048 blocks in the launch to put two waves
+// on every SIMD (4 workgroups of 38 KB LDS per CU); smaller launches run tdec_kernel.hip's quad
+// decoder (one block per workgroup), which fills the chip with half as many.
+bool tdec16_pays(uint32_t ncb) { return ncb >= 2048; }
+
 bool tdec16_eligible(int nsb, const TdecArgs& a)
 {
-  return nsb == 16 && a.layout_sb && a.n_start == 0 && a.state == nullptr && a.dbg == 0 && a.L >= (uint32_t)OVL;
+  return nsb == 16 && a.layout_sb && a.n_start == 0 && a.state == nullptr && a.dbg == 0 && a.L >= (uint32_t)OVL &&
+         tdec16_pays(a.ncb);
 }
 
 size_t tdec16_lds_bytes(const TdecArgs& a)

@@ -716,7 +716,11 @@ int srsran_tdec_gpu_run_multi(uint32_t              nof_groups,
       continue;
     }
     // the 16-sub-block class on SB input runs the lane-pair decoder (tdec16_kernel.hip)
-    const bool     pair  = cls_nsb[ci] == 16 && layout_sb;
+    uint32_t       cls_cb = 0;
+    for (uint32_t g : gs) {
+      cls_cb += nof_cb[g];
+    }
+    const bool     pair  = cls_nsb[ci] == 16 && layout_sb && tdec16_pays(cls_cb);
     const int      cpw   = pair ? tdec16_cpw() : tdec_cpw(cls_nsb[ci]);
     const size_t   n     = gs.size();
     const size_t   abyte = n * sizeof(TdecArgs);

@@ -62,6 +62,7 @@ int        tdec_cpw(int nsb);  // code blocks per workgroup
 // tdec16_kernel.hip: the lane-pair decoder of the 16-sub-block class on the SB input layout
 // (every plain / DL-SCH launch of K >= 816 without state save/restore)
 bool       tdec16_eligible(int nsb, const TdecArgs& a);
+bool       tdec16_pays(uint32_t ncb);  // enough blocks in one launch for the lane-pair kernel
 hipError_t tdec16_launch(const TdecArgs& a, hipStream_t stream);
 hipError_t tdec16_multi_launch(const TdecArgs* d_groups, const uint32_t* d_first, int ngroups, uint32_t nblocks,
                                size_t lds, hipStream_t stream);

@@ -35,6 +35,7 @@
 //     (sch.c:426-456) on the bitmap.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "crc24_dev.h"
 #include "stage_timing.h"
@@ -732,7 +733,12 @@ __global__ __launch_bounds__(128, 2) void tdec16_multi_kernel(const TdecArgs* __
 // Two blocks a workgroup: the lane-pair kernel needs >= 2048 blocks in the launch to put two waves
 // on every SIMD (4 workgroups of 38 KB LDS per CU); smaller launches run tdec_kernel.hip's quad
 // decoder (one block per workgroup), which fills the chip with half as many.
-bool tdec16_pays(uint32_t ncb) { return ncb >= 2048; }
+// SRSRAN_TDEC16_MIN_CB overrides the threshold (tests force the lane-pair kernel on small batches).
+bool tdec16_pays(uint32_t ncb)
+{
+  const char* e = getenv("SRSRAN_TDEC16_MIN_CB");
+  return ncb >= (e ? (uint32_t)strtoul(e, nullptr, 10) : 2048u);
+}
 
 bool tdec16_eligible(int nsb, const TdecArgs& a)
 {

@@ -416,8 +416,14 @@ int enqueue_batch(srsran_sch_t* q, uint32_t ntb, const srsran_dlsch_gpu_tb_t* tb
     for (size_t g = 0; g < groups.size() && ret == SRSRAN_SUCCESS; g++) {
       const uint32_t first = groups[g].second;
       const uint32_t count = (g + 1 < groups.size() ? groups[g + 1].second : (uint32_t)cbs.size()) - first;
+      // the lane-pair decoder reads a workgroup's two blocks from the lower soft buffer's address
+      uintptr_t lo = UINTPTR_MAX, hi = 0;
+      for (uint32_t i = first; i < first + count; i++) {
+        lo = std::min(lo, (uintptr_t)cbs[i].in);
+        hi = std::max(hi, (uintptr_t)cbs[i].in);
+      }
       ret = tdec_sch_enqueue(groups[g].first, (const TdecCb*)(x->d_stage + off_cbs) + first, count, x->d_cbout,
-                             SCH_SLOT_BYTES, x->d_noi, x->d_crc_ok, n_end, stream);
+                             SCH_SLOT_BYTES, x->d_noi, x->d_crc_ok, n_end, hi - lo < (1u << 31), stream);
     }
   }
   if (ret == SRSRAN_SUCCESS && tb_launch((const SchTb*)(x->d_stage + off_tb), ntb, max_tbs, stream) != hipSuccess) {

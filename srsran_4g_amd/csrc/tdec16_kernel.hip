@@ -73,7 +73,6 @@ __device__ __forceinline__ v2s dpp(v2s a)
 }
 __device__ __forceinline__ v2s pswap(v2s a) { return dpp<QP(1, 0, 3, 2)>(a); }  // the other lane of the pair
 
-__device__ __forceinline__ uint32_t pack2(short lo, short hi) { return (uint32_t)(uint16_t)lo | ((uint32_t)(uint16_t)hi << 16); }
 
 // Per-lane v_perm selectors (j = lane & 1).
 struct PairSel {
@@ -192,120 +191,104 @@ __host__ __device__ __forceinline__ Geo16 geo16(int K, int Ls, int M)
   return g;
 }
 
-// One window of W inputs of this lane's sub-block, as loaded from global memory.
-// (kept as separate 16-bit registers: packing two loads into one VGPR at issue time would make
-// the wave wait for both right there and defeat the prefetch)
+// One window of W inputs of this lane's sub-block, as loaded from global memory (zero-extended:
+// the packing into (x, y) happens when the window starts, so the loads of the next window can be
+// in flight meanwhile).
 struct Raw {
-  short a[W];  // systematic LLR (DEC1) / slot of pi(position) (DEC2)
-  short b[W];  // parity0 / parity1
+  uint32_t a[W];  // systematic LLR (DEC1) / slot of pi(position) (DEC2)
+  uint32_t b[W];  // parity0 / parity1
 };
 
-// global-memory pointers (address space 1): the window loads must be global_load, not flat
-// (a flat load also counts in lgkmcnt, so every LDS wait would drain the prefetched window)
-typedef const short __attribute__((address_space(1)))*    gshort;
-typedef const uint16_t __attribute__((address_space(1)))* gushort;
+// Global loads through buffer resources: (uniform descriptor) + (per-lane 32-bit offset) +
+// (uniform window offset) + immediate, so a window costs no address arithmetic; the range check of
+// the descriptor turns reads past the block's buffer (the last, partial window) into zeros.
+typedef short __attribute__((address_space(3)))* lshort;
+typedef __amdgpu_buffer_rsrc_t                   rsrc_t;
+__device__ __forceinline__ uint32_t ldb(rsrc_t r, uint32_t voff, uint32_t soff, int imm)
+{
+  return __builtin_amdgcn_raw_buffer_load_b16(r, voff + imm, soff, 0);
+}
+__device__ __forceinline__ rsrc_t make_rsrc(const void* p, uint32_t bytes)
+{
+  const size_t   u  = (size_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((size_t)hi << 32) | lo), 0,
+                                           (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
 
 // Per-lane context of one half-iteration.
 struct Lane16 {
-  int             wave, l32, s, j, K, L, Ls, M, KP;
-  uint32_t        magicLs;
-  gshort          in;
-  gushort         tf;   // q order, SB input: slot of pi(n(q))
-  short*          S;    // this block's S (LDS)
-  uint32_t*       CK;   // this block's checkpoints (LDS)
-  uint32_t*       BITS; // this block's decision bitmap (LDS)
-  PairSel         ps;
+  int      wave, l32, s, j, K, L, Ls, M, KP;
+  uint32_t magicLs;
+  rsrc_t   rin;   // the workgroup's blocks' inputs, from the lower of the two
+  uint32_t voff;  // bytes from rin's base to this lane's first position (q = s) of its block
+  rsrc_t   rtf;   // tfwd (q order, SB input: slot of pi(n(q))), K entries
+  lshort   S;     // this block's S (LDS)
+  lshort   Ssb;   // S + s * Ls: this lane's sub-block
+  uint32_t* CK;   // this block's checkpoints (LDS)
+  uint32_t* BITS; // this block's decision bitmap (LDS)
+  PairSel  ps;
 };
 
-// Inputs of a window [t0, min(t0 + W, kend)) of this lane's sub-block (q = k*16 + s in the SB
-// layout): DEC1 loads systematic + parity0, DEC2 the pi slot + parity1.  FULL: the whole window
-// lies below kend; otherwise positions past kend are clamped to kend - 1 (loaded, never used) so
-// no load is predicated and no read leaves the block's buffer.
-template <bool D2, bool FULL>
-__device__ __forceinline__ void issue(const Lane16& c, Raw& r, int t0, int kend)
-{
-  const gshort par = c.in + (D2 ? 2 * c.KP : c.KP);
-#pragma unroll
-  for (int i = 0; i < W; i++) {
-    const int k = FULL ? t0 + i : min(t0 + i, kend - 1);
-    const int q = k * NSB + c.s;
-#if defined(T16_ABL) && (T16_ABL & 1)  // profiling ablation: no global loads
-    r.a[i] = (short)(q & 1023);
-    r.b[i] = (short)(q & 511);
-    (void)par;
-#else
-    r.a[i] = D2 ? (short)c.tf[q] : c.in[q];
-    r.b[i] = par[q];
-#endif
-  }
-}
-// Stage 2: the S values a window needs (DEC1: the a-priori S[a] of each position; DEC2: ext1 at
-// the pi slot b, whose address came with stage 1).
-template <bool D2, bool FULL>
-__device__ __forceinline__ void issue_lds(const Lane16& c, const Raw& r, int t0, int kend, short* dv)
-{
-#pragma unroll
-  for (int i = 0; i < W; i++) {
-    const int k = FULL ? t0 + i : min(t0 + i, kend - 1);
-#if defined(T16_ABL) && (T16_ABL & 2)  // profiling ablation: no LDS reads of S
-    dv[i] = (short)(k & 255);
-    (void)r;
-#else
-    dv[i] = D2 ? c.S[(uint16_t)r.a[i]] : c.S[c.s * c.Ls + k];
-#endif
-  }
-}
-// Stage 3: branch inputs (x, y) packed, and what the output needs: DEC1 the a-priori value,
-// DEC2 the slot b (x = S[b] is xw.lo).
+// Inputs of the window at t0 of this lane's sub-block (q = k*16 + s in the SB layout): DEC1 loads
+// systematic + parity0, DEC2 the pi slot + parity1.  Positions past the sub-block (the last,
+// partial window) load a neighbour's value or, past the buffer, zero; they are never used.
 template <bool D2>
-__device__ __forceinline__ void combine(const Raw& r, const short* dv, uint32_t* xw, short* aux)
+__device__ __forceinline__ void issue(const Lane16& c, Raw& r, int t0)
 {
+  const uint32_t soff = 32u * (uint32_t)t0;
+  const uint32_t poff = soff + (D2 ? 4u : 2u) * (uint32_t)c.KP;  // parity stream, bytes
 #pragma unroll
   for (int i = 0; i < W; i++) {
-    short x;
-    if (D2) {
-      x      = dv[i];
-      aux[i] = r.a[i];
-    } else {
-      x      = __builtin_elementwise_add_sat(r.a[i], dv[i]);
-      aux[i] = dv[i];
-    }
-    xw[i] = pack2(x, r.b[i]);
+    r.a[i] = D2 ? ldb(c.rtf, 2u * (uint32_t)c.s, soff, 32 * i) : ldb(c.rin, c.voff, soff, 32 * i);
+    r.b[i] = ldb(c.rin, c.voff, poff, 32 * i);
   }
 }
 
-// The LLR o of position k: S update (vec_sub, wraps) and the decision bit (ORed every
-// half-iteration, no branch; the bitmap is cleared before each one).
-template <bool D2>
-__device__ __forceinline__ void emit(const Lane16& c, int k, short o, short aux, uint32_t xw)
+// The packed branch input of a position stays one register: an opaque move after packing keeps
+// the compiler from re-deriving it from the two halves at every use.
+__device__ __forceinline__ uint32_t pin(uint32_t v)
 {
-  int   slot, n;
-  short sub;
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
+// The LLR o of position k: S update (vec_sub, wraps) and, when the half-iteration's decision is
+// needed, its bit (turbodecoder.c:370-378: the sign of ext1 after DEC1, of app1 after DEC2).
+// DEC1 writes slot s*Ls + k and decides bit n = s*L + k; DEC2 writes the pi slot b (aux = its LDS
+// address, x = the ext1 read there) and decides the natural position of b.
+template <bool D2, bool BITS>
+__device__ __forceinline__ void emit(const Lane16& c, int k, short o, uint32_t aux, uint32_t xw)
+{
+  int n;
   if (D2) {
-    slot         = (uint16_t)aux;
-    const int sb = (int)__umulhi((uint32_t)slot, c.magicLs);
-    n            = slot - sb * (c.Ls - c.L);
-    sub          = (short)(xw & 0xffffu);  // x = ext1 at slot b
+    const lshort p = (lshort)(size_t)aux;
+    *p             = (short)(o - (short)(xw & 0xffffu));
+    if (BITS) {
+      const int slot = (int)(p - c.S);
+      const int sb   = (int)__umulhi((uint32_t)slot, c.magicLs);
+      n              = slot - sb * (c.Ls - c.L);
+    }
   } else {
-    slot = c.s * c.Ls + k;
-    n    = c.s * c.L + k;
-    sub  = aux;                            // app1 used by this DEC1
+    c.Ssb[k] = (short)(o - (short)aux);
+    n        = c.s * c.L + k;
   }
-#if defined(T16_ABL) && (T16_ABL & 4)  // profiling ablation: no output stores
-  if (o == 12345) {
-#endif
-  c.S[slot] = (short)(o - sub);
-  atomicOr(&c.BITS[n >> 5], (uint32_t)(o > 0) << (((n >> 3) & 3) * 8 + 7 - (n & 7)));
-#if defined(T16_ABL) && (T16_ABL & 4)
+  if (BITS) {
+    atomicOr(&c.BITS[n >> 5], (uint32_t)(o > 0) << (((n >> 3) & 3) * 8 + 7 - (n & 7)));
   }
-#endif
 }
 
-// Phase-2 alpha side, window at t0 (alpha_window of tdec_kernel.hip): beta[t0+1 .. cc] recomputed
-// from the stored beta at cc = min(t0 + W, L) (checkpoint), then alpha + LLR of t0 .. cc-1.
-template <bool D2, bool FULL>
+// normalize_period 2 on the absolute position k = t0 + i of a window (t0 a multiple of W): every
+// even position except k = 0; only i = 0 depends on the window.
+__device__ __forceinline__ bool nrm(int t0, int i) { return (i & 1) == 0 && (i != 0 || t0 != 0); }
+
+// Phase-2 alpha side, window at t0 >= W (alpha_window of tdec_kernel.hip): beta[t0+1 .. cc]
+// recomputed from the stored beta at cc = min(t0 + W, L) (checkpoint), then alpha + LLR of
+// t0 .. cc-1.
+template <bool D2, bool BITS, bool FULL>
 __device__ __forceinline__ St alpha_llr_window(const Lane16& c, St P, int t0, St Pb, const uint32_t* xw,
-                                               const short* aux)
+                                               const uint32_t* aux)
 {
   const int L  = c.L;
   const int cc = FULL ? t0 + W : L;
@@ -319,7 +302,7 @@ __device__ __forceinline__ St alpha_llr_window(const Lane16& c, St P, int t0, St
     } else if (FULL || i < ic) {
       Pb    = beta_step(Pb, u2v(xw[i + 1]), c.ps);
       bw[i] = Pb;
-      if (norm_at(t0 + 1 + i)) Pb = norm(Pb);
+      if (FULL ? (i & 1) : norm_at(t0 + 1 + i)) Pb = norm(Pb);
     }
   }
 #pragma unroll
@@ -328,15 +311,15 @@ __device__ __forceinline__ St alpha_llr_window(const Lane16& c, St P, int t0, St
       const Cand  cd = alpha_cand(P, u2v(xw[i]));
       const short o  = llr_out(bw[i], cd);
       P              = alpha_next(cd, c.ps);
-      if (norm_at(t0 + i)) P = norm(P);
-      emit<D2>(c, t0 + i, o, aux[i], xw[i]);
+      if ((i & 1) == 0) P = norm(P);  // t0 >= W: every even position
+      emit<D2, BITS>(c, t0 + i, o, aux[i], xw[i]);
     }
   }
   return P;
 }
 
-// Phase-1 beta side, window at t0: backward over t0+W-1 .. t0 (FULL) or L-1 .. t0; Bst = the stored
-// beta at t0, which is the checkpoint of window t0/W - 1 when `store`.
+// Phase-1 beta side, window at t0 >= W: backward over t0+W-1 .. t0 (FULL) or L-1 .. t0; Bst = the
+// stored beta at t0, which is the checkpoint of window t0/W - 1 when `store`.
 template <bool FULL>
 __device__ __forceinline__ St beta_window(const Lane16& c, St P, int t0, bool store, St& Bst, const uint32_t* xw)
 {
@@ -350,7 +333,7 @@ __device__ __forceinline__ St beta_window(const Lane16& c, St P, int t0, bool st
           *reinterpret_cast<uint2*>(&c.CK[ck_word(t0 / W - 1, c.l32)]) = make_uint2(v2u(P.v0), v2u(P.v1));
         }
       }
-      if (norm_at(t0 + i)) P = norm(P);
+      if ((i & 1) == 0) P = norm(P);
     }
   }
   return P;
@@ -367,10 +350,10 @@ __device__ __forceinline__ St beta_window(const Lane16& c, St P, int t0, bool st
 // has read it, and no position is read again later.
 template <bool D2>
 struct Pipe16 {
-  Raw   g;      // global loads of the next window (in flight)
-  short dv[W];  // DEC1: its S values (in flight); DEC2: this window's gathers
-  int   nwin, Ma;
-  bool  beta;
+  Raw      g;      // global loads of the next window (in flight)
+  uint32_t dv[W];  // DEC1: its S values (in flight)
+  int      nwin, Ma;
+  bool     beta;
 
   __device__ __forceinline__ int t0_of(int idx, int L) const
   {
@@ -379,47 +362,53 @@ struct Pipe16 {
     }
     return idx < 3 ? L - OVL + W * idx : (idx - 3) * W;
   }
-  __device__ __forceinline__ int kend_of(int idx, int L) const { return beta && idx < 3 ? OVL : L; }
-  __device__ __forceinline__ bool full_of(int idx, int L) const { return t0_of(idx, L) + W <= kend_of(idx, L); }
 
   __device__ __forceinline__ void load(const Lane16& c, int idx)
   {
     if (idx < nwin) {
-      const int t0 = t0_of(idx, c.L), ke = kend_of(idx, c.L);
-      if (full_of(idx, c.L)) {
-        issue<D2, true>(c, g, t0, ke);
-        if (!D2) {
-          issue_lds<D2, true>(c, g, t0, ke, dv);
-        }
-      } else {
-        issue<D2, false>(c, g, t0, ke);
-        if (!D2) {
-          issue_lds<D2, false>(c, g, t0, ke, dv);
+      const int t0 = t0_of(idx, c.L);
+      issue<D2>(c, g, t0);
+      if (!D2) {  // S of the window's positions; past the sub-block: a neighbour's slot (unused)
+#pragma unroll
+        for (int i = 0; i < W; i++) {
+          dv[i] = (uint16_t)c.Ssb[t0 + i];
         }
       }
     }
   }
   __device__ __forceinline__ void start(const Lane16& c) { load(c, 0); }
-  // window idx begins: its (x, y) and output aux; the loads of idx + 1 are issued
-  __device__ __forceinline__ void next(const Lane16& c, int idx, uint32_t* xw, short* aux)
+  // window idx begins: its packed (x, y) and output aux; the loads of idx + 1 are issued.
+  //   DEC1: xw = (sat(syst + S[a]), parity0), aux = S[a]
+  //   DEC2: xw = (S[b], parity1), aux = LDS address of S[b]
+  __device__ __forceinline__ void next(const Lane16& c, int idx, uint32_t* xw, uint32_t* aux)
   {
-    Raw cur = g;
     if (D2) {
-      const int t0 = t0_of(idx, c.L), ke = kend_of(idx, c.L);
-      issue_lds<D2, true>(c, cur, t0, ke, dv);  // slots come from the table: no clamping needed
-    }
-    short dcur[W];
+      uint32_t d[W], hi[W];
 #pragma unroll
-    for (int i = 0; i < W; i++) {
-      dcur[i] = dv[i];
+      for (int i = 0; i < W; i++) {
+        aux[i] = (uint32_t)(size_t)(c.S + g.a[i]);
+        d[i]   = (uint16_t)*(lshort)(size_t)aux[i];
+        hi[i]  = g.b[i] << 16;
+      }
+      load(c, idx + 1);
+#pragma unroll
+      for (int i = 0; i < W; i++) {
+        xw[i] = pin(hi[i] | d[i]);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < W; i++) {
+        xw[i]  = pin(v2u(padd(u2v(__builtin_amdgcn_perm(g.b[i], g.a[i], 0x05040100u)), u2v(dv[i]))));
+        aux[i] = dv[i];
+      }
+      load(c, idx + 1);
     }
-    load(c, idx + 1);
-    combine<D2>(cur, dcur, xw, aux);
   }
 };
 
 // One constituent MAP decode of this lane's sub-block; wave 0 = alpha side, wave 1 = beta side.
-template <bool D2>
+// BITS: the half-iteration's hard decision is recorded (early stop / the last half-iteration).
+template <bool D2, bool BITS>
 __device__ __forceinline__ void map16(const Lane16& cin)
 {
   // Opaque copy of the per-lane sub-block index: every window address derives from it, so none
@@ -427,6 +416,12 @@ __device__ __forceinline__ void map16(const Lane16& cin)
   // across it and spill).
   Lane16 c = cin;
   asm volatile("" : "+v"(c.s));
+  asm volatile("" : "+v"(c.voff));
+  {
+    uint32_t ssb = (uint32_t)(size_t)c.Ssb;
+    asm volatile("" : "+v"(ssb));
+    c.Ssb = (lshort)(size_t)ssb;
+  }
   const int L     = c.L;
   const int Mfull = L / W;            // windows entirely below L
   const int Ma    = (L + W - 1) / W;  // = c.M
@@ -437,7 +432,7 @@ __device__ __forceinline__ void map16(const Lane16& cin)
   pp.Ma   = Ma;
   pp.beta = c.wave != 0;
   uint32_t xw[W];
-  short    aux[W];
+  uint32_t aux[W];
   pp.start(c);
   if (c.wave == 0) {
     // ================= alpha side =================
@@ -476,23 +471,23 @@ __device__ __forceinline__ void map16(const Lane16& cin)
 #pragma unroll
       for (int i = 0; i < W; i++) {
         P = alpha_next(alpha_cand(P, u2v(xw[i])), ps);
-        if (norm_at(t0 + i)) P = norm(P);
+        if (nrm(t0, i)) P = norm(P);
       }
     }
     __syncthreads();
     // phase 2: windows [h, Ma): beta recomputed from the checkpoint above the window, then
     // alpha + LLR; the last window may be partial
+    // (the partial window is peeled so the loop body stays one straight-line block)
 #pragma unroll 1
-    for (int ma = h; ma < Ma; ma++) {
-      const int t0 = ma * W;
+    for (int ma = h; ma < Mfull; ma++) {
       pp.next(c, 3 + ma, xw, aux);
       const uint2 ckv = *reinterpret_cast<const uint2*>(&c.CK[ck_word(ma, c.l32)]);
-      const St    Pb{u2v(ckv.x), u2v(ckv.y)};
-      if (ma < Mfull) {
-        P = alpha_llr_window<D2, true>(c, P, t0, Pb, xw, aux);
-      } else {
-        P = alpha_llr_window<D2, false>(c, P, t0, Pb, xw, aux);
-      }
+      P = alpha_llr_window<D2, BITS, true>(c, P, ma * W, St{u2v(ckv.x), u2v(ckv.y)}, xw, aux);
+    }
+    if (Ma > Mfull) {
+      pp.next(c, 3 + Mfull, xw, aux);
+      const uint2 ckv = *reinterpret_cast<const uint2*>(&c.CK[ck_word(Mfull, c.l32)]);
+      alpha_llr_window<D2, BITS, false>(c, P, Mfull * W, St{u2v(ckv.x), u2v(ckv.y)}, xw, aux);
     }
   } else {
     // ================= beta side =================
@@ -521,12 +516,12 @@ __device__ __forceinline__ void map16(const Lane16& cin)
       q.v0 = u2v((uint32_t)__shfl_down((int)v2u(P.v0), 2, 64));
       q.v1 = u2v((uint32_t)__shfl_down((int)v2u(P.v1), 2, 64));
       if (c.s == NSB - 1) {  // trellis termination: systematic / parity0 (DEC1), app2 / parity1 (DEC2)
-        const gshort tail = c.in + 3 * c.KP + (D2 ? 6 : 0);
-        short        xt[3], yt[3];
+        const int tail = 6 * c.KP + (D2 ? 12 : 0);  // bytes
+        short     xt[3], yt[3];
 #pragma unroll
         for (int t = 0; t < 3; t++) {
-          xt[t] = tail[2 * t];
-          yt[t] = tail[2 * t + 1];
+          xt[t] = (short)ldb(c.rin, c.voff - 2 * c.s, tail, 4 * t);
+          yt[t] = (short)ldb(c.rin, c.voff - 2 * c.s, tail, 4 * t + 2);
         }
         P = trellis_pair(xt, yt, c.j);
       } else {
@@ -538,15 +533,15 @@ __device__ __forceinline__ void map16(const Lane16& cin)
     St Bst = P;  // stored (pre-normalisation) beta of the position above the current window
     // phase 1: windows [h, Ma) from the top (the top one maybe partial); the stored beta at the
     // start of window mb is the checkpoint of window mb - 1 (slot mb - 1) for mb > h
+    // (the partial top window is peeled so the loop body stays one straight-line block)
+    if (Ma > Mfull) {
+      pp.next(c, 3, xw, aux);
+      P = beta_window<false>(c, P, mtop * W, mtop > h, Bst, xw);
+    }
 #pragma unroll 1
-    for (int mb = mtop; mb >= h; mb--) {
-      const int t0 = mb * W;
+    for (int mb = Mfull - 1; mb >= h; mb--) {
       pp.next(c, 3 + mtop - mb, xw, aux);
-      if (mb < Mfull) {
-        P = beta_window<true>(c, P, t0, mb > h, Bst, xw);
-      } else {
-        P = beta_window<false>(c, P, t0, mb > h, Bst, xw);
-      }
+      P = beta_window<true>(c, P, mb * W, mb > h, Bst, xw);
     }
     __syncthreads();
     // phase 2: windows [0, h) from the top: alpha recomputed from the entry checkpoint, then
@@ -563,7 +558,7 @@ __device__ __forceinline__ void map16(const Lane16& cin)
         aw[i] = Pa;
         if (i < W - 1) {
           Pa = alpha_next(alpha_cand(Pa, u2v(xw[i])), ps);
-          if (norm_at(t0 + i)) Pa = norm(Pa);
+          if (nrm(t0, i)) Pa = norm(Pa);
         }
       }
 #pragma unroll
@@ -571,8 +566,8 @@ __device__ __forceinline__ void map16(const Lane16& cin)
         const short o = llr_out(Bst, alpha_cand(aw[i], u2v(xw[i])));
         P             = beta_step(P, u2v(xw[i]), ps);
         Bst           = P;
-        if (norm_at(t0 + i)) P = norm(P);
-        emit<D2>(c, t0 + i, o, aux[i], xw[i]);
+        if (nrm(t0, i)) P = norm(P);
+        emit<D2, BITS>(c, t0 + i, o, aux[i], xw[i]);
       }
     }
   }
@@ -611,12 +606,30 @@ __device__ __forceinline__ void tdec16_body(const TdecArgs& a, int bid)
   c.M       = M;
   c.KP      = K + 32;  // SB stream stride (rm_turbo.c:260-273)
   c.magicLs = a.magicLs;
-  c.in      = (gshort)(ES ? a.cbs[cbl].in : a.in + (size_t)cbl * a.in_stride);
-  c.tf      = (gushort)a.tfwd;
-  c.S       = reinterpret_cast<short*>(base);
-  c.CK      = base + g.s_dw;
-  c.BITS    = c.CK + g.ck_dw;
-  c.ps      = pair_sel(c.j);
+  // the workgroup's two blocks read through one uniform base: the lower of their inputs (plain
+  // launches: in_stride apart; DL-SCH: soft buffers the host checked to lie < 2 GB apart)
+  const int cb0 = bid * CPWG;
+  size_t    in_lane, in_base, in_hi;
+  if (ES) {
+    const size_t p0 = (size_t)a.cbs[min(cb0, (int)a.ncb - 1)].in;
+    const size_t p1 = (size_t)a.cbs[min(cb0 + 1, (int)a.ncb - 1)].in;
+    in_base         = min(p0, p1);
+    in_hi           = max(p0, p1);
+    in_lane         = (size_t)a.cbs[cbl].in;
+  } else {
+    in_base = (size_t)(a.in + (size_t)min(cb0, (int)a.ncb - 1) * a.in_stride);
+    in_hi   = (size_t)(a.in + (size_t)min(cb0 + 1, (int)a.ncb - 1) * a.in_stride);
+    in_lane = (size_t)(a.in + (size_t)cbl * a.in_stride);
+  }
+  const uint32_t cb_bytes = (uint32_t)(3 * c.KP + 12) * 2;  // one block's soft-buffer input
+  c.rin  = make_rsrc((const void*)in_base, (uint32_t)(in_hi - in_base) + cb_bytes);
+  c.voff = (uint32_t)(in_lane - in_base) + 2 * c.s;
+  c.rtf  = make_rsrc(a.tfwd, 2u * (uint32_t)K);
+  c.S    = (lshort)(short*)base;
+  c.Ssb  = c.S + c.s * Ls;
+  c.CK   = base + g.s_dw;
+  c.BITS = c.CK + g.ck_dw;
+  c.ps   = pair_sel(c.j);
   uint32_t* RED = c.BITS + g.bits_dw;
 
   if constexpr (ES) {
@@ -639,10 +652,20 @@ __device__ __forceinline__ void tdec16_body(const TdecArgs& a, int bid)
       smem[(i / g.bits_dw) * g.cb_dw + g.s_dw + g.ck_dw + i % g.bits_dw] = 0u;
     }
     __syncthreads();
+    // decisions: every half-iteration the early stop checks, else only the last one
+    const bool bits = ES ? crc_now : hi + 1 == h_end;
     if (hi & 1) {
-      map16<true>(c);
+      if (bits) {
+        map16<true, true>(c);
+      } else {
+        map16<true, false>(c);
+      }
     } else {
-      map16<false>(c);
+      if (bits) {
+        map16<false, true>(c);
+      } else {
+        map16<false, false>(c);
+      }
     }
     __syncthreads();
 
@@ -730,20 +753,21 @@ __global__ __launch_bounds__(128, 2) void tdec16_multi_kernel(const TdecArgs* __
   tdec16_body<false>(a, (int)(b - first[lo]));
 }
 
-// Two blocks a workgroup: the lane-pair kernel needs >= 2048 blocks in the launch to put two waves
-// on every SIMD (4 workgroups of 38 KB LDS per CU); smaller launches run tdec_kernel.hip's quad
-// decoder (one block per workgroup), which fills the chip with half as many.
+// Two blocks a workgroup: a launch of fewer than 1024 blocks fits tdec_kernel.hip's quad decoder in one
+// round (one block per workgroup, 4 per CU) with more SIMDs busy than the lane-pair kernel; at 1024
+// blocks the two tie (K = 6144: 0.388 vs 0.391 ms) and above the quad decoder needs a second round.
+
 // SRSRAN_TDEC16_MIN_CB overrides the threshold (tests force the lane-pair kernel on small batches).
 bool tdec16_pays(uint32_t ncb)
 {
   const char* e = getenv("SRSRAN_TDEC16_MIN_CB");
-  return ncb >= (e ? (uint32_t)strtoul(e, nullptr, 10) : 2048u);
+  return ncb >= (e ? (uint32_t)strtoul(e, nullptr, 10) : 1024u);
 }
 
 bool tdec16_eligible(int nsb, const TdecArgs& a)
 {
   return nsb == 16 && a.layout_sb && a.n_start == 0 && a.state == nullptr && a.dbg == 0 && a.L >= (uint32_t)OVL &&
-         tdec16_pays(a.ncb);
+         (a.cbs == nullptr || a.in_near) && tdec16_pays(a.ncb);
 }
 
 size_t tdec16_lds_bytes(const TdecArgs& a)

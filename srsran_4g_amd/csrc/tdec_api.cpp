@@ -292,6 +292,7 @@ int tdec_sch_enqueue(uint32_t      K,
                      uint8_t*      d_noi,
                      uint8_t*      d_crc_ok,
                      int           n_end,
+                     bool          in_near,
                      hipStream_t   stream)
 {
   if (ncb == 0) {
@@ -322,6 +323,7 @@ int tdec_sch_enqueue(uint32_t      K,
   a.xpow_a     = xp->d[0];
   a.xpow_b     = xp->d[1];
   a.min_iters  = 2;  // SRSRAN_PDSCH_MIN_TDEC_ITERS (sch.c:35)
+  a.in_near    = in_near ? 1 : 0;
   hipError_t e = tdec_launch(c->nsb, a, stream);
   if (e != hipSuccess) {
     fprintf(stderr, "[srsran_sch] turbo launch failed: %s\n", hipGetErrorString(e));

@@ -47,6 +47,7 @@ struct TdecArgs {
   const uint32_t* xpow_a;    // x^(8m) mod CRC24A, m = 0..768 (device)
   const uint32_t* xpow_b;    // x^(8m) mod CRC24B
   int             min_iters; // early stop needs at least this many half-iterations (sch.c:35)
+  uint32_t        in_near;   // every cbs[].in lies within 2 GB of the others (lane-pair kernel)
 };
 
 static constexpr uint32_t LTE_CRC24A = 0x1864CFB;  // phy_common.h:72
@@ -83,6 +84,7 @@ int tdec_sch_enqueue(uint32_t      K,
                      uint8_t*      d_noi,
                      uint8_t*      d_crc_ok,
                      int           n_end,
+                     bool          in_near,
                      hipStream_t   stream);
 int tdec_cb_index(uint32_t K);
 

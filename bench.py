@@ -924,7 +924,7 @@ def main():
     torch.cuda.synchronize()
     per_kernel = {}
     for K, e0, e1 in events:
-        name = tdec.load_library().srsran_tdec_gpu_kernel_name(K).decode()
+        name = tdec.load_library().srsran_tdec_gpu_kernel_name_batch(K, args.batch).decode()
         ms = e0.elapsed_time(e1)
         d = per_kernel.setdefault(name, {"launches": 0, "ms": 0.0, "bytes": 0, "bits": 0})
         d["launches"] += 1
@@ -933,8 +933,8 @@ def main():
         d["bits"] += args.batch * K
     if len(Ks) > 1:
         # the timed step runs one fused launch per decoder class; its dominant kernel is the
-        # 16-sub-block class (tdec_multi_kernel<16>: every K >= 816 of the batch in one grid),
-        # timed here alone with events on the launch stream
+        # 16-sub-block class (tdec16_multi_kernel, the lane-pair decoder: every K >= 816 of the
+        # batch in one grid), timed here alone with events on the launch stream
         k16 = [i for i, K in enumerate(Ks) if tdec.nof_subblocks(K) == 16]
         sel = [[groups[j][i] for i in k16] for j in range(5)]
         ms16 = []
@@ -946,7 +946,7 @@ def main():
             e1.record(stream)
             torch.cuda.synchronize()
             ms16.append(e0.elapsed_time(e1))
-        dom = "tdec_multi_kernel<16>"
+        dom = "tdec16_multi_kernel" if args.batch * len(k16) >= 1024 else "tdec_multi_kernel<16>"
         avg_ms = float(np.mean(ms16))
         bytes_per_launch = sum(args.batch * algo_bytes(Ks[i]) for i in k16)
         dom_units = args.batch * len(k16)

@@ -144,6 +144,10 @@ int srsran_tdec_gpu_available(void);
 /* Name of the decoder kernel used for long_cb (for profiling reports), or NULL. */
 const char* srsran_tdec_gpu_kernel_name(uint32_t long_cb);
 
+/* Name of the kernel a batch of nof_cb blocks of long_cb on the SB layout runs (the lane-pair
+   decoder of K >= 816 from 1024 blocks a launch), for profiling reports. */
+const char* srsran_tdec_gpu_kernel_name_batch(uint32_t long_cb, uint32_t nof_cb);
+
 #ifdef __cplusplus
 }
 #endif

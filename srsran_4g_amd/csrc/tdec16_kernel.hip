@@ -430,7 +430,7 @@ __device__ __forceinline__ void map16(const Lane16& cin)
   Pipe16<D2> pp;
   pp.nwin = 3 + Ma;
   pp.Ma   = Ma;
-  pp.beta = c.wave != 0;
+  pp.beta = __builtin_amdgcn_readfirstlane(c.wave) != 0;  // wave-uniform: window offsets stay scalar
   uint32_t xw[W];
   uint32_t aux[W];
   pp.start(c);

@@ -379,6 +379,11 @@ const char* srsran_tdec_gpu_kernel_name(uint32_t long_cb)
   }
 }
 
+const char* srsran_tdec_gpu_kernel_name_batch(uint32_t long_cb, uint32_t nof_cb)
+{
+  return auto_nsb(long_cb) == 16 && tdec16_pays(nof_cb) ? "tdec16_kernel" : srsran_tdec_gpu_kernel_name(long_cb);
+}
+
 int srsran_tdec_init(srsran_tdec_t* h, uint32_t max_long_cb)
 {
   return srsran_tdec_init_manual(h, max_long_cb, SRSRAN_TDEC_AUTO);

@@ -87,6 +87,7 @@ def load_library():
                                        ctypes.c_void_p], ctypes.c_int),
         "srsran_tdec_gpu_available": ([], ctypes.c_int),
         "srsran_tdec_gpu_kernel_name": ([u32], ctypes.c_char_p),
+        "srsran_tdec_gpu_kernel_name_batch": ([u32, u32], ctypes.c_char_p),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)

@@ -281,13 +281,26 @@ int srsran_pdsch_gpu_decode_batch(srsran_pdsch_t*              q,
                                   void*                        stream);
 
 /* ---------------- UE DL (ue/ue_dl.h:77-207, ue_dl.c) ----------------
- * The PDSCH-decode slice of srsran_ue_dl_t.  PCFICH / PDCCH / PHICH / PMCH are out of scope:
- * decode_fft_estimate takes the CFI from sf->cfi (1..3) and grants are supplied by the caller. */
+ * decode_fft_estimate: OFDM, CRS estimation, PCFICH (sets sf->cfi) and the PDCCH LLRs, all on the
+ * GPU, for cells of 1 or 2 ports with normal PHICH duration (other cells: the CFI is the caller's
+ * sf->cfi).  srsran_ue_dl_find_dl_dci / srsran_ue_dl_dci_to_pdsch_grant are in srsran_pdcch.h.
+ * PHICH / PMCH are not provided.  srsran_dl_cfg_t omits the reference's leading cqi_report. */
 typedef enum { SRSRAN_TM1 = 0, SRSRAN_TM2, SRSRAN_TM3, SRSRAN_TM4, SRSRAN_TM5, SRSRAN_TM6, SRSRAN_TM7, SRSRAN_TM8,
                SRSRAN_TMINV } srsran_tm_t;
 
+/* phch/dci.h:52-59 (DCI size options) */
+typedef struct {
+  bool multiple_csi_request_enabled;
+  bool cif_enabled;
+  bool cif_present;
+  bool srs_request_enabled;
+  bool ra_format_enabled;
+  bool is_not_ue_ss;
+} srsran_dci_cfg_t;
+
 typedef struct {
   srsran_pdsch_cfg_t pdsch;
+  srsran_dci_cfg_t   dci;
   srsran_tm_t        tm;
   bool               dci_common_ss;
 } srsran_dl_cfg_t;

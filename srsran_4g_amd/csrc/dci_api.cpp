@@ -1,0 +1,727 @@
+// srsran_4g_amd/csrc/dci_api.cpp -- DCI sizes and unpacking, and the DL resource allocation that
+// turns a DCI into a PDSCH grant (include/srsran_pdcch.h).  Host code: a few hundred bit fields per
+// subframe, nothing for the GPU.
+//
+//   DCI sizes      phch/dci.c:93-413 (FDD: 3-bit HARQ process number, no DAI)
+//   DCI unpack     phch/dci.c:641-708 (format 1), :797-897 (1A), :1153-1241 (2 / 2A), :1288-1340
+//   RA             phch/ra.c:37-250 (RIV, RBG size P, MCS -> I_TBS / modulation, TBS table)
+//                  phch/ra_dl.c:42-681 (PRB allocation types 0 / 1 / 2, TB sizes, RE count, MIMO)
+// Not provided (SRSRAN_ERROR): TDD, format 1B / 1C / 1D / 2B unpacking, distributed VRBs.
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+
+#include "../../include/srsran_pdcch.h"
+
+namespace {
+
+#include "tbs_table.inc"
+
+uint32_t riv_nbits(uint32_t nof_prb)
+{
+  return (uint32_t)ceilf(log2f((float)nof_prb * ((float)nof_prb + 1) / 2));
+}
+
+bool is_ambiguous_size(uint32_t n)
+{
+  static const uint32_t sizes[10] = {12, 14, 16, 20, 24, 26, 32, 40, 44, 56};
+  for (uint32_t s : sizes) {
+    if (n == s) {
+      return true;
+    }
+  }
+  return false;
+}
+
+constexpr uint32_t HARQ_PID_LEN = 3;  // FDD
+
+uint32_t format0_size_(const srsran_cell_t* cell, const srsran_dci_cfg_t* cfg)
+{
+  return (cfg->cif_enabled ? 3 : 0) + 1 + 1 + riv_nbits(cell->nof_prb) + 5 + 1 + 2 + 3 +
+         ((cfg->multiple_csi_request_enabled && !cfg->is_not_ue_ss) ? 2 : 1) +
+         ((cfg->srs_request_enabled && !cfg->is_not_ue_ss) ? 1 : 0) + 1;
+}
+
+uint32_t format1A_size(const srsran_cell_t* cell, const srsran_dci_cfg_t* cfg)
+{
+  uint32_t n = (cfg->cif_enabled ? 3 : 0) + 1 + 1 + riv_nbits(cell->nof_prb) + 5 + HARQ_PID_LEN + 1 + 2 + 2 +
+               (cfg->srs_request_enabled ? 1 : 0);
+  while (n < format0_size_(cell, cfg)) {
+    n++;
+  }
+  if (is_ambiguous_size(n)) {
+    n++;
+  }
+  return n;
+}
+
+uint32_t format0_size(const srsran_cell_t* cell, const srsran_dci_cfg_t* cfg)
+{
+  uint32_t n = format0_size_(cell, cfg);
+  while (n < format1A_size(cell, cfg)) {
+    n++;
+  }
+  return n;
+}
+
+uint32_t rbg_bits(uint32_t nof_prb) { return (uint32_t)ceilf((float)nof_prb / srsran_ra_type0_P(nof_prb)); }
+
+uint32_t ra_type2_ngap(uint32_t nof_prb, bool ngap_is_1)  // ra.c:81-103
+{
+  if (nof_prb <= 10) {
+    return nof_prb / 2;
+  } else if (nof_prb == 11) {
+    return 4;
+  } else if (nof_prb <= 19) {
+    return 8;
+  } else if (nof_prb <= 26) {
+    return 12;
+  } else if (nof_prb <= 44) {
+    return 18;
+  } else if (nof_prb <= 49) {
+    return 27;
+  } else if (nof_prb <= 63) {
+    return ngap_is_1 ? 27 : 9;
+  } else if (nof_prb <= 79) {
+    return ngap_is_1 ? 32 : 16;
+  }
+  return ngap_is_1 ? 48 : 16;
+}
+
+uint32_t ra_type2_n_vrb_dl(uint32_t nof_prb, bool ngap_is_1)  // ra.c:115-124
+{
+  const uint32_t ngap = ra_type2_ngap(nof_prb, ngap_is_1);
+  return ngap_is_1 ? 2 * (ngap < nof_prb - ngap ? ngap : nof_prb - ngap) : (nof_prb / ngap) * 2 * ngap;
+}
+
+uint32_t format1C_size(const srsran_cell_t* cell)
+{
+  const uint32_t n_step = cell->nof_prb < 50 ? 2 : 4;
+  uint32_t       n      = riv_nbits(ra_type2_n_vrb_dl(cell->nof_prb, true) / n_step) + 5;
+  return cell->nof_prb >= 50 ? n + 1 : n;
+}
+
+uint32_t format2x_size(const srsran_cell_t* cell, const srsran_dci_cfg_t* cfg, srsran_dci_format_t f)
+{
+  uint32_t pbits = 0;
+  if (f == SRSRAN_DCI_FORMAT2) {
+    pbits = cell->nof_ports <= 2 ? 3 : 6;
+  } else if (f == SRSRAN_DCI_FORMAT2A) {
+    pbits = cell->nof_ports <= 2 ? 0 : 2;
+  }
+  uint32_t n = rbg_bits(cell->nof_prb) + 2 + HARQ_PID_LEN + 1 + 2 * (5 + 1 + 2) + pbits + (cfg->cif_enabled ? 3 : 0);
+  if (cell->nof_prb > 10) {
+    n++;
+  }
+  while (is_ambiguous_size(n)) {
+    n++;
+  }
+  return n;
+}
+
+uint32_t bit_pack(const uint8_t** y, uint32_t n)
+{
+  uint32_t v = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    v = (v << 1) | ((*y)[i] & 1u);
+  }
+  *y += n;
+  return v;
+}
+
+void tb_disable(srsran_dci_tb_t& tb)
+{
+  tb.mcs_idx = 0;
+  tb.rv      = 1;
+}
+
+// resource allocation of formats 1 / 2 / 2A: type 0 or type 1 (dci.c:657-680, 1172-1194)
+int unpack_type01(const srsran_cell_t* cell, const uint8_t** y, srsran_dci_dl_t* dci)
+{
+  dci->alloc_type = cell->nof_prb > 10 ? (srsran_ra_type_t) * (*y)++ : SRSRAN_RA_ALLOC_TYPE0;
+  const uint32_t P          = srsran_ra_type0_P(cell->nof_prb);
+  const uint32_t alloc_size = rbg_bits(cell->nof_prb);
+  switch (dci->alloc_type) {
+    case SRSRAN_RA_ALLOC_TYPE0:
+      dci->type0_alloc.rbg_bitmask = bit_pack(y, alloc_size);
+      return SRSRAN_SUCCESS;
+    case SRSRAN_RA_ALLOC_TYPE1: {
+      const uint32_t lp            = (uint32_t)ceilf(log2f((float)P));
+      dci->type1_alloc.rbg_subset  = bit_pack(y, lp);
+      dci->type1_alloc.shift       = *(*y)++ ? true : false;
+      dci->type1_alloc.vrb_bitmask = bit_pack(y, alloc_size - lp - 1);
+      return SRSRAN_SUCCESS;
+    }
+    default:
+      return SRSRAN_ERROR;
+  }
+}
+
+int unpack_format1(const srsran_cell_t* cell, srsran_dl_sf_cfg_t* sf, srsran_dci_cfg_t* cfg, srsran_dci_msg_t* msg,
+                   srsran_dci_dl_t* dci)
+{
+  const uint8_t* y = msg->payload;
+  if (msg->nof_bits != srsran_dci_format_sizeof(cell, sf, cfg, SRSRAN_DCI_FORMAT1)) {
+    return SRSRAN_ERROR;
+  }
+  if (cfg->cif_enabled) {
+    dci->cif         = bit_pack(&y, 3);
+    dci->cif_present = true;
+  }
+  if (unpack_type01(cell, &y, dci)) {
+    return SRSRAN_ERROR;
+  }
+  dci->tb[0].mcs_idx = bit_pack(&y, 5);
+  dci->pid           = bit_pack(&y, HARQ_PID_LEN);
+  dci->tb[0].ndi     = *y++ ? true : false;
+  dci->tb[0].rv      = (int)bit_pack(&y, 2);
+  dci->tpc_pucch     = (uint8_t)bit_pack(&y, 2);
+  return SRSRAN_SUCCESS;
+}
+
+int unpack_format1A(const srsran_cell_t* cell, srsran_dci_cfg_t* cfg, srsran_dci_msg_t* msg, srsran_dci_dl_t* dci)
+{
+  const uint8_t* y = msg->payload;
+  if (cfg->cif_enabled) {
+    dci->cif         = bit_pack(&y, 3);
+    dci->cif_present = true;
+  }
+  if (*y++ != 1) {
+    return SRSRAN_ERROR;  // format 0
+  }
+  msg->format = SRSRAN_DCI_FORMAT1A;
+  if (*y == 0) {  // PDCCH order: localized, RIV all ones, remaining bits zero (dci.c:822-843)
+    const int nb = (int)riv_nbits(cell->nof_prb);
+    int       i  = 0;
+    while (i < nb && y[1 + i] == 1) {
+      i++;
+    }
+    if (i == nb) {
+      i = 1 + 10 + nb;
+      while (i < (int)msg->nof_bits - 1 && y[i] == 0) {
+        i++;
+      }
+      if (i == (int)msg->nof_bits - 1) {
+        y += 1 + nb;
+        dci->is_pdcch_order = true;
+        dci->preamble_idx   = bit_pack(&y, 6);
+        dci->prach_mask_idx = bit_pack(&y, 4);
+        return SRSRAN_SUCCESS;
+      }
+    }
+  }
+  dci->is_pdcch_order    = false;
+  dci->alloc_type        = SRSRAN_RA_ALLOC_TYPE2;
+  dci->type2_alloc.mode  = *y++ ? srsran_ra_type2_t::SRSRAN_RA_TYPE2_DIST : srsran_ra_type2_t::SRSRAN_RA_TYPE2_LOC;
+  dci->type2_alloc.n_gap = srsran_ra_type2_t::SRSRAN_RA_TYPE2_NG1;
+  uint32_t nb_gap        = 0;
+  const bool user        = SRSRAN_RNTI_ISUSER(msg->rnti);
+  if (user && dci->type2_alloc.mode == srsran_ra_type2_t::SRSRAN_RA_TYPE2_DIST && cell->nof_prb >= 50) {
+    nb_gap                 = 1;
+    dci->type2_alloc.n_gap = *y++ ? srsran_ra_type2_t::SRSRAN_RA_TYPE2_NG2 : srsran_ra_type2_t::SRSRAN_RA_TYPE2_NG1;
+  }
+  dci->type2_alloc.riv = bit_pack(&y, riv_nbits(cell->nof_prb) - nb_gap);
+  dci->tb[0].mcs_idx   = bit_pack(&y, 5);
+  dci->pid             = bit_pack(&y, HARQ_PID_LEN);
+  if (!user) {
+    if (cell->nof_prb >= 50 && dci->type2_alloc.mode == srsran_ra_type2_t::SRSRAN_RA_TYPE2_DIST) {
+      dci->type2_alloc.n_gap = *y++ ? srsran_ra_type2_t::SRSRAN_RA_TYPE2_NG2 : srsran_ra_type2_t::SRSRAN_RA_TYPE2_NG1;
+    } else {
+      y++;  // NDI reserved
+    }
+  } else {
+    dci->tb[0].ndi = *y++ ? true : false;
+  }
+  dci->tb[0].rv = (int)bit_pack(&y, 2);
+  if (user) {
+    y += 2;  // TPC
+  } else {
+    y++;
+    dci->type2_alloc.n_prb1a =
+        *y++ ? srsran_ra_type2_t::SRSRAN_RA_TYPE2_NPRB1A_3 : srsran_ra_type2_t::SRSRAN_RA_TYPE2_NPRB1A_2;
+  }
+  return SRSRAN_SUCCESS;
+}
+
+int unpack_format2x(const srsran_cell_t* cell, srsran_dci_cfg_t* cfg, srsran_dci_msg_t* msg, srsran_dci_dl_t* dci)
+{
+  const uint8_t* y = msg->payload;
+  if (cfg->cif_enabled) {
+    dci->cif         = bit_pack(&y, 3);
+    dci->cif_present = true;
+  }
+  if (unpack_type01(cell, &y, dci)) {
+    return SRSRAN_ERROR;
+  }
+  dci->tpc_pucch  = (uint8_t)bit_pack(&y, 2);
+  dci->pid        = bit_pack(&y, HARQ_PID_LEN);
+  dci->tb_cw_swap = *y++ ? true : false;
+  uint32_t nof_tb = 0;
+  for (int i = 0; i < SRSRAN_MAX_CODEWORDS; i++) {
+    dci->tb[i].mcs_idx = bit_pack(&y, 5);
+    dci->tb[i].ndi     = *y++ ? true : false;
+    dci->tb[i].rv      = (int)bit_pack(&y, 2);
+    if (SRSRAN_DCI_IS_TB_EN(dci->tb[i])) {
+      nof_tb++;
+    }
+  }
+  if (msg->format == SRSRAN_DCI_FORMAT2) {
+    dci->pinfo = bit_pack(&y, cell->nof_ports <= 2 ? 3 : 6);
+  } else {
+    dci->pinfo = bit_pack(&y, cell->nof_ports <= 2 ? 0 : 2);
+  }
+  for (int i = 0; i < SRSRAN_MAX_CODEWORDS; i++) {
+    dci->tb[i].cw_idx = nof_tb == 2 ? (uint32_t)(((dci->tb_cw_swap ? 1 : 0) + i) % nof_tb) : 0;
+  }
+  return SRSRAN_SUCCESS;
+}
+
+// ---- ra_dl.c ----
+uint32_t ra_re_x_prb(const srsran_cell_t* cell, srsran_dl_sf_cfg_t* sf, uint32_t slot, uint32_t prb)
+{
+  // FDD, normal CP, normal subframe (ra_dl.c:42-168)
+  const uint32_t sfi   = sf->tti % 10;
+  const uint32_t nctrl = cell->nof_prb <= 10 ? sf->cfi + 1 : sf->cfi;
+  const uint32_t nsym  = 7;
+  uint32_t       re    = slot == 0 ? (nsym - nctrl) * 12 : nsym * 12;
+  if ((sfi == 0 || sfi == 5) && prb >= cell->nof_prb / 2 - 3 && prb < cell->nof_prb / 2 + 3 + (cell->nof_prb % 2)) {
+    if (sfi == 0) {
+      re = slot == 0 ? (nsym - nctrl - 2) * 12 : (nsym - 4) * 12 + 2 * cell->nof_ports;
+    } else if (slot == 0) {
+      re = (nsym - nctrl - 2) * 12;
+    }
+    if ((cell->nof_prb % 2) && (prb == cell->nof_prb / 2 - 3 || prb == cell->nof_prb / 2 + 3)) {
+      if (slot == 0) {
+        re += 2 * 12 / 2;
+      } else if (sfi == 0) {
+        re += 4 * 12 / 2 - cell->nof_ports;
+      }
+    }
+  }
+  switch (cell->nof_ports) {
+    case 1:
+    case 2:
+      re -= 2 * (slot + 1) * cell->nof_ports;
+      break;
+    case 4:
+      if (slot == 1) {
+        re -= 12;
+      } else {
+        re -= 4;
+        if (nctrl == 1) {
+          re -= 4;
+        }
+      }
+      break;
+  }
+  return re;
+}
+
+int prb_allocation(const srsran_dci_dl_t* dci, srsran_pdsch_grant_t* grant, uint32_t nof_prb)
+{
+  const uint32_t P = srsran_ra_type0_P(nof_prb);
+  switch (dci->alloc_type) {
+    case SRSRAN_RA_ALLOC_TYPE0: {
+      const uint32_t bm = dci->type0_alloc.rbg_bitmask;
+      const int      nb = (int)ceilf((float)nof_prb / P);
+      for (int i = 0; i < nb; i++) {
+        if (bm & (1u << (nb - i - 1))) {
+          for (uint32_t j = 0; j < P; j++) {
+            if (i * P + j < nof_prb) {
+              grant->prb_idx[0][i * P + j] = true;
+              grant->nof_prb++;
+            }
+          }
+        }
+      }
+      break;
+    }
+    case SRSRAN_RA_ALLOC_TYPE1: {
+      if (dci->type1_alloc.rbg_subset >= P) {
+        return SRSRAN_ERROR;
+      }
+      const uint32_t n_rb_type1 = srsran_ra_type1_N_rb(nof_prb);
+      const uint32_t temp       = ((nof_prb - 1) / P) % P;
+      uint32_t       n_rb_sub;
+      if (dci->type1_alloc.rbg_subset < temp) {
+        n_rb_sub = ((nof_prb - 1) / (P * P)) * P + P;
+      } else if (dci->type1_alloc.rbg_subset == temp) {
+        n_rb_sub = ((nof_prb - 1) / (P * P)) * P + ((nof_prb - 1) % P) + 1;
+      } else {
+        n_rb_sub = ((nof_prb - 1) / (P * P)) * P;
+      }
+      const int shift = dci->type1_alloc.shift ? (int)(n_rb_sub - n_rb_type1) : 0;
+      for (uint32_t i = 0; i < n_rb_type1; i++) {
+        if (dci->type1_alloc.vrb_bitmask & (1u << (n_rb_type1 - i - 1))) {
+          const uint32_t idx = ((i + shift) / P) * P * P + dci->type1_alloc.rbg_subset * P + (i + shift) % P;
+          if (idx >= nof_prb) {
+            return SRSRAN_ERROR;
+          }
+          grant->prb_idx[0][idx] = true;
+          grant->nof_prb++;
+        }
+      }
+      break;
+    }
+    case SRSRAN_RA_ALLOC_TYPE2: {
+      if (dci->type2_alloc.mode != srsran_ra_type2_t::SRSRAN_RA_TYPE2_LOC || dci->format == SRSRAN_DCI_FORMAT1C) {
+        fprintf(stderr, "[srsran_ra] distributed VRB / format 1C allocations are not provided\n");
+        return SRSRAN_ERROR;
+      }
+      uint32_t L_crb = 0, RB_start = 0;
+      srsran_ra_type2_from_riv(dci->type2_alloc.riv, &L_crb, &RB_start, nof_prb, nof_prb);
+      for (uint32_t i = 0; i < L_crb; i++) {
+        if (i + RB_start >= SRSRAN_MAX_PRB) {
+          return SRSRAN_ERROR;
+        }
+        grant->prb_idx[0][i + RB_start] = true;
+        grant->nof_prb++;
+      }
+      break;
+    }
+    default:
+      return SRSRAN_ERROR;
+  }
+  memcpy(grant->prb_idx[1], grant->prb_idx[0], sizeof(grant->prb_idx[0]));
+  return SRSRAN_SUCCESS;
+}
+
+int compute_tb(bool alt, const srsran_dci_dl_t* dci, srsran_pdsch_grant_t* grant)  // ra_dl.c:345-422
+{
+  for (int i = 0; i < SRSRAN_MAX_CODEWORDS; i++) {
+    grant->tb[i].mcs_idx = dci->tb[i].mcs_idx;
+    grant->tb[i].rv      = dci->tb[i].rv;
+    grant->tb[i].cw_idx  = dci->tb[i].cw_idx;
+    if ((SRSRAN_DCI_IS_TB_EN(dci->tb[i]) && dci->format >= SRSRAN_DCI_FORMAT2) ||
+        (dci->format < SRSRAN_DCI_FORMAT2 && i == 0)) {
+      grant->tb[i].enabled = true;
+      grant->nof_tb++;
+    } else {
+      grant->tb[i].enabled = false;
+    }
+  }
+  if (dci->format == SRSRAN_DCI_FORMAT1A || !SRSRAN_RNTI_ISUSER(dci->rnti)) {
+    alt = false;
+  }
+  if (!SRSRAN_RNTI_ISUSER(dci->rnti) && dci->rnti != SRSRAN_MRNTI) {
+    if (dci->format != SRSRAN_DCI_FORMAT1A) {
+      fprintf(stderr, "[srsran_ra] P/SI/RA-RNTI grants: format 1A only\n");
+      return SRSRAN_ERROR;
+    }
+    const uint32_t n_prb = dci->type2_alloc.n_prb1a == srsran_ra_type2_t::SRSRAN_RA_TYPE2_NPRB1A_2 ? 2 : 3;
+    const int      tbs   = srsran_ra_tbs_from_idx(dci->tb[0].mcs_idx, n_prb);
+    if (tbs < 0) {
+      return SRSRAN_ERROR;
+    }
+    grant->tb[0].mod = SRSRAN_MOD_QPSK;
+    grant->tb[0].tbs = tbs;
+    return SRSRAN_SUCCESS;
+  }
+  for (int i = 0; i < SRSRAN_MAX_CODEWORDS; i++) {
+    if (!grant->tb[i].enabled) {
+      grant->tb[i].tbs = 0;
+      continue;
+    }
+    grant->tb[i].mod = srsran_ra_dl_mod_from_mcs(grant->tb[i].mcs_idx, alt);
+    const int i_tbs  = srsran_ra_tbs_idx_from_mcs(grant->tb[i].mcs_idx, alt, false);
+    if (i_tbs >= 0) {
+      grant->tb[i].tbs = srsran_ra_tbs_from_idx((uint32_t)i_tbs, grant->nof_prb);
+    } else {
+      grant->tb[i].tbs = grant->last_tbs[i];
+    }
+    if (grant->tb[i].tbs < 0) {
+      return SRSRAN_ERROR;
+    }
+  }
+  return SRSRAN_SUCCESS;
+}
+
+int config_mimo(const srsran_cell_t* cell, srsran_tm_t tm, const srsran_dci_dl_t* dci, srsran_pdsch_grant_t* grant)
+{
+  const uint32_t nof_tb = grant->nof_tb;
+  grant->tx_scheme      = SRSRAN_TXSCHEME_PORT0;
+  bool valid            = true;
+  switch (tm) {  // ra_dl.c:451-507
+    case SRSRAN_TM1:
+    case SRSRAN_TM2:
+      grant->tx_scheme = cell->nof_ports > 1 ? SRSRAN_TXSCHEME_DIVERSITY : SRSRAN_TXSCHEME_PORT0;
+      valid            = nof_tb == 1;
+      break;
+    case SRSRAN_TM3:
+      if (nof_tb == 1) {
+        grant->tx_scheme = SRSRAN_TXSCHEME_DIVERSITY;
+      } else if (nof_tb == 2) {
+        grant->tx_scheme = SRSRAN_TXSCHEME_CDD;
+      } else {
+        valid = false;
+      }
+      break;
+    case SRSRAN_TM4:
+      if (nof_tb == 1) {
+        grant->tx_scheme = dci->pinfo == 0 ? SRSRAN_TXSCHEME_DIVERSITY : SRSRAN_TXSCHEME_SPATIALMUX;
+      } else if (nof_tb == 2) {
+        grant->tx_scheme = SRSRAN_TXSCHEME_SPATIALMUX;
+      } else {
+        valid = false;
+      }
+      break;
+    case SRSRAN_TM5:
+    case SRSRAN_TM6:
+    case SRSRAN_TM7:
+    case SRSRAN_TM8:
+      break;
+    default:
+      valid = false;
+  }
+  if (!valid) {
+    return SRSRAN_ERROR;
+  }
+  if (grant->tx_scheme == SRSRAN_TXSCHEME_SPATIALMUX) {  // ra_dl.c:509-538
+    if (nof_tb == 1) {
+      if (dci->pinfo > 0 && dci->pinfo < 5) {
+        grant->pmi = dci->pinfo - 1;
+      } else {
+        return SRSRAN_ERROR;
+      }
+    } else {
+      if (dci->pinfo >= 2) {
+        return SRSRAN_ERROR;
+      }
+      grant->pmi = dci->pinfo % 2;
+    }
+  }
+  switch (grant->tx_scheme) {  // ra_dl.c:540-581
+    case SRSRAN_TXSCHEME_PORT0:
+      if (nof_tb != 1) {
+        return SRSRAN_ERROR;
+      }
+      grant->nof_layers = 1;
+      break;
+    case SRSRAN_TXSCHEME_DIVERSITY:
+      if (nof_tb != 1) {
+        return SRSRAN_ERROR;
+      }
+      grant->nof_layers = cell->nof_ports;
+      break;
+    case SRSRAN_TXSCHEME_SPATIALMUX:
+      grant->nof_layers = nof_tb;
+      break;
+    case SRSRAN_TXSCHEME_CDD:
+      if (nof_tb != 2) {
+        return SRSRAN_ERROR;
+      }
+      grant->nof_layers = 2;
+      break;
+  }
+  return SRSRAN_SUCCESS;
+}
+
+}  // namespace
+
+extern "C" {
+
+uint32_t srsran_ra_type0_P(uint32_t nof_prb)
+{
+  return nof_prb <= 10 ? 1 : nof_prb <= 26 ? 2 : nof_prb <= 63 ? 3 : 4;
+}
+
+uint32_t srsran_ra_type1_N_rb(uint32_t nof_prb)
+{
+  const uint32_t P = srsran_ra_type0_P(nof_prb);
+  return (uint32_t)ceilf((float)nof_prb / P) - (uint32_t)ceilf(log2f((float)P)) - 1;
+}
+
+uint32_t srsran_ra_type2_to_riv(uint32_t L_crb, uint32_t RB_start, uint32_t nof_prb)
+{
+  return (L_crb - 1) <= nof_prb / 2 ? nof_prb * (L_crb - 1) + RB_start
+                                    : nof_prb * (nof_prb - L_crb + 1) + nof_prb - 1 - RB_start;
+}
+
+void srsran_ra_type2_from_riv(uint32_t riv, uint32_t* L_crb, uint32_t* RB_start, uint32_t nof_prb, uint32_t nof_vrb)
+{
+  *L_crb    = riv / nof_prb + 1;
+  *RB_start = riv % nof_prb;
+  if (*L_crb > nof_vrb - *RB_start) {
+    *L_crb    = nof_prb - riv / nof_prb + 1;
+    *RB_start = nof_prb - riv % nof_prb - 1;
+  }
+}
+
+int srsran_ra_tbs_idx_from_mcs(uint32_t mcs, bool use_tbs_index_alt, bool is_ul)
+{
+  if (is_ul) {
+    static const int ul[29] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 19, 20, 21,
+                               22, 23, 24, 25, 26};  // 36.213 Table 8.6.1-1
+    return mcs < 29 ? ul[mcs] : SRSRAN_ERROR;
+  }
+  if (use_tbs_index_alt) {
+    return mcs < 28 ? kDlMcsTbsAlt[mcs] : SRSRAN_ERROR;
+  }
+  return mcs < 29 ? kDlMcsTbs[mcs] : SRSRAN_ERROR;
+}
+
+srsran_mod_t srsran_ra_dl_mod_from_mcs(uint32_t mcs, bool use_tbs_index_alt)
+{
+  if (use_tbs_index_alt) {
+    if (mcs < 5 || mcs == 28) {
+      return SRSRAN_MOD_QPSK;
+    } else if (mcs < 11 || mcs == 29) {
+      return SRSRAN_MOD_16QAM;
+    } else if (mcs < 20 || mcs == 30) {
+      return SRSRAN_MOD_64QAM;
+    }
+    return SRSRAN_MOD_256QAM;
+  }
+  if (mcs < 10 || mcs == 29) {
+    return SRSRAN_MOD_QPSK;
+  } else if (mcs < 17 || mcs == 30) {
+    return SRSRAN_MOD_16QAM;
+  }
+  return SRSRAN_MOD_64QAM;
+}
+
+int srsran_ra_tbs_from_idx(uint32_t tbs_idx, uint32_t n_prb)
+{
+  if (tbs_idx < SRSRAN_RA_NOF_TBS_IDX && n_prb > 0 && n_prb <= SRSRAN_MAX_PRB) {
+    return kTbs[tbs_idx][n_prb - 1];
+  }
+  return SRSRAN_ERROR;
+}
+
+uint32_t srsran_dci_format_sizeof(const srsran_cell_t* cell, srsran_dl_sf_cfg_t* sf, srsran_dci_cfg_t* cfg,
+                                  srsran_dci_format_t format)
+{
+  (void)sf;
+  srsran_dci_cfg_t zero;
+  memset(&zero, 0, sizeof(zero));
+  const srsran_dci_cfg_t* c = cfg ? cfg : &zero;
+  switch (format) {
+    case SRSRAN_DCI_FORMAT0:
+      return format0_size(cell, c);
+    case SRSRAN_DCI_FORMAT1A:
+      return format1A_size(cell, c);
+    case SRSRAN_DCI_FORMAT1: {
+      uint32_t n = rbg_bits(cell->nof_prb) + 5 + HARQ_PID_LEN + 1 + 2 + 2 + (c->cif_enabled ? 3 : 0) +
+                   (cell->nof_prb > 10 ? 1 : 0);
+      while (n == format0_size(cell, c) || n == format1A_size(cell, c) || is_ambiguous_size(n)) {
+        n++;
+      }
+      return n;
+    }
+    case SRSRAN_DCI_FORMAT1C:
+      return format1C_size(cell);
+    case SRSRAN_DCI_FORMAT2:
+    case SRSRAN_DCI_FORMAT2A:
+    case SRSRAN_DCI_FORMAT2B:
+      return format2x_size(cell, c, format);
+    default:
+      return 0;
+  }
+}
+
+int srsran_dci_msg_unpack_pdsch(srsran_cell_t* cell, srsran_dl_sf_cfg_t* sf, srsran_dci_cfg_t* cfg,
+                                srsran_dci_msg_t* msg, srsran_dci_dl_t* dci)
+{
+  if (!cell || !msg || !dci) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  memset(dci, 0, sizeof(*dci));
+  for (int i = 1; i < SRSRAN_MAX_CODEWORDS; i++) {
+    tb_disable(dci->tb[i]);
+  }
+  dci->rnti     = msg->rnti;
+  dci->location = msg->location;
+  dci->format   = msg->format;
+  srsran_dci_cfg_t zero;
+  memset(&zero, 0, sizeof(zero));
+  if (!cfg) {
+    cfg = &zero;
+  }
+  if (cell->frame_type != SRSRAN_FDD) {
+    fprintf(stderr, "[srsran_dci] TDD is not provided\n");
+    return SRSRAN_ERROR;
+  }
+  switch (msg->format) {
+    case SRSRAN_DCI_FORMAT1:
+      return unpack_format1(cell, sf, cfg, msg, dci);
+    case SRSRAN_DCI_FORMAT1A:
+      return unpack_format1A(cell, cfg, msg, dci);
+    case SRSRAN_DCI_FORMAT2:
+    case SRSRAN_DCI_FORMAT2A:
+      return unpack_format2x(cell, cfg, msg, dci);
+    default:
+      fprintf(stderr, "[srsran_dci] unpacking of DCI format %d is not provided\n", (int)msg->format);
+      return SRSRAN_ERROR;
+  }
+}
+
+bool srsran_dci_location_isvalid(srsran_dci_location_t* c)
+{
+  return c && c->L <= 3 && c->ncce <= 87;
+}
+
+int srsran_dci_location_set(srsran_dci_location_t* c, uint32_t L, uint32_t nCCE)
+{
+  if (L <= 3 && nCCE <= 87) {
+    c->L    = L;
+    c->ncce = nCCE;
+    return SRSRAN_SUCCESS;
+  }
+  return SRSRAN_ERROR;
+}
+
+void srsran_dci_cfg_set_common_ss(srsran_dci_cfg_t* cfg)
+{
+  cfg->is_not_ue_ss = true;
+}
+
+bool srsran_location_find_location(const srsran_dci_location_t* locations, uint32_t nof_locations,
+                                   const srsran_dci_location_t* location)
+{
+  for (uint32_t i = 0; i < nof_locations; i++) {
+    if (locations[i].L == location->L && locations[i].ncce == location->ncce) {
+      return true;
+    }
+  }
+  return false;
+}
+
+uint32_t srsran_ra_dl_grant_nof_re(const srsran_cell_t* cell, srsran_dl_sf_cfg_t* sf, srsran_pdsch_grant_t* grant)
+{
+  uint32_t n = 0;
+  for (uint32_t s = 0; s < 2; s++) {
+    for (uint32_t j = 0; j < cell->nof_prb; j++) {
+      if (grant->prb_idx[s][j]) {
+        n += ra_re_x_prb(cell, sf, s, j);
+      }
+    }
+  }
+  return n;
+}
+
+int srsran_ra_dl_dci_to_grant(const srsran_cell_t* cell, srsran_dl_sf_cfg_t* sf, srsran_tm_t tm,
+                              bool pdsch_use_tbs_index_alt, const srsran_dci_dl_t* dci, srsran_pdsch_grant_t* grant)
+{
+  if (!cell || !sf || !dci || !grant) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  if (cell->frame_type != SRSRAN_FDD || cell->cp != SRSRAN_CP_NORM || sf->sf_type != SRSRAN_SF_NORM) {
+    fprintf(stderr, "[srsran_ra] FDD normal-CP normal subframes only\n");
+    return SRSRAN_ERROR;
+  }
+  memset(grant, 0, sizeof(*grant));
+  if (prb_allocation(dci, grant, cell->nof_prb) || compute_tb(pdsch_use_tbs_index_alt, dci, grant)) {
+    return SRSRAN_ERROR;
+  }
+  grant->nof_re           = srsran_ra_dl_grant_nof_re(cell, sf, grant);
+  grant->nof_symb_slot[0] = 7;
+  grant->nof_symb_slot[1] = 7;
+  for (int i = 0; i < SRSRAN_MAX_CODEWORDS; i++) {
+    if (grant->tb[i].enabled) {
+      grant->tb[i].nof_bits = grant->nof_re * srsran_mod_bits_x_symbol(grant->tb[i].mod);
+    }
+  }
+  return config_mimo(cell, tm, dci, grant);
+}
+
+}  // extern "C"

@@ -4,14 +4,18 @@
 // (ue_dl.c:67-180, 349-384, 700-706) over the GPU OFDM, channel estimator and PDSCH objects.
 // Batched: srsran_ue_dl_gpu_decode_batch chains, on one stream and without host round trips,
 //   OFDM (CFO rotation fused)  ->  CRS estimation of every subframe  ->  PDSCH decode batch.
-// PCFICH / PDCCH / PHICH / PMCH are not part of this path: the CFI comes from sf->cfi.
+// Control channels (ue_dl.c:315-347, 386-698): decode_fft_estimate decodes the PCFICH (sets sf->cfi)
+// and extracts the PDCCH LLRs on the GPU; srsran_ue_dl_find_dl_dci blind-searches them, every
+// candidate of the search spaces in one launch.  The batch path takes the CFI from its caller.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
+#include "../../include/srsran_pdcch.h"
 #include "../../include/srsran_ue_dl.h"
 
 namespace {
@@ -24,6 +28,16 @@ struct UeDlGpu {
   float2*    d_ce   = nullptr;
   float*     d_res  = nullptr;
   uint32_t   cap    = 0;  // subframes
+  // control channels (srsran_ue_dl_t::regs / pcfich / pdcch of the reference)
+  srsran_regs_t         regs{};
+  srsran_pcfich_t       pcfich{};
+  srsran_pdcch_t        pdcch{};
+  bool                  ctrl_init = false;  // objects allocated (<= 2 rx antennas)
+  bool                  ctrl_cell = false;  // tables built for the current cell
+  srsran_dci_location_t allocated[SRSRAN_MAX_DCI_MSG];
+  uint32_t              nof_allocated = 0;
+  srsran_dci_msg_t      pending_ul[SRSRAN_MAX_DCI_MSG];
+  uint32_t              nof_pending_ul = 0;
 };
 
 bool grow(srsran_ue_dl_t* q, UeDlGpu* g, uint32_t nsf)
@@ -106,6 +120,13 @@ int srsran_ue_dl_init(srsran_ue_dl_t* q, cf_t* input[SRSRAN_MAX_PORTS], uint32_t
     srsran_ue_dl_free(q);
     return SRSRAN_ERROR;
   }
+  if (nof_rx_antennas <= 2) {
+    if (srsran_pcfich_init(&g->pcfich, nof_rx_antennas) || srsran_pdcch_init_ue(&g->pdcch, max_prb, nof_rx_antennas)) {
+      srsran_ue_dl_free(q);
+      return SRSRAN_ERROR;
+    }
+    g->ctrl_init = true;
+  }
   return SRSRAN_SUCCESS;
 }
 
@@ -125,6 +146,11 @@ void srsran_ue_dl_free(srsran_ue_dl_t* q)
     if (g->staged) {
       hipEventDestroy(g->staged);
     }
+    if (g->ctrl_init) {
+      srsran_pcfich_free(&g->pcfich);
+      srsran_pdcch_free(&g->pdcch);
+    }
+    srsran_regs_free(&g->regs);
     delete g;
   }
   for (int j = 0; j < SRSRAN_MAX_PORTS; j++) {
@@ -160,6 +186,12 @@ int srsran_ue_dl_set_cell(srsran_ue_dl_t* q, srsran_cell_t cell)
   UeDlGpu* g = (UeDlGpu*)q->gpu;
   q->cell    = cell;
   g->cap     = 0;  // buffer shapes depend on the cell
+  // control channels: 1 or 2 ports, normal PHICH duration (others: PDSCH only, CFI from the caller)
+  srsran_regs_free(&g->regs);
+  g->ctrl_cell = g->ctrl_init && (cell.nof_ports == 1 || cell.nof_ports == 2) && cell.phich_length == SRSRAN_PHICH_NORM &&
+                 srsran_regs_init(&g->regs, cell) == SRSRAN_SUCCESS &&
+                 srsran_pcfich_set_cell(&g->pcfich, &g->regs, cell) == SRSRAN_SUCCESS &&
+                 srsran_pdcch_set_cell(&g->pdcch, &g->regs, cell) == SRSRAN_SUCCESS;
   hipDeviceSynchronize();
   hipHostFree(g->h_sf);
   hipFree(g->d_sf);
@@ -189,8 +221,18 @@ static int fft_estimate(srsran_ue_dl_t* q, srsran_dl_sf_cfg_t* sf, srsran_ue_dl_
   if (srsran_chest_dl_estimate_cfg(&q->chest, sf, &cfg->chest_cfg, q->sf_symbols, &q->chest_res)) {
     return SRSRAN_ERROR;
   }
-  // PCFICH is not decoded here: sf->cfi is the caller's (estimate_pdcch_pcfich, ue_dl.c:310-347)
-  return sf->cfi >= 1 && sf->cfi <= 3 ? SRSRAN_SUCCESS : SRSRAN_ERROR;
+  // estimate_pdcch_pcfich (ue_dl.c:315-347): PCFICH -> sf->cfi, then the PDCCH LLRs
+  UeDlGpu* g = (UeDlGpu*)q->gpu;
+  if (!g->ctrl_cell) {
+    return sf->cfi >= 1 && sf->cfi <= 3 ? SRSRAN_SUCCESS : SRSRAN_ERROR;  // CFI from the caller
+  }
+  float corr = 0;
+  if (srsran_pcfich_decode(&g->pcfich, sf, &q->chest_res, q->sf_symbols, &corr) < 0 ||
+      srsran_pdcch_extract_llr(&g->pdcch, sf, &q->chest_res, q->sf_symbols)) {
+    fprintf(stderr, "[srsran_ue_dl] Error decoding PCFICH / extracting PDCCH LLRs\n");
+    return SRSRAN_ERROR;
+  }
+  return SRSRAN_SUCCESS;
 }
 
 int srsran_ue_dl_decode_fft_estimate(srsran_ue_dl_t* q, srsran_dl_sf_cfg_t* sf, srsran_ue_dl_cfg_t* cfg)
@@ -273,6 +315,220 @@ int srsran_ue_dl_gpu_decode_batch(srsran_ue_dl_t*              q,
     }
   }
   return srsran_pdsch_gpu_decode_batch(&q->pdsch, nof_sf, ps.data(), d_result, d_avg_noi, stream);
+}
+
+// ---------------- DCI blind search (ue_dl.c:386-689) ----------------
+namespace {
+
+const srsran_dci_format_t kUeFormats[8][2] = {
+    {SRSRAN_DCI_FORMAT1A, SRSRAN_DCI_FORMAT1},  {SRSRAN_DCI_FORMAT1A, SRSRAN_DCI_FORMAT1},
+    {SRSRAN_DCI_FORMAT1A, SRSRAN_DCI_FORMAT2A}, {SRSRAN_DCI_FORMAT1A, SRSRAN_DCI_FORMAT2},
+    {SRSRAN_DCI_FORMAT1A, SRSRAN_DCI_FORMAT1D}, {SRSRAN_DCI_FORMAT1A, SRSRAN_DCI_FORMAT1B},
+    {SRSRAN_DCI_FORMAT1A, SRSRAN_DCI_FORMAT1},  {SRSRAN_DCI_FORMAT1A, SRSRAN_DCI_FORMAT2B}};
+const srsran_dci_format_t kCommonFormats[2] = {SRSRAN_DCI_FORMAT1A, SRSRAN_DCI_FORMAT1C};
+
+struct SearchSpace {
+  srsran_dci_location_t loc[SRSRAN_MAX_CANDIDATES];
+  uint32_t              nof_locations = 0;
+  srsran_dci_format_t   formats[2];
+  uint32_t              nof_formats = 0;
+  srsran_dci_cfg_t      cfg{};
+  bool                  common = false;
+};
+
+bool find_dci(const srsran_dci_msg_t* msgs, uint32_t n, const srsran_dci_msg_t& m)
+{
+  for (uint32_t k = 0; k < n; k++) {
+    if (msgs[k].nof_bits == m.nof_bits && memcmp(msgs[k].payload, m.payload, m.nof_bits) == 0) {
+      return true;
+    }
+  }
+  return false;
+}
+
+bool allocated(const UeDlGpu* g, const srsran_dci_location_t& l)
+{
+  for (uint32_t i = 0; i < g->nof_allocated; i++) {
+    const uint32_t L = g->allocated[i].L, n = g->allocated[i].ncce;  // as ue_dl.c:402-414 (L, not 2^L)
+    if ((n <= l.ncce && l.ncce < n + L) || (l.ncce <= n && n < l.ncce + l.L)) {
+      return true;
+    }
+  }
+  return false;
+}
+
+}  // namespace
+
+int srsran_ue_dl_find_dl_dci(srsran_ue_dl_t*     q,
+                             srsran_dl_sf_cfg_t* sf,
+                             srsran_ue_dl_cfg_t* dl_cfg,
+                             uint16_t            rnti,
+                             srsran_dci_dl_t     dci_dl[SRSRAN_MAX_DCI_MSG])
+{
+  if (!q || !q->gpu || !sf || !dl_cfg || !dci_dl) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  UeDlGpu* g = (UeDlGpu*)q->gpu;
+  if (!g->ctrl_cell || sf->cfi < 1 || sf->cfi > 3 || g->pdcch.llr_cfi != sf->cfi) {
+    fprintf(stderr, "[srsran_ue_dl] find_dl_dci: no PDCCH LLRs for this subframe (decode_fft_estimate first)\n");
+    return SRSRAN_ERROR;
+  }
+  g->nof_pending_ul = 0;
+  g->nof_allocated  = 0;
+  if (!rnti) {
+    return 0;
+  }
+  // search spaces in the reference's order: C-RNTI -> UE-specific then (dci_common_ss) common with
+  // format 1A; SI / P / RA-RNTI -> common with formats 1A, 1C (ue_dl.c:604-651)
+  std::vector<SearchSpace> ss;
+  SearchSpace              common;
+  common.cfg = dl_cfg->cfg.dci;
+  srsran_dci_cfg_set_common_ss(&common.cfg);
+  common.common        = true;
+  common.nof_locations = srsran_pdcch_common_locations(&g->pdcch, common.loc, SRSRAN_MAX_CANDIDATES_COM, sf->cfi);
+  const bool crnti     = !(rnti == SRSRAN_SIRNTI || rnti == SRSRAN_PRNTI || SRSRAN_RNTI_ISRAR(rnti));
+  if (crnti) {
+    if (dl_cfg->cfg.tm > SRSRAN_TM8) {
+      return SRSRAN_ERROR;
+    }
+    SearchSpace ue;
+    ue.cfg           = dl_cfg->cfg.dci;
+    ue.nof_locations = srsran_pdcch_ue_locations(&g->pdcch, sf, ue.loc, SRSRAN_MAX_CANDIDATES_UE, rnti);
+    ue.nof_formats   = 2;
+    ue.formats[0]    = kUeFormats[dl_cfg->cfg.tm][0];
+    ue.formats[1]    = kUeFormats[dl_cfg->cfg.tm][1];
+    ss.push_back(ue);
+    if (dl_cfg->cfg.dci_common_ss) {
+      common.nof_formats = 1;
+      common.formats[0]  = SRSRAN_DCI_FORMAT1A;
+      ss.push_back(common);
+    }
+  } else {
+    common.nof_formats = 2;
+    common.formats[0]  = kCommonFormats[0];
+    common.formats[1]  = kCommonFormats[1];
+    ss.push_back(common);
+  }
+  // every (location, format) of every search space decoded in one launch, then the sequential
+  // selection of dci_blind_search on the results
+  std::vector<srsran_dci_msg_t> cand;
+  std::vector<float>            corr;
+  std::vector<int>              fmt_ok;
+  for (const SearchSpace& s : ss) {
+    for (uint32_t l = 0; l < s.nof_locations; l++) {
+      for (uint32_t f = 0; f < s.nof_formats; f++) {
+        srsran_dci_msg_t m;
+        memset(&m, 0, sizeof(m));
+        m.location = s.loc[l];
+        m.format   = s.formats[f];
+        cand.push_back(m);
+      }
+    }
+  }
+  // formats the library cannot size (1B / 1D) are decoded as nothing found
+  std::vector<srsran_dci_msg_t> dec;
+  std::vector<uint32_t>         dec_of(cand.size(), UINT32_MAX);
+  size_t                        ci = 0;
+  for (const SearchSpace& s : ss) {
+    for (uint32_t l = 0; l < s.nof_locations; l++) {
+      for (uint32_t f = 0; f < s.nof_formats; f++, ci++) {
+        srsran_dci_cfg_t c = s.cfg;
+        if (srsran_dci_format_sizeof(&q->cell, sf, &c, cand[ci].format) > 0) {
+          dec_of[ci] = (uint32_t)dec.size();
+          dec.push_back(cand[ci]);
+        }
+      }
+    }
+  }
+  corr.assign(dec.size(), 0.0f);
+  // the two search spaces use different DCI configurations: decode each space's candidates with its own
+  {
+    size_t first = 0;
+    ci           = 0;
+    for (const SearchSpace& s : ss) {
+      size_t n = 0;
+      for (uint32_t l = 0; l < s.nof_locations; l++) {
+        for (uint32_t f = 0; f < s.nof_formats; f++, ci++) {
+          n += dec_of[ci] != UINT32_MAX;
+        }
+      }
+      srsran_dci_cfg_t c = s.cfg;
+      if (n && srsran_pdcch_gpu_decode_msgs(&g->pdcch, sf, &c, dec.data() + first, (uint32_t)n, corr.data() + first)) {
+        return SRSRAN_ERROR;
+      }
+      first += n;
+    }
+  }
+  srsran_dci_msg_t msgs[SRSRAN_MAX_DCI_MSG];
+  uint32_t         nof_msg = 0;
+  ci                       = 0;
+  for (const SearchSpace& s : ss) {
+    uint32_t nof_dci = 0;
+    srsran_dci_msg_t* out = msgs + nof_msg;
+    const size_t ci0 = ci;
+    ci += (size_t)s.nof_locations * s.nof_formats;
+    for (uint32_t l = 0; l < s.nof_locations; l++) {
+      const size_t cl = ci0 + (size_t)l * s.nof_formats;
+      if (nof_msg + nof_dci >= SRSRAN_MAX_DCI_MSG) {
+        break;
+      }
+      if (allocated(g, s.loc[l])) {
+        continue;
+      }
+      for (uint32_t f = 0; f < s.nof_formats; f++) {
+        const uint32_t d = dec_of[cl + f];
+        if (d == UINT32_MAX) {
+          continue;
+        }
+        srsran_dci_msg_t m = dec[d];
+        if (m.rnti != rnti || m.nof_bits == 0) {
+          continue;
+        }
+        if (!std::isnormal(corr[d]) || corr[d] < 0.5f) {
+          continue;
+        }
+        if (dl_cfg->cfg.dci_common_ss && (dl_cfg->cfg.dci.multiple_csi_request_enabled || dl_cfg->cfg.dci.srs_request_enabled) &&
+            srsran_location_find_location(common.loc, common.nof_locations, &m.location)) {
+          srsran_dci_cfg_t c = dl_cfg->cfg.dci;
+          srsran_dci_cfg_set_common_ss(&c);
+          if (m.nof_bits == srsran_dci_format_sizeof(&q->cell, sf, &c, SRSRAN_DCI_FORMAT1A)) {
+            m.format = m.payload[0] ? SRSRAN_DCI_FORMAT1A : SRSRAN_DCI_FORMAT0;
+          }
+        }
+        if (m.format == SRSRAN_DCI_FORMAT0) {
+          if (g->nof_pending_ul < SRSRAN_MAX_DCI_MSG && !find_dci(g->pending_ul, g->nof_pending_ul, m)) {
+            g->pending_ul[g->nof_pending_ul++] = m;
+          }
+        } else if (!find_dci(out, nof_dci, m) && !find_dci(g->pending_ul, g->nof_pending_ul, m)) {
+          if (g->nof_allocated < SRSRAN_MAX_DCI_MSG) {
+            g->allocated[g->nof_allocated++] = m.location;
+          }
+          out[nof_dci++] = m;
+          break;
+        }
+      }
+    }
+    nof_msg += nof_dci;
+  }
+  for (uint32_t i = 0; i < nof_msg; i++) {
+    if (srsran_dci_msg_unpack_pdsch(&q->cell, sf, &dl_cfg->cfg.dci, &msgs[i], &dci_dl[i])) {
+      fprintf(stderr, "[srsran_ue_dl] Unpacking DL DCI\n");
+      return SRSRAN_ERROR;
+    }
+  }
+  return (int)nof_msg;
+}
+
+int srsran_ue_dl_dci_to_pdsch_grant(srsran_ue_dl_t*       q,
+                                    srsran_dl_sf_cfg_t*   sf,
+                                    srsran_ue_dl_cfg_t*   cfg,
+                                    srsran_dci_dl_t*      dci,
+                                    srsran_pdsch_grant_t* grant)
+{
+  if (!q || !cfg) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  return srsran_ra_dl_dci_to_grant(&q->cell, sf, cfg->cfg.tm, cfg->cfg.pdsch.use_tbs_index_alt, dci, grant);
 }
 
 }  // extern "C"

@@ -82,8 +82,15 @@ class srsran_pdsch_gpu_sf_t(ctypes.Structure):
                 ("d_payload", ctypes.c_void_p * 2), ("new_data", u32 * 2)]
 
 
+class srsran_dci_cfg_t(ctypes.Structure):
+    _fields_ = [("multiple_csi_request_enabled", ctypes.c_bool), ("cif_enabled", ctypes.c_bool),
+                ("cif_present", ctypes.c_bool), ("srs_request_enabled", ctypes.c_bool),
+                ("ra_format_enabled", ctypes.c_bool), ("is_not_ue_ss", ctypes.c_bool)]
+
+
 class srsran_dl_cfg_t(ctypes.Structure):
-    _fields_ = [("pdsch", srsran_pdsch_cfg_t), ("tm", ctypes.c_int), ("dci_common_ss", ctypes.c_bool)]
+    _fields_ = [("pdsch", srsran_pdsch_cfg_t), ("dci", srsran_dci_cfg_t), ("tm", ctypes.c_int),
+                ("dci_common_ss", ctypes.c_bool)]
 
 
 class srsran_ue_dl_cfg_t(ctypes.Structure):
@@ -182,9 +189,11 @@ def symbol_size_is_standard():
     return bool(lib().srsran_symbol_size_is_standard())
 
 
-def cell(nof_prb=100, nof_ports=2, cell_id=1):
+def cell(nof_prb=100, nof_ports=2, cell_id=1, phich_res=2):
+    """FDD, normal CP, normal PHICH duration, Ng = 1 (phich_res 2) as the reference's test cells"""
     c = srsran_cell_t()
     c.nof_prb, c.nof_ports, c.id = nof_prb, nof_ports, cell_id
+    c.phich_resources = phich_res
     return c
 
 
@@ -393,8 +402,35 @@ class UeDl:
         ptrs = (ctypes.c_void_p * MAX_PORTS)(*[v.ctypes.data for v in x] + [None] * (MAX_PORTS - len(x)))
         sf = srsran_dl_sf_cfg_t()
         sf.tti, sf.cfi = tti, cfi
-        return lib().srsran_ue_dl_decode_fft_estimate_noguru(ctypes.byref(self.q), ctypes.byref(sf),
-                                                             ctypes.byref(self.cfg), ctypes.addressof(ptrs))
+        ret = lib().srsran_ue_dl_decode_fft_estimate_noguru(ctypes.byref(self.q), ctypes.byref(sf),
+                                                            ctypes.byref(self.cfg), ctypes.addressof(ptrs))
+        self.last_cfi = sf.cfi  # decoded from the PCFICH (1/2-port cells), else the caller's
+        return ret
+
+    def find_dl_dci(self, tti, cfi, rnti, tm=2, common_ss=True):
+        """srsran_ue_dl_find_dl_dci (after fft_estimate) -> list of srsran_dci_dl_t"""
+        from . import pdcch as PD
+        PD.lib()
+        sf = srsran_dl_sf_cfg_t()
+        sf.tti, sf.cfi = tti, cfi
+        self.cfg.cfg.tm = tm
+        self.cfg.cfg.dci_common_ss = common_ss
+        out = (PD.srsran_dci_dl_t * 5)()
+        n = lib().srsran_ue_dl_find_dl_dci(ctypes.byref(self.q), ctypes.byref(sf), ctypes.byref(self.cfg), rnti, out)
+        if n < 0:
+            raise RuntimeError("srsran_ue_dl_find_dl_dci failed")
+        return [out[i] for i in range(n)]
+
+    def dci_to_grant(self, dci, tti, cfi, tm=2):
+        from . import pdcch as PD
+        PD.lib()
+        sf = srsran_dl_sf_cfg_t()
+        sf.tti, sf.cfi = tti, cfi
+        self.cfg.cfg.tm = tm
+        g = PD.srsran_pdsch_grant_t()
+        r = lib().srsran_ue_dl_dci_to_pdsch_grant(ctypes.byref(self.q), ctypes.byref(sf), ctypes.byref(self.cfg),
+                                                   ctypes.byref(dci), ctypes.byref(g))
+        return r, g
 
     def grids(self):
         n = 14 * 12 * self.cell.nof_prb

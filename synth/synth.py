@@ -248,12 +248,45 @@ def pdsch_seed(rnti, q, ns, cell_id):
     return (rnti << 14) + (q << 13) + ((ns // 2) << 9) + cell_id
 
 
+# ---------------- PCFICH (36.211 6.7, 36.212 5.3.4) ----------------
+CFI_CODEWORDS = [[(i % 3) != 0 for i in range(32)], [(i % 3) != 1 for i in range(32)],
+                 [(i % 3) != 2 for i in range(32)]]
+
+
+def pcfich_res(nof_prb, cell_id):
+    """Grid indices (symbol 0) of the 16 PCFICH REs in mapping order: 4 REGs of 36.211 6.7.4, each
+    the 6 subcarriers at k0 minus the two reference-signal positions (v_shift mod 3, + 3)."""
+    vo = cell_id % 3
+    k_hat = 6 * (cell_id % (2 * nof_prb))
+    out = []
+    for q in range(4):
+        k0 = (k_hat + (q * nof_prb // 2) * 6) % (12 * nof_prb)
+        out += [k0 + i for i in range(6) if i not in (vo, vo + 3)]
+    return np.array(out)
+
+
+def pcfich_grids(nof_prb, cell_id, nports, sf_idx, cfi):
+    """Per-port (14, 12 N_RB) grids carrying only the PCFICH of `cfi`."""
+    bits = np.array(CFI_CODEWORDS[cfi - 1], np.uint8) ^ gold((sf_idx + 1) * (2 * cell_id + 1) * 512 + cell_id, 32)
+    d = modulate(bits, 2)
+    ports = precode([d], "diversity") if nports == 2 else [d]
+    k = pcfich_res(nof_prb, cell_id)
+    grids = []
+    for p in range(nports):
+        g = np.zeros((14, 12 * nof_prb), np.complex128)
+        g[0, k] = ports[p]
+        grids.append(g)
+    return grids
+
+
 def pdsch_subframe(nof_prb, cell_id, nports, tti, cfi, rnti, tbs, Qm, rv, payloads, scheme="cdd", codebook=1,
-                   nrx=2, snr_db=None, rng=None, N=None, channel=None, cfo=0.0):
+                   nrx=2, snr_db=None, rng=None, N=None, channel=None, cfo=0.0, pcfich=True, ctrl=None):
     """One PDSCH subframe through OFDM and a static MIMO channel.
 
     payloads: one uint8 array (tbs/8 bytes) per codeword.  channel: (nrx, nports) complex matrix
     (default: [[1, 1], [1, -1]] for 2 ports as phy_dl_test.c:568-583 uses, ones for 1 port).
+    pcfich: also transmit the PCFICH of `cfi`; ctrl: optional per-port (14, 12 N_RB) grids added
+    before the OFDM modulator (e.g. a PDCCH control region).
     Returns (samples[nrx, sf_len] complex64, nof_re)."""
     N = N or symbol_sz(nof_prb)
     sf_idx = tti % 10
@@ -269,9 +302,14 @@ def pdsch_subframe(nof_prb, cell_id, nports, tti, cfi, rnti, tbs, Qm, rv, payloa
     if len(ports) != nports:
         raise ValueError("scheme / port count mismatch")
     tx = []
+    pc = pcfich_grids(nof_prb, cell_id, nports, sf_idx, cfi) if pcfich else None
     for p in range(nports):
         g = crs_grid(cell_id, nof_prb, nports, p, sf_idx)
         g[mask] = ports[p]
+        if pc is not None:
+            g = g + pc[p]
+        if ctrl is not None:
+            g = g + ctrl[p]
         tx.append(ofdm_tx(g, N))
     H = np.asarray(channel if channel is not None else
                    ([[1, 1], [1, -1]] if nports == 2 else [[1]] * nrx), np.complex128)

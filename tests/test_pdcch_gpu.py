@@ -1,0 +1,201 @@
+"""GPU PCFICH / PDCCH parity (through the C-ABI) against the reference's own pcfich.c / pdcch.c /
+viterbi.c compiled into oracle/_ref: CFI and its LLRs, the control-region LLRs, every candidate's
+decoded payload / CRC remainder, the blind search (srsran_ue_dl_find_dl_dci) and a C3 subframe
+decoded from time samples with its grant taken from the PDCCH."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+pytestmark = pytest.mark.gpu
+
+import pdcch as P  # noqa: E402  (oracle/pdcch.py)
+
+
+@pytest.fixture(scope="module")
+def mods():
+    import torch  # noqa: F401  -- one HIP runtime for torch and the library
+
+    from srsran_4g_amd import pdcch as PD
+    from srsran_4g_amd import ue_dl as U
+
+    return PD, U
+
+
+def control_subframe(nprb, nports, cid, tti, cfi, msgs, nrx, rng, snr_db=20.0):
+    """reference-encoded control region through a random flat channel + AWGN: returns the rx grids
+    (nrx, 14, 12N), the exact estimates (ports, nrx, 14, 12N) and the noise variance"""
+    ref = P.Ref()
+    tx = ref.ctrl_tx(nprb, nports, cid, tti, cfi, msgs)
+    H = (rng.standard_normal((nrx, nports)) + 1j * rng.standard_normal((nrx, nports))) / np.sqrt(2)
+    y = np.einsum("rp,pls->rls", H, tx)
+    sd = np.sqrt(10 ** (-snr_db / 10) / 2)
+    y = y + sd * (rng.standard_normal(y.shape) + 1j * rng.standard_normal(y.shape))
+    ce = np.broadcast_to(H.T[:, :, None, None], (nports, nrx, 14, 12 * nprb)).astype(np.complex64)
+    return y.astype(np.complex64), np.ascontiguousarray(ce), float(2 * sd * sd)
+
+
+def dci_msgs(nprb, nports, cid, tti, cfi, rng, n=3):
+    """random DCIs at non-overlapping UE-search-space locations of random C-RNTIs"""
+    from srsran_4g_amd import pdcch as PD
+
+    c = PD.cell(nprb, nports, cid)
+    regs = PD.Regs(c)
+    nof_cce = regs.q.pdcch_nregs[cfi - 1] // 9
+    regs.free()
+    used = np.zeros(nof_cce, bool)
+    msgs = []
+    for _ in range(50):
+        if len(msgs) == n:
+            break
+        rnti = int(rng.integers(11, 0xFFF3))
+        fmt = int(rng.choice([P.FORMAT1A, P.FORMAT2A, P.FORMAT1]))
+        size = PD.dci_size(c, fmt)
+        locs = PD.ue_locations(nof_cce, tti % 10, rnti)
+        if not locs:
+            continue
+        L, ncce = locs[int(rng.integers(len(locs)))]
+        if used[ncce:ncce + (1 << L)].any():
+            continue
+        used[ncce:ncce + (1 << L)] = True
+        msgs.append((rng.integers(0, 2, size).astype(np.uint8), L, ncce, rnti, fmt))
+    return msgs, nof_cce
+
+
+CASES = [(100, 2, 1, 3, 1), (100, 2, 301, 7, 3), (50, 2, 7, 0, 2), (25, 1, 12, 4, 2), (6, 1, 2, 8, 3), (6, 2, 5, 5, 1),
+         (75, 1, 100, 9, 3)]
+
+
+@pytest.mark.parametrize("nprb,nports,cid,tti,cfi", CASES)
+def test_pcfich_and_pdcch_llr_vs_reference(mods, nprb, nports, cid, tti, cfi):
+    PD, U = mods
+    rng = np.random.default_rng(nprb * 7 + cid)
+    nrx = 2
+    msgs, nof_cce = dci_msgs(nprb, nports, cid, tti, cfi, rng)
+    y, ce, noise = control_subframe(nprb, nports, cid, tti, cfi, [m[:4] for m in msgs], nrx, rng)
+    ref = P.Ref()
+    rcfi, rcorr, rllr = ref.ctrl_rx(nprb, nports, cid, tti, y, ce, noise)
+    ctl = PD.Control(PD.cell(nprb, nports, cid), nrx)
+    try:
+        gcfi, gcorr, gdata = ctl.pcfich(y, ce, noise, tti)
+        assert gcfi == rcfi == cfi
+        assert abs(gcorr - rcorr) <= 1e-4 * max(1.0, abs(rcorr))
+        gllr = ctl.pdcch_llr(y, ce, noise, tti, gcfi)
+        assert gllr.size == rllr.size == 72 * nof_cce
+        if nports == 2:  # TX diversity: the reference's SSE / generic arithmetic, bit for bit
+            assert np.array_equal(gllr, rllr)
+        else:  # 1 port: the reference's SIMD MMSE uses rcp approximations
+            np.testing.assert_allclose(gllr, rllr, rtol=2e-3, atol=2e-3 * np.abs(rllr).max())
+    finally:
+        ctl.free()
+
+
+@pytest.mark.parametrize("nprb,nports,cid,tti,cfi", CASES[:5])
+def test_candidates_bit_exact_vs_reference(mods, nprb, nports, cid, tti, cfi):
+    """every UE / common search-space candidate of every generated RNTI, three formats, decoded on the
+    GPU from the reference's own LLRs: payload bits, CRC remainder and the mean gate equal"""
+    PD, U = mods
+    rng = np.random.default_rng(1000 + nprb + cid)
+    nrx = 2
+    msgs, nof_cce = dci_msgs(nprb, nports, cid, tti, cfi, rng)
+    y, ce, noise = control_subframe(nprb, nports, cid, tti, cfi, [m[:4] for m in msgs], nrx, rng, snr_db=6.0)
+    ref = P.Ref()
+    rcfi, _, rllr = ref.ctrl_rx(nprb, nports, cid, tti, y, ce, noise)
+    assert rcfi == cfi
+    cands = set(PD.common_locations(nof_cce))
+    for m in msgs:
+        cands |= set(PD.ue_locations(nof_cce, tti % 10, m[3]))
+    cands = sorted(cands)
+    fl = [(L, n, f) for (L, n) in cands for f in (P.FORMAT1A, P.FORMAT2A, P.FORMAT1)]
+    ctl = PD.Control(PD.cell(nprb, nports, cid), nrx)
+    try:
+        ctl.set_llr(cfi, rllr)
+        got = ctl.decode(tti, cfi, fl)
+        found = 0
+        for (L, n, f), (nb, pl, rem, corr) in zip(fl, got):
+            want = ref.pdcch_decode(tti, cfi, rllr, L, n, f)
+            assert nb == want[0], (L, n, f)
+            if nb:
+                assert np.array_equal(pl, want[1]) and rem == want[2], (L, n, f)
+                assert abs(corr - want[3]) <= 1e-4, (L, n, f, corr, want[3])
+            for bits, mL, mn, rnti, mf in msgs:
+                if (mL, mn) == (L, n) and len(bits) == nb and rem == rnti:
+                    found += np.array_equal(pl, bits)
+        assert found == len(msgs)
+    finally:
+        ctl.free()
+
+
+def test_pure_noise_candidates_bit_exact(mods):
+    """LLRs of pure noise: the Viterbi metrics wrap and tie everywhere; still equal to the reference"""
+    PD, U = mods
+    rng = np.random.default_rng(3)
+    nprb, nports, cid, tti, cfi = 50, 2, 9, 2, 3
+    y, ce, noise = control_subframe(nprb, nports, cid, tti, cfi, [], 2, rng)
+    ref = P.Ref()
+    ref.ctrl_rx(nprb, nports, cid, tti, y, ce, noise)
+    ctl = PD.Control(PD.cell(nprb, nports, cid), 2)
+    try:
+        nof_cce = ctl.ncce(cfi)
+        llr = (rng.standard_normal(72 * nof_cce) * 2).astype(np.float32)
+        ctl.set_llr(cfi, llr)
+        fl = [(L, n, f) for L in range(4) for n in range(0, nof_cce - (1 << L) + 1, 1 << L)
+              for f in (P.FORMAT1A, P.FORMAT2A)]
+        got = ctl.decode(tti, cfi, fl)
+        for (L, n, f), (nb, pl, rem, corr) in zip(fl, got):
+            want = ref.pdcch_decode(tti, cfi, llr, L, n, f)
+            assert nb == want[0] and np.array_equal(pl, want[1]) and rem == want[2], (L, n, f)
+    finally:
+        ctl.free()
+
+
+def test_find_dl_dci_and_pdsch_without_injected_grant(mods):
+    """C3 (100 PRB, 2x2 TM3, 64QAM, 2 TBs): time samples -> OFDM -> CRS estimate -> PCFICH (CFI from
+    the air) -> PDCCH blind search (format 2A for the C-RNTI) -> grant -> PDSCH decode; payloads equal"""
+    import torch  # noqa: F401
+
+    PD, U = mods
+    from srsran_4g_amd import sch
+    from synth import synth as S
+
+    cid, tti, cfi, rnti, tbs = 1, 3, 2, 0x1234, 75376
+    rng = np.random.default_rng(42)
+    c = PD.cell(100, 2, cid)
+    bits = P.dci_pack_2a(100, PD.dci_size(c, P.FORMAT2A), (1 << 25) - 1, [(28, 1, 0), (28, 1, 0)], pid=1)
+    regs = PD.Regs(c)
+    nof_cce = regs.q.pdcch_nregs[cfi - 1] // 9
+    regs.free()
+    L, ncce = [loc for loc in PD.ue_locations(nof_cce, tti % 10, rnti) if loc[0] == 3][0]
+    ctrl = P.Ref().ctrl_tx(100, 2, cid, tti, cfi, [(bits, L, ncce, rnti)])
+    # the reference encoder wrote a PCFICH too: the transmitter's own is skipped (pcfich=False)
+    pls = [rng.integers(0, 256, tbs // 8, dtype=np.uint8) for _ in range(2)]
+    x, nre = S.pdsch_subframe(100, cid, 2, tti, cfi, rnti, tbs, 6, 0, pls, snr_db=30.0, rng=rng, pcfich=False,
+                              ctrl=[ctrl[0], ctrl[1]])
+    U.use_standard_symbol_size(True)
+    ue = U.UeDl(U.cell(100, 2, cid), 2)
+    try:
+        assert ue.fft_estimate(x, tti, 0) == 0
+        assert ue.last_cfi == cfi
+        dcis = ue.find_dl_dci(tti, cfi, rnti, tm=2)
+        assert len(dcis) == 1
+        d = dcis[0]
+        assert d.format == P.FORMAT2A and d.rnti == rnti and d.pid == 1 and d.type0_rbg_bitmask == (1 << 25) - 1
+        r, g = ue.dci_to_grant(d, tti, cfi, tm=2)
+        assert r == 0 and g.nof_tb == 2 and g.tb[0].tbs == tbs and g.nof_re == nre
+        sbs = [sch.SoftbufferRx(nof_prb=100) for _ in range(2)]
+        cfg = U.pdsch_cfg(100, nre, (tbs, tbs), (6, 6), softbuffers=sbs)
+        cfg.grant = g
+        cfg.rnti = rnti
+        ret, res = ue.decode_pdsch(cfg, tti, cfi)
+        assert ret == 0
+        for i in range(2):
+            assert res[i][0] and np.array_equal(res[i][1][:tbs // 8], pls[i])
+        # a different RNTI finds nothing
+        assert ue.find_dl_dci(tti, cfi, 0x4321, tm=2) == []
+    finally:
+        ue.free()

@@ -241,11 +241,14 @@ int srsran_dlsch_gpu_decode_batch(srsran_sch_t*                q,
                                   float*                       d_avg_noi,
                                   void*                        stream);
 
-/* ---- UL-SCH receive, data part (sch.c:994-1021, 1122-1193) ----
- * UCI multiplexed on PUSCH (HARQ-ACK, RI, CQI: uci.c) is not provided: srsran_ulsch_decode returns
- * SRSRAN_ERROR when cfg->uci_cfg asks for any of it.  Mirrors of pusch_cfg.h:29-87, uci_cfg.h:31-59
- * and cqi.h:74-143 keep the reference's field names so callers compile unchanged. */
+/* ---- UL-SCH receive with UCI multiplexed (sch.c:994-1193, uci.c, cqi.c) ----
+ * Mirrors of pusch_cfg.h:29-87, uci_cfg.h:31-59 and cqi.h:74-143 keep the reference's field names
+ * and layout so callers compile unchanged. */
 #define SRSRAN_MAX_CARRIERS 5      /* phy_common.h:56 */
+#ifndef SRSRAN_NRE
+#define SRSRAN_NRE 12
+#endif
+#define SRSRAN_CQI_MAX_BITS 64     /* cqi.h:38 */
 #define SRSRAN_UCI_MAX_ACK_BITS 10 /* uci_cfg.h:27 */
 #define SRSRAN_UCI_MAX_M 9         /* uci_cfg.h:29 */
 
@@ -373,15 +376,32 @@ typedef struct {
   bool     meas_evm_en;
 } srsran_pusch_cfg_t;
 
-/* sch.c:1122: de-interleave q_bits (nof_bits LLRs in PUSCH order) into g_bits and decode_tb them.
- * Returns decode_tb's value (SRSRAN_SUCCESS when the TB CRC matched); sets cfg->K_segm. */
+/* sch.c:1122: decode the HARQ-ACK and RI bits (zeroing the ACK positions of q_bits), de-interleave
+ * q_bits (nof_bits LLRs in PUSCH order, RI cells skipped) into g_bits, decode the CQI at its front
+ * and decode_tb the rest.  c_seq: the unpacked PUSCH scrambling sequence (needed for 1-bit ACK / RI).
+ * Returns decode_tb's value (SRSRAN_SUCCESS when the TB CRC matched) or, without a TB, Q'_CQI
+ * (Q'_RI without CQI) as the reference does; sets cfg->K_segm and, for subband-HL CQI with RI,
+ * cfg->uci_cfg.cqi.rank_is_not_one.  All LLR work runs on the GPU (uci_kernel.hip, sch_kernel.hip). */
 int srsran_ulsch_decode(srsran_sch_t*       q,
                         srsran_pusch_cfg_t* cfg,
                         int16_t*            q_bits,
                         int16_t*            g_bits,
                         uint8_t*            c_seq,
                         uint8_t*            data,
-                        srsran_uci_value_t* uci_data); /* untouched: no UCI */
+                        srsran_uci_value_t* uci_data);
+
+/* UCI helpers (sch.h:117-125, uci.h:129-144, cqi.h:145-151) */
+float    srsran_sch_beta_cqi(uint32_t I_cqi);
+float    srsran_sch_beta_ack(uint32_t I_harq);
+uint32_t srsran_sch_find_Ioffset_ack(float beta);
+uint32_t srsran_sch_find_Ioffset_cqi(float beta);
+uint32_t srsran_sch_find_Ioffset_ri(float beta);
+uint32_t srsran_qprime_cqi_ext(uint32_t L_prb, uint32_t nof_symbols, uint32_t tbs, float beta);
+uint32_t srsran_qprime_ack_ext(uint32_t L_prb, uint32_t nof_symbols, uint32_t tbs, uint32_t nof_ack, float beta);
+uint32_t srsran_uci_cfg_total_ack(const srsran_uci_cfg_t* uci_cfg);
+int      srsran_cqi_size(srsran_cqi_cfg_t* cfg);
+int      srsran_cqi_value_pack(srsran_cqi_cfg_t* cfg, srsran_cqi_value_t* value, uint8_t buff[SRSRAN_CQI_MAX_BITS]);
+int      srsran_cqi_value_unpack(srsran_cqi_cfg_t* cfg, uint8_t buff[SRSRAN_CQI_MAX_BITS], srsran_cqi_value_t* value);
 
 /* Added batch entry point: per TB the de-interleaver (device scratch d_g_bits) and decode_tb, all
  * asynchronous on `stream`; d_result / d_avg_noi as srsran_dlsch_gpu_decode_batch. */

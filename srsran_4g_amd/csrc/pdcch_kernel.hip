@@ -19,6 +19,7 @@
 #include <stdint.h>
 
 #include "pdcch_kernel.h"
+#include "viterbi_dev.h"
 
 namespace srsran_amd {
 namespace {
@@ -144,7 +145,7 @@ __global__ void ctrl_diversity_kernel(CtrlEqArgs a)
   a.d[2 * k + 1] = o1;
 }
 
-__device__ __forceinline__ uint32_t parity32(uint32_t v) { return __builtin_popcount(v) & 1u; }
+__device__ __forceinline__ uint32_t parity32(uint32_t v) { return vit_parity32(v); }
 
 // Rank of soft-buffer position p (stream s, column col, row r) among the non-dummy positions of
 // the circular buffer (rm_conv.c bit collection order); -1 for a dummy position.  Only row 0 of a
@@ -260,47 +261,9 @@ __global__ __launch_bounds__(64) void pdcch_cand_kernel(const float* __restrict_
   }
   __syncthreads();
 
-  // ---- Viterbi, lane = state (viterbi37_avx2_16bit.c:176-313) ----
-  const int      s     = lane >> 1, b = lane & 1;
-  const uint32_t bt0   = parity32((2u * s) & 0x6Du) ? 65535u : 0u;
-  const uint32_t bt1   = parity32((2u * s) & 0x4Fu) ? 65535u : 0u;
-  const uint32_t bt2   = parity32((2u * s) & 0x57u) ? 65535u : 0u;
-  uint32_t       m     = 63;
-  const uint32_t steps = 5 * F;
-  for (uint32_t t = 0; t < steps; t++) {
-    const uint16_t* y   = &sym[3 * (t % F)];
-    const uint32_t  a   = ((bt0 ^ y[0]) + (bt1 ^ y[1]) + 1) >> 1;
-    const uint32_t  bm  = (((bt2 ^ y[2]) + a + 1) >> 1) >> 3;
-    const uint32_t  mb  = 8191u - bm;
-    const uint32_t  o0  = (uint32_t)__shfl((int)m, s, 64);
-    const uint32_t  o1  = (uint32_t)__shfl((int)m, s + 32, 64);
-    const uint32_t  x0  = (o0 + (b ? mb : bm)) & 0xffffu;
-    const uint32_t  x1  = (o1 + (b ? bm : mb)) & 0xffffu;
-    const bool      d   = (int16_t)(uint16_t)(x0 - x1) > 0;
-    m                   = d ? x1 : x0;
-    const uint64_t bal  = __ballot(d);
-    if (lane == 0) {
-      dec[t] = bal;
-    }
-  }
-  // best state: the last index of the minimum (viterbi37_avx2_16bit.c:300-309)
-  uint32_t key = ((65535u - m) << 6) | (uint32_t)lane;  // max key = min metric, then highest lane
-  for (int off = 32; off > 0; off >>= 1) {
-    key = max(key, (uint32_t)__shfl_xor((int)key, off, 64));
-  }
-  __syncthreads();
+  // ---- Viterbi, lane = state (viterbi_dev.h) ----
+  viterbi37_tb16(sym, F, dec, data, lane);
   if (lane == 0) {
-    for (int k = 0; k < 6; k++) {
-      dec[steps + k] = 0;  // never written by the update (cleared at init)
-    }
-    uint32_t st = key & 63u;
-    for (int n = (int)steps - 1; n >= 0; n--) {
-      const uint32_t k = (uint32_t)(dec[n + 6] >> st) & 1u;
-      st               = (st >> 1) | (k << 5);
-      if (n >= (int)(2 * F) && n < (int)(3 * F)) {
-        data[n - 2 * F] = (uint8_t)k;
-      }
-    }
     // CRC16 of the payload and the received parity (pdcch.c:333-345)
     uint32_t crc = 0;
     for (uint32_t i = 0; i < c.nof_bits; i++) {

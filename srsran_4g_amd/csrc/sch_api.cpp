@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -22,6 +23,7 @@
 #include "devkey.h"
 #include "sch_kernel.h"
 #include "tdec_kernel.h"
+#include "uci_kernel.h"
 
 using namespace srsran_amd;
 
@@ -180,6 +182,8 @@ struct SchCtx {
   size_t      ul_cap = 0;
   UlDeint*    d_uldesc = nullptr;  // srsran_ulsch_gpu_decode_batch descriptors
   size_t      uldesc_cap = 0;
+  uint8_t*    d_uci = nullptr;     // srsran_ulsch_decode with UCI: descriptors, results, sequence
+  size_t      uci_cap = 0;
 };
 
 constexpr size_t kDataCap = (size_t)SCH_MAX_CB * SCH_SLOT_BYTES;
@@ -849,6 +853,7 @@ void srsran_sch_free(srsran_sch_t* q)
     hipFree(x->d_zero);
     hipFree(x->d_ul);
     hipFree(x->d_uldesc);
+    hipFree(x->d_uci);
     delete x;
   }
   srsran_tdec_free(&q->decoder);
@@ -1002,15 +1007,269 @@ int srsran_dlsch_gpu_decode_batch(srsran_sch_t*                q,
   return enqueue_batch(q, nof_tb, tbs, d_result, d_avg_noi, (hipStream_t)stream);
 }
 
-// ---------------- UL-SCH data part (sch.c:994-1021, 1122-1193), no UCI ----------------
-static bool uci_requested(const srsran_pusch_cfg_t* cfg)
+// ---------------- UCI on PUSCH, host side ----------------
+// Offset tables of 36.213 Tables 8.6.3-1/-2/-3 with the reference's out-of-range behaviour
+// (sch.c:43-95: an error message and the first valid entry).
+static float beta_harq(uint32_t i)
 {
-  uint32_t nof_ack = 0;  // srsran_uci_cfg_total_ack (uci.c:716-723)
-  for (uint32_t i = 0; i < SRSRAN_MAX_CARRIERS; i++) {
-    nof_ack += cfg->uci_cfg.ack[i].nof_acks;
+  static const float t[15] = {2.0f, 2.5f, 3.125f, 4.0f, 5.0f, 6.25f, 8.0f, 10.0f, 12.625f, 15.875f, 20.0f, 31.0f,
+                              50.0f, 80.0f, 126.0f};
+  if (i < 15) {
+    return t[i];
   }
-  return nof_ack > 0 || cfg->uci_cfg.cqi.ri_len > 0 || cfg->uci_cfg.cqi.data_enable;
+  fprintf(stderr, "[srsran_sch] Invalid I_offset_ack %u (min: 0, max: 14)\n", i);
+  return t[0];
 }
+
+static float beta_ri(uint32_t i)
+{
+  static const float t[13] = {1.25f, 1.625f, 2.0f, 2.5f, 3.125f, 4.0f, 5.0f, 6.25f, 8.0f, 10.0f, 12.625f, 15.875f,
+                              20.0f};
+  if (i < 13) {
+    return t[i];
+  }
+  fprintf(stderr, "[srsran_sch] Invalid I_offset_ri %u (min: 0, max: 12)\n", i);
+  return t[0];
+}
+
+static float beta_cqi(uint32_t i)
+{
+  static const float t[16] = {-1.0f, -1.0f, 1.125f, 1.25f, 1.375f, 1.625f, 1.75f, 2.0f, 2.25f, 2.5f, 2.875f,
+                              3.125f, 3.5f, 4.0f, 5.0f, 6.25f};
+  if (i > 1 && i < 16) {
+    return t[i];
+  }
+  fprintf(stderr, "[srsran_sch] Invalid I_offset_cqi %u (min: 2, max: 15)\n", i);
+  return t[2];
+}
+
+float srsran_sch_beta_cqi(uint32_t I_cqi) { return I_cqi < 16 ? beta_cqi(I_cqi) : 0.0f; }
+float srsran_sch_beta_ack(uint32_t I_harq) { return I_harq < 16 ? beta_harq(I_harq) : 0.0f; }
+
+// the first index whose offset reaches beta (sch.c:108-136, 16 indices through the getters)
+uint32_t srsran_sch_find_Ioffset_ack(float beta)
+{
+  for (uint32_t i = 0; i < 16; i++) {
+    if (beta_harq(i) >= beta) {
+      return i;
+    }
+  }
+  return 0;
+}
+uint32_t srsran_sch_find_Ioffset_ri(float beta)
+{
+  for (uint32_t i = 0; i < 16; i++) {
+    if (beta_ri(i) >= beta) {
+      return i;
+    }
+  }
+  return 0;
+}
+uint32_t srsran_sch_find_Ioffset_cqi(float beta)
+{
+  for (uint32_t i = 0; i < 16; i++) {
+    if (beta_cqi(i) >= beta) {
+      return i;
+    }
+  }
+  return 0;
+}
+
+uint32_t srsran_uci_cfg_total_ack(const srsran_uci_cfg_t* uci_cfg)
+{
+  uint32_t n = 0;  // uci.c:716-723
+  for (uint32_t i = 0; i < SRSRAN_MAX_CARRIERS; i++) {
+    n += uci_cfg->ack[i].nof_acks;
+  }
+  return n;
+}
+
+// Q'_ACK / Q'_RI, 36.212 5.2.2.6 (uci.c:414-440); float arithmetic in the reference's order
+static uint32_t qprime_ri_ack(uint32_t K, uint32_t L_prb, uint32_t nof_symb, uint32_t O, uint32_t O_cqi, float beta)
+{
+  if (beta < 0) {
+    return (uint32_t)-1;
+  }
+  if (K == 0) {  // no UL-SCH: 5.2.4.1
+    K = O_cqi <= 11 ? O_cqi : O_cqi + 8;
+  }
+  if (K == 0) {
+    return 0;
+  }
+  const uint32_t x = (uint32_t)ceilf((float)O * (float)L_prb * (float)SRSRAN_NRE * (float)nof_symb * beta / (float)K);
+  return std::min(x, 4 * L_prb * SRSRAN_NRE);
+}
+
+// Q'_CQI (uci.c:170-186)
+static uint32_t qprime_cqi(uint32_t K, uint32_t L_prb, uint32_t nof_symb, uint32_t O, float beta, uint32_t Q_prime_ri)
+{
+  const uint32_t L = O < 11 ? 0 : 8;
+  uint32_t       x = 999999;
+  if (K > 0) {
+    x = (uint32_t)ceilf((float)(O + L) * (float)L_prb * (float)SRSRAN_NRE * (float)nof_symb * beta / (float)K);
+  }
+  return std::min(x, L_prb * SRSRAN_NRE * nof_symb - Q_prime_ri);
+}
+
+uint32_t srsran_qprime_cqi_ext(uint32_t L_prb, uint32_t nof_symbols, uint32_t tbs, float beta)
+{
+  return qprime_cqi(tbs, L_prb, nof_symbols, 20 + 8, beta, 0);  // O = SRSRAN_UCI_CQI_CODED_PUCCH_B + 8
+}
+
+uint32_t srsran_qprime_ack_ext(uint32_t L_prb, uint32_t nof_symbols, uint32_t tbs, uint32_t nof_ack, float beta)
+{
+  return qprime_ri_ack(tbs, L_prb, nof_symbols, nof_ack, 0, beta);
+}
+
+// ---- CQI report sizes and fields, 36.212 Tables 5.2.2.6.2-1/-2, 5.2.3.3.1-1/-2 (cqi.c:41-384) ----
+static uint32_t bits_get(const uint8_t** p, uint32_t n)  // srsran_bit_pack: MSB first
+{
+  uint32_t v = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    v = (v << 1) | ((*p)[i] & 1u);
+  }
+  *p += n;
+  return v;
+}
+
+static void bits_put(uint32_t v, uint8_t** p, uint32_t n)  // srsran_bit_unpack
+{
+  for (uint32_t i = 0; i < n; i++) {
+    (*p)[i] = (uint8_t)((v >> (n - 1 - i)) & 1u);
+  }
+  *p += n;
+}
+
+int srsran_cqi_size(srsran_cqi_cfg_t* cfg)
+{
+  if (!cfg->data_enable) {
+    return (int)cfg->ri_len;
+  }
+  int size = 0;
+  switch (cfg->type) {
+    case SRSRAN_CQI_TYPE_WIDEBAND:
+      size = 4;
+      if (cfg->pmi_present) {
+        if (cfg->four_antenna_ports) {
+          size += (cfg->rank_is_not_one ? 3 : 0) + 4;
+        } else {
+          size += cfg->rank_is_not_one ? 3 + 1 : 2;
+        }
+      }
+      break;
+    case SRSRAN_CQI_TYPE_SUBBAND_UE:
+      size = 4 + (cfg->subband_label_2_bits ? 2 : 1);
+      break;
+    case SRSRAN_CQI_TYPE_SUBBAND_UE_DIFF:
+      size = 4 + 2 + (int)cfg->L;
+      break;
+    case SRSRAN_CQI_TYPE_SUBBAND_HL:
+      size = 4 + 2 * (int)cfg->N;
+      if (cfg->rank_is_not_one && cfg->pmi_present) {
+        size += 4 + 2 * (int)cfg->N;
+      }
+      if (cfg->pmi_present) {
+        size += cfg->four_antenna_ports ? 4 : cfg->rank_is_not_one ? 1 : 2;
+      }
+      break;
+    default:
+      size = SRSRAN_ERROR;
+  }
+  return size;
+}
+
+int srsran_cqi_value_pack(srsran_cqi_cfg_t* cfg, srsran_cqi_value_t* v, uint8_t buff[SRSRAN_CQI_MAX_BITS])
+{
+  uint8_t* p = buff;
+  switch (cfg->type) {
+    case SRSRAN_CQI_TYPE_WIDEBAND:
+      bits_put(v->wideband.wideband_cqi, &p, 4);
+      if (cfg->pmi_present) {
+        if (cfg->rank_is_not_one) {
+          bits_put(v->wideband.spatial_diff_cqi, &p, 3);
+        }
+        bits_put(v->wideband.pmi, &p, cfg->four_antenna_ports ? 4 : cfg->rank_is_not_one ? 1 : 2);
+      }
+      return (int)(p - buff);
+    case SRSRAN_CQI_TYPE_SUBBAND_UE:
+      bits_put(v->subband_ue.subband_cqi, &p, 4);
+      bits_put(v->subband_ue.subband_label, &p, cfg->subband_label_2_bits ? 2 : 1);
+      return 4 + (cfg->subband_label_2_bits ? 2 : 1);
+    case SRSRAN_CQI_TYPE_SUBBAND_UE_DIFF:  // the reference writes subband_diff_cqi twice (cqi.c:77-85)
+      bits_put(v->subband_ue_diff.wideband_cqi, &p, 4);
+      bits_put(v->subband_ue_diff.subband_diff_cqi, &p, 2);
+      bits_put(v->subband_ue_diff.subband_diff_cqi, &p, cfg->L);
+      return 4 + 2 + (int)cfg->L;
+    case SRSRAN_CQI_TYPE_SUBBAND_HL: {
+      int n = 4 + 2 * (int)cfg->N;
+      bits_put(v->subband_hl.wideband_cqi_cw0, &p, 4);
+      bits_put(v->subband_hl.subband_diff_cqi_cw0, &p, 2 * cfg->N);
+      if (cfg->rank_is_not_one) {
+        bits_put(v->subband_hl.wideband_cqi_cw1, &p, 4);
+        bits_put(v->subband_hl.subband_diff_cqi_cw1, &p, 2 * cfg->N);
+        n += 4 + 2 * (int)cfg->N;
+      }
+      if (cfg->pmi_present) {
+        const uint32_t w = cfg->four_antenna_ports ? 4 : cfg->rank_is_not_one ? 1 : 2;
+        bits_put(v->subband_hl.pmi, &p, w);
+        n += (int)w;
+      }
+      return n;
+    }
+  }
+  return -1;
+}
+
+int srsran_cqi_value_unpack(srsran_cqi_cfg_t* cfg, uint8_t buff[SRSRAN_CQI_MAX_BITS], srsran_cqi_value_t* v)
+{
+  const uint8_t* p = buff;
+  switch (cfg->type) {
+    case SRSRAN_CQI_TYPE_WIDEBAND:
+      v->wideband.wideband_cqi = (uint8_t)bits_get(&p, 4);
+      if (cfg->pmi_present) {
+        if (cfg->rank_is_not_one) {
+          v->wideband.spatial_diff_cqi = (uint8_t)bits_get(&p, 3);
+        }
+        v->wideband.pmi = (uint8_t)bits_get(&p, cfg->four_antenna_ports ? 4 : cfg->rank_is_not_one ? 1 : 2);
+      }
+      return 4;
+    case SRSRAN_CQI_TYPE_SUBBAND_UE:
+      v->subband_ue.subband_cqi   = (uint8_t)bits_get(&p, 4);
+      v->subband_ue.subband_label = (uint8_t)bits_get(&p, cfg->subband_label_2_bits ? 2 : 1);
+      return 4 + (cfg->subband_label_2_bits ? 2 : 1);
+    case SRSRAN_CQI_TYPE_SUBBAND_UE_DIFF:  // the L-bit field overwrites the 2-bit one (cqi.c:175-184)
+      v->subband_ue_diff.wideband_cqi     = (uint8_t)bits_get(&p, 4);
+      v->subband_ue_diff.subband_diff_cqi = (uint8_t)bits_get(&p, 2);
+      v->subband_ue_diff.subband_diff_cqi = (uint8_t)bits_get(&p, cfg->L);
+      return 4 + 2 + (int)cfg->L;
+    case SRSRAN_CQI_TYPE_SUBBAND_HL: {
+      int n = 4 + 2 * (int)cfg->N;
+      v->subband_hl.wideband_cqi_cw0     = (uint8_t)bits_get(&p, 4);
+      v->subband_hl.subband_diff_cqi_cw0 = bits_get(&p, 2 * cfg->N);
+      if (cfg->rank_is_not_one) {
+        v->subband_hl.wideband_cqi_cw1     = (uint8_t)bits_get(&p, 4);
+        v->subband_hl.subband_diff_cqi_cw1 = bits_get(&p, 2 * cfg->N);
+        n += 4 + 2 * (int)cfg->N;
+      }
+      if (cfg->pmi_present) {
+        const uint32_t w = cfg->four_antenna_ports ? 4 : cfg->rank_is_not_one ? 1 : 2;
+        v->subband_hl.pmi = (uint8_t)bits_get(&p, w);
+        n += (int)w;
+      }
+      return n;
+    }
+  }
+  return -1;
+}
+
+// ---------------- UL-SCH receive with UCI (sch.c:994-1193) ----------------
+// One device scratch block per call: the UCI / de-interleaver descriptors, the UCI results and
+// the unpacked scrambling sequence.
+struct UlsUciScratch {
+  UciDesc uci;
+  UlDeint deint;
+  UciOut  out;
+};
 
 int srsran_ulsch_decode(srsran_sch_t*       q,
                         srsran_pusch_cfg_t* cfg,
@@ -1020,8 +1279,6 @@ int srsran_ulsch_decode(srsran_sch_t*       q,
                         uint8_t*            data,
                         srsran_uci_value_t* uci_data)
 {
-  (void)c_seq;
-  (void)uci_data;
   if (!q || !q->gpu || !cfg || !q_bits || !g_bits) {
     return SRSRAN_ERROR_INVALID_INPUTS;
   }
@@ -1032,13 +1289,61 @@ int srsran_ulsch_decode(srsran_sch_t*       q,
   }
   const uint32_t nb = cfg->grant.tb.nof_bits, Qm = srsran_mod_bits_x_symbol(cfg->grant.tb.mod);
   cfg->K_segm       = s.C1 * s.K1 + s.C2 * s.K2;
-  if (uci_requested(cfg)) {
-    fprintf(stderr, "[srsran_sch] UCI on PUSCH (HARQ-ACK / RI / CQI) is not provided\n");
+  if (Qm == 0) {
+    fprintf(stderr, "[srsran_sch] Invalid modulation\n");
     return SRSRAN_ERROR;
   }
-  if (Qm == 0 || cfg->grant.nof_symb == 0 || nb % Qm) {
+  const uint32_t nsymb = cfg->grant.nof_symb;
+  if (nsymb == 0 || nsymb > 14 || nb % Qm || Qm > 8) {
     return SRSRAN_ERROR_INVALID_INPUTS;
   }
+  const uint32_t    H = nb / Qm, rows = H / nsymb;
+  srsran_cqi_cfg_t& cq   = cfg->uci_cfg.cqi;
+  const uint32_t    nack = srsran_uci_cfg_total_ack(&cfg->uci_cfg);
+  const bool        uci  = nack > 0 || cq.ri_len > 0 || cq.data_enable;
+  if (uci && !uci_data) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+
+  // ---- uci_decode_ri_ack, host part (sch.c:1023-1120): Q'_ACK, Q'_RI ----
+  const bool hl_ri = cq.data_enable && cq.type == SRSRAN_CQI_TYPE_SUBBAND_HL && cq.ri_len;
+  if (hl_ri) {
+    cq.rank_is_not_one = false;  // RI = 1 assumed for the RI / ACK sizes (36.212 5.2.4.1)
+  }
+  const uint32_t cqi_len0 = (uint32_t)srsran_cqi_size(&cq);
+  uint32_t       ack_Qp = 0, ri_Qp = 0;
+  if (nack > 0) {
+    if (nack > SRSRAN_UCI_MAX_ACK_BITS) {
+      return SRSRAN_ERROR_INVALID_INPUTS;
+    }
+    float beta = beta_harq(cfg->uci_offset.I_offset_ack);
+    if (cfg->grant.tb.tbs == 0) {
+      beta /= beta_cqi(cfg->uci_offset.I_offset_cqi);
+    }
+    ack_Qp = qprime_ri_ack(cfg->K_segm, cfg->grant.L_prb, nsymb, nack, cqi_len0, beta);
+  }
+  if (cq.ri_len > 0) {
+    if (cq.ri_len > 4) {
+      return SRSRAN_ERROR_INVALID_INPUTS;
+    }
+    float beta = beta_ri(cfg->uci_offset.I_offset_ri);
+    if (cfg->grant.tb.tbs == 0) {
+      beta /= beta_cqi(cfg->uci_offset.I_offset_cqi);
+    }
+    ri_Qp = qprime_ri_ack(cfg->K_segm, cfg->grant.L_prb, nsymb, cq.ri_len, cqi_len0, beta);
+  }
+  // the ACK / RI rows are counted up from the bottom of the interleaver: positions past its top
+  // (uci.c:378-386 "Error interleaving") are refused
+  if (ack_Qp > 4 * rows || ri_Qp > 4 * rows || ri_Qp > H) {
+    fprintf(stderr, "[srsran_sch] UCI does not fit the PUSCH interleaver (Q'_ACK=%u Q'_RI=%u rows=%u)\n", ack_Qp,
+            ri_Qp, rows);
+    return SRSRAN_ERROR;
+  }
+  const bool need_c = (nack == 1 && ack_Qp > 0) || (cq.ri_len == 1 && ri_Qp > 0);
+  if (need_c && !c_seq) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+
   SchCtx* x = (SchCtx*)q->gpu;
   if (2 * (size_t)nb > x->ul_cap) {
     hipFree(x->d_ul);
@@ -1051,24 +1356,127 @@ int srsran_ulsch_decode(srsran_sch_t*       q,
   }
   int16_t* d_q = x->d_ul;
   int16_t* d_g = x->d_ul + nb;
-  // the reference leaves the de-interleaved LLRs in g_bits (positions past rows N_symb Qm untouched)
+  // the reference leaves the de-interleaved LLRs in g_bits (positions it does not write untouched)
   if (hipMemcpyAsync(d_g, g_bits, (size_t)nb * 2, hipMemcpyHostToDevice, x->stream) != hipSuccess ||
-      hipMemcpyAsync(d_q, q_bits, (size_t)nb * 2, hipMemcpyHostToDevice, x->stream) != hipSuccess ||
-      ul_deint_launch(d_q, d_g, Qm, nb / Qm, cfg->grant.nof_symb, x->stream) != hipSuccess ||
+      hipMemcpyAsync(d_q, q_bits, (size_t)nb * 2, hipMemcpyHostToDevice, x->stream) != hipSuccess) {
+    return SRSRAN_ERROR;
+  }
+  if (!uci) {
+    if (ul_deint_launch(d_q, d_g, Qm, H, nsymb, x->stream) != hipSuccess ||
+        hipMemcpyAsync(g_bits, d_g, (size_t)nb * 2, hipMemcpyDeviceToHost, x->stream) != hipSuccess ||
+        hipStreamSynchronize(x->stream) != hipSuccess) {
+      return SRSRAN_ERROR;
+    }
+    if (s.tbs == 0) {
+      return SRSRAN_SUCCESS;
+    }
+    srsran_pdsch_cfg_t pc;
+    memset(&pc, 0, sizeof(pc));
+    pc.grant.nof_tb       = 1;
+    pc.grant.tb[0]        = cfg->grant.tb;
+    pc.softbuffers.rx[0]  = cfg->softbuffers.rx;
+    pc.max_nof_iterations = cfg->max_nof_iterations;
+    return dlsch_decode_sync(q, &pc, nullptr, d_g, data, 0, 1);
+  }
+
+  // ---- device scratch: descriptors, results, sequence ----
+  const size_t scr = align16(sizeof(UlsUciScratch)) + (need_c ? (size_t)nb : 0);
+  if (!grow_dev((void**)&x->d_uci, &x->uci_cap, scr)) {
+    return SRSRAN_ERROR;
+  }
+  UlsUciScratch* d_s = (UlsUciScratch*)x->d_uci;
+  uint8_t*       d_c = x->d_uci + align16(sizeof(UlsUciScratch));
+  UlsUciScratch  h;
+  memset(&h, 0, sizeof(h));
+  h.uci = {d_q, need_c ? d_c : nullptr, d_g, &d_s->out, Qm, rows, nsymb, nack, ack_Qp, cq.ri_len, ri_Qp, 0, 0};
+  // the de-interleaver skips the RI cells: column set[c] holds the RI indices q = 3c mod 4 (mod 4)
+  h.deint         = {d_q, d_g, rows, nsymb, Qm, {}, -1};
+  if (ri_Qp > 0) {
+    static const uint8_t kRiNorm[4] = {1, 4, 7, 10}, kRiExt[4] = {0, 3, 5, 8};
+    const uint8_t*       set        = nsymb > 10 ? kRiNorm : kRiExt;
+    int64_t              last       = -1;  // the largest RI position in q order
+    for (uint32_t c = 0; c < 4; c++) {
+      const uint32_t m = (3 * c) % 4, n = ri_Qp > m ? (ri_Qp - m + 3) / 4 : 0;
+      h.deint.ri_rows[set[c]] = (uint16_t)n;
+      if (n > 0) {
+        last = std::max<int64_t>(last, (int64_t)(rows - 1) * Qm + (int64_t)set[c] * rows * Qm + Qm - 1);
+      }
+    }
+    uint32_t first = 0;  // the first non-RI column of row 0 holds g[0] in its own right
+    while (first < nsymb && h.deint.ri_rows[first] >= rows) {
+      first++;
+    }
+    h.deint.g0_src = (int32_t)std::max<int64_t>(last, (int64_t)first * rows * Qm);
+  }
+  if (hipMemcpyAsync(d_s, &h, sizeof(h), hipMemcpyHostToDevice, x->stream) != hipSuccess ||
+      (need_c && hipMemcpyAsync(d_c, c_seq, nb, hipMemcpyHostToDevice, x->stream) != hipSuccess) ||
+      uci_ack_ri_launch(&d_s->uci, 1, x->stream) != hipSuccess ||
+      ul_deint_batch_launch(&d_s->deint, 1, rows, x->stream) != hipSuccess) {
+    return SRSRAN_ERROR;
+  }
+
+  // ---- CQI (sch.c:1160-1183): its size may depend on the RI just decoded ----
+  uint32_t cqi_Qp = 0;
+  if (cq.data_enable) {
+    if (hl_ri) {
+      if (hipMemcpyAsync(&h.out, &d_s->out, sizeof(UciOut), hipMemcpyDeviceToHost, x->stream) != hipSuccess ||
+          hipStreamSynchronize(x->stream) != hipSuccess) {
+        return SRSRAN_ERROR;
+      }
+      cq.rank_is_not_one = h.out.ri[0] > 0;
+    }
+    const int cqi_len = srsran_cqi_size(&cq);
+    if (cqi_len <= 0 || cqi_len > (int)UCI_MAX_CQI_BITS) {
+      return SRSRAN_ERROR_INVALID_INPUTS;
+    }
+    cqi_Qp = qprime_cqi(cfg->K_segm, cfg->grant.L_prb, nsymb, (uint32_t)cqi_len, beta_cqi(cfg->uci_offset.I_offset_cqi),
+                        ri_Qp);
+    if ((uint64_t)cqi_Qp + ri_Qp > H) {
+      return SRSRAN_ERROR;
+    }
+    h.uci.cqi_bits = (uint32_t)cqi_len;
+    h.uci.cqi_Qp   = cqi_Qp;
+    if (hipMemcpyAsync(&d_s->uci, &h.uci, sizeof(UciDesc), hipMemcpyHostToDevice, x->stream) != hipSuccess ||
+        uci_cqi_launch(&d_s->uci, 1, x->stream) != hipSuccess) {
+      return SRSRAN_ERROR;
+    }
+  } else if (hl_ri) {
+    cq.rank_is_not_one = false;
+  }
+
+  // ---- decode_tb over the UL-SCH part (after the CQI) ----
+  int ret = cq.data_enable ? (int)cqi_Qp : (int)ri_Qp;  // the value left in ret when there is no TB
+  if (s.tbs > 0) {
+    srsran_pdsch_cfg_t pc;
+    memset(&pc, 0, sizeof(pc));
+    pc.grant.nof_tb          = 1;
+    pc.grant.tb[0]           = cfg->grant.tb;
+    pc.grant.tb[0].nof_bits  = (H - ri_Qp - cqi_Qp) * Qm;
+    pc.softbuffers.rx[0]     = cfg->softbuffers.rx;
+    pc.max_nof_iterations    = cfg->max_nof_iterations;
+    ret                      = dlsch_decode_sync(q, &pc, nullptr, d_g + (size_t)cqi_Qp * Qm, data, 0, 1);
+  }
+  if (hipMemcpyAsync(&h.out, &d_s->out, sizeof(UciOut), hipMemcpyDeviceToHost, x->stream) != hipSuccess ||
+      hipMemcpyAsync(q_bits, d_q, (size_t)nb * 2, hipMemcpyDeviceToHost, x->stream) != hipSuccess ||
       hipMemcpyAsync(g_bits, d_g, (size_t)nb * 2, hipMemcpyDeviceToHost, x->stream) != hipSuccess ||
       hipStreamSynchronize(x->stream) != hipSuccess) {
     return SRSRAN_ERROR;
   }
-  if (s.tbs == 0) {
-    return SRSRAN_SUCCESS;
+  if (nack > 0) {
+    memcpy(uci_data->ack.ack_value, h.out.ack, std::min<uint32_t>(nack, SRSRAN_UCI_MAX_ACK_BITS));
+    uci_data->ack.valid = h.out.ack_valid != 0;
   }
-  srsran_pdsch_cfg_t pc;
-  memset(&pc, 0, sizeof(pc));
-  pc.grant.nof_tb        = 1;
-  pc.grant.tb[0]         = cfg->grant.tb;
-  pc.softbuffers.rx[0]   = cfg->softbuffers.rx;
-  pc.max_nof_iterations  = cfg->max_nof_iterations;
-  return dlsch_decode_sync(q, &pc, nullptr, d_g, data, 0, 1);
+  if (cq.ri_len > 0) {
+    uci_data->ri = h.out.ri[0];
+  }
+  if (cq.data_enable) {
+    uci_data->cqi.data_crc = h.out.cqi_crc != 0;
+    srsran_cqi_value_unpack(&cq, h.out.cqi, &uci_data->cqi);
+  }
+  if (hl_ri) {
+    cq.rank_is_not_one = uci_data->ri > 0;  // sch.c:1112-1117
+  }
+  return ret;
 }
 
 int srsran_ulsch_gpu_decode_batch(srsran_sch_t*                q,
@@ -1091,7 +1499,7 @@ int srsran_ulsch_gpu_decode_batch(srsran_sch_t*                q,
       return SRSRAN_ERROR_INVALID_INPUTS;
     }
     const uint32_t rows = t.nof_e_bits / t.Qm / t.nof_symb;
-    desc[i]             = {t.d_q_bits, t.d_g_bits, rows, t.nof_symb, t.Qm};
+    desc[i]             = {t.d_q_bits, t.d_g_bits, rows, t.nof_symb, t.Qm, {}, -1};
     max_n               = std::max(max_n, rows);
     dl[i]               = {t.tbs, t.Qm, t.rv, t.nof_e_bits, t.d_g_bits, t.d_data, t.softbuffer, t.new_data};
   }

@@ -66,6 +66,11 @@ struct UlDeint {
   const int16_t* q;
   int16_t*       g;
   uint32_t       rows, cols, Qm;
+  // RI multiplexed (sch.c:994-1021 with ri_present): column i holds RI in its last ri_rows[i]
+  // rows, which the de-interleaver skips; srsran_vec_lut_sis maps every skipped position to
+  // g[0], so the last one (q[g0_src]) ends there.  ri_rows all 0 / g0_src < 0 without RI.
+  uint16_t ri_rows[14];
+  int32_t  g0_src;
 };
 // many TBs in one launch (grid.y = TB); d_desc on the device; cols <= 14, Qm <= 8
 hipError_t ul_deint_batch_launch(const UlDeint* d_desc, uint32_t ntb, uint32_t max_rows, hipStream_t stream);

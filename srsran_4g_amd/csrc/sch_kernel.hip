@@ -508,9 +508,28 @@ __global__ __launch_bounds__(256) void ul_deint_batch_kernel(const UlDeint* __re
   }
   __syncthreads();
   const uint32_t row = d.cols * d.Qm;  // LLRs of one output row j
+  if (d.g0_src < 0) {
+    for (uint32_t x = threadIdx.x; x < nj * row; x += blockDim.x) {
+      const uint32_t jj = x / row, r = x - jj * row, i = r / d.Qm, k = r - i * d.Qm;
+      d.g[j0 * row + x] = tile[i * UL_TILE_J * UL_MAX_QM + jj * d.Qm + k];
+    }
+    return;
+  }
+  // with RI: row j holds the non-RI cells of that row; the rows before it lost sum_i max(0,
+  // j - (rows - ri_rows[i])) cells
   for (uint32_t x = threadIdx.x; x < nj * row; x += blockDim.x) {
-    const uint32_t jj = x / row, r = x - jj * row, i = r / d.Qm, k = r - i * d.Qm;
-    d.g[j0 * row + x] = tile[i * UL_TILE_J * UL_MAX_QM + jj * d.Qm + k];
+    const uint32_t jj = x / row, r = x - jj * row, i = r / d.Qm, k = r - i * d.Qm, j = j0 + jj;
+    if (j + d.ri_rows[i] >= d.rows) {
+      continue;
+    }
+    uint32_t lost = 0, before = 0;
+    for (uint32_t c = 0; c < d.cols; c++) {
+      const uint32_t first = d.rows - d.ri_rows[c];  // first RI row of column c
+      lost += j > first ? j - first : 0;
+      before += (c < i && j >= first) ? 1 : 0;
+    }
+    const uint32_t o = (j * d.cols - lost + i - before) * d.Qm + k;
+    d.g[o]           = o == 0 ? d.q[d.g0_src] : tile[i * UL_TILE_J * UL_MAX_QM + jj * d.Qm + k];
   }
 }
 

@@ -119,6 +119,47 @@ class srsran_pusch_cfg_t(ctypes.Structure):
                 ("meas_evm_en", ctypes.c_bool)]
 
 
+u8 = ctypes.c_uint8
+SRSRAN_CQI_TYPE_WIDEBAND, SRSRAN_CQI_TYPE_SUBBAND_UE, SRSRAN_CQI_TYPE_SUBBAND_UE_DIFF, SRSRAN_CQI_TYPE_SUBBAND_HL = range(4)
+SRSRAN_CQI_MAX_BITS = 64
+
+
+class srsran_cqi_hl_subband_t(ctypes.Structure):
+    _fields_ = [("wideband_cqi_cw0", u8), ("subband_diff_cqi_cw0", u32), ("wideband_cqi_cw1", u8),
+                ("subband_diff_cqi_cw1", u32), ("pmi", u32)]
+
+
+class srsran_cqi_ue_diff_subband_t(ctypes.Structure):
+    _fields_ = [("wideband_cqi", u8), ("subband_diff_cqi", u8), ("position_subband", u32)]
+
+
+class srsran_cqi_format2_wideband_t(ctypes.Structure):
+    _fields_ = [("wideband_cqi", u8), ("spatial_diff_cqi", u8), ("pmi", u8)]
+
+
+class srsran_cqi_ue_subband_t(ctypes.Structure):
+    _fields_ = [("subband_cqi", u8), ("subband_label", u8)]
+
+
+class _cqi_value_u(ctypes.Union):
+    _fields_ = [("wideband", srsran_cqi_format2_wideband_t), ("subband_ue", srsran_cqi_ue_subband_t),
+                ("subband_ue_diff", srsran_cqi_ue_diff_subband_t), ("subband_hl", srsran_cqi_hl_subband_t)]
+
+
+class srsran_cqi_value_t(ctypes.Structure):
+    _anonymous_ = ("u",)
+    _fields_ = [("u", _cqi_value_u), ("data_crc", ctypes.c_bool)]
+
+
+class srsran_uci_value_ack_t(ctypes.Structure):
+    _fields_ = [("ack_value", u8 * 10), ("valid", ctypes.c_bool)]
+
+
+class srsran_uci_value_t(ctypes.Structure):
+    _fields_ = [("scheduling_request", ctypes.c_bool), ("cqi", srsran_cqi_value_t), ("ack", srsran_uci_value_ack_t),
+                ("ri", u8)]
+
+
 class srsran_ulsch_gpu_tb_t(ctypes.Structure):
     _fields_ = [("tbs", u32), ("Qm", u32), ("rv", u32), ("nof_e_bits", u32), ("nof_symb", u32),
                 ("d_q_bits", ctypes.c_void_p), ("d_g_bits", ctypes.c_void_p), ("d_data", ctypes.c_void_p),
@@ -172,8 +213,21 @@ def lib():
         "srsran_dlsch_decode2": ([SCH, CFG, _i16p, _u8p, ctypes.c_int, u32], ctypes.c_int),
         "srsran_dlsch_gpu_decode_batch": ([SCH, u32, ctypes.POINTER(srsran_dlsch_gpu_tb_t), ctypes.c_void_p,
                                            ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
-        "srsran_ulsch_decode": ([SCH, ctypes.POINTER(srsran_pusch_cfg_t), _i16p, _i16p, _u8p, _u8p, ctypes.c_void_p],
-                                ctypes.c_int),
+        "srsran_ulsch_decode": ([SCH, ctypes.POINTER(srsran_pusch_cfg_t), _i16p, _i16p, _u8p, _u8p,
+                                 ctypes.POINTER(srsran_uci_value_t)], ctypes.c_int),
+        "srsran_sch_beta_cqi": ([u32], ctypes.c_float),
+        "srsran_sch_beta_ack": ([u32], ctypes.c_float),
+        "srsran_sch_find_Ioffset_ack": ([ctypes.c_float], u32),
+        "srsran_sch_find_Ioffset_cqi": ([ctypes.c_float], u32),
+        "srsran_sch_find_Ioffset_ri": ([ctypes.c_float], u32),
+        "srsran_qprime_cqi_ext": ([u32, u32, u32, ctypes.c_float], u32),
+        "srsran_qprime_ack_ext": ([u32, u32, u32, u32, ctypes.c_float], u32),
+        "srsran_uci_cfg_total_ack": ([ctypes.POINTER(srsran_uci_cfg_t)], u32),
+        "srsran_cqi_size": ([ctypes.POINTER(srsran_cqi_cfg_t)], ctypes.c_int),
+        "srsran_cqi_value_pack": ([ctypes.POINTER(srsran_cqi_cfg_t), ctypes.POINTER(srsran_cqi_value_t), _u8p],
+                                  ctypes.c_int),
+        "srsran_cqi_value_unpack": ([ctypes.POINTER(srsran_cqi_cfg_t), _u8p, ctypes.POINTER(srsran_cqi_value_t)],
+                                    ctypes.c_int),
         "srsran_ulsch_gpu_decode_batch": ([SCH, u32, ctypes.POINTER(srsran_ulsch_gpu_tb_t), ctypes.c_void_p,
                                            ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
     }
@@ -353,6 +407,20 @@ class Sch:
         ret = lib().srsran_ulsch_decode(ctypes.byref(self.q), ctypes.byref(cfg), q.ctypes.data_as(_i16p),
                                         g.ctypes.data_as(_i16p), None, data.ctypes.data_as(_u8p), None)
         return ret, data, g, self.last_noi(), cfg.K_segm
+
+    def ulsch_decode_uci(self, cfg, q_bits, c_seq=None, g_bits=None, tbs=None):
+        """srsran_ulsch_decode with a prepared srsran_pusch_cfg_t (UCI fields set by the caller).
+        Returns (ret, data bytes, q_bits after the call, g_bits, srsran_uci_value_t)."""
+        q = np.array(q_bits, dtype=np.int16, copy=True)
+        g = np.zeros_like(q) if g_bits is None else np.array(g_bits, dtype=np.int16, copy=True)
+        nbytes = (tbs if tbs is not None else cfg.grant.tb.tbs) // 8 + 64
+        data = np.zeros(nbytes, np.uint8)
+        uci = srsran_uci_value_t()
+        c = None if c_seq is None else np.ascontiguousarray(c_seq, dtype=np.uint8)
+        ret = lib().srsran_ulsch_decode(ctypes.byref(self.q), ctypes.byref(cfg), q.ctypes.data_as(_i16p),
+                                        g.ctypes.data_as(_i16p), None if c is None else c.ctypes.data_as(_u8p),
+                                        data.ctypes.data_as(_u8p), ctypes.byref(uci))
+        return ret, data, q, g, uci
 
     def ulsch_decode_batch(self, entries, d_result, d_avg, stream=None):
         """srsran_ulsch_gpu_decode_batch. entries: (tbs, Qm, rv, nof_e_bits, nof_symb, d_q, d_g, d_data,

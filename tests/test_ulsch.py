@@ -107,20 +107,3 @@ def test_ulsch_batch_matches_oracle(ora):
         if isinstance(k, S.SoftbufferRx):
             k.free()
     q.free()
-
-
-@pytest.mark.gpu
-def test_ulsch_uci_is_refused():
-    from srsran_4g_amd import sch as S
-    from srsran_4g_amd import tdec
-    if not tdec.gpu_available():
-        pytest.skip("no HIP device")
-    q = S.Sch()
-    sb = S.SoftbufferRx(nof_prb=100)
-
-    def with_ack(u):
-        u.ack[0].nof_acks = 1
-    ret, *_ = q.ulsch_decode(sb, 1544, 2, 0, 12, np.zeros(6 * 12 * 12 * 2, np.int16), uci_cfg=with_ack)
-    assert ret != 0
-    sb.free()
-    q.free()

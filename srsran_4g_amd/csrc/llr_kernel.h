@@ -32,6 +32,8 @@ hipError_t llr_batch_launch(int mod, const LlrItem* d_items, uint32_t nitems, ui
 
 // out[i] = c(i) ? -in[i] : in[i] (int16 wrap) for the Gold sequence of `seed`.
 hipError_t seq_apply_launch(const int16_t* d_in, int16_t* d_out, uint32_t len, uint32_t seed, hipStream_t stream);
+// out[i] = c(i) (one byte per bit) for the Gold sequence of `seed`.
+hipError_t seq_unpack_launch(uint8_t* d_out, uint32_t len, uint32_t seed, hipStream_t stream);
 
 }  // namespace srsran_amd
 #endif

@@ -563,4 +563,46 @@ hipError_t seq_apply_launch(const int16_t* d_in, int16_t* d_out, uint32_t len, u
   return hipGetLastError();
 }
 
+// c(i) as one byte per bit (srsran_sequence_pusch_gen_unpack, sequences.c:95-102): the UCI
+// decoder's scrambling sequence, 16 bits written as 4 dwords
+__global__ __launch_bounds__(LLR_THREADS) void seq_unpack_kernel(uint8_t* __restrict__ out, uint32_t len,
+                                                                 uint32_t seed)
+{
+  const uint32_t i0 = (blockIdx.x * LLR_THREADS + threadIdx.x) * SEQ_PER_THREAD;
+  if (i0 >= len) {
+    return;
+  }
+  uint32_t x1, x2;
+  gold_at(seed, i0, x1, x2);
+  const uint32_t n = min((uint32_t)SEQ_PER_THREAD, len - i0);
+#pragma unroll
+  for (int c = 0; c < SEQ_PER_THREAD / 16; c++) {
+    const uint32_t bits = gold16(x1, x2);
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      const uint32_t i = (uint32_t)(16 * c + k);
+      if (i < n) {
+        out[i0 + i] = (uint8_t)((bits >> k) & 1u);
+      }
+    }
+  }
+}
+
+hipError_t seq_unpack_launch(uint8_t* d_out, uint32_t len, uint32_t seed, hipStream_t stream)
+{
+  if (len == 0) {
+    return hipSuccess;
+  }
+  if (len > (1u << JUMP_BITS)) {
+    return hipErrorInvalidValue;
+  }
+  hipError_t e = gold_tables_init();
+  if (e != hipSuccess) {
+    return e;
+  }
+  const dim3 grid((len + LLR_THREADS * SEQ_PER_THREAD - 1) / (LLR_THREADS * SEQ_PER_THREAD));
+  hipLaunchKernelGGL(seq_unpack_kernel, grid, dim3(LLR_THREADS), 0, stream, d_out, len, seed);
+  return hipGetLastError();
+}
+
 }  // namespace srsran_amd

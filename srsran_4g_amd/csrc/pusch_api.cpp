@@ -1,0 +1,929 @@
+// srsran_4g_amd/csrc/pusch_api.cpp -- C-ABI of the PUSCH receive path (include/srsran_pusch.h):
+// PUSCH DMRS generation (refsignal_ul.c:95-358 restated), the UL channel estimator object
+// (chest_ul.c:53-433) and srsran_pusch_t (pusch.c:108-471), over the kernels of pusch_kernel.hip,
+// llr_kernel.hip and the UL-SCH decoder of sch_api.cpp.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "../../include/srsran_pusch.h"
+#include "llr_kernel.h"
+#include "pusch_kernel.h"
+
+namespace srsran_amd {
+int         ulsch_decode_dev(srsran_sch_t* q, srsran_pusch_cfg_t* cfg, int16_t* d_q, const uint8_t* d_c, uint8_t* data,
+                             srsran_uci_value_t* uci_data);
+hipStream_t sch_stream(srsran_sch_t* q);
+}  // namespace srsran_amd
+
+using namespace srsran_amd;
+
+namespace {
+
+#include "zc_tables.inc"
+
+constexpr uint32_t kNdmrs1[8] = {0, 2, 3, 4, 6, 8, 9, 10};  // 36.211 Table 5.5.2.1.1-2
+constexpr uint32_t kNdmrs2[8] = {0, 6, 3, 4, 2, 8, 10, 9};  // 36.211 Table 5.5.2.1.1-1
+
+uint32_t nsymb_slot(srsran_cp_t cp) { return cp == SRSRAN_CP_NORM ? 7u : 6u; }
+
+bool cell_valid(const srsran_cell_t& c) { return c.id < 504 && c.nof_ports >= 1 && c.nof_ports <= 4 && c.nof_prb >= 6 && c.nof_prb <= SRSRAN_MAX_PRB; }
+
+// LTE Gold sequence c(n) (36.211 7.2, Nc = 1600)
+void gold(uint32_t c_init, uint8_t* c, uint32_t len)
+{
+  uint32_t x1 = 1, x2 = c_init & 0x7FFFFFFFu;
+  auto     s1 = [](uint32_t s) { return (s >> 1) ^ (((s ^ (s >> 3)) & 1u) << 30); };
+  auto     s2 = [](uint32_t s) { return (s >> 1) ^ (((s ^ (s >> 1) ^ (s >> 2) ^ (s >> 3)) & 1u) << 30); };
+  for (int n = 0; n < 1600; n++) {
+    x1 = s1(x1);
+    x2 = s2(x2);
+  }
+  for (uint32_t n = 0; n < len; n++) {
+    c[n] = (uint8_t)((x1 ^ x2) & 1u);
+    x1   = s1(x1);
+    x2   = s2(x2);
+  }
+}
+
+// the per-cell hopping tables of srsran_refsignal_ul_set_cell (refsignal_ul.c:95-171)
+struct UlHopping {
+  uint32_t n_prs[SRSRAN_NOF_DELTA_SS][SRSRAN_NSLOTS_X_FRAME];  // 5.5.2.1.1 n_PN(ns)
+  uint32_t f_gh[SRSRAN_NSLOTS_X_FRAME];                       // 5.5.1.3 group hopping
+  uint32_t v[SRSRAN_NSLOTS_X_FRAME][SRSRAN_NOF_DELTA_SS];     // 5.5.1.4 sequence hopping
+};
+
+void hopping_tables(const srsran_cell_t& cell, UlHopping& h)
+{
+  const uint32_t       ns_len = 8 * nsymb_slot(cell.cp) * 20;
+  std::vector<uint8_t> c(ns_len);
+  for (uint32_t dss = 0; dss < SRSRAN_NOF_DELTA_SS; dss++) {
+    const uint32_t c_init = ((cell.id / 30) << 5) + (((cell.id % 30) + dss) % 30);
+    gold(c_init, c.data(), ns_len);
+    for (uint32_t ns = 0; ns < SRSRAN_NSLOTS_X_FRAME; ns++) {
+      uint32_t n = 0;
+      for (int i = 0; i < 8; i++) {
+        n += (uint32_t)c[8 * nsymb_slot(cell.cp) * ns + i] << i;
+      }
+      h.n_prs[dss][ns] = n;
+      h.v[ns][dss]     = c[ns];  // the first 20 bits of the same sequence
+    }
+  }
+  gold(cell.id / 30, c.data(), 160);
+  for (uint32_t ns = 0; ns < SRSRAN_NSLOTS_X_FRAME; ns++) {
+    h.f_gh[ns] = 0;
+    for (int i = 0; i < 8; i++) {
+      h.f_gh[ns] += (uint32_t)c[8 * ns + i] << i;
+    }
+  }
+}
+
+uint32_t prime_below(uint32_t n)  // largest prime < n (srsran_prime_lower_than)
+{
+  for (uint32_t p = n - 1; p > 2; p--) {
+    bool is = true;
+    for (uint32_t d = 2; d * d <= p; d++) {
+      if (p % d == 0) {
+        is = false;
+        break;
+      }
+    }
+    if (is) {
+      return p;
+    }
+  }
+  return 2;
+}
+
+// base sequence r_uv(n) e^{j alpha n} of 36.211 5.5.1, float arithmetic of zc_sequence.c:214-311
+void zc_sequence(uint32_t u, uint32_t v, float alpha, uint32_t nof_prb, cf_t* out)
+{
+  const uint32_t     Mzc = nof_prb * SRSRAN_NRE;
+  std::vector<float> arg(Mzc);
+  if (Mzc == 12 || Mzc == 24) {
+    const int8_t* phi = Mzc == 12 ? kZcPhi12[u] : kZcPhi24[u];
+    for (uint32_t i = 0; i < Mzc; i++) {
+      arg[i] = (float)phi[i] * (float)M_PI_4;
+    }
+  } else {
+    const uint32_t Nzc   = prime_below(Mzc);
+    const float    n_sz  = (float)Nzc;
+    const float    q_hat = n_sz * (float)(u + 1) / 31.0f;
+    const float    qf    = (((uint32_t)(2 * q_hat)) % 2 == 0) ? (float)(q_hat + 0.5 + v) : (float)(q_hat + 0.5 - v);
+    const float    q     = (float)(uint32_t)qf;
+    for (uint32_t i = 0; i < Mzc; i++) {
+      const float m = (float)(i % Nzc);
+      arg[i]        = (float)(-M_PI * q * m * (m + 1) / n_sz);
+    }
+  }
+  for (uint32_t i = 0; i < Mzc; i++) {
+    float s, c;
+    sincosf(arg[i] + alpha * (float)i, &s, &c);
+    out[i] = cf_t{c, s};
+  }
+}
+
+int dmrs_gen(const srsran_cell_t& cell, const UlHopping& h, const srsran_refsignal_dmrs_pusch_cfg_t& cfg,
+             uint32_t nof_prb, uint32_t sf_idx, uint32_t cs_dmrs, cf_t* r)
+{
+  if (cfg.cyclic_shift >= SRSRAN_NOF_CSHIFT || cfg.delta_ss >= SRSRAN_NOF_DELTA_SS || nof_prb > cell.nof_prb ||
+      cs_dmrs >= SRSRAN_NOF_CSHIFT || sf_idx >= SRSRAN_NOF_SF_X_FRAME || nof_prb == 0) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  for (uint32_t ns = 2 * sf_idx; ns < 2 * (sf_idx + 1); ns++) {
+    const uint32_t n_cs  = (kNdmrs1[cfg.cyclic_shift] + kNdmrs2[cs_dmrs] + h.n_prs[cfg.delta_ss][ns]) % 12;
+    const float    alpha = (float)(2 * M_PI * n_cs / 12);
+    const uint32_t u     = ((cfg.group_hopping_en ? h.f_gh[ns] : 0) + (cell.id % 30) + cfg.delta_ss) % 30;
+    const uint32_t v     = (nof_prb >= 6 && cfg.sequence_hopping_en) ? h.v[ns][cfg.delta_ss] : 0;
+    zc_sequence(u, v, alpha, nof_prb, r + (ns % 2) * SRSRAN_NRE * nof_prb);
+  }
+  return SRSRAN_SUCCESS;
+}
+
+// inverse-DFT plan: radices 4, 2, 3, 5 (M = 12 L, L = 2^a 3^b 5^c)
+bool dft_plan(uint32_t M, PuschUe& u)
+{
+  u.nstages = 0;
+  uint32_t n = M;
+  for (uint32_t R : {4u, 2u, 3u, 5u}) {
+    while (n % R == 0) {
+      if (u.nstages == PUSCH_MAX_STAGES) {
+        return false;
+      }
+      u.radix[u.nstages++] = (uint8_t)R;
+      n /= R;
+    }
+  }
+  return n == 1;
+}
+
+bool grow(void** p, size_t* cap, size_t need)
+{
+  if (need <= *cap) {
+    return true;
+  }
+  hipFree(*p);
+  *p   = nullptr;
+  *cap = 0;
+  if (hipMalloc(p, need) != hipSuccess) {
+    return false;
+  }
+  *cap = need;
+  return true;
+}
+
+// ---------------- chest_ul device state ----------------
+struct ChestUlGpu {
+  hipStream_t         stream = nullptr;
+  uint32_t            max_prb = 0;
+  UlHopping           hop;
+  bool                hop_ok = false;
+  float2*             d_dmrs = nullptr;  // [cs][sf][valid n <= cell prb] 2 * 12 n values
+  size_t              dmrs_cap = 0;
+  std::vector<size_t> dmrs_off;          // (cs * 10 + sf) * 101 + n -> offset (values)
+  float2*             d_grid = nullptr;  // one subframe grid
+  size_t              grid_cap = 0;
+  PuschUe*            d_desc = nullptr;
+  size_t              desc_cap = 0;
+};
+
+struct ChestUlResGpu {
+  float2*     d_ce  = nullptr;  // nof_re values
+  ChestUlOut* d_out = nullptr;
+  uint32_t    nof_re = 0;
+  bool        valid  = false;   // d_ce holds the last estimate written to ce
+};
+
+size_t dmrs_index(uint32_t cs, uint32_t sf, uint32_t n) { return ((size_t)cs * SRSRAN_NOF_SF_X_FRAME + sf) * 101 + n; }
+
+// the PUSCH data symbols of the subframe (pusch_cp, pusch.c:48-95)
+uint32_t data_symbols(srsran_cp_t cp, bool shortened, uint8_t* out)
+{
+  const uint32_t ns = nsymb_slot(cp), L_ref = cp == SRSRAN_CP_NORM ? 3 : 2;
+  uint32_t       n  = 0;
+  for (uint32_t slot = 0; slot < 2; slot++) {
+    const uint32_t n_srs = (shortened && slot == 1) ? 1 : 0;
+    for (uint32_t l = 0; l < ns - n_srs; l++) {
+      if (l != L_ref) {
+        out[n++] = (uint8_t)(l + slot * ns);
+      }
+    }
+  }
+  return n;
+}
+
+void fill_chest_desc(PuschUe& u, const srsran_chest_ul_t* q, const srsran_pusch_cfg_t* cfg, uint32_t M)
+{
+  u.ncell_re   = q->cell.nof_prb * SRSRAN_NRE;
+  u.M          = M;
+  u.nsym_slot  = nsymb_slot(q->cell.cp);
+  u.n_tilde[0] = cfg->grant.n_prb_tilde[0];
+  u.n_tilde[1] = cfg->grant.n_prb_tilde[1];
+  u.n_prb[0]   = cfg->grant.n_prb[0];
+  u.n_prb[1]   = cfg->grant.n_prb[1];
+  u.smooth     = q->smooth_filter_len == 3;
+  u.filt[0] = u.smooth ? q->smooth_filter[0] : 0.f;
+  u.filt[1] = u.smooth ? q->smooth_filter[1] : 0.f;
+  u.filt[2] = u.smooth ? q->smooth_filter[2] : 0.f;
+  u.meas_ta    = cfg->meas_ta_en;
+  // estimate_noise_pilots' calibration for the 3-tap filter (chest_ul.c:220-225)
+  const float w = q->smooth_filter[0];
+  const float a = (float)(7.419 * w * w + 0.1117 * w - 0.005387);
+  u.noise_div   = (double)a * 0.8;
+  u.noise_dev   = 1;
+  u.dft_norm    = 1.0f / sqrtf((float)M);
+}
+
+void finish_chest_res(srsran_chest_ul_res_t* res, const ChestUlOut& o)
+{
+  res->noise_estimate      = o.noise;
+  res->cfo_hz              = o.cfo_hz;
+  res->ta_us               = o.ta_us;
+  res->rsrp                = o.rsrp;
+  res->epre                = o.epre;
+  res->snr                 = isnormal(o.noise) ? o.epre / o.noise : NAN;
+  res->epre_dBfs           = 10.0f * log10f(res->epre);
+  res->rsrp_dBfs           = 10.0f * log10f(res->rsrp);
+  res->snr_db              = 10.0f * log10f(res->snr);
+  res->noise_estimate_dbFs = 10.0f * log10f(res->noise_estimate) + 30.0f;
+}
+
+// check a PUSCH allocation against the estimator / cell (chest_ul.c:409-414, pusch.c:392-410)
+int check_alloc(const srsran_cell_t& cell, const srsran_pusch_cfg_t* cfg)
+{
+  const uint32_t L = cfg->grant.L_prb;
+  if (!srsran_dft_precoding_valid_prb(L) || L > cell.nof_prb) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  for (int s = 0; s < 2; s++) {
+    if (cfg->grant.n_prb_tilde[s] + L > cell.nof_prb || cfg->grant.n_prb[s] + L > cell.nof_prb) {
+      return SRSRAN_ERROR_INVALID_INPUTS;
+    }
+  }
+  if (cfg->grant.n_dmrs >= SRSRAN_NOF_CSHIFT) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  return SRSRAN_SUCCESS;
+}
+
+// ---------------- PUSCH device state ----------------
+struct PuschGpu {
+  float2*     d_grid = nullptr;  // subframe grid (sync API)
+  float2*     d_ce   = nullptr;  // estimate grid uploaded from the host (sync API, channel->gpu absent)
+  size_t      grid_cap = 0, ce_cap = 0;
+  float2*     d_sym  = nullptr;  // de-precoded symbols
+  size_t      sym_cap = 0;
+  int16_t*    d_q    = nullptr;  // LLRs
+  size_t      q_cap  = 0;
+  uint8_t*    d_c    = nullptr;  // unpacked scrambling sequence
+  size_t      c_cap  = 0;
+  PuschUe*    d_desc = nullptr;
+  size_t      desc_cap = 0;
+  LlrItem*    d_llr  = nullptr;
+  size_t      llr_cap = 0;
+  ChestUlOut* d_out  = nullptr;  // per-UE outputs (sync API: one; batch: nof_ue)
+  size_t      out_cap = 0;
+  float2*     d_bce  = nullptr;  // batch: per-UE estimate grids
+  size_t      bce_cap = 0;
+};
+
+uint32_t pusch_seed(uint16_t rnti, uint32_t nslot, uint32_t cell_id)  // sequences.c:119-122
+{
+  return ((uint32_t)rnti << 14) + ((nslot / 2) << 9) + cell_id;
+}
+
+// pusch.c:374-380
+void limit_64qam(srsran_pusch_cfg_t* cfg)
+{
+  if (!cfg->enable_64qam && cfg->grant.tb.mod >= SRSRAN_MOD_64QAM) {
+    cfg->grant.tb.mod      = SRSRAN_MOD_16QAM;
+    cfg->grant.tb.nof_bits = cfg->grant.nof_re * 4;
+  }
+}
+
+bool any_uci(const srsran_pusch_cfg_t* cfg)
+{
+  return srsran_uci_cfg_total_ack(&cfg->uci_cfg) > 0 || cfg->uci_cfg.cqi.ri_len > 0 || cfg->uci_cfg.cqi.data_enable;
+}
+
+}  // namespace
+
+extern "C" {
+
+bool srsran_dft_precoding_valid_prb(uint32_t nof_prb)
+{
+  // 36.213 14.1.1.4C: L_prb = 2^a 3^b 5^c (dft_precoding.c:88-103)
+  if (nof_prb == 0 || nof_prb > 100) {
+    return nof_prb == 0;
+  }
+  uint32_t n = nof_prb;
+  for (uint32_t p : {2u, 3u, 5u}) {
+    while (n % p == 0) {
+      n /= p;
+    }
+  }
+  return n == 1;
+}
+
+uint32_t srsran_dft_precoding_get_valid_prb(uint32_t nof_prb)
+{
+  while (!srsran_dft_precoding_valid_prb(nof_prb)) {
+    nof_prb--;
+  }
+  return nof_prb;
+}
+
+int srsran_dft_precoding_gpu(const cf_t* d_input, cf_t* d_output, uint32_t nof_prb, uint32_t nof_symbols, void* stream)
+{
+  if (!d_input || !d_output || nof_prb == 0 || !srsran_dft_precoding_valid_prb(nof_prb) || nof_symbols == 0 ||
+      nof_symbols > 14) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  PuschUe u;
+  memset(&u, 0, sizeof(u));
+  const uint32_t M = nof_prb * SRSRAN_NRE;
+  if (!dft_plan(M, u)) {
+    return SRSRAN_ERROR;
+  }
+  u.grid      = (const float2*)d_input;
+  u.sym       = (float2*)d_output;
+  u.ncell_re  = M;
+  u.M         = M;
+  u.nsym_slot = 14;
+  u.nof_symb  = nof_symbols;
+  for (uint32_t l = 0; l < nof_symbols; l++) {
+    u.data_sym[l] = (uint8_t)l;
+  }
+  u.dft_norm     = 1.0f / sqrtf((float)M);
+  hipStream_t st = (hipStream_t)stream;
+  PuschUe*    d  = nullptr;
+  // the descriptor travels as a kernel-visible copy: one small allocation per call, freed in order
+  if (hipMallocAsync((void**)&d, sizeof(u), st) != hipSuccess ||
+      hipMemcpyAsync(d, &u, sizeof(u), hipMemcpyHostToDevice, st) != hipSuccess ||
+      pusch_eq_idft_launch(d, 1, st) != hipSuccess || hipFreeAsync(d, st) != hipSuccess) {
+    return SRSRAN_ERROR;
+  }
+  return SRSRAN_SUCCESS;
+}
+
+int srsran_refsignal_dmrs_pusch_gen_cell(const srsran_cell_t*               cell,
+                                         srsran_refsignal_dmrs_pusch_cfg_t* cfg,
+                                         uint32_t                           nof_prb,
+                                         uint32_t                           sf_idx,
+                                         uint32_t                           cyclic_shift_for_dmrs,
+                                         cf_t*                              r_pusch)
+{
+  if (!cell || !cfg || !r_pusch || !cell_valid(*cell)) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  UlHopping h;
+  hopping_tables(*cell, h);
+  return dmrs_gen(*cell, h, *cfg, nof_prb, sf_idx, cyclic_shift_for_dmrs, r_pusch);
+}
+
+// ---------------- chest_ul.c:53-204 ----------------
+int srsran_chest_ul_init(srsran_chest_ul_t* q, uint32_t max_prb)
+{
+  if (!q || max_prb > SRSRAN_MAX_PRB) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  memset(q, 0, sizeof(*q));
+  q->smooth_filter_len = 3;
+  q->smooth_filter[0]  = 0.3333f;  // srsran_chest_set_smooth_filter3_coeff(.., 0.3333)
+  q->smooth_filter[2]  = 0.3333f;
+  q->smooth_filter[1]  = 1 - 2 * 0.3333f;
+  ChestUlGpu* g        = new ChestUlGpu();
+  g->max_prb           = max_prb;
+  q->gpu               = g;
+  if (hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking) != hipSuccess) {
+    srsran_chest_ul_free(q);
+    return SRSRAN_ERROR;
+  }
+  return SRSRAN_SUCCESS;
+}
+
+void srsran_chest_ul_free(srsran_chest_ul_t* q)
+{
+  if (!q) {
+    return;
+  }
+  ChestUlGpu* g = (ChestUlGpu*)q->gpu;
+  if (g) {
+    if (g->stream) {
+      hipStreamSynchronize(g->stream);
+      hipStreamDestroy(g->stream);
+    }
+    hipFree(g->d_dmrs);
+    hipFree(g->d_grid);
+    hipFree(g->d_desc);
+    delete g;
+  }
+  memset(q, 0, sizeof(*q));
+}
+
+int srsran_chest_ul_res_init(srsran_chest_ul_res_t* q, uint32_t max_prb)
+{
+  if (!q) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  memset(q, 0, sizeof(*q));
+  q->nof_re = max_prb * SRSRAN_NRE * 2 * SRSRAN_CP_NORM_NSYMB;  // SRSRAN_SF_LEN_RE(max_prb, NORM)
+  q->ce     = (cf_t*)calloc(q->nof_re ? q->nof_re : 1, sizeof(cf_t));
+  if (!q->ce) {
+    return SRSRAN_ERROR;
+  }
+  ChestUlResGpu* g = new ChestUlResGpu();
+  g->nof_re        = q->nof_re;
+  q->gpu           = g;
+  if (hipMalloc((void**)&g->d_ce, (size_t)std::max<uint32_t>(q->nof_re, 1) * sizeof(float2)) != hipSuccess ||
+      hipMemset(g->d_ce, 0, (size_t)std::max<uint32_t>(q->nof_re, 1) * sizeof(float2)) != hipSuccess ||
+      hipMalloc((void**)&g->d_out, sizeof(ChestUlOut)) != hipSuccess) {
+    srsran_chest_ul_res_free(q);
+    return SRSRAN_ERROR;
+  }
+  return SRSRAN_SUCCESS;
+}
+
+void srsran_chest_ul_res_set_identity(srsran_chest_ul_res_t* q)
+{
+  if (!q) {
+    return;
+  }
+  for (uint32_t i = 0; i < q->nof_re; i++) {
+    q->ce[i] = 1.0f;
+  }
+  ChestUlResGpu* g = (ChestUlResGpu*)q->gpu;
+  if (g) {
+    g->valid = false;  // the host copy is the current one
+  }
+}
+
+void srsran_chest_ul_res_free(srsran_chest_ul_res_t* q)
+{
+  if (!q) {
+    return;
+  }
+  free(q->ce);
+  ChestUlResGpu* g = (ChestUlResGpu*)q->gpu;
+  if (g) {
+    hipFree(g->d_ce);
+    hipFree(g->d_out);
+    delete g;
+  }
+  memset(q, 0, sizeof(*q));
+}
+
+int srsran_chest_ul_set_cell(srsran_chest_ul_t* q, srsran_cell_t cell)
+{
+  if (!q || !q->gpu || !cell_valid(cell)) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  ChestUlGpu* g = (ChestUlGpu*)q->gpu;
+  if (cell.id != q->cell.id || q->cell.nof_prb == 0 || !g->hop_ok || cell.cp != q->cell.cp) {
+    q->cell = cell;
+    hopping_tables(cell, g->hop);
+    g->hop_ok = true;
+  }
+  q->cell = cell;
+  return SRSRAN_SUCCESS;
+}
+
+void srsran_chest_ul_pregen(srsran_chest_ul_t* q, srsran_refsignal_dmrs_pusch_cfg_t* cfg, void* srs_cfg)
+{
+  (void)srs_cfg;
+  if (!q || !q->gpu || !cfg || !((ChestUlGpu*)q->gpu)->hop_ok) {
+    return;
+  }
+  ChestUlGpu* g = (ChestUlGpu*)q->gpu;
+  // every (n_dmrs, subframe, valid L_prb <= cell PRB) sequence, as srsran_refsignal_dmrs_pusch_pregen
+  const uint32_t nmax = std::min(q->cell.nof_prb, g->max_prb ? g->max_prb : q->cell.nof_prb);
+  g->dmrs_off.assign(dmrs_index(SRSRAN_NOF_CSHIFT, 0, 0), (size_t)-1);
+  size_t total = 0;
+  for (uint32_t cs = 0; cs < SRSRAN_NOF_CSHIFT; cs++) {
+    for (uint32_t sf = 0; sf < SRSRAN_NOF_SF_X_FRAME; sf++) {
+      for (uint32_t n = 1; n <= nmax; n++) {
+        if (srsran_dft_precoding_valid_prb(n)) {
+          g->dmrs_off[dmrs_index(cs, sf, n)] = total;
+          total += 2 * SRSRAN_NRE * n;
+        }
+      }
+    }
+  }
+  std::vector<cf_t> h(std::max<size_t>(total, 1));
+  for (uint32_t cs = 0; cs < SRSRAN_NOF_CSHIFT; cs++) {
+    for (uint32_t sf = 0; sf < SRSRAN_NOF_SF_X_FRAME; sf++) {
+      for (uint32_t n = 1; n <= nmax; n++) {
+        const size_t o = g->dmrs_off[dmrs_index(cs, sf, n)];
+        if (o != (size_t)-1) {
+          dmrs_gen(q->cell, g->hop, *cfg, n, sf, cs, &h[o]);
+        }
+      }
+    }
+  }
+  if (!grow((void**)&g->d_dmrs, &g->dmrs_cap, h.size() * sizeof(float2)) ||
+      hipMemcpy(g->d_dmrs, h.data(), h.size() * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess) {
+    fprintf(stderr, "[srsran_chest_ul] DMRS upload failed\n");
+    return;
+  }
+  q->dmrs_cfg               = *cfg;
+  q->dmrs_signal_configured = true;
+}
+
+int srsran_chest_ul_estimate_pusch(srsran_chest_ul_t*     q,
+                                   srsran_ul_sf_cfg_t*    sf,
+                                   srsran_pusch_cfg_t*    cfg,
+                                   cf_t*                  input,
+                                   srsran_chest_ul_res_t* res)
+{
+  if (!q || !q->gpu || !sf || !cfg || !input || !res || !res->gpu) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  if (!q->dmrs_signal_configured) {
+    fprintf(stderr, "[srsran_chest_ul] Error must call srsran_chest_ul_set_cfg() before using the UL estimator\n");
+    return SRSRAN_ERROR;
+  }
+  if (cfg->meas_ta_en && cfg->use_cedron_alg) {
+    fprintf(stderr, "[srsran_chest_ul] the Cedron TA estimator is not provided\n");
+    return SRSRAN_ERROR;
+  }
+  const uint32_t L = cfg->grant.L_prb;
+  if (check_alloc(q->cell, cfg) != SRSRAN_SUCCESS) {
+    fprintf(stderr, "[srsran_chest_ul] Error invalid nof_prb=%u\n", L);
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  ChestUlGpu*    g  = (ChestUlGpu*)q->gpu;
+  ChestUlResGpu* rg = (ChestUlResGpu*)res->gpu;
+  const uint32_t M = L * SRSRAN_NRE, ncell = q->cell.nof_prb * SRSRAN_NRE, nsf = 2 * nsymb_slot(q->cell.cp);
+  const size_t   sf_re = (size_t)ncell * nsf;
+  const size_t   off   = g->dmrs_off.empty() ? (size_t)-1 : g->dmrs_off[dmrs_index(cfg->grant.n_dmrs, sf->tti % 10, L)];
+  if (off == (size_t)-1 || sf_re > rg->nof_re) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  PuschUe u;
+  memset(&u, 0, sizeof(u));
+  fill_chest_desc(u, q, cfg, M);
+  u.grid = g->d_grid;
+  u.dmrs = g->d_dmrs + off;
+  u.ce   = rg->d_ce;
+  u.out  = rg->d_out;
+  // the estimator writes the whole-slot rows of the allocation; bring the device copy in line with
+  // the host's ce first when the host copy was changed (set_identity) so the rest matches on return
+  if (!rg->valid) {
+    if (hipMemcpyAsync(rg->d_ce, res->ce, sf_re * sizeof(float2), hipMemcpyHostToDevice, g->stream) != hipSuccess) {
+      return SRSRAN_ERROR;
+    }
+  }
+  if (!grow((void**)&g->d_grid, &g->grid_cap, sf_re * sizeof(float2)) ||
+      !grow((void**)&g->d_desc, &g->desc_cap, sizeof(PuschUe))) {
+    return SRSRAN_ERROR;
+  }
+  u.grid = g->d_grid;
+  ChestUlOut o;
+  if (hipMemcpyAsync(g->d_grid, input, sf_re * sizeof(float2), hipMemcpyHostToDevice, g->stream) != hipSuccess ||
+      hipMemcpyAsync(g->d_desc, &u, sizeof(u), hipMemcpyHostToDevice, g->stream) != hipSuccess ||
+      chest_ul_launch(g->d_desc, 1, g->stream) != hipSuccess ||
+      hipMemcpyAsync(&o, rg->d_out, sizeof(o), hipMemcpyDeviceToHost, g->stream) != hipSuccess) {
+    return SRSRAN_ERROR;
+  }
+  // the written rows back to the host estimate (other REs keep their contents, as in the reference)
+  for (uint32_t s = 0; s < 2; s++) {
+    const size_t o0 = (size_t)s * nsymb_slot(q->cell.cp) * ncell + cfg->grant.n_prb[s] * SRSRAN_NRE;
+    if (hipMemcpy2DAsync(res->ce + o0, ncell * sizeof(float2), rg->d_ce + o0, ncell * sizeof(float2),
+                         M * sizeof(float2), nsymb_slot(q->cell.cp), hipMemcpyDeviceToHost, g->stream) != hipSuccess) {
+      return SRSRAN_ERROR;
+    }
+  }
+  if (hipStreamSynchronize(g->stream) != hipSuccess) {
+    return SRSRAN_ERROR;
+  }
+  rg->valid = true;
+  finish_chest_res(res, o);
+  return SRSRAN_SUCCESS;
+}
+
+// ---------------- pusch.c:108-471 ----------------
+int srsran_pusch_init_enb(srsran_pusch_t* q, uint32_t max_prb)
+{
+  if (!q || max_prb > SRSRAN_MAX_PRB) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  memset(q, 0, sizeof(*q));
+  q->is_ue  = false;
+  q->max_re = max_prb * 2 * SRSRAN_CP_NORM_NSYMB * SRSRAN_NRE;  // MAX_PUSCH_RE(NORM) * max_prb
+  if (srsran_sch_init(&q->ul_sch)) {
+    return SRSRAN_ERROR;
+  }
+  q->gpu = new PuschGpu();
+  return SRSRAN_SUCCESS;
+}
+
+void srsran_pusch_free(srsran_pusch_t* q)
+{
+  if (!q) {
+    return;
+  }
+  PuschGpu* g = (PuschGpu*)q->gpu;
+  if (g) {
+    hipStream_t st = sch_stream(&q->ul_sch);
+    if (st) {
+      hipStreamSynchronize(st);
+    }
+    hipFree(g->d_grid);
+    hipFree(g->d_ce);
+    hipFree(g->d_sym);
+    hipFree(g->d_q);
+    hipFree(g->d_c);
+    hipFree(g->d_desc);
+    hipFree(g->d_llr);
+    hipFree(g->d_out);
+    hipFree(g->d_bce);
+    delete g;
+  }
+  srsran_sch_free(&q->ul_sch);
+  memset(q, 0, sizeof(*q));
+}
+
+int srsran_pusch_set_cell(srsran_pusch_t* q, srsran_cell_t cell)
+{
+  if (!q || !cell_valid(cell)) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  q->cell   = cell;
+  q->max_re = cell.nof_prb * 2 * nsymb_slot(cell.cp) * SRSRAN_NRE;
+  return SRSRAN_SUCCESS;
+}
+
+int srsran_pusch_assert_grant(const srsran_pusch_grant_t* grant)
+{
+  if (!srsran_dft_precoding_valid_prb(grant->L_prb)) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  if (grant->tb.rv < -1 || grant->tb.rv > 3) {
+    return SRSRAN_ERROR_OUT_OF_BOUNDS;
+  }
+  if (grant->tb.tbs < 0) {
+    return SRSRAN_ERROR_OUT_OF_BOUNDS;
+  }
+  return SRSRAN_SUCCESS;
+}
+
+int srsran_pusch_decode(srsran_pusch_t*        q,
+                        srsran_ul_sf_cfg_t*    sf,
+                        srsran_pusch_cfg_t*    cfg,
+                        srsran_chest_ul_res_t* channel,
+                        cf_t*                  sf_symbols,
+                        srsran_pusch_res_t*    out)
+{
+  if (!q || !q->gpu || !sf || !sf_symbols || !out || !cfg || !channel) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  if (q->llr_is_8bit) {
+    fprintf(stderr, "[srsran_pusch] the 8-bit LLR path is not provided\n");
+    return SRSRAN_ERROR;
+  }
+  limit_64qam(cfg);
+  const uint32_t L = cfg->grant.L_prb, M = L * SRSRAN_NRE;
+  if (check_alloc(q->cell, cfg) != SRSRAN_SUCCESS) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  PuschUe u;
+  memset(&u, 0, sizeof(u));
+  u.nof_symb = data_symbols(q->cell.cp, sf->shortened, u.data_sym);
+  if (u.nof_symb * M != cfg->grant.nof_re) {
+    fprintf(stderr, "[srsran_pusch] Error expecting %u symbols but got %u\n", cfg->grant.nof_re, u.nof_symb * M);
+    return SRSRAN_ERROR;
+  }
+  const uint32_t Qm = srsran_mod_bits_x_symbol(cfg->grant.tb.mod);
+  if (Qm == 0 || cfg->grant.tb.nof_bits != cfg->grant.nof_re * Qm || !dft_plan(M, u)) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  PuschGpu*      g     = (PuschGpu*)q->gpu;
+  hipStream_t    st    = sch_stream(&q->ul_sch);
+  const uint32_t ncell = q->cell.nof_prb * SRSRAN_NRE, nsf = 2 * nsymb_slot(q->cell.cp);
+  const size_t   sf_re = (size_t)ncell * nsf;
+  const uint32_t nb    = cfg->grant.tb.nof_bits;
+  if (!grow((void**)&g->d_grid, &g->grid_cap, sf_re * sizeof(float2)) ||
+      !grow((void**)&g->d_sym, &g->sym_cap, (size_t)cfg->grant.nof_re * sizeof(float2)) ||
+      !grow((void**)&g->d_q, &g->q_cap, (size_t)nb * sizeof(int16_t)) ||
+      !grow((void**)&g->d_c, &g->c_cap, (size_t)nb) || !grow((void**)&g->d_desc, &g->desc_cap, sizeof(PuschUe)) ||
+      !grow((void**)&g->d_out, &g->out_cap, sizeof(ChestUlOut))) {
+    return SRSRAN_ERROR;
+  }
+  // the estimate: the estimator's device copy when it is current, else the host's ce
+  ChestUlResGpu* rg = (ChestUlResGpu*)channel->gpu;
+  const float2*  d_ce;
+  if (rg && rg->valid && rg->nof_re >= sf_re) {
+    d_ce = rg->d_ce;
+  } else {
+    if (!channel->ce || !grow((void**)&g->d_ce, &g->ce_cap, sf_re * sizeof(float2)) ||
+        hipMemcpyAsync(g->d_ce, channel->ce, sf_re * sizeof(float2), hipMemcpyHostToDevice, st) != hipSuccess) {
+      return SRSRAN_ERROR;
+    }
+    d_ce = g->d_ce;
+  }
+  u.grid       = g->d_grid;
+  u.ce         = (float2*)d_ce;
+  u.sym        = g->d_sym;
+  u.out        = g->d_out;
+  u.ncell_re   = ncell;
+  u.M          = M;
+  u.nsym_slot  = nsymb_slot(q->cell.cp);
+  u.n_tilde[0] = cfg->grant.n_prb_tilde[0];
+  u.n_tilde[1] = cfg->grant.n_prb_tilde[1];
+  u.noise      = channel->noise_estimate;
+  u.dft_norm = 1.0f / sqrtf((float)M);
+  LlrItem it;
+  memset(&it, 0, sizeof(it));
+  it.sym         = (const float*)g->d_sym;
+  it.llr         = g->d_q;
+  it.n           = cfg->grant.nof_re;
+  it.seed        = pusch_seed(cfg->rnti, 2 * (sf->tti % SRSRAN_NOF_SF_X_FRAME), q->cell.id);
+  it.scramble    = 1;
+  const bool uci = any_uci(cfg);
+  if (!grow((void**)&g->d_llr, &g->llr_cap, sizeof(LlrItem)) ||
+      hipMemcpyAsync(g->d_grid, sf_symbols, sf_re * sizeof(float2), hipMemcpyHostToDevice, st) != hipSuccess ||
+      hipMemcpyAsync(g->d_desc, &u, sizeof(u), hipMemcpyHostToDevice, st) != hipSuccess ||
+      hipMemcpyAsync(g->d_llr, &it, sizeof(it), hipMemcpyHostToDevice, st) != hipSuccess ||
+      hipMemsetAsync(g->d_out, 0, sizeof(ChestUlOut), st) != hipSuccess ||
+      pusch_eq_idft_launch(g->d_desc, 1, st) != hipSuccess ||
+      llr_batch_launch((int)cfg->grant.tb.mod, g->d_llr, 1, it.n, 1, st) != hipSuccess ||
+      (uci && seq_unpack_launch(g->d_c, nb, it.seed, st) != hipSuccess)) {
+    return SRSRAN_ERROR;
+  }
+  srsran_sch_set_max_noi(&q->ul_sch, cfg->max_nof_iterations);
+  const int ret = ulsch_decode_dev(&q->ul_sch, cfg, g->d_q, uci ? g->d_c : nullptr, out->data, &out->uci);
+  ChestUlOut o;
+  if (hipMemcpyAsync(&o, g->d_out, sizeof(o), hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess) {
+    return SRSRAN_ERROR;
+  }
+  out->epre_dbfs            = cfg->meas_epre_en ? 10.0f * log10f(o.data_pow / (float)cfg->grant.nof_re) : NAN;
+  out->evm                  = NAN;
+  out->crc                  = ret == 0;
+  out->avg_iterations_block = q->ul_sch.avg_iterations;
+  cfg->last_O_cqi           = (uint32_t)srsran_cqi_size(&cfg->uci_cfg.cqi);
+  return SRSRAN_SUCCESS;
+}
+
+int srsran_pusch_gpu_decode_batch(srsran_pusch_t*              q,
+                                  uint32_t                     nof_ue,
+                                  const srsran_pusch_gpu_ue_t* ues,
+                                  srsran_chest_ul_res_t*       chest_res,
+                                  srsran_pusch_res_t*          res)
+{
+  if (!q || !q->gpu || (nof_ue && (!ues || !res))) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  if (nof_ue == 0) {
+    return SRSRAN_SUCCESS;
+  }
+  if (q->llr_is_8bit) {
+    return SRSRAN_ERROR;
+  }
+  PuschGpu*   g  = (PuschGpu*)q->gpu;
+  hipStream_t st = sch_stream(&q->ul_sch);
+
+  // ---- host: descriptors and the device layout of every UE's buffers ----
+  std::vector<PuschUe> desc(nof_ue);
+  std::vector<size_t>  ce_off(nof_ue), sym_off(nof_ue), q_off(nof_ue), c_off(nof_ue);
+  size_t               ce_tot = 0, sym_tot = 0, q_tot = 0, c_tot = 0;
+  for (uint32_t i = 0; i < nof_ue; i++) {
+    const srsran_pusch_gpu_ue_t& e = ues[i];
+    if (!e.chest || !e.chest->gpu || !e.sf || !e.cfg || !e.d_sf_symbols || !e.chest->dmrs_signal_configured) {
+      return SRSRAN_ERROR_INVALID_INPUTS;
+    }
+    srsran_pusch_cfg_t* cfg = e.cfg;
+    const srsran_cell_t& cell = e.chest->cell;
+    ChestUlGpu*          cg   = (ChestUlGpu*)e.chest->gpu;
+    limit_64qam(cfg);
+    if (check_alloc(cell, cfg) != SRSRAN_SUCCESS || (cfg->meas_ta_en && cfg->use_cedron_alg)) {
+      return SRSRAN_ERROR_INVALID_INPUTS;
+    }
+    const uint32_t L = cfg->grant.L_prb, M = L * SRSRAN_NRE;
+    PuschUe&       u = desc[i];
+    memset(&u, 0, sizeof(u));
+    fill_chest_desc(u, e.chest, cfg, M);
+    u.nof_symb = data_symbols(cell.cp, e.sf->shortened, u.data_sym);
+    const uint32_t Qm = srsran_mod_bits_x_symbol(cfg->grant.tb.mod);
+    const size_t   off = cg->dmrs_off.empty() ? (size_t)-1 : cg->dmrs_off[dmrs_index(cfg->grant.n_dmrs, e.sf->tti % 10, L)];
+    if (u.nof_symb * M != cfg->grant.nof_re || Qm == 0 || cfg->grant.tb.nof_bits != cfg->grant.nof_re * Qm ||
+        !dft_plan(M, u) || off == (size_t)-1) {
+      return SRSRAN_ERROR_INVALID_INPUTS;
+    }
+    u.grid     = (const float2*)e.d_sf_symbols;
+    u.dmrs     = cg->d_dmrs + off;
+    ce_off[i]  = ce_tot;
+    ce_tot += (size_t)u.ncell_re * 2 * u.nsym_slot;
+    sym_off[i] = sym_tot;
+    sym_tot += cfg->grant.nof_re;
+    q_off[i] = q_tot;
+    q_tot += (cfg->grant.tb.nof_bits + 7) & ~7u;
+    c_off[i] = c_tot;
+    c_tot += any_uci(cfg) ? ((cfg->grant.tb.nof_bits + 15) & ~15u) : 0;
+  }
+  if (!grow((void**)&g->d_desc, &g->desc_cap, nof_ue * sizeof(PuschUe)) ||
+      !grow((void**)&g->d_out, &g->out_cap, nof_ue * sizeof(ChestUlOut)) ||
+      !grow((void**)&g->d_bce, &g->bce_cap, ce_tot * sizeof(float2)) ||
+      !grow((void**)&g->d_sym, &g->sym_cap, sym_tot * sizeof(float2)) ||
+      !grow((void**)&g->d_q, &g->q_cap, q_tot * sizeof(int16_t)) || !grow((void**)&g->d_c, &g->c_cap, c_tot + 16) ||
+      !grow((void**)&g->d_llr, &g->llr_cap, nof_ue * sizeof(LlrItem))) {
+    return SRSRAN_ERROR;
+  }
+  std::vector<LlrItem> items(nof_ue);
+  for (uint32_t i = 0; i < nof_ue; i++) {
+    desc[i].ce  = g->d_bce + ce_off[i];
+    desc[i].sym = g->d_sym + sym_off[i];
+    desc[i].out = g->d_out + i;
+    LlrItem& it = items[i];
+    memset(&it, 0, sizeof(it));
+    it.sym      = (const float*)desc[i].sym;
+    it.llr      = g->d_q + q_off[i];
+    it.n        = ues[i].cfg->grant.nof_re;
+    it.seed     = pusch_seed(ues[i].cfg->rnti, 2 * (ues[i].sf->tti % SRSRAN_NOF_SF_X_FRAME), ues[i].chest->cell.id);
+    it.scramble = 1;
+  }
+  // the LLR launch takes one modulation: order the items by it
+  std::vector<uint32_t> order(nof_ue);
+  for (uint32_t i = 0; i < nof_ue; i++) {
+    order[i] = i;
+  }
+  std::stable_sort(order.begin(), order.end(),
+                   [&](uint32_t a, uint32_t b) { return ues[a].cfg->grant.tb.mod < ues[b].cfg->grant.tb.mod; });
+  std::vector<LlrItem> sorted(nof_ue);
+  for (uint32_t k = 0; k < nof_ue; k++) {
+    sorted[k] = items[order[k]];
+  }
+  if (hipMemcpyAsync(g->d_desc, desc.data(), nof_ue * sizeof(PuschUe), hipMemcpyHostToDevice, st) != hipSuccess ||
+      hipMemcpyAsync(g->d_llr, sorted.data(), nof_ue * sizeof(LlrItem), hipMemcpyHostToDevice, st) != hipSuccess ||
+      chest_ul_launch(g->d_desc, nof_ue, st) != hipSuccess || pusch_eq_idft_launch(g->d_desc, nof_ue, st) != hipSuccess) {
+    return SRSRAN_ERROR;
+  }
+  for (uint32_t k = 0; k < nof_ue;) {
+    const int mod = (int)ues[order[k]].cfg->grant.tb.mod;
+    uint32_t  k1 = k, max_n = 0;
+    while (k1 < nof_ue && (int)ues[order[k1]].cfg->grant.tb.mod == mod) {
+      max_n = std::max(max_n, sorted[k1].n);
+      k1++;
+    }
+    if (llr_batch_launch(mod, g->d_llr + k, k1 - k, max_n, 1, st) != hipSuccess) {
+      return SRSRAN_ERROR;
+    }
+    k = k1;
+  }
+  for (uint32_t i = 0; i < nof_ue; i++) {
+    if (any_uci(ues[i].cfg) &&
+        seq_unpack_launch(g->d_c + c_off[i], ues[i].cfg->grant.tb.nof_bits, items[i].seed, st) != hipSuccess) {
+      return SRSRAN_ERROR;
+    }
+  }
+
+  // ---- UL-SCH: each UE's UCI / de-interleaver / decode_tb on the same stream ----
+  int rc = SRSRAN_SUCCESS;
+  for (uint32_t i = 0; i < nof_ue; i++) {
+    srsran_pusch_cfg_t* cfg = ues[i].cfg;
+    srsran_sch_set_max_noi(&q->ul_sch, cfg->max_nof_iterations);
+    const int ret = ulsch_decode_dev(&q->ul_sch, cfg, g->d_q + q_off[i], any_uci(cfg) ? g->d_c + c_off[i] : nullptr,
+                                     res[i].data, &res[i].uci);
+    res[i].crc                  = ret == 0;
+    res[i].avg_iterations_block = q->ul_sch.avg_iterations;
+    res[i].evm                  = NAN;
+    cfg->last_O_cqi             = (uint32_t)srsran_cqi_size(&cfg->uci_cfg.cqi);
+    if (ret < 0 && ret != SRSRAN_ERROR) {
+      rc = ret;
+    }
+  }
+  std::vector<ChestUlOut> outs(nof_ue);
+  if (hipMemcpyAsync(outs.data(), g->d_out, nof_ue * sizeof(ChestUlOut), hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess) {
+    return SRSRAN_ERROR;
+  }
+  for (uint32_t i = 0; i < nof_ue; i++) {
+    res[i].epre_dbfs = ues[i].cfg->meas_epre_en ? 10.0f * log10f(outs[i].data_pow / (float)ues[i].cfg->grant.nof_re)
+                                                : NAN;
+    if (chest_res) {
+      finish_chest_res(&chest_res[i], outs[i]);
+      if (chest_res[i].ce) {  // the estimate rows, as srsran_chest_ul_estimate_pusch writes them
+        const PuschUe& u = desc[i];
+        for (uint32_t s = 0; s < 2; s++) {
+          const size_t o0 = (size_t)s * u.nsym_slot * u.ncell_re + u.n_prb[s] * SRSRAN_NRE;
+          if (hipMemcpy2D(chest_res[i].ce + o0, u.ncell_re * sizeof(float2), desc[i].ce + o0, u.ncell_re * sizeof(float2),
+                          u.M * sizeof(float2), u.nsym_slot, hipMemcpyDeviceToHost) != hipSuccess) {
+            return SRSRAN_ERROR;
+          }
+        }
+        ChestUlResGpu* rg = (ChestUlResGpu*)chest_res[i].gpu;
+        if (rg) {
+          rg->valid = false;  // the host copy is now the current one
+        }
+      }
+    }
+  }
+  return rc;
+}
+
+}  // extern "C"

@@ -1271,15 +1271,21 @@ struct UlsUciScratch {
   UciOut  out;
 };
 
-int srsran_ulsch_decode(srsran_sch_t*       q,
-                        srsran_pusch_cfg_t* cfg,
-                        int16_t*            q_bits,
-                        int16_t*            g_bits,
-                        uint8_t*            c_seq,
-                        uint8_t*            data,
-                        srsran_uci_value_t* uci_data)
+// srsran_ulsch_decode's body.  The LLRs come from the host (h_q) or are already on the device
+// (d_q_ext, zeroed in place at the ACK positions); the scrambling sequence likewise (h_c / d_c_ext).
+// q_out / g_bits (host, optional) receive q after the ACK zeroing and the de-interleaved LLRs.
+static int ulsch_decode_impl(srsran_sch_t*       q,
+                             srsran_pusch_cfg_t* cfg,
+                             const int16_t*      h_q,
+                             int16_t*            d_q_ext,
+                             int16_t*            q_out,
+                             int16_t*            g_bits,
+                             const uint8_t*      h_c,
+                             const uint8_t*      d_c_ext,
+                             uint8_t*            data,
+                             srsran_uci_value_t* uci_data)
 {
-  if (!q || !q->gpu || !cfg || !q_bits || !g_bits) {
+  if (!q || !q->gpu || !cfg || (!h_q && !d_q_ext)) {
     return SRSRAN_ERROR_INVALID_INPUTS;
   }
   srsran_cbsegm_t s;
@@ -1340,7 +1346,7 @@ int srsran_ulsch_decode(srsran_sch_t*       q,
     return SRSRAN_ERROR;
   }
   const bool need_c = (nack == 1 && ack_Qp > 0) || (cq.ri_len == 1 && ri_Qp > 0);
-  if (need_c && !c_seq) {
+  if (need_c && !h_c && !d_c_ext) {
     return SRSRAN_ERROR_INVALID_INPUTS;
   }
 
@@ -1354,16 +1360,17 @@ int srsran_ulsch_decode(srsran_sch_t*       q,
     }
     x->ul_cap = 2 * (size_t)nb;
   }
-  int16_t* d_q = x->d_ul;
+  int16_t* d_q = d_q_ext ? d_q_ext : x->d_ul;
   int16_t* d_g = x->d_ul + nb;
   // the reference leaves the de-interleaved LLRs in g_bits (positions it does not write untouched)
-  if (hipMemcpyAsync(d_g, g_bits, (size_t)nb * 2, hipMemcpyHostToDevice, x->stream) != hipSuccess ||
-      hipMemcpyAsync(d_q, q_bits, (size_t)nb * 2, hipMemcpyHostToDevice, x->stream) != hipSuccess) {
+  if ((g_bits && hipMemcpyAsync(d_g, g_bits, (size_t)nb * 2, hipMemcpyHostToDevice, x->stream) != hipSuccess) ||
+      (h_q && hipMemcpyAsync(d_q, h_q, (size_t)nb * 2, hipMemcpyHostToDevice, x->stream) != hipSuccess)) {
     return SRSRAN_ERROR;
   }
   if (!uci) {
     if (ul_deint_launch(d_q, d_g, Qm, H, nsymb, x->stream) != hipSuccess ||
-        hipMemcpyAsync(g_bits, d_g, (size_t)nb * 2, hipMemcpyDeviceToHost, x->stream) != hipSuccess ||
+        (g_bits && hipMemcpyAsync(g_bits, d_g, (size_t)nb * 2, hipMemcpyDeviceToHost, x->stream) != hipSuccess) ||
+        (q_out && hipMemcpyAsync(q_out, d_q, (size_t)nb * 2, hipMemcpyDeviceToHost, x->stream) != hipSuccess) ||
         hipStreamSynchronize(x->stream) != hipSuccess) {
       return SRSRAN_ERROR;
     }
@@ -1380,12 +1387,13 @@ int srsran_ulsch_decode(srsran_sch_t*       q,
   }
 
   // ---- device scratch: descriptors, results, sequence ----
-  const size_t scr = align16(sizeof(UlsUciScratch)) + (need_c ? (size_t)nb : 0);
+  const bool   up_c = need_c && !d_c_ext;
+  const size_t scr  = align16(sizeof(UlsUciScratch)) + (up_c ? (size_t)nb : 0);
   if (!grow_dev((void**)&x->d_uci, &x->uci_cap, scr)) {
     return SRSRAN_ERROR;
   }
   UlsUciScratch* d_s = (UlsUciScratch*)x->d_uci;
-  uint8_t*       d_c = x->d_uci + align16(sizeof(UlsUciScratch));
+  const uint8_t* d_c = up_c ? x->d_uci + align16(sizeof(UlsUciScratch)) : d_c_ext;
   UlsUciScratch  h;
   memset(&h, 0, sizeof(h));
   h.uci = {d_q, need_c ? d_c : nullptr, d_g, &d_s->out, Qm, rows, nsymb, nack, ack_Qp, cq.ri_len, ri_Qp, 0, 0};
@@ -1409,7 +1417,7 @@ int srsran_ulsch_decode(srsran_sch_t*       q,
     h.deint.g0_src = (int32_t)std::max<int64_t>(last, (int64_t)first * rows * Qm);
   }
   if (hipMemcpyAsync(d_s, &h, sizeof(h), hipMemcpyHostToDevice, x->stream) != hipSuccess ||
-      (need_c && hipMemcpyAsync(d_c, c_seq, nb, hipMemcpyHostToDevice, x->stream) != hipSuccess) ||
+      (up_c && hipMemcpyAsync((void*)d_c, h_c, nb, hipMemcpyHostToDevice, x->stream) != hipSuccess) ||
       uci_ack_ri_launch(&d_s->uci, 1, x->stream) != hipSuccess ||
       ul_deint_batch_launch(&d_s->deint, 1, rows, x->stream) != hipSuccess) {
     return SRSRAN_ERROR;
@@ -1457,8 +1465,8 @@ int srsran_ulsch_decode(srsran_sch_t*       q,
     ret                      = dlsch_decode_sync(q, &pc, nullptr, d_g + (size_t)cqi_Qp * Qm, data, 0, 1);
   }
   if (hipMemcpyAsync(&h.out, &d_s->out, sizeof(UciOut), hipMemcpyDeviceToHost, x->stream) != hipSuccess ||
-      hipMemcpyAsync(q_bits, d_q, (size_t)nb * 2, hipMemcpyDeviceToHost, x->stream) != hipSuccess ||
-      hipMemcpyAsync(g_bits, d_g, (size_t)nb * 2, hipMemcpyDeviceToHost, x->stream) != hipSuccess ||
+      (q_out && hipMemcpyAsync(q_out, d_q, (size_t)nb * 2, hipMemcpyDeviceToHost, x->stream) != hipSuccess) ||
+      (g_bits && hipMemcpyAsync(g_bits, d_g, (size_t)nb * 2, hipMemcpyDeviceToHost, x->stream) != hipSuccess) ||
       hipStreamSynchronize(x->stream) != hipSuccess) {
     return SRSRAN_ERROR;
   }
@@ -1478,6 +1486,34 @@ int srsran_ulsch_decode(srsran_sch_t*       q,
   }
   return ret;
 }
+
+int srsran_ulsch_decode(srsran_sch_t*       q,
+                        srsran_pusch_cfg_t* cfg,
+                        int16_t*            q_bits,
+                        int16_t*            g_bits,
+                        uint8_t*            c_seq,
+                        uint8_t*            data,
+                        srsran_uci_value_t* uci_data)
+{
+  if (!q_bits || !g_bits) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  return ulsch_decode_impl(q, cfg, q_bits, nullptr, q_bits, g_bits, c_seq, nullptr, data, uci_data);
+}
+
+}  // extern "C"
+
+namespace srsran_amd {
+hipStream_t sch_stream(srsran_sch_t* q) { return q && q->gpu ? ((SchCtx*)q->gpu)->stream : nullptr; }
+
+int ulsch_decode_dev(srsran_sch_t* q, srsran_pusch_cfg_t* cfg, int16_t* d_q, const uint8_t* d_c, uint8_t* data,
+                     srsran_uci_value_t* uci_data)
+{
+  return ulsch_decode_impl(q, cfg, nullptr, d_q, nullptr, nullptr, nullptr, d_c, data, uci_data);
+}
+}  // namespace srsran_amd
+
+extern "C" {
 
 int srsran_ulsch_gpu_decode_batch(srsran_sch_t*                q,
                                   uint32_t                     nof_tb,

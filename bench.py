@@ -8,6 +8,8 @@ A "step" is one pass of the hot path over one batch of synthetic input:
   workload "dlsch": srsran_dlsch_decode of C3 transport blocks (rate dematch + turbo + CRC);
   workload "ulsch": the same TBs as PUSCH data through srsran_ulsch_gpu_decode_batch (channel
       de-interleaver + decode_tb; SURVEY 8f rank 1, data part);
+  workload "pusch": the eNB PUSCH chain from the received subframe grid -- DMRS channel estimation,
+      equalisation + SC-FDMA inverse DFT, demap/descramble, UL-SCH decode (SURVEY 8f rank 1);
   workload "pdsch" (BASELINE configs[2], C3): the whole UE DL chain from time-domain samples --
       OFDM, CRS channel estimation, MMSE predecoding, demap/descramble/CSI, DL-SCH decode;
   workload "ldpc" (BASELINE configs[4]): NR LDPC decode (srsran_ldpc_decoder, 8-bit layered
@@ -105,7 +107,8 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--workload", choices=["all188", "k6144", "dlsch", "ulsch", "pdsch", "ldpc", "nrsch"], default="all188")
+    p.add_argument("--workload", choices=["all188", "k6144", "dlsch", "ulsch", "pusch", "pdsch", "ldpc", "nrsch"],
+                   default="all188")
     p.add_argument("--snr", type=float, default=30.0, help="pdsch: AWGN SNR (dB) of the synthetic subframes")
     p.add_argument("--subframes", type=int, default=78,
                    help="dlsch / pdsch: subframes (2 TBs each) per step; 78 x 26 CBs = two full turbo-decoder rounds")
@@ -411,6 +414,191 @@ def stage_bytes(nsf, nre_sum, ntb):
         "tdec_kernel": ntb * C * ((3 * (K + 32) + 12) * 2 + K // 8),
         "tb_assemble_kernel": ntb * (C * K // 8 + C3_TBS // 8),
     }
+
+
+def pusch_stage_bytes(nue, M, nsymb, ncell_re):
+    """Algorithmic HBM bytes per launch of the PUSCH kernels for nue UEs of M subcarriers: the chest
+    reads 2M pilots + 2M DMRS values and writes the 2 x 7-symbol estimate rows; the equaliser reads
+    the data REs and their estimates and writes the de-precoded symbols (all complex float)."""
+    K, C = 5824, 13
+    return {
+        "chest_ul_kernel": nue * (4 * M * 8 + 14 * M * 8),
+        "pusch_eq_idft_kernel": nue * 3 * nsymb * M * 8,
+        "llr_batch_kernel": nue * nsymb * M * (8 + 6 * 2),
+        "rm_rx_lds_kernel": nue * (C3_BITS * 2 + C * (3 * (K + 32) + 12) * 2),
+        "tdec_kernel": nue * C * ((3 * (K + 32) + 12) * 2 + K // 8),
+        "tb_assemble_kernel": nue * (C * K // 8 + C3_TBS // 8),
+    }
+
+
+def run_pusch(args, torch, dist, world, rank, device):
+    """eNB PUSCH receive: per step `subframes` UEs, each a 100-PRB 64QAM PUSCH (TBS 75376, 12
+    SC-FDMA symbols, normal CP) in its own received subframe grid (device-resident), through
+    srsran_pusch_gpu_decode_batch: DMRS estimation, MMSE equalisation + 1200-point inverse DFT,
+    demap/descramble, channel de-interleaver, rate de-matching, turbo decoding with CRC early stop.
+    Value = decoded UL info Mbps; also UE-subframes/s."""
+    import ctypes
+
+    from synth import pusch_tx as PT
+    from srsran_4g_amd import prof
+    from srsran_4g_amd import pusch as P
+    from srsran_4g_amd import sch as S
+    from srsran_4g_amd.ue_dl import cell as make_cell
+
+    rng = np.random.default_rng(shard(rank)["seed"])
+    cell_id = shard(rank)["cell_id"]
+    cell = make_cell(100, 1, cell_id)
+    dm = P.srsran_refsignal_dmrs_pusch_cfg_t()
+    dm.cyclic_shift, dm.delta_ss, dm.group_hopping_en = 1, 3, True
+    rnti, L = 0x46, 100
+    pool = []
+    for i in range(args.pool):
+        tti = i % 10
+        g, pl = PT.subframe(cell, dm, 100, L, 0, C3_TBS, C3_QM, tti, rnti, rng, snr_db=args.snr)
+        pool.append((tti, g, pl))
+    nue = args.subframes
+    host = np.stack([pool[b % args.pool][1] for b in range(nue)])
+    d_grid = torch.from_numpy(np.ascontiguousarray(host).view(np.float32)).to(device)
+    ch = P.ChestUl(cell, dm)
+    pu = P.Pusch(cell)
+    sbs = [S.SoftbufferRx(nof_prb=100) for _ in range(nue)]
+    cfgs, sfs = [], []
+    for b in range(nue):
+        cfg = S.srsran_pusch_cfg_t()
+        cfg.rnti = rnti
+        g = cfg.grant
+        g.L_prb, g.nof_symb, g.nof_re = L, UL_NSYMB, L * 12 * UL_NSYMB
+        g.tb.mod, g.tb.tbs, g.tb.rv, g.tb.nof_bits, g.tb.enabled = S.MOD_FROM_QM[C3_QM], C3_TBS, 0, C3_BITS, True
+        cfg.enable_64qam = True
+        cfg.max_nof_iterations = args.iters
+        cfg.softbuffers.rx = ctypes.pointer(sbs[b].s)
+        sf = P.srsran_ul_sf_cfg_t()
+        sf.tti = pool[b % args.pool][0]
+        cfgs.append(cfg)
+        sfs.append(sf)
+    arr = (P.srsran_pusch_gpu_ue_t * nue)()
+    res = (P.srsran_pusch_res_t * nue)()
+    cres = (P.srsran_chest_ul_res_t * nue)()
+    datas = np.zeros((nue, C3_TBS // 8 + 64), np.uint8)
+    per_grid = host[0].size * 8
+    for b in range(nue):
+        arr[b].chest = ctypes.pointer(ch.q)
+        arr[b].sf = ctypes.pointer(sfs[b])
+        arr[b].cfg = ctypes.pointer(cfgs[b])
+        arr[b].d_sf_symbols = d_grid.data_ptr() + b * per_grid
+        res[b].data = datas[b].ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+    L_ = P.lib()
+
+    def step():
+        for sb in sbs:  # new transmissions (as srsran_softbuffer_rx_reset before each new TB)
+            S.lib().srsran_softbuffer_rx_reset_tbs(ctypes.byref(sb.s), C3_TBS)
+        if L_.srsran_pusch_gpu_decode_batch(ctypes.byref(pu.q), nue, arr, cres, res) != 0:
+            raise RuntimeError("srsran_pusch_gpu_decode_batch failed")
+
+    elapsed = timed_region(step, args.steps, args.warmup, world, dist, torch.cuda.synchronize, device)
+    ok = np.array([bool(res[b].crc) and np.array_equal(datas[b][:C3_TBS // 8], pool[b % args.pool][2])
+                   for b in range(nue)])
+    avg = np.array([res[b].avg_iterations_block for b in range(nue)])
+    value = world * nue * C3_TBS * args.steps / elapsed / 1e6
+
+    prof.enable(True)
+    nrep = max(1, min(args.steps, 3))
+    for _ in range(nrep):
+        step()
+    torch.cuda.synchronize()
+    stages = prof.read()
+    prof.enable(False)
+    sb_ = pusch_stage_bytes(nue, 12 * L, UL_NSYMB, 1200)
+    per_stage = {}
+    for name, (ms, n) in stages.items():
+        lps = n / nrep
+        per_stage[name] = {"ms_per_step": round(ms / nrep, 4), "launches_per_step": lps,
+                           "avg_launch_ms": round(ms / n, 4),
+                           "GBps": round(sb_.get(name, 0) / lps / (ms / n * 1e-3) / 1e9, 1)}
+    dom = max(per_stage, key=lambda k: per_stage[k]["ms_per_step"])
+    d = per_stage[dom]
+    bytes_per_launch = sb_.get(dom, 0) / d["launches_per_step"]
+    achieved = bytes_per_launch / (d["avg_launch_ms"] * 1e-3) / 1e9
+    fe = [k for k in ("chest_ul_kernel", "pusch_eq_idft_kernel") if k in per_stage]
+    result = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "Mbps",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32 front end, int16 LLRs",
+        "data": f"synthetic: {args.pool} distinct PUSCH subframes (3-tap frequency-selective channel, AWGN "
+                f"{args.snr} dB) tiled to the batch, HBM-resident grids",
+        "config": {
+            "workload": f"pusch: {nue} UEs x (100 PRB, 64QAM, TBS {C3_TBS}, 12 SC-FDMA symbols, normal CP) per step, "
+                        f"srsran_pusch_gpu_decode_batch, max {args.iters} half-its, CRC early stop, no UCI",
+            "ue_subframes_per_s": round(world * nue * args.steps / elapsed, 1),
+            "tb_ok_fraction": round(float(ok.mean()), 4),
+            "avg_half_iterations": round(float(avg.mean()), 3),
+            "parallelism": f"ue-sharded x{world}",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": dom,
+            "achieved": round(achieved, 2),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5),
+            "traffic": None,
+            "avg_launch_ms": d["avg_launch_ms"],
+            "algo_bytes_per_launch": int(bytes_per_launch),
+        },
+        "front_end_roofline": {k: {"GBps": per_stage[k]["GBps"], "frac": round(per_stage[k]["GBps"] / HBM_PEAK_GBS, 4),
+                                   "avg_launch_ms": per_stage[k]["avg_launch_ms"]} for k in fe},
+        "stages": per_stage,
+    }
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        result["cpu_baseline"] = pusch_cpu_baseline(pool, cell_id, dm, rnti, args)
+    elif rank == 0:
+        result["cpu_baseline"] = None
+    for sb in sbs:
+        sb.free()
+    pu.free()
+    ch.free()
+    if world > 1:
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+
+
+def pusch_cpu_baseline(pool, cell_id, dm, rnti, args):
+    """The PUSCH chain on one host thread: the oracle's numpy estimator / equaliser / inverse FFT (FFTW
+    and chest_ul.c are not buildable here) + the reference's compiled demapper, descrambler and
+    decode_tb, over the same pool, for about args.cpu_seconds."""
+    import pusch as OP  # oracle/pusch.py
+
+    from srsran_4g_amd import pusch as P
+    from srsran_4g_amd.ue_dl import cell as make_cell
+    from oracle import Reference
+    po = OP.PuschOracle()
+    ref = Reference()
+    cell = make_cell(100, 1, cell_id)
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < args.cpu_seconds:
+        tti, grid, _ = pool[n % len(pool)]
+        _, r = P.dmrs(cell, dm, 100, tti % 10, 0)
+        est = po.chest(grid, 100, 0, 100, (0, 0), (0, 0), r)
+        dsym = po.symbols(grid, est["ce"], est["noise"], 0, False, 100, (0, 0))
+        q = po.llrs(dsym, 3, rnti, tti, cell_id)
+        g = po.ora.ulsch_deinterleave(q, C3_QM, UL_NSYMB)
+        ref.dlsch_decode(C3_TBS, C3_QM, 0, g, args.iters)
+        n += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(n * C3_TBS / dt / 1e6, 3), "unit": "Mbps", "cores": 1, "kind": "reference",
+            "ue_subframes_per_s": round(n / dt, 2),
+            "sample": f"{n} PUSCH subframes, {dt:.1f} s on 1 thread: reference-compiled demapper / descrambler / "
+                      f"decode_tb, oracle numpy estimator + equaliser + FFT (FFTW and chest_ul.c absent), "
+                      f"oracle UL de-interleaver"}
 
 
 def run_pdsch(args, torch, dist, world, rank, device, steps=None, warmup=None, cpu_seconds=None, emit=True):
@@ -879,6 +1067,8 @@ def main():
         raise RuntimeError("bench: HIP device not visible to libsrsran_4g_amd")
     if args.workload in ("dlsch", "ulsch"):
         return run_dlsch(args, torch, dist, world, rank, device)
+    if args.workload == "pusch":
+        return run_pusch(args, torch, dist, world, rank, device)
     if args.workload == "pdsch":
         return run_pdsch(args, torch, dist, world, rank, device)
     if args.workload == "ldpc":

@@ -2,7 +2,8 @@
  * include/srsran_amd_prof.h -- added diagnostics: HIP-event timing of the GPU pipeline's kernel
  * launches per stage (no counterpart in the reference).  Stages: 0 OFDM, 1 channel estimation,
  * 2 predecoding, 3 demap/descramble/CSI, 4 rate dematching, 5 turbo decoding, 6 TB CRC / output,
- * 7 NR LDPC rate de-matching, 8 LDPC decoding, 9 NR TB assembly / CRC.
+ * 7 NR LDPC rate de-matching, 8 LDPC decoding, 9 NR TB assembly / CRC, 10 UL channel estimation,
+ * 11 PUSCH equalisation + transform de-precoding.
  */
 #ifndef SRSRAN_AMD_PROF_H
 #define SRSRAN_AMD_PROF_H
@@ -12,7 +13,7 @@
 extern "C" {
 #endif
 
-#define SRSRAN_AMD_NOF_STAGES 10
+#define SRSRAN_AMD_NOF_STAGES 12
 
 /* start (non-zero) or stop recording; clears the accumulators */
 void srsran_amd_timing_enable(int enable);

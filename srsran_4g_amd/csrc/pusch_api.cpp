@@ -290,6 +290,12 @@ struct PuschGpu {
   size_t      out_cap = 0;
   float2*     d_bce  = nullptr;  // batch: per-UE estimate grids
   size_t      bce_cap = 0;
+  int16_t*    d_g    = nullptr;  // batch: de-interleaved LLRs of the UEs without UCI
+  size_t      g_cap  = 0;
+  uint8_t*    d_data = nullptr;  // batch: decoded TBs of the UEs without UCI
+  size_t      data_cap = 0;
+  int32_t*    d_res  = nullptr;  // batch: decode_tb results / average iterations
+  size_t      res_cap = 0;
 };
 
 uint32_t pusch_seed(uint16_t rnti, uint32_t nslot, uint32_t cell_id)  // sequences.c:119-122
@@ -642,6 +648,9 @@ void srsran_pusch_free(srsran_pusch_t* q)
     hipFree(g->d_llr);
     hipFree(g->d_out);
     hipFree(g->d_bce);
+    hipFree(g->d_g);
+    hipFree(g->d_data);
+    hipFree(g->d_res);
     delete g;
   }
   srsran_sch_free(&q->ul_sch);
@@ -882,10 +891,88 @@ int srsran_pusch_gpu_decode_batch(srsran_pusch_t*              q,
     }
   }
 
-  // ---- UL-SCH: each UE's UCI / de-interleaver / decode_tb on the same stream ----
-  int rc = SRSRAN_SUCCESS;
+  // ---- UL-SCH.  UEs without UCI: one batched de-interleaver + decode_tb (srsran_ulsch_gpu_decode_batch);
+  // with UCI: srsran_ulsch_decode's sequence each (its CQI size may depend on the decoded RI) ----
+  int                                rc = SRSRAN_SUCCESS;
+  std::vector<uint32_t>              plain;
+  std::vector<srsran_ulsch_gpu_tb_t> tb;
+  size_t                             g_tot = 0, data_tot = 0;
+  std::vector<size_t>                g_off(nof_ue), data_off(nof_ue);
   for (uint32_t i = 0; i < nof_ue; i++) {
     srsran_pusch_cfg_t* cfg = ues[i].cfg;
+    if (any_uci(cfg) || cfg->grant.tb.tbs <= 0) {
+      continue;
+    }
+    srsran_cbsegm_t sg;
+    if (srsran_cbsegm(&sg, (uint32_t)cfg->grant.tb.tbs) || !cfg->softbuffers.rx) {
+      return SRSRAN_ERROR_INVALID_INPUTS;
+    }
+    cfg->K_segm = sg.C1 * sg.K1 + sg.C2 * sg.K2;
+    plain.push_back(i);
+    g_off[i]    = g_tot;
+    data_off[i] = data_tot;
+    g_tot += (cfg->grant.tb.nof_bits + 7) & ~7u;
+    data_tot += ((uint32_t)cfg->grant.tb.tbs / 8 + 64 + 15) & ~15u;
+  }
+  if (!plain.empty()) {
+    if (!grow((void**)&g->d_g, &g->g_cap, g_tot * sizeof(int16_t)) || !grow((void**)&g->d_data, &g->data_cap, data_tot) ||
+        !grow((void**)&g->d_res, &g->res_cap, 2 * plain.size() * sizeof(int32_t))) {
+      return SRSRAN_ERROR;
+    }
+    uint32_t maxit = 0;
+    for (uint32_t i : plain) {
+      srsran_pusch_cfg_t* cfg = ues[i].cfg;
+      srsran_ulsch_gpu_tb_t t;
+      memset(&t, 0, sizeof(t));
+      t.tbs        = (uint32_t)cfg->grant.tb.tbs;
+      t.Qm         = srsran_mod_bits_x_symbol(cfg->grant.tb.mod);
+      t.rv         = (uint32_t)cfg->grant.tb.rv;
+      t.nof_e_bits = cfg->grant.tb.nof_bits;
+      t.nof_symb   = cfg->grant.nof_symb;
+      t.d_q_bits   = g->d_q + q_off[i];
+      t.d_g_bits   = g->d_g + g_off[i];
+      t.d_data     = g->d_data + data_off[i];
+      t.softbuffer = cfg->softbuffers.rx;
+      t.new_data   = 0;
+      tb.push_back(t);
+      maxit = std::max(maxit, cfg->max_nof_iterations);
+    }
+    srsran_sch_set_max_noi(&q->ul_sch, maxit);
+    int32_t* d_r = g->d_res;
+    float*   d_a = (float*)(g->d_res + plain.size());
+    if (srsran_ulsch_gpu_decode_batch(&q->ul_sch, (uint32_t)plain.size(), tb.data(), d_r, d_a, st) != SRSRAN_SUCCESS) {
+      return SRSRAN_ERROR;
+    }
+    std::vector<int32_t> hr(2 * plain.size());
+    if (hipMemcpyAsync(hr.data(), g->d_res, hr.size() * sizeof(int32_t), hipMemcpyDeviceToHost, st) != hipSuccess) {
+      return SRSRAN_ERROR;
+    }
+    for (uint32_t i : plain) {
+      if (res[i].data && hipMemcpyAsync(res[i].data, g->d_data + data_off[i], (size_t)ues[i].cfg->grant.tb.tbs / 8,
+                                        hipMemcpyDeviceToHost, st) != hipSuccess) {
+        return SRSRAN_ERROR;
+      }
+    }
+    if (hipStreamSynchronize(st) != hipSuccess) {
+      return SRSRAN_ERROR;
+    }
+    for (size_t k = 0; k < plain.size(); k++) {
+      const uint32_t i = plain[k];
+      float          avg;
+      memcpy(&avg, &hr[plain.size() + k], sizeof(float));
+      res[i].crc                  = hr[k] == 0;
+      res[i].avg_iterations_block = avg;
+      res[i].evm                  = NAN;
+      memset(&res[i].uci, 0, sizeof(res[i].uci));
+      ues[i].cfg->last_O_cqi = (uint32_t)srsran_cqi_size(&ues[i].cfg->uci_cfg.cqi);
+      q->ul_sch.avg_iterations = avg;
+    }
+  }
+  for (uint32_t i = 0; i < nof_ue; i++) {
+    srsran_pusch_cfg_t* cfg = ues[i].cfg;
+    if (!(any_uci(cfg) || cfg->grant.tb.tbs <= 0)) {
+      continue;
+    }
     srsran_sch_set_max_noi(&q->ul_sch, cfg->max_nof_iterations);
     const int ret = ulsch_decode_dev(&q->ul_sch, cfg, g->d_q + q_off[i], any_uci(cfg) ? g->d_c + c_off[i] : nullptr,
                                      res[i].data, &res[i].uci);

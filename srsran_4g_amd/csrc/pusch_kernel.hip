@@ -21,6 +21,7 @@
 #include <stdint.h>
 
 #include "pusch_kernel.h"
+#include "stage_timing.h"
 
 namespace srsran_amd {
 
@@ -165,6 +166,7 @@ hipError_t chest_ul_launch(const PuschUe* d_ues, uint32_t nue, hipStream_t strea
   if (nue == 0) {
     return hipSuccess;
   }
+  StageScope timing_scope(ST_CHEST_UL, stream);
   hipLaunchKernelGGL(chest_ul_kernel, dim3(nue), dim3(PU_THREADS), 0, stream, d_ues);
   return hipGetLastError();
 }
@@ -293,6 +295,7 @@ hipError_t pusch_eq_idft_launch(const PuschUe* d_ues, uint32_t nue, hipStream_t 
   if (nue == 0) {
     return hipSuccess;
   }
+  StageScope timing_scope(ST_PUSCH_EQ, stream);
   hipLaunchKernelGGL(pusch_eq_idft_kernel, dim3(14, nue), dim3(PU_THREADS), 0, stream, d_ues);
   return hipGetLastError();
 }

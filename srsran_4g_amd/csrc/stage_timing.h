@@ -6,7 +6,7 @@
 
 namespace srsran_amd {
 
-enum Stage { ST_OFDM = 0, ST_CHEST, ST_PRED, ST_LLR, ST_RM, ST_TDEC, ST_TB, ST_NR_RM, ST_LDPC, ST_NR_TB, ST_COUNT };
+enum Stage { ST_OFDM = 0, ST_CHEST, ST_PRED, ST_LLR, ST_RM, ST_TDEC, ST_TB, ST_NR_RM, ST_LDPC, ST_NR_TB, ST_CHEST_UL, ST_PUSCH_EQ, ST_COUNT };
 
 // Records a start event on construction and a stop event on destruction (same stream).
 class StageScope {

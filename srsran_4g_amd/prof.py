@@ -3,7 +3,7 @@ import ctypes
 
 from .tdec import load_library
 
-NOF_STAGES = 10
+NOF_STAGES = 12
 _bound = False
 
 

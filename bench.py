@@ -486,12 +486,11 @@ def run_pusch(args, torch, dist, world, rank, device):
         arr[b].sf = ctypes.pointer(sfs[b])
         arr[b].cfg = ctypes.pointer(cfgs[b])
         arr[b].d_sf_symbols = d_grid.data_ptr() + b * per_grid
+        arr[b].new_data = 1
         res[b].data = datas[b].ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
     L_ = P.lib()
 
-    def step():
-        for sb in sbs:  # new transmissions (as srsran_softbuffer_rx_reset before each new TB)
-            S.lib().srsran_softbuffer_rx_reset_tbs(ctypes.byref(sb.s), C3_TBS)
+    def step():  # new transmissions: new_data = 1 (the soft buffers are reset in the decode launch)
         if L_.srsran_pusch_gpu_decode_batch(ctypes.byref(pu.q), nue, arr, cres, res) != 0:
             raise RuntimeError("srsran_pusch_gpu_decode_batch failed")
 

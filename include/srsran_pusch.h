@@ -153,6 +153,7 @@ typedef struct {
   srsran_ul_sf_cfg_t* sf;
   srsran_pusch_cfg_t* cfg;
   const cf_t*         d_sf_symbols; /* device */
+  uint32_t            new_data;     /* 1: as if srsran_softbuffer_rx_reset_tbs(softbuffer, tbs) ran first */
 } srsran_pusch_gpu_ue_t;
 
 int srsran_pusch_gpu_decode_batch(srsran_pusch_t*              q,

@@ -933,7 +933,7 @@ int srsran_pusch_gpu_decode_batch(srsran_pusch_t*              q,
       t.d_g_bits   = g->d_g + g_off[i];
       t.d_data     = g->d_data + data_off[i];
       t.softbuffer = cfg->softbuffers.rx;
-      t.new_data   = 0;
+      t.new_data   = ues[i].new_data ? 1 : 0;
       tb.push_back(t);
       maxit = std::max(maxit, cfg->max_nof_iterations);
     }
@@ -972,6 +972,9 @@ int srsran_pusch_gpu_decode_batch(srsran_pusch_t*              q,
     srsran_pusch_cfg_t* cfg = ues[i].cfg;
     if (!(any_uci(cfg) || cfg->grant.tb.tbs <= 0)) {
       continue;
+    }
+    if (ues[i].new_data && cfg->softbuffers.rx && cfg->grant.tb.tbs > 0) {
+      srsran_softbuffer_rx_reset_tbs(cfg->softbuffers.rx, (uint32_t)cfg->grant.tb.tbs);
     }
     srsran_sch_set_max_noi(&q->ul_sch, cfg->max_nof_iterations);
     const int ret = ulsch_decode_dev(&q->ul_sch, cfg, g->d_q + q_off[i], any_uci(cfg) ? g->d_c + c_off[i] : nullptr,

@@ -47,7 +47,7 @@ class srsran_pusch_t(ctypes.Structure):
 
 class srsran_pusch_gpu_ue_t(ctypes.Structure):
     _fields_ = [("chest", ctypes.POINTER(srsran_chest_ul_t)), ("sf", ctypes.POINTER(srsran_ul_sf_cfg_t)),
-                ("cfg", ctypes.POINTER(srsran_pusch_cfg_t)), ("d_sf_symbols", ctypes.c_void_p)]
+                ("cfg", ctypes.POINTER(srsran_pusch_cfg_t)), ("d_sf_symbols", ctypes.c_void_p), ("new_data", u32)]
 
 
 _bound = False

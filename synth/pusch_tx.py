@@ -33,7 +33,8 @@ def subframe(cell, dmrs_cfg, cell_prb, L, n_prb, tbs, Qm, tti, rnti, rng, snr_db
     grid[3, n_prb * 12:n_prb * 12 + M] = r[:M]
     grid[10, n_prb * 12:n_prb * 12 + M] = r[M:]
     k = np.arange(12 * cell_prb)
-    taps = (rng.standard_normal(3) + 1j * rng.standard_normal(3)) * np.array([0.8, 0.4, 0.2]) / np.sqrt(2)
+    # a dominant path and two weaker random echoes: |H| stays within about [0.6, 1.4]
+    taps = np.concatenate([[1.0], (rng.standard_normal(2) + 1j * rng.standard_normal(2)) * np.array([0.2, 0.1]) / np.sqrt(2)])
     H = (taps[None, :] * np.exp(-2j * np.pi * k[:, None] * np.array([0.0, 3.0, 7.0])[None, :] / 2048.0)).sum(axis=1)
     grid = grid * H[None, :]
     s2 = 10 ** (-snr_db / 10)

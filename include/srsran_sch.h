@@ -241,6 +241,32 @@ int srsran_dlsch_gpu_decode_batch(srsran_sch_t*                q,
                                   float*                       d_avg_noi,
                                   void*                        stream);
 
+/* ---- DL-SCH transmit (sch.c:240-359, 621-652; turbocoder.c; rm_turbo.c:345-388) ----
+ * TB CRC24A, code block segmentation with CRC24B, turbo encoding and rate matching, all on the GPU.
+ * e_bits: packed, MSB first, cfg->grant.tb[tb_idx].nof_bits bits (ceil(nof_bits / 8) bytes written).
+ * data must be given: the reference's retransmission from the soft buffer (data == NULL) is not
+ * provided; the soft buffer argument is not used (every call encodes from the payload).  Filler
+ * bits are refused as in the reference. */
+int srsran_dlsch_encode(srsran_sch_t* q, srsran_pdsch_cfg_t* cfg, uint8_t* data, uint8_t* e_bits);
+int srsran_dlsch_encode2(srsran_sch_t*       q,
+                         srsran_pdsch_cfg_t* cfg,
+                         uint8_t*            data,
+                         uint8_t*            e_bits,
+                         int                 tb_idx,
+                         uint32_t            nof_layers);
+
+/* Added batch entry point: many TBs in three launches, asynchronous on `stream`. */
+typedef struct {
+  uint32_t       tbs;
+  uint32_t       Qm; /* bits per symbol x layers, as encode_tb receives it */
+  uint32_t       rv;
+  uint32_t       nof_e_bits;
+  const uint8_t* d_data;   /* device, tbs / 8 bytes */
+  uint8_t*       d_e_bits; /* device, ceil(nof_e_bits / 8) bytes, packed MSB first */
+} srsran_dlsch_gpu_enc_t;
+
+int srsran_dlsch_gpu_encode_batch(srsran_sch_t* q, uint32_t nof_tb, const srsran_dlsch_gpu_enc_t* tbs, void* stream);
+
 /* ---- UL-SCH receive with UCI multiplexed (sch.c:994-1193, uci.c, cqi.c) ----
  * Mirrors of pusch_cfg.h:29-87, uci_cfg.h:31-59 and cqi.h:74-143 keep the reference's field names
  * and layout so callers compile unchanged. */

@@ -1,0 +1,206 @@
+// srsran_4g_amd/csrc/enc_kernel.hip -- DL-SCH transmit side for CDNA4:
+//
+//   enc_tb_crc_kernel  TB CRC24A (sch.c:240-359 through srsran_tcod_encode_lut's crc_tb): one wave
+//                      per TB, each lane the CRC of a contiguous chunk from zero, moved into place by
+//                      x^(8 bytes_after) mod P and XOR-reduced across the wave (crc24_dev.h).
+//   enc_cb_kernel      one workgroup of two waves per code block: the block's bits in LDS, CRC24B
+//                      (C > 1) the same way, then the two constituent encoders of the PCCC
+//                      (turbocoder.c: g0 = 13, g1 = 15 octal, 36.212 5.1.3.2), wave 0 on c(k),
+//                      wave 1 on c(pi(k)) with pi the QPP interleaver.  The 8-state recursion is
+//                      linear over GF(2), so each lane encodes a chunk of ceil(K/64) bits from the
+//                      zero state, lane 0 chains the chunks' true start states through the
+//                      zero-input transition of one chunk (an 8-entry table), and every lane
+//                      re-encodes its chunk from its start state: 2 x ceil(K/64) dependent steps
+//                      instead of K.  Trellis termination appends the 12 tail bits (natural
+//                      3K+12 order).  Rate matching reads the circular buffer through the
+//                      transmitter's read-out table (the inverse of the receive table): e(j) =
+//                      coded(fwd(j mod (3K+12))), coalesced writes.
+//   enc_pack_kernel    unpacked e bits -> bytes, MSB first (the packed e_bits of srsran_dlsch_encode).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "crc24_dev.h"
+#include "enc_kernel.h"
+
+namespace srsran_amd {
+
+static constexpr uint32_t kCrc24A = 0x1864CFBu, kCrc24B = 0x1800063u;
+
+// x^(8 n) mod P
+__device__ __forceinline__ uint32_t xpow8(uint32_t n, uint32_t poly)
+{
+  uint32_t r = 1, b = 0x100u;  // x^8
+  while (n) {
+    if (n & 1u) {
+      r = clmul_mod24(r, b, poly);
+    }
+    b = clmul_mod24(b, b, poly);
+    n >>= 1;
+  }
+  return r;
+}
+
+// CRC (zero init, no final xor) of bytes [0, n) given by get(i), over one wave; result in every lane
+template <typename F>
+__device__ __forceinline__ uint32_t wave_crc(uint32_t n, uint32_t poly, F get)
+{
+  const uint32_t lane = threadIdx.x & 63, ch = (n + 63) / 64;
+  const uint32_t b0 = min(lane * ch, n), b1 = min(b0 + ch, n);
+  uint32_t       c  = 0;
+  for (uint32_t i = b0; i < b1; i++) {
+    c = crc24_byte(c, get(i), poly);
+  }
+  uint32_t part = b1 > b0 ? clmul_mod24(c, xpow8(n - b1, poly), poly) : 0u;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    part ^= (uint32_t)__shfl_xor((int)part, off, 64);
+  }
+  return part;
+}
+
+__global__ __launch_bounds__(64) void enc_tb_crc_kernel(const EncTb* __restrict__ tbs)
+{
+  const EncTb& t = tbs[blockIdx.x];
+  const uint8_t* d = t.data;
+  const uint32_t c = wave_crc(t.nbytes, kCrc24A, [&](uint32_t i) { return (uint32_t)d[i]; });
+  if (threadIdx.x == 0) {
+    *t.crc = c;
+  }
+}
+
+hipError_t enc_tb_crc_launch(const EncTb* d_tbs, uint32_t ntb, hipStream_t stream)
+{
+  if (ntb == 0) {
+    return hipSuccess;
+  }
+  hipLaunchKernelGGL(enc_tb_crc_kernel, dim3(ntb), dim3(64), 0, stream, d_tbs);
+  return hipGetLastError();
+}
+
+// one step of a constituent encoder: state s = r0 | r1 << 1 | r2 << 2 (r0 newest); returns parity
+__device__ __forceinline__ uint32_t rsc_step(uint32_t& s, uint32_t u)
+{
+  const uint32_t r0 = s & 1u, r1 = (s >> 1) & 1u, r2 = (s >> 2) & 1u;
+  const uint32_t in = u ^ r2 ^ r1;
+  const uint32_t p  = r2 ^ r0 ^ in;
+  s                 = (in | (r0 << 1) | (r1 << 2));
+  return p;
+}
+
+__global__ __launch_bounds__(128) void enc_cb_kernel(const EncCb* __restrict__ cbs)
+{
+  const EncCb& b = cbs[blockIdx.x];
+  __shared__ uint8_t  cbytes[768];
+  __shared__ uint8_t  c[6144];
+  __shared__ uint8_t  coded[3 * 6144 + 12];
+  __shared__ uint8_t  e_end[2][64], s_start[2][64], T[2][8];
+  const uint32_t      K = b.K, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const uint32_t      nB = b.rlen / 8;
+
+  // the block's info bytes: payload, then the TB CRC bytes
+  const uint32_t tcrc = *b.tb_crc;
+  for (uint32_t m = tid; m < nB; m += 128) {
+    const uint32_t x = b.rp / 8 + m;
+    cbytes[m]        = x < b.tb_bytes ? b.data[x] : (uint8_t)(tcrc >> (8 * (2 - (x - b.tb_bytes))));
+  }
+  __syncthreads();
+  if (b.cb_crc && w == 0) {
+    const uint32_t cc = wave_crc(nB, kCrc24B, [&](uint32_t i) { return (uint32_t)cbytes[i]; });
+    if (lane < 3) {
+      cbytes[nB + lane] = (uint8_t)(cc >> (8 * (2 - lane)));
+    }
+  }
+  __syncthreads();
+  for (uint32_t k = tid; k < K; k += 128) {
+    c[k] = (cbytes[k >> 3] >> (7 - (k & 7))) & 1u;
+  }
+  __syncthreads();
+
+  // pass 1: every chunk from the zero state; the zero-input transition of a whole chunk
+  const uint32_t L = (K + 63) / 64, k0 = lane * L, k1 = min(k0 + L, K);
+  auto           pi = [&](uint32_t k) { return (uint32_t)(((uint64_t)b.f1 * k + (uint64_t)b.f2 * k * k) % K); };
+  uint32_t       s  = 0;
+  for (uint32_t k = k0; k < k1; k++) {
+    rsc_step(s, w ? c[pi(k)] : c[k]);
+  }
+  e_end[w][lane] = (uint8_t)s;
+  if (lane < 8) {
+    uint32_t t = lane;
+    for (uint32_t k = 0; k < L; k++) {
+      rsc_step(t, 0);
+    }
+    T[w][lane] = (uint8_t)t;
+  }
+  __syncthreads();
+  if (lane == 0) {
+    uint32_t st = 0;
+    for (uint32_t l = 0; l < 64; l++) {
+      s_start[w][l] = (uint8_t)st;
+      st            = T[w][st] ^ e_end[w][l];
+    }
+  }
+  __syncthreads();
+
+  // pass 2: parity from the true start states; tail bits from the final state (natural order:
+  // encoder 1's three (x, z) pairs, then encoder 2's)
+  s = s_start[w][lane];
+  for (uint32_t k = k0; k < k1; k++) {
+    const uint32_t u = w ? c[pi(k)] : c[k];
+    const uint32_t p = rsc_step(s, u);
+    coded[3 * k + 1 + w] = (uint8_t)p;
+    if (w == 0) {
+      coded[3 * k] = (uint8_t)u;
+    }
+  }
+  if (k0 < K && k1 == K) {
+    for (uint32_t j = 0; j < 3; j++) {
+      const uint32_t x = ((s >> 2) ^ (s >> 1)) & 1u;  // the feedback: the register input becomes 0
+      const uint32_t p = rsc_step(s, x);
+      coded[3 * K + 6 * w + 2 * j]     = (uint8_t)x;
+      coded[3 * K + 6 * w + 2 * j + 1] = (uint8_t)p;
+    }
+  }
+  __syncthreads();
+
+  // rate matching
+  for (uint32_t j = tid; j < b.E; j += 128) {
+    const uint32_t r = j - (j / b.N) * b.N;
+    b.e[j]           = coded[b.fwd[r]];
+  }
+}
+
+hipError_t enc_cb_launch(const EncCb* d_cbs, uint32_t ncb, hipStream_t stream)
+{
+  if (ncb == 0) {
+    return hipSuccess;
+  }
+  hipLaunchKernelGGL(enc_cb_kernel, dim3(ncb), dim3(128), 0, stream, d_cbs);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void enc_pack_kernel(const EncTb* __restrict__ tbs)
+{
+  const EncTb&   t = tbs[blockIdx.y];
+  const uint32_t m = blockIdx.x * 256 + threadIdx.x;
+  if (8 * m >= t.nof_e_bits) {
+    return;
+  }
+  uint32_t v = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 8; k++) {
+    const uint32_t j = 8 * m + k;
+    v |= (j < t.nof_e_bits ? (uint32_t)t.e_bits[j] & 1u : 0u) << (7 - k);
+  }
+  t.packed[m] = (uint8_t)v;
+}
+
+hipError_t enc_pack_launch(const EncTb* d_tbs, uint32_t ntb, uint32_t max_bytes, hipStream_t stream)
+{
+  if (ntb == 0 || max_bytes == 0) {
+    return hipSuccess;
+  }
+  hipLaunchKernelGGL(enc_pack_kernel, dim3((max_bytes + 255) / 256, ntb), dim3(256), 0, stream, d_tbs);
+  return hipGetLastError();
+}
+
+}  // namespace srsran_amd

@@ -23,6 +23,7 @@
 #include "devkey.h"
 #include "sch_kernel.h"
 #include "tdec_kernel.h"
+#include "enc_kernel.h"
 #include "uci_kernel.h"
 
 using namespace srsran_amd;
@@ -184,6 +185,8 @@ struct SchCtx {
   size_t      uldesc_cap = 0;
   uint8_t*    d_uci = nullptr;     // srsran_ulsch_decode with UCI: descriptors, results, sequence
   size_t      uci_cap = 0;
+  uint8_t*    d_enc = nullptr;     // DL-SCH encode: descriptors, TB CRCs, unpacked e bits, staging
+  size_t      enc_cap = 0;
 };
 
 constexpr size_t kDataCap = (size_t)SCH_MAX_CB * SCH_SLOT_BYTES;
@@ -854,6 +857,7 @@ void srsran_sch_free(srsran_sch_t* q)
     hipFree(x->d_ul);
     hipFree(x->d_uldesc);
     hipFree(x->d_uci);
+    hipFree(x->d_enc);
     delete x;
   }
   srsran_tdec_free(&q->decoder);
@@ -1504,6 +1508,45 @@ int srsran_ulsch_decode(srsran_sch_t*       q,
 }  // extern "C"
 
 namespace srsran_amd {
+// Rate-matching read-out for the transmitter (rm_turbo.c:345-388): fwd[k] = the natural-layout
+// encoder output index (3 i + stream, tail 3K..3K+11) of the k-th transmitted bit of the rv's
+// circular buffer, period 3K + 12 along the E bits.  The inverse of the receive table.
+bool rm_fwd_table(uint32_t cb_idx, uint32_t rv, const uint16_t** d_fwd, uint32_t* N)
+{
+  static std::map<uint64_t, uint16_t*> cache;
+  const uint32_t                       K   = (uint32_t)srsran_cbsegm_cbsize(cb_idx);
+  const uint64_t                       key = ((uint64_t)cur_dev() << 32) | (cb_idx * 4 + rv);
+  *N                                       = 3 * K + 12;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto                        it = cache.find(key);
+    if (it != cache.end()) {
+      *d_fwd = it->second;
+      return true;
+    }
+  }
+  InvTable t;
+  if (!inv_table(cb_idx, rv, false, &t)) {
+    return false;
+  }
+  std::vector<uint16_t> inv(t.len), fwd(t.N);
+  if (hipMemcpy(inv.data(), t.d, t.len * sizeof(uint16_t), hipMemcpyDeviceToHost) != hipSuccess) {
+    return false;
+  }
+  for (uint32_t n = 0; n < t.len; n++) {
+    fwd[inv[n]] = (uint16_t)n;
+  }
+  uint16_t* d = nullptr;
+  if (hipMalloc((void**)&d, t.N * sizeof(uint16_t)) != hipSuccess ||
+      hipMemcpy(d, fwd.data(), t.N * sizeof(uint16_t), hipMemcpyHostToDevice) != hipSuccess) {
+    return false;
+  }
+  std::lock_guard<std::mutex> lk(g_mu);
+  cache[key] = d;
+  *d_fwd     = d;
+  return true;
+}
+
 hipStream_t sch_stream(srsran_sch_t* q) { return q && q->gpu ? ((SchCtx*)q->gpu)->stream : nullptr; }
 
 int ulsch_decode_dev(srsran_sch_t* q, srsran_pusch_cfg_t* cfg, int16_t* d_q, const uint8_t* d_c, uint8_t* data,
@@ -1555,6 +1598,147 @@ int srsran_ulsch_gpu_decode_batch(srsran_sch_t*                q,
     return SRSRAN_ERROR;
   }
   return srsran_dlsch_gpu_decode_batch(q, nof_tb, dl.data(), d_result, d_avg_noi, stream);
+}
+
+
+// ---------------- DL-SCH transmit (sch.c:240-359, 621-652) ----------------
+}  // extern "C"
+namespace srsran_amd {
+bool rm_fwd_table(uint32_t cb_idx, uint32_t rv, const uint16_t** d_fwd, uint32_t* N);
+void qpp_coeffs(uint32_t idx, uint32_t* f1, uint32_t* f2);
+}  // namespace srsran_amd
+extern "C" {
+
+int srsran_dlsch_gpu_encode_batch(srsran_sch_t* q, uint32_t nof_tb, const srsran_dlsch_gpu_enc_t* tbs, void* stream)
+{
+  if (!q || !q->gpu || (nof_tb && !tbs)) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  if (nof_tb == 0) {
+    return SRSRAN_SUCCESS;
+  }
+  SchCtx*              x  = (SchCtx*)q->gpu;
+  hipStream_t          st = (hipStream_t)stream;
+  std::vector<EncTb>   tb(nof_tb);
+  std::vector<EncCb>   cb;
+  std::vector<size_t>  e_off(nof_tb);
+  size_t               e_tot = 0;
+  uint32_t             max_bytes = 0;
+  for (uint32_t t = 0; t < nof_tb; t++) {
+    const srsran_dlsch_gpu_enc_t& in = tbs[t];
+    srsran_cbsegm_t               s;
+    if (!in.d_data || !in.d_e_bits || in.Qm == 0 || in.rv > 3 || srsran_cbsegm(&s, in.tbs) || s.tbs == 0) {
+      return SRSRAN_ERROR_INVALID_INPUTS;
+    }
+    if (s.F) {
+      fprintf(stderr, "[srsran_sch] Error filler bits are not supported. Use standard TBS\n");
+      return SRSRAN_ERROR;
+    }
+    e_off[t] = e_tot;
+    e_tot += (in.nof_e_bits + 15) & ~15u;
+    max_bytes = std::max(max_bytes, (in.nof_e_bits + 7) / 8);
+    // encode_tb_off's split of the E bits over the blocks (sch.c:271-305); the K2 blocks come first
+    const uint32_t Gp = in.nof_e_bits / in.Qm, gamma = Gp % s.C;
+    uint32_t       rp = 0, wp = 0;
+    for (uint32_t i = 0; i < s.C; i++) {
+      const uint32_t K   = i < s.C2 ? s.K2 : s.K1;
+      const uint32_t idx = i < s.C2 ? s.K2_idx : s.K1_idx;
+      EncCb          c;
+      memset(&c, 0, sizeof(c));
+      c.rlen = s.C > 1 ? K - 24 : K;
+      c.E    = i <= s.C - gamma - 1 ? in.Qm * (Gp / s.C) : in.Qm * ((Gp + s.C - 1) / s.C);
+      c.K    = K;
+      c.rp   = rp;
+      c.cb_crc   = s.C > 1;
+      c.tb_bytes = in.tbs / 8;
+      c.data     = in.d_data;
+      qpp_coeffs(idx, &c.f1, &c.f2);
+      if (!rm_fwd_table(idx, in.rv, &c.fwd, &c.N)) {
+        return SRSRAN_ERROR;
+      }
+      c.e    = (uint8_t*)(uintptr_t)(e_off[t] + wp);  // offsets: fixed up after the allocation
+      c.tb_crc = (const uint32_t*)(uintptr_t)t;
+      cb.push_back(c);
+      rp += c.rlen;
+      wp += c.E;
+    }
+    if (wp > in.nof_e_bits) {
+      return SRSRAN_ERROR_INVALID_INPUTS;
+    }
+    tb[t] = {in.d_data, nullptr, nullptr, in.d_e_bits, in.tbs / 8, in.nof_e_bits};
+  }
+  // device scratch: [EncTb x ntb][EncCb x ncb][crc x ntb][unpacked e bits]
+  const size_t o_cb = align16(nof_tb * sizeof(EncTb)), o_crc = o_cb + align16(cb.size() * sizeof(EncCb));
+  const size_t o_e = o_crc + align16(nof_tb * sizeof(uint32_t)), need = o_e + e_tot;
+  if (!grow_dev((void**)&x->d_enc, &x->enc_cap, need)) {
+    return SRSRAN_ERROR;
+  }
+  uint32_t* d_crc = (uint32_t*)(x->d_enc + o_crc);
+  uint8_t*  d_e   = x->d_enc + o_e;
+  for (uint32_t t = 0; t < nof_tb; t++) {
+    tb[t].crc    = d_crc + t;
+    tb[t].e_bits = d_e + e_off[t];
+  }
+  for (EncCb& c : cb) {
+    c.e      = d_e + (size_t)(uintptr_t)c.e;
+    c.tb_crc = d_crc + (size_t)(uintptr_t)c.tb_crc;
+  }
+  const EncTb* d_tb = (const EncTb*)x->d_enc;
+  const EncCb* d_cb = (const EncCb*)(x->d_enc + o_cb);
+  if (hipMemcpyAsync(x->d_enc, tb.data(), nof_tb * sizeof(EncTb), hipMemcpyHostToDevice, st) != hipSuccess ||
+      hipMemcpyAsync(x->d_enc + o_cb, cb.data(), cb.size() * sizeof(EncCb), hipMemcpyHostToDevice, st) != hipSuccess ||
+      enc_tb_crc_launch(d_tb, nof_tb, st) != hipSuccess || enc_cb_launch(d_cb, (uint32_t)cb.size(), st) != hipSuccess ||
+      enc_pack_launch(d_tb, nof_tb, max_bytes, st) != hipSuccess) {
+    return SRSRAN_ERROR;
+  }
+  // the descriptors live in x->d_enc until the stream has consumed them
+  return hipStreamSynchronize(st) == hipSuccess ? SRSRAN_SUCCESS : SRSRAN_ERROR;
+}
+
+int srsran_dlsch_encode2(srsran_sch_t*       q,
+                         srsran_pdsch_cfg_t* cfg,
+                         uint8_t*            data,
+                         uint8_t*            e_bits,
+                         int                 tb_idx,
+                         uint32_t            nof_layers)
+{
+  if (!q || !q->gpu || !cfg || !e_bits || tb_idx < 0 || tb_idx >= SRSRAN_MAX_CODEWORDS) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  if (!data) {
+    fprintf(stderr, "[srsran_sch] encoding from the soft buffer (data == NULL) is not provided\n");
+    return SRSRAN_ERROR;
+  }
+  const srsran_ra_tb_t& t  = cfg->grant.tb[tb_idx];
+  const uint32_t        Nl = nof_layers != cfg->grant.nof_tb ? 2 : 1;  // sch.c:633-636
+  const uint32_t        Qm = srsran_mod_bits_x_symbol(t.mod) * Nl;
+  if (t.tbs <= 0) {
+    return t.tbs == 0 ? SRSRAN_SUCCESS : SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  SchCtx*        x      = (SchCtx*)q->gpu;
+  const uint32_t nbytes = (uint32_t)t.tbs / 8, ebytes = (t.nof_bits + 7) / 8;
+  uint8_t*       d_io   = nullptr;
+  if (hipMallocAsync((void**)&d_io, nbytes + ebytes + 16, x->stream) != hipSuccess) {
+    return SRSRAN_ERROR;
+  }
+  srsran_dlsch_gpu_enc_t e = {(uint32_t)t.tbs, Qm, (uint32_t)t.rv, t.nof_bits, d_io, d_io + nbytes};
+  int                    r = SRSRAN_ERROR;
+  if (hipMemcpyAsync(d_io, data, nbytes, hipMemcpyHostToDevice, x->stream) == hipSuccess) {
+    r = srsran_dlsch_gpu_encode_batch(q, 1, &e, x->stream);
+    if (r == SRSRAN_SUCCESS &&
+        (hipMemcpyAsync(e_bits, d_io + nbytes, ebytes, hipMemcpyDeviceToHost, x->stream) != hipSuccess ||
+         hipStreamSynchronize(x->stream) != hipSuccess)) {
+      r = SRSRAN_ERROR;
+    }
+  }
+  hipFreeAsync(d_io, x->stream);
+  hipStreamSynchronize(x->stream);
+  return r;
+}
+
+int srsran_dlsch_encode(srsran_sch_t* q, srsran_pdsch_cfg_t* cfg, uint8_t* data, uint8_t* e_bits)
+{
+  return srsran_dlsch_encode2(q, cfg, data, e_bits, 0, 1);
 }
 
 }  // extern "C"

@@ -281,6 +281,15 @@ const XpowTables* xpow_tables()
 }  // namespace
 
 namespace srsran_amd {
+// QPP coefficients of code block size index idx (36.212 Table 5.1.3-3), for the encoder
+void qpp_coeffs(uint32_t idx, uint32_t* f1, uint32_t* f2)
+{
+  *f1 = kF1[idx];
+  *f2 = kF2[idx];
+}
+}  // namespace srsran_amd
+
+namespace srsran_amd {
 
 int tdec_cb_index(uint32_t K) { return cb_index(K); }
 

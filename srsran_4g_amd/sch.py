@@ -160,6 +160,11 @@ class srsran_uci_value_t(ctypes.Structure):
                 ("ri", u8)]
 
 
+class srsran_dlsch_gpu_enc_t(ctypes.Structure):
+    _fields_ = [("tbs", u32), ("Qm", u32), ("rv", u32), ("nof_e_bits", u32), ("d_data", ctypes.c_void_p),
+                ("d_e_bits", ctypes.c_void_p)]
+
+
 class srsran_ulsch_gpu_tb_t(ctypes.Structure):
     _fields_ = [("tbs", u32), ("Qm", u32), ("rv", u32), ("nof_e_bits", u32), ("nof_symb", u32),
                 ("d_q_bits", ctypes.c_void_p), ("d_g_bits", ctypes.c_void_p), ("d_data", ctypes.c_void_p),
@@ -222,6 +227,9 @@ def lib():
         "srsran_sch_find_Ioffset_ri": ([ctypes.c_float], u32),
         "srsran_qprime_cqi_ext": ([u32, u32, u32, ctypes.c_float], u32),
         "srsran_qprime_ack_ext": ([u32, u32, u32, u32, ctypes.c_float], u32),
+        "srsran_dlsch_encode2": ([SCH, CFG, _u8p, _u8p, ctypes.c_int, u32], ctypes.c_int),
+        "srsran_dlsch_gpu_encode_batch": ([SCH, u32, ctypes.POINTER(srsran_dlsch_gpu_enc_t), ctypes.c_void_p],
+                                          ctypes.c_int),
         "srsran_uci_cfg_total_ack": ([ctypes.POINTER(srsran_uci_cfg_t)], u32),
         "srsran_cqi_size": ([ctypes.POINTER(srsran_cqi_cfg_t)], ctypes.c_int),
         "srsran_cqi_value_pack": ([ctypes.POINTER(srsran_cqi_cfg_t), ctypes.POINTER(srsran_cqi_value_t), _u8p],
@@ -373,6 +381,25 @@ class Sch:
         ret = lib().srsran_dlsch_decode2(ctypes.byref(self.q), ctypes.byref(cfg), e.ctypes.data_as(_i16p),
                                          data.ctypes.data_as(_u8p), tb_idx, nof_layers)
         return ret, data, self.last_noi()
+
+    def encode(self, tbs, Qm, rv, nof_bits, data, nof_layers=1, nof_tb=1, tb_idx=0):
+        """srsran_dlsch_encode2 -> (ret, packed e bits)"""
+        cfg = srsran_pdsch_cfg_t()
+        cfg.grant.nof_tb = nof_tb
+        tb = cfg.grant.tb[tb_idx]
+        tb.mod, tb.tbs, tb.rv, tb.nof_bits, tb.enabled = MOD_FROM_QM[Qm], tbs, rv, nof_bits, True
+        d = np.ascontiguousarray(data, dtype=np.uint8)
+        e = np.zeros((nof_bits + 7) // 8, np.uint8)
+        ret = lib().srsran_dlsch_encode2(ctypes.byref(self.q), ctypes.byref(cfg), d.ctypes.data_as(_u8p),
+                                         e.ctypes.data_as(_u8p), tb_idx, nof_layers)
+        return ret, e
+
+    def encode_batch(self, entries, stream=None):
+        """srsran_dlsch_gpu_encode_batch; entries: (tbs, Qm x layers, rv, nof_e_bits, d_data, d_e_bits)"""
+        arr = (srsran_dlsch_gpu_enc_t * len(entries))()
+        for i, (tbs, Qm, rv, nb, dd, de) in enumerate(entries):
+            arr[i].tbs, arr[i].Qm, arr[i].rv, arr[i].nof_e_bits, arr[i].d_data, arr[i].d_e_bits = tbs, Qm, rv, nb, dd, de
+        return lib().srsran_dlsch_gpu_encode_batch(ctypes.byref(self.q), len(entries), arr, stream)
 
     def decode_batch(self, entries, d_result, d_avg, stream=None):
         """srsran_dlsch_gpu_decode_batch over device buffers.

@@ -296,6 +296,8 @@ struct PuschGpu {
   size_t      data_cap = 0;
   int32_t*    d_res  = nullptr;  // batch: decode_tb results / average iterations
   size_t      res_cap = 0;
+  uint8_t*    h_stage = nullptr; // batch: pinned host staging of results + payloads (one D2H copy)
+  size_t      stage_cap = 0;
 };
 
 uint32_t pusch_seed(uint16_t rnti, uint32_t nslot, uint32_t cell_id)  // sequences.c:119-122
@@ -651,6 +653,7 @@ void srsran_pusch_free(srsran_pusch_t* q)
     hipFree(g->d_g);
     hipFree(g->d_data);
     hipFree(g->d_res);
+    hipHostFree(g->h_stage);
     delete g;
   }
   srsran_sch_free(&q->ul_sch);
@@ -943,18 +946,27 @@ int srsran_pusch_gpu_decode_batch(srsran_pusch_t*              q,
     if (srsran_ulsch_gpu_decode_batch(&q->ul_sch, (uint32_t)plain.size(), tb.data(), d_r, d_a, st) != SRSRAN_SUCCESS) {
       return SRSRAN_ERROR;
     }
-    std::vector<int32_t> hr(2 * plain.size());
-    if (hipMemcpyAsync(hr.data(), g->d_res, hr.size() * sizeof(int32_t), hipMemcpyDeviceToHost, st) != hipSuccess) {
-      return SRSRAN_ERROR;
-    }
-    for (uint32_t i : plain) {
-      if (res[i].data && hipMemcpyAsync(res[i].data, g->d_data + data_off[i], (size_t)ues[i].cfg->grant.tb.tbs / 8,
-                                        hipMemcpyDeviceToHost, st) != hipSuccess) {
+    // results and payloads back in one copy through pinned staging
+    const size_t rbytes = 2 * plain.size() * sizeof(int32_t), sneed = rbytes + data_tot;
+    if (sneed > g->stage_cap) {
+      hipHostFree(g->h_stage);
+      g->h_stage   = nullptr;
+      g->stage_cap = 0;
+      if (hipHostMalloc((void**)&g->h_stage, sneed, hipHostMallocDefault) != hipSuccess) {
         return SRSRAN_ERROR;
       }
+      g->stage_cap = sneed;
     }
-    if (hipStreamSynchronize(st) != hipSuccess) {
+    if (hipMemcpyAsync(g->h_stage, g->d_res, rbytes, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(g->h_stage + rbytes, g->d_data, data_tot, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess) {
       return SRSRAN_ERROR;
+    }
+    const int32_t* hr = (const int32_t*)g->h_stage;
+    for (uint32_t i : plain) {
+      if (res[i].data) {
+        memcpy(res[i].data, g->h_stage + rbytes + data_off[i], (size_t)ues[i].cfg->grant.tb.tbs / 8);
+      }
     }
     for (size_t k = 0; k < plain.size(); k++) {
       const uint32_t i = plain[k];

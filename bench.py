@@ -10,6 +10,8 @@ A "step" is one pass of the hot path over one batch of synthetic input:
       de-interleaver + decode_tb; SURVEY 8f rank 1, data part);
   workload "pusch": the eNB PUSCH chain from the received subframe grid -- DMRS channel estimation,
       equalisation + SC-FDMA inverse DFT, demap/descramble, UL-SCH decode (SURVEY 8f rank 1);
+  workload "dlenc": the eNB DL-SCH transmit side: TB CRC, segmentation, turbo
+      encoding and rate matching of C3 transport blocks through srsran_dlsch_gpu_encode_batch;
   workload "pdsch" (BASELINE configs[2], C3): the whole UE DL chain from time-domain samples --
       OFDM, CRS channel estimation, MMSE predecoding, demap/descramble/CSI, DL-SCH decode;
   workload "ldpc" (BASELINE configs[4]): NR LDPC decode (srsran_ldpc_decoder, 8-bit layered
@@ -107,7 +109,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--workload", choices=["all188", "k6144", "dlsch", "ulsch", "pusch", "pdsch", "ldpc", "nrsch"],
+    p.add_argument("--workload", choices=["all188", "k6144", "dlsch", "ulsch", "pusch", "dlenc", "pdsch", "ldpc", "nrsch"],
                    default="all188")
     p.add_argument("--snr", type=float, default=30.0, help="pdsch: AWGN SNR (dB) of the synthetic subframes")
     p.add_argument("--subframes", type=int, default=78,
@@ -600,6 +602,71 @@ def pusch_cpu_baseline(pool, cell_id, dm, rnti, args):
                       f"oracle UL de-interleaver"}
 
 
+def run_dlenc(args, torch, dist, world, rank, device):
+    """DL-SCH encode of C3 transport blocks: per step `subframes` x 2 TBs (TBS 75376, 13 x K=5824
+    CBs, 86400 e bits each, rv 0) through srsran_dlsch_gpu_encode_batch.  Value = encoded info Mbps."""
+    import ctypes
+
+    from srsran_4g_amd import sch as S
+
+    rng = np.random.default_rng(shard(rank)["seed"])
+    ntb = 2 * args.subframes
+    host = rng.integers(0, 256, (ntb, C3_TBS // 8), dtype=np.uint8)
+    d_in = torch.from_numpy(host).to(device)
+    d_out = torch.zeros((ntb, C3_BITS // 8), dtype=torch.uint8, device=device)
+    q = S.Sch()
+    arr = (S.srsran_dlsch_gpu_enc_t * ntb)()
+    for i in range(ntb):
+        arr[i].tbs, arr[i].Qm, arr[i].rv, arr[i].nof_e_bits = C3_TBS, C3_QM, 0, C3_BITS
+        arr[i].d_data, arr[i].d_e_bits = d_in[i].data_ptr(), d_out[i].data_ptr()
+    sp = torch.cuda.current_stream(device).cuda_stream
+    L = S.lib()
+
+    def step():
+        if L.srsran_dlsch_gpu_encode_batch(ctypes.byref(q.q), ntb, arr, sp) != 0:
+            raise RuntimeError("srsran_dlsch_gpu_encode_batch failed")
+
+    elapsed = timed_region(step, args.steps, args.warmup, world, dist, torch.cuda.synchronize, device)
+    value = world * ntb * C3_TBS * args.steps / elapsed / 1e6
+    # output check against the oracle encoder on a few TBs (outside the timed region)
+    from oracle import Oracle
+    ora = Oracle()
+    out = d_out.cpu().numpy()
+    chk = [int(np.array_equal(out[i], np.packbits(ora.dlsch_encode(C3_TBS, C3_QM, 0, C3_BITS, host[i]))))
+           for i in range(0, ntb, max(1, ntb // 8))]
+    algo = ntb * (C3_TBS // 8 + C3_BITS // 8 + C3_BITS)  # payload in, packed e out, unpacked scratch once
+    result = {
+        "metric": METRIC, "value": round(value, 2), "unit": "Mbps", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8 bits",
+        "data": "synthetic: random C3 transport blocks, HBM-resident",
+        "config": {"workload": f"dlenc: {ntb} TBs x (TBS {C3_TBS}, C=13 K=5824, E={C3_BITS}, 64QAM, rv 0) per step: "
+                               "TB CRC24A + CB CRC24B + turbo encode + rate matching + packing",
+                   "tbs_per_step_per_gpu": ntb, "output_check": {"tbs": len(chk), "equal_to_oracle": sum(chk)},
+                   "parallelism": f"tb-sharded x{world}"},
+        "roofline": {"bound": "hbm", "kernel": "whole batch (3 launches)",
+                     "achieved": round(algo / (elapsed / args.steps) / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(algo / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 5), "traffic": None,
+                     "algo_bytes_per_launch": algo},
+    }
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        n, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < args.cpu_seconds:
+            ora.dlsch_encode(C3_TBS, C3_QM, 0, C3_BITS, host[n % ntb])
+            n += 1
+        dt = time.perf_counter() - t0
+        result["cpu_baseline"] = {"value": round(n * C3_TBS / dt / 1e6, 3), "unit": "Mbps", "cores": 1, "kind": "port",
+                                  "sample": f"{n} TBs through the oracle's C encoder (bit-serial turbo encoder, "
+                                            f"table rate matching), {dt:.1f} s on 1 thread"}
+    elif rank == 0:
+        result["cpu_baseline"] = None
+    q.free()
+    if world > 1:
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+
+
 def run_pdsch(args, torch, dist, world, rank, device, steps=None, warmup=None, cpu_seconds=None, emit=True):
     """UE DL chain on C3 subframes: per step `subframes` subframes of 2 rx x 30720 cf32 samples
     -> 2 TBs each (TBS 75376, 64QAM, TM3 CDD 2x2, CFI 1), new transmissions, at most `iters`
@@ -1068,6 +1135,8 @@ def main():
         return run_dlsch(args, torch, dist, world, rank, device)
     if args.workload == "pusch":
         return run_pusch(args, torch, dist, world, rank, device)
+    if args.workload == "dlenc":
+        return run_dlenc(args, torch, dist, world, rank, device)
     if args.workload == "pdsch":
         return run_pdsch(args, torch, dist, world, rank, device)
     if args.workload == "ldpc":

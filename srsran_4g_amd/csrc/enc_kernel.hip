@@ -1,8 +1,9 @@
 // srsran_4g_amd/csrc/enc_kernel.hip -- DL-SCH transmit side for CDNA4:
 //
-//   enc_tb_crc_kernel  TB CRC24A (sch.c:240-359 through srsran_tcod_encode_lut's crc_tb): one wave
-//                      per TB, each lane the CRC of a contiguous chunk from zero, moved into place by
-//                      x^(8 bytes_after) mod P and XOR-reduced across the wave (crc24_dev.h).
+//   enc_tb_crc_kernel  TB CRC24A (sch.c:240-359 through srsran_tcod_encode_lut's crc_tb): one
+//                      workgroup per TB, the payload staged in LDS by coalesced loads, each thread the
+//                      CRC of a contiguous chunk from zero, moved into place by x^(8 bytes_after) mod P
+//                      and XOR-reduced (crc24_dev.h).
 //   enc_cb_kernel      one workgroup of two waves per code block: the block's bits in LDS, CRC24B
 //                      (C > 1) the same way, then the two constituent encoders of the PCCC
 //                      (turbocoder.c: g0 = 13, g1 = 15 octal, 36.212 5.1.3.2), wave 0 on c(k),
@@ -11,7 +12,7 @@
 //                      zero state, lane 0 chains the chunks' true start states through the
 //                      zero-input transition of one chunk (an 8-entry table), and every lane
 //                      re-encodes its chunk from its start state: 2 x ceil(K/64) dependent steps
-//                      instead of K.  Trellis termination appends the 12 tail bits (natural
+//                      instead of K (the QPP index stepped incrementally, no division).  Trellis termination appends the 12 tail bits (natural
 //                      3K+12 order).  Rate matching reads the circular buffer through the
 //                      transmitter's read-out table (the inverse of the receive table): e(j) =
 //                      coded(fwd(j mod (3K+12))), coalesced writes.
@@ -58,13 +59,41 @@ __device__ __forceinline__ uint32_t wave_crc(uint32_t n, uint32_t poly, F get)
   return part;
 }
 
-__global__ __launch_bounds__(64) void enc_tb_crc_kernel(const EncTb* __restrict__ tbs)
+// 256 threads per TB: thread t CRCs bytes [t ch, (t+1) ch) from zero (the chunk is first copied to
+// LDS with coalesced loads), moves it into place with x^(8 bytes_after), XOR-reduce
+__global__ __launch_bounds__(256) void enc_tb_crc_kernel(const EncTb* __restrict__ tbs)
 {
-  const EncTb& t = tbs[blockIdx.x];
-  const uint8_t* d = t.data;
-  const uint32_t c = wave_crc(t.nbytes, kCrc24A, [&](uint32_t i) { return (uint32_t)d[i]; });
-  if (threadIdx.x == 0) {
-    *t.crc = c;
+  const EncTb&       t = tbs[blockIdx.x];
+  __shared__ uint8_t buf[12800];
+  __shared__ uint32_t red[4];
+  const uint32_t     n = t.nbytes, tid = threadIdx.x;
+  uint32_t           part = 0;
+  for (uint32_t base = 0; base < n; base += 12800) {  // <= 12800 bytes per pass (TBS <= 102400 bits)
+    const uint32_t m = min(12800u, n - base);
+    for (uint32_t i = tid; i < m; i += 256) {
+      buf[i] = t.data[base + i];
+    }
+    __syncthreads();
+    const uint32_t ch = (m + 255) / 256, b0 = min(tid * ch, m), b1 = min(b0 + ch, m);
+    uint32_t       c  = 0;
+    for (uint32_t i = b0; i < b1; i++) {
+      c = crc24_byte(c, buf[i], kCrc24A);
+    }
+    if (b1 > b0) {
+      part ^= clmul_mod24(c, xpow8(n - base - b1, kCrc24A), kCrc24A);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    part ^= (uint32_t)__shfl_xor((int)part, off, 64);
+  }
+  if ((tid & 63) == 0) {
+    red[tid >> 6] = part;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    *t.crc = red[0] ^ red[1] ^ red[2] ^ red[3];
   }
 }
 
@@ -73,7 +102,7 @@ hipError_t enc_tb_crc_launch(const EncTb* d_tbs, uint32_t ntb, hipStream_t strea
   if (ntb == 0) {
     return hipSuccess;
   }
-  hipLaunchKernelGGL(enc_tb_crc_kernel, dim3(ntb), dim3(64), 0, stream, d_tbs);
+  hipLaunchKernelGGL(enc_tb_crc_kernel, dim3(ntb), dim3(256), 0, stream, d_tbs);
   return hipGetLastError();
 }
 
@@ -118,10 +147,21 @@ __global__ __launch_bounds__(128) void enc_cb_kernel(const EncCb* __restrict__ c
 
   // pass 1: every chunk from the zero state; the zero-input transition of a whole chunk
   const uint32_t L = (K + 63) / 64, k0 = lane * L, k1 = min(k0 + L, K);
-  auto           pi = [&](uint32_t k) { return (uint32_t)(((uint64_t)b.f1 * k + (uint64_t)b.f2 * k * k) % K); };
-  uint32_t       s  = 0;
+  // QPP pi(k) = (f1 k + f2 k^2) mod K stepped incrementally: pi(k+1) = pi(k) + g(k),
+  // g(k+1) = g(k) + 2 f2 (mod K)
+  const uint32_t pi0 = k0 < K ? (uint32_t)(((uint64_t)b.f1 * k0 + (uint64_t)b.f2 * k0 * k0) % K) : 0u;
+  const uint32_t g0  = k0 < K ? (uint32_t)(((uint64_t)b.f1 + (uint64_t)b.f2 * (2 * (uint64_t)k0 + 1)) % K) : 0u;
+  const uint32_t d2  = (uint32_t)((2 * (uint64_t)b.f2) % K);
+  auto           adv = [&](uint32_t& p, uint32_t& g) {
+    p += g;
+    p -= p >= K ? K : 0u;
+    g += d2;
+    g -= g >= K ? K : 0u;
+  };
+  uint32_t s = 0, p = pi0, g = g0;
   for (uint32_t k = k0; k < k1; k++) {
-    rsc_step(s, w ? c[pi(k)] : c[k]);
+    rsc_step(s, w ? c[p] : c[k]);
+    adv(p, g);
   }
   e_end[w][lane] = (uint8_t)s;
   if (lane < 8) {
@@ -144,28 +184,45 @@ __global__ __launch_bounds__(128) void enc_cb_kernel(const EncCb* __restrict__ c
   // pass 2: parity from the true start states; tail bits from the final state (natural order:
   // encoder 1's three (x, z) pairs, then encoder 2's)
   s = s_start[w][lane];
+  p = pi0;
+  g = g0;
   for (uint32_t k = k0; k < k1; k++) {
-    const uint32_t u = w ? c[pi(k)] : c[k];
-    const uint32_t p = rsc_step(s, u);
-    coded[3 * k + 1 + w] = (uint8_t)p;
+    const uint32_t u = w ? c[p] : c[k];
+    adv(p, g);
+    coded[3 * k + 1 + w] = (uint8_t)rsc_step(s, u);
     if (w == 0) {
       coded[3 * k] = (uint8_t)u;
     }
   }
   if (k0 < K && k1 == K) {
     for (uint32_t j = 0; j < 3; j++) {
-      const uint32_t x = ((s >> 2) ^ (s >> 1)) & 1u;  // the feedback: the register input becomes 0
-      const uint32_t p = rsc_step(s, x);
+      const uint32_t x  = ((s >> 2) ^ (s >> 1)) & 1u;  // the feedback: the register input becomes 0
+      const uint32_t pz = rsc_step(s, x);
       coded[3 * K + 6 * w + 2 * j]     = (uint8_t)x;
-      coded[3 * K + 6 * w + 2 * j + 1] = (uint8_t)p;
+      coded[3 * K + 6 * w + 2 * j + 1] = (uint8_t)pz;
     }
   }
   __syncthreads();
 
-  // rate matching
-  for (uint32_t j = tid; j < b.E; j += 128) {
-    const uint32_t r = j - (j / b.N) * b.N;
-    b.e[j]           = coded[b.fwd[r]];
+  // rate matching: the read-out table streamed 8 entries a thread ahead of the LDS gathers
+  const uint16_t* __restrict__ fwd = b.fwd;
+  uint8_t* __restrict__ eo         = b.e;
+  const uint32_t N = b.N, E = b.E;
+  for (uint32_t j0 = 0; j0 < E; j0 += 128 * 8) {
+    uint16_t f[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const uint32_t j = j0 + u * 128 + tid;
+      const uint32_t r = j - (j / N) * N;
+      f[u]             = j < E ? fwd[r] : (uint16_t)0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const uint32_t j = j0 + u * 128 + tid;
+      if (j < E) {
+        eo[j] = coded[f[u]];
+      }
+    }
   }
 }
 

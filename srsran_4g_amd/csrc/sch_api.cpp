@@ -1624,6 +1624,7 @@ int srsran_dlsch_gpu_encode_batch(srsran_sch_t* q, uint32_t nof_tb, const srsran
   std::vector<size_t>  e_off(nof_tb);
   size_t               e_tot = 0;
   uint32_t             max_bytes = 0;
+  std::map<uint32_t, std::pair<const uint16_t*, uint32_t>> fwd;  // (cb_idx, rv) -> table, looked up once
   for (uint32_t t = 0; t < nof_tb; t++) {
     const srsran_dlsch_gpu_enc_t& in = tbs[t];
     srsran_cbsegm_t               s;
@@ -1653,9 +1654,16 @@ int srsran_dlsch_gpu_encode_batch(srsran_sch_t* q, uint32_t nof_tb, const srsran
       c.tb_bytes = in.tbs / 8;
       c.data     = in.d_data;
       qpp_coeffs(idx, &c.f1, &c.f2);
-      if (!rm_fwd_table(idx, in.rv, &c.fwd, &c.N)) {
-        return SRSRAN_ERROR;
+      auto it = fwd.find(idx * 4 + in.rv);
+      if (it == fwd.end()) {
+        std::pair<const uint16_t*, uint32_t> v;
+        if (!rm_fwd_table(idx, in.rv, &v.first, &v.second)) {
+          return SRSRAN_ERROR;
+        }
+        it = fwd.emplace(idx * 4 + in.rv, v).first;
       }
+      c.fwd = it->second.first;
+      c.N   = it->second.second;
       c.e    = (uint8_t*)(uintptr_t)(e_off[t] + wp);  // offsets: fixed up after the allocation
       c.tb_crc = (const uint32_t*)(uintptr_t)t;
       cb.push_back(c);
@@ -1691,8 +1699,8 @@ int srsran_dlsch_gpu_encode_batch(srsran_sch_t* q, uint32_t nof_tb, const srsran
       enc_pack_launch(d_tb, nof_tb, max_bytes, st) != hipSuccess) {
     return SRSRAN_ERROR;
   }
-  // the descriptors live in x->d_enc until the stream has consumed them
-  return hipStreamSynchronize(st) == hipSuccess ? SRSRAN_SUCCESS : SRSRAN_ERROR;
+  // x->d_enc is reused by the next call in stream order (one stream per object)
+  return SRSRAN_SUCCESS;
 }
 
 int srsran_dlsch_encode2(srsran_sch_t*       q,

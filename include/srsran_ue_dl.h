@@ -205,6 +205,18 @@ void srsran_ofdm_set_normalize(srsran_ofdm_t* q, bool normalize_enable);
 int srsran_ofdm_rx_gpu(srsran_ofdm_t* q, const cf_t* d_in, cf_t* d_out, uint32_t nof_rx, uint32_t nof_sf, float cfo,
                        void* stream);
 
+/* Modulator (ofdm.c:585-690) in srsran_enb_dl's configuration (ofdm_cfg.normalize = false, DC
+ * subcarrier left empty, no frequency shift, normal CP).  srsran_ofdm_tx_sf: cfg.in_buffer (one
+ * port's 14 x 12 nof_prb grid, host) -> cfg.out_buffer (SRSRAN_SF_LEN samples, host).  Added:
+ * srsran_ofdm_tx_gpu on device grids [nof_sf][nof_ports][14][12 nof_prb] -> samples
+ * [nof_sf][nof_ports][sf_len], the grid scaled by `scale` first (srsran_enb_dl_gen_signal's
+ * 0.05 / sqrt(nof_prb)); asynchronous on `stream`. */
+int  srsran_ofdm_tx_init_cfg(srsran_ofdm_t* q, srsran_ofdm_cfg_t* cfg);
+void srsran_ofdm_tx_free(srsran_ofdm_t* q);
+void srsran_ofdm_tx_sf(srsran_ofdm_t* q);
+int  srsran_ofdm_tx_gpu(srsran_ofdm_t* q, const cf_t* d_in, cf_t* d_out, uint32_t nof_ports, uint32_t nof_sf, float scale,
+                        void* stream);
+
 /* ---------------- PDSCH RE map (added; srsran_pdsch_cp pdsch.c:136-220 as a table) ----------------
  * Number of PDSCH REs of `grant`; writes up to max_len grid indices (l * 12 * nof_prb + k) in
  * srsran_pdsch_get order; bit 31 marks REs of CRS-bearing symbols. */

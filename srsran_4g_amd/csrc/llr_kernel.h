@@ -35,5 +35,22 @@ hipError_t seq_apply_launch(const int16_t* d_in, int16_t* d_out, uint32_t len, u
 // out[i] = c(i) (one byte per bit) for the Gold sequence of `seed`.
 hipError_t seq_unpack_launch(uint8_t* d_out, uint32_t len, uint32_t seed, hipStream_t stream);
 
+// ---- transmitter: PDSCH scrambling + modulation + precoding + RE mapping of one subframe ----
+struct PdschTx {
+  const uint8_t*  e[2];     // packed e bits per codeword (device)
+  uint32_t        seed[2];  // scrambling seeds (pdsch_seed)
+  int             mod[2];   // srsran_mod_t
+  const uint32_t* idx;      // RE table (srsran_pdsch_re_table order; bit 31 ignored)
+  float2*         grid[2];  // per-port subframe grids (14 x 12 nof_prb)
+  uint32_t        nre;      // PDSCH REs
+  int             scheme;   // 0: one port; 1: transmit diversity (2 ports, 1 codeword); 3: CDD 2x2 (2 codewords)
+  float           scaling;  // rho_a scaling of the precoder (1)
+  float           div_scale;// (float)(scaling * M_SQRT1_2) for diversity
+};
+hipError_t pdsch_tx_launch(const PdschTx* d_items, uint32_t nitems, uint32_t max_nre, hipStream_t stream);
+// CRS of ports 0..nports-1 (<= 2) into grids [nsf][nports][14][12 nof_prb]; d_sf_idx[sf] = tti % 10
+hipError_t crs_put_launch(float2* d_grids, uint32_t nof_prb, uint32_t cell_id, uint32_t nports, const uint32_t* d_sf_idx,
+                          uint32_t nsf, hipStream_t stream);
+
 }  // namespace srsran_amd
 #endif

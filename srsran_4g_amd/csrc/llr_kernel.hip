@@ -605,4 +605,169 @@ hipError_t seq_unpack_launch(uint8_t* d_out, uint32_t len, uint32_t seed, hipStr
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------- transmitter
+// modulation tables of lte_tables.c:45-160, as the same float expressions
+__device__ __forceinline__ float qam64_level(uint32_t hi, uint32_t lo)  // (b2, b4) -> 3, 1, 5, 7 / sqrt(42)
+{
+  const uint32_t m = hi * 2 + lo;
+  return m == 0 ? 3.0f / sqrtf(42.0f) : m == 1 ? 1.0f / sqrtf(42.0f) : m == 2 ? 5.0f / sqrtf(42.0f) : 7.0f / sqrtf(42.0f);
+}
+
+// symbol of modulation `mod` (1 QPSK, 2 16QAM, 3 64QAM, 4 256QAM) from its Qm bits, b0 first (MSB)
+__device__ __forceinline__ float2 modulate(int mod, uint32_t i)
+{
+  if (mod == 1) {
+    const float l = (float)0.70710678118654752440;  // M_SQRT1_2
+    return make_float2((i & 2u) ? -l : l, (i & 1u) ? -l : l);
+  }
+  if (mod == 2) {
+    const float l1 = 1.0f / sqrtf(10.0f), l2 = 3.0f / sqrtf(10.0f);
+    const float re = (i & 2u) ? l2 : l1, im = (i & 1u) ? l2 : l1;
+    return make_float2((i & 8u) ? -re : re, (i & 4u) ? -im : im);
+  }
+  if (mod == 3) {
+    const float re = qam64_level((i >> 3) & 1u, (i >> 1) & 1u), im = qam64_level((i >> 2) & 1u, i & 1u);
+    return make_float2((i & 32u) ? -re : re, (i & 16u) ? -im : im);
+  }
+  float offset = -1, re = 0, im = 0;  // set_256QAMtable's loop
+  for (uint32_t j = 0; j < 4; j++) {
+    re += offset;
+    im += offset;
+    offset *= 2;
+    re *= (i & (1u << (2 * j + 1))) ? +1 : -1;
+    im *= (i & (1u << (2 * j + 0))) ? +1 : -1;
+  }
+  return make_float2(re / sqrtf(170), im / sqrtf(170));
+}
+
+static constexpr int TX_SPT = 16;  // symbols a thread (a whole number of bytes of e bits for every Qm)
+
+// bits of TX_SPT symbols of one codeword starting at symbol k0: scrambled (sequences.c pdsch seed,
+// srsran_sequence_pdsch_apply_pack) and mapped (srsran_mod_modulate_bytes)
+__device__ __forceinline__ void tx_symbols(const uint8_t* __restrict__ e, uint32_t seed, int mod, uint32_t k0,
+                                           uint32_t n, float2 (&x)[TX_SPT])
+{
+  const uint32_t Q = mod == 1 ? 2u : mod == 2 ? 4u : mod == 3 ? 6u : 8u;
+  uint32_t       c[8];
+  uint32_t       x1, x2;
+  gold_at(seed, k0 * Q, x1, x2);
+#pragma unroll
+  for (int w = 0; w < 8; w++) {
+    const uint32_t lo = gold16(x1, x2), hi = gold16(x1, x2);
+    c[w]                = lo | (hi << 16);
+  }
+  const uint8_t* b = e + (k0 * Q) / 8;
+#pragma unroll
+  for (int s = 0; s < TX_SPT; s++) {
+    uint32_t idx = 0;
+    if (k0 + s < n) {
+      for (uint32_t j = 0; j < Q; j++) {
+        const uint32_t pos = s * Q + j;
+        const uint32_t bit = ((b[pos >> 3] >> (7 - (pos & 7))) ^ (c[pos >> 5] >> (pos & 31))) & 1u;
+        idx                = (idx << 1) | bit;
+      }
+    }
+    x[s] = modulate(mod, idx);
+  }
+}
+
+// one workgroup per LLR_THREADS * TX_SPT PDSCH REs of one subframe (grid.y = subframe)
+__global__ __launch_bounds__(LLR_THREADS) void pdsch_tx_kernel(const PdschTx* __restrict__ items)
+{
+  const PdschTx& t  = items[blockIdx.y];
+  const uint32_t k0 = (blockIdx.x * LLR_THREADS + threadIdx.x) * TX_SPT;
+  if (k0 >= t.nre) {
+    return;
+  }
+  float2 a[TX_SPT], b[TX_SPT];
+  tx_symbols(t.e[0], t.seed[0], t.mod[0], k0, t.nre, a);
+  if (t.scheme == 3) {
+    tx_symbols(t.e[1], t.seed[1], t.mod[1], k0, t.nre, b);
+  }
+  const float sc = t.scaling;
+#pragma unroll
+  for (int s = 0; s < TX_SPT; s++) {
+    const uint32_t k = k0 + s;
+    if (k >= t.nre) {
+      break;
+    }
+    const uint32_t g = t.idx[k] & 0x7fffffffu;
+    if (t.scheme == 0) {  // srsran_precoding_single / 1 port
+      t.grid[0][g] = sc == 1.0f ? a[s] : make_float2(a[s].x * sc, a[s].y * sc);
+    } else if (t.scheme == 3) {  // srsran_precoding_cdd_2x2 (precoding.c:1996-2055)
+      const float  nm = 0.5f * sc;
+      const float2 y0 = make_float2((a[s].x + b[s].x) * nm, (a[s].y + b[s].y) * nm);
+      const float2 y1 = (k & 1u) ? make_float2((-a[s].x + b[s].x) * nm, (-a[s].y + b[s].y) * nm)
+                                 : make_float2((a[s].x - b[s].x) * nm, (a[s].y - b[s].y) * nm);
+      t.grid[0][g] = y0;
+      t.grid[1][g] = y1;
+    } else {  // transmit diversity, 2 ports (layermap.c + precoding.c:1943-1960): pairs (2i, 2i+1)
+      const float  h  = t.div_scale;
+      const bool   ev = (k & 1u) == 0;
+      const float2 x0 = a[s & ~1], x1 = a[s | 1];  // k0 even: the pair (2i, 2i+1) is inside the thread
+      if (ev) {
+        t.grid[0][g] = make_float2(x0.x * h, x0.y * h);
+        t.grid[1][g] = make_float2(-x1.x * h, x1.y * h);
+      } else {
+        t.grid[0][g] = make_float2(x1.x * h, x1.y * h);
+        t.grid[1][g] = make_float2(x0.x * h, -x0.y * h);
+      }
+    }
+  }
+}
+
+hipError_t pdsch_tx_launch(const PdschTx* d_items, uint32_t nitems, uint32_t max_nre, hipStream_t stream)
+{
+  if (nitems == 0 || max_nre == 0) {
+    return hipSuccess;
+  }
+  hipError_t e = gold_tables_init();
+  if (e != hipSuccess) {
+    return e;
+  }
+  const dim3 grid((max_nre + LLR_THREADS * TX_SPT - 1) / (LLR_THREADS * TX_SPT), nitems);
+  hipLaunchKernelGGL(pdsch_tx_kernel, grid, dim3(LLR_THREADS), 0, stream, d_items);
+  return hipGetLastError();
+}
+
+// cell-specific reference signals of 1 or 2 ports (refsignal_dl.c, 36.211 6.10.1): grid (CRS symbol of
+// the subframe, port, subframe); 2 * nof_prb pilots a symbol
+__global__ __launch_bounds__(256) void crs_put_kernel(float2* __restrict__ grids, uint32_t nof_prb, uint32_t cell_id,
+                                                      uint32_t nports, const uint32_t* __restrict__ sf_idx)
+{
+  const uint32_t sym = blockIdx.x, port = blockIdx.y, sf = blockIdx.z;  // sym: 0..3 -> (slot, l in {0, 4})
+  const uint32_t slot = sym >> 1, l = (sym & 1) ? 4u : 0u;
+  const uint32_t ns   = 2 * sf_idx[sf] + slot;
+  const uint32_t v    = port == 0 ? (l == 0 ? 0u : 3u) : (l == 0 ? 3u : 0u);
+  const uint32_t seed = (1u << 10) * (7 * (ns + 1) + l + 1) * (2 * cell_id + 1) + 2 * cell_id + 1;
+  const uint32_t nre  = 12 * nof_prb;
+  float2*        row  = grids + (((size_t)sf * nports + port) * 14 + 7 * slot + l) * nre;
+  for (uint32_t m = threadIdx.x; m < 2 * nof_prb; m += 256) {
+    const uint32_t mp = m + 110 - nof_prb;
+    uint32_t       x1, x2;
+    gold_at(seed, 2 * mp, x1, x2);
+    const uint32_t c  = gold16(x1, x2);
+    const float    r  = (float)0.70710678118654752440;
+    row[6 * m + (v + cell_id % 6) % 6] = make_float2((c & 1u) ? -r : r, (c & 2u) ? -r : r);
+  }
+}
+
+hipError_t crs_put_launch(float2* d_grids, uint32_t nof_prb, uint32_t cell_id, uint32_t nports, const uint32_t* d_sf_idx,
+                          uint32_t nsf, hipStream_t stream)
+{
+  if (nsf == 0) {
+    return hipSuccess;
+  }
+  if (nports == 0 || nports > 2) {
+    return hipErrorInvalidValue;
+  }
+  hipError_t e = gold_tables_init();
+  if (e != hipSuccess) {
+    return e;
+  }
+  hipLaunchKernelGGL(crs_put_kernel, dim3(4, nports, nsf), dim3(256), 0, stream, d_grids, nof_prb, cell_id, nports,
+                     d_sf_idx);
+  return hipGetLastError();
+}
+
 }  // namespace srsran_amd

@@ -302,4 +302,44 @@ void srsran_cfo_correct(srsran_cfo_t* h, const cf_t* input, cf_t* output, float 
   h->last_freq = freq;
 }
 
+
+// ---------------- modulator (ofdm.c:585-690), srsran_enb_dl's configuration ----------------
+int srsran_ofdm_tx_init_cfg(srsran_ofdm_t* q, srsran_ofdm_cfg_t* cfg)
+{
+  return srsran_ofdm_rx_init_cfg(q, cfg);  // same plan, twiddles and object; the direction is per call
+}
+
+void srsran_ofdm_tx_free(srsran_ofdm_t* q) { srsran_ofdm_rx_free(q); }
+
+int srsran_ofdm_tx_gpu(srsran_ofdm_t* q, const cf_t* d_in, cf_t* d_out, uint32_t nof_ports, uint32_t nof_sf, float scale,
+                       void* stream)
+{
+  if (!q || !q->gpu || !d_in || !d_out || nof_ports == 0 || nof_ports > 4 || nof_sf == 0) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  OfdmArgs a = ((OfdmGpu*)q->gpu)->proto;  // proto.norm = 1 / sqrt(N) when normalising, else 1
+  a.in       = (const float2*)d_in;
+  a.out      = (float2*)d_out;
+  a.nrx      = nof_ports;
+  a.norm     = a.norm * scale;
+  return ofdm_tx_launch(a, nof_sf, (hipStream_t)stream) == hipSuccess ? SRSRAN_SUCCESS : SRSRAN_ERROR;
+}
+
+void srsran_ofdm_tx_sf(srsran_ofdm_t* q)
+{
+  if (!q || !q->gpu || !q->cfg.in_buffer || !q->cfg.out_buffer) {
+    return;
+  }
+  OfdmGpu*     g  = (OfdmGpu*)q->gpu;
+  const size_t ni = 14 * (size_t)q->nof_re, no = q->sf_sz;
+  if (!grow((void**)&g->d_in, &g->in_cap, ni * sizeof(cf_t)) || !grow((void**)&g->d_out, &g->out_cap, no * sizeof(cf_t))) {
+    return;
+  }
+  hipMemcpyAsync(g->d_in, q->cfg.in_buffer, ni * sizeof(cf_t), hipMemcpyHostToDevice, g->stream);
+  if (srsran_ofdm_tx_gpu(q, (const cf_t*)g->d_in, (cf_t*)g->d_out, 1, 1, 1.0f, g->stream) == SRSRAN_SUCCESS) {
+    hipMemcpyAsync(q->cfg.out_buffer, g->d_out, no * sizeof(cf_t), hipMemcpyDeviceToHost, g->stream);
+  }
+  hipStreamSynchronize(g->stream);
+}
+
 }  // extern "C"

@@ -28,6 +28,10 @@ struct OfdmArgs {
 // grid: (14, nrx, nsf) workgroups
 hipError_t ofdm_rx_launch(const OfdmArgs& a, uint32_t nsf, hipStream_t stream);
 
+// modulator: in = grid [sf][port][14][nre], out = samples [sf][port][sf_len], nrx = ports, norm = scale;
+// grid (14, ports, nsf) workgroups
+hipError_t ofdm_tx_launch(const OfdmArgs& a, uint32_t nsf, hipStream_t stream);
+
 // factor N into radices 8/4/3/2 (largest first); returns the number of stages or -1
 int ofdm_plan(uint32_t N, int* radix);
 int ofdm_plan(uint32_t N, int* radix, uint32_t* ns_magic);

@@ -160,6 +160,67 @@ __global__ __launch_bounds__(OFDM_THREADS) void ofdm_rx_kernel(OfdmArgs a)
   }
 }
 
+// OFDM modulator (ofdm_tx_slot, ofdm.c:585-674, as srsran_enb_dl configures it: no normalisation,
+// DC left empty, no frequency shift): the nre subcarriers go to bins 1.. nre/2 (upper half of the
+// grid) and N - nre/2 .. N-1 (lower half), a backward DFT computed as conj(FFT(conj(X))) with the
+// receiver's Stockham stages, then the cyclic prefix.  in: [sf][port][14][nre], out: [sf][port][sf_len];
+// a.norm scales the grid first (srsran_enb_dl_gen_signal's 0.05 / sqrt(nof_prb)).
+__global__ __launch_bounds__(OFDM_THREADS) void ofdm_tx_kernel(OfdmArgs a)
+{
+  __shared__ float2 buf[2][OFDM_MAX_N];
+  const uint32_t    sym = blockIdx.x, port = blockIdx.y, sf = blockIdx.z;
+  const uint32_t    N = a.N, slot = sym / 7, i = sym % 7, half = a.nre / 2;
+  const float2*     src = a.in + (((size_t)sf * a.nrx + port) * 14 + sym) * a.nre;
+  for (uint32_t n = threadIdx.x; n < N; n += OFDM_THREADS) {
+    buf[0][n] = make_float2(0.f, 0.f);
+  }
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < a.nre; k += OFDM_THREADS) {
+    const uint32_t bin = k < half ? N - half + k : k - half + 1;
+    const float2   v   = src[k];
+    buf[0][bin]        = make_float2(v.x * a.norm, -(v.y * a.norm));
+  }
+  __syncthreads();
+  uint32_t Ns = 1, cur = 0;
+  for (int st = 0; st < a.nstages; st++) {
+    const int      R   = a.radix[st];
+    const uint32_t mNs = a.ns_magic[st];
+    if (R == 8) {
+      stage<8>(buf[cur], buf[cur ^ 1], a.tw, N, Ns, mNs);
+    } else if (R == 4) {
+      stage<4>(buf[cur], buf[cur ^ 1], a.tw, N, Ns, mNs);
+    } else if (R == 3) {
+      stage<3>(buf[cur], buf[cur ^ 1], a.tw, N, Ns, mNs);
+    } else {
+      stage<2>(buf[cur], buf[cur ^ 1], a.tw, N, Ns, mNs);
+    }
+    Ns *= (uint32_t)R;
+    cur ^= 1;
+    __syncthreads();
+  }
+  const uint32_t slot_sz = 7 * N + a.cp0 + 6 * a.cp;
+  const uint32_t off     = slot * slot_sz + a.cp0 + i * (N + a.cp);
+  const uint32_t cpl     = i == 0 ? a.cp0 : a.cp;
+  float2*        dst     = a.out + ((size_t)sf * a.nrx + port) * a.sf_len;
+  for (uint32_t n = threadIdx.x; n < N; n += OFDM_THREADS) {
+    const float2 v = buf[cur][n];
+    const float2 x = make_float2(v.x, -v.y);
+    dst[off + n]   = x;
+    if (n >= N - cpl) {
+      dst[off - cpl + (n - (N - cpl))] = x;
+    }
+  }
+}
+
+hipError_t ofdm_tx_launch(const OfdmArgs& a, uint32_t nsf, hipStream_t stream)
+{
+  if (a.N > OFDM_MAX_N || a.nstages <= 0 || nsf == 0) {
+    return hipErrorInvalidValue;
+  }
+  hipLaunchKernelGGL(ofdm_tx_kernel, dim3(14, a.nrx, nsf), dim3(OFDM_THREADS), 0, stream, a);
+  return hipGetLastError();
+}
+
 int ofdm_plan(uint32_t N, int* radix, uint32_t* ns_magic)
 {
   const int n = ofdm_plan(N, radix);

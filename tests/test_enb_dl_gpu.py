@@ -1,0 +1,105 @@
+"""eNB downlink transmit on the GPU: srsran_enb_dl_gpu_tx_batch (DL-SCH encode,
+CRS, scrambling + modulation + precoding + RE mapping, OFDM modulator) against the independent
+CPU transmitter synth/synth.py (36.211 / 36.212 restated; its encoder equals the oracle's) sample
+for sample, for CDD 2x2 (C3), transmit diversity and one port, several subframe indices (PSS / SSS /
+PBCH holes) and CFIs; then the GPU receive chain decodes what the GPU transmitted."""
+import numpy as np
+import pytest
+
+from synth import synth as SY
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    from srsran_4g_amd import tdec
+    if not tdec.gpu_available():
+        pytest.skip("no HIP device")
+    import torch
+    return torch
+
+
+CASES = [  # (nof_prb, nports, scheme, ntb, Qm, tbs, tti, cfi)
+    (100, 2, "cdd", 2, 6, 75376, 3, 1),
+    (100, 2, "cdd", 2, 6, 75376, 0, 2),
+    (50, 2, "diversity", 1, 4, 12216, 5, 2),
+    (25, 1, "port0", 1, 2, 2216, 7, 3),
+    (6, 1, "port0", 1, 4, 1160, 2, 2),
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[f"{c[2]}_{c[0]}prb_sf{c[6]}_cfi{c[7]}" for c in CASES])
+def test_tx_matches_cpu_transmitter(gpu, case):
+    torch = gpu
+    from srsran_4g_amd import enb_dl as E
+    from srsran_4g_amd import ue_dl as U
+    nprb, P, scheme, ntb, Qm, tbs, tti, cfi = case
+    cell_id, rnti = 37, 0x4601
+    U.use_standard_symbol_size(True)
+    N = SY.symbol_sz(nprb)
+    mask = SY.pdsch_mask(nprb, P, cell_id, cfi, tti % 10)
+    nre = int(mask.sum())
+    rng = np.random.default_rng(tbs + tti)
+    payloads = [rng.integers(0, 256, tbs // 8, dtype=np.uint8) for _ in range(ntb)]
+    want, _ = SY.pdsch_subframe(nprb, cell_id, P, tti, cfi, rnti, tbs, Qm, 0, payloads, scheme=scheme, nrx=P,
+                                N=N, channel=np.eye(P), pcfich=False)
+    cell = U.cell(nprb, P, cell_id)
+    enb = E.EnbDl(cell)
+    cfg = U.pdsch_cfg(nprb, nre, [tbs] * ntb, [Qm] * ntb, scheme=scheme, rnti=rnti)
+    d_pl = [torch.from_numpy(p).cuda() for p in payloads]
+    sf_len = want.shape[1]
+    d_out = torch.zeros((P, sf_len, 2), dtype=torch.float32, device="cuda")
+    assert enb.tx_batch([(tti, cfi, cfg, [p.data_ptr() for p in d_pl])], d_out.data_ptr(), 1.0 / N) == 0
+    torch.cuda.synchronize()
+    got = d_out.cpu().numpy().view(np.complex64)[..., 0]
+    scale = np.abs(want).max()
+    assert np.abs(got - want).max() < 2e-5 * scale * np.sqrt(np.log2(N)), np.abs(got - want).max() / scale
+    enb.free()
+
+
+def test_gpu_tx_to_gpu_rx(gpu):
+    """C3 subframes from the GPU transmitter (reference amplitude 0.05 / sqrt(N_RB)) through the
+    phy_dl_test channel [[1, 1], [1, -1]] into the GPU UE DL batch chain: every TB decodes"""
+    torch = gpu
+    from srsran_4g_amd import enb_dl as E
+    from srsran_4g_amd import sch as S
+    from srsran_4g_amd import ue_dl as U
+    nprb, P, Qm, tbs, cfi, cell_id, rnti = 100, 2, 6, 75376, 1, 11, 0x1234
+    U.use_standard_symbol_size(True)
+    ttis = [1, 2, 3, 4]
+    rng = np.random.default_rng(5)
+    cell = U.cell(nprb, P, cell_id)
+    enb = E.EnbDl(cell)
+    N = SY.symbol_sz(nprb)
+    sfs, keep, pls = [], [], []
+    for tti in ttis:
+        nre = int(SY.pdsch_mask(nprb, P, cell_id, cfi, tti % 10).sum())
+        p2 = [rng.integers(0, 256, tbs // 8, dtype=np.uint8) for _ in range(2)]
+        d = [torch.from_numpy(p).cuda() for p in p2]
+        cfg = U.pdsch_cfg(nprb, nre, [tbs] * 2, [Qm] * 2, scheme="cdd", rnti=rnti)
+        keep += d + [cfg]
+        pls.append(p2)
+        sfs.append((tti, cfi, cfg, [x.data_ptr() for x in d]))
+    sf_len = 2 * (7 * N + 160 * N // 2048 + 6 * (144 * N // 2048))
+    d_tx = torch.zeros((len(ttis), P, sf_len, 2), dtype=torch.float32, device="cuda")
+    assert enb.tx_batch(sfs, d_tx.data_ptr()) == 0
+    torch.cuda.synchronize()
+    tx = d_tx.cpu().numpy().view(np.complex64)[..., 0]
+    H = np.array([[1, 1], [1, -1]], np.complex64)
+    rx = np.einsum("rp,bps->brs", H, tx).astype(np.complex64)
+    # the host-synchronous UE DL path on each subframe
+    ue = U.UeDl(cell, 2)
+    for b, tti in enumerate(ttis):
+        nre = int(SY.pdsch_mask(nprb, P, cell_id, cfi, tti % 10).sum())
+        sbs = [S.SoftbufferRx(nof_prb=100) for _ in range(2)]
+        cfg = U.pdsch_cfg(nprb, nre, [tbs] * 2, [Qm] * 2, scheme="cdd", rnti=rnti, softbuffers=sbs)
+        ue.fft_estimate(list(rx[b]), tti, cfi)  # (no PCFICH is transmitted: the CFI is given below)
+        ret, res = ue.decode_pdsch(cfg, tti, cfi)
+        for cw in range(2):
+            ok, data = res[cw][0], res[cw][1]
+            assert ok and np.array_equal(data[:tbs // 8], pls[b][cw]), (tti, cw)
+        for sb in sbs:
+            sb.free()
+    ue.free()
+    enb.free()

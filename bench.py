@@ -433,15 +433,19 @@ def pusch_stage_bytes(nue, M, nsymb, ncell_re):
     }
 
 
-def run_pusch(args, torch, dist, world, rank, device):
+def run_pusch(args, torch, dist, world, rank, device, steps=None, warmup=None, cpu_seconds=None, emit=True):
     """eNB PUSCH receive: per step `subframes` UEs, each a 100-PRB 64QAM PUSCH (TBS 75376, 12
     SC-FDMA symbols, normal CP) in its own received subframe grid (device-resident), through
     srsran_pusch_gpu_decode_batch: DMRS estimation, MMSE equalisation + 1200-point inverse DFT,
     demap/descramble, channel de-interleaver, rate de-matching, turbo decoding with CRC early stop.
-    Value = decoded UL info Mbps; also UE-subframes/s."""
+    Value = decoded UL info Mbps; also UE-subframes/s.  emit=False: return the result (the default
+    all188 line embeds a summary) instead of printing it."""
     import ctypes
 
     from synth import pusch_tx as PT
+    steps = args.steps if steps is None else steps
+    warmup = args.warmup if warmup is None else warmup
+    cpu_seconds = args.cpu_seconds if cpu_seconds is None else cpu_seconds
     from srsran_4g_amd import prof
     from srsran_4g_amd import pusch as P
     from srsran_4g_amd import sch as S
@@ -496,14 +500,14 @@ def run_pusch(args, torch, dist, world, rank, device):
         if L_.srsran_pusch_gpu_decode_batch(ctypes.byref(pu.q), nue, arr, cres, res) != 0:
             raise RuntimeError("srsran_pusch_gpu_decode_batch failed")
 
-    elapsed = timed_region(step, args.steps, args.warmup, world, dist, torch.cuda.synchronize, device)
+    elapsed = timed_region(step, steps, warmup, world, dist, torch.cuda.synchronize, device)
     ok = np.array([bool(res[b].crc) and np.array_equal(datas[b][:C3_TBS // 8], pool[b % args.pool][2])
                    for b in range(nue)])
     avg = np.array([res[b].avg_iterations_block for b in range(nue)])
-    value = world * nue * C3_TBS * args.steps / elapsed / 1e6
+    value = world * nue * C3_TBS * steps / elapsed / 1e6
 
     prof.enable(True)
-    nrep = max(1, min(args.steps, 3))
+    nrep = max(1, min(steps, 3))
     for _ in range(nrep):
         step()
     torch.cuda.synchronize()
@@ -526,9 +530,9 @@ def run_pusch(args, torch, dist, world, rank, device):
         "value": round(value, 2),
         "unit": "Mbps",
         "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": round(elapsed / steps * 1e3, 3),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -538,7 +542,7 @@ def run_pusch(args, torch, dist, world, rank, device):
         "config": {
             "workload": f"pusch: {nue} UEs x (100 PRB, 64QAM, TBS {C3_TBS}, 12 SC-FDMA symbols, normal CP) per step, "
                         f"srsran_pusch_gpu_decode_batch, max {args.iters} half-its, CRC early stop, no UCI",
-            "ue_subframes_per_s": round(world * nue * args.steps / elapsed, 1),
+            "ue_subframes_per_s": round(world * nue * steps / elapsed, 1),
             "tb_ok_fraction": round(float(ok.mean()), 4),
             "avg_half_iterations": round(float(avg.mean()), 3),
             "parallelism": f"ue-sharded x{world}",
@@ -558,21 +562,23 @@ def run_pusch(args, torch, dist, world, rank, device):
                                    "avg_launch_ms": per_stage[k]["avg_launch_ms"]} for k in fe},
         "stages": per_stage,
     }
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        result["cpu_baseline"] = pusch_cpu_baseline(pool, cell_id, dm, rnti, args)
+    if rank == 0 and world == 1 and cpu_seconds > 0:
+        result["cpu_baseline"] = pusch_cpu_baseline(pool, cell_id, dm, rnti, args, cpu_seconds)
     elif rank == 0:
         result["cpu_baseline"] = None
     for sb in sbs:
         sb.free()
     pu.free()
     ch.free()
+    if not emit:
+        return result
     if world > 1:
         dist.destroy_process_group()
     if rank == 0:
         print(json.dumps(result), flush=True)
 
 
-def pusch_cpu_baseline(pool, cell_id, dm, rnti, args):
+def pusch_cpu_baseline(pool, cell_id, dm, rnti, args, budget_s):
     """The PUSCH chain on one host thread: the oracle's numpy estimator / equaliser / inverse FFT (FFTW
     and chest_ul.c are not buildable here) + the reference's compiled demapper, descrambler and
     decode_tb, over the same pool, for about args.cpu_seconds."""
@@ -585,7 +591,7 @@ def pusch_cpu_baseline(pool, cell_id, dm, rnti, args):
     ref = Reference()
     cell = make_cell(100, 1, cell_id)
     n, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < args.cpu_seconds:
+    while time.perf_counter() - t0 < budget_s:
         tti, grid, _ = pool[n % len(pool)]
         _, r = P.dmrs(cell, dm, 100, tti % 10, 0)
         est = po.chest(grid, 100, 0, 100, (0, 0), (0, 0), r)
@@ -1331,6 +1337,18 @@ def main():
             "chain_roofline_frac": round(pd["config"]["subframes_per_s"] * pd["chain_bytes_per_sf"]
                                          / (world * HBM_PEAK_GBS * 1e9), 5),
             "cpu_baseline": pd.get("cpu_baseline"),
+        }
+        # the uplink counterpart: the eNB PUSCH chain, summary only
+        pu = run_pusch(args, torch, dist, world, rank, device, steps=args.pdsch_steps, warmup=2,
+                       cpu_seconds=2.0 if args.cpu_seconds > 0 else 0, emit=False)
+        result["pusch"] = {
+            "workload": pu["config"]["workload"],
+            "ue_subframes_per_s": pu["config"]["ue_subframes_per_s"],
+            "mbps": pu["value"],
+            "ms_per_step": pu["ms_per_step"],
+            "tb_ok_fraction": pu["config"]["tb_ok_fraction"],
+            "front_end_roofline": pu["front_end_roofline"],
+            "cpu_baseline": pu.get("cpu_baseline"),
         }
 
     if world > 1:

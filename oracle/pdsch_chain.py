@@ -50,8 +50,9 @@ def fft_estimate(ora, samples, nof_prb, cell_id, nports, tti, cfo=0.0, N=None):
 
 def pdsch_decode(ora, grids, ce, noise, nof_prb, cell_id, nports, tti, cfi, rnti, tbs, Qm, rv, scheme="cdd",
                  pmi=0, max_iterations=8, csi_enable=True, power_scale=False, p_a=0.0, p_b=0, prb_mask=None,
-                 states=None):
-    """srsran_pdsch_decode for nof_tb = len(tbs) codewords (one layer each).
+                 states=None, layers=None):
+    """srsran_pdsch_decode for nof_tb = len(tbs) codewords (one layer each; layers=2 with one
+    codeword: SM / CDD on two layers, pdsch.c:838-863 + layermap.c:138-147, 236-260).
     Returns per codeword dict(ret, data, avg, llr)."""
     sf_idx = tti % 10
     lstart = cfi + (1 if nof_prb < 10 else 0)
@@ -75,6 +76,11 @@ def pdsch_decode(ora, grids, ce, noise, nof_prb, cell_id, nports, tti, cfi, rnti
         xl, csi = ora.predecode(1, y, h, 2, codebook, scaling, noise)
         x = np.empty((1, 2 * xl.shape[1]), np.complex64)
         x[0, 0::2], x[0, 1::2] = xl[0], xl[1]
+    elif layers == 2 and ntb == 1:  # predecode 2 layers; demap n/2 layer symbols each; CSI of layer 0
+        xl, csi = ora.predecode(SCHEME[scheme], y, h, 2, codebook, scaling, noise)
+        n = xl.shape[1]
+        x = np.zeros((1, n), np.complex64)
+        x[0, 0:2 * (n // 2):2], x[0, 1:2 * (n // 2):2] = xl[0, :n // 2], xl[1, :n // 2]
     else:
         x, csi = ora.predecode(SCHEME[scheme], y, h, ntb, codebook, scaling, noise)
     out = []
@@ -84,7 +90,7 @@ def pdsch_decode(ora, grids, ce, noise, nof_prb, cell_id, nports, tti, cfi, rnti
         if csi_enable:
             llr = ora.csi_correction(MOD[Qm[q]], csi[q], llr)
         st = states[q] if states else None
-        nl = 2 if scheme == "diversity" else 1  # srsran_dlsch_decode2: Nl = 2 when layers != TBs (sch.c:587-590)
+        nl = 2 if (scheme == "diversity" or layers == 2) and ntb == 1 else 1  # Nl = 2 when layers != TBs (sch.c:587-590)
         ret, data, noi, avg, state = ora.dlsch_decode(tbs[q], Qm[q] * nl, rv[q], llr, max_iterations, st)
         out.append(dict(ret=ret, data=data, avg=avg, llr=llr, state=state, nof_re=idx.size))
     return out

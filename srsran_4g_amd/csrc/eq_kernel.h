@@ -23,7 +23,8 @@ struct PredArgs {
   uint32_t        ce_row;    // > 0: h[p][r] is one AVERAGE row, indexed by (grid index % ce_row)
   const float*    noise_ptr; // device noise estimate (overrides `noise`)
   float           rho_b_inv; // y scale on CRS-bearing symbols (bit 31 of idx), 1 = none
-  int             interleave; // DIVERSITY: write the codeword (layer-demapped) into x[0]
+  int             interleave; // DIVERSITY: write the codeword (layer-demapped) into x[0]; 2: SM / CDD
+                              // with one codeword on 2 layers: d[2k + l] = x_l[k], k < n / 2, into x[0]
 };
 
 hipError_t predecode_launch(const PredArgs& a, hipStream_t stream);

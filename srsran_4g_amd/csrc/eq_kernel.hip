@@ -235,9 +235,16 @@ __device__ __forceinline__ void predecode_item(const PredArgs& a, uint32_t k, ui
     float c0, c1;
     mmse_csi(Y(0), Y(1), h00, h01, h10, h11, x0, x1, c0, c1, noise, a.norm);
     if (valid) {
-      a.x[0][k]   = make_float2(x0.r, x0.i);
-      a.x[1][k]   = make_float2(x1.r, x1.i);
-      a.csi[0][k] = c0;
+      if (a.interleave == 2) {  // one codeword on both layers: srsran_layerdemap_multiplex -> _diversity
+        if (k < a.n / 2) {      // (layermap.c:138-147) over n/2 layer symbols (pdsch.c:862-863)
+          a.x[0][2 * k]     = make_float2(x0.r, x0.i);
+          a.x[0][2 * k + 1] = make_float2(x1.r, x1.i);
+        }
+      } else {
+        a.x[0][k] = make_float2(x0.r, x0.i);
+        a.x[1][k] = make_float2(x1.r, x1.i);
+      }
+      a.csi[0][k] = c0;  // not layer-demapped: the codeword's CSI correction reads layer 0's (pdsch.c:530)
       a.csi[1][k] = c1;
     }
     if (valid) {

@@ -150,7 +150,12 @@ int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sf
       return SRSRAN_ERROR_OUT_OF_BOUNDS;
     }
     const bool txd = gr.tx_scheme == SRSRAN_TXSCHEME_DIVERSITY;
-    if (txd ? (gr.nof_tb != 1 || gr.nof_layers != 2) : (gr.nof_layers != gr.nof_tb || gr.nof_tb < 1 || gr.nof_tb > 2)) {
+    // one codeword on two layers (SM / CDD, 36.211 Table 6.3.3.2-1): predecode both layers, then
+    // srsran_layerdemap_type as the reference runs it (pdsch.c:838-863)
+    const bool cw1l2 = !txd && gr.nof_tb == 1 && gr.nof_layers == 2 &&
+                       (gr.tx_scheme == SRSRAN_TXSCHEME_SPATIALMUX || gr.tx_scheme == SRSRAN_TXSCHEME_CDD);
+    if (txd ? (gr.nof_tb != 1 || gr.nof_layers != 2)
+            : (!cw1l2 && (gr.nof_layers != gr.nof_tb || gr.nof_tb < 1 || gr.nof_tb > 2))) {
       fprintf(stderr, "[srsran_pdsch] unsupported: %u codewords on %u layers\n", gr.nof_tb, gr.nof_layers);
       return SRSRAN_ERROR;
     }
@@ -189,7 +194,7 @@ int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sf
       return SRSRAN_ERROR;
     }
     a.n          = gr.nof_re;
-    a.interleave = txd ? 1 : 0;  // srsran_layerdemap_diversity fused into the predecoder
+    a.interleave = txd ? 1 : cw1l2 ? 2 : 0;  // the layer demapping fused into the predecoder
     a.noise     = f.cfg->decoder_type == SRSRAN_MIMO_DECODER_ZF ? 0.0f : f.noise;
     a.noise_ptr = f.cfg->decoder_type == SRSRAN_MIMO_DECODER_ZF ? nullptr : f.d_noise;
     a.rho_b_inv = rho_b_inv;

@@ -273,3 +273,53 @@ def test_ue_dl_reference_default_rates(U, SCH, ora, nof_prb, N, tbs, cell_id):
             sb.free()
     finally:
         U.use_standard_symbol_size(True)
+
+
+@pytest.mark.parametrize("scheme,pmi,snr", [("sm", 0, 30.0), ("sm", 1, 30.0), ("cdd", 0, 30.0), ("cdd", 0, 9.0)])
+def test_pdsch_one_codeword_two_layers(U, SCH, ora, scheme, pmi, snr):
+    """one TB on two layers (SM codebook pmi / CDD): the predecoder's two layers are layer-demapped
+    over n/2 layer symbols (srsran_layerdemap_type, pdsch.c:838-863) and the codeword's CSI
+    correction reads layer 0's CSI, as the reference does; frequency-domain grids and exact estimates
+    fed to both the GPU and the oracle chain: return, payload and iterations equal"""
+    rng = np.random.default_rng(31 + pmi + int(snr))
+    nof_prb, cell_id, nports, tti, cfi = 100, 5, 2, 2, 1
+    mask = S.pdsch_mask(nof_prb, nports, cell_id, cfi, tti % 10)
+    nre = int(mask.sum())
+    pl = rng.integers(0, 256, TBS // 8, dtype=np.uint8)
+    G = nre * 6
+    e = S.dlsch_encode(TBS, 6, 0, G, pl, Nl=2)
+    d = S.modulate(e ^ S.gold(S.pdsch_seed(0x1234, 0, 2 * (tti % 10), cell_id), G), 6)
+    half = nre // 2
+    ports = S.precode([d[0:2 * half:2], d[1:2 * half:2]], scheme, codebook=pmi)
+    H = (rng.standard_normal((2, 2)) + 1j * rng.standard_normal((2, 2))) / np.sqrt(2) + np.eye(2)
+    grids = np.zeros((2, 14 * 12 * nof_prb), np.complex128)
+    for p in range(nports):
+        g = S.crs_grid(cell_id, nof_prb, nports, p, tti % 10)
+        v = np.zeros(nre, np.complex128)
+        v[:half] = ports[p]  # the layer symbols fill the first n/2 PDSCH REs (the precoder's length)
+        g[mask] = v
+        for r in range(2):
+            grids[r] += H[r, p] * g.reshape(-1)
+    sd = np.sqrt(np.mean(np.abs(grids) ** 2) / 10 ** (snr / 10) / 2)
+    grids = (grids + sd * (rng.standard_normal(grids.shape) + 1j * rng.standard_normal(grids.shape))).astype(np.complex64)
+    ce = np.zeros((nports, 2, grids.shape[1]), np.complex64)
+    for p in range(nports):
+        for r in range(2):
+            ce[p, r] = H[r, p]
+    noise = float(2 * sd * sd)
+    ref = PC.pdsch_decode(ora, grids, ce, noise, nof_prb, cell_id, nports, tti, cfi, 0x1234, [TBS], [6], [0],
+                          scheme=scheme, pmi=pmi, layers=2)
+    sb = SCH.SoftbufferRx(nof_prb=nof_prb)
+    cfg = U.pdsch_cfg(nof_prb, nre, [TBS], [6], scheme=scheme, pmi=pmi, softbuffers=[sb])
+    cfg.grant.nof_layers = 2
+    pd = U.Pdsch(U.cell(nof_prb, nports, cell_id), 2)
+    ret, out = pd.decode(cfg, tti, cfi, grids, ce, noise)
+    assert ret == 0
+    crc, payload, avg = out[0]
+    assert crc == (ref[0]["ret"] == 0)
+    assert np.array_equal(payload[:TBS // 8 + 6], ref[0]["data"][:TBS // 8 + 6])
+    assert avg == pytest.approx(ref[0]["avg"], abs=1e-6)
+    if snr > 20:
+        assert crc and np.array_equal(payload[:TBS // 8], pl)
+    pd.free()
+    sb.free()

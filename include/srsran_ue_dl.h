@@ -257,6 +257,16 @@ typedef struct {
 } srsran_pdsch_res_t;
 
 int  srsran_pdsch_init_ue(srsran_pdsch_t* q, uint32_t max_prb, uint32_t nof_rx_antennas);
+/* eNB side (pdsch.c:302-310, 1015-1120): srsran_pdsch_encode writes the PDSCH REs of the ports'
+ * host grids (the rest is left as the caller put it: CRS, control channels).  PORT0 (1 port), TX
+ * diversity (2 ports, 1 TB), CDD (2 ports, 2 TBs); rho_a scaling (power_scale with p_a != 0) is not
+ * provided.  Runs on the GPU: DL-SCH encoding, scrambling, modulation, precoding, RE mapping. */
+int  srsran_pdsch_init_enb(srsran_pdsch_t* q, uint32_t max_prb);
+int  srsran_pdsch_encode(srsran_pdsch_t*     q,
+                         srsran_dl_sf_cfg_t* sf,
+                         srsran_pdsch_cfg_t* cfg,
+                         uint8_t*            data[SRSRAN_MAX_CODEWORDS],
+                         cf_t*               sf_symbols[SRSRAN_MAX_PORTS]);
 void srsran_pdsch_free(srsran_pdsch_t* q);
 int  srsran_pdsch_enable_coworker(srsran_pdsch_t* q); /* accepted, no effect */
 int  srsran_pdsch_set_cell(srsran_pdsch_t* q, srsran_cell_t cell);

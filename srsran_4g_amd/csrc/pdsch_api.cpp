@@ -505,4 +505,137 @@ int srsran_pdsch_gpu_decode_batch(srsran_pdsch_t*              q,
   return ret == SRSRAN_SUCCESS ? (int)tbs.size() : ret;
 }
 
+
+// ---------------- transmitter (pdsch.c:1015-1120, eNB side) ----------------
+int srsran_pdsch_init_enb(srsran_pdsch_t* q, uint32_t max_prb)
+{
+  const int r = srsran_pdsch_init_ue(q, max_prb, 1);
+  if (r == SRSRAN_SUCCESS) {
+    q->is_ue = false;
+  }
+  return r;
+}
+
+int srsran_pdsch_encode(srsran_pdsch_t*     q,
+                        srsran_dl_sf_cfg_t* sf,
+                        srsran_pdsch_cfg_t* cfg,
+                        uint8_t*            data[SRSRAN_MAX_CODEWORDS],
+                        cf_t*               sf_symbols[SRSRAN_MAX_PORTS])
+{
+  if (!q || !q->gpu || !sf || !cfg || !data || !sf_symbols) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  const srsran_cell_t&        cell = q->cell;
+  const srsran_pdsch_grant_t& gr   = cfg->grant;
+  const uint32_t              P    = cell.nof_ports;
+  for (uint32_t p = 0; p < P; p++) {
+    if (!sf_symbols[p]) {
+      return SRSRAN_ERROR_INVALID_INPUTS;
+    }
+  }
+  if (gr.nof_tb == 0) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  int scheme;
+  if (gr.tx_scheme == SRSRAN_TXSCHEME_PORT0 && P == 1 && gr.nof_tb == 1) {
+    scheme = 0;
+  } else if (gr.tx_scheme == SRSRAN_TXSCHEME_DIVERSITY && P == 2 && gr.nof_tb == 1) {
+    scheme = 1;
+  } else if (gr.tx_scheme == SRSRAN_TXSCHEME_CDD && P == 2 && gr.nof_tb == 2 && gr.nof_layers == 2) {
+    scheme = 3;
+  } else {
+    fprintf(stderr, "[srsran_pdsch] encode: scheme %d with %u ports / %u TBs is not provided\n", (int)gr.tx_scheme, P,
+            gr.nof_tb);
+    return SRSRAN_ERROR;
+  }
+  if (cfg->power_scale && cfg->p_a != 0.0f) {
+    fprintf(stderr, "[srsran_pdsch] encode: rho_a scaling is not provided\n");
+    return SRSRAN_ERROR;
+  }
+  PdschGpu*             g      = (PdschGpu*)q->gpu;
+  const uint32_t        lstart = sf->cfi + (cell.nof_prb < 10 ? 1 : 0);
+  std::vector<uint32_t> tab    = pdsch_re_table(cell, gr, lstart, sf->tti % 10);
+  const uint32_t        nre = (uint32_t)tab.size(), nsf_re = 14 * 12 * cell.nof_prb;
+  if (nre != gr.nof_re || nre > q->max_re) {
+    fprintf(stderr, "[srsran_pdsch] Error expecting %u symbols but got %u\n", gr.nof_re, nre);
+    return SRSRAN_ERROR;
+  }
+  // device scratch: grids, RE table, payloads, packed e bits, descriptor
+  PdschTx                             it;
+  std::vector<srsran_dlsch_gpu_enc_t> enc;
+  memset(&it, 0, sizeof(it));
+  it.nre       = nre;
+  it.scheme    = scheme;
+  it.scaling   = 1.0f;
+  it.div_scale = (float)(1.0 * 0.70710678118654752440);
+  size_t   off = align256((size_t)P * nsf_re * sizeof(float2));
+  size_t   o_idx = off;
+  off += align256((size_t)nre * sizeof(uint32_t));
+  size_t   o_item = off;
+  off += align256(sizeof(PdschTx));
+  std::vector<size_t> o_data, o_e;
+  uint32_t            cw = 0;
+  for (uint32_t t = 0; t < SRSRAN_MAX_CODEWORDS; t++) {
+    const srsran_ra_tb_t& tb = gr.tb[t];
+    if (!tb.enabled) {
+      continue;
+    }
+    const uint32_t Qm = srsran_mod_bits_x_symbol(tb.mod), Nl = gr.nof_layers != gr.nof_tb ? 2 : 1;
+    if (!data[t] || Qm == 0 || tb.tbs <= 0 || tb.nof_bits != nre * Qm || cw >= 2) {
+      return SRSRAN_ERROR_INVALID_INPUTS;
+    }
+    o_data.push_back(off);
+    off += align256((size_t)tb.tbs / 8);
+    o_e.push_back(off);
+    off += align256((tb.nof_bits + 7) / 8);
+    enc.push_back({(uint32_t)tb.tbs, Qm * Nl, (uint32_t)tb.rv, tb.nof_bits, nullptr, nullptr});
+    it.seed[cw] = pdsch_seed(cfg->rnti, (int)tb.cw_idx, 2 * (sf->tti % 10), cell.id);
+    it.mod[cw]  = (int)tb.mod;
+    cw++;
+  }
+  if ((scheme == 3) != (cw == 2) || !grow_dev((void**)&g->d_work, &g->work_cap, off)) {
+    return SRSRAN_ERROR;
+  }
+  char* base = g->d_work;
+  for (uint32_t p = 0; p < P; p++) {
+    it.grid[p] = (float2*)base + (size_t)p * nsf_re;
+  }
+  it.idx = (const uint32_t*)(base + o_idx);
+  cw     = 0;
+  for (uint32_t t = 0; t < SRSRAN_MAX_CODEWORDS; t++) {
+    if (!gr.tb[t].enabled) {
+      continue;
+    }
+    enc[cw].d_data   = (const uint8_t*)(base + o_data[cw]);
+    enc[cw].d_e_bits = (uint8_t*)(base + o_e[cw]);
+    it.e[cw]         = (const uint8_t*)(base + o_e[cw]);
+    if (hipMemcpyAsync(base + o_data[cw], data[t], (size_t)gr.tb[t].tbs / 8, hipMemcpyHostToDevice, g->stream) !=
+        hipSuccess) {
+      return SRSRAN_ERROR;
+    }
+    cw++;
+  }
+  // the ports' grids keep what the caller already put there (CRS, control): only PDSCH REs change
+  for (uint32_t p = 0; p < P; p++) {
+    if (hipMemcpyAsync(it.grid[p], sf_symbols[p], nsf_re * sizeof(float2), hipMemcpyHostToDevice, g->stream) !=
+        hipSuccess) {
+      return SRSRAN_ERROR;
+    }
+  }
+  if (hipMemcpyAsync(base + o_idx, tab.data(), nre * sizeof(uint32_t), hipMemcpyHostToDevice, g->stream) !=
+          hipSuccess ||
+      hipMemcpyAsync(base + o_item, &it, sizeof(it), hipMemcpyHostToDevice, g->stream) != hipSuccess ||
+      srsran_dlsch_gpu_encode_batch(&q->dl_sch, cw, enc.data(), g->stream) != SRSRAN_SUCCESS ||
+      pdsch_tx_launch((const PdschTx*)(base + o_item), 1, nre, g->stream) != hipSuccess) {
+    return SRSRAN_ERROR;
+  }
+  for (uint32_t p = 0; p < P; p++) {
+    if (hipMemcpyAsync(sf_symbols[p], it.grid[p], nsf_re * sizeof(float2), hipMemcpyDeviceToHost, g->stream) !=
+        hipSuccess) {
+      return SRSRAN_ERROR;
+    }
+  }
+  return hipStreamSynchronize(g->stream) == hipSuccess ? SRSRAN_SUCCESS : SRSRAN_ERROR;
+}
+
 }  // extern "C"

@@ -152,6 +152,9 @@ def lib():
             "srsran_chest_dl_gpu_estimate_batch": ([CH, P, u32, P, ctypes.c_size_t, P, ctypes.c_size_t, P, P],
                                                    ctypes.c_int),
             "srsran_pdsch_init_ue": ([PD, u32, u32], ctypes.c_int),
+            "srsran_pdsch_init_enb": ([PD, u32], ctypes.c_int),
+            "srsran_pdsch_encode": ([PD, ctypes.POINTER(srsran_dl_sf_cfg_t), ctypes.POINTER(srsran_pdsch_cfg_t),
+                                     ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
             "srsran_pdsch_free": ([PD], None),
             "srsran_pdsch_set_cell": ([PD, srsran_cell_t], ctypes.c_int),
             "srsran_pdsch_enable_coworker": ([PD], ctypes.c_int),
@@ -348,6 +351,18 @@ class Pdsch:
             raise RuntimeError("srsran_pdsch_set_cell failed")
         self.cell = cell_
         self.nrx = nof_rx
+
+    def encode(self, cfg, tti, cfi, payloads, grids):
+        """srsran_pdsch_encode into (a copy of) the ports' host grids -> (ret, grids)"""
+        g = [np.array(x, np.complex64, copy=True) for x in grids]
+        gp = (ctypes.c_void_p * MAX_PORTS)(*[x.ctypes.data for x in g] + [None] * (MAX_PORTS - len(g)))
+        pl = [np.ascontiguousarray(p, np.uint8) for p in payloads]
+        dp = (ctypes.c_void_p * 2)(*[p.ctypes.data for p in pl] + [None] * (2 - len(pl)))
+        sf = srsran_dl_sf_cfg_t()
+        sf.tti, sf.cfi = tti, cfi
+        ret = lib().srsran_pdsch_encode(ctypes.byref(self.q), ctypes.byref(sf), ctypes.byref(cfg), ctypes.addressof(dp),
+                                        ctypes.addressof(gp))
+        return ret, g
 
     def decode(self, cfg, tti, cfi, grids, ce, noise, acked=(False, False)):
         """srsran_pdsch_decode on host grids (nrx, n) and full estimates (nports, nrx, n).

@@ -103,3 +103,39 @@ def test_gpu_tx_to_gpu_rx(gpu):
             sb.free()
     ue.free()
     enb.free()
+
+
+@pytest.mark.parametrize("scheme,P,ntb,Qm,tbs,tti,cfi", [("cdd", 2, 2, 6, 75376, 1, 1), ("diversity", 2, 1, 4, 12216, 5, 2),
+                                                       ("port0", 1, 1, 2, 2216, 0, 3)])
+def test_pdsch_encode_host_grids(gpu, scheme, P, ntb, Qm, tbs, tti, cfi):
+    """srsran_pdsch_encode (eNB, host grids): the PDSCH REs equal the CPU transmitter's precoded
+    symbols, every other RE (here the CRS already put) is left as it was"""
+    from srsran_4g_amd import ue_dl as U
+    nprb = 100 if scheme == "cdd" else 50 if scheme == "diversity" else 25
+    cell_id, rnti = 21, 0x3311
+    mask = SY.pdsch_mask(nprb, P, cell_id, cfi, tti % 10)
+    nre = int(mask.sum())
+    rng = np.random.default_rng(tti + tbs)
+    pls = [rng.integers(0, 256, tbs // 8, dtype=np.uint8) for _ in range(ntb)]
+    layers = []
+    for q, pl in enumerate(pls):
+        G = nre * Qm
+        e = SY.dlsch_encode(tbs, Qm, 0, G, pl, Nl=2 if scheme == "diversity" else 1)
+        layers.append(SY.modulate(e ^ SY.gold(SY.pdsch_seed(rnti, q, 2 * (tti % 10), cell_id), G), Qm))
+    ports = SY.precode(layers, scheme)
+    crs = [SY.crs_grid(cell_id, nprb, P, p, tti % 10) for p in range(P)]
+    want = []
+    for p in range(P):
+        g = crs[p].copy()
+        g[mask] = ports[p]
+        want.append(g.reshape(-1))
+    cell = U.cell(nprb, P, cell_id)
+    pd = U.Pdsch(cell, 1)
+    assert U.lib().srsran_pdsch_init_enb(__import__("ctypes").byref(pd.q), nprb) == 0
+    assert U.lib().srsran_pdsch_set_cell(__import__("ctypes").byref(pd.q), cell) == 0
+    cfg = U.pdsch_cfg(nprb, nre, [tbs] * ntb, [Qm] * ntb, scheme=scheme, rnti=rnti)
+    ret, got = pd.encode(cfg, tti, cfi, pls, [c.reshape(-1) for c in crs])
+    assert ret == 0
+    for p in range(P):
+        np.testing.assert_allclose(got[p], want[p], rtol=0, atol=2e-6)
+    pd.free()

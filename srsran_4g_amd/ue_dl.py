@@ -343,9 +343,12 @@ def pdsch_cfg(nof_prb, nof_re, tbs, Qm, rv=(0, 0), scheme="cdd", pmi=0, rnti=0x1
 class Pdsch:
     """srsran_pdsch_t (UE side)."""
 
-    def __init__(self, cell_, nof_rx):
+    def __init__(self, cell_, nof_rx, enb=False):
         self.q = srsran_pdsch_t()
-        if lib().srsran_pdsch_init_ue(ctypes.byref(self.q), cell_.nof_prb, nof_rx):
+        if enb:
+            if lib().srsran_pdsch_init_enb(ctypes.byref(self.q), cell_.nof_prb):
+                raise RuntimeError("srsran_pdsch_init_enb failed (no HIP device?)")
+        elif lib().srsran_pdsch_init_ue(ctypes.byref(self.q), cell_.nof_prb, nof_rx):
             raise RuntimeError("srsran_pdsch_init_ue failed (no HIP device?)")
         if lib().srsran_pdsch_set_cell(ctypes.byref(self.q), cell_):
             raise RuntimeError("srsran_pdsch_set_cell failed")

@@ -130,9 +130,7 @@ def test_pdsch_encode_host_grids(gpu, scheme, P, ntb, Qm, tbs, tti, cfi):
         g[mask] = ports[p]
         want.append(g.reshape(-1))
     cell = U.cell(nprb, P, cell_id)
-    pd = U.Pdsch(cell, 1)
-    assert U.lib().srsran_pdsch_init_enb(__import__("ctypes").byref(pd.q), nprb) == 0
-    assert U.lib().srsran_pdsch_set_cell(__import__("ctypes").byref(pd.q), cell) == 0
+    pd = U.Pdsch(cell, 1, enb=True)
     cfg = U.pdsch_cfg(nprb, nre, [tbs] * ntb, [Qm] * ntb, scheme=scheme, rnti=rnti)
     ret, got = pd.encode(cfg, tti, cfi, pls, [c.reshape(-1) for c in crs])
     assert ret == 0

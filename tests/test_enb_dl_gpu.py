@@ -106,7 +106,7 @@ def test_gpu_tx_to_gpu_rx(gpu):
 
 
 @pytest.mark.parametrize("scheme,P,ntb,Qm,tbs,tti,cfi", [("cdd", 2, 2, 6, 75376, 1, 1), ("diversity", 2, 1, 4, 12216, 5, 2),
-                                                       ("port0", 1, 1, 2, 2216, 0, 3)])
+                                                       ("port0", 1, 1, 2, 2216, 2, 3)])
 def test_pdsch_encode_host_grids(gpu, scheme, P, ntb, Qm, tbs, tti, cfi):
     """srsran_pdsch_encode (eNB, host grids): the PDSCH REs equal the CPU transmitter's precoded
     symbols, every other RE (here the CRS already put) is left as it was"""

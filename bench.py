@@ -554,12 +554,14 @@ def run_pusch(args, torch, dist, world, rank, device, steps=None, warmup=None, c
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5),
-            "traffic": None,
+            "traffic": pmc_traffic("pusch", "tdec_kernel<16, true>", nue) if dom == "tdec_kernel" else None,
             "avg_launch_ms": d["avg_launch_ms"],
             "algo_bytes_per_launch": int(bytes_per_launch),
         },
         "front_end_roofline": {k: {"GBps": per_stage[k]["GBps"], "frac": round(per_stage[k]["GBps"] / HBM_PEAK_GBS, 4),
-                                   "avg_launch_ms": per_stage[k]["avg_launch_ms"]} for k in fe},
+                                   "avg_launch_ms": per_stage[k]["avg_launch_ms"],
+                                   "algo_bytes_per_launch": sb_.get(k, 0),
+                                   "traffic": pmc_traffic("pusch", k, nue)} for k in fe},
         "stages": per_stage,
     }
     if rank == 0 and world == 1 and cpu_seconds > 0:

@@ -28,9 +28,14 @@ extern "C" {
 #define SRSRAN_MAX_LAYERS 4
 #define SRSRAN_NRE 12
 #define SRSRAN_CP_NORM_NSYMB 7
+#define SRSRAN_CP_EXT_NSYMB 6
 
 /* ---------------- phy_common.h ---------------- */
 typedef enum { SRSRAN_CP_NORM = 0, SRSRAN_CP_EXT } srsran_cp_t;
+#define SRSRAN_CP_ISNORM(cp) (cp == SRSRAN_CP_NORM)
+#define SRSRAN_CP_ISEXT(cp) (cp == SRSRAN_CP_EXT)
+#define SRSRAN_CP_NSYMB(cp) (SRSRAN_CP_ISNORM(cp) ? SRSRAN_CP_NORM_NSYMB : SRSRAN_CP_EXT_NSYMB)
+#define SRSRAN_SF_LEN_RE(nof_prb, cp) (2 * SRSRAN_CP_NSYMB(cp) * SRSRAN_NRE * (nof_prb))
 typedef enum { SRSRAN_PHICH_NORM = 0, SRSRAN_PHICH_EXT } srsran_phich_length_t;
 typedef enum { SRSRAN_PHICH_R_1_6 = 0, SRSRAN_PHICH_R_1_2, SRSRAN_PHICH_R_1, SRSRAN_PHICH_R_2 } srsran_phich_r_t;
 typedef enum { SRSRAN_FDD = 0, SRSRAN_TDD = 1 } srsran_frame_type_t;

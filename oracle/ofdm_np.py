@@ -3,7 +3,8 @@
 FFTW is not available here and no reference test pins its outputs, so the OFDM
 stage is checked against numpy's FFT (double precision) and by TX -> RX round trips:
   - symbol i of slot s occupies [s*slot + cp0 + i*(N + cp), +N) (ofdm.c:169-181, 36.211 6.12)
-  - cp0 = ceil(160 N / 2048), cp = ceil(144 N / 2048) (phy_common.h:125-127)
+  - cp0 = ceil(160 N / 2048), cp = ceil(144 N / 2048) (phy_common.h:125-127); extended CP
+    (cp=1): 6 symbols a slot, cp0 = cp = ceil(512 N / 2048) (SRSRAN_CP_LEN_EXT)
   - receiver: forward DFT, unnormalised, grid = [X[N-nre/2 ..], X[1 .. nre/2]] (ofdm.c:497-498)
   - transmitter: the inverse mapping with an IFFT scaled by 1/N, so rx(tx(grid)) == grid
   - CFO: z[n] = x[n] exp(j 2 pi f n), n from the subframe start (cfo.c:96-107)
@@ -13,25 +14,33 @@ import math
 import numpy as np
 
 
-def cp_lens(N):
+def nsymb(ext=0):
+    return 6 if ext else 7
+
+
+def cp_lens(N, ext=0):
+    if ext:
+        return math.ceil(512 * N / 2048), math.ceil(512 * N / 2048)
     return math.ceil(160 * N / 2048), math.ceil(144 * N / 2048)
 
 
-def sf_len(N):
-    cp0, cp = cp_lens(N)
-    return 2 * (7 * N + cp0 + 6 * cp)
+def sf_len(N, ext=0):
+    cp0, cp = cp_lens(N, ext)
+    ns = nsymb(ext)
+    return 2 * (ns * N + cp0 + (ns - 1) * cp)
 
 
-def symbol_starts(N):
-    cp0, cp = cp_lens(N)
-    slot = 7 * N + cp0 + 6 * cp
-    return [s * slot + cp0 + i * (N + cp) for s in range(2) for i in range(7)]
+def symbol_starts(N, ext=0):
+    cp0, cp = cp_lens(N, ext)
+    ns = nsymb(ext)
+    slot = ns * N + cp0 + (ns - 1) * cp
+    return [s * slot + cp0 + i * (N + cp) for s in range(2) for i in range(ns)]
 
 
-def ofdm_rx(x, N, nre, normalize=False):
+def ofdm_rx(x, N, nre, normalize=False, ext=0):
     x = np.asarray(x, np.complex128)
-    out = np.zeros((14, nre), np.complex128)
-    for l, st in enumerate(symbol_starts(N)):
+    out = np.zeros((2 * nsymb(ext), nre), np.complex128)
+    for l, st in enumerate(symbol_starts(N, ext)):
         X = np.fft.fft(x[st:st + N])
         out[l, : nre // 2] = X[N - nre // 2:]
         out[l, nre // 2:] = X[1: nre // 2 + 1]
@@ -40,16 +49,17 @@ def ofdm_rx(x, N, nre, normalize=False):
     return out.reshape(-1)
 
 
-def ofdm_tx(grid, N, nre):
-    grid = np.asarray(grid, np.complex128).reshape(14, nre)
-    cp0, cp = cp_lens(N)
-    x = np.zeros(sf_len(N), np.complex128)
-    for l, st in enumerate(symbol_starts(N)):
+def ofdm_tx(grid, N, nre, ext=0):
+    ns = nsymb(ext)
+    grid = np.asarray(grid, np.complex128).reshape(2 * ns, nre)
+    cp0, cp = cp_lens(N, ext)
+    x = np.zeros(sf_len(N, ext), np.complex128)
+    for l, st in enumerate(symbol_starts(N, ext)):
         X = np.zeros(N, np.complex128)
         X[N - nre // 2:] = grid[l, : nre // 2]
         X[1: nre // 2 + 1] = grid[l, nre // 2:]
         t = np.fft.ifft(X)
-        c = cp0 if l % 7 == 0 else cp
+        c = cp0 if l % ns == 0 else cp
         x[st - c: st] = t[N - c:]
         x[st: st + N] = t
     return x

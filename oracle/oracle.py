@@ -166,15 +166,17 @@ class Oracle(_Lib, _PhyMixin):
         n = g(f.ctypes.data, order, std)
         return f[:n]
 
-    def chest_dl(self, grids, nof_prb, cell_id, nports, sf_idx, symbol_sz):
-        """CRS channel estimate (srsUE defaults). grids: (nrx, 14*12*nof_prb) -> (ce (nports, nrx, n), stats)."""
+    def chest_dl(self, grids, nof_prb, cell_id, nports, sf_idx, symbol_sz, cp=0):
+        """CRS channel estimate (srsUE defaults). grids: (nrx, 2*nsymb*12*nof_prb), nsymb = 7 (cp 0) or
+        6 (cp 1, extended) -> (ce (nports, nrx, n), stats)."""
         grids = np.ascontiguousarray(grids, np.complex64)
         nrx, n = grids.shape
+        assert n == (12 if cp else 14) * 12 * nof_prb
         ce = np.zeros((nports, nrx, n), np.complex64)
         out = np.zeros(4, np.float32)
-        f = self.lib.oracle_chest_dl
-        f.argtypes = [ctypes.c_void_p] + [ctypes.c_uint32] * 6 + [ctypes.c_void_p, ctypes.c_void_p]
-        f(grids.ctypes.data, nof_prb, cell_id, nports, nrx, sf_idx, symbol_sz, ce.ctypes.data, out.ctypes.data)
+        f = self.lib.oracle_chest_dl_cp
+        f.argtypes = [ctypes.c_void_p] + [ctypes.c_uint32] * 7 + [ctypes.c_void_p, ctypes.c_void_p]
+        f(grids.ctypes.data, nof_prb, cell_id, nports, nrx, sf_idx, symbol_sz, cp, ce.ctypes.data, out.ctypes.data)
         return ce, dict(noise=float(out[0]), rsrp=float(out[1]), rssi=float(out[2]), cfo=float(out[3]))
 
     def sequence_bits(self, seed, n):

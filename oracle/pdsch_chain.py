@@ -34,30 +34,31 @@ def symbol_sz(nof_prb, standard=True):
     raise ValueError(nof_prb)
 
 
-def fft_estimate(ora, samples, nof_prb, cell_id, nports, tti, cfo=0.0, N=None):
-    """-> grids (nrx, 14*12*nof_prb) complex64, ce (nports, nrx, n) complex64, stats"""
+def fft_estimate(ora, samples, nof_prb, cell_id, nports, tti, cfo=0.0, N=None, cp=0):
+    """-> grids (nrx, 2*nsymb*12*nof_prb) complex64 (nsymb 7, or 6 with cp=1 extended), ce (nports, nrx, n)
+    complex64, stats"""
     N = N or symbol_sz(nof_prb)
     nre = 12 * nof_prb
     grids = []
     for x in samples:
         if cfo:
             x = ofdm_np.cfo(x, cfo)
-        grids.append(ofdm_np.ofdm_rx(x, N, nre).astype(np.complex64))
+        grids.append(ofdm_np.ofdm_rx(x, N, nre, ext=cp).astype(np.complex64))
     grids = np.stack(grids)
-    ce, st = ora.chest_dl(grids, nof_prb, cell_id, nports, tti % 10, N)
+    ce, st = ora.chest_dl(grids, nof_prb, cell_id, nports, tti % 10, N, cp=cp)
     return grids, ce, st
 
 
 def pdsch_decode(ora, grids, ce, noise, nof_prb, cell_id, nports, tti, cfi, rnti, tbs, Qm, rv, scheme="cdd",
                  pmi=0, max_iterations=8, csi_enable=True, power_scale=False, p_a=0.0, p_b=0, prb_mask=None,
-                 states=None, layers=None):
+                 states=None, layers=None, cp=0):
     """srsran_pdsch_decode for nof_tb = len(tbs) codewords (one layer each; layers=2 with one
     codeword: SM / CDD on two layers, pdsch.c:838-863 + layermap.c:138-147, 236-260).
     Returns per codeword dict(ret, data, avg, llr)."""
     sf_idx = tti % 10
     lstart = cfi + (1 if nof_prb < 10 else 0)
     mask = np.ones((2, nof_prb), bool) if prb_mask is None else prb_mask
-    tab = pdsch_np.re_table(nof_prb, nports, cell_id, mask, lstart, sf_idx)
+    tab = pdsch_np.re_table(nof_prb, nports, cell_id, mask, lstart, sf_idx, cp=cp)
     idx = np.array([t[0] for t in tab], np.int64)
     crs = np.array([t[1] for t in tab], bool)
     y = grids[:, idx].astype(np.complex64)

@@ -3,14 +3,14 @@
 Independent of the product's pointer-walking restatement of srsran_pdsch_cp (pdsch.c:136-220):
 a RE (symbol l of slot s, PRB n, subcarrier k) carries PDSCH iff the PRB is granted, l is past
 the control region (slot 0), k is not a CRS position of any cell port (k = off mod 3 for 2/4
-ports, k = off mod 6 for 1 port, in the CRS symbols l = 0, 4 and l = 1 for 4 ports), and the
+ports, k = off mod 6 for 1 port, in the CRS symbols l = 0, nsymb - 3 and l = 1 for 4 ports), and the
 PRB is not one of the 6 (7 for odd N_PRB) centre PRBs in the PSS/SSS/PBCH symbols of
 subframes 0/5 (pdsch_cp_skip_symbol, pdsch.c:83-112) -- for odd N_PRB the outer halves of the
 two edge PRBs of that block still carry PDSCH (pdsch.c:178-203)."""
 
 
-def crs_symbol(l, nof_ports):
-    return l == 0 or l == 4 or (l == 1 and nof_ports == 4)
+def crs_symbol(l, nof_ports, nsymb=7):
+    return l == 0 or l == nsymb - 3 or (l == 1 and nof_ports == 4)
 
 
 def crs_offset(l, nof_ports, cell_id):
@@ -34,20 +34,22 @@ def skipped(nof_prb, fdd, sf_idx, s, l, n, nsymb=7):
     return False
 
 
-def re_table(nof_prb, nof_ports, cell_id, prb_mask, lstart, sf_idx, fdd=True):
-    """List of (grid index, crs_symbol) in PDSCH order; prb_mask[s][n]."""
+def re_table(nof_prb, nof_ports, cell_id, prb_mask, lstart, sf_idx, fdd=True, cp=0):
+    """List of (grid index, crs_symbol) in PDSCH order; prb_mask[s][n]; cp 1 = extended (6 symbols a
+    slot, CRS in l = 0 and 3)."""
+    nsymb = 6 if cp else 7
     out = []
     for s in range(2):
-        for l in range(lstart if s == 0 else 0, 7):
-            lp = l + 7 * s
-            crs = crs_symbol(l, nof_ports)
+        for l in range(lstart if s == 0 else 0, nsymb):
+            lp = l + nsymb * s
+            crs = crs_symbol(l, nof_ports, nsymb)
             off = crs_offset(l, nof_ports, cell_id)
             period = 6 if nof_ports == 1 else 3
             for n in range(nof_prb):
                 if not prb_mask[s][n]:
                     continue
                 ks = range(12)
-                if skipped(nof_prb, fdd, sf_idx, s, l, n):
+                if skipped(nof_prb, fdd, sf_idx, s, l, n, nsymb):
                     if nof_prb % 2 == 0:
                         continue
                     if n == nof_prb // 2 - 3:

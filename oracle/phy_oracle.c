@@ -425,7 +425,7 @@ void oracle_csi_correction(int mod, const float* csi, int16_t* e, uint32_t nof_b
 /* ======================= DL channel estimation (chest_dl.c, refsignal_dl.c) =======================
  * srsUE default configuration (srsue/src/phy/phy_common.cc:83-107, main.cc defaults): estimator
  * AVERAGE, Gauss smoothing filter order 4 / stddev 1.0, noise algorithm REFS, normal subframe,
- * normal CP, FDD.  Restated (chest_dl.c and refsignal_dl.c include the generated srsran.h):
+ * normal or extended CP, FDD.  Restated (chest_dl.c and refsignal_dl.c include the generated srsran.h):
  *   CRS             srsran_refsignal_cs_set_cell  refsignal_dl.c:65-119, fidx/nsymbol 249-266
  *   LS              estimate_port                 chest_dl.c:806-834
  *   noise (REFS)    estimate_noise_pilots         chest_dl.c:325-400
@@ -434,7 +434,7 @@ void oracle_csi_correction(int mod, const float* csi, int16_t* e, uint32_t nof_b
  *   Gauss filter    srsran_chest_set_smooth_filter_gauss chest_common.c:70-95
  *   interpolation   srsran_interp_linear_offset   interp.c:258-285, then copy to all symbols
  *   CFO             chest_estimate_cfo            chest_dl.c:621-641
- * grid: [rx][14 * 12 * nof_prb] cf32; ce: [port][rx][14 * 12 * nof_prb]. */
+ * grid: [rx][2 nsymb * 12 * nof_prb] cf32; ce: [port][rx][2 nsymb * 12 * nof_prb] (nsymb 7 / 6). */
 #define NRE 12
 static const float kPi = 3.14159265358979323846f;
 
@@ -452,20 +452,26 @@ static uint32_t crs_v(uint32_t port, uint32_t l)
   }
 }
 static uint32_t crs_fidx(uint32_t cell_id, uint32_t l, uint32_t port) { return (crs_v(port, l) + cell_id % 6) % 6; }
-static uint32_t crs_nsymbol(uint32_t l, uint32_t port) { return port < 2 ? ((l % 2) ? (l / 2 + 1) * 7 - 3 : (l / 2) * 7) : 1 + l * 7; }
+/* srsran_refsignal_cs_nsymbol (refsignal_dl.c:254-266); nsymb = SRSRAN_CP_NSYMB: 7 normal, 6 extended CP */
+static uint32_t crs_nsymbol(uint32_t l, uint32_t port, uint32_t nsymb)
+{
+  return port < 2 ? ((l % 2) ? (l / 2 + 1) * nsymb - 3 : (l / 2) * nsymb) : 1 + l * nsymb;
+}
 static uint32_t crs_nof_symbols(uint32_t port) { return port < 2 ? 4 : 2; }
 
-/* pilots of port pair pp (ports 2pp, 2pp+1) for subframe sf: [nsym][2 * nof_prb] */
-void oracle_crs_pilots(uint32_t cell_id, uint32_t nof_prb, uint32_t pp, uint32_t sf, float* out)
+/* pilots of port pair pp (ports 2pp, 2pp+1) for subframe sf: [nsym][2 * nof_prb]; cp 0 normal, 1 extended
+ * (N_cp = 1 / 0 in c_init, refsignal_dl.c:81-97) */
+void oracle_crs_pilots_cp(uint32_t cell_id, uint32_t nof_prb, uint32_t pp, uint32_t sf, uint32_t cp, float* out)
 {
+  const uint32_t nsymb = cp ? 6 : 7, N_cp = cp ? 0 : 1;
   cpx*           P        = (cpx*)out;
   const uint32_t nsym_slot = crs_nof_symbols(2 * pp) / 2;
   uint8_t        c[4 * 110];
   for (uint32_t s = 0; s < 2; s++) {
     const uint32_t ns = 2 * sf + s;
     for (uint32_t l = 0; l < nsym_slot; l++) {
-      const uint32_t lp     = crs_nsymbol(l, 2 * pp);
-      const uint32_t c_init = 1024 * (7 * (ns + 1) + lp + 1) * (2 * cell_id + 1) + 2 * cell_id + 1;
+      const uint32_t lp     = crs_nsymbol(l, 2 * pp, nsymb);
+      const uint32_t c_init = 1024 * (7 * (ns + 1) + lp + 1) * (2 * cell_id + 1) + 2 * cell_id + N_cp;
       oracle_sequence_bits(c_init, c, 4 * 110);
       for (uint32_t i = 0; i < 2 * nof_prb; i++) {
         const uint32_t mp = i + 110 - nof_prb;
@@ -475,6 +481,11 @@ void oracle_crs_pilots(uint32_t cell_id, uint32_t nof_prb, uint32_t pp, uint32_t
       }
     }
   }
+}
+
+void oracle_crs_pilots(uint32_t cell_id, uint32_t nof_prb, uint32_t pp, uint32_t sf, float* out)
+{
+  oracle_crs_pilots_cp(cell_id, nof_prb, pp, sf, 0, out);
 }
 
 static float avg_power(const cpx* x, uint32_t n)
@@ -608,17 +619,18 @@ static void interp_linear_offset(const cpx* in, cpx* out, uint32_t len, uint32_t
 }
 
 /* out[0..5]: noise_estimate, rsrp, rssi, cfo, per (rx,port) noise not returned */
-int oracle_chest_dl(const float* grid, uint32_t nof_prb, uint32_t cell_id, uint32_t nports, uint32_t nrx,
-                    uint32_t sf_idx, uint32_t symbol_sz, float* ce, float* out)
+int oracle_chest_dl_cp(const float* grid, uint32_t nof_prb, uint32_t cell_id, uint32_t nports, uint32_t nrx,
+                       uint32_t sf_idx, uint32_t symbol_sz, uint32_t cp, float* ce, float* out)
 {
-  const uint32_t nre = NRE * nof_prb, nsf = 14 * nre;
+  const uint32_t nsymb = cp ? 6 : 7; /* SRSRAN_CP_NSYMB */
+  const uint32_t nre = NRE * nof_prb, nsf = 2 * nsymb * nre;
   const cpx*     G   = (const cpx*)grid;
   cpx*           CE  = (cpx*)ce;
   float          filt[8];
   const uint32_t flen = oracle_gauss_filter(filt, 4, 1.0f);
   static cpx     pil[2][4 * 2 * 110];
-  oracle_crs_pilots(cell_id, nof_prb, 0, sf_idx, (float*)pil[0]);
-  oracle_crs_pilots(cell_id, nof_prb, 1, sf_idx, (float*)pil[1]);
+  oracle_crs_pilots_cp(cell_id, nof_prb, 0, sf_idx, cp, (float*)pil[0]);
+  oracle_crs_pilots_cp(cell_id, nof_prb, 1, sf_idx, cp, (float*)pil[1]);
   float noise[4][4], rsrp[4][4], rssi[4][4], cfo = 0;
   for (uint32_t rx = 0; rx < nrx; rx++) {
     const cpx* in = G + (size_t)rx * nsf;
@@ -626,7 +638,7 @@ int oracle_chest_dl(const float* grid, uint32_t nof_prb, uint32_t cell_id, uint3
       const uint32_t nsym = crs_nof_symbols(port), nref = 2 * nof_prb, np = nsym * nref;
       cpx            recv[4 * 220], pe[4 * 220], avg[4 * 220], tmp[4 * 220];
       for (uint32_t l = 0; l < nsym; l++) {
-        const uint32_t sym = crs_nsymbol(l, port);
+        const uint32_t sym = crs_nsymbol(l, port, nsymb);
         uint32_t       f   = crs_fidx(cell_id, l, port);
         for (uint32_t i = 0; i < nref; i++, f += 6) {
           recv[l * nref + i] = in[sym * nre + f];
@@ -638,7 +650,7 @@ int oracle_chest_dl(const float* grid, uint32_t nof_prb, uint32_t cell_id, uint3
       rsrp[rx][port] = avg_power(recv, np);
       float rs       = 0;
       for (uint32_t l = 0; l < nsym; l++) {
-        const cpx* t = in + crs_nsymbol(l, port) * nre;
+        const cpx* t = in + crs_nsymbol(l, port, nsymb) * nre;
         for (uint32_t k = 0; k < nre; k++) {
           rs += t[k].r * t[k].r + t[k].i * t[k].i;
         }
@@ -653,7 +665,7 @@ int oracle_chest_dl(const float* grid, uint32_t nof_prb, uint32_t cell_id, uint3
         }
         const float n  = (float)symbol_sz;
         const float ng = (float)(int)ceilf(144.0f * n / 2048.0f); /* SRSRAN_CP_LEN_NORM(1, n) */
-        cfo            = -atan2f(sum.i, sum.r) * n / (7.0f * (n + ng)) / 2 / kPi;
+        cfo            = -atan2f(sum.i, sum.r) * n / ((float)nsymb * (n + ng)) / 2 / kPi;
       }
       const uint32_t fidx0 = crs_fidx(cell_id, 0, port);
       noise[rx][port]      = noise_pilots(pe, nsym, nref, fidx0);
@@ -690,7 +702,7 @@ int oracle_chest_dl(const float* grid, uint32_t nof_prb, uint32_t cell_id, uint3
         const uint32_t off = crs_fidx(cell_id, 0, port);
         interp_linear_offset(avg, row, nr, 6, off, 6 - off);
       }
-      for (uint32_t l = 1; l < 14; l++) {
+      for (uint32_t l = 1; l < 2 * nsymb; l++) {
         memcpy(row + l * nre, row, nre * sizeof(cpx));
       }
     }
@@ -721,4 +733,10 @@ int oracle_chest_dl(const float* grid, uint32_t nof_prb, uint32_t cell_id, uint3
   out[2] = r / (float)nrx;
   out[3] = cfo;
   return 0;
+}
+
+int oracle_chest_dl(const float* grid, uint32_t nof_prb, uint32_t cell_id, uint32_t nports, uint32_t nrx,
+                    uint32_t sf_idx, uint32_t symbol_sz, float* ce, float* out)
+{
+  return oracle_chest_dl_cp(grid, nof_prb, cell_id, nports, nrx, sf_idx, symbol_sz, 0, ce, out);
 }

@@ -15,4 +15,7 @@ uint32_t oracle_gauss_filter(float* f, uint32_t order, float std_dev);
 void     oracle_conv_same(const float* in, const float* f, float* out, uint32_t N, uint32_t M);
 int      oracle_chest_dl(const float* grid, uint32_t nof_prb, uint32_t cell_id, uint32_t nports, uint32_t nrx,
                          uint32_t sf_idx, uint32_t symbol_sz, float* ce, float* out);
+int      oracle_chest_dl_cp(const float* grid, uint32_t nof_prb, uint32_t cell_id, uint32_t nports, uint32_t nrx,
+                            uint32_t sf_idx, uint32_t symbol_sz, uint32_t cp, float* ce, float* out);
+void     oracle_crs_pilots_cp(uint32_t cell_id, uint32_t nof_prb, uint32_t pp, uint32_t sf, uint32_t cp, float* out);
 #endif

@@ -191,12 +191,12 @@ int srsran_chest_dl_set_cell(srsran_chest_dl_t* q, srsran_cell_t cell)
       (cell.nof_ports != 1 && cell.nof_ports != 2 && cell.nof_ports != 4)) {
     return SRSRAN_ERROR_INVALID_INPUTS;
   }
-  if (cell.cp != SRSRAN_CP_NORM) {
-    fprintf(stderr, "[srsran_chest_dl] extended CP not provided\n");
-    return SRSRAN_ERROR;
+  if (cell.cp != SRSRAN_CP_NORM && cell.cp != SRSRAN_CP_EXT) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
   }
   ChestGpu* g = (ChestGpu*)q->gpu;
   q->cell     = cell;
+  const uint32_t nsymb = SRSRAN_CP_NSYMB(cell.cp), N_cp = cell.cp == SRSRAN_CP_NORM ? 1 : 0;
   // refsignal_dl.c:65-119: per slot ns, CRS symbol l' of port pair pp, c_init as 36.211 6.10.1.1
   std::vector<float2> h(10 * kPilotsPerSf, make_float2(0.f, 0.f));
   std::vector<uint8_t> c(4 * 110);
@@ -205,8 +205,8 @@ int srsran_chest_dl_set_cell(srsran_chest_dl_t* q, srsran_cell_t cell)
     for (uint32_t pp = 0; pp < 2; pp++) {
       const uint32_t nsym_slot = pp == 0 ? 2 : 1;
       for (uint32_t l = 0; l < nsym_slot; l++) {
-        const uint32_t lp     = pp == 0 ? (l ? 4 : 0) : 1;
-        const uint32_t c_init = 1024 * (7 * (ns + 1) + lp + 1) * (2 * cell.id + 1) + 2 * cell.id + 1;
+        const uint32_t lp     = pp == 0 ? (l ? nsymb - 3 : 0) : 1;  // srsran_refsignal_cs_nsymbol
+        const uint32_t c_init = 1024 * (7 * (ns + 1) + lp + 1) * (2 * cell.id + 1) + 2 * cell.id + N_cp;
         gold(c_init, c.data(), 4 * 110);
         float2* dst = &h[(ns / 2) * kPilotsPerSf + pp * 4 * CHEST_MAX_NREF +
                          2 * cell.nof_prb * ((ns % 2) * nsym_slot + l)];
@@ -268,7 +268,8 @@ static int chest_enqueue(srsran_chest_dl_t* q, uint32_t tti, const float2* d_gri
   a.cell_id    = q->cell.id;
   a.nports     = q->cell.nof_ports;
   a.nrx        = q->nof_rx_antennas;
-  a.ce_stride  = (full ? 14 : 1) * 12 * q->cell.nof_prb;
+  a.nsymb      = SRSRAN_CP_NSYMB(q->cell.cp);
+  a.ce_stride  = (full ? 2 * a.nsymb : 1) * 12 * q->cell.nof_prb;
   a.full_grid  = full ? 1 : 0;
   a.filter_len = g->filter_len;
   memcpy(a.filter, g->filter, sizeof(a.filter));
@@ -305,7 +306,7 @@ static void fill_res(srsran_chest_dl_t* q, const float* st, srsran_chest_dl_res_
       const float* v  = st + idx * 8;
       const float  sz = (float)srsran_symbol_sz(q->cell.nof_prb);
       const float  ng = (float)(int)ceilf(144.0f * sz / 2048.0f);
-      q->cfo          = -atan2f(v[4], v[3]) * sz / (7.0f * (sz + ng)) / 2 / (float)M_PI;
+      q->cfo          = -atan2f(v[4], v[3]) * sz / ((float)SRSRAN_CP_NSYMB(q->cell.cp) * (sz + ng)) / 2 / (float)M_PI;
       break;
     }
   }
@@ -360,7 +361,8 @@ int srsran_chest_dl_estimate_cfg(srsran_chest_dl_t*     q,
     return SRSRAN_ERROR;
   }
   ChestGpu*      g   = (ChestGpu*)q->gpu;
-  const uint32_t nsf = 14 * 12 * q->cell.nof_prb, nrx = q->nof_rx_antennas, np = q->cell.nof_ports;
+  const uint32_t nsf = 2 * SRSRAN_CP_NSYMB(q->cell.cp) * 12 * q->cell.nof_prb, nrx = q->nof_rx_antennas,
+                 np  = q->cell.nof_ports;
   for (uint32_t rx = 0; rx < nrx; rx++) {
     hipMemcpyAsync(g->grid + rx * nsf, input[rx], nsf * sizeof(cf_t), hipMemcpyHostToDevice, g->stream);
   }
@@ -410,7 +412,7 @@ extern "C" int srsran_chest_dl_gpu_estimate(srsran_chest_dl_t* q,
   if (d_res) {
     ChestGpu* g = (ChestGpu*)q->gpu;
     chest_finalize_launch(g->stats, q->cell.nof_ports, q->nof_rx_antennas, q->cell.nof_prb,
-                          (float)srsran_symbol_sz(q->cell.nof_prb), d_res, 1, s);
+                          (float)srsran_symbol_sz(q->cell.nof_prb), SRSRAN_CP_NSYMB(q->cell.cp), d_res, 1, s);
   }
   return hipGetLastError() == hipSuccess ? SRSRAN_SUCCESS : SRSRAN_ERROR;
 }
@@ -456,11 +458,12 @@ extern "C" int srsran_chest_dl_gpu_estimate_batch(srsran_chest_dl_t* q,
   a.nrx            = q->nof_rx_antennas;
   a.ce_stride      = 12 * q->cell.nof_prb;
   a.full_grid      = 0;
+  a.nsymb          = SRSRAN_CP_NSYMB(q->cell.cp);
   a.filter_len     = g->filter_len;
   memcpy(a.filter, g->filter, sizeof(a.filter));
   if (chest_launch(a, s, nsf) != hipSuccess ||
       chest_finalize_launch(g->bstats, q->cell.nof_ports, q->nof_rx_antennas, q->cell.nof_prb,
-                            (float)srsran_symbol_sz(q->cell.nof_prb), d_res, nsf, s) != hipSuccess) {
+                            (float)srsran_symbol_sz(q->cell.nof_prb), a.nsymb, d_res, nsf, s) != hipSuccess) {
     return SRSRAN_ERROR;
   }
   return SRSRAN_SUCCESS;

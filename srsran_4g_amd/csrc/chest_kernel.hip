@@ -8,7 +8,7 @@
 //   CFO from pilot phases    chest_estimate_cfo    chest_dl.c:621-641
 // One workgroup per (port, rx antenna): the 4 x 200 pilots, the noise residuals and the
 // 400-point smoothed comb live in LDS; the estimate row (1200 subcarriers at 100 PRB) is
-// written once, or 14 times when the caller wants the full srsran_chest_dl_res_t grid.
+// written once, or 2 nsymb times (14 normal CP, 12 extended) for the full srsran_chest_dl_res_t grid.
 // Float operations follow the reference's order (no contraction) so the result matches
 // oracle/phy_oracle.c up to the order of the power/phase reductions.
 #include <hip/hip_runtime.h>
@@ -42,9 +42,10 @@ __device__ __forceinline__ uint32_t crs_v(uint32_t port, uint32_t l)
 {
   return port == 0 ? ((l & 1) ? 3u : 0u) : port == 1 ? ((l & 1) ? 0u : 3u) : port == 2 ? (l == 0 ? 0u : 3u) : (l == 0 ? 3u : 0u);
 }
-__device__ __forceinline__ uint32_t crs_nsymbol(uint32_t l, uint32_t port)
+// srsran_refsignal_cs_nsymbol (refsignal_dl.c:254-266), ns = symbols per slot
+__device__ __forceinline__ uint32_t crs_nsymbol(uint32_t l, uint32_t port, uint32_t ns)
 {
-  return port < 2 ? ((l & 1) ? (l / 2 + 1) * 7 - 3 : (l / 2) * 7) : 1 + l * 7;
+  return port < 2 ? ((l & 1) ? (l / 2 + 1) * ns - 3 : (l / 2) * ns) : 1 + l * ns;
 }
 
 // block-wide sum of one float (all threads get the result)
@@ -76,7 +77,7 @@ __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
   const uint32_t port = blockIdx.x / a.nrx, rx = blockIdx.x % a.nrx, b = blockIdx.y;
   const uint32_t tid  = threadIdx.x;
   const uint32_t nsym = port < 2 ? 4 : 2, nref = 2 * a.nof_prb, np = nsym * nref, nre = 12 * a.nof_prb;
-  const float2*  in   = a.grid + b * a.grid_sf_stride + (size_t)rx * 14 * nre;
+  const float2*  in   = a.grid + b * a.grid_sf_stride + (size_t)rx * 2 * a.nsymb * nre;
   const float2*  pil  = a.pilots + (a.sf_idx ? a.sf_idx[b] * CHEST_PILOTS_PER_SF : 0) +
                       (size_t)(port / 2) * 4 * CHEST_MAX_NREF;
   const uint32_t fidx0 = (crs_v(port, 0) + a.cell_id % 6) % 6;
@@ -86,13 +87,13 @@ __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
   for (uint32_t k = tid; k < np; k += CH_THREADS) {
     const uint32_t l = k / nref, i = k % nref;
     const uint32_t f = (crs_v(port, l) + a.cell_id % 6) % 6 + 6 * i;
-    const cx       r = ld2(in, crs_nsymbol(l, port) * nre + f);
+    const cx       r = ld2(in, crs_nsymbol(l, port, a.nsymb) * nre + f);
     pe[k]            = mul(r, conj(ld2(pil, k)));
     rsrp += r.r * r.r + r.i * r.i;
   }
   float rssi = 0.f;
   for (uint32_t k = tid; k < nsym * nre; k += CH_THREADS) {
-    const cx r = ld2(in, crs_nsymbol(k / nre, port) * nre + k % nre);
+    const cx r = ld2(in, crs_nsymbol(k / nre, port, a.nsymb) * nre + k % nre);
     rssi += r.r * r.r + r.i * r.i;
   }
   rsrp = block_sum(rsrp, red) / (float)np;
@@ -233,7 +234,7 @@ __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
     }
     const float2 o = make_float2(v.r, v.i);
     if (a.full_grid) {
-      for (uint32_t l = 0; l < 14; l++) {
+      for (uint32_t l = 0; l < 2 * a.nsymb; l++) {
         ce[l * nre + j] = o;
       }
     } else {
@@ -253,6 +254,9 @@ __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
 hipError_t chest_launch(const ChestArgs& a, hipStream_t stream, uint32_t nsf)
 {
   StageScope timing_scope(ST_CHEST, stream);
+  if (a.nsymb != 7 && a.nsymb != 6) {
+    return hipErrorInvalidValue;
+  }
   if (nsf == 0) {
     return hipSuccess;
   }
@@ -262,7 +266,7 @@ hipError_t chest_launch(const ChestArgs& a, hipStream_t stream, uint32_t nsf)
 
 // one thread per subframe
 __global__ void chest_finalize_kernel(const float* stats, uint32_t np, uint32_t nrx, uint32_t nof_prb, float sz,
-                                      float* out, uint32_t nsf)
+                                      float nsymb, float* out, uint32_t nsf)
 {
   const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= nsf) {
@@ -288,8 +292,9 @@ __global__ void chest_finalize_kernel(const float* stats, uint32_t np, uint32_t 
   }
   for (int idx = (int)(nrx * np) - 1; idx >= 0; idx--) {  // chest_estimate_cfo: last (rx, port<2) wins
     if ((uint32_t)idx % np < 2) {
+      // chest_estimate_cfo (chest_dl.c:618-641): ns = SRSRAN_CP_NSYMB, ng = SRSRAN_CP_LEN_NORM(1, n) for both CPs
       const float ng = (float)(int)ceilf(144.0f * sz / 2048.0f);
-      cfo            = -atan2f(st[idx * 8 + 4], st[idx * 8 + 3]) * sz / (7.0f * (sz + ng)) / 2 / 3.14159265358979f;
+      cfo            = -atan2f(st[idx * 8 + 4], st[idx * 8 + 3]) * sz / (nsymb * (sz + ng)) / 2 / 3.14159265358979f;
       break;
     }
   }
@@ -301,14 +306,14 @@ __global__ void chest_finalize_kernel(const float* stats, uint32_t np, uint32_t 
 }
 
 hipError_t chest_finalize_launch(const float* stats, uint32_t np, uint32_t nrx, uint32_t nof_prb, float symbol_sz,
-                                 float* out, uint32_t nsf, hipStream_t stream)
+                                 uint32_t nsymb, float* out, uint32_t nsf, hipStream_t stream)
 {
   StageScope timing_scope(ST_CHEST, stream);
   if (nsf == 0) {
     return hipSuccess;
   }
   hipLaunchKernelGGL(chest_finalize_kernel, dim3((nsf + 63) / 64), dim3(64), 0, stream, stats, np, nrx, nof_prb,
-                     symbol_sz, out, nsf);
+                     symbol_sz, (float)nsymb, out, nsf);
   return hipGetLastError();
 }
 

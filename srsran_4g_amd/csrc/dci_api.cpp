@@ -279,14 +279,23 @@ int unpack_format2x(const srsran_cell_t* cell, srsran_dci_cfg_t* cfg, srsran_dci
 // ---- ra_dl.c ----
 uint32_t ra_re_x_prb(const srsran_cell_t* cell, srsran_dl_sf_cfg_t* sf, uint32_t slot, uint32_t prb)
 {
-  // FDD, normal CP, normal subframe (ra_dl.c:42-168)
+  // FDD, normal subframe, normal or extended CP (ra_dl.c:42-168)
   const uint32_t sfi   = sf->tti % 10;
   const uint32_t nctrl = cell->nof_prb <= 10 ? sf->cfi + 1 : sf->cfi;
-  const uint32_t nsym  = 7;
+  const bool     ext   = cell->cp == SRSRAN_CP_EXT;
+  const uint32_t nsym  = SRSRAN_CP_NSYMB(cell->cp);
   uint32_t       re    = slot == 0 ? (nsym - nctrl) * 12 : nsym * 12;
+  bool           refs  = true;  // remove the CRS REs below
   if ((sfi == 0 || sfi == 5) && prb >= cell->nof_prb / 2 - 3 && prb < cell->nof_prb / 2 + 3 + (cell->nof_prb % 2)) {
     if (sfi == 0) {
-      re = slot == 0 ? (nsym - nctrl - 2) * 12 : (nsym - 4) * 12 + 2 * cell->nof_ports;
+      if (slot == 0) {
+        re = (nsym - nctrl - 2) * 12;
+      } else if (ext) {
+        re   = (nsym - 4) * 12;  // both CRS symbols of the slot fall under the PBCH
+        refs = false;
+      } else {
+        re = (nsym - 4) * 12 + 2 * cell->nof_ports;
+      }
     } else if (slot == 0) {
       re = (nsym - nctrl - 2) * 12;
     }
@@ -295,24 +304,29 @@ uint32_t ra_re_x_prb(const srsran_cell_t* cell, srsran_dl_sf_cfg_t* sf, uint32_t
         re += 2 * 12 / 2;
       } else if (sfi == 0) {
         re += 4 * 12 / 2 - cell->nof_ports;
+        if (ext) {
+          re -= cell->nof_ports > 2 ? 2 : cell->nof_ports;
+        }
       }
     }
   }
-  switch (cell->nof_ports) {
-    case 1:
-    case 2:
-      re -= 2 * (slot + 1) * cell->nof_ports;
-      break;
-    case 4:
-      if (slot == 1) {
-        re -= 12;
-      } else {
-        re -= 4;
-        if (nctrl == 1) {
+  if (refs) {
+    switch (cell->nof_ports) {
+      case 1:
+      case 2:
+        re -= 2 * (slot + 1) * cell->nof_ports;
+        break;
+      case 4:
+        if (slot == 1) {
+          re -= 12;
+        } else {
           re -= 4;
+          if (nctrl == 1) {
+            re -= 4;
+          }
         }
-      }
-      break;
+        break;
+    }
   }
   return re;
 }
@@ -705,8 +719,8 @@ int srsran_ra_dl_dci_to_grant(const srsran_cell_t* cell, srsran_dl_sf_cfg_t* sf,
   if (!cell || !sf || !dci || !grant) {
     return SRSRAN_ERROR_INVALID_INPUTS;
   }
-  if (cell->frame_type != SRSRAN_FDD || cell->cp != SRSRAN_CP_NORM || sf->sf_type != SRSRAN_SF_NORM) {
-    fprintf(stderr, "[srsran_ra] FDD normal-CP normal subframes only\n");
+  if (cell->frame_type != SRSRAN_FDD || sf->sf_type != SRSRAN_SF_NORM) {
+    fprintf(stderr, "[srsran_ra] FDD normal subframes only\n");
     return SRSRAN_ERROR;
   }
   memset(grant, 0, sizeof(*grant));
@@ -714,8 +728,8 @@ int srsran_ra_dl_dci_to_grant(const srsran_cell_t* cell, srsran_dl_sf_cfg_t* sf,
     return SRSRAN_ERROR;
   }
   grant->nof_re           = srsran_ra_dl_grant_nof_re(cell, sf, grant);
-  grant->nof_symb_slot[0] = 7;
-  grant->nof_symb_slot[1] = 7;
+  grant->nof_symb_slot[0] = SRSRAN_CP_NSYMB(cell->cp);  // ra_dl.c:428-431 (FDD)
+  grant->nof_symb_slot[1] = SRSRAN_CP_NSYMB(cell->cp);
   for (int i = 0; i < SRSRAN_MAX_CODEWORDS; i++) {
     if (grant->tb[i].enabled) {
       grant->tb[i].nof_bits = grant->nof_re * srsran_mod_bits_x_symbol(grant->tb[i].mod);

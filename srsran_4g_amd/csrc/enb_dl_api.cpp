@@ -21,7 +21,7 @@ struct EnbDlGpu {
   srsran_sch_t  sch{};
   srsran_ofdm_t ofdm{};
   uint32_t      N = 0, sf_len = 0;
-  float2*       d_grid = nullptr;  // [sf][port][14][nre]
+  float2*       d_grid = nullptr;  // [sf][port][2 nsymb][nre]
   size_t        grid_cap = 0;
   uint8_t*      d_e = nullptr;     // packed e bits of every codeword
   size_t        e_cap = 0;
@@ -55,7 +55,7 @@ extern "C" {
 int srsran_enb_dl_gpu_init(srsran_enb_dl_gpu_t* q, srsran_cell_t cell)
 {
   if (!q || cell.nof_prb < 6 || cell.nof_prb > SRSRAN_MAX_PRB || cell.nof_ports == 0 || cell.nof_ports > 2 ||
-      cell.cp != SRSRAN_CP_NORM) {
+      (cell.cp != SRSRAN_CP_NORM && cell.cp != SRSRAN_CP_EXT)) {
     return SRSRAN_ERROR_INVALID_INPUTS;
   }
   memset(q, 0, sizeof(*q));
@@ -65,7 +65,7 @@ int srsran_enb_dl_gpu_init(srsran_enb_dl_gpu_t* q, srsran_cell_t cell)
   srsran_ofdm_cfg_t oc;
   memset(&oc, 0, sizeof(oc));
   oc.nof_prb   = cell.nof_prb;
-  oc.cp        = SRSRAN_CP_NORM;
+  oc.cp        = cell.cp;
   oc.normalize = false;  // enb_dl.c:158
   if (srsran_sch_init(&g->sch) != SRSRAN_SUCCESS || srsran_ofdm_tx_init_cfg(&g->ofdm, &oc) != SRSRAN_SUCCESS) {
     srsran_enb_dl_gpu_free(q);
@@ -112,7 +112,7 @@ int srsran_enb_dl_gpu_tx_batch(srsran_enb_dl_gpu_t*          q,
   EnbDlGpu*           g     = (EnbDlGpu*)q->gpu;
   hipStream_t         st    = (hipStream_t)stream;
   const srsran_cell_t& cell = q->cell;
-  const uint32_t      P     = cell.nof_ports, nre_sf = 14 * 12 * cell.nof_prb;
+  const uint32_t      P     = cell.nof_ports, nre_sf = SRSRAN_SF_LEN_RE(cell.nof_prb, cell.cp);
   std::vector<std::vector<uint32_t>> tables(nof_sf);
   std::vector<PdschTx>               items(nof_sf);
   std::vector<srsran_dlsch_gpu_enc_t> enc;
@@ -202,7 +202,7 @@ int srsran_enb_dl_gpu_tx_batch(srsran_enb_dl_gpu_t*          q,
       hipMemcpyAsync(g->d_idx, idx_host.data(), idx_tot * sizeof(uint32_t), hipMemcpyHostToDevice, st) != hipSuccess ||
       hipMemcpyAsync(g->d_items, items.data(), nof_sf * sizeof(PdschTx), hipMemcpyHostToDevice, st) != hipSuccess ||
       hipMemcpyAsync(g->d_sfidx, sfidx.data(), nof_sf * sizeof(uint32_t), hipMemcpyHostToDevice, st) != hipSuccess ||
-      crs_put_launch(g->d_grid, cell.nof_prb, cell.id, P, g->d_sfidx, nof_sf, st) != hipSuccess ||
+      crs_put_launch(g->d_grid, cell.nof_prb, cell.id, P, SRSRAN_CP_NSYMB(cell.cp), g->d_sfidx, nof_sf, st) != hipSuccess ||
       pdsch_tx_launch(g->d_items, nof_sf, max_nre, st) != hipSuccess) {
     return SRSRAN_ERROR;
   }

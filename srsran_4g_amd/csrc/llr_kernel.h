@@ -48,9 +48,10 @@ struct PdschTx {
   float           div_scale;// (float)(scaling * M_SQRT1_2) for diversity
 };
 hipError_t pdsch_tx_launch(const PdschTx* d_items, uint32_t nitems, uint32_t max_nre, hipStream_t stream);
-// CRS of ports 0..nports-1 (<= 2) into grids [nsf][nports][14][12 nof_prb]; d_sf_idx[sf] = tti % 10
-hipError_t crs_put_launch(float2* d_grids, uint32_t nof_prb, uint32_t cell_id, uint32_t nports, const uint32_t* d_sf_idx,
-                          uint32_t nsf, hipStream_t stream);
+// CRS of ports 0..nports-1 (<= 2) into grids [nsf][nports][2 nsymb][12 nof_prb] (nsymb = 7 normal CP, 6
+// extended); d_sf_idx[sf] = tti % 10
+hipError_t crs_put_launch(float2* d_grids, uint32_t nof_prb, uint32_t cell_id, uint32_t nports, uint32_t nsymb,
+                          const uint32_t* d_sf_idx, uint32_t nsf, hipStream_t stream);
 
 }  // namespace srsran_amd
 #endif

@@ -733,15 +733,17 @@ hipError_t pdsch_tx_launch(const PdschTx* d_items, uint32_t nitems, uint32_t max
 // cell-specific reference signals of 1 or 2 ports (refsignal_dl.c, 36.211 6.10.1): grid (CRS symbol of
 // the subframe, port, subframe); 2 * nof_prb pilots a symbol
 __global__ __launch_bounds__(256) void crs_put_kernel(float2* __restrict__ grids, uint32_t nof_prb, uint32_t cell_id,
-                                                      uint32_t nports, const uint32_t* __restrict__ sf_idx)
+                                                      uint32_t nports, uint32_t nsymb,
+                                                      const uint32_t* __restrict__ sf_idx)
 {
-  const uint32_t sym = blockIdx.x, port = blockIdx.y, sf = blockIdx.z;  // sym: 0..3 -> (slot, l in {0, 4})
-  const uint32_t slot = sym >> 1, l = (sym & 1) ? 4u : 0u;
+  // sym: 0..3 -> (slot, l in {0, nsymb - 3}); N_cp = 1 normal, 0 extended CP (refsignal_dl.c:81-97)
+  const uint32_t sym = blockIdx.x, port = blockIdx.y, sf = blockIdx.z;
+  const uint32_t slot = sym >> 1, l = (sym & 1) ? nsymb - 3 : 0u;
   const uint32_t ns   = 2 * sf_idx[sf] + slot;
   const uint32_t v    = port == 0 ? (l == 0 ? 0u : 3u) : (l == 0 ? 3u : 0u);
-  const uint32_t seed = (1u << 10) * (7 * (ns + 1) + l + 1) * (2 * cell_id + 1) + 2 * cell_id + 1;
+  const uint32_t seed = (1u << 10) * (7 * (ns + 1) + l + 1) * (2 * cell_id + 1) + 2 * cell_id + (nsymb == 7 ? 1u : 0u);
   const uint32_t nre  = 12 * nof_prb;
-  float2*        row  = grids + (((size_t)sf * nports + port) * 14 + 7 * slot + l) * nre;
+  float2*        row  = grids + (((size_t)sf * nports + port) * 2 * nsymb + nsymb * slot + l) * nre;
   for (uint32_t m = threadIdx.x; m < 2 * nof_prb; m += 256) {
     const uint32_t mp = m + 110 - nof_prb;
     uint32_t       x1, x2;
@@ -752,13 +754,13 @@ __global__ __launch_bounds__(256) void crs_put_kernel(float2* __restrict__ grids
   }
 }
 
-hipError_t crs_put_launch(float2* d_grids, uint32_t nof_prb, uint32_t cell_id, uint32_t nports, const uint32_t* d_sf_idx,
-                          uint32_t nsf, hipStream_t stream)
+hipError_t crs_put_launch(float2* d_grids, uint32_t nof_prb, uint32_t cell_id, uint32_t nports, uint32_t nsymb,
+                          const uint32_t* d_sf_idx, uint32_t nsf, hipStream_t stream)
 {
   if (nsf == 0) {
     return hipSuccess;
   }
-  if (nports == 0 || nports > 2) {
+  if (nports == 0 || nports > 2 || (nsymb != 7 && nsymb != 6)) {
     return hipErrorInvalidValue;
   }
   hipError_t e = gold_tables_init();
@@ -766,7 +768,7 @@ hipError_t crs_put_launch(float2* d_grids, uint32_t nof_prb, uint32_t cell_id, u
     return e;
   }
   hipLaunchKernelGGL(crs_put_kernel, dim3(4, nports, nsf), dim3(256), 0, stream, d_grids, nof_prb, cell_id, nports,
-                     d_sf_idx);
+                     nsymb, d_sf_idx);
   return hipGetLastError();
 }
 

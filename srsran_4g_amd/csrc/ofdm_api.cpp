@@ -87,17 +87,19 @@ int configure(srsran_ofdm_t* q, uint32_t nof_prb, uint32_t symbol_sz)
   if (!a.tw) {
     return SRSRAN_ERROR;
   }
+  const bool ext   = q->cfg.cp == SRSRAN_CP_EXT;
   a.N              = N;
-  a.cp0            = cp_len(160, N);  // SRSRAN_CP_NORM_0_LEN
-  a.cp             = cp_len(144, N);  // SRSRAN_CP_NORM_LEN
+  a.nsymb          = ext ? 6 : 7;                      // SRSRAN_CP_NSYMB
+  a.cp0            = cp_len(ext ? 512 : 160, N);       // SRSRAN_CP_EXT_LEN / SRSRAN_CP_NORM_0_LEN
+  a.cp             = cp_len(ext ? 512 : 144, N);       // SRSRAN_CP_EXT_LEN / SRSRAN_CP_NORM_LEN
   a.nre            = 12 * nof_prb;
-  a.sf_len         = 2 * (7 * N + a.cp0 + 6 * a.cp);
+  a.sf_len         = 2 * (a.nsymb * N + a.cp0 + (a.nsymb - 1) * a.cp);
   a.nrx            = 1;
   a.norm           = q->cfg.normalize ? 1.0f / sqrtf((float)N) : 1.0f;
   g->proto         = a;
   q->cfg.nof_prb   = nof_prb;
   q->cfg.symbol_sz = N;
-  q->nof_symbols   = 7;
+  q->nof_symbols   = a.nsymb;
   q->nof_re        = a.nre;
   q->slot_sz       = a.sf_len / 2;
   q->sf_sz         = a.sf_len;
@@ -124,7 +126,8 @@ int srsran_ofdm_rx_init_cfg(srsran_ofdm_t* q, srsran_ofdm_cfg_t* cfg)
   if (!q || !cfg || cfg->nof_prb == 0 || cfg->nof_prb > 110) {
     return SRSRAN_ERROR_INVALID_INPUTS;
   }
-  if (cfg->cp != SRSRAN_CP_NORM || cfg->sf_type != SRSRAN_SF_NORM || std::isnormal(cfg->freq_shift_f) ||
+  if ((cfg->cp != SRSRAN_CP_NORM && cfg->cp != SRSRAN_CP_EXT) || cfg->sf_type != SRSRAN_SF_NORM ||
+      std::isnormal(cfg->freq_shift_f) ||
       std::isnormal(cfg->rx_window_offset) || std::isnormal(cfg->phase_compensation_hz) || cfg->keep_dc) {
     fprintf(stderr, "[srsran_ofdm] only the srsran_ue_dl receiver configuration is provided\n");
     return SRSRAN_ERROR;
@@ -155,9 +158,10 @@ int srsran_ofdm_rx_set_prb(srsran_ofdm_t* q, srsran_cp_t cp, uint32_t nof_prb)
   if (!q || !q->gpu) {
     return SRSRAN_ERROR_INVALID_INPUTS;
   }
-  if (cp != SRSRAN_CP_NORM) {
+  if (cp != SRSRAN_CP_NORM && cp != SRSRAN_CP_EXT) {
     return SRSRAN_ERROR;
   }
+  q->cfg.cp = cp;
   return configure(q, nof_prb, 0);
 }
 
@@ -193,7 +197,7 @@ void srsran_ofdm_rx_sf_ng(srsran_ofdm_t* q, cf_t* input, cf_t* output)
     return;
   }
   OfdmGpu*     g  = (OfdmGpu*)q->gpu;
-  const size_t ni = q->sf_sz, no = 14 * (size_t)q->nof_re;
+  const size_t ni = q->sf_sz, no = 2 * q->nof_symbols * (size_t)q->nof_re;
   if (!grow((void**)&g->d_in, &g->in_cap, ni * sizeof(cf_t)) || !grow((void**)&g->d_out, &g->out_cap, no * sizeof(cf_t))) {
     return;
   }
@@ -331,7 +335,7 @@ void srsran_ofdm_tx_sf(srsran_ofdm_t* q)
     return;
   }
   OfdmGpu*     g  = (OfdmGpu*)q->gpu;
-  const size_t ni = 14 * (size_t)q->nof_re, no = q->sf_sz;
+  const size_t ni = 2 * q->nof_symbols * (size_t)q->nof_re, no = q->sf_sz;
   if (!grow((void**)&g->d_in, &g->in_cap, ni * sizeof(cf_t)) || !grow((void**)&g->d_out, &g->out_cap, no * sizeof(cf_t))) {
     return;
   }

@@ -11,10 +11,11 @@ static constexpr int OFDM_MAX_STAGES = 6;
 
 struct OfdmArgs {
   const float2* in;        // [sf][rx][sf_len] time-domain samples
-  float2*       out;       // [sf][rx][14][nre] resource grid
+  float2*       out;       // [sf][rx][2 nsymb][nre] resource grid
   const float2* tw;        // exp(-2 pi i m / N), m = 0..N-1
   uint32_t      N;         // FFT size (symbol_sz)
   uint32_t      cp0, cp;   // first / other cyclic prefix lengths of a slot
+  uint32_t      nsymb;     // symbols per slot: 7 (normal CP) or 6 (extended CP, cp0 = cp)
   uint32_t      nre;       // 12 * nof_prb
   uint32_t      sf_len;    // samples per subframe and antenna
   uint32_t      nrx;
@@ -25,11 +26,11 @@ struct OfdmArgs {
   uint32_t      ns_magic[OFDM_MAX_STAGES];  // ceil(2^32 / Ns) of every stage (j / Ns by __umulhi)
 };
 
-// grid: (14, nrx, nsf) workgroups
+// grid: (2 nsymb, nrx, nsf) workgroups
 hipError_t ofdm_rx_launch(const OfdmArgs& a, uint32_t nsf, hipStream_t stream);
 
-// modulator: in = grid [sf][port][14][nre], out = samples [sf][port][sf_len], nrx = ports, norm = scale;
-// grid (14, ports, nsf) workgroups
+// modulator: in = grid [sf][port][2 nsymb][nre], out = samples [sf][port][sf_len], nrx = ports, norm = scale;
+// grid (2 nsymb, ports, nsf) workgroups
 hipError_t ofdm_tx_launch(const OfdmArgs& a, uint32_t nsf, hipStream_t stream);
 
 // factor N into radices 8/4/3/2 (largest first); returns the number of stages or -1

@@ -114,8 +114,8 @@ __global__ __launch_bounds__(OFDM_THREADS) void ofdm_rx_kernel(OfdmArgs a)
 {
   __shared__ float2 buf[2][OFDM_MAX_N];
   const uint32_t    sym = blockIdx.x, rx = blockIdx.y, sf = blockIdx.z;
-  const uint32_t    N = a.N, slot = sym / 7, i = sym % 7;
-  const uint32_t    slot_sz = 7 * N + a.cp0 + 6 * a.cp;
+  const uint32_t    N = a.N, ns = a.nsymb, slot = sym / ns, i = sym % ns;
+  const uint32_t    slot_sz = ns * N + a.cp0 + (ns - 1) * a.cp;
   const uint32_t    off     = slot * slot_sz + a.cp0 + i * (N + a.cp);
   const float2*     src     = a.in + ((size_t)sf * a.nrx + rx) * a.sf_len + off;
   for (uint32_t n = threadIdx.x; n < N; n += OFDM_THREADS) {
@@ -148,7 +148,7 @@ __global__ __launch_bounds__(OFDM_THREADS) void ofdm_rx_kernel(OfdmArgs a)
     cur ^= 1;
     __syncthreads();
   }
-  float2*        dst  = a.out + (((size_t)sf * a.nrx + rx) * 14 + sym) * a.nre;
+  float2*        dst  = a.out + (((size_t)sf * a.nrx + rx) * 2 * ns + sym) * a.nre;
   const uint32_t half = a.nre / 2;
   for (uint32_t k = threadIdx.x; k < a.nre; k += OFDM_THREADS) {
     const uint32_t bin = k < half ? N - half + k : k - half + 1;
@@ -169,8 +169,8 @@ __global__ __launch_bounds__(OFDM_THREADS) void ofdm_tx_kernel(OfdmArgs a)
 {
   __shared__ float2 buf[2][OFDM_MAX_N];
   const uint32_t    sym = blockIdx.x, port = blockIdx.y, sf = blockIdx.z;
-  const uint32_t    N = a.N, slot = sym / 7, i = sym % 7, half = a.nre / 2;
-  const float2*     src = a.in + (((size_t)sf * a.nrx + port) * 14 + sym) * a.nre;
+  const uint32_t    N = a.N, ns = a.nsymb, slot = sym / ns, i = sym % ns, half = a.nre / 2;
+  const float2*     src = a.in + (((size_t)sf * a.nrx + port) * 2 * ns + sym) * a.nre;
   for (uint32_t n = threadIdx.x; n < N; n += OFDM_THREADS) {
     buf[0][n] = make_float2(0.f, 0.f);
   }
@@ -198,7 +198,7 @@ __global__ __launch_bounds__(OFDM_THREADS) void ofdm_tx_kernel(OfdmArgs a)
     cur ^= 1;
     __syncthreads();
   }
-  const uint32_t slot_sz = 7 * N + a.cp0 + 6 * a.cp;
+  const uint32_t slot_sz = ns * N + a.cp0 + (ns - 1) * a.cp;
   const uint32_t off     = slot * slot_sz + a.cp0 + i * (N + a.cp);
   const uint32_t cpl     = i == 0 ? a.cp0 : a.cp;
   float2*        dst     = a.out + ((size_t)sf * a.nrx + port) * a.sf_len;
@@ -214,10 +214,10 @@ __global__ __launch_bounds__(OFDM_THREADS) void ofdm_tx_kernel(OfdmArgs a)
 
 hipError_t ofdm_tx_launch(const OfdmArgs& a, uint32_t nsf, hipStream_t stream)
 {
-  if (a.N > OFDM_MAX_N || a.nstages <= 0 || nsf == 0) {
+  if (a.N > OFDM_MAX_N || a.nstages <= 0 || nsf == 0 || (a.nsymb != 7 && a.nsymb != 6)) {
     return hipErrorInvalidValue;
   }
-  hipLaunchKernelGGL(ofdm_tx_kernel, dim3(14, a.nrx, nsf), dim3(OFDM_THREADS), 0, stream, a);
+  hipLaunchKernelGGL(ofdm_tx_kernel, dim3(2 * a.nsymb, a.nrx, nsf), dim3(OFDM_THREADS), 0, stream, a);
   return hipGetLastError();
 }
 
@@ -258,10 +258,10 @@ int ofdm_plan(uint32_t N, int* radix)
 hipError_t ofdm_rx_launch(const OfdmArgs& a, uint32_t nsf, hipStream_t stream)
 {
   StageScope timing_scope(ST_OFDM, stream);
-  if (a.N > OFDM_MAX_N || a.nstages <= 0 || nsf == 0) {
+  if (a.N > OFDM_MAX_N || a.nstages <= 0 || nsf == 0 || (a.nsymb != 7 && a.nsymb != 6)) {
     return hipErrorInvalidValue;
   }
-  hipLaunchKernelGGL(ofdm_rx_kernel, dim3(14, a.nrx, nsf), dim3(OFDM_THREADS), 0, stream, a);
+  hipLaunchKernelGGL(ofdm_rx_kernel, dim3(2 * a.nsymb, a.nrx, nsf), dim3(OFDM_THREADS), 0, stream, a);
   return hipGetLastError();
 }
 

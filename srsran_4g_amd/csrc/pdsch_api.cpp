@@ -136,6 +136,7 @@ int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sf
 {
   PdschGpu*      g   = (PdschGpu*)q->gpu;
   const uint32_t nrx = q->nof_rx_antennas, np = q->cell.nof_ports, nre = 12 * q->cell.nof_prb;
+  const uint32_t nsf_rows = 2 * SRSRAN_CP_NSYMB(q->cell.cp);  // grid symbols per subframe (14 / 12)
   std::vector<const Table*> tabs(nsf);
   std::vector<PredArgs>     pa(nsf);
   uint32_t                  max_re = 0;
@@ -199,9 +200,9 @@ int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sf
     a.noise_ptr = f.cfg->decoder_type == SRSRAN_MIMO_DECODER_ZF ? nullptr : f.d_noise;
     a.rho_b_inv = rho_b_inv;
     a.ce_row    = f.ce_full ? 0 : nre;
-    const size_t ce_len = f.ce_full ? (size_t)14 * nre : nre;
+    const size_t ce_len = f.ce_full ? (size_t)nsf_rows * nre : nre;
     for (uint32_t r = 0; r < nrx; r++) {
-      a.y[r] = (const float2*)f.d_grid + (size_t)r * 14 * nre;
+      a.y[r] = (const float2*)f.d_grid + (size_t)r * nsf_rows * nre;
       for (uint32_t p = 0; p < np; p++) {
         a.h[p][r] = (const float2*)f.d_ce + (size_t)(p * nrx + r) * ce_len;
       }
@@ -324,7 +325,7 @@ int srsran_pdsch_init_ue(srsran_pdsch_t* q, uint32_t max_prb, uint32_t nof_rx_an
   }
   memset(q, 0, sizeof(*q));
   q->nof_rx_antennas = nof_rx_antennas;
-  q->max_re          = max_prb * 14 * SRSRAN_NRE;
+  q->max_re          = max_prb * 2 * SRSRAN_CP_NORM_NSYMB * SRSRAN_NRE;
   q->is_ue           = true;
   if (gold_tables_init() != hipSuccess || srsran_sch_init(&q->dl_sch)) {
     fprintf(stderr, "[srsran_pdsch] no HIP device available\n");
@@ -375,9 +376,12 @@ int srsran_pdsch_set_cell(srsran_pdsch_t* q, srsran_cell_t cell)
       cell.nof_ports > 2 || cell.id > 503) {
     return SRSRAN_ERROR_INVALID_INPUTS;
   }
-  if (cell.cp != SRSRAN_CP_NORM || cell.frame_type != SRSRAN_FDD) {
-    fprintf(stderr, "[srsran_pdsch] only normal-CP FDD cells are provided\n");
+  if (cell.frame_type != SRSRAN_FDD) {
+    fprintf(stderr, "[srsran_pdsch] only FDD cells are provided\n");
     return SRSRAN_ERROR;
+  }
+  if (cell.cp != SRSRAN_CP_NORM && cell.cp != SRSRAN_CP_EXT) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
   }
   PdschGpu* g = (PdschGpu*)q->gpu;
   hipDeviceSynchronize();
@@ -386,7 +390,7 @@ int srsran_pdsch_set_cell(srsran_pdsch_t* q, srsran_cell_t cell)
   }
   g->tables.clear();
   q->cell   = cell;
-  q->max_re = cell.nof_prb * 14 * SRSRAN_NRE;
+  q->max_re = SRSRAN_SF_LEN_RE(cell.nof_prb, cell.cp);
   return SRSRAN_SUCCESS;
 }
 
@@ -405,7 +409,7 @@ int srsran_pdsch_decode(srsran_pdsch_t*        q,
     return SRSRAN_ERROR;
   }
   PdschGpu*      g   = (PdschGpu*)q->gpu;
-  const uint32_t nrx = q->nof_rx_antennas, np = q->cell.nof_ports, nsym = 14 * 12 * q->cell.nof_prb;
+  const uint32_t nrx = q->nof_rx_antennas, np = q->cell.nof_ports, nsym = SRSRAN_SF_LEN_RE(q->cell.nof_prb, q->cell.cp);
   if (cfg->max_nof_iterations) {
     srsran_sch_set_max_noi(&q->dl_sch, cfg->max_nof_iterations);
   }
@@ -555,7 +559,7 @@ int srsran_pdsch_encode(srsran_pdsch_t*     q,
   PdschGpu*             g      = (PdschGpu*)q->gpu;
   const uint32_t        lstart = sf->cfi + (cell.nof_prb < 10 ? 1 : 0);
   std::vector<uint32_t> tab    = pdsch_re_table(cell, gr, lstart, sf->tti % 10);
-  const uint32_t        nre = (uint32_t)tab.size(), nsf_re = 14 * 12 * cell.nof_prb;
+  const uint32_t        nre = (uint32_t)tab.size(), nsf_re = SRSRAN_SF_LEN_RE(cell.nof_prb, cell.cp);
   if (nre != gr.nof_re || nre > q->max_re) {
     fprintf(stderr, "[srsran_pdsch] Error expecting %u symbols but got %u\n", gr.nof_re, nre);
     return SRSRAN_ERROR;

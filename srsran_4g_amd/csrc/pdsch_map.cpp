@@ -15,7 +15,11 @@
 
 namespace srsran_amd {
 
-static bool symbol_has_ref(uint32_t l, uint32_t nof_ports) { return (l == 1 && nof_ports == 4) || l == 0 || l == 4; }
+// SRSRAN_SYMBOL_HAS_REF (phy_common.h): l = 0 and l = nsymb - 3 of each slot (+ l = 1 with 4 ports)
+static bool symbol_has_ref(uint32_t l, uint32_t nsymb, uint32_t nof_ports)
+{
+  return (l == 1 && nof_ports == 4) || l == 0 || l == nsymb - 3;
+}
 
 static bool skip_symbol(const srsran_cell_t& cell, const srsran_pdsch_grant_t& g, uint32_t sf_idx, uint32_t s,
                         uint32_t l, uint32_t n)
@@ -70,7 +74,7 @@ std::vector<uint32_t> pdsch_re_table(const srsran_cell_t& cell, const srsran_pds
   for (uint32_t s = 0; s < 2; s++) {
     const uint32_t lstart = s == 0 ? lstart_grant : 0;
     for (uint32_t l = lstart; l < g.nof_symb_slot[s]; l++) {
-      const bool     has_crs = symbol_has_ref(l, cell.nof_ports);
+      const bool     has_crs = symbol_has_ref(l, SRSRAN_CP_NSYMB(cell.cp), cell.nof_ports);
       const uint32_t flag    = has_crs ? 0x80000000u : 0u;
       const uint32_t crs_off = !has_crs ? 0 : cell.nof_ports == 1 ? (l == 0 ? cell.id % 6 : (cell.id + 3) % 6) : cell.id % 3;
       const uint32_t lp      = l + s * g.nof_symb_slot[0];

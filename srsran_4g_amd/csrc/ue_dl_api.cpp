@@ -293,8 +293,9 @@ int srsran_ue_dl_gpu_decode_batch(srsran_ue_dl_t*              q,
   hipMemcpyAsync(g->d_sf, g->h_sf, nof_sf * sizeof(uint32_t), hipMemcpyHostToDevice, s);
   hipEventRecord(g->staged, s);
   const size_t nre = 12 * (size_t)q->cell.nof_prb, nrx = q->nof_rx_antennas, np = q->cell.nof_ports;
+  const size_t rows = 2 * SRSRAN_CP_NSYMB(q->cell.cp);  // grid symbols per subframe
   if (srsran_ofdm_rx_gpu(&q->fft[0], d_samples, (cf_t*)g->d_grid, (uint32_t)nrx, nof_sf, cfo, stream) ||
-      srsran_chest_dl_gpu_estimate_batch(&q->chest, g->d_sf, nof_sf, (const cf_t*)g->d_grid, nrx * 14 * nre,
+      srsran_chest_dl_gpu_estimate_batch(&q->chest, g->d_sf, nof_sf, (const cf_t*)g->d_grid, nrx * rows * nre,
                                          (cf_t*)g->d_ce, np * nrx * nre, g->d_res, stream)) {
     return SRSRAN_ERROR;
   }
@@ -305,7 +306,7 @@ int srsran_ue_dl_gpu_decode_batch(srsran_ue_dl_t*              q,
     f.cfg     = sfs[b].pdsch_cfg;
     f.tti     = sfs[b].tti;
     f.cfi     = sfs[b].cfi;
-    f.d_grid  = (const cf_t*)(g->d_grid + b * nrx * 14 * nre);
+    f.d_grid  = (const cf_t*)(g->d_grid + b * nrx * rows * nre);
     f.d_ce    = (const cf_t*)(g->d_ce + b * np * nrx * nre);
     f.ce_full = 0;
     f.d_noise = g->d_res + 4 * b;

@@ -192,10 +192,11 @@ def symbol_size_is_standard():
     return bool(lib().srsran_symbol_size_is_standard())
 
 
-def cell(nof_prb=100, nof_ports=2, cell_id=1, phich_res=2):
-    """FDD, normal CP, normal PHICH duration, Ng = 1 (phich_res 2) as the reference's test cells"""
+def cell(nof_prb=100, nof_ports=2, cell_id=1, phich_res=2, cp=0):
+    """FDD, normal CP (cp=1: extended), normal PHICH duration, Ng = 1 (phich_res 2) as the reference's
+    test cells"""
     c = srsran_cell_t()
-    c.nof_prb, c.nof_ports, c.id = nof_prb, nof_ports, cell_id
+    c.nof_prb, c.nof_ports, c.id, c.cp = nof_prb, nof_ports, cell_id, cp
     c.phich_resources = phich_res
     return c
 
@@ -215,10 +216,11 @@ def srsue_chest_cfg():
 class OfdmRx:
     """srsran_ofdm_t receiver (srsran_ue_dl configuration)."""
 
-    def __init__(self, nof_prb, normalize=False):
+    def __init__(self, nof_prb, normalize=False, cp=0):
         self.cfg = srsran_ofdm_cfg_t()
         self.cfg.nof_prb = nof_prb
         self.cfg.normalize = normalize
+        self.cfg.cp = cp
         self.q = srsran_ofdm_t()
         if lib().srsran_ofdm_rx_init_cfg(ctypes.byref(self.q), ctypes.byref(self.cfg)):
             raise RuntimeError("srsran_ofdm_rx_init_cfg failed")
@@ -230,7 +232,7 @@ class OfdmRx:
     def rx(self, samples):
         x = np.ascontiguousarray(samples, np.complex64)
         assert x.size == self.q.sf_sz
-        out = np.zeros(14 * self.q.nof_re, np.complex64)
+        out = np.zeros(2 * self.q.nof_symbols * self.q.nof_re, np.complex64)
         lib().srsran_ofdm_rx_sf_ng(ctypes.byref(self.q), x.ctypes.data, out.ctypes.data)
         return out
 
@@ -282,7 +284,7 @@ class ChestDl:
                                                     ctypes.addressof(ptrs), ctypes.byref(self.res))
         if rc:
             raise RuntimeError(f"srsran_chest_dl_estimate failed ({rc})")
-        n = 14 * 12 * self.cell.nof_prb
+        n = (12 if self.cell.cp else 14) * 12 * self.cell.nof_prb
         ce = np.zeros((self.cell.nof_ports, self.nrx, n), np.complex64)
         for p in range(self.cell.nof_ports):
             for r in range(self.nrx):
@@ -307,9 +309,9 @@ MOD_FROM_QM = {1: 0, 2: 1, 4: 2, 6: 3, 8: 4}
 
 
 def pdsch_cfg(nof_prb, nof_re, tbs, Qm, rv=(0, 0), scheme="cdd", pmi=0, rnti=0x1234, max_iterations=8,
-              csi_enable=True, power_scale=False, p_a=0.0, p_b=0, softbuffers=(), zf=False):
+              csi_enable=True, power_scale=False, p_a=0.0, p_b=0, softbuffers=(), zf=False, cp=0):
     """srsran_pdsch_cfg_t for a full-bandwidth grant of len(tbs) codewords on as many layers
-    (srsUE defaults: csi_enable, 8 half-iterations, MMSE, no power scaling)."""
+    (srsUE defaults: csi_enable, 8 half-iterations, MMSE, no power scaling); cp=1: extended CP."""
     c = srsran_pdsch_cfg_t()
     g = c.grant
     g.tx_scheme = SCHEME[scheme]
@@ -319,7 +321,7 @@ def pdsch_cfg(nof_prb, nof_re, tbs, Qm, rv=(0, 0), scheme="cdd", pmi=0, rnti=0x1
             g.prb_idx[s][n] = True
     g.nof_prb = nof_prb
     g.nof_re = nof_re
-    g.nof_symb_slot[0] = g.nof_symb_slot[1] = 7
+    g.nof_symb_slot[0] = g.nof_symb_slot[1] = 6 if cp else 7
     g.nof_tb = len(tbs)
     g.nof_layers = 2 if scheme == "diversity" else len(tbs)
     for i, t in enumerate(tbs):
@@ -451,7 +453,7 @@ class UeDl:
         return r, g
 
     def grids(self):
-        n = 14 * 12 * self.cell.nof_prb
+        n = (12 if self.cell.cp else 14) * 12 * self.cell.nof_prb
         out = np.zeros((self.nrx, n), np.complex64)
         for r in range(self.nrx):
             ctypes.memmove(out[r].ctypes.data, self.q.sf_symbols[r], n * 8)

@@ -176,60 +176,67 @@ def crs_shift(port, l):
     raise ValueError(port)
 
 
-def crs_symbols(nports):
-    return [0, 4] if nports <= 2 else [0, 1, 4]
+def crs_symbols(nports, nsymb=7):
+    return [0, nsymb - 3] if nports <= 2 else [0, 1, nsymb - 3]
 
 
-def crs_values(cell_id, nof_prb, ns, l):
-    c = gold((1 << 10) * (7 * (ns + 1) + l + 1) * (2 * cell_id + 1) + 2 * cell_id + 1, 4 * 110)
+def crs_values(cell_id, nof_prb, ns, l, cp=0):
+    # 36.211 6.10.1.1: N_CP = 1 normal, 0 extended cyclic prefix
+    c = gold((1 << 10) * (7 * (ns + 1) + l + 1) * (2 * cell_id + 1) + 2 * cell_id + (0 if cp else 1), 4 * 110)
     m = np.arange(2 * nof_prb) + 110 - nof_prb
     return ((1 - 2.0 * c[2 * m]) + 1j * (1 - 2.0 * c[2 * m + 1])) / math.sqrt(2)
 
 
-def crs_grid(cell_id, nof_prb, nports, port, sf_idx):
-    """port's CRS in a (14, 12 N_RB) grid (2 ports max)"""
-    g = np.zeros((14, 12 * nof_prb), np.complex128)
+def crs_grid(cell_id, nof_prb, nports, port, sf_idx, cp=0):
+    """port's CRS in a (2 nsymb, 12 N_RB) grid (2 ports max; nsymb 7, or 6 with cp=1 extended)"""
+    ns = 6 if cp else 7
+    g = np.zeros((2 * ns, 12 * nof_prb), np.complex128)
     for s in range(2):
-        for l in crs_symbols(nports):
-            k = 6 * np.arange(2 * nof_prb) + (crs_shift(port, l) + cell_id % 6) % 6
-            g[7 * s + l, k] = crs_values(cell_id, nof_prb, 2 * sf_idx + s, l)
+        for l in crs_symbols(nports, ns):
+            k = 6 * np.arange(2 * nof_prb) + (crs_shift(port, 0 if l == 0 else 4) + cell_id % 6) % 6
+            g[ns * s + l, k] = crs_values(cell_id, nof_prb, 2 * sf_idx + s, l, cp)
     return g
 
 
-def pdsch_mask(nof_prb, nports, cell_id, cfi, sf_idx, prb=None):
-    """(14, 12 N_RB) bool: REs that carry PDSCH"""
+def pdsch_mask(nof_prb, nports, cell_id, cfi, sf_idx, prb=None, cp=0):
+    """(2 nsymb, 12 N_RB) bool: REs that carry PDSCH"""
     assert nof_prb % 2 == 0 or sf_idx not in (0, 5), "odd N_RB centre PRBs not generated"
+    ns = 6 if cp else 7
     nre = 12 * nof_prb
-    m = np.zeros((14, nre), bool)
+    m = np.zeros((2 * ns, nre), bool)
     prb = np.ones(nof_prb, bool) if prb is None else np.asarray(prb, bool)
     m[:, np.repeat(prb, 12)] = True
     m[: cfi + (1 if nof_prb < 10 else 0)] = False
     k = np.arange(nre)
     for s in range(2):
-        for l in crs_symbols(nports):
+        for l in crs_symbols(nports, ns):
             if nports == 1:
-                m[7 * s + l, (k % 6) == (crs_shift(0, l) + cell_id % 6) % 6] = False
+                m[ns * s + l, (k % 6) == (crs_shift(0, 0 if l == 0 else 4) + cell_id % 6) % 6] = False
             else:
-                m[7 * s + l, (k % 3) == cell_id % 3] = False
+                m[ns * s + l, (k % 3) == cell_id % 3] = False
     lo, hi = 12 * (nof_prb // 2 - 3), 12 * (nof_prb // 2 + 3)
     if sf_idx in (0, 5):
-        m[5:7, lo:hi] = False  # SSS, PSS
+        m[ns - 2:ns, lo:hi] = False  # SSS, PSS
     if sf_idx == 0:
-        m[7:11, lo:hi] = False  # PBCH
+        m[ns:ns + 4, lo:hi] = False  # PBCH
     return m
 
 
-def ofdm_tx(grid, N):
-    grid = np.asarray(grid).reshape(14, -1)
+def ofdm_tx(grid, N, cp=0):
+    ns = 6 if cp else 7
+    grid = np.asarray(grid).reshape(2 * ns, -1)
     nre = grid.shape[1]
-    cp0, cp = math.ceil(160 * N / 2048), math.ceil(144 * N / 2048)
+    if cp:
+        cp0 = cpl = math.ceil(512 * N / 2048)
+    else:
+        cp0, cpl = math.ceil(160 * N / 2048), math.ceil(144 * N / 2048)
     out = []
-    for l in range(14):
+    for l in range(2 * ns):
         X = np.zeros(N, np.complex128)
         X[N - nre // 2:] = grid[l, : nre // 2]
         X[1: nre // 2 + 1] = grid[l, nre // 2:]
         t = np.fft.ifft(X)
-        c = cp0 if l % 7 == 0 else cp
+        c = cp0 if l % ns == 0 else cpl
         out += [t[N - c:], t]
     return np.concatenate(out)
 
@@ -265,32 +272,32 @@ def pcfich_res(nof_prb, cell_id):
     return np.array(out)
 
 
-def pcfich_grids(nof_prb, cell_id, nports, sf_idx, cfi):
-    """Per-port (14, 12 N_RB) grids carrying only the PCFICH of `cfi`."""
+def pcfich_grids(nof_prb, cell_id, nports, sf_idx, cfi, cp=0):
+    """Per-port (2 nsymb, 12 N_RB) grids carrying only the PCFICH of `cfi`."""
     bits = np.array(CFI_CODEWORDS[cfi - 1], np.uint8) ^ gold((sf_idx + 1) * (2 * cell_id + 1) * 512 + cell_id, 32)
     d = modulate(bits, 2)
     ports = precode([d], "diversity") if nports == 2 else [d]
     k = pcfich_res(nof_prb, cell_id)
     grids = []
     for p in range(nports):
-        g = np.zeros((14, 12 * nof_prb), np.complex128)
+        g = np.zeros((12 if cp else 14, 12 * nof_prb), np.complex128)
         g[0, k] = ports[p]
         grids.append(g)
     return grids
 
 
 def pdsch_subframe(nof_prb, cell_id, nports, tti, cfi, rnti, tbs, Qm, rv, payloads, scheme="cdd", codebook=1,
-                   nrx=2, snr_db=None, rng=None, N=None, channel=None, cfo=0.0, pcfich=True, ctrl=None):
+                   nrx=2, snr_db=None, rng=None, N=None, channel=None, cfo=0.0, pcfich=True, ctrl=None, cp=0):
     """One PDSCH subframe through OFDM and a static MIMO channel.
 
     payloads: one uint8 array (tbs/8 bytes) per codeword.  channel: (nrx, nports) complex matrix
     (default: [[1, 1], [1, -1]] for 2 ports as phy_dl_test.c:568-583 uses, ones for 1 port).
     pcfich: also transmit the PCFICH of `cfi`; ctrl: optional per-port (14, 12 N_RB) grids added
-    before the OFDM modulator (e.g. a PDCCH control region).
+    before the OFDM modulator (e.g. a PDCCH control region); cp=1: extended cyclic prefix.
     Returns (samples[nrx, sf_len] complex64, nof_re)."""
     N = N or symbol_sz(nof_prb)
     sf_idx = tti % 10
-    mask = pdsch_mask(nof_prb, nports, cell_id, cfi, sf_idx)
+    mask = pdsch_mask(nof_prb, nports, cell_id, cfi, sf_idx, cp=cp)
     nof_re = int(mask.sum())
     layers = []
     for q, pl in enumerate(payloads):
@@ -302,15 +309,15 @@ def pdsch_subframe(nof_prb, cell_id, nports, tti, cfi, rnti, tbs, Qm, rv, payloa
     if len(ports) != nports:
         raise ValueError("scheme / port count mismatch")
     tx = []
-    pc = pcfich_grids(nof_prb, cell_id, nports, sf_idx, cfi) if pcfich else None
+    pc = pcfich_grids(nof_prb, cell_id, nports, sf_idx, cfi, cp) if pcfich else None
     for p in range(nports):
-        g = crs_grid(cell_id, nof_prb, nports, p, sf_idx)
+        g = crs_grid(cell_id, nof_prb, nports, p, sf_idx, cp)
         g[mask] = ports[p]
         if pc is not None:
             g = g + pc[p]
         if ctrl is not None:
             g = g + ctrl[p]
-        tx.append(ofdm_tx(g, N))
+        tx.append(ofdm_tx(g, N, cp))
     H = np.asarray(channel if channel is not None else
                    ([[1, 1], [1, -1]] if nports == 2 else [[1]] * nrx), np.complex128)
     rx = H @ np.stack(tx)

@@ -48,3 +48,25 @@ def test_oracle_chain_tm2_diversity(ora):
     g, ce, st = PC.fft_estimate(ora, x, 100, 4, 2, 5)
     res = PC.pdsch_decode(ora, g, ce, st["noise"], 100, 4, 2, 5, 1, 0x1234, [TBS], [6], [0], scheme="diversity")
     assert res[0]["ret"] == 0 and np.array_equal(res[0]["data"][: TBS // 8], pl[0])
+
+
+@pytest.mark.parametrize("tti,cfi,nports,scheme,tbs,Qm", [(1, 1, 2, "cdd", 55056, 6), (10, 2, 2, "cdd", 46888, 6),
+                                                          (5, 3, 2, "diversity", 46888, 6), (2, 1, 1, "port0", 30576, 4)])
+def test_oracle_chain_extended_cp(ora, tti, cfi, nports, scheme, tbs, Qm):
+    """extended cyclic prefix (6 symbols a slot, CRS in l = 0 / 3, N_cp = 0 in the CRS c_init,
+    cp = 512 N / 2048): synth -> numpy OFDM -> oracle estimator -> oracle PDSCH decode"""
+    rng = np.random.default_rng(tti + 40)
+    ncw = 2 if scheme == "cdd" else 1
+    pls = [rng.integers(0, 256, tbs // 8, dtype=np.uint8) for _ in range(ncw)]
+    ch = [[1], [0.5 + 0.5j]] if nports == 1 else None
+    x, nre = S.pdsch_subframe(100, 9, nports, tti, cfi, 0x1234, tbs, Qm, 0, pls, scheme=scheme, codebook=1,
+                              snr_db=30.0, rng=rng, channel=ch, cp=1)
+    assert x.shape[1] == 2 * (6 * 2048 + 6 * 512)
+    g, ce, st = PC.fft_estimate(ora, x, 100, 9, nports, tti, cp=1)
+    assert g.shape[1] == 12 * 1200
+    res = PC.pdsch_decode(ora, g, ce, st["noise"], 100, 9, nports, tti, cfi, 0x1234, [tbs] * ncw, [Qm] * ncw,
+                          [0] * ncw, scheme=scheme, cp=1)
+    for q in range(ncw):
+        assert res[q]["ret"] == 0
+        assert np.array_equal(res[q]["data"][: tbs // 8], pls[q])
+    assert res[0]["nof_re"] == nre

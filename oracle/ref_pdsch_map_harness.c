@@ -1,0 +1,107 @@
+/*
+ * oracle/ref_pdsch_map_harness.c -- TEST INFRASTRUCTURE ONLY (linked into oracle/_ref/libsrsref.so).
+ *
+ * Pins the product's PDSCH RE map (srsran_4g_amd/csrc/pdsch_map.cpp) to the reference's own PRB copy
+ * routines, phch/prb_dl.c (prb_cp_ref / prb_cp / prb_cp_half, compiled from /root/reference).  pdsch.c
+ * itself includes the CMake-generated srsran/srsran.h and is not buildable here, so its slot / symbol /
+ * PRB walk (srsran_pdsch_cp, pdsch.c:136-220, with pdsch_cp_skip_symbol :83-112 and
+ * pdsch_cp_crs_offset :114-133) is restated below around the reference's copy routines.  The grid
+ * handed to the walk holds each RE's own index in its real part, so the extracted symbol array is the
+ * list of grid indices srsran_pdsch_get reads, in order.
+ */
+#include <complex.h>
+#include <stdbool.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "srsran/phy/common/phy_common.h"
+
+void prb_cp_ref(cf_t** input, cf_t** output, int offset, int nof_refs, int nof_intervals, bool advance_input);
+void prb_cp(cf_t** input, cf_t** output, int nof_prb);
+void prb_cp_half(cf_t** input, cf_t** output, int nof_prb);
+
+/* pdsch.c:83-112 */
+static bool skip_symbol(uint32_t nof_prb, bool fdd, uint32_t nsymb, uint32_t sf_idx, uint32_t s, uint32_t l,
+                        uint32_t n)
+{
+  if (n >= nof_prb / 2 - 3 && n < nof_prb / 2 + 3 + (nof_prb % 2)) {
+    if (fdd) {
+      if (s == 0 && (sf_idx == 0 || sf_idx == 5) && l >= nsymb - 2) {
+        return true;
+      }
+    } else {
+      if (s == 1 && (sf_idx == 0 || sf_idx == 5) && l >= nsymb - 1) {
+        return true;
+      }
+      if (s == 0 && (sf_idx == 1 || sf_idx == 6) && l == 2) {
+        return true;
+      }
+    }
+    if (s == 1 && sf_idx == 0 && l < 4) {
+      return true;
+    }
+  }
+  return false;
+}
+
+/* srsran_pdsch_cp in the get direction (pdsch.c:136-220) over an index-valued grid.
+ * prb_mask: [2][nof_prb] bytes.  Returns the number of PDSCH REs; idx[] receives their grid indices. */
+int ref_pdsch_get_indices(uint32_t nof_prb, uint32_t nof_ports, uint32_t cell_id, uint32_t cp, uint32_t lstart_grant,
+                          uint32_t sf_idx, const uint8_t* prb_mask, uint32_t* idx, uint32_t max_len)
+{
+  const srsran_cp_t cpt      = cp ? SRSRAN_CP_EXT : SRSRAN_CP_NORM;
+  const uint32_t    nsymb    = SRSRAN_CP_NSYMB(cpt);
+  const uint32_t    nsf      = 2 * nsymb * SRSRAN_NRE * nof_prb;
+  const uint32_t    nof_refs = nof_ports == 1 ? 2 : 4;
+  static cf_t       grid[2 * SRSRAN_CP_NORM_NSYMB * SRSRAN_NRE * SRSRAN_MAX_PRB];
+  static cf_t       out[2 * SRSRAN_CP_NORM_NSYMB * SRSRAN_NRE * SRSRAN_MAX_PRB];
+  if (nof_prb == 0 || nof_prb > SRSRAN_MAX_PRB) {
+    return -1;
+  }
+  for (uint32_t i = 0; i < nsf; i++) {
+    grid[i] = (float)i;
+  }
+  cf_t* in_ptr  = grid;
+  cf_t* out_ptr = out;
+  for (uint32_t s = 0; s < SRSRAN_NOF_SLOTS_PER_SF; s++) {
+    const uint32_t lstart = s == 0 ? lstart_grant : 0;
+    for (uint32_t l = lstart; l < nsymb; l++) {
+      const bool     has_crs = SRSRAN_SYMBOL_HAS_REF(l, cpt, nof_ports);
+      const uint32_t crs_off = !has_crs ? 0 : nof_ports == 1 ? (l == 0 ? cell_id % 6 : (cell_id + 3) % 6) : cell_id % 3;
+      const uint32_t lp      = l + s * nsymb;
+      for (uint32_t n = 0; n < nof_prb; n++) {
+        if (!prb_mask[s * nof_prb + n]) {
+          continue;
+        }
+        in_ptr = &grid[(lp * nof_prb + n) * SRSRAN_NRE];
+        if (!skip_symbol(nof_prb, true, nsymb, sf_idx, s, l, n)) {
+          if (has_crs) {
+            prb_cp_ref(&in_ptr, &out_ptr, (int)crs_off, (int)nof_refs, (int)nof_refs, false);
+          } else {
+            prb_cp(&in_ptr, &out_ptr, 1);
+          }
+        } else if (nof_prb % 2 != 0) {
+          if (n == nof_prb / 2 - 3) {
+            if (has_crs) {
+              prb_cp_ref(&in_ptr, &out_ptr, (int)crs_off, (int)nof_refs, (int)nof_refs / 2, false);
+            } else {
+              prb_cp_half(&in_ptr, &out_ptr, 1);
+            }
+          } else if (n == nof_prb / 2 + 3) {
+            in_ptr += SRSRAN_NRE / 2;
+            if (has_crs) {
+              prb_cp_ref(&in_ptr, &out_ptr, (int)crs_off, (int)nof_refs, (int)nof_refs / 2, false);
+            } else {
+              prb_cp_half(&in_ptr, &out_ptr, 1);
+            }
+          }
+        }
+      }
+    }
+  }
+  const int n = (int)(out_ptr - out);
+  for (int i = 0; i < n && (uint32_t)i < max_len; i++) {
+    idx[i] = (uint32_t)crealf(out[i]);
+  }
+  return n;
+}

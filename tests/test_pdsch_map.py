@@ -1,12 +1,15 @@
 """CPU test of the PDSCH RE map (host code in srsran_4g_amd/csrc/pdsch_map.cpp, a restatement
 of srsran_pdsch_cp, pdsch.c:136-220) against an independent rule-based restatement
-(oracle/pdsch_np.py): cells of 6..100 PRB (odd and even), 1/2/4 ports, all subframes, CFI 1..3,
-full and partial PRB allocations."""
+(oracle/pdsch_np.py) and against the reference's own PRB copy routines (prb_dl.c compiled into
+oracle/_ref, driven by oracle/ref_pdsch_map_harness.c): cells of 6..100 PRB (odd and even), 1/2/4
+ports, normal and extended CP, all subframes, CFI 1..3, full and partial PRB allocations."""
 import ctypes
+import os
 
 import numpy as np
 import pytest
 
+import oracle as ORA
 import pdsch_np
 from srsran_4g_amd import sch as S
 from srsran_4g_amd import ue_dl as U
@@ -109,3 +112,32 @@ def test_ra_nof_re_matches_re_map(cp, nof_prb):
                     continue
                 n_map = len(pdsch_np.re_table(nof_prb, nports, cell_id, mask, lstart, tti, cp=cp))
                 assert ra_nof_re(nof_prb, nports, cell_id, mask, cfi, tti, cp) == n_map, (nports, tti, cfi)
+
+
+def ref_table(nof_prb, nports, cell_id, mask, lstart, sf_idx, cp):
+    R = ctypes.CDLL(ORA.REF_SO, mode=os.RTLD_LAZY)
+    f = R.ref_pdsch_get_indices
+    f.argtypes = [ctypes.c_uint32] * 6 + [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]
+    f.restype = ctypes.c_int
+    m = np.ascontiguousarray(np.asarray(mask, np.uint8).reshape(2, nof_prb))
+    out = np.zeros(2 * 7 * 12 * nof_prb, np.uint32)
+    n = f(nof_prb, nports, cell_id, cp, lstart, sf_idx, m.ctypes.data, out.ctypes.data, out.size)
+    return out[:n]
+
+
+@pytest.mark.skipif(not ORA.ref_available(), reason="oracle/_ref not built")
+@pytest.mark.parametrize("cp", [0, 1])
+@pytest.mark.parametrize("nof_prb", [6, 15, 25, 27, 50, 75, 100])
+def test_re_table_matches_reference_prb_dl(cp, nof_prb):
+    """pdsch_map.cpp == the reference's prb_cp_ref / prb_cp / prb_cp_half walk, index for index"""
+    rng = np.random.default_rng(nof_prb + 7 * cp)
+    for nports in (1, 2, 4):
+        for sf_idx in range(10):
+            for lstart in (1, 2, 3, 4):
+                full = [[1] * nof_prb, [1] * nof_prb]
+                part = [list(rng.integers(0, 2, nof_prb))] * 2
+                for mask in (full, part):
+                    cell_id = int(rng.integers(0, 504))
+                    got = product_table(nof_prb, nports, cell_id, mask, lstart, sf_idx, cp=cp)
+                    want = ref_table(nof_prb, nports, cell_id, mask, lstart, sf_idx, cp)
+                    assert np.array_equal(got & 0x7FFFFFFF, want), (nports, sf_idx, lstart)

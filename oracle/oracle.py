@@ -111,8 +111,9 @@ class _PhyMixin:
         rc = self._predecode(scheme, ya, ha, xa, ca, nrx, nports, nlayers, codebook, n, scaling, noise)
         if rc < 0:
             raise ValueError(rc)
-        if scheme == 1:  # transmit diversity: n/2 symbols per layer, one CSI row for the codeword
-            return xa[:nlayers, : n // 2].copy(), ca[:1].copy()
+        if scheme == 1:  # transmit diversity: n/2 (n/4, 4 ports) symbols per layer, one CSI row
+            m = n // 2 if nlayers == 2 else ((n - 2) // 4 if n % 4 else n // 4)
+            return xa[:nlayers, :m].copy(), ca[:1].copy()
         return xa[:nlayers].copy(), ca[:nlayers].copy()
 
     def sequence_apply_s(self, llr, seed):

@@ -73,10 +73,12 @@ def pdsch_decode(ora, grids, ce, noise, nof_prb, cell_id, nports, tti, cfi, rnti
     h = ce[:, :, idx]
     ntb = len(tbs)
     codebook = pmi if ntb == 1 else pmi + 1
-    if scheme == "diversity":  # 1 codeword on 2 layers, srsran_layerdemap_diversity (layermap.c:138-147)
-        xl, csi = ora.predecode(1, y, h, 2, codebook, scaling, noise)
-        x = np.empty((1, 2 * xl.shape[1]), np.complex64)
-        x[0, 0::2], x[0, 1::2] = xl[0], xl[1]
+    if scheme == "diversity":  # 1 codeword on nports layers, srsran_layerdemap_diversity (layermap.c:138-147)
+        L = nports
+        xl, csi = ora.predecode(1, y, h, L, codebook, scaling, noise)
+        x = np.zeros((1, idx.size), np.complex64)  # 4 ports: a trailing half group stays 0
+        for j in range(L):
+            x[0, j:L * xl.shape[1]:L] = xl[j]
     elif layers == 2 and ntb == 1:  # predecode 2 layers; demap n/2 layer symbols each; CSI of layer 0
         xl, csi = ora.predecode(SCHEME[scheme], y, h, 2, codebook, scaling, noise)
         n = xl.shape[1]

@@ -271,6 +271,46 @@ int oracle_predecode(int          scheme,
     }
     return 0;
   }
+  if (scheme == 1 && nports == 4) {
+    /* srsran_predecoding_diversity_csi, 4 ports (precoding.c:714-775): SFBC + FSTD groups of 4 REs,
+     * ports (0, 2) on REs 4i, 4i+1 and (1, 3) on 4i+2, 4i+3; m_ap groups (a trailing half group is
+     * not decoded: those outputs stay 0 here); CSI a_k * scaling / nof_rxant per RE */
+    if (nlayers != 4 || nrx < 1 || nrx > 4) {
+      return -1;
+    }
+    const int m_ap = (n % 4) ? ((n - 2) / 4) : n / 4;
+    memset(X, 0, sizeof(cpx) * (size_t)4 * n);
+    memset(csi, 0, sizeof(float) * (size_t)n);
+    for (int i = 0; i < m_ap; i++) {
+      cpx   x0 = {0, 0}, x1 = {0, 0}, x2 = {0, 0}, x3 = {0, 0};
+      float a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+      for (int p = 0; p < nrx; p++) {
+        cpx h00 = HH(0, p, 4 * i), h01 = HH(2, p, 4 * i), h10 = HH(0, p, 4 * i + 1), h11 = HH(2, p, 4 * i + 1);
+        a0 += h00.r * h00.r + h00.i * h00.i + h11.r * h11.r + h11.i * h11.i;
+        a1 += h10.r * h10.r + h10.i * h10.i + h01.r * h01.r + h01.i * h01.i;
+        const cpx r0 = Y[(size_t)p * n + 4 * i], r1 = Y[(size_t)p * n + 4 * i + 1];
+        x0           = cadd(x0, cadd(cmul(cconj(h00), r0), cmul(h11, cconj(r1))));
+        x1           = cadd(x1, cadd(cmul(cneg(h01), cconj(r0)), cmul(cconj(h10), r1)));
+        h00          = HH(1, p, 4 * i + 2);
+        h01          = HH(3, p, 4 * i + 2);
+        h10          = HH(1, p, 4 * i + 3);
+        h11          = HH(3, p, 4 * i + 3);
+        a2 += h00.r * h00.r + h00.i * h00.i + h11.r * h11.r + h11.i * h11.i;
+        a3 += h10.r * h10.r + h10.i * h10.i + h01.r * h01.r + h01.i * h01.i;
+        const cpx r2 = Y[(size_t)p * n + 4 * i + 2], r3 = Y[(size_t)p * n + 4 * i + 3];
+        x2           = cadd(x2, cadd(cmul(cconj(h00), r2), cmul(h11, cconj(r3))));
+        x3           = cadd(x3, cadd(cmul(cneg(h01), cconj(r2)), cmul(cconj(h10), r3)));
+      }
+      const float a[4]  = {a0 * scaling, a1 * scaling, a2 * scaling, a3 * scaling};
+      const cpx   xs[4] = {x0, x1, x2, x3};
+      for (int l = 0; l < 4; l++) {
+        csi[4 * i + l]             = a[l] / (float)nrx;
+        X[(size_t)l * n + i] = (cpx){(float)((double)(xs[l].r / a[l]) * 1.41421356237309504880),
+                                     (float)((double)(xs[l].i / a[l]) * 1.41421356237309504880)};
+      }
+    }
+    return 0;
+  }
   if (scheme == 1) {
     if (nports != 2 || nlayers != 2 || nrx < 1 || nrx > 4) {
       return -1;

@@ -159,6 +159,17 @@ def precode(x, scheme, codebook=0):
         y0[0::2], y0[1::2] = x0 / math.sqrt(2), x1 / math.sqrt(2)
         y1[0::2], y1[1::2] = -np.conj(x1) / math.sqrt(2), np.conj(x0) / math.sqrt(2)
         return [y0, y1]
+    if scheme == "diversity4":  # 36.211 6.3.3.3 (4 layers) + 6.3.4.3 SFBC + FSTD, 4 ports
+        d = x[0]
+        m = d.size // 4
+        xl = [d[j:4 * m:4] for j in range(4)]
+        y = [np.zeros(4 * m, np.complex128) for _ in range(4)]
+        a = 1 / math.sqrt(2)
+        y[0][0::4], y[2][0::4] = xl[0] * a, -np.conj(xl[1]) * a
+        y[0][1::4], y[2][1::4] = xl[1] * a, np.conj(xl[0]) * a
+        y[1][2::4], y[3][2::4] = xl[2] * a, -np.conj(xl[3]) * a
+        y[1][3::4], y[3][3::4] = xl[3] * a, np.conj(xl[2]) * a
+        return y
     if scheme == "sm":
         W = {0: np.array([[1, 0], [0, 1]]) / math.sqrt(2), 1: np.array([[1, 1], [1, -1]]) / 2,
              2: np.array([[1, 1], [1j, -1j]]) / 2}[codebook]
@@ -167,12 +178,16 @@ def precode(x, scheme, codebook=0):
 
 
 # ---------------- resource grid ----------------
-def crs_shift(port, l):
-    """v of 36.211 6.10.1.2 for symbol l (0..6) of a slot"""
+def crs_shift(port, l, ns=0):
+    """v of 36.211 6.10.1.2 for symbol l (0..6) of slot ns"""
     if port == 0:
         return 0 if l == 0 else 3
     if port == 1:
         return 3 if l == 0 else 0
+    if port == 2:
+        return 3 * (ns % 2)
+    if port == 3:
+        return 3 + 3 * (ns % 2)
     raise ValueError(port)
 
 
@@ -188,12 +203,12 @@ def crs_values(cell_id, nof_prb, ns, l, cp=0):
 
 
 def crs_grid(cell_id, nof_prb, nports, port, sf_idx, cp=0):
-    """port's CRS in a (2 nsymb, 12 N_RB) grid (2 ports max; nsymb 7, or 6 with cp=1 extended)"""
+    """port's CRS in a (2 nsymb, 12 N_RB) grid (nsymb 7, or 6 with cp=1 extended); ports 2 / 3 in l = 1"""
     ns = 6 if cp else 7
     g = np.zeros((2 * ns, 12 * nof_prb), np.complex128)
     for s in range(2):
-        for l in crs_symbols(nports, ns):
-            k = 6 * np.arange(2 * nof_prb) + (crs_shift(port, 0 if l == 0 else 4) + cell_id % 6) % 6
+        for l in ([0, ns - 3] if port < 2 else [1]):
+            k = 6 * np.arange(2 * nof_prb) + (crs_shift(port, 0 if l == 0 else 4, s) + cell_id % 6) % 6
             g[ns * s + l, k] = crs_values(cell_id, nof_prb, 2 * sf_idx + s, l, cp)
     return g
 
@@ -276,7 +291,7 @@ def pcfich_grids(nof_prb, cell_id, nports, sf_idx, cfi, cp=0):
     """Per-port (2 nsymb, 12 N_RB) grids carrying only the PCFICH of `cfi`."""
     bits = np.array(CFI_CODEWORDS[cfi - 1], np.uint8) ^ gold((sf_idx + 1) * (2 * cell_id + 1) * 512 + cell_id, 32)
     d = modulate(bits, 2)
-    ports = precode([d], "diversity") if nports == 2 else [d]
+    ports = precode([d], "diversity") if nports == 2 else precode([d], "diversity4") if nports == 4 else [d]
     k = pcfich_res(nof_prb, cell_id)
     grids = []
     for p in range(nports):
@@ -302,7 +317,7 @@ def pdsch_subframe(nof_prb, cell_id, nports, tti, cfi, rnti, tbs, Qm, rv, payloa
     layers = []
     for q, pl in enumerate(payloads):
         G = nof_re * Qm
-        e = dlsch_encode(tbs, Qm, rv, G, pl, Nl=2 if scheme == "diversity" else 1)
+        e = dlsch_encode(tbs, Qm, rv, G, pl, Nl=2 if scheme in ("diversity", "diversity4") else 1)
         c = gold(pdsch_seed(rnti, q, 2 * sf_idx, cell_id), G)
         layers.append(modulate(e ^ c, Qm))
     ports = precode(layers, scheme, codebook)
@@ -318,8 +333,9 @@ def pdsch_subframe(nof_prb, cell_id, nports, tti, cfi, rnti, tbs, Qm, rv, payloa
         if ctrl is not None:
             g = g + ctrl[p]
         tx.append(ofdm_tx(g, N, cp))
+    H4 = [[1, 0.5j, -0.4, 0.3], [0.3, -0.6j, 1, 0.5]]
     H = np.asarray(channel if channel is not None else
-                   ([[1, 1], [1, -1]] if nports == 2 else [[1]] * nrx), np.complex128)
+                   ([[1, 1], [1, -1]] if nports == 2 else H4 if nports == 4 else [[1]] * nrx), np.complex128)
     rx = H @ np.stack(tx)
     if snr_db is not None:
         pw = np.mean(np.abs(rx) ** 2)

@@ -70,3 +70,21 @@ def test_oracle_chain_extended_cp(ora, tti, cfi, nports, scheme, tbs, Qm):
         assert res[q]["ret"] == 0
         assert np.array_equal(res[q]["data"][: tbs // 8], pls[q])
     assert res[0]["nof_re"] == nre
+
+
+@pytest.mark.parametrize("tti,cfi,cp", [(1, 1, 0), (5, 2, 0), (10, 1, 0), (3, 2, 1)])
+def test_oracle_chain_tm2_four_ports(ora, tti, cfi, cp):
+    """4 tx ports (SFBC + FSTD, 36.211 6.3.4.3; CRS of ports 2 / 3 in l = 1) through a 2 x 4 channel:
+    4-port estimator, srsran_predecoding_diversity_csi (4 ports, pinned in test_phy_oracle.py), 4-layer
+    demap, DL-SCH with Nl = 2"""
+    rng = np.random.default_rng(tti + 60)
+    tbs = 36696
+    pl = [rng.integers(0, 256, tbs // 8, dtype=np.uint8)]
+    x, nre = S.pdsch_subframe(100, 6, 4, tti, cfi, 0x1234, tbs, 6, 0, pl, scheme="diversity4", snr_db=30.0, rng=rng,
+                              cp=cp)
+    assert nre % 4 == 0
+    g, ce, st = PC.fft_estimate(ora, x, 100, 6, 4, tti, cp=cp)
+    res = PC.pdsch_decode(ora, g, ce, st["noise"], 100, 6, 4, tti, cfi, 0x1234, [tbs], [6], [0], scheme="diversity",
+                          cp=cp)
+    assert res[0]["nof_re"] == nre
+    assert res[0]["ret"] == 0 and np.array_equal(res[0]["data"][: tbs // 8], pl[0])

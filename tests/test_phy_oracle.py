@@ -89,7 +89,7 @@ def channel(rng, nports, nrx, n):
 
 
 PRE_CASES = [(0, 1, 1, 1, 0), (0, 2, 1, 1, 0), (3, 2, 2, 2, 0), (2, 2, 2, 2, 0), (2, 2, 2, 2, 1), (2, 2, 2, 2, 2),
-             (1, 1, 2, 2, 0), (1, 2, 2, 2, 0), (1, 4, 2, 2, 0)]
+             (1, 1, 2, 2, 0), (1, 2, 2, 2, 0), (1, 4, 2, 2, 0), (1, 1, 4, 4, 0), (1, 2, 4, 4, 0), (1, 4, 4, 4, 0)]
 
 
 @needs_ref
@@ -106,7 +106,9 @@ def test_predecode_matches_reference(scheme, nrx, nports, nlayers, cb):
             xr, cr = ref.predecode(scheme, y, h, nlayers, cb, scaling, noise)
             assert np.all(np.isfinite(xo))
             if scheme == 1:  # diversity_csi is scalar C in the reference too: bit-exact
-                assert np.array_equal(xo, xr) and np.array_equal(co, cr), n
+                m = xo.shape[1]  # 4 ports: only the m_ap whole groups are decoded (precoding.c:715)
+                assert np.array_equal(xo, xr[:, :m]), n
+                assert np.array_equal(co[:, :nlayers * m], cr[:, :nlayers * m]), n
                 continue
             err = np.abs(xo - xr) / (np.abs(xo) + 1e-3)
             assert np.percentile(err, 99.9) < 2e-3 and err.max() < 2e-2, (n, err.max())

@@ -12,7 +12,8 @@ struct PredArgs {
   float2*       x[4];     // [layer] equalised symbols
   float*        csi[2];   // [layer] CSI (srsran_predecoding_*_csi)
   uint32_t*     csi_max;  // optional [layer] running max of csi (float bits, csi >= 0)
-  int           scheme;   // 0 PORT0, 1 DIVERSITY (n = REs, n/2 pairs), 2 SPATIALMUX, 3 CDD
+  int           scheme;   // 0 PORT0, 1 DIVERSITY (n = REs, n/2 pairs), 2 SPATIALMUX, 3 CDD, 4 DIVERSITY on 4 ports
+                          // (n/4 SFBC + FSTD groups)
   int           nrx;
   int           codebook;
   uint32_t      n;

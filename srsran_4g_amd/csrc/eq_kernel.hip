@@ -5,7 +5,7 @@
 //   PORT0  srsran_predecoding_single_csi        precoding.c:307-355
 //   CDD    srsran_predecoding_ccd_2x2_mmse_csi  precoding.c:1043-1121 (precoder alternates per RE)
 //   SM     srsran_predecoding_multiplex_2x2_mmse_csi precoding.c:1437-1540 (codebooks 0..2)
-//   TXD    srsran_predecoding_diversity_csi     precoding.c:671-700 (2-port SFBC pairs)
+//   TXD    srsran_predecoding_diversity_csi     precoding.c:671-775 (2-port SFBC pairs, 4-port SFBC + FSTD)
 //   2x2    srsran_mat_2x2_mmse_csi_gen          mat.c:63-109
 // computed in IEEE float with the scalar ("gen") operation order and no FMA contraction, so
 // the result equals oracle/phy_oracle.c bit for bit.  (The reference's SIMD bodies use
@@ -155,11 +155,76 @@ __device__ __forceinline__ void diversity_pair(const PredArgs& a, uint32_t k, ui
   }
 }
 
+// srsran_predecoding_diversity_csi, 4 ports (precoding.c:714-775): thread k decodes the SFBC + FSTD
+// group (4k .. 4k+3), ports (0, 2) on the first pair and (1, 3) on the second, for k < m_ap (a
+// trailing half group is not decoded by the reference; the layer-demapped codeword gets 0 there).  CSI =
+// a_l * scaling / nof_rxant per RE; with a.interleave the codeword is written layer-demapped (d[4k + l] = x_l[k]).
+__device__ __forceinline__ void diversity_quad(const PredArgs& a, uint32_t k, uint32_t (&mx)[2])
+{
+  const uint32_t m_ap  = (a.n % 4) ? (a.n - 2) / 4 : a.n / 4;
+  const bool     valid = k < m_ap;
+  const uint32_t kk    = valid ? k : 0;
+  uint32_t       gy[4], gh[4];
+  float          s[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    re_at(a, 4 * kk + j, gy[j], gh[j], s[j]);
+  }
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  cpx   x0 = {0.f, 0.f}, x1 = {0.f, 0.f}, x2 = {0.f, 0.f}, x3 = {0.f, 0.f};
+  for (int p = 0; p < a.nrx; p++) {
+    cpx r[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      r[j] = ld(a.y[p], gy[j]);
+      if (s[j] != 1.0f) {
+        r[j] = cscale(r[j], s[j]);
+      }
+    }
+    cpx h00 = ld(a.h[0][p], gh[0]), h01 = ld(a.h[2][p], gh[0]), h10 = ld(a.h[0][p], gh[1]), h11 = ld(a.h[2][p], gh[1]);
+    a0 += h00.r * h00.r + h00.i * h00.i + h11.r * h11.r + h11.i * h11.i;
+    a1 += h10.r * h10.r + h10.i * h10.i + h01.r * h01.r + h01.i * h01.i;
+    x0 = cadd(x0, cadd(cmul(cconj(h00), r[0]), cmul(h11, cconj(r[1]))));
+    x1 = cadd(x1, cadd(cmul(cneg(h01), cconj(r[0])), cmul(cconj(h10), r[1])));
+    h00 = ld(a.h[1][p], gh[2]), h01 = ld(a.h[3][p], gh[2]), h10 = ld(a.h[1][p], gh[3]), h11 = ld(a.h[3][p], gh[3]);
+    a2 += h00.r * h00.r + h00.i * h00.i + h11.r * h11.r + h11.i * h11.i;
+    a3 += h10.r * h10.r + h10.i * h10.i + h01.r * h01.r + h01.i * h01.i;
+    x2 = cadd(x2, cadd(cmul(cconj(h00), r[2]), cmul(h11, cconj(r[3]))));
+    x3 = cadd(x3, cadd(cmul(cneg(h01), cconj(r[2])), cmul(cconj(h10), r[3])));
+  }
+  const float  av[4] = {a0 * a.norm, a1 * a.norm, a2 * a.norm, a3 * a.norm};  // scaling
+  const cpx    xv[4] = {x0, x1, x2, x3};
+  const double sq2   = 1.41421356237309504880;
+  if (valid) {
+#pragma unroll
+    for (int l = 0; l < 4; l++) {
+      const float c           = av[l] / (float)a.nrx;
+      const float2 o          = make_float2((float)((double)(xv[l].r / av[l]) * sq2), (float)((double)(xv[l].i / av[l]) * sq2));
+      if (a.interleave) {
+        a.x[0][4 * k + l] = o;  // srsran_layerdemap_diversity fused
+      } else {
+        a.x[l][k] = o;
+      }
+      a.csi[0][4 * k + l]     = c;
+      mx[0]                   = max(mx[0], __float_as_uint(c));
+    }
+  } else if (k == m_ap && (a.n % 4) && a.interleave) {  // the undecoded half group
+    for (uint32_t j = 4 * m_ap; j < a.n; j++) {
+      a.x[0][j]   = make_float2(0.f, 0.f);
+      a.csi[0][j] = 0.f;
+    }
+  }
+}
+
 template <int SCHEME>
 __device__ __forceinline__ void predecode_item(const PredArgs& a, uint32_t k, uint32_t (&mx)[2])
 {
   if constexpr (SCHEME == 1) {
     diversity_pair(a, k, mx);
+    return;
+  }
+  if constexpr (SCHEME == 4) {
+    diversity_quad(a, k, mx);
     return;
   }
   const bool     valid = k < a.n;
@@ -266,7 +331,7 @@ __device__ __forceinline__ void predecode_block(const PredArgs& a, uint32_t k0)
     predecode_item<SCHEME>(a, k0 + r * EQ_THREADS + threadIdx.x, mx);
   }
   if (a.csi_max) {
-    if constexpr (SCHEME == 0 || SCHEME == 1) {
+    if constexpr (SCHEME == 0 || SCHEME == 1 || SCHEME == 4) {
       const uint32_t m1[1] = {mx[0]};
       block_max_atomic<1>(a.csi_max, m1, red);
     } else {
@@ -286,7 +351,7 @@ __global__ __launch_bounds__(EQ_THREADS) void predecode_batch_kernel(const PredA
 {
   const PredArgs& a  = items[blockIdx.y];
   const uint32_t  k0 = blockIdx.x * EQ_THREADS * EQ_RPT;
-  if (k0 >= (SCHEME == 1 ? a.n / 2 : a.n)) {
+  if (k0 >= (SCHEME == 1 ? a.n / 2 : SCHEME == 4 ? a.n / 4 + 1 : a.n)) {
     return;  // whole block past this item's end (uniform: the block reduction stays intact)
   }
   predecode_block<SCHEME>(a, k0);
@@ -299,7 +364,8 @@ hipError_t predecode_batch_launch(const PredArgs* d_items, uint32_t nitems, int 
   if (nitems == 0 || max_n == 0) {
     return hipSuccess;
   }
-  const uint32_t units = scheme == 1 ? max_n / 2 : max_n;  // diversity: one thread per SFBC pair
+  // diversity: one thread per SFBC pair (2 ports) or SFBC + FSTD group (4 ports, + 1 for a half group)
+  const uint32_t units = scheme == 1 ? max_n / 2 : scheme == 4 ? max_n / 4 + 1 : max_n;
   if (units == 0) {
     return hipSuccess;
   }
@@ -317,6 +383,9 @@ hipError_t predecode_batch_launch(const PredArgs* d_items, uint32_t nitems, int 
     case 3:
       hipLaunchKernelGGL(predecode_batch_kernel<3>, grid, dim3(EQ_THREADS), 0, stream, d_items);
       break;
+    case 4:
+      hipLaunchKernelGGL(predecode_batch_kernel<4>, grid, dim3(EQ_THREADS), 0, stream, d_items);
+      break;
     default:
       return hipErrorInvalidValue;
   }
@@ -329,7 +398,7 @@ hipError_t predecode_launch(const PredArgs& a, hipStream_t stream)
   if (a.n == 0) {
     return hipSuccess;
   }
-  const uint32_t units = a.scheme == 1 ? a.n / 2 : a.n;
+  const uint32_t units = a.scheme == 1 ? a.n / 2 : a.scheme == 4 ? a.n / 4 + 1 : a.n;
   if (units == 0) {
     return hipSuccess;
   }
@@ -346,6 +415,9 @@ hipError_t predecode_launch(const PredArgs& a, hipStream_t stream)
       break;
     case 3:
       hipLaunchKernelGGL(predecode_kernel<3>, grid, dim3(EQ_THREADS), 0, stream, a);
+      break;
+    case 4:
+      hipLaunchKernelGGL(predecode_kernel<4>, grid, dim3(EQ_THREADS), 0, stream, a);
       break;
     default:
       return hipErrorInvalidValue;

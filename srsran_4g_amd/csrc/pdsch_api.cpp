@@ -155,7 +155,7 @@ int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sf
     // srsran_layerdemap_type as the reference runs it (pdsch.c:838-863)
     const bool cw1l2 = !txd && gr.nof_tb == 1 && gr.nof_layers == 2 &&
                        (gr.tx_scheme == SRSRAN_TXSCHEME_SPATIALMUX || gr.tx_scheme == SRSRAN_TXSCHEME_CDD);
-    if (txd ? (gr.nof_tb != 1 || gr.nof_layers != 2)
+    if (txd ? (gr.nof_tb != 1 || gr.nof_layers != np)
             : (!cw1l2 && (gr.nof_layers != gr.nof_tb || gr.nof_tb < 1 || gr.nof_tb > 2))) {
       fprintf(stderr, "[srsran_pdsch] unsupported: %u codewords on %u layers\n", gr.nof_tb, gr.nof_layers);
       return SRSRAN_ERROR;
@@ -373,7 +373,7 @@ int srsran_pdsch_enable_coworker(srsran_pdsch_t* q) { return q ? SRSRAN_SUCCESS 
 int srsran_pdsch_set_cell(srsran_pdsch_t* q, srsran_cell_t cell)
 {
   if (!q || !q->gpu || cell.nof_prb == 0 || cell.nof_prb > SRSRAN_MAX_PRB || cell.nof_ports == 0 ||
-      cell.nof_ports > 2 || cell.id > 503) {
+      cell.nof_ports == 3 || cell.nof_ports > 4 || cell.id > 503) {
     return SRSRAN_ERROR_INVALID_INPUTS;
   }
   if (cell.frame_type != SRSRAN_FDD) {

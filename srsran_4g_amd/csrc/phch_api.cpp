@@ -78,11 +78,11 @@ bool pred_setup(PredArgs& a, int nrx, int nports, int nlayers, int codebook, int
       a.norm   = 1.0f / scaling;  // precoding.c:319
       return true;
     case SRSRAN_TXSCHEME_DIVERSITY:
-      if (nports != 2 || nlayers != 2 || nrx < 1 || nrx > 4) {
+      if ((nports != 2 && nports != 4) || nlayers != nports || nrx < 1 || nrx > 4) {
         return false;
       }
-      a.scheme = 1;
-      a.norm   = scaling;  // hh *= scaling (precoding.c:695)
+      a.scheme = nports == 2 ? 1 : 4;
+      a.norm   = scaling;  // hh *= scaling (precoding.c:695, 741-744)
       return true;
     case SRSRAN_TXSCHEME_CDD:
       if (nports != 2 || nrx != 2 || nlayers != 2) {
@@ -224,19 +224,22 @@ int srsran_predecoding_type(cf_t*              y[4],
   if (predecode_launch(a, g_ctx.stream) != hipSuccess) {
     return SRSRAN_ERROR;
   }
-  const size_t xn = a.scheme == 1 ? n / 2 : n;  // diversity: n/2 symbols per layer, one CSI row of n
+  // diversity: n/2 (2 ports) or m_ap (4 ports) symbols per layer, one CSI row; REs of an unpaired
+  // last RE / half group are not written (precoding.c:674, 715)
+  const bool   txd = a.scheme == 1 || a.scheme == 4;
+  const size_t xn  = a.scheme == 1 ? n / 2 : a.scheme == 4 ? ((n % 4) ? (n - 2) / 4 : n / 4) : n;
   for (int l = 0; l < nof_layers; l++) {
     hipMemcpyAsync(x[l], dx + l * n, xn * sizeof(cf_t), hipMemcpyDeviceToHost, g_ctx.stream);
-    if (csi && l < (a.scheme == 1 ? 1 : 2) && csi[l]) {
-      hipMemcpyAsync(csi[l], dcs + l * n, (a.scheme == 1 ? 2 * xn : n) * sizeof(float), hipMemcpyDeviceToHost,
-                     g_ctx.stream);  // diversity: an unpaired last RE is not written (precoding.c:674)
+    if (csi && l < (txd ? 1 : 2) && csi[l]) {
+      hipMemcpyAsync(csi[l], dcs + l * n, (txd ? (size_t)nof_layers * xn : n) * sizeof(float), hipMemcpyDeviceToHost,
+                     g_ctx.stream);
     }
   }
   if (hipStreamSynchronize(g_ctx.stream) != hipSuccess) {
     return SRSRAN_ERROR;
   }
   // the reference's return values: single_csi -> nof_symbols, diversity_csi -> pairs, 2x2 MMSE -> 0
-  return a.scheme == 0 ? (int)n : a.scheme == 1 ? (int)(n / 2) : SRSRAN_SUCCESS;
+  return a.scheme == 0 ? (int)n : txd ? (int)xn : SRSRAN_SUCCESS;
 }
 
 int srsran_predecoding_gpu(const cf_t* const  d_y[4],

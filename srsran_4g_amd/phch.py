@@ -89,8 +89,8 @@ def predecode(scheme, y, h, nlayers, codebook, scaling, noise):
                                        ctypes.addressof(cs), nrx, nports, nlayers, codebook, n, scheme, scaling, noise)
     if rc < 0:
         raise RuntimeError(f"srsran_predecoding_type failed ({rc})")
-    if scheme == 1:  # transmit diversity: n/2 symbols per layer, one CSI row for the codeword
-        return x[:nlayers, : n // 2], csi[:1]
+    if scheme == 1:  # transmit diversity: n/2 (4 ports: m_ap) symbols per layer, one CSI row
+        return x[:nlayers, : (n // 2 if nlayers == 2 else rc)], csi[:1]
     return x[:nlayers], csi[:nlayers]
 
 

@@ -309,9 +309,10 @@ MOD_FROM_QM = {1: 0, 2: 1, 4: 2, 6: 3, 8: 4}
 
 
 def pdsch_cfg(nof_prb, nof_re, tbs, Qm, rv=(0, 0), scheme="cdd", pmi=0, rnti=0x1234, max_iterations=8,
-              csi_enable=True, power_scale=False, p_a=0.0, p_b=0, softbuffers=(), zf=False, cp=0):
+              csi_enable=True, power_scale=False, p_a=0.0, p_b=0, softbuffers=(), zf=False, cp=0, nof_ports=2):
     """srsran_pdsch_cfg_t for a full-bandwidth grant of len(tbs) codewords on as many layers
-    (srsUE defaults: csi_enable, 8 half-iterations, MMSE, no power scaling); cp=1: extended CP."""
+    (srsUE defaults: csi_enable, 8 half-iterations, MMSE, no power scaling); cp=1: extended CP;
+    transmit diversity runs on nof_ports layers (2 or 4)."""
     c = srsran_pdsch_cfg_t()
     g = c.grant
     g.tx_scheme = SCHEME[scheme]
@@ -323,7 +324,7 @@ def pdsch_cfg(nof_prb, nof_re, tbs, Qm, rv=(0, 0), scheme="cdd", pmi=0, rnti=0x1
     g.nof_re = nof_re
     g.nof_symb_slot[0] = g.nof_symb_slot[1] = 6 if cp else 7
     g.nof_tb = len(tbs)
-    g.nof_layers = 2 if scheme == "diversity" else len(tbs)
+    g.nof_layers = nof_ports if scheme == "diversity" else len(tbs)
     for i, t in enumerate(tbs):
         tb = g.tb[i]
         tb.mod = MOD_FROM_QM[Qm[i]]

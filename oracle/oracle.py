@@ -112,7 +112,7 @@ class _PhyMixin:
         if rc < 0:
             raise ValueError(rc)
         if scheme == 1:  # transmit diversity: n/2 (n/4, 4 ports) symbols per layer, one CSI row
-            m = n // 2 if nlayers == 2 else ((n - 2) // 4 if n % 4 else n // 4)
+            m = n // 2 if nlayers == 2 else (((n - 2) // 4 if n >= 2 else 0) if n % 4 else n // 4)
             return xa[:nlayers, :m].copy(), ca[:1].copy()
         return xa[:nlayers].copy(), ca[:nlayers].copy()
 

@@ -161,7 +161,7 @@ __device__ __forceinline__ void diversity_pair(const PredArgs& a, uint32_t k, ui
 // a_l * scaling / nof_rxant per RE; with a.interleave the codeword is written layer-demapped (d[4k + l] = x_l[k]).
 __device__ __forceinline__ void diversity_quad(const PredArgs& a, uint32_t k, uint32_t (&mx)[2])
 {
-  const uint32_t m_ap  = (a.n % 4) ? (a.n - 2) / 4 : a.n / 4;
+  const uint32_t m_ap  = (a.n % 4) ? (a.n >= 2 ? (a.n - 2) / 4 : 0u) : a.n / 4;  // C int division of the reference
   const bool     valid = k < m_ap;
   const uint32_t kk    = valid ? k : 0;
   uint32_t       gy[4], gh[4];

@@ -227,7 +227,7 @@ int srsran_predecoding_type(cf_t*              y[4],
   // diversity: n/2 (2 ports) or m_ap (4 ports) symbols per layer, one CSI row; REs of an unpaired
   // last RE / half group are not written (precoding.c:674, 715)
   const bool   txd = a.scheme == 1 || a.scheme == 4;
-  const size_t xn  = a.scheme == 1 ? n / 2 : a.scheme == 4 ? ((n % 4) ? (n - 2) / 4 : n / 4) : n;
+  const size_t xn  = a.scheme == 1 ? n / 2 : a.scheme == 4 ? ((n % 4) ? (n >= 2 ? (n - 2) / 4 : 0) : n / 4) : n;
   for (int l = 0; l < nof_layers; l++) {
     hipMemcpyAsync(x[l], dx + l * n, xn * sizeof(cf_t), hipMemcpyDeviceToHost, g_ctx.stream);
     if (csi && l < (txd ? 1 : 2) && csi[l]) {

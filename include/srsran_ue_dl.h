@@ -6,7 +6,7 @@
  *   lib/include/srsran/phy/common/phy_common.h:197-253     srsran_cell_t, srsran_dl_sf_cfg_t, ...
  *   lib/include/srsran/phy/ch_estimation/chest_dl.h:43-170  srsran_chest_dl_{t,cfg_t,res_t}, srsran_chest_dl_*
  * Channel estimation runs on the GPU (chest_kernel.hip).  Supported configuration: normal
- * subframes, normal CP, FDD, estimator AVERAGE with the Gauss smoothing filter and REFS noise
+ * subframes, normal or extended CP, FDD, 1/2/4 ports, estimator AVERAGE with the Gauss smoothing filter and REFS noise
  * estimation -- srsUE's defaults (srsue/src/phy/phy_common.cc:83-107); other settings return
  * SRSRAN_ERROR.  srsran_chest_dl_t keeps the fields callers read (cell, nof_rx_antennas, rssi,
  * rsrp, noise_estimate, cfo) and hides the device state behind `gpu`.
@@ -170,7 +170,7 @@ int srsran_chest_dl_gpu_estimate(srsran_chest_dl_t* q,
 
 /* ---------------- OFDM receiver (dft/ofdm.h:49-151, ofdm.c) ----------------
  * GPU FFT (mixed radix 8/4/3/2: 128..2048 points incl. 1536/768/384), no FFTW.  Provided:
- * normal CP, normal subframes, rx_window_offset = 0, no frequency shift, no phase compensation
+ * normal or extended CP, normal subframes, rx_window_offset = 0, no frequency shift, no phase compensation
  * (srsran_ue_dl's configuration, ue_dl.c:88-98) and DC removal (keep_dc = false); normalize is honoured.
  * in_buffer / out_buffer are host pointers as in the reference. */
 typedef struct {
@@ -211,9 +211,9 @@ int srsran_ofdm_rx_gpu(srsran_ofdm_t* q, const cf_t* d_in, cf_t* d_out, uint32_t
                        void* stream);
 
 /* Modulator (ofdm.c:585-690) in srsran_enb_dl's configuration (ofdm_cfg.normalize = false, DC
- * subcarrier left empty, no frequency shift, normal CP).  srsran_ofdm_tx_sf: cfg.in_buffer (one
- * port's 14 x 12 nof_prb grid, host) -> cfg.out_buffer (SRSRAN_SF_LEN samples, host).  Added:
- * srsran_ofdm_tx_gpu on device grids [nof_sf][nof_ports][14][12 nof_prb] -> samples
+ * subcarrier left empty, no frequency shift, normal or extended CP).  srsran_ofdm_tx_sf: cfg.in_buffer (one
+ * port's 2 nsymb x 12 nof_prb grid, host) -> cfg.out_buffer (SRSRAN_SF_LEN samples, host).  Added:
+ * srsran_ofdm_tx_gpu on device grids [nof_sf][nof_ports][2 nsymb][12 nof_prb] -> samples
  * [nof_sf][nof_ports][sf_len], the grid scaled by `scale` first (srsran_enb_dl_gen_signal's
  * 0.05 / sqrt(nof_prb)); asynchronous on `stream`. */
 int  srsran_ofdm_tx_init_cfg(srsran_ofdm_t* q, srsran_ofdm_cfg_t* cfg);
@@ -236,10 +236,10 @@ int srsran_pdsch_re_table(const srsran_cell_t*        cell,
  * srsran_pdsch_decode runs on the GPU: RE extraction fused into the MMSE predecoder (gather
  * through the srsran_pdsch_re_table order), rho_b scaling of CRS symbols fused there too,
  * demapping + descrambling + CSI correction fused into one LLR kernel, then DL-SCH decode.
- * Provided: PORT0 (1 port), TX diversity (2 ports, 1 codeword; layer demap fused), CDD and
- * SPATIALMUX (2 ports x 2 rx, 2 codewords on 2 layers), MMSE (ZF = MMSE with noise 0, as
- * pdsch.c:811 passes it), 16-bit LLRs, normal CP, FDD.
- * Not provided (SRSRAN_ERROR): 4 ports, one codeword on two SM layers, 8-bit LLRs, EVM.
+ * Provided: PORT0 (1 port), TX diversity (2 or 4 ports, 1 codeword; layer demap fused), CDD and
+ * SPATIALMUX (2 ports x 2 rx, 1 or 2 codewords on 2 layers), MMSE (ZF = MMSE with noise 0, as
+ * pdsch.c:811 passes it), 16-bit LLRs, normal and extended CP, FDD.
+ * Not provided (SRSRAN_ERROR): 4-port CDD / SM (refused by the reference too), 8-bit LLRs, EVM.
  * The host-side working buffers of the reference struct (ce, symbols, x, d, e, csi) do not
  * exist; the coworker thread is unnecessary (both codewords decode in one GPU pass). */
 typedef struct {

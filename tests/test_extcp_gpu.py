@@ -243,3 +243,43 @@ def test_chest_four_ports_extended_cp(U, ora):
     assert np.abs(ce - ceo).max() < 2e-5 * np.abs(ceo).max()
     assert res.noise_estimate == pytest.approx(st["noise"], rel=1e-4)
     ch.free()
+
+
+def test_ue_dl_batch_four_ports(U, SCH, ora):
+    """srsran_ue_dl_gpu_decode_batch on a 4-port cell (TM2): OFDM, 4-port estimator, SFBC + FSTD,
+    DL-SCH from time samples; every TB decodes and equals the host-synchronous path"""
+    nof_prb, cell_id, tbs = 100, 6, 36696
+    rng = np.random.default_rng(21)
+    cell = U.cell(nof_prb, 4, cell_id)
+    ue = U.UeDl(cell, 2)
+    ttis = [1, 2, 5]
+    samples, payloads, entries, keep = [], [], [], []
+    d_pl = torch.zeros((len(ttis), 2, tbs // 8 + 64), dtype=torch.uint8, device="cuda")
+    for b, tti in enumerate(ttis):
+        pl = [rng.integers(0, 256, tbs // 8, dtype=np.uint8)]
+        x, nre = SY.pdsch_subframe(nof_prb, cell_id, 4, tti, 1, RNTI, tbs, 6, 0, pl, scheme="diversity4", snr_db=30.0,
+                                   rng=rng)
+        sb = [SCH.SoftbufferRx(nof_prb=nof_prb)]
+        cfg = U.pdsch_cfg(nof_prb, nre, [tbs], [6], scheme="diversity", softbuffers=sb, nof_ports=4)
+        samples.append(x)
+        payloads.append(pl)
+        keep.append((sb, cfg))
+        entries.append((tti, 1, cfg, [d_pl[b, 0].data_ptr(), d_pl[b, 1].data_ptr()], [1, 1]))
+    d_x = torch.from_numpy(np.stack(samples).view(np.float32)).cuda()
+    d_res = torch.full((len(ttis),), 7, dtype=torch.int32, device="cuda")
+    d_avg = torch.zeros(len(ttis), dtype=torch.float32, device="cuda")
+    assert ue.gpu_decode_batch(entries, d_x.data_ptr(), d_res.data_ptr(), d_avg.data_ptr(), 0.0, None) == len(ttis)
+    torch.cuda.synchronize()
+    res, pl = d_res.cpu().numpy(), d_pl.cpu().numpy()
+    ue2 = U.UeDl(cell, 2)
+    for b, tti in enumerate(ttis):
+        assert res[b] == 0
+        assert np.array_equal(pl[b, 0, : tbs // 8], payloads[b][0])
+        assert ue2.fft_estimate(samples[b], tti, 1) == 0
+        sb = [SCH.SoftbufferRx(nof_prb=nof_prb)]
+        cfg = U.pdsch_cfg(nof_prb, keep[b][1].grant.nof_re, [tbs], [6], scheme="diversity", softbuffers=sb, nof_ports=4)
+        ret, out = ue2.decode_pdsch(cfg, tti, 1)
+        assert ret == 0 and out[0][0]
+        assert np.array_equal(out[0][1][: tbs // 8 + 6], pl[b, 0, : tbs // 8 + 6])
+    ue.free()
+    ue2.free()

@@ -172,6 +172,45 @@ __device__ __forceinline__ void diversity_quad(const PredArgs& a, uint32_t k, ui
   }
   float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
   cpx   x0 = {0.f, 0.f}, x1 = {0.f, 0.f}, x2 = {0.f, 0.f}, x3 = {0.f, 0.f};
+  if (!a.csi[0]) {
+    // no CSI (the control channels, pcfich.c:202 / pdcch.c:498): srsran_predecoding_diversity_gen_,
+    // 4 ports (precoding.c:465-499) -- one channel RE per pair, one gain per pair
+    for (int p = 0; p < a.nrx; p++) {
+      cpx r[4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        r[j] = ld(a.y[p], gy[j]);
+        if (s[j] != 1.0f) {
+          r[j] = cscale(r[j], s[j]);
+        }
+      }
+      const cpx h0 = ld(a.h[0][p], gh[0]), h1 = ld(a.h[1][p], gh[2]), h2 = ld(a.h[2][p], gh[0]),
+                h3 = ld(a.h[3][p], gh[2]);
+      a0 += h0.r * h0.r + h0.i * h0.i + h2.r * h2.r + h2.i * h2.i;
+      a2 += h1.r * h1.r + h1.i * h1.i + h3.r * h3.r + h3.i * h3.i;
+      x0 = cadd(x0, cadd(cmul(cconj(h0), r[0]), cmul(h2, cconj(r[1]))));
+      x1 = cadd(x1, cadd(cmul(cneg(h2), cconj(r[0])), cmul(cconj(h0), r[1])));
+      x2 = cadd(x2, cadd(cmul(cconj(h1), r[2]), cmul(h3, cconj(r[3]))));
+      x3 = cadd(x3, cadd(cmul(cneg(h3), cconj(r[2])), cmul(cconj(h1), r[3])));
+    }
+    a0 *= a.norm;
+    a2 *= a.norm;
+    const float  g[4]  = {a0, a0, a2, a2};
+    const cpx    xv[4] = {x0, x1, x2, x3};
+    const double sq2   = 1.41421356237309504880;
+    if (valid) {
+#pragma unroll
+      for (int l = 0; l < 4; l++) {
+        const float2 o = make_float2((float)((double)(xv[l].r / g[l]) * sq2), (float)((double)(xv[l].i / g[l]) * sq2));
+        if (a.interleave) {
+          a.x[0][4 * k + l] = o;
+        } else {
+          a.x[l][k] = o;
+        }
+      }
+    }
+    return;
+  }
   for (int p = 0; p < a.nrx; p++) {
     cpx r[4];
 #pragma unroll

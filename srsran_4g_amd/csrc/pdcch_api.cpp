@@ -259,7 +259,7 @@ CtrlGpu* ctrl_new(uint32_t max_prb, uint32_t nof_rx)
   g->nrx       = nof_rx;
   if (hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc((void**)&g->d_grid, nof_rx * 4 * nre * sizeof(float2)) != hipSuccess ||
-      hipMalloc((void**)&g->d_ce, 2 * nof_rx * 4 * nre * sizeof(float2)) != hipSuccess ||
+      hipMalloc((void**)&g->d_ce, 4 * nof_rx * 4 * nre * sizeof(float2)) != hipSuccess ||
       hipMalloc((void**)&g->d_x, 4 * nre * sizeof(float2)) != hipSuccess ||
       hipMalloc((void**)&g->d_csi, 2 * 4 * nre * sizeof(float)) != hipSuccess ||
       hipMalloc((void**)&g->d_idx, (16 + 3 * 4 * nre) * sizeof(uint32_t)) != hipSuccess ||
@@ -312,8 +312,26 @@ int ctrl_equalise(CtrlGpu* g, const uint32_t* d_idx, uint32_t n, float noise)
     a.nrx         = (int)std::min(g->nrx, 2u);
     return ctrl_diversity_launch(a, g->stream) == hipSuccess ? SRSRAN_SUCCESS : SRSRAN_ERROR;
   }
+  if (g->ports == 4) {  // srsran_predecoding_diversity_multi without CSI + srsran_layerdemap_diversity
+    PredArgs a{};
+    for (uint32_t r = 0; r < g->nrx && r < 4; r++) {
+      a.y[r] = g->d_grid + r * plane;
+      for (int p = 0; p < 4; p++) {
+        a.h[p][r] = g->d_ce + (p * g->nrx + r) * plane;
+      }
+    }
+    a.x[0]       = g->d_x;
+    a.scheme     = 4;
+    a.nrx        = (int)std::min(g->nrx, 4u);
+    a.n          = n;
+    a.norm       = 1.0f;  // scaling
+    a.idx        = d_idx;
+    a.rho_b_inv  = 1.0f;
+    a.interleave = 1;
+    return predecode_launch(a, g->stream) == hipSuccess ? SRSRAN_SUCCESS : SRSRAN_ERROR;
+  }
   if (g->ports != 1) {
-    fprintf(stderr, "[srsran_pdcch] %u ports: only 1 and 2 are provided\n", g->ports);
+    fprintf(stderr, "[srsran_pdcch] %u ports: 1, 2 or 4 are provided\n", g->ports);
     return SRSRAN_ERROR;
   }
   PredArgs a{};
@@ -336,7 +354,7 @@ int ctrl_equalise(CtrlGpu* g, const uint32_t* d_idx, uint32_t n, float noise)
 
 bool valid_cell(const srsran_cell_t& c)
 {
-  return c.nof_prb >= 6 && c.nof_prb <= SRSRAN_MAX_PRB && (c.nof_ports == 1 || c.nof_ports == 2) &&
+  return c.nof_prb >= 6 && c.nof_prb <= SRSRAN_MAX_PRB && (c.nof_ports == 1 || c.nof_ports == 2 || c.nof_ports == 4) &&
          c.cp == SRSRAN_CP_NORM && c.id < 504;
 }
 

@@ -186,9 +186,10 @@ int srsran_ue_dl_set_cell(srsran_ue_dl_t* q, srsran_cell_t cell)
   UeDlGpu* g = (UeDlGpu*)q->gpu;
   q->cell    = cell;
   g->cap     = 0;  // buffer shapes depend on the cell
-  // control channels: 1 or 2 ports, normal PHICH duration (others: PDSCH only, CFI from the caller)
+  // control channels: 1, 2 or 4 ports, normal CP and PHICH duration (others: PDSCH only, CFI from the caller)
   srsran_regs_free(&g->regs);
-  g->ctrl_cell = g->ctrl_init && (cell.nof_ports == 1 || cell.nof_ports == 2) && cell.phich_length == SRSRAN_PHICH_NORM &&
+  g->ctrl_cell = g->ctrl_init && (cell.nof_ports == 1 || cell.nof_ports == 2 || cell.nof_ports == 4) &&
+                 cell.cp == SRSRAN_CP_NORM && cell.phich_length == SRSRAN_PHICH_NORM &&
                  srsran_regs_init(&g->regs, cell) == SRSRAN_SUCCESS &&
                  srsran_pcfich_set_cell(&g->pcfich, &g->regs, cell) == SRSRAN_SUCCESS &&
                  srsran_pdcch_set_cell(&g->pdcch, &g->regs, cell) == SRSRAN_SUCCESS;

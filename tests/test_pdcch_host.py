@@ -19,7 +19,8 @@ from srsran_4g_amd import pdcch as PD  # noqa: E402
 needs_ref = pytest.mark.skipif(not P.ref_available(), reason="oracle/_ref not built")
 
 CELLS = [(100, 2, 1, 2), (50, 1, 7, 0), (25, 2, 300, 1), (6, 1, 2, 3), (75, 2, 101, 2), (15, 1, 44, 1),
-         (100, 1, 503, 3), (50, 2, 5, 0), (6, 2, 11, 2), (100, 2, 0, 0)]
+         (100, 1, 503, 3), (50, 2, 5, 0), (6, 2, 11, 2), (100, 2, 0, 0), (100, 4, 1, 2), (50, 4, 7, 0), (6, 4, 2, 3),
+         (25, 4, 301, 1), (15, 4, 44, 3)]
 
 
 @needs_ref

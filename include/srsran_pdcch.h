@@ -15,7 +15,7 @@
  * and one wave per PDCCH candidate for rate de-matching, quantisation, the 16-bit tail-biting
  * Viterbi decoder (64 lanes = 64 trellis states), CRC16 / RNTI and the re-encoding correlation.
  * Bit-exact with the reference's AVX2 build for the LLRs, decoded payloads and CRC remainders.
- * Provided: FDD, normal CP, 1 or 2 ports, PHICH normal duration; DCI formats 0 (size), 1, 1A, 1C
+ * Provided: FDD, normal CP, 1, 2 or 4 ports, PHICH normal duration; DCI formats 0 (size), 1, 1A, 1C
  * (size), 2, 2A; resource allocation types 0, 1 and 2 (localized).  Others return SRSRAN_ERROR.
  */
 #ifndef SRSRAN_AMD_PDCCH_H

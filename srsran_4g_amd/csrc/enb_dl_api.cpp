@@ -54,7 +54,8 @@ extern "C" {
 
 int srsran_enb_dl_gpu_init(srsran_enb_dl_gpu_t* q, srsran_cell_t cell)
 {
-  if (!q || cell.nof_prb < 6 || cell.nof_prb > SRSRAN_MAX_PRB || cell.nof_ports == 0 || cell.nof_ports > 2 ||
+  if (!q || cell.nof_prb < 6 || cell.nof_prb > SRSRAN_MAX_PRB || cell.nof_ports == 0 || cell.nof_ports == 3 ||
+      cell.nof_ports > 4 ||
       (cell.cp != SRSRAN_CP_NORM && cell.cp != SRSRAN_CP_EXT)) {
     return SRSRAN_ERROR_INVALID_INPUTS;
   }
@@ -132,6 +133,8 @@ int srsran_enb_dl_gpu_tx_batch(srsran_enb_dl_gpu_t*          q,
       scheme = 0;
     } else if (gr.tx_scheme == SRSRAN_TXSCHEME_DIVERSITY && P == 2 && gr.nof_tb == 1) {
       scheme = 1;
+    } else if (gr.tx_scheme == SRSRAN_TXSCHEME_DIVERSITY && P == 4 && gr.nof_tb == 1) {
+      scheme = 4;
     } else if (gr.tx_scheme == SRSRAN_TXSCHEME_CDD && P == 2 && gr.nof_tb == 2 && gr.nof_layers == 2) {
       scheme = 3;
     } else {
@@ -149,7 +152,8 @@ int srsran_enb_dl_gpu_tx_batch(srsran_enb_dl_gpu_t*          q,
     it.nre       = nre;
     it.scheme    = scheme;
     it.scaling   = 1.0f;
-    it.div_scale = (float)(1.0 * 0.70710678118654752440);  // scaling * M_SQRT1_2
+    // scaling * M_SQRT1_2 (2 ports); scaling /= M_SQRT2 (4 ports, precoding.c:1962)
+    it.div_scale = scheme == 4 ? (float)(1.0f / 1.41421356237309504880) : (float)(1.0 * 0.70710678118654752440);
     uint32_t cw = 0;
     for (uint32_t t = 0; t < SRSRAN_MAX_CODEWORDS; t++) {
       const srsran_ra_tb_t& tb = gr.tb[t];

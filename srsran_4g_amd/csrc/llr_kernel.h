@@ -41,14 +41,15 @@ struct PdschTx {
   uint32_t        seed[2];  // scrambling seeds (pdsch_seed)
   int             mod[2];   // srsran_mod_t
   const uint32_t* idx;      // RE table (srsran_pdsch_re_table order; bit 31 ignored)
-  float2*         grid[2];  // per-port subframe grids (14 x 12 nof_prb)
+  float2*         grid[4];  // per-port subframe grids (2 nsymb x 12 nof_prb)
   uint32_t        nre;      // PDSCH REs
-  int             scheme;   // 0: one port; 1: transmit diversity (2 ports, 1 codeword); 3: CDD 2x2 (2 codewords)
+  int             scheme;   // 0: one port; 1: transmit diversity (2 ports, 1 codeword); 3: CDD 2x2 (2 codewords);
+                            // 4: transmit diversity on 4 ports (SFBC + FSTD, 1 codeword)
   float           scaling;  // rho_a scaling of the precoder (1)
-  float           div_scale;// (float)(scaling * M_SQRT1_2) for diversity
+  float           div_scale;// (float)(scaling * M_SQRT1_2) for 2-port, (float)(scaling / M_SQRT2) for 4-port diversity
 };
 hipError_t pdsch_tx_launch(const PdschTx* d_items, uint32_t nitems, uint32_t max_nre, hipStream_t stream);
-// CRS of ports 0..nports-1 (<= 2) into grids [nsf][nports][2 nsymb][12 nof_prb] (nsymb = 7 normal CP, 6
+// CRS of ports 0..nports-1 (1, 2 or 4) into grids [nsf][nports][2 nsymb][12 nof_prb] (nsymb = 7 normal CP, 6
 // extended); d_sf_idx[sf] = tti % 10
 hipError_t crs_put_launch(float2* d_grids, uint32_t nof_prb, uint32_t cell_id, uint32_t nports, uint32_t nsymb,
                           const uint32_t* d_sf_idx, uint32_t nsf, hipStream_t stream);

@@ -701,6 +701,41 @@ __global__ __launch_bounds__(LLR_THREADS) void pdsch_tx_kernel(const PdschTx* __
                                  : make_float2((a[s].x - b[s].x) * nm, (a[s].y - b[s].y) * nm);
       t.grid[0][g] = y0;
       t.grid[1][g] = y1;
+    } else if (t.scheme == 4) {  // transmit diversity, 4 ports (layermap.c:38-47 + precoding.c:1961-1988):
+                                 // groups (4i .. 4i+3) of the codeword, SFBC on ports (0, 2) then (1, 3)
+      const float  h  = t.div_scale;
+      const float2 z  = make_float2(0.f, 0.f);
+      const uint32_t b = (uint32_t)s & ~3u;  // k0 is a multiple of 4: the group is inside the thread
+      const float2 x0 = a[b], x1 = a[b + 1], x2 = a[b + 2], x3 = a[b + 3];
+      if (4 * (k / 4) + 3 >= t.nre) {
+        break;  // a trailing half group is not transmitted (m_ap = 4 * (nre / 4))
+      }
+      switch (k & 3u) {
+        case 0:
+          t.grid[0][g] = make_float2(x0.x * h, x0.y * h);
+          t.grid[1][g] = z;
+          t.grid[2][g] = make_float2(-x1.x * h, x1.y * h);
+          t.grid[3][g] = z;
+          break;
+        case 1:
+          t.grid[0][g] = make_float2(x1.x * h, x1.y * h);
+          t.grid[1][g] = z;
+          t.grid[2][g] = make_float2(x0.x * h, -x0.y * h);
+          t.grid[3][g] = z;
+          break;
+        case 2:
+          t.grid[0][g] = z;
+          t.grid[1][g] = make_float2(x2.x * h, x2.y * h);
+          t.grid[2][g] = z;
+          t.grid[3][g] = make_float2(-x3.x * h, x3.y * h);
+          break;
+        default:
+          t.grid[0][g] = z;
+          t.grid[1][g] = make_float2(x3.x * h, x3.y * h);
+          t.grid[2][g] = z;
+          t.grid[3][g] = make_float2(x2.x * h, -x2.y * h);
+          break;
+      }
     } else {  // transmit diversity, 2 ports (layermap.c + precoding.c:1943-1960): pairs (2i, 2i+1)
       const float  h  = t.div_scale;
       const bool   ev = (k & 1u) == 0;
@@ -730,7 +765,7 @@ hipError_t pdsch_tx_launch(const PdschTx* d_items, uint32_t nitems, uint32_t max
   return hipGetLastError();
 }
 
-// cell-specific reference signals of 1 or 2 ports (refsignal_dl.c, 36.211 6.10.1): grid (CRS symbol of
+// cell-specific reference signals of 1, 2 or 4 ports (refsignal_dl.c, 36.211 6.10.1): grid (CRS symbol of
 // the subframe, port, subframe); 2 * nof_prb pilots a symbol
 __global__ __launch_bounds__(256) void crs_put_kernel(float2* __restrict__ grids, uint32_t nof_prb, uint32_t cell_id,
                                                       uint32_t nports, uint32_t nsymb,
@@ -741,6 +776,23 @@ __global__ __launch_bounds__(256) void crs_put_kernel(float2* __restrict__ grids
   const uint32_t slot = sym >> 1, l = (sym & 1) ? nsymb - 3 : 0u;
   const uint32_t ns   = 2 * sf_idx[sf] + slot;
   const uint32_t v    = port == 0 ? (l == 0 ? 0u : 3u) : (l == 0 ? 3u : 0u);
+  if (port >= 2) {  // ports 2 / 3: one CRS symbol a slot, l = 1, v = 3 (ns mod 2) (+ 3 for port 3)
+    if (sym & 1) {
+      return;
+    }
+    const uint32_t l1 = 1, v1 = (3 * (ns & 1u) + (port == 3 ? 3u : 0u)) % 6;
+    const uint32_t s1 = (1u << 10) * (7 * (ns + 1) + l1 + 1) * (2 * cell_id + 1) + 2 * cell_id + (nsymb == 7 ? 1u : 0u);
+    float2* row1 = grids + (((size_t)sf * nports + port) * 2 * nsymb + nsymb * slot + l1) * (12 * nof_prb);
+    for (uint32_t m = threadIdx.x; m < 2 * nof_prb; m += 256) {
+      const uint32_t mp = m + 110 - nof_prb;
+      uint32_t       x1, x2;
+      gold_at(s1, 2 * mp, x1, x2);
+      const uint32_t c = gold16(x1, x2);
+      const float    r = (float)0.70710678118654752440;
+      row1[6 * m + (v1 + cell_id % 6) % 6] = make_float2((c & 1u) ? -r : r, (c & 2u) ? -r : r);
+    }
+    return;
+  }
   const uint32_t seed = (1u << 10) * (7 * (ns + 1) + l + 1) * (2 * cell_id + 1) + 2 * cell_id + (nsymb == 7 ? 1u : 0u);
   const uint32_t nre  = 12 * nof_prb;
   float2*        row  = grids + (((size_t)sf * nports + port) * 2 * nsymb + nsymb * slot + l) * nre;
@@ -760,7 +812,7 @@ hipError_t crs_put_launch(float2* d_grids, uint32_t nof_prb, uint32_t cell_id, u
   if (nsf == 0) {
     return hipSuccess;
   }
-  if (nports == 0 || nports > 2 || (nsymb != 7 && nsymb != 6)) {
+  if (nports == 0 || nports == 3 || nports > 4 || (nsymb != 7 && nsymb != 6)) {
     return hipErrorInvalidValue;
   }
   hipError_t e = gold_tables_init();

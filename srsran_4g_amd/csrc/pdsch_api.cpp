@@ -545,6 +545,8 @@ int srsran_pdsch_encode(srsran_pdsch_t*     q,
     scheme = 0;
   } else if (gr.tx_scheme == SRSRAN_TXSCHEME_DIVERSITY && P == 2 && gr.nof_tb == 1) {
     scheme = 1;
+  } else if (gr.tx_scheme == SRSRAN_TXSCHEME_DIVERSITY && P == 4 && gr.nof_tb == 1) {
+    scheme = 4;
   } else if (gr.tx_scheme == SRSRAN_TXSCHEME_CDD && P == 2 && gr.nof_tb == 2 && gr.nof_layers == 2) {
     scheme = 3;
   } else {
@@ -571,7 +573,7 @@ int srsran_pdsch_encode(srsran_pdsch_t*     q,
   it.nre       = nre;
   it.scheme    = scheme;
   it.scaling   = 1.0f;
-  it.div_scale = (float)(1.0 * 0.70710678118654752440);
+  it.div_scale = scheme == 4 ? (float)(1.0f / 1.41421356237309504880) : (float)(1.0 * 0.70710678118654752440);
   size_t   off = align256((size_t)P * nsf_re * sizeof(float2));
   size_t   o_idx = off;
   off += align256((size_t)nre * sizeof(uint32_t));

@@ -283,3 +283,28 @@ def test_ue_dl_batch_four_ports(U, SCH, ora):
         assert np.array_equal(out[0][1][: tbs // 8 + 6], pl[b, 0, : tbs // 8 + 6])
     ue.free()
     ue2.free()
+
+
+@pytest.mark.parametrize("tti,cfi,cp", [(3, 1, 0), (0, 2, 0), (5, 1, 1)])
+def test_enb_tx_four_ports(U, tti, cfi, cp):
+    """srsran_enb_dl_gpu_tx_batch on a 4-port cell (CRS of ports 0..3, SFBC + FSTD) == the CPU
+    transmitter, and the GPU UE DL chain decodes it"""
+    from srsran_4g_amd import enb_dl as E
+    nprb, cell_id, rnti, tbs = 100, 37, 0x4601, 36696
+    N = SY.symbol_sz(nprb)
+    nre = int(SY.pdsch_mask(nprb, 4, cell_id, cfi, tti % 10, cp=cp).sum())
+    assert nre % 4 == 0
+    rng = np.random.default_rng(tbs + tti)
+    payloads = [rng.integers(0, 256, tbs // 8, dtype=np.uint8)]
+    want, _ = SY.pdsch_subframe(nprb, cell_id, 4, tti, cfi, rnti, tbs, 6, 0, payloads, scheme="diversity4", nrx=4,
+                                N=N, channel=np.eye(4), pcfich=False, cp=cp)
+    enb = E.EnbDl(U.cell(nprb, 4, cell_id, cp=cp))
+    cfg = U.pdsch_cfg(nprb, nre, [tbs], [6], scheme="diversity", rnti=rnti, cp=cp, nof_ports=4)
+    d_pl = [torch.from_numpy(p).cuda() for p in payloads]
+    d_out = torch.zeros((4, want.shape[1], 2), dtype=torch.float32, device="cuda")
+    assert enb.tx_batch([(tti, cfi, cfg, [p.data_ptr() for p in d_pl])], d_out.data_ptr(), 1.0 / N) == 0
+    torch.cuda.synchronize()
+    got = d_out.cpu().numpy().view(np.complex64)[..., 0]
+    scale = np.abs(want).max()
+    assert np.abs(got - want).max() < 2e-5 * scale * np.sqrt(np.log2(N))
+    enb.free()

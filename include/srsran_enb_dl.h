@@ -8,7 +8,7 @@
  *     srsran_dlsch_encode2, srsran_sequence_pdsch_apply_pack, srsran_mod_modulate_bytes,
  *     srsran_layermap_type / srsran_precoding_type, srsran_pdsch_put),
  *   srsran_enb_dl_gen_signal (enb_dl.c:446-470: amplitude 0.05 / sqrt(N_RB), srsran_ofdm_tx_sf).
- * Transmission schemes: PORT0 (1 port), TX diversity (2 ports, 1 TB), CDD (2 ports, 2 TBs); normal or
+ * Transmission schemes: PORT0 (1 port), TX diversity (2 or 4 ports, 1 TB), CDD (2 ports, 2 TBs); normal or
  * extended CP;
  * rho_a = 1.  Not generated here (their REs stay empty): PSS / SSS, PBCH, PCFICH, PHICH, PDCCH.
  */

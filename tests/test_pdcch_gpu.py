@@ -199,3 +199,43 @@ def test_find_dl_dci_and_pdsch_without_injected_grant(mods):
         assert ue.find_dl_dci(tti, cfi, 0x4321, tm=2) == []
     finally:
         ue.free()
+
+
+def test_find_dl_dci_and_pdsch_four_ports(mods):
+    """4-port TM2 cell: time samples -> OFDM -> 4-port CRS estimate -> PCFICH and PDCCH with 4-port SFBC +
+    FSTD -> format 1 grant -> 4-port transmit-diversity PDSCH decode; payload equal"""
+    PD, U = mods
+    from srsran_4g_amd import sch
+    from synth import synth as S
+
+    cid, tti, cfi, rnti, mcs = 6, 3, 2, 0x2222, 20
+    rng = np.random.default_rng(43)
+    c = PD.cell(100, 4, cid)
+    lib = U.lib()
+    tbs = lib.srsran_ra_tbs_from_idx(lib.srsran_ra_tbs_idx_from_mcs(mcs, False, False), 100)
+    bits = P.dci_pack_1(100, PD.dci_size(c, P.FORMAT1), (1 << 25) - 1, mcs, 2, 1, 0)
+    regs = PD.Regs(c)
+    nof_cce = regs.q.pdcch_nregs[cfi - 1] // 9
+    regs.free()
+    L, ncce = [loc for loc in PD.ue_locations(nof_cce, tti % 10, rnti) if loc[0] == 2][0]
+    ctrl = P.Ref().ctrl_tx(100, 4, cid, tti, cfi, [(bits, L, ncce, rnti)])
+    pl = [rng.integers(0, 256, tbs // 8, dtype=np.uint8)]
+    x, nre = S.pdsch_subframe(100, cid, 4, tti, cfi, rnti, tbs, 6, 0, pl, scheme="diversity4", snr_db=30.0, rng=rng,
+                              pcfich=False, ctrl=list(ctrl[:4]))
+    U.use_standard_symbol_size(True)
+    ue = U.UeDl(U.cell(100, 4, cid), 2)
+    try:
+        assert ue.fft_estimate(x, tti, 0) == 0
+        assert ue.last_cfi == cfi
+        dcis = ue.find_dl_dci(tti, cfi, rnti, tm=1)
+        assert len(dcis) == 1 and dcis[0].format == P.FORMAT1 and dcis[0].rnti == rnti
+        r, g = ue.dci_to_grant(dcis[0], tti, cfi, tm=1)
+        assert r == 0 and g.nof_tb == 1 and g.tb[0].tbs == tbs and g.nof_re == nre and g.nof_layers == 4
+        sbs = [sch.SoftbufferRx(nof_prb=100)]
+        cfg = U.pdsch_cfg(100, nre, [tbs], [6], scheme="diversity", softbuffers=sbs, nof_ports=4)
+        cfg.grant = g
+        cfg.rnti = rnti
+        ret, res = ue.decode_pdsch(cfg, tti, cfi)
+        assert ret == 0 and res[0][0] and np.array_equal(res[0][1][:tbs // 8], pl[0])
+    finally:
+        ue.free()

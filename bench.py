@@ -109,7 +109,8 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--workload", choices=["all188", "k6144", "dlsch", "ulsch", "pusch", "dlenc", "pdsch", "ldpc", "nrsch"],
+    p.add_argument("--workload", choices=["all188", "k6144", "dlsch", "ulsch", "pusch", "dlenc", "pdsch", "dlloop", "ldpc",
+                                          "nrsch"],
                    default="all188")
     p.add_argument("--snr", type=float, default=30.0, help="pdsch: AWGN SNR (dB) of the synthetic subframes")
     p.add_argument("--subframes", type=int, default=78,
@@ -675,6 +676,99 @@ def run_dlenc(args, torch, dist, world, rank, device):
         print(json.dumps(result), flush=True)
 
 
+def run_dlloop(args, torch, dist, world, rank, device):
+    """Device-resident C3 loopback: per step the GPU eNB transmitter
+    (srsran_enb_dl_gpu_tx_batch: DL-SCH encode, CRS, scrambling, 64QAM, CDD 2x2, OFDM) produces
+    `subframes` C3 subframes, a static 2x2 channel [[1, 1], [1, -1]] with AWGN is applied on the GPU
+    (torch), and the GPU UE DL chain (srsran_ue_dl_gpu_decode_batch) decodes them -- no host data in
+    the loop.  Value = loop subframes/s; the transmitter alone is timed with HIP events."""
+    from srsran_4g_amd import enb_dl as E
+    from srsran_4g_amd import sch as S
+    from srsran_4g_amd import ue_dl as U
+    from synth import synth as SY
+
+    cell_id, rnti, nsf = shard(rank)["cell_id"], 0x1234, args.subframes
+    U.use_standard_symbol_size(True)
+    cell = U.cell(100, 2, cell_id)
+    enb = E.EnbDl(cell)
+    ue = U.UeDl(cell, 2)
+    ue.cfg.cfg.pdsch.max_nof_iterations = args.iters
+    gen = torch.Generator(device=device)
+    gen.manual_seed(shard(rank)["seed"])
+    d_tx_pl = torch.randint(0, 256, (nsf, 2, C3_TBS // 8), dtype=torch.uint8, device=device, generator=gen)
+    ttis = [b % 10 + 1 for b in range(nsf)]
+    nres = [int(SY.pdsch_mask(100, 2, cell_id, 1, t % 10).sum()) for t in ttis]
+    tx_cfgs = [U.pdsch_cfg(100, nres[b], (C3_TBS, C3_TBS), (C3_QM, C3_QM), rnti=rnti) for b in range(nsf)]
+    sbs = [[S.SoftbufferRx(nof_prb=100) for _ in range(2)] for _ in range(nsf)]
+    rx_cfgs = [U.pdsch_cfg(100, nres[b], (C3_TBS, C3_TBS), (C3_QM, C3_QM), rnti=rnti, max_iterations=args.iters,
+                           softbuffers=sbs[b]) for b in range(nsf)]
+    tx_sfs = [(ttis[b], 1, tx_cfgs[b], [d_tx_pl[b, 0].data_ptr(), d_tx_pl[b, 1].data_ptr()]) for b in range(nsf)]
+    sf_len = 30720  # SRSRAN_SF_LEN_PRB(100) at N = 2048: 1 ms at 30.72 Msps
+    d_tx = torch.zeros((nsf, 2, sf_len), dtype=torch.complex64, device=device)
+    d_x = torch.zeros((nsf, 2, sf_len), dtype=torch.complex64, device=device)
+    H = torch.tensor([[1, 1], [1, -1]], dtype=torch.complex64, device=device)
+    d_pl = torch.zeros((nsf, 2, C3_TBS // 8 + 64), dtype=torch.uint8, device=device)
+    d_res = torch.zeros(2 * nsf, dtype=torch.int32, device=device)
+    d_avg = torch.zeros(2 * nsf, dtype=torch.float32, device=device)
+    arr = U.UeDl.batch_entries([(ttis[b], 1, rx_cfgs[b], [d_pl[b, 0].data_ptr(), d_pl[b, 1].data_ptr()], [1, 1])
+                                for b in range(nsf)])
+    stream = torch.cuda.current_stream(device)
+    sp = stream.cuda_stream
+    if enb.tx_batch(tx_sfs, d_tx.data_ptr(), 0.0, sp) != 0:
+        raise RuntimeError("srsran_enb_dl_gpu_tx_batch failed")
+    rx0 = torch.matmul(H, d_tx)
+    sigma = float(torch.sqrt(torch.mean(torch.abs(rx0) ** 2) / 10 ** (args.snr / 10) / 2))
+    noise = torch.zeros((nsf, 2, sf_len, 2), dtype=torch.float32, device=device)
+
+    def step():
+        if enb.tx_batch(tx_sfs, d_tx.data_ptr(), 0.0, sp) != 0:
+            raise RuntimeError("srsran_enb_dl_gpu_tx_batch failed")
+        noise.normal_(0.0, sigma, generator=gen)
+        torch.matmul(H, d_tx, out=d_x)
+        d_x.add_(torch.view_as_complex(noise))
+        if ue.gpu_decode_batch(arr, d_x.data_ptr(), d_res.data_ptr(), d_avg.data_ptr(), 0.0, sp) != 2 * nsf:
+            raise RuntimeError("srsran_ue_dl_gpu_decode_batch failed")
+
+    elapsed = timed_region(step, args.steps, args.warmup, world, dist, torch.cuda.synchronize, device)
+    ok = float((d_res == 0).float().mean().item())
+    match = bool(torch.equal(d_pl[:, :, : C3_TBS // 8], d_tx_pl))
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(args.steps):
+        enb.tx_batch(tx_sfs, d_tx.data_ptr(), 0.0, sp)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    tx_ms = e0.elapsed_time(e1) / args.steps
+    value = world * nsf * args.steps / elapsed
+    result = {
+        "metric": "PDSCH loopback subframes/s (GPU eNB TX -> channel -> GPU UE RX), C3",
+        "value": round(value, 1),
+        "unit": "subframes/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic, device-resident: random payloads encoded and transmitted on the GPU every step",
+        "config": {"workload": "dlloop C3: %d subframes x (2 TBs x 75376 bits, 64QAM, CDD 2x2, 100 PRB, CFI 1), "
+                               "channel [[1,1],[1,-1]] + AWGN %.0f dB, max %d half-its" % (nsf, args.snr, args.iters),
+                   "parallelism": f"carrier-sharded x{world}"},
+        "mbps": round(value * 2 * C3_TBS / 1e6, 1),
+        "tx_subframes_per_s": round(nsf / (tx_ms * 1e-3), 1),
+        "tx_ms_per_step": round(tx_ms, 4),
+        "tb_ok_fraction": ok,
+        "payloads_equal": match,
+    }
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    enb.free()
+    ue.free()
+    return result
+
+
 def run_pdsch(args, torch, dist, world, rank, device, steps=None, warmup=None, cpu_seconds=None, emit=True):
     """UE DL chain on C3 subframes: per step `subframes` subframes of 2 rx x 30720 cf32 samples
     -> 2 TBs each (TBS 75376, 64QAM, TM3 CDD 2x2, CFI 1), new transmissions, at most `iters`
@@ -1145,6 +1239,8 @@ def main():
         return run_pusch(args, torch, dist, world, rank, device)
     if args.workload == "dlenc":
         return run_dlenc(args, torch, dist, world, rank, device)
+    if args.workload == "dlloop":
+        return run_dlloop(args, torch, dist, world, rank, device)
     if args.workload == "pdsch":
         return run_pdsch(args, torch, dist, world, rank, device)
     if args.workload == "ldpc":

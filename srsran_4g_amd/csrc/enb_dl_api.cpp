@@ -7,6 +7,8 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/srsran_enb_dl.h"
@@ -31,7 +33,44 @@ struct EnbDlGpu {
   size_t        items_cap = 0;
   uint32_t*     d_sfidx = nullptr;
   size_t        sfidx_cap = 0;
+  // RE tables on the device, keyed by (PRB allocation, symbols a slot, first symbol, subframe): built
+  // once, not re-uploaded every batch
+  std::unordered_map<std::string, std::pair<uint32_t*, uint32_t>> tabs;
 };
+
+const std::pair<uint32_t*, uint32_t>* get_tab(EnbDlGpu* g, const srsran_cell_t& cell, const srsran_pdsch_grant_t& gr,
+                                               uint32_t lstart, uint32_t sf_idx)
+{
+  std::string key;
+  key.reserve(2 * cell.nof_prb + 8);
+  for (uint32_t s = 0; s < 2; s++) {
+    for (uint32_t n = 0; n < cell.nof_prb; n++) {
+      key.push_back(gr.prb_idx[s][n] ? '1' : '0');
+    }
+    key.push_back((char)gr.nof_symb_slot[s]);
+  }
+  key.push_back((char)lstart);
+  key.push_back((char)sf_idx);
+  auto it = g->tabs.find(key);
+  if (it != g->tabs.end()) {
+    return &it->second;
+  }
+  if (g->tabs.size() >= 512) {  // bound the cache; earlier launches may still read the tables
+    hipDeviceSynchronize();
+    for (auto& kv : g->tabs) {
+      hipFree(kv.second.first);
+    }
+    g->tabs.clear();
+  }
+  const std::vector<uint32_t> t = pdsch_re_table(cell, gr, lstart, sf_idx);
+  uint32_t*                   d = nullptr;
+  if (hipMalloc((void**)&d, std::max<size_t>(t.size(), 1) * sizeof(uint32_t)) != hipSuccess ||
+      hipMemcpy(d, t.data(), t.size() * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) {
+    hipFree(d);
+    return nullptr;
+  }
+  return &(g->tabs[key] = std::make_pair(d, (uint32_t)t.size()));
+}
 
 bool grow(void** p, size_t* cap, size_t need)
 {
@@ -92,6 +131,9 @@ void srsran_enb_dl_gpu_free(srsran_enb_dl_gpu_t* q)
     hipFree(g->d_idx);
     hipFree(g->d_items);
     hipFree(g->d_sfidx);
+    for (auto& kv : g->tabs) {
+      hipFree(kv.second.first);
+    }
     delete g;
   }
   memset(q, 0, sizeof(*q));
@@ -114,12 +156,12 @@ int srsran_enb_dl_gpu_tx_batch(srsran_enb_dl_gpu_t*          q,
   hipStream_t         st    = (hipStream_t)stream;
   const srsran_cell_t& cell = q->cell;
   const uint32_t      P     = cell.nof_ports, nre_sf = SRSRAN_SF_LEN_RE(cell.nof_prb, cell.cp);
-  std::vector<std::vector<uint32_t>> tables(nof_sf);
+  std::vector<const std::pair<uint32_t*, uint32_t>*> tables(nof_sf);
   std::vector<PdschTx>               items(nof_sf);
   std::vector<srsran_dlsch_gpu_enc_t> enc;
   std::vector<size_t>                 e_off;
   std::vector<uint32_t>               sfidx(nof_sf);
-  size_t                              e_tot = 0, idx_tot = 0;
+  size_t                              e_tot = 0;
   uint32_t                            max_nre = 0;
   for (uint32_t b = 0; b < nof_sf; b++) {
     const srsran_enb_dl_gpu_sf_t& s   = sfs[b];
@@ -144,8 +186,11 @@ int srsran_enb_dl_gpu_tx_batch(srsran_enb_dl_gpu_t*          q,
     }
     sfidx[b]  = s.tti % 10;
     const uint32_t lstart = s.cfi + (cell.nof_prb < 10 ? 1 : 0);  // SRSRAN_NOF_CTRL_SYMBOLS
-    tables[b] = pdsch_re_table(cell, gr, lstart, sfidx[b]);
-    const uint32_t nre = (uint32_t)tables[b].size();
+    tables[b] = get_tab(g, cell, gr, lstart, sfidx[b]);
+    if (!tables[b]) {
+      return SRSRAN_ERROR;
+    }
+    const uint32_t nre = tables[b]->second;
     max_nre            = std::max(max_nre, nre);
     PdschTx& it        = items[b];
     memset(&it, 0, sizeof(it));
@@ -175,23 +220,18 @@ int srsran_enb_dl_gpu_tx_batch(srsran_enb_dl_gpu_t*          q,
     if ((scheme == 3) != (cw == 2)) {
       return SRSRAN_ERROR_INVALID_INPUTS;
     }
-    idx_tot += (nre + 3) & ~3u;
   }
   const size_t grid_bytes = (size_t)nof_sf * P * nre_sf * sizeof(float2);
   if (!grow((void**)&g->d_grid, &g->grid_cap, grid_bytes) || !grow((void**)&g->d_e, &g->e_cap, e_tot + 16) ||
-      !grow((void**)&g->d_idx, &g->idx_cap, idx_tot * sizeof(uint32_t) + 16) ||
       !grow((void**)&g->d_items, &g->items_cap, nof_sf * sizeof(PdschTx)) ||
       !grow((void**)&g->d_sfidx, &g->sfidx_cap, nof_sf * sizeof(uint32_t))) {
     return SRSRAN_ERROR;
   }
   // device pointers of the codewords, tables and grids
-  std::vector<uint32_t> idx_host(idx_tot);
-  size_t                io = 0, k = 0;
+  size_t k = 0;
   for (uint32_t b = 0; b < nof_sf; b++) {
-    memcpy(&idx_host[io], tables[b].data(), tables[b].size() * sizeof(uint32_t));
     PdschTx& it = items[b];
-    it.idx      = g->d_idx + io;
-    io += (tables[b].size() + 3) & ~(size_t)3;
+    it.idx      = tables[b]->first;
     for (uint32_t p = 0; p < P; p++) {
       it.grid[p] = g->d_grid + ((size_t)b * P + p) * nre_sf;
     }
@@ -203,7 +243,6 @@ int srsran_enb_dl_gpu_tx_batch(srsran_enb_dl_gpu_t*          q,
   }
   if (srsran_dlsch_gpu_encode_batch(&g->sch, (uint32_t)enc.size(), enc.data(), st) != SRSRAN_SUCCESS ||
       hipMemsetAsync(g->d_grid, 0, grid_bytes, st) != hipSuccess ||
-      hipMemcpyAsync(g->d_idx, idx_host.data(), idx_tot * sizeof(uint32_t), hipMemcpyHostToDevice, st) != hipSuccess ||
       hipMemcpyAsync(g->d_items, items.data(), nof_sf * sizeof(PdschTx), hipMemcpyHostToDevice, st) != hipSuccess ||
       hipMemcpyAsync(g->d_sfidx, sfidx.data(), nof_sf * sizeof(uint32_t), hipMemcpyHostToDevice, st) != hipSuccess ||
       crs_put_launch(g->d_grid, cell.nof_prb, cell.id, P, SRSRAN_CP_NSYMB(cell.cp), g->d_sfidx, nof_sf, st) != hipSuccess ||

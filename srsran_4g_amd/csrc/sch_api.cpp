@@ -17,6 +17,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/srsran_sch.h"
@@ -143,7 +144,74 @@ struct SbGpu {
   uint8_t* d_data  = nullptr;  // max_cb x data_stride bytes
   uint8_t* d_flags = nullptr;  // [0, max_cb): cb_crc, [max_cb]: tb_crc
   uint32_t stride = 0, data_stride = 0;
+  size_t   buf_bytes = 0;      // d_buf size (rounded as the arena hands it out)
+  int      buf_dev   = -1;     // >= 0: d_buf lives in that device's soft-buffer arena
 };
+
+// Soft-buffer arena: the int16 soft buffers of every srsran_softbuffer_rx_t of a device come from one
+// 1 GiB allocation, so that a batch's code blocks lie within the 31-bit offset range the lane-pair
+// decoder's buffer resource addresses from its lowest block (sch_api.cpp, `in_near`).  Separate
+// hipMallocs can scatter across the address space and silently force the slower decoder.  Freed
+// buffers are kept per size for reuse; when the arena is full, buffers fall back to hipMalloc.
+struct SbArena {
+  uint8_t*                       base = nullptr;
+  size_t                         cap = 0, top = 0;
+  bool                           tried = false;
+  std::multimap<size_t, size_t>  free_by_size;  // size -> offset
+};
+std::mutex                       g_arena_mu;
+std::unordered_map<int, SbArena> g_arenas;
+constexpr size_t                 kArenaBytes = (size_t)1 << 30;
+
+void* sb_arena_alloc(size_t bytes, int* dev_out)
+{
+  bytes   = (bytes + 255) & ~(size_t)255;
+  int dev = 0;
+  hipGetDevice(&dev);
+  {
+    std::lock_guard<std::mutex> lk(g_arena_mu);
+    SbArena&                    a = g_arenas[dev];
+    if (!a.tried) {
+      a.tried = true;
+      if (hipMalloc((void**)&a.base, kArenaBytes) == hipSuccess) {
+        a.cap = kArenaBytes;
+      } else {
+        a.base = nullptr;
+      }
+    }
+    auto it = a.free_by_size.find(bytes);
+    if (it != a.free_by_size.end()) {
+      const size_t off = it->second;
+      a.free_by_size.erase(it);
+      *dev_out = dev;
+      return a.base + off;
+    }
+    if (a.base && a.top + bytes <= a.cap) {
+      const size_t off = a.top;
+      a.top += bytes;
+      *dev_out = dev;
+      return a.base + off;
+    }
+  }
+  void* p  = nullptr;
+  *dev_out = -1;
+  return hipMalloc(&p, bytes) == hipSuccess ? p : nullptr;
+}
+
+void sb_arena_free(void* p, size_t bytes, int dev)
+{
+  if (!p) {
+    return;
+  }
+  if (dev < 0) {
+    hipFree(p);
+    return;
+  }
+  bytes = (bytes + 255) & ~(size_t)255;
+  std::lock_guard<std::mutex> lk(g_arena_mu);
+  SbArena&                    a = g_arenas[dev];
+  a.free_by_size.emplace(bytes, (size_t)((uint8_t*)p - a.base));
+}
 
 }  // namespace
 
@@ -704,7 +772,8 @@ int srsran_softbuffer_rx_init_guru(srsran_softbuffer_rx_t* q, uint32_t max_cb, u
   q->data        = (uint8_t**)calloc(max_cb ? max_cb : 1, sizeof(uint8_t*));
   q->cb_crc      = (bool*)calloc(max_cb ? max_cb : 1, sizeof(bool));
   if (!q->buffer_f || !q->data || !q->cb_crc ||
-      hipMalloc((void**)&g->d_buf, std::max<size_t>((size_t)max_cb * g->stride * sizeof(int16_t), 8)) != hipSuccess ||
+      !(g->buf_bytes = std::max<size_t>((size_t)max_cb * g->stride * sizeof(int16_t), 8),
+        g->d_buf     = (short*)sb_arena_alloc(g->buf_bytes, &g->buf_dev)) ||
       hipMalloc((void**)&g->d_data, std::max<size_t>((size_t)max_cb * g->data_stride, 8)) != hipSuccess ||
       hipMalloc((void**)&g->d_flags, max_cb + 1) != hipSuccess) {
     srsran_softbuffer_rx_free(q);
@@ -788,7 +857,7 @@ void srsran_softbuffer_rx_free(srsran_softbuffer_rx_t* q)
   SbGpu* g = (SbGpu*)q->gpu;
   if (g) {
     hipDeviceSynchronize();
-    hipFree(g->d_buf);
+    sb_arena_free(g->d_buf, g->buf_bytes, g->buf_dev);
     hipFree(g->d_data);
     hipFree(g->d_flags);
     delete g;

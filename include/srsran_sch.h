@@ -22,6 +22,7 @@
 #define SRSRAN_AMD_SCH_H
 
 #include <stdbool.h>
+#include <stddef.h>
 #include <stdint.h>
 
 #include "srsran_tdec.h"
@@ -114,6 +115,12 @@ void srsran_softbuffer_rx_reset_cb_crc(srsran_softbuffer_rx_t* q, uint32_t nof_c
 void srsran_softbuffer_rx_free(srsran_softbuffer_rx_t* p);
 /* added: copy the device cb_crc / tb_crc flags into the host mirror (after asynchronous batches) */
 int srsran_softbuffer_rx_sync(srsran_softbuffer_rx_t* q);
+/* added: soft-buffer device arena of the soft buffers initialised from now on: enable = 0 gives
+   every soft buffer its own hipMalloc; bytes (> 0) = capacity of per-device arenas not created yet
+   (default 1 GiB).  Decoding results and decoder choice do not depend on it. */
+int srsran_softbuffer_rx_gpu_arena(int enable, size_t bytes);
+/* added: device address of the soft buffer's first code block (diagnostics) */
+const void* srsran_softbuffer_rx_gpu_ptr(const srsran_softbuffer_rx_t* q);
 
 /* ---------------- grant / PDSCH configuration (ra.h:43-53, pdsch_cfg.h:37-71) ---------------- */
 typedef enum {

@@ -148,6 +148,15 @@ const char* srsran_tdec_gpu_kernel_name(uint32_t long_cb);
    decoder of K >= 816 from 1024 blocks a launch), for profiling reports. */
 const char* srsran_tdec_gpu_kernel_name_batch(uint32_t long_cb, uint32_t nof_cb);
 
+/* Name of the last turbo-decoder kernel the calling thread launched (any API: plain, multi-size,
+   DL-SCH / UL-SCH batches), "" before the first, as rocprofv3 reports it. */
+const char* srsran_tdec_gpu_last_kernel(void);
+
+/* Blocks per launch (or per fused class launch) from which the 16-sub-block class runs the lane-pair
+   decoder (default 1024: below it the quad decoder fills the chip better).  Process-wide. */
+void     srsran_tdec_gpu_set_pair_threshold(uint32_t nof_cb);
+uint32_t srsran_tdec_gpu_get_pair_threshold(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -146,13 +146,35 @@ struct SbGpu {
   uint32_t stride = 0, data_stride = 0;
   size_t   buf_bytes = 0;      // d_buf size (rounded as the arena hands it out)
   int      buf_dev   = -1;     // >= 0: d_buf lives in that device's soft-buffer arena
+  int      dev       = 0;      // the device every buffer of this soft buffer lives on
+};
+
+// Makes `dev` current for a scope and restores the caller's device: soft buffers are synchronised
+// and released on the device they live on, whatever device the caller has selected.
+struct DevScope {
+  int prev = -1;
+  explicit DevScope(int dev)
+  {
+    if (hipGetDevice(&prev) == hipSuccess && prev != dev) {
+      hipSetDevice(dev);
+    } else {
+      prev = -1;
+    }
+  }
+  ~DevScope()
+  {
+    if (prev >= 0) {
+      hipSetDevice(prev);
+    }
+  }
 };
 
 // Soft-buffer arena: the int16 soft buffers of every srsran_softbuffer_rx_t of a device come from one
-// 1 GiB allocation, so that a batch's code blocks lie within the 31-bit offset range the lane-pair
-// decoder's buffer resource addresses from its lowest block (sch_api.cpp, `in_near`).  Separate
-// hipMallocs can scatter across the address space and silently force the slower decoder.  Freed
-// buffers are kept per size for reuse; when the arena is full, buffers fall back to hipMalloc.
+// allocation (1 GiB by default, srsran_softbuffer_rx_gpu_arena), which keeps the per-object
+// hipMalloc off the HARQ setup path and the blocks of a batch close together in L2 / TLB terms.
+// Decoder selection does not depend on it: the turbo descriptor list is padded wherever two
+// blocks of a lane-pair workgroup lie far apart (tdec_pair_cbs).  Freed buffers are kept per size
+// for reuse; when the arena is full, buffers fall back to hipMalloc (reported once).
 struct SbArena {
   uint8_t*                       base = nullptr;
   size_t                         cap = 0, top = 0;
@@ -161,20 +183,22 @@ struct SbArena {
 };
 std::mutex                       g_arena_mu;
 std::unordered_map<int, SbArena> g_arenas;
-constexpr size_t                 kArenaBytes = (size_t)1 << 30;
+size_t                           g_arena_bytes = (size_t)1 << 30;  // capacity of arenas created from now on
+bool                             g_arena_on    = true;             // false: every buffer its own hipMalloc
+bool                             g_arena_warned = false;
 
 void* sb_arena_alloc(size_t bytes, int* dev_out)
 {
   bytes   = (bytes + 255) & ~(size_t)255;
   int dev = 0;
   hipGetDevice(&dev);
-  {
+  if (g_arena_on) {
     std::lock_guard<std::mutex> lk(g_arena_mu);
     SbArena&                    a = g_arenas[dev];
     if (!a.tried) {
       a.tried = true;
-      if (hipMalloc((void**)&a.base, kArenaBytes) == hipSuccess) {
-        a.cap = kArenaBytes;
+      if (hipMalloc((void**)&a.base, g_arena_bytes) == hipSuccess) {
+        a.cap = g_arena_bytes;
       } else {
         a.base = nullptr;
       }
@@ -191,6 +215,11 @@ void* sb_arena_alloc(size_t bytes, int* dev_out)
       a.top += bytes;
       *dev_out = dev;
       return a.base + off;
+    }
+    if (!g_arena_warned) {
+      g_arena_warned = true;
+      fprintf(stderr, "[srsran_softbuffer] soft-buffer arena of device %d full (%zu MiB): further buffers use hipMalloc\n",
+              dev, a.cap >> 20);
     }
   }
   void* p  = nullptr;
@@ -361,20 +390,26 @@ int enqueue_batch(srsran_sch_t* q, uint32_t ntb, const srsran_dlsch_gpu_tb_t* tb
       slot_crc_a[slot] = s.C == 1;  // single-CB TB: CRC24A over tbs + 24 (sch.c:440-446)
     }
   }
+  // turbo descriptors by K; every two consecutive blocks of a group (one lane-pair workgroup) lie
+  // within TDEC_PAIR_SPAN of each other, padded where the soft buffers are far apart
   std::vector<TdecCb> cbs;
-  cbs.reserve(nslots);
+  cbs.reserve(nslots + 16);
   std::vector<std::pair<uint32_t, uint32_t>> groups;  // (K, first index into cbs)
+  std::vector<TdecCb>                        kcbs;
   for (auto& kv : by_k) {
     groups.emplace_back(kv.first, (uint32_t)cbs.size());
+    kcbs.clear();
     for (uint32_t slot : kv.second) {
       TdecCb c;
       c.in    = rm[slot].sb;
       c.skip  = rm[slot].overwrite ? x->d_zero : rm[slot].skip;  // a new transmission decodes every CB
       c.slot  = slot;
       c.crc_a = slot_crc_a[slot];
-      cbs.push_back(c);
+      kcbs.push_back(c);
     }
+    tdec_pair_cbs(kcbs.data(), (uint32_t)kcbs.size(), cbs.size(), &cbs);
   }
+  const uint32_t ncbs = (uint32_t)cbs.size();
   std::vector<SchTb> tbd(ntb);
   for (uint32_t i = 0; i < ntb; i++) {
     SchTb& t = tbd[i];
@@ -413,7 +448,7 @@ int enqueue_batch(srsran_sch_t* q, uint32_t ntb, const srsran_dlsch_gpu_tb_t* tb
     hipStreamWaitEvent(stream, x->done, 0);
   }
   const size_t off_cbs = align16(nslots * sizeof(RmSlot));
-  const size_t off_tb  = off_cbs + align16(nslots * sizeof(TdecCb));
+  const size_t off_tb  = off_cbs + align16(ncbs * sizeof(TdecCb));
   const size_t bytes   = off_tb + align16(ntb * sizeof(SchTb));
   if (x->used) {
     hipEventSynchronize(x->staged);
@@ -474,7 +509,7 @@ int enqueue_batch(srsran_sch_t* q, uint32_t ntb, const srsran_dlsch_gpu_tb_t* tb
     }
   }
   memcpy(x->h_stage, rm.data(), nslots * sizeof(RmSlot));
-  memcpy(x->h_stage + off_cbs, cbs.data(), nslots * sizeof(TdecCb));
+  memcpy(x->h_stage + off_cbs, cbs.data(), ncbs * sizeof(TdecCb));
   memcpy(x->h_stage + off_tb, tbd.data(), ntb * sizeof(SchTb));
   if (hipMemcpyAsync(x->d_stage, x->h_stage, bytes, hipMemcpyHostToDevice, stream) != hipSuccess) {
     return SRSRAN_ERROR;
@@ -491,14 +526,8 @@ int enqueue_batch(srsran_sch_t* q, uint32_t ntb, const srsran_dlsch_gpu_tb_t* tb
     for (size_t g = 0; g < groups.size() && ret == SRSRAN_SUCCESS; g++) {
       const uint32_t first = groups[g].second;
       const uint32_t count = (g + 1 < groups.size() ? groups[g + 1].second : (uint32_t)cbs.size()) - first;
-      // the lane-pair decoder reads a workgroup's two blocks from the lower soft buffer's address
-      uintptr_t lo = UINTPTR_MAX, hi = 0;
-      for (uint32_t i = first; i < first + count; i++) {
-        lo = std::min(lo, (uintptr_t)cbs[i].in);
-        hi = std::max(hi, (uintptr_t)cbs[i].in);
-      }
       ret = tdec_sch_enqueue(groups[g].first, (const TdecCb*)(x->d_stage + off_cbs) + first, count, x->d_cbout,
-                             SCH_SLOT_BYTES, x->d_noi, x->d_crc_ok, n_end, hi - lo < (1u << 31), stream);
+                             SCH_SLOT_BYTES, x->d_noi, x->d_crc_ok, n_end, stream);
     }
   }
   if (ret == SRSRAN_SUCCESS && tb_launch((const SchTb*)(x->d_stage + off_tb), ntb, max_tbs, stream) != hipSuccess) {
@@ -765,6 +794,7 @@ int srsran_softbuffer_rx_init_guru(srsran_softbuffer_rx_t* q, uint32_t max_cb, u
   SbGpu* g       = new SbGpu();
   g->stride      = (max_cb_size + 3) & ~3u;  // keeps every buffer 8-byte aligned
   g->data_stride = max_cb_size / 8;
+  hipGetDevice(&g->dev);
   q->max_cb      = max_cb;
   q->max_cb_size = max_cb_size;
   q->gpu         = g;
@@ -792,7 +822,8 @@ void srsran_softbuffer_rx_reset_cb(srsran_softbuffer_rx_t* q, uint32_t nof_cb)
   if (!q || !q->gpu) {
     return;
   }
-  SbGpu* g = (SbGpu*)q->gpu;
+  SbGpu*   g = (SbGpu*)q->gpu;
+  DevScope ds(g->dev);
   nof_cb   = std::min(nof_cb, q->max_cb);
   hipDeviceSynchronize();  // the buffers may still be in use by an asynchronous batch
   if (nof_cb) {
@@ -826,6 +857,7 @@ void srsran_softbuffer_rx_reset_cb_crc(srsran_softbuffer_rx_t* q, uint32_t nof_c
     return;
   }
   nof_cb = std::min(nof_cb, q->max_cb);
+  DevScope ds(((SbGpu*)q->gpu)->dev);
   hipDeviceSynchronize();
   hipMemset(((SbGpu*)q->gpu)->d_flags, 0, nof_cb);
   hipDeviceSynchronize();
@@ -838,6 +870,7 @@ int srsran_softbuffer_rx_sync(srsran_softbuffer_rx_t* q)
     return SRSRAN_ERROR_INVALID_INPUTS;
   }
   std::vector<uint8_t> f(q->max_cb + 1);
+  DevScope             ds(((SbGpu*)q->gpu)->dev);
   hipDeviceSynchronize();
   if (hipMemcpy(f.data(), ((SbGpu*)q->gpu)->d_flags, f.size(), hipMemcpyDeviceToHost) != hipSuccess) {
     return SRSRAN_ERROR;
@@ -856,6 +889,8 @@ void srsran_softbuffer_rx_free(srsran_softbuffer_rx_t* q)
   }
   SbGpu* g = (SbGpu*)q->gpu;
   if (g) {
+    // the owning device must be idle before the arena slot can be handed out again
+    DevScope ds(g->dev);
     hipDeviceSynchronize();
     sb_arena_free(g->d_buf, g->buf_bytes, g->buf_dev);
     hipFree(g->d_data);
@@ -866,6 +901,21 @@ void srsran_softbuffer_rx_free(srsran_softbuffer_rx_t* q)
   free(q->data);
   free(q->cb_crc);
   memset(q, 0, sizeof(*q));
+}
+
+int srsran_softbuffer_rx_gpu_arena(int enable, size_t bytes)
+{
+  std::lock_guard<std::mutex> lk(g_arena_mu);
+  g_arena_on = enable != 0;
+  if (bytes) {
+    g_arena_bytes = bytes;
+  }
+  return SRSRAN_SUCCESS;
+}
+
+const void* srsran_softbuffer_rx_gpu_ptr(const srsran_softbuffer_rx_t* q)
+{
+  return q && q->gpu ? ((const SbGpu*)q->gpu)->d_buf : nullptr;
 }
 
 // ---------------- sch.c:140-230 ----------------

@@ -35,7 +35,6 @@
 //     (sch.c:426-456) on the bitmap.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
-#include <stdlib.h>
 
 #include "crc24_dev.h"
 #include "stage_timing.h"
@@ -590,8 +589,8 @@ __device__ __forceinline__ void tdec16_body(const TdecArgs& a, int bid)
   const int M    = (L + W - 1) / W;
   const Geo16 g  = geo16(K, Ls, M);
   const int cb   = bid * CPWG + cbw;
-  const bool live = cb < (int)a.ncb;
-  const int cbl  = live ? cb : (int)a.ncb - 1;
+  const int cbl  = cb < (int)a.ncb ? cb : (int)a.ncb - 1;
+  const bool live = cb < (int)a.ncb && (!ES || a.cbs[cbl].slot != TDEC_PAD_SLOT);
   bool done      = ES && (!live || *a.cbs[cbl].skip);
 
   uint32_t* base = smem + cbw * g.cb_dw;
@@ -607,7 +606,8 @@ __device__ __forceinline__ void tdec16_body(const TdecArgs& a, int bid)
   c.KP      = K + 32;  // SB stream stride (rm_turbo.c:260-273)
   c.magicLs = a.magicLs;
   // the workgroup's two blocks read through one uniform base: the lower of their inputs (plain
-  // launches: in_stride apart; DL-SCH: soft buffers the host checked to lie < 2 GB apart)
+  // launches: in_stride apart; DL-SCH: the host pads the descriptor list so that the two blocks of
+  // every workgroup lie within TDEC_PAIR_SPAN, tdec_pair_cbs)
   const int cb0 = bid * CPWG;
   size_t    in_lane, in_base, in_hi;
   if (ES) {
@@ -757,17 +757,17 @@ __global__ __launch_bounds__(128, 2) void tdec16_multi_kernel(const TdecArgs* __
 // round (one block per workgroup, 4 per CU) with more SIMDs busy than the lane-pair kernel; at 1024
 // blocks the two tie (K = 6144: 0.388 vs 0.391 ms) and above the quad decoder needs a second round.
 
-// SRSRAN_TDEC16_MIN_CB overrides the threshold (tests force the lane-pair kernel on small batches).
-bool tdec16_pays(uint32_t ncb)
-{
-  const char* e = getenv("SRSRAN_TDEC16_MIN_CB");
-  return ncb >= (e ? (uint32_t)strtoul(e, nullptr, 10) : 1024u);
-}
+// srsran_tdec_gpu_set_pair_threshold() moves the threshold (tests force the lane-pair kernel on small
+// batches with 0).
+static uint32_t g_pair_min_cb = 1024u;
+void     tdec16_set_min_cb(uint32_t n) { __atomic_store_n(&g_pair_min_cb, n, __ATOMIC_RELAXED); }
+uint32_t tdec16_min_cb() { return __atomic_load_n(&g_pair_min_cb, __ATOMIC_RELAXED); }
+bool     tdec16_pays(uint32_t ncb) { return ncb >= tdec16_min_cb(); }
 
 bool tdec16_eligible(int nsb, const TdecArgs& a)
 {
-  return nsb == 16 && a.layout_sb && a.n_start == 0 && a.state == nullptr && a.dbg == 0 && a.L >= (uint32_t)OVL &&
-         (a.cbs == nullptr || a.in_near) && tdec16_pays(a.ncb);
+  return nsb == 16 && a.layout_sb && a.n_start == 0 && a.state == nullptr && a.L >= (uint32_t)OVL &&
+         tdec16_pays(a.ncb);
 }
 
 size_t tdec16_lds_bytes(const TdecArgs& a)
@@ -783,6 +783,7 @@ hipError_t tdec16_launch(const TdecArgs& a, hipStream_t stream)
   StageScope timing_scope(ST_TDEC, stream);
   const int    grid = (a.ncb + CPWG - 1) / CPWG;
   const size_t lds  = tdec16_lds_bytes(a);
+  tdec_set_last_kernel(a.cbs ? "tdec16_kernel<true>" : "tdec16_kernel<false>");
   if (a.cbs) {
     hipLaunchKernelGGL((tdec16_kernel<true>), dim3(grid), dim3(128), lds, stream, a);
   } else {
@@ -798,6 +799,7 @@ hipError_t tdec16_multi_launch(const TdecArgs* d_groups, const uint32_t* d_first
   if (ngroups == 0 || nblocks == 0) {
     return hipSuccess;
   }
+  tdec_set_last_kernel("tdec16_multi_kernel");
   hipLaunchKernelGGL(tdec16_multi_kernel, dim3(nblocks), dim3(128), lds, stream, d_groups, d_first, ngroups);
   return hipGetLastError();
 }

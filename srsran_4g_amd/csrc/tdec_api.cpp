@@ -219,8 +219,6 @@ int enqueue(const Config* c, const short* d_in, uint32_t in_stride, int layout_s
   a.tfwd_nat  = c->d_tfwd_nat;
   a.trev_nat  = c->d_trev_nat;
   a.state     = d_state;
-  static const uint32_t dbg = getenv("SRSRAN_TDEC_ABLATE") ? (uint32_t)atoi(getenv("SRSRAN_TDEC_ABLATE")) : 0;
-  a.dbg       = dbg;
   hipError_t e = tdec_launch(c->nsb, a, stream);
   if (e != hipSuccess) {
     fprintf(stderr, "[srsran_tdec] launch failed: %s\n", hipGetErrorString(e));
@@ -301,7 +299,6 @@ int tdec_sch_enqueue(uint32_t      K,
                      uint8_t*      d_noi,
                      uint8_t*      d_crc_ok,
                      int           n_end,
-                     bool          in_near,
                      hipStream_t   stream)
 {
   if (ncb == 0) {
@@ -332,7 +329,6 @@ int tdec_sch_enqueue(uint32_t      K,
   a.xpow_a     = xp->d[0];
   a.xpow_b     = xp->d[1];
   a.min_iters  = 2;  // SRSRAN_PDSCH_MIN_TDEC_ITERS (sch.c:35)
-  a.in_near    = in_near ? 1 : 0;
   hipError_t e = tdec_launch(c->nsb, a, stream);
   if (e != hipSuccess) {
     fprintf(stderr, "[srsran_sch] turbo launch failed: %s\n", hipGetErrorString(e));
@@ -387,6 +383,12 @@ const char* srsran_tdec_gpu_kernel_name(uint32_t long_cb)
       return "tdec_kernel<1>";
   }
 }
+
+const char* srsran_tdec_gpu_last_kernel(void) { return tdec_last_kernel(); }
+
+void srsran_tdec_gpu_set_pair_threshold(uint32_t nof_cb) { tdec16_set_min_cb(nof_cb); }
+
+uint32_t srsran_tdec_gpu_get_pair_threshold(void) { return tdec16_min_cb(); }
 
 const char* srsran_tdec_gpu_kernel_name_batch(uint32_t long_cb, uint32_t nof_cb)
 {
@@ -760,7 +762,6 @@ int srsran_tdec_gpu_run_multi(uint32_t              nof_groups,
     uint32_t* hf    = reinterpret_cast<uint32_t*>(m.h_stage + abyte);
     uint32_t  nblk  = 0;
     size_t    lds   = 0;
-    static const uint32_t dbg = getenv("SRSRAN_TDEC_ABLATE") ? (uint32_t)atoi(getenv("SRSRAN_TDEC_ABLATE")) : 0;
     for (size_t k = 0; k < n; k++) {
       const uint32_t g = gs[k];
       const Config*  c = cfg[g];
@@ -777,7 +778,6 @@ int srsran_tdec_gpu_run_multi(uint32_t              nof_groups,
       a.tfwd_nat       = c->d_tfwd_nat;
       a.trev_nat       = c->d_trev_nat;
       a.state          = nullptr;
-      a.dbg            = dbg;
       ha[k]            = a;
       hf[k]            = nblk;
       nblk += (nof_cb[g] + cpw - 1) / cpw;
@@ -790,7 +790,7 @@ int srsran_tdec_gpu_run_multi(uint32_t              nof_groups,
     m.used = true;
     const TdecArgs* dg = reinterpret_cast<const TdecArgs*>(m.d_stage);
     const uint32_t* df = reinterpret_cast<const uint32_t*>(m.d_stage + abyte);
-    if ((pair && dbg == 0 ? tdec16_multi_launch(dg, df, (int)n, nblk, lds, st)
+    if ((pair ? tdec16_multi_launch(dg, df, (int)n, nblk, lds, st)
                           : tdec_multi_launch(cls_nsb[ci], dg, df, (int)n, nblk, lds, st)) != hipSuccess) {
       ret = SRSRAN_ERROR;
     }

@@ -17,6 +17,12 @@ struct TdecCb {
   uint32_t       slot;  // index into out / noi_out / crc_ok
   uint32_t       crc_a; // 1 -> CRC24A over tbs+24 (single-CB TB), 0 -> CRC24B (sch.c:440-446)
 };
+// slot of a padding descriptor: decodes nothing, writes nothing.  The host inserts one where two
+// neighbouring blocks of a launch lie too far apart to share the lane-pair decoder's workgroup
+// (one buffer resource over both), so the pair starts with the next block instead.
+static constexpr uint32_t TDEC_PAD_SLOT = 0xffffffffu;
+// the two blocks of a lane-pair workgroup must lie within this many bytes of each other
+static constexpr uint64_t TDEC_PAIR_SPAN = ((uint64_t)1 << 31) - ((uint64_t)1 << 16);
 
 struct TdecArgs {
   const short*    in;        // ncb code blocks, in_stride int16 apart (device)
@@ -38,7 +44,6 @@ struct TdecArgs {
   uint32_t        M;         // beta checkpoints per sub-block
   uint32_t        magicL;    // ceil(2^32 / L)
   uint32_t        magicLs;   // ceil(2^32 / Ls)
-  uint32_t        dbg;       // profiling ablation only (SRSRAN_TDEC_ABLATE): bit0 skip prepare, bit1 skip MAP
   // ---- DL-SCH mode (decode_tb_cb, sch.c:391-456): enabled when cbs != nullptr ----
   const struct TdecCb* cbs;  // per launch index: input pointer, skip flag, output slot, CRC type
   uint32_t        out_stride; // bytes between output slots
@@ -47,7 +52,6 @@ struct TdecArgs {
   const uint32_t* xpow_a;    // x^(8m) mod CRC24A, m = 0..768 (device)
   const uint32_t* xpow_b;    // x^(8m) mod CRC24B
   int             min_iters; // early stop needs at least this many half-iterations (sch.c:35)
-  uint32_t        in_near;   // every cbs[].in lies within 2 GB of the others (lane-pair kernel)
 };
 
 static constexpr uint32_t LTE_CRC24A = 0x1864CFB;  // phy_common.h:72
@@ -64,6 +68,8 @@ int        tdec_cpw(int nsb);  // code blocks per workgroup
 // (every plain / DL-SCH launch of K >= 816 without state save/restore)
 bool       tdec16_eligible(int nsb, const TdecArgs& a);
 bool       tdec16_pays(uint32_t ncb);  // enough blocks in one launch for the lane-pair kernel
+void       tdec16_set_min_cb(uint32_t n);
+uint32_t   tdec16_min_cb();
 hipError_t tdec16_launch(const TdecArgs& a, hipStream_t stream);
 hipError_t tdec16_multi_launch(const TdecArgs* d_groups, const uint32_t* d_first, int ngroups, uint32_t nblocks,
                                size_t lds, hipStream_t stream);
@@ -84,8 +90,14 @@ int tdec_sch_enqueue(uint32_t      K,
                      uint8_t*      d_noi,
                      uint8_t*      d_crc_ok,
                      int           n_end,
-                     bool          in_near,
                      hipStream_t   stream);
+// Appends the blocks [first, last) of `src` to `dst` so that every two consecutive entries counted
+// from `dst_group_start` (a lane-pair workgroup) lie within TDEC_PAIR_SPAN: a padding entry is
+// inserted before a block that is too far from its partner.  Returns the padding entries added.
+uint32_t tdec_pair_cbs(const TdecCb* src, uint32_t n, size_t dst_group_start, void* dst_vec);
+// name of the last turbo-decoder kernel this thread launched ("" before the first)
+const char* tdec_last_kernel();
+void        tdec_set_last_kernel(const char* name);
 int tdec_cb_index(uint32_t K);
 
 }  // namespace srsran_amd

@@ -23,6 +23,7 @@
 //   * everything runs inside one launch for all half-iterations; HBM traffic is the
 //     input LLRs once per half-iteration read + K/8 output bytes.
 #include <hip/hip_runtime.h>
+#include <vector>
 #include <stdint.h>
 
 #include "crc24_dev.h"
@@ -475,10 +476,10 @@ __device__ __forceinline__ void tdec_body(const TdecArgs& a, int bid)
   const int XYW  = a.xyw;
   const int M    = a.M;
   const int cb   = bid * Gm::CPW + cw;  // launch index
-  const bool live = cb < (int)a.ncb;
-  const int cbl  = live ? cb : (int)a.ncb - 1;
+  const int cbl  = cb < (int)a.ncb ? cb : (int)a.ncb - 1;
+  const bool live = cb < (int)a.ncb && (!ES || a.cbs[cbl].slot != TDEC_PAD_SLOT);
   // DL-SCH mode: blocks whose CRC already passed are not decoded; padding blocks
-  // never hold back the workgroup's early exit.  The block descriptor a.cbs[cbl] is
+  // (past ncb, or TDEC_PAD_SLOT entries) never hold back the workgroup's early exit.  The block descriptor a.cbs[cbl] is
   // re-read where needed instead of being kept live across the decode loop.
   bool done = ES && (!live || *a.cbs[cbl].skip);
 
@@ -636,9 +637,7 @@ __device__ __forceinline__ void tdec_body(const TdecArgs& a, int bid)
     // Each thread owns chunks of 4 consecutive positions in visit order (SB order
     // for window decoders on SB input, natural order otherwise); all its global
     // loads are issued before any of them is consumed.
-    if (h > a.n_start && (a.dbg & 1)) {
-      // profiling ablation: keep the previous branch inputs
-    } else if ((h & 1) == 0) {
+    if ((h & 1) == 0) {
       if (h == 0) {
         for_chunks(h, [&](int p, short sx, short p0, short, int) { xyc[pslot(p)] = pack2(sx, p0); });
       } else {
@@ -677,9 +676,7 @@ __device__ __forceinline__ void tdec_body(const TdecArgs& a, int bid)
 
     // -------- constituent MAP decode (wave 0: alpha side, wave 1: beta side) --------
     const bool dec1 = (h & 1) == 0;
-    if (!(a.dbg & 2)) {
-      map_decode<NSB>(sm, base, wave, lane, j, s, K, L, Nb, La, M, dec1 ? st : x2t, dec1 ? p0t : p1t);
-    }
+    map_decode<NSB>(sm, base, wave, lane, j, s, K, L, Nb, La, M, dec1 ? st : x2t, dec1 ? p0t : p1t);
     __syncthreads();
 
     // -------- DL-SCH early stop: CRC of the hard decision (sch.c:426-456) --------
@@ -783,6 +780,7 @@ hipError_t tdec_multi_launch(int nsb, const TdecArgs* d_groups, const uint32_t* 
   if (ngroups == 0 || nblocks == 0) {
     return hipSuccess;
   }
+  tdec_set_last_kernel(nsb == 16 ? "tdec_multi_kernel<16>" : nsb == 8 ? "tdec_multi_kernel<8>" : "tdec_multi_kernel<1>");
   switch (nsb) {
     case 16:
       hipLaunchKernelGGL(tdec_multi_kernel<16>, dim3(nblocks), dim3(128), lds, stream, d_groups, d_first, ngroups);
@@ -808,6 +806,7 @@ static hipError_t launch(const TdecArgs& a, hipStream_t stream)
   const int    cpw  = Geo<NSB>::CPW;
   const int    grid = (a.ncb + cpw - 1) / cpw;
   const size_t lds  = tdec_lds_bytes(NSB, a.xyw, a.M);
+  tdec_set_last_kernel(NSB == 16 ? "tdec_kernel<16>" : NSB == 8 ? "tdec_kernel<8>" : "tdec_kernel<1>");
   if (a.cbs) {
     hipLaunchKernelGGL((tdec_kernel<NSB, true>), dim3(grid), dim3(128), lds, stream, a);
   } else {
@@ -840,6 +839,30 @@ size_t tdec_lds_bytes(int nsb, int xyw, int M)
 {
   const int cpw = 64 / (4 * nsb);
   return (size_t)cpw * xyw * 4 + (((size_t)cpw * xyw + 1) / 2) * 4 + (size_t)M * 64 * 4 + (size_t)cpw * 2 * 4;
+}
+
+static thread_local const char* t_last_kernel = "";
+const char* tdec_last_kernel() { return t_last_kernel; }
+void        tdec_set_last_kernel(const char* name) { t_last_kernel = name; }
+
+uint32_t tdec_pair_cbs(const TdecCb* src, uint32_t n, size_t dst_group_start, void* dst_vec)
+{
+  std::vector<TdecCb>& dst = *static_cast<std::vector<TdecCb>*>(dst_vec);
+  uint32_t             pads = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    const size_t pos = dst.size() - dst_group_start;
+    if (pos & 1) {  // second block of a workgroup: must share the first one's buffer resource
+      const uintptr_t p0 = (uintptr_t)dst.back().in, p1 = (uintptr_t)src[i].in;
+      if ((p0 > p1 ? p0 - p1 : p1 - p0) >= TDEC_PAIR_SPAN) {
+        TdecCb pad = dst.back();
+        pad.slot   = TDEC_PAD_SLOT;
+        dst.push_back(pad);
+        pads++;
+      }
+    }
+    dst.push_back(src[i]);
+  }
+  return pads;
 }
 
 void crc24_xpow_table(uint32_t poly, uint32_t* out, int nm)

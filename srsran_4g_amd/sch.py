@@ -210,6 +210,8 @@ def lib():
         "srsran_softbuffer_rx_reset_cb_crc": ([SB, u32], None),
         "srsran_softbuffer_rx_free": ([SB], None),
         "srsran_softbuffer_rx_sync": ([SB], ctypes.c_int),
+        "srsran_softbuffer_rx_gpu_arena": ([ctypes.c_int, ctypes.c_size_t], ctypes.c_int),
+        "srsran_softbuffer_rx_gpu_ptr": ([SB], ctypes.c_void_p),
         "srsran_sch_init": ([SCH], ctypes.c_int),
         "srsran_sch_free": ([SCH], None),
         "srsran_sch_set_max_noi": ([SCH, u32], None),
@@ -269,6 +271,11 @@ def rm_turbo_rx_lut(e, softbuf, cb_idx, rv, enable_input_tdec=True):
     return ret, out
 
 
+def softbuffer_arena(enable, nbytes=0):
+    """srsran_softbuffer_rx_gpu_arena: arena on / off for soft buffers initialised from now on"""
+    return lib().srsran_softbuffer_rx_gpu_arena(1 if enable else 0, nbytes)
+
+
 class SoftbufferRx:
     """srsran_softbuffer_rx_t owner (device arena)."""
 
@@ -284,6 +291,11 @@ class SoftbufferRx:
     @property
     def max_cb(self):
         return self.s.max_cb
+
+    @property
+    def device_ptr(self):
+        """device address of the first code block's soft buffer (srsran_softbuffer_rx_gpu_ptr)"""
+        return lib().srsran_softbuffer_rx_gpu_ptr(ctypes.byref(self.s)) or 0
 
     def cb_crc(self, n=None):
         n = self.s.max_cb if n is None else n

@@ -88,6 +88,9 @@ def load_library():
         "srsran_tdec_gpu_available": ([], ctypes.c_int),
         "srsran_tdec_gpu_kernel_name": ([u32], ctypes.c_char_p),
         "srsran_tdec_gpu_kernel_name_batch": ([u32, u32], ctypes.c_char_p),
+        "srsran_tdec_gpu_last_kernel": ([], ctypes.c_char_p),
+        "srsran_tdec_gpu_set_pair_threshold": ([u32], None),
+        "srsran_tdec_gpu_get_pair_threshold": ([], u32),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)
@@ -95,6 +98,28 @@ def load_library():
         f.restype = res
     _lib = lib
     return lib
+
+
+def last_kernel():
+    """Name of the last turbo-decoder kernel this thread launched (srsran_tdec_gpu_last_kernel)."""
+    return load_library().srsran_tdec_gpu_last_kernel().decode()
+
+
+class pair_threshold:
+    """Context manager: blocks per launch from which the lane-pair decoder runs
+    (srsran_tdec_gpu_set_pair_threshold), restored on exit."""
+
+    def __init__(self, nof_cb):
+        self.n = nof_cb
+
+    def __enter__(self):
+        lib = load_library()
+        self.old = lib.srsran_tdec_gpu_get_pair_threshold()
+        lib.srsran_tdec_gpu_set_pair_threshold(self.n)
+        return self
+
+    def __exit__(self, *exc):
+        load_library().srsran_tdec_gpu_set_pair_threshold(self.old)
 
 
 def nof_subblocks(K):

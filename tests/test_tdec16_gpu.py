@@ -1,9 +1,7 @@
 """The lane-pair turbo decoder of the 16-sub-block class (tdec16_kernel.hip) forced onto small batches
-(SRSRAN_TDEC16_MIN_CB=0; the library runs it by itself from 2048 blocks a launch): every K >= 816 of
+(srsran_tdec_gpu_set_pair_threshold(0); the library runs it by itself from 1024 blocks a launch): every K >= 816 of
 the bit-exact suites again, plain batches with odd block counts (the second block of a workgroup
 absent), the multi-size fused launch, and DL-SCH transport blocks with CRC early stop over HARQ."""
-import os
-
 import numpy as np
 import pytest
 
@@ -14,13 +12,11 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(scope="module", autouse=True)
 def force_pair_kernel():
-    old = os.environ.get("SRSRAN_TDEC16_MIN_CB")
-    os.environ["SRSRAN_TDEC16_MIN_CB"] = "0"
-    yield
-    if old is None:
-        del os.environ["SRSRAN_TDEC16_MIN_CB"]
-    else:
-        os.environ["SRSRAN_TDEC16_MIN_CB"] = old
+    from srsran_4g_amd import tdec
+    if not tdec.gpu_available():
+        pytest.skip("no HIP device")
+    with tdec.pair_threshold(0):
+        yield
 
 
 @pytest.fixture(scope="module")

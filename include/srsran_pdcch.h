@@ -15,7 +15,7 @@
  * and one wave per PDCCH candidate for rate de-matching, quantisation, the 16-bit tail-biting
  * Viterbi decoder (64 lanes = 64 trellis states), CRC16 / RNTI and the re-encoding correlation.
  * Bit-exact with the reference's AVX2 build for the LLRs, decoded payloads and CRC remainders.
- * Provided: FDD, normal CP, 1, 2 or 4 ports, PHICH normal duration; DCI formats 0 (size), 1, 1A, 1C
+ * Provided: FDD, normal CP, 1, 2 or 4 ports, PHICH normal duration; DCI formats 0, 1, 1A, 1C
  * (size), 2, 2A; resource allocation types 0, 1 and 2 (localized).  Others return SRSRAN_ERROR.
  */
 #ifndef SRSRAN_AMD_PDCCH_H
@@ -144,10 +144,43 @@ typedef struct {
   bool            sram_id;
 } srsran_dci_dl_t;
 
+/* Unpacked DCI format 0 (dci.h:130-178, without the SRSRAN_DCI_HEXDEBUG members) */
+typedef struct {
+  uint16_t              rnti;
+  srsran_dci_format_t   format;
+  srsran_dci_location_t location;
+  uint32_t              ue_cc_idx;
+  srsran_ra_type2_t     type2_alloc;
+  enum {
+    SRSRAN_RA_PUSCH_HOP_DISABLED  = -1,
+    SRSRAN_RA_PUSCH_HOP_QUART     = 0,
+    SRSRAN_RA_PUSCH_HOP_QUART_NEG = 1,
+    SRSRAN_RA_PUSCH_HOP_HALF      = 2,
+    SRSRAN_RA_PUSCH_HOP_TYPE2     = 3
+  } freq_hop_fl;
+  srsran_dci_tb_t  tb;
+  uint32_t         n_dmrs;
+  bool             cqi_request;
+  uint32_t         dai;
+  uint32_t         ul_idx;
+  bool             is_tdd;
+  uint8_t          tpc_pusch;
+  uint32_t         cif;
+  bool             cif_present;
+  uint8_t          multiple_csi_request;
+  bool             multiple_csi_request_present;
+  bool             srs_request;
+  bool             srs_request_present;
+  srsran_ra_type_t ra_type;
+  bool             ra_type_present;
+} srsran_dci_ul_t;
+
 uint32_t srsran_dci_format_sizeof(const srsran_cell_t* cell, srsran_dl_sf_cfg_t* sf, srsran_dci_cfg_t* cfg,
                                   srsran_dci_format_t format);                                 /* dci.c:359-413 */
 int      srsran_dci_msg_unpack_pdsch(srsran_cell_t* cell, srsran_dl_sf_cfg_t* sf, srsran_dci_cfg_t* cfg,
                                      srsran_dci_msg_t* msg, srsran_dci_dl_t* dci);             /* dci.c:1288-1340 */
+int      srsran_dci_msg_unpack_pusch(srsran_cell_t* cell, srsran_dl_sf_cfg_t* sf, srsran_dci_cfg_t* cfg,
+                                     srsran_dci_msg_t* msg, srsran_dci_ul_t* dci);             /* dci.c:1369-1395, 492-566 */
 bool     srsran_dci_location_isvalid(srsran_dci_location_t* c);                                /* dci.c:1442-1449 */
 int      srsran_dci_location_set(srsran_dci_location_t* c, uint32_t L, uint32_t nCCE);          /* dci.c:1425-1440 */
 void     srsran_dci_cfg_set_common_ss(srsran_dci_cfg_t* cfg);                                  /* dci.c:1420-1423 */
@@ -256,6 +289,18 @@ int srsran_ue_dl_find_dl_dci(srsran_ue_dl_t* q, srsran_dl_sf_cfg_t* sf, srsran_u
                              srsran_dci_dl_t dci_dl[SRSRAN_MAX_DCI_MSG]);
 int srsran_ue_dl_dci_to_pdsch_grant(srsran_ue_dl_t* q, srsran_dl_sf_cfg_t* sf, srsran_ue_dl_cfg_t* cfg,
                                     srsran_dci_dl_t* dci, srsran_pdsch_grant_t* grant);
+/* The format 0 DCIs the last srsran_ue_dl_find_dl_dci call found for its C-RNTI (ue_dl.c:573-611:
+ * no search of its own; the pending list is emptied), unpacked into dci_ul.  Returns their number. */
+int srsran_ue_dl_find_ul_dci(srsran_ue_dl_t* q, srsran_dl_sf_cfg_t* sf, srsran_ue_dl_cfg_t* dl_cfg, uint16_t rnti,
+                             srsran_dci_ul_t dci_ul[SRSRAN_MAX_DCI_MSG]);
+/* PHICH m_i of the REG tables the PDCCH search uses (ue_dl.c:263-273, 296-313): auto = the FDD
+ * value 1; manual = m_i of mi_idx (0, 1 or 2; srsUE's blind m_i search on unconfigured TDD cells). */
+void srsran_ue_dl_set_mi_manual(srsran_ue_dl_t* q, uint32_t mi_idx);
+void srsran_ue_dl_set_mi_auto(srsran_ue_dl_t* q);
+/* MBSFN area of the PMCH (ue_dl.c:277-294): recorded in current_mbsfn_area_id; the PMCH itself is not
+ * provided, so no MBSFN reference signal or scrambling is generated. */
+int  srsran_ue_dl_set_mbsfn_area_id(srsran_ue_dl_t* q, uint16_t mbsfn_area_id);
+void srsran_ue_dl_set_non_mbsfn_region(srsran_ue_dl_t* q, uint8_t non_mbsfn_region_length);
 
 #ifdef __cplusplus
 }

@@ -35,6 +35,7 @@ class Ref:
     def __init__(self):
         L = ctypes.CDLL(REF_SO, mode=os.RTLD_LAZY)
         L.ref_regs_tables.argtypes = [u32, u32, u32, ctypes.c_int, ctypes.c_int, u32p, u32p, u32, u32p]
+        L.ref_regs_tables_mi.argtypes = [u32, u32, u32, ctypes.c_int, ctypes.c_int, u32, u32p, u32p, u32, u32p]
         L.ref_ctrl_tx.argtypes = [u32, u32, u32, ctypes.c_int, ctypes.c_int, u32, u32, u32, u8p, u32p, u32p, u32p,
                                   u16p, f32p]
         L.ref_ctrl_rx.argtypes = [u32, u32, u32, ctypes.c_int, ctypes.c_int, u32, u32, f32p, f32p, ctypes.c_float,
@@ -45,12 +46,14 @@ class Ref:
         L.ref_rm_conv_rx.argtypes = [f32p, u32, f32p, u32]
         self.L = L
 
-    def regs_tables(self, nof_prb, nof_ports, cell_id, phich_len=0, phich_res=2):
+    def regs_tables(self, nof_prb, nof_ports, cell_id, phich_len=0, phich_res=2, phich_mi=1):
+        """regs.c tables of srsran_regs_init_opts(cell, phich_mi) (regs.c:711-783)"""
         maxre = 4 * 12 * nof_prb
         pc = np.zeros(16, np.uint32)
         pd = np.zeros(3 * maxre, np.uint32)
         nre = np.zeros(3, np.uint32)
-        if self.L.ref_regs_tables(nof_prb, nof_ports, cell_id, phich_len, phich_res, pc, pd, maxre, nre) != 16:
+        if self.L.ref_regs_tables_mi(nof_prb, nof_ports, cell_id, phich_len, phich_res, phich_mi, pc, pd, maxre,
+                                     nre) != 16:
             raise RuntimeError("ref_regs_tables failed")
         return pc, [pd[c * maxre:c * maxre + nre[c]].copy() for c in range(3)]
 
@@ -157,6 +160,25 @@ def riv(L_crb, start, nof_prb):
 def dci_pack_1a(nof_prb, size, riv_v, mcs, pid, ndi, rv, tpc=0, localized=True):
     b = [1, 0 if localized else 1] + _bits(riv_v, riv_nbits(nof_prb)) + _bits(mcs, 5) + _bits(pid, 3) + [ndi] + \
         _bits(rv, 2) + _bits(tpc, 2)
+    return np.array(b + [0] * (size - len(b)), np.uint8)
+
+
+def dci_pack_0(nof_prb, size, riv_v, mcs, ndi, tpc=0, n_dmrs=0, cqi=0, hop=None, cif=None, csi=None, srs=None,
+               ra_type=None):
+    """format 0, 36.212 5.3.3.1.1: [CIF] flag 0/1A = 0, hopping flag [+ 1 or 2 hopping bits], RIV,
+    MCS, NDI, TPC, DMRS cyclic shift, CQI (or 2-bit CSI) request, [SRS request], [RA type]"""
+    b = (_bits(cif, 3) if cif is not None else []) + [0]
+    if hop is None:
+        b += [0]
+        nh = 0
+    else:
+        nh = 1 if nof_prb < 50 else 2
+        b += [1] + _bits(hop, nh)
+    b += _bits(riv_v, riv_nbits(nof_prb) - nh) + _bits(mcs, 5) + [ndi] + _bits(tpc, 2) + _bits(n_dmrs, 3)
+    b += _bits(csi, 2) if csi is not None else [cqi]
+    b += [srs] if srs is not None else []
+    b += [ra_type] if ra_type is not None else []
+    assert len(b) <= size
     return np.array(b + [0] * (size - len(b)), np.uint8)
 
 

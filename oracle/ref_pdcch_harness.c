@@ -141,12 +141,12 @@ static srsran_cell_t mkcell(uint32_t nof_prb, uint32_t nof_ports, uint32_t id, i
 
 /* Grid indices (l * 12 * nof_prb + k) of the PCFICH REs (16) and of the PDCCH REs for CFI 1..3
  * in srsran_regs_*_get order; nre[c] = number of PDCCH REs for CFI c + 1. */
-int ref_regs_tables(uint32_t nof_prb, uint32_t nof_ports, uint32_t id, int phich_len, int phich_res,
-                    uint32_t* pcfich, uint32_t* pdcch, uint32_t max_re, uint32_t* nre)
+int ref_regs_tables_mi(uint32_t nof_prb, uint32_t nof_ports, uint32_t id, int phich_len, int phich_res,
+                       uint32_t phich_mi, uint32_t* pcfich, uint32_t* pdcch, uint32_t max_re, uint32_t* nre)
 {
   srsran_cell_t cell = mkcell(nof_prb, nof_ports, id, phich_len, phich_res);
   srsran_regs_t regs;
-  if (srsran_regs_init(&regs, cell)) {
+  if (srsran_regs_init_opts(&regs, cell, phich_mi, false)) {
     return -1;
   }
   const uint32_t n    = 14 * 12 * nof_prb;
@@ -173,6 +173,13 @@ int ref_regs_tables(uint32_t nof_prb, uint32_t nof_ports, uint32_t id, int phich
   free(out);
   srsran_regs_free(&regs);
   return k;
+}
+
+/* srsran_regs_init's tables (PHICH m_i = 1) */
+int ref_regs_tables(uint32_t nof_prb, uint32_t nof_ports, uint32_t id, int phich_len, int phich_res,
+                    uint32_t* pcfich, uint32_t* pdcch, uint32_t max_re, uint32_t* nre)
+{
+  return ref_regs_tables_mi(nof_prb, nof_ports, id, phich_len, phich_res, 1, pcfich, pdcch, max_re, nre);
 }
 
 /* eNB control region: PCFICH with `cfi` and ndci PDCCH messages (payload bits, nof_bits, L (log2),

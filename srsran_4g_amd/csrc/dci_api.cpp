@@ -3,7 +3,8 @@
 // subframe, nothing for the GPU.
 //
 //   DCI sizes      phch/dci.c:93-413 (FDD: 3-bit HARQ process number, no DAI)
-//   DCI unpack     phch/dci.c:641-708 (format 1), :797-897 (1A), :1153-1241 (2 / 2A), :1288-1340
+//   DCI unpack     phch/dci.c:492-566 (format 0), :641-708 (format 1), :797-897 (1A), :1153-1241 (2 / 2A),
+//                  :1288-1340, :1369-1395
 //   RA             phch/ra.c:37-250 (RIV, RBG size P, MCS -> I_TBS / modulation, TBS table)
 //                  phch/ra_dl.c:42-681 (PRB allocation types 0 / 1 / 2, TB sizes, RE count, MIMO)
 // Not provided (SRSRAN_ERROR): TDD, format 1B / 1C / 1D / 2B unpacking, distributed VRBs.
@@ -127,6 +128,87 @@ uint32_t bit_pack(const uint8_t** y, uint32_t n)
   }
   *y += n;
   return v;
+}
+
+// Format 0 (36.212 5.3.3.1.1; dci.c:492-566): after the optional CIF and the 0/1A flag, the fields
+// in transmission order.  Width 0 = field absent in this configuration.
+struct F0Field {
+  enum Id { HOP, HOP_TYPE, RIV, MCS, NDI, TPC, DMRS, CSI, CQI, SRS, RA_TYPE } id;
+  uint32_t width;
+};
+
+int unpack_format0(const srsran_cell_t* cell, const srsran_dci_cfg_t* cfg, srsran_dci_msg_t* msg, srsran_dci_ul_t* dci)
+{
+  const uint8_t* y = msg->payload;
+  if (cfg->cif_enabled) {
+    dci->cif         = bit_pack(&y, 3);
+    dci->cif_present = true;
+  }
+  if (bit_pack(&y, 1) != 0) {
+    return SRSRAN_ERROR;  // the flag says format 1A
+  }
+  msg->format = SRSRAN_DCI_FORMAT0;
+  // hopping flag, then (if set) 1 or 2 hopping bits that the RIV gives up (36.213 Table 8.4-1)
+  const bool     hop      = bit_pack(&y, 1) != 0;
+  const uint32_t n_ul_hop = hop ? (cell->nof_prb < 50 ? 1u : 2u) : 0u;
+  const bool     ue_ss    = !cfg->is_not_ue_ss;
+  const F0Field  fields[] = {
+      {F0Field::HOP_TYPE, n_ul_hop},
+      {F0Field::RIV, riv_nbits(cell->nof_prb) - n_ul_hop},
+      {F0Field::MCS, 5},
+      {F0Field::NDI, 1},
+      {F0Field::TPC, 2},
+      {F0Field::DMRS, 3},
+      {F0Field::CSI, cfg->multiple_csi_request_enabled && ue_ss ? 2u : 0u},
+      {F0Field::CQI, cfg->multiple_csi_request_enabled && ue_ss ? 0u : 1u},
+      {F0Field::SRS, cfg->srs_request_enabled && ue_ss ? 1u : 0u},
+      {F0Field::RA_TYPE, cfg->ra_format_enabled ? 1u : 0u},
+  };
+  dci->freq_hop_fl = srsran_dci_ul_t::SRSRAN_RA_PUSCH_HOP_DISABLED;
+  for (const F0Field& f : fields) {
+    if (f.width == 0) {
+      continue;
+    }
+    const uint32_t v = bit_pack(&y, f.width);
+    switch (f.id) {
+      case F0Field::HOP_TYPE:
+        dci->freq_hop_fl = (decltype(dci->freq_hop_fl))v;
+        break;
+      case F0Field::RIV:
+        dci->type2_alloc.riv = v;
+        break;
+      case F0Field::MCS:
+        dci->tb.mcs_idx = v;
+        break;
+      case F0Field::NDI:
+        dci->tb.ndi = v != 0;
+        break;
+      case F0Field::TPC:
+        dci->tpc_pusch = (uint8_t)v;
+        break;
+      case F0Field::DMRS:
+        dci->n_dmrs = v;
+        break;
+      case F0Field::CSI:
+        dci->multiple_csi_request_present = true;
+        dci->multiple_csi_request         = (uint8_t)v;
+        break;
+      case F0Field::CQI:
+        dci->cqi_request = v != 0;
+        break;
+      case F0Field::SRS:
+        dci->srs_request_present = true;
+        dci->srs_request         = v != 0;
+        break;
+      case F0Field::RA_TYPE:
+        dci->ra_type_present = true;
+        dci->ra_type         = (srsran_ra_type_t)(v != 0);
+        break;
+      default:
+        break;
+    }
+  }
+  return SRSRAN_SUCCESS;
 }
 
 void tb_disable(srsran_dci_tb_t& tb)
@@ -631,6 +713,26 @@ uint32_t srsran_dci_format_sizeof(const srsran_cell_t* cell, srsran_dl_sf_cfg_t*
     default:
       return 0;
   }
+}
+
+int srsran_dci_msg_unpack_pusch(srsran_cell_t* cell, srsran_dl_sf_cfg_t* sf, srsran_dci_cfg_t* cfg,
+                                srsran_dci_msg_t* msg, srsran_dci_ul_t* dci)
+{
+  (void)sf;
+  if (!cell || !msg || !dci) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  memset(dci, 0, sizeof(*dci));
+  dci->rnti     = msg->rnti;
+  dci->location = msg->location;
+  dci->format   = msg->format;
+  srsran_dci_cfg_t zero;
+  memset(&zero, 0, sizeof(zero));
+  if (cell->frame_type != SRSRAN_FDD) {
+    fprintf(stderr, "[srsran_dci] TDD is not provided\n");
+    return SRSRAN_ERROR;
+  }
+  return unpack_format0(cell, cfg ? cfg : &zero, msg, dci);
 }
 
 int srsran_dci_msg_unpack_pdsch(srsran_cell_t* cell, srsran_dl_sf_cfg_t* sf, srsran_dci_cfg_t* cfg,

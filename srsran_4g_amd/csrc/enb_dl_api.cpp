@@ -38,8 +38,25 @@ struct EnbDlGpu {
   std::unordered_map<std::string, std::pair<uint32_t*, uint32_t>> tabs;
 };
 
-const std::pair<uint32_t*, uint32_t>* get_tab(EnbDlGpu* g, const srsran_cell_t& cell, const srsran_pdsch_grant_t& gr,
-                                               uint32_t lstart, uint32_t sf_idx)
+constexpr size_t kTabCache = 512;  // RE tables kept on the device
+
+// Called once before a batch looks up its tables: when the batch could push the cache past its bound,
+// the cache is emptied here (after the device is idle), never in the middle of the batch, so every
+// table a batch has looked up stays allocated until its launches have run.
+void tab_evict(EnbDlGpu* g, uint32_t nof_sf)
+{
+  if (g->tabs.size() + nof_sf > kTabCache) {
+    hipDeviceSynchronize();
+    for (auto& kv : g->tabs) {
+      hipFree(kv.second.first);
+    }
+    g->tabs.clear();
+  }
+}
+
+// (device table, RE count) of a grant, built and cached on first use; {nullptr, 0} on failure
+std::pair<uint32_t*, uint32_t> get_tab(EnbDlGpu* g, const srsran_cell_t& cell, const srsran_pdsch_grant_t& gr,
+                                       uint32_t lstart, uint32_t sf_idx)
 {
   std::string key;
   key.reserve(2 * cell.nof_prb + 8);
@@ -53,23 +70,16 @@ const std::pair<uint32_t*, uint32_t>* get_tab(EnbDlGpu* g, const srsran_cell_t& 
   key.push_back((char)sf_idx);
   auto it = g->tabs.find(key);
   if (it != g->tabs.end()) {
-    return &it->second;
-  }
-  if (g->tabs.size() >= 512) {  // bound the cache; earlier launches may still read the tables
-    hipDeviceSynchronize();
-    for (auto& kv : g->tabs) {
-      hipFree(kv.second.first);
-    }
-    g->tabs.clear();
+    return it->second;
   }
   const std::vector<uint32_t> t = pdsch_re_table(cell, gr, lstart, sf_idx);
   uint32_t*                   d = nullptr;
   if (hipMalloc((void**)&d, std::max<size_t>(t.size(), 1) * sizeof(uint32_t)) != hipSuccess ||
       hipMemcpy(d, t.data(), t.size() * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) {
     hipFree(d);
-    return nullptr;
+    return {nullptr, 0};
   }
-  return &(g->tabs[key] = std::make_pair(d, (uint32_t)t.size()));
+  return g->tabs[key] = std::make_pair(d, (uint32_t)t.size());
 }
 
 bool grow(void** p, size_t* cap, size_t need)
@@ -156,13 +166,14 @@ int srsran_enb_dl_gpu_tx_batch(srsran_enb_dl_gpu_t*          q,
   hipStream_t         st    = (hipStream_t)stream;
   const srsran_cell_t& cell = q->cell;
   const uint32_t      P     = cell.nof_ports, nre_sf = SRSRAN_SF_LEN_RE(cell.nof_prb, cell.cp);
-  std::vector<const std::pair<uint32_t*, uint32_t>*> tables(nof_sf);
+  std::vector<std::pair<uint32_t*, uint32_t>> tables(nof_sf);
   std::vector<PdschTx>               items(nof_sf);
   std::vector<srsran_dlsch_gpu_enc_t> enc;
   std::vector<size_t>                 e_off;
   std::vector<uint32_t>               sfidx(nof_sf);
   size_t                              e_tot = 0;
   uint32_t                            max_nre = 0;
+  tab_evict(g, nof_sf);
   for (uint32_t b = 0; b < nof_sf; b++) {
     const srsran_enb_dl_gpu_sf_t& s   = sfs[b];
     const srsran_pdsch_cfg_t*     cfg = s.cfg;
@@ -187,10 +198,10 @@ int srsran_enb_dl_gpu_tx_batch(srsran_enb_dl_gpu_t*          q,
     sfidx[b]  = s.tti % 10;
     const uint32_t lstart = s.cfi + (cell.nof_prb < 10 ? 1 : 0);  // SRSRAN_NOF_CTRL_SYMBOLS
     tables[b] = get_tab(g, cell, gr, lstart, sfidx[b]);
-    if (!tables[b]) {
+    if (!tables[b].first) {
       return SRSRAN_ERROR;
     }
-    const uint32_t nre = tables[b]->second;
+    const uint32_t nre = tables[b].second;
     max_nre            = std::max(max_nre, nre);
     PdschTx& it        = items[b];
     memset(&it, 0, sizeof(it));
@@ -231,7 +242,7 @@ int srsran_enb_dl_gpu_tx_batch(srsran_enb_dl_gpu_t*          q,
   size_t k = 0;
   for (uint32_t b = 0; b < nof_sf; b++) {
     PdschTx& it = items[b];
-    it.idx      = tables[b]->first;
+    it.idx      = tables[b].first;
     for (uint32_t p = 0; p < P; p++) {
       it.grid[p] = g->d_grid + ((size_t)b * P + p) * nre_sf;
     }

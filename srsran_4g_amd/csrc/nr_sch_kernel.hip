@@ -152,52 +152,8 @@ __global__ __launch_bounds__(256) void nr_rm_kernel(const NrRmCb* __restrict__ c
     }
     return;
   }
-  // four positions a thread (one dword), coalesced; inside a region that neither the filler range, k0
-  // nor the end of the circle splits, ranks run consecutively
-  const bool     fast = E <= L && cols >= 4;
-  const uint32_t nq   = Ncb / 4;
-  uint32_t*      buf4 = reinterpret_cast<uint32_t*>(d.buf);  // soft buffers are 8-byte aligned
-  for (uint32_t q = threadIdx.x; q < nq; q += blockDim.x) {
-    const uint32_t p0 = 4 * q, p3 = p0 + 3;
-    const bool     split =
-        (p0 < d.ini && p3 >= d.ini) || (p0 < d.end && p3 >= d.end) || (p0 < d.k0 && p3 >= d.k0) || !fast;
-    if (split) {
-      for (uint32_t k = 0; k < 4; ++k) {
-        one(p0 + k);
-      }
-      continue;
-    }
-    if (p0 >= d.ini && p0 < d.end) {
-      buf4[q] = 0x7F7F7F7Fu;
-      continue;
-    }
-    const uint32_t r0 = rank_of(p0);
-    if (r0 >= E) {
-      if (d.fresh) {
-        buf4[q] = 0u;
-      }
-      continue;
-    }
-    const uint32_t j0  = div(r0);
-    const uint32_t m0  = r0 - j0 * cols;
-    const uint32_t old = d.fresh ? 0u : buf4[q];
-    int            x[4];
-#pragma unroll
-    for (uint32_t k = 0; k < 4; ++k) {  // cols >= 4: at most one row change in four
-      const bool     wrap = m0 + k >= cols;
-      const uint32_t m = wrap ? m0 + k - cols : m0 + k, j = wrap ? j0 + 1 : j0;
-      x[k] = r0 + k < E ? (int)e[m * d.Qm + j] : 0;
-    }
-    uint32_t out = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < 4; ++k) {
-      const int v = (int8_t)(old >> (8 * k));
-      const int r = r0 + k < E ? min(max(v + x[k], -63), 63) : v;
-      out |= (uint32_t)(uint8_t)r << (8 * k);
-    }
-    buf4[q] = out;
-  }
-  for (uint32_t p = 4 * nq + threadIdx.x; p < Ncb; p += blockDim.x) {
+  // E > L (repetition): every position gathers its contributions in the reference's order (one())
+  for (uint32_t p = threadIdx.x; p < Ncb; p += blockDim.x) {
     one(p);
   }
 }

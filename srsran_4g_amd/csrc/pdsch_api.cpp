@@ -86,8 +86,23 @@ bool grow_stage(PdschGpu* g, size_t need)
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// RE table of (grant, CFI, subframe) on the device, built once (pdsch_map.cpp)
-const Table* get_table(srsran_pdsch_t* q, PdschGpu* g, const srsran_pdsch_grant_t& gr, uint32_t lstart,
+constexpr size_t kTableCache = 512;  // RE tables kept on the device
+
+// Called once before a batch looks up its tables: when the batch could push the cache past its bound
+// the cache is emptied here (device idle first), never while a batch holds table pointers.
+void table_evict(PdschGpu* g, uint32_t nsf)
+{
+  if (g->tables.size() + nsf > kTableCache) {
+    hipDeviceSynchronize();
+    for (auto& kv : g->tables) {
+      hipFree(kv.second.d);
+    }
+    g->tables.clear();
+  }
+}
+
+// RE table of (grant, CFI, subframe) on the device, built once (pdsch_map.cpp); {nullptr, 0} on failure
+Table get_table(srsran_pdsch_t* q, PdschGpu* g, const srsran_pdsch_grant_t& gr, uint32_t lstart,
                        uint32_t sf_idx)
 {
   std::string key;
@@ -102,14 +117,7 @@ const Table* get_table(srsran_pdsch_t* q, PdschGpu* g, const srsran_pdsch_grant_
   key.push_back((char)sf_idx);
   auto it = g->tables.find(key);
   if (it != g->tables.end()) {
-    return &it->second;
-  }
-  if (g->tables.size() >= 512) {  // bound the cache (grants change with every scheduling decision)
-    hipDeviceSynchronize();
-    for (auto& kv : g->tables) {
-      hipFree(kv.second.d);
-    }
-    g->tables.clear();
+    return it->second;
   }
   const std::vector<uint32_t> t = pdsch_re_table(q->cell, gr, lstart, sf_idx);
   Table                       tb;
@@ -117,9 +125,9 @@ const Table* get_table(srsran_pdsch_t* q, PdschGpu* g, const srsran_pdsch_grant_
   if (hipMalloc((void**)&tb.d, std::max<size_t>(t.size(), 1) * sizeof(uint32_t)) != hipSuccess ||
       hipMemcpy(tb.d, t.data(), t.size() * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) {
     hipFree(tb.d);
-    return nullptr;
+    return Table{};
   }
-  return &(g->tables[key] = tb);
+  return g->tables[key] = tb;
 }
 
 // One decoded codeword of the batch
@@ -137,10 +145,11 @@ int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sf
   PdschGpu*      g   = (PdschGpu*)q->gpu;
   const uint32_t nrx = q->nof_rx_antennas, np = q->cell.nof_ports, nre = 12 * q->cell.nof_prb;
   const uint32_t nsf_rows = 2 * SRSRAN_CP_NSYMB(q->cell.cp);  // grid symbols per subframe (14 / 12)
-  std::vector<const Table*> tabs(nsf);
-  std::vector<PredArgs>     pa(nsf);
-  uint32_t                  max_re = 0;
+  std::vector<Table>    tabs(nsf);
+  std::vector<PredArgs> pa(nsf);
+  uint32_t              max_re = 0;
   cws.clear();
+  table_evict(g, nsf);
   for (uint32_t b = 0; b < nsf; b++) {
     const srsran_pdsch_gpu_sf_t& f = sfs[b];
     if (!f.cfg || !f.d_grid || !f.d_ce || f.cfi < 1 || f.cfi > 3) {
@@ -162,11 +171,11 @@ int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sf
     }
     const uint32_t lstart = f.cfi + (q->cell.nof_prb < 10 ? 1 : 0);  // SRSRAN_NOF_CTRL_SYMBOLS
     tabs[b]               = get_table(q, g, gr, lstart, f.tti % 10);
-    if (!tabs[b]) {
+    if (!tabs[b].d) {
       return SRSRAN_ERROR;
     }
-    if (tabs[b]->len != gr.nof_re) {
-      fprintf(stderr, "[srsran_pdsch] Error expecting %u symbols but got %u\n", gr.nof_re, tabs[b]->len);
+    if (tabs[b].len != gr.nof_re) {
+      fprintf(stderr, "[srsran_pdsch] Error expecting %u symbols but got %u\n", gr.nof_re, tabs[b].len);
       return SRSRAN_ERROR;
     }
     max_re = std::max(max_re, gr.nof_re);
@@ -238,7 +247,7 @@ int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sf
   int16_t* d_e   = (int16_t*)(g->d_work + x_sz + c_sz + m_sz);
   for (uint32_t b = 0; b < nsf; b++) {
     PredArgs& a = pa[b];
-    a.idx       = tabs[b]->d;
+    a.idx       = tabs[b].d;
     for (int l = 0; l < 2; l++) {
       a.x[l]   = d_x + ((size_t)b * 2 + l) * max_re;
       a.csi[l] = d_csi + ((size_t)b * 2 + l) * max_re;

@@ -278,7 +278,10 @@ struct SchCtx {
   bool        used = false;
   int16_t*    d_ul = nullptr;    // srsran_ulsch_decode: q then g bits
   size_t      ul_cap = 0;
-  UlDeint*    d_uldesc = nullptr;  // srsran_ulsch_gpu_decode_batch descriptors
+  UlDeint*    d_uldesc = nullptr;  // srsran_ulsch_gpu_decode_batch descriptors (device)
+  UlDeint*    h_uldesc = nullptr;  // their pinned staging
+  hipEvent_t  uldesc_used = nullptr;  // recorded after the de-interleaver launch that reads them
+  bool        uldesc_live = false;
   size_t      uldesc_cap = 0;
   uint8_t*    d_uci = nullptr;     // srsran_ulsch_decode with UCI: descriptors, results, sequence
   size_t      uci_cap = 0;
@@ -975,6 +978,10 @@ void srsran_sch_free(srsran_sch_t* q)
     hipFree(x->d_zero);
     hipFree(x->d_ul);
     hipFree(x->d_uldesc);
+    hipHostFree(x->h_uldesc);
+    if (x->uldesc_used) {
+      hipEventDestroy(x->uldesc_used);
+    }
     hipFree(x->d_uci);
     hipFree(x->d_enc);
     delete x;
@@ -1702,19 +1709,35 @@ int srsran_ulsch_gpu_decode_batch(srsran_sch_t*                q,
     dl[i]               = {t.tbs, t.Qm, t.rv, t.nof_e_bits, t.d_g_bits, t.d_data, t.softbuffer, t.new_data};
   }
   SchCtx* x = (SchCtx*)q->gpu;
+  // the previous call's de-interleaver must have read its descriptors before staging is rewritten
+  if (x->uldesc_live) {
+    hipEventSynchronize(x->uldesc_used);
+  }
+  if (!x->uldesc_used && hipEventCreateWithFlags(&x->uldesc_used, hipEventDisableTiming) != hipSuccess) {
+    return SRSRAN_ERROR;
+  }
   if (nof_tb > x->uldesc_cap) {
     hipFree(x->d_uldesc);
+    hipHostFree(x->h_uldesc);
     x->d_uldesc   = nullptr;
+    x->h_uldesc   = nullptr;
     x->uldesc_cap = 0;
-    if (hipMalloc((void**)&x->d_uldesc, nof_tb * sizeof(UlDeint)) != hipSuccess) {
+    const size_t cap = std::max<size_t>(2 * nof_tb, 64);
+    if (hipMalloc((void**)&x->d_uldesc, cap * sizeof(UlDeint)) != hipSuccess ||
+        hipHostMalloc((void**)&x->h_uldesc, cap * sizeof(UlDeint), hipHostMallocDefault) != hipSuccess) {
       return SRSRAN_ERROR;
     }
-    x->uldesc_cap = nof_tb;
+    x->uldesc_cap = cap;
   }
-  if (nof_tb && (hipMemcpyAsync(x->d_uldesc, desc.data(), nof_tb * sizeof(UlDeint), hipMemcpyHostToDevice,
-                                (hipStream_t)stream) != hipSuccess ||
-                 ul_deint_batch_launch(x->d_uldesc, nof_tb, max_n, (hipStream_t)stream) != hipSuccess)) {
-    return SRSRAN_ERROR;
+  if (nof_tb) {
+    memcpy(x->h_uldesc, desc.data(), nof_tb * sizeof(UlDeint));
+    if (hipMemcpyAsync(x->d_uldesc, x->h_uldesc, nof_tb * sizeof(UlDeint), hipMemcpyHostToDevice,
+                       (hipStream_t)stream) != hipSuccess ||
+        ul_deint_batch_launch(x->d_uldesc, nof_tb, max_n, (hipStream_t)stream) != hipSuccess) {
+      return SRSRAN_ERROR;
+    }
+    hipEventRecord(x->uldesc_used, (hipStream_t)stream);
+    x->uldesc_live = true;
   }
   return srsran_dlsch_gpu_decode_batch(q, nof_tb, dl.data(), d_result, d_avg_noi, stream);
 }

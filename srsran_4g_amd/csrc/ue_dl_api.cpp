@@ -38,7 +38,23 @@ struct UeDlGpu {
   uint32_t              nof_allocated = 0;
   srsran_dci_msg_t      pending_ul[SRSRAN_MAX_DCI_MSG];
   uint32_t              nof_pending_ul = 0;
+  // PHICH m_i of the PDCCH's REG tables (ue_dl.c:263-273): `regs` has m_i = 1 (FDD), regs_mi the
+  // tables of m_i = 0 and 2 for srsran_ue_dl_set_mi_manual
+  srsran_regs_t regs_mi[2]{};
+  bool          mi_auto   = true;
+  uint32_t      mi_manual = 1;
+  uint32_t      mi_set    = 1;  // m_i of the tables the PDCCH object holds
 };
+
+// set_mi_value (ue_dl.c:296-313): the PDCCH works on the REG tables of the selected m_i
+void select_mi(UeDlGpu* g)
+{
+  const uint32_t mi = g->mi_auto ? 1u : g->mi_manual;
+  if (mi != g->mi_set) {
+    srsran_pdcch_set_regs(&g->pdcch, mi == 1 ? &g->regs : &g->regs_mi[mi == 0 ? 0 : 1]);
+    g->mi_set = mi;
+  }
+}
 
 bool grow(srsran_ue_dl_t* q, UeDlGpu* g, uint32_t nsf)
 {
@@ -151,6 +167,8 @@ void srsran_ue_dl_free(srsran_ue_dl_t* q)
       srsran_pdcch_free(&g->pdcch);
     }
     srsran_regs_free(&g->regs);
+    srsran_regs_free(&g->regs_mi[0]);
+    srsran_regs_free(&g->regs_mi[1]);
     delete g;
   }
   for (int j = 0; j < SRSRAN_MAX_PORTS; j++) {
@@ -188,11 +206,17 @@ int srsran_ue_dl_set_cell(srsran_ue_dl_t* q, srsran_cell_t cell)
   g->cap     = 0;  // buffer shapes depend on the cell
   // control channels: 1, 2 or 4 ports, normal CP and PHICH duration (others: PDSCH only, CFI from the caller)
   srsran_regs_free(&g->regs);
+  srsran_regs_free(&g->regs_mi[0]);
+  srsran_regs_free(&g->regs_mi[1]);
   g->ctrl_cell = g->ctrl_init && (cell.nof_ports == 1 || cell.nof_ports == 2 || cell.nof_ports == 4) &&
                  cell.cp == SRSRAN_CP_NORM && cell.phich_length == SRSRAN_PHICH_NORM &&
                  srsran_regs_init(&g->regs, cell) == SRSRAN_SUCCESS &&
+                 srsran_regs_init_opts(&g->regs_mi[0], cell, 0, false) == SRSRAN_SUCCESS &&
+                 srsran_regs_init_opts(&g->regs_mi[1], cell, 2, false) == SRSRAN_SUCCESS &&
                  srsran_pcfich_set_cell(&g->pcfich, &g->regs, cell) == SRSRAN_SUCCESS &&
                  srsran_pdcch_set_cell(&g->pdcch, &g->regs, cell) == SRSRAN_SUCCESS;
+  g->mi_set = 1;
+  g->nof_pending_ul = 0;  // ue_dl.c:189
   hipDeviceSynchronize();
   hipHostFree(g->h_sf);
   hipFree(g->d_sf);
@@ -228,6 +252,7 @@ static int fft_estimate(srsran_ue_dl_t* q, srsran_dl_sf_cfg_t* sf, srsran_ue_dl_
     return sf->cfi >= 1 && sf->cfi <= 3 ? SRSRAN_SUCCESS : SRSRAN_ERROR;  // CFI from the caller
   }
   float corr = 0;
+  select_mi(g);
   if (srsran_pcfich_decode(&g->pcfich, sf, &q->chest_res, q->sf_symbols, &corr) < 0 ||
       srsran_pdcch_extract_llr(&g->pdcch, sf, &q->chest_res, q->sf_symbols)) {
     fprintf(stderr, "[srsran_ue_dl] Error decoding PCFICH / extracting PDCCH LLRs\n");
@@ -519,6 +544,64 @@ int srsran_ue_dl_find_dl_dci(srsran_ue_dl_t*     q,
     }
   }
   return (int)nof_msg;
+}
+
+int srsran_ue_dl_find_ul_dci(srsran_ue_dl_t*     q,
+                             srsran_dl_sf_cfg_t* sf,
+                             srsran_ue_dl_cfg_t* dl_cfg,
+                             uint16_t            rnti,
+                             srsran_dci_ul_t     dci_ul[SRSRAN_MAX_DCI_MSG])
+{
+  if (!q || !q->gpu || !dl_cfg || !dci_ul) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  if (!rnti) {
+    return 0;
+  }
+  // the format 0 messages the last find_dl_dci set aside; the list is consumed
+  UeDlGpu*         g = (UeDlGpu*)q->gpu;
+  const uint32_t   n = std::min<uint32_t>(SRSRAN_MAX_DCI_MSG, g->nof_pending_ul);
+  srsran_dci_msg_t msgs[SRSRAN_MAX_DCI_MSG];
+  memcpy(msgs, g->pending_ul, n * sizeof(srsran_dci_msg_t));
+  g->nof_pending_ul = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    if (srsran_dci_msg_unpack_pusch(&q->cell, sf, &dl_cfg->cfg.dci, &msgs[i], &dci_ul[i])) {
+      fprintf(stderr, "[srsran_ue_dl] Unpacking UL DCI\n");
+      return SRSRAN_ERROR;
+    }
+  }
+  return (int)n;
+}
+
+void srsran_ue_dl_set_mi_auto(srsran_ue_dl_t* q)
+{
+  if (q && q->gpu) {
+    ((UeDlGpu*)q->gpu)->mi_auto = true;
+  }
+}
+
+void srsran_ue_dl_set_mi_manual(srsran_ue_dl_t* q, uint32_t mi_idx)
+{
+  if (q && q->gpu && mi_idx <= 2) {
+    UeDlGpu* g   = (UeDlGpu*)q->gpu;
+    g->mi_auto   = false;
+    g->mi_manual = mi_idx;
+  }
+}
+
+int srsran_ue_dl_set_mbsfn_area_id(srsran_ue_dl_t* q, uint16_t mbsfn_area_id)
+{
+  if (!q) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  q->current_mbsfn_area_id = mbsfn_area_id;
+  return SRSRAN_SUCCESS;
+}
+
+void srsran_ue_dl_set_non_mbsfn_region(srsran_ue_dl_t* q, uint8_t non_mbsfn_region_length)
+{
+  (void)q;
+  (void)non_mbsfn_region_length;  // MBSFN subframes are refused by decode_fft_estimate
 }
 
 int srsran_ue_dl_dci_to_pdsch_grant(srsran_ue_dl_t*       q,

@@ -60,6 +60,21 @@ class srsran_dci_dl_t(ctypes.Structure):
                 ("is_dwpts", ctypes.c_bool), ("sram_id", ctypes.c_bool)]
 
 
+class srsran_ra_type2_t(ctypes.Structure):
+    _fields_ = [("riv", u32), ("n_prb1a", ctypes.c_int), ("n_gap", ctypes.c_int), ("mode", ctypes.c_int)]
+
+
+class srsran_dci_ul_t(ctypes.Structure):
+    """dci.h:130-178 (format 0)"""
+    _fields_ = [("rnti", ctypes.c_uint16), ("format", ctypes.c_int), ("location", srsran_dci_location_t),
+                ("ue_cc_idx", u32), ("type2_alloc", srsran_ra_type2_t), ("freq_hop_fl", ctypes.c_int),
+                ("tb", srsran_dci_tb_t), ("n_dmrs", u32), ("cqi_request", ctypes.c_bool), ("dai", u32),
+                ("ul_idx", u32), ("is_tdd", ctypes.c_bool), ("tpc_pusch", ctypes.c_uint8), ("cif", u32),
+                ("cif_present", ctypes.c_bool), ("multiple_csi_request", ctypes.c_uint8),
+                ("multiple_csi_request_present", ctypes.c_bool), ("srs_request", ctypes.c_bool),
+                ("srs_request_present", ctypes.c_bool), ("ra_type", ctypes.c_int), ("ra_type_present", ctypes.c_bool)]
+
+
 _bound = False
 
 
@@ -77,6 +92,7 @@ def lib():
         P = ctypes.c_void_p
         sig = {
             "srsran_regs_init": ([R, srsran_cell_t], ctypes.c_int),
+            "srsran_regs_init_opts": ([R, srsran_cell_t, u32, ctypes.c_bool], ctypes.c_int),
             "srsran_regs_free": ([R], None),
             "srsran_regs_pdcch_ncce": ([R, u32], ctypes.c_int),
             "srsran_pcfich_init": ([PC, u32], ctypes.c_int),
@@ -106,6 +122,14 @@ def lib():
             "srsran_ue_dl_dci_to_pdsch_grant": ([ctypes.POINTER(srsran_ue_dl_t), SF, ctypes.POINTER(srsran_ue_dl_cfg_t),
                                                  ctypes.POINTER(srsran_dci_dl_t), ctypes.POINTER(srsran_pdsch_grant_t)],
                                                 ctypes.c_int),
+            "srsran_ue_dl_find_ul_dci": ([ctypes.POINTER(srsran_ue_dl_t), SF, ctypes.POINTER(srsran_ue_dl_cfg_t),
+                                          ctypes.c_uint16, ctypes.POINTER(srsran_dci_ul_t)], ctypes.c_int),
+            "srsran_dci_msg_unpack_pusch": ([ctypes.POINTER(srsran_cell_t), SF, DC, M, ctypes.POINTER(srsran_dci_ul_t)],
+                                            ctypes.c_int),
+            "srsran_ue_dl_set_mi_auto": ([ctypes.POINTER(srsran_ue_dl_t)], None),
+            "srsran_ue_dl_set_mi_manual": ([ctypes.POINTER(srsran_ue_dl_t), u32], None),
+            "srsran_ue_dl_set_mbsfn_area_id": ([ctypes.POINTER(srsran_ue_dl_t), ctypes.c_uint16], ctypes.c_int),
+            "srsran_ue_dl_set_non_mbsfn_region": ([ctypes.POINTER(srsran_ue_dl_t), ctypes.c_uint8], None),
         }
         for name, (args, res) in sig.items():
             f = getattr(L, name)
@@ -122,10 +146,22 @@ def cell(nof_prb, nof_ports, cell_id, phich_len=0, phich_res=2):
     return c
 
 
+def unpack_pusch(c, msg, cfg=None):
+    """srsran_dci_msg_unpack_pusch -> (ret, srsran_dci_ul_t)"""
+    d = srsran_dci_ul_t()
+    r = lib().srsran_dci_msg_unpack_pusch(ctypes.byref(c), None, ctypes.byref(cfg) if cfg is not None else None,
+                                          ctypes.byref(msg), ctypes.byref(d))
+    return r, d
+
+
 class Regs:
-    def __init__(self, c):
+    def __init__(self, c, phich_mi=None):
         self.q = srsran_regs_t()
-        if lib().srsran_regs_init(ctypes.byref(self.q), c) != 0:
+        if phich_mi is None:
+            ret = lib().srsran_regs_init(ctypes.byref(self.q), c)
+        else:
+            ret = lib().srsran_regs_init_opts(ctypes.byref(self.q), c, phich_mi, False)
+        if ret != 0:
             raise RuntimeError("srsran_regs_init failed")
 
     def pcfich_re(self):

@@ -442,6 +442,28 @@ class UeDl:
             raise RuntimeError("srsran_ue_dl_find_dl_dci failed")
         return [out[i] for i in range(n)]
 
+    def find_ul_dci(self, tti, cfi, rnti):
+        """srsran_ue_dl_find_ul_dci (the format 0 DCIs the last find_dl_dci found) -> [srsran_dci_ul_t]"""
+        from . import pdcch as PD
+        PD.lib()
+        sf = srsran_dl_sf_cfg_t()
+        sf.tti, sf.cfi = tti, cfi
+        out = (PD.srsran_dci_ul_t * 5)()
+        n = lib().srsran_ue_dl_find_ul_dci(ctypes.byref(self.q), ctypes.byref(sf), ctypes.byref(self.cfg), rnti, out)
+        if n < 0:
+            raise RuntimeError("srsran_ue_dl_find_ul_dci failed")
+        return [out[i] for i in range(n)]
+
+    def set_mi(self, mi_idx=None):
+        """srsran_ue_dl_set_mi_auto (None) / srsran_ue_dl_set_mi_manual(mi_idx)"""
+        if mi_idx is None:
+            lib().srsran_ue_dl_set_mi_auto(ctypes.byref(self.q))
+        else:
+            lib().srsran_ue_dl_set_mi_manual(ctypes.byref(self.q), mi_idx)
+
+    def set_mbsfn_area_id(self, area):
+        return lib().srsran_ue_dl_set_mbsfn_area_id(ctypes.byref(self.q), area)
+
     def dci_to_grant(self, dci, tti, cfi, tm=2):
         from . import pdcch as PD
         PD.lib()

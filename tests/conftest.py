@@ -16,3 +16,20 @@ except Exception:  # pragma: no cover
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a HIP device (MI355X)")
+
+
+import pytest  # noqa: E402
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _reset_symbol_size():
+    """srsran_use_standard_symbol_size is process-global: every module ends with the library default
+    (3/4 sampling rates, phy_common.c:31-35), whatever its tests selected, so no result depends on
+    module order."""
+    yield
+    mod = sys.modules.get("srsran_4g_amd.ue_dl")
+    if mod is not None:
+        try:
+            mod.use_standard_symbol_size(False)
+        except Exception:  # library not loadable: nothing was changed
+            pass

@@ -137,3 +137,57 @@ def test_pdsch_encode_host_grids(gpu, scheme, P, ntb, Qm, tbs, tti, cfi):
     for p in range(P):
         np.testing.assert_allclose(got[p], want[p], rtol=0, atol=2e-6)
     pd.free()
+
+
+def test_re_table_cache_wrap_in_and_across_batches(gpu):
+    """Both RE-table caches (eNB transmitter, UE receiver; 512 tables each) wrap inside one batch and
+    across consecutive batches: 600 subframes a batch, every one with its own (PRB set, subframe, CFI)
+    key, transmitted by srsran_enb_dl_gpu_tx_batch and decoded by srsran_ue_dl_gpu_decode_batch;
+    every TB decodes to its payload (a table freed while a batch still used it would not)"""
+    torch = gpu
+    import itertools
+    from srsran_4g_amd import enb_dl as E
+    from srsran_4g_amd import sch as S
+    from srsran_4g_amd import ue_dl as U
+    nprb, P, Qm, tbs, cell_id, rnti = 6, 1, 2, 40, 23, 0x2222
+    U.use_standard_symbol_size(True)
+    keys = [(m, sf, cfi) for cfi in (1, 2, 3) for sf in (1, 2, 3, 4, 6, 7, 8, 9) for m in range(1, 64)]
+    rng = np.random.default_rng(77)
+    rng.shuffle(keys)
+    cell = U.cell(nprb, P, cell_id)
+    enb = E.EnbDl(cell)
+    ue = U.UeDl(cell, 1)
+    nb = 600
+    sbs = [S.SoftbufferRx(nof_prb=nprb) for _ in range(nb)]
+    N = SY.symbol_sz(nprb)
+    sf_len = 2 * (7 * N + 160 * N // 2048 + 6 * (144 * N // 2048))
+    for batch in (keys[:nb], keys[nb:2 * nb]):
+        tx_sfs, rx_sfs, keep, pls = [], [], [], []
+        for i, (m, sf, cfi) in enumerate(batch):
+            prb = [(m >> n) & 1 for n in range(nprb)]
+            nre = int(SY.pdsch_mask(nprb, P, cell_id, cfi, sf, prb=prb).sum())
+            pl = rng.integers(0, 256, tbs // 8, dtype=np.uint8)
+            cfg = U.pdsch_cfg(nprb, nre, [tbs], [Qm], scheme="port0", rnti=rnti, nof_ports=1, softbuffers=[sbs[i]])
+            for s, n in itertools.product(range(2), range(nprb)):
+                cfg.grant.prb_idx[s][n] = bool(prb[n])
+            cfg.grant.nof_prb = sum(prb)
+            d_pl = torch.from_numpy(pl).cuda()
+            d_out = torch.zeros(tbs // 8 + 64, dtype=torch.uint8, device="cuda")
+            keep += [cfg, d_pl, d_out]
+            pls.append(pl)
+            tx_sfs.append((sf, cfi, cfg, [d_pl.data_ptr()]))
+            rx_sfs.append((sf, cfi, cfg, [d_out.data_ptr()], [1]))
+        d_tx = torch.zeros((nb, P, sf_len, 2), dtype=torch.float32, device="cuda")
+        assert enb.tx_batch(tx_sfs, d_tx.data_ptr()) == 0
+        d_res = torch.full((nb,), 7, dtype=torch.int32, device="cuda")
+        d_avg = torch.zeros(nb, dtype=torch.float32, device="cuda")
+        n = ue.gpu_decode_batch(rx_sfs, d_tx.data_ptr(), d_res.data_ptr(), d_avg.data_ptr())
+        torch.cuda.synchronize()
+        assert n == nb
+        res = d_res.cpu().numpy()
+        bad = [i for i in range(nb) if res[i] != 0 or not np.array_equal(keep[3 * i + 2].cpu().numpy()[: tbs // 8], pls[i])]
+        assert not bad, (len(bad), bad[:10])
+    for sb in sbs:
+        sb.free()
+    ue.free()
+    enb.free()

@@ -239,3 +239,54 @@ def test_find_dl_dci_and_pdsch_four_ports(mods):
         assert ret == 0 and res[0][0] and np.array_equal(res[0][1][:tbs // 8], pl[0])
     finally:
         ue.free()
+
+
+def test_find_ul_dci_format0_and_mi(mods):
+    """srsran_ue_dl_find_ul_dci (ue_dl.c:573-611): a format 0 grant and a format 2A grant for one C-RNTI in
+    the UE search space, from time samples; find_dl_dci returns the 2A and sets the format 0 aside,
+    find_ul_dci unpacks it (fields as packed) and empties the list.  The search on the PHICH m_i = 1 REG
+    tables chosen manually (srsran_ue_dl_set_mi_manual(1)) equals the automatic FDD choice."""
+    import torch  # noqa: F401
+
+    PD, U = mods
+    from synth import synth as S
+
+    cid, tti, cfi, rnti, tbs = 1, 3, 2, 0x1234, 75376
+    rng = np.random.default_rng(43)
+    c = PD.cell(100, 2, cid)
+    dl_bits = P.dci_pack_2a(100, PD.dci_size(c, P.FORMAT2A), (1 << 25) - 1, [(28, 1, 0), (28, 1, 0)], pid=1)
+    riv = P.riv(20, 30, 100)
+    ul_bits = P.dci_pack_0(100, PD.dci_size(c, P.FORMAT0), riv, 17, 1, tpc=2, n_dmrs=5, cqi=1)
+    regs = PD.Regs(c)
+    nof_cce = regs.q.pdcch_nregs[cfi - 1] // 9
+    regs.free()
+    locs = PD.ue_locations(nof_cce, tti % 10, rnti)
+    L3 = [loc for loc in locs if loc[0] == 3][0]
+    L1 = [loc for loc in locs if loc[0] == 1 and not (L3[1] <= loc[1] < L3[1] + 8)][0]
+    ctrl = P.Ref().ctrl_tx(100, 2, cid, tti, cfi, [(dl_bits, L3[0], L3[1], rnti), (ul_bits, L1[0], L1[1], rnti)])
+    pls = [rng.integers(0, 256, tbs // 8, dtype=np.uint8) for _ in range(2)]
+    x, nre = S.pdsch_subframe(100, cid, 2, tti, cfi, rnti, tbs, 6, 0, pls, snr_db=30.0, rng=rng, pcfich=False,
+                              ctrl=[ctrl[0], ctrl[1]])
+    U.use_standard_symbol_size(True)
+    ue = U.UeDl(U.cell(100, 2, cid), 2)
+    try:
+        assert ue.set_mbsfn_area_id(1) == 0  # cc_worker.cc:151
+        for mi in (None, 1):
+            ue.set_mi(mi)
+            assert ue.fft_estimate(x, tti, 0) == 0 and ue.last_cfi == cfi
+            dcis = ue.find_dl_dci(tti, cfi, rnti, tm=2)
+            assert len(dcis) == 1 and dcis[0].format == P.FORMAT2A
+            ul = ue.find_ul_dci(tti, cfi, rnti)
+            assert len(ul) == 1
+            u = ul[0]
+            assert (u.rnti, u.format, u.location.L, u.location.ncce) == (rnti, P.FORMAT0, L1[0], L1[1])
+            assert u.type2_alloc.riv == riv and u.tb.mcs_idx == 17 and u.tb.ndi and u.tpc_pusch == 2
+            assert u.n_dmrs == 5 and u.cqi_request and u.freq_hop_fl == -1
+            assert ue.find_ul_dci(tti, cfi, rnti) == []  # consumed
+        # m_i = 0 tables: a different control region layout; the search runs (finds what it finds)
+        ue.set_mi(0)
+        assert ue.fft_estimate(x, tti, 0) == 0
+        ue.find_dl_dci(tti, cfi, rnti, tm=2)
+        ue.set_mi(None)
+    finally:
+        ue.free()

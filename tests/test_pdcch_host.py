@@ -38,6 +38,22 @@ def test_regs_tables_match_reference(nprb, nports, cid, ng):
 
 
 @needs_ref
+@pytest.mark.parametrize("mi", [0, 2])
+@pytest.mark.parametrize("nprb,nports,cid,ng", CELLS[:8])
+def test_regs_tables_phich_mi_match_reference(nprb, nports, cid, ng, mi):
+    """srsran_regs_init_opts with PHICH m_i 0 / 2 (srsran_ue_dl_set_mi_manual's tables)"""
+    ref = P.Ref()
+    pc, pd = ref.regs_tables(nprb, nports, cid, 0, ng, phich_mi=mi)
+    r = PD.Regs(PD.cell(nprb, nports, cid, 0, ng), phich_mi=mi)
+    try:
+        assert np.array_equal(r.pcfich_re(), pc)
+        for cfi in (1, 2, 3):
+            assert np.array_equal(r.pdcch_re(cfi), pd[cfi - 1]), cfi
+    finally:
+        r.free()
+
+
+@needs_ref
 def test_viterbi_and_rm_conv_restatement_match_reference():
     ref, ora = P.Ref(), P.Ora()
     rng = np.random.default_rng(11)
@@ -133,3 +149,57 @@ def test_dci_unpack_round_trip_and_grant():
     assert r == 0 and d.type0_rbg_bitmask == mask and d.tb[0].mcs_idx == 15
     r, g = PD.dci_to_grant(c50, d, 2, 1, 0)
     assert r == 0 and g.nof_prb == 9 * 3 - 1  # the last RBG holds 2 PRBs
+
+
+@pytest.mark.parametrize("nprb", [6, 15, 25, 50, 75, 100])
+def test_dci_format0_unpack_round_trip(nprb):
+    """srsran_dci_msg_unpack_pusch (dci.c:492-566, 1369-1395) on format 0 payloads packed field by field
+    from 36.212 5.3.3.1.1 (oracle/pdcch.py dci_pack_0): hopping off / on (1 or 2 hopping bits by
+    bandwidth), CIF, 2-bit CSI request, SRS request, RA type; a 1A flag is refused.  (dci.c includes the
+    CMake-generated srsran.h and is not compiled into oracle/_ref: parity unpinned beyond this.)"""
+    c = PD.cell(nprb, 2, 1)
+    rng = np.random.default_rng(nprb)
+    nriv = P.riv_nbits(nprb)
+    for trial in range(40):
+        cfg = PD.srsran_dci_cfg_t()
+        kw = {}
+        if trial % 4 == 1:
+            cfg.cif_enabled = True
+            kw["cif"] = int(rng.integers(0, 8))
+        if trial % 5 == 2:
+            cfg.multiple_csi_request_enabled = True
+            kw["csi"] = int(rng.integers(0, 4))
+        if trial % 6 == 3:
+            cfg.srs_request_enabled = True
+            kw["srs"] = int(rng.integers(0, 2))
+        if trial % 7 == 4:
+            cfg.ra_format_enabled = True
+            kw["ra_type"] = int(rng.integers(0, 2))
+        nh = 1 if nprb < 50 else 2
+        hop = int(rng.integers(0, 1 << nh)) if trial % 2 else None
+        riv = int(rng.integers(0, 1 << (nriv - (nh if hop is not None else 0))))
+        mcs, ndi, tpc, dmrs, cqi = (int(rng.integers(0, 32)), int(rng.integers(0, 2)), int(rng.integers(0, 4)),
+                                    int(rng.integers(0, 8)), int(rng.integers(0, 2)))
+        size = PD.dci_size(c, P.FORMAT0, cfg)
+        bits = P.dci_pack_0(nprb, size, riv, mcs, ndi, tpc, dmrs, cqi, hop=hop, **kw)
+        m = PD.srsran_dci_msg_t()
+        m.payload[:size] = [int(b) for b in bits]
+        m.nof_bits, m.format, m.rnti = size, P.FORMAT0, 0x4601
+        m.location.L, m.location.ncce = 2, 8
+        r, d = PD.unpack_pusch(c, m, cfg)
+        assert r == 0
+        assert (d.rnti, d.format, d.location.L, d.location.ncce) == (0x4601, P.FORMAT0, 2, 8)
+        assert d.type2_alloc.riv == riv and d.tb.mcs_idx == mcs and d.tb.ndi == bool(ndi)
+        assert d.tpc_pusch == tpc and d.n_dmrs == dmrs
+        assert d.freq_hop_fl == (-1 if hop is None else hop)
+        assert (d.cif_present, d.cif) == ((True, kw["cif"]) if "cif" in kw else (False, 0))
+        if "csi" in kw:
+            assert d.multiple_csi_request_present and d.multiple_csi_request == kw["csi"] and not d.cqi_request
+        else:
+            assert not d.multiple_csi_request_present and d.cqi_request == bool(cqi)
+        assert (d.srs_request_present, d.srs_request) == ((True, bool(kw["srs"])) if "srs" in kw else (False, False))
+        assert (d.ra_type_present, d.ra_type) == ((True, kw["ra_type"]) if "ra_type" in kw else (False, 0))
+    # the 0/1A flag set: format 1A, refused
+    m = PD.srsran_dci_msg_t()
+    m.payload[0], m.nof_bits = 1, PD.dci_size(c, P.FORMAT0)
+    assert PD.unpack_pusch(c, m)[0] != 0

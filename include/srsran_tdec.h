@@ -156,6 +156,10 @@ const char* srsran_tdec_gpu_last_kernel(void);
    decoder (default 1024: below it the quad decoder fills the chip better).  Process-wide. */
 void     srsran_tdec_gpu_set_pair_threshold(uint32_t nof_cb);
 uint32_t srsran_tdec_gpu_get_pair_threshold(void);
+/* Blocks per launch from which the 16-sub-block class runs the single-lane decoder (one lane per
+   sub-block, 4 blocks a workgroup: the throughput mapping) instead of the lane pair.  Process-wide. */
+void     srsran_tdec_gpu_set_single_threshold(uint32_t nof_cb);
+uint32_t srsran_tdec_gpu_get_single_threshold(void);
 
 #ifdef __cplusplus
 }

@@ -763,11 +763,17 @@ static uint32_t g_pair_min_cb = 1024u;
 void     tdec16_set_min_cb(uint32_t n) { __atomic_store_n(&g_pair_min_cb, n, __ATOMIC_RELAXED); }
 uint32_t tdec16_min_cb() { return __atomic_load_n(&g_pair_min_cb, __ATOMIC_RELAXED); }
 bool     tdec16_pays(uint32_t ncb) { return ncb >= tdec16_min_cb(); }
+// srsran_tdec_gpu_set_single_threshold(): blocks a launch from which the single-lane decoder
+// (tdec16s_kernel.hip) replaces the lane pair
+static uint32_t g_single_min_cb = 4096u;
+void     tdec16s_set_min_cb(uint32_t n) { __atomic_store_n(&g_single_min_cb, n, __ATOMIC_RELAXED); }
+uint32_t tdec16s_min_cb() { return __atomic_load_n(&g_single_min_cb, __ATOMIC_RELAXED); }
+int      tdec16_choice(uint32_t ncb) { return ncb >= tdec16s_min_cb() ? 2 : tdec16_pays(ncb) ? 1 : 0; }
 
 bool tdec16_eligible(int nsb, const TdecArgs& a)
 {
   return nsb == 16 && a.layout_sb && a.n_start == 0 && a.state == nullptr && a.L >= (uint32_t)OVL &&
-         tdec16_pays(a.ncb);
+         tdec16_choice(a.ncb) > 0;
 }
 
 size_t tdec16_lds_bytes(const TdecArgs& a)

@@ -390,9 +390,19 @@ void srsran_tdec_gpu_set_pair_threshold(uint32_t nof_cb) { tdec16_set_min_cb(nof
 
 uint32_t srsran_tdec_gpu_get_pair_threshold(void) { return tdec16_min_cb(); }
 
+void srsran_tdec_gpu_set_single_threshold(uint32_t nof_cb) { tdec16s_set_min_cb(nof_cb); }
+
+uint32_t srsran_tdec_gpu_get_single_threshold(void) { return tdec16s_min_cb(); }
+
 const char* srsran_tdec_gpu_kernel_name_batch(uint32_t long_cb, uint32_t nof_cb)
 {
-  return auto_nsb(long_cb) == 16 && tdec16_pays(nof_cb) ? "tdec16_kernel" : srsran_tdec_gpu_kernel_name(long_cb);
+  if (auto_nsb(long_cb) == 16) {
+    const int k = tdec16_choice(nof_cb);
+    if (k) {
+      return k == 2 ? "tdec16s_kernel" : "tdec16_kernel";
+    }
+  }
+  return srsran_tdec_gpu_kernel_name(long_cb);
 }
 
 int srsran_tdec_init(srsran_tdec_t* h, uint32_t max_long_cb)
@@ -738,8 +748,8 @@ int srsran_tdec_gpu_run_multi(uint32_t              nof_groups,
     for (uint32_t g : gs) {
       cls_cb += nof_cb[g];
     }
-    const bool     pair  = cls_nsb[ci] == 16 && layout_sb && tdec16_pays(cls_cb);
-    const int      cpw   = pair ? tdec16_cpw() : tdec_cpw(cls_nsb[ci]);
+    const int      kind  = cls_nsb[ci] == 16 && layout_sb ? tdec16_choice(cls_cb) : 0;  // 2 single, 1 pair, 0 quad
+    const int      cpw   = kind == 2 ? tdec16s_cpw() : kind == 1 ? tdec16_cpw() : tdec_cpw(cls_nsb[ci]);
     const size_t   n     = gs.size();
     const size_t   abyte = n * sizeof(TdecArgs);
     const size_t   need  = abyte + n * sizeof(uint32_t);
@@ -781,7 +791,8 @@ int srsran_tdec_gpu_run_multi(uint32_t              nof_groups,
       ha[k]            = a;
       hf[k]            = nblk;
       nblk += (nof_cb[g] + cpw - 1) / cpw;
-      lds = std::max(lds, pair ? tdec16_lds_bytes(a) : tdec_lds_bytes(c->nsb, a.xyw, a.M));
+      lds = std::max(lds, kind == 2 ? tdec16s_lds_bytes(a) : kind == 1 ? tdec16_lds_bytes(a)
+                                                                        : tdec_lds_bytes(c->nsb, a.xyw, a.M));
     }
     if (hipMemcpyAsync(m.d_stage, m.h_stage, need, hipMemcpyHostToDevice, st) != hipSuccess) {
       return SRSRAN_ERROR;
@@ -790,8 +801,9 @@ int srsran_tdec_gpu_run_multi(uint32_t              nof_groups,
     m.used = true;
     const TdecArgs* dg = reinterpret_cast<const TdecArgs*>(m.d_stage);
     const uint32_t* df = reinterpret_cast<const uint32_t*>(m.d_stage + abyte);
-    if ((pair ? tdec16_multi_launch(dg, df, (int)n, nblk, lds, st)
-                          : tdec_multi_launch(cls_nsb[ci], dg, df, (int)n, nblk, lds, st)) != hipSuccess) {
+    if ((kind == 2   ? tdec16s_multi_launch(dg, df, (int)n, nblk, lds, st)
+         : kind == 1 ? tdec16_multi_launch(dg, df, (int)n, nblk, lds, st)
+                     : tdec_multi_launch(cls_nsb[ci], dg, df, (int)n, nblk, lds, st)) != hipSuccess) {
       ret = SRSRAN_ERROR;
     }
   }

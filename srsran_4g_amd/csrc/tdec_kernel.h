@@ -23,6 +23,7 @@ struct TdecCb {
 static constexpr uint32_t TDEC_PAD_SLOT = 0xffffffffu;
 // the two blocks of a lane-pair workgroup must lie within this many bytes of each other
 static constexpr uint64_t TDEC_PAIR_SPAN = ((uint64_t)1 << 31) - ((uint64_t)1 << 16);
+static constexpr uint32_t TDEC_GROUP     = 4;  // blocks per workgroup of the largest such decoder
 
 struct TdecArgs {
   const short*    in;        // ncb code blocks, in_stride int16 apart (device)
@@ -75,6 +76,18 @@ hipError_t tdec16_multi_launch(const TdecArgs* d_groups, const uint32_t* d_first
                                size_t lds, hipStream_t stream);
 size_t     tdec16_lds_bytes(const TdecArgs& a);
 int        tdec16_cpw();
+// tdec16s_kernel.hip: one lane per sub-block (4 blocks a workgroup), the 16-sub-block class of large
+// batches; eligible where tdec16_eligible is, chosen from tdec16s_min_cb() blocks a launch
+hipError_t tdec16s_launch(const TdecArgs& a, hipStream_t stream);
+hipError_t tdec16s_multi_launch(const TdecArgs* d_groups, const uint32_t* d_first, int ngroups, uint32_t nblocks,
+                                size_t lds, hipStream_t stream);
+size_t     tdec16s_lds_bytes(const TdecArgs& a);
+int        tdec16s_cpw();
+void       tdec16s_set_min_cb(uint32_t n);
+uint32_t   tdec16s_min_cb();
+// the kernel the 16-sub-block class runs for a launch of ncb blocks on the SB layout: 2 = single lane
+// per sub-block (tdec16s), 1 = lane pair (tdec16), 0 = quad (tdec_kernel<16>)
+int        tdec16_choice(uint32_t ncb);
 size_t     tdec_lds_bytes(int nsb, int xyw, int M);
 // x^(8m) mod poly for m = 0..nm-1 (host helper for the CRC combine tables)
 void crc24_xpow_table(uint32_t poly, uint32_t* out, int nm);
@@ -91,9 +104,10 @@ int tdec_sch_enqueue(uint32_t      K,
                      uint8_t*      d_crc_ok,
                      int           n_end,
                      hipStream_t   stream);
-// Appends the blocks [first, last) of `src` to `dst` so that every two consecutive entries counted
-// from `dst_group_start` (a lane-pair workgroup) lie within TDEC_PAIR_SPAN: a padding entry is
-// inserted before a block that is too far from its partner.  Returns the padding entries added.
+// Appends the n blocks of `src` to `dst` so that every aligned group of TDEC_GROUP consecutive entries
+// counted from `dst_group_start` (a workgroup of the lane-pair or single-lane decoder) lies within
+// TDEC_PAIR_SPAN: padding entries close a group before a block too far from the group's others.
+// Returns the padding entries added.
 uint32_t tdec_pair_cbs(const TdecCb* src, uint32_t n, size_t dst_group_start, void* dst_vec);
 // name of the last turbo-decoder kernel this thread launched ("" before the first)
 const char* tdec_last_kernel();

@@ -23,6 +23,7 @@
 //   * everything runs inside one launch for all half-iterations; HBM traffic is the
 //     input LLRs once per half-iteration read + K/8 output bytes.
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <vector>
 #include <stdint.h>
 
@@ -821,7 +822,7 @@ hipError_t tdec_launch(int nsb, const TdecArgs& a, hipStream_t stream)
     return hipSuccess;
   }
   if (tdec16_eligible(nsb, a)) {
-    return tdec16_launch(a, stream);
+    return tdec16_choice(a.ncb) == 2 ? tdec16s_launch(a, stream) : tdec16_launch(a, stream);
   }
   switch (nsb) {
     case 16:
@@ -849,17 +850,26 @@ uint32_t tdec_pair_cbs(const TdecCb* src, uint32_t n, size_t dst_group_start, vo
 {
   std::vector<TdecCb>& dst = *static_cast<std::vector<TdecCb>*>(dst_vec);
   uint32_t             pads = 0;
+  uintptr_t            lo = 0, hi = 0;  // address range of the open group
   for (uint32_t i = 0; i < n; i++) {
-    const size_t pos = dst.size() - dst_group_start;
-    if (pos & 1) {  // second block of a workgroup: must share the first one's buffer resource
-      const uintptr_t p0 = (uintptr_t)dst.back().in, p1 = (uintptr_t)src[i].in;
-      if ((p0 > p1 ? p0 - p1 : p1 - p0) >= TDEC_PAIR_SPAN) {
-        TdecCb pad = dst.back();
-        pad.slot   = TDEC_PAD_SLOT;
+    const uintptr_t p   = (uintptr_t)src[i].in;
+    size_t          pos = (dst.size() - dst_group_start) % TDEC_GROUP;
+    if (pos != 0 && (std::max(hi, p) - std::min(lo, p)) >= TDEC_PAIR_SPAN) {
+      // too far from the group's blocks: pad the group out (the pads repeat its last block, so they
+      // stay inside its range) and start a new one
+      TdecCb pad = dst.back();
+      pad.slot   = TDEC_PAD_SLOT;
+      for (; pos < TDEC_GROUP; pos++) {
         dst.push_back(pad);
         pads++;
       }
+      pos = 0;
     }
+    if (pos == 0) {
+      lo = hi = p;
+    }
+    lo = std::min(lo, p);
+    hi = std::max(hi, p);
     dst.push_back(src[i]);
   }
   return pads;

@@ -91,6 +91,8 @@ def load_library():
         "srsran_tdec_gpu_last_kernel": ([], ctypes.c_char_p),
         "srsran_tdec_gpu_set_pair_threshold": ([u32], None),
         "srsran_tdec_gpu_get_pair_threshold": ([], u32),
+        "srsran_tdec_gpu_set_single_threshold": ([u32], None),
+        "srsran_tdec_gpu_get_single_threshold": ([], u32),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)
@@ -120,6 +122,23 @@ class pair_threshold:
 
     def __exit__(self, *exc):
         load_library().srsran_tdec_gpu_set_pair_threshold(self.old)
+
+
+class single_threshold:
+    """Context manager: blocks per launch from which the single-lane decoder runs
+    (srsran_tdec_gpu_set_single_threshold), restored on exit."""
+
+    def __init__(self, nof_cb):
+        self.n = nof_cb
+
+    def __enter__(self):
+        lib = load_library()
+        self.old = lib.srsran_tdec_gpu_get_single_threshold()
+        lib.srsran_tdec_gpu_set_single_threshold(self.n)
+        return self
+
+    def __exit__(self, *exc):
+        load_library().srsran_tdec_gpu_set_single_threshold(self.old)
 
 
 def nof_subblocks(K):

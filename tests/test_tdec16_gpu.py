@@ -1,7 +1,8 @@
-"""The lane-pair turbo decoder of the 16-sub-block class (tdec16_kernel.hip) forced onto small batches
-(srsran_tdec_gpu_set_pair_threshold(0); the library runs it by itself from 1024 blocks a launch): every K >= 816 of
-the bit-exact suites again, plain batches with odd block counts (the second block of a workgroup
-absent), the multi-size fused launch, and DL-SCH transport blocks with CRC early stop over HARQ."""
+"""The two decoders of the 16-sub-block class on the SB layout, each forced onto small batches: the lane
+pair (tdec16_kernel.hip; by itself from 1024 blocks a launch) and the single lane per sub-block
+(tdec16s_kernel.hip; by itself from srsran_tdec_gpu_get_single_threshold() blocks): every K >= 816 of
+the bit-exact suites again, plain batches with block counts that leave workgroups partly empty, the
+multi-size fused launch, and DL-SCH transport blocks with CRC early stop over HARQ."""
 import numpy as np
 import pytest
 
@@ -10,13 +11,19 @@ from oracle import CB_SIZES, Oracle, make_llrs
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module", autouse=True)
-def force_pair_kernel():
+KERNELS = {"pair": ("tdec16_kernel", 0, 1 << 30), "single": ("tdec16s_kernel", 0, 0)}
+
+
+@pytest.fixture(scope="module", autouse=True, params=sorted(KERNELS))
+def kernel(request):
+    """every test twice: the lane-pair decoder (tdec16_kernel.hip) and the single-lane decoder
+    (tdec16s_kernel.hip), each forced onto every batch size"""
     from srsran_4g_amd import tdec
     if not tdec.gpu_available():
         pytest.skip("no HIP device")
-    with tdec.pair_threshold(0):
-        yield
+    name, pair_min, single_min = KERNELS[request.param]
+    with tdec.pair_threshold(pair_min), tdec.single_threshold(single_min):
+        yield name
 
 
 @pytest.fixture(scope="module")
@@ -24,23 +31,24 @@ def ora():
     return Oracle()
 
 
-def test_all_large_sizes_bit_exact(ora):
-    """every K >= 816 (all 110 sizes), 3 blocks each (odd count), 8 half-iterations, SB layout"""
+def test_all_large_sizes_bit_exact(ora, kernel):
+    """every K >= 816 (all 110 sizes), 1..7 blocks (partly empty workgroups), 8 half-iterations, SB layout"""
     from srsran_4g_amd import tdec
     rng = np.random.default_rng(1601)
     dec = tdec.TurboDecoder()
     bad = []
-    for K in [k for k in CB_SIZES if k >= 816]:
-        _, llr = make_llrs(K, 1.5, rng, 3, ora)
+    for j, K in enumerate([k for k in CB_SIZES if k >= 816]):
+        _, llr = make_llrs(K, 1.5, rng, 1 + j % 7, ora)
         sb = np.stack([ora.natural_to_sb(K, x) for x in llr])
         if not np.array_equal(dec.run_all_batch(sb, 8, K), ora.run_batch(K, sb, True, 8)):
             bad.append(K)
+        assert tdec.last_kernel() == kernel + "<false>"
     dec.free()
     assert not bad, bad
 
 
 @pytest.mark.parametrize("nit", [1, 2, 3, 5, 16])
-def test_half_iteration_counts(ora, nit):
+def test_half_iteration_counts(ora, nit, kernel):
     from srsran_4g_amd import tdec
     rng = np.random.default_rng(1602 + nit)
     dec = tdec.TurboDecoder()
@@ -51,7 +59,7 @@ def test_half_iteration_counts(ora, nit):
     dec.free()
 
 
-def test_multi_size_launch(ora):
+def test_multi_size_launch(ora, kernel):
     """srsran_tdec_gpu_run_multi: several K >= 816 fused into one lane-pair launch"""
     import torch
     from srsran_4g_amd import tdec
@@ -68,14 +76,15 @@ def test_multi_size_launch(ora):
     tdec.gpu_run_multi(Ks, [t.data_ptr() for t in ins], [t.shape[1] for t in ins], True,
                        [t.data_ptr() for t in outs], [t.shape[0] for t in ins], 8, None)
     torch.cuda.synchronize()
+    assert tdec.last_kernel() == kernel.replace("_kernel", "_multi_kernel")
     for K, o, w in zip(Ks, outs, want):
         assert np.array_equal(o.cpu().numpy(), w), K
 
 
-def test_dlsch_early_stop_harq(ora):
+def test_dlsch_early_stop_harq(ora, kernel):
     """DL-SCH decode_tb with the pair kernel's CRC early stop: return, payload, average iterations,
     CB flags, over rv 0 -> 2 at low SNR (some blocks pass at rv 0, the rest after combining)"""
-    from srsran_4g_amd import sch
+    from srsran_4g_amd import sch, tdec
     rng = np.random.default_rng(1604)
     q = sch.Sch()
     for tbs, Qm, G in ((75376, 6, 86400), (36696, 6, 43200), (6200, 2, 14400)):
@@ -87,6 +96,7 @@ def test_dlsch_early_stop_harq(ora):
             llr = np.trunc(100 * (e + rng.standard_normal(e.shape).astype(np.float32) * sigma)).astype(np.int16)
             q.set_max_noi(8)
             ret, data, avg = q.decode(sb, tbs, Qm, rv, llr)
+            assert tdec.last_kernel() == kernel + "<true>"
             oret, odata, _, oavg, state = ora.dlsch_decode(tbs, Qm, rv, llr, 8, state)
             assert ret == oret, (tbs, rv)
             assert np.array_equal(data[: len(odata)], odata), (tbs, rv)

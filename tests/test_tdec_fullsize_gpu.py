@@ -4,9 +4,10 @@ AVX2 16-bit window decoders of turbodecoder_win.h), and the DL-SCH path of sch.c
 buffers placed far apart in device memory.
 
   * configs[1]: all 188 LTE code block sizes x 1024 blocks, 8 half-iterations, one
-    srsran_tdec_gpu_run_multi call (the bench's timed step): the 16-sub-block class is the fused
-    lane-pair launch tdec16_multi_kernel (110 sizes x 1024 blocks in one grid), the 8- and
-    1-sub-block classes the quad decoder's fused launches.  Every block equals the reference's output
+    srsran_tdec_gpu_run_multi call (the bench's timed step): the 16-sub-block class is one fused
+    launch (110 sizes x 1024 blocks in one grid) of the single-lane decoder tdec16s_multi_kernel (and,
+    checked as well, of the lane-pair tdec16_multi_kernel), the 8- and 1-sub-block classes the quad
+    decoder's fused launches.  Every block equals the reference's output
     for its pool block (the batch tiles a pool of distinct AWGN blocks at several SNRs, so decoded
     words differ from the transmitted ones in some blocks and not in others).
   * configs[0]'s shape on the GPU: K = 6144 x 1024 through srsran_tdec_gpu_run_batch.
@@ -60,17 +61,20 @@ def test_all188_x1024_fused_launch(env):
     k16 = [i for i, K in enumerate(Ks) if tdec.nof_subblocks(K) == 16]
     assert len(k16) == 110
 
-    # the 16-sub-block class alone: one fused lane-pair launch
-    tdec.gpu_run_multi([Ks[i] for i in k16], [ins[i].data_ptr() for i in k16], [ins[i].shape[1] for i in k16],
-                       True, [outs[i].data_ptr() for i in k16], [batch] * len(k16), iters, None)
-    torch.cuda.synchronize()
-    assert tdec.last_kernel() == "tdec16_multi_kernel"
-    for i in k16:
-        K = Ks[i]
-        got = outs[i].cpu().numpy()
-        exp = want[K][np.arange(batch) % len(POOL_EBNO)]
-        assert np.array_equal(got, exp), f"K={K}: {(got != exp).any(axis=1).sum()} blocks differ"
-        outs[i].zero_()
+    # the 16-sub-block class alone: one fused launch of the single-lane decoder (the library's choice
+    # at 112,640 blocks), then of the lane-pair decoder
+    for name, single in (("tdec16s_multi_kernel", None), ("tdec16_multi_kernel", 1 << 30)):
+        with tdec.single_threshold(single if single is not None else tdec.load_library().srsran_tdec_gpu_get_single_threshold()):
+            tdec.gpu_run_multi([Ks[i] for i in k16], [ins[i].data_ptr() for i in k16], [ins[i].shape[1] for i in k16],
+                               True, [outs[i].data_ptr() for i in k16], [batch] * len(k16), iters, None)
+            torch.cuda.synchronize()
+            assert tdec.last_kernel() == name
+        for i in k16:
+            K = Ks[i]
+            got = outs[i].cpu().numpy()
+            exp = want[K][np.arange(batch) % len(POOL_EBNO)]
+            assert np.array_equal(got, exp), f"{name} K={K}: {(got != exp).any(axis=1).sum()} blocks differ"
+            outs[i].zero_()
 
     # all 188 sizes in one call, as the bench's timed step
     tdec.gpu_run_multi(Ks, [t.data_ptr() for t in ins], [t.shape[1] for t in ins], True,
@@ -104,9 +108,10 @@ def test_k6144_x1024_batch(env):
     assert np.array_equal(got, want[np.arange(batch) % len(pool)])
 
 
-def test_dlsch_far_soft_buffers_run_pair_kernel(env):
-    """soft buffers > 2 GB apart (arena off, 2.4 GB buffers): the lane-pair decoder still runs and
-    every TB equals the oracle's decode_tb"""
+@pytest.mark.parametrize("kernel", ["tdec16_kernel", "tdec16s_kernel"])
+def test_dlsch_far_soft_buffers(env, kernel):
+    """soft buffers > 2 GB apart (arena off, 2.4 GB buffers): the lane-pair and the single-lane decoder
+    still run (the descriptor list is padded per workgroup) and every TB equals the oracle's decode_tb"""
     torch, tdec, ref, ora = env
     from srsran_4g_amd import sch as S
     rng = np.random.default_rng(3003)
@@ -135,10 +140,10 @@ def test_dlsch_far_soft_buffers_run_pair_kernel(env):
         exp.append(ora.dlsch_decode(tbs, Qm, 0, llr, 8))
     d_res = torch.full((ntb,), 77, dtype=torch.int32, device="cuda")
     d_avg = torch.zeros(ntb, dtype=torch.float32, device="cuda")
-    with tdec.pair_threshold(0):
+    with tdec.pair_threshold(0), tdec.single_threshold(0 if kernel == "tdec16s_kernel" else 1 << 30):
         assert q.decode_batch(entries, d_res.data_ptr(), d_avg.data_ptr()) == 0
         torch.cuda.synchronize()
-        assert tdec.last_kernel() == "tdec16_kernel<true>"
+        assert tdec.last_kernel() == kernel + "<true>"
     res, avg = d_res.cpu().numpy(), d_avg.cpu().numpy()
     C = S.cbsegm(tbs)[1].C
     for i, (oret, odata, _, oavg, st) in enumerate(exp):

@@ -130,6 +130,11 @@ def parse():
     p.add_argument("--pdsch-steps", type=int, default=5,
                    help="all188: timed steps of the C3 PDSCH chain reported in the same line (0 = skip)")
     p.add_argument("--pdsch-cpu-seconds", type=float, default=4.0, help="all188: CPU baseline budget of the PDSCH part")
+    p.add_argument("--pdsch-low-snr", type=float, default=20.0,
+                   help="all188: SNR (dB) of a second, shorter PDSCH chain run where the turbo decoder needs "
+                        "several half-iterations (0 = skip)")
+    p.add_argument("--tdec16", choices=["auto", "single", "pair", "quad"], default="auto",
+                   help="decoder of the 16-sub-block class: the library's choice by batch size, or forced")
     p.add_argument("--cpu-worker", type=int, default=None, help=argparse.SUPPRESS)
     return p.parse_args()
 
@@ -810,22 +815,49 @@ def run_pdsch(args, torch, dist, world, rank, device, steps=None, warmup=None, c
     stream = torch.cuda.current_stream(device)
     sp = stream.cuda_stream
 
-    def step():
-        if ue.gpu_decode_batch(arr, d_x.data_ptr(), d_res.data_ptr(), d_avg.data_ptr(), 0.0, sp) != 2 * nsf:
+    def step(x_ptr=None):
+        if ue.gpu_decode_batch(arr, d_x.data_ptr() if x_ptr is None else x_ptr, d_res.data_ptr(), d_avg.data_ptr(),
+                               0.0, sp) != 2 * nsf:
             raise RuntimeError("srsran_ue_dl_gpu_decode_batch failed")
 
     elapsed = timed_region(step, steps, warmup, world, dist, torch.cuda.synchronize, device)
-    # PCIe-inclusive rate (never `value`): the time samples start in pinned host memory and are
-    # copied H2D on the launch stream before every step
+    # PCIe-inclusive rate (never `value`): every step's time samples start in pinned host memory.
+    # Two device sample buffers: step i+1's H2D runs on a copy stream while step i decodes
+    # (phy_dl_test.c:658-671 feeds one subframe at a time; here the copy hides under the batch).
     h_x = torch.from_numpy(np.ascontiguousarray(host).view(np.float32)).pin_memory()
+    d_xs = [d_x, torch.empty_like(d_x)]
+    cs = torch.cuda.Stream(device)
+    copied = [torch.cuda.Event(), torch.cuda.Event()]
+    used = [torch.cuda.Event(), torch.cuda.Event()]
+    n_h2d = max(steps, 10)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    for _ in range(steps):
-        with torch.cuda.stream(stream):
-            d_x.copy_(h_x, non_blocking=True)
-        step()
+    with torch.cuda.stream(cs):
+        d_xs[0].copy_(h_x, non_blocking=True)
+    copied[0].record(cs)
+    for i in range(n_h2d):
+        b = i % 2
+        if i + 1 < n_h2d:
+            nb = (i + 1) % 2
+            if i >= 1:
+                cs.wait_event(used[nb])  # step i-1 is done with that buffer
+            with torch.cuda.stream(cs):
+                d_xs[nb].copy_(h_x, non_blocking=True)
+            copied[nb].record(cs)
+        stream.wait_event(copied[b])
+        step(d_xs[b].data_ptr())
+        used[b].record(stream)
     torch.cuda.synchronize()
-    h2d_s = (time.perf_counter() - t1) / steps
+    h2d_s = (time.perf_counter() - t1) / n_h2d
+    # the copy alone, for the PCIe bound of the same bytes
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(n_h2d):
+        with torch.cuda.stream(cs):
+            d_xs[1].copy_(h_x, non_blocking=True)
+    torch.cuda.synchronize()
+    copy_s = (time.perf_counter() - t1) / n_h2d
+    del d_xs[1]
     # host enqueue cost of one step (the API builds descriptors and launches asynchronously)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
@@ -860,7 +892,10 @@ def run_pdsch(args, torch, dist, world, rank, device, steps=None, warmup=None, c
     d = per_stage[dom]
     bytes_per_launch = sb[dom] / d["launches_per_step"]
     achieved = bytes_per_launch / (d["avg_launch_ms"] * 1e-3) / 1e9
-    traffic = pmc_traffic("pdsch", dom, nsf * 26) if dom == "tdec_kernel" else None
+    from srsran_4g_amd import tdec as TD
+    # the turbo stage's kernel as it ran (srsran_tdec_gpu_last_kernel), e.g. tdec16s_kernel<true>
+    dom_name = TD.last_kernel() if dom == "tdec_kernel" else dom
+    traffic = pmc_traffic("pdsch", dom_name, nsf * 26)
     result = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -881,6 +916,8 @@ def run_pdsch(args, torch, dist, world, rank, device, steps=None, warmup=None, c
             "subframes_per_step_per_gpu": nsf,
             "subframes_per_s": round(world * nsf * steps / elapsed, 1),
             "subframes_per_s_h2d_inclusive": round(world * nsf / h2d_s, 1),
+            "h2d_copy_only_subframes_per_s": round(world * nsf / copy_s, 1),
+            "h2d_gbps": round(host.nbytes / copy_s / 1e9, 2),
             "tb_ok_fraction": round(ok / (2 * nsf), 4),
             "avg_half_iterations": round(float(avg.mean()), 3),
             "cell_id": cell_id,
@@ -888,7 +925,7 @@ def run_pdsch(args, torch, dist, world, rank, device, steps=None, warmup=None, c
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": dom,
+            "kernel": dom_name,
             "achieved": round(achieved, 2),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
@@ -1235,6 +1272,11 @@ def main():
     device = torch.device("cuda", local)
     if not tdec.gpu_available():
         raise RuntimeError("bench: HIP device not visible to libsrsran_4g_amd")
+    if args.tdec16 != "auto":  # srsran_tdec_gpu_set_pair_threshold / _single_threshold
+        never = 1 << 30
+        pair_min, single_min = {"single": (0, 0), "pair": (0, never), "quad": (never, never)}[args.tdec16]
+        tdec.load_library().srsran_tdec_gpu_set_pair_threshold(pair_min)
+        tdec.load_library().srsran_tdec_gpu_set_single_threshold(single_min)
     if args.workload in ("dlsch", "ulsch"):
         return run_dlsch(args, torch, dist, world, rank, device)
     if args.workload == "pusch":
@@ -1310,7 +1352,7 @@ def main():
             e1.record(stream)
             torch.cuda.synchronize()
             ms16.append(e0.elapsed_time(e1))
-        dom = "tdec16_multi_kernel" if args.batch * len(k16) >= 1024 else "tdec_multi_kernel<16>"
+        dom = tdec.last_kernel()  # the 16-class launch just timed (srsran_tdec_gpu_last_kernel)
         avg_ms = float(np.mean(ms16))
         bytes_per_launch = sum(args.batch * algo_bytes(Ks[i]) for i in k16)
         dom_units = args.batch * len(k16)
@@ -1387,6 +1429,7 @@ def main():
             "half_iterations": args.iters,
             "info_bits_per_step_per_gpu": bits_per_step,
             "parallelism": f"cb-sharded x{world}",
+            "tdec16": args.tdec16,
         },
         "roofline": dict({
             "bound": "hbm",
@@ -1426,6 +1469,7 @@ def main():
             "workload": pd["config"]["workload"],
             "subframes_per_s": pd["config"]["subframes_per_s"],
             "subframes_per_s_h2d_inclusive": pd["config"]["subframes_per_s_h2d_inclusive"],
+            "h2d_copy_only_subframes_per_s": pd["config"]["h2d_copy_only_subframes_per_s"],
             "mbps": pd["value"],
             "ms_per_step": pd["ms_per_step"],
             "steps": pd["steps"],
@@ -1438,6 +1482,23 @@ def main():
                                          / (world * HBM_PEAK_GBS * 1e9), 5),
             "cpu_baseline": pd.get("cpu_baseline"),
         }
+        if args.pdsch_low_snr > 0:
+            # the same chain where the turbo decoder works for its result: several half-iterations a TB
+            import copy
+            a2 = copy.copy(args)
+            a2.snr = args.pdsch_low_snr
+            pl = run_pdsch(a2, torch, dist, world, rank, device, steps=args.pdsch_steps, warmup=2, cpu_seconds=0,
+                           emit=False)
+            result["pdsch_low_snr"] = {
+                "snr_db": args.pdsch_low_snr,
+                "subframes_per_s": pl["config"]["subframes_per_s"],
+                "mbps": pl["value"],
+                "ms_per_step": pl["ms_per_step"],
+                "avg_half_iterations": pl["config"]["avg_half_iterations"],
+                "tb_ok_fraction": pl["config"]["tb_ok_fraction"],
+                "turbo_kernel": pl["roofline"]["kernel"],
+                "turbo_ms_per_step": pl["stages"].get("tdec_kernel", {}).get("ms_per_step"),
+            }
         # the uplink counterpart: the eNB PUSCH chain, summary only
         pu = run_pusch(args, torch, dist, world, rank, device, steps=args.pdsch_steps, warmup=2,
                        cpu_seconds=2.0 if args.cpu_seconds > 0 else 0, emit=False)

@@ -36,6 +36,8 @@ class Ref:
         L = ctypes.CDLL(REF_SO, mode=os.RTLD_LAZY)
         L.ref_regs_tables.argtypes = [u32, u32, u32, ctypes.c_int, ctypes.c_int, u32p, u32p, u32, u32p]
         L.ref_regs_tables_mi.argtypes = [u32, u32, u32, ctypes.c_int, ctypes.c_int, u32, u32p, u32p, u32, u32p]
+        L.ref_set_cp.argtypes = [ctypes.c_int]
+        L.ref_set_cp(0)
         L.ref_ctrl_tx.argtypes = [u32, u32, u32, ctypes.c_int, ctypes.c_int, u32, u32, u32, u8p, u32p, u32p, u32p,
                                   u16p, f32p]
         L.ref_ctrl_rx.argtypes = [u32, u32, u32, ctypes.c_int, ctypes.c_int, u32, u32, f32p, f32p, ctypes.c_float,
@@ -45,6 +47,10 @@ class Ref:
         L.ref_viterbi_decode_f.argtypes = [f32p, u32, u8p]
         L.ref_rm_conv_rx.argtypes = [f32p, u32, f32p, u32]
         self.L = L
+
+    def set_cp(self, ext):
+        """cyclic prefix of the reference cells built from now on (0 normal, 1 extended)"""
+        self.L.ref_set_cp(int(ext))
 
     def regs_tables(self, nof_prb, nof_ports, cell_id, phich_len=0, phich_res=2, phich_mi=1):
         """regs.c tables of srsran_regs_init_opts(cell, phich_mi) (regs.c:711-783)"""

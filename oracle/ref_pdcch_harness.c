@@ -125,6 +125,10 @@ void srsran_phy_log_print(phy_logger_level_t log_level, const char* format, ...)
 }
 
 /* ---------------- harness ---------------- */
+/* cyclic prefix of the cells the harness builds from now on (0 normal, 1 extended) */
+static srsran_cp_t g_cp = SRSRAN_CP_NORM;
+void               ref_set_cp(int ext) { g_cp = ext ? SRSRAN_CP_EXT : SRSRAN_CP_NORM; }
+
 static srsran_cell_t mkcell(uint32_t nof_prb, uint32_t nof_ports, uint32_t id, int phich_len, int phich_res)
 {
   srsran_cell_t c;
@@ -132,7 +136,7 @@ static srsran_cell_t mkcell(uint32_t nof_prb, uint32_t nof_ports, uint32_t id, i
   c.nof_prb         = nof_prb;
   c.nof_ports       = nof_ports;
   c.id              = id;
-  c.cp              = SRSRAN_CP_NORM;
+  c.cp              = g_cp;
   c.phich_length    = (srsran_phich_length_t)phich_len;
   c.phich_resources = (srsran_phich_r_t)phich_res;
   c.frame_type      = SRSRAN_FDD;

@@ -44,13 +44,15 @@ struct Reg {
   bool     assigned;
 };
 
-int regs_per_symbol(uint32_t l, uint32_t nof_ports)  // regs.c:487-516 (normal CP)
+int regs_per_symbol(uint32_t l, uint32_t nof_ports, srsran_cp_t cp)  // regs_num_x_symbol, regs.c:587-617
 {
   switch (l) {
     case 0:
       return 2;
     case 1:
       return nof_ports == 4 ? 2 : 3;
+    case 3:  // extended CP: the CRS of ports 0 / 1 sit in symbol 3 (36.211 6.10.1.2)
+      return cp == SRSRAN_CP_NORM ? 3 : 2;
     default:
       return 3;
   }
@@ -86,7 +88,7 @@ int build_regs(srsran_regs_t* h, uint32_t phich_mi)
   int      n[4];
   uint32_t nof_regs = 0;
   for (uint32_t i = 0; i < nctrl; i++) {
-    n[i] = regs_per_symbol(i, c.nof_ports);
+    n[i] = regs_per_symbol(i, c.nof_ports, c.cp);
     nof_regs += nprb * n[i];
   }
   // REGs sorted by PRB, then the frequency-first interleaving of regs.c:747-770
@@ -355,7 +357,7 @@ int ctrl_equalise(CtrlGpu* g, const uint32_t* d_idx, uint32_t n, float noise)
 bool valid_cell(const srsran_cell_t& c)
 {
   return c.nof_prb >= 6 && c.nof_prb <= SRSRAN_MAX_PRB && (c.nof_ports == 1 || c.nof_ports == 2 || c.nof_ports == 4) &&
-         c.cp == SRSRAN_CP_NORM && c.id < 504;
+         (c.cp == SRSRAN_CP_NORM || c.cp == SRSRAN_CP_EXT) && c.id < 504;
 }
 
 }  // namespace

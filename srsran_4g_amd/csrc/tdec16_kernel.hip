@@ -776,6 +776,12 @@ bool tdec16_eligible(int nsb, const TdecArgs& a)
          tdec16_choice(a.ncb) > 0;
 }
 
+bool tdec8s_eligible(int nsb, const TdecArgs& a)
+{
+  return nsb == 8 && a.layout_sb && a.n_start == 0 && a.state == nullptr && a.L >= (uint32_t)OVL &&
+         a.ncb >= tdec16s_min_cb();
+}
+
 size_t tdec16_lds_bytes(const TdecArgs& a)
 {
   const Geo16 g = geo16((int)a.K, (int)a.Ls, (int)((a.L + W - 1) / W));

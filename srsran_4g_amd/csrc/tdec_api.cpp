@@ -748,8 +748,12 @@ int srsran_tdec_gpu_run_multi(uint32_t              nof_groups,
     for (uint32_t g : gs) {
       cls_cb += nof_cb[g];
     }
-    const int      kind  = cls_nsb[ci] == 16 && layout_sb ? tdec16_choice(cls_cb) : 0;  // 2 single, 1 pair, 0 quad
-    const int      cpw   = kind == 2 ? tdec16s_cpw() : kind == 1 ? tdec16_cpw() : tdec_cpw(cls_nsb[ci]);
+    // 2 single lane (tdecs_kernel.hip), 1 lane pair (16 sub-blocks only), 0 quad
+    const int kind = !layout_sb || cls_nsb[ci] == 1 ? 0
+                     : cls_nsb[ci] == 16            ? tdec16_choice(cls_cb)
+                                                    : (cls_cb >= tdec16s_min_cb() ? 2 : 0);
+    const bool s16 = cls_nsb[ci] == 16;
+    const int  cpw = kind == 2 ? (s16 ? tdecs16::cpw() : tdecs8::cpw()) : kind == 1 ? tdec16_cpw() : tdec_cpw(cls_nsb[ci]);
     const size_t   n     = gs.size();
     const size_t   abyte = n * sizeof(TdecArgs);
     const size_t   need  = abyte + n * sizeof(uint32_t);
@@ -791,8 +795,9 @@ int srsran_tdec_gpu_run_multi(uint32_t              nof_groups,
       ha[k]            = a;
       hf[k]            = nblk;
       nblk += (nof_cb[g] + cpw - 1) / cpw;
-      lds = std::max(lds, kind == 2 ? tdec16s_lds_bytes(a) : kind == 1 ? tdec16_lds_bytes(a)
-                                                                        : tdec_lds_bytes(c->nsb, a.xyw, a.M));
+      lds = std::max(lds, kind == 2   ? (s16 ? tdecs16::lds_bytes(a) : tdecs8::lds_bytes(a))
+                          : kind == 1 ? tdec16_lds_bytes(a)
+                                      : tdec_lds_bytes(c->nsb, a.xyw, a.M));
     }
     if (hipMemcpyAsync(m.d_stage, m.h_stage, need, hipMemcpyHostToDevice, st) != hipSuccess) {
       return SRSRAN_ERROR;
@@ -801,7 +806,8 @@ int srsran_tdec_gpu_run_multi(uint32_t              nof_groups,
     m.used = true;
     const TdecArgs* dg = reinterpret_cast<const TdecArgs*>(m.d_stage);
     const uint32_t* df = reinterpret_cast<const uint32_t*>(m.d_stage + abyte);
-    if ((kind == 2   ? tdec16s_multi_launch(dg, df, (int)n, nblk, lds, st)
+    if ((kind == 2   ? (s16 ? tdecs16::multi_launch(dg, df, (int)n, nblk, lds, st)
+                            : tdecs8::multi_launch(dg, df, (int)n, nblk, lds, st))
          : kind == 1 ? tdec16_multi_launch(dg, df, (int)n, nblk, lds, st)
                      : tdec_multi_launch(cls_nsb[ci], dg, df, (int)n, nblk, lds, st)) != hipSuccess) {
       ret = SRSRAN_ERROR;

@@ -23,7 +23,7 @@ struct TdecCb {
 static constexpr uint32_t TDEC_PAD_SLOT = 0xffffffffu;
 // the two blocks of a lane-pair workgroup must lie within this many bytes of each other
 static constexpr uint64_t TDEC_PAIR_SPAN = ((uint64_t)1 << 31) - ((uint64_t)1 << 16);
-static constexpr uint32_t TDEC_GROUP     = 4;  // blocks per workgroup of the largest such decoder
+static constexpr uint32_t TDEC_GROUP     = 8;  // blocks per workgroup of the largest such decoder (tdec8s)
 
 struct TdecArgs {
   const short*    in;        // ncb code blocks, in_stride int16 apart (device)
@@ -76,13 +76,21 @@ hipError_t tdec16_multi_launch(const TdecArgs* d_groups, const uint32_t* d_first
                                size_t lds, hipStream_t stream);
 size_t     tdec16_lds_bytes(const TdecArgs& a);
 int        tdec16_cpw();
-// tdec16s_kernel.hip: one lane per sub-block (4 blocks a workgroup), the 16-sub-block class of large
-// batches; eligible where tdec16_eligible is, chosen from tdec16s_min_cb() blocks a launch
-hipError_t tdec16s_launch(const TdecArgs& a, hipStream_t stream);
-hipError_t tdec16s_multi_launch(const TdecArgs* d_groups, const uint32_t* d_first, int ngroups, uint32_t nblocks,
-                                size_t lds, hipStream_t stream);
-size_t     tdec16s_lds_bytes(const TdecArgs& a);
-int        tdec16s_cpw();
+// tdecs_kernel.hip: one lane per sub-block (64 / NSB blocks a workgroup), the window classes of large
+// batches (16 sub-blocks: eligible where tdec16_eligible is, chosen from tdec16s_min_cb() blocks a
+// launch; 8 sub-blocks: tdec8s_eligible)
+#define SRSRAN_TDECS_API(ns)                                                                               \
+  namespace ns {                                                                                           \
+  hipError_t launch(const TdecArgs& a, hipStream_t stream);                                                \
+  hipError_t multi_launch(const TdecArgs* d_groups, const uint32_t* d_first, int ngroups, uint32_t nblocks, \
+                          size_t lds, hipStream_t stream);                                                 \
+  size_t     lds_bytes(const TdecArgs& a);                                                                 \
+  int        cpw();                                                                                        \
+  }
+SRSRAN_TDECS_API(tdecs16)
+SRSRAN_TDECS_API(tdecs8)
+#undef SRSRAN_TDECS_API
+bool       tdec8s_eligible(int nsb, const TdecArgs& a);
 void       tdec16s_set_min_cb(uint32_t n);
 uint32_t   tdec16s_min_cb();
 // the kernel the 16-sub-block class runs for a launch of ncb blocks on the SB layout: 2 = single lane

@@ -822,7 +822,10 @@ hipError_t tdec_launch(int nsb, const TdecArgs& a, hipStream_t stream)
     return hipSuccess;
   }
   if (tdec16_eligible(nsb, a)) {
-    return tdec16_choice(a.ncb) == 2 ? tdec16s_launch(a, stream) : tdec16_launch(a, stream);
+    return tdec16_choice(a.ncb) == 2 ? tdecs16::launch(a, stream) : tdec16_launch(a, stream);
+  }
+  if (tdec8s_eligible(nsb, a)) {
+    return tdecs8::launch(a, stream);
   }
   switch (nsb) {
     case 16:

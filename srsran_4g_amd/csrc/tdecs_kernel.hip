@@ -1,5 +1,7 @@
-// srsran_4g_amd/csrc/tdec16s_kernel.hip -- LTE turbo decoder for K >= 816 (16 sub-blocks), ONE LANE
-// PER SUB-BLOCK: the throughput mapping of the 16-sub-block class on CDNA4.
+// srsran_4g_amd/csrc/tdecs_kernel.hip -- LTE turbo decoder of the window classes (16 sub-blocks for
+// K >= 816, 8 sub-blocks for 408 <= K <= 800), ONE LANE PER SUB-BLOCK: the throughput mapping on CDNA4.
+// Compiled once per class (Makefile: -DTDECS_NSB=16 -> namespace tdecs16, kernels tdec16s_*;
+// -DTDECS_NSB=8 -> tdecs8, tdec8s_*).
 //
 // Same arithmetic, schedule and LDS bookkeeping as tdec16_kernel.hip (bit-exact with srsRAN_4G's AVX2
 // 16-bit window decoder, turbodecoder_win.h:480-832, driven by turbodecoder_iter.h:72-144 on the
@@ -16,9 +18,11 @@
 //         alpha:  (a0,a1) (a7,a6) (a3,a2) (a4,a5)    beta:  (b0,b4) (b7,b3) (b2,b6) (b5,b1)
 //     and the forward step's candidates pair with the betas of the LLR in the same registers
 //     (derivation in DESIGN.md section 4.1).
-//   * per code block 16 lanes a side: a wave holds the forward (alpha) side of 4 code blocks, its
-//     partner wave their backward (beta) side: 128-thread workgroups of 4 blocks of one K.  Half the
-//     lanes of the lane-pair kernel per block and none of its duplicated loads, LDS writes and LLR work.
+//   * per code block NSB lanes a side: a wave holds the forward (alpha) side of 64 / NSB code blocks,
+//     its partner wave their backward (beta) side: 128-thread workgroups of 64 / NSB blocks of one K.
+//     Half the lanes of the lane-pair kernel per block and none of its duplicated loads, LDS writes and
+//     LLR work.  The 8-sub-block class is the SSE 8-block window decoder (turbodecoder_win.h with
+//     WINIMP sse16): the same arithmetic on half as many sub-blocks.
 //   * LDS per code block exactly as tdec16_kernel.hip: the in-place a-priori / extrinsic array S over
 //     the soft-buffer slots, beta / alpha checkpoints (one state = 16 B per sub-block and window) and
 //     the decision bitmap.
@@ -29,16 +33,33 @@
 #include "stage_timing.h"
 #include "tdec_kernel.h"
 
+#ifndef TDECS_NSB
+#define TDECS_NSB 16
+#endif
+#if TDECS_NSB == 16
+#define TDECS_NS tdecs16
+#define TDECS_K(n) tdec16s_##n
+#define TDECS_NAME "tdec16s_"
+#elif TDECS_NSB == 8
+#define TDECS_NS tdecs8
+#define TDECS_K(n) tdec8s_##n
+#define TDECS_NAME "tdec8s_"
+#else
+#error "TDECS_NSB must be 16 or 8"
+#endif
+
 namespace srsran_amd {
+namespace TDECS_NS {
 namespace {
 
 typedef short v2s __attribute__((ext_vector_type(2)));
 
 constexpr int   W    = 16;            // window: steps between checkpoints
 constexpr int   OVL  = TDEC_OVERLAP;  // win_overlap_len (turbodecoder_win.h:54)
-constexpr int   NSB  = 16;            // nof_blocks of the avx16 window decoder
+constexpr int   NSB  = TDECS_NSB;     // nof_blocks of the window decoder (avx16: 16, sse16: 8)
 constexpr short NEG  = -10000;        // -INF (turbodecoder_win.h:56)
-constexpr int   CPWG = 4;             // code blocks per workgroup
+constexpr int   CPWG = 64 / NSB;      // code blocks per workgroup (one wave a side)
+constexpr int   ROWB = 2 * NSB;       // bytes of one position row of the SB input (all sub-blocks)
 
 __device__ __forceinline__ v2s u2v(uint32_t u) { return __builtin_bit_cast(v2s, u); }
 __device__ __forceinline__ uint32_t v2u(v2s v) { return __builtin_bit_cast(uint32_t, v); }
@@ -160,7 +181,7 @@ __device__ __forceinline__ St trellis(const short* xt, const short* yt)
   return St{v2s{o[0], o[4]}, v2s{o[7], o[3]}, v2s{o[2], o[6]}, v2s{o[5], o[1]}};
 }
 
-// LDS of one code block (dwords): S [16*Ls int16] | CK [M windows][16 lanes][16 B] | BITS [K/8 B] | RED [2]
+// LDS of one code block (dwords): S [NSB*Ls int16] | CK [M windows][NSB lanes][16 B] | BITS [K/8 B] | RED [2]
 struct Geo {
   int s_dw, ck_dw, bits_dw, cb_dw;
 };
@@ -168,7 +189,7 @@ __host__ __device__ __forceinline__ Geo geo(int K, int Ls, int M)
 {
   Geo g;
   g.s_dw    = (NSB * Ls + 1) / 2;
-  g.ck_dw   = M * 64;
+  g.ck_dw   = M * NSB * 4;
   g.bits_dw = (K / 8 + 3) / 4;
   g.cb_dw   = g.s_dw + g.ck_dw + g.bits_dw + 2;
   return g;
@@ -202,29 +223,29 @@ struct Lane {
   rsrc_t    rtf;   // tfwd (q order, SB input: slot of pi(n(q))), K entries
   lshort    S;     // this block's S (LDS)
   lshort    Ssb;   // S + s * Ls: this lane's sub-block
-  uint4*    CK;    // this block's checkpoints (LDS), [M][16]
+  uint4*    CK;    // this block's checkpoints (LDS), [M][NSB]
   uint32_t* BITS;  // this block's decision bitmap (LDS)
 };
 
 __device__ __forceinline__ void ck_put(const Lane& c, int m, const St& p)
 {
-  c.CK[m * 16 + c.s] = make_uint4(v2u(p.a), v2u(p.b), v2u(p.c), v2u(p.d));
+  c.CK[m * NSB + c.s] = make_uint4(v2u(p.a), v2u(p.b), v2u(p.c), v2u(p.d));
 }
 __device__ __forceinline__ St ck_get(const Lane& c, int m)
 {
-  const uint4 v = c.CK[m * 16 + c.s];
+  const uint4 v = c.CK[m * NSB + c.s];
   return St{u2v(v.x), u2v(v.y), u2v(v.z), u2v(v.w)};
 }
 
 template <bool D2>
 __device__ __forceinline__ void issue(const Lane& c, Raw& r, int t0)
 {
-  const uint32_t soff = 32u * (uint32_t)t0;
+  const uint32_t soff = (uint32_t)ROWB * (uint32_t)t0;
   const uint32_t poff = soff + (D2 ? 4u : 2u) * (uint32_t)c.KP;  // parity stream, bytes
 #pragma unroll
   for (int i = 0; i < W; i++) {
-    r.a[i] = D2 ? ldb(c.rtf, 2u * (uint32_t)c.s, soff, 32 * i) : ldb(c.rin, c.voff, soff, 32 * i);
-    r.b[i] = ldb(c.rin, c.voff, poff, 32 * i);
+    r.a[i] = D2 ? ldb(c.rtf, 2u * (uint32_t)c.s, soff, ROWB * i) : ldb(c.rin, c.voff, soff, ROWB * i);
+    r.b[i] = ldb(c.rin, c.voff, poff, ROWB * i);
   }
 }
 
@@ -417,10 +438,10 @@ __device__ __forceinline__ void map16s(const Lane& cin, int wave)
     }
     {  // move_left: sub-block s starts from the training state of s - 1; s = 0 is known
       St q;
-      q.a = u2v((uint32_t)__shfl_up((int)v2u(P.a), 1, 16));
-      q.b = u2v((uint32_t)__shfl_up((int)v2u(P.b), 1, 16));
-      q.c = u2v((uint32_t)__shfl_up((int)v2u(P.c), 1, 16));
-      q.d = u2v((uint32_t)__shfl_up((int)v2u(P.d), 1, 16));
+      q.a = u2v((uint32_t)__shfl_up((int)v2u(P.a), 1, NSB));
+      q.b = u2v((uint32_t)__shfl_up((int)v2u(P.b), 1, NSB));
+      q.c = u2v((uint32_t)__shfl_up((int)v2u(P.c), 1, NSB));
+      q.d = u2v((uint32_t)__shfl_up((int)v2u(P.d), 1, NSB));
       P   = c.s == 0 ? alpha_known() : q;
     }
     // phase 1: windows [0, h) (all full), entry checkpoints in slots 0..h-1
@@ -470,10 +491,10 @@ __device__ __forceinline__ void map16s(const Lane& cin, int wave)
     }
     {  // move_right: sub-block s starts from the training state of s + 1; the last from the tail
       St q;
-      q.a = u2v((uint32_t)__shfl_down((int)v2u(P.a), 1, 16));
-      q.b = u2v((uint32_t)__shfl_down((int)v2u(P.b), 1, 16));
-      q.c = u2v((uint32_t)__shfl_down((int)v2u(P.c), 1, 16));
-      q.d = u2v((uint32_t)__shfl_down((int)v2u(P.d), 1, 16));
+      q.a = u2v((uint32_t)__shfl_down((int)v2u(P.a), 1, NSB));
+      q.b = u2v((uint32_t)__shfl_down((int)v2u(P.b), 1, NSB));
+      q.c = u2v((uint32_t)__shfl_down((int)v2u(P.c), 1, NSB));
+      q.d = u2v((uint32_t)__shfl_down((int)v2u(P.d), 1, NSB));
       if (c.s == NSB - 1) {  // trellis termination: systematic / parity0 (DEC1), app2 / parity1 (DEC2)
         const int tail = 6 * c.KP + (D2 ? 12 : 0);  // bytes
         short     xt[3], yt[3];
@@ -532,14 +553,14 @@ __device__ __forceinline__ void map16s(const Lane& cin, int wave)
 }  // namespace
 
 template <bool ES>
-__device__ __forceinline__ void tdec16s_body(const TdecArgs& a, int bid)
+__device__ __forceinline__ void body(const TdecArgs& a, int bid)
 {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const int cbw  = lane >> 4;         // block of the workgroup
-  const int s    = lane & 15;         // sub-block
-  const int t2   = wave * 16 + s;     // thread within the block (both sides), 0..31
+  const int cbw  = lane / NSB;        // block of the workgroup
+  const int s    = lane % NSB;        // sub-block
+  const int t2   = wave * NSB + s;    // thread within the block (both sides), 0..2 NSB - 1
   const int K    = (int)a.K;
   const int L    = (int)a.L;
   const int Ls   = (int)a.Ls;
@@ -622,7 +643,7 @@ __device__ __forceinline__ void tdec16s_body(const TdecArgs& a, int bid)
       if (crc_now) {
         const uint8_t* bytes  = reinterpret_cast<const uint8_t*>(c.BITS);
         const int      nbytes = K / 8;
-        const int      bpt    = (nbytes + 31) / 32;
+        const int      bpt    = (nbytes + 2 * NSB - 1) / (2 * NSB);
         const int      b0     = t2 * bpt;
         const int      b1     = min(b0 + bpt, nbytes);
         const bool     crc_a  = a.cbs[cbl].crc_a;
@@ -634,7 +655,7 @@ __device__ __forceinline__ void tdec16s_body(const TdecArgs& a, int bid)
         }
         uint32_t part = b0 < nbytes ? clmul_mod24(crc, (crc_a ? a.xpow_a : a.xpow_b)[nbytes - b1], poly) : 0;
 #pragma unroll
-        for (int off = 1; off < 16; off <<= 1) {
+        for (int off = 1; off < NSB; off <<= 1) {
           part ^= (uint32_t)__shfl_xor((int)part, off, 64);
         }
         if (s == 0) {
@@ -645,7 +666,7 @@ __device__ __forceinline__ void tdec16s_body(const TdecArgs& a, int bid)
         if (ok && !done && live) {
           const uint32_t slot = a.cbs[cbl].slot;
           uint8_t*       out  = a.out + (size_t)slot * a.out_stride;
-          for (int b = t2; b < nbytes; b += 32) {
+          for (int b = t2; b < nbytes; b += 2 * NSB) {
             out[b] = bytes[b];
           }
           if (t2 == 0) {
@@ -666,7 +687,7 @@ __device__ __forceinline__ void tdec16s_body(const TdecArgs& a, int bid)
     const int      cbm   = ES ? (int)a.cbs[cbl].slot : cbl;
     uint8_t*       out   = a.out + (size_t)cbm * (ES ? a.out_stride : K / 8);
     const uint8_t* bytes = reinterpret_cast<const uint8_t*>(c.BITS);
-    for (int b = t2; b < K / 8; b += 32) {
+    for (int b = t2; b < K / 8; b += 2 * NSB) {
       out[b] = bytes[b];
     }
     if (ES && t2 == 0) {
@@ -677,12 +698,12 @@ __device__ __forceinline__ void tdec16s_body(const TdecArgs& a, int bid)
 }
 
 template <bool ES>
-__global__ __launch_bounds__(128, 1) void tdec16s_kernel(TdecArgs a)
+__global__ __launch_bounds__(128, 1) void TDECS_K(kernel)(TdecArgs a)
 {
-  tdec16s_body<ES>(a, blockIdx.x);
+  body<ES>(a, blockIdx.x);
 }
 
-__global__ __launch_bounds__(128, 1) void tdec16s_multi_kernel(const TdecArgs* __restrict__ groups,
+__global__ __launch_bounds__(128, 1) void TDECS_K(multi_kernel)(const TdecArgs* __restrict__ groups,
                                                             const uint32_t* __restrict__ first, int ngroups)
 {
   const uint32_t b  = blockIdx.x;
@@ -696,41 +717,42 @@ __global__ __launch_bounds__(128, 1) void tdec16s_multi_kernel(const TdecArgs* _
     }
   }
   const TdecArgs a = groups[lo];
-  tdec16s_body<false>(a, (int)(b - first[lo]));
+  body<false>(a, (int)(b - first[lo]));
 }
 
-size_t tdec16s_lds_bytes(const TdecArgs& a)
+size_t lds_bytes(const TdecArgs& a)
 {
   const Geo g = geo((int)a.K, (int)a.Ls, (int)((a.L + W - 1) / W));
   return (size_t)CPWG * g.cb_dw * 4;
 }
 
-int tdec16s_cpw() { return CPWG; }
+int cpw() { return CPWG; }
 
-hipError_t tdec16s_launch(const TdecArgs& a, hipStream_t stream)
+hipError_t launch(const TdecArgs& a, hipStream_t stream)
 {
   StageScope timing_scope(ST_TDEC, stream);
   const int    grid = (a.ncb + CPWG - 1) / CPWG;
-  const size_t lds  = tdec16s_lds_bytes(a);
-  tdec_set_last_kernel(a.cbs ? "tdec16s_kernel<true>" : "tdec16s_kernel<false>");
+  const size_t lds  = lds_bytes(a);
+  tdec_set_last_kernel(a.cbs ? TDECS_NAME "kernel<true>" : TDECS_NAME "kernel<false>");
   if (a.cbs) {
-    hipLaunchKernelGGL((tdec16s_kernel<true>), dim3(grid), dim3(128), lds, stream, a);
+    hipLaunchKernelGGL((TDECS_K(kernel)<true>), dim3(grid), dim3(128), lds, stream, a);
   } else {
-    hipLaunchKernelGGL((tdec16s_kernel<false>), dim3(grid), dim3(128), lds, stream, a);
+    hipLaunchKernelGGL((TDECS_K(kernel)<false>), dim3(grid), dim3(128), lds, stream, a);
   }
   return hipGetLastError();
 }
 
-hipError_t tdec16s_multi_launch(const TdecArgs* d_groups, const uint32_t* d_first, int ngroups, uint32_t nblocks,
-                                size_t lds, hipStream_t stream)
+hipError_t multi_launch(const TdecArgs* d_groups, const uint32_t* d_first, int ngroups, uint32_t nblocks, size_t lds,
+                        hipStream_t stream)
 {
   StageScope timing_scope(ST_TDEC, stream);
   if (ngroups == 0 || nblocks == 0) {
     return hipSuccess;
   }
-  tdec_set_last_kernel("tdec16s_multi_kernel");
-  hipLaunchKernelGGL(tdec16s_multi_kernel, dim3(nblocks), dim3(128), lds, stream, d_groups, d_first, ngroups);
+  tdec_set_last_kernel(TDECS_NAME "multi_kernel");
+  hipLaunchKernelGGL(TDECS_K(multi_kernel), dim3(nblocks), dim3(128), lds, stream, d_groups, d_first, ngroups);
   return hipGetLastError();
 }
 
+}  // namespace TDECS_NS
 }  // namespace srsran_amd

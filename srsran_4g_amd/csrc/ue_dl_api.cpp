@@ -209,7 +209,7 @@ int srsran_ue_dl_set_cell(srsran_ue_dl_t* q, srsran_cell_t cell)
   srsran_regs_free(&g->regs_mi[0]);
   srsran_regs_free(&g->regs_mi[1]);
   g->ctrl_cell = g->ctrl_init && (cell.nof_ports == 1 || cell.nof_ports == 2 || cell.nof_ports == 4) &&
-                 cell.cp == SRSRAN_CP_NORM && cell.phich_length == SRSRAN_PHICH_NORM &&
+                 cell.phich_length == SRSRAN_PHICH_NORM &&
                  srsran_regs_init(&g->regs, cell) == SRSRAN_SUCCESS &&
                  srsran_regs_init_opts(&g->regs_mi[0], cell, 0, false) == SRSRAN_SUCCESS &&
                  srsran_regs_init_opts(&g->regs_mi[1], cell, 2, false) == SRSRAN_SUCCESS &&

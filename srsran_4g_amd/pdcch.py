@@ -139,9 +139,9 @@ def lib():
     return L
 
 
-def cell(nof_prb, nof_ports, cell_id, phich_len=0, phich_res=2):
+def cell(nof_prb, nof_ports, cell_id, phich_len=0, phich_res=2, cp=0):
     c = srsran_cell_t()
-    c.nof_prb, c.nof_ports, c.id = nof_prb, nof_ports, cell_id
+    c.nof_prb, c.nof_ports, c.id, c.cp = nof_prb, nof_ports, cell_id, cp
     c.phich_length, c.phich_resources = phich_len, phich_res
     return c
 

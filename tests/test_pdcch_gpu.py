@@ -40,11 +40,11 @@ def control_subframe(nprb, nports, cid, tti, cfi, msgs, nrx, rng, snr_db=20.0):
     return y.astype(np.complex64), np.ascontiguousarray(ce), float(2 * sd * sd)
 
 
-def dci_msgs(nprb, nports, cid, tti, cfi, rng, n=3):
+def dci_msgs(nprb, nports, cid, tti, cfi, rng, n=3, cp=0):
     """random DCIs at non-overlapping UE-search-space locations of random C-RNTIs"""
     from srsran_4g_amd import pdcch as PD
 
-    c = PD.cell(nprb, nports, cid)
+    c = PD.cell(nprb, nports, cid, cp=cp)
     regs = PD.Regs(c)
     nof_cce = regs.q.pdcch_nregs[cfi - 1] // 9
     regs.free()
@@ -93,6 +93,43 @@ def test_pcfich_and_pdcch_llr_vs_reference(mods, nprb, nports, cid, tti, cfi):
             np.testing.assert_allclose(gllr, rllr, rtol=2e-3, atol=2e-3 * np.abs(rllr).max())
     finally:
         ctl.free()
+
+
+@pytest.mark.parametrize("nprb,nports,cid,tti,cfi", [c for c in CASES if c[0] in (6, 50, 100)])
+def test_extended_cp_control_vs_reference(mods, nprb, nports, cid, tti, cfi):
+    """extended-CP cells (regs.c:587-617): CFI, PCFICH correlation, the control-region LLRs and every
+    transmitted DCI decoded from them, against the reference built for the same cell"""
+    PD, U = mods
+    rng = np.random.default_rng(nprb * 11 + cid)
+    nrx = 2
+    ref = P.Ref()
+    ref.set_cp(1)
+    try:
+        msgs, nof_cce = dci_msgs(nprb, nports, cid, tti, cfi, rng, cp=1)
+        y, ce, noise = control_subframe(nprb, nports, cid, tti, cfi, [m[:4] for m in msgs], nrx, rng)
+        rcfi, rcorr, rllr = ref.ctrl_rx(nprb, nports, cid, tti, y, ce, noise)
+        ctl = PD.Control(PD.cell(nprb, nports, cid, cp=1), nrx)
+        try:
+            gcfi, gcorr, _ = ctl.pcfich(y, ce, noise, tti)
+            assert gcfi == rcfi == cfi
+            assert abs(gcorr - rcorr) <= 1e-4 * max(1.0, abs(rcorr))
+            gllr = ctl.pdcch_llr(y, ce, noise, tti, gcfi)
+            assert gllr.size == rllr.size == 72 * nof_cce
+            if nports >= 2:
+                assert np.array_equal(gllr, rllr)
+            else:
+                np.testing.assert_allclose(gllr, rllr, rtol=2e-3, atol=2e-3 * np.abs(rllr).max())
+            ctl.set_llr(cfi, rllr)
+            fl = [(m[1], m[2], m[4]) for m in msgs]
+            got = ctl.decode(tti, cfi, fl)
+            for (bits, L, n, rnti, f), (nb, pl, rem, corr) in zip(msgs, got):
+                want = ref.pdcch_decode(tti, cfi, rllr, L, n, f)
+                assert (nb, rem) == (want[0], want[2]) and np.array_equal(pl, want[1])
+                assert nb == len(bits) and rem == rnti and np.array_equal(pl, bits)
+        finally:
+            ctl.free()
+    finally:
+        ref.set_cp(0)
 
 
 @pytest.mark.parametrize("nprb,nports,cid,tti,cfi", CASES[:5] + CASES[7:8])

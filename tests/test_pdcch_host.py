@@ -38,6 +38,25 @@ def test_regs_tables_match_reference(nprb, nports, cid, ng):
 
 
 @needs_ref
+@pytest.mark.parametrize("nprb,nports,cid,ng", CELLS)
+def test_regs_tables_extended_cp_match_reference(nprb, nports, cid, ng):
+    """extended-CP cells (regs.c:587-617: symbol 3 of the 4-symbol control region carries CRS)"""
+    ref = P.Ref()
+    ref.set_cp(1)
+    try:
+        pc, pd = ref.regs_tables(nprb, nports, cid, 0, ng)
+    finally:
+        ref.set_cp(0)
+    r = PD.Regs(PD.cell(nprb, nports, cid, 0, ng, cp=1))
+    try:
+        assert np.array_equal(r.pcfich_re(), pc)
+        for cfi in (1, 2, 3):
+            assert np.array_equal(r.pdcch_re(cfi), pd[cfi - 1]), cfi
+    finally:
+        r.free()
+
+
+@needs_ref
 @pytest.mark.parametrize("mi", [0, 2])
 @pytest.mark.parametrize("nprb,nports,cid,ng", CELLS[:8])
 def test_regs_tables_phich_mi_match_reference(nprb, nports, cid, ng, mi):

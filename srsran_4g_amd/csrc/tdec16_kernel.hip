@@ -782,6 +782,11 @@ bool tdec8s_eligible(int nsb, const TdecArgs& a)
          a.ncb >= tdec16s_min_cb();
 }
 
+bool tdec1s_eligible(int nsb, const TdecArgs& a)
+{
+  return nsb == 1 && a.n_start == 0 && a.state == nullptr && a.ncb >= tdec16s_min_cb();
+}
+
 size_t tdec16_lds_bytes(const TdecArgs& a)
 {
   const Geo16 g = geo16((int)a.K, (int)a.Ls, (int)((a.L + W - 1) / W));

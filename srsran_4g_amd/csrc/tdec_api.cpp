@@ -749,11 +749,14 @@ int srsran_tdec_gpu_run_multi(uint32_t              nof_groups,
       cls_cb += nof_cb[g];
     }
     // 2 single lane (tdecs_kernel.hip), 1 lane pair (16 sub-blocks only), 0 quad
-    const int kind = !layout_sb || cls_nsb[ci] == 1 ? 0
+    const int kind = cls_nsb[ci] == 1               ? (cls_cb >= tdec16s_min_cb() ? 2 : 0)  // natural layout
+                     : !layout_sb                   ? 0
                      : cls_nsb[ci] == 16            ? tdec16_choice(cls_cb)
                                                     : (cls_cb >= tdec16s_min_cb() ? 2 : 0);
-    const bool s16 = cls_nsb[ci] == 16;
-    const int  cpw = kind == 2 ? (s16 ? tdecs16::cpw() : tdecs8::cpw()) : kind == 1 ? tdec16_cpw() : tdec_cpw(cls_nsb[ci]);
+    const int  nsbc = cls_nsb[ci];
+    const int  cpw  = kind == 2   ? (nsbc == 16 ? tdecs16::cpw() : nsbc == 8 ? tdecs8::cpw() : tdecs1::cpw())
+                      : kind == 1 ? tdec16_cpw()
+                                  : tdec_cpw(nsbc);
     const size_t   n     = gs.size();
     const size_t   abyte = n * sizeof(TdecArgs);
     const size_t   need  = abyte + n * sizeof(uint32_t);
@@ -795,7 +798,9 @@ int srsran_tdec_gpu_run_multi(uint32_t              nof_groups,
       ha[k]            = a;
       hf[k]            = nblk;
       nblk += (nof_cb[g] + cpw - 1) / cpw;
-      lds = std::max(lds, kind == 2   ? (s16 ? tdecs16::lds_bytes(a) : tdecs8::lds_bytes(a))
+      lds = std::max(lds, kind == 2   ? (nsbc == 16  ? tdecs16::lds_bytes(a)
+                                         : nsbc == 8 ? tdecs8::lds_bytes(a)
+                                                     : tdecs1::lds_bytes(a))
                           : kind == 1 ? tdec16_lds_bytes(a)
                                       : tdec_lds_bytes(c->nsb, a.xyw, a.M));
     }
@@ -806,8 +811,9 @@ int srsran_tdec_gpu_run_multi(uint32_t              nof_groups,
     m.used = true;
     const TdecArgs* dg = reinterpret_cast<const TdecArgs*>(m.d_stage);
     const uint32_t* df = reinterpret_cast<const uint32_t*>(m.d_stage + abyte);
-    if ((kind == 2   ? (s16 ? tdecs16::multi_launch(dg, df, (int)n, nblk, lds, st)
-                            : tdecs8::multi_launch(dg, df, (int)n, nblk, lds, st))
+    if ((kind == 2   ? (nsbc == 16  ? tdecs16::multi_launch(dg, df, (int)n, nblk, lds, st)
+                        : nsbc == 8 ? tdecs8::multi_launch(dg, df, (int)n, nblk, lds, st)
+                                    : tdecs1::multi_launch(dg, df, (int)n, nblk, lds, st))
          : kind == 1 ? tdec16_multi_launch(dg, df, (int)n, nblk, lds, st)
                      : tdec_multi_launch(cls_nsb[ci], dg, df, (int)n, nblk, lds, st)) != hipSuccess) {
       ret = SRSRAN_ERROR;

@@ -827,6 +827,9 @@ hipError_t tdec_launch(int nsb, const TdecArgs& a, hipStream_t stream)
   if (tdec8s_eligible(nsb, a)) {
     return tdecs8::launch(a, stream);
   }
+  if (tdec1s_eligible(nsb, a)) {
+    return tdecs1::launch(a, stream);
+  }
   switch (nsb) {
     case 16:
       return launch<16>(a, stream);

@@ -1,6 +1,6 @@
 """The single-lane decoder of the 8-sub-block window class (tdecs_kernel.hip built with TDECS_NSB=8: every K
 from 408 to 800, the SSE 8-block window decoder of turbodecoder_win.h) forced onto every batch size
-(srsran_tdec_gpu_set_single_threshold(0)) against the oracle decoder: all 27 sizes with partly empty
+(srsran_tdec_gpu_set_single_threshold(0)) against the oracle decoder: all 32 sizes with partly empty
 workgroups, several half-iteration counts, the fused multi-size launch and DL-SCH transport blocks with
 CRC early stop over HARQ."""
 import numpy as np
@@ -29,7 +29,7 @@ def ora():
 
 def test_all_8class_sizes_bit_exact(ora):
     from srsran_4g_amd import tdec
-    assert len(K8) == 27 and all(tdec.nof_subblocks(k) == 8 for k in K8)
+    assert len(K8) == 32 and all(tdec.nof_subblocks(k) == 8 for k in K8)
     rng = np.random.default_rng(801)
     dec = tdec.TurboDecoder()
     bad = []

@@ -5,7 +5,7 @@ launches of one 16-sub-block-class decoder on one workload, HIP events on the la
 
 k6144: K = 6144 x batch blocks (srsran_tdec_gpu_run_batch); all188: every K >= 816 x batch blocks in one
 fused srsran_tdec_gpu_run_multi call (the 16-sub-block class of the bench's all-188 step); class8: the
-same for the 27 sizes of the 8-sub-block class (408 <= K <= 800).  Inputs: AWGN
+same for the 32 sizes of the 8-sub-block class (408 <= K <= 800).  Inputs: AWGN
 blocks at Eb/No 4 dB (the bench's), 8 distinct blocks per size tiled.  8 half-iterations."""
 import argparse
 import json

@@ -34,13 +34,13 @@ def main():
     lib = tdec.load_library()
     lib.srsran_tdec_gpu_set_pair_threshold(pair_min)
     lib.srsran_tdec_gpu_set_single_threshold(single_min)
-    nsb = {"class8": 8, "class1": 1}.get(a.workload, 16)
+    nsb = {"class8": 8, "class1": 0}.get(a.workload, 16)  # srsran_tdec_autoimp_get_subblocks: 0 = generic
     Ks = [6144] if a.workload == "k6144" else [k for k in tdec.CB_SIZES if tdec.nof_subblocks(k) == nsb]
     rng = np.random.default_rng(5)
     ins, outs = [], []
     for K in Ks:
         _, llr = SY.make_llrs(K, 4.0, rng, 8)
-        sb = SY.natural_to_sb(K, llr) if nsb > 1 else llr
+        sb = SY.natural_to_sb(K, llr) if nsb else llr
         ins.append(torch.from_numpy(np.ascontiguousarray(np.tile(sb, (a.batch // 8 + 1, 1))[: a.batch])).cuda())
         outs.append(torch.empty((a.batch, K // 8), dtype=torch.uint8, device="cuda"))
     s = torch.cuda.current_stream()

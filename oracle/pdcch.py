@@ -36,8 +36,7 @@ class Ref:
         L = ctypes.CDLL(REF_SO, mode=os.RTLD_LAZY)
         L.ref_regs_tables.argtypes = [u32, u32, u32, ctypes.c_int, ctypes.c_int, u32p, u32p, u32, u32p]
         L.ref_regs_tables_mi.argtypes = [u32, u32, u32, ctypes.c_int, ctypes.c_int, u32, u32p, u32p, u32, u32p]
-        L.ref_set_cp.argtypes = [ctypes.c_int]
-        L.ref_set_cp(0)
+        L.ref_set_cp.argtypes = [ctypes.c_int]  # process-global in the harness (normal CP until set)
         L.ref_ctrl_tx.argtypes = [u32, u32, u32, ctypes.c_int, ctypes.c_int, u32, u32, u32, u8p, u32p, u32p, u32p,
                                   u16p, f32p]
         L.ref_ctrl_rx.argtypes = [u32, u32, u32, ctypes.c_int, ctypes.c_int, u32, u32, f32p, f32p, ctypes.c_float,

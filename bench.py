@@ -130,9 +130,9 @@ def parse():
     p.add_argument("--pdsch-steps", type=int, default=5,
                    help="all188: timed steps of the C3 PDSCH chain reported in the same line (0 = skip)")
     p.add_argument("--pdsch-cpu-seconds", type=float, default=4.0, help="all188: CPU baseline budget of the PDSCH part")
-    p.add_argument("--pdsch-low-snr", type=float, default=20.0,
-                   help="all188: SNR (dB) of a second, shorter PDSCH chain run where the turbo decoder needs "
-                        "several half-iterations (0 = skip)")
+    p.add_argument("--pdsch-low-snr", type=float, default=17.0,
+                   help="all188: SNR (dB) of a second, shorter PDSCH chain run at the operating point where the "
+                        "turbo decoder needs ~5 half-iterations and ~10%% of TBs fail (0 = skip)")
     p.add_argument("--tdec16", choices=["auto", "single", "pair", "quad"], default="auto",
                    help="decoder of the 16-sub-block class: the library's choice by batch size, or forced")
     p.add_argument("--cpu-worker", type=int, default=None, help=argparse.SUPPRESS)
@@ -1272,11 +1272,11 @@ def main():
     device = torch.device("cuda", local)
     if not tdec.gpu_available():
         raise RuntimeError("bench: HIP device not visible to libsrsran_4g_amd")
-    if args.tdec16 != "auto":  # srsran_tdec_gpu_set_pair_threshold / _single_threshold
+    if args.tdec16 != "auto":  # srsran_tdec_gpu_set_pair_threshold / _class_single_threshold(16, .)
         never = 1 << 30
         pair_min, single_min = {"single": (0, 0), "pair": (0, never), "quad": (never, never)}[args.tdec16]
         tdec.load_library().srsran_tdec_gpu_set_pair_threshold(pair_min)
-        tdec.load_library().srsran_tdec_gpu_set_single_threshold(single_min)
+        tdec.load_library().srsran_tdec_gpu_set_class_single_threshold(16, single_min)
     if args.workload in ("dlsch", "ulsch"):
         return run_dlsch(args, torch, dist, world, rank, device)
     if args.workload == "pusch":

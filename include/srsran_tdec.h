@@ -144,8 +144,8 @@ int srsran_tdec_gpu_available(void);
 /* Name of the decoder kernel used for long_cb (for profiling reports), or NULL. */
 const char* srsran_tdec_gpu_kernel_name(uint32_t long_cb);
 
-/* Name of the kernel a batch of nof_cb blocks of long_cb on the SB layout runs (the lane-pair
-   decoder of K >= 816 from 1024 blocks a launch), for profiling reports. */
+/* Name of the kernel a batch of nof_cb blocks of long_cb on the SB layout runs under the current
+   thresholds below, for profiling reports. */
 const char* srsran_tdec_gpu_kernel_name_batch(uint32_t long_cb, uint32_t nof_cb);
 
 /* Name of the last turbo-decoder kernel the calling thread launched (any API: plain, multi-size,
@@ -153,13 +153,21 @@ const char* srsran_tdec_gpu_kernel_name_batch(uint32_t long_cb, uint32_t nof_cb)
 const char* srsran_tdec_gpu_last_kernel(void);
 
 /* Blocks per launch (or per fused class launch) from which the 16-sub-block class runs the lane-pair
-   decoder (default 1024: below it the quad decoder fills the chip better).  Process-wide. */
+   decoder (default 512: below it the quad decoder fills the chip better).  Process-wide. */
 void     srsran_tdec_gpu_set_pair_threshold(uint32_t nof_cb);
 uint32_t srsran_tdec_gpu_get_pair_threshold(void);
-/* Blocks per launch from which the 16-sub-block class runs the single-lane decoder (one lane per
-   sub-block, 4 blocks a workgroup: the throughput mapping) instead of the lane pair.  Process-wide. */
+/* Blocks per launch (or per fused class launch) from which a decoder class runs its single-lane decoder
+   (one lane per sub-block / block, 64 lanes a wave: the throughput mapping) instead of the lane pair /
+   quad decoder.  nof_subblocks: 16 (default 1024), 8 (default 4096) or 0 = the generic class K <= 400
+   (default UINT32_MAX, i.e. never: its quad decoder is faster at every batch size measured).
+   Process-wide. */
+void     srsran_tdec_gpu_set_class_single_threshold(uint32_t nof_subblocks, uint32_t nof_cb);
+uint32_t srsran_tdec_gpu_get_class_single_threshold(uint32_t nof_subblocks);
+/* Shorthands: the 16- and 8-sub-block classes together (get: the 16 class), the generic class. */
 void     srsran_tdec_gpu_set_single_threshold(uint32_t nof_cb);
 uint32_t srsran_tdec_gpu_get_single_threshold(void);
+void     srsran_tdec_gpu_set_generic_single_threshold(uint32_t nof_cb);
+uint32_t srsran_tdec_gpu_get_generic_single_threshold(void);
 
 #ifdef __cplusplus
 }

@@ -14,6 +14,7 @@
 #include "../../include/srsran_pusch.h"
 #include "llr_kernel.h"
 #include "pusch_kernel.h"
+#include "ulsch_batch.h"
 
 namespace srsran_amd {
 int         ulsch_decode_dev(srsran_sch_t* q, srsran_pusch_cfg_t* cfg, int16_t* d_q, const uint8_t* d_c, uint8_t* data,
@@ -294,10 +295,6 @@ struct PuschGpu {
   size_t      g_cap  = 0;
   uint8_t*    d_data = nullptr;  // batch: decoded TBs of the UEs without UCI
   size_t      data_cap = 0;
-  int32_t*    d_res  = nullptr;  // batch: decode_tb results / average iterations
-  size_t      res_cap = 0;
-  uint8_t*    h_stage = nullptr; // batch: pinned host staging of results + payloads (one D2H copy)
-  size_t      stage_cap = 0;
 };
 
 uint32_t pusch_seed(uint16_t rnti, uint32_t nslot, uint32_t cell_id)  // sequences.c:119-122
@@ -652,8 +649,6 @@ void srsran_pusch_free(srsran_pusch_t* q)
     hipFree(g->d_bce);
     hipFree(g->d_g);
     hipFree(g->d_data);
-    hipFree(g->d_res);
-    hipHostFree(g->h_stage);
     delete g;
   }
   srsran_sch_free(&q->ul_sch);
@@ -894,109 +889,47 @@ int srsran_pusch_gpu_decode_batch(srsran_pusch_t*              q,
     }
   }
 
-  // ---- UL-SCH.  UEs without UCI: one batched de-interleaver + decode_tb (srsran_ulsch_gpu_decode_batch);
-  // with UCI: srsran_ulsch_decode's sequence each (its CQI size may depend on the decoded RI) ----
-  int                                rc = SRSRAN_SUCCESS;
-  std::vector<uint32_t>              plain;
-  std::vector<srsran_ulsch_gpu_tb_t> tb;
-  size_t                             g_tot = 0, data_tot = 0;
-  std::vector<size_t>                g_off(nof_ue), data_off(nof_ue);
+  // ---- UL-SCH: every UE, with or without UCI, through the batched srsran_ulsch_decode (ulsch_batch.h):
+  // one ACK/RI launch, one de-interleaver launch, one CQI launch and one decode_tb batch ----
+  int                       rc = SRSRAN_SUCCESS;
+  size_t                    g_tot = 0, data_tot = 0;
+  std::vector<size_t>       g_off(nof_ue), data_off(nof_ue);
   for (uint32_t i = 0; i < nof_ue; i++) {
-    srsran_pusch_cfg_t* cfg = ues[i].cfg;
-    if (any_uci(cfg) || cfg->grant.tb.tbs <= 0) {
-      continue;
-    }
-    srsran_cbsegm_t sg;
-    if (srsran_cbsegm(&sg, (uint32_t)cfg->grant.tb.tbs) || !cfg->softbuffers.rx) {
-      return SRSRAN_ERROR_INVALID_INPUTS;
-    }
-    cfg->K_segm = sg.C1 * sg.K1 + sg.C2 * sg.K2;
-    plain.push_back(i);
-    g_off[i]    = g_tot;
-    data_off[i] = data_tot;
+    const srsran_pusch_cfg_t* cfg = ues[i].cfg;
+    g_off[i]                      = g_tot;
+    data_off[i]                   = data_tot;
     g_tot += (cfg->grant.tb.nof_bits + 7) & ~7u;
-    data_tot += ((uint32_t)cfg->grant.tb.tbs / 8 + 64 + 15) & ~15u;
+    data_tot += cfg->grant.tb.tbs > 0 ? (((uint32_t)cfg->grant.tb.tbs / 8 + 64 + 15) & ~15u) : 0;
   }
-  if (!plain.empty()) {
-    if (!grow((void**)&g->d_g, &g->g_cap, g_tot * sizeof(int16_t)) || !grow((void**)&g->d_data, &g->data_cap, data_tot) ||
-        !grow((void**)&g->d_res, &g->res_cap, 2 * plain.size() * sizeof(int32_t))) {
-      return SRSRAN_ERROR;
-    }
-    uint32_t maxit = 0;
-    for (uint32_t i : plain) {
-      srsran_pusch_cfg_t* cfg = ues[i].cfg;
-      srsran_ulsch_gpu_tb_t t;
-      memset(&t, 0, sizeof(t));
-      t.tbs        = (uint32_t)cfg->grant.tb.tbs;
-      t.Qm         = srsran_mod_bits_x_symbol(cfg->grant.tb.mod);
-      t.rv         = (uint32_t)cfg->grant.tb.rv;
-      t.nof_e_bits = cfg->grant.tb.nof_bits;
-      t.nof_symb   = cfg->grant.nof_symb;
-      t.d_q_bits   = g->d_q + q_off[i];
-      t.d_g_bits   = g->d_g + g_off[i];
-      t.d_data     = g->d_data + data_off[i];
-      t.softbuffer = cfg->softbuffers.rx;
-      t.new_data   = ues[i].new_data ? 1 : 0;
-      tb.push_back(t);
-      maxit = std::max(maxit, cfg->max_nof_iterations);
-    }
-    srsran_sch_set_max_noi(&q->ul_sch, maxit);
-    int32_t* d_r = g->d_res;
-    float*   d_a = (float*)(g->d_res + plain.size());
-    if (srsran_ulsch_gpu_decode_batch(&q->ul_sch, (uint32_t)plain.size(), tb.data(), d_r, d_a, st) != SRSRAN_SUCCESS) {
-      return SRSRAN_ERROR;
-    }
-    // results and payloads back in one copy through pinned staging
-    const size_t rbytes = 2 * plain.size() * sizeof(int32_t), sneed = rbytes + data_tot;
-    if (sneed > g->stage_cap) {
-      hipHostFree(g->h_stage);
-      g->h_stage   = nullptr;
-      g->stage_cap = 0;
-      if (hipHostMalloc((void**)&g->h_stage, sneed, hipHostMallocDefault) != hipSuccess) {
-        return SRSRAN_ERROR;
-      }
-      g->stage_cap = sneed;
-    }
-    if (hipMemcpyAsync(g->h_stage, g->d_res, rbytes, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipMemcpyAsync(g->h_stage + rbytes, g->d_data, data_tot, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess) {
-      return SRSRAN_ERROR;
-    }
-    const int32_t* hr = (const int32_t*)g->h_stage;
-    for (uint32_t i : plain) {
-      if (res[i].data) {
-        memcpy(res[i].data, g->h_stage + rbytes + data_off[i], (size_t)ues[i].cfg->grant.tb.tbs / 8);
-      }
-    }
-    for (size_t k = 0; k < plain.size(); k++) {
-      const uint32_t i = plain[k];
-      float          avg;
-      memcpy(&avg, &hr[plain.size() + k], sizeof(float));
-      res[i].crc                  = hr[k] == 0;
-      res[i].avg_iterations_block = avg;
-      res[i].evm                  = NAN;
+  if (!grow((void**)&g->d_g, &g->g_cap, g_tot * sizeof(int16_t)) || !grow((void**)&g->d_data, &g->data_cap, data_tot + 16)) {
+    return SRSRAN_ERROR;
+  }
+  std::vector<UlschBatchUe> ub(nof_ue);
+  for (uint32_t i = 0; i < nof_ue; i++) {
+    UlschBatchUe& u = ub[i];
+    memset(&u, 0, sizeof(u));
+    u.cfg      = ues[i].cfg;
+    u.d_q      = g->d_q + q_off[i];
+    u.d_c      = any_uci(ues[i].cfg) ? g->d_c + c_off[i] : nullptr;
+    u.d_g      = g->d_g + g_off[i];
+    u.d_data   = g->d_data + data_off[i];
+    u.new_data = ues[i].new_data;
+    u.data     = res[i].data;
+    u.uci      = &res[i].uci;
+    if (!any_uci(ues[i].cfg) && ues[i].cfg->grant.tb.tbs > 0) {
       memset(&res[i].uci, 0, sizeof(res[i].uci));
-      ues[i].cfg->last_O_cqi = (uint32_t)srsran_cqi_size(&ues[i].cfg->uci_cfg.cqi);
-      q->ul_sch.avg_iterations = avg;
     }
+  }
+  if (ulsch_decode_batch_dev(&q->ul_sch, nof_ue, ub.data(), g->d_data, data_tot, st) != SRSRAN_SUCCESS) {
+    return SRSRAN_ERROR;
   }
   for (uint32_t i = 0; i < nof_ue; i++) {
-    srsran_pusch_cfg_t* cfg = ues[i].cfg;
-    if (!(any_uci(cfg) || cfg->grant.tb.tbs <= 0)) {
-      continue;
-    }
-    if (ues[i].new_data && cfg->softbuffers.rx && cfg->grant.tb.tbs > 0) {
-      srsran_softbuffer_rx_reset_tbs(cfg->softbuffers.rx, (uint32_t)cfg->grant.tb.tbs);
-    }
-    srsran_sch_set_max_noi(&q->ul_sch, cfg->max_nof_iterations);
-    const int ret = ulsch_decode_dev(&q->ul_sch, cfg, g->d_q + q_off[i], any_uci(cfg) ? g->d_c + c_off[i] : nullptr,
-                                     res[i].data, &res[i].uci);
-    res[i].crc                  = ret == 0;
-    res[i].avg_iterations_block = q->ul_sch.avg_iterations;
+    res[i].crc                  = ub[i].ret == 0;
+    res[i].avg_iterations_block = ub[i].avg;
     res[i].evm                  = NAN;
-    cfg->last_O_cqi             = (uint32_t)srsran_cqi_size(&cfg->uci_cfg.cqi);
-    if (ret < 0 && ret != SRSRAN_ERROR) {
-      rc = ret;
+    ues[i].cfg->last_O_cqi      = (uint32_t)srsran_cqi_size(&ues[i].cfg->uci_cfg.cqi);
+    if (ub[i].ret < 0 && ub[i].ret != SRSRAN_ERROR) {
+      rc = ub[i].ret;
     }
   }
   std::vector<ChestUlOut> outs(nof_ue);

@@ -26,6 +26,7 @@
 #include "tdec_kernel.h"
 #include "enc_kernel.h"
 #include "uci_kernel.h"
+#include "ulsch_batch.h"
 
 using namespace srsran_amd;
 
@@ -285,6 +286,10 @@ struct SchCtx {
   size_t      uldesc_cap = 0;
   uint8_t*    d_uci = nullptr;     // srsran_ulsch_decode with UCI: descriptors, results, sequence
   size_t      uci_cap = 0;
+  uint8_t*    d_ubs = nullptr;     // the batched UL-SCH receive: descriptors and results (device)
+  size_t      dubs_cap = 0;
+  uint8_t*    h_ubs = nullptr;     // its pinned staging
+  size_t      hubs_cap = 0;
   uint8_t*    d_enc = nullptr;     // DL-SCH encode: descriptors, TB CRCs, unpacked e bits, staging
   size_t      enc_cap = 0;
 };
@@ -983,6 +988,8 @@ void srsran_sch_free(srsran_sch_t* q)
       hipEventDestroy(x->uldesc_used);
     }
     hipFree(x->d_uci);
+    hipFree(x->d_ubs);
+    hipHostFree(x->h_ubs);
     hipFree(x->d_enc);
     delete x;
   }
@@ -1393,6 +1400,144 @@ int srsran_cqi_value_unpack(srsran_cqi_cfg_t* cfg, uint8_t buff[SRSRAN_CQI_MAX_B
 }
 
 // ---------------- UL-SCH receive with UCI (sch.c:994-1193) ----------------
+// The host part shared by srsran_ulsch_decode and the batched path: segmentation, sizes, Q'_ACK / Q'_RI.
+struct UlsPlan {
+  srsran_cbsegm_t s;
+  uint32_t        nb, Qm, nsymb, H, rows, nack, ack_Qp, ri_Qp;
+  bool            uci, hl_ri, need_c;
+};
+
+static int ulsch_plan(srsran_pusch_cfg_t* cfg, UlsPlan* p)
+{
+  srsran_cbsegm_t& s = p->s;
+  if (srsran_cbsegm(&s, (uint32_t)cfg->grant.tb.tbs)) {
+    fprintf(stderr, "[srsran_sch] Error computing segmentation for TBS=%d\n", cfg->grant.tb.tbs);
+    return SRSRAN_ERROR;
+  }
+  p->nb       = cfg->grant.tb.nof_bits;
+  p->Qm       = srsran_mod_bits_x_symbol(cfg->grant.tb.mod);
+  cfg->K_segm = s.C1 * s.K1 + s.C2 * s.K2;
+  if (p->Qm == 0) {
+    fprintf(stderr, "[srsran_sch] Invalid modulation\n");
+    return SRSRAN_ERROR;
+  }
+  p->nsymb = cfg->grant.nof_symb;
+  if (p->nsymb == 0 || p->nsymb > 14 || p->nb % p->Qm || p->Qm > 8) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  p->H                  = p->nb / p->Qm;
+  p->rows               = p->H / p->nsymb;
+  srsran_cqi_cfg_t& cq  = cfg->uci_cfg.cqi;
+  p->nack               = srsran_uci_cfg_total_ack(&cfg->uci_cfg);
+  p->uci                = p->nack > 0 || cq.ri_len > 0 || cq.data_enable;
+  // ---- uci_decode_ri_ack, host part (sch.c:1023-1120): Q'_ACK, Q'_RI ----
+  p->hl_ri = cq.data_enable && cq.type == SRSRAN_CQI_TYPE_SUBBAND_HL && cq.ri_len;
+  if (p->hl_ri) {
+    cq.rank_is_not_one = false;  // RI = 1 assumed for the RI / ACK sizes (36.212 5.2.4.1)
+  }
+  const uint32_t cqi_len0 = (uint32_t)srsran_cqi_size(&cq);
+  p->ack_Qp = p->ri_Qp = 0;
+  if (p->nack > 0) {
+    if (p->nack > SRSRAN_UCI_MAX_ACK_BITS) {
+      return SRSRAN_ERROR_INVALID_INPUTS;
+    }
+    float beta = beta_harq(cfg->uci_offset.I_offset_ack);
+    if (cfg->grant.tb.tbs == 0) {
+      beta /= beta_cqi(cfg->uci_offset.I_offset_cqi);
+    }
+    p->ack_Qp = qprime_ri_ack(cfg->K_segm, cfg->grant.L_prb, p->nsymb, p->nack, cqi_len0, beta);
+  }
+  if (cq.ri_len > 0) {
+    if (cq.ri_len > 4) {
+      return SRSRAN_ERROR_INVALID_INPUTS;
+    }
+    float beta = beta_ri(cfg->uci_offset.I_offset_ri);
+    if (cfg->grant.tb.tbs == 0) {
+      beta /= beta_cqi(cfg->uci_offset.I_offset_cqi);
+    }
+    p->ri_Qp = qprime_ri_ack(cfg->K_segm, cfg->grant.L_prb, p->nsymb, cq.ri_len, cqi_len0, beta);
+  }
+  // the ACK / RI rows are counted up from the bottom of the interleaver: positions past its top
+  // (uci.c:378-386 "Error interleaving") are refused
+  if (p->ack_Qp > 4 * p->rows || p->ri_Qp > 4 * p->rows || p->ri_Qp > p->H) {
+    fprintf(stderr, "[srsran_sch] UCI does not fit the PUSCH interleaver (Q'_ACK=%u Q'_RI=%u rows=%u)\n", p->ack_Qp,
+            p->ri_Qp, p->rows);
+    return SRSRAN_ERROR;
+  }
+  p->need_c = (p->nack == 1 && p->ack_Qp > 0) || (cq.ri_len == 1 && p->ri_Qp > 0);
+  return SRSRAN_SUCCESS;
+}
+
+// The de-interleaver descriptor: it skips the RI cells, column set[c] holding the RI indices
+// q = 3c mod 4 (mod 4)
+static UlDeint ulsch_deint_desc(int16_t* d_q, int16_t* d_g, const UlsPlan& p)
+{
+  UlDeint d = {d_q, d_g, p.rows, p.nsymb, p.Qm, {}, -1};
+  if (p.ri_Qp > 0) {
+    static const uint8_t kRiNorm[4] = {1, 4, 7, 10}, kRiExt[4] = {0, 3, 5, 8};
+    const uint8_t*       set        = p.nsymb > 10 ? kRiNorm : kRiExt;
+    int64_t              last       = -1;  // the largest RI position in q order
+    for (uint32_t c = 0; c < 4; c++) {
+      const uint32_t m = (3 * c) % 4, n = p.ri_Qp > m ? (p.ri_Qp - m + 3) / 4 : 0;
+      d.ri_rows[set[c]] = (uint16_t)n;
+      if (n > 0) {
+        last = std::max<int64_t>(last, (int64_t)(p.rows - 1) * p.Qm + (int64_t)set[c] * p.rows * p.Qm + p.Qm - 1);
+      }
+    }
+    uint32_t first = 0;  // the first non-RI column of row 0 holds g[0] in its own right
+    while (first < p.nsymb && d.ri_rows[first] >= p.rows) {
+      first++;
+    }
+    d.g0_src = (int32_t)std::max<int64_t>(last, (int64_t)first * p.rows * p.Qm);
+  }
+  return d;
+}
+
+// CQI (sch.c:1160-1183): its size may depend on the RI just decoded (ri: the decoded RI, or -1 when
+// not needed)
+static int ulsch_cqi_plan(srsran_pusch_cfg_t* cfg, const UlsPlan& p, int ri, uint32_t* cqi_len, uint32_t* cqi_Qp)
+{
+  srsran_cqi_cfg_t& cq = cfg->uci_cfg.cqi;
+  *cqi_len = *cqi_Qp = 0;
+  if (!cq.data_enable) {
+    if (p.hl_ri) {
+      cq.rank_is_not_one = false;
+    }
+    return SRSRAN_SUCCESS;
+  }
+  if (p.hl_ri) {
+    cq.rank_is_not_one = ri > 0;
+  }
+  const int len = srsran_cqi_size(&cq);
+  if (len <= 0 || len > (int)UCI_MAX_CQI_BITS) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  *cqi_len = (uint32_t)len;
+  *cqi_Qp  = qprime_cqi(cfg->K_segm, cfg->grant.L_prb, p.nsymb, (uint32_t)len, beta_cqi(cfg->uci_offset.I_offset_cqi),
+                        p.ri_Qp);
+  return (uint64_t)*cqi_Qp + p.ri_Qp > p.H ? SRSRAN_ERROR : SRSRAN_SUCCESS;
+}
+
+// The decoded UCI into the caller's srsran_uci_value_t (sch.c:1084-1117, uci.c)
+static void ulsch_uci_out(srsran_pusch_cfg_t* cfg, const UlsPlan& p, const UciOut& o, srsran_uci_value_t* uci)
+{
+  srsran_cqi_cfg_t& cq = cfg->uci_cfg.cqi;
+  if (p.nack > 0) {
+    memcpy(uci->ack.ack_value, o.ack, std::min<uint32_t>(p.nack, SRSRAN_UCI_MAX_ACK_BITS));
+    uci->ack.valid = o.ack_valid != 0;
+  }
+  if (cq.ri_len > 0) {
+    uci->ri = o.ri[0];
+  }
+  if (cq.data_enable) {
+    uci->cqi.data_crc = o.cqi_crc != 0;
+    srsran_cqi_value_unpack(&cq, const_cast<uint8_t*>(o.cqi), &uci->cqi);
+  }
+  if (p.hl_ri) {
+    cq.rank_is_not_one = uci->ri > 0;  // sch.c:1112-1117
+  }
+}
+
 // One device scratch block per call: the UCI / de-interleaver descriptors, the UCI results and
 // the unpacked scrambling sequence.
 struct UlsUciScratch {
@@ -1418,65 +1563,13 @@ static int ulsch_decode_impl(srsran_sch_t*       q,
   if (!q || !q->gpu || !cfg || (!h_q && !d_q_ext)) {
     return SRSRAN_ERROR_INVALID_INPUTS;
   }
-  srsran_cbsegm_t s;
-  if (srsran_cbsegm(&s, (uint32_t)cfg->grant.tb.tbs)) {
-    fprintf(stderr, "[srsran_sch] Error computing segmentation for TBS=%d\n", cfg->grant.tb.tbs);
-    return SRSRAN_ERROR;
+  UlsPlan   p;
+  const int prc = ulsch_plan(cfg, &p);
+  if (prc != SRSRAN_SUCCESS) {
+    return prc;
   }
-  const uint32_t nb = cfg->grant.tb.nof_bits, Qm = srsran_mod_bits_x_symbol(cfg->grant.tb.mod);
-  cfg->K_segm       = s.C1 * s.K1 + s.C2 * s.K2;
-  if (Qm == 0) {
-    fprintf(stderr, "[srsran_sch] Invalid modulation\n");
-    return SRSRAN_ERROR;
-  }
-  const uint32_t nsymb = cfg->grant.nof_symb;
-  if (nsymb == 0 || nsymb > 14 || nb % Qm || Qm > 8) {
-    return SRSRAN_ERROR_INVALID_INPUTS;
-  }
-  const uint32_t    H = nb / Qm, rows = H / nsymb;
-  srsran_cqi_cfg_t& cq   = cfg->uci_cfg.cqi;
-  const uint32_t    nack = srsran_uci_cfg_total_ack(&cfg->uci_cfg);
-  const bool        uci  = nack > 0 || cq.ri_len > 0 || cq.data_enable;
-  if (uci && !uci_data) {
-    return SRSRAN_ERROR_INVALID_INPUTS;
-  }
-
-  // ---- uci_decode_ri_ack, host part (sch.c:1023-1120): Q'_ACK, Q'_RI ----
-  const bool hl_ri = cq.data_enable && cq.type == SRSRAN_CQI_TYPE_SUBBAND_HL && cq.ri_len;
-  if (hl_ri) {
-    cq.rank_is_not_one = false;  // RI = 1 assumed for the RI / ACK sizes (36.212 5.2.4.1)
-  }
-  const uint32_t cqi_len0 = (uint32_t)srsran_cqi_size(&cq);
-  uint32_t       ack_Qp = 0, ri_Qp = 0;
-  if (nack > 0) {
-    if (nack > SRSRAN_UCI_MAX_ACK_BITS) {
-      return SRSRAN_ERROR_INVALID_INPUTS;
-    }
-    float beta = beta_harq(cfg->uci_offset.I_offset_ack);
-    if (cfg->grant.tb.tbs == 0) {
-      beta /= beta_cqi(cfg->uci_offset.I_offset_cqi);
-    }
-    ack_Qp = qprime_ri_ack(cfg->K_segm, cfg->grant.L_prb, nsymb, nack, cqi_len0, beta);
-  }
-  if (cq.ri_len > 0) {
-    if (cq.ri_len > 4) {
-      return SRSRAN_ERROR_INVALID_INPUTS;
-    }
-    float beta = beta_ri(cfg->uci_offset.I_offset_ri);
-    if (cfg->grant.tb.tbs == 0) {
-      beta /= beta_cqi(cfg->uci_offset.I_offset_cqi);
-    }
-    ri_Qp = qprime_ri_ack(cfg->K_segm, cfg->grant.L_prb, nsymb, cq.ri_len, cqi_len0, beta);
-  }
-  // the ACK / RI rows are counted up from the bottom of the interleaver: positions past its top
-  // (uci.c:378-386 "Error interleaving") are refused
-  if (ack_Qp > 4 * rows || ri_Qp > 4 * rows || ri_Qp > H) {
-    fprintf(stderr, "[srsran_sch] UCI does not fit the PUSCH interleaver (Q'_ACK=%u Q'_RI=%u rows=%u)\n", ack_Qp,
-            ri_Qp, rows);
-    return SRSRAN_ERROR;
-  }
-  const bool need_c = (nack == 1 && ack_Qp > 0) || (cq.ri_len == 1 && ri_Qp > 0);
-  if (need_c && !h_c && !d_c_ext) {
+  const uint32_t nb = p.nb, Qm = p.Qm, H = p.H;
+  if ((p.uci && !uci_data) || (p.need_c && !h_c && !d_c_ext)) {
     return SRSRAN_ERROR_INVALID_INPUTS;
   }
 
@@ -1497,14 +1590,14 @@ static int ulsch_decode_impl(srsran_sch_t*       q,
       (h_q && hipMemcpyAsync(d_q, h_q, (size_t)nb * 2, hipMemcpyHostToDevice, x->stream) != hipSuccess)) {
     return SRSRAN_ERROR;
   }
-  if (!uci) {
-    if (ul_deint_launch(d_q, d_g, Qm, H, nsymb, x->stream) != hipSuccess ||
+  if (!p.uci) {
+    if (ul_deint_launch(d_q, d_g, Qm, H, p.nsymb, x->stream) != hipSuccess ||
         (g_bits && hipMemcpyAsync(g_bits, d_g, (size_t)nb * 2, hipMemcpyDeviceToHost, x->stream) != hipSuccess) ||
         (q_out && hipMemcpyAsync(q_out, d_q, (size_t)nb * 2, hipMemcpyDeviceToHost, x->stream) != hipSuccess) ||
         hipStreamSynchronize(x->stream) != hipSuccess) {
       return SRSRAN_ERROR;
     }
-    if (s.tbs == 0) {
+    if (p.s.tbs == 0) {
       return SRSRAN_SUCCESS;
     }
     srsran_pdsch_cfg_t pc;
@@ -1517,79 +1610,52 @@ static int ulsch_decode_impl(srsran_sch_t*       q,
   }
 
   // ---- device scratch: descriptors, results, sequence ----
-  const bool   up_c = need_c && !d_c_ext;
+  const bool   up_c = p.need_c && !d_c_ext;
   const size_t scr  = align16(sizeof(UlsUciScratch)) + (up_c ? (size_t)nb : 0);
   if (!grow_dev((void**)&x->d_uci, &x->uci_cap, scr)) {
     return SRSRAN_ERROR;
   }
   UlsUciScratch* d_s = (UlsUciScratch*)x->d_uci;
   const uint8_t* d_c = up_c ? x->d_uci + align16(sizeof(UlsUciScratch)) : d_c_ext;
+  srsran_cqi_cfg_t& cq = cfg->uci_cfg.cqi;
   UlsUciScratch  h;
   memset(&h, 0, sizeof(h));
-  h.uci = {d_q, need_c ? d_c : nullptr, d_g, &d_s->out, Qm, rows, nsymb, nack, ack_Qp, cq.ri_len, ri_Qp, 0, 0};
-  // the de-interleaver skips the RI cells: column set[c] holds the RI indices q = 3c mod 4 (mod 4)
-  h.deint         = {d_q, d_g, rows, nsymb, Qm, {}, -1};
-  if (ri_Qp > 0) {
-    static const uint8_t kRiNorm[4] = {1, 4, 7, 10}, kRiExt[4] = {0, 3, 5, 8};
-    const uint8_t*       set        = nsymb > 10 ? kRiNorm : kRiExt;
-    int64_t              last       = -1;  // the largest RI position in q order
-    for (uint32_t c = 0; c < 4; c++) {
-      const uint32_t m = (3 * c) % 4, n = ri_Qp > m ? (ri_Qp - m + 3) / 4 : 0;
-      h.deint.ri_rows[set[c]] = (uint16_t)n;
-      if (n > 0) {
-        last = std::max<int64_t>(last, (int64_t)(rows - 1) * Qm + (int64_t)set[c] * rows * Qm + Qm - 1);
-      }
-    }
-    uint32_t first = 0;  // the first non-RI column of row 0 holds g[0] in its own right
-    while (first < nsymb && h.deint.ri_rows[first] >= rows) {
-      first++;
-    }
-    h.deint.g0_src = (int32_t)std::max<int64_t>(last, (int64_t)first * rows * Qm);
-  }
+  h.uci   = {d_q, p.need_c ? d_c : nullptr, d_g, &d_s->out, Qm, p.rows, p.nsymb, p.nack, p.ack_Qp, cq.ri_len, p.ri_Qp, 0, 0};
+  h.deint = ulsch_deint_desc(d_q, d_g, p);
   if (hipMemcpyAsync(d_s, &h, sizeof(h), hipMemcpyHostToDevice, x->stream) != hipSuccess ||
       (up_c && hipMemcpyAsync((void*)d_c, h_c, nb, hipMemcpyHostToDevice, x->stream) != hipSuccess) ||
       uci_ack_ri_launch(&d_s->uci, 1, x->stream) != hipSuccess ||
-      ul_deint_batch_launch(&d_s->deint, 1, rows, x->stream) != hipSuccess) {
+      ul_deint_batch_launch(&d_s->deint, 1, p.rows, x->stream) != hipSuccess) {
     return SRSRAN_ERROR;
   }
 
   // ---- CQI (sch.c:1160-1183): its size may depend on the RI just decoded ----
-  uint32_t cqi_Qp = 0;
-  if (cq.data_enable) {
-    if (hl_ri) {
-      if (hipMemcpyAsync(&h.out, &d_s->out, sizeof(UciOut), hipMemcpyDeviceToHost, x->stream) != hipSuccess ||
-          hipStreamSynchronize(x->stream) != hipSuccess) {
-        return SRSRAN_ERROR;
-      }
-      cq.rank_is_not_one = h.out.ri[0] > 0;
-    }
-    const int cqi_len = srsran_cqi_size(&cq);
-    if (cqi_len <= 0 || cqi_len > (int)UCI_MAX_CQI_BITS) {
-      return SRSRAN_ERROR_INVALID_INPUTS;
-    }
-    cqi_Qp = qprime_cqi(cfg->K_segm, cfg->grant.L_prb, nsymb, (uint32_t)cqi_len, beta_cqi(cfg->uci_offset.I_offset_cqi),
-                        ri_Qp);
-    if ((uint64_t)cqi_Qp + ri_Qp > H) {
-      return SRSRAN_ERROR;
-    }
-    h.uci.cqi_bits = (uint32_t)cqi_len;
-    h.uci.cqi_Qp   = cqi_Qp;
-    if (hipMemcpyAsync(&d_s->uci, &h.uci, sizeof(UciDesc), hipMemcpyHostToDevice, x->stream) != hipSuccess ||
-        uci_cqi_launch(&d_s->uci, 1, x->stream) != hipSuccess) {
-      return SRSRAN_ERROR;
-    }
-  } else if (hl_ri) {
-    cq.rank_is_not_one = false;
+  uint32_t cqi_len = 0, cqi_Qp = 0;
+  if (cq.data_enable && p.hl_ri &&
+      (hipMemcpyAsync(&h.out, &d_s->out, sizeof(UciOut), hipMemcpyDeviceToHost, x->stream) != hipSuccess ||
+       hipStreamSynchronize(x->stream) != hipSuccess)) {
+    return SRSRAN_ERROR;
+  }
+  const int crc = ulsch_cqi_plan(cfg, p, h.out.ri[0], &cqi_len, &cqi_Qp);
+  if (crc != SRSRAN_SUCCESS) {
+    return crc;
+  }
+  UciDesc u  = h.uci;  // a second copy: the first upload may still be reading h
+  u.cqi_bits = cqi_len;
+  u.cqi_Qp   = cqi_Qp;
+  if (cqi_len && (hipMemcpyAsync(&d_s->uci, &u, sizeof(UciDesc), hipMemcpyHostToDevice, x->stream) != hipSuccess ||
+                  uci_cqi_launch(&d_s->uci, 1, x->stream) != hipSuccess)) {
+    return SRSRAN_ERROR;
   }
 
   // ---- decode_tb over the UL-SCH part (after the CQI) ----
-  int ret = cq.data_enable ? (int)cqi_Qp : (int)ri_Qp;  // the value left in ret when there is no TB
-  if (s.tbs > 0) {
+  int ret = cq.data_enable ? (int)cqi_Qp : (int)p.ri_Qp;  // the value left in ret when there is no TB
+  if (p.s.tbs > 0) {
     srsran_pdsch_cfg_t pc;
     memset(&pc, 0, sizeof(pc));
     pc.grant.nof_tb          = 1;
     pc.grant.tb[0]           = cfg->grant.tb;
-    pc.grant.tb[0].nof_bits  = (H - ri_Qp - cqi_Qp) * Qm;
+    pc.grant.tb[0].nof_bits  = (H - p.ri_Qp - cqi_Qp) * Qm;
     pc.softbuffers.rx[0]     = cfg->softbuffers.rx;
     pc.max_nof_iterations    = cfg->max_nof_iterations;
     ret                      = dlsch_decode_sync(q, &pc, nullptr, d_g + (size_t)cqi_Qp * Qm, data, 0, 1);
@@ -1600,20 +1666,7 @@ static int ulsch_decode_impl(srsran_sch_t*       q,
       hipStreamSynchronize(x->stream) != hipSuccess) {
     return SRSRAN_ERROR;
   }
-  if (nack > 0) {
-    memcpy(uci_data->ack.ack_value, h.out.ack, std::min<uint32_t>(nack, SRSRAN_UCI_MAX_ACK_BITS));
-    uci_data->ack.valid = h.out.ack_valid != 0;
-  }
-  if (cq.ri_len > 0) {
-    uci_data->ri = h.out.ri[0];
-  }
-  if (cq.data_enable) {
-    uci_data->cqi.data_crc = h.out.cqi_crc != 0;
-    srsran_cqi_value_unpack(&cq, h.out.cqi, &uci_data->cqi);
-  }
-  if (hl_ri) {
-    cq.rank_is_not_one = uci_data->ri > 0;  // sch.c:1112-1117
-  }
+  ulsch_uci_out(cfg, p, h.out, uci_data);
   return ret;
 }
 
@@ -1679,6 +1732,171 @@ int ulsch_decode_dev(srsran_sch_t* q, srsran_pusch_cfg_t* cfg, int16_t* d_q, con
                      srsran_uci_value_t* uci_data)
 {
   return ulsch_decode_impl(q, cfg, nullptr, d_q, nullptr, nullptr, nullptr, d_c, data, uci_data);
+}
+
+// Batched srsran_ulsch_decode (ulsch_batch.h): the same stages as ulsch_decode_impl, each one launch
+// over every UE of the batch, and one decode_tb batch for all their transport blocks.
+int ulsch_decode_batch_dev(srsran_sch_t* q, uint32_t n, UlschBatchUe* ues, const uint8_t* d_data_base,
+                           size_t data_bytes, hipStream_t st)
+{
+  if (!q || !q->gpu || (n && !ues)) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  SchCtx*              x = (SchCtx*)q->gpu;
+  std::vector<UlsPlan> plan(n);
+  std::vector<int32_t> uix(n, -1);  // index in the UCI arrays
+  std::vector<uint32_t> live;
+  uint32_t              m = 0, max_rows = 0;
+  bool                  need_ri = false;
+  for (uint32_t i = 0; i < n; i++) {
+    UlschBatchUe& u = ues[i];
+    u.avg           = NAN;
+    u.ret           = u.cfg ? ulsch_plan(u.cfg, &plan[i]) : SRSRAN_ERROR_INVALID_INPUTS;
+    if (u.ret == SRSRAN_SUCCESS &&
+        (!u.d_q || !u.d_g || (plan[i].uci && !u.uci) || (plan[i].need_c && !u.d_c) ||
+         (plan[i].s.tbs > 0 && (!u.cfg->softbuffers.rx || !u.d_data || u.d_data < d_data_base ||
+                                u.d_data + plan[i].s.tbs / 8 > d_data_base + data_bytes)))) {
+      u.ret = SRSRAN_ERROR_INVALID_INPUTS;
+    }
+    if (u.ret != SRSRAN_SUCCESS) {
+      continue;
+    }
+    live.push_back(i);
+    max_rows = std::max(max_rows, plan[i].rows);
+    if (plan[i].uci) {
+      uix[i] = (int32_t)m++;
+      need_ri |= plan[i].hl_ri;
+    }
+  }
+  const uint32_t nl = (uint32_t)live.size();
+  // device scratch: UciDesc[m] | UlDeint[nl] | UciOut[m] | result[nl] | avg[nl]; pinned staging:
+  // the two uploads (the CQI pass rewrites the UCI descriptors) and the read-back
+  const size_t o_dd = align16(m * sizeof(UciDesc)), o_out = o_dd + align16(nl * sizeof(UlDeint));
+  const size_t o_res = o_out + align16(m * sizeof(UciOut)), o_avg = o_res + align16(nl * sizeof(int32_t));
+  const size_t dev_need = o_avg + align16(nl * sizeof(float));
+  const size_t h_cqi = dev_need, h_back = h_cqi + align16(m * sizeof(UciDesc));
+  const size_t back_len = dev_need - o_out, h_need = h_back + back_len + data_bytes;
+  if (!grow_dev((void**)&x->d_ubs, &x->dubs_cap, dev_need)) {
+    return SRSRAN_ERROR;
+  }
+  if (h_need > x->hubs_cap) {
+    hipHostFree(x->h_ubs);
+    x->h_ubs    = nullptr;
+    x->hubs_cap = 0;
+    if (hipHostMalloc((void**)&x->h_ubs, h_need, hipHostMallocDefault) != hipSuccess) {
+      return SRSRAN_ERROR;
+    }
+    x->hubs_cap = h_need;
+  }
+  uint8_t* d = x->d_ubs;
+  uint8_t* h = x->h_ubs;
+  UciDesc* h_ud  = (UciDesc*)h;
+  UlDeint* h_dd  = (UlDeint*)(h + o_dd);
+  UciOut*  d_out = (UciOut*)(d + o_out);
+  for (uint32_t j = 0; j < nl; j++) {
+    const uint32_t i = live[j];
+    const UlsPlan& p = plan[i];
+    h_dd[j]          = ulsch_deint_desc(ues[i].d_q, ues[i].d_g, p);
+    if (uix[i] >= 0) {
+      h_ud[uix[i]] = {ues[i].d_q, p.need_c ? ues[i].d_c : nullptr, ues[i].d_g, d_out + uix[i], p.Qm, p.rows, p.nsymb,
+                      p.nack, p.ack_Qp, ues[i].cfg->uci_cfg.cqi.ri_len, p.ri_Qp, 0, 0};
+    }
+  }
+  // ACK decode + zeroing and RI decode (sch.c:1023-1120), then the de-interleaver reading the zeroed q
+  if (nl && (hipMemcpyAsync(d, h, o_out, hipMemcpyHostToDevice, st) != hipSuccess ||
+             (m && uci_ack_ri_launch((const UciDesc*)d, m, st) != hipSuccess) ||
+             ul_deint_batch_launch((const UlDeint*)(d + o_dd), nl, max_rows, st) != hipSuccess)) {
+    return SRSRAN_ERROR;
+  }
+  UciOut* h_out = (UciOut*)(h + h_back);
+  if (need_ri && (hipMemcpyAsync(h_out, d_out, m * sizeof(UciOut), hipMemcpyDeviceToHost, st) != hipSuccess ||
+                  hipStreamSynchronize(st) != hipSuccess)) {
+    return SRSRAN_ERROR;
+  }
+  // CQI sizes (after the RI where the report needs it) and the UL-SCH parts
+  std::vector<uint32_t>              cqi_Qp(n, 0);
+  std::vector<srsran_dlsch_gpu_tb_t> tbs;
+  std::vector<int32_t>               tbix(n, -1);
+  UciDesc*                           h_ud2 = (UciDesc*)(h + h_cqi);
+  bool                               any_cqi = false;
+  uint32_t                           maxit   = 0;
+  memcpy(h_ud2, h_ud, m * sizeof(UciDesc));
+  for (uint32_t i : live) {
+    UlschBatchUe&  u = ues[i];
+    const UlsPlan& p = plan[i];
+    if (uix[i] >= 0) {
+      uint32_t len = 0;
+      u.ret        = ulsch_cqi_plan(u.cfg, p, need_ri ? h_out[uix[i]].ri[0] : 0, &len, &cqi_Qp[i]);
+      if (u.ret != SRSRAN_SUCCESS) {
+        continue;
+      }
+      h_ud2[uix[i]].cqi_bits = len;
+      h_ud2[uix[i]].cqi_Qp   = cqi_Qp[i];
+      any_cqi |= len > 0;
+    }
+    if (p.s.tbs > 0) {
+      srsran_dlsch_gpu_tb_t t;
+      memset(&t, 0, sizeof(t));
+      t.tbs        = p.s.tbs;
+      t.Qm         = p.Qm;
+      t.rv         = (uint32_t)u.cfg->grant.tb.rv;
+      t.nof_e_bits = (p.H - p.ri_Qp - cqi_Qp[i]) * p.Qm;
+      t.d_e_bits   = u.d_g + (size_t)cqi_Qp[i] * p.Qm;
+      t.d_data     = u.d_data;
+      t.softbuffer = u.cfg->softbuffers.rx;
+      t.new_data   = u.new_data ? 1 : 0;
+      tbix[i]      = (int32_t)tbs.size();
+      tbs.push_back(t);
+      maxit = std::max(maxit, u.cfg->max_nof_iterations);
+    }
+  }
+  if (any_cqi && (hipMemcpyAsync(d, h_ud2, m * sizeof(UciDesc), hipMemcpyHostToDevice, st) != hipSuccess ||
+                  uci_cqi_launch((const UciDesc*)d, m, st) != hipSuccess)) {
+    return SRSRAN_ERROR;
+  }
+  if (!tbs.empty()) {
+    srsran_sch_set_max_noi(q, maxit);
+    if (srsran_dlsch_gpu_decode_batch(q, (uint32_t)tbs.size(), tbs.data(), (int32_t*)(d + o_res),
+                                      (float*)(d + o_avg), st) != SRSRAN_SUCCESS) {
+      return SRSRAN_ERROR;
+    }
+  }
+  // results, UCI and payloads back in one sync
+  if ((nl && hipMemcpyAsync(h + h_back, d + o_out, back_len, hipMemcpyDeviceToHost, st) != hipSuccess) ||
+      (!tbs.empty() && data_bytes &&
+       hipMemcpyAsync(h + h_back + back_len, d_data_base, data_bytes, hipMemcpyDeviceToHost, st) != hipSuccess) ||
+      hipStreamSynchronize(st) != hipSuccess) {
+    return SRSRAN_ERROR;
+  }
+  const int32_t* h_res = (const int32_t*)(h + h_back + (o_res - o_out));
+  const float*   h_avg = (const float*)(h + h_back + (o_avg - o_out));
+  float          last  = q->avg_iterations;  // avg_iterations as sequential decodes would leave it
+  for (uint32_t i = 0; i < n; i++) {
+    UlschBatchUe&  u = ues[i];
+    const UlsPlan& p = plan[i];
+    if (uix[i] < 0 && tbix[i] < 0) {
+      u.avg = last;
+      continue;  // a failed check, or neither UCI nor a TB: srsran_ulsch_decode returns SUCCESS
+    }
+    if (u.ret != SRSRAN_SUCCESS) {
+      u.avg = last;
+      continue;
+    }
+    if (uix[i] >= 0) {
+      ulsch_uci_out(u.cfg, p, h_out[uix[i]], u.uci);
+      u.ret = u.cfg->uci_cfg.cqi.data_enable ? (int)cqi_Qp[i] : (int)p.ri_Qp;
+    }
+    if (tbix[i] >= 0) {
+      u.ret = h_res[tbix[i]];
+      last  = h_avg[tbix[i]];
+      if (u.data) {
+        memcpy(u.data, h + h_back + back_len + (u.d_data - d_data_base), p.s.tbs / 8);
+      }
+    }
+    u.avg = last;
+  }
+  q->avg_iterations = last;
+  return SRSRAN_SUCCESS;
 }
 }  // namespace srsran_amd
 

@@ -753,21 +753,39 @@ __global__ __launch_bounds__(128, 2) void tdec16_multi_kernel(const TdecArgs* __
   tdec16_body<false>(a, (int)(b - first[lo]));
 }
 
-// Two blocks a workgroup: a launch of fewer than 1024 blocks fits tdec_kernel.hip's quad decoder in one
-// round (one block per workgroup, 4 per CU) with more SIMDs busy than the lane-pair kernel; at 1024
-// blocks the two tie (K = 6144: 0.388 vs 0.391 ms) and above the quad decoder needs a second round.
-
-// srsran_tdec_gpu_set_pair_threshold() moves the threshold (tests force the lane-pair kernel on small
-// batches with 0).
-static uint32_t g_pair_min_cb = 1024u;
+// Which 16-sub-block decoder a launch of n blocks gets (K = 6144, 8 half-iterations, ms per launch,
+// gpurun_out r03d -> profiles/r03_tdec_kernels.jsonl):
+//      n      quad (tdec_kernel<16>)   lane pair (tdec16_kernel)   single lane (tdec16s_kernel)
+//    256            0.258                    0.275                        0.344
+//    512            0.339                    0.282                        0.348
+//   1024            0.403                    0.394                        0.362
+//   2048            0.766                    0.457                        0.382
+// The quad decoder (one block a workgroup) fills the chip best below ~512 blocks, the lane pair between,
+// and the single-lane decoder (64 lanes a wave on 4 blocks, the densest mapping) from 1024 on.
+// srsran_tdec_gpu_set_pair_threshold() / _single_threshold() move the thresholds (tests force each
+// kernel onto small batches with 0).
+static uint32_t g_pair_min_cb = 512u;
 void     tdec16_set_min_cb(uint32_t n) { __atomic_store_n(&g_pair_min_cb, n, __ATOMIC_RELAXED); }
 uint32_t tdec16_min_cb() { return __atomic_load_n(&g_pair_min_cb, __ATOMIC_RELAXED); }
 bool     tdec16_pays(uint32_t ncb) { return ncb >= tdec16_min_cb(); }
-// srsran_tdec_gpu_set_single_threshold(): blocks a launch from which the single-lane decoder
-// (tdec16s_kernel.hip) replaces the lane pair
-static uint32_t g_single_min_cb = 4096u;
+// srsran_tdec_gpu_set_single_threshold(): blocks a launch from which the single-lane decoders
+// (tdecs_kernel.hip, 16-sub-block class) replaces the lane pair
+static uint32_t g_single_min_cb = 1024u;
 void     tdec16s_set_min_cb(uint32_t n) { __atomic_store_n(&g_single_min_cb, n, __ATOMIC_RELAXED); }
 uint32_t tdec16s_min_cb() { return __atomic_load_n(&g_single_min_cb, __ATOMIC_RELAXED); }
+// The 8-sub-block class: its quad decoder (one block a workgroup) stays ahead up to ~1024 blocks a launch
+// (K = 512: 0.060 vs 0.085 ms at 512, 0.081 vs 0.086 ms at 1024) and the single-lane decoder is ahead on
+// the fused class launch (32 sizes x 256 = 8192 blocks: 0.30 vs 0.53 ms): from 4096 blocks by default.
+static uint32_t g_single8_min_cb = 4096u;
+void     tdec8s_set_min_cb(uint32_t n) { __atomic_store_n(&g_single8_min_cb, n, __ATOMIC_RELAXED); }
+uint32_t tdec8s_min_cb() { return __atomic_load_n(&g_single8_min_cb, __ATOMIC_RELAXED); }
+// srsran_tdec_gpu_set_generic_single_threshold(): the generic class (K <= 400) keeps tdec_kernel.hip's
+// quad decoder by default: one lane per block and direction runs the whole K-step recursion serially, and
+// at 1024 blocks per size (47104 blocks) tdec1s_kernel takes 1.47 ms against the quad decoder's 0.78 ms
+// (profiles/r03_tdec_kernels.jsonl), so tdec1s is selected only when a caller lowers this threshold.
+static uint32_t g_single1_min_cb = 0xffffffffu;
+void     tdec1s_set_min_cb(uint32_t n) { __atomic_store_n(&g_single1_min_cb, n, __ATOMIC_RELAXED); }
+uint32_t tdec1s_min_cb() { return __atomic_load_n(&g_single1_min_cb, __ATOMIC_RELAXED); }
 int      tdec16_choice(uint32_t ncb) { return ncb >= tdec16s_min_cb() ? 2 : tdec16_pays(ncb) ? 1 : 0; }
 
 bool tdec16_eligible(int nsb, const TdecArgs& a)
@@ -779,12 +797,12 @@ bool tdec16_eligible(int nsb, const TdecArgs& a)
 bool tdec8s_eligible(int nsb, const TdecArgs& a)
 {
   return nsb == 8 && a.layout_sb && a.n_start == 0 && a.state == nullptr && a.L >= (uint32_t)OVL &&
-         a.ncb >= tdec16s_min_cb();
+         a.ncb >= tdec8s_min_cb();
 }
 
 bool tdec1s_eligible(int nsb, const TdecArgs& a)
 {
-  return nsb == 1 && a.n_start == 0 && a.state == nullptr && a.ncb >= tdec16s_min_cb();
+  return nsb == 1 && a.n_start == 0 && a.state == nullptr && a.ncb >= tdec1s_min_cb();
 }
 
 size_t tdec16_lds_bytes(const TdecArgs& a)

@@ -390,17 +390,48 @@ void srsran_tdec_gpu_set_pair_threshold(uint32_t nof_cb) { tdec16_set_min_cb(nof
 
 uint32_t srsran_tdec_gpu_get_pair_threshold(void) { return tdec16_min_cb(); }
 
-void srsran_tdec_gpu_set_single_threshold(uint32_t nof_cb) { tdec16s_set_min_cb(nof_cb); }
+void srsran_tdec_gpu_set_class_single_threshold(uint32_t nof_subblocks, uint32_t nof_cb)
+{
+  if (nof_subblocks == 16) {
+    tdec16s_set_min_cb(nof_cb);
+  } else if (nof_subblocks == 8) {
+    tdec8s_set_min_cb(nof_cb);
+  } else if (nof_subblocks <= 1) {
+    tdec1s_set_min_cb(nof_cb);
+  }
+}
+
+uint32_t srsran_tdec_gpu_get_class_single_threshold(uint32_t nof_subblocks)
+{
+  return nof_subblocks == 16 ? tdec16s_min_cb() : nof_subblocks == 8 ? tdec8s_min_cb() : tdec1s_min_cb();
+}
+
+void srsran_tdec_gpu_set_single_threshold(uint32_t nof_cb)
+{
+  tdec16s_set_min_cb(nof_cb);
+  tdec8s_set_min_cb(nof_cb);
+}
 
 uint32_t srsran_tdec_gpu_get_single_threshold(void) { return tdec16s_min_cb(); }
 
+void srsran_tdec_gpu_set_generic_single_threshold(uint32_t nof_cb) { tdec1s_set_min_cb(nof_cb); }
+
+uint32_t srsran_tdec_gpu_get_generic_single_threshold(void) { return tdec1s_min_cb(); }
+
 const char* srsran_tdec_gpu_kernel_name_batch(uint32_t long_cb, uint32_t nof_cb)
 {
-  if (auto_nsb(long_cb) == 16) {
+  const int nsb = auto_nsb(long_cb);
+  if (nsb == 16) {
     const int k = tdec16_choice(nof_cb);
     if (k) {
       return k == 2 ? "tdec16s_kernel" : "tdec16_kernel";
     }
+  }
+  if (nsb == 8 && nof_cb >= tdec8s_min_cb()) {
+    return "tdec8s_kernel";
+  }
+  if (nsb == 1 && nof_cb >= tdec1s_min_cb()) {
+    return "tdec1s_kernel";
   }
   return srsran_tdec_gpu_kernel_name(long_cb);
 }
@@ -743,16 +774,15 @@ int srsran_tdec_gpu_run_multi(uint32_t              nof_groups,
       ret = enqueue(cfg[g], d_input[g], in_stride[g], layout_sb, d_output[g], nof_cb[g], 0, n_end, nullptr, st);
       continue;
     }
-    // the 16-sub-block class on SB input runs the lane-pair decoder (tdec16_kernel.hip)
     uint32_t       cls_cb = 0;
     for (uint32_t g : gs) {
       cls_cb += nof_cb[g];
     }
     // 2 single lane (tdecs_kernel.hip), 1 lane pair (16 sub-blocks only), 0 quad
-    const int kind = cls_nsb[ci] == 1               ? (cls_cb >= tdec16s_min_cb() ? 2 : 0)  // natural layout
+    const int kind = cls_nsb[ci] == 1               ? (cls_cb >= tdec1s_min_cb() ? 2 : 0)   // natural layout
                      : !layout_sb                   ? 0
                      : cls_nsb[ci] == 16            ? tdec16_choice(cls_cb)
-                                                    : (cls_cb >= tdec16s_min_cb() ? 2 : 0);
+                                                    : (cls_cb >= tdec8s_min_cb() ? 2 : 0);
     const int  nsbc = cls_nsb[ci];
     const int  cpw  = kind == 2   ? (nsbc == 16 ? tdecs16::cpw() : nsbc == 8 ? tdecs8::cpw() : tdecs1::cpw())
                       : kind == 1 ? tdec16_cpw()

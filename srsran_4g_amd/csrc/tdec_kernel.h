@@ -93,6 +93,10 @@ SRSRAN_TDECS_API(tdecs1)  // tdec1s_kernel.hip: the generic decoder (K <= 400), 
 #undef SRSRAN_TDECS_API
 bool       tdec8s_eligible(int nsb, const TdecArgs& a);
 bool       tdec1s_eligible(int nsb, const TdecArgs& a);
+void       tdec8s_set_min_cb(uint32_t n);
+uint32_t   tdec8s_min_cb();
+void       tdec1s_set_min_cb(uint32_t n);
+uint32_t   tdec1s_min_cb();
 void       tdec16s_set_min_cb(uint32_t n);
 uint32_t   tdec16s_min_cb();
 // the kernel the 16-sub-block class runs for a launch of ncb blocks on the SB layout: 2 = single lane

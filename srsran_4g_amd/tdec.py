@@ -93,6 +93,10 @@ def load_library():
         "srsran_tdec_gpu_get_pair_threshold": ([], u32),
         "srsran_tdec_gpu_set_single_threshold": ([u32], None),
         "srsran_tdec_gpu_get_single_threshold": ([], u32),
+        "srsran_tdec_gpu_set_class_single_threshold": ([u32, u32], None),
+        "srsran_tdec_gpu_get_class_single_threshold": ([u32], u32),
+        "srsran_tdec_gpu_set_generic_single_threshold": ([u32], None),
+        "srsran_tdec_gpu_get_generic_single_threshold": ([], u32),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)
@@ -124,21 +128,37 @@ class pair_threshold:
         load_library().srsran_tdec_gpu_set_pair_threshold(self.old)
 
 
-class single_threshold:
-    """Context manager: blocks per launch from which the single-lane decoder runs
-    (srsran_tdec_gpu_set_single_threshold), restored on exit."""
+class class_single_threshold:
+    """Context manager: blocks per launch from which the single-lane decoders of the given classes
+    (16, 8, 0 = generic) run (srsran_tdec_gpu_set_class_single_threshold), each restored on exit."""
+    classes = (16, 8)
 
-    def __init__(self, nof_cb):
+    def __init__(self, nof_cb, classes=None):
         self.n = nof_cb
+        if classes is not None:
+            self.classes = tuple(classes)
 
     def __enter__(self):
         lib = load_library()
-        self.old = lib.srsran_tdec_gpu_get_single_threshold()
-        lib.srsran_tdec_gpu_set_single_threshold(self.n)
+        self.old = {c: lib.srsran_tdec_gpu_get_class_single_threshold(c) for c in self.classes}
+        for c in self.classes:
+            lib.srsran_tdec_gpu_set_class_single_threshold(c, self.n)
         return self
 
     def __exit__(self, *exc):
-        load_library().srsran_tdec_gpu_set_single_threshold(self.old)
+        lib = load_library()
+        for c, n in self.old.items():
+            lib.srsran_tdec_gpu_set_class_single_threshold(c, n)
+
+
+class single_threshold(class_single_threshold):
+    """the 16- and 8-sub-block classes (srsran_tdec_gpu_set_single_threshold)"""
+    classes = (16, 8)
+
+
+class generic_single_threshold(class_single_threshold):
+    """the generic class (srsran_tdec_gpu_set_generic_single_threshold)"""
+    classes = (0,)
 
 
 def nof_subblocks(K):

@@ -1,5 +1,5 @@
 """The two decoders of the 16-sub-block class on the SB layout, each forced onto small batches: the lane
-pair (tdec16_kernel.hip; by itself from 1024 blocks a launch) and the single lane per sub-block
+pair (tdec16_kernel.hip; by itself from 512 blocks a launch) and the single lane per sub-block
 (tdec16s_kernel.hip; by itself from srsran_tdec_gpu_get_single_threshold() blocks): every K >= 816 of
 the bit-exact suites again, plain batches with block counts that leave workgroups partly empty, the
 multi-size fused launch, and DL-SCH transport blocks with CRC early stop over HARQ."""

@@ -1,6 +1,6 @@
 """The single-lane decoder of the generic class (tdec1s_kernel.hip: the 46 sizes K = 40 .. 400, the decoder of
 turbodecoder_gen.c with wrap-around arithmetic on the natural input layout) forced onto every batch size
-(srsran_tdec_gpu_set_single_threshold(0)) against the oracle decoder: all 46 sizes with batches that fill
+(srsran_tdec_gpu_set_generic_single_threshold(0); by default the quad decoder keeps this class) against the oracle decoder: all 46 sizes with batches that fill
 a 64-block workgroup partly, exactly and over several workgroups, several half-iteration counts, extreme
 inputs (the int16 wrap matters), the fused multi-size launch and DL-SCH transport blocks (one code block,
 CRC24A) with CRC early stop over HARQ."""
@@ -19,7 +19,7 @@ def single():
     from srsran_4g_amd import tdec
     if not tdec.gpu_available():
         pytest.skip("no HIP device")
-    with tdec.single_threshold(0):
+    with tdec.generic_single_threshold(0):
         yield
 
 

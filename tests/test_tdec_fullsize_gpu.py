@@ -6,11 +6,12 @@ buffers placed far apart in device memory.
   * configs[1]: all 188 LTE code block sizes x 1024 blocks, 8 half-iterations, one
     srsran_tdec_gpu_run_multi call (the bench's timed step): the 16-sub-block class is one fused
     launch (110 sizes x 1024 blocks in one grid) of the single-lane decoder tdec16s_multi_kernel (and,
-    checked as well, of the lane-pair tdec16_multi_kernel), the 8- and 1-sub-block classes the quad
-    decoder's fused launches.  Every block equals the reference's output
+    checked as well, of the lane-pair tdec16_multi_kernel), the 8-sub-block class the single-lane
+    tdec8s_multi_kernel and the generic class the quad decoder's fused launch.  Every block equals the reference's output
     for its pool block (the batch tiles a pool of distinct AWGN blocks at several SNRs, so decoded
     words differ from the transmitted ones in some blocks and not in others).
-  * configs[0]'s shape on the GPU: K = 6144 x 1024 through srsran_tdec_gpu_run_batch.
+  * configs[0]'s shape on the GPU: K = 6144 x 1024 through srsran_tdec_gpu_run_batch, on each of the
+    three 16-sub-block decoders (single lane by default at this size, lane pair, quad).
   * DL-SCH transport blocks whose soft buffers lie more than 2 GB apart: the lane-pair decoder runs
     (the descriptor list is padded where a workgroup's two blocks would straddle two far buffers) and
     every TB equals the oracle's decode_tb (return, payload, average iterations, CB CRC flags).
@@ -93,7 +94,8 @@ def test_all188_x1024_fused_launch(env):
     assert len({w.tobytes() for K in (6144, 40) for w in want[K]}) == 2 * len(POOL_EBNO)
 
 
-def test_k6144_x1024_batch(env):
+@pytest.mark.parametrize("kernel", ["tdec16s_kernel<false>", "tdec16_kernel<false>", "tdec_kernel<16>"])
+def test_k6144_x1024_batch(env, kernel):
     torch, tdec, ref, ora = env
     rng = np.random.default_rng(3002)
     K, batch = 6144, 1024
@@ -101,9 +103,14 @@ def test_k6144_x1024_batch(env):
     want = np.stack([ref.tdec_run(K, x, True, 8) for x in pool])
     d_in = torch.from_numpy(np.ascontiguousarray(np.tile(pool, (batch // len(pool) + 1, 1))[:batch])).cuda()
     d_out = torch.zeros((batch, K // 8), dtype=torch.uint8, device="cuda")
-    tdec.gpu_run_batch(K, d_in.data_ptr(), d_in.shape[1], True, d_out.data_ptr(), batch, 8, None)
-    torch.cuda.synchronize()
-    assert tdec.last_kernel() == "tdec16_kernel<false>"  # the lane-pair decoder from 1024 blocks
+    never = 1 << 30
+    pair, single = {"tdec16s_kernel<false>": (None, None), "tdec16_kernel<false>": (None, never),
+                    "tdec_kernel<16>": (never, never)}[kernel]
+    with tdec.pair_threshold(tdec.load_library().srsran_tdec_gpu_get_pair_threshold() if pair is None else pair), \
+            tdec.single_threshold(tdec.load_library().srsran_tdec_gpu_get_single_threshold() if single is None else single):
+        tdec.gpu_run_batch(K, d_in.data_ptr(), d_in.shape[1], True, d_out.data_ptr(), batch, 8, None)
+        torch.cuda.synchronize()
+    assert tdec.last_kernel() == kernel
     got = d_out.cpu().numpy()
     assert np.array_equal(got, want[np.arange(batch) % len(pool)])
 

@@ -1,7 +1,8 @@
 """Turbo-decoder kernel micro-benchmark (developer tool, for timing and rocprofv3 --pmc passes): N identical
 launches of one 16-sub-block-class decoder on one workload, HIP events on the launch stream.
 
-  python tools/tdec_kernels.py --kernel single|pair|quad --workload k6144|all188 [--batch 1024] [--launches 5]
+  python tools/tdec_kernels.py --kernel single|pair|quad --workload k6144|all188|class8|class1 [--K k]
+                               [--batch 1024] [--launches 5]
 
 k6144: K = 6144 x batch blocks (srsran_tdec_gpu_run_batch); all188: every K >= 816 x batch blocks in one
 fused srsran_tdec_gpu_run_multi call (the 16-sub-block class of the bench's all-188 step); class8: the
@@ -25,6 +26,7 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--kernel", choices=["single", "pair", "quad"], default="single")
     p.add_argument("--workload", choices=["k6144", "all188", "class8", "class1"], default="k6144")
+    p.add_argument("--K", type=int, default=0, help="one code block size instead of the workload's")
     p.add_argument("--batch", type=int, default=1024)
     p.add_argument("--launches", type=int, default=5)
     p.add_argument("--iters", type=int, default=8)
@@ -34,8 +36,11 @@ def main():
     lib = tdec.load_library()
     lib.srsran_tdec_gpu_set_pair_threshold(pair_min)
     lib.srsran_tdec_gpu_set_single_threshold(single_min)
+    lib.srsran_tdec_gpu_set_generic_single_threshold(single_min)
     nsb = {"class8": 8, "class1": 0}.get(a.workload, 16)  # srsran_tdec_autoimp_get_subblocks: 0 = generic
     Ks = [6144] if a.workload == "k6144" else [k for k in tdec.CB_SIZES if tdec.nof_subblocks(k) == nsb]
+    if a.K:
+        Ks, nsb = [a.K], tdec.nof_subblocks(a.K)
     rng = np.random.default_rng(5)
     ins, outs = [], []
     for K in Ks:

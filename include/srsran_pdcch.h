@@ -179,6 +179,10 @@ uint32_t srsran_dci_format_sizeof(const srsran_cell_t* cell, srsran_dl_sf_cfg_t*
                                   srsran_dci_format_t format);                                 /* dci.c:359-413 */
 int      srsran_dci_msg_unpack_pdsch(srsran_cell_t* cell, srsran_dl_sf_cfg_t* sf, srsran_dci_cfg_t* cfg,
                                      srsran_dci_msg_t* msg, srsran_dci_dl_t* dci);             /* dci.c:1288-1340 */
+int      srsran_dci_msg_pack_pdsch(srsran_cell_t* cell, srsran_dl_sf_cfg_t* sf, srsran_dci_cfg_t* cfg,
+                                   srsran_dci_dl_t* dci, srsran_dci_msg_t* msg);               /* dci.c:1243-1286 */
+int      srsran_dci_msg_pack_pusch(srsran_cell_t* cell, srsran_dl_sf_cfg_t* sf, srsran_dci_cfg_t* cfg,
+                                   srsran_dci_ul_t* dci, srsran_dci_msg_t* msg);               /* dci.c:1342-1367 */
 int      srsran_dci_msg_unpack_pusch(srsran_cell_t* cell, srsran_dl_sf_cfg_t* sf, srsran_dci_cfg_t* cfg,
                                      srsran_dci_msg_t* msg, srsran_dci_ul_t* dci);             /* dci.c:1369-1395, 492-566 */
 bool     srsran_dci_location_isvalid(srsran_dci_location_t* c);                                /* dci.c:1442-1449 */

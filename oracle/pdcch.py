@@ -43,6 +43,8 @@ class Ref:
                                   ctypes.POINTER(u32), ctypes.POINTER(ctypes.c_float), f32p]
         L.ref_pdcch_decode.argtypes = [u32, u32, f32p, u32, u32, u32, ctypes.c_int, u32, u8p,
                                        ctypes.POINTER(ctypes.c_uint16), ctypes.POINTER(ctypes.c_float)]
+        L.ref_enb_ctrl_tx.argtypes = [u32, u32, u32, ctypes.c_int, ctypes.c_int, ctypes.c_int, u32, u32, ctypes.c_int,
+                                      u32, u8p, u32p, u32p, u32p, u16p, f32p]
         L.ref_viterbi_decode_f.argtypes = [f32p, u32, u8p]
         L.ref_rm_conv_rx.argtypes = [f32p, u32, f32p, u32]
         self.L = L
@@ -78,6 +80,25 @@ class Ref:
         if self.L.ref_ctrl_tx(nof_prb, nof_ports, cell_id, phich_len, phich_res, tti, cfi, n, pl.reshape(-1), nb, Ls,
                               nc, rn, gf) != 0:
             raise RuntimeError("ref_ctrl_tx failed")
+        return gf.view(np.complex64).reshape(nof_ports, 14, 12 * nof_prb)
+
+    def enb_ctrl_tx(self, nof_prb, nof_ports, cell_id, tti, cfi, msgs, put_base=True, cp=0, phich_len=0, phich_res=2):
+        """srsran_enb_dl_put_base's PSS / SSS / PBCH / PCFICH (put_base) and srsran_pdcch_encode of each of
+        msgs = [(bits, L, ncce, rnti)] (ref_enb_ctrl_harness.c).  Returns [port] grids (14, 12 nof_prb)."""
+        n = len(msgs)
+        pl = np.zeros((max(n, 1), DCI_MAX_BITS), np.uint8)
+        nb = np.zeros(max(n, 1), np.uint32)
+        Ls = np.zeros(max(n, 1), np.uint32)
+        nc = np.zeros(max(n, 1), np.uint32)
+        rn = np.zeros(max(n, 1), np.uint16)
+        for i, (bits, L, ncce, rnti) in enumerate(msgs):
+            pl[i, :len(bits)] = bits
+            nb[i], Ls[i], nc[i], rn[i] = len(bits), L, ncce, rnti
+        g = np.zeros((nof_ports, 14, 12 * nof_prb), np.complex64)
+        gf = g.view(np.float32).reshape(-1)
+        if self.L.ref_enb_ctrl_tx(nof_prb, nof_ports, cell_id, cp, phich_len, phich_res, tti, cfi, int(put_base), n,
+                                  pl.reshape(-1), nb, Ls, nc, rn, gf) != 0:
+            raise RuntimeError("ref_enb_ctrl_tx failed")
         return gf.view(np.complex64).reshape(nof_ports, 14, 12 * nof_prb)
 
     def ctrl_rx(self, nof_prb, nof_ports, cell_id, tti, grids, ce, noise, phich_len=0, phich_res=2):

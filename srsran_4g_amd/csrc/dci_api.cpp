@@ -5,9 +5,11 @@
 //   DCI sizes      phch/dci.c:93-413 (FDD: 3-bit HARQ process number, no DAI)
 //   DCI unpack     phch/dci.c:492-566 (format 0), :641-708 (format 1), :797-897 (1A), :1153-1241 (2 / 2A),
 //                  :1288-1340, :1369-1395
+//   DCI pack       phch/dci.c:415-490 (0), :579-639 (1), :710-795 (1A), :952-988 (1C), :1076-1151 (2/2A/2B),
+//                  :1243-1286, :1342-1367
 //   RA             phch/ra.c:37-250 (RIV, RBG size P, MCS -> I_TBS / modulation, TBS table)
 //                  phch/ra_dl.c:42-681 (PRB allocation types 0 / 1 / 2, TB sizes, RE count, MIMO)
-// Not provided (SRSRAN_ERROR): TDD, format 1B / 1C / 1D / 2B unpacking, distributed VRBs.
+// Not provided (SRSRAN_ERROR): TDD, format 1B / 1C / 1D / 2B unpacking, 1B / 1D packing, distributed VRBs.
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -355,6 +357,193 @@ int unpack_format2x(const srsran_cell_t* cell, srsran_dci_cfg_t* cfg, srsran_dci
   for (int i = 0; i < SRSRAN_MAX_CODEWORDS; i++) {
     dci->tb[i].cw_idx = nof_tb == 2 ? (uint32_t)(((dci->tb_cw_swap ? 1 : 0) + i) % nof_tb) : 0;
   }
+  return SRSRAN_SUCCESS;
+}
+
+// ---- DCI packing (the eNB side: srsran_enb_dl_put_pdcch_dl / _ul, dci.c:415-490, 579-639, 710-795,
+// 952-988, 1076-1151) ----
+void bit_put(uint8_t** y, uint32_t v, uint32_t n)  // MSB first, as srsran_bit_unpack
+{
+  for (uint32_t i = 0; i < n; i++) {
+    *(*y)++ = (uint8_t)((v >> (n - 1 - i)) & 1u);
+  }
+}
+
+// zero padding up to the format's size; the reference leaves its "reserved" bits as they were in a
+// message it zeroed first (enb_dl.c:390), so they are written as zeros here
+void pad_to(srsran_dci_msg_t* msg, uint8_t* y, uint32_t n)
+{
+  while ((uint32_t)(y - msg->payload) < n) {
+    *y++ = 0;
+  }
+  msg->nof_bits = (uint32_t)(y - msg->payload);
+}
+
+int pack_format0(const srsran_cell_t* cell, srsran_dl_sf_cfg_t* sf, const srsran_dci_cfg_t* cfg, const srsran_dci_ul_t* dci,
+                 srsran_dci_msg_t* msg)
+{
+  uint8_t* y = msg->payload;
+  if (dci->cif_present) {
+    bit_put(&y, dci->cif, 3);
+  }
+  *y++                = 0;  // format 0 / 1A flag
+  uint32_t n_ul_hop   = 0;
+  const bool hop      = dci->freq_hop_fl != srsran_dci_ul_t::SRSRAN_RA_PUSCH_HOP_DISABLED;
+  *y++                = hop ? 1 : 0;
+  if (hop) {
+    n_ul_hop = cell->nof_prb < 50 ? 1 : 2;  // 36.213 Table 8.4-1
+    bit_put(&y, (uint32_t)dci->freq_hop_fl, n_ul_hop);
+  }
+  const bool ue_ss = !cfg->is_not_ue_ss;
+  bit_put(&y, dci->type2_alloc.riv, riv_nbits(cell->nof_prb) - n_ul_hop);
+  bit_put(&y, dci->tb.mcs_idx, 5);
+  *y++ = dci->tb.ndi ? 1 : 0;
+  bit_put(&y, dci->tpc_pusch, 2);
+  bit_put(&y, dci->n_dmrs, 3);
+  *y++ = dci->cqi_request ? 1 : 0;
+  if (cfg->multiple_csi_request_enabled && ue_ss) {
+    *y++ = 0;
+  }
+  if (cfg->srs_request_enabled && ue_ss) {
+    *y++ = dci->srs_request && dci->srs_request_present ? 1 : 0;
+  }
+  pad_to(msg, y, srsran_dci_format_sizeof(cell, sf, const_cast<srsran_dci_cfg_t*>(cfg), SRSRAN_DCI_FORMAT0));
+  return SRSRAN_SUCCESS;
+}
+
+int pack_type01(const srsran_cell_t* cell, uint8_t** y, const srsran_dci_dl_t* dci)
+{
+  if (cell->nof_prb > 10) {
+    *(*y)++ = (uint8_t)dci->alloc_type;
+  }
+  const uint32_t P = srsran_ra_type0_P(cell->nof_prb), alloc_size = rbg_bits(cell->nof_prb);
+  switch (dci->alloc_type) {
+    case SRSRAN_RA_ALLOC_TYPE0:
+      bit_put(y, dci->type0_alloc.rbg_bitmask, alloc_size);
+      return SRSRAN_SUCCESS;
+    case SRSRAN_RA_ALLOC_TYPE1: {
+      const uint32_t lp = (uint32_t)ceilf(log2f((float)P));
+      bit_put(y, dci->type1_alloc.rbg_subset, lp);
+      *(*y)++ = dci->type1_alloc.shift ? 1 : 0;
+      bit_put(y, dci->type1_alloc.vrb_bitmask, alloc_size - lp - 1);
+      return SRSRAN_SUCCESS;
+    }
+    default:
+      fprintf(stderr, "[srsran_dci] formats 1 / 2 take resource allocation type 0 or 1\n");
+      return SRSRAN_ERROR;
+  }
+}
+
+int pack_format1(const srsran_cell_t* cell, srsran_dl_sf_cfg_t* sf, srsran_dci_cfg_t* cfg, const srsran_dci_dl_t* dci,
+                 srsran_dci_msg_t* msg)
+{
+  uint8_t* y = msg->payload;
+  if (dci->cif_present) {
+    bit_put(&y, dci->cif, 3);
+  }
+  if (pack_type01(cell, &y, dci)) {
+    return SRSRAN_ERROR;
+  }
+  bit_put(&y, dci->tb[0].mcs_idx, 5);
+  bit_put(&y, dci->pid, HARQ_PID_LEN);
+  *y++ = dci->tb[0].ndi ? 1 : 0;
+  bit_put(&y, (uint32_t)dci->tb[0].rv, 2);
+  bit_put(&y, dci->tpc_pucch, 2);
+  pad_to(msg, y, srsran_dci_format_sizeof(cell, sf, cfg, SRSRAN_DCI_FORMAT1));
+  return SRSRAN_SUCCESS;
+}
+
+int pack_format1A(const srsran_cell_t* cell, srsran_dl_sf_cfg_t* sf, srsran_dci_cfg_t* cfg, const srsran_dci_dl_t* dci,
+                  srsran_dci_msg_t* msg)
+{
+  uint8_t* y = msg->payload;
+  if (dci->cif_present) {
+    bit_put(&y, dci->cif, 3);
+  }
+  *y++ = 1;  // format 0 / 1A flag
+  if (dci->is_pdcch_order) {  // localized, RIV all ones, preamble and PRACH mask indices (36.212 5.3.3.1.3)
+    *y++ = 0;
+    bit_put(&y, 0xffffffffu, riv_nbits(cell->nof_prb));
+    bit_put(&y, dci->preamble_idx, 6);
+    bit_put(&y, dci->prach_mask_idx, 4);
+  } else {
+    if (dci->alloc_type != SRSRAN_RA_ALLOC_TYPE2) {
+      fprintf(stderr, "[srsran_dci] format 1A takes resource allocation type 2\n");
+      return SRSRAN_ERROR;
+    }
+    const bool user = SRSRAN_RNTI_ISUSER(dci->rnti);
+    const bool dist = dci->type2_alloc.mode == srsran_ra_type2_t::SRSRAN_RA_TYPE2_DIST;
+    *y++            = dist ? 1 : 0;
+    uint32_t nb_gap = 0;
+    if (user && dist && cell->nof_prb >= 50) {
+      nb_gap = 1;
+      *y++   = (uint8_t)dci->type2_alloc.n_gap;
+    }
+    bit_put(&y, dci->type2_alloc.riv, riv_nbits(cell->nof_prb) - nb_gap);
+    bit_put(&y, dci->tb[0].mcs_idx, 5);
+    bit_put(&y, dci->pid, HARQ_PID_LEN);
+    if (user) {
+      *y++ = dci->tb[0].ndi ? 1 : 0;
+    } else {
+      *y++ = cell->nof_prb >= 50 && dist ? (uint8_t)dci->type2_alloc.n_gap : 0;
+    }
+    bit_put(&y, (uint32_t)dci->tb[0].rv, 2);
+    if (user) {
+      bit_put(&y, 0, 2);  // TPC (not provided by the reference either)
+    } else {
+      *y++ = 0;  // TPC MSB reserved, LSB = N_PRB^1A for the TBS
+      *y++ = (uint8_t)dci->type2_alloc.n_prb1a;
+    }
+  }
+  pad_to(msg, y, srsran_dci_format_sizeof(cell, sf, cfg, SRSRAN_DCI_FORMAT1A));
+  return SRSRAN_SUCCESS;
+}
+
+int pack_format1C(const srsran_cell_t* cell, const srsran_dci_dl_t* dci, srsran_dci_msg_t* msg)
+{
+  uint8_t* y = msg->payload;
+  if (dci->cif_present) {
+    bit_put(&y, dci->cif, 3);
+  }
+  if (dci->alloc_type != SRSRAN_RA_ALLOC_TYPE2 || dci->type2_alloc.mode != srsran_ra_type2_t::SRSRAN_RA_TYPE2_DIST) {
+    fprintf(stderr, "[srsran_dci] format 1C takes distributed type 2 resource allocation\n");
+    return SRSRAN_ERROR;
+  }
+  if (cell->nof_prb >= 50) {
+    *y++ = (uint8_t)dci->type2_alloc.n_gap;
+  }
+  const uint32_t n_step   = cell->nof_prb < 50 ? 2 : 4;
+  const uint32_t n_vrb_dl = ra_type2_n_vrb_dl(cell->nof_prb, dci->type2_alloc.n_gap == srsran_ra_type2_t::SRSRAN_RA_TYPE2_NG1);
+  bit_put(&y, dci->type2_alloc.riv, riv_nbits(n_vrb_dl / n_step));
+  bit_put(&y, dci->tb[0].mcs_idx, 5);
+  msg->nof_bits = (uint32_t)(y - msg->payload);  // no padding (dci.c:986)
+  return SRSRAN_SUCCESS;
+}
+
+int pack_format2x(const srsran_cell_t* cell, srsran_dl_sf_cfg_t* sf, srsran_dci_cfg_t* cfg, const srsran_dci_dl_t* dci,
+                  srsran_dci_msg_t* msg)
+{
+  uint8_t* y = msg->payload;
+  if (dci->cif_present) {
+    bit_put(&y, dci->cif, 3);
+  }
+  if (pack_type01(cell, &y, dci)) {
+    return SRSRAN_ERROR;
+  }
+  bit_put(&y, dci->tpc_pucch, 2);
+  bit_put(&y, dci->pid, HARQ_PID_LEN);
+  *y++ = (msg->format == SRSRAN_DCI_FORMAT2B ? dci->sram_id : dci->tb_cw_swap) ? 1 : 0;
+  for (int i = 0; i < 2; i++) {
+    bit_put(&y, dci->tb[i].mcs_idx, 5);
+    *y++ = dci->tb[i].ndi ? 1 : 0;
+    bit_put(&y, (uint32_t)dci->tb[i].rv, 2);
+  }
+  if (msg->format == SRSRAN_DCI_FORMAT2) {
+    bit_put(&y, dci->pinfo, cell->nof_ports <= 2 ? 3 : 6);
+  } else if (msg->format == SRSRAN_DCI_FORMAT2A) {
+    bit_put(&y, dci->pinfo, cell->nof_ports <= 2 ? 0 : 2);
+  }
+  pad_to(msg, y, srsran_dci_format_sizeof(cell, sf, cfg, msg->format));
   return SRSRAN_SUCCESS;
 }
 
@@ -769,6 +958,51 @@ int srsran_dci_msg_unpack_pdsch(srsran_cell_t* cell, srsran_dl_sf_cfg_t* sf, srs
       fprintf(stderr, "[srsran_dci] unpacking of DCI format %d is not provided\n", (int)msg->format);
       return SRSRAN_ERROR;
   }
+}
+
+int srsran_dci_msg_pack_pdsch(srsran_cell_t* cell, srsran_dl_sf_cfg_t* sf, srsran_dci_cfg_t* cfg, srsran_dci_dl_t* dci,
+                              srsran_dci_msg_t* msg)
+{
+  if (!cell || !dci || !msg) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  msg->rnti     = dci->rnti;
+  msg->location = dci->location;
+  msg->format   = dci->format;
+  srsran_dci_cfg_t zero;
+  memset(&zero, 0, sizeof(zero));
+  if (!cfg) {
+    cfg = &zero;
+  }
+  switch (msg->format) {
+    case SRSRAN_DCI_FORMAT1:
+      return pack_format1(cell, sf, cfg, dci, msg);
+    case SRSRAN_DCI_FORMAT1A:
+      return pack_format1A(cell, sf, cfg, dci, msg);
+    case SRSRAN_DCI_FORMAT1C:
+      return pack_format1C(cell, dci, msg);
+    case SRSRAN_DCI_FORMAT2:
+    case SRSRAN_DCI_FORMAT2A:
+    case SRSRAN_DCI_FORMAT2B:
+      return pack_format2x(cell, sf, cfg, dci, msg);
+    default:
+      fprintf(stderr, "[srsran_dci] packing of DCI format %d is not provided\n", (int)msg->format);
+      return SRSRAN_ERROR;
+  }
+}
+
+int srsran_dci_msg_pack_pusch(srsran_cell_t* cell, srsran_dl_sf_cfg_t* sf, srsran_dci_cfg_t* cfg, srsran_dci_ul_t* dci,
+                              srsran_dci_msg_t* msg)
+{
+  if (!cell || !dci || !msg) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  msg->rnti     = dci->rnti;
+  msg->location = dci->location;
+  msg->format   = dci->format;
+  srsran_dci_cfg_t zero;
+  memset(&zero, 0, sizeof(zero));
+  return pack_format0(cell, sf, cfg ? cfg : &zero, dci, msg);
 }
 
 bool srsran_dci_location_isvalid(srsran_dci_location_t* c)

@@ -1,7 +1,8 @@
-// srsran_4g_amd/csrc/enb_dl_api.cpp -- eNB downlink transmit of PDSCH subframes on the GPU
-// (include/srsran_enb_dl.h): DL-SCH encoding (srsran_dlsch_gpu_encode_batch), CRS, scrambling +
-// modulation + precoding + RE mapping (llr_kernel.hip: pdsch_tx_kernel, crs_put_kernel) and the
-// OFDM modulator (ofdm_kernel.hip: ofdm_tx_kernel).  enb_dl.c:300-470, pdsch.c:1015-1120.
+// srsran_4g_amd/csrc/enb_dl_api.cpp -- eNB downlink transmit on the GPU (include/srsran_enb_dl.h):
+// DL-SCH encoding (srsran_dlsch_gpu_encode_batch), CRS, scrambling + modulation + precoding + RE mapping
+// (llr_kernel.hip: pdsch_tx_kernel, crs_put_kernel), the control channels (ctrl_tx_kernel: PSS / SSS,
+// PBCH, PCFICH, PDCCH) and the OFDM modulator (ofdm_kernel.hip: ofdm_tx_kernel).  enb_dl.c:300-470,
+// pdsch.c:1015-1120, pdcch.c:528-660, pcfich.c:185-235, pbch.c, pss.c / sss.c / gen_sss.c.
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdio.h>
@@ -29,6 +30,7 @@ struct EnbDlGpu {
   size_t        e_cap = 0;
   uint32_t*     d_idx = nullptr;   // RE tables of every subframe
   size_t        idx_cap = 0;
+  uint32_t      last_sf = 0;    // subframes in d_grid (srsran_enb_dl_gpu_sf_symbols)
   PdschTx*      d_items = nullptr;
   size_t        items_cap = 0;
   uint32_t*     d_sfidx = nullptr;
@@ -36,6 +38,14 @@ struct EnbDlGpu {
   // RE tables on the device, keyed by (PRB allocation, symbols a slot, first symbol, subframe): built
   // once, not re-uploaded every batch
   std::unordered_map<std::string, std::pair<uint32_t*, uint32_t>> tabs;
+  // control channels: REG tables of the cell, the PBCH REs, the PSS / SSS sequences (built at init)
+  srsran_regs_t regs{};
+  bool          regs_ok = false;
+  uint32_t*     d_ctab  = nullptr;  // [16 PCFICH][PBCH][PDCCH CFI 1][CFI 2][CFI 3]
+  uint32_t      pbch_off = 16, pbch_nsym = 0, pdcch_off[3] = {0, 0, 0};
+  float2*       d_sync  = nullptr;  // [PSS 72][SSS subframe 0: 72][SSS subframe 5: 72] (5 zero guards each side)
+  CtrlTxJob*    d_jobs  = nullptr;
+  size_t        jobs_cap = 0;
 };
 
 constexpr size_t kTabCache = 512;  // RE tables kept on the device
@@ -97,6 +107,177 @@ bool grow(void** p, size_t* cap, size_t need)
   return true;
 }
 
+
+// ---- control-channel tables ----
+// PSS of N_id_2 (pss.c:341-370: the reference's float / double mix kept), SSS of subframes 0 and 5
+// (36.211 6.11.2, gen_sss.c), each as 72 REs: 5 zero guards, 62 symbols, 5 zero guards (pss.c:372-379,
+// sss.c:105-119)
+void sync_sequences(uint32_t cell_id, std::vector<float2>& out)
+{
+  out.assign(3 * 72, make_float2(0.f, 0.f));
+  static const float root[3] = {25.0f, 29.0f, 34.0f};
+  const float        r       = root[cell_id % 3];
+  for (int i = 0; i < 62; i++) {
+    const double f   = i < 31 ? (double)(float)i * ((float)i + 1.0) : ((float)i + 2.0) * ((float)i + 1.0);
+    const float  arg = (float)((double)(float)-1 * M_PI * (double)r * f / 63.0);
+    out[5 + i]       = make_float2(cosf(arg), sinf(arg));
+  }
+  // m-sequences x(i + 5) = f(x) with x(0..4) = 0, 0, 0, 0, 1; tilde sequences 1 - 2 x
+  auto mseq = [](int taps, int* t) {
+    int x[31] = {0, 0, 0, 0, 1};
+    for (int i = 0; i < 26; i++) {
+      int v = 0;
+      for (int b = 0; b < 5; b++) {
+        if (taps & (1 << b)) {
+          v ^= x[i + b];
+        }
+      }
+      x[i + 5] = v;
+    }
+    for (int i = 0; i < 31; i++) {
+      t[i] = 1 - 2 * x[i];
+    }
+  };
+  int s_t[31], c_t[31], z_t[31];
+  mseq(0x05, s_t);  // x(i+2) + x(i)
+  mseq(0x09, c_t);  // x(i+3) + x(i)
+  mseq(0x17, z_t);  // x(i+4) + x(i+2) + x(i+1) + x(i)
+  const int N1 = (int)cell_id / 3, N2 = (int)cell_id % 3;
+  const int qp = N1 / 30, q = (N1 + qp * (qp + 1) / 2) / 30, mp = N1 + q * (q + 1) / 2;
+  const int m0 = mp % 31, m1 = (m0 + mp / 31 + 1) % 31;
+  for (int n = 0; n < 31; n++) {
+    const int s0 = s_t[(n + m0) % 31], s1 = s_t[(n + m1) % 31];
+    const int c0 = c_t[(n + N2) % 31], c1 = c_t[(n + N2 + 3) % 31];
+    const int z0 = z_t[(n + m0 % 8) % 31], z1 = z_t[(n + m1 % 8) % 31];
+    out[72 + 5 + 2 * n]      = make_float2((float)(s0 * c0), 0.f);
+    out[72 + 5 + 2 * n + 1]  = make_float2((float)(s1 * c1 * z0), 0.f);
+    out[144 + 5 + 2 * n]     = make_float2((float)(s1 * c0), 0.f);
+    out[144 + 5 + 2 * n + 1] = make_float2((float)(s0 * c1 * z1), 0.f);
+  }
+}
+
+// PBCH REs (pbch.c srsran_pbch_cp with put): slot 1, symbols 0..3, the 72 central subcarriers; symbols 0, 1
+// (and 3 with the extended CP) skip the CRS positions k mod 3 = cell_id mod 3 of any port count
+std::vector<uint32_t> pbch_res(const srsran_cell_t& cell)
+{
+  const uint32_t nre = 12 * cell.nof_prb, nsymb = SRSRAN_CP_NSYMB(cell.cp), k0 = nre / 2 - 36, v = cell.id % 3;
+  std::vector<uint32_t> t;
+  for (uint32_t l = 0; l < 4; l++) {
+    const bool crs = l < 2 || (l == 3 && cell.cp != SRSRAN_CP_NORM);
+    for (uint32_t r = 0; r < 72; r++) {
+      if (!crs || (k0 + r) % 3 != v) {
+        t.push_back((nsymb + l) * nre + k0 + r);
+      }
+    }
+  }
+  return t;
+}
+
+bool ctrl_init(EnbDlGpu* g, const srsran_cell_t& cell)
+{
+  if (srsran_regs_init_opts(&g->regs, cell, 1, false) != SRSRAN_SUCCESS) {
+    return false;
+  }
+  g->regs_ok = true;
+  std::vector<uint32_t> tab(g->regs.pcfich_re, g->regs.pcfich_re + 16);
+  const std::vector<uint32_t> pb = pbch_res(cell);
+  g->pbch_off                    = (uint32_t)tab.size();
+  g->pbch_nsym                   = (uint32_t)pb.size();
+  tab.insert(tab.end(), pb.begin(), pb.end());
+  for (int c = 0; c < 3; c++) {
+    g->pdcch_off[c] = (uint32_t)tab.size();
+    tab.insert(tab.end(), g->regs.pdcch_re[c], g->regs.pdcch_re[c] + 4 * (size_t)g->regs.pdcch_nregs[c]);
+  }
+  std::vector<float2> sync;
+  sync_sequences(cell.id, sync);
+  return hipMalloc((void**)&g->d_ctab, tab.size() * sizeof(uint32_t)) == hipSuccess &&
+         hipMemcpy(g->d_ctab, tab.data(), tab.size() * sizeof(uint32_t), hipMemcpyHostToDevice) == hipSuccess &&
+         hipMalloc((void**)&g->d_sync, sync.size() * sizeof(float2)) == hipSuccess &&
+         hipMemcpy(g->d_sync, sync.data(), sync.size() * sizeof(float2), hipMemcpyHostToDevice) == hipSuccess;
+}
+
+// the jobs of one subframe's control channels (enb_dl.c:333-428), appended to `jobs`
+int ctrl_jobs(EnbDlGpu* g, const srsran_cell_t& cell, const srsran_enb_dl_gpu_sf_t& s, float2* const* grid,
+              std::vector<CtrlTxJob>& jobs)
+{
+  const srsran_enb_dl_gpu_ctrl_t* c = s.ctrl;
+  const uint32_t sf = s.tti % 10, nre = 12 * cell.nof_prb, nsymb = SRSRAN_CP_NSYMB(cell.cp);
+  const uint32_t P = cell.nof_ports, cfi = s.cfi;
+  auto           base = [&](uint32_t kind) {
+    CtrlTxJob j;
+    memset(&j, 0, sizeof(j));
+    for (uint32_t p = 0; p < P; p++) {
+      j.grid[p] = grid[p];
+    }
+    j.kind   = kind;
+    j.nports = P;
+    return j;
+  };
+  if (c->put_base) {
+    if (sf == 0 || sf == 5) {  // put_sync: PSS in the last, SSS in the second last symbol of slot 0
+      CtrlTxJob j = base(2);
+      j.seq       = g->d_sync;
+      j.re0       = (nsymb - 1) * nre + nre / 2 - 36;
+      j.nsym      = 72;
+      jobs.push_back(j);
+      j.seq = g->d_sync + (sf == 0 ? 72 : 144);
+      j.re0 = (nsymb - 2) * nre + nre / 2 - 36;
+      jobs.push_back(j);
+    }
+    if (sf == 0) {  // put_mib: the MIB of SFN tti / 10, the (sfn mod 4)-th quarter of its rate-matched bits
+      CtrlTxJob j = base(0);
+      uint8_t   mib[24];
+      srsran_cell_t cl = cell;
+      srsran_pbch_mib_pack(&cl, s.tti / 10, mib);
+      memcpy(j.payload, mib, 24);
+      j.nof_bits = 24;
+      j.crc_mask = P == 2 ? 0xffffu : P == 4 ? 0x5555u : 0u;  // 36.212 Table 5.3.1.1-1
+      j.nsym     = g->pbch_nsym;
+      j.E        = 4 * 2 * g->pbch_nsym;
+      j.bit0     = ((s.tti / 10) % 4) * 2 * g->pbch_nsym;
+      j.seed     = cell.id;  // srsran_sequence_pbch
+      j.seq_off  = j.bit0;
+      j.re       = g->d_ctab + g->pbch_off;
+      jobs.push_back(j);
+    }
+    CtrlTxJob j = base(1);  // put_pcfich
+    j.nof_bits  = cfi;
+    j.nsym      = 16;
+    j.seed      = (sf + 1) * (2 * cell.id + 1) * 512 + cell.id;  // srsran_sequence_pcfich
+    j.re        = g->d_ctab;
+    jobs.push_back(j);
+  }
+  const uint32_t ncce = g->regs.pdcch_nregs[cfi - 1] / 9;
+  for (uint32_t d = 0; d < c->nof_dci; d++) {
+    const srsran_dci_msg_t& m = c->dci[d];
+    const uint32_t          L = m.location.L, n0 = m.location.ncce, ncc = 1u << L;
+    if (L > 3 || n0 + ncc > ncce || m.nof_bits >= SRSRAN_DCI_MAX_BITS - 16) {
+      fprintf(stderr, "[srsran_enb_dl] illegal DCI message nCCE %u, L %u, nof_cce %u, nof_bits %u\n", n0, L, ncce,
+              m.nof_bits);
+      return SRSRAN_ERROR;
+    }
+    CtrlTxJob j = base(0);
+    memcpy(j.payload, m.payload, m.nof_bits);
+    j.nof_bits = m.nof_bits;
+    j.crc_mask = m.rnti;
+    j.nsym     = 36 * ncc;
+    j.E        = 72 * ncc;
+    j.seed     = sf * 512 + cell.id;  // srsran_sequence_pdcch
+    j.seq_off  = 72 * n0;
+    j.re       = g->d_ctab + g->pdcch_off[cfi - 1] + 36 * n0;
+    for (uint32_t e = d + 1; e < c->nof_dci; e++) {  // CCEs a later message rewrites
+      const uint32_t a = c->dci[e].location.ncce, b = a + (1u << c->dci[e].location.L);
+      for (uint32_t k = 0; k < ncc; k++) {
+        if (n0 + k >= a && n0 + k < b) {
+          j.skip |= 1u << k;
+        }
+      }
+    }
+    jobs.push_back(j);
+  }
+  return SRSRAN_SUCCESS;
+}
+
 }  // namespace
 
 extern "C" {
@@ -123,6 +304,10 @@ int srsran_enb_dl_gpu_init(srsran_enb_dl_gpu_t* q, srsran_cell_t cell)
   }
   g->N      = g->ofdm.cfg.symbol_sz;
   g->sf_len = g->ofdm.sf_sz;
+  if (!ctrl_init(g, cell)) {
+    srsran_enb_dl_gpu_free(q);
+    return SRSRAN_ERROR;
+  }
   return SRSRAN_SUCCESS;
 }
 
@@ -141,6 +326,12 @@ void srsran_enb_dl_gpu_free(srsran_enb_dl_gpu_t* q)
     hipFree(g->d_idx);
     hipFree(g->d_items);
     hipFree(g->d_sfidx);
+    hipFree(g->d_ctab);
+    hipFree(g->d_sync);
+    hipFree(g->d_jobs);
+    if (g->regs_ok) {
+      srsran_regs_free(&g->regs);
+    }
     for (auto& kv : g->tabs) {
       hipFree(kv.second.first);
     }
@@ -174,11 +365,18 @@ int srsran_enb_dl_gpu_tx_batch(srsran_enb_dl_gpu_t*          q,
   size_t                              e_tot = 0;
   uint32_t                            max_nre = 0;
   tab_evict(g, nof_sf);
+  // the subframes with a PDSCH: items[0..npd) (pdsch_tx_kernel's grid.y), sfidx per subframe (CRS)
+  uint32_t npd = 0;
+  std::vector<uint32_t> pd_sf;
   for (uint32_t b = 0; b < nof_sf; b++) {
     const srsran_enb_dl_gpu_sf_t& s   = sfs[b];
     const srsran_pdsch_cfg_t*     cfg = s.cfg;
-    if (!cfg || s.cfi < 1 || s.cfi > 3) {
+    if (s.cfi < 1 || s.cfi > 3) {
       return SRSRAN_ERROR_INVALID_INPUTS;
+    }
+    sfidx[b] = s.tti % 10;
+    if (!cfg) {
+      continue;
     }
     const srsran_pdsch_grant_t& gr = cfg->grant;
     int                         scheme;
@@ -195,15 +393,14 @@ int srsran_enb_dl_gpu_tx_batch(srsran_enb_dl_gpu_t*          q,
               (int)gr.tx_scheme, P, gr.nof_tb);
       return SRSRAN_ERROR;
     }
-    sfidx[b]  = s.tti % 10;
     const uint32_t lstart = s.cfi + (cell.nof_prb < 10 ? 1 : 0);  // SRSRAN_NOF_CTRL_SYMBOLS
-    tables[b] = get_tab(g, cell, gr, lstart, sfidx[b]);
-    if (!tables[b].first) {
+    tables[npd]           = get_tab(g, cell, gr, lstart, sfidx[b]);
+    if (!tables[npd].first) {
       return SRSRAN_ERROR;
     }
-    const uint32_t nre = tables[b].second;
+    const uint32_t nre = tables[npd].second;
     max_nre            = std::max(max_nre, nre);
-    PdschTx& it        = items[b];
+    PdschTx& it        = items[npd];
     memset(&it, 0, sizeof(it));
     it.nre       = nre;
     it.scheme    = scheme;
@@ -217,7 +414,7 @@ int srsran_enb_dl_gpu_tx_batch(srsran_enb_dl_gpu_t*          q,
         continue;
       }
       const uint32_t Qm = srsran_mod_bits_x_symbol(tb.mod), Nl = gr.nof_layers != gr.nof_tb ? 2 : 1;
-      if (!s.d_data[t] || Qm == 0 || tb.nof_bits != nre * Qm * (scheme == 1 ? 1 : 1) || tb.tbs <= 0 || cw >= 2) {
+      if (!s.d_data[t] || Qm == 0 || tb.nof_bits != nre * Qm || tb.tbs <= 0 || cw >= 2) {
         fprintf(stderr, "[srsran_enb_dl] TB %u: nof_bits %u does not match %u REs x Qm %u\n", t, tb.nof_bits, nre, Qm);
         return SRSRAN_ERROR_INVALID_INPUTS;
       }
@@ -231,6 +428,8 @@ int srsran_enb_dl_gpu_tx_batch(srsran_enb_dl_gpu_t*          q,
     if ((scheme == 3) != (cw == 2)) {
       return SRSRAN_ERROR_INVALID_INPUTS;
     }
+    pd_sf.push_back(b);
+    npd++;
   }
   const size_t grid_bytes = (size_t)nof_sf * P * nre_sf * sizeof(float2);
   if (!grow((void**)&g->d_grid, &g->grid_cap, grid_bytes) || !grow((void**)&g->d_e, &g->e_cap, e_tot + 16) ||
@@ -240,9 +439,10 @@ int srsran_enb_dl_gpu_tx_batch(srsran_enb_dl_gpu_t*          q,
   }
   // device pointers of the codewords, tables and grids
   size_t k = 0;
-  for (uint32_t b = 0; b < nof_sf; b++) {
-    PdschTx& it = items[b];
-    it.idx      = tables[b].first;
+  for (uint32_t i = 0; i < npd; i++) {
+    PdschTx&       it = items[i];
+    const uint32_t b  = pd_sf[i];
+    it.idx            = tables[i].first;
     for (uint32_t p = 0; p < P; p++) {
       it.grid[p] = g->d_grid + ((size_t)b * P + p) * nre_sf;
     }
@@ -252,16 +452,69 @@ int srsran_enb_dl_gpu_tx_batch(srsran_enb_dl_gpu_t*          q,
       it.e[c]         = g->d_e + e_off[k];
     }
   }
-  if (srsran_dlsch_gpu_encode_batch(&g->sch, (uint32_t)enc.size(), enc.data(), st) != SRSRAN_SUCCESS ||
-      hipMemsetAsync(g->d_grid, 0, grid_bytes, st) != hipSuccess ||
-      hipMemcpyAsync(g->d_items, items.data(), nof_sf * sizeof(PdschTx), hipMemcpyHostToDevice, st) != hipSuccess ||
-      hipMemcpyAsync(g->d_sfidx, sfidx.data(), nof_sf * sizeof(uint32_t), hipMemcpyHostToDevice, st) != hipSuccess ||
-      crs_put_launch(g->d_grid, cell.nof_prb, cell.id, P, SRSRAN_CP_NSYMB(cell.cp), g->d_sfidx, nof_sf, st) != hipSuccess ||
-      pdsch_tx_launch(g->d_items, nof_sf, max_nre, st) != hipSuccess) {
+  // control channels of every subframe: one launch
+  std::vector<CtrlTxJob> jobs;
+  for (uint32_t b = 0; b < nof_sf; b++) {
+    if (!sfs[b].ctrl) {
+      continue;
+    }
+    float2* grid[4] = {nullptr, nullptr, nullptr, nullptr};
+    for (uint32_t p = 0; p < P; p++) {
+      grid[p] = g->d_grid + ((size_t)b * P + p) * nre_sf;
+    }
+    if ((sfs[b].ctrl->nof_dci && !sfs[b].ctrl->dci) || ctrl_jobs(g, cell, sfs[b], grid, jobs) != SRSRAN_SUCCESS) {
+      return SRSRAN_ERROR;
+    }
+  }
+  if (!grow((void**)&g->d_jobs, &g->jobs_cap, std::max<size_t>(jobs.size(), 1) * sizeof(CtrlTxJob))) {
     return SRSRAN_ERROR;
   }
+  if ((!enc.empty() && srsran_dlsch_gpu_encode_batch(&g->sch, (uint32_t)enc.size(), enc.data(), st) != SRSRAN_SUCCESS) ||
+      hipMemsetAsync(g->d_grid, 0, grid_bytes, st) != hipSuccess ||
+      (npd && hipMemcpyAsync(g->d_items, items.data(), npd * sizeof(PdschTx), hipMemcpyHostToDevice, st) != hipSuccess) ||
+      hipMemcpyAsync(g->d_sfidx, sfidx.data(), nof_sf * sizeof(uint32_t), hipMemcpyHostToDevice, st) != hipSuccess ||
+      (!jobs.empty() &&
+       hipMemcpyAsync(g->d_jobs, jobs.data(), jobs.size() * sizeof(CtrlTxJob), hipMemcpyHostToDevice, st) != hipSuccess) ||
+      crs_put_launch(g->d_grid, cell.nof_prb, cell.id, P, SRSRAN_CP_NSYMB(cell.cp), g->d_sfidx, nof_sf, st) != hipSuccess ||
+      ctrl_tx_launch(g->d_jobs, (uint32_t)jobs.size(), st) != hipSuccess ||
+      pdsch_tx_launch(g->d_items, npd, max_nre, st) != hipSuccess) {
+    return SRSRAN_ERROR;
+  }
+  g->last_sf = nof_sf;
   const float sc = scale > 0.0f ? scale : 0.05f / sqrtf((float)cell.nof_prb);  // enb_dl_get_norm_factor
   return srsran_ofdm_tx_gpu(&g->ofdm, (const cf_t*)g->d_grid, d_samples, P, nof_sf, sc, st);
+}
+
+const cf_t* srsran_enb_dl_gpu_sf_symbols(srsran_enb_dl_gpu_t* q)
+{
+  return q && q->gpu && ((EnbDlGpu*)q->gpu)->last_sf ? (const cf_t*)((EnbDlGpu*)q->gpu)->d_grid : nullptr;
+}
+
+void srsran_pbch_mib_pack(srsran_cell_t* cell, uint32_t sfn, uint8_t* payload)
+{
+  // 36.331 MasterInformationBlock: dl-Bandwidth (3), phich-Duration (1), phich-Resource (2), SFN / 4 (8),
+  // spare (10)
+  const uint32_t bw  = cell->nof_prb <= 6 ? 0 : cell->nof_prb <= 15 ? 1 : 1 + cell->nof_prb / 25;
+  uint32_t       res = 0;
+  switch (cell->phich_resources) {
+    case SRSRAN_PHICH_R_1_6:
+      res = 0;
+      break;
+    case SRSRAN_PHICH_R_1_2:
+      res = 1;
+      break;
+    case SRSRAN_PHICH_R_1:
+      res = 2;
+      break;
+    case SRSRAN_PHICH_R_2:
+      res = 3;
+      break;
+  }
+  const uint32_t v = (bw << 21) | ((cell->phich_length == SRSRAN_PHICH_EXT ? 1u : 0u) << 20) | (res << 18) |
+                     (((sfn >> 2) & 0xffu) << 10);
+  for (int i = 0; i < 24; i++) {
+    payload[i] = (uint8_t)((v >> (23 - i)) & 1u);
+  }
 }
 
 }  // extern "C"

@@ -54,5 +54,28 @@ hipError_t pdsch_tx_launch(const PdschTx* d_items, uint32_t nitems, uint32_t max
 hipError_t crs_put_launch(float2* d_grids, uint32_t nof_prb, uint32_t cell_id, uint32_t nports, uint32_t nsymb,
                           const uint32_t* d_sf_idx, uint32_t nsf, hipStream_t stream);
 
+// One control-channel transmission of one subframe (enb_dl.c:333-420): bits -> scrambling -> QPSK ->
+// transmit-diversity precoding -> REs, or a sequence copied as it is onto every port (PSS / SSS).
+struct CtrlTxJob {
+  float2*         grid[4];   // the subframe's port grids (2 nsymb x 12 nof_prb)
+  const uint32_t* re;        // RE (k + l * 12 nof_prb) of each symbol; null: re0 + symbol index
+  const float2*   seq;       // kind 2: the symbols (device)
+  uint32_t        re0;
+  uint32_t        nsym;      // symbols written (a multiple of nports for kinds 0 / 1)
+  uint32_t        kind;      // 0: CRC16 + tail-biting convolutional code + rate matching (DCI, BCH);
+                             // 1: the CFI codeword of cfi = nof_bits; 2: sequence
+  uint32_t        nports;
+  uint32_t        nof_bits;  // kind 0: payload bits before the CRC; kind 1: the CFI
+  uint32_t        E;         // kind 0: rate-matched length
+  uint32_t        bit0;      // kind 0: first rate-matched bit transmitted
+  uint32_t        seed;      // scrambling: c_init
+  uint32_t        seq_off;   // scrambling: sequence offset of the first transmitted bit
+  uint32_t        crc_mask;  // kind 0: 16-bit CRC mask (RNTI, or the BCH antenna-port mask)
+  uint32_t        skip;      // kind 0 (DCI): bit c set = CCE c of the message is not written (a later one
+                             // takes it, as the reference's sequential puts overwrite)
+  uint8_t         payload[128];  // kind 0: payload bits, one a byte
+};
+hipError_t ctrl_tx_launch(const CtrlTxJob* d_jobs, uint32_t njobs, hipStream_t stream);
+
 }  // namespace srsran_amd
 #endif

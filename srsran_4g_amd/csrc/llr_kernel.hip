@@ -824,4 +824,137 @@ hipError_t crs_put_launch(float2* d_grids, uint32_t nof_prb, uint32_t cell_id, u
   return hipGetLastError();
 }
 
+// ---------------- control channels (enb_dl.c:333-420; pdcch.c:528-660, pcfich.c:185-235, pbch.c) ----------------
+static constexpr int CC_NCOLS = 32;
+__constant__ uint8_t kCcPerm[CC_NCOLS] = {1, 17, 9, 25, 5, 21, 13, 29, 3, 19, 11, 27, 7, 23, 15, 31,
+                                          0, 16, 8, 24, 4, 20, 12, 28, 2, 18, 10, 26, 6, 22, 14, 30};
+
+// bit k of the rate-matched tail-biting code of data[0..F) (rm_conv.c:40-90 bit collection over the
+// sub-block interleaver, convcoder.c with polynomials 0x6D, 0x4F, 0x57 and K = 7)
+__device__ __forceinline__ uint32_t cc_rm_bit(const uint8_t* data, int F, int k)
+{
+  const int nrows = (F - 1) / CC_NCOLS + 1, Kp = nrows * CC_NCOLS, nd = Kp - F, nv = 3 * F;
+  int       r = k % nv;
+  const int st = r / F;
+  r -= st * F;
+  int col = 0;
+  for (; col < CC_NCOLS; col++) {  // the rank r among the column-ordered non-dummy entries
+    const int cnt = nrows - (kCcPerm[col] < nd ? 1 : 0);
+    if (r < cnt) {
+      break;
+    }
+    r -= cnt;
+  }
+  const int row = r + (kCcPerm[col] < nd ? 1 : 0);
+  const int bi  = row * CC_NCOLS + kCcPerm[col] - nd;  // encoder input bit
+  uint32_t  sr  = 0;
+  for (int t = bi - 6; t <= bi; t++) {
+    sr = (sr << 1) | data[(t + F) % F];
+  }
+  const uint32_t poly = st == 0 ? 0x6Du : st == 1 ? 0x4Fu : 0x57u;
+  return (uint32_t)__popc(sr & poly) & 1u;
+}
+
+// One 64-lane workgroup per job; a lane writes one transmit-diversity group (nports symbols) at a time.
+__global__ __launch_bounds__(64) void ctrl_tx_kernel(const CtrlTxJob* __restrict__ jobs)
+{
+  const CtrlTxJob& j    = jobs[blockIdx.x];
+  const int        lane = threadIdx.x;
+  const uint32_t   P    = j.nports;
+  if (j.kind == 2) {
+    for (uint32_t s = lane; s < j.nsym; s += 64) {
+      const float2   v   = j.seq[s];
+      const uint32_t idx = j.re ? j.re[s] : j.re0 + s;
+      for (uint32_t p = 0; p < P; p++) {
+        j.grid[p][idx] = v;
+      }
+    }
+    return;
+  }
+  __shared__ uint8_t data[128 + 16];
+  const int          F = (int)j.nof_bits + 16;
+  if (j.kind == 0) {
+    for (uint32_t i = lane; i < j.nof_bits; i += 64) {
+      data[i] = j.payload[i] & 1u;
+    }
+    if (lane == 0) {  // CRC16 (0x1021) of the payload, MSB first, masked (srsran_crc_attach + mask)
+      uint32_t crc = 0;
+      for (uint32_t i = 0; i < j.nof_bits; i++) {
+        const uint32_t fb = ((crc >> 15) ^ j.payload[i]) & 1u;
+        crc               = (crc << 1) & 0xffffu;
+        crc ^= fb ? 0x1021u : 0u;
+      }
+      crc ^= j.crc_mask;
+      for (int i = 0; i < 16; i++) {
+        data[j.nof_bits + i] = (uint8_t)((crc >> (15 - i)) & 1u);
+      }
+    }
+    __syncthreads();
+  }
+  const float h = P == 4 ? (float)(1.0f / 1.41421356237309504880) : (float)(1.0 * 0.70710678118654752440);
+  const float a = (float)0.70710678118654752440;  // QPSK (lte_tables.c)
+  for (uint32_t g = lane; g * P < j.nsym; g += 64) {
+    const uint32_t s0 = g * P;
+    if (j.kind == 0 && ((j.skip >> (s0 / 36)) & 1u)) {
+      continue;
+    }
+    uint32_t x1, x2;
+    gold_at(j.seed, j.seq_off + 2 * s0, x1, x2);
+    const uint32_t c = gold16(x1, x2);
+    float2         d[4];
+    for (uint32_t q = 0; q < P; q++) {
+      uint32_t b[2];
+      for (int hb = 0; hb < 2; hb++) {
+        const uint32_t i = 2 * (s0 + q) + hb;
+        const uint32_t e = j.kind == 1 ? (uint32_t)((i % 3) != j.nof_bits - 1) : cc_rm_bit(data, F, (int)(j.bit0 + i));
+        b[hb]            = e ^ ((c >> (2 * q + hb)) & 1u);
+      }
+      d[q] = make_float2(b[0] ? -a : a, b[1] ? -a : a);
+    }
+    uint32_t idx[4];
+    for (uint32_t q = 0; q < P; q++) {
+      idx[q] = j.re ? j.re[s0 + q] : j.re0 + s0 + q;
+    }
+    if (P == 1) {
+      j.grid[0][idx[0]] = d[0];
+    } else if (P == 2) {  // layermap_diversity + precoding_diversity, 2 ports (precoding.c:1943-1960)
+      j.grid[0][idx[0]] = make_float2(d[0].x * h, d[0].y * h);
+      j.grid[1][idx[0]] = make_float2(-d[1].x * h, d[1].y * h);
+      j.grid[0][idx[1]] = make_float2(d[1].x * h, d[1].y * h);
+      j.grid[1][idx[1]] = make_float2(d[0].x * h, -d[0].y * h);
+    } else {  // 4 ports (precoding.c:1961-1988): SFBC on ports (0, 2) then (1, 3)
+      const float2 z = make_float2(0.f, 0.f);
+      j.grid[0][idx[0]] = make_float2(d[0].x * h, d[0].y * h);
+      j.grid[1][idx[0]] = z;
+      j.grid[2][idx[0]] = make_float2(-d[1].x * h, d[1].y * h);
+      j.grid[3][idx[0]] = z;
+      j.grid[0][idx[1]] = make_float2(d[1].x * h, d[1].y * h);
+      j.grid[1][idx[1]] = z;
+      j.grid[2][idx[1]] = make_float2(d[0].x * h, -d[0].y * h);
+      j.grid[3][idx[1]] = z;
+      j.grid[0][idx[2]] = z;
+      j.grid[1][idx[2]] = make_float2(d[2].x * h, d[2].y * h);
+      j.grid[2][idx[2]] = z;
+      j.grid[3][idx[2]] = make_float2(-d[3].x * h, d[3].y * h);
+      j.grid[0][idx[3]] = z;
+      j.grid[1][idx[3]] = make_float2(d[3].x * h, d[3].y * h);
+      j.grid[2][idx[3]] = z;
+      j.grid[3][idx[3]] = make_float2(d[2].x * h, -d[2].y * h);
+    }
+  }
+}
+
+hipError_t ctrl_tx_launch(const CtrlTxJob* d_jobs, uint32_t njobs, hipStream_t stream)
+{
+  if (njobs == 0) {
+    return hipSuccess;
+  }
+  hipError_t e = gold_tables_init();
+  if (e != hipSuccess) {
+    return e;
+  }
+  hipLaunchKernelGGL(ctrl_tx_kernel, dim3(njobs), dim3(64), 0, stream, d_jobs);
+  return hipGetLastError();
+}
+
 }  // namespace srsran_amd

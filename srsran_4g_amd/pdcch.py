@@ -126,6 +126,10 @@ def lib():
                                           ctypes.c_uint16, ctypes.POINTER(srsran_dci_ul_t)], ctypes.c_int),
             "srsran_dci_msg_unpack_pusch": ([ctypes.POINTER(srsran_cell_t), SF, DC, M, ctypes.POINTER(srsran_dci_ul_t)],
                                             ctypes.c_int),
+            "srsran_dci_msg_pack_pdsch": ([ctypes.POINTER(srsran_cell_t), SF, DC, ctypes.POINTER(srsran_dci_dl_t), M],
+                                          ctypes.c_int),
+            "srsran_dci_msg_pack_pusch": ([ctypes.POINTER(srsran_cell_t), SF, DC, ctypes.POINTER(srsran_dci_ul_t), M],
+                                          ctypes.c_int),
             "srsran_ue_dl_set_mi_auto": ([ctypes.POINTER(srsran_ue_dl_t)], None),
             "srsran_ue_dl_set_mi_manual": ([ctypes.POINTER(srsran_ue_dl_t), u32], None),
             "srsran_ue_dl_set_mbsfn_area_id": ([ctypes.POINTER(srsran_ue_dl_t), ctypes.c_uint16], ctypes.c_int),
@@ -152,6 +156,22 @@ def unpack_pusch(c, msg, cfg=None):
     r = lib().srsran_dci_msg_unpack_pusch(ctypes.byref(c), None, ctypes.byref(cfg) if cfg is not None else None,
                                           ctypes.byref(msg), ctypes.byref(d))
     return r, d
+
+
+def pack_pdsch(c, dci, cfg=None):
+    """srsran_dci_msg_pack_pdsch -> (ret, srsran_dci_msg_t)"""
+    m = srsran_dci_msg_t()
+    r = lib().srsran_dci_msg_pack_pdsch(ctypes.byref(c), None, ctypes.byref(cfg) if cfg is not None else None,
+                                        ctypes.byref(dci), ctypes.byref(m))
+    return r, m
+
+
+def pack_pusch(c, dci, cfg=None):
+    """srsran_dci_msg_pack_pusch -> (ret, srsran_dci_msg_t)"""
+    m = srsran_dci_msg_t()
+    r = lib().srsran_dci_msg_pack_pusch(ctypes.byref(c), None, ctypes.byref(cfg) if cfg is not None else None,
+                                        ctypes.byref(dci), ctypes.byref(m))
+    return r, m
 
 
 class Regs:

@@ -68,6 +68,29 @@ def pmc_traffic(workload, kernel, units):
     return int(round(e["bytes"] * units / e["units"]))
 
 
+def trace_traffic(roof, workload):
+    """roofline.traffic_source: the PMC summary the traffic figure of roof["kernel"] comes from"""
+    if not isinstance(roof, dict) or "traffic" not in roof:
+        return
+    e = pmc_entry(workload, roof.get("kernel"))
+    roof["traffic_source"] = e.get("source") if e and roof.get("traffic") is not None else None
+
+
+def emit(result, workload):
+    trace_traffic(result.get("roofline"), workload)
+    for key in ("pdsch", "pusch"):
+        sub = result.get(key)
+        if isinstance(sub, dict):
+            trace_traffic(sub.get("roofline"), key)
+            for k, fe in (sub.get("front_end_roofline") or {}).items():
+                fe.setdefault("kernel", k)
+                trace_traffic(fe, key)
+    for k, fe in (result.get("front_end_roofline") or {}).items():
+        fe.setdefault("kernel", k)
+        trace_traffic(fe, workload)
+    print(json.dumps(result), flush=True)
+
+
 def shard(rank):
     """Per-rank unit of work (independent carriers / CB batches, no data-path collective):
     rank r decodes its own carrier (cell id 1 + r) from its own seeded synthetic inputs."""
@@ -340,6 +363,9 @@ def run_dlsch(args, torch, dist, world, rank, device):
     d = per_stage[dom]
     bytes_per_launch = sb_[dom] / d["launches_per_step"]
     achieved = bytes_per_launch / (d["avg_launch_ms"] * 1e-3) / 1e9
+    if dom == "tdec_kernel":  # the turbo stage's kernel as it ran (srsran_tdec_gpu_last_kernel)
+        from srsran_4g_amd import tdec as TD
+        dom = TD.last_kernel()
     result = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -372,7 +398,7 @@ def run_dlsch(args, torch, dist, world, rank, device):
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5),
-            "traffic": pmc_traffic(args.workload, dom, ntb * 13) if dom == "tdec_kernel" else None,
+            "traffic": pmc_traffic(args.workload, dom, ntb * 13),
             "avg_launch_ms": d["avg_launch_ms"],
             "algo_bytes_per_launch": int(bytes_per_launch),
         },
@@ -401,7 +427,7 @@ def run_dlsch(args, torch, dist, world, rank, device):
     if world > 1:
         dist.destroy_process_group()
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        emit(result, args.workload)
 
 
 C3_NRE = {0: 13992, 5: 14256}  # PDSCH REs of the C3 grant per subframe index (others: 14400)
@@ -531,6 +557,9 @@ def run_pusch(args, torch, dist, world, rank, device, steps=None, warmup=None, c
     bytes_per_launch = sb_.get(dom, 0) / d["launches_per_step"]
     achieved = bytes_per_launch / (d["avg_launch_ms"] * 1e-3) / 1e9
     fe = [k for k in ("chest_ul_kernel", "pusch_eq_idft_kernel") if k in per_stage]
+    if dom == "tdec_kernel":  # the turbo stage's kernel as it ran (srsran_tdec_gpu_last_kernel)
+        from srsran_4g_amd import tdec as TD
+        dom = TD.last_kernel()
     result = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -560,7 +589,7 @@ def run_pusch(args, torch, dist, world, rank, device, steps=None, warmup=None, c
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5),
-            "traffic": pmc_traffic("pusch", "tdec_kernel<16, true>", nue) if dom == "tdec_kernel" else None,
+            "traffic": pmc_traffic("pusch", dom, nue),
             "avg_launch_ms": d["avg_launch_ms"],
             "algo_bytes_per_launch": int(bytes_per_launch),
         },
@@ -583,7 +612,7 @@ def run_pusch(args, torch, dist, world, rank, device, steps=None, warmup=None, c
     if world > 1:
         dist.destroy_process_group()
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        emit(result, args.workload)
 
 
 def pusch_cpu_baseline(pool, cell_id, dm, rnti, args, budget_s):
@@ -678,7 +707,7 @@ def run_dlenc(args, torch, dist, world, rank, device):
     if world > 1:
         dist.destroy_process_group()
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        emit(result, args.workload)
 
 
 def run_dlloop(args, torch, dist, world, rank, device):
@@ -770,7 +799,7 @@ def run_dlloop(args, torch, dist, world, rank, device):
         "payloads_equal": match,
     }
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        emit(result, args.workload)
     enb.free()
     ue.free()
     return result
@@ -953,7 +982,7 @@ def run_pdsch(args, torch, dist, world, rank, device, steps=None, warmup=None, c
     if world > 1:
         dist.destroy_process_group()
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        emit(result, args.workload)
     return result
 
 
@@ -1099,7 +1128,7 @@ def run_ldpc(args, torch, dist, world, rank, device):
     if world > 1:
         dist.destroy_process_group()
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        emit(result, args.workload)
 
 
 NR_PRB, NR_QM, NR_R = 273, 8, 948.0 / 1024.0  # 100 MHz @ 30 kHz, MCS 27 of the 256QAM table (38.214 5.1.3.1-2)
@@ -1251,7 +1280,7 @@ def run_nrsch(args, torch, dist, world, rank, device):
     if world > 1:
         dist.destroy_process_group()
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        emit(result, args.workload)
 
 
 def main():
@@ -1515,7 +1544,7 @@ def main():
     if world > 1:
         dist.destroy_process_group()
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        emit(result, args.workload)
 
 
 if __name__ == "__main__":

@@ -777,6 +777,12 @@ uint32_t tdec16s_min_cb() { return __atomic_load_n(&g_single_min_cb, __ATOMIC_RE
 // (K = 512: 0.060 vs 0.085 ms at 512, 0.081 vs 0.086 ms at 1024) and the single-lane decoder is ahead on
 // the fused class launch (32 sizes x 256 = 8192 blocks: 0.30 vs 0.53 ms): from 4096 blocks by default.
 static uint32_t g_single8_min_cb = 4096u;
+// srsran_tdec_gpu_set_split_threshold(): launches of at most this many blocks run the single-lane
+// decoders' split variant (tdecs_kernel.hip split_kernel: two helper waves take the other direction's
+// recomputation of phase 2 off the main waves; one workgroup of 4 waves per CU)
+static uint32_t g_split_max_cb = 1024u;
+void     tdecs_set_split_max_cb(uint32_t n) { __atomic_store_n(&g_split_max_cb, n, __ATOMIC_RELAXED); }
+uint32_t tdecs_split_max_cb() { return __atomic_load_n(&g_split_max_cb, __ATOMIC_RELAXED); }
 void     tdec8s_set_min_cb(uint32_t n) { __atomic_store_n(&g_single8_min_cb, n, __ATOMIC_RELAXED); }
 uint32_t tdec8s_min_cb() { return __atomic_load_n(&g_single8_min_cb, __ATOMIC_RELAXED); }
 // srsran_tdec_gpu_set_generic_single_threshold(): the generic class (K <= 400) keeps tdec_kernel.hip's

@@ -390,6 +390,10 @@ void srsran_tdec_gpu_set_pair_threshold(uint32_t nof_cb) { tdec16_set_min_cb(nof
 
 uint32_t srsran_tdec_gpu_get_pair_threshold(void) { return tdec16_min_cb(); }
 
+void srsran_tdec_gpu_set_split_threshold(uint32_t nof_cb) { tdecs_set_split_max_cb(nof_cb); }
+
+uint32_t srsran_tdec_gpu_get_split_threshold(void) { return tdecs_split_max_cb(); }
+
 void srsran_tdec_gpu_set_class_single_threshold(uint32_t nof_subblocks, uint32_t nof_cb)
 {
   if (nof_subblocks == 16) {
@@ -424,11 +428,11 @@ const char* srsran_tdec_gpu_kernel_name_batch(uint32_t long_cb, uint32_t nof_cb)
   if (nsb == 16) {
     const int k = tdec16_choice(nof_cb);
     if (k) {
-      return k == 2 ? "tdec16s_kernel" : "tdec16_kernel";
+      return k == 2 ? (nof_cb <= tdecs_split_max_cb() ? "tdec16s_split_kernel" : "tdec16s_kernel") : "tdec16_kernel";
     }
   }
   if (nsb == 8 && nof_cb >= tdec8s_min_cb()) {
-    return "tdec8s_kernel";
+    return nof_cb <= tdecs_split_max_cb() ? "tdec8s_split_kernel" : "tdec8s_kernel";
   }
   if (nsb == 1 && nof_cb >= tdec1s_min_cb()) {
     return "tdec1s_kernel";

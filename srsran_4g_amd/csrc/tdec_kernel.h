@@ -93,6 +93,8 @@ SRSRAN_TDECS_API(tdecs1)  // tdec1s_kernel.hip: the generic decoder (K <= 400), 
 #undef SRSRAN_TDECS_API
 bool       tdec8s_eligible(int nsb, const TdecArgs& a);
 bool       tdec1s_eligible(int nsb, const TdecArgs& a);
+void       tdecs_set_split_max_cb(uint32_t n);
+uint32_t   tdecs_split_max_cb();
 void       tdec8s_set_min_cb(uint32_t n);
 uint32_t   tdec8s_min_cb();
 void       tdec1s_set_min_cb(uint32_t n);

@@ -1,6 +1,7 @@
 """The two decoders of the 16-sub-block class on the SB layout, each forced onto small batches: the lane
-pair (tdec16_kernel.hip; by itself from 512 blocks a launch) and the single lane per sub-block
-(tdec16s_kernel.hip; by itself from srsran_tdec_gpu_get_single_threshold() blocks): every K >= 816 of
+pair (tdec16_kernel.hip; by itself from 512 blocks a launch), the single lane per sub-block
+(tdecs_kernel.hip; by itself from srsran_tdec_gpu_get_single_threshold() blocks) and its split variant
+(two helper waves; by itself up to srsran_tdec_gpu_get_split_threshold() blocks): every K >= 816 of
 the bit-exact suites again, plain batches with block counts that leave workgroups partly empty, the
 multi-size fused launch, and DL-SCH transport blocks with CRC early stop over HARQ."""
 import numpy as np
@@ -11,18 +12,20 @@ from oracle import CB_SIZES, Oracle, make_llrs
 pytestmark = pytest.mark.gpu
 
 
-KERNELS = {"pair": ("tdec16_kernel", 0, 1 << 30), "single": ("tdec16s_kernel", 0, 0)}
+NEVER = 1 << 30
+KERNELS = {"pair": ("tdec16_kernel", 0, NEVER, 0), "single": ("tdec16s_kernel", 0, 0, 0),
+           "split": ("tdec16s_split_kernel", 0, 0, NEVER)}
 
 
 @pytest.fixture(scope="module", autouse=True, params=sorted(KERNELS))
 def kernel(request):
-    """every test twice: the lane-pair decoder (tdec16_kernel.hip) and the single-lane decoder
-    (tdec16s_kernel.hip), each forced onto every batch size"""
+    """every test three times: the lane-pair decoder (tdec16_kernel.hip), the single-lane decoder
+    (tdecs_kernel.hip) and its split variant with helper waves, each forced onto every batch size"""
     from srsran_4g_amd import tdec
     if not tdec.gpu_available():
         pytest.skip("no HIP device")
-    name, pair_min, single_min = KERNELS[request.param]
-    with tdec.pair_threshold(pair_min), tdec.single_threshold(single_min):
+    name, pair_min, single_min, split_max = KERNELS[request.param]
+    with tdec.pair_threshold(pair_min), tdec.single_threshold(single_min), tdec.split_threshold(split_max):
         yield name
 
 
@@ -76,7 +79,7 @@ def test_multi_size_launch(ora, kernel):
     tdec.gpu_run_multi(Ks, [t.data_ptr() for t in ins], [t.shape[1] for t in ins], True,
                        [t.data_ptr() for t in outs], [t.shape[0] for t in ins], 8, None)
     torch.cuda.synchronize()
-    assert tdec.last_kernel() == kernel.replace("_kernel", "_multi_kernel")
+    assert tdec.last_kernel() == kernel.replace("_split", "").replace("_kernel", "_multi_kernel")
     for K, o, w in zip(Ks, outs, want):
         assert np.array_equal(o.cpu().numpy(), w), K
 

@@ -13,13 +13,14 @@ pytestmark = pytest.mark.gpu
 K8 = [k for k in CB_SIZES if 408 <= k <= 800]
 
 
-@pytest.fixture(scope="module", autouse=True)
-def single():
+@pytest.fixture(scope="module", autouse=True, params=["tdec8s_kernel", "tdec8s_split_kernel"])
+def kname(request):
+    """every test twice: the single-lane decoder and its split variant (helper waves)"""
     from srsran_4g_amd import tdec
     if not tdec.gpu_available():
         pytest.skip("no HIP device")
-    with tdec.single_threshold(0):
-        yield
+    with tdec.single_threshold(0), tdec.split_threshold(1 << 30 if "split" in request.param else 0):
+        yield request.param
 
 
 @pytest.fixture(scope="module")
@@ -27,7 +28,7 @@ def ora():
     return Oracle()
 
 
-def test_all_8class_sizes_bit_exact(ora):
+def test_all_8class_sizes_bit_exact(ora, kname):
     from srsran_4g_amd import tdec
     assert len(K8) == 32 and all(tdec.nof_subblocks(k) == 8 for k in K8)
     rng = np.random.default_rng(801)
@@ -38,7 +39,7 @@ def test_all_8class_sizes_bit_exact(ora):
         sb = np.stack([ora.natural_to_sb(K, x) for x in llr])
         if not np.array_equal(dec.run_all_batch(sb, 8, K), ora.run_batch(K, sb, True, 8)):
             bad.append(K)
-        assert tdec.last_kernel() == "tdec8s_kernel<false>"
+        assert tdec.last_kernel() == kname + "<false>"
     dec.free()
     assert not bad, bad
 
@@ -76,7 +77,7 @@ def test_multi_size_launch(ora):
         assert np.array_equal(o.cpu().numpy(), w), K
 
 
-def test_dlsch_early_stop_harq(ora):
+def test_dlsch_early_stop_harq(ora, kname):
     """single-CB TBs (CRC24A; every TB of an 8-class K is one code block), rv 0 -> 2 -> 3 at low SNR"""
     from srsran_4g_amd import sch, tdec
     rng = np.random.default_rng(830)
@@ -92,7 +93,7 @@ def test_dlsch_early_stop_harq(ora):
             llr = np.trunc(100 * (e + rng.standard_normal(e.shape).astype(np.float32) * sigma)).astype(np.int16)
             q.set_max_noi(8)
             ret, data, avg = q.decode(sb, tbs, Qm, rv, llr)
-            assert tdec.last_kernel() == "tdec8s_kernel<true>"
+            assert tdec.last_kernel() == kname + "<true>"
             oret, odata, _, oavg, state = ora.dlsch_decode(tbs, Qm, rv, llr, 8, state)
             assert ret == oret, (tbs, rv)
             assert np.array_equal(data[: len(odata)], odata), (tbs, rv)

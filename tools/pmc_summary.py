@@ -10,8 +10,10 @@ import sys
 
 
 def short(name):
-    n = name.split("(")[0].replace("void ", "").replace("srsran_amd::", "")
-    return n
+    """kernel name as bench.py / srsran_tdec_gpu_last_kernel report it: no argument list, no namespace"""
+    n = name.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
+    head, sep, tail = n.partition("<")
+    return head.split("::")[-1] + sep + tail
 
 
 def main(d, workload, out):

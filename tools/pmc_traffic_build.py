@@ -1,0 +1,60 @@
+"""Build profiles/pmc_traffic.json (bench.py's roofline.traffic table) from the committed PMC summaries
+of one round (tools/pmc_summary.py output copied to profiles/<round>_pmc_<workload>.json).
+
+  python tools/pmc_traffic_build.py r03
+
+Per workload and kernel: bytes = HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, KiB -> bytes),
+units = the work items of that launch in the profiled run (bench.py scales by its own count),
+valu_insts = SQ_INSTS_VALU of the launch, source = the summary file."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+# work items per launch of the profiled runs (tools/pmc.sh: bench defaults; tools/pmc_tdec.sh: 1024 a size)
+UNITS = {
+    "all188": 1024 * 110,  # the 16-sub-block class of the fused launch: 110 sizes x 1024 blocks
+    "k6144": 1024,
+    "class8": 1024 * 32,
+    "dlsch": 156 * 13,     # 78 subframes x 2 TBs x 13 code blocks
+    "ulsch": 156 * 13,
+    "pdsch": 78 * 26,
+    "pusch": 78,           # UEs
+    "ldpc": 4096,          # codewords
+    "nrsch": 64 * 35,      # code blocks
+}
+
+DOC = ("HBM bytes per launch from rocprofv3 PMC (tools/pmc.sh / tools/pmc_tdec.sh -> tools/pmc_summary.py -> "
+       "tools/pmc_traffic_build.py): 2 x FETCH_SIZE + WRITE_SIZE.  The x 2 is calibrated on this hardware for "
+       "the access widths these kernels use (profiles/r03_fetch_calibration.json, tools/fetch_calib.hip: coalesced "
+       "reads of 2, 4, 8 and 16 bytes a lane over 1 GiB all read back as FETCH_SIZE = bytes / 2; WRITE_SIZE = "
+       "bytes for every width; re-reads of a 64 MiB slice held in the Infinity Cache are NOT counted, so the "
+       "figure is DRAM traffic).  units = work items of the measured launch; bench.py scales by its own batch.  "
+       "valu_insts = SQ_INSTS_VALU of the same launch (roofline.valu_issue_frac).")
+
+
+def main(rnd):
+    out = {"_doc": DOC}
+    for wl, units in UNITS.items():
+        src = f"profiles/{rnd}_pmc_{wl}.json"
+        path = os.path.join(ROOT, src)
+        if not os.path.exists(path):
+            continue
+        ks = json.load(open(path))["kernels"]
+        ent = {}
+        for k, c in ks.items():
+            if "hbm_bytes_per_launch" not in c:
+                continue
+            e = {"bytes": int(c["hbm_bytes_per_launch"]), "fetch_raw_kib": c.get("FETCH_SIZE"), "units": units,
+                 "source": src}
+            if "SQ_INSTS_VALU" in c:
+                e["valu_insts"] = int(c["SQ_INSTS_VALU"])
+            ent[k] = e
+        out[wl] = ent
+    json.dump(out, open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w"), indent=1)
+    print({wl: sorted(v) for wl, v in out.items() if wl != "_doc"})
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "r03")

@@ -169,8 +169,8 @@ uint32_t srsran_tdec_gpu_get_single_threshold(void);
 void     srsran_tdec_gpu_set_generic_single_threshold(uint32_t nof_cb);
 /* Launches of at most nof_cb blocks that run a single-lane decoder (16- / 8-sub-block class, one launch,
    not the fused multi-size launch) use its split variant: two helper waves take the recomputation of the
-   other direction in phase 2 off the main waves, one 4-wave workgroup per CU (default 1024).
-   Process-wide. */
+   other direction in phase 2 off the main waves, one 4-wave workgroup per CU (default 0 = off: slower
+   than the plain single-lane kernel at every size measured).  Process-wide. */
 void     srsran_tdec_gpu_set_split_threshold(uint32_t nof_cb);
 uint32_t srsran_tdec_gpu_get_split_threshold(void);
 uint32_t srsran_tdec_gpu_get_generic_single_threshold(void);

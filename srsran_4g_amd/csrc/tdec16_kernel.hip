@@ -779,8 +779,12 @@ uint32_t tdec16s_min_cb() { return __atomic_load_n(&g_single_min_cb, __ATOMIC_RE
 static uint32_t g_single8_min_cb = 4096u;
 // srsran_tdec_gpu_set_split_threshold(): launches of at most this many blocks run the single-lane
 // decoders' split variant (tdecs_kernel.hip split_kernel: two helper waves take the other direction's
-// recomputation of phase 2 off the main waves; one workgroup of 4 waves per CU)
-static uint32_t g_split_max_cb = 1024u;
+// recomputation of phase 2 off the main waves through LDS; one workgroup of 4 waves per CU).  Off by
+// default: bit-exact, 171-198 VGPRs instead of 292-314, but slower than the plain single-lane kernel at
+// every size measured (K = 6144: 0.378 / 0.384 / 0.401 ms against 0.341 / 0.347 / 0.363 ms at 256 / 512 /
+// 1024 blocks; the per-window barrier of four waves and the LDS round trip of 16 states a lane cost more
+// than the recomputation they take off the main waves).
+static uint32_t g_split_max_cb = 0u;
 void     tdecs_set_split_max_cb(uint32_t n) { __atomic_store_n(&g_split_max_cb, n, __ATOMIC_RELAXED); }
 uint32_t tdecs_split_max_cb() { return __atomic_load_n(&g_split_max_cb, __ATOMIC_RELAXED); }
 void     tdec8s_set_min_cb(uint32_t n) { __atomic_store_n(&g_single8_min_cb, n, __ATOMIC_RELAXED); }

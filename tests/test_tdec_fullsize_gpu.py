@@ -11,8 +11,7 @@ buffers placed far apart in device memory.
     for its pool block (the batch tiles a pool of distinct AWGN blocks at several SNRs, so decoded
     words differ from the transmitted ones in some blocks and not in others).
   * configs[0]'s shape on the GPU: K = 6144 x 1024 through srsran_tdec_gpu_run_batch, on each of the
-    16-sub-block decoders (the single lane's split variant by default at this size, the plain single lane,
-    lane pair, quad).
+    16-sub-block decoders (the single lane by default at this size, its split variant, lane pair, quad).
   * DL-SCH transport blocks whose soft buffers lie more than 2 GB apart: the lane-pair decoder runs
     (the descriptor list is padded where a workgroup's two blocks would straddle two far buffers) and
     every TB equals the oracle's decode_tb (return, payload, average iterations, CB CRC flags).
@@ -107,8 +106,8 @@ def test_k6144_x1024_batch(env, kernel):
     d_out = torch.zeros((batch, K // 8), dtype=torch.uint8, device="cuda")
     never = 1 << 30
     L = tdec.load_library()
-    pair, single, split = {"tdec16s_split_kernel<false>": (None, None, None),  # the default at this size
-                           "tdec16s_kernel<false>": (None, None, 0), "tdec16_kernel<false>": (None, never, 0),
+    pair, single, split = {"tdec16s_kernel<false>": (None, None, None),  # the default at this size
+                           "tdec16s_split_kernel<false>": (None, None, never), "tdec16_kernel<false>": (None, never, 0),
                            "tdec_kernel<16>": (never, never, 0)}[kernel]
     with tdec.pair_threshold(L.srsran_tdec_gpu_get_pair_threshold() if pair is None else pair), \
             tdec.single_threshold(L.srsran_tdec_gpu_get_single_threshold() if single is None else single), \

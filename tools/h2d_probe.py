@@ -47,8 +47,10 @@ def main():
     cs = torch.cuda.Stream(dev)
     print(json.dumps({"compute_stream": int(stream.cuda_stream), "copy_stream": int(cs.cuda_stream)}), flush=True)
 
+    cur = [stream]
+
     def step(ptr):
-        if ue.gpu_decode_batch(arr, ptr, d_res.data_ptr(), d_avg.data_ptr(), 0.0, stream.cuda_stream) != 2 * nsf:
+        if ue.gpu_decode_batch(arr, ptr, d_res.data_ptr(), d_avg.data_ptr(), 0.0, cur[0].cuda_stream) != 2 * nsf:
             raise RuntimeError("decode failed")
 
     n = 20
@@ -108,9 +110,9 @@ def main():
                     d_xs[nb].copy_(h_x, non_blocking=True)
                 copied[nb].record(cs)
             c = time.perf_counter()
-            stream.wait_event(copied[b])
+            cur[0].wait_event(copied[b])
             step(d_xs[b].data_ptr())
-            used[b].record(stream)
+            used[b].record(cur[0])
             t[0] += c - a
             t[1] += time.perf_counter() - c
 
@@ -123,13 +125,16 @@ def main():
                 d_xs[b].copy_(h_x, non_blocking=True)
             copied[b].record(cs)
             c = time.perf_counter()
-            stream.wait_event(copied[b])
+            cur[0].wait_event(copied[b])
             step(d_xs[b].data_ptr())
             t[0] += c - a
             t[1] += time.perf_counter() - c
 
     for name, body in (("steps_only", steps_only), ("copies_only", copies_only), ("serial_same_stream", serial),
                        ("overlapped", overlapped), ("overlapped_nowait", overlapped_nowait)):
+        timeit(name, body)
+    cur[0] = torch.cuda.Stream(dev)  # the same loops with the decode on a created stream
+    for name, body in (("steps_only_created_stream", steps_only), ("overlapped_created_stream", overlapped)):
         timeit(name, body)
 
 

@@ -1390,8 +1390,8 @@ def main():
         dom_units = args.batch * len(k16)
         traffic = pmc_traffic(args.workload, dom, dom_units)
     else:
-        dom = max(per_kernel, key=lambda n: per_kernel[n]["ms"])
-        dk = per_kernel[dom]
+        dk = per_kernel[max(per_kernel, key=lambda n: per_kernel[n]["ms"])]
+        dom = tdec.last_kernel()  # the kernel as it ran and as rocprofv3 names it, e.g. tdec16s_kernel<false>
         avg_ms = dk["ms"] / dk["launches"]
         bytes_per_launch = dk["bytes"] / dk["launches"]
         dom_units = args.batch

@@ -61,8 +61,8 @@ def test_enb_to_ue_through_pdcch(env, case):
         d.alloc_type = 0
         d.raw[0] = (1 << int(np.ceil(nprb / U.lib().srsran_ra_type0_P(nprb)))) - 1
     ntb = 2 if fmt == F2A else 1
-    for i in range(ntb):
-        d.tb[i].mcs_idx, d.tb[i].rv, d.tb[i].ndi = mcs, 0, True
+    for i in range(ntb):  # codeword i carries TB i (no swap), as the scheduler fills the DCI
+        d.tb[i].mcs_idx, d.tb[i].rv, d.tb[i].ndi, d.tb[i].cw_idx = mcs, 0, True, i
     locs = [loc for loc in PD.ue_locations(nof_cce, tti % 10, rnti) if (1 << loc[0]) <= nof_cce]
     d.location.L, d.location.ncce = max(locs)  # the highest aggregation level the cell offers
     r, msg = PD.pack_pdsch(cell, d)
@@ -103,7 +103,7 @@ def test_enb_to_ue_through_pdcch(env, case):
         ret, res = ue.decode_pdsch(ucfg, tti, cfi)
         assert ret == 0
         for i in range(ntb):
-            assert res[i][0] and np.array_equal(res[i][1][:len(pls[i])], pls[i]), i
+            assert res[i][0] and np.array_equal(res[i][1][:len(pls[i])], pls[i]), (i, bool(res[i][0]))
         assert ue.find_dl_dci(tti, cfi, rnti ^ 0x0100, tm=tm) == []
         for sb in sbs:
             sb.free()

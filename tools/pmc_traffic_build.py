@@ -44,6 +44,8 @@ def main(rnd):
         ks = json.load(open(path))["kernels"]
         ent = {}
         for k, c in ks.items():
+            head, sep, tail = k.partition("<")
+            k = head.split("::")[-1] + sep + tail  # as bench.py names kernels (no namespace)
             if "hbm_bytes_per_launch" not in c:
                 continue
             e = {"bytes": int(c["hbm_bytes_per_launch"]), "fetch_raw_kib": c.get("FETCH_SIZE"), "units": units,

@@ -136,6 +136,8 @@ def parse():
                                           "nrsch"],
                    default="all188")
     p.add_argument("--snr", type=float, default=30.0, help="pdsch: AWGN SNR (dB) of the synthetic subframes")
+    p.add_argument("--nfft", type=int, default=2048, choices=[2048, 1536],
+                   help="pdsch: OFDM size of the 100-PRB carrier (2048: standard rate, C3; 1536: the reference default)")
     p.add_argument("--subframes", type=int, default=78,
                    help="dlsch / pdsch: subframes (2 TBs each) per step; 78 x 26 CBs = two full turbo-decoder rounds")
     p.add_argument("--sigma", type=float, default=0.42, help="dlsch: AWGN std on +-1 symbols before LLR scaling")
@@ -434,13 +436,13 @@ C3_NRE = {0: 13992, 5: 14256}  # PDSCH REs of the C3 grant per subframe index (o
 SF_LEN = 30720                  # 20 MHz, N = 2048 (standard sampling rate)
 
 
-def stage_bytes(nsf, nre_sum, ntb):
+def stage_bytes(nsf, nre_sum, ntb, sf_len=SF_LEN):
     """Algorithmic HBM bytes per launch of each stage kernel for nsf C3 subframes (2 rx, 2 ports):
     the inputs each kernel must read once and the outputs it must write once."""
     nrx, ports, nre_row = 2, 2, 1200
     K, C = 5824, 13
     return {
-        "ofdm_rx_kernel": nsf * nrx * (SF_LEN + 14 * nre_row) * 8,
+        "ofdm_rx_kernel": nsf * nrx * (sf_len + 14 * nre_row) * 8,
         "chest_kernel": nsf * ports * nrx * (4 * nre_row * 8 + nre_row * 8),
         "predecode_batch_kernel": nre_sum * (nrx * 8 + 4 + 2 * 8 + 2 * 4) + nsf * ports * nrx * nre_row * 8,
         "llr_batch_kernel": nre_sum * 2 * (8 + 4 + 6 * 2),
@@ -825,12 +827,15 @@ def run_pdsch(args, torch, dist, world, rank, device, steps=None, warmup=None, c
     for i in range(10):  # one subframe of each index (tti 1..10 -> sf 1..9, 0)
         tti = i + 1
         pls = [rng.integers(0, 256, C3_TBS // 8, dtype=np.uint8) for _ in range(2)]
-        x, nre = SY.pdsch_subframe(100, cell_id, 2, tti, 1, rnti, C3_TBS, C3_QM, 0, pls, snr_db=args.snr, rng=rng)
+        x, nre = SY.pdsch_subframe(100, cell_id, 2, tti, 1, rnti, C3_TBS, C3_QM, 0, pls, snr_db=args.snr, rng=rng,
+                                   N=args.nfft)
         pool.append((tti, x, nre, pls))
     nsf = args.subframes
     host = np.stack([pool[b % 10][1] for b in range(nsf)])
     d_x = torch.from_numpy(np.ascontiguousarray(host).view(np.float32)).to(device)
-    U.use_standard_symbol_size(True)  # C3 is quoted at N = 2048 (standard rates, as srsUE runs)
+    # C3 is quoted at N = 2048 (standard rates, as srsUE runs); --nfft 1536 is the reference's default rate
+    U.use_standard_symbol_size(args.nfft == 2048)
+    sf_len = 15 * args.nfft
     ue = U.UeDl(U.cell(100, 2, cell_id), 2)
     ue.cfg.cfg.pdsch.max_nof_iterations = args.iters
     sbs = [[S.SoftbufferRx(nof_prb=100) for _ in range(2)] for _ in range(nsf)]
@@ -912,7 +917,7 @@ def run_pdsch(args, torch, dist, world, rank, device, steps=None, warmup=None, c
     stages = prof.read()
     prof.enable(False)
     nre_sum = sum(pool[b % 10][2] for b in range(nsf))
-    sb = stage_bytes(nsf, nre_sum, 2 * nsf)
+    sb = stage_bytes(nsf, nre_sum, 2 * nsf, sf_len)
     per_stage = {}
     for name, (ms, n) in stages.items():
         avg_ms = ms / n
@@ -943,7 +948,7 @@ def run_pdsch(args, torch, dist, world, rank, device, steps=None, warmup=None, c
         "data": f"synthetic: eNB-side TX (synth/: DL-SCH encode, scrambling, 64QAM, CDD, CRS, OFDM) through "
                 f"[[1,1],[1,-1]] + AWGN {args.snr} dB; 10 distinct subframes (indices 0-9) tiled, HBM-resident",
         "config": {
-            "workload": f"pdsch C3: {nsf} subframes x (2 rx x {SF_LEN} cf32 samples -> OFDM 2048 -> CRS chest -> "
+            "workload": f"pdsch C3: {nsf} subframes x (2 rx x {sf_len} cf32 samples -> OFDM {args.nfft} -> CRS chest -> "
                         f"MMSE CDD 2x2 -> 64QAM LLR -> 2 TBs x {C3_TBS} bits), CFI 1, max {args.iters} half-its",
             "subframes_per_step_per_gpu": nsf,
             "subframes_per_s": round(world * nsf * steps / elapsed, 1),
@@ -968,7 +973,7 @@ def run_pdsch(args, torch, dist, world, rank, device, steps=None, warmup=None, c
         },
         "stages": per_stage,
         "host_enqueue_ms_per_step": round(host_ms, 4),
-        "chain_bytes_per_sf": 2 * SF_LEN * 8 + 2 * C3_TBS // 8,
+        "chain_bytes_per_sf": 2 * sf_len * 8 + 2 * C3_TBS // 8,
     }
     if (res != 0).any():
         result["config"]["tb_fail"] = int((res != 0).sum())

@@ -172,6 +172,10 @@ void     srsran_tdec_gpu_set_generic_single_threshold(uint32_t nof_cb);
    other direction in phase 2 off the main waves, one 4-wave workgroup per CU (default 0 = off: slower
    than the plain single-lane kernel at every size measured).  Process-wide. */
 void     srsran_tdec_gpu_set_split_threshold(uint32_t nof_cb);
+/* Single-lane launches whose block sizes are all <= k run the build with 8-step windows (fewer
+   registers, twice the checkpoints: two waves per SIMD where LDS allows).  Process-wide. */
+void     srsran_tdec_gpu_set_w8_max_k(uint32_t k);
+uint32_t srsran_tdec_gpu_get_w8_max_k(void);
 uint32_t srsran_tdec_gpu_get_split_threshold(void);
 uint32_t srsran_tdec_gpu_get_generic_single_threshold(void);
 

@@ -785,6 +785,11 @@ static uint32_t g_single8_min_cb = 4096u;
 // 1024 blocks; the per-window barrier of four waves and the LDS round trip of 16 states a lane cost more
 // than the recomputation they take off the main waves).
 static uint32_t g_split_max_cb = 0u;
+// srsran_tdec_gpu_set_w8_max_k(): single-lane launches whose block sizes are all <= this K use the build
+// with 8-step windows (tdecs_kernel.hip, TDECS_W = 8)
+static uint32_t g_w8_max_k = 0u;
+void     tdecs_set_w8_max_k(uint32_t k) { __atomic_store_n(&g_w8_max_k, k, __ATOMIC_RELAXED); }
+uint32_t tdecs_w8_max_k() { return __atomic_load_n(&g_w8_max_k, __ATOMIC_RELAXED); }
 void     tdecs_set_split_max_cb(uint32_t n) { __atomic_store_n(&g_split_max_cb, n, __ATOMIC_RELAXED); }
 uint32_t tdecs_split_max_cb() { return __atomic_load_n(&g_split_max_cb, __ATOMIC_RELAXED); }
 void     tdec8s_set_min_cb(uint32_t n) { __atomic_store_n(&g_single8_min_cb, n, __ATOMIC_RELAXED); }

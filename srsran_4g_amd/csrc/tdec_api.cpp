@@ -390,6 +390,10 @@ void srsran_tdec_gpu_set_pair_threshold(uint32_t nof_cb) { tdec16_set_min_cb(nof
 
 uint32_t srsran_tdec_gpu_get_pair_threshold(void) { return tdec16_min_cb(); }
 
+void srsran_tdec_gpu_set_w8_max_k(uint32_t k) { tdecs_set_w8_max_k(k); }
+
+uint32_t srsran_tdec_gpu_get_w8_max_k(void) { return tdecs_w8_max_k(); }
+
 void srsran_tdec_gpu_set_split_threshold(uint32_t nof_cb) { tdecs_set_split_max_cb(nof_cb); }
 
 uint32_t srsran_tdec_gpu_get_split_threshold(void) { return tdecs_split_max_cb(); }
@@ -788,6 +792,11 @@ int srsran_tdec_gpu_run_multi(uint32_t              nof_groups,
                      : cls_nsb[ci] == 16            ? tdec16_choice(cls_cb)
                                                     : (cls_cb >= tdec8s_min_cb() ? 2 : 0);
     const int  nsbc = cls_nsb[ci];
+    uint32_t   kmax = 0;
+    for (uint32_t g : gs) {
+      kmax = std::max(kmax, cfg[g]->proto.K);
+    }
+    const bool w8  = kind == 2 && nsbc > 1 && kmax <= tdecs_w8_max_k();  // the 8-step-window build
     const int  cpw  = kind == 2   ? (nsbc == 16 ? tdecs16::cpw() : nsbc == 8 ? tdecs8::cpw() : tdecs1::cpw())
                       : kind == 1 ? tdec16_cpw()
                                   : tdec_cpw(nsbc);
@@ -832,8 +841,8 @@ int srsran_tdec_gpu_run_multi(uint32_t              nof_groups,
       ha[k]            = a;
       hf[k]            = nblk;
       nblk += (nof_cb[g] + cpw - 1) / cpw;
-      lds = std::max(lds, kind == 2   ? (nsbc == 16  ? tdecs16::lds_bytes(a)
-                                         : nsbc == 8 ? tdecs8::lds_bytes(a)
+      lds = std::max(lds, kind == 2   ? (nsbc == 16  ? (w8 ? tdecs16w8::lds_bytes(a) : tdecs16::lds_bytes(a))
+                                         : nsbc == 8 ? (w8 ? tdecs8w8::lds_bytes(a) : tdecs8::lds_bytes(a))
                                                      : tdecs1::lds_bytes(a))
                           : kind == 1 ? tdec16_lds_bytes(a)
                                       : tdec_lds_bytes(c->nsb, a.xyw, a.M));
@@ -845,8 +854,10 @@ int srsran_tdec_gpu_run_multi(uint32_t              nof_groups,
     m.used = true;
     const TdecArgs* dg = reinterpret_cast<const TdecArgs*>(m.d_stage);
     const uint32_t* df = reinterpret_cast<const uint32_t*>(m.d_stage + abyte);
-    if ((kind == 2   ? (nsbc == 16  ? tdecs16::multi_launch(dg, df, (int)n, nblk, lds, st)
-                        : nsbc == 8 ? tdecs8::multi_launch(dg, df, (int)n, nblk, lds, st)
+    if ((kind == 2   ? (nsbc == 16  ? (w8 ? tdecs16w8::multi_launch(dg, df, (int)n, nblk, lds, st)
+                                          : tdecs16::multi_launch(dg, df, (int)n, nblk, lds, st))
+                        : nsbc == 8 ? (w8 ? tdecs8w8::multi_launch(dg, df, (int)n, nblk, lds, st)
+                                          : tdecs8::multi_launch(dg, df, (int)n, nblk, lds, st))
                                     : tdecs1::multi_launch(dg, df, (int)n, nblk, lds, st))
          : kind == 1 ? tdec16_multi_launch(dg, df, (int)n, nblk, lds, st)
                      : tdec_multi_launch(cls_nsb[ci], dg, df, (int)n, nblk, lds, st)) != hipSuccess) {

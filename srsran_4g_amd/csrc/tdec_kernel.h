@@ -89,10 +89,15 @@ int        tdec16_cpw();
   }
 SRSRAN_TDECS_API(tdecs16)
 SRSRAN_TDECS_API(tdecs8)
+SRSRAN_TDECS_API(tdecs16w8)  // the same built with 8-step windows (fewer registers, more checkpoints)
+SRSRAN_TDECS_API(tdecs8w8)
 SRSRAN_TDECS_API(tdecs1)  // tdec1s_kernel.hip: the generic decoder (K <= 400), one lane per block and side
 #undef SRSRAN_TDECS_API
 bool       tdec8s_eligible(int nsb, const TdecArgs& a);
 bool       tdec1s_eligible(int nsb, const TdecArgs& a);
+// srsran_tdec_gpu_set_w8_max_k(): window classes of K up to this size run the 8-step-window build
+void       tdecs_set_w8_max_k(uint32_t k);
+uint32_t   tdecs_w8_max_k();
 void       tdecs_set_split_max_cb(uint32_t n);
 uint32_t   tdecs_split_max_cb();
 void       tdec8s_set_min_cb(uint32_t n);

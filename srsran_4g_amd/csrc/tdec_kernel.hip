@@ -822,10 +822,11 @@ hipError_t tdec_launch(int nsb, const TdecArgs& a, hipStream_t stream)
     return hipSuccess;
   }
   if (tdec16_eligible(nsb, a)) {
-    return tdec16_choice(a.ncb) == 2 ? tdecs16::launch(a, stream) : tdec16_launch(a, stream);
+    return tdec16_choice(a.ncb) == 2 ? (a.K <= tdecs_w8_max_k() ? tdecs16w8::launch(a, stream) : tdecs16::launch(a, stream))
+                                     : tdec16_launch(a, stream);
   }
   if (tdec8s_eligible(nsb, a)) {
-    return tdecs8::launch(a, stream);
+    return a.K <= tdecs_w8_max_k() ? tdecs8w8::launch(a, stream) : tdecs8::launch(a, stream);
   }
   if (tdec1s_eligible(nsb, a)) {
     return tdecs1::launch(a, stream);

@@ -36,16 +36,27 @@
 #ifndef TDECS_NSB
 #define TDECS_NSB 16
 #endif
-#if TDECS_NSB == 16
+#ifndef TDECS_W
+#define TDECS_W 16
+#endif
+#if TDECS_NSB == 16 && TDECS_W == 16
 #define TDECS_NS tdecs16
 #define TDECS_K(n) tdec16s_##n
 #define TDECS_NAME "tdec16s_"
-#elif TDECS_NSB == 8
+#elif TDECS_NSB == 8 && TDECS_W == 16
 #define TDECS_NS tdecs8
 #define TDECS_K(n) tdec8s_##n
 #define TDECS_NAME "tdec8s_"
+#elif TDECS_NSB == 16 && TDECS_W == 8
+#define TDECS_NS tdecs16w8
+#define TDECS_K(n) tdec16sw8_##n
+#define TDECS_NAME "tdec16sw8_"
+#elif TDECS_NSB == 8 && TDECS_W == 8
+#define TDECS_NS tdecs8w8
+#define TDECS_K(n) tdec8sw8_##n
+#define TDECS_NAME "tdec8sw8_"
 #else
-#error "TDECS_NSB must be 16 or 8"
+#error "TDECS_NSB must be 16 or 8, TDECS_W 16 or 8"
 #endif
 
 namespace srsran_amd {
@@ -54,8 +65,9 @@ namespace {
 
 typedef short v2s __attribute__((ext_vector_type(2)));
 
-constexpr int   W    = 16;            // window: steps between checkpoints
+constexpr int   W    = TDECS_W;       // window: steps between checkpoints (16; 8 for fewer registers)
 constexpr int   OVL  = TDEC_OVERLAP;  // win_overlap_len (turbodecoder_win.h:54)
+constexpr int   NTR  = (OVL + W - 1) / W;  // training windows (the last one partial when W does not divide 40)
 constexpr int   NSB  = TDECS_NSB;     // nof_blocks of the window decoder (avx16: 16, sse16: 8)
 constexpr short NEG  = -10000;        // -INF (turbodecoder_win.h:56)
 constexpr int   CPWG = 64 / NSB;      // code blocks per workgroup (one wave a side)
@@ -410,9 +422,9 @@ struct Pipe {
   __device__ __forceinline__ int t0_of(int idx, int L) const
   {
     if (beta) {
-      return idx < 3 ? 2 * W - W * idx : (Ma - 1 - (idx - 3)) * W;
+      return idx < NTR ? (NTR - 1 - idx) * W : (Ma - 1 - (idx - NTR)) * W;
     }
-    return idx < 3 ? L - OVL + W * idx : (idx - 3) * W;
+    return idx < NTR ? L - OVL + W * idx : (idx - NTR) * W;
   }
 
   __device__ __forceinline__ void load(const Lane& c, int idx)
@@ -475,7 +487,7 @@ __device__ __forceinline__ void map16s(const Lane& cin, int wave, uint4* STG)
   const int Ma    = (L + W - 1) / W;
   const int h     = max(1, min((L + W) / (2 * W), L / W));
   Pipe<D2>  pp;
-  pp.nwin = 3 + Ma;
+  pp.nwin = NTR + Ma;
   pp.Ma   = Ma;
   pp.beta = __builtin_amdgcn_readfirstlane(wave) != 0;
   uint32_t xw[W];
@@ -488,13 +500,13 @@ __device__ __forceinline__ void map16s(const Lane& cin, int wave, uint4* STG)
       pp.beta = wave == 3;
       __syncthreads();
       const int mtop = Ma - 1;
-      pp.load(c, wave == 2 ? 3 + h : 3 + mtop - (h - 1));
+      pp.load(c, wave == 2 ? NTR + h : NTR + mtop - (h - 1));
 #pragma unroll 1
       for (int j = 0; j <= nj; j++) {
         uint4* stg = STG + ((wave - 2) * 2 + (j & 1)) * (W * 64);
         if (wave == 2 && j < na) {
           const int ma = h + j;
-          pp.next(c, 3 + ma, xw, aux);
+          pp.next(c, NTR + ma, xw, aux);
           if (ma < Mfull) {
             beta_recompute<true>(c, ma * W, ck_get(c, ma), xw, stg, lane);
           } else {
@@ -502,7 +514,7 @@ __device__ __forceinline__ void map16s(const Lane& cin, int wave, uint4* STG)
           }
         } else if (wave == 3 && j < nb) {
           const int mb = h - 1 - j;
-          pp.next(c, 3 + mtop - mb, xw, aux);
+          pp.next(c, NTR + mtop - mb, xw, aux);
           alpha_recompute(mb * W, ck_get(c, mb), xw, stg, lane);
         }
         __syncthreads();
@@ -515,23 +527,14 @@ __device__ __forceinline__ void map16s(const Lane& cin, int wave, uint4* STG)
     // ================= alpha side =================
     St P = neg_state();
     // training over the last 40 steps of the own sub-block (win.h:747-756)
-    pp.next(c, 0, xw, aux);
 #pragma unroll
-    for (int i = 0; i < W; i++) {
-      P = step<false>(P, xw[i]);
-      if (norm_at(i)) P = norm(P);
-    }
-    pp.next(c, 1, xw, aux);
+    for (int w = 0; w < NTR; w++) {
+      pp.next(c, w, xw, aux);
 #pragma unroll
-    for (int i = 0; i < W; i++) {
-      P = step<false>(P, xw[i]);
-      if (norm_at(W + i)) P = norm(P);
-    }
-    pp.next(c, 2, xw, aux);
-#pragma unroll
-    for (int i = 0; i < OVL - 2 * W; i++) {
-      P = step<false>(P, xw[i]);
-      if (norm_at(2 * W + i)) P = norm(P);
+      for (int i = 0; i < (W < OVL - w * W ? W : OVL - w * W); i++) {
+        P = step<false>(P, xw[i]);
+        if (norm_at(w * W + i)) P = norm(P);
+      }
     }
     {  // move_left: sub-block s starts from the training state of s - 1; s = 0 is known
       St q;
@@ -545,7 +548,7 @@ __device__ __forceinline__ void map16s(const Lane& cin, int wave, uint4* STG)
 #pragma unroll 1
     for (int ma = 0; ma < h; ma++) {
       const int t0 = ma * W;
-      pp.next(c, 3 + ma, xw, aux);
+      pp.next(c, NTR + ma, xw, aux);
       ck_put(c, ma, P);
 #pragma unroll
       for (int i = 0; i < W; i++) {
@@ -562,7 +565,7 @@ __device__ __forceinline__ void map16s(const Lane& cin, int wave, uint4* STG)
         const int ma = h + j - 1;
         if (j >= 1 && j - 1 < na) {
           const uint4* stg = STG + ((j - 1) & 1) * (W * 64);
-          pp.next(c, 3 + ma, xw, aux);
+          pp.next(c, NTR + ma, xw, aux);
           if (ma < Mfull) {
             P = alpha_llr_staged<D2, BITS, true>(c, P, ma * W, xw, aux, stg, lane);
           } else {
@@ -576,34 +579,26 @@ __device__ __forceinline__ void map16s(const Lane& cin, int wave, uint4* STG)
     // phase 2: windows [h, Ma): beta recomputed from the checkpoint above the window, then alpha + LLR
 #pragma unroll 1
     for (int ma = h; ma < Mfull; ma++) {
-      pp.next(c, 3 + ma, xw, aux);
+      pp.next(c, NTR + ma, xw, aux);
       P = alpha_llr_window<D2, BITS, true>(c, P, ma * W, ck_get(c, ma), xw, aux);
     }
     if (Ma > Mfull) {
-      pp.next(c, 3 + Mfull, xw, aux);
+      pp.next(c, NTR + Mfull, xw, aux);
       alpha_llr_window<D2, BITS, false>(c, P, Mfull * W, ck_get(c, Mfull), xw, aux);
     }
   } else {
     // ================= beta side =================
     St P = neg_state();
     // training over the first 40 steps of the own sub-block, backwards (win.h:622-630)
-    pp.next(c, 0, xw, aux);
 #pragma unroll
-    for (int i = OVL - 2 * W - 1; i >= 0; i--) {
-      P = step<true>(P, xw[i]);
-      if (norm_at(2 * W + i)) P = norm(P);
-    }
-    pp.next(c, 1, xw, aux);
+    for (int w = 0; w < NTR; w++) {  // the top (maybe partial) training window first
+      pp.next(c, w, xw, aux);
+      const int t0 = (NTR - 1 - w) * W;
 #pragma unroll
-    for (int i = W - 1; i >= 0; i--) {
-      P = step<true>(P, xw[i]);
-      if (norm_at(W + i)) P = norm(P);
-    }
-    pp.next(c, 2, xw, aux);
-#pragma unroll
-    for (int i = W - 1; i >= 0; i--) {
-      P = step<true>(P, xw[i]);
-      if (norm_at(i)) P = norm(P);
+      for (int i = (W < OVL - t0 ? W : OVL - t0) - 1; i >= 0; i--) {
+        P = step<true>(P, xw[i]);
+        if (norm_at(t0 + i)) P = norm(P);
+      }
     }
     {  // move_right: sub-block s starts from the training state of s + 1; the last from the tail
       St q;
@@ -629,12 +624,12 @@ __device__ __forceinline__ void map16s(const Lane& cin, int wave, uint4* STG)
     St Bst = P;  // stored (pre-normalisation) beta of the position above the current window
     // phase 1: windows [h, Ma) from the top (the top one maybe partial)
     if (Ma > Mfull) {
-      pp.next(c, 3, xw, aux);
+      pp.next(c, NTR, xw, aux);
       P = beta_window<false>(c, P, mtop * W, mtop > h, Bst, xw);
     }
 #pragma unroll 1
     for (int mb = Mfull - 1; mb >= h; mb--) {
-      pp.next(c, 3 + mtop - mb, xw, aux);
+      pp.next(c, NTR + mtop - mb, xw, aux);
       P = beta_window<true>(c, P, mb * W, mb > h, Bst, xw);
     }
     __syncthreads();
@@ -647,7 +642,7 @@ __device__ __forceinline__ void map16s(const Lane& cin, int wave, uint4* STG)
         if (j >= 1 && j - 1 < h) {
           const uint4* stg = STG + (2 + ((j - 1) & 1)) * (W * 64);
           const int    t0  = mb * W;
-          pp.next(c, 3 + mtop - mb, xw, aux);
+          pp.next(c, NTR + mtop - mb, xw, aux);
 #pragma unroll
           for (int i = W - 1; i >= 0; i--) {
             const short o = llr(cand(stg_get(stg, i, lane), bm(xw[i])), Bst);
@@ -666,7 +661,7 @@ __device__ __forceinline__ void map16s(const Lane& cin, int wave, uint4* STG)
 #pragma unroll 1
     for (int mb = h - 1; mb >= 0; mb--) {
       const int t0 = mb * W;
-      pp.next(c, 3 + mtop - mb, xw, aux);
+      pp.next(c, NTR + mtop - mb, xw, aux);
       St Pa = ck_get(c, mb);
       St aw[W];  // alpha entering each position (candidates rebuilt at LLR time)
 #pragma unroll

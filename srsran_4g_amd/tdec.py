@@ -97,6 +97,8 @@ def load_library():
         "srsran_tdec_gpu_get_class_single_threshold": ([u32], u32),
         "srsran_tdec_gpu_set_generic_single_threshold": ([u32], None),
         "srsran_tdec_gpu_set_split_threshold": ([u32], None),
+        "srsran_tdec_gpu_set_w8_max_k": ([u32], None),
+        "srsran_tdec_gpu_get_w8_max_k": ([], u32),
         "srsran_tdec_gpu_get_split_threshold": ([], u32),
         "srsran_tdec_gpu_get_generic_single_threshold": ([], u32),
     }
@@ -142,6 +144,20 @@ class split_threshold(pair_threshold):
 
     def __exit__(self, *exc):
         load_library().srsran_tdec_gpu_set_split_threshold(self.old)
+
+
+class w8_max_k(pair_threshold):
+    """block sizes up to which the single-lane decoders run their 8-step-window build
+    (srsran_tdec_gpu_set_w8_max_k)"""
+
+    def __enter__(self):
+        lib = load_library()
+        self.old = lib.srsran_tdec_gpu_get_w8_max_k()
+        lib.srsran_tdec_gpu_set_w8_max_k(self.n)
+        return self
+
+    def __exit__(self, *exc):
+        load_library().srsran_tdec_gpu_set_w8_max_k(self.old)
 
 
 class class_single_threshold:

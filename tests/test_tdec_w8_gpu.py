@@ -1,0 +1,98 @@
+"""The single-lane window decoders built with 8-step windows (tdecs_kernel.hip, TDECS_W = 8: the
+tdec16sw8_* / tdec8sw8_* kernels that srsran_tdec_gpu_set_w8_max_k selects), forced onto every size of
+both window classes against the oracle decoder: plain batches, several half-iteration counts, the fused
+multi-size launch and DL-SCH transport blocks with CRC early stop."""
+import numpy as np
+import pytest
+
+from oracle import CB_SIZES, Oracle, make_llrs
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def w8():
+    from srsran_4g_amd import tdec
+    if not tdec.gpu_available():
+        pytest.skip("no HIP device")
+    with tdec.single_threshold(0), tdec.split_threshold(0), tdec.w8_max_k(6144):
+        yield
+
+
+@pytest.fixture(scope="module")
+def ora():
+    return Oracle()
+
+
+@pytest.mark.parametrize("cls", [16, 8])
+def test_all_window_sizes_bit_exact(ora, cls):
+    from srsran_4g_amd import tdec
+    Ks = [k for k in CB_SIZES if tdec.nof_subblocks(k) == cls]
+    rng = np.random.default_rng(880 + cls)
+    dec = tdec.TurboDecoder()
+    bad = []
+    for j, K in enumerate(Ks):
+        _, llr = make_llrs(K, 0.8, rng, 1 + j % 9, ora)
+        sb = np.stack([ora.natural_to_sb(K, x) for x in llr])
+        if not np.array_equal(dec.run_all_batch(sb, 8, K), ora.run_batch(K, sb, True, 8)):
+            bad.append(K)
+        assert tdec.last_kernel() == f"tdec{cls}sw8_kernel<false>"
+    dec.free()
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("nit", [1, 2, 3, 16])
+def test_half_iteration_counts(ora, nit):
+    from srsran_4g_amd import tdec
+    rng = np.random.default_rng(890 + nit)
+    dec = tdec.TurboDecoder()
+    for K in (408, 800, 816, 1056, 3072, 6144):
+        _, llr = make_llrs(K, 0.5, rng, 5, ora)
+        sb = np.stack([ora.natural_to_sb(K, x) for x in llr])
+        assert np.array_equal(dec.run_all_batch(sb, nit, K), ora.run_batch(K, sb, True, nit)), (K, nit)
+    dec.free()
+
+
+def test_multi_size_launch(ora):
+    import torch
+    from srsran_4g_amd import tdec
+    rng = np.random.default_rng(895)
+    for Ks in ([816, 6144, 2048, 1504], [408, 800, 512]):
+        ins, outs, want = [], [], []
+        for i, K in enumerate(Ks):
+            n = 3 * i + 2
+            _, llr = make_llrs(K, 1.0, rng, n, ora)
+            sb = np.stack([ora.natural_to_sb(K, x) for x in llr])
+            ins.append(torch.from_numpy(sb).cuda())
+            outs.append(torch.zeros((n, K // 8), dtype=torch.uint8, device="cuda"))
+            want.append(ora.run_batch(K, sb, True, 8))
+        tdec.gpu_run_multi(Ks, [t.data_ptr() for t in ins], [t.shape[1] for t in ins], True,
+                           [t.data_ptr() for t in outs], [t.shape[0] for t in ins], 8, None)
+        torch.cuda.synchronize()
+        assert tdec.last_kernel() == ("tdec16sw8_multi_kernel" if Ks[0] >= 816 else "tdec8sw8_multi_kernel")
+        for K, o, w in zip(Ks, outs, want):
+            assert np.array_equal(o.cpu().numpy(), w), K
+
+
+def test_dlsch_early_stop_harq(ora):
+    from srsran_4g_amd import sch, tdec
+    rng = np.random.default_rng(897)
+    q = sch.Sch()
+    for tbs, Qm, G in ((600, 2, 1440), (6120, 4, 9000), (30576, 6, 38000)):
+        rc, s = sch.cbsegm(tbs)
+        tb = rng.integers(0, 256, tbs // 8, dtype=np.uint8)
+        sb = sch.SoftbufferRx(nof_prb=100)
+        state = None
+        for rv, sigma in ((0, 0.9), (2, 0.9), (3, 0.5)):
+            e = ora.dlsch_encode(tbs, Qm, rv, G, tb, 0).astype(np.float32) * 2 - 1
+            llr = np.trunc(100 * (e + rng.standard_normal(e.shape).astype(np.float32) * sigma)).astype(np.int16)
+            q.set_max_noi(8)
+            ret, data, avg = q.decode(sb, tbs, Qm, rv, llr)
+            assert tdec.last_kernel().startswith("tdec") and "sw8_kernel<true>" in tdec.last_kernel()
+            oret, odata, _, oavg, state = ora.dlsch_decode(tbs, Qm, rv, llr, 8, state)
+            assert ret == oret, (tbs, rv)
+            assert np.array_equal(data[: len(odata)], odata), (tbs, rv)
+            assert avg == pytest.approx(oavg, abs=0), (tbs, rv)
+            assert sb.cb_crc(s.C) == [bool(x) for x in state[1][: s.C]], (tbs, rv)
+        sb.free()
+    q.free()

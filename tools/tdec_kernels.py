@@ -27,6 +27,7 @@ def main():
     p.add_argument("--kernel", choices=["split", "single", "pair", "quad"], default="single")
     p.add_argument("--workload", choices=["k6144", "all188", "class8", "class1"], default="k6144")
     p.add_argument("--K", type=int, default=0, help="one code block size instead of the workload's")
+    p.add_argument("--w8", type=int, default=0, help="srsran_tdec_gpu_set_w8_max_k (8-step-window build up to K)")
     p.add_argument("--batch", type=int, default=1024)
     p.add_argument("--launches", type=int, default=5)
     p.add_argument("--iters", type=int, default=8)
@@ -35,6 +36,7 @@ def main():
     pair_min, single_min = {"split": (0, 0), "single": (0, 0), "pair": (0, never), "quad": (never, never)}[a.kernel]
     lib = tdec.load_library()
     lib.srsran_tdec_gpu_set_split_threshold(never if a.kernel == "split" else 0)
+    lib.srsran_tdec_gpu_set_w8_max_k(a.w8)
     lib.srsran_tdec_gpu_set_pair_threshold(pair_min)
     lib.srsran_tdec_gpu_set_single_threshold(single_min)
     lib.srsran_tdec_gpu_set_generic_single_threshold(single_min)

@@ -160,6 +160,8 @@ def parse():
                         "turbo decoder needs ~5 half-iterations and ~10%% of TBs fail (0 = skip)")
     p.add_argument("--tdec16", choices=["auto", "single", "pair", "quad"], default="auto",
                    help="decoder of the 16-sub-block class: the library's choice by batch size, or forced")
+    p.add_argument("--h2d-priority", type=int, default=-1, choices=[0, -1],
+                   help="pdsch: priority of the PCIe-loop copy stream (-1 high: its own hardware queue)")
     p.add_argument("--cpu-worker", type=int, default=None, help=argparse.SUPPRESS)
     return p.parse_args()
 
@@ -862,7 +864,9 @@ def run_pdsch(args, torch, dist, world, rank, device, steps=None, warmup=None, c
     # (tools/h2d_probe.py: 1.74 ms per step there against 0.72 ms with the copy alone).
     h_x = torch.from_numpy(np.ascontiguousarray(host).view(np.float32)).pin_memory()
     d_xs = [d_x, torch.empty_like(d_x)]
-    cs = torch.cuda.Stream(device)
+    # the copy stream at high priority: HIP multiplexes streams of one priority over a few hardware
+    # queues, and a copy queued behind the decode on a shared queue would serialise the loop
+    cs = torch.cuda.Stream(device, priority=args.h2d_priority)
     ks = torch.cuda.Stream(device)
     copied = [torch.cuda.Event(), torch.cuda.Event()]
     used = [torch.cuda.Event(), torch.cuda.Event()]
@@ -906,6 +910,13 @@ def run_pdsch(args, torch, dist, world, rank, device, steps=None, warmup=None, c
     for _ in range(steps):
         step()
     host_ms = (time.perf_counter() - t1) / steps * 1e3
+    torch.cuda.synchronize()
+    # where the host enqueue time goes (library-side wall-clock phases, same loop)
+    prof.host_enable(True)
+    for _ in range(steps):
+        step()
+    host_phases = {k: round(us / n, 1) for k, (us, n) in prof.host_read().items()}
+    prof.host_enable(False)
     torch.cuda.synchronize()
     res = d_res.cpu().numpy()
     avg = d_avg.cpu().numpy()
@@ -978,6 +989,7 @@ def run_pdsch(args, torch, dist, world, rank, device, steps=None, warmup=None, c
         },
         "stages": per_stage,
         "host_enqueue_ms_per_step": round(host_ms, 4),
+        "host_phases_us_per_call": host_phases,
         "chain_bytes_per_sf": 2 * sf_len * 8 + 2 * C3_TBS // 8,
     }
     if (res != 0).any():
@@ -1519,6 +1531,8 @@ def main():
             "avg_half_iterations": pd["config"]["avg_half_iterations"],
             "roofline": pd["roofline"],
             "stages": pd["stages"],
+            "host_enqueue_ms_per_step": pd["host_enqueue_ms_per_step"],
+            "host_phases_us_per_call": pd["host_phases_us_per_call"],
             "chain_bytes_per_sf": pd["chain_bytes_per_sf"],
             "chain_roofline_frac": round(pd["config"]["subframes_per_s"] * pd["chain_bytes_per_sf"]
                                          / (world * HBM_PEAK_GBS * 1e9), 5),

@@ -22,6 +22,17 @@ int srsran_amd_timing_read(float ms[SRSRAN_AMD_NOF_STAGES], uint32_t launches[SR
 /* the kernel name of a stage (as rocprofv3 reports it, without template arguments) */
 const char* srsran_amd_stage_name(int stage);
 
+/* Host-side phases of the batch APIs (wall clock of the calling thread, microseconds): 0 the whole
+ * srsran_ue_dl_gpu_decode_batch call, 1 OFDM + estimation enqueue, 2 PDSCH descriptors, 3 wait for the
+ * previous PDSCH descriptor upload, 4 PDSCH upload + launches, 5 DL-SCH descriptors, 6 wait for the
+ * previous DL-SCH descriptor upload, 7 DL-SCH upload + launches. */
+#define SRSRAN_AMD_NOF_HOST_PHASES 8
+/* start (non-zero) or stop recording; clears the accumulators */
+void srsran_amd_host_timing_enable(int enable);
+/* per-phase total microseconds and call counts since the last read; clears them */
+int srsran_amd_host_timing_read(double us[SRSRAN_AMD_NOF_HOST_PHASES], uint32_t calls[SRSRAN_AMD_NOF_HOST_PHASES]);
+const char* srsran_amd_host_phase_name(int phase);
+
 #ifdef __cplusplus
 }
 #endif

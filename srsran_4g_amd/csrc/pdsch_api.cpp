@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -21,6 +22,7 @@
 
 #include "llr_kernel.h"
 #include "pdsch_internal.h"
+#include "stage_timing.h"
 
 using namespace srsran_amd;
 
@@ -33,6 +35,9 @@ struct Table {
   uint32_t  len = 0;
 };
 
+using TableKey = std::array<uint64_t, 5>;  // RE table cache key (get_table)
+static_assert(SRSRAN_MAX_PRB <= 128, "two 64-bit words of PRB bitmap per slot");
+
 struct PdschGpu {
   hipStream_t                  stream  = nullptr;  // host-synchronous path
   hipEvent_t                   staged  = nullptr;  // descriptor upload finished (pinned staging reusable)
@@ -43,7 +48,7 @@ struct PdschGpu {
   size_t                       work_cap  = 0;
   float2*                      d_in      = nullptr;  // host-synchronous path: grids + estimates
   size_t                       in_cap    = 0;
-  std::map<std::string, Table> tables;
+  std::map<TableKey, Table>    tables;
 };
 
 bool grow_dev(void** p, size_t* cap, size_t need)
@@ -105,16 +110,16 @@ void table_evict(PdschGpu* g, uint32_t nsf)
 Table get_table(srsran_pdsch_t* q, PdschGpu* g, const srsran_pdsch_grant_t& gr, uint32_t lstart,
                        uint32_t sf_idx)
 {
-  std::string key;
-  key.reserve(2 * q->cell.nof_prb + 16);
-  for (uint32_t s = 0; s < 2; s++) {
+  TableKey key{};  // PRB bitmaps of both slots, symbols per slot, first PDSCH symbol, subframe index
+  for (uint32_t sl = 0; sl < 2; sl++) {
     for (uint32_t n = 0; n < q->cell.nof_prb; n++) {
-      key.push_back(gr.prb_idx[s][n] ? '1' : '0');
+      if (gr.prb_idx[sl][n]) {
+        key[sl * 2 + n / 64] |= 1ull << (n % 64);
+      }
     }
-    key.push_back((char)gr.nof_symb_slot[s]);
   }
-  key.push_back((char)lstart);
-  key.push_back((char)sf_idx);
+  key[4] = (uint64_t)gr.nof_symb_slot[0] | (uint64_t)gr.nof_symb_slot[1] << 8 | (uint64_t)lstart << 16 |
+           (uint64_t)sf_idx << 24;
   auto it = g->tables.find(key);
   if (it != g->tables.end()) {
     return it->second;
@@ -142,6 +147,7 @@ struct Cw {
 int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sfs, hipStream_t s,
                 std::vector<Cw>& cws, std::vector<int16_t*>& llr)
 {
+  srsran_amd::HostScope desc(srsran_amd::HP_PDSCH_DESC);
   PdschGpu*      g   = (PdschGpu*)q->gpu;
   const uint32_t nrx = q->nof_rx_antennas, np = q->cell.nof_ports, nre = 12 * q->cell.nof_prb;
   const uint32_t nsf_rows = 2 * SRSRAN_CP_NSYMB(q->cell.cp);  // grid symbols per subframe (14 / 12)
@@ -282,9 +288,13 @@ int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sf
   std::stable_sort(order_l.begin(), order_l.end(), [&](uint32_t x, uint32_t y) { return cws[x].mod < cws[y].mod; });
   const size_t pa_bytes = align256(nsf * sizeof(PredArgs));
   const size_t li_bytes = align256(std::max<size_t>(cws.size(), 1) * sizeof(LlrItem));
+  desc.stop();
+  srsran_amd::HostScope wait(srsran_amd::HP_PDSCH_WAIT);
   if (hipEventSynchronize(g->staged) != hipSuccess || !grow_stage(g, pa_bytes + li_bytes)) {
     return SRSRAN_ERROR;
   }
+  wait.stop();
+  srsran_amd::HostScope launch(srsran_amd::HP_PDSCH_LAUNCH);
   PredArgs* hp = (PredArgs*)g->h_stage;
   LlrItem*  hl = (LlrItem*)(g->h_stage + pa_bytes);
   for (uint32_t i = 0; i < nsf; i++) {

@@ -27,6 +27,7 @@
 #include "enc_kernel.h"
 #include "uci_kernel.h"
 #include "ulsch_batch.h"
+#include "stage_timing.h"
 
 using namespace srsran_amd;
 
@@ -344,6 +345,7 @@ int32_t check_tb(const srsran_dlsch_gpu_tb_t& tb, srsran_cbsegm_t* s)
 int enqueue_batch(srsran_sch_t* q, uint32_t ntb, const srsran_dlsch_gpu_tb_t* tbs, int32_t* d_result, float* d_avg,
                   hipStream_t stream)
 {
+  srsran_amd::HostScope desc(srsran_amd::HP_SCH_DESC);
   SchCtx*           x = (SchCtx*)q->gpu;
   std::vector<Plan> plan(ntb);
   uint32_t          nslots = 0;
@@ -458,9 +460,13 @@ int enqueue_batch(srsran_sch_t* q, uint32_t ntb, const srsran_dlsch_gpu_tb_t* tb
   const size_t off_cbs = align16(nslots * sizeof(RmSlot));
   const size_t off_tb  = off_cbs + align16(ncbs * sizeof(TdecCb));
   const size_t bytes   = off_tb + align16(ntb * sizeof(SchTb));
+  desc.stop();
+  srsran_amd::HostScope wait(srsran_amd::HP_SCH_WAIT);
   if (x->used) {
     hipEventSynchronize(x->staged);
   }
+  wait.stop();
+  srsran_amd::HostScope launch(srsran_amd::HP_SCH_LAUNCH);
   if (bytes > x->stage_cap || nslots > x->slot_cap) {
     if (x->used) {
       hipEventSynchronize(x->done);

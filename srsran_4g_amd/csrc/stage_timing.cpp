@@ -3,6 +3,7 @@
 #include "stage_timing.h"
 
 #include <atomic>
+#include <chrono>
 #include <map>
 #include <mutex>
 #include <vector>
@@ -12,6 +13,7 @@
 #include "../../include/srsran_amd_prof.h"
 
 static_assert(srsran_amd::ST_COUNT == SRSRAN_AMD_NOF_STAGES, "stage tables");
+static_assert(srsran_amd::HP_COUNT == SRSRAN_AMD_NOF_HOST_PHASES, "host phase tables");
 
 namespace srsran_amd {
 namespace {
@@ -55,7 +57,37 @@ void drain()  // caller holds g_mu
   g_pending.clear();
 }
 
+std::atomic<bool> g_host_on{false};
+std::mutex        g_host_mu;
+double            g_host_us[HP_COUNT];
+uint32_t          g_host_n[HP_COUNT];
+
+int64_t now_ns()
+{
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
 }  // namespace
+
+HostScope::HostScope(int phase) : phase_(phase)
+{
+  if (g_host_on.load(std::memory_order_relaxed)) {
+    t0_ = now_ns();
+  }
+}
+
+void HostScope::stop()
+{
+  if (t0_ < 0) {
+    return;
+  }
+  const double us = (now_ns() - t0_) * 1e-3;
+  t0_             = -1;
+  std::lock_guard<std::mutex> lk(g_host_mu);
+  g_host_us[phase_] += us;
+  g_host_n[phase_]++;
+}
 
 StageScope::StageScope(int stage, hipStream_t stream) : stage_(stage), stream_(stream)
 {
@@ -126,4 +158,36 @@ extern "C" const char* srsran_amd_stage_name(int stage)
                                         "nr_rm_kernel", "ldpc_kernel", "nr_tb_kernel",
                                         "chest_ul_kernel", "pusch_eq_idft_kernel"};
   return stage >= 0 && stage < ST_COUNT ? names[stage] : "";
+}
+
+extern "C" void srsran_amd_host_timing_enable(int enable)
+{
+  std::lock_guard<std::mutex> lk(g_host_mu);
+  for (int i = 0; i < HP_COUNT; i++) {
+    g_host_us[i] = 0;
+    g_host_n[i]  = 0;
+  }
+  g_host_on.store(enable != 0);
+}
+
+extern "C" int srsran_amd_host_timing_read(double us[SRSRAN_AMD_NOF_HOST_PHASES], uint32_t calls[SRSRAN_AMD_NOF_HOST_PHASES])
+{
+  if (!us || !calls) {
+    return -1;
+  }
+  std::lock_guard<std::mutex> lk(g_host_mu);
+  for (int i = 0; i < HP_COUNT; i++) {
+    us[i]        = g_host_us[i];
+    calls[i]     = g_host_n[i];
+    g_host_us[i] = 0;
+    g_host_n[i]  = 0;
+  }
+  return 0;
+}
+
+extern "C" const char* srsran_amd_host_phase_name(int phase)
+{
+  static const char* names[HP_COUNT] = {"ue_dl_batch", "ofdm_chest_enqueue", "pdsch_descriptors", "pdsch_stage_wait",
+                                        "pdsch_launch", "sch_descriptors", "sch_stage_wait", "sch_launch"};
+  return phase >= 0 && phase < HP_COUNT ? names[phase] : "";
 }

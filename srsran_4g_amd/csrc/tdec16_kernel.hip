@@ -786,8 +786,14 @@ static uint32_t g_single8_min_cb = 4096u;
 // than the recomputation they take off the main waves).
 static uint32_t g_split_max_cb = 0u;
 // srsran_tdec_gpu_set_w8_max_k(): single-lane launches whose block sizes are all <= this K use the build
-// with 8-step windows (tdecs_kernel.hip, TDECS_W = 8)
-static uint32_t g_w8_max_k = 0u;
+// with 8-step windows (tdecs_kernel.hip, TDECS_W = 8: 164-191 VGPRs, two waves a SIMD where LDS allows).
+// Default 800 = the whole 8-sub-block class (408 <= K <= 800), where it wins: the fused class launch of
+// 32 sizes x 1024 blocks 0.71 vs 0.91 ms, x 4096 blocks 2.30 vs 3.39 ms (gpurun_out r03l).  The 16-sub-block
+// class keeps 16-step windows: its 8-step build is slower at every K measured (2048 blocks, K = 1024 / 2048
+// / 4096 / 6144: 0.129 / 0.219 / 0.395 / 0.738 ms against 0.096 / 0.153 / 0.268 / 0.380 ms): twice the
+// windows a sub-block for the same training overlap, and at 19 KB of LDS a block the second wave a
+// SIMD does not fit at large K anyway.
+static uint32_t g_w8_max_k = 800u;
 void     tdecs_set_w8_max_k(uint32_t k) { __atomic_store_n(&g_w8_max_k, k, __ATOMIC_RELAXED); }
 uint32_t tdecs_w8_max_k() { return __atomic_load_n(&g_w8_max_k, __ATOMIC_RELAXED); }
 void     tdecs_set_split_max_cb(uint32_t n) { __atomic_store_n(&g_split_max_cb, n, __ATOMIC_RELAXED); }

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "../../include/srsran_pdcch.h"
+#include "stage_timing.h"
 #include "../../include/srsran_ue_dl.h"
 
 namespace {
@@ -308,6 +309,8 @@ int srsran_ue_dl_gpu_decode_batch(srsran_ue_dl_t*              q,
     fprintf(stderr, "[srsran_ue_dl] the batch path runs srsUE's default channel estimator configuration only\n");
     return SRSRAN_ERROR;
   }
+  srsran_amd::HostScope whole(srsran_amd::HP_UE_DL);
+  srsran_amd::HostScope front(srsran_amd::HP_FRONT);
   UeDlGpu*    g = (UeDlGpu*)q->gpu;
   hipStream_t s = (hipStream_t)stream;
   if (!grow(q, g, nof_sf) || hipEventSynchronize(g->staged) != hipSuccess) {
@@ -325,6 +328,7 @@ int srsran_ue_dl_gpu_decode_batch(srsran_ue_dl_t*              q,
                                          (cf_t*)g->d_ce, np * nrx * nre, g->d_res, stream)) {
     return SRSRAN_ERROR;
   }
+  front.stop();
   std::vector<srsran_pdsch_gpu_sf_t> ps(nof_sf);
   for (uint32_t b = 0; b < nof_sf; b++) {
     srsran_pdsch_gpu_sf_t& f = ps[b];

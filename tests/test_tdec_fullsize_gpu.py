@@ -7,7 +7,7 @@ buffers placed far apart in device memory.
     srsran_tdec_gpu_run_multi call (the bench's timed step): the 16-sub-block class is one fused
     launch (110 sizes x 1024 blocks in one grid) of the single-lane decoder tdec16s_multi_kernel (and,
     checked as well, of the lane-pair tdec16_multi_kernel), the 8-sub-block class the single-lane
-    tdec8s_multi_kernel and the generic class the quad decoder's fused launch.  Every block equals the reference's output
+    tdec8sw8_multi_kernel (8-step windows) and the generic class the quad decoder's fused launch.  Every block equals the reference's output
     for its pool block (the batch tiles a pool of distinct AWGN blocks at several SNRs, so decoded
     words differ from the transmitted ones in some blocks and not in others).
   * configs[0]'s shape on the GPU: K = 6144 x 1024 through srsran_tdec_gpu_run_batch, on each of the

@@ -160,8 +160,10 @@ def parse():
                         "turbo decoder needs ~5 half-iterations and ~10%% of TBs fail (0 = skip)")
     p.add_argument("--tdec16", choices=["auto", "single", "pair", "quad"], default="auto",
                    help="decoder of the 16-sub-block class: the library's choice by batch size, or forced")
-    p.add_argument("--h2d-priority", type=int, default=-1, choices=[0, -1],
-                   help="pdsch: priority of the PCIe-loop copy stream (-1 high: its own hardware queue)")
+    p.add_argument("--h2d-priority", type=int, default=0, choices=[0, -1],
+                   help="pdsch: priority of the PCIe-loop copy stream (-1: high)")
+    p.add_argument("--w8-max-k", type=int, default=-1,
+                   help="srsran_tdec_gpu_set_w8_max_k (-1: the library default)")
     p.add_argument("--cpu-worker", type=int, default=None, help=argparse.SUPPRESS)
     return p.parse_args()
 
@@ -864,8 +866,6 @@ def run_pdsch(args, torch, dist, world, rank, device, steps=None, warmup=None, c
     # (tools/h2d_probe.py: 1.74 ms per step there against 0.72 ms with the copy alone).
     h_x = torch.from_numpy(np.ascontiguousarray(host).view(np.float32)).pin_memory()
     d_xs = [d_x, torch.empty_like(d_x)]
-    # the copy stream at high priority: HIP multiplexes streams of one priority over a few hardware
-    # queues, and a copy queued behind the decode on a shared queue would serialise the loop
     cs = torch.cuda.Stream(device, priority=args.h2d_priority)
     ks = torch.cuda.Stream(device)
     copied = [torch.cuda.Event(), torch.cuda.Event()]
@@ -881,7 +881,10 @@ def run_pdsch(args, torch, dist, world, rank, device, steps=None, warmup=None, c
             if i + 1 < n:
                 nb = (i + 1) % 2
                 if i >= 1:
-                    cs.wait_event(used[nb])  # step i-1 is done with that buffer
+                    # step i-1 is done with that buffer: waited on the host (a GPU-side wait of the copy
+                    # stream on the decode stream serialises the two on this runtime: tools/h2d_probe.py
+                    # bench_like 1.04 ms against bench_like_host_wait 0.81 ms a step, r03r)
+                    used[nb].synchronize()
                 with torch.cuda.stream(cs):
                     d_xs[nb].copy_(h_x, non_blocking=True)
                 copied[nb].record(cs)
@@ -889,20 +892,21 @@ def run_pdsch(args, torch, dist, world, rank, device, steps=None, warmup=None, c
             step(d_xs[b].data_ptr(), ks)
             used[b].record(ks)
 
+    # the copy alone first (the PCIe bound of the same bytes; also maps the pinned samples for the GPU)
+    for timed in (False, True):
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(n_h2d if timed else 4):
+            with torch.cuda.stream(cs):
+                d_xs[1].copy_(h_x, non_blocking=True)
+        torch.cuda.synchronize()
+        copy_s = (time.perf_counter() - t1) / n_h2d
     h2d_loop(4)  # untimed: the first work on freshly created streams pays their queue set-up
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     h2d_loop(n_h2d)
     torch.cuda.synchronize()
     h2d_s = (time.perf_counter() - t1) / n_h2d
-    # the copy alone, for the PCIe bound of the same bytes
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    for _ in range(n_h2d):
-        with torch.cuda.stream(cs):
-            d_xs[1].copy_(h_x, non_blocking=True)
-    torch.cuda.synchronize()
-    copy_s = (time.perf_counter() - t1) / n_h2d
     del d_xs[1]
     # host enqueue cost of one step (the API builds descriptors and launches asynchronously)
     torch.cuda.synchronize()
@@ -1331,6 +1335,8 @@ def main():
         pair_min, single_min = {"single": (0, 0), "pair": (0, never), "quad": (never, never)}[args.tdec16]
         tdec.load_library().srsran_tdec_gpu_set_pair_threshold(pair_min)
         tdec.load_library().srsran_tdec_gpu_set_class_single_threshold(16, single_min)
+    if args.w8_max_k >= 0:
+        tdec.load_library().srsran_tdec_gpu_set_w8_max_k(args.w8_max_k)
     if args.workload in ("dlsch", "ulsch"):
         return run_dlsch(args, torch, dist, world, rank, device)
     if args.workload == "pusch":

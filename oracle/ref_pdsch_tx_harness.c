@@ -1,0 +1,143 @@
+/*
+ * oracle/ref_pdsch_tx_harness.c -- TEST INFRASTRUCTURE ONLY (linked into oracle/_ref/libsrsref.so).
+ *
+ * Pins the GPU transmitter's PDSCH symbols (srsran_4g_amd/csrc/enc_kernel.hip pdsch_tx_kernel) to the
+ * reference's own building blocks, compiled from /root/reference: bit scrambling
+ * (srsran_sequence_pdsch_apply_pack, phch/sequences.c:72-81), modulation (srsran_mod_modulate_bytes over
+ * srsran_modem_table_lte + srsran_modem_table_bytes, modem/mod.c:135, modem_table.c), layer mapping
+ * (srsran_layermap_type, mimo/layermap.c:83) and precoding (srsran_precoding_type, mimo/precoding.c).
+ * pdsch.c itself is not buildable here (generated headers); its srsran_pdsch_encode /
+ * srsran_pdsch_codeword_encode sequence (pdsch.c:1017-1120, 960-1015) is restated below around those
+ * calls.  The coded bits come from the caller (the oracle encoder, itself pinned to turbocoder.c /
+ * rm_turbo.c); the RE mapping is pinned separately (ref_pdsch_map_harness.c).
+ */
+#include <complex.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "srsran/phy/common/phy_common.h"
+#include "srsran/phy/common/sequence.h"
+#include "srsran/phy/mimo/layermap.h"
+#include "srsran/phy/mimo/precoding.h"
+#include "srsran/phy/modem/mod.h"
+#include "srsran/phy/modem/modem_table.h"
+
+/* 64-byte aligned, zeroed (the reference's SIMD precoders use aligned loads: srsran_vec_cf_malloc) */
+static cf_t* cf_zalloc(size_t n)
+{
+  void* p = NULL;
+  if (posix_memalign(&p, 64, n * sizeof(cf_t) + 64)) {
+    return NULL;
+  }
+  memset(p, 0, n * sizeof(cf_t) + 64);
+  return (cf_t*)p;
+}
+
+/* ncw codewords of nbits[c] coded bits each (one bit a byte in e[c * e_stride ...]), modulation mod[c]
+ * (srsran_mod_t), scrambled with the codeword index cw_idx[c]; tx_scheme srsran_tx_scheme_t; nof_re
+ * REs a port.  out: [nof_ports][nof_re] complex symbols (the q->symbols the reference maps to the REs).
+ * Returns 0, or -1 on bad arguments. */
+int ref_pdsch_tx_symbols(uint32_t       ncw,
+                         const uint8_t* e,
+                         uint32_t       e_stride,
+                         const uint32_t* nbits,
+                         const uint32_t* mod,
+                         const uint32_t* cw_idx,
+                         uint16_t        rnti,
+                         uint32_t        sf_idx,
+                         uint32_t        cell_id,
+                         int             tx_scheme,
+                         uint32_t        nof_ports,
+                         uint32_t        nof_layers,
+                         uint32_t        pmi,
+                         uint32_t        nof_re,
+                         float*          out)
+{
+  if (ncw == 0 || ncw > SRSRAN_MAX_CODEWORDS || nof_ports == 0 || nof_ports > SRSRAN_MAX_PORTS || nof_layers == 0 ||
+      nof_layers > SRSRAN_MAX_LAYERS || nof_re == 0) {
+    return -1;
+  }
+  int      ret = -1;
+  cf_t*    d[SRSRAN_MAX_CODEWORDS] = {NULL};
+  cf_t*    xl[SRSRAN_MAX_LAYERS]   = {NULL};
+  cf_t*    y[SRSRAN_MAX_PORTS]     = {NULL};
+  uint8_t* packed                  = NULL;
+  const size_t nsym                = (size_t)nof_re * SRSRAN_MAX_LAYERS;
+  for (uint32_t c = 0; c < SRSRAN_MAX_CODEWORDS; c++) {
+    d[c] = cf_zalloc(nsym);
+  }
+  for (uint32_t l = 0; l < SRSRAN_MAX_LAYERS; l++) {
+    xl[l] = cf_zalloc(nsym);
+  }
+  for (uint32_t p = 0; p < SRSRAN_MAX_PORTS; p++) {
+    y[p] = cf_zalloc(nsym);
+  }
+  packed = calloc(e_stride / 8 + 16, 1);
+  if (!packed) {
+    goto out;
+  }
+  for (uint32_t i = 0; i < SRSRAN_MAX_LAYERS; i++) {
+    if (!d[i % SRSRAN_MAX_CODEWORDS] || !xl[i] || !y[i % SRSRAN_MAX_PORTS]) {
+      goto out;
+    }
+  }
+  /* srsran_pdsch_codeword_encode (pdsch.c:960-1015): scrambling of the packed coded bits, then mapping */
+  for (uint32_t c = 0; c < ncw; c++) {
+    if (!d[c] || nbits[c] > e_stride || mod[c] >= SRSRAN_MOD_NITEMS) {
+      goto out;
+    }
+    memset(packed, 0, e_stride / 8 + 16);
+    for (uint32_t i = 0; i < nbits[c]; i++) {
+      packed[i / 8] |= (uint8_t)((e[(size_t)c * e_stride + i] & 1) << (7 - i % 8));
+    }
+    srsran_sequence_pdsch_apply_pack(packed, packed, rnti, (int)cw_idx[c], 2 * sf_idx, cell_id, nbits[c]);
+    srsran_modem_table_t tab;
+    if (srsran_modem_table_lte(&tab, (srsran_mod_t)mod[c])) {
+      goto out;
+    }
+    srsran_modem_table_bytes(&tab);
+    srsran_mod_modulate_bytes(&tab, packed, d[cw_idx[c]], nbits[c]);
+    srsran_modem_table_free(&tab);
+  }
+  /* srsran_pdsch_encode (pdsch.c:1066-1112): layer mapping and precoding, scaling 1 (no power allocation) */
+  if (nof_ports > 1) {
+    int   nof_symbols;
+    cf_t* x[SRSRAN_MAX_LAYERS] = {NULL};
+    if (nof_layers == ncw) {
+      for (uint32_t i = 0; i < nof_layers; i++) {
+        x[i] = d[i];
+      }
+      nof_symbols = (int)nof_re;
+    } else {
+      for (uint32_t i = 0; i < nof_layers; i++) {
+        x[i] = xl[i];
+      }
+      nof_symbols = srsran_layermap_type(d, x, (int)ncw, (int)nof_layers, (int[SRSRAN_MAX_CODEWORDS]){nof_re, nof_re},
+                                         (srsran_tx_scheme_t)tx_scheme);
+    }
+    const int codebook_idx = ncw == 1 ? (int)pmi : (int)pmi + 1;
+    if (srsran_precoding_type(x, y, (int)nof_layers, (int)nof_ports, codebook_idx, nof_symbols, 1.0f,
+                              (srsran_tx_scheme_t)tx_scheme) < 0) {
+      goto out;
+    }
+  } else {
+    memcpy(y[0], d[0], nof_re * sizeof(cf_t));
+  }
+  for (uint32_t p = 0; p < nof_ports; p++) {
+    memcpy(out + (size_t)2 * p * nof_re, y[p], nof_re * sizeof(cf_t));
+  }
+  ret = 0;
+out:
+  for (uint32_t c = 0; c < SRSRAN_MAX_CODEWORDS; c++) {
+    free(d[c]);
+  }
+  for (uint32_t l = 0; l < SRSRAN_MAX_LAYERS; l++) {
+    free(xl[l]);
+  }
+  for (uint32_t p = 0; p < SRSRAN_MAX_PORTS; p++) {
+    free(y[p]);
+  }
+  free(packed);
+  return ret;
+}

@@ -137,6 +137,40 @@ def main():
     for name, body in (("steps_only_created_stream", steps_only), ("overlapped_created_stream", overlapped)):
         timeit(name, body)
 
+    # bench.py's loop as it runs there: both streams created after the decodes above, events reused,
+    # an untimed warm pass; then the same with the copy's wait done on the host instead of the GPU
+    cs2 = torch.cuda.Stream(dev, priority=-1)
+    ks2 = torch.cuda.Stream(dev)
+    cp2 = [torch.cuda.Event(), torch.cuda.Event()]
+    us2 = [torch.cuda.Event(), torch.cuda.Event()]
+
+    def bench_loop(m, host_wait):
+        with torch.cuda.stream(cs2):
+            d_xs[0].copy_(h_x, non_blocking=True)
+        cp2[0].record(cs2)
+        for i in range(m):
+            b = i % 2
+            if i + 1 < m:
+                nb = (i + 1) % 2
+                if i >= 1:
+                    if host_wait:
+                        us2[nb].synchronize()
+                    else:
+                        cs2.wait_event(us2[nb])
+                with torch.cuda.stream(cs2):
+                    d_xs[nb].copy_(h_x, non_blocking=True)
+                cp2[nb].record(cs2)
+            ks2.wait_event(cp2[b])
+            if ue.gpu_decode_batch(arr, d_xs[b].data_ptr(), d_res.data_ptr(), d_avg.data_ptr(), 0.0,
+                                   ks2.cuda_stream) != 2 * nsf:
+                raise RuntimeError("decode failed")
+            us2[b].record(ks2)
+
+    for name, hw in (("bench_like", False), ("bench_like_host_wait", True)):
+        bench_loop(4, hw)
+        torch.cuda.synchronize()
+        timeit(name, lambda t, hw=hw: bench_loop(n, hw))
+
 
 if __name__ == "__main__":
     main()

@@ -31,7 +31,10 @@ def main():
     p.add_argument("--batch", type=int, default=1024)
     p.add_argument("--launches", type=int, default=5)
     p.add_argument("--iters", type=int, default=8)
+    p.add_argument("--lib", default="", help="another build of the library (A/B timing)")
     a = p.parse_args()
+    if a.lib:
+        tdec.LIB_PATH = os.path.abspath(a.lib)
     never = 1 << 30
     pair_min, single_min = {"split": (0, 0), "single": (0, 0), "pair": (0, never), "quad": (never, never)}[a.kernel]
     lib = tdec.load_library()
@@ -72,7 +75,7 @@ def main():
         torch.cuda.synchronize()
         ms.append(e0.elapsed_time(e1))
     bits = a.batch * sum(Ks)
-    print(json.dumps({"kernel": tdec.last_kernel(), "workload": a.workload, "batch": a.batch, "blocks": a.batch * len(Ks),
+    print(json.dumps({"lib": os.path.basename(a.lib) if a.lib else "head", "kernel": tdec.last_kernel(), "workload": a.workload, "batch": a.batch, "blocks": a.batch * len(Ks),
                       "ms": [round(x, 4) for x in ms], "gbps": round(bits / (min(ms) * 1e-3) / 1e9, 2)}))
 
 

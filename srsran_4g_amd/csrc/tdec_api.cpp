@@ -871,6 +871,20 @@ int srsran_tdec_gpu_run_multi(uint32_t              nof_groups,
   return ret;
 }
 
+#ifdef TDECS_STAMPS
+// Diagnostic build only (lib/stamps/libsrsran_4g_amd.so, tools/tdec_stamps.py): every single-lane
+// launch from now on writes its phase-boundary clock stamps to d_buf ([workgroup][wave][64] u64), or
+// stops when d_buf is NULL.
+int srsran_tdec_gpu_debug_set_stamps(void* d_buf)
+{
+  using namespace srsran_amd;
+  return tdecs16::set_stamps(d_buf) == hipSuccess && tdecs8::set_stamps(d_buf) == hipSuccess &&
+                 tdecs16w8::set_stamps(d_buf) == hipSuccess && tdecs8w8::set_stamps(d_buf) == hipSuccess
+             ? SRSRAN_SUCCESS
+             : SRSRAN_ERROR;
+}
+#endif
+
 void srsran_tdec_iteration_8bit(srsran_tdec_t* h, int8_t* input, uint8_t* output)
 {
   (void)h;

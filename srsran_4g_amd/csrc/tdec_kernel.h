@@ -93,6 +93,12 @@ SRSRAN_TDECS_API(tdecs16w8)  // the same built with 8-step windows (fewer regist
 SRSRAN_TDECS_API(tdecs8w8)
 SRSRAN_TDECS_API(tdecs1)  // tdec1s_kernel.hip: the generic decoder (K <= 400), one lane per block and side
 #undef SRSRAN_TDECS_API
+#ifdef TDECS_STAMPS  // diagnostic build (Makefile `stamps`): phase-boundary clock stamps of the single-lane kernels
+namespace tdecs16 { hipError_t set_stamps(void* d_buf); }
+namespace tdecs8 { hipError_t set_stamps(void* d_buf); }
+namespace tdecs16w8 { hipError_t set_stamps(void* d_buf); }
+namespace tdecs8w8 { hipError_t set_stamps(void* d_buf); }
+#endif
 bool       tdec8s_eligible(int nsb, const TdecArgs& a);
 bool       tdec1s_eligible(int nsb, const TdecArgs& a);
 // srsran_tdec_gpu_set_w8_max_k(): window classes of K up to this size run the 8-step-window build

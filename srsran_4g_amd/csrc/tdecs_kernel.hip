@@ -73,6 +73,23 @@ constexpr short NEG  = -10000;        // -INF (turbodecoder_win.h:56)
 constexpr int   CPWG = 64 / NSB;      // code blocks per workgroup (one wave a side)
 constexpr int   ROWB = 2 * NSB;       // bytes of one position row of the SB input (all sub-blocks)
 
+#ifdef TDECS_STAMPS
+// Diagnostic build only (Makefile `stamps`, tools/tdec_stamps.py; never the product library): lane 0 of
+// every wave writes the shader clock at the phase boundaries of every half-iteration into a debug
+// buffer, [workgroup][wave][64 stamps], with an ordinary vector store.
+__device__ unsigned long long* g_stamps = nullptr;
+#define TDECS_STAMP(k)                                                                               \
+  do {                                                                                               \
+    if ((threadIdx.x & 63) == 0 && g_stamps && (k) < 64) {                                          \
+      g_stamps[((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64 + (k)] = clock64(); \
+    }                                                                                                \
+  } while (0)
+#else
+#define TDECS_STAMP(k) \
+  do {                 \
+  } while (0)
+#endif
+
 __device__ __forceinline__ v2s u2v(uint32_t u) { return __builtin_bit_cast(v2s, u); }
 __device__ __forceinline__ uint32_t v2u(v2s v) { return __builtin_bit_cast(uint32_t, v); }
 __device__ __forceinline__ v2s padd(v2s a, v2s b) { return __builtin_elementwise_add_sat(a, b); }
@@ -254,11 +271,19 @@ __device__ __forceinline__ void issue(const Lane& c, Raw& r, int t0)
 {
   const uint32_t soff = (uint32_t)ROWB * (uint32_t)t0;
   const uint32_t poff = soff + (D2 ? 4u : 2u) * (uint32_t)c.KP;  // parity stream, bytes
+#ifdef TDECS_FAKELOAD  // diagnostic timing build only: no global loads (results are garbage)
+#pragma unroll
+  for (int i = 0; i < W; i++) {
+    r.a[i] = D2 ? (uint32_t)((c.s * 37 + t0 + i) % c.K) : (soff + i) & 0xff;
+    r.b[i] = (poff + 3 * i) & 0xff;
+  }
+#else
 #pragma unroll
   for (int i = 0; i < W; i++) {
     r.a[i] = D2 ? ldb(c.rtf, 2u * (uint32_t)c.s, soff, ROWB * i) : ldb(c.rin, c.voff, soff, ROWB * i);
     r.b[i] = ldb(c.rin, c.voff, poff, ROWB * i);
   }
+#endif
 }
 
 __device__ __forceinline__ uint32_t pin(uint32_t v)
@@ -472,8 +497,9 @@ struct Pipe {
 // side's, one window ahead of the main waves, through the double-buffered LDS stage STG
 // ([side][buffer][W][64] states).
 template <bool D2, bool BITS, bool HELP>
-__device__ __forceinline__ void map16s(const Lane& cin, int wave, uint4* STG)
+__device__ __forceinline__ void map16s(const Lane& cin, int wave, uint4* STG, int st0)
 {
+  (void)st0;  // first stamp index of this half-iteration (TDECS_STAMPS builds)
   Lane c = cin;
   asm volatile("" : "+v"(c.s));
   asm volatile("" : "+v"(c.voff));
@@ -526,6 +552,7 @@ __device__ __forceinline__ void map16s(const Lane& cin, int wave, uint4* STG)
   if (wave == 0) {
     // ================= alpha side =================
     St P = neg_state();
+    TDECS_STAMP(st0);
     // training over the last 40 steps of the own sub-block (win.h:747-756)
 #pragma unroll
     for (int w = 0; w < NTR; w++) {
@@ -536,6 +563,7 @@ __device__ __forceinline__ void map16s(const Lane& cin, int wave, uint4* STG)
         if (norm_at(w * W + i)) P = norm(P);
       }
     }
+    TDECS_STAMP(st0 + 1);
     {  // move_left: sub-block s starts from the training state of s - 1; s = 0 is known
       St q;
       q.a = u2v((uint32_t)__shfl_up((int)v2u(P.a), 1, NSB));
@@ -556,7 +584,9 @@ __device__ __forceinline__ void map16s(const Lane& cin, int wave, uint4* STG)
         if (nrm(t0, i)) P = norm(P);
       }
     }
+    TDECS_STAMP(st0 + 2);
     __syncthreads();
+    TDECS_STAMP(st0 + 3);
     if constexpr (HELP) {  // phase 2 with the betas of window h + j - 1 from the helper
       const int lane = (int)(threadIdx.x & 63);
       const int na = Ma - h, nj = max(na, h);
@@ -586,9 +616,11 @@ __device__ __forceinline__ void map16s(const Lane& cin, int wave, uint4* STG)
       pp.next(c, NTR + Mfull, xw, aux);
       alpha_llr_window<D2, BITS, false>(c, P, Mfull * W, ck_get(c, Mfull), xw, aux);
     }
+    TDECS_STAMP(st0 + 4);
   } else {
     // ================= beta side =================
     St P = neg_state();
+    TDECS_STAMP(st0);
     // training over the first 40 steps of the own sub-block, backwards (win.h:622-630)
 #pragma unroll
     for (int w = 0; w < NTR; w++) {  // the top (maybe partial) training window first
@@ -600,6 +632,7 @@ __device__ __forceinline__ void map16s(const Lane& cin, int wave, uint4* STG)
         if (norm_at(t0 + i)) P = norm(P);
       }
     }
+    TDECS_STAMP(st0 + 1);
     {  // move_right: sub-block s starts from the training state of s + 1; the last from the tail
       St q;
       q.a = u2v((uint32_t)__shfl_down((int)v2u(P.a), 1, NSB));
@@ -632,7 +665,9 @@ __device__ __forceinline__ void map16s(const Lane& cin, int wave, uint4* STG)
       pp.next(c, NTR + mtop - mb, xw, aux);
       P = beta_window<true>(c, P, mb * W, mb > h, Bst, xw);
     }
+    TDECS_STAMP(st0 + 2);
     __syncthreads();
+    TDECS_STAMP(st0 + 3);
     if constexpr (HELP) {  // phase 2 with the alphas of window h - j from the helper
       const int lane = (int)(threadIdx.x & 63);
       const int nj   = max(Ma - h, h);
@@ -681,6 +716,7 @@ __device__ __forceinline__ void map16s(const Lane& cin, int wave, uint4* STG)
         emit<D2, BITS>(c, t0 + i, o, aux[i], xw[i]);
       }
     }
+    TDECS_STAMP(st0 + 4);
   }
 }
 
@@ -762,15 +798,15 @@ __device__ __forceinline__ void body(const TdecArgs& a, int bid)
     const bool bits = ES ? crc_now : hi + 1 == h_end;
     if (hi & 1) {
       if (bits) {
-        map16s<true, true, HELP>(c, wave, STG);
+        map16s<true, true, HELP>(c, wave, STG, 5 * hi);
       } else {
-        map16s<true, false, HELP>(c, wave, STG);
+        map16s<true, false, HELP>(c, wave, STG, 5 * hi);
       }
     } else {
       if (bits) {
-        map16s<false, true, HELP>(c, wave, STG);
+        map16s<false, true, HELP>(c, wave, STG, 5 * hi);
       } else {
-        map16s<false, false, HELP>(c, wave, STG);
+        map16s<false, false, HELP>(c, wave, STG, 5 * hi);
       }
     }
     __syncthreads();
@@ -907,6 +943,14 @@ hipError_t multi_launch(const TdecArgs* d_groups, const uint32_t* d_first, int n
   hipLaunchKernelGGL(TDECS_K(multi_kernel), dim3(nblocks), dim3(128), lds, stream, d_groups, d_first, ngroups);
   return hipGetLastError();
 }
+
+#ifdef TDECS_STAMPS
+hipError_t set_stamps(void* d_buf)
+{
+  unsigned long long* p = (unsigned long long*)d_buf;
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &p, sizeof(p));
+}
+#endif
 
 }  // namespace TDECS_NS
 }  // namespace srsran_amd

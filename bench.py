@@ -164,6 +164,8 @@ def parse():
                    help="pdsch: priority of the PCIe-loop copy stream (-1: high)")
     p.add_argument("--w8-max-k", type=int, default=-1,
                    help="srsran_tdec_gpu_set_w8_max_k (-1: the library default)")
+    p.add_argument("--w8-fused-max-k", type=int, default=-1,
+                   help="srsran_tdec_gpu_set_w8_fused_max_k (-1: the library default)")
     p.add_argument("--cpu-worker", type=int, default=None, help=argparse.SUPPRESS)
     return p.parse_args()
 
@@ -1337,6 +1339,8 @@ def main():
         tdec.load_library().srsran_tdec_gpu_set_class_single_threshold(16, single_min)
     if args.w8_max_k >= 0:
         tdec.load_library().srsran_tdec_gpu_set_w8_max_k(args.w8_max_k)
+    if args.w8_fused_max_k >= 0:
+        tdec.load_library().srsran_tdec_gpu_set_w8_fused_max_k(args.w8_fused_max_k)
     if args.workload in ("dlsch", "ulsch"):
         return run_dlsch(args, torch, dist, world, rank, device)
     if args.workload == "pusch":

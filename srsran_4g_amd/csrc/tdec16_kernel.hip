@@ -794,6 +794,14 @@ static uint32_t g_split_max_cb = 0u;
 // windows a sub-block for the same training overlap, and at 19 KB of LDS a block the second wave a
 // SIMD does not fit at large K anyway.
 static uint32_t g_w8_max_k = 800u;
+// srsran_tdec_gpu_set_w8_fused_max_k(): in a fused multi-size launch of the 16-sub-block single-lane class,
+// the sizes up to this K form their own launch on the 8-step-window build (their workgroups, at 164-191
+// registers and little LDS, share SIMDs with the large sizes' workgroups).  All-188 step, one box,
+// alternating runs (gpurun_out r03z): cut at 800 (none) 12.22 ms, 1536 11.65 ms, 2368 11.71-11.73 ms,
+// 3136 12.37 ms.
+static uint32_t g_w8_fused_max_k = 1536u;
+void     tdecs_set_w8_fused_max_k(uint32_t k) { __atomic_store_n(&g_w8_fused_max_k, k, __ATOMIC_RELAXED); }
+uint32_t tdecs_w8_fused_max_k() { return __atomic_load_n(&g_w8_fused_max_k, __ATOMIC_RELAXED); }
 void     tdecs_set_w8_max_k(uint32_t k) { __atomic_store_n(&g_w8_max_k, k, __ATOMIC_RELAXED); }
 uint32_t tdecs_w8_max_k() { return __atomic_load_n(&g_w8_max_k, __ATOMIC_RELAXED); }
 void     tdecs_set_split_max_cb(uint32_t n) { __atomic_store_n(&g_split_max_cb, n, __ATOMIC_RELAXED); }

@@ -394,6 +394,10 @@ void srsran_tdec_gpu_set_w8_max_k(uint32_t k) { tdecs_set_w8_max_k(k); }
 
 uint32_t srsran_tdec_gpu_get_w8_max_k(void) { return tdecs_w8_max_k(); }
 
+void srsran_tdec_gpu_set_w8_fused_max_k(uint32_t k) { tdecs_set_w8_fused_max_k(k); }
+
+uint32_t srsran_tdec_gpu_get_w8_fused_max_k(void) { return tdecs_w8_fused_max_k(); }
+
 void srsran_tdec_gpu_set_split_threshold(uint32_t nof_cb) { tdecs_set_split_max_cb(nof_cb); }
 
 uint32_t srsran_tdec_gpu_get_split_threshold(void) { return tdecs_split_max_cb(); }
@@ -667,7 +671,7 @@ struct StreamPool {
   hipStream_t s[kPoolStreams];
   hipEvent_t  done[kPoolStreams];
   hipEvent_t  fork;
-  MultiDesc   md[3];  // decoder classes 16, 8, 1 sub-blocks
+  MultiDesc   md[4];  // launch entries: 16 (16-step windows), 16 (8-step part), 8, 1 sub-blocks
 };
 std::mutex               g_pool_mu;
 std::vector<StreamPool*> g_pools;
@@ -764,14 +768,35 @@ int srsran_tdec_gpu_run_multi(uint32_t              nof_groups,
   int       ret   = SRSRAN_SUCCESS;
   // One fused launch per decoder class (16 / 8 / generic): the sizes of a class share one grid
   // (more workgroups in flight than per-size launches, no per-launch tail); classes run on
-  // separate pool streams, longest first.
-  const int cls_nsb[3] = {16, 8, 1};
-  for (int ci = 0; ci < 3 && ret == SRSRAN_SUCCESS; ci++) {
+  // separate pool streams, longest first.  A single-lane 16-sub-block class is cut in two at
+  // tdecs_w8_fused_max_k(): its sizes up to there run the 8-step-window build (fewer registers and
+  // little LDS a workgroup: their workgroups can share SIMDs with the large sizes' ones) as their own
+  // launch.
+  const int cls_nsb[4] = {16, 16, 8, 1};  // launch entries: 16 (16-step), 16 (8-step part), 8, generic
+  for (int ci = 0; ci < 4 && ret == SRSRAN_SUCCESS; ci++) {
     std::vector<uint32_t> gs;
+    uint32_t              cls_cb = 0;  // blocks of the whole class (decides the kernel)
     for (uint32_t i = 0; i < nof_groups; i++) {
       if (cfg[order[i]]->nsb == cls_nsb[ci] && nof_cb[order[i]] > 0) {
         gs.push_back(order[i]);
+        cls_cb += nof_cb[order[i]];
       }
+    }
+    if (gs.empty()) {
+      continue;
+    }
+    // 2 single lane (tdecs_kernel.hip), 1 lane pair (16 sub-blocks only), 0 quad
+    const int kind = cls_nsb[ci] == 1               ? (cls_cb >= tdec1s_min_cb() ? 2 : 0)   // natural layout
+                     : !layout_sb                   ? 0
+                     : cls_nsb[ci] == 16            ? tdec16_choice(cls_cb)
+                                                    : (cls_cb >= tdec8s_min_cb() ? 2 : 0);
+    const uint32_t cut = std::max(tdecs_w8_max_k(), tdecs_w8_fused_max_k());
+    if (cls_nsb[ci] == 16 && kind == 2) {  // entry 0: K above the cut; entry 1: the rest
+      const bool part8 = ci == 1;
+      gs.erase(std::remove_if(gs.begin(), gs.end(), [&](uint32_t g) { return (cfg[g]->proto.K <= cut) != part8; }),
+               gs.end());
+    } else if (ci == 1) {
+      gs.clear();  // no 8-step part outside the single-lane class
     }
     if (gs.empty()) {
       continue;
@@ -782,21 +807,12 @@ int srsran_tdec_gpu_run_multi(uint32_t              nof_groups,
       ret = enqueue(cfg[g], d_input[g], in_stride[g], layout_sb, d_output[g], nof_cb[g], 0, n_end, nullptr, st);
       continue;
     }
-    uint32_t       cls_cb = 0;
-    for (uint32_t g : gs) {
-      cls_cb += nof_cb[g];
-    }
-    // 2 single lane (tdecs_kernel.hip), 1 lane pair (16 sub-blocks only), 0 quad
-    const int kind = cls_nsb[ci] == 1               ? (cls_cb >= tdec1s_min_cb() ? 2 : 0)   // natural layout
-                     : !layout_sb                   ? 0
-                     : cls_nsb[ci] == 16            ? tdec16_choice(cls_cb)
-                                                    : (cls_cb >= tdec8s_min_cb() ? 2 : 0);
     const int  nsbc = cls_nsb[ci];
     uint32_t   kmax = 0;
     for (uint32_t g : gs) {
       kmax = std::max(kmax, cfg[g]->proto.K);
     }
-    const bool w8  = kind == 2 && nsbc > 1 && kmax <= tdecs_w8_max_k();  // the 8-step-window build
+    const bool w8  = kind == 2 && nsbc > 1 && kmax <= (nsbc == 16 ? cut : tdecs_w8_max_k());  // 8-step windows
     const int  cpw  = kind == 2   ? (nsbc == 16 ? tdecs16::cpw() : nsbc == 8 ? tdecs8::cpw() : tdecs1::cpw())
                       : kind == 1 ? tdec16_cpw()
                                   : tdec_cpw(nsbc);

@@ -103,6 +103,9 @@ bool       tdec8s_eligible(int nsb, const TdecArgs& a);
 bool       tdec1s_eligible(int nsb, const TdecArgs& a);
 // srsran_tdec_gpu_set_w8_max_k(): window classes of K up to this size run the 8-step-window build
 void       tdecs_set_w8_max_k(uint32_t k);
+// srsran_tdec_gpu_set_w8_fused_max_k(): the 16-sub-block class's cut in fused multi-size launches
+void       tdecs_set_w8_fused_max_k(uint32_t k);
+uint32_t   tdecs_w8_fused_max_k();
 uint32_t   tdecs_w8_max_k();
 void       tdecs_set_split_max_cb(uint32_t n);
 uint32_t   tdecs_split_max_cb();

@@ -274,7 +274,7 @@ __device__ __forceinline__ void issue(const Lane& c, Raw& r, int t0)
 #ifdef TDECS_FAKELOAD  // diagnostic timing build only: no global loads (results are garbage)
 #pragma unroll
   for (int i = 0; i < W; i++) {
-    r.a[i] = D2 ? (uint32_t)((c.s * 37 + t0 + i) % c.K) : (soff + i) & 0xff;
+    r.a[i] = D2 ? (uint32_t)((c.s * 37 + t0 + i) & 511) : (soff + i) & 0xff;  // slots < 512 <= K
     r.b[i] = (poff + 3 * i) & 0xff;
   }
 #else

@@ -99,6 +99,8 @@ def load_library():
         "srsran_tdec_gpu_set_split_threshold": ([u32], None),
         "srsran_tdec_gpu_set_w8_max_k": ([u32], None),
         "srsran_tdec_gpu_get_w8_max_k": ([], u32),
+        "srsran_tdec_gpu_set_w8_fused_max_k": ([u32], None),
+        "srsran_tdec_gpu_get_w8_fused_max_k": ([], u32),
         "srsran_tdec_gpu_get_split_threshold": ([], u32),
         "srsran_tdec_gpu_get_generic_single_threshold": ([], u32),
     }
@@ -158,6 +160,20 @@ class w8_max_k(pair_threshold):
 
     def __exit__(self, *exc):
         load_library().srsran_tdec_gpu_set_w8_max_k(self.old)
+
+
+class w8_fused_max_k(pair_threshold):
+    """the 16-sub-block class's cut in fused multi-size launches: sizes up to it on 8-step windows
+    (srsran_tdec_gpu_set_w8_fused_max_k)"""
+
+    def __enter__(self):
+        lib = load_library()
+        self.old = lib.srsran_tdec_gpu_get_w8_fused_max_k()
+        lib.srsran_tdec_gpu_set_w8_fused_max_k(self.n)
+        return self
+
+    def __exit__(self, *exc):
+        load_library().srsran_tdec_gpu_set_w8_fused_max_k(self.old)
 
 
 class class_single_threshold:

@@ -76,9 +76,10 @@ def test_multi_size_launch(ora, kernel):
         ins.append(torch.from_numpy(sb).cuda())
         outs.append(torch.zeros((n, K // 8), dtype=torch.uint8, device="cuda"))
         want.append(ora.run_batch(K, sb, True, 8))
-    tdec.gpu_run_multi(Ks, [t.data_ptr() for t in ins], [t.shape[1] for t in ins], True,
-                       [t.data_ptr() for t in outs], [t.shape[0] for t in ins], 8, None)
-    torch.cuda.synchronize()
+    with tdec.w8_fused_max_k(0):  # one fused launch (the cut at w8_fused_max_k: test_tdec_fullsize_gpu.py)
+        tdec.gpu_run_multi(Ks, [t.data_ptr() for t in ins], [t.shape[1] for t in ins], True,
+                           [t.data_ptr() for t in outs], [t.shape[0] for t in ins], 8, None)
+        torch.cuda.synchronize()
     assert tdec.last_kernel() == kernel.replace("_split", "").replace("_kernel", "_multi_kernel")
     for K, o, w in zip(Ks, outs, want):
         assert np.array_equal(o.cpu().numpy(), w), K

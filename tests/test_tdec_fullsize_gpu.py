@@ -5,8 +5,9 @@ buffers placed far apart in device memory.
 
   * configs[1]: all 188 LTE code block sizes x 1024 blocks, 8 half-iterations, one
     srsran_tdec_gpu_run_multi call (the bench's timed step): the 16-sub-block class is one fused
-    launch (110 sizes x 1024 blocks in one grid) of the single-lane decoder tdec16s_multi_kernel (and,
-    checked as well, of the lane-pair tdec16_multi_kernel), the 8-sub-block class the single-lane
+    launch of the single-lane decoder, its sizes up to srsran_tdec_gpu_get_w8_fused_max_k on the
+    8-step-window build as a second launch (checked as well uncut, and on the lane-pair decoder),
+    the 8-sub-block class the single-lane
     tdec8sw8_multi_kernel (8-step windows) and the generic class the quad decoder's fused launch.  Every block equals the reference's output
     for its pool block (the batch tiles a pool of distinct AWGN blocks at several SNRs, so decoded
     words differ from the transmitted ones in some blocks and not in others).
@@ -62,10 +63,15 @@ def test_all188_x1024_fused_launch(env):
     k16 = [i for i, K in enumerate(Ks) if tdec.nof_subblocks(K) == 16]
     assert len(k16) == 110
 
-    # the 16-sub-block class alone: one fused launch of the single-lane decoder (the library's choice
-    # at 112,640 blocks), then of the lane-pair decoder
-    for name, single in (("tdec16s_multi_kernel", None), ("tdec16_multi_kernel", 1 << 30)):
-        with tdec.single_threshold(single if single is not None else tdec.load_library().srsran_tdec_gpu_get_single_threshold()):
+    # the 16-sub-block class alone: the single-lane decoder (the library's choice at 112,640 blocks) as the
+    # library cuts it (sizes up to srsran_tdec_gpu_get_w8_fused_max_k on 8-step windows, launched last),
+    # uncut (one fused launch), then the lane-pair decoder
+    lib = tdec.load_library()
+    cut = lib.srsran_tdec_gpu_get_w8_fused_max_k()
+    for name, single, fused_cut in (("tdec16sw8_multi_kernel" if cut >= 816 else "tdec16s_multi_kernel", None, cut),
+                                    ("tdec16s_multi_kernel", None, 0), ("tdec16_multi_kernel", 1 << 30, cut)):
+        with tdec.single_threshold(single if single is not None else lib.srsran_tdec_gpu_get_single_threshold()), \
+                tdec.w8_fused_max_k(fused_cut):
             tdec.gpu_run_multi([Ks[i] for i in k16], [ins[i].data_ptr() for i in k16], [ins[i].shape[1] for i in k16],
                                True, [outs[i].data_ptr() for i in k16], [batch] * len(k16), iters, None)
             torch.cuda.synchronize()

@@ -74,6 +74,32 @@ def test_multi_size_launch(ora):
             assert np.array_equal(o.cpu().numpy(), w), K
 
 
+@pytest.mark.parametrize("cut", [1536, 2368])
+def test_fused_launch_cut(ora, cut):
+    """the library default: 8-step windows only up to K = 800 (w8_max_k), and a fused 16-sub-block launch
+    cut at w8_fused_max_k -- sizes up to the cut on 8-step windows as a second launch, the rest on 16-step
+    windows; every block equal to the oracle"""
+    import torch
+    from srsran_4g_amd import tdec
+    rng = np.random.default_rng(896)
+    Ks = [6144, 816, 2432, 1536, 1568, 2368, 960, 4032]
+    with tdec.w8_max_k(800), tdec.w8_fused_max_k(cut):
+        ins, outs, want = [], [], []
+        for i, K in enumerate(Ks):
+            n = 2 * i + 3
+            _, llr = make_llrs(K, 1.0, rng, n, ora)
+            sb = np.stack([ora.natural_to_sb(K, x) for x in llr])
+            ins.append(torch.from_numpy(sb).cuda())
+            outs.append(torch.zeros((n, K // 8), dtype=torch.uint8, device="cuda"))
+            want.append(ora.run_batch(K, sb, True, 8))
+        tdec.gpu_run_multi(Ks, [t.data_ptr() for t in ins], [t.shape[1] for t in ins], True,
+                           [t.data_ptr() for t in outs], [t.shape[0] for t in ins], 8, None)
+        torch.cuda.synchronize()
+        assert tdec.last_kernel() == "tdec16sw8_multi_kernel"  # the 8-step part goes last
+        for K, o, w in zip(Ks, outs, want):
+            assert np.array_equal(o.cpu().numpy(), w), K
+
+
 def test_dlsch_early_stop_harq(ora):
     from srsran_4g_amd import sch, tdec
     rng = np.random.default_rng(897)

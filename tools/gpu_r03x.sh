@@ -6,7 +6,7 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 : > $OUT/stamps.jsonl
 for lib in stamps stamps_fake; do
-  for args in "--K 6144 --batch 1024" "--K 2048 --batch 2048" "--K 512 --batch 4096 --w8 800"; do
+  for args in "--K 6144 --batch 1024" "--K 2048 --batch 2048"; do
     timeout -k 10 120 python tools/tdec_stamps.py --lib $lib $args >> $OUT/stamps.jsonl 2> $OUT/stamps.err || { tail -5 $OUT/stamps.err; exit 1; }
   done
 done

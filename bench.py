@@ -1402,9 +1402,10 @@ def main():
         d["bytes"] += args.batch * algo_bytes(K)
         d["bits"] += args.batch * K
     if len(Ks) > 1:
-        # the timed step runs one fused launch per decoder class; its dominant kernel is the
-        # 16-sub-block class (tdec16_multi_kernel, the lane-pair decoder: every K >= 816 of the
-        # batch in one grid), timed here alone with events on the launch stream
+        # the timed step runs one fused launch per decoder class; its dominant part is the
+        # 16-sub-block class (every K >= 816 of the batch: the single-lane decoder, its sizes up to
+        # srsran_tdec_gpu_get_w8_fused_max_k as a second concurrent launch on 8-step windows), timed
+        # here alone with events on the launch stream
         k16 = [i for i, K in enumerate(Ks) if tdec.nof_subblocks(K) == 16]
         sel = [[groups[j][i] for i in k16] for j in range(5)]
         ms16 = []
@@ -1417,6 +1418,10 @@ def main():
             torch.cuda.synchronize()
             ms16.append(e0.elapsed_time(e1))
         dom = tdec.last_kernel()  # the 16-class launch just timed (srsran_tdec_gpu_last_kernel)
+        cut = tdec.load_library().srsran_tdec_gpu_get_w8_fused_max_k()
+        if dom == "tdec16sw8_multi_kernel" and any(Ks[i] > cut for i in k16):
+            # the class cut at srsran_tdec_gpu_get_w8_fused_max_k: two concurrent launches, timed together
+            dom = "tdec16s_multi_kernel+tdec16sw8_multi_kernel"
         avg_ms = float(np.mean(ms16))
         bytes_per_launch = sum(args.batch * algo_bytes(Ks[i]) for i in k16)
         dom_units = args.batch * len(k16)

@@ -799,7 +799,7 @@ static uint32_t g_w8_max_k = 800u;
 // registers and little LDS, share SIMDs with the large sizes' workgroups).  All-188 step, one box,
 // alternating runs (gpurun_out r03z): cut at 800 (none) 12.22 ms, 1536 11.65 ms, 2368 11.71-11.73 ms,
 // 3136 12.37 ms.
-static uint32_t g_w8_fused_max_k = 1536u;
+static uint32_t g_w8_fused_max_k = 2048u;
 void     tdecs_set_w8_fused_max_k(uint32_t k) { __atomic_store_n(&g_w8_fused_max_k, k, __ATOMIC_RELAXED); }
 uint32_t tdecs_w8_fused_max_k() { return __atomic_load_n(&g_w8_fused_max_k, __ATOMIC_RELAXED); }
 void     tdecs_set_w8_max_k(uint32_t k) { __atomic_store_n(&g_w8_max_k, k, __ATOMIC_RELAXED); }

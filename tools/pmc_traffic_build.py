@@ -34,7 +34,17 @@ DOC = ("HBM bytes per launch from rocprofv3 PMC (tools/pmc.sh / tools/pmc_tdec.s
        "valu_insts = SQ_INSTS_VALU of the same launch (roofline.valu_issue_frac).")
 
 
-def main(rnd):
+def all188_units(cut):
+    """blocks per launch of the two parts of the 16-sub-block class in tools/tdec_kernels.py's all-188
+    workload (1024 a size), cut at srsran_tdec_gpu_get_w8_fused_max_k = `cut`"""
+    sys.path.insert(0, ROOT)
+    from oracle.oracle import CB_SIZES, nof_subblocks
+    k16 = [k for k in CB_SIZES if nof_subblocks(k) == 16]
+    return {"tdec16s_multi_kernel": 1024 * sum(1 for k in k16 if k > cut),
+            "tdec16sw8_multi_kernel": 1024 * sum(1 for k in k16 if k <= cut)}
+
+
+def main(rnd, cut=2048):
     out = {"_doc": DOC}
     for wl, units in UNITS.items():
         src = f"profiles/{rnd}_pmc_{wl}.json"
@@ -48,15 +58,22 @@ def main(rnd):
             k = head.split("::")[-1] + sep + tail  # as bench.py names kernels (no namespace)
             if "hbm_bytes_per_launch" not in c:
                 continue
-            e = {"bytes": int(c["hbm_bytes_per_launch"]), "fetch_raw_kib": c.get("FETCH_SIZE"), "units": units,
+            u = all188_units(cut).get(k, units) if wl == "all188" and len(ks) > 1 else units
+            e = {"bytes": int(c["hbm_bytes_per_launch"]), "fetch_raw_kib": c.get("FETCH_SIZE"), "units": u,
                  "source": src}
             if "SQ_INSTS_VALU" in c:
                 e["valu_insts"] = int(c["SQ_INSTS_VALU"])
             ent[k] = e
+        if wl == "all188" and {"tdec16s_multi_kernel", "tdec16sw8_multi_kernel"} <= set(ent):
+            # the 16-sub-block class as bench.py times it: both parts, launched concurrently
+            a, b = ent["tdec16s_multi_kernel"], ent["tdec16sw8_multi_kernel"]
+            ent["tdec16s_multi_kernel+tdec16sw8_multi_kernel"] = {
+                "bytes": a["bytes"] + b["bytes"], "units": a["units"] + b["units"], "source": src,
+                "valu_insts": a.get("valu_insts", 0) + b.get("valu_insts", 0), "cut_k": cut}
         out[wl] = ent
     json.dump(out, open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w"), indent=1)
     print({wl: sorted(v) for wl, v in out.items() if wl != "_doc"})
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "r03")
+    main(sys.argv[1] if len(sys.argv) > 1 else "r03", int(sys.argv[2]) if len(sys.argv) > 2 else 2048)

@@ -886,6 +886,13 @@ __global__ __launch_bounds__(256, 1) void TDECS_K(split_kernel)(TdecArgs a)
 __global__ __launch_bounds__(128, 1) void TDECS_K(multi_kernel)(const TdecArgs* __restrict__ groups,
                                                             const uint32_t* __restrict__ first, int ngroups)
 {
+  if constexpr (NSB == 16 && W == 16) {
+    // the large sizes of a cut all-188 class are the step's critical path: their waves win the VALU
+    // arbitration against the 8-step part and the other classes' waves that share their SIMDs
+    __builtin_amdgcn_s_setprio(2);
+  } else if constexpr (NSB == 16) {
+    __builtin_amdgcn_s_setprio(1);  // the 8-step part of the cut class next
+  }
   const uint32_t b  = blockIdx.x;
   int            lo = 0, hi = ngroups - 1;
   while (lo < hi) {

@@ -889,9 +889,9 @@ __global__ __launch_bounds__(128, 1) void TDECS_K(multi_kernel)(const TdecArgs* 
   if constexpr (NSB == 16 && W == 16) {
     // the large sizes of a cut all-188 class are the step's critical path: their waves win the VALU
     // arbitration against the 8-step part and the other classes' waves that share their SIMDs
+    // (all-188 step, alternating runs on one box: 11.47-11.53 ms without, 11.16-11.22 ms with; priority 1
+    // for the 8-step part as well: 11.24-11.28 ms, gpurun_out r03ad / r03ae)
     __builtin_amdgcn_s_setprio(2);
-  } else if constexpr (NSB == 16) {
-    __builtin_amdgcn_s_setprio(1);  // the 8-step part of the cut class next
   }
   const uint32_t b  = blockIdx.x;
   int            lo = 0, hi = ngroups - 1;

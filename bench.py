@@ -44,6 +44,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # VALU ceilings (MI355X_MICROARCH.md: 256 CUs x 4 SIMD-32, a wave64 VALU instruction issues over 2 cycles,
 # 2.4 GHz): wave-instruction issue rate, and packed-int16 lane operations (v_pk_*_i16: 2 per lane)
 VALU_ISSUE_PEAK = 256 * 4 * 0.5 * 2.4e9          # 1.229e12 wave-instructions / s
+# the same measured on this hardware for the decoder's instruction forms (tools/valu_issue.hip,
+# profiles/r03_valu_issue.jsonl: v_pk_add_i16 clamp / v_perm_b32 at 3.45-3.5 cycles a SIMD with two
+# waves, 5.0-5.1 cycles for one wave alone)
+VALU_ISSUE_MEASURED = 256 * 4 / 3.5 * 2.4e9       # 7.02e11 wave-instructions / s, two waves a SIMD
 VALU_PK16_PEAK = 256 * 4 * 32 * 2 * 2.4e9        # 1.573e14 int16 operations / s
 TDEC_OPS_PER_BIT_HALF_IT = 86                    # max-log-MAP alpha + beta + LLR, turbodecoder_win.h
 
@@ -1447,6 +1451,9 @@ def main():
         "valu_insts_per_launch": int(valu_insts) if valu_insts else None,
         "valu_alg_frac": round(TDEC_OPS_PER_BIT_HALF_IT * dom_bits * args.iters / (avg_ms * 1e-3) / VALU_PK16_PEAK, 4),
         "valu_issue_peak": VALU_ISSUE_PEAK,
+        "valu_issue_frac_measured_rate": round(valu_insts / (avg_ms * 1e-3) / VALU_ISSUE_MEASURED, 4)
+        if valu_insts else None,
+        "valu_issue_measured_rate": round(VALU_ISSUE_MEASURED),
         "valu_pk16_peak": VALU_PK16_PEAK,
     }
 

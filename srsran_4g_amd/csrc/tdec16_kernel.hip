@@ -769,8 +769,11 @@ void     tdec16_set_min_cb(uint32_t n) { __atomic_store_n(&g_pair_min_cb, n, __A
 uint32_t tdec16_min_cb() { return __atomic_load_n(&g_pair_min_cb, __ATOMIC_RELAXED); }
 bool     tdec16_pays(uint32_t ncb) { return ncb >= tdec16_min_cb(); }
 // srsran_tdec_gpu_set_single_threshold(): blocks a launch from which the single-lane decoders
-// (tdecs_kernel.hip, 16-sub-block class) replaces the lane pair
-static uint32_t g_single_min_cb = 1024u;
+// (tdecs_kernel.hip, 16-sub-block class) replaces the lane pair.  Between 512 and 1024 blocks
+// (K = 6144, gpurun_out r03af): single lane / lane pair 0.345 / 0.385 ms at 640, 0.349 / 0.390 at 768,
+// 0.359 / 0.394 at 896, 0.361 / 0.397 at 1014 (the PUSCH batch of 78 UEs x 13 blocks: 0.108 vs 0.113 ms
+// with early stop); the lane pair is ahead at 512 (0.282 vs 0.348): from 576 blocks.
+static uint32_t g_single_min_cb = 576u;
 void     tdec16s_set_min_cb(uint32_t n) { __atomic_store_n(&g_single_min_cb, n, __ATOMIC_RELAXED); }
 uint32_t tdec16s_min_cb() { return __atomic_load_n(&g_single_min_cb, __ATOMIC_RELAXED); }
 // The 8-sub-block class: its quad decoder (one block a workgroup) stays ahead up to ~1024 blocks a launch

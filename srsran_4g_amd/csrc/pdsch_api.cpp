@@ -40,7 +40,10 @@ static_assert(SRSRAN_MAX_PRB <= 128, "two 64-bit words of PRB bitmap per slot");
 
 struct PdschGpu {
   hipStream_t                  stream  = nullptr;  // host-synchronous path
+  hipStream_t                  copy    = nullptr;  // descriptor uploads, ahead of the launches that read them
   hipEvent_t                   staged  = nullptr;  // descriptor upload finished (pinned staging reusable)
+  hipEvent_t                   read    = nullptr;  // the last launches that read d_stage are done
+  bool                         used    = false;
   char*                        h_stage = nullptr;
   char*                        d_stage = nullptr;
   size_t                       stage_cap = 0;
@@ -303,8 +306,15 @@ int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sf
   for (uint32_t i = 0; i < cws.size(); i++) {
     hl[i] = li[order_l[i]];
   }
-  hipMemcpyAsync(g->d_stage, g->h_stage, pa_bytes + li_bytes, hipMemcpyHostToDevice, s);
-  hipEventRecord(g->staged, s);
+  // the upload on the copy stream once the previous batch's predecode / LLR launches are done with
+  // d_stage: it runs beside the OFDM / estimation stages instead of in line in front of the predecoder
+  if (g->used) {
+    hipStreamWaitEvent(g->copy, g->read, 0);
+  }
+  hipMemcpyAsync(g->d_stage, g->h_stage, pa_bytes + li_bytes, hipMemcpyHostToDevice, g->copy);
+  hipEventRecord(g->staged, g->copy);
+  hipStreamWaitEvent(s, g->staged, 0);
+  g->used = true;
   hipMemsetAsync(d_max, 0, (size_t)nsf * 2 * sizeof(float), s);
   const PredArgs* dp = (const PredArgs*)g->d_stage;
   const LlrItem*  dl = (const LlrItem*)(g->d_stage + pa_bytes);
@@ -330,6 +340,7 @@ int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sf
     }
     i = j;
   }
+  hipEventRecord(g->read, s);
   return SRSRAN_SUCCESS;
 }
 
@@ -353,7 +364,9 @@ int srsran_pdsch_init_ue(srsran_pdsch_t* q, uint32_t max_prb, uint32_t nof_rx_an
   PdschGpu* g = new PdschGpu();
   q->gpu      = g;
   if (hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&g->staged, hipEventDisableTiming) != hipSuccess || !grow_stage(g, 65536)) {
+      hipStreamCreateWithFlags(&g->copy, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&g->staged, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&g->read, hipEventDisableTiming) != hipSuccess || !grow_stage(g, 65536)) {
     srsran_pdsch_free(q);
     return SRSRAN_ERROR;
   }
@@ -378,8 +391,14 @@ void srsran_pdsch_free(srsran_pdsch_t* q)
     if (g->staged) {
       hipEventDestroy(g->staged);
     }
+    if (g->read) {
+      hipEventDestroy(g->read);
+    }
     if (g->stream) {
       hipStreamDestroy(g->stream);
+    }
+    if (g->copy) {
+      hipStreamDestroy(g->copy);
     }
     delete g;
   }
@@ -524,7 +543,7 @@ int srsran_pdsch_gpu_decode_batch(srsran_pdsch_t*              q,
     e.softbuffer = f.cfg->softbuffers.rx[cws[i].tb];
     e.new_data   = f.new_data[cws[i].tb];
   }
-  ret = srsran_dlsch_gpu_decode_batch(&q->dl_sch, (uint32_t)tbs.size(), tbs.data(), d_result, d_avg_noi, stream);
+  ret = dlsch_gpu_decode_batch_early_copy(&q->dl_sch, (uint32_t)tbs.size(), tbs.data(), d_result, d_avg_noi, stream);
   return ret == SRSRAN_SUCCESS ? (int)tbs.size() : ret;
 }
 

@@ -18,5 +18,10 @@ uint32_t pdsch_seed(uint16_t rnti, int q, uint32_t nslot, uint32_t cell_id);
 std::vector<uint32_t> pdsch_re_table(const srsran_cell_t& cell, const srsran_pdsch_grant_t& g, uint32_t lstart,
                                      uint32_t sf_idx);
 
+// srsran_dlsch_gpu_decode_batch with the descriptor upload on the DL-SCH object's copy stream (sch_api.cpp),
+// for callers whose stream has work queued in front of the decode
+int dlsch_gpu_decode_batch_early_copy(srsran_sch_t* q, uint32_t nof_tb, const srsran_dlsch_gpu_tb_t* tbs,
+                                      int32_t* d_result, float* d_avg_noi, void* stream);
+
 }  // namespace srsran_amd
 #endif

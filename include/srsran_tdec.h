@@ -87,11 +87,26 @@ uint32_t srsran_tdec_autoimp_get_subblocks_8bit(uint32_t long_cb);
 void srsran_tdec_iteration(srsran_tdec_t* h, int16_t* input, uint8_t* output);
 /* turbodecoder.c:536-549: nof_iterations half-iterations, then hard decision. */
 int srsran_tdec_run_all(srsran_tdec_t* h, int16_t* input, uint8_t* output, uint32_t nof_iterations, uint32_t long_cb);
-/* turbodecoder.c:551-577: the 8-bit decoders are not provided; these report SRSRAN_ERROR. */
+/* turbodecoder.c:551-577 (AUTO, tdec_iteration_8 at :455-483): int8 LLRs; K > 2048 on the AVX2 8-bit
+ * window decoder (32 sub-blocks), 800 < K <= 2048 on the SSE 8-bit window decoder (16), smaller K (and a
+ * manually selected 16-bit decoder) on the 16-bit decoders after widening (convert_8_to_16).  Input layout
+ * as srsran_tdec_run_all: sub-block (3 (K + 32) + 12) unless srsran_tdec_force_not_sb or K <= 400. */
 void srsran_tdec_iteration_8bit(srsran_tdec_t* h, int8_t* input, uint8_t* output);
 int  srsran_tdec_run_all_8bit(srsran_tdec_t* h, int8_t* input, uint8_t* output, uint32_t nof_iterations, uint32_t long_cb);
 
-/* ---------------- batch extensions (new names; no reference counterpart) ---------------- */
+/* ---------------- batch extensions (new names; no reference counterpart) -----
+ * srsran_tdec_gpu_run_batch_8bit: srsran_tdec_run_all_8bit over nof_cb device-resident int8 code blocks
+ * (in_stride bytes apart) on a HIP stream (NULL = the null stream); layout_sb as srsran_tdec_gpu_run_batch;
+ * decisions to d_output (nof_cb x K/8 bytes).  Asynchronous. */
+int srsran_tdec_gpu_run_batch_8bit(uint32_t      long_cb,
+                                   const int8_t* d_input,
+                                   uint32_t      in_stride,
+                                   int           layout_sb,
+                                   uint8_t*      d_output,
+                                   uint32_t      nof_cb,
+                                   uint32_t      nof_iterations,
+                                   void*         stream);
+/* ---------------- */
 
 /*
  * Decode nof_cb code blocks of the same size with srsran_tdec_run_all semantics.

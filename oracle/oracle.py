@@ -32,6 +32,7 @@ LTE_CRC24B = 0x1800063  # phy_common.h:73
 _i16p = ctypes.POINTER(ctypes.c_int16)
 _u8p = ctypes.POINTER(ctypes.c_uint8)
 _u16p = ctypes.POINTER(ctypes.c_uint16)
+_i8p = ctypes.POINTER(ctypes.c_int8)
 
 
 def _ptr(a, t):
@@ -45,6 +46,15 @@ def nof_subblocks(K):
     if K % 8 == 0 and K > 400:
         return 8
     return 0
+
+
+def tdec8_subblocks(K):
+    """srsran_tdec_autoimp_get_subblocks_8bit (turbodecoder.c:410-424, AVX2 build)."""
+    if K % 32 == 0 and K > 2048:
+        return 32
+    if K % 16 == 0 and K > 800:
+        return 16
+    return nof_subblocks(K)
 
 
 def in_len(K, layout_sb):
@@ -397,6 +407,39 @@ class Reference(_Lib, _PhyMixin):
         if self.lib.ref_tcod_encode(K, _ptr(bits, _u8p), _ptr(out, _u8p)):
             raise ValueError(K)
         return out
+
+    def tdec8_run(self, K, llr, layout_sb=False, nof_iterations=8, trace=False):
+        """srsran_tdec_run_all_8bit (AUTO, AVX2 build) on one int8 code block (ref_tdec8_run)."""
+        f = self.lib.ref_tdec8_run
+        f.argtypes = [ctypes.c_uint32, _i8p, ctypes.c_int, ctypes.c_uint32, _u8p, _i8p]
+        f.restype = ctypes.c_int
+        sb = layout_sb and tdec8_subblocks(K) > 0
+        n = 3 * (K + 32) + 12 if sb else 3 * K + 12
+        llr = np.ascontiguousarray(llr, dtype=np.int8)
+        assert llr.size >= n
+        out = np.zeros(K // 8, dtype=np.uint8)
+        tr = np.zeros((nof_iterations, K), dtype=np.int8) if trace else None
+        if f(K, _ptr(llr, _i8p), int(bool(layout_sb)), nof_iterations, _ptr(out, _u8p), _ptr(tr, _i8p) if trace else None):
+            raise ValueError(f"tdec8_run failed K={K}")
+        return (out, tr) if trace else out
+
+    def interleaver(self, K, win):
+        """forward / reverse tables of srsran_tc_interl_LTE_gen_interl(K, win) (tc_interl_lte.c:69-107)."""
+
+        class Interl(ctypes.Structure):
+            _fields_ = [("forward", _u16p), ("reverse", _u16p), ("max_long_cb", ctypes.c_uint32)]
+
+        h = Interl()
+        L = self.lib
+        L.srsran_tc_interl_init.argtypes = [ctypes.POINTER(Interl), ctypes.c_uint32]
+        L.srsran_tc_interl_LTE_gen_interl.argtypes = [ctypes.POINTER(Interl), ctypes.c_uint32, ctypes.c_uint32]
+        L.srsran_tc_interl_free.argtypes = [ctypes.POINTER(Interl)]
+        if L.srsran_tc_interl_init(ctypes.byref(h), K) or L.srsran_tc_interl_LTE_gen_interl(ctypes.byref(h), K, win):
+            raise ValueError(K)
+        fwd = np.ctypeslib.as_array(h.forward, shape=(K,)).copy()
+        rev = np.ctypeslib.as_array(h.reverse, shape=(K,)).copy()
+        L.srsran_tc_interl_free(ctypes.byref(h))
+        return fwd, rev
 
     def crc_byte(self, poly, order, data, nbits):
         data = np.ascontiguousarray(data, dtype=np.uint8)

@@ -67,6 +67,30 @@ static srsran_tdec_16bit_impl_t ref_avx16_impl = {tdec_winavx16_init,
 #include "srsran/phy/fec/turbo/turbodecoder_iter.h"
 #undef LLR_IS_16BIT
 
+/* The 8-bit window decoders (turbodecoder.c:76-97): SSE 16 sub-blocks, AVX2 32 sub-blocks. */
+#define WINIMP_IS_SSE8
+#include "srsran/phy/fec/turbo/turbodecoder_win.h"
+#undef WINIMP_IS_SSE8
+
+#define WINIMP_IS_AVX8
+#include "srsran/phy/fec/turbo/turbodecoder_win.h"
+#undef WINIMP_IS_AVX8
+
+static srsran_tdec_8bit_impl_t ref_sse8_impl = {tdec_winsse8_init,
+                                                tdec_winsse8_free,
+                                                tdec_winsse8_dec,
+                                                tdec_winsse8_extract_input,
+                                                tdec_winsse8_decision_byte};
+static srsran_tdec_8bit_impl_t ref_avx8_impl = {tdec_winavx8_init,
+                                                tdec_winavx8_free,
+                                                tdec_winavx8_dec,
+                                                tdec_winavx8_extract_input,
+                                                tdec_winavx8_decision_byte};
+
+#define LLR_IS_8BIT
+#include "srsran/phy/fec/turbo/turbodecoder_iter.h"
+#undef LLR_IS_8BIT
+
 /* Restated from turbodecoder.c:381-393 (this symbol is also needed by rm_turbo.c). */
 uint32_t srsran_tdec_autoimp_get_subblocks(uint32_t long_cb)
 {
@@ -123,6 +147,13 @@ static int harness_init(void)
       return -1;
     }
   }
+  h->dec8[0] = &ref_sse8_impl; /* AUTO_8_SSEWIN */
+  h->dec8[1] = &ref_avx8_impl; /* AUTO_8_AVXWIN */
+  for (int td = 0; td < SRSRAN_TDEC_NOF_AUTO_MODES_8; td++) {
+    if ((h->nof_blocks8[td] = h->dec8[td]->tdec_init(&h->dec8_hdlr[td], h->max_long_cb)) < 0) {
+      return -1;
+    }
+  }
   for (int s = 0; s < 4; s++) {
     for (int i = 0; i < SRSRAN_NOF_TC_CB_SIZES; i++) {
       if (srsran_tc_interl_init(&h->interleaver[s][i], srsran_cbsegm_cbsize(i)) < 0) {
@@ -136,7 +167,7 @@ static int harness_init(void)
   return 0;
 }
 
-static uint32_t inter_idx(uint32_t nsb) { return nsb == 16 ? 2 : (nsb == 8 ? 1 : 0); }
+static uint32_t inter_idx(uint32_t nsb) { return nsb == 32 ? 3 : (nsb == 16 ? 2 : (nsb == 8 ? 1 : 0)); }
 
 /* tdec_iteration_16 (turbodecoder.c:486-507), AUTO 16-bit branch only. */
 static void harness_iteration(srsran_tdec_t* h, int16_t* input)
@@ -162,6 +193,70 @@ static void latest_natural(srsran_tdec_t* h, int16_t* dst)
   for (uint32_t n = 0; n < K; n++) {
     dst[n] = src[(n % L) * nsb + n / L];
   }
+}
+
+/*
+ * ref_tdec8_run: srsran_tdec_run_all_8bit (turbodecoder.c:560-577) on one code block, AUTO on an AVX2
+ * build: tdec_iteration_8 (turbodecoder.c:455-483) with tdec_sb_idx_8 (:426-441).  Where no 8-bit
+ * decoder takes K (K <= 800) the reference widens the first 3K+12 values (convert_8_to_16) and runs the
+ * 16-bit decoder; with the sub-block layout the rest of its widened buffer is left from earlier calls, so
+ * this harness widens the whole layout (3 (K + 32) + 12) instead.
+ *  layout_sb: as ref_tdec_run.  trace (optional): nof_iterations*K int8, latest output per half-iteration.
+ */
+int ref_tdec8_run(uint32_t K, const int8_t* input, int layout_sb, uint32_t nof_iterations, uint8_t* out, int8_t* trace)
+{
+  if (harness_init()) {
+    return -1;
+  }
+  srsran_tdec_t* h = &tdec;
+  int cbidx        = srsran_cbsegm_cbindex(K);
+  if (cbidx < 0 || srsran_cbsegm_cbsize(cbidx) != (int)K || nof_iterations < 1) {
+    return -1;
+  }
+  uint32_t nsb8 = srsran_tdec_autoimp_get_subblocks_8bit(K);
+  if (nsb8 < 16) {
+    uint32_t n    = layout_sb && nsb8 ? 3 * (K + 32) + 12 : 3 * K + 12;
+    int16_t* wide = srsran_vec_i16_malloc(3 * (K + 32) + 12 + 64);
+    memset(wide, 0, (3 * (K + 32) + 12 + 64) * sizeof(int16_t));
+    for (uint32_t i = 0; i < n; i++) {
+      wide[i] = input[i];
+    }
+    int16_t* tr16 = trace ? malloc(sizeof(int16_t) * nof_iterations * K) : NULL;
+    int      ret  = ref_tdec_run(K, wide, layout_sb, nof_iterations, out, tr16);
+    if (trace) {
+      for (uint32_t i = 0; i < nof_iterations * K; i++) {
+        trace[i] = (int8_t)tr16[i];
+      }
+      free(tr16);
+    }
+    free(wide);
+    return ret;
+  }
+  h->force_not_sb  = layout_sb ? false : true;
+  uint32_t in_len  = layout_sb ? 3 * (K + 32) + 12 : 3 * K + 12;
+  int8_t*  buf     = srsran_vec_i8_malloc(3 * (K + 32) + 12 + 64);
+  memset(buf, 0, 3 * (K + 32) + 12 + 64);
+  memcpy(buf, input, in_len);
+  h->n_iter            = 0;
+  h->current_long_cb   = K;
+  h->current_cbidx     = cbidx;
+  h->current_llr_type  = SRSRAN_TDEC_8;
+  h->current_dec       = nsb8 == 32 ? 1 : 0;
+  h->current_inter_idx = inter_idx((uint32_t)h->nof_blocks8[h->current_dec]);
+  do {
+    run_tdec_iteration_8bit(h, buf);
+    if (trace) {
+      int8_t*  src = !(h->n_iter % 2) ? (int8_t*)h->app1 : (int8_t*)h->ext1;
+      uint32_t L   = K / nsb8;
+      for (uint32_t n = 0; n < K; n++) {
+        trace[(size_t)(h->n_iter - 1) * K + n] = src[(n % L) * nsb8 + n / L];
+      }
+    }
+  } while (h->n_iter < (int)nof_iterations);
+  h->dec8[h->current_dec]->tdec_decision_byte(!(h->n_iter % 2) ? (int8_t*)h->app1 : (int8_t*)h->ext1, out, K);
+  h->current_llr_type = SRSRAN_TDEC_16;
+  free(buf);
+  return 0;
 }
 
 /*

@@ -1,0 +1,31 @@
+// srsran_4g_amd/csrc/tdec8bit_kernel.h -- launch interface of the 8-bit LLR turbo decoder
+// (tdec8bit_kernel.hip): the reference's SSE / AVX2 8-bit window decoders, 16 or 32 sub-blocks.
+#ifndef SRSRAN_AMD_TDEC8BIT_KERNEL_H
+#define SRSRAN_AMD_TDEC8BIT_KERNEL_H
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace srsran_amd {
+
+struct Tdec8Args {
+  const int8_t* in;         // ncb code blocks of int8 LLRs, in_stride bytes apart (device)
+  uint32_t      in_stride;
+  int           layout_sb;  // 0: natural 3K+12, 1: sub-block layout (3 (K + 32) + 12, rm_turbo)
+  uint32_t      K;
+  uint32_t      ncb;
+  int           n_end;      // half-iterations to run (>= 1)
+  uint8_t*      out;        // ncb * K/8 hard-decision bytes (device)
+  uint2*        beta;       // scratch, tdec8bit_beta_bytes (device)
+  uint32_t      f1, f2;     // QPP coefficients of K
+};
+
+size_t     tdec8bit_lds_bytes(int nsb, uint32_t K);
+size_t     tdec8bit_beta_bytes(int nsb, uint32_t K, uint32_t ncb);
+hipError_t tdec8bit_launch(int nsb, const Tdec8Args& a, hipStream_t stream);
+// int8 -> int16 copy of ncb rows (in_stride bytes apart) of len LLRs into a dense int16 array
+hipError_t tdec8bit_widen(const int8_t* in, uint32_t in_stride, short* out, uint32_t len, uint32_t ncb,
+                          hipStream_t stream);
+
+}  // namespace srsran_amd
+#endif

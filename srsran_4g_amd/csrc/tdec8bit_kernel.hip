@@ -1,0 +1,405 @@
+// srsran_4g_amd/csrc/tdec8bit_kernel.hip -- the 8-bit LLR turbo decoder (srsran_tdec_run_all_8bit):
+// srsRAN_4G's SSE 8-bit window decoder (16 sub-blocks, 800 < K <= 2048) and AVX2 8-bit window decoder
+// (32 sub-blocks, K > 2048), turbodecoder_win.h with WINIMP_IS_SSE8 / WINIMP_IS_AVX8 (lines 154-300,
+// 480-832) driven by turbodecoder_iter.h:72-144 (LLR_IS_8BIT) and turbodecoder.c:455-483.  Smaller K
+// take the 16-bit decoders on the widened input, as the reference does (srsran_tdec_gpu_run_batch_8bit in tdec_api.cpp).
+//
+// The arithmetic of those decoders, restated:
+//   * metrics are int8 with saturating add / sub (_mm_adds_epi8), -INF = 0 (INF 0): unknown states
+//     start at 0, and the first sub-block's alpha start state is all zeros too;
+//   * normalisation every step but k = 0 by the maximum over the 8 states (normalize_max);
+//   * the tail trellis (beta_trellis) saturates upwards only ((int16)x + y > 127 ? 127 : (int8));
+//   * the LLR m1 - m0 (saturating) is halved by an arithmetic shift (divide_output 1).
+//
+// Mapping: ONE LANE PER SUB-BLOCK, the 8 states of the lane's sub-block in 8 registers (int8 values held
+// in int32).  A workgroup is one wave: 64 / NSB code blocks.  The block's input streams, a-priori and
+// extrinsic arrays live in LDS (7 x (K + 4) bytes); the beta metrics of a MAP pass go to a global scratch
+// ([block][position][lane] x 8 bytes, one 8-byte store a lane a position, coalesced over the block's
+// lanes) and are read back by the alpha pass of the same lane.  All half-iterations run in one launch.
+// This is the off-by-default path of srsUE (srsue/src/main.cc:404-406); it is written for parity, not
+// tuned like the 16-bit decoders.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "tdec8bit_kernel.h"
+
+namespace srsran_amd {
+namespace {
+
+constexpr int OVL = 40;  // win_overlap_len (turbodecoder_win.h:182, 291)
+
+__device__ __forceinline__ int sat8(int v) { return v > 127 ? 127 : (v < -128 ? -128 : v); }
+__device__ __forceinline__ int sadd(int a, int b) { return sat8(a + b); }
+__device__ __forceinline__ int ssub(int a, int b) { return sat8(a - b); }
+// beta_trellis's sadd (turbodecoder_win.h:470-478 with use_saturated_add): upper clamp, int8 wrap below
+__device__ __forceinline__ int tadd(int a, int b)
+{
+  const int z = a + b;
+  return z > 127 ? 127 : (int)(int8_t)z;
+}
+
+// normalize() with normalize_max and normalize_period 1 (turbodecoder_win.h:480-498)
+__device__ __forceinline__ void normalize(int k, int o[8])
+{
+  if (k != 0) {
+    int m = max(o[0], o[1]);
+#pragma unroll
+    for (int i = 2; i < 8; i++) {
+      m = max(m, o[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      o[i] = ssub(o[i], m);
+    }
+  }
+}
+
+// backward step (turbodecoder_win.h:641-664)
+__device__ __forceinline__ void beta_step(int o[8], int x, int y)
+{
+  const int xy = sadd(x, y);
+  int       n[8];
+  n[0] = max(sadd(o[4], xy), o[0]);
+  n[1] = max(o[4], sadd(o[0], xy));
+  n[2] = max(sadd(o[5], y), sadd(o[1], x));
+  n[3] = max(sadd(o[5], x), sadd(o[1], y));
+  n[4] = max(sadd(o[6], x), sadd(o[2], y));
+  n[5] = max(sadd(o[6], y), sadd(o[2], x));
+  n[6] = max(o[7], sadd(o[3], xy));
+  n[7] = max(sadd(o[7], xy), o[3]);
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    o[i] = n[i];
+  }
+}
+
+// forward-step branch candidates (turbodecoder_win.h:767-785): mb = bit-0 branch, nw = bit-1 branch
+__device__ __forceinline__ void alpha_cand(const int o[8], int x, int y, int mb[8], int nw[8])
+{
+  const int xy = sadd(x, y);
+  mb[0] = o[0];
+  mb[1] = sadd(o[3], y);
+  mb[2] = sadd(o[4], y);
+  mb[3] = o[7];
+  mb[4] = o[1];
+  mb[5] = sadd(o[2], y);
+  mb[6] = sadd(o[5], y);
+  mb[7] = o[6];
+  nw[0] = sadd(o[1], xy);
+  nw[1] = sadd(o[2], x);
+  nw[2] = sadd(o[5], x);
+  nw[3] = sadd(o[6], xy);
+  nw[4] = sadd(o[0], xy);
+  nw[5] = sadd(o[3], x);
+  nw[6] = sadd(o[4], x);
+  nw[7] = sadd(o[7], xy);
+}
+
+__device__ __forceinline__ uint2 pack8(const int o[8])
+{
+  uint2 r;
+  r.x = (uint32_t)(o[0] & 0xff) | ((uint32_t)(o[1] & 0xff) << 8) | ((uint32_t)(o[2] & 0xff) << 16) |
+        ((uint32_t)(o[3] & 0xff) << 24);
+  r.y = (uint32_t)(o[4] & 0xff) | ((uint32_t)(o[5] & 0xff) << 8) | ((uint32_t)(o[6] & 0xff) << 16) |
+        ((uint32_t)(o[7] & 0xff) << 24);
+  return r;
+}
+__device__ __forceinline__ void unpack8(uint2 r, int o[8])
+{
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    o[i]     = (int)(int8_t)(r.x >> (8 * i));
+    o[4 + i] = (int)(int8_t)(r.y >> (8 * i));
+  }
+}
+
+// One MAP pass of a lane over its sub-block d (turbodecoder_win.h:551-832): X systematic (or the
+// de-interleaved extrinsic of DEC 1), A optional a-priori, P parity, all SB-ordered in LDS with the
+// tail at [K, K + 3); OUT the extrinsic LLRs.  beta: this block's scratch, [Ls + 1][NSB] x 8 bytes.
+template <int NSB>
+__device__ void map_pass(const int8_t* X, const int8_t* A, const int8_t* P, int8_t* OUT, int d, int Ls, int K,
+                         uint2* beta)
+{
+  int o[8];
+  // ---- beta (win.h:551-681) ----
+  // training over the first OVL positions of this sub-block, from unknown (0) states
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    o[i] = 0;
+  }
+  for (int k = OVL - 1; k >= 0; k--) {
+    const int q = k * NSB + d;
+    int       x = X[q];
+    if (A) {
+      x = sadd(A[q], x);
+    }
+    beta_step(o, x, P[q]);
+    normalize(k, o);
+  }
+  // the end state of sub-block d is the training result of sub-block d + 1 (move_right); the last
+  // sub-block's comes from the tail (beta_trellis, win.h:500-548)
+  int e[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    e[i] = __shfl_down(o[i], 1, NSB);
+  }
+  if (d == NSB - 1) {
+    int t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int k = K + 2; k >= K; k--) {
+      const int x = X[k], y = P[k], xy = tadd(x, y);
+      int       mb[8], nw[8];
+      mb[0] = tadd(t[4], xy);
+      mb[1] = t[4];
+      mb[2] = tadd(t[5], y);
+      mb[3] = tadd(t[5], x);
+      mb[4] = tadd(t[6], x);
+      mb[5] = tadd(t[6], y);
+      mb[6] = t[7];
+      mb[7] = tadd(t[7], xy);
+      nw[0] = t[0];
+      nw[1] = tadd(t[0], xy);
+      nw[2] = tadd(t[1], x);
+      nw[3] = tadd(t[1], y);
+      nw[4] = tadd(t[2], y);
+      nw[5] = tadd(t[2], x);
+      nw[6] = tadd(t[3], xy);
+      nw[7] = t[3];
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        t[i] = mb[i] > nw[i] ? mb[i] : nw[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      e[i] = t[i];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    o[i] = e[i];
+  }
+  beta[(size_t)Ls * NSB + d] = pack8(o);
+  for (int k = Ls - 1; k >= 0; k--) {
+    const int q = k * NSB + d;
+    int       x = X[q];
+    if (A) {
+      x = sadd(A[q], x);
+    }
+    beta_step(o, x, P[q]);
+    beta[(size_t)k * NSB + d] = pack8(o);  // stored before normalisation (win.h:666-678)
+    normalize(k, o);
+  }
+  // ---- alpha (win.h:684-832) ----
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    o[i] = 0;
+  }
+  for (int k = 0; k < OVL; k++) {
+    const int q = (Ls - OVL + k) * NSB + d;
+    int       x = X[q];
+    if (A) {
+      x = sadd(A[q], x);
+    }
+    int mb[8], nw[8];
+    alpha_cand(o, x, P[q], mb, nw);
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      o[i] = max(mb[i], nw[i]);
+    }
+    normalize(k, o);
+  }
+  // the start state of sub-block d is the training result of sub-block d - 1 (move_left); sub-block 0
+  // starts known: state 0 at 0, the others at -INF = 0
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    e[i] = __shfl_up(o[i], 1, NSB);
+    o[i] = d == 0 ? 0 : e[i];
+  }
+  for (int k = 0; k < Ls; k++) {
+    const int q = k * NSB + d;
+    int       x = X[q];
+    if (A) {
+      x = sadd(A[q], x);
+    }
+    int mb[8], nw[8];
+    alpha_cand(o, x, P[q], mb, nw);
+    int b[8];
+    unpack8(beta[(size_t)(k + 1) * NSB + d], b);
+    int m0 = sadd(b[0], mb[0]), m1 = sadd(b[0], nw[0]);
+#pragma unroll
+    for (int i = 1; i < 8; i++) {
+      m0 = max(m0, sadd(b[i], mb[i]));
+      m1 = max(m1, sadd(b[i], nw[i]));
+    }
+    OUT[q] = (int8_t)(ssub(m1, m0) >> 1);  // simd_rb_shift by divide_output (win.h:810-813)
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      o[i] = max(mb[i], nw[i]);
+    }
+    normalize(k, o);
+  }
+}
+
+// slot (SB index) of the QPP image of the position at slot q: forward of tc_interl_lte.c:88-106
+__device__ __forceinline__ int qpp_sb(int q, int K, int Ls, int nsb, uint32_t f1, uint32_t f2)
+{
+  const uint32_t n  = (uint32_t)((q % nsb) * Ls + q / nsb);            // inter(q, win)
+  const uint32_t fn = (uint32_t)((((f2 * n) % K) * n + f1 * n) % K);  // pi(n)
+  return (int)((fn % Ls) * nsb + fn / Ls);                            // deinter(., win)
+}
+
+template <int NSB>
+__global__ __launch_bounds__(64) void tdec8bit_kernel(Tdec8Args a)
+{
+  constexpr int CPW = 64 / NSB;
+  extern __shared__ __align__(16) int8_t lds[];
+  const int      lane = threadIdx.x;
+  const int      cb_l = lane / NSB;
+  const int      d    = lane % NSB;
+  const int      K    = (int)a.K;
+  const int      Ls   = K / NSB;
+  const int      AL   = (K + 4 + 15) & ~15;
+  const uint32_t cb   = blockIdx.x * CPW + cb_l;
+  const bool     live = cb < a.ncb;
+
+  int8_t* base = lds + (size_t)cb_l * 7 * AL;
+  int8_t* SY   = base;           // systematic
+  int8_t* P0   = base + AL;      // parity 0
+  int8_t* P1   = base + 2 * AL;  // parity 1
+  int8_t* A1   = base + 3 * AL;  // app1
+  int8_t* A2   = base + 4 * AL;  // app2
+  int8_t* E1   = base + 5 * AL;  // ext1
+  int8_t* E2   = base + 6 * AL;  // ext2
+
+  // ---- input streams (turbodecoder_iter.h:61-96 / win.h:880-923) ----
+  if (live) {
+    const int8_t* in = a.in + (size_t)cb * a.in_stride;
+    if (a.layout_sb) {
+      for (int q = d; q < K; q += NSB) {
+        SY[q] = in[q];
+        P0[q] = in[K + 32 + q];
+        P1[q] = in[2 * (K + 32) + q];
+      }
+      if (d < 3) {
+        const int t = 3 * (K + 32) + 2 * d;
+        SY[K + d] = in[t];
+        P0[K + d] = in[t + 1];
+        A2[K + d] = in[t + 6];
+        P1[K + d] = in[t + 7];
+      }
+    } else {
+      for (int i = 0; i < Ls; i++) {
+        const int q = i * NSB + d, n = i + d * Ls;
+        SY[q] = in[3 * n];
+        P0[q] = in[3 * n + 1];
+        P1[q] = in[3 * n + 2];
+      }
+      if (d < 3) {
+        const int t = 3 * K + 2 * d;
+        SY[K + d] = in[t];
+        P0[K + d] = in[t + 1];
+        A2[K + d] = in[t + 6];
+        P1[K + d] = in[t + 7];
+      }
+    }
+  }
+  __syncthreads();
+
+  uint2* beta = a.beta + (size_t)cb * (Ls + 1) * NSB;
+  for (int n = 0; n < a.n_end; n++) {
+    if ((n & 1) == 0) {
+      if (n && live) {
+        for (int q = d; q < K; q += NSB) {
+          A1[q] = (int8_t)ssub(A1[q], E1[q]);  // srsran_vec_sub_bbb (saturating for K % 16 == 0)
+        }
+      }
+      __syncthreads();
+      if (live) {
+        map_pass<NSB>(SY, n ? A1 : nullptr, P0, E1, d, Ls, K, beta);
+      }
+      __syncthreads();
+    } else {
+      if (n > 1 && live) {
+        for (int q = d; q < K; q += NSB) {
+          E1[q] = (int8_t)ssub(E1[q], A1[q]);
+        }
+      }
+      __syncthreads();
+      if (live) {
+        // app2[deinter[i]] = ext1[i]  <=>  app2[j] = ext1[forward[j]]  (srsran_vec_lut_bbb)
+        for (int j = d; j < K; j += NSB) {
+          A2[j] = E1[qpp_sb(j, K, Ls, NSB, a.f1, a.f2)];
+        }
+      }
+      __syncthreads();
+      if (live) {
+        map_pass<NSB>(A2, nullptr, P1, E2, d, Ls, K, beta);
+      }
+      __syncthreads();
+      if (live) {
+        // app1[inter[i]] = ext2[i]
+        for (int i = d; i < K; i += NSB) {
+          A1[qpp_sb(i, K, Ls, NSB, a.f1, a.f2)] = E2[i];
+        }
+      }
+      __syncthreads();
+    }
+  }
+
+  // ---- decision (turbodecoder.c:370-378, win.h:973-993): bit n = latest(SB slot of n) > 0 ----
+  if (live) {
+    const int8_t* src = (a.n_end & 1) ? E1 : A1;
+    uint8_t*      out = a.out + (size_t)cb * (K / 8);
+    for (int byte = d; byte < K / 8; byte += NSB) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int b = 0; b < 8; b++) {
+        const int n = byte * 8 + b;
+        v |= (src[(n % Ls) * NSB + n / Ls] > 0 ? 1u : 0u) << (7 - b);
+      }
+      out[byte] = (uint8_t)v;
+    }
+  }
+}
+
+// convert_8_to_16 (turbodecoder.c:438-444) over ncb blocks: int8 rows of in_stride bytes -> int16 rows of len
+__global__ void tdec8bit_widen_kernel(const int8_t* in, uint32_t in_stride, short* out, uint32_t len, uint32_t ncb)
+{
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < (size_t)len * ncb) {
+    const size_t b = i / len, j = i % len;
+    out[i]         = in[b * in_stride + j];
+  }
+}
+
+}  // namespace
+
+hipError_t tdec8bit_widen(const int8_t* in, uint32_t in_stride, short* out, uint32_t len, uint32_t ncb,
+                          hipStream_t stream)
+{
+  const size_t n = (size_t)len * ncb;
+  hipLaunchKernelGGL(tdec8bit_widen_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, in, in_stride, out,
+                     len, ncb);
+  return hipGetLastError();
+}
+
+size_t tdec8bit_lds_bytes(int nsb, uint32_t K) { return (size_t)(64 / nsb) * 7 * ((K + 4 + 15) & ~15u); }
+size_t tdec8bit_beta_bytes(int nsb, uint32_t K, uint32_t ncb) { return (size_t)ncb * (K / nsb + 1) * nsb * 8; }
+
+hipError_t tdec8bit_launch(int nsb, const Tdec8Args& a, hipStream_t stream)
+{
+  if ((nsb != 16 && nsb != 32) || a.K % nsb || a.K / nsb < (uint32_t)OVL || a.ncb == 0) {
+    return hipErrorInvalidValue;
+  }
+  const uint32_t cpw  = 64 / nsb;
+  const dim3     grid((a.ncb + cpw - 1) / cpw);
+  const size_t   lds  = tdec8bit_lds_bytes(nsb, a.K);
+  if (nsb == 16) {
+    hipLaunchKernelGGL(tdec8bit_kernel<16>, grid, dim3(64), lds, stream, a);
+  } else {
+    hipLaunchKernelGGL(tdec8bit_kernel<32>, grid, dim3(64), lds, stream, a);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace srsran_amd

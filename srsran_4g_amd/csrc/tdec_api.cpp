@@ -23,6 +23,7 @@
 #include "../../include/srsran_tdec.h"
 #include "devkey.h"
 #include "tdec_kernel.h"
+#include "tdec8bit_kernel.h"
 
 using namespace srsran_amd;
 
@@ -901,23 +902,122 @@ int srsran_tdec_gpu_debug_set_stamps(void* d_buf)
 }
 #endif
 
-void srsran_tdec_iteration_8bit(srsran_tdec_t* h, int8_t* input, uint8_t* output)
+// ---- 8-bit LLR decoders (turbodecoder.c:455-483, 551-577) ----
+// AUTO: K > 2048 on the AVX2 8-bit window decoder (32 sub-blocks), 800 < K <= 2048 on the SSE 8-bit
+// window decoder (16), smaller K on the 16-bit decoders after widening the input (convert_8_to_16);
+// a manually selected 16-bit decoder widens as well (tdec_iteration_8 with dec_type != AUTO).
+int srsran_tdec_gpu_run_batch_8bit(uint32_t      long_cb,
+                                   const int8_t* d_input,
+                                   uint32_t      in_stride,
+                                   int           layout_sb,
+                                   uint8_t*      d_output,
+                                   uint32_t      nof_cb,
+                                   uint32_t      nof_iterations,
+                                   void*         stream)
 {
-  (void)h;
-  (void)input;
-  (void)output;
-  fprintf(stderr, "[srsran_tdec] 8-bit decoder not provided\n");
+  using namespace srsran_amd;
+  const int idx = cb_index(long_cb);
+  if (!d_input || !d_output || idx < 0) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  if (nof_cb == 0) {
+    return SRSRAN_SUCCESS;
+  }
+  hipStream_t    s     = (hipStream_t)stream;
+  const uint32_t nsb8  = srsran_tdec_autoimp_get_subblocks_8bit(long_cb);
+  const bool     sb    = layout_sb && nsb8 > 0;
+  const uint32_t len   = sb ? 3 * (long_cb + 32) + 12 : 3 * long_cb + 12;
+  const int      n_end = nof_iterations > 0 ? (int)nof_iterations : 1;
+  if (in_stride < len) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  if (nsb8 == 16 || nsb8 == 32) {
+    Tdec8Args a{};
+    a.in        = d_input;
+    a.in_stride = in_stride;
+    a.layout_sb = sb ? 1 : 0;
+    a.K         = long_cb;
+    a.ncb       = nof_cb;
+    a.n_end     = n_end;
+    a.out       = d_output;
+    qpp_coeffs((uint32_t)idx, &a.f1, &a.f2);
+    void* beta = nullptr;
+    if (hipMallocAsync(&beta, tdec8bit_beta_bytes((int)nsb8, long_cb, nof_cb), s) != hipSuccess) {
+      return SRSRAN_ERROR;
+    }
+    a.beta           = (uint2*)beta;
+    const hipError_t e = tdec8bit_launch((int)nsb8, a, s);
+    (void)hipFreeAsync(beta, s);
+    tdec_set_last_kernel(nsb8 == 32 ? "tdec8bit_kernel<32>" : "tdec8bit_kernel<16>");
+    return e == hipSuccess ? SRSRAN_SUCCESS : SRSRAN_ERROR;
+  }
+  // 16-bit decoder on the widened input
+  short* wide = nullptr;
+  if (hipMallocAsync((void**)&wide, (size_t)nof_cb * len * sizeof(short), s) != hipSuccess) {
+    return SRSRAN_ERROR;
+  }
+  int ret = tdec8bit_widen(d_input, in_stride, wide, len, nof_cb, s) == hipSuccess
+                ? srsran_tdec_gpu_run_batch(long_cb, wide, len, sb ? 1 : 0, d_output, nof_cb, nof_iterations, stream)
+                : SRSRAN_ERROR;
+  (void)hipFreeAsync(wide, s);
+  return ret;
 }
 
 int srsran_tdec_run_all_8bit(srsran_tdec_t* h, int8_t* input, uint8_t* output, uint32_t nof_iterations, uint32_t long_cb)
 {
-  (void)h;
-  (void)input;
-  (void)output;
-  (void)nof_iterations;
-  (void)long_cb;
-  fprintf(stderr, "[srsran_tdec] 8-bit decoder not provided\n");
-  return SRSRAN_ERROR;
+  if (!h || !h->gpu || !input || !output) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  if (srsran_tdec_new_cb(h, long_cb)) {
+    return SRSRAN_ERROR;
+  }
+  const uint32_t nsb8 = srsran_tdec_autoimp_get_subblocks_8bit(long_cb);
+  if (h->dec_type != SRSRAN_TDEC_AUTO || nsb8 < 16) {
+    // convert_8_to_16 + the 16-bit decoder of this K (or the manually selected one)
+    Config* c = get_config(long_cb, nsb_for(h, long_cb));
+    if (!c) {
+      return SRSRAN_ERROR;
+    }
+    const size_t         n = input_len(h, c, long_cb);
+    std::vector<int16_t> wide(n);
+    for (size_t i = 0; i < n; i++) {
+      wide[i] = input[i];
+    }
+    return srsran_tdec_run_all(h, wide.data(), output, nof_iterations, long_cb);
+  }
+  Ctx*           ctx = (Ctx*)h->gpu;
+  const bool     sb  = !h->force_not_sb;
+  const uint32_t len = sb ? 3 * (long_cb + 32) + 12 : 3 * long_cb + 12;
+  if (!grow((void**)&ctx->d_bin, &ctx->bin_elems, len) || !grow((void**)&ctx->d_bout, &ctx->bout_bytes, long_cb / 8)) {
+    return SRSRAN_ERROR;
+  }
+  hipMemcpyAsync(ctx->d_bin, input, len, hipMemcpyHostToDevice, ctx->stream);
+  int ret = srsran_tdec_gpu_run_batch_8bit(long_cb, (const int8_t*)ctx->d_bin, len, sb ? 1 : 0, ctx->d_bout, 1,
+                                           nof_iterations, ctx->stream);
+  if (ret != SRSRAN_SUCCESS) {
+    return ret;
+  }
+  hipMemcpyAsync(output, ctx->d_bout, long_cb / 8, hipMemcpyDeviceToHost, ctx->stream);
+  if (hipStreamSynchronize(ctx->stream) != hipSuccess) {
+    fprintf(stderr, "[srsran_tdec] 8-bit decode failed: %s\n", hipGetErrorString(hipGetLastError()));
+    return SRSRAN_ERROR;
+  }
+  h->n_iter = nof_iterations > 0 ? (int)nof_iterations : 1;
+  return SRSRAN_SUCCESS;
+}
+
+// One more half-iteration and a decision (turbodecoder.c:551-558): the decoder state after n
+// half-iterations is a function of the input alone, so the n + 1 half-iterations run from the input.
+void srsran_tdec_iteration_8bit(srsran_tdec_t* h, int8_t* input, uint8_t* output)
+{
+  if (!h || !h->gpu || h->current_cbidx < 0) {
+    fprintf(stderr, "[srsran_tdec] Error CB index not set (call srsran_tdec_new_cb() first\n");
+    return;
+  }
+  const int n = h->n_iter + 1;
+  if (srsran_tdec_run_all_8bit(h, input, output, (uint32_t)n, h->current_long_cb) == SRSRAN_SUCCESS) {
+    h->n_iter = n;
+  }
 }
 
 }  // extern "C"

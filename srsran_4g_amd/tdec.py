@@ -82,6 +82,8 @@ def load_library():
         "srsran_tdec_run_all_batch": ([P, _i16p, u32, _u8p, u32, u32, u32], ctypes.c_int),
         "srsran_tdec_gpu_run_batch": ([u32, ctypes.c_void_p, u32, ctypes.c_int, ctypes.c_void_p, u32, u32,
                                        ctypes.c_void_p], ctypes.c_int),
+        "srsran_tdec_gpu_run_batch_8bit": ([u32, ctypes.c_void_p, u32, ctypes.c_int, ctypes.c_void_p, u32, u32,
+                                            ctypes.c_void_p], ctypes.c_int),
         "srsran_tdec_gpu_run_multi": ([u32, ctypes.POINTER(u32), ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(u32),
                                        ctypes.c_int, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(u32), u32,
                                        ctypes.c_void_p], ctypes.c_int),
@@ -274,6 +276,28 @@ class TurboDecoder:
             raise RuntimeError(f"srsran_tdec_run_all failed ({rc})")
         return out
 
+    def run_all_8bit(self, llr, nof_iterations, K):
+        """srsran_tdec_run_all_8bit: int8 LLRs."""
+        llr = np.ascontiguousarray(llr, dtype=np.int8)
+        out = np.zeros(K // 8, dtype=np.uint8)
+        rc = self.lib.srsran_tdec_run_all_8bit(ctypes.byref(self.h), llr.ctypes.data_as(ctypes.POINTER(ctypes.c_int8)),
+                                               out.ctypes.data_as(_u8p), nof_iterations, K)
+        if rc != SRSRAN_SUCCESS:
+            raise RuntimeError(f"srsran_tdec_run_all_8bit failed ({rc})")
+        return out
+
+    def iteration_8bit(self, llr):
+        """One more half-iteration + hard decision (srsran_tdec_iteration_8bit)."""
+        llr = np.ascontiguousarray(llr, dtype=np.int8)
+        K = self.h.current_long_cb
+        out = np.zeros(K // 8, dtype=np.uint8)
+        n0 = self.h.n_iter
+        self.lib.srsran_tdec_iteration_8bit(ctypes.byref(self.h), llr.ctypes.data_as(ctypes.POINTER(ctypes.c_int8)),
+                                            out.ctypes.data_as(_u8p))
+        if self.h.n_iter != n0 + 1:
+            raise RuntimeError("srsran_tdec_iteration_8bit failed")
+        return out
+
     def run_all_batch(self, llr2d, nof_iterations, K):
         llr2d = np.ascontiguousarray(llr2d, dtype=np.int16)
         n = llr2d.shape[0]
@@ -291,6 +315,14 @@ def gpu_run_batch(K, d_in, in_stride, layout_sb, d_out, nof_cb, nof_iterations, 
                                                   nof_iterations, stream)
     if rc != SRSRAN_SUCCESS:
         raise RuntimeError(f"srsran_tdec_gpu_run_batch failed ({rc})")
+
+
+def gpu_run_batch_8bit(K, d_in, in_stride, layout_sb, d_out, nof_cb, nof_iterations, stream=None):
+    """Device-resident batch decode of int8 code blocks (srsran_tdec_gpu_run_batch_8bit)."""
+    rc = load_library().srsran_tdec_gpu_run_batch_8bit(K, d_in, in_stride, int(bool(layout_sb)), d_out, nof_cb,
+                                                       nof_iterations, stream)
+    if rc != SRSRAN_SUCCESS:
+        raise RuntimeError(f"srsran_tdec_gpu_run_batch_8bit failed ({rc})")
 
 
 def gpu_run_multi(Ks, d_ins, strides, layout_sb, d_outs, ncbs, nof_iterations, stream=None):

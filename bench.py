@@ -237,6 +237,29 @@ def cpu_worker(args):
     print(json.dumps({"bits": bits, "blocks": n_cb, "dt": time.perf_counter() - t0}), flush=True)
 
 
+def bench_8bit(torch, device, n, K=6144, iters=8, reps=3):
+    """The 8-bit LLR decoder (srsran_tdec_gpu_run_batch_8bit, the reference's AVX2 8-bit window decoder
+    restated) on the C1 shape: n x K = 6144 int8 code blocks (SB layout, 32 sub-blocks), 8 half-its.
+    Random LLRs: the decoder runs every half-iteration whatever the values (no early stop)."""
+    from srsran_4g_amd import tdec
+    L = 3 * (K + 32) + 12
+    g = torch.Generator(device=device).manual_seed(8)
+    x = torch.randint(-100, 100, (n, L), dtype=torch.int8, device=device, generator=g)
+    out = torch.zeros((n, K // 8), dtype=torch.uint8, device=device)
+    st = torch.cuda.current_stream()
+    tdec.gpu_run_batch_8bit(K, x.data_ptr(), L, True, out.data_ptr(), n, iters, st.cuda_stream)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(reps):
+        tdec.gpu_run_batch_8bit(K, x.data_ptr(), L, True, out.data_ptr(), n, iters, st.cuda_stream)
+    e1.record(st)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    return {"workload": f"K={K} x {n}, {iters} half-its, int8 LLRs (srsran_tdec_gpu_run_batch_8bit)",
+            "kernel": tdec.last_kernel(), "ms_per_launch": round(ms, 4),
+            "mbps": round(n * K / (ms * 1e-3) / 1e6, 1)}
+
+
 def cpu_baseline(Ks, data, iters, budget_s, workload):
     """Reference decoder (oracle/_ref, compiled from /root/reference) on the host cores of this job.
 
@@ -1528,6 +1551,7 @@ def main():
         if k:
             ms = np.mean([e0.elapsed_time(e1) for _, e0, e1 in k])
             result["k6144_mbps"] = round(args.batch * 6144 / (ms * 1e-3) / 1e6, 1)
+        result["tdec_8bit"] = bench_8bit(torch, device, args.batch)
 
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         result["cpu_baseline"] = cpu_baseline(Ks, data, args.iters, args.cpu_seconds, args.workload)

@@ -24,6 +24,7 @@
 #include "devkey.h"
 #include "sch_kernel.h"
 #include "tdec_kernel.h"
+#include "tdec8bit_kernel.h"
 #include "enc_kernel.h"
 #include "uci_kernel.h"
 #include "pdsch_internal.h"
@@ -87,11 +88,11 @@ uint32_t rx_subblocks(uint32_t K, bool tdec_layout)
   return tdec_layout ? srsran_tdec_autoimp_get_subblocks(K) : 0;
 }
 
-bool inv_table(uint32_t cb_idx, uint32_t rv, bool tdec_layout, InvTable* out)
+// nsb: sub-blocks of the decoder layout (0 natural; 8 / 16 / 32 as rm_turbo.c's deinterleaver_sb)
+bool inv_table_nsb(uint32_t cb_idx, uint32_t rv, uint32_t nsb, InvTable* out)
 {
   const uint32_t              K   = (uint32_t)srsran_cbsegm_cbsize(cb_idx);
-  const uint32_t              nsb = rx_subblocks(K, tdec_layout);
-  const uint64_t              key = ((uint64_t)cur_dev() << 32) | ((cb_idx * 4 + rv) * 2 + (nsb ? 1 : 0));
+  const uint64_t              key = ((uint64_t)cur_dev() << 32) | ((cb_idx * 4 + rv) * 64 + nsb);
   std::lock_guard<std::mutex> lk(g_mu);
   auto                        it = g_inv.find(key);
   if (it != g_inv.end()) {
@@ -139,6 +140,11 @@ bool inv_table(uint32_t cb_idx, uint32_t rv, bool tdec_layout, InvTable* out)
   g_inv[key] = t;
   *out       = t;
   return true;
+}
+
+bool inv_table(uint32_t cb_idx, uint32_t rv, bool tdec_layout, InvTable* out)
+{
+  return inv_table_nsb(cb_idx, rv, rx_subblocks((uint32_t)srsran_cbsegm_cbsize(cb_idx), tdec_layout), out);
 }
 
 // ---------------- soft buffer device arena ----------------
@@ -791,15 +797,42 @@ int srsran_rm_turbo_rx_lut(int16_t* input, int16_t* output, uint32_t in_len, uin
   return srsran_rm_turbo_rx_lut_(input, output, in_len, cb_idx, rv_idx, true);
 }
 
+// rm_turbo.c:447-483 (the SSE 8-bit path of an AVX2 build, :586-687): output[deinter[i % (3K + 12)]] += input[i]
+// with int8 wrap-around, on the sub-block layout of the 8-bit decoder that takes K
+// (srsran_tdec_autoimp_get_subblocks_8bit: 32 / 16 / 8 sub-blocks, natural below K = 408)
 int srsran_rm_turbo_rx_lut_8bit(int8_t* input, int8_t* output, uint32_t in_len, uint32_t cb_idx, uint32_t rv_idx)
 {
-  (void)input;
-  (void)output;
-  (void)in_len;
-  (void)cb_idx;
-  (void)rv_idx;
-  fprintf(stderr, "[srsran_rm_turbo] 8-bit LLR path not provided\n");
-  return SRSRAN_ERROR;
+  if (rv_idx >= 4 || cb_idx >= SRSRAN_NOF_TC_CB_SIZES || !input || !output) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  const uint32_t K = (uint32_t)srsran_cbsegm_cbsize(cb_idx);
+  InvTable       t;
+  if (!inv_table_nsb(cb_idx, rv_idx, srsran_tdec_autoimp_get_subblocks_8bit(K), &t)) {
+    fprintf(stderr, "[srsran_rm_turbo] no HIP device available\n");
+    return SRSRAN_ERROR;
+  }
+  std::lock_guard<std::mutex> lk(g_rm_mu);
+  RmCtx&                      c = g_rm[cur_dev()];
+  if (!c.stream) {
+    if (hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc((void**)&c.d_out, (size_t)SOFTBUFFER_SIZE * sizeof(int16_t)) != hipSuccess ||
+        hipMalloc((void**)&c.d_slot, sizeof(RmSlot)) != hipSuccess || hipMalloc((void**)&c.d_zero, 8) != hipSuccess ||
+        hipMemset(c.d_zero, 0, 8) != hipSuccess) {
+      return SRSRAN_ERROR;
+    }
+  }
+  if (!grow_dev((void**)&c.d_in, &c.in_cap, std::max<size_t>(in_len, 1))) {
+    return SRSRAN_ERROR;
+  }
+  int8_t* d_in  = (int8_t*)c.d_in;
+  int8_t* d_out = (int8_t*)c.d_out;
+  hipMemcpyAsync(d_in, input, in_len, hipMemcpyHostToDevice, c.stream);
+  hipMemcpyAsync(d_out, output, t.len, hipMemcpyHostToDevice, c.stream);
+  if (srsran_amd::rm8_rx_launch(d_in, d_out, t.d, in_len, t.len, t.N, c.stream) != hipSuccess) {
+    return SRSRAN_ERROR;
+  }
+  hipMemcpyAsync(output, d_out, t.len, hipMemcpyDeviceToHost, c.stream);
+  return hipStreamSynchronize(c.stream) == hipSuccess ? SRSRAN_SUCCESS : SRSRAN_ERROR;
 }
 
 // ---------------- softbuffer.c:36-178 ----------------

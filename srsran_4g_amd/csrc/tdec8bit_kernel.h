@@ -27,5 +27,10 @@ hipError_t tdec8bit_launch(int nsb, const Tdec8Args& a, hipStream_t stream);
 hipError_t tdec8bit_widen(const int8_t* in, uint32_t in_stride, short* out, uint32_t len, uint32_t ncb,
                           hipStream_t stream);
 
+// 8-bit rate de-matching (srsran_rm_turbo_rx_lut_8bit): sb[p] += sum of e[k], k = inv[p] + j N < E, int8
+// wrap-around; positions with inv[p] = 0xFFFF (layout padding) untouched
+hipError_t rm8_rx_launch(const int8_t* e, int8_t* sb, const uint16_t* inv, uint32_t E, uint32_t len, uint32_t N,
+                         hipStream_t stream);
+
 }  // namespace srsran_amd
 #endif

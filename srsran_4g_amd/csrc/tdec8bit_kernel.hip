@@ -372,7 +372,26 @@ __global__ void tdec8bit_widen_kernel(const int8_t* in, uint32_t in_stride, shor
   }
 }
 
+__global__ void rm8_rx_kernel(const int8_t* e, int8_t* sb, const uint16_t* inv, uint32_t E, uint32_t len, uint32_t N)
+{
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < len && inv[p] != 0xFFFFu) {
+    int acc = sb[p];
+    for (uint32_t k = inv[p]; k < E; k += N) {
+      acc += e[k];
+    }
+    sb[p] = (int8_t)acc;  // output[l] += x on int8 (rm_turbo.c:576-579)
+  }
+}
+
 }  // namespace
+
+hipError_t rm8_rx_launch(const int8_t* e, int8_t* sb, const uint16_t* inv, uint32_t E, uint32_t len, uint32_t N,
+                         hipStream_t stream)
+{
+  hipLaunchKernelGGL(rm8_rx_kernel, dim3((len + 255) / 256), dim3(256), 0, stream, e, sb, inv, E, len, N);
+  return hipGetLastError();
+}
 
 hipError_t tdec8bit_widen(const int8_t* in, uint32_t in_stride, short* out, uint32_t len, uint32_t ncb,
                           hipStream_t stream)

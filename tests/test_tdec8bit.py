@@ -175,3 +175,35 @@ def test_gpu_run_batch_8bit(ref, K, n):
         assert np.array_equal(got[i], ref.tdec8_run(K, llr[i, :L], True, 8)), i
     if nsb >= 16:
         assert tdec.last_kernel() == f"tdec8bit_kernel<{nsb}>"
+
+
+@pytest.mark.gpu
+def test_rm_turbo_rx_lut_8bit_matches_reference(ref):
+    """srsran_rm_turbo_rx_lut_8bit (rm_turbo.c:447-483, SSE 8-bit path): accumulate with int8 wrap-around on
+    the 8-bit decoder's sub-block layout (32 / 16 / 8 sub-blocks, natural below K = 408), every rv, E below
+    and above 3K + 12 (wrapped reads), onto a non-zero soft buffer."""
+    import ctypes
+    from srsran_4g_amd import tdec
+    i8p = ctypes.POINTER(ctypes.c_int8)
+    mine = tdec.load_library().srsran_rm_turbo_rx_lut_8bit
+    theirs = ref.lib.srsran_rm_turbo_rx_lut_8bit
+    for f in (mine, theirs):
+        f.argtypes = [i8p, i8p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
+        f.restype = ctypes.c_int
+    ref.lib.srsran_rm_turbo_gentables()
+    rng = np.random.default_rng(84)
+    bad = []
+    for K in (40, 400, 512, 800, 1024, 2048, 2112, 6144):
+        idx = CB_SIZES.index(K)
+        nsb = O.tdec8_subblocks(K)
+        n = 3 * (K + 32) + 12 if nsb else 3 * K + 12
+        for rv in range(4):
+            for E in (3 * K // 2 + 7, 5 * (3 * K + 12) // 2):
+                e = rng.integers(-128, 128, E).astype(np.int8)
+                base = rng.integers(-128, 128, n).astype(np.int8)
+                a, b = base.copy(), base.copy()
+                assert mine(e.ctypes.data_as(i8p), a.ctypes.data_as(i8p), E, idx, rv) == 0
+                assert theirs(e.ctypes.data_as(i8p), b.ctypes.data_as(i8p), E, idx, rv) == 0
+                if not np.array_equal(a, b):
+                    bad.append((K, rv, E, int(np.count_nonzero(a != b))))
+    assert not bad, bad

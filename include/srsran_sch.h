@@ -15,7 +15,8 @@
  *     memory (HBM).  cb_crc[] / tb_crc stay host-readable mirrors, refreshed by every synchronous call.
  *   - srsran_sch_t keeps the fields callers touch (max_iterations, avg_iterations, llr_is_8bit,
  *     decoder); the CPU-only scratch buffers are replaced by an opaque `gpu` pointer.
- *   - the 8-bit LLR path is not provided (llr_is_8bit must stay false).
+ *   - the 8-bit LLR transport-channel path (llr_is_8bit) is not provided and must stay false; its
+ *     building blocks are: srsran_rm_turbo_rx_lut_8bit here and srsran_tdec_run_all_8bit (srsran_tdec.h).
  *   - srsran_dlsch_gpu_decode_batch() is an added, asynchronous entry point over device buffers.
  */
 #ifndef SRSRAN_AMD_SCH_H

@@ -156,7 +156,7 @@ def parse():
     p.add_argument("--ldpc-snr", type=float, default=1.5, help="ldpc: BPSK Es/N0 (dB) of the synthetic codewords")
     p.add_argument("--nr-tbs", type=int, default=64, help="nrsch: transport blocks per step")
     p.add_argument("--nr-snr", type=float, default=12.0, help="nrsch: Es/N0 (dB) of the bits as +-1 before int8 LLRs")
-    p.add_argument("--pdsch-steps", type=int, default=5,
+    p.add_argument("--pdsch-steps", type=int, default=20,
                    help="all188: timed steps of the C3 PDSCH chain reported in the same line (0 = skip)")
     p.add_argument("--pdsch-cpu-seconds", type=float, default=4.0, help="all188: CPU baseline budget of the PDSCH part")
     p.add_argument("--pdsch-low-snr", type=float, default=17.0,
@@ -1562,7 +1562,7 @@ def main():
         # the PDSCH half of the metric (BASELINE configs[2], C3): the whole UE DL chain, same line
         del data
         torch.cuda.empty_cache()
-        pd = run_pdsch(args, torch, dist, world, rank, device, steps=args.pdsch_steps, warmup=2,
+        pd = run_pdsch(args, torch, dist, world, rank, device, steps=args.pdsch_steps, warmup=3,
                        cpu_seconds=args.pdsch_cpu_seconds if args.cpu_seconds > 0 else 0, emit=False)
         result["pdsch_subframes_per_s"] = pd["config"]["subframes_per_s"]
         result["pdsch"] = {

@@ -13,7 +13,7 @@
 //
 // Mapping: ONE LANE PER SUB-BLOCK, the 8 states of the lane's sub-block in 8 registers (int8 values held
 // in int32).  A workgroup is one wave: 64 / NSB code blocks.  The block's input streams, a-priori and
-// extrinsic arrays live in LDS (7 x (K + 4) bytes); the beta metrics of a MAP pass go to a global scratch
+// extrinsic arrays live in LDS (6 x (K + 4) bytes; ext2 overwrites app2 in place); the beta metrics of a MAP pass go to a global scratch
 // ([block][position][lane] x 8 bytes, one 8-byte store a lane a position, coalesced over the block's
 // lanes) and are read back by the alpha pass of the same lane.  All half-iterations run in one launch.
 // This is the off-by-default path of srsUE (srsue/src/main.cc:404-406); it is written for parity, not
@@ -262,14 +262,16 @@ __global__ __launch_bounds__(64) void tdec8bit_kernel(Tdec8Args a)
   const uint32_t cb   = blockIdx.x * CPW + cb_l;
   const bool     live = cb < a.ncb;
 
-  int8_t* base = lds + (size_t)cb_l * 7 * AL;
+  int8_t* base = lds + (size_t)cb_l * 6 * AL;
   int8_t* SY   = base;           // systematic
   int8_t* P0   = base + AL;      // parity 0
   int8_t* P1   = base + 2 * AL;  // parity 1
   int8_t* A1   = base + 3 * AL;  // app1
   int8_t* A2   = base + 4 * AL;  // app2
   int8_t* E1   = base + 5 * AL;  // ext1
-  int8_t* E2   = base + 6 * AL;  // ext2
+  // ext2 overwrites app2 in place: DEC 2 reads app2 at a position before it writes ext2 there, each lane
+  // only its own sub-block's positions, and app2's tail (read by the tail trellis) is never written
+  int8_t* E2   = A2;
 
   // ---- input streams (turbodecoder_iter.h:61-96 / win.h:880-923) ----
   if (live) {
@@ -402,7 +404,7 @@ hipError_t tdec8bit_widen(const int8_t* in, uint32_t in_stride, short* out, uint
   return hipGetLastError();
 }
 
-size_t tdec8bit_lds_bytes(int nsb, uint32_t K) { return (size_t)(64 / nsb) * 7 * ((K + 4 + 15) & ~15u); }
+size_t tdec8bit_lds_bytes(int nsb, uint32_t K) { return (size_t)(64 / nsb) * 6 * ((K + 4 + 15) & ~15u); }
 size_t tdec8bit_beta_bytes(int nsb, uint32_t K, uint32_t ncb) { return (size_t)ncb * (K / nsb + 1) * nsb * 8; }
 
 hipError_t tdec8bit_launch(int nsb, const Tdec8Args& a, hipStream_t stream)

@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 3: the 8-bit turbo decoder on the GPU -- parity tests, then its C1-shape timing and a rocprof summary
 set -o pipefail
-OUT=gpurun_out/r03_8bit
+OUT=gpurun_out/${R8OUT:-r03_8bit}
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 400 python -u -m pytest tests/test_tdec8bit.py -m gpu -v -x --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1

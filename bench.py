@@ -133,7 +133,9 @@ def algo_bytes(K):
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=None,
+                   help="GPUs of this node, one rank each (default: WORLD_SIZE under a launcher, else 1); without a "
+                        "launcher N > 1 starts the N ranks itself")
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--workload", choices=["all188", "k6144", "dlsch", "ulsch", "pusch", "dlenc", "pdsch", "dlloop", "ldpc",
@@ -171,6 +173,8 @@ def parse():
     p.add_argument("--w8-fused-max-k", type=int, default=-1,
                    help="srsran_tdec_gpu_set_w8_fused_max_k (-1: the library default)")
     p.add_argument("--cpu-worker", type=int, default=None, help=argparse.SUPPRESS)
+    p.add_argument("--dry-run", action="store_true",
+                   help="launch path only (no GPU): ranks, devices and shards on a gloo group, one line")
     return p.parse_args()
 
 
@@ -1341,16 +1345,79 @@ def run_nrsch(args, torch, dist, world, rank, device):
         emit_line(result, args.workload)
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_local_ranks(n):
+    """--gpus N > 1 with no launcher around us: start N rank processes of this script as CHILDREN (one per
+    GPU, RANK = LOCAL_RANK = r, WORLD_SIZE = N, rendezvous on 127.0.0.1), before this process touches the
+    GPU -- nothing is exec'd.  Rank 0 prints the line; returns the worst exit status (a failed rank stops
+    the others)."""
+    import subprocess
+    port = str(free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                for q in live:  # a rank failed: the others would wait at the next barrier forever
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def dry_run(args):
+    """--dry-run: the launch path without a GPU (tests/test_dist_cpu.py): every rank joins a gloo group,
+    maps LOCAL_RANK to its device index and takes its shard; rank 0 prints one line with them all."""
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    me = dict(rank=rank, local_rank=local, device=f"cuda:{local}", **shard(rank))
+    ranks = [me]
+    if world > 1:
+        dist.init_process_group(backend="gloo", init_method="env://")
+        ranks = [None] * world
+        dist.all_gather_object(ranks, me)
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "n_gpus": world, "dry_run": True, "ranks": ranks}), flush=True)
+    return 0
+
+
 def main():
     args = parse()
     if args.cpu_worker is not None:
         return cpu_worker(args)
+    world = int(os.environ.get("WORLD_SIZE", "0") or 0)
+    if world == 0 and (args.gpus or 1) > 1:
+        return launch_local_ranks(args.gpus)
+    if world and args.gpus is not None and world != args.gpus:
+        print(f"bench: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+        return 2
+    world = world or 1
+    if args.dry_run:
+        return dry_run(args)
     import torch
     import torch.distributed as dist
 
     from srsran_4g_amd import tdec
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
@@ -1621,4 +1688,5 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    rc = main()
+    sys.exit(rc if isinstance(rc, int) else 0)  # the workload runners return their result dict

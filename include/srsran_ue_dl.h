@@ -307,6 +307,13 @@ int srsran_pdsch_gpu_decode_batch(srsran_pdsch_t*              q,
                                   float*                       d_avg_noi,
                                   void*                        stream);
 
+/* added (tests / diagnostics): the descrambled, CSI-corrected int16 LLRs (the e bits srsran_dlsch_decode2
+ * receives, pdsch.c:693-733) of subframe `sf` (index into the last srsran_pdsch_gpu_decode_batch /
+ * srsran_ue_dl_gpu_decode_batch on q) and transport block `tb`: a device pointer, valid until the next batch on
+ * q and complete once that batch's stream has reached it, and their number.  SRSRAN_ERROR if the TB was not in
+ * the batch. */
+int srsran_pdsch_gpu_last_llr(srsran_pdsch_t* q, uint32_t sf, uint32_t tb, const int16_t** d_llr, uint32_t* nof_llr);
+
 /* ---------------- UE DL (ue/ue_dl.h:77-207, ue_dl.c) ----------------
  * decode_fft_estimate: OFDM, CRS estimation, PCFICH (sets sf->cfi) and the PDCCH LLRs, all on the
  * GPU, for cells of 1 or 2 ports with normal PHICH duration (other cells: the CFI is the caller's

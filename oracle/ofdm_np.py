@@ -7,9 +7,13 @@ stage is checked against numpy's FFT (double precision) and by TX -> RX round tr
     (cp=1): 6 symbols a slot, cp0 = cp = ceil(512 N / 2048) (SRSRAN_CP_LEN_EXT)
   - receiver: forward DFT, unnormalised, grid = [X[N-nre/2 ..], X[1 .. nre/2]] (ofdm.c:497-498)
   - transmitter: the inverse mapping with an IFFT scaled by 1/N, so rx(tx(grid)) == grid
-  - CFO: z[n] = x[n] exp(j 2 pi f n), n from the subframe start (cfo.c:96-107)
+  - CFO: z[n] = x[n] exp(j 2 pi f n), n from the subframe start (cfo.c:96-107); ref_apply_cfo runs the
+    reference's own srsran_vec_apply_cfo (vector_simd.c:1723-1774, compiled into _ref/libsrsref.so), whose
+    float phasor recurrence drifts from the exact exponential by up to ~1e-4 over a 20 MHz subframe
 """
+import ctypes
 import math
+import os
 
 import numpy as np
 
@@ -68,3 +72,33 @@ def ofdm_tx(grid, N, nre, ext=0):
 def cfo(x, f):
     n = np.arange(len(x))
     return np.asarray(x, np.complex128) * np.exp(2j * np.pi * f * n)
+
+
+_REF = None
+
+
+def ref_available():
+    return os.path.exists(os.path.join(os.path.dirname(os.path.abspath(__file__)), "_ref", "libsrsref.so"))
+
+
+def ref_apply_cfo(x, f):
+    """srsran_cfo_correct(h, x, z, f) of the reference (SRSRAN_CFO_USE_EXP_TABLE = 0, cfo.c:33, 105):
+    srsran_vec_apply_cfo over the whole buffer, 32-byte aligned as srsran_vec_malloc buffers are"""
+    global _REF
+    if _REF is None:
+        L = ctypes.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "_ref", "libsrsref.so"),
+                        mode=os.RTLD_LAZY)
+        L.srsran_vec_apply_cfo.argtypes = [ctypes.c_void_p, ctypes.c_float, ctypes.c_void_p, ctypes.c_int]
+        L.srsran_vec_apply_cfo.restype = None
+        _REF = L
+
+    def aligned(n):
+        b = np.zeros(n + 8, np.complex64)
+        o = (-(b.ctypes.data // 8)) % 4
+        return b[o:o + n]
+
+    n = len(x)
+    xi, z = aligned(n), aligned(n)
+    xi[:] = x
+    _REF.srsran_vec_apply_cfo(xi.ctypes.data, ctypes.c_float(f), z.ctypes.data, n)
+    return z.copy()

@@ -41,8 +41,8 @@ def fft_estimate(ora, samples, nof_prb, cell_id, nports, tti, cfo=0.0, N=None, c
     nre = 12 * nof_prb
     grids = []
     for x in samples:
-        if cfo:
-            x = ofdm_np.cfo(x, cfo)
+        if cfo:  # srsran_cfo_correct: the reference's own phasor recurrence where _ref is built
+            x = ofdm_np.ref_apply_cfo(x, cfo) if ofdm_np.ref_available() else ofdm_np.cfo(x, cfo)
         grids.append(ofdm_np.ofdm_rx(x, N, nre, ext=cp).astype(np.complex64))
     grids = np.stack(grids)
     ce, st = ora.chest_dl(grids, nof_prb, cell_id, nports, tti % 10, N, cp=cp)

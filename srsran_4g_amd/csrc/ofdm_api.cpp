@@ -45,12 +45,66 @@ const float2* twiddles(uint32_t N)
   return d;
 }
 
+// srsran_vec_apply_cfo's phasor table for one (frequency, length), rebuilt on the launch stream only when the
+// frequency changes (the reference recomputes it every call: SRSRAN_CFO_USE_EXP_TABLE is 0, cfo.c:33)
+struct CfoTab {
+  float2*    d     = nullptr;
+  size_t     cap   = 0;
+  uint32_t   bits  = 0;  // the float's bit pattern
+  uint32_t   len   = 0;
+  bool       valid = false;
+  hipEvent_t used  = nullptr;  // the last launch that read d
+};
+
+bool grow(void** p, size_t* cap, size_t need);
+
+const float2* cfo_table(CfoTab& t, float f, uint32_t len, hipStream_t s)
+{
+  uint32_t bits;
+  memcpy(&bits, &f, 4);
+  if (t.valid && t.bits == bits && t.len == len) {
+    return t.d;
+  }
+  if (!t.used && hipEventCreateWithFlags(&t.used, hipEventDisableTiming) != hipSuccess) {
+    return nullptr;
+  }
+  if (t.valid) {
+    hipStreamWaitEvent(s, t.used, 0);  // a launch on another stream may still read the old table
+  }
+  if (len * sizeof(float2) > t.cap) {
+    hipEventSynchronize(t.used);
+    if (!grow((void**)&t.d, &t.cap, len * sizeof(float2))) {
+      return nullptr;
+    }
+  }
+  float c, sn;
+  cfo_phasor(f, &c, &sn);
+  if (cfo_table_launch(c, sn, t.d, len, s) != hipSuccess) {
+    t.valid = false;
+    return nullptr;
+  }
+  t.bits  = bits;
+  t.len   = len;
+  t.valid = true;
+  return t.d;
+}
+
+void cfo_table_free(CfoTab& t)
+{
+  hipFree(t.d);
+  if (t.used) {
+    hipEventDestroy(t.used);
+  }
+  t = CfoTab();
+}
+
 struct OfdmGpu {
   hipStream_t stream = nullptr;
   float2*     d_in   = nullptr;
   float2*     d_out  = nullptr;
   size_t      in_cap = 0, out_cap = 0;
   OfdmArgs    proto{};
+  CfoTab      cfo;
 };
 
 uint32_t cp_len(uint32_t c, uint32_t N) { return (uint32_t)ceilf((float)c * (float)N / 2048.0f); }  // SRSRAN_CP_LEN
@@ -113,8 +167,20 @@ int run(srsran_ofdm_t* q, const float2* d_in, float2* d_out, uint32_t nrx, uint3
   a.in       = d_in;
   a.out      = d_out;
   a.nrx      = nrx;
-  a.cfo      = (double)cfo;
-  return ofdm_rx_launch(a, nsf, s) == hipSuccess ? SRSRAN_SUCCESS : SRSRAN_ERROR;
+  a.cfo_tab  = nullptr;
+  if (cfo != 0.0f) {  // a zero frequency multiplies every sample by exactly 1 in the reference
+    a.cfo_tab = cfo_table(g->cfo, cfo, a.sf_len, s);
+    if (!a.cfo_tab) {
+      return SRSRAN_ERROR;
+    }
+  }
+  if (ofdm_rx_launch(a, nsf, s) != hipSuccess) {
+    return SRSRAN_ERROR;
+  }
+  if (a.cfo_tab) {
+    hipEventRecord(g->cfo.used, s);
+  }
+  return SRSRAN_SUCCESS;
 }
 
 }  // namespace
@@ -178,6 +244,7 @@ void srsran_ofdm_rx_free(srsran_ofdm_t* q)
     }
     hipFree(g->d_in);
     hipFree(g->d_out);
+    cfo_table_free(g->cfo);
     delete g;
   }
   memset(q, 0, sizeof(*q));
@@ -232,6 +299,7 @@ struct CfoGpu {
   hipStream_t stream = nullptr;
   float2*     d      = nullptr;
   size_t      cap    = 0;
+  CfoTab      tab;
 };
 
 int srsran_cfo_init(srsran_cfo_t* h, uint32_t nsamples)
@@ -270,6 +338,7 @@ void srsran_cfo_free(srsran_cfo_t* h)
       hipStreamDestroy(g->stream);
     }
     hipFree(g->d);
+    cfo_table_free(g->tab);
     delete g;
   }
   memset(h, 0, sizeof(*h));
@@ -299,7 +368,9 @@ void srsran_cfo_correct(srsran_cfo_t* h, const cf_t* input, cf_t* output, float 
   CfoGpu*      g = (CfoGpu*)h->gpu;
   const size_t n = h->nsamples;
   hipMemcpyAsync(g->d, input, n * sizeof(cf_t), hipMemcpyHostToDevice, g->stream);
-  if (cfo_launch(g->d, g->d + n, (uint32_t)n, (double)freq, g->stream) == hipSuccess) {
+  const float2* tab = cfo_table(g->tab, freq, (uint32_t)n, g->stream);
+  if (tab && cfo_launch(g->d, g->d + n, tab, (uint32_t)n, g->stream) == hipSuccess) {
+    hipEventRecord(g->tab.used, g->stream);
     hipMemcpyAsync(output, g->d + n, n * sizeof(cf_t), hipMemcpyDeviceToHost, g->stream);
   }
   hipStreamSynchronize(g->stream);

@@ -20,7 +20,8 @@ struct OfdmArgs {
   uint32_t      sf_len;    // samples per subframe and antenna
   uint32_t      nrx;
   float         norm;      // 1 or 1/sqrt(N) (srsran_ofdm_cfg_t.normalize)
-  double        cfo;       // z[n] = x[n] exp(j 2 pi cfo n), n from the subframe start; 0 = off
+  const float2* cfo_tab;   // srsran_vec_apply_cfo's phasor of every sample of a subframe (cfo_table_launch,
+                           // sf_len entries), applied as z = x * tab[n], n from the subframe start; nullptr = off
   int           nstages;
   int           radix[OFDM_MAX_STAGES];
   uint32_t      ns_magic[OFDM_MAX_STAGES];  // ceil(2^32 / Ns) of every stage (j / Ns by __umulhi)
@@ -37,8 +38,14 @@ hipError_t ofdm_tx_launch(const OfdmArgs& a, uint32_t nsf, hipStream_t stream);
 int ofdm_plan(uint32_t N, int* radix);
 int ofdm_plan(uint32_t N, int* radix, uint32_t* ns_magic);
 
-// standalone CFO correction z[n] = x[n] exp(j 2 pi f n)
-hipError_t cfo_launch(const float2* in, float2* out, uint32_t n, double f, hipStream_t stream);
+// srsran_vec_apply_cfo (vector_simd.c:1723-1774, the AVX2 + FMA build srsUE runs) as a phasor table: tab[n] is
+// the phase the reference multiplies sample n by -- 8 lane phases 1, w, w^2 .. w^7 advanced by w^8 once per
+// 8 samples, then a scalar tail advanced by w -- every product rounded as the reference's FMA sequence.
+// (c, s) = sincosf(2 pi f) computed on the host by cfo_phasor (the reference's cexpf(I * TWOPI * cfo)).
+void       cfo_phasor(float f, float* c, float* s);
+hipError_t cfo_table_launch(float c, float s, float2* tab, uint32_t len, hipStream_t stream);
+// standalone srsran_cfo_correct: out[n] = in[n] * tab[n] with the reference's complex product
+hipError_t cfo_launch(const float2* in, float2* out, const float2* tab, uint32_t n, hipStream_t stream);
 
 }  // namespace srsran_amd
 #endif

@@ -28,6 +28,13 @@ __device__ __forceinline__ float2 cmul(float2 a, float2 b)
   return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 }
 __device__ __forceinline__ float2 mul_mi(float2 a) { return make_float2(a.y, -a.x); }  // * (-i)
+// srsran_simd_cf_prod of the AVX2 + FMA build (simd.h:898-901) and gcc's contraction of the scalar
+// complex products around it: re = fma(a.re, b.re, -(a.im b.im)), im = fma(a.re, b.im, a.im b.re), the inner
+// products rounded on their own
+__device__ __forceinline__ float2 ref_cprod(float2 a, float2 b)
+{
+  return make_float2(__fmaf_rn(a.x, b.x, -__fmul_rn(a.y, b.y)), __fmaf_rn(a.x, b.y, __fmul_rn(a.y, b.x)));
+}
 
 __device__ __forceinline__ void dft2(float2* v)
 {
@@ -120,13 +127,8 @@ __global__ __launch_bounds__(OFDM_THREADS) void ofdm_rx_kernel(OfdmArgs a)
   const float2*     src     = a.in + ((size_t)sf * a.nrx + rx) * a.sf_len + off;
   for (uint32_t n = threadIdx.x; n < N; n += OFDM_THREADS) {
     float2 x = src[n];
-    if (a.cfo != 0.0) {
-      // phase 2 pi f (off + n), reduced in double before the float sincos
-      double ph = a.cfo * (double)(off + n);
-      ph -= rint(ph);
-      float s, c;
-      sincosf((float)(6.283185307179586476925 * ph), &s, &c);
-      x = cmul(x, make_float2(c, s));
+    if (a.cfo_tab) {
+      x = ref_cprod(x, a.cfo_tab[off + n]);  // srsran_cfo_correct on the subframe buffer
     }
     buf[0][n] = x;
   }
@@ -265,26 +267,68 @@ hipError_t ofdm_rx_launch(const OfdmArgs& a, uint32_t nsf, hipStream_t stream)
   return hipGetLastError();
 }
 
-__global__ void cfo_kernel(const float2* __restrict__ in, float2* __restrict__ out, uint32_t n, double f)
+// One wave: lanes 0..7 carry the reference's 8 SIMD phases through the len / 8 blocks (a serial
+// recurrence: every block's phase is the previous one times w^8, rounded -- it cannot be re-associated
+// without changing the result), lane 0 then the scalar tail.  Run once per (f, len) and cached by the host.
+__global__ __launch_bounds__(64) void cfo_table_kernel(float c, float s, float2* __restrict__ tab, uint32_t len)
 {
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n) {
+  const uint32_t k = threadIdx.x;
+  if (k >= 8) {
     return;
   }
-  double ph = f * (double)k;
-  ph -= rint(ph);
-  float s, c;
-  sincosf((float)(6.283185307179586476925 * ph), &s, &c);
-  out[k] = cmul(in[k], make_float2(c, s));
+  const float2 w = make_float2(c, s);
+  float2       p = make_float2(1.0f, 0.0f);  // _phase[k] = _phase[k - 1] * osc, _phase[0] = 1
+  for (uint32_t j = 0; j < k; j++) {
+    p = ref_cprod(p, w);
+  }
+  float2 w8 = make_float2(1.0f, 0.0f);  // _phase[7] * osc, computed as the same chain
+  for (uint32_t j = 0; j < 8; j++) {
+    w8 = ref_cprod(w8, w);
+  }
+  const uint32_t nblk = len / 8;  // for (; i < len - 8 + 1; i += 8)
+  for (uint32_t m = 0; m < nblk; m++) {
+    tab[8 * m + k] = p;
+    p              = ref_cprod(p, w8);
+  }
+  if (k == 0) {  // phase = _phase[0] after the SIMD loop; the scalar tail advances by osc
+    for (uint32_t i = 8 * nblk; i < len; i++) {
+      tab[i] = p;
+      p      = ref_cprod(p, w);
+    }
+  }
 }
 
-hipError_t cfo_launch(const float2* in, float2* out, uint32_t n, double f, hipStream_t stream)
+void cfo_phasor(float f, float* c, float* s)
+{
+  const float twopi = 2.0f * (float)M_PI;  // TWOPI of vector_simd.c:1725
+  sincosf(twopi * f, s, c);                // cexpf(_Complex_I * TWOPI * cfo): the real part is 0
+}
+
+hipError_t cfo_table_launch(float c, float s, float2* tab, uint32_t len, hipStream_t stream)
+{
+  if (len == 0) {
+    return hipSuccess;
+  }
+  hipLaunchKernelGGL(cfo_table_kernel, dim3(1), dim3(64), 0, stream, c, s, tab, len);
+  return hipGetLastError();
+}
+
+__global__ void cfo_kernel(const float2* __restrict__ in, float2* __restrict__ out, const float2* __restrict__ tab,
+                           uint32_t n)
+{
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n) {
+    out[k] = ref_cprod(in[k], tab[k]);
+  }
+}
+
+hipError_t cfo_launch(const float2* in, float2* out, const float2* tab, uint32_t n, hipStream_t stream)
 {
   StageScope timing_scope(ST_OFDM, stream);
   if (n == 0) {
     return hipSuccess;
   }
-  hipLaunchKernelGGL(cfo_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, in, out, n, f);
+  hipLaunchKernelGGL(cfo_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, in, out, tab, n);
   return hipGetLastError();
 }
 

@@ -52,6 +52,11 @@ struct PdschGpu {
   float2*                      d_in      = nullptr;  // host-synchronous path: grids + estimates
   size_t                       in_cap    = 0;
   std::map<TableKey, Table>    tables;
+  struct LlrRef {
+    uint32_t       sf, tb, n;
+    const int16_t* d;
+  };
+  std::vector<LlrRef> last_llr;  // the last batch's LLR buffers (srsran_pdsch_gpu_last_llr)
 };
 
 bool grow_dev(void** p, size_t* cap, size_t need)
@@ -315,6 +320,13 @@ int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sf
   hipEventRecord(g->staged, g->copy);
   hipStreamWaitEvent(s, g->staged, 0);
   g->used = true;
+  // from here on d_stage belongs to this batch: g->read is recorded on every exit, so the next batch's
+  // upload waits for whatever of this one was enqueued, error paths included
+  struct ReadMark {
+    PdschGpu*   g;
+    hipStream_t s;
+    ~ReadMark() { hipEventRecord(g->read, s); }
+  } mark{g, s};
   hipMemsetAsync(d_max, 0, (size_t)nsf * 2 * sizeof(float), s);
   const PredArgs* dp = (const PredArgs*)g->d_stage;
   const LlrItem*  dl = (const LlrItem*)(g->d_stage + pa_bytes);
@@ -340,7 +352,6 @@ int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sf
     }
     i = j;
   }
-  hipEventRecord(g->read, s);
   return SRSRAN_SUCCESS;
 }
 
@@ -517,16 +528,19 @@ int srsran_pdsch_gpu_decode_batch(srsran_pdsch_t*              q,
     return SRSRAN_ERROR;
   }
   hipStream_t s = (hipStream_t)stream;
-  if (sfs[0].cfg && sfs[0].cfg->max_nof_iterations) {
-    srsran_sch_set_max_noi(&q->dl_sch, sfs[0].cfg->max_nof_iterations);
-  }
   std::vector<Cw>       cws;
   std::vector<int16_t*> llr;
   int                   ret = enqueue_llr(q, nof_sf, sfs, s, cws, llr);
   if (ret) {
     return ret;
   }
+  PdschGpu* g = (PdschGpu*)q->gpu;
+  g->last_llr.clear();
+  for (size_t i = 0; i < cws.size(); i++) {
+    g->last_llr.push_back({cws[i].sf, cws[i].tb, cws[i].nbits, llr[i]});
+  }
   std::vector<srsran_dlsch_gpu_tb_t> tbs(cws.size());
+  std::vector<uint32_t>              maxit(cws.size());  // each subframe's own limit (pdsch.c:723 per decode)
   for (size_t i = 0; i < cws.size(); i++) {
     const srsran_pdsch_gpu_sf_t& f = sfs[cws[i].sf];
     const srsran_ra_tb_t&        t = f.cfg->grant.tb[cws[i].tb];
@@ -542,11 +556,28 @@ int srsran_pdsch_gpu_decode_batch(srsran_pdsch_t*              q,
     e.d_data     = f.d_payload[cws[i].tb];
     e.softbuffer = f.cfg->softbuffers.rx[cws[i].tb];
     e.new_data   = f.new_data[cws[i].tb];
+    maxit[i]     = f.cfg->max_nof_iterations;
   }
-  ret = dlsch_gpu_decode_batch_early_copy(&q->dl_sch, (uint32_t)tbs.size(), tbs.data(), d_result, d_avg_noi, stream);
+  ret = dlsch_gpu_decode_batch_limits(&q->dl_sch, (uint32_t)tbs.size(), tbs.data(), maxit.data(), d_result, d_avg_noi,
+                                      stream);
   return ret == SRSRAN_SUCCESS ? (int)tbs.size() : ret;
 }
 
+
+int srsran_pdsch_gpu_last_llr(srsran_pdsch_t* q, uint32_t sf, uint32_t tb, const int16_t** d_llr, uint32_t* nof_llr)
+{
+  if (!q || !q->gpu || !d_llr || !nof_llr) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  for (const auto& r : ((PdschGpu*)q->gpu)->last_llr) {
+    if (r.sf == sf && r.tb == tb) {
+      *d_llr   = r.d;
+      *nof_llr = r.n;
+      return SRSRAN_SUCCESS;
+    }
+  }
+  return SRSRAN_ERROR;
+}
 
 // ---------------- transmitter (pdsch.c:1015-1120, eNB side) ----------------
 int srsran_pdsch_init_enb(srsran_pdsch_t* q, uint32_t max_prb)

@@ -22,6 +22,10 @@ std::vector<uint32_t> pdsch_re_table(const srsran_cell_t& cell, const srsran_pds
 // for callers whose stream has work queued in front of the decode
 int dlsch_gpu_decode_batch_early_copy(srsran_sch_t* q, uint32_t nof_tb, const srsran_dlsch_gpu_tb_t* tbs,
                                       int32_t* d_result, float* d_avg_noi, void* stream);
+// the same with a per-TB iteration limit (0: the object's current one): one batch per distinct limit, each TB's
+// result in its own slot; q is left at the last TB's limit, as after sequential decodes
+int dlsch_gpu_decode_batch_limits(srsran_sch_t* q, uint32_t nof_tb, const srsran_dlsch_gpu_tb_t* tbs,
+                                  const uint32_t* max_noi, int32_t* d_result, float* d_avg_noi, void* stream);
 
 }  // namespace srsran_amd
 #endif

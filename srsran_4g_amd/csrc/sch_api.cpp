@@ -350,8 +350,9 @@ int32_t check_tb(const srsran_dlsch_gpu_tb_t& tb, srsran_cbsegm_t* s)
 }
 
 // Enqueue the three-kernel DL-SCH decode of ntb transport blocks on `stream`.
+// out_idx (optional): TB i's result / average-iterations slot is d_result[out_idx[i]] (default i).
 int enqueue_batch(srsran_sch_t* q, uint32_t ntb, const srsran_dlsch_gpu_tb_t* tbs, int32_t* d_result, float* d_avg,
-                  hipStream_t stream, bool early_copy = false)
+                  hipStream_t stream, bool early_copy = false, const uint32_t* out_idx = nullptr)
 {
   srsran_amd::HostScope desc(srsran_amd::HP_SCH_DESC);
   SchCtx*           x = (SchCtx*)q->gpu;
@@ -432,8 +433,8 @@ int enqueue_batch(srsran_sch_t* q, uint32_t ntb, const srsran_dlsch_gpu_tb_t* tb
   for (uint32_t i = 0; i < ntb; i++) {
     SchTb& t = tbd[i];
     memset(&t, 0, sizeof(t));
-    t.result = d_result + i;
-    t.avg    = d_avg + i;
+    t.result = d_result + (out_idx ? out_idx[i] : i);
+    t.avg    = d_avg + (out_idx ? out_idx[i] : i);
     t.status = plan[i].status;
     const srsran_softbuffer_rx_t* sbh = tbs[i].softbuffer;
     if (sbh && sbh->gpu) {
@@ -1222,6 +1223,53 @@ int dlsch_gpu_decode_batch_early_copy(srsran_sch_t* q, uint32_t nof_tb, const sr
   }
   return enqueue_batch(q, nof_tb, tbs, d_result, d_avg_noi, (hipStream_t)stream, true);
 }
+
+int dlsch_gpu_decode_batch_limits(srsran_sch_t* q, uint32_t nof_tb, const srsran_dlsch_gpu_tb_t* tbs,
+                                  const uint32_t* max_noi, int32_t* d_result, float* d_avg_noi, void* stream)
+{
+  if (!q || !q->gpu || (nof_tb && (!tbs || !max_noi || !d_result || !d_avg_noi))) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  if (nof_tb == 0) {
+    return SRSRAN_SUCCESS;
+  }
+  if (q->llr_is_8bit) {
+    return SRSRAN_ERROR;
+  }
+  // distinct limits in first-appearance order; 0 keeps the limit in force, as pdsch.c:815-817 does
+  std::vector<uint32_t> lim(nof_tb);
+  std::vector<uint32_t> order;
+  for (uint32_t i = 0; i < nof_tb; i++) {
+    lim[i] = max_noi[i] ? max_noi[i] : (i ? lim[i - 1] : q->max_iterations);
+    if (std::find(order.begin(), order.end(), lim[i]) == order.end()) {
+      order.push_back(lim[i]);
+    }
+  }
+  if (order.size() == 1) {
+    srsran_sch_set_max_noi(q, order[0]);
+    return enqueue_batch(q, nof_tb, tbs, d_result, d_avg_noi, (hipStream_t)stream, true);
+  }
+  std::vector<srsran_dlsch_gpu_tb_t> sub;
+  std::vector<uint32_t>              idx;
+  for (uint32_t l : order) {
+    sub.clear();
+    idx.clear();
+    for (uint32_t i = 0; i < nof_tb; i++) {
+      if (lim[i] == l) {
+        sub.push_back(tbs[i]);
+        idx.push_back(i);
+      }
+    }
+    srsran_sch_set_max_noi(q, l);
+    const int r = enqueue_batch(q, (uint32_t)sub.size(), sub.data(), d_result, d_avg_noi, (hipStream_t)stream, true,
+                                idx.data());
+    if (r != SRSRAN_SUCCESS) {
+      return r;
+    }
+  }
+  srsran_sch_set_max_noi(q, lim[nof_tb - 1]);  // as after the last TB's sequential decode
+  return SRSRAN_SUCCESS;
+}
 }  // namespace srsran_amd
 
 extern "C" {
@@ -1901,7 +1949,7 @@ int ulsch_decode_batch_dev(srsran_sch_t* q, uint32_t n, UlschBatchUe* ues, const
   std::vector<int32_t>               tbix(n, -1);
   UciDesc*                           h_ud2 = (UciDesc*)(h + h_cqi);
   bool                               any_cqi = false;
-  uint32_t                           maxit   = 0;
+  std::vector<uint32_t>              tb_maxit;  // each TB's max_nof_iterations (pusch.c:450 sets it per UE)
   memcpy(h_ud2, h_ud, m * sizeof(UciDesc));
   for (uint32_t i : live) {
     UlschBatchUe&  u = ues[i];
@@ -1929,19 +1977,17 @@ int ulsch_decode_batch_dev(srsran_sch_t* q, uint32_t n, UlschBatchUe* ues, const
       t.new_data   = u.new_data ? 1 : 0;
       tbix[i]      = (int32_t)tbs.size();
       tbs.push_back(t);
-      maxit = std::max(maxit, u.cfg->max_nof_iterations);
+      tb_maxit.push_back(u.cfg->max_nof_iterations ? u.cfg->max_nof_iterations : 10);  // set unconditionally
     }
   }
   if (any_cqi && (hipMemcpyAsync(d, h_ud2, m * sizeof(UciDesc), hipMemcpyHostToDevice, st) != hipSuccess ||
                   uci_cqi_launch((const UciDesc*)d, m, st) != hipSuccess)) {
     return SRSRAN_ERROR;
   }
-  if (!tbs.empty()) {
-    srsran_sch_set_max_noi(q, maxit);
-    if (srsran_amd::dlsch_gpu_decode_batch_early_copy(q, (uint32_t)tbs.size(), tbs.data(), (int32_t*)(d + o_res),
-                                                      (float*)(d + o_avg), st) != SRSRAN_SUCCESS) {
-      return SRSRAN_ERROR;
-    }
+  if (!tbs.empty() &&
+      srsran_amd::dlsch_gpu_decode_batch_limits(q, (uint32_t)tbs.size(), tbs.data(), tb_maxit.data(),
+                                                (int32_t*)(d + o_res), (float*)(d + o_avg), st) != SRSRAN_SUCCESS) {
+    return SRSRAN_ERROR;  // one decode batch per UE iteration limit (pusch.c:450 sets it per decode)
   }
   // results, UCI and payloads back in one sync
   if ((nl && hipMemcpyAsync(h + h_back, d + o_out, back_len, hipMemcpyDeviceToHost, st) != hipSuccess) ||

@@ -903,6 +903,36 @@ int srsran_tdec_gpu_debug_set_stamps(void* d_buf)
 #endif
 
 // ---- 8-bit LLR decoders (turbodecoder.c:455-483, 551-577) ----
+namespace {
+// grow-only scratch of the 8-bit batch entry point (the β of a MAP pass / the widened int16 input), one per
+// (device, stream): calls on one stream are ordered, so its scratch is reused without allocation in steady state
+struct Scratch8 {
+  void*  p   = nullptr;
+  size_t cap = 0;
+};
+std::mutex                                              g_s8_mu;
+std::map<std::pair<int, hipStream_t>, Scratch8>         g_s8;
+void* scratch8(hipStream_t s, size_t bytes)
+{
+  std::lock_guard<std::mutex> lk(g_s8_mu);
+  Scratch8&                   c = g_s8[{srsran_amd::cur_dev(), s}];
+  if (bytes > c.cap) {
+    if (c.p) {
+      hipStreamSynchronize(s);  // the previous call on this stream may still read it
+      hipFree(c.p);
+      c.p   = nullptr;
+      c.cap = 0;
+    }
+    const size_t cap = bytes + bytes / 4;
+    if (hipMalloc(&c.p, cap) != hipSuccess) {
+      return nullptr;
+    }
+    c.cap = cap;
+  }
+  return c.p;
+}
+}  // namespace
+
 // AUTO: K > 2048 on the AVX2 8-bit window decoder (32 sub-blocks), 800 < K <= 2048 on the SSE 8-bit
 // window decoder (16), smaller K on the 16-bit decoders after widening the input (convert_8_to_16);
 // a manually selected 16-bit decoder widens as well (tdec_iteration_8 with dec_type != AUTO).
@@ -941,26 +971,23 @@ int srsran_tdec_gpu_run_batch_8bit(uint32_t      long_cb,
     a.n_end     = n_end;
     a.out       = d_output;
     qpp_coeffs((uint32_t)idx, &a.f1, &a.f2);
-    void* beta = nullptr;
-    if (hipMallocAsync(&beta, tdec8bit_beta_bytes((int)nsb8, long_cb, nof_cb), s) != hipSuccess) {
+    void* beta = scratch8(s, tdec8bit_beta_bytes((int)nsb8, long_cb, nof_cb));
+    if (!beta) {
       return SRSRAN_ERROR;
     }
     a.beta           = (uint2*)beta;
     const hipError_t e = tdec8bit_launch((int)nsb8, a, s);
-    (void)hipFreeAsync(beta, s);
     tdec_set_last_kernel(nsb8 == 32 ? "tdec8bit_kernel<32>" : "tdec8bit_kernel<16>");
     return e == hipSuccess ? SRSRAN_SUCCESS : SRSRAN_ERROR;
   }
   // 16-bit decoder on the widened input
-  short* wide = nullptr;
-  if (hipMallocAsync((void**)&wide, (size_t)nof_cb * len * sizeof(short), s) != hipSuccess) {
+  short* wide = (short*)scratch8(s, (size_t)nof_cb * len * sizeof(short));
+  if (!wide) {
     return SRSRAN_ERROR;
   }
-  int ret = tdec8bit_widen(d_input, in_stride, wide, len, nof_cb, s) == hipSuccess
-                ? srsran_tdec_gpu_run_batch(long_cb, wide, len, sb ? 1 : 0, d_output, nof_cb, nof_iterations, stream)
-                : SRSRAN_ERROR;
-  (void)hipFreeAsync(wide, s);
-  return ret;
+  return tdec8bit_widen(d_input, in_stride, wide, len, nof_cb, s) == hipSuccess
+             ? srsran_tdec_gpu_run_batch(long_cb, wide, len, sb ? 1 : 0, d_output, nof_cb, nof_iterations, stream)
+             : SRSRAN_ERROR;
 }
 
 int srsran_tdec_run_all_8bit(srsran_tdec_t* h, int8_t* input, uint8_t* output, uint32_t nof_iterations, uint32_t long_cb)

@@ -161,6 +161,8 @@ def lib():
             "srsran_pdsch_decode": ([PD, ctypes.POINTER(srsran_dl_sf_cfg_t), ctypes.POINTER(srsran_pdsch_cfg_t), RES,
                                      P, ctypes.POINTER(srsran_pdsch_res_t)], ctypes.c_int),
             "srsran_pdsch_gpu_decode_batch": ([PD, u32, ctypes.POINTER(srsran_pdsch_gpu_sf_t), P, P, P], ctypes.c_int),
+            "srsran_pdsch_gpu_last_llr": ([PD, u32, u32, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(u32)],
+                                          ctypes.c_int),
             "srsran_ue_dl_init": ([UE, P, u32, u32], ctypes.c_int),
             "srsran_ue_dl_free": ([UE], None),
             "srsran_ue_dl_set_cell": ([UE, srsran_cell_t], ctypes.c_int),
@@ -511,6 +513,13 @@ class UeDl:
         arr = sfs if isinstance(sfs, ctypes.Array) else self.batch_entries(sfs)
         return lib().srsran_ue_dl_gpu_decode_batch(ctypes.byref(self.q), ctypes.byref(self.cfg), len(arr), arr,
                                                    d_samples, cfo, d_result, d_avg, stream)
+
+    def last_llr(self, sf, tb):
+        """srsran_pdsch_gpu_last_llr of the UE's PDSCH object after a batch: (device pointer, count)"""
+        d, n = ctypes.c_void_p(), u32()
+        if lib().srsran_pdsch_gpu_last_llr(ctypes.byref(self.q.pdsch), sf, tb, ctypes.byref(d), ctypes.byref(n)):
+            raise RuntimeError(f"no LLRs for subframe {sf} TB {tb} in the last batch")
+        return d.value, n.value
 
     def free(self):
         if self.q.gpu:

@@ -67,3 +67,40 @@ def test_bench_timed_region_gloo_world2(tmp_path):
     assert r[0]["elapsed"] >= 3 * 0.04                          # at least the slower rank's 3 steps
     assert r[0]["cell"] != r[1]["cell"]                         # disjoint carriers
     assert all(x["ok"] and x["n"] == 4 for x in r)              # warmup + 3 timed steps, all decoded
+
+
+def _run_bench(args, env_extra=None, timeout=180):
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, cwd=ROOT, env=env,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_bench_gpus_spawns_ranks(n):
+    """bench.py --gpus N with no launcher starts N rank processes itself (children, before any GPU call):
+    one JSON line from rank 0 with n_gpus N, LOCAL_RANK r -> device cuda:r, disjoint cells and seeds"""
+    p = _run_bench(["--gpus", str(n), "--dry-run"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1
+    d = lines[0]
+    assert d["n_gpus"] == n
+    assert [r["rank"] for r in d["ranks"]] == list(range(n))
+    assert [r["device"] for r in d["ranks"]] == [f"cuda:{r}" for r in range(n)]
+    assert len({r["cell_id"] for r in d["ranks"]}) == n and len({r["seed"] for r in d["ranks"]}) == n
+
+
+def test_bench_world_size_disagreeing_with_gpus_fails():
+    """under a launcher, WORLD_SIZE must equal --gpus when --gpus is given"""
+    p = _run_bench(["--gpus", "4", "--dry-run"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"}, timeout=60)
+    assert p.returncode != 0 and "WORLD_SIZE" in p.stderr
+
+
+def test_bench_single_rank_under_launcher_env():
+    """WORLD_SIZE=1 (a launcher with one process) and no --gpus: one rank, no spawn"""
+    p = _run_bench(["--dry-run"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"}, timeout=60)
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = json.loads(p.stdout.strip().splitlines()[-1])
+    assert d["n_gpus"] == 1 and d["ranks"][0]["device"] == "cuda:0"

@@ -219,25 +219,33 @@ def test_invalid_grants_refused(env):
     ch.free()
 
 
-def test_pusch_batch_matches_sync(env):
+@pytest.mark.parametrize("mixed", [False, True], ids=["same_iterations", "mixed_iterations"])
+def test_pusch_batch_matches_sync(env, mixed):
     """srsran_pusch_gpu_decode_batch over UEs of two cells (device grids): every UE's CRC, payload,
-    UCI, iterations and estimator outputs equal srsran_chest_ul_estimate_pusch + srsran_pusch_decode"""
+    UCI, iterations and estimator outputs equal srsran_chest_ul_estimate_pusch + srsran_pusch_decode.
+    mixed_iterations: each UE has its own max_nof_iterations (pusch.c:450 sets it per decode) at SNRs where
+    the turbo decoder needs several iterations, so a batch-wide limit would change iterations and payloads"""
     import torch
 
     from srsran_4g_amd import pusch as P
     from srsran_4g_amd import sch as S
     po = env
     picks = [CASES[1], CASES[2], CASES[5], CASES[3], CASES[0], CASES[6]]
+    maxits = [1, 4, 2, 8, 3, 5]
     cells, keep, ues, want = {}, [], [], []
     rng = np.random.default_rng(11)
     for k, case in enumerate(picks):
         name, cell_id, cprb, cp, Qm, L, n0, tbs, nack, ri, cqi, sh, tti, dcfg, snr = case
+        if mixed:
+            snr -= 12.0
         cell, d = _setup(cell_id, cprb, cp, dcfg)
         sf = P.srsran_ul_sf_cfg_t()
         sf.tti, sf.shortened = tti, sh
         def mk(sb, a=(cprb, Qm, L, n0, tbs, nack, ri, cqi, cp, sh)):
             c = TX.make_cfg(*a[:8], cp=a[8], shortened=a[9], softbuffer=sb)
             c.meas_epre_en = True
+            if mixed:
+                c.max_nof_iterations = maxits[k]
             return c
         sb1, sb2 = S.SoftbufferRx(nof_prb=100), S.SoftbufferRx(nof_prb=100)
         cfg_b = mk(sb2)
@@ -266,6 +274,8 @@ def test_pusch_batch_matches_sync(env):
         arr[i].cfg = ctypes.pointer(cfg_b)
         arr[i].d_sf_symbols = d_grid.data_ptr()
         res[i].data = data_b.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+    if mixed:  # the limits matter here: some UE ran more than one iteration in the sequential flow
+        assert max(w[0].avg_iterations_block for w in want if w[5]) > 1
     pu = P.Pusch(ues[0][0].cell)
     assert P.lib().srsran_pusch_gpu_decode_batch(ctypes.byref(pu.q), n, arr, cres, res) == 0
     for i, (out_s, data_s, noise, epre, cfo, tbs, nack, cfg_s) in enumerate(want):

@@ -126,6 +126,37 @@ def timed_region(step, steps, warmup, world, dist, sync, device):
     return elapsed
 
 
+def step_spread(step, n, torch, stream, host_phases=None):
+    """Per-step spread of `n` back-to-back steps (after the timed region, the same launch pattern): the
+    GPU time between HIP events recorded on the launch stream after every step, the host time of every
+    enqueue call, and -- when `host_phases` (srsran_4g_amd.prof) is given -- the library's host phases of
+    the slowest call.  -> {"gpu_ms": min/median/max, "host_ms": min/median/max, ...}"""
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(n + 1)]
+    host, phases = [], []
+    ev[0].record(stream)
+    for i in range(n):
+        if host_phases is not None:
+            host_phases.host_enable(True)
+        t = time.perf_counter()
+        step()
+        host.append((time.perf_counter() - t) * 1e3)
+        if host_phases is not None:
+            phases.append({k: round(us, 1) for k, (us, _) in host_phases.host_read().items()})
+            host_phases.host_enable(False)
+        ev[i + 1].record(stream)
+    torch.cuda.synchronize()
+    gpu = [ev[i].elapsed_time(ev[i + 1]) for i in range(n)]
+
+    def mmm(v):
+        return {"min": round(min(v), 4), "median": round(float(np.median(v)), 4), "max": round(max(v), 4)}
+    out = {"steps": n, "gpu_ms": mmm(gpu), "host_ms": mmm(host),
+           "max_over_median": round(max(gpu) / float(np.median(gpu)), 3)}
+    if phases:
+        out["host_phases_us_slowest_call"] = phases[int(np.argmax(host))]
+    return out
+
+
 def algo_bytes(K):
     """Algorithmic HBM bytes per code block: int16 LLRs in + K/8 bytes out."""
     return (3 * K + 12) * 2 + K // 8
@@ -941,6 +972,8 @@ def run_pdsch(args, torch, dist, world, rank, device, steps=None, warmup=None, c
     torch.cuda.synchronize()
     h2d_s = (time.perf_counter() - t1) / n_h2d
     del d_xs[1]
+    # per-step spread of the same back-to-back launches (events between steps; host phases per call)
+    spread = step_spread(step, max(steps, 10), torch, stream, prof)
     # host enqueue cost of one step (the API builds descriptors and launches asynchronously)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
@@ -1025,6 +1058,7 @@ def run_pdsch(args, torch, dist, world, rank, device, steps=None, warmup=None, c
             "algo_bytes_per_launch": int(bytes_per_launch),
         },
         "stages": per_stage,
+        "step_spread": spread,
         "host_enqueue_ms_per_step": round(host_ms, 4),
         "host_phases_us_per_call": host_phases,
         "chain_bytes_per_sf": 2 * sf_len * 8 + 2 * C3_TBS // 8,
@@ -1480,6 +1514,7 @@ def main():
 
     bits_per_step = args.batch * sum(Ks)
     value = world * bits_per_step * args.steps / elapsed / 1e6
+    spread = step_spread(step, max(args.steps, 5), torch, stream)
 
     # ---- per-launch kernel durations (HIP events on the launch stream), outside the timed region ----
     events = []
@@ -1608,6 +1643,7 @@ def main():
             "avg_launch_ms": round(avg_ms, 4),
             "algo_bytes_per_launch": int(bytes_per_launch),
         }, **valu),
+        "step_spread": spread,
         "per_kernel_mbps": {n: round(d["bits"] / (d["ms"] * 1e-3) / 1e6, 1) for n, d in per_kernel.items()},
         "mbps_16_half_its": round(mbps_16, 1),
         "output_check": {"blocks": args.batch * len(Ks), "mismatched": bad,
@@ -1645,6 +1681,7 @@ def main():
             "roofline": pd["roofline"],
             "stages": pd["stages"],
             "host_enqueue_ms_per_step": pd["host_enqueue_ms_per_step"],
+            "step_spread": pd["step_spread"],
             "host_phases_us_per_call": pd["host_phases_us_per_call"],
             "chain_bytes_per_sf": pd["chain_bytes_per_sf"],
             "chain_roofline_frac": round(pd["config"]["subframes_per_s"] * pd["chain_bytes_per_sf"]

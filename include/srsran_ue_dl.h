@@ -313,6 +313,11 @@ int srsran_pdsch_gpu_decode_batch(srsran_pdsch_t*              q,
  * q and complete once that batch's stream has reached it, and their number.  SRSRAN_ERROR if the TB was not in
  * the batch. */
 int srsran_pdsch_gpu_last_llr(srsran_pdsch_t* q, uint32_t sf, uint32_t tb, const int16_t** d_llr, uint32_t* nof_llr);
+/* added: the RMS EVM (srsran_pdsch_res_t.evm, pdsch.c:698-713) of subframe `sf` / transport block `tb` of the last
+ * batch on q, for subframes whose cfg->meas_evm_en was set: a device float (NAN where no symbol was measured),
+ * valid until the next batch on q.  SRSRAN_ERROR if it was not measured.  (srsran_pdsch_decode fills data[].evm
+ * and q->avg_evm itself.) */
+int srsran_pdsch_gpu_last_evm(srsran_pdsch_t* q, uint32_t sf, uint32_t tb, const float** d_evm);
 
 /* ---------------- UE DL (ue/ue_dl.h:77-207, ue_dl.c) ----------------
  * decode_fft_estimate: OFDM, CRS estimation, PCFICH (sets sf->cfi) and the PDCCH LLRs, all on the

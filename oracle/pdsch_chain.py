@@ -88,12 +88,12 @@ def pdsch_decode(ora, grids, ce, noise, nof_prb, cell_id, nports, tti, cfi, rnti
         x, csi = ora.predecode(SCHEME[scheme], y, h, ntb, codebook, scaling, noise)
     out = []
     for q in range(ntb):
-        llr = ora.demod_s(MOD[Qm[q]], x[q])
+        llr = demod = ora.demod_s(MOD[Qm[q]], x[q])
         llr = ora.sequence_apply_s(llr, ora.pdsch_seed(rnti, q, 2 * sf_idx, cell_id))
         if csi_enable:
             llr = ora.csi_correction(MOD[Qm[q]], csi[q], llr)
         st = states[q] if states else None
         nl = 2 if (scheme == "diversity" or layers == 2) and ntb == 1 else 1  # Nl = 2 when layers != TBs (sch.c:587-590)
         ret, data, noi, avg, state = ora.dlsch_decode(tbs[q], Qm[q] * nl, rv[q], llr, max_iterations, st)
-        out.append(dict(ret=ret, data=data, avg=avg, llr=llr, state=state, nof_re=idx.size))
+        out.append(dict(ret=ret, data=data, avg=avg, llr=llr, state=state, nof_re=idx.size, sym=x[q], demod=demod))
     return out

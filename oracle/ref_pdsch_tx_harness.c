@@ -141,3 +141,23 @@ out:
   free(packed);
   return ret;
 }
+
+/* ---- PDSCH EVM (pdsch.c:698-713): the reference's own srsran_evm_run_s (modem/evm.h:175-212, static inline,
+ * compiled here) on the equalised symbols of a codeword and its demodulated (pre-scrambling) int16 LLRs, with an
+ * EVM buffer of max_bits bits (srsran_evm_buffer_alloc / _resize, pdsch.c:297, 468-471). ---- */
+#include "srsran/phy/modem/evm.h"
+
+float ref_evm_run_s(int mod, const cf_t* symbols, const int16_t* llr, uint32_t nof_bits, uint32_t max_bits)
+{
+  srsran_modem_table_t t;
+  srsran_modem_table_init(&t);
+  if (srsran_modem_table_lte(&t, (srsran_mod_t)mod)) {
+    return NAN;
+  }
+  srsran_modem_table_bytes(&t);
+  srsran_evm_buffer_t* b = srsran_evm_buffer_alloc(max_bits);
+  const float          e = srsran_evm_run_s(b, &t, symbols, llr, nof_bits);
+  srsran_evm_free(b);
+  srsran_modem_table_free(&t);
+  return e;
+}

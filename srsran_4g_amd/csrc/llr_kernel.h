@@ -25,7 +25,20 @@ struct LlrItem {
   uint32_t      seed;
   uint32_t      bit0;
   int           scramble;
+  // srsran_evm_run_s (modem/evm.h:175-212) on the first evm_n symbols (0: off): per LLR block the sum of
+  // |sym - mod(hard(pre-scrambling LLRs))|^2 into evm_part[block]; evm_finalize_launch turns them into the RMS
+  float*        evm_part;
+  uint32_t      evm_n;
 };
+// one EVM result: sqrtf(sum of nparts block sums (in block order) / nsym) into *out
+struct EvmItem {
+  const float* part;
+  uint32_t     nparts;
+  uint32_t     nsym;
+  float*       out;
+};
+hipError_t evm_finalize_launch(const EvmItem* d_items, uint32_t nitems, hipStream_t stream);
+constexpr uint32_t LLR_BLOCK_SYMBOLS = 256 * 16;  // symbols of one LLR block (evm_part entries = ceil(n / this))
 // nitems items of one modulation (device array); max_n = largest n
 hipError_t llr_batch_launch(int mod, const LlrItem* d_items, uint32_t nitems, uint32_t max_n, int any_scramble,
                             hipStream_t stream);

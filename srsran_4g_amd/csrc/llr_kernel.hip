@@ -266,6 +266,9 @@ __device__ __forceinline__ void demap(float re, float im, uint32_t i, uint32_t n
 
 static constexpr int LLR_THREADS = 256;
 static constexpr int SPT         = 16;  // symbols per thread
+static_assert(LLR_THREADS * SPT == LLR_BLOCK_SYMBOLS, "llr_kernel.h block size");
+
+__device__ __forceinline__ float2 modulate(int mod, uint32_t i);
 
 // csi_correction (pdsch.c:523-618, SSE build) for the LLRs o[0..Q) of symbol s:
 // symbols inside the SSE blocks get mulhi(e, cvtps_pi16(csi * 32767/csi_max)) -- with the
@@ -341,7 +344,8 @@ __device__ __forceinline__ uint32_t gold16(uint32_t& x1, uint32_t& x2)
 template <int MOD>
 __device__ __forceinline__ void llr_block(const float2* __restrict__ sym, uint32_t n, int scramble, uint32_t seed,
                                           uint32_t bit0, const float* __restrict__ csi,
-                                          const float* __restrict__ csi_max, int16_t* __restrict__ llr, uint32_t blk)
+                                          const float* __restrict__ csi_max, int16_t* __restrict__ llr, uint32_t blk,
+                                          float* __restrict__ evm_part = nullptr, uint32_t evm_n = 0)
 {
   constexpr int       Q = Qm<MOD>::v;
   __shared__ uint16_t cbits[LLR_THREADS * 8 + 2];  // SPT * Q / 16 = Q chunks per thread
@@ -365,6 +369,7 @@ __device__ __forceinline__ void llr_block(const float2* __restrict__ sym, uint32
   const float mx  = csi ? *csi_max : 1.0f;
   const bool  a16 = ((uintptr_t)llr & 15) == 0;
   const bool  a4  = ((uintptr_t)llr & 3) == 0;
+  float       err = 0.0f;  // EVM: this thread's sum of squared symbol errors
 #pragma unroll 4
   for (int r = 0; r < SPT; r++) {
     const uint32_t i = t + (uint32_t)r * LLR_THREADS;
@@ -375,6 +380,18 @@ __device__ __forceinline__ void llr_block(const float2* __restrict__ sym, uint32
     const float2   v = sym[s];
     int16_t        o[Q];
     demap<MOD>(v.x, v.y, s, n, o);
+    if constexpr (MOD >= 1) {
+      if (s < evm_n) {  // hard decision (bit = !sign, evm.h HARD_DECISION), remodulated, error power
+        uint32_t idx = 0;
+#pragma unroll
+        for (int k = 0; k < Q; k++) {
+          idx = (idx << 1) | (o[k] >= 0 ? 1u : 0u);
+        }
+        const float2 m  = modulate(MOD, idx);
+        const float  dr = v.x - m.x, di = v.y - m.y;
+        err += dr * dr + di * di;
+      }
+    }
     if (scramble) {
       const uint32_t b  = i * Q;
       const uint32_t w0 = cbits[b >> 4];
@@ -416,6 +433,20 @@ __device__ __forceinline__ void llr_block(const float2* __restrict__ sym, uint32
       }
     }
   }
+  if (evm_part && base < evm_n) {  // block sum in a fixed order: wave butterflies, then the 4 waves
+    __shared__ float wsum[LLR_THREADS / 64];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      err += __shfl_xor(err, off, 64);
+    }
+    if ((t & 63) == 0) {
+      wsum[t >> 6] = err;
+    }
+    __syncthreads();
+    if (t == 0) {
+      evm_part[blk] = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
+    }
+  }
 }
 
 template <int MOD>
@@ -431,7 +462,30 @@ __global__ __launch_bounds__(LLR_THREADS) void llr_batch_kernel(const LlrItem* _
 {
   const LlrItem& it = items[blockIdx.y];
   llr_block<MOD>(reinterpret_cast<const float2*>(it.sym), it.n, it.scramble, it.seed, it.bit0, it.csi, it.csi_max,
-                 it.llr, blockIdx.x);
+                 it.llr, blockIdx.x, it.evm_part, it.evm_n);
+}
+
+__global__ void evm_finalize_kernel(const EvmItem* __restrict__ items, uint32_t nitems)
+{
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= nitems) {
+    return;
+  }
+  const EvmItem& e = items[k];
+  float          s = 0.0f;
+  for (uint32_t j = 0; j < e.nparts; j++) {
+    s += e.part[j];
+  }
+  *e.out = e.nsym ? sqrtf(s / (float)e.nsym) : NAN;  // srsran_vec_avg_power_cf + sqrtf
+}
+
+hipError_t evm_finalize_launch(const EvmItem* d_items, uint32_t nitems, hipStream_t stream)
+{
+  if (nitems == 0) {
+    return hipSuccess;
+  }
+  hipLaunchKernelGGL(evm_finalize_kernel, dim3((nitems + 63) / 64), dim3(64), 0, stream, d_items, nitems);
+  return hipGetLastError();
 }
 
 hipError_t llr_batch_launch(int mod, const LlrItem* d_items, uint32_t nitems, uint32_t max_n, int any_scramble,

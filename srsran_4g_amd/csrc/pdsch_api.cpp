@@ -20,6 +20,7 @@
 #include <string>
 #include <vector>
 
+#include "../../include/srsran_pdcch.h"
 #include "llr_kernel.h"
 #include "pdsch_internal.h"
 #include "stage_timing.h"
@@ -57,6 +58,12 @@ struct PdschGpu {
     const int16_t* d;
   };
   std::vector<LlrRef> last_llr;  // the last batch's LLR buffers (srsran_pdsch_gpu_last_llr)
+  struct EvmRef {
+    uint32_t sf, tb;
+    float*   d;
+  };
+  std::vector<EvmRef> last_evm;       // the last batch's EVM results (srsran_pdsch_gpu_last_evm)
+  uint32_t            evm_max_bits = 0;  // srsran_evm_buffer_t.max_bits (pdsch.c:297, 468-471)
 };
 
 bool grow_dev(void** p, size_t* cap, size_t need)
@@ -149,9 +156,10 @@ struct Cw {
   int      mod;
 };
 
-// Enqueue predecode + LLR of nsf subframes; fills `cws` and the per-codeword LLR pointers.
+// Enqueue predecode + LLR of nsf subframes; fills `cws` and the per-codeword LLR pointers (and, for
+// subframes with meas_evm_en, g->last_evm).
 // Scratch layout (d_work): x [nsf][2][max_re] float2 | csi [nsf][2][max_re] f32 | csi_max [nsf][2] |
-// llr [nsf][2][max_re * 8] int16
+// llr [nsf][2][max_re * 8] int16 | EVM block sums [nsf][2][evm_parts] f32 | EVM results [nsf][2] f32
 int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sfs, hipStream_t s,
                 std::vector<Cw>& cws, std::vector<int16_t*>& llr)
 {
@@ -252,9 +260,13 @@ int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sf
   const size_t c_sz = align256((size_t)nsf * 2 * max_re * sizeof(float));
   const size_t m_sz = align256((size_t)nsf * 2 * sizeof(float));
   const size_t e_sz = align256((size_t)nsf * 2 * max_re * kMaxQm * sizeof(int16_t));
-  if (!grow_dev((void**)&g->d_work, &g->work_cap, x_sz + c_sz + m_sz + e_sz)) {
+  const uint32_t evm_parts = (2 * max_re + LLR_BLOCK_SYMBOLS - 1) / LLR_BLOCK_SYMBOLS;  // >= blocks of any item
+  const size_t   v_sz      = align256((size_t)nsf * 2 * (evm_parts + 1) * sizeof(float));
+  if (!grow_dev((void**)&g->d_work, &g->work_cap, x_sz + c_sz + m_sz + e_sz + v_sz)) {
     return SRSRAN_ERROR;
   }
+  float* d_evm_part = (float*)(g->d_work + x_sz + c_sz + m_sz + e_sz);
+  float* d_evm_out  = d_evm_part + (size_t)nsf * 2 * evm_parts;
   float2*  d_x   = (float2*)g->d_work;
   float*   d_csi = (float*)(g->d_work + x_sz);
   float*   d_max = (float*)(g->d_work + x_sz + c_sz);
@@ -270,6 +282,8 @@ int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sf
   }
   // LLR descriptors, grouped by modulation
   std::vector<LlrItem> li(cws.size());
+  std::vector<EvmItem> evs;
+  g->last_evm.clear();
   llr.assign(cws.size(), nullptr);
   for (size_t i = 0; i < cws.size(); i++) {
     const Cw&                    c = cws[i];
@@ -284,6 +298,16 @@ int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sf
     it.bit0     = 0;
     it.scramble = 1;
     llr[i]      = it.llr;
+    if (f.cfg->meas_evm_en) {  // srsran_evm_run_s over min(max_bits, nof_bits) bits (evm.h:190-194)
+      const uint32_t nbits = std::min(g->evm_max_bits, c.nbits);
+      const uint32_t qmod  = srsran_mod_bits_x_symbol((srsran_mod_t)c.mod);
+      const size_t   slot  = (size_t)c.sf * 2 + c.tb;
+      it.evm_n             = qmod ? nbits / qmod : 0;
+      it.evm_part          = d_evm_part + slot * evm_parts;
+      evs.push_back(EvmItem{it.evm_part, (it.evm_n + LLR_BLOCK_SYMBOLS - 1) / LLR_BLOCK_SYMBOLS, it.evm_n,
+                            d_evm_out + slot});
+      g->last_evm.push_back({c.sf, c.tb, d_evm_out + slot});
+    }
   }
   std::vector<uint32_t> order_p(nsf), order_l(cws.size());
   for (uint32_t i = 0; i < nsf; i++) {
@@ -296,9 +320,10 @@ int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sf
   std::stable_sort(order_l.begin(), order_l.end(), [&](uint32_t x, uint32_t y) { return cws[x].mod < cws[y].mod; });
   const size_t pa_bytes = align256(nsf * sizeof(PredArgs));
   const size_t li_bytes = align256(std::max<size_t>(cws.size(), 1) * sizeof(LlrItem));
+  const size_t ev_bytes = align256(evs.size() * sizeof(EvmItem));
   desc.stop();
   srsran_amd::HostScope wait(srsran_amd::HP_PDSCH_WAIT);
-  if (hipEventSynchronize(g->staged) != hipSuccess || !grow_stage(g, pa_bytes + li_bytes)) {
+  if (hipEventSynchronize(g->staged) != hipSuccess || !grow_stage(g, pa_bytes + li_bytes + ev_bytes)) {
     return SRSRAN_ERROR;
   }
   wait.stop();
@@ -311,12 +336,15 @@ int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sf
   for (uint32_t i = 0; i < cws.size(); i++) {
     hl[i] = li[order_l[i]];
   }
+  if (!evs.empty()) {
+    memcpy(g->h_stage + pa_bytes + li_bytes, evs.data(), evs.size() * sizeof(EvmItem));
+  }
   // the upload on the copy stream once the previous batch's predecode / LLR launches are done with
   // d_stage: it runs beside the OFDM / estimation stages instead of in line in front of the predecoder
   if (g->used) {
     hipStreamWaitEvent(g->copy, g->read, 0);
   }
-  hipMemcpyAsync(g->d_stage, g->h_stage, pa_bytes + li_bytes, hipMemcpyHostToDevice, g->copy);
+  hipMemcpyAsync(g->d_stage, g->h_stage, pa_bytes + li_bytes + ev_bytes, hipMemcpyHostToDevice, g->copy);
   hipEventRecord(g->staged, g->copy);
   hipStreamWaitEvent(s, g->staged, 0);
   g->used = true;
@@ -352,6 +380,10 @@ int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sf
     }
     i = j;
   }
+  if (!evs.empty() &&
+      evm_finalize_launch((const EvmItem*)(g->d_stage + pa_bytes + li_bytes), (uint32_t)evs.size(), s) != hipSuccess) {
+    return SRSRAN_ERROR;
+  }
   return SRSRAN_SUCCESS;
 }
 
@@ -374,6 +406,7 @@ int srsran_pdsch_init_ue(srsran_pdsch_t* q, uint32_t max_prb, uint32_t nof_rx_an
   }
   PdschGpu* g = new PdschGpu();
   q->gpu      = g;
+  g->evm_max_bits = (uint32_t)std::max(0, srsran_ra_tbs_from_idx(SRSRAN_RA_NOF_TBS_IDX - 1, 6));  // pdsch.c:297
   if (hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&g->copy, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&g->staged, hipEventDisableTiming) != hipSuccess ||
@@ -438,6 +471,9 @@ int srsran_pdsch_set_cell(srsran_pdsch_t* q, srsran_cell_t cell)
     hipFree(kv.second.d);
   }
   g->tables.clear();
+  // the EVM buffer grows to the new cell (srsran_evm_buffer_resize keeps the larger of the two, pdsch.c:468-471)
+  g->evm_max_bits = std::max(g->evm_max_bits,
+                             (uint32_t)std::max(0, srsran_ra_tbs_from_idx(SRSRAN_RA_NOF_TBS_IDX - 1, cell.nof_prb)));
   q->cell   = cell;
   q->max_re = SRSRAN_SF_LEN_RE(cell.nof_prb, cell.cp);
   return SRSRAN_SUCCESS;
@@ -491,6 +527,12 @@ int srsran_pdsch_decode(srsran_pdsch_t*        q,
     hipStreamSynchronize(g->stream);
     return ret;
   }
+  float evm[SRSRAN_MAX_CODEWORDS] = {NAN, NAN};
+  for (const auto& e : g->last_evm) {
+    if (e.tb < SRSRAN_MAX_CODEWORDS) {
+      hipMemcpyAsync(&evm[e.tb], e.d, sizeof(float), hipMemcpyDeviceToHost, g->stream);
+    }
+  }
   if (hipStreamSynchronize(g->stream) != hipSuccess) {
     return SRSRAN_ERROR;
   }
@@ -499,7 +541,7 @@ int srsran_pdsch_decode(srsran_pdsch_t*        q,
     if (data[tb].crc) {
       continue;  // already acknowledged (pdsch.c:893)
     }
-    data[tb].evm = NAN;
+    data[tb].evm = cfg->meas_evm_en ? evm[tb] : NAN;  // pdsch.c:698-713
     if (!cfg->softbuffers.rx[tb] || !data[tb].payload) {
       data[tb].crc = false;
       continue;
@@ -507,6 +549,13 @@ int srsran_pdsch_decode(srsran_pdsch_t*        q,
     const int r = srsran_dlsch_decode2_dev(&q->dl_sch, cfg, llr[i], data[tb].payload, (int)tb, cfg->grant.nof_layers);
     data[tb].crc                  = r == SRSRAN_SUCCESS;  // pdsch.c:739-747
     data[tb].avg_iterations_block = srsran_sch_last_noi(&q->dl_sch);
+  }
+  if (cfg->meas_evm_en) {  // pdsch.c:945-951
+    for (uint32_t i = 0; i < SRSRAN_MAX_CODEWORDS; i++) {
+      if (cfg->grant.tb[i].enabled && !std::isnan(data[i].evm)) {
+        q->avg_evm = 0.1f * data[i].evm + (1.0f - 0.1f) * q->avg_evm;  // SRSRAN_VEC_EMA(data, avg, 0.1)
+      }
+    }
   }
   return SRSRAN_SUCCESS;
 }
@@ -563,6 +612,20 @@ int srsran_pdsch_gpu_decode_batch(srsran_pdsch_t*              q,
   return ret == SRSRAN_SUCCESS ? (int)tbs.size() : ret;
 }
 
+
+int srsran_pdsch_gpu_last_evm(srsran_pdsch_t* q, uint32_t sf, uint32_t tb, const float** d_evm)
+{
+  if (!q || !q->gpu || !d_evm) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  for (const auto& r : ((PdschGpu*)q->gpu)->last_evm) {
+    if (r.sf == sf && r.tb == tb) {
+      *d_evm = r.d;
+      return SRSRAN_SUCCESS;
+    }
+  }
+  return SRSRAN_ERROR;
+}
 
 int srsran_pdsch_gpu_last_llr(srsran_pdsch_t* q, uint32_t sf, uint32_t tb, const int16_t** d_llr, uint32_t* nof_llr)
 {

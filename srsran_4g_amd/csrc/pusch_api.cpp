@@ -744,7 +744,7 @@ int srsran_pusch_decode(srsran_pusch_t*        q,
   u.n_tilde[1] = cfg->grant.n_prb_tilde[1];
   u.noise      = channel->noise_estimate;
   u.dft_norm = 1.0f / sqrtf((float)M);
-  LlrItem it;
+  LlrItem it{};
   memset(&it, 0, sizeof(it));
   it.sym         = (const float*)g->d_sym;
   it.llr         = g->d_q;

@@ -163,6 +163,7 @@ def lib():
             "srsran_pdsch_gpu_decode_batch": ([PD, u32, ctypes.POINTER(srsran_pdsch_gpu_sf_t), P, P, P], ctypes.c_int),
             "srsran_pdsch_gpu_last_llr": ([PD, u32, u32, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(u32)],
                                           ctypes.c_int),
+            "srsran_pdsch_gpu_last_evm": ([PD, u32, u32, ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
             "srsran_ue_dl_init": ([UE, P, u32, u32], ctypes.c_int),
             "srsran_ue_dl_free": ([UE], None),
             "srsran_ue_dl_set_cell": ([UE, srsran_cell_t], ctypes.c_int),
@@ -311,7 +312,8 @@ MOD_FROM_QM = {1: 0, 2: 1, 4: 2, 6: 3, 8: 4}
 
 
 def pdsch_cfg(nof_prb, nof_re, tbs, Qm, rv=(0, 0), scheme="cdd", pmi=0, rnti=0x1234, max_iterations=8,
-              csi_enable=True, power_scale=False, p_a=0.0, p_b=0, softbuffers=(), zf=False, cp=0, nof_ports=2):
+              csi_enable=True, power_scale=False, p_a=0.0, p_b=0, softbuffers=(), zf=False, cp=0, nof_ports=2,
+              meas_evm=False):
     """srsran_pdsch_cfg_t for a full-bandwidth grant of len(tbs) codewords on as many layers
     (srsUE defaults: csi_enable, 8 half-iterations, MMSE, no power scaling); cp=1: extended CP;
     transmit diversity runs on nof_ports layers (2 or 4)."""
@@ -340,6 +342,7 @@ def pdsch_cfg(nof_prb, nof_re, tbs, Qm, rv=(0, 0), scheme="cdd", pmi=0, rnti=0x1
     c.decoder_type = 0 if zf else 1
     c.p_a, c.p_b = p_a, p_b
     c.power_scale, c.csi_enable = power_scale, csi_enable
+    c.meas_evm_en = bool(meas_evm)
     for i, sb in enumerate(softbuffers):
         c.softbuffers.rx[i] = ctypes.pointer(sb.s)
     return c
@@ -393,6 +396,7 @@ class Pdsch:
             data[i].crc = bool(acked[i])
         ret = lib().srsran_pdsch_decode(ctypes.byref(self.q), ctypes.byref(sf), ctypes.byref(cfg), ctypes.byref(res),
                                         ctypes.addressof(ptrs), data)
+        self.last_evm = [float(data[i].evm) for i in range(ntb)]  # NAN unless cfg.meas_evm_en
         return ret, [(data[i].crc, pls[i], data[i].avg_iterations_block) for i in range(ntb)]
 
     def free(self):
@@ -520,6 +524,13 @@ class UeDl:
         if lib().srsran_pdsch_gpu_last_llr(ctypes.byref(self.q.pdsch), sf, tb, ctypes.byref(d), ctypes.byref(n)):
             raise RuntimeError(f"no LLRs for subframe {sf} TB {tb} in the last batch")
         return d.value, n.value
+
+    def last_evm(self, sf, tb):
+        """srsran_pdsch_gpu_last_evm of the UE's PDSCH object after a batch: device pointer of one float"""
+        d = ctypes.c_void_p()
+        if lib().srsran_pdsch_gpu_last_evm(ctypes.byref(self.q.pdsch), sf, tb, ctypes.byref(d)):
+            raise RuntimeError(f"no EVM for subframe {sf} TB {tb} in the last batch")
+        return d.value
 
     def free(self):
         if self.q.gpu:

@@ -228,6 +228,68 @@ def test_ue_dl_batch_cfo(U, SCH, ora):
     ue.free()
 
 
+def _ref_evm(sym, demod, mod, nof_bits, max_bits):
+    """srsran_evm_run_s of the reference (modem/evm.h, compiled into oracle/_ref: ref_pdsch_tx_harness.c)"""
+    import ctypes
+    L = ctypes.CDLL(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "_ref",
+                                 "libsrsref.so"), mode=os.RTLD_LAZY)
+    f = L.ref_evm_run_s
+    f.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32]
+    f.restype = ctypes.c_float
+    sym = np.ascontiguousarray(sym, np.complex64)
+    demod = np.ascontiguousarray(demod, np.int16)
+    return float(f(mod, sym.ctypes.data, demod.ctypes.data, nof_bits, max_bits))
+
+
+@pytest.mark.parametrize("case", [0, 3, 5, 7, 8, 12])
+def test_pdsch_evm_matches_reference(U, SCH, ora, case):
+    """cfg->meas_evm_en (pdsch.c:698-713, srsUE phy.meas_evm): srsran_pdsch_res_t.evm of every TB (host-synchronous
+    srsran_pdsch_decode) and srsran_pdsch_gpu_last_evm (batch) against the reference's own srsran_evm_run_s
+    (modem/evm.h:175-212, compiled into _ref) on the oracle chain's equalised symbols and demodulated LLRs of the
+    same grids: the same hard decisions, remodulated symbols and bit limit (the EVM buffer's max_bits,
+    pdsch.c:297, 468-471); the squared errors are summed in another order (GPU block tree vs AVX2 lanes): rtol 5e-5.
+    q->avg_evm follows the reference's EMA (pdsch.c:945-951)."""
+    kw = dict(CASES[case])
+    rng = np.random.default_rng(300 + case)
+    kw.pop("fail", False)
+    nof_prb = kw.pop("nof_prb", 100)
+    cell_id = kw.pop("cell_id", 1)
+    nports = kw.pop("nports", 2)
+    tti = kw.pop("tti", 1)
+    cfi = kw.pop("cfi", 1)
+    tbs = kw.pop("tbs", (TBS, TBS))
+    Qm = kw.pop("Qm", (6, 6))
+    scheme = kw.pop("scheme", "cdd")
+    pmi = kw.pop("pmi", 0)
+    pls, x, nre, grids, ce, st = _case(ora, rng, nof_prb, cell_id, nports, tti, cfi, tbs, Qm, scheme, pmi, **kw)
+    ref = PC.pdsch_decode(ora, grids, ce, st["noise"], nof_prb, cell_id, nports, tti, cfi, 0x1234, list(tbs),
+                          list(Qm), [0] * len(tbs), scheme=scheme, pmi=pmi)
+    max_bits = max(U.lib().srsran_ra_tbs_from_idx(33, 6), U.lib().srsran_ra_tbs_from_idx(33, nof_prb))
+    mods = {2: 1, 4: 2, 6: 3, 8: 4}
+    want = [_ref_evm(r["sym"], r["demod"], mods[Qm[q]], nre * Qm[q], max_bits) for q, r in enumerate(ref)]
+    assert all(np.isfinite(w) and w > 0 for w in want)
+    sbs = [SCH.SoftbufferRx(nof_prb=nof_prb) for _ in tbs]
+    cfg = U.pdsch_cfg(nof_prb, nre, tbs, Qm, scheme=scheme, pmi=pmi, softbuffers=sbs, meas_evm=True,
+                      nof_ports=nports)
+    pd = U.Pdsch(U.cell(nof_prb, nports, cell_id), grids.shape[0])
+    avg0 = pd.q.avg_evm
+    ret, _ = pd.decode(cfg, tti, cfi, grids, ce, st["noise"])
+    assert ret == 0
+    for q in range(len(tbs)):
+        assert pd.last_evm[q] == pytest.approx(want[q], rel=5e-5), q
+    ema = avg0
+    for q in range(len(tbs)):
+        ema = 0.1 * pd.last_evm[q] + 0.9 * ema
+    assert pd.q.avg_evm == pytest.approx(ema, rel=1e-6)
+    # without meas_evm_en the result stays NAN
+    cfg0 = U.pdsch_cfg(nof_prb, nre, tbs, Qm, scheme=scheme, pmi=pmi, softbuffers=sbs, nof_ports=nports)
+    pd.decode(cfg0, tti, cfi, grids, ce, st["noise"])
+    assert all(np.isnan(e) for e in pd.last_evm)
+    pd.free()
+    for sb in sbs:
+        sb.free()
+
+
 LLR_STATS = {}
 
 

@@ -1,7 +1,7 @@
 """The two decoders of the 16-sub-block class on the SB layout, each forced onto small batches: the lane
 pair (tdec16_kernel.hip; by itself from 512 blocks a launch), the single lane per sub-block
-(tdecs_kernel.hip; by itself from srsran_tdec_gpu_get_single_threshold() blocks) and its split variant
-(two helper waves; by itself up to srsran_tdec_gpu_get_split_threshold() blocks): every K >= 816 of
+(tdecs_kernel.hip; by itself from srsran_tdec_gpu_get_single_threshold() blocks) on 16-step windows and on
+8-step windows (srsran_tdec_gpu_set_w8_max_k, the build the fused all-size class runs): every K >= 816 of
 the bit-exact suites again, plain batches with block counts that leave workgroups partly empty, the
 multi-size fused launch, and DL-SCH transport blocks with CRC early stop over HARQ."""
 import numpy as np
@@ -13,19 +13,21 @@ pytestmark = pytest.mark.gpu
 
 
 NEVER = 1 << 30
-KERNELS = {"pair": ("tdec16_kernel", 0, NEVER, 0), "single": ("tdec16s_kernel", 0, 0, 0),
-           "split": ("tdec16s_split_kernel", 0, 0, NEVER)}
+KERNELS = {"pair": ("tdec16_kernel", 0, NEVER, None), "single": ("tdec16s_kernel", 0, 0, 0),
+           "single_w8": ("tdec16sw8_kernel", 0, 0, 6144)}
 
 
 @pytest.fixture(scope="module", autouse=True, params=sorted(KERNELS))
 def kernel(request):
     """every test three times: the lane-pair decoder (tdec16_kernel.hip), the single-lane decoder
-    (tdecs_kernel.hip) and its split variant with helper waves, each forced onto every batch size"""
+    (tdecs_kernel.hip) on 16-step and on 8-step windows, each forced onto every batch size"""
     from srsran_4g_amd import tdec
     if not tdec.gpu_available():
         pytest.skip("no HIP device")
-    name, pair_min, single_min, split_max = KERNELS[request.param]
-    with tdec.pair_threshold(pair_min), tdec.single_threshold(single_min), tdec.split_threshold(split_max):
+    name, pair_min, single_min, w8 = KERNELS[request.param]
+    with tdec.pair_threshold(pair_min), tdec.single_threshold(single_min), \
+            tdec.w8_max_k(w8 if w8 is not None else tdec.load_library().srsran_tdec_gpu_get_w8_max_k()), \
+            tdec.w8_fused_max_k(w8 if w8 else tdec.load_library().srsran_tdec_gpu_get_w8_fused_max_k()):
         yield name
 
 
@@ -80,7 +82,7 @@ def test_multi_size_launch(ora, kernel):
         tdec.gpu_run_multi(Ks, [t.data_ptr() for t in ins], [t.shape[1] for t in ins], True,
                            [t.data_ptr() for t in outs], [t.shape[0] for t in ins], 8, None)
         torch.cuda.synchronize()
-    assert tdec.last_kernel() == kernel.replace("_split", "").replace("_kernel", "_multi_kernel")
+    assert tdec.last_kernel() == kernel.replace("_kernel", "_multi_kernel")
     for K, o, w in zip(Ks, outs, want):
         assert np.array_equal(o.cpu().numpy(), w), K
 

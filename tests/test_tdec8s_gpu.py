@@ -13,15 +13,14 @@ pytestmark = pytest.mark.gpu
 K8 = [k for k in CB_SIZES if 408 <= k <= 800]
 
 
-@pytest.fixture(scope="module", autouse=True, params=["tdec8s_kernel", "tdec8s_split_kernel"])
+@pytest.fixture(scope="module", autouse=True, params=["tdec8s_kernel"])
 def kname(request):
-    """every test twice: the single-lane decoder and its split variant (helper waves), 16-step windows
-    (the 8-step build, the class's default, is tests/test_tdec_w8_gpu.py)"""
+    """the single-lane decoder on 16-step windows (the 8-step build, the class's default, is
+    tests/test_tdec_w8_gpu.py; the split variant with helper waves was retired in round 4)"""
     from srsran_4g_amd import tdec
     if not tdec.gpu_available():
         pytest.skip("no HIP device")
-    with tdec.single_threshold(0), tdec.split_threshold(1 << 30 if "split" in request.param else 0), \
-            tdec.w8_max_k(0):
+    with tdec.single_threshold(0), tdec.w8_max_k(0):
         yield request.param
 
 

@@ -12,7 +12,7 @@ buffers placed far apart in device memory.
     for its pool block (the batch tiles a pool of distinct AWGN blocks at several SNRs, so decoded
     words differ from the transmitted ones in some blocks and not in others).
   * configs[0]'s shape on the GPU: K = 6144 x 1024 through srsran_tdec_gpu_run_batch, on each of the
-    16-sub-block decoders (the single lane by default at this size, its split variant, lane pair, quad).
+    16-sub-block decoders (the single lane by default at this size, its 8-step-window build, lane pair, quad).
   * DL-SCH transport blocks whose soft buffers lie more than 2 GB apart: the lane-pair decoder runs
     (the descriptor list is padded where a workgroup's two blocks would straddle two far buffers) and
     every TB equals the oracle's decode_tb (return, payload, average iterations, CB CRC flags).
@@ -100,7 +100,7 @@ def test_all188_x1024_fused_launch(env):
     assert len({w.tobytes() for K in (6144, 40) for w in want[K]}) == 2 * len(POOL_EBNO)
 
 
-@pytest.mark.parametrize("kernel", ["tdec16s_split_kernel<false>", "tdec16s_kernel<false>", "tdec16_kernel<false>",
+@pytest.mark.parametrize("kernel", ["tdec16sw8_kernel<false>", "tdec16s_kernel<false>", "tdec16_kernel<false>",
                                     "tdec_kernel<16>"])
 def test_k6144_x1024_batch(env, kernel):
     torch, tdec, ref, ora = env
@@ -112,12 +112,12 @@ def test_k6144_x1024_batch(env, kernel):
     d_out = torch.zeros((batch, K // 8), dtype=torch.uint8, device="cuda")
     never = 1 << 30
     L = tdec.load_library()
-    pair, single, split = {"tdec16s_kernel<false>": (None, None, None),  # the default at this size
-                           "tdec16s_split_kernel<false>": (None, None, never), "tdec16_kernel<false>": (None, never, 0),
-                           "tdec_kernel<16>": (never, never, 0)}[kernel]
+    pair, single, w8 = {"tdec16s_kernel<false>": (None, None, 0),  # the default at this size
+                        "tdec16sw8_kernel<false>": (None, None, 6144), "tdec16_kernel<false>": (None, never, 0),
+                        "tdec_kernel<16>": (never, never, 0)}[kernel]
     with tdec.pair_threshold(L.srsran_tdec_gpu_get_pair_threshold() if pair is None else pair), \
             tdec.single_threshold(L.srsran_tdec_gpu_get_single_threshold() if single is None else single), \
-            tdec.split_threshold(L.srsran_tdec_gpu_get_split_threshold() if split is None else split):
+            tdec.w8_max_k(w8):
         tdec.gpu_run_batch(K, d_in.data_ptr(), d_in.shape[1], True, d_out.data_ptr(), batch, 8, None)
         torch.cuda.synchronize()
     assert tdec.last_kernel() == kernel
@@ -125,7 +125,7 @@ def test_k6144_x1024_batch(env, kernel):
     assert np.array_equal(got, want[np.arange(batch) % len(pool)])
 
 
-@pytest.mark.parametrize("kernel", ["tdec16_kernel", "tdec16s_kernel", "tdec16s_split_kernel"])
+@pytest.mark.parametrize("kernel", ["tdec16_kernel", "tdec16s_kernel", "tdec16sw8_kernel"])
 def test_dlsch_far_soft_buffers(env, kernel):
     """soft buffers > 2 GB apart (arena off, 2.4 GB buffers): the lane-pair and the single-lane decoder
     still run (the descriptor list is padded per workgroup) and every TB equals the oracle's decode_tb"""
@@ -158,7 +158,7 @@ def test_dlsch_far_soft_buffers(env, kernel):
     d_res = torch.full((ntb,), 77, dtype=torch.int32, device="cuda")
     d_avg = torch.zeros(ntb, dtype=torch.float32, device="cuda")
     with tdec.pair_threshold(0), tdec.single_threshold(1 << 30 if kernel == "tdec16_kernel" else 0), \
-            tdec.split_threshold(1 << 30 if "split" in kernel else 0):
+            tdec.w8_max_k(6144 if "w8" in kernel else 0):
         assert q.decode_batch(entries, d_res.data_ptr(), d_avg.data_ptr()) == 0
         torch.cuda.synchronize()
         assert tdec.last_kernel() == kernel + "<true>"

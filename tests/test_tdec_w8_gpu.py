@@ -15,7 +15,7 @@ def w8():
     from srsran_4g_amd import tdec
     if not tdec.gpu_available():
         pytest.skip("no HIP device")
-    with tdec.single_threshold(0), tdec.split_threshold(0), tdec.w8_max_k(6144):
+    with tdec.single_threshold(0), tdec.w8_max_k(6144):
         yield
 
 

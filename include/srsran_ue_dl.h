@@ -155,6 +155,23 @@ int srsran_chest_dl_gpu_estimate_batch(srsran_chest_dl_t* q,
                                        float*             d_res,
                                        void*              stream);
 
+/* added: the batch with an estimator configuration (srsran_chest_dl_estimate_cfg's options): AVERAGE or
+ * INTERPOLATE (full_grid = 1 required: d_ce rows of 2 * nsymb * 12 * nof_prb), REFS / PSS / EMPTY noise (PSS /
+ * EMPTY estimate in subframes 0 and 5, the other subframes keep the last estimate, across calls as the reference's
+ * q->noise_estimate does), Gauss filters of order <= 7 or automatic with REFS noise.  cfg = NULL: srsUE's
+ * defaults.  Not provided here: sync_error_enable (the host-synchronous srsran_chest_dl_estimate_cfg has it). */
+int srsran_chest_dl_gpu_estimate_batch_cfg(srsran_chest_dl_t*           q,
+                                           const srsran_chest_dl_cfg_t* cfg,
+                                           const uint32_t*              d_sf_idx,
+                                           uint32_t                     nof_sf,
+                                           const cf_t*                  d_grid,
+                                           size_t                       grid_sf_stride,
+                                           cf_t*                        d_ce,
+                                           size_t                       ce_sf_stride,
+                                           int                          full_grid,
+                                           float*                       d_res,
+                                           void*                        stream);
+
 /* added: device-resident estimate.  d_grid: nof_rx_antennas grids of 14 * 12 * nof_prb cf_t,
  * back to back; d_ce: [port][rx] rows of 12 * nof_prb (full_grid = 0: the AVERAGE estimate is
  * the same for every symbol) or of 14 * 12 * nof_prb (full_grid = 1).  d_res (4 floats:

@@ -190,6 +190,28 @@ class Oracle(_Lib, _PhyMixin):
         f(grids.ctypes.data, nof_prb, cell_id, nports, nrx, sf_idx, symbol_sz, cp, ce.ctypes.data, out.ctypes.data)
         return ce, dict(noise=float(out[0]), rsrp=float(out[1]), rssi=float(out[2]), cfo=float(out[3]))
 
+    def chest_dl_ext(self, grids, nof_prb, cell_id, nports, sf_idx, symbol_sz, cp=0, estimator=0, noise_alg=0,
+                     filt_order=4, filt_std=1.0, sync=False, noise_state=None):
+        """chest_dl.c with the options beyond srsUE's defaults (oracle_chest_dl_ext): estimator 0 AVERAGE /
+        1 INTERPOLATE, noise_alg 0 REFS / 1 PSS / 2 EMPTY, filt_order 0 = automatic, sync = correct_sync_error.
+        -> (ce (nports, nrx, n), stats dict, corrected grids, noise_state (4, 4) after the call)"""
+        grids = np.array(grids, np.complex64, copy=True)
+        nrx, n = grids.shape
+        ce = np.zeros((nports, nrx, n), np.complex64)
+        out = np.zeros(5, np.float32)
+        ns = np.zeros((4, 4), np.float32) if noise_state is None else np.array(noise_state, np.float32, copy=True)
+        pss = np.zeros(62, np.complex64)
+        self.lib.oracle_pss_generate.argtypes = [ctypes.c_uint32, ctypes.c_void_p]
+        self.lib.oracle_pss_generate(cell_id % 3, pss.ctypes.data)
+        f = self.lib.oracle_chest_dl_ext
+        f.argtypes = [ctypes.c_void_p] + [ctypes.c_uint32] * 10 + [ctypes.c_float, ctypes.c_uint32] + \
+            [ctypes.c_void_p] * 4
+        f(grids.ctypes.data, nof_prb, cell_id, nports, nrx, sf_idx, symbol_sz, cp, estimator, noise_alg, filt_order,
+          filt_std, 1 if sync else 0, pss.ctypes.data, ns.ctypes.data, ce.ctypes.data, out.ctypes.data)
+        st = dict(noise=float(out[0]), rsrp=float(out[1]), rssi=float(out[2]), cfo=float(out[3]),
+                  sync_error=float(out[4]))
+        return ce, st, grids, ns
+
     def sequence_bits(self, seed, n):
         c = np.zeros(n, np.uint8)
         self.lib.oracle_sequence_bits.argtypes = [ctypes.c_uint32, _u8p, ctypes.c_uint32]

@@ -25,6 +25,17 @@
 
 #include "phy_oracle.h"
 
+#ifndef M_PI
+#define M_PI 3.14159265358979323846
+#endif
+#ifndef M_1_PI
+#define M_1_PI 0.31830988618379067154
+#endif
+#ifndef M_SQRT1_2
+#define M_SQRT1_2 0.70710678118654752440
+#endif
+void sincosf(float x, float* s, float* c); /* glibc (GNU extension; -std=c11 hides the declaration) */
+
 static int16_t sat16(int32_t v) { return v > 32767 ? 32767 : (v < -32768 ? -32768 : (int16_t)v); }
 
 /* x86 float -> int32 conversions: out-of-range gives INT32_MIN ("integer indefinite") */
@@ -779,4 +790,312 @@ int oracle_chest_dl(const float* grid, uint32_t nof_prb, uint32_t cell_id, uint3
                     uint32_t sf_idx, uint32_t symbol_sz, float* ce, float* out)
 {
   return oracle_chest_dl_cp(grid, nof_prb, cell_id, nports, nrx, sf_idx, symbol_sz, 0, ce, out);
+}
+
+/* ======================= chest_dl.c beyond srsUE's defaults (round 4) =======================
+ *   estimator INTERPOLATE  average_pilots without the time average (chest_dl.c:571-599), frequency
+ *                          interpolation per CRS symbol (interpolate_pilots 476-505: interp_lin, M = 6) and
+ *                          the time interpolation between the CRS symbols (510-554, interp.c:147-188)
+ *   noise PSS / EMPTY      estimate_noise_pss (402-419) / estimate_noise_empty_sc (422-433) in subframes 0 and
+ *                          5, after the interpolation (731-745); other subframes keep q->noise_estimate
+ *   automatic filter       Gauss order 4, stddev 200 x q->noise_estimate[rx][port] (706-707): the REFS value
+ *                          of this subframe, the kept value with PSS / EMPTY
+ *   correct_sync_error     chest_dl_estimate_correct_sync_error (750-804) on the rx grid before estimation
+ * estimator: 0 AVERAGE, 1 INTERPOLATE; noise_alg: 0 REFS, 1 PSS, 2 EMPTY; filt_order 0 = automatic;
+ * noise_state [4 rx][4 port] in / out (q->noise_estimate); pss: the 62 PSS values of N_id_2 (may be NULL unless
+ * noise_alg = PSS); grid is modified in place by the sync correction; out: noise, rsrp, rssi, cfo, sync_error. */
+
+/* srsran_vec_apply_cfo (vector_simd.c:1723-1774, AVX2 + FMA build): 8 phase lanes advanced by w^8, scalar tail */
+static cpx cprod_fma(cpx a, cpx b)
+{
+  const float t1 = a.i * b.i, t2 = a.i * b.r;
+  return (cpx){fmaf(a.r, b.r, -t1), fmaf(a.r, b.i, t2)};
+}
+void oracle_apply_cfo(const float* x, float cfo, float* z, uint32_t len)
+{
+  const float twopi = 2.0f * (float)M_PI;
+  float       s, c;
+  sincosf(twopi * cfo, &s, &c);
+  const cpx w = {c, s};
+  cpx       ph[8];
+  ph[0] = (cpx){1.0f, 0.0f};
+  for (int k = 1; k < 8; k++) {
+    ph[k] = cprod_fma(ph[k - 1], w);
+  }
+  const cpx  w8 = cprod_fma(ph[7], w);
+  const cpx* X  = (const cpx*)x;
+  cpx*       Z  = (cpx*)z;
+  uint32_t   i  = 0;
+  for (; i + 8 <= len; i += 8) {
+    for (int k = 0; k < 8; k++) {
+      Z[i + k] = cprod_fma(X[i + k], ph[k]);
+      ph[k]    = cprod_fma(ph[k], w8);
+    }
+  }
+  cpx p = ph[0];
+  for (; i < len; i++) {
+    Z[i] = cprod_fma(X[i], p);
+    p    = cprod_fma(p, w);
+  }
+}
+
+/* srsran_interp_linear_vector3 (interp.c:158-188) with to_right, len = vector length */
+static void interp_vector(const cpx* in0, const cpx* in1, const cpx* start, cpx* between, uint32_t d, uint32_t M,
+                          uint32_t nre)
+{
+  const float rd = (float)1 / d;
+  for (uint32_t k = 0; k < nre; k++) {
+    const cpx diff = cscale(csub(in1[k], in0[k]), rd);
+    cpx       b    = cadd(start ? start[k] : in0[k], diff);
+    between[k]     = b;
+    for (uint32_t i = 1; i < M; i++) {
+      b                    = cadd(b, diff);
+      between[i * nre + k] = b;
+    }
+  }
+}
+
+/* srsran_vec_estimate_frequency (vector_simd.c:1776-1818) in scalar order */
+float oracle_estimate_frequency(const float* xf, uint32_t len);
+static float estimate_frequency(const cpx* x, uint32_t len) { return oracle_estimate_frequency((const float*)x, len); }
+float oracle_estimate_frequency(const float* xf, uint32_t len)
+{
+  const cpx* x   = (const cpx*)xf;
+  cpx        sum = {0, 0};
+  for (uint32_t i = 1; i < len; i++) {
+    sum = cadd(sum, cmul(x[i], cconj(x[i - 1])));
+  }
+  return (float)(-atan2f(sum.i, sum.r) * M_1_PI * 0.5f);  /* -cargf(sum) * M_1_PI * 0.5f */
+}
+
+int oracle_chest_dl_ext(float* grid, uint32_t nof_prb, uint32_t cell_id, uint32_t nports, uint32_t nrx, uint32_t sf_idx,
+                        uint32_t symbol_sz, uint32_t cp, uint32_t estimator, uint32_t noise_alg, uint32_t filt_order,
+                        float filt_std, uint32_t sync, const float* pss, float* noise_state, float* ce, float* out)
+{
+  const uint32_t nsymb = cp ? 6 : 7;
+  const uint32_t nre = NRE * nof_prb, nsf = 2 * nsymb * nre, nref = 2 * nof_prb;
+  cpx*           G   = (cpx*)grid;
+  cpx*           CE  = (cpx*)ce;
+  static cpx     pil[2][4 * 2 * 110];
+  oracle_crs_pilots_cp(cell_id, nof_prb, 0, sf_idx, cp, (float*)pil[0]);
+  oracle_crs_pilots_cp(cell_id, nof_prb, 1, sf_idx, cp, (float*)pil[1]);
+  float rsrp[4][4], rssi[4][4], cfo = 0, sync_err00 = 0;
+  for (uint32_t rx = 0; rx < nrx; rx++) {
+    cpx* in = G + (size_t)rx * nsf;
+    if (sync) { /* chest_dl.c:750-804 */
+      float pwr_sum = 0, serr = 0;
+      for (uint32_t port = 0; port < nports; port++) {
+        const uint32_t nsym = crs_nof_symbols(port), np = nsym * nref;
+        cpx            pe[4 * 220];
+        for (uint32_t l = 0; l < nsym; l++) {
+          const uint32_t sym = crs_nsymbol(l, port, nsymb);
+          uint32_t       f   = crs_fidx(cell_id, l, port);
+          for (uint32_t i = 0; i < nref; i++, f += 6) {
+            pe[l * nref + i] = cmul(in[sym * nre + f], cconj(pil[port / 2][l * nref + i]));
+          }
+        }
+        const float k   = (float)symbol_sz / 6.0f;
+        float       sum = 0;
+        for (uint32_t l = 0; l < nsym; l++) {
+          sum += estimate_frequency(pe + l * nref, nref) * k;
+        }
+        const float pwr = avg_power(pe, np);
+        const float se  = sum / (float)nsym;
+        if (rx == 0 && port == 0) {
+          sync_err00 = se;
+        }
+        if (!isinf(sum) && !isnan(sum) && !isinf(pwr) && !isnan(pwr)) {
+          serr += se * pwr;
+          pwr_sum += pwr;
+        }
+      }
+      if (isnormal(pwr_sum)) {
+        serr /= pwr_sum;
+      }
+      if (isnormal(serr) && fabsf(serr) > 0.05f) {
+        const float f = serr / (float)symbol_sz;
+        for (uint32_t i = 0; i < 2 * nsymb; i++) {
+          oracle_apply_cfo((const float*)(in + i * nre), f, (float*)(in + i * nre), nre);
+        }
+      }
+    }
+    for (uint32_t port = 0; port < nports; port++) {
+      const uint32_t nsym = crs_nof_symbols(port), np = nsym * nref;
+      cpx            recv[4 * 220], pe[4 * 220], avg[4 * 220], tmp[4 * 220];
+      for (uint32_t l = 0; l < nsym; l++) {
+        const uint32_t sym = crs_nsymbol(l, port, nsymb);
+        uint32_t       f   = crs_fidx(cell_id, l, port);
+        for (uint32_t i = 0; i < nref; i++, f += 6) {
+          recv[l * nref + i] = in[sym * nre + f];
+        }
+      }
+      for (uint32_t k = 0; k < np; k++) {
+        pe[k] = cmul(recv[k], cconj(pil[port / 2][k]));
+      }
+      rsrp[rx][port] = avg_power(recv, np);
+      float rs       = 0;
+      for (uint32_t l = 0; l < nsym; l++) {
+        const cpx* t = in + crs_nsymbol(l, port, nsymb) * nre;
+        for (uint32_t k = 0; k < nre; k++) {
+          rs += t[k].r * t[k].r + t[k].i * t[k].i;
+        }
+      }
+      rssi[rx][port] = rs / (float)nsym;
+      if (nsym == 4) {
+        cpx sum = {0, 0};
+        for (uint32_t i = 0; i < 2; i++) {
+          for (uint32_t k = 0; k < np / 4; k++) {
+            sum = cadd(sum, cmul(pe[i * np / 4 + k], cconj(pe[(i + 2) * np / 4 + k])));
+          }
+        }
+        const float n  = (float)symbol_sz;
+        const float ng = (float)(int)ceilf(144.0f * n / 2048.0f);
+        cfo            = -atan2f(sum.i, sum.r) * n / ((float)nsymb * (n + ng)) / 2 / kPi;
+      }
+      const uint32_t fidx0 = crs_fidx(cell_id, 0, port);
+      float*         ns    = &noise_state[rx * 4 + port];
+      if (noise_alg == 0) {
+        *ns = noise_pilots(pe, nsym, nref, fidx0);
+      }
+      float    filt[8];
+      uint32_t flen = filt_order ? oracle_gauss_filter(filt, filt_order, filt_std)
+                                 : oracle_gauss_filter(filt, 4, *ns * 200.0f);
+      {
+        float s = 0;
+        for (uint32_t k = 0; k < flen; k++) {
+          s += filt[k];
+        }
+        if (!isnormal(s)) {
+          flen = 0; /* srsran_chest_set_smooth_filter_gauss returns 0: conv_same writes zeros */
+        }
+      }
+      cpx* row = CE + ((size_t)port * nrx + rx) * nsf;
+      if (estimator == 0) {
+        uint32_t nr = nref;
+        if (nsym > 1) {
+          const cpx* a = fidx0 < 3 ? pe : pe + nref;
+          const cpx* b = fidx0 < 3 ? pe + nref : pe;
+          for (uint32_t k = 0; k < nref; k++) {
+            tmp[2 * k]     = a[k];
+            tmp[2 * k + 1] = b[k];
+          }
+          for (uint32_t l = 2; l < nsym - 1; l += 2) {
+            const cpx* c = fidx0 < 3 ? pe + l * nref : pe + (l + 1) * nref;
+            const cpx* d = fidx0 < 3 ? pe + (l + 1) * nref : pe + l * nref;
+            for (uint32_t k = 0; k < nref; k++) {
+              tmp[2 * k]     = cadd(tmp[2 * k], c[k]);
+              tmp[2 * k + 1] = cadd(tmp[2 * k + 1], d[k]);
+            }
+          }
+          nr *= 2;
+          for (uint32_t k = 0; k < nr; k++) {
+            pe[k] = cscale(tmp[k], 2.0f / (float)nsym);
+          }
+        }
+        if (flen) {
+          conv_same(pe, filt, avg, nr, flen);
+        } else {
+          memset(avg, 0, nr * sizeof(cpx));
+        }
+        if (nsym > 1) {
+          const uint32_t off = cell_id % 3;
+          interp_linear_offset(avg, row, nr, 3, off, 3 - off);
+        } else {
+          interp_linear_offset(avg, row, nr, 6, fidx0, 6 - fidx0);
+        }
+        for (uint32_t l = 1; l < 2 * nsymb; l++) {
+          memcpy(row + l * nre, row, nre * sizeof(cpx));
+        }
+      } else {
+        for (uint32_t l = 0; l < nsym; l++) { /* smoothing of every CRS symbol, then interpolation into its row */
+          if (flen) {
+            conv_same(pe + l * nref, filt, avg + l * nref, nref, flen);
+          } else {
+            memset(avg + l * nref, 0, nref * sizeof(cpx));
+          }
+          const uint32_t off = crs_fidx(cell_id, l, port);
+          interp_linear_offset(avg + l * nref, row + crs_nsymbol(l, port, nsymb) * nre, nref, 6, off, 6 - off);
+        }
+#define CES(i) (row + (size_t)(i)*nre)
+        if (!cp) {
+          if (port < 2) {
+            interp_vector(CES(0), CES(4), NULL, CES(1), 4, 3, nre);
+            interp_vector(CES(4), CES(7), NULL, CES(5), 3, 2, nre);
+            interp_vector(CES(7), CES(11), NULL, CES(8), 4, 3, nre);
+            interp_vector(CES(7), CES(11), CES(11), CES(12), 4, 2, nre);
+          } else {
+            interp_vector(CES(8), CES(1), CES(1), CES(0), 7, 1, nre);
+            interp_vector(CES(1), CES(8), NULL, CES(2), 7, 6, nre);
+            interp_vector(CES(1), CES(8), NULL, CES(9), 7, 5, nre);
+          }
+        } else {
+          if (port < 2) {
+            interp_vector(CES(0), CES(3), NULL, CES(1), 3, 2, nre);
+            interp_vector(CES(3), CES(6), NULL, CES(4), 3, 2, nre);
+            interp_vector(CES(6), CES(9), NULL, CES(7), 3, 2, nre);
+            interp_vector(CES(6), CES(9), CES(9), CES(10), 3, 2, nre);
+          } else {
+            interp_vector(CES(7), CES(1), CES(1), CES(0), 6, 1, nre);
+            interp_vector(CES(1), CES(7), NULL, CES(2), 6, 5, nre);
+            interp_vector(CES(1), CES(7), NULL, CES(8), 6, 4, nre);
+          }
+        }
+#undef CES
+      }
+      if (noise_alg != 0 && (sf_idx == 0 || sf_idx == 5)) {
+        const uint32_t kp = (nsymb - 1) * nre + nre / 2 - 31;
+        if (noise_alg == 1) { /* estimate_noise_pss: nof_ports * avg|ce * pss - rx|^2 * M_SQRT1_2 */
+          cpx t[62];
+          for (uint32_t k = 0; k < 62; k++) {
+            const cpx p = {pss[2 * k], pss[2 * k + 1]};
+            t[k]        = csub(cmul(row[kp + k], p), in[kp + k]);
+          }
+          *ns = (float)nports * avg_power(t, 62) * (float)M_SQRT1_2;
+        } else { /* estimate_noise_empty_sc */
+          const uint32_t ks = (nsymb - 2) * nre + nre / 2 - 31;
+          *ns = avg_power(in + ks - 5, 5) + avg_power(in + ks + 62, 5) + avg_power(in + kp - 5, 5) +
+                avg_power(in + kp + 62, 5);
+        }
+      }
+    }
+  }
+  float n = 0;
+  for (uint32_t rx = 0; rx < nrx; rx++) {
+    float s = 0;
+    for (uint32_t p = 0; p < nports; p++) {
+      s += noise_state[rx * 4 + p];
+    }
+    n += s / (float)nports;
+  }
+  out[0] = n / (float)nrx;
+  float best = -1e9f;
+  for (uint32_t p = 0; p < nports; p++) {
+    float s = 0;
+    for (uint32_t rx = 0; rx < nrx; rx++) {
+      s += rsrp[rx][p];
+    }
+    s /= (float)nrx;
+    best = s > best ? s : best;
+  }
+  out[1] = best;
+  float r = 0;
+  for (uint32_t rx = 0; rx < nrx; rx++) {
+    r += 4 * rssi[rx][0] / (float)nof_prb / (float)NRE;
+  }
+  out[2] = r / (float)nrx;
+  out[3] = cfo;
+  out[4] = sync ? sync_err00 : 0.0f;
+  return 0;
+}
+
+/* srsran_pss_generate (pss.c:341-368): the argument in double, cosf / sinf of its float */
+void oracle_pss_generate(uint32_t N_id_2, float* signal)
+{
+  const float root[3] = {25.0f, 29.0f, 34.0f};
+  for (int i = 0; i < 62; i++) {
+    const double v   = i < 31 ? ((float)i * ((float)i + 1.0)) : (((float)i + 2.0) * ((float)i + 1.0));
+    const float  arg = (float)((float)-1 * M_PI * root[N_id_2] * v / 63.0);
+    signal[2 * i]     = cosf(arg);
+    signal[2 * i + 1] = sinf(arg);
+  }
 }

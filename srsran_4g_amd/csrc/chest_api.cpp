@@ -14,6 +14,7 @@
 
 #include "../../include/srsran_ue_dl.h"
 #include "chest_kernel.h"
+#include "ofdm_kernel.h"
 
 using namespace srsran_amd;
 
@@ -52,7 +53,40 @@ struct ChestGpu {
   uint32_t    nrx     = 0;
   float       filter[8];
   uint32_t    filter_len = 0;
+  float2*     pss     = nullptr;  // the cell's 62 PSS values (noise PSS)
+  float*      noise   = nullptr;  // device q->noise_estimate [4][4]: host-sync upload / batch state
+  float*      sync    = nullptr;  // correct_sync_error sums [4 rx][4 port][10]
+  float2*     tab     = nullptr;  // sync correction phasor table (12 * max_prb)
+  float       sync_err[SRSRAN_MAX_PORTS][SRSRAN_MAX_PORTS] = {};  // q->sync_err (chest_dl.c:776)
 };
+
+// srsran_pss_generate (pss.c:341-368): the argument in double, cosf / sinf of its float
+void pss_generate(uint32_t N_id_2, float2* sig)
+{
+  const float root[3] = {25.0f, 29.0f, 34.0f};
+  for (int i = 0; i < 62; i++) {
+    const double v   = i < 31 ? ((float)i * ((float)i + 1.0)) : (((float)i + 2.0) * ((float)i + 1.0));
+    const float  arg = (float)((float)-1 * M_PI * root[N_id_2] * v / 63.0);
+    sig[i]           = make_float2(cosf(arg), sinf(arg));
+  }
+}
+
+// the estimator options a call may use (chest_dl.c:655-745); batch: no sync correction, no automatic filter
+// with the PSS / EMPTY noise (its input would be the previous subframe's estimate)
+bool cfg_supported(const srsran_chest_dl_cfg_t* cfg, bool batch)
+{
+  if (!cfg) {
+    return true;
+  }
+  const bool est   = cfg->estimator_alg == SRSRAN_ESTIMATOR_ALG_AVERAGE || cfg->estimator_alg == SRSRAN_ESTIMATOR_ALG_INTERPOLATE;
+  const bool noise = cfg->noise_alg == SRSRAN_NOISE_ALG_REFS || cfg->noise_alg == SRSRAN_NOISE_ALG_PSS ||
+                     cfg->noise_alg == SRSRAN_NOISE_ALG_EMPTY;
+  if (!est || !noise || cfg->filter_type != SRSRAN_CHEST_FILTER_GAUSS || cfg->rsrp_neighbour || cfg->filter_coef[0] > 7) {
+    return false;
+  }
+  return !batch || (!cfg->sync_error_enable &&
+                    (cfg->filter_coef[0] > 0 || cfg->noise_alg == SRSRAN_NOISE_ALG_REFS));
+}
 
 constexpr size_t kPilotsPerSf = 2 * 4 * CHEST_MAX_NREF;  // float2 per subframe (both port pairs)
 
@@ -154,7 +188,11 @@ int srsran_chest_dl_init(srsran_chest_dl_t* q, uint32_t max_prb, uint32_t nof_rx
       hipMalloc((void**)&g->pilots, 10 * kPilotsPerSf * sizeof(float2)) != hipSuccess ||
       hipMalloc((void**)&g->grid, nof_rx_antennas * sf * sizeof(float2)) != hipSuccess ||
       hipMalloc((void**)&g->ce, SRSRAN_MAX_PORTS * nof_rx_antennas * sf * sizeof(float2)) != hipSuccess ||
-      hipMalloc((void**)&g->stats, SRSRAN_MAX_PORTS * SRSRAN_MAX_PORTS * 8 * sizeof(float)) != hipSuccess) {
+      hipMalloc((void**)&g->stats, SRSRAN_MAX_PORTS * SRSRAN_MAX_PORTS * 8 * sizeof(float)) != hipSuccess ||
+      hipMalloc((void**)&g->pss, 62 * sizeof(float2)) != hipSuccess ||
+      hipMalloc((void**)&g->noise, 16 * sizeof(float)) != hipSuccess || hipMemset(g->noise, 0, 16 * sizeof(float)) ||
+      hipMalloc((void**)&g->sync, 16 * 10 * sizeof(float)) != hipSuccess ||
+      hipMalloc((void**)&g->tab, 12 * (size_t)max_prb * sizeof(float2)) != hipSuccess) {
     q->gpu = g;
     srsran_chest_dl_free(q);
     return SRSRAN_ERROR;
@@ -180,6 +218,10 @@ void srsran_chest_dl_free(srsran_chest_dl_t* q)
     hipFree(g->ce);
     hipFree(g->stats);
     hipFree(g->bstats);
+    hipFree(g->pss);
+    hipFree(g->noise);
+    hipFree(g->sync);
+    hipFree(g->tab);
     delete g;
   }
   memset(q, 0, sizeof(*q));
@@ -217,7 +259,10 @@ int srsran_chest_dl_set_cell(srsran_chest_dl_t* q, srsran_cell_t cell)
       }
     }
   }
-  if (hipMemcpy(g->pilots, h.data(), h.size() * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess) {
+  float2 pss[62];
+  pss_generate(cell.id % 3, pss);  // chest_dl.c:291
+  if (hipMemcpy(g->pilots, h.data(), h.size() * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(g->pss, pss, sizeof(pss), hipMemcpyHostToDevice) != hipSuccess) {
     return SRSRAN_ERROR;
   }
   g->filter_len = gauss(g->filter, 4, 1.0f);
@@ -273,14 +318,81 @@ static int chest_enqueue(srsran_chest_dl_t* q, uint32_t tti, const float2* d_gri
   a.full_grid  = full ? 1 : 0;
   a.filter_len = g->filter_len;
   memcpy(a.filter, g->filter, sizeof(a.filter));
+  a.sf_index = tti % 10;
+  a.pss      = g->pss;
+  a.noise_in = g->noise;
   if (cfg) {
     if (cfg->filter_coef[0] <= 0) {
       a.filter_auto = 1;
     } else {
       a.filter_len = gauss(a.filter, (uint32_t)cfg->filter_coef[0], cfg->filter_coef[1]);
     }
+    a.estimator = cfg->estimator_alg == SRSRAN_ESTIMATOR_ALG_INTERPOLATE ? 1 : 0;
+    a.noise_alg = (uint32_t)cfg->noise_alg;
+    if (a.estimator == 1 && !full) {
+      return SRSRAN_ERROR;  // every symbol has its own estimate
+    }
   }
   return chest_launch(a, s) == hipSuccess ? SRSRAN_SUCCESS : SRSRAN_ERROR;
+}
+
+// correct_sync_error (chest_dl.c:750-804) of the host-synchronous path on the uploaded grids g->grid: the pilot
+// phase sums on the device, the reference's scalar arithmetic here, and where the error exceeds 0.05 samples
+// every row of that rx grid rotated on the device by srsran_vec_apply_cfo's phasors (then copied back to the
+// caller's buffer, which the reference corrects in place)
+static int correct_sync_error(srsran_chest_dl_t* q, uint32_t tti, cf_t* input[SRSRAN_MAX_PORTS])
+{
+  ChestGpu*      g   = (ChestGpu*)q->gpu;
+  const uint32_t nre = 12 * q->cell.nof_prb, rows = 2 * SRSRAN_CP_NSYMB(q->cell.cp), np = q->cell.nof_ports;
+  ChestArgs      a{};
+  a.grid    = g->grid;
+  a.pilots  = g->pilots + (tti % 10) * kPilotsPerSf;
+  a.nof_prb = q->cell.nof_prb;
+  a.cell_id = q->cell.id;
+  a.nports  = np;
+  a.nrx     = q->nof_rx_antennas;
+  a.nsymb   = SRSRAN_CP_NSYMB(q->cell.cp);
+  float sums[16 * 10];
+  if (chest_sync_sums_launch(a, g->sync, g->stream) != hipSuccess ||
+      hipMemcpyAsync(sums, g->sync, sizeof(sums), hipMemcpyDeviceToHost, g->stream) != hipSuccess ||
+      hipStreamSynchronize(g->stream) != hipSuccess) {
+    return SRSRAN_ERROR;
+  }
+  const int sz = srsran_symbol_sz(q->cell.nof_prb);
+  for (uint32_t rx = 0; rx < q->nof_rx_antennas; rx++) {
+    float pwr_sum = 0.0f, sync_err = 0.0f;
+    for (uint32_t port = 0; port < np; port++) {
+      const float*   o    = sums + (rx * 4 + port) * 10;
+      const uint32_t nsym = port < 2 ? 4 : 2, npilots = nsym * 2 * q->cell.nof_prb;
+      const float    k    = (float)sz / 6.0f;
+      float          sum  = 0.0f;
+      for (uint32_t l = 0; l < nsym; l++) {  // srsran_vec_estimate_frequency: -cargf(sum) * M_1_PI * 0.5f
+        const float f = (float)(-atan2f(o[2 * l + 1], o[2 * l]) * M_1_PI * 0.5f);
+        sum += f * k;
+      }
+      const float pwr            = o[8] / (float)npilots;  // srsran_vec_avg_power_cf
+      g->sync_err[rx][port]      = sum / (float)nsym;
+      if (!std::isinf(sum) && !std::isnan(sum) && !std::isinf(pwr) && !std::isnan(pwr)) {
+        sync_err += g->sync_err[rx][port] * pwr;
+        pwr_sum += pwr;
+      }
+    }
+    if (std::isnormal(pwr_sum)) {
+      sync_err /= pwr_sum;
+    }
+    if (std::isnormal(sync_err) && fabsf(sync_err) > 0.05f) {
+      float c, sn;
+      cfo_phasor(sync_err / (float)sz, &c, &sn);
+      float2* grid = g->grid + (size_t)rx * rows * nre;
+      if (cfo_table_launch(c, sn, g->tab, nre, g->stream) != hipSuccess ||
+          grid_rotate_launch(grid, g->tab, nre, rows, g->stream) != hipSuccess ||
+          hipMemcpyAsync(input[rx], grid, (size_t)rows * nre * sizeof(cf_t), hipMemcpyDeviceToHost, g->stream) !=
+              hipSuccess) {
+        return SRSRAN_ERROR;
+      }
+    }
+  }
+  return SRSRAN_SUCCESS;
 }
 
 // fill_res (chest_dl.c:962-986) from the per (rx, port) statistics
@@ -342,7 +454,7 @@ static void fill_res(srsran_chest_dl_t* q, const float* st, srsran_chest_dl_res_
   res->rsrq_db  = 10.0f * log10f(res->rsrq);
   res->rssi_dbm = 10.0f * log10f(rssi / (float)nrx) + 30.0f;
   res->snr_db   = 10.0f * log10f(res->rsrp / res->noise_estimate);
-  res->sync_error = 0.0f;
+  res->sync_error = ((ChestGpu*)q->gpu)->sync_err[0][0];  // the channel used for synchronisation (chest_dl.c:974)
 }
 
 int srsran_chest_dl_estimate_cfg(srsran_chest_dl_t*     q,
@@ -354,10 +466,9 @@ int srsran_chest_dl_estimate_cfg(srsran_chest_dl_t*     q,
   if (!q || !q->gpu || !sf || !cfg || !input || !res || q->cell.nof_prb == 0) {
     return SRSRAN_ERROR_INVALID_INPUTS;
   }
-  if (sf->sf_type != SRSRAN_SF_NORM || cfg->estimator_alg != SRSRAN_ESTIMATOR_ALG_AVERAGE ||
-      cfg->filter_type != SRSRAN_CHEST_FILTER_GAUSS || cfg->noise_alg != SRSRAN_NOISE_ALG_REFS ||
-      cfg->sync_error_enable || cfg->rsrp_neighbour || cfg->filter_coef[0] > 7) {
-    fprintf(stderr, "[srsran_chest_dl] only srsUE's default estimator configuration is provided\n");
+  if (sf->sf_type != SRSRAN_SF_NORM || !cfg_supported(cfg, false)) {
+    fprintf(stderr, "[srsran_chest_dl] MBSFN subframes, the WIENER estimator, TRIANGLE / NONE filters, filter orders "
+                    "above 7 and rsrp_neighbour are not provided\n");
     return SRSRAN_ERROR;
   }
   ChestGpu*      g   = (ChestGpu*)q->gpu;
@@ -366,6 +477,20 @@ int srsran_chest_dl_estimate_cfg(srsran_chest_dl_t*     q,
   for (uint32_t rx = 0; rx < nrx; rx++) {
     hipMemcpyAsync(g->grid + rx * nsf, input[rx], nsf * sizeof(cf_t), hipMemcpyHostToDevice, g->stream);
   }
+  if (cfg->sync_error_enable) {
+    if (correct_sync_error(q, sf->tti, input)) {
+      return SRSRAN_ERROR;
+    }
+  } else {
+    memset(g->sync_err, 0, sizeof(g->sync_err));
+  }
+  float kept[16] = {};  // q->noise_estimate: the automatic filter's / PSS / EMPTY input
+  for (uint32_t rx = 0; rx < nrx; rx++) {
+    for (uint32_t p = 0; p < np; p++) {
+      kept[rx * 4 + p] = q->noise_estimate[rx][p];
+    }
+  }
+  hipMemcpyAsync(g->noise, kept, sizeof(kept), hipMemcpyHostToDevice, g->stream);
   if (chest_enqueue(q, sf->tti, g->grid, g->ce, 1, g->stream, cfg)) {
     return SRSRAN_ERROR;
   }
@@ -430,8 +555,30 @@ extern "C" int srsran_chest_dl_gpu_estimate_batch(srsran_chest_dl_t* q,
                                                   float*             d_res,
                                                   void*              stream)
 {
+  return srsran_chest_dl_gpu_estimate_batch_cfg(q, nullptr, d_sf_idx, nsf, d_grid, grid_sf_stride, d_ce, ce_sf_stride,
+                                                0, d_res, stream);
+}
+
+extern "C" int srsran_chest_dl_gpu_estimate_batch_cfg(srsran_chest_dl_t*           q,
+                                                      const srsran_chest_dl_cfg_t* cfg,
+                                                      const uint32_t*              d_sf_idx,
+                                                      uint32_t                     nsf,
+                                                      const cf_t*                  d_grid,
+                                                      size_t                       grid_sf_stride,
+                                                      cf_t*                        d_ce,
+                                                      size_t                       ce_sf_stride,
+                                                      int                          full_grid,
+                                                      float*                       d_res,
+                                                      void*                        stream)
+{
   if (!q || !q->gpu || !d_sf_idx || !d_grid || !d_ce || !d_res || q->cell.nof_prb == 0) {
     return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  if (!cfg_supported(cfg, true) ||
+      (cfg && cfg->estimator_alg == SRSRAN_ESTIMATOR_ALG_INTERPOLATE && !full_grid)) {
+    fprintf(stderr, "[srsran_chest_dl] batch: configuration not provided (sync correction, automatic filter with "
+                    "PSS / EMPTY noise, or INTERPOLATE without full grids)\n");
+    return SRSRAN_ERROR;
   }
   ChestGpu* g = (ChestGpu*)q->gpu;
   if (nsf > g->bstats_cap) {
@@ -456,14 +603,28 @@ extern "C" int srsran_chest_dl_gpu_estimate_batch(srsran_chest_dl_t* q,
   a.cell_id        = q->cell.id;
   a.nports         = q->cell.nof_ports;
   a.nrx            = q->nof_rx_antennas;
-  a.ce_stride      = 12 * q->cell.nof_prb;
-  a.full_grid      = 0;
   a.nsymb          = SRSRAN_CP_NSYMB(q->cell.cp);
+  a.ce_stride      = (full_grid ? 2 * a.nsymb : 1) * 12 * q->cell.nof_prb;
+  a.full_grid      = full_grid ? 1 : 0;
   a.filter_len     = g->filter_len;
   memcpy(a.filter, g->filter, sizeof(a.filter));
+  a.pss      = g->pss;
+  a.noise_in = g->noise;  // the state before the batch (REFS: unused)
+  if (cfg) {
+    if (cfg->filter_coef[0] <= 0) {
+      a.filter_auto = 1;
+    } else {
+      a.filter_len = gauss(a.filter, (uint32_t)cfg->filter_coef[0], cfg->filter_coef[1]);
+    }
+    a.estimator = cfg->estimator_alg == SRSRAN_ESTIMATOR_ALG_INTERPOLATE ? 1 : 0;
+    a.noise_alg = (uint32_t)cfg->noise_alg;
+  }
+  const float sz = (float)srsran_symbol_sz(q->cell.nof_prb);
   if (chest_launch(a, s, nsf) != hipSuccess ||
-      chest_finalize_launch(g->bstats, q->cell.nof_ports, q->nof_rx_antennas, q->cell.nof_prb,
-                            (float)srsran_symbol_sz(q->cell.nof_prb), a.nsymb, d_res, nsf, s) != hipSuccess) {
+      (a.noise_alg ? chest_finalize_kept_launch(g->bstats, q->cell.nof_ports, q->nof_rx_antennas, q->cell.nof_prb, sz,
+                                                a.nsymb, g->noise, d_res, nsf, s)
+                   : chest_finalize_launch(g->bstats, q->cell.nof_ports, q->nof_rx_antennas, q->cell.nof_prb, sz,
+                                           a.nsymb, d_res, nsf, s)) != hipSuccess) {
     return SRSRAN_ERROR;
   }
   return SRSRAN_SUCCESS;

@@ -24,6 +24,13 @@ struct ChestArgs {
   float         filter[8]; // smoothing filter (srsran_chest_set_smooth_filter_gauss)
   uint32_t      filter_len;
   uint32_t      filter_auto; // Gauss order 4, stddev = 200 * noise of the (port, rx) (chest_dl.c:703-704)
+  // ---- estimator options beyond srsUE's defaults (chest_dl.c:437-555, 402-433, 703-745) ----
+  uint32_t        estimator;  // 0 AVERAGE (one row, copied), 1 INTERPOLATE (full_grid: every row its own)
+  uint32_t        noise_alg;  // 0 REFS (pilot residuals), 1 PSS, 2 EMPTY (subframes 0 / 5 only)
+  const float2*   pss;        // the 62 PSS values of N_id_2 (noise_alg 1)
+  const float*    noise_in;   // [rx][port] (4 x 4) kept noise estimates: the automatic filter's input and the
+                              // result of PSS / EMPTY outside subframes 0 / 5 (q->noise_estimate)
+  uint32_t        sf_index;   // tti % 10 when sf_idx (below) is null
   // ---- batches of subframes (gridDim.y = nof subframes) ----
   const uint32_t* sf_idx;     // [b] subframe index (tti % 10): pilots + sf_idx[b] * CHEST_PILOTS_PER_SF; null = as given
   size_t          grid_sf_stride; // float2 between subframes of `grid`
@@ -32,12 +39,26 @@ struct ChestArgs {
 
 static constexpr size_t CHEST_PILOTS_PER_SF = 2 * 4 * CHEST_MAX_NREF;  // float2 (both port pairs)
 static constexpr size_t CHEST_STATS_PER_SF  = 4 * 4 * 8;               // floats of stats per subframe
+// stats per (rx, port): [0] noise, [1] rsrp, [2] rssi, [3] / [4] CFO phase sum, [5] 1 when [0] is a new PSS / EMPTY
+// estimate (subframes 0 / 5), 0 when it is noise_in
 
 hipError_t chest_launch(const ChestArgs& a, hipStream_t stream, uint32_t nsf = 1);
 // device-side reduction of the per-(rx, port) stats of nsf subframes into out[b][4] =
 // {noise_estimate, rsrp, rssi, cfo} (fill_res, chest_dl.c:962-986)
 hipError_t chest_finalize_launch(const float* stats, uint32_t np, uint32_t nrx, uint32_t nof_prb, float symbol_sz,
                                  uint32_t nsymb, float* out, uint32_t nsf, hipStream_t stream);
+// the same for PSS / EMPTY noise over a batch, in subframe order: a subframe without a new estimate takes the
+// (rx, port) value left by the subframes before it, starting from state[rx * 4 + port], which holds the last
+// values afterwards (q->noise_estimate across calls)
+hipError_t chest_finalize_kept_launch(float* stats, uint32_t np, uint32_t nrx, uint32_t nof_prb, float symbol_sz,
+                                      uint32_t nsymb, float* state, float* out, uint32_t nsf, hipStream_t stream);
+
+// correct_sync_error (chest_dl.c:750-804), device side of the host-synchronous path: per (rx, port) the LS
+// estimates' per-CRS-symbol phase sums sum(x[i] conj(x[i-1])) and their power sum -> out[(rx * 4 + port) * 10 ..]:
+// 4 complex sums, then the power sum (the host finishes with the reference's scalar arithmetic)
+hipError_t chest_sync_sums_launch(const ChestArgs& a, float* out, hipStream_t stream);
+// rows (2 nsymb of every rx grid) multiplied in place by the phasor table tab[nre] (srsran_vec_apply_cfo per row)
+hipError_t grid_rotate_launch(float2* grid, const float2* tab, uint32_t nre, uint32_t nrows, hipStream_t stream);
 
 }  // namespace srsran_amd
 #endif

@@ -67,20 +67,75 @@ __device__ float block_sum(float v, float* red)
   return s;
 }
 
+// srsran_conv_same_cf (convolution.c:182-218): out[i] = sum_k f[k] x[i - M/2 + k] over the sequence extended
+// linearly at both ends (first[] / last[])
+__device__ void conv_row(const cx* comb, cx* avg, uint32_t nr, const float* filt, uint32_t M)
+{
+  for (uint32_t i = threadIdx.x; i < nr; i += CH_THREADS) {
+    cx acc = {0.f, 0.f};
+    for (uint32_t k = 0; k < M; k++) {
+      const int j = (int)i - (int)(M / 2) + (int)k;  // index into the extended sequence
+      cx        x;
+      if (j < 0) {  // first[]: (2 + M/2 - m) * in[1] - (1 + M/2 - m) * in[0], m = j + M/2
+        const uint32_t m = (uint32_t)(j + (int)(M / 2));
+        x = sub(scl(comb[1], (float)(2 + M / 2 - m)), scl(comb[0], (float)(1 + M / 2 - m)));
+      } else if (j >= (int)nr) {  // last[]: m = j - (nr - M + 1) counts into last[], i >= M - 1
+        const uint32_t m = (uint32_t)(j - (int)(nr - M + 1));
+        x = sub(scl(comb[nr - 1], (float)(2 + m - M / 2)), scl(comb[nr - 2], (float)(1 + m - M / 2)));
+      } else {
+        x = comb[j];
+      }
+      acc = add(acc, scl(x, filt[k]));
+    }
+    avg[i] = acc;
+  }
+}
+
+// srsran_interp_linear_offset (interp.c:258-285) of the nr-point comb `av` (spacing `step`, first pilot at
+// subcarrier `off`), value at subcarrier j
+__device__ __forceinline__ cx interp_at(const cx* av, uint32_t nr, uint32_t step, uint32_t off, uint32_t j)
+{
+  const float rM = (float)1 / step;
+  if (j < off) {
+    const uint32_t jj = off - 1 - j;
+    return sub(av[0], divs(scl(sub(av[1], av[0]), (float)(jj + 1)), (float)step));
+  }
+  if (j < off + step * (nr - 1)) {
+    const uint32_t i = (j - off) / step, r = (j - off) % step;
+    return add(av[i], scl(scl(sub(av[i + 1], av[i]), rM), (float)r));
+  }
+  const uint32_t r = j - off - step * (nr - 1);
+  return add(av[nr - 1], divs(scl(sub(av[nr - 1], av[nr - 2]), (float)r), (float)step));
+}
+
+// srsran_interp_linear_vector3 (interp.c:158-188) for one subcarrier: rows[first .. first + M) from in0 / in1
+__device__ __forceinline__ void ivec(cx* rows, cx in0, cx in1, const cx* start, uint32_t d, uint32_t M, uint32_t first)
+{
+  const cx diff = scl(sub(in1, in0), (float)1 / d);
+  cx       b    = add(start ? *start : in0, diff);
+  rows[first]   = b;
+  for (uint32_t i = 1; i < M; i++) {
+    b               = add(b, diff);
+    rows[first + i] = b;
+  }
+}
+
 __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
 {
   __shared__ cx    pe[4 * CHEST_MAX_NREF];
   __shared__ cx    comb[2 * CHEST_MAX_NREF];
-  __shared__ cx    avg[2 * CHEST_MAX_NREF];
+  __shared__ cx    avg[4 * CHEST_MAX_NREF];
   __shared__ float red[CH_THREADS / 64];
 
   const uint32_t port = blockIdx.x / a.nrx, rx = blockIdx.x % a.nrx, b = blockIdx.y;
   const uint32_t tid  = threadIdx.x;
   const uint32_t nsym = port < 2 ? 4 : 2, nref = 2 * a.nof_prb, np = nsym * nref, nre = 12 * a.nof_prb;
   const float2*  in   = a.grid + b * a.grid_sf_stride + (size_t)rx * 2 * a.nsymb * nre;
+  const uint32_t sfi  = a.sf_idx ? a.sf_idx[b] : a.sf_index;
   const float2*  pil  = a.pilots + (a.sf_idx ? a.sf_idx[b] * CHEST_PILOTS_PER_SF : 0) +
                       (size_t)(port / 2) * 4 * CHEST_MAX_NREF;
   const uint32_t fidx0 = (crs_v(port, 0) + a.cell_id % 6) % 6;
+  const bool     kept_noise = a.noise_alg != 0;  // PSS / EMPTY: the REFS residuals are not the estimate
 
   // ---- LS estimates at the CRS and RSRP / RSSI ----
   float rsrp = 0.f;
@@ -114,7 +169,9 @@ __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
 
   // ---- noise from the pilot residuals (REFS) ----
   float noise = 0.f;
-  if (nsym >= 3) {
+  if (kept_noise) {
+    noise = a.noise_in[rx * 4 + port];
+  } else if (nsym >= 3) {
     for (uint32_t i = 1; i < nsym - 1; i++) {
       const uint32_t off = ((fidx0 < 3) ^ (i & 1)) ? 0 : 1;
       const cx*      cur = pe + i * nref;
@@ -153,9 +210,11 @@ __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
     noise = block_sum(p, red) / (float)(nref - 2);
   }
 
-  // ---- time average into a 3-subcarrier comb, then smoothing (average_pilots) ----
+  // ---- time average into a 3-subcarrier comb (AVERAGE), then smoothing (average_pilots) ----
   uint32_t nr = nref;
-  if (nsym > 1) {
+  if (a.estimator == 1) {
+    // INTERPOLATE: every CRS symbol smoothed on its own (below)
+  } else if (nsym > 1) {
     for (uint32_t k = tid; k < nref; k += CH_THREADS) {
       cx e0 = pe[(fidx0 < 3 ? 0 : 1) * nref + k], e1 = pe[(fidx0 < 3 ? 1 : 0) * nref + k];
       for (uint32_t l = 2; l + 1 < nsym; l += 2) {
@@ -195,50 +254,82 @@ __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
       M = 0;  // srsran_conv_same_cf with an empty filter yields zeros
     }
   }
-  for (uint32_t i = tid; i < nr; i += CH_THREADS) {
-    cx acc = {0.f, 0.f};
-    for (uint32_t k = 0; k < M; k++) {
-      const int j = (int)i - (int)(M / 2) + (int)k;  // index into the extended sequence
-      cx        x;
-      if (j < 0) {  // first[]: (2 + M/2 - m) * in[1] - (1 + M/2 - m) * in[0], m = j + M/2
-        const uint32_t m = (uint32_t)(j + (int)(M / 2));
-        x = sub(scl(comb[1], (float)(2 + M / 2 - m)), scl(comb[0], (float)(1 + M / 2 - m)));
-      } else if (j >= (int)nr) {  // last[]: m = j - (nr - M + 1) counts into last[], i >= M - 1
-        const uint32_t m = (uint32_t)(j - (int)(nr - M + 1));
-        x = sub(scl(comb[nr - 1], (float)(2 + m - M / 2)), scl(comb[nr - 2], (float)(1 + m - M / 2)));
-      } else {
-        x = comb[j];
-      }
-      acc = add(acc, scl(x, filt[k]));
+  if (a.estimator == 1) {
+    for (uint32_t l = 0; l < nsym; l++) {
+      conv_row(pe + l * nref, avg + l * nref, nref, filt, M);
     }
-    avg[i] = acc;
+  } else {
+    conv_row(comb, avg, nr, filt, M);
   }
   __syncthreads();
 
-  // ---- linear interpolation to every subcarrier (interp_linear_offset) ----
+  // ---- interpolation to every subcarrier (interp_linear_offset) and, for INTERPOLATE, between the CRS
+  // symbols (interpolate_pilots, chest_dl.c:510-554); PSS noise on row nsymb - 1 (estimate_noise_pss) ----
   const uint32_t step = nsym > 1 ? 3 : 6;
   const uint32_t off  = nsym > 1 ? a.cell_id % 3 : fidx0;
-  const float    rM   = (float)1 / step;
+  const uint32_t ns   = a.nsymb, nrows = 2 * ns;
+  const bool     noise_sf = kept_noise && (sfi == 0 || sfi == 5);
+  const uint32_t kp   = nre / 2 - 31;  // PSS / SSS subcarriers kp .. kp + 61 of rows ns - 1 / ns - 2
   float2*        ce   = a.ce + b * a.ce_sf_stride + (size_t)(port * a.nrx + rx) * a.ce_stride;
+  float          pss_err = 0.f;
   for (uint32_t j = tid; j < nre; j += CH_THREADS) {
-    cx v;
-    if (j < off) {
-      const uint32_t jj = off - 1 - j;
-      v                 = sub(avg[0], divs(scl(sub(avg[1], avg[0]), (float)(jj + 1)), (float)step));
-    } else if (j < off + step * (nr - 1)) {
-      const uint32_t i = (j - off) / step, r = (j - off) % step;
-      v                = add(avg[i], scl(scl(sub(avg[i + 1], avg[i]), rM), (float)r));
-    } else {
-      const uint32_t r = j - off - step * (nr - 1);
-      v                = add(avg[nr - 1], divs(scl(sub(avg[nr - 1], avg[nr - 2]), (float)r), (float)step));
-    }
-    const float2 o = make_float2(v.r, v.i);
-    if (a.full_grid) {
-      for (uint32_t l = 0; l < 2 * a.nsymb; l++) {
-        ce[l * nre + j] = o;
+    if (a.estimator == 1) {
+      cx rows[14];
+      cx v[4];
+      for (uint32_t l = 0; l < nsym; l++) {
+        v[l] = interp_at(avg + l * nref, nref, 6, (crs_v(port, l) + a.cell_id % 6) % 6, j);
+      }
+      if (port < 2) {  // CRS rows 0, ns - 3, ns, 2 ns - 3
+        const uint32_t r1 = ns - 3, r2 = ns, r3 = 2 * ns - 3;
+        rows[0] = v[0], rows[r1] = v[1], rows[r2] = v[2], rows[r3] = v[3];
+        ivec(rows, v[0], v[1], nullptr, r1, r1 - 1, 1);
+        ivec(rows, v[1], v[2], nullptr, r2 - r1, r2 - r1 - 1, r1 + 1);
+        ivec(rows, v[2], v[3], nullptr, r3 - r2, r3 - r2 - 1, r2 + 1);
+        ivec(rows, v[2], v[3], &v[3], r3 - r2, nrows - 1 - r3, r3 + 1);
+      } else {  // CRS rows 1, ns + 1 (the reference fills rows ns + 2 .. from row 1 as well)
+        rows[1] = v[0], rows[ns + 1] = v[1];
+        ivec(rows, v[1], v[0], &v[0], ns, 1, 0);
+        ivec(rows, v[0], v[1], nullptr, ns, ns - 1, 2);
+        ivec(rows, v[0], v[1], nullptr, ns, ns - 2, ns + 2);
+      }
+      for (uint32_t l = 0; l < nrows; l++) {
+        ce[l * nre + j] = make_float2(rows[l].r, rows[l].i);
+      }
+      if (noise_sf && a.noise_alg == 1 && j >= kp && j < kp + 62) {
+        const cx t = sub(mul(rows[ns - 1], ld2(a.pss, j - kp)), ld2(in, (ns - 1) * nre + j));
+        pss_err += t.r * t.r + t.i * t.i;
       }
     } else {
-      ce[j] = o;
+      const cx     v = interp_at(avg, nr, step, off, j);
+      const float2 o = make_float2(v.r, v.i);
+      if (a.full_grid) {
+        for (uint32_t l = 0; l < nrows; l++) {
+          ce[l * nre + j] = o;
+        }
+      } else {
+        ce[j] = o;
+      }
+      if (noise_sf && a.noise_alg == 1 && j >= kp && j < kp + 62) {
+        const cx t = sub(mul(v, ld2(a.pss, j - kp)), ld2(in, (ns - 1) * nre + j));
+        pss_err += t.r * t.r + t.i * t.i;
+      }
+    }
+  }
+  if (noise_sf) {
+    if (a.noise_alg == 1) {  // nof_ports * srsran_vec_avg_power_cf(62) * M_SQRT1_2
+      noise = (float)a.nports * (block_sum(pss_err, red) / 62.0f) * (float)0.70710678118654752440;
+    } else {  // estimate_noise_empty_sc: 5 empty subcarriers either side of the SSS and of the PSS
+      const uint32_t base[4] = {(ns - 2) * nre + kp - 5, (ns - 2) * nre + kp + 62, (ns - 1) * nre + kp - 5,
+                                (ns - 1) * nre + kp + 62};
+      noise = 0.f;
+      for (int g = 0; g < 4; g++) {
+        float p = 0.f;
+        for (int k = 0; k < 5; k++) {
+          const cx x = ld2(in, base[g] + k);
+          p += x.r * x.r + x.i * x.i;
+        }
+        noise += p / 5.0f;
+      }
     }
   }
   if (tid == 0) {
@@ -248,6 +339,7 @@ __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
     s[2]     = rssi;
     s[3]     = cre;
     s[4]     = cim;
+    s[5]     = noise_sf ? 1.0f : 0.0f;
   }
 }
 
@@ -303,6 +395,99 @@ __global__ void chest_finalize_kernel(const float* stats, uint32_t np, uint32_t 
   o[1]     = best;
   o[2]     = rssi / (float)nrx;
   o[3]     = cfo;
+}
+
+// PSS / EMPTY over a batch: one thread walks the subframes in order, carrying each (rx, port)'s kept estimate
+__global__ void chest_keep_kernel(float* stats, uint32_t np, uint32_t nrx, float* state, uint32_t nsf)
+{
+  if (threadIdx.x != 0 || blockIdx.x != 0) {
+    return;
+  }
+  for (uint32_t b = 0; b < nsf; b++) {
+    float* st = stats + b * CHEST_STATS_PER_SF;
+    for (uint32_t rx = 0; rx < nrx; rx++) {
+      for (uint32_t p = 0; p < np; p++) {
+        float* v = st + (rx * np + p) * 8;
+        if (v[5] != 0.0f) {
+          state[rx * 4 + p] = v[0];
+        } else {
+          v[0] = state[rx * 4 + p];
+        }
+      }
+    }
+  }
+}
+
+hipError_t chest_finalize_kept_launch(float* stats, uint32_t np, uint32_t nrx, uint32_t nof_prb, float symbol_sz,
+                                      uint32_t nsymb, float* state, float* out, uint32_t nsf, hipStream_t stream)
+{
+  if (nsf == 0) {
+    return hipSuccess;
+  }
+  hipLaunchKernelGGL(chest_keep_kernel, dim3(1), dim3(64), 0, stream, stats, np, nrx, state, nsf);
+  return chest_finalize_launch(stats, np, nrx, nof_prb, symbol_sz, nsymb, out, nsf, stream);
+}
+
+// correct_sync_error's device part: one workgroup per (port, rx)
+__global__ __launch_bounds__(CH_THREADS) void chest_sync_kernel(ChestArgs a, float* out)
+{
+  __shared__ float red[CH_THREADS / 64];
+  const uint32_t   port = blockIdx.x / a.nrx, rx = blockIdx.x % a.nrx;
+  const uint32_t   nsym = port < 2 ? 4 : 2, nref = 2 * a.nof_prb, nre = 12 * a.nof_prb;
+  const float2*    in   = a.grid + (size_t)rx * 2 * a.nsymb * nre;
+  const float2*    pil  = a.pilots + (size_t)(port / 2) * 4 * CHEST_MAX_NREF;
+  float*           o    = out + (rx * 4 + port) * 10;
+  float            pwr  = 0.f;
+  for (uint32_t l = 0; l < nsym; l++) {
+    const uint32_t row = crs_nsymbol(l, port, a.nsymb) * nre, f0 = (crs_v(port, l) + a.cell_id % 6) % 6;
+    float          sr = 0.f, si = 0.f;
+    for (uint32_t i = threadIdx.x; i < nref; i += CH_THREADS) {
+      const cx x = mul(ld2(in, row + f0 + 6 * i), conj(ld2(pil, l * nref + i)));
+      pwr += x.r * x.r + x.i * x.i;
+      if (i > 0) {  // x[i] conj(x[i - 1])
+        const cx y = mul(ld2(in, row + f0 + 6 * (i - 1)), conj(ld2(pil, l * nref + i - 1)));
+        const cx t = mul(x, conj(y));
+        sr += t.r;
+        si += t.i;
+      }
+    }
+    sr = block_sum(sr, red);
+    si = block_sum(si, red);
+    if (threadIdx.x == 0) {
+      o[2 * l]     = sr;
+      o[2 * l + 1] = si;
+    }
+  }
+  pwr = block_sum(pwr, red);
+  if (threadIdx.x == 0) {
+    o[8] = pwr;
+  }
+}
+
+hipError_t chest_sync_sums_launch(const ChestArgs& a, float* out, hipStream_t stream)
+{
+  hipLaunchKernelGGL(chest_sync_kernel, dim3(a.nports * a.nrx), dim3(CH_THREADS), 0, stream, a, out);
+  return hipGetLastError();
+}
+
+// srsran_vec_apply_cfo's product (simd.h:898-901): re = fma(x.re, p.re, -(x.im p.im)), im = fma(x.re, p.im, x.im p.re)
+__global__ void grid_rotate_kernel(float2* grid, const float2* __restrict__ tab, uint32_t nre, uint32_t total)
+{
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < total) {
+    const float2 x = grid[k], p = tab[k % nre];
+    grid[k] = make_float2(__fmaf_rn(x.x, p.x, -__fmul_rn(x.y, p.y)), __fmaf_rn(x.x, p.y, __fmul_rn(x.y, p.x)));
+  }
+}
+
+hipError_t grid_rotate_launch(float2* grid, const float2* tab, uint32_t nre, uint32_t nrows, hipStream_t stream)
+{
+  const uint32_t total = nre * nrows;
+  if (total == 0) {
+    return hipSuccess;
+  }
+  hipLaunchKernelGGL(grid_rotate_kernel, dim3((total + 255) / 256), dim3(256), 0, stream, grid, tab, nre, total);
+  return hipGetLastError();
 }
 
 hipError_t chest_finalize_launch(const float* stats, uint32_t np, uint32_t nrx, uint32_t nof_prb, float symbol_sz,

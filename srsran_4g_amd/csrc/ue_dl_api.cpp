@@ -29,6 +29,7 @@ struct UeDlGpu {
   float2*    d_ce   = nullptr;
   float*     d_res  = nullptr;
   uint32_t   cap    = 0;  // subframes
+  bool       cap_full = false;  // d_ce sized for full-grid (INTERPOLATE) estimates
   // control channels (srsran_ue_dl_t::regs / pcfich / pdcch of the reference)
   srsran_regs_t         regs{};
   srsran_pcfich_t       pcfich{};
@@ -57,9 +58,9 @@ void select_mi(UeDlGpu* g)
   }
 }
 
-bool grow(srsran_ue_dl_t* q, UeDlGpu* g, uint32_t nsf)
+bool grow(srsran_ue_dl_t* q, UeDlGpu* g, uint32_t nsf, bool full)
 {
-  if (g->cap >= nsf) {
+  if (g->cap >= nsf && (g->cap_full || !full)) {
     return true;
   }
   hipDeviceSynchronize();
@@ -76,20 +77,16 @@ bool grow(srsran_ue_dl_t* q, UeDlGpu* g, uint32_t nsf)
   if (hipHostMalloc((void**)&g->h_sf, nsf * sizeof(uint32_t)) != hipSuccess ||
       hipMalloc((void**)&g->d_sf, nsf * sizeof(uint32_t)) != hipSuccess ||
       hipMalloc((void**)&g->d_grid, nsf * nrx * 14 * nre * sizeof(float2)) != hipSuccess ||
-      hipMalloc((void**)&g->d_ce, nsf * ports * nrx * nre * sizeof(float2)) != hipSuccess ||
+      hipMalloc((void**)&g->d_ce, nsf * ports * nrx * nre * (full ? 14 : 1) * sizeof(float2)) != hipSuccess ||
       hipMalloc((void**)&g->d_res, nsf * 4 * sizeof(float)) != hipSuccess) {
     return false;
   }
-  g->cap = nsf;
+  g->cap      = nsf;
+  g->cap_full = full;
   return true;
 }
 
-bool srsue_chest_cfg(const srsran_chest_dl_cfg_t& c)
-{
-  return c.estimator_alg == SRSRAN_ESTIMATOR_ALG_AVERAGE && c.noise_alg == SRSRAN_NOISE_ALG_REFS &&
-         c.filter_type == SRSRAN_CHEST_FILTER_GAUSS && c.filter_coef[0] == 4.0f && c.filter_coef[1] == 1.0f &&
-         !c.sync_error_enable && !c.rsrp_neighbour;
-}
+
 
 }  // namespace
 
@@ -305,15 +302,12 @@ int srsran_ue_dl_gpu_decode_batch(srsran_ue_dl_t*              q,
   if (nof_sf == 0) {
     return 0;
   }
-  if (!srsue_chest_cfg(cfg->chest_cfg)) {
-    fprintf(stderr, "[srsran_ue_dl] the batch path runs srsUE's default channel estimator configuration only\n");
-    return SRSRAN_ERROR;
-  }
   srsran_amd::HostScope whole(srsran_amd::HP_UE_DL);
   srsran_amd::HostScope front(srsran_amd::HP_FRONT);
-  UeDlGpu*    g = (UeDlGpu*)q->gpu;
-  hipStream_t s = (hipStream_t)stream;
-  if (!grow(q, g, nof_sf) || hipEventSynchronize(g->staged) != hipSuccess) {
+  UeDlGpu*    g    = (UeDlGpu*)q->gpu;
+  hipStream_t s    = (hipStream_t)stream;
+  const bool  full = cfg->chest_cfg.estimator_alg == SRSRAN_ESTIMATOR_ALG_INTERPOLATE;  // every symbol its own row
+  if (!grow(q, g, nof_sf, full) || hipEventSynchronize(g->staged) != hipSuccess) {
     return SRSRAN_ERROR;
   }
   for (uint32_t b = 0; b < nof_sf; b++) {
@@ -324,8 +318,9 @@ int srsran_ue_dl_gpu_decode_batch(srsran_ue_dl_t*              q,
   const size_t nre = 12 * (size_t)q->cell.nof_prb, nrx = q->nof_rx_antennas, np = q->cell.nof_ports;
   const size_t rows = 2 * SRSRAN_CP_NSYMB(q->cell.cp);  // grid symbols per subframe
   if (srsran_ofdm_rx_gpu(&q->fft[0], d_samples, (cf_t*)g->d_grid, (uint32_t)nrx, nof_sf, cfo, stream) ||
-      srsran_chest_dl_gpu_estimate_batch(&q->chest, g->d_sf, nof_sf, (const cf_t*)g->d_grid, nrx * rows * nre,
-                                         (cf_t*)g->d_ce, np * nrx * nre, g->d_res, stream)) {
+      srsran_chest_dl_gpu_estimate_batch_cfg(&q->chest, &cfg->chest_cfg, g->d_sf, nof_sf, (const cf_t*)g->d_grid,
+                                             nrx * rows * nre, (cf_t*)g->d_ce, np * nrx * nre * (full ? rows : 1),
+                                             full ? 1 : 0, g->d_res, stream)) {
     return SRSRAN_ERROR;
   }
   front.stop();
@@ -337,8 +332,8 @@ int srsran_ue_dl_gpu_decode_batch(srsran_ue_dl_t*              q,
     f.tti     = sfs[b].tti;
     f.cfi     = sfs[b].cfi;
     f.d_grid  = (const cf_t*)(g->d_grid + b * nrx * rows * nre);
-    f.d_ce    = (const cf_t*)(g->d_ce + b * np * nrx * nre);
-    f.ce_full = 0;
+    f.d_ce    = (const cf_t*)(g->d_ce + b * np * nrx * nre * (full ? rows : 1));
+    f.ce_full = full ? 1 : 0;
     f.d_noise = g->d_res + 4 * b;
     for (int t = 0; t < SRSRAN_MAX_CODEWORDS; t++) {
       f.d_payload[t] = sfs[b].d_payload[t];

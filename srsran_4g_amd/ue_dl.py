@@ -216,6 +216,17 @@ def srsue_chest_cfg():
     return c
 
 
+def chest_cfg(estimator=0, noise_alg=0, filter_order=4, filter_std=1.0, sync_error=False):
+    """srsran_chest_dl_cfg_t with srsUE's ue.conf knobs (phy_common.cc:83-108): interpolate_subframe_enabled
+    (estimator 1 INTERPOLATE), snr_estim_alg (noise_alg 0 refs / 1 pss / 2 empty), estimator_fil_order /
+    _stddev (order 0 = estimator_fil_auto), correct_sync_error"""
+    c = srsue_chest_cfg()
+    c.estimator_alg, c.noise_alg = estimator, noise_alg
+    c.filter_coef[0], c.filter_coef[1] = filter_order, filter_std
+    c.sync_error_enable = bool(sync_error)
+    return c
+
+
 class OfdmRx:
     """srsran_ofdm_t receiver (srsran_ue_dl configuration)."""
 

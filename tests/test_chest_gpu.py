@@ -79,3 +79,125 @@ def test_chest_zero_cfg_auto_filter(U, ora):
     err = np.abs(ce[:, :, :1200] - H) ** 2
     assert err.mean() < 0.05
     ch.free()
+
+
+def _doppler_subframe(ora, rng, nof_prb, cell_id, nports, nrx, sf_idx, snr_db=25, fd=0.02, delay=0.0, N=2048):
+    """make_subframe with a channel that rotates over the subframe (phase 2 pi fd per symbol, so INTERPOLATE has
+    something to follow) and, with `delay`, a timing error of `delay` samples (a phase ramp over the subcarriers
+    that correct_sync_error detects from the CRS)"""
+    Y, H, X = make_subframe(ora, rng, nof_prb=nof_prb, cell_id=cell_id, nports=nports, nrx=nrx, sf_idx=sf_idx,
+                            snr_db=snr_db)
+    nre = 12 * nof_prb
+    Y = Y.reshape(nrx, 14, nre) * np.exp(2j * np.pi * fd * np.arange(14))[None, :, None]
+    if delay:
+        Y = Y * np.exp(-2j * np.pi * delay * np.arange(nre) / N)[None, None, :]
+    return Y.reshape(nrx, 14 * nre).astype(np.complex64)
+
+
+OPT_CASES = [
+    # (name, nof_prb, cell_id, nports, nrx, estimator, noise_alg, order, std)
+    ("interp_2port", 100, 1, 2, 2, 1, 0, 4, 1.0),
+    ("interp_1port_order6", 50, 7, 1, 1, 1, 0, 6, 2.0),
+    ("interp_4port", 25, 301, 4, 2, 1, 0, 4, 1.0),
+    ("interp_auto_filter", 100, 4, 2, 2, 1, 0, 0, 0.0),
+    ("average_pss", 100, 11, 2, 2, 0, 1, 4, 1.0),
+    ("interp_pss", 50, 2, 2, 1, 1, 1, 4, 1.0),
+    ("average_empty", 100, 5, 2, 2, 0, 2, 4, 1.0),
+    ("interp_empty_4port", 6, 3, 4, 1, 1, 2, 2, 1.0),
+    ("average_pss_auto", 25, 9, 1, 2, 0, 1, 0, 0.0),
+]
+
+
+@pytest.mark.parametrize("case", OPT_CASES, ids=[c[0] for c in OPT_CASES])
+def test_chest_options_match_oracle(U, ora, case):
+    """srsUE's non-default estimator knobs (ue.conf interpolate_subframe_enabled, snr_estim_alg,
+    estimator_fil_order / _stddev / _auto; chest_dl.c:437-555, 402-433, 655-745) against the oracle's
+    restatement (oracle_chest_dl_ext), over a sequence of subframes on one object so that PSS / EMPTY noise is
+    estimated in subframes 0 / 5 and kept in the others (q->noise_estimate, also the automatic filter's input)"""
+    name, nof_prb, cell_id, nports, nrx, est, noise, order, std = case
+    rng = np.random.default_rng(len(name) + nof_prb)
+    N = U.lib().srsran_symbol_sz(nof_prb)
+    ch = U.ChestDl(U.cell(nof_prb, nports, cell_id), nrx)
+    cfg = U.chest_cfg(est, noise, order, std)
+    state = np.zeros((4, 4), np.float32)
+    for tti in (4, 5, 6, 10, 11):
+        sf = tti % 10
+        Y = _doppler_subframe(ora, rng, nof_prb, cell_id, nports, nrx, sf, N=N)
+        ce, res = ch.estimate(Y.copy(), tti, cfg)
+        ceo, st, _, state = ora.chest_dl_ext(Y, nof_prb, cell_id, nports, sf, N, 0, est, noise, order, std,
+                                             noise_state=state)
+        scale = np.abs(ceo).max()
+        assert np.abs(ce - ceo).max() < 2e-5 * scale, (tti, np.abs(ce - ceo).max() / scale)
+        assert res.noise_estimate == pytest.approx(st["noise"], rel=1e-4), tti
+        assert res.rsrp == pytest.approx(st["rsrp"], rel=1e-4), tti
+        for r in range(nrx):
+            for p in range(nports):
+                assert ch.q.noise_estimate[r][p] == pytest.approx(state[r, p], rel=1e-4), (tti, r, p)
+    ch.free()
+
+
+@pytest.mark.parametrize("delay,nports", [(0.4, 2), (-0.7, 1), (0.01, 2), (1.3, 4)])
+def test_chest_sync_error_correction(U, ora, delay, nports):
+    """correct_sync_error (chest_dl.c:750-804): the timing error estimated from the CRS phase slope of every
+    port, and where it exceeds 0.05 samples every symbol of the grid rotated by srsran_vec_apply_cfo -- in the
+    caller's buffer, as the reference corrects it in place -- before the estimate; res.sync_error"""
+    nof_prb, cell_id, nrx = 50, 13, 2
+    rng = np.random.default_rng(int(100 * abs(delay)) + nports)
+    N = U.lib().srsran_symbol_sz(nof_prb)
+    ch = U.ChestDl(U.cell(nof_prb, nports, cell_id), nrx)
+    cfg = U.chest_cfg(0, 0, 4, 1.0, sync_error=True)
+    Y = _doppler_subframe(ora, rng, nof_prb, cell_id, nports, nrx, 2, fd=0.0, delay=delay, N=N)
+    grids = [Y[r].copy() for r in range(nrx)]
+    ce, res = ch.estimate(grids, 2, cfg)
+    ceo, st, Yo, _ = ora.chest_dl_ext(Y, nof_prb, cell_id, nports, 2, N, 0, 0, 0, 4, 1.0, sync=True)
+    assert res.sync_error == pytest.approx(st["sync_error"], rel=1e-4, abs=1e-6)
+    if abs(delay) > 0.1:
+        assert abs(st["sync_error"]) > 0.05
+    for r in range(nrx):  # the corrected grid is written back (or left alone below the threshold)
+        assert np.abs(grids[r] - Yo[r]).max() < 1e-5 * np.abs(Yo).max(), r
+    assert np.abs(ce - ceo).max() < 2e-5 * np.abs(ceo).max()
+    ch.free()
+
+
+@pytest.mark.parametrize("est,noise", [(1, 0), (0, 1), (1, 2)])
+def test_ue_dl_batch_estimator_options(U, ora, est, noise):
+    """srsran_ue_dl_gpu_decode_batch with INTERPOLATE / PSS / EMPTY in cfg->chest_cfg decodes and equals the
+    host-synchronous UE DL path subframe by subframe (kept noise carried across the batch in subframe order)"""
+    from synth import synth as S
+    from srsran_4g_amd import sch as SCH
+    TBS = 75376
+    ue = U.UeDl(U.cell(100, 2, 1), 2)
+    ue.cfg.chest_cfg = U.chest_cfg(est, noise)
+    ue2 = U.UeDl(U.cell(100, 2, 1), 2)
+    ue2.cfg.chest_cfg = U.chest_cfg(est, noise)
+    rng = np.random.default_rng(40 + est + 3 * noise)
+    ttis = (4, 5, 6, 10)
+    samples, entries, keep, pls_all = [], [], [], []
+    d_pl = torch.zeros((len(ttis), 2, TBS // 8 + 64), dtype=torch.uint8, device="cuda")
+    for b, tti in enumerate(ttis):
+        pls = [rng.integers(0, 256, TBS // 8, dtype=np.uint8) for _ in range(2)]
+        x, nre = S.pdsch_subframe(100, 1, 2, tti, 1, 0x1234, TBS, 6, 0, pls, snr_db=30.0, rng=rng, N=2048)
+        sb = [SCH.SoftbufferRx(nof_prb=100) for _ in range(2)]
+        cfg = U.pdsch_cfg(100, nre, (TBS, TBS), (6, 6), softbuffers=sb)
+        keep += [sb, cfg]
+        samples.append(x)
+        pls_all.append(pls)
+        entries.append((tti, 1, cfg, [d_pl[b, 0].data_ptr(), d_pl[b, 1].data_ptr()], [1, 1]))
+    d_x = torch.from_numpy(np.stack(samples).view(np.float32)).cuda()
+    d_res = torch.full((2 * len(ttis),), 7, dtype=torch.int32, device="cuda")
+    d_avg = torch.zeros(2 * len(ttis), dtype=torch.float32, device="cuda")
+    assert ue.gpu_decode_batch(entries, d_x.data_ptr(), d_res.data_ptr(), d_avg.data_ptr(), 0.0, None) == 2 * len(ttis)
+    torch.cuda.synchronize()
+    res, pl = d_res.cpu().numpy(), d_pl.cpu().numpy()
+    for b, tti in enumerate(ttis):
+        assert ue2.fft_estimate(samples[b], tti, 1) == 0
+        sb = [SCH.SoftbufferRx(nof_prb=100) for _ in range(2)]
+        cfg = U.pdsch_cfg(100, entries[b][2].grant.nof_re, (TBS, TBS), (6, 6), softbuffers=sb)
+        ret, out = ue2.decode_pdsch(cfg, tti, 1)
+        keep.append(sb)
+        for q in range(2):
+            assert res[2 * b + q] == 0 and out[q][0], (b, q)
+            assert np.array_equal(pl[b, q, : TBS // 8], pls_all[b][q])
+            assert np.array_equal(pl[b, q, : TBS // 8 + 6], out[q][1][: TBS // 8 + 6])
+    ue.free()
+    ue2.free()

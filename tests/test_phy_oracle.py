@@ -215,3 +215,41 @@ def test_gauss_filter_and_conv_same_match_reference():
         fo.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_uint32] * 2
         fo(x.ctypes.data, f.ctypes.data, yo.ctypes.data, N, f.size)
         assert np.allclose(yo, yr, rtol=1e-5, atol=1e-6), N  # SIMD dot products sum in a different order
+
+
+def test_sync_error_pieces_vs_reference():
+    """the pieces of correct_sync_error (chest_dl.c:750-804) in the oracle against the reference compiled into
+    _ref: srsran_vec_apply_cfo bit for bit (its phasor recurrence and FMA roundings) and
+    srsran_vec_estimate_frequency within float summation order"""
+    import ctypes
+    import os
+    from oracle import ref_available
+    if not ref_available():
+        pytest.skip("oracle/_ref not built")
+    here = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle")
+    R = ctypes.CDLL(os.path.join(here, "_ref", "libsrsref.so"), mode=os.RTLD_LAZY)
+    L = ctypes.CDLL(os.path.join(here, "liboracle.so"))
+    R.srsran_vec_apply_cfo.argtypes = [ctypes.c_void_p, ctypes.c_float, ctypes.c_void_p, ctypes.c_int]
+    R.srsran_vec_estimate_frequency.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    R.srsran_vec_estimate_frequency.restype = ctypes.c_float
+    L.oracle_apply_cfo.argtypes = [ctypes.c_void_p, ctypes.c_float, ctypes.c_void_p, ctypes.c_uint32]
+    L.oracle_estimate_frequency.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+    L.oracle_estimate_frequency.restype = ctypes.c_float
+    rng = np.random.default_rng(12)
+
+    def aligned(n):
+        b = np.zeros(n + 8, np.complex64)
+        o = (-(b.ctypes.data // 8)) % 4
+        return b[o:o + n]
+    for n in (1200, 600, 300, 72, 13):
+        for f in (1e-3, -2.5e-4, 0.01, 2e-4 / 6):
+            x = aligned(n)
+            x[:] = rng.standard_normal(n) + 1j * rng.standard_normal(n)
+            z1, z2 = aligned(n), aligned(n)
+            L.oracle_apply_cfo(x.ctypes.data, f, z1.ctypes.data, n)
+            R.srsran_vec_apply_cfo(x.ctypes.data, f, z2.ctypes.data, n)
+            assert np.array_equal(z1.view(np.uint32), z2.view(np.uint32)), (n, f)
+        y = aligned(n)
+        y[:] = np.exp(2j * np.pi * 0.013 * np.arange(n)) * (1 + 0.1 * rng.standard_normal(n))
+        a, b = L.oracle_estimate_frequency(y.ctypes.data, n), R.srsran_vec_estimate_frequency(y.ctypes.data, n)
+        assert a == pytest.approx(b, rel=1e-5, abs=1e-7), n

@@ -97,7 +97,7 @@ def test_ofdm_gpu_batch_with_cfo(U, ref_cfo, f):
                                           ctypes.c_float(ff), None) == 0
     torch.cuda.synchronize()
     got = d_out.cpu().numpy().view(np.complex64).reshape(nsf, nrx, 14 * nre)
-    assert np.abs(got - grids).max() < 2e-4
+    assert np.abs(got - grids).max() < 2e-3  # the reference's phasor drift, up to ~1e-3 by the end of a subframe
     want = np.stack([np.stack([ofdm_np.ofdm_rx(ref_cfo(x[s, r], f), 2048, nre) for r in range(nrx)])
                      for s in range(nsf)])
     assert np.abs(got - want).max() < 2e-5 * np.abs(want).max() * 11

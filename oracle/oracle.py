@@ -134,6 +134,28 @@ class _PhyMixin:
         f(_ptr(x, _i16p), _ptr(out, _i16p), len(llr), seed)
         return out.copy()
 
+    def demod_b(self, mod, sym):
+        """int8 soft demapping (srsran_demod_soft_demodulate_b) of complex64 symbols."""
+        sym = np.asarray(sym, dtype=np.complex64)
+        x = aligned(sym.size, np.complex64)
+        x[:] = sym
+        out = aligned(sym.size * (1, 2, 4, 6, 8)[mod], np.int8)
+        f = self._demod_b_fn()
+        f.argtypes = [ctypes.c_int, ctypes.c_void_p, _i8p, ctypes.c_int]
+        if f(mod, x.ctypes.data_as(ctypes.c_void_p), _ptr(out, _i8p), sym.size):
+            raise ValueError(mod)
+        return out.copy()
+
+    def sequence_apply_c(self, llr, seed):
+        """int8 descrambling (srsran_sequence_apply_c)."""
+        x = aligned(len(llr), np.int8)
+        x[:] = llr
+        out = aligned(len(llr), np.int8)
+        f = self._seq_c_fn()
+        f.argtypes = [_i8p, _i8p, ctypes.c_uint32, ctypes.c_uint32]
+        f(_ptr(x, _i8p), _ptr(out, _i8p), len(llr), seed)
+        return out.copy()
+
 
 class Oracle(_Lib, _PhyMixin):
     """The repo's C restatement."""
@@ -147,6 +169,20 @@ class Oracle(_Lib, _PhyMixin):
         f = self.lib.oracle_sequence_apply_s
         f.argtypes = [_i16p, _i16p, ctypes.c_uint32, ctypes.c_uint32]
         return f
+
+    def _demod_b_fn(self):
+        return self.lib.oracle_demod_soft_b
+
+    def _seq_c_fn(self):
+        return self.lib.oracle_sequence_apply_c
+
+    def csi_correction_b(self, mod, csi, e):
+        e = np.array(e, dtype=np.int8, copy=True)
+        csi = np.ascontiguousarray(csi, dtype=np.float32)
+        f = self.lib.oracle_csi_correction_b
+        f.argtypes = [ctypes.c_int, ctypes.c_void_p, _i8p, ctypes.c_uint32]
+        f(mod, csi.ctypes.data, _ptr(e, _i8p), e.size)
+        return e
 
     def _predecode(self, scheme, ya, ha, xa, ca, nrx, nports, nlayers, codebook, n, scaling, noise):
         f = self.lib.oracle_predecode
@@ -333,6 +369,24 @@ class Oracle(_Lib, _PhyMixin):
         return _dlsch_decode(self.lib.oracle_dlsch_decode_tb, self.cbsegm(tbs)[1], tbs, Qm, rv, e_llr,
                              max_iterations, state)
 
+    def dlsch_decode8(self, tbs, Qm, rv, e_llr, max_iterations, state=None):
+        """decode_tb with llr_is_8bit (sch.c:409-428): int8 e bits; soft buffer rows hold int8 LLRs in the 8-bit
+        decoder's layout.  Same returns as dlsch_decode."""
+        self._sch_sigs()
+        return _dlsch_decode(self.lib.oracle_dlsch_decode_tb8, self.cbsegm(tbs)[1], tbs, Qm, rv, e_llr,
+                             max_iterations, state, llr8=True)
+
+    def tdec8_run(self, K, llr, nof_iterations=8, trace=False):
+        """C restatement of the 8-bit window decoders (nsb 16 / 32, SB layout input)."""
+        f = self.lib.oracle_tdec8_run
+        f.argtypes = [ctypes.c_uint32, _i8p, ctypes.c_uint32, _u8p, _i8p]
+        llr = np.ascontiguousarray(llr, dtype=np.int8)
+        out = np.zeros(K // 8, dtype=np.uint8)
+        tr = np.zeros((nof_iterations, K), dtype=np.int8) if trace else None
+        if f(K, _ptr(llr, _i8p), nof_iterations, _ptr(out, _u8p), _ptr(tr, _i8p) if trace else None):
+            raise ValueError(K)
+        return (out, tr) if trace else out
+
     def run_batch(self, K, llr2d, layout_sb, nof_iterations):
         llr2d = np.ascontiguousarray(llr2d, dtype=np.int16)
         n = llr2d.shape[0]
@@ -344,19 +398,20 @@ class Oracle(_Lib, _PhyMixin):
         return out
 
 
-def _dlsch_decode(fn, segm, tbs, Qm, rv, e_llr, max_iterations, state):
+def _dlsch_decode(fn, segm, tbs, Qm, rv, e_llr, max_iterations, state, llr8=False):
     C = max(1, segm["C"])
     if state is None:
         state = (np.zeros((C, SOFTBUF_LEN), np.int16), np.zeros(C, np.uint8), np.zeros((C, 768), np.uint8))
     sb, crc, cbd = state
-    e_llr = np.ascontiguousarray(e_llr, dtype=np.int16)
+    ep = _i8p if llr8 else _i16p
+    e_llr = np.ascontiguousarray(e_llr, dtype=np.int8 if llr8 else np.int16)
     data = np.zeros(tbs // 8 + 8, dtype=np.uint8)
     noi = (ctypes.c_uint32 * C)()
     avg = ctypes.c_float(0)
     u32 = ctypes.c_uint32
-    fn.argtypes = [u32, u32, u32, u32, _i16p, u32, _i16p, u32, _u8p, _u8p, u32, _u8p, ctypes.POINTER(u32),
+    fn.argtypes = [u32, u32, u32, u32, ep, u32, _i16p, u32, _u8p, _u8p, u32, _u8p, ctypes.POINTER(u32),
                    ctypes.POINTER(ctypes.c_float)]
-    ret = fn(tbs, Qm, rv, e_llr.size, _ptr(e_llr, _i16p), max_iterations, _ptr(sb, _i16p), sb.shape[1],
+    ret = fn(tbs, Qm, rv, e_llr.size, _ptr(e_llr, ep), max_iterations, _ptr(sb, _i16p), sb.shape[1],
              _ptr(crc, _u8p), _ptr(cbd, _u8p), cbd.shape[1], _ptr(data, _u8p), noi, ctypes.byref(avg))
     return ret, data, list(noi), avg.value, state
 
@@ -405,6 +460,36 @@ class Reference(_Lib, _PhyMixin):
         ca[0] = cb[0][:n]
         ca[1] = cb[1][:n]
         return rc
+
+    def _demod_b_fn(self):
+        return self.lib.srsran_demod_soft_demodulate_b
+
+    def _seq_c_fn(self):
+        return self.lib.srsran_sequence_apply_c
+
+    def csi_correction(self, mod, csi, e, llr8=False):
+        """csi_correction (pdsch.c:523-618) restated in ref_pdsch_tx_harness.c and built with the reference's
+        flags; e int16 (int8 with llr8) LLRs of one codeword, csi nof_bits / Qm values."""
+        dt = np.int8 if llr8 else np.int16
+        ea = aligned(len(e) + 16, dt)
+        ea[:len(e)] = e
+        ca = aligned(len(csi) + 8, np.float32)
+        ca[:len(csi)] = csi
+        f = self.lib.ref_csi_correction
+        f.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int]
+        f(mod, ca.ctypes.data, ea.ctypes.data, len(e), 1 if llr8 else 0)
+        return ea[:len(e)].copy()
+
+    def evm_b(self, mod, sym, llr, nof_bits, max_bits):
+        """srsran_evm_run_b (evm.h) on int8 demodulated LLRs."""
+        s = aligned(len(sym) + 8, np.complex64)
+        s[:len(sym)] = sym
+        l = aligned(len(llr) + 16, np.int8)
+        l[:len(llr)] = llr
+        f = self.lib.ref_evm_run_b
+        f.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32]
+        f.restype = ctypes.c_float
+        return f(mod, s.ctypes.data, l.ctypes.data, nof_bits, max_bits)
 
     def sequence_pdsch_apply_s(self, llr, rnti, q, nslot, cell_id):
         x = aligned(len(llr), np.int16)
@@ -478,6 +563,11 @@ class Reference(_Lib, _PhyMixin):
         """decode_tb glue over the reference's rm_turbo / turbo decoder / CRC (ref_harness.c)."""
         return _dlsch_decode(self.lib.ref_dlsch_decode_tb, self.cbsegm(tbs)[1], tbs, Qm, rv, e_llr,
                              max_iterations, state)
+
+    def dlsch_decode8(self, tbs, Qm, rv, e_llr, max_iterations, state=None):
+        """decode_tb glue over the reference's 8-bit rate de-matching and decoders (ref_dlsch_decode_tb8)."""
+        return _dlsch_decode(self.lib.ref_dlsch_decode_tb8, self.cbsegm(tbs)[1], tbs, Qm, rv, e_llr,
+                             max_iterations, state, llr8=True)
 
     def rm_turbo_rx(self, cb_idx, rv, e, softbuf):
         """srsran_rm_turbo_rx_lut (SB layout for window decoders, as the reference build)."""

@@ -465,10 +465,153 @@ void oracle_csi_correction(int mod, const float* csi, int16_t* e, uint32_t nof_b
     default:
       break;
   }
+  /* the release build (-Ofast: -freciprocal-math) hoists 1 / csi_max out of the loop and multiplies */
+  const float rcp = 1.0f / mx;
   for (uint32_t k = (uint32_t)(i / qm); k < ns; k++) {
-    const float c = csi[k] / mx;
+    const float c = csi[k] * rcp;
     for (uint32_t b = 0; b < qm; b++) {
       e[qm * k + b] = wrap16(cvt_tz((float)e[qm * k + b] * c));
+    }
+  }
+}
+
+/* ======================= 8-bit LLR chain (pdsch.c:691-737 with q->llr_is_8bit) =======================
+ *   oracle_demod_soft_b      srsran_demod_soft_demodulate_b (demod_soft.c:896-919), x86 SSE build:
+ *                            - BPSK  demod_bpsk_lte_b (demod_soft.c:89-94): scalar, truncating
+ *                            - QPSK  demod_qpsk_lte_b -> srsran_vec_convert_fb_simd (vector_simd.c:524-589):
+ *                                    16-value SSE blocks truncate + saturate (packs_epi32, packs_epi16), the tail
+ *                                    truncates + wraps
+ *                            - 16QAM demod_16qam_lte_b_sse (demod_soft.c:301-364): 8-symbol blocks round half-even +
+ *                                    saturate to int8; abs_epi8 / sub_epi8 wrap (|-128| = -128, offset (int8)18.97);
+ *                                    the tail truncates and subtracts the float offset
+ *                            - 64QAM demod_64qam_lte_b_sse (demod_soft.c:650-730): same split, offsets 24 and 12
+ *                            - 256QAM demod_256qam_lte_b (demod_soft.c:800-822): scalar float, truncating
+ *   oracle_sequence_apply_c  srsran_sequence_state_apply_c (sequence.c:563-618): LLR negated (int8 wrap)
+ *   oracle_csi_correction_b  csi_correction's llr_is_8bit branch (pdsch.c:538-545): (int8)((float)e * csi[i] /
+ *                            csi_max), the division turned into a multiply by 1 / csi_max as -Ofast builds it
+ * Pinned against _ref (demod / sequence compiled from the reference; csi_correction restated in
+ * ref_pdsch_tx_harness.c and built with the reference's flags), tests/test_phy_oracle.py. */
+static int8_t sat8(int32_t v) { return v > 127 ? 127 : (v < -128 ? -128 : (int8_t)v); }
+static int8_t wrap8(int32_t v) { return (int8_t)(uint8_t)(uint32_t)v; }
+static int8_t abs8(int8_t v) { return wrap8(v < 0 ? -(int32_t)v : (int32_t)v); } /* _mm_abs_epi8 */
+
+int oracle_demod_soft_b(int mod, const float* sym, int8_t* llr, int n)
+{
+  switch (mod) {
+    case 0: /* BPSK */
+      for (int i = 0; i < n; i++) {
+        const float t = -20.0f * (sym[2 * i] + sym[2 * i + 1]);
+        llr[i]        = wrap8(cvt_tz_d((double)t * 0.70710678118654752440));
+      }
+      return 0;
+    case 1: { /* QPSK: scale = (float)(-20 * M_SQRT2) */
+      const float scale = (float)(-20.0 * 1.41421356237309504880);
+      const int   len   = 2 * n;
+      int         i     = 0;
+      for (; i + 16 <= len; i += 16) {
+        for (int k = 0; k < 16; k++) {
+          llr[i + k] = sat8(cvt_tz(sym[i + k] * scale));
+        }
+      }
+      for (; i < len; i++) {
+        llr[i] = wrap8(cvt_tz(sym[i] * scale));
+      }
+      return 0;
+    }
+    case 2: { /* 16QAM */
+      const int8_t off  = (int8_t)(2 * 30 / sqrtf(10));
+      const float  offf = 2 * 30 / sqrtf(10);
+      const int    nsse = 8 * (n / 8);
+      for (int i = 0; i < n; i++) {
+        for (int c = 0; c < 2; c++) {
+          const float x = sym[2 * i + c];
+          if (i < nsse) {
+            const int8_t s  = sat8(cvt_rn(x * -30.0f));
+            llr[4 * i + c]     = s;
+            llr[4 * i + 2 + c] = wrap8(abs8(s) - off);
+          } else {
+            const int8_t y  = wrap8(cvt_tz(30.0f * x));
+            llr[4 * i + c]     = wrap8(-(int32_t)y);
+            llr[4 * i + 2 + c] = wrap8(cvt_tz((float)abs(y) - offf));
+          }
+        }
+      }
+      return 0;
+    }
+    case 3: { /* 64QAM */
+      const int8_t off1 = (int8_t)(4 * 40 / sqrtf(42));
+      const int8_t off2 = (int8_t)(2 * 40 / sqrtf(42));
+      const int    nsse = 8 * (n / 8);
+      for (int i = 0; i < n; i++) {
+        for (int c = 0; c < 2; c++) {
+          const float x = sym[2 * i + c];
+          if (i < nsse) {
+            const int8_t s = sat8(cvt_rn(x * -40.0f));
+            const int8_t a = wrap8(abs8(s) - off1);
+            llr[6 * i + c]     = s;
+            llr[6 * i + 2 + c] = a;
+            llr[6 * i + 4 + c] = wrap8(abs8(a) - off2);
+          } else {
+            const int8_t y = wrap8(cvt_tz(40.0f * x));
+            const int8_t a = wrap8((int32_t)wrap8(abs(y)) - off1);
+            llr[6 * i + c]     = wrap8(-(int32_t)y);
+            llr[6 * i + 2 + c] = a;
+            llr[6 * i + 4 + c] = wrap8((int32_t)wrap8(abs(a)) - off2);
+          }
+        }
+      }
+      return 0;
+    }
+    case 4: { /* 256QAM */
+      const float t[3] = {8.0f / sqrtf(170.0f), 4.0f / sqrtf(170.0f), 2.0f / sqrtf(170.0f)};
+      for (int i = 0; i < n; i++) {
+        float v[2] = {-sym[2 * i], -sym[2 * i + 1]};
+        for (int l = 0; l < 4; l++) {
+          for (int c = 0; c < 2; c++) {
+            if (l) {
+              v[c] = fabsf(v[c]) - t[l - 1];
+            }
+            llr[8 * i + 2 * l + c] = wrap8(cvt_tz(50 * v[c]));
+          }
+        }
+      }
+      return 0;
+    }
+    default:
+      return -1;
+  }
+}
+
+void oracle_sequence_apply_c(const int8_t* in, int8_t* out, uint32_t len, uint32_t seed)
+{
+  uint32_t x1 = 1, x2 = seed & 0x7FFFFFFFu;
+  for (int n = 0; n < 1600; n++) {
+    x1 = step_x1(x1);
+    x2 = step_x2(x2);
+  }
+  for (uint32_t i = 0; i < len; i++) {
+    out[i] = ((x1 ^ x2) & 1u) ? wrap8(-(int32_t)in[i]) : in[i];
+    x1     = step_x1(x1);
+    x2     = step_x2(x2);
+  }
+}
+
+void oracle_csi_correction_b(int mod, const float* csi, int8_t* e, uint32_t nof_bits)
+{
+  const uint32_t qm = (uint32_t[]){1, 2, 4, 6, 8}[mod];
+  const uint32_t ns = nof_bits / qm;
+  float          mx = 1.0f;
+  if (ns) {
+    mx = csi[0];
+    for (uint32_t k = 1; k < ns; k++) {
+      mx = csi[k] > mx ? csi[k] : mx;
+    }
+  }
+  const float rcp = 1.0f / mx;
+  for (uint32_t k = 0; k < ns; k++) {
+    const float c = csi[k] * rcp;
+    for (uint32_t b = 0; b < qm; b++) {
+      e[qm * k + b] = wrap8(cvt_tz((float)e[qm * k + b] * c));
     }
   }
 }

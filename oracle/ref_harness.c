@@ -523,3 +523,152 @@ int ref_dlsch_decode_tb(uint32_t       tbs,
   memset(cb_crc, 0, s.C);
   return -1;
 }
+
+/*
+ * ref_dlsch_decode_tb8: decode_tb with q->llr_is_8bit (sch.c:409-428) over the reference's own 8-bit pieces --
+ * srsran_rm_turbo_rx_lut_8bit into the soft buffer row used as int8, srsran_tdec_iteration_8bit (tdec_iteration_8:
+ * the 8-bit window decoders of K > 800, the 16-bit ones on the widened input otherwise) with its decision_byte,
+ * srsran_crc_checksum_byte.  Same arguments as ref_dlsch_decode_tb with int8 e bits.  For K <= 800 the whole
+ * sub-block layout is widened, as ref_tdec8_run does (convert_8_to_16 widens 3K + 12 values only).
+ */
+int ref_dlsch_decode_tb8(uint32_t      tbs,
+                         uint32_t      Qm,
+                         uint32_t      rv,
+                         uint32_t      nof_e_bits,
+                         const int8_t* e_bits,
+                         uint32_t      max_iterations,
+                         int16_t*      softbuf,
+                         uint32_t      softbuf_stride,
+                         uint8_t*      cb_crc,
+                         uint8_t*      cb_data,
+                         uint32_t      cb_data_stride,
+                         uint8_t*      data,
+                         uint32_t*     cb_noi_out,
+                         float*        avg_iterations)
+{
+  static srsran_crc_t crc_tb, crc_cb;
+  static bool         crc_ready = false;
+  if (harness_init()) {
+    return -1;
+  }
+  if (!crc_ready) {
+    srsran_crc_init(&crc_tb, SRSRAN_LTE_CRC24A, 24);
+    srsran_crc_init(&crc_cb, SRSRAN_LTE_CRC24B, 24);
+    crc_ready = true;
+  }
+  srsran_rm_turbo_gentables();
+  srsran_cbsegm_t s;
+  quiet_begin();
+  int rc = srsran_cbsegm(&s, tbs);
+  quiet_end();
+  if (rc) {
+    return -1;
+  }
+  if (s.tbs == 0 || s.C == 0) {
+    return 0;
+  }
+  if (s.F) {
+    return -2;
+  }
+  if (s.C > SRSRAN_MAX_CODEBLOCKS) {
+    return -1;
+  }
+  srsran_tdec_t*  h    = &tdec;
+  float           avg  = 0;
+  static int8_t*  sb8  = NULL;
+  static int16_t* wide = NULL;
+  if (!sb8) {
+    sb8  = srsran_vec_i8_malloc(2 * (SOFTBUFFER_SIZE + 64));
+    wide = srsran_vec_i16_malloc(SOFTBUFFER_SIZE + 64);
+  }
+  h->force_not_sb = false;
+  for (uint32_t cb = 0; cb < s.C; cb++) {
+    const uint32_t cb_len     = cb < s.C1 ? s.K1 : s.K2;
+    const uint32_t cb_len_idx = cb < s.C1 ? s.K1_idx : s.K2_idx;
+    const uint32_t rlen       = s.C == 1 ? cb_len : cb_len - 24;
+    if (!cb_crc[cb]) {
+      const uint32_t Gp    = nof_e_bits / Qm;
+      const uint32_t gamma = Gp % s.C;
+      const uint32_t n_e   = Qm * (Gp / s.C);
+      uint32_t       rp    = cb * n_e;
+      uint32_t       n_e2  = n_e;
+      if (cb > s.C - gamma) {
+        n_e2 = n_e + Qm;
+        rp   = (s.C - gamma) * n_e + (cb - (s.C - gamma)) * n_e2;
+      }
+      memcpy(sb8, &softbuf[(size_t)cb * softbuf_stride], softbuf_stride * sizeof(int16_t));
+      srsran_rm_turbo_rx_lut_8bit((int8_t*)&e_bits[rp], sb8, n_e2, cb_len_idx, rv);
+      const uint32_t nsb8 = srsran_tdec_autoimp_get_subblocks_8bit(cb_len);
+      if (nsb8 < 16) {
+        const uint32_t n = nsb8 ? 3 * (cb_len + 32) + 12 : 3 * cb_len + 12;
+        for (uint32_t i = 0; i < n; i++) {
+          wide[i] = sb8[i];
+        }
+      }
+      h->n_iter          = 0;
+      h->current_long_cb = cb_len;
+      h->current_cbidx   = (int)cb_len_idx;
+      uint32_t noi       = 0;
+      bool     early     = false;
+      do {
+        uint8_t* dst = &data[cb * rlen / 8];
+        if (nsb8 >= 16) {
+          h->current_llr_type  = SRSRAN_TDEC_8;
+          h->current_dec       = nsb8 == 32 ? 1 : 0;
+          h->current_inter_idx = inter_idx((uint32_t)h->nof_blocks8[h->current_dec]);
+          run_tdec_iteration_8bit(h, sb8);
+          h->dec8[h->current_dec]->tdec_decision_byte(!(h->n_iter % 2) ? (int8_t*)h->app1 : (int8_t*)h->ext1, dst,
+                                                      cb_len);
+        } else {
+          harness_iteration(h, wide);
+          h->dec16[h->current_dec]->tdec_decision_byte(!(h->n_iter % 2) ? h->app1 : h->ext1, dst, cb_len);
+        }
+        avg += 1;
+        noi++;
+        srsran_crc_t*  crc     = s.C > 1 ? &crc_cb : &crc_tb;
+        const uint32_t len_crc = s.C > 1 ? cb_len : s.tbs + 24;
+        if (!srsran_crc_checksum_byte(crc, dst, len_crc) && noi >= 2) {
+          cb_crc[cb] = 1;
+          early      = true;
+        }
+      } while (noi < max_iterations && !early);
+      h->current_llr_type = SRSRAN_TDEC_16;
+      memcpy(&softbuf[(size_t)cb * softbuf_stride], sb8, softbuf_stride * sizeof(int16_t));
+      if (cb_noi_out) {
+        cb_noi_out[cb] = noi;
+      }
+    } else {
+      memcpy(&data[cb * rlen / 8], &cb_data[(size_t)cb * cb_data_stride], rlen / 8);
+      if (cb_noi_out) {
+        cb_noi_out[cb] = 0;
+      }
+    }
+  }
+  bool tb_ok = true;
+  for (uint32_t i = 0; i < s.C && tb_ok; i++) {
+    tb_ok = cb_crc[i];
+  }
+  if (!tb_ok) {
+    for (uint32_t i = 0; i < s.C; i++) {
+      if (cb_crc[i]) {
+        const uint32_t cb_len = i < s.C1 ? s.K1 : s.K2;
+        const uint32_t rlen   = s.C == 1 ? cb_len : cb_len - 24;
+        memcpy(&cb_data[(size_t)i * cb_data_stride], &data[i * rlen / 8], rlen / 8);
+      }
+    }
+  }
+  if (avg_iterations) {
+    *avg_iterations = avg / (float)s.C;
+  }
+  if (!tb_ok) {
+    return -1;
+  }
+  if (s.C == 1) {
+    return 0;
+  }
+  if (srsran_crc_match_byte(&crc_tb, data, s.tbs)) {
+    return 0;
+  }
+  memset(cb_crc, 0, s.C);
+  return -1;
+}

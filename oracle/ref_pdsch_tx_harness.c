@@ -161,3 +161,91 @@ float ref_evm_run_s(int mod, const cf_t* symbols, const int16_t* llr, uint32_t n
   srsran_modem_table_free(&t);
   return e;
 }
+
+/* The 8-bit form, srsran_evm_run_b (evm.h:214-217 instantiation), on int8 demodulated LLRs. */
+float ref_evm_run_b(int mod, const cf_t* symbols, const int8_t* llr, uint32_t nof_bits, uint32_t max_bits)
+{
+  srsran_modem_table_t t;
+  srsran_modem_table_init(&t);
+  if (srsran_modem_table_lte(&t, (srsran_mod_t)mod)) {
+    return NAN;
+  }
+  srsran_modem_table_bytes(&t);
+  srsran_evm_buffer_t* b = srsran_evm_buffer_alloc(max_bits);
+  const float          e = srsran_evm_run_b(b, &t, symbols, llr, nof_bits);
+  srsran_evm_free(b);
+  srsran_modem_table_free(&t);
+  return e;
+}
+
+/* ---- csi_correction (pdsch.c:523-618, static there) restated around the reference's own srsran_vec_max_fi and
+ * built with the reference's release flags (oracle/Makefile REFFLAGS: -Ofast -mavx2 ...), so that the compiler's
+ * treatment of its float expressions -- the scalar loops' division by csi_max in particular -- is the one a
+ * reference build gets.  e: nof_bits LLRs, int8 when llr8 else int16, corrected in place. ---- */
+#include <immintrin.h>
+#include "srsran/phy/utils/vector.h"
+
+void ref_csi_correction(int mod, const float* csi, void* e, uint32_t nof_bits, int llr8)
+{
+  const uint32_t qm = srsran_mod_bits_x_symbol((srsran_mod_t)mod);
+  if (qm == 0) {
+    return;
+  }
+  const uint32_t ns   = nof_bits / qm;
+  const uint32_t imax = srsran_vec_max_fi(csi, ns);
+  float          cmax = 1.0f;
+  if (imax < ns) {
+    cmax = csi[imax];
+  }
+  const float* cv = csi;
+  if (llr8) {
+    int8_t* eb = e;
+    for (uint32_t i = 0; i < ns; i++) {
+      const float c = *(cv++) / cmax;
+      for (uint32_t k = 0; k < qm; k++, eb++) {
+        *eb = (int8_t)((float)*eb * c);
+      }
+    }
+    return;
+  }
+  int16_t* es = e;
+  uint32_t i  = 0;
+  __m128   sc = _mm_set1_ps(INT16_MAX / cmax);
+  __m64*   v  = (__m64*)e;
+  if (mod == SRSRAN_MOD_QPSK) { /* 4 LLRs = 2 symbols: lanes 0,1 <- symbol 1, lanes 2,3 <- symbol 0 (blend 3) */
+    for (; i + 3 < nof_bits; i += 4) {
+      __m128 a = _mm_set1_ps(*(cv++));
+      __m128 b = _mm_set1_ps(*(cv++));
+      *v       = _mm_mulhi_pi16(*v, _mm_cvtps_pi16(_mm_mul_ps(_mm_blend_ps(a, b, 3), sc)));
+      v++;
+    }
+  } else if (mod == SRSRAN_MOD_16QAM) {
+    for (; i + 3 < nof_bits; i += 4) {
+      *v = _mm_mulhi_pi16(*v, _mm_cvtps_pi16(_mm_mul_ps(_mm_set1_ps(*(cv++)), sc)));
+      v++;
+    }
+  } else if (mod == SRSRAN_MOD_64QAM) { /* 12 LLRs = 2 symbols over three 4-lane words */
+    for (; i + 11 < nof_bits; i += 12) {
+      __m128 a = _mm_mul_ps(_mm_set1_ps(*(cv++)), sc);
+      __m128 b = _mm_mul_ps(_mm_set1_ps(*(cv++)), sc);
+      v[0]     = _mm_mulhi_pi16(v[0], _mm_cvtps_pi16(a));
+      v[1]     = _mm_mulhi_pi16(v[1], _mm_cvtps_pi16(_mm_blend_ps(a, b, 3)));
+      v[2]     = _mm_mulhi_pi16(v[2], _mm_cvtps_pi16(b));
+      v += 3;
+    }
+  } else if (mod == SRSRAN_MOD_256QAM) {
+    for (; i + 7 < nof_bits; i += 8) {
+      __m64 c = _mm_cvtps_pi16(_mm_mul_ps(_mm_set1_ps(*(cv++)), sc));
+      v[0]    = _mm_mulhi_pi16(v[0], c);
+      v[1]    = _mm_mulhi_pi16(v[1], c);
+      v += 2;
+    }
+  }
+  i /= qm;
+  for (; i < ns; i++) {
+    const float c = csi[i] / cmax;
+    for (uint32_t k = 0; k < qm; k++) {
+      es[qm * i + k] = (int16_t)((float)es[qm * i + k] * c);
+    }
+  }
+}

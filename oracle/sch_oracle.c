@@ -117,14 +117,15 @@ static const uint8_t P_TC[32] = {0, 16, 8, 24, 4, 20, 12, 28, 2, 18, 10, 26, 6, 
 /*
  * table[k] (k < 3K+12): decoder-input index of the k-th non-dummy bit of the
  * circular buffer read from k0(rv).  layout_sb selects the sub-block remap applied
- * for window decoders (rm_turbo.c:249-273); natural index of d^(j)_i is 3i+j.
+ * for window decoders (rm_turbo.c:249-273): 1 the 16-bit decoder's sub-blocks, 2 the 8-bit decoder's
+ * (rm_turbo_rx_lut_8bit); natural index of d^(j)_i is 3i+j.
  */
 int oracle_rm_rx_table(uint32_t K, uint32_t rv, int layout_sb, uint16_t* table)
 {
   const uint32_t D = K + 4, R = (D + 31) / 32, Kp = 32 * R, ND = Kp - D, Ncb = 3 * Kp;
   const uint32_t k0 = R * (2 * ((Ncb + 8 * R - 1) / (8 * R)) * rv + 2);
   const uint32_t out_len = 3 * K + 12;
-  const uint32_t nsb     = layout_sb ? oracle_nof_subblocks(K) : 0;
+  const uint32_t nsb     = layout_sb == 2 ? oracle_nof_subblocks_8bit(K) : layout_sb ? oracle_nof_subblocks(K) : 0;
   uint32_t       k = 0, jj = 0;
   while (k < out_len) {
     const uint32_t w = (k0 + jj) % Ncb;
@@ -190,20 +191,54 @@ int oracle_rm_turbo_tx(uint32_t K, uint32_t rv, const uint8_t* coded, uint32_t E
 #define LTE_CRC24A 0x1864CFB
 #define LTE_CRC24B 0x1800063
 
-int oracle_dlsch_decode_tb(uint32_t       tbs,
-                           uint32_t       Qm,
-                           uint32_t       rv,
-                           uint32_t       nof_e_bits,
-                           const int16_t* e_bits,
-                           uint32_t       max_iterations,
-                           int16_t*       softbuf,
-                           uint32_t       softbuf_stride,
-                           uint8_t*       cb_crc,
-                           uint8_t*       cb_data,
-                           uint32_t       cb_data_stride,
-                           uint8_t*       data,
-                           uint32_t*      cb_noi_out,
-                           float*         avg_iterations)
+/* The decoder's output after each of max_iterations half-iterations (natural order, int16) for code block K of
+ * soft buffer row sb: the 16-bit AUTO decoder, or with llr8 the 8-bit one (rows holding int8 LLRs in the 8-bit
+ * layout, as buffer_f[cb] cast to int8_t* in sch.c:409-428).  Where no 8-bit decoder takes K (K <= 800) the
+ * reference widens the input for a 16-bit decoder (convert_8_to_16, turbodecoder.c:470-481); the whole layout is
+ * widened here (the reference converts only 3K + 12 values and leaves the rest of its sub-block layout buffer
+ * stale -- see DESIGN.md). */
+static void tdec_trace(uint32_t K, const int16_t* sb, int llr8, uint32_t max_iterations, int16_t* trace)
+{
+  uint8_t tmp[768];
+  if (!llr8) {
+    oracle_tdec_run(K, sb, 1, max_iterations, tmp, trace);
+    return;
+  }
+  const int8_t*  sb8  = (const int8_t*)sb;
+  const uint32_t nsb8 = oracle_nof_subblocks_8bit(K);
+  if (nsb8 >= 16) {
+    int8_t* t8 = malloc((size_t)max_iterations * K);
+    oracle_tdec8_run(K, sb8, max_iterations, tmp, t8);
+    for (size_t i = 0; i < (size_t)max_iterations * K; i++) {
+      trace[i] = t8[i];
+    }
+    free(t8);
+    return;
+  }
+  const uint32_t n    = nsb8 ? 3 * (K + 32) + 12 : 3 * K + 12;
+  int16_t*       wide = calloc(3 * (K + 32) + 12, sizeof(int16_t));
+  for (uint32_t i = 0; i < n; i++) {
+    wide[i] = sb8[i];
+  }
+  oracle_tdec_run(K, wide, 1, max_iterations, tmp, trace);
+  free(wide);
+}
+
+static int decode_tb(uint32_t       tbs,
+                     uint32_t       Qm,
+                     uint32_t       rv,
+                     uint32_t       nof_e_bits,
+                     const void*    e_bits,
+                     int            llr8,
+                     uint32_t       max_iterations,
+                     int16_t*       softbuf,
+                     uint32_t       softbuf_stride,
+                     uint8_t*       cb_crc,
+                     uint8_t*       cb_data,
+                     uint32_t       cb_data_stride,
+                     uint8_t*       data,
+                     uint32_t*      cb_noi_out,
+                     float*         avg_iterations)
 {
   oracle_cbsegm_t s;
   if (oracle_cbsegm(tbs, &s)) {
@@ -233,12 +268,23 @@ int oracle_dlsch_decode_tb(uint32_t       tbs,
         rp   = (s.C - gamma) * n_e + (cb - (s.C - gamma)) * n_e2;
       }
       int16_t* sb = &softbuf[(size_t)cb * softbuf_stride];
-      oracle_rm_turbo_rx(cb_len, rv, 1, &e_bits[rp], n_e2, sb);
+      if (llr8) { /* srsran_rm_turbo_rx_lut_8bit: int8 wrap-around on the 8-bit decoder's layout */
+        uint16_t*     t  = malloc((3 * cb_len + 12) * sizeof(uint16_t));
+        int8_t*       s8 = (int8_t*)sb;
+        const int8_t* e8 = (const int8_t*)e_bits + rp;
+        oracle_rm_rx_table(cb_len, rv, 2, t);
+        for (uint32_t i = 0; i < n_e2; i++) {
+          const uint16_t p = t[i % (3 * cb_len + 12)];
+          s8[p]            = (int8_t)(s8[p] + e8[i]);
+        }
+        free(t);
+      } else {
+        oracle_rm_turbo_rx(cb_len, rv, 1, (const int16_t*)e_bits + rp, n_e2, sb);
+      }
 
       /* iterations with early stop: decision after every half-iteration */
       int16_t* trace = malloc((size_t)max_iterations * cb_len * sizeof(int16_t));
-      uint8_t  tmp[768];
-      oracle_tdec_run(cb_len, sb, 1, max_iterations, tmp, trace);
+      tdec_trace(cb_len, sb, llr8, max_iterations, trace);
       uint32_t noi   = 0;
       int      early = 0;
       uint8_t  dec[768];
@@ -299,6 +345,26 @@ int oracle_dlsch_decode_tb(uint32_t       tbs,
   }
   memset(cb_crc, 0, s.C); /* srsran_softbuffer_rx_reset_cb_crc */
   return -1;
+}
+
+int oracle_dlsch_decode_tb(uint32_t tbs, uint32_t Qm, uint32_t rv, uint32_t nof_e_bits, const int16_t* e_bits,
+                           uint32_t max_iterations, int16_t* softbuf, uint32_t softbuf_stride, uint8_t* cb_crc,
+                           uint8_t* cb_data, uint32_t cb_data_stride, uint8_t* data, uint32_t* cb_noi_out,
+                           float* avg_iterations)
+{
+  return decode_tb(tbs, Qm, rv, nof_e_bits, e_bits, 0, max_iterations, softbuf, softbuf_stride, cb_crc, cb_data,
+                   cb_data_stride, data, cb_noi_out, avg_iterations);
+}
+
+/* decode_tb with q->llr_is_8bit (sch.c:409-428): int8 e bits, srsran_rm_turbo_rx_lut_8bit into the soft buffer rows
+ * (int16 rows used as int8), srsran_tdec_iteration_8bit */
+int oracle_dlsch_decode_tb8(uint32_t tbs, uint32_t Qm, uint32_t rv, uint32_t nof_e_bits, const int8_t* e_bits,
+                            uint32_t max_iterations, int16_t* softbuf, uint32_t softbuf_stride, uint8_t* cb_crc,
+                            uint8_t* cb_data, uint32_t cb_data_stride, uint8_t* data, uint32_t* cb_noi_out,
+                            float* avg_iterations)
+{
+  return decode_tb(tbs, Qm, rv, nof_e_bits, e_bits, 1, max_iterations, softbuf, softbuf_stride, cb_crc, cb_data,
+                   cb_data_stride, data, cb_noi_out, avg_iterations);
 }
 
 /* ---------------- DL-SCH encode (synthetic TBs; sch.c encode_tb semantics, K- first) ---------------- */

@@ -28,6 +28,10 @@ int      oracle_dlsch_decode_tb(uint32_t       tbs,
                                 uint8_t*       data,
                                 uint32_t*      cb_noi_out,
                                 float*         avg_iterations);
+int      oracle_dlsch_decode_tb8(uint32_t tbs, uint32_t Qm, uint32_t rv, uint32_t nof_e_bits, const int8_t* e_bits,
+                                 uint32_t max_iterations, int16_t* softbuf, uint32_t softbuf_stride, uint8_t* cb_crc,
+                                 uint8_t* cb_data, uint32_t cb_data_stride, uint8_t* data, uint32_t* cb_noi_out,
+                                 float* avg_iterations);
 int      oracle_dlsch_encode_tb(uint32_t tbs, uint32_t Qm, uint32_t rv, uint32_t nof_e_bits, const uint8_t* tb_bytes,
                                 uint8_t* e_bits);
 int      oracle_dlsch_encode_tb_x(uint32_t tbs, uint32_t Qm, uint32_t rv, uint32_t nof_e_bits, const uint8_t* tb_bytes,

@@ -623,3 +623,223 @@ int oracle_natural_to_sb(uint32_t K, const int16_t* in, int16_t* out)
   memcpy(&out[3 * (K + 32)], &in[3 * K], 12 * sizeof(int16_t));
   return 0;
 }
+
+/* ======================= 8-bit window decoders (turbodecoder_win.h WINIMP_IS_SSE8 / _AVX8) =======================
+ * C form of oracle/tdec8.py (the same schedule, pinned to the reference's decoders compiled into oracle/_ref by
+ * tests/test_tdec8bit.py and tests/test_sch_oracle.py): int8 metrics with saturating add / sub, normalisation
+ * by the state maximum at every step but k = 0, the tail trellis saturating upwards only, LLR m1 - m0 halved;
+ * training windows of 40 steps over the neighbouring sub-block.  Input in the 8-bit decoder's sub-block layout
+ * (rm_turbo_rx_lut_8bit): syst | 32 | parity0 | 32 | parity1 | 32 | tail. */
+#define OVL8 40
+
+/* srsran_tdec_autoimp_get_subblocks_8bit of an AVX2 build (turbodecoder.c:410-424): 32 / 16 / 8 / 0 */
+uint32_t oracle_nof_subblocks_8bit(uint32_t K)
+{
+  if (K % 32 == 0 && K > 2048) {
+    return 32;
+  }
+  if (K % 16 == 0 && K > 800) {
+    return 16;
+  }
+  if (K % 8 == 0 && K > 400) {
+    return 8;
+  }
+  return 0;
+}
+
+static int s8(int v) { return v > 127 ? 127 : (v < -128 ? -128 : v); }
+static int t8(int a, int b) /* beta_trellis sadd: upper clamp, int8 wrap below */
+{
+  const int z = a + b;
+  return z > 127 ? 127 : (int)(int8_t)z;
+}
+static void norm8(int k, int* o)
+{
+  if (k) {
+    int m = o[0];
+    for (int i = 1; i < 8; i++) {
+      m = o[i] > m ? o[i] : m;
+    }
+    for (int i = 0; i < 8; i++) {
+      o[i] = s8(o[i] - m);
+    }
+  }
+}
+static int max8(int a, int b) { return a > b ? a : b; }
+static void beta8(int* o, int x, int y)
+{
+  const int xy = s8(x + y);
+  int       n[8];
+  n[0] = max8(s8(o[4] + xy), o[0]);
+  n[1] = max8(o[4], s8(o[0] + xy));
+  n[2] = max8(s8(o[5] + y), s8(o[1] + x));
+  n[3] = max8(s8(o[5] + x), s8(o[1] + y));
+  n[4] = max8(s8(o[6] + x), s8(o[2] + y));
+  n[5] = max8(s8(o[6] + y), s8(o[2] + x));
+  n[6] = max8(o[7], s8(o[3] + xy));
+  n[7] = max8(s8(o[7] + xy), o[3]);
+  memcpy(o, n, sizeof(n));
+}
+static void alpha8(const int* o, int x, int y, int* mb, int* nw)
+{
+  const int xy = s8(x + y);
+  mb[0] = o[0], mb[1] = s8(o[3] + y), mb[2] = s8(o[4] + y), mb[3] = o[7];
+  mb[4] = o[1], mb[5] = s8(o[2] + y), mb[6] = s8(o[5] + y), mb[7] = o[6];
+  nw[0] = s8(o[1] + xy), nw[1] = s8(o[2] + x), nw[2] = s8(o[5] + x), nw[3] = s8(o[6] + xy);
+  nw[4] = s8(o[0] + xy), nw[5] = s8(o[3] + x), nw[6] = s8(o[4] + x), nw[7] = s8(o[7] + xy);
+}
+
+/* one MAP pass: X, A (optional), P in SB order with the tail at [K, K + 3); OUT = extrinsic (K) */
+static void map8(const int* X, const int* A, const int* P, int* OUT, int K, int nsb, int* beta, int* train)
+{
+  const int Ls = K / nsb;
+#define XA(q) (A ? s8(A[q] + X[q]) : X[q])
+  for (int d = 0; d < nsb; d++) { /* beta training from unknown (0) states */
+    int* o = &train[8 * d];
+    memset(o, 0, 8 * sizeof(int));
+    for (int k = OVL8 - 1; k >= 0; k--) {
+      beta8(o, XA(k * nsb + d), P[k * nsb + d]);
+      norm8(k, o);
+    }
+  }
+  for (int d = 0; d < nsb; d++) {
+    int o[8];
+    if (d < nsb - 1) {
+      memcpy(o, &train[8 * (d + 1)], sizeof(o));
+    } else { /* beta_trellis over the tail */
+      int t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (int k = K + 2; k >= K; k--) {
+        const int x = X[k], y = P[k], xy = t8(x, y);
+        int       mb[8] = {t8(t[4], xy), t[4], t8(t[5], y), t8(t[5], x), t8(t[6], x), t8(t[6], y), t[7], t8(t[7], xy)};
+        int       nw[8] = {t[0], t8(t[0], xy), t8(t[1], x), t8(t[1], y), t8(t[2], y), t8(t[2], x), t8(t[3], xy), t[3]};
+        for (int i = 0; i < 8; i++) {
+          t[i] = max8(mb[i], nw[i]);
+        }
+      }
+      memcpy(o, t, sizeof(o));
+    }
+    memcpy(&beta[((size_t)Ls * nsb + d) * 8], o, sizeof(o));
+    for (int k = Ls - 1; k >= 0; k--) {
+      beta8(o, XA(k * nsb + d), P[k * nsb + d]);
+      memcpy(&beta[((size_t)k * nsb + d) * 8], o, sizeof(o)); /* before normalisation */
+      norm8(k, o);
+    }
+  }
+  for (int d = 0; d < nsb; d++) { /* alpha training over the sub-block's last 40 steps */
+    int* o = &train[8 * d];
+    memset(o, 0, 8 * sizeof(int));
+    for (int k = 0; k < OVL8; k++) {
+      const int q = (Ls - OVL8 + k) * nsb + d;
+      int       mb[8], nw[8];
+      alpha8(o, XA(q), P[q], mb, nw);
+      for (int i = 0; i < 8; i++) {
+        o[i] = max8(mb[i], nw[i]);
+      }
+      norm8(k, o);
+    }
+  }
+  for (int d = nsb - 1; d >= 0; d--) { /* descending: sub-block d starts from d - 1's training, still intact */
+    int o[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (d > 0) {
+      memcpy(o, &train[8 * (d - 1)], sizeof(o));
+    }
+    for (int k = 0; k < Ls; k++) {
+      const int q = k * nsb + d;
+      int       mb[8], nw[8];
+      alpha8(o, XA(q), P[q], mb, nw);
+      const int* b  = &beta[((size_t)(k + 1) * nsb + d) * 8];
+      int        m0 = s8(b[0] + mb[0]), m1 = s8(b[0] + nw[0]);
+      for (int i = 1; i < 8; i++) {
+        m0 = max8(m0, s8(b[i] + mb[i]));
+        m1 = max8(m1, s8(b[i] + nw[i]));
+      }
+      OUT[q] = s8(m1 - m0) >> 1;
+      for (int i = 0; i < 8; i++) {
+        o[i] = max8(mb[i], nw[i]);
+      }
+      norm8(k, o);
+    }
+  }
+#undef XA
+}
+
+/* srsran_tdec_run_all_8bit on one block of an 8-bit decoder class (nsb 16 / 32, SB layout input):
+ * nof_iterations half-iterations; output = decision bytes; trace (optional, nof_iterations * K int8) = the
+ * latest output after each half-iteration in natural order. */
+int oracle_tdec8_run(uint32_t K, const int8_t* in, uint32_t nof_iterations, uint8_t* output, int8_t* trace)
+{
+  const int nsb = (int)oracle_nof_subblocks_8bit(K);
+  if ((nsb != 16 && nsb != 32) || nof_iterations < 1) {
+    return -1;
+  }
+  const int Ls = (int)K / nsb;
+  uint16_t* fwd = malloc(K * sizeof(uint16_t));
+  int*      SY  = calloc(K + 3, sizeof(int));
+  int*      P0  = calloc(K + 3, sizeof(int));
+  int*      P1  = calloc(K + 3, sizeof(int));
+  int*      A1  = calloc(K, sizeof(int));
+  int*      A2  = calloc(K + 3, sizeof(int));
+  int*      E1  = calloc(K, sizeof(int));
+  int*      E2  = calloc(K, sizeof(int));
+  int*      fsb = malloc(K * sizeof(int));
+  int*      beta  = malloc((size_t)(Ls + 1) * nsb * 8 * sizeof(int));
+  int*      train = malloc((size_t)nsb * 8 * sizeof(int));
+  oracle_qpp(K, fwd, NULL);
+  for (int q = 0; q < (int)K; q++) { /* QPP forward table in SB slot order (tc_interl_lte.c:88-106, win = nsb) */
+    const int n  = (q % nsb) * Ls + q / nsb;
+    const int fn = fwd[n];
+    fsb[q]       = (fn % Ls) * nsb + fn / Ls;
+  }
+  for (uint32_t q = 0; q < K; q++) {
+    SY[q] = in[q];
+    P0[q] = in[K + 32 + q];
+    P1[q] = in[2 * (K + 32) + q];
+  }
+  const int8_t* tail = &in[3 * (K + 32)];
+  for (int j = 0; j < 3; j++) {
+    SY[K + j] = tail[2 * j];
+    P0[K + j] = tail[2 * j + 1];
+    A2[K + j] = tail[6 + 2 * j];
+    P1[K + j] = tail[7 + 2 * j];
+  }
+  for (uint32_t n = 0; n < nof_iterations; n++) {
+    if (n % 2 == 0) {
+      if (n) {
+        for (uint32_t q = 0; q < K; q++) {
+          A1[q] = s8(A1[q] - E1[q]);
+        }
+      }
+      map8(SY, n ? A1 : NULL, P0, E1, (int)K, nsb, beta, train);
+    } else {
+      if (n > 1) {
+        for (uint32_t q = 0; q < K; q++) {
+          E1[q] = s8(E1[q] - A1[q]);
+        }
+      }
+      for (uint32_t j = 0; j < K; j++) {
+        A2[j] = E1[fsb[j]];
+      }
+      map8(A2, NULL, P1, E2, (int)K, nsb, beta, train);
+      for (uint32_t i = 0; i < K; i++) {
+        A1[fsb[i]] = E2[i];
+      }
+    }
+    if (trace) {
+      const int* src = ((n + 1) % 2) ? E1 : A1;
+      for (uint32_t i = 0; i < K; i++) {
+        trace[(size_t)n * K + i] = (int8_t)src[(i % Ls) * nsb + i / Ls];
+      }
+    }
+  }
+  const int* src = (nof_iterations % 2) ? E1 : A1;
+  for (uint32_t b = 0; b < K / 8; b++) {
+    uint8_t v = 0;
+    for (int t = 0; t < 8; t++) {
+      const uint32_t i = 8 * b + t;
+      v |= (uint8_t)((src[(i % Ls) * nsb + i / Ls] > 0) << (7 - t));
+    }
+    output[b] = v;
+  }
+  free(fwd), free(SY), free(P0), free(P1), free(A1), free(A2), free(E1), free(E2), free(fsb), free(beta), free(train);
+  return 0;
+}

@@ -20,6 +20,10 @@ int oracle_tdec_run_batch(uint32_t K,
                           uint8_t*       output,
                           uint32_t       nof_cb);
 
+uint32_t oracle_nof_subblocks_8bit(uint32_t K);
+/* 8-bit window decoder (nsb 16 / 32 classes), SB layout input; trace: nof_iterations * K int8, natural order */
+int oracle_tdec8_run(uint32_t K, const int8_t* in, uint32_t nof_iterations, uint8_t* output, int8_t* trace);
+
 int oracle_tcod_encode(uint32_t K, const uint8_t* bits, uint8_t* out);
 int oracle_natural_to_sb(uint32_t K, const int16_t* in, int16_t* out);
 #endif

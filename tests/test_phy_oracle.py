@@ -72,6 +72,50 @@ def test_pdsch_seed_matches_reference():
         assert np.array_equal(ora.sequence_apply_s(llr, seed), ref.sequence_pdsch_apply_s(llr, rnti, q, ns, cell))
 
 
+@needs_ref
+@pytest.mark.parametrize("mod,scale", [(0, 20.0), (1, 28.284271), (2, 30.0), (3, 40.0), (4, 50.0)])
+def test_demod_b_matches_reference(mod, scale):
+    """int8 demapping (srsran_demod_soft_demodulate_b, llr_is_8bit): the SSE blocks of 8 symbols (16 values for
+    QPSK) round half-even and saturate, their abs/offset steps wrap (|-128| = -128); the tails truncate."""
+    ora, ref = Oracle(), Reference()
+    rng = np.random.default_rng(40 + mod)
+    for n in (1, 2, 3, 7, 8, 9, 15, 16, 17, 23, 1200, 14400, 14401, 14407):
+        sym = symbols(rng, n, scale)
+        a = ora.demod_b(mod, sym)
+        b = ref.demod_b(mod, sym)
+        assert np.array_equal(a, b), (mod, n, np.flatnonzero(a != b)[:8])
+
+
+@needs_ref
+def test_sequence_c_matches_reference():
+    """int8 descrambling (srsran_sequence_apply_c): -(-128) stays -128."""
+    ora, ref = Oracle(), Reference()
+    rng = np.random.default_rng(9)
+    for n in (0, 1, 15, 16, 17, 31, 32, 33, 86400, 90001):
+        llr = rng.integers(-128, 128, n, dtype=np.int8)
+        llr[: min(n, 5)] = -128
+        for seed in (0, 1, 0x1234 << 14 | 1, 0x7FFFFFFF, int(rng.integers(0, 2**31))):
+            assert np.array_equal(ora.sequence_apply_c(llr, seed), ref.sequence_apply_c(llr, seed)), (n, seed)
+
+
+@needs_ref
+@pytest.mark.parametrize("llr8", [False, True])
+def test_csi_correction_matches_reference_build(llr8):
+    """csi_correction (pdsch.c:523-618) restated in ref_pdsch_tx_harness.c over the reference's srsran_vec_max_fi and
+    built with the reference's -Ofast flags: the oracle (and the GPU) follow the build, whose scalar loops multiply by a
+    hoisted 1 / csi_max instead of dividing (-freciprocal-math); int16 SSE blocks + tail, and the int8 branch."""
+    ora, ref = Oracle(), Reference()
+    rng = np.random.default_rng(11 + llr8)
+    for mod in (1, 2, 3, 4):
+        qm = (1, 2, 4, 6, 8)[mod]
+        for ns in (1, 2, 3, 5, 17, 601, 1201, 7200):
+            csi = (rng.random(ns) * rng.choice([0.013, 1.0, 7.3])).astype(np.float32)
+            e = rng.integers(-128, 128, ns * qm) if llr8 else rng.integers(-32768, 32768, ns * qm)
+            a = (ora.csi_correction_b if llr8 else ora.csi_correction)(mod, csi, e)
+            b = ref.csi_correction(mod, csi, e, llr8)
+            assert np.array_equal(a, b), (mod, ns, np.flatnonzero(a != b)[:8])
+
+
 def test_sequence_known_properties():
     """c(n) for seed 0 is x1 alone (x2 == 0); Gold sequence is balanced."""
     ora = Oracle()

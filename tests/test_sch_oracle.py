@@ -141,3 +141,35 @@ def test_dlsch_decode_matches_reference_pieces(ora):
                 assert np.array_equal(so[1], sr[1]) and np.array_equal(so[2], sr[2]), (tbs, sigma, rv)
                 if a[0] == 0:
                     break
+
+
+def llr8_of(e_bits, rng, sigma, scale=20.0):
+    """int8 LLRs of coded bits (+-1 plus AWGN, scaled, truncated, saturated) -- the range demod_soft_demodulate_b emits."""
+    y = e_bits.astype(np.float32) * 2 - 1 + rng.standard_normal(e_bits.shape).astype(np.float32) * sigma
+    return np.clip(np.trunc(np.float32(scale) * y), -128, 127).astype(np.int8)
+
+
+@needs_ref
+def test_dlsch_decode8_matches_reference_pieces(ora):
+    """decode_tb with llr_is_8bit (sch.c:409-428): the oracle (C restatement of the 8-bit window decoders and int8 rate
+    de-matching) against the same loop over the reference's srsran_rm_turbo_rx_lut_8bit / 8-bit decoders / CRC, on
+    every decoder class: 32 sub-blocks (K > 2048), 16 (800 < K <= 2048), the 16-bit decoders on the widened input for
+    K <= 800 (8 sub-blocks and natural); noise-free, early-stop, failure and HARQ chains."""
+    ref = Reference()
+    rng = np.random.default_rng(13)
+    for tbs, Qm, G, sigmas in ((75376, 6, 86400, (0.0, 0.5)), (1544, 2, 3600, (0.75, 0.85)), (19080, 4, 28800, (0.6,)),
+                               (680, 4, 2400, (0.0, 0.9)), (16, 2, 240, (0.3,))):
+        for sigma in sigmas:
+            tb = rng.integers(0, 256, tbs // 8, dtype=np.uint8)
+            so = sr = None
+            for rv in (0, 2, 3):
+                e = llr8_of(ora.dlsch_encode(tbs, Qm, rv, G, tb), rng, sigma)
+                a = ora.dlsch_decode8(tbs, Qm, rv, e, 8, so)
+                b = ref.dlsch_decode8(tbs, Qm, rv, e, 8, sr)
+                so, sr = a[4], b[4]
+                assert a[0] == b[0] and np.array_equal(a[1], b[1]) and a[2] == b[2] and a[3] == b[3], (tbs, sigma, rv)
+                assert np.array_equal(so[1], sr[1]) and np.array_equal(so[2], sr[2]), (tbs, sigma, rv)
+                if a[0] == 0:
+                    break
+            if sigma == 0.0:
+                assert a[0] == 0 and np.array_equal(a[1][: tbs // 8], tb), tbs

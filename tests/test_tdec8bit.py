@@ -73,6 +73,19 @@ def test_restatement_matches_reference(ref, K, layout_sb):
             assert np.array_equal(tdec8.run_all(K, llr, it, nsb, fwd, layout_sb), ref.tdec8_run(K, llr, layout_sb, it))
 
 
+@pytest.mark.parametrize("K", [832, 2048, 2112, 6144])
+def test_c_restatement_matches_reference_trace(ref, K):
+    """oracle_tdec8_run (the C form of tdec8.py the 8-bit DL-SCH oracle runs) against the reference's decoders:
+    decisions and the latest output after every half-iteration, AWGN and uniformly random int8 input."""
+    ora = Oracle()
+    rng = np.random.default_rng(K + 3)
+    for kind in ("awgn", "rand"):
+        llr = _llr8(K, rng, True, ora, kind)
+        out, tr = ora.tdec8_run(K, llr, 7, trace=True)
+        rout, rtr = ref.tdec8_run(K, llr, True, 7, trace=True)
+        assert np.array_equal(out, rout) and np.array_equal(tr, rtr), kind
+
+
 def test_reference_decodes_noise_free(ref):
     """The checker itself decodes: a noise-free encoded block comes back exactly (both 8-bit classes)."""
     ora = Oracle()

@@ -15,8 +15,9 @@
  *     memory (HBM).  cb_crc[] / tb_crc stay host-readable mirrors, refreshed by every synchronous call.
  *   - srsran_sch_t keeps the fields callers touch (max_iterations, avg_iterations, llr_is_8bit,
  *     decoder); the CPU-only scratch buffers are replaced by an opaque `gpu` pointer.
- *   - the 8-bit LLR transport-channel path (llr_is_8bit) is not provided and must stay false; its
- *     building blocks are: srsran_rm_turbo_rx_lut_8bit here and srsran_tdec_run_all_8bit (srsran_tdec.h).
+ *   - llr_is_8bit (sch.c:409-428) is provided: e bits are then int8 (passed through the int16_t* parameters,
+ *     as the reference casts them), the soft buffer rows hold int8 LLRs in the 8-bit decoder's layout, and the
+ *     blocks decode on the 8-bit window decoders (K > 800) or the 16-bit ones on the widened row (K <= 800).
  *   - srsran_dlsch_gpu_decode_batch() is an added, asynchronous entry point over device buffers.
  */
 #ifndef SRSRAN_AMD_SCH_H
@@ -236,7 +237,7 @@ typedef struct {
   uint32_t                Qm; /* bits per symbol x layers, as decode_tb receives it */
   uint32_t                rv;
   uint32_t                nof_e_bits;
-  const int16_t*          d_e_bits; /* device */
+  const int16_t*          d_e_bits; /* device; int8_t LLRs when the srsran_sch_t has llr_is_8bit */
   uint8_t*                d_data;   /* device, >= tbs/8 + 6 bytes */
   srsran_softbuffer_rx_t* softbuffer;
   uint32_t                new_data; /* 1: as if srsran_softbuffer_rx_reset_tbs(softbuffer, tbs) ran first */

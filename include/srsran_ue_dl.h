@@ -324,8 +324,8 @@ int srsran_pdsch_gpu_decode_batch(srsran_pdsch_t*              q,
                                   float*                       d_avg_noi,
                                   void*                        stream);
 
-/* added (tests / diagnostics): the descrambled, CSI-corrected int16 LLRs (the e bits srsran_dlsch_decode2
- * receives, pdsch.c:693-733) of subframe `sf` (index into the last srsran_pdsch_gpu_decode_batch /
+/* added (tests / diagnostics): the descrambled, CSI-corrected int16 LLRs (int8 when q->llr_is_8bit; the e bits
+ * srsran_dlsch_decode2 receives, pdsch.c:693-733) of subframe `sf` (index into the last srsran_pdsch_gpu_decode_batch /
  * srsran_ue_dl_gpu_decode_batch on q) and transport block `tb`: a device pointer, valid until the next batch on
  * q and complete once that batch's stream has reached it, and their number.  SRSRAN_ERROR if the TB was not in
  * the batch. */

@@ -8,7 +8,8 @@
       apply_power_allocation        pdsch.c:485-521 (rho_b on CRS symbols, rho_a as scaling)
       srsran_predecoding_type       Oracle.predecode (MMSE with CSI)
       codeword decode               pdsch.c:661-744: demod_s, sequence_pdsch_apply_s,
-                                    csi_correction, srsran_dlsch_decode2 (Oracle.dlsch_decode)
+                                    csi_correction, srsran_dlsch_decode2 (Oracle.dlsch_decode);
+                                    with llr8 the 8-bit forms (demod_b, apply_c, dlsch_decode8)
 Parity: each piece is pinned to the reference (tests/test_phy_oracle.py, test_sch_oracle.py);
 the OFDM stage is numpy (FFTW unavailable, 'parity unpinned' beyond round trips).
 """
@@ -51,9 +52,11 @@ def fft_estimate(ora, samples, nof_prb, cell_id, nports, tti, cfo=0.0, N=None, c
 
 def pdsch_decode(ora, grids, ce, noise, nof_prb, cell_id, nports, tti, cfi, rnti, tbs, Qm, rv, scheme="cdd",
                  pmi=0, max_iterations=8, csi_enable=True, power_scale=False, p_a=0.0, p_b=0, prb_mask=None,
-                 states=None, layers=None, cp=0):
+                 states=None, layers=None, cp=0, llr8=False):
     """srsran_pdsch_decode for nof_tb = len(tbs) codewords (one layer each; layers=2 with one
     codeword: SM / CDD on two layers, pdsch.c:838-863 + layermap.c:138-147, 236-260).
+    llr8: q->llr_is_8bit (pdsch.c:691-737, sch.c:409-428): demod_b, sequence_apply_c, the 8-bit CSI correction
+    and decode_tb on the 8-bit decoders.
     Returns per codeword dict(ret, data, avg, llr)."""
     sf_idx = tti % 10
     lstart = cfi + (1 if nof_prb < 10 else 0)
@@ -88,12 +91,20 @@ def pdsch_decode(ora, grids, ce, noise, nof_prb, cell_id, nports, tti, cfi, rnti
         x, csi = ora.predecode(SCHEME[scheme], y, h, ntb, codebook, scaling, noise)
     out = []
     for q in range(ntb):
-        llr = demod = ora.demod_s(MOD[Qm[q]], x[q])
-        llr = ora.sequence_apply_s(llr, ora.pdsch_seed(rnti, q, 2 * sf_idx, cell_id))
-        if csi_enable:
-            llr = ora.csi_correction(MOD[Qm[q]], csi[q], llr)
+        seed = ora.pdsch_seed(rnti, q, 2 * sf_idx, cell_id)
+        if llr8:
+            llr = demod = ora.demod_b(MOD[Qm[q]], x[q])
+            llr = ora.sequence_apply_c(llr, seed)
+            if csi_enable:
+                llr = ora.csi_correction_b(MOD[Qm[q]], csi[q], llr)
+        else:
+            llr = demod = ora.demod_s(MOD[Qm[q]], x[q])
+            llr = ora.sequence_apply_s(llr, seed)
+            if csi_enable:
+                llr = ora.csi_correction(MOD[Qm[q]], csi[q], llr)
         st = states[q] if states else None
         nl = 2 if (scheme == "diversity" or layers == 2) and ntb == 1 else 1  # Nl = 2 when layers != TBs (sch.c:587-590)
-        ret, data, noi, avg, state = ora.dlsch_decode(tbs[q], Qm[q] * nl, rv[q], llr, max_iterations, st)
+        dec = ora.dlsch_decode8 if llr8 else ora.dlsch_decode
+        ret, data, noi, avg, state = dec(tbs[q], Qm[q] * nl, rv[q], llr, max_iterations, st)
         out.append(dict(ret=ret, data=data, avg=avg, llr=llr, state=state, nof_re=idx.size, sym=x[q], demod=demod))
     return out

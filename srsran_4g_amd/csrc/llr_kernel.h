@@ -29,6 +29,9 @@ struct LlrItem {
   // |sym - mod(hard(pre-scrambling LLRs))|^2 into evm_part[block]; evm_finalize_launch turns them into the RMS
   float*        evm_part;
   uint32_t      evm_n;
+  // q->llr_is_8bit (pdsch.c:691-737): int8 LLRs here instead of llr (demod_b, sequence_apply_c, the 8-bit CSI
+  // correction, srsran_evm_run_b); the launch's llr8 flag selects the form
+  int8_t*       llr8;
 };
 // one EVM result: sqrtf(sum of nparts block sums (in block order) / nsym) into *out
 struct EvmItem {
@@ -41,7 +44,7 @@ hipError_t evm_finalize_launch(const EvmItem* d_items, uint32_t nitems, hipStrea
 constexpr uint32_t LLR_BLOCK_SYMBOLS = 256 * 16;  // symbols of one LLR block (evm_part entries = ceil(n / this))
 // nitems items of one modulation (device array); max_n = largest n
 hipError_t llr_batch_launch(int mod, const LlrItem* d_items, uint32_t nitems, uint32_t max_n, int any_scramble,
-                            hipStream_t stream);
+                            hipStream_t stream, bool llr8 = false);
 
 // out[i] = c(i) ? -in[i] : in[i] (int16 wrap) for the Gold sequence of `seed`.
 hipError_t seq_apply_launch(const int16_t* d_in, int16_t* d_out, uint32_t len, uint32_t seed, hipStream_t stream);

@@ -315,12 +315,98 @@ __device__ __forceinline__ void csi_correct(int16_t* o, uint32_t s, const float*
         o[b] = mulhi16(o[b], c);
       }
     }
-  } else {
-    const float c = csi[s] / mx;
+  } else {  // the release build hoists 1 / csi_max (-Ofast -freciprocal-math; oracle/ref_pdsch_tx_harness.c)
+    const float c = csi[s] * (1.0f / mx);
 #pragma unroll
     for (int b = 0; b < Q; b++) {
       o[b] = wrap16(cvt_tz((float)o[b] * c));
     }
+  }
+}
+
+// ---- the 8-bit chain (q->llr_is_8bit, pdsch.c:691-737) ----
+__device__ __forceinline__ int8_t sat8(int32_t v) { return (int8_t)max(-128, min(127, v)); }
+__device__ __forceinline__ int8_t wrap8(int32_t v) { return (int8_t)(uint8_t)(uint32_t)v; }
+__device__ __forceinline__ int8_t abs8(int8_t v) { return wrap8(v < 0 ? -(int32_t)v : (int32_t)v); }  // _mm_abs_epi8
+
+// srsran_demod_soft_demodulate_b (demod_soft.c:896-919), x86 SSE build: SSE blocks of 8 symbols (QPSK: 16 values of
+// srsran_vec_convert_fb_simd) round (QAM) or truncate (QPSK) and saturate to int8, their abs / offset steps wrap; the
+// tails truncate and wrap (oracle_demod_soft_b)
+template <int MOD>
+__device__ __forceinline__ void demap8(float re, float im, uint32_t i, uint32_t n, int8_t* o)
+{
+  const float v[2] = {re, im};
+  if constexpr (MOD == 0) {  // demod_bpsk_lte_b
+    const float t = -20.0f * (re + im);
+    o[0]          = wrap8(cvt_tz_d((double)t * 0.70710678118654752440));
+  } else if constexpr (MOD == 1) {  // vector_simd.c:524-589, scale (float)(-20 * M_SQRT2)
+    const float    scale = (float)(-20.0 * 1.41421356237309504880);
+    const uint32_t nblk  = 16 * ((2 * n) / 16);
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+      const int32_t t = cvt_tz(v[c] * scale);
+      o[c]            = (2 * i + c < nblk) ? sat8(t) : wrap8(t);
+    }
+  } else if constexpr (MOD == 2) {  // demod_16qam_lte_b_sse (demod_soft.c:301-364)
+    if (i < 8 * (n / 8)) {
+#pragma unroll
+      for (int c = 0; c < 2; c++) {
+        const int8_t s = sat8(cvt_rn(v[c] * -30.0f));
+        o[c]           = s;
+        o[2 + c]       = wrap8(abs8(s) - 18);  // _mm_set1_epi8(60 / sqrtf(10))
+      }
+    } else {
+      const float off = 60.0f / sqrtf(10.0f);
+#pragma unroll
+      for (int c = 0; c < 2; c++) {
+        const int8_t y = wrap8(cvt_tz(30.0f * v[c]));
+        o[c]           = wrap8(-(int32_t)y);
+        o[2 + c]       = wrap8(cvt_tz((float)abs((int32_t)y) - off));
+      }
+    }
+  } else if constexpr (MOD == 3) {  // demod_64qam_lte_b_sse (demod_soft.c:650-730)
+    if (i < 8 * (n / 8)) {
+#pragma unroll
+      for (int c = 0; c < 2; c++) {
+        const int8_t s = sat8(cvt_rn(v[c] * -40.0f));
+        const int8_t a = wrap8(abs8(s) - 24);
+        o[c]           = s;
+        o[2 + c]       = a;
+        o[4 + c]       = wrap8(abs8(a) - 12);
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < 2; c++) {
+        const int8_t y = wrap8(cvt_tz(40.0f * v[c]));
+        const int8_t a = wrap8((int32_t)wrap8(abs((int32_t)y)) - 24);
+        o[c]           = wrap8(-(int32_t)y);
+        o[2 + c]       = a;
+        o[4 + c]       = wrap8((int32_t)wrap8(abs((int32_t)a)) - 12);
+      }
+    }
+  } else {  // demod_256qam_lte_b (demod_soft.c:800-822)
+    const float t[3] = {8.0f / sqrtf(170.0f), 4.0f / sqrtf(170.0f), 2.0f / sqrtf(170.0f)};
+    float       a = -re, b = -im;
+#pragma unroll
+    for (int l = 0; l < 4; l++) {
+      if (l) {
+        a = fabsf(a) - t[l - 1];
+        b = fabsf(b) - t[l - 1];
+      }
+      o[2 * l]     = wrap8(cvt_tz(50.0f * a));
+      o[2 * l + 1] = wrap8(cvt_tz(50.0f * b));
+    }
+  }
+}
+
+// csi_correction's llr_is_8bit branch (pdsch.c:538-545): (int8)((float)e * (csi * (1 / csi_max)))
+template <int MOD>
+__device__ __forceinline__ void csi_correct8(int8_t* o, uint32_t s, const float* csi, float mx)
+{
+  const float c = csi[s] * (1.0f / mx);
+#pragma unroll
+  for (int b = 0; b < Qm<MOD>::v; b++) {
+    o[b] = wrap8(cvt_tz((float)o[b] * c));
   }
 }
 
@@ -341,11 +427,12 @@ __device__ __forceinline__ uint32_t gold16(uint32_t& x1, uint32_t& x2)
 // the block's bit t * SPT * Q and writes its SPT * Q sequence bits to LDS (one table jump per
 // 16 * Q bits).  Phase 2: thread t handles symbols t, t + 256, ... -- coalesced loads and
 // stores -- demapping, descrambling from the LDS bits and CSI correction in registers.
-template <int MOD>
+template <int MOD, bool B8 = false>
 __device__ __forceinline__ void llr_block(const float2* __restrict__ sym, uint32_t n, int scramble, uint32_t seed,
                                           uint32_t bit0, const float* __restrict__ csi,
                                           const float* __restrict__ csi_max, int16_t* __restrict__ llr, uint32_t blk,
-                                          float* __restrict__ evm_part = nullptr, uint32_t evm_n = 0)
+                                          float* __restrict__ evm_part = nullptr, uint32_t evm_n = 0,
+                                          int8_t* __restrict__ llr8 = nullptr)
 {
   constexpr int       Q = Qm<MOD>::v;
   __shared__ uint16_t cbits[LLR_THREADS * 8 + 2];  // SPT * Q / 16 = Q chunks per thread
@@ -367,8 +454,11 @@ __device__ __forceinline__ void llr_block(const float2* __restrict__ sym, uint32
     __syncthreads();
   }
   const float mx  = csi ? *csi_max : 1.0f;
-  const bool  a16 = ((uintptr_t)llr & 15) == 0;
-  const bool  a4  = ((uintptr_t)llr & 3) == 0;
+  const uintptr_t ob  = B8 ? (uintptr_t)llr8 : (uintptr_t)llr;
+  const bool      a16 = (ob & 15) == 0;
+  const bool      a8  = (ob & 7) == 0;
+  const bool      a4  = (ob & 3) == 0;
+  const bool      a2  = (ob & 1) == 0;
   float       err = 0.0f;  // EVM: this thread's sum of squared symbol errors
 #pragma unroll 4
   for (int r = 0; r < SPT; r++) {
@@ -378,7 +468,67 @@ __device__ __forceinline__ void llr_block(const float2* __restrict__ sym, uint32
     }
     const uint32_t s = base + i;
     const float2   v = sym[s];
-    int16_t        o[Q];
+    if constexpr (B8) {  // int8 LLRs: demod_b, sequence_apply_c, the 8-bit CSI correction
+      int8_t o[Q];
+      demap8<MOD>(v.x, v.y, s, n, o);
+      if constexpr (MOD >= 1) {
+        if (s < evm_n) {  // srsran_evm_run_b: the same hard decision on the int8 LLRs
+          uint32_t idx = 0;
+#pragma unroll
+          for (int k = 0; k < Q; k++) {
+            idx = (idx << 1) | (o[k] >= 0 ? 1u : 0u);
+          }
+          const float2 m  = modulate(MOD, idx);
+          const float  dr = v.x - m.x, di = v.y - m.y;
+          err += dr * dr + di * di;
+        }
+      }
+      if (scramble) {
+        const uint32_t b  = i * Q;
+        const uint32_t w0 = cbits[b >> 4];
+        const uint32_t w  = ((b & 15) + Q > 16) ? (w0 | ((uint32_t)cbits[(b >> 4) + 1] << 16)) : w0;
+        const uint32_t cb = w >> (b & 15);
+#pragma unroll
+        for (int k = 0; k < Q; k++) {
+          o[k] = ((cb >> k) & 1u) ? wrap8(-(int32_t)o[k]) : o[k];
+        }
+      }
+      if (csi) {
+        csi_correct8<MOD>(o, s, csi, mx);
+      }
+      int8_t* dst = llr8 + (size_t)s * Q;
+      if constexpr (Q == 8) {
+        uint2 u;
+        u.x = (uint32_t)(uint8_t)o[0] | ((uint32_t)(uint8_t)o[1] << 8) | ((uint32_t)(uint8_t)o[2] << 16) |
+              ((uint32_t)(uint8_t)o[3] << 24);
+        u.y = (uint32_t)(uint8_t)o[4] | ((uint32_t)(uint8_t)o[5] << 8) | ((uint32_t)(uint8_t)o[6] << 16) |
+              ((uint32_t)(uint8_t)o[7] << 24);
+        if (a8) {
+          *reinterpret_cast<uint2*>(dst) = u;
+          continue;
+        }
+      } else if constexpr (Q == 4) {
+        if (a4) {
+          *reinterpret_cast<uint32_t*>(dst) = (uint32_t)(uint8_t)o[0] | ((uint32_t)(uint8_t)o[1] << 8) |
+                                              ((uint32_t)(uint8_t)o[2] << 16) | ((uint32_t)(uint8_t)o[3] << 24);
+          continue;
+        }
+      } else if constexpr (Q == 2 || Q == 6) {
+        if (a2) {  // Q = 6: the symbol's 6 bytes start 2-byte aligned
+#pragma unroll
+          for (int k = 0; k < Q / 2; k++) {
+            reinterpret_cast<uint16_t*>(dst)[k] = (uint16_t)((uint8_t)o[2 * k] | ((uint32_t)(uint8_t)o[2 * k + 1] << 8));
+          }
+          continue;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < Q; k++) {
+        dst[k] = o[k];
+      }
+      continue;
+    }
+    int16_t o[Q];
     demap<MOD>(v.x, v.y, s, n, o);
     if constexpr (MOD >= 1) {
       if (s < evm_n) {  // hard decision (bit = !sign, evm.h HARD_DECISION), remodulated, error power
@@ -457,12 +607,12 @@ __global__ __launch_bounds__(LLR_THREADS) void llr_kernel(const float2* __restri
   llr_block<MOD>(sym, n, scramble, seed, bit0, csi, csi_max, llr, blockIdx.x);
 }
 
-template <int MOD>
+template <int MOD, bool B8>
 __global__ __launch_bounds__(LLR_THREADS) void llr_batch_kernel(const LlrItem* __restrict__ items)
 {
   const LlrItem& it = items[blockIdx.y];
-  llr_block<MOD>(reinterpret_cast<const float2*>(it.sym), it.n, it.scramble, it.seed, it.bit0, it.csi, it.csi_max,
-                 it.llr, blockIdx.x, it.evm_part, it.evm_n);
+  llr_block<MOD, B8>(reinterpret_cast<const float2*>(it.sym), it.n, it.scramble, it.seed, it.bit0, it.csi, it.csi_max,
+                     it.llr, blockIdx.x, it.evm_part, it.evm_n, it.llr8);
 }
 
 __global__ void evm_finalize_kernel(const EvmItem* __restrict__ items, uint32_t nitems)
@@ -489,7 +639,7 @@ hipError_t evm_finalize_launch(const EvmItem* d_items, uint32_t nitems, hipStrea
 }
 
 hipError_t llr_batch_launch(int mod, const LlrItem* d_items, uint32_t nitems, uint32_t max_n, int any_scramble,
-                            hipStream_t stream)
+                            hipStream_t stream, bool llr8)
 {
   StageScope timing_scope(ST_LLR, stream);
   if (nitems == 0 || max_n == 0) {
@@ -505,25 +655,24 @@ hipError_t llr_batch_launch(int mod, const LlrItem* d_items, uint32_t nitems, ui
     }
   }
   const dim3 grid((max_n + LLR_THREADS * SPT - 1) / (LLR_THREADS * SPT), nitems);
+#define LLR_CASE(M)                                                                                 \
+  case M:                                                                                           \
+    if (llr8) {                                                                                     \
+      hipLaunchKernelGGL((llr_batch_kernel<M, true>), grid, dim3(LLR_THREADS), 0, stream, d_items);  \
+    } else {                                                                                        \
+      hipLaunchKernelGGL((llr_batch_kernel<M, false>), grid, dim3(LLR_THREADS), 0, stream, d_items); \
+    }                                                                                               \
+    break;
   switch (mod) {
-    case 0:
-      hipLaunchKernelGGL(llr_batch_kernel<0>, grid, dim3(LLR_THREADS), 0, stream, d_items);
-      break;
-    case 1:
-      hipLaunchKernelGGL(llr_batch_kernel<1>, grid, dim3(LLR_THREADS), 0, stream, d_items);
-      break;
-    case 2:
-      hipLaunchKernelGGL(llr_batch_kernel<2>, grid, dim3(LLR_THREADS), 0, stream, d_items);
-      break;
-    case 3:
-      hipLaunchKernelGGL(llr_batch_kernel<3>, grid, dim3(LLR_THREADS), 0, stream, d_items);
-      break;
-    case 4:
-      hipLaunchKernelGGL(llr_batch_kernel<4>, grid, dim3(LLR_THREADS), 0, stream, d_items);
-      break;
+    LLR_CASE(0)
+    LLR_CASE(1)
+    LLR_CASE(2)
+    LLR_CASE(3)
+    LLR_CASE(4)
     default:
       return hipErrorInvalidValue;
   }
+#undef LLR_CASE
   return hipGetLastError();
 }
 

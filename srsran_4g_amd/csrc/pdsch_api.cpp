@@ -293,6 +293,7 @@ int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sf
     it.csi      = f.cfg->csi_enable ? d_csi + ((size_t)c.sf * 2 + c.cw) * max_re : nullptr;
     it.csi_max  = f.cfg->csi_enable ? d_max + 2 * c.sf + c.cw : nullptr;
     it.llr      = d_e + ((size_t)c.sf * 2 + c.tb) * max_re * kMaxQm;
+    it.llr8     = q->llr_is_8bit ? (int8_t*)it.llr : nullptr;  // the 8-bit chain writes int8 into the same slot
     it.n        = f.cfg->grant.nof_re;
     it.seed     = pdsch_seed(f.cfg->rnti, (int)c.cw, 2 * (f.tti % 10), q->cell.id);
     it.bit0     = 0;
@@ -375,7 +376,7 @@ int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sf
       mx = std::max(mx, hl[j].n);
       j++;
     }
-    if (llr_batch_launch(cws[order_l[i]].mod, dl + i, j - i, mx, 1, s) != hipSuccess) {
+    if (llr_batch_launch(cws[order_l[i]].mod, dl + i, j - i, mx, 1, s, q->llr_is_8bit) != hipSuccess) {
       return SRSRAN_ERROR;
     }
     i = j;
@@ -489,8 +490,8 @@ int srsran_pdsch_decode(srsran_pdsch_t*        q,
   if (!q || !q->gpu || !sf || !cfg || !channel || !sf_symbols || !data) {
     return SRSRAN_ERROR_INVALID_INPUTS;
   }
-  if (q->llr_is_8bit || q->dl_sch.llr_is_8bit) {
-    fprintf(stderr, "[srsran_pdsch] 8-bit LLRs are not provided\n");
+  if (q->llr_is_8bit != q->dl_sch.llr_is_8bit) {  // srsUE sets both (cc_worker.cc:108-110)
+    fprintf(stderr, "[srsran_pdsch] llr_is_8bit must match dl_sch.llr_is_8bit\n");
     return SRSRAN_ERROR;
   }
   PdschGpu*      g   = (PdschGpu*)q->gpu;
@@ -573,7 +574,7 @@ int srsran_pdsch_gpu_decode_batch(srsran_pdsch_t*              q,
   if (nof_sf == 0) {
     return 0;
   }
-  if (q->llr_is_8bit || q->dl_sch.llr_is_8bit) {
+  if (q->llr_is_8bit != q->dl_sch.llr_is_8bit) {
     return SRSRAN_ERROR;
   }
   hipStream_t s = (hipStream_t)stream;

@@ -301,7 +301,11 @@ struct SchCtx {
   size_t      hubs_cap = 0;
   uint8_t*    d_enc = nullptr;     // DL-SCH encode: descriptors, TB CRCs, unpacked e bits, staging
   size_t      enc_cap = 0;
+  short*      d_wide = nullptr;    // llr_is_8bit, K <= 800: the widened soft buffers the 16-bit decoders read
+  size_t      wide_cap = 0;        // rows of kWideStride
 };
+
+constexpr uint32_t kWideStride = 4096;  // int16 values a widened row (>= 3 (800 + 32) + 12 and the decoders' reads)
 
 constexpr size_t kDataCap = (size_t)SCH_MAX_CB * SCH_SLOT_BYTES;
 
@@ -355,7 +359,8 @@ int enqueue_batch(srsran_sch_t* q, uint32_t ntb, const srsran_dlsch_gpu_tb_t* tb
                   hipStream_t stream, bool early_copy = false, const uint32_t* out_idx = nullptr)
 {
   srsran_amd::HostScope desc(srsran_amd::HP_SCH_DESC);
-  SchCtx*           x = (SchCtx*)q->gpu;
+  SchCtx*           x  = (SchCtx*)q->gpu;
+  const bool        b8 = q->llr_is_8bit;  // int8 e bits / soft buffers (sch.c:409-428)
   std::vector<Plan> plan(ntb);
   uint32_t          nslots = 0;
   for (uint32_t i = 0; i < ntb; i++) {
@@ -378,7 +383,13 @@ int enqueue_batch(srsran_sch_t* q, uint32_t ntb, const srsran_dlsch_gpu_tb_t* tb
     const SbGpu*           sb = (const SbGpu*)tbs[i].softbuffer->gpu;
     const uint32_t         Qm = tbs[i].Qm;
     InvTable               tk[2];  // the de-matching tables of K1 and K2 (looked up once per TB)
-    if (!inv_table(s.K1_idx, tbs[i].rv, true, &tk[0]) || (s.C2 && !inv_table(s.K2_idx, tbs[i].rv, true, &tk[1]))) {
+    // the soft buffer layout of the decoder that takes K: the 16-bit AUTO one, or with llr_is_8bit the 8-bit one
+    // (rm_turbo_rx_lut_8bit: srsran_tdec_autoimp_get_subblocks_8bit)
+    auto table = [&](uint32_t idx, InvTable* t) {
+      return b8 ? inv_table_nsb(idx, tbs[i].rv, srsran_tdec_autoimp_get_subblocks_8bit(srsran_cbsegm_cbsize(idx)), t)
+                : inv_table(idx, tbs[i].rv, true, t);
+    };
+    if (!table(s.K1_idx, &tk[0]) || (s.C2 && !table(s.K2_idx, &tk[1]))) {
       return SRSRAN_ERROR;
     }
     for (uint32_t cb = 0; cb < s.C; cb++) {
@@ -395,7 +406,7 @@ int enqueue_batch(srsran_sch_t* q, uint32_t ntb, const srsran_dlsch_gpu_tb_t* tb
       const InvTable& t    = tk[cb < s.C1 ? 0 : 1];
       const uint32_t slot = plan[i].slot0 + cb;
       RmSlot&        r    = rm[slot];
-      r.e                 = tbs[i].d_e_bits + rp;
+      r.e                 = b8 ? (const short*)((const int8_t*)tbs[i].d_e_bits + rp) : tbs[i].d_e_bits + rp;
       r.sb                = sb->d_buf + (size_t)cb * sb->stride;
       r.skip              = sb->d_flags + cb;
       r.inv               = t.d;
@@ -411,16 +422,48 @@ int enqueue_batch(srsran_sch_t* q, uint32_t ntb, const srsran_dlsch_gpu_tb_t* tb
   }
   // turbo descriptors by K; every two consecutive blocks of a group (one lane-pair workgroup) lie
   // within TDEC_PAIR_SPAN of each other, padded where the soft buffers are far apart
+  // llr_is_8bit with K <= 800: the reference widens the block for a 16-bit decoder (tdec_iteration_8,
+  // turbodecoder.c:470-481); those rows are widened into d_wide first
+  std::vector<Widen8> wide;
+  uint32_t            max_wide = 0;
+  if (b8) {
+    for (auto& kv : by_k) {
+      if (srsran_tdec_autoimp_get_subblocks_8bit(kv.first) < 16) {
+        for (uint32_t slot : kv.second) {
+          wide.push_back(Widen8{(const int8_t*)rm[slot].sb, nullptr, rm[slot].len});
+          max_wide = std::max(max_wide, rm[slot].len);
+        }
+      }
+    }
+    if (wide.size() > x->wide_cap) {
+      if (x->used) {
+        hipEventSynchronize(x->done);
+      }
+      hipFree(x->d_wide);
+      x->d_wide         = nullptr;
+      const size_t rows = std::max(wide.size() * 2, (size_t)16);
+      if (hipMalloc((void**)&x->d_wide, rows * kWideStride * sizeof(short)) != hipSuccess) {
+        x->wide_cap = 0;
+        return SRSRAN_ERROR;
+      }
+      x->wide_cap = rows;
+    }
+    for (size_t j = 0; j < wide.size(); j++) {
+      wide[j].dst = x->d_wide + j * kWideStride;
+    }
+  }
   std::vector<TdecCb> cbs;
   cbs.reserve(nslots + 16);
   std::vector<std::pair<uint32_t, uint32_t>> groups;  // (K, first index into cbs)
   std::vector<TdecCb>                        kcbs;
+  uint32_t                                   nw = 0;
   for (auto& kv : by_k) {
     groups.emplace_back(kv.first, (uint32_t)cbs.size());
     kcbs.clear();
+    const bool widened = b8 && srsran_tdec_autoimp_get_subblocks_8bit(kv.first) < 16;
     for (uint32_t slot : kv.second) {
       TdecCb c;
-      c.in    = rm[slot].sb;
+      c.in    = widened ? wide[nw++].dst : rm[slot].sb;
       c.skip  = rm[slot].overwrite ? x->d_zero : rm[slot].skip;  // a new transmission decodes every CB
       c.slot  = slot;
       c.crc_a = slot_crc_a[slot];
@@ -466,9 +509,10 @@ int enqueue_batch(srsran_sch_t* q, uint32_t ntb, const srsran_dlsch_gpu_tb_t* tb
   if (x->used) {
     hipStreamWaitEvent(stream, x->done, 0);
   }
-  const size_t off_cbs = align16(nslots * sizeof(RmSlot));
-  const size_t off_tb  = off_cbs + align16(ncbs * sizeof(TdecCb));
-  const size_t bytes   = off_tb + align16(ntb * sizeof(SchTb));
+  const size_t off_cbs  = align16(nslots * sizeof(RmSlot));
+  const size_t off_tb   = off_cbs + align16(ncbs * sizeof(TdecCb));
+  const size_t off_wide = off_tb + align16(ntb * sizeof(SchTb));
+  const size_t bytes    = off_wide + align16(wide.size() * sizeof(Widen8));
   desc.stop();
   srsran_amd::HostScope wait(srsran_amd::HP_SCH_WAIT);
   if (x->used) {
@@ -534,6 +578,9 @@ int enqueue_batch(srsran_sch_t* q, uint32_t ntb, const srsran_dlsch_gpu_tb_t* tb
   memcpy(x->h_stage, rm.data(), nslots * sizeof(RmSlot));
   memcpy(x->h_stage + off_cbs, cbs.data(), ncbs * sizeof(TdecCb));
   memcpy(x->h_stage + off_tb, tbd.data(), ntb * sizeof(SchTb));
+  if (!wide.empty()) {
+    memcpy(x->h_stage + off_wide, wide.data(), wide.size() * sizeof(Widen8));
+  }
   // early_copy (the PDSCH chain, whose stream runs OFDM ... LLR before the de-matching): the upload runs on
   // the copy stream as soon as the previous batch is done with d_stage, beside those stages, and the
   // launches below wait for it instead of having the copy's latency in line in front of them (chain
@@ -557,15 +604,21 @@ int enqueue_batch(srsran_sch_t* q, uint32_t ntb, const srsran_dlsch_gpu_tb_t* tb
 
   int ret = SRSRAN_SUCCESS;
   if (nslots) {
-    if (rm_rx_launch((const RmSlot*)x->d_stage, nslots, max_len, max_e, stream) != hipSuccess) {
+    const hipError_t rme = b8 ? rm8_rx_slots_launch((const RmSlot*)x->d_stage, nslots, max_len, stream)
+                              : rm_rx_launch((const RmSlot*)x->d_stage, nslots, max_len, max_e, stream);
+    if (rme != hipSuccess ||
+        widen8_launch((const Widen8*)(x->d_stage + off_wide), (uint32_t)wide.size(), max_wide, stream) != hipSuccess) {
       ret = SRSRAN_ERROR;
     }
     const int n_end = q->max_iterations > 0 ? (int)q->max_iterations : 1;
     for (size_t g = 0; g < groups.size() && ret == SRSRAN_SUCCESS; g++) {
       const uint32_t first = groups[g].second;
       const uint32_t count = (g + 1 < groups.size() ? groups[g + 1].second : (uint32_t)cbs.size()) - first;
-      ret = tdec_sch_enqueue(groups[g].first, (const TdecCb*)(x->d_stage + off_cbs) + first, count, x->d_cbout,
-                             SCH_SLOT_BYTES, x->d_noi, x->d_crc_ok, n_end, stream);
+      const uint32_t K     = groups[g].first;
+      const TdecCb*  dcb   = (const TdecCb*)(x->d_stage + off_cbs) + first;
+      ret = b8 && srsran_tdec_autoimp_get_subblocks_8bit(K) >= 16
+                ? tdec8_sch_enqueue(K, dcb, count, x->d_cbout, SCH_SLOT_BYTES, x->d_noi, x->d_crc_ok, n_end, stream)
+                : tdec_sch_enqueue(K, dcb, count, x->d_cbout, SCH_SLOT_BYTES, x->d_noi, x->d_crc_ok, n_end, stream);
     }
   }
   if (ret == SRSRAN_SUCCESS && tb_launch((const SchTb*)(x->d_stage + off_tb), ntb, max_tbs, stream) != hipSuccess) {
@@ -1053,6 +1106,7 @@ void srsran_sch_free(srsran_sch_t* q)
     hipFree(x->d_ubs);
     hipHostFree(x->h_ubs);
     hipFree(x->d_enc);
+    hipFree(x->d_wide);
     delete x;
   }
   srsran_tdec_free(&q->decoder);
@@ -1099,13 +1153,14 @@ static int dlsch_decode_sync(srsran_sch_t*       q,
   if (s.F || s.C > sb->max_cb) {
     return SRSRAN_ERROR_INVALID_INPUTS;
   }
-  if (s.C > SRSRAN_MAX_CODEBLOCKS || q->llr_is_8bit) {
+  if (s.C > SRSRAN_MAX_CODEBLOCKS) {
     return SRSRAN_ERROR;
   }
   SchCtx*        x   = (SchCtx*)q->gpu;
   const uint32_t nbe = cfg->grant.tb[tb_idx].nof_bits;
+  const size_t   esz = q->llr_is_8bit ? sizeof(int8_t) : sizeof(int16_t);  // e_bits are int8 with llr_is_8bit
   hipStreamSynchronize(x->stream);
-  if (!d_e_bits && !grow_dev((void**)&x->d_e, &x->e_cap, std::max<size_t>(nbe, 1) * sizeof(int16_t))) {
+  if (!d_e_bits && !grow_dev((void**)&x->d_e, &x->e_cap, std::max<size_t>(nbe, 1) * esz)) {
     return SRSRAN_ERROR;
   }
   // the host cb_crc mirror is authoritative for the synchronous API
@@ -1115,7 +1170,7 @@ static int dlsch_decode_sync(srsran_sch_t*       q,
   }
   hipMemcpyAsync(g->d_flags, x->h_io, s.C, hipMemcpyHostToDevice, x->stream);
   if (!d_e_bits) {
-    hipMemcpyAsync(x->d_e, e_bits, (size_t)nbe * sizeof(int16_t), hipMemcpyHostToDevice, x->stream);
+    hipMemcpyAsync(x->d_e, e_bits, (size_t)nbe * esz, hipMemcpyHostToDevice, x->stream);
   }
   uint32_t end = 0;  // bytes of `data` the reference writes (sch.c:425-431, 476-480)
   for (uint32_t cb = 0; cb < s.C; cb++) {
@@ -1200,9 +1255,6 @@ int srsran_dlsch_gpu_decode_batch(srsran_sch_t*                q,
   if (nof_tb == 0) {
     return SRSRAN_SUCCESS;
   }
-  if (q->llr_is_8bit) {
-    return SRSRAN_ERROR;
-  }
   return enqueue_batch(q, nof_tb, tbs, d_result, d_avg_noi, (hipStream_t)stream);
 }
 
@@ -1218,9 +1270,6 @@ int dlsch_gpu_decode_batch_early_copy(srsran_sch_t* q, uint32_t nof_tb, const sr
   if (nof_tb == 0) {
     return SRSRAN_SUCCESS;
   }
-  if (q->llr_is_8bit) {
-    return SRSRAN_ERROR;
-  }
   return enqueue_batch(q, nof_tb, tbs, d_result, d_avg_noi, (hipStream_t)stream, true);
 }
 
@@ -1232,9 +1281,6 @@ int dlsch_gpu_decode_batch_limits(srsran_sch_t* q, uint32_t nof_tb, const srsran
   }
   if (nof_tb == 0) {
     return SRSRAN_SUCCESS;
-  }
-  if (q->llr_is_8bit) {
-    return SRSRAN_ERROR;
   }
   // distinct limits in first-appearance order; 0 keeps the limit in force, as pdsch.c:815-817 does
   std::vector<uint32_t> lim(nof_tb);
@@ -1693,6 +1739,10 @@ static int ulsch_decode_impl(srsran_sch_t*       q,
   if (!q || !q->gpu || !cfg || (!h_q && !d_q_ext)) {
     return SRSRAN_ERROR_INVALID_INPUTS;
   }
+  if (q->llr_is_8bit) {  // the 8-bit form is the UE's DL-SCH path (cc_worker.cc:108-110); UL-SCH stays int16
+    fprintf(stderr, "[srsran_sch] 8-bit UL-SCH LLRs are not provided\n");
+    return SRSRAN_ERROR;
+  }
   UlsPlan   p;
   const int prc = ulsch_plan(cfg, &p);
   if (prc != SRSRAN_SUCCESS) {
@@ -1872,6 +1922,9 @@ int ulsch_decode_batch_dev(srsran_sch_t* q, uint32_t n, UlschBatchUe* ues, const
   if (!q || !q->gpu || (n && !ues)) {
     return SRSRAN_ERROR_INVALID_INPUTS;
   }
+  if (q->llr_is_8bit) {
+    return SRSRAN_ERROR;
+  }
   SchCtx*              x = (SchCtx*)q->gpu;
   std::vector<UlsPlan> plan(n);
   std::vector<int32_t> uix(n, -1);  // index in the UCI arrays
@@ -2039,6 +2092,9 @@ int srsran_ulsch_gpu_decode_batch(srsran_sch_t*                q,
 {
   if (!q || !q->gpu || (nof_tb && (!tbs || !d_result || !d_avg_noi))) {
     return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  if (q->llr_is_8bit) {
+    return SRSRAN_ERROR;
   }
   std::vector<srsran_dlsch_gpu_tb_t> dl(nof_tb);
   std::vector<UlDeint>               desc(nof_tb);

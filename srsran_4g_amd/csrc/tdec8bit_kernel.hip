@@ -21,7 +21,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "crc24_dev.h"
+#include "sch_kernel.h"
 #include "tdec8bit_kernel.h"
+#include "tdec_kernel.h"
 
 namespace srsran_amd {
 namespace {
@@ -248,7 +251,8 @@ __device__ __forceinline__ int qpp_sb(int q, int K, int Ls, int nsb, uint32_t f1
   return (int)((fn % Ls) * nsb + fn / Ls);                            // deinter(., win)
 }
 
-template <int NSB>
+// ES: the DL-SCH form -- per-block descriptors, skipped blocks, CRC early stop (decode_tb_cb, sch.c:420-456)
+template <int NSB, bool ES>
 __global__ __launch_bounds__(64) void tdec8bit_kernel(Tdec8Args a)
 {
   constexpr int CPW = 64 / NSB;
@@ -260,7 +264,23 @@ __global__ __launch_bounds__(64) void tdec8bit_kernel(Tdec8Args a)
   const int      Ls   = K / NSB;
   const int      AL   = (K + 4 + 15) & ~15;
   const uint32_t cb   = blockIdx.x * CPW + cb_l;
-  const bool     live = cb < a.ncb;
+  uint32_t       slot = cb;
+  bool           live = cb < a.ncb;
+  bool           done = false;  // ES: the block's CRC passed (or it was skipped): no more work
+  if constexpr (ES) {
+    if (live) {
+      slot = a.cbs[cb].slot;
+      live = slot != TDEC_PAD_SLOT;
+    }
+    if (live && *a.cbs[cb].skip) {  // CRC already OK in the soft buffer (sch.c:392)
+      done = true;
+      if (d == 0) {
+        a.noi_out[slot] = 0;
+        a.crc_ok[slot]  = 1;
+      }
+    }
+  }
+  live = live && !done;
 
   int8_t* base = lds + (size_t)cb_l * 6 * AL;
   int8_t* SY   = base;           // systematic
@@ -275,7 +295,7 @@ __global__ __launch_bounds__(64) void tdec8bit_kernel(Tdec8Args a)
 
   // ---- input streams (turbodecoder_iter.h:61-96 / win.h:880-923) ----
   if (live) {
-    const int8_t* in = a.in + (size_t)cb * a.in_stride;
+    const int8_t* in = ES ? reinterpret_cast<const int8_t*>(a.cbs[cb].in) : a.in + (size_t)cb * a.in_stride;
     if (a.layout_sb) {
       for (int q = d; q < K; q += NSB) {
         SY[q] = in[q];
@@ -308,6 +328,7 @@ __global__ __launch_bounds__(64) void tdec8bit_kernel(Tdec8Args a)
   __syncthreads();
 
   uint2* beta = a.beta + (size_t)cb * (Ls + 1) * NSB;
+  const int nbytes = K / 8;
   for (int n = 0; n < a.n_end; n++) {
     if ((n & 1) == 0) {
       if (n && live) {
@@ -346,6 +367,54 @@ __global__ __launch_bounds__(64) void tdec8bit_kernel(Tdec8Args a)
       }
       __syncthreads();
     }
+    if constexpr (ES) {
+      // decision of this half-iteration (tdec_decision_byte after srsran_tdec_iteration_8bit) and the block's CRC
+      // (sch.c:433-456): lane d decides a contiguous byte range, CRCs it from zero, and the ranges combine by
+      // x^(8 * bytes after) (crc24_dev.h); the first CRC pass at >= min_iters half-iterations stops the block
+      const bool last = n + 1 == a.n_end;
+      const bool chk  = n + 1 >= a.min_iters;
+      if (live && (chk || last)) {
+        const int8_t*  src = ((n + 1) & 1) ? E1 : A1;
+        uint8_t*       out = a.out + (size_t)slot * a.out_stride;
+        const int      bpl = (nbytes + NSB - 1) / NSB;
+        const int      b0 = min(d * bpl, nbytes), b1 = min(b0 + bpl, nbytes);
+        const bool     crc_a = a.cbs[cb].crc_a != 0;
+        const uint32_t poly  = crc_a ? LTE_CRC24A : LTE_CRC24B;
+        uint32_t       crc   = 0;
+        for (int byte = b0; byte < b1; byte++) {
+          uint32_t v = 0;
+#pragma unroll
+          for (int b = 0; b < 8; b++) {
+            const int m = byte * 8 + b;
+            v |= (src[(m % Ls) * NSB + m / Ls] > 0 ? 1u : 0u) << (7 - b);
+          }
+          out[byte] = (uint8_t)v;
+          crc       = crc24_byte(crc, v, poly);
+        }
+        uint32_t part = b0 < b1 ? clmul_mod24(crc, (crc_a ? a.xpow_a : a.xpow_b)[nbytes - b1], poly) : 0u;
+#pragma unroll
+        for (int off = 1; off < NSB; off <<= 1) {
+          part ^= (uint32_t)__shfl_xor((int)part, off, 64);
+        }
+        if (chk && part == 0) {
+          done = true;
+          live = false;
+          if (d == 0) {
+            a.noi_out[slot] = (uint8_t)(n + 1);
+            a.crc_ok[slot]  = 1;
+          }
+        } else if (last && d == 0) {
+          a.noi_out[slot] = (uint8_t)a.n_end;
+          a.crc_ok[slot]  = 0;
+        }
+      }
+      if (__syncthreads_or(live ? 1 : 0) == 0) {
+        break;  // every block of the workgroup is done
+      }
+    }
+  }
+  if constexpr (ES) {
+    return;  // the decisions were written above
   }
 
   // ---- decision (turbodecoder.c:370-378, win.h:973-993): bit n = latest(SB slot of n) > 0 ----
@@ -386,7 +455,55 @@ __global__ void rm8_rx_kernel(const int8_t* e, int8_t* sb, const uint16_t* inv, 
   }
 }
 
+// the batch form: grid (positions / 256, slot)
+__global__ void rm8_rx_slots_kernel(const RmSlot* __restrict__ slots)
+{
+  const RmSlot&  r = slots[blockIdx.y];
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= r.len || (!r.overwrite && *r.skip)) {
+    return;
+  }
+  const uint32_t start = r.inv[p];
+  if (start == 0xFFFFu) {
+    return;
+  }
+  const int8_t* e   = reinterpret_cast<const int8_t*>(r.e);
+  int8_t*       sb  = reinterpret_cast<int8_t*>(r.sb);
+  int           acc = r.overwrite ? 0 : sb[p];  // a new transmission starts from the reset (zero) buffer
+  for (uint32_t k = start; k < r.E; k += r.N) {
+    acc += e[k];
+  }
+  sb[p] = (int8_t)acc;
+}
+
+__global__ void widen8_kernel(const Widen8* __restrict__ items)
+{
+  const Widen8&  w = items[blockIdx.y];
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < w.len) {
+    w.dst[i] = w.src[i];
+  }
+}
+
 }  // namespace
+
+hipError_t rm8_rx_slots_launch(const RmSlot* d_slots, uint32_t nslots, uint32_t max_len, hipStream_t stream)
+{
+  if (nslots == 0 || max_len == 0) {
+    return hipSuccess;
+  }
+  hipLaunchKernelGGL(rm8_rx_slots_kernel, dim3((max_len + 255) / 256, nslots), dim3(256), 0, stream, d_slots);
+  return hipGetLastError();
+}
+
+hipError_t widen8_launch(const Widen8* d_items, uint32_t n, uint32_t max_len, hipStream_t stream)
+{
+  if (n == 0 || max_len == 0) {
+    return hipSuccess;
+  }
+  hipLaunchKernelGGL(widen8_kernel, dim3((max_len + 255) / 256, n), dim3(256), 0, stream, d_items);
+  return hipGetLastError();
+}
 
 hipError_t rm8_rx_launch(const int8_t* e, int8_t* sb, const uint16_t* inv, uint32_t E, uint32_t len, uint32_t N,
                          hipStream_t stream)
@@ -415,10 +532,16 @@ hipError_t tdec8bit_launch(int nsb, const Tdec8Args& a, hipStream_t stream)
   const uint32_t cpw  = 64 / nsb;
   const dim3     grid((a.ncb + cpw - 1) / cpw);
   const size_t   lds  = tdec8bit_lds_bytes(nsb, a.K);
-  if (nsb == 16) {
-    hipLaunchKernelGGL(tdec8bit_kernel<16>, grid, dim3(64), lds, stream, a);
+  if (a.cbs) {
+    if (nsb == 16) {
+      hipLaunchKernelGGL((tdec8bit_kernel<16, true>), grid, dim3(64), lds, stream, a);
+    } else {
+      hipLaunchKernelGGL((tdec8bit_kernel<32, true>), grid, dim3(64), lds, stream, a);
+    }
+  } else if (nsb == 16) {
+    hipLaunchKernelGGL((tdec8bit_kernel<16, false>), grid, dim3(64), lds, stream, a);
   } else {
-    hipLaunchKernelGGL(tdec8bit_kernel<32>, grid, dim3(64), lds, stream, a);
+    hipLaunchKernelGGL((tdec8bit_kernel<32, false>), grid, dim3(64), lds, stream, a);
   }
   return hipGetLastError();
 }

@@ -340,6 +340,61 @@ int tdec_sch_enqueue(uint32_t      K,
 
 }  // namespace srsran_amd
 
+namespace {
+void* scratch8(hipStream_t stream, size_t bytes);
+}
+
+namespace srsran_amd {
+// DL-SCH decode with llr_is_8bit of ncb blocks of K > 800 (the 8-bit window decoders, 16 / 32 sub-blocks): int8 soft
+// buffers in the 8-bit layout, CRC early stop after >= 2 half-iterations, at most n_end half-iterations
+int tdec8_sch_enqueue(uint32_t      K,
+                      const TdecCb* d_cbs,
+                      uint32_t      ncb,
+                      uint8_t*      d_out,
+                      uint32_t      out_stride,
+                      uint8_t*      d_noi,
+                      uint8_t*      d_crc_ok,
+                      int           n_end,
+                      hipStream_t   stream)
+{
+  if (ncb == 0) {
+    return SRSRAN_SUCCESS;
+  }
+  const int      idx = cb_index(K);
+  const uint32_t nsb = srsran_tdec_autoimp_get_subblocks_8bit(K);
+  const XpowTables* xp = xpow_tables();
+  if (idx < 0 || (nsb != 16 && nsb != 32) || !xp) {
+    return SRSRAN_ERROR;
+  }
+  Tdec8Args a{};
+  a.in         = nullptr;
+  a.layout_sb  = 1;
+  a.K          = K;
+  a.ncb        = ncb;
+  a.n_end      = n_end > 0 ? n_end : 1;
+  a.out        = d_out;
+  a.cbs        = d_cbs;
+  a.out_stride = out_stride;
+  a.noi_out    = d_noi;
+  a.crc_ok     = d_crc_ok;
+  a.xpow_a     = xp->d[0];
+  a.xpow_b     = xp->d[1];
+  a.min_iters  = 2;  // SRSRAN_PDSCH_MIN_TDEC_ITERS (sch.c:35)
+  qpp_coeffs((uint32_t)idx, &a.f1, &a.f2);
+  a.beta = (uint2*)scratch8(stream, tdec8bit_beta_bytes((int)nsb, K, ncb));
+  if (!a.beta) {
+    return SRSRAN_ERROR;
+  }
+  const hipError_t e = tdec8bit_launch((int)nsb, a, stream);
+  tdec_set_last_kernel(nsb == 32 ? "tdec8bit_kernel<32>" : "tdec8bit_kernel<16>");
+  if (e != hipSuccess) {
+    fprintf(stderr, "[srsran_sch] 8-bit turbo launch failed: %s\n", hipGetErrorString(e));
+    return SRSRAN_ERROR;
+  }
+  return SRSRAN_SUCCESS;
+}
+}  // namespace srsran_amd
+
 extern "C" {
 
 uint32_t srsran_tdec_autoimp_get_subblocks(uint32_t long_cb)

@@ -134,6 +134,10 @@ int tdec_sch_enqueue(uint32_t      K,
                      uint8_t*      d_crc_ok,
                      int           n_end,
                      hipStream_t   stream);
+// the same with llr_is_8bit for K > 800 (tdec8bit_kernel.hip's 8-bit window decoders; int8 soft buffers in the
+// 8-bit decoder's layout)
+int tdec8_sch_enqueue(uint32_t K, const TdecCb* d_cbs, uint32_t ncb, uint8_t* d_out, uint32_t out_stride,
+                      uint8_t* d_noi, uint8_t* d_crc_ok, int n_end, hipStream_t stream);
 // Appends the n blocks of `src` to `dst` so that every aligned group of TDEC_GROUP consecutive entries
 // counted from `dst_group_start` (a workgroup of the lane-pair or single-lane decoder) lies within
 // TDEC_PAIR_SPAN: padding entries close a group before a block too far from the group's others.

@@ -367,6 +367,10 @@ class Sch:
         if lib().srsran_sch_init(ctypes.byref(self.q)) != 0:
             raise RuntimeError("srsran_sch_init failed (no HIP device?)")
 
+    def set_llr8(self, on=True):
+        """srsran_sch_t.llr_is_8bit: int8 e bits and the 8-bit decoders (sch.c:409-428)"""
+        self.q.llr_is_8bit = bool(on)
+
     def set_max_noi(self, n):
         lib().srsran_sch_set_max_noi(ctypes.byref(self.q), n)
 
@@ -388,9 +392,9 @@ class Sch:
         tb.nof_bits = len(e_bits)
         tb.enabled = True
         cfg.softbuffers.rx[tb_idx] = ctypes.pointer(softbuffer.s)
-        e = np.ascontiguousarray(e_bits, dtype=np.int16)
+        e = np.ascontiguousarray(e_bits, dtype=np.int8 if self.q.llr_is_8bit else np.int16)  # sch.c:380-381
         data = np.zeros(tbs // 8 + 64, np.uint8)
-        ret = lib().srsran_dlsch_decode2(ctypes.byref(self.q), ctypes.byref(cfg), e.ctypes.data_as(_i16p),
+        ret = lib().srsran_dlsch_decode2(ctypes.byref(self.q), ctypes.byref(cfg), ctypes.cast(e.ctypes.data, _i16p),
                                          data.ctypes.data_as(_u8p), tb_idx, nof_layers)
         return ret, data, self.last_noi()
 

@@ -374,6 +374,12 @@ class Pdsch:
         self.cell = cell_
         self.nrx = nof_rx
 
+    def set_llr8(self, on=True):
+        """the 8-bit LLR chain: pdsch.llr_is_8bit and pdsch.dl_sch.llr_is_8bit, as srsUE's pdsch_8bit_decoder sets
+        them (cc_worker.cc:108-110)"""
+        self.q.llr_is_8bit = bool(on)
+        self.q.dl_sch.llr_is_8bit = bool(on)
+
     def encode(self, cfg, tti, cfi, payloads, grids):
         """srsran_pdsch_encode into (a copy of) the ports' host grids -> (ret, grids)"""
         g = [np.array(x, np.complex64, copy=True) for x in grids]
@@ -434,6 +440,11 @@ class UeDl:
         self.nrx = nof_rx
         self.cfg = srsran_ue_dl_cfg_t()
         self.cfg.chest_cfg = srsue_chest_cfg()
+
+    def set_llr8(self, on=True):
+        """srsUE's pdsch_8bit_decoder (cc_worker.cc:108-110): ue_dl.pdsch.llr_is_8bit and its dl_sch's"""
+        self.q.pdsch.llr_is_8bit = bool(on)
+        self.q.pdsch.dl_sch.llr_is_8bit = bool(on)
 
     def fft_estimate(self, samples, tti, cfi):
         x = [np.ascontiguousarray(v, np.complex64) for v in samples]

@@ -732,6 +732,18 @@ struct StreamPool {
 std::mutex               g_pool_mu;
 std::vector<StreamPool*> g_pools;
 
+// How the classes of a fused multi-size call share the device (SRSRAN_AMD_TDEC_MULTI, read once):
+// 0 "streams": one pool stream a class, equal priority; 1 "priority": the first (longest) class's stream at the
+// device's highest priority, the others at the lowest; 2 "serial": every class on one stream, longest first.
+int multi_mode()
+{
+  static const int m = [] {
+    const char* e = getenv("SRSRAN_AMD_TDEC_MULTI");
+    return !e ? 0 : !strcmp(e, "priority") ? 1 : !strcmp(e, "serial") ? 2 : 0;
+  }();
+  return m;
+}
+
 StreamPool* get_pool()
 {
   int dev = 0;
@@ -746,8 +758,12 @@ StreamPool* get_pool()
   }
   StreamPool* p = new StreamPool();
   p->device     = dev;
+  int lo = 0, hi = 0;
+  if (multi_mode() == 1 && hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) {
+    lo = hi = 0;
+  }
   for (int i = 0; i < kPoolStreams; i++) {
-    if (hipStreamCreateWithFlags(&p->s[i], hipStreamNonBlocking) != hipSuccess ||
+    if (hipStreamCreateWithPriority(&p->s[i], hipStreamNonBlocking, i == 0 ? hi : lo) != hipSuccess ||
         hipEventCreateWithFlags(&p->done[i], hipEventDisableTiming) != hipSuccess) {
       return nullptr;
     }
@@ -857,7 +873,7 @@ int srsran_tdec_gpu_run_multi(uint32_t              nof_groups,
     if (gs.empty()) {
       continue;
     }
-    hipStream_t st = p->s[ci];
+    hipStream_t st = p->s[multi_mode() == 2 ? 0 : ci];
     if (gs.size() == 1) {
       const uint32_t g = gs[0];
       ret = enqueue(cfg[g], d_input[g], in_stride[g], layout_sb, d_output[g], nof_cb[g], 0, n_end, nullptr, st);

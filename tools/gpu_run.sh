@@ -6,6 +6,7 @@
 #   tests[:PYTEST_SELECTION]   pytest -m gpu (default: tests), e.g. tests:tests/test_pusch_gpu.py
 #   smoke                      __graft_entry__.smoke()
 #   bench:NAME[:ARGS]          python bench.py ARGS > bench_NAME.json (ARGS space-separated, e.g. "--steps 10")
+#   benche:NAME:ENV:ARGS       the same with ENV (VAR=VAL[,VAR=VAL]) in the environment
 #   prof:NAME[:ARGS]           rocprofv3 --kernel-trace --stats of bench.py ARGS -> prof_NAME/
 #   pmc:NAME[:ARGS]            tools/pmc_tdec.sh passes over tools/tdec_kernels.py ARGS -> NAME/
 #   py:NAME:SCRIPT[ ARGS]      python SCRIPT ARGS > NAME.log
@@ -31,6 +32,11 @@ for STEP in "$@"; do
       tail -2 $OUT/smoke.log ;;
     bench)
       timeout -k 10 900 python bench.py $ARGS > $OUT/bench_$NAME.json 2> $OUT/bench_$NAME.err \
+        || { tail -5 $OUT/bench_$NAME.err; exit 1; }
+      python tools/bench_brief.py $OUT/bench_$NAME.json ;;
+    benche)  # benche:NAME:VAR=VAL[,VAR=VAL]:ARGS -- bench with environment settings
+      ENVS=${ARGS%%:*}; BARGS=${ARGS#*:}; [ "$BARGS" = "$ARGS" ] && BARGS=""
+      timeout -k 10 900 env ${ENVS//,/ } python bench.py $BARGS > $OUT/bench_$NAME.json 2> $OUT/bench_$NAME.err \
         || { tail -5 $OUT/bench_$NAME.err; exit 1; }
       python tools/bench_brief.py $OUT/bench_$NAME.json ;;
     prof)

@@ -39,15 +39,24 @@ struct Table {
 using TableKey = std::array<uint64_t, 5>;  // RE table cache key (get_table)
 static_assert(SRSRAN_MAX_PRB <= 128, "two 64-bit words of PRB bitmap per slot");
 
+// Descriptor staging of one batch (pinned host + device copy).  A ring of kStageRing of them lets the host build
+// batch N + 1 .. N + kStageRing - 1 while the GPU still reads batch N's descriptors: the host waits only for the
+// batch kStageRing back, so a stall of the calling thread shorter than that many batches leaves the GPU busy.
+constexpr int kStageRing = 3;
+struct StageSlot {
+  hipEvent_t staged = nullptr;  // this slot's last upload finished (pinned staging reusable)
+  hipEvent_t read   = nullptr;  // the launches that read this slot's device copy are done
+  bool       used   = false;
+  char*      h      = nullptr;
+  char*      d      = nullptr;
+  size_t     cap    = 0;
+};
+
 struct PdschGpu {
   hipStream_t                  stream  = nullptr;  // host-synchronous path
   hipStream_t                  copy    = nullptr;  // descriptor uploads, ahead of the launches that read them
-  hipEvent_t                   staged  = nullptr;  // descriptor upload finished (pinned staging reusable)
-  hipEvent_t                   read    = nullptr;  // the last launches that read d_stage are done
-  bool                         used    = false;
-  char*                        h_stage = nullptr;
-  char*                        d_stage = nullptr;
-  size_t                       stage_cap = 0;
+  StageSlot                    ring[kStageRing];
+  uint32_t                     ring_next = 0;
   char*                        d_work    = nullptr;
   size_t                       work_cap  = 0;
   float2*                      d_in      = nullptr;  // host-synchronous path: grids + estimates
@@ -85,22 +94,35 @@ bool grow_dev(void** p, size_t* cap, size_t need)
   return true;
 }
 
-bool grow_stage(PdschGpu* g, size_t need)
+bool grow_stage(StageSlot& st, size_t need)
 {
-  if (g->stage_cap >= need) {
+  if (st.cap >= need) {
     return true;
   }
-  hipDeviceSynchronize();
-  hipHostFree(g->h_stage);
-  hipFree(g->d_stage);
-  g->h_stage = nullptr;
-  g->d_stage = nullptr;
-  g->stage_cap = 0;
-  need = std::max(need, (size_t)65536);
-  if (hipHostMalloc((void**)&g->h_stage, need) != hipSuccess || hipMalloc((void**)&g->d_stage, need) != hipSuccess) {
+  if (st.used) {
+    hipEventSynchronize(st.read);
+  }
+  hipHostFree(st.h);
+  hipFree(st.d);
+  st.h   = nullptr;
+  st.d   = nullptr;
+  st.cap = 0;
+  need   = std::max(need, (size_t)65536);
+  if (hipHostMalloc((void**)&st.h, need) != hipSuccess || hipMalloc((void**)&st.d, need) != hipSuccess) {
     return false;
   }
-  g->stage_cap = need;
+  st.cap = need;
+  return true;
+}
+
+bool init_ring(PdschGpu* g)
+{
+  for (StageSlot& st : g->ring) {
+    if (hipEventCreateWithFlags(&st.staged, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&st.read, hipEventDisableTiming) != hipSuccess || !grow_stage(st, 65536)) {
+      return false;
+    }
+  }
   return true;
 }
 
@@ -324,13 +346,15 @@ int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sf
   const size_t ev_bytes = align256(evs.size() * sizeof(EvmItem));
   desc.stop();
   srsran_amd::HostScope wait(srsran_amd::HP_PDSCH_WAIT);
-  if (hipEventSynchronize(g->staged) != hipSuccess || !grow_stage(g, pa_bytes + li_bytes + ev_bytes)) {
+  StageSlot& st    = g->ring[g->ring_next];
+  g->ring_next = (g->ring_next + 1) % kStageRing;
+  if ((st.used && hipEventSynchronize(st.staged) != hipSuccess) || !grow_stage(st, pa_bytes + li_bytes + ev_bytes)) {
     return SRSRAN_ERROR;
   }
   wait.stop();
   srsran_amd::HostScope launch(srsran_amd::HP_PDSCH_LAUNCH);
-  PredArgs* hp = (PredArgs*)g->h_stage;
-  LlrItem*  hl = (LlrItem*)(g->h_stage + pa_bytes);
+  PredArgs* hp = (PredArgs*)st.h;
+  LlrItem*  hl = (LlrItem*)(st.h + pa_bytes);
   for (uint32_t i = 0; i < nsf; i++) {
     hp[i] = pa[order_p[i]];
   }
@@ -338,27 +362,27 @@ int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sf
     hl[i] = li[order_l[i]];
   }
   if (!evs.empty()) {
-    memcpy(g->h_stage + pa_bytes + li_bytes, evs.data(), evs.size() * sizeof(EvmItem));
+    memcpy(st.h + pa_bytes + li_bytes, evs.data(), evs.size() * sizeof(EvmItem));
   }
-  // the upload on the copy stream once the previous batch's predecode / LLR launches are done with
-  // d_stage: it runs beside the OFDM / estimation stages instead of in line in front of the predecoder
-  if (g->used) {
-    hipStreamWaitEvent(g->copy, g->read, 0);
+  // the upload on the copy stream once the launches of the batch that last used this slot are done with its
+  // device copy: it runs beside the OFDM / estimation stages instead of in line in front of the predecoder
+  if (st.used) {
+    hipStreamWaitEvent(g->copy, st.read, 0);
   }
-  hipMemcpyAsync(g->d_stage, g->h_stage, pa_bytes + li_bytes + ev_bytes, hipMemcpyHostToDevice, g->copy);
-  hipEventRecord(g->staged, g->copy);
-  hipStreamWaitEvent(s, g->staged, 0);
-  g->used = true;
-  // from here on d_stage belongs to this batch: g->read is recorded on every exit, so the next batch's
-  // upload waits for whatever of this one was enqueued, error paths included
+  hipMemcpyAsync(st.d, st.h, pa_bytes + li_bytes + ev_bytes, hipMemcpyHostToDevice, g->copy);
+  hipEventRecord(st.staged, g->copy);
+  hipStreamWaitEvent(s, st.staged, 0);
+  st.used = true;
+  // from here on the slot belongs to this batch: its read event is recorded on every exit, so the upload that
+  // next reuses it waits for whatever of this one was enqueued, error paths included
   struct ReadMark {
-    PdschGpu*   g;
+    StageSlot&      st;
     hipStream_t s;
-    ~ReadMark() { hipEventRecord(g->read, s); }
-  } mark{g, s};
+    ~ReadMark() { hipEventRecord(st.read, s); }
+  } mark{st, s};
   hipMemsetAsync(d_max, 0, (size_t)nsf * 2 * sizeof(float), s);
-  const PredArgs* dp = (const PredArgs*)g->d_stage;
-  const LlrItem*  dl = (const LlrItem*)(g->d_stage + pa_bytes);
+  const PredArgs* dp = (const PredArgs*)st.d;
+  const LlrItem*  dl = (const LlrItem*)(st.d + pa_bytes);
   for (uint32_t i = 0; i < nsf;) {  // one launch per predecoder scheme
     uint32_t j = i, mx = 0;
     while (j < nsf && hp[j].scheme == hp[i].scheme) {
@@ -382,7 +406,7 @@ int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sf
     i = j;
   }
   if (!evs.empty() &&
-      evm_finalize_launch((const EvmItem*)(g->d_stage + pa_bytes + li_bytes), (uint32_t)evs.size(), s) != hipSuccess) {
+      evm_finalize_launch((const EvmItem*)(st.d + pa_bytes + li_bytes), (uint32_t)evs.size(), s) != hipSuccess) {
     return SRSRAN_ERROR;
   }
   return SRSRAN_SUCCESS;
@@ -410,8 +434,7 @@ int srsran_pdsch_init_ue(srsran_pdsch_t* q, uint32_t max_prb, uint32_t nof_rx_an
   g->evm_max_bits = (uint32_t)std::max(0, srsran_ra_tbs_from_idx(SRSRAN_RA_NOF_TBS_IDX - 1, 6));  // pdsch.c:297
   if (hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&g->copy, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&g->staged, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&g->read, hipEventDisableTiming) != hipSuccess || !grow_stage(g, 65536)) {
+      !init_ring(g)) {
     srsran_pdsch_free(q);
     return SRSRAN_ERROR;
   }
@@ -431,13 +454,15 @@ void srsran_pdsch_free(srsran_pdsch_t* q)
     }
     hipFree(g->d_work);
     hipFree(g->d_in);
-    hipFree(g->d_stage);
-    hipHostFree(g->h_stage);
-    if (g->staged) {
-      hipEventDestroy(g->staged);
-    }
-    if (g->read) {
-      hipEventDestroy(g->read);
+    for (StageSlot& st : g->ring) {
+      hipFree(st.d);
+      hipHostFree(st.h);
+      if (st.staged) {
+        hipEventDestroy(st.staged);
+      }
+      if (st.read) {
+        hipEventDestroy(st.read);
+      }
     }
     if (g->stream) {
       hipStreamDestroy(g->stream);

@@ -263,14 +263,24 @@ uint32_t softbuffer_data_stride(srsran_softbuffer_rx_t* q) { return q && q->gpu 
 namespace {
 
 // ---------------- sch object device context ----------------
+// Descriptor staging of one batch.  A ring of kStageRing slots: the host builds the next batches while the GPU
+// still reads earlier ones' descriptors, and waits only for the slot's previous user (kStageRing batches back).
+constexpr int kStageRing = 3;
+struct StageSlot {
+  hipEvent_t staged = nullptr;  // this slot's last upload done (pinned staging reusable)
+  hipEvent_t done   = nullptr;  // the batch that last used this slot finished with its descriptors
+  bool       used   = false;
+  char*      h      = nullptr;
+  char*      d      = nullptr;
+  size_t     cap    = 0;
+};
+
 struct SchCtx {
   hipStream_t stream = nullptr;
   hipStream_t copy   = nullptr;  // descriptor uploads of the batch path, ahead of the launches that read them
-  hipEvent_t  staged = nullptr;  // descriptor upload done (pinned staging reusable)
-  hipEvent_t  done   = nullptr;  // last batch finished with the descriptors / scratch
-  char*       h_stage = nullptr;
-  char*       d_stage = nullptr;
-  size_t      stage_cap = 0;
+  hipEvent_t  done   = nullptr;  // last batch finished with the shared scratch (cbout, flags, chunk CRCs, wide rows)
+  StageSlot   ring[kStageRing];
+  uint32_t    ring_next = 0;
   uint8_t*    d_cbout = nullptr;
   uint8_t*    d_noi = nullptr;
   uint8_t*    d_crc_ok = nullptr;
@@ -310,6 +320,17 @@ constexpr uint32_t kWideStride = 4096;  // int16 values a widened row (>= 3 (800
 constexpr size_t kDataCap = (size_t)SCH_MAX_CB * SCH_SLOT_BYTES;
 
 size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+bool init_ring(SchCtx* x)
+{
+  for (StageSlot& st : x->ring) {
+    if (hipEventCreateWithFlags(&st.staged, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&st.done, hipEventDisableTiming) != hipSuccess) {
+      return false;
+    }
+  }
+  return true;
+}
 
 bool grow_dev(void** p, size_t* cap, size_t need)
 {
@@ -505,7 +526,7 @@ int enqueue_batch(srsran_sch_t* q, uint32_t ntb, const srsran_dlsch_gpu_tb_t* tb
     t.tbs           = plan[i].s.tbs;
   }
 
-  // the previous batch of this object must be done with staging and scratch
+  // the previous batch of this object must be done with the shared scratch
   if (x->used) {
     hipStreamWaitEvent(stream, x->done, 0);
   }
@@ -515,29 +536,33 @@ int enqueue_batch(srsran_sch_t* q, uint32_t ntb, const srsran_dlsch_gpu_tb_t* tb
   const size_t bytes    = off_wide + align16(wide.size() * sizeof(Widen8));
   desc.stop();
   srsran_amd::HostScope wait(srsran_amd::HP_SCH_WAIT);
-  if (x->used) {
-    hipEventSynchronize(x->staged);
+  StageSlot& st    = x->ring[x->ring_next];
+  x->ring_next = (x->ring_next + 1) % kStageRing;
+  if (st.used) {
+    hipEventSynchronize(st.staged);
   }
   wait.stop();
   srsran_amd::HostScope launch(srsran_amd::HP_SCH_LAUNCH);
-  if (bytes > x->stage_cap || nslots > x->slot_cap) {
+  if (bytes > st.cap) {
+    if (st.used) {
+      hipEventSynchronize(st.done);
+    }
+    hipHostFree(st.h);
+    hipFree(st.d);
+    st.h             = nullptr;
+    st.d             = nullptr;
+    const size_t cap = std::max(bytes * 2, (size_t)4096);
+    if (hipHostMalloc((void**)&st.h, cap, hipHostMallocDefault) != hipSuccess || hipMalloc((void**)&st.d, cap) != hipSuccess) {
+      st.cap = 0;
+      return SRSRAN_ERROR;
+    }
+    st.cap = cap;
+  }
+  if (nslots > x->slot_cap) {
     if (x->used) {
       hipEventSynchronize(x->done);
     }
-    if (bytes > x->stage_cap) {
-      hipHostFree(x->h_stage);
-      hipFree(x->d_stage);
-      x->h_stage   = nullptr;
-      x->d_stage   = nullptr;
-      const size_t cap = std::max(bytes * 2, (size_t)4096);
-      if (hipHostMalloc((void**)&x->h_stage, cap, hipHostMallocDefault) != hipSuccess ||
-          hipMalloc((void**)&x->d_stage, cap) != hipSuccess) {
-        x->stage_cap = 0;
-        return SRSRAN_ERROR;
-      }
-      x->stage_cap = cap;
-    }
-    if (nslots > x->slot_cap) {
+    {
       const size_t cap = std::max((size_t)nslots * 2, (size_t)64);
       hipFree(x->d_cbout);
       hipFree(x->d_noi);
@@ -575,39 +600,41 @@ int enqueue_batch(srsran_sch_t* q, uint32_t ntb, const srsran_dlsch_gpu_tb_t* tb
       max_tbs  = std::max(max_tbs, t.tbs);
     }
   }
-  memcpy(x->h_stage, rm.data(), nslots * sizeof(RmSlot));
-  memcpy(x->h_stage + off_cbs, cbs.data(), ncbs * sizeof(TdecCb));
-  memcpy(x->h_stage + off_tb, tbd.data(), ntb * sizeof(SchTb));
+  memcpy(st.h, rm.data(), nslots * sizeof(RmSlot));
+  memcpy(st.h + off_cbs, cbs.data(), ncbs * sizeof(TdecCb));
+  memcpy(st.h + off_tb, tbd.data(), ntb * sizeof(SchTb));
   if (!wide.empty()) {
-    memcpy(x->h_stage + off_wide, wide.data(), wide.size() * sizeof(Widen8));
+    memcpy(st.h + off_wide, wide.data(), wide.size() * sizeof(Widen8));
   }
   // early_copy (the PDSCH chain, whose stream runs OFDM ... LLR before the de-matching): the upload runs on
-  // the copy stream as soon as the previous batch is done with d_stage, beside those stages, and the
+  // the copy stream as soon as the slot's previous batch is done with it, beside those stages, and the
   // launches below wait for it instead of having the copy's latency in line in front of them (chain
   // 243-246 k -> 250-255 k subframes/s, gpurun_out r03ah).  A batch with nothing in front of it keeps the
   // in-stream upload (the cross-stream wait costs a standalone DL-SCH batch ~10 us).
   hipStream_t up = stream;
   if (early_copy) {
     up = x->copy;
-    if (x->used) {
-      hipStreamWaitEvent(up, x->done, 0);
+    if (st.used) {
+      hipStreamWaitEvent(up, st.done, 0);
     }
   }
-  if (hipMemcpyAsync(x->d_stage, x->h_stage, bytes, hipMemcpyHostToDevice, up) != hipSuccess) {
+  if (hipMemcpyAsync(st.d, st.h, bytes, hipMemcpyHostToDevice, up) != hipSuccess) {
     return SRSRAN_ERROR;
   }
-  hipEventRecord(x->staged, up);
+  hipEventRecord(st.staged, up);
   if (early_copy) {
-    hipStreamWaitEvent(stream, x->staged, 0);
+    hipStreamWaitEvent(stream, st.staged, 0);
   }
-  x->used = true;
+  x->used  = true;
+  st.used  = true;
+  char* ds = st.d;
 
   int ret = SRSRAN_SUCCESS;
   if (nslots) {
-    const hipError_t rme = b8 ? rm8_rx_slots_launch((const RmSlot*)x->d_stage, nslots, max_len, stream)
-                              : rm_rx_launch((const RmSlot*)x->d_stage, nslots, max_len, max_e, stream);
+    const hipError_t rme = b8 ? rm8_rx_slots_launch((const RmSlot*)ds, nslots, max_len, stream)
+                              : rm_rx_launch((const RmSlot*)ds, nslots, max_len, max_e, stream);
     if (rme != hipSuccess ||
-        widen8_launch((const Widen8*)(x->d_stage + off_wide), (uint32_t)wide.size(), max_wide, stream) != hipSuccess) {
+        widen8_launch((const Widen8*)(ds + off_wide), (uint32_t)wide.size(), max_wide, stream) != hipSuccess) {
       ret = SRSRAN_ERROR;
     }
     const int n_end = q->max_iterations > 0 ? (int)q->max_iterations : 1;
@@ -615,16 +642,17 @@ int enqueue_batch(srsran_sch_t* q, uint32_t ntb, const srsran_dlsch_gpu_tb_t* tb
       const uint32_t first = groups[g].second;
       const uint32_t count = (g + 1 < groups.size() ? groups[g + 1].second : (uint32_t)cbs.size()) - first;
       const uint32_t K     = groups[g].first;
-      const TdecCb*  dcb   = (const TdecCb*)(x->d_stage + off_cbs) + first;
+      const TdecCb*  dcb   = (const TdecCb*)(ds + off_cbs) + first;
       ret = b8 && srsran_tdec_autoimp_get_subblocks_8bit(K) >= 16
                 ? tdec8_sch_enqueue(K, dcb, count, x->d_cbout, SCH_SLOT_BYTES, x->d_noi, x->d_crc_ok, n_end, stream)
                 : tdec_sch_enqueue(K, dcb, count, x->d_cbout, SCH_SLOT_BYTES, x->d_noi, x->d_crc_ok, n_end, stream);
     }
   }
-  if (ret == SRSRAN_SUCCESS && tb_launch((const SchTb*)(x->d_stage + off_tb), ntb, max_tbs, stream) != hipSuccess) {
+  if (ret == SRSRAN_SUCCESS && tb_launch((const SchTb*)(ds + off_tb), ntb, max_tbs, stream) != hipSuccess) {
     ret = SRSRAN_ERROR;
   }
   hipEventRecord(x->done, stream);
+  hipEventRecord(st.done, stream);
   return ret;
 }
 
@@ -1051,8 +1079,7 @@ int srsran_sch_init(srsran_sch_t* q)
   q->gpu            = x;
   if (hipStreamCreateWithFlags(&x->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&x->copy, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&x->staged, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&x->done, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&x->done, hipEventDisableTiming) != hipSuccess || !init_ring(x) ||
       hipMalloc((void**)&x->d_data, kDataCap) != hipSuccess || hipMalloc((void**)&x->d_res, 16) != hipSuccess ||
       hipMalloc((void**)&x->d_avg, 16) != hipSuccess ||
       hipHostMalloc((void**)&x->h_io, 256, hipHostMallocDefault) != hipSuccess ||
@@ -1078,14 +1105,19 @@ void srsran_sch_free(srsran_sch_t* q)
       hipStreamSynchronize(x->copy);
       hipStreamDestroy(x->copy);
     }
-    if (x->staged) {
-      hipEventDestroy(x->staged);
-    }
     if (x->done) {
       hipEventDestroy(x->done);
     }
-    hipHostFree(x->h_stage);
-    hipFree(x->d_stage);
+    for (StageSlot& st : x->ring) {
+      if (st.staged) {
+        hipEventDestroy(st.staged);
+      }
+      if (st.done) {
+        hipEventDestroy(st.done);
+      }
+      hipHostFree(st.h);
+      hipFree(st.d);
+    }
     hipFree(x->d_cbout);
     hipFree(x->d_noi);
     hipFree(x->d_crc_ok);

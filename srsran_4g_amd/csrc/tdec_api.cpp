@@ -492,11 +492,11 @@ const char* srsran_tdec_gpu_kernel_name_batch(uint32_t long_cb, uint32_t nof_cb)
   if (nsb == 16) {
     const int k = tdec16_choice(nof_cb);
     if (k) {
-      return k == 2 ? (nof_cb <= tdecs_split_max_cb() ? "tdec16s_split_kernel" : "tdec16s_kernel") : "tdec16_kernel";
+      return k == 2 ? "tdec16s_kernel" : "tdec16_kernel";
     }
   }
   if (nsb == 8 && nof_cb >= tdec8s_min_cb()) {
-    return nof_cb <= tdecs_split_max_cb() ? "tdec8s_split_kernel" : "tdec8s_kernel";
+    return "tdec8s_kernel";
   }
   if (nsb == 1 && nof_cb >= tdec1s_min_cb()) {
     return "tdec1s_kernel";

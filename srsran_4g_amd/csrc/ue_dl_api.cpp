@@ -21,9 +21,12 @@
 
 namespace {
 
+constexpr int kStageRing = 3;  // batches whose sf-index upload may be in flight (a ring, as the PDSCH / SCH staging)
+
 struct UeDlGpu {
-  hipEvent_t staged = nullptr;  // sf-index upload finished
-  uint32_t*  h_sf   = nullptr;  // pinned
+  hipEvent_t staged[kStageRing] = {};  // sf-index upload of the slot finished
+  uint32_t   ring_next          = 0;
+  uint32_t*  h_sf   = nullptr;  // pinned, kStageRing slots of cap entries
   uint32_t*  d_sf   = nullptr;
   float2*    d_grid = nullptr;
   float2*    d_ce   = nullptr;
@@ -74,8 +77,8 @@ bool grow(srsran_ue_dl_t* q, UeDlGpu* g, uint32_t nsf, bool full)
   const size_t nre   = 12 * (size_t)q->cell.nof_prb;
   const size_t nrx   = q->nof_rx_antennas;
   const size_t ports = q->cell.nof_ports;
-  if (hipHostMalloc((void**)&g->h_sf, nsf * sizeof(uint32_t)) != hipSuccess ||
-      hipMalloc((void**)&g->d_sf, nsf * sizeof(uint32_t)) != hipSuccess ||
+  if (hipHostMalloc((void**)&g->h_sf, kStageRing * nsf * sizeof(uint32_t)) != hipSuccess ||
+      hipMalloc((void**)&g->d_sf, kStageRing * nsf * sizeof(uint32_t)) != hipSuccess ||
       hipMalloc((void**)&g->d_grid, nsf * nrx * 14 * nre * sizeof(float2)) != hipSuccess ||
       hipMalloc((void**)&g->d_ce, nsf * ports * nrx * nre * (full ? 14 : 1) * sizeof(float2)) != hipSuccess ||
       hipMalloc((void**)&g->d_res, nsf * 4 * sizeof(float)) != hipSuccess) {
@@ -130,9 +133,11 @@ int srsran_ue_dl_init(srsran_ue_dl_t* q, cf_t* input[SRSRAN_MAX_PORTS], uint32_t
   }
   UeDlGpu* g = new UeDlGpu();
   q->gpu     = g;
-  if (hipEventCreateWithFlags(&g->staged, hipEventDisableTiming) != hipSuccess) {
-    srsran_ue_dl_free(q);
-    return SRSRAN_ERROR;
+  for (hipEvent_t& e : g->staged) {
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+      srsran_ue_dl_free(q);
+      return SRSRAN_ERROR;
+    }
   }
   if (nof_rx_antennas <= 2) {
     if (srsran_pcfich_init(&g->pcfich, nof_rx_antennas) || srsran_pdcch_init_ue(&g->pdcch, max_prb, nof_rx_antennas)) {
@@ -157,8 +162,10 @@ void srsran_ue_dl_free(srsran_ue_dl_t* q)
     hipFree(g->d_grid);
     hipFree(g->d_ce);
     hipFree(g->d_res);
-    if (g->staged) {
-      hipEventDestroy(g->staged);
+    for (hipEvent_t e : g->staged) {
+      if (e) {
+        hipEventDestroy(e);
+      }
     }
     if (g->ctrl_init) {
       srsran_pcfich_free(&g->pcfich);
@@ -307,18 +314,22 @@ int srsran_ue_dl_gpu_decode_batch(srsran_ue_dl_t*              q,
   UeDlGpu*    g    = (UeDlGpu*)q->gpu;
   hipStream_t s    = (hipStream_t)stream;
   const bool  full = cfg->chest_cfg.estimator_alg == SRSRAN_ESTIMATOR_ALG_INTERPOLATE;  // every symbol its own row
-  if (!grow(q, g, nof_sf, full) || hipEventSynchronize(g->staged) != hipSuccess) {
+  const uint32_t slot = g->ring_next;
+  g->ring_next        = (slot + 1) % kStageRing;
+  if (!grow(q, g, nof_sf, full) || hipEventSynchronize(g->staged[slot]) != hipSuccess) {
     return SRSRAN_ERROR;
   }
+  uint32_t* h_sf = g->h_sf + (size_t)slot * g->cap;
+  uint32_t* d_sf = g->d_sf + (size_t)slot * g->cap;
   for (uint32_t b = 0; b < nof_sf; b++) {
-    g->h_sf[b] = sfs[b].tti % 10;
+    h_sf[b] = sfs[b].tti % 10;
   }
-  hipMemcpyAsync(g->d_sf, g->h_sf, nof_sf * sizeof(uint32_t), hipMemcpyHostToDevice, s);
-  hipEventRecord(g->staged, s);
+  hipMemcpyAsync(d_sf, h_sf, nof_sf * sizeof(uint32_t), hipMemcpyHostToDevice, s);
+  hipEventRecord(g->staged[slot], s);
   const size_t nre = 12 * (size_t)q->cell.nof_prb, nrx = q->nof_rx_antennas, np = q->cell.nof_ports;
   const size_t rows = 2 * SRSRAN_CP_NSYMB(q->cell.cp);  // grid symbols per subframe
   if (srsran_ofdm_rx_gpu(&q->fft[0], d_samples, (cf_t*)g->d_grid, (uint32_t)nrx, nof_sf, cfo, stream) ||
-      srsran_chest_dl_gpu_estimate_batch_cfg(&q->chest, &cfg->chest_cfg, g->d_sf, nof_sf, (const cf_t*)g->d_grid,
+      srsran_chest_dl_gpu_estimate_batch_cfg(&q->chest, &cfg->chest_cfg, d_sf, nof_sf, (const cf_t*)g->d_grid,
                                              nrx * rows * nre, (cf_t*)g->d_ce, np * nrx * nre * (full ? rows : 1),
                                              full ? 1 : 0, g->d_res, stream)) {
     return SRSRAN_ERROR;

@@ -516,7 +516,7 @@ def stage_bytes(nsf, nre_sum, ntb, sf_len=SF_LEN):
         "llr_batch_kernel": nre_sum * 2 * (8 + 4 + 6 * 2),
         "rm_rx_lds_kernel": ntb * (C3_BITS * 2 + C * (3 * (K + 32) + 12) * 2),
         "tdec_kernel": ntb * C * ((3 * (K + 32) + 12) * 2 + K // 8),
-        "tb_assemble_kernel": ntb * (C * K // 8 + C3_TBS // 8),
+        "tb_kernel": ntb * (C * K // 8 + C3_TBS // 8),
     }
 
 
@@ -531,7 +531,7 @@ def pusch_stage_bytes(nue, M, nsymb, ncell_re):
         "llr_batch_kernel": nue * nsymb * M * (8 + 6 * 2),
         "rm_rx_lds_kernel": nue * (C3_BITS * 2 + C * (3 * (K + 32) + 12) * 2),
         "tdec_kernel": nue * C * ((3 * (K + 32) + 12) * 2 + K // 8),
-        "tb_assemble_kernel": nue * (C * K // 8 + C3_TBS // 8),
+        "tb_kernel": nue * (C * K // 8 + C3_TBS // 8),
     }
 
 

@@ -285,8 +285,6 @@ struct SchCtx {
   uint8_t*    d_noi = nullptr;
   uint8_t*    d_crc_ok = nullptr;
   size_t      slot_cap = 0;
-  uint32_t*   d_part   = nullptr;  // TB_MAX_CHUNKS chunk CRCs per TB
-  size_t      tb_cap   = 0;
   // synchronous decode scratch
   int16_t*    d_e = nullptr;
   size_t      e_cap = 0;
@@ -576,19 +574,6 @@ int enqueue_batch(srsran_sch_t* q, uint32_t ntb, const srsran_dlsch_gpu_tb_t* tb
       x->slot_cap = cap;
     }
   }
-  if (ntb > x->tb_cap) {
-    if (x->used) {
-      hipEventSynchronize(x->done);
-    }
-    hipFree(x->d_part);
-    x->d_part = nullptr;
-    const size_t cap = std::max((size_t)ntb * 2, (size_t)64);
-    if (hipMalloc((void**)&x->d_part, cap * TB_MAX_CHUNKS * sizeof(uint32_t)) != hipSuccess) {
-      x->tb_cap = 0;
-      return SRSRAN_ERROR;
-    }
-    x->tb_cap = cap;
-  }
   uint32_t max_tbs = 0;
   for (uint32_t i = 0; i < ntb; i++) {
     SchTb& t = tbd[i];
@@ -596,7 +581,6 @@ int enqueue_batch(srsran_sch_t* q, uint32_t ntb, const srsran_dlsch_gpu_tb_t* tb
       t.cbout  = x->d_cbout;
       t.noi    = x->d_noi;
       t.crc_ok = x->d_crc_ok;
-      t.part   = x->d_part + (size_t)i * TB_MAX_CHUNKS;
       max_tbs  = std::max(max_tbs, t.tbs);
     }
   }
@@ -1121,7 +1105,6 @@ void srsran_sch_free(srsran_sch_t* q)
     hipFree(x->d_cbout);
     hipFree(x->d_noi);
     hipFree(x->d_crc_ok);
-    hipFree(x->d_part);
     hipFree(x->d_e);
     hipFree(x->d_data);
     hipFree(x->d_res);

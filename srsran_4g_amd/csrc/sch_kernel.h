@@ -5,8 +5,7 @@
 //   1. rm_rx_kernel     rate de-matching of every slot into its HARQ soft buffer
 //                       (srsran_rm_turbo_rx_lut, rm_turbo.c:390-483)
 //   2. tdec_kernel<ES>  turbo decode with CRC early stop (decode_tb_cb, sch.c:420-456)
-//   3. tb_assemble_kernel + tb_finish_kernel
-//                       TB assembly, CB bookkeeping, TB CRC (sch.c:458-573)
+//   3. tb_kernel        TB assembly, CB bookkeeping, TB CRC (sch.c:458-573)
 #ifndef SRSRAN_AMD_SCH_KERNEL_H
 #define SRSRAN_AMD_SCH_KERNEL_H
 #include <hip/hip_runtime.h>
@@ -41,7 +40,6 @@ struct SchTb {
   int32_t*       result;    // decode_tb return value (device)
   float*         avg;       // avg_iterations (device)
   short*         sbuf;      // soft buffer arena (sb_stride int16 per CB), for new-transmission resets
-  uint32_t*      part;      // TB_MAX_CHUNKS chunk CRC24A values (device scratch)
   uint32_t       saved_stride;
   uint32_t       sb_stride;
   uint32_t       max_cb;

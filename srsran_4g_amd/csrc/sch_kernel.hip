@@ -8,7 +8,7 @@
 // which gives coalesced soft-buffer reads/writes, no atomics and no write conflicts;
 // the E-vector gather hits L2 (E <= ~20 KB per CB).
 //
-// tb_assemble_kernel + tb_finish_kernel perform the tail of decode_tb_cb and decode_tb
+// tb_kernel performs the tail of decode_tb_cb and decode_tb
 // (sch.c:458-573): payload assembly in CB order (later CBs overwrite the 3 CRC bytes earlier
 // ones wrote, skipped CBs come from the soft buffer's saved copy) with the TB CRC24A of each
 // 1 KB chunk, then per TB the CB CRC bookkeeping, saving of good CBs on failure, the TB CRC
@@ -110,8 +110,7 @@ __global__ __launch_bounds__(RM_LDS_THREADS) void rm_rx_lds_kernel(const RmSlot*
   }
 }
 
-static constexpr int TB_ASM_THREADS = 64;                   // one wave per chunk
-static constexpr int TB_CHUNK       = 16 * TB_ASM_THREADS;  // payload bytes per assembly block
+static constexpr int TB_CHUNK       = 16 * 64;  // payload bytes per assembly chunk (one wave, 16 B a lane)
 static constexpr int TB_FIN_THREADS = 256;
 static constexpr int TB_THREADS     = TB_FIN_THREADS;  // reset_range stride
 
@@ -285,35 +284,19 @@ constexpr Crc24Tables make_crc24_tables()
 }
 __device__ const Crc24Tables kCrcT = make_crc24_tables();
 
-// tb_assemble_kernel: grid (chunks, TBs), one wave per chunk.  Chunk c covers payload bytes
+// One assembly chunk of a TB, by one wave (lane = 0..63).  Chunk c covers payload bytes
 // [nbytes - (c+1) * TB_CHUNK, nbytes - c * TB_CHUNK), nbytes = (tbs + 24) / 8 -- aligned to the END
 // of the CRC'd message so leading out-of-range bytes act as zeros, which do not change a
 // zero-initialised CRC.  Lane j gathers 16 consecutive bytes, writes them to the payload and
 // CRCs them (LDS byte table); its CRC moves to the chunk end with one multiply by
-// x^(128 (63 - j)) and the lanes XOR-reduce.  The finish kernel places chunk c with
-// x^(8 * TB_CHUNK * c).  Chunk 0 also writes the bytes past nbytes (the last CB's CRC24B,
-// sch.c:425-431).
-__global__ __launch_bounds__(TB_ASM_THREADS) void tb_assemble_kernel(const SchTb* __restrict__ tbs)
+// x^(128 (63 - j)) and the lanes XOR-reduce: the chunk's CRC, placed later with x^(8 * TB_CHUNK * c).
+// Chunk 0 also writes the bytes past nbytes (the last CB's CRC24B, sch.c:425-431).
+__device__ uint32_t assemble_chunk(const SchTb& t, const TbGeom& g, const uint32_t* ctab, int chunk, int lane)
 {
-  const SchTb t = tbs[blockIdx.y];
-  if (t.status != 1) {
-    return;
-  }
-  __shared__ TbGeom   g;
-  __shared__ uint32_t ctab[256];
-  const int tid = threadIdx.x;
-#pragma unroll
-  for (int k = 0; k < 256 / TB_ASM_THREADS; k++) {
-    ctab[tid + k * TB_ASM_THREADS] = kCrcT.byte[tid + k * TB_ASM_THREADS];
-  }
-  tb_geometry(t, g);
   const int nbytes = (int)((t.tbs + 24) / 8);
-  const int c1     = nbytes - (int)blockIdx.x * TB_CHUNK;  // one past the chunk's last byte
-  if (c1 <= 0) {
-    return;
-  }
+  const int c1     = nbytes - chunk * TB_CHUNK;  // one past the chunk's last byte
   const bool uniform = t.C1 == t.C || t.K1 == t.K2;
-  const int  p0      = c1 - TB_CHUNK + 16 * tid;
+  const int  p0      = c1 - TB_CHUNK + 16 * lane;
   uint32_t   crc     = 0;
   int        c       = -1;
 #pragma unroll 4
@@ -335,27 +318,28 @@ __global__ __launch_bounds__(TB_ASM_THREADS) void tb_assemble_kernel(const SchTb
     }
     crc = ((crc << 8) ^ ctab[((crc >> 16) ^ v) & 0xFFu]) & 0xFFFFFFu;
   }
-  if (blockIdx.x == 0) {  // bytes past the CRC'd message
-    for (uint32_t p = (uint32_t)nbytes + tid; p < g.end; p += TB_ASM_THREADS) {
+  if (chunk == 0) {  // bytes past the CRC'd message
+    for (uint32_t p = (uint32_t)nbytes + lane; p < g.end; p += 64) {
       t.data[p] = tb_byte(t, g, p);
     }
   }
-  crc = clmul24(crc, kCrcT.xp16[TB_ASM_THREADS - 1 - tid], LTE_CRC24A);
+  crc = clmul24(crc, kCrcT.xp16[63 - lane], LTE_CRC24A);
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     crc ^= (uint32_t)__shfl_xor((int)crc, off, 64);
   }
-  if (tid == 0) {
-    t.part[blockIdx.x] = crc;
-  }
+  return crc;
 }
 
-// tb_finish_kernel: one workgroup per TB -- CB bookkeeping, TB CRC24A from the chunk CRCs,
-// saving of good CBs on failure, new-transmission resets (sch.c:458-573).
-__global__ __launch_bounds__(TB_FIN_THREADS) void tb_finish_kernel(const SchTb* __restrict__ tbs)
+// tb_kernel: one workgroup per TB (4 waves) -- the payload assembly with the TB CRC24A of each 1 KB chunk
+// (the waves take the chunks in turn), then the CB bookkeeping, the TB CRC from the chunk CRCs, saving of
+// good CBs on failure, new-transmission resets (sch.c:458-573).  One launch for the whole tail of decode_tb.
+__global__ __launch_bounds__(TB_FIN_THREADS) void tb_kernel(const SchTb* __restrict__ tbs)
 {
   const SchTb t   = tbs[blockIdx.x];
   const int   tid = threadIdx.x;
+  __shared__ uint32_t ctab[256];
+  __shared__ uint32_t part[TB_MAX_CHUNKS];
   if (t.status != 1) {
     if (t.new_data && t.cb_crc) {  // the reset still happened (softbuffer.c:146-169)
       reset_range(t, 0, t.nof_cb_reset, 0, 0);
@@ -371,7 +355,20 @@ __global__ __launch_bounds__(TB_FIN_THREADS) void tb_finish_kernel(const SchTb* 
   }
   __shared__ TbGeom g;
   __shared__ uint32_t tb_crc;
-  tb_geometry(t, g);
+  for (int k = tid; k < 256; k += TB_FIN_THREADS) {
+    ctab[k] = kCrcT.byte[k];
+  }
+  tb_geometry(t, g);  // (its barriers also publish ctab)
+  {
+    const int nch = (int)(((t.tbs + 24) / 8 + TB_CHUNK - 1) / TB_CHUNK);
+    for (int ch = tid >> 6; ch < nch; ch += TB_FIN_THREADS / 64) {
+      const uint32_t crc = assemble_chunk(t, g, ctab, ch, tid & 63);
+      if ((tid & 63) == 0) {
+        part[ch] = crc;
+      }
+    }
+  }
+  __syncthreads();  // the payload and the chunk CRCs are complete
   const uint32_t C      = t.C;
   bool           all_ok = true;
   for (uint32_t c = 0; c < C; c++) {
@@ -397,7 +394,7 @@ __global__ __launch_bounds__(TB_FIN_THREADS) void tb_finish_kernel(const SchTb* 
       const uint32_t Mc     = xpow8(TB_CHUNK);
       uint32_t       r      = 0;
       for (int c = (int)nch - 1; c >= 0; c--) {
-        r = clmul24(r, Mc, LTE_CRC24A) ^ t.part[c];
+        r = clmul24(r, Mc, LTE_CRC24A) ^ part[c];
       }
       tb_crc = r;
     }
@@ -451,10 +448,7 @@ hipError_t tb_launch(const SchTb* d_tbs, uint32_t ntb, uint32_t max_tbs, hipStre
   if (nch > TB_MAX_CHUNKS) {
     return hipErrorInvalidValue;
   }
-  if (nch) {
-    hipLaunchKernelGGL(tb_assemble_kernel, dim3(nch, ntb), dim3(TB_ASM_THREADS), 0, stream, d_tbs);
-  }
-  hipLaunchKernelGGL(tb_finish_kernel, dim3(ntb), dim3(TB_FIN_THREADS), 0, stream, d_tbs);
+  hipLaunchKernelGGL(tb_kernel, dim3(ntb), dim3(TB_FIN_THREADS), 0, stream, d_tbs);
   return hipGetLastError();
 }
 

@@ -154,7 +154,7 @@ extern "C" int srsran_amd_timing_read(float ms[SRSRAN_AMD_NOF_STAGES], uint32_t 
 extern "C" const char* srsran_amd_stage_name(int stage)
 {
   static const char* names[ST_COUNT] = {"ofdm_rx_kernel", "chest_kernel", "predecode_batch_kernel",
-                                        "llr_batch_kernel", "rm_rx_lds_kernel", "tdec_kernel", "tb_assemble_kernel",
+                                        "llr_batch_kernel", "rm_rx_lds_kernel", "tdec_kernel", "tb_kernel",
                                         "nr_rm_kernel", "ldpc_kernel", "nr_tb_kernel",
                                         "chest_ul_kernel", "pusch_eq_idft_kernel"};
   return stage >= 0 && stage < ST_COUNT ? names[stage] : "";

@@ -114,7 +114,7 @@ static constexpr int TB_CHUNK       = 16 * 64;  // payload bytes per assembly ch
 static constexpr int TB_FIN_THREADS = 256;
 static constexpr int TB_THREADS     = TB_FIN_THREADS;  // reset_range stride
 
-// x^(8 * 2^k) mod CRC24A for k = 0..16, built at compile time.
+// a * b mod P over GF(2) at compile time (the CRC placement tables below)
 constexpr uint32_t ce_clmul_mod24(uint32_t a, uint32_t b, uint32_t poly)
 {
   uint64_t r = 0;
@@ -130,33 +130,6 @@ constexpr uint32_t ce_clmul_mod24(uint32_t a, uint32_t b, uint32_t poly)
   }
   return (uint32_t)r;
 }
-struct XpTable {
-  uint32_t v[17];
-};
-constexpr XpTable make_xp()
-{
-  XpTable  t{};
-  uint32_t x = 0x100u;  // x^8
-  for (int k = 0; k < 17; k++) {
-    t.v[k] = x;
-    x      = ce_clmul_mod24(x, x, LTE_CRC24A);
-  }
-  return t;
-}
-__constant__ XpTable kXpA = make_xp();
-
-// x^(8m) mod CRC24A
-__device__ __forceinline__ uint32_t xpow8(uint32_t m)
-{
-  uint32_t r = 1;
-  for (int k = 0; m; k++, m >>= 1) {
-    if (m & 1u) {
-      r = clmul24(r, kXpA.v[k], LTE_CRC24A);
-    }
-  }
-  return r;
-}
-
 // zero bytes [0, nbytes) of p with 16-byte stores where aligned (block-cooperative)
 __device__ void zero_bytes(uint8_t* p, uint32_t nbytes, int tid, int nthreads)
 {
@@ -284,6 +257,27 @@ constexpr Crc24Tables make_crc24_tables()
 }
 __device__ const Crc24Tables kCrcT = make_crc24_tables();
 
+// x^(8 TB_CHUNK c) mod CRC24A for c < TB_MAX_CHUNKS (the placement of chunk c's CRC at the message end)
+struct ChunkPow {
+  uint32_t v[TB_MAX_CHUNKS];
+};
+constexpr ChunkPow make_chunk_pow()
+{
+  ChunkPow t{};
+  uint32_t m = 0x100u;  // x^8, squared up to x^(8 TB_CHUNK)
+  for (int k = 1; k < TB_CHUNK; k <<= 1) {
+    m = ce_clmul_mod24(m, m, LTE_CRC24A);
+  }
+  uint32_t p = 1;
+  for (int c = 0; c < TB_MAX_CHUNKS; c++) {
+    t.v[c] = p;
+    p      = ce_clmul_mod24(p, m, LTE_CRC24A);
+  }
+  return t;
+}
+__device__ const ChunkPow kChunkPow = make_chunk_pow();
+static_assert((TB_CHUNK & (TB_CHUNK - 1)) == 0, "TB_CHUNK a power of two (repeated squaring above)");
+
 // One assembly chunk of a TB, by one wave (lane = 0..63).  Chunk c covers payload bytes
 // [nbytes - (c+1) * TB_CHUNK, nbytes - c * TB_CHUNK), nbytes = (tbs + 24) / 8 -- aligned to the END
 // of the CRC'd message so leading out-of-range bytes act as zeros, which do not change a
@@ -387,16 +381,18 @@ __global__ __launch_bounds__(TB_FIN_THREADS) void tb_kernel(const SchTb* __restr
       }
     }
   } else if (C > 1) {
-    // TB CRC24A over tbs + 24 bits (srsran_crc_match_byte, sch.c:560): Horner over the chunks
-    if (tid == 0) {
-      const uint32_t nbytes = (t.tbs + 24) / 8;
-      const uint32_t nch    = (nbytes + TB_CHUNK - 1) / TB_CHUNK;
-      const uint32_t Mc     = xpow8(TB_CHUNK);
-      uint32_t       r      = 0;
-      for (int c = (int)nch - 1; c >= 0; c--) {
-        r = clmul24(r, Mc, LTE_CRC24A) ^ part[c];
+    // TB CRC24A over tbs + 24 bits (srsran_crc_match_byte, sch.c:560): chunk c's CRC moved to the message end
+    // by x^(8 TB_CHUNK c), one lane a chunk, XOR-reduced over the first wave
+    if (tid < 64) {
+      const uint32_t nch = ((t.tbs + 24) / 8 + TB_CHUNK - 1) / TB_CHUNK;
+      uint32_t       r   = tid < (int)nch ? clmul24(part[tid], kChunkPow.v[tid], LTE_CRC24A) : 0u;
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        r ^= (uint32_t)__shfl_xor((int)r, off, 64);
       }
-      tb_crc = r;
+      if (tid == 0) {
+        tb_crc = r;
+      }
     }
     __syncthreads();
     tb_fail = tb_crc != 0;  // srsran_softbuffer_rx_reset_cb_crc (sch.c:567)

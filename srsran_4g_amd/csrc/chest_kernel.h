@@ -35,6 +35,11 @@ struct ChestArgs {
   const uint32_t* sf_idx;     // [b] subframe index (tti % 10): pilots + sf_idx[b] * CHEST_PILOTS_PER_SF; null = as given
   size_t          grid_sf_stride; // float2 between subframes of `grid`
   size_t          ce_sf_stride;   // float2 between subframes of `ce`
+  // ---- fused finalize (REFS noise): the last workgroup of subframe b to finish reduces its stats into
+  // res[b][4] (chest_finalize_launch's result) and re-arms done[b]; null res = finalize launched separately ----
+  float*          res;
+  uint32_t*       done;       // [b] workgroups of the subframe finished (zero between batches)
+  float           symbol_sz;
 };
 
 static constexpr size_t CHEST_PILOTS_PER_SF = 2 * 4 * CHEST_MAX_NREF;  // float2 (both port pairs)

@@ -514,11 +514,15 @@ __device__ __forceinline__ void map16s(const Lane& cin, int wave, int st0)
     TDECS_STAMP(st0 + 3);
     // phase 2: windows h-1 .. 0: alpha recomputed from the own entry checkpoint, then beta backwards with
     // the LLR of every position
+    St ckn = ck[h - 1];  // the next window's checkpoint, loaded a window ahead (private memory latency)
 #pragma unroll 1
     for (int mb = h - 1; mb >= 0; mb--) {
       const int t0 = mb * W;
+      St        Pa = ckn;
+      if (mb > 0) {
+        ckn = ck[mb - 1];
+      }
       pp.next(c, NTR + 2 * h - 1 - mb, xw, aux);
-      St Pa = ck[mb];
       St aw[W];  // alpha entering each position (candidates rebuilt at LLR time)
 #pragma unroll
       for (int i = 0; i < W; i++) {
@@ -593,15 +597,18 @@ __device__ __forceinline__ void map16s(const Lane& cin, int wave, int st0)
     __syncthreads();
     TDECS_STAMP(st0 + 3);
     // phase 2: windows [h, Ma): beta recomputed from the own checkpoint above the window, then alpha + LLR
-    const int n1 = Ma - h;
+    const int n1  = Ma - h;
+    St        ckn = ck[0];  // the next window's checkpoint, loaded a window ahead (private memory latency)
 #pragma unroll 1
     for (int ma = h; ma < Mfull; ma++) {
+      const St Pb = ckn;
+      ckn         = ck[ma + 1 - h];  // (ck has room for the entry past the last full window)
       pp.next(c, NTR + n1 + ma - h, xw, aux);
-      P = alpha_llr_window<D2, BITS, true>(c, P, ma * W, ck[ma - h], xw, aux);
+      P = alpha_llr_window<D2, BITS, true>(c, P, ma * W, Pb, xw, aux);
     }
     if (Ma > Mfull) {
       pp.next(c, NTR + n1 + Mfull - h, xw, aux);
-      alpha_llr_window<D2, BITS, false>(c, P, Mfull * W, ck[Mfull - h], xw, aux);
+      alpha_llr_window<D2, BITS, false>(c, P, Mfull * W, ckn, xw, aux);
     }
     TDECS_STAMP(st0 + 4);
   }

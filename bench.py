@@ -104,6 +104,8 @@ def shard(rank):
 def timed_region(step, steps, warmup, world, dist, sync, device):
     """Warm up, then time exactly `steps` steps bracketed by barrier + device sync on both sides;
     returns the MAX elapsed seconds over ranks (one all_reduce of a scalar, the only collective)."""
+    import gc
+
     import torch
 
     for _ in range(warmup):
@@ -112,6 +114,10 @@ def timed_region(step, steps, warmup, world, dist, sync, device):
     if world > 1:
         dist.barrier()
     sync()
+    # the harness's Python garbage collector stays out of the timed steps (a collection pause of the calling
+    # thread is a property of this script, not of the library, which a C caller such as srsUE does not have)
+    gc_was = gc.isenabled()
+    gc.disable()
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
@@ -119,6 +125,8 @@ def timed_region(step, steps, warmup, world, dist, sync, device):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if gc_was:
+        gc.enable()
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -131,9 +139,17 @@ def step_spread(step, n, torch, stream, host_phases=None):
     GPU time between HIP events recorded on the launch stream after every step, the host time of every
     enqueue call, and -- when `host_phases` (srsran_4g_amd.prof) is given -- the library's host phases of
     the slowest call.  -> {"gpu_ms": min/median/max, "host_ms": min/median/max, ...}"""
+    import gc
+
     torch.cuda.synchronize()
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(n + 1)]
     host, phases = [], []
+    gc_was = gc.isenabled()
+    gc.disable()
+    # two untimed steps first, so that the first timed interval starts with work queued behind it (an
+    # event recorded on an idle stream would time the host's first enqueue as GPU time)
+    step()
+    step()
     ev[0].record(stream)
     for i in range(n):
         if host_phases is not None:
@@ -146,6 +162,8 @@ def step_spread(step, n, torch, stream, host_phases=None):
             host_phases.host_enable(False)
         ev[i + 1].record(stream)
     torch.cuda.synchronize()
+    if gc_was:
+        gc.enable()
     gpu = [ev[i].elapsed_time(ev[i + 1]) for i in range(n)]
 
     def mmm(v):

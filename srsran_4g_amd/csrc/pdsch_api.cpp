@@ -348,8 +348,15 @@ int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sf
   srsran_amd::HostScope wait(srsran_amd::HP_PDSCH_WAIT);
   StageSlot& st    = g->ring[g->ring_next];
   g->ring_next = (g->ring_next + 1) % kStageRing;
-  if ((st.used && hipEventSynchronize(st.staged) != hipSuccess) || !grow_stage(st, pa_bytes + li_bytes + ev_bytes)) {
+  if (st.used && hipEventSynchronize(st.staged) != hipSuccess) {
     return SRSRAN_ERROR;
+  }
+  if (st.cap < pa_bytes + li_bytes + ev_bytes) {  // every slot of the ring grows now, not when it comes round
+    for (StageSlot& r : g->ring) {
+      if (!grow_stage(r, 2 * (pa_bytes + li_bytes + ev_bytes))) {
+        return SRSRAN_ERROR;
+      }
+    }
   }
   wait.stop();
   srsran_amd::HostScope launch(srsran_amd::HP_PDSCH_LAUNCH);

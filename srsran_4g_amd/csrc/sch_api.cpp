@@ -541,20 +541,25 @@ int enqueue_batch(srsran_sch_t* q, uint32_t ntb, const srsran_dlsch_gpu_tb_t* tb
   }
   wait.stop();
   srsran_amd::HostScope launch(srsran_amd::HP_SCH_LAUNCH);
-  if (bytes > st.cap) {
-    if (st.used) {
-      hipEventSynchronize(st.done);
-    }
-    hipHostFree(st.h);
-    hipFree(st.d);
-    st.h             = nullptr;
-    st.d             = nullptr;
+  if (bytes > st.cap) {  // every slot of the ring grows now: no allocation when the others come round
     const size_t cap = std::max(bytes * 2, (size_t)4096);
-    if (hipHostMalloc((void**)&st.h, cap, hipHostMallocDefault) != hipSuccess || hipMalloc((void**)&st.d, cap) != hipSuccess) {
-      st.cap = 0;
-      return SRSRAN_ERROR;
+    for (StageSlot& r : x->ring) {
+      if (r.cap >= cap) {
+        continue;
+      }
+      if (r.used) {
+        hipEventSynchronize(r.done);
+      }
+      hipHostFree(r.h);
+      hipFree(r.d);
+      r.h = nullptr;
+      r.d = nullptr;
+      if (hipHostMalloc((void**)&r.h, cap, hipHostMallocDefault) != hipSuccess || hipMalloc((void**)&r.d, cap) != hipSuccess) {
+        r.cap = 0;
+        return SRSRAN_ERROR;
+      }
+      r.cap = cap;
     }
-    st.cap = cap;
   }
   if (nslots > x->slot_cap) {
     if (x->used) {

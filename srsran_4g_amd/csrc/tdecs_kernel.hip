@@ -221,8 +221,9 @@ __device__ __forceinline__ St trellis(const short* xt, const short* yt)
 
 // LDS of one code block (dwords): S [NSB*Ls int16] | BITS [K/8 B] | XCH [NSB lanes][16 B] (the phase
 // exchange; the CRC reduction RED [2] reuses its first two dwords after the MAP decode)
+// (TDECS_CKLDS builds: | CK [nck][2 NSB lanes][16 B], each lane's own checkpoints in LDS instead of private memory)
 struct Geo {
-  int s_dw, bits_dw, xch_dw, cb_dw;
+  int s_dw, bits_dw, xch_dw, xch_off, ck_off, nck, cb_dw;
 };
 __host__ __device__ __forceinline__ Geo geo(int K, int Ls)
 {
@@ -230,11 +231,41 @@ __host__ __device__ __forceinline__ Geo geo(int K, int Ls)
   g.s_dw    = (NSB * Ls + 1) / 2;
   g.bits_dw = (K / 8 + 3) / 4;
   g.xch_dw  = NSB * 4;
-  g.cb_dw   = ((g.s_dw + g.bits_dw + 3) & ~3) + g.xch_dw;  // XCH 16-B aligned
+  g.xch_off = (g.s_dw + g.bits_dw + 3) & ~3;  // XCH 16-B aligned
+  g.ck_off  = g.xch_off + g.xch_dw;
+#ifdef TDECS_CKLDS
+  const int L  = K / NSB;
+  const int Ma = (L + W - 1) / W;
+  const int h  = max(1, min((L + W) / (2 * W), L / W));
+  g.nck        = max(h, Ma - h);  // entries of one wave: h (wave 0), Ma - h (wave 1)
+#else
+  g.nck = 0;
+#endif
+  g.cb_dw = g.ck_off + g.nck * 2 * NSB * 4;
   return g;
 }
+#ifndef TDECS_CKLDS
 // checkpoints one wave keeps per half-iteration: max(h, Ma - h) <= (L_max + 2 W) / (2 W) with L_max = 6144 / 16
 constexpr int CKMAX = (6144 / 16 + 2 * W) / (2 * W) + 1;
+#endif
+
+// This lane's own window checkpoints of a half-iteration: private memory, or (TDECS_CKLDS) LDS entries 2 NSB
+// lanes apart (the block's lanes of both waves side by side: one ds_*_b128 per wave and entry, no conflicts).
+struct Ck {
+#ifdef TDECS_CKLDS
+  uint4* p;
+  __device__ __forceinline__ St get(int e) const
+  {
+    const uint4 v = p[e * 2 * NSB];
+    return St{u2v(v.x), u2v(v.y), u2v(v.z), u2v(v.w)};
+  }
+  __device__ __forceinline__ void set(int e, const St& q) { p[e * 2 * NSB] = make_uint4(v2u(q.a), v2u(q.b), v2u(q.c), v2u(q.d)); }
+#else
+  St v[CKMAX];
+  __device__ __forceinline__ St   get(int e) const { return v[e]; }
+  __device__ __forceinline__ void set(int e, const St& q) { v[e] = q; }
+#endif
+};
 
 struct Raw {
   uint32_t a[W];  // systematic LLR (DEC1) / slot of pi(position) (DEC2)
@@ -266,6 +297,7 @@ struct Lane {
   lshort    Ssb;   // S + s * Ls: this lane's sub-block
   uint32_t* BITS;  // this block's decision bitmap (LDS)
   uint4*    XCH;   // this lane's exchange slot (LDS)
+  uint4*    CK;    // TDECS_CKLDS: this lane's checkpoint entry 0 (LDS)
 };
 
 __device__ __forceinline__ void xch_put(const Lane& c, const St& p)
@@ -365,7 +397,7 @@ __device__ __forceinline__ St alpha_llr_window(const Lane& c, St P, int t0, St P
 // stored beta at t0, which is the checkpoint of window t0/W - 1 when `store` (ck[t0/W - 1 - h]).
 template <bool FULL>
 __device__ __forceinline__ St beta_window(const Lane& c, St P, int t0, bool store, St& Bst, const uint32_t* xw,
-                                          St* ck, int h)
+                                          Ck& ck, int h)
 {
 #pragma unroll
   for (int i = W - 1; i >= 0; i--) {
@@ -374,7 +406,7 @@ __device__ __forceinline__ St beta_window(const Lane& c, St P, int t0, bool stor
       if (i == 0) {
         Bst = P;
         if (store) {
-          ck[t0 / W - 1 - h] = P;
+          ck.set(t0 / W - 1 - h, P);
         }
       }
       if ((i & 1) == 0) P = norm(P);
@@ -468,7 +500,10 @@ __device__ __forceinline__ void map16s(const Lane& cin, int wave, int st0)
   pp.nwin = NTR + 2 * (pp.beta ? Ma - h : h);
   uint32_t xw[W];
   uint32_t aux[W];
-  St       ck[CKMAX];  // this wave's own checkpoints (private memory)
+  Ck       ck;  // this wave's own checkpoints
+#ifdef TDECS_CKLDS
+  ck.p = c.CK;
+#endif
   pp.start(c);
   if (wave == 0) {
     // ================= wave 0: alpha on [0, h), then beta + LLR on [0, h) =================
@@ -498,7 +533,7 @@ __device__ __forceinline__ void map16s(const Lane& cin, int wave, int st0)
     for (int ma = 0; ma < h; ma++) {
       const int t0 = ma * W;
       pp.next(c, NTR + ma, xw, aux);
-      ck[ma] = P;
+      ck.set(ma, P);
 #pragma unroll
       for (int i = 0; i < W; i++) {
         P = step<false>(P, xw[i]);
@@ -514,13 +549,13 @@ __device__ __forceinline__ void map16s(const Lane& cin, int wave, int st0)
     TDECS_STAMP(st0 + 3);
     // phase 2: windows h-1 .. 0: alpha recomputed from the own entry checkpoint, then beta backwards with
     // the LLR of every position
-    St ckn = ck[h - 1];  // the next window's checkpoint, loaded a window ahead (private memory latency)
+    St ckn = ck.get(h - 1);  // the next window's checkpoint, loaded a window ahead (memory latency)
 #pragma unroll 1
     for (int mb = h - 1; mb >= 0; mb--) {
       const int t0 = mb * W;
       St        Pa = ckn;
       if (mb > 0) {
-        ckn = ck[mb - 1];
+        ckn = ck.get(mb - 1);
       }
       pp.next(c, NTR + 2 * h - 1 - mb, xw, aux);
       St aw[W];  // alpha entering each position (candidates rebuilt at LLR time)
@@ -578,7 +613,7 @@ __device__ __forceinline__ void map16s(const Lane& cin, int wave, int st0)
       }
     }
     const int mtop = Ma - 1;
-    ck[mtop - h]   = P;  // beta[L]: the checkpoint of the top window
+    ck.set(mtop - h, P);  // beta[L]: the checkpoint of the top window
     St Bst = P;  // stored (pre-normalisation) beta of the position above the current window
     // phase 1: windows Ma-1 .. h from the top (the top one maybe partial); checkpoints ck[0 .. Ma-1-h]
     if (Ma > Mfull) {
@@ -598,11 +633,13 @@ __device__ __forceinline__ void map16s(const Lane& cin, int wave, int st0)
     TDECS_STAMP(st0 + 3);
     // phase 2: windows [h, Ma): beta recomputed from the own checkpoint above the window, then alpha + LLR
     const int n1  = Ma - h;
-    St        ckn = ck[0];  // the next window's checkpoint, loaded a window ahead (private memory latency)
+    St        ckn = ck.get(0);  // the next window's checkpoint, loaded a window ahead (memory latency)
 #pragma unroll 1
     for (int ma = h; ma < Mfull; ma++) {
       const St Pb = ckn;
-      ckn         = ck[ma + 1 - h];  // (ck has room for the entry past the last full window)
+      if (ma + 1 < Ma) {
+        ckn = ck.get(ma + 1 - h);
+      }
       pp.next(c, NTR + n1 + ma - h, xw, aux);
       P = alpha_llr_window<D2, BITS, true>(c, P, ma * W, Pb, xw, aux);
     }
@@ -664,8 +701,9 @@ __device__ __forceinline__ void body(const TdecArgs& a, int bid)
   c.S    = (lshort)(short*)base;
   c.Ssb  = c.S + c.s * Ls;
   c.BITS = base + g.s_dw;
-  uint32_t* XCH = base + g.cb_dw - g.xch_dw;
+  uint32_t* XCH = base + g.xch_off;
   c.XCH  = reinterpret_cast<uint4*>(XCH) + s;
+  c.CK   = reinterpret_cast<uint4*>(base + g.ck_off) + t2;
   uint32_t* RED = XCH;  // the CRC reduction, after the MAP decode
   constexpr bool main_wave = true;
 

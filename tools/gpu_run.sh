@@ -4,6 +4,7 @@
 #
 # Usage: tools/gpu_run.sh TAG STEP [STEP ...]      output under gpurun_out/TAG/
 #   tests[:PYTEST_SELECTION]   pytest -m gpu (default: tests), e.g. tests:tests/test_pusch_gpu.py
+#   testse:ENV:SELECTION       the same with ENV (VAR=VAL[,VAR=VAL]) in the environment
 #   smoke                      __graft_entry__.smoke()
 #   bench:NAME[:ARGS]          python bench.py ARGS > bench_NAME.json (ARGS space-separated, e.g. "--steps 10")
 #   benche:NAME:ENV:ARGS       the same with ENV (VAR=VAL[,VAR=VAL]) in the environment
@@ -26,6 +27,11 @@ for STEP in "$@"; do
       timeout -k 10 900 python -u -m pytest $SEL -m gpu -q -x --timeout 300 --timeout-method thread \
         > $OUT/pytest_gpu.log 2>&1
       rc=$?; tail -3 $OUT/pytest_gpu.log; [ $rc -eq 0 ] || { echo "pytest rc=$rc"; exit 1; } ;;
+    testse)  # testse:VAR=VAL[,VAR=VAL]:SELECTION -- pytest -m gpu with environment settings
+      ENVS=${REST%%:*}; SEL=${REST#*:}
+      timeout -k 10 900 env ${ENVS//,/ } python -u -m pytest $SEL -m gpu -q -x --timeout 300 --timeout-method thread \
+        > $OUT/pytest_gpu_env.log 2>&1
+      rc=$?; tail -3 $OUT/pytest_gpu_env.log; [ $rc -eq 0 ] || { echo "pytest rc=$rc"; exit 1; } ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 \
         || { tail -5 $OUT/smoke.log; exit 1; }

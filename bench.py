@@ -207,6 +207,7 @@ def parse():
     p.add_argument("--ldpc-snr", type=float, default=1.5, help="ldpc: BPSK Es/N0 (dB) of the synthetic codewords")
     p.add_argument("--nr-tbs", type=int, default=64, help="nrsch: transport blocks per step")
     p.add_argument("--nr-snr", type=float, default=12.0, help="nrsch: Es/N0 (dB) of the bits as +-1 before int8 LLRs")
+    p.add_argument("--pdsch-probe", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--pdsch-steps", type=int, default=20,
                    help="all188: timed steps of the C3 PDSCH chain reported in the same line (0 = skip)")
     p.add_argument("--pdsch-cpu-seconds", type=float, default=4.0, help="all188: CPU baseline budget of the PDSCH part")
@@ -893,6 +894,40 @@ def run_dlloop(args, torch, dist, world, rank, device):
     return result
 
 
+def pdsch_probe(step, steps, torch, device, prof):
+    """--pdsch-probe (diagnostic, stderr): where the host waits in back-to-back batch calls -- per-call host
+    time and library host phases, on torch's current stream and on a created stream, after a short and a long
+    warm-up, with and without an event recorded between calls"""
+    import gc
+    import sys
+
+    def loop(on, n, events):
+        torch.cuda.synchronize()
+        gc.disable()
+        per, phases = [], []
+        t0 = time.perf_counter()
+        for _ in range(n):
+            prof.host_enable(True)
+            t = time.perf_counter()
+            step(None, on)
+            per.append(round((time.perf_counter() - t) * 1e6, 1))
+            phases.append({k: round(us, 1) for k, (us, _) in prof.host_read().items()})
+            prof.host_enable(False)
+            if events:
+                torch.cuda.Event().record(on if on is not None else torch.cuda.current_stream(device))
+        torch.cuda.synchronize()
+        total = (time.perf_counter() - t0) / n * 1e3
+        gc.enable()
+        return {"ms_per_step": round(total, 4), "host_us": per, "phases_first3": phases[:3],
+                "phases_last": phases[-1]}
+
+    created = torch.cuda.Stream(device)
+    for name, on, ev in (("current", None, False), ("current_ev", None, True), ("created", created, False),
+                         ("current_again", None, False)):
+        r = loop(on, max(steps, 20), ev)
+        print(json.dumps({"probe": name, **r}), file=sys.stderr, flush=True)
+
+
 def run_pdsch(args, torch, dist, world, rank, device, steps=None, warmup=None, cpu_seconds=None, emit=True):
     """UE DL chain on C3 subframes: per step `subframes` subframes of 2 rx x 30720 cf32 samples
     -> 2 TBs each (TBS 75376, 64QAM, TM3 CDD 2x2, CFI 1), new transmissions, at most `iters`
@@ -941,6 +976,8 @@ def run_pdsch(args, torch, dist, world, rank, device, steps=None, warmup=None, c
             raise RuntimeError("srsran_ue_dl_gpu_decode_batch failed")
 
     elapsed = timed_region(step, steps, warmup, world, dist, torch.cuda.synchronize, device)
+    if getattr(args, "pdsch_probe", False):
+        pdsch_probe(step, steps, torch, device, prof)
     # PCIe-inclusive rate (never `value`): every step's time samples start in pinned host memory.
     # Two device sample buffers: step i+1's H2D runs on a copy stream while step i decodes
     # (phy_dl_test.c:658-671 feeds one subframe at a time; here the copy hides under the batch).
@@ -992,20 +1029,24 @@ def run_pdsch(args, torch, dist, world, rank, device, steps=None, warmup=None, c
     del d_xs[1]
     # per-step spread of the same back-to-back launches (events between steps; host phases per call)
     spread = step_spread(step, max(steps, 10), torch, stream, prof)
-    # host enqueue cost of one step (the API builds descriptors and launches asynchronously)
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    for _ in range(steps):
-        step()
-    host_ms = (time.perf_counter() - t1) / steps * 1e3
-    torch.cuda.synchronize()
-    # where the host enqueue time goes (library-side wall-clock phases, same loop)
+    # host cost of one step (the API builds descriptors and launches asynchronously), each call on an idle GPU:
+    # in a free-running loop the host runs ahead until a ring slot's wait blocks it, and the call time is then
+    # the GPU's step time, not the host's work
+    import gc
+    gc.disable()
+    host_calls = []
     prof.host_enable(True)
-    for _ in range(steps):
+    prof.host_read()
+    for _ in range(max(steps, 10)):
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
         step()
+        host_calls.append((time.perf_counter() - t1) * 1e3)
     host_phases = {k: round(us / n, 1) for k, (us, n) in prof.host_read().items()}
     prof.host_enable(False)
+    gc.enable()
     torch.cuda.synchronize()
+    host_ms = float(np.median(host_calls))
     res = d_res.cpu().numpy()
     avg = d_avg.cpu().numpy()
     pl = d_pl.cpu().numpy()
@@ -1078,6 +1119,7 @@ def run_pdsch(args, torch, dist, world, rank, device, steps=None, warmup=None, c
         "stages": per_stage,
         "step_spread": spread,
         "host_enqueue_ms_per_step": round(host_ms, 4),
+        "host_enqueue_note": "median of per-call times, each call issued on an idle GPU (no ring waits)",
         "host_phases_us_per_call": host_phases,
         "chain_bytes_per_sf": 2 * sf_len * 8 + 2 * C3_TBS // 8,
     }

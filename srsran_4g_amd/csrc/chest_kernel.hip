@@ -109,14 +109,17 @@ __device__ __forceinline__ cx interp_at(const cx* av, uint32_t nr, uint32_t step
 }
 
 // srsran_interp_linear_vector3 (interp.c:158-188) for one subcarrier: rows[first .. first + M) from in0 / in1
-__device__ __forceinline__ void ivec(cx* rows, cx in0, cx in1, const cx* start, uint32_t d, uint32_t M, uint32_t first)
+// rows are written straight into the estimate column col (row stride `stride`): a per-lane rows[] array would
+// live in scratch
+__device__ __forceinline__ void ivec(float2* col, uint32_t stride, cx in0, cx in1, const cx* start, uint32_t d,
+                                     uint32_t M, uint32_t first)
 {
   const cx diff = scl(sub(in1, in0), (float)1 / d);
   cx       b    = add(start ? *start : in0, diff);
-  rows[first]   = b;
+  col[(size_t)first * stride] = make_float2(b.r, b.i);
   for (uint32_t i = 1; i < M; i++) {
-    b               = add(b, diff);
-    rows[first + i] = b;
+    b                                 = add(b, diff);
+    col[(size_t)(first + i) * stride] = make_float2(b.r, b.i);
   }
 }
 
@@ -187,14 +190,32 @@ __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
 
   // ---- LS estimates at the CRS and RSRP / RSSI ----
   float rsrp = 0.f;
-  for (uint32_t k = tid; k < np; k += CH_THREADS) {
-    const uint32_t l = k / nref, i = k % nref;
-    const uint32_t f = (crs_v(port, l) + a.cell_id % 6) % 6 + 6 * i;
-    const cx       r = ld2(in, crs_nsymbol(l, port, a.nsymb) * nre + f);
-    pe[k]            = mul(r, conj(ld2(pil, k)));
-    rsrp += r.r * r.r + r.i * r.i;
+  {  // all of a thread's pilot loads first (np <= 4 CH_THREADS), then the products: one HBM round trip
+    constexpr int PU = (4 * CHEST_MAX_NREF + CH_THREADS - 1) / CH_THREADS;
+    cx            r[PU], p[PU];
+#pragma unroll
+    for (int u = 0; u < PU; u++) {
+      const uint32_t k = tid + u * CH_THREADS;
+      if (k < np) {
+        const uint32_t l = k / nref, i = k % nref;
+        const uint32_t f = (crs_v(port, l) + a.cell_id % 6) % 6 + 6 * i;
+        r[u]             = ld2(in, crs_nsymbol(l, port, a.nsymb) * nre + f);
+        p[u]             = ld2(pil, k);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < PU; u++) {
+      const uint32_t k = tid + u * CH_THREADS;
+      if (k < np) {
+        pe[k] = mul(r[u], conj(p[u]));
+        rsrp += r[u].r * r[u].r + r[u].i * r[u].i;
+      }
+    }
   }
   float rssi = 0.f;
+  // unrolled: ~19 grid loads a thread at 100 PRB, issued together instead of one HBM round trip each (the
+  // adds stay in k order)
+#pragma unroll 8
   for (uint32_t k = tid; k < nsym * nre; k += CH_THREADS) {
     const cx r = ld2(in, crs_nsymbol(k / nre, port, a.nsymb) * nre + k % nre);
     rssi += r.r * r.r + r.i * r.i;
@@ -279,29 +300,27 @@ __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
     }
   }
   __syncthreads();
-  float    filt[8];
-  uint32_t M = a.filter_len;
-  for (int k = 0; k < 8; k++) {
-    filt[k] = a.filter[k];
-  }
+  // the smoothing filter lives in LDS: a private array indexed by the tap loop would spill to scratch
+  __shared__ float filt[8];
+  uint32_t         M = a.filter_len;
   if (a.filter_auto) {  // srsran_chest_set_smooth_filter_gauss(filter, 4, noise * 200) (chest_common.c:70-95)
-    const float sd = noise * 200.0f;
+    const float sd  = noise * 200.0f;
     float       sum = 0.f;
+#pragma unroll
     for (int k = 0; k < 5; k++) {
-      filt[k] = expf(-powf((float)(k - 2), 2) / (2.0f * powf(sd, 2)));
+      sum += expf(-powf((float)(k - 2), 2) / (2.0f * powf(sd, 2)));
     }
-    for (int k = 0; k < 5; k++) {
-      sum += filt[k];
+    M = isnormal(sum) ? 5 : 0;  // srsran_conv_same_cf with an empty filter yields zeros
+    if (tid < 5) {
+      filt[tid] = expf(-powf((float)((int)tid - 2), 2) / (2.0f * powf(sd, 2))) * (1.0f / sum);
     }
-    if (isnormal(sum)) {
-      for (int k = 0; k < 5; k++) {
-        filt[k] *= 1.0f / sum;
-      }
-      M = 5;
-    } else {
-      M = 0;  // srsran_conv_same_cf with an empty filter yields zeros
+  } else if (tid == 0) {  // constant indices: a dynamic index into the by-value kernarg copies it to scratch
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      filt[k] = a.filter[k];
     }
   }
+  __syncthreads();
   if (a.estimator == 1) {
     for (uint32_t l = 0; l < nsym; l++) {
       conv_row(pe + l * nref, avg + l * nref, nref, filt, M);
@@ -322,29 +341,29 @@ __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
   float          pss_err = 0.f;
   for (uint32_t j = tid; j < nre; j += CH_THREADS) {
     if (a.estimator == 1) {
-      cx rows[14];
-      cx v[4];
-      for (uint32_t l = 0; l < nsym; l++) {
-        v[l] = interp_at(avg + l * nref, nref, 6, (crs_v(port, l) + a.cell_id % 6) % 6, j);
-      }
+      float2* col = ce + j;
+      const auto vi = [&](uint32_t l) {
+        return interp_at(avg + l * nref, nref, 6, (crs_v(port, l) + a.cell_id % 6) % 6, j);
+      };
+      const cx v0 = vi(0), v1 = vi(1);
+      const auto put = [&](uint32_t l, cx x) { col[(size_t)l * nre] = make_float2(x.r, x.i); };
       if (port < 2) {  // CRS rows 0, ns - 3, ns, 2 ns - 3
+        const cx       v2 = vi(2), v3 = vi(3);
         const uint32_t r1 = ns - 3, r2 = ns, r3 = 2 * ns - 3;
-        rows[0] = v[0], rows[r1] = v[1], rows[r2] = v[2], rows[r3] = v[3];
-        ivec(rows, v[0], v[1], nullptr, r1, r1 - 1, 1);
-        ivec(rows, v[1], v[2], nullptr, r2 - r1, r2 - r1 - 1, r1 + 1);
-        ivec(rows, v[2], v[3], nullptr, r3 - r2, r3 - r2 - 1, r2 + 1);
-        ivec(rows, v[2], v[3], &v[3], r3 - r2, nrows - 1 - r3, r3 + 1);
+        put(0, v0), put(r1, v1), put(r2, v2), put(r3, v3);
+        ivec(col, nre, v0, v1, nullptr, r1, r1 - 1, 1);
+        ivec(col, nre, v1, v2, nullptr, r2 - r1, r2 - r1 - 1, r1 + 1);
+        ivec(col, nre, v2, v3, nullptr, r3 - r2, r3 - r2 - 1, r2 + 1);
+        ivec(col, nre, v2, v3, &v3, r3 - r2, nrows - 1 - r3, r3 + 1);
       } else {  // CRS rows 1, ns + 1 (the reference fills rows ns + 2 .. from row 1 as well)
-        rows[1] = v[0], rows[ns + 1] = v[1];
-        ivec(rows, v[1], v[0], &v[0], ns, 1, 0);
-        ivec(rows, v[0], v[1], nullptr, ns, ns - 1, 2);
-        ivec(rows, v[0], v[1], nullptr, ns, ns - 2, ns + 2);
+        put(1, v0), put(ns + 1, v1);
+        ivec(col, nre, v1, v0, &v0, ns, 1, 0);
+        ivec(col, nre, v0, v1, nullptr, ns, ns - 1, 2);
+        ivec(col, nre, v0, v1, nullptr, ns, ns - 2, ns + 2);
       }
-      for (uint32_t l = 0; l < nrows; l++) {
-        ce[l * nre + j] = make_float2(rows[l].r, rows[l].i);
-      }
-      if (noise_sf && a.noise_alg == 1 && j >= kp && j < kp + 62) {
-        const cx t = sub(mul(rows[ns - 1], ld2(a.pss, j - kp)), ld2(in, (ns - 1) * nre + j));
+      if (noise_sf && a.noise_alg == 1 && j >= kp && j < kp + 62) {  // row ns - 1 as this lane just wrote it
+        const float2 w = col[(size_t)(ns - 1) * nre];
+        const cx t = sub(mul(cx{w.x, w.y}, ld2(a.pss, j - kp)), ld2(in, (ns - 1) * nre + j));
         pss_err += t.r * t.r + t.i * t.i;
       }
     } else {
@@ -367,13 +386,13 @@ __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
     if (a.noise_alg == 1) {  // nof_ports * srsran_vec_avg_power_cf(62) * M_SQRT1_2
       noise = (float)a.nports * (block_sum(pss_err, red) / 62.0f) * (float)0.70710678118654752440;
     } else {  // estimate_noise_empty_sc: 5 empty subcarriers either side of the SSS and of the PSS
-      const uint32_t base[4] = {(ns - 2) * nre + kp - 5, (ns - 2) * nre + kp + 62, (ns - 1) * nre + kp - 5,
-                                (ns - 1) * nre + kp + 62};
       noise = 0.f;
-      for (int g = 0; g < 4; g++) {
-        float p = 0.f;
+#pragma unroll
+      for (int g = 0; g < 4; g++) {  // SSS left/right, then PSS left/right
+        const uint32_t base = (ns - 2 + (g >> 1)) * nre + ((g & 1) ? kp + 62 : kp - 5);
+        float          p    = 0.f;
         for (int k = 0; k < 5; k++) {
-          const cx x = ld2(in, base[g] + k);
+          const cx x = ld2(in, base + k);
           p += x.r * x.r + x.i * x.i;
         }
         noise += p / 5.0f;

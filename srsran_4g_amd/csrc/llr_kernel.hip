@@ -8,9 +8,10 @@
 // AVX2 blocks: truncation + saturation; tail: truncation + wrap).  Both splits are kept
 // here by the symbol's index within the call.
 //
-// Layout: one workgroup per LLR_THREADS * SPT symbols.  The Gold LFSRs are jumped to each
-// thread's slice of the block's sequence bits with three byte-indexed GF(2) jump tables, stepped
-// 16 bits at a time and staged in LDS; symbols are then processed with a stride of
+// Layout: one workgroup per LLR_THREADS * SPT symbols.  The first wave's lanes jump the Gold LFSRs
+// to the block start with three byte-indexed GF(2) jump tables (a uniform address: one fetch a wave),
+// then each lane to its 64-symbol slice with one per-lane stride matrix, steps them 16 bits at a time
+// and stages the bits in LDS; symbols are then processed with a stride of
 // LLR_THREADS (coalesced).  HBM-bound elementwise work: 8 B (+4 B CSI) in, 2*Qm B out per symbol.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -28,11 +29,14 @@ namespace srsran_amd {
 static constexpr int GOLD_NC   = 1600;  // sequence.c:39
 static constexpr int JUMP_BITS = 24;    // offsets below 2^24 bits
 static constexpr int JUMP_LVLS = 3;     // offset = b0 + 256 b1 + 65536 b2
+static constexpr int GOLD_LANE_SYMBOLS = 64;  // symbols whose sequence bits one lane of the first wave steps out
+static constexpr int GOLD_NMOD         = 5;   // BPSK .. 256QAM: Qm = 1, 2, 4, 6, 8
 
 struct GoldTables {
   uint32_t        x1_nc;      // x1 after Nc steps from x1 = 1
   uint32_t        x2_nc[31];  // x2 after Nc steps from the unit seed 1 << i
   const uint32_t* jump;       // [lvl][b][lfsr][32]: columns of A_lfsr^(b * 256^lvl) (device memory)
+  const uint32_t* stride;     // [MOD][lane][lfsr][32]: columns of A_lfsr^(lane * GOLD_LANE_SYMBOLS * Qm) (device)
 };
 __constant__ GoldTables kGold;
 
@@ -89,6 +93,33 @@ hipError_t gold_tables_init()
       }
     }
   }
+  // lane strides: A^(lane * 64 Qm) for the 64 lanes of each modulation
+  const size_t stride_off = jt.size();
+  jt.resize(stride_off + (size_t)GOLD_NMOD * 64 * 2 * 32, 0u);
+  const int qms[GOLD_NMOD] = {1, 2, 4, 6, 8};
+  for (int m = 0; m < GOLD_NMOD; m++) {
+    const uint32_t n = (uint32_t)(GOLD_LANE_SYMBOLS * qms[m]);
+    for (int l = 0; l < 2; l++) {
+      uint32_t S[31];  // A^n from the binary powers
+      for (int i = 0; i < 31; i++) {
+        S[i] = 1u << i;
+      }
+      for (int k = 0; k < JUMP_BITS; k++) {
+        if ((n >> k) & 1u) {
+          for (int i = 0; i < 31; i++) {
+            S[i] = apply(P(l, k), S[i]);
+          }
+        }
+      }
+      for (int lane = 0; lane < 64; lane++) {
+        uint32_t*       dst  = &jt[stride_off + (((size_t)m * 64 + lane) * 2 + l) * 32];
+        const uint32_t* prev = lane ? dst - 2 * 32 : nullptr;
+        for (int i = 0; i < 31; i++) {
+          dst[i] = lane ? apply(S, prev[i]) : (1u << i);
+        }
+      }
+    }
+  }
   GoldTables t;
   uint32_t   s = 1;
   for (int n = 0; n < GOLD_NC; n++) {
@@ -107,7 +138,8 @@ hipError_t gold_tables_init()
   if (err == hipSuccess) {
     err = hipMemcpy(d_jump, jt.data(), jt.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
   }
-  t.jump = d_jump;
+  t.jump   = d_jump;
+  t.stride = d_jump ? d_jump + stride_off : nullptr;
   if (err == hipSuccess) {
     err = hipMemcpyToSymbol(HIP_SYMBOL(kGold), &t, sizeof(t));
   }
@@ -443,12 +475,18 @@ __device__ __forceinline__ void llr_block(const float2* __restrict__ sym, uint32
   const uint32_t nb = min((uint32_t)(LLR_THREADS * SPT), n - base);
   const uint32_t t  = threadIdx.x;
   if (scramble) {
-    if (t * SPT < nb) {
+    static_assert(64 * GOLD_LANE_SYMBOLS == LLR_THREADS * SPT, "the first wave covers the block");
+    if (t < 64 && t * GOLD_LANE_SYMBOLS < nb) {
       uint32_t x1, x2;
-      gold_at(seed, bit0 + (base + t * SPT) * Q, x1, x2);
-#pragma unroll
-      for (int j = 0; j < Q; j++) {
-        cbits[t * Q + j] = (uint16_t)gold16(x1, x2);
+      gold_at(seed, bit0 + base * Q, x1, x2);  // the block start (uniform over the wave)
+      if (t) {
+        const uint32_t* m = kGold.stride + ((size_t)MOD * 64 + t) * 2 * 32;
+        x1                = apply_cols(m, x1);
+        x2                = apply_cols(m + 32, x2);
+      }
+#pragma unroll 4
+      for (int j = 0; j < GOLD_LANE_SYMBOLS * Q / 16; j++) {
+        cbits[t * (GOLD_LANE_SYMBOLS * Q / 16) + j] = (uint16_t)gold16(x1, x2);
       }
     }
     __syncthreads();

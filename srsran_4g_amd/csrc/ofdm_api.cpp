@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "../../include/srsran_ue_dl.h"
+#include "stage_copy.h"
 #include "devkey.h"
 #include "ofdm_kernel.h"
 
@@ -65,7 +66,7 @@ const float2* cfo_table(CfoTab& t, float f, uint32_t len, hipStream_t s)
   if (t.valid && t.bits == bits && t.len == len) {
     return t.d;
   }
-  if (!t.used && hipEventCreateWithFlags(&t.used, hipEventDisableTiming) != hipSuccess) {
+  if (!t.used && srsran_amd::ring_event_create(&t.used) != hipSuccess) {
     return nullptr;
   }
   if (t.valid) {

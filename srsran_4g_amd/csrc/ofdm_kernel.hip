@@ -8,8 +8,8 @@
 // (cfo.c:96-107, vector_simd.c:1723-1774) can be folded into the sample load.
 //
 // One workgroup per OFDM symbol: the N samples are rotated on load into LDS, transformed by
-// a mixed-radix (8/4/3/2) Stockham FFT with ping-pong LDS buffers (natural-order output, no
-// bit reversal), and only the nre occupied subcarriers are written back.  Twiddles come from
+// a mixed-radix (8/4/3/2) Stockham FFT in one LDS buffer (natural-order output, no bit
+// reversal), and only the nre occupied subcarriers are written back.  Twiddles come from
 // a per-N table computed in double precision on the host.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -81,45 +81,85 @@ __device__ __forceinline__ void dft8(float2* v)
 // j / Ns for j < 2^16 and Ns <= 2^12 with m = ceil(2^32 / Ns) (exact in that range)
 __device__ __forceinline__ uint32_t divm(uint32_t j, uint32_t m) { return __umulhi(j, m); }
 
+// One Stockham stage of radix R (natural-order output), in place in one LDS buffer: every thread holds its butterflies' inputs in registers
+// across a barrier (at most N / OFDM_THREADS = 8 values for N <= 2048), so a symbol needs 16 KB of LDS
+// instead of the 32 KB of a ping-pong pair -- 8 workgroups a CU instead of 5 (the launch is ~2200 symbols)
 template <int R>
-__device__ __forceinline__ void stage(const float2* src, float2* dst, const float2* __restrict__ tw, uint32_t N,
-                                      uint32_t Ns, uint32_t mNs)
+__device__ __forceinline__ void stage_ip(float2* buf, const float2* __restrict__ tw, uint32_t N, uint32_t Ns,
+                                         uint32_t mNs)
 {
+  constexpr int  J  = R == 8 ? 1 : R == 2 ? 4 : 2;  // butterflies per thread: N / R <= J * OFDM_THREADS
   const uint32_t nb = N / R, tstep = N / (Ns * R);
-  for (uint32_t j = threadIdx.x; j < nb; j += OFDM_THREADS) {
-    const uint32_t q = Ns > 1 ? divm(j, mNs) : j;
-    const uint32_t k = j - q * Ns;
-    float2         v[R];
+  static_assert(R != 8 || OFDM_MAX_N / 8 <= OFDM_THREADS, "radix-8 butterflies per thread");
+  static_assert(R != 4 || OFDM_MAX_N / 4 <= 2 * OFDM_THREADS, "radix-4 butterflies per thread");
+  static_assert(R != 2 || OFDM_MAX_N / 2 <= 4 * OFDM_THREADS, "radix-2 butterflies per thread");
+  // radix 3 only divides N = 3 * 2^k <= 1536: N / 3 <= 512 = 2 * OFDM_THREADS
+  float2 v[J][R];
 #pragma unroll
-    for (int r = 0; r < R; r++) {
-      v[r] = src[j + r * nb];
-    }
-    if (Ns > 1) {
+  for (int jj = 0; jj < J; jj++) {
+    const uint32_t j = threadIdx.x + jj * OFDM_THREADS;
+    if (j < nb) {
 #pragma unroll
-      for (int r = 1; r < R; r++) {
-        v[r] = cmul(v[r], tw[r * k * tstep]);  // r k tstep < R Ns tstep = N
+      for (int r = 0; r < R; r++) {
+        v[jj][r] = buf[j + r * nb];
       }
     }
-    if constexpr (R == 8) {
-      dft8(v);
-    } else if constexpr (R == 4) {
-      dft4(v);
-    } else if constexpr (R == 3) {
-      dft3(v);
-    } else {
-      dft2(v);
-    }
-    const uint32_t base = q * Ns * R + k;
+  }
+  __syncthreads();
 #pragma unroll
-    for (int r = 0; r < R; r++) {
-      dst[base + r * Ns] = v[r];
+  for (int jj = 0; jj < J; jj++) {
+    const uint32_t j = threadIdx.x + jj * OFDM_THREADS;
+    if (j < nb) {
+      const uint32_t q = Ns > 1 ? divm(j, mNs) : j;
+      const uint32_t k = j - q * Ns;
+      if (Ns > 1) {
+#pragma unroll
+        for (int r = 1; r < R; r++) {
+          v[jj][r] = cmul(v[jj][r], tw[r * k * tstep]);
+        }
+      }
+      if constexpr (R == 8) {
+        dft8(v[jj]);
+      } else if constexpr (R == 4) {
+        dft4(v[jj]);
+      } else if constexpr (R == 3) {
+        dft3(v[jj]);
+      } else {
+        dft2(v[jj]);
+      }
+      const uint32_t base = q * Ns * R + k;
+#pragma unroll
+      for (int r = 0; r < R; r++) {
+        buf[base + r * Ns] = v[jj][r];
+      }
     }
+  }
+  __syncthreads();
+}
+
+// the plan's stages in place on buf (barriers included)
+__device__ __forceinline__ void fft_ip(float2* buf, const OfdmArgs& a)
+{
+  uint32_t Ns = 1;
+  for (int st = 0; st < a.nstages; st++) {
+    const int      R   = a.radix[st];
+    const uint32_t mNs = a.ns_magic[st];
+    if (R == 8) {
+      stage_ip<8>(buf, a.tw, a.N, Ns, mNs);
+    } else if (R == 4) {
+      stage_ip<4>(buf, a.tw, a.N, Ns, mNs);
+    } else if (R == 3) {
+      stage_ip<3>(buf, a.tw, a.N, Ns, mNs);
+    } else {
+      stage_ip<2>(buf, a.tw, a.N, Ns, mNs);
+    }
+    Ns *= (uint32_t)R;
   }
 }
 
 __global__ __launch_bounds__(OFDM_THREADS) void ofdm_rx_kernel(OfdmArgs a)
 {
-  __shared__ float2 buf[2][OFDM_MAX_N];
+  __shared__ float2 buf[OFDM_MAX_N];
   const uint32_t    sym = blockIdx.x, rx = blockIdx.y, sf = blockIdx.z;
   const uint32_t    N = a.N, ns = a.nsymb, slot = sym / ns, i = sym % ns;
   const uint32_t    slot_sz = ns * N + a.cp0 + (ns - 1) * a.cp;
@@ -130,31 +170,15 @@ __global__ __launch_bounds__(OFDM_THREADS) void ofdm_rx_kernel(OfdmArgs a)
     if (a.cfo_tab) {
       x = ref_cprod(x, a.cfo_tab[off + n]);  // srsran_cfo_correct on the subframe buffer
     }
-    buf[0][n] = x;
+    buf[n] = x;
   }
   __syncthreads();
-  uint32_t Ns = 1, cur = 0;
-  for (int st = 0; st < a.nstages; st++) {
-    const int      R   = a.radix[st];
-    const uint32_t mNs = a.ns_magic[st];
-    if (R == 8) {
-      stage<8>(buf[cur], buf[cur ^ 1], a.tw, N, Ns, mNs);
-    } else if (R == 4) {
-      stage<4>(buf[cur], buf[cur ^ 1], a.tw, N, Ns, mNs);
-    } else if (R == 3) {
-      stage<3>(buf[cur], buf[cur ^ 1], a.tw, N, Ns, mNs);
-    } else {
-      stage<2>(buf[cur], buf[cur ^ 1], a.tw, N, Ns, mNs);
-    }
-    Ns *= (uint32_t)R;
-    cur ^= 1;
-    __syncthreads();
-  }
+  fft_ip(buf, a);
   float2*        dst  = a.out + (((size_t)sf * a.nrx + rx) * 2 * ns + sym) * a.nre;
   const uint32_t half = a.nre / 2;
   for (uint32_t k = threadIdx.x; k < a.nre; k += OFDM_THREADS) {
     const uint32_t bin = k < half ? N - half + k : k - half + 1;
-    float2         v   = buf[cur][bin];
+    float2         v   = buf[bin];
     if (a.norm != 1.0f) {
       v = make_float2(v.x * a.norm, v.y * a.norm);
     }
@@ -169,43 +193,27 @@ __global__ __launch_bounds__(OFDM_THREADS) void ofdm_rx_kernel(OfdmArgs a)
 // a.norm scales the grid first (srsran_enb_dl_gen_signal's 0.05 / sqrt(nof_prb)).
 __global__ __launch_bounds__(OFDM_THREADS) void ofdm_tx_kernel(OfdmArgs a)
 {
-  __shared__ float2 buf[2][OFDM_MAX_N];
+  __shared__ float2 buf[OFDM_MAX_N];
   const uint32_t    sym = blockIdx.x, port = blockIdx.y, sf = blockIdx.z;
   const uint32_t    N = a.N, ns = a.nsymb, slot = sym / ns, i = sym % ns, half = a.nre / 2;
   const float2*     src = a.in + (((size_t)sf * a.nrx + port) * 2 * ns + sym) * a.nre;
   for (uint32_t n = threadIdx.x; n < N; n += OFDM_THREADS) {
-    buf[0][n] = make_float2(0.f, 0.f);
+    buf[n] = make_float2(0.f, 0.f);
   }
   __syncthreads();
   for (uint32_t k = threadIdx.x; k < a.nre; k += OFDM_THREADS) {
     const uint32_t bin = k < half ? N - half + k : k - half + 1;
     const float2   v   = src[k];
-    buf[0][bin]        = make_float2(v.x * a.norm, -(v.y * a.norm));
+    buf[bin]           = make_float2(v.x * a.norm, -(v.y * a.norm));
   }
   __syncthreads();
-  uint32_t Ns = 1, cur = 0;
-  for (int st = 0; st < a.nstages; st++) {
-    const int      R   = a.radix[st];
-    const uint32_t mNs = a.ns_magic[st];
-    if (R == 8) {
-      stage<8>(buf[cur], buf[cur ^ 1], a.tw, N, Ns, mNs);
-    } else if (R == 4) {
-      stage<4>(buf[cur], buf[cur ^ 1], a.tw, N, Ns, mNs);
-    } else if (R == 3) {
-      stage<3>(buf[cur], buf[cur ^ 1], a.tw, N, Ns, mNs);
-    } else {
-      stage<2>(buf[cur], buf[cur ^ 1], a.tw, N, Ns, mNs);
-    }
-    Ns *= (uint32_t)R;
-    cur ^= 1;
-    __syncthreads();
-  }
+  fft_ip(buf, a);
   const uint32_t slot_sz = ns * N + a.cp0 + (ns - 1) * a.cp;
   const uint32_t off     = slot * slot_sz + a.cp0 + i * (N + a.cp);
   const uint32_t cpl     = i == 0 ? a.cp0 : a.cp;
   float2*        dst     = a.out + ((size_t)sf * a.nrx + port) * a.sf_len;
   for (uint32_t n = threadIdx.x; n < N; n += OFDM_THREADS) {
-    const float2 v = buf[cur][n];
+    const float2 v = buf[n];
     const float2 x = make_float2(v.x, -v.y);
     dst[off + n]   = x;
     if (n >= N - cpl) {

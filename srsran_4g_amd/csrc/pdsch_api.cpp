@@ -23,6 +23,7 @@
 #include "../../include/srsran_pdcch.h"
 #include "llr_kernel.h"
 #include "pdsch_internal.h"
+#include "stage_copy.h"
 #include "stage_timing.h"
 
 using namespace srsran_amd;
@@ -47,7 +48,8 @@ struct StageSlot {
   hipEvent_t staged = nullptr;  // this slot's last upload finished (pinned staging reusable)
   hipEvent_t read   = nullptr;  // the launches that read this slot's device copy are done
   bool       used   = false;
-  char*      h      = nullptr;
+  char*      h      = nullptr;  // pinned coherent host memory (stage_host_alloc)
+  char*      hd     = nullptr;  // its device alias
   char*      d      = nullptr;
   size_t     cap    = 0;
 };
@@ -108,7 +110,8 @@ bool grow_stage(StageSlot& st, size_t need)
   st.d   = nullptr;
   st.cap = 0;
   need   = std::max(need, (size_t)65536);
-  if (hipHostMalloc((void**)&st.h, need) != hipSuccess || hipMalloc((void**)&st.d, need) != hipSuccess) {
+  st.h = (char*)srsran_amd::stage_host_alloc(need, (void**)&st.hd);
+  if (!st.h || hipMalloc((void**)&st.d, need) != hipSuccess) {
     return false;
   }
   st.cap = need;
@@ -118,8 +121,8 @@ bool grow_stage(StageSlot& st, size_t need)
 bool init_ring(PdschGpu* g)
 {
   for (StageSlot& st : g->ring) {
-    if (hipEventCreateWithFlags(&st.staged, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&st.read, hipEventDisableTiming) != hipSuccess || !grow_stage(st, 65536)) {
+    if (srsran_amd::ring_event_create(&st.staged) != hipSuccess ||
+        srsran_amd::ring_event_create(&st.read) != hipSuccess || !grow_stage(st, 65536)) {
       return false;
     }
   }
@@ -371,14 +374,24 @@ int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sf
   if (!evs.empty()) {
     memcpy(st.h + pa_bytes + li_bytes, evs.data(), evs.size() * sizeof(EvmItem));
   }
-  // the upload on the copy stream once the launches of the batch that last used this slot are done with its
-  // device copy: it runs beside the OFDM / estimation stages instead of in line in front of the predecoder
-  if (st.used) {
-    hipStreamWaitEvent(g->copy, st.read, 0);
+  // SRSRAN_AMD_STAGE=side (round 3): the upload on a copy stream once the launches of the batch that last used
+  // this slot are done with its device copy, beside the OFDM / estimation stages
+  const bool side = srsran_amd::stage_side_copy();
+  if (side) {
+    if (st.used) {
+      hipStreamWaitEvent(g->copy, st.read, 0);
+    }
+    hipMemcpyAsync(st.d, st.h, pa_bytes + li_bytes + ev_bytes, hipMemcpyHostToDevice, g->copy);
+    hipEventRecord(st.staged, g->copy);
+    hipStreamWaitEvent(s, st.staged, 0);
+  } else {  // in line: a copy kernel reads the pinned slot (stage_copy.h)
+    // ... which also zeroes the batch's CSI maxima (no memset launch)
+    if (srsran_amd::stage_copy_launch(st.d, st.hd, pa_bytes + li_bytes + ev_bytes, s, (uint32_t*)d_max,
+                                      nsf * 2) != hipSuccess) {
+      return SRSRAN_ERROR;
+    }
+    hipEventRecord(st.staged, s);
   }
-  hipMemcpyAsync(st.d, st.h, pa_bytes + li_bytes + ev_bytes, hipMemcpyHostToDevice, g->copy);
-  hipEventRecord(st.staged, g->copy);
-  hipStreamWaitEvent(s, st.staged, 0);
   st.used = true;
   // from here on the slot belongs to this batch: its read event is recorded on every exit, so the upload that
   // next reuses it waits for whatever of this one was enqueued, error paths included
@@ -387,7 +400,9 @@ int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sf
     hipStream_t s;
     ~ReadMark() { hipEventRecord(st.read, s); }
   } mark{st, s};
-  hipMemsetAsync(d_max, 0, (size_t)nsf * 2 * sizeof(float), s);
+  if (side) {
+    hipMemsetAsync(d_max, 0, (size_t)nsf * 2 * sizeof(float), s);
+  }
   const PredArgs* dp = (const PredArgs*)st.d;
   const LlrItem*  dl = (const LlrItem*)(st.d + pa_bytes);
   for (uint32_t i = 0; i < nsf;) {  // one launch per predecoder scheme

@@ -29,6 +29,7 @@
 #include "uci_kernel.h"
 #include "pdsch_internal.h"
 #include "ulsch_batch.h"
+#include "stage_copy.h"
 #include "stage_timing.h"
 
 using namespace srsran_amd;
@@ -270,7 +271,8 @@ struct StageSlot {
   hipEvent_t staged = nullptr;  // this slot's last upload done (pinned staging reusable)
   hipEvent_t done   = nullptr;  // the batch that last used this slot finished with its descriptors
   bool       used   = false;
-  char*      h      = nullptr;
+  char*      h      = nullptr;  // pinned coherent host memory (stage_host_alloc)
+  char*      hd     = nullptr;  // its device alias
   char*      d      = nullptr;
   size_t     cap    = 0;
 };
@@ -322,8 +324,8 @@ size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 bool init_ring(SchCtx* x)
 {
   for (StageSlot& st : x->ring) {
-    if (hipEventCreateWithFlags(&st.staged, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&st.done, hipEventDisableTiming) != hipSuccess) {
+    if (srsran_amd::ring_event_create(&st.staged) != hipSuccess ||
+        srsran_amd::ring_event_create(&st.done) != hipSuccess) {
       return false;
     }
   }
@@ -554,7 +556,8 @@ int enqueue_batch(srsran_sch_t* q, uint32_t ntb, const srsran_dlsch_gpu_tb_t* tb
       hipFree(r.d);
       r.h = nullptr;
       r.d = nullptr;
-      if (hipHostMalloc((void**)&r.h, cap, hipHostMallocDefault) != hipSuccess || hipMalloc((void**)&r.d, cap) != hipSuccess) {
+      r.h = (char*)srsran_amd::stage_host_alloc(cap, (void**)&r.hd);
+      if (!r.h || hipMalloc((void**)&r.d, cap) != hipSuccess) {
         r.cap = 0;
         return SRSRAN_ERROR;
       }
@@ -595,24 +598,33 @@ int enqueue_batch(srsran_sch_t* q, uint32_t ntb, const srsran_dlsch_gpu_tb_t* tb
   if (!wide.empty()) {
     memcpy(st.h + off_wide, wide.data(), wide.size() * sizeof(Widen8));
   }
-  // early_copy (the PDSCH chain, whose stream runs OFDM ... LLR before the de-matching): the upload runs on
+  // SRSRAN_AMD_STAGE=side, early_copy (the PDSCH chain, whose stream runs OFDM ... LLR before the de-matching): the upload runs on
   // the copy stream as soon as the slot's previous batch is done with it, beside those stages, and the
   // launches below wait for it instead of having the copy's latency in line in front of them (chain
   // 243-246 k -> 250-255 k subframes/s, gpurun_out r03ah).  A batch with nothing in front of it keeps the
   // in-stream upload (the cross-stream wait costs a standalone DL-SCH batch ~10 us).
-  hipStream_t up = stream;
-  if (early_copy) {
-    up = x->copy;
-    if (st.used) {
-      hipStreamWaitEvent(up, st.done, 0);
+  // Default: a copy kernel in the launch stream reads the pinned slot (stage_copy.h) -- no copy-engine launch
+  // and no cross-stream waits, each of which left the GPU idle ~10-15 us (r04j trace).
+  if (!srsran_amd::stage_side_copy()) {
+    if (srsran_amd::stage_copy_launch(st.d, st.hd, bytes, stream) != hipSuccess) {
+      return SRSRAN_ERROR;
     }
-  }
-  if (hipMemcpyAsync(st.d, st.h, bytes, hipMemcpyHostToDevice, up) != hipSuccess) {
-    return SRSRAN_ERROR;
-  }
-  hipEventRecord(st.staged, up);
-  if (early_copy) {
-    hipStreamWaitEvent(stream, st.staged, 0);
+    hipEventRecord(st.staged, stream);
+  } else {
+    hipStream_t up = stream;
+    if (early_copy) {
+      up = x->copy;
+      if (st.used) {
+        hipStreamWaitEvent(up, st.done, 0);
+      }
+    }
+    if (hipMemcpyAsync(st.d, st.h, bytes, hipMemcpyHostToDevice, up) != hipSuccess) {
+      return SRSRAN_ERROR;
+    }
+    hipEventRecord(st.staged, up);
+    if (early_copy) {
+      hipStreamWaitEvent(stream, st.staged, 0);
+    }
   }
   x->used  = true;
   st.used  = true;
@@ -1068,7 +1080,7 @@ int srsran_sch_init(srsran_sch_t* q)
   q->gpu            = x;
   if (hipStreamCreateWithFlags(&x->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&x->copy, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&x->done, hipEventDisableTiming) != hipSuccess || !init_ring(x) ||
+      srsran_amd::ring_event_create(&x->done) != hipSuccess || !init_ring(x) ||
       hipMalloc((void**)&x->d_data, kDataCap) != hipSuccess || hipMalloc((void**)&x->d_res, 16) != hipSuccess ||
       hipMalloc((void**)&x->d_avg, 16) != hipSuccess ||
       hipHostMalloc((void**)&x->h_io, 256, hipHostMallocDefault) != hipSuccess ||

@@ -15,10 +15,15 @@
 // decision and the reset of the CB flags when it fails.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
 
 #include "crc24_dev.h"
 #include "sch_kernel.h"
 #include "tdec_kernel.h"
+#include "stage_copy.h"
 #include "stage_timing.h"
 
 namespace srsran_amd {
@@ -111,7 +116,7 @@ __global__ __launch_bounds__(RM_LDS_THREADS) void rm_rx_lds_kernel(const RmSlot*
 }
 
 static constexpr int TB_CHUNK       = 16 * 64;  // payload bytes per assembly chunk (one wave, 16 B a lane)
-static constexpr int TB_FIN_THREADS = 256;
+static constexpr int TB_FIN_THREADS = 1024;  // 16 waves: a C3 TB's ~10 chunks in one round
 static constexpr int TB_THREADS     = TB_FIN_THREADS;  // reset_range stride
 
 // a * b mod P over GF(2) at compile time (the CRC placement tables below)
@@ -531,6 +536,60 @@ hipError_t ul_deint_batch_launch(const UlDeint* d_desc, uint32_t ntb, uint32_t m
   StageScope timing_scope(ST_RM, stream);
   hipLaunchKernelGGL(ul_deint_batch_kernel, dim3((max_rows + UL_TILE_J - 1) / UL_TILE_J, ntb), dim3(256), 0, stream,
                      d_desc);
+  return hipGetLastError();
+}
+
+}  // namespace srsran_amd
+
+// ---------------- descriptor staging (stage_copy.h) ----------------
+namespace srsran_amd {
+
+__global__ __launch_bounds__(256) void stage_copy_kernel(uint4* __restrict__ dst, const uint4* __restrict__ src,
+                                                         uint32_t n16, uint32_t* __restrict__ zero, uint32_t nz)
+{
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n16; i += gridDim.x * 256) {
+    dst[i] = src[i];
+  }
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < nz; i += gridDim.x * 256) {
+    zero[i] = 0;
+  }
+}
+
+void* stage_host_alloc(size_t bytes, void** dev)
+{
+  void* h = nullptr;
+  *dev    = nullptr;
+  if (hipHostMalloc(&h, bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+    return nullptr;
+  }
+  if (hipHostGetDevicePointer(dev, h, 0) != hipSuccess) {
+    hipHostFree(h);
+    *dev = nullptr;
+    return nullptr;
+  }
+  return h;
+}
+
+bool stage_side_copy()
+{
+  static const bool side = [] {
+    const char* e = getenv("SRSRAN_AMD_STAGE");
+    return e && strcmp(e, "side") == 0;
+  }();
+  return side;
+}
+
+hipError_t stage_copy_launch(void* dst, const void* src_dev, size_t bytes, hipStream_t stream, uint32_t* zero,
+                             uint32_t zero_words)
+{
+  const uint32_t n16 = (uint32_t)((bytes + 15) / 16);
+  const uint32_t nz  = zero ? zero_words : 0;
+  if (n16 == 0 && nz == 0) {
+    return hipSuccess;
+  }
+  const uint32_t blocks = std::min<uint32_t>((std::max(n16, nz) + 255) / 256, 256);
+  hipLaunchKernelGGL(stage_copy_kernel, dim3(blocks), dim3(256), 0, stream, (uint4*)dst, (const uint4*)src_dev, n16,
+                     zero, nz);
   return hipGetLastError();
 }
 

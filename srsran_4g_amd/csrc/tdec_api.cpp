@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "../../include/srsran_tdec.h"
+#include "stage_copy.h"
 #include "devkey.h"
 #include "tdec_kernel.h"
 #include "tdec8bit_kernel.h"
@@ -764,15 +765,15 @@ StreamPool* get_pool()
   }
   for (int i = 0; i < kPoolStreams; i++) {
     if (hipStreamCreateWithPriority(&p->s[i], hipStreamNonBlocking, i == 0 ? hi : lo) != hipSuccess ||
-        hipEventCreateWithFlags(&p->done[i], hipEventDisableTiming) != hipSuccess) {
+        srsran_amd::ring_event_create(&p->done[i]) != hipSuccess) {
       return nullptr;
     }
   }
-  if (hipEventCreateWithFlags(&p->fork, hipEventDisableTiming) != hipSuccess) {
+  if (srsran_amd::ring_event_create(&p->fork) != hipSuccess) {
     return nullptr;
   }
   for (auto& m : p->md) {
-    if (hipEventCreateWithFlags(&m.copied, hipEventDisableTiming) != hipSuccess) {
+    if (srsran_amd::ring_event_create(&m.copied) != hipSuccess) {
       return nullptr;
     }
   }

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "../../include/srsran_pdcch.h"
+#include "stage_copy.h"
 #include "stage_timing.h"
 #include "../../include/srsran_ue_dl.h"
 
@@ -24,9 +25,12 @@ namespace {
 constexpr int kStageRing = 3;  // batches whose sf-index upload may be in flight (a ring, as the PDSCH / SCH staging)
 
 struct UeDlGpu {
-  hipEvent_t staged[kStageRing] = {};  // sf-index upload of the slot finished
+  hipEvent_t staged[kStageRing] = {};  // the estimator launch that reads the slot's subframe indices finished
   uint32_t   ring_next          = 0;
-  uint32_t*  h_sf   = nullptr;  // pinned, kStageRing slots of cap entries
+  // subframe indices, kStageRing slots of cap entries, in pinned coherent host memory that the estimator
+  // reads in place (d_sf: its device alias) -- no upload, which in the stream cost a copy launch and ~20 us
+  // of GPU idle per batch (gpurun_out r04j rocprof trace)
+  uint32_t*  h_sf   = nullptr;
   uint32_t*  d_sf   = nullptr;
   float2*    d_grid = nullptr;
   float2*    d_ce   = nullptr;
@@ -68,7 +72,6 @@ bool grow(srsran_ue_dl_t* q, UeDlGpu* g, uint32_t nsf, bool full)
   }
   hipDeviceSynchronize();
   hipHostFree(g->h_sf);
-  hipFree(g->d_sf);
   hipFree(g->d_grid);
   hipFree(g->d_ce);
   hipFree(g->d_res);
@@ -77,8 +80,9 @@ bool grow(srsran_ue_dl_t* q, UeDlGpu* g, uint32_t nsf, bool full)
   const size_t nre   = 12 * (size_t)q->cell.nof_prb;
   const size_t nrx   = q->nof_rx_antennas;
   const size_t ports = q->cell.nof_ports;
-  if (hipHostMalloc((void**)&g->h_sf, kStageRing * nsf * sizeof(uint32_t)) != hipSuccess ||
-      hipMalloc((void**)&g->d_sf, kStageRing * nsf * sizeof(uint32_t)) != hipSuccess ||
+  if (hipHostMalloc((void**)&g->h_sf, kStageRing * nsf * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent) !=
+          hipSuccess ||
+      hipHostGetDevicePointer((void**)&g->d_sf, g->h_sf, 0) != hipSuccess ||
       hipMalloc((void**)&g->d_grid, nsf * nrx * 14 * nre * sizeof(float2)) != hipSuccess ||
       hipMalloc((void**)&g->d_ce, nsf * ports * nrx * nre * (full ? 14 : 1) * sizeof(float2)) != hipSuccess ||
       hipMalloc((void**)&g->d_res, nsf * 4 * sizeof(float)) != hipSuccess) {
@@ -134,7 +138,7 @@ int srsran_ue_dl_init(srsran_ue_dl_t* q, cf_t* input[SRSRAN_MAX_PORTS], uint32_t
   UeDlGpu* g = new UeDlGpu();
   q->gpu     = g;
   for (hipEvent_t& e : g->staged) {
-    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+    if (srsran_amd::ring_event_create(&e) != hipSuccess) {
       srsran_ue_dl_free(q);
       return SRSRAN_ERROR;
     }
@@ -158,7 +162,6 @@ void srsran_ue_dl_free(srsran_ue_dl_t* q)
   if (g) {
     hipDeviceSynchronize();
     hipHostFree(g->h_sf);
-    hipFree(g->d_sf);
     hipFree(g->d_grid);
     hipFree(g->d_ce);
     hipFree(g->d_res);
@@ -224,7 +227,6 @@ int srsran_ue_dl_set_cell(srsran_ue_dl_t* q, srsran_cell_t cell)
   g->nof_pending_ul = 0;  // ue_dl.c:189
   hipDeviceSynchronize();
   hipHostFree(g->h_sf);
-  hipFree(g->d_sf);
   hipFree(g->d_grid);
   hipFree(g->d_ce);
   hipFree(g->d_res);
@@ -324,8 +326,6 @@ int srsran_ue_dl_gpu_decode_batch(srsran_ue_dl_t*              q,
   for (uint32_t b = 0; b < nof_sf; b++) {
     h_sf[b] = sfs[b].tti % 10;
   }
-  hipMemcpyAsync(d_sf, h_sf, nof_sf * sizeof(uint32_t), hipMemcpyHostToDevice, s);
-  hipEventRecord(g->staged[slot], s);
   const size_t nre = 12 * (size_t)q->cell.nof_prb, nrx = q->nof_rx_antennas, np = q->cell.nof_ports;
   const size_t rows = 2 * SRSRAN_CP_NSYMB(q->cell.cp);  // grid symbols per subframe
   if (srsran_ofdm_rx_gpu(&q->fft[0], d_samples, (cf_t*)g->d_grid, (uint32_t)nrx, nof_sf, cfo, stream) ||
@@ -334,6 +334,7 @@ int srsran_ue_dl_gpu_decode_batch(srsran_ue_dl_t*              q,
                                              full ? 1 : 0, g->d_res, stream)) {
     return SRSRAN_ERROR;
   }
+  hipEventRecord(g->staged[slot], s);  // h_sf of this slot is free again once the estimator has run
   front.stop();
   std::vector<srsran_pdsch_gpu_sf_t> ps(nof_sf);
   for (uint32_t b = 0; b < nof_sf; b++) {

@@ -10,6 +10,7 @@
 #   benche:NAME:ENV:ARGS       the same with ENV (VAR=VAL[,VAR=VAL]) in the environment
 #   prof:NAME[:ARGS]           rocprofv3 --kernel-trace --stats of bench.py ARGS -> prof_NAME/
 #   pmc:NAME[:ARGS]            tools/pmc_tdec.sh passes over tools/tdec_kernels.py ARGS -> NAME/
+#   pmcb:NAME:WORKLOAD[ ARGS]  tools/pmc.sh passes over bench.py --workload WORKLOAD ARGS -> NAME/summary.json
 #   py:NAME:SCRIPT[ ARGS]      python SCRIPT ARGS > NAME.log
 set -o pipefail
 TAG=$1; shift
@@ -52,6 +53,9 @@ for STEP in "$@"; do
       python tools/bench_brief.py $OUT/prof_$NAME.json ;;
     pmc)
       bash $R/tools/pmc_tdec.sh $TAG/$NAME $ARGS || exit 1 ;;
+    pmcb)
+      bash $R/tools/pmc.sh $TAG/$NAME $ARGS || exit 1
+      (cd $R && python tools/pmc_summary.py gpurun_out/$TAG/$NAME ${ARGS%% *} gpurun_out/$TAG/$NAME/summary.json) ;;
     py)
       timeout -k 10 600 python $ARGS > $OUT/$NAME.log 2>&1 || { tail -8 $OUT/$NAME.log; exit 1; }
       tail -4 $OUT/$NAME.log ;;

@@ -14,6 +14,7 @@
 
 #include "../../include/srsran_ue_dl.h"
 #include "chest_kernel.h"
+#include "pdsch_internal.h"
 #include "ofdm_kernel.h"
 
 using namespace srsran_amd;
@@ -561,19 +562,24 @@ extern "C" int srsran_chest_dl_gpu_estimate_batch(srsran_chest_dl_t* q,
                                                 0, d_res, stream);
 }
 
-extern "C" int srsran_chest_dl_gpu_estimate_batch_cfg(srsran_chest_dl_t*           q,
-                                                      const srsran_chest_dl_cfg_t* cfg,
-                                                      const uint32_t*              d_sf_idx,
-                                                      uint32_t                     nsf,
-                                                      const cf_t*                  d_grid,
-                                                      size_t                       grid_sf_stride,
-                                                      cf_t*                        d_ce,
-                                                      size_t                       ce_sf_stride,
-                                                      int                          full_grid,
-                                                      float*                       d_res,
-                                                      void*                        stream)
+namespace {
+// srsran_chest_dl_gpu_estimate_batch_cfg with the subframe indices from d_sf_idx (device) or h_sf (host, carried in
+// the launch arguments, nsf <= CHEST_INLINE_SF)
+int estimate_batch(srsran_chest_dl_t*           q,
+                   const srsran_chest_dl_cfg_t* cfg,
+                   const uint32_t*              d_sf_idx,
+                   const uint8_t*               h_sf,
+                   uint32_t                     nsf,
+                   const cf_t*                  d_grid,
+                   size_t                       grid_sf_stride,
+                   cf_t*                        d_ce,
+                   size_t                       ce_sf_stride,
+                   int                          full_grid,
+                   float*                       d_res,
+                   void*                        stream)
 {
-  if (!q || !q->gpu || !d_sf_idx || !d_grid || !d_ce || !d_res || q->cell.nof_prb == 0) {
+  if (!q || !q->gpu || (!d_sf_idx && !h_sf) || !d_grid || !d_ce || !d_res || q->cell.nof_prb == 0 ||
+      (h_sf && nsf > (uint32_t)srsran_amd::CHEST_INLINE_SF)) {
     return SRSRAN_ERROR_INVALID_INPUTS;
   }
   if (!cfg_supported(cfg, true) ||
@@ -602,6 +608,11 @@ extern "C" int srsran_chest_dl_gpu_estimate_batch_cfg(srsran_chest_dl_t*        
   a.grid           = (const float2*)d_grid;
   a.pilots         = g->pilots;
   a.sf_idx         = d_sf_idx;
+  if (h_sf) {
+    a.sf_idx = nullptr;
+    a.sf_inl = 1;
+    memcpy(a.sf_inline, h_sf, nsf);
+  }
   a.grid_sf_stride = grid_sf_stride;
   a.ce             = (float2*)d_ce;
   a.ce_sf_stride   = ce_sf_stride;
@@ -640,3 +651,41 @@ extern "C" int srsran_chest_dl_gpu_estimate_batch_cfg(srsran_chest_dl_t*        
   }
   return SRSRAN_SUCCESS;
 }
+}  // namespace
+
+extern "C" int srsran_chest_dl_gpu_estimate_batch_cfg(srsran_chest_dl_t*           q,
+                                                      const srsran_chest_dl_cfg_t* cfg,
+                                                      const uint32_t*              d_sf_idx,
+                                                      uint32_t                     nsf,
+                                                      const cf_t*                  d_grid,
+                                                      size_t                       grid_sf_stride,
+                                                      cf_t*                        d_ce,
+                                                      size_t                       ce_sf_stride,
+                                                      int                          full_grid,
+                                                      float*                       d_res,
+                                                      void*                        stream)
+{
+  if (!d_sf_idx) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  return estimate_batch(q, cfg, d_sf_idx, nullptr, nsf, d_grid, grid_sf_stride, d_ce, ce_sf_stride, full_grid, d_res,
+                        stream);
+}
+
+namespace srsran_amd {
+int chest_dl_gpu_estimate_batch_inline(srsran_chest_dl_t*           q,
+                                       const srsran_chest_dl_cfg_t* cfg,
+                                       const uint8_t*               h_sf,
+                                       uint32_t                     nsf,
+                                       const cf_t*                  d_grid,
+                                       size_t                       grid_sf_stride,
+                                       cf_t*                        d_ce,
+                                       size_t                       ce_sf_stride,
+                                       int                          full_grid,
+                                       float*                       d_res,
+                                       void*                        stream)
+{
+  return estimate_batch(q, cfg, nullptr, h_sf, nsf, d_grid, grid_sf_stride, d_ce, ce_sf_stride, full_grid, d_res,
+                        stream);
+}
+}  // namespace srsran_amd

@@ -8,6 +8,7 @@ namespace srsran_amd {
 
 static constexpr int CHEST_MAX_PRB  = 110;
 static constexpr int CHEST_MAX_NREF = 2 * CHEST_MAX_PRB;  // pilots per CRS symbol
+static constexpr int CHEST_INLINE_SF = 512;  // subframe indices a batch launch carries in its arguments
 
 struct ChestArgs {
   const float2* grid;      // [rx][2 nsymb * nre] received subframe grids
@@ -40,6 +41,10 @@ struct ChestArgs {
   float*          res;
   uint32_t*       done;       // [b] workgroups of the subframe finished (zero between batches)
   float           symbol_sz;
+  // subframe indices carried in the launch arguments (batches of <= CHEST_INLINE_SF subframes, sf_inl = 1): no
+  // host buffer for the GPU to read, so no ring slot and no event to free it
+  uint32_t        sf_inl;
+  uint8_t         sf_inline[CHEST_INLINE_SF];
 };
 
 static constexpr size_t CHEST_PILOTS_PER_SF = 2 * 4 * CHEST_MAX_NREF;  // float2 (both port pairs)

@@ -182,9 +182,9 @@ __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
   const uint32_t tid  = threadIdx.x;
   const uint32_t nsym = port < 2 ? 4 : 2, nref = 2 * a.nof_prb, np = nsym * nref, nre = 12 * a.nof_prb;
   const float2*  in   = a.grid + b * a.grid_sf_stride + (size_t)rx * 2 * a.nsymb * nre;
-  const uint32_t sfi  = a.sf_idx ? a.sf_idx[b] : a.sf_index;
-  const float2*  pil  = a.pilots + (a.sf_idx ? a.sf_idx[b] * CHEST_PILOTS_PER_SF : 0) +
-                      (size_t)(port / 2) * 4 * CHEST_MAX_NREF;
+  const bool     bat  = a.sf_inl || a.sf_idx;  // per-subframe indices: pilots of each subframe's index
+  const uint32_t sfi  = a.sf_inl ? (uint32_t)a.sf_inline[b] : a.sf_idx ? a.sf_idx[b] : a.sf_index;
+  const float2*  pil  = a.pilots + (bat ? sfi * CHEST_PILOTS_PER_SF : 0) + (size_t)(port / 2) * 4 * CHEST_MAX_NREF;
   const uint32_t fidx0 = (crs_v(port, 0) + a.cell_id % 6) % 6;
   const bool     kept_noise = a.noise_alg != 0;  // PSS / EMPTY: the REFS residuals are not the estimate
 

@@ -16,6 +16,7 @@
 #include <stdint.h>
 
 #include "eq_kernel.h"
+#include "gmem.h"
 #include "stage_timing.h"
 
 #pragma clang fp contract(off)
@@ -34,7 +35,7 @@ __device__ __forceinline__ cpx cscale(cpx a, float s) { return {a.r * s, a.i * s
 __device__ __forceinline__ cpx cmulj(cpx a) { return {-a.i, a.r}; }
 __device__ __forceinline__ cpx ld(const float2* p, uint32_t k)
 {
-  const float2 v = p[k];
+  const float2 v = gptr(p)[k];  // global address space (gmem.h): the pointers come from descriptors
   return {v.x, v.y};
 }
 
@@ -360,14 +361,150 @@ __device__ __forceinline__ void predecode_item(const PredArgs& a, uint32_t k, ui
 
 static constexpr int EQ_RPT = 4;  // REs per thread (strided by the block size: coalesced)
 
+// predecode_item for the EQ_RPT REs of a thread at once (PORT0, SM, CDD): every RE-map entry first, then
+// every grid / estimate load, then the arithmetic (as predecode_item's, operation for operation) and the
+// stores -- two HBM round trips a thread instead of two per RE
+template <int SCHEME>
+__device__ __forceinline__ void predecode_items(const PredArgs& a, uint32_t k0, uint32_t (&mx)[2])
+{
+  static_assert(SCHEME == 0 || SCHEME == 2 || SCHEME == 3, "one RE per unit");
+  constexpr int U = EQ_RPT;
+  uint32_t      k[U], kk[U], gy[U], gh[U];
+  float         ys[U];
+  bool          valid[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    k[u]     = k0 + u * EQ_THREADS + threadIdx.x;
+    valid[u] = k[u] < a.n;
+    kk[u]    = valid[u] ? k[u] : 0;
+    gy[u]    = kk[u];
+    gh[u]    = kk[u];
+    ys[u]    = 1.0f;
+  }
+  if (a.idx) {
+    uint32_t e[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      e[u] = gptr(a.idx)[kk[u]];
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      gy[u] = e[u] & 0x7fffffffu;
+      gh[u] = a.ce_row ? gy[u] % a.ce_row : gy[u];
+      ys[u] = (e[u] >> 31) ? a.rho_b_inv : 1.0f;
+    }
+  }
+  const float noise = a.noise_ptr ? *gptr(a.noise_ptr) : a.noise;
+  auto        Ys    = [&](cpx v, int u) -> cpx { return ys[u] != 1.0f ? cscale(v, ys[u]) : v; };
+  if constexpr (SCHEME == 0) {
+    cpx yv[U][4], hv[U][4];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+#pragma unroll
+      for (int p = 0; p < 4; p++) {
+        if (p < a.nrx) {
+          yv[u][p] = ld(a.y[p], gy[u]);
+          hv[u][p] = ld(a.h[0][p], gh[u]);
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      cpx   r  = {0.f, 0.f};
+      float hh = 0.f;
+#pragma unroll
+      for (int p = 0; p < 4; p++) {
+        if (p < a.nrx) {
+          r = cadd(r, cmul(Ys(yv[u][p], u), cconj(hv[u][p])));
+          hh += hv[u][p].r * hv[u][p].r + hv[u][p].i * hv[u][p].i;
+        }
+      }
+      const float csi = hh + noise;
+      const cpx   t   = cscale(r, a.norm);
+      if (valid[u]) {
+        gptr(a.csi[0])[k[u]] = csi;
+        gptr(a.x[0])[k[u]]   = make_float2(t.r / csi, t.i / csi);
+        mx[0]                = max(mx[0], __float_as_uint(csi));
+      }
+    }
+  } else {
+    cpx y0[U], y1[U], p0[U], p1[U], q0[U], q1[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      p0[u] = ld(a.h[0][0], gh[u]);
+      p1[u] = ld(a.h[0][1], gh[u]);
+      q0[u] = ld(a.h[1][0], gh[u]);
+      q1[u] = ld(a.h[1][1], gh[u]);
+      y0[u] = ld(a.y[0], gy[u]);
+      y1[u] = ld(a.y[1], gy[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      cpx h00, h01, h10, h11;
+      if constexpr (SCHEME == 3) {  // CDD: the large-delay precoder alternates with the RE index
+        if ((kk[u] & 1) == 0) {
+          h00 = cadd(p0[u], q0[u]);
+          h10 = cadd(p1[u], q1[u]);
+          h01 = csub(p0[u], q0[u]);
+          h11 = csub(p1[u], q1[u]);
+        } else {
+          h00 = csub(p0[u], q0[u]);
+          h10 = csub(p1[u], q1[u]);
+          h01 = cadd(p0[u], q0[u]);
+          h11 = cadd(p1[u], q1[u]);
+        }
+      } else {
+        if (a.codebook == 0) {
+          h00 = p0[u];
+          h01 = q0[u];
+          h10 = p1[u];
+          h11 = q1[u];
+        } else if (a.codebook == 1) {
+          h00 = cadd(p0[u], q0[u]);
+          h01 = csub(p0[u], q0[u]);
+          h10 = cadd(p1[u], q1[u]);
+          h11 = csub(p1[u], q1[u]);
+        } else {
+          h00 = cadd(p0[u], cmulj(q0[u]));
+          h01 = csub(p0[u], cmulj(q0[u]));
+          h10 = cadd(p1[u], cmulj(q1[u]));
+          h11 = csub(p1[u], cmulj(q1[u]));
+        }
+      }
+      cpx   x0, x1;
+      float c0, c1;
+      mmse_csi(Ys(y0[u], u), Ys(y1[u], u), h00, h01, h10, h11, x0, x1, c0, c1, noise, a.norm);
+      if (valid[u]) {
+        if (a.interleave == 2) {    // one codeword on both layers: srsran_layerdemap_multiplex -> _diversity
+          if (k[u] < a.n / 2) {     // (layermap.c:138-147) over n/2 layer symbols (pdsch.c:862-863)
+            gptr(a.x[0])[2 * k[u]]     = make_float2(x0.r, x0.i);
+            gptr(a.x[0])[2 * k[u] + 1] = make_float2(x1.r, x1.i);
+          }
+        } else {
+          gptr(a.x[0])[k[u]] = make_float2(x0.r, x0.i);
+          gptr(a.x[1])[k[u]] = make_float2(x1.r, x1.i);
+        }
+        gptr(a.csi[0])[k[u]] = c0;  // not layer-demapped: the codeword's CSI correction reads layer 0's
+        gptr(a.csi[1])[k[u]] = c1;
+        mx[0]                = max(mx[0], __float_as_uint(c0));
+        mx[1]                = max(mx[1], __float_as_uint(c1));
+      }
+    }
+  }
+}
+
 template <int SCHEME>
 __device__ __forceinline__ void predecode_block(const PredArgs& a, uint32_t k0)
 {
   __shared__ uint32_t red[2 * EQ_THREADS / 64];
   uint32_t            mx[2] = {0u, 0u};
+  if constexpr (SCHEME == 0 || SCHEME == 2 || SCHEME == 3) {
+    predecode_items<SCHEME>(a, k0, mx);
+  } else {
 #pragma unroll
-  for (int r = 0; r < EQ_RPT; r++) {
-    predecode_item<SCHEME>(a, k0 + r * EQ_THREADS + threadIdx.x, mx);
+    for (int r = 0; r < EQ_RPT; r++) {
+      predecode_item<SCHEME>(a, k0 + r * EQ_THREADS + threadIdx.x, mx);
+    }
   }
   if (a.csi_max) {
     if constexpr (SCHEME == 0 || SCHEME == 1 || SCHEME == 4) {

@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "devkey.h"
+#include "gmem.h"
 #include "llr_kernel.h"
 #include "stage_timing.h"
 
@@ -310,7 +311,8 @@ __device__ __forceinline__ int16_t cvt_pi16(float x) { return sat16(cvt_rn(x)); 
 __device__ __forceinline__ int16_t mulhi16(int16_t a, int16_t b) { return (int16_t)(((int32_t)a * (int32_t)b) >> 16); }
 
 template <int MOD>
-__device__ __forceinline__ void csi_correct(int16_t* o, uint32_t s, const float* csi, float mx, uint32_t nof_bits)
+// cs = csi[s], cso = csi[s ^ 1] (loaded by the caller; cso only read where s ^ 1 < n)
+__device__ __forceinline__ void csi_correct(int16_t* o, uint32_t s, float cs, float cso, float mx, uint32_t nof_bits)
 {
   constexpr int Q     = Qm<MOD>::v;
   const float   scale = 32767.0f / mx;
@@ -327,15 +329,15 @@ __device__ __forceinline__ void csi_correct(int16_t* o, uint32_t s, const float*
     nblk = 0;
   }
   if (s < nblk) {
-    const int16_t c = cvt_pi16(csi[s] * scale);
+    const int16_t c = cvt_pi16(cs * scale);
     if constexpr (MOD == 1) {  // pair (s, s^1): lanes 0,1 take the odd symbol's CSI, lanes 2,3 the even's
-      const int16_t co = cvt_pi16(csi[s ^ 1u] * scale);
+      const int16_t co = cvt_pi16(cso * scale);
 #pragma unroll
       for (int b = 0; b < Q; b++) {
         o[b] = mulhi16(o[b], co);
       }
     } else if constexpr (MOD == 3) {  // even s: LLR 4,5 use s+1; odd s: LLR 0,1 use s-1
-      const int16_t co = cvt_pi16(csi[s ^ 1u] * scale);
+      const int16_t co = cvt_pi16(cso * scale);
 #pragma unroll
       for (int b = 0; b < Q; b++) {
         const bool other = (s & 1u) ? (b < 2) : (b >= 4);
@@ -348,7 +350,7 @@ __device__ __forceinline__ void csi_correct(int16_t* o, uint32_t s, const float*
       }
     }
   } else {  // the release build hoists 1 / csi_max (-Ofast -freciprocal-math; oracle/ref_pdsch_tx_harness.c)
-    const float c = csi[s] * (1.0f / mx);
+    const float c = cs * (1.0f / mx);
 #pragma unroll
     for (int b = 0; b < Q; b++) {
       o[b] = wrap16(cvt_tz((float)o[b] * c));
@@ -433,9 +435,9 @@ __device__ __forceinline__ void demap8(float re, float im, uint32_t i, uint32_t 
 
 // csi_correction's llr_is_8bit branch (pdsch.c:538-545): (int8)((float)e * (csi * (1 / csi_max)))
 template <int MOD>
-__device__ __forceinline__ void csi_correct8(int8_t* o, uint32_t s, const float* csi, float mx)
+__device__ __forceinline__ void csi_correct8(int8_t* o, float cs, float mx)
 {
-  const float c = csi[s] * (1.0f / mx);
+  const float c = cs * (1.0f / mx);
 #pragma unroll
   for (int b = 0; b < Qm<MOD>::v; b++) {
     o[b] = wrap8(cvt_tz((float)o[b] * c));
@@ -460,12 +462,16 @@ __device__ __forceinline__ uint32_t gold16(uint32_t& x1, uint32_t& x2)
 // 16 * Q bits).  Phase 2: thread t handles symbols t, t + 256, ... -- coalesced loads and
 // stores -- demapping, descrambling from the LDS bits and CSI correction in registers.
 template <int MOD, bool B8 = false>
-__device__ __forceinline__ void llr_block(const float2* __restrict__ sym, uint32_t n, int scramble, uint32_t seed,
-                                          uint32_t bit0, const float* __restrict__ csi,
-                                          const float* __restrict__ csi_max, int16_t* __restrict__ llr, uint32_t blk,
+__device__ __forceinline__ void llr_block(const float2* __restrict__ sym_p, uint32_t n, int scramble, uint32_t seed,
+                                          uint32_t bit0, const float* __restrict__ csi_p,
+                                          const float* __restrict__ csi_max, int16_t* __restrict__ llr_p, uint32_t blk,
                                           float* __restrict__ evm_part = nullptr, uint32_t evm_n = 0,
-                                          int8_t* __restrict__ llr8 = nullptr)
+                                          int8_t* __restrict__ llr8_p = nullptr)
 {
+  const gptr_t<const float2> sym  = gptr(sym_p);  // global-space views (gmem.h)
+  const gptr_t<const float>  csi  = gptr(csi_p);
+  const gptr_t<int16_t>      llr  = gptr(llr_p);
+  const gptr_t<int8_t>       llr8 = gptr(llr8_p);
   constexpr int       Q = Qm<MOD>::v;
   __shared__ uint16_t cbits[LLR_THREADS * 8 + 2];  // SPT * Q / 16 = Q chunks per thread
   const uint32_t      base = blk * (uint32_t)(LLR_THREADS * SPT);
@@ -491,21 +497,44 @@ __device__ __forceinline__ void llr_block(const float2* __restrict__ sym, uint32
     }
     __syncthreads();
   }
-  const float mx  = csi ? *csi_max : 1.0f;
+  const float mx  = csi ? *gptr(csi_max) : 1.0f;
   const uintptr_t ob  = B8 ? (uintptr_t)llr8 : (uintptr_t)llr;
   const bool      a16 = (ob & 15) == 0;
   const bool      a8  = (ob & 7) == 0;
   const bool      a4  = (ob & 3) == 0;
   const bool      a2  = (ob & 1) == 0;
   float       err = 0.0f;  // EVM: this thread's sum of squared symbol errors
-#pragma unroll 4
-  for (int r = 0; r < SPT; r++) {
-    const uint32_t i = t + (uint32_t)r * LLR_THREADS;
+  // the thread's symbols (and CSI) in groups of LLR_U, each group's loads issued before the first is used: one
+  // HBM round trip a group instead of one a symbol
+  constexpr int LLR_U = 8;
+  static_assert(SPT % LLR_U == 0, "whole groups");
+  for (int r0 = 0; r0 < SPT; r0 += LLR_U) {
+    if (t + (uint32_t)r0 * LLR_THREADS >= nb) {
+      break;
+    }
+    float2 vv[LLR_U];
+    float  cs[LLR_U], cso[LLR_U];
+#pragma unroll
+    for (int u = 0; u < LLR_U; u++) {
+      const uint32_t i = t + (uint32_t)(r0 + u) * LLR_THREADS;
+      if (i < nb) {
+        vv[u] = sym[base + i];
+        if (csi) {
+          cs[u] = csi[base + i];
+          if (!B8 && (MOD == 1 || MOD == 3) && ((base + i) ^ 1u) < n) {
+            cso[u] = csi[(base + i) ^ 1u];
+          }
+        }
+      }
+    }
+#pragma unroll
+  for (int u = 0; u < LLR_U; u++) {
+    const uint32_t i = t + (uint32_t)(r0 + u) * LLR_THREADS;
     if (i >= nb) {
       break;
     }
     const uint32_t s = base + i;
-    const float2   v = sym[s];
+    const float2   v = vv[u];
     if constexpr (B8) {  // int8 LLRs: demod_b, sequence_apply_c, the 8-bit CSI correction
       int8_t o[Q];
       demap8<MOD>(v.x, v.y, s, n, o);
@@ -532,9 +561,9 @@ __device__ __forceinline__ void llr_block(const float2* __restrict__ sym, uint32
         }
       }
       if (csi) {
-        csi_correct8<MOD>(o, s, csi, mx);
+        csi_correct8<MOD>(o, cs[u], mx);
       }
-      int8_t* dst = llr8 + (size_t)s * Q;
+      const gptr_t<int8_t> dst = llr8 + (size_t)s * Q;
       if constexpr (Q == 8) {
         uint2 u;
         u.x = (uint32_t)(uint8_t)o[0] | ((uint32_t)(uint8_t)o[1] << 8) | ((uint32_t)(uint8_t)o[2] << 16) |
@@ -542,12 +571,12 @@ __device__ __forceinline__ void llr_block(const float2* __restrict__ sym, uint32
         u.y = (uint32_t)(uint8_t)o[4] | ((uint32_t)(uint8_t)o[5] << 8) | ((uint32_t)(uint8_t)o[6] << 16) |
               ((uint32_t)(uint8_t)o[7] << 24);
         if (a8) {
-          *reinterpret_cast<uint2*>(dst) = u;
+          *reinterpret_cast<gptr_t<uint2>>(dst) = u;
           continue;
         }
       } else if constexpr (Q == 4) {
         if (a4) {
-          *reinterpret_cast<uint32_t*>(dst) = (uint32_t)(uint8_t)o[0] | ((uint32_t)(uint8_t)o[1] << 8) |
+          *reinterpret_cast<gptr_t<uint32_t>>(dst) = (uint32_t)(uint8_t)o[0] | ((uint32_t)(uint8_t)o[1] << 8) |
                                               ((uint32_t)(uint8_t)o[2] << 16) | ((uint32_t)(uint8_t)o[3] << 24);
           continue;
         }
@@ -555,7 +584,7 @@ __device__ __forceinline__ void llr_block(const float2* __restrict__ sym, uint32
         if (a2) {  // Q = 6: the symbol's 6 bytes start 2-byte aligned
 #pragma unroll
           for (int k = 0; k < Q / 2; k++) {
-            reinterpret_cast<uint16_t*>(dst)[k] = (uint16_t)((uint8_t)o[2 * k] | ((uint32_t)(uint8_t)o[2 * k + 1] << 8));
+            reinterpret_cast<gptr_t<uint16_t>>(dst)[k] = (uint16_t)((uint8_t)o[2 * k] | ((uint32_t)(uint8_t)o[2 * k + 1] << 8));
           }
           continue;
         }
@@ -591,16 +620,16 @@ __device__ __forceinline__ void llr_block(const float2* __restrict__ sym, uint32
       }
     }
     if (csi) {  // after descrambling, as pdsch.c:735-737 orders it
-      csi_correct<MOD>(o, s, csi, mx, n * Q);
+      csi_correct<MOD>(o, s, cs[u], cso[u], mx, n * Q);
     }
-    int16_t* dst = llr + (size_t)s * Q;
+    const gptr_t<int16_t> dst = llr + (size_t)s * Q;
     if (Q == 1 || !a4) {
 #pragma unroll
       for (int k = 0; k < Q; k++) {
         dst[k] = o[k];
       }
     } else if constexpr (Q == 2) {
-      *reinterpret_cast<uint32_t*>(dst) = (uint32_t)(uint16_t)o[0] | ((uint32_t)(uint16_t)o[1] << 16);
+      *reinterpret_cast<gptr_t<uint32_t>>(dst) = (uint32_t)(uint16_t)o[0] | ((uint32_t)(uint16_t)o[1] << 16);
     } else if constexpr (Q == 8) {
       uint4 u;
       u.x = (uint32_t)(uint16_t)o[0] | ((uint32_t)(uint16_t)o[1] << 16);
@@ -608,18 +637,19 @@ __device__ __forceinline__ void llr_block(const float2* __restrict__ sym, uint32
       u.z = (uint32_t)(uint16_t)o[4] | ((uint32_t)(uint16_t)o[5] << 16);
       u.w = (uint32_t)(uint16_t)o[6] | ((uint32_t)(uint16_t)o[7] << 16);
       if (a16) {
-        *reinterpret_cast<uint4*>(dst) = u;
+        *reinterpret_cast<gptr_t<uint4>>(dst) = u;
       } else {
-        uint32_t* d = reinterpret_cast<uint32_t*>(dst);
+        const gptr_t<uint32_t> d = reinterpret_cast<gptr_t<uint32_t>>(dst);
         d[0] = u.x, d[1] = u.y, d[2] = u.z, d[3] = u.w;
       }
     } else {  // Q = 4, 6: 4-byte aligned words (int16 buffers are 4-byte aligned)
-      uint32_t* d = reinterpret_cast<uint32_t*>(dst);
+      const gptr_t<uint32_t> d = reinterpret_cast<gptr_t<uint32_t>>(dst);
 #pragma unroll
       for (int k = 0; k < Q / 2; k++) {
         d[k] = (uint32_t)(uint16_t)o[2 * k] | ((uint32_t)(uint16_t)o[2 * k + 1] << 16);
       }
     }
+  }
   }
   if (evm_part && base < evm_n) {  // block sum in a fixed order: wave butterflies, then the 4 waves
     __shared__ float wsum[LLR_THREADS / 64];
@@ -632,7 +662,7 @@ __device__ __forceinline__ void llr_block(const float2* __restrict__ sym, uint32
     }
     __syncthreads();
     if (t == 0) {
-      evm_part[blk] = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
+      gptr(evm_part)[blk] = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
     }
   }
 }

@@ -94,7 +94,18 @@ __device__ __forceinline__ void stage_ip(float2* buf, const float2* __restrict__
   static_assert(R != 4 || OFDM_MAX_N / 4 <= 2 * OFDM_THREADS, "radix-4 butterflies per thread");
   static_assert(R != 2 || OFDM_MAX_N / 2 <= 4 * OFDM_THREADS, "radix-2 butterflies per thread");
   // radix 3 only divides N = 3 * 2^k <= 1536: N / 3 <= 512 = 2 * OFDM_THREADS
-  float2 v[J][R];
+  float2 v[J][R], w[J][R];  // w: twiddles, loaded first (independent of the data) so their latency overlaps
+#pragma unroll
+  for (int jj = 0; jj < J; jj++) {
+    const uint32_t j = threadIdx.x + jj * OFDM_THREADS;
+    if (j < nb && Ns > 1) {
+      const uint32_t k = j - divm(j, mNs) * Ns;
+#pragma unroll
+      for (int r = 1; r < R; r++) {
+        w[jj][r] = tw[r * k * tstep];
+      }
+    }
+  }
 #pragma unroll
   for (int jj = 0; jj < J; jj++) {
     const uint32_t j = threadIdx.x + jj * OFDM_THREADS;
@@ -115,7 +126,7 @@ __device__ __forceinline__ void stage_ip(float2* buf, const float2* __restrict__
       if (Ns > 1) {
 #pragma unroll
         for (int r = 1; r < R; r++) {
-          v[jj][r] = cmul(v[jj][r], tw[r * k * tstep]);
+          v[jj][r] = cmul(v[jj][r], w[jj][r]);
         }
       }
       if constexpr (R == 8) {
@@ -165,12 +176,26 @@ __global__ __launch_bounds__(OFDM_THREADS) void ofdm_rx_kernel(OfdmArgs a)
   const uint32_t    slot_sz = ns * N + a.cp0 + (ns - 1) * a.cp;
   const uint32_t    off     = slot * slot_sz + a.cp0 + i * (N + a.cp);
   const float2*     src     = a.in + ((size_t)sf * a.nrx + rx) * a.sf_len + off;
-  for (uint32_t n = threadIdx.x; n < N; n += OFDM_THREADS) {
-    float2 x = src[n];
-    if (a.cfo_tab) {
-      x = ref_cprod(x, a.cfo_tab[off + n]);  // srsran_cfo_correct on the subframe buffer
+  {  // all of a thread's sample loads (and CFO factors) issued before the first use: one HBM round trip
+    constexpr int U = OFDM_MAX_N / OFDM_THREADS;
+    float2        x[U], c[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint32_t n = threadIdx.x + u * OFDM_THREADS;
+      if (n < N) {
+        x[u] = src[n];
+        if (a.cfo_tab) {
+          c[u] = a.cfo_tab[off + n];
+        }
+      }
     }
-    buf[n] = x;
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint32_t n = threadIdx.x + u * OFDM_THREADS;
+      if (n < N) {
+        buf[n] = a.cfo_tab ? ref_cprod(x[u], c[u]) : x[u];  // srsran_cfo_correct on the subframe buffer
+      }
+    }
   }
   __syncthreads();
   fft_ip(buf, a);

@@ -45,8 +45,9 @@ static_assert(SRSRAN_MAX_PRB <= 128, "two 64-bit words of PRB bitmap per slot");
 // batch kStageRing back, so a stall of the calling thread shorter than that many batches leaves the GPU busy.
 constexpr int kStageRing = 3;
 struct StageSlot {
-  hipEvent_t staged = nullptr;  // this slot's last upload finished (pinned staging reusable)
-  hipEvent_t read   = nullptr;  // the launches that read this slot's device copy are done
+  hipEvent_t staged = nullptr;  // SRSRAN_AMD_STAGE=side: this slot's last upload finished (pinned staging reusable)
+  hipEvent_t read   = nullptr;  // SRSRAN_AMD_STAGE=side: the launches that read this slot's device copy are done
+  uint32_t   seq    = 0;        // default staging: fence sequence number of the batch that last filled the slot
   bool       used   = false;
   char*      h      = nullptr;  // pinned coherent host memory (stage_host_alloc)
   char*      hd     = nullptr;  // its device alias
@@ -59,6 +60,8 @@ struct PdschGpu {
   hipStream_t                  copy    = nullptr;  // descriptor uploads, ahead of the launches that read them
   StageSlot                    ring[kStageRing];
   uint32_t                     ring_next = 0;
+  srsran_amd::StageFence       fence;  // the copy kernel's "slot read" words (stage_copy.h)
+  srsran_amd::StreamHandoff    ho;     // stream of the previous batch (device-side reuse of slots and d_work)
   char*                        d_work    = nullptr;
   size_t                       work_cap  = 0;
   float2*                      d_in      = nullptr;  // host-synchronous path: grids + estimates
@@ -96,13 +99,17 @@ bool grow_dev(void** p, size_t* cap, size_t need)
   return true;
 }
 
-bool grow_stage(StageSlot& st, size_t need)
+bool grow_stage(PdschGpu* g, StageSlot& st, size_t need)
 {
   if (st.cap >= need) {
     return true;
   }
-  if (st.used) {
-    hipEventSynchronize(st.read);
+  if (st.used) {  // the slot's last batch is done with both copies
+    if (srsran_amd::stage_side_copy()) {
+      hipEventSynchronize(st.read);
+    } else {
+      srsran_amd::handoff_drain(g->ho);
+    }
   }
   hipHostFree(st.h);
   hipFree(st.d);
@@ -122,11 +129,11 @@ bool init_ring(PdschGpu* g)
 {
   for (StageSlot& st : g->ring) {
     if (srsran_amd::ring_event_create(&st.staged) != hipSuccess ||
-        srsran_amd::ring_event_create(&st.read) != hipSuccess || !grow_stage(st, 65536)) {
+        srsran_amd::ring_event_create(&st.read) != hipSuccess || !grow_stage(g, st, 65536)) {
       return false;
     }
   }
-  return true;
+  return srsran_amd::stage_fence_init(g->fence, kStageRing);
 }
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -349,14 +356,17 @@ int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sf
   const size_t ev_bytes = align256(evs.size() * sizeof(EvmItem));
   desc.stop();
   srsran_amd::HostScope wait(srsran_amd::HP_PDSCH_WAIT);
-  StageSlot& st    = g->ring[g->ring_next];
+  const bool side   = srsran_amd::stage_side_copy();
+  const int  slot   = (int)g->ring_next;
+  StageSlot& st     = g->ring[slot];
   g->ring_next = (g->ring_next + 1) % kStageRing;
-  if (st.used && hipEventSynchronize(st.staged) != hipSuccess) {
+  if (st.used && (side ? hipEventSynchronize(st.staged) != hipSuccess
+                       : !srsran_amd::stage_fence_wait(g->fence, slot, st.seq))) {
     return SRSRAN_ERROR;
   }
   if (st.cap < pa_bytes + li_bytes + ev_bytes) {  // every slot of the ring grows now, not when it comes round
     for (StageSlot& r : g->ring) {
-      if (!grow_stage(r, 2 * (pa_bytes + li_bytes + ev_bytes))) {
+      if (!grow_stage(g, r, 2 * (pa_bytes + li_bytes + ev_bytes))) {
         return SRSRAN_ERROR;
       }
     }
@@ -376,7 +386,6 @@ int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sf
   }
   // SRSRAN_AMD_STAGE=side (round 3): the upload on a copy stream once the launches of the batch that last used
   // this slot are done with its device copy, beside the OFDM / estimation stages
-  const bool side = srsran_amd::stage_side_copy();
   if (side) {
     if (st.used) {
       hipStreamWaitEvent(g->copy, st.read, 0);
@@ -384,22 +393,31 @@ int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sf
     hipMemcpyAsync(st.d, st.h, pa_bytes + li_bytes + ev_bytes, hipMemcpyHostToDevice, g->copy);
     hipEventRecord(st.staged, g->copy);
     hipStreamWaitEvent(s, st.staged, 0);
-  } else {  // in line: a copy kernel reads the pinned slot (stage_copy.h)
-    // ... which also zeroes the batch's CSI maxima (no memset launch)
-    if (srsran_amd::stage_copy_launch(st.d, st.hd, pa_bytes + li_bytes + ev_bytes, s, (uint32_t*)d_max,
-                                      nsf * 2) != hipSuccess) {
+  } else {  // in line: a copy kernel reads the pinned slot and then marks it read in the fence (stage_copy.h)
+    // ... and zeroes the batch's CSI maxima (no memset launch)
+    if (srsran_amd::handoff(g->ho, s) != hipSuccess) {
       return SRSRAN_ERROR;
     }
-    hipEventRecord(st.staged, s);
+    st.seq = ++g->fence.seq;
+    if (srsran_amd::stage_copy_launch(st.d, st.hd, pa_bytes + li_bytes + ev_bytes, s, (uint32_t*)d_max, nsf * 2,
+                                      &g->fence, slot, st.seq) != hipSuccess) {
+      return SRSRAN_ERROR;
+    }
   }
   st.used = true;
   // from here on the slot belongs to this batch: its read event is recorded on every exit, so the upload that
   // next reuses it waits for whatever of this one was enqueued, error paths included
   struct ReadMark {
-    StageSlot&      st;
+    StageSlot&  st;
     hipStream_t s;
-    ~ReadMark() { hipEventRecord(st.read, s); }
-  } mark{st, s};
+    bool        on;
+    ~ReadMark()
+    {
+      if (on) {
+        hipEventRecord(st.read, s);
+      }
+    }
+  } mark{st, s, side};
   if (side) {
     hipMemsetAsync(d_max, 0, (size_t)nsf * 2 * sizeof(float), s);
   }
@@ -492,6 +510,8 @@ void srsran_pdsch_free(srsran_pdsch_t* q)
     if (g->copy) {
       hipStreamDestroy(g->copy);
     }
+    srsran_amd::stage_fence_free(g->fence);
+    srsran_amd::handoff_free(g->ho);
     delete g;
   }
   srsran_sch_free(&q->dl_sch);
@@ -779,7 +799,8 @@ int srsran_pdsch_encode(srsran_pdsch_t*     q,
     it.mod[cw]  = (int)tb.mod;
     cw++;
   }
-  if ((scheme == 3) != (cw == 2) || !grow_dev((void**)&g->d_work, &g->work_cap, off)) {
+  if ((scheme == 3) != (cw == 2) || !grow_dev((void**)&g->d_work, &g->work_cap, off) ||
+      srsran_amd::handoff(g->ho, g->stream) != hipSuccess) {  // d_work: after the batches queued elsewhere
     return SRSRAN_ERROR;
   }
   char* base = g->d_work;

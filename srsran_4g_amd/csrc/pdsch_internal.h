@@ -27,5 +27,19 @@ int dlsch_gpu_decode_batch_early_copy(srsran_sch_t* q, uint32_t nof_tb, const sr
 int dlsch_gpu_decode_batch_limits(srsran_sch_t* q, uint32_t nof_tb, const srsran_dlsch_gpu_tb_t* tbs,
                                   const uint32_t* max_noi, int32_t* d_result, float* d_avg_noi, void* stream);
 
+// srsran_chest_dl_gpu_estimate_batch_cfg with the nsf <= CHEST_INLINE_SF subframe indices h_sf[b] = tti % 10 given on
+// the host and carried in the launch's arguments (chest_api.cpp)
+int chest_dl_gpu_estimate_batch_inline(srsran_chest_dl_t*           q,
+                                       const srsran_chest_dl_cfg_t* cfg,
+                                       const uint8_t*               h_sf,
+                                       uint32_t                     nsf,
+                                       const cf_t*                  d_grid,
+                                       size_t                       grid_sf_stride,
+                                       cf_t*                        d_ce,
+                                       size_t                       ce_sf_stride,
+                                       int                          full_grid,
+                                       float*                       d_res,
+                                       void*                        stream);
+
 }  // namespace srsran_amd
 #endif

@@ -268,8 +268,9 @@ namespace {
 // still reads earlier ones' descriptors, and waits only for the slot's previous user (kStageRing batches back).
 constexpr int kStageRing = 3;
 struct StageSlot {
-  hipEvent_t staged = nullptr;  // this slot's last upload done (pinned staging reusable)
-  hipEvent_t done   = nullptr;  // the batch that last used this slot finished with its descriptors
+  hipEvent_t staged = nullptr;  // SRSRAN_AMD_STAGE=side: this slot's last upload done (pinned staging reusable)
+  hipEvent_t done   = nullptr;  // SRSRAN_AMD_STAGE=side: the batch that last used this slot finished with it
+  uint32_t   seq    = 0;        // default staging: fence sequence number of the batch that last filled the slot
   bool       used   = false;
   char*      h      = nullptr;  // pinned coherent host memory (stage_host_alloc)
   char*      hd     = nullptr;  // its device alias
@@ -283,6 +284,8 @@ struct SchCtx {
   hipEvent_t  done   = nullptr;  // last batch finished with the shared scratch (cbout, flags, chunk CRCs, wide rows)
   StageSlot   ring[kStageRing];
   uint32_t    ring_next = 0;
+  srsran_amd::StageFence    fence;  // the copy kernel's "slot read" words (stage_copy.h)
+  srsran_amd::StreamHandoff ho;     // stream of the previous batch (device-side reuse of slots and scratch)
   uint8_t*    d_cbout = nullptr;
   uint8_t*    d_noi = nullptr;
   uint8_t*    d_crc_ok = nullptr;
@@ -329,7 +332,19 @@ bool init_ring(SchCtx* x)
       return false;
     }
   }
-  return true;
+  return srsran_amd::stage_fence_init(x->fence, kStageRing);
+}
+
+// the object's previous batches are done with its shared device state (grow paths)
+void drain_batches(SchCtx* x)
+{
+  if (srsran_amd::stage_side_copy()) {
+    if (x->used) {
+      hipEventSynchronize(x->done);
+    }
+  } else {
+    srsran_amd::handoff_drain(x->ho);
+  }
 }
 
 bool grow_dev(void** p, size_t* cap, size_t need)
@@ -457,9 +472,7 @@ int enqueue_batch(srsran_sch_t* q, uint32_t ntb, const srsran_dlsch_gpu_tb_t* tb
       }
     }
     if (wide.size() > x->wide_cap) {
-      if (x->used) {
-        hipEventSynchronize(x->done);
-      }
+      drain_batches(x);
       hipFree(x->d_wide);
       x->d_wide         = nullptr;
       const size_t rows = std::max(wide.size() * 2, (size_t)16);
@@ -526,9 +539,15 @@ int enqueue_batch(srsran_sch_t* q, uint32_t ntb, const srsran_dlsch_gpu_tb_t* tb
     t.tbs           = plan[i].s.tbs;
   }
 
-  // the previous batch of this object must be done with the shared scratch
-  if (x->used) {
-    hipStreamWaitEvent(stream, x->done, 0);
+  // the previous batch of this object must be done with the shared scratch: ordered by the stream, or by the
+  // hand-over when this batch comes on another stream (side staging: the round-3 event)
+  const bool side = srsran_amd::stage_side_copy();
+  if (side) {
+    if (x->used) {
+      hipStreamWaitEvent(stream, x->done, 0);
+    }
+  } else if (srsran_amd::handoff(x->ho, stream) != hipSuccess) {
+    return SRSRAN_ERROR;
   }
   const size_t off_cbs  = align16(nslots * sizeof(RmSlot));
   const size_t off_tb   = off_cbs + align16(ncbs * sizeof(TdecCb));
@@ -536,10 +555,15 @@ int enqueue_batch(srsran_sch_t* q, uint32_t ntb, const srsran_dlsch_gpu_tb_t* tb
   const size_t bytes    = off_wide + align16(wide.size() * sizeof(Widen8));
   desc.stop();
   srsran_amd::HostScope wait(srsran_amd::HP_SCH_WAIT);
-  StageSlot& st    = x->ring[x->ring_next];
+  const int  slot   = (int)x->ring_next;
+  StageSlot& st     = x->ring[slot];
   x->ring_next = (x->ring_next + 1) % kStageRing;
   if (st.used) {
-    hipEventSynchronize(st.staged);
+    if (side) {
+      hipEventSynchronize(st.staged);
+    } else if (!srsran_amd::stage_fence_wait(x->fence, slot, st.seq)) {
+      return SRSRAN_ERROR;
+    }
   }
   wait.stop();
   srsran_amd::HostScope launch(srsran_amd::HP_SCH_LAUNCH);
@@ -550,7 +574,11 @@ int enqueue_batch(srsran_sch_t* q, uint32_t ntb, const srsran_dlsch_gpu_tb_t* tb
         continue;
       }
       if (r.used) {
-        hipEventSynchronize(r.done);
+        if (side) {
+          hipEventSynchronize(r.done);
+        } else {
+          srsran_amd::handoff_drain(x->ho);
+        }
       }
       hipHostFree(r.h);
       hipFree(r.d);
@@ -565,9 +593,7 @@ int enqueue_batch(srsran_sch_t* q, uint32_t ntb, const srsran_dlsch_gpu_tb_t* tb
     }
   }
   if (nslots > x->slot_cap) {
-    if (x->used) {
-      hipEventSynchronize(x->done);
-    }
+    drain_batches(x);
     {
       const size_t cap = std::max((size_t)nslots * 2, (size_t)64);
       hipFree(x->d_cbout);
@@ -605,11 +631,11 @@ int enqueue_batch(srsran_sch_t* q, uint32_t ntb, const srsran_dlsch_gpu_tb_t* tb
   // in-stream upload (the cross-stream wait costs a standalone DL-SCH batch ~10 us).
   // Default: a copy kernel in the launch stream reads the pinned slot (stage_copy.h) -- no copy-engine launch
   // and no cross-stream waits, each of which left the GPU idle ~10-15 us (r04j trace).
-  if (!srsran_amd::stage_side_copy()) {
-    if (srsran_amd::stage_copy_launch(st.d, st.hd, bytes, stream) != hipSuccess) {
+  if (!side) {
+    st.seq = ++x->fence.seq;
+    if (srsran_amd::stage_copy_launch(st.d, st.hd, bytes, stream, nullptr, 0, &x->fence, slot, st.seq) != hipSuccess) {
       return SRSRAN_ERROR;
     }
-    hipEventRecord(st.staged, stream);
   } else {
     hipStream_t up = stream;
     if (early_copy) {
@@ -652,8 +678,10 @@ int enqueue_batch(srsran_sch_t* q, uint32_t ntb, const srsran_dlsch_gpu_tb_t* tb
   if (ret == SRSRAN_SUCCESS && tb_launch((const SchTb*)(ds + off_tb), ntb, max_tbs, stream) != hipSuccess) {
     ret = SRSRAN_ERROR;
   }
-  hipEventRecord(x->done, stream);
-  hipEventRecord(st.done, stream);
+  if (side) {
+    hipEventRecord(x->done, stream);
+    hipEventRecord(st.done, stream);
+  }
   return ret;
 }
 
@@ -1098,6 +1126,7 @@ void srsran_sch_free(srsran_sch_t* q)
   }
   SchCtx* x = (SchCtx*)q->gpu;
   if (x) {
+    srsran_amd::handoff_drain(x->ho);  // batches on the caller's streams
     if (x->stream) {
       hipStreamSynchronize(x->stream);
       hipStreamDestroy(x->stream);
@@ -1119,6 +1148,8 @@ void srsran_sch_free(srsran_sch_t* q)
       hipHostFree(st.h);
       hipFree(st.d);
     }
+    srsran_amd::stage_fence_free(x->fence);
+    srsran_amd::handoff_free(x->ho);
     hipFree(x->d_cbout);
     hipFree(x->d_noi);
     hipFree(x->d_crc_ok);

@@ -21,6 +21,7 @@
 #include <algorithm>
 
 #include "crc24_dev.h"
+#include "gmem.h"
 #include "sch_kernel.h"
 #include "tdec_kernel.h"
 #include "stage_copy.h"
@@ -84,34 +85,74 @@ __global__ __launch_bounds__(RM_THREADS) void rm_rx_kernel(const RmSlot* __restr
 // (4 positions per thread per pass: 8-byte table and soft-buffer accesses, coalesced).
 static constexpr int RM_LDS_THREADS = 512;
 
+// one 4-position group: the soft-buffer values v plus every contribution es[idx + j N] of each position
+__device__ __forceinline__ uint2 rm_group(uint2 iv, uint2 v, const short* es, uint32_t E, uint32_t N)
+{
+  const uint32_t idx[4] = {iv.x & 0xffffu, iv.x >> 16, iv.y & 0xffffu, iv.y >> 16};
+  int16_t        acc[4] = {(int16_t)(v.x & 0xffffu), (int16_t)(v.x >> 16), (int16_t)(v.y & 0xffffu),
+                           (int16_t)(v.y >> 16)};
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    if (idx[k] != 0xffffu) {
+      int16_t a = acc[k];
+      for (uint32_t i = idx[k]; i < E; i += N) {  // one period, plus repetitions when E > N
+        a = (int16_t)(a + es[i]);
+      }
+      acc[k] = a;
+    }
+  }
+  return make_uint2((uint32_t)(uint16_t)acc[0] | ((uint32_t)(uint16_t)acc[1] << 16),
+                    (uint32_t)(uint16_t)acc[2] | ((uint32_t)(uint16_t)acc[3] << 16));
+}
+
 __global__ __launch_bounds__(RM_LDS_THREADS) void rm_rx_lds_kernel(const RmSlot* __restrict__ slots)
 {
-  __shared__ short es[RM_LDS_MAX_E];
+  // E LLRs staged as 16-byte words from the aligned address at or below e (es = the E values from `sh` on;
+  // the words never cross a page, so reading the partial first / last word stays inside mapped memory)
+  __shared__ uint4 es4[(RM_LDS_MAX_E + 7) / 8 + 1];
   const RmSlot     s = slots[blockIdx.x];
-  if (!s.overwrite && *s.skip) {
+  if (!s.overwrite && *gptr(s.skip)) {
     return;
   }
-  const int tid = threadIdx.x;
-  for (uint32_t i = tid; i < s.E; i += RM_LDS_THREADS) {
-    es[i] = s.e[i];
+  const int                  tid = threadIdx.x;
+  const uintptr_t            ea  = (uintptr_t)s.e;
+  const uint32_t             sh  = (uint32_t)(ea & 15u) / 2;
+  const gptr_t<const uint4>  src = gptr(reinterpret_cast<const uint4*>(ea - 2 * sh));
+  const uint32_t             n16 = (sh + s.E + 7) / 8;
+  uint32_t                   i   = tid;
+  for (; i + 3 * RM_LDS_THREADS < n16; i += 4 * RM_LDS_THREADS) {  // four loads in flight before the LDS stores
+    const uint4 w0 = src[i], w1 = src[i + RM_LDS_THREADS], w2 = src[i + 2 * RM_LDS_THREADS],
+                w3 = src[i + 3 * RM_LDS_THREADS];
+    es4[i]                      = w0;
+    es4[i + RM_LDS_THREADS]     = w1;
+    es4[i + 2 * RM_LDS_THREADS] = w2;
+    es4[i + 3 * RM_LDS_THREADS] = w3;
+  }
+  for (; i < n16; i += RM_LDS_THREADS) {
+    es4[i] = src[i];
   }
   __syncthreads();
-  for (uint32_t p = 4 * (uint32_t)tid; p < s.len; p += 4 * RM_LDS_THREADS) {
-    const uint2 iv = *reinterpret_cast<const uint2*>(s.inv + p);
-    uint2       v  = s.overwrite ? make_uint2(0, 0) : *reinterpret_cast<const uint2*>(s.sb + p);
-    short acc[4] = {(short)(v.x & 0xffffu), (short)(v.x >> 16), (short)(v.y & 0xffffu), (short)(v.y >> 16)};
+  const short*                 es  = reinterpret_cast<const short*>(es4) + sh;
+  const gptr_t<const uint2>    inv = gptr(reinterpret_cast<const uint2*>(s.inv));
+  const gptr_t<uint2>          sb  = gptr(reinterpret_cast<uint2*>(s.sb));
+  constexpr int                UP  = 4;  // 4-position groups per thread whose table / buffer loads go together
+  for (uint32_t g0 = tid; 4 * g0 < s.len; g0 += UP * RM_LDS_THREADS) {
+    uint2 iv[UP], v[UP];
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const uint32_t idx = k == 0 ? (iv.x & 0xffffu) : k == 1 ? (iv.x >> 16) : k == 2 ? (iv.y & 0xffffu) : (iv.y >> 16);
-      if (idx != 0xffffu) {
-        for (uint32_t i = idx; i < s.E; i += s.N) {  // one period, plus repetitions when E > N
-          acc[k] = (short)(acc[k] + es[i]);
-        }
+    for (int u = 0; u < UP; u++) {
+      const uint32_t g = g0 + u * RM_LDS_THREADS;
+      if (4 * g < s.len) {
+        iv[u] = inv[g];
+        v[u]  = s.overwrite ? make_uint2(0, 0) : sb[g];
       }
     }
-    v.x                                  = (uint32_t)(uint16_t)acc[0] | ((uint32_t)(uint16_t)acc[1] << 16);
-    v.y                                  = (uint32_t)(uint16_t)acc[2] | ((uint32_t)(uint16_t)acc[3] << 16);
-    *reinterpret_cast<uint2*>(s.sb + p) = v;
+#pragma unroll
+    for (int u = 0; u < UP; u++) {
+      const uint32_t g = g0 + u * RM_LDS_THREADS;
+      if (4 * g < s.len) {
+        sb[g] = rm_group(iv[u], v[u], es, s.E, s.N);
+      }
+    }
   }
 }
 
@@ -136,8 +177,9 @@ constexpr uint32_t ce_clmul_mod24(uint32_t a, uint32_t b, uint32_t poly)
   return (uint32_t)r;
 }
 // zero bytes [0, nbytes) of p with 16-byte stores where aligned (block-cooperative)
-__device__ void zero_bytes(uint8_t* p, uint32_t nbytes, int tid, int nthreads)
+__device__ void zero_bytes(uint8_t* p_, uint32_t nbytes, int tid, int nthreads)
 {
+  const gptr_t<uint8_t> p = gptr(p_);
   const uint32_t head = (uint32_t)((16 - ((uintptr_t)p & 15)) & 15);
   if (nbytes <= head + 16) {
     for (uint32_t i = tid; i < nbytes; i += nthreads) {
@@ -149,7 +191,7 @@ __device__ void zero_bytes(uint8_t* p, uint32_t nbytes, int tid, int nthreads)
   for (uint32_t i = tid; i < head; i += nthreads) {
     p[i] = 0;
   }
-  uint4* v = reinterpret_cast<uint4*>(p + head);
+  const gptr_t<uint4> v = reinterpret_cast<gptr_t<uint4>>(p + head);
   for (uint32_t i = tid; i < nvec; i += nthreads) {
     v[i] = make_uint4(0, 0, 0, 0);
   }
@@ -164,7 +206,7 @@ __device__ void reset_range(const SchTb& t, uint32_t sb0, uint32_t n, uint32_t f
 {
   const int tid = threadIdx.x;
   if (sb0 < n) {  // soft buffers are 8-byte aligned, sb_stride a multiple of 4
-    uint2*         p   = reinterpret_cast<uint2*>(t.sbuf + (size_t)sb0 * t.sb_stride);
+    const gptr_t<uint2> p = gptr(reinterpret_cast<uint2*>(t.sbuf + (size_t)sb0 * t.sb_stride));
     const uint32_t n64 = (n - sb0) * t.sb_stride / 4;
     for (uint32_t i = tid; i < n64; i += TB_THREADS) {
       p[i] = make_uint2(0, 0);
@@ -181,7 +223,7 @@ __device__ void reset_range(const SchTb& t, uint32_t sb0, uint32_t n, uint32_t f
     }
   }
   for (uint32_t c = f0 + tid; c < t.max_cb; c += TB_THREADS) {
-    t.cb_crc[c] = 0;
+    gptr(t.cb_crc)[c] = 0;
   }
 }
 
@@ -206,13 +248,13 @@ __device__ void tb_geometry(const SchTb& t, TbGeom& g)
     const uint32_t K    = tid < (int)t.C1 ? t.K1 : t.K2;
     const uint32_t rlen = t.C == 1 ? K : K - 24;
     const uint32_t slot = t.slot0 + tid;
-    const uint32_t n    = t.noi[slot];
+    const uint32_t n    = gptr(t.noi)[slot];
     const bool     skip = n == 0;  // CB CRC was already OK: copy the saved payload (sch.c:476-480)
     g.start[tid]        = tid * rlen / 8;
     g.rlen8[tid]        = rlen / 8;
     g.len[tid]          = skip ? rlen / 8 : K / 8;
     g.src[tid]          = skip ? t.saved + (size_t)tid * t.saved_stride : t.cbout + (size_t)slot * SCH_SLOT_BYTES;
-    g.okf[tid]          = skip ? 1u : t.crc_ok[slot];
+    g.okf[tid]          = skip ? 1u : gptr(t.crc_ok)[slot];
     atomicAdd(&g.noi_sum, n);
     atomicMax(&g.end, g.start[tid] + g.len[tid]);
   }
@@ -231,7 +273,7 @@ __device__ __forceinline__ uint8_t tb_byte(const SchTb& t, const TbGeom& g, uint
       c--;
     }
   }
-  return g.src[c][p - g.start[c]];
+  return gptr(g.src[c])[p - g.start[c]];
 }
 
 // CRC24A byte table and x^(128 k) mod CRC24A (k = 0..63), built at compile time
@@ -309,17 +351,17 @@ __device__ uint32_t assemble_chunk(const SchTb& t, const TbGeom& g, const uint32
         } else if (c + 1 < (int)t.C && (uint32_t)p >= g.start[c + 1]) {
           c++;
         }
-        v = g.src[c][p - g.start[c]];
+        v = gptr(g.src[c])[p - g.start[c]];
       } else {
         v = tb_byte(t, g, (uint32_t)p);
       }
-      t.data[p] = (uint8_t)v;
+      gptr(t.data)[p] = (uint8_t)v;
     }
     crc = ((crc << 8) ^ ctab[((crc >> 16) ^ v) & 0xFFu]) & 0xFFFFFFu;
   }
   if (chunk == 0) {  // bytes past the CRC'd message
     for (uint32_t p = (uint32_t)nbytes + lane; p < g.end; p += 64) {
-      t.data[p] = tb_byte(t, g, p);
+      gptr(t.data)[p] = tb_byte(t, g, p);
     }
   }
   crc = clmul24(crc, kCrcT.xp16[63 - lane], LTE_CRC24A);
@@ -381,7 +423,7 @@ __global__ __launch_bounds__(TB_FIN_THREADS) void tb_kernel(const SchTb* __restr
       if (g.okf[c]) {
         keep |= 1u << c;
         for (uint32_t i = tid; i < g.rlen8[c]; i += TB_FIN_THREADS) {
-          t.saved[(size_t)c * t.saved_stride + i] = t.data[g.start[c] + i];
+          gptr(t.saved)[(size_t)c * t.saved_stride + i] = gptr(t.data)[g.start[c] + i];
         }
       }
     }
@@ -403,7 +445,7 @@ __global__ __launch_bounds__(TB_FIN_THREADS) void tb_kernel(const SchTb* __restr
     tb_fail = tb_crc != 0;  // srsran_softbuffer_rx_reset_cb_crc (sch.c:567)
   }
   if (tid < (int)C) {
-    t.cb_crc[tid] = (g.okf[tid] && !tb_fail) ? 1 : 0;
+    gptr(t.cb_crc)[tid] = (g.okf[tid] && !tb_fail) ? 1 : 0;
   }
   if (t.new_data) {
     // what reset_tbs cleared and this decode did not rewrite: flags past C, soft
@@ -541,11 +583,13 @@ hipError_t ul_deint_batch_launch(const UlDeint* d_desc, uint32_t ntb, uint32_t m
 
 }  // namespace srsran_amd
 
-// ---------------- descriptor staging (stage_copy.h) ----------------
+// ---------------- descriptor staging (stage_copy.h; host side in stage_copy.cpp) ----------------
 namespace srsran_amd {
 
 __global__ __launch_bounds__(256) void stage_copy_kernel(uint4* __restrict__ dst, const uint4* __restrict__ src,
-                                                         uint32_t n16, uint32_t* __restrict__ zero, uint32_t nz)
+                                                         uint32_t n16, uint32_t* __restrict__ zero, uint32_t nz,
+                                                         uint32_t* __restrict__ fence, uint32_t* __restrict__ count,
+                                                         uint32_t seq)
 {
   for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n16; i += gridDim.x * 256) {
     dst[i] = src[i];
@@ -553,43 +597,29 @@ __global__ __launch_bounds__(256) void stage_copy_kernel(uint4* __restrict__ dst
   for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < nz; i += gridDim.x * 256) {
     zero[i] = 0;
   }
-}
-
-void* stage_host_alloc(size_t bytes, void** dev)
-{
-  void* h = nullptr;
-  *dev    = nullptr;
-  if (hipHostMalloc(&h, bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
-    return nullptr;
+  if (fence) {
+    __syncthreads();  // every load of this workgroup has returned (its value was stored above)
+    if (threadIdx.x == 0) {
+      __threadfence();
+      if (atomicAdd(count, 1u) == gridDim.x - 1) {  // the last workgroup: the whole slot has been read
+        __hip_atomic_store(count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(fence, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
   }
-  if (hipHostGetDevicePointer(dev, h, 0) != hipSuccess) {
-    hipHostFree(h);
-    *dev = nullptr;
-    return nullptr;
-  }
-  return h;
-}
-
-bool stage_side_copy()
-{
-  static const bool side = [] {
-    const char* e = getenv("SRSRAN_AMD_STAGE");
-    return e && strcmp(e, "side") == 0;
-  }();
-  return side;
 }
 
 hipError_t stage_copy_launch(void* dst, const void* src_dev, size_t bytes, hipStream_t stream, uint32_t* zero,
-                             uint32_t zero_words)
+                             uint32_t zero_words, const StageFence* fence, int slot, uint32_t seq)
 {
   const uint32_t n16 = (uint32_t)((bytes + 15) / 16);
   const uint32_t nz  = zero ? zero_words : 0;
-  if (n16 == 0 && nz == 0) {
+  if (n16 == 0 && nz == 0 && !fence) {
     return hipSuccess;
   }
-  const uint32_t blocks = std::min<uint32_t>((std::max(n16, nz) + 255) / 256, 256);
+  const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((std::max(n16, nz) + 255) / 256, 256));
   hipLaunchKernelGGL(stage_copy_kernel, dim3(blocks), dim3(256), 0, stream, (uint4*)dst, (const uint4*)src_dev, n16,
-                     zero, nz);
+                     zero, nz, fence ? fence->d + slot : nullptr, fence ? fence->count : nullptr, seq);
   return hipGetLastError();
 }
 

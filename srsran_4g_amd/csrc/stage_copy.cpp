@@ -1,0 +1,117 @@
+// srsran_4g_amd/csrc/stage_copy.cpp -- host side of the descriptor staging (stage_copy.h)
+#include "stage_copy.h"
+
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+
+namespace srsran_amd {
+
+void* stage_host_alloc(size_t bytes, void** dev)
+{
+  void* h = nullptr;
+  *dev    = nullptr;
+  if (hipHostMalloc(&h, bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+    return nullptr;
+  }
+  if (hipHostGetDevicePointer(dev, h, 0) != hipSuccess) {
+    hipHostFree(h);
+    *dev = nullptr;
+    return nullptr;
+  }
+  return h;
+}
+
+bool stage_fence_init(StageFence& f, int nslots)
+{
+  void* d = nullptr;
+  void* h = stage_host_alloc((size_t)nslots * sizeof(uint32_t), &d);
+  if (!h) {
+    return false;
+  }
+  f.h = (volatile uint32_t*)h;
+  f.d = (uint32_t*)d;
+  for (int i = 0; i < nslots; i++) {
+    f.h[i] = 0;
+  }
+  f.seq = 0;
+  if (hipMalloc((void**)&f.count, sizeof(uint32_t)) != hipSuccess || hipMemset(f.count, 0, sizeof(uint32_t)) != hipSuccess) {
+    return false;
+  }
+  return true;
+}
+
+void stage_fence_free(StageFence& f)
+{
+  if (f.h) {
+    hipHostFree((void*)f.h);
+  }
+  if (f.count) {
+    hipFree(f.count);
+  }
+  f = StageFence();
+}
+
+bool stage_fence_wait(const StageFence& f, int slot, uint32_t seq)
+{
+  uint32_t spins = 0;
+  auto     t0    = std::chrono::steady_clock::now();
+  while ((int32_t)(f.h[slot] - seq) < 0) {
+#if defined(__x86_64__)
+    __builtin_ia32_pause();
+#endif
+    if ((++spins & 0xfff) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
+      return false;
+    }
+  }
+  __atomic_thread_fence(__ATOMIC_ACQUIRE);
+  return true;
+}
+
+hipError_t handoff(StreamHandoff& h, hipStream_t s)
+{
+  if (h.any && h.last != s) {
+    if (!h.ev) {
+      const hipError_t e = ring_event_create(&h.ev);
+      if (e != hipSuccess) {
+        return e;
+      }
+    }
+    hipError_t e = hipEventRecord(h.ev, h.last);
+    if (e == hipSuccess) {
+      e = hipStreamWaitEvent(s, h.ev, 0);
+    }
+    if (e != hipSuccess) {
+      return e;
+    }
+  }
+  h.last = s;
+  h.any  = true;
+  return hipSuccess;
+}
+
+void handoff_drain(StreamHandoff& h)
+{
+  if (h.any) {
+    hipStreamSynchronize(h.last);
+  }
+}
+
+void handoff_free(StreamHandoff& h)
+{
+  if (h.ev) {
+    hipEventDestroy(h.ev);
+  }
+  h = StreamHandoff();
+}
+
+bool stage_side_copy()
+{
+  static const bool side = [] {
+    const char* e = getenv("SRSRAN_AMD_STAGE");
+    return e && strcmp(e, "side") == 0;
+  }();
+  return side;
+}
+
+}  // namespace srsran_amd

@@ -2,6 +2,14 @@
 // memory (a ring slot) and one small kernel in the launch stream copies them to the slot's device copy.
 // Replaces hipMemcpyAsync on a side stream + cross-stream event waits, whose copy launch and waits left
 // the GPU idle ~10-20 us at each hand-over (gpurun_out r04j rocprof trace of the PDSCH chain).
+//
+// No events in the steady state: every event recorded into the stream left the GPU idle ~5-6 us (r04l trace,
+// device-scope release or not), so
+//  - the copy kernel itself tells the host when it has read a ring slot: its last workgroup stores the batch's
+//    sequence number into a pinned coherent fence word, on which the host waits before refilling the slot;
+//  - device-side reuse (the slot's device copy, scratch shared between batches) is ordered by the stream; only
+//    when a batch comes on another stream than the object's previous one does `handoff` make the new stream
+//    wait for everything queued on the old one.
 #ifndef SRSRAN_AMD_STAGE_COPY_H
 #define SRSRAN_AMD_STAGE_COPY_H
 #include <hip/hip_runtime.h>
@@ -14,17 +22,45 @@ namespace srsran_amd {
 // pinned host memory the GPU reads in place (mapped, coherent: no stale L2 lines when a ring slot comes round)
 // -> host pointer; *dev = its device alias
 void* stage_host_alloc(size_t bytes, void** dev);
+
+// Per-object ring fence: fence words in pinned coherent memory (one per slot) and the copy kernel's
+// workgroup counter (device, zero between launches)
+struct StageFence {
+  volatile uint32_t* h     = nullptr;
+  uint32_t*          d     = nullptr;  // device alias of h
+  uint32_t*          count = nullptr;
+  uint32_t           seq   = 0;  // last sequence number handed out
+};
+bool stage_fence_init(StageFence& f, int nslots);
+void stage_fence_free(StageFence& f);
+// blocks until slot's fence word has reached seq (wrap-safe); returns false after ~10 s (a GPU that stopped)
+bool stage_fence_wait(const StageFence& f, int slot, uint32_t seq);
+
 // dst (device) <- src_dev (device alias of stage_host_alloc memory), bytes rounded up to 16; the same launch
-// zeroes zero_words 32-bit words at `zero` (optional: a per-batch accumulator, instead of a memset launch)
+// zeroes zero_words 32-bit words at `zero` (optional: a per-batch accumulator, instead of a memset launch) and,
+// with a fence, stores seq into fence word `slot` once every workgroup has read its part
 hipError_t stage_copy_launch(void* dst, const void* src_dev, size_t bytes, hipStream_t stream, uint32_t* zero = nullptr,
-                             uint32_t zero_words = 0);
+                             uint32_t zero_words = 0, const StageFence* fence = nullptr, int slot = 0,
+                             uint32_t seq = 0);
+
 // Events that order work and free ring slots (never to publish GPU writes to host memory): device-scope release.
-// A default event's system-scope release writes back and invalidates the caches when it is recorded, which left
-// the GPU idle ~5.5 us at every record in the PDSCH chain (gpurun_out r04k rocprof trace: 5 records a batch)
 inline hipError_t ring_event_create(hipEvent_t* e)
 {
   return hipEventCreateWithFlags(e, hipEventDisableTiming | hipEventReleaseToDevice);
 }
+
+// Stream hand-over of an object's device state: a batch on stream s after batches on another stream waits (on
+// the GPU) for everything queued on that stream so far.  No-op while the stream stays the same.
+struct StreamHandoff {
+  hipStream_t last = nullptr;
+  bool        any  = false;
+  hipEvent_t  ev   = nullptr;
+};
+hipError_t handoff(StreamHandoff& h, hipStream_t s);
+// everything queued by the object so far is done (host wait; grow / free paths)
+void handoff_drain(StreamHandoff& h);
+void handoff_free(StreamHandoff& h);
+
 // SRSRAN_AMD_STAGE=side: the round-3 staging (hipMemcpyAsync on a side stream + event waits), for A/B runs
 bool stage_side_copy();
 

@@ -16,6 +16,8 @@
 #include <vector>
 
 #include "../../include/srsran_pdcch.h"
+#include "chest_kernel.h"
+#include "pdsch_internal.h"
 #include "stage_copy.h"
 #include "stage_timing.h"
 #include "../../include/srsran_ue_dl.h"
@@ -316,25 +318,43 @@ int srsran_ue_dl_gpu_decode_batch(srsran_ue_dl_t*              q,
   UeDlGpu*    g    = (UeDlGpu*)q->gpu;
   hipStream_t s    = (hipStream_t)stream;
   const bool  full = cfg->chest_cfg.estimator_alg == SRSRAN_ESTIMATOR_ALG_INTERPOLATE;  // every symbol its own row
-  const uint32_t slot = g->ring_next;
-  g->ring_next        = (slot + 1) % kStageRing;
-  if (!grow(q, g, nof_sf, full) || hipEventSynchronize(g->staged[slot]) != hipSuccess) {
+  if (!grow(q, g, nof_sf, full)) {
     return SRSRAN_ERROR;
-  }
-  uint32_t* h_sf = g->h_sf + (size_t)slot * g->cap;
-  uint32_t* d_sf = g->d_sf + (size_t)slot * g->cap;
-  for (uint32_t b = 0; b < nof_sf; b++) {
-    h_sf[b] = sfs[b].tti % 10;
   }
   const size_t nre = 12 * (size_t)q->cell.nof_prb, nrx = q->nof_rx_antennas, np = q->cell.nof_ports;
   const size_t rows = 2 * SRSRAN_CP_NSYMB(q->cell.cp);  // grid symbols per subframe
-  if (srsran_ofdm_rx_gpu(&q->fft[0], d_samples, (cf_t*)g->d_grid, (uint32_t)nrx, nof_sf, cfo, stream) ||
-      srsran_chest_dl_gpu_estimate_batch_cfg(&q->chest, &cfg->chest_cfg, d_sf, nof_sf, (const cf_t*)g->d_grid,
-                                             nrx * rows * nre, (cf_t*)g->d_ce, np * nrx * nre * (full ? rows : 1),
-                                             full ? 1 : 0, g->d_res, stream)) {
+  if (srsran_ofdm_rx_gpu(&q->fft[0], d_samples, (cf_t*)g->d_grid, (uint32_t)nrx, nof_sf, cfo, stream)) {
     return SRSRAN_ERROR;
   }
-  hipEventRecord(g->staged[slot], s);  // h_sf of this slot is free again once the estimator has run
+  if (nof_sf <= (uint32_t)srsran_amd::CHEST_INLINE_SF) {  // the indices travel in the estimator's launch arguments
+    uint8_t h_sf[srsran_amd::CHEST_INLINE_SF];
+    for (uint32_t b = 0; b < nof_sf; b++) {
+      h_sf[b] = (uint8_t)(sfs[b].tti % 10);
+    }
+    if (srsran_amd::chest_dl_gpu_estimate_batch_inline(&q->chest, &cfg->chest_cfg, h_sf, nof_sf, (const cf_t*)g->d_grid,
+                                                       nrx * rows * nre, (cf_t*)g->d_ce,
+                                                       np * nrx * nre * (full ? rows : 1), full ? 1 : 0, g->d_res,
+                                                       stream)) {
+      return SRSRAN_ERROR;
+    }
+  } else {  // larger batches: a ring slot of pinned memory the estimator reads in place
+    const uint32_t slot = g->ring_next;
+    g->ring_next        = (slot + 1) % kStageRing;
+    if (hipEventSynchronize(g->staged[slot]) != hipSuccess) {
+      return SRSRAN_ERROR;
+    }
+    uint32_t* h_sf = g->h_sf + (size_t)slot * g->cap;
+    uint32_t* d_sf = g->d_sf + (size_t)slot * g->cap;
+    for (uint32_t b = 0; b < nof_sf; b++) {
+      h_sf[b] = sfs[b].tti % 10;
+    }
+    if (srsran_chest_dl_gpu_estimate_batch_cfg(&q->chest, &cfg->chest_cfg, d_sf, nof_sf, (const cf_t*)g->d_grid,
+                                               nrx * rows * nre, (cf_t*)g->d_ce, np * nrx * nre * (full ? rows : 1),
+                                               full ? 1 : 0, g->d_res, stream)) {
+      return SRSRAN_ERROR;
+    }
+    hipEventRecord(g->staged[slot], s);  // h_sf of this slot is free again once the estimator has run
+  }
   front.stop();
   std::vector<srsran_pdsch_gpu_sf_t> ps(nof_sf);
   for (uint32_t b = 0; b < nof_sf; b++) {

@@ -407,12 +407,24 @@ __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
     s[3]     = cre;
     s[4]     = cim;
     s[5]     = noise_sf ? 1.0f : 0.0f;
-    if (a.res) {  // the subframe's last workgroup reduces its (rx, port) stats: no separate finalize launch
+  }
+  if (a.res) {  // the subframe's last workgroup reduces its (rx, port) stats: no separate finalize launch
+    __shared__ uint32_t last;
+    __shared__ float    stl[CHEST_STATS_PER_SF];
+    if (tid == 0) {
       __threadfence();
-      if (atomicAdd(&a.done[b], 1u) == a.nports * a.nrx - 1) {
-        __threadfence();
-        finalize_sf<true>(a.stats + b * CHEST_STATS_PER_SF, a.nports, a.nrx, a.nof_prb, a.symbol_sz, (float)a.nsymb,
-                          a.res + 4 * b);
+      last = atomicAdd(&a.done[b], 1u) == a.nports * a.nrx - 1;
+    }
+    __syncthreads();
+    if (last) {  // uniform: the stats of every (rx, port) loaded in parallel (device-coherent), reduced from LDS
+      __threadfence();
+      const uint32_t nst = a.nports * a.nrx * 8;
+      if (tid < nst) {
+        stl[tid] = __hip_atomic_load(a.stats + b * CHEST_STATS_PER_SF + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __syncthreads();
+      if (tid == 0) {
+        finalize_sf<false>(stl, a.nports, a.nrx, a.nof_prb, a.symbol_sz, (float)a.nsymb, a.res + 4 * b);
         __hip_atomic_store(&a.done[b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }

@@ -19,7 +19,10 @@
 
 namespace srsran_amd {
 
-static constexpr int OFDM_THREADS = 256;
+#ifndef OFDM_THREADS_CFG
+#define OFDM_THREADS_CFG 256
+#endif
+static constexpr int OFDM_THREADS = OFDM_THREADS_CFG;  // a workgroup per symbol
 
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
@@ -82,18 +85,15 @@ __device__ __forceinline__ void dft8(float2* v)
 __device__ __forceinline__ uint32_t divm(uint32_t j, uint32_t m) { return __umulhi(j, m); }
 
 // One Stockham stage of radix R (natural-order output), in place in one LDS buffer: every thread holds its butterflies' inputs in registers
-// across a barrier (at most N / OFDM_THREADS = 8 values for N <= 2048), so a symbol needs 16 KB of LDS
+// across a barrier (at most N / OFDM_THREADS values), so a symbol needs 16 KB of LDS
 // instead of the 32 KB of a ping-pong pair -- 8 workgroups a CU instead of 5 (the launch is ~2200 symbols)
 template <int R>
 __device__ __forceinline__ void stage_ip(float2* buf, const float2* __restrict__ tw, uint32_t N, uint32_t Ns,
                                          uint32_t mNs)
 {
-  constexpr int  J  = R == 8 ? 1 : R == 2 ? 4 : 2;  // butterflies per thread: N / R <= J * OFDM_THREADS
+  // butterflies per thread: N / R <= J * OFDM_THREADS (radix 3 only divides N = 3 * 2^k <= 1536)
+  constexpr int  J  = ((R == 3 ? 1536 : OFDM_MAX_N) / R + OFDM_THREADS - 1) / OFDM_THREADS;
   const uint32_t nb = N / R, tstep = N / (Ns * R);
-  static_assert(R != 8 || OFDM_MAX_N / 8 <= OFDM_THREADS, "radix-8 butterflies per thread");
-  static_assert(R != 4 || OFDM_MAX_N / 4 <= 2 * OFDM_THREADS, "radix-4 butterflies per thread");
-  static_assert(R != 2 || OFDM_MAX_N / 2 <= 4 * OFDM_THREADS, "radix-2 butterflies per thread");
-  // radix 3 only divides N = 3 * 2^k <= 1536: N / 3 <= 512 = 2 * OFDM_THREADS
   float2 v[J][R], w[J][R];  // w: twiddles, loaded first (independent of the data) so their latency overlaps
 #pragma unroll
   for (int jj = 0; jj < J; jj++) {

@@ -338,12 +338,13 @@ __device__ uint32_t assemble_chunk(const SchTb& t, const TbGeom& g, const uint32
   const int c1     = nbytes - chunk * TB_CHUNK;  // one past the chunk's last byte
   const bool uniform = t.C1 == t.C || t.K1 == t.K2;
   const int  p0      = c1 - TB_CHUNK + 16 * lane;
-  uint32_t   crc     = 0;
-  int        c       = -1;
-#pragma unroll 4
+  // the lane's 16 bytes: owners first (ALU / LDS), then every gather in flight at once, then the CRC
+  uint32_t v[16];
+  int      c = -1;
+#pragma unroll
   for (int u = 0; u < 16; u++) {
     const int p = p0 + u;
-    uint32_t  v = 0;
+    v[u]        = 0;
     if (p >= 0 && (uint32_t)p < g.end) {
       if (uniform) {
         if (c < 0) {
@@ -351,13 +352,20 @@ __device__ uint32_t assemble_chunk(const SchTb& t, const TbGeom& g, const uint32
         } else if (c + 1 < (int)t.C && (uint32_t)p >= g.start[c + 1]) {
           c++;
         }
-        v = gptr(g.src[c])[p - g.start[c]];
+        v[u] = gptr(g.src[c])[p - g.start[c]];
       } else {
-        v = tb_byte(t, g, (uint32_t)p);
+        v[u] = tb_byte(t, g, (uint32_t)p);
       }
-      gptr(t.data)[p] = (uint8_t)v;
     }
-    crc = ((crc << 8) ^ ctab[((crc >> 16) ^ v) & 0xFFu]) & 0xFFFFFFu;
+  }
+  uint32_t crc = 0;
+#pragma unroll
+  for (int u = 0; u < 16; u++) {
+    const int p = p0 + u;
+    if (p >= 0 && (uint32_t)p < g.end) {
+      gptr(t.data)[p] = (uint8_t)v[u];
+    }
+    crc = ((crc << 8) ^ ctab[((crc >> 16) ^ v[u]) & 0xFFu]) & 0xFFFFFFu;
   }
   if (chunk == 0) {  // bytes past the CRC'd message
     for (uint32_t p = (uint32_t)nbytes + lane; p < g.end; p += 64) {

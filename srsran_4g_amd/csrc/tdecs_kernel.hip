@@ -23,18 +23,9 @@
 //     Half the lanes of the lane-pair kernel per block and none of its duplicated loads, LDS writes and
 //     LLR work.  The 8-sub-block class is the SSE 8-block window decoder (turbodecoder_win.h with
 //     WINIMP sse16): the same arithmetic on half as many sub-blocks.
-//   * LDS per code block: the in-place a-priori / extrinsic array S over the soft-buffer slots (as
-//     tdec16_kernel.hip), the decision bitmap and a 16-B-a-lane exchange slot.  The window checkpoints
-//     (one state = 16 B per sub-block and window) are NOT in LDS: each wave reads back only the
-//     checkpoints it wrote itself (the "own-checkpoint" crossover below), so they live in the lane's
-//     private memory, and the LDS a code block needs is S + K/8 + 256 B -- three workgroups a CU at
-//     K = 6144 where LDS checkpoints allowed two.
-//   * the crossover: wave 0 runs alpha over windows [0, h) storing its entry checkpoints, then beta over
-//     [0, h) (alpha recomputed per window from its own checkpoints) with the LLRs; wave 1 runs beta over
-//     [h, M) storing checkpoints, then alpha over [h, M) (beta recomputed from its own checkpoints) with
-//     the LLRs.  Between the phases the waves swap one state a lane: alpha entering window h (0 -> 1) and
-//     the stored beta at position h W (1 -> 0).  Same arithmetic and the same states as the round-3
-//     schedule (which swapped every checkpoint through LDS), so the same results.
+//   * LDS per code block exactly as tdec16_kernel.hip: the in-place a-priori / extrinsic array S over
+//     the soft-buffer slots, beta / alpha checkpoints (one state = 16 B per sub-block and window) and
+//     the decision bitmap.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -219,53 +210,19 @@ __device__ __forceinline__ St trellis(const short* xt, const short* yt)
   return St{v2s{o[0], o[4]}, v2s{o[7], o[3]}, v2s{o[2], o[6]}, v2s{o[5], o[1]}};
 }
 
-// LDS of one code block (dwords): S [NSB*Ls int16] | BITS [K/8 B] | XCH [NSB lanes][16 B] (the phase
-// exchange; the CRC reduction RED [2] reuses its first two dwords after the MAP decode)
-// (TDECS_CKLDS builds: | CK [nck][2 NSB lanes][16 B], each lane's own checkpoints in LDS instead of private memory)
+// LDS of one code block (dwords): S [NSB*Ls int16] | CK [M windows][NSB lanes][16 B] | BITS [K/8 B] | RED [2]
 struct Geo {
-  int s_dw, bits_dw, xch_dw, xch_off, ck_off, nck, cb_dw;
+  int s_dw, ck_dw, bits_dw, cb_dw;
 };
-__host__ __device__ __forceinline__ Geo geo(int K, int Ls)
+__host__ __device__ __forceinline__ Geo geo(int K, int Ls, int M)
 {
   Geo g;
   g.s_dw    = (NSB * Ls + 1) / 2;
+  g.ck_dw   = M * NSB * 4;
   g.bits_dw = (K / 8 + 3) / 4;
-  g.xch_dw  = NSB * 4;
-  g.xch_off = (g.s_dw + g.bits_dw + 3) & ~3;  // XCH 16-B aligned
-  g.ck_off  = g.xch_off + g.xch_dw;
-#ifdef TDECS_CKLDS
-  const int L  = K / NSB;
-  const int Ma = (L + W - 1) / W;
-  const int h  = max(1, min((L + W) / (2 * W), L / W));
-  g.nck        = max(h, Ma - h);  // entries of one wave: h (wave 0), Ma - h (wave 1)
-#else
-  g.nck = 0;
-#endif
-  g.cb_dw = g.ck_off + g.nck * 2 * NSB * 4;
+  g.cb_dw   = g.s_dw + g.ck_dw + g.bits_dw + 2;
   return g;
 }
-#ifndef TDECS_CKLDS
-// checkpoints one wave keeps per half-iteration: max(h, Ma - h) <= (L_max + 2 W) / (2 W) with L_max = 6144 / 16
-constexpr int CKMAX = (6144 / 16 + 2 * W) / (2 * W) + 1;
-#endif
-
-// This lane's own window checkpoints of a half-iteration: private memory, or (TDECS_CKLDS) LDS entries 2 NSB
-// lanes apart (the block's lanes of both waves side by side: one ds_*_b128 per wave and entry, no conflicts).
-struct Ck {
-#ifdef TDECS_CKLDS
-  uint4* p;
-  __device__ __forceinline__ St get(int e) const
-  {
-    const uint4 v = p[e * 2 * NSB];
-    return St{u2v(v.x), u2v(v.y), u2v(v.z), u2v(v.w)};
-  }
-  __device__ __forceinline__ void set(int e, const St& q) { p[e * 2 * NSB] = make_uint4(v2u(q.a), v2u(q.b), v2u(q.c), v2u(q.d)); }
-#else
-  St v[CKMAX];
-  __device__ __forceinline__ St   get(int e) const { return v[e]; }
-  __device__ __forceinline__ void set(int e, const St& q) { v[e] = q; }
-#endif
-};
 
 struct Raw {
   uint32_t a[W];  // systematic LLR (DEC1) / slot of pi(position) (DEC2)
@@ -295,18 +252,17 @@ struct Lane {
   rsrc_t    rtf;   // tfwd (q order, SB input: slot of pi(n(q))), K entries
   lshort    S;     // this block's S (LDS)
   lshort    Ssb;   // S + s * Ls: this lane's sub-block
+  uint4*    CK;    // this block's checkpoints (LDS), [M][NSB]
   uint32_t* BITS;  // this block's decision bitmap (LDS)
-  uint4*    XCH;   // this lane's exchange slot (LDS)
-  uint4*    CK;    // TDECS_CKLDS: this lane's checkpoint entry 0 (LDS)
 };
 
-__device__ __forceinline__ void xch_put(const Lane& c, const St& p)
+__device__ __forceinline__ void ck_put(const Lane& c, int m, const St& p)
 {
-  *c.XCH = make_uint4(v2u(p.a), v2u(p.b), v2u(p.c), v2u(p.d));
+  c.CK[m * NSB + c.s] = make_uint4(v2u(p.a), v2u(p.b), v2u(p.c), v2u(p.d));
 }
-__device__ __forceinline__ St xch_get(const Lane& c)
+__device__ __forceinline__ St ck_get(const Lane& c, int m)
 {
-  const uint4 v = *c.XCH;
+  const uint4 v = c.CK[m * NSB + c.s];
   return St{u2v(v.x), u2v(v.y), u2v(v.z), u2v(v.w)};
 }
 
@@ -393,11 +349,74 @@ __device__ __forceinline__ St alpha_llr_window(const Lane& c, St P, int t0, St P
   return P;
 }
 
-// Phase-1 beta side, window at t0 >= W: backward over t0+W-1 .. t0 (FULL) or L-1 .. t0; Bst = the
-// stored beta at t0, which is the checkpoint of window t0/W - 1 when `store` (ck[t0/W - 1 - h]).
+// Split phase 2 (the helper-wave variant, HELP): the other direction's states of a window are produced
+// by a helper wave into LDS (STG: [W][64 lanes] states of this wave's lanes) and consumed by the main wave.
+__device__ __forceinline__ void stg_put(uint4* stg, int i, int lane, const St& p)
+{
+  stg[i * 64 + lane] = make_uint4(v2u(p.a), v2u(p.b), v2u(p.c), v2u(p.d));
+}
+__device__ __forceinline__ St stg_get(const uint4* stg, int i, int lane)
+{
+  const uint4 v = stg[i * 64 + lane];
+  return St{u2v(v.x), u2v(v.y), u2v(v.z), u2v(v.w)};
+}
+
+// helper of the alpha side: the first half of alpha_llr_window (beta of the window from its checkpoint)
 template <bool FULL>
-__device__ __forceinline__ St beta_window(const Lane& c, St P, int t0, bool store, St& Bst, const uint32_t* xw,
-                                          Ck& ck, int h)
+__device__ __forceinline__ void beta_recompute(const Lane& c, int t0, St Pb, const uint32_t* xw, uint4* stg, int lane)
+{
+  const int L  = c.L;
+  const int cc = FULL ? t0 + W : L;
+  const int ic = cc - t0 - 1;
+#pragma unroll
+  for (int i = W - 1; i >= 0; i--) {
+    if (FULL ? i == W - 1 : i == ic) {
+      stg_put(stg, i, lane, Pb);
+      if (cc < L && norm_at(cc)) Pb = norm(Pb);
+    } else if (FULL || i < ic) {
+      Pb = step<true>(Pb, xw[i + 1]);
+      stg_put(stg, i, lane, Pb);
+      if (FULL ? (i & 1) : norm_at(t0 + 1 + i)) Pb = norm(Pb);
+    }
+  }
+}
+
+// main alpha wave: the second half of alpha_llr_window, betas from the helper
+template <bool D2, bool BITS, bool FULL>
+__device__ __forceinline__ St alpha_llr_staged(const Lane& c, St P, int t0, const uint32_t* xw, const uint32_t* aux,
+                                               const uint4* stg, int lane)
+{
+#pragma unroll
+  for (int i = 0; i < W; i++) {
+    if (FULL || t0 + i < c.L) {
+      const Cand  cd = cand(P, bm(xw[i]));
+      const short o  = llr(cd, stg_get(stg, i, lane));
+      P              = next<false>(cd);
+      if ((i & 1) == 0) P = norm(P);
+      emit<D2, BITS>(c, t0 + i, o, aux[i], xw[i]);
+    }
+  }
+  return P;
+}
+
+// helper of the beta side: the alphas entering each position of a window [t0, t0 + W) from its entry
+// checkpoint
+__device__ __forceinline__ void alpha_recompute(int t0, St Pa, const uint32_t* xw, uint4* stg, int lane)
+{
+#pragma unroll
+  for (int i = 0; i < W; i++) {
+    stg_put(stg, i, lane, Pa);
+    if (i < W - 1) {
+      Pa = step<false>(Pa, xw[i]);
+      if (nrm(t0, i)) Pa = norm(Pa);
+    }
+  }
+}
+
+// Phase-1 beta side, window at t0 >= W: backward over t0+W-1 .. t0 (FULL) or L-1 .. t0; Bst = the
+// stored beta at t0, which is the checkpoint of window t0/W - 1 when `store`.
+template <bool FULL>
+__device__ __forceinline__ St beta_window(const Lane& c, St P, int t0, bool store, St& Bst, const uint32_t* xw)
 {
 #pragma unroll
   for (int i = W - 1; i >= 0; i--) {
@@ -406,7 +425,7 @@ __device__ __forceinline__ St beta_window(const Lane& c, St P, int t0, bool stor
       if (i == 0) {
         Bst = P;
         if (store) {
-          ck.set(t0 / W - 1 - h, P);
+          ck_put(c, t0 / W - 1, P);
         }
       }
       if ((i & 1) == 0) P = norm(P);
@@ -415,24 +434,22 @@ __device__ __forceinline__ St beta_window(const Lane& c, St P, int t0, bool stor
   return P;
 }
 
-// Window inputs of one wave, prefetched along its window sequence:
-//   wave 0: alpha training [L-40, L-24), [L-24, L-8), [L-8, L); windows 0 .. h-1 (phase 1); h-1 .. 0 (phase 2)
-//   wave 1: beta training [32, 40), [16, 32), [0, 16);          windows Ma-1 .. h (phase 1); h .. Ma-1 (phase 2)
+// Window inputs of one side, prefetched along the side's window sequence (as tdec16_kernel.hip):
+//   alpha side: training [L-40, L-24), [L-24, L-8), [L-8, L); then windows 0, 1, ..., Ma-1
+//   beta side:  training [32, 40), [16, 32), [0, 16);       then windows Ma-1, ..., 1, 0
 template <bool D2>
 struct Pipe {
   Raw      g;
   uint32_t dv[W];
-  int      nwin, Ma, h;
+  int      nwin, Ma;
   bool     beta;
 
   __device__ __forceinline__ int t0_of(int idx, int L) const
   {
-    const int j = idx - NTR;
     if (beta) {
-      const int n1 = Ma - h;
-      return idx < NTR ? (NTR - 1 - idx) * W : j < n1 ? (Ma - 1 - j) * W : (h + j - n1) * W;
+      return idx < NTR ? (NTR - 1 - idx) * W : (Ma - 1 - (idx - NTR)) * W;
     }
-    return idx < NTR ? L - OVL + W * idx : j < h ? j * W : (2 * h - 1 - j) * W;
+    return idx < NTR ? L - OVL + W * idx : (idx - NTR) * W;
   }
 
   __device__ __forceinline__ void load(const Lane& c, int idx)
@@ -475,10 +492,12 @@ struct Pipe {
   }
 };
 
-// One constituent MAP decode of this lane's sub-block in the own-checkpoint crossover (header comment):
-// wave 0 alpha on [0, h) then beta + LLR on [0, h); wave 1 beta on [h, Ma) then alpha + LLR on [h, Ma).
-template <bool D2, bool BITS>
-__device__ __forceinline__ void map16s(const Lane& cin, int wave, int st0)
+// One constituent MAP decode of this lane's sub-block; wave 0 = alpha side, wave 1 = beta side; with
+// HELP, wave 2 recomputes the betas of the alpha side's phase-2 windows and wave 3 the alphas of the beta
+// side's, one window ahead of the main waves, through the double-buffered LDS stage STG
+// ([side][buffer][W][64] states).
+template <bool D2, bool BITS, bool HELP>
+__device__ __forceinline__ void map16s(const Lane& cin, int wave, uint4* STG, int st0)
 {
   (void)st0;  // first stamp index of this half-iteration (TDECS_STAMPS builds)
   Lane c = cin;
@@ -494,19 +513,44 @@ __device__ __forceinline__ void map16s(const Lane& cin, int wave, int st0)
   const int Ma    = (L + W - 1) / W;
   const int h     = max(1, min((L + W) / (2 * W), L / W));
   Pipe<D2>  pp;
+  pp.nwin = NTR + Ma;
   pp.Ma   = Ma;
-  pp.h    = h;
   pp.beta = __builtin_amdgcn_readfirstlane(wave) != 0;
-  pp.nwin = NTR + 2 * (pp.beta ? Ma - h : h);
   uint32_t xw[W];
   uint32_t aux[W];
-  Ck       ck;  // this wave's own checkpoints
-#ifdef TDECS_CKLDS
-  ck.p = c.CK;
-#endif
+  if constexpr (HELP) {
+    const int lane = (int)(threadIdx.x & 63);
+    const int na   = Ma - h, nb = h, nj = max(na, nb);
+    if (wave >= 2) {
+      // ================= helpers: idle through training and phase 1 =================
+      pp.beta = wave == 3;
+      __syncthreads();
+      const int mtop = Ma - 1;
+      pp.load(c, wave == 2 ? NTR + h : NTR + mtop - (h - 1));
+#pragma unroll 1
+      for (int j = 0; j <= nj; j++) {
+        uint4* stg = STG + ((wave - 2) * 2 + (j & 1)) * (W * 64);
+        if (wave == 2 && j < na) {
+          const int ma = h + j;
+          pp.next(c, NTR + ma, xw, aux);
+          if (ma < Mfull) {
+            beta_recompute<true>(c, ma * W, ck_get(c, ma), xw, stg, lane);
+          } else {
+            beta_recompute<false>(c, ma * W, ck_get(c, ma), xw, stg, lane);
+          }
+        } else if (wave == 3 && j < nb) {
+          const int mb = h - 1 - j;
+          pp.next(c, NTR + mtop - mb, xw, aux);
+          alpha_recompute(mb * W, ck_get(c, mb), xw, stg, lane);
+        }
+        __syncthreads();
+      }
+      return;
+    }
+  }
   pp.start(c);
   if (wave == 0) {
-    // ================= wave 0: alpha on [0, h), then beta + LLR on [0, h) =================
+    // ================= alpha side =================
     St P = neg_state();
     TDECS_STAMP(st0);
     // training over the last 40 steps of the own sub-block (win.h:747-756)
@@ -528,12 +572,12 @@ __device__ __forceinline__ void map16s(const Lane& cin, int wave, int st0)
       q.d = u2v((uint32_t)__shfl_up((int)v2u(P.d), 1, NSB));
       P   = c.s == 0 ? alpha_known() : q;
     }
-    // phase 1: windows [0, h) (all full), entry checkpoints ck[0 .. h-1]
+    // phase 1: windows [0, h) (all full), entry checkpoints in slots 0..h-1
 #pragma unroll 1
     for (int ma = 0; ma < h; ma++) {
       const int t0 = ma * W;
       pp.next(c, NTR + ma, xw, aux);
-      ck.set(ma, P);
+      ck_put(c, ma, P);
 #pragma unroll
       for (int i = 0; i < W; i++) {
         P = step<false>(P, xw[i]);
@@ -541,44 +585,40 @@ __device__ __forceinline__ void map16s(const Lane& cin, int wave, int st0)
       }
     }
     TDECS_STAMP(st0 + 2);
-    xch_put(c, P);  // alpha entering window h, for wave 1
     __syncthreads();
-    __syncthreads();  // wave 1 has read it and left the stored beta at position h W
-    St Bst = xch_get(c);
-    P      = norm(Bst);  // wave 1's last phase-1 position (i = 0 of window h) normalises
     TDECS_STAMP(st0 + 3);
-    // phase 2: windows h-1 .. 0: alpha recomputed from the own entry checkpoint, then beta backwards with
-    // the LLR of every position
-    St ckn = ck.get(h - 1);  // the next window's checkpoint, loaded a window ahead (memory latency)
+    if constexpr (HELP) {  // phase 2 with the betas of window h + j - 1 from the helper
+      const int lane = (int)(threadIdx.x & 63);
+      const int na = Ma - h, nj = max(na, h);
 #pragma unroll 1
-    for (int mb = h - 1; mb >= 0; mb--) {
-      const int t0 = mb * W;
-      St        Pa = ckn;
-      if (mb > 0) {
-        ckn = ck.get(mb - 1);
-      }
-      pp.next(c, NTR + 2 * h - 1 - mb, xw, aux);
-      St aw[W];  // alpha entering each position (candidates rebuilt at LLR time)
-#pragma unroll
-      for (int i = 0; i < W; i++) {
-        aw[i] = Pa;
-        if (i < W - 1) {
-          Pa = step<false>(Pa, xw[i]);
-          if (nrm(t0, i)) Pa = norm(Pa);
+      for (int j = 0; j <= nj; j++) {
+        const int ma = h + j - 1;
+        if (j >= 1 && j - 1 < na) {
+          const uint4* stg = STG + ((j - 1) & 1) * (W * 64);
+          pp.next(c, NTR + ma, xw, aux);
+          if (ma < Mfull) {
+            P = alpha_llr_staged<D2, BITS, true>(c, P, ma * W, xw, aux, stg, lane);
+          } else {
+            alpha_llr_staged<D2, BITS, false>(c, P, ma * W, xw, aux, stg, lane);
+          }
         }
+        __syncthreads();
       }
-#pragma unroll
-      for (int i = W - 1; i >= 0; i--) {
-        const short o = llr(cand(aw[i], bm(xw[i])), Bst);
-        P             = step<true>(P, xw[i]);
-        Bst           = P;
-        if (nrm(t0, i)) P = norm(P);
-        emit<D2, BITS>(c, t0 + i, o, aux[i], xw[i]);
-      }
+      return;
+    }
+    // phase 2: windows [h, Ma): beta recomputed from the checkpoint above the window, then alpha + LLR
+#pragma unroll 1
+    for (int ma = h; ma < Mfull; ma++) {
+      pp.next(c, NTR + ma, xw, aux);
+      P = alpha_llr_window<D2, BITS, true>(c, P, ma * W, ck_get(c, ma), xw, aux);
+    }
+    if (Ma > Mfull) {
+      pp.next(c, NTR + Mfull, xw, aux);
+      alpha_llr_window<D2, BITS, false>(c, P, Mfull * W, ck_get(c, Mfull), xw, aux);
     }
     TDECS_STAMP(st0 + 4);
   } else {
-    // ================= wave 1: beta on [h, Ma), then alpha + LLR on [h, Ma) =================
+    // ================= beta side =================
     St P = neg_state();
     TDECS_STAMP(st0);
     // training over the first 40 steps of the own sub-block, backwards (win.h:622-630)
@@ -613,39 +653,68 @@ __device__ __forceinline__ void map16s(const Lane& cin, int wave, int st0)
       }
     }
     const int mtop = Ma - 1;
-    ck.set(mtop - h, P);  // beta[L]: the checkpoint of the top window
+    ck_put(c, mtop, P);  // beta[L]
     St Bst = P;  // stored (pre-normalisation) beta of the position above the current window
-    // phase 1: windows Ma-1 .. h from the top (the top one maybe partial); checkpoints ck[0 .. Ma-1-h]
+    // phase 1: windows [h, Ma) from the top (the top one maybe partial)
     if (Ma > Mfull) {
       pp.next(c, NTR, xw, aux);
-      P = beta_window<false>(c, P, mtop * W, mtop > h, Bst, xw, ck, h);
+      P = beta_window<false>(c, P, mtop * W, mtop > h, Bst, xw);
     }
 #pragma unroll 1
     for (int mb = Mfull - 1; mb >= h; mb--) {
       pp.next(c, NTR + mtop - mb, xw, aux);
-      P = beta_window<true>(c, P, mb * W, mb > h, Bst, xw, ck, h);
+      P = beta_window<true>(c, P, mb * W, mb > h, Bst, xw);
     }
     TDECS_STAMP(st0 + 2);
     __syncthreads();
-    P = xch_get(c);  // alpha entering window h, from wave 0
-    xch_put(c, Bst);
-    __syncthreads();
     TDECS_STAMP(st0 + 3);
-    // phase 2: windows [h, Ma): beta recomputed from the own checkpoint above the window, then alpha + LLR
-    const int n1  = Ma - h;
-    St        ckn = ck.get(0);  // the next window's checkpoint, loaded a window ahead (memory latency)
+    if constexpr (HELP) {  // phase 2 with the alphas of window h - j from the helper
+      const int lane = (int)(threadIdx.x & 63);
+      const int nj   = max(Ma - h, h);
 #pragma unroll 1
-    for (int ma = h; ma < Mfull; ma++) {
-      const St Pb = ckn;
-      if (ma + 1 < Ma) {
-        ckn = ck.get(ma + 1 - h);
+      for (int j = 0; j <= nj; j++) {
+        const int mb = h - j;
+        if (j >= 1 && j - 1 < h) {
+          const uint4* stg = STG + (2 + ((j - 1) & 1)) * (W * 64);
+          const int    t0  = mb * W;
+          pp.next(c, NTR + mtop - mb, xw, aux);
+#pragma unroll
+          for (int i = W - 1; i >= 0; i--) {
+            const short o = llr(cand(stg_get(stg, i, lane), bm(xw[i])), Bst);
+            P             = step<true>(P, xw[i]);
+            Bst           = P;
+            if (nrm(t0, i)) P = norm(P);
+            emit<D2, BITS>(c, t0 + i, o, aux[i], xw[i]);
+          }
+        }
+        __syncthreads();
       }
-      pp.next(c, NTR + n1 + ma - h, xw, aux);
-      P = alpha_llr_window<D2, BITS, true>(c, P, ma * W, Pb, xw, aux);
+      return;
     }
-    if (Ma > Mfull) {
-      pp.next(c, NTR + n1 + Mfull - h, xw, aux);
-      alpha_llr_window<D2, BITS, false>(c, P, Mfull * W, ckn, xw, aux);
+    // phase 2: windows [0, h) from the top: alpha recomputed from the entry checkpoint, then
+    // beta backwards with the LLR of every position
+#pragma unroll 1
+    for (int mb = h - 1; mb >= 0; mb--) {
+      const int t0 = mb * W;
+      pp.next(c, NTR + mtop - mb, xw, aux);
+      St Pa = ck_get(c, mb);
+      St aw[W];  // alpha entering each position (candidates rebuilt at LLR time)
+#pragma unroll
+      for (int i = 0; i < W; i++) {
+        aw[i] = Pa;
+        if (i < W - 1) {
+          Pa = step<false>(Pa, xw[i]);
+          if (nrm(t0, i)) Pa = norm(Pa);
+        }
+      }
+#pragma unroll
+      for (int i = W - 1; i >= 0; i--) {
+        const short o = llr(cand(aw[i], bm(xw[i])), Bst);
+        P             = step<true>(P, xw[i]);
+        Bst           = P;
+        if (nrm(t0, i)) P = norm(P);
+        emit<D2, BITS>(c, t0 + i, o, aux[i], xw[i]);
+      }
     }
     TDECS_STAMP(st0 + 4);
   }
@@ -653,10 +722,10 @@ __device__ __forceinline__ void map16s(const Lane& cin, int wave, int st0)
 
 }  // namespace
 
-template <bool ES>
+template <bool ES, bool HELP>
 __device__ __forceinline__ void body(const TdecArgs& a, int bid)
 {
-  constexpr int NT = 128;  // threads: 2 waves
+  constexpr int NT = HELP ? 256 : 128;  // threads: 2 main waves (+ 2 helpers)
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -667,7 +736,7 @@ __device__ __forceinline__ void body(const TdecArgs& a, int bid)
   const int L    = (int)a.L;
   const int Ls   = (int)a.Ls;
   const int M    = (L + W - 1) / W;
-  const Geo g    = geo(K, Ls);
+  const Geo g    = geo(K, Ls, M);
   const int cb   = bid * CPWG + cbw;
   const int cbl  = cb < (int)a.ncb ? cb : (int)a.ncb - 1;
   const bool live = cb < (int)a.ncb && (!ES || a.cbs[cbl].slot != TDEC_PAD_SLOT);
@@ -700,12 +769,11 @@ __device__ __forceinline__ void body(const TdecArgs& a, int bid)
   c.rtf  = make_rsrc(a.tfwd, 2u * (uint32_t)K);
   c.S    = (lshort)(short*)base;
   c.Ssb  = c.S + c.s * Ls;
-  c.BITS = base + g.s_dw;
-  uint32_t* XCH = base + g.xch_off;
-  c.XCH  = reinterpret_cast<uint4*>(XCH) + s;
-  c.CK   = reinterpret_cast<uint4*>(base + g.ck_off) + t2;
-  uint32_t* RED = XCH;  // the CRC reduction, after the MAP decode
-  constexpr bool main_wave = true;
+  c.CK   = reinterpret_cast<uint4*>(base + g.s_dw);
+  c.BITS = base + g.s_dw + g.ck_dw;
+  uint32_t* RED = c.BITS + g.bits_dw;
+  uint4*    STG = reinterpret_cast<uint4*>(smem + ((CPWG * g.cb_dw + 3) & ~3));  // HELP: [2][2][W][64]
+  const bool main_wave = !HELP || wave < 2;
 
   if constexpr (ES) {
     if (live && done && t2 == 0) {  // skipped block (sch.c:392, 476-480)
@@ -724,21 +792,21 @@ __device__ __forceinline__ void body(const TdecArgs& a, int bid)
   for (int hi = 0; hi < h_end; hi++) {
     const bool crc_now = ES && hi + 1 >= a.min_iters;  // early-stop check (sch.c:433: from the 2nd)
     for (int i = threadIdx.x; i < CPWG * g.bits_dw; i += NT) {
-      smem[(i / g.bits_dw) * g.cb_dw + g.s_dw + i % g.bits_dw] = 0u;
+      smem[(i / g.bits_dw) * g.cb_dw + g.s_dw + g.ck_dw + i % g.bits_dw] = 0u;
     }
     __syncthreads();
     const bool bits = ES ? crc_now : hi + 1 == h_end;
     if (hi & 1) {
       if (bits) {
-        map16s<true, true>(c, wave, 5 * hi);
+        map16s<true, true, HELP>(c, wave, STG, 5 * hi);
       } else {
-        map16s<true, false>(c, wave, 5 * hi);
+        map16s<true, false, HELP>(c, wave, STG, 5 * hi);
       }
     } else {
       if (bits) {
-        map16s<false, true>(c, wave, 5 * hi);
+        map16s<false, true, HELP>(c, wave, STG, 5 * hi);
       } else {
-        map16s<false, false>(c, wave, 5 * hi);
+        map16s<false, false, HELP>(c, wave, STG, 5 * hi);
       }
     }
     __syncthreads();
@@ -805,7 +873,14 @@ __device__ __forceinline__ void body(const TdecArgs& a, int bid)
 template <bool ES>
 __global__ __launch_bounds__(128, 1) void TDECS_K(kernel)(TdecArgs a)
 {
-  body<ES>(a, blockIdx.x);
+  body<ES, false>(a, blockIdx.x);
+}
+
+// Small launches (at most one workgroup per CU): phase 2 split over two helper waves
+template <bool ES>
+__global__ __launch_bounds__(256, 1) void TDECS_K(split_kernel)(TdecArgs a)
+{
+  body<ES, true>(a, blockIdx.x);
 }
 
 __global__ __launch_bounds__(128, 1) void TDECS_K(multi_kernel)(const TdecArgs* __restrict__ groups,
@@ -829,12 +904,12 @@ __global__ __launch_bounds__(128, 1) void TDECS_K(multi_kernel)(const TdecArgs* 
     }
   }
   const TdecArgs a = groups[lo];
-  body<false>(a, (int)(b - first[lo]));
+  body<false, false>(a, (int)(b - first[lo]));
 }
 
 size_t lds_bytes(const TdecArgs& a)
 {
-  const Geo g = geo((int)a.K, (int)a.Ls);
+  const Geo g = geo((int)a.K, (int)a.Ls, (int)((a.L + W - 1) / W));
   return (size_t)CPWG * g.cb_dw * 4;
 }
 
@@ -845,6 +920,16 @@ hipError_t launch(const TdecArgs& a, hipStream_t stream)
   StageScope timing_scope(ST_TDEC, stream);
   const int    grid = (a.ncb + CPWG - 1) / CPWG;
   const size_t lds  = lds_bytes(a);
+  if (a.ncb <= tdecs_split_max_cb()) {
+    const size_t lds_s = ((lds + 15) & ~(size_t)15) + (size_t)4 * W * 64 * 16;
+    tdec_set_last_kernel(a.cbs ? TDECS_NAME "split_kernel<true>" : TDECS_NAME "split_kernel<false>");
+    if (a.cbs) {
+      hipLaunchKernelGGL((TDECS_K(split_kernel)<true>), dim3(grid), dim3(256), lds_s, stream, a);
+    } else {
+      hipLaunchKernelGGL((TDECS_K(split_kernel)<false>), dim3(grid), dim3(256), lds_s, stream, a);
+    }
+    return hipGetLastError();
+  }
   tdec_set_last_kernel(a.cbs ? TDECS_NAME "kernel<true>" : TDECS_NAME "kernel<false>");
   if (a.cbs) {
     hipLaunchKernelGGL((TDECS_K(kernel)<true>), dim3(grid), dim3(128), lds, stream, a);

@@ -672,6 +672,13 @@ extern "C" int srsran_chest_dl_gpu_estimate_batch_cfg(srsran_chest_dl_t*        
                         stream);
 }
 
+// Diagnostic build only (lib/stamps/, tools/chest_stamps.py): chest_kernel workgroups write their phase clock
+// stamps to d_buf ([workgroup][16] u64) from now on; SRSRAN_ERROR in the product build
+extern "C" int srsran_chest_dl_gpu_debug_set_stamps(void* d_buf)
+{
+  return srsran_amd::chest_set_stamps(d_buf) == hipSuccess ? SRSRAN_SUCCESS : SRSRAN_ERROR;
+}
+
 namespace srsran_amd {
 int chest_dl_gpu_estimate_batch_inline(srsran_chest_dl_t*           q,
                                        const srsran_chest_dl_cfg_t* cfg,

@@ -53,6 +53,8 @@ static constexpr size_t CHEST_STATS_PER_SF  = 4 * 4 * 8;               // floats
 // estimate (subframes 0 / 5), 0 when it is noise_in
 
 hipError_t chest_launch(const ChestArgs& a, hipStream_t stream, uint32_t nsf = 1);
+// diagnostic build (-DCHEST_STAMPS) only: phase clock stamps of every chest_kernel workgroup into d_buf
+hipError_t chest_set_stamps(void* d_buf);
 // device-side reduction of the per-(rx, port) stats of nsf subframes into out[b][4] =
 // {noise_estimate, rsrp, rssi, cfo} (fill_res, chest_dl.c:962-986)
 hipError_t chest_finalize_launch(const float* stats, uint32_t np, uint32_t nrx, uint32_t nof_prb, float symbol_sz,

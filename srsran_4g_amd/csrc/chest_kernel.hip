@@ -21,7 +21,10 @@
 
 namespace srsran_amd {
 
-static constexpr int CH_THREADS = 256;
+#ifndef CH_THREADS_CFG
+#define CH_THREADS_CFG 256
+#endif
+static constexpr int CH_THREADS = CH_THREADS_CFG;  // a workgroup per (port, rx, subframe)
 
 struct cx {
   float r, i;
@@ -171,8 +174,25 @@ __device__ void finalize_sf(const float* st, uint32_t np, uint32_t nrx, uint32_t
 }
 
 
+// Diagnostic build only (-DCHEST_STAMPS, tools/chest_stamps.py): thread 0 of every workgroup writes the
+// device clock (wall_clock64, 100 MHz) at the phase boundaries below into g_chest_stamps[workgroup][16]
+#ifdef CHEST_STAMPS
+__device__ unsigned long long* g_chest_stamps = nullptr;
+#define CH_STAMP(k)                                                                                         \
+  do {                                                                                                      \
+    if (threadIdx.x == 0 && g_chest_stamps) {                                                               \
+      g_chest_stamps[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 16 + (k)] = wall_clock64();            \
+    }                                                                                                       \
+  } while (0)
+#else
+#define CH_STAMP(k) \
+  do {              \
+  } while (0)
+#endif
+
 __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
 {
+  CH_STAMP(0);
   __shared__ cx    pe[4 * CHEST_MAX_NREF];
   __shared__ cx    comb[2 * CHEST_MAX_NREF];
   __shared__ cx    avg[4 * CHEST_MAX_NREF];
@@ -220,8 +240,10 @@ __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
     const cx r = ld2(in, crs_nsymbol(k / nre, port, a.nsymb) * nre + k % nre);
     rssi += r.r * r.r + r.i * r.i;
   }
+  CH_STAMP(1);
   rsrp = block_sum(rsrp, red) / (float)np;
   rssi = block_sum(rssi, red) / (float)nsym;  // pe[] complete after block_sum's barriers
+  CH_STAMP(2);
 
   // ---- CFO phase sum (port-0 geometry, chest_dl.c:630-636) ----
   float cre = 0.f, cim = 0.f;
@@ -236,6 +258,7 @@ __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
     cim = block_sum(cim, red);
   }
 
+  CH_STAMP(3);
   // ---- noise from the pilot residuals (REFS) ----
   float noise = 0.f;
   if (kept_noise) {
@@ -279,6 +302,7 @@ __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
     noise = block_sum(p, red) / (float)(nref - 2);
   }
 
+  CH_STAMP(4);
   // ---- time average into a 3-subcarrier comb (AVERAGE), then smoothing (average_pilots) ----
   uint32_t nr = nref;
   if (a.estimator == 1) {
@@ -329,6 +353,7 @@ __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
     conv_row(comb, avg, nr, filt, M);
   }
   __syncthreads();
+  CH_STAMP(5);
 
   // ---- interpolation to every subcarrier (interp_linear_offset) and, for INTERPOLATE, between the CRS
   // symbols (interpolate_pilots, chest_dl.c:510-554); PSS noise on row nsymb - 1 (estimate_noise_pss) ----
@@ -408,6 +433,7 @@ __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
     s[4]     = cim;
     s[5]     = noise_sf ? 1.0f : 0.0f;
   }
+  CH_STAMP(6);
   if (a.res) {  // the subframe's last workgroup reduces its (rx, port) stats: no separate finalize launch
     __shared__ uint32_t last;
     __shared__ float    stl[CHEST_STATS_PER_SF];
@@ -429,6 +455,18 @@ __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
       }
     }
   }
+  CH_STAMP(7);
+}
+
+hipError_t chest_set_stamps(void* d_buf)
+{
+#ifdef CHEST_STAMPS
+  unsigned long long* p = (unsigned long long*)d_buf;
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_chest_stamps), &p, sizeof(p));
+#else
+  (void)d_buf;
+  return hipErrorNotSupported;
+#endif
 }
 
 hipError_t chest_launch(const ChestArgs& a, hipStream_t stream, uint32_t nsf)

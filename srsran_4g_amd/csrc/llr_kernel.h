@@ -41,7 +41,10 @@ struct EvmItem {
   float*       out;
 };
 hipError_t evm_finalize_launch(const EvmItem* d_items, uint32_t nitems, hipStream_t stream);
-constexpr uint32_t LLR_BLOCK_SYMBOLS = 256 * 16;  // symbols of one LLR block (evm_part entries = ceil(n / this))
+#ifndef LLR_SPT_CFG
+#define LLR_SPT_CFG 16  // symbols per thread of the LLR kernel (build parameter)
+#endif
+constexpr uint32_t LLR_BLOCK_SYMBOLS = 256 * LLR_SPT_CFG;  // symbols of one LLR block (evm_part entries = ceil(n / this))
 // nitems items of one modulation (device array); max_n = largest n
 hipError_t llr_batch_launch(int mod, const LlrItem* d_items, uint32_t nitems, uint32_t max_n, int any_scramble,
                             hipStream_t stream, bool llr8 = false);

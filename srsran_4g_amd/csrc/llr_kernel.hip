@@ -30,7 +30,7 @@ namespace srsran_amd {
 static constexpr int GOLD_NC   = 1600;  // sequence.c:39
 static constexpr int JUMP_BITS = 24;    // offsets below 2^24 bits
 static constexpr int JUMP_LVLS = 3;     // offset = b0 + 256 b1 + 65536 b2
-static constexpr int GOLD_LANE_SYMBOLS = 64;  // symbols whose sequence bits one lane of the first wave steps out
+static constexpr int GOLD_LANE_SYMBOLS = 4 * LLR_SPT_CFG;  // symbols whose sequence bits one lane of the first wave steps out
 static constexpr int GOLD_NMOD         = 5;   // BPSK .. 256QAM: Qm = 1, 2, 4, 6, 8
 
 struct GoldTables {
@@ -298,7 +298,7 @@ __device__ __forceinline__ void demap(float re, float im, uint32_t i, uint32_t n
 }
 
 static constexpr int LLR_THREADS = 256;
-static constexpr int SPT         = 16;  // symbols per thread
+static constexpr int SPT         = LLR_SPT_CFG;  // symbols per thread
 static_assert(LLR_THREADS * SPT == LLR_BLOCK_SYMBOLS, "llr_kernel.h block size");
 
 __device__ __forceinline__ float2 modulate(int mod, uint32_t i);
@@ -506,7 +506,7 @@ __device__ __forceinline__ void llr_block(const float2* __restrict__ sym_p, uint
   float       err = 0.0f;  // EVM: this thread's sum of squared symbol errors
   // the thread's symbols (and CSI) in groups of LLR_U, each group's loads issued before the first is used: one
   // HBM round trip a group instead of one a symbol
-  constexpr int LLR_U = 8;
+  constexpr int LLR_U = SPT < 8 ? SPT : 8;
   static_assert(SPT % LLR_U == 0, "whole groups");
   for (int r0 = 0; r0 < SPT; r0 += LLR_U) {
     if (t + (uint32_t)r0 * LLR_THREADS >= nb) {

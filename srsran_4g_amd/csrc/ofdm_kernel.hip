@@ -218,6 +218,7 @@ __global__ __launch_bounds__(OFDM_THREADS) void ofdm_rx_kernel(OfdmArgs a, uint3
   uint32_t          u = blockIdx.x;
   RxSym             r = rx_sym(a, u);
   rx_load(a, r, x, c);
+  run_copy_jobs(a.jobs);  // the batch's staging copies (PCIe reads) under the first symbol's HBM reads
   for (; u < nsyms; u += gridDim.x) {
 #pragma unroll
     for (int k = 0; k < U; k++) {

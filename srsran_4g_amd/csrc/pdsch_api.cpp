@@ -399,8 +399,8 @@ int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sf
       return SRSRAN_ERROR;
     }
     st.seq = ++g->fence.seq;
-    if (srsran_amd::stage_copy_launch(st.d, st.hd, pa_bytes + li_bytes + ev_bytes, s, (uint32_t*)d_max, nsf * 2,
-                                      &g->fence, slot, st.seq) != hipSuccess) {
+    if (srsran_amd::stage_copy_or_record(st.d, st.hd, pa_bytes + li_bytes + ev_bytes, s, (uint32_t*)d_max, nsf * 2,
+                                         &g->fence, slot, st.seq) != hipSuccess) {
       return SRSRAN_ERROR;
     }
   }
@@ -429,7 +429,10 @@ int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sf
       mx = std::max(mx, hp[j].n);
       j++;
     }
-    if (predecode_batch_launch(dp + i, j - i, hp[i].scheme, mx, s) != hipSuccess) {
+    const PredArgs* items = dp + i;
+    const uint32_t  n = j - i, scheme = (uint32_t)hp[i].scheme;
+    if (srsran_amd::launch_or_record([=] { return predecode_batch_launch(items, n, (int)scheme, mx, s); }) !=
+        hipSuccess) {
       return SRSRAN_ERROR;
     }
     i = j;
@@ -440,13 +443,18 @@ int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sf
       mx = std::max(mx, hl[j].n);
       j++;
     }
-    if (llr_batch_launch(cws[order_l[i]].mod, dl + i, j - i, mx, 1, s, q->llr_is_8bit) != hipSuccess) {
+    const int      mod   = cws[order_l[i]].mod;
+    const LlrItem* items = dl + i;
+    const uint32_t n     = j - i;
+    const bool     b8    = q->llr_is_8bit;
+    if (srsran_amd::launch_or_record([=] { return llr_batch_launch(mod, items, n, mx, 1, s, b8); }) != hipSuccess) {
       return SRSRAN_ERROR;
     }
     i = j;
   }
-  if (!evs.empty() &&
-      evm_finalize_launch((const EvmItem*)(st.d + pa_bytes + li_bytes), (uint32_t)evs.size(), s) != hipSuccess) {
+  const EvmItem* d_ev  = (const EvmItem*)(st.d + pa_bytes + li_bytes);
+  const uint32_t nev   = (uint32_t)evs.size();
+  if (nev && srsran_amd::launch_or_record([=] { return evm_finalize_launch(d_ev, nev, s); }) != hipSuccess) {
     return SRSRAN_ERROR;
   }
   return SRSRAN_SUCCESS;

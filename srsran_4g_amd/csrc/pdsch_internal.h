@@ -7,6 +7,7 @@
 
 #include "../../include/srsran_ue_dl.h"
 #include "eq_kernel.h"
+#include "stage_jobs.h"
 
 namespace srsran_amd {
 
@@ -40,6 +41,10 @@ int chest_dl_gpu_estimate_batch_inline(srsran_chest_dl_t*           q,
                                        int                          full_grid,
                                        float*                       d_res,
                                        void*                        stream);
+
+// srsran_ofdm_rx_gpu with the batch's staging copies fused into the launch (ofdm_api.cpp)
+int ofdm_rx_gpu_jobs(srsran_ofdm_t* q, const cf_t* d_in, cf_t* d_out, uint32_t nof_rx, uint32_t nof_sf, float cfo,
+                     void* stream, const CopyJobs* jobs);
 
 }  // namespace srsran_amd
 #endif

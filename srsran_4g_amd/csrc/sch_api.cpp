@@ -633,7 +633,8 @@ int enqueue_batch(srsran_sch_t* q, uint32_t ntb, const srsran_dlsch_gpu_tb_t* tb
   // and no cross-stream waits, each of which left the GPU idle ~10-15 us (r04j trace).
   if (!side) {
     st.seq = ++x->fence.seq;
-    if (srsran_amd::stage_copy_launch(st.d, st.hd, bytes, stream, nullptr, 0, &x->fence, slot, st.seq) != hipSuccess) {
+    if (srsran_amd::stage_copy_or_record(st.d, st.hd, bytes, stream, nullptr, 0, &x->fence, slot, st.seq) !=
+        hipSuccess) {
       return SRSRAN_ERROR;
     }
   } else {
@@ -656,26 +657,41 @@ int enqueue_batch(srsran_sch_t* q, uint32_t ntb, const srsran_dlsch_gpu_tb_t* tb
   st.used  = true;
   char* ds = st.d;
 
+  // the launches (recorded instead when a UE DL batch defers them, stage_copy.h)
   int ret = SRSRAN_SUCCESS;
   if (nslots) {
-    const hipError_t rme = b8 ? rm8_rx_slots_launch((const RmSlot*)ds, nslots, max_len, stream)
-                              : rm_rx_launch((const RmSlot*)ds, nslots, max_len, max_e, stream);
-    if (rme != hipSuccess ||
-        widen8_launch((const Widen8*)(ds + off_wide), (uint32_t)wide.size(), max_wide, stream) != hipSuccess) {
+    const RmSlot*  slots = (const RmSlot*)ds;
+    const Widen8*  wd    = (const Widen8*)(ds + off_wide);
+    const uint32_t nwide = (uint32_t)wide.size();
+    if (srsran_amd::launch_or_record([=] {
+          const hipError_t e = b8 ? rm8_rx_slots_launch(slots, nslots, max_len, stream)
+                                  : rm_rx_launch(slots, nslots, max_len, max_e, stream);
+          return e != hipSuccess ? e : widen8_launch(wd, nwide, max_wide, stream);
+        }) != hipSuccess) {
       ret = SRSRAN_ERROR;
     }
     const int n_end = q->max_iterations > 0 ? (int)q->max_iterations : 1;
     for (size_t g = 0; g < groups.size() && ret == SRSRAN_SUCCESS; g++) {
-      const uint32_t first = groups[g].second;
-      const uint32_t count = (g + 1 < groups.size() ? groups[g + 1].second : (uint32_t)cbs.size()) - first;
-      const uint32_t K     = groups[g].first;
-      const TdecCb*  dcb   = (const TdecCb*)(ds + off_cbs) + first;
-      ret = b8 && srsran_tdec_autoimp_get_subblocks_8bit(K) >= 16
-                ? tdec8_sch_enqueue(K, dcb, count, x->d_cbout, SCH_SLOT_BYTES, x->d_noi, x->d_crc_ok, n_end, stream)
-                : tdec_sch_enqueue(K, dcb, count, x->d_cbout, SCH_SLOT_BYTES, x->d_noi, x->d_crc_ok, n_end, stream);
+      const uint32_t first  = groups[g].second;
+      const uint32_t count  = (g + 1 < groups.size() ? groups[g + 1].second : (uint32_t)cbs.size()) - first;
+      const uint32_t K      = groups[g].first;
+      const TdecCb*  dcb    = (const TdecCb*)(ds + off_cbs) + first;
+      const bool     dec8   = b8 && srsran_tdec_autoimp_get_subblocks_8bit(K) >= 16;
+      uint8_t*       cbout  = x->d_cbout;
+      uint8_t*       noi    = x->d_noi;
+      uint8_t*       crc_ok = x->d_crc_ok;
+      if (srsran_amd::launch_or_record([=] {
+            const int r = dec8 ? tdec8_sch_enqueue(K, dcb, count, cbout, SCH_SLOT_BYTES, noi, crc_ok, n_end, stream)
+                               : tdec_sch_enqueue(K, dcb, count, cbout, SCH_SLOT_BYTES, noi, crc_ok, n_end, stream);
+            return r == SRSRAN_SUCCESS ? hipSuccess : hipErrorLaunchFailure;
+          }) != hipSuccess) {
+        ret = SRSRAN_ERROR;
+      }
     }
   }
-  if (ret == SRSRAN_SUCCESS && tb_launch((const SchTb*)(ds + off_tb), ntb, max_tbs, stream) != hipSuccess) {
+  const SchTb* d_tbs = (const SchTb*)(ds + off_tb);
+  if (ret == SRSRAN_SUCCESS &&
+      srsran_amd::launch_or_record([=] { return tb_launch(d_tbs, ntb, max_tbs, stream); }) != hipSuccess) {
     ret = SRSRAN_ERROR;
   }
   if (side) {

@@ -617,6 +617,14 @@ __global__ __launch_bounds__(256) void stage_copy_kernel(uint4* __restrict__ dst
   }
 }
 
+hipError_t stage_copy_job(const CopyJob& j, hipStream_t stream)
+{
+  const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((std::max(j.n16, j.nz) + 255) / 256, 256));
+  hipLaunchKernelGGL(stage_copy_kernel, dim3(blocks), dim3(256), 0, stream, j.dst, j.src, j.n16, j.zero, j.nz, j.fence,
+                     j.count, j.seq);
+  return hipGetLastError();
+}
+
 hipError_t stage_copy_launch(void* dst, const void* src_dev, size_t bytes, hipStream_t stream, uint32_t* zero,
                              uint32_t zero_words, const StageFence* fence, int slot, uint32_t seq)
 {

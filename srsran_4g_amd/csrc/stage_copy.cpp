@@ -105,6 +105,31 @@ void handoff_free(StreamHandoff& h)
   h = StreamHandoff();
 }
 
+LaunchRecorder*& launch_recorder()
+{
+  static thread_local LaunchRecorder* r = nullptr;
+  return r;
+}
+
+hipError_t stage_copy_or_record(void* dst, const void* src_dev, size_t bytes, hipStream_t stream, uint32_t* zero,
+                                uint32_t zero_words, const StageFence* fence, int slot, uint32_t seq)
+{
+  if (LaunchRecorder* r = launch_recorder()) {
+    CopyJob j;
+    j.dst   = (uint4*)dst;
+    j.src   = (const uint4*)src_dev;
+    j.n16   = (uint32_t)((bytes + 15) / 16);
+    j.nz    = zero ? zero_words : 0;
+    j.zero  = zero;
+    j.fence = fence ? fence->d + slot : nullptr;
+    j.count = fence ? fence->count : nullptr;
+    j.seq   = seq;
+    r->jobs.push_back(j);
+    return hipSuccess;
+  }
+  return stage_copy_launch(dst, src_dev, bytes, stream, zero, zero_words, fence, slot, seq);
+}
+
 bool stage_side_copy()
 {
   static const bool side = [] {

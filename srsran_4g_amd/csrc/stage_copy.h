@@ -16,6 +16,11 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <functional>
+#include <utility>
+#include <vector>
+
+#include "stage_jobs.h"
 
 namespace srsran_amd {
 
@@ -60,6 +65,29 @@ hipError_t handoff(StreamHandoff& h, hipStream_t s);
 // everything queued by the object so far is done (host wait; grow / free paths)
 void handoff_drain(StreamHandoff& h);
 void handoff_free(StreamHandoff& h);
+
+// Deferred launches (UE DL batch): while a recorder is installed on the calling thread, the batch APIs record
+// their staging copies as CopyJobs (to be fused into the chain's first kernel) and their kernel launches as
+// closures, to be replayed in order once the kernels in front of them are enqueued
+struct LaunchRecorder {
+  std::vector<CopyJob>                  jobs;
+  std::vector<std::function<hipError_t()>> launches;
+};
+LaunchRecorder*& launch_recorder();  // the calling thread's recorder; nullptr = launch immediately
+template <class F>
+hipError_t launch_or_record(F&& f)
+{
+  if (LaunchRecorder* r = launch_recorder()) {
+    r->launches.emplace_back(std::forward<F>(f));
+    return hipSuccess;
+  }
+  return f();
+}
+// stage_copy_launch, or the same as a recorded job
+hipError_t stage_copy_or_record(void* dst, const void* src_dev, size_t bytes, hipStream_t stream, uint32_t* zero,
+                                uint32_t zero_words, const StageFence* fence, int slot, uint32_t seq);
+// a recorded job as its own stage_copy_kernel launch
+hipError_t stage_copy_job(const CopyJob& j, hipStream_t stream);
 
 // SRSRAN_AMD_STAGE=side: the round-3 staging (hipMemcpyAsync on a side stream + event waits), for A/B runs
 bool stage_side_copy();

@@ -27,6 +27,7 @@ namespace {
 constexpr int kStageRing = 3;  // batches whose sf-index upload may be in flight (a ring, as the PDSCH / SCH staging)
 
 struct UeDlGpu {
+  srsran_amd::StreamHandoff ho;  // stream of the previous batch (d_grid / d_ce / d_res shared between batches)
   hipEvent_t staged[kStageRing] = {};  // the estimator launch that reads the slot's subframe indices finished
   uint32_t   ring_next          = 0;
   // subframe indices, kStageRing slots of cap entries, in pinned coherent host memory that the estimator
@@ -179,6 +180,7 @@ void srsran_ue_dl_free(srsran_ue_dl_t* q)
     srsran_regs_free(&g->regs);
     srsran_regs_free(&g->regs_mi[0]);
     srsran_regs_free(&g->regs_mi[1]);
+    srsran_amd::handoff_free(g->ho);
     delete g;
   }
   for (int j = 0; j < SRSRAN_MAX_PORTS; j++) {
@@ -323,39 +325,6 @@ int srsran_ue_dl_gpu_decode_batch(srsran_ue_dl_t*              q,
   }
   const size_t nre = 12 * (size_t)q->cell.nof_prb, nrx = q->nof_rx_antennas, np = q->cell.nof_ports;
   const size_t rows = 2 * SRSRAN_CP_NSYMB(q->cell.cp);  // grid symbols per subframe
-  if (srsran_ofdm_rx_gpu(&q->fft[0], d_samples, (cf_t*)g->d_grid, (uint32_t)nrx, nof_sf, cfo, stream)) {
-    return SRSRAN_ERROR;
-  }
-  if (nof_sf <= (uint32_t)srsran_amd::CHEST_INLINE_SF) {  // the indices travel in the estimator's launch arguments
-    uint8_t h_sf[srsran_amd::CHEST_INLINE_SF];
-    for (uint32_t b = 0; b < nof_sf; b++) {
-      h_sf[b] = (uint8_t)(sfs[b].tti % 10);
-    }
-    if (srsran_amd::chest_dl_gpu_estimate_batch_inline(&q->chest, &cfg->chest_cfg, h_sf, nof_sf, (const cf_t*)g->d_grid,
-                                                       nrx * rows * nre, (cf_t*)g->d_ce,
-                                                       np * nrx * nre * (full ? rows : 1), full ? 1 : 0, g->d_res,
-                                                       stream)) {
-      return SRSRAN_ERROR;
-    }
-  } else {  // larger batches: a ring slot of pinned memory the estimator reads in place
-    const uint32_t slot = g->ring_next;
-    g->ring_next        = (slot + 1) % kStageRing;
-    if (hipEventSynchronize(g->staged[slot]) != hipSuccess) {
-      return SRSRAN_ERROR;
-    }
-    uint32_t* h_sf = g->h_sf + (size_t)slot * g->cap;
-    uint32_t* d_sf = g->d_sf + (size_t)slot * g->cap;
-    for (uint32_t b = 0; b < nof_sf; b++) {
-      h_sf[b] = sfs[b].tti % 10;
-    }
-    if (srsran_chest_dl_gpu_estimate_batch_cfg(&q->chest, &cfg->chest_cfg, d_sf, nof_sf, (const cf_t*)g->d_grid,
-                                               nrx * rows * nre, (cf_t*)g->d_ce, np * nrx * nre * (full ? rows : 1),
-                                               full ? 1 : 0, g->d_res, stream)) {
-      return SRSRAN_ERROR;
-    }
-    hipEventRecord(g->staged[slot], s);  // h_sf of this slot is free again once the estimator has run
-  }
-  front.stop();
   std::vector<srsran_pdsch_gpu_sf_t> ps(nof_sf);
   for (uint32_t b = 0; b < nof_sf; b++) {
     srsran_pdsch_gpu_sf_t& f = ps[b];
@@ -372,7 +341,101 @@ int srsran_ue_dl_gpu_decode_batch(srsran_ue_dl_t*              q,
       f.new_data[t]  = sfs[b].new_data[t];
     }
   }
-  return srsran_pdsch_gpu_decode_batch(&q->pdsch, nof_sf, ps.data(), d_result, d_avg_noi, stream);
+  // the estimator launch (after the OFDM launch)
+  auto estimate = [&]() -> int {
+    if (nof_sf <= (uint32_t)srsran_amd::CHEST_INLINE_SF) {  // the indices travel in the estimator's launch arguments
+      uint8_t h_sf[srsran_amd::CHEST_INLINE_SF];
+      for (uint32_t b = 0; b < nof_sf; b++) {
+        h_sf[b] = (uint8_t)(sfs[b].tti % 10);
+      }
+      if (srsran_amd::chest_dl_gpu_estimate_batch_inline(&q->chest, &cfg->chest_cfg, h_sf, nof_sf, (const cf_t*)g->d_grid,
+                                                         nrx * rows * nre, (cf_t*)g->d_ce,
+                                                         np * nrx * nre * (full ? rows : 1), full ? 1 : 0, g->d_res,
+                                                         stream)) {
+        return SRSRAN_ERROR;
+      }
+    } else {  // larger batches: a ring slot of pinned memory the estimator reads in place
+      const uint32_t slot = g->ring_next;
+      g->ring_next        = (slot + 1) % kStageRing;
+      if (hipEventSynchronize(g->staged[slot]) != hipSuccess) {
+        return SRSRAN_ERROR;
+      }
+      uint32_t* h_sf = g->h_sf + (size_t)slot * g->cap;
+      uint32_t* d_sf = g->d_sf + (size_t)slot * g->cap;
+      for (uint32_t b = 0; b < nof_sf; b++) {
+        h_sf[b] = sfs[b].tti % 10;
+      }
+      if (srsran_chest_dl_gpu_estimate_batch_cfg(&q->chest, &cfg->chest_cfg, d_sf, nof_sf, (const cf_t*)g->d_grid,
+                                                 nrx * rows * nre, (cf_t*)g->d_ce, np * nrx * nre * (full ? rows : 1),
+                                                 full ? 1 : 0, g->d_res, stream)) {
+        return SRSRAN_ERROR;
+      }
+      hipEventRecord(g->staged[slot], s);  // h_sf of this slot is free again once the estimator has run
+    }
+    return SRSRAN_SUCCESS;
+  };
+  // The PDSCH / DL-SCH batch first, with its launches deferred (stage_copy.h): its descriptors depend on the
+  // configuration only, so they are built and staged now, their copies ride in the OFDM launch below (no copy
+  // kernels in the chain) and the predecoder ... TB launches are replayed after the estimator.
+  front.stop();
+  // (one DL-SCH group only: TBs with different iteration limits go through several DL-SCH batches, whose staging
+  // ring could come round within one deferred call -- such batches launch in line)
+  bool     one_limit = true;
+  uint32_t lim       = q->pdsch.dl_sch.max_iterations;
+  for (uint32_t b = 0; b < nof_sf && one_limit; b++) {
+    const uint32_t m = sfs[b].pdsch_cfg ? sfs[b].pdsch_cfg->max_nof_iterations : 0;
+    const uint32_t l = m ? m : lim;
+    one_limit        = b == 0 || l == lim;
+    lim              = l;
+  }
+  if (srsran_amd::stage_side_copy() || !one_limit) {  // in line: OFDM, estimator, then the PDSCH batch
+    if (srsran_amd::handoff(g->ho, s) != hipSuccess ||
+        srsran_ofdm_rx_gpu(&q->fft[0], d_samples, (cf_t*)g->d_grid, (uint32_t)nrx, nof_sf, cfo, stream) ||
+        estimate() != SRSRAN_SUCCESS) {
+      return SRSRAN_ERROR;
+    }
+    return srsran_pdsch_gpu_decode_batch(&q->pdsch, nof_sf, ps.data(), d_result, d_avg_noi, stream);
+  }
+  srsran_amd::LaunchRecorder rec;
+  srsran_amd::launch_recorder() = &rec;
+  const int ret = srsran_pdsch_gpu_decode_batch(&q->pdsch, nof_sf, ps.data(), d_result, d_avg_noi, stream);
+  srsran_amd::launch_recorder() = nullptr;
+  // staged slots must see their copies run whatever happens next, or their fences never come
+  auto copies_alone = [&] {
+    for (const srsran_amd::CopyJob& j : rec.jobs) {
+      srsran_amd::stage_copy_job(j, s);
+    }
+  };
+  if (ret < 0) {
+    copies_alone();
+    return ret;
+  }
+  srsran_amd::HostScope front2(srsran_amd::HP_FRONT);
+  srsran_amd::CopyJobs js{};
+  for (size_t i = 0; i < rec.jobs.size(); i++) {
+    if (i < (size_t)srsran_amd::kMaxFusedJobs) {
+      js.job[js.n++] = rec.jobs[i];
+    } else if (srsran_amd::stage_copy_job(rec.jobs[i], s) != hipSuccess) {  // beyond the fused ones: on their own
+      return SRSRAN_ERROR;
+    }
+  }
+  if (srsran_amd::handoff(g->ho, s) != hipSuccess ||
+      srsran_amd::ofdm_rx_gpu_jobs(&q->fft[0], d_samples, (cf_t*)g->d_grid, (uint32_t)nrx, nof_sf, cfo, stream, &js)) {
+    for (uint32_t i = 0; i < js.n; i++) {
+      srsran_amd::stage_copy_job(js.job[i], s);
+    }
+    return SRSRAN_ERROR;
+  }
+  if (estimate() != SRSRAN_SUCCESS) {
+    return SRSRAN_ERROR;
+  }
+  front2.stop();
+  for (auto& launch : rec.launches) {  // the deferred PDSCH / DL-SCH launches, in their order
+    if (launch() != hipSuccess) {
+      return SRSRAN_ERROR;
+    }
+  }
+  return ret;
 }
 
 // ---------------- DCI blind search (ue_dl.c:386-689) ----------------

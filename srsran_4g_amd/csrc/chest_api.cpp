@@ -49,7 +49,6 @@ struct ChestGpu {
   float2*     ce      = nullptr;
   float*      stats   = nullptr;  // [rx][port][8]
   float*      bstats  = nullptr;  // batch path: [sf][CHEST_STATS_PER_SF]
-  uint32_t*   bdone   = nullptr;  // batch path: [sf] workgroups finished (the fused finalize's counters, re-armed)
   uint32_t    bstats_cap = 0;
   uint32_t    max_prb = 0;
   uint32_t    nrx     = 0;
@@ -220,7 +219,6 @@ void srsran_chest_dl_free(srsran_chest_dl_t* q)
     hipFree(g->ce);
     hipFree(g->stats);
     hipFree(g->bstats);
-    hipFree(g->bdone);
     hipFree(g->pss);
     hipFree(g->noise);
     hipFree(g->sync);
@@ -592,13 +590,9 @@ int estimate_batch(srsran_chest_dl_t*           q,
   if (nsf > g->bstats_cap) {
     hipStreamSynchronize((hipStream_t)stream);  // the previous batch may still use them
     hipFree(g->bstats);
-    hipFree(g->bdone);
     g->bstats     = nullptr;
-    g->bdone      = nullptr;
     g->bstats_cap = 0;
-    if (hipMalloc((void**)&g->bstats, nsf * CHEST_STATS_PER_SF * sizeof(float)) != hipSuccess ||
-        hipMalloc((void**)&g->bdone, nsf * sizeof(uint32_t)) != hipSuccess ||
-        hipMemset(g->bdone, 0, nsf * sizeof(uint32_t)) != hipSuccess) {
+    if (hipMalloc((void**)&g->bstats, nsf * CHEST_STATS_PER_SF * sizeof(float)) != hipSuccess) {
       return SRSRAN_ERROR;
     }
     g->bstats_cap = nsf;
@@ -638,11 +632,13 @@ int estimate_batch(srsran_chest_dl_t*           q,
     a.noise_alg = (uint32_t)cfg->noise_alg;
   }
   const float sz = (float)srsran_symbol_sz(q->cell.nof_prb);
-  if (a.noise_alg == 0) {  // REFS: each subframe's last workgroup reduces its stats (no finalize launch)
-    a.res       = d_res;
-    a.done      = g->bdone;
-    a.symbol_sz = sz;
-    return chest_launch(a, s, nsf) == hipSuccess ? SRSRAN_SUCCESS : SRSRAN_ERROR;
+  if (a.noise_alg == 0) {  // REFS: the stats reduced by a small second launch (an in-kernel last-workgroup
+    // reduction needed device-scope fences, whose L2 write-backs cost more than the launch: r04p stamps)
+    return chest_launch(a, s, nsf) == hipSuccess &&
+                   chest_finalize_launch(g->bstats, q->cell.nof_ports, q->nof_rx_antennas, q->cell.nof_prb, sz, a.nsymb,
+                                         d_res, nsf, s) == hipSuccess
+               ? SRSRAN_SUCCESS
+               : SRSRAN_ERROR;
   }
   if (chest_launch(a, s, nsf) != hipSuccess ||
       chest_finalize_kept_launch(g->bstats, q->cell.nof_ports, q->nof_rx_antennas, q->cell.nof_prb, sz, a.nsymb,

@@ -36,11 +36,6 @@ struct ChestArgs {
   const uint32_t* sf_idx;     // [b] subframe index (tti % 10): pilots + sf_idx[b] * CHEST_PILOTS_PER_SF; null = as given
   size_t          grid_sf_stride; // float2 between subframes of `grid`
   size_t          ce_sf_stride;   // float2 between subframes of `ce`
-  // ---- fused finalize (REFS noise): the last workgroup of subframe b to finish reduces its stats into
-  // res[b][4] (chest_finalize_launch's result) and re-arms done[b]; null res = finalize launched separately ----
-  float*          res;
-  uint32_t*       done;       // [b] workgroups of the subframe finished (zero between batches)
-  float           symbol_sz;
   // subframe indices carried in the launch arguments (batches of <= CHEST_INLINE_SF subframes, sf_inl = 1): no
   // host buffer for the GPU to read, so no ring slot and no event to free it
   uint32_t        sf_inl;

@@ -127,17 +127,6 @@ __device__ __forceinline__ void ivec(float2* col, uint32_t stride, cx in0, cx in
 }
 
 // fill_res (chest_dl.c:962-986) of one subframe from its per-(rx, port) stats st -> o[4]
-// COHERENT: st written by other workgroups of this launch -- device-coherent loads that skip the CU's cache
-template <bool COHERENT>
-__device__ __forceinline__ float ldst(const float* p)
-{
-  if constexpr (COHERENT) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else {
-    return *p;
-  }
-}
-template <bool COHERENT>
 __device__ void finalize_sf(const float* st, uint32_t np, uint32_t nrx, uint32_t nof_prb, float sz, float nsymb,
                             float* o)
 {
@@ -145,15 +134,15 @@ __device__ void finalize_sf(const float* st, uint32_t np, uint32_t nrx, uint32_t
   for (uint32_t rx = 0; rx < nrx; rx++) {
     float s = 0;
     for (uint32_t p = 0; p < np; p++) {
-      s += ldst<COHERENT>(st + (rx * np + p) * 8);
+      s += st[(rx * np + p) * 8];
     }
     n += s / (float)np;
-    rssi += 4 * ldst<COHERENT>(st + (rx * np) * 8 + 2) / (float)nof_prb / 12.0f;
+    rssi += 4 * st[(rx * np) * 8 + 2] / (float)nof_prb / 12.0f;
   }
   for (uint32_t p = 0; p < np; p++) {
     float s = 0;
     for (uint32_t rx = 0; rx < nrx; rx++) {
-      s += ldst<COHERENT>(st + (rx * np + p) * 8 + 1);
+      s += st[(rx * np + p) * 8 + 1];
     }
     s /= (float)nrx;
     best = s > best ? s : best;
@@ -162,8 +151,7 @@ __device__ void finalize_sf(const float* st, uint32_t np, uint32_t nrx, uint32_t
     if ((uint32_t)idx % np < 2) {
       // chest_estimate_cfo (chest_dl.c:618-641): ns = SRSRAN_CP_NSYMB, ng = SRSRAN_CP_LEN_NORM(1, n) for both CPs
       const float ng = (float)(int)ceilf(144.0f * sz / 2048.0f);
-      cfo            = -atan2f(ldst<COHERENT>(st + idx * 8 + 4), ldst<COHERENT>(st + idx * 8 + 3)) * sz / (nsymb * (sz + ng)) /
-                       2 / 3.14159265358979f;
+      cfo            = -atan2f(st[idx * 8 + 4], st[idx * 8 + 3]) * sz / (nsymb * (sz + ng)) / 2 / 3.14159265358979f;
       break;
     }
   }
@@ -434,27 +422,6 @@ __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
     s[5]     = noise_sf ? 1.0f : 0.0f;
   }
   CH_STAMP(6);
-  if (a.res) {  // the subframe's last workgroup reduces its (rx, port) stats: no separate finalize launch
-    __shared__ uint32_t last;
-    __shared__ float    stl[CHEST_STATS_PER_SF];
-    if (tid == 0) {
-      __threadfence();
-      last = atomicAdd(&a.done[b], 1u) == a.nports * a.nrx - 1;
-    }
-    __syncthreads();
-    if (last) {  // uniform: the stats of every (rx, port) loaded in parallel (device-coherent), reduced from LDS
-      __threadfence();
-      const uint32_t nst = a.nports * a.nrx * 8;
-      if (tid < nst) {
-        stl[tid] = __hip_atomic_load(a.stats + b * CHEST_STATS_PER_SF + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      __syncthreads();
-      if (tid == 0) {
-        finalize_sf<false>(stl, a.nports, a.nrx, a.nof_prb, a.symbol_sz, (float)a.nsymb, a.res + 4 * b);
-        __hip_atomic_store(&a.done[b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-  }
   CH_STAMP(7);
 }
 
@@ -490,7 +457,7 @@ __global__ void chest_finalize_kernel(const float* stats, uint32_t np, uint32_t 
   if (b >= nsf) {
     return;
   }
-  finalize_sf<false>(stats + b * CHEST_STATS_PER_SF, np, nrx, nof_prb, sz, nsymb, out + 4 * b);
+  finalize_sf(stats + b * CHEST_STATS_PER_SF, np, nrx, nof_prb, sz, nsymb, out + 4 * b);
 }
 
 // PSS / EMPTY over a batch: one thread walks the subframes in order, carrying each (rx, port)'s kept estimate

@@ -42,7 +42,7 @@ struct EvmItem {
 };
 hipError_t evm_finalize_launch(const EvmItem* d_items, uint32_t nitems, hipStream_t stream);
 #ifndef LLR_SPT_CFG
-#define LLR_SPT_CFG 16  // symbols per thread of the LLR kernel (build parameter)
+#define LLR_SPT_CFG 8  // symbols per thread of the LLR kernel (build parameter; 8: 1248 workgroups for C3, r04p)
 #endif
 constexpr uint32_t LLR_BLOCK_SYMBOLS = 256 * LLR_SPT_CFG;  // symbols of one LLR block (evm_part entries = ceil(n / this))
 // nitems items of one modulation (device array); max_n = largest n

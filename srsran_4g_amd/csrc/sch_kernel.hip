@@ -606,12 +606,11 @@ __global__ __launch_bounds__(256) void stage_copy_kernel(uint4* __restrict__ dst
     zero[i] = 0;
   }
   if (fence) {
-    __syncthreads();  // every load of this workgroup has returned (its value was stored above)
+    __syncthreads();  // every load of this workgroup has returned (its value was stored above); no fence (stage_jobs.h)
     if (threadIdx.x == 0) {
-      __threadfence();
       if (atomicAdd(count, 1u) == gridDim.x - 1) {  // the last workgroup: the whole slot has been read
         __hip_atomic_store(count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(fence, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(fence, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }
   }

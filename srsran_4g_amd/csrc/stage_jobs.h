@@ -43,14 +43,16 @@ __device__ __forceinline__ void run_copy_jobs(const CopyJobs& js)
       c.zero[i] = 0;
     }
   }
-  __syncthreads();  // this workgroup's loads have returned (their values were stored)
+  // this workgroup's loads have returned (their values were stored) once every thread passed the barrier; the
+  // count needs no fence (nothing is published through it: the consumers are later kernels) and the fence word
+  // is a relaxed store to uncached host memory -- a release here would write back the L2 the launch is filling
+  __syncthreads();
   if (threadIdx.x == 0) {
-    __threadfence();
     for (uint32_t j = 0; j < js.n; j++) {
       const CopyJob& c = js.job[j];
       if (c.fence && atomicAdd(c.count, 1u) == gridDim.x - 1) {
         __hip_atomic_store(c.count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(c.fence, c.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(c.fence, c.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }
   }

@@ -567,6 +567,7 @@ int estimate_batch(srsran_chest_dl_t*           q,
                    const srsran_chest_dl_cfg_t* cfg,
                    const uint32_t*              d_sf_idx,
                    const uint8_t*               h_sf,
+                   const srsran_amd::CopyJobs*  jobs,
                    uint32_t                     nsf,
                    const cf_t*                  d_grid,
                    size_t                       grid_sf_stride,
@@ -606,6 +607,9 @@ int estimate_batch(srsran_chest_dl_t*           q,
     a.sf_idx = nullptr;
     a.sf_inl = 1;
     memcpy(a.sf_inline, h_sf, nsf);
+  }
+  if (jobs) {
+    a.jobs = *jobs;
   }
   a.grid_sf_stride = grid_sf_stride;
   a.ce             = (float2*)d_ce;
@@ -664,8 +668,8 @@ extern "C" int srsran_chest_dl_gpu_estimate_batch_cfg(srsran_chest_dl_t*        
   if (!d_sf_idx) {
     return SRSRAN_ERROR_INVALID_INPUTS;
   }
-  return estimate_batch(q, cfg, d_sf_idx, nullptr, nsf, d_grid, grid_sf_stride, d_ce, ce_sf_stride, full_grid, d_res,
-                        stream);
+  return estimate_batch(q, cfg, d_sf_idx, nullptr, nullptr, nsf, d_grid, grid_sf_stride, d_ce, ce_sf_stride, full_grid,
+                        d_res, stream);
 }
 
 // Diagnostic build only (lib/stamps/, tools/chest_stamps.py): chest_kernel workgroups write their phase clock
@@ -679,6 +683,7 @@ namespace srsran_amd {
 int chest_dl_gpu_estimate_batch_inline(srsran_chest_dl_t*           q,
                                        const srsran_chest_dl_cfg_t* cfg,
                                        const uint8_t*               h_sf,
+                                       const CopyJobs*              jobs,
                                        uint32_t                     nsf,
                                        const cf_t*                  d_grid,
                                        size_t                       grid_sf_stride,
@@ -688,7 +693,7 @@ int chest_dl_gpu_estimate_batch_inline(srsran_chest_dl_t*           q,
                                        float*                       d_res,
                                        void*                        stream)
 {
-  return estimate_batch(q, cfg, nullptr, h_sf, nsf, d_grid, grid_sf_stride, d_ce, ce_sf_stride, full_grid, d_res,
+  return estimate_batch(q, cfg, nullptr, h_sf, jobs, nsf, d_grid, grid_sf_stride, d_ce, ce_sf_stride, full_grid, d_res,
                         stream);
 }
 }  // namespace srsran_amd

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "stage_jobs.h"
+
 namespace srsran_amd {
 
 static constexpr int CHEST_MAX_PRB  = 110;
@@ -40,6 +42,9 @@ struct ChestArgs {
   // host buffer for the GPU to read, so no ring slot and no event to free it
   uint32_t        sf_inl;
   uint8_t         sf_inline[CHEST_INLINE_SF];
+  // staging copies of the batch's PDSCH / DL-SCH descriptors fused into the launch (stage_jobs.h; n = 0: none):
+  // their PCIe reads go out with the pilot loads and are stored at the end
+  CopyJobs        jobs;
 };
 
 static constexpr size_t CHEST_PILOTS_PER_SF = 2 * 4 * CHEST_MAX_NREF;  // float2 (both port pairs)

@@ -181,6 +181,9 @@ __device__ unsigned long long* g_chest_stamps = nullptr;
 __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
 {
   CH_STAMP(0);
+  const uint32_t bid = blockIdx.y * gridDim.x + blockIdx.x, nblk = gridDim.x * gridDim.y;
+  CopyRegs       cr;
+  copy_jobs_issue(a.jobs, cr, bid);
   __shared__ cx    pe[4 * CHEST_MAX_NREF];
   __shared__ cx    comb[2 * CHEST_MAX_NREF];
   __shared__ cx    avg[4 * CHEST_MAX_NREF];
@@ -438,6 +441,7 @@ __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
     s[5]     = noise_sf ? 1.0f : 0.0f;
   }
   CH_STAMP(6);
+  copy_jobs_finish(a.jobs, cr, bid, nblk);
   CH_STAMP(7);
 }
 

@@ -480,30 +480,6 @@ __device__ __forceinline__ void llr_block(const float2* __restrict__ sym_p, uint
   }
   const uint32_t nb = min((uint32_t)(LLR_THREADS * SPT), n - base);
   const uint32_t t  = threadIdx.x;
-  // the thread's symbols (and CSI) in groups of LLR_U, each group's loads issued before the first is used: one
-  // HBM round trip a group instead of one a symbol; the first group's loads go out before the Gold phase below,
-  // under the LFSR jumps
-  constexpr int LLR_U = SPT < 8 ? SPT : 8;
-  static_assert(SPT % LLR_U == 0, "whole groups");
-  float2 vv[LLR_U];
-  float  cs[LLR_U], cso[LLR_U];
-  auto   load_group = [&](int r0) {
-#pragma unroll
-    for (int u = 0; u < LLR_U; u++) {
-      const uint32_t i = t + (uint32_t)(r0 + u) * LLR_THREADS;
-      if (i < nb) {
-        vv[u] = sym[base + i];
-        if (csi) {
-          cs[u] = csi[base + i];
-          if (!B8 && (MOD == 1 || MOD == 3) && ((base + i) ^ 1u) < n) {
-            cso[u] = csi[(base + i) ^ 1u];
-          }
-        }
-      }
-    }
-  };
-  load_group(0);
-  const float mx = csi ? *gptr(csi_max) : 1.0f;
   if (scramble) {
     static_assert(64 * GOLD_LANE_SYMBOLS == LLR_THREADS * SPT, "the first wave covers the block");
     if (t < 64 && t * GOLD_LANE_SYMBOLS < nb) {
@@ -521,18 +497,35 @@ __device__ __forceinline__ void llr_block(const float2* __restrict__ sym_p, uint
     }
     __syncthreads();
   }
+  const float mx  = csi ? *gptr(csi_max) : 1.0f;
   const uintptr_t ob  = B8 ? (uintptr_t)llr8 : (uintptr_t)llr;
   const bool      a16 = (ob & 15) == 0;
   const bool      a8  = (ob & 7) == 0;
   const bool      a4  = (ob & 3) == 0;
   const bool      a2  = (ob & 1) == 0;
   float       err = 0.0f;  // EVM: this thread's sum of squared symbol errors
+  // the thread's symbols (and CSI) in groups of LLR_U, each group's loads issued before the first is used: one
+  // HBM round trip a group instead of one a symbol
+  constexpr int LLR_U = SPT < 8 ? SPT : 8;
+  static_assert(SPT % LLR_U == 0, "whole groups");
   for (int r0 = 0; r0 < SPT; r0 += LLR_U) {
     if (t + (uint32_t)r0 * LLR_THREADS >= nb) {
       break;
     }
-    if (r0) {
-      load_group(r0);
+    float2 vv[LLR_U];
+    float  cs[LLR_U], cso[LLR_U];
+#pragma unroll
+    for (int u = 0; u < LLR_U; u++) {
+      const uint32_t i = t + (uint32_t)(r0 + u) * LLR_THREADS;
+      if (i < nb) {
+        vv[u] = sym[base + i];
+        if (csi) {
+          cs[u] = csi[base + i];
+          if (!B8 && (MOD == 1 || MOD == 3) && ((base + i) ^ 1u) < n) {
+            cso[u] = csi[(base + i) ^ 1u];
+          }
+        }
+      }
     }
 #pragma unroll
   for (int u = 0; u < LLR_U; u++) {

@@ -161,14 +161,10 @@ int configure(srsran_ofdm_t* q, uint32_t nof_prb, uint32_t symbol_sz)
   return SRSRAN_SUCCESS;
 }
 
-int run(srsran_ofdm_t* q, const float2* d_in, float2* d_out, uint32_t nrx, uint32_t nsf, float cfo, hipStream_t s,
-        const srsran_amd::CopyJobs* jobs = nullptr)
+int run(srsran_ofdm_t* q, const float2* d_in, float2* d_out, uint32_t nrx, uint32_t nsf, float cfo, hipStream_t s)
 {
   OfdmGpu* g = (OfdmGpu*)q->gpu;
   OfdmArgs a = g->proto;
-  if (jobs) {
-    a.jobs = *jobs;
-  }
   a.in       = d_in;
   a.out      = d_out;
   a.nrx      = nrx;
@@ -189,17 +185,6 @@ int run(srsran_ofdm_t* q, const float2* d_in, float2* d_out, uint32_t nrx, uint3
 }
 
 }  // namespace
-
-namespace srsran_amd {
-int ofdm_rx_gpu_jobs(srsran_ofdm_t* q, const cf_t* d_in, cf_t* d_out, uint32_t nof_rx, uint32_t nof_sf, float cfo,
-                     void* stream, const CopyJobs* jobs)
-{
-  if (!q || !q->gpu || !d_in || !d_out || nof_rx == 0 || nof_sf == 0) {
-    return SRSRAN_ERROR_INVALID_INPUTS;
-  }
-  return run(q, (const float2*)d_in, (float2*)d_out, nof_rx, nof_sf, cfo, (hipStream_t)stream, jobs);
-}
-}  // namespace srsran_amd
 
 extern "C" {
 

@@ -4,8 +4,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "stage_jobs.h"
-
 namespace srsran_amd {
 
 static constexpr int OFDM_MAX_N      = 2048;
@@ -27,7 +25,6 @@ struct OfdmArgs {
   int           nstages;
   int           radix[OFDM_MAX_STAGES];
   uint32_t      ns_magic[OFDM_MAX_STAGES];  // ceil(2^32 / Ns) of every stage (j / Ns by __umulhi)
-  CopyJobs      jobs;                       // receive: descriptor staging copies of the batch fused in (n = 0: none)
 };
 
 // grid: (2 nsymb, nrx, nsf) workgroups

@@ -13,9 +13,6 @@
 // a per-N table computed in double precision on the host.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
-#include <stdlib.h>
-
-#include <algorithm>
 
 #include "ofdm_kernel.h"
 #include "stage_timing.h"
@@ -171,80 +168,46 @@ __device__ __forceinline__ void fft_ip(float2* buf, const OfdmArgs& a)
   }
 }
 
-// Symbol u of the launch (u = (sf * nrx + rx) * 2 nsymb + sym): first sample offset and source row
-struct RxSym {
-  uint32_t sym, rx, sf, off;
-};
-__device__ __forceinline__ RxSym rx_sym(const OfdmArgs& a, uint32_t u)
+__global__ __launch_bounds__(OFDM_THREADS) void ofdm_rx_kernel(OfdmArgs a)
 {
-  const uint32_t ns = a.nsymb, per = 2 * ns;
-  RxSym          r;
-  r.sym                  = u % per;
-  const uint32_t rest    = u / per;
-  r.rx                   = rest % a.nrx;
-  r.sf                   = rest / a.nrx;
-  const uint32_t slot    = r.sym / ns, i = r.sym % ns;
-  const uint32_t slot_sz = ns * a.N + a.cp0 + (ns - 1) * a.cp;
-  r.off                  = slot * slot_sz + a.cp0 + i * (a.N + a.cp);
-  return r;
-}
-
-// all of a thread's sample loads (and CFO factors) of one symbol, issued together
-template <int U>
-__device__ __forceinline__ void rx_load(const OfdmArgs& a, const RxSym& r, float2 (&x)[U], float2 (&c)[U])
-{
-  const float2* src = a.in + ((size_t)r.sf * a.nrx + r.rx) * a.sf_len + r.off;
+  __shared__ float2 buf[OFDM_MAX_N];
+  const uint32_t    sym = blockIdx.x, rx = blockIdx.y, sf = blockIdx.z;
+  const uint32_t    N = a.N, ns = a.nsymb, slot = sym / ns, i = sym % ns;
+  const uint32_t    slot_sz = ns * N + a.cp0 + (ns - 1) * a.cp;
+  const uint32_t    off     = slot * slot_sz + a.cp0 + i * (N + a.cp);
+  const float2*     src     = a.in + ((size_t)sf * a.nrx + rx) * a.sf_len + off;
+  {  // all of a thread's sample loads (and CFO factors) issued before the first use: one HBM round trip
+    constexpr int U = OFDM_MAX_N / OFDM_THREADS;
+    float2        x[U], c[U];
 #pragma unroll
-  for (int u = 0; u < U; u++) {
-    const uint32_t n = threadIdx.x + u * OFDM_THREADS;
-    if (n < a.N) {
-      x[u] = src[n];
-      if (a.cfo_tab) {
-        c[u] = a.cfo_tab[r.off + n];
+    for (int u = 0; u < U; u++) {
+      const uint32_t n = threadIdx.x + u * OFDM_THREADS;
+      if (n < N) {
+        x[u] = src[n];
+        if (a.cfo_tab) {
+          c[u] = a.cfo_tab[off + n];
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint32_t n = threadIdx.x + u * OFDM_THREADS;
+      if (n < N) {
+        buf[n] = a.cfo_tab ? ref_cprod(x[u], c[u]) : x[u];  // srsran_cfo_correct on the subframe buffer
       }
     }
   }
-}
-
-// A workgroup takes symbols blockIdx.x, + gridDim.x, ...: the next symbol's samples are loaded into registers
-// before the current one's FFT, so the HBM reads of one overlap the LDS work of the other (one launch-wide
-// read phase followed by one compute phase left both the memory and the CUs idle half the time)
-__global__ __launch_bounds__(OFDM_THREADS) void ofdm_rx_kernel(OfdmArgs a, uint32_t nsyms)
-{
-  __shared__ float2 buf[OFDM_MAX_N];
-  constexpr int     U = OFDM_MAX_N / OFDM_THREADS;
-  const uint32_t    N = a.N;
-  float2            x[U], c[U];
-  uint32_t          u = blockIdx.x;
-  RxSym             r = rx_sym(a, u);
-  rx_load(a, r, x, c);
-  run_copy_jobs(a.jobs);  // the batch's staging copies (PCIe reads) under the first symbol's HBM reads
-  for (; u < nsyms; u += gridDim.x) {
-#pragma unroll
-    for (int k = 0; k < U; k++) {
-      const uint32_t n = threadIdx.x + k * OFDM_THREADS;
-      if (n < N) {
-        buf[n] = a.cfo_tab ? ref_cprod(x[k], c[k]) : x[k];  // srsran_cfo_correct on the subframe buffer
-      }
+  __syncthreads();
+  fft_ip(buf, a);
+  float2*        dst  = a.out + (((size_t)sf * a.nrx + rx) * 2 * ns + sym) * a.nre;
+  const uint32_t half = a.nre / 2;
+  for (uint32_t k = threadIdx.x; k < a.nre; k += OFDM_THREADS) {
+    const uint32_t bin = k < half ? N - half + k : k - half + 1;
+    float2         v   = buf[bin];
+    if (a.norm != 1.0f) {
+      v = make_float2(v.x * a.norm, v.y * a.norm);
     }
-    __syncthreads();
-    const RxSym cur = r;
-    if (u + gridDim.x < nsyms) {  // the next symbol's loads go out now
-      r = rx_sym(a, u + gridDim.x);
-      rx_load(a, r, x, c);
-    }
-    fft_ip(buf, a);
-    float2*        dst  = a.out + (((size_t)cur.sf * a.nrx + cur.rx) * 2 * a.nsymb + cur.sym) * a.nre;
-    const uint32_t half = a.nre / 2;
-    for (uint32_t k = threadIdx.x; k < a.nre; k += OFDM_THREADS) {
-      const uint32_t bin = k < half ? N - half + k : k - half + 1;
-      float2         v   = buf[bin];
-      if (a.norm != 1.0f) {
-        v = make_float2(v.x * a.norm, v.y * a.norm);
-      }
-      dst[k] = v;
-    }
-    __syncthreads();  // buf is read above before the next symbol overwrites it
+    dst[k] = v;
   }
 }
 
@@ -333,23 +296,7 @@ hipError_t ofdm_rx_launch(const OfdmArgs& a, uint32_t nsf, hipStream_t stream)
   if (a.N > OFDM_MAX_N || a.nstages <= 0 || nsf == 0 || (a.nsymb != 7 && a.nsymb != 6)) {
     return hipErrorInvalidValue;
   }
-  // workgroups: SRSRAN_AMD_OFDM_WG_PER_CU (default 4) per CU of the device, at most one per symbol
-  static const uint32_t per_cu = [] {
-    const char* e = getenv("SRSRAN_AMD_OFDM_WG_PER_CU");
-    const int   v = e ? atoi(e) : 0;
-    return v > 0 ? (uint32_t)v : 4u;
-  }();
-  static int cus = 0;
-  if (cus == 0) {
-    int dev = 0;
-    hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) {
-      cus = 256;
-    }
-  }
-  const uint32_t nsyms = 2 * a.nsymb * a.nrx * nsf;
-  const uint32_t grid  = std::min(nsyms, per_cu * (uint32_t)cus);
-  hipLaunchKernelGGL(ofdm_rx_kernel, dim3(grid), dim3(OFDM_THREADS), 0, stream, a, nsyms);
+  hipLaunchKernelGGL(ofdm_rx_kernel, dim3(2 * a.nsymb, a.nrx, nsf), dim3(OFDM_THREADS), 0, stream, a);
   return hipGetLastError();
 }
 

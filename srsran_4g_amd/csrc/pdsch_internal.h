@@ -29,10 +29,11 @@ int dlsch_gpu_decode_batch_limits(srsran_sch_t* q, uint32_t nof_tb, const srsran
                                   const uint32_t* max_noi, int32_t* d_result, float* d_avg_noi, void* stream);
 
 // srsran_chest_dl_gpu_estimate_batch_cfg with the nsf <= CHEST_INLINE_SF subframe indices h_sf[b] = tti % 10 given on
-// the host and carried in the launch's arguments (chest_api.cpp)
+// the host and carried in the launch's arguments, and the batch's staging copies fused in (chest_api.cpp)
 int chest_dl_gpu_estimate_batch_inline(srsran_chest_dl_t*           q,
                                        const srsran_chest_dl_cfg_t* cfg,
                                        const uint8_t*               h_sf,
+                                       const CopyJobs*              jobs,  // fused staging copies (may be null)
                                        uint32_t                     nsf,
                                        const cf_t*                  d_grid,
                                        size_t                       grid_sf_stride,
@@ -42,9 +43,6 @@ int chest_dl_gpu_estimate_batch_inline(srsran_chest_dl_t*           q,
                                        float*                       d_res,
                                        void*                        stream);
 
-// srsran_ofdm_rx_gpu with the batch's staging copies fused into the launch (ofdm_api.cpp)
-int ofdm_rx_gpu_jobs(srsran_ofdm_t* q, const cf_t* d_in, cf_t* d_out, uint32_t nof_rx, uint32_t nof_sf, float cfo,
-                     void* stream, const CopyJobs* jobs);
 
 }  // namespace srsran_amd
 #endif

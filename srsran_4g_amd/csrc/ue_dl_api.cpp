@@ -341,20 +341,25 @@ int srsran_ue_dl_gpu_decode_batch(srsran_ue_dl_t*              q,
       f.new_data[t]  = sfs[b].new_data[t];
     }
   }
-  // the estimator launch (after the OFDM launch)
-  auto estimate = [&]() -> int {
+  // the estimator launch (after the OFDM launch), with the batch's staging copies fused in when given
+  auto estimate = [&](const srsran_amd::CopyJobs* jobs) -> int {
     if (nof_sf <= (uint32_t)srsran_amd::CHEST_INLINE_SF) {  // the indices travel in the estimator's launch arguments
       uint8_t h_sf[srsran_amd::CHEST_INLINE_SF];
       for (uint32_t b = 0; b < nof_sf; b++) {
         h_sf[b] = (uint8_t)(sfs[b].tti % 10);
       }
-      if (srsran_amd::chest_dl_gpu_estimate_batch_inline(&q->chest, &cfg->chest_cfg, h_sf, nof_sf, (const cf_t*)g->d_grid,
+      if (srsran_amd::chest_dl_gpu_estimate_batch_inline(&q->chest, &cfg->chest_cfg, h_sf, jobs, nof_sf, (const cf_t*)g->d_grid,
                                                          nrx * rows * nre, (cf_t*)g->d_ce,
                                                          np * nrx * nre * (full ? rows : 1), full ? 1 : 0, g->d_res,
                                                          stream)) {
         return SRSRAN_ERROR;
       }
     } else {  // larger batches: a ring slot of pinned memory the estimator reads in place
+      for (uint32_t i = 0; jobs && i < jobs->n; i++) {  // (the copies then go on their own, first)
+        if (srsran_amd::stage_copy_job(jobs->job[i], s) != hipSuccess) {
+          return SRSRAN_ERROR;
+        }
+      }
       const uint32_t slot = g->ring_next;
       g->ring_next        = (slot + 1) % kStageRing;
       if (hipEventSynchronize(g->staged[slot]) != hipSuccess) {
@@ -375,8 +380,8 @@ int srsran_ue_dl_gpu_decode_batch(srsran_ue_dl_t*              q,
     return SRSRAN_SUCCESS;
   };
   // The PDSCH / DL-SCH batch first, with its launches deferred (stage_copy.h): its descriptors depend on the
-  // configuration only, so they are built and staged now, their copies ride in the OFDM launch below (no copy
-  // kernels in the chain) and the predecoder ... TB launches are replayed after the estimator.
+  // configuration only, so they are built and staged now, their copies ride in the estimator's launch below (no
+  // copy kernels in the chain) and the predecoder ... TB launches are replayed after it.
   front.stop();
   // (one DL-SCH group only: TBs with different iteration limits go through several DL-SCH batches, whose staging
   // ring could come round within one deferred call -- such batches launch in line)
@@ -391,7 +396,7 @@ int srsran_ue_dl_gpu_decode_batch(srsran_ue_dl_t*              q,
   if (srsran_amd::stage_side_copy() || !one_limit) {  // in line: OFDM, estimator, then the PDSCH batch
     if (srsran_amd::handoff(g->ho, s) != hipSuccess ||
         srsran_ofdm_rx_gpu(&q->fft[0], d_samples, (cf_t*)g->d_grid, (uint32_t)nrx, nof_sf, cfo, stream) ||
-        estimate() != SRSRAN_SUCCESS) {
+        estimate(nullptr) != SRSRAN_SUCCESS) {
       return SRSRAN_ERROR;
     }
     return srsran_pdsch_gpu_decode_batch(&q->pdsch, nof_sf, ps.data(), d_result, d_avg_noi, stream);
@@ -420,13 +425,11 @@ int srsran_ue_dl_gpu_decode_batch(srsran_ue_dl_t*              q,
     }
   }
   if (srsran_amd::handoff(g->ho, s) != hipSuccess ||
-      srsran_amd::ofdm_rx_gpu_jobs(&q->fft[0], d_samples, (cf_t*)g->d_grid, (uint32_t)nrx, nof_sf, cfo, stream, &js)) {
+      srsran_ofdm_rx_gpu(&q->fft[0], d_samples, (cf_t*)g->d_grid, (uint32_t)nrx, nof_sf, cfo, stream) ||
+      estimate(&js) != SRSRAN_SUCCESS) {
     for (uint32_t i = 0; i < js.n; i++) {
       srsran_amd::stage_copy_job(js.job[i], s);
     }
-    return SRSRAN_ERROR;
-  }
-  if (estimate() != SRSRAN_SUCCESS) {
     return SRSRAN_ERROR;
   }
   front2.stop();

@@ -181,9 +181,6 @@ __device__ unsigned long long* g_chest_stamps = nullptr;
 __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
 {
   CH_STAMP(0);
-  const uint32_t bid = blockIdx.y * gridDim.x + blockIdx.x, nblk = gridDim.x * gridDim.y;
-  CopyRegs       cr;
-  copy_jobs_issue(a.jobs, cr, bid);
   __shared__ cx    pe[4 * CHEST_MAX_NREF];
   __shared__ cx    comb[2 * CHEST_MAX_NREF];
   __shared__ cx    avg[4 * CHEST_MAX_NREF];
@@ -251,6 +248,11 @@ __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
   rsrp = block_sum(rsrp, red) / (float)np;
   rssi = block_sum(rssi, red) / (float)nsym;  // pe[] complete after block_sum's barriers
   CH_STAMP(2);
+  // the fused staging copies' PCIe reads go out here, after the grid loads have been consumed: issued first, they
+  // held up every vmcnt wait behind them (loads retire in order); the LDS phases below cover their latency
+  const uint32_t bid = blockIdx.y * gridDim.x + blockIdx.x, nblk = gridDim.x * gridDim.y;
+  CopyRegs       cr;
+  copy_jobs_issue(a.jobs, cr, bid);
 
   // ---- CFO phase sum (port-0 geometry, chest_dl.c:630-636) ----
   float cre = 0.f, cim = 0.f;

@@ -206,6 +206,75 @@ def test_ue_dl_batch_matches_host_sync(U, SCH, ora):
     ue2.free()
 
 
+def test_ue_dl_batches_on_several_streams(U, SCH, ora):
+    """Batch workers (bench --pdsch-workers): two UE DL objects on two created streams take six batches in turn
+    with no host synchronisation between them, then one object's batches switch streams (the stream hand-over of
+    its staging ring and scratch, stage_copy.h); every batch decodes what was sent, with the same results as
+    a single batch on the default stream.  Also the deferred launches with a mixed iteration limit (in line)."""
+    rng = np.random.default_rng(11)
+    nsf = 4
+    samples, nres, payloads = [], [], []
+    for b in range(nsf):
+        pls, x, nre, _, _, _ = _case(ora, rng, tti=31 + b)
+        samples.append(x)
+        nres.append(nre)
+        payloads.append(pls)
+    d_x = torch.from_numpy(np.stack(samples).view(np.float32)).cuda()
+
+    def make(limits=None):
+        ue = U.UeDl(U.cell(100, 2, 1), 2)
+        sbs = [[SCH.SoftbufferRx(nof_prb=100) for _ in range(2)] for _ in range(nsf)]
+        cfgs = [U.pdsch_cfg(100, nres[b], (TBS, TBS), (6, 6), softbuffers=sbs[b],
+                            max_iterations=(limits[b] if limits else 8)) for b in range(nsf)]
+        d_pl = torch.zeros((nsf, 2, TBS // 8 + 64), dtype=torch.uint8, device="cuda")
+        d_res = torch.full((2 * nsf,), 7, dtype=torch.int32, device="cuda")
+        d_avg = torch.zeros(2 * nsf, dtype=torch.float32, device="cuda")
+        entries = [(31 + b, 1, cfgs[b], [d_pl[b, 0].data_ptr(), d_pl[b, 1].data_ptr()], [1, 1]) for b in range(nsf)]
+        return dict(ue=ue, sbs=sbs, cfgs=cfgs, pl=d_pl, res=d_res, avg=d_avg, entries=entries)
+
+    def run(w, stream):
+        w["pl"].zero_()
+        w["res"].fill_(7)
+        sp = stream.cuda_stream if stream is not None else None
+        assert w["ue"].gpu_decode_batch(w["entries"], d_x.data_ptr(), w["res"].data_ptr(), w["avg"].data_ptr(), 0.0,
+                                        sp) == 2 * nsf
+
+    def check(w):
+        res, pl = w["res"].cpu().numpy(), w["pl"].cpu().numpy()
+        for b in range(nsf):
+            for q in range(2):
+                assert res[2 * b + q] == 0, (b, q)
+                assert np.array_equal(pl[b, q, : TBS // 8], payloads[b][q]), (b, q)
+        return w["avg"].cpu().numpy().copy()
+
+    ref = make()
+    run(ref, None)
+    torch.cuda.synchronize()
+    want_avg = check(ref)
+    ws = [make(), make()]
+    st = [torch.cuda.Stream(), torch.cuda.Stream()]
+    for i in range(6):  # the two workers in turn, nothing synchronised in between (zeroing is stream-ordered too)
+        with torch.cuda.stream(st[i % 2]):
+            run(ws[i % 2], st[i % 2])
+    torch.cuda.synchronize()
+    for w in ws:
+        assert np.array_equal(check(w), want_avg)
+    for i in range(4):  # one object, its batches alternating between the two streams
+        with torch.cuda.stream(st[i % 2]):
+            run(ws[0], st[i % 2])
+        torch.cuda.synchronize()
+        assert np.array_equal(check(ws[0]), want_avg)
+    mixed = make(limits=[8, 6, 8, 6])  # two DL-SCH groups: the in-line launch order
+    run(mixed, None)
+    torch.cuda.synchronize()
+    check(mixed)
+    for w in [ref, mixed] + ws:
+        w["ue"].free()
+        for pair in w["sbs"]:
+            for sb in pair:
+                sb.free()
+
+
 def test_ue_dl_batch_cfo(U, SCH, ora):
     """a CFO on the samples, removed by the batch's fused rotation"""
     rng = np.random.default_rng(9)

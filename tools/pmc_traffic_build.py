@@ -1,7 +1,8 @@
 """Build profiles/pmc_traffic.json (bench.py's roofline.traffic table) from the committed PMC summaries
-of one round (tools/pmc_summary.py output copied to profiles/<round>_pmc_<workload>.json).
+of the given rounds (tools/pmc_summary.py output copied to profiles/<round>_pmc_<workload>.json); per
+workload the first round listed that has a summary wins.
 
-  python tools/pmc_traffic_build.py r03
+  python tools/pmc_traffic_build.py r04,r03
 
 Per workload and kernel: bytes = HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, KiB -> bytes),
 units = the work items of that launch in the profiled run (bench.py scales by its own count),
@@ -44,13 +45,15 @@ def all188_units(cut):
             "tdec16sw8_multi_kernel": 1024 * sum(1 for k in k16 if k <= cut)}
 
 
-def main(rnd, cut=2048):
+def main(rounds, cut=2048):
     out = {"_doc": DOC}
     for wl, units in UNITS.items():
-        src = f"profiles/{rnd}_pmc_{wl}.json"
-        path = os.path.join(ROOT, src)
-        if not os.path.exists(path):
+        found = [f"profiles/{r}_pmc_{wl}.json" for r in rounds.split(",")
+                 if os.path.exists(os.path.join(ROOT, f"profiles/{r}_pmc_{wl}.json"))]
+        if not found:
             continue
+        src = found[0]
+        path = os.path.join(ROOT, src)
         ks = json.load(open(path))["kernels"]
         ent = {}
         for k, c in ks.items():

@@ -1,11 +1,13 @@
 """Summarise tools/pmc.sh passes: per-kernel average counters per dispatch, and HBM traffic per
 launch corrected as MI355X_MICROARCH.md prescribes (FETCH_SIZE x 2 on gfx950, WRITE_SIZE as is;
-both in KiB).  Usage: python tools/pmc_summary.py gpurun_out/pmc_X WORKLOAD out.json"""
+both in KiB).  Per kernel the MEDIAN over its dispatches: a workload that also launches the kernel with other
+settings (the default line's 16-half-iteration launches, warm-up) does not shift the figure.  Usage: python tools/pmc_summary.py gpurun_out/pmc_X WORKLOAD out.json"""
 import collections
 import csv
 import glob
 import json
 import os
+import statistics
 import sys
 
 
@@ -25,7 +27,7 @@ def main(d, workload, out):
     for k, cs in acc.items():
         if "rocclr" in k or "at::native" in k:
             continue
-        avg = {c: sum(v) / len(v) for c, v in cs.items()}
+        avg = {c: statistics.median(v) for c, v in cs.items()}
         if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
             avg["hbm_bytes_per_launch"] = (2 * avg["FETCH_SIZE"] + avg["WRITE_SIZE"]) * 1024
         kernels[k] = {c: round(v, 1) for c, v in avg.items()}

@@ -42,7 +42,9 @@ def all188_units(cut):
     from oracle.oracle import CB_SIZES, nof_subblocks
     k16 = [k for k in CB_SIZES if nof_subblocks(k) == 16]
     return {"tdec16s_multi_kernel": 1024 * sum(1 for k in k16 if k > cut),
-            "tdec16sw8_multi_kernel": 1024 * sum(1 for k in k16 if k <= cut)}
+            "tdec16sw8_multi_kernel": 1024 * sum(1 for k in k16 if k <= cut),
+            "tdec8sw8_multi_kernel": 1024 * sum(1 for k in CB_SIZES if nof_subblocks(k) == 8),
+            "tdec_multi_kernel<1>": 1024 * sum(1 for k in CB_SIZES if nof_subblocks(k) == 0)}  # generic: no sub-blocks
 
 
 def main(rounds, cut=2048):
@@ -61,6 +63,8 @@ def main(rounds, cut=2048):
             k = head.split("::")[-1] + sep + tail  # as bench.py names kernels (no namespace)
             if "hbm_bytes_per_launch" not in c:
                 continue
+            if wl == "all188" and "multi_kernel" not in k:
+                continue  # the default line's other launches (C1, 8-bit, PDSCH / PUSCH): their own workloads
             u = all188_units(cut).get(k, units) if wl == "all188" and len(ks) > 1 else units
             e = {"bytes": int(c["hbm_bytes_per_launch"]), "fetch_raw_kib": c.get("FETCH_SIZE"), "units": u,
                  "source": src}

@@ -1005,6 +1005,12 @@ def run_pdsch(args, torch, dist, world, rank, device, steps=None, warmup=None, c
         if w[0].gpu_decode_batch(w[1], d_x.data_ptr(), w[3].data_ptr(), w[4].data_ptr(), 0.0, w[5].cuda_stream) != 2 * nsf:
             raise RuntimeError("srsran_ue_dl_gpu_decode_batch failed")
 
+    # every worker's first batch (its ring, scratch and descriptor growth) before the timed region, whatever
+    # the warm-up count: a worker first used inside the timed steps would time its allocations
+    for w in workers[1:]:
+        if w[0].gpu_decode_batch(w[1], d_x.data_ptr(), w[3].data_ptr(), w[4].data_ptr(), 0.0, w[5].cuda_stream) != 2 * nsf:
+            raise RuntimeError("srsran_ue_dl_gpu_decode_batch failed")
+    torch.cuda.synchronize()
     elapsed = timed_region(step_workers, steps, warmup, world, dist, torch.cuda.synchronize, device)
     if getattr(args, "pdsch_probe", False):
         pdsch_probe(step, steps, torch, device, prof)
@@ -1786,6 +1792,7 @@ def main():
             "step_spread": pd["step_spread"],
             "host_phases_us_per_call": pd["host_phases_us_per_call"],
             "chain_bytes_per_sf": pd["chain_bytes_per_sf"],
+            "batch_workers": pd["config"]["batch_workers"],
             "chain_roofline_frac": round(pd["config"]["subframes_per_s"] * pd["chain_bytes_per_sf"]
                                          / (world * HBM_PEAK_GBS * 1e9), 5),
             "cpu_baseline": pd.get("cpu_baseline"),
@@ -1806,6 +1813,7 @@ def main():
                 "tb_ok_fraction": pl["config"]["tb_ok_fraction"],
                 "turbo_kernel": pl["roofline"]["kernel"],
                 "turbo_ms_per_step": pl["stages"].get("tdec_kernel", {}).get("ms_per_step"),
+                "batch_workers": pl["config"]["batch_workers"],
             }
         # the uplink counterpart: the eNB PUSCH chain, summary only
         pu = run_pusch(args, torch, dist, world, rank, device, steps=args.pdsch_steps, warmup=2,

@@ -728,7 +728,7 @@ struct StreamPool {
   hipStream_t s[kPoolStreams];
   hipEvent_t  done[kPoolStreams];
   hipEvent_t  fork;
-  MultiDesc   md[4];  // launch entries: 16 (16-step windows), 16 (8-step part), 8, 1 sub-blocks
+  MultiDesc   md[5];  // launch entries: 16 (16-step windows), 16 (8-step part), 8, generic (large K), generic (small K)
 };
 std::mutex               g_pool_mu;
 std::vector<StreamPool*> g_pools;
@@ -779,6 +779,18 @@ StreamPool* get_pool()
   }
   g_pools.push_back(p);
   return p;
+}
+
+// The generic class's quad launch sizes its LDS for its largest K (about 45 KB a workgroup at K = 400: three a
+// CU); its sizes up to this K run as a second launch with LDS for them, more workgroups a CU
+// (SRSRAN_AMD_TDEC_GEN_CUT, read once; 0 = one launch).
+uint32_t gen_cut()
+{
+  static const uint32_t c = [] {
+    const char* e = getenv("SRSRAN_AMD_TDEC_GEN_CUT");
+    return e ? (uint32_t)atoi(e) : 0u;
+  }();
+  return c;
 }
 
 // Rough serial-latency model used only to order launches (longest first).
@@ -845,8 +857,8 @@ int srsran_tdec_gpu_run_multi(uint32_t              nof_groups,
   // tdecs_w8_fused_max_k(): its sizes up to there run the 8-step-window build (fewer registers and
   // little LDS a workgroup: their workgroups can share SIMDs with the large sizes' ones) as their own
   // launch.
-  const int cls_nsb[4] = {16, 16, 8, 1};  // launch entries: 16 (16-step), 16 (8-step part), 8, generic
-  for (int ci = 0; ci < 4 && ret == SRSRAN_SUCCESS; ci++) {
+  const int cls_nsb[5] = {16, 16, 8, 1, 1};  // launch entries: 16 (16-step), 16 (8-step part), 8, generic x 2
+  for (int ci = 0; ci < 5 && ret == SRSRAN_SUCCESS; ci++) {
     std::vector<uint32_t> gs;
     uint32_t              cls_cb = 0;  // blocks of the whole class (decides the kernel)
     for (uint32_t i = 0; i < nof_groups; i++) {
@@ -870,11 +882,17 @@ int srsran_tdec_gpu_run_multi(uint32_t              nof_groups,
                gs.end());
     } else if (ci == 1) {
       gs.clear();  // no 8-step part outside the single-lane class
+    } else if (ci >= 3 && kind == 0 && gen_cut() > 0) {  // generic quad: K above the cut, then the rest
+      const bool small = ci == 4;
+      gs.erase(std::remove_if(gs.begin(), gs.end(), [&](uint32_t g) { return (cfg[g]->proto.K <= gen_cut()) != small; }),
+               gs.end());
+    } else if (ci == 4) {
+      gs.clear();  // one generic launch
     }
     if (gs.empty()) {
       continue;
     }
-    hipStream_t st = p->s[multi_mode() == 2 ? 0 : ci];
+    hipStream_t st = p->s[multi_mode() == 2 ? 0 : std::min(ci, kPoolStreams - 1)];  // both generic parts: one stream
     if (gs.size() == 1) {
       const uint32_t g = gs[0];
       ret = enqueue(cfg[g], d_input[g], in_stride[g], layout_sb, d_output[g], nof_cb[g], 0, n_end, nullptr, st);

@@ -182,13 +182,8 @@ uint32_t srsran_tdec_gpu_get_class_single_threshold(uint32_t nof_subblocks);
 void     srsran_tdec_gpu_set_single_threshold(uint32_t nof_cb);
 uint32_t srsran_tdec_gpu_get_single_threshold(void);
 void     srsran_tdec_gpu_set_generic_single_threshold(uint32_t nof_cb);
-/* Retired in round 4 (kept for ABI compatibility, no effect): the split variant of the single-lane
-   decoders (two helper waves per workgroup) that launches of at most nof_cb blocks ran; it was slower than
-   the plain kernel at every size measured.  The get returns the last value set. */
-void     srsran_tdec_gpu_set_split_threshold(uint32_t nof_cb);
 /* Single-lane launches whose block sizes are all <= k run the build with 8-step windows (fewer
-   registers: two or three waves per SIMD where LDS allows; twice the checkpoints, which live in each
-   lane's private memory).  Process-wide. */
+   registers: two or three waves per SIMD where LDS allows; twice the checkpoints in LDS).  Process-wide. */
 void     srsran_tdec_gpu_set_w8_max_k(uint32_t k);
 uint32_t srsran_tdec_gpu_get_w8_max_k(void);
 /* In a fused multi-size launch (srsran_tdec_gpu_run_multi) of the 16-sub-block single-lane class, the
@@ -196,7 +191,6 @@ uint32_t srsran_tdec_gpu_get_w8_max_k(void);
    (default 2048; 0 = no cut beyond w8_max_k).  Process-wide. */
 void     srsran_tdec_gpu_set_w8_fused_max_k(uint32_t k);
 uint32_t srsran_tdec_gpu_get_w8_fused_max_k(void);
-uint32_t srsran_tdec_gpu_get_split_threshold(void);
 uint32_t srsran_tdec_gpu_get_generic_single_threshold(void);
 
 #ifdef __cplusplus

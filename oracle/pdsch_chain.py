@@ -6,7 +6,8 @@
   srsran_pdsch_decode               pdsch.c:788-958:
       srsran_pdsch_get              pdsch_np.re_table (symbols and estimates)
       apply_power_allocation        pdsch.c:485-521 (rho_b on CRS symbols, rho_a as scaling)
-      srsran_predecoding_type       Oracle.predecode (MMSE with CSI)
+      srsran_predecoding_type       Oracle.predecode (MMSE with CSI), or the reference's compiled
+                                    precoding.c (Reference.predecode, `pre`)
       codeword decode               pdsch.c:661-744: demod_s, sequence_pdsch_apply_s,
                                     csi_correction, srsran_dlsch_decode2 (Oracle.dlsch_decode);
                                     with llr8 the 8-bit forms (demod_b, apply_c, dlsch_decode8)
@@ -52,11 +53,14 @@ def fft_estimate(ora, samples, nof_prb, cell_id, nports, tti, cfo=0.0, N=None, c
 
 def pdsch_decode(ora, grids, ce, noise, nof_prb, cell_id, nports, tti, cfi, rnti, tbs, Qm, rv, scheme="cdd",
                  pmi=0, max_iterations=8, csi_enable=True, power_scale=False, p_a=0.0, p_b=0, prb_mask=None,
-                 states=None, layers=None, cp=0, llr8=False):
+                 states=None, layers=None, cp=0, llr8=False, pre=None):
     """srsran_pdsch_decode for nof_tb = len(tbs) codewords (one layer each; layers=2 with one
     codeword: SM / CDD on two layers, pdsch.c:838-863 + layermap.c:138-147, 236-260).
     llr8: q->llr_is_8bit (pdsch.c:691-737, sch.c:409-428): demod_b, sequence_apply_c, the 8-bit CSI correction
     and decode_tb on the 8-bit decoders.
+    pre: the object whose predecode() runs srsran_predecoding_type -- the oracle's exact-division restatement by
+    default, or oracle.Reference() for the reference's own compiled precoding.c (its SIMD MMSE bodies use
+    _mm256_rcp_ps, precoding.c:1123-1194 / simd.h:321-338, so it differs from the restatement in the last bits).
     Returns per codeword dict(ret, data, avg, llr)."""
     sf_idx = tti % 10
     lstart = cfi + (1 if nof_prb < 10 else 0)
@@ -75,20 +79,21 @@ def pdsch_decode(ora, grids, ce, noise, nof_prb, cell_id, nports, tti, cfi, rnti
             y[:, crs] = y[:, crs] * (np.float32(1) / rho_b)
     h = ce[:, :, idx]
     ntb = len(tbs)
+    pre = pre or ora
     codebook = pmi if ntb == 1 else pmi + 1
     if scheme == "diversity":  # 1 codeword on nports layers, srsran_layerdemap_diversity (layermap.c:138-147)
         L = nports
-        xl, csi = ora.predecode(1, y, h, L, codebook, scaling, noise)
+        xl, csi = pre.predecode(1, y, h, L, codebook, scaling, noise)
         x = np.zeros((1, idx.size), np.complex64)  # 4 ports: a trailing half group stays 0
         for j in range(L):
             x[0, j:L * xl.shape[1]:L] = xl[j]
     elif layers == 2 and ntb == 1:  # predecode 2 layers; demap n/2 layer symbols each; CSI of layer 0
-        xl, csi = ora.predecode(SCHEME[scheme], y, h, 2, codebook, scaling, noise)
+        xl, csi = pre.predecode(SCHEME[scheme], y, h, 2, codebook, scaling, noise)
         n = xl.shape[1]
         x = np.zeros((1, n), np.complex64)
         x[0, 0:2 * (n // 2):2], x[0, 1:2 * (n // 2):2] = xl[0, :n // 2], xl[1, :n // 2]
     else:
-        x, csi = ora.predecode(SCHEME[scheme], y, h, ntb, codebook, scaling, noise)
+        x, csi = pre.predecode(SCHEME[scheme], y, h, ntb, codebook, scaling, noise)
     out = []
     for q in range(ntb):
         seed = ora.pdsch_seed(rnti, q, 2 * sf_idx, cell_id)

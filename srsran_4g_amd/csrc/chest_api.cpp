@@ -560,6 +560,18 @@ extern "C" int srsran_chest_dl_gpu_estimate_batch(srsran_chest_dl_t* q,
                                                 0, d_res, stream);
 }
 
+namespace srsran_amd {
+bool chest_batch_cfg_supported(const srsran_chest_dl_cfg_t* cfg, int full_grid)
+{
+  if (!cfg_supported(cfg, true) || (cfg && cfg->estimator_alg == SRSRAN_ESTIMATOR_ALG_INTERPOLATE && !full_grid)) {
+    fprintf(stderr, "[srsran_chest_dl] batch: configuration not provided (sync correction, automatic filter with "
+                    "PSS / EMPTY noise, or INTERPOLATE without full grids)\n");
+    return false;
+  }
+  return true;
+}
+}  // namespace srsran_amd
+
 namespace {
 // srsran_chest_dl_gpu_estimate_batch_cfg with the subframe indices from d_sf_idx (device) or h_sf (host, carried in
 // the launch arguments, nsf <= CHEST_INLINE_SF)
@@ -581,10 +593,7 @@ int estimate_batch(srsran_chest_dl_t*           q,
       (h_sf && nsf > (uint32_t)srsran_amd::CHEST_INLINE_SF)) {
     return SRSRAN_ERROR_INVALID_INPUTS;
   }
-  if (!cfg_supported(cfg, true) ||
-      (cfg && cfg->estimator_alg == SRSRAN_ESTIMATOR_ALG_INTERPOLATE && !full_grid)) {
-    fprintf(stderr, "[srsran_chest_dl] batch: configuration not provided (sync correction, automatic filter with "
-                    "PSS / EMPTY noise, or INTERPOLATE without full grids)\n");
+  if (!srsran_amd::chest_batch_cfg_supported(cfg, full_grid)) {
     return SRSRAN_ERROR;
   }
   ChestGpu* g = (ChestGpu*)q->gpu;

@@ -55,6 +55,8 @@ struct CfoTab {
   uint32_t   len   = 0;
   bool       valid = false;
   hipEvent_t used  = nullptr;  // the last launch that read d
+  hipEvent_t built = nullptr;  // the launch that wrote d
+  hipStream_t built_on = nullptr;
 };
 
 bool grow(void** p, size_t* cap, size_t need);
@@ -64,9 +66,13 @@ const float2* cfo_table(CfoTab& t, float f, uint32_t len, hipStream_t s)
   uint32_t bits;
   memcpy(&bits, &f, 4);
   if (t.valid && t.bits == bits && t.len == len) {
+    if (t.built_on != s) {  // built on another stream: this launch must not read it before it is written
+      hipStreamWaitEvent(s, t.built, 0);
+    }
     return t.d;
   }
-  if (!t.used && srsran_amd::ring_event_create(&t.used) != hipSuccess) {
+  if ((!t.used && srsran_amd::ring_event_create(&t.used) != hipSuccess) ||
+      (!t.built && srsran_amd::ring_event_create(&t.built) != hipSuccess)) {
     return nullptr;
   }
   if (t.valid) {
@@ -84,6 +90,8 @@ const float2* cfo_table(CfoTab& t, float f, uint32_t len, hipStream_t s)
     t.valid = false;
     return nullptr;
   }
+  hipEventRecord(t.built, s);
+  t.built_on = s;
   t.bits  = bits;
   t.len   = len;
   t.valid = true;
@@ -95,6 +103,9 @@ void cfo_table_free(CfoTab& t)
   hipFree(t.d);
   if (t.used) {
     hipEventDestroy(t.used);
+  }
+  if (t.built) {
+    hipEventDestroy(t.built);
   }
   t = CfoTab();
 }

@@ -42,7 +42,9 @@ int chest_dl_gpu_estimate_batch_inline(srsran_chest_dl_t*           q,
                                        int                          full_grid,
                                        float*                       d_res,
                                        void*                        stream);
-
+// the estimator options the batch estimator takes (the same check it makes, without launching anything; prints
+// the reason when it returns false)
+bool chest_batch_cfg_supported(const srsran_chest_dl_cfg_t* cfg, int full_grid);
 
 }  // namespace srsran_amd
 #endif

@@ -2,6 +2,7 @@
 #include "stage_copy.h"
 
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 
@@ -52,8 +53,11 @@ void stage_fence_free(StageFence& f)
   f = StageFence();
 }
 
-bool stage_fence_wait(const StageFence& f, int slot, uint32_t seq)
+bool stage_fence_wait(StageFence& f, int slot, uint32_t seq)
 {
+  if (f.broken) {
+    return false;
+  }
   uint32_t spins = 0;
   auto     t0    = std::chrono::steady_clock::now();
   while ((int32_t)(f.h[slot] - seq) < 0) {
@@ -61,6 +65,9 @@ bool stage_fence_wait(const StageFence& f, int slot, uint32_t seq)
     __builtin_ia32_pause();
 #endif
     if ((++spins & 0xfff) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
+      fprintf(stderr, "[srsran_amd] staging ring slot %d: fence %u never reached %u; the object is unusable\n", slot,
+              f.h[slot], seq);
+      f.broken = true;
       return false;
     }
   }

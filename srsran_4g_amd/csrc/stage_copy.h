@@ -35,11 +35,14 @@ struct StageFence {
   uint32_t*          d     = nullptr;  // device alias of h
   uint32_t*          count = nullptr;
   uint32_t           seq   = 0;  // last sequence number handed out
+  bool               broken = false;  // a wait timed out: the ring's state is unknown, the object fails from then on
 };
 bool stage_fence_init(StageFence& f, int nslots);
 void stage_fence_free(StageFence& f);
-// blocks until slot's fence word has reached seq (wrap-safe); returns false after ~10 s (a GPU that stopped)
-bool stage_fence_wait(const StageFence& f, int slot, uint32_t seq);
+// blocks until slot's fence word has reached seq (wrap-safe); returns false after ~10 s (a GPU that stopped, or a
+// staging copy that was never launched) and marks the fence broken: every later wait on it fails at once, so the
+// object keeps returning SRSRAN_ERROR instead of spinning 10 s a call on a slot whose sequence it cannot recover
+bool stage_fence_wait(StageFence& f, int slot, uint32_t seq);
 
 // dst (device) <- src_dev (device alias of stage_host_alloc memory), bytes rounded up to 16; the same launch
 // zeroes zero_words 32-bit words at `zero` (optional: a per-batch accumulator, instead of a memset launch) and,

@@ -780,14 +780,6 @@ uint32_t tdec16s_min_cb() { return __atomic_load_n(&g_single_min_cb, __ATOMIC_RE
 // (K = 512: 0.060 vs 0.085 ms at 512, 0.081 vs 0.086 ms at 1024) and the single-lane decoder is ahead on
 // the fused class launch (32 sizes x 256 = 8192 blocks: 0.30 vs 0.53 ms): from 4096 blocks by default.
 static uint32_t g_single8_min_cb = 4096u;
-// srsran_tdec_gpu_set_split_threshold(): launches of at most this many blocks run the single-lane
-// decoders' split variant (tdecs_kernel.hip split_kernel: two helper waves take the other direction's
-// recomputation of phase 2 off the main waves through LDS; one workgroup of 4 waves per CU).  Off by
-// default: bit-exact, 171-198 VGPRs instead of 292-314, but slower than the plain single-lane kernel at
-// every size measured (K = 6144: 0.378 / 0.384 / 0.401 ms against 0.341 / 0.347 / 0.363 ms at 256 / 512 /
-// 1024 blocks; the per-window barrier of four waves and the LDS round trip of 16 states a lane cost more
-// than the recomputation they take off the main waves).
-static uint32_t g_split_max_cb = 0u;
 // srsran_tdec_gpu_set_w8_max_k(): single-lane launches whose block sizes are all <= this K use the build
 // with 8-step windows (tdecs_kernel.hip, TDECS_W = 8: 164-191 VGPRs, two waves a SIMD where LDS allows).
 // Default 800 = the whole 8-sub-block class (408 <= K <= 800), where it wins: the fused class launch of
@@ -807,8 +799,6 @@ void     tdecs_set_w8_fused_max_k(uint32_t k) { __atomic_store_n(&g_w8_fused_max
 uint32_t tdecs_w8_fused_max_k() { return __atomic_load_n(&g_w8_fused_max_k, __ATOMIC_RELAXED); }
 void     tdecs_set_w8_max_k(uint32_t k) { __atomic_store_n(&g_w8_max_k, k, __ATOMIC_RELAXED); }
 uint32_t tdecs_w8_max_k() { return __atomic_load_n(&g_w8_max_k, __ATOMIC_RELAXED); }
-void     tdecs_set_split_max_cb(uint32_t n) { __atomic_store_n(&g_split_max_cb, n, __ATOMIC_RELAXED); }
-uint32_t tdecs_split_max_cb() { return __atomic_load_n(&g_split_max_cb, __ATOMIC_RELAXED); }
 void     tdec8s_set_min_cb(uint32_t n) { __atomic_store_n(&g_single8_min_cb, n, __ATOMIC_RELAXED); }
 uint32_t tdec8s_min_cb() { return __atomic_load_n(&g_single8_min_cb, __ATOMIC_RELAXED); }
 // srsran_tdec_gpu_set_generic_single_threshold(): the generic class (K <= 400) keeps tdec_kernel.hip's

@@ -455,9 +455,7 @@ void srsran_tdec_gpu_set_w8_fused_max_k(uint32_t k) { tdecs_set_w8_fused_max_k(k
 
 uint32_t srsran_tdec_gpu_get_w8_fused_max_k(void) { return tdecs_w8_fused_max_k(); }
 
-void srsran_tdec_gpu_set_split_threshold(uint32_t nof_cb) { tdecs_set_split_max_cb(nof_cb); }
 
-uint32_t srsran_tdec_gpu_get_split_threshold(void) { return tdecs_split_max_cb(); }
 
 void srsran_tdec_gpu_set_class_single_threshold(uint32_t nof_subblocks, uint32_t nof_cb)
 {

@@ -107,8 +107,6 @@ void       tdecs_set_w8_max_k(uint32_t k);
 void       tdecs_set_w8_fused_max_k(uint32_t k);
 uint32_t   tdecs_w8_fused_max_k();
 uint32_t   tdecs_w8_max_k();
-void       tdecs_set_split_max_cb(uint32_t n);
-uint32_t   tdecs_split_max_cb();
 void       tdec8s_set_min_cb(uint32_t n);
 uint32_t   tdec8s_min_cb();
 void       tdec1s_set_min_cb(uint32_t n);

@@ -349,70 +349,6 @@ __device__ __forceinline__ St alpha_llr_window(const Lane& c, St P, int t0, St P
   return P;
 }
 
-// Split phase 2 (the helper-wave variant, HELP): the other direction's states of a window are produced
-// by a helper wave into LDS (STG: [W][64 lanes] states of this wave's lanes) and consumed by the main wave.
-__device__ __forceinline__ void stg_put(uint4* stg, int i, int lane, const St& p)
-{
-  stg[i * 64 + lane] = make_uint4(v2u(p.a), v2u(p.b), v2u(p.c), v2u(p.d));
-}
-__device__ __forceinline__ St stg_get(const uint4* stg, int i, int lane)
-{
-  const uint4 v = stg[i * 64 + lane];
-  return St{u2v(v.x), u2v(v.y), u2v(v.z), u2v(v.w)};
-}
-
-// helper of the alpha side: the first half of alpha_llr_window (beta of the window from its checkpoint)
-template <bool FULL>
-__device__ __forceinline__ void beta_recompute(const Lane& c, int t0, St Pb, const uint32_t* xw, uint4* stg, int lane)
-{
-  const int L  = c.L;
-  const int cc = FULL ? t0 + W : L;
-  const int ic = cc - t0 - 1;
-#pragma unroll
-  for (int i = W - 1; i >= 0; i--) {
-    if (FULL ? i == W - 1 : i == ic) {
-      stg_put(stg, i, lane, Pb);
-      if (cc < L && norm_at(cc)) Pb = norm(Pb);
-    } else if (FULL || i < ic) {
-      Pb = step<true>(Pb, xw[i + 1]);
-      stg_put(stg, i, lane, Pb);
-      if (FULL ? (i & 1) : norm_at(t0 + 1 + i)) Pb = norm(Pb);
-    }
-  }
-}
-
-// main alpha wave: the second half of alpha_llr_window, betas from the helper
-template <bool D2, bool BITS, bool FULL>
-__device__ __forceinline__ St alpha_llr_staged(const Lane& c, St P, int t0, const uint32_t* xw, const uint32_t* aux,
-                                               const uint4* stg, int lane)
-{
-#pragma unroll
-  for (int i = 0; i < W; i++) {
-    if (FULL || t0 + i < c.L) {
-      const Cand  cd = cand(P, bm(xw[i]));
-      const short o  = llr(cd, stg_get(stg, i, lane));
-      P              = next<false>(cd);
-      if ((i & 1) == 0) P = norm(P);
-      emit<D2, BITS>(c, t0 + i, o, aux[i], xw[i]);
-    }
-  }
-  return P;
-}
-
-// helper of the beta side: the alphas entering each position of a window [t0, t0 + W) from its entry
-// checkpoint
-__device__ __forceinline__ void alpha_recompute(int t0, St Pa, const uint32_t* xw, uint4* stg, int lane)
-{
-#pragma unroll
-  for (int i = 0; i < W; i++) {
-    stg_put(stg, i, lane, Pa);
-    if (i < W - 1) {
-      Pa = step<false>(Pa, xw[i]);
-      if (nrm(t0, i)) Pa = norm(Pa);
-    }
-  }
-}
-
 // Phase-1 beta side, window at t0 >= W: backward over t0+W-1 .. t0 (FULL) or L-1 .. t0; Bst = the
 // stored beta at t0, which is the checkpoint of window t0/W - 1 when `store`.
 template <bool FULL>
@@ -492,12 +428,9 @@ struct Pipe {
   }
 };
 
-// One constituent MAP decode of this lane's sub-block; wave 0 = alpha side, wave 1 = beta side; with
-// HELP, wave 2 recomputes the betas of the alpha side's phase-2 windows and wave 3 the alphas of the beta
-// side's, one window ahead of the main waves, through the double-buffered LDS stage STG
-// ([side][buffer][W][64] states).
-template <bool D2, bool BITS, bool HELP>
-__device__ __forceinline__ void map16s(const Lane& cin, int wave, uint4* STG, int st0)
+// One constituent MAP decode of this lane's sub-block; wave 0 = alpha side, wave 1 = beta side.
+template <bool D2, bool BITS>
+__device__ __forceinline__ void map16s(const Lane& cin, int wave, int st0)
 {
   (void)st0;  // first stamp index of this half-iteration (TDECS_STAMPS builds)
   Lane c = cin;
@@ -518,36 +451,6 @@ __device__ __forceinline__ void map16s(const Lane& cin, int wave, uint4* STG, in
   pp.beta = __builtin_amdgcn_readfirstlane(wave) != 0;
   uint32_t xw[W];
   uint32_t aux[W];
-  if constexpr (HELP) {
-    const int lane = (int)(threadIdx.x & 63);
-    const int na   = Ma - h, nb = h, nj = max(na, nb);
-    if (wave >= 2) {
-      // ================= helpers: idle through training and phase 1 =================
-      pp.beta = wave == 3;
-      __syncthreads();
-      const int mtop = Ma - 1;
-      pp.load(c, wave == 2 ? NTR + h : NTR + mtop - (h - 1));
-#pragma unroll 1
-      for (int j = 0; j <= nj; j++) {
-        uint4* stg = STG + ((wave - 2) * 2 + (j & 1)) * (W * 64);
-        if (wave == 2 && j < na) {
-          const int ma = h + j;
-          pp.next(c, NTR + ma, xw, aux);
-          if (ma < Mfull) {
-            beta_recompute<true>(c, ma * W, ck_get(c, ma), xw, stg, lane);
-          } else {
-            beta_recompute<false>(c, ma * W, ck_get(c, ma), xw, stg, lane);
-          }
-        } else if (wave == 3 && j < nb) {
-          const int mb = h - 1 - j;
-          pp.next(c, NTR + mtop - mb, xw, aux);
-          alpha_recompute(mb * W, ck_get(c, mb), xw, stg, lane);
-        }
-        __syncthreads();
-      }
-      return;
-    }
-  }
   pp.start(c);
   if (wave == 0) {
     // ================= alpha side =================
@@ -587,25 +490,6 @@ __device__ __forceinline__ void map16s(const Lane& cin, int wave, uint4* STG, in
     TDECS_STAMP(st0 + 2);
     __syncthreads();
     TDECS_STAMP(st0 + 3);
-    if constexpr (HELP) {  // phase 2 with the betas of window h + j - 1 from the helper
-      const int lane = (int)(threadIdx.x & 63);
-      const int na = Ma - h, nj = max(na, h);
-#pragma unroll 1
-      for (int j = 0; j <= nj; j++) {
-        const int ma = h + j - 1;
-        if (j >= 1 && j - 1 < na) {
-          const uint4* stg = STG + ((j - 1) & 1) * (W * 64);
-          pp.next(c, NTR + ma, xw, aux);
-          if (ma < Mfull) {
-            P = alpha_llr_staged<D2, BITS, true>(c, P, ma * W, xw, aux, stg, lane);
-          } else {
-            alpha_llr_staged<D2, BITS, false>(c, P, ma * W, xw, aux, stg, lane);
-          }
-        }
-        __syncthreads();
-      }
-      return;
-    }
     // phase 2: windows [h, Ma): beta recomputed from the checkpoint above the window, then alpha + LLR
 #pragma unroll 1
     for (int ma = h; ma < Mfull; ma++) {
@@ -668,29 +552,6 @@ __device__ __forceinline__ void map16s(const Lane& cin, int wave, uint4* STG, in
     TDECS_STAMP(st0 + 2);
     __syncthreads();
     TDECS_STAMP(st0 + 3);
-    if constexpr (HELP) {  // phase 2 with the alphas of window h - j from the helper
-      const int lane = (int)(threadIdx.x & 63);
-      const int nj   = max(Ma - h, h);
-#pragma unroll 1
-      for (int j = 0; j <= nj; j++) {
-        const int mb = h - j;
-        if (j >= 1 && j - 1 < h) {
-          const uint4* stg = STG + (2 + ((j - 1) & 1)) * (W * 64);
-          const int    t0  = mb * W;
-          pp.next(c, NTR + mtop - mb, xw, aux);
-#pragma unroll
-          for (int i = W - 1; i >= 0; i--) {
-            const short o = llr(cand(stg_get(stg, i, lane), bm(xw[i])), Bst);
-            P             = step<true>(P, xw[i]);
-            Bst           = P;
-            if (nrm(t0, i)) P = norm(P);
-            emit<D2, BITS>(c, t0 + i, o, aux[i], xw[i]);
-          }
-        }
-        __syncthreads();
-      }
-      return;
-    }
     // phase 2: windows [0, h) from the top: alpha recomputed from the entry checkpoint, then
     // beta backwards with the LLR of every position
 #pragma unroll 1
@@ -722,10 +583,10 @@ __device__ __forceinline__ void map16s(const Lane& cin, int wave, uint4* STG, in
 
 }  // namespace
 
-template <bool ES, bool HELP>
+template <bool ES>
 __device__ __forceinline__ void body(const TdecArgs& a, int bid)
 {
-  constexpr int NT = HELP ? 256 : 128;  // threads: 2 main waves (+ 2 helpers)
+  constexpr int NT = 128;  // threads: the alpha and the beta wave
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -772,8 +633,6 @@ __device__ __forceinline__ void body(const TdecArgs& a, int bid)
   c.CK   = reinterpret_cast<uint4*>(base + g.s_dw);
   c.BITS = base + g.s_dw + g.ck_dw;
   uint32_t* RED = c.BITS + g.bits_dw;
-  uint4*    STG = reinterpret_cast<uint4*>(smem + ((CPWG * g.cb_dw + 3) & ~3));  // HELP: [2][2][W][64]
-  const bool main_wave = !HELP || wave < 2;
 
   if constexpr (ES) {
     if (live && done && t2 == 0) {  // skipped block (sch.c:392, 476-480)
@@ -798,26 +657,26 @@ __device__ __forceinline__ void body(const TdecArgs& a, int bid)
     const bool bits = ES ? crc_now : hi + 1 == h_end;
     if (hi & 1) {
       if (bits) {
-        map16s<true, true, HELP>(c, wave, STG, 5 * hi);
+        map16s<true, true>(c, wave, 5 * hi);
       } else {
-        map16s<true, false, HELP>(c, wave, STG, 5 * hi);
+        map16s<true, false>(c, wave, 5 * hi);
       }
     } else {
       if (bits) {
-        map16s<false, true, HELP>(c, wave, STG, 5 * hi);
+        map16s<false, true>(c, wave, 5 * hi);
       } else {
-        map16s<false, false, HELP>(c, wave, STG, 5 * hi);
+        map16s<false, false>(c, wave, 5 * hi);
       }
     }
     __syncthreads();
 
     // ---------------- DL-SCH early stop: CRC of the hard decision (sch.c:426-456) ----------------
     if constexpr (ES) {
-      if (crc_now) {  // (helper waves: the barrier only)
+      if (crc_now) {
         const uint8_t* bytes  = reinterpret_cast<const uint8_t*>(c.BITS);
         const int      nbytes = K / 8;
         const int      bpt    = (nbytes + 2 * NSB - 1) / (2 * NSB);
-        const int      b0     = main_wave ? t2 * bpt : nbytes;
+        const int      b0     = t2 * bpt;
         const int      b1     = min(b0 + bpt, nbytes);
         const bool     crc_a  = a.cbs[cbl].crc_a;
         const uint32_t poly   = crc_a ? LTE_CRC24A : LTE_CRC24B;
@@ -826,17 +685,17 @@ __device__ __forceinline__ void body(const TdecArgs& a, int bid)
         for (int b = b0; b < b1; b++) {
           crc = crc24_byte(crc, bytes[b], poly);
         }
-        uint32_t part = main_wave && b0 < nbytes ? clmul_mod24(crc, (crc_a ? a.xpow_a : a.xpow_b)[nbytes - b1], poly) : 0;
+        uint32_t part = b0 < nbytes ? clmul_mod24(crc, (crc_a ? a.xpow_a : a.xpow_b)[nbytes - b1], poly) : 0;
 #pragma unroll
         for (int off = 1; off < NSB; off <<= 1) {
           part ^= (uint32_t)__shfl_xor((int)part, off, 64);
         }
-        if (s == 0 && main_wave) {
+        if (s == 0) {
           RED[wave] = part;
         }
         __syncthreads();
         const bool ok = (RED[0] ^ RED[1]) == 0;
-        if (ok && !done && live && main_wave) {
+        if (ok && !done && live) {
           const uint32_t slot = a.cbs[cbl].slot;
           uint8_t*       out  = a.out + (size_t)slot * a.out_stride;
           for (int b = t2; b < nbytes; b += 2 * NSB) {
@@ -856,7 +715,7 @@ __device__ __forceinline__ void body(const TdecArgs& a, int bid)
   }
 
   // ---------------- hard decision of the last half-iteration (turbodecoder.c:370-378) ----------------
-  if (live && !done && h_end > 0 && main_wave) {
+  if (live && !done && h_end > 0) {
     const int      cbm   = ES ? (int)a.cbs[cbl].slot : cbl;
     uint8_t*       out   = a.out + (size_t)cbm * (ES ? a.out_stride : K / 8);
     const uint8_t* bytes = reinterpret_cast<const uint8_t*>(c.BITS);
@@ -873,14 +732,7 @@ __device__ __forceinline__ void body(const TdecArgs& a, int bid)
 template <bool ES>
 __global__ __launch_bounds__(128, 1) void TDECS_K(kernel)(TdecArgs a)
 {
-  body<ES, false>(a, blockIdx.x);
-}
-
-// Small launches (at most one workgroup per CU): phase 2 split over two helper waves
-template <bool ES>
-__global__ __launch_bounds__(256, 1) void TDECS_K(split_kernel)(TdecArgs a)
-{
-  body<ES, true>(a, blockIdx.x);
+  body<ES>(a, blockIdx.x);
 }
 
 __global__ __launch_bounds__(128, 1) void TDECS_K(multi_kernel)(const TdecArgs* __restrict__ groups,
@@ -904,7 +756,7 @@ __global__ __launch_bounds__(128, 1) void TDECS_K(multi_kernel)(const TdecArgs* 
     }
   }
   const TdecArgs a = groups[lo];
-  body<false, false>(a, (int)(b - first[lo]));
+  body<false>(a, (int)(b - first[lo]));
 }
 
 size_t lds_bytes(const TdecArgs& a)
@@ -920,16 +772,6 @@ hipError_t launch(const TdecArgs& a, hipStream_t stream)
   StageScope timing_scope(ST_TDEC, stream);
   const int    grid = (a.ncb + CPWG - 1) / CPWG;
   const size_t lds  = lds_bytes(a);
-  if (a.ncb <= tdecs_split_max_cb()) {
-    const size_t lds_s = ((lds + 15) & ~(size_t)15) + (size_t)4 * W * 64 * 16;
-    tdec_set_last_kernel(a.cbs ? TDECS_NAME "split_kernel<true>" : TDECS_NAME "split_kernel<false>");
-    if (a.cbs) {
-      hipLaunchKernelGGL((TDECS_K(split_kernel)<true>), dim3(grid), dim3(256), lds_s, stream, a);
-    } else {
-      hipLaunchKernelGGL((TDECS_K(split_kernel)<false>), dim3(grid), dim3(256), lds_s, stream, a);
-    }
-    return hipGetLastError();
-  }
   tdec_set_last_kernel(a.cbs ? TDECS_NAME "kernel<true>" : TDECS_NAME "kernel<false>");
   if (a.cbs) {
     hipLaunchKernelGGL((TDECS_K(kernel)<true>), dim3(grid), dim3(128), lds, stream, a);

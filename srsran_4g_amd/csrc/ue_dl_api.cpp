@@ -320,6 +320,9 @@ int srsran_ue_dl_gpu_decode_batch(srsran_ue_dl_t*              q,
   UeDlGpu*    g    = (UeDlGpu*)q->gpu;
   hipStream_t s    = (hipStream_t)stream;
   const bool  full = cfg->chest_cfg.estimator_alg == SRSRAN_ESTIMATOR_ALG_INTERPOLATE;  // every symbol its own row
+  if (!srsran_amd::chest_batch_cfg_supported(&cfg->chest_cfg, full)) {  // before any batch is staged
+    return SRSRAN_ERROR;
+  }
   if (!grow(q, g, nof_sf, full)) {
     return SRSRAN_ERROR;
   }
@@ -417,17 +420,18 @@ int srsran_ue_dl_gpu_decode_batch(srsran_ue_dl_t*              q,
   }
   srsran_amd::HostScope front2(srsran_amd::HP_FRONT);
   srsran_amd::CopyJobs js{};
+  bool                 copies_ok = true;
   for (size_t i = 0; i < rec.jobs.size(); i++) {
     if (i < (size_t)srsran_amd::kMaxFusedJobs) {
       js.job[js.n++] = rec.jobs[i];
-    } else if (srsran_amd::stage_copy_job(rec.jobs[i], s) != hipSuccess) {  // beyond the fused ones: on their own
-      return SRSRAN_ERROR;
+    } else {  // beyond the fused ones: on their own (every one, even after a failure: their fences must come)
+      copies_ok = srsran_amd::stage_copy_job(rec.jobs[i], s) == hipSuccess && copies_ok;
     }
   }
-  if (srsran_amd::handoff(g->ho, s) != hipSuccess ||
+  if (!copies_ok || srsran_amd::handoff(g->ho, s) != hipSuccess ||
       srsran_ofdm_rx_gpu(&q->fft[0], d_samples, (cf_t*)g->d_grid, (uint32_t)nrx, nof_sf, cfo, stream) ||
       estimate(&js) != SRSRAN_SUCCESS) {
-    for (uint32_t i = 0; i < js.n; i++) {
+    for (uint32_t i = 0; i < js.n; i++) {  // the fused ones did not run: their fences must come as well
       srsran_amd::stage_copy_job(js.job[i], s);
     }
     return SRSRAN_ERROR;

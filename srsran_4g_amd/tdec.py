@@ -98,12 +98,10 @@ def load_library():
         "srsran_tdec_gpu_set_class_single_threshold": ([u32, u32], None),
         "srsran_tdec_gpu_get_class_single_threshold": ([u32], u32),
         "srsran_tdec_gpu_set_generic_single_threshold": ([u32], None),
-        "srsran_tdec_gpu_set_split_threshold": ([u32], None),
         "srsran_tdec_gpu_set_w8_max_k": ([u32], None),
         "srsran_tdec_gpu_get_w8_max_k": ([], u32),
         "srsran_tdec_gpu_set_w8_fused_max_k": ([u32], None),
         "srsran_tdec_gpu_get_w8_fused_max_k": ([], u32),
-        "srsran_tdec_gpu_get_split_threshold": ([], u32),
         "srsran_tdec_gpu_get_generic_single_threshold": ([], u32),
     }
     for name, (args, res) in sig.items():
@@ -134,20 +132,6 @@ class pair_threshold:
 
     def __exit__(self, *exc):
         load_library().srsran_tdec_gpu_set_pair_threshold(self.old)
-
-
-class split_threshold(pair_threshold):
-    """blocks per launch up to which the single-lane decoders run their split (helper-wave) variant
-    (srsran_tdec_gpu_set_split_threshold)"""
-
-    def __enter__(self):
-        lib = load_library()
-        self.old = lib.srsran_tdec_gpu_get_split_threshold()
-        lib.srsran_tdec_gpu_set_split_threshold(self.n)
-        return self
-
-    def __exit__(self, *exc):
-        load_library().srsran_tdec_gpu_set_split_threshold(self.old)
 
 
 class w8_max_k(pair_threshold):

@@ -2,6 +2,9 @@
 is absent and no reference test holds its results): it is checked against numpy's
 double-precision FFT with srsRAN's symbol timing / subcarrier mapping (oracle/ofdm_np.py) and
 by TX -> RX round trips, at float32 tolerance."""
+import json
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -9,6 +12,22 @@ import torch
 import ofdm_np
 
 pytestmark = pytest.mark.gpu
+
+# north_star: soft values within 1e-4.  The FFT has no pinned reference output, so its error is taken against
+# numpy's double-precision transform, relative to the largest bin; the measured figures are written to
+# $SRSRAN_AMD_FFT_STATS.
+FFT_TOL = 1e-4
+FFT_STATS = {}
+
+
+def _fft_check(key, got, exp):
+    err = float(np.abs(got - exp).max() / np.abs(exp).max())
+    FFT_STATS[key] = err
+    out = os.environ.get("SRSRAN_AMD_FFT_STATS")
+    if out:
+        with open(out, "w") as f:
+            json.dump(FFT_STATS, f, indent=1)
+    assert err <= FFT_TOL, (key, err)
 
 
 @pytest.fixture(scope="module")
@@ -35,7 +54,7 @@ def test_ofdm_rx_matches_numpy(U, nof_prb):
     x = (rng.standard_normal(ofdm_np.sf_len(N)) + 1j * rng.standard_normal(ofdm_np.sf_len(N))).astype(np.complex64)
     got = rx.rx(x)
     exp = ofdm_np.ofdm_rx(x, N, nre)
-    assert np.abs(got - exp).max() < 2e-5 * np.abs(exp).max() * np.log2(N)
+    _fft_check(f"N{N}", got, exp)
     # round trip of a QAM grid
     g = (rng.choice([-3, -1, 1, 3], 14 * nre) + 1j * rng.choice([-3, -1, 1, 3], 14 * nre)).astype(np.complex64)
     back = rx.rx(ofdm_np.ofdm_tx(g, N, nre).astype(np.complex64))
@@ -48,7 +67,7 @@ def test_ofdm_normalize(U):
     rx = U.OfdmRx(100, normalize=True)
     x = (rng.standard_normal(30720) + 1j * rng.standard_normal(30720)).astype(np.complex64)
     exp = ofdm_np.ofdm_rx(x, 2048, 1200, normalize=True)
-    assert np.abs(rx.rx(x) - exp).max() < 1e-5 * np.abs(exp).max() * 11
+    _fft_check("N2048_normalize", rx.rx(x), exp)
     rx.free()
 
 
@@ -100,7 +119,44 @@ def test_ofdm_gpu_batch_with_cfo(U, ref_cfo, f):
     assert np.abs(got - grids).max() < 2e-3  # the reference's phasor drift, up to ~1e-3 by the end of a subframe
     want = np.stack([np.stack([ofdm_np.ofdm_rx(ref_cfo(x[s, r], f), 2048, nre) for r in range(nrx)])
                      for s in range(nsf)])
-    assert np.abs(got - want).max() < 2e-5 * np.abs(want).max() * 11
+    _fft_check(f"N2048_batch_cfo{f:g}", got, want)
+    rx.free()
+
+
+def test_ofdm_gpu_cfo_table_two_streams(U, ref_cfo):
+    """The cached CFO phasor table of one OFDM object used from two streams (advisor round 4): the table for
+    f2 is rebuilt on stream A behind a long-running kernel; a call on stream B with the same f2 finds it in the
+    cache and must wait for that rebuild instead of reading f1's table."""
+    import ctypes
+    rng = np.random.default_rng(4)
+    rx = U.OfdmRx(100)
+    nsf, nrx, nre = 2, 2, 1200
+    x = (rng.standard_normal((nsf, nrx, 30720)) + 1j * rng.standard_normal((nsf, nrx, 30720))).astype(np.complex64)
+    d_in = torch.from_numpy(x.view(np.float32).reshape(-1)).cuda()
+    outs = [torch.zeros(nsf * nrx * 14 * nre * 2, dtype=torch.float32, device="cuda") for _ in range(2)]
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    f1, f2 = 1.1e-4, -2.7e-4
+    busy = torch.randn(4096, 4096, device="cuda")
+    for rep in range(3):
+        lib = U.lib()
+        assert lib.srsran_ofdm_rx_gpu(ctypes.byref(rx.q), d_in.data_ptr(), outs[0].data_ptr(), nrx, nsf,
+                                      ctypes.c_float(f1), ctypes.c_void_p(sa.cuda_stream)) == 0
+        torch.cuda.synchronize()
+        with torch.cuda.stream(sa):
+            for _ in range(8):
+                busy = busy @ busy
+                busy = busy / busy.abs().max()
+        assert lib.srsran_ofdm_rx_gpu(ctypes.byref(rx.q), d_in.data_ptr(), outs[0].data_ptr(), nrx, nsf,
+                                      ctypes.c_float(f2), ctypes.c_void_p(sa.cuda_stream)) == 0
+        assert lib.srsran_ofdm_rx_gpu(ctypes.byref(rx.q), d_in.data_ptr(), outs[1].data_ptr(), nrx, nsf,
+                                      ctypes.c_float(f2), ctypes.c_void_p(sb.cuda_stream)) == 0
+        torch.cuda.synchronize()
+        a = outs[0].cpu().numpy().view(np.complex64)
+        b = outs[1].cpu().numpy().view(np.complex64)
+        np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32), err_msg=f"rep {rep}")
+    want = np.stack([np.stack([ofdm_np.ofdm_rx(ref_cfo(x[s, r], f2), 2048, nre) for r in range(nrx)])
+                     for s in range(nsf)]).reshape(-1)
+    _fft_check("N2048_two_streams", b, want)
     rx.free()
 
 
@@ -118,7 +174,7 @@ def test_ofdm_rx_reference_default_rates(U, nof_prb, N):
         assert rx.symbol_sz == N
         x = (rng.standard_normal(ofdm_np.sf_len(N)) + 1j * rng.standard_normal(ofdm_np.sf_len(N))).astype(np.complex64)
         exp = ofdm_np.ofdm_rx(x, N, nre)
-        assert np.abs(rx.rx(x) - exp).max() < 2e-5 * np.abs(exp).max() * np.log2(N)
+        _fft_check(f"N{N}_default_rates", rx.rx(x), exp)
         rx.free()
     finally:
         U.use_standard_symbol_size(True)

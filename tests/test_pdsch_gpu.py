@@ -362,15 +362,41 @@ def test_pdsch_evm_matches_reference(U, SCH, ora, case):
 LLR_STATS = {}
 
 
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            return next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "?")
+    except OSError:
+        return "?"
+
+
+@pytest.mark.parametrize("pred", ["restated", "reference"])
 @pytest.mark.parametrize("N,snr,cfo", [(2048, 30.0, 0.0), (1536, 30.0, 0.0), (2048, 17.0, 0.0), (2048, 20.0, 3e-5)])
-def test_chain_llrs_match_oracle_chain(U, SCH, ora, N, snr, cfo):
+def test_chain_llrs_match_oracle_chain(U, SCH, ora, N, snr, cfo, pred):
     """Soft-output agreement of the whole chain from time samples (north_star: LLRs within 1e-4): every
     TB's descrambled, CSI-corrected int16 LLRs from srsran_ue_dl_gpu_decode_batch (OFDM + CFO, CRS estimate,
-    MMSE, demap, descramble, CSI -- read back by srsran_pdsch_gpu_last_llr) against the oracle chain's
-    (numpy FFT, the reference's srsran_vec_apply_cfo, the chest restatement, the reference's compiled
-    predecoder / demapper / scrambler / CSI correction: demod_soft.c:569-644, pdsch.c:662-762) on the same
-    samples.  The GPU FFT and estimator reductions round in another order (FFT parity unpinned), so a few
-    LLRs sit one LSB apart: >= 99.9 % equal and |delta| <= 1 LSB per TB; the figures go to DESIGN.md s2."""
+    MMSE, demap, descramble, CSI -- read back by srsran_pdsch_gpu_last_llr) against the oracle chain on the same
+    samples: numpy FFT, the reference's srsran_vec_apply_cfo, the chest restatement, then the MMSE predecoder --
+
+      pred = "restated":  the oracle's exact-division restatement of precoding.c (oracle_predecode), which the
+                          GPU predecoder equals bit for bit on the same inputs (test_eq_gpu.py).  The GPU FFT and
+                          estimator reductions round in another order (FFT parity unpinned), so a few LLRs sit
+                          one LSB apart: >= 99.9 % equal and |delta| <= 1 LSB per TB.
+      pred = "reference": the reference's own precoding.c compiled into oracle/_ref (Reference.predecode), run
+                          on this host's CPU.  Its AVX2 MMSE bodies divide by _mm256_rcp_ps (precoding.c:1123-1194,
+                          simd.h:321-338: a 12-bit reciprocal estimate, whose exact bits differ between CPU
+                          vendors), so ~4 % of the LLRs land one LSB away from exact division: >= 95 % equal and
+                          |delta| <= 2 LSB per TB (1 from rcp_ps, 1 from the FFT order), decode results equal.
+
+    then the demapper / scrambler / CSI correction (demod_soft.c:569-644, pdsch.c:662-762, pinned to _ref).  The
+    figures go to DESIGN.md section 2 (written to $SRSRAN_AMD_LLR_STATS)."""
+    pre = None
+    if pred == "reference":
+        from oracle import Reference, ref_available
+        if not ref_available():  # on a HIP box the checker must be there: fail, never skip
+            pytest.fail("oracle/_ref/libsrsref.so missing: the reference predecoder (the checker) was not built")
+        pre = Reference()
+    eq_min, d_max = (0.999, 1) if pred == "restated" else (0.95, 2)
     U.use_standard_symbol_size(N == 2048)
     try:
         rng = np.random.default_rng(int(N + 10 * snr))
@@ -382,7 +408,7 @@ def test_chain_llrs_match_oracle_chain(U, SCH, ora, N, snr, cfo):
             pls, x, nre, _, _, _ = _case(ora, rng, tti=tti, snr_db=snr, N=N, cfo=cfo)
             grids, ce, st = PC.fft_estimate(ora, x, 100, 1, 2, tti, cfo=-cfo, N=N)
             wants.append(PC.pdsch_decode(ora, grids, ce, st["noise"], 100, 1, 2, tti, 1, 0x1234, [TBS, TBS], [6, 6],
-                                         [0, 0]))
+                                         [0, 0], pre=pre))
             sb = [SCH.SoftbufferRx(nof_prb=100) for _ in range(2)]
             cfg = U.pdsch_cfg(100, nre, (TBS, TBS), (6, 6), softbuffers=sb)
             keep += [sb, cfg]
@@ -408,10 +434,11 @@ def test_chain_llrs_match_oracle_chain(U, SCH, ora, N, snr, cfo):
                 tot += n
                 eq += int((d == 0).sum())
                 worst = max(worst, int(d.max()))
-                assert (d == 0).mean() >= 0.999, (b, q, (d == 0).mean())
-                assert d.max() <= 1, (b, q, int(d.max()), int((d > 1).sum()))
+                assert (d == 0).mean() >= eq_min, (b, q, (d == 0).mean())
+                assert d.max() <= d_max, (b, q, int(d.max()), int((d > d_max).sum()))
                 assert (res[2 * b + q] == 0) == (wants[b][q]["ret"] == 0), (b, q)
-        LLR_STATS[f"N{N}_snr{snr:g}_cfo{cfo:g}"] = dict(llrs=tot, equal_frac=eq / tot, max_abs_delta=worst)
+        LLR_STATS[f"{pred}_N{N}_snr{snr:g}_cfo{cfo:g}"] = dict(llrs=tot, equal_frac=eq / tot, max_abs_delta=worst,
+                                                               cpu=_cpu_model())
         out = os.environ.get("SRSRAN_AMD_LLR_STATS")
         if out:
             with open(out, "w") as f:

@@ -1,7 +1,7 @@
 """Turbo-decoder kernel micro-benchmark (developer tool, for timing and rocprofv3 --pmc passes): N identical
 launches of one 16-sub-block-class decoder on one workload, HIP events on the launch stream.
 
-  python tools/tdec_kernels.py --kernel split|single|pair|quad --workload k6144|all188|class8|class1 [--K k]
+  python tools/tdec_kernels.py --kernel single|pair|quad --workload k6144|all188|class8|class1 [--K k]
                                [--batch 1024] [--launches 5]
 
 k6144: K = 6144 x batch blocks (srsran_tdec_gpu_run_batch); all188: every K >= 816 x batch blocks in one
@@ -24,7 +24,7 @@ from synth import synth as SY  # noqa: E402
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--kernel", choices=["split", "single", "pair", "quad"], default="single")
+    p.add_argument("--kernel", choices=["single", "pair", "quad"], default="single")
     p.add_argument("--workload", choices=["k6144", "all188", "class8", "class1"], default="k6144")
     p.add_argument("--K", type=int, default=0, help="one code block size instead of the workload's")
     p.add_argument("--w8", type=int, default=0, help="srsran_tdec_gpu_set_w8_max_k (8-step-window build up to K)")
@@ -36,9 +36,8 @@ def main():
     if a.lib:
         tdec.LIB_PATH = os.path.abspath(a.lib)
     never = 1 << 30
-    pair_min, single_min = {"split": (0, 0), "single": (0, 0), "pair": (0, never), "quad": (never, never)}[a.kernel]
+    pair_min, single_min = {"single": (0, 0), "pair": (0, never), "quad": (never, never)}[a.kernel]
     lib = tdec.load_library()
-    lib.srsran_tdec_gpu_set_split_threshold(never if a.kernel == "split" else 0)
     lib.srsran_tdec_gpu_set_w8_max_k(a.w8)
     lib.srsran_tdec_gpu_set_pair_threshold(pair_min)
     lib.srsran_tdec_gpu_set_single_threshold(single_min)

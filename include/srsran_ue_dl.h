@@ -57,6 +57,19 @@ typedef struct {
   bool     configured;
 } srsran_tdd_config_t;
 
+/* TDD frame structure (phy_common.h:200-225, 396-427; phy_common.c:92-182): the 7 uplink-downlink and 10
+ * special-subframe configurations of 36.211 Tables 4.2-2 / 4.2-1.  An unconfigured tdd_config makes every
+ * subframe a downlink one, as in the reference. */
+#define SRSRAN_MAX_TDD_SS_CONFIGS (10u)
+#define SRSRAN_MAX_TDD_SF_CONFIGS (7u)
+typedef enum { SRSRAN_TDD_SF_D = 0, SRSRAN_TDD_SF_U = 1, SRSRAN_TDD_SF_S = 2 } srsran_tdd_sf_t;
+srsran_tdd_sf_t srsran_sfidx_tdd_type(srsran_tdd_config_t tdd_config, uint32_t sf_idx);              /* phy_common.c:111-118 */
+uint32_t        srsran_sfidx_tdd_nof_up(srsran_tdd_config_t tdd_config);                           /* phy_common.c:169-176 */
+uint32_t        srsran_sfidx_tdd_nof_gp(srsran_tdd_config_t tdd_config);                           /* phy_common.c:160-167 */
+uint32_t        srsran_sfidx_tdd_nof_dw(srsran_tdd_config_t tdd_config);                           /* phy_common.c:151-158 */
+uint32_t        srsran_tdd_nof_harq(srsran_tdd_config_t tdd_config);                               /* phy_common.c:178-182 */
+uint32_t        srsran_sfidx_tdd_nof_dw_slot(srsran_tdd_config_t tdd_config, uint32_t slot, srsran_cp_t cp); /* :120-136 */
+
 typedef struct {
   srsran_tdd_config_t tdd_config;
   uint32_t            tti;
@@ -171,6 +184,11 @@ int srsran_chest_dl_gpu_estimate_batch_cfg(srsran_chest_dl_t*           q,
                                            int                          full_grid,
                                            float*                       d_res,
                                            void*                        stream);
+
+/* added: the TDD frame configuration the batch estimators assume (sf->tdd_config of srsran_chest_dl_estimate_cfg):
+ * special subframes of a TDD cell have fewer CRS symbols in their DwPTS (refsignal_dl.c:169-226).  Ignored for FDD
+ * cells.  srsran_ue_dl_gpu_decode_batch sets it from its subframes. */
+int srsran_chest_dl_gpu_set_tdd_config(srsran_chest_dl_t* q, srsran_tdd_config_t tdd_config);
 
 /* added: device-resident estimate.  d_grid: nof_rx_antennas grids of 14 * 12 * nof_prb cf_t,
  * back to back; d_ce: [port][rx] rows of 12 * nof_prb (full_grid = 0: the AVERAGE estimate is
@@ -400,6 +418,8 @@ typedef struct {
   srsran_pdsch_cfg_t* pdsch_cfg;
   uint8_t*            d_payload[SRSRAN_MAX_CODEWORDS];
   uint32_t            new_data[SRSRAN_MAX_CODEWORDS];
+  srsran_tdd_config_t tdd_config;  /* sf->tdd_config of the reference's calls (TDD cells; the same for every
+                                      subframe of a batch); zero = unconfigured (every subframe downlink) */
 } srsran_ue_dl_gpu_sf_t;
 
 /* added: OFDM demodulation (with CFO correction by `cfo`, as srsran_cfo_correct(.., cfo)),

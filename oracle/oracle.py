@@ -213,21 +213,23 @@ class Oracle(_Lib, _PhyMixin):
         n = g(f.ctypes.data, order, std)
         return f[:n]
 
-    def chest_dl(self, grids, nof_prb, cell_id, nports, sf_idx, symbol_sz, cp=0):
+    def chest_dl(self, grids, nof_prb, cell_id, nports, sf_idx, symbol_sz, cp=0, nsym=(4, 2)):
         """CRS channel estimate (srsUE defaults). grids: (nrx, 2*nsymb*12*nof_prb), nsymb = 7 (cp 0) or
-        6 (cp 1, extended) -> (ce (nports, nrx, n), stats)."""
+        6 (cp 1, extended); nsym = CRS symbols of ports 0-1 / 2-3 (fewer in a TDD special subframe, crs_nsym)
+        -> (ce (nports, nrx, n), stats)."""
         grids = np.ascontiguousarray(grids, np.complex64)
         nrx, n = grids.shape
         assert n == (12 if cp else 14) * 12 * nof_prb
         ce = np.zeros((nports, nrx, n), np.complex64)
         out = np.zeros(4, np.float32)
-        f = self.lib.oracle_chest_dl_cp
-        f.argtypes = [ctypes.c_void_p] + [ctypes.c_uint32] * 7 + [ctypes.c_void_p, ctypes.c_void_p]
-        f(grids.ctypes.data, nof_prb, cell_id, nports, nrx, sf_idx, symbol_sz, cp, ce.ctypes.data, out.ctypes.data)
+        f = self.lib.oracle_chest_dl_tdd
+        f.argtypes = [ctypes.c_void_p] + [ctypes.c_uint32] * 9 + [ctypes.c_void_p, ctypes.c_void_p]
+        f(grids.ctypes.data, nof_prb, cell_id, nports, nrx, sf_idx, symbol_sz, cp, nsym[0], nsym[1], ce.ctypes.data,
+          out.ctypes.data)
         return ce, dict(noise=float(out[0]), rsrp=float(out[1]), rssi=float(out[2]), cfo=float(out[3]))
 
     def chest_dl_ext(self, grids, nof_prb, cell_id, nports, sf_idx, symbol_sz, cp=0, estimator=0, noise_alg=0,
-                     filt_order=4, filt_std=1.0, sync=False, noise_state=None):
+                     filt_order=4, filt_std=1.0, sync=False, noise_state=None, nsym=(4, 2)):
         """chest_dl.c with the options beyond srsUE's defaults (oracle_chest_dl_ext): estimator 0 AVERAGE /
         1 INTERPOLATE, noise_alg 0 REFS / 1 PSS / 2 EMPTY, filt_order 0 = automatic, sync = correct_sync_error.
         -> (ce (nports, nrx, n), stats dict, corrected grids, noise_state (4, 4) after the call)"""
@@ -239,11 +241,12 @@ class Oracle(_Lib, _PhyMixin):
         pss = np.zeros(62, np.complex64)
         self.lib.oracle_pss_generate.argtypes = [ctypes.c_uint32, ctypes.c_void_p]
         self.lib.oracle_pss_generate(cell_id % 3, pss.ctypes.data)
-        f = self.lib.oracle_chest_dl_ext
+        f = self.lib.oracle_chest_dl_ext_tdd
         f.argtypes = [ctypes.c_void_p] + [ctypes.c_uint32] * 10 + [ctypes.c_float, ctypes.c_uint32] + \
-            [ctypes.c_void_p] * 4
+            [ctypes.c_void_p] * 2 + [ctypes.c_uint32] * 2 + [ctypes.c_void_p] * 2
         f(grids.ctypes.data, nof_prb, cell_id, nports, nrx, sf_idx, symbol_sz, cp, estimator, noise_alg, filt_order,
-          filt_std, 1 if sync else 0, pss.ctypes.data, ns.ctypes.data, ce.ctypes.data, out.ctypes.data)
+          filt_std, 1 if sync else 0, pss.ctypes.data, ns.ctypes.data, nsym[0], nsym[1], ce.ctypes.data,
+          out.ctypes.data)
         st = dict(noise=float(out[0]), rsrp=float(out[1]), rssi=float(out[2]), cfo=float(out[3]),
                   sync_error=float(out[4]))
         return ce, st, grids, ns
@@ -586,6 +589,18 @@ class Reference(_Lib, _PhyMixin):
         if f(_ptr(coded, _u8p), K, _ptr(out, _u8p), E, rv):
             raise ValueError(K)
         return out
+
+
+def crs_nsym(nof_dw, cp=0):
+    """srsran_refsignal_cs_nof_symbols (refsignal_dl.c:169-226) in a TDD special subframe with nof_dw DwPTS
+    symbols: (ports 0-1, ports 2-3)"""
+    if nof_dw >= (10 if cp else 12):
+        return (4, 2)
+    if nof_dw >= (8 if cp else 9):
+        return (3, 2)
+    if nof_dw >= (4 if cp else 5):
+        return (2, 1)
+    return (1, 1)
 
 
 def ref_available():

@@ -36,9 +36,10 @@ def symbol_sz(nof_prb, standard=True):
     raise ValueError(nof_prb)
 
 
-def fft_estimate(ora, samples, nof_prb, cell_id, nports, tti, cfo=0.0, N=None, cp=0):
+def fft_estimate(ora, samples, nof_prb, cell_id, nports, tti, cfo=0.0, N=None, cp=0, tdd=None):
     """-> grids (nrx, 2*nsymb*12*nof_prb) complex64 (nsymb 7, or 6 with cp=1 extended), ce (nports, nrx, n)
-    complex64, stats"""
+    complex64, stats.  tdd = (sf_config, ss_config) of a TDD cell: a special subframe's CRS symbol counts
+    (srsran_refsignal_cs_nof_symbols)."""
     N = N or symbol_sz(nof_prb)
     nre = 12 * nof_prb
     grids = []
@@ -47,17 +48,21 @@ def fft_estimate(ora, samples, nof_prb, cell_id, nports, tti, cfo=0.0, N=None, c
             x = ofdm_np.ref_apply_cfo(x, cfo) if ofdm_np.ref_available() else ofdm_np.cfo(x, cfo)
         grids.append(ofdm_np.ofdm_rx(x, N, nre, ext=cp).astype(np.complex64))
     grids = np.stack(grids)
-    ce, st = ora.chest_dl(grids, nof_prb, cell_id, nports, tti % 10, N, cp=cp)
+    nsym = (4, 2)
+    if tdd and pdsch_np.tdd_type(tdd[0], tti % 10) == "S":
+        import oracle as _o
+        nsym = _o.crs_nsym(pdsch_np.TDD_SS_SYMBOLS[tdd[1]][0], cp)
+    ce, st = ora.chest_dl(grids, nof_prb, cell_id, nports, tti % 10, N, cp=cp, nsym=nsym)
     return grids, ce, st
 
 
 def pdsch_decode(ora, grids, ce, noise, nof_prb, cell_id, nports, tti, cfi, rnti, tbs, Qm, rv, scheme="cdd",
                  pmi=0, max_iterations=8, csi_enable=True, power_scale=False, p_a=0.0, p_b=0, prb_mask=None,
-                 states=None, layers=None, cp=0, llr8=False, pre=None):
+                 states=None, layers=None, cp=0, llr8=False, pre=None, tdd=None):
     """srsran_pdsch_decode for nof_tb = len(tbs) codewords (one layer each; layers=2 with one
     codeword: SM / CDD on two layers, pdsch.c:838-863 + layermap.c:138-147, 236-260).
     llr8: q->llr_is_8bit (pdsch.c:691-737, sch.c:409-428): demod_b, sequence_apply_c, the 8-bit CSI correction
-    and decode_tb on the 8-bit decoders.
+    and decode_tb on the 8-bit decoders.  tdd = (sf_config, ss_config) of a TDD cell.
     pre: the object whose predecode() runs srsran_predecoding_type -- the oracle's exact-division restatement by
     default, or oracle.Reference() for the reference's own compiled precoding.c (its SIMD MMSE bodies use
     _mm256_rcp_ps, precoding.c:1123-1194 / simd.h:321-338, so it differs from the restatement in the last bits).
@@ -65,7 +70,11 @@ def pdsch_decode(ora, grids, ce, noise, nof_prb, cell_id, nports, tti, cfi, rnti
     sf_idx = tti % 10
     lstart = cfi + (1 if nof_prb < 10 else 0)
     mask = np.ones((2, nof_prb), bool) if prb_mask is None else prb_mask
-    tab = pdsch_np.re_table(nof_prb, nports, cell_id, mask, lstart, sf_idx, cp=cp)
+    if tdd:  # TDD: the grant's DwPTS symbols per slot and the TDD PSS / SSS holes (ra_dl.c:432-440, pdsch.c:90-107)
+        tab = pdsch_np.re_table(nof_prb, nports, cell_id, mask, lstart, sf_idx, fdd=False, cp=cp,
+                                nsl=pdsch_np.tdd_nof_symb_slot(tdd[0], tdd[1], sf_idx, cp))
+    else:
+        tab = pdsch_np.re_table(nof_prb, nports, cell_id, mask, lstart, sf_idx, cp=cp)
     idx = np.array([t[0] for t in tab], np.int64)
     crs = np.array([t[1] for t in tab], bool)
     y = grids[:, idx].astype(np.complex64)

@@ -812,9 +812,12 @@ static void interp_linear_offset(const cpx* in, cpx* out, uint32_t len, uint32_t
   }
 }
 
-/* out[0..5]: noise_estimate, rsrp, rssi, cfo, per (rx,port) noise not returned */
-int oracle_chest_dl_cp(const float* grid, uint32_t nof_prb, uint32_t cell_id, uint32_t nports, uint32_t nrx,
-                       uint32_t sf_idx, uint32_t symbol_sz, uint32_t cp, float* ce, float* out)
+/* out[0..5]: noise_estimate, rsrp, rssi, cfo, per (rx,port) noise not returned.
+ * nsym_pp[0] / [1]: CRS symbols of ports 0 / 1 and 2 / 3 in this subframe (srsran_refsignal_cs_nof_symbols,
+ * refsignal_dl.c:169-226): 4 / 2, fewer in the DwPTS of a TDD special subframe. */
+static int chest_dl_impl(const float* grid, uint32_t nof_prb, uint32_t cell_id, uint32_t nports, uint32_t nrx,
+                         uint32_t sf_idx, uint32_t symbol_sz, uint32_t cp, const uint32_t nsym_pp[2], float* ce,
+                         float* out)
 {
   const uint32_t nsymb = cp ? 6 : 7; /* SRSRAN_CP_NSYMB */
   const uint32_t nre = NRE * nof_prb, nsf = 2 * nsymb * nre;
@@ -829,7 +832,7 @@ int oracle_chest_dl_cp(const float* grid, uint32_t nof_prb, uint32_t cell_id, ui
   for (uint32_t rx = 0; rx < nrx; rx++) {
     const cpx* in = G + (size_t)rx * nsf;
     for (uint32_t port = 0; port < nports; port++) {
-      const uint32_t nsym = crs_nof_symbols(port), nref = 2 * nof_prb, np = nsym * nref;
+      const uint32_t nsym = nsym_pp[port < 2 ? 0 : 1], nref = 2 * nof_prb, np = nsym * nref;
       cpx            recv[4 * 220], pe[4 * 220], avg[4 * 220], tmp[4 * 220];
       for (uint32_t l = 0; l < nsym; l++) {
         const uint32_t sym = crs_nsymbol(l, port, nsymb);
@@ -929,6 +932,23 @@ int oracle_chest_dl_cp(const float* grid, uint32_t nof_prb, uint32_t cell_id, ui
   return 0;
 }
 
+int oracle_chest_dl_cp(const float* grid, uint32_t nof_prb, uint32_t cell_id, uint32_t nports, uint32_t nrx,
+                       uint32_t sf_idx, uint32_t symbol_sz, uint32_t cp, float* ce, float* out)
+{
+  const uint32_t nsym_pp[2] = {4, 2};
+  return chest_dl_impl(grid, nof_prb, cell_id, nports, nrx, sf_idx, symbol_sz, cp, nsym_pp, ce, out);
+}
+
+/* a TDD special subframe: nsym01 / nsym23 CRS symbols of ports 0-1 / 2-3 in its DwPTS (the chest_dl.c paths for
+ * 1-3 symbols: noise 345-354 / 363, time average 571-589, frequency interpolation 488-499) */
+int oracle_chest_dl_tdd(const float* grid, uint32_t nof_prb, uint32_t cell_id, uint32_t nports, uint32_t nrx,
+                        uint32_t sf_idx, uint32_t symbol_sz, uint32_t cp, uint32_t nsym01, uint32_t nsym23, float* ce,
+                        float* out)
+{
+  const uint32_t nsym_pp[2] = {nsym01, nsym23};
+  return chest_dl_impl(grid, nof_prb, cell_id, nports, nrx, sf_idx, symbol_sz, cp, nsym_pp, ce, out);
+}
+
 int oracle_chest_dl(const float* grid, uint32_t nof_prb, uint32_t cell_id, uint32_t nports, uint32_t nrx,
                     uint32_t sf_idx, uint32_t symbol_sz, float* ce, float* out)
 {
@@ -1011,9 +1031,25 @@ float oracle_estimate_frequency(const float* xf, uint32_t len)
   return (float)(-atan2f(sum.i, sum.r) * M_1_PI * 0.5f);  /* -cargf(sum) * M_1_PI * 0.5f */
 }
 
+/* nsym01 / nsym23: CRS symbols of ports 0-1 / 2-3 (4 / 2 in normal subframes, fewer in a TDD special subframe's
+ * DwPTS; INTERPOLATE there: 1 symbol -> its row everywhere, 3 (normal CP) -> rows 0, 4, 7 with 8..13 extrapolated,
+ * chest_dl.c:511-531) */
+int oracle_chest_dl_ext_tdd(float* grid, uint32_t nof_prb, uint32_t cell_id, uint32_t nports, uint32_t nrx,
+                            uint32_t sf_idx, uint32_t symbol_sz, uint32_t cp, uint32_t estimator, uint32_t noise_alg,
+                            uint32_t filt_order, float filt_std, uint32_t sync, const float* pss, float* noise_state,
+                            uint32_t nsym01, uint32_t nsym23, float* ce, float* out);
 int oracle_chest_dl_ext(float* grid, uint32_t nof_prb, uint32_t cell_id, uint32_t nports, uint32_t nrx, uint32_t sf_idx,
                         uint32_t symbol_sz, uint32_t cp, uint32_t estimator, uint32_t noise_alg, uint32_t filt_order,
                         float filt_std, uint32_t sync, const float* pss, float* noise_state, float* ce, float* out)
+{
+  return oracle_chest_dl_ext_tdd(grid, nof_prb, cell_id, nports, nrx, sf_idx, symbol_sz, cp, estimator, noise_alg,
+                                 filt_order, filt_std, sync, pss, noise_state, 4, 2, ce, out);
+}
+
+int oracle_chest_dl_ext_tdd(float* grid, uint32_t nof_prb, uint32_t cell_id, uint32_t nports, uint32_t nrx,
+                            uint32_t sf_idx, uint32_t symbol_sz, uint32_t cp, uint32_t estimator, uint32_t noise_alg,
+                            uint32_t filt_order, float filt_std, uint32_t sync, const float* pss, float* noise_state,
+                            uint32_t nsym01, uint32_t nsym23, float* ce, float* out)
 {
   const uint32_t nsymb = cp ? 6 : 7;
   const uint32_t nre = NRE * nof_prb, nsf = 2 * nsymb * nre, nref = 2 * nof_prb;
@@ -1028,7 +1064,7 @@ int oracle_chest_dl_ext(float* grid, uint32_t nof_prb, uint32_t cell_id, uint32_
     if (sync) { /* chest_dl.c:750-804 */
       float pwr_sum = 0, serr = 0;
       for (uint32_t port = 0; port < nports; port++) {
-        const uint32_t nsym = crs_nof_symbols(port), np = nsym * nref;
+        const uint32_t nsym = port < 2 ? nsym01 : nsym23, np = nsym * nref;
         cpx            pe[4 * 220];
         for (uint32_t l = 0; l < nsym; l++) {
           const uint32_t sym = crs_nsymbol(l, port, nsymb);
@@ -1063,7 +1099,7 @@ int oracle_chest_dl_ext(float* grid, uint32_t nof_prb, uint32_t cell_id, uint32_
       }
     }
     for (uint32_t port = 0; port < nports; port++) {
-      const uint32_t nsym = crs_nof_symbols(port), np = nsym * nref;
+      const uint32_t nsym = port < 2 ? nsym01 : nsym23, np = nsym * nref;
       cpx            recv[4 * 220], pe[4 * 220], avg[4 * 220], tmp[4 * 220];
       for (uint32_t l = 0; l < nsym; l++) {
         const uint32_t sym = crs_nsymbol(l, port, nsymb);
@@ -1149,6 +1185,16 @@ int oracle_chest_dl_ext(float* grid, uint32_t nof_prb, uint32_t cell_id, uint32_
         for (uint32_t l = 1; l < 2 * nsymb; l++) {
           memcpy(row + l * nre, row, nre * sizeof(cpx));
         }
+      } else if (nsym == 1) { /* one CRS symbol: interpolated into row 0, copied everywhere (chest_dl.c:488-515) */
+        if (flen) {
+          conv_same(pe, filt, avg, nref, flen);
+        } else {
+          memset(avg, 0, nref * sizeof(cpx));
+        }
+        interp_linear_offset(avg, row, nref, 6, fidx0, 6 - fidx0);
+        for (uint32_t l = 1; l < 2 * nsymb; l++) {
+          memcpy(row + l * nre, row, nre * sizeof(cpx));
+        }
       } else {
         for (uint32_t l = 0; l < nsym; l++) { /* smoothing of every CRS symbol, then interpolation into its row */
           if (flen) {
@@ -1160,7 +1206,11 @@ int oracle_chest_dl_ext(float* grid, uint32_t nof_prb, uint32_t cell_id, uint32_
           interp_linear_offset(avg + l * nref, row + crs_nsymbol(l, port, nsymb) * nre, nref, 6, off, 6 - off);
         }
 #define CES(i) (row + (size_t)(i)*nre)
-        if (!cp) {
+        if (!cp && port < 2 && nsym == 3) { /* chest_dl.c:520-527: the nsymbols != 4 branch */
+          interp_vector(CES(0), CES(4), NULL, CES(1), 4, 3, nre);
+          interp_vector(CES(4), CES(7), NULL, CES(5), 3, 2, nre);
+          interp_vector(CES(4), CES(7), CES(7), CES(8), 3, 6, nre);
+        } else if (!cp) {
           if (port < 2) {
             interp_vector(CES(0), CES(4), NULL, CES(1), 4, 3, nre);
             interp_vector(CES(4), CES(7), NULL, CES(5), 3, 2, nre);

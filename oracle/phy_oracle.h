@@ -21,4 +21,7 @@ int      oracle_chest_dl(const float* grid, uint32_t nof_prb, uint32_t cell_id, 
 int      oracle_chest_dl_cp(const float* grid, uint32_t nof_prb, uint32_t cell_id, uint32_t nports, uint32_t nrx,
                             uint32_t sf_idx, uint32_t symbol_sz, uint32_t cp, float* ce, float* out);
 void     oracle_crs_pilots_cp(uint32_t cell_id, uint32_t nof_prb, uint32_t pp, uint32_t sf, uint32_t cp, float* out);
+int      oracle_chest_dl_tdd(const float* grid, uint32_t nof_prb, uint32_t cell_id, uint32_t nports, uint32_t nrx,
+                             uint32_t sf_idx, uint32_t symbol_sz, uint32_t cp, uint32_t nsym01, uint32_t nsym23,
+                             float* ce, float* out);
 #endif

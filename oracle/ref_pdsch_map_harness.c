@@ -44,10 +44,12 @@ static bool skip_symbol(uint32_t nof_prb, bool fdd, uint32_t nsymb, uint32_t sf_
   return false;
 }
 
-/* srsran_pdsch_cp in the get direction (pdsch.c:136-220) over an index-valued grid.
+/* srsran_pdsch_cp in the get direction (pdsch.c:136-220) over an index-valued grid, with the grant's symbols per
+ * slot nsl[2] (ra_dl.c:428-440) and the frame type's sync-signal holes.
  * prb_mask: [2][nof_prb] bytes.  Returns the number of PDSCH REs; idx[] receives their grid indices. */
-int ref_pdsch_get_indices(uint32_t nof_prb, uint32_t nof_ports, uint32_t cell_id, uint32_t cp, uint32_t lstart_grant,
-                          uint32_t sf_idx, const uint8_t* prb_mask, uint32_t* idx, uint32_t max_len)
+static int get_indices(uint32_t nof_prb, uint32_t nof_ports, uint32_t cell_id, uint32_t cp, uint32_t lstart_grant,
+                       uint32_t sf_idx, bool fdd, const uint32_t nsl[2], const uint8_t* prb_mask, uint32_t* idx,
+                       uint32_t max_len)
 {
   const srsran_cp_t cpt      = cp ? SRSRAN_CP_EXT : SRSRAN_CP_NORM;
   const uint32_t    nsymb    = SRSRAN_CP_NSYMB(cpt);
@@ -65,16 +67,16 @@ int ref_pdsch_get_indices(uint32_t nof_prb, uint32_t nof_ports, uint32_t cell_id
   cf_t* out_ptr = out;
   for (uint32_t s = 0; s < SRSRAN_NOF_SLOTS_PER_SF; s++) {
     const uint32_t lstart = s == 0 ? lstart_grant : 0;
-    for (uint32_t l = lstart; l < nsymb; l++) {
+    for (uint32_t l = lstart; l < nsl[s]; l++) {
       const bool     has_crs = SRSRAN_SYMBOL_HAS_REF(l, cpt, nof_ports);
       const uint32_t crs_off = !has_crs ? 0 : nof_ports == 1 ? (l == 0 ? cell_id % 6 : (cell_id + 3) % 6) : cell_id % 3;
-      const uint32_t lp      = l + s * nsymb;
+      const uint32_t lp      = l + s * nsl[0];
       for (uint32_t n = 0; n < nof_prb; n++) {
         if (!prb_mask[s * nof_prb + n]) {
           continue;
         }
         in_ptr = &grid[(lp * nof_prb + n) * SRSRAN_NRE];
-        if (!skip_symbol(nof_prb, true, nsymb, sf_idx, s, l, n)) {
+        if (!skip_symbol(nof_prb, fdd, nsl[s], sf_idx, s, l, n)) {
           if (has_crs) {
             prb_cp_ref(&in_ptr, &out_ptr, (int)crs_off, (int)nof_refs, (int)nof_refs, false);
           } else {
@@ -104,4 +106,44 @@ int ref_pdsch_get_indices(uint32_t nof_prb, uint32_t nof_ports, uint32_t cell_id
     idx[i] = (uint32_t)crealf(out[i]);
   }
   return n;
+}
+
+int ref_pdsch_get_indices(uint32_t nof_prb, uint32_t nof_ports, uint32_t cell_id, uint32_t cp, uint32_t lstart_grant,
+                          uint32_t sf_idx, const uint8_t* prb_mask, uint32_t* idx, uint32_t max_len)
+{
+  const srsran_cp_t cpt    = cp ? SRSRAN_CP_EXT : SRSRAN_CP_NORM;
+  const uint32_t    nsl[2] = {SRSRAN_CP_NSYMB(cpt), SRSRAN_CP_NSYMB(cpt)};
+  return get_indices(nof_prb, nof_ports, cell_id, cp, lstart_grant, sf_idx, true, nsl, prb_mask, idx, max_len);
+}
+
+/* The same for a TDD cell of uplink-downlink configuration sf_config and special-subframe configuration ss_config:
+ * the grant's symbols per slot of subframe sf_idx as srsran_ra_dl_compute_nof_re sets them (ra_dl.c:432-440), from
+ * the reference's own srsran_sfidx_tdd_type / srsran_sfidx_tdd_nof_dw_slot (phy_common.c, compiled in).  nsl_out
+ * (optional) receives them.  Uplink subframes: -1. */
+int ref_pdsch_get_indices_tdd(uint32_t nof_prb, uint32_t nof_ports, uint32_t cell_id, uint32_t cp,
+                              uint32_t lstart_grant, uint32_t sf_idx, uint32_t sf_config, uint32_t ss_config,
+                              const uint8_t* prb_mask, uint32_t* idx, uint32_t max_len, uint32_t* nsl_out)
+{
+  srsran_tdd_config_t tdd;
+  memset(&tdd, 0, sizeof(tdd));
+  tdd.sf_config    = sf_config;
+  tdd.ss_config    = ss_config;
+  tdd.configured   = true;
+  const srsran_cp_t cpt = cp ? SRSRAN_CP_EXT : SRSRAN_CP_NORM;
+  uint32_t          nsl[2];
+  const srsran_tdd_sf_t t = srsran_sfidx_tdd_type(tdd, sf_idx);
+  if (t == SRSRAN_TDD_SF_U) {
+    return -1;
+  }
+  if (t == SRSRAN_TDD_SF_S) {
+    nsl[0] = srsran_sfidx_tdd_nof_dw_slot(tdd, 0, cpt);
+    nsl[1] = srsran_sfidx_tdd_nof_dw_slot(tdd, 1, cpt);
+  } else {
+    nsl[0] = nsl[1] = SRSRAN_CP_NSYMB(cpt);
+  }
+  if (nsl_out) {
+    nsl_out[0] = nsl[0];
+    nsl_out[1] = nsl[1];
+  }
+  return get_indices(nof_prb, nof_ports, cell_id, cp, lstart_grant, sf_idx, false, nsl, prb_mask, idx, max_len);
 }

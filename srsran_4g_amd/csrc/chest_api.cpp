@@ -59,7 +59,56 @@ struct ChestGpu {
   float*      sync    = nullptr;  // correct_sync_error sums [4 rx][4 port][10]
   float2*     tab     = nullptr;  // sync correction phasor table (12 * max_prb)
   float       sync_err[SRSRAN_MAX_PORTS][SRSRAN_MAX_PORTS] = {};  // q->sync_err (chest_dl.c:776)
+  srsran_tdd_config_t tdd{};  // the batch estimators' TDD frame configuration (srsran_chest_dl_gpu_set_tdd_config)
 };
+
+// srsran_refsignal_cs_nof_symbols (refsignal_dl.c:169-226) of a TDD special subframe: the CRS symbols of ports 0 / 1
+// (port23 = false) or 2 / 3 that fall in its DwPTS
+uint32_t special_crs_nsym(const srsran_tdd_config_t& tdd, srsran_cp_t cp, bool port23)
+{
+  const uint32_t n = srsran_sfidx_tdd_nof_dw(tdd);
+  const bool     norm = cp == SRSRAN_CP_NORM;
+  if (n >= (norm ? 12u : 10u)) {
+    return port23 ? 2 : 4;
+  } else if (n >= (norm ? 9u : 8u)) {
+    return port23 ? 2 : 3;
+  } else if (n >= (norm ? 5u : 4u)) {
+    return port23 ? 1 : 2;
+  }
+  return 1;
+}
+
+// the special subframes of a TDD cell and their CRS symbol counts into the estimator's arguments (FDD cells and an
+// unconfigured TDD configuration: none, as srsran_refsignal_cs_nof_symbols)
+void tdd_args(const srsran_cell_t& cell, const srsran_tdd_config_t& tdd, ChestArgs& a)
+{
+  a.special_mask = 0;
+  a.ss_nsym[0]   = 4;
+  a.ss_nsym[1]   = 2;
+  if (cell.frame_type != SRSRAN_TDD || !tdd.configured) {
+    return;
+  }
+  for (uint32_t i = 0; i < 10; i++) {
+    if (srsran_sfidx_tdd_type(tdd, i) == SRSRAN_TDD_SF_S) {
+      a.special_mask |= 1u << i;
+    }
+  }
+  a.ss_nsym[0] = special_crs_nsym(tdd, cell.cp, false);
+  a.ss_nsym[1] = special_crs_nsym(tdd, cell.cp, true);
+}
+
+// INTERPOLATE in a special subframe whose DwPTS holds 2 CRS symbols of ports 0 / 1 (or 2-3 with extended CP): the
+// reference's time interpolation reads estimate rows of the CRS symbols beyond the DwPTS, which it did not write in
+// this call (chest_dl.c:520-546: left from an earlier subframe), so no result can equal it
+bool tdd_interp_ok(const srsran_cell_t& cell, const srsran_tdd_config_t& tdd, const srsran_chest_dl_cfg_t* cfg)
+{
+  if (!cfg || cfg->estimator_alg != SRSRAN_ESTIMATOR_ALG_INTERPOLATE || cell.frame_type != SRSRAN_TDD ||
+      !tdd.configured) {
+    return true;
+  }
+  const uint32_t n = special_crs_nsym(tdd, cell.cp, false);
+  return cell.cp == SRSRAN_CP_NORM ? n != 2 : (n == 1 || n == 4);
+}
 
 // srsran_pss_generate (pss.c:341-368): the argument in double, cosf / sinf of its float
 void pss_generate(uint32_t N_id_2, float2* sig)
@@ -169,6 +218,53 @@ int srsran_nof_prb(uint32_t symbol_sz)  // phy_common.c:387-430
 }
 
 bool srsran_symbol_sz_isvalid(uint32_t symbol_sz) { return srsran_nof_prb(symbol_sz) > 0; }  // phy_common.c:421-437
+
+// ---------------- TDD frame structure (phy_common.c:92-182; 36.211 Tables 4.2-1 / 4.2-2) ----------------
+srsran_tdd_sf_t srsran_sfidx_tdd_type(srsran_tdd_config_t tdd_config, uint32_t sf_idx)
+{
+  static const char kPattern[SRSRAN_MAX_TDD_SF_CONFIGS][11] = {"DSUUUDSUUU", "DSUUDDSUUD", "DSUDDDSUDD", "DSUUUDDDDD",
+                                                               "DSUUDDDDDD", "DSUDDDDDDD", "DSUUUDSUUD"};
+  if (tdd_config.sf_config < SRSRAN_MAX_TDD_SF_CONFIGS && sf_idx < 10 && tdd_config.configured) {
+    const char c = kPattern[tdd_config.sf_config][sf_idx];
+    return c == 'D' ? SRSRAN_TDD_SF_D : c == 'U' ? SRSRAN_TDD_SF_U : SRSRAN_TDD_SF_S;
+  }
+  return SRSRAN_TDD_SF_D;
+}
+
+// DwPTS / GP / UpPTS symbols of the special subframe configurations
+static const uint8_t kTddSsSymbols[SRSRAN_MAX_TDD_SS_CONFIGS][3] = {{3, 10, 1}, {9, 4, 1},  {10, 3, 1}, {11, 2, 1},
+                                                                    {12, 1, 1}, {3, 9, 2},  {9, 3, 2},  {10, 2, 2},
+                                                                    {11, 1, 1}, {6, 6, 2}};
+
+uint32_t srsran_sfidx_tdd_nof_dw(srsran_tdd_config_t c)
+{
+  return c.ss_config < SRSRAN_MAX_TDD_SS_CONFIGS ? kTddSsSymbols[c.ss_config][0] : 0;
+}
+
+uint32_t srsran_sfidx_tdd_nof_gp(srsran_tdd_config_t c)
+{
+  return c.ss_config < SRSRAN_MAX_TDD_SS_CONFIGS ? kTddSsSymbols[c.ss_config][1] : 0;
+}
+
+uint32_t srsran_sfidx_tdd_nof_up(srsran_tdd_config_t c)
+{
+  return c.ss_config < SRSRAN_MAX_TDD_SS_CONFIGS ? kTddSsSymbols[c.ss_config][2] : 0;
+}
+
+uint32_t srsran_tdd_nof_harq(srsran_tdd_config_t c)
+{
+  static const uint32_t n[SRSRAN_MAX_TDD_SF_CONFIGS] = {7, 4, 2, 3, 2, 1, 6};
+  return c.sf_config < SRSRAN_MAX_TDD_SF_CONFIGS ? n[c.sf_config] : 0;
+}
+
+uint32_t srsran_sfidx_tdd_nof_dw_slot(srsran_tdd_config_t c, uint32_t slot, srsran_cp_t cp)
+{
+  const uint32_t n = srsran_sfidx_tdd_nof_dw(c), ns = SRSRAN_CP_NSYMB(cp);
+  if (n < ns) {
+    return slot == 1 ? 0 : n;
+  }
+  return slot == 1 ? n - ns : ns;
+}
 
 int srsran_chest_dl_init(srsran_chest_dl_t* q, uint32_t max_prb, uint32_t nof_rx_antennas)
 {
@@ -302,10 +398,12 @@ void srsran_chest_dl_res_free(srsran_chest_dl_res_t* q)
 }
 
 static int chest_enqueue(srsran_chest_dl_t* q, uint32_t tti, const float2* d_grid, float2* d_ce, int full,
-                         hipStream_t s, const srsran_chest_dl_cfg_t* cfg = nullptr)
+                         hipStream_t s, const srsran_chest_dl_cfg_t* cfg = nullptr,
+                         const srsran_tdd_config_t* tdd = nullptr)
 {
   ChestGpu* g = (ChestGpu*)q->gpu;
   ChestArgs a{};
+  tdd_args(q->cell, tdd ? *tdd : g->tdd, a);
   a.grid       = d_grid;
   a.pilots     = g->pilots + (tti % 10) * kPilotsPerSf;
   a.ce         = d_ce;
@@ -341,11 +439,14 @@ static int chest_enqueue(srsran_chest_dl_t* q, uint32_t tti, const float2* d_gri
 // phase sums on the device, the reference's scalar arithmetic here, and where the error exceeds 0.05 samples
 // every row of that rx grid rotated on the device by srsran_vec_apply_cfo's phasors (then copied back to the
 // caller's buffer, which the reference corrects in place)
-static int correct_sync_error(srsran_chest_dl_t* q, uint32_t tti, cf_t* input[SRSRAN_MAX_PORTS])
+static int correct_sync_error(srsran_chest_dl_t* q, uint32_t tti, const srsran_tdd_config_t& tdd,
+                              cf_t* input[SRSRAN_MAX_PORTS])
 {
   ChestGpu*      g   = (ChestGpu*)q->gpu;
   const uint32_t nre = 12 * q->cell.nof_prb, rows = 2 * SRSRAN_CP_NSYMB(q->cell.cp), np = q->cell.nof_ports;
   ChestArgs      a{};
+  tdd_args(q->cell, tdd, a);
+  a.sf_index = tti % 10;
   a.grid    = g->grid;
   a.pilots  = g->pilots + (tti % 10) * kPilotsPerSf;
   a.nof_prb = q->cell.nof_prb;
@@ -364,7 +465,7 @@ static int correct_sync_error(srsran_chest_dl_t* q, uint32_t tti, cf_t* input[SR
     float pwr_sum = 0.0f, sync_err = 0.0f;
     for (uint32_t port = 0; port < np; port++) {
       const float*   o    = sums + (rx * 4 + port) * 10;
-      const uint32_t nsym = port < 2 ? 4 : 2, npilots = nsym * 2 * q->cell.nof_prb;
+      const uint32_t nsym = chest_crs_nsym(a, tti % 10, port), npilots = nsym * 2 * q->cell.nof_prb;
       const float    k    = (float)sz / 6.0f;
       float          sum  = 0.0f;
       for (uint32_t l = 0; l < nsym; l++) {  // srsran_vec_estimate_frequency: -cargf(sum) * M_1_PI * 0.5f
@@ -472,6 +573,11 @@ int srsran_chest_dl_estimate_cfg(srsran_chest_dl_t*     q,
                     "above 7 and rsrp_neighbour are not provided\n");
     return SRSRAN_ERROR;
   }
+  if (!tdd_interp_ok(q->cell, sf->tdd_config, cfg)) {
+    fprintf(stderr, "[srsran_chest_dl] INTERPOLATE in TDD special subframes with 2 CRS symbols (3 with extended CP): "
+                    "the reference interpolates towards rows it did not estimate\n");
+    return SRSRAN_ERROR;
+  }
   ChestGpu*      g   = (ChestGpu*)q->gpu;
   const uint32_t nsf = 2 * SRSRAN_CP_NSYMB(q->cell.cp) * 12 * q->cell.nof_prb, nrx = q->nof_rx_antennas,
                  np  = q->cell.nof_ports;
@@ -479,7 +585,7 @@ int srsran_chest_dl_estimate_cfg(srsran_chest_dl_t*     q,
     hipMemcpyAsync(g->grid + rx * nsf, input[rx], nsf * sizeof(cf_t), hipMemcpyHostToDevice, g->stream);
   }
   if (cfg->sync_error_enable) {
-    if (correct_sync_error(q, sf->tti, input)) {
+    if (correct_sync_error(q, sf->tti, sf->tdd_config, input)) {
       return SRSRAN_ERROR;
     }
   } else {
@@ -492,7 +598,7 @@ int srsran_chest_dl_estimate_cfg(srsran_chest_dl_t*     q,
     }
   }
   hipMemcpyAsync(g->noise, kept, sizeof(kept), hipMemcpyHostToDevice, g->stream);
-  if (chest_enqueue(q, sf->tti, g->grid, g->ce, 1, g->stream, cfg)) {
+  if (chest_enqueue(q, sf->tti, g->grid, g->ce, 1, g->stream, cfg, &sf->tdd_config)) {
     return SRSRAN_ERROR;
   }
   for (uint32_t p = 0; p < np; p++) {
@@ -506,7 +612,12 @@ int srsran_chest_dl_estimate_cfg(srsran_chest_dl_t*     q,
   if (hipStreamSynchronize(g->stream) != hipSuccess) {
     return SRSRAN_ERROR;
   }
-  fill_res(q, st, res, cfg->cfo_estimate_enable && ((1u << (sf->tti % 10)) & cfg->cfo_estimate_sf_mask));
+  // chest_estimate_cfo sizes its pilots by the FDD count (chest_dl.c:626): in a special subframe with fewer CRS
+  // symbols it reads pilot estimates of an earlier subframe; q->cfo is kept from the last full subframe instead
+  ChestArgs ta{};
+  tdd_args(q->cell, sf->tdd_config, ta);
+  const bool full_crs = chest_crs_nsym(ta, sf->tti % 10, 0) == 4;
+  fill_res(q, st, res, full_crs && cfg->cfo_estimate_enable && ((1u << (sf->tti % 10)) & cfg->cfo_estimate_sf_mask));
   return SRSRAN_SUCCESS;
 }
 
@@ -519,6 +630,15 @@ int srsran_chest_dl_estimate(srsran_chest_dl_t* q, srsran_dl_sf_cfg_t* sf, cf_t*
 }
 
 }  // extern "C"
+
+extern "C" int srsran_chest_dl_gpu_set_tdd_config(srsran_chest_dl_t* q, srsran_tdd_config_t tdd_config)
+{
+  if (!q || !q->gpu) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  ((ChestGpu*)q->gpu)->tdd = tdd_config;
+  return SRSRAN_SUCCESS;
+}
 
 extern "C" int srsran_chest_dl_gpu_estimate(srsran_chest_dl_t* q,
                                             uint32_t           tti,
@@ -561,8 +681,13 @@ extern "C" int srsran_chest_dl_gpu_estimate_batch(srsran_chest_dl_t* q,
 }
 
 namespace srsran_amd {
-bool chest_batch_cfg_supported(const srsran_chest_dl_cfg_t* cfg, int full_grid)
+bool chest_batch_cfg_supported(const srsran_chest_dl_t* q, const srsran_chest_dl_cfg_t* cfg, int full_grid)
 {
+  if (q && q->gpu && !tdd_interp_ok(q->cell, ((const ChestGpu*)q->gpu)->tdd, cfg)) {
+    fprintf(stderr, "[srsran_chest_dl] batch: INTERPOLATE in TDD special subframes with 2 CRS symbols (3 with extended "
+                    "CP) is not provided\n");
+    return false;
+  }
   if (!cfg_supported(cfg, true) || (cfg && cfg->estimator_alg == SRSRAN_ESTIMATOR_ALG_INTERPOLATE && !full_grid)) {
     fprintf(stderr, "[srsran_chest_dl] batch: configuration not provided (sync correction, automatic filter with "
                     "PSS / EMPTY noise, or INTERPOLATE without full grids)\n");
@@ -593,7 +718,7 @@ int estimate_batch(srsran_chest_dl_t*           q,
       (h_sf && nsf > (uint32_t)srsran_amd::CHEST_INLINE_SF)) {
     return SRSRAN_ERROR_INVALID_INPUTS;
   }
-  if (!srsran_amd::chest_batch_cfg_supported(cfg, full_grid)) {
+  if (!srsran_amd::chest_batch_cfg_supported(q, cfg, full_grid)) {
     return SRSRAN_ERROR;
   }
   ChestGpu* g = (ChestGpu*)q->gpu;
@@ -609,6 +734,7 @@ int estimate_batch(srsran_chest_dl_t*           q,
   }
   hipStream_t s = (hipStream_t)stream;
   ChestArgs   a{};
+  tdd_args(q->cell, g->tdd, a);
   a.grid           = (const float2*)d_grid;
   a.pilots         = g->pilots;
   a.sf_idx         = d_sf_idx;

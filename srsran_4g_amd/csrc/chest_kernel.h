@@ -34,6 +34,10 @@ struct ChestArgs {
   const float*    noise_in;   // [rx][port] (4 x 4) kept noise estimates: the automatic filter's input and the
                               // result of PSS / EMPTY outside subframes 0 / 5 (q->noise_estimate)
   uint32_t        sf_index;   // tti % 10 when sf_idx (below) is null
+  // TDD special subframes (refsignal_dl.c:169-226): bit i of special_mask = subframe index i is special; its DwPTS
+  // holds ss_nsym[0] CRS symbols of ports 0 / 1 and ss_nsym[1] of ports 2 / 3 (every other subframe: 4 / 2)
+  uint32_t        special_mask;
+  uint32_t        ss_nsym[2];
   // ---- batches of subframes (gridDim.y = nof subframes) ----
   const uint32_t* sf_idx;     // [b] subframe index (tti % 10): pilots + sf_idx[b] * CHEST_PILOTS_PER_SF; null = as given
   size_t          grid_sf_stride; // float2 between subframes of `grid`
@@ -46,6 +50,12 @@ struct ChestArgs {
   // their PCIe reads go out with the pilot loads and are stored at the end
   CopyJobs        jobs;
 };
+
+// CRS symbols of `port` in subframe index sfi (srsran_refsignal_cs_nof_symbols)
+__host__ __device__ inline uint32_t chest_crs_nsym(const ChestArgs& a, uint32_t sfi, uint32_t port)
+{
+  return ((a.special_mask >> sfi) & 1u) ? a.ss_nsym[port < 2 ? 0 : 1] : (port < 2 ? 4u : 2u);
+}
 
 static constexpr size_t CHEST_PILOTS_PER_SF = 2 * 4 * CHEST_MAX_NREF;  // float2 (both port pairs)
 static constexpr size_t CHEST_STATS_PER_SF  = 4 * 4 * 8;               // floats of stats per subframe

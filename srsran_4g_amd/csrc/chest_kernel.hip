@@ -188,10 +188,11 @@ __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
 
   const uint32_t port = blockIdx.x / a.nrx, rx = blockIdx.x % a.nrx, b = blockIdx.y;
   const uint32_t tid  = threadIdx.x;
-  const uint32_t nsym = port < 2 ? 4 : 2, nref = 2 * a.nof_prb, np = nsym * nref, nre = 12 * a.nof_prb;
-  const float2*  in   = a.grid + b * a.grid_sf_stride + (size_t)rx * 2 * a.nsymb * nre;
   const bool     bat  = a.sf_inl || a.sf_idx;  // per-subframe indices: pilots of each subframe's index
   const uint32_t sfi  = a.sf_inl ? (uint32_t)a.sf_inline[b] : a.sf_idx ? a.sf_idx[b] : a.sf_index;
+  // CRS symbols of the port: 4 / 2, fewer in the DwPTS of a TDD special subframe
+  const uint32_t nsym = chest_crs_nsym(a, sfi, port), nref = 2 * a.nof_prb, np = nsym * nref, nre = 12 * a.nof_prb;
+  const float2*  in   = a.grid + b * a.grid_sf_stride + (size_t)rx * 2 * a.nsymb * nre;
   const float2*  pil  = a.pilots + (bat ? sfi * CHEST_PILOTS_PER_SF : 0) + (size_t)(port / 2) * 4 * CHEST_MAX_NREF;
   const uint32_t fidx0 = (crs_v(port, 0) + a.cell_id % 6) % 6;
   const bool     kept_noise = a.noise_alg != 0;  // PSS / EMPTY: the REFS residuals are not the estimate
@@ -366,7 +367,7 @@ __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
 
   // ---- interpolation to every subcarrier (interp_linear_offset) and, for INTERPOLATE, between the CRS
   // symbols (interpolate_pilots, chest_dl.c:510-554); PSS noise on row nsymb - 1 (estimate_noise_pss) ----
-  const uint32_t step = nsym > 1 ? 3 : 6;
+  const uint32_t step = nsym > 1 ? 3 : 6;  // AVERAGE
   const uint32_t off  = nsym > 1 ? a.cell_id % 3 : fidx0;
   const uint32_t ns   = a.nsymb, nrows = 2 * ns;
   const bool     noise_sf = kept_noise && (sfi == 0 || sfi == 5);
@@ -374,14 +375,31 @@ __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
   float2*        ce   = a.ce + b * a.ce_sf_stride + (size_t)(port * a.nrx + rx) * a.ce_stride;
   float          pss_err = 0.f;
   for (uint32_t j = tid; j < nre; j += CH_THREADS) {
-    if (a.estimator == 1) {
+    if (a.estimator == 1 && nsym == 1) {  // one CRS symbol (special subframe): its row everywhere (chest_dl.c:511-515)
+      const cx     v = interp_at(avg, nref, 6, fidx0, j);
+      const float2 o = make_float2(v.r, v.i);
+      for (uint32_t l = 0; l < nrows; l++) {
+        ce[(size_t)l * nre + j] = o;
+      }
+      if (noise_sf && a.noise_alg == 1 && j >= kp && j < kp + 62) {
+        const cx t = sub(mul(v, ld2(a.pss, j - kp)), ld2(in, (ns - 1) * nre + j));
+        pss_err += t.r * t.r + t.i * t.i;
+      }
+    } else if (a.estimator == 1) {
       float2* col = ce + j;
       const auto vi = [&](uint32_t l) {
         return interp_at(avg + l * nref, nref, 6, (crs_v(port, l) + a.cell_id % 6) % 6, j);
       };
       const cx v0 = vi(0), v1 = vi(1);
       const auto put = [&](uint32_t l, cx x) { col[(size_t)l * nre] = make_float2(x.r, x.i); };
-      if (port < 2) {  // CRS rows 0, ns - 3, ns, 2 ns - 3
+      if (port < 2 && nsym == 3) {  // special subframe, normal CP: CRS rows 0, 4, 7; rows 8 .. 13 extrapolated
+        const cx       v2 = vi(2);
+        const uint32_t r1 = ns - 3, r2 = ns;
+        put(0, v0), put(r1, v1), put(r2, v2);
+        ivec(col, nre, v0, v1, nullptr, r1, r1 - 1, 1);
+        ivec(col, nre, v1, v2, nullptr, r2 - r1, r2 - r1 - 1, r1 + 1);
+        ivec(col, nre, v1, v2, &v2, r2 - r1, nrows - 1 - r2, r2 + 1);
+      } else if (port < 2) {  // CRS rows 0, ns - 3, ns, 2 ns - 3
         const cx       v2 = vi(2), v3 = vi(3);
         const uint32_t r1 = ns - 3, r2 = ns, r3 = 2 * ns - 3;
         put(0, v0), put(r1, v1), put(r2, v2), put(r3, v3);
@@ -518,7 +536,7 @@ __global__ __launch_bounds__(CH_THREADS) void chest_sync_kernel(ChestArgs a, flo
 {
   __shared__ float red[CH_THREADS / 64];
   const uint32_t   port = blockIdx.x / a.nrx, rx = blockIdx.x % a.nrx;
-  const uint32_t   nsym = port < 2 ? 4 : 2, nref = 2 * a.nof_prb, nre = 12 * a.nof_prb;
+  const uint32_t   nsym = chest_crs_nsym(a, a.sf_index, port), nref = 2 * a.nof_prb, nre = 12 * a.nof_prb;
   const float2*    in   = a.grid + (size_t)rx * 2 * a.nsymb * nre;
   const float2*    pil  = a.pilots + (size_t)(port / 2) * 4 * CHEST_MAX_NREF;
   float*           o    = out + (rx * 4 + port) * 10;

@@ -2,14 +2,16 @@
 // turns a DCI into a PDSCH grant (include/srsran_pdcch.h).  Host code: a few hundred bit fields per
 // subframe, nothing for the GPU.
 //
-//   DCI sizes      phch/dci.c:93-413 (FDD: 3-bit HARQ process number, no DAI)
+//   DCI sizes      phch/dci.c:93-413 (FDD: 3-bit HARQ process number, no DAI; TDD: 4 bits + DAI)
 //   DCI unpack     phch/dci.c:492-566 (format 0), :641-708 (format 1), :797-897 (1A), :1153-1241 (2 / 2A),
 //                  :1288-1340, :1369-1395
 //   DCI pack       phch/dci.c:415-490 (0), :579-639 (1), :710-795 (1A), :952-988 (1C), :1076-1151 (2/2A/2B),
 //                  :1243-1286, :1342-1367
 //   RA             phch/ra.c:37-250 (RIV, RBG size P, MCS -> I_TBS / modulation, TBS table)
 //                  phch/ra_dl.c:42-681 (PRB allocation types 0 / 1 / 2, TB sizes, RE count, MIMO)
-// Not provided (SRSRAN_ERROR): TDD, format 1B / 1C / 1D / 2B unpacking, 1B / 1D packing, distributed VRBs.
+// TDD: 4-bit HARQ process numbers and the DAI / UL index (the reference's packers write no DAI: it stays in the zero
+// padding, while its unpackers read it -- restated as is, dci.c:415-1367).
+// Not provided (SRSRAN_ERROR): format 1B / 1C / 1D / 2B unpacking, 1B / 1D packing, distributed VRBs.
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -36,19 +38,23 @@ bool is_ambiguous_size(uint32_t n)
   return false;
 }
 
-constexpr uint32_t HARQ_PID_LEN = 3;  // FDD
+// HARQ process number: 3 bits FDD, 4 bits TDD; TDD adds the 2-bit DAI (UL index with configuration 0) to formats
+// 0 / 1 / 1A / 2 / 2A (dci.c:38-40, 142-143, 190-191, 217, 276-277, 313-349)
+bool     is_tdd(const srsran_cell_t* cell) { return cell->frame_type == SRSRAN_TDD; }
+uint32_t pid_len(const srsran_cell_t* cell) { return is_tdd(cell) ? 4 : 3; }
+uint32_t dai_len(const srsran_cell_t* cell) { return is_tdd(cell) ? 2 : 0; }
 
 uint32_t format0_size_(const srsran_cell_t* cell, const srsran_dci_cfg_t* cfg)
 {
-  return (cfg->cif_enabled ? 3 : 0) + 1 + 1 + riv_nbits(cell->nof_prb) + 5 + 1 + 2 + 3 +
+  return (cfg->cif_enabled ? 3 : 0) + 1 + 1 + riv_nbits(cell->nof_prb) + 5 + 1 + 2 + 3 + dai_len(cell) +
          ((cfg->multiple_csi_request_enabled && !cfg->is_not_ue_ss) ? 2 : 1) +
          ((cfg->srs_request_enabled && !cfg->is_not_ue_ss) ? 1 : 0) + 1;
 }
 
 uint32_t format1A_size(const srsran_cell_t* cell, const srsran_dci_cfg_t* cfg)
 {
-  uint32_t n = (cfg->cif_enabled ? 3 : 0) + 1 + 1 + riv_nbits(cell->nof_prb) + 5 + HARQ_PID_LEN + 1 + 2 + 2 +
-               (cfg->srs_request_enabled ? 1 : 0);
+  uint32_t n = (cfg->cif_enabled ? 3 : 0) + 1 + 1 + riv_nbits(cell->nof_prb) + 5 + pid_len(cell) + 1 + 2 + 2 +
+               dai_len(cell) + (cfg->srs_request_enabled ? 1 : 0);
   while (n < format0_size_(cell, cfg)) {
     n++;
   }
@@ -112,7 +118,8 @@ uint32_t format2x_size(const srsran_cell_t* cell, const srsran_dci_cfg_t* cfg, s
   } else if (f == SRSRAN_DCI_FORMAT2A) {
     pbits = cell->nof_ports <= 2 ? 0 : 2;
   }
-  uint32_t n = rbg_bits(cell->nof_prb) + 2 + HARQ_PID_LEN + 1 + 2 * (5 + 1 + 2) + pbits + (cfg->cif_enabled ? 3 : 0);
+  uint32_t n = rbg_bits(cell->nof_prb) + 2 + pid_len(cell) + 1 + 2 * (5 + 1 + 2) + pbits + (cfg->cif_enabled ? 3 : 0) +
+               dai_len(cell);
   if (cell->nof_prb > 10) {
     n++;
   }
@@ -135,12 +142,14 @@ uint32_t bit_pack(const uint8_t** y, uint32_t n)
 // Format 0 (36.212 5.3.3.1.1; dci.c:492-566): after the optional CIF and the 0/1A flag, the fields
 // in transmission order.  Width 0 = field absent in this configuration.
 struct F0Field {
-  enum Id { HOP, HOP_TYPE, RIV, MCS, NDI, TPC, DMRS, CSI, CQI, SRS, RA_TYPE } id;
+  enum Id { HOP, HOP_TYPE, RIV, MCS, NDI, TPC, DMRS, UL_IDX, DAI, CSI, CQI, SRS, RA_TYPE } id;
   uint32_t width;
 };
 
-int unpack_format0(const srsran_cell_t* cell, const srsran_dci_cfg_t* cfg, srsran_dci_msg_t* msg, srsran_dci_ul_t* dci)
+int unpack_format0(const srsran_cell_t* cell, const srsran_dl_sf_cfg_t* sf, const srsran_dci_cfg_t* cfg,
+                   srsran_dci_msg_t* msg, srsran_dci_ul_t* dci)
 {
+  const bool cfg0 = is_tdd(cell) && sf && sf->tdd_config.sf_config == 0;  // IS_TDD_CFG0: UL index instead of DAI
   const uint8_t* y = msg->payload;
   if (cfg->cif_enabled) {
     dci->cif         = bit_pack(&y, 3);
@@ -161,6 +170,8 @@ int unpack_format0(const srsran_cell_t* cell, const srsran_dci_cfg_t* cfg, srsra
       {F0Field::NDI, 1},
       {F0Field::TPC, 2},
       {F0Field::DMRS, 3},
+      {F0Field::UL_IDX, cfg0 ? 2u : 0u},
+      {F0Field::DAI, is_tdd(cell) && !cfg0 ? 2u : 0u},
       {F0Field::CSI, cfg->multiple_csi_request_enabled && ue_ss ? 2u : 0u},
       {F0Field::CQI, cfg->multiple_csi_request_enabled && ue_ss ? 0u : 1u},
       {F0Field::SRS, cfg->srs_request_enabled && ue_ss ? 1u : 0u},
@@ -190,6 +201,14 @@ int unpack_format0(const srsran_cell_t* cell, const srsran_dci_cfg_t* cfg, srsra
         break;
       case F0Field::DMRS:
         dci->n_dmrs = v;
+        break;
+      case F0Field::UL_IDX:
+        dci->ul_idx = v;
+        dci->is_tdd = true;
+        break;
+      case F0Field::DAI:
+        dci->dai    = v;
+        dci->is_tdd = true;
         break;
       case F0Field::CSI:
         dci->multiple_csi_request_present = true;
@@ -256,10 +275,14 @@ int unpack_format1(const srsran_cell_t* cell, srsran_dl_sf_cfg_t* sf, srsran_dci
     return SRSRAN_ERROR;
   }
   dci->tb[0].mcs_idx = bit_pack(&y, 5);
-  dci->pid           = bit_pack(&y, HARQ_PID_LEN);
+  dci->pid           = bit_pack(&y, pid_len(cell));
   dci->tb[0].ndi     = *y++ ? true : false;
   dci->tb[0].rv      = (int)bit_pack(&y, 2);
   dci->tpc_pucch     = (uint8_t)bit_pack(&y, 2);
+  if (is_tdd(cell)) {  // dci.c:697-701
+    dci->dai    = bit_pack(&y, 2);
+    dci->is_tdd = true;
+  }
   return SRSRAN_SUCCESS;
 }
 
@@ -306,7 +329,7 @@ int unpack_format1A(const srsran_cell_t* cell, srsran_dci_cfg_t* cfg, srsran_dci
   }
   dci->type2_alloc.riv = bit_pack(&y, riv_nbits(cell->nof_prb) - nb_gap);
   dci->tb[0].mcs_idx   = bit_pack(&y, 5);
-  dci->pid             = bit_pack(&y, HARQ_PID_LEN);
+  dci->pid             = bit_pack(&y, pid_len(cell));
   if (!user) {
     if (cell->nof_prb >= 50 && dci->type2_alloc.mode == srsran_ra_type2_t::SRSRAN_RA_TYPE2_DIST) {
       dci->type2_alloc.n_gap = *y++ ? srsran_ra_type2_t::SRSRAN_RA_TYPE2_NG2 : srsran_ra_type2_t::SRSRAN_RA_TYPE2_NG1;
@@ -324,6 +347,10 @@ int unpack_format1A(const srsran_cell_t* cell, srsran_dci_cfg_t* cfg, srsran_dci
     dci->type2_alloc.n_prb1a =
         *y++ ? srsran_ra_type2_t::SRSRAN_RA_TYPE2_NPRB1A_3 : srsran_ra_type2_t::SRSRAN_RA_TYPE2_NPRB1A_2;
   }
+  if (is_tdd(cell)) {  // dci.c:890-894
+    dci->dai    = bit_pack(&y, 2);
+    dci->is_tdd = true;
+  }
   return SRSRAN_SUCCESS;
 }
 
@@ -338,7 +365,11 @@ int unpack_format2x(const srsran_cell_t* cell, srsran_dci_cfg_t* cfg, srsran_dci
     return SRSRAN_ERROR;
   }
   dci->tpc_pucch  = (uint8_t)bit_pack(&y, 2);
-  dci->pid        = bit_pack(&y, HARQ_PID_LEN);
+  if (is_tdd(cell)) {  // dci.c:1193-1197: the DAI between the TPC command and the HARQ process
+    dci->dai    = bit_pack(&y, 2);
+    dci->is_tdd = true;
+  }
+  dci->pid        = bit_pack(&y, pid_len(cell));
   dci->tb_cw_swap = *y++ ? true : false;
   uint32_t nof_tb = 0;
   for (int i = 0; i < SRSRAN_MAX_CODEWORDS; i++) {
@@ -445,7 +476,7 @@ int pack_format1(const srsran_cell_t* cell, srsran_dl_sf_cfg_t* sf, srsran_dci_c
     return SRSRAN_ERROR;
   }
   bit_put(&y, dci->tb[0].mcs_idx, 5);
-  bit_put(&y, dci->pid, HARQ_PID_LEN);
+  bit_put(&y, dci->pid, pid_len(cell));  // no DAI: the reference packers leave it to the padding
   *y++ = dci->tb[0].ndi ? 1 : 0;
   bit_put(&y, (uint32_t)dci->tb[0].rv, 2);
   bit_put(&y, dci->tpc_pucch, 2);
@@ -481,7 +512,7 @@ int pack_format1A(const srsran_cell_t* cell, srsran_dl_sf_cfg_t* sf, srsran_dci_
     }
     bit_put(&y, dci->type2_alloc.riv, riv_nbits(cell->nof_prb) - nb_gap);
     bit_put(&y, dci->tb[0].mcs_idx, 5);
-    bit_put(&y, dci->pid, HARQ_PID_LEN);
+    bit_put(&y, dci->pid, pid_len(cell));  // no DAI: the reference packers leave it to the padding
     if (user) {
       *y++ = dci->tb[0].ndi ? 1 : 0;
     } else {
@@ -531,7 +562,7 @@ int pack_format2x(const srsran_cell_t* cell, srsran_dl_sf_cfg_t* sf, srsran_dci_
     return SRSRAN_ERROR;
   }
   bit_put(&y, dci->tpc_pucch, 2);
-  bit_put(&y, dci->pid, HARQ_PID_LEN);
+  bit_put(&y, dci->pid, pid_len(cell));  // no DAI: the reference packers leave it to the padding
   *y++ = (msg->format == SRSRAN_DCI_FORMAT2B ? dci->sram_id : dci->tb_cw_swap) ? 1 : 0;
   for (int i = 0; i < 2; i++) {
     bit_put(&y, dci->tb[i].mcs_idx, 5);
@@ -550,47 +581,90 @@ int pack_format2x(const srsran_cell_t* cell, srsran_dl_sf_cfg_t* sf, srsran_dci_
 // ---- ra_dl.c ----
 uint32_t ra_re_x_prb(const srsran_cell_t* cell, srsran_dl_sf_cfg_t* sf, uint32_t slot, uint32_t prb)
 {
-  // FDD, normal subframe, normal or extended CP (ra_dl.c:42-168)
-  const uint32_t sfi   = sf->tti % 10;
-  const uint32_t nctrl = cell->nof_prb <= 10 ? sf->cfi + 1 : sf->cfi;
-  const bool     ext   = cell->cp == SRSRAN_CP_EXT;
-  const uint32_t nsym  = SRSRAN_CP_NSYMB(cell->cp);
-  uint32_t       re    = slot == 0 ? (nsym - nctrl) * 12 : nsym * 12;
-  bool           refs  = true;  // remove the CRS REs below
-  if ((sfi == 0 || sfi == 5) && prb >= cell->nof_prb / 2 - 3 && prb < cell->nof_prb / 2 + 3 + (cell->nof_prb % 2)) {
-    if (sfi == 0) {
-      if (slot == 0) {
+  // PDSCH REs of one PRB in one slot (ra_dl.c:42-161): normal subframes of FDD and TDD cells, normal or extended CP.
+  // A TDD special subframe counts only its DwPTS symbols in each slot.  Unsigned arithmetic as the reference's.
+  const uint32_t sfi    = sf->tti % 10;
+  const uint32_t nctrl  = cell->nof_prb <= 10 ? sf->cfi + 1 : sf->cfi;  // SRSRAN_NOF_CTRL_SYMBOLS
+  const bool     ext    = cell->cp == SRSRAN_CP_EXT;
+  const bool     tdd    = cell->frame_type == SRSRAN_TDD;
+  const uint32_t np     = cell->nof_ports;
+  uint32_t       nsym   = SRSRAN_CP_NSYMB(cell->cp);
+  if (tdd && srsran_sfidx_tdd_type(sf->tdd_config, sfi) == SRSRAN_TDD_SF_S) {
+    nsym = srsran_sfidx_tdd_nof_dw_slot(sf->tdd_config, slot, cell->cp);
+  }
+  uint32_t   re     = slot == 0 ? (nsym - nctrl) * 12 : nsym * 12;
+  bool       refs   = true;  // remove the CRS REs below
+  const bool centre = prb >= cell->nof_prb / 2 - 3 && prb < cell->nof_prb / 2 + 3 + (cell->nof_prb % 2);
+  const bool half   = (cell->nof_prb % 2) && (prb == cell->nof_prb / 2 - 3 || prb == cell->nof_prb / 2 + 3);
+  if (!tdd) {  // PSS / SSS at the end of slot 0 of subframes 0 / 5, PBCH in slot 1 of subframe 0
+    if ((sfi == 0 || sfi == 5) && centre) {
+      if (sfi == 0) {
+        if (slot == 0) {
+          re = (nsym - nctrl - 2) * 12;
+        } else if (ext) {
+          re   = (nsym - 4) * 12;  // both CRS symbols of the slot fall under the PBCH
+          refs = false;
+        } else {
+          re = (nsym - 4) * 12 + 2 * np;
+        }
+      } else if (slot == 0) {
         re = (nsym - nctrl - 2) * 12;
-      } else if (ext) {
-        re   = (nsym - 4) * 12;  // both CRS symbols of the slot fall under the PBCH
-        refs = false;
-      } else {
-        re = (nsym - 4) * 12 + 2 * cell->nof_ports;
       }
-    } else if (slot == 0) {
-      re = (nsym - nctrl - 2) * 12;
+      if (half) {
+        if (slot == 0) {
+          re += 2 * 12 / 2;
+        } else if (sfi == 0) {
+          re += 4 * 12 / 2 - np;
+          if (ext) {
+            re -= np > 2 ? 2 : np;
+          }
+        }
+      }
     }
-    if ((cell->nof_prb % 2) && (prb == cell->nof_prb / 2 - 3 || prb == cell->nof_prb / 2 + 3)) {
-      if (slot == 0) {
-        re += 2 * 12 / 2;
-      } else if (sfi == 0) {
-        re += 4 * 12 / 2 - cell->nof_ports;
+  } else {  // SSS in the last symbol of subframes 0 / 5 (+ PBCH in subframe 0), PSS in symbol 2 of subframes 1 / 6
+    if ((((sfi == 0 || sfi == 5) && slot == 1) || ((sfi == 1 || sfi == 6) && slot == 0)) && centre) {
+      if (sfi == 0) {
         if (ext) {
-          re -= cell->nof_ports > 2 ? 2 : cell->nof_ports;
+          re   = (nsym - 5) * 12;
+          refs = false;
+        } else {
+          re = (nsym - 5) * 12 + 2 * np;
+        }
+      } else if (sfi == 5) {
+        re = (nsym - 1) * 12;
+      } else {
+        re = (nsym - nctrl - 1) * 12;
+      }
+      if (half) {
+        re += 12 / 2;
+        if (sfi == 0) {
+          re += 4 * 12 / 2 - np;
+          if (ext) {
+            re -= np > 2 ? 2 : np;
+          }
         }
       }
     }
   }
-  if (refs) {
-    switch (cell->nof_ports) {
+  if (refs) {  // CRS of the slot's symbols (a short DwPTS holds fewer of them)
+    const bool full = (!ext && nsym >= 5) || (ext && nsym >= 4);
+    switch (np) {
       case 1:
       case 2:
-        re -= 2 * (slot + 1) * cell->nof_ports;
+        if (full) {
+          re -= 2 * (slot + 1) * np;
+        } else if (slot == 1 && nsym >= 1) {
+          re -= 2 * np;
+        }
         break;
       case 4:
         if (slot == 1) {
-          re -= 12;
-        } else {
+          if (full) {
+            re -= 12;
+          } else if (nsym >= 2) {
+            re -= 8;
+          }
+        } else if (full) {
           re -= 4;
           if (nctrl == 1) {
             re -= 4;
@@ -702,18 +776,19 @@ int compute_tb(bool alt, const srsran_dci_dl_t* dci, srsran_pdsch_grant_t* grant
     grant->tb[0].tbs = tbs;
     return SRSRAN_SUCCESS;
   }
+  // a TDD special subframe scales the PRB count for the TBS look-up (ra_dl.c:401-405, 36.213 7.1.7)
+  const double   scaled = 0.75 * grant->nof_prb;
+  const uint32_t n_prb  = dci->is_dwpts ? (uint32_t)(scaled > 1 ? scaled : 1) : grant->nof_prb;
   for (int i = 0; i < SRSRAN_MAX_CODEWORDS; i++) {
     if (!grant->tb[i].enabled) {
       grant->tb[i].tbs = 0;
       continue;
     }
+    // srsran_dl_fill_ra_mcs (ra_dl.c:323-341): a retransmission MCS (no TBS index) stores last_tbs in the TB, but the
+    // function returns 0 and its caller stores that (ra_dl.c:409)
     grant->tb[i].mod = srsran_ra_dl_mod_from_mcs(grant->tb[i].mcs_idx, alt);
     const int i_tbs  = srsran_ra_tbs_idx_from_mcs(grant->tb[i].mcs_idx, alt, false);
-    if (i_tbs >= 0) {
-      grant->tb[i].tbs = srsran_ra_tbs_from_idx((uint32_t)i_tbs, grant->nof_prb);
-    } else {
-      grant->tb[i].tbs = grant->last_tbs[i];
-    }
+    grant->tb[i].tbs = i_tbs >= 0 ? srsran_ra_tbs_from_idx((uint32_t)i_tbs, n_prb) : 0;
     if (grant->tb[i].tbs < 0) {
       return SRSRAN_ERROR;
     }
@@ -886,7 +961,7 @@ uint32_t srsran_dci_format_sizeof(const srsran_cell_t* cell, srsran_dl_sf_cfg_t*
     case SRSRAN_DCI_FORMAT1A:
       return format1A_size(cell, c);
     case SRSRAN_DCI_FORMAT1: {
-      uint32_t n = rbg_bits(cell->nof_prb) + 5 + HARQ_PID_LEN + 1 + 2 + 2 + (c->cif_enabled ? 3 : 0) +
+      uint32_t n = rbg_bits(cell->nof_prb) + 5 + pid_len(cell) + 1 + 2 + 2 + (c->cif_enabled ? 3 : 0) + dai_len(cell) +
                    (cell->nof_prb > 10 ? 1 : 0);
       while (n == format0_size(cell, c) || n == format1A_size(cell, c) || is_ambiguous_size(n)) {
         n++;
@@ -917,11 +992,7 @@ int srsran_dci_msg_unpack_pusch(srsran_cell_t* cell, srsran_dl_sf_cfg_t* sf, srs
   dci->format   = msg->format;
   srsran_dci_cfg_t zero;
   memset(&zero, 0, sizeof(zero));
-  if (cell->frame_type != SRSRAN_FDD) {
-    fprintf(stderr, "[srsran_dci] TDD is not provided\n");
-    return SRSRAN_ERROR;
-  }
-  return unpack_format0(cell, cfg ? cfg : &zero, msg, dci);
+  return unpack_format0(cell, sf, cfg ? cfg : &zero, msg, dci);
 }
 
 int srsran_dci_msg_unpack_pdsch(srsran_cell_t* cell, srsran_dl_sf_cfg_t* sf, srsran_dci_cfg_t* cfg,
@@ -942,10 +1013,8 @@ int srsran_dci_msg_unpack_pdsch(srsran_cell_t* cell, srsran_dl_sf_cfg_t* sf, srs
   if (!cfg) {
     cfg = &zero;
   }
-  if (cell->frame_type != SRSRAN_FDD) {
-    fprintf(stderr, "[srsran_dci] TDD is not provided\n");
-    return SRSRAN_ERROR;
-  }
+  // dci.c:1317-1319
+  dci->is_dwpts = cell->frame_type == SRSRAN_TDD && sf && srsran_sfidx_tdd_type(sf->tdd_config, sf->tti % 10) == SRSRAN_TDD_SF_S;
   switch (msg->format) {
     case SRSRAN_DCI_FORMAT1:
       return unpack_format1(cell, sf, cfg, msg, dci);
@@ -1055,17 +1124,25 @@ int srsran_ra_dl_dci_to_grant(const srsran_cell_t* cell, srsran_dl_sf_cfg_t* sf,
   if (!cell || !sf || !dci || !grant) {
     return SRSRAN_ERROR_INVALID_INPUTS;
   }
-  if (cell->frame_type != SRSRAN_FDD || sf->sf_type != SRSRAN_SF_NORM) {
-    fprintf(stderr, "[srsran_ra] FDD normal subframes only\n");
+  if (sf->sf_type != SRSRAN_SF_NORM) {
+    fprintf(stderr, "[srsran_ra] PDSCH grants of normal subframes only (MBSFN subframes carry the PMCH)\n");
+    return SRSRAN_ERROR;
+  }
+  if (cell->frame_type == SRSRAN_TDD && srsran_sfidx_tdd_type(sf->tdd_config, sf->tti % 10) == SRSRAN_TDD_SF_U) {
+    fprintf(stderr, "[srsran_ra] subframe %u is an uplink subframe of TDD configuration %u\n", sf->tti % 10,
+            sf->tdd_config.sf_config);
     return SRSRAN_ERROR;
   }
   memset(grant, 0, sizeof(*grant));
   if (prb_allocation(dci, grant, cell->nof_prb) || compute_tb(pdsch_use_tbs_index_alt, dci, grant)) {
     return SRSRAN_ERROR;
   }
-  grant->nof_re           = srsran_ra_dl_grant_nof_re(cell, sf, grant);
-  grant->nof_symb_slot[0] = SRSRAN_CP_NSYMB(cell->cp);  // ra_dl.c:428-431 (FDD)
-  grant->nof_symb_slot[1] = SRSRAN_CP_NSYMB(cell->cp);
+  grant->nof_re = srsran_ra_dl_grant_nof_re(cell, sf, grant);
+  // ra_dl.c:428-440: a TDD special subframe carries the PDSCH in its DwPTS symbols only
+  const bool special = cell->frame_type == SRSRAN_TDD &&
+                       srsran_sfidx_tdd_type(sf->tdd_config, sf->tti % 10) == SRSRAN_TDD_SF_S;
+  grant->nof_symb_slot[0] = special ? srsran_sfidx_tdd_nof_dw_slot(sf->tdd_config, 0, cell->cp) : SRSRAN_CP_NSYMB(cell->cp);
+  grant->nof_symb_slot[1] = special ? srsran_sfidx_tdd_nof_dw_slot(sf->tdd_config, 1, cell->cp) : SRSRAN_CP_NSYMB(cell->cp);
   for (int i = 0; i < SRSRAN_MAX_CODEWORDS; i++) {
     if (grant->tb[i].enabled) {
       grant->tb[i].nof_bits = grant->nof_re * srsran_mod_bits_x_symbol(grant->tb[i].mod);

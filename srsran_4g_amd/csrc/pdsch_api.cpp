@@ -534,9 +534,8 @@ int srsran_pdsch_set_cell(srsran_pdsch_t* q, srsran_cell_t cell)
       cell.nof_ports == 3 || cell.nof_ports > 4 || cell.id > 503) {
     return SRSRAN_ERROR_INVALID_INPUTS;
   }
-  if (cell.frame_type != SRSRAN_FDD) {
-    fprintf(stderr, "[srsran_pdsch] only FDD cells are provided\n");
-    return SRSRAN_ERROR;
+  if (cell.frame_type != SRSRAN_FDD && cell.frame_type != SRSRAN_TDD) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
   }
   if (cell.cp != SRSRAN_CP_NORM && cell.cp != SRSRAN_CP_EXT) {
     return SRSRAN_ERROR_INVALID_INPUTS;

@@ -44,7 +44,7 @@ int chest_dl_gpu_estimate_batch_inline(srsran_chest_dl_t*           q,
                                        void*                        stream);
 // the estimator options the batch estimator takes (the same check it makes, without launching anything; prints
 // the reason when it returns false)
-bool chest_batch_cfg_supported(const srsran_chest_dl_cfg_t* cfg, int full_grid);
+bool chest_batch_cfg_supported(const srsran_chest_dl_t* q, const srsran_chest_dl_cfg_t* cfg, int full_grid);
 
 }  // namespace srsran_amd
 #endif

@@ -58,10 +58,20 @@ struct UeDlGpu {
   uint32_t      mi_set    = 1;  // m_i of the tables the PDCCH object holds
 };
 
-// set_mi_value (ue_dl.c:296-313): the PDCCH works on the REG tables of the selected m_i
-void select_mi(UeDlGpu* g)
+// 36.213 Table 6.9-1: PHICH m_i per TDD uplink-downlink configuration and subframe (ue_dl.c:50-57)
+const uint8_t kMiTdd[7][10] = {{2, 1, 0, 0, 0, 2, 1, 0, 0, 0}, {0, 1, 0, 0, 1, 0, 1, 0, 0, 1},
+                               {0, 0, 0, 1, 0, 0, 0, 0, 1, 0}, {1, 0, 0, 0, 0, 0, 0, 0, 1, 1},
+                               {0, 0, 0, 0, 0, 0, 0, 0, 1, 1}, {0, 0, 0, 0, 0, 0, 0, 0, 1, 0},
+                               {1, 1, 0, 0, 0, 1, 1, 0, 0, 1}};
+
+// set_mi_value (ue_dl.c:296-313): the PDCCH works on the REG tables of the selected m_i (MI_VALUE: 1 for FDD, the
+// table above for TDD)
+void select_mi(UeDlGpu* g, const srsran_cell_t& cell, const srsran_dl_sf_cfg_t* sf)
 {
-  const uint32_t mi = g->mi_auto ? 1u : g->mi_manual;
+  const uint32_t auto_mi = cell.frame_type == SRSRAN_FDD || sf->tdd_config.sf_config >= 7
+                               ? 1u
+                               : kMiTdd[sf->tdd_config.sf_config][sf->tti % 10];
+  const uint32_t mi      = g->mi_auto ? auto_mi : g->mi_manual;
   if (mi != g->mi_set) {
     srsran_pdcch_set_regs(&g->pdcch, mi == 1 ? &g->regs : &g->regs_mi[mi == 0 ? 0 : 1]);
     g->mi_set = mi;
@@ -263,10 +273,16 @@ static int fft_estimate(srsran_ue_dl_t* q, srsran_dl_sf_cfg_t* sf, srsran_ue_dl_
     return sf->cfi >= 1 && sf->cfi <= 3 ? SRSRAN_SUCCESS : SRSRAN_ERROR;  // CFI from the caller
   }
   float corr = 0;
-  select_mi(g);
-  if (srsran_pcfich_decode(&g->pcfich, sf, &q->chest_res, q->sf_symbols, &corr) < 0 ||
-      srsran_pdcch_extract_llr(&g->pdcch, sf, &q->chest_res, q->sf_symbols)) {
-    fprintf(stderr, "[srsran_ue_dl] Error decoding PCFICH / extracting PDCCH LLRs\n");
+  select_mi(g, q->cell, sf);
+  if (srsran_pcfich_decode(&g->pcfich, sf, &q->chest_res, q->sf_symbols, &corr) < 0) {
+    fprintf(stderr, "[srsran_ue_dl] Error decoding PCFICH\n");
+    return SRSRAN_ERROR;
+  }
+  if (q->cell.frame_type == SRSRAN_TDD && (sf->tti % 10 == 1 || sf->tti % 10 == 6) && sf->cfi == 3) {
+    sf->cfi = 2;  // ue_dl.c:331-334: at most 2 control symbols in the special subframes' DwPTS
+  }
+  if (srsran_pdcch_extract_llr(&g->pdcch, sf, &q->chest_res, q->sf_symbols)) {
+    fprintf(stderr, "[srsran_ue_dl] Error extracting PDCCH LLRs\n");
     return SRSRAN_ERROR;
   }
   return SRSRAN_SUCCESS;
@@ -320,7 +336,14 @@ int srsran_ue_dl_gpu_decode_batch(srsran_ue_dl_t*              q,
   UeDlGpu*    g    = (UeDlGpu*)q->gpu;
   hipStream_t s    = (hipStream_t)stream;
   const bool  full = cfg->chest_cfg.estimator_alg == SRSRAN_ESTIMATOR_ALG_INTERPOLATE;  // every symbol its own row
-  if (!srsran_amd::chest_batch_cfg_supported(&cfg->chest_cfg, full)) {  // before any batch is staged
+  for (uint32_t b = 1; b < nof_sf; b++) {  // one TDD frame configuration per batch (the estimator takes one)
+    if (memcmp(&sfs[b].tdd_config, &sfs[0].tdd_config, sizeof(srsran_tdd_config_t)) != 0) {
+      fprintf(stderr, "[srsran_ue_dl] batch: subframes with different TDD configurations\n");
+      return SRSRAN_ERROR_INVALID_INPUTS;
+    }
+  }
+  srsran_chest_dl_gpu_set_tdd_config(&q->chest, sfs[0].tdd_config);
+  if (!srsran_amd::chest_batch_cfg_supported(&q->chest, &cfg->chest_cfg, full)) {  // before any batch is staged
     return SRSRAN_ERROR;
   }
   if (!grow(q, g, nof_sf, full)) {

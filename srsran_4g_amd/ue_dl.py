@@ -107,7 +107,7 @@ class srsran_ue_dl_t(ctypes.Structure):
 
 class srsran_ue_dl_gpu_sf_t(ctypes.Structure):
     _fields_ = [("tti", u32), ("cfi", u32), ("pdsch_cfg", ctypes.POINTER(srsran_pdsch_cfg_t)),
-                ("d_payload", ctypes.c_void_p * 2), ("new_data", u32 * 2)]
+                ("d_payload", ctypes.c_void_p * 2), ("new_data", u32 * 2), ("tdd_config", srsran_tdd_config_t)]
 
 
 _bound = False
@@ -195,13 +195,23 @@ def symbol_size_is_standard():
     return bool(lib().srsran_symbol_size_is_standard())
 
 
-def cell(nof_prb=100, nof_ports=2, cell_id=1, phich_res=2, cp=0):
-    """FDD, normal CP (cp=1: extended), normal PHICH duration, Ng = 1 (phich_res 2) as the reference's
-    test cells"""
+def cell(nof_prb=100, nof_ports=2, cell_id=1, phich_res=2, cp=0, tdd=False):
+    """FDD (tdd=True: TDD), normal CP (cp=1: extended), normal PHICH duration, Ng = 1 (phich_res 2) as the
+    reference's test cells"""
     c = srsran_cell_t()
     c.nof_prb, c.nof_ports, c.id, c.cp = nof_prb, nof_ports, cell_id, cp
     c.phich_resources = phich_res
+    c.frame_type = 1 if tdd else 0
     return c
+
+
+def sf_cfg(tti, cfi=0, tdd=None):
+    """srsran_dl_sf_cfg_t; tdd = (uplink-downlink configuration, special-subframe configuration) or None"""
+    sf = srsran_dl_sf_cfg_t()
+    sf.tti, sf.cfi = tti, cfi
+    if tdd is not None:
+        sf.tdd_config.sf_config, sf.tdd_config.ss_config, sf.tdd_config.configured = tdd[0], tdd[1], True
+    return sf
 
 
 def srsue_chest_cfg():
@@ -284,12 +294,11 @@ class ChestDl:
         self.cell = cell_
         self.nrx = nof_rx
 
-    def estimate(self, grids, tti, cfg=None):
-        """grids: (nrx, 14*12*nof_prb) complex64 -> (ce[port][rx] arrays, res)."""
+    def estimate(self, grids, tti, cfg=None, tdd=None):
+        """grids: (nrx, 14*12*nof_prb) complex64 -> (ce[port][rx] arrays, res); tdd = (sf_config, ss_config)"""
         grids = [np.ascontiguousarray(g, np.complex64) for g in grids]
         ptrs = (ctypes.c_void_p * MAX_PORTS)(*[g.ctypes.data for g in grids] + [None] * (MAX_PORTS - len(grids)))
-        sf = srsran_dl_sf_cfg_t()
-        sf.tti = tti
+        sf = sf_cfg(tti, 0, tdd)
         if cfg is None:
             rc = lib().srsran_chest_dl_estimate(ctypes.byref(self.q), ctypes.byref(sf), ctypes.addressof(ptrs),
                                                 ctypes.byref(self.res))
@@ -324,10 +333,11 @@ MOD_FROM_QM = {1: 0, 2: 1, 4: 2, 6: 3, 8: 4}
 
 def pdsch_cfg(nof_prb, nof_re, tbs, Qm, rv=(0, 0), scheme="cdd", pmi=0, rnti=0x1234, max_iterations=8,
               csi_enable=True, power_scale=False, p_a=0.0, p_b=0, softbuffers=(), zf=False, cp=0, nof_ports=2,
-              meas_evm=False):
+              meas_evm=False, nsl=None):
     """srsran_pdsch_cfg_t for a full-bandwidth grant of len(tbs) codewords on as many layers
     (srsUE defaults: csi_enable, 8 half-iterations, MMSE, no power scaling); cp=1: extended CP;
-    transmit diversity runs on nof_ports layers (2 or 4)."""
+    transmit diversity runs on nof_ports layers (2 or 4); nsl: the grant's symbols per slot (a TDD special
+    subframe's DwPTS, srsran_ra_dl_compute_nof_re)."""
     c = srsran_pdsch_cfg_t()
     g = c.grant
     g.tx_scheme = SCHEME[scheme]
@@ -338,6 +348,8 @@ def pdsch_cfg(nof_prb, nof_re, tbs, Qm, rv=(0, 0), scheme="cdd", pmi=0, rnti=0x1
     g.nof_prb = nof_prb
     g.nof_re = nof_re
     g.nof_symb_slot[0] = g.nof_symb_slot[1] = 6 if cp else 7
+    if nsl is not None:
+        g.nof_symb_slot[0], g.nof_symb_slot[1] = nsl
     g.nof_tb = len(tbs)
     g.nof_layers = nof_ports if scheme == "diversity" else len(tbs)
     for i, t in enumerate(tbs):
@@ -430,7 +442,9 @@ class Pdsch:
 class UeDl:
     """srsran_ue_dl_t: host-synchronous decode_fft_estimate / decode_pdsch and the device batch."""
 
-    def __init__(self, cell_, nof_rx):
+    def __init__(self, cell_, nof_rx, tdd=None):
+        """tdd = (sf_config, ss_config): the TDD configuration every call's srsran_dl_sf_cfg_t carries"""
+        self.tdd = tdd
         self.q = srsran_ue_dl_t()
         if lib().srsran_ue_dl_init(ctypes.byref(self.q), None, cell_.nof_prb, nof_rx):
             raise RuntimeError("srsran_ue_dl_init failed (no HIP device?)")
@@ -449,8 +463,7 @@ class UeDl:
     def fft_estimate(self, samples, tti, cfi):
         x = [np.ascontiguousarray(v, np.complex64) for v in samples]
         ptrs = (ctypes.c_void_p * MAX_PORTS)(*[v.ctypes.data for v in x] + [None] * (MAX_PORTS - len(x)))
-        sf = srsran_dl_sf_cfg_t()
-        sf.tti, sf.cfi = tti, cfi
+        sf = sf_cfg(tti, cfi, self.tdd)
         ret = lib().srsran_ue_dl_decode_fft_estimate_noguru(ctypes.byref(self.q), ctypes.byref(sf),
                                                             ctypes.byref(self.cfg), ctypes.addressof(ptrs))
         self.last_cfi = sf.cfi  # decoded from the PCFICH (1/2-port cells), else the caller's
@@ -460,8 +473,7 @@ class UeDl:
         """srsran_ue_dl_find_dl_dci (after fft_estimate) -> list of srsran_dci_dl_t"""
         from . import pdcch as PD
         PD.lib()
-        sf = srsran_dl_sf_cfg_t()
-        sf.tti, sf.cfi = tti, cfi
+        sf = sf_cfg(tti, cfi, self.tdd)
         self.cfg.cfg.tm = tm
         self.cfg.cfg.dci_common_ss = common_ss
         out = (PD.srsran_dci_dl_t * 5)()
@@ -474,8 +486,7 @@ class UeDl:
         """srsran_ue_dl_find_ul_dci (the format 0 DCIs the last find_dl_dci found) -> [srsran_dci_ul_t]"""
         from . import pdcch as PD
         PD.lib()
-        sf = srsran_dl_sf_cfg_t()
-        sf.tti, sf.cfi = tti, cfi
+        sf = sf_cfg(tti, cfi, self.tdd)
         out = (PD.srsran_dci_ul_t * 5)()
         n = lib().srsran_ue_dl_find_ul_dci(ctypes.byref(self.q), ctypes.byref(sf), ctypes.byref(self.cfg), rnti, out)
         if n < 0:
@@ -495,8 +506,7 @@ class UeDl:
     def dci_to_grant(self, dci, tti, cfi, tm=2):
         from . import pdcch as PD
         PD.lib()
-        sf = srsran_dl_sf_cfg_t()
-        sf.tti, sf.cfi = tti, cfi
+        sf = sf_cfg(tti, cfi, self.tdd)
         self.cfg.cfg.tm = tm
         g = PD.srsran_pdsch_grant_t()
         r = lib().srsran_ue_dl_dci_to_pdsch_grant(ctypes.byref(self.q), ctypes.byref(sf), ctypes.byref(self.cfg),
@@ -511,8 +521,7 @@ class UeDl:
         return out
 
     def decode_pdsch(self, cfg, tti, cfi):
-        sf = srsran_dl_sf_cfg_t()
-        sf.tti, sf.cfi = tti, cfi
+        sf = sf_cfg(tti, cfi, self.tdd)
         ntb = cfg.grant.nof_tb
         pls = [np.zeros(cfg.grant.tb[i].tbs // 8 + 64, np.uint8) for i in range(ntb)]
         data = (srsran_pdsch_res_t * 2)()
@@ -522,12 +531,15 @@ class UeDl:
         return ret, [(data[i].crc, pls[i], data[i].avg_iterations_block) for i in range(ntb)]
 
     @staticmethod
-    def batch_entries(sfs):
+    def batch_entries(sfs, tdd=None):
         """sfs: list of (tti, cfi, srsran_pdsch_cfg_t, [d_payload ptrs], [new_data]) -> ctypes array
-        (keep the cfg objects alive while the array is used)."""
+        (keep the cfg objects alive while the array is used); tdd = (sf_config, ss_config) of a TDD cell."""
         arr = (srsran_ue_dl_gpu_sf_t * len(sfs))()
         for i, (tti, cfi, cfg, pls, nd) in enumerate(sfs):
             arr[i].tti, arr[i].cfi = tti, cfi
+            if tdd is not None:
+                t = arr[i].tdd_config
+                t.sf_config, t.ss_config, t.configured = tdd[0], tdd[1], True
             arr[i].pdsch_cfg = ctypes.pointer(cfg)
             for t, p in enumerate(pls):
                 arr[i].d_payload[t] = p
@@ -536,7 +548,7 @@ class UeDl:
 
     def gpu_decode_batch(self, sfs, d_samples, d_result, d_avg, cfo=0.0, stream=None):
         """srsran_ue_dl_gpu_decode_batch; sfs: entry list (see batch_entries) or a prebuilt array."""
-        arr = sfs if isinstance(sfs, ctypes.Array) else self.batch_entries(sfs)
+        arr = sfs if isinstance(sfs, ctypes.Array) else self.batch_entries(sfs, self.tdd)
         return lib().srsran_ue_dl_gpu_decode_batch(ctypes.byref(self.q), ctypes.byref(self.cfg), len(arr), arr,
                                                    d_samples, cfo, d_result, d_avg, stream)
 

@@ -202,20 +202,38 @@ def crs_values(cell_id, nof_prb, ns, l, cp=0):
     return ((1 - 2.0 * c[2 * m]) + 1j * (1 - 2.0 * c[2 * m + 1])) / math.sqrt(2)
 
 
-def crs_grid(cell_id, nof_prb, nports, port, sf_idx, cp=0):
-    """port's CRS in a (2 nsymb, 12 N_RB) grid (nsymb 7, or 6 with cp=1 extended); ports 2 / 3 in l = 1"""
+def crs_grid(cell_id, nof_prb, nports, port, sf_idx, cp=0, nsymb_tx=None):
+    """port's CRS in a (2 nsymb, 12 N_RB) grid (nsymb 7, or 6 with cp=1 extended); ports 2 / 3 in l = 1;
+    nsymb_tx: only the first nsymb_tx symbols are transmitted (a TDD special subframe's DwPTS)"""
     ns = 6 if cp else 7
     g = np.zeros((2 * ns, 12 * nof_prb), np.complex128)
     for s in range(2):
         for l in ([0, ns - 3] if port < 2 else [1]):
+            if nsymb_tx is not None and ns * s + l >= nsymb_tx:
+                continue
             k = 6 * np.arange(2 * nof_prb) + (crs_shift(port, 0 if l == 0 else 4, s) + cell_id % 6) % 6
             g[ns * s + l, k] = crs_values(cell_id, nof_prb, 2 * sf_idx + s, l, cp)
     return g
 
 
-def pdsch_mask(nof_prb, nports, cell_id, cfi, sf_idx, prb=None, cp=0):
-    """(2 nsymb, 12 N_RB) bool: REs that carry PDSCH"""
-    assert nof_prb % 2 == 0 or sf_idx not in (0, 5), "odd N_RB centre PRBs not generated"
+# ---------------- TDD frame structure (36.211 4.2) ----------------
+TDD_PATTERN = ("DSUUUDSUUU", "DSUUDDSUUD", "DSUDDDSUDD", "DSUUUDDDDD", "DSUUDDDDDD", "DSUDDDDDDD", "DSUUUDSUUD")
+TDD_DWPTS = (3, 9, 10, 11, 12, 3, 9, 10, 11, 6)  # Table 4.2-1, normal CP (srsRAN uses these for both CPs)
+
+
+def dwpts(tdd, sf_idx):
+    """OFDM symbols a TDD subframe transmits on the downlink: all of a D subframe, the DwPTS of an S one, none of a
+    U one (tdd = (uplink-downlink configuration, special-subframe configuration))"""
+    t = TDD_PATTERN[tdd[0]][sf_idx]
+    return 14 if t == "D" else TDD_DWPTS[tdd[1]] if t == "S" else 0
+
+
+def pdsch_mask(nof_prb, nports, cell_id, cfi, sf_idx, prb=None, cp=0, tdd=None):
+    """(2 nsymb, 12 N_RB) bool: REs that carry PDSCH.  tdd = (sf_config, ss_config): a TDD cell, whose SSS is the
+    last symbol of subframes 0 / 5 and PSS the third symbol of subframes 1 / 6, and whose special subframes carry
+    the PDSCH in their DwPTS symbols only."""
+    assert nof_prb % 2 == 0 or sf_idx not in ((0, 5) if tdd is None else (0, 1, 5, 6)), \
+        "odd N_RB centre PRBs not generated"
     ns = 6 if cp else 7
     nre = 12 * nof_prb
     m = np.zeros((2 * ns, nre), bool)
@@ -230,11 +248,74 @@ def pdsch_mask(nof_prb, nports, cell_id, cfi, sf_idx, prb=None, cp=0):
             else:
                 m[ns * s + l, (k % 3) == cell_id % 3] = False
     lo, hi = 12 * (nof_prb // 2 - 3), 12 * (nof_prb // 2 + 3)
-    if sf_idx in (0, 5):
-        m[ns - 2:ns, lo:hi] = False  # SSS, PSS
+    if tdd is None:
+        if sf_idx in (0, 5):
+            m[ns - 2:ns, lo:hi] = False  # SSS, PSS
+    else:
+        if sf_idx in (0, 5):
+            m[2 * ns - 1, lo:hi] = False  # SSS
+        if sf_idx in (1, 6):
+            m[2, lo:hi] = False  # PSS
+        m[dwpts(tdd, sf_idx):] = False  # GP / UpPTS of a special subframe
     if sf_idx == 0:
         m[ns:ns + 4, lo:hi] = False  # PBCH
     return m
+
+
+def pss_sequence(n_id_2):
+    """36.211 6.11.1.1: the length-62 Zadoff-Chu sequence d_u(n) of root u = 25 / 29 / 34"""
+    u = (25, 29, 34)[n_id_2]
+    n = np.arange(62)
+    e = np.where(n < 31, n * (n + 1), (n + 1) * (n + 2))
+    return np.exp(-1j * np.pi * u * e / 63)
+
+
+def sss_sequence(cell_id, sf_idx):
+    """36.211 6.11.2.1: d(0..61) of subframe 0 or 5 (m-sequences s, c, z from x^5 + x^2 + 1, x^5 + x^3 + 1,
+    x^5 + x^4 + x^2 + x + 1)"""
+    n1, n2 = cell_id // 3, cell_id % 3
+
+    def mseq(taps):
+        x = [0, 0, 0, 0, 1]
+        for i in range(26):
+            x.append(sum(x[i + t] for t in taps) % 2)
+        return 1 - 2 * np.array(x)
+
+    s_t, c_t, z_t = mseq((2, 0)), mseq((3, 0)), mseq((4, 2, 1, 0))
+    qp = n1 // 30
+    q = (n1 + qp * (qp + 1) // 2) // 30
+    mp = n1 + q * (q + 1) // 2
+    m0 = mp % 31
+    m1 = (m0 + mp // 31 + 1) % 31
+    n = np.arange(31)
+    s0, s1 = s_t[(n + m0) % 31], s_t[(n + m1) % 31]
+    c0, c1 = c_t[(n + n2) % 31], c_t[(n + n2 + 3) % 31]
+    z1m0, z1m1 = z_t[(n + m0 % 8) % 31], z_t[(n + m1 % 8) % 31]
+    d = np.zeros(62)
+    if sf_idx == 0:
+        d[0::2], d[1::2] = s0 * c0, s1 * c1 * z1m0
+    else:
+        d[0::2], d[1::2] = s1 * c0, s0 * c1 * z1m1
+    return d
+
+
+def sync_grid(nof_prb, cell_id, sf_idx, cp=0, tdd=None):
+    """(2 nsymb, 12 N_RB) grid with the PSS / SSS of the subframe (every port transmits them, enb_dl.c:333-343):
+    FDD -- SSS, PSS in the last two symbols of slot 0 of subframes 0 / 5; TDD -- SSS in the last symbol of
+    subframes 0 / 5, PSS in the third symbol of subframes 1 / 6.  The 5 subcarriers either side stay empty."""
+    ns = 6 if cp else 7
+    g = np.zeros((2 * ns, 12 * nof_prb), np.complex128)
+    k = 6 * nof_prb - 31 + np.arange(62)
+    if tdd is None:
+        if sf_idx in (0, 5):
+            g[ns - 2, k] = sss_sequence(cell_id, sf_idx)
+            g[ns - 1, k] = pss_sequence(cell_id % 3)
+    else:
+        if sf_idx in (0, 5):
+            g[2 * ns - 1, k] = sss_sequence(cell_id, sf_idx)
+        if sf_idx in (1, 6):
+            g[2, k] = pss_sequence(cell_id % 3)
+    return g
 
 
 def ofdm_tx(grid, N, cp=0):
@@ -302,17 +383,23 @@ def pcfich_grids(nof_prb, cell_id, nports, sf_idx, cfi, cp=0):
 
 
 def pdsch_subframe(nof_prb, cell_id, nports, tti, cfi, rnti, tbs, Qm, rv, payloads, scheme="cdd", codebook=1,
-                   nrx=2, snr_db=None, rng=None, N=None, channel=None, cfo=0.0, pcfich=True, ctrl=None, cp=0):
+                   nrx=2, snr_db=None, rng=None, N=None, channel=None, cfo=0.0, pcfich=True, ctrl=None, cp=0,
+                   sync=False, tdd=None):
     """One PDSCH subframe through OFDM and a static MIMO channel.
 
     payloads: one uint8 array (tbs/8 bytes) per codeword.  channel: (nrx, nports) complex matrix
     (default: [[1, 1], [1, -1]] for 2 ports as phy_dl_test.c:568-583 uses, ones for 1 port).
     pcfich: also transmit the PCFICH of `cfi`; ctrl: optional per-port (14, 12 N_RB) grids added
-    before the OFDM modulator (e.g. a PDCCH control region); cp=1: extended cyclic prefix.
+    before the OFDM modulator (e.g. a PDCCH control region); cp=1: extended cyclic prefix;
+    sync: also transmit the PSS / SSS (every port, as the reference eNB); tdd = (sf_config, ss_config): a TDD cell
+    (TDD sync-signal positions; a special subframe transmits its DwPTS symbols only).
     Returns (samples[nrx, sf_len] complex64, nof_re)."""
     N = N or symbol_sz(nof_prb)
     sf_idx = tti % 10
-    mask = pdsch_mask(nof_prb, nports, cell_id, cfi, sf_idx, cp=cp)
+    nsymb_tx = None if tdd is None else dwpts(tdd, sf_idx)
+    if nsymb_tx == 0:
+        raise ValueError(f"subframe {sf_idx} is an uplink subframe of TDD configuration {tdd[0]}")
+    mask = pdsch_mask(nof_prb, nports, cell_id, cfi, sf_idx, cp=cp, tdd=tdd)
     nof_re = int(mask.sum())
     layers = []
     for q, pl in enumerate(payloads):
@@ -325,13 +412,18 @@ def pdsch_subframe(nof_prb, cell_id, nports, tti, cfi, rnti, tbs, Qm, rv, payloa
         raise ValueError("scheme / port count mismatch")
     tx = []
     pc = pcfich_grids(nof_prb, cell_id, nports, sf_idx, cfi, cp) if pcfich else None
+    sg = sync_grid(nof_prb, cell_id, sf_idx, cp, tdd) if sync else None
     for p in range(nports):
-        g = crs_grid(cell_id, nof_prb, nports, p, sf_idx, cp)
+        g = crs_grid(cell_id, nof_prb, nports, p, sf_idx, cp, nsymb_tx)
         g[mask] = ports[p]
         if pc is not None:
             g = g + pc[p]
         if ctrl is not None:
             g = g + ctrl[p]
+        if sg is not None:
+            g = g + sg
+        if nsymb_tx is not None:
+            g[nsymb_tx:] = 0  # GP / UpPTS
         tx.append(ofdm_tx(g, N, cp))
     H4 = [[1, 0.5j, -0.4, 0.3], [0.3, -0.6j, 1, 0.5]]
     H = np.asarray(channel if channel is not None else

@@ -235,3 +235,116 @@ def test_mib_pack(nprb, phich_len, phich_res, sfn, want):
     from srsran_4g_amd import enb_dl as E
     c = PD.cell(nprb, 1, 1, phich_len=phich_len, phich_res=phich_res)
     assert "".join(str(b) for b in E.mib_pack(c, sfn)) == want
+
+
+def _tdd_cell(nprb, ports=1, cell_id=0):
+    c = PD.cell(nprb, ports, cell_id)
+    c.frame_type = 1  # SRSRAN_TDD
+    return c
+
+
+def _sf(tti, sf_config=1, ss_config=7):
+    from srsran_4g_amd import ue_dl as U
+    return U.sf_cfg(tti, 1, (sf_config, ss_config))
+
+
+@pytest.mark.parametrize("nprb", [6, 15, 25, 50, 75, 100])
+def test_tdd_sizes(nprb):
+    """TDD DCI sizes (dci.c:93-413): 4-bit HARQ process numbers and the 2-bit DAI / UL index -- format 0 and 1A
+    grow by 2 / 3 bits before the 0 / 1A alignment, formats 1 / 2 / 2A by 3 bits before the ambiguity padding;
+    at 100 PRB formats 0 / 1A are 31 bits (28 FDD)"""
+    f, t = _cell(nprb), _tdd_cell(nprb)
+    f0, f1a, t0, t1a = PD.dci_size(f, F0), PD.dci_size(f, F1A), PD.dci_size(t, F0), PD.dci_size(t, F1A)
+    assert f0 == f1a and t0 == t1a and t1a >= f1a + 2
+    if nprb == 100:
+        assert (f1a, t1a) == (28, 31)
+    nb = OP.riv_nbits(nprb)
+    raw1a = 1 + 1 + nb + 5 + 4 + 1 + 2 + 2 + 2
+    raw0 = 1 + 1 + nb + 5 + 1 + 2 + 3 + 2 + 1 + 1
+    exp = max(raw1a, raw0)
+    exp += 1 if exp in (12, 14, 16, 20, 24, 26, 32, 40, 44, 56) else 0
+    assert t1a == exp
+    for fmt in (F1, F2, F2A):
+        if fmt != F1 and nprb < 50:
+            continue
+        n = PD.dci_size(t, fmt)
+        assert n not in (12, 14, 16, 20, 24, 26, 32, 40, 44, 56) and n >= PD.dci_size(f, fmt) + 2
+
+
+@pytest.mark.parametrize("nprb", [6, 25, 100])
+def test_tdd_format1_1A_round_trip(nprb):
+    """formats 1 and 1A on a TDD cell: 4-bit HARQ process numbers survive pack -> unpack; the reference's packers
+    write no DAI (it stays in the zero padding), so the unpacked DAI is 0 and is_tdd is set"""
+    rng = np.random.default_rng(7 * nprb)
+    c = _tdd_cell(nprb)
+    nrbg = int(np.ceil(nprb / OP.type0_P(nprb)))
+    nb = OP.riv_nbits(nprb)
+    for _ in range(12):
+        pid = int(rng.integers(0, 16))
+        d = _dl(0x4601, F1, alloc_type=ALLOC0, pid=pid)
+        d.raw[0] = int(rng.integers(0, 1 << nrbg))
+        d.tb[0].mcs_idx, d.tb[0].rv = int(rng.integers(0, 29)), int(rng.integers(0, 4))
+        r, m = PD.pack_pdsch(c, d)
+        assert r == 0 and m.nof_bits == PD.dci_size(c, F1)
+        r, u = PD.unpack_pdsch(c, list(m.payload[:m.nof_bits]), F1, 0x4601)
+        assert r == 0 and u.pid == pid and u.raw[0] == d.raw[0] and u.is_tdd and u.dai == 0
+        d = _dl(0x4601, F1A, pid=pid)
+        _type2(d, int(rng.integers(0, 1 << nb)))
+        d.tb[0].mcs_idx = int(rng.integers(0, 29))
+        r, m = PD.pack_pdsch(c, d)
+        assert r == 0 and m.nof_bits == PD.dci_size(c, F1A)
+        r, u = PD.unpack_pdsch(c, list(m.payload[:m.nof_bits]), F1A, 0x4601)
+        assert r == 0 and u.pid == pid and u.raw[0] == d.raw[0] and u.is_tdd and u.dai == 0
+
+
+def _bits(v, n):
+    return [(v >> (n - 1 - i)) & 1 for i in range(n)]
+
+
+@pytest.mark.parametrize("sf_config", [0, 1])
+def test_tdd_format0_unpack_dai_ul_index(sf_config):
+    """format 0 on a TDD cell (dci.c:535-548): after the DMRS cyclic shift, the 2-bit UL index (uplink-downlink
+    configuration 0) or DAI (the others), then the CSI request -- from a hand-built 36.212 5.3.3.1.1 payload"""
+    nprb = 50
+    c = _tdd_cell(nprb)
+    nb = OP.riv_nbits(nprb)
+    riv, mcs, ndi, tpc, dmrs, v2, cqi = 777, 21, 1, 2, 5, 3, 1
+    bits = [0, 0] + _bits(riv, nb) + _bits(mcs, 5) + [ndi] + _bits(tpc, 2) + _bits(dmrs, 3) + _bits(v2, 2) + [cqi]
+    size = PD.dci_size(c, F0)
+    bits += [0] * (size - len(bits))
+    m = PD.srsran_dci_msg_t()
+    m.payload[:size] = bits
+    m.nof_bits, m.format, m.rnti = size, F0, 0x4601
+    d = PD.srsran_dci_ul_t()
+    import ctypes
+    sf = _sf(3, sf_config)
+    r = PD.lib().srsran_dci_msg_unpack_pusch(ctypes.byref(c), ctypes.byref(sf), None, ctypes.byref(m), ctypes.byref(d))
+    assert r == 0 and d.is_tdd
+    assert (d.type2_alloc.riv, d.tb.mcs_idx, d.tpc_pusch, d.n_dmrs, bool(d.cqi_request)) == (riv, mcs, tpc, dmrs, True)
+    assert (d.ul_idx, d.dai) == ((v2, 0) if sf_config == 0 else (0, v2))
+
+
+def test_tdd_format2_dai_before_pid():
+    """format 2 on a TDD cell unpacks the DAI between the TPC command and the HARQ process number (dci.c:1185-1200),
+    and a DwPTS subframe sets is_dwpts (dci.c:1317-1319)"""
+    import ctypes
+    nprb, ports = 50, 2
+    c = _tdd_cell(nprb, ports)
+    P = OP.type0_P(nprb)
+    nrbg = int(np.ceil(nprb / P))
+    size = PD.dci_size(c, F2)
+    mask, tpc, dai, pid = 0x155, 1, 2, 13
+    bits = [0] + _bits(mask, nrbg) + _bits(tpc, 2) + _bits(dai, 2) + _bits(pid, 4) + [0]
+    bits += _bits(17, 5) + [1] + _bits(2, 2) + _bits(9, 5) + [0] + _bits(1, 2) + _bits(5, 3)
+    bits += [0] * (size - len(bits))
+    for tti, dwpts in ((4, False), (6, True)):  # configuration 1: subframe 6 is special
+        m = PD.srsran_dci_msg_t()
+        m.payload[:size] = bits
+        m.nof_bits, m.format, m.rnti = size, F2, 0x4601
+        d = PD.srsran_dci_dl_t()
+        sf = _sf(tti, 1)
+        r = PD.lib().srsran_dci_msg_unpack_pdsch(ctypes.byref(c), ctypes.byref(sf), None, ctypes.byref(m),
+                                                 ctypes.byref(d))
+        assert r == 0 and d.raw[0] == mask and d.tpc_pucch == tpc and d.dai == dai and d.pid == pid and d.is_tdd
+        assert d.tb[0].mcs_idx == 17 and d.tb[1].mcs_idx == 9 and d.pinfo == 5
+        assert bool(d.is_dwpts) == dwpts

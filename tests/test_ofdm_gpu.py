@@ -16,7 +16,7 @@ pytestmark = pytest.mark.gpu
 # north_star: soft values within 1e-4.  The FFT has no pinned reference output, so its error is taken against
 # numpy's double-precision transform, relative to the largest bin; the measured figures are written to
 # $SRSRAN_AMD_FFT_STATS.
-FFT_TOL = 1e-4
+FFT_TOL = 1e-6  # measured <= 3.3e-7 (profiles/r05a_fft_stats.json); north_star asks 1e-4
 FFT_STATS = {}
 
 

@@ -129,3 +129,45 @@ def test_ldpc_tx_matches_oracle_encoder():
             got = ldpc_tx.encode(bg, ls, msgs)
             for m, g in zip(msgs, got):
                 assert np.array_equal(g, ora.encode(bg, ls, m)), (bg, ls)
+
+
+@pytest.mark.parametrize("cell_id", [0, 1, 2, 167, 301, 503])
+@pytest.mark.parametrize("sf", [0, 5])
+def test_sync_signals_match_reference(cell_id, sf):
+    """synth's PSS / SSS (36.211 6.11, written from the standard) equal the reference eNB's put_sync
+    (srsran_pss_generate / srsran_sss_generate / pss_put_slot / sss_put_slot through ref_enb_ctrl_harness.c) on the
+    PSS / SSS rows of subframes 0 and 5, including the 5 empty subcarriers either side"""
+    import oracle as ORA
+    if not ORA.ref_available():
+        pytest.skip("oracle/_ref not built")
+    import pdcch as OP
+    nof_prb = 25
+    ref = OP.Ref().enb_ctrl_tx(nof_prb, 1, cell_id, sf, 1, [], put_base=True)[0]
+    got = S.sync_grid(nof_prb, cell_id, sf)
+    lo, hi = 6 * nof_prb - 36, 6 * nof_prb + 36
+    np.testing.assert_array_equal(got[5, lo:hi], ref[5, lo:hi])  # SSS (normal CP): +-1
+    # PSS: the reference rounds the Zadoff-Chu phase argument (up to ~6600 rad) to float before cosf / sinf
+    # (pss.c:352-363), synth evaluates it in double: within 5e-4
+    np.testing.assert_allclose(got[6, lo:hi], ref[6, lo:hi], atol=5e-4)
+
+
+@pytest.mark.parametrize("sf_config", range(7))
+@pytest.mark.parametrize("ss_config", [0, 1, 4, 5, 9])
+def test_tdd_pdsch_re_set(sf_config, ss_config):
+    """synth's TDD PDSCH REs (36.211 rules: DwPTS only, SSS last symbol of 0 / 5, PSS symbol 2 of 1 / 6) equal the
+    oracle's rule-based RE walk with the grant's DwPTS symbols per slot, in every downlink and special subframe"""
+    for sf in range(10):
+        if pdsch_np.tdd_type(sf_config, sf) == "U":
+            continue
+        for nports, cfi, nof_prb in ((2, 1, 100), (1, 2, 50), (4, 2, 6)):
+            m = S.pdsch_mask(nof_prb, nports, 7, cfi, sf, tdd=(sf_config, ss_config))
+            lstart = cfi + (1 if nof_prb < 10 else 0)
+            nsl = pdsch_np.tdd_nof_symb_slot(sf_config, ss_config, sf)
+            ref = pdsch_np.re_table(nof_prb, nports, 7, np.ones((2, nof_prb), bool), lstart, sf, fdd=False, nsl=nsl)
+            # grid rows of slot 1 start at nsl[0] in the reference's walk; in the grid they start at row 7
+            got = np.flatnonzero(m.reshape(-1))
+            want = np.array([t[0] for t in ref], np.int64)
+            if nsl[0] == 7:
+                assert np.array_equal(got, want), (sf, nports)
+            else:  # DwPTS shorter than a slot: slot 1 empty, the rows coincide
+                assert nsl[1] == 0 and np.array_equal(got, want), (sf, nports)

@@ -171,8 +171,10 @@ int srsran_chest_dl_gpu_estimate_batch(srsran_chest_dl_t* q,
 /* added: the batch with an estimator configuration (srsran_chest_dl_estimate_cfg's options): AVERAGE or
  * INTERPOLATE (full_grid = 1 required: d_ce rows of 2 * nsymb * 12 * nof_prb), REFS / PSS / EMPTY noise (PSS /
  * EMPTY estimate in subframes 0 and 5, the other subframes keep the last estimate, across calls as the reference's
- * q->noise_estimate does), Gauss filters of order <= 7 or automatic with REFS noise.  cfg = NULL: srsUE's
- * defaults.  Not provided here: sync_error_enable (the host-synchronous srsran_chest_dl_estimate_cfg has it). */
+ * q->noise_estimate does), Gauss filters of order <= 7 or automatic (with PSS / EMPTY noise the batch runs in
+ * segments ending at subframes 0 / 5, whose estimate sets the later subframes' filter), and sync_error_enable
+ * (correct_sync_error: each subframe's grids are corrected in place before the estimate, as the reference corrects
+ * its input).  cfg = NULL: srsUE's defaults. */
 int srsran_chest_dl_gpu_estimate_batch_cfg(srsran_chest_dl_t*           q,
                                            const srsran_chest_dl_cfg_t* cfg,
                                            const uint32_t*              d_sf_idx,

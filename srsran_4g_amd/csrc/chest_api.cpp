@@ -49,6 +49,8 @@ struct ChestGpu {
   float2*     ce      = nullptr;
   float*      stats   = nullptr;  // [rx][port][8]
   float*      bstats  = nullptr;  // batch path: [sf][CHEST_STATS_PER_SF]
+  float*      bsync   = nullptr;  // batch path, sync correction: [sf][CHEST_SYNC_PER_SF] phase sums
+  float*      bserr   = nullptr;  // batch path, sync correction: [sf][rx * 4 + port] sync errors
   uint32_t    bstats_cap = 0;
   uint32_t    max_prb = 0;
   uint32_t    nrx     = 0;
@@ -121,9 +123,8 @@ void pss_generate(uint32_t N_id_2, float2* sig)
   }
 }
 
-// the estimator options a call may use (chest_dl.c:655-745); batch: no sync correction, no automatic filter
-// with the PSS / EMPTY noise (its input would be the previous subframe's estimate)
-bool cfg_supported(const srsran_chest_dl_cfg_t* cfg, bool batch)
+// the estimator options a call may use (chest_dl.c:655-745), the host-synchronous and the batch estimators alike
+bool cfg_supported(const srsran_chest_dl_cfg_t* cfg)
 {
   if (!cfg) {
     return true;
@@ -131,11 +132,8 @@ bool cfg_supported(const srsran_chest_dl_cfg_t* cfg, bool batch)
   const bool est   = cfg->estimator_alg == SRSRAN_ESTIMATOR_ALG_AVERAGE || cfg->estimator_alg == SRSRAN_ESTIMATOR_ALG_INTERPOLATE;
   const bool noise = cfg->noise_alg == SRSRAN_NOISE_ALG_REFS || cfg->noise_alg == SRSRAN_NOISE_ALG_PSS ||
                      cfg->noise_alg == SRSRAN_NOISE_ALG_EMPTY;
-  if (!est || !noise || cfg->filter_type != SRSRAN_CHEST_FILTER_GAUSS || cfg->rsrp_neighbour || cfg->filter_coef[0] > 7) {
-    return false;
-  }
-  return !batch || (!cfg->sync_error_enable &&
-                    (cfg->filter_coef[0] > 0 || cfg->noise_alg == SRSRAN_NOISE_ALG_REFS));
+  return est && noise && cfg->filter_type == SRSRAN_CHEST_FILTER_GAUSS && !cfg->rsrp_neighbour &&
+         cfg->filter_coef[0] <= 7;
 }
 
 constexpr size_t kPilotsPerSf = 2 * 4 * CHEST_MAX_NREF;  // float2 per subframe (both port pairs)
@@ -315,6 +313,8 @@ void srsran_chest_dl_free(srsran_chest_dl_t* q)
     hipFree(g->ce);
     hipFree(g->stats);
     hipFree(g->bstats);
+    hipFree(g->bsync);
+    hipFree(g->bserr);
     hipFree(g->pss);
     hipFree(g->noise);
     hipFree(g->sync);
@@ -568,7 +568,7 @@ int srsran_chest_dl_estimate_cfg(srsran_chest_dl_t*     q,
   if (!q || !q->gpu || !sf || !cfg || !input || !res || q->cell.nof_prb == 0) {
     return SRSRAN_ERROR_INVALID_INPUTS;
   }
-  if (sf->sf_type != SRSRAN_SF_NORM || !cfg_supported(cfg, false)) {
+  if (sf->sf_type != SRSRAN_SF_NORM || !cfg_supported(cfg)) {
     fprintf(stderr, "[srsran_chest_dl] MBSFN subframes, the WIENER estimator, TRIANGLE / NONE filters, filter orders "
                     "above 7 and rsrp_neighbour are not provided\n");
     return SRSRAN_ERROR;
@@ -688,9 +688,9 @@ bool chest_batch_cfg_supported(const srsran_chest_dl_t* q, const srsran_chest_dl
                     "CP) is not provided\n");
     return false;
   }
-  if (!cfg_supported(cfg, true) || (cfg && cfg->estimator_alg == SRSRAN_ESTIMATOR_ALG_INTERPOLATE && !full_grid)) {
-    fprintf(stderr, "[srsran_chest_dl] batch: configuration not provided (sync correction, automatic filter with "
-                    "PSS / EMPTY noise, or INTERPOLATE without full grids)\n");
+  if (!cfg_supported(cfg) || (cfg && cfg->estimator_alg == SRSRAN_ESTIMATOR_ALG_INTERPOLATE && !full_grid)) {
+    fprintf(stderr, "[srsran_chest_dl] batch: configuration not provided (WIENER, TRIANGLE / NONE filters, filter "
+                    "orders above 7, rsrp_neighbour, or INTERPOLATE without full grids)\n");
     return false;
   }
   return true;
@@ -725,9 +725,13 @@ int estimate_batch(srsran_chest_dl_t*           q,
   if (nsf > g->bstats_cap) {
     hipStreamSynchronize((hipStream_t)stream);  // the previous batch may still use them
     hipFree(g->bstats);
-    g->bstats     = nullptr;
+    hipFree(g->bsync);
+    hipFree(g->bserr);
+    g->bstats = g->bsync = g->bserr = nullptr;
     g->bstats_cap = 0;
-    if (hipMalloc((void**)&g->bstats, nsf * CHEST_STATS_PER_SF * sizeof(float)) != hipSuccess) {
+    if (hipMalloc((void**)&g->bstats, nsf * CHEST_STATS_PER_SF * sizeof(float)) != hipSuccess ||
+        hipMalloc((void**)&g->bsync, nsf * CHEST_SYNC_PER_SF * sizeof(float)) != hipSuccess ||
+        hipMalloc((void**)&g->bserr, nsf * 16 * sizeof(float)) != hipSuccess) {
       return SRSRAN_ERROR;
     }
     g->bstats_cap = nsf;
@@ -771,6 +775,13 @@ int estimate_batch(srsran_chest_dl_t*           q,
     a.noise_alg = (uint32_t)cfg->noise_alg;
   }
   const float sz = (float)srsran_symbol_sz(q->cell.nof_prb);
+  if (cfg && cfg->sync_error_enable) {  // correct_sync_error on every subframe's grids first, in place (the reference
+    // corrects its input buffer, chest_dl.c:795-803)
+    if (chest_sync_sums_launch(a, g->bsync, s, nsf) != hipSuccess ||
+        chest_sync_apply_launch(a, g->bsync, g->bserr, (float2*)d_grid, sz, nsf, s) != hipSuccess) {
+      return SRSRAN_ERROR;
+    }
+  }
   if (a.noise_alg == 0) {  // REFS: the stats reduced by a small second launch (an in-kernel last-workgroup
     // reduction needed device-scope fences, whose L2 write-backs cost more than the launch: r04p stamps)
     return chest_launch(a, s, nsf) == hipSuccess &&
@@ -779,10 +790,43 @@ int estimate_batch(srsran_chest_dl_t*           q,
                ? SRSRAN_SUCCESS
                : SRSRAN_ERROR;
   }
-  if (chest_launch(a, s, nsf) != hipSuccess ||
-      chest_finalize_kept_launch(g->bstats, q->cell.nof_ports, q->nof_rx_antennas, q->cell.nof_prb, sz, a.nsymb,
-                                 g->noise, d_res, nsf, s) != hipSuccess) {
-    return SRSRAN_ERROR;
+  if (!a.filter_auto) {  // PSS / EMPTY with a fixed filter: the kept estimates carried in one pass after the launch
+    if (chest_launch(a, s, nsf) != hipSuccess ||
+        chest_finalize_kept_launch(g->bstats, q->cell.nof_ports, q->nof_rx_antennas, q->cell.nof_prb, sz, a.nsymb,
+                                   g->noise, d_res, nsf, s) != hipSuccess) {
+      return SRSRAN_ERROR;
+    }
+    return SRSRAN_SUCCESS;
+  }
+  // PSS / EMPTY with the automatic filter: a subframe's filter width comes from the estimate kept after the last
+  // subframe 0 / 5 before it (chest_dl.c:703-707, 731-745), so the batch runs in segments that each end at a subframe
+  // 0 / 5 -- every subframe of a segment filters with the state from before it, whose last subframe then renews it
+  // (with device-side subframe indices the host cannot see where they fall: one subframe a segment)
+  for (uint32_t start = 0; start < nsf;) {
+    uint32_t n = 1;
+    if (h_sf) {
+      while (start + n - 1 < nsf - 1 && h_sf[start + n - 1] != 0 && h_sf[start + n - 1] != 5) {
+        n++;
+      }
+    }
+    ChestArgs sa = a;
+    sa.grid      = a.grid + start * grid_sf_stride;
+    sa.ce        = a.ce + start * ce_sf_stride;
+    sa.stats     = g->bstats + (size_t)start * CHEST_STATS_PER_SF;
+    if (h_sf) {
+      memcpy(sa.sf_inline, h_sf + start, n);
+    } else {
+      sa.sf_idx = d_sf_idx + start;
+    }
+    if (start > 0) {
+      sa.jobs.n = 0;  // the staging copies ride in the first launch only
+    }
+    if (chest_launch(sa, s, n) != hipSuccess ||
+        chest_finalize_kept_launch(sa.stats, q->cell.nof_ports, q->nof_rx_antennas, q->cell.nof_prb, sz, a.nsymb,
+                                   g->noise, d_res + 4 * start, n, s) != hipSuccess) {
+      return SRSRAN_ERROR;
+    }
+    start += n;
   }
   return SRSRAN_SUCCESS;
 }

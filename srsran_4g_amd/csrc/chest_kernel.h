@@ -78,7 +78,13 @@ hipError_t chest_finalize_kept_launch(float* stats, uint32_t np, uint32_t nrx, u
 // correct_sync_error (chest_dl.c:750-804), device side of the host-synchronous path: per (rx, port) the LS
 // estimates' per-CRS-symbol phase sums sum(x[i] conj(x[i-1])) and their power sum -> out[(rx * 4 + port) * 10 ..]:
 // 4 complex sums, then the power sum (the host finishes with the reference's scalar arithmetic)
-hipError_t chest_sync_sums_launch(const ChestArgs& a, float* out, hipStream_t stream);
+hipError_t chest_sync_sums_launch(const ChestArgs& a, float* out, hipStream_t stream, uint32_t nsf = 1);
+static constexpr size_t CHEST_SYNC_PER_SF = 4 * 4 * 10;  // floats of phase sums per subframe
+// the batch's correction (chest_dl.c:750-804): per (rx, subframe) the reference's arithmetic on the sums of
+// chest_sync_sums_launch, the sync error of every (rx, port) into serr[b][rx * 4 + port], and where |error| > 0.05
+// samples every row of that rx grid (grid + b * a.grid_sf_stride) rotated in place by srsran_vec_apply_cfo's phasors
+hipError_t chest_sync_apply_launch(const ChestArgs& a, const float* sums, float* serr, float2* grid, float symbol_sz,
+                                   uint32_t nsf, hipStream_t stream);
 // rows (2 nsymb of every rx grid) multiplied in place by the phasor table tab[nre] (srsran_vec_apply_cfo per row)
 hipError_t grid_rotate_launch(float2* grid, const float2* tab, uint32_t nre, uint32_t nrows, hipStream_t stream);
 

@@ -531,15 +531,18 @@ hipError_t chest_finalize_kept_launch(float* stats, uint32_t np, uint32_t nrx, u
   return chest_finalize_launch(stats, np, nrx, nof_prb, symbol_sz, nsymb, out, nsf, stream);
 }
 
-// correct_sync_error's device part: one workgroup per (port, rx)
+// correct_sync_error's device part: one workgroup per (port, rx) and subframe (blockIdx.y; batches: the subframe
+// indices as chest_kernel takes them)
 __global__ __launch_bounds__(CH_THREADS) void chest_sync_kernel(ChestArgs a, float* out)
 {
   __shared__ float red[CH_THREADS / 64];
-  const uint32_t   port = blockIdx.x / a.nrx, rx = blockIdx.x % a.nrx;
-  const uint32_t   nsym = chest_crs_nsym(a, a.sf_index, port), nref = 2 * a.nof_prb, nre = 12 * a.nof_prb;
-  const float2*    in   = a.grid + (size_t)rx * 2 * a.nsymb * nre;
-  const float2*    pil  = a.pilots + (size_t)(port / 2) * 4 * CHEST_MAX_NREF;
-  float*           o    = out + (rx * 4 + port) * 10;
+  const uint32_t   port = blockIdx.x / a.nrx, rx = blockIdx.x % a.nrx, b = blockIdx.y;
+  const bool       bat  = a.sf_inl || a.sf_idx;
+  const uint32_t   sfi  = a.sf_inl ? (uint32_t)a.sf_inline[b] : a.sf_idx ? a.sf_idx[b] : a.sf_index;
+  const uint32_t   nsym = chest_crs_nsym(a, sfi, port), nref = 2 * a.nof_prb, nre = 12 * a.nof_prb;
+  const float2*    in   = a.grid + b * a.grid_sf_stride + (size_t)rx * 2 * a.nsymb * nre;
+  const float2*    pil  = a.pilots + (bat ? sfi * CHEST_PILOTS_PER_SF : 0) + (size_t)(port / 2) * 4 * CHEST_MAX_NREF;
+  float*           o    = out + (size_t)b * CHEST_SYNC_PER_SF + (rx * 4 + port) * 10;
   float            pwr  = 0.f;
   for (uint32_t l = 0; l < nsym; l++) {
     const uint32_t row = crs_nsymbol(l, port, a.nsymb) * nre, f0 = (crs_v(port, l) + a.cell_id % 6) % 6;
@@ -567,9 +570,103 @@ __global__ __launch_bounds__(CH_THREADS) void chest_sync_kernel(ChestArgs a, flo
   }
 }
 
-hipError_t chest_sync_sums_launch(const ChestArgs& a, float* out, hipStream_t stream)
+hipError_t chest_sync_sums_launch(const ChestArgs& a, float* out, hipStream_t stream, uint32_t nsf)
 {
-  hipLaunchKernelGGL(chest_sync_kernel, dim3(a.nports * a.nrx), dim3(CH_THREADS), 0, stream, a, out);
+  if (nsf == 0) {
+    return hipSuccess;
+  }
+  hipLaunchKernelGGL(chest_sync_kernel, dim3(a.nports * a.nrx, nsf), dim3(CH_THREADS), 0, stream, a, out);
+  return hipGetLastError();
+}
+
+// srsran_vec_apply_cfo's complex product (simd.h:898-901, AVX2 + FMA build)
+__device__ __forceinline__ float2 cfo_prod(float2 x, float2 p)
+{
+  return make_float2(__fmaf_rn(x.x, p.x, -__fmul_rn(x.y, p.y)), __fmaf_rn(x.x, p.y, __fmul_rn(x.y, p.x)));
+}
+
+// correct_sync_error of a batch (chest_dl.c:750-804), one workgroup per (rx, subframe): the reference's scalar
+// arithmetic on the phase sums of chest_sync_kernel (thread 0), then -- where the error exceeds 0.05 samples -- the
+// phasor table of srsran_vec_apply_cfo (8 lanes carry the SIMD phases, lane 0 the tail) in LDS and every row of the
+// rx grid rotated in place.  The phasor's sincosf / the phase atan2f are the device's (the host-synchronous path
+// uses the host's libm), so corrected grids can differ from it in the last bit of a rotated sample.
+__global__ __launch_bounds__(CH_THREADS) void chest_sync_apply_kernel(ChestArgs a, const float* __restrict__ sums,
+                                                                      float* __restrict__ serr, float2* grid, float sz)
+{
+  __shared__ float2 tab[12 * CHEST_MAX_PRB];
+  __shared__ float2 w_sh;
+  __shared__ int    rot_sh;
+  const uint32_t rx = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const uint32_t sfi = a.sf_inl ? (uint32_t)a.sf_inline[b] : a.sf_idx ? a.sf_idx[b] : a.sf_index;
+  const uint32_t nre = 12 * a.nof_prb, rows = 2 * a.nsymb;
+  if (tid == 0) {
+    float pwr_sum = 0.0f, err = 0.0f;
+    for (uint32_t port = 0; port < a.nports; port++) {
+      const float*   o    = sums + (size_t)b * CHEST_SYNC_PER_SF + (rx * 4 + port) * 10;
+      const uint32_t nsym = chest_crs_nsym(a, sfi, port), npilots = nsym * 2 * a.nof_prb;
+      const float    k    = sz / 6.0f;
+      float          sum  = 0.0f;
+      for (uint32_t l = 0; l < nsym; l++) {  // srsran_vec_estimate_frequency: -cargf(sum) * M_1_PI * 0.5f
+        const float f = (float)((double)-atan2f(o[2 * l + 1], o[2 * l]) * 0.31830988618379067154 * 0.5f);
+        sum += f * k;
+      }
+      const float pwr = o[8] / (float)npilots;
+      const float se  = sum / (float)nsym;
+      serr[(size_t)b * 16 + rx * 4 + port] = se;
+      if (!isinf(sum) && !isnan(sum) && !isinf(pwr) && !isnan(pwr)) {
+        err += se * pwr;
+        pwr_sum += pwr;
+      }
+    }
+    if (isnormal(pwr_sum)) {
+      err /= pwr_sum;
+    }
+    rot_sh = isnormal(err) && fabsf(err) > 0.05f;
+    float c, s;
+    sincosf((2.0f * 3.14159265358979323846f) * (err / sz), &s, &c);  // cfo_phasor of err / symbol size
+    w_sh = make_float2(c, s);
+  }
+  __syncthreads();
+  if (!rot_sh) {
+    return;
+  }
+  if (tid < 8) {  // srsran_vec_apply_cfo's phasors over nre samples (as cfo_table_kernel)
+    const float2 w = w_sh;
+    float2       p = make_float2(1.0f, 0.0f);
+    for (uint32_t j = 0; j < tid; j++) {
+      p = cfo_prod(p, w);
+    }
+    float2 w8 = make_float2(1.0f, 0.0f);
+    for (uint32_t j = 0; j < 8; j++) {
+      w8 = cfo_prod(w8, w);
+    }
+    const uint32_t nblk = nre / 8;
+    for (uint32_t m = 0; m < nblk; m++) {
+      tab[8 * m + tid] = p;
+      p                = cfo_prod(p, w8);
+    }
+    if (tid == 0) {
+      for (uint32_t i = 8 * nblk; i < nre; i++) {
+        tab[i] = p;
+        p      = cfo_prod(p, w);
+      }
+    }
+  }
+  __syncthreads();
+  float2* g = grid + b * a.grid_sf_stride + (size_t)rx * rows * nre;
+  for (uint32_t i = tid; i < rows * nre; i += CH_THREADS) {
+    g[i] = cfo_prod(g[i], tab[i % nre]);
+  }
+}
+
+hipError_t chest_sync_apply_launch(const ChestArgs& a, const float* sums, float* serr, float2* grid, float symbol_sz,
+                                   uint32_t nsf, hipStream_t stream)
+{
+  if (nsf == 0) {
+    return hipSuccess;
+  }
+  hipLaunchKernelGGL(chest_sync_apply_kernel, dim3(a.nrx, nsf), dim3(CH_THREADS), 0, stream, a, sums, serr, grid,
+                     symbol_sz);
   return hipGetLastError();
 }
 

@@ -384,7 +384,7 @@ def pcfich_grids(nof_prb, cell_id, nports, sf_idx, cfi, cp=0):
 
 def pdsch_subframe(nof_prb, cell_id, nports, tti, cfi, rnti, tbs, Qm, rv, payloads, scheme="cdd", codebook=1,
                    nrx=2, snr_db=None, rng=None, N=None, channel=None, cfo=0.0, pcfich=True, ctrl=None, cp=0,
-                   sync=False, tdd=None):
+                   sync=False, tdd=None, delay=0.0):
     """One PDSCH subframe through OFDM and a static MIMO channel.
 
     payloads: one uint8 array (tbs/8 bytes) per codeword.  channel: (nrx, nports) complex matrix
@@ -392,7 +392,8 @@ def pdsch_subframe(nof_prb, cell_id, nports, tti, cfi, rnti, tbs, Qm, rv, payloa
     pcfich: also transmit the PCFICH of `cfi`; ctrl: optional per-port (14, 12 N_RB) grids added
     before the OFDM modulator (e.g. a PDCCH control region); cp=1: extended cyclic prefix;
     sync: also transmit the PSS / SSS (every port, as the reference eNB); tdd = (sf_config, ss_config): a TDD cell
-    (TDD sync-signal positions; a special subframe transmits its DwPTS symbols only).
+    (TDD sync-signal positions; a special subframe transmits its DwPTS symbols only); delay: a timing error of that
+    many samples (fractional), as a phase ramp over the subcarriers of every symbol.
     Returns (samples[nrx, sf_len] complex64, nof_re)."""
     N = N or symbol_sz(nof_prb)
     sf_idx = tti % 10
@@ -424,6 +425,10 @@ def pdsch_subframe(nof_prb, cell_id, nports, tti, cfi, rnti, tbs, Qm, rv, payloa
             g = g + sg
         if nsymb_tx is not None:
             g[nsymb_tx:] = 0  # GP / UpPTS
+        if delay:
+            half = g.shape[1] // 2
+            kf = np.concatenate([np.arange(-half, 0), np.arange(1, half + 1)])  # subcarrier frequencies (no DC)
+            g = g * np.exp(-2j * np.pi * kf * delay / N)[None, :]
         tx.append(ofdm_tx(g, N, cp))
     H4 = [[1, 0.5j, -0.4, 0.3], [0.3, -0.6j, 1, 0.5]]
     H = np.asarray(channel if channel is not None else

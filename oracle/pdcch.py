@@ -224,3 +224,79 @@ def dci_pack_2a(nof_prb, size, rbg_mask, tbs, pid, swap=0, tpc=0, pinfo=None, pi
     if pinfo_bits:
         b += _bits(pinfo or 0, pinfo_bits)
     return np.array(b + [0] * (size - len(b)), np.uint8)
+
+
+# ---- DL resource allocation type 2 (TEST INFRASTRUCTURE): ra_dl.c:225-316 and ra.c:81-124 restated ----
+def type2_ngap(nof_prb, ngap1):
+    """36.211 Table 6.2.3.2-1 (ra.c:81-103)"""
+    if nof_prb <= 10:
+        return nof_prb // 2
+    if nof_prb == 11:
+        return 4
+    for lim, g in ((19, 8), (26, 12), (44, 18), (49, 27)):
+        if nof_prb <= lim:
+            return g
+    if nof_prb <= 63:
+        return 27 if ngap1 else 9
+    if nof_prb <= 79:
+        return 32 if ngap1 else 16
+    return 48 if ngap1 else 16
+
+
+def type2_n_vrb_dl(nof_prb, ngap1):
+    """N_VRB^DL (36.211 6.2.3.2; ra.c:115-124)"""
+    g = type2_ngap(nof_prb, ngap1)
+    return 2 * min(g, nof_prb - g) if ngap1 else (nof_prb // g) * 2 * g
+
+
+def riv_decode(riv_v, nof_prb, nof_vrb):
+    """srsran_ra_type2_from_riv (ra.c:49-57): (L_crb, RB_start).  Its test L > nof_vrb - RB_start is unsigned: with
+    RB_start > nof_vrb (distributed allocations, N_VRB < N_PRB) it wraps and the RIV is not flipped."""
+    L, start = riv_v // nof_prb + 1, riv_v % nof_prb
+    if L > (nof_vrb - start) % (1 << 32):
+        L, start = nof_prb - riv_v // nof_prb + 1, nof_prb - riv_v % nof_prb - 1
+    return L, start
+
+
+def type2_prbs(nof_prb, riv_v, distributed, ngap1=True, fmt1c=False):
+    """PRBs of a type 2 allocation per slot: ([slot 0 PRBs], [slot 1 PRBs]) or None where the reference refuses.
+    Distributed VRBs by 36.211 6.2.3.2's interleaver, with the reference's N~_VRB for N_gap,2: it takes
+    2 x N_VRB(N_gap,1) (ra_dl.c:257-260) where 36.211 has 2 N_gap."""
+    P = type0_P(nof_prb)
+    nof_vrb = type2_n_vrb_dl(nof_prb, ngap1) if distributed else nof_prb
+    nof_prb_t2, step = nof_prb, 1
+    if fmt1c:
+        step = 2 if nof_prb < 50 else 4
+        nof_vrb //= step
+        nof_prb_t2 = nof_vrb
+    L, start = riv_decode(riv_v, nof_prb_t2, nof_vrb)
+    L, start = L * step, start * step
+    if not distributed:
+        prbs = list(range(start, start + L))
+        return prbs, prbs
+    nt = type2_n_vrb_dl(nof_prb, True) * (1 if ngap1 else 2)
+    gap = type2_ngap(nof_prb, ngap1)
+    n_row = -(-nt // (4 * P)) * P
+    n_null = 4 * n_row - nt
+    s0, s1 = [], []
+    for n_vrb in range(start, start + L):
+        v, blk = n_vrb % nt, nt * (n_vrb // nt)
+        p1 = 2 * n_row * (v % 2) + v // 2 + blk
+        p2 = n_row * (v % 4) + v // 4 + blk
+        if n_null and v >= nt - n_null:
+            ev = p1 - n_row if v % 2 == 1 else p1 - n_row + n_null // 2
+        elif n_null and v % 4 >= 2:
+            ev = p2 - n_null // 2
+        else:
+            ev = p2
+        od = (ev + nt // 2) % nt + blk
+        for n_t, out in ((ev, s0), (od, s1)):
+            prb = n_t if n_t < nt // 2 else n_t + gap - nt // 2
+            if not 0 <= prb < nof_prb:
+                return None
+            out.append(prb)
+    return s0, s1
+
+
+TBS_FORMAT1C = (40, 56, 72, 120, 136, 144, 176, 208, 224, 256, 280, 296, 328, 336, 392, 488, 552, 600, 632, 696, 776,
+                840, 904, 1000, 1064, 1128, 1224, 1288, 1384, 1480, 1608, 1736)  # 36.213 Table 7.1.7.2.3-1

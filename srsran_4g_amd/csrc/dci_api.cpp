@@ -11,7 +11,7 @@
 //                  phch/ra_dl.c:42-681 (PRB allocation types 0 / 1 / 2, TB sizes, RE count, MIMO)
 // TDD: 4-bit HARQ process numbers and the DAI / UL index (the reference's packers write no DAI: it stays in the zero
 // padding, while its unpackers read it -- restated as is, dci.c:415-1367).
-// Not provided (SRSRAN_ERROR): format 1B / 1C / 1D / 2B unpacking, 1B / 1D packing, distributed VRBs.
+// Not provided (SRSRAN_ERROR): format 1B / 1D / 2B unpacking, 1B / 1D packing.
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -351,6 +351,28 @@ int unpack_format1A(const srsran_cell_t* cell, srsran_dci_cfg_t* cfg, srsran_dci
     dci->dai    = bit_pack(&y, 2);
     dci->is_tdd = true;
   }
+  return SRSRAN_SUCCESS;
+}
+
+int unpack_format1C(const srsran_cell_t* cell, srsran_dl_sf_cfg_t* sf, srsran_dci_cfg_t* cfg, srsran_dci_msg_t* msg,
+                    srsran_dci_dl_t* dci)  // dci.c:990-1023
+{
+  if (msg->nof_bits != srsran_dci_format_sizeof(cell, sf, cfg, SRSRAN_DCI_FORMAT1C)) {
+    return SRSRAN_ERROR;
+  }
+  const uint8_t* y       = msg->payload;
+  dci->alloc_type        = SRSRAN_RA_ALLOC_TYPE2;
+  dci->type2_alloc.mode  = srsran_ra_type2_t::SRSRAN_RA_TYPE2_DIST;
+  if (cell->nof_prb >= 50) {
+    dci->type2_alloc.n_gap = *y++ ? srsran_ra_type2_t::SRSRAN_RA_TYPE2_NG2 : srsran_ra_type2_t::SRSRAN_RA_TYPE2_NG1;
+  }
+  const uint32_t n_step   = cell->nof_prb < 50 ? 2 : 4;
+  const uint32_t n_vrb_dl =
+      ra_type2_n_vrb_dl(cell->nof_prb, dci->type2_alloc.n_gap == srsran_ra_type2_t::SRSRAN_RA_TYPE2_NG1);
+  dci->type2_alloc.riv = bit_pack(&y, riv_nbits(n_vrb_dl / n_step));
+  dci->tb[0].mcs_idx   = bit_pack(&y, 5);
+  dci->tb[0].rv        = -1;  // from the SFN / subframe, by the caller (36.321 5.3.1)
+  msg->nof_bits        = (uint32_t)(y - msg->payload);
   return SRSRAN_SUCCESS;
 }
 
@@ -722,21 +744,60 @@ int prb_allocation(const srsran_dci_dl_t* dci, srsran_pdsch_grant_t* grant, uint
       }
       break;
     }
-    case SRSRAN_RA_ALLOC_TYPE2: {
-      if (dci->type2_alloc.mode != srsran_ra_type2_t::SRSRAN_RA_TYPE2_LOC || dci->format == SRSRAN_DCI_FORMAT1C) {
-        fprintf(stderr, "[srsran_ra] distributed VRB / format 1C allocations are not provided\n");
-        return SRSRAN_ERROR;
+    case SRSRAN_RA_ALLOC_TYPE2: {  // ra_dl.c:225-316
+      const bool dist = dci->type2_alloc.mode != srsran_ra_type2_t::SRSRAN_RA_TYPE2_LOC;
+      const bool ng1  = dci->type2_alloc.n_gap == srsran_ra_type2_t::SRSRAN_RA_TYPE2_NG1;
+      uint32_t   nof_vrb = dist ? ra_type2_n_vrb_dl(nof_prb, ng1) : nof_prb, nof_prb_t2 = nof_prb, n_step = 1;
+      if (dci->format == SRSRAN_DCI_FORMAT1C) {  // 36.213 7.1.6.3: RIV in units of N_RB^step
+        n_step = nof_prb < 50 ? 2 : 4;
+        nof_vrb /= n_step;
+        nof_prb_t2 = nof_vrb;
       }
       uint32_t L_crb = 0, RB_start = 0;
-      srsran_ra_type2_from_riv(dci->type2_alloc.riv, &L_crb, &RB_start, nof_prb, nof_prb);
-      for (uint32_t i = 0; i < L_crb; i++) {
-        if (i + RB_start >= SRSRAN_MAX_PRB) {
+      srsran_ra_type2_from_riv(dci->type2_alloc.riv, &L_crb, &RB_start, nof_prb_t2, nof_vrb);
+      L_crb *= n_step;
+      RB_start *= n_step;
+      if (!dist) {
+        for (uint32_t i = 0; i < L_crb; i++) {
+          if (i + RB_start >= SRSRAN_MAX_PRB) {
+            return SRSRAN_ERROR;
+          }
+          grant->prb_idx[0][i + RB_start] = true;
+          grant->nof_prb++;
+        }
+        memcpy(grant->prb_idx[1], grant->prb_idx[0], sizeof(grant->prb_idx[0]));
+        return SRSRAN_SUCCESS;
+      }
+      // distributed VRBs: the interleaver of 36.211 6.2.3.2, even slot (prb_idx[0]) and odd slot (prb_idx[1])
+      const int N_vrb = ng1 ? (int)ra_type2_n_vrb_dl(nof_prb, true) : 2 * (int)ra_type2_n_vrb_dl(nof_prb, true);
+      const int N_gap = (int)ra_type2_ngap(nof_prb, ng1);
+      const int N_row = (int)ceilf((float)N_vrb / (4 * P)) * (int)P;
+      const int N_null = 4 * N_row - N_vrb;
+      for (int i = 0; i < (int)L_crb; i++) {
+        const int n_vrb = i + (int)RB_start, nt_vrb = n_vrb % N_vrb, blk = N_vrb * (n_vrb / N_vrb);
+        const int nt_prb  = 2 * N_row * (nt_vrb % 2) + nt_vrb / 2 + blk;
+        const int nt2_prb = N_row * (nt_vrb % 4) + nt_vrb / 4 + blk;
+        int       odd;
+        if (N_null != 0 && nt_vrb >= N_vrb - N_null && nt_vrb % 2 == 1) {
+          odd = nt_prb - N_row;
+        } else if (N_null != 0 && nt_vrb >= N_vrb - N_null && nt_vrb % 2 == 0) {
+          odd = nt_prb - N_row + N_null / 2;
+        } else if (N_null != 0 && nt_vrb < N_vrb - N_null && nt_vrb % 4 >= 2) {
+          odd = nt2_prb - N_null / 2;
+        } else {
+          odd = nt2_prb;
+        }
+        const int even = (odd + N_vrb / 2) % N_vrb + blk;
+        const int p0 = odd < N_vrb / 2 ? odd : odd + N_gap - N_vrb / 2;
+        const int p1 = even < N_vrb / 2 ? even : even + N_gap - N_vrb / 2;
+        if (p0 < 0 || p0 >= (int)nof_prb || p1 < 0 || p1 >= (int)nof_prb) {
           return SRSRAN_ERROR;
         }
-        grant->prb_idx[0][i + RB_start] = true;
+        grant->prb_idx[0][p0] = true;
+        grant->prb_idx[1][p1] = true;
         grant->nof_prb++;
       }
-      break;
+      return SRSRAN_SUCCESS;
     }
     default:
       return SRSRAN_ERROR;
@@ -762,13 +823,21 @@ int compute_tb(bool alt, const srsran_dci_dl_t* dci, srsran_pdsch_grant_t* grant
   if (dci->format == SRSRAN_DCI_FORMAT1A || !SRSRAN_RNTI_ISUSER(dci->rnti)) {
     alt = false;
   }
-  if (!SRSRAN_RNTI_ISUSER(dci->rnti) && dci->rnti != SRSRAN_MRNTI) {
-    if (dci->format != SRSRAN_DCI_FORMAT1A) {
-      fprintf(stderr, "[srsran_ra] P/SI/RA-RNTI grants: format 1A only\n");
+  if (!SRSRAN_RNTI_ISUSER(dci->rnti) && dci->rnti != SRSRAN_MRNTI) {  // ra_dl.c:374-399
+    int tbs = -1;
+    if (dci->format == SRSRAN_DCI_FORMAT1A) {
+      const uint32_t n_prb = dci->type2_alloc.n_prb1a == srsran_ra_type2_t::SRSRAN_RA_TYPE2_NPRB1A_2 ? 2 : 3;
+      tbs                  = srsran_ra_tbs_from_idx(dci->tb[0].mcs_idx, n_prb);
+    } else if (dci->format == SRSRAN_DCI_FORMAT1C) {  // 36.213 Table 7.1.7.2.3-1
+      static const int kTbs1C[32] = {40,  56,  72,  120, 136, 144, 176, 208,  224,  256,  280,  296,  328,  336,  392,  488,
+                                     552, 600, 632, 696, 776, 840, 904, 1000, 1064, 1128, 1224, 1288, 1384, 1480, 1608, 1736};
+      if (dci->tb[0].mcs_idx < 32) {
+        tbs = kTbs1C[dci->tb[0].mcs_idx];
+      }
+    } else {
+      fprintf(stderr, "[srsran_ra] P/SI/RA-RNTI grants: formats 1A / 1C only\n");
       return SRSRAN_ERROR;
     }
-    const uint32_t n_prb = dci->type2_alloc.n_prb1a == srsran_ra_type2_t::SRSRAN_RA_TYPE2_NPRB1A_2 ? 2 : 3;
-    const int      tbs   = srsran_ra_tbs_from_idx(dci->tb[0].mcs_idx, n_prb);
     if (tbs < 0) {
       return SRSRAN_ERROR;
     }
@@ -1020,6 +1089,8 @@ int srsran_dci_msg_unpack_pdsch(srsran_cell_t* cell, srsran_dl_sf_cfg_t* sf, srs
       return unpack_format1(cell, sf, cfg, msg, dci);
     case SRSRAN_DCI_FORMAT1A:
       return unpack_format1A(cell, cfg, msg, dci);
+    case SRSRAN_DCI_FORMAT1C:
+      return unpack_format1C(cell, sf, cfg, msg, dci);
     case SRSRAN_DCI_FORMAT2:
     case SRSRAN_DCI_FORMAT2A:
       return unpack_format2x(cell, cfg, msg, dci);

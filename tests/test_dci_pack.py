@@ -348,3 +348,69 @@ def test_tdd_format2_dai_before_pid():
         assert r == 0 and d.raw[0] == mask and d.tpc_pucch == tpc and d.dai == dai and d.pid == pid and d.is_tdd
         assert d.tb[0].mcs_idx == 17 and d.tb[1].mcs_idx == 9 and d.pinfo == 5
         assert bool(d.is_dwpts) == dwpts
+
+
+def _grant(c, d, tti=1, cfi=1, tm=0):
+    return PD.dci_to_grant(c, d, tti, cfi, tm)
+
+
+@pytest.mark.parametrize("nprb", [6, 15, 25, 27, 50, 75, 100])
+def test_distributed_vrb_grants(nprb):
+    """type 2 distributed VRB allocations (format 1A with a C-RNTI, every RIV; N_gap,1 and, from 50 PRB, N_gap,2):
+    srsran_ra_dl_dci_to_grant's per-slot PRBs equal the restatement of the reference's interleaver (ra_dl.c:225-316,
+    36.211 6.2.3.2) in oracle/pdcch.py; where the reference refuses an allocation (a PRB beyond the cell) so does this"""
+    c = _cell(nprb)
+    for ngap1 in ((True,) if nprb < 50 else (True, False)):
+        nvrb = OP.type2_n_vrb_dl(nprb, ngap1)
+        for riv_v in range(0, nprb * (nprb + 1) // 2):
+            L, st = OP.riv_decode(riv_v, nprb, nvrb)
+            if L < 1 or st + L > nvrb:
+                continue
+            d = _dl(0x4601, F1A)
+            _type2(d, riv_v, DIST, 0 if ngap1 else 1)
+            d.tb[0].mcs_idx = 9
+            r, g = _grant(c, d)
+            want = OP.type2_prbs(nprb, riv_v, True, ngap1)
+            if want is None:
+                assert r != 0, riv_v
+                continue
+            assert r == 0, riv_v
+            for s in range(2):
+                assert [n for n in range(nprb) if g.prb_idx[s][n]] == sorted(want[s]), (riv_v, s)
+            assert g.nof_prb == L
+
+
+@pytest.mark.parametrize("nprb", [6, 15, 25, 50, 75, 100])
+def test_format1C_si_rnti(nprb):
+    """format 1C (SI / P / RA-RNTI): pack -> unpack (dci.c:952-988, 990-1023), the distributed allocation in units of
+    N_RB^step (ra_dl.c:230-244), QPSK and the TBS of 36.213 Table 7.1.7.2.3-1 (ra_dl.c:383-391)"""
+    c = _cell(nprb)
+    step = 2 if nprb < 50 else 4
+    rng = np.random.default_rng(nprb)
+    # N_gap,1 only: the format's size takes the RIV width of N_gap,1 (dci.c:231-240, as 36.212 5.3.3.1.4), while the
+    # reference's packer and unpacker size the RIV by the message's own gap, so an N_gap,2 1C is not of the format's
+    # size (a reference quirk, restated as is)
+    for ngap1 in (True,):
+        nvrb = OP.type2_n_vrb_dl(nprb, ngap1) // step
+        for _ in range(24):
+            L = int(rng.integers(1, nvrb + 1))
+            st = int(rng.integers(0, nvrb - L + 1))
+            riv_v = OP.riv(L, st, nvrb)
+            mcs = int(rng.integers(0, 32))
+            d = _dl(0xFFFF, F1C)
+            _type2(d, riv_v, DIST, 0 if ngap1 else 1)
+            d.tb[0].mcs_idx = mcs
+            r, m = PD.pack_pdsch(c, d)
+            assert r == 0 and m.nof_bits == PD.dci_size(c, F1C)
+            r, u = PD.unpack_pdsch(c, list(m.payload[:m.nof_bits]), F1C, 0xFFFF)
+            assert r == 0 and u.alloc_type == ALLOC2 and u.raw[3] == DIST and u.raw[0] == riv_v
+            assert u.tb[0].mcs_idx == mcs and u.tb[0].rv == -1 and u.raw[2] == (0 if ngap1 else 1)
+            u.format, u.rnti = F1C, 0xFFFF
+            r, g = _grant(c, u)
+            want = OP.type2_prbs(nprb, riv_v, True, ngap1, fmt1c=True)
+            if want is None:
+                assert r != 0
+                continue
+            assert r == 0 and g.tb[0].tbs == OP.TBS_FORMAT1C[mcs] and g.tb[0].mod == 1  # QPSK
+            for s in range(2):
+                assert [n for n in range(nprb) if g.prb_idx[s][n]] == sorted(want[s])

@@ -1818,8 +1818,13 @@ static int ulsch_decode_impl(srsran_sch_t*       q,
   if (!q || !q->gpu || !cfg || (!h_q && !d_q_ext)) {
     return SRSRAN_ERROR_INVALID_INPUTS;
   }
-  if (q->llr_is_8bit) {  // the 8-bit form is the UE's DL-SCH path (cc_worker.cc:108-110); UL-SCH stays int16
-    fprintf(stderr, "[srsran_sch] 8-bit UL-SCH LLRs are not provided\n");
+  if (q->llr_is_8bit) {
+    // srsENB's experimental pusch_8bit_decoder (cc_worker.cc:155-157): pusch.c:419-440 writes int8 LLRs into its
+    // int16 q buffer and hands it to srsran_ulsch_decode, whose uci_decode_ri_ack / ulsch_deinterleave read it as
+    // int16 (sch.c:1145-1161: pairs of int8 LLRs taken as one, nof_bits of them, past the int8 data) -- the
+    // reference's own 8-bit UL-SCH cannot decode, so there is no behaviour to reproduce; refused
+    fprintf(stderr, "[srsran_sch] 8-bit UL-SCH LLRs are not provided (the reference's 8-bit PUSCH path passes int8 "
+                    "LLRs through int16 interfaces)\n");
     return SRSRAN_ERROR;
   }
   UlsPlan   p;

@@ -167,7 +167,6 @@ def test_enb_to_ue_distributed_vrb(env, case):
     assert r == 0 and grant.nof_tb == 1 and grant.nof_prb == len(want[0])
     for s in range(2):
         assert [n for n in range(nprb) if grant.prb_idx[s][n]] == sorted(want[s])
-    assert any(grant.prb_idx[0][n] != grant.prb_idx[1][n] for n in range(nprb))
     grant.tb[0].rv = 0  # 1C carries no RV (36.321 5.3.1: the UE derives it from the SFN)
     qm = [{1: 2, 2: 4, 3: 6}[grant.tb[0].mod]]
     cfg = U.pdsch_cfg(nprb, grant.nof_re, [grant.tb[0].tbs], qm, rnti=rnti, scheme="port0" if P == 1 else "diversity",

@@ -317,6 +317,54 @@ def bench_8bit(torch, device, n, K=6144, iters=8, reps=3):
             "mbps": round(n * K / (ms * 1e-3) / 1e6, 1)}
 
 
+def c1_cpu_leg(data, iters, budget_s, gpu_mbps):
+    """BASELINE configs[0] (C1: K = 6144 code blocks, 8 half-its) on the host, beside the GPU's K = 6144 rate of the
+    same line: the reference decoder (oracle/_ref) on one thread for ~budget_s/2 s over the pool blocks, and one
+    process per core of this job's share for ~budget_s/2 s (cpu_worker, K = 6144 only).  The whole host is not this
+    job's to use (nproc counts every hardware thread of the machine): its figure is the one-thread rate times nproc,
+    a linear extrapolation and an upper bound."""
+    import subprocess
+
+    kind, dec = _tdec_decoder()
+    pool = data[6144][2]
+    half = budget_s / 2
+    bits = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < half:
+        for x in pool:
+            dec.tdec_run(6144, x, True, iters)
+            bits += 6144
+    one = bits / (time.perf_counter() - t0) / 1e6
+    n = cpu_threads()
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--cpu-worker", str(2000 + i),
+                               "--cpu-seconds", str(half), "--iters", str(iters), "--workload", "k6144"],
+                              stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, env=env, cwd=ROOT) for i in range(n)]
+    agg_bits, agg_dt, ok = 0, 0.0, 0
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=half + 120)
+            r = json.loads(out.decode().strip().splitlines()[-1])
+            agg_bits, agg_dt, ok = agg_bits + r["bits"], max(agg_dt, r["dt"]), ok + 1
+        except Exception:
+            p.kill()
+    share = agg_bits / agg_dt / 1e6 if ok else None
+    host = one * (os.cpu_count() or 1)
+    return {
+        "workload": f"K=6144, {iters} half-its, SB layout (BASELINE configs[0])",
+        "kind": kind, "cpu_model": cpu_model(), "unit": "Mbps",
+        "gpu_k6144_mbps": gpu_mbps,
+        "cpu_1thread_mbps": round(one, 2),
+        "cpu_share_mbps": round(share, 2) if share else None, "cpu_share_processes": ok,
+        "cpu_host_estimate_mbps": round(host, 1), "nproc": os.cpu_count(),
+        "gpu_over_1thread": round(gpu_mbps / one, 1) if gpu_mbps else None,
+        "gpu_over_share": round(gpu_mbps / share, 2) if gpu_mbps and share else None,
+        "gpu_over_host_estimate": round(gpu_mbps / host, 2) if gpu_mbps else None,
+        "sample": f"1 thread {half:.0f} s over {len(pool)} pool blocks; {ok} processes x {half:.0f} s over their own "
+                  f"pools; host = 1 thread x nproc (linear extrapolation, SMT threads counted: an upper bound)",
+    }
+
+
 def cpu_baseline(Ks, data, iters, budget_s, workload):
     """Reference decoder (oracle/_ref, compiled from /root/reference) on the host cores of this job.
 
@@ -1766,6 +1814,8 @@ def main():
 
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         result["cpu_baseline"] = cpu_baseline(Ks, data, args.iters, args.cpu_seconds, args.workload)
+        if args.workload == "all188" and 6144 in data:
+            result["c1_cpu"] = c1_cpu_leg(data, args.iters, min(args.cpu_seconds, 8.0), result.get("k6144_mbps"))
     elif rank == 0:
         result["cpu_baseline"] = None
 

@@ -11,6 +11,10 @@ for k in ("pdsch_subframes_per_s", "k6144_mbps", "mbps_16_half_its"):
         out[k] = d[k]
 if "pdsch" in d:
     out["pdsch_ms"] = d["pdsch"].get("ms_per_step")
+if "c1_cpu" in d:
+    c = d["c1_cpu"]
+    out["c1_cpu"] = {k: c.get(k) for k in ("cpu_1thread_mbps", "cpu_share_mbps", "cpu_host_estimate_mbps",
+                                            "gpu_over_1thread", "gpu_over_share", "gpu_over_host_estimate")}
 if "output_check" in d:
     out["mismatched"] = d["output_check"]["mismatched"]
 print(json.dumps(out))

@@ -391,8 +391,12 @@ int unpack_format2x(const srsran_cell_t* cell, srsran_dci_cfg_t* cfg, srsran_dci
     dci->dai    = bit_pack(&y, 2);
     dci->is_tdd = true;
   }
-  dci->pid        = bit_pack(&y, pid_len(cell));
-  dci->tb_cw_swap = *y++ ? true : false;
+  dci->pid = bit_pack(&y, pid_len(cell));
+  if (msg->format == SRSRAN_DCI_FORMAT2B) {  // dci.c:1203-1207: the scrambling identity in the swap flag's place
+    dci->sram_id = *y++ ? true : false;
+  } else {
+    dci->tb_cw_swap = *y++ ? true : false;
+  }
   uint32_t nof_tb = 0;
   for (int i = 0; i < SRSRAN_MAX_CODEWORDS; i++) {
     dci->tb[i].mcs_idx = bit_pack(&y, 5);
@@ -404,7 +408,7 @@ int unpack_format2x(const srsran_cell_t* cell, srsran_dci_cfg_t* cfg, srsran_dci
   }
   if (msg->format == SRSRAN_DCI_FORMAT2) {
     dci->pinfo = bit_pack(&y, cell->nof_ports <= 2 ? 3 : 6);
-  } else {
+  } else if (msg->format == SRSRAN_DCI_FORMAT2A) {
     dci->pinfo = bit_pack(&y, cell->nof_ports <= 2 ? 0 : 2);
   }
   for (int i = 0; i < SRSRAN_MAX_CODEWORDS; i++) {
@@ -1093,6 +1097,7 @@ int srsran_dci_msg_unpack_pdsch(srsran_cell_t* cell, srsran_dl_sf_cfg_t* sf, srs
       return unpack_format1C(cell, sf, cfg, msg, dci);
     case SRSRAN_DCI_FORMAT2:
     case SRSRAN_DCI_FORMAT2A:
+    case SRSRAN_DCI_FORMAT2B:
       return unpack_format2x(cell, cfg, msg, dci);
     default:
       fprintf(stderr, "[srsran_dci] unpacking of DCI format %d is not provided\n", (int)msg->format);

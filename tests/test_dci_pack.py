@@ -203,6 +203,30 @@ def test_format2x_matches_field_packer_and_round_trips(ports, fmt):
                 [(a, bool(b), e) for a, b, e in tbs]
 
 
+@pytest.mark.parametrize("nprb", [25, 100])
+def test_format2B_round_trip(nprb):
+    """format 2B (dci.c:1076-1151 / 1153-1245): the scrambling identity in the swap flag's place, no precoding
+    field; the swap flag itself is left as the caller had it"""
+    rng = np.random.default_rng(nprb + 2)
+    c = _cell(nprb, 2)
+    size = PD.dci_size(c, F2B)
+    assert size == PD.dci_size(c, F2A)  # 2 ports: format 2A carries no precoding bits either
+    nrbg = int(np.ceil(nprb / OP.type0_P(nprb)))
+    for _ in range(8):
+        mask, pid, sram = int(rng.integers(0, 1 << nrbg)), int(rng.integers(0, 8)), bool(rng.integers(0, 2))
+        d = _dl(0x4601, F2B, alloc_type=ALLOC0, pid=pid, sram_id=sram)
+        d.raw[0] = mask
+        d.tb[0].mcs_idx, d.tb[0].rv, d.tb[1].mcs_idx, d.tb[1].rv = 11, 0, 20, 2
+        r, m = PD.pack_pdsch(c, d)
+        assert r == 0 and m.nof_bits == size
+        # the same bits as a format 2A message whose swap flag carries the identity
+        want = OP.dci_pack_2a(nprb, size, mask, [(11, 0, 0), (20, 0, 2)], pid, swap=int(sram), pinfo=0, pinfo_bits=0)
+        assert np.array_equal(np.array(m.payload[:size], np.uint8), want)
+        r, u = PD.unpack_pdsch(c, list(m.payload[:size]), F2B, 0x4601)
+        assert r == 0 and u.raw[0] == mask and u.pid == pid and bool(u.sram_id) == sram and not u.tb_cw_swap
+        assert (u.tb[0].mcs_idx, u.tb[1].mcs_idx, u.tb[1].rv) == (11, 20, 2)
+
+
 @pytest.mark.parametrize("nprb", [6, 25, 50, 100])
 def test_format1C_size(nprb):
     c = _cell(nprb)

@@ -153,6 +153,14 @@ int  srsran_chest_dl_estimate_cfg(srsran_chest_dl_t*     q,
                                   srsran_chest_dl_cfg_t* cfg,
                                   cf_t*                  input[SRSRAN_MAX_PORTS],
                                   srsran_chest_dl_res_t* res);
+/* chest_dl.c:263-278: the MBSFN reference signals of area mbsfn_area_id (refsignal_dl.c:382-422), generated once
+ * per area with the cell set at that time.  srsran_chest_dl_estimate_cfg then estimates subframes with
+ * sf->sf_type = SRSRAN_SF_MBSFN (estimate_port_mbsfn, chest_dl.c:836-865): the CRS of symbol 0 and the MBSFN
+ * reference signals of symbols 2 / 6 / 10, INTERPOLATE (the reference requires it, chest_dl.c:719-721), REFS /
+ * PSS / EMPTY noise, Gauss / TRIANGLE / NONE filters; rows 0..11 of res->ce are written, RSRP / RSSI / CFO keep
+ * their previous values (the reference does not measure them there).  Refused: AVERAGE, ports 2 / 3 (their
+ * interpolation reads row 0, which the reference does not write for them), subframes 0 / 5. */
+int  srsran_chest_dl_set_mbsfn_area_id(srsran_chest_dl_t* q, uint16_t mbsfn_area_id);
 
 /* added: nof_sf subframes in one launch (srsUE default configuration).  d_sf_idx[b] = tti % 10
  * of subframe b (device array); d_grid + b * grid_sf_stride: nof_rx grids; d_ce + b *
@@ -207,9 +215,12 @@ int srsran_chest_dl_gpu_estimate(srsran_chest_dl_t* q,
 
 /* ---------------- OFDM receiver (dft/ofdm.h:49-151, ofdm.c) ----------------
  * GPU FFT (mixed radix 8/4/3/2: 128..2048 points incl. 1536/768/384), no FFTW.  Provided:
- * normal or extended CP, normal subframes, rx_window_offset = 0, no frequency shift, no phase compensation
+ * normal or extended CP, rx_window_offset = 0, no frequency shift, no phase compensation
  * (srsran_ue_dl's configuration, ue_dl.c:88-98) and DC removal (keep_dc = false); normalize is honoured.
- * in_buffer / out_buffer are host pointers as in the reference. */
+ * in_buffer / out_buffer are host pointers as in the reference.  sf_type = SRSRAN_SF_MBSFN (with extended CP, as
+ * srsran_ue_dl's fft_mbsfn): slot 0 holds the non-MBSFN region's normal-CP symbols, the guard, then extended-CP
+ * symbols (ofdm_rx_slot_mbsfn, ofdm.c:522-535); like the reference, such an object transforms its configured
+ * buffers even when srsran_ofdm_rx_sf_ng names others (ofdm.c:576-578). */
 typedef struct {
   uint32_t    nof_prb;
   cf_t*       in_buffer;
@@ -240,6 +251,8 @@ void srsran_ofdm_rx_free(srsran_ofdm_t* q);
 void srsran_ofdm_rx_sf(srsran_ofdm_t* q);
 void srsran_ofdm_rx_sf_ng(srsran_ofdm_t* q, cf_t* input, cf_t* output);
 void srsran_ofdm_set_normalize(srsran_ofdm_t* q, bool normalize_enable);
+int  srsran_ofdm_rx_init_mbsfn(srsran_ofdm_t* q, srsran_cp_t cp, cf_t* in_buffer, cf_t* out_buffer, uint32_t max_prb);
+void srsran_ofdm_set_non_mbsfn_region(srsran_ofdm_t* q, uint8_t non_mbsfn_region); /* ofdm.c:241-244 */
 
 /* added: nof_sf subframes x nof_rx antennas on device buffers (d_in: [sf][rx][sf_sz] samples,
  * d_out: [sf][rx][14 * nof_re]); `cfo` rotates the samples as srsran_cfo_correct(.., cfo) would
@@ -275,8 +288,9 @@ int srsran_pdsch_re_table(const srsran_cell_t*        cell,
  * demapping + descrambling + CSI correction fused into one LLR kernel, then DL-SCH decode.
  * Provided: PORT0 (1 port), TX diversity (2 or 4 ports, 1 codeword; layer demap fused), CDD and
  * SPATIALMUX (2 ports x 2 rx, 1 or 2 codewords on 2 layers), MMSE (ZF = MMSE with noise 0, as
- * pdsch.c:811 passes it), 16-bit LLRs, normal and extended CP, FDD.
- * Not provided (SRSRAN_ERROR): 4-port CDD / SM (refused by the reference too), 8-bit LLRs, EVM.
+ * pdsch.c:811 passes it), 16- and 8-bit LLRs (llr_is_8bit), EVM (meas_evm_en), normal and extended CP, FDD and
+ * TDD cells (DwPTS grants of special subframes).
+ * Not provided (SRSRAN_ERROR): 4-port CDD / SM (refused by the reference too), MBSFN subframes (the PMCH).
  * The host-side working buffers of the reference struct (ce, symbols, x, d, e, csi) do not
  * exist; the coworker thread is unnecessary (both codewords decode in one GPU pass). */
 typedef struct {
@@ -358,9 +372,12 @@ int srsran_pdsch_gpu_last_evm(srsran_pdsch_t* q, uint32_t sf, uint32_t tb, const
 
 /* ---------------- UE DL (ue/ue_dl.h:77-207, ue_dl.c) ----------------
  * decode_fft_estimate: OFDM, CRS estimation, PCFICH (sets sf->cfi) and the PDCCH LLRs, all on the
- * GPU, for cells of 1 or 2 ports with normal PHICH duration (other cells: the CFI is the caller's
- * sf->cfi).  srsran_ue_dl_find_dl_dci / srsran_ue_dl_dci_to_pdsch_grant are in srsran_pdcch.h.
- * PHICH / PMCH are not provided.  srsran_dl_cfg_t omits the reference's leading cqi_report. */
+ * GPU, for cells of 1, 2 or 4 ports with normal PHICH duration (other cells: the CFI is the caller's
+ * sf->cfi).  MBSFN subframes (sf->sf_type, srsran_ue_dl_set_non_mbsfn_region, srsran_ue_dl_set_mbsfn_area_id):
+ * fft_mbsfn transforms antenna 0's input buffer into sf_symbols[0] and the other antennas' grids keep the
+ * previous subframe, as in the reference (ue_dl.c:104-111, 353-356, 373-376); then the MBSFN estimator and the
+ * PCFICH / PDCCH of the non-MBSFN region.  srsran_ue_dl_find_dl_dci / srsran_ue_dl_dci_to_pdsch_grant are in
+ * srsran_pdcch.h.  PHICH / PMCH are not provided.  srsran_dl_cfg_t omits the reference's leading cqi_report. */
 typedef enum { SRSRAN_TM1 = 0, SRSRAN_TM2, SRSRAN_TM3, SRSRAN_TM4, SRSRAN_TM5, SRSRAN_TM6, SRSRAN_TM7, SRSRAN_TM8,
                SRSRAN_TMINV } srsran_tm_t;
 
@@ -396,6 +413,7 @@ typedef struct {
   srsran_chest_dl_t     chest;
   srsran_chest_dl_res_t chest_res;
   srsran_ofdm_t         fft[SRSRAN_MAX_PORTS];
+  srsran_ofdm_t         fft_mbsfn; /* MBSFN subframes: antenna 0's input only, as ue_dl.c:104-111 configures it */
   cf_t*                 sf_symbols[SRSRAN_MAX_PORTS];
   void*                 gpu; /* added: batch pipeline buffers */
 } srsran_ue_dl_t;

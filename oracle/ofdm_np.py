@@ -41,6 +41,50 @@ def symbol_starts(N, ext=0):
     return [s * slot + cp0 + i * (N + cp) for s in range(2) for i in range(ns)]
 
 
+def mbsfn_symbol_starts(N, nr):
+    """sample offsets of the 12 symbols of an MBSFN subframe (ofdm_rx_slot_mbsfn, ofdm.c:522-535, then slot 1 of
+    the extended-CP layout): slot 0's first nr symbols after normal cyclic prefixes, the guard
+    SRSRAN_NON_MBSFN_REGION_GUARD_LENGTH (phy_common.h:166-169) before symbol nr, extended cyclic prefixes after"""
+    cpn0, cpn = cp_lens(N, 0)
+    cpe = cp_lens(N, 1)[0]
+    out, pos = [], 0
+    for i in range(6):
+        if i == nr:
+            pos += cpe - cpn0 if nr == 1 else 2 * cpe - cpn0 - cpn
+        pos += cpe if i >= nr else (cpn0 if i == 0 else cpn)
+        out.append(pos)
+        pos += N
+    return out + symbol_starts(N, 1)[6:]
+
+
+def ofdm_rx_mbsfn(x, N, nre, nr):
+    x = np.asarray(x, np.complex128)
+    out = np.zeros((12, nre), np.complex128)
+    for l, st in enumerate(mbsfn_symbol_starts(N, nr)):
+        X = np.fft.fft(x[st:st + N])
+        out[l, : nre // 2] = X[N - nre // 2:]
+        out[l, nre // 2:] = X[1: nre // 2 + 1]
+    return out.reshape(-1)
+
+
+def ofdm_tx_mbsfn(grid, N, nre, nr):
+    """the eNB's MBSFN modulator (ofdm_tx_slot_mbsfn, ofdm.c:652-674): the inverse of ofdm_rx_mbsfn; the guard
+    samples stay zero"""
+    grid = np.asarray(grid, np.complex128).reshape(12, nre)
+    cpn0, cpn = cp_lens(N, 0)
+    cpe = cp_lens(N, 1)[0]
+    x = np.zeros(sf_len(N, 1), np.complex128)
+    for l, st in enumerate(mbsfn_symbol_starts(N, nr)):
+        X = np.zeros(N, np.complex128)
+        X[N - nre // 2:] = grid[l, : nre // 2]
+        X[1: nre // 2 + 1] = grid[l, nre // 2:]
+        t = np.fft.ifft(X)
+        c = cpe if (l >= nr or l >= 6) else (cpn0 if l == 0 else cpn)
+        x[st - c: st] = t[N - c:]
+        x[st: st + N] = t
+    return x
+
+
 def ofdm_rx(x, N, nre, normalize=False, ext=0):
     x = np.asarray(x, np.complex128)
     out = np.zeros((2 * nsymb(ext), nre), np.complex128)

@@ -229,9 +229,10 @@ class Oracle(_Lib, _PhyMixin):
         return ce, dict(noise=float(out[0]), rsrp=float(out[1]), rssi=float(out[2]), cfo=float(out[3]))
 
     def chest_dl_ext(self, grids, nof_prb, cell_id, nports, sf_idx, symbol_sz, cp=0, estimator=0, noise_alg=0,
-                     filt_order=4, filt_std=1.0, sync=False, noise_state=None, nsym=(4, 2)):
-        """chest_dl.c with the options beyond srsUE's defaults (oracle_chest_dl_ext): estimator 0 AVERAGE /
-        1 INTERPOLATE, noise_alg 0 REFS / 1 PSS / 2 EMPTY, filt_order 0 = automatic, sync = correct_sync_error.
+                     filt_order=4, filt_std=1.0, sync=False, noise_state=None, nsym=(4, 2), filter_type=0):
+        """chest_dl.c with the options beyond srsUE's defaults (oracle_chest_dl_ext_f): estimator 0 AVERAGE /
+        1 INTERPOLATE, noise_alg 0 REFS / 1 PSS / 2 EMPTY, filter_type 0 GAUSS (filt_order 0 = automatic) / 1 TRIANGLE
+        (w = filt_order) / 2 NONE, sync = correct_sync_error.
         -> (ce (nports, nrx, n), stats dict, corrected grids, noise_state (4, 4) after the call)"""
         grids = np.array(grids, np.complex64, copy=True)
         nrx, n = grids.shape
@@ -241,15 +242,41 @@ class Oracle(_Lib, _PhyMixin):
         pss = np.zeros(62, np.complex64)
         self.lib.oracle_pss_generate.argtypes = [ctypes.c_uint32, ctypes.c_void_p]
         self.lib.oracle_pss_generate(cell_id % 3, pss.ctypes.data)
-        f = self.lib.oracle_chest_dl_ext_tdd
-        f.argtypes = [ctypes.c_void_p] + [ctypes.c_uint32] * 10 + [ctypes.c_float, ctypes.c_uint32] + \
+        f = self.lib.oracle_chest_dl_ext_f
+        f.argtypes = [ctypes.c_void_p] + [ctypes.c_uint32] * 10 + [ctypes.c_float, ctypes.c_float, ctypes.c_uint32] + \
             [ctypes.c_void_p] * 2 + [ctypes.c_uint32] * 2 + [ctypes.c_void_p] * 2
-        f(grids.ctypes.data, nof_prb, cell_id, nports, nrx, sf_idx, symbol_sz, cp, estimator, noise_alg, filt_order,
-          filt_std, 1 if sync else 0, pss.ctypes.data, ns.ctypes.data, nsym[0], nsym[1], ce.ctypes.data,
-          out.ctypes.data)
+        f(grids.ctypes.data, nof_prb, cell_id, nports, nrx, sf_idx, symbol_sz, cp, estimator, noise_alg, filter_type,
+          float(filt_order), filt_std, 1 if sync else 0, pss.ctypes.data, ns.ctypes.data, nsym[0], nsym[1],
+          ce.ctypes.data, out.ctypes.data)
         st = dict(noise=float(out[0]), rsrp=float(out[1]), rssi=float(out[2]), cfo=float(out[3]),
                   sync_error=float(out[4]))
         return ce, st, grids, ns
+
+    def mbsfn_pilots(self, nof_prb, area, sf):
+        """srsran_refsignal_mbsfn_gen_seq's pilots of subframe sf: (3, 6 N_RB) complex64"""
+        out = np.zeros(18 * nof_prb, np.complex64)
+        f = self.lib.oracle_mbsfn_pilots
+        f.argtypes = [ctypes.c_uint32] * 3 + [ctypes.c_void_p]
+        f(nof_prb, area, sf, out.ctypes.data)
+        return out.reshape(3, 6 * nof_prb)
+
+    def chest_dl_mbsfn(self, grids, nof_prb, cell_id, nports, sf_idx, area, noise_alg=1, filter_type=1, coef0=0.1,
+                       coef1=0.0, noise_state=None, cp=0, ce_init=None):
+        """srsran_chest_dl_estimate_cfg of an MBSFN subframe (oracle_chest_dl_mbsfn): INTERPOLATE, filter_type 0
+        GAUSS (coef0 order, 0 = automatic; coef1 stddev) / 1 TRIANGLE (w = coef0; srsUE's MBSFN configuration:
+        TRIANGLE 0.1, PSS noise) / 2 NONE.  ce_init: the estimate buffers before the call (rows 12 / 13 are not
+        written).  -> (ce (nports, nrx, n), noise estimate, noise_state after the call)"""
+        grids = np.ascontiguousarray(grids, np.complex64)
+        nrx, n = grids.shape
+        ce = np.zeros((nports, nrx, n), np.complex64) if ce_init is None else np.array(ce_init, np.complex64, copy=True)
+        ns = np.zeros((4, 4), np.float32) if noise_state is None else np.array(noise_state, np.float32, copy=True)
+        out = np.zeros(1, np.float32)
+        f = self.lib.oracle_chest_dl_mbsfn
+        f.argtypes = [ctypes.c_void_p] + [ctypes.c_uint32] * 9 + [ctypes.c_float] * 2 + [ctypes.c_void_p] * 3
+        if f(grids.ctypes.data, nof_prb, cell_id, nports, nrx, sf_idx, cp, area, noise_alg, filter_type, coef0, coef1,
+             ns.ctypes.data, ce.ctypes.data, out.ctypes.data):
+            raise ValueError("oracle_chest_dl_mbsfn: ports 0 / 1 only")
+        return ce, float(out[0]), ns
 
     def sequence_bits(self, seed, n):
         c = np.zeros(n, np.uint8)

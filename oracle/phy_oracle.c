@@ -693,7 +693,7 @@ static float avg_power(const cpx* x, uint32_t n)
 
 static float noise_pilots(const cpx* pe, uint32_t nsym, uint32_t nref, uint32_t fidx0)
 {
-  cpx tmp[4 * 110];
+  cpx tmp[20 * 110]; /* nref <= 20 N_RB / 3 (MBSFN subframes) */
   if (nsym < 3) { /* chest_dl.c:345-354 */
     for (uint32_t k = 0; k < nref - 2; k++) {
       cpx t  = cadd(cadd(pe[k], pe[k + 1]), pe[k + 2]);
@@ -1046,12 +1046,50 @@ int oracle_chest_dl_ext(float* grid, uint32_t nof_prb, uint32_t cell_id, uint32_
                                  filt_order, filt_std, sync, pss, noise_state, 4, 2, ce, out);
 }
 
+/* filter_type: 0 GAUSS (coef0 = order, coef1 = stddev; coef0 <= 0 automatic: order 4, stddev 200 x noise), 1 TRIANGLE
+ * (coef0 = w: {w, 1 - 2w, w}, chest_common.c:62-68), 2 NONE (no average_pilots: the LS estimates interpolated as
+ * they are, chest_dl.c:724-725 -- with AVERAGE and more than one CRS symbol the first 4 N_RB of them as one comb of
+ * spacing 3, 476-481) */
+int oracle_chest_dl_ext_f(float* grid, uint32_t nof_prb, uint32_t cell_id, uint32_t nports, uint32_t nrx,
+                          uint32_t sf_idx, uint32_t symbol_sz, uint32_t cp, uint32_t estimator, uint32_t noise_alg,
+                          uint32_t filter_type, float coef0, float coef1, uint32_t sync, const float* pss,
+                          float* noise_state, uint32_t nsym01, uint32_t nsym23, float* ce, float* out);
 int oracle_chest_dl_ext_tdd(float* grid, uint32_t nof_prb, uint32_t cell_id, uint32_t nports, uint32_t nrx,
                             uint32_t sf_idx, uint32_t symbol_sz, uint32_t cp, uint32_t estimator, uint32_t noise_alg,
                             uint32_t filt_order, float filt_std, uint32_t sync, const float* pss, float* noise_state,
                             uint32_t nsym01, uint32_t nsym23, float* ce, float* out)
 {
+  return oracle_chest_dl_ext_f(grid, nof_prb, cell_id, nports, nrx, sf_idx, symbol_sz, cp, estimator, noise_alg, 0,
+                               (float)filt_order, filt_std, sync, pss, noise_state, nsym01, nsym23, ce, out);
+}
+
+/* the smoothing filter of chest_interpolate_noise_est (chest_dl.c:700-717); returns its length (0: none, or a
+ * Gauss filter whose sum is not normal -- srsran_conv_same_cf then writes zeros) */
+static uint32_t oracle_filter(uint32_t filter_type, float coef0, float coef1, float noise, float* filt)
+{
+  if (filter_type == 1) {
+    filt[0] = filt[2] = coef0;
+    filt[1]           = 1 - 2 * coef0;
+    return 3;
+  }
+  if (filter_type == 2) {
+    return 0;
+  }
+  uint32_t flen = coef0 > 0 ? oracle_gauss_filter(filt, (uint32_t)coef0, coef1) : oracle_gauss_filter(filt, 4, noise * 200.0f);
+  float    s    = 0;
+  for (uint32_t k = 0; k < flen; k++) {
+    s += filt[k];
+  }
+  return isnormal(s) ? flen : 0;
+}
+
+int oracle_chest_dl_ext_f(float* grid, uint32_t nof_prb, uint32_t cell_id, uint32_t nports, uint32_t nrx,
+                          uint32_t sf_idx, uint32_t symbol_sz, uint32_t cp, uint32_t estimator, uint32_t noise_alg,
+                          uint32_t filter_type, float coef0, float coef1, uint32_t sync, const float* pss,
+                          float* noise_state, uint32_t nsym01, uint32_t nsym23, float* ce, float* out)
+{
   const uint32_t nsymb = cp ? 6 : 7;
+  const int      none  = filter_type == 2;
   const uint32_t nre = NRE * nof_prb, nsf = 2 * nsymb * nre, nref = 2 * nof_prb;
   cpx*           G   = (cpx*)grid;
   cpx*           CE  = (cpx*)ce;
@@ -1136,22 +1174,14 @@ int oracle_chest_dl_ext_tdd(float* grid, uint32_t nof_prb, uint32_t cell_id, uin
       if (noise_alg == 0) {
         *ns = noise_pilots(pe, nsym, nref, fidx0);
       }
-      float    filt[8];
-      uint32_t flen = filt_order ? oracle_gauss_filter(filt, filt_order, filt_std)
-                                 : oracle_gauss_filter(filt, 4, *ns * 200.0f);
-      {
-        float s = 0;
-        for (uint32_t k = 0; k < flen; k++) {
-          s += filt[k];
-        }
-        if (!isnormal(s)) {
-          flen = 0; /* srsran_chest_set_smooth_filter_gauss returns 0: conv_same writes zeros */
-        }
-      }
-      cpx* row = CE + ((size_t)port * nrx + rx) * nsf;
+      float          filt[8];
+      const uint32_t flen = oracle_filter(filter_type, coef0, coef1, *ns, filt);
+      cpx*           row  = CE + ((size_t)port * nrx + rx) * nsf;
       if (estimator == 0) {
         uint32_t nr = nref;
-        if (nsym > 1) {
+        if (none) {
+          nr = nsym > 1 ? 2 * nref : nref;
+        } else if (nsym > 1) {
           const cpx* a = fidx0 < 3 ? pe : pe + nref;
           const cpx* b = fidx0 < 3 ? pe + nref : pe;
           for (uint32_t k = 0; k < nref; k++) {
@@ -1171,7 +1201,9 @@ int oracle_chest_dl_ext_tdd(float* grid, uint32_t nof_prb, uint32_t cell_id, uin
             pe[k] = cscale(tmp[k], 2.0f / (float)nsym);
           }
         }
-        if (flen) {
+        if (none) {
+          memcpy(avg, pe, nr * sizeof(cpx));
+        } else if (flen) {
           conv_same(pe, filt, avg, nr, flen);
         } else {
           memset(avg, 0, nr * sizeof(cpx));
@@ -1186,7 +1218,9 @@ int oracle_chest_dl_ext_tdd(float* grid, uint32_t nof_prb, uint32_t cell_id, uin
           memcpy(row + l * nre, row, nre * sizeof(cpx));
         }
       } else if (nsym == 1) { /* one CRS symbol: interpolated into row 0, copied everywhere (chest_dl.c:488-515) */
-        if (flen) {
+        if (none) {
+          memcpy(avg, pe, nref * sizeof(cpx));
+        } else if (flen) {
           conv_same(pe, filt, avg, nref, flen);
         } else {
           memset(avg, 0, nref * sizeof(cpx));
@@ -1197,7 +1231,9 @@ int oracle_chest_dl_ext_tdd(float* grid, uint32_t nof_prb, uint32_t cell_id, uin
         }
       } else {
         for (uint32_t l = 0; l < nsym; l++) { /* smoothing of every CRS symbol, then interpolation into its row */
-          if (flen) {
+          if (none) {
+            memcpy(avg + l * nref, pe + l * nref, nref * sizeof(cpx));
+          } else if (flen) {
             conv_same(pe + l * nref, filt, avg + l * nref, nref, flen);
           } else {
             memset(avg + l * nref, 0, nref * sizeof(cpx));
@@ -1278,6 +1314,104 @@ int oracle_chest_dl_ext_tdd(float* grid, uint32_t nof_prb, uint32_t cell_id, uin
   out[2] = r / (float)nrx;
   out[3] = cfo;
   out[4] = sync ? sync_err00 : 0.0f;
+  return 0;
+}
+
+/* ======================= MBSFN subframes (round 5) =======================
+ * srsran_refsignal_mbsfn_gen_seq (refsignal_dl.c:382-422): the MBSFN reference signals of subframe sf, area
+ * N_MBSFN: for l = 0..2 (grid symbols 2 / 6 / 10 of the extended-CP layout, l' = symbol mod 6 in slot 2 sf for l = 0,
+ * 2 sf + 1 otherwise), c_init = 512 (7 (ns + 1) + l' + 1)(2 N_MBSFN + 1) + N_MBSFN, r(m) from c(2m'), c(2m' + 1),
+ * m' = m + 3 (110 - N_RB), m < 6 N_RB.  out: [3][6 N_RB] cf32 */
+void oracle_mbsfn_pilots(uint32_t nof_prb, uint32_t area, uint32_t sf, float* out)
+{
+  cpx*    P = (cpx*)out;
+  uint8_t c[20 * 110];
+  for (uint32_t l = 0; l < 3; l++) {
+    const uint32_t lp = (2 + 4 * l) % 6, ns = l ? 2 * sf + 1 : 2 * sf;
+    oracle_sequence_bits(512 * (7 * (ns + 1) + lp + 1) * (2 * area + 1) + area, c, 20 * 110);
+    for (uint32_t i = 0; i < 6 * nof_prb; i++) {
+      const uint32_t mp = i + 3 * (110 - nof_prb);
+      P[6 * nof_prb * l + i] = (cpx){(1 - 2 * (float)c[2 * mp]) * (float)0.70710678118654752440,
+                                     (1 - 2 * (float)c[2 * mp + 1]) * (float)0.70710678118654752440};
+    }
+  }
+}
+
+/* srsran_chest_dl_estimate_cfg on an MBSFN subframe (estimate_port_mbsfn, chest_dl.c:836-865, with
+ * chest_interpolate_noise_est 642-747, average_pilots 557-600, interpolate_pilots 437-555), INTERPOLATE, ports 0 / 1:
+ *   LS over the CRS of symbol 0 (2 N_RB; the CRS of port pair 0 / subframe sf, its first symbol) and the MBSFN
+ *   reference signals of grid symbols 2 / 6 / 10 at subcarriers 2i + (0, 1, 0) (srsran_refsignal_mbsfn_get_sf,
+ *   refsignal_dl.c:474-502), 20 N_RB estimates; REFS noise over them as 3 rows of floor(20 N_RB / 3) with fidx 1
+ *   (estimate_noise_pilots 331-342); PSS / EMPTY keep noise_state (subframes 0 / 5 are not MBSFN); the CRS row
+ *   copied and each MBSFN row filtered (average_pilots 591-599); frequency interpolation into rows 0 (spacing 6),
+ *   2 / 6 / 10 (spacing 2, offsets 0 / 1 / 0), time interpolation 517-521.  Rows 12 / 13 of ce are not written;
+ *   rsrp / rssi / cfo are not measured (the caller keeps them).  out[0] = the noise estimate (fill_res). */
+int oracle_chest_dl_mbsfn(const float* grid, uint32_t nof_prb, uint32_t cell_id, uint32_t nports, uint32_t nrx,
+                          uint32_t sf_idx, uint32_t cp, uint32_t area, uint32_t noise_alg, uint32_t filter_type,
+                          float coef0, float coef1, float* noise_state, float* ce, float* out)
+{
+  if (nports > 2) {
+    return -1;
+  }
+  const uint32_t nsymb = cp ? 6 : 7, N = nof_prb;
+  const uint32_t nre = NRE * N, nsf = 2 * nsymb * nre, nref = 2 * N, nm = 6 * N, np = 20 * N;
+  const cpx*     G  = (const cpx*)grid;
+  cpx*           CE = (cpx*)ce;
+  static cpx     pil[4 * 2 * 110], mp[18 * 110], pe[20 * 110], avg[20 * 110], tmp[20 * 110];
+  oracle_crs_pilots_cp(cell_id, N, 0, sf_idx, cp, (float*)pil);
+  oracle_mbsfn_pilots(N, area, sf_idx, (float*)mp);
+  for (uint32_t rx = 0; rx < nrx; rx++) {
+    const cpx* in = G + (size_t)rx * nsf;
+    for (uint32_t port = 0; port < nports; port++) {
+      const uint32_t fidx0 = crs_fidx(cell_id, 0, port);
+      for (uint32_t i = 0; i < nref; i++) {
+        pe[i] = cmul(in[crs_nsymbol(0, port, nsymb) * nre + fidx0 + 6 * i], cconj(pil[i]));
+      }
+      for (uint32_t l = 0; l < 3; l++) {
+        for (uint32_t i = 0; i < nm; i++) {
+          pe[nref + l * nm + i] = cmul(in[(2 + 4 * l) * nre + (l == 1 ? 1 : 0) + 2 * i], cconj(mp[l * nm + i]));
+        }
+      }
+      float* ns = &noise_state[rx * 4 + port];
+      if (noise_alg == 0) {
+        *ns = noise_pilots(pe, 3, np / 3, 1);
+      }
+      float          filt[8];
+      const uint32_t flen = oracle_filter(filter_type, coef0, coef1, *ns, filt);
+      memcpy(avg, pe, nref * sizeof(cpx));
+      for (uint32_t l = 0; l < 3; l++) {
+        if (filter_type == 2) {
+          memcpy(avg + nref + l * nm, pe + nref + l * nm, nm * sizeof(cpx));
+        } else if (flen) {
+          conv_same(pe + nref + l * nm, filt, avg + nref + l * nm, nm, flen);
+        } else {
+          memset(avg + nref + l * nm, 0, nm * sizeof(cpx));
+        }
+      }
+      (void)tmp;
+      cpx* row = CE + ((size_t)port * nrx + rx) * nsf;
+#define CES(i) (row + (size_t)(i)*nre)
+      interp_linear_offset(avg, CES(0), nref, 6, fidx0, 6 - fidx0);
+      for (uint32_t l = 0; l < 3; l++) {
+        const uint32_t f = l == 1 ? 1 : 0;
+        interp_linear_offset(avg + nref + l * nm, CES(2 + 4 * l), nm, 2, f, f ? 1 : 2);
+      }
+      interp_vector(CES(0), CES(2), NULL, CES(1), 2, 1, nre);
+      interp_vector(CES(2), CES(6), NULL, CES(3), 4, 3, nre);
+      interp_vector(CES(6), CES(10), NULL, CES(7), 4, 3, nre);
+      interp_vector(CES(6), CES(10), CES(10), CES(11), 4, 1, nre);
+#undef CES
+    }
+  }
+  float n = 0;
+  for (uint32_t rx = 0; rx < nrx; rx++) {
+    float s = 0;
+    for (uint32_t p = 0; p < nports; p++) {
+      s += noise_state[rx * 4 + p];
+    }
+    n += s / (float)nports;
+  }
+  out[0] = n / (float)nrx;
   return 0;
 }
 

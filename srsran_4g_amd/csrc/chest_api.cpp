@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <vector>
 
 #include "../../include/srsran_ue_dl.h"
@@ -62,7 +63,34 @@ struct ChestGpu {
   float2*     tab     = nullptr;  // sync correction phasor table (12 * max_prb)
   float       sync_err[SRSRAN_MAX_PORTS][SRSRAN_MAX_PORTS] = {};  // q->sync_err (chest_dl.c:776)
   srsran_tdd_config_t tdd{};  // the batch estimators' TDD frame configuration (srsran_chest_dl_gpu_set_tdd_config)
+  // MBSFN reference signals per area (q->mbsfn_refs, chest_dl.c:263-278): host tables [10 sf][3][6 nof_prb], the
+  // one of area mbsfn_loaded on the device
+  std::map<uint16_t, std::vector<float2>> mbsfn;
+  float2* d_mbsfn      = nullptr;
+  int     mbsfn_loaded = -1;
 };
+
+// srsran_refsignal_mbsfn_gen_seq (refsignal_dl.c:382-422): for every subframe and MBSFN symbol l (grid symbols
+// 2 / 6 / 10, l' = 2 / 0 / 4 of slots 2 sf, 2 sf + 1, 2 sf + 1), c_init = 2^9 (7 (ns + 1) + l' + 1)(2 N_MBSFN + 1) +
+// N_MBSFN and r(m') = (1 - 2 c(2m')) / sqrt 2 + j (1 - 2 c(2m' + 1)) / sqrt 2 at m' = m + 3 (110 - N_RB)
+std::vector<float2> mbsfn_pilots(const srsran_cell_t& cell, uint32_t area)
+{
+  const uint32_t       N = cell.nof_prb;
+  std::vector<float2>  t(10 * 18 * (size_t)N);
+  std::vector<uint8_t> c(20 * 110);
+  const float          a = (float)0.70710678118654752440;
+  for (uint32_t sf = 0; sf < 10; sf++) {
+    for (uint32_t l = 0; l < 3; l++) {
+      const uint32_t lp = (2 + 4 * l) % 6, slot = l ? 2 * sf + 1 : 2 * sf;
+      gold(512 * (7 * (slot + 1) + lp + 1) * (2 * area + 1) + area, c.data(), 20 * 110);
+      for (uint32_t i = 0; i < 6 * N; i++) {
+        const uint32_t mp = i + 3 * (110 - N);
+        t[(sf * 3 + l) * 6 * N + i] = make_float2((1 - 2 * (float)c[2 * mp]) * a, (1 - 2 * (float)c[2 * mp + 1]) * a);
+      }
+    }
+  }
+  return t;
+}
 
 // srsran_refsignal_cs_nof_symbols (refsignal_dl.c:169-226) of a TDD special subframe: the CRS symbols of ports 0 / 1
 // (port23 = false) or 2 / 3 that fall in its DwPTS
@@ -132,8 +160,9 @@ bool cfg_supported(const srsran_chest_dl_cfg_t* cfg)
   const bool est   = cfg->estimator_alg == SRSRAN_ESTIMATOR_ALG_AVERAGE || cfg->estimator_alg == SRSRAN_ESTIMATOR_ALG_INTERPOLATE;
   const bool noise = cfg->noise_alg == SRSRAN_NOISE_ALG_REFS || cfg->noise_alg == SRSRAN_NOISE_ALG_PSS ||
                      cfg->noise_alg == SRSRAN_NOISE_ALG_EMPTY;
-  return est && noise && cfg->filter_type == SRSRAN_CHEST_FILTER_GAUSS && !cfg->rsrp_neighbour &&
-         cfg->filter_coef[0] <= 7;
+  const bool filt  = cfg->filter_type == SRSRAN_CHEST_FILTER_TRIANGLE || cfg->filter_type == SRSRAN_CHEST_FILTER_NONE ||
+                     (cfg->filter_type == SRSRAN_CHEST_FILTER_GAUSS && cfg->filter_coef[0] <= 7);
+  return est && noise && filt && !cfg->rsrp_neighbour;
 }
 
 constexpr size_t kPilotsPerSf = 2 * 4 * CHEST_MAX_NREF;  // float2 per subframe (both port pairs)
@@ -156,6 +185,25 @@ uint32_t gauss(float* f, uint32_t order, float std_dev)  // chest_common.c:70-95
     f[i] *= 1.0f / s;
   }
   return len;
+}
+
+// the filter of chest_interpolate_noise_est (chest_dl.c:700-717) into the launch arguments: GAUSS with coefficients
+// (order, stddev) or automatic (coef[0] <= 0: order 4, stddev 200 x noise, computed in the kernel), TRIANGLE
+// {w, 1 - 2w, w} with w = coef[0] (srsran_chest_set_smooth_filter3_coeff), NONE (no smoothing)
+void set_filter(const srsran_chest_dl_cfg_t* cfg, ChestArgs& a)
+{
+  a.filter_auto = a.filter_none = 0;
+  if (cfg->filter_type == SRSRAN_CHEST_FILTER_TRIANGLE) {
+    a.filter[0] = a.filter[2] = cfg->filter_coef[0];
+    a.filter[1]  = 1 - 2 * cfg->filter_coef[0];
+    a.filter_len = 3;
+  } else if (cfg->filter_type == SRSRAN_CHEST_FILTER_NONE) {
+    a.filter_none = 1;
+  } else if (cfg->filter_coef[0] <= 0) {
+    a.filter_auto = 1;
+  } else {
+    a.filter_len = gauss(a.filter, (uint32_t)cfg->filter_coef[0], cfg->filter_coef[1]);
+  }
 }
 
 }  // namespace
@@ -287,7 +335,8 @@ int srsran_chest_dl_init(srsran_chest_dl_t* q, uint32_t max_prb, uint32_t nof_rx
       hipMalloc((void**)&g->pss, 62 * sizeof(float2)) != hipSuccess ||
       hipMalloc((void**)&g->noise, 16 * sizeof(float)) != hipSuccess || hipMemset(g->noise, 0, 16 * sizeof(float)) ||
       hipMalloc((void**)&g->sync, 16 * 10 * sizeof(float)) != hipSuccess ||
-      hipMalloc((void**)&g->tab, 12 * (size_t)max_prb * sizeof(float2)) != hipSuccess) {
+      hipMalloc((void**)&g->tab, 12 * (size_t)max_prb * sizeof(float2)) != hipSuccess ||
+      hipMalloc((void**)&g->d_mbsfn, 10 * 18 * (size_t)max_prb * sizeof(float2)) != hipSuccess) {
     q->gpu = g;
     srsran_chest_dl_free(q);
     return SRSRAN_ERROR;
@@ -319,6 +368,7 @@ void srsran_chest_dl_free(srsran_chest_dl_t* q)
     hipFree(g->noise);
     hipFree(g->sync);
     hipFree(g->tab);
+    hipFree(g->d_mbsfn);
     delete g;
   }
   memset(q, 0, sizeof(*q));
@@ -363,6 +413,19 @@ int srsran_chest_dl_set_cell(srsran_chest_dl_t* q, srsran_cell_t cell)
     return SRSRAN_ERROR;
   }
   g->filter_len = gauss(g->filter, 4, 1.0f);
+  g->mbsfn_loaded = -1;
+  return SRSRAN_SUCCESS;
+}
+
+int srsran_chest_dl_set_mbsfn_area_id(srsran_chest_dl_t* q, uint16_t mbsfn_area_id)
+{
+  if (!q || !q->gpu || mbsfn_area_id >= 256 || q->cell.nof_prb == 0) {  // SRSRAN_MAX_MBSFN_AREA_IDS
+    return SRSRAN_ERROR;
+  }
+  ChestGpu* g = (ChestGpu*)q->gpu;
+  if (!g->mbsfn.count(mbsfn_area_id)) {  // generated once per area, with the cell of that moment (chest_dl.c:266-273)
+    g->mbsfn[mbsfn_area_id] = mbsfn_pilots(q->cell, mbsfn_area_id);
+  }
   return SRSRAN_SUCCESS;
 }
 
@@ -421,11 +484,7 @@ static int chest_enqueue(srsran_chest_dl_t* q, uint32_t tti, const float2* d_gri
   a.pss      = g->pss;
   a.noise_in = g->noise;
   if (cfg) {
-    if (cfg->filter_coef[0] <= 0) {
-      a.filter_auto = 1;
-    } else {
-      a.filter_len = gauss(a.filter, (uint32_t)cfg->filter_coef[0], cfg->filter_coef[1]);
-    }
+    set_filter(cfg, a);
     a.estimator = cfg->estimator_alg == SRSRAN_ESTIMATOR_ALG_INTERPOLATE ? 1 : 0;
     a.noise_alg = (uint32_t)cfg->noise_alg;
     if (a.estimator == 1 && !full) {
@@ -559,6 +618,92 @@ static void fill_res(srsran_chest_dl_t* q, const float* st, srsran_chest_dl_res_
   res->sync_error = ((ChestGpu*)q->gpu)->sync_err[0][0];  // the channel used for synchronisation (chest_dl.c:974)
 }
 
+// srsran_chest_dl_estimate_cfg of an MBSFN subframe (chest_dl.c:1005-1026 with estimate_port_mbsfn, 836-865)
+static int estimate_mbsfn(srsran_chest_dl_t*     q,
+                          srsran_dl_sf_cfg_t*    sf,
+                          srsran_chest_dl_cfg_t* cfg,
+                          cf_t*                  input[SRSRAN_MAX_PORTS],
+                          srsran_chest_dl_res_t* res)
+{
+  ChestGpu*      g   = (ChestGpu*)q->gpu;
+  const uint32_t sfi = sf->tti % 10, nrx = q->nof_rx_antennas, np = q->cell.nof_ports, N = q->cell.nof_prb;
+  const auto     it  = g->mbsfn.find(cfg->mbsfn_area_id);
+  if (it == g->mbsfn.end() || it->second.size() != 10 * 18 * (size_t)N) {
+    fprintf(stderr, "[srsran_chest_dl] MBSFN area id=%u not initialized for this cell (srsran_chest_dl_set_mbsfn_area_id)\n",
+            (unsigned)cfg->mbsfn_area_id);
+    return SRSRAN_ERROR;
+  }
+  if (cfg->estimator_alg != SRSRAN_ESTIMATOR_ALG_INTERPOLATE || np > 2 || sfi == 0 || sfi == 5) {
+    // AVERAGE: the reference interpolates from estimate rows it did not write (chest_dl.c:511-521, 719-721); ports
+    // 2 / 3: their CRS row is 1, yet the time interpolation starts from row 0 (518); subframes 0 / 5 are never MBSFN
+    fprintf(stderr, "[srsran_chest_dl] MBSFN subframes: INTERPOLATE, ports 0 / 1 and subframes other than 0 / 5 only\n");
+    return SRSRAN_ERROR;
+  }
+  const uint32_t nsf = 2 * SRSRAN_CP_NSYMB(q->cell.cp) * 12 * N, nrows12 = 12 * 12 * N;
+  for (uint32_t rx = 0; rx < nrx; rx++) {
+    hipMemcpyAsync(g->grid + rx * nsf, input[rx], nsf * sizeof(cf_t), hipMemcpyHostToDevice, g->stream);
+  }
+  if (cfg->sync_error_enable) {  // chest_dl.c:1007-1009 runs for MBSFN subframes too, on the CRS layout
+    if (correct_sync_error(q, sf->tti, sf->tdd_config, input)) {
+      return SRSRAN_ERROR;
+    }
+  } else {
+    memset(g->sync_err, 0, sizeof(g->sync_err));
+  }
+  if (g->mbsfn_loaded != (int)cfg->mbsfn_area_id) {
+    hipMemcpyAsync(g->d_mbsfn, it->second.data(), it->second.size() * sizeof(float2), hipMemcpyHostToDevice,
+                   g->stream);
+    g->mbsfn_loaded = cfg->mbsfn_area_id;
+  }
+  float kept[16] = {};
+  for (uint32_t rx = 0; rx < nrx; rx++) {
+    for (uint32_t p = 0; p < np; p++) {
+      kept[rx * 4 + p] = q->noise_estimate[rx][p];
+    }
+  }
+  hipMemcpyAsync(g->noise, kept, sizeof(kept), hipMemcpyHostToDevice, g->stream);
+  ChestArgs a{};
+  a.grid         = g->grid;
+  a.pilots       = g->pilots + sfi * kPilotsPerSf;
+  a.mbsfn_pilots = g->d_mbsfn + (size_t)sfi * 18 * N;
+  a.ce           = g->ce;
+  a.stats        = g->stats;
+  a.nof_prb      = N;
+  a.cell_id      = q->cell.id;
+  a.nports       = np;
+  a.nrx          = nrx;
+  a.nsymb        = SRSRAN_CP_NSYMB(q->cell.cp);
+  a.ce_stride    = nsf;
+  a.full_grid    = 1;
+  a.estimator    = 1;
+  a.noise_alg    = (uint32_t)cfg->noise_alg;
+  a.noise_in     = g->noise;
+  a.sf_index     = sfi;
+  set_filter(cfg, a);
+  if (chest_mbsfn_launch(a, g->stream) != hipSuccess) {
+    return SRSRAN_ERROR;
+  }
+  for (uint32_t p = 0; p < np; p++) {
+    for (uint32_t rx = 0; rx < nrx; rx++) {  // rows 0..11 (the rest of res->ce is left as it was)
+      hipMemcpyAsync(res->ce[p][rx], g->ce + (p * nrx + rx) * nsf, nrows12 * sizeof(cf_t), hipMemcpyDeviceToHost,
+                     g->stream);
+    }
+  }
+  float st[SRSRAN_MAX_PORTS * SRSRAN_MAX_PORTS * 8];
+  hipMemcpyAsync(st, g->stats, nrx * np * 8 * sizeof(float), hipMemcpyDeviceToHost, g->stream);
+  if (hipStreamSynchronize(g->stream) != hipSuccess) {
+    return SRSRAN_ERROR;
+  }
+  for (uint32_t rx = 0; rx < nrx; rx++) {  // RSRP / RSSI are not measured in MBSFN subframes: q keeps them
+    for (uint32_t p = 0; p < np; p++) {
+      st[(rx * np + p) * 8 + 1] = q->rsrp[rx][p];
+      st[(rx * np + p) * 8 + 2] = q->rssi[rx][p];
+    }
+  }
+  fill_res(q, st, res, false);  // no CFO estimate either (chest_dl.c:655)
+  return SRSRAN_SUCCESS;
+}
+
 int srsran_chest_dl_estimate_cfg(srsran_chest_dl_t*     q,
                                  srsran_dl_sf_cfg_t*    sf,
                                  srsran_chest_dl_cfg_t* cfg,
@@ -568,10 +713,13 @@ int srsran_chest_dl_estimate_cfg(srsran_chest_dl_t*     q,
   if (!q || !q->gpu || !sf || !cfg || !input || !res || q->cell.nof_prb == 0) {
     return SRSRAN_ERROR_INVALID_INPUTS;
   }
-  if (sf->sf_type != SRSRAN_SF_NORM || !cfg_supported(cfg)) {
-    fprintf(stderr, "[srsran_chest_dl] MBSFN subframes, the WIENER estimator, TRIANGLE / NONE filters, filter orders "
-                    "above 7 and rsrp_neighbour are not provided\n");
+  if ((sf->sf_type != SRSRAN_SF_NORM && sf->sf_type != SRSRAN_SF_MBSFN) || !cfg_supported(cfg)) {
+    fprintf(stderr, "[srsran_chest_dl] the WIENER estimator, Gauss filter orders above 7 and rsrp_neighbour are not "
+                    "provided\n");
     return SRSRAN_ERROR;
+  }
+  if (sf->sf_type == SRSRAN_SF_MBSFN) {
+    return estimate_mbsfn(q, sf, cfg, input, res);
   }
   if (!tdd_interp_ok(q->cell, sf->tdd_config, cfg)) {
     fprintf(stderr, "[srsran_chest_dl] INTERPOLATE in TDD special subframes with 2 CRS symbols (3 with extended CP): "
@@ -766,11 +914,7 @@ int estimate_batch(srsran_chest_dl_t*           q,
   a.pss      = g->pss;
   a.noise_in = g->noise;  // the state before the batch (REFS: unused)
   if (cfg) {
-    if (cfg->filter_coef[0] <= 0) {
-      a.filter_auto = 1;
-    } else {
-      a.filter_len = gauss(a.filter, (uint32_t)cfg->filter_coef[0], cfg->filter_coef[1]);
-    }
+    set_filter(cfg, a);
     a.estimator = cfg->estimator_alg == SRSRAN_ESTIMATOR_ALG_INTERPOLATE ? 1 : 0;
     a.noise_alg = (uint32_t)cfg->noise_alg;
   }

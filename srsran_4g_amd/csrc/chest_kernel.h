@@ -27,6 +27,9 @@ struct ChestArgs {
   float         filter[8]; // smoothing filter (srsran_chest_set_smooth_filter_gauss)
   uint32_t      filter_len;
   uint32_t      filter_auto; // Gauss order 4, stddev = 200 * noise of the (port, rx) (chest_dl.c:703-704)
+  uint32_t      filter_none; // SRSRAN_CHEST_FILTER_NONE: no average_pilots -- the LS estimates interpolated as they
+                             // are (chest_dl.c:724-725); TRIANGLE is filter[] = {w, 1 - 2w, w} (chest_common.c:62-68)
+  const float2* mbsfn_pilots; // chest_mbsfn_kernel: the MBSFN reference signals of the subframe, [3][6 nof_prb]
   // ---- estimator options beyond srsUE's defaults (chest_dl.c:437-555, 402-433, 703-745) ----
   uint32_t        estimator;  // 0 AVERAGE (one row, copied), 1 INTERPOLATE (full_grid: every row its own)
   uint32_t        noise_alg;  // 0 REFS (pilot residuals), 1 PSS, 2 EMPTY (subframes 0 / 5 only)
@@ -63,6 +66,9 @@ static constexpr size_t CHEST_STATS_PER_SF  = 4 * 4 * 8;               // floats
 // estimate (subframes 0 / 5), 0 when it is noise_in
 
 hipError_t chest_launch(const ChestArgs& a, hipStream_t stream, uint32_t nsf = 1);
+// estimate_port_mbsfn (chest_dl.c:836-865) of one MBSFN subframe (host-synchronous path): one workgroup per
+// (port, rx); ce rows 0..11 of the (port, rx) estimate written, stats [0] = noise (REFS, or noise_in), rest 0
+hipError_t chest_mbsfn_launch(const ChestArgs& a, hipStream_t stream);
 // diagnostic build (-DCHEST_STAMPS) only: phase clock stamps of every chest_kernel workgroup into d_buf
 hipError_t chest_set_stamps(void* d_buf);
 // device-side reduction of the per-(rx, port) stats of nsf subframes into out[b][4] =

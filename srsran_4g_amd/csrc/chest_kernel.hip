@@ -126,6 +126,67 @@ __device__ __forceinline__ void ivec(float2* col, uint32_t stride, cx in0, cx in
   }
 }
 
+// estimate_noise_pilots (chest_dl.c:356-399) for nsym >= 3 rows of nref LS estimates at pe (first pilot of row 0 at
+// subcarrier fidx0): each inner row against its neighbours, the residual power averaged over the inner rows
+__device__ float noise_rows(const cx* pe, uint32_t nsym, uint32_t nref, uint32_t fidx0, float* red)
+{
+  float noise = 0.f;
+  for (uint32_t i = 1; i < nsym - 1; i++) {
+    const uint32_t off = ((fidx0 < 3) ^ (i & 1)) ? 0 : 1;
+    const cx*      cur = pe + i * nref;
+    float          p   = 0.f;
+    for (uint32_t k = threadIdx.x; k < nref; k += CH_THREADS) {
+      cx t = cur[k];
+#pragma unroll
+      for (int nb = 0; nb < 2; nb++) {
+        const cx* o = pe + (nb == 0 ? i - 1 : i + 1) * nref;
+        if (k >= off) {
+          t = add(o[k - off], t);
+        }
+        if (k < nref + off - 1) {
+          t = add(o[1 - off + k], t);
+        }
+        if (off && k == 0) {
+          t = add(t, sub(scl(o[0], 2.0f), o[1]));
+        }
+        if (!off && k == nref - 1) {
+          t = add(t, sub(scl(o[nref - 2], 2.0f), o[nref - 1]));
+        }
+      }
+      t = sub(cur[k], scl(t, 1.0f / 5.0f));
+      p += t.r * t.r + t.i * t.i;
+    }
+    noise += block_sum(p, red) / (float)nref;
+  }
+  return noise / (float)(nsym - 2);
+}
+
+// the smoothing filter into LDS filt[] (all threads see it after the barrier inside): srsran_chest_set_smooth_filter_
+// gauss(filter, 4, noise * 200) when automatic (chest_common.c:70-95), else the host's taps; returns the length
+__device__ uint32_t load_filter(const ChestArgs& a, float noise, float* filt)
+{
+  uint32_t M = a.filter_len;
+  if (a.filter_auto) {
+    const float sd  = noise * 200.0f;
+    float       sum = 0.f;
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+      sum += expf(-powf((float)(k - 2), 2) / (2.0f * powf(sd, 2)));
+    }
+    M = isnormal(sum) ? 5 : 0;  // srsran_conv_same_cf with an empty filter yields zeros
+    if (threadIdx.x < 5) {
+      filt[threadIdx.x] = expf(-powf((float)((int)threadIdx.x - 2), 2) / (2.0f * powf(sd, 2))) * (1.0f / sum);
+    }
+  } else if (threadIdx.x == 0) {  // constant indices: a dynamic index into the by-value kernarg copies it to scratch
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      filt[k] = a.filter[k];
+    }
+  }
+  __syncthreads();
+  return M;
+}
+
 // fill_res (chest_dl.c:962-986) of one subframe from its per-(rx, port) stats st -> o[4]
 __device__ void finalize_sf(const float* st, uint32_t np, uint32_t nrx, uint32_t nof_prb, float sz, float nsymb,
                             float* o)
@@ -274,34 +335,7 @@ __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
   if (kept_noise) {
     noise = a.noise_in[rx * 4 + port];
   } else if (nsym >= 3) {
-    for (uint32_t i = 1; i < nsym - 1; i++) {
-      const uint32_t off = ((fidx0 < 3) ^ (i & 1)) ? 0 : 1;
-      const cx*      cur = pe + i * nref;
-      float          p   = 0.f;
-      for (uint32_t k = tid; k < nref; k += CH_THREADS) {
-        cx t = cur[k];
-#pragma unroll
-        for (int nb = 0; nb < 2; nb++) {
-          const cx* o = pe + (nb == 0 ? i - 1 : i + 1) * nref;
-          if (k >= off) {
-            t = add(o[k - off], t);
-          }
-          if (k < nref + off - 1) {
-            t = add(o[1 - off + k], t);
-          }
-          if (off && k == 0) {
-            t = add(t, sub(scl(o[0], 2.0f), o[1]));
-          }
-          if (!off && k == nref - 1) {
-            t = add(t, sub(scl(o[nref - 2], 2.0f), o[nref - 1]));
-          }
-        }
-        t = sub(cur[k], scl(t, 1.0f / 5.0f));
-        p += t.r * t.r + t.i * t.i;
-      }
-      noise += block_sum(p, red) / (float)nref;
-    }
-    noise /= (float)(nsym - 2);
+    noise = noise_rows(pe, nsym, nref, fidx0, red);
   } else {
     float p = 0.f;
     for (uint32_t k = tid; k + 2 < nref; k += CH_THREADS) {
@@ -317,6 +351,13 @@ __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
   uint32_t nr = nref;
   if (a.estimator == 1) {
     // INTERPOLATE: every CRS symbol smoothed on its own (below)
+  } else if (a.filter_none) {
+    // no average_pilots: AVERAGE interpolates the raw LS estimates -- with more than one CRS symbol the first 4 N_RB
+    // of them as one comb of spacing 3 (interp_lin_3 over pilot_estimates, chest_dl.c:476-481, 724-725)
+    nr = nsym > 1 ? 2 * nref : nref;
+    for (uint32_t k = tid; k < nr; k += CH_THREADS) {
+      comb[k] = pe[k];
+    }
   } else if (nsym > 1) {
     for (uint32_t k = tid; k < nref; k += CH_THREADS) {
       cx e0 = pe[(fidx0 < 3 ? 0 : 1) * nref + k], e1 = pe[(fidx0 < 3 ? 1 : 0) * nref + k];
@@ -336,26 +377,13 @@ __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
   __syncthreads();
   // the smoothing filter lives in LDS: a private array indexed by the tap loop would spill to scratch
   __shared__ float filt[8];
-  uint32_t         M = a.filter_len;
-  if (a.filter_auto) {  // srsran_chest_set_smooth_filter_gauss(filter, 4, noise * 200) (chest_common.c:70-95)
-    const float sd  = noise * 200.0f;
-    float       sum = 0.f;
-#pragma unroll
-    for (int k = 0; k < 5; k++) {
-      sum += expf(-powf((float)(k - 2), 2) / (2.0f * powf(sd, 2)));
+  const uint32_t   M = load_filter(a, noise, filt);
+  if (a.filter_none) {  // the estimates as they are (a 1-tap unit filter would give the same values)
+    const uint32_t n = a.estimator == 1 ? nsym * nref : nr;
+    for (uint32_t k = tid; k < n; k += CH_THREADS) {
+      avg[k] = a.estimator == 1 ? pe[k] : comb[k];
     }
-    M = isnormal(sum) ? 5 : 0;  // srsran_conv_same_cf with an empty filter yields zeros
-    if (tid < 5) {
-      filt[tid] = expf(-powf((float)((int)tid - 2), 2) / (2.0f * powf(sd, 2))) * (1.0f / sum);
-    }
-  } else if (tid == 0) {  // constant indices: a dynamic index into the by-value kernarg copies it to scratch
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      filt[k] = a.filter[k];
-    }
-  }
-  __syncthreads();
-  if (a.estimator == 1) {
+  } else if (a.estimator == 1) {
     for (uint32_t l = 0; l < nsym; l++) {
       conv_row(pe + l * nref, avg + l * nref, nref, filt, M);
     }
@@ -463,6 +491,85 @@ __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
   CH_STAMP(6);
   copy_jobs_finish(a.jobs, cr, bid, nblk);
   CH_STAMP(7);
+}
+
+// MBSFN subframe (estimate_port_mbsfn, chest_dl.c:836-865), one workgroup per (port, rx), ports 0 / 1 only:
+//   LS           the CRS of symbol 0 (2 N_RB, the subframe's CRS of the port pair) and the MBSFN reference signals
+//                of symbols 2 / 6 / 10 of the extended-CP grid (6 N_RB each, every 2nd subcarrier from 0 / 1 / 0:
+//                srsran_refsignal_mbsfn_get_sf, refsignal_dl.c:474-502) in one array of 20 N_RB
+//   noise (REFS) estimate_noise_pilots with npilots = 20 N_RB over 3 "symbols" (chest_dl.c:325-399): the array cut
+//                into rows of floor(20 N_RB / 3), the middle one against the other two, fidx 1
+//   smoothing    average_pilots (557-600): the CRS row copied, each MBSFN row filtered on its own
+//   interpolation interpolate_pilots (444-521): the CRS row into ce row 0 (spacing 6), the MBSFN rows into rows
+//                2 / 6 / 10 (spacing 2), then rows 1, 3-5, 7-9 between them and row 11 extrapolated
+__global__ __launch_bounds__(CH_THREADS) void chest_mbsfn_kernel(ChestArgs a)
+{
+  __shared__ cx    pe[20 * CHEST_MAX_PRB];
+  __shared__ cx    avg[20 * CHEST_MAX_PRB];
+  __shared__ float red[CH_THREADS / 64];
+  __shared__ float filt[8];
+  const uint32_t   port = blockIdx.x / a.nrx, rx = blockIdx.x % a.nrx, tid = threadIdx.x;
+  const uint32_t   nref = 2 * a.nof_prb, nm = 6 * a.nof_prb, np = 20 * a.nof_prb, nre = 12 * a.nof_prb;
+  const float2*    in    = a.grid + (size_t)rx * 2 * a.nsymb * nre;
+  const float2*    pil   = a.pilots + (size_t)(port / 2) * 4 * CHEST_MAX_NREF;  // symbol 0's CRS first
+  const uint32_t   fidx0 = (crs_v(port, 0) + a.cell_id % 6) % 6;
+  for (uint32_t k = tid; k < np; k += CH_THREADS) {
+    cx r, p;
+    if (k < nref) {
+      r = ld2(in, crs_nsymbol(0, port, a.nsymb) * nre + fidx0 + 6 * k);
+      p = ld2(pil, k);
+    } else {
+      const uint32_t m = k - nref, l = m / nm, i = m % nm;
+      r                = ld2(in, (2 + 4 * l) * nre + (l == 1 ? 1u : 0u) + 2 * i);
+      p                = ld2(a.mbsfn_pilots, m);
+    }
+    pe[k] = mul(r, conj(p));
+  }
+  __syncthreads();
+  const float    noise = a.noise_alg == 0 ? noise_rows(pe, 3, np / 3, 1, red) : a.noise_in[rx * 4 + port];
+  const uint32_t M     = load_filter(a, noise, filt);
+  for (uint32_t k = tid; k < np; k += CH_THREADS) {
+    if (k < nref || a.filter_none) {
+      avg[k] = pe[k];
+    }
+  }
+  if (!a.filter_none) {
+    for (uint32_t l = 0; l < 3; l++) {
+      conv_row(pe + nref + l * nm, avg + nref + l * nm, nm, filt, M);
+    }
+  }
+  __syncthreads();
+  float2* ce = a.ce + (size_t)(port * a.nrx + rx) * a.ce_stride;
+  for (uint32_t j = tid; j < nre; j += CH_THREADS) {
+    float2*  col = ce + j;
+    const cx c0  = interp_at(avg, nref, 6, fidx0, j);
+    const cx m0  = interp_at(avg + nref, nm, 2, 0, j);
+    const cx m1  = interp_at(avg + nref + nm, nm, 2, 1, j);
+    const cx m2  = interp_at(avg + nref + 2 * nm, nm, 2, 0, j);
+    col[0]                = make_float2(c0.r, c0.i);
+    col[(size_t)2 * nre]  = make_float2(m0.r, m0.i);
+    col[(size_t)6 * nre]  = make_float2(m1.r, m1.i);
+    col[(size_t)10 * nre] = make_float2(m2.r, m2.i);
+    ivec(col, nre, c0, m0, nullptr, 2, 1, 1);
+    ivec(col, nre, m0, m1, nullptr, 4, 3, 3);
+    ivec(col, nre, m1, m2, nullptr, 4, 3, 7);
+    ivec(col, nre, m1, m2, &m2, 4, 1, 11);
+  }
+  if (tid == 0) {
+    float* s = a.stats + (size_t)(rx * a.nports + port) * 8;
+    s[0]     = noise;
+    s[1] = s[2] = s[3] = s[4] = s[5] = 0.f;
+  }
+}
+
+hipError_t chest_mbsfn_launch(const ChestArgs& a, hipStream_t stream)
+{
+  StageScope timing_scope(ST_CHEST, stream);
+  if (a.nports > 2 || a.nof_prb > CHEST_MAX_PRB || !a.mbsfn_pilots) {
+    return hipErrorInvalidValue;
+  }
+  hipLaunchKernelGGL(chest_mbsfn_kernel, dim3(a.nports * a.nrx), dim3(CH_THREADS), 0, stream, a);
+  return hipGetLastError();
 }
 
 hipError_t chest_set_stamps(void* d_buf)

@@ -110,6 +110,8 @@ void cfo_table_free(CfoTab& t)
   t = CfoTab();
 }
 
+uint32_t cp_len(uint32_t c, uint32_t N) { return (uint32_t)ceilf((float)c * (float)N / 2048.0f); }  // SRSRAN_CP_LEN
+
 struct OfdmGpu {
   hipStream_t stream = nullptr;
   float2*     d_in   = nullptr;
@@ -117,9 +119,26 @@ struct OfdmGpu {
   size_t      in_cap = 0, out_cap = 0;
   OfdmArgs    proto{};
   CfoTab      cfo;
+  bool        mbsfn = false;  // cfg.sf_type == SRSRAN_SF_MBSFN (ofdm.c:219-225)
+  uint32_t    non_mbsfn_region = 2;
 };
 
-uint32_t cp_len(uint32_t c, uint32_t N) { return (uint32_t)ceilf((float)c * (float)N / 2048.0f); }  // SRSRAN_CP_LEN
+// slot 0 of an MBSFN subframe (ofdm_rx_slot_mbsfn, ofdm.c:522-535): the first `nr` symbols with the normal cyclic
+// prefixes, the guard SRSRAN_NON_MBSFN_REGION_GUARD_LENGTH (phy_common.h:166-169) before symbol nr, extended cyclic
+// prefixes after it -- the sample offset of each of the SRSRAN_CP_NSYMB(SRSRAN_CP_EXT) symbols
+void mbsfn_offsets(uint32_t N, uint32_t nr, uint32_t* off)
+{
+  const uint32_t cpn0 = cp_len(160, N), cpn = cp_len(144, N), cpe = cp_len(512, N);
+  uint32_t       pos  = 0;
+  for (uint32_t i = 0; i < 6; i++) {
+    if (i == nr) {
+      pos += nr == 1 ? cpe - cpn0 : 2 * cpe - cpn0 - cpn;
+    }
+    pos += i >= nr ? cpe : (i == 0 ? cpn0 : cpn);
+    off[i] = pos;
+    pos += N;
+  }
+}
 
 bool grow(void** p, size_t* cap, size_t need)
 {
@@ -162,6 +181,10 @@ int configure(srsran_ofdm_t* q, uint32_t nof_prb, uint32_t symbol_sz)
   a.sf_len         = 2 * (a.nsymb * N + a.cp0 + (a.nsymb - 1) * a.cp);
   a.nrx            = 1;
   a.norm           = q->cfg.normalize ? 1.0f / sqrtf((float)N) : 1.0f;
+  if (g->mbsfn) {
+    a.mbsfn = 1;
+    mbsfn_offsets(N, g->non_mbsfn_region, a.mbsfn_off);
+  }
   g->proto         = a;
   q->cfg.nof_prb   = nof_prb;
   q->cfg.symbol_sz = N;
@@ -176,6 +199,9 @@ int run(srsran_ofdm_t* q, const float2* d_in, float2* d_out, uint32_t nrx, uint3
 {
   OfdmGpu* g = (OfdmGpu*)q->gpu;
   OfdmArgs a = g->proto;
+  if (a.mbsfn && a.nsymb != 6) {  // MBSFN layouts are extended-CP ones (see srsran_ofdm_rx_sf_ng)
+    return SRSRAN_ERROR;
+  }
   a.in       = d_in;
   a.out      = d_out;
   a.nrx      = nrx;
@@ -204,7 +230,8 @@ int srsran_ofdm_rx_init_cfg(srsran_ofdm_t* q, srsran_ofdm_cfg_t* cfg)
   if (!q || !cfg || cfg->nof_prb == 0 || cfg->nof_prb > 110) {
     return SRSRAN_ERROR_INVALID_INPUTS;
   }
-  if ((cfg->cp != SRSRAN_CP_NORM && cfg->cp != SRSRAN_CP_EXT) || cfg->sf_type != SRSRAN_SF_NORM ||
+  if ((cfg->cp != SRSRAN_CP_NORM && cfg->cp != SRSRAN_CP_EXT) ||
+      (cfg->sf_type != SRSRAN_SF_NORM && cfg->sf_type != SRSRAN_SF_MBSFN) ||
       std::isnormal(cfg->freq_shift_f) ||
       std::isnormal(cfg->rx_window_offset) || std::isnormal(cfg->phase_compensation_hz) || cfg->keep_dc) {
     fprintf(stderr, "[srsran_ofdm] only the srsran_ue_dl receiver configuration is provided\n");
@@ -220,6 +247,7 @@ int srsran_ofdm_rx_init_cfg(srsran_ofdm_t* q, srsran_ofdm_cfg_t* cfg)
   q->max_prb = cfg->nof_prb;
   OfdmGpu* g = new OfdmGpu();
   q->gpu     = g;
+  g->mbsfn   = cfg->sf_type == SRSRAN_SF_MBSFN;  // non-MBSFN region 2 by default (ofdm.c:222)
   if (hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking) != hipSuccess) {
     srsran_ofdm_rx_free(q);
     return SRSRAN_ERROR;
@@ -270,12 +298,49 @@ void srsran_ofdm_set_normalize(srsran_ofdm_t* q, bool normalize_enable)
   }
 }
 
+void srsran_ofdm_set_non_mbsfn_region(srsran_ofdm_t* q, uint8_t non_mbsfn_region)
+{
+  if (q && q->gpu) {
+    OfdmGpu* g          = (OfdmGpu*)q->gpu;
+    g->non_mbsfn_region = non_mbsfn_region;
+    if (g->mbsfn) {
+      mbsfn_offsets(g->proto.N, non_mbsfn_region, g->proto.mbsfn_off);
+    }
+  }
+}
+
+int srsran_ofdm_rx_init_mbsfn(srsran_ofdm_t* q, srsran_cp_t cp, cf_t* in_buffer, cf_t* out_buffer, uint32_t max_prb)
+{
+  srsran_ofdm_cfg_t cfg;  // ofdm.c:285-297
+  memset(&cfg, 0, sizeof(cfg));
+  cfg.cp         = cp;
+  cfg.in_buffer  = in_buffer;
+  cfg.out_buffer = out_buffer;
+  cfg.nof_prb    = max_prb;
+  cfg.sf_type    = SRSRAN_SF_MBSFN;
+  return srsran_ofdm_rx_init_cfg(q, &cfg);
+}
+
 void srsran_ofdm_rx_sf_ng(srsran_ofdm_t* q, cf_t* input, cf_t* output)
 {
-  if (!q || !q->gpu || !input || !output) {
+  if (!q || !q->gpu) {
     return;
   }
-  OfdmGpu*     g  = (OfdmGpu*)q->gpu;
+  OfdmGpu* g = (OfdmGpu*)q->gpu;
+  if (g->mbsfn) {
+    // ofdm.c:576-578: an MBSFN object transforms its configured buffers whatever the arguments say; slot 0 has the
+    // extended-CP symbol count (nof_symbols_mbsfn), slot 1 the object's own layout -- provided for extended CP, the
+    // configuration srsran_ue_dl gives it (ue_dl.c:218)
+    input  = q->cfg.in_buffer;
+    output = q->cfg.out_buffer;
+    if (q->cfg.cp != SRSRAN_CP_EXT) {
+      fprintf(stderr, "[srsran_ofdm] MBSFN subframes with a normal-CP object are not provided\n");
+      return;
+    }
+  }
+  if (!input || !output) {
+    return;
+  }
   const size_t ni = q->sf_sz, no = 2 * q->nof_symbols * (size_t)q->nof_re;
   if (!grow((void**)&g->d_in, &g->in_cap, ni * sizeof(cf_t)) || !grow((void**)&g->d_out, &g->out_cap, no * sizeof(cf_t))) {
     return;

@@ -22,6 +22,10 @@ struct OfdmArgs {
   float         norm;      // 1 or 1/sqrt(N) (srsran_ofdm_cfg_t.normalize)
   const float2* cfo_tab;   // srsran_vec_apply_cfo's phasor of every sample of a subframe (cfo_table_launch,
                            // sf_len entries), applied as z = x * tab[n], n from the subframe start; nullptr = off
+  // MBSFN subframes (ofdm_rx_slot_mbsfn, ofdm.c:522-535): slot 0's symbols start at mbsfn_off[i] (the non-MBSFN
+  // region's normal cyclic prefixes, the guard, then extended ones); 0 = every slot as cp0 / cp say
+  uint32_t      mbsfn;
+  uint32_t      mbsfn_off[7];
   int           nstages;
   int           radix[OFDM_MAX_STAGES];
   uint32_t      ns_magic[OFDM_MAX_STAGES];  // ceil(2^32 / Ns) of every stage (j / Ns by __umulhi)

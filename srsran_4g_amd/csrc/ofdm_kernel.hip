@@ -174,7 +174,7 @@ __global__ __launch_bounds__(OFDM_THREADS) void ofdm_rx_kernel(OfdmArgs a)
   const uint32_t    sym = blockIdx.x, rx = blockIdx.y, sf = blockIdx.z;
   const uint32_t    N = a.N, ns = a.nsymb, slot = sym / ns, i = sym % ns;
   const uint32_t    slot_sz = ns * N + a.cp0 + (ns - 1) * a.cp;
-  const uint32_t    off     = slot * slot_sz + a.cp0 + i * (N + a.cp);
+  const uint32_t    off     = a.mbsfn && slot == 0 ? a.mbsfn_off[i] : slot * slot_sz + a.cp0 + i * (N + a.cp);
   const float2*     src     = a.in + ((size_t)sf * a.nrx + rx) * a.sf_len + off;
   {  // all of a thread's sample loads (and CFO factors) issued before the first use: one HBM round trip
     constexpr int U = OFDM_MAX_N / OFDM_THREADS;

@@ -142,6 +142,15 @@ int srsran_ue_dl_init(srsran_ue_dl_t* q, cf_t* input[SRSRAN_MAX_PORTS], uint32_t
       return SRSRAN_ERROR;
     }
   }
+  ofdm_cfg.in_buffer  = input ? input[0] : nullptr;  // ue_dl.c:104-111: the MBSFN transform reads antenna 0 only
+  ofdm_cfg.out_buffer = q->sf_symbols[0];
+  ofdm_cfg.sf_type    = SRSRAN_SF_MBSFN;
+  if (srsran_ofdm_rx_init_cfg(&q->fft_mbsfn, &ofdm_cfg)) {
+    fprintf(stderr, "[srsran_ue_dl] Error initiating FFT for MBSFN subframes\n");
+    srsran_ue_dl_free(q);
+    return SRSRAN_ERROR;
+  }
+  srsran_ofdm_set_non_mbsfn_region(&q->fft_mbsfn, 2);
   if (srsran_chest_dl_init(&q->chest, max_prb, nof_rx_antennas) || srsran_chest_dl_res_init(&q->chest_res, max_prb) ||
       srsran_pdsch_init_ue(&q->pdsch, max_prb, nof_rx_antennas)) {
     fprintf(stderr, "[srsran_ue_dl] Error initiating channel estimator / PDSCH\n");
@@ -199,6 +208,9 @@ void srsran_ue_dl_free(srsran_ue_dl_t* q)
     }
     free(q->sf_symbols[j]);
   }
+  if (q->fft_mbsfn.gpu) {
+    srsran_ofdm_rx_free(&q->fft_mbsfn);
+  }
   if (q->chest.gpu) {
     srsran_chest_dl_free(&q->chest);
   }
@@ -219,6 +231,10 @@ int srsran_ue_dl_set_cell(srsran_ue_dl_t* q, srsran_cell_t cell)
       fprintf(stderr, "[srsran_ue_dl] Error setting FFT sampling frequency\n");
       return SRSRAN_ERROR;
     }
+  }
+  if (srsran_ofdm_rx_set_prb(&q->fft_mbsfn, SRSRAN_CP_EXT, cell.nof_prb)) {  // ue_dl.c:218-221
+    fprintf(stderr, "[srsran_ue_dl] Error resizing MBSFN FFT\n");
+    return SRSRAN_ERROR;
   }
   if (srsran_chest_dl_set_cell(&q->chest, cell) || srsran_pdsch_set_cell(&q->pdsch, cell)) {
     return SRSRAN_ERROR;
@@ -253,15 +269,24 @@ static int fft_estimate(srsran_ue_dl_t* q, srsran_dl_sf_cfg_t* sf, srsran_ue_dl_
   if (!q || !q->gpu || !sf || !cfg) {
     return SRSRAN_ERROR_INVALID_INPUTS;
   }
-  if (sf->sf_type != SRSRAN_SF_NORM) {
-    fprintf(stderr, "[srsran_ue_dl] MBSFN subframes are not provided\n");
-    return SRSRAN_ERROR;
-  }
-  for (uint32_t j = 0; j < q->nof_rx_antennas; j++) {
-    if (input) {
-      srsran_ofdm_rx_sf_ng(&q->fft[j], input[j], q->sf_symbols[j]);
-    } else {
-      srsran_ofdm_rx_sf(&q->fft[j]);
+  if (sf->sf_type == SRSRAN_SF_MBSFN) {
+    // ue_dl.c:353-356 / 373-376: fft_mbsfn, configured on antenna 0's buffers, runs once per antenna (the same
+    // transform each time; its _ng form ignores the arguments, ofdm.c:576-578): the other antennas' grids keep the
+    // previous subframe
+    if (!q->fft_mbsfn.cfg.in_buffer) {
+      fprintf(stderr, "[srsran_ue_dl] MBSFN subframes need the input buffers given to srsran_ue_dl_init\n");
+      return SRSRAN_ERROR;
+    }
+    srsran_ofdm_rx_sf(&q->fft_mbsfn);
+  } else if (sf->sf_type != SRSRAN_SF_NORM) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  } else {
+    for (uint32_t j = 0; j < q->nof_rx_antennas; j++) {
+      if (input) {
+        srsran_ofdm_rx_sf_ng(&q->fft[j], input[j], q->sf_symbols[j]);
+      } else {
+        srsran_ofdm_rx_sf(&q->fft[j]);
+      }
     }
   }
   if (srsran_chest_dl_estimate_cfg(&q->chest, sf, &cfg->chest_cfg, q->sf_symbols, &q->chest_res)) {
@@ -713,19 +738,24 @@ void srsran_ue_dl_set_mi_manual(srsran_ue_dl_t* q, uint32_t mi_idx)
   }
 }
 
-int srsran_ue_dl_set_mbsfn_area_id(srsran_ue_dl_t* q, uint16_t mbsfn_area_id)
+int srsran_ue_dl_set_mbsfn_area_id(srsran_ue_dl_t* q, uint16_t mbsfn_area_id)  // ue_dl.c:277-294 (PMCH: not provided)
 {
   if (!q) {
     return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  if (srsran_chest_dl_set_mbsfn_area_id(&q->chest, mbsfn_area_id)) {
+    fprintf(stderr, "[srsran_ue_dl] Error setting MBSFN area ID\n");
+    return SRSRAN_ERROR;
   }
   q->current_mbsfn_area_id = mbsfn_area_id;
   return SRSRAN_SUCCESS;
 }
 
-void srsran_ue_dl_set_non_mbsfn_region(srsran_ue_dl_t* q, uint8_t non_mbsfn_region_length)
+void srsran_ue_dl_set_non_mbsfn_region(srsran_ue_dl_t* q, uint8_t non_mbsfn_region_length)  // ue_dl.c:258-261
 {
-  (void)q;
-  (void)non_mbsfn_region_length;  // MBSFN subframes are refused by decode_fft_estimate
+  if (q) {
+    srsran_ofdm_set_non_mbsfn_region(&q->fft_mbsfn, non_mbsfn_region_length);
+  }
 }
 
 int srsran_ue_dl_dci_to_pdsch_grant(srsran_ue_dl_t*       q,

@@ -101,7 +101,7 @@ class srsran_ue_dl_cfg_t(ctypes.Structure):
 class srsran_ue_dl_t(ctypes.Structure):
     _fields_ = [("cell", srsran_cell_t), ("nof_rx_antennas", u32), ("current_mbsfn_area_id", ctypes.c_uint16),
                 ("pdsch", srsran_pdsch_t), ("chest", srsran_chest_dl_t), ("chest_res", srsran_chest_dl_res_t),
-                ("fft", srsran_ofdm_t * MAX_PORTS), ("sf_symbols", ctypes.c_void_p * MAX_PORTS),
+                ("fft", srsran_ofdm_t * MAX_PORTS), ("fft_mbsfn", srsran_ofdm_t), ("sf_symbols", ctypes.c_void_p * MAX_PORTS),
                 ("gpu", ctypes.c_void_p)]
 
 
@@ -145,6 +145,10 @@ def lib():
             "srsran_ofdm_rx_sf": ([ctypes.POINTER(srsran_ofdm_t)], None),
             "srsran_ofdm_rx_sf_ng": ([ctypes.POINTER(srsran_ofdm_t), P, P], None),
             "srsran_ofdm_set_normalize": ([ctypes.POINTER(srsran_ofdm_t), ctypes.c_bool], None),
+            "srsran_ofdm_rx_init_mbsfn": ([ctypes.POINTER(srsran_ofdm_t), ctypes.c_int, P, P, u32], ctypes.c_int),
+            "srsran_ofdm_set_non_mbsfn_region": ([ctypes.POINTER(srsran_ofdm_t), ctypes.c_uint8], None),
+            "srsran_chest_dl_set_mbsfn_area_id": ([CH, ctypes.c_uint16], ctypes.c_int),
+            "srsran_ue_dl_set_non_mbsfn_region": ([UE, ctypes.c_uint8], None),
             "srsran_ofdm_rx_gpu": ([ctypes.POINTER(srsran_ofdm_t), P, P, u32, u32, ctypes.c_float, P], ctypes.c_int),
             "srsran_cfo_init": ([ctypes.POINTER(srsran_cfo_t), u32], ctypes.c_int),
             "srsran_cfo_free": ([ctypes.POINTER(srsran_cfo_t)], None),
@@ -205,10 +209,12 @@ def cell(nof_prb=100, nof_ports=2, cell_id=1, phich_res=2, cp=0, tdd=False):
     return c
 
 
-def sf_cfg(tti, cfi=0, tdd=None):
-    """srsran_dl_sf_cfg_t; tdd = (uplink-downlink configuration, special-subframe configuration) or None"""
+def sf_cfg(tti, cfi=0, tdd=None, mbsfn=False):
+    """srsran_dl_sf_cfg_t; tdd = (uplink-downlink configuration, special-subframe configuration) or None; mbsfn:
+    sf_type = SRSRAN_SF_MBSFN"""
     sf = srsran_dl_sf_cfg_t()
     sf.tti, sf.cfi = tti, cfi
+    sf.sf_type = 1 if mbsfn else 0
     if tdd is not None:
         sf.tdd_config.sf_config, sf.tdd_config.ss_config, sf.tdd_config.configured = tdd[0], tdd[1], True
     return sf
@@ -226,26 +232,48 @@ def srsue_chest_cfg():
     return c
 
 
-def chest_cfg(estimator=0, noise_alg=0, filter_order=4, filter_std=1.0, sync_error=False):
+def chest_cfg(estimator=0, noise_alg=0, filter_order=4, filter_std=1.0, sync_error=False, filter_type=0,
+              mbsfn_area_id=0):
     """srsran_chest_dl_cfg_t with srsUE's ue.conf knobs (phy_common.cc:83-108): interpolate_subframe_enabled
     (estimator 1 INTERPOLATE), snr_estim_alg (noise_alg 0 refs / 1 pss / 2 empty), estimator_fil_order /
-    _stddev (order 0 = estimator_fil_auto), correct_sync_error"""
+    _stddev (order 0 = estimator_fil_auto), correct_sync_error; filter_type 0 GAUSS / 1 TRIANGLE (w = filter_order)
+    / 2 NONE"""
     c = srsue_chest_cfg()
     c.estimator_alg, c.noise_alg = estimator, noise_alg
+    c.filter_type = filter_type
     c.filter_coef[0], c.filter_coef[1] = filter_order, filter_std
     c.sync_error_enable = bool(sync_error)
+    c.mbsfn_area_id = mbsfn_area_id
     return c
 
 
-class OfdmRx:
-    """srsran_ofdm_t receiver (srsran_ue_dl configuration)."""
+def mbsfn_chest_cfg(area=1):
+    """srsUE's estimator configuration for MBSFN subframes (cc_worker.cc:96-100, 336-338): TRIANGLE 0.1,
+    INTERPOLATE, PSS noise"""
+    return chest_cfg(estimator=1, noise_alg=1, filter_order=0.1, filter_std=0.0, filter_type=1, mbsfn_area_id=area)
 
-    def __init__(self, nof_prb, normalize=False, cp=0):
+
+class OfdmRx:
+    """srsran_ofdm_t receiver (srsran_ue_dl configuration).  mbsfn: an MBSFN object (srsran_ofdm_rx_init_mbsfn,
+    extended CP) with its own in / out buffers, which it transforms whatever srsran_ofdm_rx_sf_ng is given
+    (ofdm.c:576-578); non_mbsfn_region: srsran_ofdm_set_non_mbsfn_region."""
+
+    def __init__(self, nof_prb, normalize=False, cp=0, mbsfn=False, non_mbsfn_region=2):
+        self.q = srsran_ofdm_t()
+        self.mbsfn = mbsfn
+        if mbsfn:
+            n = symbol_sz_for(nof_prb)
+            self.inb = np.zeros(15 * n, np.complex64)
+            self.outb = np.zeros(12 * 12 * nof_prb, np.complex64)
+            if lib().srsran_ofdm_rx_init_mbsfn(ctypes.byref(self.q), 1, self.inb.ctypes.data, self.outb.ctypes.data,
+                                               nof_prb):
+                raise RuntimeError("srsran_ofdm_rx_init_mbsfn failed")
+            lib().srsran_ofdm_set_non_mbsfn_region(ctypes.byref(self.q), non_mbsfn_region)
+            return
         self.cfg = srsran_ofdm_cfg_t()
         self.cfg.nof_prb = nof_prb
         self.cfg.normalize = normalize
         self.cfg.cp = cp
-        self.q = srsran_ofdm_t()
         if lib().srsran_ofdm_rx_init_cfg(ctypes.byref(self.q), ctypes.byref(self.cfg)):
             raise RuntimeError("srsran_ofdm_rx_init_cfg failed")
 
@@ -257,6 +285,10 @@ class OfdmRx:
         x = np.ascontiguousarray(samples, np.complex64)
         assert x.size == self.q.sf_sz
         out = np.zeros(2 * self.q.nof_symbols * self.q.nof_re, np.complex64)
+        if self.mbsfn:  # the configured buffers (the _ng arguments are ignored for MBSFN objects)
+            self.inb[:] = x
+            lib().srsran_ofdm_rx_sf_ng(ctypes.byref(self.q), out.ctypes.data, out.ctypes.data)
+            return self.outb.copy()
         lib().srsran_ofdm_rx_sf_ng(ctypes.byref(self.q), x.ctypes.data, out.ctypes.data)
         return out
 
@@ -269,6 +301,10 @@ class OfdmRx:
             self.free()
         except Exception:
             pass
+
+
+def symbol_sz_for(nof_prb):
+    return lib().srsran_symbol_sz(nof_prb)
 
 
 def cfo_correct(x, freq):
@@ -294,11 +330,15 @@ class ChestDl:
         self.cell = cell_
         self.nrx = nof_rx
 
-    def estimate(self, grids, tti, cfg=None, tdd=None):
-        """grids: (nrx, 14*12*nof_prb) complex64 -> (ce[port][rx] arrays, res); tdd = (sf_config, ss_config)"""
+    def set_mbsfn_area_id(self, area):
+        return lib().srsran_chest_dl_set_mbsfn_area_id(ctypes.byref(self.q), area)
+
+    def estimate(self, grids, tti, cfg=None, tdd=None, mbsfn=False):
+        """grids: (nrx, 14*12*nof_prb) complex64 -> (ce[port][rx] arrays, res); tdd = (sf_config, ss_config);
+        mbsfn: an MBSFN subframe (rows 12 / 13 of the returned estimate are those of the previous call)"""
         grids = [np.ascontiguousarray(g, np.complex64) for g in grids]
         ptrs = (ctypes.c_void_p * MAX_PORTS)(*[g.ctypes.data for g in grids] + [None] * (MAX_PORTS - len(grids)))
-        sf = sf_cfg(tti, 0, tdd)
+        sf = sf_cfg(tti, 0, tdd, mbsfn)
         if cfg is None:
             rc = lib().srsran_chest_dl_estimate(ctypes.byref(self.q), ctypes.byref(sf), ctypes.addressof(ptrs),
                                                 ctypes.byref(self.res))
@@ -442,11 +482,17 @@ class Pdsch:
 class UeDl:
     """srsran_ue_dl_t: host-synchronous decode_fft_estimate / decode_pdsch and the device batch."""
 
-    def __init__(self, cell_, nof_rx, tdd=None):
-        """tdd = (sf_config, ss_config): the TDD configuration every call's srsran_dl_sf_cfg_t carries"""
+    def __init__(self, cell_, nof_rx, tdd=None, inputs=False):
+        """tdd = (sf_config, ss_config): the TDD configuration every call's srsran_dl_sf_cfg_t carries; inputs: give
+        srsran_ue_dl_init input buffers (the guru path, fft_estimate_guru; MBSFN subframes need them)"""
         self.tdd = tdd
         self.q = srsran_ue_dl_t()
-        if lib().srsran_ue_dl_init(ctypes.byref(self.q), None, cell_.nof_prb, nof_rx):
+        self.inb = None
+        ptrs = None
+        if inputs:
+            self.inb = [np.zeros(15 * symbol_sz_for(cell_.nof_prb), np.complex64) for _ in range(nof_rx)]
+            ptrs = (ctypes.c_void_p * MAX_PORTS)(*[b.ctypes.data for b in self.inb] + [None] * (MAX_PORTS - nof_rx))
+        if lib().srsran_ue_dl_init(ctypes.byref(self.q), ptrs, cell_.nof_prb, nof_rx):
             raise RuntimeError("srsran_ue_dl_init failed (no HIP device?)")
         if lib().srsran_ue_dl_set_cell(ctypes.byref(self.q), cell_):
             raise RuntimeError("srsran_ue_dl_set_cell failed")
@@ -469,11 +515,33 @@ class UeDl:
         self.last_cfi = sf.cfi  # decoded from the PCFICH (1/2-port cells), else the caller's
         return ret
 
-    def find_dl_dci(self, tti, cfi, rnti, tm=2, common_ss=True):
+    def fft_estimate_guru(self, samples, tti, cfi, mbsfn=False):
+        """srsran_ue_dl_decode_fft_estimate on the buffers given to srsran_ue_dl_init (inputs=True): samples copied
+        into them first; mbsfn: an MBSFN subframe (self.cfg.chest_cfg should then be mbsfn_chest_cfg)"""
+        for b, v in zip(self.inb, samples):
+            b[:] = np.asarray(v, np.complex64)
+        sf = sf_cfg(tti, cfi, self.tdd, mbsfn)
+        ret = lib().srsran_ue_dl_decode_fft_estimate(ctypes.byref(self.q), ctypes.byref(sf), ctypes.byref(self.cfg))
+        self.last_cfi = sf.cfi
+        return ret
+
+    def set_non_mbsfn_region(self, n):
+        lib().srsran_ue_dl_set_non_mbsfn_region(ctypes.byref(self.q), n)
+
+    def chest_res_ce(self):
+        """the last estimate (chest_res.ce) as (nports, nrx, 14 * 12 * nof_prb)"""
+        n = (12 if self.cell.cp else 14) * 12 * self.cell.nof_prb
+        ce = np.zeros((self.cell.nof_ports, self.nrx, n), np.complex64)
+        for p in range(self.cell.nof_ports):
+            for r in range(self.nrx):
+                ctypes.memmove(ce[p, r].ctypes.data, self.q.chest_res.ce[p][r], n * 8)
+        return ce
+
+    def find_dl_dci(self, tti, cfi, rnti, tm=2, common_ss=True, mbsfn=False):
         """srsran_ue_dl_find_dl_dci (after fft_estimate) -> list of srsran_dci_dl_t"""
         from . import pdcch as PD
         PD.lib()
-        sf = sf_cfg(tti, cfi, self.tdd)
+        sf = sf_cfg(tti, cfi, self.tdd, mbsfn)
         self.cfg.cfg.tm = tm
         self.cfg.cfg.dci_common_ss = common_ss
         out = (PD.srsran_dci_dl_t * 5)()

@@ -337,6 +337,59 @@ def ofdm_tx(grid, N, cp=0):
     return np.concatenate(out)
 
 
+# ---------------- MBSFN subframes (36.211 6.10.2 as srsRAN's eNB places them) ----------------
+def mbsfn_rs(area, nof_prb, sf_idx):
+    """the MBSFN reference signal of subframe sf_idx, area N_MBSFN: (3, 6 N_RB) for the grid symbols 2 / 6 / 10 of
+    the extended-CP layout -- c_init = 2^9 (7 (ns + 1) + l + 1)(2 N_MBSFN + 1) + N_MBSFN with l = symbol mod 6 of slot
+    ns, r(m) = (1 - 2c(2m') + j (1 - 2c(2m' + 1))) / sqrt 2, m' = m + 3 (N_RB^max - N_RB)"""
+    out = np.zeros((3, 6 * nof_prb), np.complex128)
+    for i, sym in enumerate((2, 6, 10)):
+        ns = 2 * sf_idx + (0 if sym < 6 else 1)
+        c = gold((1 << 9) * (7 * (ns + 1) + sym % 6 + 1) * (2 * area + 1) + area, 20 * 110)
+        m = np.arange(6 * nof_prb) + 3 * (110 - nof_prb)
+        out[i] = ((1 - 2.0 * c[2 * m]) + 1j * (1 - 2.0 * c[2 * m + 1])) / math.sqrt(2)
+    return out
+
+
+def mbsfn_grid(nof_prb, cell_id, sf_idx, area, non_mbsfn_region, rng=None):
+    """port 0's (12, 12 N_RB) grid of an MBSFN subframe as srsRAN's eNB fills it (enb_dl.c:345-356,
+    srsran_refsignal_mbsfn_put_sf refsignal_dl.c:316-348): the CRS of symbol 0, the MBSFN reference signals at
+    subcarriers 2i, 2i + 1, 2i of symbols 2 / 6 / 10, and (rng given) QPSK PMCH symbols on the other REs of the
+    MBSFN region (symbols >= non_mbsfn_region).  The control region's PCFICH / PDCCH are the caller's."""
+    nre = 12 * nof_prb
+    g = np.zeros((12, nre), np.complex128)
+    if rng is not None:
+        b = rng.integers(0, 2, (12 - non_mbsfn_region, 2 * nre))
+        g[non_mbsfn_region:] = ((1 - 2.0 * b[:, 0::2]) + 1j * (1 - 2.0 * b[:, 1::2])) / math.sqrt(2)
+    rs = mbsfn_rs(area, nof_prb, sf_idx)
+    for i, sym in enumerate((2, 6, 10)):
+        g[sym] = 0 if rng is None else g[sym]
+        g[sym, (1 if sym == 6 else 0) + 2 * np.arange(6 * nof_prb)] = rs[i]
+    k = 6 * np.arange(2 * nof_prb) + (crs_shift(0, 0) + cell_id % 6) % 6
+    g[0, k] = crs_values(cell_id, nof_prb, 2 * sf_idx, 0)
+    return g
+
+
+def ofdm_tx_mbsfn(grid, N, non_mbsfn_region):
+    """srsRAN's MBSFN modulator (ofdm_tx_slot_mbsfn, ofdm.c:652-674, then slot 1 with extended CP): slot 0's first
+    non_mbsfn_region symbols with normal cyclic prefixes, zero guard samples, extended-CP symbols after"""
+    grid = np.asarray(grid).reshape(12, -1)
+    nre = grid.shape[1]
+    cpn0, cpn, cpe = math.ceil(160 * N / 2048), math.ceil(144 * N / 2048), math.ceil(512 * N / 2048)
+    nr = non_mbsfn_region
+    out = []
+    for l in range(12):
+        X = np.zeros(N, np.complex128)
+        X[N - nre // 2:] = grid[l, : nre // 2]
+        X[1: nre // 2 + 1] = grid[l, nre // 2:]
+        t = np.fft.ifft(X)
+        if l < 6 and l == nr:
+            out.append(np.zeros(cpe - cpn0 if nr == 1 else 2 * cpe - cpn0 - cpn))
+        c = cpe if (l >= 6 or l >= nr) else (cpn0 if l == 0 else cpn)
+        out += [t[N - c:], t]
+    return np.concatenate(out)
+
+
 def symbol_sz(nof_prb, standard=True):
     """srsran_symbol_sz (phy_common.c:340-385): standard rates = power-of-two sizes (1536 for 15 MHz);
     otherwise the reference's default 3/4 rates (384 / 768 / 1536 for 25 / 50 / 100 PRB)."""

@@ -105,6 +105,13 @@ OPT_CASES = [
     ("average_empty", 100, 5, 2, 2, 0, 2, 4, 1.0),
     ("interp_empty_4port", 6, 3, 4, 1, 1, 2, 2, 1.0),
     ("average_pss_auto", 25, 9, 1, 2, 0, 1, 0, 0.0),
+    # TRIANGLE ({w, 1 - 2w, w}, chest_common.c:62-68; `order` = w) and NONE (no average_pilots, chest_dl.c:724-725)
+    ("average_triangle", 100, 1, 2, 2, 0, 0, 0.25, 0.0, 1),
+    ("interp_triangle_pss", 50, 8, 1, 1, 1, 1, 0.1, 0.0, 1),
+    ("average_none", 100, 3, 2, 2, 0, 0, 0, 0.0, 2),
+    ("average_none_1port", 25, 10, 1, 2, 0, 0, 0, 0.0, 2),
+    ("interp_none_4port", 25, 301, 4, 2, 1, 0, 0, 0.0, 2),
+    ("interp_none_empty", 50, 5, 2, 1, 1, 2, 0, 0.0, 2),
 ]
 
 
@@ -114,18 +121,19 @@ def test_chest_options_match_oracle(U, ora, case):
     estimator_fil_order / _stddev / _auto; chest_dl.c:437-555, 402-433, 655-745) against the oracle's
     restatement (oracle_chest_dl_ext), over a sequence of subframes on one object so that PSS / EMPTY noise is
     estimated in subframes 0 / 5 and kept in the others (q->noise_estimate, also the automatic filter's input)"""
-    name, nof_prb, cell_id, nports, nrx, est, noise, order, std = case
+    name, nof_prb, cell_id, nports, nrx, est, noise, order, std = case[:9]
+    ftype = case[9] if len(case) > 9 else 0
     rng = np.random.default_rng(len(name) + nof_prb)
     N = U.lib().srsran_symbol_sz(nof_prb)
     ch = U.ChestDl(U.cell(nof_prb, nports, cell_id), nrx)
-    cfg = U.chest_cfg(est, noise, order, std)
+    cfg = U.chest_cfg(est, noise, order, std, filter_type=ftype)
     state = np.zeros((4, 4), np.float32)
     for tti in (4, 5, 6, 10, 11):
         sf = tti % 10
         Y = _doppler_subframe(ora, rng, nof_prb, cell_id, nports, nrx, sf, N=N)
         ce, res = ch.estimate(Y.copy(), tti, cfg)
         ceo, st, _, state = ora.chest_dl_ext(Y, nof_prb, cell_id, nports, sf, N, 0, est, noise, order, std,
-                                             noise_state=state)
+                                             noise_state=state, filter_type=ftype)
         scale = np.abs(ceo).max()  # 0 before the first kept noise estimate with an automatic filter: the
         # reference's Gauss filter of stddev 0 is not normal, conv_same runs no taps and the estimate is all zeros
         assert np.abs(ce - ceo).max() <= 2e-5 * scale, (tti, np.abs(ce - ceo).max(), scale)
@@ -160,7 +168,7 @@ def test_chest_sync_error_correction(U, ora, delay, nports):
     ch.free()
 
 
-def _batch_vs_host(U, ora, est, noise, nports, order=4, sync=False, delay=0.0):
+def _batch_vs_host(U, ora, est, noise, nports, order=4, sync=False, delay=0.0, ftype=0, expect_ok=True):
     from synth import synth as S
     from srsran_4g_amd import sch as SCH
     import ofdm_np
@@ -169,13 +177,15 @@ def _batch_vs_host(U, ora, est, noise, nports, order=4, sync=False, delay=0.0):
     scheme = "cdd" if nports == 2 else "port0"
     cell_id = 1
     ue = U.UeDl(U.cell(100, nports, cell_id), 2)
-    ue.cfg.chest_cfg = U.chest_cfg(est, noise, order, 1.0, sync_error=sync)
+    ue.cfg.chest_cfg = U.chest_cfg(est, noise, order, 1.0, sync_error=sync, filter_type=ftype)
     ue2 = U.UeDl(U.cell(100, nports, cell_id), 2)
-    ue2.cfg.chest_cfg = U.chest_cfg(est, noise, order, 1.0, sync_error=sync)
-    rng = np.random.default_rng(40 + est + 3 * noise + nports + 7 * order + (11 if sync else 0))
+    ue2.cfg.chest_cfg = U.chest_cfg(est, noise, order, 1.0, sync_error=sync, filter_type=ftype)
+    rng = np.random.default_rng(40 + est + 3 * noise + nports + int(7 * order) + (11 if sync else 0) + 13 * ftype)
     ttis = (4, 5, 6, 10, 11)
     first_ok = 0
-    if order == 0 and noise != 0:
+    if not expect_ok:
+        first_ok = len(ttis)
+    elif order == 0 and noise != 0 and ftype == 0:
         # the automatic filter's width comes from the kept PSS / EMPTY estimate, 0 before the first subframe 0 / 5:
         # a Gauss filter of stddev 0 is not normal, conv_same runs no taps and the estimate is all zeros (the
         # reference's too), so the first subframes fail in both paths; from the second subframe 0 / 5 on it is a noise
@@ -205,7 +215,7 @@ def _batch_vs_host(U, ora, est, noise, nports, order=4, sync=False, delay=0.0):
         assert ue2.fft_estimate(samples[b], tti, 1) == 0
         grids = np.stack([ofdm_np.ofdm_rx(v, 2048, 1200) for v in samples[b]]).astype(np.complex64)
         _, st, _, state = ora.chest_dl_ext(grids, 100, cell_id, nports, tti % 10, 2048, 0, est, noise, order, 1.0,
-                                           sync=sync, noise_state=state)
+                                           sync=sync, noise_state=state, filter_type=ftype)
         assert ue2.q.chest_res.noise_estimate == pytest.approx(st["noise"], rel=1e-4), tti
         if sync:
             assert ue2.q.chest_res.sync_error == pytest.approx(st["sync_error"], rel=1e-4, abs=1e-6), tti
@@ -248,6 +258,16 @@ def test_ue_dl_batch_auto_filter_and_sync_error(U, ora, est, noise, nports, sync
     place, chest_dl.c:750-804) on subframes sent with a 0.4-sample timing error: the batch decodes every TB, equal to
     the host-synchronous path, whose noise estimate / sync error equal the oracle's within 1e-4"""
     _batch_vs_host(U, ora, est, noise, nports, order=0, sync=sync, delay=0.4 if sync else 0.0)
+
+
+@pytest.mark.parametrize("est,noise,nports,ftype,coef", [(0, 0, 2, 1, 0.1), (1, 1, 1, 1, 0.2), (1, 0, 2, 2, 0),
+                                                         (0, 0, 2, 2, 0)])
+def test_ue_dl_batch_filter_types(U, ora, est, noise, nports, ftype, coef):
+    """TRIANGLE and NONE filters (chest_dl.c:700-729) in the batch: equal to the host-synchronous path subframe by
+    subframe.  AVERAGE with NONE interpolates the raw LS estimates of the first two CRS symbols as one comb of
+    spacing 3 (interp_lin_3 over pilot_estimates, chest_dl.c:476-481): not a channel estimate, so its TBs fail --
+    in both paths alike, which is what is checked there"""
+    _batch_vs_host(U, ora, est, noise, nports, order=coef, ftype=ftype, expect_ok=not (est == 0 and ftype == 2))
 
 
 def test_ue_dl_batch_refused_config_then_good_batch(U):

@@ -1,0 +1,223 @@
+"""MBSFN subframes on the GPU (verdict round 4, missing item 3; ue_dl.c:104-111, 218-221, 258-294, 353-376;
+ofdm.c:522-578; chest_dl.c:263-278, 437-600, 836-865; refsignal_dl.c:316-502).
+
+* OFDM: the MBSFN layout of an MBSFN srsran_ofdm_t (normal-CP non-MBSFN region, guard, extended CP) against numpy's
+  FFT at the reference's sample offsets, non-MBSFN regions of 1 and 2 symbols, and the reference's behaviour of
+  transforming the object's own buffers whatever srsran_ofdm_rx_sf_ng names;
+* the MBSFN estimator (srsran_chest_dl_estimate_cfg with sf_type MBSFN) against oracle_chest_dl_mbsfn at 2e-5 of
+  the largest estimate: TRIANGLE (srsUE's MBSFN configuration, cc_worker.cc:96-100), Gauss (fixed and automatic)
+  and NONE filters, REFS and PSS noise, 1 / 2 ports, 1 / 2 antennas; RSRP / RSSI / CFO kept from the previous
+  subframe and rows 12 / 13 of the estimate left as they were, as the reference leaves them;
+* the UE: an MBSFN subframe whose control region the GPU eNB built (PCFICH + PDCCH) and whose MBSFN region carries
+  the MBSFN reference signals and PMCH symbols, through a channel: srsran_ue_dl_decode_fft_estimate finds the CFI
+  and srsran_ue_dl_find_dl_dci / _find_ul_dci the DCIs, with the grid and estimate equal to the oracle's on the
+  same samples.  As in the reference, only antenna 0 is transformed (the other antennas keep the previous grid).
+The MBSFN reference-signal expressions are restatements (refsignal_dl.c does not build here): parity unpinned for
+their composition, as for the CRS estimator's."""
+import numpy as np
+import pytest
+import torch
+
+import ofdm_np
+from oracle import Oracle
+from synth import synth as S
+
+from test_phy_oracle import make_subframe
+
+pytestmark = pytest.mark.gpu
+
+FFT_TOL = 1e-6  # as tests/test_ofdm_gpu.py
+
+
+@pytest.fixture(scope="module")
+def ora():
+    return Oracle()
+
+
+@pytest.fixture(scope="module")
+def U():
+    from srsran_4g_amd import ue_dl
+    ue_dl.use_standard_symbol_size(True)
+    yield ue_dl
+    ue_dl.use_standard_symbol_size(False)
+
+
+@pytest.mark.parametrize("nprb", [6, 25, 75, 100])
+@pytest.mark.parametrize("nr", [1, 2])
+def test_ofdm_mbsfn_matches_numpy(U, nprb, nr):
+    rng = np.random.default_rng(nprb * 3 + nr)
+    N = U.symbol_sz_for(nprb)
+    nre = 12 * nprb
+    x = ((rng.standard_normal(15 * N) + 1j * rng.standard_normal(15 * N)) / np.sqrt(2)).astype(np.complex64)
+    o = U.OfdmRx(nprb, mbsfn=True, non_mbsfn_region=nr)
+    got = o.rx(x)
+    want = ofdm_np.ofdm_rx_mbsfn(x, N, nre, nr)
+    assert np.abs(got - want).max() <= FFT_TOL * np.abs(want).max()
+    # the region can change between subframes (srsran_ofdm_set_non_mbsfn_region before each, ue_dl.c:258-261)
+    U.lib().srsran_ofdm_set_non_mbsfn_region(U.ctypes.byref(o.q), 3 - nr)
+    got = o.rx(x)
+    want = ofdm_np.ofdm_rx_mbsfn(x, N, nre, 3 - nr)
+    assert np.abs(got - want).max() <= FFT_TOL * np.abs(want).max()
+    o.free()
+
+
+def _mbsfn_rx(rng, nprb, cell_id, sf, area, nr, nrx, snr_db=30.0, ctrl=None):
+    """samples of an MBSFN subframe (port 0 only, as srsRAN's eNB sends it) through a 2-tap channel per antenna:
+    (samples (nrx, 15 N), numpy grids (nrx, 14 * nre) with rows 12 / 13 random, per-antenna responses)"""
+    N = S.symbol_sz(nprb)
+    nre = 12 * nprb
+    g = S.mbsfn_grid(nprb, cell_id, sf, area, nr, rng)
+    if ctrl is not None:  # the control region of port 0 (CRS of symbol 0 included)
+        g[:nr] = ctrl[:nr]
+    x = S.ofdm_tx_mbsfn(g, N, nr)
+    out, grids, Hs = [], [], []
+    for r in range(nrx):
+        taps = np.array([1.0, 0.4 * np.exp(1j * (r + 1))])
+        d = 2 + 3 * r
+        y = x + taps[1] * np.roll(x, d)  # a circular echo d samples later (shorter than every cyclic prefix)
+        y = y * taps[0]
+        sigma = np.sqrt(np.mean(np.abs(y) ** 2) / 10 ** (snr_db / 10) / 2)
+        y = (y + sigma * (rng.standard_normal(y.size) + 1j * rng.standard_normal(y.size))).astype(np.complex64)
+        out.append(y)
+        gr = np.zeros(14 * nre, np.complex64)
+        gr[:12 * nre] = ofdm_np.ofdm_rx_mbsfn(y, N, nre, nr)
+        gr[12 * nre:] = rng.standard_normal(2 * nre)
+        grids.append(gr)
+        k = np.concatenate([np.arange(N - nre // 2, N), np.arange(1, nre // 2 + 1)])
+        Hs.append(1.0 + taps[1] * np.exp(-2j * np.pi * k * d / N))
+    return np.stack(out), np.stack(grids), Hs
+
+
+CHEST_CASES = [  # (name, nprb, cell_id, nports, nrx, filter_type, coef0, coef1, noise_alg)
+    ("srsue_triangle_pss", 100, 1, 1, 2, 1, 0.1, 0.0, 1),
+    ("triangle_refs_2port", 50, 22, 2, 2, 1, 0.25, 0.0, 0),
+    ("gauss_fixed_refs", 25, 7, 1, 1, 0, 4, 1.0, 0),
+    ("gauss_auto_refs", 100, 9, 2, 1, 0, 0, 0.0, 0),
+    ("none_pss", 15, 3, 1, 2, 2, 0, 0.0, 1),
+    ("none_refs_6prb", 6, 5, 2, 1, 2, 0, 0.0, 0),
+]
+
+
+@pytest.mark.parametrize("case", CHEST_CASES, ids=[c[0] for c in CHEST_CASES])
+def test_chest_mbsfn_matches_oracle(U, ora, case):
+    name, nprb, cell_id, nports, nrx, ftype, c0, c1, noise_alg = case
+    rng = np.random.default_rng(len(name) * 7 + nprb)
+    N = U.symbol_sz_for(nprb)
+    nre = 12 * nprb
+    area = 1 + nprb % 5
+    ch = U.ChestDl(U.cell(nprb, nports, cell_id), nrx)
+    assert ch.set_mbsfn_area_id(area) == 0
+    # a normal subframe first: its RSRP / RSSI / CFO / noise are what the MBSFN subframe keeps (or, REFS, replaces)
+    Yn, _, _ = make_subframe(ora, rng, nof_prb=nprb, cell_id=cell_id, nports=nports, nrx=nrx, sf_idx=2, snr_db=25)
+    ce_n, res_n = ch.estimate(Yn, 2, U.chest_cfg(1, 0, 4, 1.0))
+    rsrp_n, rssi_n, cfo_n = res_n.rsrp, res_n.rssi_dbm, res_n.cfo
+    state = np.array([[ch.q.noise_estimate[r][p] for p in range(4)] for r in range(4)], np.float32)
+    sf = 3
+    _, Y, Hs = _mbsfn_rx(rng, nprb, cell_id, sf, area, 2, nrx)
+    cfg = U.chest_cfg(1, noise_alg, c0, c1, filter_type=ftype, mbsfn_area_id=area)
+    ce, res = ch.estimate(Y, 10 + sf, cfg, mbsfn=True)
+    ceo, noise_o, _ = ora.chest_dl_mbsfn(Y, nprb, cell_id, nports, sf, area, noise_alg=noise_alg, filter_type=ftype,
+                                         coef0=c0, coef1=c1, noise_state=state, ce_init=ce_n)
+    scale = np.abs(ceo[:, :, :12 * nre]).max()
+    assert np.abs(ce[:, :, :12 * nre] - ceo[:, :, :12 * nre]).max() <= 2e-5 * scale
+    assert np.array_equal(ce[:, :, 12 * nre:], ce_n[:, :, 12 * nre:])  # rows 12 / 13 as the previous call left them
+    assert res.noise_estimate == pytest.approx(noise_o, rel=1e-4)
+    assert res.rsrp == rsrp_n and res.rssi_dbm == rssi_n and res.cfo == cfo_n  # not measured in MBSFN subframes
+    if ftype != 2:  # the estimate of port 0 (the port srsRAN's eNB sends) follows the channel
+        err = np.abs(ce[0, 0, :12 * nre].reshape(12, nre) - Hs[0][None, :])
+        assert np.median(err) < 0.1, float(np.median(err))
+    ch.free()
+
+
+def test_chest_mbsfn_refused(U, ora):
+    """what the reference cannot estimate consistently is refused: AVERAGE (chest_dl.c:719-721: rows it does not
+    write are read), 4-port cells (ports 2 / 3 interpolate from row 0, 518), subframes 0 / 5, an area never set"""
+    rng = np.random.default_rng(4)
+    _, Y, _ = _mbsfn_rx(rng, 25, 3, 3, 1, 2, 1)
+    ch = U.ChestDl(U.cell(25, 1, 3), 1)
+    with pytest.raises(RuntimeError):  # area 1 not initialised yet
+        ch.estimate(Y, 3, U.chest_cfg(1, 1, 0.1, 0.0, filter_type=1, mbsfn_area_id=1), mbsfn=True)
+    assert ch.set_mbsfn_area_id(1) == 0
+    with pytest.raises(RuntimeError):
+        ch.estimate(Y, 3, U.chest_cfg(0, 1, 0.1, 0.0, filter_type=1, mbsfn_area_id=1), mbsfn=True)
+    with pytest.raises(RuntimeError):
+        ch.estimate(Y, 5, U.chest_cfg(1, 1, 0.1, 0.0, filter_type=1, mbsfn_area_id=1), mbsfn=True)
+    ch.estimate(Y, 3, U.chest_cfg(1, 1, 0.1, 0.0, filter_type=1, mbsfn_area_id=1), mbsfn=True)
+    ch.free()
+    ch4 = U.ChestDl(U.cell(25, 4, 3), 1)
+    assert ch4.set_mbsfn_area_id(1) == 0
+    with pytest.raises(RuntimeError):
+        ch4.estimate(Y, 3, U.chest_cfg(1, 1, 0.1, 0.0, filter_type=1, mbsfn_area_id=1), mbsfn=True)
+    ch4.free()
+
+
+@pytest.mark.parametrize("nprb,nrx,cfi,nr,tti", [(25, 1, 1, 1, 3), (50, 2, 2, 2, 7), (100, 1, 2, 2, 18)])
+def test_ue_dl_mbsfn_subframe_pdcch(U, ora, nprb, nrx, cfi, nr, tti):
+    """srsUE's MBSFN subframe work (cc_worker.cc:321-351): set_mbsfn_area_id, set_non_mbsfn_region, the MBSFN
+    estimator configuration, decode_fft_estimate, then the DL / UL DCIs of the non-MBSFN region"""
+    from srsran_4g_amd import enb_dl as E
+    from srsran_4g_amd import pdcch as PD
+    from srsran_4g_amd.sch import _memcpy_d2h
+    cell_id, rnti, area = 57, 0x3C11, 2
+    rng = np.random.default_rng(nprb + 10 * cfi + nr)
+    cell = U.cell(nprb, 1, cell_id)
+    nre = 12 * nprb
+    regs = PD.Regs(cell)
+    nof_cce = regs.q.pdcch_nregs[cfi - 1] // 9
+    regs.free()
+    locs = [loc for loc in PD.ue_locations(nof_cce, tti % 10, rnti) if (1 << loc[0]) <= nof_cce]
+    # a format 1A DL DCI and a format 0 UL DCI at two different candidates
+    d = PD.srsran_dci_dl_t()
+    d.rnti, d.format, d.pid = rnti, 2, 5
+    for i in range(2):
+        d.tb[i].rv = 1
+    d.alloc_type = 2
+    d.raw[0] = U.lib().srsran_ra_type2_to_riv(4, 1, nprb)
+    d.tb[0].mcs_idx, d.tb[0].rv, d.tb[0].ndi = 9, 0, True
+    (d.location.L, d.location.ncce), loc_ul = locs[0], locs[-1]
+    r, m_dl = PD.pack_pdsch(cell, d)
+    assert r == 0
+    du = PD.srsran_dci_ul_t()
+    du.rnti, du.format, du.freq_hop_fl = rnti, 0, -1
+    du.type2_alloc.riv, du.tb.mcs_idx, du.n_dmrs = 33, 11, 2
+    du.location.L, du.location.ncce = loc_ul
+    r, m_ul = PD.pack_pusch(cell, du)
+    assert r == 0
+    # the eNB's control region (GPU transmitter): PCFICH, PDCCH and the CRS of symbol 0 on port 0
+    enb = E.EnbDl(cell)
+    N = S.symbol_sz(nprb)
+    d_out = torch.zeros((1, 1, 15 * N, 2), dtype=torch.float32, device="cuda")
+    assert enb.tx_batch([(tti, cfi, None, [], (False, [m_dl, m_ul]))], d_out.data_ptr(), 1.0) == 0
+    torch.cuda.synchronize()
+    host = torch.empty(2 * 14 * nre, dtype=torch.float32)
+    _memcpy_d2h(host, enb.sf_symbols(), 14 * nre * 8)
+    ctrl = host.numpy().view(np.complex64).reshape(14, nre)
+    enb.free()
+    # the previous subframe (normal) on the same UE, then the MBSFN subframe
+    ue = U.UeDl(cell, nrx, inputs=True)
+    try:
+        assert ue.set_mbsfn_area_id(area) == 0
+        x0, _, _ = _mbsfn_rx(rng, nprb, cell_id, (tti - 1) % 10, area, nr, nrx)  # any samples for the prior grids
+        assert ue.fft_estimate_guru(list(x0), tti - 1, 0) == 0
+        prev = ue.grids()
+        ue.set_non_mbsfn_region(nr)
+        ue.cfg.chest_cfg = U.mbsfn_chest_cfg(area)
+        x, Y, _ = _mbsfn_rx(rng, nprb, cell_id, tti % 10, area, nr, nrx, ctrl=ctrl)
+        assert ue.fft_estimate_guru(list(x), tti, 0, mbsfn=True) == 0
+        assert ue.last_cfi == cfi
+        grids = ue.grids()
+        want0 = Y[0, :12 * nre]
+        assert np.abs(grids[0, :12 * nre] - want0).max() <= FFT_TOL * np.abs(want0).max()
+        for r in range(1, nrx):  # fft_mbsfn reads antenna 0 only: the other grids are the previous subframe's
+            assert np.array_equal(grids[r], prev[r])
+        ce = ue.chest_res_ce()
+        state = np.zeros((4, 4), np.float32)  # PSS noise: the normal subframe before was not 0 / 5 either
+        ceo, _, _ = ora.chest_dl_mbsfn(grids, nprb, cell_id, 1, tti % 10, area, noise_alg=1, filter_type=1, coef0=0.1,
+                                       noise_state=state, ce_init=ce)
+        assert np.abs(ce[:, :, :12 * nre] - ceo[:, :, :12 * nre]).max() <= 2e-5 * np.abs(ceo).max()
+        dcis = ue.find_dl_dci(tti, cfi, rnti, tm=0, mbsfn=True)
+        assert len(dcis) == 1 and dcis[0].format == 2 and dcis[0].pid == 5 and dcis[0].raw[0] == d.raw[0]
+        uls = ue.find_ul_dci(tti, cfi, rnti)
+        assert len(uls) == 1 and uls[0].type2_alloc.riv == 33 and uls[0].tb.mcs_idx == 11 and uls[0].n_dmrs == 2
+    finally:
+        ue.free()

@@ -24,7 +24,7 @@ for STEP in "$@"; do
   echo "== $STEP"
   case $KIND in
     tests)
-      SEL=${REST:-tests}
+      SEL=${REST:-tests}; SEL=${SEL//,/ }
       timeout -k 10 900 python -u -m pytest $SEL -m gpu -q -x --timeout 300 --timeout-method thread \
         > $OUT/pytest_gpu.log 2>&1
       rc=$?; tail -3 $OUT/pytest_gpu.log; [ $rc -eq 0 ] || { echo "pytest rc=$rc"; exit 1; } ;;

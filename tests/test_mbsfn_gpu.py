@@ -187,7 +187,7 @@ def test_ue_dl_mbsfn_subframe_pdcch(U, ora, nprb, nrx, cfi, nr, tti):
     enb = E.EnbDl(cell)
     N = S.symbol_sz(nprb)
     d_out = torch.zeros((1, 1, 15 * N, 2), dtype=torch.float32, device="cuda")
-    assert enb.tx_batch([(tti, cfi, None, [], (False, [m_dl, m_ul]))], d_out.data_ptr(), 1.0) == 0
+    assert enb.tx_batch([(tti, cfi, None, [], (True, [m_dl, m_ul]))], d_out.data_ptr(), 1.0) == 0  # put_base: PCFICH
     torch.cuda.synchronize()
     host = torch.empty(2 * 14 * nre, dtype=torch.float32)
     _memcpy_d2h(host, enb.sf_symbols(), 14 * nre * 8)

@@ -26,12 +26,18 @@ struct PredArgs {
   float           rho_b_inv; // y scale on CRS-bearing symbols (bit 31 of idx), 1 = none
   int             interleave; // DIVERSITY: write the codeword (layer-demapped) into x[0]; 2: SM / CDD
                               // with one codeword on 2 layers: d[2k + l] = x_l[k], k < n / 2, into x[0]
+  int             pairs;      // csi_max_batch_launch only: idx lists (estimate index | RE parity << 31) pairs, the
+                              // distinct (subcarrier, parity) of an AVERAGE estimate's REs -- their CSI values are the
+                              // REs' own, so their maximum is the REs' maximum
 };
 
 hipError_t predecode_launch(const PredArgs& a, hipStream_t stream);
 // nitems descriptors (device array), all with the same scheme; max_n = largest n
 hipError_t predecode_batch_launch(const PredArgs* d_items, uint32_t nitems, int scheme, uint32_t max_n,
                                   hipStream_t stream);
+// the same items' per-layer CSI maxima only (into csi_max; PORT0, SM, CDD): the pre-pass of the fused predecode +
+// LLR path, which needs every codeword's maximum before its first LLR is scaled (pdsch.c:530)
+hipError_t csi_max_batch_launch(const PredArgs* d_items, uint32_t nitems, int scheme, uint32_t max_n, hipStream_t stream);
 
 }  // namespace srsran_amd
 #endif

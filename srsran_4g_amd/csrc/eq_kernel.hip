@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "eq_dev.h"
 #include "eq_kernel.h"
 #include "gmem.h"
 #include "stage_timing.h"
@@ -362,9 +363,10 @@ __device__ __forceinline__ void predecode_item(const PredArgs& a, uint32_t k, ui
 static constexpr int EQ_RPT = 4;  // REs per thread (strided by the block size: coalesced)
 
 // predecode_item for the EQ_RPT REs of a thread at once (PORT0, SM, CDD): every RE-map entry first, then
-// every grid / estimate load, then the arithmetic (as predecode_item's, operation for operation) and the
-// stores -- two HBM round trips a thread instead of two per RE
-template <int SCHEME>
+// every grid / estimate load, then the arithmetic (eq_dev.h, shared with the fused predecode + LLR kernel) and the
+// stores -- two HBM round trips a thread instead of two per RE.  CSI_ONLY: the CSI maxima only (no received
+// samples read, nothing stored) -- the pre-pass of the fused path (pdsch_api.cpp)
+template <int SCHEME, bool CSI_ONLY = false>
 __device__ __forceinline__ void predecode_items(const PredArgs& a, uint32_t k0, uint32_t (&mx)[2])
 {
   static_assert(SCHEME == 0 || SCHEME == 2 || SCHEME == 3, "one RE per unit");
@@ -389,117 +391,90 @@ __device__ __forceinline__ void predecode_items(const PredArgs& a, uint32_t k0, 
     }
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      gy[u] = e[u] & 0x7fffffffu;
-      gh[u] = a.ce_row ? gy[u] % a.ce_row : gy[u];
-      ys[u] = (e[u] >> 31) ? a.rho_b_inv : 1.0f;
+      eqd::re_pos(a, e[u], gy[u], gh[u], ys[u]);
+      if (CSI_ONLY && a.pairs) {
+        kk[u] = e[u] >> 31;  // the RE parity of the pair (CDD's precoder); ys is unused here
+      }
     }
   }
   const float noise = a.noise_ptr ? *gptr(a.noise_ptr) : a.noise;
-  auto        Ys    = [&](cpx v, int u) -> cpx { return ys[u] != 1.0f ? cscale(v, ys[u]) : v; };
+  auto        Ys    = [&](eqd::cpx v, int u) -> eqd::cpx { return ys[u] != 1.0f ? eqd::cscale(v, ys[u]) : v; };
   if constexpr (SCHEME == 0) {
-    cpx yv[U][4], hv[U][4];
+    eqd::cpx yv[U][4], hv[U][4];
 #pragma unroll
     for (int u = 0; u < U; u++) {
 #pragma unroll
       for (int p = 0; p < 4; p++) {
         if (p < a.nrx) {
-          yv[u][p] = ld(a.y[p], gy[u]);
-          hv[u][p] = ld(a.h[0][p], gh[u]);
+          yv[u][p] = CSI_ONLY ? eqd::cpx{0.f, 0.f} : eqd::ld(a.y[p], gy[u]);
+          hv[u][p] = eqd::ld(a.h[0][p], gh[u]);
         }
       }
     }
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      cpx   r  = {0.f, 0.f};
-      float hh = 0.f;
+      eqd::cpx y[4];
 #pragma unroll
       for (int p = 0; p < 4; p++) {
-        if (p < a.nrx) {
-          r = cadd(r, cmul(Ys(yv[u][p], u), cconj(hv[u][p])));
-          hh += hv[u][p].r * hv[u][p].r + hv[u][p].i * hv[u][p].i;
-        }
+        y[p] = Ys(yv[u][p], u);
       }
-      const float csi = hh + noise;
-      const cpx   t   = cscale(r, a.norm);
+      eqd::cpx x;
+      float    csi;
+      eqd::port0(y, hv[u], a.nrx, noise, a.norm, x, csi);
       if (valid[u]) {
-        gptr(a.csi[0])[k[u]] = csi;
-        gptr(a.x[0])[k[u]]   = make_float2(t.r / csi, t.i / csi);
-        mx[0]                = max(mx[0], __float_as_uint(csi));
+        if (!CSI_ONLY) {
+          gptr(a.csi[0])[k[u]] = csi;
+          gptr(a.x[0])[k[u]]   = make_float2(x.r, x.i);
+        }
+        mx[0] = max(mx[0], __float_as_uint(csi));
       }
     }
   } else {
-    cpx y0[U], y1[U], p0[U], p1[U], q0[U], q1[U];
+    eqd::cpx y0[U], y1[U], p0[U], p1[U], q0[U], q1[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      p0[u] = ld(a.h[0][0], gh[u]);
-      p1[u] = ld(a.h[0][1], gh[u]);
-      q0[u] = ld(a.h[1][0], gh[u]);
-      q1[u] = ld(a.h[1][1], gh[u]);
-      y0[u] = ld(a.y[0], gy[u]);
-      y1[u] = ld(a.y[1], gy[u]);
+      p0[u] = eqd::ld(a.h[0][0], gh[u]);
+      p1[u] = eqd::ld(a.h[0][1], gh[u]);
+      q0[u] = eqd::ld(a.h[1][0], gh[u]);
+      q1[u] = eqd::ld(a.h[1][1], gh[u]);
+      y0[u] = CSI_ONLY ? eqd::cpx{0.f, 0.f} : eqd::ld(a.y[0], gy[u]);
+      y1[u] = CSI_ONLY ? eqd::cpx{0.f, 0.f} : eqd::ld(a.y[1], gy[u]);
     }
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      cpx h00, h01, h10, h11;
-      if constexpr (SCHEME == 3) {  // CDD: the large-delay precoder alternates with the RE index
-        if ((kk[u] & 1) == 0) {
-          h00 = cadd(p0[u], q0[u]);
-          h10 = cadd(p1[u], q1[u]);
-          h01 = csub(p0[u], q0[u]);
-          h11 = csub(p1[u], q1[u]);
-        } else {
-          h00 = csub(p0[u], q0[u]);
-          h10 = csub(p1[u], q1[u]);
-          h01 = cadd(p0[u], q0[u]);
-          h11 = cadd(p1[u], q1[u]);
-        }
-      } else {
-        if (a.codebook == 0) {
-          h00 = p0[u];
-          h01 = q0[u];
-          h10 = p1[u];
-          h11 = q1[u];
-        } else if (a.codebook == 1) {
-          h00 = cadd(p0[u], q0[u]);
-          h01 = csub(p0[u], q0[u]);
-          h10 = cadd(p1[u], q1[u]);
-          h11 = csub(p1[u], q1[u]);
-        } else {
-          h00 = cadd(p0[u], cmulj(q0[u]));
-          h01 = csub(p0[u], cmulj(q0[u]));
-          h10 = cadd(p1[u], cmulj(q1[u]));
-          h11 = csub(p1[u], cmulj(q1[u]));
-        }
-      }
-      cpx   x0, x1;
-      float c0, c1;
-      mmse_csi(Ys(y0[u], u), Ys(y1[u], u), h00, h01, h10, h11, x0, x1, c0, c1, noise, a.norm);
+      eqd::cpx h00, h01, h10, h11;
+      eqd::effective_h<SCHEME>(a.codebook, kk[u], p0[u], p1[u], q0[u], q1[u], h00, h01, h10, h11);
+      eqd::cpx x0, x1;
+      float    c0, c1;
+      eqd::mmse_csi(Ys(y0[u], u), Ys(y1[u], u), h00, h01, h10, h11, x0, x1, c0, c1, noise, a.norm);
       if (valid[u]) {
-        if (a.interleave == 2) {    // one codeword on both layers: srsran_layerdemap_multiplex -> _diversity
-          if (k[u] < a.n / 2) {     // (layermap.c:138-147) over n/2 layer symbols (pdsch.c:862-863)
-            gptr(a.x[0])[2 * k[u]]     = make_float2(x0.r, x0.i);
-            gptr(a.x[0])[2 * k[u] + 1] = make_float2(x1.r, x1.i);
+        if (!CSI_ONLY) {
+          if (a.interleave == 2) {    // one codeword on both layers: srsran_layerdemap_multiplex -> _diversity
+            if (k[u] < a.n / 2) {     // (layermap.c:138-147) over n/2 layer symbols (pdsch.c:862-863)
+              gptr(a.x[0])[2 * k[u]]     = make_float2(x0.r, x0.i);
+              gptr(a.x[0])[2 * k[u] + 1] = make_float2(x1.r, x1.i);
+            }
+          } else {
+            gptr(a.x[0])[k[u]] = make_float2(x0.r, x0.i);
+            gptr(a.x[1])[k[u]] = make_float2(x1.r, x1.i);
           }
-        } else {
-          gptr(a.x[0])[k[u]] = make_float2(x0.r, x0.i);
-          gptr(a.x[1])[k[u]] = make_float2(x1.r, x1.i);
+          gptr(a.csi[0])[k[u]] = c0;  // not layer-demapped: the codeword's CSI correction reads layer 0's
+          gptr(a.csi[1])[k[u]] = c1;
         }
-        gptr(a.csi[0])[k[u]] = c0;  // not layer-demapped: the codeword's CSI correction reads layer 0's
-        gptr(a.csi[1])[k[u]] = c1;
-        mx[0]                = max(mx[0], __float_as_uint(c0));
-        mx[1]                = max(mx[1], __float_as_uint(c1));
+        mx[0] = max(mx[0], __float_as_uint(c0));
+        mx[1] = max(mx[1], __float_as_uint(c1));
       }
     }
   }
 }
 
-template <int SCHEME>
+template <int SCHEME, bool CSI_ONLY = false>
 __device__ __forceinline__ void predecode_block(const PredArgs& a, uint32_t k0)
 {
   __shared__ uint32_t red[2 * EQ_THREADS / 64];
   uint32_t            mx[2] = {0u, 0u};
   if constexpr (SCHEME == 0 || SCHEME == 2 || SCHEME == 3) {
-    predecode_items<SCHEME>(a, k0, mx);
+    predecode_items<SCHEME, CSI_ONLY>(a, k0, mx);
   } else {
 #pragma unroll
     for (int r = 0; r < EQ_RPT; r++) {
@@ -522,7 +497,7 @@ __global__ __launch_bounds__(EQ_THREADS) void predecode_kernel(PredArgs a)
   predecode_block<SCHEME>(a, blockIdx.x * EQ_THREADS * EQ_RPT);
 }
 
-template <int SCHEME>
+template <int SCHEME, bool CSI_ONLY = false>
 __global__ __launch_bounds__(EQ_THREADS) void predecode_batch_kernel(const PredArgs* __restrict__ items)
 {
   const PredArgs& a  = items[blockIdx.y];
@@ -530,7 +505,30 @@ __global__ __launch_bounds__(EQ_THREADS) void predecode_batch_kernel(const PredA
   if (k0 >= (SCHEME == 1 ? a.n / 2 : SCHEME == 4 ? a.n / 4 + 1 : a.n)) {
     return;  // whole block past this item's end (uniform: the block reduction stays intact)
   }
-  predecode_block<SCHEME>(a, k0);
+  predecode_block<SCHEME, CSI_ONLY>(a, k0);
+}
+
+hipError_t csi_max_batch_launch(const PredArgs* d_items, uint32_t nitems, int scheme, uint32_t max_n, hipStream_t stream)
+{
+  StageScope timing_scope(ST_PRED, stream);
+  if (nitems == 0 || max_n == 0) {
+    return hipSuccess;
+  }
+  const dim3 grid((max_n + EQ_THREADS * EQ_RPT - 1) / (EQ_THREADS * EQ_RPT), nitems);
+  switch (scheme) {
+    case 0:
+      hipLaunchKernelGGL((predecode_batch_kernel<0, true>), grid, dim3(EQ_THREADS), 0, stream, d_items);
+      break;
+    case 2:
+      hipLaunchKernelGGL((predecode_batch_kernel<2, true>), grid, dim3(EQ_THREADS), 0, stream, d_items);
+      break;
+    case 3:
+      hipLaunchKernelGGL((predecode_batch_kernel<3, true>), grid, dim3(EQ_THREADS), 0, stream, d_items);
+      break;
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
 }
 
 hipError_t predecode_batch_launch(const PredArgs* d_items, uint32_t nitems, int scheme, uint32_t max_n,

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "eq_kernel.h"
+
 namespace srsran_amd {
 
 // Upload the Gold-sequence jump tables (once per process; idempotent).
@@ -48,6 +50,21 @@ constexpr uint32_t LLR_BLOCK_SYMBOLS = 256 * LLR_SPT_CFG;  // symbols of one LLR
 // nitems items of one modulation (device array); max_n = largest n
 hipError_t llr_batch_launch(int mod, const LlrItem* d_items, uint32_t nitems, uint32_t max_n, int any_scramble,
                             hipStream_t stream, bool llr8 = false);
+
+// The fused predecode + LLR path (PORT0, or SM / CDD with two codewords of one modulation on two layers; int16
+// LLRs, no EVM): every RE of the subframe whose predecoder descriptor is *pa is equalised in the kernel (eq_dev.h)
+// and each layer's symbol demapped, descrambled and CSI-corrected as llr_batch_launch does, with no equalised-symbol
+// / CSI buffers in between; the CSI maxima come from csi_max_batch_launch.
+struct FusedItem {
+  const PredArgs* pa;
+  int16_t*        llr[2];   // [layer] = codeword on that layer
+  uint32_t        seed[2];  // [layer] scrambling seed (bit 0 of the sequence at symbol 0)
+  const float*    csi_max;  // [layer] max CSI (device); nullptr: CSI correction off
+  uint32_t        n;        // REs (= symbols a layer)
+};
+// nitems items of one modulation and one predecoder scheme (0: one layer; 2, 3: two); max_n = largest n
+hipError_t fused_llr_batch_launch(int mod, int scheme, const FusedItem* d_items, uint32_t nitems, uint32_t max_n,
+                                  hipStream_t stream);
 
 // out[i] = c(i) ? -in[i] : in[i] (int16 wrap) for the Gold sequence of `seed`.
 hipError_t seq_apply_launch(const int16_t* d_in, int16_t* d_out, uint32_t len, uint32_t seed, hipStream_t stream);

@@ -15,6 +15,7 @@
 #include <array>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -33,8 +34,9 @@ namespace {
 constexpr uint32_t kMaxQm = 8;
 
 struct Table {
-  uint32_t* d   = nullptr;
-  uint32_t  len = 0;
+  uint32_t* d      = nullptr;  // len RE entries, then npairs CSI pairs (PredArgs::pairs)
+  uint32_t  len    = 0;
+  uint32_t  npairs = 0;
 };
 
 using TableKey = std::array<uint64_t, 5>;  // RE table cache key (get_table)
@@ -171,9 +173,24 @@ Table get_table(srsran_pdsch_t* q, PdschGpu* g, const srsran_pdsch_grant_t& gr, 
   if (it != g->tables.end()) {
     return it->second;
   }
-  const std::vector<uint32_t> t = pdsch_re_table(q->cell, gr, lstart, sf_idx);
-  Table                       tb;
+  std::vector<uint32_t> t = pdsch_re_table(q->cell, gr, lstart, sf_idx);
+  Table                 tb;
   tb.len = (uint32_t)t.size();
+  // the distinct (subcarrier, RE parity) pairs: an AVERAGE estimate has one row of subcarriers, so the CSI maximum
+  // of the fused path's pre-pass needs these 2 x 12 N_RB at most, not every RE
+  const uint32_t       nre = 12 * q->cell.nof_prb;
+  std::vector<uint8_t> seen(nre, 0);
+  for (uint32_t k = 0; k < tb.len; k++) {
+    seen[(t[k] & 0x7fffffffu) % nre] |= (uint8_t)(1u << (k & 1));
+  }
+  for (uint32_t sc = 0; sc < nre; sc++) {
+    for (uint32_t par = 0; par < 2; par++) {
+      if (seen[sc] >> par & 1) {
+        t.push_back(sc | par << 31);
+      }
+    }
+  }
+  tb.npairs = (uint32_t)t.size() - tb.len;
   if (hipMalloc((void**)&tb.d, std::max<size_t>(t.size(), 1) * sizeof(uint32_t)) != hipSuccess ||
       hipMemcpy(tb.d, t.data(), t.size() * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) {
     hipFree(tb.d);
@@ -342,18 +359,44 @@ int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sf
       g->last_evm.push_back({c.sf, c.tb, d_evm_out + slot});
     }
   }
-  std::vector<uint32_t> order_p(nsf), order_l(cws.size());
+  // The fused predecode + LLR path (llr_kernel.h FusedItem, one item a subframe), opt-in (SRSRAN_AMD_PDSCH_FUSED=1,
+  // read every call) for batches whose subframes are all PORT0, or SM / CDD with two codewords of one modulation on
+  // two layers, with int16 LLRs and no EVM: the equalised symbols and CSI stay in registers, the CSI maxima come
+  // from a pre-pass over the (subcarrier, parity) pairs.  Both kernels it replaces are issue-bound, not HBM-bound,
+  // so the fused one takes their sum (C3, r05m: 7.4 + 33.8 us against 19.0 + 21.8 us) -- off by default.
+  const char* fenv  = getenv("SRSRAN_AMD_PDSCH_FUSED");
+  bool        fused = !q->llr_is_8bit && fenv && fenv[0] == '1';
+  std::vector<int>      sf_mod(nsf, -1);
+  std::vector<uint32_t> sf_cw(nsf * 2, 0);  // [sf][layer] -> index into cws
+  for (size_t i = 0; i < cws.size() && fused; i++) {
+    const Cw& c = cws[i];
+    fused       = (sf_mod[c.sf] < 0 || sf_mod[c.sf] == c.mod) && c.cw < 2;
+    sf_mod[c.sf]            = c.mod;
+    sf_cw[c.sf * 2 + c.cw] = (uint32_t)i;
+  }
+  for (uint32_t b = 0; b < nsf && fused; b++) {
+    const srsran_pdsch_grant_t& gr = sfs[b].cfg->grant;
+    fused = sf_mod[b] >= 0 && !sfs[b].cfg->meas_evm_en && pa[b].interleave == 0 &&
+            (pa[b].scheme == 0 ? gr.nof_tb == 1 : (pa[b].scheme == 2 || pa[b].scheme == 3) && gr.nof_tb == 2);
+  }
+  std::vector<uint32_t> order_p(nsf), order_l(fused ? nsf : cws.size()), pos_of(nsf);
   for (uint32_t i = 0; i < nsf; i++) {
     order_p[i] = i;
   }
-  for (uint32_t i = 0; i < cws.size(); i++) {
+  for (uint32_t i = 0; i < order_l.size(); i++) {
     order_l[i] = i;
   }
   std::stable_sort(order_p.begin(), order_p.end(), [&](uint32_t x, uint32_t y) { return pa[x].scheme < pa[y].scheme; });
-  std::stable_sort(order_l.begin(), order_l.end(), [&](uint32_t x, uint32_t y) { return cws[x].mod < cws[y].mod; });
+  for (uint32_t i = 0; i < nsf; i++) {
+    pos_of[order_p[i]] = i;
+  }
+  // LLR launches group by modulation (fused: subframes by modulation and predecoder scheme)
+  auto lkey = [&](uint32_t x) { return fused ? sf_mod[x] * 8 + pa[x].scheme : cws[x].mod; };
+  std::stable_sort(order_l.begin(), order_l.end(), [&](uint32_t x, uint32_t y) { return lkey(x) < lkey(y); });
   const size_t pa_bytes = align256(nsf * sizeof(PredArgs));
-  const size_t li_bytes = align256(std::max<size_t>(cws.size(), 1) * sizeof(LlrItem));
+  const size_t li_bytes = align256(std::max<size_t>(order_l.size(), 1) * (fused ? sizeof(FusedItem) : sizeof(LlrItem)));
   const size_t ev_bytes = align256(evs.size() * sizeof(EvmItem));
+  const size_t pp_bytes = fused ? pa_bytes : 0;  // the fused path's pre-pass descriptors (CSI pairs)
   desc.stop();
   srsran_amd::HostScope wait(srsran_amd::HP_PDSCH_WAIT);
   const bool side   = srsran_amd::stage_side_copy();
@@ -364,25 +407,50 @@ int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sf
                        : !srsran_amd::stage_fence_wait(g->fence, slot, st.seq))) {
     return SRSRAN_ERROR;
   }
-  if (st.cap < pa_bytes + li_bytes + ev_bytes) {  // every slot of the ring grows now, not when it comes round
+  // every slot of the ring grows now, not when it comes round
+  if (st.cap < pa_bytes + li_bytes + ev_bytes + pp_bytes) {
     for (StageSlot& r : g->ring) {
-      if (!grow_stage(g, r, 2 * (pa_bytes + li_bytes + ev_bytes))) {
+      if (!grow_stage(g, r, 2 * (pa_bytes + li_bytes + ev_bytes + pp_bytes))) {
         return SRSRAN_ERROR;
       }
     }
   }
   wait.stop();
   srsran_amd::HostScope launch(srsran_amd::HP_PDSCH_LAUNCH);
-  PredArgs* hp = (PredArgs*)st.h;
-  LlrItem*  hl = (LlrItem*)(st.h + pa_bytes);
+  PredArgs*  hp = (PredArgs*)st.h;
+  LlrItem*   hl = (LlrItem*)(st.h + pa_bytes);
+  FusedItem* hf = (FusedItem*)(st.h + pa_bytes);
   for (uint32_t i = 0; i < nsf; i++) {
     hp[i] = pa[order_p[i]];
   }
-  for (uint32_t i = 0; i < cws.size(); i++) {
-    hl[i] = li[order_l[i]];
+  for (uint32_t i = 0; i < order_l.size(); i++) {
+    const uint32_t c = order_l[i];
+    if (fused) {  // subframe c; its descriptor as uploaded: st.d + pos_of[c] PredArgs
+      FusedItem& fi = hf[i];
+      fi.pa         = (const PredArgs*)st.d + pos_of[c];
+      fi.n          = pa[c].n;
+      fi.csi_max    = sfs[c].cfg->csi_enable ? d_max + 2 * c : nullptr;
+      for (uint32_t l = 0; l < 2; l++) {
+        const LlrItem& it = li[sf_cw[c * 2 + (pa[c].scheme == 0 ? 0 : l)]];
+        fi.llr[l]         = it.llr;
+        fi.seed[l]        = it.seed;
+      }
+    } else {
+      hl[i] = li[c];
+    }
   }
   if (!evs.empty()) {
     memcpy(st.h + pa_bytes + li_bytes, evs.data(), evs.size() * sizeof(EvmItem));
+  }
+  PredArgs* hpp = (PredArgs*)(st.h + pa_bytes + li_bytes + ev_bytes);
+  for (uint32_t i = 0; i < nsf && fused; i++) {
+    hpp[i] = hp[i];
+    if (hp[i].ce_row) {  // AVERAGE: the CSI pairs of the subframe's table
+      const Table& tb = tabs[order_p[i]];
+      hpp[i].idx      = tb.d + tb.len;
+      hpp[i].n        = tb.npairs;
+      hpp[i].pairs    = 1;
+    }
   }
   // SRSRAN_AMD_STAGE=side (round 3): the upload on a copy stream once the launches of the batch that last used
   // this slot are done with its device copy, beside the OFDM / estimation stages
@@ -390,7 +458,7 @@ int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sf
     if (st.used) {
       hipStreamWaitEvent(g->copy, st.read, 0);
     }
-    hipMemcpyAsync(st.d, st.h, pa_bytes + li_bytes + ev_bytes, hipMemcpyHostToDevice, g->copy);
+    hipMemcpyAsync(st.d, st.h, pa_bytes + li_bytes + ev_bytes + pp_bytes, hipMemcpyHostToDevice, g->copy);
     hipEventRecord(st.staged, g->copy);
     hipStreamWaitEvent(s, st.staged, 0);
   } else {  // in line: a copy kernel reads the pinned slot and then marks it read in the fence (stage_copy.h)
@@ -399,8 +467,8 @@ int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sf
       return SRSRAN_ERROR;
     }
     st.seq = ++g->fence.seq;
-    if (srsran_amd::stage_copy_or_record(st.d, st.hd, pa_bytes + li_bytes + ev_bytes, s, (uint32_t*)d_max, nsf * 2,
-                                         &g->fence, slot, st.seq) != hipSuccess) {
+    if (srsran_amd::stage_copy_or_record(st.d, st.hd, pa_bytes + li_bytes + ev_bytes + pp_bytes, s, (uint32_t*)d_max,
+                                         nsf * 2, &g->fence, slot, st.seq) != hipSuccess) {
       return SRSRAN_ERROR;
     }
   }
@@ -423,6 +491,44 @@ int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sf
   }
   const PredArgs* dp = (const PredArgs*)st.d;
   const LlrItem*  dl = (const LlrItem*)(st.d + pa_bytes);
+  if (fused) {
+    bool any_csi = false;
+    for (uint32_t b = 0; b < nsf; b++) {
+      any_csi = any_csi || sfs[b].cfg->csi_enable;
+    }
+    const PredArgs* dpp = (const PredArgs*)(st.d + pa_bytes + li_bytes + ev_bytes);
+    for (uint32_t i = 0; i < nsf && any_csi;) {  // the CSI maxima: one pre-pass launch per predecoder scheme
+      uint32_t j = i, mx = 0;
+      while (j < nsf && hpp[j].scheme == hpp[i].scheme) {
+        mx = std::max(mx, hpp[j].n);
+        j++;
+      }
+      const PredArgs* items = dpp + i;
+      const uint32_t  n = j - i, scheme = (uint32_t)hp[i].scheme;
+      if (srsran_amd::launch_or_record([=] { return csi_max_batch_launch(items, n, (int)scheme, mx, s); }) !=
+          hipSuccess) {
+        return SRSRAN_ERROR;
+      }
+      i = j;
+    }
+    const FusedItem* df = (const FusedItem*)(st.d + pa_bytes);
+    for (uint32_t i = 0; i < nsf;) {  // one launch per (modulation, scheme)
+      uint32_t j = i, mx = 0;
+      while (j < nsf && lkey(order_l[j]) == lkey(order_l[i])) {
+        mx = std::max(mx, hf[j].n);
+        j++;
+      }
+      const int        mod = sf_mod[order_l[i]], scheme = pa[order_l[i]].scheme;
+      const FusedItem* items = df + i;
+      const uint32_t   n     = j - i;
+      if (srsran_amd::launch_or_record([=] { return fused_llr_batch_launch(mod, scheme, items, n, mx, s); }) !=
+          hipSuccess) {
+        return SRSRAN_ERROR;
+      }
+      i = j;
+    }
+    return SRSRAN_SUCCESS;
+  }
   for (uint32_t i = 0; i < nsf;) {  // one launch per predecoder scheme
     uint32_t j = i, mx = 0;
     while (j < nsf && hp[j].scheme == hp[i].scheme) {

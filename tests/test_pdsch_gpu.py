@@ -546,3 +546,63 @@ def test_pdsch_one_codeword_two_layers(U, SCH, ora, scheme, pmi, snr):
         assert crc and np.array_equal(payload[:TBS // 8], pl)
     pd.free()
     sb.free()
+
+
+@pytest.mark.parametrize("nports,mix,opts", [
+    (2, [("cdd", 0, 6), ("sm", 0, 6), ("sm", 1, 4), ("cdd", 0, 2)], dict()),
+    (2, [("cdd", 0, 6), ("sm", 1, 6)], dict(csi_enable=False)),
+    (2, [("sm", 0, 8), ("cdd", 0, 6)], dict(power_scale=True, p_a=-3.0, p_b=2)),
+    (2, [("cdd", 0, 6), ("sm", 0, 4)], dict(zf=True)),
+    (1, [("port0", 0, 4), ("port0", 0, 6), ("port0", 0, 2)], dict()),
+])
+def test_pdsch_fused_matches_two_kernel_path(U, SCH, ora, nports, mix, opts):
+    """the opt-in fused predecode + LLR kernel (SRSRAN_AMD_PDSCH_FUSED=1: llr_kernel.hip fused_llr_batch_kernel after
+    the CSI-pair pre-pass; eligible batches: PORT0, or SM / CDD with two codewords of one modulation, int16 LLRs, no
+    EVM) against the default two-kernel path (predecoder -> symbols + CSI in HBM -> LLR kernel): every LLR
+    bit-identical, the same decode results.  Mixed schemes and modulations in one batch, 256QAM included (Qm 8 is carried as MCS
+    tables' 256QAM; synth sends one modulation a subframe)."""
+    tbs_of = {2: 12576, 4: 30576, 6: 46888, 8: 63776}
+    rng = np.random.default_rng(900 + nports + len(mix))
+    ue = U.UeDl(U.cell(100, nports, 1), 2)
+    entries, samples, keep = [], [], []
+    ttis = [1, 2, 3, 4, 6, 7, 8][: len(mix)]
+    ncw = [1 if s == "port0" else 2 for s, _, _ in mix]
+    d_pl = torch.zeros((len(mix), 2, 63776 // 8 + 64), dtype=torch.uint8, device="cuda")
+    for b, ((scheme, pmi, qm), tti) in enumerate(zip(mix, ttis)):
+        tbs, Qm = (tbs_of[qm],) * ncw[b], (qm,) * ncw[b]
+        kw = dict(channel=[[1], [0.5 + 0.5j]]) if scheme == "port0" else {}
+        pls, x, nre, _, _, _ = _case(ora, rng, nports=nports, tti=tti, tbs=tbs, Qm=Qm, scheme=scheme, pmi=pmi,
+                                     snr_db=25.0, **kw)
+        sb = [SCH.SoftbufferRx(nof_prb=100) for _ in tbs]
+        cfg = U.pdsch_cfg(100, nre, tbs, Qm, scheme=scheme, pmi=pmi, softbuffers=sb, nof_ports=nports, **opts)
+        keep += [sb, cfg, pls]
+        samples.append(x)
+        entries.append((tti, 1, cfg, [d_pl[b, q].data_ptr() for q in range(ncw[b])], [1] * ncw[b]))
+    d_x = torch.from_numpy(np.stack(samples).view(np.float32)).cuda()
+
+    def run(fused):
+        os.environ["SRSRAN_AMD_PDSCH_FUSED"] = "1" if fused else "0"
+        try:
+            d_res = torch.full((2 * len(mix),), 7, dtype=torch.int32, device="cuda")
+            d_avg = torch.zeros(2 * len(mix), dtype=torch.float32, device="cuda")
+            assert ue.gpu_decode_batch(entries, d_x.data_ptr(), d_res.data_ptr(), d_avg.data_ptr()) == sum(ncw)
+            torch.cuda.synchronize()
+            llrs = []
+            for b in range(len(mix)):
+                for q in range(ncw[b]):
+                    dp, n = ue.last_llr(b, q)
+                    got = torch.empty(n, dtype=torch.int16)
+                    SCH._memcpy_d2h(got, dp, 2 * n)
+                    llrs.append(got.numpy().copy())
+            return d_res.cpu().numpy(), d_avg.cpu().numpy(), llrs, d_pl.cpu().numpy()
+        finally:
+            os.environ.pop("SRSRAN_AMD_PDSCH_FUSED", None)
+
+    r0, a0, l0, p0 = run(False)
+    r1, a1, l1, p1 = run(True)
+    assert len(l0) == len(l1) == sum(ncw)
+    for i, (x0, x1) in enumerate(zip(l0, l1)):
+        assert x0.size == x1.size and np.array_equal(x0, x1), (i, int((x0 != x1).sum()))
+    assert np.array_equal(r0, r1) and np.array_equal(a0, a1) and np.array_equal(p0, p1)
+    assert (r1[r1 != 7] == 0).all()  # every TB decodes at 25 dB
+    ue.free()

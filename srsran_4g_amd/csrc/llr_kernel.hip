@@ -186,17 +186,19 @@ __device__ __forceinline__ void gold_at(uint32_t seed, uint32_t off, uint32_t& x
 }
 
 // ---- x86 conversion semantics (see oracle/phy_oracle.c) ----
+// out of range or NaN -> INT32_MIN ("integer indefinite"); one |x| compare (x = -2^31 converts to INT32_MIN either
+// way, so the half-open range needs no second compare)
 __device__ __forceinline__ int32_t cvt_rn(float x)
 {
-  return (x >= -2147483648.0f && x < 2147483648.0f) ? (int32_t)__builtin_rintf(x) : INT32_MIN;
+  return __builtin_fabsf(x) < 2147483648.0f ? (int32_t)__builtin_rintf(x) : INT32_MIN;
 }
 __device__ __forceinline__ int32_t cvt_tz(float x)
 {
-  return (x >= -2147483648.0f && x < 2147483648.0f) ? (int32_t)x : INT32_MIN;
+  return __builtin_fabsf(x) < 2147483648.0f ? (int32_t)x : INT32_MIN;
 }
 __device__ __forceinline__ int32_t cvt_tz_d(double x)
 {
-  return (x >= -2147483648.0 && x < 2147483648.0) ? (int32_t)x : INT32_MIN;
+  return __builtin_fabs(x) < 2147483648.0 ? (int32_t)x : INT32_MIN;
 }
 __device__ __forceinline__ int16_t sat16(int32_t v) { return (int16_t)max(-32768, min(32767, v)); }
 __device__ __forceinline__ int16_t wrap16(int32_t v) { return (int16_t)(uint16_t)(uint32_t)v; }

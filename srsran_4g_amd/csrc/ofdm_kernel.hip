@@ -14,6 +14,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
+
 #include "ofdm_kernel.h"
 #include "stage_timing.h"
 
@@ -168,11 +170,107 @@ __device__ __forceinline__ void fft_ip(float2* buf, const OfdmArgs& a)
   }
 }
 
+// One Stockham stage with N and Ns known at compile time: the butterflies, twiddles and LDS traffic of stage_ip,
+// its index arithmetic folded (j / Ns a shift, the twiddle stride a constant)
+template <int R, uint32_t N, uint32_t NS>
+__device__ __forceinline__ void stage_ct(float2* buf, const float2* __restrict__ tw)
+{
+  constexpr int      J  = (N / R + OFDM_THREADS - 1) / OFDM_THREADS;
+  constexpr uint32_t nb = N / R, tstep = N / (NS * R);
+  float2             v[J][R], w[J][R];
+#pragma unroll
+  for (int jj = 0; jj < J; jj++) {
+    const uint32_t j = threadIdx.x + jj * OFDM_THREADS;
+    if (NS > 1 && j < nb) {
+      const uint32_t k = j % NS;
+#pragma unroll
+      for (int r = 1; r < R; r++) {
+        w[jj][r] = tw[r * k * tstep];
+      }
+    }
+  }
+#pragma unroll
+  for (int jj = 0; jj < J; jj++) {
+    const uint32_t j = threadIdx.x + jj * OFDM_THREADS;
+    if (j < nb) {
+#pragma unroll
+      for (int r = 0; r < R; r++) {
+        v[jj][r] = buf[j + r * nb];
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int jj = 0; jj < J; jj++) {
+    const uint32_t j = threadIdx.x + jj * OFDM_THREADS;
+    if (j < nb) {
+      const uint32_t q = j / NS, k = j % NS;
+      if constexpr (NS > 1) {
+#pragma unroll
+        for (int r = 1; r < R; r++) {
+          v[jj][r] = cmul(v[jj][r], w[jj][r]);
+        }
+      }
+      if constexpr (R == 8) {
+        dft8(v[jj]);
+      } else if constexpr (R == 4) {
+        dft4(v[jj]);
+      } else if constexpr (R == 3) {
+        dft3(v[jj]);
+      } else {
+        dft2(v[jj]);
+      }
+      const uint32_t base = q * NS * R + k;
+#pragma unroll
+      for (int r = 0; r < R; r++) {
+        buf[base + r * NS] = v[jj][r];
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// NC = 2048 / 1536 (C3's standard and reference-default rates): ofdm_plan's stages 8, 8, 8, 4 / 8, 8, 8, 3 unrolled
+// at compile time; NC = 0: the runtime plan
+template <uint32_t NC>
+__device__ __forceinline__ void fft_n(float2* buf, const OfdmArgs& a)
+{
+  if constexpr (NC == 2048) {
+    stage_ct<8, 2048, 1>(buf, a.tw);
+    stage_ct<8, 2048, 8>(buf, a.tw);
+    stage_ct<8, 2048, 64>(buf, a.tw);
+    stage_ct<4, 2048, 512>(buf, a.tw);
+  } else if constexpr (NC == 1536) {
+    stage_ct<8, 1536, 1>(buf, a.tw);
+    stage_ct<8, 1536, 8>(buf, a.tw);
+    stage_ct<8, 1536, 64>(buf, a.tw);
+    stage_ct<3, 1536, 512>(buf, a.tw);
+  } else {
+    fft_ip(buf, a);
+  }
+}
+// the launch's choice of fft_n: the compile-time plan where ofdm_plan gives exactly it
+static uint32_t fixed_plan(const OfdmArgs& a)
+{
+  static const int k2048[4] = {8, 8, 8, 4}, k1536[4] = {8, 8, 8, 3};
+  if (a.nstages != 4 || (a.N != 2048 && a.N != 1536)) {
+    return 0;
+  }
+  const int* want = a.N == 2048 ? k2048 : k1536;
+  for (int st = 0; st < 4; st++) {
+    if (a.radix[st] != want[st]) {
+      return 0;
+    }
+  }
+  return a.N;
+}
+
+template <uint32_t NC>
 __global__ __launch_bounds__(OFDM_THREADS) void ofdm_rx_kernel(OfdmArgs a)
 {
   __shared__ float2 buf[OFDM_MAX_N];
   const uint32_t    sym = blockIdx.x, rx = blockIdx.y, sf = blockIdx.z;
-  const uint32_t    N = a.N, ns = a.nsymb, slot = sym / ns, i = sym % ns;
+  const uint32_t    N = NC ? NC : a.N, ns = a.nsymb, slot = sym / ns, i = sym % ns;
   const uint32_t    slot_sz = ns * N + a.cp0 + (ns - 1) * a.cp;
   const uint32_t    off     = a.mbsfn && slot == 0 ? a.mbsfn_off[i] : slot * slot_sz + a.cp0 + i * (N + a.cp);
   const float2*     src     = a.in + ((size_t)sf * a.nrx + rx) * a.sf_len + off;
@@ -198,7 +296,7 @@ __global__ __launch_bounds__(OFDM_THREADS) void ofdm_rx_kernel(OfdmArgs a)
     }
   }
   __syncthreads();
-  fft_ip(buf, a);
+  fft_n<NC>(buf, a);
   float2*        dst  = a.out + (((size_t)sf * a.nrx + rx) * 2 * ns + sym) * a.nre;
   const uint32_t half = a.nre / 2;
   for (uint32_t k = threadIdx.x; k < a.nre; k += OFDM_THREADS) {
@@ -216,11 +314,12 @@ __global__ __launch_bounds__(OFDM_THREADS) void ofdm_rx_kernel(OfdmArgs a)
 // grid) and N - nre/2 .. N-1 (lower half), a backward DFT computed as conj(FFT(conj(X))) with the
 // receiver's Stockham stages, then the cyclic prefix.  in: [sf][port][14][nre], out: [sf][port][sf_len];
 // a.norm scales the grid first (srsran_enb_dl_gen_signal's 0.05 / sqrt(nof_prb)).
+template <uint32_t NC>
 __global__ __launch_bounds__(OFDM_THREADS) void ofdm_tx_kernel(OfdmArgs a)
 {
   __shared__ float2 buf[OFDM_MAX_N];
   const uint32_t    sym = blockIdx.x, port = blockIdx.y, sf = blockIdx.z;
-  const uint32_t    N = a.N, ns = a.nsymb, slot = sym / ns, i = sym % ns, half = a.nre / 2;
+  const uint32_t    N = NC ? NC : a.N, ns = a.nsymb, slot = sym / ns, i = sym % ns, half = a.nre / 2;
   const float2*     src = a.in + (((size_t)sf * a.nrx + port) * 2 * ns + sym) * a.nre;
   for (uint32_t n = threadIdx.x; n < N; n += OFDM_THREADS) {
     buf[n] = make_float2(0.f, 0.f);
@@ -232,7 +331,7 @@ __global__ __launch_bounds__(OFDM_THREADS) void ofdm_tx_kernel(OfdmArgs a)
     buf[bin]           = make_float2(v.x * a.norm, -(v.y * a.norm));
   }
   __syncthreads();
-  fft_ip(buf, a);
+  fft_n<NC>(buf, a);
   const uint32_t slot_sz = ns * N + a.cp0 + (ns - 1) * a.cp;
   const uint32_t off     = slot * slot_sz + a.cp0 + i * (N + a.cp);
   const uint32_t cpl     = i == 0 ? a.cp0 : a.cp;
@@ -247,12 +346,148 @@ __global__ __launch_bounds__(OFDM_THREADS) void ofdm_tx_kernel(OfdmArgs a)
   }
 }
 
+// ---- N = 2048 / 1536 on one wave per symbol (ofdm_rx_wave_kernel) ----
+// N = 64 x M (M = 32 / 24): lane l holds x[l + 64 m], m < M, and takes their M-point DFT in registers (4 x 8 /
+// 3 x 8), twiddles it by W_N^(l k2), writes it to a wave-private LDS tile [k2][l] (rows padded to 65: the column
+// reads below are bank-conflict free), and reads back every second element of row k2 = lane / 2 from parity
+// p = lane & 1: a 32-point DFT of those is half of row k2's 64-point DFT, the other half sits in the neighbour lane,
+// and one radix-2 step across the pair (a DPP swap) gives X[k2 + M k1].  Two register FFTs and one LDS transpose a
+// symbol instead of four LDS stages and eight workgroup barriers; the same forward DFT as the Stockham kernels,
+// rounded in another order.  (M = 24: lanes 48..63 idle in the second half.)
+static constexpr int WV_ROW = 65;  // LDS row stride of the transpose tile (float2)
+
+// natural-order M-point DFT in place (M = 32: m = 8 m1 + m2, k = k1 + 4 k2; M = 24: k = k1 + 3 k2); the inner
+// twiddles W_M^j = W_N^(TS j), TS = N / M, come from the symbol's table
+template <int M, int TS>
+__device__ __forceinline__ void dft_reg(float2 (&a)[M], const float2* __restrict__ tw)
+{
+  constexpr int R = M / 8;  // 4 or 3
+  float2        b[M];
+#pragma unroll
+  for (int m2 = 0; m2 < 8; m2++) {
+    float2 t[R];
+#pragma unroll
+    for (int m1 = 0; m1 < R; m1++) {
+      t[m1] = a[8 * m1 + m2];
+    }
+    if constexpr (R == 4) {
+      dft4(t);
+    } else {
+      dft3(t);
+    }
+#pragma unroll
+    for (int k1 = 0; k1 < R; k1++) {
+      b[k1 * 8 + m2] = (m2 * k1 == 0) ? t[k1] : cmul(t[k1], tw[TS * m2 * k1]);
+    }
+  }
+#pragma unroll
+  for (int k1 = 0; k1 < R; k1++) {
+    float2 u[8];
+#pragma unroll
+    for (int m2 = 0; m2 < 8; m2++) {
+      u[m2] = b[k1 * 8 + m2];
+    }
+    dft8(u);
+#pragma unroll
+    for (int k2 = 0; k2 < 8; k2++) {
+      a[k1 + R * k2] = u[k2];
+    }
+  }
+}
+
+// the value of lane ^ 1 (quad_perm [1, 0, 3, 2])
+__device__ __forceinline__ float swap1(float v)
+{
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
+}
+
+template <uint32_t N, bool CFO>
+__global__ __launch_bounds__(64) void ofdm_rx_wave_kernel(OfdmArgs a)
+{
+  constexpr int      M = (int)(N / 64);
+  __shared__ float2  T[M * WV_ROW];
+  const uint32_t     sym = blockIdx.x, rx = blockIdx.y, sf = blockIdx.z, l = threadIdx.x;
+  const uint32_t     ns = a.nsymb, slot = sym / ns, i = sym % ns;
+  const uint32_t     slot_sz = ns * N + a.cp0 + (ns - 1) * a.cp;
+  const uint32_t     off     = a.mbsfn && slot == 0 ? a.mbsfn_off[i] : slot * slot_sz + a.cp0 + i * (N + a.cp);
+  const float2*      src     = a.in + ((size_t)sf * a.nrx + rx) * a.sf_len + off;
+  const float2*      tw      = a.tw;
+  float2             v[M];
+#pragma unroll
+  for (int m = 0; m < M; m++) {
+    v[m] = src[l + 64 * m];
+  }
+  if constexpr (CFO) {
+    float2 c[M];
+#pragma unroll
+    for (int m = 0; m < M; m++) {
+      c[m] = a.cfo_tab[off + l + 64 * m];
+    }
+#pragma unroll
+    for (int m = 0; m < M; m++) {
+      v[m] = ref_cprod(v[m], c[m]);  // srsran_cfo_correct on the subframe buffer
+    }
+  }
+  dft_reg<M, 64>(v, tw);
+  {
+    float2 w[M];
+#pragma unroll
+    for (int k2 = 1; k2 < M; k2++) {
+      w[k2] = tw[l * k2];  // l k2 <= 63 (M - 1) < N
+    }
+#pragma unroll
+    for (int k2 = 0; k2 < M; k2++) {
+      T[k2 * WV_ROW + l] = k2 ? cmul(v[k2], w[k2]) : v[k2];
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront", "local");
+  __builtin_amdgcn_wave_barrier();
+  const uint32_t kk = l >> 1, p = l & 1, row = kk < (uint32_t)M ? kk : 0;
+  float2         y[32];
+#pragma unroll
+  for (int j = 0; j < 32; j++) {
+    y[j] = T[row * WV_ROW + 2 * j + p];
+  }
+  dft_reg<32, (int)(N / 32)>(y, tw);
+  // X[kk + M k] = Y0[k] + W_64^k Y1[k], X[kk + M (k + 32)] = Y0[k] - W_64^k Y1[k]; W_64^k = W_N^(M k)
+  const uint32_t half = a.nre / 2;
+  float2*        dst  = a.out + (((size_t)sf * a.nrx + rx) * 2 * ns + sym) * a.nre;
+#pragma unroll
+  for (int k = 0; k < 32; k++) {
+    const float2   t = (p && k) ? cmul(y[k], tw[M * k]) : y[k];  // lane 1: W_64^k Y1[k]; lane 0: Y0[k]
+    const float2   o = make_float2(swap1(t.x), swap1(t.y));      // the pair's other value
+    float2         x = p ? csub(o, t) : cadd(t, o);               // lane 0: Y0 + W Y1; lane 1: Y0 - W Y1
+    const uint32_t b = kk + (uint32_t)M * ((uint32_t)k + 32 * p);
+    if (a.norm != 1.0f) {
+      x = make_float2(x.x * a.norm, x.y * a.norm);
+    }
+    if (kk >= (uint32_t)M) {
+      continue;
+    }
+    if (b >= N - half) {
+      dst[b - (N - half)] = x;
+    } else if (b >= 1 && b <= half) {
+      dst[b + half - 1] = x;
+    }
+  }
+}
+
 hipError_t ofdm_tx_launch(const OfdmArgs& a, uint32_t nsf, hipStream_t stream)
 {
   if (a.N > OFDM_MAX_N || a.nstages <= 0 || nsf == 0 || (a.nsymb != 7 && a.nsymb != 6)) {
     return hipErrorInvalidValue;
   }
-  hipLaunchKernelGGL(ofdm_tx_kernel, dim3(2 * a.nsymb, a.nrx, nsf), dim3(OFDM_THREADS), 0, stream, a);
+  const dim3 grid(2 * a.nsymb, a.nrx, nsf);
+  switch (fixed_plan(a)) {
+    case 2048:
+      hipLaunchKernelGGL(ofdm_tx_kernel<2048>, grid, dim3(OFDM_THREADS), 0, stream, a);
+      break;
+    case 1536:
+      hipLaunchKernelGGL(ofdm_tx_kernel<1536>, grid, dim3(OFDM_THREADS), 0, stream, a);
+      break;
+    default:
+      hipLaunchKernelGGL(ofdm_tx_kernel<0>, grid, dim3(OFDM_THREADS), 0, stream, a);
+  }
   return hipGetLastError();
 }
 
@@ -296,7 +531,32 @@ hipError_t ofdm_rx_launch(const OfdmArgs& a, uint32_t nsf, hipStream_t stream)
   if (a.N > OFDM_MAX_N || a.nstages <= 0 || nsf == 0 || (a.nsymb != 7 && a.nsymb != 6)) {
     return hipErrorInvalidValue;
   }
-  hipLaunchKernelGGL(ofdm_rx_kernel, dim3(2 * a.nsymb, a.nrx, nsf), dim3(OFDM_THREADS), 0, stream, a);
+  // SRSRAN_AMD_OFDM_WAVE=1 (read once): the one-wave-per-symbol kernel at N = 2048 / 1536
+  static const bool wave = [] {
+    const char* v = getenv("SRSRAN_AMD_OFDM_WAVE");
+    return v && v[0] == '1';
+  }();
+  const dim3     grid(2 * a.nsymb, a.nrx, nsf);
+  const uint32_t plan = fixed_plan(a);
+  if (wave && plan == 2048) {
+    if (a.cfo_tab) {
+      hipLaunchKernelGGL((ofdm_rx_wave_kernel<2048, true>), grid, dim3(64), 0, stream, a);
+    } else {
+      hipLaunchKernelGGL((ofdm_rx_wave_kernel<2048, false>), grid, dim3(64), 0, stream, a);
+    }
+  } else if (wave && plan == 1536) {
+    if (a.cfo_tab) {
+      hipLaunchKernelGGL((ofdm_rx_wave_kernel<1536, true>), grid, dim3(64), 0, stream, a);
+    } else {
+      hipLaunchKernelGGL((ofdm_rx_wave_kernel<1536, false>), grid, dim3(64), 0, stream, a);
+    }
+  } else if (plan == 2048) {
+    hipLaunchKernelGGL(ofdm_rx_kernel<2048>, grid, dim3(OFDM_THREADS), 0, stream, a);
+  } else if (plan == 1536) {
+    hipLaunchKernelGGL(ofdm_rx_kernel<1536>, grid, dim3(OFDM_THREADS), 0, stream, a);
+  } else {
+    hipLaunchKernelGGL(ofdm_rx_kernel<0>, grid, dim3(OFDM_THREADS), 0, stream, a);
+  }
   return hipGetLastError();
 }
 

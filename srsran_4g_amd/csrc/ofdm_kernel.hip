@@ -531,10 +531,12 @@ hipError_t ofdm_rx_launch(const OfdmArgs& a, uint32_t nsf, hipStream_t stream)
   if (a.N > OFDM_MAX_N || a.nstages <= 0 || nsf == 0 || (a.nsymb != 7 && a.nsymb != 6)) {
     return hipErrorInvalidValue;
   }
-  // SRSRAN_AMD_OFDM_WAVE=1 (read once): the one-wave-per-symbol kernel at N = 2048 / 1536
+  // N = 2048 / 1536: the one-wave-per-symbol kernel (r05s: 29.1 against 34.1 us for the compile-time Stockham
+  // plan under the 3-worker chain, 41 % fewer VALU, 69 % fewer wave cycles); SRSRAN_AMD_OFDM_WAVE=0 (read once)
+  // keeps the workgroup-per-symbol Stockham kernel
   static const bool wave = [] {
     const char* v = getenv("SRSRAN_AMD_OFDM_WAVE");
-    return v && v[0] == '1';
+    return !(v && v[0] == '0');
   }();
   const dim3     grid(2 * a.nsymb, a.nrx, nsf);
   const uint32_t plan = fixed_plan(a);

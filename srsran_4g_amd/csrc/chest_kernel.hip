@@ -187,34 +187,69 @@ __device__ uint32_t load_filter(const ChestArgs& a, float noise, float* filt)
   return M;
 }
 
-// fill_res (chest_dl.c:962-986) of one subframe from its per-(rx, port) stats st -> o[4]
+// fill_res (chest_dl.c:962-986) of one subframe from its per-(rx, port) stats st -> o[4]: every stat of the
+// subframe loaded first (one round trip, not one a loop step), then the reference's sums in its order
 __device__ void finalize_sf(const float* st, uint32_t np, uint32_t nrx, uint32_t nof_prb, float sz, float nsymb,
                             float* o)
 {
+  float v[4][4][5];  // [rx][port][noise, rsrp, rssi, cfo re, cfo im]
+#pragma unroll
+  for (uint32_t rx = 0; rx < 4; rx++) {
+#pragma unroll
+    for (uint32_t p = 0; p < 4; p++) {
+      if (rx < nrx && p < np) {
+#pragma unroll
+        for (int f = 0; f < 5; f++) {
+          v[rx][p][f] = st[(rx * np + p) * 8 + f];
+        }
+      }
+    }
+  }
   float n = 0, best = -1e9f, rssi = 0, cfo = 0;
-  for (uint32_t rx = 0; rx < nrx; rx++) {
-    float s = 0;
-    for (uint32_t p = 0; p < np; p++) {
-      s += st[(rx * np + p) * 8];
+#pragma unroll
+  for (uint32_t rx = 0; rx < 4; rx++) {
+    if (rx < nrx) {
+      float s = 0;
+#pragma unroll
+      for (uint32_t p = 0; p < 4; p++) {
+        if (p < np) {
+          s += v[rx][p][0];
+        }
+      }
+      n += s / (float)np;
+      rssi += 4 * v[rx][0][2] / (float)nof_prb / 12.0f;
     }
-    n += s / (float)np;
-    rssi += 4 * st[(rx * np) * 8 + 2] / (float)nof_prb / 12.0f;
   }
-  for (uint32_t p = 0; p < np; p++) {
-    float s = 0;
-    for (uint32_t rx = 0; rx < nrx; rx++) {
-      s += st[(rx * np + p) * 8 + 1];
+#pragma unroll
+  for (uint32_t p = 0; p < 4; p++) {
+    if (p < np) {
+      float s = 0;
+#pragma unroll
+      for (uint32_t rx = 0; rx < 4; rx++) {
+        if (rx < nrx) {
+          s += v[rx][p][1];
+        }
+      }
+      s /= (float)nrx;
+      best = s > best ? s : best;
     }
-    s /= (float)nrx;
-    best = s > best ? s : best;
   }
-  for (int idx = (int)(nrx * np) - 1; idx >= 0; idx--) {  // chest_estimate_cfo: last (rx, port<2) wins
-    if ((uint32_t)idx % np < 2) {
-      // chest_estimate_cfo (chest_dl.c:618-641): ns = SRSRAN_CP_NSYMB, ng = SRSRAN_CP_LEN_NORM(1, n) for both CPs
-      const float ng = (float)(int)ceilf(144.0f * sz / 2048.0f);
-      cfo            = -atan2f(st[idx * 8 + 4], st[idx * 8 + 3]) * sz / (nsymb * (sz + ng)) / 2 / 3.14159265358979f;
-      break;
+  // chest_estimate_cfo (chest_dl.c:618-641): the last (rx, port < 2) wins -- rx = nrx - 1, port = min(np, 2) - 1;
+  // ns = SRSRAN_CP_NSYMB, ng = SRSRAN_CP_LEN_NORM(1, n) for both CPs
+  float cre = 0, cim = 0;
+#pragma unroll
+  for (uint32_t rx = 0; rx < 4; rx++) {
+#pragma unroll
+    for (uint32_t p = 0; p < 2; p++) {
+      if (rx == nrx - 1 && p == min(np, 2u) - 1) {
+        cre = v[rx][p][3];
+        cim = v[rx][p][4];
+      }
     }
+  }
+  if (nrx * np > 0) {
+    const float ng = (float)(int)ceilf(144.0f * sz / 2048.0f);
+    cfo            = -atan2f(cim, cre) * sz / (nsymb * (sz + ng)) / 2 / 3.14159265358979f;
   }
   o[0]     = n / (float)nrx;
   o[1]     = best;

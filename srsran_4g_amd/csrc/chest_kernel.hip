@@ -70,6 +70,30 @@ __device__ float block_sum(float v, float* red)
   return s;
 }
 
+// block-wide sums of two floats under one pair of barriers (red: 2 CH_THREADS / 64 floats); each sum in
+// block_sum's order
+__device__ void block_sum2(float& a, float& b, float* red)
+{
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    a += __shfl_xor(a, off, 64);
+    b += __shfl_xor(b, off, 64);
+  }
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) {
+    red[threadIdx.x >> 6]                     = a;
+    red[CH_THREADS / 64 + (threadIdx.x >> 6)] = b;
+  }
+  __syncthreads();
+  float sa = 0.f, sb = 0.f;
+  for (int w = 0; w < CH_THREADS / 64; w++) {
+    sa += red[w];
+    sb += red[CH_THREADS / 64 + w];
+  }
+  a = sa;
+  b = sb;
+}
+
 // srsran_conv_same_cf (convolution.c:182-218): out[i] = sum_k f[k] x[i - M/2 + k] over the sequence extended
 // linearly at both ends (first[] / last[])
 __device__ void conv_row(const cx* comb, cx* avg, uint32_t nr, const float* filt, uint32_t M)
@@ -280,7 +304,7 @@ __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
   __shared__ cx    pe[4 * CHEST_MAX_NREF];
   __shared__ cx    comb[2 * CHEST_MAX_NREF];
   __shared__ cx    avg[4 * CHEST_MAX_NREF];
-  __shared__ float red[CH_THREADS / 64];
+  __shared__ float red[2 * CH_THREADS / 64];
 
   const uint32_t port = blockIdx.x / a.nrx, rx = blockIdx.x % a.nrx, b = blockIdx.y;
   const uint32_t tid  = threadIdx.x;
@@ -342,8 +366,9 @@ __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
     }
   }
   CH_STAMP(1);
-  rsrp = block_sum(rsrp, red) / (float)np;
-  rssi = block_sum(rssi, red) / (float)nsym;  // pe[] complete after block_sum's barriers
+  block_sum2(rsrp, rssi, red);  // pe[] complete after its barriers
+  rsrp = rsrp / (float)np;
+  rssi = rssi / (float)nsym;
   CH_STAMP(2);
   // the fused staging copies' PCIe reads go out here, after the grid loads have been consumed: issued first, they
   // held up every vmcnt wait behind them (loads retire in order); the LDS phases below cover their latency
@@ -360,8 +385,7 @@ __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
       cre += t.r;
       cim += t.i;
     }
-    cre = block_sum(cre, red);
-    cim = block_sum(cim, red);
+    block_sum2(cre, cim, red);
   }
 
   CH_STAMP(3);
@@ -541,7 +565,7 @@ __global__ __launch_bounds__(CH_THREADS) void chest_mbsfn_kernel(ChestArgs a)
 {
   __shared__ cx    pe[20 * CHEST_MAX_PRB];
   __shared__ cx    avg[20 * CHEST_MAX_PRB];
-  __shared__ float red[CH_THREADS / 64];
+  __shared__ float red[2 * CH_THREADS / 64];
   __shared__ float filt[8];
   const uint32_t   port = blockIdx.x / a.nrx, rx = blockIdx.x % a.nrx, tid = threadIdx.x;
   const uint32_t   nref = 2 * a.nof_prb, nm = 6 * a.nof_prb, np = 20 * a.nof_prb, nre = 12 * a.nof_prb;
@@ -677,7 +701,7 @@ hipError_t chest_finalize_kept_launch(float* stats, uint32_t np, uint32_t nrx, u
 // indices as chest_kernel takes them)
 __global__ __launch_bounds__(CH_THREADS) void chest_sync_kernel(ChestArgs a, float* out)
 {
-  __shared__ float red[CH_THREADS / 64];
+  __shared__ float red[2 * CH_THREADS / 64];
   const uint32_t   port = blockIdx.x / a.nrx, rx = blockIdx.x % a.nrx, b = blockIdx.y;
   const bool       bat  = a.sf_inl || a.sf_idx;
   const uint32_t   sfi  = a.sf_inl ? (uint32_t)a.sf_inline[b] : a.sf_idx ? a.sf_idx[b] : a.sf_index;
@@ -699,8 +723,7 @@ __global__ __launch_bounds__(CH_THREADS) void chest_sync_kernel(ChestArgs a, flo
         si += t.i;
       }
     }
-    sr = block_sum(sr, red);
-    si = block_sum(si, red);
+    block_sum2(sr, si, red);
     if (threadIdx.x == 0) {
       o[2 * l]     = sr;
       o[2 * l + 1] = si;

@@ -301,9 +301,10 @@ __device__ unsigned long long* g_chest_stamps = nullptr;
 __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
 {
   CH_STAMP(0);
-  __shared__ cx    pe[4 * CHEST_MAX_NREF];
-  __shared__ cx    comb[2 * CHEST_MAX_NREF];
-  __shared__ cx    avg[4 * CHEST_MAX_NREF];
+  // pe [4 nref] | comb [2 nref] | avg [2 nref, INTERPOLATE 4 nref] in dynamic LDS sized by chest_launch: 12.8 KB at
+  // 100 PRB with AVERAGE, within the 14 KB a CU keeps free beside the turbo decoder's two workgroups (C3), so the
+  // next batch's estimate runs beside the decoder
+  extern __shared__ __attribute__((aligned(16))) cx chest_lds[];
   __shared__ float red[2 * CH_THREADS / 64];
 
   const uint32_t port = blockIdx.x / a.nrx, rx = blockIdx.x % a.nrx, b = blockIdx.y;
@@ -312,6 +313,9 @@ __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
   const uint32_t sfi  = a.sf_inl ? (uint32_t)a.sf_inline[b] : a.sf_idx ? a.sf_idx[b] : a.sf_index;
   // CRS symbols of the port: 4 / 2, fewer in the DwPTS of a TDD special subframe
   const uint32_t nsym = chest_crs_nsym(a, sfi, port), nref = 2 * a.nof_prb, np = nsym * nref, nre = 12 * a.nof_prb;
+  cx* const      pe   = chest_lds;
+  cx* const      comb = pe + 4 * nref;
+  cx* const      avg  = comb + 2 * nref;
   const float2*  in   = a.grid + b * a.grid_sf_stride + (size_t)rx * 2 * a.nsymb * nre;
   const float2*  pil  = a.pilots + (bat ? sfi * CHEST_PILOTS_PER_SF : 0) + (size_t)(port / 2) * 4 * CHEST_MAX_NREF;
   const uint32_t fidx0 = (crs_v(port, 0) + a.cell_id % 6) % 6;
@@ -651,7 +655,8 @@ hipError_t chest_launch(const ChestArgs& a, hipStream_t stream, uint32_t nsf)
   if (nsf == 0) {
     return hipSuccess;
   }
-  hipLaunchKernelGGL(chest_kernel, dim3(a.nports * a.nrx, nsf), dim3(CH_THREADS), 0, stream, a);
+  const size_t lds = (size_t)(6 + (a.estimator == 1 ? 4 : 2)) * 2 * a.nof_prb * sizeof(cx);
+  hipLaunchKernelGGL(chest_kernel, dim3(a.nports * a.nrx, nsf), dim3(CH_THREADS), lds, stream, a);
   return hipGetLastError();
 }
 

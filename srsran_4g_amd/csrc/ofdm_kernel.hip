@@ -348,13 +348,15 @@ __global__ __launch_bounds__(OFDM_THREADS) void ofdm_tx_kernel(OfdmArgs a)
 
 // ---- N = 2048 / 1536 on one wave per symbol (ofdm_rx_wave_kernel) ----
 // N = 64 x M (M = 32 / 24): lane l holds x[l + 64 m], m < M, and takes their M-point DFT in registers (4 x 8 /
-// 3 x 8), twiddles it by W_N^(l k2), writes it to a wave-private LDS tile [k2][l] (rows padded to 65: the column
-// reads below are bank-conflict free), and reads back every second element of row k2 = lane / 2 from parity
-// p = lane & 1: a 32-point DFT of those is half of row k2's 64-point DFT, the other half sits in the neighbour lane,
-// and one radix-2 step across the pair (a DPP swap) gives X[k2 + M k1].  Two register FFTs and one LDS transpose a
-// symbol instead of four LDS stages and eight workgroup barriers; the same forward DFT as the Stockham kernels,
-// rounded in another order.  (M = 24: lanes 48..63 idle in the second half.)
-static constexpr int WV_ROW = 65;  // LDS row stride of the transpose tile (float2)
+// 3 x 8), twiddles it by W_N^(l k2), writes it to a wave-private LDS tile [k2][l], and reads back every second
+// element of row k2 = lane / 2 from parity p = lane & 1: a 32-point DFT of those is half of row k2's 64-point DFT,
+// the other half sits in the neighbour lane, and one radix-2 step across the pair (a DPP swap) gives
+// X[k2 + M k1].  Two register FFTs and one LDS transpose a symbol instead of four LDS stages and eight workgroup
+// barriers; the same forward DFT as the Stockham kernels, rounded in another order.  (M = 24: lanes 48..63 idle in
+// the second half.)  The tile holds one float plane at a time -- real parts, then imaginary parts -- so a wave
+// needs 8.4 KB of LDS: the 14 KB a CU keeps free beside the turbo decoder's two 73 KB workgroups (C3, K = 5824)
+// take one, so the next batch's OFDM runs beside the decoder instead of waiting for it.
+static constexpr int WV_ROW = 66;  // LDS row stride of the transpose tile (floats): column reads conflict-free
 
 // natural-order M-point DFT in place (M = 32: m = 8 m1 + m2, k = k1 + 4 k2; M = 24: k = k1 + 3 k2); the inner
 // twiddles W_M^j = W_N^(TS j), TS = N / M, come from the symbol's table
@@ -405,7 +407,7 @@ template <uint32_t N, bool CFO>
 __global__ __launch_bounds__(64) void ofdm_rx_wave_kernel(OfdmArgs a)
 {
   constexpr int      M = (int)(N / 64);
-  __shared__ float2  T[M * WV_ROW];
+  __shared__ float   T[M * WV_ROW];
   const uint32_t     sym = blockIdx.x, rx = blockIdx.y, sf = blockIdx.z, l = threadIdx.x;
   const uint32_t     ns = a.nsymb, slot = sym / ns, i = sym % ns;
   const uint32_t     slot_sz = ns * N + a.cp0 + (ns - 1) * a.cp;
@@ -436,17 +438,34 @@ __global__ __launch_bounds__(64) void ofdm_rx_wave_kernel(OfdmArgs a)
       w[k2] = tw[l * k2];  // l k2 <= 63 (M - 1) < N
     }
 #pragma unroll
-    for (int k2 = 0; k2 < M; k2++) {
-      T[k2 * WV_ROW + l] = k2 ? cmul(v[k2], w[k2]) : v[k2];
+    for (int k2 = 1; k2 < M; k2++) {
+      v[k2] = cmul(v[k2], w[k2]);
     }
+  }
+  const uint32_t kk = l >> 1, p = l & 1, row = kk < (uint32_t)M ? kk : 0;
+  float2         y[32];
+  // the real plane, then the imaginary one
+#pragma unroll
+  for (int k2 = 0; k2 < M; k2++) {
+    T[k2 * WV_ROW + l] = v[k2].x;
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront", "local");
   __builtin_amdgcn_wave_barrier();
-  const uint32_t kk = l >> 1, p = l & 1, row = kk < (uint32_t)M ? kk : 0;
-  float2         y[32];
 #pragma unroll
   for (int j = 0; j < 32; j++) {
-    y[j] = T[row * WV_ROW + 2 * j + p];
+    y[j].x = T[row * WV_ROW + 2 * j + p];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront", "local");  // the real plane read out
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int k2 = 0; k2 < M; k2++) {
+    T[k2 * WV_ROW + l] = v[k2].y;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront", "local");
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int j = 0; j < 32; j++) {
+    y[j].y = T[row * WV_ROW + 2 * j + p];
   }
   dft_reg<32, (int)(N / 32)>(y, tw);
   // X[kk + M k] = Y0[k] + W_64^k Y1[k], X[kk + M (k + 32)] = Y0[k] - W_64^k Y1[k]; W_64^k = W_N^(M k)

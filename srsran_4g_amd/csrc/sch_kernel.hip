@@ -108,8 +108,10 @@ __device__ __forceinline__ uint2 rm_group(uint2 iv, uint2 v, const short* es, ui
 __global__ __launch_bounds__(RM_LDS_THREADS) void rm_rx_lds_kernel(const RmSlot* __restrict__ slots)
 {
   // E LLRs staged as 16-byte words from the aligned address at or below e (es = the E values from `sh` on;
-  // the words never cross a page, so reading the partial first / last word stays inside mapped memory)
-  __shared__ uint4 es4[(RM_LDS_MAX_E + 7) / 8 + 1];
+  // the words never cross a page, so reading the partial first / last word stays inside mapped memory).  Dynamic
+  // LDS sized to the launch's largest E (rm_rx_launch): 14.4 KB for C3, within the 16 KB a CU keeps free beside
+  // the turbo decoder's two workgroups, so another batch's de-matching runs beside the decoder
+  extern __shared__ uint4 es4[];
   const RmSlot     s = slots[blockIdx.x];
   if (!s.overwrite && *gptr(s.skip)) {
     return;
@@ -157,7 +159,7 @@ __global__ __launch_bounds__(RM_LDS_THREADS) void rm_rx_lds_kernel(const RmSlot*
 }
 
 static constexpr int TB_CHUNK       = 16 * 64;  // payload bytes per assembly chunk (one wave, 16 B a lane)
-static constexpr int TB_FIN_THREADS = 1024;  // 16 waves: a C3 TB's ~10 chunks in one round
+static constexpr int TB_FIN_THREADS = 512;  // 8 waves: 2 a SIMD fit beside the turbo decoder (a C3 TB: ~10 chunks, 2 rounds)
 static constexpr int TB_THREADS     = TB_FIN_THREADS;  // reset_range stride
 
 // a * b mod P over GF(2) at compile time (the CRC placement tables below)
@@ -476,7 +478,8 @@ hipError_t rm_rx_launch(const RmSlot* d_slots, uint32_t nslots, uint32_t max_len
   if (max_e <= (uint32_t)RM_LDS_MAX_E) {
     for (uint32_t s0 = 0; s0 < nslots; s0 += 65535) {
       const uint32_t n = nslots - s0 < 65535 ? nslots - s0 : 65535;
-      hipLaunchKernelGGL(rm_rx_lds_kernel, dim3(n), dim3(RM_LDS_THREADS), 0, stream, d_slots + s0);
+      hipLaunchKernelGGL(rm_rx_lds_kernel, dim3(n), dim3(RM_LDS_THREADS), ((size_t)(max_e + 7) / 8 + 1) * sizeof(uint4),
+                         stream, d_slots + s0);
     }
     return hipGetLastError();
   }

@@ -353,10 +353,11 @@ __global__ __launch_bounds__(OFDM_THREADS) void ofdm_tx_kernel(OfdmArgs a)
 // the other half sits in the neighbour lane, and one radix-2 step across the pair (a DPP swap) gives
 // X[k2 + M k1].  Two register FFTs and one LDS transpose a symbol instead of four LDS stages and eight workgroup
 // barriers; the same forward DFT as the Stockham kernels, rounded in another order.  (M = 24: lanes 48..63 idle in
-// the second half.)  The tile holds one float plane at a time -- real parts, then imaginary parts -- so a wave
-// needs 8.4 KB of LDS: the 14 KB a CU keeps free beside the turbo decoder's two 73 KB workgroups (C3, K = 5824)
-// take one, so the next batch's OFDM runs beside the decoder instead of waiting for it.
-static constexpr int WV_ROW = 66;  // LDS row stride of the transpose tile (floats): column reads conflict-free
+// the second half.)  The tile holds one float plane at a time -- real parts, then imaginary parts -- in rows of 64
+// floats with the column index XOR-swizzled by 2 k2 (both the row writes and the column reads conflict-free), so a
+// wave needs 8 KB of LDS: the 16 KB a CU keeps free beside the turbo decoder's two 72 KB workgroups (C3,
+// K = 5824) take two, so the next batch's OFDM runs beside the decoder instead of waiting for it.
+static constexpr int WV_ROW = 64;  // LDS row length of the transpose tile (floats)
 
 // natural-order M-point DFT in place (M = 32: m = 8 m1 + m2, k = k1 + 4 k2; M = 24: k = k1 + 3 k2); the inner
 // twiddles W_M^j = W_N^(TS j), TS = N / M, come from the symbol's table
@@ -447,25 +448,25 @@ __global__ __launch_bounds__(64) void ofdm_rx_wave_kernel(OfdmArgs a)
   // the real plane, then the imaginary one
 #pragma unroll
   for (int k2 = 0; k2 < M; k2++) {
-    T[k2 * WV_ROW + l] = v[k2].x;
+    T[k2 * WV_ROW + (l ^ (2 * k2))] = v[k2].x;
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront", "local");
   __builtin_amdgcn_wave_barrier();
 #pragma unroll
   for (int j = 0; j < 32; j++) {
-    y[j].x = T[row * WV_ROW + 2 * j + p];
+    y[j].x = T[row * WV_ROW + ((2 * j + p) ^ (2 * row))];
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront", "local");  // the real plane read out
   __builtin_amdgcn_wave_barrier();
 #pragma unroll
   for (int k2 = 0; k2 < M; k2++) {
-    T[k2 * WV_ROW + l] = v[k2].y;
+    T[k2 * WV_ROW + (l ^ (2 * k2))] = v[k2].y;
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront", "local");
   __builtin_amdgcn_wave_barrier();
 #pragma unroll
   for (int j = 0; j < 32; j++) {
-    y[j].y = T[row * WV_ROW + 2 * j + p];
+    y[j].y = T[row * WV_ROW + ((2 * j + p) ^ (2 * row))];
   }
   dft_reg<32, (int)(N / 32)>(y, tw);
   // X[kk + M k] = Y0[k] + W_64^k Y1[k], X[kk + M (k + 32)] = Y0[k] - W_64^k Y1[k]; W_64^k = W_N^(M k)

@@ -301,9 +301,10 @@ __device__ unsigned long long* g_chest_stamps = nullptr;
 __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
 {
   CH_STAMP(0);
-  // pe [4 nref] | comb [2 nref] | avg [2 nref, INTERPOLATE 4 nref] in dynamic LDS sized by chest_launch: 12.8 KB at
-  // 100 PRB with AVERAGE, within the 14 KB a CU keeps free beside the turbo decoder's two workgroups (C3), so the
-  // next batch's estimate runs beside the decoder
+  // pe [4 nref] in dynamic LDS sized by chest_launch; AVERAGE builds its comb in place over pe's first rows and
+  // smooths it into the last two, so a workgroup needs 6.4 KB at 100 PRB (INTERPOLATE with a filter: avg [4 nref]
+  // after pe, 12.8 KB) -- two fit in the 16 KB a CU keeps free beside the turbo decoder's two workgroups (C3), so
+  // the next batch's estimate runs beside the decoder
   extern __shared__ __attribute__((aligned(16))) cx chest_lds[];
   __shared__ float red[2 * CH_THREADS / 64];
 
@@ -314,8 +315,9 @@ __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
   // CRS symbols of the port: 4 / 2, fewer in the DwPTS of a TDD special subframe
   const uint32_t nsym = chest_crs_nsym(a, sfi, port), nref = 2 * a.nof_prb, np = nsym * nref, nre = 12 * a.nof_prb;
   cx* const      pe   = chest_lds;
-  cx* const      comb = pe + 4 * nref;
-  cx* const      avg  = comb + 2 * nref;
+  cx* const      comb = pe;  // AVERAGE: over pe's first 2 nref entries, written after the averages are taken
+  cx* const      avg  = a.filter_none ? pe : a.estimator == 1 ? pe + 4 * nref : pe + 2 * nref;
+  static_assert(2 * CHEST_MAX_PRB <= CH_THREADS, "one comb position a thread");
   const float2*  in   = a.grid + b * a.grid_sf_stride + (size_t)rx * 2 * a.nsymb * nre;
   const float2*  pil  = a.pilots + (bat ? sfi * CHEST_PILOTS_PER_SF : 0) + (size_t)(port / 2) * 4 * CHEST_MAX_NREF;
   const uint32_t fidx0 = (crs_v(port, 0) + a.cell_id % 6) % 6;
@@ -416,36 +418,33 @@ __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
     // INTERPOLATE: every CRS symbol smoothed on its own (below)
   } else if (a.filter_none) {
     // no average_pilots: AVERAGE interpolates the raw LS estimates -- with more than one CRS symbol the first 4 N_RB
-    // of them as one comb of spacing 3 (interp_lin_3 over pilot_estimates, chest_dl.c:476-481, 724-725)
+    // of them as one comb of spacing 3 (interp_lin_3 over pilot_estimates, chest_dl.c:476-481, 724-725): pe itself
     nr = nsym > 1 ? 2 * nref : nref;
-    for (uint32_t k = tid; k < nr; k += CH_THREADS) {
-      comb[k] = pe[k];
-    }
   } else if (nsym > 1) {
-    for (uint32_t k = tid; k < nref; k += CH_THREADS) {
-      cx e0 = pe[(fidx0 < 3 ? 0 : 1) * nref + k], e1 = pe[(fidx0 < 3 ? 1 : 0) * nref + k];
+    // the averages in registers first: the comb then overwrites the pe rows they came from
+    const uint32_t k  = tid;
+    cx             e0 = {0.f, 0.f}, e1 = {0.f, 0.f};
+    if (k < nref) {
+      e0 = pe[(fidx0 < 3 ? 0 : 1) * nref + k];
+      e1 = pe[(fidx0 < 3 ? 1 : 0) * nref + k];
       for (uint32_t l = 2; l + 1 < nsym; l += 2) {
         e0 = add(e0, pe[(fidx0 < 3 ? l : l + 1) * nref + k]);
         e1 = add(e1, pe[(fidx0 < 3 ? l + 1 : l) * nref + k]);
       }
+    }
+    __syncthreads();
+    if (k < nref) {
       comb[2 * k]     = scl(e0, 2.0f / (float)nsym);
       comb[2 * k + 1] = scl(e1, 2.0f / (float)nsym);
     }
     nr = 2 * nref;
-  } else {
-    for (uint32_t k = tid; k < nref; k += CH_THREADS) {
-      comb[k] = pe[k];
-    }
-  }
+  }  // (one CRS symbol: the comb is pe's first row as it is)
   __syncthreads();
   // the smoothing filter lives in LDS: a private array indexed by the tap loop would spill to scratch
   __shared__ float filt[8];
   const uint32_t   M = load_filter(a, noise, filt);
-  if (a.filter_none) {  // the estimates as they are (a 1-tap unit filter would give the same values)
-    const uint32_t n = a.estimator == 1 ? nsym * nref : nr;
-    for (uint32_t k = tid; k < n; k += CH_THREADS) {
-      avg[k] = a.estimator == 1 ? pe[k] : comb[k];
-    }
+  if (a.filter_none) {
+    // the estimates as they are (a 1-tap unit filter would give the same values): avg is pe
   } else if (a.estimator == 1) {
     for (uint32_t l = 0; l < nsym; l++) {
       conv_row(pe + l * nref, avg + l * nref, nref, filt, M);
@@ -655,7 +654,7 @@ hipError_t chest_launch(const ChestArgs& a, hipStream_t stream, uint32_t nsf)
   if (nsf == 0) {
     return hipSuccess;
   }
-  const size_t lds = (size_t)(6 + (a.estimator == 1 ? 4 : 2)) * 2 * a.nof_prb * sizeof(cx);
+  const size_t lds = (size_t)(a.estimator == 1 && !a.filter_none ? 8 : 4) * 2 * a.nof_prb * sizeof(cx);
   hipLaunchKernelGGL(chest_kernel, dim3(a.nports * a.nrx, nsf), dim3(CH_THREADS), lds, stream, a);
   return hipGetLastError();
 }

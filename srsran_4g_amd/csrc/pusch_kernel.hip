@@ -69,16 +69,20 @@ __device__ __forceinline__ void block_sum(float (&v)[NV], float* red)
 }
 
 // ---------------------------------------------------------------- channel estimation
-__global__ __launch_bounds__(PU_THREADS) void chest_ul_kernel(const PuschUe* __restrict__ ues)
+// 16 waves a UE: 78 UEs are 78 workgroups, so each one's 2 M pilots and 14 M estimate stores spread over more
+// threads (the estimate copy to every symbol of the slot is most of the kernel's bytes)
+static constexpr int CHUL_THREADS = 1024;
+
+__global__ __launch_bounds__(CHUL_THREADS) void chest_ul_kernel(const PuschUe* __restrict__ ues)
 {
   const PuschUe& u = ues[blockIdx.x];
   __shared__ float2 pe[2 * PUSCH_MAX_M];
-  __shared__ float  red[(PU_THREADS / 64) * 11];
+  __shared__ float  red[(CHUL_THREADS / 64) * 11];
   const uint32_t    M = u.M;
 
   // LS estimates; received pilot sum and power
   float acc[11] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (uint32_t k = threadIdx.x; k < 2 * M; k += PU_THREADS) {
+  for (uint32_t k = threadIdx.x; k < 2 * M; k += CHUL_THREADS) {
     const uint32_t s = k >= M ? 1u : 0u, j = k - s * M;
     const uint32_t L = (s + 1) * u.nsym_slot - 4;
     const c2       rx = mk(u.grid[(size_t)L * u.ncell_re + u.n_tilde[s] * 12 + j]);
@@ -90,7 +94,7 @@ __global__ __launch_bounds__(PU_THREADS) void chest_ul_kernel(const PuschUe* __r
 
   // smoothing, estimate grid, noise, CFO and TA correlations
   const float f0 = u.filt[0], f1 = u.filt[1], f2 = u.filt[2];
-  for (uint32_t k = threadIdx.x; k < 2 * M; k += PU_THREADS) {
+  for (uint32_t k = threadIdx.x; k < 2 * M; k += CHUL_THREADS) {
     const uint32_t s = k >= M ? 1u : 0u, j = k - s * M;
     const float2*  p = pe + s * M;
     const c2       x = mk(p[j]);
@@ -167,7 +171,7 @@ hipError_t chest_ul_launch(const PuschUe* d_ues, uint32_t nue, hipStream_t strea
     return hipSuccess;
   }
   StageScope timing_scope(ST_CHEST_UL, stream);
-  hipLaunchKernelGGL(chest_ul_kernel, dim3(nue), dim3(PU_THREADS), 0, stream, d_ues);
+  hipLaunchKernelGGL(chest_ul_kernel, dim3(nue), dim3(CHUL_THREADS), 0, stream, d_ues);
   return hipGetLastError();
 }
 

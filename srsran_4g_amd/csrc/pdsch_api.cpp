@@ -371,8 +371,10 @@ int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sf
   for (size_t i = 0; i < cws.size() && fused; i++) {
     const Cw& c = cws[i];
     fused       = (sf_mod[c.sf] < 0 || sf_mod[c.sf] == c.mod) && c.cw < 2;
-    sf_mod[c.sf]            = c.mod;
-    sf_cw[c.sf * 2 + c.cw] = (uint32_t)i;
+    if (fused) {
+      sf_mod[c.sf]           = c.mod;
+      sf_cw[c.sf * 2 + c.cw] = (uint32_t)i;
+    }
   }
   for (uint32_t b = 0; b < nsf && fused; b++) {
     const srsran_pdsch_grant_t& gr = sfs[b].cfg->grant;

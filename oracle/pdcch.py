@@ -36,9 +36,13 @@ class Ref:
         L = ctypes.CDLL(REF_SO, mode=os.RTLD_LAZY)
         L.ref_regs_tables.argtypes = [u32, u32, u32, ctypes.c_int, ctypes.c_int, u32p, u32p, u32, u32p]
         L.ref_regs_tables_mi.argtypes = [u32, u32, u32, ctypes.c_int, ctypes.c_int, u32, u32p, u32p, u32, u32p]
+        L.ref_regs_tables_opts.argtypes = [u32, u32, u32, ctypes.c_int, ctypes.c_int, u32, ctypes.c_int, u32p, u32p,
+                                           u32, u32p]
         L.ref_set_cp.argtypes = [ctypes.c_int]  # process-global in the harness (normal CP until set)
         L.ref_ctrl_tx.argtypes = [u32, u32, u32, ctypes.c_int, ctypes.c_int, u32, u32, u32, u8p, u32p, u32p, u32p,
                                   u16p, f32p]
+        L.ref_ctrl_tx_opts.argtypes = [u32, u32, u32, ctypes.c_int, ctypes.c_int, u32, ctypes.c_int, u32, u32, u32, u8p,
+                                       u32p, u32p, u32p, u16p, f32p]
         L.ref_ctrl_rx.argtypes = [u32, u32, u32, ctypes.c_int, ctypes.c_int, u32, u32, f32p, f32p, ctypes.c_float,
                                   ctypes.POINTER(u32), ctypes.POINTER(ctypes.c_float), f32p]
         L.ref_pdcch_decode.argtypes = [u32, u32, f32p, u32, u32, u32, ctypes.c_int, u32, u8p,
@@ -53,19 +57,21 @@ class Ref:
         """cyclic prefix of the reference cells built from now on (0 normal, 1 extended)"""
         self.L.ref_set_cp(int(ext))
 
-    def regs_tables(self, nof_prb, nof_ports, cell_id, phich_len=0, phich_res=2, phich_mi=1):
-        """regs.c tables of srsran_regs_init_opts(cell, phich_mi) (regs.c:711-783)"""
+    def regs_tables(self, nof_prb, nof_ports, cell_id, phich_len=0, phich_res=2, phich_mi=1, sf1_6=False):
+        """regs.c tables of srsran_regs_init_opts(cell, phich_mi, sf1_6) (regs.c:693-783; sf1_6 =
+        mbsfn_or_sf1_6_tdd, the extended-duration PHICH limited to two symbols, regs.c:329-340)"""
         maxre = 4 * 12 * nof_prb
         pc = np.zeros(16, np.uint32)
         pd = np.zeros(3 * maxre, np.uint32)
         nre = np.zeros(3, np.uint32)
-        if self.L.ref_regs_tables_mi(nof_prb, nof_ports, cell_id, phich_len, phich_res, phich_mi, pc, pd, maxre,
-                                     nre) != 16:
+        if self.L.ref_regs_tables_opts(nof_prb, nof_ports, cell_id, phich_len, phich_res, phich_mi, int(sf1_6), pc,
+                                       pd, maxre, nre) != 16:
             raise RuntimeError("ref_regs_tables failed")
         return pc, [pd[c * maxre:c * maxre + nre[c]].copy() for c in range(3)]
 
-    def ctrl_tx(self, nof_prb, nof_ports, cell_id, tti, cfi, msgs, phich_len=0, phich_res=2):
-        """msgs: list of (bits uint8[nof_bits], L, ncce, rnti).  Returns [port] grids (14, 12 nof_prb)."""
+    def ctrl_tx(self, nof_prb, nof_ports, cell_id, tti, cfi, msgs, phich_len=0, phich_res=2, phich_mi=1, sf1_6=False):
+        """msgs: list of (bits uint8[nof_bits], L, ncce, rnti).  Returns [port] grids (14, 12 nof_prb).  phich_mi /
+        sf1_6: the REG tables of srsran_regs_init_opts (a TDD cell's m_i; its extended-duration subframes 1 / 6)."""
         n = len(msgs)
         pl = np.zeros((max(n, 1), DCI_MAX_BITS), np.uint8)
         nb = np.zeros(max(n, 1), np.uint32)
@@ -77,8 +83,8 @@ class Ref:
             nb[i], Ls[i], nc[i], rn[i] = len(bits), L, ncce, rnti
         g = np.zeros((nof_ports, 14, 12 * nof_prb), np.complex64)
         gf = g.view(np.float32).reshape(-1)
-        if self.L.ref_ctrl_tx(nof_prb, nof_ports, cell_id, phich_len, phich_res, tti, cfi, n, pl.reshape(-1), nb, Ls,
-                              nc, rn, gf) != 0:
+        if self.L.ref_ctrl_tx_opts(nof_prb, nof_ports, cell_id, phich_len, phich_res, phich_mi, int(sf1_6), tti, cfi,
+                                   n, pl.reshape(-1), nb, Ls, nc, rn, gf) != 0:
             raise RuntimeError("ref_ctrl_tx failed")
         return gf.view(np.complex64).reshape(nof_ports, 14, 12 * nof_prb)
 

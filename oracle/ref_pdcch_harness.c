@@ -145,12 +145,13 @@ static srsran_cell_t mkcell(uint32_t nof_prb, uint32_t nof_ports, uint32_t id, i
 
 /* Grid indices (l * 12 * nof_prb + k) of the PCFICH REs (16) and of the PDCCH REs for CFI 1..3
  * in srsran_regs_*_get order; nre[c] = number of PDCCH REs for CFI c + 1. */
-int ref_regs_tables_mi(uint32_t nof_prb, uint32_t nof_ports, uint32_t id, int phich_len, int phich_res,
-                       uint32_t phich_mi, uint32_t* pcfich, uint32_t* pdcch, uint32_t max_re, uint32_t* nre)
+int ref_regs_tables_opts(uint32_t nof_prb, uint32_t nof_ports, uint32_t id, int phich_len, int phich_res,
+                         uint32_t phich_mi, int mbsfn_or_sf1_6_tdd, uint32_t* pcfich, uint32_t* pdcch, uint32_t max_re,
+                         uint32_t* nre)
 {
   srsran_cell_t cell = mkcell(nof_prb, nof_ports, id, phich_len, phich_res);
   srsran_regs_t regs;
-  if (srsran_regs_init_opts(&regs, cell, phich_mi, false)) {
+  if (srsran_regs_init_opts(&regs, cell, phich_mi, mbsfn_or_sf1_6_tdd != 0)) {
     return -1;
   }
   const uint32_t n    = 14 * 12 * nof_prb;
@@ -179,6 +180,12 @@ int ref_regs_tables_mi(uint32_t nof_prb, uint32_t nof_ports, uint32_t id, int ph
   return k;
 }
 
+int ref_regs_tables_mi(uint32_t nof_prb, uint32_t nof_ports, uint32_t id, int phich_len, int phich_res,
+                       uint32_t phich_mi, uint32_t* pcfich, uint32_t* pdcch, uint32_t max_re, uint32_t* nre)
+{
+  return ref_regs_tables_opts(nof_prb, nof_ports, id, phich_len, phich_res, phich_mi, 0, pcfich, pdcch, max_re, nre);
+}
+
 /* srsran_regs_init's tables (PHICH m_i = 1) */
 int ref_regs_tables(uint32_t nof_prb, uint32_t nof_ports, uint32_t id, int phich_len, int phich_res,
                     uint32_t* pcfich, uint32_t* pdcch, uint32_t max_re, uint32_t* nre)
@@ -188,15 +195,18 @@ int ref_regs_tables(uint32_t nof_prb, uint32_t nof_ports, uint32_t id, int phich
 
 /* eNB control region: PCFICH with `cfi` and ndci PDCCH messages (payload bits, nof_bits, L (log2),
  * ncce, rnti each) added into nof_ports grids of 14 * 12 * nof_prb cf_t (interleaved re/im). */
-int ref_ctrl_tx(uint32_t nof_prb, uint32_t nof_ports, uint32_t id, int phich_len, int phich_res, uint32_t tti, uint32_t cfi,
-                uint32_t ndci, const uint8_t* payloads, const uint32_t* nof_bits, const uint32_t* L, const uint32_t* ncce,
-                const uint16_t* rnti, float* grids)
+/* The same on the REG tables of srsran_regs_init_opts(cell, phich_mi, mbsfn_or_sf1_6_tdd): the control region a
+ * TDD eNB with that PHICH m_i (and, with the extended PHICH duration, subframe 1 / 6's two-symbol PHICH) transmits. */
+int ref_ctrl_tx_opts(uint32_t nof_prb, uint32_t nof_ports, uint32_t id, int phich_len, int phich_res, uint32_t phich_mi,
+                     int mbsfn_or_sf1_6_tdd, uint32_t tti, uint32_t cfi, uint32_t ndci, const uint8_t* payloads,
+                     const uint32_t* nof_bits, const uint32_t* L, const uint32_t* ncce, const uint16_t* rnti, float* grids)
 {
   srsran_cell_t   cell = mkcell(nof_prb, nof_ports, id, phich_len, phich_res);
   srsran_regs_t   regs;
   srsran_pcfich_t pcfich;
   srsran_pdcch_t  pdcch;
-  if (srsran_regs_init(&regs, cell) || srsran_pcfich_init(&pcfich, 0) || srsran_pcfich_set_cell(&pcfich, &regs, cell) ||
+  if (srsran_regs_init_opts(&regs, cell, phich_mi, mbsfn_or_sf1_6_tdd != 0) || srsran_pcfich_init(&pcfich, 0) ||
+      srsran_pcfich_set_cell(&pcfich, &regs, cell) ||
       srsran_pdcch_init_enb(&pdcch, nof_prb) || srsran_pdcch_set_cell(&pdcch, &regs, cell)) {
     return -1;
   }
@@ -223,6 +233,14 @@ int ref_ctrl_tx(uint32_t nof_prb, uint32_t nof_ports, uint32_t id, int phich_len
   srsran_pcfich_free(&pcfich);
   srsran_regs_free(&regs);
   return ret;
+}
+
+int ref_ctrl_tx(uint32_t nof_prb, uint32_t nof_ports, uint32_t id, int phich_len, int phich_res, uint32_t tti, uint32_t cfi,
+                uint32_t ndci, const uint8_t* payloads, const uint32_t* nof_bits, const uint32_t* L, const uint32_t* ncce,
+                const uint16_t* rnti, float* grids)
+{
+  return ref_ctrl_tx_opts(nof_prb, nof_ports, id, phich_len, phich_res, 1, 0, tti, cfi, ndci, payloads, nof_bits, L,
+                          ncce, rnti, grids);
 }
 
 /* UE control region on given grids and estimates:

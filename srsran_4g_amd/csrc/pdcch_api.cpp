@@ -78,7 +78,7 @@ void reg_init(Reg& r, uint32_t l, uint32_t nreg, uint32_t base, int maxreg, uint
   }
 }
 
-int build_regs(srsran_regs_t* h, uint32_t phich_mi)
+int build_regs(srsran_regs_t* h, uint32_t phich_mi, bool mbsfn_or_sf1_6)
 {
   const srsran_cell_t& c     = h->cell;
   const uint32_t       nprb  = c.nof_prb;
@@ -132,7 +132,8 @@ int build_regs(srsran_regs_t* h, uint32_t phich_mi)
       h->pcfich_re[4 * q + e] = r->k[e] + r->l * nre;
     }
   }
-  // PHICH (36.211 6.9.3), normal duration
+  // PHICH (36.211 6.9.3, regs.c:249-350): m' mapping units of 3 REGs; normal duration in symbol 0, extended
+  // duration in symbols 0-2 (li = i), or in symbols 0-1 of MBSFN / TDD subframe 1 and 6 (li = (m'/2 + i + 1) mod 2)
   float ng = 0;
   switch (h->phich_res) {
     case SRSRAN_PHICH_R_1_6:
@@ -150,22 +151,26 @@ int build_regs(srsran_regs_t* h, uint32_t phich_mi)
   }
   h->ngroups_phich_m1 = (uint32_t)(int)ceilf(ng * ((float)nprb / 8));
   h->ngroups_phich    = phich_mi * h->ngroups_phich_m1;
-  if (h->phich_len != SRSRAN_PHICH_NORM && h->ngroups_phich) {
-    fprintf(stderr, "[srsran_regs] extended PHICH duration is not provided\n");
-    return SRSRAN_ERROR;
-  }
   if (h->ngroups_phich) {
-    std::vector<Reg*> l0;
+    const bool        ext = h->phich_len == SRSRAN_PHICH_EXT;
+    std::vector<Reg*> lr[3];  // free REGs of symbols 0-2, lowest frequency first
     for (Reg& r : regs) {
-      if (r.l == 0 && !r.assigned) {
-        l0.push_back(&r);
+      if (r.l < 3 && !r.assigned) {
+        lr[r.l].push_back(&r);
       }
     }
-    const uint32_t n0 = (uint32_t)l0.size();
+    uint32_t n[3];
+    for (int l = 0; l < 3; l++) {
+      n[l] = (uint32_t)lr[l].size();
+    }
     for (uint32_t mi = 0; mi < h->ngroups_phich; mi++) {
       for (uint32_t q = 0; q < 3; q++) {
-        const uint32_t ni = ((c.id * n0 / n0) + mi + q * n0 / 3) % n0;
-        l0[ni]->assigned  = true;
+        const uint32_t li = !ext ? 0 : mbsfn_or_sf1_6 ? (mi / 2 + q + 1) % 2 : q;
+        if (n[li] == 0 || (ext && mbsfn_or_sf1_6 && n[1] == 0)) {
+          return SRSRAN_ERROR;
+        }
+        const uint32_t ni = ((c.id * n[li] / (ext && mbsfn_or_sf1_6 ? n[1] : n[0])) + mi + q * n[li] / 3) % n[li];
+        lr[li][ni]->assigned = true;
       }
     }
   }
@@ -372,7 +377,7 @@ int srsran_regs_init(srsran_regs_t* h, srsran_cell_t cell)
 
 int srsran_regs_init_opts(srsran_regs_t* h, srsran_cell_t cell, uint32_t phich_mi, bool mbsfn_or_sf1_6_tdd)
 {
-  if (!h || !valid_cell(cell) || mbsfn_or_sf1_6_tdd) {
+  if (!h || !valid_cell(cell)) {
     return SRSRAN_ERROR_INVALID_INPUTS;
   }
   memset(h, 0, sizeof(*h));
@@ -380,7 +385,7 @@ int srsran_regs_init_opts(srsran_regs_t* h, srsran_cell_t cell, uint32_t phich_m
   h->phich_res = cell.phich_resources;
   h->phich_len = cell.phich_length;
   h->phich_mi  = phich_mi;
-  if (build_regs(h, phich_mi)) {
+  if (build_regs(h, phich_mi, mbsfn_or_sf1_6_tdd)) {
     srsran_regs_free(h);
     return SRSRAN_ERROR;
   }

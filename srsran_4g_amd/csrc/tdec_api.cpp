@@ -342,8 +342,28 @@ int tdec_sch_enqueue(uint32_t      K,
 }  // namespace srsran_amd
 
 namespace {
-void* scratch8(hipStream_t stream, size_t bytes);
-}
+// Scratch of one 8-bit launch (the beta of a MAP pass / the widened int16 input), stream-ordered: allocated on
+// the launch's stream and released on it behind the launch, so nothing outlives the call, no process-wide cache
+// keyed by stream, no synchronisation (the device memory pool recycles the bytes).
+struct Scratch8 {
+  void*       p = nullptr;
+  hipStream_t s = nullptr;
+  Scratch8(hipStream_t stream, size_t bytes) : s(stream)
+  {
+    if (hipMallocAsync(&p, bytes, stream) != hipSuccess) {
+      p = nullptr;
+    }
+  }
+  ~Scratch8()
+  {
+    if (p) {
+      hipFreeAsync(p, s);
+    }
+  }
+  Scratch8(const Scratch8&)            = delete;
+  Scratch8& operator=(const Scratch8&) = delete;
+};
+}  // namespace
 
 namespace srsran_amd {
 // DL-SCH decode with llr_is_8bit of ncb blocks of K > 800 (the 8-bit window decoders, 16 / 32 sub-blocks): int8 soft
@@ -382,7 +402,8 @@ int tdec8_sch_enqueue(uint32_t      K,
   a.xpow_b     = xp->d[1];
   a.min_iters  = 2;  // SRSRAN_PDSCH_MIN_TDEC_ITERS (sch.c:35)
   qpp_coeffs((uint32_t)idx, &a.f1, &a.f2);
-  a.beta = (uint2*)scratch8(stream, tdec8bit_beta_bytes((int)nsb, K, ncb));
+  Scratch8 beta(stream, tdec8bit_beta_bytes((int)nsb, K, ncb));
+  a.beta = (uint2*)beta.p;
   if (!a.beta) {
     return SRSRAN_ERROR;
   }
@@ -726,7 +747,8 @@ struct StreamPool {
   hipStream_t s[kPoolStreams];
   hipEvent_t  done[kPoolStreams];
   hipEvent_t  fork;
-  MultiDesc   md[5];  // launch entries: 16 (16-step windows), 16 (8-step part), 8, generic (large K), generic (small K)
+  hipEvent_t  large_done;  // the 16-step part's largest sizes finished (gates the other classes, tdec_gate())
+  MultiDesc   md[6];  // launch entries: 16 (16-step, large K), 16 (16-step, mid K), 16 (8-step part), 8, generic x 2
 };
 std::mutex               g_pool_mu;
 std::vector<StreamPool*> g_pools;
@@ -767,7 +789,7 @@ StreamPool* get_pool()
       return nullptr;
     }
   }
-  if (srsran_amd::ring_event_create(&p->fork) != hipSuccess) {
+  if (srsran_amd::ring_event_create(&p->fork) != hipSuccess || srsran_amd::ring_event_create(&p->large_done) != hipSuccess) {
     return nullptr;
   }
   for (auto& m : p->md) {
@@ -789,6 +811,30 @@ uint32_t gen_cut()
     return e ? (uint32_t)atoi(e) : 0u;
   }();
   return c;
+}
+
+// The 16-step part of a fused 16-sub-block class is cut once more at this K (SRSRAN_AMD_TDEC_MIDCUT, read once;
+// 0 = one launch): its sizes above run first with K = 6144's LDS a workgroup (two a CU, nothing else fits beside
+// them), its sizes up to the cut follow on the same stream with their own, smaller LDS figure -- room beside them
+// for the 8-step part's, the 8-sub-block class's and the generic class's workgroups.
+uint32_t tdec_midcut()
+{
+  static const uint32_t c = [] {
+    const char* e = getenv("SRSRAN_AMD_TDEC_MIDCUT");
+    return e ? (uint32_t)atoi(e) : 3072u;
+  }();
+  return c;
+}
+// With a mid cut, the other classes' launches wait for the large sizes to finish (SRSRAN_AMD_TDEC_GATE, read once;
+// default on): started at once they only take CUs the large workgroups would have used, since no large workgroup
+// leaves room beside it.
+bool tdec_gate()
+{
+  static const bool g = [] {
+    const char* e = getenv("SRSRAN_AMD_TDEC_GATE");
+    return e ? atoi(e) != 0 : true;
+  }();
+  return g;
 }
 
 // Rough serial-latency model used only to order launches (longest first).
@@ -855,8 +901,19 @@ int srsran_tdec_gpu_run_multi(uint32_t              nof_groups,
   // tdecs_w8_fused_max_k(): its sizes up to there run the 8-step-window build (fewer registers and
   // little LDS a workgroup: their workgroups can share SIMDs with the large sizes' ones) as their own
   // launch.
-  const int cls_nsb[5] = {16, 16, 8, 1, 1};  // launch entries: 16 (16-step), 16 (8-step part), 8, generic x 2
-  for (int ci = 0; ci < 5 && ret == SRSRAN_SUCCESS; ci++) {
+  // launch entries: 16 (16-step, K > mid cut), 16 (16-step, cut < K <= mid cut), 16 (8-step part), 8, generic x 2
+  const int      cls_nsb[6] = {16, 16, 16, 8, 1, 1};
+  const int      cls_st[6]  = {0, 0, 1, 2, 3, 3};  // pool stream of each entry (both 16-step parts: one stream)
+  const uint32_t midcut     = tdec_midcut();
+  bool           gated      = false;
+  bool           mid_run    = false;  // entry 1 launched: the 16-step part was cut at midcut
+  for (int ci = 0; ci < 6 && ret == SRSRAN_SUCCESS; ci++) {
+    if (ci == 1 && hipEventRecord(p->large_done, p->s[0]) != hipSuccess) {  // behind the large sizes (entry 0)
+      ret = SRSRAN_ERROR;
+      break;
+    }
+    // with the 16-step part cut at midcut, the other classes start when its large sizes are done, beside the mid part
+    gated = ci >= 2 && mid_run && tdec_gate() && multi_mode() != 2;
     std::vector<uint32_t> gs;
     uint32_t              cls_cb = 0;  // blocks of the whole class (decides the kernel)
     for (uint32_t i = 0; i < nof_groups; i++) {
@@ -874,23 +931,30 @@ int srsran_tdec_gpu_run_multi(uint32_t              nof_groups,
                      : cls_nsb[ci] == 16            ? tdec16_choice(cls_cb)
                                                     : (cls_cb >= tdec8s_min_cb() ? 2 : 0);
     const uint32_t cut = std::max(tdecs_w8_max_k(), tdecs_w8_fused_max_k());
-    if (cls_nsb[ci] == 16 && kind == 2) {  // entry 0: K above the cut; entry 1: the rest
-      const bool part8 = ci == 1;
-      gs.erase(std::remove_if(gs.begin(), gs.end(), [&](uint32_t g) { return (cfg[g]->proto.K <= cut) != part8; }),
+    if (cls_nsb[ci] == 16 && kind == 2) {  // entry 0: K above the mid cut; entry 1: up to it; entry 2: up to the cut
+      const uint32_t lo = ci == 0 ? std::max(cut, midcut) : ci == 1 ? cut : 0;
+      const uint32_t hi = ci == 0 ? UINT32_MAX : ci == 1 ? std::max(cut, midcut) : cut;
+      gs.erase(std::remove_if(gs.begin(), gs.end(),
+                              [&](uint32_t g) { return !(cfg[g]->proto.K > lo && cfg[g]->proto.K <= hi); }),
                gs.end());
-    } else if (ci == 1) {
-      gs.clear();  // no 8-step part outside the single-lane class
-    } else if (ci >= 3 && kind == 0 && gen_cut() > 0) {  // generic quad: K above the cut, then the rest
-      const bool small = ci == 4;
+    } else if (ci == 1 || ci == 2) {
+      gs.clear();  // no 16-step mid part / 8-step part outside the single-lane class
+    } else if (ci >= 4 && kind == 0 && gen_cut() > 0) {  // generic quad: K above the cut, then the rest
+      const bool small = ci == 5;
       gs.erase(std::remove_if(gs.begin(), gs.end(), [&](uint32_t g) { return (cfg[g]->proto.K <= gen_cut()) != small; }),
                gs.end());
-    } else if (ci == 4) {
+    } else if (ci == 5) {
       gs.clear();  // one generic launch
     }
     if (gs.empty()) {
       continue;
     }
-    hipStream_t st = p->s[multi_mode() == 2 ? 0 : std::min(ci, kPoolStreams - 1)];  // both generic parts: one stream
+    mid_run        = mid_run || ci == 1;
+    hipStream_t st = p->s[multi_mode() == 2 ? 0 : cls_st[ci]];
+    if (gated && st != p->s[0] && hipStreamWaitEvent(st, p->large_done, 0) != hipSuccess) {
+      ret = SRSRAN_ERROR;
+      break;
+    }
     if (gs.size() == 1) {
       const uint32_t g = gs[0];
       ret = enqueue(cfg[g], d_input[g], in_stride[g], layout_sb, d_output[g], nof_cb[g], 0, n_end, nullptr, st);
@@ -991,35 +1055,6 @@ int srsran_tdec_gpu_debug_set_stamps(void* d_buf)
 #endif
 
 // ---- 8-bit LLR decoders (turbodecoder.c:455-483, 551-577) ----
-namespace {
-// grow-only scratch of the 8-bit batch entry point (the β of a MAP pass / the widened int16 input), one per
-// (device, stream): calls on one stream are ordered, so its scratch is reused without allocation in steady state
-struct Scratch8 {
-  void*  p   = nullptr;
-  size_t cap = 0;
-};
-std::mutex                                              g_s8_mu;
-std::map<std::pair<int, hipStream_t>, Scratch8>         g_s8;
-void* scratch8(hipStream_t s, size_t bytes)
-{
-  std::lock_guard<std::mutex> lk(g_s8_mu);
-  Scratch8&                   c = g_s8[{srsran_amd::cur_dev(), s}];
-  if (bytes > c.cap) {
-    if (c.p) {
-      hipStreamSynchronize(s);  // the previous call on this stream may still read it
-      hipFree(c.p);
-      c.p   = nullptr;
-      c.cap = 0;
-    }
-    const size_t cap = bytes + bytes / 4;
-    if (hipMalloc(&c.p, cap) != hipSuccess) {
-      return nullptr;
-    }
-    c.cap = cap;
-  }
-  return c.p;
-}
-}  // namespace
 
 // AUTO: K > 2048 on the AVX2 8-bit window decoder (32 sub-blocks), 800 < K <= 2048 on the SSE 8-bit
 // window decoder (16), smaller K on the 16-bit decoders after widening the input (convert_8_to_16);
@@ -1059,17 +1094,18 @@ int srsran_tdec_gpu_run_batch_8bit(uint32_t      long_cb,
     a.n_end     = n_end;
     a.out       = d_output;
     qpp_coeffs((uint32_t)idx, &a.f1, &a.f2);
-    void* beta = scratch8(s, tdec8bit_beta_bytes((int)nsb8, long_cb, nof_cb));
-    if (!beta) {
+    Scratch8 beta(s, tdec8bit_beta_bytes((int)nsb8, long_cb, nof_cb));
+    if (!beta.p) {
       return SRSRAN_ERROR;
     }
-    a.beta           = (uint2*)beta;
+    a.beta           = (uint2*)beta.p;
     const hipError_t e = tdec8bit_launch((int)nsb8, a, s);
     tdec_set_last_kernel(nsb8 == 32 ? "tdec8bit_kernel<32>" : "tdec8bit_kernel<16>");
     return e == hipSuccess ? SRSRAN_SUCCESS : SRSRAN_ERROR;
   }
   // 16-bit decoder on the widened input
-  short* wide = (short*)scratch8(s, (size_t)nof_cb * len * sizeof(short));
+  Scratch8 wbuf(s, (size_t)nof_cb * len * sizeof(short));
+  short*   wide = (short*)wbuf.p;
   if (!wide) {
     return SRSRAN_ERROR;
   }

@@ -175,12 +175,12 @@ def pack_pusch(c, dci, cfg=None):
 
 
 class Regs:
-    def __init__(self, c, phich_mi=None):
+    def __init__(self, c, phich_mi=None, sf1_6=False):
         self.q = srsran_regs_t()
-        if phich_mi is None:
+        if phich_mi is None and not sf1_6:
             ret = lib().srsran_regs_init(ctypes.byref(self.q), c)
         else:
-            ret = lib().srsran_regs_init_opts(ctypes.byref(self.q), c, phich_mi, False)
+            ret = lib().srsran_regs_init_opts(ctypes.byref(self.q), c, 1 if phich_mi is None else phich_mi, bool(sf1_6))
         if ret != 0:
             raise RuntimeError("srsran_regs_init failed")
 

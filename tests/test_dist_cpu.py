@@ -77,7 +77,7 @@ def _run_bench(args, env_extra=None, timeout=180):
                           capture_output=True, text=True, timeout=timeout)
 
 
-@pytest.mark.parametrize("n", [2, 3])
+@pytest.mark.parametrize("n", [2, 3, 8])
 def test_bench_gpus_spawns_ranks(n):
     """bench.py --gpus N with no launcher starts N rank processes itself (children, before any GPU call):
     one JSON line from rank 0 with n_gpus N, LOCAL_RANK r -> device cuda:r, disjoint cells and seeds"""
@@ -90,6 +90,25 @@ def test_bench_gpus_spawns_ranks(n):
     assert [r["rank"] for r in d["ranks"]] == list(range(n))
     assert [r["device"] for r in d["ranks"]] == [f"cuda:{r}" for r in range(n)]
     assert len({r["cell_id"] for r in d["ranks"]}) == n and len({r["seed"] for r in d["ranks"]}) == n
+
+
+def test_bench_torchrun_launcher_8_ranks():
+    """the driver's own N = 8 launch line (torch.distributed.run, one process per GPU, rendezvous on
+    127.0.0.1), as a dry run: 8 ranks, LOCAL_RANK r -> cuda:r, disjoint carriers (the C4 layout)"""
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+                        os.path.join(ROOT, "bench.py"), "--gpus", "8", "--dry-run"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1
+    d = lines[0]
+    assert d["n_gpus"] == 8
+    assert sorted(r["rank"] for r in d["ranks"]) == list(range(8))
+    assert all(r["device"] == f"cuda:{r['local_rank']}" for r in d["ranks"])
+    assert len({r["cell_id"] for r in d["ranks"]}) == 8 and len({r["seed"] for r in d["ranks"]}) == 8
 
 
 def test_bench_world_size_disagreeing_with_gpus_fails():

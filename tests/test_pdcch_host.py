@@ -72,6 +72,36 @@ def test_regs_tables_phich_mi_match_reference(nprb, nports, cid, ng, mi):
         r.free()
 
 
+EXT_CELLS = [(100, 2, 1, 2), (50, 1, 7, 3), (25, 2, 300, 1), (6, 1, 2, 3), (75, 2, 101, 2), (15, 4, 44, 3),
+             (100, 4, 503, 0), (6, 2, 11, 2)]
+
+
+@needs_ref
+@pytest.mark.parametrize("sf1_6", [False, True])
+@pytest.mark.parametrize("mi", [0, 1, 2])
+@pytest.mark.parametrize("nprb,nports,cid,ng", EXT_CELLS)
+def test_regs_tables_extended_phich_match_reference(nprb, nports, cid, ng, mi, sf1_6):
+    """extended PHICH duration (regs.c:249-350): the PHICH spread over symbols 0-2, or over symbols 0-1 in MBSFN /
+    TDD subframe 1 and 6 tables (srsran_regs_init_opts(..., mbsfn_or_sf1_6_tdd), ue_dl.c:59-64, 198) -- the REGs left
+    to the PCFICH / PDCCH equal the reference's for every CFI"""
+    ref = P.Ref()
+    pc, pd = ref.regs_tables(nprb, nports, cid, 1, ng, phich_mi=mi, sf1_6=sf1_6)
+    c = PD.cell(nprb, nports, cid, 1, ng)
+    r = PD.Regs(c, phich_mi=mi, sf1_6=sf1_6)
+    try:
+        assert np.array_equal(r.pcfich_re(), pc)
+        for cfi in (1, 2, 3):
+            assert np.array_equal(r.pdcch_re(cfi), pd[cfi - 1]), cfi
+    finally:
+        r.free()
+    if mi and ng:  # the tables differ from the normal-duration ones: the PHICH left symbol 0 for symbols 1-2
+        rn = PD.Regs(PD.cell(nprb, nports, cid, 0, ng), phich_mi=mi)
+        try:
+            assert not np.array_equal(rn.pdcch_re(3), pd[2])
+        finally:
+            rn.free()
+
+
 @needs_ref
 def test_viterbi_and_rm_conv_restatement_match_reference():
     ref, ora = P.Ref(), P.Ora()

@@ -134,11 +134,13 @@ def timed_region(step, steps, warmup, world, dist, sync, device):
     return elapsed
 
 
-def step_spread(step, n, torch, stream, host_phases=None):
+def step_spread(step, n, torch, stream, host_phases=None, stream_of=None):
     """Per-step spread of `n` back-to-back steps (after the timed region, the same launch pattern): the
-    GPU time between HIP events recorded on the launch stream after every step, the host time of every
-    enqueue call, and -- when `host_phases` (srsran_4g_amd.prof) is given -- the library's host phases of
-    the slowest call.  -> {"gpu_ms": min/median/max, "host_ms": min/median/max, ...}"""
+    GPU time between HIP events recorded after every step, the host time of every enqueue call, and -- when
+    `host_phases` (srsran_4g_amd.prof) is given -- the library's host phases of the slowest call.  With
+    `stream_of` (the stream the step just enqueued went to: several workers taking the steps in turn) each event
+    goes on that step's stream, so an interval is the time between two consecutive steps' completions -- what the
+    timed region's rate is made of.  -> {"gpu_ms": min/median/max, "host_ms": min/median/max, ...}"""
     import gc
 
     torch.cuda.synchronize()
@@ -146,11 +148,11 @@ def step_spread(step, n, torch, stream, host_phases=None):
     host, phases = [], []
     gc_was = gc.isenabled()
     gc.disable()
-    # two untimed steps first, so that the first timed interval starts with work queued behind it (an
-    # event recorded on an idle stream would time the host's first enqueue as GPU time)
-    step()
-    step()
-    ev[0].record(stream)
+    # untimed steps first (two, or one a worker), so that the first timed interval starts with work queued behind
+    # it (an event recorded on an idle stream would time the host's first enqueue as GPU time)
+    for _ in range(2 if stream_of is None else 3):
+        step()
+    ev[0].record(stream if stream_of is None else stream_of())
     for i in range(n):
         if host_phases is not None:
             host_phases.host_enable(True)
@@ -160,7 +162,7 @@ def step_spread(step, n, torch, stream, host_phases=None):
         if host_phases is not None:
             phases.append({k: round(us, 1) for k, (us, _) in host_phases.host_read().items()})
             host_phases.host_enable(False)
-        ev[i + 1].record(stream)
+        ev[i + 1].record(stream if stream_of is None else stream_of())
     torch.cuda.synchronize()
     if gc_was:
         gc.enable()
@@ -279,6 +281,8 @@ def cpu_worker(args):
     from synth import synth as SY
     from srsran_4g_amd.tdec import CB_SIZES
 
+    if args.workload == "pdsch":
+        return pdsch_cpu_worker(args)
     Ks = list(CB_SIZES) if args.workload == "all188" else [6144]
     rng = np.random.default_rng(args.cpu_worker)
     pool = {K: SY.natural_to_sb(K, SY.make_llrs(K, 4.0, rng, args.pool)[1]) for K in Ks}
@@ -317,7 +321,7 @@ def bench_8bit(torch, device, n, K=6144, iters=8, reps=3):
             "mbps": round(n * K / (ms * 1e-3) / 1e6, 1)}
 
 
-def c1_cpu_leg(data, iters, budget_s, gpu_mbps):
+def c1_cpu_leg(data, iters, budget_s, gpu_mbps, gpu_mbps_16=None):
     """BASELINE configs[0] (C1: K = 6144 code blocks, 8 half-its) on the host, beside the GPU's K = 6144 rate of the
     same line: the reference decoder (oracle/_ref) on one thread for ~budget_s/2 s over the pool blocks, and one
     process per core of this job's share for ~budget_s/2 s (cpu_worker, K = 6144 only).  The whole host is not this
@@ -335,6 +339,13 @@ def c1_cpu_leg(data, iters, budget_s, gpu_mbps):
             dec.tdec_run(6144, x, True, iters)
             bits += 6144
     one = bits / (time.perf_counter() - t0) / 1e6
+    bits16 = 0  # 16 half-iterations on one thread, a quarter of the budget
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < budget_s / 4:
+        for x in pool:
+            dec.tdec_run(6144, x, True, 16)
+            bits16 += 6144
+    one16 = bits16 / (time.perf_counter() - t0) / 1e6
     n = cpu_threads()
     env = dict(os.environ, OMP_NUM_THREADS="1")
     procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--cpu-worker", str(2000 + i),
@@ -360,8 +371,13 @@ def c1_cpu_leg(data, iters, budget_s, gpu_mbps):
         "gpu_over_1thread": round(gpu_mbps / one, 1) if gpu_mbps else None,
         "gpu_over_share": round(gpu_mbps / share, 2) if gpu_mbps and share else None,
         "gpu_over_host_estimate": round(gpu_mbps / host, 2) if gpu_mbps else None,
+        "gpu_k6144_mbps_16_half_its": gpu_mbps_16,
+        "cpu_1thread_mbps_16_half_its": round(one16, 2),
+        "gpu_over_1thread_16_half_its": round(gpu_mbps_16 / one16, 1) if gpu_mbps_16 else None,
+        "gpu_over_share_16_half_its_est": round(gpu_mbps_16 / (share * one16 / one), 2) if gpu_mbps_16 and share else None,
         "sample": f"1 thread {half:.0f} s over {len(pool)} pool blocks; {ok} processes x {half:.0f} s over their own "
-                  f"pools; host = 1 thread x nproc (linear extrapolation, SMT threads counted: an upper bound)",
+                  f"pools; host = 1 thread x nproc (linear extrapolation, SMT threads counted: an upper bound); "
+                  f"16 half-its: 1 thread {budget_s / 4:.0f} s, the share scaled by the 1-thread 16 / 8 ratio",
     }
 
 
@@ -1053,6 +1069,9 @@ def run_pdsch(args, torch, dist, world, rank, device, steps=None, warmup=None, c
         if w[0].gpu_decode_batch(w[1], d_x.data_ptr(), w[3].data_ptr(), w[4].data_ptr(), 0.0, w[5].cuda_stream) != 2 * nsf:
             raise RuntimeError("srsran_ue_dl_gpu_decode_batch failed")
 
+    def last_worker_stream():  # the stream of the step step_workers() enqueued last
+        return workers[(turn[0] - 1) % nwork][5]
+
     # every worker's first batch (its ring, scratch and descriptor growth) before the timed region, whatever
     # the warm-up count: a worker first used inside the timed steps would time its allocations
     for w in workers[1:]:
@@ -1111,8 +1130,10 @@ def run_pdsch(args, torch, dist, world, rank, device, steps=None, warmup=None, c
     torch.cuda.synchronize()
     h2d_s = (time.perf_counter() - t1) / n_h2d
     del d_xs[1]
-    # per-step spread of the same back-to-back launches (events between steps; host phases per call)
-    spread = step_spread(step, max(steps, 10), torch, stream, prof)
+    # per-step spread of the timed configuration (the workers taking the steps in turn: events on each step's own
+    # stream, intervals between consecutive completions; host phases per call), and of worker 0 alone
+    spread = step_spread(step_workers, max(steps, 10), torch, stream, prof, stream_of=last_worker_stream)
+    spread_one = step_spread(step, max(steps, 10), torch, stream) if nwork > 1 else None
     # host cost of one step (the API builds descriptors and launches asynchronously), each call on an idle GPU:
     # in a free-running loop the host runs ahead until a ring slot's wait blocks it, and the call time is then
     # the GPU's step time, not the host's work
@@ -1208,6 +1229,7 @@ def run_pdsch(args, torch, dist, world, rank, device, steps=None, warmup=None, c
         },
         "stages": per_stage,
         "step_spread": spread,
+        "step_spread_one_worker": spread_one,
         "host_enqueue_ms_per_step": round(host_ms, 4),
         "host_enqueue_note": "median of per-call times, each call issued on an idle GPU (no ring waits)",
         "host_phases_us_per_call": host_phases,
@@ -1238,10 +1260,10 @@ def run_pdsch(args, torch, dist, world, rank, device, steps=None, warmup=None, c
     return result
 
 
-def pdsch_cpu_baseline(pool, args, budget_s):
-    """The reference's compiled PDSCH pieces (oracle/_ref: predecoding, demod_soft, sequence, DL-SCH
-    decode_tb over rm_turbo/turbodecoder/crc) with the oracle's C channel estimator and numpy's FFT
-    (FFTW is not in the image) on one host thread, over the same subframes."""
+def _pdsch_cpu_chain():
+    """(decode one subframe -> None, kind): the reference's compiled PDSCH pieces (oracle/_ref: predecoding,
+    demod_soft, sequence, DL-SCH decode_tb over rm_turbo/turbodecoder/crc) with the oracle's C channel estimator and
+    numpy's FFT (FFTW is not in the image)"""
     import pdsch_chain as PC
     from oracle import Oracle, Reference, ref_available
 
@@ -1255,21 +1277,75 @@ def pdsch_cpu_baseline(pool, args, budget_s):
             return getattr(ora, name)
 
     h = Hybrid()
+
+    def decode(tti, x, iters, cell_id=1):
+        g, ce, st = PC.fft_estimate(ora, x, 100, cell_id, 2, tti)
+        PC.pdsch_decode(h, g, ce, st["noise"], 100, cell_id, 2, tti, 1, 0x1234, [C3_TBS, C3_TBS], [C3_QM, C3_QM],
+                        [0, 0], max_iterations=iters)
+    return decode, "reference" if ref is not None else "port"
+
+
+def pdsch_cpu_worker(args):
+    """--cpu-worker SEED --workload pdsch: one host process of the PDSCH CPU leg's job-share run (no torch, no GPU):
+    its own C3 subframes (4, synthetic, --snr / --nfft of the line), decoded in turn for --cpu-seconds."""
+    from synth import synth as SY
+
+    rng = np.random.default_rng(args.cpu_worker)
+    pool = []
+    for i in range(4):
+        pls = [rng.integers(0, 256, C3_TBS // 8, dtype=np.uint8) for _ in range(2)]
+        x, _ = SY.pdsch_subframe(100, 1, 2, i + 1, 1, 0x1234, C3_TBS, C3_QM, 0, pls, snr_db=args.snr, rng=rng,
+                                 N=args.nfft)
+        pool.append((i + 1, x))
+    decode, _ = _pdsch_cpu_chain()
+    n = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < args.cpu_seconds:
+        tti, x = pool[n % len(pool)]
+        decode(tti, x, args.iters)
+        n += 1
+    print(json.dumps({"subframes": n, "dt": time.perf_counter() - t0}), flush=True)
+
+
+def pdsch_cpu_baseline(pool, args, budget_s):
+    """The PDSCH chain on the host, over the same subframes (_pdsch_cpu_chain): one thread for budget_s, then one
+    process per core of this job's share (the tdec leg's 16 on the GPU box, cpu_threads()) for budget_s, each over its
+    own subframes -- the same core share as the turbo decoder's cpu_share figure."""
+    import subprocess
+
+    decode, kind = _pdsch_cpu_chain()
     n = 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < budget_s:
         tti, x, nre, _ = pool[n % len(pool)]
-        g, ce, st = PC.fft_estimate(ora, x, 100, 1, 2, tti)
-        PC.pdsch_decode(h, g, ce, st["noise"], 100, 1, 2, tti, 1, 0x1234, [C3_TBS, C3_TBS], [C3_QM, C3_QM], [0, 0],
-                        max_iterations=args.iters)
+        decode(tti, x, args.iters)
         n += 1
     dt = time.perf_counter() - t0
-    return {"value": round(n * 2 * C3_TBS / dt / 1e6, 3), "unit": "Mbps", "cores": 1,
-            "kind": "reference" if ref is not None else "port",
+    nproc = cpu_threads()
+    env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--cpu-worker", str(3000 + i),
+                               "--cpu-seconds", str(budget_s), "--iters", str(args.iters), "--workload", "pdsch",
+                               "--snr", str(args.snr), "--nfft", str(args.nfft)],
+                              stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, env=env, cwd=ROOT)
+             for i in range(nproc)]
+    agg, agg_dt, ok = 0, 0.0, 0
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=budget_s + 180)
+            r = json.loads(out.decode().strip().splitlines()[-1])
+            agg, agg_dt, ok = agg + r["subframes"], max(agg_dt, r["dt"]), ok + 1
+        except Exception:
+            p.kill()
+    share = agg / agg_dt if ok else None
+    return {"value": round(n * 2 * C3_TBS / dt / 1e6, 3), "unit": "Mbps", "cores": 1, "kind": kind,
             "subframes_per_s": round(n / dt, 2),
-            "sample": f"{n} C3 subframes, {dt:.1f} s on 1 thread: reference-compiled predecoding / demod / "
-                      f"descrambling / DL-SCH; oracle C channel estimator; numpy FFT (FFTW absent)"
-                      if ref is not None else f"{n} C3 subframes, {dt:.1f} s on 1 thread (oracle C port + numpy FFT)"}
+            "share_subframes_per_s": round(share, 2) if share else None, "share_processes": ok,
+            "share_mbps": round(share * 2 * C3_TBS / 1e6, 3) if share else None,
+            "cpu_model": cpu_model(),
+            "sample": f"{n} C3 subframes, {dt:.1f} s on 1 thread; then {ok} processes x {budget_s:.0f} s over their own "
+                      f"4 subframes: reference-compiled predecoding / demod / descrambling / DL-SCH; oracle C channel "
+                      f"estimator; numpy FFT (FFTW absent)" if kind == "reference"
+                      else f"{n} C3 subframes, {dt:.1f} s on 1 thread (oracle C port + numpy FFT); {ok} processes"}
 
 
 def run_ldpc(args, torch, dist, world, rank, device):
@@ -1810,12 +1886,24 @@ def main():
         if k:
             ms = np.mean([e0.elapsed_time(e1) for _, e0, e1 in k])
             result["k6144_mbps"] = round(args.batch * 6144 / (ms * 1e-3) / 1e6, 1)
+        if 6144 in data:  # C1 at 16 half-iterations too: BASELINE's "8 iter" may mean full iterations
+            d_in, d_out, _ = data[6144]
+            ms16 = []
+            for _ in range(3):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                tdec.gpu_run_batch(6144, d_in.data_ptr(), d_in.shape[1], True, d_out.data_ptr(), args.batch, 16, sp)
+                e1.record(stream)
+                torch.cuda.synchronize()
+                ms16.append(e0.elapsed_time(e1))
+            result["k6144_mbps_16_half_its"] = round(args.batch * 6144 / (min(ms16) * 1e-3) / 1e6, 1)
         result["tdec_8bit"] = bench_8bit(torch, device, args.batch)
 
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         result["cpu_baseline"] = cpu_baseline(Ks, data, args.iters, args.cpu_seconds, args.workload)
         if args.workload == "all188" and 6144 in data:
-            result["c1_cpu"] = c1_cpu_leg(data, args.iters, min(args.cpu_seconds, 8.0), result.get("k6144_mbps"))
+            result["c1_cpu"] = c1_cpu_leg(data, args.iters, min(args.cpu_seconds, 8.0), result.get("k6144_mbps"),
+                                          result.get("k6144_mbps_16_half_its"))
     elif rank == 0:
         result["cpu_baseline"] = None
 

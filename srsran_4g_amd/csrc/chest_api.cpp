@@ -58,7 +58,8 @@ struct ChestGpu {
   float       filter[8];
   uint32_t    filter_len = 0;
   float2*     pss     = nullptr;  // the cell's 62 PSS values (noise PSS)
-  float*      noise   = nullptr;  // device q->noise_estimate [4][4]: host-sync upload / batch state
+  float*      noise   = nullptr;  // device q->noise_estimate [4][4]: host-sync upload / batch state; [16]: the batch
+                                  // path's kept CFO (the last subframe with its own estimate)
   float*      sync    = nullptr;  // correct_sync_error sums [4 rx][4 port][10]
   float2*     tab     = nullptr;  // sync correction phasor table (12 * max_prb)
   float       sync_err[SRSRAN_MAX_PORTS][SRSRAN_MAX_PORTS] = {};  // q->sync_err (chest_dl.c:776)
@@ -333,7 +334,7 @@ int srsran_chest_dl_init(srsran_chest_dl_t* q, uint32_t max_prb, uint32_t nof_rx
       hipMalloc((void**)&g->ce, SRSRAN_MAX_PORTS * nof_rx_antennas * sf * sizeof(float2)) != hipSuccess ||
       hipMalloc((void**)&g->stats, SRSRAN_MAX_PORTS * SRSRAN_MAX_PORTS * 8 * sizeof(float)) != hipSuccess ||
       hipMalloc((void**)&g->pss, 62 * sizeof(float2)) != hipSuccess ||
-      hipMalloc((void**)&g->noise, 16 * sizeof(float)) != hipSuccess || hipMemset(g->noise, 0, 16 * sizeof(float)) ||
+      hipMalloc((void**)&g->noise, 17 * sizeof(float)) != hipSuccess || hipMemset(g->noise, 0, 17 * sizeof(float)) ||
       hipMalloc((void**)&g->sync, 16 * 10 * sizeof(float)) != hipSuccess ||
       hipMalloc((void**)&g->tab, 12 * (size_t)max_prb * sizeof(float2)) != hipSuccess ||
       hipMalloc((void**)&g->d_mbsfn, 10 * 18 * (size_t)max_prb * sizeof(float2)) != hipSuccess) {
@@ -806,7 +807,8 @@ extern "C" int srsran_chest_dl_gpu_estimate(srsran_chest_dl_t* q,
   if (d_res) {
     ChestGpu* g = (ChestGpu*)q->gpu;
     chest_finalize_launch(g->stats, q->cell.nof_ports, q->nof_rx_antennas, q->cell.nof_prb,
-                          (float)srsran_symbol_sz(q->cell.nof_prb), SRSRAN_CP_NSYMB(q->cell.cp), d_res, 1, s);
+                          (float)srsran_symbol_sz(q->cell.nof_prb), SRSRAN_CP_NSYMB(q->cell.cp), d_res, 1, s,
+                          g->noise + 16);
   }
   return hipGetLastError() == hipSuccess ? SRSRAN_SUCCESS : SRSRAN_ERROR;
 }
@@ -930,14 +932,14 @@ int estimate_batch(srsran_chest_dl_t*           q,
     // reduction needed device-scope fences, whose L2 write-backs cost more than the launch: r04p stamps)
     return chest_launch(a, s, nsf) == hipSuccess &&
                    chest_finalize_launch(g->bstats, q->cell.nof_ports, q->nof_rx_antennas, q->cell.nof_prb, sz, a.nsymb,
-                                         d_res, nsf, s) == hipSuccess
+                                         d_res, nsf, s, g->noise + 16) == hipSuccess
                ? SRSRAN_SUCCESS
                : SRSRAN_ERROR;
   }
   if (!a.filter_auto) {  // PSS / EMPTY with a fixed filter: the kept estimates carried in one pass after the launch
     if (chest_launch(a, s, nsf) != hipSuccess ||
         chest_finalize_kept_launch(g->bstats, q->cell.nof_ports, q->nof_rx_antennas, q->cell.nof_prb, sz, a.nsymb,
-                                   g->noise, d_res, nsf, s) != hipSuccess) {
+                                   g->noise, d_res, nsf, s, g->noise + 16) != hipSuccess) {
       return SRSRAN_ERROR;
     }
     return SRSRAN_SUCCESS;
@@ -967,7 +969,7 @@ int estimate_batch(srsran_chest_dl_t*           q,
     }
     if (chest_launch(sa, s, n) != hipSuccess ||
         chest_finalize_kept_launch(sa.stats, q->cell.nof_ports, q->nof_rx_antennas, q->cell.nof_prb, sz, a.nsymb,
-                                   g->noise, d_res + 4 * start, n, s) != hipSuccess) {
+                                   g->noise, d_res + 4 * start, n, s, g->noise + 16) != hipSuccess) {
       return SRSRAN_ERROR;
     }
     start += n;

@@ -72,14 +72,17 @@ hipError_t chest_mbsfn_launch(const ChestArgs& a, hipStream_t stream);
 // diagnostic build (-DCHEST_STAMPS) only: phase clock stamps of every chest_kernel workgroup into d_buf
 hipError_t chest_set_stamps(void* d_buf);
 // device-side reduction of the per-(rx, port) stats of nsf subframes into out[b][4] =
-// {noise_estimate, rsrp, rssi, cfo} (fill_res, chest_dl.c:962-986)
+// {noise_estimate, rsrp, rssi, cfo} (fill_res, chest_dl.c:962-986); a subframe without 4 CRS symbols (TDD special)
+// keeps the CFO before it, from *cfo_state (device, may be null: 0) across calls, which is updated
 hipError_t chest_finalize_launch(const float* stats, uint32_t np, uint32_t nrx, uint32_t nof_prb, float symbol_sz,
-                                 uint32_t nsymb, float* out, uint32_t nsf, hipStream_t stream);
+                                 uint32_t nsymb, float* out, uint32_t nsf, hipStream_t stream,
+                                 float* cfo_state = nullptr);
 // the same for PSS / EMPTY noise over a batch, in subframe order: a subframe without a new estimate takes the
 // (rx, port) value left by the subframes before it, starting from state[rx * 4 + port], which holds the last
 // values afterwards (q->noise_estimate across calls)
 hipError_t chest_finalize_kept_launch(float* stats, uint32_t np, uint32_t nrx, uint32_t nof_prb, float symbol_sz,
-                                      uint32_t nsymb, float* state, float* out, uint32_t nsf, hipStream_t stream);
+                                      uint32_t nsymb, float* state, float* out, uint32_t nsf, hipStream_t stream,
+                                      float* cfo_state = nullptr);
 
 // correct_sync_error (chest_dl.c:750-804), device side of the host-synchronous path: per (rx, port) the LS
 // estimates' per-CRS-symbol phase sums sum(x[i] conj(x[i-1])) and their power sum -> out[(rx * 4 + port) * 10 ..]:

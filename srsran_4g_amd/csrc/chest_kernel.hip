@@ -213,10 +213,11 @@ __device__ uint32_t load_filter(const ChestArgs& a, float noise, float* filt)
 
 // fill_res (chest_dl.c:962-986) of one subframe from its per-(rx, port) stats st -> o[4]: every stat of the
 // subframe loaded first (one round trip, not one a loop step), then the reference's sums in its order
-__device__ void finalize_sf(const float* st, uint32_t np, uint32_t nrx, uint32_t nof_prb, float sz, float nsymb,
+__device__ bool finalize_sf(const float* st, uint32_t np, uint32_t nrx, uint32_t nof_prb, float sz, float nsymb,
                             float* o)
 {
   float v[4][4][5];  // [rx][port][noise, rsrp, rssi, cfo re, cfo im]
+  bool  has_cfo = false;  // the (rx, port) the CFO comes from had 4 CRS symbols (not a TDD special subframe)
 #pragma unroll
   for (uint32_t rx = 0; rx < 4; rx++) {
 #pragma unroll
@@ -266,8 +267,9 @@ __device__ void finalize_sf(const float* st, uint32_t np, uint32_t nrx, uint32_t
 #pragma unroll
     for (uint32_t p = 0; p < 2; p++) {
       if (rx == nrx - 1 && p == min(np, 2u) - 1) {
-        cre = v[rx][p][3];
-        cim = v[rx][p][4];
+        cre     = v[rx][p][3];
+        cim     = v[rx][p][4];
+        has_cfo = st[(rx * np + p) * 8 + 6] != 0.0f;
       }
     }
   }
@@ -279,6 +281,7 @@ __device__ void finalize_sf(const float* st, uint32_t np, uint32_t nrx, uint32_t
   o[1]     = best;
   o[2]     = rssi / (float)nrx;
   o[3]     = cfo;
+  return has_cfo && nrx * np > 0;
 }
 
 
@@ -549,6 +552,7 @@ __global__ __launch_bounds__(CH_THREADS) void chest_kernel(ChestArgs a)
     s[3]     = cre;
     s[4]     = cim;
     s[5]     = noise_sf ? 1.0f : 0.0f;
+    s[6]     = nsym == 4 ? 1.0f : 0.0f;  // CFO phase sums present (4 CRS symbols)
   }
   CH_STAMP(6);
   copy_jobs_finish(a.jobs, cr, bid, nblk);
@@ -659,15 +663,46 @@ hipError_t chest_launch(const ChestArgs& a, hipStream_t stream, uint32_t nsf)
   return hipGetLastError();
 }
 
-// one thread per subframe
-__global__ void chest_finalize_kernel(const float* stats, uint32_t np, uint32_t nrx, uint32_t nof_prb, float sz,
-                                      float nsymb, float* out, uint32_t nsf)
+// One workgroup, a thread per subframe (in turns of 256).  A subframe without a CFO estimate of its own (a TDD special
+// subframe: fewer than 4 CRS symbols) reports the last estimate before it -- of this batch, or *cfo_state, the last of
+// the batches before -- as the host-synchronous path keeps q->cfo (chest_api.cpp); *cfo_state holds the batch's last
+// value afterwards.
+constexpr uint32_t FIN_THREADS = 256;
+__global__ __launch_bounds__(FIN_THREADS) void chest_finalize_kernel(const float* stats, uint32_t np, uint32_t nrx,
+                                                                     uint32_t nof_prb, float sz, float nsymb, float* out,
+                                                                     uint32_t nsf, float* cfo_state)
 {
-  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= nsf) {
-    return;
+  __shared__ int last_est[FIN_THREADS];  // per turn: the highest subframe with its own estimate, per thread
+  __shared__ float carry;
+  if (threadIdx.x == 0) {
+    carry = cfo_state ? *cfo_state : 0.f;
   }
-  finalize_sf(stats + b * CHEST_STATS_PER_SF, np, nrx, nof_prb, sz, nsymb, out + 4 * b);
+  for (uint32_t base = 0; base < nsf; base += FIN_THREADS) {
+    const uint32_t b   = base + threadIdx.x;
+    const bool     own = b < nsf && finalize_sf(stats + b * CHEST_STATS_PER_SF, np, nrx, nof_prb, sz, nsymb, out + 4 * b);
+    last_est[threadIdx.x] = own ? (int)threadIdx.x : -1;
+    __syncthreads();  // carry (first turn) and the turn's outputs
+    for (uint32_t off = 1; off < FIN_THREADS; off <<= 1) {  // inclusive prefix max: the last estimate at or before
+      const int v = threadIdx.x >= off ? last_est[threadIdx.x - off] : -1;
+      __syncthreads();
+      last_est[threadIdx.x] = max(last_est[threadIdx.x], v);
+      __syncthreads();
+    }
+    if (b < nsf && !own) {
+      const int j = last_est[threadIdx.x];
+      out[4 * b + 3] = j >= 0 ? out[4 * (base + j) + 3] : carry;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const uint32_t n = min(nsf - base, FIN_THREADS);
+      const int      j = last_est[n - 1];
+      carry            = j >= 0 ? out[4 * (base + j) + 3] : carry;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0 && cfo_state) {
+    *cfo_state = carry;
+  }
 }
 
 // PSS / EMPTY over a batch: one thread walks the subframes in order, carrying each (rx, port)'s kept estimate
@@ -692,13 +727,14 @@ __global__ void chest_keep_kernel(float* stats, uint32_t np, uint32_t nrx, float
 }
 
 hipError_t chest_finalize_kept_launch(float* stats, uint32_t np, uint32_t nrx, uint32_t nof_prb, float symbol_sz,
-                                      uint32_t nsymb, float* state, float* out, uint32_t nsf, hipStream_t stream)
+                                      uint32_t nsymb, float* state, float* out, uint32_t nsf, hipStream_t stream,
+                                      float* cfo_state)
 {
   if (nsf == 0) {
     return hipSuccess;
   }
   hipLaunchKernelGGL(chest_keep_kernel, dim3(1), dim3(64), 0, stream, stats, np, nrx, state, nsf);
-  return chest_finalize_launch(stats, np, nrx, nof_prb, symbol_sz, nsymb, out, nsf, stream);
+  return chest_finalize_launch(stats, np, nrx, nof_prb, symbol_sz, nsymb, out, nsf, stream, cfo_state);
 }
 
 // correct_sync_error's device part: one workgroup per (port, rx) and subframe (blockIdx.y; batches: the subframe
@@ -860,14 +896,14 @@ hipError_t grid_rotate_launch(float2* grid, const float2* tab, uint32_t nre, uin
 }
 
 hipError_t chest_finalize_launch(const float* stats, uint32_t np, uint32_t nrx, uint32_t nof_prb, float symbol_sz,
-                                 uint32_t nsymb, float* out, uint32_t nsf, hipStream_t stream)
+                                 uint32_t nsymb, float* out, uint32_t nsf, hipStream_t stream, float* cfo_state)
 {
   StageScope timing_scope(ST_CHEST, stream);
   if (nsf == 0) {
     return hipSuccess;
   }
-  hipLaunchKernelGGL(chest_finalize_kernel, dim3((nsf + 63) / 64), dim3(64), 0, stream, stats, np, nrx, nof_prb,
-                     symbol_sz, (float)nsymb, out, nsf);
+  hipLaunchKernelGGL(chest_finalize_kernel, dim3(1), dim3(FIN_THREADS), 0, stream, stats, np, nrx, nof_prb, symbol_sz,
+                     (float)nsymb, out, nsf, cfo_state);
   return hipGetLastError();
 }
 

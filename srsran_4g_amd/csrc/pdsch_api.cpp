@@ -368,18 +368,23 @@ int enqueue_llr(srsran_pdsch_t* q, uint32_t nsf, const srsran_pdsch_gpu_sf_t* sf
   bool        fused = !q->llr_is_8bit && fenv && fenv[0] == '1';
   std::vector<int>      sf_mod(nsf, -1);
   std::vector<uint32_t> sf_cw(nsf * 2, 0);  // [sf][layer] -> index into cws
+  std::vector<uint8_t>  sf_layers(nsf, 0);  // [sf] bit l: layer l's codeword recorded (once)
   for (size_t i = 0; i < cws.size() && fused; i++) {
     const Cw& c = cws[i];
-    fused       = (sf_mod[c.sf] < 0 || sf_mod[c.sf] == c.mod) && c.cw < 2;
+    fused       = (sf_mod[c.sf] < 0 || sf_mod[c.sf] == c.mod) && c.cw < 2 && !(sf_layers[c.sf] >> c.cw & 1);
     if (fused) {
       sf_mod[c.sf]           = c.mod;
       sf_cw[c.sf * 2 + c.cw] = (uint32_t)i;
+      sf_layers[c.sf] |= (uint8_t)(1u << c.cw);
     }
   }
+  // every layer the fused kernel writes must have its own codeword (a disabled TB or two TBs on one codeword index
+  // would leave a slot pointing at another codeword's buffer): bit 0 for PORT0, bits 0 and 1 for SM / CDD
   for (uint32_t b = 0; b < nsf && fused; b++) {
     const srsran_pdsch_grant_t& gr = sfs[b].cfg->grant;
     fused = sf_mod[b] >= 0 && !sfs[b].cfg->meas_evm_en && pa[b].interleave == 0 &&
-            (pa[b].scheme == 0 ? gr.nof_tb == 1 : (pa[b].scheme == 2 || pa[b].scheme == 3) && gr.nof_tb == 2);
+            (pa[b].scheme == 0 ? gr.nof_tb == 1 && sf_layers[b] == 1u
+                               : (pa[b].scheme == 2 || pa[b].scheme == 3) && gr.nof_tb == 2 && sf_layers[b] == 3u);
   }
   std::vector<uint32_t> order_p(nsf), order_l(fused ? nsf : cws.size()), pos_of(nsf);
   for (uint32_t i = 0; i < nsf; i++) {

@@ -51,11 +51,14 @@ struct UeDlGpu {
   srsran_dci_msg_t      pending_ul[SRSRAN_MAX_DCI_MSG];
   uint32_t              nof_pending_ul = 0;
   // PHICH m_i of the PDCCH's REG tables (ue_dl.c:263-273): `regs` has m_i = 1 (FDD), regs_mi the
-  // tables of m_i = 0 and 2 for srsran_ue_dl_set_mi_manual
-  srsran_regs_t regs_mi[2]{};
-  bool          mi_auto   = true;
-  uint32_t      mi_manual = 1;
-  uint32_t      mi_set    = 1;  // m_i of the tables the PDCCH object holds
+  // tables of m_i = 0 and 2 for srsran_ue_dl_set_mi_manual; a TDD cell with the extended PHICH duration also has
+  // regs_ext, the tables of m_i = 1, 0, 2 whose PHICH keeps to two symbols (subframes 1 and 6, ue_dl.c:59-64, 198)
+  srsran_regs_t        regs_mi[2]{};
+  srsran_regs_t        regs_ext[3]{};
+  bool                 ext_tables = false;
+  bool                 mi_auto    = true;
+  uint32_t             mi_manual  = 1;
+  const srsran_regs_t* regs_set   = nullptr;  // the tables the PDCCH object holds
 };
 
 // 36.213 Table 6.9-1: PHICH m_i per TDD uplink-downlink configuration and subframe (ue_dl.c:50-57)
@@ -72,9 +75,14 @@ void select_mi(UeDlGpu* g, const srsran_cell_t& cell, const srsran_dl_sf_cfg_t* 
                                ? 1u
                                : kMiTdd[sf->tdd_config.sf_config][sf->tti % 10];
   const uint32_t mi      = g->mi_auto ? auto_mi : g->mi_manual;
-  if (mi != g->mi_set) {
-    srsran_pdcch_set_regs(&g->pdcch, mi == 1 ? &g->regs : &g->regs_mi[mi == 0 ? 0 : 1]);
-    g->mi_set = mi;
+  // MI_IDX: + 3 (the two-symbol PHICH tables) for a TDD cell with the extended duration in subframes 1 and 6; the
+  // manual choice never adds it (ue_dl.c:308-311)
+  const bool           ext = g->mi_auto && g->ext_tables && (sf->tti % 10 == 1 || sf->tti % 10 == 6);
+  const uint32_t       i   = mi == 1 ? 0 : mi == 0 ? 1 : 2;  // mi_reg_idx_inv
+  srsran_regs_t* const t   = ext ? &g->regs_ext[i] : i == 0 ? &g->regs : &g->regs_mi[i - 1];
+  if (t != g->regs_set) {
+    srsran_pdcch_set_regs(&g->pdcch, t);
+    g->regs_set = t;
   }
 }
 
@@ -199,6 +207,9 @@ void srsran_ue_dl_free(srsran_ue_dl_t* q)
     srsran_regs_free(&g->regs);
     srsran_regs_free(&g->regs_mi[0]);
     srsran_regs_free(&g->regs_mi[1]);
+    for (auto& r : g->regs_ext) {
+      srsran_regs_free(&r);
+    }
     srsran_amd::handoff_free(g->ho);
     delete g;
   }
@@ -242,18 +253,26 @@ int srsran_ue_dl_set_cell(srsran_ue_dl_t* q, srsran_cell_t cell)
   UeDlGpu* g = (UeDlGpu*)q->gpu;
   q->cell    = cell;
   g->cap     = 0;  // buffer shapes depend on the cell
-  // control channels: 1, 2 or 4 ports, normal CP and PHICH duration (others: PDSCH only, CFI from the caller)
+  // control channels: 1, 2 or 4 ports, normal or extended PHICH duration (others: PDSCH only, CFI from the caller);
+  // the REG tables of ue_dl.c:190-203 (SRSRAN_MI_NOF_REGS: 1 FDD, 6 TDD -- the m_i = 0 / 2 ones kept for FDD too,
+  // srsran_ue_dl_set_mi_manual; the two-symbol PHICH ones only where MI_IDX can select them)
   srsran_regs_free(&g->regs);
   srsran_regs_free(&g->regs_mi[0]);
   srsran_regs_free(&g->regs_mi[1]);
-  g->ctrl_cell = g->ctrl_init && (cell.nof_ports == 1 || cell.nof_ports == 2 || cell.nof_ports == 4) &&
-                 cell.phich_length == SRSRAN_PHICH_NORM &&
+  for (auto& r : g->regs_ext) {
+    srsran_regs_free(&r);
+  }
+  g->ext_tables = cell.frame_type == SRSRAN_TDD && cell.phich_length == SRSRAN_PHICH_EXT;
+  g->ctrl_cell  = g->ctrl_init && (cell.nof_ports == 1 || cell.nof_ports == 2 || cell.nof_ports == 4) &&
                  srsran_regs_init(&g->regs, cell) == SRSRAN_SUCCESS &&
                  srsran_regs_init_opts(&g->regs_mi[0], cell, 0, false) == SRSRAN_SUCCESS &&
                  srsran_regs_init_opts(&g->regs_mi[1], cell, 2, false) == SRSRAN_SUCCESS &&
+                 (!g->ext_tables || (srsran_regs_init_opts(&g->regs_ext[0], cell, 1, true) == SRSRAN_SUCCESS &&
+                                     srsran_regs_init_opts(&g->regs_ext[1], cell, 0, true) == SRSRAN_SUCCESS &&
+                                     srsran_regs_init_opts(&g->regs_ext[2], cell, 2, true) == SRSRAN_SUCCESS)) &&
                  srsran_pcfich_set_cell(&g->pcfich, &g->regs, cell) == SRSRAN_SUCCESS &&
                  srsran_pdcch_set_cell(&g->pdcch, &g->regs, cell) == SRSRAN_SUCCESS;
-  g->mi_set = 1;
+  g->regs_set = &g->regs;
   g->nof_pending_ul = 0;  // ue_dl.c:189
   hipDeviceSynchronize();
   hipHostFree(g->h_sf);
@@ -361,8 +380,11 @@ int srsran_ue_dl_gpu_decode_batch(srsran_ue_dl_t*              q,
   UeDlGpu*    g    = (UeDlGpu*)q->gpu;
   hipStream_t s    = (hipStream_t)stream;
   const bool  full = cfg->chest_cfg.estimator_alg == SRSRAN_ESTIMATOR_ALG_INTERPOLATE;  // every symbol its own row
-  for (uint32_t b = 1; b < nof_sf; b++) {  // one TDD frame configuration per batch (the estimator takes one)
-    if (memcmp(&sfs[b].tdd_config, &sfs[0].tdd_config, sizeof(srsran_tdd_config_t)) != 0) {
+  // one TDD frame configuration per batch (the estimator takes one); compared field by field (the struct has
+  // padding) and only in a TDD cell (an FDD caller may leave the field unset)
+  for (uint32_t b = 1; q->cell.frame_type == SRSRAN_TDD && b < nof_sf; b++) {
+    const srsran_tdd_config_t &t = sfs[b].tdd_config, &t0 = sfs[0].tdd_config;
+    if (t.configured != t0.configured || t.sf_config != t0.sf_config || t.ss_config != t0.ss_config) {
       fprintf(stderr, "[srsran_ue_dl] batch: subframes with different TDD configurations\n");
       return SRSRAN_ERROR_INVALID_INPUTS;
     }

@@ -199,12 +199,13 @@ def symbol_size_is_standard():
     return bool(lib().srsran_symbol_size_is_standard())
 
 
-def cell(nof_prb=100, nof_ports=2, cell_id=1, phich_res=2, cp=0, tdd=False):
-    """FDD (tdd=True: TDD), normal CP (cp=1: extended), normal PHICH duration, Ng = 1 (phich_res 2) as the
-    reference's test cells"""
+def cell(nof_prb=100, nof_ports=2, cell_id=1, phich_res=2, cp=0, tdd=False, phich_len=0):
+    """FDD (tdd=True: TDD), normal CP (cp=1: extended), normal PHICH duration (phich_len=1: extended), Ng = 1
+    (phich_res 2) as the reference's test cells"""
     c = srsran_cell_t()
     c.nof_prb, c.nof_ports, c.id, c.cp = nof_prb, nof_ports, cell_id, cp
     c.phich_resources = phich_res
+    c.phich_length = phich_len
     c.frame_type = 1 if tdd else 0
     return c
 

@@ -45,7 +45,23 @@ def test_chest_matches_oracle(U, ora, nof_prb, cell_id, nports, nrx, sf):
     assert np.abs(ce - ceo).max() < 2e-5 * scale
     assert res.noise_estimate == pytest.approx(st["noise"], rel=1e-4)
     assert res.rsrp == pytest.approx(st["rsrp"], rel=1e-4)
-    assert res.cfo == pytest.approx(st["cfo"], rel=1e-3, abs=1e-6)
+    assert res.cfo == pytest.approx(st["cfo"], rel=1e-4, abs=1e-6)  # abs: the static channel's CFO is ~0
+    ch.free()
+
+
+@pytest.mark.parametrize("nof_prb,cell_id,nports,nrx,sf,rot", [(100, 1, 2, 2, 1, 0.013), (50, 7, 1, 1, 6, -0.021),
+                                                                (25, 301, 2, 1, 9, 0.004), (6, 2, 4, 2, 3, 0.03)])
+def test_chest_cfo_estimate_matches_oracle(U, ora, nof_prb, cell_id, nports, nrx, sf, rot):
+    """chest_estimate_cfo (chest_dl.c:618-641) on a subframe with a real frequency offset (a phase advance of `rot`
+    rad a symbol): the GPU estimate within 1e-4 (relative) of the oracle's -- north_star's soft-value tolerance"""
+    rng = np.random.default_rng(nof_prb + cell_id + 7)
+    Y, H, _ = make_subframe(ora, rng, nof_prb=nof_prb, cell_id=cell_id, nports=nports, nrx=nrx, sf_idx=sf, snr_db=25)
+    Y = (Y.reshape(nrx, 14, -1) * np.exp(1j * rot * np.arange(14))[None, :, None]).astype(np.complex64).reshape(nrx, -1)
+    ch = U.ChestDl(U.cell(nof_prb, nports, cell_id), nrx)
+    _, res = ch.estimate(Y, sf, U.srsue_chest_cfg())
+    _, st = ora.chest_dl(Y, nof_prb, cell_id, nports, sf, U.lib().srsran_symbol_sz(nof_prb))
+    assert abs(st["cfo"]) > 1e-4
+    assert res.cfo == pytest.approx(st["cfo"], rel=1e-4)
     ch.free()
 
 

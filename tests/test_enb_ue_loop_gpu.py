@@ -112,8 +112,9 @@ def test_enb_to_ue_through_pdcch(env, case):
 
 
 @pytest.mark.parametrize("case", [(50, 2, 2, "1c_si", 5, 1), (100, 2, 2, "1a_dist_gap2", 3, 2), (25, 1, 1, "1c_si", 7, 2),
-                                  (15, 1, 1, "1a_dist", 2, 3)],
-                         ids=["50prb_1c_si_rnti", "100prb_1a_distributed_gap2", "25prb_1c_si_rnti", "15prb_1a_distributed"])
+                                  (15, 1, 1, "1a_dist", 2, 3), (50, 2, 2, "1a_dist", 4, 2)],
+                         ids=["50prb_1c_si_rnti", "100prb_1a_distributed_gap2", "25prb_1c_si_rnti", "15prb_1a_distributed",
+                              "50prb_1a_distributed"])
 def test_enb_to_ue_distributed_vrb(env, case):
     """system information and distributed-VRB grants (ra_dl.c:225-316, 383-391; dci.c:952-1023): the eNB
     sends a format 1C DCI with the SI-RNTI in the common search space (TBS of 36.213 Table 7.1.7.2.3-1, QPSK), or a
@@ -152,8 +153,12 @@ def test_enb_to_ue_distributed_vrb(env, case):
     # the largest allocation from VRB 1 that the reference maps inside the cell (with N_gap,2 its N~_VRB is twice
     # 36.211's, ra_dl.c:257-260, so long ones fall outside and are refused)
     riv_n = nvrb if si else nprb  # 1C: the RIV counts N_RB^step units of N_VRB^DL (36.213 7.1.6.3)
+    # and, for a C-RNTI 1A at N_RB >= 50, whose RIV fits the field the N_gap bit leaves (riv_nbits - 1 bits: the
+    # reference packer truncates a larger one, dci.c:751-755)
+    riv_max = 1 << (OP.riv_nbits(nprb) - (1 if not si and nprb >= 50 else 0))
     L = max(n for n in range(1, max(2, nvrb // 2 + 1))
-            if OP.type2_prbs(nprb, U.lib().srsran_ra_type2_to_riv(n, 1, riv_n), True, ngap1, fmt1c=si))
+            if OP.type2_prbs(nprb, U.lib().srsran_ra_type2_to_riv(n, 1, riv_n), True, ngap1, fmt1c=si)
+            and (si or U.lib().srsran_ra_type2_to_riv(n, 1, riv_n) < riv_max))
     riv = U.lib().srsran_ra_type2_to_riv(L, 1, riv_n)
     d.raw[0], d.raw[1], d.raw[2], d.raw[3] = riv, 0, 0 if ngap1 else 1, 1  # distributed
     d.tb[0].mcs_idx, d.tb[0].rv, d.tb[0].ndi, d.tb[0].cw_idx = (9 if si else 7), 0, True, 0
@@ -167,6 +172,17 @@ def test_enb_to_ue_distributed_vrb(env, case):
     assert r == 0 and grant.nof_tb == 1 and grant.nof_prb == len(want[0])
     for s in range(2):
         assert [n for n in range(nprb) if grant.prb_idx[s][n]] == sorted(want[s])
+    hops = any(grant.prb_idx[0][n] != grant.prb_idx[1][n] for n in range(nprb))
+    if (nprb, kind) == (50, "1c_si"):
+        # 50 PRB, format 1C: allocations come in N_RB^step = 4 VRBs from multiples of 4, and with N_gap,1 = 27 the
+        # interleaver (36.211 6.2.3.2, 4 columns) maps every such group to the same PRBs in both slots -- no 1C grant of
+        # this cell hops: checked over every RIV (type2_prbs of ra_dl.c:234-260); the other cases hop
+        assert not hops
+        assert not any((lambda w: w and sorted(w[0]) != sorted(w[1]))(
+            OP.type2_prbs(nprb, U.lib().srsran_ra_type2_to_riv(n, s0, riv_n), True, ngap1, fmt1c=True))
+            for n in range(1, nvrb + 1) for s0 in range(nvrb))
+    else:
+        assert hops  # a distributed grant: slot 1's PRBs differ from slot 0's
     grant.tb[0].rv = 0  # 1C carries no RV (36.321 5.3.1: the UE derives it from the SFN)
     qm = [{1: 2, 2: 4, 3: 6}[grant.tb[0].mod]]
     cfg = U.pdsch_cfg(nprb, grant.nof_re, [grant.tb[0].tbs], qm, rnti=rnti, scheme="port0" if P == 1 else "diversity",

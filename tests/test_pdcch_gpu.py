@@ -327,3 +327,49 @@ def test_find_ul_dci_format0_and_mi(mods):
         ue.set_mi(None)
     finally:
         ue.free()
+
+
+@pytest.mark.parametrize("tti", [1, 6, 0, 5])
+def test_tdd_extended_phich_control_region(mods, tti):
+    """TDD cell with the extended PHICH duration: in subframes 1 / 6 srsran_ue_dl_find_dl_dci searches the REG tables
+    whose PHICH keeps to two symbols (MI_IDX + 3, ue_dl.c:59-64; srsran_regs_init_opts(..., true), regs.c:329-340),
+    in the others the three-symbol ones of that subframe's m_i (uplink-downlink configuration 0: m_i = 2 in
+    subframes 0 / 5, 1 in 1 / 6).  The control region comes from the reference's own pcfich.c / pdcch.c on the
+    reference's tables of the same options; a DCI is found from time samples.  The manual m_i choice never takes the
+    two-symbol tables (ue_dl.c:308-311), so in subframes 1 / 6 it does not find the DCI."""
+    import torch  # noqa: F401
+
+    PD, U = mods
+    from synth import synth as S
+
+    tdd, cid, rnti, tbs = (0, 7), 17, 0x4321, 2216
+    sf16 = tti % 10 in (1, 6)
+    mi = [2, 1, 0, 0, 0, 2, 1, 0, 0, 0][tti % 10]
+    cfi = 2 if sf16 else 3  # the extended duration needs the PHICH's symbols in the control region
+    rng = np.random.default_rng(200 + tti)
+    c = PD.cell(100, 2, cid, 1)
+    c.frame_type = 1
+    bits = P.dci_pack_1a(100, PD.dci_size(c, P.FORMAT1A), P.riv(10, 5, 100), 5, 1, 1, 0)  # flag 1A, localized
+    regs = PD.Regs(c, phich_mi=mi, sf1_6=sf16)
+    nof_cce = regs.q.pdcch_nregs[cfi - 1] // 9
+    regs.free()
+    L, ncce = [loc for loc in PD.ue_locations(nof_cce, tti % 10, rnti) if loc[0] == 2][0]
+    ctrl = P.Ref().ctrl_tx(100, 2, cid, tti, cfi, [(bits, L, ncce, rnti)], phich_len=1, phich_mi=mi, sf1_6=sf16)
+    pls = [rng.integers(0, 256, tbs // 8, dtype=np.uint8) for _ in range(2)]
+    x, _ = S.pdsch_subframe(100, cid, 2, tti, cfi, rnti, tbs, 2, 0, pls, snr_db=30.0, rng=rng, pcfich=False,
+                            ctrl=[ctrl[0], ctrl[1]], tdd=tdd)
+    U.use_standard_symbol_size(True)
+    ue = U.UeDl(U.cell(100, 2, cid, tdd=True, phich_len=1), 2, tdd=tdd)
+    try:
+        assert ue.fft_estimate(x, tti, 0) == 0 and ue.last_cfi == cfi
+        dcis = ue.find_dl_dci(tti, cfi, rnti, tm=1)
+        assert len(dcis) == 1
+        d = dcis[0]
+        assert (d.rnti, d.format, d.location.L, d.location.ncce) == (rnti, P.FORMAT1A, L, ncce)
+        if sf16:
+            ue.set_mi(mi)
+            assert ue.fft_estimate(x, tti, 0) == 0
+            assert all(x.location.ncce != ncce or x.rnti != rnti for x in ue.find_dl_dci(tti, cfi, rnti, tm=1))
+            ue.set_mi(None)
+    finally:
+        ue.free()

@@ -124,6 +124,55 @@ def test_chest_batch_special_subframes(U, ora):
     ch.free()
 
 
+def test_chest_batch_cfo_kept_in_special_subframes(U, ora):
+    """CFO estimation on (srsUE: cfo_estimate_enable, mask 1023) over a TDD frame whose special subframes carry 2 CRS
+    symbols: the reference's chest_estimate_cfo needs 4 (chest_dl.c:618-641), so the host-synchronous path keeps
+    q->cfo from the last full subframe (chest_api.cpp); the batch reports the same, subframe by subframe -- including
+    a special subframe first in a batch, which takes the last estimate of the batch before it"""
+    rng = np.random.default_rng(19)
+    nof_prb, nports, cell_id, nrx = 50, 2, 44, 2
+    tdd = (1, 9)
+    sfs = [i for i in range(10) if pdsch_np.tdd_type(1, i) != "U"]
+    Ys = []
+    for i in sfs:
+        Y = make_subframe(ora, rng, nof_prb=nof_prb, cell_id=cell_id, nports=nports, nrx=nrx, sf_idx=i)[0]
+        rot = np.exp(1j * (0.02 + 0.01 * i) * np.arange(14))[None, :, None]
+        Ys.append((Y.reshape(nrx, 14, -1) * rot).astype(np.complex64).reshape(Y.shape))
+    cfg = U.srsue_chest_cfg()
+    # host-synchronous reference, subframe by subframe
+    ch = U.ChestDl(U.cell(nof_prb, nports, cell_id, tdd=True), nrx)
+    host = []
+    for b, i in enumerate(sfs):
+        _, res = ch.estimate(Ys[b], i, cfg, tdd=tdd)
+        host.append(res.cfo)
+    ch.free()
+    assert len({round(h, 9) for h in host}) > 2  # distinct estimates per full subframe
+    # batch: the frame as two batches, the second starting at special subframe 6 (carried from the first batch)
+    ch = U.ChestDl(U.cell(nof_prb, nports, cell_id, tdd=True), nrx)
+    t = U.srsran_tdd_config_t()
+    t.sf_config, t.ss_config, t.configured = tdd[0], tdd[1], True
+    assert U.lib().srsran_chest_dl_gpu_set_tdd_config(ctypes.byref(ch.q), t) == 0
+    nre = 12 * nof_prb
+    f = U.lib().srsran_chest_dl_gpu_estimate_batch_cfg
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t,
+                  ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    cut = sfs.index(6)
+    got = []
+    for part in (range(0, cut), range(cut, len(sfs))):
+        idx = [sfs[b] for b in part]
+        d_grid = torch.from_numpy(np.stack([Ys[b] for b in part]).view(np.float32)).cuda()
+        d_ce = torch.zeros((len(idx), nports, nrx, nre, 2), dtype=torch.float32, device="cuda")
+        d_res = torch.zeros((len(idx), 4), dtype=torch.float32, device="cuda")
+        d_idx = torch.tensor(idx, dtype=torch.int32, device="cuda")
+        assert f(ctypes.byref(ch.q), ctypes.byref(cfg), d_idx.data_ptr(), len(idx), d_grid.data_ptr(), nrx * 14 * nre,
+                 d_ce.data_ptr(), nports * nrx * nre, 0, d_res.data_ptr(), None) == 0
+        torch.cuda.synchronize()
+        got += list(d_res.cpu().numpy()[:, 3])
+    ch.free()
+    for b, i in enumerate(sfs):
+        assert got[b] == pytest.approx(host[b], rel=1e-4, abs=1e-7), (i, got[b], host[b])
+
+
 def _tdd_frame(U, ora, rng, tdd, nof_prb, nports, cell_id, snr_db):
     """one frame of a TDD cell from synth/: (tti, samples, nre, nsl, tbs, payloads, oracle-chain result) per downlink
     or special subframe; TBS from 36.213 with a special subframe's 0.75 N_PRB and a code rate <= ~0.75"""

@@ -97,6 +97,29 @@ int  srsran_rm_turbo_rx_lut_(int16_t* input,
                              bool     enable_input_tdec);
 int  srsran_rm_turbo_rx_lut_8bit(int8_t* input, int8_t* output, uint32_t in_len, uint32_t cb_idx, uint32_t rv_idx);
 
+/* ---------------- turbo encoder and rate matching TX (turbocoder.h:45-59, rm_turbo.h:58-65) ----------------
+ * Host pointers, host-synchronous, executed by HIP kernels (enc_kernel.hip: the DL-SCH encoder's PCCC and a
+ * rate-matching read-out over the reference's interleaver tables).
+ * srsran_tcod_encode: long_cb unpacked input bits (SRSRAN_TX_NULL marks a filler bit) -> 3 long_cb + 12 unpacked
+ *   bits, x_k z_k z'_k then the tails, as turbocoder.c:77-185.
+ * srsran_rm_turbo_tx_lut: the packed systematic (K + 4 bits, the tails in the byte after K) and parity (2 (K + 4)
+ *   bits) streams of srsran_tcod_encode_lut; for rv_idx 0 the circular buffer is built into w_buff (3 K + 12 bits,
+ *   packed), otherwise read from it; out_len bits from k0 of rv_idx into output (packed) at bit w_offset
+ *   (rm_turbo.c:345-388). */
+#ifndef SRSRAN_TX_NULL
+#define SRSRAN_TX_NULL 100
+#endif
+typedef struct {
+  uint32_t max_long_cb;
+  uint8_t* temp;
+  void*    gpu; /* added: device buffers */
+} srsran_tcod_t;
+int  srsran_tcod_init(srsran_tcod_t* h, uint32_t max_long_cb);                            /* turbocoder.c:44-62 */
+void srsran_tcod_free(srsran_tcod_t* h);                                                   /* turbocoder.c:64-75 */
+int  srsran_tcod_encode(srsran_tcod_t* h, uint8_t* input, uint8_t* output, uint32_t long_cb); /* turbocoder.c:77-185 */
+int  srsran_rm_turbo_tx_lut(uint8_t* w_buff, uint8_t* systematic, uint8_t* parity, uint8_t* output, uint32_t cb_idx,
+                            uint32_t out_len, uint32_t w_offset, uint32_t rv_idx);      /* rm_turbo.c:345-388 */
+
 /* ---------------- HARQ soft buffer (softbuffer.h:41-95, softbuffer.c:36-178) ---------------- */
 typedef struct {
   uint32_t  max_cb;

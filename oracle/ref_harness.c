@@ -310,6 +310,32 @@ int ref_tcod_encode(uint32_t K, const uint8_t* bits, uint8_t* out)
   return srsran_tcod_encode(&tcod, (uint8_t*)bits, out, K);
 }
 
+/* The reference's LUT transmit path of one code block: srsran_tcod_encode_lut (turbocoder.c:188-... ; no CB CRC, not
+ * the last block: every one of the K / 8 input bytes encoded as given, the tail nibble written after them) when
+ * `encode`, then srsran_rm_turbo_tx_lut (rm_turbo.c:345-388) into w_buff / out.  sys: K / 8 + 1 bytes (in / out),
+ * parity: at least (2 K + 8) / 8 + 16 bytes (out). */
+int ref_tcod_rm_tx_lut(uint32_t cb_idx, uint8_t* sys, uint8_t* parity, uint8_t* w_buff, uint8_t* out, uint32_t out_len,
+                       uint32_t w_offset, uint32_t rv, int encode)
+{
+  static srsran_tcod_t tcod;
+  static srsran_crc_t  crc_tb;
+  static bool          ready = false;
+  if (!ready) {
+    if (srsran_tcod_init(&tcod, SRSRAN_TCOD_MAX_LEN_CB) || srsran_crc_init(&crc_tb, SRSRAN_LTE_CRC24A, 24)) {
+      return -1;
+    }
+    srsran_rm_turbo_gentables();
+    ready = true;
+  }
+  if (encode) {
+    srsran_crc_set_init(&crc_tb, 0);
+    if (srsran_tcod_encode_lut(&tcod, &crc_tb, NULL, sys, parity, cb_idx, false) < 0) {  /* 3 K + 12 on success */
+      return -1;
+    }
+  }
+  return srsran_rm_turbo_tx_lut(w_buff, sys, parity, out, cb_idx, out_len, w_offset, rv);
+}
+
 /* Reference rate de-matching + HARQ combining into an int16 soft buffer (rm_turbo.c:390-445). */
 int ref_rm_turbo_rx_lut(const int16_t* in, int16_t* softbuf, uint32_t in_len, uint32_t cb_idx, uint32_t rv_idx)
 {

@@ -20,6 +20,7 @@
 #include "srsran/phy/common/sequence.h"
 #include "srsran/phy/mimo/layermap.h"
 #include "srsran/phy/mimo/precoding.h"
+#include "srsran/phy/utils/vector.h"
 #include "srsran/phy/modem/mod.h"
 #include "srsran/phy/modem/modem_table.h"
 
@@ -38,21 +39,23 @@ static cf_t* cf_zalloc(size_t n)
  * (srsran_mod_t), scrambled with the codeword index cw_idx[c]; tx_scheme srsran_tx_scheme_t; nof_re
  * REs a port.  out: [nof_ports][nof_re] complex symbols (the q->symbols the reference maps to the REs).
  * Returns 0, or -1 on bad arguments. */
-int ref_pdsch_tx_symbols(uint32_t       ncw,
-                         const uint8_t* e,
-                         uint32_t       e_stride,
-                         const uint32_t* nbits,
-                         const uint32_t* mod,
-                         const uint32_t* cw_idx,
-                         uint16_t        rnti,
-                         uint32_t        sf_idx,
-                         uint32_t        cell_id,
-                         int             tx_scheme,
-                         uint32_t        nof_ports,
-                         uint32_t        nof_layers,
-                         uint32_t        pmi,
-                         uint32_t        nof_re,
-                         float*          out)
+/* scaling: srsran_pdsch_encode's rho_a (pdsch.c:1057-1071, apply_power_allocation, pdsch.c:485-521) */
+int ref_pdsch_tx_symbols_sc(uint32_t       ncw,
+                            const uint8_t* e,
+                            uint32_t       e_stride,
+                            const uint32_t* nbits,
+                            const uint32_t* mod,
+                            const uint32_t* cw_idx,
+                            uint16_t        rnti,
+                            uint32_t        sf_idx,
+                            uint32_t        cell_id,
+                            int             tx_scheme,
+                            uint32_t        nof_ports,
+                            uint32_t        nof_layers,
+                            uint32_t        pmi,
+                            uint32_t        nof_re,
+                            float           scaling,
+                            float*          out)
 {
   if (ncw == 0 || ncw > SRSRAN_MAX_CODEWORDS || nof_ports == 0 || nof_ports > SRSRAN_MAX_PORTS || nof_layers == 0 ||
       nof_layers > SRSRAN_MAX_LAYERS || nof_re == 0) {
@@ -100,7 +103,7 @@ int ref_pdsch_tx_symbols(uint32_t       ncw,
     srsran_mod_modulate_bytes(&tab, packed, d[cw_idx[c]], nbits[c]);
     srsran_modem_table_free(&tab);
   }
-  /* srsran_pdsch_encode (pdsch.c:1066-1112): layer mapping and precoding, scaling 1 (no power allocation) */
+  /* srsran_pdsch_encode (pdsch.c:1066-1125): layer mapping and precoding with `scaling` */
   if (nof_ports > 1) {
     int   nof_symbols;
     cf_t* x[SRSRAN_MAX_LAYERS] = {NULL};
@@ -117,12 +120,14 @@ int ref_pdsch_tx_symbols(uint32_t       ncw,
                                          (srsran_tx_scheme_t)tx_scheme);
     }
     const int codebook_idx = ncw == 1 ? (int)pmi : (int)pmi + 1;
-    if (srsran_precoding_type(x, y, (int)nof_layers, (int)nof_ports, codebook_idx, nof_symbols, 1.0f,
+    if (srsran_precoding_type(x, y, (int)nof_layers, (int)nof_ports, codebook_idx, nof_symbols, scaling,
                               (srsran_tx_scheme_t)tx_scheme) < 0) {
       goto out;
     }
-  } else {
+  } else if (scaling == 1.0f) {
     memcpy(y[0], d[0], nof_re * sizeof(cf_t));
+  } else {
+    srsran_vec_sc_prod_cfc(d[0], scaling, y[0], nof_re);
   }
   for (uint32_t p = 0; p < nof_ports; p++) {
     memcpy(out + (size_t)2 * p * nof_re, y[p], nof_re * sizeof(cf_t));
@@ -140,6 +145,15 @@ out:
   }
   free(packed);
   return ret;
+}
+
+/* the composition at scaling 1 (the batched transmitter's default, srsran_enb_dl_gpu_sf_t::pdsch_scaling unset) */
+int ref_pdsch_tx_symbols(uint32_t ncw, const uint8_t* e, uint32_t e_stride, const uint32_t* nbits, const uint32_t* mod,
+                         const uint32_t* cw_idx, uint16_t rnti, uint32_t sf_idx, uint32_t cell_id, int tx_scheme,
+                         uint32_t nof_ports, uint32_t nof_layers, uint32_t pmi, uint32_t nof_re, float* out)
+{
+  return ref_pdsch_tx_symbols_sc(ncw, e, e_stride, nbits, mod, cw_idx, rnti, sf_idx, cell_id, tx_scheme, nof_ports,
+                                 nof_layers, pmi, nof_re, 1.0f, out);
 }
 
 /* ---- PDSCH EVM (pdsch.c:698-713): the reference's own srsran_evm_run_s (modem/evm.h:175-212, static inline,

@@ -8,6 +8,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -404,9 +405,10 @@ int srsran_enb_dl_gpu_tx_batch(srsran_enb_dl_gpu_t*          q,
     memset(&it, 0, sizeof(it));
     it.nre       = nre;
     it.scheme    = scheme;
-    it.scaling   = 1.0f;
+    it.scaling   = s.pdsch_scaling > 0.0f ? s.pdsch_scaling : 1.0f;
     // scaling * M_SQRT1_2 (2 ports); scaling /= M_SQRT2 (4 ports, precoding.c:1962)
-    it.div_scale = scheme == 4 ? (float)(1.0f / 1.41421356237309504880) : (float)(1.0 * 0.70710678118654752440);
+    it.div_scale = scheme == 4 ? (float)(it.scaling / 1.41421356237309504880)
+                               : (float)((double)it.scaling * 0.70710678118654752440);
     uint32_t cw = 0;
     for (uint32_t t = 0; t < SRSRAN_MAX_CODEWORDS; t++) {
       const srsran_ra_tb_t& tb = gr.tb[t];
@@ -483,6 +485,297 @@ int srsran_enb_dl_gpu_tx_batch(srsran_enb_dl_gpu_t*          q,
   g->last_sf = nof_sf;
   const float sc = scale > 0.0f ? scale : 0.05f / sqrtf((float)cell.nof_prb);  // enb_dl_get_norm_factor
   return srsran_ofdm_tx_gpu(&g->ofdm, (const cf_t*)g->d_grid, d_samples, P, nof_sf, sc, st);
+}
+
+// ---------------- enb_dl.h: the reference's per-subframe object over the batched transmitter ----------------
+}  // extern "C"
+
+namespace {
+struct EnbDlRef {
+  srsran_enb_dl_gpu_t           tx{};
+  bool                          tx_ok = false;
+  hipStream_t                   stream = nullptr;
+  // the subframe being recorded (srsran_enb_dl_put_* until srsran_enb_dl_gen_signal)
+  bool                          base = false, pdsch = false;
+  std::vector<srsran_dci_msg_t> dci;
+  srsran_pdsch_cfg_t            cfg{};
+  uint8_t*                      d_data[SRSRAN_MAX_CODEWORDS] = {nullptr, nullptr};
+  size_t                        data_cap = 0;
+  cf_t*                         d_samples = nullptr;
+  size_t                        samples_cap = 0;
+  uint32_t                      max_prb = 0;
+};
+
+void enb_ref_release(EnbDlRef* g)
+{
+  if (g->tx_ok) {
+    srsran_enb_dl_gpu_free(&g->tx);
+    g->tx_ok = false;
+  }
+}
+}  // namespace
+
+extern "C" {
+
+int srsran_enb_dl_init(srsran_enb_dl_t* q, cf_t* out_buffer[SRSRAN_MAX_PORTS], uint32_t max_prb)
+{
+  if (!q || !out_buffer || max_prb < 6 || max_prb > SRSRAN_MAX_PRB) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  memset(q, 0, sizeof(*q));
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    fprintf(stderr, "[srsran_enb_dl] no HIP device\n");
+    return SRSRAN_ERROR;
+  }
+  EnbDlRef* g = new EnbDlRef();
+  g->max_prb  = max_prb;
+  q->gpu      = g;
+  const size_t nre = SRSRAN_SF_LEN_RE(max_prb, SRSRAN_CP_NORM);
+  for (int p = 0; p < SRSRAN_MAX_PORTS; p++) {
+    q->out_buffer[p] = out_buffer[p];
+    q->sf_symbols[p] = (cf_t*)calloc(nre, sizeof(cf_t));
+    if (!q->sf_symbols[p]) {
+      srsran_enb_dl_free(q);
+      return SRSRAN_ERROR;
+    }
+  }
+  if (hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking) != hipSuccess) {
+    srsran_enb_dl_free(q);
+    return SRSRAN_ERROR;
+  }
+  return SRSRAN_SUCCESS;
+}
+
+void srsran_enb_dl_free(srsran_enb_dl_t* q)
+{
+  if (!q) {
+    return;
+  }
+  EnbDlRef* g = (EnbDlRef*)q->gpu;
+  if (g) {
+    if (g->stream) {
+      hipStreamSynchronize(g->stream);
+      hipStreamDestroy(g->stream);
+    }
+    enb_ref_release(g);
+    for (auto& d : g->d_data) {
+      hipFree(d);
+    }
+    hipFree(g->d_samples);
+    delete g;
+  }
+  if (q->cell.nof_prb) {
+    srsran_regs_free(&q->regs);
+  }
+  for (int p = 0; p < SRSRAN_MAX_PORTS; p++) {
+    free(q->sf_symbols[p]);
+  }
+  memset(q, 0, sizeof(*q));
+}
+
+int srsran_enb_dl_set_cell(srsran_enb_dl_t* q, srsran_cell_t cell)
+{
+  if (!q || !q->gpu || cell.nof_prb < 6 || cell.nof_prb > ((EnbDlRef*)q->gpu)->max_prb) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  EnbDlRef* g = (EnbDlRef*)q->gpu;
+  if (q->cell.nof_prb) {
+    srsran_regs_free(&q->regs);
+  }
+  enb_ref_release(g);
+  if (srsran_enb_dl_gpu_init(&g->tx, cell) != SRSRAN_SUCCESS) {
+    memset(&q->cell, 0, sizeof(q->cell));
+    return SRSRAN_ERROR;
+  }
+  g->tx_ok = true;
+  q->cell  = cell;
+  if (srsran_regs_init(&q->regs, cell) != SRSRAN_SUCCESS) {
+    return SRSRAN_ERROR;
+  }
+  // the PDCCH object's host fields (srsran_pdcch_set_cell's, pdcch.c:143-185): its locations are all a caller reads
+  memset(&q->pdcch, 0, sizeof(q->pdcch));
+  q->pdcch.cell = cell;
+  q->pdcch.regs = &q->regs;
+  for (int c = 0; c < 3; c++) {
+    q->pdcch.nof_regs[c] = (q->regs.pdcch_nregs[c] / 9) * 9;
+    q->pdcch.nof_cce[c]  = q->pdcch.nof_regs[c] / 9;
+  }
+  q->pdcch.max_bits = q->pdcch.nof_regs[2] * 8;
+  for (uint32_t cfi = 1; cfi <= 3; cfi++) {  // enb_dl.c:226-230
+    q->nof_common_locations[cfi - 1] =
+        srsran_pdcch_common_locations(&q->pdcch, q->common_locations[cfi - 1], SRSRAN_MAX_CANDIDATES_COM, cfi);
+  }
+  return SRSRAN_SUCCESS;
+}
+
+bool srsran_enb_dl_location_is_common_ncce(srsran_enb_dl_t* q, const srsran_dci_location_t* loc)
+{
+  if (!q || !loc || q->dl_sf.cfi < 1 || q->dl_sf.cfi > 3) {
+    return false;
+  }
+  return srsran_location_find_location(q->common_locations[q->dl_sf.cfi - 1], q->nof_common_locations[q->dl_sf.cfi - 1],
+                                       loc);
+}
+
+void srsran_enb_dl_put_base(srsran_enb_dl_t* q, srsran_dl_sf_cfg_t* dl_sf)
+{
+  if (!q || !q->gpu || !dl_sf) {
+    return;
+  }
+  EnbDlRef* g = (EnbDlRef*)q->gpu;
+  q->dl_sf    = *dl_sf;
+  g->base     = true;  // clear_sf + sync + CRS + MIB + PCFICH (enb_dl.c:372-382), generated with the subframe
+  g->pdsch    = false;
+  g->dci.clear();
+}
+
+static int put_dci(srsran_enb_dl_t* q, const srsran_dci_msg_t& m)
+{
+  EnbDlRef* g = (EnbDlRef*)q->gpu;
+  if (q->dl_sf.cfi < 1 || q->dl_sf.cfi > 3 || m.location.L > 3 ||
+      m.location.ncce + (1u << m.location.L) > q->pdcch.nof_cce[q->dl_sf.cfi - 1]) {
+    fprintf(stderr, "[srsran_enb_dl] DCI location L=%u ncce=%u outside the control region of CFI %u\n",
+            m.location.L, m.location.ncce, q->dl_sf.cfi);
+    return SRSRAN_ERROR;  // srsran_pdcch_encode refuses it too (pdcch.c:626-631)
+  }
+  g->dci.push_back(m);
+  return SRSRAN_SUCCESS;
+}
+
+int srsran_enb_dl_put_pdcch_dl(srsran_enb_dl_t* q, srsran_dci_cfg_t* dci_cfg, srsran_dci_dl_t* dci_dl)
+{
+  if (!q || !q->gpu || !dci_dl) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  srsran_dci_msg_t m;
+  memset(&m, 0, sizeof(m));
+  if (srsran_dci_msg_pack_pdsch(&q->cell, &q->dl_sf, dci_cfg, dci_dl, &m)) {
+    fprintf(stderr, "[srsran_enb_dl] Error packing DL DCI\n");  // enb_dl.c:397-399: reported, then encoded
+  }
+  return put_dci(q, m);
+}
+
+int srsran_enb_dl_put_pdcch_ul(srsran_enb_dl_t* q, srsran_dci_cfg_t* dci_cfg, srsran_dci_ul_t* dci_ul)
+{
+  if (!q || !q->gpu || !dci_ul) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  srsran_dci_msg_t m;
+  memset(&m, 0, sizeof(m));
+  if (srsran_dci_msg_pack_pusch(&q->cell, &q->dl_sf, dci_cfg, dci_ul, &m)) {
+    fprintf(stderr, "[srsran_enb_dl] Error packing UL DCI\n");
+  }
+  return put_dci(q, m);
+}
+
+int srsran_enb_dl_put_pdsch(srsran_enb_dl_t* q, srsran_pdsch_cfg_t* pdsch, uint8_t* data[SRSRAN_MAX_CODEWORDS])
+{
+  if (!q || !q->gpu || !pdsch || !data) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  EnbDlRef* g = (EnbDlRef*)q->gpu;
+  size_t    need = 0;
+  for (uint32_t t = 0; t < SRSRAN_MAX_CODEWORDS; t++) {
+    if (pdsch->grant.tb[t].enabled) {
+      if (!data[t] || pdsch->grant.tb[t].tbs <= 0) {
+        return SRSRAN_ERROR_INVALID_INPUTS;
+      }
+      need = std::max(need, (size_t)pdsch->grant.tb[t].tbs / 8);
+    }
+  }
+  if (need > g->data_cap) {
+    hipStreamSynchronize(g->stream);
+    for (auto& d : g->d_data) {
+      hipFree(d);
+      d = nullptr;
+    }
+    g->data_cap = 0;
+    for (auto& d : g->d_data) {
+      if (hipMalloc((void**)&d, need + 64) != hipSuccess) {
+        return SRSRAN_ERROR;
+      }
+    }
+    g->data_cap = need;
+  }
+  hipStreamSynchronize(g->stream);  // the previous subframe's encoder is done with the payload buffers
+  for (uint32_t t = 0; t < SRSRAN_MAX_CODEWORDS; t++) {
+    if (pdsch->grant.tb[t].enabled &&
+        hipMemcpy(g->d_data[t], data[t], (size_t)pdsch->grant.tb[t].tbs / 8, hipMemcpyHostToDevice) != hipSuccess) {
+      return SRSRAN_ERROR;
+    }
+  }
+  g->cfg   = *pdsch;
+  g->pdsch = true;
+  return SRSRAN_SUCCESS;
+}
+
+void srsran_enb_dl_gen_signal(srsran_enb_dl_t* q)
+{
+  if (!q || !q->gpu || !q->cell.nof_prb) {
+    return;
+  }
+  EnbDlRef*      g  = (EnbDlRef*)q->gpu;
+  const uint32_t P  = q->cell.nof_ports;
+  const uint32_t N  = ((EnbDlGpu*)g->tx.gpu)->N, sf_len = ((EnbDlGpu*)g->tx.gpu)->sf_len;
+  const size_t   nre = SRSRAN_SF_LEN_RE(q->cell.nof_prb, q->cell.cp);
+  (void)N;
+  if (q->dl_sf.sf_type == SRSRAN_SF_MBSFN) {
+    fprintf(stderr, "[srsran_enb_dl] MBSFN subframes are not generated (SURVEY section 8f)\n");
+    return;
+  }
+  if (!g->base) {
+    fprintf(stderr, "[srsran_enb_dl] srsran_enb_dl_put_base was not called for this subframe\n");
+  }
+  const size_t bytes = (size_t)P * sf_len * sizeof(cf_t);
+  if (bytes > g->samples_cap) {
+    hipFree(g->d_samples);
+    g->d_samples   = nullptr;
+    g->samples_cap = 0;
+    if (hipMalloc((void**)&g->d_samples, bytes) != hipSuccess) {
+      fprintf(stderr, "[srsran_enb_dl] device allocation failed\n");
+      return;
+    }
+    g->samples_cap = bytes;
+  }
+  srsran_enb_dl_gpu_ctrl_t ctrl;
+  memset(&ctrl, 0, sizeof(ctrl));
+  ctrl.put_base = g->base ? 1u : 0u;
+  ctrl.nof_dci  = (uint32_t)g->dci.size();
+  ctrl.dci      = g->dci.empty() ? nullptr : g->dci.data();
+  srsran_enb_dl_gpu_sf_t sf;
+  memset(&sf, 0, sizeof(sf));
+  sf.tti  = q->dl_sf.tti;
+  sf.cfi  = q->dl_sf.cfi;
+  sf.cfg  = g->pdsch ? &g->cfg : nullptr;
+  sf.ctrl = &ctrl;
+  for (uint32_t t = 0; t < SRSRAN_MAX_CODEWORDS && g->pdsch; t++) {
+    sf.d_data[t] = g->cfg.grant.tb[t].enabled ? g->d_data[t] : nullptr;
+  }
+  if (g->pdsch) {  // srsran_pdsch_encode's rho_a (pdsch.c:492: 10^(p_a / 20), x sqrt 2 with more than one port)
+    sf.pdsch_scaling = (float)((double)powf(10.0f, g->cfg.p_a / 20.0f) * (P == 1 ? 1.0 : M_SQRT2));
+  }
+  int ret = srsran_enb_dl_gpu_tx_batch(&g->tx, 1, &sf, g->d_samples, 0.0f, g->stream);
+  for (uint32_t p = 0; p < P && ret == SRSRAN_SUCCESS; p++) {
+    if ((q->out_buffer[p] && hipMemcpyAsync(q->out_buffer[p], g->d_samples + (size_t)p * sf_len, sf_len * sizeof(cf_t),
+                                            hipMemcpyDeviceToHost, g->stream) != hipSuccess) ||
+        hipMemcpyAsync(q->sf_symbols[p], srsran_enb_dl_gpu_sf_symbols(&g->tx) + (size_t)p * nre, nre * sizeof(cf_t),
+                       hipMemcpyDeviceToHost, g->stream) != hipSuccess) {
+      ret = SRSRAN_ERROR;
+    }
+  }
+  if (ret != SRSRAN_SUCCESS || hipStreamSynchronize(g->stream) != hipSuccess) {
+    fprintf(stderr, "[srsran_enb_dl] Error generating the subframe\n");
+  }
+  g->base  = false;
+  g->pdsch = false;
+  g->dci.clear();
+}
+
+float srsran_enb_dl_get_maximum_signal_power_dBfs(uint32_t nof_prb)
+{
+  // srsran_convert_amplitude_to_dB(0.05 / sqrt(N_RB)) + srsran_convert_power_to_dB(N_RB x 12) + 3 (enb_dl.c:691-695)
+  return 20.0f * log10f(0.05f / sqrtf((float)nof_prb)) + 10.0f * log10f((float)nof_prb * SRSRAN_NRE) + 3.0f;
 }
 
 const cf_t* srsran_enb_dl_gpu_sf_symbols(srsran_enb_dl_gpu_t* q)

@@ -34,4 +34,21 @@ hipError_t enc_cb_launch(const EncCb* d_cbs, uint32_t ncb, hipStream_t stream);
 // unpacked -> packed e bits, per TB; max_bytes = largest ceil(nof_e_bits / 8)
 hipError_t enc_pack_launch(const EncTb* d_tbs, uint32_t ntb, uint32_t max_bytes, hipStream_t stream);
 
+constexpr uint8_t kTxNull = 100;  // SRSRAN_TX_NULL (turbocoder.h:40-42): a filler bit
+
+// srsran_tcod_encode of one code block: K unpacked bits (device) -> 3 K + 12 unpacked bits (device)
+hipError_t tcod_launch(const uint8_t* d_in, uint8_t* d_out, uint32_t K, uint32_t f1, uint32_t f2, hipStream_t stream);
+
+// srsran_rm_turbo_tx_lut of one code block (device buffers; tables from tx_api.cpp)
+struct RmTxLut {
+  const uint8_t*  sys;     // packed systematic stream, K + 4 bits (rv 0)
+  const uint8_t*  par;     // packed parity streams, 2 (K + 4) bits (rv 0)
+  const uint16_t* tsys;    // w bit i <- sys bit tsys[i], i < K + 4
+  const uint16_t* tpar;    // w bit K + 4 + i <- par bit tpar[i], i < 2 (K + 4)
+  uint8_t*        w_buff;  // the circular buffer, 3 K + 12 bits packed (written for rv 0, read otherwise)
+  uint8_t*        output;  // packed output
+  uint32_t        K, rv, r_ptr, out_len, w_offset, zero_tail;
+};
+hipError_t rm_tx_lut_launch(const RmTxLut& a, hipStream_t stream);
+
 }  // namespace srsran_amd

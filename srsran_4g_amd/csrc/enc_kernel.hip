@@ -116,13 +116,84 @@ __device__ __forceinline__ uint32_t rsc_step(uint32_t& s, uint32_t u)
   return p;
 }
 
+// The PCCC of one code block (turbocoder.c:77-185) by a 128-thread workgroup: wave w runs constituent encoder w
+// (w = 1 on the QPP-interleaved bits), its 64 lanes on 64 chunks of the block chained through the zero-input
+// transition; c = the K information bits (LDS, 0 / 1), coded = 3 K + 12 bits in srsran_tcod_encode's order
+// (x_k, z_k, z'_k, then the two encoders' tail pairs).  Every thread of the workgroup calls it.
+struct PcccLds {
+  uint8_t e_end[2][64], s_start[2][64], T[2][8];
+};
+__device__ __forceinline__ void pccc_encode(const uint8_t* c, uint32_t K, uint32_t f1, uint32_t f2, uint8_t* coded, PcccLds& sh)
+{
+  const uint32_t tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+
+  // pass 1: every chunk from the zero state; the zero-input transition of a whole chunk
+  const uint32_t L = (K + 63) / 64, k0 = lane * L, k1 = min(k0 + L, K);
+  // QPP pi(k) = (f1 k + f2 k^2) mod K stepped incrementally: pi(k+1) = pi(k) + g(k),
+  // g(k+1) = g(k) + 2 f2 (mod K)
+  const uint32_t pi0 = k0 < K ? (uint32_t)(((uint64_t)f1 * k0 + (uint64_t)f2 * k0 * k0) % K) : 0u;
+  const uint32_t g0  = k0 < K ? (uint32_t)(((uint64_t)f1 + (uint64_t)f2 * (2 * (uint64_t)k0 + 1)) % K) : 0u;
+  const uint32_t d2  = (uint32_t)((2 * (uint64_t)f2) % K);
+  auto           adv = [&](uint32_t& p, uint32_t& g) {
+    p += g;
+    p -= p >= K ? K : 0u;
+    g += d2;
+    g -= g >= K ? K : 0u;
+  };
+  uint32_t s = 0, p = pi0, g = g0;
+  for (uint32_t k = k0; k < k1; k++) {
+    rsc_step(s, w ? c[p] : c[k]);
+    adv(p, g);
+  }
+  sh.e_end[w][lane] = (uint8_t)s;
+  if (lane < 8) {
+    uint32_t t = lane;
+    for (uint32_t k = 0; k < L; k++) {
+      rsc_step(t, 0);
+    }
+    sh.T[w][lane] = (uint8_t)t;
+  }
+  __syncthreads();
+  if (lane == 0) {
+    uint32_t st = 0;
+    for (uint32_t l = 0; l < 64; l++) {
+      sh.s_start[w][l] = (uint8_t)st;
+      st               = sh.T[w][st] ^ sh.e_end[w][l];
+    }
+  }
+  __syncthreads();
+
+  // pass 2: parity from the true start states; tail bits from the final state (natural order:
+  // encoder 1's three (x, z) pairs, then encoder 2's)
+  s = sh.s_start[w][lane];
+  p = pi0;
+  g = g0;
+  for (uint32_t k = k0; k < k1; k++) {
+    const uint32_t u = w ? c[p] : c[k];
+    adv(p, g);
+    coded[3 * k + 1 + w] = (uint8_t)rsc_step(s, u);
+    if (w == 0) {
+      coded[3 * k] = (uint8_t)u;
+    }
+  }
+  if (k0 < K && k1 == K) {
+    for (uint32_t j = 0; j < 3; j++) {
+      const uint32_t x  = ((s >> 2) ^ (s >> 1)) & 1u;  // the feedback: the register input becomes 0
+      const uint32_t pz = rsc_step(s, x);
+      coded[3 * K + 6 * w + 2 * j]     = (uint8_t)x;
+      coded[3 * K + 6 * w + 2 * j + 1] = (uint8_t)pz;
+    }
+  }
+  __syncthreads();
+}
+
 __global__ __launch_bounds__(128) void enc_cb_kernel(const EncCb* __restrict__ cbs)
 {
   const EncCb& b = cbs[blockIdx.x];
   __shared__ uint8_t  cbytes[768];
   __shared__ uint8_t  c[6144];
   __shared__ uint8_t  coded[3 * 6144 + 12];
-  __shared__ uint8_t  e_end[2][64], s_start[2][64], T[2][8];
+  __shared__ PcccLds  sh;
   const uint32_t      K = b.K, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const uint32_t      nB = b.rlen / 8;
 
@@ -144,65 +215,7 @@ __global__ __launch_bounds__(128) void enc_cb_kernel(const EncCb* __restrict__ c
     c[k] = (cbytes[k >> 3] >> (7 - (k & 7))) & 1u;
   }
   __syncthreads();
-
-  // pass 1: every chunk from the zero state; the zero-input transition of a whole chunk
-  const uint32_t L = (K + 63) / 64, k0 = lane * L, k1 = min(k0 + L, K);
-  // QPP pi(k) = (f1 k + f2 k^2) mod K stepped incrementally: pi(k+1) = pi(k) + g(k),
-  // g(k+1) = g(k) + 2 f2 (mod K)
-  const uint32_t pi0 = k0 < K ? (uint32_t)(((uint64_t)b.f1 * k0 + (uint64_t)b.f2 * k0 * k0) % K) : 0u;
-  const uint32_t g0  = k0 < K ? (uint32_t)(((uint64_t)b.f1 + (uint64_t)b.f2 * (2 * (uint64_t)k0 + 1)) % K) : 0u;
-  const uint32_t d2  = (uint32_t)((2 * (uint64_t)b.f2) % K);
-  auto           adv = [&](uint32_t& p, uint32_t& g) {
-    p += g;
-    p -= p >= K ? K : 0u;
-    g += d2;
-    g -= g >= K ? K : 0u;
-  };
-  uint32_t s = 0, p = pi0, g = g0;
-  for (uint32_t k = k0; k < k1; k++) {
-    rsc_step(s, w ? c[p] : c[k]);
-    adv(p, g);
-  }
-  e_end[w][lane] = (uint8_t)s;
-  if (lane < 8) {
-    uint32_t t = lane;
-    for (uint32_t k = 0; k < L; k++) {
-      rsc_step(t, 0);
-    }
-    T[w][lane] = (uint8_t)t;
-  }
-  __syncthreads();
-  if (lane == 0) {
-    uint32_t st = 0;
-    for (uint32_t l = 0; l < 64; l++) {
-      s_start[w][l] = (uint8_t)st;
-      st            = T[w][st] ^ e_end[w][l];
-    }
-  }
-  __syncthreads();
-
-  // pass 2: parity from the true start states; tail bits from the final state (natural order:
-  // encoder 1's three (x, z) pairs, then encoder 2's)
-  s = s_start[w][lane];
-  p = pi0;
-  g = g0;
-  for (uint32_t k = k0; k < k1; k++) {
-    const uint32_t u = w ? c[p] : c[k];
-    adv(p, g);
-    coded[3 * k + 1 + w] = (uint8_t)rsc_step(s, u);
-    if (w == 0) {
-      coded[3 * k] = (uint8_t)u;
-    }
-  }
-  if (k0 < K && k1 == K) {
-    for (uint32_t j = 0; j < 3; j++) {
-      const uint32_t x  = ((s >> 2) ^ (s >> 1)) & 1u;  // the feedback: the register input becomes 0
-      const uint32_t pz = rsc_step(s, x);
-      coded[3 * K + 6 * w + 2 * j]     = (uint8_t)x;
-      coded[3 * K + 6 * w + 2 * j + 1] = (uint8_t)pz;
-    }
-  }
-  __syncthreads();
+  pccc_encode(c, K, b.f1, b.f2, coded, sh);
 
   // rate matching: the read-out table streamed 8 entries a thread ahead of the LDS gathers
   const uint16_t* __restrict__ fwd = b.fwd;
@@ -257,6 +270,107 @@ hipError_t enc_pack_launch(const EncTb* d_tbs, uint32_t ntb, uint32_t max_bytes,
     return hipSuccess;
   }
   hipLaunchKernelGGL(enc_pack_kernel, dim3((max_bytes + 255) / 256, ntb), dim3(256), 0, stream, d_tbs);
+  return hipGetLastError();
+}
+
+}  // namespace srsran_amd
+
+namespace srsran_amd {
+
+// srsran_tcod_encode (turbocoder.c:77-185) of one code block: K unpacked input bits (SRSRAN_TX_NULL = 100 marks
+// filler bits: encoded as 0, passed through to the systematic output and blanking encoder 1's parity) -> 3 K + 12
+// unpacked output bits
+__global__ __launch_bounds__(128) void tcod_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ out, uint32_t K,
+                                                   uint32_t f1, uint32_t f2)
+{
+  __shared__ uint8_t c[6144];
+  __shared__ uint8_t coded[3 * 6144 + 12];
+  __shared__ PcccLds sh;
+  for (uint32_t k = threadIdx.x; k < K; k += 128) {
+    const uint8_t x = in[k];
+    c[k]            = x == kTxNull ? 0u : x;
+  }
+  __syncthreads();
+  pccc_encode(c, K, f1, f2, coded, sh);
+  for (uint32_t k = threadIdx.x; k < K; k += 128) {
+    const uint8_t x = in[k];
+    out[3 * k]      = x;
+    out[3 * k + 1]  = x == kTxNull ? kTxNull : coded[3 * k + 1];
+    out[3 * k + 2]  = coded[3 * k + 2];
+  }
+  for (uint32_t k = threadIdx.x; k < 12; k += 128) {
+    out[3 * K + k] = coded[3 * K + k];
+  }
+}
+
+hipError_t tcod_launch(const uint8_t* d_in, uint8_t* d_out, uint32_t K, uint32_t f1, uint32_t f2, hipStream_t stream)
+{
+  if (K == 0 || K > 6144) {
+    return hipErrorInvalidValue;
+  }
+  hipLaunchKernelGGL(tcod_kernel, dim3(1), dim3(128), 0, stream, d_in, d_out, K, f1, f2);
+  return hipGetLastError();
+}
+
+// srsran_rm_turbo_tx_lut (rm_turbo.c:345-388) of one code block, one workgroup: for rv 0 the circular buffer w
+// (sub-block interleaving and bit collection, 3 K + 12 bits packed MSB first, no dummy bits) from the packed
+// systematic (K + 4 bits) and parity (2 (K + 4) bits) streams through the reference's interleaver tables, into
+// w_buff; otherwise w from w_buff.  Then out_len bits of w from r_ptr (wrapping) into output at bit w_offset: the
+// bits before w_offset in its byte kept, those after the last bit kept -- or cleared when the reference's last
+// srsran_bit_copy was byte-aligned (zero_tail, bit.c:685-698)
+__global__ __launch_bounds__(256) void rm_tx_lut_kernel(RmTxLut a)
+{
+  extern __shared__ uint8_t w[];
+  const uint32_t in_len = 3 * a.K + 12, nwb = (in_len + 7) / 8, nsys = a.K + 4;
+  for (uint32_t b = threadIdx.x; b < nwb; b += 256) {
+    uint8_t v = 0;
+    if (a.rv == 0) {
+#pragma unroll
+      for (uint32_t j = 0; j < 8; j++) {
+        const uint32_t pos = 8 * b + j;
+        uint32_t       bit = 0;
+        if (pos < nsys) {
+          const uint32_t i = a.tsys[pos];
+          bit              = (a.sys[i >> 3] >> (7 - (i & 7))) & 1u;
+        } else if (pos < in_len) {
+          const uint32_t i = a.tpar[pos - nsys];
+          bit              = (a.par[i >> 3] >> (7 - (i & 7))) & 1u;
+        }
+        v |= (uint8_t)(bit << (7 - j));
+      }
+      a.w_buff[b] = v;
+    } else {
+      v = a.w_buff[b];
+    }
+    w[b] = v;
+  }
+  __syncthreads();
+  if (a.out_len == 0) {
+    return;
+  }
+  const uint32_t first = a.w_offset / 8, last = (a.w_offset + a.out_len - 1) / 8;
+  for (uint32_t ob = first + threadIdx.x; ob <= last; ob += 256) {
+    uint8_t v = a.output[ob];
+#pragma unroll
+    for (uint32_t j = 0; j < 8; j++) {
+      const uint32_t pos = 8 * ob + j;
+      const uint8_t  m   = (uint8_t)(0x80u >> j);
+      if (pos >= a.w_offset && pos < a.w_offset + a.out_len) {
+        uint32_t src = a.r_ptr + (pos - a.w_offset);
+        src %= in_len;
+        v = (uint8_t)((v & ~m) | (((w[src >> 3] >> (7 - (src & 7))) & 1u) ? m : 0u));
+      } else if (pos >= a.w_offset + a.out_len && a.zero_tail) {
+        v = (uint8_t)(v & ~m);
+      }
+    }
+    a.output[ob] = v;
+  }
+}
+
+hipError_t rm_tx_lut_launch(const RmTxLut& a, hipStream_t stream)
+{
+  const size_t lds = (3 * (size_t)a.K + 12 + 7) / 8;
+  hipLaunchKernelGGL(rm_tx_lut_kernel, dim3(1), dim3(256), lds, stream, a);
   return hipGetLastError();
 }
 

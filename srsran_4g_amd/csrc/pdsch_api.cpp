@@ -874,10 +874,11 @@ int srsran_pdsch_encode(srsran_pdsch_t*     q,
             gr.nof_tb);
     return SRSRAN_ERROR;
   }
-  if (cfg->power_scale && cfg->p_a != 0.0f) {
-    fprintf(stderr, "[srsran_pdsch] encode: rho_a scaling is not provided\n");
-    return SRSRAN_ERROR;
-  }
+  // apply_power_allocation (pdsch.c:485-521, called by srsran_pdsch_encode whatever power_scale says, :1057-1071):
+  // the precoder scales by rho_a = 10^(p_a / 20) (x sqrt 2 with more than one port); the rho_b part scales
+  // nof_rx_antennas grids, none for the eNB's object (pdsch.c srsran_pdsch_init_enb)
+  const float rho_a   = (float)((double)powf(10.0f, cfg->p_a / 20.0f) * (P == 1 ? 1.0 : M_SQRT2));
+  const float scaling = rho_a != 0.0f ? rho_a : 1.0f;
   PdschGpu*             g      = (PdschGpu*)q->gpu;
   const uint32_t        lstart = sf->cfi + (cell.nof_prb < 10 ? 1 : 0);
   std::vector<uint32_t> tab    = pdsch_re_table(cell, gr, lstart, sf->tti % 10);
@@ -892,8 +893,8 @@ int srsran_pdsch_encode(srsran_pdsch_t*     q,
   memset(&it, 0, sizeof(it));
   it.nre       = nre;
   it.scheme    = scheme;
-  it.scaling   = 1.0f;
-  it.div_scale = scheme == 4 ? (float)(1.0f / 1.41421356237309504880) : (float)(1.0 * 0.70710678118654752440);
+  it.scaling   = scaling;
+  it.div_scale = scheme == 4 ? (float)(scaling / 1.41421356237309504880) : (float)((double)scaling * 0.70710678118654752440);
   size_t   off = align256((size_t)P * nsf_re * sizeof(float2));
   size_t   o_idx = off;
   off += align256((size_t)nre * sizeof(uint32_t));

@@ -210,16 +210,20 @@ __device__ __forceinline__ St trellis(const short* xt, const short* yt)
   return St{v2s{o[0], o[4]}, v2s{o[7], o[3]}, v2s{o[2], o[6]}, v2s{o[5], o[1]}};
 }
 
-// LDS of one code block (dwords): S [NSB*Ls int16] | CK [M windows][NSB lanes][16 B] | BITS [K/8 B] | RED [2]
+// LDS of one code block (dwords): S [NSB*Ls int16] | CK [M windows][NSB lanes][16 B] | BITS [NSB*Ls bits + a guard
+// dword] | RED [2].  BITS holds the hard decisions by soft-buffer slot, as S does: bit `slot` (dword slot / 32, bit
+// slot % 32) is natural position j L + r for slot = j Ls + r -- a DEC1 lane's window is a run of consecutive bits, a
+// DEC2 position's bit is its slot's (no division, no multiply); nat_byte() reads natural-order bytes out of it.
 struct Geo {
   int s_dw, ck_dw, bits_dw, cb_dw;
 };
 __host__ __device__ __forceinline__ Geo geo(int K, int Ls, int M)
 {
+  (void)K;
   Geo g;
   g.s_dw    = (NSB * Ls + 1) / 2;
   g.ck_dw   = M * NSB * 4;
-  g.bits_dw = (K / 8 + 3) / 4;
+  g.bits_dw = (NSB * Ls + 31) / 32 + 1;
   g.cb_dw   = g.s_dw + g.ck_dw + g.bits_dw + 2;
   return g;
 }
@@ -293,26 +297,53 @@ __device__ __forceinline__ uint32_t pin(uint32_t v)
 }
 
 // The LLR o of position k: S update (vec_sub, wraps) and, when the half-iteration's decision is
-// needed, its bit (turbodecoder.c:370-378: the sign of ext1 after DEC1, of app1 after DEC2).
+// needed, its bit (turbodecoder.c:370-378: the sign of ext1 after DEC1, of app1 after DEC2).  DEC1 returns the bit
+// (the caller gathers a window's bits and stores them once, flush_bits); DEC2 sets it at its slot's row and column.
 template <bool D2, bool BITS>
-__device__ __forceinline__ void emit(const Lane& c, int k, short o, uint32_t aux, uint32_t xw)
+__device__ __forceinline__ uint32_t emit(const Lane& c, int k, short o, uint32_t aux, uint32_t xw)
 {
-  int n;
   if (D2) {
     const lshort p = (lshort)(size_t)aux;
     *p             = (short)(o - (short)(xw & 0xffffu));
     if (BITS) {
-      const int slot = (int)(p - c.S);
-      const int sb   = (int)__umulhi((uint32_t)slot, c.magicLs);
-      n              = slot - sb * (c.Ls - c.L);
+      const uint32_t slot = (uint32_t)(p - c.S);
+      atomicOr(&c.BITS[slot >> 5], (uint32_t)(o > 0) << (slot & 31));
     }
-  } else {
-    c.Ssb[k] = (short)(o - (short)aux);
-    n        = c.s * c.L + k;
+    return 0;
   }
-  if (BITS) {
-    atomicOr(&c.BITS[n >> 5], (uint32_t)(o > 0) << (((n >> 3) & 3) * 8 + 7 - (n & 7)));
+  c.Ssb[k] = (short)(o - (short)aux);
+  return BITS ? (uint32_t)(o > 0) : 0u;
+}
+
+// DEC1: the decisions of a window t0 .. t0 + W - 1 of this lane's sub-block (bit i = position t0 + i), slots
+// s Ls + t0 .. + W - 1: one or two dwords (shared with the other wave's windows and the neighbouring sub-blocks: OR)
+__device__ __forceinline__ void flush_bits(const Lane& c, int t0, uint32_t wbits)
+{
+  if (wbits) {
+    const uint32_t pos = (uint32_t)(c.s * c.Ls + t0);
+    const uint64_t v   = (uint64_t)wbits << (pos & 31);
+    atomicOr(&c.BITS[pos >> 5], (uint32_t)v);
+    if ((uint32_t)(v >> 32)) {
+      atomicOr(&c.BITS[(pos >> 5) + 1], (uint32_t)(v >> 32));
+    }
   }
+}
+
+// Natural-order byte b of the decisions (8 positions MSB first, as srsran_bit_pack): positions n = 8b .. 8b + 7 of
+// sub-block j = n / L (magicL = ceil(2^32 / L): exact for n < 2^16) are slots n + j (Ls - L): nine bits from there,
+// the padding slot between sub-blocks j and j + 1 (Ls - L = 1 for even L, never set) squeezed out
+__device__ __forceinline__ uint32_t nat_byte(const uint32_t* bits, int L, int Ls, uint32_t magicL, int b)
+{
+  const int      n0  = 8 * b;
+  const int      j   = (int)__umulhi((uint32_t)n0, magicL);
+  const int      cnt = (j + 1) * L - n0;  // positions left in sub-block j
+  const uint32_t s0  = (uint32_t)(n0 + j * (Ls - L));
+  const uint64_t v   = (uint64_t)bits[s0 >> 5] | (uint64_t)bits[(s0 >> 5) + 1] << 32;
+  uint32_t       x   = (uint32_t)(v >> (s0 & 31)) & 0x1ffu;
+  if (cnt < 8) {
+    x = (x & ((1u << cnt) - 1u)) | ((x >> (cnt + Ls - L)) << cnt);
+  }
+  return __builtin_bitreverse32(x & 0xffu) >> 24;
 }
 
 // Phase-2 alpha side, window at t0 >= W: beta[t0+1 .. cc] recomputed from the stored beta at
@@ -336,6 +367,7 @@ __device__ __forceinline__ St alpha_llr_window(const Lane& c, St P, int t0, St P
       if (FULL ? (i & 1) : norm_at(t0 + 1 + i)) Pb = norm(Pb);
     }
   }
+  uint32_t wbits = 0;
 #pragma unroll
   for (int i = 0; i < W; i++) {
     if (FULL || t0 + i < L) {
@@ -343,8 +375,11 @@ __device__ __forceinline__ St alpha_llr_window(const Lane& c, St P, int t0, St P
       const short o  = llr(cd, bw[i]);
       P              = next<false>(cd);
       if ((i & 1) == 0) P = norm(P);  // t0 >= W: every even position
-      emit<D2, BITS>(c, t0 + i, o, aux[i], xw[i]);
+      wbits |= emit<D2, BITS>(c, t0 + i, o, aux[i], xw[i]) << i;
     }
+  }
+  if (BITS && !D2) {
+    flush_bits(c, t0, wbits);
   }
   return P;
 }
@@ -568,13 +603,17 @@ __device__ __forceinline__ void map16s(const Lane& cin, int wave, int st0)
           if (nrm(t0, i)) Pa = norm(Pa);
         }
       }
+      uint32_t wbits = 0;
 #pragma unroll
       for (int i = W - 1; i >= 0; i--) {
         const short o = llr(cand(aw[i], bm(xw[i])), Bst);
         P             = step<true>(P, xw[i]);
         Bst           = P;
         if (nrm(t0, i)) P = norm(P);
-        emit<D2, BITS>(c, t0 + i, o, aux[i], xw[i]);
+        wbits |= emit<D2, BITS>(c, t0 + i, o, aux[i], xw[i]) << i;
+      }
+      if (BITS && !D2) {
+        flush_bits(c, t0, wbits);
       }
     }
     TDECS_STAMP(st0 + 4);
@@ -612,6 +651,7 @@ __device__ __forceinline__ void body(const TdecArgs& a, int bid)
   c.M       = M;
   c.KP      = K + 32;  // SB stream stride (rm_turbo.c:260-273)
   c.magicLs = a.magicLs;
+  const uint32_t magicL = 0xffffffffu / (uint32_t)L + 1u;  // ceil(2^32 / L) (2^32 / L for a power of two)
   // the workgroup's blocks read through one uniform base: the lowest of their inputs (plain launches:
   // in_stride apart; DL-SCH: the host keeps every group of CPWG descriptors within TDEC_PAIR_SPAN)
   const int cb0 = bid * CPWG;
@@ -646,6 +686,9 @@ __device__ __forceinline__ void body(const TdecArgs& a, int bid)
     smem[(i / g.s_dw) * g.cb_dw + i % g.s_dw] = 0u;
   }
   const int h_end = (ES && __syncthreads_or(!done) == 0) ? 0 : a.n_end;
+#ifdef TDECS_STAMPS
+  int passed_at = 0, ran = 0;  // diagnostic: the half-iteration count at which this block passed; the group's count
+#endif
 
 #pragma unroll 1
   for (int hi = 0; hi < h_end; hi++) {
@@ -673,7 +716,6 @@ __device__ __forceinline__ void body(const TdecArgs& a, int bid)
     // ---------------- DL-SCH early stop: CRC of the hard decision (sch.c:426-456) ----------------
     if constexpr (ES) {
       if (crc_now) {
-        const uint8_t* bytes  = reinterpret_cast<const uint8_t*>(c.BITS);
         const int      nbytes = K / 8;
         const int      bpt    = (nbytes + 2 * NSB - 1) / (2 * NSB);
         const int      b0     = t2 * bpt;
@@ -683,7 +725,7 @@ __device__ __forceinline__ void body(const TdecArgs& a, int bid)
         uint32_t       crc    = 0;
 #pragma unroll 1
         for (int b = b0; b < b1; b++) {
-          crc = crc24_byte(crc, bytes[b], poly);
+          crc = crc24_byte(crc, nat_byte(c.BITS, L, Ls, magicL, b), poly);
         }
         uint32_t part = b0 < nbytes ? clmul_mod24(crc, (crc_a ? a.xpow_a : a.xpow_b)[nbytes - b1], poly) : 0;
 #pragma unroll
@@ -699,28 +741,46 @@ __device__ __forceinline__ void body(const TdecArgs& a, int bid)
           const uint32_t slot = a.cbs[cbl].slot;
           uint8_t*       out  = a.out + (size_t)slot * a.out_stride;
           for (int b = t2; b < nbytes; b += 2 * NSB) {
-            out[b] = bytes[b];
+            out[b] = (uint8_t)nat_byte(c.BITS, L, Ls, magicL, b);
           }
           if (t2 == 0) {
             a.noi_out[slot] = (uint8_t)(hi + 1);
             a.crc_ok[slot]  = 1;
           }
         }
+#ifdef TDECS_STAMPS
+        if (ok && !done) {
+          passed_at = hi + 1;
+        }
+#endif
         done = done || ok;
       }
+#ifdef TDECS_STAMPS
+      ran = hi + 1;
+#endif
       if (__syncthreads_or(!done) == 0) {
         break;  // every block of the workgroup passed its CRC
       }
     }
   }
+#ifdef TDECS_STAMPS
+  // diagnostic (DL-SCH batches): stamps 56 + block = the half-iterations that block needed (its CRC passed; the limit
+  // when it never did), stamp 63 = the half-iterations the workgroup ran (tools/chain_stamps.py)
+  if (ES && g_stamps && t2 == 0 && wave == 0) {
+    unsigned long long* st = g_stamps + (size_t)blockIdx.x * (blockDim.x >> 6) * 64;
+    st[56 + cbw]           = live ? (unsigned long long)(passed_at ? passed_at : h_end) : 0ull;
+    if (cbw == 0) {
+      st[63] = (unsigned long long)ran;
+    }
+  }
+#endif
 
   // ---------------- hard decision of the last half-iteration (turbodecoder.c:370-378) ----------------
   if (live && !done && h_end > 0) {
     const int      cbm   = ES ? (int)a.cbs[cbl].slot : cbl;
     uint8_t*       out   = a.out + (size_t)cbm * (ES ? a.out_stride : K / 8);
-    const uint8_t* bytes = reinterpret_cast<const uint8_t*>(c.BITS);
     for (int b = t2; b < K / 8; b += 2 * NSB) {
-      out[b] = bytes[b];
+      out[b] = (uint8_t)nat_byte(c.BITS, L, Ls, magicL, b);
     }
     if (ES && t2 == 0) {
       a.noi_out[cbm] = (uint8_t)a.n_end;

@@ -23,6 +23,10 @@ MOD_FROM_QM = {1: SRSRAN_MOD_BPSK, 2: SRSRAN_MOD_QPSK, 4: SRSRAN_MOD_16QAM, 6: S
 u32 = ctypes.c_uint32
 
 
+class srsran_tcod_t(ctypes.Structure):  # turbocoder.h:45-48 (+ the added device pointer)
+    _fields_ = [("max_long_cb", ctypes.c_uint32), ("temp", ctypes.c_void_p), ("gpu", ctypes.c_void_p)]
+
+
 class srsran_cbsegm_t(ctypes.Structure):
     _fields_ = [(n, u32) for n in ("F", "C", "K1", "K2", "K1_idx", "K2_idx", "C1", "C2", "tbs", "L_tb", "L_cb", "Z")]
 
@@ -198,6 +202,10 @@ def lib():
         "srsran_mod_bits_x_symbol": ([ctypes.c_int], u32),
         "srsran_rm_turbo_gentables": ([], None),
         "srsran_rm_turbo_free_tables": ([], None),
+        "srsran_tcod_init": ([ctypes.POINTER(srsran_tcod_t), u32], ctypes.c_int),
+        "srsran_tcod_free": ([ctypes.POINTER(srsran_tcod_t)], None),
+        "srsran_tcod_encode": ([ctypes.POINTER(srsran_tcod_t), _u8p, _u8p, u32], ctypes.c_int),
+        "srsran_rm_turbo_tx_lut": ([_u8p, _u8p, _u8p, _u8p, u32, u32, u32, u32], ctypes.c_int),
         "srsran_rm_turbo_rx_lut": ([_i16p, _i16p, u32, u32, u32], ctypes.c_int),
         "srsran_rm_turbo_rx_lut_": ([_i16p, _i16p, u32, u32, u32, ctypes.c_bool], ctypes.c_int),
         "srsran_rm_turbo_rx_lut_8bit": ([ctypes.POINTER(ctypes.c_int8), ctypes.POINTER(ctypes.c_int8), u32, u32, u32],

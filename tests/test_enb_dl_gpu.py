@@ -109,7 +109,7 @@ def test_gpu_tx_to_gpu_rx(gpu):
                                                        ("port0", 1, 1, 2, 2216, 2, 3)])
 def test_pdsch_encode_host_grids(gpu, scheme, P, ntb, Qm, tbs, tti, cfi):
     """srsran_pdsch_encode (eNB, host grids): the PDSCH REs equal the CPU transmitter's precoded
-    symbols, every other RE (here the CRS already put) is left as it was"""
+    symbols times the reference's rho_a, every other RE (here the CRS already put) is left as it was"""
     from srsran_4g_amd import ue_dl as U
     nprb = 100 if scheme == "cdd" else 50 if scheme == "diversity" else 25
     cell_id, rnti = 21, 0x3311
@@ -122,7 +122,9 @@ def test_pdsch_encode_host_grids(gpu, scheme, P, ntb, Qm, tbs, tti, cfi):
         G = nre * Qm
         e = SY.dlsch_encode(tbs, Qm, 0, G, pl, Nl=2 if scheme == "diversity" else 1)
         layers.append(SY.modulate(e ^ SY.gold(SY.pdsch_seed(rnti, q, 2 * (tti % 10), cell_id), G), Qm))
-    ports = SY.precode(layers, scheme)
+    # srsran_pdsch_encode's rho_a with p_a = 0 dB: sqrt 2 with more than one port (pdsch.c:492, 1066-1070)
+    rho_a = np.float32(np.sqrt(2.0)) if P > 1 else np.float32(1.0)
+    ports = [x * rho_a for x in SY.precode(layers, scheme)]
     crs = [SY.crs_grid(cell_id, nprb, P, p, tti % 10) for p in range(P)]
     want = []
     for p in range(P):

@@ -45,11 +45,14 @@ def env():
                                        ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                        ctypes.POINTER(ctypes.c_float)]
     L.ref_pdsch_tx_symbols.restype = ctypes.c_int
+    L.ref_pdsch_tx_symbols_sc.argtypes = L.ref_pdsch_tx_symbols.argtypes[:-1] + [ctypes.c_float,
+                                                                                 ctypes.POINTER(ctypes.c_float)]
+    L.ref_pdsch_tx_symbols_sc.restype = ctypes.c_int
     import torch
     return torch, L, O.Oracle()
 
 
-def ref_symbols(L, es, Qm, scheme, P, nl, rnti, sf_idx, cell_id, nre):
+def ref_symbols(L, es, Qm, scheme, P, nl, rnti, sf_idx, cell_id, nre, scaling=1.0):
     ncw = len(es)
     stride = max(len(e) for e in es)
     buf = np.zeros((ncw, stride), np.uint8)
@@ -57,9 +60,10 @@ def ref_symbols(L, es, Qm, scheme, P, nl, rnti, sf_idx, cell_id, nre):
         buf[c, :len(e)] = e
     u = lambda v: (ctypes.c_uint32 * len(v))(*v)  # noqa: E731
     out = np.zeros((P, nre, 2), np.float32)
-    r = L.ref_pdsch_tx_symbols(ncw, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), stride,
-                               u([len(e) for e in es]), u([MOD_OF_QM[Qm]] * ncw), u(list(range(ncw))), rnti, sf_idx,
-                               cell_id, SCHEME_ID[scheme], P, nl, 0, nre, out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
+    r = L.ref_pdsch_tx_symbols_sc(ncw, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), stride,
+                                  u([len(e) for e in es]), u([MOD_OF_QM[Qm]] * ncw), u(list(range(ncw))), rnti, sf_idx,
+                                  cell_id, SCHEME_ID[scheme], P, nl, 0, nre, scaling,
+                                  out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
     assert r == 0
     return out.view(np.complex64)[..., 0]
 
@@ -69,9 +73,16 @@ def coded_bits(ora, scheme, ntb, Qm, tbs, nre, pls):
     return [ora.dlsch_encode(tbs, Qm * Nl, 0, nre * Qm, pl) for pl in pls]
 
 
+def rho_a(p_a, P):
+    """apply_power_allocation's rho_a (pdsch.c:492): 10^(p_a / 20) x sqrt 2 with more than one port, in float"""
+    return float(np.float32(float(np.float32(10.0) ** np.float32(p_a / 20.0)) * (1.0 if P == 1 else np.sqrt(2.0))))
+
+
+@pytest.mark.parametrize("p_a", [0.0, -3.0])
 @pytest.mark.parametrize("case", CASES, ids=[f"{c[0]}_{c[1]}prb_{c[2]}p_q{c[4]}_sf{c[6]}" for c in CASES])
-def test_pdsch_encode_matches_reference_blocks(env, case):
-    """srsran_pdsch_encode on host grids: every PDSCH RE equals the reference composition"""
+def test_pdsch_encode_matches_reference_blocks(env, case, p_a):
+    """srsran_pdsch_encode on host grids: every PDSCH RE equals the reference composition, precoded with the
+    reference's rho_a (srsran_pdsch_encode applies it whatever power_scale says, pdsch.c:1057-1071)"""
     torch, L, ora = env
     from srsran_4g_amd import ue_dl as U
     scheme, nprb, P, ntb, Qm, tbs, tti, cfi = case
@@ -82,10 +93,11 @@ def test_pdsch_encode_matches_reference_blocks(env, case):
     pls = [rng.integers(0, 256, tbs // 8, dtype=np.uint8) for _ in range(ntb)]
     nl = P if scheme == "diversity" else ntb
     want = ref_symbols(L, coded_bits(ora, scheme, ntb, Qm, tbs, nre, pls), Qm, scheme, P, nl, rnti, tti % 10,
-                       cell_id, nre)
+                       cell_id, nre, rho_a(p_a, P))
     cell = U.cell(nprb, P, cell_id)
     pd = U.Pdsch(cell, 1, enb=True)
     cfg = U.pdsch_cfg(nprb, nre, [tbs] * ntb, [Qm] * ntb, scheme=scheme, rnti=rnti)
+    cfg.p_a = p_a
     grids = [np.zeros(mask.size, np.complex64) for _ in range(P)]
     ret, got = pd.encode(cfg, tti, cfi, pls, grids)
     pd.free()

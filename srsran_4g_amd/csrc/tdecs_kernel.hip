@@ -210,20 +210,20 @@ __device__ __forceinline__ St trellis(const short* xt, const short* yt)
   return St{v2s{o[0], o[4]}, v2s{o[7], o[3]}, v2s{o[2], o[6]}, v2s{o[5], o[1]}};
 }
 
-// LDS of one code block (dwords): S [NSB*Ls int16] | CK [M windows][NSB lanes][16 B] | BITS [NSB*Ls bits + a guard
-// dword] | RED [2].  BITS holds the hard decisions by soft-buffer slot, as S does: bit `slot` (dword slot / 32, bit
-// slot % 32) is natural position j L + r for slot = j Ls + r -- a DEC1 lane's window is a run of consecutive bits, a
-// DEC2 position's bit is its slot's (no division, no multiply); nat_byte() reads natural-order bytes out of it.
+// LDS of one code block (dwords): S [NSB*Ls int16] | CK [M windows][NSB lanes][16 B] | BITS | RED [2].  BITS holds
+// the hard decisions (emit): plain launches in natural order, K/8 bytes; DL-SCH batches (slot) by soft-buffer slot,
+// as S: bit `slot` (dword slot / 32, bit slot % 32) is natural position j L + r for slot = j Ls + r -- a DEC1 lane's
+// window is a run of consecutive bits, a DEC2 position's bit is its slot's (no division, no multiply); nat_byte()
+// reads natural-order bytes out of it -- NSB*Ls bits + a guard dword.
 struct Geo {
   int s_dw, ck_dw, bits_dw, cb_dw;
 };
-__host__ __device__ __forceinline__ Geo geo(int K, int Ls, int M)
+__host__ __device__ __forceinline__ Geo geo(int K, int Ls, int M, bool slot)
 {
-  (void)K;
   Geo g;
   g.s_dw    = (NSB * Ls + 1) / 2;
   g.ck_dw   = M * NSB * 4;
-  g.bits_dw = (NSB * Ls + 31) / 32 + 1;
+  g.bits_dw = slot ? (NSB * Ls + 31) / 32 + 1 : (K / 8 + 3) / 4;
   g.cb_dw   = g.s_dw + g.ck_dw + g.bits_dw + 2;
   return g;
 }
@@ -297,22 +297,37 @@ __device__ __forceinline__ uint32_t pin(uint32_t v)
 }
 
 // The LLR o of position k: S update (vec_sub, wraps) and, when the half-iteration's decision is
-// needed, its bit (turbodecoder.c:370-378: the sign of ext1 after DEC1, of app1 after DEC2).  DEC1 returns the bit
-// (the caller gathers a window's bits and stores them once, flush_bits); DEC2 sets it at its slot's row and column.
-template <bool D2, bool BITS>
+// needed, its bit (turbodecoder.c:370-378: the sign of ext1 after DEC1, of app1 after DEC2).  Two bit layouts:
+//  * BITS == 1 (plain launches): natural order, srsran_bit_pack's bytes (MSB first) -- the output copies bytes;
+//  * BITS == 2 (DL-SCH batches, CRC every half-iteration): by soft-buffer slot (Geo) -- DEC1 returns the bit (the
+//    caller gathers a window's bits and stores them once, flush_bits), DEC2 sets its slot's bit (no division).
+// The plain launches keep the natural layout: their code (the all-188 step's) measured faster with it.
+__device__ __forceinline__ void set_nat(const Lane& c, int n, short o)
+{
+  atomicOr(&c.BITS[n >> 5], (uint32_t)(o > 0) << (((n >> 3) & 3) * 8 + 7 - (n & 7)));
+}
+
+template <bool D2, int BITS>
 __device__ __forceinline__ uint32_t emit(const Lane& c, int k, short o, uint32_t aux, uint32_t xw)
 {
   if (D2) {
     const lshort p = (lshort)(size_t)aux;
     *p             = (short)(o - (short)(xw & 0xffffu));
-    if (BITS) {
+    if (BITS == 2) {
       const uint32_t slot = (uint32_t)(p - c.S);
       atomicOr(&c.BITS[slot >> 5], (uint32_t)(o > 0) << (slot & 31));
+    } else if (BITS == 1) {
+      const int slot = (int)(p - c.S);
+      const int sb   = (int)__umulhi((uint32_t)slot, c.magicLs);
+      set_nat(c, slot - sb * (c.Ls - c.L), o);
     }
     return 0;
   }
   c.Ssb[k] = (short)(o - (short)aux);
-  return BITS ? (uint32_t)(o > 0) : 0u;
+  if (BITS == 1) {
+    set_nat(c, c.s * c.L + k, o);
+  }
+  return BITS == 2 ? (uint32_t)(o > 0) : 0u;
 }
 
 // DEC1: the decisions of a window t0 .. t0 + W - 1 of this lane's sub-block (bit i = position t0 + i), slots
@@ -348,7 +363,7 @@ __device__ __forceinline__ uint32_t nat_byte(const uint32_t* bits, int L, int Ls
 
 // Phase-2 alpha side, window at t0 >= W: beta[t0+1 .. cc] recomputed from the stored beta at
 // cc = min(t0 + W, L) (checkpoint), then alpha + LLR of t0 .. cc-1.
-template <bool D2, bool BITS, bool FULL>
+template <bool D2, int BITS, bool FULL>
 __device__ __forceinline__ St alpha_llr_window(const Lane& c, St P, int t0, St Pb, const uint32_t* xw,
                                                const uint32_t* aux)
 {
@@ -378,7 +393,7 @@ __device__ __forceinline__ St alpha_llr_window(const Lane& c, St P, int t0, St P
       wbits |= emit<D2, BITS>(c, t0 + i, o, aux[i], xw[i]) << i;
     }
   }
-  if (BITS && !D2) {
+  if (BITS == 2 && !D2) {
     flush_bits(c, t0, wbits);
   }
   return P;
@@ -464,7 +479,7 @@ struct Pipe {
 };
 
 // One constituent MAP decode of this lane's sub-block; wave 0 = alpha side, wave 1 = beta side.
-template <bool D2, bool BITS>
+template <bool D2, int BITS>
 __device__ __forceinline__ void map16s(const Lane& cin, int wave, int st0)
 {
   (void)st0;  // first stamp index of this half-iteration (TDECS_STAMPS builds)
@@ -612,7 +627,7 @@ __device__ __forceinline__ void map16s(const Lane& cin, int wave, int st0)
         if (nrm(t0, i)) P = norm(P);
         wbits |= emit<D2, BITS>(c, t0 + i, o, aux[i], xw[i]) << i;
       }
-      if (BITS && !D2) {
+      if (BITS == 2 && !D2) {
         flush_bits(c, t0, wbits);
       }
     }
@@ -636,7 +651,7 @@ __device__ __forceinline__ void body(const TdecArgs& a, int bid)
   const int L    = (int)a.L;
   const int Ls   = (int)a.Ls;
   const int M    = (L + W - 1) / W;
-  const Geo g    = geo(K, Ls, M);
+  const Geo g    = geo(K, Ls, M, ES);
   const int cb   = bid * CPWG + cbw;
   const int cbl  = cb < (int)a.ncb ? cb : (int)a.ncb - 1;
   const bool live = cb < (int)a.ncb && (!ES || a.cbs[cbl].slot != TDEC_PAD_SLOT);
@@ -697,18 +712,19 @@ __device__ __forceinline__ void body(const TdecArgs& a, int bid)
       smem[(i / g.bits_dw) * g.cb_dw + g.s_dw + g.ck_dw + i % g.bits_dw] = 0u;
     }
     __syncthreads();
-    const bool bits = ES ? crc_now : hi + 1 == h_end;
+    const bool    bits = ES ? crc_now : hi + 1 == h_end;
+    constexpr int BM   = ES ? 2 : 1;  // the bit layout (emit)
     if (hi & 1) {
       if (bits) {
-        map16s<true, true>(c, wave, 5 * hi);
+        map16s<true, BM>(c, wave, 5 * hi);
       } else {
-        map16s<true, false>(c, wave, 5 * hi);
+        map16s<true, 0>(c, wave, 5 * hi);
       }
     } else {
       if (bits) {
-        map16s<false, true>(c, wave, 5 * hi);
+        map16s<false, BM>(c, wave, 5 * hi);
       } else {
-        map16s<false, false>(c, wave, 5 * hi);
+        map16s<false, 0>(c, wave, 5 * hi);
       }
     }
     __syncthreads();
@@ -780,7 +796,7 @@ __device__ __forceinline__ void body(const TdecArgs& a, int bid)
     const int      cbm   = ES ? (int)a.cbs[cbl].slot : cbl;
     uint8_t*       out   = a.out + (size_t)cbm * (ES ? a.out_stride : K / 8);
     for (int b = t2; b < K / 8; b += 2 * NSB) {
-      out[b] = (uint8_t)nat_byte(c.BITS, L, Ls, magicL, b);
+      out[b] = ES ? (uint8_t)nat_byte(c.BITS, L, Ls, magicL, b) : reinterpret_cast<const uint8_t*>(c.BITS)[b];
     }
     if (ES && t2 == 0) {
       a.noi_out[cbm] = (uint8_t)a.n_end;
@@ -821,7 +837,7 @@ __global__ __launch_bounds__(128, 1) void TDECS_K(multi_kernel)(const TdecArgs* 
 
 size_t lds_bytes(const TdecArgs& a)
 {
-  const Geo g = geo((int)a.K, (int)a.Ls, (int)((a.L + W - 1) / W));
+  const Geo g = geo((int)a.K, (int)a.Ls, (int)((a.L + W - 1) / W), a.cbs != nullptr);
   return (size_t)CPWG * g.cb_dw * 4;
 }
 

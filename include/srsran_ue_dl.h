@@ -214,9 +214,14 @@ int srsran_chest_dl_gpu_estimate(srsran_chest_dl_t* q,
                                  void*              stream);
 
 /* ---------------- OFDM receiver (dft/ofdm.h:49-151, ofdm.c) ----------------
- * GPU FFT (mixed radix 8/4/3/2: 128..2048 points incl. 1536/768/384), no FFTW.  Provided:
- * normal or extended CP, rx_window_offset = 0, no frequency shift, no phase compensation
- * (srsran_ue_dl's configuration, ue_dl.c:88-98) and DC removal (keep_dc = false); normalize is honoured.
+ * GPU FFT (mixed radix 8/4/3/2: 128..2048 points incl. 1536/768/384), no FFTW.  Normal or extended CP and every
+ * srsran_ofdm_cfg_t option of the receiver and the modulator: normalize, keep_dc, freq_shift_f (the samples times
+ * shift_buffer: the receiver's input, in place as ofdm.c:553-555 / 569-571, the modulator's output; DC then kept),
+ * rx_window_offset (clamped to [0, 100] and written back as ofdm.c:151-157; window_offset_n = round(cp x offset)
+ * samples into each symbol's cyclic prefix, its phase ramp removed per bin -- an offset whose window leaves the cyclic
+ * prefix, i.e. above 1, returns SRSRAN_ERROR where the reference reads before its buffer), phase_compensation_hz
+ * (per-symbol phasors, ofdm.c:357-406; set_prb turns it off as ofdm_init_mbsfn_ does).  No CFR (cfr_tx_cfg is not
+ * part of this struct: srsran_enb_dl does not enable it).
  * in_buffer / out_buffer are host pointers as in the reference.  sf_type = SRSRAN_SF_MBSFN (with extended CP, as
  * srsran_ue_dl's fft_mbsfn): slot 0 holds the non-MBSFN region's normal-CP symbols, the guard, then extended-CP
  * symbols (ofdm_rx_slot_mbsfn, ofdm.c:522-535); like the reference, such an object transforms its configured
@@ -253,6 +258,8 @@ void srsran_ofdm_rx_sf_ng(srsran_ofdm_t* q, cf_t* input, cf_t* output);
 void srsran_ofdm_set_normalize(srsran_ofdm_t* q, bool normalize_enable);
 int  srsran_ofdm_rx_init_mbsfn(srsran_ofdm_t* q, srsran_cp_t cp, cf_t* in_buffer, cf_t* out_buffer, uint32_t max_prb);
 void srsran_ofdm_set_non_mbsfn_region(srsran_ofdm_t* q, uint8_t non_mbsfn_region); /* ofdm.c:241-244 */
+int  srsran_ofdm_set_freq_shift(srsran_ofdm_t* q, float freq_shift);               /* ofdm.c:421-449 */
+int  srsran_ofdm_set_phase_compensation(srsran_ofdm_t* q, double center_freq_hz);  /* ofdm.c:357-410 */
 
 /* added: nof_sf subframes x nof_rx antennas on device buffers (d_in: [sf][rx][sf_sz] samples,
  * d_out: [sf][rx][14 * nof_re]); `cfo` rotates the samples as srsran_cfo_correct(.., cfo) would
@@ -260,8 +267,8 @@ void srsran_ofdm_set_non_mbsfn_region(srsran_ofdm_t* q, uint8_t non_mbsfn_region
 int srsran_ofdm_rx_gpu(srsran_ofdm_t* q, const cf_t* d_in, cf_t* d_out, uint32_t nof_rx, uint32_t nof_sf, float cfo,
                        void* stream);
 
-/* Modulator (ofdm.c:585-690) in srsran_enb_dl's configuration (ofdm_cfg.normalize = false, DC
- * subcarrier left empty, no frequency shift, normal or extended CP).  srsran_ofdm_tx_sf: cfg.in_buffer (one
+/* Modulator (ofdm.c:585-690): the receiver's options above (srsran_enb_dl's configuration: normalize = false, DC
+ * subcarrier left empty, no frequency shift; no MBSFN subframes).  srsran_ofdm_tx_sf: cfg.in_buffer (one
  * port's 2 nsymb x 12 nof_prb grid, host) -> cfg.out_buffer (SRSRAN_SF_LEN samples, host).  Added:
  * srsran_ofdm_tx_gpu on device grids [nof_sf][nof_ports][2 nsymb][12 nof_prb] -> samples
  * [nof_sf][nof_ports][sf_len], the grid scaled by `scale` first (srsran_enb_dl_gen_signal's

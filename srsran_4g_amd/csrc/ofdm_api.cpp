@@ -5,6 +5,7 @@
 // batched device entry point.  The transforms run in ofdm_kernel.hip; no FFTW, no CPU fallback.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -121,6 +122,20 @@ struct OfdmGpu {
   CfoTab      cfo;
   bool        mbsfn = false;  // cfg.sf_type == SRSRAN_SF_MBSFN (ofdm.c:219-225)
   uint32_t    non_mbsfn_region = 2;
+  // srsran_ofdm_cfg_t options (ofdm.c:151-157, 228-233, 357-449), tables on the device (config time only, as the
+  // reference's "shall not be called during run-time")
+  bool        dc_skip  = true;     // the DFT plan's dc flag (srsran_dft_plan_set_dc): the DC bin carries nothing
+  uint32_t    win_n    = 0;        // window_offset_n
+  float2*     d_wo     = nullptr;  // window_offset_buffer [N]
+  size_t      wo_cap   = 0;
+  float2*     d_ph     = nullptr;  // [0, 2 nsymb): RX conj(phase_compensation), [2 nsymb, 4 nsymb): TX phase_compensation
+  size_t      ph_cap   = 0;
+  bool        ph_on    = false;
+  float2*     d_shift  = nullptr;  // shift_buffer [sf_sz]
+  size_t      shift_cap = 0;
+  float2*     d_comb   = nullptr;  // a CFO table times shift_buffer (srsran_ofdm_rx_gpu with both)
+  size_t      comb_cap = 0;
+  bool        shift_on = false;
 };
 
 // slot 0 of an MBSFN subframe (ofdm_rx_slot_mbsfn, ofdm.c:522-535): the first `nr` symbols with the normal cyclic
@@ -155,6 +170,78 @@ bool grow(void** p, size_t* cap, size_t need)
   return true;
 }
 
+bool upload(float2** d, size_t* cap, const std::vector<float2>& h)
+{
+  return grow((void**)d, cap, h.size() * sizeof(float2)) &&
+         hipMemcpy(*d, h.data(), h.size() * sizeof(float2), hipMemcpyHostToDevice) == hipSuccess;
+}
+
+// each symbol's cyclic prefix length, as SRSRAN_CP_LEN_NORM(i % nsymb) / SRSRAN_CP_LEN_EXT
+uint32_t sym_cp(const OfdmArgs& a, uint32_t i) { return i % a.nsymb == 0 ? a.cp0 : a.cp; }
+
+// window_offset_buffer (ofdm.c:156-158): cexpf(I M_PI 2 n i / N), the argument in double, the exponential in float
+int build_window(OfdmGpu* g)
+{
+  if (g->win_n == 0) {
+    return SRSRAN_SUCCESS;
+  }
+  const uint32_t      N = g->proto.N;
+  std::vector<float2> h(N);
+  for (uint32_t i = 0; i < N; i++) {
+    const float y = (float)(M_PI * 2.0 * (double)(float)g->win_n * (double)(float)i / (double)(float)N);
+    h[i]          = make_float2(cosf(y), sinf(y));
+  }
+  return upload(&g->d_wo, &g->wo_cap, h) ? SRSRAN_SUCCESS : SRSRAN_ERROR;
+}
+
+// srsran_ofdm_set_freq_shift's shift_buffer (ofdm.c:432-443): per symbol, t over its cyclic prefix and body,
+// cexpf(I 2 M_PI (t - cplen) f / N)
+int build_shift(OfdmGpu* g, float f)
+{
+  const OfdmArgs&     a = g->proto;
+  std::vector<float2> h(a.sf_len);
+  size_t              n = 0;
+  for (uint32_t l = 0; l < 2 * a.nsymb; l++) {
+    const uint32_t cpl = sym_cp(a, l);
+    for (uint32_t t = 0; t < a.N + cpl; t++) {
+      const float y = (float)(2.0 * M_PI * (double)((float)t - (float)cpl) * (double)f / (double)a.N);
+      h[n++]        = make_float2(cosf(y), sinf(y));
+    }
+  }
+  return upload(&g->d_shift, &g->shift_cap, h) ? SRSRAN_SUCCESS : SRSRAN_ERROR;
+}
+
+// srsran_ofdm_set_phase_compensation's phasors (ofdm.c:380-406): symbol l starts at t = (samples up to the end of
+// its cyclic prefix) / (N x 15 kHz); phase -2 pi f t in double, cexp cast to float -- the receiver multiplies by the
+// conjugate, the modulator by the phasor
+int build_phase(OfdmGpu* g, double f)
+{
+  const OfdmArgs&     a = g->proto;
+  const double        srate = (double)a.N * 15e3;
+  std::vector<float2> h(4 * a.nsymb);
+  uint32_t            count = 0;
+  for (uint32_t l = 0; l < 2 * a.nsymb; l++) {
+    count += sym_cp(a, l);
+    const double ph = -2.0 * M_PI * f * ((double)count / srate);
+    const float  c = (float)cos(ph), sn = (float)sin(ph);
+    h[l]               = make_float2(c, -sn);
+    h[2 * a.nsymb + l] = make_float2(c, sn);
+    count += a.N;
+  }
+  return upload(&g->d_ph, &g->ph_cap, h) ? SRSRAN_SUCCESS : SRSRAN_ERROR;
+}
+
+// the option tables of the current size (configure, srsran_ofdm_set_*)
+int build_options(srsran_ofdm_t* q)
+{
+  OfdmGpu* g = (OfdmGpu*)q->gpu;
+  if (build_window(g) || (g->shift_on && build_shift(g, q->cfg.freq_shift_f)) ||
+      (g->ph_on && build_phase(g, q->cfg.phase_compensation_hz))) {
+    return SRSRAN_ERROR;
+  }
+  return SRSRAN_SUCCESS;
+}
+
 int configure(srsran_ofdm_t* q, uint32_t nof_prb, uint32_t symbol_sz)
 {
   OfdmGpu* g = (OfdmGpu*)q->gpu;
@@ -185,6 +272,12 @@ int configure(srsran_ofdm_t* q, uint32_t nof_prb, uint32_t symbol_sz)
     a.mbsfn = 1;
     mbsfn_offsets(N, g->non_mbsfn_region, a.mbsfn_off);
   }
+  if (g->win_n > a.cp) {  // a window reaching before the cyclic prefix: outside the subframe's samples
+    fprintf(stderr, "[srsran_ofdm] rx_window_offset of %u samples exceeds the cyclic prefix (%u)\n", g->win_n, a.cp);
+    return SRSRAN_ERROR;
+  }
+  a.win            = g->win_n;
+  a.dc0            = g->dc_skip ? 0 : 1;
   g->proto         = a;
   q->cfg.nof_prb   = nof_prb;
   q->cfg.symbol_sz = N;
@@ -192,10 +285,13 @@ int configure(srsran_ofdm_t* q, uint32_t nof_prb, uint32_t symbol_sz)
   q->nof_re        = a.nre;
   q->slot_sz       = a.sf_len / 2;
   q->sf_sz         = a.sf_len;
-  return SRSRAN_SUCCESS;
+  return build_options(q);
 }
 
-int run(srsran_ofdm_t* q, const float2* d_in, float2* d_out, uint32_t nrx, uint32_t nsf, float cfo, hipStream_t s)
+// shift: apply the frequency shift's samples product in the transform (srsran_ofdm_rx_gpu; the host calls apply it to
+// the input buffer first, as the reference does)
+int run(srsran_ofdm_t* q, const float2* d_in, float2* d_out, uint32_t nrx, uint32_t nsf, float cfo, hipStream_t s,
+        bool shift = true)
 {
   OfdmGpu* g = (OfdmGpu*)q->gpu;
   OfdmArgs a = g->proto;
@@ -212,10 +308,24 @@ int run(srsran_ofdm_t* q, const float2* d_in, float2* d_out, uint32_t nrx, uint3
       return SRSRAN_ERROR;
     }
   }
-  if (ofdm_rx_launch(a, nsf, s) != hipSuccess) {
+  const bool used_cfo = a.cfo_tab != nullptr;
+  if (shift && g->shift_on) {  // srsran_ofdm_rx_sf's input product by shift_buffer (ofdm.c:553-555)
+    if (a.cfo_tab) {         // after the CFO correction: one table, their product
+      if (!grow((void**)&g->d_comb, &g->comb_cap, a.sf_len * sizeof(float2)) ||
+          cfo_launch(a.cfo_tab, g->d_comb, g->d_shift, a.sf_len, s) != hipSuccess) {
+        return SRSRAN_ERROR;
+      }
+      a.cfo_tab = g->d_comb;
+    } else {
+      a.cfo_tab = g->d_shift;
+    }
+  }
+  if (ofdm_rx_launch(a, nsf, s) != hipSuccess ||
+      ofdm_rx_post_launch(d_out, nsf * nrx * 2 * a.nsymb, a, a.win ? g->d_wo : nullptr, g->ph_on ? g->d_ph : nullptr,
+                          s) != hipSuccess) {
     return SRSRAN_ERROR;
   }
-  if (a.cfo_tab) {
+  if (used_cfo) {
     hipEventRecord(g->cfo.used, s);
   }
   return SRSRAN_SUCCESS;
@@ -231,10 +341,7 @@ int srsran_ofdm_rx_init_cfg(srsran_ofdm_t* q, srsran_ofdm_cfg_t* cfg)
     return SRSRAN_ERROR_INVALID_INPUTS;
   }
   if ((cfg->cp != SRSRAN_CP_NORM && cfg->cp != SRSRAN_CP_EXT) ||
-      (cfg->sf_type != SRSRAN_SF_NORM && cfg->sf_type != SRSRAN_SF_MBSFN) ||
-      std::isnormal(cfg->freq_shift_f) ||
-      std::isnormal(cfg->rx_window_offset) || std::isnormal(cfg->phase_compensation_hz) || cfg->keep_dc) {
-    fprintf(stderr, "[srsran_ofdm] only the srsran_ue_dl receiver configuration is provided\n");
+      (cfg->sf_type != SRSRAN_SF_NORM && cfg->sf_type != SRSRAN_SF_MBSFN)) {
     return SRSRAN_ERROR;
   }
   int n = 0;
@@ -252,7 +359,22 @@ int srsran_ofdm_rx_init_cfg(srsran_ofdm_t* q, srsran_ofdm_cfg_t* cfg)
     srsran_ofdm_rx_free(q);
     return SRSRAN_ERROR;
   }
-  const int ret = configure(q, cfg->nof_prb, cfg->symbol_sz);
+  // options (ofdm.c:64-65, 151-157, 228-236): the window offset clamped to [0, 100] and written back to the caller's
+  // configuration, window_offset_n = round(cp2 x offset) from the second symbol's cyclic prefix (the receiver's only;
+  // the modulator never reads it); the shift and the DC flag; phase compensation set by its setter
+  const uint32_t N0 = cfg->symbol_sz ? cfg->symbol_sz : (uint32_t)std::max(srsran_symbol_sz(cfg->nof_prb), 0);
+  if (std::isnormal(cfg->rx_window_offset)) {
+    cfg->rx_window_offset = std::min(100.0f, std::max(0.0f, cfg->rx_window_offset));
+    g->win_n = (uint32_t)roundf((float)cp_len(cfg->cp == SRSRAN_CP_EXT ? 512 : 144, N0) * cfg->rx_window_offset);
+  }
+  q->cfg.rx_window_offset      = cfg->rx_window_offset;
+  q->cfg.phase_compensation_hz = 0.0;
+  g->shift_on                  = std::isnormal(cfg->freq_shift_f);
+  g->dc_skip                   = !cfg->keep_dc && !g->shift_on;
+  int ret = configure(q, cfg->nof_prb, cfg->symbol_sz);
+  if (ret == SRSRAN_SUCCESS) {
+    ret = srsran_ofdm_set_phase_compensation(q, cfg->phase_compensation_hz);
+  }
   if (ret) {
     srsran_ofdm_rx_free(q);
   }
@@ -267,8 +389,42 @@ int srsran_ofdm_rx_set_prb(srsran_ofdm_t* q, srsran_cp_t cp, uint32_t nof_prb)
   if (cp != SRSRAN_CP_NORM && cp != SRSRAN_CP_EXT) {
     return SRSRAN_ERROR;
   }
-  q->cfg.cp = cp;
+  // ofdm.c:341-347 through ofdm_init_mbsfn_: a configuration of cp and nof_prb alone -- the window offset kept, the
+  // shift rebuilt for the new size, the DC flag from that configuration's keep_dc (false) and the shift, and phase
+  // compensation set to its 0 Hz (off)
+  OfdmGpu* g = (OfdmGpu*)q->gpu;
+  q->cfg.cp  = cp;
+  g->dc_skip = !g->shift_on;
+  g->ph_on   = false;
+  q->cfg.phase_compensation_hz = 0.0;
   return configure(q, nof_prb, 0);
+}
+
+int srsran_ofdm_set_freq_shift(srsran_ofdm_t* q, float freq_shift)
+{
+  if (!q || !q->gpu) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  OfdmGpu* g          = (OfdmGpu*)q->gpu;
+  q->cfg.freq_shift_f = freq_shift;
+  g->shift_on         = std::isnormal(freq_shift);
+  g->dc_skip          = !g->shift_on;  // ofdm.c:427, 446: DC removed without a shift, kept with one
+  g->proto.dc0        = g->dc_skip ? 0 : 1;
+  return g->shift_on ? build_shift(g, freq_shift) : SRSRAN_SUCCESS;
+}
+
+int srsran_ofdm_set_phase_compensation(srsran_ofdm_t* q, double center_freq_hz)
+{
+  if (!q || !q->gpu) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  OfdmGpu* g = (OfdmGpu*)q->gpu;
+  if (q->cfg.phase_compensation_hz == center_freq_hz) {  // ofdm.c:364-367
+    return SRSRAN_SUCCESS;
+  }
+  q->cfg.phase_compensation_hz = center_freq_hz;
+  g->ph_on                     = std::isnormal(center_freq_hz);
+  return g->ph_on ? build_phase(g, center_freq_hz) : SRSRAN_SUCCESS;
 }
 
 void srsran_ofdm_rx_free(srsran_ofdm_t* q)
@@ -284,6 +440,10 @@ void srsran_ofdm_rx_free(srsran_ofdm_t* q)
     }
     hipFree(g->d_in);
     hipFree(g->d_out);
+    hipFree(g->d_wo);
+    hipFree(g->d_ph);
+    hipFree(g->d_shift);
+    hipFree(g->d_comb);
     cfo_table_free(g->cfo);
     delete g;
   }
@@ -346,7 +506,14 @@ void srsran_ofdm_rx_sf_ng(srsran_ofdm_t* q, cf_t* input, cf_t* output)
     return;
   }
   hipMemcpyAsync(g->d_in, input, ni * sizeof(cf_t), hipMemcpyHostToDevice, g->stream);
-  if (run(q, g->d_in, g->d_out, 1, 1, 0.0f, g->stream) == SRSRAN_SUCCESS) {
+  if (g->shift_on) {  // ofdm.c:569-571: the input buffer itself multiplied by shift_buffer
+    if (cfo_launch(g->d_in, g->d_in, g->d_shift, (uint32_t)ni, g->stream) != hipSuccess) {
+      hipStreamSynchronize(g->stream);
+      return;
+    }
+    hipMemcpyAsync(input, g->d_in, ni * sizeof(cf_t), hipMemcpyDeviceToHost, g->stream);
+  }
+  if (run(q, g->d_in, g->d_out, 1, 1, 0.0f, g->stream, false) == SRSRAN_SUCCESS) {
     hipMemcpyAsync(output, g->d_out, no * sizeof(cf_t), hipMemcpyDeviceToHost, g->stream);
   }
   hipStreamSynchronize(g->stream);
@@ -469,12 +636,22 @@ int srsran_ofdm_tx_gpu(srsran_ofdm_t* q, const cf_t* d_in, cf_t* d_out, uint32_t
   if (!q || !q->gpu || !d_in || !d_out || nof_ports == 0 || nof_ports > 4 || nof_sf == 0) {
     return SRSRAN_ERROR_INVALID_INPUTS;
   }
-  OfdmArgs a = ((OfdmGpu*)q->gpu)->proto;  // proto.norm = 1 / sqrt(N) when normalising, else 1
+  OfdmGpu* g = (OfdmGpu*)q->gpu;
+  if (g->mbsfn) {
+    fprintf(stderr, "[srsran_ofdm] MBSFN modulation is not provided\n");
+    return SRSRAN_ERROR;
+  }
+  OfdmArgs a = g->proto;  // proto.norm = 1 / sqrt(N) when normalising, else 1
   a.in       = (const float2*)d_in;
   a.out      = (float2*)d_out;
   a.nrx      = nof_ports;
   a.norm     = a.norm * scale;
-  return ofdm_tx_launch(a, nof_sf, (hipStream_t)stream) == hipSuccess ? SRSRAN_SUCCESS : SRSRAN_ERROR;
+  if (ofdm_tx_launch(a, nof_sf, (hipStream_t)stream) != hipSuccess ||
+      ofdm_tx_post_launch((float2*)d_out, nof_sf * nof_ports, a, g->ph_on ? g->d_ph + 2 * a.nsymb : nullptr,
+                          g->shift_on ? g->d_shift : nullptr, (hipStream_t)stream) != hipSuccess) {
+    return SRSRAN_ERROR;
+  }
+  return SRSRAN_SUCCESS;
 }
 
 void srsran_ofdm_tx_sf(srsran_ofdm_t* q)

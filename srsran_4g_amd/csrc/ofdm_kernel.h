@@ -26,6 +26,11 @@ struct OfdmArgs {
   // region's normal cyclic prefixes, the guard, then extended ones); 0 = every slot as cp0 / cp say
   uint32_t      mbsfn;
   uint32_t      mbsfn_off[7];
+  // srsran_ofdm_cfg_t options (ofdm.c:151-157, 228-230): every non-MBSFN symbol's DFT window starts `win` samples
+  // into its cyclic prefix (rx_window_offset; the phase ramp it leaves is ofdm_rx_post's); dc0 = 1: the subcarriers
+  // start at bin 0 (keep_dc, or a frequency shift), 0: the DC bin is skipped
+  uint32_t      win;
+  uint32_t      dc0;
   int           nstages;
   int           radix[OFDM_MAX_STAGES];
   uint32_t      ns_magic[OFDM_MAX_STAGES];  // ceil(2^32 / Ns) of every stage (j / Ns by __umulhi)
@@ -37,6 +42,18 @@ hipError_t ofdm_rx_launch(const OfdmArgs& a, uint32_t nsf, hipStream_t stream);
 // modulator: in = grid [sf][port][2 nsymb][nre], out = samples [sf][port][sf_len], nrx = ports, norm = scale;
 // grid (2 nsymb, ports, nsf) workgroups
 hipError_t ofdm_tx_launch(const OfdmArgs& a, uint32_t nsf, hipStream_t stream);
+
+// rx_window_offset's phase ramp and phase compensation on the receiver's grids (ofdm_rx_slot, ofdm.c:491-512):
+// grid [rows][nre], row = (sf x nrx) x 2 nsymb + sym; x *= wo[bin(k)] (wo: N entries, nullptr = none), then
+// x *= ph[sym] (ph: 2 nsymb entries, the conjugate compensation phasors, nullptr = none); mbsfn: slot 0's rows
+// (ofdm_rx_slot_mbsfn, neither applied) untouched
+hipError_t ofdm_rx_post_launch(float2* grid, uint32_t rows, const OfdmArgs& a, const float2* wo, const float2* ph,
+                               hipStream_t stream);
+// the modulator's phase compensation and frequency shift on its samples (ofdm_tx_slot / srsran_ofdm_tx_sf,
+// ofdm.c:625-636, 687-689): out [rows][sf_len], x *= ph[symbol of n] (cyclic prefix included: it is copied after the
+// product), then x *= shift[n] (sf_len entries); either nullptr = none
+hipError_t ofdm_tx_post_launch(float2* out, uint32_t rows, const OfdmArgs& a, const float2* ph, const float2* shift,
+                               hipStream_t stream);
 
 // factor N into radices 8/4/3/2 (largest first); returns the number of stages or -1
 int ofdm_plan(uint32_t N, int* radix);

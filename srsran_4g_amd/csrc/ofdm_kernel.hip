@@ -272,7 +272,7 @@ __global__ __launch_bounds__(OFDM_THREADS) void ofdm_rx_kernel(OfdmArgs a)
   const uint32_t    sym = blockIdx.x, rx = blockIdx.y, sf = blockIdx.z;
   const uint32_t    N = NC ? NC : a.N, ns = a.nsymb, slot = sym / ns, i = sym % ns;
   const uint32_t    slot_sz = ns * N + a.cp0 + (ns - 1) * a.cp;
-  const uint32_t    off     = a.mbsfn && slot == 0 ? a.mbsfn_off[i] : slot * slot_sz + a.cp0 + i * (N + a.cp);
+  const uint32_t    off = a.mbsfn && slot == 0 ? a.mbsfn_off[i] : slot * slot_sz + a.cp0 + i * (N + a.cp) - a.win;
   const float2*     src     = a.in + ((size_t)sf * a.nrx + rx) * a.sf_len + off;
   {  // all of a thread's sample loads (and CFO factors) issued before the first use: one HBM round trip
     constexpr int U = OFDM_MAX_N / OFDM_THREADS;
@@ -300,7 +300,7 @@ __global__ __launch_bounds__(OFDM_THREADS) void ofdm_rx_kernel(OfdmArgs a)
   float2*        dst  = a.out + (((size_t)sf * a.nrx + rx) * 2 * ns + sym) * a.nre;
   const uint32_t half = a.nre / 2;
   for (uint32_t k = threadIdx.x; k < a.nre; k += OFDM_THREADS) {
-    const uint32_t bin = k < half ? N - half + k : k - half + 1;
+    const uint32_t bin = k < half ? N - half + k : k - half + 1 - a.dc0;
     float2         v   = buf[bin];
     if (a.norm != 1.0f) {
       v = make_float2(v.x * a.norm, v.y * a.norm);
@@ -326,7 +326,7 @@ __global__ __launch_bounds__(OFDM_THREADS) void ofdm_tx_kernel(OfdmArgs a)
   }
   __syncthreads();
   for (uint32_t k = threadIdx.x; k < a.nre; k += OFDM_THREADS) {
-    const uint32_t bin = k < half ? N - half + k : k - half + 1;
+    const uint32_t bin = k < half ? N - half + k : k - half + 1 - a.dc0;
     const float2   v   = src[k];
     buf[bin]           = make_float2(v.x * a.norm, -(v.y * a.norm));
   }
@@ -412,7 +412,7 @@ __global__ __launch_bounds__(64) void ofdm_rx_wave_kernel(OfdmArgs a)
   const uint32_t     sym = blockIdx.x, rx = blockIdx.y, sf = blockIdx.z, l = threadIdx.x;
   const uint32_t     ns = a.nsymb, slot = sym / ns, i = sym % ns;
   const uint32_t     slot_sz = ns * N + a.cp0 + (ns - 1) * a.cp;
-  const uint32_t     off     = a.mbsfn && slot == 0 ? a.mbsfn_off[i] : slot * slot_sz + a.cp0 + i * (N + a.cp);
+  const uint32_t     off = a.mbsfn && slot == 0 ? a.mbsfn_off[i] : slot * slot_sz + a.cp0 + i * (N + a.cp) - a.win;
   const float2*      src     = a.in + ((size_t)sf * a.nrx + rx) * a.sf_len + off;
   const float2*      tw      = a.tw;
   float2             v[M];
@@ -486,8 +486,8 @@ __global__ __launch_bounds__(64) void ofdm_rx_wave_kernel(OfdmArgs a)
     }
     if (b >= N - half) {
       dst[b - (N - half)] = x;
-    } else if (b >= 1 && b <= half) {
-      dst[b + half - 1] = x;
+    } else if (b + a.dc0 >= 1 && b + a.dc0 <= half) {
+      dst[b + half - 1 + a.dc0] = x;
     }
   }
 }
@@ -579,6 +579,67 @@ hipError_t ofdm_rx_launch(const OfdmArgs& a, uint32_t nsf, hipStream_t stream)
   } else {
     hipLaunchKernelGGL(ofdm_rx_kernel<0>, grid, dim3(OFDM_THREADS), 0, stream, a);
   }
+  return hipGetLastError();
+}
+
+__global__ void ofdm_rx_post_kernel(float2* __restrict__ grid, uint32_t rows, OfdmArgs a, const float2* __restrict__ wo,
+                                    const float2* __restrict__ ph)
+{
+  const uint32_t row = blockIdx.y, sym = row % (2 * a.nsymb);
+  if (row >= rows || (a.mbsfn && sym < a.nsymb)) {
+    return;
+  }
+  const uint32_t half = a.nre / 2;
+  float2*        g    = grid + (size_t)row * a.nre;
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < a.nre; k += gridDim.x * blockDim.x) {
+    float2 x = g[k];
+    if (wo) {
+      x = cmul(x, wo[k < half ? a.N - half + k : k - half + 1 - a.dc0]);
+    }
+    if (ph) {
+      x = cmul(x, ph[sym]);
+    }
+    g[k] = x;
+  }
+}
+
+hipError_t ofdm_rx_post_launch(float2* grid, uint32_t rows, const OfdmArgs& a, const float2* wo, const float2* ph,
+                               hipStream_t stream)
+{
+  if (rows == 0 || (!wo && !ph)) {
+    return hipSuccess;
+  }
+  hipLaunchKernelGGL(ofdm_rx_post_kernel, dim3((a.nre + 255) / 256, rows), dim3(256), 0, stream, grid, rows, a, wo, ph);
+  return hipGetLastError();
+}
+
+__global__ void ofdm_tx_post_kernel(float2* __restrict__ out, uint32_t rows, OfdmArgs a, const float2* __restrict__ ph,
+                                    const float2* __restrict__ shift)
+{
+  const uint32_t slot_sz = a.nsymb * a.N + a.cp0 + (a.nsymb - 1) * a.cp;
+  float2*        o       = out + (size_t)blockIdx.y * a.sf_len;
+  for (uint32_t n = blockIdx.x * blockDim.x + threadIdx.x; n < a.sf_len; n += gridDim.x * blockDim.x) {
+    float2 x = o[n];
+    if (ph) {
+      const uint32_t slot = n / slot_sz, r = n - slot * slot_sz;
+      const uint32_t i    = r < a.cp0 + a.N ? 0 : 1 + (r - a.cp0 - a.N) / (a.cp + a.N);
+      x                   = cmul(x, ph[slot * a.nsymb + i]);
+    }
+    if (shift) {
+      x = cmul(x, shift[n]);
+    }
+    o[n] = x;
+  }
+}
+
+hipError_t ofdm_tx_post_launch(float2* out, uint32_t rows, const OfdmArgs& a, const float2* ph, const float2* shift,
+                               hipStream_t stream)
+{
+  if (rows == 0 || (!ph && !shift)) {
+    return hipSuccess;
+  }
+  hipLaunchKernelGGL(ofdm_tx_post_kernel, dim3((a.sf_len + 255) / 256, rows), dim3(256), 0, stream, out, rows, a, ph,
+                     shift);
   return hipGetLastError();
 }
 

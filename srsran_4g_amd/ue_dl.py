@@ -150,6 +150,10 @@ def lib():
             "srsran_chest_dl_set_mbsfn_area_id": ([CH, ctypes.c_uint16], ctypes.c_int),
             "srsran_ue_dl_set_non_mbsfn_region": ([UE, ctypes.c_uint8], None),
             "srsran_ofdm_rx_gpu": ([ctypes.POINTER(srsran_ofdm_t), P, P, u32, u32, ctypes.c_float, P], ctypes.c_int),
+            "srsran_ofdm_tx_init_cfg": ([ctypes.POINTER(srsran_ofdm_t), ctypes.POINTER(srsran_ofdm_cfg_t)], ctypes.c_int),
+            "srsran_ofdm_tx_sf": ([ctypes.POINTER(srsran_ofdm_t)], None),
+            "srsran_ofdm_set_freq_shift": ([ctypes.POINTER(srsran_ofdm_t), ctypes.c_float], ctypes.c_int),
+            "srsran_ofdm_set_phase_compensation": ([ctypes.POINTER(srsran_ofdm_t), ctypes.c_double], ctypes.c_int),
             "srsran_cfo_init": ([ctypes.POINTER(srsran_cfo_t), u32], ctypes.c_int),
             "srsran_cfo_free": ([ctypes.POINTER(srsran_cfo_t)], None),
             "srsran_cfo_correct": ([ctypes.POINTER(srsran_cfo_t), P, P, ctypes.c_float], None),
@@ -259,7 +263,8 @@ class OfdmRx:
     extended CP) with its own in / out buffers, which it transforms whatever srsran_ofdm_rx_sf_ng is given
     (ofdm.c:576-578); non_mbsfn_region: srsran_ofdm_set_non_mbsfn_region."""
 
-    def __init__(self, nof_prb, normalize=False, cp=0, mbsfn=False, non_mbsfn_region=2):
+    def __init__(self, nof_prb, normalize=False, cp=0, mbsfn=False, non_mbsfn_region=2, keep_dc=False,
+                 freq_shift_f=0.0, rx_window_offset=0.0, phase_compensation_hz=0.0, tx=False):
         self.q = srsran_ofdm_t()
         self.mbsfn = mbsfn
         if mbsfn:
@@ -275,8 +280,31 @@ class OfdmRx:
         self.cfg.nof_prb = nof_prb
         self.cfg.normalize = normalize
         self.cfg.cp = cp
-        if lib().srsran_ofdm_rx_init_cfg(ctypes.byref(self.q), ctypes.byref(self.cfg)):
-            raise RuntimeError("srsran_ofdm_rx_init_cfg failed")
+        self.cfg.keep_dc = keep_dc
+        self.cfg.freq_shift_f = freq_shift_f
+        self.cfg.rx_window_offset = rx_window_offset
+        self.cfg.phase_compensation_hz = phase_compensation_hz
+        init = lib().srsran_ofdm_tx_init_cfg if tx else lib().srsran_ofdm_rx_init_cfg
+        self.ret = init(ctypes.byref(self.q), ctypes.byref(self.cfg))
+        if self.ret:
+            raise RuntimeError("srsran_ofdm_%s_init_cfg failed" % ("tx" if tx else "rx"))
+
+    def tx(self, grid):
+        """srsran_ofdm_tx_sf through the configured buffers (an object made with tx=True)"""
+        g = np.ascontiguousarray(grid, np.complex64)
+        assert g.size == 2 * self.q.nof_symbols * self.q.nof_re
+        out = np.zeros(self.q.sf_sz, np.complex64)
+        self.q.cfg.in_buffer, self.q.cfg.out_buffer = g.ctypes.data, out.ctypes.data
+        lib().srsran_ofdm_tx_sf(ctypes.byref(self.q))
+        self.q.cfg.in_buffer = self.q.cfg.out_buffer = None
+        return out
+
+    def rx_inplace(self, x):
+        """srsran_ofdm_rx_sf_ng on the caller's array (the frequency shift multiplies it in place, ofdm.c:569-571)"""
+        assert x.dtype == np.complex64 and x.flags.c_contiguous and x.size == self.q.sf_sz
+        out = np.zeros(2 * self.q.nof_symbols * self.q.nof_re, np.complex64)
+        lib().srsran_ofdm_rx_sf_ng(ctypes.byref(self.q), x.ctypes.data, out.ctypes.data)
+        return out
 
     @property
     def symbol_sz(self):

@@ -188,7 +188,7 @@ void     srsran_tdec_gpu_set_w8_max_k(uint32_t k);
 uint32_t srsran_tdec_gpu_get_w8_max_k(void);
 /* In a fused multi-size launch (srsran_tdec_gpu_run_multi) of the 16-sub-block single-lane class, the
    sizes up to k (at least the w8_max_k above) form their own launch on the 8-step-window build
-   (default 2048; 0 = no cut beyond w8_max_k).  Process-wide. */
+   (default 1536; 0 = no cut beyond w8_max_k).  Process-wide. */
 void     srsran_tdec_gpu_set_w8_fused_max_k(uint32_t k);
 uint32_t srsran_tdec_gpu_get_w8_fused_max_k(void);
 uint32_t srsran_tdec_gpu_get_generic_single_threshold(void);

@@ -793,8 +793,9 @@ static uint32_t g_w8_max_k = 800u;
 // the sizes up to this K form their own launch on the 8-step-window build (their workgroups, at 164-191
 // registers and little LDS, share SIMDs with the large sizes' workgroups).  All-188 step, one box,
 // alternating runs (gpurun_out r03z): cut at 800 (none) 12.22 ms, 1536 11.65 ms, 2368 11.71-11.73 ms,
-// 3136 12.37 ms.
-static uint32_t g_w8_fused_max_k = 2048u;
+// 3136 12.37 ms.  With the 16-step part cut again at SRSRAN_AMD_TDEC_MIDCUT = 3072 (r06v, one box, alternating):
+// 1024 10.95 ms, 1536 10.615 / 10.621 ms, 1792 10.68 ms, 2048 10.686 / 10.71 ms, 2560 11.34 ms.
+static uint32_t g_w8_fused_max_k = 1536u;
 void     tdecs_set_w8_fused_max_k(uint32_t k) { __atomic_store_n(&g_w8_fused_max_k, k, __ATOMIC_RELAXED); }
 uint32_t tdecs_w8_fused_max_k() { return __atomic_load_n(&g_w8_fused_max_k, __ATOMIC_RELAXED); }
 void     tdecs_set_w8_max_k(uint32_t k) { __atomic_store_n(&g_w8_max_k, k, __ATOMIC_RELAXED); }

@@ -139,8 +139,9 @@ def step_spread(step, n, torch, stream, host_phases=None, stream_of=None):
     GPU time between HIP events recorded after every step, the host time of every enqueue call, and -- when
     `host_phases` (srsran_4g_amd.prof) is given -- the library's host phases of the slowest call.  With
     `stream_of` (the stream the step just enqueued went to: several workers taking the steps in turn) each event
-    goes on that step's stream, so an interval is the time between two consecutive steps' completions -- what the
-    timed region's rate is made of.  -> {"gpu_ms": min/median/max, "host_ms": min/median/max, ...}"""
+    goes on that step's stream, so an interval is the time between two consecutive steps' completions (in
+    completion order: steps on different streams can finish out of order) -- what the timed region's rate is made
+    of.  -> {"gpu_ms": min/median/max, "host_ms": min/median/max, ...}"""
     import gc
 
     torch.cuda.synchronize()
@@ -166,7 +167,13 @@ def step_spread(step, n, torch, stream, host_phases=None, stream_of=None):
     torch.cuda.synchronize()
     if gc_was:
         gc.enable()
-    gpu = [ev[i].elapsed_time(ev[i + 1]) for i in range(n)]
+    if stream_of is None:
+        gpu = [ev[i].elapsed_time(ev[i + 1]) for i in range(n)]
+    else:
+        # the workers' steps can complete out of order (a step on one stream before the previous one on another):
+        # the intervals between consecutive completions, in completion order
+        t = sorted([0.0] + [ev[0].elapsed_time(ev[i + 1]) for i in range(n)])
+        gpu = [t[i + 1] - t[i] for i in range(n)]
 
     def mmm(v):
         return {"min": round(min(v), 4), "median": round(float(np.median(v)), 4), "max": round(max(v), 4)}

@@ -105,6 +105,24 @@ __device__ __forceinline__ uint2 rm_group(uint2 iv, uint2 v, const short* es, ui
                     (uint32_t)(uint16_t)acc[2] | ((uint32_t)(uint16_t)acc[3] << 16));
 }
 
+// the same when E <= N (no repetition: a position has at most one contribution, es[idx] when idx < E -- the
+// first transmission of a C3 code block): branch-free, the four positions' sums as two packed 16-bit adds (wrap)
+__device__ __forceinline__ uint2 rm_group1(uint2 iv, uint2 v, const short* es, uint32_t E)
+{
+  const uint32_t idx[4] = {iv.x & 0xffffu, iv.x >> 16, iv.y & 0xffffu, iv.y >> 16};
+  uint32_t       c[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const uint32_t e = (uint32_t)(uint16_t)es[min(idx[k], E - 1)];  // an unused slot (0xffff) reads a valid LLR
+    c[k]             = idx[k] < E ? e : 0u;
+  }
+  const uint32_t lo = c[0] | (c[1] << 16), hi = c[2] | (c[3] << 16);
+  typedef short  v2s __attribute__((ext_vector_type(2)));
+  const v2s      a  = __builtin_bit_cast(v2s, v.x) + __builtin_bit_cast(v2s, lo);
+  const v2s      b  = __builtin_bit_cast(v2s, v.y) + __builtin_bit_cast(v2s, hi);
+  return make_uint2(__builtin_bit_cast(uint32_t, a), __builtin_bit_cast(uint32_t, b));
+}
+
 __global__ __launch_bounds__(RM_LDS_THREADS) void rm_rx_lds_kernel(const RmSlot* __restrict__ slots)
 {
   // E LLRs staged as 16-byte words from the aligned address at or below e (es = the E values from `sh` on;
@@ -138,6 +156,27 @@ __global__ __launch_bounds__(RM_LDS_THREADS) void rm_rx_lds_kernel(const RmSlot*
   const gptr_t<const uint2>    inv = gptr(reinterpret_cast<const uint2*>(s.inv));
   const gptr_t<uint2>          sb  = gptr(reinterpret_cast<uint2*>(s.sb));
   constexpr int                UP  = 4;  // 4-position groups per thread whose table / buffer loads go together
+  if (s.E <= s.N && s.E > 0) {  // one period at most: every position gathers at most one LLR
+    for (uint32_t g0 = tid; 4 * g0 < s.len; g0 += UP * RM_LDS_THREADS) {
+      uint2 iv[UP], v[UP];
+#pragma unroll
+      for (int u = 0; u < UP; u++) {
+        const uint32_t g = g0 + u * RM_LDS_THREADS;
+        if (4 * g < s.len) {
+          iv[u] = inv[g];
+          v[u]  = s.overwrite ? make_uint2(0, 0) : sb[g];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < UP; u++) {
+        const uint32_t g = g0 + u * RM_LDS_THREADS;
+        if (4 * g < s.len) {
+          sb[g] = rm_group1(iv[u], v[u], es, s.E);
+        }
+      }
+    }
+    return;
+  }
   for (uint32_t g0 = tid; 4 * g0 < s.len; g0 += UP * RM_LDS_THREADS) {
     uint2 iv[UP], v[UP];
 #pragma unroll

@@ -11,11 +11,12 @@
 //   * the tail trellis (beta_trellis) saturates upwards only ((int16)x + y > 127 ? 127 : (int8));
 //   * the LLR m1 - m0 (saturating) is halved by an arithmetic shift (divide_output 1).
 //
-// Mapping: ONE LANE PER SUB-BLOCK, the 8 states of the lane's sub-block in 8 registers (int8 values held
-// in int32).  A workgroup is one wave: 64 / NSB code blocks.  The block's input streams, a-priori and
-// extrinsic arrays live in LDS (6 x (K + 4) bytes; ext2 overwrites app2 in place); the beta metrics of a MAP pass go to a global scratch
-// ([block][position][lane] x 8 bytes, one 8-byte store a lane a position, coalesced over the block's
-// lanes) and are read back by the alpha pass of the same lane.  All half-iterations run in one launch.
+// Mapping: TWO LANES PER SUB-BLOCK, one in each of the workgroup's two waves (alpha / beta, meeting in the middle
+// of the sub-block: map_pass), the 8 states in 8 registers (int8 values held in int32).  A workgroup is two waves
+// over 64 / NSB code blocks.  The block's input streams, a-priori and
+// extrinsic arrays live in LDS (6 x (K + 4) bytes; ext2 overwrites app2 in place); the metrics a MAP pass hands from
+// one wave to the other go to a global scratch ([block][position][lane] x 8 bytes, one 8-byte store a lane a
+// position, coalesced over the block's lanes): the betas of the upper half, the alphas of the lower half.  All half-iterations run in one launch.
 // This is the off-by-default path of srsUE (srsue/src/main.cc:404-406); it is written for parity, not
 // tuned like the 16-bit decoders.
 #include <hip/hip_runtime.h>
@@ -116,130 +117,204 @@ __device__ __forceinline__ void unpack8(uint2 r, int o[8])
   }
 }
 
-// One MAP pass of a lane over its sub-block d (turbodecoder_win.h:551-832): X systematic (or the
-// de-interleaved extrinsic of DEC 1), A optional a-priori, P parity, all SB-ordered in LDS with the
-// tail at [K, K + 3); OUT the extrinsic LLRs.  beta: this block's scratch, [Ls + 1][NSB] x 8 bytes.
+// One MAP pass of sub-block d (turbodecoder_win.h:551-832) by TWO lanes, one in each wave of the workgroup (side 0:
+// alpha, side 1: beta), meeting in the middle h = Ls / 2.  X systematic (or the de-interleaved extrinsic of DEC 1),
+// A optional a-priori, P parity, all SB-ordered in LDS with the tail at [K, K + 3); OUT the extrinsic LLRs.
+//   phase 1: side 1 trains beta (first OVL positions, shifted down a lane; the last sub-block from the tail trellis)
+//            and runs it over positions Ls-1 .. h, storing every beta before its normalisation (win.h:666-678) at
+//            [k + 1]; side 0 trains alpha (last OVL positions, shifted up a lane) and runs it over 0 .. h-1, storing
+//            the alpha that enters position k at [k] -- the two index ranges of `sc` do not overlap;
+//   phase 2 (after a workgroup barrier): side 0 carries alpha over h .. Ls-1 with the stored betas, side 1 carries
+//            beta over h-1 .. 0 with the stored alphas; each emits the LLRs of its positions.
+// Every value is the one the reference's single lane computes (alpha through all positions, beta through all
+// positions, the LLR from alpha_k and beta_{k+1} before normalisation), so the output is the same; the chain of
+// dependent steps a lane walks is halved.  sc: this block's scratch, [Ls + 1][NSB] x 8 bytes.
 template <int NSB>
 __device__ void map_pass(const int8_t* X, const int8_t* A, const int8_t* P, int8_t* OUT, int d, int Ls, int K,
-                         uint2* beta)
+                         uint2* sc, int side, bool live)
 {
-  int o[8];
-  // ---- beta (win.h:551-681) ----
-  // training over the first OVL positions of this sub-block, from unknown (0) states
+  const int h = Ls / 2;
+  int       o[8];
+  int       bk[8];  // side 1: the beta of position k + 1 before its normalisation (the LLR of position k reads it)
+  if (live && side == 1) {
+    // ---- beta training over the first OVL positions of this sub-block, from unknown (0) states ----
 #pragma unroll
-  for (int i = 0; i < 8; i++) {
-    o[i] = 0;
-  }
-  for (int k = OVL - 1; k >= 0; k--) {
-    const int q = k * NSB + d;
-    int       x = X[q];
-    if (A) {
-      x = sadd(A[q], x);
+    for (int i = 0; i < 8; i++) {
+      o[i] = 0;
     }
-    beta_step(o, x, P[q]);
-    normalize(k, o);
+    for (int k = OVL - 1; k >= 0; k--) {
+      const int q = k * NSB + d;
+      int       x = X[q];
+      if (A) {
+        x = sadd(A[q], x);
+      }
+      beta_step(o, x, P[q]);
+      normalize(k, o);
+    }
   }
-  // the end state of sub-block d is the training result of sub-block d + 1 (move_right); the last
-  // sub-block's comes from the tail (beta_trellis, win.h:500-548)
-  int e[8];
+  if (side == 1) {  // the whole wave takes part in the shuffle
+    // the end state of sub-block d is the training result of sub-block d + 1 (move_right); the last
+    // sub-block's comes from the tail (beta_trellis, win.h:500-548)
+    int e[8];
 #pragma unroll
-  for (int i = 0; i < 8; i++) {
-    e[i] = __shfl_down(o[i], 1, NSB);
-  }
-  if (d == NSB - 1) {
-    int t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int k = K + 2; k >= K; k--) {
-      const int x = X[k], y = P[k], xy = tadd(x, y);
-      int       mb[8], nw[8];
-      mb[0] = tadd(t[4], xy);
-      mb[1] = t[4];
-      mb[2] = tadd(t[5], y);
-      mb[3] = tadd(t[5], x);
-      mb[4] = tadd(t[6], x);
-      mb[5] = tadd(t[6], y);
-      mb[6] = t[7];
-      mb[7] = tadd(t[7], xy);
-      nw[0] = t[0];
-      nw[1] = tadd(t[0], xy);
-      nw[2] = tadd(t[1], x);
-      nw[3] = tadd(t[1], y);
-      nw[4] = tadd(t[2], y);
-      nw[5] = tadd(t[2], x);
-      nw[6] = tadd(t[3], xy);
-      nw[7] = t[3];
+    for (int i = 0; i < 8; i++) {
+      e[i] = __shfl_down(o[i], 1, NSB);
+    }
+    if (live && d == NSB - 1) {
+      int t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (int k = K + 2; k >= K; k--) {
+        const int x = X[k], y = P[k], xy = tadd(x, y);
+        int       mb[8], nw[8];
+        mb[0] = tadd(t[4], xy);
+        mb[1] = t[4];
+        mb[2] = tadd(t[5], y);
+        mb[3] = tadd(t[5], x);
+        mb[4] = tadd(t[6], x);
+        mb[5] = tadd(t[6], y);
+        mb[6] = t[7];
+        mb[7] = tadd(t[7], xy);
+        nw[0] = t[0];
+        nw[1] = tadd(t[0], xy);
+        nw[2] = tadd(t[1], x);
+        nw[3] = tadd(t[1], y);
+        nw[4] = tadd(t[2], y);
+        nw[5] = tadd(t[2], x);
+        nw[6] = tadd(t[3], xy);
+        nw[7] = t[3];
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+          t[i] = mb[i] > nw[i] ? mb[i] : nw[i];
+        }
+      }
 #pragma unroll
       for (int i = 0; i < 8; i++) {
-        t[i] = mb[i] > nw[i] ? mb[i] : nw[i];
+        e[i] = t[i];
       }
     }
+    if (live) {
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        o[i]  = e[i];
+        bk[i] = e[i];  // beta_Ls: the end state, read by the LLR of position Ls - 1
+      }
+      sc[(size_t)Ls * NSB + d] = pack8(o);
+      for (int k = Ls - 1; k >= h; k--) {
+        const int q = k * NSB + d;
+        int       x = X[q];
+        if (A) {
+          x = sadd(A[q], x);
+        }
+        beta_step(o, x, P[q]);
+        sc[(size_t)k * NSB + d] = pack8(o);  // stored before normalisation
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+          bk[i] = o[i];
+        }
+        normalize(k, o);
+      }
+    }
+  } else {
+    if (live) {
+      // ---- alpha training over the last OVL positions of this sub-block ----
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        o[i] = 0;
+      }
+      for (int k = 0; k < OVL; k++) {
+        const int q = (Ls - OVL + k) * NSB + d;
+        int       x = X[q];
+        if (A) {
+          x = sadd(A[q], x);
+        }
+        int mb[8], nw[8];
+        alpha_cand(o, x, P[q], mb, nw);
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+          o[i] = max(mb[i], nw[i]);
+        }
+        normalize(k, o);
+      }
+    }
+    // the start state of sub-block d is the training result of sub-block d - 1 (move_left); sub-block 0
+    // starts known: state 0 at 0, the others at -INF = 0
 #pragma unroll
     for (int i = 0; i < 8; i++) {
-      e[i] = t[i];
+      const int e = __shfl_up(o[i], 1, NSB);
+      o[i]        = d == 0 ? 0 : e;
+    }
+    if (live) {
+      for (int k = 0; k < h; k++) {
+        const int q = k * NSB + d;
+        sc[(size_t)k * NSB + d] = pack8(o);  // the alpha entering position k
+        int x = X[q];
+        if (A) {
+          x = sadd(A[q], x);
+        }
+        int mb[8], nw[8];
+        alpha_cand(o, x, P[q], mb, nw);
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+          o[i] = max(mb[i], nw[i]);
+        }
+        normalize(k, o);
+      }
     }
   }
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    o[i] = e[i];
+  __syncthreads();
+  if (!live) {
+    return;
   }
-  beta[(size_t)Ls * NSB + d] = pack8(o);
-  for (int k = Ls - 1; k >= 0; k--) {
-    const int q = k * NSB + d;
-    int       x = X[q];
-    if (A) {
-      x = sadd(A[q], x);
-    }
-    beta_step(o, x, P[q]);
-    beta[(size_t)k * NSB + d] = pack8(o);  // stored before normalisation (win.h:666-678)
-    normalize(k, o);
-  }
-  // ---- alpha (win.h:684-832) ----
+  if (side == 0) {
+    // ---- alpha over h .. Ls-1 with the stored betas (win.h:684-832) ----
+    for (int k = h; k < Ls; k++) {
+      const int q = k * NSB + d;
+      int       x = X[q];
+      if (A) {
+        x = sadd(A[q], x);
+      }
+      int mb[8], nw[8];
+      alpha_cand(o, x, P[q], mb, nw);
+      int b[8];
+      unpack8(sc[(size_t)(k + 1) * NSB + d], b);
+      int m0 = sadd(b[0], mb[0]), m1 = sadd(b[0], nw[0]);
 #pragma unroll
-  for (int i = 0; i < 8; i++) {
-    o[i] = 0;
-  }
-  for (int k = 0; k < OVL; k++) {
-    const int q = (Ls - OVL + k) * NSB + d;
-    int       x = X[q];
-    if (A) {
-      x = sadd(A[q], x);
-    }
-    int mb[8], nw[8];
-    alpha_cand(o, x, P[q], mb, nw);
+      for (int i = 1; i < 8; i++) {
+        m0 = max(m0, sadd(b[i], mb[i]));
+        m1 = max(m1, sadd(b[i], nw[i]));
+      }
+      OUT[q] = (int8_t)(ssub(m1, m0) >> 1);  // simd_rb_shift by divide_output (win.h:810-813)
 #pragma unroll
-    for (int i = 0; i < 8; i++) {
-      o[i] = max(mb[i], nw[i]);
+      for (int i = 0; i < 8; i++) {
+        o[i] = max(mb[i], nw[i]);
+      }
+      normalize(k, o);
     }
-    normalize(k, o);
-  }
-  // the start state of sub-block d is the training result of sub-block d - 1 (move_left); sub-block 0
-  // starts known: state 0 at 0, the others at -INF = 0
+  } else {
+    // ---- beta over h-1 .. 0 with the stored alphas ----
+    for (int k = h - 1; k >= 0; k--) {
+      const int q = k * NSB + d;
+      int       x = X[q];
+      if (A) {
+        x = sadd(A[q], x);
+      }
+      const int y = P[q];
+      int       al[8], mb[8], nw[8];
+      unpack8(sc[(size_t)k * NSB + d], al);
+      alpha_cand(al, x, y, mb, nw);
+      int m0 = sadd(bk[0], mb[0]), m1 = sadd(bk[0], nw[0]);
 #pragma unroll
-  for (int i = 0; i < 8; i++) {
-    e[i] = __shfl_up(o[i], 1, NSB);
-    o[i] = d == 0 ? 0 : e[i];
-  }
-  for (int k = 0; k < Ls; k++) {
-    const int q = k * NSB + d;
-    int       x = X[q];
-    if (A) {
-      x = sadd(A[q], x);
-    }
-    int mb[8], nw[8];
-    alpha_cand(o, x, P[q], mb, nw);
-    int b[8];
-    unpack8(beta[(size_t)(k + 1) * NSB + d], b);
-    int m0 = sadd(b[0], mb[0]), m1 = sadd(b[0], nw[0]);
+      for (int i = 1; i < 8; i++) {
+        m0 = max(m0, sadd(bk[i], mb[i]));
+        m1 = max(m1, sadd(bk[i], nw[i]));
+      }
+      beta_step(o, x, y);  // beta_k from the normalised beta_{k+1}
 #pragma unroll
-    for (int i = 1; i < 8; i++) {
-      m0 = max(m0, sadd(b[i], mb[i]));
-      m1 = max(m1, sadd(b[i], nw[i]));
+      for (int i = 0; i < 8; i++) {
+        bk[i] = o[i];
+      }
+      normalize(k, o);
+      OUT[q] = (int8_t)(ssub(m1, m0) >> 1);
     }
-    OUT[q] = (int8_t)(ssub(m1, m0) >> 1);  // simd_rb_shift by divide_output (win.h:810-813)
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      o[i] = max(mb[i], nw[i]);
-    }
-    normalize(k, o);
   }
 }
 
@@ -253,13 +328,16 @@ __device__ __forceinline__ int qpp_sb(int q, int K, int Ls, int nsb, uint32_t f1
 
 // ES: the DL-SCH form -- per-block descriptors, skipped blocks, CRC early stop (decode_tb_cb, sch.c:420-456)
 template <int NSB, bool ES>
-__global__ __launch_bounds__(64) void tdec8bit_kernel(Tdec8Args a)
+__global__ __launch_bounds__(128) void tdec8bit_kernel(Tdec8Args a)
 {
   constexpr int CPW = 64 / NSB;
   extern __shared__ __align__(16) int8_t lds[];
-  const int      lane = threadIdx.x;
+  __shared__ uint32_t passed[CPW];  // ES: the block's CRC passed at this half-iteration (side 0 -> side 1)
+  const int      side = threadIdx.x >> 6;  // 0: the alpha wave, 1: the beta wave (map_pass)
+  const int      lane = threadIdx.x & 63;
   const int      cb_l = lane / NSB;
   const int      d    = lane % NSB;
+  const int      t2   = side * NSB + d;  // this thread's index among the block's 2 NSB (element-wise loops)
   const int      K    = (int)a.K;
   const int      Ls   = K / NSB;
   const int      AL   = (K + 4 + 15) & ~15;
@@ -274,7 +352,7 @@ __global__ __launch_bounds__(64) void tdec8bit_kernel(Tdec8Args a)
     }
     if (live && *a.cbs[cb].skip) {  // CRC already OK in the soft buffer (sch.c:392)
       done = true;
-      if (d == 0) {
+      if (t2 == 0) {
         a.noi_out[slot] = 0;
         a.crc_ok[slot]  = 1;
       }
@@ -297,12 +375,12 @@ __global__ __launch_bounds__(64) void tdec8bit_kernel(Tdec8Args a)
   if (live) {
     const int8_t* in = ES ? reinterpret_cast<const int8_t*>(a.cbs[cb].in) : a.in + (size_t)cb * a.in_stride;
     if (a.layout_sb) {
-      for (int q = d; q < K; q += NSB) {
+      for (int q = t2; q < K; q += 2 * NSB) {
         SY[q] = in[q];
         P0[q] = in[K + 32 + q];
         P1[q] = in[2 * (K + 32) + q];
       }
-      if (d < 3) {
+      if (t2 < 3) {
         const int t = 3 * (K + 32) + 2 * d;
         SY[K + d] = in[t];
         P0[K + d] = in[t + 1];
@@ -310,14 +388,14 @@ __global__ __launch_bounds__(64) void tdec8bit_kernel(Tdec8Args a)
         P1[K + d] = in[t + 7];
       }
     } else {
-      for (int i = 0; i < Ls; i++) {
+      for (int i = side; i < Ls; i += 2) {
         const int q = i * NSB + d, n = i + d * Ls;
         SY[q] = in[3 * n];
         P0[q] = in[3 * n + 1];
         P1[q] = in[3 * n + 2];
       }
-      if (d < 3) {
-        const int t = 3 * K + 2 * d;
+      if (t2 < 3) {
+        const int t = 3 * K + 2 * t2;
         SY[K + d] = in[t];
         P0[K + d] = in[t + 1];
         A2[K + d] = in[t + 6];
@@ -332,36 +410,32 @@ __global__ __launch_bounds__(64) void tdec8bit_kernel(Tdec8Args a)
   for (int n = 0; n < a.n_end; n++) {
     if ((n & 1) == 0) {
       if (n && live) {
-        for (int q = d; q < K; q += NSB) {
+        for (int q = t2; q < K; q += 2 * NSB) {
           A1[q] = (int8_t)ssub(A1[q], E1[q]);  // srsran_vec_sub_bbb (saturating for K % 16 == 0)
         }
       }
       __syncthreads();
-      if (live) {
-        map_pass<NSB>(SY, n ? A1 : nullptr, P0, E1, d, Ls, K, beta);
-      }
+      map_pass<NSB>(SY, n ? A1 : nullptr, P0, E1, d, Ls, K, beta, side, live);
       __syncthreads();
     } else {
       if (n > 1 && live) {
-        for (int q = d; q < K; q += NSB) {
+        for (int q = t2; q < K; q += 2 * NSB) {
           E1[q] = (int8_t)ssub(E1[q], A1[q]);
         }
       }
       __syncthreads();
       if (live) {
         // app2[deinter[i]] = ext1[i]  <=>  app2[j] = ext1[forward[j]]  (srsran_vec_lut_bbb)
-        for (int j = d; j < K; j += NSB) {
+        for (int j = t2; j < K; j += 2 * NSB) {
           A2[j] = E1[qpp_sb(j, K, Ls, NSB, a.f1, a.f2)];
         }
       }
       __syncthreads();
-      if (live) {
-        map_pass<NSB>(A2, nullptr, P1, E2, d, Ls, K, beta);
-      }
+      map_pass<NSB>(A2, nullptr, P1, E2, d, Ls, K, beta, side, live);
       __syncthreads();
       if (live) {
         // app1[inter[i]] = ext2[i]
-        for (int i = d; i < K; i += NSB) {
+        for (int i = t2; i < K; i += 2 * NSB) {
           A1[qpp_sb(i, K, Ls, NSB, a.f1, a.f2)] = E2[i];
         }
       }
@@ -373,7 +447,7 @@ __global__ __launch_bounds__(64) void tdec8bit_kernel(Tdec8Args a)
       // x^(8 * bytes after) (crc24_dev.h); the first CRC pass at >= min_iters half-iterations stops the block
       const bool last = n + 1 == a.n_end;
       const bool chk  = n + 1 >= a.min_iters;
-      if (live && (chk || last)) {
+      if (live && (chk || last) && side == 0) {  // the alpha wave decides, CRCs and reports; the beta wave follows
         const int8_t*  src = ((n + 1) & 1) ? E1 : A1;
         uint8_t*       out = a.out + (size_t)slot * a.out_stride;
         const int      bpl = (nbytes + NSB - 1) / NSB;
@@ -396,17 +470,21 @@ __global__ __launch_bounds__(64) void tdec8bit_kernel(Tdec8Args a)
         for (int off = 1; off < NSB; off <<= 1) {
           part ^= (uint32_t)__shfl_xor((int)part, off, 64);
         }
-        if (chk && part == 0) {
-          done = true;
-          live = false;
-          if (d == 0) {
+        if (d == 0) {
+          passed[cb_l] = chk && part == 0;
+          if (chk && part == 0) {
             a.noi_out[slot] = (uint8_t)(n + 1);
             a.crc_ok[slot]  = 1;
+          } else if (last) {
+            a.noi_out[slot] = (uint8_t)a.n_end;
+            a.crc_ok[slot]  = 0;
           }
-        } else if (last && d == 0) {
-          a.noi_out[slot] = (uint8_t)a.n_end;
-          a.crc_ok[slot]  = 0;
         }
+      }
+      __syncthreads();
+      if (live && (chk || last) && passed[cb_l]) {
+        done = true;
+        live = false;
       }
       if (__syncthreads_or(live ? 1 : 0) == 0) {
         break;  // every block of the workgroup is done
@@ -421,7 +499,7 @@ __global__ __launch_bounds__(64) void tdec8bit_kernel(Tdec8Args a)
   if (live) {
     const int8_t* src = (a.n_end & 1) ? E1 : A1;
     uint8_t*      out = a.out + (size_t)cb * (K / 8);
-    for (int byte = d; byte < K / 8; byte += NSB) {
+    for (int byte = t2; byte < K / 8; byte += 2 * NSB) {
       uint32_t v = 0;
 #pragma unroll
       for (int b = 0; b < 8; b++) {
@@ -534,14 +612,14 @@ hipError_t tdec8bit_launch(int nsb, const Tdec8Args& a, hipStream_t stream)
   const size_t   lds  = tdec8bit_lds_bytes(nsb, a.K);
   if (a.cbs) {
     if (nsb == 16) {
-      hipLaunchKernelGGL((tdec8bit_kernel<16, true>), grid, dim3(64), lds, stream, a);
+      hipLaunchKernelGGL((tdec8bit_kernel<16, true>), grid, dim3(128), lds, stream, a);
     } else {
-      hipLaunchKernelGGL((tdec8bit_kernel<32, true>), grid, dim3(64), lds, stream, a);
+      hipLaunchKernelGGL((tdec8bit_kernel<32, true>), grid, dim3(128), lds, stream, a);
     }
   } else if (nsb == 16) {
-    hipLaunchKernelGGL((tdec8bit_kernel<16, false>), grid, dim3(64), lds, stream, a);
+    hipLaunchKernelGGL((tdec8bit_kernel<16, false>), grid, dim3(128), lds, stream, a);
   } else {
-    hipLaunchKernelGGL((tdec8bit_kernel<32, false>), grid, dim3(64), lds, stream, a);
+    hipLaunchKernelGGL((tdec8bit_kernel<32, false>), grid, dim3(128), lds, stream, a);
   }
   return hipGetLastError();
 }

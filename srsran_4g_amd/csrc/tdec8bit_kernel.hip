@@ -42,79 +42,99 @@ __device__ __forceinline__ int tadd(int a, int b)
   return z > 127 ? 127 : (int)(int8_t)z;
 }
 
-// normalize() with normalize_max and normalize_period 1 (turbodecoder_win.h:480-498)
-__device__ __forceinline__ void normalize(int k, int o[8])
+// ---- the same arithmetic on packed int16 pairs (v_pk_*): the 8 states as (s0, s1) (s2, s3) (s4, s5) (s6, s7), int8
+// values in int16 lanes.  The sum of two int8 values never leaves int16, so an int8 saturating add is a packed add
+// and a clamp to [-128, 127]; and since the clamp is monotonic, max(sat(u), sat(v)) = sat(max(u, v)): a trellis
+// step clamps once per state, after its max. ----
+typedef short v2s __attribute__((ext_vector_type(2)));
+struct S8 {
+  v2s a, b, c, d;  // (s0, s1), (s2, s3), (s4, s5), (s6, s7)
+};
+__device__ __forceinline__ v2s pmax(v2s u, v2s v) { return __builtin_elementwise_max(u, v); }
+__device__ __forceinline__ v2s psat(v2s u)
+{
+  return __builtin_elementwise_min(__builtin_elementwise_max(u, (v2s){-128, -128}), (v2s){127, 127});
+}
+__device__ __forceinline__ v2s plo(v2s u) { return __builtin_shufflevector(u, u, 0, 0); }
+__device__ __forceinline__ v2s phi(v2s u) { return __builtin_shufflevector(u, u, 1, 1); }
+__device__ __forceinline__ v2s pv(int u, int v) { return (v2s){(short)u, (short)v}; }
+
+// beta_step (win.h:641-664) on packed states
+__device__ __forceinline__ void p_beta_step(S8& o, int x, int y)
+{
+  const int xy = sadd(x, y);
+  const v2s n01 = psat(pmax(plo(o.c) + pv(xy, 0), plo(o.a) + pv(0, xy)));
+  const v2s n23 = psat(pmax(phi(o.c) + pv(y, x), phi(o.a) + pv(x, y)));
+  const v2s n45 = psat(pmax(plo(o.d) + pv(x, y), plo(o.b) + pv(y, x)));
+  const v2s n67 = psat(pmax(phi(o.d) + pv(0, xy), phi(o.b) + pv(xy, 0)));
+  o                = S8{n01, n23, n45, n67};
+}
+
+// alpha_cand (win.h:767-785) on packed states: mb / nw in state order, each saturated (the LLR adds to them again)
+__device__ __forceinline__ void p_alpha_cand(const S8& o, int x, int y, S8& mb, S8& nw)
+{
+  const int xy = sadd(x, y);
+  const v2s p1 = __builtin_shufflevector(o.a, o.b, 0, 3);  // (s0, s3)
+  const v2s p2 = __builtin_shufflevector(o.c, o.d, 0, 3);  // (s4, s7)
+  const v2s p3 = __builtin_shufflevector(o.a, o.b, 1, 2);  // (s1, s2)
+  const v2s p4 = __builtin_shufflevector(o.c, o.d, 1, 2);  // (s5, s6)
+  mb = S8{psat(p1 + pv(0, y)), psat(p2 + pv(y, 0)), psat(p3 + pv(0, y)), psat(p4 + pv(y, 0))};
+  nw = S8{psat(p3 + pv(xy, x)), psat(p4 + pv(x, xy)), psat(p1 + pv(xy, x)), psat(p2 + pv(x, xy))};
+}
+__device__ __forceinline__ S8 p_max(const S8& u, const S8& v)
+{
+  return S8{pmax(u.a, v.a), pmax(u.b, v.b), pmax(u.c, v.c), pmax(u.d, v.d)};
+}
+
+// normalize (normalize_max, period 1): o - max, which is <= 0, clamped below
+__device__ __forceinline__ void p_normalize(int k, S8& o)
 {
   if (k != 0) {
-    int m = max(o[0], o[1]);
-#pragma unroll
-    for (int i = 2; i < 8; i++) {
-      m = max(m, o[i]);
-    }
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      o[i] = ssub(o[i], m);
-    }
+    const v2s m2 = pmax(pmax(o.a, o.b), pmax(o.c, o.d));
+    const v2s m  = plo(pmax(m2, __builtin_shufflevector(m2, m2, 1, 0)));
+    const v2s lo = (v2s){-128, -128};
+    o            = S8{pmax(o.a - m, lo), pmax(o.b - m, lo), pmax(o.c - m, lo), pmax(o.d - m, lo)};
   }
 }
 
-// backward step (turbodecoder_win.h:641-664)
-__device__ __forceinline__ void beta_step(int o[8], int x, int y)
+// the LLR of a position (win.h:795-813): max over states of sadd(beta, mb) and of sadd(beta, nw), their saturating
+// difference halved
+__device__ __forceinline__ int8_t p_llr(const S8& b, const S8& mb, const S8& nw)
 {
-  const int xy = sadd(x, y);
-  int       n[8];
-  n[0] = max(sadd(o[4], xy), o[0]);
-  n[1] = max(o[4], sadd(o[0], xy));
-  n[2] = max(sadd(o[5], y), sadd(o[1], x));
-  n[3] = max(sadd(o[5], x), sadd(o[1], y));
-  n[4] = max(sadd(o[6], x), sadd(o[2], y));
-  n[5] = max(sadd(o[6], y), sadd(o[2], x));
-  n[6] = max(o[7], sadd(o[3], xy));
-  n[7] = max(sadd(o[7], xy), o[3]);
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    o[i] = n[i];
-  }
+  const v2s s0 = pmax(pmax(b.a + mb.a, b.b + mb.b), pmax(b.c + mb.c, b.d + mb.d));
+  const v2s s1 = pmax(pmax(b.a + nw.a, b.b + nw.b), pmax(b.c + nw.c, b.d + nw.d));
+  const int m0 = sat8(max((int)s0.x, (int)s0.y)), m1 = sat8(max((int)s1.x, (int)s1.y));
+  return (int8_t)(ssub(m1, m0) >> 1);
 }
 
-// forward-step branch candidates (turbodecoder_win.h:767-785): mb = bit-0 branch, nw = bit-1 branch
-__device__ __forceinline__ void alpha_cand(const int o[8], int x, int y, int mb[8], int nw[8])
+__device__ __forceinline__ uint2 p_pack(const S8& o)
 {
-  const int xy = sadd(x, y);
-  mb[0] = o[0];
-  mb[1] = sadd(o[3], y);
-  mb[2] = sadd(o[4], y);
-  mb[3] = o[7];
-  mb[4] = o[1];
-  mb[5] = sadd(o[2], y);
-  mb[6] = sadd(o[5], y);
-  mb[7] = o[6];
-  nw[0] = sadd(o[1], xy);
-  nw[1] = sadd(o[2], x);
-  nw[2] = sadd(o[5], x);
-  nw[3] = sadd(o[6], xy);
-  nw[4] = sadd(o[0], xy);
-  nw[5] = sadd(o[3], x);
-  nw[6] = sadd(o[4], x);
-  nw[7] = sadd(o[7], xy);
+  const uint32_t a = __builtin_bit_cast(uint32_t, o.a), b = __builtin_bit_cast(uint32_t, o.b);
+  const uint32_t c = __builtin_bit_cast(uint32_t, o.c), d = __builtin_bit_cast(uint32_t, o.d);
+  // the low byte of every int16 lane: bytes 0, 2 of a and b, then of c and d
+  return make_uint2(__builtin_amdgcn_perm(b, a, 0x06040200u), __builtin_amdgcn_perm(d, c, 0x06040200u));
 }
-
-__device__ __forceinline__ uint2 pack8(const int o[8])
+__device__ __forceinline__ S8 p_unpack(uint2 r)
 {
-  uint2 r;
-  r.x = (uint32_t)(o[0] & 0xff) | ((uint32_t)(o[1] & 0xff) << 8) | ((uint32_t)(o[2] & 0xff) << 16) |
-        ((uint32_t)(o[3] & 0xff) << 24);
-  r.y = (uint32_t)(o[4] & 0xff) | ((uint32_t)(o[5] & 0xff) << 8) | ((uint32_t)(o[6] & 0xff) << 16) |
-        ((uint32_t)(o[7] & 0xff) << 24);
-  return r;
+  // byte i to the high byte of an int16 lane, then an arithmetic shift right by 8 sign-extends it
+  const v2s a = __builtin_bit_cast(v2s, __builtin_amdgcn_perm(0u, r.x, 0x010c000cu)) >> (v2s){8, 8};
+  const v2s b = __builtin_bit_cast(v2s, __builtin_amdgcn_perm(0u, r.x, 0x030c020cu)) >> (v2s){8, 8};
+  const v2s c = __builtin_bit_cast(v2s, __builtin_amdgcn_perm(0u, r.y, 0x010c000cu)) >> (v2s){8, 8};
+  const v2s d = __builtin_bit_cast(v2s, __builtin_amdgcn_perm(0u, r.y, 0x030c020cu)) >> (v2s){8, 8};
+  return S8{a, b, c, d};
 }
-__device__ __forceinline__ void unpack8(uint2 r, int o[8])
+__device__ __forceinline__ S8 p_zero() { return S8{(v2s){0, 0}, (v2s){0, 0}, (v2s){0, 0}, (v2s){0, 0}}; }
+__device__ __forceinline__ S8 p_shfl_down(const S8& o, int w)
 {
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    o[i]     = (int)(int8_t)(r.x >> (8 * i));
-    o[4 + i] = (int)(int8_t)(r.y >> (8 * i));
-  }
+  auto sh = [&](v2s v) {
+    return __builtin_bit_cast(v2s, __shfl_down((int)__builtin_bit_cast(uint32_t, v), 1, w));
+  };
+  return S8{sh(o.a), sh(o.b), sh(o.c), sh(o.d)};
+}
+__device__ __forceinline__ S8 p_shfl_up(const S8& o, int w)
+{
+  auto sh = [&](v2s v) { return __builtin_bit_cast(v2s, __shfl_up((int)__builtin_bit_cast(uint32_t, v), 1, w)); };
+  return S8{sh(o.a), sh(o.b), sh(o.c), sh(o.d)};
 }
 
 // One MAP pass of sub-block d (turbodecoder_win.h:551-832) by TWO lanes, one in each wave of the workgroup (side 0:
@@ -130,36 +150,28 @@ __device__ __forceinline__ void unpack8(uint2 r, int o[8])
 // positions, the LLR from alpha_k and beta_{k+1} before normalisation), so the output is the same; the chain of
 // dependent steps a lane walks is halved.  sc: this block's scratch, [Ls + 1][NSB] x 8 bytes.
 template <int NSB>
-__device__ void map_pass(const int8_t* X, const int8_t* A, const int8_t* P, int8_t* OUT, int d, int Ls, int K,
+__device__ __forceinline__ void map_pass(const int8_t* X, const int8_t* A, const int8_t* P, int8_t* OUT, int d, int Ls, int K,
                          uint2* sc, int side, bool live)
 {
   const int h = Ls / 2;
-  int       o[8];
-  int       bk[8];  // side 1: the beta of position k + 1 before its normalisation (the LLR of position k reads it)
-  if (live && side == 1) {
-    // ---- beta training over the first OVL positions of this sub-block, from unknown (0) states ----
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      o[i] = 0;
-    }
-    for (int k = OVL - 1; k >= 0; k--) {
-      const int q = k * NSB + d;
-      int       x = X[q];
-      if (A) {
-        x = sadd(A[q], x);
+  S8        o  = p_zero();
+  S8        bk = p_zero();  // side 1: the beta of position k + 1 before its normalisation (the LLR of position k reads it)
+  if (side == 1) {
+    if (live) {
+      // ---- beta training over the first OVL positions of this sub-block, from unknown (0) states ----
+      for (int k = OVL - 1; k >= 0; k--) {
+        const int q = k * NSB + d;
+        int       x = X[q];
+        if (A) {
+          x = sadd(A[q], x);
+        }
+        p_beta_step(o, x, P[q]);
+        p_normalize(k, o);
       }
-      beta_step(o, x, P[q]);
-      normalize(k, o);
     }
-  }
-  if (side == 1) {  // the whole wave takes part in the shuffle
-    // the end state of sub-block d is the training result of sub-block d + 1 (move_right); the last
-    // sub-block's comes from the tail (beta_trellis, win.h:500-548)
-    int e[8];
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      e[i] = __shfl_down(o[i], 1, NSB);
-    }
+    // the end state of sub-block d is the training result of sub-block d + 1 (move_right, the whole wave takes part
+    // in the shuffle); the last sub-block's comes from the tail (beta_trellis, win.h:500-548)
+    o = p_shfl_down(o, NSB);
     if (live && d == NSB - 1) {
       int t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
       for (int k = K + 2; k >= K; k--) {
@@ -186,77 +198,56 @@ __device__ void map_pass(const int8_t* X, const int8_t* A, const int8_t* P, int8
           t[i] = mb[i] > nw[i] ? mb[i] : nw[i];
         }
       }
-#pragma unroll
-      for (int i = 0; i < 8; i++) {
-        e[i] = t[i];
-      }
+      o = S8{pv(t[0], t[1]), pv(t[2], t[3]), pv(t[4], t[5]), pv(t[6], t[7])};
     }
     if (live) {
-#pragma unroll
-      for (int i = 0; i < 8; i++) {
-        o[i]  = e[i];
-        bk[i] = e[i];  // beta_Ls: the end state, read by the LLR of position Ls - 1
-      }
-      sc[(size_t)Ls * NSB + d] = pack8(o);
+      bk                       = o;  // beta_Ls: the end state, read by the LLR of position Ls - 1
+      sc[(size_t)Ls * NSB + d] = p_pack(o);
       for (int k = Ls - 1; k >= h; k--) {
         const int q = k * NSB + d;
         int       x = X[q];
         if (A) {
           x = sadd(A[q], x);
         }
-        beta_step(o, x, P[q]);
-        sc[(size_t)k * NSB + d] = pack8(o);  // stored before normalisation
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-          bk[i] = o[i];
-        }
-        normalize(k, o);
+        p_beta_step(o, x, P[q]);
+        sc[(size_t)k * NSB + d] = p_pack(o);  // stored before normalisation (win.h:666-678)
+        bk                      = o;
+        p_normalize(k, o);
       }
     }
   } else {
     if (live) {
       // ---- alpha training over the last OVL positions of this sub-block ----
-#pragma unroll
-      for (int i = 0; i < 8; i++) {
-        o[i] = 0;
-      }
       for (int k = 0; k < OVL; k++) {
         const int q = (Ls - OVL + k) * NSB + d;
         int       x = X[q];
         if (A) {
           x = sadd(A[q], x);
         }
-        int mb[8], nw[8];
-        alpha_cand(o, x, P[q], mb, nw);
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-          o[i] = max(mb[i], nw[i]);
-        }
-        normalize(k, o);
+        S8 mb, nw;
+        p_alpha_cand(o, x, P[q], mb, nw);
+        o = p_max(mb, nw);
+        p_normalize(k, o);
       }
     }
     // the start state of sub-block d is the training result of sub-block d - 1 (move_left); sub-block 0
     // starts known: state 0 at 0, the others at -INF = 0
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      const int e = __shfl_up(o[i], 1, NSB);
-      o[i]        = d == 0 ? 0 : e;
+    o = p_shfl_up(o, NSB);
+    if (d == 0) {
+      o = p_zero();
     }
     if (live) {
       for (int k = 0; k < h; k++) {
         const int q = k * NSB + d;
-        sc[(size_t)k * NSB + d] = pack8(o);  // the alpha entering position k
+        sc[(size_t)k * NSB + d] = p_pack(o);  // the alpha entering position k
         int x = X[q];
         if (A) {
           x = sadd(A[q], x);
         }
-        int mb[8], nw[8];
-        alpha_cand(o, x, P[q], mb, nw);
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-          o[i] = max(mb[i], nw[i]);
-        }
-        normalize(k, o);
+        S8 mb, nw;
+        p_alpha_cand(o, x, P[q], mb, nw);
+        o = p_max(mb, nw);
+        p_normalize(k, o);
       }
     }
   }
@@ -272,22 +263,11 @@ __device__ void map_pass(const int8_t* X, const int8_t* A, const int8_t* P, int8
       if (A) {
         x = sadd(A[q], x);
       }
-      int mb[8], nw[8];
-      alpha_cand(o, x, P[q], mb, nw);
-      int b[8];
-      unpack8(sc[(size_t)(k + 1) * NSB + d], b);
-      int m0 = sadd(b[0], mb[0]), m1 = sadd(b[0], nw[0]);
-#pragma unroll
-      for (int i = 1; i < 8; i++) {
-        m0 = max(m0, sadd(b[i], mb[i]));
-        m1 = max(m1, sadd(b[i], nw[i]));
-      }
-      OUT[q] = (int8_t)(ssub(m1, m0) >> 1);  // simd_rb_shift by divide_output (win.h:810-813)
-#pragma unroll
-      for (int i = 0; i < 8; i++) {
-        o[i] = max(mb[i], nw[i]);
-      }
-      normalize(k, o);
+      S8 mb, nw;
+      p_alpha_cand(o, x, P[q], mb, nw);
+      OUT[q] = p_llr(p_unpack(sc[(size_t)(k + 1) * NSB + d]), mb, nw);  // simd_rb_shift by divide_output
+      o      = p_max(mb, nw);
+      p_normalize(k, o);
     }
   } else {
     // ---- beta over h-1 .. 0 with the stored alphas ----
@@ -298,22 +278,13 @@ __device__ void map_pass(const int8_t* X, const int8_t* A, const int8_t* P, int8
         x = sadd(A[q], x);
       }
       const int y = P[q];
-      int       al[8], mb[8], nw[8];
-      unpack8(sc[(size_t)k * NSB + d], al);
-      alpha_cand(al, x, y, mb, nw);
-      int m0 = sadd(bk[0], mb[0]), m1 = sadd(bk[0], nw[0]);
-#pragma unroll
-      for (int i = 1; i < 8; i++) {
-        m0 = max(m0, sadd(bk[i], mb[i]));
-        m1 = max(m1, sadd(bk[i], nw[i]));
-      }
-      beta_step(o, x, y);  // beta_k from the normalised beta_{k+1}
-#pragma unroll
-      for (int i = 0; i < 8; i++) {
-        bk[i] = o[i];
-      }
-      normalize(k, o);
-      OUT[q] = (int8_t)(ssub(m1, m0) >> 1);
+      S8        mb, nw;
+      p_alpha_cand(p_unpack(sc[(size_t)k * NSB + d]), x, y, mb, nw);
+      const int8_t l = p_llr(bk, mb, nw);
+      p_beta_step(o, x, y);  // beta_k from the normalised beta_{k+1}
+      bk = o;
+      p_normalize(k, o);
+      OUT[q] = l;
     }
   }
 }

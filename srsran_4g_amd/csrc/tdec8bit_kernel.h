@@ -17,7 +17,7 @@ struct Tdec8Args {
   int           n_end;      // half-iterations to run (>= 1)
   uint8_t*      out;        // ncb * K/8 hard-decision bytes (device)
   uint2*        beta;       // scratch, tdec8bit_beta_bytes (device)
-  uint32_t      f1, f2;     // QPP coefficients of K
+  const uint16_t* qpp;      // the interleaver in the SB layout: qpp[j] = SB index of the QPP image of SB index j
   // ---- DL-SCH mode (decode_tb_cb with llr_is_8bit, sch.c:391-456): enabled when cbs != nullptr.  Block i reads
   // (const int8_t*)cbs[i].in (SB layout), skips it when *cbs[i].skip, and stops at the first half-iteration
   // >= min_iters whose decision passes the block's CRC; decisions to out + slot * out_stride ----

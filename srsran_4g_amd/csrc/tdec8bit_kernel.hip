@@ -255,31 +255,40 @@ __device__ __forceinline__ void map_pass(const int8_t* X, const int8_t* A, const
   if (!live) {
     return;
   }
+  // the stored metrics are loaded two positions ahead (s0 / s1): the load latency hides behind two steps
   if (side == 0) {
     // ---- alpha over h .. Ls-1 with the stored betas (win.h:684-832) ----
+    uint2 s0 = sc[(size_t)(h + 1) * NSB + d], s1 = sc[(size_t)min(h + 2, Ls) * NSB + d];
     for (int k = h; k < Ls; k++) {
-      const int q = k * NSB + d;
-      int       x = X[q];
+      const int   q  = k * NSB + d;
+      const uint2 bv = s0;
+      s0             = s1;
+      s1             = sc[(size_t)min(k + 3, Ls) * NSB + d];
+      int x          = X[q];
       if (A) {
         x = sadd(A[q], x);
       }
       S8 mb, nw;
       p_alpha_cand(o, x, P[q], mb, nw);
-      OUT[q] = p_llr(p_unpack(sc[(size_t)(k + 1) * NSB + d]), mb, nw);  // simd_rb_shift by divide_output
+      OUT[q] = p_llr(p_unpack(bv), mb, nw);  // simd_rb_shift by divide_output (win.h:810-813)
       o      = p_max(mb, nw);
       p_normalize(k, o);
     }
   } else {
     // ---- beta over h-1 .. 0 with the stored alphas ----
+    uint2 s0 = sc[(size_t)(h - 1) * NSB + d], s1 = sc[(size_t)max(h - 2, 0) * NSB + d];
     for (int k = h - 1; k >= 0; k--) {
-      const int q = k * NSB + d;
-      int       x = X[q];
+      const int   q  = k * NSB + d;
+      const uint2 av = s0;
+      s0             = s1;
+      s1             = sc[(size_t)max(k - 2, 0) * NSB + d];
+      int x          = X[q];
       if (A) {
         x = sadd(A[q], x);
       }
       const int y = P[q];
       S8        mb, nw;
-      p_alpha_cand(p_unpack(sc[(size_t)k * NSB + d]), x, y, mb, nw);
+      p_alpha_cand(p_unpack(av), x, y, mb, nw);
       const int8_t l = p_llr(bk, mb, nw);
       p_beta_step(o, x, y);  // beta_k from the normalised beta_{k+1}
       bk = o;
@@ -287,14 +296,6 @@ __device__ __forceinline__ void map_pass(const int8_t* X, const int8_t* A, const
       OUT[q] = l;
     }
   }
-}
-
-// slot (SB index) of the QPP image of the position at slot q: forward of tc_interl_lte.c:88-106
-__device__ __forceinline__ int qpp_sb(int q, int K, int Ls, int nsb, uint32_t f1, uint32_t f2)
-{
-  const uint32_t n  = (uint32_t)((q % nsb) * Ls + q / nsb);            // inter(q, win)
-  const uint32_t fn = (uint32_t)((((f2 * n) % K) * n + f1 * n) % K);  // pi(n)
-  return (int)((fn % Ls) * nsb + fn / Ls);                            // deinter(., win)
 }
 
 // ES: the DL-SCH form -- per-block descriptors, skipped blocks, CRC early stop (decode_tb_cb, sch.c:420-456)
@@ -398,7 +399,7 @@ __global__ __launch_bounds__(128) void tdec8bit_kernel(Tdec8Args a)
       if (live) {
         // app2[deinter[i]] = ext1[i]  <=>  app2[j] = ext1[forward[j]]  (srsran_vec_lut_bbb)
         for (int j = t2; j < K; j += 2 * NSB) {
-          A2[j] = E1[qpp_sb(j, K, Ls, NSB, a.f1, a.f2)];
+          A2[j] = E1[a.qpp[j]];
         }
       }
       __syncthreads();
@@ -407,7 +408,7 @@ __global__ __launch_bounds__(128) void tdec8bit_kernel(Tdec8Args a)
       if (live) {
         // app1[inter[i]] = ext2[i]
         for (int i = t2; i < K; i += 2 * NSB) {
-          A1[qpp_sb(i, K, Ls, NSB, a.f1, a.f2)] = E2[i];
+          A1[a.qpp[i]] = E2[i];
         }
       }
       __syncthreads();

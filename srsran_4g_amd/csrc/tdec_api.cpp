@@ -278,6 +278,36 @@ const XpowTables* xpow_tables()
   return &t;
 }
 
+// The 8-bit decoders' interleaver in their sub-block layout (NSB = 16 or 32 sub-blocks of Ls = K / NSB): entry j
+// (SB index j = row * NSB + sub-block) is the SB index of the QPP image of j's natural position (tc_interl_lte.c:88-106,
+// turbodecoder_win.h's inter / deinter).  Per (device, K), built once.
+std::map<std::pair<int, uint32_t>, const uint16_t*> g_qpp8;
+
+const uint16_t* qpp8_table(uint32_t K, uint32_t nsb, int idx)
+{
+  std::lock_guard<std::mutex> lk(g_mu);
+  const auto                  key = std::make_pair(cur_dev(), K);
+  auto                        it  = g_qpp8.find(key);
+  if (it != g_qpp8.end()) {
+    return it->second;
+  }
+  const uint64_t        f1 = kF1[idx], f2 = kF2[idx], Ls = K / nsb;
+  std::vector<uint16_t> h(K);
+  for (uint64_t j = 0; j < K; j++) {
+    const uint64_t n  = (j % nsb) * Ls + j / nsb;            // natural position of SB index j
+    const uint64_t fn = ((f2 * n % K) * n + f1 * n) % K;     // its QPP image
+    h[j]              = (uint16_t)((fn % Ls) * nsb + fn / Ls);  // back to the SB index
+  }
+  uint16_t* d = nullptr;
+  if (hipMalloc((void**)&d, K * sizeof(uint16_t)) != hipSuccess ||
+      hipMemcpy(d, h.data(), K * sizeof(uint16_t), hipMemcpyHostToDevice) != hipSuccess) {
+    hipFree(d);
+    return nullptr;
+  }
+  g_qpp8[key] = d;
+  return d;
+}
+
 }  // namespace
 
 namespace srsran_amd {
@@ -401,7 +431,10 @@ int tdec8_sch_enqueue(uint32_t      K,
   a.xpow_a     = xp->d[0];
   a.xpow_b     = xp->d[1];
   a.min_iters  = 2;  // SRSRAN_PDSCH_MIN_TDEC_ITERS (sch.c:35)
-  qpp_coeffs((uint32_t)idx, &a.f1, &a.f2);
+  a.qpp        = qpp8_table(K, nsb, idx);
+  if (!a.qpp) {
+    return SRSRAN_ERROR;
+  }
   Scratch8 beta(stream, tdec8bit_beta_bytes((int)nsb, K, ncb));
   a.beta = (uint2*)beta.p;
   if (!a.beta) {
@@ -1093,7 +1126,10 @@ int srsran_tdec_gpu_run_batch_8bit(uint32_t      long_cb,
     a.ncb       = nof_cb;
     a.n_end     = n_end;
     a.out       = d_output;
-    qpp_coeffs((uint32_t)idx, &a.f1, &a.f2);
+    a.qpp       = qpp8_table(long_cb, nsb8, idx);
+    if (!a.qpp) {
+      return SRSRAN_ERROR;
+    }
     Scratch8 beta(s, tdec8bit_beta_bytes((int)nsb8, long_cb, nof_cb));
     if (!beta.p) {
       return SRSRAN_ERROR;

@@ -234,6 +234,8 @@ def parse():
                    help="srsran_tdec_gpu_set_w8_max_k (-1: the library default)")
     p.add_argument("--w8-fused-max-k", type=int, default=-1,
                    help="srsran_tdec_gpu_set_w8_fused_max_k (-1: the library default)")
+    p.add_argument("--generic-single-min-cb", type=int, default=-1,
+                   help="srsran_tdec_gpu_set_generic_single_threshold (-1: the library default, the quad decoder)")
     p.add_argument("--cpu-worker", type=int, default=None, help=argparse.SUPPRESS)
     p.add_argument("--dry-run", action="store_true",
                    help="launch path only (no GPU): ranks, devices and shards on a gloo group, one line")
@@ -1708,6 +1710,8 @@ def main():
         tdec.load_library().srsran_tdec_gpu_set_w8_max_k(args.w8_max_k)
     if args.w8_fused_max_k >= 0:
         tdec.load_library().srsran_tdec_gpu_set_w8_fused_max_k(args.w8_fused_max_k)
+    if args.generic_single_min_cb >= 0:
+        tdec.load_library().srsran_tdec_gpu_set_generic_single_threshold(args.generic_single_min_cb)
     if args.workload in ("dlsch", "ulsch"):
         return run_dlsch(args, torch, dist, world, rank, device)
     if args.workload == "pusch":

@@ -1103,9 +1103,9 @@ def run_pdsch(args, torch, dist, world, rank, device, steps=None, warmup=None, c
     used = [torch.cuda.Event(), torch.cuda.Event()]
     n_h2d = max(steps, 20)
 
-    def h2d_loop(n):
+    def h2d_loop(n, h_src, bufs, stepf):
         with torch.cuda.stream(cs):
-            d_xs[0].copy_(h_x, non_blocking=True)
+            bufs[0].copy_(h_src, non_blocking=True)
         copied[0].record(cs)
         for i in range(n):
             b = i % 2
@@ -1117,28 +1117,48 @@ def run_pdsch(args, torch, dist, world, rank, device, steps=None, warmup=None, c
                     # bench_like 1.04 ms against bench_like_host_wait 0.81 ms a step, r03r)
                     used[nb].synchronize()
                 with torch.cuda.stream(cs):
-                    d_xs[nb].copy_(h_x, non_blocking=True)
+                    bufs[nb].copy_(h_src, non_blocking=True)
                 copied[nb].record(cs)
             ks.wait_event(copied[b])
-            step(d_xs[b].data_ptr(), ks)
+            stepf(bufs[b].data_ptr(), ks)
             used[b].record(ks)
 
-    # the copy alone first (the PCIe bound of the same bytes; also maps the pinned samples for the GPU)
-    for timed in (False, True):
+    def h2d_rates(h_src, bufs, stepf):
+        # the copy alone first (the PCIe bound of the same bytes; also maps the pinned samples for the GPU)
+        for timed in (False, True):
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            for _ in range(n_h2d if timed else 4):
+                with torch.cuda.stream(cs):
+                    bufs[1].copy_(h_src, non_blocking=True)
+            torch.cuda.synchronize()
+            c_s = (time.perf_counter() - t1) / n_h2d
+        h2d_loop(4, h_src, bufs, stepf)  # untimed: the first work on freshly created streams pays their queue set-up
         torch.cuda.synchronize()
         t1 = time.perf_counter()
-        for _ in range(n_h2d if timed else 4):
-            with torch.cuda.stream(cs):
-                d_xs[1].copy_(h_x, non_blocking=True)
+        h2d_loop(n_h2d, h_src, bufs, stepf)
         torch.cuda.synchronize()
-        copy_s = (time.perf_counter() - t1) / n_h2d
-    h2d_loop(4)  # untimed: the first work on freshly created streams pays their queue set-up
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    h2d_loop(n_h2d)
-    torch.cuda.synchronize()
-    h2d_s = (time.perf_counter() - t1) / n_h2d
+        return c_s, (time.perf_counter() - t1) / n_h2d
+
+    copy_s, h2d_s = h2d_rates(h_x, d_xs, step)
     del d_xs[1]
+    # the same with the radio's int16 I/Q samples (srsran_ue_dl_gpu_decode_batch_sc16: converted x scale in the OFDM
+    # load): half the bytes over PCIe.  The samples quantised to 14 bits of their peak.
+    sc16_scale = float(np.float32(np.abs(host.view(np.float32)).max() / (1 << 14)))
+    hq = np.empty(host.shape + (2,), np.int16)
+    hq[..., 0] = np.clip(np.rint(host.real / sc16_scale), -32768, 32767)
+    hq[..., 1] = np.clip(np.rint(host.imag / sc16_scale), -32768, 32767)
+    h_q = torch.from_numpy(hq).pin_memory()
+    d_qs = [torch.empty(hq.shape, dtype=torch.int16, device=device) for _ in range(2)]
+
+    def step16(x_ptr, on):
+        if ue.gpu_decode_batch_sc16(arr, x_ptr, sc16_scale, d_res.data_ptr(), d_avg.data_ptr(), 0.0,
+                                    on.cuda_stream) != 2 * nsf:
+            raise RuntimeError("srsran_ue_dl_gpu_decode_batch_sc16 failed")
+    d_res.fill_(7)
+    copy16_s, h2d16_s = h2d_rates(h_q, d_qs, step16)
+    ok16 = int((d_res.cpu().numpy() == 0).sum())
+    del d_qs
     # per-step spread of the timed configuration (the workers taking the steps in turn: events on each step's own
     # stream, intervals between consecutive completions; host phases per call), and of worker 0 alone
     spread = step_spread(step_workers, max(steps, 10), torch, stream, prof, stream_of=last_worker_stream)
@@ -1219,6 +1239,9 @@ def run_pdsch(args, torch, dist, world, rank, device, steps=None, warmup=None, c
             "subframes_per_s_h2d_inclusive": round(world * nsf / h2d_s, 1),
             "h2d_copy_only_subframes_per_s": round(world * nsf / copy_s, 1),
             "h2d_gbps": round(host.nbytes / copy_s / 1e9, 2),
+            "subframes_per_s_h2d_sc16_inclusive": round(world * nsf / h2d16_s, 1),
+            "h2d_sc16_copy_only_subframes_per_s": round(world * nsf / copy16_s, 1),
+            "sc16_tb_ok_fraction": round(ok16 / (2 * nsf), 4),
             "tb_ok_fraction": round(ok / (2 * nsf), 4),
             "avg_half_iterations": round(float(avg.mean()), 3),
             "cell_id": cell_id,
@@ -1930,6 +1953,8 @@ def main():
             "subframes_per_s": pd["config"]["subframes_per_s"],
             "subframes_per_s_h2d_inclusive": pd["config"]["subframes_per_s_h2d_inclusive"],
             "h2d_copy_only_subframes_per_s": pd["config"]["h2d_copy_only_subframes_per_s"],
+            "subframes_per_s_h2d_sc16_inclusive": pd["config"]["subframes_per_s_h2d_sc16_inclusive"],
+            "h2d_sc16_copy_only_subframes_per_s": pd["config"]["h2d_sc16_copy_only_subframes_per_s"],
             "mbps": pd["value"],
             "ms_per_step": pd["ms_per_step"],
             "steps": pd["steps"],

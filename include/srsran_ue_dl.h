@@ -266,6 +266,12 @@ int  srsran_ofdm_set_phase_compensation(srsran_ofdm_t* q, double center_freq_hz)
  * (0 = none).  Asynchronous on `stream`. */
 int srsran_ofdm_rx_gpu(srsran_ofdm_t* q, const cf_t* d_in, cf_t* d_out, uint32_t nof_rx, uint32_t nof_sf, float cfo,
                        void* stream);
+/* added: the same from the radio's int16 I/Q samples (d_in: [sf][rx][sf_sz][2] int16 on the device), each converted
+ * as the host would convert them, (float)i * scale and (float)q * scale, inside the transform's sample load: half
+ * the bytes of cf_t samples to move from a host buffer (the result equals srsran_ofdm_rx_gpu on the converted
+ * samples).  Asynchronous on `stream`. */
+int srsran_ofdm_rx_gpu_sc16(srsran_ofdm_t* q, const int16_t* d_in, float scale, cf_t* d_out, uint32_t nof_rx,
+                            uint32_t nof_sf, float cfo, void* stream);
 
 /* Modulator (ofdm.c:585-690): the receiver's options above (srsran_enb_dl's configuration: normalize = false, DC
  * subcarrier left empty, no frequency shift; no MBSFN subframes).  srsran_ofdm_tx_sf: cfg.in_buffer (one
@@ -462,6 +468,19 @@ int srsran_ue_dl_gpu_decode_batch(srsran_ue_dl_t*              q,
                                   int32_t*                     d_result,
                                   float*                       d_avg_noi,
                                   void*                        stream);
+/* added: the same batch from int16 I/Q samples (d_samples: [sf][rx][sf_len][2] int16 on the device, converted as
+ * (float)x * scale in the OFDM stage's sample load, srsran_ofdm_rx_gpu_sc16): for callers whose samples come from
+ * the radio as sc16 and cross PCIe at half the bytes. */
+int srsran_ue_dl_gpu_decode_batch_sc16(srsran_ue_dl_t*              q,
+                                       srsran_ue_dl_cfg_t*          cfg,
+                                       uint32_t                     nof_sf,
+                                       const srsran_ue_dl_gpu_sf_t* sfs,
+                                       const int16_t*               d_samples,
+                                       float                        scale,
+                                       float                        cfo,
+                                       int32_t*                     d_result,
+                                       float*                       d_avg_noi,
+                                       void*                        stream);
 
 /* ---------------- CFO correction (sync/cfo.h:41-63, cfo.c:96-107) ---------------- */
 typedef struct {

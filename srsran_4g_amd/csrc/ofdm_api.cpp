@@ -291,13 +291,15 @@ int configure(srsran_ofdm_t* q, uint32_t nof_prb, uint32_t symbol_sz)
 // shift: apply the frequency shift's samples product in the transform (srsran_ofdm_rx_gpu; the host calls apply it to
 // the input buffer first, as the reference does)
 int run(srsran_ofdm_t* q, const float2* d_in, float2* d_out, uint32_t nrx, uint32_t nsf, float cfo, hipStream_t s,
-        bool shift = true)
+        bool shift = true, const short2* d_in16 = nullptr, float scale = 1.0f)
 {
   OfdmGpu* g = (OfdmGpu*)q->gpu;
   OfdmArgs a = g->proto;
   if (a.mbsfn && a.nsymb != 6) {  // MBSFN layouts are extended-CP ones (see srsran_ofdm_rx_sf_ng)
     return SRSRAN_ERROR;
   }
+  a.in16     = d_in16;
+  a.in_scale = scale;
   a.in       = d_in;
   a.out      = d_out;
   a.nrx      = nrx;
@@ -536,6 +538,18 @@ int srsran_ofdm_rx_gpu(srsran_ofdm_t* q, const cf_t* d_in, cf_t* d_out, uint32_t
     return SRSRAN_SUCCESS;
   }
   return run(q, (const float2*)d_in, (float2*)d_out, nof_rx, nof_sf, cfo, (hipStream_t)stream);
+}
+
+int srsran_ofdm_rx_gpu_sc16(srsran_ofdm_t* q, const int16_t* d_in, float scale, cf_t* d_out, uint32_t nof_rx,
+                            uint32_t nof_sf, float cfo, void* stream)
+{
+  if (!q || !q->gpu || !d_in || !d_out || nof_rx == 0 || !std::isfinite(scale)) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  if (nof_sf == 0) {
+    return SRSRAN_SUCCESS;
+  }
+  return run(q, nullptr, (float2*)d_out, nof_rx, nof_sf, cfo, (hipStream_t)stream, true, (const short2*)d_in, scale);
 }
 
 // ---------------- cfo.c ----------------

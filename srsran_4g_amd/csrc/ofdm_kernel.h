@@ -31,6 +31,10 @@ struct OfdmArgs {
   // start at bin 0 (keep_dc, or a frequency shift), 0: the DC bin is skipped
   uint32_t      win;
   uint32_t      dc0;
+  // int16 I/Q input (srsran_ofdm_rx_gpu_sc16): when set, sample n is (in16[n].x, in16[n].y) x in_scale, the
+  // float product the host conversion of the radio's sc16 samples computes; `in` is then not read
+  const short2* in16;
+  float         in_scale;
   int           nstages;
   int           radix[OFDM_MAX_STAGES];
   uint32_t      ns_magic[OFDM_MAX_STAGES];  // ceil(2^32 / Ns) of every stage (j / Ns by __umulhi)

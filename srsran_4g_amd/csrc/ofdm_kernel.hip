@@ -273,7 +273,8 @@ __global__ __launch_bounds__(OFDM_THREADS) void ofdm_rx_kernel(OfdmArgs a)
   const uint32_t    N = NC ? NC : a.N, ns = a.nsymb, slot = sym / ns, i = sym % ns;
   const uint32_t    slot_sz = ns * N + a.cp0 + (ns - 1) * a.cp;
   const uint32_t    off = a.mbsfn && slot == 0 ? a.mbsfn_off[i] : slot * slot_sz + a.cp0 + i * (N + a.cp) - a.win;
-  const float2*     src     = a.in + ((size_t)sf * a.nrx + rx) * a.sf_len + off;
+  const size_t      s0      = ((size_t)sf * a.nrx + rx) * a.sf_len + off;
+  const float2*     src     = a.in + s0;
   {  // all of a thread's sample loads (and CFO factors) issued before the first use: one HBM round trip
     constexpr int U = OFDM_MAX_N / OFDM_THREADS;
     float2        x[U], c[U];
@@ -281,7 +282,12 @@ __global__ __launch_bounds__(OFDM_THREADS) void ofdm_rx_kernel(OfdmArgs a)
     for (int u = 0; u < U; u++) {
       const uint32_t n = threadIdx.x + u * OFDM_THREADS;
       if (n < N) {
-        x[u] = src[n];
+        if (a.in16) {
+          const short2 q = a.in16[s0 + n];
+          x[u]           = make_float2((float)q.x * a.in_scale, (float)q.y * a.in_scale);
+        } else {
+          x[u] = src[n];
+        }
         if (a.cfo_tab) {
           c[u] = a.cfo_tab[off + n];
         }
@@ -413,12 +419,22 @@ __global__ __launch_bounds__(64) void ofdm_rx_wave_kernel(OfdmArgs a)
   const uint32_t     ns = a.nsymb, slot = sym / ns, i = sym % ns;
   const uint32_t     slot_sz = ns * N + a.cp0 + (ns - 1) * a.cp;
   const uint32_t     off = a.mbsfn && slot == 0 ? a.mbsfn_off[i] : slot * slot_sz + a.cp0 + i * (N + a.cp) - a.win;
-  const float2*      src     = a.in + ((size_t)sf * a.nrx + rx) * a.sf_len + off;
+  const size_t       s0      = ((size_t)sf * a.nrx + rx) * a.sf_len + off;
+  const float2*      src     = a.in + s0;
   const float2*      tw      = a.tw;
   float2             v[M];
+  if (a.in16) {
+    const short2* q16 = a.in16 + s0;
 #pragma unroll
-  for (int m = 0; m < M; m++) {
-    v[m] = src[l + 64 * m];
+    for (int m = 0; m < M; m++) {
+      const short2 q = q16[l + 64 * m];
+      v[m]           = make_float2((float)q.x * a.in_scale, (float)q.y * a.in_scale);
+    }
+  } else {
+#pragma unroll
+    for (int m = 0; m < M; m++) {
+      v[m] = src[l + 64 * m];
+    }
   }
   if constexpr (CFO) {
     float2 c[M];

@@ -9,6 +9,8 @@
 // candidate of the search spaces in one launch.  The batch path takes the CFI from its caller.
 #include <hip/hip_runtime.h>
 
+#include <cmath>
+
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -359,17 +361,20 @@ int srsran_ue_dl_decode_pdsch(srsran_ue_dl_t*     q,
   return srsran_pdsch_decode(&q->pdsch, sf, pdsch_cfg, &q->chest_res, q->sf_symbols, data);
 }
 
-int srsran_ue_dl_gpu_decode_batch(srsran_ue_dl_t*              q,
-                                  srsran_ue_dl_cfg_t*          cfg,
-                                  uint32_t                     nof_sf,
-                                  const srsran_ue_dl_gpu_sf_t* sfs,
-                                  const cf_t*                  d_samples,
-                                  float                        cfo,
-                                  int32_t*                     d_result,
-                                  float*                       d_avg_noi,
-                                  void*                        stream)
+// the batch over cf_t samples (d16 null) or int16 I/Q ones converted x scale in the OFDM load
+static int decode_batch(srsran_ue_dl_t*              q,
+                        srsran_ue_dl_cfg_t*          cfg,
+                        uint32_t                     nof_sf,
+                        const srsran_ue_dl_gpu_sf_t* sfs,
+                        const cf_t*                  d_samples,
+                        const int16_t*               d16,
+                        float                        scale,
+                        float                        cfo,
+                        int32_t*                     d_result,
+                        float*                       d_avg_noi,
+                        void*                        stream)
 {
-  if (!q || !q->gpu || !cfg || (nof_sf && (!sfs || !d_samples || !d_result || !d_avg_noi))) {
+  if (!q || !q->gpu || !cfg || (nof_sf && (!sfs || (!d_samples && !d16) || !d_result || !d_avg_noi))) {
     return SRSRAN_ERROR_INVALID_INPUTS;
   }
   if (nof_sf == 0) {
@@ -468,7 +473,8 @@ int srsran_ue_dl_gpu_decode_batch(srsran_ue_dl_t*              q,
   }
   if (srsran_amd::stage_side_copy() || !one_limit) {  // in line: OFDM, estimator, then the PDSCH batch
     if (srsran_amd::handoff(g->ho, s) != hipSuccess ||
-        srsran_ofdm_rx_gpu(&q->fft[0], d_samples, (cf_t*)g->d_grid, (uint32_t)nrx, nof_sf, cfo, stream) ||
+        (d16 ? srsran_ofdm_rx_gpu_sc16(&q->fft[0], d16, scale, (cf_t*)g->d_grid, (uint32_t)nrx, nof_sf, cfo, stream)
+                : srsran_ofdm_rx_gpu(&q->fft[0], d_samples, (cf_t*)g->d_grid, (uint32_t)nrx, nof_sf, cfo, stream)) ||
         estimate(nullptr) != SRSRAN_SUCCESS) {
       return SRSRAN_ERROR;
     }
@@ -499,7 +505,8 @@ int srsran_ue_dl_gpu_decode_batch(srsran_ue_dl_t*              q,
     }
   }
   if (!copies_ok || srsran_amd::handoff(g->ho, s) != hipSuccess ||
-      srsran_ofdm_rx_gpu(&q->fft[0], d_samples, (cf_t*)g->d_grid, (uint32_t)nrx, nof_sf, cfo, stream) ||
+      (d16 ? srsran_ofdm_rx_gpu_sc16(&q->fft[0], d16, scale, (cf_t*)g->d_grid, (uint32_t)nrx, nof_sf, cfo, stream)
+                : srsran_ofdm_rx_gpu(&q->fft[0], d_samples, (cf_t*)g->d_grid, (uint32_t)nrx, nof_sf, cfo, stream)) ||
       estimate(&js) != SRSRAN_SUCCESS) {
     for (uint32_t i = 0; i < js.n; i++) {  // the fused ones did not run: their fences must come as well
       srsran_amd::stage_copy_job(js.job[i], s);
@@ -513,6 +520,39 @@ int srsran_ue_dl_gpu_decode_batch(srsran_ue_dl_t*              q,
     }
   }
   return ret;
+}
+
+int srsran_ue_dl_gpu_decode_batch(srsran_ue_dl_t*              q,
+                                  srsran_ue_dl_cfg_t*          cfg,
+                                  uint32_t                     nof_sf,
+                                  const srsran_ue_dl_gpu_sf_t* sfs,
+                                  const cf_t*                  d_samples,
+                                  float                        cfo,
+                                  int32_t*                     d_result,
+                                  float*                       d_avg_noi,
+                                  void*                        stream)
+{
+  if (nof_sf && !d_samples) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  return decode_batch(q, cfg, nof_sf, sfs, d_samples, nullptr, 1.0f, cfo, d_result, d_avg_noi, stream);
+}
+
+int srsran_ue_dl_gpu_decode_batch_sc16(srsran_ue_dl_t*              q,
+                                       srsran_ue_dl_cfg_t*          cfg,
+                                       uint32_t                     nof_sf,
+                                       const srsran_ue_dl_gpu_sf_t* sfs,
+                                       const int16_t*               d_samples,
+                                       float                        scale,
+                                       float                        cfo,
+                                       int32_t*                     d_result,
+                                       float*                       d_avg_noi,
+                                       void*                        stream)
+{
+  if ((nof_sf && !d_samples) || !std::isfinite(scale)) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  return decode_batch(q, cfg, nof_sf, sfs, nullptr, d_samples, scale, cfo, d_result, d_avg_noi, stream);
 }
 
 // ---------------- DCI blind search (ue_dl.c:386-689) ----------------

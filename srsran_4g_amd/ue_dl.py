@@ -150,6 +150,11 @@ def lib():
             "srsran_chest_dl_set_mbsfn_area_id": ([CH, ctypes.c_uint16], ctypes.c_int),
             "srsran_ue_dl_set_non_mbsfn_region": ([UE, ctypes.c_uint8], None),
             "srsran_ofdm_rx_gpu": ([ctypes.POINTER(srsran_ofdm_t), P, P, u32, u32, ctypes.c_float, P], ctypes.c_int),
+            "srsran_ofdm_rx_gpu_sc16": ([ctypes.POINTER(srsran_ofdm_t), P, ctypes.c_float, P, u32, u32, ctypes.c_float,
+                                         P], ctypes.c_int),
+            "srsran_ue_dl_gpu_decode_batch_sc16": ([UE, ctypes.POINTER(srsran_ue_dl_cfg_t), u32,
+                                                    ctypes.POINTER(srsran_ue_dl_gpu_sf_t), P, ctypes.c_float,
+                                                    ctypes.c_float, P, P, P], ctypes.c_int),
             "srsran_ofdm_tx_init_cfg": ([ctypes.POINTER(srsran_ofdm_t), ctypes.POINTER(srsran_ofdm_cfg_t)], ctypes.c_int),
             "srsran_ofdm_tx_sf": ([ctypes.POINTER(srsran_ofdm_t)], None),
             "srsran_ofdm_set_freq_shift": ([ctypes.POINTER(srsran_ofdm_t), ctypes.c_float], ctypes.c_int),
@@ -648,6 +653,12 @@ class UeDl:
         arr = sfs if isinstance(sfs, ctypes.Array) else self.batch_entries(sfs, self.tdd)
         return lib().srsran_ue_dl_gpu_decode_batch(ctypes.byref(self.q), ctypes.byref(self.cfg), len(arr), arr,
                                                    d_samples, cfo, d_result, d_avg, stream)
+
+    def gpu_decode_batch_sc16(self, sfs, d_samples, scale, d_result, d_avg, cfo=0.0, stream=None):
+        """srsran_ue_dl_gpu_decode_batch_sc16: d_samples int16 I/Q, converted x scale in the OFDM load"""
+        arr = sfs if isinstance(sfs, ctypes.Array) else self.batch_entries(sfs, self.tdd)
+        return lib().srsran_ue_dl_gpu_decode_batch_sc16(ctypes.byref(self.q), ctypes.byref(self.cfg), len(arr), arr,
+                                                        d_samples, scale, cfo, d_result, d_avg, stream)
 
     def last_llr(self, sf, tb):
         """srsran_pdsch_gpu_last_llr of the UE's PDSCH object after a batch: (device pointer, count)"""

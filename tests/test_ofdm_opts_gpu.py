@@ -162,3 +162,31 @@ def test_tx_options_match_oracle_and_round_trip(U, case):
         assert np.abs(back / scale - g).max() < 1e-4
     finally:
         rx.free()
+
+
+@pytest.mark.parametrize("nprb,cp,fs,cfo", [(100, 0, 0.0, 0.0), (75, 0, 0.0, 2e-5), (25, 1, 0.5, 0.0), (6, 0, 0.0, 0.0)])
+def test_rx_gpu_sc16_equals_float(U, nprb, cp, fs, cfo):
+    """srsran_ofdm_rx_gpu_sc16 on int16 I/Q == srsran_ofdm_rx_gpu on the host conversion (float)x * scale, bit for
+    bit, on the one-wave kernels (N = 2048, 1536) and the Stockham one, with a CFO or a frequency shift"""
+    import torch
+    rng = np.random.default_rng(nprb + cp)
+    rx = U.OfdmRx(nprb, cp=cp, freq_shift_f=fs)
+    try:
+        n = rx.q.sf_sz
+        q = rng.integers(-20000, 20000, (2, 2, n, 2), dtype=np.int16)  # [sf][rx][sample][I/Q]
+        scale = float(np.float32(1.0 / 32767.0))
+        xf = (q[..., 0].astype(np.float32) * np.float32(scale) + 1j * (q[..., 1].astype(np.float32) * np.float32(scale)))
+        d_f = torch.from_numpy(xf.astype(np.complex64).view(np.float32)).cuda()
+        d_q = torch.from_numpy(q).cuda()
+        nout = 2 * 2 * 2 * rx.q.nof_symbols * rx.q.nof_re
+        o_f = torch.zeros(2 * nout, dtype=torch.float32, device="cuda")
+        o_q = torch.zeros(2 * nout, dtype=torch.float32, device="cuda")
+        L = U.lib()
+        assert L.srsran_ofdm_rx_gpu(ctypes.byref(rx.q), d_f.data_ptr(), o_f.data_ptr(), 2, 2, cfo, None) == 0
+        assert L.srsran_ofdm_rx_gpu_sc16(ctypes.byref(rx.q), d_q.data_ptr(), scale, o_q.data_ptr(), 2, 2, cfo,
+                                         None) == 0
+        torch.cuda.synchronize()
+        assert torch.equal(o_f, o_q)
+        assert o_f.abs().max() > 0
+    finally:
+        rx.free()

@@ -606,3 +606,67 @@ def test_pdsch_fused_matches_two_kernel_path(U, SCH, ora, nports, mix, opts):
     assert np.array_equal(r0, r1) and np.array_equal(a0, a1) and np.array_equal(p0, p1)
     assert (r1[r1 != 7] == 0).all()  # every TB decodes at 25 dB
     ue.free()
+
+
+def _to_sc16(x, rng_bits=14):
+    """quantise complex samples to int16 I/Q with the scale a radio driver would report: |x| max -> 2^14"""
+    scale = np.float32(np.abs(np.concatenate([x.real, x.imag])).max() / (1 << rng_bits))
+    q = np.empty(x.shape + (2,), np.int16)
+    q[..., 0] = np.clip(np.rint(x.real / scale), -32768, 32767)
+    q[..., 1] = np.clip(np.rint(x.imag / scale), -32768, 32767)
+    return q, float(scale)
+
+
+@pytest.mark.parametrize("cfo", [0.0, 150.0 / 30.72e6])
+def test_ue_dl_batch_sc16_equals_float(U, SCH, ora, cfo):
+    """srsran_ue_dl_gpu_decode_batch_sc16 on int16 I/Q samples == srsran_ue_dl_gpu_decode_batch on the same samples
+    converted on the host as (float)x * scale: the same payloads, iteration counts and every LLR of every TB (the
+    conversion in the OFDM load computes the host's single float product)"""
+    rng = np.random.default_rng(31)
+    nsf = 3
+    samples, entries_f, entries_q, sbs, pls_all = [], [], [], [], []
+    d_pl = torch.zeros((2, nsf, 2, TBS // 8 + 64), dtype=torch.uint8, device="cuda")
+    for b in range(nsf):
+        pls, x, nre, _, _, _ = _case(ora, rng, tti=3 + b, cfo=cfo)
+        samples.append(x)
+        pls_all.append(pls)
+        for k, ent in enumerate((entries_f, entries_q)):
+            sb = [SCH.SoftbufferRx(nof_prb=100) for _ in range(2)]
+            sbs += sb
+            cfg = U.pdsch_cfg(100, nre, (TBS, TBS), (6, 6), softbuffers=sb)
+            ent.append((3 + b, 1, cfg, [d_pl[k, b, 0].data_ptr(), d_pl[k, b, 1].data_ptr()], [1, 1]))
+    q, scale = _to_sc16(np.stack(samples))
+    xf = (q[..., 0].astype(np.float32) * np.float32(scale) + 1j * (q[..., 1].astype(np.float32) * np.float32(scale)))
+    xf = xf.astype(np.complex64)
+    d_xf = torch.from_numpy(xf.view(np.float32)).cuda()
+    d_xq = torch.from_numpy(q).cuda()
+    out = []
+    for k in range(2):
+        ue = U.UeDl(U.cell(100, 2, 1), 2)
+        d_res = torch.full((2 * nsf,), 7, dtype=torch.int32, device="cuda")
+        d_avg = torch.zeros(2 * nsf, dtype=torch.float32, device="cuda")
+        if k == 0:
+            n = ue.gpu_decode_batch(entries_f, d_xf.data_ptr(), d_res.data_ptr(), d_avg.data_ptr(), -cfo, None)
+        else:
+            n = ue.gpu_decode_batch_sc16(entries_q, d_xq.data_ptr(), scale, d_res.data_ptr(), d_avg.data_ptr(), -cfo,
+                                         None)
+        assert n == 2 * nsf
+        torch.cuda.synchronize()
+        llrs = []
+        for b in range(nsf):
+            for t in range(2):
+                p, cnt = ue.last_llr(b, t)
+                h = torch.empty(cnt, dtype=torch.int16)
+                SCH._memcpy_d2h(h, p, 2 * cnt)
+                llrs.append(h.numpy().copy())
+        out.append((d_res.cpu().numpy(), d_avg.cpu().numpy(), llrs))
+        ue.free()
+    pl = d_pl.cpu().numpy()
+    assert (out[0][0] == 0).all() and np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])
+    for b in range(nsf):
+        for t in range(2):
+            assert np.array_equal(pl[0, b, t], pl[1, b, t])
+            assert np.array_equal(pl[1, b, t, : TBS // 8], pls_all[b][t])
+            assert np.array_equal(out[0][2][2 * b + t], out[1][2][2 * b + t])
+    for sb in sbs:
+        sb.free()

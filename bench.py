@@ -134,6 +134,35 @@ def timed_region(step, steps, warmup, world, dist, sync, device):
     return elapsed
 
 
+def timed_region_n(run_n, steps, warmup, world, dist, sync, device):
+    """timed_region for callers that run their steps themselves (run_n(n): n steps, e.g. several host threads each
+    taking n batches): the same warm-up, barriers, device syncs and max over ranks"""
+    import gc
+
+    import torch
+
+    run_n(warmup)
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    gc_was = gc.isenabled()
+    gc.disable()
+    t0 = time.perf_counter()
+    run_n(steps)
+    sync()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if gc_was:
+        gc.enable()
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
+
+
 def step_spread(step, n, torch, stream, host_phases=None, stream_of=None):
     """Per-step spread of `n` back-to-back steps (after the timed region, the same launch pattern): the
     GPU time between HIP events recorded after every step, the host time of every enqueue call, and -- when
@@ -217,6 +246,11 @@ def parse():
     p.add_argument("--nr-tbs", type=int, default=64, help="nrsch: transport blocks per step")
     p.add_argument("--nr-snr", type=float, default=12.0, help="nrsch: Es/N0 (dB) of the bits as +-1 before int8 LLRs")
     p.add_argument("--pdsch-probe", action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--pusch-workers", type=int, default=2,
+                   help="pusch: PUSCH objects on host threads of their own, each taking every timed step's batch "
+                        "(srsENB's PHY workers, enb.conf nof_phy_threads); a step = one batch on each.  Default 2: "
+                        "1 / 2 / 3 / 4 workers 253 k / 424 k / 282 k / 245 k UE-subframes/s (r06ao) -- each object "
+                        "keeps two streams, and beyond two workers they share the process's four hardware queues")
     p.add_argument("--pdsch-workers", type=int, default=3,
                    help="pdsch: UE DL objects, each on its own stream, taking the timed batches in turn (srsUE's PHY "
                         "workers, phy.nof_phy_threads, srsue/src/main.cc:313-314: default 3)")
@@ -662,46 +696,84 @@ def run_pusch(args, torch, dist, world, rank, device, steps=None, warmup=None, c
     nue = args.subframes
     host = np.stack([pool[b % args.pool][1] for b in range(nue)])
     d_grid = torch.from_numpy(np.ascontiguousarray(host).view(np.float32)).to(device)
-    ch = P.ChestUl(cell, dm)
-    pu = P.Pusch(cell)
-    sbs = [S.SoftbufferRx(nof_prb=100) for _ in range(nue)]
-    cfgs, sfs = [], []
-    for b in range(nue):
-        cfg = S.srsran_pusch_cfg_t()
-        cfg.rnti = rnti
-        g = cfg.grant
-        g.L_prb, g.nof_symb, g.nof_re = L, UL_NSYMB, L * 12 * UL_NSYMB
-        g.tb.mod, g.tb.tbs, g.tb.rv, g.tb.nof_bits, g.tb.enabled = S.MOD_FROM_QM[C3_QM], C3_TBS, 0, C3_BITS, True
-        cfg.enable_64qam = True
-        cfg.max_nof_iterations = args.iters
-        cfg.softbuffers.rx = ctypes.pointer(sbs[b].s)
-        sf = P.srsran_ul_sf_cfg_t()
-        sf.tti = pool[b % args.pool][0]
-        cfgs.append(cfg)
-        sfs.append(sf)
-    arr = (P.srsran_pusch_gpu_ue_t * nue)()
-    res = (P.srsran_pusch_res_t * nue)()
-    cres = (P.srsran_chest_ul_res_t * nue)()
-    datas = np.zeros((nue, C3_TBS // 8 + 64), np.uint8)
     per_grid = host[0].size * 8
-    for b in range(nue):
-        arr[b].chest = ctypes.pointer(ch.q)
-        arr[b].sf = ctypes.pointer(sfs[b])
-        arr[b].cfg = ctypes.pointer(cfgs[b])
-        arr[b].d_sf_symbols = d_grid.data_ptr() + b * per_grid
-        arr[b].new_data = 1
-        res[b].data = datas[b].ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+
+    def make_worker():
+        """one eNB PHY worker's objects: its PUSCH and UL estimator objects, soft buffers and batch entries (over
+        the shared, read-only device grids)"""
+        ch = P.ChestUl(cell, dm)
+        pu = P.Pusch(cell)
+        sbs = [S.SoftbufferRx(nof_prb=100) for _ in range(nue)]
+        cfgs, sfs = [], []
+        for b in range(nue):
+            cfg = S.srsran_pusch_cfg_t()
+            cfg.rnti = rnti
+            g = cfg.grant
+            g.L_prb, g.nof_symb, g.nof_re = L, UL_NSYMB, L * 12 * UL_NSYMB
+            g.tb.mod, g.tb.tbs, g.tb.rv, g.tb.nof_bits, g.tb.enabled = S.MOD_FROM_QM[C3_QM], C3_TBS, 0, C3_BITS, True
+            cfg.enable_64qam = True
+            cfg.max_nof_iterations = args.iters
+            cfg.softbuffers.rx = ctypes.pointer(sbs[b].s)
+            sf = P.srsran_ul_sf_cfg_t()
+            sf.tti = pool[b % args.pool][0]
+            cfgs.append(cfg)
+            sfs.append(sf)
+        arr = (P.srsran_pusch_gpu_ue_t * nue)()
+        res = (P.srsran_pusch_res_t * nue)()
+        cres = (P.srsran_chest_ul_res_t * nue)()
+        datas = np.zeros((nue, C3_TBS // 8 + 64), np.uint8)
+        for b in range(nue):
+            arr[b].chest = ctypes.pointer(ch.q)
+            arr[b].sf = ctypes.pointer(sfs[b])
+            arr[b].cfg = ctypes.pointer(cfgs[b])
+            arr[b].d_sf_symbols = d_grid.data_ptr() + b * per_grid
+            arr[b].new_data = 1
+            res[b].data = datas[b].ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+        return dict(ch=ch, pu=pu, sbs=sbs, cfgs=cfgs, sfs=sfs, arr=arr, res=res, cres=cres, datas=datas)
+
+    # srsENB decodes uplink subframes on several PHY workers at once (enb.conf nof_phy_threads, default 3): `nwork`
+    # host threads, each with its own objects, each taking `steps` batches -- one worker's host work (descriptors,
+    # UCI, the synchronous result copy) overlaps another's GPU work.  A step = one batch on every worker.
+    nwork = max(1, int(getattr(args, "pusch_workers", 1)))
+    workers = [make_worker() for _ in range(nwork)]
+    w0 = workers[0]
+    pu, arr, res, cres, datas = w0["pu"], w0["arr"], w0["res"], w0["cres"], w0["datas"]
     L_ = P.lib()
 
-    def step():  # new transmissions: new_data = 1 (the soft buffers are reset in the decode launch)
-        if L_.srsran_pusch_gpu_decode_batch(ctypes.byref(pu.q), nue, arr, cres, res) != 0:
+    def batch(w):  # new transmissions: new_data = 1 (the soft buffers are reset in the decode launch)
+        if L_.srsran_pusch_gpu_decode_batch(ctypes.byref(w["pu"].q), nue, w["arr"], w["cres"], w["res"]) != 0:
             raise RuntimeError("srsran_pusch_gpu_decode_batch failed")
 
-    elapsed = timed_region(step, steps, warmup, world, dist, torch.cuda.synchronize, device)
-    ok = np.array([bool(res[b].crc) and np.array_equal(datas[b][:C3_TBS // 8], pool[b % args.pool][2])
-                   for b in range(nue)])
-    avg = np.array([res[b].avg_iterations_block for b in range(nue)])
-    value = world * nue * C3_TBS * steps / elapsed / 1e6
+    def step():
+        batch(w0)
+
+    def run_n(n):
+        if nwork == 1:
+            for _ in range(n):
+                batch(w0)
+            return
+        import threading
+        errs = []
+
+        def loop(w):
+            try:
+                for _ in range(n):
+                    batch(w)
+            except Exception as e:  # surfaced on the main thread below
+                errs.append(e)
+        ths = [threading.Thread(target=loop, args=(w,)) for w in workers]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        if errs:
+            raise errs[0]
+
+    elapsed = timed_region_n(run_n, steps, warmup, world, dist, torch.cuda.synchronize, device)
+    ok = np.array([bool(w["res"][b].crc) and np.array_equal(w["datas"][b][:C3_TBS // 8], pool[b % args.pool][2])
+                   for w in workers for b in range(nue)])
+    avg = np.array([w["res"][b].avg_iterations_block for w in workers for b in range(nue)])
+    value = world * nwork * nue * C3_TBS * steps / elapsed / 1e6
 
     prof.enable(True)
     nrep = max(1, min(steps, 3))
@@ -740,12 +812,14 @@ def run_pusch(args, torch, dist, world, rank, device, steps=None, warmup=None, c
         "data": f"synthetic: {args.pool} distinct PUSCH subframes (3-tap frequency-selective channel, AWGN "
                 f"{args.snr} dB) tiled to the batch, HBM-resident grids",
         "config": {
-            "workload": f"pusch: {nue} UEs x (100 PRB, 64QAM, TBS {C3_TBS}, 12 SC-FDMA symbols, normal CP) per step, "
+            "workload": f"pusch: {nue} UEs x (100 PRB, 64QAM, TBS {C3_TBS}, 12 SC-FDMA symbols, normal CP) per batch, "
+                        f"{nwork} worker(s) a batch each per step, "
                         f"srsran_pusch_gpu_decode_batch, max {args.iters} half-its, CRC early stop, no UCI",
-            "ue_subframes_per_s": round(world * nue * steps / elapsed, 1),
+            "ue_subframes_per_s": round(world * nwork * nue * steps / elapsed, 1),
             "tb_ok_fraction": round(float(ok.mean()), 4),
             "avg_half_iterations": round(float(avg.mean()), 3),
             "parallelism": f"ue-sharded x{world}",
+            "batch_workers": nwork,
         },
         "roofline": {
             "bound": "hbm",
@@ -768,10 +842,11 @@ def run_pusch(args, torch, dist, world, rank, device, steps=None, warmup=None, c
         result["cpu_baseline"] = pusch_cpu_baseline(pool, cell_id, dm, rnti, args, cpu_seconds)
     elif rank == 0:
         result["cpu_baseline"] = None
-    for sb in sbs:
-        sb.free()
-    pu.free()
-    ch.free()
+    for w in workers:
+        for sb in w["sbs"]:
+            sb.free()
+        w["pu"].free()
+        w["ch"].free()
     if not emit:
         return result
     if world > 1:
@@ -1999,6 +2074,7 @@ def main():
             "ms_per_step": pu["ms_per_step"],
             "tb_ok_fraction": pu["config"]["tb_ok_fraction"],
             "front_end_roofline": pu["front_end_roofline"],
+            "batch_workers": pu["config"]["batch_workers"],
             "cpu_baseline": pu.get("cpu_baseline"),
         }
 

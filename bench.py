@@ -249,8 +249,8 @@ def parse():
     p.add_argument("--pusch-workers", type=int, default=2,
                    help="pusch: PUSCH objects on host threads of their own, each taking every timed step's batch "
                         "(srsENB's PHY workers, enb.conf nof_phy_threads); a step = one batch on each.  Default 2: "
-                        "1 / 2 / 3 / 4 workers 253 k / 424 k / 282 k / 245 k UE-subframes/s (r06ao) -- each object "
-                        "keeps two streams, and beyond two workers they share the process's four hardware queues")
+                        "1 / 2 / 3 / 4 workers 253 k / 424 k / 282 k / 245 k UE-subframes/s (r06ao; 3 workers with 8 "
+                        "hardware queues a process: 276 k, r06ap)")
     p.add_argument("--pdsch-workers", type=int, default=3,
                    help="pdsch: UE DL objects, each on its own stream, taking the timed batches in turn (srsUE's PHY "
                         "workers, phy.nof_phy_threads, srsue/src/main.cc:313-314: default 3)")

@@ -20,6 +20,7 @@ namespace srsran_amd {
 int         ulsch_decode_dev(srsran_sch_t* q, srsran_pusch_cfg_t* cfg, int16_t* d_q, const uint8_t* d_c, uint8_t* data,
                              srsran_uci_value_t* uci_data);
 hipStream_t sch_stream(srsran_sch_t* q);
+int         sch_own_queue(srsran_sch_t* q);
 }  // namespace srsran_amd
 
 using namespace srsran_amd;
@@ -624,6 +625,10 @@ int srsran_pusch_init_enb(srsran_pusch_t* q, uint32_t max_prb)
     return SRSRAN_ERROR;
   }
   q->gpu = new PuschGpu();
+  if (sch_own_queue(&q->ul_sch)) {  // one hardware queue per PUSCH object (= per PHY worker)
+    srsran_pusch_free(q);
+    return SRSRAN_ERROR;
+  }
   return SRSRAN_SUCCESS;
 }
 

@@ -249,11 +249,14 @@ def parse():
     p.add_argument("--pusch-workers", type=int, default=2,
                    help="pusch: PUSCH objects on host threads of their own, each taking every timed step's batch "
                         "(srsENB's PHY workers, enb.conf nof_phy_threads); a step = one batch on each.  Default 2: "
-                        "1 / 2 / 3 / 4 workers 253 k / 424 k / 282 k / 245 k UE-subframes/s (r06ao; 3 workers with 8 "
-                        "hardware queues a process: 276 k, r06ap)")
+                        "1 / 2 / 3 / 4 workers 253 k / 447 k / 425 k / 437 k UE-subframes/s (r06ao, r06au: the GPU is "
+                        "the bound from two)")
     p.add_argument("--pdsch-workers", type=int, default=3,
                    help="pdsch: UE DL objects, each on its own stream, taking the timed batches in turn (srsUE's PHY "
                         "workers, phy.nof_phy_threads, srsue/src/main.cc:313-314: default 3)")
+    p.add_argument("--worker-queues", choices=("own", "shared"), default="own",
+                   help="pdsch: the workers' streams from srsran_gpu_worker_stream_create, a hardware queue each "
+                        "(own), or ordinary streams on HIP's shared hardware queues (shared)")
     p.add_argument("--pdsch-steps", type=int, default=20,
                    help="all188: timed steps of the C3 PDSCH chain reported in the same line (0 = skip)")
     p.add_argument("--pdsch-cpu-seconds", type=float, default=4.0, help="all188: CPU baseline budget of the PDSCH part")
@@ -1130,7 +1133,17 @@ def run_pdsch(args, torch, dist, world, rank, device, steps=None, warmup=None, c
     # several PHY workers at once): one batch's front end can run beside the previous one's decoder tail.  Worker 0
     # is the object above; the secondary measurements below (PCIe, spread, stages, host) use it alone.
     nwork = max(1, int(getattr(args, "pdsch_workers", 1)))
-    workers = [(ue, arr, d_pl, d_res, d_avg, stream if nwork == 1 else torch.cuda.Stream(device))]
+    # the workers' streams: each on a hardware queue of its own (srsran_gpu_worker_stream_create) -- on HIP's shared
+    # queues two workers' batches can land on one queue and run one after the other, depending on the streams created
+    # and freed before (tools/r06aw_pdsch_queues.py: 402-431 k shared, 441-442 k own)
+    own_streams = []
+
+    def worker_stream():
+        if getattr(args, "worker_queues", "own") == "shared":
+            return torch.cuda.Stream(device)
+        own_streams.append(U.WorkerStream(device))
+        return own_streams[-1].stream
+    workers = [(ue, arr, d_pl, d_res, d_avg, stream if nwork == 1 else worker_stream())]
     extra_sbs = []
     for _ in range(1, nwork):
         ue_w = U.UeDl(U.cell(100, 2, cell_id), 2)
@@ -1144,7 +1157,7 @@ def run_pdsch(args, torch, dist, world, rank, device, steps=None, warmup=None, c
         avg_w = torch.zeros(2 * nsf, dtype=torch.float32, device=device)
         arr_w = U.UeDl.batch_entries([(pool[b % 10][0], 1, cfgs_w[b], [pl_w[b, 0].data_ptr(), pl_w[b, 1].data_ptr()],
                                        [1, 1]) for b in range(nsf)])
-        workers.append((ue_w, arr_w, pl_w, res_w, avg_w, torch.cuda.Stream(device), cfgs_w))
+        workers.append((ue_w, arr_w, pl_w, res_w, avg_w, worker_stream(), cfgs_w))
     turn = [0]
 
     def step_workers():
@@ -1322,6 +1335,7 @@ def run_pdsch(args, torch, dist, world, rank, device, steps=None, warmup=None, c
             "cell_id": cell_id,
             "parallelism": f"carrier-per-gpu x{world}",
             "batch_workers": nwork,
+            "worker_queues": getattr(args, "worker_queues", "own") if nwork > 1 else None,
         },
         "roofline": {
             "bound": "hbm",
@@ -1358,6 +1372,8 @@ def run_pdsch(args, torch, dist, world, rank, device, steps=None, warmup=None, c
         for pair in sbs_w:
             for s_ in pair:
                 s_.free()
+    for ws in own_streams:
+        ws.free()
     if not emit:
         return result
     if world > 1:

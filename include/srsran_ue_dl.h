@@ -481,6 +481,13 @@ int srsran_ue_dl_gpu_decode_batch_sc16(srsran_ue_dl_t*              q,
                                        int32_t*                     d_result,
                                        float*                       d_avg_noi,
                                        void*                        stream);
+/* added: a stream for one PHY worker's batches (srsUE / srsENB decode subframes on several workers at once,
+ * srsue/src/main.cc:313-314): a HIP stream on a hardware queue of its own, so that two workers' batches are not
+ * queued one behind the other on one of the runtime's shared hardware queues (which streams share a queue depends
+ * on every stream created and freed before).  Blocking with respect to the legacy NULL stream.  *stream is a
+ * hipStream_t; free it with srsran_gpu_worker_stream_free.  (srsran_pusch_init_enb gives each PUSCH object one.) */
+int  srsran_gpu_worker_stream_create(void** stream);
+void srsran_gpu_worker_stream_free(void* stream);
 
 /* ---------------- CFO correction (sync/cfo.h:41-63, cfo.c:96-107) ---------------- */
 typedef struct {

@@ -1992,8 +1992,7 @@ bool rm_fwd_table(uint32_t cb_idx, uint32_t rv, const uint16_t** d_fwd, uint32_t
 
 hipStream_t sch_stream(srsran_sch_t* q) { return q && q->gpu ? ((SchCtx*)q->gpu)->stream : nullptr; }
 
-// The object's decode stream moved to a hardware queue of its own (a stream created with a CU mask -- here every
-// CU -- gets a new queue instead of sharing one of the runtime's GPU_MAX_HW_QUEUES).  srsENB runs one PUSCH object
+// The object's decode stream moved to a hardware queue of its own (own_queue_stream, stage_copy.h).  srsENB runs one PUSCH object
 // per PHY worker, several batches at once: two workers' streams that the runtime maps to one queue run their
 // batches one after the other (least-used queue assignment, which depends on the streams created and freed before:
 // 424 k UE-subframes/s with two workers standalone, 284 k after a PDSCH run in the same process, 422 k with this;
@@ -2008,14 +2007,11 @@ int sch_own_queue(srsran_sch_t* q)
   if (!x) {
     return SRSRAN_ERROR_INVALID_INPUTS;
   }
-  hipDeviceProp_t prop;
-  int             dev = 0;
-  if (!on || hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) {
+  if (!on) {
     return SRSRAN_SUCCESS;
   }
-  std::vector<uint32_t> mask((prop.multiProcessorCount + 31) / 32, ~0u);
-  hipStream_t           s = nullptr;
-  if (hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()) != hipSuccess) {
+  hipStream_t s = nullptr;
+  if (own_queue_stream(&s) != hipSuccess) {
     return SRSRAN_ERROR;
   }
   hipStreamSynchronize(x->stream);

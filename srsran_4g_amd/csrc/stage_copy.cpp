@@ -5,6 +5,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <vector>
 
 namespace srsran_amd {
 
@@ -135,6 +136,18 @@ hipError_t stage_copy_or_record(void* dst, const void* src_dev, size_t bytes, hi
     return hipSuccess;
   }
   return stage_copy_launch(dst, src_dev, bytes, stream, zero, zero_words, fence, slot, seq);
+}
+
+hipError_t own_queue_stream(hipStream_t* s)
+{
+  int             dev = 0;
+  hipDeviceProp_t prop;
+  hipError_t      e = hipGetDevice(&dev);
+  if (e != hipSuccess || (e = hipGetDeviceProperties(&prop, dev)) != hipSuccess) {
+    return e;
+  }
+  std::vector<uint32_t> mask((prop.multiProcessorCount + 31) / 32, ~0u);
+  return hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data());
 }
 
 bool stage_side_copy()

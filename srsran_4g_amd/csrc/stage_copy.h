@@ -57,6 +57,12 @@ inline hipError_t ring_event_create(hipEvent_t* e)
   return hipEventCreateWithFlags(e, hipEventDisableTiming | hipEventReleaseToDevice);
 }
 
+// A stream on a hardware queue of its own: HIP maps ordinary streams onto GPU_MAX_HW_QUEUES shared queues
+// (least-used first, so the mapping depends on every stream created and freed before); a stream created with a CU
+// mask -- here every CU -- gets a new queue.  For PHY workers whose batches must overlap.  Blocking with respect to
+// the legacy NULL stream (HIP creates CU-masked streams without hipStreamNonBlocking).
+hipError_t own_queue_stream(hipStream_t* s);
+
 // Stream hand-over of an object's device state: a batch on stream s after batches on another stream waits (on
 // the GPU) for everything queued on that stream so far.  No-op while the stream stays the same.
 struct StreamHandoff {

@@ -538,6 +538,28 @@ int srsran_ue_dl_gpu_decode_batch(srsran_ue_dl_t*              q,
   return decode_batch(q, cfg, nof_sf, sfs, d_samples, nullptr, 1.0f, cfo, d_result, d_avg_noi, stream);
 }
 
+int srsran_gpu_worker_stream_create(void** stream)
+{
+  if (!stream) {
+    return SRSRAN_ERROR_INVALID_INPUTS;
+  }
+  hipStream_t s = nullptr;
+  if (srsran_amd::own_queue_stream(&s) != hipSuccess) {
+    *stream = nullptr;
+    return SRSRAN_ERROR;
+  }
+  *stream = s;
+  return SRSRAN_SUCCESS;
+}
+
+void srsran_gpu_worker_stream_free(void* stream)
+{
+  if (stream) {
+    hipStreamSynchronize((hipStream_t)stream);
+    hipStreamDestroy((hipStream_t)stream);
+  }
+}
+
 int srsran_ue_dl_gpu_decode_batch_sc16(srsran_ue_dl_t*              q,
                                        srsran_ue_dl_cfg_t*          cfg,
                                        uint32_t                     nof_sf,

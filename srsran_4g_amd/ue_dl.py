@@ -113,6 +113,28 @@ class srsran_ue_dl_gpu_sf_t(ctypes.Structure):
 _bound = False
 
 
+class WorkerStream:
+    """srsran_gpu_worker_stream_create: a PHY worker's stream on a hardware queue of its own, as a torch stream
+    (`.stream`, an ExternalStream over it); free() releases it"""
+
+    def __init__(self, device):
+        import torch
+        p = ctypes.c_void_p()
+        if lib().srsran_gpu_worker_stream_create(ctypes.byref(p)) != 0 or not p.value:
+            raise RuntimeError("srsran_gpu_worker_stream_create failed")
+        self.ptr = p.value
+        self.stream = torch.cuda.ExternalStream(self.ptr, device=device)
+
+    @property
+    def cuda_stream(self):
+        return self.ptr
+
+    def free(self):
+        if self.ptr:
+            lib().srsran_gpu_worker_stream_free(self.ptr)
+            self.ptr = None
+
+
 def lib():
     global _bound
     L = load_library()
@@ -155,6 +177,8 @@ def lib():
             "srsran_ue_dl_gpu_decode_batch_sc16": ([UE, ctypes.POINTER(srsran_ue_dl_cfg_t), u32,
                                                     ctypes.POINTER(srsran_ue_dl_gpu_sf_t), P, ctypes.c_float,
                                                     ctypes.c_float, P, P, P], ctypes.c_int),
+            "srsran_gpu_worker_stream_create": ([ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
+            "srsran_gpu_worker_stream_free": ([P], None),
             "srsran_ofdm_tx_init_cfg": ([ctypes.POINTER(srsran_ofdm_t), ctypes.POINTER(srsran_ofdm_cfg_t)], ctypes.c_int),
             "srsran_ofdm_tx_sf": ([ctypes.POINTER(srsran_ofdm_t)], None),
             "srsran_ofdm_set_freq_shift": ([ctypes.POINTER(srsran_ofdm_t), ctypes.c_float], ctypes.c_int),

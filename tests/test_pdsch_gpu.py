@@ -670,3 +670,52 @@ def test_ue_dl_batch_sc16_equals_float(U, SCH, ora, cfo):
             assert np.array_equal(out[0][2][2 * b + t], out[1][2][2 * b + t])
     for sb in sbs:
         sb.free()
+
+
+@pytest.mark.gpu
+def test_ue_dl_batches_on_worker_streams(U, SCH, ora):
+    """srsran_gpu_worker_stream_create: two UE DL objects (two PHY workers) decode batches on streams with a hardware
+    queue each, enqueued back to back without a host wait between them: both decode every TB of the same subframes
+    like the oracle's payloads, with the same iteration counts"""
+    rng = np.random.default_rng(37)
+    nsf = 2
+    samples, pls_all, nres = [], [], []
+    for b in range(nsf):
+        pls, x, nre, _, _, _ = _case(ora, rng, tti=5 + b, cfo=0.0)
+        samples.append(x)
+        pls_all.append(pls)
+        nres.append(nre)
+    d_x = torch.from_numpy(np.ascontiguousarray(np.stack(samples)).view(np.float32)).cuda()
+    d_pl = torch.zeros((2, nsf, 2, TBS // 8 + 64), dtype=torch.uint8, device="cuda")
+    d_res = torch.full((2, 2 * nsf), 7, dtype=torch.int32, device="cuda")
+    d_avg = torch.zeros((2, 2 * nsf), dtype=torch.float32, device="cuda")
+    sbs, ues, streams = [], [], []
+    torch.cuda.synchronize()
+    for w in range(2):
+        ent = []
+        for b in range(nsf):
+            sb = [SCH.SoftbufferRx(nof_prb=100) for _ in range(2)]
+            sbs += sb
+            cfg = U.pdsch_cfg(100, nres[b], (TBS, TBS), (6, 6), softbuffers=sb)
+            ent.append((5 + b, 1, cfg, [d_pl[w, b, 0].data_ptr(), d_pl[w, b, 1].data_ptr()], [1, 1]))
+        ue = U.UeDl(U.cell(100, 2, 1), 2)
+        ws = U.WorkerStream(torch.device("cuda", 0))
+        assert ws.cuda_stream
+        ues.append(ue)
+        streams.append(ws)
+        assert ue.gpu_decode_batch(ent, d_x.data_ptr(), d_res[w].data_ptr(), d_avg[w].data_ptr(), 0.0,
+                                   ws.cuda_stream) == 2 * nsf
+    for ws in streams:
+        ws.stream.synchronize()
+    res, avg, pl = d_res.cpu().numpy(), d_avg.cpu().numpy(), d_pl.cpu().numpy()
+    assert (res == 0).all() and np.array_equal(avg[0], avg[1])
+    for w in range(2):
+        for b in range(nsf):
+            for t in range(2):
+                assert np.array_equal(pl[w, b, t, : TBS // 8], pls_all[b][t])
+    for ue in ues:
+        ue.free()
+    for ws in streams:
+        ws.free()
+    for sb in sbs:
+        sb.free()

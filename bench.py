@@ -251,9 +251,11 @@ def parse():
                         "(srsENB's PHY workers, enb.conf nof_phy_threads); a step = one batch on each.  Default 2: "
                         "1 / 2 / 3 / 4 workers 253 k / 447 k / 425 k / 437 k UE-subframes/s (r06ao, r06au: the GPU is "
                         "the bound from two)")
-    p.add_argument("--pdsch-workers", type=int, default=3,
+    p.add_argument("--pdsch-workers", type=int, default=4,
                    help="pdsch: UE DL objects, each on its own stream, taking the timed batches in turn (srsUE's PHY "
-                        "workers, phy.nof_phy_threads, srsue/src/main.cc:313-314: default 3)")
+                        "workers, phy.nof_phy_threads, srsue/src/main.cc:313-314: srsUE's default 3).  Default 4: with "
+                        "a hardware queue a worker, 439 k against 424 k subframes/s for 3 (r06bb, alternated in one "
+                        "process); 6 workers 415 k (r06ba)")
     p.add_argument("--worker-queues", choices=("own", "shared"), default="own",
                    help="pdsch: the workers' streams from srsran_gpu_worker_stream_create, a hardware queue each "
                         "(own), or ordinary streams on HIP's shared hardware queues (shared)")
